@@ -1,0 +1,342 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ``dfs_cli benchmark write`` + ``read`` (1 MiB x 100 files, concurrency
+10) on MI355X ChunkServers — the BASELINE.json metric.
+
+One rank per GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``):
+* every rank starts a ChunkServer process bound to its GPU (HBM chunk store + CDNA4
+  CRC kernels + RCCL replication rank r of N); rank 0 also starts the metadata master;
+* every rank runs the reference benchmark client against its local ChunkServer:
+  per step, 100 random 1 MiB files are written (CreateFile -> AllocateBlock ->
+  WriteBlock chain with RF = min(3, N) -> CompleteFile) and then read back in full;
+* W untimed warmup steps, then K timed steps bracketed by barrier + cuda synchronize;
+  the reported value is aggregate (write+read) MiB/s over all ranks / max rank time.
+
+Per-GPU work is fixed as N grows ("weak" scaling). Durability defaults to nvme-sync:
+every replica's data and .meta are fdatasync'ed before the ack, like the reference.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import signal
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "dfs_cli benchmark write+read MB/s & p50 lat, 1MB\u00d7100 conc=10, 1/2/4/8 GPUs"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--count", type=int, default=100)
+    p.add_argument("--size", type=int, default=1 << 20)
+    p.add_argument("--concurrency", type=int, default=10)
+    p.add_argument("--durability", choices=["nvme-sync", "hbm-ack"], default="nvme-sync")
+    p.add_argument("--hbm-capacity", default="32G")
+    p.add_argument("--transport", choices=["rccl", "grpc"], default="rccl")
+    p.add_argument("--cpu", action="store_true", help="CPU chunk store (plumbing config 1)")
+    p.add_argument("--workdir", default=None)
+    p.add_argument("--timeout", type=float, default=1500.0)
+    p.add_argument("--keep", action="store_true")
+    p.add_argument("--profile-dir", default=None,
+                   help="run each ChunkServer under rocprofv3 --kernel-trace --stats, output here")
+    return p.parse_args()
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class Procs:
+    def __init__(self):
+        self.items: list[subprocess.Popen] = []
+        self.logs: list[str] = []
+
+    def spawn(self, args: list[str], log: str, env: dict) -> subprocess.Popen:
+        return self.spawn_raw([sys.executable, "-m", *args], log, env)
+
+    def spawn_raw(self, cmd: list[str], log: str, env: dict) -> subprocess.Popen:
+        f = open(log, "ab")
+        p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, env=env,
+                             cwd=str(ROOT), start_new_session=True)
+        f.close()
+        self.items.append(p)
+        self.logs.append(log)
+        return p
+
+    def stop(self):
+        for p in self.items:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        deadline = time.time() + 30
+        for p in self.items:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+
+    def tails(self) -> str:
+        out = []
+        for log in self.logs:
+            try:
+                with open(log, errors="replace") as f:
+                    out.append(f"==> {log}\n" + "".join(f.readlines()[-30:]))
+            except OSError:
+                pass
+        return "\n".join(out)
+
+
+def wait_file(path: str, proc: subprocess.Popen, timeout: float, procs: Procs) -> dict:
+    deadline = time.time() + timeout
+    while not os.path.exists(path):
+        if proc.poll() is not None:
+            raise RuntimeError(f"process exited ({proc.returncode}) before ready:\n{procs.tails()}")
+        if time.time() > deadline:
+            raise TimeoutError(f"not ready after {timeout}s:\n{procs.tails()}")
+        time.sleep(0.05)
+    time.sleep(0.02)
+    with open(path) as f:
+        return json.load(f)
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != a.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
+    n = max(world, 1)
+
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+
+    def bcast(obj):
+        if world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    procs = Procs()
+    killed = threading.Event()
+
+    def watchdog():
+        if not killed.wait(a.timeout):
+            print(f"bench watchdog: exceeded {a.timeout}s, tearing down", file=sys.stderr, flush=True)
+            print(procs.tails(), file=sys.stderr, flush=True)
+            procs.stop()
+            os._exit(3)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+
+    base = bcast(a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=os.environ.get("TMPDIR", "/tmp")))
+    base_p = Path(base)
+    (base_p / f"rank{rank}").mkdir(parents=True, exist_ok=True)
+    env = dict(os.environ)
+    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+    env.setdefault("DFS_LOG", "warning")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE",
+              "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID"):
+        env.pop(k, None)
+    fs = []
+    result = None
+    try:
+        # ---------------- master (rank 0)
+        if rank == 0:
+            gport, hport = free_port(), free_port()
+            ready = str(base_p / "master.ready")
+            menv = dict(env, DFS_READY_FILE=ready)
+            mp = procs.spawn(["rust_hadoop_generated_by_llm_amd.master.server", "--addr", f"127.0.0.1:{gport}",
+                              "--http-port", str(hport), "--storage-dir", str(base_p / "master"), *fs],
+                             str(base_p / "master.log"), menv)
+            wait_file(ready, mp, 300, procs)
+            master = f"http://127.0.0.1:{gport}"
+        else:
+            master = None
+        master = bcast(master)
+        # ---------------- chunkserver for this rank's GPU
+        cport, chttp = free_port(), free_port()
+        ready = str(base_p / f"cs{rank}.ready")
+        gpu = -1 if a.cpu else local_rank
+        args = ["rust_hadoop_generated_by_llm_amd.chunkserver.server", "--addr", f"127.0.0.1:{cport}",
+                "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
+                "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
+                "--masters", master, "--heartbeat-interval", "0.5", "--scrub-interval", "3600", *fs]
+        if n > 1 and not a.cpu and a.transport == "rccl":
+            args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
+                     str(base_p / "rccl_rdv")]
+        else:
+            args += ["--replication-transport", "grpc"]
+        cs_env = dict(env, DFS_READY_FILE=ready)
+        if a.profile_dir:
+            # profile only the ChunkServer (where the kernels run); rocprofv3 is started
+            # before anything in this process touches the GPU
+            pdir = os.path.abspath(os.path.join(a.profile_dir, f"cs{rank}"))
+            os.makedirs(pdir, exist_ok=True)
+            cs_env["TMPDIR"] = "/tmp"
+            cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", pdir,
+                                  "-o", "cs", "--", sys.executable, "-m", *args],
+                                 str(base_p / f"cs{rank}.log"), cs_env)
+        else:
+            cp = procs.spawn(args, str(base_p / f"cs{rank}.log"), cs_env)
+        cs_info = wait_file(ready, cp, 600, procs)
+        my_cs = f"127.0.0.1:{cport}"
+
+        from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_read, bench_write, make_payloads
+        from rust_hadoop_generated_by_llm_amd.client.client import Client
+        from rust_hadoop_generated_by_llm_amd.models import proto as pb
+        from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
+
+        # wait until the master has registered every chunkserver and left safe mode
+        pool = ChannelPool()
+        deadline = time.time() + 300
+        while True:
+            try:
+                st = pool.call(master, "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(), timeout=2)
+                if st.chunk_server_count >= n and not st.is_safe_mode:
+                    break
+            except Exception:  # noqa: BLE001
+                pass
+            if time.time() > deadline:
+                raise TimeoutError("master never registered all chunkservers")
+            time.sleep(0.1)
+        barrier()
+
+        client = Client([master], local_chunkserver=my_cs)
+        payloads = make_payloads(a.count, a.size)
+        from concurrent.futures import ThreadPoolExecutor
+
+        tpool = ThreadPoolExecutor(max_workers=a.concurrency, thread_name_prefix="bench")
+
+        def step(tag: str):
+            ws, names = bench_write(client, a.count, a.size, a.concurrency, prefix=f"/bench_r{rank}",
+                                    payloads=payloads, run_id=tag, pool=tpool)
+            rs = bench_read(client, files=names, pool=tpool,
+                            verify={nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if tag == "w0"
+                            else None)
+            return ws, rs
+
+        for w in range(a.warmup):
+            step(f"w{w}")
+        use_cuda = torch.cuda.is_available() and not a.cpu
+        if use_cuda:
+            torch.cuda.set_device(local_rank)
+            torch.cuda.synchronize()
+        barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        wl, rl, wbytes, rbytes = [], [], 0, 0
+        wt = rt = 0.0
+        for s in range(a.steps):
+            ws, rs = step(f"s{s}")
+            wl += ws.latencies
+            rl += rs.latencies
+            wbytes += ws.count * ws.avg_size
+            rbytes += rs.count * rs.avg_size
+            wt += ws.total_s
+            rt += rs.total_s
+        if use_cuda:
+            torch.cuda.synchronize()
+        barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+
+        stats = {}
+        try:
+            import urllib.request
+
+            stats = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
+        except Exception:  # noqa: BLE001
+            pass
+        mine = {"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt, "rt": rt,
+                "cs": stats, "rccl": cs_info.get("rccl", False)}
+        if world > 1:
+            allr = [None] * world
+            dist.all_gather_object(allr, mine)
+        else:
+            allr = [mine]
+        if rank == 0:
+            import statistics
+
+            tmax = max(r["elapsed"] for r in allr)
+            tot = sum(r["wbytes"] + r["rbytes"] for r in allr)
+            wlat = sorted(x for r in allr for x in r["wl"])
+            rlat = sorted(x for r in allr for x in r["rl"])
+
+            def pct(v, p):
+                return 1e3 * v[min(len(v) - 1, len(v) * p // 100)] if v else 0.0
+
+            wbytes_all = sum(r["wbytes"] for r in allr)
+            rbytes_all = sum(r["rbytes"] for r in allr)
+            value = tot / (1 << 20) / tmax
+            result = {
+                "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": n, "steps": a.steps,
+                "warmup": a.warmup, "ms_per_step": round(1e3 * tmax / a.steps, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "uint8", "data": "synthetic random bytes",
+                "config": {"model": "dfs_cli benchmark write+read (1 MiB files)", "global_batch": a.count * n,
+                           "seq_len": a.size, "parallelism": f"cs{n}",
+                           "files_per_gpu_per_step": a.count, "file_size": a.size, "concurrency": a.concurrency,
+                           "replication_factor": min(3, n), "durability": a.durability,
+                           "store": "cpu" if a.cpu else "hbm", "transport": a.transport if n > 1 else "local"},
+                "write_mb_per_s": round(wbytes_all / (1 << 20) / max(r["wt"] for r in allr), 2),
+                "read_mb_per_s": round(rbytes_all / (1 << 20) / max(r["rt"] for r in allr), 2),
+                "write_p50_ms": round(pct(wlat, 50), 3), "write_p95_ms": round(pct(wlat, 95), 3),
+                "write_p99_ms": round(pct(wlat, 99), 3), "read_p50_ms": round(pct(rlat, 50), 3),
+                "read_p95_ms": round(pct(rlat, 95), 3), "read_p99_ms": round(pct(rlat, 99), 3),
+                "write_ops_per_s": round(len(wlat) / max(r["wt"] for r in allr), 1),
+                "rccl_ranks": sum(1 for r in allr if r["rccl"]),
+                "rccl_forwards": sum(r["cs"].get("rccl_forwards", 0) for r in allr),
+                "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
+                "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
+            }
+            _ = statistics
+            print(json.dumps(result), flush=True)
+        barrier()
+        tpool.shutdown(wait=False)
+        client.close()
+    finally:
+        killed.set()
+        procs.stop()
+        if world > 1:
+            try:
+                dist.destroy_process_group()
+            except Exception:  # noqa: BLE001
+                pass
+        if not a.keep and rank == 0:
+            shutil.rmtree(base, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

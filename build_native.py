@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Build the in-tree native extension `_dfs_native` for gfx950.
+
+Every source in csrc/ is compiled by hipcc (host C++ and HIP device code alike) with
+`--offload-arch=gfx950` and linked against the HIP runtime, RCCL and OpenSSL. The .so is
+written INSIDE the package so it travels with the repo snapshot to the GPU box.
+
+    python build_native.py            # incremental
+    python build_native.py --clean    # full rebuild
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "native"
+PKG = ROOT / "rust_hadoop_generated_by_llm_amd"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
+
+
+def ext_path() -> Path:
+    return PKG / ("_dfs_native" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _includes() -> list[str]:
+    import pybind11
+
+    return [f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+            f"-I{ROCM}/include"]
+
+
+def _newer(src: Path, obj: Path, headers: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+
+
+def build(clean: bool = False, verbose: bool = False) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    sources = sorted(list(CSRC.glob("*.cpp")) + list(CSRC.glob("*.hip")))
+    headers = sorted(CSRC.glob("*.h"))
+    flags = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", "-fvisibility=hidden",
+             f"--offload-arch={ARCH}", "-D__HIP_PLATFORM_AMD__"] + _includes()
+    jobs = []
+    objs = []
+    for src in sources:
+        obj = BUILD / (src.name + ".o")
+        objs.append(obj)
+        if clean or _newer(src, obj, headers):
+            lang = ["-x", "hip"] if src.suffix == ".hip" else []
+            jobs.append([HIPCC, *flags, *lang, "-c", str(src), "-o", str(obj)])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return cmd[-3]
+
+    workers = min(len(jobs), int(os.environ.get("MAX_JOBS", "8"))) or 1
+    with cf.ThreadPoolExecutor(workers) as ex:
+        for name in ex.map(run, jobs):
+            if verbose:
+                print("built", name, flush=True)
+    out = ext_path()
+    if clean or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
+        link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(out), *map(str, objs),
+                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lcrypto", "-lpthread",
+                f"-Wl,-rpath,{ROCM}/lib"]
+        r = subprocess.run(link, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    p = build(a.clean, a.verbose)
+    print(p)
+    sys.exit(0)

@@ -1,0 +1,349 @@
+// pybind11 module `_dfs_native`: the native data plane exposed to the service layer.
+// Every long-running call releases the GIL so gRPC worker threads run in parallel.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "chunk_store.h"
+#include "crc32.h"
+#include "crypto.h"
+#include "gf256.h"
+#include "rccl_engine.h"
+#include "wal.h"
+
+namespace py = pybind11;
+using namespace dfs;
+
+namespace {
+
+struct Buf {
+  const uint8_t* p;
+  size_t n;
+};
+
+Buf view(const py::buffer& b, py::buffer_info& keep) {
+  keep = b.request();
+  return Buf{static_cast<const uint8_t*>(keep.ptr), static_cast<size_t>(keep.size * keep.itemsize)};
+}
+
+py::bytes new_bytes(size_t n, char** data) {
+  PyObject* o = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(n));
+  if (!o) throw py::error_already_set();
+  *data = PyBytes_AS_STRING(o);
+  return py::reinterpret_steal<py::bytes>(o);
+}
+
+py::bytes meta_image(const std::vector<uint32_t>& v) {
+  char* d;
+  py::bytes out = new_bytes(v.size() * 4, &d);
+  for (size_t i = 0; i < v.size(); ++i) {
+    uint32_t be = __builtin_bswap32(v[i]);
+    std::memcpy(d + 4 * i, &be, 4);
+  }
+  return out;
+}
+
+gf::Matrix to_matrix(const std::vector<std::vector<int>>& m) {
+  gf::Matrix out;
+  for (auto& row : m) {
+    std::vector<uint8_t> r;
+    for (int v : row) r.push_back(static_cast<uint8_t>(v));
+    out.push_back(r);
+  }
+  return out;
+}
+
+std::vector<std::vector<int>> from_matrix(const gf::Matrix& m) {
+  std::vector<std::vector<int>> out;
+  for (auto& row : m) out.emplace_back(row.begin(), row.end());
+  return out;
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_dfs_native, m) {
+  m.doc() = "MI355X-native data plane: HBM chunk store, CDNA4 CRC/RS kernels, RCCL replication, WAL";
+
+  // ---------------- checksums
+  m.def("crc32", [](py::buffer b, uint32_t crc) {
+    py::buffer_info k;
+    Buf v = view(b, k);
+    py::gil_scoped_release r;
+    return crc32_update(crc, v.p, v.n);
+  }, py::arg("data"), py::arg("crc") = 0);
+  m.def("crc32_meta", [](py::buffer b) {
+    py::buffer_info k;
+    Buf v = view(b, k);
+    std::vector<uint32_t> s(num_slices(v.n));
+    {
+      py::gil_scoped_release r;
+      crc32_slices(v.p, v.n, s.data());
+    }
+    return meta_image(s);
+  }, "Per-512B-slice CRC32 as the big-endian .meta image");
+  m.def("crc32_combine", &crc32_combine);
+  m.def("crc32_from_meta", [](py::buffer meta, uint64_t n) {
+    py::buffer_info k;
+    Buf v = view(meta, k);
+    std::vector<uint32_t> s(v.n / 4);
+    for (size_t i = 0; i < s.size(); ++i) {
+      uint32_t be;
+      std::memcpy(&be, v.p + 4 * i, 4);
+      s[i] = __builtin_bswap32(be);
+    }
+    return crc32_from_slices(s.data(), n);
+  });
+  m.def("cpu_has_pclmul", &cpu_has_pclmul);
+  m.def("device_count", &device_count);
+
+  // ---------------- GF(2^8) / Reed-Solomon
+  m.def("rs_matrix", [](int k, int mm) { return from_matrix(gf::rs_matrix(k, mm)); });
+  m.def("rs_decode_rows", [](int k, int mm, std::vector<int> present, std::vector<int> wanted) {
+    return from_matrix(gf::rs_decode_rows(k, mm, present, wanted));
+  });
+  m.def("gf_mul", &gf::mul);
+  m.def("gf_matmul_cpu", [](std::vector<std::vector<int>> mat, std::vector<py::buffer> inputs, uint64_t len) {
+    gf::Matrix M = to_matrix(mat);
+    std::vector<py::buffer_info> keep(inputs.size());
+    std::vector<const uint8_t*> in;
+    for (size_t i = 0; i < inputs.size(); ++i) {
+      Buf v = view(inputs[i], keep[i]);
+      if (v.n < len) throw std::runtime_error("shard shorter than len");
+      in.push_back(v.p);
+    }
+    std::vector<py::bytes> outs;
+    std::vector<uint8_t*> out;
+    for (size_t r = 0; r < M.size(); ++r) {
+      char* d;
+      outs.push_back(new_bytes(len, &d));
+      out.push_back(reinterpret_cast<uint8_t*>(d));
+    }
+    {
+      py::gil_scoped_release rel;
+      gf::matmul_cpu(M, in.data(), out.data(), len);
+    }
+    return outs;
+  });
+
+  // ---------------- chunk store
+  py::class_<ChunkStore>(m, "ChunkStore")
+      .def(py::init([](std::string storage_dir, std::string cold_dir, int device, uint64_t hbm_capacity,
+                       int durability, int cache_blocks, int lanes, int spill_threads, bool sync_writes) {
+             StoreConfig c;
+             c.storage_dir = storage_dir;
+             c.cold_dir = cold_dir;
+             c.device = device;
+             c.hbm_capacity = hbm_capacity;
+             c.durability = static_cast<Durability>(durability);
+             c.cache_blocks = cache_blocks;
+             c.lanes = lanes;
+             c.spill_threads = spill_threads;
+             c.sync_writes = sync_writes;
+             py::gil_scoped_release r;
+             return new ChunkStore(c);
+           }),
+           py::arg("storage_dir"), py::arg("cold_dir") = "", py::arg("device") = -1, py::arg("hbm_capacity") = 0,
+           py::arg("durability") = 0, py::arg("cache_blocks") = 100, py::arg("lanes") = 8,
+           py::arg("spill_threads") = 4, py::arg("sync_writes") = true)
+      .def_property_readonly("gpu", &ChunkStore::gpu)
+      .def_property_readonly("device", [](ChunkStore& s) { return s.config().device; })
+      .def("write", [](ChunkStore& s, const std::string& id, py::buffer data, uint32_t expected) {
+        py::buffer_info k;
+        Buf v = view(data, k);
+        WriteResult w;
+        {
+          py::gil_scoped_release r;
+          w = s.write(id, v.p, v.n, expected);
+        }
+        return py::make_tuple(w.ok, w.actual_crc, w.error);
+      }, py::arg("block_id"), py::arg("data"), py::arg("expected_crc") = 0)
+      .def("read", [](ChunkStore& s, const std::string& id, uint64_t offset, uint64_t length) -> py::tuple {
+        ReadResult st;
+        {
+          py::gil_scoped_release r;
+          st = s.stat(id, offset, length);
+        }
+        if (st.status != ReadStatus::Ok)
+          return py::make_tuple(static_cast<int>(st.status), st.total_size, py::bytes(), false, (int64_t)-1, st.error);
+        char* d;
+        py::bytes out = new_bytes(st.bytes, &d);
+        ReadResult rr;
+        {
+          py::gil_scoped_release r;
+          rr = s.read_into(id, offset, st.bytes, reinterpret_cast<uint8_t*>(d));
+        }
+        if (rr.status == ReadStatus::NotFound || rr.status == ReadStatus::OutOfRange || rr.status == ReadStatus::IoError)
+          return py::make_tuple(static_cast<int>(rr.status), rr.total_size, py::bytes(), false, (int64_t)-1, rr.error);
+        return py::make_tuple(static_cast<int>(rr.status), rr.total_size, out, rr.partial_corrupt, rr.bad_slice,
+                              rr.error);
+      }, py::arg("block_id"), py::arg("offset") = 0, py::arg("length") = 0)
+      .def("exists", &ChunkStore::exists)
+      .def("size", &ChunkStore::block_size)
+      .def("crc", &ChunkStore::block_crc, py::call_guard<py::gil_scoped_release>())
+      .def("remove", &ChunkStore::remove, py::call_guard<py::gil_scoped_release>())
+      .def("move_to_cold", &ChunkStore::move_to_cold, py::call_guard<py::gil_scoped_release>())
+      .def("verify_on_disk", &ChunkStore::verify_on_disk, py::call_guard<py::gil_scoped_release>())
+      .def("meta", [](ChunkStore& s, const std::string& id) {
+        std::vector<uint32_t> v;
+        {
+          py::gil_scoped_release r;
+          v = s.meta(id);
+        }
+        return meta_image(v);
+      })
+      .def("scrub", &ChunkStore::scrub, py::call_guard<py::gil_scoped_release>())
+      .def("list_blocks", &ChunkStore::list_blocks)
+      .def("flush", &ChunkStore::flush, py::call_guard<py::gil_scoped_release>())
+      .def("drop_resident", &ChunkStore::drop_resident, py::call_guard<py::gil_scoped_release>())
+      .def("debug_corrupt", &ChunkStore::debug_corrupt, py::call_guard<py::gil_scoped_release>())
+      .def("stats", [](ChunkStore& s) {
+        StoreStats t = s.stats();
+        py::dict d;
+        d["blocks"] = t.blocks;
+        d["bytes"] = t.bytes;
+        d["hbm_capacity"] = t.hbm_capacity;
+        d["hbm_used"] = t.hbm_used;
+        d["hbm_resident_blocks"] = t.hbm_resident_blocks;
+        d["dirty_blocks"] = t.dirty_blocks;
+        d["spill_queue"] = t.spill_queue;
+        d["evictions"] = t.evictions;
+        d["promotions"] = t.promotions;
+        d["crc_mismatches"] = t.crc_mismatches;
+        d["gpu_kernel_launches"] = t.gpu_kernel_launches;
+        return d;
+      })
+      .def("gpu_crc", [](ChunkStore& s, py::buffer data) {
+        py::buffer_info k;
+        Buf v = view(data, k);
+        std::vector<uint32_t> sl;
+        uint32_t c;
+        {
+          py::gil_scoped_release r;
+          c = s.gpu_crc(v.p, v.n, &sl);
+        }
+        return py::make_tuple(c, meta_image(sl));
+      })
+      .def("gf_matmul", [](ChunkStore& s, std::vector<std::vector<int>> mat, std::vector<py::buffer> inputs,
+                           uint64_t len) -> py::object {
+        gf::Matrix M = to_matrix(mat);
+        std::vector<py::buffer_info> keep(inputs.size());
+        std::vector<const uint8_t*> in;
+        for (size_t i = 0; i < inputs.size(); ++i) {
+          Buf v = view(inputs[i], keep[i]);
+          if (v.n < len) throw std::runtime_error("shard shorter than len");
+          in.push_back(v.p);
+        }
+        std::vector<py::bytes> outs;
+        std::vector<uint8_t*> out;
+        for (size_t r = 0; r < M.size(); ++r) {
+          char* d;
+          outs.push_back(new_bytes(len, &d));
+          out.push_back(reinterpret_cast<uint8_t*>(d));
+        }
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = s.gf_matmul_gpu(M, in, out, len);
+        }
+        if (!ok) return py::none();
+        return py::cast(outs);
+      });
+
+  // ---------------- RCCL replication
+  py::class_<RcclEngine>(m, "RcclEngine")
+      .def(py::init<ChunkStore*, int, int, std::string, int>(), py::keep_alive<1, 2>(), py::arg("store"),
+           py::arg("rank"), py::arg("world"), py::arg("rendezvous_dir"), py::arg("timeout_ms") = 30000)
+      .def("init", [](RcclEngine& e) {
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = e.init(&err);
+        }
+        return py::make_tuple(ok, err);
+      })
+      .def_property_readonly("ready", &RcclEngine::ready)
+      .def_property_readonly("rank", &RcclEngine::rank)
+      .def_property_readonly("world", &RcclEngine::world)
+      .def("pair_ok", &RcclEngine::pair_ok)
+      .def("abort_pair", &RcclEngine::abort_pair, py::call_guard<py::gil_scoped_release>())
+      .def("send", [](RcclEngine& e, int peer, const std::string& id) {
+        std::string err;
+        uint64_t size = 0;
+        int64_t seq;
+        {
+          py::gil_scoped_release r;
+          seq = e.send(peer, id, &size, &err);
+        }
+        return py::make_tuple(seq, size, err);
+      })
+      .def("wait_send", [](RcclEngine& e, int peer, int64_t seq) {
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = e.wait_send(peer, seq, &err);
+        }
+        return py::make_tuple(ok, err);
+      })
+      .def("recv", [](RcclEngine& e, int src, int64_t seq, const std::string& id, uint64_t size, uint32_t crc) {
+        WriteResult w;
+        {
+          py::gil_scoped_release r;
+          w = e.recv(src, seq, id, size, crc);
+        }
+        return py::make_tuple(w.ok, w.actual_crc, w.error);
+      })
+      .def_property_readonly("bytes_sent", &RcclEngine::bytes_sent)
+      .def_property_readonly("bytes_recv", &RcclEngine::bytes_recv);
+
+  // ---------------- WAL
+  py::class_<Wal>(m, "Wal")
+      .def(py::init<std::string, bool>(), py::arg("path"), py::arg("sync") = true)
+      .def("replay", [](Wal& w) {
+        std::vector<std::string> v;
+        {
+          py::gil_scoped_release r;
+          v = w.replay();
+        }
+        py::list out;
+        for (auto& s : v) out.append(py::bytes(s));
+        return out;
+      })
+      .def("append", [](Wal& w, std::vector<std::string> recs) {
+        py::gil_scoped_release r;
+        w.append(recs);
+      })
+      .def("reset", [](Wal& w, std::vector<std::string> recs) {
+        py::gil_scoped_release r;
+        w.reset(recs);
+      })
+      .def_property_readonly("size_bytes", &Wal::size_bytes)
+      .def_property_readonly("syncs", &Wal::syncs);
+  m.def("atomic_write", [](std::string path, py::bytes data, bool sync) {
+    std::string d = data;
+    py::gil_scoped_release r;
+    atomic_write_file(path, d, sync);
+  }, py::arg("path"), py::arg("data"), py::arg("sync") = true);
+
+  // ---------------- crypto
+  m.def("aes256gcm_encrypt", [](py::bytes key, py::bytes nonce, py::bytes pt, py::bytes aad) {
+    std::string o = crypto::aes256gcm_encrypt(key, nonce, pt, aad);
+    return py::bytes(o);
+  }, py::arg("key"), py::arg("nonce"), py::arg("plaintext"), py::arg("aad") = py::bytes());
+  m.def("aes256gcm_decrypt", [](py::bytes key, py::bytes nonce, py::bytes ct, py::bytes aad) {
+    std::string o = crypto::aes256gcm_decrypt(key, nonce, ct, aad);
+    return py::bytes(o);
+  }, py::arg("key"), py::arg("nonce"), py::arg("ciphertext"), py::arg("aad") = py::bytes());
+  m.def("rsa_sha256_verify", [](py::bytes n, py::bytes e, py::bytes msg, py::bytes sig) {
+    return crypto::rsa_sha256_verify(n, e, msg, sig);
+  });
+  m.def("random_bytes", [](size_t n) { return py::bytes(crypto::random_bytes(n)); });
+}

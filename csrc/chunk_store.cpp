@@ -1,0 +1,1382 @@
+// ChunkStore implementation. See chunk_store.h for the design.
+#include "chunk_store.h"
+
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+#include "crc32.h"
+#include "gf256.h"
+
+namespace dfs {
+
+namespace {
+
+inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
+
+std::string errno_str(const std::string& what) { return what + ": " + std::strerror(errno); }
+
+#define HIP_OK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + \
+                                                   " at " #expr);                             \
+  } while (0)
+
+bool write_all(int fd, const uint8_t* p, uint64_t n, uint64_t off) {
+  while (n) {
+    ssize_t w = ::pwrite(fd, p, n, static_cast<off_t>(off));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += w;
+    n -= static_cast<uint64_t>(w);
+    off += static_cast<uint64_t>(w);
+  }
+  return true;
+}
+
+bool read_all(int fd, uint8_t* p, uint64_t n, uint64_t off) {
+  while (n) {
+    ssize_t r = ::pread(fd, p, n, static_cast<off_t>(off));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    if (r == 0) return false;
+    p += r;
+    n -= static_cast<uint64_t>(r);
+    off += static_cast<uint64_t>(r);
+  }
+  return true;
+}
+
+bool file_exists(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0;
+}
+
+int64_t file_size(const std::string& p) {
+  struct stat st;
+  if (::stat(p.c_str(), &st) != 0) return -1;
+  return st.st_size;
+}
+
+bool ends_with(const std::string& s, const std::string& suf) {
+  return s.size() >= suf.size() && s.compare(s.size() - suf.size(), suf.size(), suf) == 0;
+}
+
+void mkdirs(const std::string& path) {
+  std::string cur;
+  for (size_t i = 0; i < path.size(); ++i) {
+    cur.push_back(path[i]);
+    if (path[i] == '/' || i + 1 == path.size()) ::mkdir(cur.c_str(), 0755);
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- ExtentAllocator
+ExtentAllocator::ExtentAllocator(uint64_t capacity) : cap_(capacity) {
+  if (capacity) free_[0] = capacity;
+}
+
+int64_t ExtentAllocator::alloc(uint64_t bytes) {
+  if (bytes == 0) bytes = 256;
+  for (auto it = free_.begin(); it != free_.end(); ++it) {
+    if (it->second >= bytes) {
+      uint64_t off = it->first, len = it->second;
+      free_.erase(it);
+      if (len > bytes) free_[off + bytes] = len - bytes;
+      used_ += bytes;
+      return static_cast<int64_t>(off);
+    }
+  }
+  return -1;
+}
+
+void ExtentAllocator::free(uint64_t off, uint64_t bytes) {
+  if (bytes == 0) bytes = 256;
+  used_ -= bytes;
+  auto next = free_.lower_bound(off);
+  if (next != free_.begin()) {
+    auto prev = std::prev(next);
+    if (prev->first + prev->second == off) {
+      off = prev->first;
+      bytes += prev->second;
+      free_.erase(prev);
+    }
+  }
+  next = free_.lower_bound(off);
+  if (next != free_.end() && off + bytes == next->first) {
+    bytes += next->second;
+    free_.erase(next);
+  }
+  free_[off] = bytes;
+}
+
+uint64_t ExtentAllocator::largest_free() const {
+  uint64_t m = 0;
+  for (auto& kv : free_) m = std::max(m, kv.second);
+  return m;
+}
+
+// ---------------------------------------------------------------- ChunkStore
+ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
+  mkdirs(cfg_.storage_dir);
+  if (!cfg_.cold_dir.empty()) mkdirs(cfg_.cold_dir);
+  if (gpu()) {
+    HIP_OK(hipSetDevice(cfg_.device));
+    uint64_t cap = cfg_.hbm_capacity;
+    if (cap == 0) {
+      size_t fr = 0, tot = 0;
+      HIP_OK(hipMemGetInfo(&fr, &tot));
+      cap = std::min<uint64_t>(fr / 2, 64ull << 30);
+    }
+    cap = align_up(cap, 1 << 20);
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&arena_), cap));
+    alloc_ = ExtentAllocator(cap);
+    int nl = std::max(1, cfg_.lanes);
+    for (int i = 0; i < nl; ++i) {
+      auto l = std::make_unique<Lane>();
+      HIP_OK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
+      for (int b = 0; b < 2; ++b) {
+        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&l->pinned[b]), kChunk, hipHostMallocDefault));
+        HIP_OK(hipEventCreateWithFlags(&l->ev[b], hipEventDisableTiming));
+      }
+      HIP_OK(hipMalloc(reinterpret_cast<void**>(&l->dscratch), 2 * kMaxGridCrc * sizeof(uint32_t)));
+      ensure_hscratch(l.get(), 64 << 10);
+      free_lanes_.push_back(l.get());
+      lanes_.push_back(std::move(l));
+    }
+    dtables_ = upload_crc_tables(lanes_[0]->stream);
+    dgf_ = upload_gf_tables(lanes_[0]->stream);
+    if (!dtables_ || !dgf_) throw std::runtime_error("failed to upload GPU tables");
+    st_.hbm_capacity = cap;
+    if (cfg_.durability == Durability::HbmAck)
+      for (int i = 0; i < std::max(1, cfg_.spill_threads); ++i) spillers_.emplace_back([this] { spill_worker(); });
+  }
+  scan_dirs();
+}
+
+ChunkStore::~ChunkStore() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : spillers_) t.join();
+  if (gpu()) {
+    (void)hipSetDevice(cfg_.device);
+    for (auto& l : lanes_) {
+      (void)hipStreamSynchronize(l->stream);
+      for (int b = 0; b < 2; ++b) {
+        (void)hipHostFree(l->pinned[b]);
+        (void)hipEventDestroy(l->ev[b]);
+      }
+      (void)hipFree(l->dscratch);
+      if (l->hscratch) (void)hipHostFree(l->hscratch);
+      (void)hipStreamDestroy(l->stream);
+    }
+    if (arena_) (void)hipFree(arena_);
+    if (dtables_) (void)hipFree(dtables_);
+    if (dgf_) (void)hipFree(const_cast<uint8_t*>(dgf_));
+  }
+}
+
+std::string ChunkStore::data_path(const std::string& id, bool cold) const {
+  return (cold ? cfg_.cold_dir : cfg_.storage_dir) + "/" + id;
+}
+std::string ChunkStore::meta_path(const std::string& id, bool cold) const {
+  return data_path(id, cold) + ".meta";
+}
+
+void ChunkStore::scan_dirs() {
+  auto scan = [&](const std::string& dir, bool cold) {
+    if (dir.empty()) return;
+    DIR* d = ::opendir(dir.c_str());
+    if (!d) return;
+    while (dirent* e = ::readdir(d)) {
+      std::string name = e->d_name;
+      if (name == "." || name == ".." || ends_with(name, ".meta") || ends_with(name, ".tmp")) continue;
+      int64_t sz = file_size(dir + "/" + name);
+      if (sz < 0) continue;
+      Block& b = index_[name];
+      b.size = static_cast<uint64_t>(sz);
+      b.on_disk = true;
+      b.cold = cold;
+    }
+    ::closedir(d);
+  };
+  std::lock_guard<std::mutex> g(mu_);
+  scan(cfg_.storage_dir, false);
+  scan(cfg_.cold_dir, true);
+}
+
+uint64_t ChunkStore::alloc_bytes(uint64_t n) const {
+  return align_up(std::max<uint64_t>(n, 1), 256) + align_up(std::max<uint64_t>(num_slices(n) * 4, 4), 256);
+}
+
+void ChunkStore::touch_locked(const std::string& id, Block& b) {
+  if (b.in_lru) lru_.erase(b.lru);
+  lru_.push_front(id);
+  b.lru = lru_.begin();
+  b.in_lru = true;
+}
+
+void ChunkStore::lru_remove_locked(Block& b) {
+  if (b.in_lru) lru_.erase(b.lru);
+  b.in_lru = false;
+}
+
+void ChunkStore::free_extent_locked(Block& b) {
+  if (b.dev_off >= 0) {
+    alloc_.free(static_cast<uint64_t>(b.dev_off), b.dev_bytes);
+    b.dev_off = -1;
+    b.dev_bytes = 0;
+  }
+}
+
+int64_t ChunkStore::alloc_locked(std::unique_lock<std::mutex>& lk, uint64_t bytes) {
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+  for (;;) {
+    int64_t off = alloc_.alloc(bytes);
+    if (off >= 0) return off;
+    bool evicted = false, any_dirty = false;
+    for (auto it = lru_.rbegin(); it != lru_.rend(); ++it) {
+      Block& b = index_[*it];
+      if (b.dirty) any_dirty = true;
+      if (b.pins == 0 && !b.dirty && b.on_disk && b.dev_off >= 0) {
+        free_extent_locked(b);
+        lru_remove_locked(b);
+        ++st_.evictions;
+        evicted = true;
+        break;
+      }
+    }
+    if (evicted) continue;
+    if (std::chrono::steady_clock::now() > deadline) return -1;
+    if (!any_dirty && lru_.empty()) return -1;
+    cv_.wait_for(lk, std::chrono::milliseconds(50));
+  }
+}
+
+ChunkStore::Lane* ChunkStore::acquire_lane() {
+  std::unique_lock<std::mutex> lk(lane_mu_);
+  lane_cv_.wait(lk, [&] { return !free_lanes_.empty(); });
+  Lane* l = free_lanes_.back();
+  free_lanes_.pop_back();
+  return l;
+}
+
+void ChunkStore::release_lane(Lane* l) {
+  {
+    std::lock_guard<std::mutex> g(lane_mu_);
+    free_lanes_.push_back(l);
+  }
+  lane_cv_.notify_one();
+}
+
+void ChunkStore::ensure_hscratch(Lane* l, uint64_t bytes) {
+  bytes = align_up(bytes + 2 * kMaxGridCrc * sizeof(uint32_t), 4096);
+  if (l->hscratch_cap >= bytes) return;
+  if (l->hscratch) HIP_OK(hipHostFree(l->hscratch));
+  HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&l->hscratch), bytes, hipHostMallocDefault));
+  l->hscratch_cap = bytes;
+}
+
+// Enqueue the CRC kernel on the lane stream and the D2H of its partials into hscratch
+// (partials at [0, 2*kMaxGridCrc) u32). Returns the grid used (0 = nothing launched).
+namespace {
+struct CrcPlan {
+  CrcLaunch a{};
+  int grid = 0;
+};
+CrcPlan plan_crc(const uint8_t* d, uint64_t n, uint32_t* meta_out, const uint32_t* meta_expect, bool want_block,
+                 uint64_t byte_lo, uint64_t byte_hi) {
+  CrcPlan p;
+  CrcLaunch& a = p.a;
+  a.data = d;
+  a.n = n;
+  a.s_full = n / kSliceBytes;
+  a.tail_len = static_cast<uint32_t>(n % kSliceBytes);
+  a.full_init = crc_init_term(kSliceBytes);
+  a.tail_init = a.tail_len ? crc_init_term(a.tail_len) : 0;
+  a.meta_out = meta_out;
+  a.meta_expect = meta_expect;
+  if (n == 0) return p;
+  if (want_block) {
+    a.slice_lo = 0;
+    a.slice_hi = a.s_full;
+    a.vfront = (kSlicesPerTile - a.s_full % kSlicesPerTile) % kSlicesPerTile;
+    a.ntiles = (a.s_full + a.vfront) / kSlicesPerTile;
+    a.has_tail = a.tail_len ? 1 : 0;
+  } else {
+    uint64_t first = byte_lo / kSliceBytes;
+    uint64_t last = (byte_hi - 1) / kSliceBytes;
+    a.slice_lo = first;
+    a.slice_hi = std::min<uint64_t>(last + 1, a.s_full);
+    a.vfront = 0;
+    a.ntiles = a.slice_hi > a.slice_lo ? (a.slice_hi - a.slice_lo + kSlicesPerTile - 1) / kSlicesPerTile : 0;
+    if (a.slice_hi < a.slice_lo) a.slice_hi = a.slice_lo;
+    a.has_tail = (a.tail_len && last >= a.s_full) ? 1 : 0;
+  }
+  p.grid = crc_grid_for(a.ntiles, a.has_tail);
+  return p;
+}
+}  // namespace
+
+bool ChunkStore::run_crc(Lane* l, const uint8_t* dptr, uint64_t n, uint32_t* meta_out, const uint32_t* meta_expect,
+                         bool want_block, uint64_t byte_lo, uint64_t byte_hi, CrcOut* out, std::string* err) {
+  // Synchronous helper used by paths that do not need to overlap anything else.
+  CrcPlan p = plan_crc(dptr, n, meta_out, meta_expect, want_block, byte_lo, byte_hi);
+  if (p.grid == 0) {
+    out->block_crc = 0;
+    out->bad_slice = -1;
+    return true;
+  }
+  p.a.part_crc = want_block ? l->dscratch : nullptr;
+  p.a.part_bad = meta_expect ? l->dscratch + kMaxGridCrc : nullptr;
+  hipError_t e = launch_crc(p.a, dtables_, p.grid, l->stream);
+  launches_++;
+  if (e != hipSuccess) {
+    *err = std::string("crc kernel launch: ") + hipGetErrorString(e);
+    return false;
+  }
+  auto* hp = reinterpret_cast<uint32_t*>(l->hscratch);
+  uint64_t tail_meta_off = 2 * kMaxGridCrc;
+  HIP_OK(hipMemcpyAsync(hp, l->dscratch, 2 * kMaxGridCrc * sizeof(uint32_t), hipMemcpyDeviceToHost, l->stream));
+  if (want_block && p.a.has_tail && meta_out)
+    HIP_OK(hipMemcpyAsync(hp + tail_meta_off, meta_out + p.a.s_full, 4, hipMemcpyDeviceToHost, l->stream));
+  HIP_OK(hipStreamSynchronize(l->stream));
+  out->bad_slice = -1;
+  if (meta_expect) {
+    uint32_t bad = 0xFFFFFFFFu;
+    for (int g = 0; g < p.grid; ++g) bad = std::min(bad, hp[kMaxGridCrc + g]);
+    if (bad != 0xFFFFFFFFu) out->bad_slice = bad;
+  }
+  if (want_block) {
+    uint32_t r = 0;
+    for (int g = 0; g < p.grid; ++g) r ^= hp[g];
+    if (p.a.has_tail) {
+      uint32_t tail_crc = __builtin_bswap32(hp[tail_meta_off]);
+      r = crc_shift(r, p.a.tail_len) ^ (tail_crc ^ p.a.tail_init);
+    }
+    out->block_crc = r ^ crc_init_term(n);
+  }
+  return true;
+}
+
+bool ChunkStore::h2d_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n) {
+  int i = 0;
+  for (uint64_t off = 0; off < n; off += kChunk, i ^= 1) {
+    uint64_t len = std::min<uint64_t>(kChunk, n - off);
+    HIP_OK(hipEventSynchronize(l->ev[i]));
+    std::memcpy(l->pinned[i], src + off, len);
+    HIP_OK(hipMemcpyAsync(dst + off, l->pinned[i], len, hipMemcpyHostToDevice, l->stream));
+    HIP_OK(hipEventRecord(l->ev[i], l->stream));
+  }
+  return true;
+}
+
+bool ChunkStore::d2h_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n) {
+  uint64_t nch = (n + kChunk - 1) / kChunk;
+  auto issue = [&](uint64_t c) {
+    uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
+    HIP_OK(hipMemcpyAsync(l->pinned[c & 1], src + off, len, hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipEventRecord(l->ev[c & 1], l->stream));
+  };
+  if (nch) issue(0);
+  for (uint64_t c = 0; c < nch; ++c) {
+    if (c + 1 < nch) issue(c + 1);
+    HIP_OK(hipEventSynchronize(l->ev[c & 1]));
+    uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
+    std::memcpy(dst + off, l->pinned[c & 1], len);
+  }
+  return true;
+}
+
+bool ChunkStore::persist(const std::string& id, bool cold, const uint8_t* data, uint64_t n, const uint8_t* meta_be,
+                         uint64_t nslices, std::string* err) {
+  std::string dp = data_path(id, cold), mp = meta_path(id, cold);
+  int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) {
+    *err = errno_str("open " + dp);
+    return false;
+  }
+  bool ok = write_all(fd, data, n, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
+  if (!ok) *err = errno_str("write " + dp);
+  ::close(fd);
+  if (!ok) return false;
+  fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) {
+    *err = errno_str("open " + mp);
+    return false;
+  }
+  ok = write_all(fd, meta_be, nslices * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
+  if (!ok) *err = errno_str("write " + mp);
+  ::close(fd);
+  return ok;
+}
+
+// ---------------------------------------------------------------- write
+WriteResult ChunkStore::write(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
+  if (!gpu()) return write_host(id, data, n, expected_crc);
+  HIP_OK(hipSetDevice(cfg_.device));
+  WriteResult res;
+  DevExtent ext = reserve(n);
+  if (ext.off < 0) {
+    res.error = "HBM arena full";
+    return res;
+  }
+  Lane* l = acquire_lane();
+  uint64_t S = num_slices(n);
+  auto* dmeta = reinterpret_cast<uint32_t*>(ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
+  ensure_hscratch(l, S * 4 + 16);
+  uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+  std::string err;
+  h2d_chunked(l, ext.ptr, data, n);
+  CrcOut co;
+  bool ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err);
+  if (ok && S) {
+    HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+  }
+  if (!ok) {
+    release_lane(l);
+    release(ext);
+    res.error = err;
+    return res;
+  }
+  res.actual_crc = co.block_crc;
+  if (expected_crc != 0 && co.block_crc != expected_crc) {
+    release_lane(l);
+    release(ext);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      ++st_.crc_mismatches;
+    }
+    res.error = "Checksum mismatch: expected " + std::to_string(expected_crc) + ", actual " +
+                std::to_string(co.block_crc);
+    return res;
+  }
+  bool durable = cfg_.durability == Durability::NvmeSync;
+  if (durable && !persist(id, false, data, n, hmeta, S, &err)) {
+    release_lane(l);
+    release(ext);
+    res.error = err;
+    return res;
+  }
+  release_lane(l);
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end()) {
+      cv_.wait(lk, [&] { return it->second.pins == 0; });
+      free_extent_locked(it->second);
+      lru_remove_locked(it->second);
+      if (it->second.cold && durable) {  // new version lives in the hot dir
+        ::unlink(data_path(id, true).c_str());
+        ::unlink(meta_path(id, true).c_str());
+      }
+    }
+    Block& b = index_[id];
+    b = Block{};
+    b.size = n;
+    b.crc = co.block_crc;
+    b.crc_known = true;
+    b.on_disk = durable;
+    b.dirty = !durable;
+    b.dev_off = ext.off;
+    b.dev_bytes = ext.bytes;
+    touch_locked(id, b);
+    if (!durable) spill_q_.push_back(id);
+  }
+  cv_.notify_all();
+  res.ok = true;
+  return res;
+}
+
+WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
+  WriteResult res;
+  uint32_t actual = crc32(data, n);
+  res.actual_crc = actual;
+  if (expected_crc != 0 && actual != expected_crc) {
+    std::lock_guard<std::mutex> g(mu_);
+    ++st_.crc_mismatches;
+    res.error = "Checksum mismatch: expected " + std::to_string(expected_crc) + ", actual " + std::to_string(actual);
+    return res;
+  }
+  uint64_t S = num_slices(n);
+  std::vector<uint32_t> sl(S);
+  crc32_slices(data, n, sl.data());
+  for (auto& v : sl) v = __builtin_bswap32(v);
+  std::string err;
+  if (!persist(id, false, data, n, reinterpret_cast<const uint8_t*>(sl.data()), S, &err)) {
+    res.error = err;
+    return res;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end() && it->second.cold) {
+      ::unlink(data_path(id, true).c_str());
+      ::unlink(meta_path(id, true).c_str());
+    }
+    Block& b = index_[id];
+    lru_remove_locked(b);
+    b = Block{};
+    b.size = n;
+    b.crc = actual;
+    b.crc_known = true;
+    b.on_disk = true;
+  }
+  res.ok = true;
+  return res;
+}
+
+// ---------------------------------------------------------------- read
+ReadResult ChunkStore::stat(const std::string& id, uint64_t offset, uint64_t length) {
+  ReadResult r;
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = index_.find(id);
+  if (it == index_.end()) {
+    r.status = ReadStatus::NotFound;
+    r.error = "Block not found";
+    return r;
+  }
+  r.total_size = it->second.size;
+  uint64_t len = length == 0 ? (r.total_size > offset ? r.total_size - offset : 0) : length;
+  if (offset >= r.total_size) {
+    r.status = ReadStatus::OutOfRange;
+    r.error = "Offset " + std::to_string(offset) + " exceeds block size " + std::to_string(r.total_size);
+    return r;
+  }
+  r.bytes = std::min<uint64_t>(len, r.total_size - offset);
+  return r;
+}
+
+ReadResult ChunkStore::read_into(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out) {
+  if (!gpu()) return read_host(id, offset, bytes, out);
+  HIP_OK(hipSetDevice(cfg_.device));
+  ReadResult r;
+  uint64_t size = 0;
+  const uint8_t* d = pin_device(id, &size);
+  if (!d) {
+    r.status = ReadStatus::NotFound;
+    r.error = "Block not found";
+    return r;
+  }
+  r.total_size = size;
+  if (offset >= size || offset + bytes > size) {
+    unpin(id);
+    r.status = ReadStatus::OutOfRange;
+    r.error = "Offset " + std::to_string(offset) + " exceeds block size " + std::to_string(size);
+    return r;
+  }
+  auto* dmeta = reinterpret_cast<const uint32_t*>(d + align_up(std::max<uint64_t>(size, 1), 256));
+  Lane* l = acquire_lane();
+  std::string err;
+  CrcOut co;
+  CrcPlan p = plan_crc(d, size, nullptr, dmeta, false, offset, offset + bytes);
+  if (p.grid > 0) {
+    p.a.part_bad = l->dscratch + kMaxGridCrc;
+    hipError_t e = launch_crc(p.a, dtables_, p.grid, l->stream);
+    launches_++;
+    if (e != hipSuccess) err = hipGetErrorString(e);
+    HIP_OK(hipMemcpyAsync(l->hscratch, l->dscratch + kMaxGridCrc, p.grid * 4, hipMemcpyDeviceToHost, l->stream));
+  }
+  d2h_chunked(l, out, d + offset, bytes);  // overlaps with verification on the same stream order
+  HIP_OK(hipStreamSynchronize(l->stream));
+  uint32_t bad = 0xFFFFFFFFu;
+  for (int g = 0; g < p.grid; ++g) bad = std::min(bad, reinterpret_cast<uint32_t*>(l->hscratch)[g]);
+  release_lane(l);
+  unpin(id);
+  r.bytes = bytes;
+  if (!err.empty()) {
+    r.status = ReadStatus::IoError;
+    r.error = err;
+    return r;
+  }
+  if (bad != 0xFFFFFFFFu) {
+    std::lock_guard<std::mutex> g(mu_);
+    ++st_.crc_mismatches;
+    r.bad_slice = bad;
+    r.error = "Checksum mismatch at chunk " + std::to_string(bad);
+    if (offset == 0 && bytes == size) r.status = ReadStatus::Corrupt;
+    else r.partial_corrupt = true;
+  }
+  return r;
+}
+
+std::vector<uint32_t> ChunkStore::load_meta_file(const std::string& id, bool cold, bool* ok) {
+  std::vector<uint32_t> m;
+  *ok = false;
+  std::string mp = meta_path(id, cold);
+  int fd = ::open(mp.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return m;
+  struct stat st;
+  if (::fstat(fd, &st) == 0) {
+    m.resize(static_cast<size_t>(st.st_size) / 4);
+    if (read_all(fd, reinterpret_cast<uint8_t*>(m.data()), m.size() * 4, 0)) {
+      for (auto& v : m) v = __builtin_bswap32(v);
+      *ok = true;
+    }
+  }
+  ::close(fd);
+  return m;
+}
+
+ReadResult ChunkStore::read_host(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out) {
+  ReadResult r;
+  bool cold = false;
+  uint64_t size = 0;
+  bool full = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end()) {
+      r.status = ReadStatus::NotFound;
+      r.error = "Block not found";
+      return r;
+    }
+    Block& b = it->second;
+    size = b.size;
+    cold = b.cold;
+    r.total_size = size;
+    if (offset >= size || offset + bytes > size) {
+      r.status = ReadStatus::OutOfRange;
+      r.error = "Offset " + std::to_string(offset) + " exceeds block size " + std::to_string(size);
+      return r;
+    }
+    full = offset == 0 && bytes == size;
+    if (full && b.host) {  // LRU hit (reference: no re-verification on cache hit)
+      std::memcpy(out, b.host->data(), bytes);
+      touch_locked(id, b);
+      r.bytes = bytes;
+      return r;
+    }
+  }
+  std::string dp = data_path(id, cold);
+  int fd = ::open(dp.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    r.status = errno == ENOENT ? ReadStatus::NotFound : ReadStatus::IoError;
+    r.error = errno == ENOENT ? "Block not found" : errno_str("Failed to read block");
+    return r;
+  }
+  bool ok = read_all(fd, out, bytes, offset);
+  if (!ok) {
+    ::close(fd);
+    r.status = ReadStatus::IoError;
+    r.error = errno_str("Failed to read block");
+    return r;
+  }
+  r.bytes = bytes;
+  bool mok = false;
+  std::vector<uint32_t> meta = load_meta_file(id, cold, &mok);
+  if (!mok) {
+    ::close(fd);
+    r.error = "Checksum file missing";
+    if (full) r.status = ReadStatus::Corrupt;
+    else r.partial_corrupt = true;
+    return r;
+  }
+  if (full) {
+    std::vector<uint32_t> act(num_slices(size));
+    crc32_slices(out, size, act.data());
+    if (act.size() != meta.size()) {
+      r.status = ReadStatus::Corrupt;
+      r.error = "Checksum count mismatch";
+    } else {
+      for (size_t i = 0; i < act.size(); ++i)
+        if (act[i] != meta[i]) {
+          r.status = ReadStatus::Corrupt;
+          r.bad_slice = static_cast<int64_t>(i);
+          r.error = "Checksum mismatch at chunk " + std::to_string(i);
+          break;
+        }
+    }
+    if (r.status == ReadStatus::Ok) {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = index_.find(id);
+      if (it != index_.end()) {
+        it->second.host = std::make_shared<std::vector<uint8_t>>(out, out + bytes);
+        touch_locked(id, it->second);
+        while (static_cast<int>(lru_.size()) > std::max(0, cfg_.cache_blocks)) {
+          auto& victim = index_[lru_.back()];
+          victim.host.reset();
+          victim.in_lru = false;
+          lru_.pop_back();
+        }
+      }
+    } else {
+      std::lock_guard<std::mutex> g(mu_);
+      ++st_.crc_mismatches;
+    }
+  } else {
+    uint64_t first = offset / kSliceBytes, last = (offset + bytes - 1) / kSliceBytes;
+    std::vector<uint8_t> buf(kSliceBytes);
+    for (uint64_t s = first; s <= last && s < meta.size(); ++s) {
+      uint64_t so = s * kSliceBytes, sl = std::min<uint64_t>(kSliceBytes, size - so);
+      if (!read_all(fd, buf.data(), sl, so)) break;
+      if (crc32(buf.data(), sl) != meta[s]) {
+        r.partial_corrupt = true;
+        r.bad_slice = static_cast<int64_t>(s);
+        r.error = "Checksum mismatch at chunk " + std::to_string(s);
+        std::lock_guard<std::mutex> g(mu_);
+        ++st_.crc_mismatches;
+        break;
+      }
+    }
+  }
+  ::close(fd);
+  return r;
+}
+
+// ---------------------------------------------------------------- residency
+DevExtent ChunkStore::reserve(uint64_t n) {
+  DevExtent e;
+  if (!gpu()) return e;
+  uint64_t bytes = alloc_bytes(n);
+  std::unique_lock<std::mutex> lk(mu_);
+  e.off = alloc_locked(lk, bytes);
+  if (e.off >= 0) {
+    e.bytes = bytes;
+    e.ptr = arena_ + e.off;
+  }
+  return e;
+}
+
+void ChunkStore::release(const DevExtent& e) {
+  if (e.off < 0) return;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    alloc_.free(static_cast<uint64_t>(e.off), e.bytes);
+  }
+  cv_.notify_all();
+}
+
+bool ChunkStore::promote(const std::string& id, std::string* err) {
+  uint64_t size = 0;
+  bool cold = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end()) {
+      *err = "Block not found";
+      return false;
+    }
+    if (it->second.dev_off >= 0) return true;
+    if (!it->second.on_disk) {
+      *err = "block neither resident nor on disk";
+      return false;
+    }
+    size = it->second.size;
+    cold = it->second.cold;
+  }
+  bool mok = false;
+  std::vector<uint32_t> meta = load_meta_file(id, cold, &mok);
+  if (!mok) {
+    *err = "Checksum file missing";
+    return false;
+  }
+  uint64_t S = num_slices(size);
+  if (meta.size() != S) {
+    *err = "Checksum count mismatch";
+    return false;
+  }
+  DevExtent ext = reserve(size);
+  if (ext.off < 0) {
+    *err = "HBM arena full";
+    return false;
+  }
+  std::string dp = data_path(id, cold);
+  int fd = ::open(dp.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) {
+    release(ext);
+    *err = "Block not found";
+    return false;
+  }
+  Lane* l = acquire_lane();
+  bool ok = true;
+  int i = 0;
+  for (uint64_t off = 0; off < size; off += kChunk, i ^= 1) {
+    uint64_t len = std::min<uint64_t>(kChunk, size - off);
+    HIP_OK(hipEventSynchronize(l->ev[i]));
+    if (!read_all(fd, l->pinned[i], len, off)) {
+      ok = false;
+      break;
+    }
+    HIP_OK(hipMemcpyAsync(ext.ptr + off, l->pinned[i], len, hipMemcpyHostToDevice, l->stream));
+    HIP_OK(hipEventRecord(l->ev[i], l->stream));
+  }
+  ::close(fd);
+  ensure_hscratch(l, S * 4 + 16);
+  uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+  for (uint64_t s = 0; s < S; ++s) reinterpret_cast<uint32_t*>(hmeta)[s] = __builtin_bswap32(meta[s]);
+  if (S)
+    HIP_OK(hipMemcpyAsync(ext.ptr + align_up(std::max<uint64_t>(size, 1), 256), hmeta, S * 4,
+                          hipMemcpyHostToDevice, l->stream));
+  HIP_OK(hipStreamSynchronize(l->stream));
+  release_lane(l);
+  if (!ok) {
+    release(ext);
+    *err = errno_str("Failed to read block");
+    return false;
+  }
+  bool keep = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end() && it->second.dev_off < 0 && it->second.size == size) {
+      Block& b = it->second;
+      b.dev_off = ext.off;
+      b.dev_bytes = ext.bytes;
+      if (!b.crc_known) {
+        b.crc = crc32_from_slices(meta.data(), size);
+        b.crc_known = true;
+      }
+      touch_locked(id, b);
+      ++st_.promotions;
+      keep = true;
+    }
+  }
+  if (!keep) release(ext);
+  return true;
+}
+
+const uint8_t* ChunkStore::pin_device(const std::string& id, uint64_t* size) {
+  if (!gpu()) return nullptr;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = index_.find(id);
+      if (it == index_.end()) return nullptr;
+      Block& b = it->second;
+      if (b.dev_off >= 0) {
+        b.pins++;
+        touch_locked(id, b);
+        *size = b.size;
+        return arena_ + b.dev_off;
+      }
+    }
+    std::string err;
+    if (!promote(id, &err)) return nullptr;
+  }
+  return nullptr;
+}
+
+void ChunkStore::unpin(const std::string& id) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end() && it->second.pins > 0) it->second.pins--;
+  }
+  cv_.notify_all();
+}
+
+WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t expected_crc,
+                                      hipStream_t s) {
+  WriteResult res;
+  HIP_OK(hipSetDevice(cfg_.device));
+  if (s) HIP_OK(hipStreamSynchronize(s));
+  Lane* l = acquire_lane();
+  uint64_t S = num_slices(n);
+  auto* dmeta = reinterpret_cast<uint32_t*>(ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
+  ensure_hscratch(l, S * 4 + 16);
+  uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+  std::string err;
+  CrcOut co;
+  bool ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err);
+  if (ok && S) {
+    HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+  }
+  if (!ok) {
+    release_lane(l);
+    release(ext);
+    res.error = err;
+    return res;
+  }
+  res.actual_crc = co.block_crc;
+  if (expected_crc != 0 && co.block_crc != expected_crc) {
+    release_lane(l);
+    release(ext);
+    res.error = "Replication checksum mismatch: expected " + std::to_string(expected_crc) + ", actual " +
+                std::to_string(co.block_crc);
+    return res;
+  }
+  bool durable = cfg_.durability == Durability::NvmeSync;
+  if (durable) {
+    // Stream the block out of HBM chunk by chunk straight into the data file.
+    std::string dp = data_path(id, false);
+    int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    bool wok = fd >= 0;
+    uint64_t nch = (n + kChunk - 1) / kChunk;
+    for (uint64_t c = 0; wok && c < nch; ++c) {
+      uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
+      HIP_OK(hipMemcpyAsync(l->pinned[c & 1], ext.ptr + off, len, hipMemcpyDeviceToHost, l->stream));
+      HIP_OK(hipStreamSynchronize(l->stream));
+      wok = write_all(fd, l->pinned[c & 1], len, off);
+    }
+    if (wok && cfg_.sync_writes) wok = ::fdatasync(fd) == 0;
+    if (fd >= 0) ::close(fd);
+    if (wok) {
+      std::string mp = meta_path(id, false);
+      fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      wok = fd >= 0 && write_all(fd, hmeta, S * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
+      if (fd >= 0) ::close(fd);
+    }
+    if (!wok) {
+      release_lane(l);
+      release(ext);
+      res.error = errno_str("persist " + id);
+      return res;
+    }
+  }
+  release_lane(l);
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end()) {
+      cv_.wait(lk, [&] { return it->second.pins == 0; });
+      free_extent_locked(it->second);
+      lru_remove_locked(it->second);
+    }
+    Block& b = index_[id];
+    b = Block{};
+    b.size = n;
+    b.crc = co.block_crc;
+    b.crc_known = true;
+    b.on_disk = durable;
+    b.dirty = !durable;
+    b.dev_off = ext.off;
+    b.dev_bytes = ext.bytes;
+    touch_locked(id, b);
+    if (!durable) spill_q_.push_back(id);
+  }
+  cv_.notify_all();
+  res.ok = true;
+  return res;
+}
+
+void ChunkStore::spill_worker() {
+  (void)hipSetDevice(cfg_.device);
+  for (;;) {
+    std::string id;
+    uint64_t size = 0;
+    const uint8_t* d = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || !spill_q_.empty(); });
+      if (stop_ && spill_q_.empty()) return;
+      id = spill_q_.front();
+      spill_q_.pop_front();
+      auto it = index_.find(id);
+      if (it == index_.end() || !it->second.dirty || it->second.dev_off < 0) continue;
+      it->second.pins++;
+      size = it->second.size;
+      d = arena_ + it->second.dev_off;
+    }
+    Lane* l = acquire_lane();
+    uint64_t S = num_slices(size);
+    ensure_hscratch(l, S * 4 + 16);
+    uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+    bool ok = true;
+    std::string dp = data_path(id, false);
+    int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    ok = fd >= 0;
+    uint64_t nch = (size + kChunk - 1) / kChunk;
+    for (uint64_t c = 0; ok && c < nch; ++c) {
+      uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, size - off);
+      if (hipMemcpyAsync(l->pinned[c & 1], d + off, len, hipMemcpyDeviceToHost, l->stream) != hipSuccess ||
+          hipStreamSynchronize(l->stream) != hipSuccess) {
+        ok = false;
+        break;
+      }
+      ok = write_all(fd, l->pinned[c & 1], len, off);
+    }
+    if (ok && cfg_.sync_writes) ok = ::fdatasync(fd) == 0;
+    if (fd >= 0) ::close(fd);
+    if (ok && S) {
+      ok = hipMemcpyAsync(hmeta, d + align_up(std::max<uint64_t>(size, 1), 256), S * 4, hipMemcpyDeviceToHost,
+                          l->stream) == hipSuccess &&
+           hipStreamSynchronize(l->stream) == hipSuccess;
+    }
+    if (ok) {
+      std::string mp = meta_path(id, false);
+      fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      ok = fd >= 0 && write_all(fd, hmeta, S * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
+      if (fd >= 0) ::close(fd);
+    }
+    release_lane(l);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = index_.find(id);
+      if (it != index_.end()) {
+        it->second.pins--;
+        if (ok && it->second.size == size) {
+          it->second.dirty = false;
+          it->second.on_disk = true;
+        } else if (!ok) {
+          spill_q_.push_back(id);  // retry later
+        }
+      }
+    }
+    cv_.notify_all();
+  }
+}
+
+// ---------------------------------------------------------------- misc ops
+bool ChunkStore::exists(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  return index_.count(id) > 0;
+}
+
+int64_t ChunkStore::block_size(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = index_.find(id);
+  return it == index_.end() ? -1 : static_cast<int64_t>(it->second.size);
+}
+
+uint32_t ChunkStore::block_crc(const std::string& id) {
+  bool cold = false;
+  uint64_t size = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end()) return 0;
+    if (it->second.crc_known) return it->second.crc;
+    cold = it->second.cold;
+    size = it->second.size;
+  }
+  bool ok = false;
+  auto m = load_meta_file(id, cold, &ok);
+  if (!ok) return 0;
+  uint32_t c = crc32_from_slices(m.data(), size);
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = index_.find(id);
+  if (it != index_.end()) {
+    it->second.crc = c;
+    it->second.crc_known = true;
+  }
+  return c;
+}
+
+bool ChunkStore::remove(const std::string& id) {
+  bool cold = false;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end()) return false;
+    cv_.wait(lk, [&] { return it->second.pins == 0; });
+    cold = it->second.cold;
+    free_extent_locked(it->second);
+    lru_remove_locked(it->second);
+    index_.erase(it);
+  }
+  cv_.notify_all();
+  ::unlink(data_path(id, cold).c_str());
+  ::unlink(meta_path(id, cold).c_str());
+  return true;
+}
+
+bool ChunkStore::move_to_cold(const std::string& id) {
+  if (cfg_.cold_dir.empty()) return false;
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = index_.find(id);
+  if (it == index_.end() || it->second.cold) return false;
+  if (it->second.dirty) {
+    lk.unlock();
+    flush();
+    lk.lock();
+    it = index_.find(id);
+    if (it == index_.end()) return false;
+  }
+  if (::rename(data_path(id, false).c_str(), data_path(id, true).c_str()) != 0) return false;
+  if (::rename(meta_path(id, false).c_str(), meta_path(id, true).c_str()) != 0) return false;
+  it->second.cold = true;
+  // cold blocks leave the fast tier
+  if (it->second.pins == 0) {
+    free_extent_locked(it->second);
+    lru_remove_locked(it->second);
+    it->second.host.reset();
+  }
+  return true;
+}
+
+std::string ChunkStore::verify_on_disk(const std::string& id) {
+  bool cold = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end()) cold = it->second.cold;
+    else if (!cfg_.cold_dir.empty() && file_exists(data_path(id, true))) cold = true;
+  }
+  bool mok = false;
+  auto meta = load_meta_file(id, cold, &mok);
+  if (!mok) return "Checksum file missing";
+  std::string dp = data_path(id, cold);
+  int64_t sz = file_size(dp);
+  if (sz < 0) return "Block not found";
+  std::vector<uint8_t> data(static_cast<size_t>(sz));
+  int fd = ::open(dp.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return "Block not found";
+  bool ok = read_all(fd, data.data(), data.size(), 0);
+  ::close(fd);
+  if (!ok && sz > 0) return "read failed";
+  std::vector<uint32_t> act(num_slices(data.size()));
+  crc32_slices(data.data(), data.size(), act.data());
+  if (act.size() != meta.size()) return "Checksum count mismatch";
+  for (size_t i = 0; i < act.size(); ++i)
+    if (act[i] != meta[i]) return "Checksum mismatch at chunk " + std::to_string(i);
+  return "";
+}
+
+std::vector<uint32_t> ChunkStore::meta(const std::string& id) {
+  uint64_t size = 0;
+  bool cold = false;
+  int64_t off = -1;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end()) return {};
+    size = it->second.size;
+    cold = it->second.cold;
+    off = it->second.dev_off;
+    if (off >= 0) it->second.pins++;
+  }
+  if (off >= 0) {
+    HIP_OK(hipSetDevice(cfg_.device));
+    std::vector<uint32_t> m(num_slices(size));
+    if (!m.empty())
+      HIP_OK(hipMemcpy(m.data(), arena_ + off + align_up(std::max<uint64_t>(size, 1), 256), m.size() * 4,
+                       hipMemcpyDeviceToHost));
+    for (auto& v : m) v = __builtin_bswap32(v);
+    unpin(id);
+    return m;
+  }
+  bool ok = false;
+  return load_meta_file(id, cold, &ok);
+}
+
+std::vector<std::string> ChunkStore::scrub() {
+  std::vector<std::string> bad;
+  std::vector<std::string> resident, disk;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : index_) {
+      if (gpu() && kv.second.dev_off >= 0) {
+        kv.second.pins++;
+        resident.push_back(kv.first);
+      } else if (kv.second.on_disk) {
+        disk.push_back(kv.first);
+      }
+    }
+  }
+  if (!resident.empty()) {
+    HIP_OK(hipSetDevice(cfg_.device));
+    // One stream, one launch per block, one sync per batch: K1b batched verify.
+    constexpr size_t kBatch = 256;
+    uint32_t* dbad = nullptr;
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&dbad), kBatch * kMaxGridCrc * sizeof(uint32_t)));
+    std::vector<uint32_t> hbad(kBatch * kMaxGridCrc);
+    Lane* l = acquire_lane();
+    for (size_t base = 0; base < resident.size(); base += kBatch) {
+      size_t cnt = std::min(kBatch, resident.size() - base);
+      std::vector<int> grids(cnt, 0);
+      for (size_t j = 0; j < cnt; ++j) {
+        const std::string& id = resident[base + j];
+        uint64_t size;
+        const uint8_t* d;
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          Block& b = index_[id];
+          size = b.size;
+          d = arena_ + b.dev_off;
+        }
+        if (size == 0) continue;
+        auto* dmeta = reinterpret_cast<const uint32_t*>(d + align_up(size, 256));
+        CrcPlan p = plan_crc(d, size, nullptr, dmeta, false, 0, size);
+        p.a.part_bad = dbad + j * kMaxGridCrc;
+        grids[j] = p.grid;
+        HIP_OK(launch_crc(p.a, dtables_, p.grid, l->stream));
+        launches_++;
+      }
+      HIP_OK(hipMemcpyAsync(hbad.data(), dbad, cnt * kMaxGridCrc * sizeof(uint32_t), hipMemcpyDeviceToHost, l->stream));
+      HIP_OK(hipStreamSynchronize(l->stream));
+      for (size_t j = 0; j < cnt; ++j) {
+        uint32_t m = 0xFFFFFFFFu;
+        for (int g = 0; g < grids[j]; ++g) m = std::min(m, hbad[j * kMaxGridCrc + g]);
+        if (m != 0xFFFFFFFFu) bad.push_back(resident[base + j]);
+      }
+    }
+    release_lane(l);
+    (void)hipFree(dbad);
+    for (auto& id : resident) unpin(id);
+  }
+  for (auto& id : disk)
+    if (!verify_on_disk(id).empty()) bad.push_back(id);
+  // resident blocks are also checked against their NVMe copy when one exists
+  if (gpu())
+    for (auto& id : resident) {
+      bool on_disk;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = index_.find(id);
+        on_disk = it != index_.end() && it->second.on_disk && !it->second.dirty;
+      }
+      if (on_disk && std::find(bad.begin(), bad.end(), id) == bad.end() && !verify_on_disk(id).empty())
+        bad.push_back(id);
+    }
+  std::lock_guard<std::mutex> g(mu_);
+  st_.crc_mismatches += bad.size();
+  return bad;
+}
+
+std::vector<std::string> ChunkStore::list_blocks() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> v;
+  v.reserve(index_.size());
+  for (auto& kv : index_) v.push_back(kv.first);
+  return v;
+}
+
+StoreStats ChunkStore::stats() {
+  std::lock_guard<std::mutex> g(mu_);
+  StoreStats s = st_;
+  s.blocks = index_.size();
+  s.bytes = 0;
+  s.hbm_resident_blocks = 0;
+  s.dirty_blocks = 0;
+  for (auto& kv : index_) {
+    s.bytes += kv.second.size;
+    if (kv.second.dev_off >= 0) s.hbm_resident_blocks++;
+    if (kv.second.dirty) s.dirty_blocks++;
+  }
+  s.hbm_used = alloc_.used();
+  s.spill_queue = spill_q_.size();
+  s.gpu_kernel_launches = launches_.load();
+  return s;
+}
+
+void ChunkStore::flush() {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] {
+    if (stop_) return true;
+    for (auto& kv : index_)
+      if (kv.second.dirty) return false;
+    return true;
+  });
+}
+
+void ChunkStore::drop_resident() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& kv : index_) {
+    Block& b = kv.second;
+    if (b.pins == 0 && !b.dirty && b.on_disk) {
+      free_extent_locked(b);
+      lru_remove_locked(b);
+      b.host.reset();
+    }
+  }
+}
+
+bool ChunkStore::debug_corrupt(const std::string& id, uint64_t offset) {
+  bool cold = false;
+  int64_t off = -1;
+  uint64_t size = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end() || offset >= it->second.size) return false;
+    cold = it->second.cold;
+    off = it->second.dev_off;
+    size = it->second.size;
+    if (it->second.host) (*it->second.host)[offset] ^= 0xFF;
+  }
+  (void)size;
+  std::string dp = data_path(id, cold);
+  int fd = ::open(dp.c_str(), O_RDWR | O_CLOEXEC);
+  if (fd >= 0) {
+    uint8_t c = 0;
+    if (read_all(fd, &c, 1, offset)) {
+      c ^= 0xFF;
+      write_all(fd, &c, 1, offset);
+    }
+    ::close(fd);
+  }
+  if (off >= 0) {
+    HIP_OK(hipSetDevice(cfg_.device));
+    uint8_t c = 0;
+    HIP_OK(hipMemcpy(&c, arena_ + off + offset, 1, hipMemcpyDeviceToHost));
+    c ^= 0xFF;
+    HIP_OK(hipMemcpy(arena_ + off + offset, &c, 1, hipMemcpyHostToDevice));
+  }
+  return true;
+}
+
+bool ChunkStore::gf_matmul_gpu(const std::vector<std::vector<uint8_t>>& mat, const std::vector<const uint8_t*>& in,
+                               const std::vector<uint8_t*>& out, uint64_t len) {
+  if (!gpu()) return false;
+  int k = static_cast<int>(in.size()), rows = static_cast<int>(out.size());
+  if (k > kMaxShards || rows > kMaxShards || static_cast<int>(mat.size()) != rows) return false;
+  HIP_OK(hipSetDevice(cfg_.device));
+  uint64_t stride = align_up(std::max<uint64_t>(len, 16), 256);
+  DevExtent ext = reserve(stride * (k + rows));
+  if (ext.off < 0) return false;
+  Lane* l = acquire_lane();
+  GfLaunch a{};
+  a.k = k;
+  a.rows = rows;
+  a.len = len;
+  a.gf_tables = dgf_;
+  for (int c = 0; c < k; ++c) {
+    a.in[c] = ext.ptr + c * stride;
+    h2d_chunked(l, ext.ptr + c * stride, in[c], len);
+  }
+  for (int r = 0; r < rows; ++r) {
+    a.out[r] = ext.ptr + (k + r) * stride;
+    for (int c = 0; c < k; ++c) a.mat[r * k + c] = mat[r][c];
+  }
+  HIP_OK(launch_gf_matmul(a, l->stream));
+  launches_++;
+  for (int r = 0; r < rows; ++r) d2h_chunked(l, out[r], a.out[r], len);
+  HIP_OK(hipStreamSynchronize(l->stream));
+  release_lane(l);
+  release(ext);
+  return true;
+}
+
+uint32_t ChunkStore::gpu_crc(const uint8_t* data, uint64_t n, std::vector<uint32_t>* slices) {
+  if (!gpu()) throw std::runtime_error("gpu_crc: store has no GPU");
+  HIP_OK(hipSetDevice(cfg_.device));
+  DevExtent ext = reserve(n);
+  if (ext.off < 0) throw std::runtime_error("HBM arena full");
+  Lane* l = acquire_lane();
+  uint64_t S = num_slices(n);
+  auto* dmeta = reinterpret_cast<uint32_t*>(ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
+  h2d_chunked(l, ext.ptr, data, n);
+  CrcOut co;
+  std::string err;
+  bool ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err);
+  if (ok && slices) {
+    slices->resize(S);
+    if (S) HIP_OK(hipMemcpy(slices->data(), dmeta, S * 4, hipMemcpyDeviceToHost));
+    for (auto& v : *slices) v = __builtin_bswap32(v);
+  }
+  release_lane(l);
+  release(ext);
+  if (!ok) throw std::runtime_error(err);
+  return co.block_crc;
+}
+
+}  // namespace dfs

@@ -1,0 +1,223 @@
+// ChunkStore: the ChunkServer's block store (reference: dfs/chunkserver/src/chunkserver.rs
+// write_block_async/read_block_async/verify_block/verify_partial_read/move_block_to_cold,
+// :110-143,192-351). On-disk format is identical to the reference:
+//   <dir>/<block_id>        raw bytes
+//   <dir>/<block_id>.meta   big-endian CRC-32/IEEE per 512 B slice
+//
+// Two backends behind one API:
+//  * HBM mode (device >= 0): blocks live in a hipMalloc arena carved by an extent
+//    allocator (host-side index + LRU). Checksums are computed/verified by the CDNA4
+//    kernels in gpu_kernels.hip; persistence is either synchronous (nvme-sync: data and
+//    .meta fdatasync'ed before ack, like the reference) or asynchronous spill threads
+//    (hbm-ack: D2H into pinned buffers then pwrite/fdatasync). Non-dirty blocks are evicted
+//    LRU when the arena is full and re-promoted from NVMe on the next read.
+//  * Host mode (device < 0): reference semantics on the CPU (PCLMUL CRC, LRU of full
+//    blocks, BLOCK_CACHE_SIZE).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <list>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "gpu_kernels.h"
+
+namespace dfs {
+
+enum class Durability : int { NvmeSync = 0, HbmAck = 1 };
+
+struct StoreConfig {
+  std::string storage_dir = "/tmp/chunkserver_data";
+  std::string cold_dir;          // empty = no cold tier
+  int device = -1;               // < 0: host mode
+  uint64_t hbm_capacity = 0;     // 0: auto (half of free HBM, capped at 64 GiB)
+  Durability durability = Durability::NvmeSync;
+  int cache_blocks = 100;        // host-mode LRU (BLOCK_CACHE_SIZE)
+  int lanes = 8;                 // concurrent GPU stream contexts
+  int spill_threads = 4;
+  bool sync_writes = true;       // fdatasync data + .meta
+};
+
+struct WriteResult {
+  bool ok = false;
+  uint32_t actual_crc = 0;
+  std::string error;
+};
+
+enum class ReadStatus : int { Ok = 0, NotFound = 1, OutOfRange = 2, Corrupt = 3, IoError = 4 };
+
+struct ReadResult {
+  ReadStatus status = ReadStatus::Ok;
+  uint64_t total_size = 0;
+  uint64_t bytes = 0;
+  bool partial_corrupt = false;  // partial read whose touched slices failed verification
+  int64_t bad_slice = -1;
+  std::string error;
+};
+
+struct StoreStats {
+  uint64_t blocks = 0;
+  uint64_t bytes = 0;
+  uint64_t hbm_capacity = 0;
+  uint64_t hbm_used = 0;
+  uint64_t hbm_resident_blocks = 0;
+  uint64_t dirty_blocks = 0;
+  uint64_t spill_queue = 0;
+  uint64_t evictions = 0;
+  uint64_t promotions = 0;
+  uint64_t crc_mismatches = 0;
+  uint64_t gpu_kernel_launches = 0;
+};
+
+// First-fit extent allocator over [0, capacity) with coalescing.
+class ExtentAllocator {
+ public:
+  explicit ExtentAllocator(uint64_t capacity = 0);
+  int64_t alloc(uint64_t bytes);  // -1 when no fit
+  void free(uint64_t off, uint64_t bytes);
+  uint64_t used() const { return used_; }
+  uint64_t capacity() const { return cap_; }
+  uint64_t largest_free() const;
+
+ private:
+  uint64_t cap_, used_ = 0;
+  std::map<uint64_t, uint64_t> free_;  // off -> len
+};
+
+class ChunkStore;
+
+// A region of the arena owned by an in-flight operation (RCCL receive target).
+struct DevExtent {
+  int64_t off = -1;
+  uint64_t bytes = 0;
+  uint8_t* ptr = nullptr;
+};
+
+class ChunkStore {
+ public:
+  explicit ChunkStore(StoreConfig cfg);
+  ~ChunkStore();
+  ChunkStore(const ChunkStore&) = delete;
+
+  bool gpu() const { return cfg_.device >= 0; }
+  const StoreConfig& config() const { return cfg_; }
+
+  WriteResult write(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
+  // Resolves [offset, offset+length) against the block (length 0 = rest of block).
+  ReadResult stat(const std::string& id, uint64_t offset, uint64_t length);
+  ReadResult read_into(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out);
+  bool exists(const std::string& id);
+  int64_t block_size(const std::string& id);
+  uint32_t block_crc(const std::string& id);
+  bool remove(const std::string& id);
+  bool move_to_cold(const std::string& id);
+  // Reference verify_block against the on-disk .meta (CPU).
+  std::string verify_on_disk(const std::string& id);
+  std::vector<uint32_t> meta(const std::string& id);  // native-endian slice CRCs
+  // Batched scrub (GPU verify of resident blocks + CPU verify of the rest).
+  std::vector<std::string> scrub();
+  std::vector<std::string> list_blocks();
+  StoreStats stats();
+  void flush();          // wait until no dirty blocks remain
+  void drop_resident();  // evict every clean resident block (tests / memory pressure)
+  bool debug_corrupt(const std::string& id, uint64_t offset);  // flip a byte everywhere
+
+  // ---- replication engine hooks (RCCL receive / send) ----
+  DevExtent reserve(uint64_t n);
+  void release(const DevExtent& e);
+  WriteResult commit_device(const std::string& id, const DevExtent& e, uint64_t n, uint32_t expected_crc,
+                            hipStream_t s);
+  // Pin a resident block (promoting it if needed) and return its device pointer.
+  const uint8_t* pin_device(const std::string& id, uint64_t* size);
+  void unpin(const std::string& id);
+
+  // GPU-resident RS codec: shards are host buffers; returns false when no GPU.
+  bool gf_matmul_gpu(const std::vector<std::vector<uint8_t>>& mat, const std::vector<const uint8_t*>& in,
+                     const std::vector<uint8_t*>& out, uint64_t len);
+  // Device checksum of a host buffer (K1+K2) for benchmarks / tests.
+  uint32_t gpu_crc(const uint8_t* data, uint64_t n, std::vector<uint32_t>* slices);
+
+ private:
+  struct Block {
+    uint64_t size = 0;
+    uint32_t crc = 0;
+    bool crc_known = false;
+    bool cold = false;
+    bool on_disk = false;
+    bool dirty = false;
+    int64_t dev_off = -1;
+    uint64_t dev_bytes = 0;
+    int pins = 0;
+    bool doomed = false;  // removed while pinned: free on last unpin
+    std::list<std::string>::iterator lru;
+    bool in_lru = false;
+    std::shared_ptr<std::vector<uint8_t>> host;  // host-mode cache
+  };
+  struct Lane {
+    hipStream_t stream = nullptr;
+    uint8_t* pinned[2] = {nullptr, nullptr};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    uint32_t* dscratch = nullptr;  // device: part_crc[kMaxGridCrc], part_bad[kMaxGridCrc]
+    uint8_t* hscratch = nullptr;   // pinned: meta image + partials
+    uint64_t hscratch_cap = 0;
+  };
+  static constexpr uint64_t kChunk = 4ull << 20;
+
+  std::string data_path(const std::string& id, bool cold) const;
+  std::string meta_path(const std::string& id, bool cold) const;
+  void scan_dirs();
+  uint64_t alloc_bytes(uint64_t n) const;
+  int64_t alloc_locked(std::unique_lock<std::mutex>& lk, uint64_t bytes);
+  void free_extent_locked(Block& b);
+  void touch_locked(const std::string& id, Block& b);
+  void lru_remove_locked(Block& b);
+  Lane* acquire_lane();
+  void release_lane(Lane* l);
+  void ensure_hscratch(Lane* l, uint64_t bytes);
+  // Device pass: CRC (and meta write or verify) over [slice range] of a resident block.
+  struct CrcOut {
+    uint32_t block_crc = 0;
+    int64_t bad_slice = -1;
+  };
+  bool run_crc(Lane* l, const uint8_t* dptr, uint64_t n, uint32_t* meta_out, const uint32_t* meta_expect,
+               bool want_block, uint64_t byte_lo, uint64_t byte_hi, CrcOut* out, std::string* err);
+  bool h2d_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n);
+  bool d2h_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n);
+  bool promote(const std::string& id, std::string* err);  // load from NVMe into HBM
+  bool persist(const std::string& id, bool cold, const uint8_t* data, uint64_t n, const uint8_t* meta_be,
+               uint64_t nslices, std::string* err);
+  void spill_worker();
+  WriteResult write_host(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
+  ReadResult read_host(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out);
+  std::vector<uint32_t> load_meta_file(const std::string& id, bool cold, bool* ok);
+
+  StoreConfig cfg_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::unordered_map<std::string, Block> index_;
+  std::list<std::string> lru_;  // front = most recent
+  ExtentAllocator alloc_;
+  uint8_t* arena_ = nullptr;
+  DevCrcTables* dtables_ = nullptr;
+  const uint8_t* dgf_ = nullptr;
+  std::vector<std::unique_ptr<Lane>> lanes_;
+  std::vector<Lane*> free_lanes_;
+  std::mutex lane_mu_;
+  std::condition_variable lane_cv_;
+  std::deque<std::string> spill_q_;
+  std::vector<std::thread> spillers_;
+  bool stop_ = false;
+  StoreStats st_;
+  std::atomic<uint64_t> launches_{0};
+};
+
+}  // namespace dfs

@@ -1,0 +1,20 @@
+// OpenSSL-backed primitives for the S3 gateway: AES-256-GCM (SSE-S3 envelope and STS
+// session tokens; reference dfs/common/src/auth/sse.rs, sts.rs) and RS256 signature
+// verification for OIDC JWTs (reference auth/oidc.rs). SigV4 HMAC/SHA-256 and MD5 ETags
+// use Python's hashlib/hmac, which are the same OpenSSL routines.
+#pragma once
+#include <string>
+
+namespace dfs::crypto {
+
+// Returns ciphertext || 16-byte tag.
+std::string aes256gcm_encrypt(const std::string& key, const std::string& nonce, const std::string& plaintext,
+                              const std::string& aad);
+// Throws std::runtime_error on authentication failure.
+std::string aes256gcm_decrypt(const std::string& key, const std::string& nonce, const std::string& ct_and_tag,
+                              const std::string& aad);
+// n, e: big-endian unsigned integers (JWK "n", "e" after base64url decoding).
+bool rsa_sha256_verify(const std::string& n, const std::string& e, const std::string& msg, const std::string& sig);
+std::string random_bytes(size_t n);
+
+}  // namespace dfs::crypto

@@ -1,0 +1,64 @@
+// CDNA4 (gfx950) kernels for the chunk data path.
+//   K1/K2  crc_slices_kernel  : per-512B-slice CRC32 (big-endian .meta image) fused with the
+//                               whole-block CRC (shift-combine tree, per-workgroup partials).
+//   K3     same kernel in range/verify mode: recompute only touched slices and compare with
+//          the HBM-resident .meta image (reference verify_partial_read, chunkserver.rs:296-351).
+//   K1b    batched scrub: same kernel, verify mode over every resident block.
+//   K4/K5  gf256_matmul_kernel: GF(2^8) matrix x shards (Reed-Solomon encode / reconstruct;
+//          reference erasure.rs:7-49).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dfs {
+
+constexpr int kCrcWgThreads = 256;
+constexpr int kSlicesPerTile = 32;  // 4 waves x 8 slices x 512 B = 16 KiB per tile
+constexpr int kMaxGridCrc = 1024;
+constexpr int kMaxShards = 32;
+
+struct DevCrcTables {
+  uint32_t slice16[16][256];
+  uint32_t sh64[4][256], sh128[4][256], sh256[4][256];  // lane combine inside a slice
+  uint32_t sh512[4][256], sh1k[4][256], sh2k[4][256];   // slice combine inside a wave
+  uint32_t sh4k[4][256];                                 // wave combine inside a workgroup
+  uint32_t tile_pow2[32][32];                            // GF(2) matrices: 16 KiB * 2^b
+};
+
+struct CrcLaunch {
+  const uint8_t* data;
+  uint64_t n;
+  uint64_t s_full;      // number of full 512 B slices in the block
+  uint64_t slice_lo;    // first full slice processed
+  uint64_t slice_hi;    // one past last full slice processed
+  uint64_t vfront;      // virtual leading zero slices (aligns block combine to tiles)
+  uint64_t ntiles;      // virtual tiles covering [slice_lo - vfront, slice_hi)
+  uint32_t full_init;   // S(512)
+  uint32_t has_tail;    // process the short tail slice (index s_full)
+  uint32_t tail_len;
+  uint32_t tail_init;   // S(tail_len)
+  uint32_t* meta_out;             // BE CRC per slice (nullable)
+  const uint32_t* meta_expect;    // BE CRC per slice to verify against (nullable)
+  uint32_t* part_crc;             // [grid] raw shifted partials for whole-block CRC (nullable)
+  uint32_t* part_bad;             // [grid] min mismatching slice index, 0xFFFFFFFF = none
+};
+
+struct GfLaunch {
+  const uint8_t* in[kMaxShards];
+  uint8_t* out[kMaxShards];
+  uint64_t len;   // bytes per shard (buffers padded to 16 B)
+  int k;          // inputs
+  int rows;       // outputs
+  const uint8_t* gf_tables;  // device: log[256] then exp[512] (poly 0x11D, generator 2)
+  uint8_t mat[kMaxShards * kMaxShards];  // rows x k, row-major
+};
+
+// Upload tables once per device. Returns device pointer.
+DevCrcTables* upload_crc_tables(hipStream_t s);
+int crc_grid_for(uint64_t ntiles, uint32_t has_tail);
+hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
+hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s);
+const uint8_t* upload_gf_tables(hipStream_t s);
+
+}  // namespace dfs

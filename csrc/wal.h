@@ -1,0 +1,41 @@
+// Append-only, CRC-framed write-ahead log for the Raft metadata plane. Replaces the
+// reference's RocksDB column of `log:{i}` keys + term/vote keys
+// (reference: dfs/metaserver/src/simple_raft.rs:809-991, 1033-1097).
+//
+// Frame: [u32 length LE][u32 crc32(payload) LE][payload]. A batch of records is written
+// with one pwrite and made durable with ONE fdatasync (leader batching / group commit,
+// simple_raft.rs:1689-1778). Replay stops at the first torn or corrupt frame and
+// truncates the tail, so a crash mid-append loses only the unacknowledged batch.
+#pragma once
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace dfs {
+
+class Wal {
+ public:
+  Wal(std::string path, bool sync);
+  ~Wal();
+  std::vector<std::string> replay();
+  void append(const std::vector<std::string>& records);
+  // Replace the whole log (compaction after a snapshot): new file + fsync + rename.
+  void reset(const std::vector<std::string>& records);
+  uint64_t size_bytes() const { return size_; }
+  uint64_t syncs() const { return syncs_; }
+
+ private:
+  void open_for_append();
+  std::string path_;
+  bool sync_;
+  int fd_ = -1;
+  uint64_t size_ = 0;
+  uint64_t syncs_ = 0;
+  std::mutex mu_;
+};
+
+// temp file + fdatasync + rename + directory fsync.
+void atomic_write_file(const std::string& path, const std::string& data, bool sync);
+
+}  // namespace dfs

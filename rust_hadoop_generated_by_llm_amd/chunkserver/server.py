@@ -1,0 +1,266 @@
+"""``dfs_chunkserver --gpu <i>`` — one ChunkServer process per MI355X (C43; reference
+dfs/chunkserver/src/bin/chunkserver.rs).
+
+Startup: HBM ChunkStore on GPU i (or the CPU store with ``--gpu -1``), optional RCCL
+replication rank (``--rccl-rank/--rccl-world/--rccl-rendezvous``), gRPC server, HTTP
+/health + /metrics, a 5 s heartbeat loop to every master of every shard (stats, bad
+blocks, commands, master term) and the 60 s scrubber."""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import shutil
+import signal
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from pathlib import Path
+
+from ..models import proto as pb
+from ..native import lib as native
+from ..native import require_gpu
+from ..parallel.sharding import ShardMap
+from ..utils import log as logsetup
+from ..utils.metrics import Registry
+from ..utils.rpc import ChannelPool, make_sync_server, rpc_details, server_credentials, strip_scheme, with_scheme
+from .service import ChunkServer
+
+log = logging.getLogger("dfs.chunkserver")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser("dfs_chunkserver", description="DFS ChunkServer (one per GPU)")
+    p.add_argument("--addr", default="127.0.0.1:50052")
+    p.add_argument("--config-servers", default="")
+    p.add_argument("--storage-dir", default="/tmp/chunkserver_data")
+    p.add_argument("--cold-storage-dir", default="")
+    p.add_argument("--advertise-addr", default=None)
+    p.add_argument("--http-port", type=int, default=8082)
+    p.add_argument("--tls-cert")
+    p.add_argument("--tls-key")
+    p.add_argument("--ca-cert")
+    p.add_argument("--domain-name")
+    p.add_argument("--rack-id", default="")
+    # MI355X-native build additions
+    p.add_argument("--masters", default="", help="static master list when no shard map/config server")
+    p.add_argument("--gpu", type=int, default=-1, help="HIP device for the HBM store (-1 = CPU store)")
+    p.add_argument("--hbm-capacity", default="0", help="arena bytes (suffix K/M/G ok); 0 = auto")
+    p.add_argument("--durability", choices=["nvme-sync", "hbm-ack"], default="nvme-sync")
+    p.add_argument("--lanes", type=int, default=8)
+    p.add_argument("--rccl-rank", type=int, default=-1)
+    p.add_argument("--rccl-world", type=int, default=0)
+    p.add_argument("--rccl-rendezvous", default="")
+    p.add_argument("--rccl-timeout-ms", type=int, default=60000)
+    p.add_argument("--replication-transport", choices=["rccl", "grpc"], default="rccl")
+    p.add_argument("--heartbeat-interval", type=float, default=5.0)
+    p.add_argument("--scrub-interval", type=float, default=60.0)
+    p.add_argument("--no-fsync", action="store_true", help="skip fdatasync (tests only)")
+    p.add_argument("--workers", type=int, default=64)
+    return p
+
+
+def parse_size(s: str) -> int:
+    s = str(s).strip().upper()
+    mult = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30, "T": 1 << 40}
+    if s and s[-1] in mult:
+        return int(float(s[:-1]) * mult[s[-1]])
+    return int(s)
+
+
+def rendezvous_ranks(d: str, rank: int, world: int, addr: str, timeout: float = 120.0) -> dict[str, int]:
+    """Publish our advertise address for our rank and wait for every rank's."""
+    Path(d).mkdir(parents=True, exist_ok=True)
+    tmp = Path(d) / f".addr_{rank}.tmp"
+    tmp.write_text(addr)
+    os.replace(tmp, Path(d) / f"addr_{rank}")
+    deadline = time.time() + timeout
+    out: dict[str, int] = {}
+    while time.time() < deadline:
+        out = {}
+        for r in range(world):
+            f = Path(d) / f"addr_{r}"
+            if f.exists():
+                out[strip_scheme(f.read_text().strip())] = r
+        if len(out) == world:
+            return out
+        time.sleep(0.05)
+    raise TimeoutError(f"rendezvous: only {len(out)}/{world} chunkservers published in {d}")
+
+
+class ChunkServerProcess:
+    def __init__(self, args):
+        self.args = args
+        # chunkserver addresses travel scheme-less, as in the reference (clients prepend http://)
+        self.advertise = strip_scheme(args.advertise_addr or args.addr)
+        if args.gpu >= 0:
+            require_gpu(args.gpu)
+        self.store = native.ChunkStore(
+            args.storage_dir, args.cold_storage_dir, args.gpu, parse_size(args.hbm_capacity),
+            0 if args.durability == "nvme-sync" else 1, int(os.environ.get("BLOCK_CACHE_SIZE", "100")),
+            args.lanes, 4, not args.no_fsync)
+        self.pool = ChannelPool(args.ca_cert, args.domain_name)
+        self.config_servers = [with_scheme(c) for c in args.config_servers.split(",") if c.strip()]
+        self.static_masters = [with_scheme(m) for m in args.masters.split(",") if m.strip()]
+        shard_cfg = os.environ.get("SHARD_CONFIG")
+        self.shard_map = ShardMap.load_config_file(shard_cfg) if shard_cfg else ShardMap.new_range()
+        self.rccl = None
+        rank_map: dict[str, int] = {}
+        if (args.replication_transport == "rccl" and args.rccl_world > 1 and args.rccl_rank >= 0
+                and args.rccl_rendezvous and args.gpu >= 0):
+            rank_map = rendezvous_ranks(args.rccl_rendezvous, args.rccl_rank, args.rccl_world, self.advertise)
+            eng = native.RcclEngine(self.store, args.rccl_rank, args.rccl_world, args.rccl_rendezvous,
+                                    args.rccl_timeout_ms)
+            ok, err = eng.init()
+            if ok:
+                self.rccl = eng
+                log.info("RCCL replication ready: rank %d/%d", args.rccl_rank, args.rccl_world)
+            else:
+                log.error("RCCL init failed (%s); using gRPC replication", err)
+        self.metrics = Registry()
+        self.cs = ChunkServer(self.store, self.advertise, self.pool, self.masters, self.rccl, rank_map,
+                              args.rccl_rank, self.metrics)
+        self._setup_metrics()
+        self._stop = threading.Event()
+
+    # ------------------------------------------------------------------ helpers
+    def masters(self) -> list[str]:
+        ms = self.shard_map.get_all_masters()
+        return [with_scheme(m) for m in ms] if ms else self.static_masters
+
+    def disk_stats(self) -> tuple[int, int]:
+        du = shutil.disk_usage(self.args.storage_dir)
+        return du.total - du.free, du.free
+
+    def _setup_metrics(self) -> None:
+        m = self.metrics
+        m.gauge("dfs_chunkserver_available_space_bytes", "free bytes on the storage fs", fn=lambda: self.disk_stats()[1])
+        m.gauge("dfs_chunkserver_used_space_bytes", "used bytes on the storage fs", fn=lambda: self.disk_stats()[0])
+        m.gauge("dfs_chunkserver_total_chunks", "blocks held", fn=lambda: self.store.stats()["blocks"])
+        for k in ("hbm_capacity", "hbm_used", "hbm_resident_blocks", "dirty_blocks", "spill_queue", "evictions",
+                  "promotions", "crc_mismatches", "gpu_kernel_launches"):
+            m.gauge(f"dfs_chunkserver_{k}", f"chunk store {k}", fn=lambda k=k: self.store.stats()[k])
+        m.gauge("dfs_chunkserver_rccl_bytes_sent", "bytes replicated over RCCL",
+                fn=lambda: self.rccl.bytes_sent if self.rccl else 0)
+        m.gauge("dfs_chunkserver_rccl_bytes_recv", "bytes received over RCCL",
+                fn=lambda: self.rccl.bytes_recv if self.rccl else 0)
+        for k in self.cs.stats:
+            m.gauge(f"dfs_chunkserver_{k}_total", k, fn=lambda k=k: self.cs.stats[k])
+
+    def refresh_shard_map(self) -> bool:
+        for c in self.config_servers:
+            try:
+                r = self.pool.call(c, "ConfigService", "FetchShardMap", pb.FetchShardMapRequest(), timeout=5.0)
+                new = ShardMap.from_peers({k: list(v.peers) for k, v in r.shards.items()})
+                sm = self.shard_map
+                sm.strategy, sm.ranges, sm.ring, sm.shards, sm.shard_peers = (
+                    new.strategy, new.ranges, new.ring, new.shards, new.shard_peers)
+                sm._dirty()
+                return True
+            except Exception as e:  # noqa: BLE001
+                log.debug("FetchShardMap from %s failed: %s", c, rpc_details(e))
+        return False
+
+    def heartbeat_once(self) -> None:
+        if self.config_servers:
+            self.refresh_shard_map()
+        used, avail = self.disk_stats()
+        st = self.store.stats()
+        bad, new = self.cs.drain_reports()
+        req = pb.HeartbeatRequest(chunk_server_address=self.advertise, used_space=used, available_space=avail,
+                                  chunk_count=st["blocks"], bad_blocks=bad, rack_id=self.args.rack_id,
+                                  gpu_rank=self.args.rccl_rank, hbm_capacity=st["hbm_capacity"],
+                                  hbm_used=st["hbm_used"], new_blocks=new)
+        for m in self.masters():
+            try:
+                r = self.pool.call(m, "MasterService", "Heartbeat", req, timeout=5.0)
+            except Exception as e:  # noqa: BLE001
+                log.debug("heartbeat to %s failed: %s", m, rpc_details(e))
+                continue
+            self.cs.adopt_term(r.master_term)
+            for cmd in r.commands:
+                self.cs.handle_command(cmd)
+
+    def _heartbeat_loop(self) -> None:
+        if self.config_servers:
+            while not self._stop.is_set() and not self.refresh_shard_map():
+                self._stop.wait(2.0)
+        while not self._stop.is_set():
+            try:
+                self.heartbeat_once()
+            except Exception:  # noqa: BLE001
+                log.exception("heartbeat failed")
+            self._stop.wait(self.args.heartbeat_interval)
+
+    def _scrub_loop(self) -> None:
+        while not self._stop.wait(self.args.scrub_interval):
+            try:
+                bad = self.cs.scrub_once()
+                if bad:
+                    log.warning("scrubber found %d corrupt block(s)", len(bad))
+            except Exception:  # noqa: BLE001
+                log.exception("scrub failed")
+
+    def _http(self) -> ThreadingHTTPServer:
+        proc = self
+
+        class H(BaseHTTPRequestHandler):
+            def log_message(self, *a):  # noqa: D401
+                pass
+
+            def do_GET(self):
+                if self.path == "/health":
+                    body, ctype = b"OK", "text/plain"
+                elif self.path == "/metrics":
+                    body, ctype = proc.metrics.render().encode(), "text/plain"
+                elif self.path == "/stats":
+                    d = dict(proc.store.stats())
+                    d.update(proc.cs.stats)
+                    body, ctype = json.dumps(d).encode(), "application/json"
+                else:
+                    self.send_response(404)
+                    self.end_headers()
+                    return
+                self.send_response(200)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        host = strip_scheme(self.args.addr).rsplit(":", 1)[0] or "0.0.0.0"
+        srv = ThreadingHTTPServer((host, self.args.http_port), H)
+        srv.daemon_threads = True
+        return srv
+
+    def run(self) -> None:
+        a = self.args
+        creds = server_credentials(a.tls_cert, a.tls_key)
+        server = make_sync_server({"ChunkServerService": self.cs}, a.addr, workers=a.workers, creds=creds)
+        server.start()
+        http = self._http()
+        threading.Thread(target=http.serve_forever, daemon=True, name="cs-http").start()
+        threading.Thread(target=self._heartbeat_loop, daemon=True, name="cs-heartbeat").start()
+        threading.Thread(target=self._scrub_loop, daemon=True, name="cs-scrub").start()
+        ready = os.environ.get("DFS_READY_FILE")
+        if ready:
+            with open(ready, "w") as f:
+                json.dump({"addr": a.addr, "gpu": a.gpu, "rccl": self.rccl is not None}, f)
+        for sig in (signal.SIGTERM, signal.SIGINT):
+            signal.signal(sig, lambda *_: self._stop.set())
+        log.info("chunkserver %s serving (gpu=%d, durability=%s)", self.advertise, a.gpu, a.durability)
+        while not self._stop.wait(0.5):
+            pass
+        server.stop(1.0).wait()
+        http.shutdown()
+        self.store.flush()
+
+
+def main(argv=None) -> None:
+    args = build_parser().parse_args(argv)
+    logsetup.setup("chunkserver")
+    ChunkServerProcess(args).run()
+
+
+if __name__ == "__main__":
+    main()

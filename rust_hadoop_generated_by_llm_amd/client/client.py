@@ -1,0 +1,412 @@
+"""DFS client library (C46-C48; reference dfs/client/src/mod.rs).
+
+Routing, retry and redirect semantics follow the reference: a path is routed to its
+shard's peers from the cached ShardMap (else the --master list); ``REDIRECT:<addr>`` and
+``Not Leader|<addr>`` become the next target; UNAVAILABLE / "Not Leader" try the next
+address; up to ``max_retries`` rounds with 500 ms doubling backoff capped at 5 s.
+
+MI355X-native differences:
+* persistent gRPC channels (the reference reconnects on every RPC, mod.rs:1412);
+* CRC-32 of the payload with the native PCLMUL engine, MD5 via OpenSSL (GIL released);
+* optional ``local_chunkserver``: passed to AllocateBlock so the first replica lands on
+  the writer's own GPU, and preferred as the read replica;
+* EC encode/decode on the GPU when a GPU ChunkStore handle is supplied.
+"""
+from __future__ import annotations
+
+import hashlib
+import logging
+import os
+import threading
+import time
+from concurrent.futures import FIRST_COMPLETED, ThreadPoolExecutor, wait
+
+import grpc
+
+from ..models import proto as pb
+from ..ops import crc as crcops
+from ..ops import erasure
+from ..parallel.sharding import ShardMap
+from ..utils.rpc import ChannelPool, rpc_code, rpc_details, strip_scheme, with_scheme
+
+log = logging.getLogger("dfs.client")
+
+MAX_RETRIES = 5
+INITIAL_BACKOFF_MS = 500
+
+
+class DfsError(Exception):
+    pass
+
+
+class _Retry(Exception):
+    """Internal: convert a success=false 'Not Leader' reply into a retryable failure."""
+
+    def __init__(self, hint: str):
+        super().__init__(f"Not Leader|{hint}")
+        self.hint = hint
+
+
+class Client:
+    def __init__(self, master_addrs: list[str], config_server_addrs: list[str] | None = None, *,
+                 max_retries: int = MAX_RETRIES, initial_backoff_ms: int = INITIAL_BACKOFF_MS,
+                 ca_cert: str | None = None, domain_name: str | None = None, hedge_delay_ms: int | None = None,
+                 local_chunkserver: str | None = None, ec_store=None, rpc_timeout: float = 30.0,
+                 data_timeout: float = 120.0):
+        self.tls = ca_cert is not None
+        self.master_addrs = [with_scheme(a, self.tls) for a in master_addrs if a]
+        self.config_server_addrs = [with_scheme(a, self.tls) for a in (config_server_addrs or []) if a]
+        self.shard_map = ShardMap.new_consistent_hash(100)
+        self._map_lock = threading.Lock()
+        self.host_aliases: dict[str, str] = {}
+        self.max_retries = max_retries
+        self.initial_backoff_ms = initial_backoff_ms
+        self.hedge_delay_ms = hedge_delay_ms
+        self.local_chunkserver = strip_scheme(local_chunkserver) if local_chunkserver else None
+        self.ec_store = ec_store
+        self.rpc_timeout = rpc_timeout
+        self.data_timeout = data_timeout
+        self.pool = ChannelPool(ca_cert, domain_name)
+        self._exec = ThreadPoolExecutor(max_workers=32, thread_name_prefix="dfs-client")
+
+    # ------------------------------------------------------------------ config
+    def with_retry_config(self, max_retries: int, initial_backoff_ms: int) -> "Client":
+        self.max_retries, self.initial_backoff_ms = max_retries, initial_backoff_ms
+        return self
+
+    def with_hedge_delay(self, delay_ms: int) -> "Client":
+        self.hedge_delay_ms = delay_ms
+        return self
+
+    def set_shard_map(self, m: ShardMap) -> None:
+        with self._map_lock:
+            self.shard_map = m
+
+    def add_host_alias(self, alias: str, real: str) -> None:
+        self.host_aliases[alias] = real
+
+    def resolve_url(self, url: str) -> str:
+        for alias, real in self.host_aliases.items():
+            if alias in url:
+                return url.replace(alias, real)
+        return url
+
+    def close(self) -> None:
+        self.pool.close()
+        self._exec.shutdown(wait=False)
+
+    # ------------------------------------------------------------------ master RPC routing
+    def _targets_for(self, key: str | None) -> list[str]:
+        if key is not None:
+            with self._map_lock:
+                sid = self.shard_map.get_shard(key)
+                peers = self.shard_map.get_shard_peers(sid) if sid else None
+            if peers:
+                return [with_scheme(p, self.tls) for p in peers]
+        return list(self.master_addrs)
+
+    def execute_rpc(self, key: str | None, method: str, request, check=None):
+        return self.execute_rpc_internal(self._targets_for(key), method, request, check)
+
+    def execute_rpc_internal(self, masters: list[str], method: str, request, check=None):
+        """Returns (response, address that answered)."""
+        backoff = self.initial_backoff_ms / 1000.0
+        hint: str | None = None
+        last_err = "no masters configured"
+        for attempt in range(1, max(1, self.max_retries) + 1):
+            targets = list(masters)
+            if hint:
+                targets.insert(0, with_scheme(hint, self.tls) if "://" not in hint else hint)
+                hint = None
+            for addr in targets:
+                if not addr:
+                    continue
+                resolved = self.resolve_url(addr)
+                try:
+                    resp = self.pool.call(resolved, "MasterService", method, request, timeout=self.rpc_timeout)
+                    if check is not None:
+                        check(resp)
+                    return resp, addr
+                except _Retry as e:
+                    last_err = str(e)
+                    if e.hint:
+                        hint = e.hint
+                        break
+                    continue
+                except grpc.RpcError as e:
+                    msg = rpc_details(e)
+                    code = rpc_code(e)
+                    last_err = f"{code}: {msg}"
+                    if msg.startswith("REDIRECT:") and msg[len("REDIRECT:"):]:
+                        hint = msg[len("REDIRECT:"):]
+                        self._exec.submit(self.refresh_shard_map)
+                        break
+                    if msg.startswith("Not Leader|") and msg.split("|", 1)[1]:
+                        hint = msg.split("|", 1)[1]
+                        break
+                    if "Not Leader" in msg or code in (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED):
+                        continue
+                    raise DfsError(f"{code.name if code else 'ERROR'}: {msg}") from e
+            if attempt >= self.max_retries:
+                break
+            if hint is None:
+                time.sleep(backoff)
+                backoff = min(backoff * 2, 5.0)
+        raise DfsError(f"No available leader found after retries ({last_err})")
+
+    @staticmethod
+    def _not_leader_check(resp):
+        if not resp.success and resp.error_message == "Not Leader":
+            raise _Retry(resp.leader_hint)
+
+    def refresh_shard_map(self) -> None:
+        for c in self.config_server_addrs:
+            try:
+                r = self.pool.call(self.resolve_url(c), "ConfigService", "FetchShardMap", pb.FetchShardMapRequest(),
+                                   timeout=5.0)
+            except Exception as e:  # noqa: BLE001
+                log.debug("FetchShardMap from %s failed: %s", c, rpc_details(e))
+                continue
+            if r.shards:
+                self.set_shard_map(ShardMap.from_peers({k: list(v.peers) for k, v in r.shards.items()}))
+            return
+
+    # ------------------------------------------------------------------ namespace ops
+    def list_files(self, path: str) -> list[str]:
+        resp, _ = self.execute_rpc(path, "ListFiles", pb.ListFilesRequest(path=path))
+        return list(resp.files)
+
+    def list_all_files(self, path: str = "/") -> list[str]:
+        """Union over every shard (reference list_all_files, mod.rs:125-200)."""
+        if self.config_server_addrs:
+            self.refresh_shard_map()
+        with self._map_lock:
+            shards = self.shard_map.get_all_shards()
+            peer_lists = [self.shard_map.get_shard_peers(s) or [] for s in shards]
+        files: set[str] = set()
+        if not peer_lists:
+            peer_lists = [self.master_addrs]
+        for peers in peer_lists:
+            resp, _ = self.execute_rpc_internal([with_scheme(p, self.tls) for p in peers], "ListFiles",
+                                                pb.ListFilesRequest(path=path))
+            files.update(resp.files)
+        return sorted(files)
+
+    def get_file_info(self, path: str):
+        resp, _ = self.execute_rpc(path, "GetFileInfo", pb.GetFileInfoRequest(path=path))
+        return resp.metadata if resp.found else None
+
+    def exists(self, path: str) -> bool:
+        return self.get_file_info(path) is not None
+
+    def delete_file(self, path: str) -> None:
+        resp, _ = self.execute_rpc(path, "DeleteFile", pb.DeleteFileRequest(path=path), self._not_leader_check)
+        if not resp.success:
+            raise DfsError(f"Failed to delete file: {resp.error_message}")
+
+    def rename_file(self, source: str, dest: str) -> None:
+        resp, _ = self.execute_rpc(source, "Rename", pb.RenameRequest(source_path=source, dest_path=dest),
+                                   self._not_leader_check)
+        if not resp.success:
+            raise DfsError(f"Rename failed: {resp.error_message}")
+
+    def initiate_shuffle(self, prefix: str) -> None:
+        resp, _ = self.execute_rpc(prefix, "InitiateShuffle", pb.InitiateShuffleRequest(prefix=prefix),
+                                   self._not_leader_check)
+        if not resp.success:
+            raise DfsError(f"Shuffle failed: {resp.error_message}")
+
+    # ------------------------------------------------------------------ write path
+    def create_file(self, local_path: str, dest: str, ec: tuple[int, int] | None = None) -> None:
+        with open(local_path, "rb") as f:
+            data = f.read()
+        if ec:
+            self.create_file_from_buffer_ec(data, dest, *ec)
+        else:
+            self.create_file_from_buffer(data, dest)
+
+    def _create_and_allocate(self, dest: str, ec_d: int = 0, ec_p: int = 0):
+        resp, addr = self.execute_rpc(dest, "CreateFile", pb.CreateFileRequest(
+            path=dest, ec_data_shards=ec_d, ec_parity_shards=ec_p), self._not_leader_check)
+        if not resp.success:
+            raise DfsError(f"Failed to create file: {resp.error_message}")
+        masters = [addr] + [m for m in self.master_addrs if m != addr]
+
+        def alloc_check(r):
+            if not r.HasField("block"):
+                raise _Retry(r.leader_hint)
+
+        req = pb.AllocateBlockRequest(path=dest, preferred_chunk_server=self.local_chunkserver or "")
+        alloc, _ = self.execute_rpc_internal(masters, "AllocateBlock", req, alloc_check)
+        if not alloc.chunk_server_addresses:
+            raise DfsError("No chunk servers available")
+        return alloc
+
+    def _complete(self, dest: str, size: int, etag: str, sums: list) -> None:
+        req = pb.CompleteFileRequest(path=dest, size=size, etag_md5=etag, created_at_ms=int(time.time() * 1000),
+                                     block_checksums=sums)
+        resp, _ = self.execute_rpc(dest, "CompleteFile", req)
+        if not resp.success:
+            raise DfsError("Failed to complete file")
+
+    def _cs(self, addr: str) -> str:
+        return self.resolve_url(with_scheme(addr, self.tls))
+
+    def create_file_from_buffer(self, data: bytes, dest: str) -> int:
+        """CreateFile -> AllocateBlock -> WriteBlock(chain) -> CompleteFile. Returns
+        replicas_written (reference mod.rs:225-494)."""
+        alloc = self._create_and_allocate(dest)
+        block = alloc.block
+        servers = list(alloc.chunk_server_addresses)
+        crc = crcops.crc32(data)
+        etag = hashlib.md5(data).hexdigest()
+        req = pb.WriteBlockRequest(block_id=block.block_id, data=data, next_servers=servers[1:],
+                                   expected_checksum_crc32c=crc, shard_index=-1, master_term=alloc.master_term)
+        try:
+            resp = self.pool.call(self._cs(servers[0]), "ChunkServerService", "WriteBlock", req,
+                                  timeout=self.data_timeout)
+        except grpc.RpcError as e:
+            raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
+        if not resp.success:
+            raise DfsError(f"Failed to write block: {resp.error_message}")
+        if resp.replicas_written < len(servers):
+            log.warning("block written to %d/%d replicas", resp.replicas_written, len(servers))
+        self._complete(dest, len(data), etag, [pb.BlockChecksumInfo(block_id=block.block_id, checksum_crc32c=crc,
+                                                                    actual_size=len(data))])
+        return resp.replicas_written
+
+    def create_file_from_buffer_ec(self, data: bytes, dest: str, ec_data_shards: int, ec_parity_shards: int) -> None:
+        """RS(k,m) encode, scatter shard i to chunk_servers[i] in parallel, CompleteFile with
+        the whole-buffer CRC and an empty etag (reference mod.rs:496-677)."""
+        alloc = self._create_and_allocate(dest, ec_data_shards, ec_parity_shards)
+        k, m = alloc.ec_data_shards, alloc.ec_parity_shards
+        servers = list(alloc.chunk_server_addresses)
+        if k == 0 or m == 0:
+            raise DfsError(f"Master returned non-EC policy (data={k}, parity={m}) for EC file")
+        if len(servers) != k + m:
+            raise DfsError(f"Expected {k + m} chunk servers for EC({k},{m}), got {len(servers)}")
+        shards = erasure.encode(data, k, m, self.ec_store)
+        bid = alloc.block.block_id
+
+        def put(i):
+            req = pb.WriteBlockRequest(block_id=bid, data=shards[i], expected_checksum_crc32c=crcops.crc32(shards[i]),
+                                       shard_index=i, master_term=alloc.master_term)
+            r = self.pool.call(self._cs(servers[i]), "ChunkServerService", "WriteBlock", req, timeout=self.data_timeout)
+            if not r.success:
+                raise DfsError(f"Shard {i} write failed: {r.error_message}")
+
+        for f in [self._exec.submit(put, i) for i in range(k + m)]:
+            f.result()
+        self._complete(dest, len(data), "", [pb.BlockChecksumInfo(block_id=bid, checksum_crc32c=crcops.crc32(data),
+                                                                  actual_size=len(data))])
+
+    # ------------------------------------------------------------------ read path
+    def _order_locations(self, locations) -> list[str]:
+        locs = list(locations)
+        if self.local_chunkserver and self.local_chunkserver in locs:
+            locs.remove(self.local_chunkserver)
+            locs.insert(0, self.local_chunkserver)
+        return locs
+
+    def read_block_from_location(self, location: str, block_id: str, offset: int = 0, length: int = 0) -> bytes:
+        r = self.pool.call(self._cs(location), "ChunkServerService", "ReadBlock",
+                           pb.ReadBlockRequest(block_id=block_id, offset=offset, length=length),
+                           timeout=self.data_timeout)
+        return r.data
+
+    def read_block_range(self, locations, block_id: str, offset: int = 0, length: int = 0) -> bytes:
+        locs = self._order_locations(locations)
+        if not locs:
+            raise DfsError(f"No locations for block {block_id}")
+        if self.hedge_delay_ms is not None and len(locs) >= 2:
+            return self._hedged_read(locs, block_id, offset, length)
+        last = None
+        for loc in locs:
+            try:
+                return self.read_block_from_location(loc, block_id, offset, length)
+            except grpc.RpcError as e:
+                last = e
+                log.debug("read %s from %s failed: %s", block_id, loc, rpc_details(e))
+        raise DfsError(f"Failed to read block {block_id} from any location: {rpc_details(last) if last else ''}")
+
+    def _hedged_read(self, locs, block_id, offset, length) -> bytes:
+        """Race the primary against a delayed second replica; first success wins, then the
+        remaining replicas are tried in order (reference mod.rs:948-1107)."""
+        primary = self._exec.submit(self.read_block_from_location, locs[0], block_id, offset, length)
+        done, _ = wait([primary], timeout=self.hedge_delay_ms / 1000.0)
+        futs = [primary]
+        if not done:
+            futs.append(self._exec.submit(self.read_block_from_location, locs[1], block_id, offset, length))
+        pending = set(futs)
+        while pending:
+            done, pending = wait(pending, return_when=FIRST_COMPLETED)
+            for f in done:
+                if f.exception() is None:
+                    return f.result()
+        for loc in locs[len(futs):]:
+            try:
+                return self.read_block_from_location(loc, block_id, offset, length)
+            except grpc.RpcError:
+                continue
+        raise DfsError(f"Hedged read of {block_id} failed on every replica")
+
+    def read_ec_block(self, block) -> bytes:
+        k, m = block.ec_data_shards, block.ec_parity_shards
+        locs = list(block.locations)
+        futs = [self._exec.submit(self.read_block_from_location, a, block.block_id) if a else None for a in locs]
+        shards: list[bytes | None] = []
+        for f in futs:
+            try:
+                shards.append(f.result() if f is not None else None)
+            except Exception:  # noqa: BLE001
+                shards.append(None)
+        orig = block.original_size or block.size
+        if all(s is not None for s in shards[:k]):
+            return b"".join(shards[:k])[:orig]  # fast path: data shards intact
+        return erasure.decode(shards, k, m, orig, self.ec_store)
+
+    def fetch_single_block(self, block) -> bytes:
+        if block.ec_data_shards > 0:
+            return self.read_ec_block(block)
+        return self.read_block_range(block.locations, block.block_id)
+
+    def get_file_content(self, path: str) -> bytes:
+        meta = self.get_file_info(path)
+        if meta is None:
+            raise DfsError("File not found")
+        if len(meta.blocks) == 1:
+            return self.fetch_single_block(meta.blocks[0])
+        parts = list(self._exec.map(self.fetch_single_block, meta.blocks))
+        return b"".join(parts)
+
+    def get_file(self, source: str, dest: str) -> None:
+        data = self.get_file_content(source)
+        with open(dest, "wb") as f:
+            f.write(data)
+
+    get_file_concurrent = get_file
+
+    def read_file_range(self, path: str, offset: int, length: int) -> bytes:
+        meta = self.get_file_info(path)
+        if meta is None:
+            raise DfsError("File not found")
+        if offset >= meta.size:
+            raise DfsError(f"Offset {offset} exceeds file size {meta.size}")
+        end = offset + min(length, meta.size - offset)
+        out = []
+        pos = 0
+        for b in meta.blocks:
+            bstart, bend = pos, pos + b.size
+            pos = bend
+            if bend <= offset:
+                continue
+            if bstart >= end:
+                break
+            boff = max(0, offset - bstart)
+            blen = min(b.size, end - bstart) - boff
+            if b.ec_data_shards > 0:
+                full = self.read_ec_block(b)
+                out.append(full[boff:boff + blen])
+            else:
+                out.append(self.read_block_range(b.locations, b.block_id, boff, blen))
+        return b"".join(out)

@@ -1,0 +1,281 @@
+"""Single-host multi-process cluster launcher — the replacement for the reference's
+docker-compose topologies (C60; docker-compose.yml, docker-compose.auto-scaling.yml).
+
+One process per role: config server(s), one master per shard (or a Raft group per shard),
+and one ChunkServer per GPU (``gpus=[0..7]``) or CPU ChunkServers (``gpus=None``). All
+ports are picked free at start; readiness is signalled through ``DFS_READY_FILE``.
+Used by the tests, ``bench.py`` and ``dfs_cli cluster up``.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+PKG = "rust_hadoop_generated_by_llm_amd"
+ROOT = Path(__file__).resolve().parents[2]
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@dataclass
+class Proc:
+    name: str
+    popen: subprocess.Popen
+    ready_file: str
+    info: dict = field(default_factory=dict)
+    log_path: str = ""
+
+
+class LocalCluster:
+    def __init__(self, base_dir: str | None = None, *, n_chunkservers: int = 1, gpus: list[int] | None = None,
+                 shards: int = 1, masters_per_shard: int = 1, config_server: bool = False,
+                 durability: str = "nvme-sync", fsync: bool = True, rccl: bool = True,
+                 hbm_capacity: str = "0", heartbeat_interval: float = 0.5, scrub_interval: float = 60.0,
+                 rack_ids: list[str] | None = None, fast_intervals: bool = False, cold_dir: bool = False,
+                 env: dict | None = None, master_args: list[str] | None = None, cs_args: list[str] | None = None):
+        self.owns_dir = base_dir is None
+        self.base = Path(base_dir or tempfile.mkdtemp(prefix="dfs_cluster_"))
+        self.base.mkdir(parents=True, exist_ok=True)
+        self.gpus = gpus
+        self.n_cs = len(gpus) if gpus is not None else n_chunkservers
+        self.shards = shards
+        self.masters_per_shard = masters_per_shard
+        self.use_config = config_server or shards > 1
+        self.durability = durability
+        self.fsync = fsync
+        self.rccl = rccl
+        self.hbm_capacity = hbm_capacity
+        self.heartbeat_interval = heartbeat_interval
+        self.scrub_interval = scrub_interval
+        self.rack_ids = rack_ids
+        self.fast_intervals = fast_intervals
+        self.cold_dir = cold_dir
+        self.env = dict(os.environ)
+        self.env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        self.env["PYTHONPATH"] = str(ROOT) + os.pathsep + self.env.get("PYTHONPATH", "")
+        self.env.setdefault("DFS_LOG", "warning")
+        if env:
+            self.env.update(env)
+        self.master_args = master_args or []
+        self.cs_args = cs_args or []
+        self.procs: list[Proc] = []
+        self.config_addrs: list[str] = []
+        self.shard_masters: dict[str, list[str]] = {}
+        self.master_http: dict[str, str] = {}
+        self.cs_addrs: list[str] = []
+        self.cs_http: list[str] = []
+
+    # ------------------------------------------------------------------ process helpers
+    def _spawn(self, name: str, module: str, args: list[str], extra_env: dict | None = None) -> Proc:
+        ready = str(self.base / f"{name}.ready")
+        if os.path.exists(ready):
+            os.unlink(ready)
+        env = dict(self.env)
+        env["DFS_READY_FILE"] = ready
+        if extra_env:
+            env.update(extra_env)
+        log_path = str(self.base / f"{name}.log")
+        logf = open(log_path, "ab")
+        p = subprocess.Popen([sys.executable, "-m", f"{PKG}.{module}", *args], env=env, stdout=logf,
+                             stderr=subprocess.STDOUT, cwd=str(ROOT), start_new_session=True)
+        logf.close()
+        proc = Proc(name, p, ready, log_path=log_path)
+        self.procs.append(proc)
+        return proc
+
+    def _wait_ready(self, procs: list[Proc], timeout: float = 180.0) -> None:
+        deadline = time.time() + timeout
+        for pr in procs:
+            while not os.path.exists(pr.ready_file):
+                if pr.popen.poll() is not None:
+                    raise RuntimeError(f"{pr.name} exited with {pr.popen.returncode}:\n{self.tail(pr)}")
+                if time.time() > deadline:
+                    raise TimeoutError(f"{pr.name} not ready after {timeout}s:\n{self.tail(pr)}")
+                time.sleep(0.05)
+            with open(pr.ready_file) as f:
+                try:
+                    pr.info = json.load(f)
+                except ValueError:
+                    pr.info = {}
+
+    @staticmethod
+    def tail(pr: Proc, n: int = 40) -> str:
+        try:
+            with open(pr.log_path, errors="replace") as f:
+                return "".join(f.readlines()[-n:])
+        except OSError:
+            return ""
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> "LocalCluster":
+        try:
+            self._start()
+        except Exception:
+            self.stop()
+            raise
+        return self
+
+    def _start(self) -> None:
+        fs = [] if self.fsync else ["--no-fsync"]
+        if self.use_config:
+            port, http = free_port(), free_port()
+            pr = self._spawn("config", "config_server.server", [
+                "--addr", f"127.0.0.1:{port}", "--http-port", str(http), "--storage-dir",
+                str(self.base / "config"), *fs])
+            self._wait_ready([pr])
+            self.config_addrs = [f"http://127.0.0.1:{port}"]
+        # masters
+        shard_cfg: dict[str, list[str]] = {}
+        plans = []
+        for s in range(self.shards):
+            sid = f"shard-{s}"
+            ids = list(range(1, self.masters_per_shard + 1))
+            ports = {i: (free_port(), free_port()) for i in ids}
+            shard_cfg[sid] = [f"http://127.0.0.1:{ports[i][0]}" for i in ids]
+            plans.append((sid, ids, ports))
+        shard_file = self.base / "shard_config.json"
+        shard_file.write_text(json.dumps({"shards": shard_cfg}))
+        mprocs = []
+        for sid, ids, ports in plans:
+            for i in ids:
+                gport, hport = ports[i]
+                peers = ",".join(f"{j}@http://127.0.0.1:{ports[j][1]}" for j in ids if j != i)
+                args = ["--addr", f"127.0.0.1:{gport}", "--id", str(i), "--http-port", str(hport),
+                        "--storage-dir", str(self.base / f"master_{sid}"), "--shard-id", sid, *fs, *self.master_args]
+                if peers:
+                    args += ["--peers", peers]
+                if self.use_config:
+                    args += ["--config-servers", ",".join(self.config_addrs)]
+                else:
+                    args += ["--shard-config", str(shard_file)]
+                if self.fast_intervals:
+                    args.append("--fast-intervals")
+                mprocs.append(self._spawn(f"master_{sid}_{i}", "master.server", args))
+                self.master_http[f"http://127.0.0.1:{gport}"] = f"http://127.0.0.1:{hport}"
+        self._wait_ready(mprocs)
+        self.shard_masters = shard_cfg
+        # chunkservers
+        rdv = self.base / "rccl_rendezvous"
+        if rdv.exists():
+            shutil.rmtree(rdv)
+        cprocs = []
+        for i in range(self.n_cs):
+            port, http = free_port(), free_port()
+            gpu = self.gpus[i] if self.gpus is not None else -1
+            args = ["--addr", f"127.0.0.1:{port}", "--http-port", str(http),
+                    "--storage-dir", str(self.base / f"cs{i}"), "--gpu", str(gpu),
+                    "--durability", self.durability, "--hbm-capacity", self.hbm_capacity,
+                    "--heartbeat-interval", str(self.heartbeat_interval),
+                    "--scrub-interval", str(self.scrub_interval), *fs, *self.cs_args]
+            if self.cold_dir:
+                args += ["--cold-storage-dir", str(self.base / f"cs{i}_cold")]
+            if self.rack_ids:
+                args += ["--rack-id", self.rack_ids[i % len(self.rack_ids)]]
+            if self.use_config:
+                args += ["--config-servers", ",".join(self.config_addrs)]
+            else:
+                args += ["--masters", ",".join(m for ms in shard_cfg.values() for m in ms)]
+            if self.gpus is not None and self.n_cs > 1 and self.rccl:
+                args += ["--rccl-rank", str(i), "--rccl-world", str(self.n_cs), "--rccl-rendezvous", str(rdv)]
+            else:
+                args += ["--replication-transport", "grpc"]
+            cprocs.append(self._spawn(f"cs{i}", "chunkserver.server", args))
+            self.cs_addrs.append(f"127.0.0.1:{port}")
+            self.cs_http.append(f"http://127.0.0.1:{http}")
+        self._wait_ready(cprocs)
+        self.wait_registered()
+
+    @property
+    def master_addrs(self) -> list[str]:
+        return [m for ms in self.shard_masters.values() for m in ms]
+
+    def client(self, **kw):
+        from ..client.client import Client
+
+        c = Client(self.master_addrs, self.config_addrs, **kw)
+        if not self.use_config:
+            from ..parallel.sharding import ShardMap
+
+            c.set_shard_map(ShardMap.from_config(self.shard_masters))
+        else:
+            c.refresh_shard_map()
+        return c
+
+    def wait_registered(self, timeout: float = 60.0) -> None:
+        """Block until every master leader has seen every chunkserver and left safe mode."""
+        import grpc
+
+        from ..models import proto as pb
+        from ..utils.rpc import ChannelPool
+
+        pool = ChannelPool()
+        deadline = time.time() + timeout
+        try:
+            for sid, masters in self.shard_masters.items():
+                while True:
+                    ok = False
+                    for m in masters:
+                        try:
+                            st = pool.call(m, "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(),
+                                           timeout=2.0)
+                            if st.chunk_server_count >= self.n_cs and not st.is_safe_mode:
+                                ok = True
+                                break
+                        except grpc.RpcError:
+                            pass
+                    if ok:
+                        break
+                    if time.time() > deadline:
+                        raise TimeoutError(f"shard {sid} never saw {self.n_cs} chunkservers")
+                    time.sleep(0.1)
+        finally:
+            pool.close()
+
+    def kill(self, name: str, sig: int = signal.SIGKILL) -> None:
+        for pr in self.procs:
+            if pr.name == name and pr.popen.poll() is None:
+                try:
+                    os.killpg(pr.popen.pid, sig)
+                except ProcessLookupError:
+                    pass
+                pr.popen.wait(timeout=30)
+
+    def stop(self) -> None:
+        for pr in reversed(self.procs):
+            if pr.popen.poll() is None:
+                try:
+                    os.killpg(pr.popen.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        deadline = time.time() + 20
+        for pr in self.procs:
+            try:
+                pr.popen.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(pr.popen.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                pr.popen.wait(timeout=10)
+        self.procs = []
+        if self.owns_dir:
+            shutil.rmtree(self.base, ignore_errors=True)
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()

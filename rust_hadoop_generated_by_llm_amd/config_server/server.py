@@ -1,0 +1,236 @@
+"""``dfs_config_server`` — Raft-replicated shard map + master registry (C36; reference
+dfs/metaserver/src/config_server.rs and bin/config_server.rs).
+
+State ``{"Config": {"shard_map": ShardMap(Range), "masters": {addr: MasterInfo}}}``.
+FetchShardMap is linearizable (ReadIndex) and, like the reference, returns only
+shard -> peers (no range boundaries). SplitShard without peers auto-allocates the three
+most recently heartbeated masters. HTTP: /raft/{vote,append,snapshot}, /shards, plus
+/health and /metrics (the reference has neither)."""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import signal
+import time
+
+from aiohttp import web
+
+from ..models import proto as pb
+from ..parallel.sharding import ShardMap
+from ..raft.membership import initial_members
+from ..raft.node import NotLeader, RaftNode
+from ..raft.transport import HttpTransport
+from ..utils import log as logsetup
+from ..utils.metrics import Registry
+from ..utils.rpc import RpcStatus, StatusCode, make_aio_server, server_credentials, with_scheme
+
+
+class ConfigState:
+    def __init__(self):
+        self.shard_map = ShardMap.new_range()
+        self.masters: dict[str, dict] = {}
+
+    def apply(self, command, index: int = 0):
+        if not isinstance(command, dict) or "Config" not in command:
+            return None
+        (name, a), = command["Config"].items()
+        sm = self.shard_map
+        if name == "AddShard":
+            sm.add_shard(a["shard_id"], a["peers"])
+        elif name == "RemoveShard":
+            sm.remove_shard(a["shard_id"])
+        elif name == "SplitShard":
+            return sm.split_shard(a["split_key"], a["new_shard_id"], a["new_shard_peers"])
+        elif name == "MergeShard":
+            return sm.merge_shards(a["victim_shard_id"], a["retained_shard_id"])
+        elif name == "RebalanceShard":
+            return sm.rebalance_boundary(a["old_key"], a["new_key"])
+        elif name == "RegisterMaster":
+            addr, sid = a["address"], a["shard_id"]
+            if not sm.has_shard(sid):
+                sm.add_shard(sid, [addr])
+            else:
+                peers = sm.get_shard_peers(sid) or []
+                if addr not in peers:
+                    sm.add_shard(sid, peers + [addr])
+            self.masters[addr] = {"address": addr, "shard_id": sid, "last_heartbeat": int(time.time()),
+                                  "rps_per_prefix": {}}
+        elif name == "ShardHeartbeat":
+            info = self.masters.get(a["address"])
+            if info is not None:
+                info["last_heartbeat"] = int(time.time())
+                info["rps_per_prefix"] = dict(a.get("rps_per_prefix", {}))
+        return None
+
+    def snapshot(self) -> dict:
+        return {"Config": {"shard_map": self.shard_map.to_json(), "masters": self.masters}}
+
+    def restore(self, state: dict) -> None:
+        c = state.get("Config", state)
+        self.shard_map = ShardMap.from_json(c.get("shard_map", {"strategy": {"Range": {"ranges": {}}}}))
+        self.masters = dict(c.get("masters", {}))
+
+
+class ConfigService:
+    def __init__(self, state: ConfigState, raft: RaftNode):
+        self.state = state
+        self.raft = raft
+
+    async def _propose(self, name, args):
+        return await self.raft.propose({"Config": {name: args}})
+
+    async def _simple(self, resp_cls, name, args):
+        try:
+            await self._propose(name, args)
+        except NotLeader as e:
+            return resp_cls(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return resp_cls(success=True)
+
+    async def fetch_shard_map(self, req, ctx):
+        try:
+            await self.raft.read_index()
+        except NotLeader as e:
+            raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"Not Leader|{e.hint}")
+        resp = pb.FetchShardMapResponse()
+        sm = self.state.shard_map
+        for sid in sm.get_all_shards():
+            resp.shards[sid].peers.extend(sm.get_shard_peers(sid) or [])
+        return resp
+
+    async def add_shard(self, req, ctx):
+        return await self._simple(pb.AddShardResponse, "AddShard", {"shard_id": req.shard_id, "peers": list(req.peers)})
+
+    async def remove_shard(self, req, ctx):
+        return await self._simple(pb.RemoveShardResponse, "RemoveShard", {"shard_id": req.shard_id})
+
+    async def split_shard(self, req, ctx):
+        peers = list(req.new_shard_peers)
+        if not peers:
+            avail = sorted(self.state.masters.values(), key=lambda m: -m["last_heartbeat"])
+            peers = [m["address"] for m in avail[:3]]
+        if not peers:
+            return pb.SplitShardResponse(success=False, error_message="No available master nodes for new shard")
+        try:
+            await self._propose("SplitShard", {"shard_id": req.shard_id, "split_key": req.split_key,
+                                               "new_shard_id": req.new_shard_id, "new_shard_peers": peers})
+        except NotLeader as e:
+            return pb.SplitShardResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return pb.SplitShardResponse(success=True, new_shard_peers=peers)
+
+    async def merge_shard(self, req, ctx):
+        return await self._simple(pb.MergeShardResponse, "MergeShard", {
+            "victim_shard_id": req.victim_shard_id, "retained_shard_id": req.retained_shard_id})
+
+    async def rebalance_shard(self, req, ctx):
+        return await self._simple(pb.RebalanceShardResponse, "RebalanceShard",
+                                  {"old_key": req.old_key, "new_key": req.new_key})
+
+    async def register_master(self, req, ctx):
+        try:
+            await self._propose("RegisterMaster", {"address": req.address, "shard_id": req.shard_id})
+        except NotLeader:
+            return pb.RegisterMasterResponse(success=False)
+        return pb.RegisterMasterResponse(success=True)
+
+    async def shard_heartbeat(self, req, ctx):
+        if not self.raft.is_leader():
+            return pb.ShardHeartbeatResponse(success=False)
+        self.raft.propose_nowait({"Config": {"ShardHeartbeat": {"address": req.address,
+                                                                "rps_per_prefix": dict(req.rps_per_prefix)}}})
+        return pb.ShardHeartbeatResponse(success=True)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser("dfs_config_server")
+    p.add_argument("--addr", default="127.0.0.1:50052")
+    p.add_argument("--id", type=int, default=1)
+    p.add_argument("--peers", default="")
+    p.add_argument("--http-port", type=int, default=8081)
+    p.add_argument("--advertise-addr", default=None)
+    p.add_argument("--storage-dir", default="/tmp/config-raft-logs")
+    p.add_argument("--tls-cert")
+    p.add_argument("--tls-key")
+    p.add_argument("--ca-cert")
+    p.add_argument("--no-fsync", action="store_true")
+    p.add_argument("--snapshot-threshold", type=int, default=10000)
+    return p
+
+
+async def run(args) -> None:
+    host = args.addr.split(":")[0] if ":" in args.addr else "127.0.0.1"
+    self_http = f"http://{host}:{args.http_port}"
+    state = ConfigState()
+    members = initial_members(args.id, self_http, [p for p in args.peers.split(",") if p.strip()])
+    transport = HttpTransport()
+    raft = RaftNode(args.id, members, with_scheme(args.advertise_addr or args.addr),
+                    os.path.join(args.storage_dir, f"raft_node_{args.id}"), state, transport,
+                    snapshot_threshold=args.snapshot_threshold, sync=not args.no_fsync)
+    svc = ConfigService(state, raft)
+    metrics = Registry()
+    metrics.gauge("raft_role", "0=follower 1=candidate 2=leader",
+                  fn=lambda: {"Follower": 0, "Candidate": 1, "Leader": 2}[raft.role])
+    metrics.gauge("config_shards", "shards in the map", fn=lambda: len(state.shard_map.shards))
+    app = web.Application(client_max_size=1 << 30)
+
+    def raft_route(kind):
+        async def h(req):
+            try:
+                return web.json_response(await raft.handle(kind, await req.json()))
+            except Exception:  # noqa: BLE001
+                return web.Response(status=500, text="Internal server error")
+
+        return h
+
+    for k in ("vote", "append", "snapshot", "timeout_now"):
+        app.router.add_post(f"/raft/{k}", raft_route(k))
+
+    async def shards(_):
+        return web.json_response({"shards": state.shard_map.get_all_shards()})
+
+    async def health(_):
+        return web.Response(text="OK")
+
+    async def metrics_h(_):
+        return web.Response(text=metrics.render(), content_type="text/plain")
+
+    async def raft_state(_):
+        return web.json_response(raft.cluster_info())
+
+    app.router.add_get("/shards", shards)
+    app.router.add_get("/health", health)
+    app.router.add_get("/metrics", metrics_h)
+    app.router.add_get("/raft/state", raft_state)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    await web.TCPSite(runner, host, args.http_port, reuse_address=True).start()
+    server = make_aio_server({"ConfigService": svc}, args.addr, server_credentials(args.tls_cert, args.tls_key))
+    await server.start()
+    await raft.start()
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    ready = os.environ.get("DFS_READY_FILE")
+    if ready:
+        with open(ready, "w") as f:
+            json.dump({"addr": args.addr}, f)
+    await stop.wait()
+    await server.stop(0.5)
+    await raft.stop()
+    await transport.close()
+    await runner.cleanup()
+
+
+def main(argv=None) -> None:
+    args = build_parser().parse_args(argv)
+    logsetup.setup("config_server")
+    asyncio.run(run(args))
+
+
+if __name__ == "__main__":
+    main()

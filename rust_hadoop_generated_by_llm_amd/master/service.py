@@ -1,0 +1,453 @@
+"""MasterService gRPC handlers (C27, C33) on grpc.aio + the Raft node.
+
+Status codes and message strings match the reference so unmodified clients behave the
+same (reference: dfs/metaserver/src/master.rs:2141-3660):
+* wrong shard            -> OUT_OF_RANGE ``REDIRECT:<first peer of owning shard>``
+* not leader (reads)     -> FAILED_PRECONDITION ``Not Leader|<leader>``
+* not leader (writes)    -> success=false, error_message ``Not Leader``, leader_hint
+* safe mode (writes)     -> UNAVAILABLE ``Cluster is in Safe Mode. Write operations are blocked.``
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+import uuid
+
+from ..models import meta as M
+from ..models import proto as pb
+from ..parallel.sharding import ShardMap
+from ..raft.node import NotLeader, RaftNode
+from ..utils.rpc import AioChannelPool, RpcStatus, StatusCode, rpc_details
+from .monitor import ThroughputMonitor
+from .state import (REPLICATION_FACTOR, SCHEDULE_QUANTUM, ChunkServerStatus, MasterState, now_ms,
+                    select_servers_rack_aware)
+
+log = logging.getLogger("dfs.master")
+
+SAFE_MODE_MSG = "Cluster is in Safe Mode. Write operations are blocked."
+
+
+def new_rename_record(tx_id, source_path, dest_path, source_shard, dest_shard, dest_meta) -> dict:
+    return {
+        "tx_id": tx_id,
+        "tx_type": {"Rename": {"source_path": source_path, "dest_path": dest_path}},
+        "state": "Pending",
+        "timestamp": now_ms(),
+        "participants": [source_shard, dest_shard],
+        "operations": [
+            {"shard_id": source_shard, "op_type": {"Delete": {"path": source_path}}},
+            {"shard_id": dest_shard, "op_type": {"Create": {"path": dest_path, "metadata": M.file_to_dict(dest_meta)}}},
+        ],
+        "coordinator_shard": source_shard,
+        "participant_acked": False,
+        "inquiry_count": 0,
+    }
+
+
+class MasterService:
+    def __init__(self, state: MasterState, raft: RaftNode, shard_map: ShardMap, shard_id: str,
+                 monitor: ThroughputMonitor, pool: AioChannelPool, *, advertise_addr: str = "",
+                 access_stats: bool = True, access_stats_flush_ms: int = 200):
+        self.state = state
+        self.raft = raft
+        self.shard_map = shard_map
+        self.shard_id = shard_id
+        self.monitor = monitor
+        self.pool = pool
+        self.advertise_addr = advertise_addr
+        self.access_stats = access_stats
+        self._access_buf: dict[str, int] = {}
+        self._access_flush_ms = access_stats_flush_ms
+        self._access_task: asyncio.Task | None = None
+        self.requests = 0
+
+    # ------------------------------------------------------------------ guards
+    def check_shard_ownership(self, path: str) -> None:
+        target = self.shard_map.get_shard(path)
+        if target is not None and target != self.shard_id:
+            peers = self.shard_map.get_shard_peers(target) or []
+            raise RpcStatus(StatusCode.OUT_OF_RANGE, f"REDIRECT:{peers[0] if peers else ''}")
+
+    def check_safe_mode(self) -> None:
+        if self.state.safe_mode:
+            raise RpcStatus(StatusCode.UNAVAILABLE, SAFE_MODE_MSG)
+
+    async def ensure_linearizable_read(self) -> None:
+        try:
+            await self.raft.read_index()
+        except NotLeader as e:
+            raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"Not Leader|{e.hint}" if e.hint else "Not Leader")
+
+    async def _propose(self, name: str, args: dict):
+        return await self.raft.propose({"Master": {name: args}})
+
+    # ------------------------------------------------------------------ access stats
+    def _record_access(self, path: str) -> None:
+        """The reference fires one Raft write per GetFileInfo (master.rs:2187-2209). Same
+        semantics (last_access_ms, access_count) but coalesced: reads within a short
+        window become one replicated UpdateAccessStats per path."""
+        if not self.access_stats or not self.raft.is_leader():
+            return
+        self._access_buf[path] = self._access_buf.get(path, 0) + 1
+        if self._access_task is None or self._access_task.done():
+            self._access_task = asyncio.get_running_loop().create_task(self._flush_access())
+
+    async def _flush_access(self) -> None:
+        await asyncio.sleep(self._access_flush_ms / 1000.0)
+        buf, self._access_buf = self._access_buf, {}
+        t = now_ms()
+        for path, count in buf.items():
+            for _ in range(count):
+                self.raft.propose_nowait({"Master": {"UpdateAccessStats": {"path": path, "accessed_at_ms": t}}})
+
+    # ------------------------------------------------------------------ file operations
+    async def get_file_info(self, req, ctx):
+        self.monitor.record_request(req.path)
+        self._record_access(req.path)
+        self.check_shard_ownership(req.path)
+        await self.ensure_linearizable_read()
+        m = self.state.files.get(req.path)
+        if m is None:
+            return pb.GetFileInfoResponse(found=False)
+        return pb.GetFileInfoResponse(metadata=m, found=True)
+
+    async def create_file(self, req, ctx):
+        self.monitor.record_request(req.path)
+        self.check_shard_ownership(req.path)
+        self.check_safe_mode()
+        if req.path in self.state.files:
+            return pb.CreateFileResponse(success=False, error_message="File already exists")
+        try:
+            await self._propose("CreateFile", {"path": req.path, "ec_data_shards": req.ec_data_shards,
+                                               "ec_parity_shards": req.ec_parity_shards})
+        except NotLeader as e:
+            return pb.CreateFileResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return pb.CreateFileResponse(success=True)
+
+    async def delete_file(self, req, ctx):
+        self.monitor.record_request(req.path)
+        self.check_shard_ownership(req.path)
+        self.check_safe_mode()
+        m = self.state.files.get(req.path)
+        if m is None:
+            return pb.DeleteFileResponse(success=False, error_message="File not found")
+        blocks = [(b.block_id, list(b.locations)) for b in m.blocks]
+        try:
+            await self._propose("DeleteFile", {"path": req.path})
+        except NotLeader as e:
+            return pb.DeleteFileResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        self._queue_block_gc(blocks)
+        return pb.DeleteFileResponse(success=True)
+
+    def _queue_block_gc(self, blocks) -> None:
+        """Extension: issue DELETE commands for blocks no file references any more (the
+        reference never garbage-collects blocks; proto DELETE is 'future use')."""
+        T = pb.ChunkServerCommand
+        for bid, locs in blocks:
+            if bid in self.state.block_index:
+                continue
+            for loc in locs:
+                self.state.pending_commands.setdefault(loc, []).append(T(type=T.DELETE, block_id=bid))
+
+    async def allocate_block(self, req, ctx):
+        self.monitor.record_request(req.path)
+        self.check_shard_ownership(req.path)
+        self.check_safe_mode()
+        m = self.state.files.get(req.path)
+        if m is None:
+            raise RpcStatus(StatusCode.NOT_FOUND, "File not found")
+        ec_d, ec_p = m.ec_data_shards, m.ec_parity_shards
+        cands = list(self.state.chunk_servers.items())
+        if ec_d > 0 and ec_p > 0:
+            total = ec_d + ec_p
+            if len(cands) < total:
+                raise RpcStatus(StatusCode.UNAVAILABLE,
+                                f"Need {total} chunk servers for EC({ec_d},{ec_p}), only {len(cands)} available")
+            needed = total
+        else:
+            needed = min(REPLICATION_FACTOR, len(cands))
+        if needed == 0:
+            raise RpcStatus(StatusCode.UNAVAILABLE, "No chunk servers available")
+        preferred = req.preferred_chunk_server if not (ec_d > 0 and ec_p > 0) else None
+        selected = select_servers_rack_aware(cands, needed, preferred or None)
+        for a in selected:
+            self.state.chunk_servers[a].scheduled += SCHEDULE_QUANTUM
+        block_id = str(uuid.uuid4())
+        try:
+            await self._propose("AllocateBlock", {"path": req.path, "block_id": block_id, "locations": selected})
+        except NotLeader as e:
+            return pb.AllocateBlockResponse(leader_hint=e.hint)
+        blk = pb.BlockInfo(block_id=block_id, locations=selected, ec_data_shards=ec_d, ec_parity_shards=ec_p)
+        return pb.AllocateBlockResponse(block=blk, chunk_server_addresses=selected, ec_data_shards=ec_d,
+                                        ec_parity_shards=ec_p, master_term=self.raft.current_term)
+
+    async def complete_file(self, req, ctx):
+        self.check_shard_ownership(req.path)
+        args = {"path": req.path, "size": req.size,
+                "etag_md5": req.etag_md5 or None, "created_at_ms": req.created_at_ms or None,
+                "block_checksums": [M.checksum_to_dict(c) for c in req.block_checksums]}
+        try:
+            await self._propose("CompleteFile", args)
+        except NotLeader:
+            return pb.CompleteFileResponse(success=False)
+        return pb.CompleteFileResponse(success=True)
+
+    async def list_files(self, req, ctx):
+        await self.ensure_linearizable_read()
+        prefix = req.path
+        if not prefix:
+            files = list(self.state.files)
+        else:
+            files = [p for p in self.state.files if p.startswith(prefix)]
+        return pb.ListFilesResponse(files=files)
+
+    async def register_chunk_server(self, req, ctx):
+        self.state.chunk_servers[req.address] = ChunkServerStatus(
+            last_heartbeat=now_ms(), available_space=req.capacity, rack_id=req.rack_id)
+        return pb.RegisterChunkServerResponse(success=True)
+
+    async def heartbeat(self, req, ctx):
+        st = self.state
+        addr = req.chunk_server_address
+        is_new = addr not in st.chunk_servers
+        rack = req.rack_id or (st.chunk_servers[addr].rack_id if addr in st.chunk_servers else "")
+        st.chunk_servers[addr] = ChunkServerStatus(
+            last_heartbeat=now_ms(), used_space=req.used_space, available_space=req.available_space,
+            chunk_count=req.chunk_count, rack_id=rack, gpu_rank=req.gpu_rank,
+            hbm_capacity=req.hbm_capacity, hbm_used=req.hbm_used)
+        for bid in req.new_blocks:  # ext: replicas created by REPLICATE / reconstruction
+            self.raft.propose_nowait({"Master": {"AddBlockLocation": {"block_id": bid, "address": addr}}})
+        if st.safe_mode and is_new:
+            st.update_reported_blocks(req.chunk_count)
+        if st.safe_mode and st.should_exit_safe_mode():
+            st.exit_safe_mode()
+        if req.bad_blocks:
+            log.warning("heartbeat: %d bad block(s) reported by %s", len(req.bad_blocks), addr)
+            for bid in req.bad_blocks:
+                st.bad_block_locations.setdefault(bid, set()).add(addr)
+            st.heal_under_replicated_blocks()
+        cmds = st.pending_commands.pop(addr, [])
+        return pb.HeartbeatResponse(success=True, commands=cmds, master_term=self.raft.current_term)
+
+    async def get_block_locations(self, req, ctx):
+        await self.ensure_linearizable_read()
+        _, b = self.state.find_block(req.block_id)
+        if b is None:
+            return pb.GetBlockLocationsResponse(found=False)
+        return pb.GetBlockLocationsResponse(locations=list(b.locations), found=True)
+
+    # ------------------------------------------------------------------ rename / 2PC
+    async def rename(self, req, ctx):
+        src, dst = req.source_path, req.dest_path
+        self.monitor.record_request(src)
+        self.check_shard_ownership(src)
+        self.check_safe_mode()
+        src_shard = self.shard_map.get_shard(src) or self.shard_id
+        dst_shard = self.shard_map.get_shard(dst) or self.shard_id
+        dst_peers = self.shard_map.get_shard_peers(dst_shard) or []
+        meta = self.state.files.get(src)
+        if meta is None:
+            return pb.RenameResponse(success=False, error_message=f"Source file not found: {src}")
+        if src_shard == dst_shard:
+            try:
+                await self._propose("RenameFile", {"source_path": src, "dest_path": dst})
+            except NotLeader as e:
+                return pb.RenameResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+            return pb.RenameResponse(success=True)
+        tx_id = str(uuid.uuid4())
+        dmeta = pb.FileMetadata()
+        dmeta.CopyFrom(meta)
+        dmeta.path = dst
+        rec = new_rename_record(tx_id, src, dst, src_shard, dst_shard, dmeta)
+        try:
+            await self._propose("CreateTransactionRecord", {"record": rec})
+        except NotLeader as e:
+            return pb.RenameResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        try:
+            await self._propose("UpdateTransactionState", {"tx_id": tx_id, "new_state": "Prepared"})
+        except Exception:  # noqa: BLE001
+            await self.send_abort(tx_id, dst_peers)
+            return pb.RenameResponse(success=False, error_message="Internal error: Raft commit failed")
+        ok = await self.send_prepare(tx_id, dst, dmeta, dst_peers)
+        if not ok:
+            await self.send_abort(tx_id, dst_peers)
+            try:
+                await self._propose("UpdateTransactionState", {"tx_id": tx_id, "new_state": "Aborted"})
+            except Exception:  # noqa: BLE001
+                pass
+            return pb.RenameResponse(success=False, error_message="Cross-shard prepare failed")
+        if not await self.send_commit(tx_id, dst_peers):
+            log.warning("commit RPC failed for tx %s; recovery task will retry", tx_id)
+            return pb.RenameResponse(success=False, error_message="Cross-shard commit pending, will be retried")
+        await self._finish_coordinator_commit(tx_id, src_shard, src)
+        return pb.RenameResponse(success=True)
+
+    async def _finish_coordinator_commit(self, tx_id: str, src_shard: str, src: str) -> None:
+        try:
+            await self._propose("ApplyTransactionOperation", {
+                "tx_id": tx_id, "operation": {"shard_id": src_shard, "op_type": {"Delete": {"path": src}}}})
+            await self._propose("UpdateTransactionState", {"tx_id": tx_id, "new_state": "Committed"})
+            await self._propose("SetParticipantAcked", {"tx_id": tx_id})
+        except Exception as e:  # noqa: BLE001
+            log.error("tx %s: coordinator finish failed: %s", tx_id, e)
+
+    async def _call_peers(self, peers: list[str], method: str, request, ok) -> bool:
+        """Try each peer of the shard, following ``leader_hint`` on Not Leader."""
+        tried: set[str] = set()
+        queue = list(peers)
+        while queue:
+            addr = queue.pop(0)
+            if addr in tried or not addr:
+                continue
+            tried.add(addr)
+            try:
+                resp = await self.pool.call(addr, "MasterService", method, request, timeout=5.0)
+            except Exception as e:  # noqa: BLE001
+                log.debug("%s to %s failed: %s", method, addr, rpc_details(e))
+                continue
+            if ok(resp):
+                return True
+            hint = getattr(resp, "leader_hint", "")
+            if hint and hint not in tried:
+                queue.insert(0, hint)
+            elif getattr(resp, "error_message", "") not in ("Not Leader", ""):
+                return False
+        return False
+
+    async def send_prepare(self, tx_id, path, meta, peers) -> bool:
+        req = pb.PrepareTransactionRequest(tx_id=tx_id, operation_type="CREATE", path=path, metadata=meta,
+                                           coordinator_shard=self.shard_id,
+                                           coordinator_peers=self.shard_map.get_shard_peers(self.shard_id) or [])
+        return await self._call_peers(peers, "PrepareTransaction", req, lambda r: r.success)
+
+    async def send_commit(self, tx_id, peers) -> bool:
+        return await self._call_peers(peers, "CommitTransaction", pb.CommitTransactionRequest(tx_id=tx_id),
+                                      lambda r: r.success)
+
+    async def send_abort(self, tx_id, peers) -> bool:
+        return await self._call_peers(peers, "AbortTransaction", pb.AbortTransactionRequest(tx_id=tx_id),
+                                      lambda r: r.success)
+
+    async def prepare_transaction(self, req, ctx):
+        if req.tx_id in self.state.transaction_records:
+            return pb.PrepareTransactionResponse(success=True)
+        self.check_shard_ownership(req.path)
+        if req.path in self.state.files:
+            return pb.PrepareTransactionResponse(success=False,
+                                                 error_message=f"Destination file already exists: {req.path}")
+        meta = req.metadata if req.HasField("metadata") else pb.FileMetadata()
+        rec = {
+            "tx_id": req.tx_id, "tx_type": {"Rename": {"source_path": "", "dest_path": req.path}},
+            "state": "Prepared", "timestamp": now_ms(), "participants": [req.coordinator_shard, self.shard_id],
+            "operations": [{"shard_id": self.shard_id,
+                            "op_type": {"Create": {"path": req.path, "metadata": M.file_to_dict(meta)}}}],
+            "coordinator_shard": req.coordinator_shard, "participant_acked": False, "inquiry_count": 0,
+            "coordinator_peers": list(req.coordinator_peers),
+        }
+        try:
+            await self._propose("CreateTransactionRecord", {"record": rec})
+        except NotLeader as e:
+            return pb.PrepareTransactionResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return pb.PrepareTransactionResponse(success=True)
+
+    async def commit_transaction(self, req, ctx):
+        rec = self.state.transaction_records.get(req.tx_id)
+        if rec is not None and rec["state"] == "Committed":
+            return pb.CommitTransactionResponse(success=True)
+        if rec is None or not rec.get("operations"):
+            return pb.CommitTransactionResponse(success=False, error_message=f"Transaction not found: {req.tx_id}")
+        try:
+            await self._propose("ApplyTransactionOperation", {"tx_id": req.tx_id, "operation": rec["operations"][0]})
+        except NotLeader as e:
+            return pb.CommitTransactionResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        try:
+            await self._propose("UpdateTransactionState", {"tx_id": req.tx_id, "new_state": "Committed"})
+        except Exception:  # noqa: BLE001
+            pass
+        return pb.CommitTransactionResponse(success=True)
+
+    async def abort_transaction(self, req, ctx):
+        try:
+            await self._propose("UpdateTransactionState", {"tx_id": req.tx_id, "new_state": "Aborted"})
+        except NotLeader as e:
+            return pb.AbortTransactionResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return pb.AbortTransactionResponse(success=True)
+
+    async def inquire_transaction(self, req, ctx):
+        await self.ensure_linearizable_read()
+        rec = self.state.transaction_records.get(req.tx_id)
+        status = "UNKNOWN"
+        if rec is not None:
+            status = {"Committed": "COMMITTED", "Aborted": "ABORTED"}.get(rec["state"], "UNKNOWN")
+        return pb.InquireTransactionResponse(status=status)
+
+    # ------------------------------------------------------------------ safe mode
+    async def get_safe_mode_status(self, req, ctx):
+        await self.ensure_linearizable_read()
+        st = self.state
+        return pb.GetSafeModeStatusResponse(
+            is_safe_mode=st.safe_mode, is_manual=st.safe_mode_manual, chunk_server_count=len(st.chunk_servers),
+            expected_blocks=st.expected_block_count, reported_blocks=st.reported_block_count,
+            threshold=st.safe_mode_threshold, entered_at=st.safe_mode_entered_at)
+
+    async def set_safe_mode(self, req, ctx):
+        if req.enter:
+            self.state.force_enter_safe_mode()
+        else:
+            self.state.force_exit_safe_mode()
+        return pb.SetSafeModeResponse(success=True, is_safe_mode=self.state.safe_mode)
+
+    # ------------------------------------------------------------------ membership
+    async def add_raft_server(self, req, ctx):
+        try:
+            await self.raft.add_server(req.server_id, req.server_address)
+        except NotLeader as e:
+            return pb.AddRaftServerResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return pb.AddRaftServerResponse(success=True)
+
+    async def remove_raft_server(self, req, ctx):
+        if not self.raft.is_leader():
+            return pb.RemoveRaftServerResponse(success=False, error_message="Not Leader",
+                                               leader_hint=self.raft.leader_address or "")
+        if len(self.raft.config.voters()) <= 1:
+            return pb.RemoveRaftServerResponse(success=False,
+                                               error_message="Cannot remove server: would leave cluster empty")
+        try:
+            await self.raft.remove_server(req.server_id)
+        except NotLeader as e:
+            return pb.RemoveRaftServerResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return pb.RemoveRaftServerResponse(success=True)
+
+    async def get_cluster_info(self, req, ctx):
+        info = self.raft.cluster_info()
+        members = [pb.ClusterMember(server_id=i, address=a, is_self=(i == self.raft.id))
+                   for i, a in sorted(self.raft.config.all_members().items())]
+        return pb.GetClusterInfoResponse(
+            node_id=info["node_id"], role=info["role"], current_term=info["current_term"],
+            leader_id=info["leader_id"] or 0, leader_address=info["leader_address"] or "", members=members,
+            commit_index=info["commit_index"], last_applied=info["last_applied"])
+
+    # ------------------------------------------------------------------ sharding
+    async def ingest_metadata(self, req, ctx):
+        prefix = None
+        if req.files:
+            p = req.files[0].path
+            if "/" in p:
+                prefix = p[: p.rfind("/") + 1]
+        try:
+            await self._propose("IngestBatch", {"files": [M.file_to_dict(f) for f in req.files]})
+        except NotLeader as e:
+            return pb.IngestMetadataResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        if prefix:
+            self.raft.propose_nowait({"Master": {"TriggerShuffle": {"prefix": prefix}}})
+        return pb.IngestMetadataResponse(success=True)
+
+    async def initiate_shuffle(self, req, ctx):
+        self.check_shard_ownership(req.prefix)
+        self.check_safe_mode()
+        try:
+            await self._propose("TriggerShuffle", {"prefix": req.prefix})
+        except NotLeader as e:
+            return pb.InitiateShuffleResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        return pb.InitiateShuffleResponse(success=True)

@@ -1,0 +1,22 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, 1-GPU bench (nvme-sync + hbm-ack) and a
+# rocprofv3 kernel-trace of the ChunkServer during the bench. Every GPU step has its own
+# timeout and the steps are chained with && so the first failure ends the session.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+STEP=${1:-all}
+rocm-smi --showproductname > gpurun_out/rocm_smi.txt 2>&1 || true
+if [ "$STEP" = "all" ] || [ "$STEP" = "test" ]; then
+  timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && \
+  timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || exit $?
+fi
+if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
+  timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/bench_nvme.json 2> gpurun_out/bench_nvme.err && \
+  timeout -k 10 600 python bench.py --steps 5 --warmup 1 --durability hbm-ack > gpurun_out/bench_hbm.json 2> gpurun_out/bench_hbm.err || exit $?
+fi
+if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
+  timeout -k 10 600 python bench.py --steps 3 --warmup 1 --profile-dir gpurun_out/prof > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit $?
+fi
+echo "gpu_round done"
