@@ -1,0 +1,85 @@
+"""CRC-32/IEEE and Reed-Solomon numerics (reference: chunkserver.rs:182-190, erasure.rs tests)."""
+import os
+import random
+import struct
+import zlib
+
+import pytest
+
+from rust_hadoop_generated_by_llm_amd.ops import crc as C
+from rust_hadoop_generated_by_llm_amd.ops import erasure as E
+
+
+def test_crc_golden():
+    assert C.crc32(b"123456789") == 0xCBF43926
+    assert C.crc32(b"") == 0
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 16, 17, 63, 64, 65, 127, 511, 512, 513, 1023, 4096, 65537, (1 << 20) + 3])
+def test_crc_matches_zlib(n):
+    d = os.urandom(n)
+    assert C.crc32(d) == zlib.crc32(d)
+    assert C.crc32(d[n // 2:], C.crc32(d[: n // 2])) == zlib.crc32(d)
+
+
+@pytest.mark.parametrize("n", [0, 1, 511, 512, 513, 2048, 100_000])
+def test_meta_image_format(n):
+    d = os.urandom(n)
+    meta = C.meta_image(d)
+    assert len(meta) == 4 * ((n + 511) // 512)
+    assert meta == b"".join(struct.pack(">I", zlib.crc32(d[i:i + 512])) for i in range(0, n, 512))
+    assert C.parse_meta(meta) == [zlib.crc32(d[i:i + 512]) for i in range(0, n, 512)]
+    assert C.crc32_from_meta(meta, n) == zlib.crc32(d)
+
+
+def test_crc_combine():
+    a, b = os.urandom(1234), os.urandom(4321)
+    assert C.combine(zlib.crc32(a), zlib.crc32(b), len(b)) == zlib.crc32(a + b)
+
+
+def test_rs_matrix_is_systematic_vandermonde():
+    from rust_hadoop_generated_by_llm_amd.native import lib
+
+    m = lib.rs_matrix(2, 2)
+    assert m == [[1, 0], [0, 1], [3, 2], [2, 3]]
+    m63 = lib.rs_matrix(6, 3)
+    assert m63[:6] == [[int(i == j) for j in range(6)] for i in range(6)]
+
+
+def test_encode_decode_round_trip():
+    data = b"Hello, erasure coding world! " * 10
+    shards = E.encode(data, 4, 2)
+    assert len(shards) == 6 and len({len(s) for s in shards}) == 1
+    assert E.decode(list(shards), 4, 2, len(data)) == data
+
+
+def test_decode_with_two_missing():
+    data = bytes(range(256)) * 4
+    shards = E.encode(data, 4, 2)
+    shards = [None if i in (1, 4) else s for i, s in enumerate(shards)]
+    assert E.decode(shards, 4, 2, len(data)) == data
+
+
+def test_large_10k_and_random_losses():
+    data = os.urandom(10_000)
+    for k, m in [(2, 2), (4, 2), (6, 3), (10, 4)]:
+        shards = E.encode(data, k, m)
+        for _ in range(5):
+            lost = set(random.sample(range(k + m), m))
+            rebuilt = E.reconstruct([None if i in lost else s for i, s in enumerate(shards)], k, m)
+            assert rebuilt == shards
+
+
+def test_too_few_shards():
+    shards = E.encode(b"abcdefgh", 2, 2)
+    with pytest.raises(E.ErasureError):
+        E.decode([shards[0], None, None, None], 2, 2, 8)
+
+
+def test_shard_len_and_errors():
+    assert E.shard_len(10, 3) == 4
+    assert E.shard_len(9, 3) == 3
+    with pytest.raises(E.ErasureError):
+        E.encode(b"", 2, 2)
+    with pytest.raises(E.ErasureError):
+        E.encode(b"x", 0, 2)
