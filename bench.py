@@ -4,7 +4,9 @@
 
 One rank per GPU (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``):
 * every rank starts a ChunkServer process bound to its GPU (HBM chunk store + CDNA4
-  CRC kernels + RCCL replication rank r of N); rank 0 also starts the metadata master;
+  CRC kernels + RCCL replication rank r of N) and a metadata master for namespace
+  shard r (single-node Raft group, as in the reference's compose topology); the shard
+  map routes ``/bench_r<r>/...`` to shard r, every chunkserver heartbeats to every master;
 * every rank runs the reference benchmark client against its local ChunkServer:
   per step, 100 random 1 MiB files are written (CreateFile -> AllocateBlock ->
   WriteBlock chain with RF = min(3, N) -> CompleteFile) and then read back in full;
@@ -32,6 +34,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "dfs_cli benchmark write+read MB/s & p50 lat, 1MB\u00d7100 conc=10, 1/2/4/8 GPUs"
+PKG = "rust_hadoop_generated_by_llm_amd"
 
 
 def parse():
@@ -45,6 +48,8 @@ def parse():
     p.add_argument("--durability", choices=["nvme-sync", "hbm-ack"], default="nvme-sync")
     p.add_argument("--hbm-capacity", default="32G")
     p.add_argument("--transport", choices=["rccl", "grpc"], default="rccl")
+    p.add_argument("--shards", choices=["per-gpu", "one"], default="per-gpu",
+                   help="metadata shards: one per GPU rank (default) or a single master")
     p.add_argument("--cpu", action="store_true", help="CPU chunk store (plumbing config 1)")
     p.add_argument("--workdir", default=None)
     p.add_argument("--timeout", type=float, default=1500.0)
@@ -72,8 +77,8 @@ class Procs:
 
     def spawn_raw(self, cmd: list[str], log: str, env: dict) -> subprocess.Popen:
         f = open(log, "ab")
-        p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, env=env,
-                             cwd=str(ROOT), start_new_session=True)
+        p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, env=env, cwd=str(ROOT),
+                             start_new_session=True)
         f.close()
         self.items.append(p)
         self.logs.append(log)
@@ -120,6 +125,10 @@ def wait_file(path: str, proc: subprocess.Popen, timeout: float, procs: Procs) -
         return json.load(f)
 
 
+def prefix_of(rank: int) -> str:
+    return f"/bench_r{rank:03d}"
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -135,6 +144,13 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")
 
+    def gather(obj):
+        if world == 1:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
     def bcast(obj):
         if world == 1:
             return obj
@@ -147,10 +163,10 @@ def main():
             dist.barrier()
 
     procs = Procs()
-    killed = threading.Event()
+    done = threading.Event()
 
     def watchdog():
-        if not killed.wait(a.timeout):
+        if not done.wait(a.timeout):
             print(f"bench watchdog: exceeded {a.timeout}s, tearing down", file=sys.stderr, flush=True)
             print(procs.tails(), file=sys.stderr, flush=True)
             procs.stop()
@@ -168,36 +184,48 @@ def main():
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE",
               "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
-    fs = []
-    result = None
     try:
-        # ---------------- master (rank 0)
-        if rank == 0:
-            gport, hport = free_port(), free_port()
-            ready = str(base_p / "master.ready")
-            menv = dict(env, DFS_READY_FILE=ready)
-            mp = procs.spawn(["rust_hadoop_generated_by_llm_amd.master.server", "--addr", f"127.0.0.1:{gport}",
-                              "--http-port", str(hport), "--storage-dir", str(base_p / "master"), *fs],
-                             str(base_p / "master.log"), menv)
-            wait_file(ready, mp, 300, procs)
-            master = f"http://127.0.0.1:{gport}"
+        # ---------------- metadata shards: shard r owns /bench_r<r>/...
+        per_gpu = a.shards == "per-gpu"
+        runs_master = per_gpu or rank == 0
+        gport, hport = (free_port(), free_port()) if runs_master else (0, 0)
+        ports = gather(gport)
+        if per_gpu:
+            shards = {f"shard-{r:03d}": [f"http://127.0.0.1:{ports[r]}"] for r in range(n)}
+            ranges = {prefix_of(r) + "/\U0010FFFF": f"shard-{r:03d}" for r in range(n - 1)}
+            ranges["\U0010FFFF"] = f"shard-{n - 1:03d}"
         else:
-            master = None
-        master = bcast(master)
+            shards = {"shard-000": [f"http://127.0.0.1:{ports[0]}"]}
+            ranges = {"\U0010FFFF": "shard-000"}
+        shard_file = base_p / "shard_config.json"
+        if rank == 0:
+            shard_file.write_text(json.dumps({"shards": shards, "ranges": ranges}))
+        barrier()
+        if runs_master:
+            ready = str(base_p / f"master{rank}.ready")
+            mp = procs.spawn([f"{PKG}.master.server", "--addr", f"127.0.0.1:{gport}", "--http-port", str(hport),
+                              "--storage-dir", str(base_p / f"rank{rank}" / "master"),
+                              "--shard-id", f"shard-{rank:03d}", "--shard-config", str(shard_file)],
+                             str(base_p / f"master{rank}.log"), dict(env, DFS_READY_FILE=ready))
+            wait_file(ready, mp, 300, procs)
+        barrier()
+        my_master = f"http://127.0.0.1:{ports[rank if per_gpu else 0]}"
         # ---------------- chunkserver for this rank's GPU
         cport, chttp = free_port(), free_port()
         ready = str(base_p / f"cs{rank}.ready")
-        gpu = -1 if a.cpu else local_rank
-        args = ["rust_hadoop_generated_by_llm_amd.chunkserver.server", "--addr", f"127.0.0.1:{cport}",
+        ndev = torch.cuda.device_count() if not a.cpu else 0  # does not initialise HIP
+        gpu = -1 if a.cpu else local_rank % max(1, ndev)
+        shared_gpu = (not a.cpu) and ndev < n  # rehearsal mode: several ranks on one GPU
+        args = [f"{PKG}.chunkserver.server", "--addr", f"127.0.0.1:{cport}",
                 "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
                 "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
-                "--masters", master, "--heartbeat-interval", "0.5", "--scrub-interval", "3600", *fs]
-        if n > 1 and not a.cpu and a.transport == "rccl":
+                "--heartbeat-interval", "0.5", "--scrub-interval", "3600"]
+        if n > 1 and not a.cpu and a.transport == "rccl" and not shared_gpu:
             args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
                      str(base_p / "rccl_rdv")]
         else:
             args += ["--replication-transport", "grpc"]
-        cs_env = dict(env, DFS_READY_FILE=ready)
+        cs_env = dict(env, DFS_READY_FILE=ready, SHARD_CONFIG=str(shard_file))
         if a.profile_dir:
             # profile only the ChunkServer (where the kernels run); rocprofv3 is started
             # before anything in this process touches the GPU
@@ -209,20 +237,22 @@ def main():
                                  str(base_p / f"cs{rank}.log"), cs_env)
         else:
             cp = procs.spawn(args, str(base_p / f"cs{rank}.log"), cs_env)
-        cs_info = wait_file(ready, cp, 600, procs)
+        cs_info = wait_file(ready, cp, 900, procs)
         my_cs = f"127.0.0.1:{cport}"
 
         from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_read, bench_write, make_payloads
         from rust_hadoop_generated_by_llm_amd.client.client import Client
         from rust_hadoop_generated_by_llm_amd.models import proto as pb
+        from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
         from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
 
-        # wait until the master has registered every chunkserver and left safe mode
+        # wait until our shard's master has registered every chunkserver and left safe mode
         pool = ChannelPool()
         deadline = time.time() + 300
         while True:
             try:
-                st = pool.call(master, "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(), timeout=2)
+                st = pool.call(my_master, "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(),
+                               timeout=2)
                 if st.chunk_server_count >= n and not st.is_safe_mode:
                     break
             except Exception:  # noqa: BLE001
@@ -230,20 +260,21 @@ def main():
             if time.time() > deadline:
                 raise TimeoutError("master never registered all chunkservers")
             time.sleep(0.1)
+        pool.close()
         barrier()
 
-        client = Client([master], local_chunkserver=my_cs)
+        client = Client([my_master], local_chunkserver=my_cs)
+        client.set_shard_map(ShardMap.load_config_file(str(shard_file)))
         payloads = make_payloads(a.count, a.size)
         from concurrent.futures import ThreadPoolExecutor
 
         tpool = ThreadPoolExecutor(max_workers=a.concurrency, thread_name_prefix="bench")
 
         def step(tag: str):
-            ws, names = bench_write(client, a.count, a.size, a.concurrency, prefix=f"/bench_r{rank}",
+            ws, names = bench_write(client, a.count, a.size, a.concurrency, prefix=prefix_of(rank),
                                     payloads=payloads, run_id=tag, pool=tpool)
-            rs = bench_read(client, files=names, pool=tpool,
-                            verify={nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if tag == "w0"
-                            else None)
+            verify = {nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if tag == "w0" else None
+            rs = bench_read(client, files=names, pool=tpool, verify=verify)
             return ws, rs
 
         for w in range(a.warmup):
@@ -280,16 +311,9 @@ def main():
             stats = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
         except Exception:  # noqa: BLE001
             pass
-        mine = {"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt, "rt": rt,
-                "cs": stats, "rccl": cs_info.get("rccl", False)}
-        if world > 1:
-            allr = [None] * world
-            dist.all_gather_object(allr, mine)
-        else:
-            allr = [mine]
+        allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
+                       "rt": rt, "cs": stats, "rccl": cs_info.get("rccl", False)})
         if rank == 0:
-            import statistics
-
             tmax = max(r["elapsed"] for r in allr)
             tot = sum(r["wbytes"] + r["rbytes"] for r in allr)
             wlat = sorted(x for r in allr for x in r["wl"])
@@ -298,39 +322,41 @@ def main():
             def pct(v, p):
                 return 1e3 * v[min(len(v) - 1, len(v) * p // 100)] if v else 0.0
 
-            wbytes_all = sum(r["wbytes"] for r in allr)
-            rbytes_all = sum(r["rbytes"] for r in allr)
-            value = tot / (1 << 20) / tmax
+            wmax = max(r["wt"] for r in allr)
+            rmax = max(r["rt"] for r in allr)
             result = {
-                "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": n, "steps": a.steps,
-                "warmup": a.warmup, "ms_per_step": round(1e3 * tmax / a.steps, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "uint8", "data": "synthetic random bytes",
+                "metric": METRIC, "value": round(tot / (1 << 20) / tmax, 2), "unit": "MB/s", "n_gpus": n,
+                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * tmax / a.steps, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "uint8",
+                "data": "synthetic random bytes",
                 "config": {"model": "dfs_cli benchmark write+read (1 MiB files)", "global_batch": a.count * n,
-                           "seq_len": a.size, "parallelism": f"cs{n}",
+                           "seq_len": a.size, "parallelism": f"cs{n}-shards{n if per_gpu else 1}",
                            "files_per_gpu_per_step": a.count, "file_size": a.size, "concurrency": a.concurrency,
                            "replication_factor": min(3, n), "durability": a.durability,
-                           "store": "cpu" if a.cpu else "hbm", "transport": a.transport if n > 1 else "local"},
-                "write_mb_per_s": round(wbytes_all / (1 << 20) / max(r["wt"] for r in allr), 2),
-                "read_mb_per_s": round(rbytes_all / (1 << 20) / max(r["rt"] for r in allr), 2),
+                           "store": "cpu" if a.cpu else "hbm",
+                           "transport": ("grpc" if (a.cpu or shared_gpu) else a.transport) if n > 1 else "local"},
+                "write_mb_per_s": round(sum(r["wbytes"] for r in allr) / (1 << 20) / wmax, 2),
+                "read_mb_per_s": round(sum(r["rbytes"] for r in allr) / (1 << 20) / rmax, 2),
                 "write_p50_ms": round(pct(wlat, 50), 3), "write_p95_ms": round(pct(wlat, 95), 3),
                 "write_p99_ms": round(pct(wlat, 99), 3), "read_p50_ms": round(pct(rlat, 50), 3),
                 "read_p95_ms": round(pct(rlat, 95), 3), "read_p99_ms": round(pct(rlat, 99), 3),
-                "write_ops_per_s": round(len(wlat) / max(r["wt"] for r in allr), 1),
+                "write_ops_per_s": round(len(wlat) / wmax, 1),
                 "rccl_ranks": sum(1 for r in allr if r["rccl"]),
                 "rccl_forwards": sum(r["cs"].get("rccl_forwards", 0) for r in allr),
                 "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
+                "rccl_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) for r in allr),
                 "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
             }
-            _ = statistics
             print(json.dumps(result), flush=True)
         barrier()
         tpool.shutdown(wait=False)
         client.close()
     finally:
-        killed.set()
+        done.set()
         procs.stop()
         if world > 1:
             try:
+                dist.barrier()
                 dist.destroy_process_group()
             except Exception:  # noqa: BLE001
                 pass

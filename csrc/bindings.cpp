@@ -164,6 +164,30 @@ PYBIND11_MODULE(_dfs_native, m) {
         }
         return py::make_tuple(w.ok, w.actual_crc, w.error);
       }, py::arg("block_id"), py::arg("data"), py::arg("expected_crc") = 0)
+      .def("stage", [](ChunkStore& s, const std::string& id, py::buffer data, uint32_t expected) {
+        py::buffer_info k;
+        Buf v = view(data, k);
+        WriteResult w;
+        {
+          py::gil_scoped_release r;
+          w = s.stage(id, v.p, v.n, expected);
+        }
+        return py::make_tuple(w.ok, w.actual_crc, w.error);
+      }, py::arg("block_id"), py::arg("data"), py::arg("expected_crc") = 0)
+      .def("persist", [](ChunkStore& s, const std::string& id, py::object data) {
+        std::string err;
+        bool ok;
+        if (data.is_none()) {
+          py::gil_scoped_release r;
+          ok = s.persist(id, nullptr, 0, &err);
+        } else {
+          py::buffer_info k;
+          Buf v = view(data.cast<py::buffer>(), k);
+          py::gil_scoped_release r;
+          ok = s.persist(id, v.p, v.n, &err);
+        }
+        return py::make_tuple(ok, err);
+      }, py::arg("block_id"), py::arg("data") = py::none())
       .def("read", [](ChunkStore& s, const std::string& id, uint64_t offset, uint64_t length) -> py::tuple {
         ReadResult st;
         {
@@ -293,14 +317,16 @@ PYBIND11_MODULE(_dfs_native, m) {
         }
         return py::make_tuple(ok, err);
       })
-      .def("recv", [](RcclEngine& e, int src, int64_t seq, const std::string& id, uint64_t size, uint32_t crc) {
+      .def("recv", [](RcclEngine& e, int src, int64_t seq, const std::string& id, uint64_t size, uint32_t crc,
+                      bool persist) {
         WriteResult w;
         {
           py::gil_scoped_release r;
-          w = e.recv(src, seq, id, size, crc);
+          w = e.recv(src, seq, id, size, crc, persist);
         }
         return py::make_tuple(w.ok, w.actual_crc, w.error);
-      })
+      }, py::arg("src"), py::arg("seq"), py::arg("block_id"), py::arg("size"), py::arg("crc"),
+         py::arg("persist") = true)
       .def_property_readonly("bytes_sent", &RcclEngine::bytes_sent)
       .def_property_readonly("bytes_recv", &RcclEngine::bytes_recv);
 

@@ -430,6 +430,50 @@ bool ChunkStore::persist(const std::string& id, bool cold, const uint8_t* data, 
 // ---------------------------------------------------------------- write
 WriteResult ChunkStore::write(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
   if (!gpu()) return write_host(id, data, n, expected_crc);
+  return stage_impl(id, data, n, expected_crc, true);
+}
+
+WriteResult ChunkStore::stage(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
+  if (!gpu()) return write_host(id, data, n, expected_crc);
+  return stage_impl(id, data, n, expected_crc, false);
+}
+
+void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t crc, bool on_disk,
+                                 std::shared_ptr<std::vector<uint8_t>> meta) {
+  bool hbm_ack = cfg_.durability == Durability::HbmAck;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end()) {
+      cv_.wait(lk, [&] { return it->second.pins == 0; });
+      free_extent_locked(it->second);
+      lru_remove_locked(it->second);
+      if (it->second.cold) {  // the new version lives in the hot dir
+        ::unlink(data_path(id, true).c_str());
+        ::unlink(meta_path(id, true).c_str());
+      }
+    }
+    Block& b = index_[id];
+    b = Block{};
+    b.size = n;
+    b.crc = crc;
+    b.crc_known = true;
+    b.on_disk = on_disk;
+    b.dirty = !on_disk;
+    b.dev_off = ext.off;
+    b.dev_bytes = ext.bytes;
+    if (!on_disk && !hbm_ack) b.staged_meta = std::move(meta);
+    touch_locked(id, b);
+    if (!on_disk && hbm_ack) spill_q_.push_back(id);
+  }
+  cv_.notify_all();
+}
+
+// H2D (double-buffered pinned chunks) + fused K1/K2 kernel + D2H of the .meta image, then
+// verification against the client's whole-block CRC. With durable_now the data and .meta
+// are fdatasync'ed from the caller's host buffer before the block becomes visible.
+WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
+                                   bool durable_now) {
   HIP_OK(hipSetDevice(cfg_.device));
   WriteResult res;
   DevExtent ext = reserve(n);
@@ -468,41 +512,86 @@ WriteResult ChunkStore::write(const std::string& id, const uint8_t* data, uint64
                 std::to_string(co.block_crc);
     return res;
   }
-  bool durable = cfg_.durability == Durability::NvmeSync;
-  if (durable && !persist(id, false, data, n, hmeta, S, &err)) {
-    release_lane(l);
+  auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
+  release_lane(l);
+  bool sync_now = durable_now && cfg_.durability == Durability::NvmeSync;
+  if (sync_now && !persist(id, false, data, n, meta->data(), S, &err)) {
     release(ext);
     res.error = err;
     return res;
   }
-  release_lane(l);
-  {
-    std::unique_lock<std::mutex> lk(mu_);
-    auto it = index_.find(id);
-    if (it != index_.end()) {
-      cv_.wait(lk, [&] { return it->second.pins == 0; });
-      free_extent_locked(it->second);
-      lru_remove_locked(it->second);
-      if (it->second.cold && durable) {  // new version lives in the hot dir
-        ::unlink(data_path(id, true).c_str());
-        ::unlink(meta_path(id, true).c_str());
-      }
-    }
-    Block& b = index_[id];
-    b = Block{};
-    b.size = n;
-    b.crc = co.block_crc;
-    b.crc_known = true;
-    b.on_disk = durable;
-    b.dirty = !durable;
-    b.dev_off = ext.off;
-    b.dev_bytes = ext.bytes;
-    touch_locked(id, b);
-    if (!durable) spill_q_.push_back(id);
-  }
-  cv_.notify_all();
+  insert_resident(id, ext, n, co.block_crc, sync_now, meta);
   res.ok = true;
   return res;
+}
+
+bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64_t n, std::string* err) {
+  if (!gpu() || cfg_.durability == Durability::HbmAck) return true;
+  std::shared_ptr<std::vector<uint8_t>> meta;
+  const uint8_t* d = nullptr;
+  uint64_t size = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end()) {
+      *err = "Block not found";
+      return false;
+    }
+    Block& b = it->second;
+    if (!b.dirty) return true;
+    if (b.dev_off < 0 || !b.staged_meta) {
+      *err = "block not staged";
+      return false;
+    }
+    meta = b.staged_meta;
+    size = b.size;
+    d = arena_ + b.dev_off;
+    b.pins++;
+  }
+  bool ok;
+  if (host_data && n == size) ok = persist(id, false, host_data, size, meta->data(), meta->size() / 4, err);
+  else ok = persist_from_device(id, d, size, meta->data(), meta->size() / 4, err);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end()) {
+      it->second.pins--;
+      if (ok && it->second.staged_meta == meta) {
+        it->second.on_disk = true;
+        it->second.dirty = false;
+        it->second.staged_meta.reset();
+      }
+    }
+  }
+  cv_.notify_all();
+  return ok;
+}
+
+bool ChunkStore::persist_from_device(const std::string& id, const uint8_t* d, uint64_t n, const uint8_t* meta_be,
+                                     uint64_t nslices, std::string* err) {
+  HIP_OK(hipSetDevice(cfg_.device));
+  Lane* l = acquire_lane();
+  std::string dp = data_path(id, false);
+  int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  bool ok = fd >= 0;
+  uint64_t nch = (n + kChunk - 1) / kChunk;
+  for (uint64_t c = 0; ok && c < nch; ++c) {
+    uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
+    HIP_OK(hipMemcpyAsync(l->pinned[c & 1], d + off, len, hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+    ok = write_all(fd, l->pinned[c & 1], len, off);
+  }
+  if (ok && cfg_.sync_writes) ok = ::fdatasync(fd) == 0;
+  if (fd >= 0) ::close(fd);
+  release_lane(l);
+  if (ok) {
+    std::string mp = meta_path(id, false);
+    fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    ok = fd >= 0 && write_all(fd, meta_be, nslices * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
+    if (fd >= 0) ::close(fd);
+  }
+  if (!ok) *err = errno_str("persist " + id);
+  return ok;
 }
 
 WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
@@ -884,7 +973,7 @@ void ChunkStore::unpin(const std::string& id) {
 }
 
 WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t expected_crc,
-                                      hipStream_t s) {
+                                      hipStream_t s, bool persist_now) {
   WriteResult res;
   HIP_OK(hipSetDevice(cfg_.device));
   if (s) HIP_OK(hipStreamSynchronize(s));
@@ -900,70 +989,27 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
     HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
     HIP_OK(hipStreamSynchronize(l->stream));
   }
+  auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
+  release_lane(l);
   if (!ok) {
-    release_lane(l);
     release(ext);
     res.error = err;
     return res;
   }
   res.actual_crc = co.block_crc;
   if (expected_crc != 0 && co.block_crc != expected_crc) {
-    release_lane(l);
     release(ext);
     res.error = "Replication checksum mismatch: expected " + std::to_string(expected_crc) + ", actual " +
                 std::to_string(co.block_crc);
     return res;
   }
-  bool durable = cfg_.durability == Durability::NvmeSync;
-  if (durable) {
-    // Stream the block out of HBM chunk by chunk straight into the data file.
-    std::string dp = data_path(id, false);
-    int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-    bool wok = fd >= 0;
-    uint64_t nch = (n + kChunk - 1) / kChunk;
-    for (uint64_t c = 0; wok && c < nch; ++c) {
-      uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
-      HIP_OK(hipMemcpyAsync(l->pinned[c & 1], ext.ptr + off, len, hipMemcpyDeviceToHost, l->stream));
-      HIP_OK(hipStreamSynchronize(l->stream));
-      wok = write_all(fd, l->pinned[c & 1], len, off);
-    }
-    if (wok && cfg_.sync_writes) wok = ::fdatasync(fd) == 0;
-    if (fd >= 0) ::close(fd);
-    if (wok) {
-      std::string mp = meta_path(id, false);
-      fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-      wok = fd >= 0 && write_all(fd, hmeta, S * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
-      if (fd >= 0) ::close(fd);
-    }
-    if (!wok) {
-      release_lane(l);
-      release(ext);
-      res.error = errno_str("persist " + id);
-      return res;
-    }
+  bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
+  if (sync_now && !persist_from_device(id, ext.ptr, n, meta->data(), S, &err)) {
+    release(ext);
+    res.error = err;
+    return res;
   }
-  release_lane(l);
-  {
-    std::unique_lock<std::mutex> lk(mu_);
-    auto it = index_.find(id);
-    if (it != index_.end()) {
-      cv_.wait(lk, [&] { return it->second.pins == 0; });
-      free_extent_locked(it->second);
-      lru_remove_locked(it->second);
-    }
-    Block& b = index_[id];
-    b = Block{};
-    b.size = n;
-    b.crc = co.block_crc;
-    b.crc_known = true;
-    b.on_disk = durable;
-    b.dirty = !durable;
-    b.dev_off = ext.off;
-    b.dev_bytes = ext.bytes;
-    touch_locked(id, b);
-    if (!durable) spill_q_.push_back(id);
-  }
-  cv_.notify_all();
+  insert_resident(id, ext, n, co.block_crc, sync_now, meta);
   res.ok = true;
   return res;
 }

@@ -112,6 +112,13 @@ class ChunkStore {
   const StoreConfig& config() const { return cfg_; }
 
   WriteResult write(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
+  // Two-phase write used by pipelined chain replication: stage() lands the block in HBM
+  // and verifies it (the block is then readable and can be forwarded over RCCL while
+  // persist() makes it durable). persist() writes from `host_data` when given (no D2H),
+  // otherwise streams the block out of HBM. In hbm-ack mode persist() returns at once and
+  // the spill threads make the block durable.
+  WriteResult stage(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
+  bool persist(const std::string& id, const uint8_t* host_data, uint64_t n, std::string* err);
   // Resolves [offset, offset+length) against the block (length 0 = rest of block).
   ReadResult stat(const std::string& id, uint64_t offset, uint64_t length);
   ReadResult read_into(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out);
@@ -135,7 +142,7 @@ class ChunkStore {
   DevExtent reserve(uint64_t n);
   void release(const DevExtent& e);
   WriteResult commit_device(const std::string& id, const DevExtent& e, uint64_t n, uint32_t expected_crc,
-                            hipStream_t s);
+                            hipStream_t s, bool persist_now = true);
   // Pin a resident block (promoting it if needed) and return its device pointer.
   const uint8_t* pin_device(const std::string& id, uint64_t* size);
   void unpin(const std::string& id);
@@ -161,6 +168,7 @@ class ChunkStore {
     std::list<std::string>::iterator lru;
     bool in_lru = false;
     std::shared_ptr<std::vector<uint8_t>> host;  // host-mode cache
+    std::shared_ptr<std::vector<uint8_t>> staged_meta;  // BE .meta image awaiting persist()
   };
   struct Lane {
     hipStream_t stream = nullptr;
@@ -193,6 +201,12 @@ class ChunkStore {
   bool h2d_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n);
   bool d2h_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n);
   bool promote(const std::string& id, std::string* err);  // load from NVMe into HBM
+  WriteResult stage_impl(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
+                         bool durable_now);
+  void insert_resident(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t crc, bool on_disk,
+                       std::shared_ptr<std::vector<uint8_t>> meta);
+  bool persist_from_device(const std::string& id, const uint8_t* d, uint64_t n, const uint8_t* meta_be,
+                           uint64_t nslices, std::string* err);
   bool persist(const std::string& id, bool cold, const uint8_t* data, uint64_t n, const uint8_t* meta_be,
                uint64_t nslices, std::string* err);
   void spill_worker();

@@ -205,7 +205,8 @@ bool RcclEngine::wait_send(int peer, int64_t seq, std::string* err) {
   return ok;
 }
 
-WriteResult RcclEngine::recv(int src, int64_t seq, const std::string& id, uint64_t size, uint32_t expected_crc) {
+WriteResult RcclEngine::recv(int src, int64_t seq, const std::string& id, uint64_t size, uint32_t expected_crc,
+                             bool persist_now) {
   WriteResult res;
   Pair* p = pair(src, rank_);
   if (!p || p->broken) {
@@ -256,7 +257,7 @@ WriteResult RcclEngine::recv(int src, int64_t seq, const std::string& id, uint64
     return res;  // extent intentionally leaked: a late DMA may still land in it
   }
   bytes_recv_ += size;
-  return store_->commit_device(id, ext, size, expected_crc, nullptr);
+  return store_->commit_device(id, ext, size, expected_crc, nullptr, persist_now);
 }
 
 }  // namespace dfs

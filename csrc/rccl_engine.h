@@ -43,7 +43,8 @@ class RcclEngine {
   int64_t send(int peer, const std::string& id, uint64_t* size, std::string* err);
   bool wait_send(int peer, int64_t seq, std::string* err);
   // Receiver side: post the recv for `seq` in order, then verify + persist + index.
-  WriteResult recv(int src, int64_t seq, const std::string& id, uint64_t size, uint32_t expected_crc);
+  WriteResult recv(int src, int64_t seq, const std::string& id, uint64_t size, uint32_t expected_crc,
+                   bool persist_now = true);
   void abort_pair(int src, int dst);
   uint64_t bytes_sent() const { return bytes_sent_; }
   uint64_t bytes_recv() const { return bytes_recv_; }

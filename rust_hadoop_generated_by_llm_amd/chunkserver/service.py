@@ -44,6 +44,7 @@ class ChunkServer:
         self.new_blocks: list[str] = []
         self._lists_lock = threading.Lock()
         self._bg = ThreadPoolExecutor(max_workers=4, thread_name_prefix="cs-bg")
+        self._fwd = ThreadPoolExecutor(max_workers=64, thread_name_prefix="cs-fwd")
         self.metrics = metrics
         self.stats = {"writes": 0, "reads": 0, "replicas_in": 0, "rccl_forwards": 0, "grpc_forwards": 0,
                       "rccl_fallbacks": 0, "recoveries": 0}
@@ -116,27 +117,64 @@ class ChunkServer:
         return resp.replicas_written
 
     # ------------------------------------------------------------------ RPCs
+    def _store_and_forward(self, block_id: str, data: bytes | None, next_servers: list[str], crc: int, term: int,
+                           heal: bool, rccl_src: int = -1, rccl_seq: int = -1, rccl_size: int = 0):
+        """Local write + downstream forwarding, pipelined.
+
+        The reference writes+fsyncs locally and only then forwards (serial chain,
+        chunkserver.rs:777-819). Here the block is first *staged* (landed in HBM and
+        CRC-verified), then the forward to the next replica (RCCL send from HBM, or gRPC)
+        runs concurrently with the local fdatasync. The ack still waits for both, so the
+        durability contract (every counted replica is on NVMe) is unchanged while the
+        chain latency drops from sum(hops x (copy + 2 fsync)) to roughly one fsync.
+        Returns (ok, error, replicas_written)."""
+        if rccl_src >= 0:
+            ok, _crc, err = self.rccl.recv(rccl_src, rccl_seq, block_id, rccl_size, crc, persist=not next_servers)
+            staged_in_hbm = True
+        elif next_servers and self.store.gpu:
+            ok, _crc, err = self.store.stage(block_id, data, crc)
+            staged_in_hbm = True
+        elif next_servers:
+            # CPU store: forward and write at the same time (downstream re-verifies the CRC)
+            fut = self._fwd.submit(self.forward, block_id, data, next_servers, crc, term, heal)
+            ok, _crc, err = self.store.write(block_id, data, crc)
+            down = fut.result()
+            return ok, err, (1 + down) if ok else 0
+        else:
+            ok, _crc, err = self.store.write(block_id, data, crc)
+            return ok, err, 1 if ok else 0
+        if not ok:
+            return False, err, 0
+        if not next_servers:
+            return True, "", 1
+        fut = self._fwd.submit(self.forward, block_id, data, next_servers, crc, term, heal)
+        pok, perr = self.store.persist(block_id, data if rccl_src < 0 else None)
+        down = fut.result()
+        if not pok:
+            return False, perr, 0
+        _ = staged_in_hbm
+        return True, "", 1 + down
+
     def write_block(self, req, ctx):
         self.fence(req.master_term)
-        ok, _crc, err = self.store.write(req.block_id, req.data, req.expected_checksum_crc32c)
+        ok, err, replicas = self._store_and_forward(req.block_id, req.data, list(req.next_servers),
+                                                    req.expected_checksum_crc32c, req.master_term, False)
         if not ok:
             return pb.WriteBlockResponse(success=False, error_message=err)
         self.stats["writes"] += 1
-        replicas = 1
-        if req.next_servers:
-            replicas += self.forward(req.block_id, req.data, list(req.next_servers), req.expected_checksum_crc32c,
-                                     req.master_term)
         return pb.WriteBlockResponse(success=True, replicas_written=replicas)
 
     def replicate_block(self, req, ctx):
         self.fence(req.master_term)
+        if req.rccl and self.rccl is None:
+            return pb.ReplicateBlockResponse(success=False, error_message="RCCL transport not enabled")
         if req.rccl:
-            if self.rccl is None:
-                return pb.ReplicateBlockResponse(success=False, error_message="RCCL transport not enabled")
-            ok, _crc, err = self.rccl.recv(req.rccl_src_rank, req.rccl_seq, req.block_id, req.rccl_size,
-                                           req.expected_checksum_crc32c)
+            ok, err, replicas = self._store_and_forward(req.block_id, None, list(req.next_servers),
+                                                        req.expected_checksum_crc32c, req.master_term, req.heal,
+                                                        req.rccl_src_rank, req.rccl_seq, req.rccl_size)
         else:
-            ok, _crc, err = self.store.write(req.block_id, req.data, req.expected_checksum_crc32c)
+            ok, err, replicas = self._store_and_forward(req.block_id, req.data, list(req.next_servers),
+                                                        req.expected_checksum_crc32c, req.master_term, req.heal)
         if not ok:
             if err.startswith("Checksum mismatch"):
                 err = "Replication c" + err[1:]
@@ -145,11 +183,6 @@ class ChunkServer:
         if req.heal:
             with self._lists_lock:
                 self.new_blocks.append(req.block_id)
-        replicas = 1
-        if req.next_servers:
-            data = None if req.rccl else req.data
-            replicas += self.forward(req.block_id, data, list(req.next_servers), req.expected_checksum_crc32c,
-                                     req.master_term, req.heal)
         return pb.ReplicateBlockResponse(success=True, replicas_written=replicas)
 
     def read_block(self, req, ctx):

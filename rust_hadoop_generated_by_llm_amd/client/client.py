@@ -259,7 +259,10 @@ class Client:
         block = alloc.block
         servers = list(alloc.chunk_server_addresses)
         crc = crcops.crc32(data)
-        etag = hashlib.md5(data).hexdigest()
+        # MD5 is a strictly sequential chain (one core per object): run it while the block
+        # is on the wire instead of before it (hashlib releases the GIL); it is only
+        # needed for CompleteFile.
+        md5_fut = self._exec.submit(lambda: hashlib.md5(data).hexdigest())
         req = pb.WriteBlockRequest(block_id=block.block_id, data=data, next_servers=servers[1:],
                                    expected_checksum_crc32c=crc, shard_index=-1, master_term=alloc.master_term)
         try:
@@ -267,6 +270,7 @@ class Client:
                                   timeout=self.data_timeout)
         except grpc.RpcError as e:
             raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
+        etag = md5_fut.result()
         if not resp.success:
             raise DfsError(f"Failed to write block: {resp.error_message}")
         if resp.replicas_written < len(servers):

@@ -46,12 +46,17 @@ class ShardMap:
         return cls("range")
 
     @classmethod
-    def from_config(cls, shards: dict[str, list[str]]) -> "ShardMap":
+    def from_config(cls, shards: dict[str, list[str]], ranges: dict[str, str] | None = None) -> "ShardMap":
         """Shard JSON config ``{"shards": {id: [peers]}}``: sorted ids added to a Range map
-        (reference ShardConfig::to_shard_map, sharding.rs:288-296)."""
+        (reference ShardConfig::to_shard_map, sharding.rs:288-296). Extension: an optional
+        ``"ranges": {end_key: shard_id}`` gives explicit boundaries instead of the
+        order-dependent bootstrap (used to give each writer prefix its own shard)."""
         m = cls.new_range()
         for sid in sorted(shards):
             m.add_shard(sid, list(shards[sid]))
+        if ranges:
+            m.ranges = {k: v for k, v in ranges.items() if v in m.shards}
+            m._dirty()
         return m
 
     @classmethod
@@ -59,7 +64,8 @@ class ShardMap:
         if path:
             try:
                 with open(path) as f:
-                    return cls.from_config(json.load(f)["shards"])
+                    cfg = json.load(f)
+                return cls.from_config(cfg["shards"], cfg.get("ranges"))
             except (OSError, ValueError, KeyError):
                 pass
         return cls.new_consistent_hash(virtual_nodes)

@@ -19,4 +19,9 @@ fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
   timeout -k 10 600 python bench.py --steps 3 --warmup 1 --profile-dir gpurun_out/prof > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit $?
 fi
+if [ "$STEP" = "multi" ]; then
+  # N=2 rehearsal on a single GPU: two ranks share the device, gRPC replication
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > gpurun_out/bench_n2_shared.json 2> gpurun_out/bench_n2_shared.err || exit $?
+fi
 echo "gpu_round done"
