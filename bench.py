@@ -281,7 +281,7 @@ def main():
             step(f"w{w}")
         use_cuda = torch.cuda.is_available() and not a.cpu
         if use_cuda:
-            torch.cuda.set_device(local_rank)
+            torch.cuda.set_device(gpu)
             torch.cuda.synchronize()
         barrier()
         if use_cuda:

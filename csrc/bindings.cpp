@@ -208,6 +208,29 @@ PYBIND11_MODULE(_dfs_native, m) {
         return py::make_tuple(static_cast<int>(rr.status), rr.total_size, out, rr.partial_corrupt, rr.bad_slice,
                               rr.error);
       }, py::arg("block_id"), py::arg("offset") = 0, py::arg("length") = 0)
+      .def("read_into", [](ChunkStore& s, const std::string& id, uint64_t offset, uint64_t length,
+                           py::buffer out) -> py::tuple {
+        // Zero-copy read into a caller-owned writable buffer (short-circuit shm slot).
+        py::buffer_info bi = out.request(true);
+        ReadResult st;
+        {
+          py::gil_scoped_release r;
+          st = s.stat(id, offset, length);
+        }
+        if (st.status != ReadStatus::Ok)
+          return py::make_tuple(static_cast<int>(st.status), st.total_size, (uint64_t)0, false, (int64_t)-1,
+                                st.error);
+        if (static_cast<uint64_t>(bi.size * bi.itemsize) < st.bytes)
+          return py::make_tuple(static_cast<int>(ReadStatus::IoError), st.total_size, (uint64_t)0, false,
+                                (int64_t)-1, std::string("destination buffer too small"));
+        ReadResult rr;
+        {
+          py::gil_scoped_release r;
+          rr = s.read_into(id, offset, st.bytes, static_cast<uint8_t*>(bi.ptr));
+        }
+        return py::make_tuple(static_cast<int>(rr.status), rr.total_size, rr.bytes, rr.partial_corrupt,
+                              rr.bad_slice, rr.error);
+      }, py::arg("block_id"), py::arg("offset"), py::arg("length"), py::arg("out"))
       .def("exists", &ChunkStore::exists)
       .def("size", &ChunkStore::block_size)
       .def("crc", &ChunkStore::block_crc, py::call_guard<py::gil_scoped_release>())

@@ -22,6 +22,7 @@ from ..models import proto as pb
 from ..ops import crc as crcops
 from ..ops import erasure
 from ..utils.rpc import ChannelPool, RpcStatus, StatusCode, rpc_details, strip_scheme
+from ..utils.shm import ShmMapper
 
 log = logging.getLogger("dfs.chunkserver")
 
@@ -47,7 +48,8 @@ class ChunkServer:
         self._fwd = ThreadPoolExecutor(max_workers=64, thread_name_prefix="cs-fwd")
         self.metrics = metrics
         self.stats = {"writes": 0, "reads": 0, "replicas_in": 0, "rccl_forwards": 0, "grpc_forwards": 0,
-                      "rccl_fallbacks": 0, "recoveries": 0}
+                      "rccl_fallbacks": 0, "recoveries": 0, "shm_writes": 0, "shm_reads": 0}
+        self.shm = ShmMapper()
 
     # ------------------------------------------------------------------ fencing
     def fence(self, term: int) -> None:
@@ -103,6 +105,8 @@ class ChunkServer:
             if st != ST_OK:
                 log.error("cannot forward %s: %s", block_id, err)
                 return 0
+        elif not isinstance(data, bytes):
+            data = bytes(data)  # short-circuit shm view -> owned payload for the gRPC hop
         req = pb.ReplicateBlockRequest(block_id=block_id, data=data, next_servers=rest,
                                        expected_checksum_crc32c=crc, master_term=term, heal=heal)
         try:
@@ -157,7 +161,14 @@ class ChunkServer:
 
     def write_block(self, req, ctx):
         self.fence(req.master_term)
-        ok, err, replicas = self._store_and_forward(req.block_id, req.data, list(req.next_servers),
+        data = req.data
+        if req.shm_path:
+            try:
+                data = self.shm.view(req.shm_path, req.shm_offset, req.shm_length)
+            except (OSError, ValueError) as e:
+                raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"short-circuit unavailable: {e}")
+            self.stats["shm_writes"] += 1
+        ok, err, replicas = self._store_and_forward(req.block_id, data, list(req.next_servers),
                                                     req.expected_checksum_crc32c, req.master_term, False)
         if not ok:
             return pb.WriteBlockResponse(success=False, error_message=err)
@@ -185,7 +196,36 @@ class ChunkServer:
                 self.new_blocks.append(req.block_id)
         return pb.ReplicateBlockResponse(success=True, replicas_written=replicas)
 
+    def _read_shm(self, req):
+        try:
+            out = self.shm.view(req.shm_path, req.shm_offset, req.shm_capacity)
+        except (OSError, ValueError) as e:
+            raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"short-circuit unavailable: {e}")
+        st, total, n, partial_bad, bad_slice, err = self.store.read_into(req.block_id, req.offset, req.length, out)
+        if st == ST_CORRUPT:
+            log.error("CRITICAL: data corruption detected for block %s: %s", req.block_id, err)
+            rec_err = self.recover_block(req.block_id)
+            if rec_err is not None:
+                raise RpcStatus(StatusCode.DATA_LOSS, f"Data corruption detected: {err}. Recovery failed: {rec_err}")
+            st, total, n, partial_bad, bad_slice, err = self.store.read_into(req.block_id, req.offset, req.length,
+                                                                             out)
+            if st != ST_OK:
+                raise RpcStatus(StatusCode.DATA_LOSS, f"Recovered block is still corrupted: {err}")
+        elif st == ST_NOT_FOUND:
+            raise RpcStatus(StatusCode.NOT_FOUND, "Block not found")
+        elif st == ST_OUT_OF_RANGE:
+            raise RpcStatus(StatusCode.OUT_OF_RANGE, err)
+        elif st != ST_OK:
+            raise RpcStatus(StatusCode.INTERNAL, f"Failed to read block: {err}")
+        if partial_bad:
+            self._bg.submit(self.recover_block, req.block_id)
+        self.stats["reads"] += 1
+        self.stats["shm_reads"] += 1
+        return pb.ReadBlockResponse(bytes_read=n, total_size=total, shm_filled=True)
+
     def read_block(self, req, ctx):
+        if req.shm_path:
+            return self._read_shm(req)
         st, total, data, partial_bad, bad_slice, err = self.store.read(req.block_id, req.offset, req.length)
         if st == ST_NOT_FOUND:
             raise RpcStatus(StatusCode.NOT_FOUND, "Block not found")

@@ -28,6 +28,7 @@ from ..ops import crc as crcops
 from ..ops import erasure
 from ..parallel.sharding import ShardMap
 from ..utils.rpc import ChannelPool, rpc_code, rpc_details, strip_scheme, with_scheme
+from ..utils.shm import ShmArena
 
 log = logging.getLogger("dfs.client")
 
@@ -52,7 +53,7 @@ class Client:
                  max_retries: int = MAX_RETRIES, initial_backoff_ms: int = INITIAL_BACKOFF_MS,
                  ca_cert: str | None = None, domain_name: str | None = None, hedge_delay_ms: int | None = None,
                  local_chunkserver: str | None = None, ec_store=None, rpc_timeout: float = 30.0,
-                 data_timeout: float = 120.0):
+                 data_timeout: float = 120.0, short_circuit: bool = True):
         self.tls = ca_cert is not None
         self.master_addrs = [with_scheme(a, self.tls) for a in master_addrs if a]
         self.config_server_addrs = [with_scheme(a, self.tls) for a in (config_server_addrs or []) if a]
@@ -68,6 +69,32 @@ class Client:
         self.data_timeout = data_timeout
         self.pool = ChannelPool(ca_cert, domain_name)
         self._exec = ThreadPoolExecutor(max_workers=32, thread_name_prefix="dfs-client")
+        self.short_circuit = short_circuit and self.local_chunkserver is not None
+        self._arena: ShmArena | None = None
+        self._arena_lock = threading.Lock()
+        self.sc_ops = 0
+
+    # ------------------------------------------------------------------ short-circuit I/O
+    def _shm(self) -> ShmArena | None:
+        if not self.short_circuit:
+            return None
+        if self._arena is None:
+            with self._arena_lock:
+                if self._arena is None:
+                    try:
+                        self._arena = ShmArena()
+                    except OSError as e:
+                        log.info("short-circuit disabled: %s", e)
+                        self.short_circuit = False
+                        return None
+        return self._arena
+
+    def _sc_failed(self, e: Exception) -> bool:
+        if rpc_code(e) == grpc.StatusCode.FAILED_PRECONDITION and "short-circuit" in rpc_details(e):
+            log.info("chunkserver refused short-circuit I/O (%s); using the gRPC payload path", rpc_details(e))
+            self.short_circuit = False
+            return True
+        return False
 
     # ------------------------------------------------------------------ config
     def with_retry_config(self, max_retries: int, initial_backoff_ms: int) -> "Client":
@@ -94,6 +121,8 @@ class Client:
     def close(self) -> None:
         self.pool.close()
         self._exec.shutdown(wait=False)
+        if self._arena is not None:
+            self._arena.close()
 
     # ------------------------------------------------------------------ master RPC routing
     def _targets_for(self, key: str | None) -> list[str]:
@@ -263,13 +292,32 @@ class Client:
         # is on the wire instead of before it (hashlib releases the GIL); it is only
         # needed for CompleteFile.
         md5_fut = self._exec.submit(lambda: hashlib.md5(data).hexdigest())
-        req = pb.WriteBlockRequest(block_id=block.block_id, data=data, next_servers=servers[1:],
-                                   expected_checksum_crc32c=crc, shard_index=-1, master_term=alloc.master_term)
-        try:
-            resp = self.pool.call(self._cs(servers[0]), "ChunkServerService", "WriteBlock", req,
-                                  timeout=self.data_timeout)
-        except grpc.RpcError as e:
-            raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
+        resp = None
+        arena = self._shm() if strip_scheme(servers[0]) == self.local_chunkserver else None
+        slot = arena.acquire(len(data)) if arena is not None else None
+        if slot is not None:
+            try:
+                arena.view[slot:slot + len(data)] = data
+                req = pb.WriteBlockRequest(block_id=block.block_id, next_servers=servers[1:],
+                                           expected_checksum_crc32c=crc, shard_index=-1,
+                                           master_term=alloc.master_term, shm_path=arena.path, shm_offset=slot,
+                                           shm_length=len(data))
+                resp = self.pool.call(self._cs(servers[0]), "ChunkServerService", "WriteBlock", req,
+                                      timeout=self.data_timeout)
+                self.sc_ops += 1
+            except grpc.RpcError as e:
+                if not self._sc_failed(e):
+                    raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
+            finally:
+                arena.release(slot)
+        if resp is None:
+            req = pb.WriteBlockRequest(block_id=block.block_id, data=data, next_servers=servers[1:],
+                                       expected_checksum_crc32c=crc, shard_index=-1, master_term=alloc.master_term)
+            try:
+                resp = self.pool.call(self._cs(servers[0]), "ChunkServerService", "WriteBlock", req,
+                                      timeout=self.data_timeout)
+            except grpc.RpcError as e:
+                raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
         etag = md5_fut.result()
         if not resp.success:
             raise DfsError(f"Failed to write block: {resp.error_message}")
@@ -312,13 +360,34 @@ class Client:
             locs.insert(0, self.local_chunkserver)
         return locs
 
-    def read_block_from_location(self, location: str, block_id: str, offset: int = 0, length: int = 0) -> bytes:
+    def read_block_from_location(self, location: str, block_id: str, offset: int = 0, length: int = 0,
+                                 size_hint: int | None = None) -> bytes:
+        want = length if length else (size_hint - offset if size_hint else None)
+        if want is not None and strip_scheme(location) == self.local_chunkserver:
+            arena = self._shm()
+            slot = arena.acquire(want) if arena is not None else None
+            if slot is not None:
+                try:
+                    r = self.pool.call(self._cs(location), "ChunkServerService", "ReadBlock",
+                                       pb.ReadBlockRequest(block_id=block_id, offset=offset, length=length,
+                                                           shm_path=arena.path, shm_offset=slot,
+                                                           shm_capacity=arena.slot), timeout=self.data_timeout)
+                    if r.shm_filled:
+                        self.sc_ops += 1
+                        return bytes(arena.view[slot:slot + r.bytes_read])
+                    return r.data
+                except grpc.RpcError as e:
+                    if not self._sc_failed(e):
+                        raise
+                finally:
+                    arena.release(slot)
         r = self.pool.call(self._cs(location), "ChunkServerService", "ReadBlock",
                            pb.ReadBlockRequest(block_id=block_id, offset=offset, length=length),
                            timeout=self.data_timeout)
         return r.data
 
-    def read_block_range(self, locations, block_id: str, offset: int = 0, length: int = 0) -> bytes:
+    def read_block_range(self, locations, block_id: str, offset: int = 0, length: int = 0,
+                         size_hint: int | None = None) -> bytes:
         locs = self._order_locations(locations)
         if not locs:
             raise DfsError(f"No locations for block {block_id}")
@@ -327,7 +396,7 @@ class Client:
         last = None
         for loc in locs:
             try:
-                return self.read_block_from_location(loc, block_id, offset, length)
+                return self.read_block_from_location(loc, block_id, offset, length, size_hint)
             except grpc.RpcError as e:
                 last = e
                 log.debug("read %s from %s failed: %s", block_id, loc, rpc_details(e))
@@ -372,7 +441,7 @@ class Client:
     def fetch_single_block(self, block) -> bytes:
         if block.ec_data_shards > 0:
             return self.read_ec_block(block)
-        return self.read_block_range(block.locations, block.block_id)
+        return self.read_block_range(block.locations, block.block_id, size_hint=block.size or None)
 
     def get_file_content(self, path: str) -> bytes:
         meta = self.get_file_info(path)
