@@ -216,9 +216,9 @@ class RaftNode:
             try:
                 if self.role == LEADER:
                     self._broadcast()
-                    self._maybe_snapshot()
                 elif time.monotonic() >= self._election_deadline and self.id in self.config.voters():
                     await self._start_election()
+                self._maybe_snapshot()  # every member compacts its own log
             except Exception:  # noqa: BLE001
                 log.exception("raft tick failed")
 
