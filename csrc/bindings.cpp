@@ -384,11 +384,19 @@ PYBIND11_MODULE(_dfs_native, m) {
 
   // ---------------- crypto
   m.def("aes256gcm_encrypt", [](py::bytes key, py::bytes nonce, py::bytes pt, py::bytes aad) {
-    std::string o = crypto::aes256gcm_encrypt(key, nonce, pt, aad);
+    std::string k = key, n = nonce, p = pt, a = aad, o;
+    {
+      py::gil_scoped_release r;
+      o = crypto::aes256gcm_encrypt(k, n, p, a);
+    }
     return py::bytes(o);
   }, py::arg("key"), py::arg("nonce"), py::arg("plaintext"), py::arg("aad") = py::bytes());
   m.def("aes256gcm_decrypt", [](py::bytes key, py::bytes nonce, py::bytes ct, py::bytes aad) {
-    std::string o = crypto::aes256gcm_decrypt(key, nonce, ct, aad);
+    std::string k = key, n = nonce, c = ct, a = aad, o;
+    {
+      py::gil_scoped_release r;
+      o = crypto::aes256gcm_decrypt(k, n, c, a);
+    }
     return py::bytes(o);
   }, py::arg("key"), py::arg("nonce"), py::arg("ciphertext"), py::arg("aad") = py::bytes());
   m.def("rsa_sha256_verify", [](py::bytes n, py::bytes e, py::bytes msg, py::bytes sig) {

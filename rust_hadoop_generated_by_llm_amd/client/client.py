@@ -447,6 +447,10 @@ class Client:
         meta = self.get_file_info(path)
         if meta is None:
             raise DfsError("File not found")
+        if meta.size == 0:
+            # an empty object's block holds no bytes; the chunkserver rejects offset 0 of a
+            # 0-byte block as OUT_OF_RANGE (reference semantics), so never ask for it
+            return b""
         if len(meta.blocks) == 1:
             return self.fetch_single_block(meta.blocks[0])
         parts = list(self._exec.map(self.fetch_single_block, meta.blocks))

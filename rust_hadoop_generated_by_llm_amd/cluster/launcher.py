@@ -198,6 +198,20 @@ class LocalCluster:
         self._wait_ready(cprocs)
         self.wait_registered()
 
+    def start_s3(self, env: dict | None = None, name: str = "s3") -> str:
+        """Start an S3 gateway process against this cluster; returns its endpoint URL."""
+        port = free_port()
+        e = {"PORT": str(port), "MASTER_ADDR": self.master_addrs[0],
+             "AUDIT_LOG_DIR": str(self.base / f"{name}_audit")}
+        if self.use_config:
+            e["CONFIG_SERVERS"] = ",".join(self.config_addrs)
+        else:
+            e["SHARD_CONFIG"] = str(self.base / "shard_config.json")
+        e.update(env or {})
+        pr = self._spawn(name, "s3.server", [], e)
+        self._wait_ready([pr])
+        return f"http://127.0.0.1:{port}"
+
     @property
     def master_addrs(self) -> list[str]:
         return [m for ms in self.shard_masters.values() for m in ms]

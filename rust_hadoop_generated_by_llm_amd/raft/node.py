@@ -271,14 +271,17 @@ class RaftNode:
         self._broadcast()
 
     async def _step_down(self, term: int, leader_address: str | None, leader_id: int | None = None) -> None:
+        # The role must change in the same step as the term: persisting the hard state
+        # yields, and a concurrent _replicate() of this node that still saw LEADER would
+        # otherwise send AppendEntries stamped with the *new* term it never won.
         was_leader = self.role == LEADER
+        self.role = FOLLOWER
+        self.leader_id = leader_id
+        self.leader_address = leader_address
         if term > self.current_term:
             self.current_term = term
             self.voted_for = None
             await self._persist_hard_state()
-        self.role = FOLLOWER
-        self.leader_id = leader_id
-        self.leader_address = leader_address
         self._reset_election_timer()
         if was_leader:
             self._fail_pending(NotLeader(leader_address))
@@ -549,6 +552,8 @@ class RaftNode:
                 if idx <= self.last_index():
                     if self.term_at(idx) == e["term"]:
                         continue
+                    log.debug("node %d truncating from %d (term %d, role %s) on append term %d from %s prev %d",
+                              self.id, idx, self.current_term, self.role, a["term"], a.get("leader_id"), prev)
                     del self.log[idx - self.first_index:]
                     recs.append(json.dumps({"k": "T", "from": idx}).encode())
                 self.log.append((e["term"], e["command"]))

@@ -1,0 +1,324 @@
+"""Tamper-evident S3 audit log (C56) and its reader (C59).
+
+Reference: dfs/s3_server/src/audit.rs (RocksDB column families ``logs``/``idx_user``/
+``idx_resource``) and src/bin/audit_reader.rs. Semantics kept:
+
+* bounded queue of 10 000 records, ``log()`` never blocks — overflow is counted as dropped;
+* one worker batches ``batch_size`` records (default 100) or flushes every 5 s, sorts a
+  batch by (timestamp_ms, request_id), assigns a monotonic key timestamp, and chains
+  ``previous_hash`` → ``record_hash = HMAC-SHA256(secret, JSON(record, record_hash=null))``;
+  the chain head advances only after a successful write (3 attempts, 0.5 s·n backoff);
+* the chain head is recovered from the newest stored record at start-up; the queue is
+  drained on shutdown; records older than ``retention_days`` are deleted hourly.
+
+Storage is an append-only segment directory instead of RocksDB: one file per UTC hour
+(``seg-<hour_start_ms>.log``), one ``<key_ts>\\t<json>`` line per record, so a time-range
+query opens only the overlapping segments and retention is an ``unlink``. The record JSON
+uses the reference field order and compact separators, so hashes verify against the
+reference's ``compute_hmac`` definition.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import hmac
+import json
+import logging
+import os
+import queue
+import sys
+import threading
+import time
+from datetime import datetime, timezone
+
+from ..utils.metrics import Registry
+
+log = logging.getLogger("dfs.s3.audit")
+
+FIELDS = ("timestamp", "timestamp_ms", "request_id", "remote_ip", "user_id", "role_arn", "action", "resource",
+          "status_code", "error_code", "user_agent", "duration_ms", "previous_hash", "record_hash")
+HOUR_MS = 3_600_000
+
+
+def make_record(*, request_id: str, remote_ip: str, user_id: str, role_arn: str | None, action: str, resource: str,
+                status_code: int, error_code: str | None, user_agent: str | None, duration_ms: int | None,
+                now: datetime | None = None) -> dict:
+    now = now or datetime.now(timezone.utc)
+    return {"timestamp": now.isoformat(),
+            "timestamp_ms": int(now.timestamp() * 1000), "request_id": request_id, "remote_ip": remote_ip,
+            "user_id": user_id, "role_arn": role_arn, "action": action, "resource": resource,
+            "status_code": int(status_code), "error_code": error_code, "user_agent": user_agent,
+            "duration_ms": duration_ms, "previous_hash": None, "record_hash": None}
+
+
+def canonical_json(rec: dict) -> str:
+    return json.dumps({k: rec.get(k) for k in FIELDS}, separators=(",", ":"), ensure_ascii=False)
+
+
+def compute_hmac(rec: dict, secret: str) -> str:
+    r = dict(rec)
+    r["record_hash"] = None
+    return hmac.new(secret.encode(), canonical_json(r).encode(), hashlib.sha256).hexdigest()
+
+
+def extract_bucket_name(resource: str) -> str:
+    parts = resource.split(":")
+    bid = parts[5] if len(parts) > 5 else resource
+    return bid.split("/", 1)[0]
+
+
+class SegmentStore:
+    def __init__(self, path: str):
+        self.path = path
+        os.makedirs(path, exist_ok=True)
+
+    def segments(self) -> list[tuple[int, str]]:
+        out = []
+        for n in os.listdir(self.path):
+            if n.startswith("seg-") and n.endswith(".log"):
+                try:
+                    out.append((int(n[4:-4]), os.path.join(self.path, n)))
+                except ValueError:
+                    pass
+        return sorted(out)
+
+    def append(self, keyed: list[tuple[int, dict]], sync: bool = False) -> None:
+        by_seg: dict[int, list[str]] = {}
+        for key_ts, rec in keyed:
+            by_seg.setdefault(key_ts // HOUR_MS * HOUR_MS, []).append(f"{key_ts}\t{canonical_json(rec)}\n")
+        for seg, lines in sorted(by_seg.items()):
+            with open(os.path.join(self.path, f"seg-{seg}.log"), "a", encoding="utf-8") as f:
+                f.write("".join(lines))
+                f.flush()
+                if sync:
+                    os.fsync(f.fileno())
+
+    def last(self) -> tuple[int, dict] | None:
+        for _, p in reversed(self.segments()):
+            last_line = None
+            with open(p, "rb") as f:
+                for line in f:
+                    if line.strip():
+                        last_line = line
+            if last_line is not None:
+                try:
+                    ts, js = last_line.decode().rstrip("\n").split("\t", 1)
+                    return int(ts), json.loads(js)
+                except ValueError:
+                    continue
+        return None
+
+    def scan(self, start_ms: int | None = None, end_ms: int | None = None):
+        for seg, p in self.segments():
+            if end_ms is not None and seg > end_ms:
+                break
+            if start_ms is not None and seg + HOUR_MS <= start_ms:
+                continue
+            with open(p, encoding="utf-8") as f:
+                for line in f:
+                    line = line.rstrip("\n")
+                    if not line:
+                        continue
+                    try:
+                        ts_s, js = line.split("\t", 1)
+                        ts = int(ts_s)
+                        rec = json.loads(js)
+                    except ValueError:
+                        continue
+                    if start_ms is not None and ts < start_ms:
+                        continue
+                    if end_ms is not None and ts > end_ms:
+                        continue
+                    yield ts, rec
+
+    def cleanup(self, retention_days: int, now_ms: int | None = None) -> int:
+        now_ms = int(time.time() * 1000) if now_ms is None else now_ms
+        cutoff = now_ms - retention_days * 86_400_000
+        n = 0
+        for seg, p in self.segments():
+            if seg + HOUR_MS <= cutoff:
+                os.unlink(p)
+                n += 1
+        return n
+
+
+class AuditLogger:
+    def __init__(self, path: str, retention_days: int = 30, batch_size: int = 100, hmac_secret: str = "",
+                 *, registry: Registry | None = None, flush_interval: float = 5.0, capacity: int = 10_000,
+                 sync: bool = False):
+        self.store = SegmentStore(path)
+        self.retention_days = retention_days
+        self.batch_size = max(1, batch_size)
+        self.secret = hmac_secret
+        self.flush_interval = flush_interval
+        self.sync = sync
+        self.q: queue.Queue = queue.Queue(maxsize=capacity)
+        reg = registry or Registry()
+        self.m_total = reg.counter("audit_log_total", "Total number of audit logs sent to the logger")
+        self.m_dropped = reg.counter("audit_log_dropped_total", "Total number of audit logs dropped due to full buffer")
+        self.m_flush_err = reg.counter("audit_log_flush_errors_total", "Total number of audit log flush failures")
+        last = self.store.last()
+        self.committed_hash = last[1].get("record_hash") if last else None
+        self.last_ts = last[0] if last else 0
+        self._stop = threading.Event()
+        self._flushed = threading.Condition()
+        self._pending = 0
+        self._worker = threading.Thread(target=self._run, name="audit-logger", daemon=True)
+        self._worker.start()
+
+    def log(self, rec: dict) -> None:
+        self.m_total.inc()
+        try:
+            with self._flushed:
+                self._pending += 1
+            self.q.put_nowait(rec)
+        except queue.Full:
+            with self._flushed:
+                self._pending -= 1
+            self.m_dropped.inc()
+            log.warning("audit log queue full, dropping record")
+
+    def _commit(self, batch: list[dict]) -> None:
+        batch.sort(key=lambda r: (r["timestamp_ms"], r["request_id"]))
+        keyed = []
+        h = self.committed_hash
+        last_ts = self.last_ts
+        for rec in batch:
+            key_ts = max(int(rec["timestamp_ms"]), last_ts)
+            last_ts = key_ts
+            rec = dict(rec)
+            rec["previous_hash"] = h
+            h = compute_hmac(rec, self.secret)
+            rec["record_hash"] = h
+            keyed.append((key_ts, rec))
+        for attempt in range(1, 4):
+            try:
+                self.store.append(keyed, self.sync)
+                self.committed_hash, self.last_ts = h, last_ts
+                break
+            except OSError as e:
+                self.m_flush_err.inc()
+                log.error("audit flush failed (attempt %d): %s", attempt, e)
+                if attempt < 3:
+                    time.sleep(0.5 * attempt)
+        else:
+            log.error("audit flush failed after 3 attempts; %d records lost", len(batch))
+        with self._flushed:
+            self._pending -= len(batch)
+            self._flushed.notify_all()
+
+    def _run(self) -> None:
+        batch: list[dict] = []
+        next_flush = time.monotonic() + self.flush_interval
+        next_cleanup = time.monotonic() + 3600
+        while not self._stop.is_set() or not self.q.empty():
+            timeout = max(0.0, next_flush - time.monotonic())
+            try:
+                batch.append(self.q.get(timeout=min(timeout, 0.2)))
+            except queue.Empty:
+                pass
+            now = time.monotonic()
+            if len(batch) >= self.batch_size or (batch and now >= next_flush) or (batch and self._stop.is_set()):
+                self._commit(batch)
+                batch = []
+            if now >= next_flush:
+                next_flush = now + self.flush_interval
+            if now >= next_cleanup:
+                next_cleanup = now + 3600
+                try:
+                    self.store.cleanup(self.retention_days)
+                except OSError as e:
+                    log.error("audit cleanup failed: %s", e)
+        if batch:
+            self._commit(batch)
+
+    def flush(self, timeout: float = 10.0) -> bool:
+        """Wait until every logged record is committed (tests, shutdown)."""
+        deadline = time.monotonic() + timeout
+        saved = self.flush_interval
+        self.flush_interval = 0.0
+        try:
+            with self._flushed:
+                while self._pending > 0:
+                    left = deadline - time.monotonic()
+                    if left <= 0:
+                        return False
+                    self._flushed.wait(min(left, 0.1))
+            return True
+        finally:
+            self.flush_interval = saved
+
+    def close(self) -> None:
+        self._stop.set()
+        self._worker.join(timeout=30)
+
+
+# ---------------------------------------------------------------------------- reader
+def verify_chain(store: SegmentStore, secret: str) -> tuple[int, list[str]]:
+    errors = []
+    prev = None
+    n = 0
+    for key_ts, rec in store.scan():
+        n += 1
+        if rec.get("previous_hash") != prev:
+            errors.append(f"record {rec.get('request_id')} @ {key_ts}: previous_hash does not link")
+        if compute_hmac(rec, secret) != rec.get("record_hash"):
+            errors.append(f"record {rec.get('request_id')} @ {key_ts}: record_hash mismatch")
+        prev = rec.get("record_hash")
+    return n, errors
+
+
+def _parse_time(s: str) -> int:
+    return int(datetime.fromisoformat(s.replace("Z", "+00:00")).timestamp() * 1000)
+
+
+def reader_main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(prog="audit_reader", description="Read and filter S3 server audit logs")
+    ap.add_argument("db_path", help="audit log directory")
+    ap.add_argument("-u", "--user", help="filter by user id (access key or OIDC sub)")
+    ap.add_argument("-r", "--resource", help="filter by bucket / resource id")
+    ap.add_argument("-a", "--action", help="filter by S3 action (e.g. s3:GetObject)")
+    ap.add_argument("-s", "--status", type=int, help="filter by HTTP status code")
+    ap.add_argument("--start", help="start time (ISO8601)")
+    ap.add_argument("--end", help="end time (ISO8601)")
+    ap.add_argument("--json", action="store_true", help="raw JSON lines")
+    ap.add_argument("-l", "--limit", type=int, default=100)
+    ap.add_argument("--verify-chain", metavar="SECRET", help="verify the HMAC hash chain")
+    a = ap.parse_args(argv)
+    store = SegmentStore(a.db_path)
+    if a.verify_chain:
+        n, errs = verify_chain(store, a.verify_chain)
+        for e in errs:
+            print(e)
+        print(f"verified {n} records: {'OK' if not errs else f'{len(errs)} errors'}")
+        return 0 if not errs else 1
+    start = _parse_time(a.start) if a.start else None
+    end = _parse_time(a.end) if a.end else None
+    count = 0
+    if not a.json:
+        print(f"{'TIMESTAMP':<32} {'USER':<20} {'ACTION':<22} {'STATUS':<6} RESOURCE")
+    for _, rec in store.scan(start, end):
+        if a.user and rec.get("user_id") != a.user:
+            continue
+        if a.resource and extract_bucket_name(rec.get("resource", "")) != a.resource and \
+                rec.get("resource") != a.resource:
+            continue
+        if a.action and rec.get("action") != a.action:
+            continue
+        if a.status is not None and rec.get("status_code") != a.status:
+            continue
+        if a.json:
+            print(json.dumps(rec, separators=(",", ":")))
+        else:
+            print(f"{rec.get('timestamp', ''):<32} {rec.get('user_id', ''):<20} {rec.get('action', ''):<22} "
+                  f"{rec.get('status_code', ''):<6} {rec.get('resource', '')}")
+        count += 1
+        if count >= a.limit:
+            break
+    if not a.json and count == 0:
+        print("no matching records")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(reader_main())
