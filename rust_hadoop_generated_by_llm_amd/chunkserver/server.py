@@ -218,6 +218,27 @@ class ChunkServerProcess:
                     d = dict(proc.store.stats())
                     d.update(proc.cs.stats)
                     body, ctype = json.dumps(d).encode(), "application/json"
+                elif self.path.startswith("/debug/") and os.environ.get("DFS_DEBUG_ENDPOINTS") == "1":
+                    # fault injection for tests (off unless DFS_DEBUG_ENDPOINTS=1):
+                    # /debug/corrupt?block=<id>&offset=<n>  flips one byte everywhere it lives
+                    # /debug/scrub                           runs one scrub pass now
+                    from urllib.parse import parse_qs, urlsplit
+
+                    u = urlsplit(self.path)
+                    q = {k: v[0] for k, v in parse_qs(u.query).items()}
+                    if u.path == "/debug/corrupt":
+                        ok = proc.store.debug_corrupt(q["block"], int(q.get("offset", "0")))
+                        body = json.dumps({"corrupted": bool(ok)}).encode()
+                    elif u.path == "/debug/scrub":
+                        body = json.dumps({"bad": proc.cs.scrub_once()}).encode()
+                    elif u.path == "/debug/drop_resident":
+                        proc.store.drop_resident(q["block"])
+                        body = b"{}"
+                    else:
+                        self.send_response(404)
+                        self.end_headers()
+                        return
+                    ctype = "application/json"
                 else:
                     self.send_response(404)
                     self.end_headers()

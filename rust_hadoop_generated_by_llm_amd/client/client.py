@@ -141,6 +141,7 @@ class Client:
         """Returns (response, address that answered)."""
         backoff = self.initial_backoff_ms / 1000.0
         hint: str | None = None
+        redirects = 0
         last_err = "no masters configured"
         for attempt in range(1, max(1, self.max_retries) + 1):
             targets = list(masters)
@@ -168,7 +169,12 @@ class Client:
                     last_err = f"{code}: {msg}"
                     if msg.startswith("REDIRECT:") and msg[len("REDIRECT:"):]:
                         hint = msg[len("REDIRECT:"):]
+                        redirects += 1
                         self._exec.submit(self.refresh_shard_map)
+                        if redirects > 1:
+                            # bounced between masters whose shard maps disagree (a map
+                            # change is propagating): give them time to converge
+                            time.sleep(min(0.05 * redirects, 1.0))
                         break
                     if msg.startswith("Not Leader|") and msg.split("|", 1)[1]:
                         hint = msg.split("|", 1)[1]

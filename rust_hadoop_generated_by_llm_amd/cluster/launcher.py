@@ -197,6 +197,28 @@ class LocalCluster:
             self.cs_http.append(f"http://127.0.0.1:{http}")
         self._wait_ready(cprocs)
         self.wait_registered()
+        if self.shards > 1:
+            self.wait_shard_maps()
+
+    def wait_shard_maps(self, timeout: float = 30.0) -> None:
+        """Block until every master's shard map lists every shard (maps propagate from the
+        config server by polling; a master with a stale map would misroute renames)."""
+        import urllib.request
+
+        want = set(self.shard_masters)
+        deadline = time.time() + timeout
+        for http in self.master_http.values():
+            while True:
+                try:
+                    with urllib.request.urlopen(f"{http}/shard_map", timeout=2) as r:
+                        have = set(json.load(r)["map"].get("shards", []))
+                    if have >= want:
+                        break
+                except OSError:
+                    pass
+                if time.time() > deadline:
+                    raise TimeoutError(f"master {http} never learned all shards {sorted(want)}")
+                time.sleep(0.05)
 
     def start_s3(self, env: dict | None = None, name: str = "s3") -> str:
         """Start an S3 gateway process against this cluster; returns its endpoint URL."""

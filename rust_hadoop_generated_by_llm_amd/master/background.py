@@ -26,7 +26,7 @@ from .state import TX_STALE_MS, TX_TIMEOUT_MS, now_ms
 log = logging.getLogger("dfs.master.bg")
 
 MAX_INQUIRY_RETRIES = 60
-CS_DEAD_MS = 15_000
+CS_DEAD_MS = int(os.environ.get("DFS_CS_DEAD_MS", "15000"))  # reference: 15 s
 BALANCE_GAP = 100 * 1024 * 1024
 
 
@@ -40,7 +40,7 @@ class Intervals:
     tx_recovery: float = 30.0
     shuffler: float = 10.0
     decay: float = 5.0
-    shard_refresh: float = 5.0
+    shard_refresh: float = 1.0  # reference: 5 s; a stale map misroutes renames
     split: float = 5.0
     tiering: float = 60.0
 
@@ -68,6 +68,8 @@ class MasterBackground:
             else ec_conversion
         self.registered = False
         self._tasks: list[asyncio.Task] = []
+        if config_servers:
+            svc.shard_map_refresher = self.refresh_shard_map
 
     def start(self) -> None:
         loop = asyncio.get_running_loop()
@@ -263,20 +265,25 @@ class MasterBackground:
         if resp is None or not resp.shards:
             return
         new = ShardMap.from_peers({k: list(v.peers) for k, v in resp.shards.items()})
+        self.svc.shard_map_fetched_ms = now_ms()
         m = self.svc.shard_map
         m.strategy, m.ranges, m.ring, m.shards, m.shard_peers = new.strategy, new.ranges, new.ring, new.shards, \
             new.shard_peers
         m._dirty()
+
+    async def register(self) -> None:
+        if self.registered or not self.config_servers:
+            return
+        r = await self._config_call("RegisterMaster", pb.RegisterMasterRequest(address=self.svc.advertise_addr,
+                                                                              shard_id=self.svc.shard_id))
+        self.registered = bool(r and r.success)
 
     async def split_detector(self) -> None:
         if not self.config_servers:
             return
         mon = self.svc.monitor
         addr = self.svc.advertise_addr
-        if not self.registered:
-            r = await self._config_call("RegisterMaster", pb.RegisterMasterRequest(address=addr,
-                                                                                  shard_id=self.svc.shard_id))
-            self.registered = bool(r and r.success)
+        await self.register()
         hb = pb.ShardHeartbeatRequest(address=addr)
         for p, v in mon.rps_per_prefix().items():
             hb.rps_per_prefix[p] = v

@@ -86,7 +86,7 @@ class MasterProcess:
         iv = Intervals()
         if args.fast_intervals:
             iv = Intervals(liveness=1, healer_first=2, healer=5, balancer=2, tx_cleanup=1, tx_recovery=2,
-                           shuffler=1, decay=1, shard_refresh=1, split=1, tiering=2)
+                           shuffler=1, decay=1, shard_refresh=0.5, split=1, tiering=2)
         cold = int(os.environ.get("COLD_THRESHOLD_SECS", "604800"))
         ecs = int(os.environ.get("EC_THRESHOLD_SECS", "2592000"))
         self.bg = MasterBackground(self.svc, self.config_servers, iv, cold, ecs)
@@ -129,6 +129,10 @@ class MasterProcess:
         app.router.add_get("/health", health)
         app.router.add_get("/metrics", metrics)
         app.router.add_get("/raft/state", raft_state)
+
+        async def shard_map(_):
+            return web.json_response({"shard_id": self.svc.shard_id, "map": self.svc.shard_map.to_json()})
+        app.router.add_get("/shard_map", shard_map)
         for k in ("vote", "append", "snapshot", "timeout_now"):
             app.router.add_post(f"/raft/{k}", raft_route(k))
         return app
@@ -145,6 +149,7 @@ class MasterProcess:
         await server.start()
         await self.raft.start()
         if self.config_servers:
+            await self.bg.register()
             await self.bg.refresh_shard_map()
         self.bg.start()
         stop = asyncio.Event()

@@ -61,13 +61,48 @@ class MasterService:
         self._access_flush_ms = access_stats_flush_ms
         self._access_task: asyncio.Task | None = None
         self.requests = 0
+        # set by MasterBackground when config servers exist: a rename decides same-shard
+        # vs 2PC from the shard map, so it refreshes a map older than this first
+        self.shard_map_refresher = None
+        self.shard_map_fetched_ms = 0
+        self.shard_map_max_age_ms = 1000
+
+    async def fresh_shard_map(self, force: bool = False) -> None:
+        if self.shard_map_refresher is None:
+            return
+        if not force and now_ms() - self.shard_map_fetched_ms < self.shard_map_max_age_ms:
+            return
+        try:
+            await asyncio.wait_for(self.shard_map_refresher(), 2.0)
+        except Exception as e:  # noqa: BLE001 - fall back to the cached map
+            log.debug("shard map refresh before rename failed: %s", e)
 
     # ------------------------------------------------------------------ guards
     def check_shard_ownership(self, path: str) -> None:
         target = self.shard_map.get_shard(path)
         if target is not None and target != self.shard_id:
+            # our map may be the stale one (e.g. a shard registered moments ago): refresh it
+            # in the background so a client bounced between two masters converges
+            if self.shard_map_refresher is not None and \
+                    now_ms() - self.shard_map_fetched_ms >= self.shard_map_max_age_ms:
+                self.shard_map_fetched_ms = now_ms()
+                asyncio.get_running_loop().create_task(self.fresh_shard_map(force=True))
             peers = self.shard_map.get_shard_peers(target) or []
             raise RpcStatus(StatusCode.OUT_OF_RANGE, f"REDIRECT:{peers[0] if peers else ''}")
+
+    async def wait_unlocked(self, path: str, timeout: float = 5.0) -> None:
+        """Block while ``path`` is pinned by an unresolved cross-shard rename."""
+        if path not in self.state.tx_locks:
+            return
+        loop = asyncio.get_running_loop()
+        end = loop.time() + timeout
+        delay = 0.002
+        while path in self.state.tx_locks:
+            if loop.time() > end:
+                raise RpcStatus(StatusCode.UNAVAILABLE, f"{path} is locked by transaction "
+                                                        f"{self.state.tx_locks.get(path)}")
+            await asyncio.sleep(delay)
+            delay = min(delay * 2, 0.05)
 
     def check_safe_mode(self) -> None:
         if self.state.safe_mode:
@@ -81,6 +116,16 @@ class MasterService:
 
     async def _propose(self, name: str, args: dict):
         return await self.raft.propose({"Master": {name: args}})
+
+    async def _propose_unlocked(self, name: str, args: dict, attempts: int = 50):
+        """Propose a namespace mutation whose apply refuses paths pinned by an in-flight
+        cross-shard rename ({"locked": path}); wait for the pin to clear and retry."""
+        for _ in range(attempts):
+            res = await self._propose(name, args)
+            if not (isinstance(res, dict) and res.get("locked")):
+                return res
+            await self.wait_unlocked(res["locked"])
+        raise RpcStatus(StatusCode.UNAVAILABLE, f"{name}: path stays locked by cross-shard renames")
 
     # ------------------------------------------------------------------ access stats
     def _record_access(self, path: str) -> None:
@@ -107,7 +152,8 @@ class MasterService:
         self._record_access(req.path)
         self.check_shard_ownership(req.path)
         await self.ensure_linearizable_read()
-        m = self.state.files.get(req.path)
+        await self.wait_unlocked(req.path)
+        m = self.state.visible(req.path)
         if m is None:
             return pb.GetFileInfoResponse(found=False)
         return pb.GetFileInfoResponse(metadata=m, found=True)
@@ -116,28 +162,35 @@ class MasterService:
         self.monitor.record_request(req.path)
         self.check_shard_ownership(req.path)
         self.check_safe_mode()
-        if req.path in self.state.files:
+        await self.wait_unlocked(req.path)
+        if req.path in self.state.files and req.path not in self.state.under_construction:
             return pb.CreateFileResponse(success=False, error_message="File already exists")
         try:
-            await self._propose("CreateFile", {"path": req.path, "ec_data_shards": req.ec_data_shards,
-                                               "ec_parity_shards": req.ec_parity_shards})
+            res = await self._propose_unlocked("CreateFile", {"path": req.path, "ec_data_shards": req.ec_data_shards,
+                                                     "ec_parity_shards": req.ec_parity_shards, "ts": now_ms()})
         except NotLeader as e:
             return pb.CreateFileResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        if isinstance(res, dict):
+            if res.get("exists"):
+                return pb.CreateFileResponse(success=False, error_message="File already exists")
+            if res.get("orphans"):
+                self._queue_block_gc(res["orphans"])
         return pb.CreateFileResponse(success=True)
 
     async def delete_file(self, req, ctx):
         self.monitor.record_request(req.path)
         self.check_shard_ownership(req.path)
         self.check_safe_mode()
-        m = self.state.files.get(req.path)
-        if m is None:
+        await self.wait_unlocked(req.path)
+        if self.state.visible(req.path) is None:
             return pb.DeleteFileResponse(success=False, error_message="File not found")
-        blocks = [(b.block_id, list(b.locations)) for b in m.blocks]
         try:
-            await self._propose("DeleteFile", {"path": req.path})
+            res = await self._propose_unlocked("DeleteFile", {"path": req.path})
         except NotLeader as e:
             return pb.DeleteFileResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
-        self._queue_block_gc(blocks)
+        if isinstance(res, dict) and not res.get("found", True):
+            return pb.DeleteFileResponse(success=False, error_message="File not found")
+        self._queue_block_gc(res.get("blocks", []) if isinstance(res, dict) else [])
         return pb.DeleteFileResponse(success=True)
 
     def _queue_block_gc(self, blocks) -> None:
@@ -188,18 +241,21 @@ class MasterService:
                 "etag_md5": req.etag_md5 or None, "created_at_ms": req.created_at_ms or None,
                 "block_checksums": [M.checksum_to_dict(c) for c in req.block_checksums]}
         try:
-            await self._propose("CompleteFile", args)
-        except NotLeader:
-            return pb.CompleteFileResponse(success=False)
-        return pb.CompleteFileResponse(success=True)
+            res = await self._propose("CompleteFile", args)
+        except NotLeader as e:
+            # CompleteFileResponse has no leader_hint field: use the read-path status so
+            # clients follow the hint instead of failing the whole write
+            raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"Not Leader|{e.hint}" if e.hint else "Not Leader")
+        return pb.CompleteFileResponse(success=not (isinstance(res, dict) and not res.get("found", True)))
 
     async def list_files(self, req, ctx):
         await self.ensure_linearizable_read()
         prefix = req.path
+        uc = self.state.under_construction
         if not prefix:
-            files = list(self.state.files)
+            files = [p for p in self.state.files if p not in uc]
         else:
-            files = [p for p in self.state.files if p.startswith(prefix)]
+            files = [p for p in self.state.files if p.startswith(prefix) and p not in uc]
         return pb.ListFilesResponse(files=files)
 
     async def register_chunk_server(self, req, ctx):
@@ -241,19 +297,25 @@ class MasterService:
     async def rename(self, req, ctx):
         src, dst = req.source_path, req.dest_path
         self.monitor.record_request(src)
+        await self.fresh_shard_map()
         self.check_shard_ownership(src)
         self.check_safe_mode()
         src_shard = self.shard_map.get_shard(src) or self.shard_id
         dst_shard = self.shard_map.get_shard(dst) or self.shard_id
         dst_peers = self.shard_map.get_shard_peers(dst_shard) or []
-        meta = self.state.files.get(src)
+        await self.wait_unlocked(src)
+        if src_shard == dst_shard:
+            await self.wait_unlocked(dst)
+        meta = self.state.visible(src)
         if meta is None:
             return pb.RenameResponse(success=False, error_message=f"Source file not found: {src}")
         if src_shard == dst_shard:
             try:
-                await self._propose("RenameFile", {"source_path": src, "dest_path": dst})
+                res = await self._propose_unlocked("RenameFile", {"source_path": src, "dest_path": dst})
             except NotLeader as e:
                 return pb.RenameResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+            if isinstance(res, dict) and res.get("error"):
+                return pb.RenameResponse(success=False, error_message=res["error"])
             return pb.RenameResponse(success=True)
         tx_id = str(uuid.uuid4())
         dmeta = pb.FileMetadata()
@@ -261,9 +323,11 @@ class MasterService:
         dmeta.path = dst
         rec = new_rename_record(tx_id, src, dst, src_shard, dst_shard, dmeta)
         try:
-            await self._propose("CreateTransactionRecord", {"record": rec})
+            res = await self._propose("CreateTransactionRecord", {"record": rec})
         except NotLeader as e:
             return pb.RenameResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        if isinstance(res, dict) and res.get("conflict"):
+            return pb.RenameResponse(success=False, error_message=res["conflict"])
         try:
             await self._propose("UpdateTransactionState", {"tx_id": tx_id, "new_state": "Prepared"})
         except Exception:  # noqa: BLE001
@@ -332,7 +396,13 @@ class MasterService:
     async def prepare_transaction(self, req, ctx):
         if req.tx_id in self.state.transaction_records:
             return pb.PrepareTransactionResponse(success=True)
+        await self.fresh_shard_map()
         self.check_shard_ownership(req.path)
+        try:
+            await self.wait_unlocked(req.path, timeout=1.0)
+        except RpcStatus:
+            return pb.PrepareTransactionResponse(success=False,
+                                                 error_message=f"Destination is locked by another transaction: {req.path}")
         if req.path in self.state.files:
             return pb.PrepareTransactionResponse(success=False,
                                                  error_message=f"Destination file already exists: {req.path}")
@@ -346,9 +416,11 @@ class MasterService:
             "coordinator_peers": list(req.coordinator_peers),
         }
         try:
-            await self._propose("CreateTransactionRecord", {"record": rec})
+            res = await self._propose("CreateTransactionRecord", {"record": rec})
         except NotLeader as e:
             return pb.PrepareTransactionResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        if isinstance(res, dict) and res.get("conflict"):
+            return pb.PrepareTransactionResponse(success=False, error_message=res["conflict"])
         return pb.PrepareTransactionResponse(success=True)
 
     async def commit_transaction(self, req, ctx):

@@ -12,11 +12,15 @@ Differences from the reference, all behaviour-preserving for clients:
   the target chunkserver reports them, so the healer stops re-issuing the same copy
   (the reference never learns about new replicas);
 * placement can put a writer-local chunkserver first (``preferred``) and treats each GPU
-  ChunkServer of a node as its own failure domain inside the node's rack.
+  ChunkServer of a node as its own failure domain inside the node's rack;
+* files are invisible to GetFileInfo/ListFiles until CompleteFile (the reference shows a
+  half-written file as an empty one, which a concurrent reader can observe — a
+  linearizability violation), and CreateFile decides existence at apply time.
 """
 from __future__ import annotations
 
 import logging
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Any
@@ -31,6 +35,8 @@ SAFE_MODE_THRESHOLD = 0.99
 SAFE_MODE_TIMEOUT_MS = 60_000
 TX_TIMEOUT_MS = 10_000
 TX_STALE_MS = 3_600_000
+# a file left under construction this long (writer died) may be re-created by CreateFile
+CREATE_LEASE_MS = int(os.environ.get("DFS_CREATE_LEASE_MS", "60000"))
 
 
 def now_ms() -> int:
@@ -104,6 +110,15 @@ class MasterState:
         self.transaction_records: dict[str, dict] = {}
         self.shuffling_prefixes: set[str] = set()
         self.block_index: dict[str, str] = {}
+        # files between CreateFile and CompleteFile -> creation time (ms, from the command):
+        # invisible to GetFileInfo/ListFiles so a concurrent reader never observes a
+        # half-written (empty) file; an expired lease lets CreateFile take the path over
+        self.under_construction: dict[str, int] = {}
+        # paths pinned by an unresolved cross-shard rename (derived from
+        # transaction_records): the source on the coordinator shard, the reserved
+        # destination on the participant. Readers and writers of a pinned path wait for
+        # the outcome, which makes the 2PC rename atomic to observers.
+        self.tx_locks: dict[str, str] = {}
         # local (not replicated)
         self.chunk_servers: dict[str, ChunkServerStatus] = {}
         self.pending_commands: dict[str, list] = {}
@@ -129,6 +144,7 @@ class MasterState:
             self.block_index[b.block_id] = path
 
     def _del(self, path: str):
+        self.under_construction.pop(path, None)
         m = self.files.pop(path, None)
         if m is not None:
             for b in m.blocks:
@@ -206,11 +222,34 @@ class MasterState:
         return fn(a)
 
     def _cmd_CreateFile(self, a):
-        self._put(a["path"], pb.FileMetadata(path=a["path"], ec_data_shards=a.get("ec_data_shards", 0),
-                                             ec_parity_shards=a.get("ec_parity_shards", 0)))
+        """Existence is decided here, in log order, so two racing creates of one path
+        cannot both succeed. Returns the replaced (expired) metadata's blocks for GC."""
+        path, ts = a["path"], int(a.get("ts", 0))
+        if path in self.tx_locks:
+            return {"locked": path}
+        old = self.files.get(path)
+        if old is not None:
+            started = self.under_construction.get(path)
+            if started is None or ts - started < CREATE_LEASE_MS:
+                return {"exists": True}
+        self._put(path, pb.FileMetadata(path=path, ec_data_shards=a.get("ec_data_shards", 0),
+                                        ec_parity_shards=a.get("ec_parity_shards", 0)))
+        self.under_construction[path] = ts
+        return {"exists": False, "orphans": [(b.block_id, list(b.locations)) for b in old.blocks] if old else []}
+
+    def visible(self, path: str):
+        """Metadata of a completed file, else None."""
+        if path in self.under_construction:
+            return None
+        return self.files.get(path)
 
     def _cmd_DeleteFile(self, a):
-        self._del(a["path"])
+        if a["path"] in self.tx_locks:
+            return {"locked": a["path"]}
+        if self.visible(a["path"]) is None:
+            return {"found": False}
+        m = self._del(a["path"])
+        return {"found": True, "blocks": [(b.block_id, list(b.locations)) for b in m.blocks]}
 
     def _cmd_AllocateBlock(self, a):
         m = self.files.get(a["path"])
@@ -226,19 +265,63 @@ class MasterState:
         return None
 
     def _cmd_RenameFile(self, a):
-        m = self._del(a["source_path"])
-        if m is not None:
-            m.path = a["dest_path"]
-            self._put(a["dest_path"], m)
+        """Same-shard rename, decided in log order: the source must be a completed file and
+        the destination must not exist (the reference silently overwrote it, so two racing
+        renames onto one name could both "succeed")."""
+        src, dst = a["source_path"], a["dest_path"]
+        for p in (src, dst):
+            if p in self.tx_locks:
+                return {"locked": p}
+        if self.visible(src) is None:
+            return {"error": f"Source file not found: {src}"}
+        if dst in self.files:
+            return {"error": f"Destination file already exists: {dst}"}
+        m = self._del(src)
+        m.path = dst
+        self._put(dst, m)
+        return {"error": None}
+
+    @staticmethod
+    def _locked_path(rec: dict) -> str | None:
+        ren = rec.get("tx_type", {}).get("Rename")
+        if not ren or rec.get("state") in ("Committed", "Aborted"):
+            return None
+        return ren.get("source_path") or ren.get("dest_path") or None
+
+    def _relock(self, rec: dict) -> None:
+        for p, t in list(self.tx_locks.items()):
+            if t == rec["tx_id"]:
+                del self.tx_locks[p]
+        p = self._locked_path(rec)
+        if p:
+            self.tx_locks[p] = rec["tx_id"]
 
     def _cmd_CreateTransactionRecord(self, a):
+        """Admission happens here, in log order: a rename may only pin a path nobody else
+        has pinned; the coordinator's source must be a completed file and the
+        participant's destination must not exist. Returns {"conflict": reason} if not."""
         rec = a["record"]
+        if rec["tx_id"] in self.transaction_records:
+            return {"conflict": None}
+        ren = rec.get("tx_type", {}).get("Rename")
+        p = self._locked_path(rec)
+        if ren and p:
+            if self.tx_locks.get(p, rec["tx_id"]) != rec["tx_id"]:
+                return {"conflict": f"{p} is locked by another transaction"}
+            if ren.get("source_path"):
+                if self.visible(p) is None:
+                    return {"conflict": f"Source file not found: {p}"}
+            elif p in self.files:
+                return {"conflict": f"Destination file already exists: {p}"}
         self.transaction_records[rec["tx_id"]] = rec
+        self._relock(rec)
+        return {"conflict": None}
 
     def _cmd_UpdateTransactionState(self, a):
         rec = self.transaction_records.get(a["tx_id"])
         if rec is not None:
             rec["state"] = a["new_state"]
+            self._relock(rec)
 
     def _cmd_ApplyTransactionOperation(self, a):
         op = a["operation"]["op_type"]
@@ -252,7 +335,10 @@ class MasterState:
                 self._put(c["path"], m)
 
     def _cmd_DeleteTransactionRecord(self, a):
-        self.transaction_records.pop(a["tx_id"], None)
+        rec = self.transaction_records.pop(a["tx_id"], None)
+        if rec is not None:
+            rec = dict(rec, state="Aborted")
+            self._relock(rec)
 
     def _cmd_SplitShard(self, a):
         key = a["split_key"]
@@ -276,7 +362,8 @@ class MasterState:
     def _cmd_CompleteFile(self, a):
         m = self.files.get(a["path"])
         if m is None:
-            return None
+            return {"found": False}
+        self.under_construction.pop(a["path"], None)
         m.size = a["size"]
         if a.get("etag_md5"):
             m.etag_md5 = a["etag_md5"]
@@ -297,7 +384,7 @@ class MasterState:
             for b in m.blocks[:-1]:
                 b.size = per
             m.blocks[-1].size = m.size - per * (n - 1)
-        return None
+        return {"found": True}
 
     def _cmd_UpdateAccessStats(self, a):
         m = self.files.get(a["path"])
@@ -351,6 +438,7 @@ class MasterState:
             "files": {p: M.file_to_dict(m) for p, m in self.files.items()},
             "transaction_records": self.transaction_records,
             "shuffling_prefixes": sorted(self.shuffling_prefixes),
+            "under_construction": self.under_construction,
         }}
 
     def restore(self, state: dict) -> None:
@@ -360,7 +448,12 @@ class MasterState:
         for p, d in st.get("files", {}).items():
             self._put(p, M.file_from_dict(d))
         self.transaction_records = dict(st.get("transaction_records", {}))
+        self.tx_locks = {}
+        for rec in self.transaction_records.values():
+            self._relock(rec)
         self.shuffling_prefixes = set(st.get("shuffling_prefixes", []))
+        self.under_construction = {p: int(t) for p, t in st.get("under_construction", {}).items()
+                                   if p in self.files}
 
     # ------------------------------------------------------------------ healer (C29)
     def heal_under_replicated_blocks(self, rf: int = REPLICATION_FACTOR) -> int:
