@@ -286,6 +286,20 @@ def main():
         barrier()
         if use_cuda:
             torch.cuda.synchronize()
+        import psutil
+
+        def cpu_snapshot():
+            snap = {"client": sum(psutil.Process().cpu_times()[:2])}
+            for i, p in enumerate(procs.items):
+                try:
+                    kids = [psutil.Process(p.pid)] + psutil.Process(p.pid).children(recursive=True)
+                    snap[os.path.basename(procs.logs[i]).split(".")[0]] = sum(sum(k.cpu_times()[:2]) for k in kids)
+                except psutil.Error:
+                    pass
+            return snap
+
+        client.phase_times = {}
+        cpu0 = cpu_snapshot()
         t0 = time.perf_counter()
         wl, rl, wbytes, rbytes = [], [], 0, 0
         wt = rt = 0.0
@@ -303,6 +317,8 @@ def main():
         if use_cuda:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        cpu1 = cpu_snapshot()
+        host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
 
         stats = {}
         try:
@@ -312,7 +328,9 @@ def main():
         except Exception:  # noqa: BLE001
             pass
         allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
-                       "rt": rt, "cs": stats, "rccl": cs_info.get("rccl", False)})
+                       "rt": rt, "cs": stats, "rccl": cs_info.get("rccl", False),
+                       "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
+                                                   for k, v in (client.phase_times or {}).items() if v}})
         if rank == 0:
             tmax = max(r["elapsed"] for r in allr)
             tot = sum(r["wbytes"] + r["rbytes"] for r in allr)
@@ -346,6 +364,8 @@ def main():
                 "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
                 "rccl_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) for r in allr),
                 "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
+                "host_cpu_util_rank0": allr[0]["cpu"],
+                "client_phase_p50_ms_rank0": allr[0]["phases"],
             }
             print(json.dumps(result), flush=True)
         barrier()

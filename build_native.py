@@ -81,7 +81,30 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    build_tools(objs, flags, clean, headers)
     return out
+
+
+def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[Path]) -> list[Path]:
+    """Native executables (csrc/bench/*.cpp) linked against the runtime objects, e.g. the
+    io_bench microbenchmark. Written to build/native/ (ships to the GPU box)."""
+    runtime = [o for o in objs if not o.name.startswith("bindings.")]
+    outs = []
+    for src in sorted((CSRC / "bench").glob("*.cpp")):
+        obj = BUILD / ("bench_" + src.name + ".o")
+        exe = BUILD / src.stem
+        if clean or _newer(src, obj, headers):
+            r = subprocess.run([HIPCC, *flags, "-c", str(src), "-o", str(obj)], capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+        if clean or not exe.exists() or any(o.stat().st_mtime > exe.stat().st_mtime for o in [obj, *runtime]):
+            r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-o", str(exe), str(obj), *map(str, runtime),
+                                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lcrypto", "-lpthread",
+                                f"-Wl,-rpath,{ROCM}/lib"], capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"link failed: {exe}\n{r.stdout}\n{r.stderr}")
+        outs.append(exe)
+    return outs
 
 
 if __name__ == "__main__":

@@ -1,0 +1,216 @@
+// io_bench — native ChunkServer I/O + kernel microbenchmark (C45).
+//
+// Reference: dfs/chunkserver/benches/io_bench.rs (criterion: write+fsync and read of
+// 4 KiB / 64 KiB / 1 MiB, plus a 4 KiB partial read at offset 32 KiB of a 64 KiB file).
+// Same cases against the HBM chunk store, in both durability modes, plus the data-plane
+// kernels the reference runs on the CPU: CRC-32 slice checksums (GPU vs PCLMUL CPU),
+// batched scrub, and Reed-Solomon RS(6,3) encode (GPU vs CPU). Run under
+// `rocprofv3 --kernel-trace --stats` to get per-kernel device time.
+//
+//   io_bench [--device N] [--dir PATH] [--iters N] [--no-fsync]   -> one JSON object on stdout
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <filesystem>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "chunk_store.h"
+#include "crc32.h"
+#include "gf256.h"
+
+using namespace dfs;
+using Clock = std::chrono::steady_clock;
+
+static double secs(Clock::time_point a, Clock::time_point b) {
+  return std::chrono::duration<double>(b - a).count();
+}
+
+struct Lat {
+  std::vector<double> v;
+  void add(double s) { v.push_back(s); }
+  double pct(double p) {
+    if (v.empty()) return 0;
+    std::vector<double> s = v;
+    std::sort(s.begin(), s.end());
+    return s[std::min(s.size() - 1, static_cast<size_t>(p * s.size()))];
+  }
+  double mean() const {
+    double t = 0;
+    for (double x : v) t += x;
+    return v.empty() ? 0 : t / v.size();
+  }
+};
+
+static std::vector<uint8_t> random_bytes(size_t n, uint32_t seed) {
+  std::vector<uint8_t> b(n);
+  std::mt19937_64 g(seed);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t x = g();
+    std::memcpy(&b[i], &x, 8);
+  }
+  for (; i < n; ++i) b[i] = static_cast<uint8_t>(g());
+  return b;
+}
+
+static void emit_case(bool& first, const char* name, size_t size, Lat& l) {
+  std::printf("%s\n    \"%s_%zu\": {\"mean_us\": %.2f, \"p50_us\": %.2f, \"p99_us\": %.2f, \"MBps\": %.1f}",
+              first ? "" : ",", name, size, l.mean() * 1e6, l.pct(0.5) * 1e6, l.pct(0.99) * 1e6,
+              l.mean() > 0 ? size / l.mean() / (1 << 20) : 0.0);
+  first = false;
+}
+
+int main(int argc, char** argv) {
+  int device = 0, iters = 50;
+  bool fsync = true;
+  std::string dir = "/tmp/io_bench_store";
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--device" && i + 1 < argc) device = std::atoi(argv[++i]);
+    else if (a == "--dir" && i + 1 < argc) dir = argv[++i];
+    else if (a == "--iters" && i + 1 < argc) iters = std::atoi(argv[++i]);
+    else if (a == "--no-fsync") fsync = false;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) device = -1;
+  std::filesystem::remove_all(dir);
+
+  std::printf("{\n  \"device\": %d, \"iters\": %d, \"fsync\": %s,\n  \"store\": {", device, iters,
+              fsync ? "true" : "false");
+  bool first = true;
+  const size_t sizes[] = {4096, 65536, 1 << 20, 64u << 20};
+  for (int mode = 0; mode < 2; ++mode) {
+    StoreConfig cfg;
+    cfg.storage_dir = dir + (mode == 0 ? "/nvme" : "/hbm");
+    cfg.device = device;
+    cfg.hbm_capacity = device >= 0 ? (8ull << 30) : 0;
+    cfg.durability = mode == 0 ? Durability::NvmeSync : Durability::HbmAck;
+    cfg.sync_writes = fsync;
+    ChunkStore store(cfg);
+    const char* tag = mode == 0 ? "write_nvme_sync" : "write_hbm_ack";
+    for (size_t sz : sizes) {
+      int n = sz >= (64u << 20) ? std::max(3, iters / 10) : iters;
+      auto data = random_bytes(sz, static_cast<uint32_t>(sz + mode));
+      uint32_t crc = crc32(data.data(), sz);
+      Lat w, r, pr;
+      std::vector<uint8_t> out(sz);
+      for (int i = 0; i < n; ++i) {
+        std::string id = std::string("b") + std::to_string(mode) + "_" + std::to_string(sz) + "_" + std::to_string(i);
+        auto t0 = Clock::now();
+        WriteResult wr = store.write(id, data.data(), sz, crc);
+        auto t1 = Clock::now();
+        if (!wr.ok) {
+          std::fprintf(stderr, "write failed: %s\n", wr.error.c_str());
+          return 1;
+        }
+        w.add(secs(t0, t1));
+        t0 = Clock::now();
+        ReadResult rr = store.read_into(id, 0, sz, out.data());
+        t1 = Clock::now();
+        if (rr.status != ReadStatus::Ok || std::memcmp(out.data(), data.data(), sz) != 0) {
+          std::fprintf(stderr, "read mismatch (%s)\n", rr.error.c_str());
+          return 1;
+        }
+        r.add(secs(t0, t1));
+        if (sz >= 65536) {
+          t0 = Clock::now();
+          rr = store.read_into(id, 32768, 4096, out.data());
+          t1 = Clock::now();
+          if (rr.status != ReadStatus::Ok || std::memcmp(out.data(), data.data() + 32768, 4096) != 0) {
+            std::fprintf(stderr, "partial read mismatch\n");
+            return 1;
+          }
+          pr.add(secs(t0, t1));
+        }
+      }
+      emit_case(first, tag, sz, w);
+      emit_case(first, mode == 0 ? "read_after_nvme_sync" : "read_after_hbm_ack", sz, r);
+      if (sz >= 65536) emit_case(first, mode == 0 ? "partial4k_nvme" : "partial4k_hbm", sz, pr);
+    }
+    store.flush();
+    if (mode == 0) {
+      auto t0 = Clock::now();
+      auto bad = store.scrub();
+      auto t1 = Clock::now();
+      StoreStats st = store.stats();
+      std::printf(",\n    \"scrub\": {\"blocks\": %llu, \"bytes\": %llu, \"seconds\": %.4f, \"GBps\": %.2f, \"bad\": %zu}",
+                  static_cast<unsigned long long>(st.blocks), static_cast<unsigned long long>(st.bytes),
+                  secs(t0, t1), st.bytes / std::max(1e-9, secs(t0, t1)) / 1e9, bad.size());
+    }
+  }
+  std::printf("\n  },\n");
+
+  // ---- CRC: GPU (H2D + K1/K2) vs CPU PCLMUL, 256 MiB
+  {
+    const size_t n = 256u << 20;
+    auto data = random_bytes(n, 7);
+    auto t0 = Clock::now();
+    uint32_t cpu = crc32(data.data(), n);
+    auto t1 = Clock::now();
+    double cpu_s = secs(t0, t1);
+    double gpu_s = 0;
+    uint32_t gpu = cpu;
+    if (device >= 0) {
+      StoreConfig cfg;
+      cfg.storage_dir = dir + "/crc";
+      cfg.device = device;
+      cfg.hbm_capacity = 1ull << 30;
+      ChunkStore s(cfg);
+      std::vector<uint32_t> sl;
+      s.gpu_crc(data.data(), 1 << 20, &sl);  // warm-up (tables, lanes)
+      t0 = Clock::now();
+      gpu = s.gpu_crc(data.data(), n, &sl);
+      t1 = Clock::now();
+      gpu_s = secs(t0, t1);
+    }
+    std::printf("  \"crc32_256MiB\": {\"cpu_GBps\": %.2f, \"gpu_incl_h2d_GBps\": %.2f, \"match\": %s},\n",
+                n / cpu_s / 1e9, gpu_s > 0 ? n / gpu_s / 1e9 : 0.0, cpu == gpu ? "true" : "false");
+  }
+
+  // ---- RS(6,3) encode of 6 x 16 MiB shards: GPU vs CPU
+  {
+    const int k = 6, m = 3;
+    const size_t len = 16u << 20;
+    gf::Matrix full = gf::rs_matrix(k, m);
+    gf::Matrix parity(full.begin() + k, full.end());
+    std::vector<std::vector<uint8_t>> in(k), out_c(m, std::vector<uint8_t>(len)), out_g(m, std::vector<uint8_t>(len));
+    std::vector<const uint8_t*> ip;
+    std::vector<uint8_t*> oc, og;
+    for (int i = 0; i < k; ++i) {
+      in[i] = random_bytes(len, 100 + i);
+      ip.push_back(in[i].data());
+    }
+    for (int i = 0; i < m; ++i) {
+      oc.push_back(out_c[i].data());
+      og.push_back(out_g[i].data());
+    }
+    auto t0 = Clock::now();
+    gf::matmul_cpu(parity, ip.data(), oc.data(), len);
+    auto t1 = Clock::now();
+    double cpu_s = secs(t0, t1), gpu_s = 0;
+    bool match = true;
+    if (device >= 0) {
+      StoreConfig cfg;
+      cfg.storage_dir = dir + "/rs";
+      cfg.device = device;
+      cfg.hbm_capacity = 1ull << 30;
+      ChunkStore s(cfg);
+      s.gf_matmul_gpu(parity, ip, og, 4096);  // warm-up
+      t0 = Clock::now();
+      s.gf_matmul_gpu(parity, ip, og, len);
+      t1 = Clock::now();
+      gpu_s = secs(t0, t1);
+      for (int i = 0; i < m; ++i) match = match && out_c[i] == out_g[i];
+    }
+    std::printf("  \"rs63_encode_96MiB\": {\"cpu_GBps\": %.2f, \"gpu_incl_copies_GBps\": %.2f, \"match\": %s}\n}\n",
+                k * len / cpu_s / 1e9, gpu_s > 0 ? k * len / gpu_s / 1e9 : 0.0, match ? "true" : "false");
+  }
+  std::filesystem::remove_all(dir);
+  return 0;
+}

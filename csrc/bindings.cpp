@@ -8,6 +8,7 @@
 #include "chunk_store.h"
 #include "crc32.h"
 #include "crypto.h"
+#include "fastpath.h"
 #include "gf256.h"
 #include "rccl_engine.h"
 #include "wal.h"
@@ -304,6 +305,38 @@ PYBIND11_MODULE(_dfs_native, m) {
       });
 
   // ---------------- RCCL replication
+  py::class_<FastPathServer>(m, "FastPathServer")
+      .def(py::init<ChunkStore*, std::string>(), py::arg("store"), py::arg("name"), py::keep_alive<1, 2>())
+      .def("start", [](FastPathServer& f) {
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = f.start(&err);
+        }
+        return py::make_tuple(ok, err);
+      })
+      .def("stop", &FastPathServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("name", &FastPathServer::name)
+      .def("fence", [](FastPathServer& f, uint64_t term) {
+        uint64_t known = 0;
+        bool ok = f.fence(term, &known);
+        return py::make_tuple(ok, known);
+      })
+      .def("adopt_term", &FastPathServer::adopt_term)
+      .def_property_readonly("term", &FastPathServer::term)
+      .def("drain_suspects", &FastPathServer::drain_suspects)
+      .def("stats", [](FastPathServer& f) {
+        FpStats s = f.stats();
+        py::dict d;
+        d["fp_writes"] = s.writes;
+        d["fp_reads"] = s.reads;
+        d["fp_fenced"] = s.fenced;
+        d["fp_punts"] = s.punts;
+        d["fp_connections"] = s.connections;
+        return d;
+      });
+
   py::class_<RcclEngine>(m, "RcclEngine")
       .def(py::init<ChunkStore*, int, int, std::string, int>(), py::keep_alive<1, 2>(), py::arg("store"),
            py::arg("rank"), py::arg("world"), py::arg("rendezvous_dir"), py::arg("timeout_ms") = 30000)

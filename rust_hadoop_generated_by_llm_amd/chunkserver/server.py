@@ -58,6 +58,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--scrub-interval", type=float, default=60.0)
     p.add_argument("--no-fsync", action="store_true", help="skip fdatasync (tests only)")
     p.add_argument("--workers", type=int, default=64)
+    p.add_argument("--no-fastpath", action="store_true", help="disable the native local UNIX-socket data path")
     return p
 
 
@@ -119,8 +120,17 @@ class ChunkServerProcess:
             else:
                 log.error("RCCL init failed (%s); using gRPC replication", err)
         self.metrics = Registry()
+        self.fastpath = None
+        if not args.no_fastpath:
+            port = strip_scheme(args.addr).rsplit(":", 1)[-1]
+            fp = native.FastPathServer(self.store, f"dfs_fp_{os.getpid()}_{port}")
+            ok, err = fp.start()
+            if ok:
+                self.fastpath = fp
+            else:
+                log.warning("native fast path disabled: %s", err)
         self.cs = ChunkServer(self.store, self.advertise, self.pool, self.masters, self.rccl, rank_map,
-                              args.rccl_rank, self.metrics)
+                              args.rccl_rank, self.metrics, fastpath=self.fastpath)
         self._setup_metrics()
         self._stop = threading.Event()
 
@@ -167,6 +177,9 @@ class ChunkServerProcess:
             self.refresh_shard_map()
         used, avail = self.disk_stats()
         st = self.store.stats()
+        if self.fastpath is not None:
+            for bid in self.fastpath.drain_suspects():  # partial-read corruption seen natively
+                self.cs.queue_recovery(bid)
         bad, new = self.cs.drain_reports()
         req = pb.HeartbeatRequest(chunk_server_address=self.advertise, used_space=used, available_space=avail,
                                   chunk_count=st["blocks"], bad_blocks=bad, rack_id=self.args.rack_id,
@@ -217,6 +230,8 @@ class ChunkServerProcess:
                 elif self.path == "/stats":
                     d = dict(proc.store.stats())
                     d.update(proc.cs.stats)
+                    if proc.fastpath is not None:
+                        d.update(proc.fastpath.stats())
                     body, ctype = json.dumps(d).encode(), "application/json"
                 elif self.path.startswith("/debug/") and os.environ.get("DFS_DEBUG_ENDPOINTS") == "1":
                     # fault injection for tests (off unless DFS_DEBUG_ENDPOINTS=1):

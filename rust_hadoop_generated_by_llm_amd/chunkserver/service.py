@@ -31,8 +31,11 @@ ST_OK, ST_NOT_FOUND, ST_OUT_OF_RANGE, ST_CORRUPT, ST_IO = 0, 1, 2, 3, 4
 
 class ChunkServer:
     def __init__(self, store, advertise_addr: str, pool: ChannelPool, masters_fn, rccl=None,
-                 rank_map: dict[str, int] | None = None, my_rank: int = -1, metrics=None):
+                 rank_map: dict[str, int] | None = None, my_rank: int = -1, metrics=None, fastpath=None):
         self.store = store
+        # native local data path (csrc/fastpath.cpp); when present it owns the fencing term
+        self.fastpath = fastpath
+        self.fastpath_socket = fastpath.name if fastpath is not None else ""
         self.addr = advertise_addr
         self.pool = pool
         self.masters_fn = masters_fn  # () -> list of master addresses
@@ -53,6 +56,13 @@ class ChunkServer:
 
     # ------------------------------------------------------------------ fencing
     def fence(self, term: int) -> None:
+        if self.fastpath is not None:
+            ok, known = self.fastpath.fence(term)
+            self.known_term = known
+            if not ok:
+                raise RpcStatus(StatusCode.FAILED_PRECONDITION,
+                                f"Stale master term: request has {term} but known term is {known}")
+            return
         with self._term_lock:
             known = self.known_term
             if 0 < term < known:
@@ -62,9 +72,16 @@ class ChunkServer:
                 self.known_term = term
 
     def adopt_term(self, term: int) -> None:
+        if self.fastpath is not None:
+            self.fastpath.adopt_term(term)
+            self.known_term = self.fastpath.term
+            return
         with self._term_lock:
             if term > self.known_term:
                 self.known_term = term
+
+    def queue_recovery(self, block_id: str) -> None:
+        self._bg.submit(self.recover_block, block_id)
 
     # ------------------------------------------------------------------ forwarding
     def _rank_of(self, addr: str) -> int | None:
@@ -173,7 +190,8 @@ class ChunkServer:
         if not ok:
             return pb.WriteBlockResponse(success=False, error_message=err)
         self.stats["writes"] += 1
-        return pb.WriteBlockResponse(success=True, replicas_written=replicas)
+        return pb.WriteBlockResponse(success=True, replicas_written=replicas,
+                                     fastpath_socket=self.fastpath_socket if req.shm_path else "")
 
     def replicate_block(self, req, ctx):
         self.fence(req.master_term)
@@ -221,7 +239,8 @@ class ChunkServer:
             self._bg.submit(self.recover_block, req.block_id)
         self.stats["reads"] += 1
         self.stats["shm_reads"] += 1
-        return pb.ReadBlockResponse(bytes_read=n, total_size=total, shm_filled=True)
+        return pb.ReadBlockResponse(bytes_read=n, total_size=total, shm_filled=True,
+                                    fastpath_socket=self.fastpath_socket)
 
     def read_block(self, req, ctx):
         if req.shm_path:

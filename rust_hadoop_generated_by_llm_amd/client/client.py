@@ -28,6 +28,7 @@ from ..ops import crc as crcops
 from ..ops import erasure
 from ..parallel.sharding import ShardMap
 from ..utils.rpc import ChannelPool, rpc_code, rpc_details, strip_scheme, with_scheme
+from ..utils import fastpath as fpmod
 from ..utils.shm import ShmArena
 
 log = logging.getLogger("dfs.client")
@@ -73,6 +74,17 @@ class Client:
         self._arena: ShmArena | None = None
         self._arena_lock = threading.Lock()
         self.sc_ops = 0
+        # native local data path of the co-located chunkserver (learned from its replies)
+        self.fastpath: fpmod.FastPathClient | None = None
+        self.fp_ops = 0
+        # optional per-phase latency capture (benchmarks): {"create": [...], "write": [...], ...}
+        self.phase_times: dict[str, list[float]] | None = None
+
+    def _phase(self, name: str, t0: float) -> float:
+        t1 = time.perf_counter()
+        if self.phase_times is not None:
+            self.phase_times.setdefault(name, []).append(t1 - t0)
+        return t1
 
     # ------------------------------------------------------------------ short-circuit I/O
     def _shm(self) -> ShmArena | None:
@@ -88,6 +100,16 @@ class Client:
                         self.short_circuit = False
                         return None
         return self._arena
+
+    def _learn_fastpath(self, resp) -> None:
+        name = getattr(resp, "fastpath_socket", "")
+        if name and (self.fastpath is None or self.fastpath.name != name) and \
+                os.environ.get("DFS_NO_FASTPATH") != "1":
+            self.fastpath = fpmod.FastPathClient(name)
+
+    def _fp_failed(self, e: Exception) -> None:
+        log.info("native fast path unavailable (%s); using gRPC", e)
+        self.fastpath = None
 
     def _sc_failed(self, e: Exception) -> bool:
         if rpc_code(e) == grpc.StatusCode.FAILED_PRECONDITION and "short-circuit" in rpc_details(e):
@@ -262,9 +284,16 @@ class Client:
 
     def _create_and_allocate(self, dest: str, ec_d: int = 0, ec_p: int = 0):
         resp, addr = self.execute_rpc(dest, "CreateFile", pb.CreateFileRequest(
-            path=dest, ec_data_shards=ec_d, ec_parity_shards=ec_p), self._not_leader_check)
+            path=dest, ec_data_shards=ec_d, ec_parity_shards=ec_p, allocate_block=True,
+            preferred_chunk_server=self.local_chunkserver or ""), self._not_leader_check)
         if not resp.success:
             raise DfsError(f"Failed to create file: {resp.error_message}")
+        if resp.HasField("allocation") and resp.allocation.HasField("block"):
+            alloc = resp.allocation  # fused create+allocate (one RPC, one Raft entry)
+            if not alloc.chunk_server_addresses:
+                raise DfsError("No chunk servers available")
+            return alloc
+        # a master without the extension: the reference's separate AllocateBlock RPC
         masters = [addr] + [m for m in self.master_addrs if m != addr]
 
         def alloc_check(r):
@@ -290,10 +319,13 @@ class Client:
     def create_file_from_buffer(self, data: bytes, dest: str) -> int:
         """CreateFile -> AllocateBlock -> WriteBlock(chain) -> CompleteFile. Returns
         replicas_written (reference mod.rs:225-494)."""
+        t = time.perf_counter()
         alloc = self._create_and_allocate(dest)
+        t = self._phase("create", t)
         block = alloc.block
         servers = list(alloc.chunk_server_addresses)
         crc = crcops.crc32(data)
+        t = self._phase("crc", t)
         # MD5 is a strictly sequential chain (one core per object): run it while the block
         # is on the wire instead of before it (hashlib releases the GIL); it is only
         # needed for CompleteFile.
@@ -304,13 +336,29 @@ class Client:
         if slot is not None:
             try:
                 arena.view[slot:slot + len(data)] = data
-                req = pb.WriteBlockRequest(block_id=block.block_id, next_servers=servers[1:],
-                                           expected_checksum_crc32c=crc, shard_index=-1,
-                                           master_term=alloc.master_term, shm_path=arena.path, shm_offset=slot,
-                                           shm_length=len(data))
-                resp = self.pool.call(self._cs(servers[0]), "ChunkServerService", "WriteBlock", req,
-                                      timeout=self.data_timeout)
-                self.sc_ops += 1
+                fp = self.fastpath
+                if fp is not None and len(servers) == 1:
+                    # last hop of the chain on this host: the native UNIX-socket data path
+                    try:
+                        st, msg = fp.write(block.block_id, arena.path, slot, len(data), crc, alloc.master_term)
+                        if st == fpmod.OK:
+                            resp = pb.WriteBlockResponse(success=True, replicas_written=1)
+                            self.fp_ops += 1
+                        elif st == fpmod.FENCED:
+                            raise DfsError(f"Failed to write block: {msg}")
+                        elif st == fpmod.IO_ERROR:
+                            resp = pb.WriteBlockResponse(success=False, error_message=msg)
+                    except fpmod.FastPathError as e:
+                        self._fp_failed(e)
+                if resp is None:
+                    req = pb.WriteBlockRequest(block_id=block.block_id, next_servers=servers[1:],
+                                               expected_checksum_crc32c=crc, shard_index=-1,
+                                               master_term=alloc.master_term, shm_path=arena.path, shm_offset=slot,
+                                               shm_length=len(data))
+                    resp = self.pool.call(self._cs(servers[0]), "ChunkServerService", "WriteBlock", req,
+                                          timeout=self.data_timeout)
+                    self._learn_fastpath(resp)
+                    self.sc_ops += 1
             except grpc.RpcError as e:
                 if not self._sc_failed(e):
                     raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
@@ -324,13 +372,16 @@ class Client:
                                       timeout=self.data_timeout)
             except grpc.RpcError as e:
                 raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
+        t = self._phase("write", t)
         etag = md5_fut.result()
+        t = self._phase("md5_wait", t)
         if not resp.success:
             raise DfsError(f"Failed to write block: {resp.error_message}")
         if resp.replicas_written < len(servers):
             log.warning("block written to %d/%d replicas", resp.replicas_written, len(servers))
         self._complete(dest, len(data), etag, [pb.BlockChecksumInfo(block_id=block.block_id, checksum_crc32c=crc,
                                                                     actual_size=len(data))])
+        self._phase("complete", t)
         return resp.replicas_written
 
     def create_file_from_buffer_ec(self, data: bytes, dest: str, ec_data_shards: int, ec_parity_shards: int) -> None:
@@ -374,10 +425,21 @@ class Client:
             slot = arena.acquire(want) if arena is not None else None
             if slot is not None:
                 try:
+                    fp = self.fastpath
+                    if fp is not None:
+                        try:
+                            st, _total, n, _msg = fp.read(block_id, offset, length, arena.path, slot, arena.slot)
+                            if st in (fpmod.OK, fpmod.PARTIAL_CORRUPT):
+                                self.fp_ops += 1
+                                return bytes(arena.view[slot:slot + n])
+                        except fpmod.FastPathError as e:
+                            self._fp_failed(e)
+                        # any other status: the gRPC call below reports/recovers it
                     r = self.pool.call(self._cs(location), "ChunkServerService", "ReadBlock",
                                        pb.ReadBlockRequest(block_id=block_id, offset=offset, length=length,
                                                            shm_path=arena.path, shm_offset=slot,
                                                            shm_capacity=arena.slot), timeout=self.data_timeout)
+                    self._learn_fastpath(r)
                     if r.shm_filled:
                         self.sc_ops += 1
                         return bytes(arena.view[slot:slot + r.bytes_read])
@@ -450,7 +512,9 @@ class Client:
         return self.read_block_range(block.locations, block.block_id, size_hint=block.size or None)
 
     def get_file_content(self, path: str) -> bytes:
+        t = time.perf_counter()
         meta = self.get_file_info(path)
+        t = self._phase("getinfo", t)
         if meta is None:
             raise DfsError("File not found")
         if meta.size == 0:
@@ -458,7 +522,9 @@ class Client:
             # 0-byte block as OUT_OF_RANGE (reference semantics), so never ask for it
             return b""
         if len(meta.blocks) == 1:
-            return self.fetch_single_block(meta.blocks[0])
+            data = self.fetch_single_block(meta.blocks[0])
+            self._phase("read", t)
+            return data
         parts = list(self._exec.map(self.fetch_single_block, meta.blocks))
         return b"".join(parts)
 

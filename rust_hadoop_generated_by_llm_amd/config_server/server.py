@@ -11,6 +11,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import logging
 import os
 import signal
 import time
@@ -24,7 +25,10 @@ from ..raft.node import NotLeader, RaftNode
 from ..raft.transport import HttpTransport
 from ..utils import log as logsetup
 from ..utils.metrics import Registry
+from ..utils.localrpc import serve_local
 from ..utils.rpc import RpcStatus, StatusCode, make_aio_server, server_credentials, with_scheme
+
+log = logging.getLogger("dfs.config_server")
 
 
 class ConfigState:
@@ -205,8 +209,15 @@ async def run(args) -> None:
     runner = web.AppRunner(app, access_log=None)
     await runner.setup()
     await web.TCPSite(runner, host, args.http_port, reuse_address=True).start()
-    server = make_aio_server({"ConfigService": svc}, args.addr, server_credentials(args.tls_cert, args.tls_key))
+    creds = server_credentials(args.tls_cert, args.tls_key)
+    server = make_aio_server({"ConfigService": svc}, args.addr, creds)
     await server.start()
+    local_srv = None
+    if creds is None and os.environ.get("DFS_NO_LOCALRPC") != "1":
+        try:
+            local_srv = await serve_local({"ConfigService": svc}, args.addr.rsplit(":", 1)[-1])
+        except OSError as e:
+            log.warning("local RPC listener unavailable: %s", e)
     await raft.start()
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()

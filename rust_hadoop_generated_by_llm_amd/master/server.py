@@ -7,6 +7,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import json
+import logging
 import os
 import signal
 import ssl
@@ -19,11 +20,14 @@ from ..raft.node import RaftNode
 from ..raft.transport import HttpTransport
 from ..utils import log as logsetup
 from ..utils.metrics import Registry
+from ..utils.localrpc import serve_local
 from ..utils.rpc import AioChannelPool, make_aio_server, server_credentials, with_scheme
 from .background import Intervals, MasterBackground
 from .monitor import ThroughputMonitor
 from .service import MasterService
 from .state import MasterState
+
+log = logging.getLogger("dfs.master.server")
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -147,6 +151,11 @@ class MasterProcess:
         creds = server_credentials(a.tls_cert, a.tls_key)
         server = make_aio_server({"MasterService": self.svc}, a.addr if ":" in a.addr else f"0.0.0.0:{a.addr}", creds)
         await server.start()
+        if creds is None and os.environ.get("DFS_NO_LOCALRPC") != "1":
+            try:  # same-host clients skip HTTP/2 (utils/localrpc.py)
+                self._local_srv = await serve_local({"MasterService": self.svc}, a.addr.rsplit(":", 1)[-1])
+            except OSError as e:
+                log.warning("local RPC listener unavailable: %s", e)
         await self.raft.start()
         if self.config_servers:
             await self.bg.register()
@@ -174,6 +183,18 @@ class MasterProcess:
 def main(argv=None) -> None:
     args = build_parser().parse_args(argv)
     logsetup.setup("master")
+    prof_path = os.environ.get("DFS_CPROFILE")  # perf investigations: dump cProfile stats on exit
+    if prof_path:
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
+        try:
+            asyncio.run(MasterProcess(args).run(os.environ.get("DFS_READY_FILE")))
+        finally:
+            prof.disable()
+            prof.dump_stats(f"{prof_path}.{os.getpid()}")
+        return
     asyncio.run(MasterProcess(args).run(os.environ.get("DFS_READY_FILE")))
 
 

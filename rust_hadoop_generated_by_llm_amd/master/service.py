@@ -165,9 +165,16 @@ class MasterService:
         await self.wait_unlocked(req.path)
         if req.path in self.state.files and req.path not in self.state.under_construction:
             return pb.CreateFileResponse(success=False, error_message="File already exists")
+        args = {"path": req.path, "ec_data_shards": req.ec_data_shards, "ec_parity_shards": req.ec_parity_shards,
+                "ts": now_ms()}
+        selected = None
+        if req.allocate_block:
+            # extension: CreateFile + AllocateBlock as ONE Raft entry and one round trip
+            # (the reference client always issues both RPCs back to back)
+            selected = self._place(req.ec_data_shards, req.ec_parity_shards, req.preferred_chunk_server)
+            args.update(block_id=str(uuid.uuid4()), locations=selected)
         try:
-            res = await self._propose_unlocked("CreateFile", {"path": req.path, "ec_data_shards": req.ec_data_shards,
-                                                     "ec_parity_shards": req.ec_parity_shards, "ts": now_ms()})
+            res = await self._propose_unlocked("CreateFile", args)
         except NotLeader as e:
             return pb.CreateFileResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
         if isinstance(res, dict):
@@ -175,6 +182,11 @@ class MasterService:
                 return pb.CreateFileResponse(success=False, error_message="File already exists")
             if res.get("orphans"):
                 self._queue_block_gc(res["orphans"])
+        if selected is not None:
+            m = self.state.files.get(req.path)
+            ec_d, ec_p = (m.ec_data_shards, m.ec_parity_shards) if m is not None else (0, 0)
+            return pb.CreateFileResponse(success=True, allocation=self._allocation(args["block_id"], selected,
+                                                                                   ec_d, ec_p))
         return pb.CreateFileResponse(success=True)
 
     async def delete_file(self, req, ctx):
@@ -211,6 +223,21 @@ class MasterService:
         if m is None:
             raise RpcStatus(StatusCode.NOT_FOUND, "File not found")
         ec_d, ec_p = m.ec_data_shards, m.ec_parity_shards
+        selected = self._place(ec_d, ec_p, req.preferred_chunk_server)
+        block_id = str(uuid.uuid4())
+        try:
+            await self._propose("AllocateBlock", {"path": req.path, "block_id": block_id, "locations": selected})
+        except NotLeader as e:
+            return pb.AllocateBlockResponse(leader_hint=e.hint)
+        return self._allocation(block_id, selected, ec_d, ec_p)
+
+    def _allocation(self, block_id: str, selected: list[str], ec_d: int, ec_p: int):
+        blk = pb.BlockInfo(block_id=block_id, locations=selected, ec_data_shards=ec_d, ec_parity_shards=ec_p)
+        return pb.AllocateBlockResponse(block=blk, chunk_server_addresses=selected, ec_data_shards=ec_d,
+                                        ec_parity_shards=ec_p, master_term=self.raft.current_term)
+
+    def _place(self, ec_d: int, ec_p: int, preferred: str) -> list[str]:
+        """Pick the chunkservers for a new block (rack-aware, writer-local first)."""
         cands = list(self.state.chunk_servers.items())
         if ec_d > 0 and ec_p > 0:
             total = ec_d + ec_p
@@ -222,18 +249,11 @@ class MasterService:
             needed = min(REPLICATION_FACTOR, len(cands))
         if needed == 0:
             raise RpcStatus(StatusCode.UNAVAILABLE, "No chunk servers available")
-        preferred = req.preferred_chunk_server if not (ec_d > 0 and ec_p > 0) else None
+        preferred = preferred if not (ec_d > 0 and ec_p > 0) else None
         selected = select_servers_rack_aware(cands, needed, preferred or None)
         for a in selected:
             self.state.chunk_servers[a].scheduled += SCHEDULE_QUANTUM
-        block_id = str(uuid.uuid4())
-        try:
-            await self._propose("AllocateBlock", {"path": req.path, "block_id": block_id, "locations": selected})
-        except NotLeader as e:
-            return pb.AllocateBlockResponse(leader_hint=e.hint)
-        blk = pb.BlockInfo(block_id=block_id, locations=selected, ec_data_shards=ec_d, ec_parity_shards=ec_p)
-        return pb.AllocateBlockResponse(block=blk, chunk_server_addresses=selected, ec_data_shards=ec_d,
-                                        ec_parity_shards=ec_p, master_term=self.raft.current_term)
+        return selected
 
     async def complete_file(self, req, ctx):
         self.check_shard_ownership(req.path)

@@ -232,8 +232,13 @@ class MasterState:
             started = self.under_construction.get(path)
             if started is None or ts - started < CREATE_LEASE_MS:
                 return {"exists": True}
-        self._put(path, pb.FileMetadata(path=path, ec_data_shards=a.get("ec_data_shards", 0),
-                                        ec_parity_shards=a.get("ec_parity_shards", 0)))
+        m = pb.FileMetadata(path=path, ec_data_shards=a.get("ec_data_shards", 0),
+                            ec_parity_shards=a.get("ec_parity_shards", 0))
+        if a.get("block_id"):
+            b = m.blocks.add(block_id=a["block_id"], ec_data_shards=m.ec_data_shards,
+                             ec_parity_shards=m.ec_parity_shards)
+            b.locations.extend(a.get("locations", []))
+        self._put(path, m)
         self.under_construction[path] = ts
         return {"exists": False, "orphans": [(b.block_id, list(b.locations)) for b in old.blocks] if old else []}
 

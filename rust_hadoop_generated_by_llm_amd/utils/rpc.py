@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import contextvars
 import inspect
+import os
 import re
 import threading
 import uuid
@@ -158,6 +159,9 @@ def with_scheme(addr: str, tls: bool = False) -> str:
     return ("https://" if tls else "http://") + addr
 
 
+LOCAL_SERVICES = frozenset({"MasterService", "ConfigService"})
+
+
 class ChannelPool:
     """Persistent channels keyed by (target, tls). Thread-safe; shared per process."""
 
@@ -170,6 +174,13 @@ class ChannelPool:
                 self._ca = f.read()
         self._domain = domain_name
         self._callables: dict[tuple[str, str, str], Callable] = {}
+        # same-host fast transport for metadata services (utils/localrpc.py)
+        self._local = None
+        if os.environ.get("DFS_NO_LOCALRPC") != "1" and ca_cert is None:
+            from .localrpc import LocalRegistry
+
+            self._local = LocalRegistry()
+        self._resp_cls: dict[tuple[str, str], Any] = {}
 
     def channel(self, addr: str) -> grpc.Channel:
         key = addr
@@ -210,6 +221,20 @@ class ChannelPool:
     def call(self, addr: str, service: str, method: str, request, timeout: float | None = 30.0,
              request_id: str | None = None):
         rid = request_id or current_request_id.get() or uuid.uuid4().hex
+        if self._local is not None and service in LOCAL_SERVICES:
+            lc = self._local.client_for(addr)
+            if lc is not None:
+                key = (service, method)
+                rc = self._resp_cls.get(key)
+                if rc is None:
+                    rc = next(rs for name, _rq, rs in pb.SERVICES[service] if name == method)
+                    self._resp_cls[key] = rc
+                try:
+                    return lc.call(pb.method_path(service, method), request, rc, timeout, rid)
+                except grpc.RpcError:
+                    raise
+                except OSError:
+                    self._local.forget(addr)  # listener gone: plain gRPC from now on
         return self.callable(addr, service, method)(request, timeout=timeout, metadata=((REQUEST_ID_HEADER, rid),))
 
     def drop(self, addr: str) -> None:

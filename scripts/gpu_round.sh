@@ -19,6 +19,15 @@ fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
   timeout -k 10 600 python bench.py --steps 3 --warmup 1 --profile-dir gpurun_out/prof > gpurun_out/bench_prof.json 2> gpurun_out/bench_prof.err || exit $?
 fi
+if [ "$STEP" = "all" ] || [ "$STEP" = "micro" ]; then
+  # native I/O + kernel microbenchmark (C45) under a kernel trace
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+     -d "$OLDPWD/gpurun_out/prof_io" -o io -- "$OLDPWD/build/native/io_bench" --iters 30) \
+     > gpurun_out/io_bench.json 2> gpurun_out/io_bench.err || exit $?
+fi
+if [ "$STEP" = "quick" ]; then
+  timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || exit $?
+fi
 if [ "$STEP" = "multi" ]; then
   # N=2 rehearsal on a single GPU: two ranks share the device, gRPC replication
   timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

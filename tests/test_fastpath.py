@@ -1,0 +1,148 @@
+"""Native local data path (csrc/fastpath.cpp) on a host-mode ChunkStore: write/read through
+a /dev/shm arena slot over the abstract UNIX socket, epoch fencing shared with the gRPC
+service, status codes that send the client back to gRPC, and path validation."""
+import os
+import zlib
+
+import pytest
+
+from rust_hadoop_generated_by_llm_amd.utils import fastpath as fp
+from rust_hadoop_generated_by_llm_amd.utils.shm import ShmArena
+
+
+@pytest.fixture()
+def server(native, tmp_path):
+    store = native.ChunkStore(str(tmp_path / "data"), "", -1, 0, 0, 100, 2, 1, False)
+    srv = native.FastPathServer(store, f"dfs_fp_test_{os.getpid()}_{id(tmp_path)}")
+    ok, err = srv.start()
+    assert ok, err
+    yield store, srv
+    srv.stop()
+
+
+def test_write_read_roundtrip(server):
+    store, srv = server
+    arena = ShmArena(size=32 << 20, slot=16 << 20)
+    cli = fp.FastPathClient(srv.name)
+    try:
+        data = os.urandom(3 * 1000 * 1000 + 17)
+        slot = arena.acquire(len(data))
+        arena.view[slot:slot + len(data)] = data
+        st, msg = cli.write("blk1", arena.path, slot, len(data), zlib.crc32(data), 5)
+        assert st == fp.OK, msg
+        assert store.exists("blk1") and store.size("blk1") == len(data)
+        # wrong CRC: the store rejects it, reported as IO_ERROR (client falls back / fails)
+        st, msg = cli.write("blk2", arena.path, slot, len(data), zlib.crc32(data) ^ 1, 5)
+        assert st == fp.IO_ERROR and "mismatch" in msg.lower()
+        out = arena.acquire(1 << 20)
+        st, total, n, _ = cli.read("blk1", 1000, 5000, arena.path, out, arena.slot)
+        assert st == fp.OK and total == len(data) and n == 5000
+        assert bytes(arena.view[out:out + n]) == data[1000:6000]
+        st, total, n, _ = cli.read("missing", 0, 0, arena.path, out, arena.slot)
+        assert st == fp.NOT_FOUND
+        st, total, n, _ = cli.read("blk1", len(data) + 5, 10, arena.path, out, arena.slot)
+        assert st == fp.OUT_OF_RANGE
+        # a full read larger than the slot capacity is punted to gRPC
+        st, *_ = cli.read("blk1", 0, 0, arena.path, out, 1024)
+        assert st == fp.UNSUPPORTED
+        assert srv.stats()["fp_writes"] == 1 and srv.stats()["fp_reads"] == 1
+    finally:
+        cli.close()
+        arena.close()
+
+
+def test_fencing_is_shared(server):
+    _store, srv = server
+    arena = ShmArena(size=16 << 20, slot=16 << 20)
+    cli = fp.FastPathClient(srv.name)
+    try:
+        srv.adopt_term(7)
+        assert srv.term == 7
+        slot = arena.acquire(10)
+        arena.view[slot:slot + 10] = b"0123456789"
+        st, msg = cli.write("old", arena.path, slot, 10, zlib.crc32(b"0123456789"), 3)
+        assert st == fp.FENCED and "Stale master term" in msg
+        assert srv.fence(9) == (True, 9)      # higher term adopted
+        assert srv.fence(0) == (True, 9)      # term 0 = unfenced (legacy clients)
+        assert srv.fence(8) == (False, 9)
+        st, _ = cli.write("new", arena.path, slot, 10, zlib.crc32(b"0123456789"), 9)
+        assert st == fp.OK
+    finally:
+        cli.close()
+        arena.close()
+
+
+def test_rejects_foreign_paths_and_corruption_punts(server, tmp_path):
+    store, srv = server
+    cli = fp.FastPathClient(srv.name)
+    arena = ShmArena(size=16 << 20, slot=16 << 20)
+    try:
+        st, msg = cli.write("x", "/etc/passwd", 0, 10, 0, 0)
+        assert st == fp.UNSUPPORTED and "refusing" in msg
+        st, msg = cli.write("x", "/dev/shm/dfs_sc_../../etc/passwd", 0, 10, 0, 0)
+        assert st == fp.UNSUPPORTED
+        data = os.urandom(100_000)
+        slot = arena.acquire(len(data))
+        arena.view[slot:slot + len(data)] = data
+        assert cli.write("c", arena.path, slot, len(data), zlib.crc32(data), 0)[0] == fp.OK
+        assert store.debug_corrupt("c", 50_000)
+        store.drop_resident()
+        st, *_ = cli.read("c", 0, 0, arena.path, slot, arena.slot)
+        assert st == fp.CORRUPT  # whole-block read: recovery belongs to the gRPC service
+        st, total, n, _ = cli.read("c", 49_800, 400, arena.path, slot, arena.slot)
+        assert st == fp.PARTIAL_CORRUPT and n == 400
+        assert srv.drain_suspects() == ["c"]
+    finally:
+        cli.close()
+        arena.close()
+
+
+def test_localrpc_target_selection():
+    from rust_hadoop_generated_by_llm_amd.utils.localrpc import LocalRegistry, local_name_for
+
+    assert local_name_for("http://127.0.0.1:50051") == "dfs_rpc_50051"
+    assert local_name_for("localhost:7000") == "dfs_rpc_7000"
+    assert local_name_for("https://127.0.0.1:50051") is None      # TLS stays on gRPC
+    assert local_name_for("http://10.1.2.3:50051") is None        # remote host
+    assert LocalRegistry().client_for("http://127.0.0.1:1") is None  # nothing listening
+
+
+def test_localrpc_roundtrip_and_status(tmp_path):
+    import asyncio
+    import threading
+
+    import grpc
+
+    from rust_hadoop_generated_by_llm_amd.cluster.launcher import free_port
+    from rust_hadoop_generated_by_llm_amd.models import proto as pb
+    from rust_hadoop_generated_by_llm_amd.utils.localrpc import serve_local
+    from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool, RpcStatus, StatusCode
+
+    class Svc:
+        async def get_file_info(self, req, ctx):
+            if req.path == "/redirect":
+                raise RpcStatus(StatusCode.OUT_OF_RANGE, "REDIRECT:http://127.0.0.1:9")
+            return pb.GetFileInfoResponse(found=True, metadata=pb.FileMetadata(path=req.path, size=7))
+
+    port = free_port()
+    loop = asyncio.new_event_loop()
+    started = threading.Event()
+
+    def run():
+        asyncio.set_event_loop(loop)
+        loop.run_until_complete(serve_local({"MasterService": Svc()}, port))
+        started.set()
+        loop.run_forever()
+
+    threading.Thread(target=run, daemon=True).start()
+    assert started.wait(10)
+    pool = ChannelPool()
+    try:
+        r = pool.call(f"http://127.0.0.1:{port}", "MasterService", "GetFileInfo", pb.GetFileInfoRequest(path="/a"))
+        assert r.found and r.metadata.size == 7 and r.metadata.path == "/a"
+        with pytest.raises(grpc.RpcError) as ei:
+            pool.call(f"http://127.0.0.1:{port}", "MasterService", "GetFileInfo", pb.GetFileInfoRequest(path="/redirect"))
+        assert ei.value.code() == grpc.StatusCode.OUT_OF_RANGE and ei.value.details().startswith("REDIRECT:")
+    finally:
+        pool.close()
+        loop.call_soon_threadsafe(loop.stop)
