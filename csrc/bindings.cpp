@@ -73,6 +73,16 @@ PYBIND11_MODULE(_dfs_native, m) {
   m.doc() = "MI355X-native data plane: HBM chunk store, CDNA4 CRC/RS kernels, RCCL replication, WAL";
 
   // ---------------- checksums
+  m.def("copy_into", [](py::buffer dst, uint64_t off, py::buffer src) {
+    // memcpy into a writable buffer (shared-memory slot) with the GIL released
+    py::buffer_info d = dst.request(true);
+    py::buffer_info sk;
+    Buf sv = view(src, sk);
+    uint64_t cap = static_cast<uint64_t>(d.size * d.itemsize);
+    if (off > cap || sv.n > cap - off) throw std::out_of_range("copy_into: destination too small");
+    py::gil_scoped_release r;
+    std::memcpy(static_cast<uint8_t*>(d.ptr) + off, sv.p, sv.n);
+  }, py::arg("dst"), py::arg("offset"), py::arg("src"));
   m.def("crc32", [](py::buffer b, uint32_t crc) {
     py::buffer_info k;
     Buf v = view(b, k);

@@ -28,6 +28,7 @@ from ..ops import crc as crcops
 from ..ops import erasure
 from ..parallel.sharding import ShardMap
 from ..utils.rpc import ChannelPool, rpc_code, rpc_details, strip_scheme, with_scheme
+from ..native import lib as _native
 from ..utils import fastpath as fpmod
 from ..utils.shm import ShmArena
 
@@ -79,6 +80,11 @@ class Client:
         self.fp_ops = 0
         # optional per-phase latency capture (benchmarks): {"create": [...], "write": [...], ...}
         self.phase_times: dict[str, list[float]] | None = None
+        # deferred create: the master places the block without a Raft entry and the file
+        # is created by CompleteFile{create} once its data is durable (masters without the
+        # extension simply create the file in CreateFile as before)
+        self.defer_create = os.environ.get("DFS_DEFER_CREATE", "1") == "1"
+        self._deferred: set[str] = set()
 
     def _phase(self, name: str, t0: float) -> float:
         t1 = time.perf_counter()
@@ -285,13 +291,18 @@ class Client:
     def _create_and_allocate(self, dest: str, ec_d: int = 0, ec_p: int = 0):
         resp, addr = self.execute_rpc(dest, "CreateFile", pb.CreateFileRequest(
             path=dest, ec_data_shards=ec_d, ec_parity_shards=ec_p, allocate_block=True,
-            preferred_chunk_server=self.local_chunkserver or ""), self._not_leader_check)
+            defer_create=self.defer_create, preferred_chunk_server=self.local_chunkserver or ""),
+            self._not_leader_check)
         if not resp.success:
             raise DfsError(f"Failed to create file: {resp.error_message}")
         if resp.HasField("allocation") and resp.allocation.HasField("block"):
-            alloc = resp.allocation  # fused create+allocate (one RPC, one Raft entry)
+            # fused create+allocate (one RPC) or, when deferred, placement only: the file is
+            # created together with its completion (one Raft entry per write)
+            alloc = resp.allocation
             if not alloc.chunk_server_addresses:
                 raise DfsError("No chunk servers available")
+            if resp.deferred:
+                self._deferred.add(alloc.block.block_id)
             return alloc
         # a master without the extension: the reference's separate AllocateBlock RPC
         masters = [addr] + [m for m in self.master_addrs if m != addr]
@@ -306,11 +317,18 @@ class Client:
             raise DfsError("No chunk servers available")
         return alloc
 
-    def _complete(self, dest: str, size: int, etag: str, sums: list) -> None:
+    def _complete(self, dest: str, size: int, etag: str, sums: list, alloc=None) -> None:
         req = pb.CompleteFileRequest(path=dest, size=size, etag_md5=etag, created_at_ms=int(time.time() * 1000),
                                      block_checksums=sums)
+        if alloc is not None and alloc.block.block_id in self._deferred:
+            self._deferred.discard(alloc.block.block_id)
+            req.create = True
+            req.ec_data_shards, req.ec_parity_shards = alloc.ec_data_shards, alloc.ec_parity_shards
+            req.blocks.append(alloc.block)
         resp, _ = self.execute_rpc(dest, "CompleteFile", req)
         if not resp.success:
+            if resp.error_message:
+                raise DfsError(f"Failed to create file: {resp.error_message}")
             raise DfsError("Failed to complete file")
 
     def _cs(self, addr: str) -> str:
@@ -320,22 +338,23 @@ class Client:
         """CreateFile -> AllocateBlock -> WriteBlock(chain) -> CompleteFile. Returns
         replicas_written (reference mod.rs:225-494)."""
         t = time.perf_counter()
+        # MD5 is a strictly sequential chain (~1.5 ms per MiB on one core) and only needed
+        # by CompleteFile: start it first so it overlaps the create RPC, the CRC and the
+        # block transfer (hashlib and the native CRC both release the GIL).
+        md5_fut = self._exec.submit(lambda: hashlib.md5(data).hexdigest())
+        crc_fut = self._exec.submit(crcops.crc32, data)
         alloc = self._create_and_allocate(dest)
         t = self._phase("create", t)
         block = alloc.block
         servers = list(alloc.chunk_server_addresses)
-        crc = crcops.crc32(data)
+        crc = crc_fut.result()
         t = self._phase("crc", t)
-        # MD5 is a strictly sequential chain (one core per object): run it while the block
-        # is on the wire instead of before it (hashlib releases the GIL); it is only
-        # needed for CompleteFile.
-        md5_fut = self._exec.submit(lambda: hashlib.md5(data).hexdigest())
         resp = None
         arena = self._shm() if strip_scheme(servers[0]) == self.local_chunkserver else None
         slot = arena.acquire(len(data)) if arena is not None else None
         if slot is not None:
             try:
-                arena.view[slot:slot + len(data)] = data
+                _native.copy_into(arena.mm, slot, data)  # GIL-free memcpy into the slot
                 fp = self.fastpath
                 if fp is not None and len(servers) == 1:
                     # last hop of the chain on this host: the native UNIX-socket data path
@@ -380,7 +399,7 @@ class Client:
         if resp.replicas_written < len(servers):
             log.warning("block written to %d/%d replicas", resp.replicas_written, len(servers))
         self._complete(dest, len(data), etag, [pb.BlockChecksumInfo(block_id=block.block_id, checksum_crc32c=crc,
-                                                                    actual_size=len(data))])
+                                                                    actual_size=len(data))], alloc)
         self._phase("complete", t)
         return resp.replicas_written
 
@@ -407,7 +426,7 @@ class Client:
         for f in [self._exec.submit(put, i) for i in range(k + m)]:
             f.result()
         self._complete(dest, len(data), "", [pb.BlockChecksumInfo(block_id=bid, checksum_crc32c=crcops.crc32(data),
-                                                                  actual_size=len(data))])
+                                                                  actual_size=len(data))], alloc)
 
     # ------------------------------------------------------------------ read path
     def _order_locations(self, locations) -> list[str]:

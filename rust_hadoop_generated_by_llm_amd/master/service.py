@@ -168,6 +168,16 @@ class MasterService:
         args = {"path": req.path, "ec_data_shards": req.ec_data_shards, "ec_parity_shards": req.ec_parity_shards,
                 "ts": now_ms()}
         selected = None
+        if req.allocate_block and req.defer_create:
+            # extension: place the block now, create the file with its data in CompleteFile
+            # (one Raft entry — one WAL fsync — per write instead of two)
+            selected = self._place(req.ec_data_shards, req.ec_parity_shards, req.preferred_chunk_server)
+            if not self.raft.is_leader():
+                return pb.CreateFileResponse(success=False, error_message="Not Leader",
+                                             leader_hint=self.raft.leader_address or "")
+            return pb.CreateFileResponse(success=True, deferred=True, allocation=self._allocation(
+                str(uuid.uuid4()), selected, req.ec_data_shards if req.ec_parity_shards else 0,
+                req.ec_parity_shards if req.ec_data_shards else 0))
         if req.allocate_block:
             # extension: CreateFile + AllocateBlock as ONE Raft entry and one round trip
             # (the reference client always issues both RPCs back to back)
@@ -260,6 +270,21 @@ class MasterService:
         args = {"path": req.path, "size": req.size,
                 "etag_md5": req.etag_md5 or None, "created_at_ms": req.created_at_ms or None,
                 "block_checksums": [M.checksum_to_dict(c) for c in req.block_checksums]}
+        if req.create:
+            self.check_safe_mode()
+            await self.wait_unlocked(req.path)
+            args.update(ts=now_ms(), ec_data_shards=req.ec_data_shards, ec_parity_shards=req.ec_parity_shards,
+                        blocks=[M.block_to_dict(b) for b in req.blocks])
+            try:
+                res = await self._propose_unlocked("CreateComplete", args)
+            except NotLeader as e:
+                raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"Not Leader|{e.hint}" if e.hint else "Not Leader")
+            if isinstance(res, dict) and res.get("exists"):
+                self._queue_block_gc([(b.block_id, list(b.locations)) for b in req.blocks])
+                return pb.CompleteFileResponse(success=False, error_message="File already exists")
+            if isinstance(res, dict) and res.get("orphans"):
+                self._queue_block_gc(res["orphans"])
+            return pb.CompleteFileResponse(success=True)
         try:
             res = await self._propose("CompleteFile", args)
         except NotLeader as e:

@@ -242,6 +242,25 @@ class MasterState:
         self.under_construction[path] = ts
         return {"exists": False, "orphans": [(b.block_id, list(b.locations)) for b in old.blocks] if old else []}
 
+    def _cmd_CreateComplete(self, a):
+        """Deferred create: the file appears, complete, in one entry (after its data)."""
+        path, ts = a["path"], int(a.get("ts", 0))
+        if path in self.tx_locks:
+            return {"locked": path}
+        old = self.files.get(path)
+        if old is not None:
+            started = self.under_construction.get(path)
+            if started is None or ts - started < CREATE_LEASE_MS:
+                return {"exists": True}
+        m = pb.FileMetadata(path=path, ec_data_shards=a.get("ec_data_shards", 0),
+                            ec_parity_shards=a.get("ec_parity_shards", 0))
+        for bd in a.get("blocks", []):
+            m.blocks.append(M.block_from_dict(bd))
+        self._put(path, m)
+        self.under_construction.pop(path, None)
+        self._cmd_CompleteFile(a)
+        return {"exists": False, "orphans": [(b.block_id, list(b.locations)) for b in old.blocks] if old else []}
+
     def visible(self, path: str):
         """Metadata of a completed file, else None."""
         if path in self.under_construction:

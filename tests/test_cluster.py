@@ -228,3 +228,31 @@ def test_master_raft_failover():
         assert c.get_file_content("/raft/after") == b"after"
         pool.close()
         c.close()
+
+
+def test_local_short_circuit_and_fast_path():
+    """Co-located client: shm short-circuit on the first op, then the native UNIX-socket
+    fast path (utils/fastpath.py <-> csrc/fastpath.cpp) for RF=1 writes and all reads;
+    deferred create keeps one Raft entry per write; a dead fast-path socket falls back."""
+    with LocalCluster(n_chunkservers=1, fsync=False) as cl:
+        c = cl.client(local_chunkserver=cl.cs_addrs[0])
+        blobs = {f"/sc/f{i}": os.urandom(200_000 + i) for i in range(6)}
+        for p, d in blobs.items():
+            c.create_file_from_buffer(d, p)
+        for p, d in blobs.items():
+            assert c.get_file_content(p) == d
+        assert c.read_file_range("/sc/f3", 1234, 5000) == blobs["/sc/f3"][1234:6234]
+        assert c.sc_ops >= 1 and c.fp_ops >= 10 and c.fastpath is not None
+        st = json.load(urllib.request.urlopen(f"{cl.cs_http[0]}/stats"))
+        assert st["fp_writes"] >= 5 and st["fp_reads"] >= 6
+        # duplicate create through the deferred path is refused at CompleteFile/CreateFile
+        with pytest.raises(DfsError):
+            c.create_file_from_buffer(b"again", "/sc/f0")
+        assert c.get_file_content("/sc/f0") == blobs["/sc/f0"]
+        # a stale socket name: the client drops the fast path and uses gRPC
+        from rust_hadoop_generated_by_llm_amd.utils import fastpath as fpmod
+
+        c.fastpath = fpmod.FastPathClient("dfs_fp_nonexistent")
+        c.create_file_from_buffer(b"fallback", "/sc/fallback")
+        assert c.get_file_content("/sc/fallback") == b"fallback"
+        c.close()

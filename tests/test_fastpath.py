@@ -128,13 +128,23 @@ def test_localrpc_roundtrip_and_status(tmp_path):
     loop = asyncio.new_event_loop()
     started = threading.Event()
 
+    holder = {}
+
     def run():
         asyncio.set_event_loop(loop)
-        loop.run_until_complete(serve_local({"MasterService": Svc()}, port))
+        holder["srv"] = loop.run_until_complete(serve_local({"MasterService": Svc()}, port))
         started.set()
         loop.run_forever()
+        holder["srv"].close()
+        loop.run_until_complete(holder["srv"].wait_closed())
+        pending = asyncio.all_tasks(loop)
+        for t in pending:
+            t.cancel()
+        loop.run_until_complete(asyncio.gather(*pending, return_exceptions=True))
+        loop.close()
 
-    threading.Thread(target=run, daemon=True).start()
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
     assert started.wait(10)
     pool = ChannelPool()
     try:
@@ -146,3 +156,4 @@ def test_localrpc_roundtrip_and_status(tmp_path):
     finally:
         pool.close()
         loop.call_soon_threadsafe(loop.stop)
+        th.join(10)
