@@ -336,6 +336,8 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("adopt_term", &FastPathServer::adopt_term)
       .def_property_readonly("term", &FastPathServer::term)
       .def("drain_suspects", &FastPathServer::drain_suspects)
+      .def("set_rccl", &FastPathServer::set_rccl, py::arg("engine"), py::keep_alive<1, 2>())
+      .def("set_peer", &FastPathServer::set_peer, py::arg("addr"), py::arg("rank"), py::arg("name"))
       .def("stats", [](FastPathServer& f) {
         FpStats s = f.stats();
         py::dict d;
@@ -344,6 +346,9 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["fp_fenced"] = s.fenced;
         d["fp_punts"] = s.punts;
         d["fp_connections"] = s.connections;
+        d["fp_replicas_in"] = s.replicas_in;
+        d["fp_rccl_forwards"] = s.rccl_forwards;
+        d["fp_forward_failures"] = s.forward_failures;
         return d;
       });
 

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -16,6 +17,40 @@
 #include "gf256.h"
 
 namespace dfs {
+
+// ---------------------------------------------------------------- group commit
+GroupSync::GroupSync(const std::string& dir) { fd_ = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC); }
+
+GroupSync::~GroupSync() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+bool GroupSync::sync() {
+  if (fd_ < 0) return false;
+  std::unique_lock<std::mutex> lk(mu_);
+  uint64_t ticket = ++issued_;
+  while (done_ < ticket) {
+    if (running_) {
+      cv_.wait(lk);
+      continue;
+    }
+    // lead a round: it covers every ticket issued before the flush starts
+    running_ = true;
+    uint64_t covers = issued_;
+    lk.unlock();
+    bool ok = ::syncfs(fd_) == 0;
+    lk.lock();
+    running_ = false;
+    if (!ok) failed_.emplace_back(done_ + 1, covers);
+    done_ = covers;
+    rounds_++;
+    cv_.notify_all();
+  }
+  for (const auto& f : failed_)
+    if (ticket >= f.first && ticket <= f.second) return false;
+  return true;
+}
+
 
 namespace {
 
@@ -133,6 +168,11 @@ uint64_t ExtentAllocator::largest_free() const {
 ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
   mkdirs(cfg_.storage_dir);
   if (!cfg_.cold_dir.empty()) mkdirs(cfg_.cold_dir);
+  // Opt-in (DFS_GROUP_SYNC=1): a syncfs() round wins on devices where each flush is
+  // expensive and many writers are in flight; on overlay filesystems it flushes far more
+  // than our two files, so the per-file fdatasync pair stays the default.
+  const char* gs = std::getenv("DFS_GROUP_SYNC");
+  if (cfg_.sync_writes && gs && std::string(gs) == "1") gsync_ = std::make_unique<GroupSync>(cfg_.storage_dir);
   if (gpu()) {
     HIP_OK(hipSetDevice(cfg_.device));
     uint64_t cap = cfg_.hbm_capacity;
@@ -412,19 +452,37 @@ bool ChunkStore::persist(const std::string& id, bool cold, const uint8_t* data, 
     *err = errno_str("open " + dp);
     return false;
   }
-  bool ok = write_all(fd, data, n, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
-  if (!ok) *err = errno_str("write " + dp);
-  ::close(fd);
-  if (!ok) return false;
-  fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-  if (fd < 0) {
-    *err = errno_str("open " + mp);
+  bool ok = write_all(fd, data, n, 0);
+  if (!ok) {
+    *err = errno_str("write " + dp);
+    ::close(fd);
     return false;
   }
-  ok = write_all(fd, meta_be, nslices * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
+  int mfd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (mfd < 0) {
+    *err = errno_str("open " + mp);
+    ::close(fd);
+    return false;
+  }
+  ok = write_all(mfd, meta_be, nslices * 4, 0);
   if (!ok) *err = errno_str("write " + mp);
+  if (ok && !make_durable(fd, mfd, cold)) {
+    ok = false;
+    *err = errno_str("sync " + dp);
+  }
   ::close(fd);
+  ::close(mfd);
   return ok;
+}
+
+bool ChunkStore::make_durable(int data_fd, int meta_fd, bool cold) {
+  if (!cfg_.sync_writes) return true;
+  // Group commit: one syncfs() covers the data + .meta of every writer that finished
+  // writing before it started (one device cache flush for a whole burst of blocks,
+  // instead of two fdatasync flushes per block). Cold-tier files may live on another
+  // filesystem: they take the per-file path.
+  if (gsync_ && !cold) return gsync_->sync();
+  return ::fdatasync(data_fd) == 0 && ::fdatasync(meta_fd) == 0;
 }
 
 // ---------------------------------------------------------------- write
@@ -581,15 +639,16 @@ bool ChunkStore::persist_from_device(const std::string& id, const uint8_t* d, ui
     HIP_OK(hipStreamSynchronize(l->stream));
     ok = write_all(fd, l->pinned[c & 1], len, off);
   }
-  if (ok && cfg_.sync_writes) ok = ::fdatasync(fd) == 0;
-  if (fd >= 0) ::close(fd);
   release_lane(l);
+  int mfd = -1;
   if (ok) {
     std::string mp = meta_path(id, false);
-    fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-    ok = fd >= 0 && write_all(fd, meta_be, nslices * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
-    if (fd >= 0) ::close(fd);
+    mfd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    ok = mfd >= 0 && write_all(mfd, meta_be, nslices * 4, 0);
   }
+  if (ok) ok = make_durable(fd, mfd, false);
+  if (fd >= 0) ::close(fd);
+  if (mfd >= 0) ::close(mfd);
   if (!ok) *err = errno_str("persist " + id);
   return ok;
 }
@@ -1050,19 +1109,20 @@ void ChunkStore::spill_worker() {
       }
       ok = write_all(fd, l->pinned[c & 1], len, off);
     }
-    if (ok && cfg_.sync_writes) ok = ::fdatasync(fd) == 0;
-    if (fd >= 0) ::close(fd);
     if (ok && S) {
       ok = hipMemcpyAsync(hmeta, d + align_up(std::max<uint64_t>(size, 1), 256), S * 4, hipMemcpyDeviceToHost,
                           l->stream) == hipSuccess &&
            hipStreamSynchronize(l->stream) == hipSuccess;
     }
+    int mfd = -1;
     if (ok) {
       std::string mp = meta_path(id, false);
-      fd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-      ok = fd >= 0 && write_all(fd, hmeta, S * 4, 0) && (!cfg_.sync_writes || ::fdatasync(fd) == 0);
-      if (fd >= 0) ::close(fd);
+      mfd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      ok = mfd >= 0 && write_all(mfd, hmeta, S * 4, 0);
     }
+    if (ok) ok = make_durable(fd, mfd, false);
+    if (fd >= 0) ::close(fd);
+    if (mfd >= 0) ::close(mfd);
     release_lane(l);
     {
       std::lock_guard<std::mutex> g(mu_);

@@ -93,6 +93,23 @@ class ExtentAllocator {
   std::map<uint64_t, uint64_t> free_;  // off -> len
 };
 
+// Group commit of data files: callers that finished writing share one syncfs() round.
+class GroupSync {
+ public:
+  explicit GroupSync(const std::string& dir);
+  ~GroupSync();
+  bool sync();  // returns once a flush that started after this call has completed
+  uint64_t rounds() const { return rounds_; }
+
+ private:
+  int fd_ = -1;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  uint64_t issued_ = 0, done_ = 0, rounds_ = 0;
+  bool running_ = false;
+  std::vector<std::pair<uint64_t, uint64_t>> failed_;  // ticket ranges of failed rounds
+};
+
 class ChunkStore;
 
 // A region of the arena owned by an in-flight operation (RCCL receive target).
@@ -210,6 +227,7 @@ class ChunkStore {
   bool persist(const std::string& id, bool cold, const uint8_t* data, uint64_t n, const uint8_t* meta_be,
                uint64_t nslices, std::string* err);
   void spill_worker();
+  bool make_durable(int data_fd, int meta_fd, bool cold);
   WriteResult write_host(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
   ReadResult read_host(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out);
   std::vector<uint32_t> load_meta_file(const std::string& id, bool cold, bool* ok);
@@ -232,6 +250,7 @@ class ChunkStore {
   bool stop_ = false;
   StoreStats st_;
   std::atomic<uint64_t> launches_{0};
+  std::unique_ptr<GroupSync> gsync_;
 };
 
 }  // namespace dfs

@@ -11,6 +11,7 @@
 
 #include <cerrno>
 #include <cstring>
+#include <future>
 
 namespace dfs {
 
@@ -94,6 +95,27 @@ bool send_response(int fd, FpStatus st, uint64_t total, uint64_t bytes, const st
   return write_full(fd, out.data(), out.size());
 }
 
+void put_str(std::vector<uint8_t>& b, const std::string& s) {
+  uint16_t n = static_cast<uint16_t>(s.size());
+  const auto* q = reinterpret_cast<const uint8_t*>(&n);
+  b.insert(b.end(), q, q + 2);
+  b.insert(b.end(), s.begin(), s.end());
+}
+
+template <class T>
+void put(std::vector<uint8_t>& b, T v) {
+  const auto* q = reinterpret_cast<const uint8_t*>(&v);
+  b.insert(b.end(), q, q + sizeof(T));
+}
+
+std::vector<std::string> read_list(Reader& rd, bool optional) {
+  std::vector<std::string> out;
+  if (optional && rd.p == rd.end) return out;
+  uint16_t n = rd.get<uint16_t>();
+  for (uint16_t i = 0; rd.ok && i < n; ++i) out.push_back(rd.str());
+  return out;
+}
+
 bool valid_shm_path(const std::string& path) {
   // only our client arenas: /dev/shm/dfs_sc_<...> with no path tricks
   if (path.rfind(kShmDir, 0) != 0) return false;
@@ -150,6 +172,12 @@ void FastPathServer::stop() {
   std::lock_guard<std::mutex> g(mu_);
   for (auto& kv : maps_) ::munmap(kv.second.p, kv.second.size);
   maps_.clear();
+  for (auto& m : retired_) ::munmap(m.p, m.size);
+  retired_.clear();
+  std::lock_guard<std::mutex> pg(peers_mu_);
+  for (auto& kv : peers_)
+    for (int fd : kv.second->idle) ::close(fd);
+  peers_.clear();
 }
 
 bool FastPathServer::fence(uint64_t term, uint64_t* known) {
@@ -214,8 +242,10 @@ uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t need, std::st
     std::lock_guard<std::mutex> g(mu_);
     auto it = maps_.find(path);
     if (it != maps_.end() && it->second.size >= need) return it->second.p;
-    if (it != maps_.end()) {  // the client recreated a bigger arena: remap
-      ::munmap(it->second.p, it->second.size);
+    if (it != maps_.end()) {
+      // the client recreated a bigger arena under the same name: map it again but keep
+      // the old mapping alive (another connection may still be copying from it)
+      retired_.push_back(it->second);
       maps_.erase(it);
     }
   }
@@ -247,8 +277,148 @@ uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t need, std::st
   return m.p;
 }
 
+void FastPathServer::set_rccl(RcclEngine* engine) { rccl_ = engine; }
+
+void FastPathServer::set_peer(const std::string& addr, int rank, const std::string& fp_name) {
+  std::lock_guard<std::mutex> g(peers_mu_);
+  auto& p = peers_[addr];
+  if (!p) p = std::make_unique<Peer>();
+  p->rank = rank;
+  p->name = fp_name;
+}
+
+FastPathServer::Peer* FastPathServer::peer(const std::string& addr) {
+  std::lock_guard<std::mutex> g(peers_mu_);
+  auto it = peers_.find(addr);
+  return it == peers_.end() ? nullptr : it->second.get();
+}
+
+namespace {
+
+int connect_abstract(const std::string& name) {
+  int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -1;
+  sockaddr_un addr{};
+  addr.sun_family = AF_UNIX;
+  addr.sun_path[0] = '\0';
+  std::memcpy(addr.sun_path + 1, name.data(), std::min(name.size(), sizeof(addr.sun_path) - 2));
+  socklen_t len = static_cast<socklen_t>(offsetof(sockaddr_un, sun_path) + 1 + name.size());
+  timeval tv{120, 0};  // bounded like every other wait on the replication path
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&addr), len) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+}  // namespace
+
+bool FastPathServer::forward(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
+                             int* replicas, std::string* err) {
+  *replicas = 0;
+  Peer* p = next.empty() ? nullptr : peer(next[0]);
+  if (p == nullptr || rccl_ == nullptr || !rccl_->pair_ok(rccl_->rank(), p->rank)) {
+    *err = "no native route to " + (next.empty() ? std::string("?") : next[0]);
+    return false;
+  }
+  int fd = -1;
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    if (!p->idle.empty()) {
+      fd = p->idle.back();
+      p->idle.pop_back();
+    }
+  }
+  if (fd < 0 && (fd = connect_abstract(p->name)) < 0) {
+    *err = "cannot reach fast path of " + next[0];
+    return false;
+  }
+  uint64_t size = 0;
+  int64_t seq = rccl_->send(p->rank, id, &size, err);
+  if (seq < 0) {
+    std::lock_guard<std::mutex> g(p->mu);
+    p->idle.push_back(fd);
+    return false;
+  }
+  std::vector<uint8_t> req(4, 0);
+  req.push_back(3);
+  put<uint64_t>(req, term);
+  put<uint32_t>(req, crc);
+  put<int32_t>(req, rccl_->rank());
+  put<int64_t>(req, seq);
+  put<uint64_t>(req, size);
+  put_str(req, id);
+  put<uint16_t>(req, static_cast<uint16_t>(next.size() - 1));
+  for (size_t i = 1; i < next.size(); ++i) put_str(req, next[i]);
+  uint32_t body = static_cast<uint32_t>(req.size() - 4);
+  std::memcpy(req.data(), &body, 4);
+  bool io_ok = write_full(fd, req.data(), req.size());
+  uint32_t n = 0;
+  std::vector<uint8_t> resp;
+  if (io_ok) io_ok = read_full(fd, &n, 4) && n >= 19 && n <= kMaxBody;
+  if (io_ok) {
+    resp.resize(n);
+    io_ok = read_full(fd, resp.data(), n);
+  }
+  std::string werr;
+  bool sent = rccl_->wait_send(p->rank, seq, &werr);
+  if (!io_ok || !sent) {
+    ::close(fd);
+    // an unmatched send would wedge this pair's stream: retire it (the gRPC path takes over)
+    rccl_->abort_pair(rccl_->rank(), p->rank);
+    *err = !io_ok ? "descriptor to " + next[0] + " failed" : "RCCL send failed: " + werr;
+    return false;
+  }
+  {
+    std::lock_guard<std::mutex> g(p->mu);
+    p->idle.push_back(fd);
+  }
+  auto st = static_cast<FpStatus>(resp[0]);
+  uint64_t downstream = 0;
+  std::memcpy(&downstream, resp.data() + 9, 8);
+  if (st != FpStatus::Ok) {
+    uint16_t ml = 0;
+    std::memcpy(&ml, resp.data() + 17, 2);
+    *err = "downstream " + next[0] + ": " + std::string(reinterpret_cast<const char*>(resp.data() + 19),
+                                                         std::min<size_t>(ml, resp.size() - 19));
+    return false;
+  }
+  *replicas = static_cast<int>(downstream);
+  std::lock_guard<std::mutex> g(mu_);
+  st_.rccl_forwards++;
+  return true;
+}
+
 void FastPathServer::serve(int fd) {
   std::vector<uint8_t> body;
+  auto bump = [this](uint64_t FpStats::*field) {
+    std::lock_guard<std::mutex> g(mu_);
+    (st_.*field)++;
+  };
+  auto fenced = [&](uint64_t term, std::string* msg) {
+    uint64_t known = 0;
+    if (fence(term, &known)) return false;
+    bump(&FpStats::fenced);
+    *msg = "Stale master term: request has " + std::to_string(term) + " but known term is " + std::to_string(known);
+    return true;
+  };
+  // Local persist and downstream forward run concurrently; the ack waits for both.
+  auto persist_and_forward = [&](const std::string& id, const uint8_t* host, uint64_t len, uint32_t crc,
+                                 uint64_t term, const std::vector<std::string>& next) -> bool {
+    int down = 0;
+    std::string ferr, perr;
+    auto fut = std::async(std::launch::async, [&] { return forward(id, crc, term, next, &down, &ferr); });
+    bool pok = store_->persist(id, host, host ? len : 0, &perr);
+    bool fok = fut.get();
+    if (!pok) return send_response(fd, FpStatus::IoError, 0, 0, perr);
+    if (!fok) {
+      bump(&FpStats::forward_failures);
+      return send_response(fd, FpStatus::Unsupported, 0, 0, "native forward failed: " + ferr);
+    }
+    return send_response(fd, FpStatus::Ok, len, 1 + static_cast<uint64_t>(down), "");
+  };
   while (!stop_.load()) {
     uint32_t n = 0;
     if (!read_full(fd, &n, 4) || n == 0 || n > kMaxBody) break;
@@ -257,38 +427,60 @@ void FastPathServer::serve(int fd) {
     Reader rd{body.data() + 1, body.data() + n};
     uint8_t op = body[0];
     bool sent = false;
-    if (op == 1) {  // WRITE (no downstream replicas)
+    std::string msg;
+    if (op == 1) {  // WRITE from a co-located client (optionally the head of a chain)
       uint64_t term = rd.get<uint64_t>();
       uint32_t crc = rd.get<uint32_t>();
       uint64_t off = rd.get<uint64_t>(), len = rd.get<uint64_t>();
       std::string id = rd.str(), path = rd.str();
+      std::vector<std::string> next = read_list(rd, true);
+      std::string err;
+      uint8_t* base = nullptr;
       if (!rd.ok || id.empty()) {
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed write request");
+      } else if (fenced(term, &msg)) {
+        sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
+      } else if (!next.empty() && (rccl_ == nullptr || peer(next[0]) == nullptr)) {
+        sent = send_response(fd, FpStatus::Unsupported, 0, 0, "no native route for the chain");
+      } else if ((base = map_shm(path, off + len, &err)) == nullptr) {
+        sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
+      } else if (next.empty()) {
+        WriteResult wr = store_->write(id, base + off, len, crc);
+        if (wr.ok) bump(&FpStats::writes);
+        sent = wr.ok ? send_response(fd, FpStatus::Ok, len, 1, "") : send_response(fd, FpStatus::IoError, 0, 0, wr.error);
       } else {
-        uint64_t known = 0;
-        std::string err;
-        uint8_t* base = nullptr;
-        if (!fence(term, &known)) {
-          {
-            std::lock_guard<std::mutex> g(mu_);
-            st_.fenced++;
-          }
-          sent = send_response(fd, FpStatus::Fenced, known, 0,
-                               "Stale master term: request has " + std::to_string(term) + " but known term is " +
-                                   std::to_string(known));
-        } else if ((base = map_shm(path, off + len, &err)) == nullptr) {
-          sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
+        WriteResult wr = store_->stage(id, base + off, len, crc);  // HBM + CRC verify, not yet durable
+        if (!wr.ok) {
+          sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
         } else {
-          WriteResult wr = store_->write(id, base + off, len, crc);
-          if (wr.ok) {
-            {
-              std::lock_guard<std::mutex> g(mu_);
-              st_.writes++;
-            }
-            sent = send_response(fd, FpStatus::Ok, len, len, "");
-          } else {
-            sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
-          }
+          bump(&FpStats::writes);
+          sent = persist_and_forward(id, base + off, len, crc, term, next);
+        }
+      }
+    } else if (op == 3) {  // REPL: block arrives over RCCL from the previous hop
+      uint64_t term = rd.get<uint64_t>();
+      uint32_t crc = rd.get<uint32_t>();
+      int32_t src = rd.get<int32_t>();
+      int64_t seq = rd.get<int64_t>();
+      uint64_t size = rd.get<uint64_t>();
+      std::string id = rd.str();
+      std::vector<std::string> next = read_list(rd, false);
+      if (!rd.ok || id.empty() || rccl_ == nullptr) {
+        sent = send_response(fd, FpStatus::BadRequest, 0, 0, rccl_ ? "malformed replicate request" : "RCCL disabled");
+      } else {
+        // The recv must be posted even when the request is refused, or the sender's
+        // ncclSend never completes; recv first, then judge the request.
+        bool last = next.empty();
+        bool stale = fenced(term, &msg);
+        WriteResult wr = rccl_->recv(src, seq, id, size, crc, last && !stale);
+        if (stale) {
+          sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
+        } else if (!wr.ok) {
+          sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
+        } else {
+          bump(&FpStats::replicas_in);
+          sent = last ? send_response(fd, FpStatus::Ok, size, 1, "")
+                      : persist_and_forward(id, nullptr, size, crc, term, next);
         }
       }
     } else if (op == 2) {  // READ into the client's slot
@@ -310,10 +502,7 @@ void FastPathServer::serve(int fd) {
         } else {
           ReadResult rr = store_->read_into(id, offset, st.bytes, base + shm_off);
           if (rr.status == ReadStatus::Ok && !rr.partial_corrupt) {
-            {
-              std::lock_guard<std::mutex> g(mu_);
-              st_.reads++;
-            }
+            bump(&FpStats::reads);
             sent = send_response(fd, FpStatus::Ok, rr.total_size, rr.bytes, "");
           } else if (rr.status == ReadStatus::Ok) {
             {
@@ -323,10 +512,7 @@ void FastPathServer::serve(int fd) {
             }
             sent = send_response(fd, FpStatus::PartialCorrupt, rr.total_size, rr.bytes, rr.error);
           } else {
-            {
-              std::lock_guard<std::mutex> g(mu_);
-              st_.punts++;
-            }
+            bump(&FpStats::punts);
             sent = send_response(fd, static_cast<FpStatus>(rr.status), rr.total_size, 0, rr.error);
           }
         }

@@ -8,20 +8,30 @@
 // no HTTP/2 framing on the ChunkServer side. Reads DMA the verified range from HBM
 // straight into the client's slot.
 //
-// Scope: WriteBlock without downstream replicas (the last hop of any chain, RF=1) and
-// ReadBlock. Anything else — chain forwarding, corruption needing recovery, fenced or
-// malformed requests — is answered with a status telling the client to use the regular
-// gRPC service, which keeps every semantic of the reference (fencing, recovery,
-// replicas_written) in one place.
+// Scope: WriteBlock (locally, and along same-node RCCL chains) and ReadBlock. Anything
+// else — cross-node hops, corruption needing recovery, fenced or malformed requests — is
+// answered with a status telling the client to use the regular gRPC service, which keeps
+// every semantic of the reference (fencing, recovery, replicas_written) in one place.
 //
 // Wire format (little endian), one request/response pair at a time per connection:
 //   request  = u32 body_len | u8 op | body
 //     op 1 WRITE: u64 term | u32 crc | u64 shm_off | u64 len | u16 id_len id | u16 path_len path
+//               [| u16 n_next | (u16 len addr)*]      -- chain: forwarded natively over RCCL
 //     op 2 READ : u64 offset | u64 length | u64 shm_off | u64 shm_cap | u16 id_len id | u16 path_len path
+//     op 3 REPL : u64 term | u32 crc | i32 src_rank | i64 seq | u64 size | u16 id_len id
+//               | u16 n_next | (u16 len addr)*      -- server-to-server: block arrives over RCCL
 //   response = u32 body_len | u8 status | u64 total | u64 bytes | u16 msg_len msg
+//   (for WRITE/REPL ``bytes`` carries replicas_written)
+//
+// Chain replication stays native when every hop is a ChunkServer of this node with an
+// RCCL pair: the block is staged in HBM, sent GPU->GPU over xGMI with ncclSend, and the
+// ~100-byte descriptor goes to the next server's fast-path socket, concurrently with the
+// local fdatasync. Any hop without that route answers Unsupported and the client redoes
+// the write on the gRPC path (which has its own RCCL + gRPC fallback).
 #pragma once
 #include <atomic>
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -29,6 +39,7 @@
 #include <vector>
 
 #include "chunk_store.h"
+#include "rccl_engine.h"
 
 namespace dfs {
 
@@ -46,6 +57,7 @@ enum class FpStatus : uint8_t {
 
 struct FpStats {
   uint64_t writes = 0, reads = 0, fenced = 0, punts = 0, connections = 0;
+  uint64_t replicas_in = 0, rccl_forwards = 0, forward_failures = 0;
 };
 
 class FastPathServer {
@@ -68,10 +80,26 @@ class FastPathServer {
   std::vector<std::string> drain_suspects();  // blocks needing background recovery
   FpStats stats();
 
+  // Native chain replication: this server's RCCL engine and the fast-path socket of every
+  // same-node peer (advertised address -> rank, socket name).
+  void set_rccl(RcclEngine* engine);
+  void set_peer(const std::string& addr, int rank, const std::string& fp_name);
+
  private:
+  struct Peer {
+    int rank = -1;
+    std::string name;
+    std::mutex mu;
+    std::vector<int> idle;  // pooled connections to the peer's fast-path socket
+  };
   void accept_loop();
   void serve(int fd);
   uint8_t* map_shm(const std::string& path, uint64_t need, std::string* err);
+  // Send block `id` (resident in HBM) to next[0] over RCCL + descriptor; *replicas gets
+  // the downstream count. False (with *err) when there is no native route or it failed.
+  bool forward(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
+               int* replicas, std::string* err);
+  Peer* peer(const std::string& addr);
 
   ChunkStore* store_;
   std::string name_;
@@ -87,8 +115,12 @@ class FastPathServer {
     uint64_t size = 0;
   };
   std::unordered_map<std::string, Mapping> maps_;
+  std::vector<Mapping> retired_;
   std::vector<std::string> suspects_;
   FpStats st_;
+  RcclEngine* rccl_ = nullptr;
+  std::mutex peers_mu_;
+  std::unordered_map<std::string, std::unique_ptr<Peer>> peers_;
 };
 
 }  // namespace dfs

@@ -70,22 +70,29 @@ def parse_size(s: str) -> int:
     return int(s)
 
 
-def rendezvous_ranks(d: str, rank: int, world: int, addr: str, timeout: float = 120.0) -> dict[str, int]:
-    """Publish our advertise address for our rank and wait for every rank's."""
+def rendezvous_ranks(d: str, rank: int, world: int, addr: str, timeout: float = 120.0,
+                     fastpath: str = "") -> tuple[dict[str, int], dict[str, str]]:
+    """Publish our advertise address (and native fast-path socket) for our rank and wait
+    for every rank's. Returns ({addr: rank}, {addr: fast-path socket name})."""
     Path(d).mkdir(parents=True, exist_ok=True)
     tmp = Path(d) / f".addr_{rank}.tmp"
-    tmp.write_text(addr)
+    tmp.write_text(addr + ("\n" + fastpath if fastpath else ""))
     os.replace(tmp, Path(d) / f"addr_{rank}")
     deadline = time.time() + timeout
     out: dict[str, int] = {}
+    names: dict[str, str] = {}
     while time.time() < deadline:
-        out = {}
+        out, names = {}, {}
         for r in range(world):
             f = Path(d) / f"addr_{r}"
             if f.exists():
-                out[strip_scheme(f.read_text().strip())] = r
+                lines = f.read_text().split("\n")
+                a = strip_scheme(lines[0].strip())
+                out[a] = r
+                if len(lines) > 1 and lines[1].strip():
+                    names[a] = lines[1].strip()
         if len(out) == world:
-            return out
+            return out, names
         time.sleep(0.05)
     raise TimeoutError(f"rendezvous: only {len(out)}/{world} chunkservers published in {d}")
 
@@ -106,20 +113,6 @@ class ChunkServerProcess:
         self.static_masters = [with_scheme(m) for m in args.masters.split(",") if m.strip()]
         shard_cfg = os.environ.get("SHARD_CONFIG")
         self.shard_map = ShardMap.load_config_file(shard_cfg) if shard_cfg else ShardMap.new_range()
-        self.rccl = None
-        rank_map: dict[str, int] = {}
-        if (args.replication_transport == "rccl" and args.rccl_world > 1 and args.rccl_rank >= 0
-                and args.rccl_rendezvous and args.gpu >= 0):
-            rank_map = rendezvous_ranks(args.rccl_rendezvous, args.rccl_rank, args.rccl_world, self.advertise)
-            eng = native.RcclEngine(self.store, args.rccl_rank, args.rccl_world, args.rccl_rendezvous,
-                                    args.rccl_timeout_ms)
-            ok, err = eng.init()
-            if ok:
-                self.rccl = eng
-                log.info("RCCL replication ready: rank %d/%d", args.rccl_rank, args.rccl_world)
-            else:
-                log.error("RCCL init failed (%s); using gRPC replication", err)
-        self.metrics = Registry()
         self.fastpath = None
         if not args.no_fastpath:
             port = strip_scheme(args.addr).rsplit(":", 1)[-1]
@@ -129,6 +122,28 @@ class ChunkServerProcess:
                 self.fastpath = fp
             else:
                 log.warning("native fast path disabled: %s", err)
+        self.rccl = None
+        rank_map: dict[str, int] = {}
+        if (args.replication_transport == "rccl" and args.rccl_world > 1 and args.rccl_rank >= 0
+                and args.rccl_rendezvous and args.gpu >= 0):
+            rank_map, fp_names = rendezvous_ranks(args.rccl_rendezvous, args.rccl_rank, args.rccl_world,
+                                                  self.advertise,
+                                                  fastpath=self.fastpath.name if self.fastpath else "")
+            eng = native.RcclEngine(self.store, args.rccl_rank, args.rccl_world, args.rccl_rendezvous,
+                                    args.rccl_timeout_ms)
+            ok, err = eng.init()
+            if ok:
+                self.rccl = eng
+                log.info("RCCL replication ready: rank %d/%d", args.rccl_rank, args.rccl_world)
+                if self.fastpath is not None:
+                    # chains between same-node GPUs stay native: RCCL payload + socket descriptor
+                    self.fastpath.set_rccl(eng)
+                    for a, r in rank_map.items():
+                        if r != args.rccl_rank and a in fp_names:
+                            self.fastpath.set_peer(a, r, fp_names[a])
+            else:
+                log.error("RCCL init failed (%s); using gRPC replication", err)
+        self.metrics = Registry()
         self.cs = ChunkServer(self.store, self.advertise, self.pool, self.masters, self.rccl, rank_map,
                               args.rccl_rank, self.metrics, fastpath=self.fastpath)
         self._setup_metrics()

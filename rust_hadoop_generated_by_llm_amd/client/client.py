@@ -356,12 +356,14 @@ class Client:
             try:
                 _native.copy_into(arena.mm, slot, data)  # GIL-free memcpy into the slot
                 fp = self.fastpath
-                if fp is not None and len(servers) == 1:
-                    # last hop of the chain on this host: the native UNIX-socket data path
+                if fp is not None:
+                    # the chain head is on this host: native UNIX-socket data path (the
+                    # server forwards same-node hops over RCCL, else answers UNSUPPORTED)
                     try:
-                        st, msg = fp.write(block.block_id, arena.path, slot, len(data), crc, alloc.master_term)
+                        st, replicas, msg = fp.write(block.block_id, arena.path, slot, len(data), crc,
+                                                     alloc.master_term, [strip_scheme(x) for x in servers[1:]])
                         if st == fpmod.OK:
-                            resp = pb.WriteBlockResponse(success=True, replicas_written=1)
+                            resp = pb.WriteBlockResponse(success=True, replicas_written=replicas)
                             self.fp_ops += 1
                         elif st == fpmod.FENCED:
                             raise DfsError(f"Failed to write block: {msg}")

@@ -79,10 +79,15 @@ class FastPathClient:
         msg = resp[_RESP.size:_RESP.size + ml].decode("utf-8", "replace")
         return st, total, nbytes, msg
 
-    def write(self, block_id: str, shm_path: str, shm_off: int, length: int, crc: int, term: int):
+    def write(self, block_id: str, shm_path: str, shm_off: int, length: int, crc: int, term: int,
+              next_servers: list[str] | tuple = ()):
+        """Returns (status, replicas_written, message). With ``next_servers`` the server
+        forwards the block along the chain natively (RCCL) or answers UNSUPPORTED."""
         body = _WRITE.pack(term, crc & 0xFFFFFFFF, shm_off, length) + _s(block_id.encode()) + _s(shm_path.encode())
-        st, _total, _n, msg = self._call(1, body)
-        return st, msg
+        if next_servers:
+            body += struct.pack("<H", len(next_servers)) + b"".join(_s(a.encode()) for a in next_servers)
+        st, _total, replicas, msg = self._call(1, body)
+        return st, replicas, msg
 
     def read(self, block_id: str, offset: int, length: int, shm_path: str, shm_off: int, cap: int):
         body = _READ.pack(offset, length, shm_off, cap) + _s(block_id.encode()) + _s(shm_path.encode())

@@ -25,6 +25,11 @@ if [ "$STEP" = "all" ] || [ "$STEP" = "micro" ]; then
      -d "$OLDPWD/gpurun_out/prof_io" -o io -- "$OLDPWD/build/native/io_bench" --iters 30) \
      > gpurun_out/io_bench.json 2> gpurun_out/io_bench.err || exit $?
 fi
+if [ "$STEP" = "sync" ]; then
+  # A/B of the durability flush: per-file fdatasync pair vs group-commit syncfs
+  DFS_GROUP_SYNC=0 timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_sync0.json 2> gpurun_out/bench_sync0.err && \
+  DFS_GROUP_SYNC=1 timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_sync1.json 2> gpurun_out/bench_sync1.err || exit $?
+fi
 if [ "$STEP" = "quick" ]; then
   timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || exit $?
 fi

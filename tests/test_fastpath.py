@@ -28,11 +28,11 @@ def test_write_read_roundtrip(server):
         data = os.urandom(3 * 1000 * 1000 + 17)
         slot = arena.acquire(len(data))
         arena.view[slot:slot + len(data)] = data
-        st, msg = cli.write("blk1", arena.path, slot, len(data), zlib.crc32(data), 5)
+        st, _r, msg = cli.write("blk1", arena.path, slot, len(data), zlib.crc32(data), 5)
         assert st == fp.OK, msg
         assert store.exists("blk1") and store.size("blk1") == len(data)
         # wrong CRC: the store rejects it, reported as IO_ERROR (client falls back / fails)
-        st, msg = cli.write("blk2", arena.path, slot, len(data), zlib.crc32(data) ^ 1, 5)
+        st, _r, msg = cli.write("blk2", arena.path, slot, len(data), zlib.crc32(data) ^ 1, 5)
         assert st == fp.IO_ERROR and "mismatch" in msg.lower()
         out = arena.acquire(1 << 20)
         st, total, n, _ = cli.read("blk1", 1000, 5000, arena.path, out, arena.slot)
@@ -60,12 +60,12 @@ def test_fencing_is_shared(server):
         assert srv.term == 7
         slot = arena.acquire(10)
         arena.view[slot:slot + 10] = b"0123456789"
-        st, msg = cli.write("old", arena.path, slot, 10, zlib.crc32(b"0123456789"), 3)
+        st, _r, msg = cli.write("old", arena.path, slot, 10, zlib.crc32(b"0123456789"), 3)
         assert st == fp.FENCED and "Stale master term" in msg
         assert srv.fence(9) == (True, 9)      # higher term adopted
         assert srv.fence(0) == (True, 9)      # term 0 = unfenced (legacy clients)
         assert srv.fence(8) == (False, 9)
-        st, _ = cli.write("new", arena.path, slot, 10, zlib.crc32(b"0123456789"), 9)
+        st, _r, _ = cli.write("new", arena.path, slot, 10, zlib.crc32(b"0123456789"), 9)
         assert st == fp.OK
     finally:
         cli.close()
@@ -77,9 +77,9 @@ def test_rejects_foreign_paths_and_corruption_punts(server, tmp_path):
     cli = fp.FastPathClient(srv.name)
     arena = ShmArena(size=16 << 20, slot=16 << 20)
     try:
-        st, msg = cli.write("x", "/etc/passwd", 0, 10, 0, 0)
+        st, _r, msg = cli.write("x", "/etc/passwd", 0, 10, 0, 0)
         assert st == fp.UNSUPPORTED and "refusing" in msg
-        st, msg = cli.write("x", "/dev/shm/dfs_sc_../../etc/passwd", 0, 10, 0, 0)
+        st, _r, msg = cli.write("x", "/dev/shm/dfs_sc_../../etc/passwd", 0, 10, 0, 0)
         assert st == fp.UNSUPPORTED
         data = os.urandom(100_000)
         slot = arena.acquire(len(data))
