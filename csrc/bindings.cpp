@@ -337,7 +337,8 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def_property_readonly("term", &FastPathServer::term)
       .def("drain_suspects", &FastPathServer::drain_suspects)
       .def("set_rccl", &FastPathServer::set_rccl, py::arg("engine"), py::keep_alive<1, 2>())
-      .def("set_peer", &FastPathServer::set_peer, py::arg("addr"), py::arg("rank"), py::arg("name"))
+      .def("set_peer", &FastPathServer::set_peer, py::arg("addr"), py::arg("rank"), py::arg("name") = "")
+      .def("set_self_host", &FastPathServer::set_self_host, py::arg("host"))
       .def("stats", [](FastPathServer& f) {
         FpStats s = f.stats();
         py::dict d;
@@ -348,6 +349,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["fp_connections"] = s.connections;
         d["fp_replicas_in"] = s.replicas_in;
         d["fp_rccl_forwards"] = s.rccl_forwards;
+        d["fp_shm_forwards"] = s.shm_forwards;
         d["fp_forward_failures"] = s.forward_failures;
         return d;
       });

@@ -284,13 +284,7 @@ void FastPathServer::set_peer(const std::string& addr, int rank, const std::stri
   auto& p = peers_[addr];
   if (!p) p = std::make_unique<Peer>();
   p->rank = rank;
-  p->name = fp_name;
-}
-
-FastPathServer::Peer* FastPathServer::peer(const std::string& addr) {
-  std::lock_guard<std::mutex> g(peers_mu_);
-  auto it = peers_.find(addr);
-  return it == peers_.end() ? nullptr : it->second.get();
+  if (!fp_name.empty()) p->name = fp_name;
 }
 
 namespace {
@@ -315,12 +309,63 @@ int connect_abstract(const std::string& name) {
 
 }  // namespace
 
+namespace {
+
+// One request/response exchange on a pooled peer connection.
+bool exchange(int fd, const std::vector<uint8_t>& req, std::vector<uint8_t>* resp) {
+  uint32_t n = 0;
+  if (!write_full(fd, req.data(), req.size())) return false;
+  if (!read_full(fd, &n, 4) || n < 19 || n > kMaxBody) return false;
+  resp->resize(n);
+  return read_full(fd, resp->data(), n);
+}
+
+std::string resp_msg(const std::vector<uint8_t>& r) {
+  uint16_t ml = 0;
+  std::memcpy(&ml, r.data() + 17, 2);
+  return std::string(reinterpret_cast<const char*>(r.data() + 19), std::min<size_t>(ml, r.size() - 19));
+}
+
+void finish_frame(std::vector<uint8_t>& req) {
+  uint32_t body = static_cast<uint32_t>(req.size() - 4);
+  std::memcpy(req.data(), &body, 4);
+}
+
+}  // namespace
+
+void FastPathServer::set_self_host(const std::string& host) {
+  std::lock_guard<std::mutex> g(peers_mu_);
+  self_host_ = host;
+}
+
+FastPathServer::Peer* FastPathServer::local_peer(const std::string& addr) {
+  // same-host peers are reachable at the deterministic socket "dfs_fp_<port>"
+  auto colon = addr.rfind(':');
+  if (colon == std::string::npos) return nullptr;
+  std::string host = addr.substr(0, colon), port = addr.substr(colon + 1);
+  std::lock_guard<std::mutex> g(peers_mu_);
+  auto it = peers_.find(addr);
+  if (it != peers_.end()) return it->second.get();
+  bool local = host == "127.0.0.1" || host == "localhost" || host == "::1" || (!self_host_.empty() && host == self_host_);
+  if (!local || port.empty()) return nullptr;
+  auto& p = peers_[addr];
+  p = std::make_unique<Peer>();
+  p->name = "dfs_fp_" + port;
+  return p.get();
+}
+
 bool FastPathServer::forward(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
-                             int* replicas, std::string* err) {
+                             const ShmSrc& src, int* replicas, std::string* err) {
   *replicas = 0;
-  Peer* p = next.empty() ? nullptr : peer(next[0]);
-  if (p == nullptr || rccl_ == nullptr || !rccl_->pair_ok(rccl_->rank(), p->rank)) {
+  Peer* p = next.empty() ? nullptr : local_peer(next[0]);
+  if (p == nullptr) {
     *err = "no native route to " + (next.empty() ? std::string("?") : next[0]);
+    return false;
+  }
+  bool use_rccl = rccl_ != nullptr && p->rank >= 0 && rccl_->pair_ok(rccl_->rank(), p->rank);
+  bool use_shm = !use_rccl && !src.path.empty();
+  if (!use_rccl && !use_shm) {
+    *err = "no RCCL pair and no shared-memory source for " + next[0];
     return false;
   }
   int fd = -1;
@@ -335,59 +380,74 @@ bool FastPathServer::forward(const std::string& id, uint32_t crc, uint64_t term,
     *err = "cannot reach fast path of " + next[0];
     return false;
   }
-  uint64_t size = 0;
-  int64_t seq = rccl_->send(p->rank, id, &size, err);
-  if (seq < 0) {
-    std::lock_guard<std::mutex> g(p->mu);
-    p->idle.push_back(fd);
-    return false;
-  }
-  std::vector<uint8_t> req(4, 0);
-  req.push_back(3);
-  put<uint64_t>(req, term);
-  put<uint32_t>(req, crc);
-  put<int32_t>(req, rccl_->rank());
-  put<int64_t>(req, seq);
-  put<uint64_t>(req, size);
-  put_str(req, id);
-  put<uint16_t>(req, static_cast<uint16_t>(next.size() - 1));
-  for (size_t i = 1; i < next.size(); ++i) put_str(req, next[i]);
-  uint32_t body = static_cast<uint32_t>(req.size() - 4);
-  std::memcpy(req.data(), &body, 4);
-  bool io_ok = write_full(fd, req.data(), req.size());
-  uint32_t n = 0;
-  std::vector<uint8_t> resp;
-  if (io_ok) io_ok = read_full(fd, &n, 4) && n >= 19 && n <= kMaxBody;
-  if (io_ok) {
-    resp.resize(n);
-    io_ok = read_full(fd, resp.data(), n);
-  }
-  std::string werr;
-  bool sent = rccl_->wait_send(p->rank, seq, &werr);
-  if (!io_ok || !sent) {
-    ::close(fd);
-    // an unmatched send would wedge this pair's stream: retire it (the gRPC path takes over)
-    rccl_->abort_pair(rccl_->rank(), p->rank);
-    *err = !io_ok ? "descriptor to " + next[0] + " failed" : "RCCL send failed: " + werr;
-    return false;
+  auto put_next = [&](std::vector<uint8_t>& req) {
+    put<uint16_t>(req, static_cast<uint16_t>(next.size() - 1));
+    for (size_t i = 1; i < next.size(); ++i) put_str(req, next[i]);
+  };
+  std::vector<uint8_t> req(4, 0), resp;
+  bool io_ok;
+  if (use_rccl) {
+    // payload GPU->GPU over xGMI (ncclSend from HBM), descriptor over the socket
+    uint64_t size = 0;
+    int64_t seq = rccl_->send(p->rank, id, &size, err);
+    if (seq < 0) {
+      std::lock_guard<std::mutex> g(p->mu);
+      p->idle.push_back(fd);
+      return false;
+    }
+    req.push_back(3);
+    put<uint64_t>(req, term);
+    put<uint32_t>(req, crc);
+    put<int32_t>(req, rccl_->rank());
+    put<int64_t>(req, seq);
+    put<uint64_t>(req, size);
+    put_str(req, id);
+    put_next(req);
+    finish_frame(req);
+    io_ok = exchange(fd, req, &resp);
+    std::string werr;
+    bool sent = rccl_->wait_send(p->rank, seq, &werr);
+    if (!io_ok || !sent) {
+      ::close(fd);
+      // an unmatched send would wedge this pair's stream: retire it; the next block on
+      // this hop uses the shared-memory route (or the client's gRPC fallback)
+      rccl_->abort_pair(rccl_->rank(), p->rank);
+      *err = !io_ok ? "descriptor to " + next[0] + " failed" : "RCCL send failed: " + werr;
+      return false;
+    }
+  } else {
+    // same-host hop without RCCL: the next server stages straight from the client's
+    // shared-memory slot (H2D on its own GPU) — no payload on any socket
+    req.push_back(4);
+    put<uint64_t>(req, term);
+    put<uint32_t>(req, crc);
+    put<uint64_t>(req, src.off);
+    put<uint64_t>(req, src.len);
+    put_str(req, id);
+    put_str(req, src.path);
+    put_next(req);
+    finish_frame(req);
+    io_ok = exchange(fd, req, &resp);
+    if (!io_ok) {
+      ::close(fd);
+      *err = "forward to " + next[0] + " failed";
+      return false;
+    }
   }
   {
     std::lock_guard<std::mutex> g(p->mu);
     p->idle.push_back(fd);
   }
-  auto st = static_cast<FpStatus>(resp[0]);
-  uint64_t downstream = 0;
-  std::memcpy(&downstream, resp.data() + 9, 8);
-  if (st != FpStatus::Ok) {
-    uint16_t ml = 0;
-    std::memcpy(&ml, resp.data() + 17, 2);
-    *err = "downstream " + next[0] + ": " + std::string(reinterpret_cast<const char*>(resp.data() + 19),
-                                                         std::min<size_t>(ml, resp.size() - 19));
+  if (static_cast<FpStatus>(resp[0]) != FpStatus::Ok) {
+    *err = "downstream " + next[0] + ": " + resp_msg(resp);
     return false;
   }
+  uint64_t downstream = 0;
+  std::memcpy(&downstream, resp.data() + 9, 8);
   *replicas = static_cast<int>(downstream);
   std::lock_guard<std::mutex> g(mu_);
-  st_.rccl_forwards++;
+  if (use_rccl) st_.rccl_forwards++;
+  else st_.shm_forwards++;
   return true;
 }
 
@@ -406,10 +466,10 @@ void FastPathServer::serve(int fd) {
   };
   // Local persist and downstream forward run concurrently; the ack waits for both.
   auto persist_and_forward = [&](const std::string& id, const uint8_t* host, uint64_t len, uint32_t crc,
-                                 uint64_t term, const std::vector<std::string>& next) -> bool {
+                                 uint64_t term, const std::vector<std::string>& next, const ShmSrc& src) -> bool {
     int down = 0;
     std::string ferr, perr;
-    auto fut = std::async(std::launch::async, [&] { return forward(id, crc, term, next, &down, &ferr); });
+    auto fut = std::async(std::launch::async, [&] { return forward(id, crc, term, next, src, &down, &ferr); });
     bool pok = store_->persist(id, host, host ? len : 0, &perr);
     bool fok = fut.get();
     if (!pok) return send_response(fd, FpStatus::IoError, 0, 0, perr);
@@ -440,7 +500,7 @@ void FastPathServer::serve(int fd) {
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed write request");
       } else if (fenced(term, &msg)) {
         sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
-      } else if (!next.empty() && (rccl_ == nullptr || peer(next[0]) == nullptr)) {
+      } else if (!next.empty() && local_peer(next[0]) == nullptr) {
         sent = send_response(fd, FpStatus::Unsupported, 0, 0, "no native route for the chain");
       } else if ((base = map_shm(path, off + len, &err)) == nullptr) {
         sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
@@ -454,7 +514,7 @@ void FastPathServer::serve(int fd) {
           sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
         } else {
           bump(&FpStats::writes);
-          sent = persist_and_forward(id, base + off, len, crc, term, next);
+          sent = persist_and_forward(id, base + off, len, crc, term, next, ShmSrc{path, off, len});
         }
       }
     } else if (op == 3) {  // REPL: block arrives over RCCL from the previous hop
@@ -480,7 +540,34 @@ void FastPathServer::serve(int fd) {
         } else {
           bump(&FpStats::replicas_in);
           sent = last ? send_response(fd, FpStatus::Ok, size, 1, "")
-                      : persist_and_forward(id, nullptr, size, crc, term, next);
+                      : persist_and_forward(id, nullptr, size, crc, term, next, ShmSrc{});
+        }
+      }
+    } else if (op == 4) {  // REPL_SHM: a same-host hop; stage from the client's slot
+      uint64_t term = rd.get<uint64_t>();
+      uint32_t crc = rd.get<uint32_t>();
+      uint64_t off = rd.get<uint64_t>(), len = rd.get<uint64_t>();
+      std::string id = rd.str(), path = rd.str();
+      std::vector<std::string> next = read_list(rd, false);
+      std::string err;
+      uint8_t* base = nullptr;
+      if (!rd.ok || id.empty()) {
+        sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed replicate request");
+      } else if (fenced(term, &msg)) {
+        sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
+      } else if ((base = map_shm(path, off + len, &err)) == nullptr) {
+        sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
+      } else if (next.empty()) {
+        WriteResult wr = store_->write(id, base + off, len, crc);
+        if (wr.ok) bump(&FpStats::replicas_in);
+        sent = wr.ok ? send_response(fd, FpStatus::Ok, len, 1, "") : send_response(fd, FpStatus::IoError, 0, 0, wr.error);
+      } else {
+        WriteResult wr = store_->stage(id, base + off, len, crc);
+        if (!wr.ok) {
+          sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
+        } else {
+          bump(&FpStats::replicas_in);
+          sent = persist_and_forward(id, base + off, len, crc, term, next, ShmSrc{path, off, len});
         }
       }
     } else if (op == 2) {  // READ into the client's slot

@@ -20,14 +20,17 @@
 //     op 2 READ : u64 offset | u64 length | u64 shm_off | u64 shm_cap | u16 id_len id | u16 path_len path
 //     op 3 REPL : u64 term | u32 crc | i32 src_rank | i64 seq | u64 size | u16 id_len id
 //               | u16 n_next | (u16 len addr)*      -- server-to-server: block arrives over RCCL
+//     op 4 REPL_SHM: u64 term | u32 crc | u64 shm_off | u64 len | u16 id_len id | u16 path_len path
+//               | u16 n_next | (u16 len addr)*      -- same-host hop without RCCL: read the client slot
 //   response = u32 body_len | u8 status | u64 total | u64 bytes | u16 msg_len msg
 //   (for WRITE/REPL ``bytes`` carries replicas_written)
 //
-// Chain replication stays native when every hop is a ChunkServer of this node with an
-// RCCL pair: the block is staged in HBM, sent GPU->GPU over xGMI with ncclSend, and the
-// ~100-byte descriptor goes to the next server's fast-path socket, concurrently with the
-// local fdatasync. Any hop without that route answers Unsupported and the client redoes
-// the write on the gRPC path (which has its own RCCL + gRPC fallback).
+// Chain replication stays native when every hop is a ChunkServer of this host: with an
+// RCCL pair the block is staged in HBM and sent GPU->GPU over xGMI with ncclSend while a
+// ~100-byte descriptor goes to the next server's fast-path socket (named dfs_fp_<port>);
+// without one (pair broken, GPUs shared, CPU store) the next server stages straight from
+// the client's shared-memory slot. Either way the hop overlaps the local fdatasync. A hop
+// off this host answers Unsupported and the client redoes the write on the gRPC path.
 #pragma once
 #include <atomic>
 #include <cstdint>
@@ -57,7 +60,7 @@ enum class FpStatus : uint8_t {
 
 struct FpStats {
   uint64_t writes = 0, reads = 0, fenced = 0, punts = 0, connections = 0;
-  uint64_t replicas_in = 0, rccl_forwards = 0, forward_failures = 0;
+  uint64_t replicas_in = 0, rccl_forwards = 0, shm_forwards = 0, forward_failures = 0;
 };
 
 class FastPathServer {
@@ -84,6 +87,7 @@ class FastPathServer {
   // same-node peer (advertised address -> rank, socket name).
   void set_rccl(RcclEngine* engine);
   void set_peer(const std::string& addr, int rank, const std::string& fp_name);
+  void set_self_host(const std::string& host);  // our advertised host: same-host peer detection
 
  private:
   struct Peer {
@@ -97,9 +101,13 @@ class FastPathServer {
   uint8_t* map_shm(const std::string& path, uint64_t need, std::string* err);
   // Send block `id` (resident in HBM) to next[0] over RCCL + descriptor; *replicas gets
   // the downstream count. False (with *err) when there is no native route or it failed.
+  struct ShmSrc {
+    std::string path;  // client arena the block came from (empty: HBM-only, e.g. RCCL-received)
+    uint64_t off = 0, len = 0;
+  };
   bool forward(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
-               int* replicas, std::string* err);
-  Peer* peer(const std::string& addr);
+               const ShmSrc& src, int* replicas, std::string* err);
+  Peer* local_peer(const std::string& addr);
 
   ChunkStore* store_;
   std::string name_;
@@ -121,6 +129,7 @@ class FastPathServer {
   RcclEngine* rccl_ = nullptr;
   std::mutex peers_mu_;
   std::unordered_map<std::string, std::unique_ptr<Peer>> peers_;
+  std::string self_host_;
 };
 
 }  // namespace dfs

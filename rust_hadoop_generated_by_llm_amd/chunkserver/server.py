@@ -116,9 +116,11 @@ class ChunkServerProcess:
         self.fastpath = None
         if not args.no_fastpath:
             port = strip_scheme(args.addr).rsplit(":", 1)[-1]
-            fp = native.FastPathServer(self.store, f"dfs_fp_{os.getpid()}_{port}")
+            # deterministic name: same-host peers find each other from the advertised port
+            fp = native.FastPathServer(self.store, f"dfs_fp_{port}")
             ok, err = fp.start()
             if ok:
+                fp.set_self_host(self.advertise.rsplit(":", 1)[0])
                 self.fastpath = fp
             else:
                 log.warning("native fast path disabled: %s", err)
@@ -139,8 +141,8 @@ class ChunkServerProcess:
                     # chains between same-node GPUs stay native: RCCL payload + socket descriptor
                     self.fastpath.set_rccl(eng)
                     for a, r in rank_map.items():
-                        if r != args.rccl_rank and a in fp_names:
-                            self.fastpath.set_peer(a, r, fp_names[a])
+                        if r != args.rccl_rank:
+                            self.fastpath.set_peer(a, r, fp_names.get(a, ""))
             else:
                 log.error("RCCL init failed (%s); using gRPC replication", err)
         self.metrics = Registry()
