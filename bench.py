@@ -40,8 +40,8 @@ PKG = "rust_hadoop_generated_by_llm_amd"
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--count", type=int, default=100)
     p.add_argument("--size", type=int, default=1 << 20)
     p.add_argument("--concurrency", type=int, default=10)
@@ -142,7 +142,20 @@ def main():
     import torch.distributed as dist
 
     if world > 1:
-        dist.init_process_group("gloo")
+        # gloo prints its connection banner straight to fd 1; the driver reads exactly one
+        # JSON line from rank 0's stdout, so keep the banner off it
+        sys.stdout.flush()
+        saved = os.dup(1)
+        devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(devnull)
 
     def gather(obj):
         if world == 1:

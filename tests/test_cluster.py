@@ -242,7 +242,7 @@ def test_local_short_circuit_and_fast_path():
         for p, d in blobs.items():
             assert c.get_file_content(p) == d
         assert c.read_file_range("/sc/f3", 1234, 5000) == blobs["/sc/f3"][1234:6234]
-        assert c.sc_ops >= 1 and c.fp_ops >= 10 and c.fastpath is not None
+        assert c.fp_ops >= 12 and c.fastpath is not None  # socket name known up front
         st = json.load(urllib.request.urlopen(f"{cl.cs_http[0]}/stats"))
         assert st["fp_writes"] >= 5 and st["fp_reads"] >= 6
         # duplicate create through the deferred path is refused at CompleteFile/CreateFile
@@ -255,4 +255,5 @@ def test_local_short_circuit_and_fast_path():
         c.fastpath = fpmod.FastPathClient("dfs_fp_nonexistent")
         c.create_file_from_buffer(b"fallback", "/sc/fallback")
         assert c.get_file_content("/sc/fallback") == b"fallback"
+        assert c.sc_ops >= 1  # the gRPC shm short-circuit carried it
         c.close()
