@@ -83,6 +83,19 @@ PYBIND11_MODULE(_dfs_native, m) {
     py::gil_scoped_release r;
     std::memcpy(static_cast<uint8_t*>(d.ptr) + off, sv.p, sv.n);
   }, py::arg("dst"), py::arg("offset"), py::arg("src"));
+  m.def("copy_out", [](py::buffer src, uint64_t off, uint64_t n) {
+    // new bytes object holding src[off:off+n], memcpy with the GIL released
+    py::buffer_info sk;
+    Buf sv = view(src, sk);
+    if (off > sv.n || n > sv.n - off) throw std::out_of_range("copy_out: range outside source");
+    char* d;
+    py::bytes out = new_bytes(n, &d);
+    {
+      py::gil_scoped_release r;
+      std::memcpy(d, sv.p + off, n);
+    }
+    return out;
+  }, py::arg("src"), py::arg("offset"), py::arg("length"));
   m.def("crc32", [](py::buffer b, uint32_t crc) {
     py::buffer_info k;
     Buf v = view(b, k);

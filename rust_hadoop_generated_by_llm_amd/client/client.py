@@ -454,7 +454,7 @@ class Client:
                             st, _total, n, _msg = fp.read(block_id, offset, length, arena.path, slot, arena.slot)
                             if st in (fpmod.OK, fpmod.PARTIAL_CORRUPT):
                                 self.fp_ops += 1
-                                return bytes(arena.view[slot:slot + n])
+                                return _native.copy_out(arena.mm, slot, n)
                         except fpmod.FastPathError as e:
                             self._fp_failed(e)
                         # any other status: the gRPC call below reports/recovers it
@@ -465,7 +465,7 @@ class Client:
                     self._learn_fastpath(r)
                     if r.shm_filled:
                         self.sc_ops += 1
-                        return bytes(arena.view[slot:slot + r.bytes_read])
+                        return _native.copy_out(arena.mm, slot, r.bytes_read)
                     return r.data
                 except grpc.RpcError as e:
                     if not self._sc_failed(e):

@@ -45,7 +45,8 @@ class LocalCluster:
                  durability: str = "nvme-sync", fsync: bool = True, rccl: bool = True,
                  hbm_capacity: str = "0", heartbeat_interval: float = 0.5, scrub_interval: float = 60.0,
                  rack_ids: list[str] | None = None, fast_intervals: bool = False, cold_dir: bool = False,
-                 env: dict | None = None, master_args: list[str] | None = None, cs_args: list[str] | None = None):
+                 env: dict | None = None, master_args: list[str] | None = None, cs_args: list[str] | None = None,
+                 tls: bool = False):
         self.owns_dir = base_dir is None
         self.base = Path(base_dir or tempfile.mkdtemp(prefix="dfs_cluster_"))
         self.base.mkdir(parents=True, exist_ok=True)
@@ -71,6 +72,8 @@ class LocalCluster:
             self.env.update(env)
         self.master_args = master_args or []
         self.cs_args = cs_args or []
+        self.tls = tls
+        self.ca_cert: str | None = None
         self.procs: list[Proc] = []
         self.config_addrs: list[str] = []
         self.shard_masters: dict[str, list[str]] = {}
@@ -128,8 +131,28 @@ class LocalCluster:
             raise
         return self
 
+    def make_certs(self) -> tuple[str, str, str]:
+        """Self-signed CA + a server certificate for 127.0.0.1/localhost (openssl CLI)."""
+        d = self.base / "tls"
+        d.mkdir(exist_ok=True)
+        ca_key, ca, key, csr, crt = (str(d / n) for n in ("ca.key", "ca.pem", "server.key", "server.csr", "server.pem"))
+        ext = d / "san.cnf"
+        ext.write_text("subjectAltName=IP:127.0.0.1,DNS:localhost\nbasicConstraints=CA:FALSE\n")
+        run = lambda *a: subprocess.run(["openssl", *a], check=True, capture_output=True)  # noqa: E731
+        run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", ca_key, "-out", ca, "-days", "2",
+            "-subj", "/CN=dfs-test-ca")
+        run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", key, "-out", csr, "-subj", "/CN=localhost")
+        run("x509", "-req", "-in", csr, "-CA", ca, "-CAkey", ca_key, "-CAcreateserial", "-out", crt, "-days", "2",
+            "-extfile", str(ext))
+        return ca, crt, key
+
     def _start(self) -> None:
         fs = [] if self.fsync else ["--no-fsync"]
+        tls_args: list[str] = []
+        if self.tls:
+            ca, crt, key = self.make_certs()
+            self.ca_cert = ca
+            tls_args = ["--tls-cert", crt, "--tls-key", key, "--ca-cert", ca]
         if self.use_config:
             port, http = free_port(), free_port()
             pr = self._spawn("config", "config_server.server", [
@@ -154,7 +177,8 @@ class LocalCluster:
                 gport, hport = ports[i]
                 peers = ",".join(f"{j}@http://127.0.0.1:{ports[j][1]}" for j in ids if j != i)
                 args = ["--addr", f"127.0.0.1:{gport}", "--id", str(i), "--http-port", str(hport),
-                        "--storage-dir", str(self.base / f"master_{sid}"), "--shard-id", sid, *fs, *self.master_args]
+                        "--storage-dir", str(self.base / f"master_{sid}"), "--shard-id", sid, *fs, *tls_args,
+                        *self.master_args]
                 if peers:
                     args += ["--peers", peers]
                 if self.use_config:
@@ -179,7 +203,7 @@ class LocalCluster:
                     "--storage-dir", str(self.base / f"cs{i}"), "--gpu", str(gpu),
                     "--durability", self.durability, "--hbm-capacity", self.hbm_capacity,
                     "--heartbeat-interval", str(self.heartbeat_interval),
-                    "--scrub-interval", str(self.scrub_interval), *fs, *self.cs_args]
+                    "--scrub-interval", str(self.scrub_interval), *fs, *tls_args, *self.cs_args]
             if self.cold_dir:
                 args += ["--cold-storage-dir", str(self.base / f"cs{i}_cold")]
             if self.rack_ids:
@@ -241,6 +265,8 @@ class LocalCluster:
     def client(self, **kw):
         from ..client.client import Client
 
+        if self.tls:
+            kw.setdefault("ca_cert", self.ca_cert)
         c = Client(self.master_addrs, self.config_addrs, **kw)
         if not self.use_config:
             from ..parallel.sharding import ShardMap
@@ -257,7 +283,7 @@ class LocalCluster:
         from ..models import proto as pb
         from ..utils.rpc import ChannelPool
 
-        pool = ChannelPool()
+        pool = ChannelPool(self.ca_cert)
         deadline = time.time() + timeout
         try:
             for sid, masters in self.shard_masters.items():

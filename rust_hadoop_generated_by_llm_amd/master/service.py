@@ -48,7 +48,7 @@ def new_rename_record(tx_id, source_path, dest_path, source_shard, dest_shard, d
 class MasterService:
     def __init__(self, state: MasterState, raft: RaftNode, shard_map: ShardMap, shard_id: str,
                  monitor: ThroughputMonitor, pool: AioChannelPool, *, advertise_addr: str = "",
-                 access_stats: bool = True, access_stats_flush_ms: int = 200):
+                 access_stats: bool = True, access_stats_flush_ms: int = 1000):
         self.state = state
         self.raft = raft
         self.shard_map = shard_map
@@ -130,8 +130,8 @@ class MasterService:
     # ------------------------------------------------------------------ access stats
     def _record_access(self, path: str) -> None:
         """The reference fires one Raft write per GetFileInfo (master.rs:2187-2209). Same
-        semantics (last_access_ms, access_count) but coalesced: reads within a short
-        window become one replicated UpdateAccessStats per path."""
+        semantics (last_access_ms, access_count) but batched: all reads of a short window
+        become ONE replicated UpdateAccessStatsBatch entry ({path: [ts, count]})."""
         if not self.access_stats or not self.raft.is_leader():
             return
         self._access_buf[path] = self._access_buf.get(path, 0) + 1
@@ -141,10 +141,10 @@ class MasterService:
     async def _flush_access(self) -> None:
         await asyncio.sleep(self._access_flush_ms / 1000.0)
         buf, self._access_buf = self._access_buf, {}
-        t = now_ms()
-        for path, count in buf.items():
-            for _ in range(count):
-                self.raft.propose_nowait({"Master": {"UpdateAccessStats": {"path": path, "accessed_at_ms": t}}})
+        if buf:
+            t = now_ms()
+            self.raft.propose_nowait({"Master": {"UpdateAccessStatsBatch": {
+                "accessed_at_ms": t, "paths": buf}}})
 
     # ------------------------------------------------------------------ file operations
     async def get_file_info(self, req, ctx):

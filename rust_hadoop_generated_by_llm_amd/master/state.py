@@ -416,6 +416,14 @@ class MasterState:
             m.last_access_ms = a["accessed_at_ms"]
             m.access_count += 1
 
+    def _cmd_UpdateAccessStatsBatch(self, a):
+        t = a["accessed_at_ms"]
+        for path, count in a["paths"].items():
+            m = self.files.get(path)
+            if m is not None:
+                m.last_access_ms = t
+                m.access_count += int(count)
+
     def _cmd_MoveToCold(self, a):
         m = self.files.get(a["path"])
         if m is not None:

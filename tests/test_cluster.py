@@ -257,3 +257,20 @@ def test_local_short_circuit_and_fast_path():
         assert c.get_file_content("/sc/fallback") == b"fallback"
         assert c.sc_ops >= 1  # the gRPC shm short-circuit carried it
         c.close()
+
+
+def test_tls_cluster():
+    """gRPC over TLS end to end (reference C06 TLS helper): masters and chunkservers serve
+    with a CA-signed certificate, clients verify it; a plaintext client cannot talk to them."""
+    with LocalCluster(n_chunkservers=2, fsync=False, tls=True) as cl:
+        c = cl.client()
+        data = os.urandom(300_000)
+        c.create_file_from_buffer(data, "/tls/f")
+        assert c.get_file_content("/tls/f") == data
+        assert len(c.get_file_info("/tls/f").blocks[0].locations) == 2
+        c.close()
+        plain = ChannelPool()
+        with pytest.raises(grpc.RpcError):
+            plain.call(cl.master_addrs[0].replace("https://", "http://"), "MasterService", "GetSafeModeStatus",
+                       pb.GetSafeModeStatusRequest(), timeout=3)
+        plain.close()
