@@ -486,12 +486,32 @@ bool ChunkStore::make_durable(int data_fd, int meta_fd, bool cold) {
 }
 
 // ---------------------------------------------------------------- write
+// Block ids become file names under the storage directories: accept only a plain name
+// (letters, digits, '-', '_', '.', not starting with '.'), so no id reaches outside them.
+bool valid_block_id(const std::string& id) {
+  if (id.empty() || id.size() > 200 || id[0] == '.') return false;
+  for (char c : id) {
+    bool ok = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '-' || c == '_' ||
+              c == '.';
+    if (!ok) return false;
+  }
+  return !ends_with(id, ".meta") && !ends_with(id, ".tmp");
+}
+
+static WriteResult bad_id(const std::string& id) {
+  WriteResult r;
+  r.error = "invalid block id: " + id.substr(0, 64);
+  return r;
+}
+
 WriteResult ChunkStore::write(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
+  if (!valid_block_id(id)) return bad_id(id);
   if (!gpu()) return write_host(id, data, n, expected_crc);
   return stage_impl(id, data, n, expected_crc, true);
 }
 
 WriteResult ChunkStore::stage(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
+  if (!valid_block_id(id)) return bad_id(id);
   if (!gpu()) return write_host(id, data, n, expected_crc);
   return stage_impl(id, data, n, expected_crc, false);
 }
@@ -654,6 +674,7 @@ bool ChunkStore::persist_from_device(const std::string& id, const uint8_t* d, ui
 }
 
 WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc) {
+  if (!valid_block_id(id)) return bad_id(id);
   WriteResult res;
   uint32_t actual = crc32(data, n);
   res.actual_crc = actual;

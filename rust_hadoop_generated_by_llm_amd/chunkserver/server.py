@@ -179,7 +179,7 @@ class ChunkServerProcess:
         for c in self.config_servers:
             try:
                 r = self.pool.call(c, "ConfigService", "FetchShardMap", pb.FetchShardMapRequest(), timeout=5.0)
-                new = ShardMap.from_peers({k: list(v.peers) for k, v in r.shards.items()})
+                new = ShardMap.from_fetch(r)
                 sm = self.shard_map
                 sm.strategy, sm.ranges, sm.ring, sm.shards, sm.shard_peers = (
                     new.strategy, new.ranges, new.ring, new.shards, new.shard_peers)
@@ -197,11 +197,12 @@ class ChunkServerProcess:
         if self.fastpath is not None:
             for bid in self.fastpath.drain_suspects():  # partial-read corruption seen natively
                 self.cs.queue_recovery(bid)
-        bad, new = self.cs.drain_reports()
+        bad, new, enc, fail, rebuilt = self.cs.drain_reports()
         req = pb.HeartbeatRequest(chunk_server_address=self.advertise, used_space=used, available_space=avail,
                                   chunk_count=st["blocks"], bad_blocks=bad, rack_id=self.args.rack_id,
                                   gpu_rank=self.args.rccl_rank, hbm_capacity=st["hbm_capacity"],
-                                  hbm_used=st["hbm_used"], new_blocks=new)
+                                  hbm_used=st["hbm_used"], new_blocks=new, ec_encoded=enc,
+                                  ec_failed=fail, ec_rebuilt=rebuilt)
         for m in self.masters():
             try:
                 r = self.pool.call(m, "MasterService", "Heartbeat", req, timeout=5.0)

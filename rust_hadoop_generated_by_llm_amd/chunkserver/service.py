@@ -46,6 +46,9 @@ class ChunkServer:
         self._term_lock = threading.Lock()
         self.pending_bad_blocks: list[str] = []
         self.new_blocks: list[str] = []
+        self.ec_encoded: list[str] = []
+        self.ec_failed: list[str] = []
+        self.ec_rebuilt: list[str] = []
         self._lists_lock = threading.Lock()
         self._bg = ThreadPoolExecutor(max_workers=4, thread_name_prefix="cs-bg")
         self._fwd = ThreadPoolExecutor(max_workers=64, thread_name_prefix="cs-fwd")
@@ -339,8 +342,51 @@ class ChunkServer:
         full = erasure.reconstruct(shards, k, m, self.store)
         ok, _c, err = self.store.write(cmd.block_id, full[cmd.shard_index], 0)
         if ok:
-            with self._lists_lock:
-                self.new_blocks.append(cmd.block_id)
+            with self._lists_lock:  # the master puts us at the shard's index, not at the end
+                self.ec_rebuilt.append(f"{cmd.block_id}/{cmd.shard_index}")
+        return ok
+
+    def encode_ec(self, cmd) -> bool:
+        """Tiering's EC conversion (C32) done for real: read the verified local replica,
+        RS(k,m)-encode it (GF(2^8) kernel on the GPU when the store has one) and write shard
+        i as block ``new_block_id`` to ec_shard_sources[i]. The master swaps the file to the
+        new shards only after every block reported success, then deletes the replicas —
+        the reference converts metadata only and never re-encodes (master.rs:2108-2118)."""
+        k, m = cmd.ec_data_shards, cmd.ec_parity_shards
+        targets = list(cmd.ec_shard_sources)
+        new_id = cmd.new_block_id
+        ok = False
+        try:
+            if k <= 0 or m <= 0 or len(targets) != k + m or not new_id:
+                raise ValueError(f"bad ENCODE_EC command for {cmd.block_id}")
+            st, _total, data, _p, _b, err = self.store.read(cmd.block_id, 0, 0)
+            if st != ST_OK:
+                raise ValueError(f"source replica unreadable: {err}")
+            shards = erasure.encode(data, k, m, self.store)
+            me = strip_scheme(self.addr)
+
+            def put(i: int) -> None:
+                crc = crcops.crc32(shards[i])
+                if strip_scheme(targets[i]) == me:
+                    w_ok, _c, w_err = self.store.write(new_id, shards[i], crc)
+                    if not w_ok:
+                        raise ValueError(f"local shard {i}: {w_err}")
+                    return
+                r = self.pool.call(targets[i], "ChunkServerService", "WriteBlock",
+                                   pb.WriteBlockRequest(block_id=new_id, data=shards[i], expected_checksum_crc32c=crc,
+                                                        shard_index=i, master_term=cmd.master_term), timeout=60.0)
+                if not r.success:
+                    raise ValueError(f"shard {i} at {targets[i]}: {r.error_message}")
+
+            with ThreadPoolExecutor(max_workers=min(16, k + m), thread_name_prefix="cs-ec") as ex:
+                for f in [ex.submit(put, i) for i in range(k + m)]:
+                    f.result()
+            ok = True
+            log.info("encoded %s as RS(%d,%d) -> %s", cmd.block_id, k, m, new_id)
+        except Exception as e:  # noqa: BLE001
+            log.error("ENCODE_EC %s failed: %s", cmd.block_id, rpc_details(e) if hasattr(e, "code") else e)
+        with self._lists_lock:
+            (self.ec_encoded if ok else self.ec_failed).append(cmd.block_id)
         return ok
 
     def handle_command(self, cmd) -> None:
@@ -355,12 +401,19 @@ class ChunkServer:
             self._bg.submit(self.store.move_to_cold, cmd.block_id)
         elif cmd.type == T.DELETE:
             self._bg.submit(self.store.remove, cmd.block_id)
+        elif cmd.type == T.ENCODE_EC:
+            self._bg.submit(self.encode_ec, cmd)
 
-    def drain_reports(self) -> tuple[list[str], list[str]]:
+    def drain_reports(self) -> tuple[list[str], list[str], list[str], list[str], list[str]]:
+        """(bad blocks, new blocks, EC jobs finished, EC jobs failed, EC shards rebuilt) for
+        the next heartbeat."""
         with self._lists_lock:
             bad, self.pending_bad_blocks = self.pending_bad_blocks, []
             new, self.new_blocks = self.new_blocks, []
-        return bad, new
+            enc, self.ec_encoded = self.ec_encoded, []
+            fail, self.ec_failed = self.ec_failed, []
+            rebuilt, self.ec_rebuilt = self.ec_rebuilt, []
+        return bad, new, enc, fail, rebuilt
 
     def scrub_once(self) -> list[str]:
         """K1b batched scrub: verify every block; queue bad ones for the next heartbeat

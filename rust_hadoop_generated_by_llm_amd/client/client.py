@@ -234,7 +234,7 @@ class Client:
                 log.debug("FetchShardMap from %s failed: %s", c, rpc_details(e))
                 continue
             if r.shards:
-                self.set_shard_map(ShardMap.from_peers({k: list(v.peers) for k, v in r.shards.items()}))
+                self.set_shard_map(ShardMap.from_fetch(r))
             return
 
     # ------------------------------------------------------------------ namespace ops

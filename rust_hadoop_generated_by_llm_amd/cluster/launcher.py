@@ -46,7 +46,7 @@ class LocalCluster:
                  hbm_capacity: str = "0", heartbeat_interval: float = 0.5, scrub_interval: float = 60.0,
                  rack_ids: list[str] | None = None, fast_intervals: bool = False, cold_dir: bool = False,
                  env: dict | None = None, master_args: list[str] | None = None, cs_args: list[str] | None = None,
-                 tls: bool = False):
+                 tls: bool = False, standby_masters: int = 0):
         self.owns_dir = base_dir is None
         self.base = Path(base_dir or tempfile.mkdtemp(prefix="dfs_cluster_"))
         self.base.mkdir(parents=True, exist_ok=True)
@@ -63,6 +63,8 @@ class LocalCluster:
         self.scrub_interval = scrub_interval
         self.rack_ids = rack_ids
         self.fast_intervals = fast_intervals
+        self.standby_masters = standby_masters
+        self.standby_addrs: list[str] = []
         self.cold_dir = cold_dir
         self.env = dict(os.environ)
         self.env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -189,6 +191,16 @@ class LocalCluster:
                     args.append("--fast-intervals")
                 mprocs.append(self._spawn(f"master_{sid}_{i}", "master.server", args))
                 self.master_http[f"http://127.0.0.1:{gport}"] = f"http://127.0.0.1:{hport}"
+        for i in range(self.standby_masters if self.use_config else 0):
+            gport, hport = free_port(), free_port()
+            args = ["--addr", f"127.0.0.1:{gport}", "--id", "1", "--http-port", str(hport), "--storage-dir",
+                    str(self.base / f"master_standby{i}"), "--standby", "--config-servers", ",".join(self.config_addrs),
+                    *fs, *tls_args, *self.master_args]
+            if self.fast_intervals:
+                args.append("--fast-intervals")
+            mprocs.append(self._spawn(f"master_standby{i}", "master.server", args))
+            self.standby_addrs.append(f"http://127.0.0.1:{gport}")
+            self.master_http[f"http://127.0.0.1:{gport}"] = f"http://127.0.0.1:{hport}"
         self._wait_ready(mprocs)
         self.shard_masters = shard_cfg
         # chunkservers

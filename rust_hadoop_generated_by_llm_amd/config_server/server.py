@@ -3,8 +3,9 @@ dfs/metaserver/src/config_server.rs and bin/config_server.rs).
 
 State ``{"Config": {"shard_map": ShardMap(Range), "masters": {addr: MasterInfo}}}``.
 FetchShardMap is linearizable (ReadIndex) and, like the reference, returns only
-shard -> peers (no range boundaries). SplitShard without peers auto-allocates the three
-most recently heartbeated masters. HTTP: /raft/{vote,append,snapshot}, /shards, plus
+shard -> peers (no range boundaries). SplitShard without peers allocates standby masters (registered
+with an empty shard id) first, else the three most recently heartbeated masters; the
+``ranges`` extension of FetchShardMap carries the split keys. HTTP: /raft/{vote,append,snapshot}, /shards, plus
 /health and /metrics (the reference has neither)."""
 from __future__ import annotations
 
@@ -46,13 +47,24 @@ class ConfigState:
         elif name == "RemoveShard":
             sm.remove_shard(a["shard_id"])
         elif name == "SplitShard":
-            return sm.split_shard(a["split_key"], a["new_shard_id"], a["new_shard_peers"])
+            ok = sm.split_shard(a["split_key"], a["new_shard_id"], a["new_shard_peers"])
+            if ok:
+                for addr in a["new_shard_peers"]:
+                    if addr in self.masters:
+                        self.masters[addr]["shard_id"] = a["new_shard_id"]
+            return ok
         elif name == "MergeShard":
             return sm.merge_shards(a["victim_shard_id"], a["retained_shard_id"])
         elif name == "RebalanceShard":
             return sm.rebalance_boundary(a["old_key"], a["new_key"])
         elif name == "RegisterMaster":
             addr, sid = a["address"], a["shard_id"]
+            if not sid:  # standby master: waits in the registry for a SplitShard allocation
+                # (a standby that a split already placed keeps that shard)
+                owned = next((s for s in sm.get_all_shards() if addr in (sm.get_shard_peers(s) or [])), "")
+                self.masters[addr] = {"address": addr, "shard_id": owned,
+                                      "last_heartbeat": int(time.time()), "rps_per_prefix": {}}
+                return None
             if not sm.has_shard(sid):
                 sm.add_shard(sid, [addr])
             else:
@@ -101,6 +113,9 @@ class ConfigService:
         sm = self.state.shard_map
         for sid in sm.get_all_shards():
             resp.shards[sid].peers.extend(sm.get_shard_peers(sid) or [])
+        if sm.strategy == "range":
+            for end, sid in sm.ranges.items():
+                resp.ranges[end] = sid
         return resp
 
     async def add_shard(self, req, ctx):
@@ -112,20 +127,33 @@ class ConfigService:
     async def split_shard(self, req, ctx):
         peers = list(req.new_shard_peers)
         if not peers:
+            # prefer standby masters (registered without a shard); the reference takes the
+            # three most recently heartbeated masters even if they serve another shard
             avail = sorted(self.state.masters.values(), key=lambda m: -m["last_heartbeat"])
-            peers = [m["address"] for m in avail[:3]]
+            standby = [m["address"] for m in avail if not m.get("shard_id")]
+            peers = standby[:3] or [m["address"] for m in avail[:3]]
         if not peers:
             return pb.SplitShardResponse(success=False, error_message="No available master nodes for new shard")
         try:
-            await self._propose("SplitShard", {"shard_id": req.shard_id, "split_key": req.split_key,
-                                               "new_shard_id": req.new_shard_id, "new_shard_peers": peers})
+            ok = await self._propose("SplitShard", {"shard_id": req.shard_id, "split_key": req.split_key,
+                                                    "new_shard_id": req.new_shard_id, "new_shard_peers": peers})
         except NotLeader as e:
             return pb.SplitShardResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        if not ok:
+            return pb.SplitShardResponse(success=False, error_message="split rejected by the shard map")
         return pb.SplitShardResponse(success=True, new_shard_peers=peers)
 
     async def merge_shard(self, req, ctx):
-        return await self._simple(pb.MergeShardResponse, "MergeShard", {
-            "victim_shard_id": req.victim_shard_id, "retained_shard_id": req.retained_shard_id})
+        # the apply result decides: two idle neighbours may try to merge into each other,
+        # and only the first may win (the reference reports success either way)
+        try:
+            ok = await self._propose("MergeShard", {"victim_shard_id": req.victim_shard_id,
+                                                    "retained_shard_id": req.retained_shard_id})
+        except NotLeader as e:
+            return pb.MergeShardResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
+        if not ok:
+            return pb.MergeShardResponse(success=False, error_message="merge rejected: unknown shard")
+        return pb.MergeShardResponse(success=True)
 
     async def rebalance_shard(self, req, ctx):
         return await self._simple(pb.RebalanceShardResponse, "RebalanceShard",

@@ -28,6 +28,7 @@ log = logging.getLogger("dfs.master.bg")
 MAX_INQUIRY_RETRIES = 60
 CS_DEAD_MS = int(os.environ.get("DFS_CS_DEAD_MS", "15000"))  # reference: 15 s
 BALANCE_GAP = 100 * 1024 * 1024
+EC_JOB_TIMEOUT_MS = 120_000
 
 
 @dataclass
@@ -66,6 +67,9 @@ class MasterBackground:
         self.ec_threshold_ms = ec_threshold_secs * 1000
         self.ec_conversion = (os.environ.get("EC_CONVERSION_ENABLED", "0") == "1") if ec_conversion is None \
             else ec_conversion
+        # reference converts to RS(6,3); smaller codes for small clusters / tests
+        self.ec_k = int(os.environ.get("EC_CONVERSION_DATA_SHARDS", "6"))
+        self.ec_m = int(os.environ.get("EC_CONVERSION_PARITY_SHARDS", "3"))
         self.registered = False
         self._tasks: list[asyncio.Task] = []
         if config_servers:
@@ -264,12 +268,19 @@ class MasterBackground:
         resp = await self._config_call("FetchShardMap", pb.FetchShardMapRequest())
         if resp is None or not resp.shards:
             return
-        new = ShardMap.from_peers({k: list(v.peers) for k, v in resp.shards.items()})
+        new = ShardMap.from_fetch(resp)
         self.svc.shard_map_fetched_ms = now_ms()
         m = self.svc.shard_map
         m.strategy, m.ranges, m.ring, m.shards, m.shard_peers = new.strategy, new.ranges, new.ring, new.shards, \
             new.shard_peers
         m._dirty()
+        if not self.svc.shard_id:  # standby master: a SplitShard allocated us a shard
+            me = self.svc.advertise_addr
+            for sid in m.get_all_shards():
+                if me in (m.get_shard_peers(sid) or []):
+                    self.svc.shard_id = sid
+                    log.info("standby master %s now serves shard %s", me, sid)
+                    break
 
     async def register(self) -> None:
         if self.registered or not self.config_servers:
@@ -291,38 +302,77 @@ class MasterBackground:
         if not self.raft.is_leader():
             return
         hot = mon.hot_prefix()
-        if hot is not None:
+        if hot is not None and self.svc.shard_id:
             prefix, rps = hot
-            log.info("hot prefix %s (%.1f rps): splitting shard %s", prefix, rps, self.svc.shard_id)
-            new_id = f"{self.svc.shard_id}-split-{uuid.uuid4().hex[:8]}"
-            # collect BEFORE the split removes them (the reference collects afterwards and
-            # ships an empty batch, master.rs:1600-1615)
-            moving = [M.file_to_dict(f) for p, f in self.state.files.items() if p >= prefix]
-            if not await self._propose("SplitShard", {"split_key": prefix, "new_shard_id": new_id,
-                                                      "new_shard_peers": []}):
-                return
-            import time as _t
-
-            mon.last_split_time = _t.monotonic()
-            r = await self._config_call("SplitShard", pb.SplitShardRequest(
-                shard_id=self.svc.shard_id, split_key=prefix, new_shard_id=new_id))
-            if r is not None and r.success and moving:
-                req = pb.IngestMetadataRequest(files=[M.file_from_dict(d) for d in moving])
-                await self.svc._call_peers(list(r.new_shard_peers), "IngestMetadata", req, lambda x: x.success)
+            await self._split(prefix, rps)
             return
         total = mon.total_rps()
-        if 0 <= mon.merge_threshold_rps and total < mon.merge_threshold_rps and self.state.files:
+        if 0 <= mon.merge_threshold_rps and total < mon.merge_threshold_rps and self.state.files \
+                and self.svc.shard_id:
             prev, nxt = self.svc.shard_map.get_neighbors(self.svc.shard_id)
             neighbor = prev or nxt
             if neighbor is None:
                 return
-            r = await self._config_call("MergeShard", pb.MergeShardRequest(
-                victim_shard_id=self.svc.shard_id, retained_shard_id=neighbor))
-            if r is not None and r.success:
-                peers = self.svc.shard_map.get_shard_peers(neighbor) or []
-                req = pb.IngestMetadataRequest(files=list(self.state.files.values()))
-                await self.svc._call_peers(peers, "IngestMetadata", req, lambda x: x.success)
-                log.info("merged shard %s into %s", self.svc.shard_id, neighbor)
+            await self._merge_into(neighbor)
+
+    async def _merge_into(self, neighbor: str) -> None:
+        """Hand this idle shard's range and files to ``neighbor`` (C31 merge). The config
+        server's MergeShard goes first because it arbitrates: two idle neighbours may try
+        to merge into each other and only one MergeShard can apply. The winner then pushes
+        its files (IngestMetadata, retried until the retained shard takes them), drops its
+        namespace in one Raft entry and re-registers as a standby master that a later split
+        can reuse. The reference reports success to both and keeps serving stale copies."""
+        victim = self.svc.shard_id
+        r = await self._config_call("MergeShard", pb.MergeShardRequest(victim_shard_id=victim,
+                                                                       retained_shard_id=neighbor))
+        if r is None or not r.success:
+            return
+        peers = self.svc.shard_map.get_shard_peers(neighbor) or []
+        self.svc.shard_id = ""  # stop accepting our old range (requests now redirect)
+        paths = list(self.state.files)
+        for attempt in range(30):
+            req = pb.IngestMetadataRequest(files=[self.state.files[p] for p in paths if p in self.state.files])
+            if not req.files or await self.svc._call_peers(peers, "IngestMetadata", req, lambda x: x.success):
+                break
+            await asyncio.sleep(min(0.1 * (attempt + 1), 1.0))
+        else:
+            log.error("merge of %s into %s: ingest kept failing; files stay here", victim, neighbor)
+            return
+        await self._propose("SplitShard", {"split_key": "", "new_shard_id": neighbor, "new_shard_peers": [],
+                                           "paths": paths})
+        log.info("merged shard %s into %s; now standby", victim, neighbor)
+        self.registered = False
+        await self.refresh_shard_map()
+
+    async def _split(self, prefix: str, rps: float) -> None:
+        """Split this shard at ``prefix`` (C31). The files that move are exactly the ones the
+        post-split map routes to the new shard (reference ShardMap semantics: the new id takes
+        the keys below the split key), so routing and data agree — the reference deletes
+        ``p >= key`` while routing the other side there, and ships the batch after the
+        delete (master.rs:1600-1615). Order: config SplitShard (allocates standby masters),
+        IngestMetadata at the new shard, then one Raft entry dropping the moved files here."""
+        import time as _t
+
+        mon = self.svc.monitor
+        new_id = f"{self.svc.shard_id}-split-{uuid.uuid4().hex[:8]}"
+        after = self.svc.shard_map.copy()
+        if not after.split_shard(prefix, new_id, []):
+            mon.last_split_time = _t.monotonic()
+            return
+        log.info("hot prefix %s (%.1f rps): splitting shard %s -> %s", prefix, rps, self.svc.shard_id, new_id)
+        mon.last_split_time = _t.monotonic()
+        moving = [p for p in self.state.files if after.get_shard(p) == new_id]
+        r = await self._config_call("SplitShard", pb.SplitShardRequest(
+            shard_id=self.svc.shard_id, split_key=prefix, new_shard_id=new_id))
+        if r is None or not r.success:
+            log.warning("config server refused split of %s at %s", self.svc.shard_id, prefix)
+            return
+        if moving:
+            req = pb.IngestMetadataRequest(files=[self.state.files[p] for p in moving if p in self.state.files])
+            await self.svc._call_peers(list(r.new_shard_peers), "IngestMetadata", req, lambda x: x.success)
+        await self._propose("SplitShard", {"split_key": prefix, "new_shard_id": new_id,
+                                           "new_shard_peers": list(r.new_shard_peers), "paths": moving})
+        await self.refresh_shard_map()
 
     # ---------------------------------------------------------------- tiering (C32)
     async def tiering(self) -> None:
@@ -340,16 +390,59 @@ class MasterBackground:
                 await self._propose("MoveToCold", {"path": f.path, "moved_at_ms": now})
         if not self.ec_conversion:
             return
-        k, m = 6, 3
+        await self._ec_convert(now)
+
+    async def _ec_convert(self, now: int) -> None:
+        """Cold files older than EC_THRESHOLD_SECS become RS(k,m): each block is re-encoded
+        by a chunkserver holding a replica (ENCODE_EC, GPU RS kernel) into shards under a new
+        block id; once every block of the file reported success one Raft ConvertToEc swaps
+        the metadata and the old replicas get DELETE. Jobs are leader-local; a failed or
+        lost job is simply retried on a later pass."""
+        k, m = self.ec_k, self.ec_m
+        T = pb.ChunkServerCommand
+        jobs = self.svc.ec_jobs
+        for bid, job in list(jobs.items()):
+            if not job["done"] and now - job["started_ms"] > EC_JOB_TIMEOUT_MS:
+                log.warning("EC job for %s timed out; will retry", bid)
+                jobs.pop(bid, None)
+        live = {a for a, s in self.state.chunk_servers.items() if s.available_space > 0}
         for f in list(self.state.files.values()):
-            if f.moved_to_cold_at_ms > 0 and f.ec_data_shards == 0 and now - f.moved_to_cold_at_ms > self.ec_threshold_ms:
-                servers = sorted(a for a, s in self.state.chunk_servers.items() if s.available_space > 0)[: k + m]
-                if len(servers) < k + m:
-                    continue
+            if not (f.moved_to_cold_at_ms > 0 and f.ec_data_shards == 0 and f.blocks
+                    and now - f.moved_to_cold_at_ms > self.ec_threshold_ms):
+                continue
+            if all(b.block_id in jobs and jobs[b.block_id]["done"] for b in f.blocks):
                 new_blocks = []
                 for b in f.blocks:
+                    job = jobs[b.block_id]
                     d = M.block_to_dict(b)
-                    d.update(locations=servers, ec_data_shards=k, ec_parity_shards=m)
+                    d.update(block_id=job["new_id"], locations=job["targets"], ec_data_shards=job["k"],
+                             ec_parity_shards=job["m"], original_size=b.original_size or b.size)
                     new_blocks.append(d)
-                await self._propose("ConvertToEc", {"path": f.path, "ec_data_shards": k, "ec_parity_shards": m,
-                                                    "new_blocks": new_blocks})
+                old = [(b.block_id, list(b.locations)) for b in f.blocks]
+                jk, jm = jobs[f.blocks[0].block_id]["k"], jobs[f.blocks[0].block_id]["m"]
+                ok = await self._propose("ConvertToEc", {"path": f.path, "ec_data_shards": jk,
+                                                         "ec_parity_shards": jm, "new_blocks": new_blocks})
+                for bid, locs in old:
+                    jobs.pop(bid, None)
+                    if ok:
+                        for loc in locs:
+                            self.state.pending_commands.setdefault(loc, []).append(T(type=T.DELETE, block_id=bid))
+                if ok:
+                    log.info("converted %s to RS(%d,%d)", f.path, jk, jm)
+                continue
+            servers = sorted(live)[: k + m]
+            if len(servers) < k + m:
+                continue
+            for b in f.blocks:
+                if b.block_id in jobs:
+                    continue
+                src = next((loc for loc in b.locations if loc in live), None)
+                if src is None:
+                    continue
+                new_id = f"{b.block_id}-rs{k}.{m}"
+                jobs[b.block_id] = {"path": f.path, "new_id": new_id, "targets": servers, "k": k, "m": m,
+                                    "started_ms": now, "done": False}
+                self.state.pending_commands.setdefault(src, []).append(
+                    T(type=T.ENCODE_EC, block_id=b.block_id, new_block_id=new_id, ec_data_shards=k,
+                      ec_parity_shards=m, ec_shard_sources=servers, original_block_size=b.size,
+                      master_term=self.raft.current_term))

@@ -39,6 +39,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--advertise-addr", default=None)
     p.add_argument("--storage-dir", default="/tmp/raft-logs")
     p.add_argument("--shard-id", default="shard-0")
+    p.add_argument("--standby", action="store_true",
+                   help="start without a shard: registered with the config server until a split allocates one")
     p.add_argument("--shard-config", default=None)
     p.add_argument("--config-servers", default="")
     p.add_argument("--split-threshold-rps", type=float, default=100.0)
@@ -85,7 +87,8 @@ class MasterProcess:
             self.shard_map = ShardMap.load_config_file(args.shard_config)
         self.monitor = ThroughputMonitor(args.split_threshold_rps, args.merge_threshold_rps, args.split_cooldown_secs)
         self.pool = AioChannelPool(args.ca_cert, args.domain_name)
-        self.svc = MasterService(self.state, self.raft, self.shard_map, args.shard_id, self.monitor, self.pool,
+        self.svc = MasterService(self.state, self.raft, self.shard_map, "" if args.standby else args.shard_id,
+                                 self.monitor, self.pool,
                                  advertise_addr=self.client_addr)
         iv = Intervals()
         if args.fast_intervals:

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import asyncio
 import logging
+import os
 import time
 import uuid
 
@@ -66,6 +67,9 @@ class MasterService:
         self.shard_map_refresher = None
         self.shard_map_fetched_ms = 0
         self.shard_map_max_age_ms = 1000
+        # leader-local EC conversion jobs (tiering, C32): source block id ->
+        # {"path", "new_id", "targets", "k", "m", "started_ms", "done"}
+        self.ec_jobs: dict[str, dict] = {}
 
     async def fresh_shard_map(self, force: bool = False) -> None:
         if self.shard_map_refresher is None:
@@ -319,6 +323,18 @@ class MasterService:
             hbm_capacity=req.hbm_capacity, hbm_used=req.hbm_used)
         for bid in req.new_blocks:  # ext: replicas created by REPLICATE / reconstruction
             self.raft.propose_nowait({"Master": {"AddBlockLocation": {"block_id": bid, "address": addr}}})
+        for ent in req.ec_rebuilt:  # ext: EC shard rebuilt here -> location at its shard index
+            bid, _, idx = ent.rpartition("/")
+            if bid and idx.isdigit():
+                self.raft.propose_nowait({"Master": {"AddBlockLocation": {"block_id": bid, "address": addr,
+                                                                          "shard_index": int(idx)}}})
+        for bid in req.ec_encoded:
+            job = self.ec_jobs.get(bid)
+            if job is not None:
+                job["done"] = True
+        for bid in req.ec_failed:
+            if self.ec_jobs.pop(bid, None) is not None:
+                log.warning("EC conversion of block %s failed at %s; will retry", bid, addr)
         if st.safe_mode and is_new:
             st.update_reported_blocks(req.chunk_count)
         if st.safe_mode and st.should_exit_safe_mode():
@@ -386,6 +402,11 @@ class MasterService:
             except Exception:  # noqa: BLE001
                 pass
             return pb.RenameResponse(success=False, error_message="Cross-shard prepare failed")
+        if os.environ.get("DFS_DEBUG_2PC_DROP_COMMIT") == "1":
+            # fault injection (tests): behave as if the coordinator died right after the
+            # participant prepared; tx_recovery must finish the rename
+            log.warning("tx %s: debug hook dropped the commit RPC", tx_id)
+            return pb.RenameResponse(success=False, error_message="Cross-shard commit pending, will be retried")
         if not await self.send_commit(tx_id, dst_peers):
             log.warning("commit RPC failed for tx %s; recovery task will retry", tx_id)
             return pb.RenameResponse(success=False, error_message="Cross-shard commit pending, will be retried")

@@ -33,7 +33,7 @@ log = logging.getLogger("dfs.master.state")
 REPLICATION_FACTOR = 3
 SAFE_MODE_THRESHOLD = 0.99
 SAFE_MODE_TIMEOUT_MS = 60_000
-TX_TIMEOUT_MS = 10_000
+TX_TIMEOUT_MS = int(os.environ.get("DFS_TX_TIMEOUT_MS", "10000"))  # reference: 10 s
 TX_STALE_MS = 3_600_000
 # a file left under construction this long (writer died) may be re-created by CreateFile
 CREATE_LEASE_MS = int(os.environ.get("DFS_CREATE_LEASE_MS", "60000"))
@@ -365,6 +365,11 @@ class MasterState:
             self._relock(rec)
 
     def _cmd_SplitShard(self, a):
+        if "paths" in a:  # explicit list: the files the post-split map routes away
+            for p in a["paths"]:
+                if p in self.files:
+                    self._del(p)
+            return
         key = a["split_key"]
         for p in [p for p in self.files if p >= key]:
             self._del(p)
@@ -455,7 +460,16 @@ class MasterState:
 
     def _cmd_AddBlockLocation(self, a):
         _, b = self.find_block(a["block_id"])
-        if b is not None and a["address"] not in b.locations:
+        if b is None:
+            return
+        idx = a.get("shard_index")
+        if idx is not None and b.ec_data_shards > 0:
+            # EC locations are positional (shard i lives at locations[i]): a rebuilt shard
+            # replaces its dead holder instead of being appended
+            if 0 <= idx < len(b.locations):
+                b.locations[idx] = a["address"]
+            return
+        if a["address"] not in b.locations:
             b.locations.append(a["address"])
 
     def _cmd_UpdateBlockLocations(self, a):

@@ -219,6 +219,12 @@ class ShardMap:
         the same because split keys are not transported, config_server.rs:43-61)."""
         return cls.from_config({k: list(v) for k, v in shards.items()})
 
+    @classmethod
+    def from_fetch(cls, resp) -> "ShardMap":
+        """FetchShardMapResponse -> map. With the ``ranges`` extension the boundaries are
+        exact (dynamic split keys included); without it, the reference's id-sorted rebuild."""
+        return cls.from_config({k: list(v.peers) for k, v in resp.shards.items()}, dict(resp.ranges) or None)
+
     def copy(self) -> "ShardMap":
         return ShardMap.from_json(json.loads(json.dumps(self.to_json())))
 

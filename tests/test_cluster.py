@@ -274,3 +274,220 @@ def test_tls_cluster():
             plain.call(cl.master_addrs[0].replace("https://", "http://"), "MasterService", "GetSafeModeStatus",
                        pb.GetSafeModeStatusRequest(), timeout=3)
         plain.close()
+
+
+def test_tiering_moves_cold_and_converts_to_ec():
+    """C32 end to end: a file not accessed for COLD_THRESHOLD_SECS moves to the cold tier;
+    after EC_THRESHOLD_SECS a chunkserver re-encodes each block as RS(2,1) shards under a
+    new id, the master swaps the metadata and deletes the old replicas, reads still work
+    (also with one shard server gone)."""
+    env = {"COLD_THRESHOLD_SECS": "1", "EC_THRESHOLD_SECS": "1", "EC_CONVERSION_ENABLED": "1",
+           "EC_CONVERSION_DATA_SHARDS": "2", "EC_CONVERSION_PARITY_SHARDS": "1"}
+    with LocalCluster(n_chunkservers=3, fsync=False, fast_intervals=True, cold_dir=True, env=env) as cl:
+        c = cl.client()
+        data = os.urandom(400_001)
+        c.create_file_from_buffer(data, "/tier/f")
+        old = c.get_file_info("/tier/f").blocks[0]
+        assert old.ec_data_shards == 0 and len(old.locations) == 3
+        assert c.get_file_content("/tier/f") == data  # sets last_access_ms
+        # GetFileInfo counts as an access (reference master.rs:2201), so wait on the
+        # chunkservers until the RS shards exist, then on the metadata swap
+        new_id = f"{old.block_id}-rs2.1"
+        deadline = time.time() + 40
+        while time.time() < deadline:
+            have = 0
+            for loc in old.locations:
+                try:
+                    c.read_block_from_location(loc, new_id, 0, 1)
+                    have += 1
+                except grpc.RpcError:
+                    pass
+            if have == 3:
+                break
+            time.sleep(0.5)
+        info = None
+        while time.time() < deadline:
+            info = c.get_file_info("/tier/f")
+            if info.blocks[0].ec_data_shards:
+                break
+            time.sleep(0.5)
+        b = info.blocks[0]
+        assert (b.ec_data_shards, b.ec_parity_shards) == (2, 1) and b.block_id != old.block_id
+        assert info.moved_to_cold_at_ms > 0 and len(b.locations) == 3
+        assert c.get_file_content("/tier/f") == data
+        assert c.read_file_range("/tier/f", 300_000, 5000) == data[300_000:305_000]
+        # old replicas are deleted once the heartbeat delivers DELETE
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            left = 0
+            for loc in old.locations:
+                try:
+                    c.read_block_from_location(loc, old.block_id)
+                    left += 1
+                except grpc.RpcError:
+                    pass
+            if left == 0:
+                break
+            time.sleep(0.3)
+        assert left == 0
+        cl.kill(f"cs{cs_index(cl, b.locations[0])}")
+        assert c.get_file_content("/tier/f") == data  # degraded decode
+        c.close()
+
+
+def test_healer_rereplicates_and_rebuilds_ec_shards():
+    """C29: a chunkserver that stops heartbeating is dropped after DFS_CS_DEAD_MS; the
+    healer REPLICATEs its replicated blocks to a spare server and RECONSTRUCTs its EC
+    shard there, the rebuilt shard taking the dead server's position in the location list."""
+    env = {"DFS_CS_DEAD_MS": "2000"}
+    with LocalCluster(n_chunkservers=4, fsync=False, fast_intervals=True, env=env) as cl:
+        c = cl.client()
+        rep, ec = os.urandom(300_000), os.urandom(500_003)
+        c.create_file_from_buffer(rep, "/heal/rep")
+        c.create_file_from_buffer_ec(ec, "/heal/ec", 2, 1)
+        rb, eb = c.get_file_info("/heal/rep").blocks[0], c.get_file_info("/heal/ec").blocks[0]
+        common = [loc for loc in rb.locations if loc in eb.locations]
+        assert common, "with 4 servers a 3-replica block and a 3-shard block share a server"
+        dead = common[0]
+        shard_idx = list(eb.locations).index(dead)
+        cl.kill(f"cs{cs_index(cl, dead)}")
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            rb2, eb2 = c.get_file_info("/heal/rep").blocks[0], c.get_file_info("/heal/ec").blocks[0]
+            live_rep = [loc for loc in rb2.locations if loc != dead]
+            if len(live_rep) >= 3 and dead not in eb2.locations:
+                break
+            time.sleep(0.5)
+        assert len(live_rep) >= 3
+        assert dead not in eb2.locations and len(eb2.locations) == 3
+        spare = eb2.locations[shard_idx]
+        assert spare not in eb.locations
+        assert c.read_block_from_location(spare, eb.block_id) is not None
+        assert c.get_file_content("/heal/rep") == rep
+        assert c.get_file_content("/heal/ec") == ec
+        c.close()
+
+
+def test_dynamic_split_hands_range_to_standby_master():
+    """C31/C36: a prefix above --split-threshold-rps splits the shard. The config server
+    allocates a standby master, the split key travels in FetchShardMap (ranges extension),
+    the moved files are ingested by the new shard and dropped by the old one, and clients
+    follow the new map for reads and writes."""
+    margs = ["--split-threshold-rps", "15", "--split-cooldown-secs", "3600", "--merge-threshold-rps", "-1"]
+    with LocalCluster(n_chunkservers=2, config_server=True, standby_masters=1, fast_intervals=True,
+                      master_args=margs) as cl:
+        c = cl.client()
+        files = {p: os.urandom(1000 + i) for i, p in enumerate(["/a/f1", "/b/f2", "/hot/x", "/zz/y"])}
+        for p, d in files.items():
+            c.create_file_from_buffer(d, p)
+        old_master = cl.master_addrs[0]
+        deadline = time.time() + 40
+        while time.time() < deadline:
+            for _ in range(30):
+                c.get_file_info("/hot/x")
+            c.refresh_shard_map()
+            if len(c.shard_map.get_all_shards()) == 2:
+                break
+            time.sleep(0.05)
+        shards = c.shard_map.get_all_shards()
+        assert len(shards) == 2, shards
+        new_sid = next(s for s in shards if "-split-" in s)
+        assert c.shard_map.get_shard_peers(new_sid) == cl.standby_addrs
+        assert c.shard_map.get_shard("/a/f1") == new_sid and c.shard_map.get_shard("/hot/x") == "shard-0"
+        http = cl.master_http[cl.standby_addrs[0]]
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            if json.load(urllib.request.urlopen(f"{http}/shard_map"))["shard_id"] == new_sid:
+                break
+            time.sleep(0.2)
+        for p, d in files.items():
+            assert c.get_file_content(p) == d
+        c.create_file_from_buffer(b"after split", "/a/new")
+        assert c.get_file_content("/a/new") == b"after split"
+        assert c.shard_map.get_shard("/a/new") == new_sid
+        # the old shard no longer holds the moved files
+        pool = ChannelPool()
+        with pytest.raises(grpc.RpcError) as ei:
+            pool.call(old_master, "MasterService", "GetFileInfo", pb.GetFileInfoRequest(path="/a/f1"))
+        assert "REDIRECT" in (ei.value.details() or "")
+        assert pool.call(old_master, "MasterService", "GetFileInfo", pb.GetFileInfoRequest(path="/hot/x")).found
+        old_files = set(pool.call(old_master, "MasterService", "ListFiles", pb.ListFilesRequest()).files)
+        new_files = set(pool.call(cl.standby_addrs[0], "MasterService", "ListFiles", pb.ListFilesRequest()).files)
+        assert old_files == {"/hot/x", "/zz/y"} and new_files == {"/a/f1", "/b/f2", "/a/new"}
+        pool.close()
+        assert set(files) | {"/a/new"} <= set(c.list_all_files())
+        c.close()
+
+
+# fast background intervals + the reference's default merge threshold (1 rps) would merge
+# an idle shard into its neighbour within a second
+NO_MERGE = ["--merge-threshold-rps", "-1"]
+
+
+def test_2pc_abort_when_destination_shard_is_down():
+    """C27 presumed abort (reference transaction_abort_test.sh): the destination shard's
+    master is gone, PrepareTransaction fails, the coordinator aborts; the source file stays
+    readable and unlocked."""
+    with LocalCluster(n_chunkservers=2, shards=2, fsync=False, fast_intervals=True, master_args=NO_MERGE) as cl:
+        c = cl.client(max_retries=2, initial_backoff_ms=20)
+        c.create_file_from_buffer(b"stay", "/a/src")
+        assert c.shard_map.get_shard("/a/src") != c.shard_map.get_shard("/z/dst")
+        cl.kill(f"master_{c.shard_map.get_shard('/z/dst')}_1")
+        with pytest.raises(DfsError):
+            c.rename_file("/a/src", "/z/dst")
+        assert c.get_file_content("/a/src") == b"stay"
+        c.rename_file("/a/src", "/a/src2")  # not pinned by a leftover transaction lock
+        assert c.get_file_content("/a/src2") == b"stay"
+        c.close()
+
+
+def test_2pc_recovery_finishes_commit_after_coordinator_loss():
+    """C27 recovery (reference transaction_recovery_test.sh): the coordinator's commit RPC
+    is lost after the participant prepared; the coordinator's tx_recovery task re-sends
+    the commit, applies the source delete, and the rename becomes visible."""
+    env = {"DFS_DEBUG_2PC_DROP_COMMIT": "1", "DFS_TX_TIMEOUT_MS": "1500"}
+    with LocalCluster(n_chunkservers=2, shards=2, fsync=False, fast_intervals=True, env=env,
+                      master_args=NO_MERGE) as cl:
+        c = cl.client()
+        c.create_file_from_buffer(b"moving", "/a/tx")
+        with pytest.raises(DfsError, match="pending"):
+            c.rename_file("/a/tx", "/z/tx")
+        deadline = time.time() + 20
+        while time.time() < deadline:
+            if c.exists("/z/tx") and not c.exists("/a/tx"):
+                break
+            time.sleep(0.3)
+        assert c.get_file_content("/z/tx") == b"moving"
+        assert not c.exists("/a/tx")
+        c.close()
+
+
+def test_idle_shard_merges_and_becomes_standby():
+    """C31 merge: with total rps below --merge-threshold-rps an idle shard pushes its files
+    to its neighbour, the config server drops its range, and the master re-registers as a
+    standby (no shard) that a later split can reuse. Every file stays readable."""
+    with LocalCluster(n_chunkservers=2, shards=2, fsync=False, fast_intervals=True,
+                      master_args=["--merge-threshold-rps", "1000", "--split-threshold-rps", "1e9"]) as cl:
+        c = cl.client()
+        files = {p: os.urandom(500 + i) for i, p in enumerate(["/a/m1", "/b/m2", "/x/m3", "/z/m4"])}
+        for p, d in files.items():
+            c.create_file_from_buffer(d, p)
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            c.refresh_shard_map()
+            if len(c.shard_map.get_all_shards()) == 1:
+                break
+            time.sleep(0.3)
+        (survivor,) = c.shard_map.get_all_shards()
+        time.sleep(1.5)  # the victim's final Raft entry + re-registration
+        for p, d in files.items():
+            assert c.get_file_content(p) == d
+        pool = ChannelPool()
+        (owner,) = c.shard_map.get_shard_peers(survivor)
+        assert set(pool.call(owner, "MasterService", "ListFiles", pb.ListFilesRequest()).files) == set(files)
+        victim = next(m for m in cl.master_addrs if m != owner)
+        assert list(pool.call(victim, "MasterService", "ListFiles", pb.ListFilesRequest()).files) == []
+        http = cl.master_http[victim]
+        assert json.load(urllib.request.urlopen(f"{http}/shard_map"))["shard_id"] == ""
+        pool.close()
+        c.close()
