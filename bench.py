@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--workdir", default=None)
     p.add_argument("--timeout", type=float, default=1500.0)
     p.add_argument("--keep", action="store_true")
+    p.add_argument("--rehearse-rccl", action="store_true",
+                   help="bring RCCL up even when ranks share a GPU (it must fail cleanly and every "
+                        "rank must fall back together) - a 1-GPU rehearsal of the failure path")
     p.add_argument("--profile-dir", default=None,
                    help="run each ChunkServer under rocprofv3 --kernel-trace --stats, output here")
     return p.parse_args()
@@ -232,8 +235,8 @@ def main():
         args = [f"{PKG}.chunkserver.server", "--addr", f"127.0.0.1:{cport}",
                 "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
                 "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
-                "--heartbeat-interval", "0.5", "--scrub-interval", "3600"]
-        if n > 1 and not a.cpu and a.transport == "rccl" and not shared_gpu:
+                "--heartbeat-interval", "0.5", "--scrub-interval", "3600", "--rccl-timeout-ms", "90000"]
+        if n > 1 and not a.cpu and a.transport == "rccl" and (not shared_gpu or a.rehearse_rccl):
             args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
                      str(base_p / "rccl_rdv")]
         else:

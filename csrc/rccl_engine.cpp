@@ -8,6 +8,7 @@
 #include <cstring>
 #include <fstream>
 #include <thread>
+#include <algorithm>
 
 namespace dfs {
 
@@ -63,11 +64,80 @@ RcclEngine::~RcclEngine() {
   }
 }
 
+// Poll a nonblocking communicator until its pending operation (init or a lazily
+// connected first send/recv) finishes. Returns false on error or deadline.
+static bool settle(ncclComm_t comm, ncclResult_t r, Clock::time_point deadline, std::string* err,
+                   const char* what) {
+  while (r == ncclInProgress) {
+    if (Clock::now() > deadline) {
+      *err = std::string(what) + ": timed out";
+      return false;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) break;
+  }
+  if (r != ncclSuccess) {
+    *err = std::string(what) + ": " + ncclGetErrorString(r);
+    return false;
+  }
+  return true;
+}
+
 bool RcclEngine::init(std::string* err) {
   if (world_ <= 1) {
     ready_ = true;
     return true;
   }
+  bool ok = init_pairs(err);
+  // Every rank publishes its verdict and waits for everyone else's: RCCL is used only if
+  // ALL ranks brought up ALL their pairs. A partially working mesh would leave a sender
+  // blocked on a receiver that has no communicator, so it is all or nothing.
+  std::string mine = dir_ + "/rccl_status_" + std::to_string(rank_);
+  {
+    std::string tmp = mine + ".tmp";
+    int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd >= 0) {
+      const char c = ok ? '1' : '0';
+      (void)!::write(fd, &c, 1);
+      ::close(fd);
+      (void)::rename(tmp.c_str(), mine.c_str());
+    }
+  }
+  auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms_);
+  bool all = ok;
+  for (int r = 0; r < world_ && all; ++r) {
+    std::string path = dir_ + "/rccl_status_" + std::to_string(r);
+    char c = 0;
+    for (;;) {
+      int fd = ::open(path.c_str(), O_RDONLY);
+      if (fd >= 0) {
+        ssize_t n = ::read(fd, &c, 1);
+        ::close(fd);
+        if (n == 1) break;
+      }
+      if (Clock::now() > deadline) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+    if (c != '1') {
+      all = false;
+      if (ok) *err = "rank " + std::to_string(r) + (c == '0' ? " failed RCCL bring-up" : " never reported RCCL status");
+    }
+  }
+  if (!all) {
+    for (auto& kv : pairs_) {
+      if (kv.second->comm) ncclCommAbort(kv.second->comm);
+      kv.second->comm = nullptr;
+      if (kv.second->stream) (void)hipStreamDestroy(kv.second->stream);
+      kv.second->stream = nullptr;
+    }
+    pairs_.clear();
+    return false;
+  }
+  ready_ = true;
+  return true;
+}
+
+bool RcclEngine::init_pairs(std::string* err) {
   if (!store_->gpu()) {
     *err = "RCCL replication requires a GPU chunk store";
     return false;
@@ -76,38 +146,82 @@ bool RcclEngine::init(std::string* err) {
     *err = "hipSetDevice failed";
     return false;
   }
-  for (int a = 0; a < world_; ++a)
-    for (int b = 0; b < world_; ++b) {
-      if (a == b || (a != rank_ && b != rank_)) continue;
-      auto p = std::make_unique<Pair>();
-      ncclUniqueId uid;
-      std::string path = uid_path(dir_, a, b);
-      if (a == rank_) {
-        if (ncclGetUniqueId(&uid) != ncclSuccess || !write_uid(path, uid)) {
-          *err = "failed to publish RCCL unique id " + path;
-          return false;
-        }
-      } else if (!read_uid(path, &uid, timeout_ms_)) {
+  auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms_);
+  // Pairs are brought up in rounds of a round-robin tournament (circle method): in round
+  // r every rank meets exactly one partner and the two ordered pairs (lo->hi, hi->lo) are
+  // initialised back to back. Every rank walks the same schedule, pairs inside a round are
+  // disjoint, so there is no wait cycle, and the critical path is world-1 rounds instead
+  // of the world*(world-1) serial steps of a lexicographic order.
+  std::vector<std::pair<int, int>> order;
+  const int m = world_ % 2 ? world_ + 1 : world_;  // odd world: rank m-1 is a bye
+  for (int r = 0; r < m - 1; ++r) {
+    int partner = -1;
+    for (int x = 0; x < m - 1; ++x) {
+      int y = ((2 * r - x) % (m - 1) + (m - 1)) % (m - 1);
+      if (y == x) y = m - 1;
+      if (x == rank_) partner = y;
+      if (y == rank_) partner = x;
+    }
+    if (partner < 0 || partner >= world_ || partner == rank_) continue;
+    int lo = std::min(rank_, partner), hi = std::max(rank_, partner);
+    order.emplace_back(lo, hi);
+    order.emplace_back(hi, lo);
+  }
+  for (auto [a, b] : order) {
+    auto p = std::make_unique<Pair>();
+    ncclUniqueId uid;
+    std::string path = uid_path(dir_, a, b);
+    if (a == rank_) {
+      if (ncclGetUniqueId(&uid) != ncclSuccess || !write_uid(path, uid)) {
+        *err = "failed to publish RCCL unique id " + path;
+        return false;
+      }
+    } else {
+      int left = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count());
+      if (left <= 0 || !read_uid(path, &uid, left)) {
         *err = "timed out waiting for RCCL unique id " + path;
         return false;
       }
-      if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
-        *err = "hipStreamCreate failed";
-        return false;
-      }
-      ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-      cfg.blocking = 1;
-      cfg.minCTAs = 1;
-      cfg.maxCTAs = 4;
-      ncclResult_t r = ncclCommInitRankConfig(&p->comm, 2, uid, a == rank_ ? 0 : 1, &cfg);
-      if (r != ncclSuccess) {
-        *err = std::string("ncclCommInitRank(") + std::to_string(a) + "->" + std::to_string(b) +
-               "): " + ncclGetErrorString(r);
-        return false;
-      }
-      pairs_[{a, b}] = std::move(p);
     }
-  ready_ = true;
+    if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+      *err = "hipStreamCreate failed";
+      return false;
+    }
+    // Nonblocking communicator: a peer that never shows up costs a deadline, not a hang.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    cfg.minCTAs = 1;
+    cfg.maxCTAs = 4;
+    ncclResult_t r = ncclCommInitRankConfig(&p->comm, 2, uid, a == rank_ ? 0 : 1, &cfg);
+    std::string what = "ncclCommInitRank(" + std::to_string(a) + "->" + std::to_string(b) + ")";
+    bool good = p->comm != nullptr && settle(p->comm, r, deadline, err, what.c_str());
+    if (!good && p->comm == nullptr && r != ncclInProgress && r != ncclSuccess)
+      *err = what + ": " + ncclGetErrorString(r);
+    if (good) {
+      // Warm-up: one tiny transfer per pair connects the p2p channel (RCCL connects
+      // lazily) and proves the path end to end before any block depends on it.
+      int32_t* probe = nullptr;
+      good = hipMalloc(reinterpret_cast<void**>(&probe), sizeof(int32_t)) == hipSuccess;
+      if (good) {
+        r = a == rank_ ? ncclSend(probe, 1, ncclInt32, 1, p->comm, p->stream)
+                       : ncclRecv(probe, 1, ncclInt32, 0, p->comm, p->stream);
+        good = settle(p->comm, r, deadline, err, (what + " warm-up").c_str());
+        while (good) {
+          hipError_t q = hipStreamQuery(p->stream);
+          if (q == hipSuccess) break;
+          if (q != hipErrorNotReady || Clock::now() > deadline) {
+            *err = what + " warm-up transfer did not complete";
+            good = false;
+            break;
+          }
+          std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        (void)hipFree(probe);
+      }
+    }
+    pairs_[{a, b}] = std::move(p);
+    if (!good) return false;
+  }
   return true;
 }
 
@@ -168,8 +282,7 @@ int64_t RcclEngine::send(int peer, const std::string& id, uint64_t* size, std::s
   (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
   if (*size) {
     ncclResult_t r = ncclSend(d, *size, ncclUint8, 1, p->comm, p->stream);
-    if (r != ncclSuccess) {
-      *err = std::string("ncclSend: ") + ncclGetErrorString(r);
+    if (!settle(p->comm, r, Clock::now() + std::chrono::milliseconds(timeout_ms_), err, "ncclSend")) {
       (void)hipEventDestroy(ev);
       store_->unpin(id);
       return -1;
@@ -236,11 +349,12 @@ WriteResult RcclEngine::recv(int src, int64_t seq, const std::string& id, uint64
     }
     if (size) {
       ncclResult_t r = ncclRecv(ext.ptr, size, ncclUint8, 0, p->comm, p->stream);
-      if (r != ncclSuccess) {
+      std::string rerr;
+      if (!settle(p->comm, r, Clock::now() + std::chrono::milliseconds(timeout_ms_), &rerr, "ncclRecv")) {
         lk.unlock();
         (void)hipEventDestroy(ev);
         store_->release(ext);
-        res.error = std::string("ncclRecv: ") + ncclGetErrorString(r);
+        res.error = rerr;
         abort_pair(src, rank_);
         return res;
       }

@@ -10,8 +10,11 @@
 // receiver posts ncclRecv in sequence order (the gRPC descriptor carries the seq).
 // Communicator bootstrap: unique ids through a shared rendezvous directory, pairs
 // initialised in a global lexicographic order (deadlock-free, like ordered locking).
-// Every wait is bounded; on timeout the pair is aborted and the caller falls back to the
-// gRPC ReplicateBlock data path.
+// Every wait is bounded: communicators are nonblocking (init and lazily connected p2p
+// channels are polled against a deadline), each pair is proven with a warm-up transfer,
+// and RCCL is enabled only if every rank brought up every pair (published through the
+// rendezvous directory) — otherwise all ranks fall back together. On a later timeout the
+// pair is aborted and the caller falls back to the shared-memory / gRPC data path.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -64,6 +67,7 @@ class RcclEngine {
     std::map<int64_t, Pending> pending;  // sender: in-flight sends
   };
   Pair* pair(int src, int dst);
+  bool init_pairs(std::string* err);
   bool wait_event(hipEvent_t ev, Pair* p);
 
   ChunkStore* store_;

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 STEP=${1:-all}
 rocm-smi --showproductname > gpurun_out/rocm_smi.txt 2>&1 || true
 if [ "$STEP" = "all" ] || [ "$STEP" = "test" ]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && \
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 && \
   timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || exit $?
 fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
@@ -37,5 +37,14 @@ if [ "$STEP" = "multi" ]; then
   # N=2 rehearsal on a single GPU: two ranks share the device, gRPC replication
   timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 > gpurun_out/bench_n2_shared.json 2> gpurun_out/bench_n2_shared.err || exit $?
+fi
+if [ "$STEP" = "rccl-fail" ]; then
+  # RCCL failure-path rehearsal: two ranks on one GPU cannot form a communicator
+  # (duplicate device); both must give up within the deadline and fall back together
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29535 bench.py --gpus 2 --steps 2 --warmup 1 --rehearse-rccl --keep --workdir /tmp/dfs_rccl_rehearsal \
+    > gpurun_out/bench_rccl_rehearsal.json 2> gpurun_out/bench_rccl_rehearsal.err; rc=$?
+  cp /tmp/dfs_rccl_rehearsal/cs*.log gpurun_out/ 2>/dev/null || true
+  [ $rc -eq 0 ] || exit $rc
 fi
 echo "gpu_round done"
