@@ -88,7 +88,7 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
 def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[Path]) -> list[Path]:
     """Native executables (csrc/bench/*.cpp) linked against the runtime objects, e.g. the
     io_bench microbenchmark. Written to build/native/ (ships to the GPU box)."""
-    runtime = [o for o in objs if not o.name.startswith("bindings.")]
+    runtime = [o for o in objs if not o.name.startswith("bindings")]
     outs = []
     for src in sorted((CSRC / "bench").glob("*.cpp")):
         obj = BUILD / ("bench_" + src.name + ".o")

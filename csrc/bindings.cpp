@@ -69,6 +69,8 @@ int device_count() {
 
 }  // namespace
 
+void bind_meta(py::module_& m);  // bindings_meta.cpp
+
 PYBIND11_MODULE(_dfs_native, m) {
   m.doc() = "MI355X-native data plane: HBM chunk store, CDNA4 CRC/RS kernels, RCCL replication, WAL";
 
@@ -466,4 +468,7 @@ PYBIND11_MODULE(_dfs_native, m) {
     return crypto::rsa_sha256_verify(n, e, msg, sig);
   });
   m.def("random_bytes", [](size_t n) { return py::bytes(crypto::random_bytes(n)); });
+
+  // ---------------- metadata plane (Raft)
+  bind_meta(m);
 }

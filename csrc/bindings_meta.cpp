@@ -1,0 +1,184 @@
+// pybind11 bindings of the native metadata plane (Raft node). The service layer drives a
+// node through a handful of non-blocking calls; completions come back through Python
+// callables invoked from native threads with the GIL acquired. Every binding that can
+// wait on a node mutex releases the GIL first, and no native thread ever waits for the
+// GIL while holding a node mutex.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "raft.h"
+
+namespace py = pybind11;
+using namespace dfs;
+
+namespace {
+
+// A Python object that may be dropped on any thread: the decref takes the GIL.
+struct PyRef {
+  py::object obj;
+  explicit PyRef(py::object o) : obj(std::move(o)) {}
+  ~PyRef() {
+    if (!Py_IsInitialized()) {
+      obj.release();  // interpreter gone: leak rather than touch it
+      return;
+    }
+    py::gil_scoped_acquire g;
+    obj = py::object();
+  }
+};
+
+// Host backed by a Python object with apply_batch / snapshot / restore / send / backup.
+class PyRaftHost : public raft::Host {
+ public:
+  explicit PyRaftHost(py::object host) : host_(std::make_shared<PyRef>(std::move(host))) {}
+
+  std::vector<std::string> apply(const std::vector<std::pair<uint64_t, std::string>>& cmds) override {
+    py::gil_scoped_acquire g;
+    try {
+      py::list l;
+      for (auto& c : cmds) l.append(py::make_tuple(c.first, py::str(c.second)));
+      return host_->obj.attr("apply_batch")(l).cast<std::vector<std::string>>();
+    } catch (py::error_already_set& e) {
+      throw std::runtime_error(e.what());
+    }
+  }
+  std::string snapshot() override {
+    py::gil_scoped_acquire g;
+    try {
+      return host_->obj.attr("snapshot")().cast<std::string>();
+    } catch (py::error_already_set& e) {
+      throw std::runtime_error(e.what());
+    }
+  }
+  void restore(const std::string& state) override {
+    py::gil_scoped_acquire g;
+    try {
+      host_->obj.attr("restore")(py::str(state));
+    } catch (py::error_already_set& e) {
+      throw std::runtime_error(e.what());
+    }
+  }
+  bool send(const std::string& addr, const std::string& kind, const std::string& body, std::string* reply) override {
+    py::gil_scoped_acquire g;
+    try {
+      py::object r = host_->obj.attr("send")(addr, kind, py::str(body));
+      if (r.is_none()) return false;
+      *reply = r.cast<std::string>();
+      return true;
+    } catch (py::error_already_set& e) {
+      return false;
+    }
+  }
+  void backup(const std::string& url, const std::string& data) override {
+    py::gil_scoped_acquire g;
+    try {
+      host_->obj.attr("backup")(url, py::bytes(data));
+    } catch (py::error_already_set& e) {
+    }
+  }
+
+ private:
+  std::shared_ptr<PyRef> host_;
+};
+
+// Read a node property with the GIL released (the getter may wait on the node mutex).
+template <class F>
+auto unlocked(F f) -> decltype(f()) {
+  py::gil_scoped_release r;
+  return f();
+}
+
+raft::Done py_done(py::object cb) {
+  auto ref = std::make_shared<PyRef>(std::move(cb));
+  return [ref](int code, const std::string& payload) {
+    py::gil_scoped_acquire g;
+    try {
+      ref->obj(code, py::str(payload));
+    } catch (py::error_already_set& e) {
+      e.discard_as_unraisable("raft completion callback");
+    }
+  };
+}
+
+// Destroying a node joins its threads, which may need the GIL: never hold it meanwhile.
+struct NodeDeleter {
+  void operator()(raft::Node* n) const {
+    py::gil_scoped_release r;
+    delete n;
+  }
+};
+
+}  // namespace
+
+void bind_meta(py::module_& m) {
+  py::class_<raft::Node, std::unique_ptr<raft::Node, NodeDeleter>>(m, "RaftNode")
+      .def(py::init([](int id, std::map<int, std::string> members, std::string client_address, std::string dir,
+                       py::object host, double elo, double ehi, double hb, bool sync, uint64_t snapshot_threshold,
+                       int max_batch, std::string backup_endpoint, std::string backup_bucket) {
+             raft::Options o;
+             o.id = id;
+             o.members = std::move(members);
+             o.client_address = std::move(client_address);
+             o.dir = std::move(dir);
+             o.election_lo = elo;
+             o.election_hi = ehi;
+             o.heartbeat = hb;
+             o.sync = sync;
+             o.snapshot_threshold = snapshot_threshold;
+             o.max_append_batch = max_batch;
+             o.backup_endpoint = std::move(backup_endpoint);
+             o.backup_bucket = std::move(backup_bucket);
+             auto h = std::make_shared<PyRaftHost>(std::move(host));
+             return std::unique_ptr<raft::Node, NodeDeleter>(new raft::Node(std::move(o), h));
+           }),
+           py::arg("id"), py::arg("members"), py::arg("client_address"), py::arg("dir"), py::arg("host"),
+           py::arg("election_lo") = 1.5, py::arg("election_hi") = 3.0, py::arg("heartbeat") = 0.1,
+           py::arg("sync") = true, py::arg("snapshot_threshold") = 10000, py::arg("max_append_batch") = 512,
+           py::arg("backup_endpoint") = "", py::arg("backup_bucket") = "dfs-backups")
+      .def("start", &raft::Node::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &raft::Node::stop, py::call_guard<py::gil_scoped_release>())
+      .def("propose", [](raft::Node& n, std::string cmd, py::object cb) {
+        raft::Done d = py_done(std::move(cb));
+        py::gil_scoped_release r;
+        n.propose(cmd, std::move(d));
+      })
+      .def("propose_nowait", &raft::Node::propose_nowait, py::call_guard<py::gil_scoped_release>())
+      .def("read_index", [](raft::Node& n, py::object cb) {
+        raft::Done d = py_done(std::move(cb));
+        py::gil_scoped_release r;
+        n.read_index(std::move(d));
+      })
+      .def("handle", &raft::Node::handle, py::call_guard<py::gil_scoped_release>())
+      .def("transfer_leadership", &raft::Node::transfer_leadership, py::call_guard<py::gil_scoped_release>())
+      .def("snapshot_now", &raft::Node::snapshot_now, py::call_guard<py::gil_scoped_release>())
+      .def("add_non_voter", &raft::Node::add_non_voter, py::call_guard<py::gil_scoped_release>())
+      .def("drop_non_voter", &raft::Node::drop_non_voter, py::call_guard<py::gil_scoped_release>())
+      .def("caught_up", &raft::Node::caught_up, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("role", [](raft::Node& n) {
+        raft::Role r;
+        {
+          py::gil_scoped_release g;
+          r = n.role();
+        }
+        return std::string(raft::role_name(r));
+      })
+      .def_property_readonly("term", [](raft::Node& n) { return unlocked([&] { return n.term(); }); })
+      .def_property_readonly("leader_id", [](raft::Node& n) { return unlocked([&] { return n.leader_id(); }); })
+      .def_property_readonly("leader_address", [](raft::Node& n) { return unlocked([&] { return n.leader_address(); }); })
+      .def_property_readonly("commit_index", [](raft::Node& n) { return unlocked([&] { return n.commit_index(); }); })
+      .def_property_readonly("last_applied", [](raft::Node& n) { return unlocked([&] { return n.last_applied(); }); })
+      .def_property_readonly("last_index", [](raft::Node& n) { return unlocked([&] { return n.last_index(); }); })
+      .def_property_readonly("last_included_index", [](raft::Node& n) { return unlocked([&] { return n.last_included_index(); }); })
+      .def_property_readonly("votes", [](raft::Node& n) { return unlocked([&] { return n.votes(); }); })
+      .def_property_readonly("config_json", [](raft::Node& n) {
+        std::string s;
+        {
+          py::gil_scoped_release g;
+          s = n.config().to_json().dump();
+        }
+        return s;
+      })
+      .def("info_json", &raft::Node::info_json, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("wal_syncs", &raft::Node::wal_syncs)
+      .def_property_readonly("wal_bytes", &raft::Node::wal_bytes);
+}

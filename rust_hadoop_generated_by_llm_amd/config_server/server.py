@@ -209,7 +209,8 @@ async def run(args) -> None:
     def raft_route(kind):
         async def h(req):
             try:
-                return web.json_response(await raft.handle(kind, await req.json()))
+                return web.Response(text=await raft.handle_raw(kind, await req.text()),
+                                    content_type="application/json")
             except Exception:  # noqa: BLE001
                 return web.Response(status=500, text="Internal server error")
 

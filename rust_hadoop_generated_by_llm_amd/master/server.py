@@ -105,7 +105,7 @@ class MasterProcess:
         self.metrics.gauge("raft_commit_index", "commit index", fn=lambda: r.commit_index)
         self.metrics.gauge("raft_last_applied", "last applied", fn=lambda: r.last_applied)
         self.metrics.gauge("raft_log_len", "log length", fn=lambda: r.last_index())
-        self.metrics.gauge("raft_votes_received", "votes", fn=lambda: len(r.votes))
+        self.metrics.gauge("raft_votes_received", "votes", fn=lambda: r.votes_received)
         self.metrics.gauge("raft_wal_fsyncs", "WAL group-commit fsyncs", fn=lambda: r.wal.syncs)
         self.metrics.gauge("dfs_master_safe_mode_status", "1 if in safe mode", fn=lambda: int(self.state.safe_mode))
         self.metrics.gauge("dfs_master_files", "files in this shard", fn=lambda: len(self.state.files))
@@ -126,8 +126,8 @@ class MasterProcess:
         def raft_route(kind):
             async def h(req):
                 try:
-                    body = await req.json()
-                    return web.json_response(await self.raft.handle(kind, body))
+                    return web.Response(text=await self.raft.handle_raw(kind, await req.text()),
+                                        content_type="application/json")
                 except Exception:  # noqa: BLE001
                     return web.Response(status=500, text="Internal server error")
 

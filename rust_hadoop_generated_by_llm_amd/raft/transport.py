@@ -57,6 +57,27 @@ class HttpTransport:
                     await asyncio.sleep(backoff * (2 ** attempt))
         raise TransportError(str(last))
 
+    async def send_raw(self, addr: str, kind: str, body: str) -> str:
+        """Same as :meth:`send` with the JSON body already encoded (the native node builds
+        AppendEntries text directly from its log)."""
+        tries, backoff = _RETRY.get(kind, (1, 0.0))
+        sess = await self._sess()
+        url = addr.rstrip("/") + f"/raft/{kind}"
+        if not url.startswith("http"):
+            url = "http://" + url
+        last: Exception | None = None
+        for attempt in range(tries):
+            try:
+                async with sess.post(url, data=body, headers={"Content-Type": "application/json"}) as r:
+                    if r.status != 200:
+                        raise TransportError(f"{url}: HTTP {r.status}")
+                    return await r.text()
+            except Exception as e:  # noqa: BLE001
+                last = e
+                if attempt + 1 < tries:
+                    await asyncio.sleep(backoff * (2 ** attempt))
+        raise TransportError(str(last))
+
     async def put_bytes(self, url: str, data: bytes) -> int:
         sess = await self._sess()
         async with sess.put(url, data=data) as r:

@@ -162,7 +162,7 @@ def test_snapshot_and_install_snapshot(tmp_path):
         for i in range(60):
             await l.propose({"set": [f"k{i}", i]})
         await asyncio.sleep(0.3)
-        l._maybe_snapshot()
+        await l.snapshot_now()
         assert l.last_included_index > 0
         c.faults.heal()
         for _ in range(100):
