@@ -47,6 +47,11 @@ def _newer(src: Path, obj: Path, headers: list[Path]) -> bool:
 
 def build(clean: bool = False, verbose: bool = False) -> Path:
     BUILD.mkdir(parents=True, exist_ok=True)
+    # native proto3 codec generated from proto/dfs.proto (no protoc in this toolchain)
+    sys.path.insert(0, str(ROOT / "scripts"))
+    import gen_proto
+
+    gen_proto.main()
     sources = sorted(list(CSRC.glob("*.cpp")) + list(CSRC.glob("*.hip")))
     headers = sorted(CSRC.glob("*.h"))
     flags = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result", "-fvisibility=hidden",

@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "dfs_pb.h"
 #include "raft.h"
 
 namespace py = pybind11;
@@ -111,6 +112,12 @@ struct NodeDeleter {
 }  // namespace
 
 void bind_meta(py::module_& m) {
+  m.def("pb_roundtrip", [](const std::string& name, py::bytes data) -> py::object {
+    std::string in = data, out;
+    if (!pb::roundtrip(name, in, &out)) return py::none();
+    return py::bytes(out);
+  }, "decode `data` as dfs.<name> with the native codec and re-encode it");
+
   py::class_<raft::Node, std::unique_ptr<raft::Node, NodeDeleter>>(m, "RaftNode")
       .def(py::init([](int id, std::map<int, std::string> members, std::string client_address, std::string dir,
                        py::object host, double elo, double ehi, double hb, bool sync, uint64_t snapshot_threshold,
