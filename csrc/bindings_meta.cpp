@@ -7,6 +7,8 @@
 #include <pybind11/stl.h>
 
 #include "dfs_pb.h"
+#include "localrpc.h"
+#include "master_core.h"
 #include "raft.h"
 
 namespace py = pybind11;
@@ -31,9 +33,11 @@ struct PyRef {
 // Host backed by a Python object with apply_batch / snapshot / restore / send / backup.
 class PyRaftHost : public raft::Host {
  public:
-  explicit PyRaftHost(py::object host) : host_(std::make_shared<PyRef>(std::move(host))) {}
+  PyRaftHost(py::object host, std::shared_ptr<raft::StateMachine> sm)
+      : host_(std::make_shared<PyRef>(std::move(host))), sm_(std::move(sm)) {}
 
   std::vector<std::string> apply(const std::vector<std::pair<uint64_t, std::string>>& cmds) override {
+    if (sm_) return sm_->apply(cmds);  // native state machine: no GIL on the apply path
     py::gil_scoped_acquire g;
     try {
       py::list l;
@@ -44,6 +48,7 @@ class PyRaftHost : public raft::Host {
     }
   }
   std::string snapshot() override {
+    if (sm_) return sm_->snapshot();
     py::gil_scoped_acquire g;
     try {
       return host_->obj.attr("snapshot")().cast<std::string>();
@@ -52,6 +57,7 @@ class PyRaftHost : public raft::Host {
     }
   }
   void restore(const std::string& state) override {
+    if (sm_) return sm_->restore(state);
     py::gil_scoped_acquire g;
     try {
       host_->obj.attr("restore")(py::str(state));
@@ -80,6 +86,7 @@ class PyRaftHost : public raft::Host {
 
  private:
   std::shared_ptr<PyRef> host_;
+  std::shared_ptr<raft::StateMachine> sm_;
 };
 
 // Read a node property with the GIL released (the getter may wait on the node mutex).
@@ -121,7 +128,7 @@ void bind_meta(py::module_& m) {
   py::class_<raft::Node, std::unique_ptr<raft::Node, NodeDeleter>>(m, "RaftNode")
       .def(py::init([](int id, std::map<int, std::string> members, std::string client_address, std::string dir,
                        py::object host, double elo, double ehi, double hb, bool sync, uint64_t snapshot_threshold,
-                       int max_batch, std::string backup_endpoint, std::string backup_bucket) {
+                       int max_batch, std::string backup_endpoint, std::string backup_bucket, py::object native_sm) {
              raft::Options o;
              o.id = id;
              o.members = std::move(members);
@@ -135,13 +142,16 @@ void bind_meta(py::module_& m) {
              o.max_append_batch = max_batch;
              o.backup_endpoint = std::move(backup_endpoint);
              o.backup_bucket = std::move(backup_bucket);
-             auto h = std::make_shared<PyRaftHost>(std::move(host));
+             std::shared_ptr<raft::StateMachine> sm;
+             if (!native_sm.is_none()) sm = native_sm.cast<std::shared_ptr<MasterCore>>();
+             auto h = std::make_shared<PyRaftHost>(std::move(host), sm);
              return std::unique_ptr<raft::Node, NodeDeleter>(new raft::Node(std::move(o), h));
            }),
            py::arg("id"), py::arg("members"), py::arg("client_address"), py::arg("dir"), py::arg("host"),
            py::arg("election_lo") = 1.5, py::arg("election_hi") = 3.0, py::arg("heartbeat") = 0.1,
            py::arg("sync") = true, py::arg("snapshot_threshold") = 10000, py::arg("max_append_batch") = 512,
-           py::arg("backup_endpoint") = "", py::arg("backup_bucket") = "dfs-backups")
+           py::arg("backup_endpoint") = "", py::arg("backup_bucket") = "dfs-backups",
+           py::arg("native_sm") = py::none())
       .def("start", &raft::Node::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &raft::Node::stop, py::call_guard<py::gil_scoped_release>())
       .def("propose", [](raft::Node& n, std::string cmd, py::object cb) {
@@ -188,4 +198,120 @@ void bind_meta(py::module_& m) {
       .def("info_json", &raft::Node::info_json, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("wal_syncs", &raft::Node::wal_syncs)
       .def_property_readonly("wal_bytes", &raft::Node::wal_bytes);
+
+  // ---------------- native master core + same-host RPC listener
+  py::class_<MasterCore, std::shared_ptr<MasterCore>>(m, "MasterCore")
+      .def(py::init([]() { return std::make_shared<MasterCore>(); }))
+      .def("attach", [](MasterCore& c, raft::Node& n) { c.attach(&n); }, py::keep_alive<1, 2>())
+      .def("detach", &MasterCore::detach)
+      .def("native_method", &MasterCore::native_method)
+      .def("handle", [](MasterCore& c, const std::string& method, py::bytes req) {
+        std::string in = req, out;
+        int code;
+        {
+          py::gil_scoped_release r;
+          code = c.handle(method, in, &out);
+        }
+        return py::make_tuple(code, py::bytes(out));
+      })
+      .def("set_shard_map", &MasterCore::set_shard_map, py::call_guard<py::gil_scoped_release>())
+      .def("set_access_stats", &MasterCore::set_access_stats)
+      .def("upsert_chunk_server", [](MasterCore& c, const std::string& addr, int64_t last_heartbeat, uint64_t used,
+                                     uint64_t avail, uint64_t chunks, const std::string& rack, int32_t gpu_rank,
+                                     uint64_t hbm_capacity, uint64_t hbm_used, uint64_t scheduled) {
+        ChunkServerStatus st;
+        st.address = addr;
+        st.last_heartbeat = last_heartbeat;
+        st.used_space = used;
+        st.available_space = avail;
+        st.chunk_count = chunks;
+        st.rack_id = rack;
+        st.gpu_rank = gpu_rank;
+        st.hbm_capacity = hbm_capacity;
+        st.hbm_used = hbm_used;
+        st.scheduled = scheduled;
+        c.upsert_chunk_server(st);
+      })
+      .def("remove_chunk_server", &MasterCore::remove_chunk_server)
+      .def("chunk_servers", [](MasterCore& c) {
+        py::list out;
+        for (auto& s : c.chunk_servers())
+          out.append(py::make_tuple(s.address, s.last_heartbeat, s.used_space, s.available_space, s.chunk_count,
+                                    s.rack_id, s.gpu_rank, s.hbm_capacity, s.hbm_used, s.scheduled));
+        return out;
+      })
+      .def("enter_safe_mode", &MasterCore::enter_safe_mode, py::arg("manual") = false)
+      .def("exit_safe_mode", &MasterCore::exit_safe_mode)
+      .def("should_exit_safe_mode", &MasterCore::should_exit_safe_mode)
+      .def("report_blocks", &MasterCore::report_blocks)
+      .def("safe_mode_status", [](MasterCore& c) { return c.safe_mode_status().dump(); })
+      .def("get_file", [](MasterCore& c, const std::string& path, bool visible_only) -> py::object {
+        std::string out;
+        if (!c.get_file(path, visible_only, &out)) return py::none();
+        return py::bytes(out);
+      }, py::arg("path"), py::arg("visible_only") = false)
+      .def("contains", &MasterCore::contains)
+      .def("under_construction", &MasterCore::under_construction)
+      .def("file_count", &MasterCore::file_count)
+      .def("paths", &MasterCore::paths, py::arg("prefix") = "", py::arg("visible_only") = false)
+      .def("files_pb", [](MasterCore& c, const std::string& prefix) {
+        py::list out;
+        for (auto& s : c.files_pb(prefix)) out.append(py::bytes(s));
+        return out;
+      }, py::arg("prefix") = "")
+      .def("find_block", [](MasterCore& c, const std::string& id) -> py::object {
+        std::string out;
+        if (!c.find_block(id, &out)) return py::none();
+        return py::bytes(out);
+      })
+      .def("has_block", &MasterCore::has_block)
+      .def("total_blocks", &MasterCore::total_blocks)
+      .def("tx_record", &MasterCore::tx_record)
+      .def("tx_records", &MasterCore::tx_records)
+      .def("tx_lock", &MasterCore::tx_lock)
+      .def("shuffling_prefixes", &MasterCore::shuffling_prefixes)
+      .def("take_request_counts", &MasterCore::take_request_counts)
+      .def("take_gc", &MasterCore::take_gc)
+      .def("snapshot", &MasterCore::snapshot, py::call_guard<py::gil_scoped_release>())
+      .def("restore", &MasterCore::restore, py::call_guard<py::gil_scoped_release>())
+      .def("apply", [](MasterCore& c, uint64_t idx, const std::string& cmd) {
+        return c.apply({{idx, cmd}}).front();  // tests: apply one command outside Raft
+      })
+      .def_property_readonly("requests", &MasterCore::requests);
+
+  m.def("select_servers_rack_aware", [](MasterCore& c, size_t n, const std::string& preferred) {
+    return select_servers_rack_aware(c.chunk_servers(), n, preferred);
+  });
+
+  py::class_<LocalRpcServer>(m, "MasterLocalServer")
+      .def(py::init([](const std::string& name, std::shared_ptr<MasterCore> core, py::object fallback) {
+             auto fb = std::make_shared<PyRef>(std::move(fallback));
+             static const std::string kPrefix = "/dfs.MasterService/";
+             LocalRpcServer::Handler h = [core, fb](const std::string& path, const std::string& rid,
+                                                    const std::string& payload, std::string* out) -> int {
+               if (path.compare(0, kPrefix.size(), kPrefix) == 0) {
+                 std::string method = path.substr(kPrefix.size());
+                 if (core->native_method(method)) return core->handle(method, payload, out);
+               }
+               // everything else runs the Python service handler on its event loop
+               py::gil_scoped_acquire g;
+               try {
+                 py::tuple r = fb->obj(path, rid, py::bytes(payload));
+                 *out = r[1].cast<std::string>();
+                 return r[0].cast<int>();
+               } catch (py::error_already_set& e) {
+                 *out = e.what();
+                 return 13;
+               }
+             };
+             return std::make_unique<LocalRpcServer>(name, std::move(h));
+           }),
+           py::keep_alive<1, 3>())
+      .def("start", [](LocalRpcServer& s) {
+        std::string err;
+        bool ok = s.start(&err);
+        return py::make_tuple(ok, err);
+      })
+      .def("stop", &LocalRpcServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("requests", &LocalRpcServer::requests);
 }

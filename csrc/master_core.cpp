@@ -1,0 +1,1224 @@
+#include "master_core.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <future>
+#include <memory>
+
+namespace dfs {
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+const char* kSafeModeMsg = "Cluster is in Safe Mode. Write operations are blocked.";
+constexpr uint64_t kScheduleQuantum = 64ull << 20;
+constexpr size_t kReplication = 3;
+
+int64_t create_lease_ms() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("DFS_CREATE_LEASE_MS");
+    return e ? std::atoll(e) : 60000;
+  }();
+  return v;
+}
+
+// ---- serde layout of FileMetadata / BlockInfo (reference build.rs serde derives; models/meta.py)
+Json block_json(const pb::BlockInfo& b) {
+  Json d = Json::object();
+  d.set("block_id", b.block_id);
+  d.set("size", b.size);
+  d.set("checksum_crc32c", b.checksum_crc32c);
+  d.set("ec_data_shards", b.ec_data_shards);
+  d.set("ec_parity_shards", b.ec_parity_shards);
+  d.set("original_size", b.original_size);
+  Json l = Json::array();
+  for (auto& x : b.locations) l.push_back(x);
+  d.set("locations", l);
+  return d;
+}
+
+pb::BlockInfo block_from(const Json& d) {
+  pb::BlockInfo b;
+  b.block_id = d["block_id"].str();
+  b.size = d["size"].as_u64();
+  b.checksum_crc32c = static_cast<uint32_t>(d["checksum_crc32c"].as_u64());
+  b.ec_data_shards = static_cast<int32_t>(d["ec_data_shards"].as_int());
+  b.ec_parity_shards = static_cast<int32_t>(d["ec_parity_shards"].as_int());
+  b.original_size = d["original_size"].as_u64();
+  for (auto& x : d["locations"].items()) b.locations.push_back(x.str());
+  return b;
+}
+
+Json file_json(const pb::FileMetadata& m) {
+  Json d = Json::object();
+  d.set("path", m.path);
+  d.set("size", m.size);
+  d.set("etag_md5", m.etag_md5);
+  d.set("created_at_ms", m.created_at_ms);
+  d.set("ec_data_shards", m.ec_data_shards);
+  d.set("ec_parity_shards", m.ec_parity_shards);
+  d.set("last_access_ms", m.last_access_ms);
+  d.set("access_count", m.access_count);
+  d.set("moved_to_cold_at_ms", m.moved_to_cold_at_ms);
+  Json bl = Json::array();
+  for (auto& b : m.blocks) bl.push_back(block_json(b));
+  d.set("blocks", bl);
+  return d;
+}
+
+pb::FileMetadata file_from(const Json& d) {
+  pb::FileMetadata m;
+  m.path = d["path"].str();
+  m.size = d["size"].as_u64();
+  m.etag_md5 = d["etag_md5"].str();
+  m.created_at_ms = d["created_at_ms"].as_u64();
+  m.ec_data_shards = static_cast<int32_t>(d["ec_data_shards"].as_int());
+  m.ec_parity_shards = static_cast<int32_t>(d["ec_parity_shards"].as_int());
+  m.last_access_ms = d["last_access_ms"].as_u64();
+  m.access_count = d["access_count"].as_u64();
+  m.moved_to_cold_at_ms = d["moved_to_cold_at_ms"].as_u64();
+  for (auto& b : d["blocks"].items()) m.blocks.push_back(block_from(b));
+  return m;
+}
+
+Json block_list(const pb::FileMetadata& m) {  // [[block_id, [locations]], ...]
+  Json out = Json::array();
+  for (auto& b : m.blocks) {
+    Json locs = Json::array();
+    for (auto& l : b.locations) locs.push_back(l);
+    out.push_back(Json(Json::Array{Json(b.block_id), locs}));
+  }
+  return out;
+}
+
+Json obj(std::initializer_list<std::pair<const char*, Json>> kv) {
+  Json o = Json::object();
+  for (auto& p : kv) o.set(p.first, p.second);
+  return o;
+}
+
+std::string prefix_of(const std::string& path) {
+  size_t i = 0;
+  while (i < path.size() && path[i] == '/') ++i;
+  if (i == path.size()) return "/";
+  size_t j = path.find('/', i);
+  return "/" + path.substr(i, j == std::string::npos ? std::string::npos : j - i) + "/";
+}
+
+std::string locked_path(const Json& rec) {
+  const Json& ren = rec["tx_type"]["Rename"];
+  const std::string& st = rec["state"].as_string();
+  if (ren.is_null() || st == "Committed" || st == "Aborted") return "";
+  const std::string& src = ren["source_path"].as_string();
+  return src.empty() ? ren["dest_path"].str() : src;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- placement
+std::vector<std::string> select_servers_rack_aware(const std::vector<ChunkServerStatus>& servers, size_t n,
+                                                   const std::string& preferred) {
+  std::vector<std::string> selected;
+  if (n == 0 || servers.empty()) return selected;
+  // free space net of blocks scheduled since the last heartbeat (HDFS-style), so a burst of
+  // allocations rotates over equally-free servers instead of piling onto the same ones
+  std::vector<const ChunkServerStatus*> cands;
+  for (auto& s : servers) cands.push_back(&s);
+  auto net = [](const ChunkServerStatus* s) {
+    return static_cast<int64_t>(s->available_space) - static_cast<int64_t>(s->scheduled);
+  };
+  std::sort(cands.begin(), cands.end(), [&](const ChunkServerStatus* a, const ChunkServerStatus* b) {
+    int64_t na = net(a), nb = net(b);
+    return na != nb ? na > nb : a->address < b->address;
+  });
+  std::string pref_rack;
+  if (!preferred.empty()) {
+    auto it = std::find_if(cands.begin(), cands.end(), [&](auto* s) { return s->address == preferred; });
+    if (it != cands.end()) {
+      selected.push_back(preferred);
+      pref_rack = (*it)->rack_id;
+      cands.erase(it);
+    }
+  }
+  std::vector<std::string> order;
+  std::map<std::string, std::vector<const ChunkServerStatus*>> buckets;
+  for (auto* s : cands) {
+    std::string key = s->rack_id.empty() ? "__addr__" + s->address : s->rack_id;
+    if (!buckets.count(key)) order.push_back(key);
+    buckets[key].push_back(s);
+  }
+  // the writer's rack goes last so the next replicas spread to other racks first
+  if (!selected.empty() && !pref_rack.empty() && buckets.count(pref_rack)) {
+    order.erase(std::find(order.begin(), order.end(), pref_rack));
+    order.push_back(pref_rack);
+  }
+  std::vector<size_t> pos(order.size(), 0);
+  while (selected.size() < n) {
+    bool picked = false;
+    for (size_t i = 0; i < order.size() && selected.size() < n; ++i) {
+      auto& rack = buckets[order[i]];
+      if (pos[i] < rack.size()) {
+        selected.push_back(rack[pos[i]++]->address);
+        picked = true;
+      }
+    }
+    if (!picked) break;
+  }
+  selected.resize(std::min(selected.size(), n));
+  return selected;
+}
+
+// ---------------------------------------------------------------- lifecycle
+MasterCore::MasterCore() : rng_(std::random_device{}()) {
+  access_thread_ = std::thread([this] { access_loop(); });
+}
+
+MasterCore::~MasterCore() {
+  running_ = false;
+  access_cv_.notify_all();
+  if (access_thread_.joinable()) access_thread_.join();
+}
+
+void MasterCore::attach(raft::Node* node) { node_ = node; }
+void MasterCore::detach() { node_ = nullptr; }
+
+void MasterCore::set_access_stats(bool on, int flush_ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  access_stats_ = on;
+  access_flush_ms_ = flush_ms;
+}
+
+void MasterCore::set_shard_map(const std::string& json, const std::string& shard_id) {
+  ShardMap m = json.empty() ? ShardMap::new_range() : ShardMap::from_json(Json::parse(json));
+  std::lock_guard<std::mutex> g(mu_);
+  shard_map_ = std::move(m);
+  shard_id_ = shard_id;
+  have_map_ = !json.empty();
+}
+
+// ---------------------------------------------------------------- state machine
+void MasterCore::put(const std::string& path, pb::FileMetadata m) {
+  auto it = files_.find(path);
+  if (it != files_.end())
+    for (auto& b : it->second.blocks) {
+      auto bi = block_index_.find(b.block_id);
+      if (bi != block_index_.end() && bi->second == path) block_index_.erase(bi);
+    }
+  for (auto& b : m.blocks) block_index_[b.block_id] = path;
+  files_[path] = std::move(m);
+}
+
+bool MasterCore::del(const std::string& path, pb::FileMetadata* out) {
+  under_construction_.erase(path);
+  auto it = files_.find(path);
+  if (it == files_.end()) return false;
+  for (auto& b : it->second.blocks) {
+    auto bi = block_index_.find(b.block_id);
+    if (bi != block_index_.end() && bi->second == path) block_index_.erase(bi);
+  }
+  if (out) *out = std::move(it->second);
+  files_.erase(it);
+  return true;
+}
+
+const pb::FileMetadata* MasterCore::visible(const std::string& path) const {
+  if (under_construction_.count(path)) return nullptr;
+  auto it = files_.find(path);
+  return it == files_.end() ? nullptr : &it->second;
+}
+
+pb::BlockInfo* MasterCore::find_block_locked(const std::string& block_id, pb::FileMetadata** file) {
+  auto bi = block_index_.find(block_id);
+  if (bi == block_index_.end()) return nullptr;
+  auto it = files_.find(bi->second);
+  if (it == files_.end()) return nullptr;
+  for (auto& b : it->second.blocks)
+    if (b.block_id == block_id) {
+      if (file) *file = &it->second;
+      return &b;
+    }
+  return nullptr;
+}
+
+void MasterCore::relock(const Json& rec) {
+  const std::string id = rec["tx_id"].str();
+  for (auto it = tx_locks_.begin(); it != tx_locks_.end();) it = it->second == id ? tx_locks_.erase(it) : std::next(it);
+  std::string p = locked_path(rec);
+  if (!p.empty()) tx_locks_[p] = id;
+}
+
+std::vector<std::string> MasterCore::apply(const std::vector<std::pair<uint64_t, std::string>>& cmds) {
+  std::vector<std::string> out;
+  out.reserve(cmds.size());
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& c : cmds) {
+      try {
+        Json j = Json::parse(c.second);
+        const Json* m = j.find("Master");
+        if (!m || m->fields().empty()) {
+          out.push_back("null");
+          continue;
+        }
+        auto& kv = m->fields().front();
+        out.push_back(apply_one(kv.first, kv.second).dump());
+      } catch (const std::exception& e) {
+        out.push_back(std::string("!") + e.what());
+      }
+    }
+  }
+  applied_cv_.notify_all();
+  return out;
+}
+
+Json MasterCore::apply_one(const std::string& name, const Json& a) {
+  const std::string path = a["path"].str();
+  if (name == "CreateFile" || name == "CreateComplete") {
+    // existence is decided here, in log order: two racing creates cannot both succeed
+    if (tx_locks_.count(path)) return obj({{"locked", path}});
+    int64_t ts = a["ts"].as_int();
+    pb::FileMetadata old;
+    bool had_old = false;
+    auto it = files_.find(path);
+    if (it != files_.end()) {
+      auto uc = under_construction_.find(path);
+      if (uc == under_construction_.end() || ts - uc->second < create_lease_ms()) return obj({{"exists", true}});
+      old = it->second;  // a writer that died mid-create: its lease expired, take the path over
+      had_old = true;
+    }
+    pb::FileMetadata m;
+    m.path = path;
+    m.ec_data_shards = static_cast<int32_t>(a["ec_data_shards"].as_int());
+    m.ec_parity_shards = static_cast<int32_t>(a["ec_parity_shards"].as_int());
+    if (name == "CreateFile") {
+      if (!a["block_id"].str().empty()) {
+        pb::BlockInfo b;
+        b.block_id = a["block_id"].str();
+        b.ec_data_shards = m.ec_data_shards;
+        b.ec_parity_shards = m.ec_parity_shards;
+        for (auto& l : a["locations"].items()) b.locations.push_back(l.str());
+        m.blocks.push_back(std::move(b));
+      }
+      put(path, std::move(m));
+      under_construction_[path] = ts;
+    } else {
+      for (auto& bd : a["blocks"].items()) m.blocks.push_back(block_from(bd));
+      put(path, std::move(m));
+      under_construction_.erase(path);
+      apply_one("CompleteFile", a);
+    }
+    return obj({{"exists", false}, {"orphans", had_old ? block_list(old) : Json::array()}});
+  }
+  if (name == "CompleteFile") {
+    auto it = files_.find(path);
+    if (it == files_.end()) return obj({{"found", false}});
+    pb::FileMetadata& m = it->second;
+    under_construction_.erase(path);
+    m.size = a["size"].as_u64();
+    if (!a["etag_md5"].str().empty()) m.etag_md5 = a["etag_md5"].str();
+    if (a["created_at_ms"].as_u64()) m.created_at_ms = a["created_at_ms"].as_u64();
+    const Json& sums = a["block_checksums"];
+    if (sums.size()) {
+      for (auto& s : sums.items())
+        for (auto& b : m.blocks)
+          if (b.block_id == s["block_id"].as_string()) {
+            b.checksum_crc32c = static_cast<uint32_t>(s["checksum_crc32c"].as_u64());
+            b.size = s["actual_size"].as_u64();
+            b.original_size = b.size;
+          }
+    } else if (!m.blocks.empty()) {
+      uint64_t n = m.blocks.size(), per = m.size / n;
+      for (size_t i = 0; i + 1 < n; ++i) m.blocks[i].size = per;
+      m.blocks.back().size = m.size - per * (n - 1);
+    }
+    return obj({{"found", true}});
+  }
+  if (name == "DeleteFile") {
+    if (tx_locks_.count(path)) return obj({{"locked", path}});
+    if (!visible(path)) return obj({{"found", false}});
+    pb::FileMetadata m;
+    del(path, &m);
+    return obj({{"found", true}, {"blocks", block_list(m)}});
+  }
+  if (name == "AllocateBlock") {
+    auto it = files_.find(path);
+    if (it == files_.end()) return Json();
+    pb::BlockInfo b;
+    b.block_id = a["block_id"].str();
+    b.ec_data_shards = it->second.ec_data_shards;
+    b.ec_parity_shards = it->second.ec_parity_shards;
+    for (auto& l : a["locations"].items()) b.locations.push_back(l.str());
+    block_index_[b.block_id] = path;
+    it->second.blocks.push_back(std::move(b));
+    return Json();
+  }
+  if (name == "RenameFile") {
+    // decided in log order: the source must be complete, the destination must not exist
+    std::string src = a["source_path"].str(), dst = a["dest_path"].str();
+    for (auto* p : {&src, &dst})
+      if (tx_locks_.count(*p)) return obj({{"locked", *p}});
+    if (!visible(src)) return obj({{"error", "Source file not found: " + src}});
+    if (files_.count(dst)) return obj({{"error", "Destination file already exists: " + dst}});
+    pb::FileMetadata m;
+    del(src, &m);
+    m.path = dst;
+    put(dst, std::move(m));
+    return obj({{"error", Json()}});
+  }
+  if (name == "CreateTransactionRecord") {
+    const Json& rec = a["record"];
+    std::string id = rec["tx_id"].str();
+    if (tx_records_.count(id)) return obj({{"conflict", Json()}});
+    std::string p = locked_path(rec);
+    const Json& ren = rec["tx_type"]["Rename"];
+    if (!ren.is_null() && !p.empty()) {
+      auto lk = tx_locks_.find(p);
+      if (lk != tx_locks_.end() && lk->second != id) return obj({{"conflict", p + " is locked by another transaction"}});
+      if (!ren["source_path"].str().empty()) {
+        if (!visible(p)) return obj({{"conflict", "Source file not found: " + p}});
+      } else if (files_.count(p)) {
+        return obj({{"conflict", "Destination file already exists: " + p}});
+      }
+    }
+    tx_records_[id] = rec;
+    relock(rec);
+    return obj({{"conflict", Json()}});
+  }
+  if (name == "UpdateTransactionState") {
+    auto it = tx_records_.find(a["tx_id"].str());
+    if (it != tx_records_.end()) {
+      it->second.set("state", a["new_state"]);
+      relock(it->second);
+    }
+    return Json();
+  }
+  if (name == "ApplyTransactionOperation") {
+    const Json& op = a["operation"]["op_type"];
+    if (const Json* d = op.find("Delete")) {
+      del((*d)["path"].str(), nullptr);
+    } else if (const Json* c = op.find("Create")) {
+      std::string p = (*c)["path"].str();
+      if (!files_.count(p)) {
+        pb::FileMetadata m = file_from((*c)["metadata"]);
+        m.path = p;
+        put(p, std::move(m));
+      }
+    }
+    return Json();
+  }
+  if (name == "DeleteTransactionRecord") {
+    auto it = tx_records_.find(a["tx_id"].str());
+    if (it != tx_records_.end()) {
+      Json rec = it->second;
+      tx_records_.erase(it);
+      rec.set("state", "Aborted");
+      relock(rec);
+    }
+    return Json();
+  }
+  if (name == "SplitShard") {
+    if (const Json* ps = a.find("paths")) {  // explicit list: the files the post-split map routes away
+      for (auto& p : ps->items()) del(p.str(), nullptr);
+      return Json();
+    }
+    std::string key = a["split_key"].str();
+    std::vector<std::string> moving;
+    for (auto& kv : files_)
+      if (kv.first >= key) moving.push_back(kv.first);
+    for (auto& p : moving) del(p, nullptr);
+    return Json();
+  }
+  if (name == "IngestBatch") {
+    for (auto& f : a["files"].items()) {
+      pb::FileMetadata m = file_from(f);
+      std::string p = m.path;
+      put(p, std::move(m));
+    }
+    return Json();
+  }
+  if (name == "TriggerShuffle") {
+    shuffling_prefixes_.insert(a["prefix"].str());
+    return Json();
+  }
+  if (name == "StopShuffle") {
+    shuffling_prefixes_.erase(a["prefix"].str());
+    return Json();
+  }
+  if (name == "UpdateAccessStats") {
+    auto it = files_.find(path);
+    if (it != files_.end()) {
+      it->second.last_access_ms = a["accessed_at_ms"].as_u64();
+      it->second.access_count++;
+    }
+    return Json();
+  }
+  if (name == "UpdateAccessStatsBatch") {
+    uint64_t t = a["accessed_at_ms"].as_u64();
+    for (auto& kv : a["paths"].fields()) {
+      auto it = files_.find(kv.first);
+      if (it != files_.end()) {
+        it->second.last_access_ms = t;
+        it->second.access_count += kv.second.as_u64();
+      }
+    }
+    return Json();
+  }
+  if (name == "MoveToCold") {
+    auto it = files_.find(path);
+    if (it != files_.end()) it->second.moved_to_cold_at_ms = a["moved_at_ms"].as_u64();
+    return Json();
+  }
+  if (name == "ConvertToEc") {
+    auto it = files_.find(path);
+    if (it == files_.end()) return Json();
+    pb::FileMetadata& m = it->second;
+    for (auto& b : m.blocks) block_index_.erase(b.block_id);
+    m.ec_data_shards = static_cast<int32_t>(a["ec_data_shards"].as_int());
+    m.ec_parity_shards = static_cast<int32_t>(a["ec_parity_shards"].as_int());
+    m.blocks.clear();
+    for (auto& bd : a["new_blocks"].items()) m.blocks.push_back(block_from(bd));
+    for (auto& b : m.blocks) block_index_[b.block_id] = m.path;
+    return Json();
+  }
+  if (name == "SetParticipantAcked" || name == "IncrementInquiryCount") {
+    auto it = tx_records_.find(a["tx_id"].str());
+    if (it != tx_records_.end()) {
+      if (name == "SetParticipantAcked") it->second.set("participant_acked", true);
+      else it->second.set("inquiry_count", it->second["inquiry_count"].as_int() + 1);
+    }
+    return Json();
+  }
+  if (name == "AddBlockLocation") {
+    pb::BlockInfo* b = find_block_locked(a["block_id"].str(), nullptr);
+    if (!b) return Json();
+    std::string addr = a["address"].str();
+    const Json& idx = a["shard_index"];
+    if (!idx.is_null() && b->ec_data_shards > 0) {
+      // EC locations are positional (shard i lives at locations[i]): a rebuilt shard
+      // replaces its dead holder instead of being appended
+      int64_t i = idx.as_int();
+      if (i >= 0 && static_cast<size_t>(i) < b->locations.size()) b->locations[i] = addr;
+      return Json();
+    }
+    if (std::find(b->locations.begin(), b->locations.end(), addr) == b->locations.end()) b->locations.push_back(addr);
+    return Json();
+  }
+  if (name == "UpdateBlockLocations") {
+    pb::BlockInfo* b = find_block_locked(a["block_id"].str(), nullptr);
+    if (b) {
+      b->locations.clear();
+      for (auto& l : a["locations"].items()) b->locations.push_back(l.str());
+    }
+    return Json();
+  }
+  if (name == "MergeShard" || name == "RegisterChunkServer") return Json();
+  std::fprintf(stderr, "master: unknown command %s\n", name.c_str());
+  return Json();
+}
+
+std::string MasterCore::snapshot() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::string out = "{\"Master\":{\"files\":{";
+  bool first = true;
+  std::vector<const std::string*> keys;
+  keys.reserve(files_.size());
+  for (auto& kv : files_) keys.push_back(&kv.first);
+  std::sort(keys.begin(), keys.end(), [](auto* a, auto* b) { return *a < *b; });
+  for (auto* k : keys) {
+    if (!first) out += ",";
+    first = false;
+    json_escape(*k, out);
+    out += ":";
+    file_json(files_.at(*k)).dump_to(out);
+  }
+  out += "},\"transaction_records\":";
+  Json tx = Json::object();
+  for (auto& kv : tx_records_) tx.set(kv.first, kv.second);
+  tx.dump_to(out);
+  out += ",\"shuffling_prefixes\":";
+  Json sp = Json::array();
+  for (auto& p : shuffling_prefixes_) sp.push_back(p);
+  sp.dump_to(out);
+  out += ",\"under_construction\":";
+  Json uc = Json::object();
+  for (auto& kv : under_construction_) uc.set(kv.first, kv.second);
+  uc.dump_to(out);
+  out += "}}";
+  return out;
+}
+
+void MasterCore::restore(const std::string& text) {
+  Json j = Json::parse(text);
+  const Json* st = j.find("Master");
+  const Json& s = st ? *st : j;  // a legacy raw MasterState is accepted too
+  std::lock_guard<std::mutex> g(mu_);
+  files_.clear();
+  block_index_.clear();
+  for (auto& kv : s["files"].fields()) put(kv.first, file_from(kv.second));
+  tx_records_.clear();
+  tx_locks_.clear();
+  for (auto& kv : s["transaction_records"].fields()) {
+    tx_records_[kv.first] = kv.second;
+    relock(kv.second);
+  }
+  shuffling_prefixes_.clear();
+  for (auto& p : s["shuffling_prefixes"].items()) shuffling_prefixes_.insert(p.str());
+  under_construction_.clear();
+  for (auto& kv : s["under_construction"].fields())
+    if (files_.count(kv.first)) under_construction_[kv.first] = kv.second.as_int();
+}
+
+// ---------------------------------------------------------------- chunkservers / safe mode
+void MasterCore::upsert_chunk_server(const ChunkServerStatus& st) {
+  std::lock_guard<std::mutex> g(mu_);
+  chunk_servers_[st.address] = st;
+}
+
+bool MasterCore::remove_chunk_server(const std::string& addr) {
+  std::lock_guard<std::mutex> g(mu_);
+  return chunk_servers_.erase(addr) != 0;
+}
+
+std::vector<ChunkServerStatus> MasterCore::chunk_servers() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<ChunkServerStatus> out;
+  for (auto& kv : chunk_servers_) out.push_back(kv.second);
+  return out;
+}
+
+void MasterCore::enter_safe_mode(bool manual) {
+  std::lock_guard<std::mutex> g(mu_);
+  safe_mode_ = true;
+  safe_mode_entered_at_ = now_ms();
+  safe_mode_threshold_ = 0.99;
+  uint64_t n = 0;
+  for (auto& kv : files_) n += kv.second.blocks.size();
+  expected_blocks_ = n;
+  reported_blocks_ = 0;
+  safe_mode_manual_ = manual;
+}
+
+void MasterCore::exit_safe_mode() {
+  std::lock_guard<std::mutex> g(mu_);
+  safe_mode_ = false;
+  safe_mode_manual_ = false;
+}
+
+bool MasterCore::should_exit_safe_mode() const {
+  std::lock_guard<std::mutex> g(mu_);
+  if (safe_mode_manual_ || !safe_mode_ || chunk_servers_.empty()) return false;
+  if (expected_blocks_ == 0) return true;
+  if (static_cast<double>(reported_blocks_) / static_cast<double>(expected_blocks_) >= safe_mode_threshold_) return true;
+  return now_ms() - safe_mode_entered_at_ > 60000;
+}
+
+void MasterCore::report_blocks(uint64_t n) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    reported_blocks_ += n;
+  }
+  if (should_exit_safe_mode()) exit_safe_mode();
+}
+
+Json MasterCore::safe_mode_status() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return obj({{"is_safe_mode", safe_mode_},
+              {"is_manual", safe_mode_manual_},
+              {"chunk_server_count", static_cast<uint64_t>(chunk_servers_.size())},
+              {"expected_blocks", expected_blocks_},
+              {"reported_blocks", reported_blocks_},
+              {"threshold", safe_mode_threshold_},
+              {"entered_at", safe_mode_entered_at_}});
+}
+
+// ---------------------------------------------------------------- queries
+bool MasterCore::get_file(const std::string& path, bool visible_only, std::string* out) const {
+  std::lock_guard<std::mutex> g(mu_);
+  const pb::FileMetadata* m = nullptr;
+  if (visible_only) {
+    m = visible(path);
+  } else {
+    auto it = files_.find(path);
+    if (it != files_.end()) m = &it->second;
+  }
+  if (!m) return false;
+  m->encode(*out);
+  return true;
+}
+
+bool MasterCore::contains(const std::string& path) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return files_.count(path) != 0;
+}
+
+bool MasterCore::under_construction(const std::string& path) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return under_construction_.count(path) != 0;
+}
+
+size_t MasterCore::file_count() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return files_.size();
+}
+
+std::vector<std::string> MasterCore::paths(const std::string& prefix, bool visible_only) const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> out;
+  for (auto& kv : files_) {
+    if (kv.first.compare(0, prefix.size(), prefix) != 0) continue;
+    if (visible_only && under_construction_.count(kv.first)) continue;
+    out.push_back(kv.first);
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+std::vector<std::string> MasterCore::files_pb(const std::string& prefix) const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> out;
+  for (auto& kv : files_)
+    if (kv.first.compare(0, prefix.size(), prefix) == 0) out.push_back(kv.second.str());
+  return out;
+}
+
+bool MasterCore::find_block(const std::string& block_id, std::string* file_pb) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto bi = block_index_.find(block_id);
+  if (bi == block_index_.end()) return false;
+  auto it = files_.find(bi->second);
+  if (it == files_.end()) return false;
+  it->second.encode(*file_pb);
+  return true;
+}
+
+bool MasterCore::has_block(const std::string& block_id) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return block_index_.count(block_id) != 0;
+}
+
+uint64_t MasterCore::total_blocks() const {
+  std::lock_guard<std::mutex> g(mu_);
+  uint64_t n = 0;
+  for (auto& kv : files_) n += kv.second.blocks.size();
+  return n;
+}
+
+std::string MasterCore::tx_record(const std::string& tx_id) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = tx_records_.find(tx_id);
+  return it == tx_records_.end() ? std::string() : it->second.dump();
+}
+
+std::string MasterCore::tx_records() const {
+  std::lock_guard<std::mutex> g(mu_);
+  Json o = Json::object();
+  for (auto& kv : tx_records_) o.set(kv.first, kv.second);
+  return o.dump();
+}
+
+std::string MasterCore::tx_lock(const std::string& path) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = tx_locks_.find(path);
+  return it == tx_locks_.end() ? std::string() : it->second;
+}
+
+std::vector<std::string> MasterCore::shuffling_prefixes() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return {shuffling_prefixes_.begin(), shuffling_prefixes_.end()};
+}
+
+std::map<std::string, uint64_t> MasterCore::take_request_counts() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::map<std::string, uint64_t> out;
+  out.swap(request_counts_);
+  return out;
+}
+
+std::vector<std::pair<std::string, std::vector<std::string>>> MasterCore::take_gc() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::pair<std::string, std::vector<std::string>>> out;
+  out.swap(gc_);
+  return out;
+}
+
+// ---------------------------------------------------------------- RPC plumbing
+MasterCore::Result MasterCore::propose(const Json& cmd) {
+  raft::Node* node = node_.load();
+  if (!node) return {1, ""};
+  auto prom = std::make_shared<std::promise<Result>>();
+  auto fut = prom->get_future();
+  node->propose(cmd.dump(), [prom](int code, const std::string& payload) { prom->set_value(Result{code, payload}); });
+  if (fut.wait_for(std::chrono::seconds(30)) != std::future_status::ready) return {2, "proposal timed out"};
+  return fut.get();
+}
+
+MasterCore::Result MasterCore::propose_unlocked(const std::string& name, const Json& args) {
+  for (int attempt = 0; attempt < 50; ++attempt) {
+    Json master = Json::object();
+    master.set(name, args);
+    Result r = propose(obj({{"Master", master}}));
+    if (r.code != 0) return r;
+    Json res = Json::parse(r.payload);
+    const Json* lk = res.find("locked");
+    if (!lk) return r;
+    std::string err;
+    if (!wait_unlocked(lk->str(), 5000, &err)) return {3, err};
+  }
+  return {3, name + ": path stays locked by cross-shard renames"};
+}
+
+int MasterCore::read_index(std::string* err) {
+  raft::Node* node = node_.load();
+  if (!node) {
+    *err = "Not Leader";
+    return FAILED_PRECONDITION;
+  }
+  auto prom = std::make_shared<std::promise<Result>>();
+  auto fut = prom->get_future();
+  node->read_index([prom](int code, const std::string& payload) { prom->set_value(Result{code, payload}); });
+  if (fut.wait_for(std::chrono::seconds(10)) != std::future_status::ready) {
+    *err = "ReadIndex timed out";
+    return UNAVAILABLE;
+  }
+  Result r = fut.get();
+  if (r.code == 0) return OK;
+  if (r.code == 1) {
+    *err = r.payload.empty() ? "Not Leader" : "Not Leader|" + r.payload;
+    return FAILED_PRECONDITION;
+  }
+  *err = r.payload;
+  return INTERNAL;
+}
+
+bool MasterCore::wait_unlocked(const std::string& path, int timeout_ms, std::string* err) {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!tx_locks_.count(path)) return true;
+  if (applied_cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !tx_locks_.count(path); }))
+    return true;
+  auto it = tx_locks_.find(path);
+  *err = path + " is locked by transaction " + (it == tx_locks_.end() ? std::string() : it->second);
+  return false;
+}
+
+int MasterCore::check_ownership(const std::string& path, std::string* err) const {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!have_map_) return OK;
+  std::string target = shard_map_.get_shard(path);
+  if (target.empty() || target == shard_id_) return OK;
+  const auto* peers = shard_map_.peers(target);
+  *err = "REDIRECT:" + (peers && !peers->empty() ? peers->front() : std::string());
+  return OUT_OF_RANGE;
+}
+
+bool MasterCore::place(int ec_d, int ec_p, const std::string& preferred, std::vector<std::string>* out,
+                       std::string* err) {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<ChunkServerStatus> cands;
+  for (auto& kv : chunk_servers_) cands.push_back(kv.second);
+  size_t needed;
+  bool ec = ec_d > 0 && ec_p > 0;
+  if (ec) {
+    size_t total = static_cast<size_t>(ec_d + ec_p);
+    if (cands.size() < total) {
+      *err = "Need " + std::to_string(total) + " chunk servers for EC(" + std::to_string(ec_d) + "," +
+             std::to_string(ec_p) + "), only " + std::to_string(cands.size()) + " available";
+      return false;
+    }
+    needed = total;
+  } else {
+    needed = std::min(kReplication, cands.size());
+  }
+  if (needed == 0) {
+    *err = "No chunk servers available";
+    return false;
+  }
+  *out = select_servers_rack_aware(cands, needed, ec ? std::string() : preferred);
+  for (auto& a : *out) chunk_servers_[a].scheduled += kScheduleQuantum;
+  return true;
+}
+
+void MasterCore::allocation(const std::string& block_id, const std::vector<std::string>& sel, int ec_d, int ec_p,
+                            pb::AllocateBlockResponse* a) const {
+  a->block.block_id = block_id;
+  a->block.locations = sel;
+  a->block.ec_data_shards = ec_d;
+  a->block.ec_parity_shards = ec_p;
+  a->has_block = true;
+  a->chunk_server_addresses = sel;
+  a->ec_data_shards = ec_d;
+  a->ec_parity_shards = ec_p;
+  raft::Node* node = node_.load();
+  a->master_term = node ? node->term() : 0;
+}
+
+void MasterCore::record_request(const std::string& path) {
+  std::string p = prefix_of(path);
+  std::lock_guard<std::mutex> g(mu_);
+  request_counts_[p]++;
+  requests_++;
+}
+
+void MasterCore::record_access(const std::string& path) {
+  raft::Node* node = node_.load();
+  if (!node || !node->is_leader()) return;
+  std::lock_guard<std::mutex> g(mu_);
+  if (!access_stats_) return;
+  access_buf_[path]++;
+}
+
+void MasterCore::access_loop() {
+  // The reference fires one Raft write per GetFileInfo (master.rs:2187-2209); the same
+  // statistics (last_access_ms, access_count) go out as ONE batched entry per window.
+  while (running_) {
+    std::map<std::string, uint64_t> buf;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      access_cv_.wait_for(lk, std::chrono::milliseconds(access_flush_ms_), [&] { return !running_.load(); });
+      buf.swap(access_buf_);
+    }
+    raft::Node* node = node_.load();
+    if (buf.empty() || !node || !node->is_leader()) continue;
+    Json paths = Json::object();
+    for (auto& kv : buf) paths.set(kv.first, kv.second);
+    Json batch = obj({{"accessed_at_ms", now_ms()}, {"paths", paths}});
+    Json master = obj({{"UpdateAccessStatsBatch", batch}});
+    node->propose_nowait(obj({{"Master", master}}).dump());
+  }
+}
+
+void MasterCore::queue_gc(const Json& blocks) {
+  // Extension: blocks no file references any more get DELETE commands (the reference never
+  // garbage-collects blocks; proto DELETE is "future use").
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& e : blocks.items()) {
+    std::string bid = e[0].str();
+    if (block_index_.count(bid)) continue;
+    std::vector<std::string> locs;
+    for (auto& l : e[1].items()) locs.push_back(l.str());
+    gc_.emplace_back(bid, locs);
+  }
+}
+
+std::string MasterCore::new_uuid() {
+  uint64_t hi, lo;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    hi = rng_();
+    lo = rng_();
+  }
+  hi = (hi & ~0xF000ull) | 0x4000ull;                  // version 4
+  lo = (lo & 0x3FFFFFFFFFFFFFFFull) | 0x8000000000000000ull;  // RFC 4122 variant
+  char buf[40];
+  std::snprintf(buf, sizeof buf, "%08x-%04x-%04x-%04x-%012llx", static_cast<unsigned>(hi >> 32),
+                static_cast<unsigned>((hi >> 16) & 0xFFFF), static_cast<unsigned>(hi & 0xFFFF),
+                static_cast<unsigned>(lo >> 48), static_cast<unsigned long long>(lo & 0xFFFFFFFFFFFFull));
+  return buf;
+}
+
+// ---------------------------------------------------------------- handlers
+bool MasterCore::native_method(const std::string& m) const {
+  return m == "GetFileInfo" || m == "CreateFile" || m == "AllocateBlock" || m == "CompleteFile" ||
+         m == "ListFiles" || m == "DeleteFile" || m == "GetBlockLocations";
+}
+
+int MasterCore::handle(const std::string& method, const std::string& req, std::string* out) {
+  try {
+    if (method == "GetFileInfo") return get_file_info(req, out);
+    if (method == "CreateFile") return create_file(req, out);
+    if (method == "CompleteFile") return complete_file(req, out);
+    if (method == "AllocateBlock") return allocate_block(req, out);
+    if (method == "ListFiles") return list_files(req, out);
+    if (method == "DeleteFile") return delete_file(req, out);
+    if (method == "GetBlockLocations") return get_block_locations(req, out);
+  } catch (const std::exception& e) {
+    *out = e.what();
+    return INTERNAL;
+  }
+  *out = "unknown method " + method;
+  return UNIMPLEMENTED;
+}
+
+int MasterCore::get_file_info(const std::string& raw, std::string* out) {
+  pb::GetFileInfoRequest r;
+  if (!r.decode(raw)) return (*out = "malformed GetFileInfoRequest", INTERNAL);
+  record_request(r.path);
+  record_access(r.path);
+  int c;
+  if ((c = check_ownership(r.path, out)) != OK) return c;
+  if ((c = read_index(out)) != OK) return c;
+  if (!wait_unlocked(r.path, 5000, out)) return UNAVAILABLE;
+  pb::GetFileInfoResponse resp;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (const pb::FileMetadata* m = visible(r.path)) {
+      resp.metadata = *m;
+      resp.has_metadata = true;
+      resp.found = true;
+    }
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::create_file(const std::string& raw, std::string* out) {
+  pb::CreateFileRequest r;
+  if (!r.decode(raw)) return (*out = "malformed CreateFileRequest", INTERNAL);
+  record_request(r.path);
+  int c;
+  if ((c = check_ownership(r.path, out)) != OK) return c;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (safe_mode_) return (*out = kSafeModeMsg, UNAVAILABLE);
+  }
+  if (!wait_unlocked(r.path, 5000, out)) return UNAVAILABLE;
+  pb::CreateFileResponse resp;
+  auto reply = [&]() {
+    out->clear();
+    resp.encode(*out);
+    return static_cast<int>(OK);
+  };
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (files_.count(r.path) && !under_construction_.count(r.path)) {
+      resp.error_message = "File already exists";
+      return reply();
+    }
+  }
+  raft::Node* node = node_.load();
+  std::vector<std::string> sel;
+  if (r.allocate_block && r.defer_create) {
+    // place the block now; the file appears with its data in CompleteFile{create}: one
+    // Raft entry (one WAL fdatasync) per write instead of two
+    std::string err;
+    if (!place(r.ec_data_shards, r.ec_parity_shards, r.preferred_chunk_server, &sel, &err))
+      return (*out = err, UNAVAILABLE);
+    if (!node || !node->is_leader()) {
+      resp.error_message = "Not Leader";
+      resp.leader_hint = node ? node->leader_address() : "";
+      return reply();
+    }
+    resp.success = true;
+    resp.deferred = true;
+    allocation(new_uuid(), sel, r.ec_parity_shards ? r.ec_data_shards : 0, r.ec_data_shards ? r.ec_parity_shards : 0,
+               &resp.allocation);
+    resp.has_allocation = true;
+    return reply();
+  }
+  Json args = obj({{"path", r.path},
+                   {"ec_data_shards", r.ec_data_shards},
+                   {"ec_parity_shards", r.ec_parity_shards},
+                   {"ts", now_ms()}});
+  std::string block_id;
+  if (r.allocate_block) {
+    // CreateFile + AllocateBlock as ONE Raft entry and one round trip
+    std::string err;
+    if (!place(r.ec_data_shards, r.ec_parity_shards, r.preferred_chunk_server, &sel, &err))
+      return (*out = err, UNAVAILABLE);
+    block_id = new_uuid();
+    Json locs = Json::array();
+    for (auto& s : sel) locs.push_back(s);
+    args.set("block_id", block_id);
+    args.set("locations", locs);
+  }
+  Result res = propose_unlocked("CreateFile", args);
+  if (res.code == 1) {
+    resp.error_message = "Not Leader";
+    resp.leader_hint = res.payload;
+    return reply();
+  }
+  if (res.code != 0) return (*out = res.payload, res.code == 3 ? UNAVAILABLE : INTERNAL);
+  Json j = Json::parse(res.payload);
+  if (j["exists"].as_bool()) {
+    resp.error_message = "File already exists";
+    return reply();
+  }
+  if (j["orphans"].size()) queue_gc(j["orphans"]);
+  resp.success = true;
+  if (r.allocate_block) {
+    int ec_d = 0, ec_p = 0;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = files_.find(r.path);
+      if (it != files_.end()) {
+        ec_d = it->second.ec_data_shards;
+        ec_p = it->second.ec_parity_shards;
+      }
+    }
+    allocation(block_id, sel, ec_d, ec_p, &resp.allocation);
+    resp.has_allocation = true;
+  }
+  return reply();
+}
+
+int MasterCore::allocate_block(const std::string& raw, std::string* out) {
+  pb::AllocateBlockRequest r;
+  if (!r.decode(raw)) return (*out = "malformed AllocateBlockRequest", INTERNAL);
+  record_request(r.path);
+  int c;
+  if ((c = check_ownership(r.path, out)) != OK) return c;
+  int ec_d, ec_p;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (safe_mode_) return (*out = kSafeModeMsg, UNAVAILABLE);
+    auto it = files_.find(r.path);
+    if (it == files_.end()) return (*out = "File not found", NOT_FOUND);
+    ec_d = it->second.ec_data_shards;
+    ec_p = it->second.ec_parity_shards;
+  }
+  std::vector<std::string> sel;
+  std::string err;
+  if (!place(ec_d, ec_p, r.preferred_chunk_server, &sel, &err)) return (*out = err, UNAVAILABLE);
+  std::string block_id = new_uuid();
+  Json locs = Json::array();
+  for (auto& s : sel) locs.push_back(s);
+  Json master = obj({{"AllocateBlock", obj({{"path", r.path}, {"block_id", block_id}, {"locations", locs}})}});
+  Result res = propose(obj({{"Master", master}}));
+  pb::AllocateBlockResponse resp;
+  if (res.code == 1) {
+    resp.leader_hint = res.payload;
+  } else if (res.code != 0) {
+    return (*out = res.payload, INTERNAL);
+  } else {
+    allocation(block_id, sel, ec_d, ec_p, &resp);
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::complete_file(const std::string& raw, std::string* out) {
+  pb::CompleteFileRequest r;
+  if (!r.decode(raw)) return (*out = "malformed CompleteFileRequest", INTERNAL);
+  int c;
+  if ((c = check_ownership(r.path, out)) != OK) return c;
+  Json sums = Json::array();
+  for (auto& s : r.block_checksums)
+    sums.push_back(obj({{"block_id", s.block_id}, {"checksum_crc32c", s.checksum_crc32c}, {"actual_size", s.actual_size}}));
+  Json args = obj({{"path", r.path},
+                   {"size", r.size},
+                   {"etag_md5", r.etag_md5.empty() ? Json() : Json(r.etag_md5)},
+                   {"created_at_ms", r.created_at_ms ? Json(r.created_at_ms) : Json()},
+                   {"block_checksums", sums}});
+  pb::CompleteFileResponse resp;
+  auto not_leader = [&](const std::string& hint) {
+    // CompleteFileResponse has no leader_hint: the read-path status makes clients follow it
+    *out = hint.empty() ? "Not Leader" : "Not Leader|" + hint;
+    return static_cast<int>(FAILED_PRECONDITION);
+  };
+  if (r.create) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (safe_mode_) return (*out = kSafeModeMsg, UNAVAILABLE);
+    }
+    if (!wait_unlocked(r.path, 5000, out)) return UNAVAILABLE;
+    Json blocks = Json::array();
+    for (auto& b : r.blocks) blocks.push_back(block_json(b));
+    args.set("ts", now_ms());
+    args.set("ec_data_shards", r.ec_data_shards);
+    args.set("ec_parity_shards", r.ec_parity_shards);
+    args.set("blocks", blocks);
+    Result res = propose_unlocked("CreateComplete", args);
+    if (res.code == 1) return not_leader(res.payload);
+    if (res.code != 0) return (*out = res.payload, res.code == 3 ? UNAVAILABLE : INTERNAL);
+    Json j = Json::parse(res.payload);
+    if (j["exists"].as_bool()) {
+      pb::FileMetadata tmp;
+      tmp.blocks = r.blocks;
+      queue_gc(block_list(tmp));  // our freshly written replicas belong to nobody
+      resp.error_message = "File already exists";
+    } else {
+      if (j["orphans"].size()) queue_gc(j["orphans"]);
+      resp.success = true;
+    }
+  } else {
+    Result res = propose(obj({{"Master", obj({{"CompleteFile", args}})}}));
+    if (res.code == 1) return not_leader(res.payload);
+    if (res.code != 0) return (*out = res.payload, INTERNAL);
+    resp.success = Json::parse(res.payload)["found"].as_bool(true);
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::list_files(const std::string& raw, std::string* out) {
+  pb::ListFilesRequest r;
+  if (!r.decode(raw)) return (*out = "malformed ListFilesRequest", INTERNAL);
+  int c;
+  if ((c = read_index(out)) != OK) return c;
+  pb::ListFilesResponse resp;
+  resp.files = paths(r.path, true);
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::delete_file(const std::string& raw, std::string* out) {
+  pb::DeleteFileRequest r;
+  if (!r.decode(raw)) return (*out = "malformed DeleteFileRequest", INTERNAL);
+  record_request(r.path);
+  int c;
+  if ((c = check_ownership(r.path, out)) != OK) return c;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (safe_mode_) return (*out = kSafeModeMsg, UNAVAILABLE);
+  }
+  if (!wait_unlocked(r.path, 5000, out)) return UNAVAILABLE;
+  pb::DeleteFileResponse resp;
+  bool exists;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    exists = visible(r.path) != nullptr;
+  }
+  if (!exists) {
+    resp.error_message = "File not found";
+  } else {
+    Result res = propose_unlocked("DeleteFile", obj({{"path", r.path}}));
+    if (res.code == 1) {
+      resp.error_message = "Not Leader";
+      resp.leader_hint = res.payload;
+    } else if (res.code != 0) {
+      return (*out = res.payload, res.code == 3 ? UNAVAILABLE : INTERNAL);
+    } else {
+      Json j = Json::parse(res.payload);
+      if (!j["found"].as_bool(true)) {
+        resp.error_message = "File not found";
+      } else {
+        queue_gc(j["blocks"]);
+        resp.success = true;
+      }
+    }
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::get_block_locations(const std::string& raw, std::string* out) {
+  pb::GetBlockLocationsRequest r;
+  if (!r.decode(raw)) return (*out = "malformed GetBlockLocationsRequest", INTERNAL);
+  int c;
+  if ((c = read_index(out)) != OK) return c;
+  pb::GetBlockLocationsResponse resp;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (pb::BlockInfo* b = find_block_locked(r.block_id, nullptr)) {
+      resp.locations = b->locations;
+      resp.found = true;
+    }
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+}  // namespace dfs

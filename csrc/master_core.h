@@ -1,0 +1,183 @@
+// Native metadata master of one namespace shard: the replicated state machine (C24, C26)
+// and the hot MasterService handlers (C33) — GetFileInfo, CreateFile, AllocateBlock,
+// CompleteFile, ListFiles, DeleteFile, GetBlockLocations — served straight from C++,
+// with rack/GPU-aware placement (C28) and the Raft node (raft.h) underneath.
+//
+// Reference: dfs/metaserver/src/master.rs:195-367 (state, safe mode), :378-432
+// (placement), :2141-2560 (handlers), :2684-2723 (GetBlockLocations), and the command
+// semantics of simple_raft.rs:2995-3398. Behaviour differences, all client-compatible:
+//   * a block_id -> path index makes GetBlockLocations O(1) (reference: linear scan);
+//   * files are invisible until CompleteFile, and CreateFile/Rename decide existence at
+//     apply time, so racing writers cannot both succeed (linearizability);
+//   * paths pinned by an unresolved cross-shard rename make readers and writers wait;
+//   * access statistics (the reference's Raft write per GetFileInfo) are batched into one
+//     UpdateAccessStatsBatch entry per second;
+//   * a deferred create places the block without a Raft entry and creates the file in
+//     CompleteFile{create=true}: one Raft entry (one WAL fdatasync) per write.
+// Status codes and message strings match the reference (REDIRECT:, Not Leader|, safe mode).
+//
+// Threading: the state lives under one mutex. Raft applies on its applier thread; RPCs
+// run on the callers' threads (native local-RPC connections, or gRPC workers through the
+// Python binding) and block only on Raft completions, never while holding the mutex.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <random>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "dfs_pb.h"
+#include "json.h"
+#include "raft.h"
+#include "shard_map.h"
+
+namespace dfs {
+
+struct ChunkServerStatus {
+  std::string address;
+  int64_t last_heartbeat = 0;
+  uint64_t used_space = 0, available_space = 0, chunk_count = 0;
+  std::string rack_id;
+  int32_t gpu_rank = -1;
+  uint64_t hbm_capacity = 0, hbm_used = 0;
+  uint64_t scheduled = 0;  // bytes placed here since the last heartbeat (local only)
+};
+
+// Rack-aware round robin by free space (reference master.rs:378-432); `preferred` (the
+// writer-local chunkserver) is pinned first when live.
+std::vector<std::string> select_servers_rack_aware(const std::vector<ChunkServerStatus>& servers, size_t n,
+                                                   const std::string& preferred);
+
+class MasterCore : public raft::StateMachine {
+ public:
+  enum Code { OK = 0, NOT_FOUND = 5, FAILED_PRECONDITION = 9, INTERNAL = 13, UNAVAILABLE = 14, OUT_OF_RANGE = 11,
+              UNIMPLEMENTED = 12 };
+
+  MasterCore();
+  ~MasterCore() override;
+
+  void attach(raft::Node* node);  // the Raft node proposals go to
+  void detach();
+
+  // raft::StateMachine
+  std::vector<std::string> apply(const std::vector<std::pair<uint64_t, std::string>>& cmds) override;
+  std::string snapshot() override;
+  void restore(const std::string& state) override;
+
+  // Hot RPCs: `method` is the bare MasterService method name. Returns a gRPC status code;
+  // *out holds the serialized response (OK) or the status message.
+  bool native_method(const std::string& method) const;
+  int handle(const std::string& method, const std::string& req, std::string* out);
+
+  // Routing: the shard map (JSON, ShardMap serde layout) and this master's shard id.
+  void set_shard_map(const std::string& json, const std::string& shard_id);
+
+  // Chunkserver registry (local, rebuilt from heartbeats).
+  void upsert_chunk_server(const ChunkServerStatus& st);
+  bool remove_chunk_server(const std::string& addr);
+  std::vector<ChunkServerStatus> chunk_servers() const;
+
+  // Safe mode (reference master.rs:258-367).
+  void enter_safe_mode(bool manual);
+  void exit_safe_mode();
+  bool should_exit_safe_mode() const;
+  void report_blocks(uint64_t n);  // + reported blocks, auto-exit when due
+  Json safe_mode_status() const;
+
+  // Queries for the Python services (serialized FileMetadata / JSON).
+  bool get_file(const std::string& path, bool visible_only, std::string* pb) const;
+  bool contains(const std::string& path) const;
+  bool under_construction(const std::string& path) const;
+  size_t file_count() const;
+  std::vector<std::string> paths(const std::string& prefix, bool visible_only) const;
+  std::vector<std::string> files_pb(const std::string& prefix) const;
+  bool find_block(const std::string& block_id, std::string* file_pb) const;
+  bool has_block(const std::string& block_id) const;
+  uint64_t total_blocks() const;
+  std::string tx_record(const std::string& tx_id) const;  // "" if absent
+  std::string tx_records() const;                          // JSON object
+  std::string tx_lock(const std::string& path) const;      // tx id or ""
+  std::vector<std::string> shuffling_prefixes() const;
+
+  // Drained by the Python side: per-prefix request counts (dynamic sharding monitor) and
+  // blocks no file references any more (DELETE commands for their holders).
+  std::map<std::string, uint64_t> take_request_counts();
+  std::vector<std::pair<std::string, std::vector<std::string>>> take_gc();
+
+  void set_access_stats(bool on, int flush_ms);
+  uint64_t requests() const { return requests_.load(); }
+
+ private:
+  struct Result {  // of a proposal
+    int code;      // 0 ok, 1 not leader (payload = hint), 2 error
+    std::string payload;
+  };
+  Result propose(const Json& cmd);
+  Result propose_unlocked(const std::string& name, const Json& args);  // waits out tx pins
+  int read_index(std::string* err);
+  bool wait_unlocked(const std::string& path, int timeout_ms, std::string* err);
+  int check_ownership(const std::string& path, std::string* err) const;
+  bool place(int ec_d, int ec_p, const std::string& preferred, std::vector<std::string>* out, std::string* err);
+  void allocation(const std::string& block_id, const std::vector<std::string>& sel, int ec_d, int ec_p,
+                  pb::AllocateBlockResponse* a) const;
+  void record_request(const std::string& path);
+  void record_access(const std::string& path);
+  void access_loop();
+  void queue_gc(const Json& blocks);  // [[block_id, [locations]]...]
+  std::string new_uuid();
+
+  int get_file_info(const std::string& req, std::string* out);
+  int create_file(const std::string& req, std::string* out);
+  int allocate_block(const std::string& req, std::string* out);
+  int complete_file(const std::string& req, std::string* out);
+  int list_files(const std::string& req, std::string* out);
+  int delete_file(const std::string& req, std::string* out);
+  int get_block_locations(const std::string& req, std::string* out);
+
+  // state machine helpers (mu_ held)
+  Json apply_one(const std::string& name, const Json& a);
+  void put(const std::string& path, pb::FileMetadata m);
+  bool del(const std::string& path, pb::FileMetadata* out);
+  const pb::FileMetadata* visible(const std::string& path) const;
+  pb::BlockInfo* find_block_locked(const std::string& block_id, pb::FileMetadata** file);
+  void relock(const Json& rec);
+
+  mutable std::mutex mu_;
+  std::condition_variable applied_cv_;
+  // replicated
+  std::unordered_map<std::string, pb::FileMetadata> files_;
+  std::unordered_map<std::string, std::string> block_index_;
+  std::unordered_map<std::string, int64_t> under_construction_;
+  std::map<std::string, Json> tx_records_;
+  std::unordered_map<std::string, std::string> tx_locks_;
+  std::set<std::string> shuffling_prefixes_;
+  // local
+  std::map<std::string, ChunkServerStatus> chunk_servers_;
+  bool safe_mode_ = false, safe_mode_manual_ = false;
+  int64_t safe_mode_entered_at_ = 0;
+  uint64_t expected_blocks_ = 0, reported_blocks_ = 0;
+  double safe_mode_threshold_ = 0.99;
+  ShardMap shard_map_;
+  std::string shard_id_;
+  bool have_map_ = false;
+  std::map<std::string, uint64_t> request_counts_;
+  std::vector<std::pair<std::string, std::vector<std::string>>> gc_;
+  std::map<std::string, uint64_t> access_buf_;
+  bool access_stats_ = true;
+  int access_flush_ms_ = 1000;
+  std::mt19937_64 rng_;
+
+  std::atomic<raft::Node*> node_{nullptr};
+  std::atomic<uint64_t> requests_{0};
+  std::atomic<bool> running_{true};
+  std::condition_variable access_cv_;
+  std::thread access_thread_;
+};
+
+}  // namespace dfs

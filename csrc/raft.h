@@ -67,6 +67,15 @@ struct ClusterConfig {
 //   code 2: failed (payload = message)
 using Done = std::function<void(int code, const std::string& payload)>;
 
+// A state machine implemented natively (master / config state); a Host may delegate to one.
+class StateMachine {
+ public:
+  virtual ~StateMachine() = default;
+  virtual std::vector<std::string> apply(const std::vector<std::pair<uint64_t, std::string>>& cmds) = 0;
+  virtual std::string snapshot() = 0;
+  virtual void restore(const std::string& state) = 0;
+};
+
 class Host {
  public:
   virtual ~Host() = default;

@@ -274,6 +274,7 @@ class MasterBackground:
         m.strategy, m.ranges, m.ring, m.shards, m.shard_peers = new.strategy, new.ranges, new.ring, new.shards, \
             new.shard_peers
         m._dirty()
+        self.svc.sync_routing()
         if not self.svc.shard_id:  # standby master: a SplitShard allocated us a shard
             me = self.svc.advertise_addr
             for sid in m.get_all_shards():

@@ -33,6 +33,7 @@ class ThroughputMonitor:
         self.window = window_secs
         self.last_split_time = time.monotonic() - split_cooldown_secs
         self._lock = threading.Lock()
+        self.source = None  # callable -> {prefix: count}: requests counted by the native handlers
 
     def record_request(self, path: str, nbytes: int = 0) -> None:
         p = path_prefix(path)
@@ -44,7 +45,13 @@ class ThroughputMonitor:
             m.last_bytes += nbytes
 
     def decay_metrics(self) -> None:
+        native_counts = self.source() if self.source is not None else {}
         with self._lock:
+            for p, n in native_counts.items():
+                m = self.metrics.get(p)
+                if m is None:
+                    m = self.metrics[p] = PrefixMetrics()
+                m.last_count += n
             for m in self.metrics.values():
                 m.rps = m.rps * 0.3 + (m.last_count / self.window) * 0.7
                 m.bps = m.bps * 0.3 + (m.last_bytes / self.window) * 0.7

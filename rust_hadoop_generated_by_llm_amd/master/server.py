@@ -20,7 +20,8 @@ from ..raft.node import RaftNode
 from ..raft.transport import HttpTransport
 from ..utils import log as logsetup
 from ..utils.metrics import Registry
-from ..utils.localrpc import serve_local
+from ..native import lib as native
+from ..utils.localrpc import build_dispatch, socket_name
 from ..utils.rpc import AioChannelPool, make_aio_server, server_credentials, with_scheme
 from .background import Intervals, MasterBackground
 from .monitor import ThroughputMonitor
@@ -68,7 +69,7 @@ class MasterProcess:
         self.http_host = args.http_host or host
         self.self_http = f"http://{self.http_host}:{args.http_port}"
         self.client_addr = with_scheme(args.advertise_addr or args.addr)
-        self.state = MasterState()
+        self.state = MasterState()  # facade over the native MasterCore
         peers = [p for p in args.peers.split(",") if p.strip()]
         members = initial_members(args.id, self.self_http, peers)
         ssl_ctx = None
@@ -78,7 +79,8 @@ class MasterProcess:
         self.raft = RaftNode(args.id, members, self.client_addr, os.path.join(args.storage_dir, f"raft_node_{args.id}"),
                              self.state, self.transport, snapshot_threshold=args.snapshot_threshold,
                              sync=not args.no_fsync, backup_s3_endpoint=args.backup_s3_endpoint,
-                             backup_bucket=args.backup_bucket)
+                             backup_bucket=args.backup_bucket, native_sm=self.state.core)
+        self.state.core.attach(self.raft._core)
         self.state.enter_safe_mode()
         self.config_servers = [with_scheme(c) for c in args.config_servers.split(",") if c.strip()]
         if self.config_servers:
@@ -86,6 +88,7 @@ class MasterProcess:
         else:
             self.shard_map = ShardMap.load_config_file(args.shard_config)
         self.monitor = ThroughputMonitor(args.split_threshold_rps, args.merge_threshold_rps, args.split_cooldown_secs)
+        self.monitor.source = self.state.core.take_request_counts
         self.pool = AioChannelPool(args.ca_cert, args.domain_name)
         self.svc = MasterService(self.state, self.raft, self.shard_map, "" if args.standby else args.shard_id,
                                  self.monitor, self.pool,
@@ -110,6 +113,8 @@ class MasterProcess:
         self.metrics.gauge("dfs_master_safe_mode_status", "1 if in safe mode", fn=lambda: int(self.state.safe_mode))
         self.metrics.gauge("dfs_master_files", "files in this shard", fn=lambda: len(self.state.files))
         self.metrics.gauge("dfs_master_chunkservers", "live chunkservers", fn=lambda: len(self.state.chunk_servers))
+        self.metrics.gauge("dfs_master_native_requests", "requests served by the native handlers",
+                           fn=lambda: self.state.core.requests)
 
     def http_app(self) -> web.Application:
         app = web.Application(client_max_size=1 << 30)
@@ -154,11 +159,22 @@ class MasterProcess:
         creds = server_credentials(a.tls_cert, a.tls_key)
         server = make_aio_server({"MasterService": self.svc}, a.addr if ":" in a.addr else f"0.0.0.0:{a.addr}", creds)
         await server.start()
+        self._local_srv = None
         if creds is None and os.environ.get("DFS_NO_LOCALRPC") != "1":
-            try:  # same-host clients skip HTTP/2 (utils/localrpc.py)
-                self._local_srv = await serve_local({"MasterService": self.svc}, a.addr.rsplit(":", 1)[-1])
-            except OSError as e:
-                log.warning("local RPC listener unavailable: %s", e)
+            # same-host clients skip HTTP/2: a native listener serves the hot methods from
+            # MasterCore and hands the rest to the Python handlers on this loop
+            loop = asyncio.get_running_loop()
+            dispatch = build_dispatch({"MasterService": self.svc})
+
+            def fallback(path, rid, payload):
+                return asyncio.run_coroutine_threadsafe(dispatch(path, rid, bytes(payload)), loop).result(120)
+
+            srv = native.MasterLocalServer(socket_name(a.addr.rsplit(":", 1)[-1]), self.state.core, fallback)
+            ok, err = srv.start()
+            if ok:
+                self._local_srv = srv
+            else:
+                log.warning("local RPC listener unavailable: %s", err)
         await self.raft.start()
         if self.config_servers:
             await self.bg.register()
@@ -176,8 +192,11 @@ class MasterProcess:
                 json.dump({"addr": a.addr, "http": self.self_http}, f)
         await stop.wait()
         await self.bg.stop()
+        if self._local_srv is not None:
+            await asyncio.get_running_loop().run_in_executor(None, self._local_srv.stop)
         await server.stop(0.5)
         await self.raft.stop()
+        self.state.core.detach()
         await self.transport.close()
         await self.pool.close()
         await runner.cleanup()

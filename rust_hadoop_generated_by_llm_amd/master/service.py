@@ -10,10 +10,11 @@ same (reference: dfs/metaserver/src/master.rs:2141-3660):
 from __future__ import annotations
 
 import asyncio
+import json
 import logging
 import os
-import time
 import uuid
+from concurrent.futures import ThreadPoolExecutor
 
 from ..models import meta as M
 from ..models import proto as pb
@@ -21,12 +22,12 @@ from ..parallel.sharding import ShardMap
 from ..raft.node import NotLeader, RaftNode
 from ..utils.rpc import AioChannelPool, RpcStatus, StatusCode, rpc_details
 from .monitor import ThroughputMonitor
-from .state import (REPLICATION_FACTOR, SCHEDULE_QUANTUM, ChunkServerStatus, MasterState, now_ms,
-                    select_servers_rack_aware)
+from .state import ChunkServerStatus, MasterState, now_ms
 
 log = logging.getLogger("dfs.master")
 
 SAFE_MODE_MSG = "Cluster is in Safe Mode. Write operations are blocked."
+_CODES = {c.value[0]: c for c in StatusCode}
 
 
 def new_rename_record(tx_id, source_path, dest_path, source_shard, dest_shard, dest_meta) -> dict:
@@ -51,17 +52,16 @@ class MasterService:
                  monitor: ThroughputMonitor, pool: AioChannelPool, *, advertise_addr: str = "",
                  access_stats: bool = True, access_stats_flush_ms: int = 1000):
         self.state = state
+        self.core = state.core
         self.raft = raft
         self.shard_map = shard_map
-        self.shard_id = shard_id
+        self._shard_id = shard_id
+        self._exec = ThreadPoolExecutor(max_workers=16, thread_name_prefix="master-native")
         self.monitor = monitor
         self.pool = pool
         self.advertise_addr = advertise_addr
-        self.access_stats = access_stats
-        self._access_buf: dict[str, int] = {}
-        self._access_flush_ms = access_stats_flush_ms
-        self._access_task: asyncio.Task | None = None
-        self.requests = 0
+        self.core.set_access_stats(access_stats, access_stats_flush_ms)
+        self.sync_routing()
         # set by MasterBackground when config servers exist: a rename decides same-shard
         # vs 2PC from the shard map, so it refreshes a map older than this first
         self.shard_map_refresher = None
@@ -70,6 +70,19 @@ class MasterService:
         # leader-local EC conversion jobs (tiering, C32): source block id ->
         # {"path", "new_id", "targets", "k", "m", "started_ms", "done"}
         self.ec_jobs: dict[str, dict] = {}
+
+    @property
+    def shard_id(self) -> str:
+        return self._shard_id
+
+    @shard_id.setter
+    def shard_id(self, value: str) -> None:
+        self._shard_id = value
+        self.sync_routing()
+
+    def sync_routing(self) -> None:
+        """Push the shard map + our shard id into the native handlers (ownership checks)."""
+        self.core.set_shard_map(json.dumps(self.shard_map.to_json()), self._shard_id)
 
     async def fresh_shard_map(self, force: bool = False) -> None:
         if self.shard_map_refresher is None:
@@ -131,181 +144,37 @@ class MasterService:
             await self.wait_unlocked(res["locked"])
         raise RpcStatus(StatusCode.UNAVAILABLE, f"{name}: path stays locked by cross-shard renames")
 
-    # ------------------------------------------------------------------ access stats
-    def _record_access(self, path: str) -> None:
-        """The reference fires one Raft write per GetFileInfo (master.rs:2187-2209). Same
-        semantics (last_access_ms, access_count) but batched: all reads of a short window
-        become ONE replicated UpdateAccessStatsBatch entry ({path: [ts, count]})."""
-        if not self.access_stats or not self.raft.is_leader():
-            return
-        self._access_buf[path] = self._access_buf.get(path, 0) + 1
-        if self._access_task is None or self._access_task.done():
-            self._access_task = asyncio.get_running_loop().create_task(self._flush_access())
+    # ------------------------------------------------------------------ native hot path
+    async def _native(self, method: str, req, resp_cls):
+        """GetFileInfo / CreateFile / AllocateBlock / CompleteFile / ListFiles / DeleteFile /
+        GetBlockLocations run in the native MasterCore (the same-host RPC listener calls it
+        directly; gRPC requests come through here on a worker thread)."""
+        code, out = await asyncio.get_running_loop().run_in_executor(
+            self._exec, self.core.handle, method, req.SerializeToString())
+        if code != 0:
+            raise RpcStatus(_CODES.get(code, StatusCode.UNKNOWN), out.decode("utf-8", "replace"))
+        return resp_cls.FromString(out)
 
-    async def _flush_access(self) -> None:
-        await asyncio.sleep(self._access_flush_ms / 1000.0)
-        buf, self._access_buf = self._access_buf, {}
-        if buf:
-            t = now_ms()
-            self.raft.propose_nowait({"Master": {"UpdateAccessStatsBatch": {
-                "accessed_at_ms": t, "paths": buf}}})
-
-    # ------------------------------------------------------------------ file operations
     async def get_file_info(self, req, ctx):
-        self.monitor.record_request(req.path)
-        self._record_access(req.path)
-        self.check_shard_ownership(req.path)
-        await self.ensure_linearizable_read()
-        await self.wait_unlocked(req.path)
-        m = self.state.visible(req.path)
-        if m is None:
-            return pb.GetFileInfoResponse(found=False)
-        return pb.GetFileInfoResponse(metadata=m, found=True)
+        return await self._native("GetFileInfo", req, pb.GetFileInfoResponse)
 
     async def create_file(self, req, ctx):
-        self.monitor.record_request(req.path)
-        self.check_shard_ownership(req.path)
-        self.check_safe_mode()
-        await self.wait_unlocked(req.path)
-        if req.path in self.state.files and req.path not in self.state.under_construction:
-            return pb.CreateFileResponse(success=False, error_message="File already exists")
-        args = {"path": req.path, "ec_data_shards": req.ec_data_shards, "ec_parity_shards": req.ec_parity_shards,
-                "ts": now_ms()}
-        selected = None
-        if req.allocate_block and req.defer_create:
-            # extension: place the block now, create the file with its data in CompleteFile
-            # (one Raft entry — one WAL fsync — per write instead of two)
-            selected = self._place(req.ec_data_shards, req.ec_parity_shards, req.preferred_chunk_server)
-            if not self.raft.is_leader():
-                return pb.CreateFileResponse(success=False, error_message="Not Leader",
-                                             leader_hint=self.raft.leader_address or "")
-            return pb.CreateFileResponse(success=True, deferred=True, allocation=self._allocation(
-                str(uuid.uuid4()), selected, req.ec_data_shards if req.ec_parity_shards else 0,
-                req.ec_parity_shards if req.ec_data_shards else 0))
-        if req.allocate_block:
-            # extension: CreateFile + AllocateBlock as ONE Raft entry and one round trip
-            # (the reference client always issues both RPCs back to back)
-            selected = self._place(req.ec_data_shards, req.ec_parity_shards, req.preferred_chunk_server)
-            args.update(block_id=str(uuid.uuid4()), locations=selected)
-        try:
-            res = await self._propose_unlocked("CreateFile", args)
-        except NotLeader as e:
-            return pb.CreateFileResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
-        if isinstance(res, dict):
-            if res.get("exists"):
-                return pb.CreateFileResponse(success=False, error_message="File already exists")
-            if res.get("orphans"):
-                self._queue_block_gc(res["orphans"])
-        if selected is not None:
-            m = self.state.files.get(req.path)
-            ec_d, ec_p = (m.ec_data_shards, m.ec_parity_shards) if m is not None else (0, 0)
-            return pb.CreateFileResponse(success=True, allocation=self._allocation(args["block_id"], selected,
-                                                                                   ec_d, ec_p))
-        return pb.CreateFileResponse(success=True)
+        return await self._native("CreateFile", req, pb.CreateFileResponse)
 
     async def delete_file(self, req, ctx):
-        self.monitor.record_request(req.path)
-        self.check_shard_ownership(req.path)
-        self.check_safe_mode()
-        await self.wait_unlocked(req.path)
-        if self.state.visible(req.path) is None:
-            return pb.DeleteFileResponse(success=False, error_message="File not found")
-        try:
-            res = await self._propose_unlocked("DeleteFile", {"path": req.path})
-        except NotLeader as e:
-            return pb.DeleteFileResponse(success=False, error_message="Not Leader", leader_hint=e.hint)
-        if isinstance(res, dict) and not res.get("found", True):
-            return pb.DeleteFileResponse(success=False, error_message="File not found")
-        self._queue_block_gc(res.get("blocks", []) if isinstance(res, dict) else [])
-        return pb.DeleteFileResponse(success=True)
-
-    def _queue_block_gc(self, blocks) -> None:
-        """Extension: issue DELETE commands for blocks no file references any more (the
-        reference never garbage-collects blocks; proto DELETE is 'future use')."""
-        T = pb.ChunkServerCommand
-        for bid, locs in blocks:
-            if bid in self.state.block_index:
-                continue
-            for loc in locs:
-                self.state.pending_commands.setdefault(loc, []).append(T(type=T.DELETE, block_id=bid))
+        return await self._native("DeleteFile", req, pb.DeleteFileResponse)
 
     async def allocate_block(self, req, ctx):
-        self.monitor.record_request(req.path)
-        self.check_shard_ownership(req.path)
-        self.check_safe_mode()
-        m = self.state.files.get(req.path)
-        if m is None:
-            raise RpcStatus(StatusCode.NOT_FOUND, "File not found")
-        ec_d, ec_p = m.ec_data_shards, m.ec_parity_shards
-        selected = self._place(ec_d, ec_p, req.preferred_chunk_server)
-        block_id = str(uuid.uuid4())
-        try:
-            await self._propose("AllocateBlock", {"path": req.path, "block_id": block_id, "locations": selected})
-        except NotLeader as e:
-            return pb.AllocateBlockResponse(leader_hint=e.hint)
-        return self._allocation(block_id, selected, ec_d, ec_p)
-
-    def _allocation(self, block_id: str, selected: list[str], ec_d: int, ec_p: int):
-        blk = pb.BlockInfo(block_id=block_id, locations=selected, ec_data_shards=ec_d, ec_parity_shards=ec_p)
-        return pb.AllocateBlockResponse(block=blk, chunk_server_addresses=selected, ec_data_shards=ec_d,
-                                        ec_parity_shards=ec_p, master_term=self.raft.current_term)
-
-    def _place(self, ec_d: int, ec_p: int, preferred: str) -> list[str]:
-        """Pick the chunkservers for a new block (rack-aware, writer-local first)."""
-        cands = list(self.state.chunk_servers.items())
-        if ec_d > 0 and ec_p > 0:
-            total = ec_d + ec_p
-            if len(cands) < total:
-                raise RpcStatus(StatusCode.UNAVAILABLE,
-                                f"Need {total} chunk servers for EC({ec_d},{ec_p}), only {len(cands)} available")
-            needed = total
-        else:
-            needed = min(REPLICATION_FACTOR, len(cands))
-        if needed == 0:
-            raise RpcStatus(StatusCode.UNAVAILABLE, "No chunk servers available")
-        preferred = preferred if not (ec_d > 0 and ec_p > 0) else None
-        selected = select_servers_rack_aware(cands, needed, preferred or None)
-        for a in selected:
-            self.state.chunk_servers[a].scheduled += SCHEDULE_QUANTUM
-        return selected
+        return await self._native("AllocateBlock", req, pb.AllocateBlockResponse)
 
     async def complete_file(self, req, ctx):
-        self.check_shard_ownership(req.path)
-        args = {"path": req.path, "size": req.size,
-                "etag_md5": req.etag_md5 or None, "created_at_ms": req.created_at_ms or None,
-                "block_checksums": [M.checksum_to_dict(c) for c in req.block_checksums]}
-        if req.create:
-            self.check_safe_mode()
-            await self.wait_unlocked(req.path)
-            args.update(ts=now_ms(), ec_data_shards=req.ec_data_shards, ec_parity_shards=req.ec_parity_shards,
-                        blocks=[M.block_to_dict(b) for b in req.blocks])
-            try:
-                res = await self._propose_unlocked("CreateComplete", args)
-            except NotLeader as e:
-                raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"Not Leader|{e.hint}" if e.hint else "Not Leader")
-            if isinstance(res, dict) and res.get("exists"):
-                self._queue_block_gc([(b.block_id, list(b.locations)) for b in req.blocks])
-                return pb.CompleteFileResponse(success=False, error_message="File already exists")
-            if isinstance(res, dict) and res.get("orphans"):
-                self._queue_block_gc(res["orphans"])
-            return pb.CompleteFileResponse(success=True)
-        try:
-            res = await self._propose("CompleteFile", args)
-        except NotLeader as e:
-            # CompleteFileResponse has no leader_hint field: use the read-path status so
-            # clients follow the hint instead of failing the whole write
-            raise RpcStatus(StatusCode.FAILED_PRECONDITION, f"Not Leader|{e.hint}" if e.hint else "Not Leader")
-        return pb.CompleteFileResponse(success=not (isinstance(res, dict) and not res.get("found", True)))
+        return await self._native("CompleteFile", req, pb.CompleteFileResponse)
 
     async def list_files(self, req, ctx):
-        await self.ensure_linearizable_read()
-        prefix = req.path
-        uc = self.state.under_construction
-        if not prefix:
-            files = [p for p in self.state.files if p not in uc]
-        else:
-            files = [p for p in self.state.files if p.startswith(prefix) and p not in uc]
-        return pb.ListFilesResponse(files=files)
+        return await self._native("ListFiles", req, pb.ListFilesResponse)
+
+    async def get_block_locations(self, req, ctx):
+        return await self._native("GetBlockLocations", req, pb.GetBlockLocationsResponse)
 
     async def register_chunk_server(self, req, ctx):
         self.state.chunk_servers[req.address] = ChunkServerStatus(
@@ -344,15 +213,9 @@ class MasterService:
             for bid in req.bad_blocks:
                 st.bad_block_locations.setdefault(bid, set()).add(addr)
             st.heal_under_replicated_blocks()
+        st.drain_gc()
         cmds = st.pending_commands.pop(addr, [])
         return pb.HeartbeatResponse(success=True, commands=cmds, master_term=self.raft.current_term)
-
-    async def get_block_locations(self, req, ctx):
-        await self.ensure_linearizable_read()
-        _, b = self.state.find_block(req.block_id)
-        if b is None:
-            return pb.GetBlockLocationsResponse(found=False)
-        return pb.GetBlockLocationsResponse(locations=list(b.locations), found=True)
 
     # ------------------------------------------------------------------ rename / 2PC
     async def rename(self, req, ctx):

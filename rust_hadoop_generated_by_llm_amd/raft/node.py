@@ -6,10 +6,11 @@ reference dfs/metaserver/src/simple_raft.rs). This module only adapts it to the 
 services:
 
 * proposals / ReadIndex return asyncio futures completed from native threads;
-* the state machine stays a Python object for the services that still keep their state
-  in Python — its ``apply``/``snapshot``/``restore`` always run on the event loop thread
-  (the native applier hands a committed batch over and waits), so service code never
-  races the state machine;
+* the state machine is either native (``native_sm``: the master's MasterCore, applied on
+  the Raft applier thread without the GIL) or a Python object (config server, tests),
+  whose ``apply``/``snapshot``/``restore`` always run on the event loop thread (the
+  native applier hands a committed batch over and waits), so service code never races
+  the state machine;
 * peer RPCs go out through the asyncio transport (HTTP/JSON or the in-process fault
   injector of the tests), incoming ones run the native handler on a worker thread.
 """
@@ -157,7 +158,7 @@ class RaftNode:
                  state_machine: StateMachine, transport, *, snapshot_threshold: int = 10000,
                  election_timeout: tuple[float, float] = (1.5, 3.0), heartbeat_interval: float = 0.1,
                  sync: bool = True, backup_s3_endpoint: str | None = None, backup_bucket: str = "dfs-backups",
-                 max_append_batch: int = 512):
+                 max_append_batch: int = 512, native_sm=None):
         self.id = node_id
         self.client_address = client_address
         self.dir = storage_dir
@@ -173,7 +174,7 @@ class RaftNode:
         self._core = native.RaftNode(
             node_id, {int(k): v for k, v in members.items()}, client_address, storage_dir, self._host,
             election_timeout[0], election_timeout[1], heartbeat_interval, sync, snapshot_threshold,
-            max_append_batch, backup_s3_endpoint or "", backup_bucket)
+            max_append_batch, backup_s3_endpoint or "", backup_bucket, native_sm)
         self.wal = _Wal(self._core)
         self._rpc = ThreadPoolExecutor(max_workers=4, thread_name_prefix=f"raft-rpc-{node_id}")
         self._running = False

@@ -80,8 +80,11 @@ class _Abort(Exception):
         self.code, self.details = code, details
 
 
-async def serve_local(services: dict, port: int | str):
-    """Start the UNIX-socket listener for ``services`` ({service name: impl})."""
+def build_dispatch(services: dict):
+    """``async dispatch(path, request_id, payload) -> (grpc code, response or message bytes)``
+    over the service handlers ({service name: impl}); shared by the Python listener below
+    and the native one (csrc/localrpc.cpp), which forwards the methods it does not serve
+    itself."""
     from .rpc import RpcStatus, current_request_id, snake
 
     table = {}
@@ -91,6 +94,33 @@ async def serve_local(services: dict, port: int | str):
             if fn is not None:
                 table[pb.method_path(sname, mname)] = (fn, req_cls, inspect.iscoroutinefunction(fn))
     ctx = _AbortCtx()
+
+    async def dispatch(path: str, rid: str, payload: bytes) -> tuple[int, bytes]:
+        ent = table.get(path)
+        if ent is None:
+            return grpc.StatusCode.UNIMPLEMENTED.value[0], f"unknown method {path}".encode()
+        fn, req_cls, is_async = ent
+        token = current_request_id.set(rid)
+        try:
+            req = req_cls.FromString(payload)
+            resp = (await fn(req, ctx)) if is_async else fn(req, ctx)
+            return 0, resp.SerializeToString()
+        except RpcStatus as e:
+            return e.code.value[0], e.message.encode()
+        except _Abort as e:
+            return e.code.value[0], str(e.details).encode()
+        except Exception as e:  # noqa: BLE001
+            log.exception("local rpc %s failed", path)
+            return grpc.StatusCode.INTERNAL.value[0], str(e).encode()
+        finally:
+            current_request_id.reset(token)
+
+    return dispatch
+
+
+async def serve_local(services: dict, port: int | str):
+    """Start the UNIX-socket listener for ``services`` ({service name: impl})."""
+    dispatch = build_dispatch(services)
 
     async def handle(reader: asyncio.StreamReader, writer: asyncio.StreamWriter):
         try:
@@ -102,26 +132,8 @@ async def serve_local(services: dict, port: int | str):
                 path = body[2:2 + pl].decode()
                 (rl,) = struct.unpack_from("<H", body, 2 + pl)
                 rid = body[4 + pl:4 + pl + rl].decode()
-                payload = body[4 + pl + rl:]
-                ent = table.get(path)
-                if ent is None:
-                    out = bytes([grpc.StatusCode.UNIMPLEMENTED.value[0]]) + f"unknown method {path}".encode()
-                else:
-                    fn, req_cls, is_async = ent
-                    token = current_request_id.set(rid)
-                    try:
-                        req = req_cls.FromString(payload)
-                        resp = (await fn(req, ctx)) if is_async else fn(req, ctx)
-                        out = b"\x00" + resp.SerializeToString()
-                    except RpcStatus as e:
-                        out = bytes([e.code.value[0]]) + e.message.encode()
-                    except _Abort as e:
-                        out = bytes([e.code.value[0]]) + str(e.details).encode()
-                    except Exception as e:  # noqa: BLE001
-                        log.exception("local rpc %s failed", path)
-                        out = bytes([grpc.StatusCode.INTERNAL.value[0]]) + str(e).encode()
-                    finally:
-                        current_request_id.reset(token)
+                code, data = await dispatch(path, rid, body[4 + pl + rl:])
+                out = bytes([code]) + data
                 writer.write(struct.pack("<I", len(out)) + out)
                 await writer.drain()
         except (asyncio.IncompleteReadError, ConnectionError):
