@@ -6,6 +6,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstring>
+
+#include "client_fast.h"
 #include "dfs_pb.h"
 #include "localrpc.h"
 #include "master_core.h"
@@ -314,4 +317,53 @@ void bind_meta(py::module_& m) {
       })
       .def("stop", &LocalRpcServer::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("requests", &LocalRpcServer::requests);
+
+  // ---------------- native client data path (co-located writers/readers)
+  py::class_<FastClient>(m, "FastClient")
+      .def(py::init<std::string, std::string, size_t, size_t, int>(), py::arg("fastpath_socket"),
+           py::arg("local_chunkserver"), py::arg("arena_bytes") = 256u << 20, py::arg("slot_bytes") = 16u << 20,
+           py::arg("hash_threads") = 8)
+      .def_property_readonly("ok", &FastClient::ok)
+      .def_property_readonly("arena_path", &FastClient::arena_path)
+      .def_property_readonly("writes", &FastClient::writes)
+      .def_property_readonly("reads", &FastClient::reads)
+      .def("set_routing", &FastClient::set_routing, py::call_guard<py::gil_scoped_release>())
+      .def("write", [](FastClient& c, const std::string& path, py::buffer data) {
+        py::buffer_info bi = data.request();
+        int replicas = 0;
+        std::string msg;
+        FastClient::Times t;
+        FastClient::Status st;
+        {
+          py::gil_scoped_release r;
+          st = c.write(path, static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize),
+                       &replicas, &msg, &t);
+        }
+        return py::make_tuple(static_cast<int>(st), replicas, msg,
+                              py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete));
+      })
+      .def("read", [](FastClient& c, const std::string& path) {
+        int64_t slot = -1;
+        uint64_t n = 0;
+        std::string msg;
+        FastClient::Times t;
+        FastClient::Status st;
+        {
+          py::gil_scoped_release r;
+          st = c.read(path, &slot, &n, &msg, &t);
+        }
+        py::object data = py::none();
+        if (st == FastClient::Ok) {
+          PyObject* o = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(n));
+          if (!o) throw py::error_already_set();
+          data = py::reinterpret_steal<py::object>(o);
+          char* dst = PyBytes_AS_STRING(o);
+          {
+            py::gil_scoped_release r;  // the new object is not visible to anyone else yet
+            if (n) std::memcpy(dst, c.slot_ptr(slot), n);
+            if (slot >= 0) c.release(slot);
+          }
+        }
+        return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
+      });
 }

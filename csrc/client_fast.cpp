@@ -1,0 +1,472 @@
+#include "client_fast.h"
+
+#include <fcntl.h>
+#include <openssl/evp.h>
+#include <sys/mman.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstddef>
+#include <cstring>
+#include <future>
+#include <random>
+
+#include "crc32.h"
+#include "dfs_pb.h"
+
+namespace dfs {
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+double since(Clock::time_point& t) {
+  auto now = Clock::now();
+  double d = std::chrono::duration<double>(now - t).count();
+  t = now;
+  return d;
+}
+
+int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+std::string strip_scheme(const std::string& a) {
+  auto p = a.find("://");
+  std::string s = p == std::string::npos ? a : a.substr(p + 3);
+  while (!s.empty() && s.back() == '/') s.pop_back();
+  return s;
+}
+
+// "http://127.0.0.1:50051" -> "dfs_rpc_50051" for loopback targets, else "".
+std::string local_rpc_name(const std::string& addr) {
+  if (addr.rfind("https://", 0) == 0) return "";
+  std::string a = strip_scheme(addr);
+  auto colon = a.rfind(':');
+  if (colon == std::string::npos) return "";
+  std::string host = a.substr(0, colon), port = a.substr(colon + 1);
+  if (host != "127.0.0.1" && host != "localhost" && host != "::1" && host != "[::1]") return "";
+  if (port.empty() || port.find_first_not_of("0123456789") != std::string::npos) return "";
+  return "dfs_rpc_" + port;
+}
+
+int connect_abstract(const std::string& name) {
+  int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -1;
+  sockaddr_un sa{};
+  sa.sun_family = AF_UNIX;
+  if (name.size() + 1 > sizeof(sa.sun_path)) {
+    ::close(fd);
+    return -1;
+  }
+  std::memcpy(sa.sun_path + 1, name.data(), name.size());
+  socklen_t len = static_cast<socklen_t>(offsetof(sockaddr_un, sun_path) + 1 + name.size());
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), len) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  timeval tv{120, 0};
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+  return fd;
+}
+
+bool send_all(int fd, const std::string& s) {
+  const char* p = s.data();
+  size_t n = s.size();
+  while (n) {
+    ssize_t r = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += r;
+    n -= static_cast<size_t>(r);
+  }
+  return true;
+}
+
+bool recv_all(int fd, void* buf, size_t n) {
+  auto* p = static_cast<char*>(buf);
+  while (n) {
+    ssize_t r = ::recv(fd, p, n, 0);
+    if (r == 0) return false;
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += r;
+    n -= static_cast<size_t>(r);
+  }
+  return true;
+}
+
+template <class T>
+void put(std::string& s, T v) {
+  s.append(reinterpret_cast<const char*>(&v), sizeof v);
+}
+
+void put_str(std::string& s, const std::string& v) {
+  put<uint16_t>(s, static_cast<uint16_t>(v.size()));
+  s += v;
+}
+
+std::string md5_hex(const uint8_t* p, size_t n) {
+  unsigned char d[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  EVP_Digest(p, n, d, &len, EVP_md5(), nullptr);
+  static const char* hx = "0123456789abcdef";
+  std::string out;
+  for (unsigned i = 0; i < len; ++i) {
+    out.push_back(hx[d[i] >> 4]);
+    out.push_back(hx[d[i] & 15]);
+  }
+  return out;
+}
+
+constexpr int kOutOfRange = 11, kFailedPrecondition = 9, kUnavailable = 14, kNotFound = 5;
+
+}  // namespace
+
+FastClient::FastClient(std::string fastpath_socket, std::string local_chunkserver, size_t arena_bytes,
+                       size_t slot_bytes, int hash_threads)
+    : fp_socket_(std::move(fastpath_socket)), local_cs_(strip_scheme(local_chunkserver)), slot_bytes_(slot_bytes) {
+  arena_bytes_ = std::max(slot_bytes, arena_bytes / slot_bytes * slot_bytes);
+  std::random_device rd;
+  char name[96];
+  std::snprintf(name, sizeof name, "/dev/shm/dfs_sc_%d_n%08x", static_cast<int>(::getpid()), rd());
+  int fd = ::open(name, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
+  if (fd >= 0) {
+    if (::ftruncate(fd, static_cast<off_t>(arena_bytes_)) == 0) {
+      void* p = ::mmap(nullptr, arena_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      if (p != MAP_FAILED) {
+        base_ = static_cast<uint8_t*>(p);
+        arena_path_ = name;
+      }
+    }
+    ::close(fd);
+    if (!base_) ::unlink(name);
+  }
+  for (int64_t off = 0; off + static_cast<int64_t>(slot_bytes_) <= static_cast<int64_t>(arena_bytes_);
+       off += static_cast<int64_t>(slot_bytes_))
+    free_slots_.push_back(off);
+  for (int i = 0; i < std::max(1, hash_threads); ++i) hashers_.emplace_back([this] { hash_loop(); });
+}
+
+FastClient::~FastClient() {
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    stop_ = true;
+  }
+  q_cv_.notify_all();
+  for (auto& t : hashers_) t.join();
+  {
+    std::lock_guard<std::mutex> g(conn_mu_);
+    for (auto& kv : idle_)
+      for (int fd : kv.second) ::close(fd);
+    idle_.clear();
+  }
+  if (base_) {
+    ::munmap(base_, arena_bytes_);
+    ::unlink(arena_path_.c_str());
+  }
+}
+
+void FastClient::hash_loop() {
+  for (;;) {
+    std::function<void()> job;
+    {
+      std::unique_lock<std::mutex> lk(q_mu_);
+      q_cv_.wait(lk, [&] { return stop_ || !queue_.empty(); });
+      if (queue_.empty()) return;
+      job = std::move(queue_.front());
+      queue_.pop_front();
+    }
+    job();
+  }
+}
+
+void FastClient::set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters) {
+  ShardMap m = shard_map_json.empty() ? ShardMap::new_range() : ShardMap::from_json(Json::parse(shard_map_json));
+  std::lock_guard<std::mutex> g(route_mu_);
+  map_ = std::move(m);
+  have_map_ = !shard_map_json.empty();
+  masters_ = masters;
+}
+
+std::string FastClient::master_socket(const std::string& path) {
+  std::lock_guard<std::mutex> g(route_mu_);
+  std::string addr;
+  if (have_map_) {
+    std::string shard = map_.get_shard(path);
+    const auto* peers = shard.empty() ? nullptr : map_.peers(shard);
+    if (peers && !peers->empty()) addr = peers->front();
+  }
+  if (addr.empty() && !masters_.empty()) addr = masters_.front();
+  return addr.empty() ? std::string() : local_rpc_name(addr);
+}
+
+int64_t FastClient::acquire(size_t n) {
+  if (!base_ || n > slot_bytes_) return -1;
+  std::unique_lock<std::mutex> lk(slot_mu_);
+  if (!slot_cv_.wait_for(lk, std::chrono::seconds(5), [&] { return !free_slots_.empty(); })) return -1;
+  int64_t s = free_slots_.back();
+  free_slots_.pop_back();
+  return s;
+}
+
+void FastClient::release(int64_t slot) {
+  {
+    std::lock_guard<std::mutex> g(slot_mu_);
+    free_slots_.push_back(slot);
+  }
+  slot_cv_.notify_one();
+}
+
+int FastClient::take_conn(const std::string& name) {
+  {
+    std::lock_guard<std::mutex> g(conn_mu_);
+    auto& v = idle_[name];
+    if (!v.empty()) {
+      int fd = v.back();
+      v.pop_back();
+      return fd;
+    }
+  }
+  return connect_abstract(name);
+}
+
+void FastClient::give_conn(const std::string& name, int fd) {
+  std::lock_guard<std::mutex> g(conn_mu_);
+  idle_[name].push_back(fd);
+}
+
+bool FastClient::call(const std::string& sock, const std::string& method_path, const std::string& req, int* code,
+                      std::string* resp) {
+  int fd = take_conn(sock);
+  if (fd < 0) return false;
+  std::string msg;
+  msg.reserve(8 + method_path.size() + req.size());
+  put<uint32_t>(msg, static_cast<uint32_t>(2 + method_path.size() + 2 + req.size()));
+  put_str(msg, method_path);
+  put<uint16_t>(msg, 0);  // request id: none
+  msg += req;
+  uint32_t n = 0;
+  if (!send_all(fd, msg) || !recv_all(fd, &n, 4) || n == 0 || n > (1u << 30)) {
+    ::close(fd);
+    return false;
+  }
+  resp->resize(n);
+  if (!recv_all(fd, resp->data(), n)) {
+    ::close(fd);
+    return false;
+  }
+  give_conn(sock, fd);
+  *code = static_cast<uint8_t>((*resp)[0]);
+  resp->erase(0, 1);
+  return true;
+}
+
+bool FastClient::fp_call(uint8_t op, const std::string& body, uint8_t* status, uint64_t* total, uint64_t* nbytes,
+                         std::string* msg) {
+  int fd = take_conn(fp_socket_);
+  if (fd < 0) return false;
+  std::string req;
+  put<uint32_t>(req, static_cast<uint32_t>(body.size() + 1));
+  req.push_back(static_cast<char>(op));
+  req += body;
+  uint32_t n = 0;
+  std::string resp;
+  if (!send_all(fd, req) || !recv_all(fd, &n, 4) || n < 19 || n > (1u << 20)) {
+    ::close(fd);
+    return false;
+  }
+  resp.resize(n);
+  if (!recv_all(fd, resp.data(), n)) {
+    ::close(fd);
+    return false;
+  }
+  give_conn(fp_socket_, fd);
+  *status = static_cast<uint8_t>(resp[0]);
+  std::memcpy(total, resp.data() + 1, 8);
+  std::memcpy(nbytes, resp.data() + 9, 8);
+  uint16_t ml;
+  std::memcpy(&ml, resp.data() + 17, 2);
+  msg->assign(resp, 19, std::min<size_t>(ml, resp.size() - 19));
+  return true;
+}
+
+FastClient::Status FastClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
+                                     std::string* msg, Times* t) {
+  if (!base_ || n > slot_bytes_) return NotHandled;
+  std::string sock = master_socket(path);
+  if (sock.empty()) return NotHandled;
+  auto clk = Clock::now();
+  // MD5 (the ETag) is a sequential chain and only CompleteFile needs it: hash on a worker
+  // while the create RPC, the CRC and the block transfer run here
+  auto md5_task = std::make_shared<std::packaged_task<std::string()>>([data, n] { return md5_hex(data, n); });
+  std::future<std::string> md5 = md5_task->get_future();
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    queue_.emplace_back([md5_task] { (*md5_task)(); });
+  }
+  q_cv_.notify_one();
+  struct Join {  // never return while the worker still reads the caller's buffer
+    std::future<std::string>& f;
+    ~Join() {
+      if (f.valid()) f.wait();
+    }
+  } join{md5};
+  uint32_t crc = crc32(data, n);
+  t->crc = since(clk);
+
+  pb::CreateFileRequest creq;
+  creq.path = path;
+  creq.allocate_block = true;
+  creq.defer_create = true;
+  creq.preferred_chunk_server = local_cs_;
+  int code;
+  std::string raw;
+  if (!call(sock, "/dfs.MasterService/CreateFile", creq.str(), &code, &raw)) return NotHandled;
+  if (code == kOutOfRange || code == kFailedPrecondition || code == kUnavailable) return NotHandled;
+  if (code != 0) {
+    *msg = "Failed to create file: " + raw;
+    return Failed;
+  }
+  pb::CreateFileResponse cresp;
+  if (!cresp.decode(raw)) return NotHandled;
+  if (!cresp.success) {
+    if (cresp.error_message == "Not Leader") return NotHandled;
+    *msg = "Failed to create file: " + cresp.error_message;
+    return Failed;
+  }
+  if (!cresp.has_allocation || !cresp.allocation.has_block) return NotHandled;
+  const pb::AllocateBlockResponse& alloc = cresp.allocation;
+  if (alloc.chunk_server_addresses.empty()) {
+    *msg = "No chunk servers available";
+    return Failed;
+  }
+  if (!cresp.deferred || strip_scheme(alloc.chunk_server_addresses[0]) != local_cs_)
+    return NotHandled;  // nothing was recorded yet: the Python path redoes it
+  t->create = since(clk);
+
+  int64_t slot = acquire(n);
+  if (slot < 0) return NotHandled;
+  std::memcpy(base_ + slot, data, n);
+  std::string body;
+  put<uint64_t>(body, alloc.master_term);
+  put<uint32_t>(body, crc);
+  put<uint64_t>(body, static_cast<uint64_t>(slot));
+  put<uint64_t>(body, n);
+  put_str(body, alloc.block.block_id);
+  put_str(body, arena_path_);
+  if (alloc.chunk_server_addresses.size() > 1) {
+    put<uint16_t>(body, static_cast<uint16_t>(alloc.chunk_server_addresses.size() - 1));
+    for (size_t i = 1; i < alloc.chunk_server_addresses.size(); ++i)
+      put_str(body, strip_scheme(alloc.chunk_server_addresses[i]));
+  }
+  uint8_t st;
+  uint64_t total, written;
+  std::string fmsg;
+  bool sent = fp_call(1, body, &st, &total, &written, &fmsg);
+  release(slot);
+  if (!sent) return NotHandled;
+  if (st == 5 || st == 4) {  // fenced / I/O error: what the gRPC path would report
+    *msg = "Failed to write block: " + fmsg;
+    return Failed;
+  }
+  if (st != 0) return NotHandled;
+  *replicas = static_cast<int>(written);
+  t->write = since(clk);
+
+  pb::CompleteFileRequest done;
+  done.path = path;
+  done.size = n;
+  done.etag_md5 = md5.get();
+  t->md5_wait = since(clk);
+  done.created_at_ms = static_cast<uint64_t>(now_ms());
+  pb::BlockChecksumInfo sum;
+  sum.block_id = alloc.block.block_id;
+  sum.checksum_crc32c = crc;
+  sum.actual_size = n;
+  done.block_checksums.push_back(sum);
+  done.create = true;
+  done.ec_data_shards = alloc.ec_data_shards;
+  done.ec_parity_shards = alloc.ec_parity_shards;
+  done.blocks.push_back(alloc.block);
+  if (!call(sock, "/dfs.MasterService/CompleteFile", done.str(), &code, &raw)) {
+    *msg = "Failed to complete file: master connection lost";
+    return Failed;
+  }
+  if (code != 0) {
+    *msg = "Failed to complete file: " + raw;
+    return Failed;
+  }
+  pb::CompleteFileResponse dresp;
+  dresp.decode(raw);
+  if (!dresp.success) {
+    *msg = dresp.error_message.empty() ? "Failed to complete file" : "Failed to create file: " + dresp.error_message;
+    return Failed;
+  }
+  t->complete = since(clk);
+  writes_++;
+  return Ok;
+}
+
+FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg,
+                                    Times* t) {
+  if (!base_) return NotHandled;
+  std::string sock = master_socket(path);
+  if (sock.empty()) return NotHandled;
+  auto clk = Clock::now();
+  pb::GetFileInfoRequest req;
+  req.path = path;
+  int code;
+  std::string raw;
+  if (!call(sock, "/dfs.MasterService/GetFileInfo", req.str(), &code, &raw)) return NotHandled;
+  if (code != 0) return code == kNotFound ? (*msg = raw, Failed) : NotHandled;
+  pb::GetFileInfoResponse info;
+  if (!info.decode(raw)) return NotHandled;
+  if (!info.found) {
+    *msg = "File not found";
+    return Failed;
+  }
+  t->getinfo = since(clk);
+  const pb::FileMetadata& m = info.metadata;
+  if (m.size == 0) {
+    *slot = -1;
+    *n = 0;
+    return Ok;
+  }
+  if (m.blocks.size() != 1 || m.blocks[0].ec_data_shards > 0 || m.size > slot_bytes_) return NotHandled;
+  const pb::BlockInfo& b = m.blocks[0];
+  bool local = false;
+  for (auto& l : b.locations) local |= strip_scheme(l) == local_cs_;
+  if (!local) return NotHandled;
+  int64_t s = acquire(slot_bytes_);
+  if (s < 0) return NotHandled;
+  std::string body;
+  put<uint64_t>(body, 0);  // offset
+  put<uint64_t>(body, 0);  // length 0 = the whole block
+  put<uint64_t>(body, static_cast<uint64_t>(s));
+  put<uint64_t>(body, slot_bytes_);
+  put_str(body, b.block_id);
+  put_str(body, arena_path_);
+  uint8_t st;
+  uint64_t total, got;
+  std::string fmsg;
+  if (!fp_call(2, body, &st, &total, &got, &fmsg) || (st != 0 && st != 8)) {
+    release(s);
+    return NotHandled;  // corrupt / missing here: the Python path recovers from a replica
+  }
+  t->read = since(clk);
+  *slot = s;
+  *n = got;
+  reads_++;
+  return Ok;
+}
+
+}  // namespace dfs

@@ -1,0 +1,95 @@
+// Native client data path for co-located writers/readers (C46-C48 hot path): the whole
+// `create_file_from_buffer` / `get_file_content` sequence of the reference client
+// (dfs/client/src/mod.rs:225-494, 856-917) runs in C++ without the GIL:
+//
+//   write: CRC-32 (PCLMUL) + MD5 on a worker thread, overlapped with
+//          CreateFile{allocate, deferred} -> shared-memory slot -> ChunkServer fast path
+//          (the server chains the replicas over RCCL/xGMI) -> CompleteFile{create}
+//   read:  GetFileInfo -> ChunkServer fast path DMAs the block from HBM into our slot
+//
+// Metadata RPCs go to the shard's master over its same-host socket (localrpc.h) with the
+// generated proto3 codec; the payload travels through a /dev/shm arena that the
+// chunkserver maps (utils/shm.py protocol). Anything this path does not own — a remote or
+// non-leader master, a redirect, EC files, multi-block files, a remote chain head —
+// returns NotHandled and the Python client takes over, so semantics never change.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "shard_map.h"
+
+namespace dfs {
+
+class FastClient {
+ public:
+  enum Status { Ok = 0, NotHandled = 1, Failed = 2 };
+  struct Times {  // seconds, per phase (benchmark breakdown)
+    double crc = 0, create = 0, write = 0, md5_wait = 0, complete = 0, getinfo = 0, read = 0;
+  };
+
+  FastClient(std::string fastpath_socket, std::string local_chunkserver, size_t arena_bytes, size_t slot_bytes,
+             int hash_threads);
+  ~FastClient();
+  bool ok() const { return base_ != nullptr; }
+  const std::string& arena_path() const { return arena_path_; }
+
+  // Routing: shard map (serde JSON, "" = none) and the fallback master list.
+  void set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters);
+
+  Status write(const std::string& path, const uint8_t* data, size_t n, int* replicas, std::string* msg, Times* t);
+  // On Ok the block sits in slot `*slot` (`*n` bytes); the caller copies it out and calls
+  // release(*slot).
+  Status read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg, Times* t);
+  const uint8_t* slot_ptr(int64_t slot) const { return base_ + slot; }
+  void release(int64_t slot);
+
+  uint64_t writes() const { return writes_.load(); }
+  uint64_t reads() const { return reads_.load(); }
+
+ private:
+  int64_t acquire(size_t n);
+  std::string master_socket(const std::string& path);
+  // one request/response on a pooled connection; false on a transport error
+  bool call(const std::string& sock, const std::string& method_path, const std::string& req, int* code,
+            std::string* resp);
+  bool fp_call(uint8_t op, const std::string& body, uint8_t* status, uint64_t* total, uint64_t* nbytes,
+               std::string* msg);
+  int take_conn(const std::string& name);
+  void give_conn(const std::string& name, int fd);
+  void hash_loop();
+
+  std::string fp_socket_, local_cs_, arena_path_;
+  uint8_t* base_ = nullptr;
+  size_t arena_bytes_ = 0, slot_bytes_ = 0;
+
+  std::mutex slot_mu_;
+  std::condition_variable slot_cv_;
+  std::vector<int64_t> free_slots_;
+
+  std::mutex route_mu_;
+  ShardMap map_;
+  bool have_map_ = false;
+  std::vector<std::string> masters_;
+
+  std::mutex conn_mu_;
+  std::map<std::string, std::vector<int>> idle_;
+
+  // MD5 workers (the etag is a strictly sequential hash: overlap it with the RPCs)
+  std::mutex q_mu_;
+  std::condition_variable q_cv_;
+  std::deque<std::function<void()>> queue_;
+  std::vector<std::thread> hashers_;
+  bool stop_ = false;
+
+  std::atomic<uint64_t> writes_{0}, reads_{0};
+};
+
+}  // namespace dfs

@@ -15,6 +15,7 @@ MI355X-native differences:
 from __future__ import annotations
 
 import hashlib
+import json
 import logging
 import os
 import threading
@@ -88,6 +89,15 @@ class Client:
         # extension simply create the file in CreateFile as before)
         self.defer_create = os.environ.get("DFS_DEFER_CREATE", "1") == "1"
         self._deferred: set[str] = set()
+        # native client data path (csrc/client_fast.cpp): whole writes/reads of single-block
+        # files through a co-located chunkserver and same-host masters, without the GIL
+        self._fast = None
+        if (self.fastpath is not None and self.defer_create and not self.tls
+                and os.environ.get("DFS_NATIVE_CLIENT", "1") == "1"):
+            fc = _native.FastClient(self.fastpath.name, self.local_chunkserver)
+            if fc.ok:
+                self._fast = fc
+                self._sync_fast()
 
     def _phase(self, name: str, t0: float) -> float:
         t1 = time.perf_counter()
@@ -139,9 +149,17 @@ class Client:
     def set_shard_map(self, m: ShardMap) -> None:
         with self._map_lock:
             self.shard_map = m
+        self._sync_fast()
+
+    def _sync_fast(self) -> None:
+        if self._fast is not None:
+            with self._map_lock:
+                js = json.dumps(self.shard_map.to_json()) if self.shard_map.shards else ""
+            self._fast.set_routing(js, [self.resolve_url(a) for a in self.master_addrs])
 
     def add_host_alias(self, alias: str, real: str) -> None:
         self.host_aliases[alias] = real
+        self._fast = None  # aliases rewrite addresses: keep every call on the Python path
 
     def resolve_url(self, url: str) -> str:
         for alias, real in self.host_aliases.items():
@@ -150,6 +168,7 @@ class Client:
         return url
 
     def close(self) -> None:
+        self._fast = None  # unmaps and unlinks the native client's shared-memory arena
         self.pool.close()
         self._exec.shutdown(wait=False)
         if self._arena is not None:
@@ -340,6 +359,18 @@ class Client:
     def create_file_from_buffer(self, data: bytes, dest: str) -> int:
         """CreateFile -> AllocateBlock -> WriteBlock(chain) -> CompleteFile. Returns
         replicas_written (reference mod.rs:225-494)."""
+        fc = self._fast
+        if fc is not None:
+            st, replicas, msg, times = fc.write(dest, data)
+            if st == 0:
+                self.fp_ops += 1
+                if self.phase_times is not None:
+                    for name, v in zip(("crc", "create", "write", "md5_wait", "complete"), times):
+                        self.phase_times.setdefault(name, []).append(v)
+                return replicas
+            if st == 2:
+                raise DfsError(msg)
+            # not handled natively (remote master/head, redirect, not leader): Python path
         t = time.perf_counter()
         # MD5 is a strictly sequential chain (~1.5 ms per MiB on one core) and only needed
         # by CompleteFile: start it first so it overlaps the create RPC, the CRC and the
@@ -535,6 +566,17 @@ class Client:
         return self.read_block_range(block.locations, block.block_id, size_hint=block.size or None)
 
     def get_file_content(self, path: str) -> bytes:
+        fc = self._fast
+        if fc is not None:
+            st, data, msg, times = fc.read(path)
+            if st == 0:
+                self.fp_ops += 1
+                if self.phase_times is not None:
+                    for name, v in zip(("getinfo", "read"), times):
+                        self.phase_times.setdefault(name, []).append(v)
+                return data
+            if st == 2:
+                raise DfsError(msg)
         t = time.perf_counter()
         meta = self.get_file_info(path)
         t = self._phase("getinfo", t)

@@ -243,15 +243,24 @@ def test_local_short_circuit_and_fast_path():
             assert c.get_file_content(p) == d
         assert c.read_file_range("/sc/f3", 1234, 5000) == blobs["/sc/f3"][1234:6234]
         assert c.fp_ops >= 12 and c.fastpath is not None  # socket name known up front
+        assert c._fast is not None and c._fast.writes >= 6 and c._fast.reads >= 6  # native client path
         st = json.load(urllib.request.urlopen(f"{cl.cs_http[0]}/stats"))
         assert st["fp_writes"] >= 5 and st["fp_reads"] >= 6
         # duplicate create through the deferred path is refused at CompleteFile/CreateFile
         with pytest.raises(DfsError):
             c.create_file_from_buffer(b"again", "/sc/f0")
         assert c.get_file_content("/sc/f0") == blobs["/sc/f0"]
-        # a stale socket name: the client drops the fast path and uses gRPC
+        # a stale socket name in the native client: it hands the op to the Python path
+        from rust_hadoop_generated_by_llm_amd.native import lib as native
         from rust_hadoop_generated_by_llm_amd.utils import fastpath as fpmod
 
+        c._fast = native.FastClient("dfs_fp_nonexistent", cl.cs_addrs[0])
+        c._sync_fast()
+        c.create_file_from_buffer(b"native-fallback", "/sc/native_fallback")
+        assert c.get_file_content("/sc/native_fallback") == b"native-fallback"
+        assert c._fast.writes == 0
+        # ... and a stale Python fast-path socket: the client drops it and uses gRPC
+        c._fast = None
         c.fastpath = fpmod.FastPathClient("dfs_fp_nonexistent")
         c.create_file_from_buffer(b"fallback", "/sc/fallback")
         assert c.get_file_content("/sc/fallback") == b"fallback"
