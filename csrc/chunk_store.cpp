@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <stdexcept>
 
 #include "crc32.h"
@@ -482,7 +483,27 @@ bool ChunkStore::make_durable(int data_fd, int meta_fd, bool cold) {
   // instead of two fdatasync flushes per block). Cold-tier files may live on another
   // filesystem: they take the per-file path.
   if (gsync_ && !cold) return gsync_->sync();
-  return ::fdatasync(data_fd) == 0 && ::fdatasync(meta_fd) == 0;
+  // The two flushes are independent: issue them concurrently (NVMe queues them side by
+  // side) instead of paying two device round trips back to back.
+  auto meta = std::async(std::launch::async, [meta_fd] { return ::fdatasync(meta_fd) == 0; });
+  bool ok = ::fdatasync(data_fd) == 0;
+  return meta.get() && ok;
+}
+
+bool ChunkStore::write_file_durable(const std::string& path, const uint8_t* p, uint64_t n, std::string* err) {
+  int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) {
+    *err = errno_str("open " + path);
+    return false;
+  }
+  bool ok = write_all(fd, p, n, 0);
+  if (!ok) *err = errno_str("write " + path);
+  if (ok && cfg_.sync_writes && ::fdatasync(fd) != 0) {
+    ok = false;
+    *err = errno_str("sync " + path);
+  }
+  ::close(fd);
+  return ok;
 }
 
 // ---------------------------------------------------------------- write
@@ -559,6 +580,24 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
     res.error = "HBM arena full";
     return res;
   }
+  bool sync_now = durable_now && cfg_.durability == Durability::NvmeSync;
+  // nvme-sync: the data file (the slow part: page-cache write + device flush) is written
+  // and fdatasync'ed on a helper thread WHILE the GPU stages and checksums the block; the
+  // .meta (known only after the CRC kernel) follows. A checksum mismatch removes the file.
+  std::future<bool> data_file;
+  std::string data_err;
+  if (sync_now && !gsync_) {
+    std::string dp = data_path(id, false);
+    data_file = std::async(std::launch::async, [this, dp, data, n, &data_err] {
+      return write_file_durable(dp, data, n, &data_err);
+    });
+  }
+  auto abandon_data_file = [&] {
+    if (data_file.valid()) {
+      data_file.get();
+      ::unlink(data_path(id, false).c_str());
+    }
+  };
   Lane* l = acquire_lane();
   uint64_t S = num_slices(n);
   auto* dmeta = reinterpret_cast<uint32_t*>(ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
@@ -575,6 +614,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   if (!ok) {
     release_lane(l);
     release(ext);
+    abandon_data_file();
     res.error = err;
     return res;
   }
@@ -582,6 +622,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   if (expected_crc != 0 && co.block_crc != expected_crc) {
     release_lane(l);
     release(ext);
+    abandon_data_file();
     {
       std::lock_guard<std::mutex> g(mu_);
       ++st_.crc_mismatches;
@@ -592,8 +633,17 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   }
   auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
   release_lane(l);
-  bool sync_now = durable_now && cfg_.durability == Durability::NvmeSync;
-  if (sync_now && !persist(id, false, data, n, meta->data(), S, &err)) {
+  if (data_file.valid()) {
+    bool mok = write_file_durable(meta_path(id, false), meta->data(), S * 4, &err);
+    bool dok = data_file.get();
+    if (!mok || !dok) {
+      ::unlink(data_path(id, false).c_str());
+      ::unlink(meta_path(id, false).c_str());
+      release(ext);
+      res.error = dok ? err : data_err;
+      return res;
+    }
+  } else if (sync_now && !persist(id, false, data, n, meta->data(), S, &err)) {
     release(ext);
     res.error = err;
     return res;

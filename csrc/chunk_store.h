@@ -228,6 +228,7 @@ class ChunkStore {
                uint64_t nslices, std::string* err);
   void spill_worker();
   bool make_durable(int data_fd, int meta_fd, bool cold);
+  bool write_file_durable(const std::string& path, const uint8_t* p, uint64_t n, std::string* err);
   WriteResult write_host(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
   ReadResult read_host(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out);
   std::vector<uint32_t> load_meta_file(const std::string& id, bool cold, bool* ok);
