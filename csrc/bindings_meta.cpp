@@ -122,6 +122,9 @@ struct NodeDeleter {
 }  // namespace
 
 void bind_meta(py::module_& m) {
+  m.def("raft_has_joint_majority", [](const std::string& config_json, const std::vector<int>& acks) {
+    return raft::ClusterConfig::from_json(Json::parse(config_json)).has_joint_majority({acks.begin(), acks.end()});
+  }, "the native node's (joint) quorum rule, for tests");
   m.def("pb_roundtrip", [](const std::string& name, py::bytes data) -> py::object {
     std::string in = data, out;
     if (!pb::roundtrip(name, in, &out)) return py::none();

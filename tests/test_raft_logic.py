@@ -1,0 +1,385 @@
+"""Raft logic on the REAL native node (csrc/raft.cpp), driven through its RPC handlers and
+an in-process faulty network. The reference's tier-2 suites check the same rules on plain
+integers and mock objects (dfs/metaserver/tests/raft_logic_tests.rs,
+network_partition_tests.rs, membership_change_unit_tests.rs, property_based_tests.rs,
+jepsen_style_tests.rs); here every assertion runs against the production node."""
+import asyncio
+import json
+import random
+import time
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from rust_hadoop_generated_by_llm_amd.client.checker import check_linearizability, parse_history
+from rust_hadoop_generated_by_llm_amd.native import lib as native
+from rust_hadoop_generated_by_llm_amd.raft.membership import ClusterConfiguration
+from rust_hadoop_generated_by_llm_amd.raft.node import LEADER, NotLeader
+from rust_hadoop_generated_by_llm_amd.raft.transport import TransportError
+
+from .test_raft import Cluster, run
+
+
+class NullHost:
+    """Host of a node that is never started: only its RPC handlers run."""
+
+    restored = None
+
+    def apply_batch(self, items):
+        return ["null"] * len(items)
+
+    def snapshot(self):
+        return "{}"
+
+    def restore(self, text):
+        self.restored = text
+
+    def send(self, addr, kind, body):
+        return None
+
+    def backup(self, url, data):
+        pass
+
+
+def mk(tmp_path, nid=1, members=None):
+    host = NullHost()
+    node = native.RaftNode(nid, members or {1: "a", 2: "b", 3: "c"}, "client-a", str(tmp_path / f"n{nid}"), host,
+                           sync=False)
+    return node, host
+
+
+def rpc(node, kind, **args):
+    return json.loads(node.handle(kind, json.dumps(args)))
+
+
+def append(node, term, prev, prev_term, terms, commit=0):
+    return rpc(node, "append", term=term, leader_id=2, prev_log_index=prev, prev_log_term=prev_term,
+               entries=[{"term": t, "command": {"set": [f"k{i}", i]}} for i, t in enumerate(terms)],
+               leader_commit=commit, leader_address="client-b")
+
+
+# ------------------------------------------------------------------ RPC rules (raft_logic_tests.rs)
+def test_request_vote_decision(tmp_path):
+    n, _ = mk(tmp_path)
+    assert append(n, 3, 0, 0, [1, 1, 3])["success"]  # our log: terms 1, 1, 3
+    # stale candidate term -> rejected, our term unchanged
+    r = rpc(n, "vote", term=2, candidate_id=2, last_log_index=9, last_log_term=3)
+    assert not r["vote_granted"] and r["term"] == 3
+    # newer term but an older last-log term (even with more entries) -> rejected, term adopted
+    r = rpc(n, "vote", term=5, candidate_id=2, last_log_index=10, last_log_term=2)
+    assert not r["vote_granted"] and n.term == 5
+    # same last term but a shorter log -> rejected
+    assert not rpc(n, "vote", term=5, candidate_id=2, last_log_index=2, last_log_term=3)["vote_granted"]
+    # up to date -> granted; a second candidate in the same term -> rejected
+    assert rpc(n, "vote", term=5, candidate_id=3, last_log_index=3, last_log_term=3)["vote_granted"]
+    assert not rpc(n, "vote", term=5, candidate_id=2, last_log_index=9, last_log_term=4)["vote_granted"]
+    # the vote is durable: after a restart candidate 2 is still refused, 3 is re-granted
+    del n
+    n2, _ = mk(tmp_path)
+    assert n2.term == 5
+    assert not rpc(n2, "vote", term=5, candidate_id=2, last_log_index=9, last_log_term=4)["vote_granted"]
+    assert rpc(n2, "vote", term=5, candidate_id=3, last_log_index=3, last_log_term=3)["vote_granted"]
+
+
+def test_append_entries_consistency_truncation_and_commit(tmp_path):
+    n, _ = mk(tmp_path)
+    r = append(n, 1, 0, 0, [1, 1])
+    assert r["success"] and r["match_index"] == 2 and n.last_index == 2
+    assert append(n, 1, 2, 1, [1])["success"] and n.last_index == 3
+    # prev_log_index beyond our log -> rejected, hint = our last index
+    r = append(n, 1, 5, 1, [1])
+    assert not r["success"] and r["match_index"] == 3
+    # term mismatch at prev_log_index -> rejected (the newer term is adopted)
+    r = append(n, 2, 3, 2, [2])
+    assert not r["success"] and n.term == 2
+    # a term-2 leader overwrites the conflicting suffix from index 2 on
+    r = append(n, 2, 1, 1, [2, 2])
+    assert r["success"] and n.last_index == 3 and r["match_index"] == 3
+    # a re-delivered shorter append with a matching prefix keeps the rest of the log
+    r = append(n, 2, 1, 1, [2])
+    assert r["success"] and n.last_index == 3 and r["match_index"] == 2
+    # commit follows the leader, bounded by what this append verified (log matching)
+    append(n, 2, 3, 2, [], commit=10)
+    assert n.commit_index == 3
+    # a stale leader is refused and told the current term
+    r = append(n, 1, 3, 2, [])
+    assert not r["success"] and r["term"] == 2
+    # the log, its truncation and the term survive a restart
+    del n
+    n2, _ = mk(tmp_path)
+    assert n2.last_index == 3 and n2.term == 2
+    assert not append(n2, 2, 3, 1, [])["success"]  # index 3 holds a term-2 entry now
+    assert append(n2, 2, 3, 2, [])["success"]
+
+
+def test_install_snapshot_rules(tmp_path):
+    n, host = mk(tmp_path)
+    append(n, 1, 0, 0, [1, 1])
+    data = json.dumps({"meta": [5, 1], "state": {"x": 1}, "config": None})
+    r = rpc(n, "snapshot", term=1, leader_id=2, last_included_index=5, last_included_term=1, data=data,
+            leader_address="b")
+    assert r["last_included_index"] == 5
+    assert n.last_included_index == 5 and n.last_index == 5 and n.commit_index == 5
+    assert json.loads(host.restored) == {"x": 1}
+    # an older snapshot never rolls the state back
+    host.restored = None
+    r = rpc(n, "snapshot", term=1, leader_id=2, last_included_index=3, last_included_term=1, data=data,
+            leader_address="b")
+    assert r["last_included_index"] == 5 and host.restored is None
+    # a snapshot from a stale term is ignored
+    rpc(n, "vote", term=4, candidate_id=3, last_log_index=5, last_log_term=1)
+    r = rpc(n, "snapshot", term=2, leader_id=2, last_included_index=9, last_included_term=2, data=data,
+            leader_address="b")
+    assert r["term"] == 4 and n.last_included_index == 5
+    # restart: restored from snapshot.json, log continues after it
+    del n
+    n2, host2 = mk(tmp_path)
+    assert n2.last_included_index == 5 and json.loads(host2.restored) == {"x": 1}
+
+
+def test_timeout_now_only_for_current_or_newer_terms(tmp_path):
+    n, _ = mk(tmp_path)
+    append(n, 3, 0, 0, [1])
+    assert not rpc(n, "timeout_now", term=2, sender_id=2)["success"]
+    assert rpc(n, "timeout_now", term=3, sender_id=2)["success"]
+
+
+# ------------------------------------------------------------------ membership (membership_change_unit_tests.rs)
+def _cfg(members, old=None):
+    return ClusterConfiguration({i: f"addr{i}" for i in members}, {i: f"addr{i}" for i in old} if old else None, 1)
+
+
+@pytest.mark.parametrize("members,old,acks,expect", [
+    ([0, 1, 2, 3, 4], None, {0, 1, 2}, True),
+    ([0, 1, 2, 3, 4], None, {0, 1}, False),
+    ([0, 1, 2, 3, 4], [0, 1, 2], {0, 1, 3}, True),        # adding two: 2/3 old and 3/5 new
+    ([0, 1, 2, 3, 4], [0, 1, 2], {0, 3, 4}, False),       # only 1/3 of the old config
+    ([0, 1, 2], [0, 1, 2, 3, 4], {0, 1, 2}, True),        # removing two: 3/5 old and 3/3 new
+    ([0, 1, 2], [0, 1, 2, 3, 4], {0, 3, 4}, False),       # 3/5 old but 1/3 new
+    ([7], None, set(), False),                             # single node, no acks
+    ([7], None, {7}, True),
+])
+def test_joint_majority_python_and_native_agree(members, old, acks, expect):
+    c = _cfg(members, old)
+    assert c.has_joint_majority(acks) is expect
+    assert native.raft_has_joint_majority(json.dumps(c.to_json()), sorted(acks)) is expect
+
+
+# ------------------------------------------------------------------ properties (property_based_tests.rs)
+@given(st.integers(min_value=1, max_value=19))
+def test_majority_threshold_property(n):
+    c = _cfg(range(n))
+    assert c.has_joint_majority(set(range(n // 2 + 1)))
+    assert not c.has_joint_majority(set(range(n // 2)))
+
+
+@settings(max_examples=60)
+@given(st.integers(min_value=1, max_value=11), st.data())
+def test_any_two_quorums_intersect(n, data):
+    ids = list(range(n))
+    c = _cfg(ids)
+    q1 = set(data.draw(st.lists(st.sampled_from(ids), unique=True)))
+    q2 = set(data.draw(st.lists(st.sampled_from(ids), unique=True)))
+    if c.has_joint_majority(q1) and c.has_joint_majority(q2):
+        assert q1 & q2
+
+
+@settings(max_examples=60)
+@given(st.sets(st.integers(0, 8), min_size=1), st.sets(st.integers(0, 8), min_size=1), st.sets(st.integers(0, 8)))
+def test_joint_majority_is_both_majorities(new, old, acks):
+    c = _cfg(sorted(new), sorted(old))
+    both = (len(acks & new) > len(new) // 2) and (len(acks & old) > len(old) // 2)
+    assert c.has_joint_majority(acks) == both
+    assert native.raft_has_joint_majority(json.dumps(c.to_json()), sorted(acks)) == both
+
+
+# ------------------------------------------------------------------ partitions (network_partition_tests.rs)
+def _leaders_by_term(c):
+    seen = {}
+    for n in c.nodes.values():
+        if n.role == LEADER:
+            assert seen.setdefault(n.current_term, n.id) == n.id, "two leaders in one term"
+    return seen
+
+
+async def propose_any(c, cmd, timeout=10.0):
+    """What a client does: find the leader, retry on Not Leader (elections may churn
+    right after a partition heals — campaigners come back with higher terms)."""
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while True:
+        try:
+            leader = await c.leader(timeout=max(0.1, end - loop.time()))
+            return await asyncio.wait_for(leader.propose(cmd), 1.0)
+        except (NotLeader, asyncio.TimeoutError, AssertionError):
+            if loop.time() > end:
+                raise
+            await asyncio.sleep(0.05)
+
+
+def test_minority_partition_cannot_commit_majority_elects(tmp_path):
+    async def go():
+        c = Cluster(tmp_path, n=5)
+        await c.start()
+        l1 = await c.leader()
+        await l1.propose({"set": ["a", 1]})
+        others = [i for i in c.nodes if i != l1.id]
+        minority = [f"node{l1.id}", f"node{others[0]}"]
+        majority = [f"node{i}" for i in others[1:]]
+        c.faults.partition(minority, majority)
+        l2 = await c.leader(exclude=(l1.id, others[0]))
+        assert l2.current_term > l1.current_term
+        await l2.propose({"set": ["b", 2]})
+        with pytest.raises((NotLeader, asyncio.TimeoutError)):
+            await asyncio.wait_for(l1.propose({"set": ["lost", 3]}), 0.7)
+        _leaders_by_term(c)
+        c.faults.heal()
+        for _ in range(100):
+            if all(n.sm.d.get("b") == 2 for n in c.nodes.values()):
+                break
+            await asyncio.sleep(0.05)
+        for n in c.nodes.values():
+            assert n.sm.d.get("b") == 2 and "lost" not in n.sm.d and n.sm.d.get("a") == 1
+        await c.stop()
+
+    run(go())
+
+
+def test_three_way_partition_blocks_progress_until_healed(tmp_path):
+    async def go():
+        c = Cluster(tmp_path, n=5)
+        await c.start()
+        l1 = await c.leader()
+        await l1.propose({"set": ["a", 1]})
+        ids = sorted(c.nodes)
+        groups = [[f"node{i}" for i in ids[:2]], [f"node{i}" for i in ids[2:4]], [f"node{ids[4]}"]]
+        for i, g in enumerate(groups):
+            for h in groups[i + 1:]:
+                c.faults.partition(g, h)
+        # no group has 3 of 5: nothing can commit anywhere
+        with pytest.raises((NotLeader, asyncio.TimeoutError)):
+            await asyncio.wait_for(l1.propose({"set": ["x", 1]}), 0.7)
+        await asyncio.sleep(0.5)
+        for n in c.nodes.values():
+            assert "x" not in n.sm.d
+        c.faults.heal()
+        await propose_any(c, {"set": ["after", 1]})
+        _leaders_by_term(c)
+        await c.stop()
+
+    run(go())
+
+
+def test_isolated_node_rejoins_and_terms_converge(tmp_path):
+    async def go():
+        c = Cluster(tmp_path, n=3)
+        await c.start()
+        l1 = await c.leader()
+        lone = next(n for n in c.nodes.values() if n is not l1)
+        c.faults.isolate(f"node{lone.id}", list(c.registry))
+        t0 = lone.current_term
+        await asyncio.sleep(1.0)
+        assert lone.current_term > t0 and lone.role != LEADER  # keeps campaigning, never wins alone
+        await propose_any(c, {"set": ["k", 1]})
+        c.faults.heal()
+        for _ in range(100):
+            terms = {n.current_term for n in c.nodes.values()}
+            if len(terms) == 1 and lone.sm.d.get("k") == 1:
+                break
+            await asyncio.sleep(0.05)
+        assert len({n.current_term for n in c.nodes.values()}) == 1 and lone.sm.d.get("k") == 1
+        await c.stop()
+
+    run(go())
+
+
+# ------------------------------------------------------------------ jepsen-style (jepsen_style_tests.rs)
+class FileKV:
+    """The checker's sequential spec (client/checker.py): put only if absent, get, delete."""
+
+    def __init__(self):
+        self.d = {}
+
+    def apply(self, cmd, idx):
+        op, path, h = cmd["op"], cmd["path"], cmd.get("h")
+        if op == "put":
+            if path in self.d:
+                return "error"
+            self.d[path] = h
+            return f"put_ok:{h}"
+        if op == "delete":
+            return "ok" if self.d.pop(path, None) is not None else "not_found"
+        raise ValueError(op)
+
+    def snapshot(self):
+        return {"d": self.d}
+
+    def restore(self, s):
+        self.d = dict(s["d"])
+
+
+def test_linearizable_register_under_nemesis(tmp_path):
+    """Concurrent clients against the native Raft group while a nemesis isolates nodes,
+    drops and delays messages; the WGL checker must find the history linearizable."""
+
+    async def go():
+        c = Cluster(tmp_path, n=3)
+        for n in c.nodes.values():  # swap in the checker's register spec
+            n.sm = n._host.sm = FileKV()
+        await c.start()
+        await c.leader()
+        history: list[str] = []
+        ids = iter(range(1, 1_000_000))
+        stop = asyncio.Event()
+        rng = random.Random(7)
+
+        def rec(**kw):
+            history.append(json.dumps(dict(kw, ts_ns=time.monotonic_ns())))
+
+        async def client(name: str):
+            while not stop.is_set():
+                op = rng.choice(["put", "put", "get", "get", "delete"])
+                path = f"/k{rng.randrange(3)}"
+                oid = next(ids)
+                h = f"h{oid}"
+                rec(id=oid, client=name, type="invoke", op=op, path=path, data_hash=h if op == "put" else "")
+                leaders = [n for n in c.nodes.values() if n.role == LEADER]
+                result = "error"
+                try:
+                    if not leaders:
+                        raise NotLeader(None)
+                    node = rng.choice(leaders)
+                    if op == "get":
+                        await asyncio.wait_for(node.read_index(), 0.5)
+                        v = node.sm.d.get(path)
+                        result = f"get_ok:{v}" if v is not None else "not_found"
+                    else:
+                        result = await asyncio.wait_for(node.propose({"op": op, "path": path, "h": h}), 0.5)
+                except (NotLeader, asyncio.TimeoutError, RuntimeError, TransportError):
+                    result = "error"  # outcome unknown: the checker tries both
+                rec(id=oid, client=name, type="return", result=result)
+                await asyncio.sleep(rng.uniform(0, 0.01))
+
+        async def nemesis():
+            names = list(c.registry)
+            for cycle in range(12):
+                kind = cycle % 3
+                if kind == 0:
+                    c.faults.isolate(rng.choice(names), names)
+                elif kind == 1:
+                    c.faults.drop_rate = 0.2
+                else:
+                    c.faults.delay_s[rng.choice(names)] = 0.02
+                await asyncio.sleep(0.25)
+                c.faults.heal()
+                await asyncio.sleep(0.1)
+            stop.set()
+
+        await asyncio.gather(nemesis(), *(client(f"c{i}") for i in range(4)))
+        await c.stop()
+        ops = parse_history(history)
+        assert len(ops) > 40
+        assert check_linearizability(ops) == []
+
+    run(go())
