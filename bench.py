@@ -309,7 +309,10 @@ def main():
             for i, p in enumerate(procs.items):
                 try:
                     kids = [psutil.Process(p.pid)] + psutil.Process(p.pid).children(recursive=True)
-                    snap[os.path.basename(procs.logs[i]).split(".")[0]] = sum(sum(k.cpu_times()[:2]) for k in kids)
+                    name = os.path.basename(procs.logs[i]).split(".")[0]
+                    times = [k.cpu_times() for k in kids]
+                    snap[name] = sum(t.user + t.system for t in times)
+                    snap[name + "_sys"] = sum(t.system for t in times)  # page cache / reclaim / flush
                 except psutil.Error:
                     pass
             return snap
@@ -380,6 +383,7 @@ def main():
                 "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
                 "rccl_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) for r in allr),
                 "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
+                "disk_gate_waits": sum(r["cs"].get("disk_gate_waits", 0) for r in allr),
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],
             }

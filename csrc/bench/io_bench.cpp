@@ -8,9 +8,15 @@
 // `rocprofv3 --kernel-trace --stats` to get per-kernel device time.
 //
 //   io_bench [--device N] [--dir PATH] [--iters N] [--no-fsync]   -> one JSON object on stdout
+//   io_bench --disk-sweep [--dir PATH]   -> aggregate 1 MiB write+fdatasync bandwidth of the
+//            storage directory at 1..240 concurrent writers, buffered and O_DIRECT (what bounds
+//            nvme-sync replication when every GPU of a node writes RF replicas to one volume)
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -18,9 +24,11 @@
 #include <filesystem>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "chunk_store.h"
+#include "disk_gate.h"
 #include "crc32.h"
 #include "gf256.h"
 
@@ -66,9 +74,85 @@ static void emit_case(bool& first, const char* name, size_t size, Lat& l) {
   first = false;
 }
 
+// T threads each write `per` 1 MiB files (+ an 8 KiB sidecar like the .meta) with fdatasync.
+static void disk_case(const std::string& dir, int threads, int per, bool direct, int gate_slots, bool first) {
+  std::filesystem::create_directories(dir);
+  DiskGate gate(dir, gate_slots);
+  const size_t n = 1 << 20, meta = 8192;
+  std::vector<Lat> lat(threads);
+  std::vector<std::thread> ts;
+  std::atomic<int> errors{0};
+  auto t0 = Clock::now();
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      void* buf = nullptr;
+      if (posix_memalign(&buf, 4096, n) != 0) { ++errors; return; }
+      std::memset(buf, t + 1, n);
+      for (int i = 0; i < per; ++i) {
+        std::string f = dir + "/t" + std::to_string(t) + "_" + std::to_string(i);
+        auto a = Clock::now();
+        DiskGate::Slot slot = gate.acquire();
+        int fd = ::open(f.c_str(), O_CREAT | O_WRONLY | O_TRUNC | (direct ? O_DIRECT : 0), 0644);
+        int fm = ::open((f + ".meta").c_str(), O_CREAT | O_WRONLY | O_TRUNC | (direct ? O_DIRECT : 0), 0644);
+        if (fd < 0 || fm < 0 || ::pwrite(fd, buf, n, 0) != static_cast<ssize_t>(n) ||
+            ::pwrite(fm, buf, meta, 0) != static_cast<ssize_t>(meta) || ::fdatasync(fd) != 0 || ::fdatasync(fm) != 0)
+          ++errors;
+        if (fd >= 0) ::close(fd);
+        if (fm >= 0) ::close(fm);
+        slot.release();
+        lat[t].add(secs(a, Clock::now()));
+      }
+      std::free(buf);
+    });
+  for (auto& th : ts) th.join();
+  double el = secs(t0, Clock::now());
+  Lat all;
+  for (auto& l : lat) all.v.insert(all.v.end(), l.v.begin(), l.v.end());
+  std::printf("%s\n    {\"threads\": %d, \"direct\": %s, \"gate\": %d, \"files\": %d, \"GBps\": %.2f, \"p50_ms\": %.3f, \"p99_ms\": %.3f, \"errors\": %d}",
+              first ? "" : ",", threads, direct ? "true" : "false", gate_slots, threads * per,
+              double(threads) * per * n / el / 1e9, all.pct(0.5) * 1e3, all.pct(0.99) * 1e3, errors.load());
+  std::fflush(stdout);
+  std::filesystem::remove_all(dir);
+}
+
 int main(int argc, char** argv) {
   int device = 0, iters = 50;
   bool fsync = true;
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--disk-sweep") {
+      std::string dir = "/tmp/io_bench_disk";
+      for (int j = 1; j + 1 < argc; ++j)
+        if (std::string(argv[j]) == "--dir") dir = argv[j + 1];
+      std::printf("{\"disk_sweep\": [");
+      bool first = true;
+      for (int j = 1; j + 1 < argc; ++j)  // --cases "threads:gate[:direct],..." in this order
+        if (std::string(argv[j]) == "--cases") {
+          std::string c = argv[j + 1];
+          size_t p = 0;
+          while (p < c.size()) {
+            size_t e = c.find(',', p);
+            if (e == std::string::npos) e = c.size();
+            int t = 0, g = 0, d = 0;  // threads:gate[:direct]
+            if (std::sscanf(c.substr(p, e - p).c_str(), "%d:%d:%d", &t, &g, &d) >= 2 && t > 0) {
+              disk_case(dir, t, std::max(4, 2400 / t / 4), d != 0, g, first);
+              first = false;
+            }
+            p = e + 1;
+          }
+          std::printf("\n]}\n");
+          return 0;
+        }
+      for (int direct = 0; direct < 2; ++direct)
+        for (int t : {1, 10, 30, 60, 120, 240}) {
+          disk_case(dir, t, std::max(4, 2400 / t / 4), direct != 0, 0, first);
+          first = false;
+        }
+      // the same overload behind the node-wide gate (what ChunkStore does)
+      for (int g : {8, 16, 24, 32})
+        for (int t : {60, 240}) disk_case(dir, t, std::max(4, 2400 / t / 4), false, g, false);
+      std::printf("\n]}\n");
+      return 0;
+    }
   std::string dir = "/tmp/io_bench_store";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];

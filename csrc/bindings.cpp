@@ -290,6 +290,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["promotions"] = t.promotions;
         d["crc_mismatches"] = t.crc_mismatches;
         d["gpu_kernel_launches"] = t.gpu_kernel_launches;
+        d["disk_gate_waits"] = t.disk_gate_waits;
         return d;
       })
       .def("gpu_crc", [](ChunkStore& s, py::buffer data) {

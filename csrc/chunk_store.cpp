@@ -20,6 +20,15 @@
 namespace dfs {
 
 // ---------------------------------------------------------------- group commit
+// The block stays resident in HBM (or is re-read on a miss): once its bytes are on the
+// device, the host page-cache copy is dead weight that the kernel would otherwise have to
+// reclaim in our writers' context under memory pressure. Drop it.
+static void drop_cached(int fd) {
+#ifdef POSIX_FADV_DONTNEED
+  if (fd >= 0) (void)::posix_fadvise(fd, 0, 0, POSIX_FADV_DONTNEED);
+#endif
+}
+
 GroupSync::GroupSync(const std::string& dir) { fd_ = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC); }
 
 GroupSync::~GroupSync() {
@@ -174,6 +183,9 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
   // than our two files, so the per-file fdatasync pair stays the default.
   const char* gs = std::getenv("DFS_GROUP_SYNC");
   if (cfg_.sync_writes && gs && std::string(gs) == "1") gsync_ = std::make_unique<GroupSync>(cfg_.storage_dir);
+  if (cfg_.sync_writes)
+    gate_ = std::make_unique<DiskGate>(cfg_.storage_dir,
+                                       cfg_.disk_inflight < 0 ? disk_inflight_default() : cfg_.disk_inflight);
   if (gpu()) {
     HIP_OK(hipSetDevice(cfg_.device));
     uint64_t cap = cfg_.hbm_capacity;
@@ -448,6 +460,7 @@ bool ChunkStore::d2h_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t
 bool ChunkStore::persist(const std::string& id, bool cold, const uint8_t* data, uint64_t n, const uint8_t* meta_be,
                          uint64_t nslices, std::string* err) {
   std::string dp = data_path(id, cold), mp = meta_path(id, cold);
+  DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
   int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
   if (fd < 0) {
     *err = errno_str("open " + dp);
@@ -471,6 +484,7 @@ bool ChunkStore::persist(const std::string& id, bool cold, const uint8_t* data, 
     ok = false;
     *err = errno_str("sync " + dp);
   }
+  if (ok && cfg_.sync_writes && gpu()) drop_cached(fd);
   ::close(fd);
   ::close(mfd);
   return ok;
@@ -502,6 +516,7 @@ bool ChunkStore::write_file_durable(const std::string& path, const uint8_t* p, u
     ok = false;
     *err = errno_str("sync " + path);
   }
+  if (ok && cfg_.sync_writes) drop_cached(fd);
   ::close(fd);
   return ok;
 }
@@ -589,6 +604,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   if (sync_now && !gsync_) {
     std::string dp = data_path(id, false);
     data_file = std::async(std::launch::async, [this, dp, data, n, &data_err] {
+      DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
       return write_file_durable(dp, data, n, &data_err);
     });
   }
@@ -698,6 +714,7 @@ bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64
 bool ChunkStore::persist_from_device(const std::string& id, const uint8_t* d, uint64_t n, const uint8_t* meta_be,
                                      uint64_t nslices, std::string* err) {
   HIP_OK(hipSetDevice(cfg_.device));
+  DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
   Lane* l = acquire_lane();
   std::string dp = data_path(id, false);
   int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
@@ -717,6 +734,7 @@ bool ChunkStore::persist_from_device(const std::string& id, const uint8_t* d, ui
     ok = mfd >= 0 && write_all(mfd, meta_be, nslices * 4, 0);
   }
   if (ok) ok = make_durable(fd, mfd, false);
+  if (ok && cfg_.sync_writes) drop_cached(fd);
   if (fd >= 0) ::close(fd);
   if (mfd >= 0) ::close(mfd);
   if (!ok) *err = errno_str("persist " + id);
@@ -1162,6 +1180,7 @@ void ChunkStore::spill_worker() {
       size = it->second.size;
       d = arena_ + it->second.dev_off;
     }
+    DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
     Lane* l = acquire_lane();
     uint64_t S = num_slices(size);
     ensure_hscratch(l, S * 4 + 16);
@@ -1192,6 +1211,7 @@ void ChunkStore::spill_worker() {
       ok = mfd >= 0 && write_all(mfd, hmeta, S * 4, 0);
     }
     if (ok) ok = make_durable(fd, mfd, false);
+    if (ok && cfg_.sync_writes) drop_cached(fd);
     if (fd >= 0) ::close(fd);
     if (mfd >= 0) ::close(mfd);
     release_lane(l);
@@ -1430,6 +1450,7 @@ std::vector<std::string> ChunkStore::list_blocks() {
 StoreStats ChunkStore::stats() {
   std::lock_guard<std::mutex> g(mu_);
   StoreStats s = st_;
+  s.disk_gate_waits = gate_ ? gate_->waits() : 0;
   s.blocks = index_.size();
   s.bytes = 0;
   s.hbm_resident_blocks = 0;

@@ -29,6 +29,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "disk_gate.h"
 #include "gpu_kernels.h"
 
 namespace dfs {
@@ -45,6 +46,8 @@ struct StoreConfig {
   int lanes = 8;                 // concurrent GPU stream contexts
   int spill_threads = 4;
   bool sync_writes = true;       // fdatasync data + .meta
+  int disk_inflight = -1;        // node-wide cap on durable writes per filesystem (disk_gate.h);
+                                 // -1: DFS_DISK_INFLIGHT (default 12), 0: ungated
 };
 
 struct WriteResult {
@@ -76,6 +79,7 @@ struct StoreStats {
   uint64_t promotions = 0;
   uint64_t crc_mismatches = 0;
   uint64_t gpu_kernel_launches = 0;
+  uint64_t disk_gate_waits = 0;  // durable writes that queued for a node-wide disk slot
 };
 
 // First-fit extent allocator over [0, capacity) with coalescing.
@@ -252,6 +256,7 @@ class ChunkStore {
   StoreStats st_;
   std::atomic<uint64_t> launches_{0};
   std::unique_ptr<GroupSync> gsync_;
+  std::unique_ptr<DiskGate> gate_;
 };
 
 }  // namespace dfs

@@ -166,7 +166,7 @@ class ChunkServerProcess:
         m.gauge("dfs_chunkserver_used_space_bytes", "used bytes on the storage fs", fn=lambda: self.disk_stats()[0])
         m.gauge("dfs_chunkserver_total_chunks", "blocks held", fn=lambda: self.store.stats()["blocks"])
         for k in ("hbm_capacity", "hbm_used", "hbm_resident_blocks", "dirty_blocks", "spill_queue", "evictions",
-                  "promotions", "crc_mismatches", "gpu_kernel_launches"):
+                  "promotions", "crc_mismatches", "gpu_kernel_launches", "disk_gate_waits"):
             m.gauge(f"dfs_chunkserver_{k}", f"chunk store {k}", fn=lambda k=k: self.store.stats()[k])
         m.gauge("dfs_chunkserver_rccl_bytes_sent", "bytes replicated over RCCL",
                 fn=lambda: self.rccl.bytes_sent if self.rccl else 0)

@@ -47,4 +47,47 @@ if [ "$STEP" = "rccl-fail" ]; then
   cp /tmp/dfs_rccl_rehearsal/cs*.log gpurun_out/ 2>/dev/null || true
   [ $rc -eq 0 ] || exit $rc
 fi
+if [ "$STEP" = "gate" ]; then
+  # Node-wide disk admission (csrc/disk_gate.h): 4 ranks share the GPU and the volume, RF=3,
+  # so ~120 durable replica writes are in flight; A/B ungated vs the default gate, then N=1
+  DFS_DISK_INFLIGHT=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+    --master-port 29537 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/bench_n4_gate0.json 2> gpurun_out/bench_n4_gate0.err && \
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+    --master-port 29539 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/bench_n4_gate.json 2> gpurun_out/bench_n4_gate.err && \
+  timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/bench_n1.json 2> gpurun_out/bench_n1.err || exit $?
+fi
+if [ "$STEP" = "gate2" ]; then
+  # interleaved: fresh N=1, N=4 gated, N=4 ungated, N=1 again (the volume throttles after bursts)
+  timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/g2_n1a.json 2> gpurun_out/g2_n1a.err && \
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+    --master-port 29541 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/g2_n4_gate.json 2> gpurun_out/g2_n4_gate.err && \
+  DFS_DISK_INFLIGHT=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+    --master-port 29543 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/g2_n4_gate0.json 2> gpurun_out/g2_n4_gate0.err && \
+  timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/g2_n1b.json 2> gpurun_out/g2_n1b.err || exit $?
+fi
+if [ "$STEP" = "diag" ]; then
+  # why does a 1-GPU write get slow (and burn kernel CPU) after a burst of runs?
+  D=gpurun_out/diag.txt
+  { stat -f . ; grep -v "^overlay\|cgroup\|proc\|sysfs\|devpts\|mqueue" /proc/mounts | head -20; } > $D 2>&1
+  { TIMEFORMAT="io_bench 10:0 fresh user=%U sys=%S wall=%R"; time timeout -k 10 120 build/native/io_bench --disk-sweep --dir ./iob --cases "10:0,10:0" ; } >> $D 2>&1 && \
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+    --master-port 29545 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/d_n4.json 2> gpurun_out/d_n4.err || exit $?
+  { echo "--- after n4"; ps -eo pid,stat,pcpu,etime,comm | awk '$3 > 1.0' ; cat /proc/pressure/io; grep -E "Dirty|Writeback:|MemFree|^Cached" /proc/meminfo; } >> $D 2>&1
+  { TIMEFORMAT="io_bench 10:0 after user=%U sys=%S wall=%R"; time timeout -k 10 120 build/native/io_bench --disk-sweep --dir ./iob --cases "10:0,10:0" ; } >> $D 2>&1 && \
+  { TIMEFORMAT="io_bench 10:0 tmp-after user=%U sys=%S wall=%R"; time timeout -k 10 120 build/native/io_bench --disk-sweep --dir /tmp/iob --cases "10:0" ; } >> $D 2>&1 && \
+  sleep 45 && echo "--- after 45s" >> $D && cat /proc/pressure/io >> $D && \
+  { TIMEFORMAT="io_bench 10:0 later user=%U sys=%S wall=%R"; time timeout -k 10 120 build/native/io_bench --disk-sweep --dir ./iob --cases "10:0,10:0" ; } >> $D 2>&1 && \
+  timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/d_n1.json 2> gpurun_out/d_n1.err || exit $?
+fi
+if [ "$STEP" = "diag2" ]; then
+  # buffered vs O_DIRECT durable writes, fresh and after an N=4 burst
+  D=gpurun_out/diag2.txt
+  C="10:0:0,10:0:1,30:12:0,30:12:1,10:0:0,10:0:1"
+  { TIMEFORMAT="fresh user=%U sys=%S wall=%R"; time timeout -k 10 200 build/native/io_bench --disk-sweep --dir ./iob --cases "$C" ; } > $D 2>&1 && \
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+    --master-port 29547 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/d2_n4.json 2> gpurun_out/d2_n4.err && \
+  { TIMEFORMAT="after user=%U sys=%S wall=%R"; time timeout -k 10 200 build/native/io_bench --disk-sweep --dir ./iob --cases "$C" ; } >> $D 2>&1 && \
+  sleep 30 && \
+  { TIMEFORMAT="later user=%U sys=%S wall=%R"; time timeout -k 10 200 build/native/io_bench --disk-sweep --dir ./iob --cases "$C" ; } >> $D 2>&1 || exit $?
+fi
 echo "gpu_round done"
