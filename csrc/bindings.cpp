@@ -8,6 +8,7 @@
 #include "chunk_store.h"
 #include "crc32.h"
 #include "crypto.h"
+#include "disk_gate.h"
 #include "fastpath.h"
 #include "gf256.h"
 #include "rccl_engine.h"
@@ -469,6 +470,23 @@ PYBIND11_MODULE(_dfs_native, m) {
     return crypto::rsa_sha256_verify(n, e, msg, sig);
   });
   m.def("random_bytes", [](size_t n) { return py::bytes(crypto::random_bytes(n)); });
+
+  // ---------------- node-wide disk admission (disk_gate.h)
+  py::class_<DiskGate::Slot>(m, "DiskSlot")
+      .def("release", &DiskGate::Slot::release)
+      .def_property_readonly("held", &DiskGate::Slot::held);
+  py::class_<DiskGate>(m, "DiskGate")
+      .def(py::init<const std::string&, int>(), py::arg("dir"), py::arg("slots"))
+      .def_property_readonly("enabled", &DiskGate::enabled)
+      .def_property_readonly("slots", &DiskGate::slots)
+      .def_property_readonly("waits", &DiskGate::waits)
+      .def("acquire", &DiskGate::acquire, py::call_guard<py::gil_scoped_release>(), py::keep_alive<0, 1>())
+      .def("try_acquire", [](DiskGate& g) -> py::object {
+        bool got = false;
+        DiskGate::Slot s = g.try_acquire(&got);
+        if (!got) return py::none();
+        return py::cast(std::move(s));
+      }, py::keep_alive<0, 1>());
 
   // ---------------- metadata plane (Raft)
   bind_meta(m);

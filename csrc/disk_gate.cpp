@@ -67,40 +67,53 @@ void DiskGate::unlock(int i) {
   local_[i].cv.notify_one();
 }
 
-DiskGate::Slot DiskGate::acquire() {
+bool DiskGate::take(int i, bool block, Slot* s) {
+  {
+    std::unique_lock<std::mutex> lk(local_[i].m);
+    if (block) local_[i].cv.wait(lk, [&] { return !local_[i].busy; });
+    else if (local_[i].busy) return false;
+    local_[i].busy = true;
+  }
+  int r;
+  do r = ::flock(fds_[i], LOCK_EX | (block ? 0 : LOCK_NB));
+  while (r != 0 && errno == EINTR);
+  if (r != 0) {
+    {
+      std::lock_guard<std::mutex> g(local_[i].m);
+      local_[i].busy = false;
+    }
+    local_[i].cv.notify_one();
+    return false;
+  }
+  s->g_ = this;
+  s->i_ = i;
+  return true;
+}
+
+DiskGate::Slot DiskGate::try_acquire(bool* got) {
   Slot s;
+  *got = fds_.empty();
   if (fds_.empty()) return s;
   const int n = static_cast<int>(fds_.size());
+  int start = static_cast<int>(__atomic_fetch_add(&next_, 1, __ATOMIC_RELAXED) % n);
+  for (int k = 0; k < n; ++k)
+    if (take((start + k) % n, false, &s)) {
+      *got = true;
+      break;
+    }
+  return s;
+}
+
+DiskGate::Slot DiskGate::acquire() {
   // One non-blocking pass over every slot (rotating start so processes spread out); when
   // the node is saturated, queue on one slot with a blocking flock: K independent FIFO
   // queues, no polling (hundreds of waiters must not burn CPU).
-  auto take = [&](int i, bool block) {
-    {
-      std::unique_lock<std::mutex> lk(local_[i].m);
-      if (block) local_[i].cv.wait(lk, [&] { return !local_[i].busy; });
-      else if (local_[i].busy) return false;
-      local_[i].busy = true;
-    }
-    int r;
-    do r = ::flock(fds_[i], LOCK_EX | (block ? 0 : LOCK_NB));
-    while (r != 0 && errno == EINTR);
-    if (r != 0) {
-      {
-        std::lock_guard<std::mutex> g(local_[i].m);
-        local_[i].busy = false;
-      }
-      local_[i].cv.notify_one();
-      return false;
-    }
-    s.g_ = this;
-    s.i_ = i;
-    return true;
-  };
-  int start = static_cast<int>(__atomic_fetch_add(&next_, 1, __ATOMIC_RELAXED) % n);
-  for (int k = 0; k < n; ++k)
-    if (take((start + k) % n, false)) return s;
+  bool got = false;
+  Slot s = try_acquire(&got);
+  if (got) return s;
   __atomic_fetch_add(&waits_, 1, __ATOMIC_RELAXED);
-  while (!take(start, true)) {
+  const int i = static_cast<int>(__atomic_fetch_add(&next_, 1, __ATOMIC_RELAXED) % fds_.size());
+  while (!take(i, true, &s)) {
   }
   return s;
 }

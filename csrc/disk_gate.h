@@ -35,6 +35,7 @@ class DiskGate {
     Slot& operator=(Slot&& o) noexcept;
     ~Slot() { release(); }
     void release();
+    bool held() const { return g_ != nullptr; }
 
    private:
     friend class DiskGate;
@@ -43,9 +44,12 @@ class DiskGate {
   };
   // Blocks until one of the node's slots is free (immediately when disabled).
   Slot acquire();
+  // One non-blocking pass; `*got` says whether a slot was taken.
+  Slot try_acquire(bool* got);
   uint64_t waits() const { return waits_; }
 
  private:
+  bool take(int i, bool block, Slot* s);
   void unlock(int i);
   std::vector<int> fds_;
   struct Local {  // one holder per slot inside this process (released from any thread)
