@@ -11,6 +11,7 @@
 #include "client_fast.h"
 #include "dfs_pb.h"
 #include "localrpc.h"
+#include "config_core.h"
 #include "master_core.h"
 #include "raft.h"
 
@@ -131,6 +132,8 @@ void bind_meta(py::module_& m) {
     return py::bytes(out);
   }, "decode `data` as dfs.<name> with the native codec and re-encode it");
 
+  py::class_<raft::StateMachine, std::shared_ptr<raft::StateMachine>>(m, "StateMachine",
+                                                                     "a natively applied Raft state machine");
   py::class_<raft::Node, std::unique_ptr<raft::Node, NodeDeleter>>(m, "RaftNode")
       .def(py::init([](int id, std::map<int, std::string> members, std::string client_address, std::string dir,
                        py::object host, double elo, double ehi, double hb, bool sync, uint64_t snapshot_threshold,
@@ -149,7 +152,7 @@ void bind_meta(py::module_& m) {
              o.backup_endpoint = std::move(backup_endpoint);
              o.backup_bucket = std::move(backup_bucket);
              std::shared_ptr<raft::StateMachine> sm;
-             if (!native_sm.is_none()) sm = native_sm.cast<std::shared_ptr<MasterCore>>();
+             if (!native_sm.is_none()) sm = native_sm.cast<std::shared_ptr<raft::StateMachine>>();
              auto h = std::make_shared<PyRaftHost>(std::move(host), sm);
              return std::unique_ptr<raft::Node, NodeDeleter>(new raft::Node(std::move(o), h));
            }),
@@ -205,8 +208,22 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("wal_syncs", &raft::Node::wal_syncs)
       .def_property_readonly("wal_bytes", &raft::Node::wal_bytes);
 
+  // ---------------- native config-server state machine (C36)
+  py::class_<ConfigCore, raft::StateMachine, std::shared_ptr<ConfigCore>>(m, "ConfigCore")
+      .def(py::init([]() { return std::make_shared<ConfigCore>(); }))
+      .def("apply", [](ConfigCore& c, uint64_t idx, const std::string& cmd) {
+        py::gil_scoped_release r;
+        return c.apply({{idx, cmd}}).front();
+      })
+      .def("snapshot", &ConfigCore::snapshot, py::call_guard<py::gil_scoped_release>())
+      .def("restore", &ConfigCore::restore, py::call_guard<py::gil_scoped_release>())
+      .def("shard_map_json", &ConfigCore::shard_map_json)
+      .def("masters_json", &ConfigCore::masters_json)
+      .def_property_readonly("version", &ConfigCore::version)
+      .def("split_candidates", &ConfigCore::split_candidates, py::arg("n") = 3);
+
   // ---------------- native master core + same-host RPC listener
-  py::class_<MasterCore, std::shared_ptr<MasterCore>>(m, "MasterCore")
+  py::class_<MasterCore, raft::StateMachine, std::shared_ptr<MasterCore>>(m, "MasterCore")
       .def(py::init([]() { return std::make_shared<MasterCore>(); }))
       .def("attach", [](MasterCore& c, raft::Node& n) { c.attach(&n); }, py::keep_alive<1, 2>())
       .def("detach", &MasterCore::detach)

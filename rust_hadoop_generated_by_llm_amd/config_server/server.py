@@ -1,7 +1,8 @@
 """``dfs_config_server`` — Raft-replicated shard map + master registry (C36; reference
 dfs/metaserver/src/config_server.rs and bin/config_server.rs).
 
-State ``{"Config": {"shard_map": ShardMap(Range), "masters": {addr: MasterInfo}}}``.
+State ``{"Config": {"shard_map": ShardMap(Range), "masters": {addr: MasterInfo}}}``, held and
+applied natively (csrc/config_core.cpp) on the native Raft node's applier thread.
 FetchShardMap is linearizable (ReadIndex) and, like the reference, returns only
 shard -> peers (no range boundaries). SplitShard without peers allocates standby masters (registered
 with an empty shard id) first, else the three most recently heartbeated masters; the
@@ -15,11 +16,11 @@ import json
 import logging
 import os
 import signal
-import time
 
 from aiohttp import web
 
 from ..models import proto as pb
+from ..native import lib as _native
 from ..parallel.sharding import ShardMap
 from ..raft.membership import initial_members
 from ..raft.node import NotLeader, RaftNode
@@ -33,60 +34,35 @@ log = logging.getLogger("dfs.config_server")
 
 
 class ConfigState:
+    """Facade over the native state machine (csrc/config_core.cpp), which the native Raft
+    node applies on its own thread; views are re-parsed only when the state changed."""
+
     def __init__(self):
-        self.shard_map = ShardMap.new_range()
-        self.masters: dict[str, dict] = {}
+        self.core = _native.ConfigCore()
+        self._map: tuple[int, ShardMap | None] = (-1, None)
+
+    @property
+    def shard_map(self) -> ShardMap:
+        v = self.core.version
+        if self._map[0] != v or self._map[1] is None:
+            self._map = (v, ShardMap.from_json(json.loads(self.core.shard_map_json())))
+        return self._map[1]
+
+    @property
+    def masters(self) -> dict[str, dict]:
+        return json.loads(self.core.masters_json())
 
     def apply(self, command, index: int = 0):
-        if not isinstance(command, dict) or "Config" not in command:
-            return None
-        (name, a), = command["Config"].items()
-        sm = self.shard_map
-        if name == "AddShard":
-            sm.add_shard(a["shard_id"], a["peers"])
-        elif name == "RemoveShard":
-            sm.remove_shard(a["shard_id"])
-        elif name == "SplitShard":
-            ok = sm.split_shard(a["split_key"], a["new_shard_id"], a["new_shard_peers"])
-            if ok:
-                for addr in a["new_shard_peers"]:
-                    if addr in self.masters:
-                        self.masters[addr]["shard_id"] = a["new_shard_id"]
-            return ok
-        elif name == "MergeShard":
-            return sm.merge_shards(a["victim_shard_id"], a["retained_shard_id"])
-        elif name == "RebalanceShard":
-            return sm.rebalance_boundary(a["old_key"], a["new_key"])
-        elif name == "RegisterMaster":
-            addr, sid = a["address"], a["shard_id"]
-            if not sid:  # standby master: waits in the registry for a SplitShard allocation
-                # (a standby that a split already placed keeps that shard)
-                owned = next((s for s in sm.get_all_shards() if addr in (sm.get_shard_peers(s) or [])), "")
-                self.masters[addr] = {"address": addr, "shard_id": owned,
-                                      "last_heartbeat": int(time.time()), "rps_per_prefix": {}}
-                return None
-            if not sm.has_shard(sid):
-                sm.add_shard(sid, [addr])
-            else:
-                peers = sm.get_shard_peers(sid) or []
-                if addr not in peers:
-                    sm.add_shard(sid, peers + [addr])
-            self.masters[addr] = {"address": addr, "shard_id": sid, "last_heartbeat": int(time.time()),
-                                  "rps_per_prefix": {}}
-        elif name == "ShardHeartbeat":
-            info = self.masters.get(a["address"])
-            if info is not None:
-                info["last_heartbeat"] = int(time.time())
-                info["rps_per_prefix"] = dict(a.get("rps_per_prefix", {}))
-        return None
+        r = self.core.apply(index, json.dumps(command))
+        if r.startswith("!"):
+            raise ValueError(r[1:])
+        return json.loads(r)
 
     def snapshot(self) -> dict:
-        return {"Config": {"shard_map": self.shard_map.to_json(), "masters": self.masters}}
+        return json.loads(self.core.snapshot())
 
     def restore(self, state: dict) -> None:
-        c = state.get("Config", state)
-        self.shard_map = ShardMap.from_json(c.get("shard_map", {"strategy": {"Range": {"ranges": {}}}}))
-        self.masters = dict(c.get("masters", {}))
+        self.core.restore(json.dumps(state))
 
 
 class ConfigService:
@@ -129,9 +105,7 @@ class ConfigService:
         if not peers:
             # prefer standby masters (registered without a shard); the reference takes the
             # three most recently heartbeated masters even if they serve another shard
-            avail = sorted(self.state.masters.values(), key=lambda m: -m["last_heartbeat"])
-            standby = [m["address"] for m in avail if not m.get("shard_id")]
-            peers = standby[:3] or [m["address"] for m in avail[:3]]
+            peers = self.state.core.split_candidates(3)
         if not peers:
             return pb.SplitShardResponse(success=False, error_message="No available master nodes for new shard")
         try:
@@ -198,7 +172,8 @@ async def run(args) -> None:
     transport = HttpTransport()
     raft = RaftNode(args.id, members, with_scheme(args.advertise_addr or args.addr),
                     os.path.join(args.storage_dir, f"raft_node_{args.id}"), state, transport,
-                    snapshot_threshold=args.snapshot_threshold, sync=not args.no_fsync)
+                    snapshot_threshold=args.snapshot_threshold, sync=not args.no_fsync,
+                    native_sm=state.core)
     svc = ConfigService(state, raft)
     metrics = Registry()
     metrics.gauge("raft_role", "0=follower 1=candidate 2=leader",

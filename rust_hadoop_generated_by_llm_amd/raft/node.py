@@ -6,8 +6,9 @@ reference dfs/metaserver/src/simple_raft.rs). This module only adapts it to the 
 services:
 
 * proposals / ReadIndex return asyncio futures completed from native threads;
-* the state machine is either native (``native_sm``: the master's MasterCore, applied on
-  the Raft applier thread without the GIL) or a Python object (config server, tests),
+* the state machine is either native (``native_sm``: the master's MasterCore or the config
+  server's ConfigCore, applied on the Raft applier thread without the GIL) or a Python
+  object (tests),
   whose ``apply``/``snapshot``/``restore`` always run on the event loop thread (the
   native applier hands a committed batch over and waits), so service code never races
   the state machine;
