@@ -230,6 +230,33 @@ int main(int argc, char** argv) {
   }
   std::printf("\n  },\n");
 
+  // ---- K1b: batched scrub of HBM-resident blocks (kernel path only; no disk re-read)
+  if (device >= 0) {
+    StoreConfig cfg;
+    cfg.storage_dir = dir + "/scrub";
+    cfg.device = device;
+    cfg.hbm_capacity = 2ull << 30;
+    cfg.durability = Durability::HbmAck;
+    cfg.sync_writes = false;
+    ChunkStore s(cfg);
+    const int nb = 1024;
+    auto data = random_bytes((1 << 20) + 100, 11);
+    std::vector<std::string> ids;
+    for (int i = 0; i < nb; ++i) {
+      size_t sz = (i % 4 == 3) ? (1 << 20) + 100 : (1 << 20);  // every 4th block has a short tail slice
+      std::string id = "s" + std::to_string(i);
+      if (!s.stage(id, data.data(), sz, crc32(data.data(), sz)).ok) return 1;
+      ids.push_back(id);
+    }
+    s.scrub_resident(ids);  // warm-up (allocations, code object)
+    auto t0 = Clock::now();
+    auto bad = s.scrub_resident(ids);
+    auto t1 = Clock::now();
+    double bytes = nb * double(1 << 20) + (nb / 4) * 100.0;
+    std::printf("  \"scrub_hbm_1024x1MiB\": {\"seconds\": %.6f, \"GBps\": %.1f, \"bad\": %zu},\n", secs(t0, t1),
+                bytes / secs(t0, t1) / 1e9, bad.size());
+  }
+
   // ---- CRC: GPU (H2D + K1/K2) vs CPU PCLMUL, 256 MiB
   {
     const size_t n = 256u << 20;

@@ -273,6 +273,8 @@ PYBIND11_MODULE(_dfs_native, m) {
         return meta_image(v);
       })
       .def("scrub", &ChunkStore::scrub, py::call_guard<py::gil_scoped_release>())
+      .def("scrub_resident", &ChunkStore::scrub_resident, py::call_guard<py::gil_scoped_release>(),
+           "K1b only: verify the listed HBM-resident blocks against their .meta images")
       .def("list_blocks", &ChunkStore::list_blocks)
       .def("flush", &ChunkStore::flush, py::call_guard<py::gil_scoped_release>())
       .def("drop_resident", &ChunkStore::drop_resident, py::call_guard<py::gil_scoped_release>())

@@ -1365,6 +1365,69 @@ std::vector<uint32_t> ChunkStore::meta(const std::string& id) {
   return load_meta_file(id, cold, &ok);
 }
 
+// K1b: every resident block (pinned by the caller) verified against its HBM .meta image in
+// one kernel launch per 64K blocks, one sync, one small D2H of the per-block verdicts.
+std::vector<std::string> ChunkStore::scrub_resident(const std::vector<std::string>& ids) {
+  std::vector<std::string> bad;
+  if (!gpu() || ids.empty()) return bad;
+  HIP_OK(hipSetDevice(cfg_.device));
+  constexpr size_t kBatch = 65536;
+  const size_t cap = std::min(kBatch, ids.size());
+  ScrubBlock* dblocks = nullptr;
+  uint32_t* dbad = nullptr;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&dblocks), cap * sizeof(ScrubBlock)));
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&dbad), cap * sizeof(uint32_t)));
+  std::vector<ScrubBlock> hb;
+  std::vector<size_t> which;
+  std::vector<uint32_t> hbad;
+  Lane* l = acquire_lane();
+  for (size_t base = 0; base < ids.size(); base += kBatch) {
+    size_t cnt = std::min(kBatch, ids.size() - base);
+    hb.clear();
+    which.clear();
+    uint64_t tiles = 0;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t j = 0; j < cnt; ++j) {
+        auto it = index_.find(ids[base + j]);
+        if (it == index_.end() || it->second.dev_off < 0 || it->second.size == 0) continue;
+        uint64_t size = it->second.size;
+        const uint8_t* d = arena_ + it->second.dev_off;
+        ScrubBlock b{};
+        b.data = d;
+        b.meta = reinterpret_cast<const uint32_t*>(d + align_up(size, 256));
+        b.s_full = size / kSliceBytes;
+        b.tile_start = tiles;
+        b.tail_len = static_cast<uint32_t>(size % kSliceBytes);
+        b.tail_init = b.tail_len ? crc_init_term(b.tail_len) : 0;
+        tiles += (b.s_full + kSlicesPerTile - 1) / kSlicesPerTile;
+        hb.push_back(b);
+        which.push_back(base + j);
+      }
+    }
+    if (hb.empty()) continue;
+    HIP_OK(hipMemcpyAsync(dblocks, hb.data(), hb.size() * sizeof(ScrubBlock), hipMemcpyHostToDevice, l->stream));
+    HIP_OK(hipMemsetAsync(dbad, 0xFF, hb.size() * sizeof(uint32_t), l->stream));
+    ScrubLaunch a{};
+    a.blocks = dblocks;
+    a.nblocks = static_cast<uint32_t>(hb.size());
+    a.ntiles = tiles;
+    a.full_init = crc_init_term(kSliceBytes);
+    a.bad = dbad;
+    HIP_OK(launch_scrub(a, dtables_, l->stream));
+    launches_++;
+    hbad.resize(hb.size());
+    HIP_OK(hipMemcpyAsync(hbad.data(), dbad, hb.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+    for (size_t j = 0; j < hb.size(); ++j)
+      if (hbad[j] != 0xFFFFFFFFu) bad.push_back(ids[which[j]]);
+  }
+  release_lane(l);
+  (void)hipFree(dblocks);
+  (void)hipFree(dbad);
+  return bad;
+}
+
 std::vector<std::string> ChunkStore::scrub() {
   std::vector<std::string> bad;
   std::vector<std::string> resident, disk;
@@ -1380,44 +1443,7 @@ std::vector<std::string> ChunkStore::scrub() {
     }
   }
   if (!resident.empty()) {
-    HIP_OK(hipSetDevice(cfg_.device));
-    // One stream, one launch per block, one sync per batch: K1b batched verify.
-    constexpr size_t kBatch = 256;
-    uint32_t* dbad = nullptr;
-    HIP_OK(hipMalloc(reinterpret_cast<void**>(&dbad), kBatch * kMaxGridCrc * sizeof(uint32_t)));
-    std::vector<uint32_t> hbad(kBatch * kMaxGridCrc);
-    Lane* l = acquire_lane();
-    for (size_t base = 0; base < resident.size(); base += kBatch) {
-      size_t cnt = std::min(kBatch, resident.size() - base);
-      std::vector<int> grids(cnt, 0);
-      for (size_t j = 0; j < cnt; ++j) {
-        const std::string& id = resident[base + j];
-        uint64_t size;
-        const uint8_t* d;
-        {
-          std::lock_guard<std::mutex> g(mu_);
-          Block& b = index_[id];
-          size = b.size;
-          d = arena_ + b.dev_off;
-        }
-        if (size == 0) continue;
-        auto* dmeta = reinterpret_cast<const uint32_t*>(d + align_up(size, 256));
-        CrcPlan p = plan_crc(d, size, nullptr, dmeta, false, 0, size);
-        p.a.part_bad = dbad + j * kMaxGridCrc;
-        grids[j] = p.grid;
-        HIP_OK(launch_crc(p.a, dtables_, p.grid, l->stream));
-        launches_++;
-      }
-      HIP_OK(hipMemcpyAsync(hbad.data(), dbad, cnt * kMaxGridCrc * sizeof(uint32_t), hipMemcpyDeviceToHost, l->stream));
-      HIP_OK(hipStreamSynchronize(l->stream));
-      for (size_t j = 0; j < cnt; ++j) {
-        uint32_t m = 0xFFFFFFFFu;
-        for (int g = 0; g < grids[j]; ++g) m = std::min(m, hbad[j * kMaxGridCrc + g]);
-        if (m != 0xFFFFFFFFu) bad.push_back(resident[base + j]);
-      }
-    }
-    release_lane(l);
-    (void)hipFree(dbad);
+    for (auto& id : scrub_resident(resident)) bad.push_back(id);
     for (auto& id : resident) unpin(id);
   }
   for (auto& id : disk)

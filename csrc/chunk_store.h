@@ -153,6 +153,8 @@ class ChunkStore {
   std::vector<uint32_t> meta(const std::string& id);  // native-endian slice CRCs
   // Batched scrub (GPU verify of resident blocks + CPU verify of the rest).
   std::vector<std::string> scrub();
+  // GPU part only: verify the given resident blocks (caller keeps them pinned), K1b.
+  std::vector<std::string> scrub_resident(const std::vector<std::string>& ids);
   std::vector<std::string> list_blocks();
   StoreStats stats();
   void flush();          // wait until no dirty blocks remain

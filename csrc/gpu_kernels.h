@@ -3,7 +3,7 @@
 //                               whole-block CRC (shift-combine tree, per-workgroup partials).
 //   K3     same kernel in range/verify mode: recompute only touched slices and compare with
 //          the HBM-resident .meta image (reference verify_partial_read, chunkserver.rs:296-351).
-//   K1b    batched scrub: same kernel, verify mode over every resident block.
+//   K1b    crc_scrub_kernel: one launch verifies every resident block against its .meta.
 //   K4/K5  gf256_matmul_kernel: GF(2^8) matrix x shards (Reed-Solomon encode / reconstruct;
 //          reference erasure.rs:7-49).
 #pragma once
@@ -44,6 +44,27 @@ struct CrcLaunch {
   uint32_t* part_bad;             // [grid] min mismatching slice index, 0xFFFFFFFF = none
 };
 
+// K1b: one launch verifies many resident blocks against their HBM .meta images. Blocks are
+// laid out on a global tile axis (tile_start = prefix sum of ceil(s_full / 32)); each
+// workgroup finds its block by binary search, so every tile of every block is one
+// grid-stride step and the LDS table fill is paid once per workgroup per launch.
+struct ScrubBlock {
+  const uint8_t* data;
+  const uint32_t* meta;  // BE CRC per slice (HBM-resident .meta image)
+  uint64_t s_full;
+  uint64_t tile_start;
+  uint32_t tail_len;
+  uint32_t tail_init;
+};
+
+struct ScrubLaunch {
+  const ScrubBlock* blocks;  // device, sorted by tile_start
+  uint32_t nblocks;
+  uint64_t ntiles;
+  uint32_t full_init;
+  uint32_t* bad;  // [nblocks] min mismatching slice index, pre-set to 0xFFFFFFFF
+};
+
 struct GfLaunch {
   const uint8_t* in[kMaxShards];
   uint8_t* out[kMaxShards];
@@ -59,6 +80,7 @@ DevCrcTables* upload_crc_tables(hipStream_t s);
 int crc_grid_for(uint64_t ntiles, uint32_t has_tail);
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
 hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s);
+hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s);
 const uint8_t* upload_gf_tables(hipStream_t s);
 
 }  // namespace dfs

@@ -57,18 +57,62 @@ __device__ __forceinline__ uint32_t mat_apply(const uint32_t* col, uint32_t v, i
   return x;
 }
 
+__device__ __forceinline__ void load_tables(const DevCrcTables* __restrict__ gt, DevCrcTables* lt) {
+  const uint4* src = reinterpret_cast<const uint4*>(gt);
+  uint4* dst = reinterpret_cast<uint4*>(lt);
+  constexpr int n16 = sizeof(DevCrcTables) / 16;
+  for (int i = threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
+}
+
+// One 512 B slice per 8 lanes: lane `sl` hashes bytes [sl*64, sl*64+64), then the three
+// butterflies leave the slice CRC (raw, before the init term) in lane sl == 0.
+__device__ __forceinline__ uint32_t slice_crc(const DevCrcTables& lt, const uint8_t* slice, int sl, int lane,
+                                              bool valid) {
+  uint32_t r = 0;
+  if (valid) {
+    const uint4* p = reinterpret_cast<const uint4*>(slice + sl * 64);
+    uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
+    r = chunk16(lt.slice16, 0, c0);
+    r = chunk16(lt.slice16, r, c1);
+    r = chunk16(lt.slice16, r, c2);
+    r = chunk16(lt.slice16, r, c3);
+  }
+  r = combine(r, 1, lane, lt.sh64);
+  r = combine(r, 2, lane, lt.sh128);
+  return combine(r, 4, lane, lt.sh256);
+}
+
+// Short slice of `len` bytes, front-padded with zeros to 512 B (wave-wide call, lanes 0..7 work).
+__device__ __forceinline__ uint32_t tail_crc(const DevCrcTables& lt, const uint8_t* base, uint32_t len, int lane) {
+  const int sw = lane >> 3, sl = lane & 7;
+  const uint32_t pad = 512u - len;
+  uint32_t r = 0;
+  if (sw == 0) {
+    uint32_t words[16];
+    for (int q = 0; q < 16; ++q) {
+      uint32_t w = 0;
+      for (int b = 0; b < 4; ++b) {
+        uint32_t pos = sl * 64 + q * 4 + b;
+        uint32_t byte = pos >= pad ? base[pos - pad] : 0u;
+        w |= byte << (8 * b);
+      }
+      words[q] = w;
+    }
+    for (int q = 0; q < 4; ++q)
+      r = chunk16(lt.slice16, r, make_uint4(words[4 * q], words[4 * q + 1], words[4 * q + 2], words[4 * q + 3]));
+  }
+  r = combine(r, 1, lane, lt.sh64);
+  r = combine(r, 2, lane, lt.sh128);
+  return combine(r, 4, lane, lt.sh256);
+}
+
 __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
                                                                    const DevCrcTables* __restrict__ gt) {
   __shared__ DevCrcTables lt;
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t wg_bad;
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(gt);
-    uint4* dst = reinterpret_cast<uint4*>(&lt);
-    constexpr int n16 = sizeof(DevCrcTables) / 16;
-    for (int i = threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
-    if (threadIdx.x == 0) wg_bad = 0xFFFFFFFFu;
-  }
+  load_tables(gt, &lt);
+  if (threadIdx.x == 0) wg_bad = 0xFFFFFFFFu;
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -82,18 +126,7 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
     int64_t v = static_cast<int64_t>(t * kSlicesPerTile + wave * 8 + sw);
     int64_t i = static_cast<int64_t>(a.slice_lo) + v - static_cast<int64_t>(a.vfront);
     bool valid = i >= static_cast<int64_t>(a.slice_lo) && i < static_cast<int64_t>(a.slice_hi);
-    uint32_t r = 0;
-    if (valid) {
-      const uint4* p = reinterpret_cast<const uint4*>(a.data + static_cast<uint64_t>(i) * 512 + sl * 64);
-      uint4 c0 = p[0], c1 = p[1], c2 = p[2], c3 = p[3];
-      r = chunk16(lt.slice16, 0, c0);
-      r = chunk16(lt.slice16, r, c1);
-      r = chunk16(lt.slice16, r, c2);
-      r = chunk16(lt.slice16, r, c3);
-    }
-    r = combine(r, 1, lane, lt.sh64);
-    r = combine(r, 2, lane, lt.sh128);
-    r = combine(r, 4, lane, lt.sh256);
+    uint32_t r = slice_crc(lt, a.data + (valid ? static_cast<uint64_t>(i) * 512 : 0), sl, lane, valid);
     if (valid && sl == 0) {
       uint32_t be = __builtin_bswap32(r ^ a.full_init);
       if (a.meta_out) a.meta_out[i] = be;
@@ -121,26 +154,7 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
 
   // Short tail slice: front-pad the window with zeros (raw CRC is invariant to them).
   if (a.has_tail && blockIdx.x == 0 && wave == 0) {
-    const uint32_t pad = 512u - a.tail_len;
-    const uint8_t* base = a.data + a.s_full * 512;
-    uint32_t r = 0;
-    if (sw == 0) {
-      uint32_t words[16];
-      for (int q = 0; q < 16; ++q) {
-        uint32_t w = 0;
-        for (int b = 0; b < 4; ++b) {
-          uint32_t pos = sl * 64 + q * 4 + b;
-          uint32_t byte = pos >= pad ? base[pos - pad] : 0u;
-          w |= byte << (8 * b);
-        }
-        words[q] = w;
-      }
-      for (int q = 0; q < 4; ++q)
-        r = chunk16(lt.slice16, r, make_uint4(words[4 * q], words[4 * q + 1], words[4 * q + 2], words[4 * q + 3]));
-    }
-    r = combine(r, 1, lane, lt.sh64);
-    r = combine(r, 2, lane, lt.sh128);
-    r = combine(r, 4, lane, lt.sh256);
+    uint32_t r = tail_crc(lt, a.data + a.s_full * 512, a.tail_len, lane);
     if (lane == 0) {
       uint32_t be = __builtin_bswap32(r ^ a.tail_init);
       if (a.meta_out) a.meta_out[a.s_full] = be;
@@ -153,6 +167,42 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
   if (threadIdx.x == 0) {
     if (a.part_crc) a.part_crc[blockIdx.x] = acc;
     if (a.part_bad) a.part_bad[blockIdx.x] = wg_bad;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// K1b: batched scrub over many blocks in one launch (see ScrubLaunch).
+__global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_kernel(ScrubLaunch a, const DevCrcTables* __restrict__ gt) {
+  __shared__ DevCrcTables lt;
+  load_tables(gt, &lt);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int sw = lane >> 3, sl = lane & 7;
+  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    // last block whose tile range starts at or before t (workgroup-uniform)
+    uint32_t lo = 0, hi = a.nblocks;
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (a.blocks[mid].tile_start <= t) lo = mid;
+      else hi = mid;
+    }
+    const ScrubBlock& b = a.blocks[lo];
+    uint64_t i = (t - b.tile_start) * kSlicesPerTile + wave * 8 + sw;
+    bool valid = i < b.s_full;
+    uint32_t r = slice_crc(lt, b.data + (valid ? i * 512 : 0), sl, lane, valid);
+    if (valid && sl == 0 && b.meta[i] != __builtin_bswap32(r ^ a.full_init))
+      atomicMin(&a.bad[lo], static_cast<uint32_t>(i));
+  }
+  // short tail slices: one wave per block
+  const int waves = kCrcWgThreads / 64;
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * waves + wave; k < a.nblocks;
+       k += static_cast<uint64_t>(gridDim.x) * waves) {
+    const ScrubBlock& b = a.blocks[k];
+    if (!b.tail_len) continue;
+    uint32_t r = tail_crc(lt, b.data + b.s_full * 512, b.tail_len, lane);
+    if (lane == 0 && b.meta[b.s_full] != __builtin_bswap32(r ^ b.tail_init))
+      atomicMin(&a.bad[k], static_cast<uint32_t>(b.s_full));
   }
 }
 
@@ -258,6 +308,16 @@ int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
   hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s) {
+  if (a.nblocks == 0) return hipSuccess;
+  uint64_t g = a.ntiles < 2048 ? a.ntiles : 2048;
+  uint64_t tail_waves = (a.nblocks + 3) / 4;
+  if (g < tail_waves) g = tail_waves < 2048 ? tail_waves : 2048;
+  if (g == 0) g = 1;
+  hipLaunchKernelGGL(crc_scrub_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
   return hipGetLastError();
 }
 

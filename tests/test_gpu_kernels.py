@@ -75,6 +75,27 @@ def test_gpu_corruption_detected_full_and_partial(gstore):
     gstore.remove("corrupt")
 
 
+def test_gpu_batched_scrub_finds_exactly_the_corrupt_blocks(gstore):
+    # K1b: one launch over blocks of every shape (tiny, exact slices, tails, multi-tile);
+    # corrupt a middle slice, a last full slice and a tail byte in different blocks
+    sizes = [1, 100, 511, 512, 513, 4096, 16384 + 1, 65536, (1 << 20), (1 << 20) + 300, 3 * (1 << 20) + 7]
+    ids = []
+    for i, n in enumerate(sizes * 3):
+        bid = f"scrub{i}"
+        d = os.urandom(n)
+        assert gstore.write(bid, d, zlib.crc32(d))[0]
+        ids.append((bid, n))
+    assert gstore.scrub_resident([b for b, _ in ids]) == []
+    targets = {ids[9][0]: 600000, ids[10 + 11][0]: 3 * (1 << 20) + 3, ids[2 * 11 + 7][0]: 65535,
+               ids[4][0]: 512}
+    for bid, off in targets.items():
+        assert gstore.debug_corrupt(bid, off), bid
+    found = gstore.scrub_resident([b for b, _ in ids])
+    assert sorted(found) == sorted(targets)
+    for bid, _ in ids:
+        gstore.remove(bid)
+
+
 def test_gpu_eviction_and_promotion(native, tmp_path):
     s = native.ChunkStore(str(tmp_path), "", 0, 8 << 20, 0, 100, 2, 1, False)
     blobs = {f"e{i}": os.urandom(1 << 20) for i in range(20)}
