@@ -248,7 +248,8 @@ def main():
             pdir = os.path.abspath(os.path.join(a.profile_dir, f"cs{rank}"))
             os.makedirs(pdir, exist_ok=True)
             cs_env["TMPDIR"] = "/tmp"
-            cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", pdir,
+            cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "--output-format", "csv",
+                                  "-d", pdir,
                                   "-o", "cs", "--", sys.executable, "-m", *args],
                                  str(base_p / f"cs{rank}.log"), cs_env)
         else:

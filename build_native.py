@@ -81,12 +81,14 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
     out = ext_path()
     if clean or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(out), *map(str, objs),
-                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lcrypto", "-lpthread",
+                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto", "-lpthread",
                 f"-Wl,-rpath,{ROCM}/lib"]
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     build_tools(objs, flags, clean, headers)
+    if os.environ.get("DFS_BUILD_SANITIZERS", "1") == "1":
+        build_sanitized(clean=clean)
     return out
 
 
@@ -104,10 +106,39 @@ def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[P
                 raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
         if clean or not exe.exists() or any(o.stat().st_mtime > exe.stat().st_mtime for o in [obj, *runtime]):
             r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-o", str(exe), str(obj), *map(str, runtime),
-                                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lcrypto", "-lpthread",
+                                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto", "-lpthread",
                                 f"-Wl,-rpath,{ROCM}/lib"], capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"link failed: {exe}\n{r.stdout}\n{r.stderr}")
+        outs.append(exe)
+    return outs
+
+
+# Host-only runtime sources the native unit tests need (no HIP): they also build with the
+# host compiler under ASan/UBSan and TSan (SURVEY §5.2 — the reference has no sanitizer runs).
+SANITIZE_SOURCES = ["json.cpp", "json_dump.cpp", "shard_map.cpp", "raft.cpp", "wal.cpp", "crc32.cpp", "gf256.cpp",
+                    "disk_gate.cpp", "extent_alloc.cpp"]
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+def build_sanitized(kinds=("asan", "tsan"), clean: bool = False) -> list[Path]:
+    """build/native/unit_tests_<kind>: the native unit tests + host runtime under a sanitizer
+    (host clang++, -O1 -g). GPU code never gets sanitizer instrumentation."""
+    outs = []
+    srcs = [CSRC / n for n in SANITIZE_SOURCES] + [CSRC / "bench" / "unit_tests.cpp"]
+    headers = sorted(CSRC.glob("*.h"))
+    for kind in kinds:
+        exe = BUILD / f"unit_tests_{kind}"
+        newest = max(p.stat().st_mtime for p in srcs + headers)
+        if clean or not exe.exists() or exe.stat().st_mtime < newest:
+            # LLVM's runtime (not GCC 11's) intercepts pthread_cond_clockwait, which libstdc++
+            # uses for condition_variable::wait_for; without it TSan misreads every timed wait
+            cmd = [f"{ROCM}/llvm/bin/clang++", "-std=c++17", "-O1", "-g", "-pthread", *SANITIZERS[kind],
+                   f"-I{CSRC}", "-o", str(exe), *map(str, srcs)]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"sanitizer build failed ({kind}):\n{r.stdout}\n{r.stderr}")
         outs.append(exe)
     return outs
 

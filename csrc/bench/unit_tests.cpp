@@ -27,9 +27,9 @@
 #include <thread>
 #include <vector>
 
-#include "chunk_store.h"
 #include "crc32.h"
 #include "disk_gate.h"
+#include "extent_alloc.h"
 #include "gf256.h"
 #include "json.h"
 #include "raft.h"

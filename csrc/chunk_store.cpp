@@ -1,5 +1,6 @@
 // ChunkStore implementation. See chunk_store.h for the design.
 #include "chunk_store.h"
+#include "trace.h"
 
 #include <dirent.h>
 #include <fcntl.h>
@@ -128,51 +129,6 @@ void mkdirs(const std::string& path) {
 }
 
 }  // namespace
-
-// ---------------------------------------------------------------- ExtentAllocator
-ExtentAllocator::ExtentAllocator(uint64_t capacity) : cap_(capacity) {
-  if (capacity) free_[0] = capacity;
-}
-
-int64_t ExtentAllocator::alloc(uint64_t bytes) {
-  if (bytes == 0) bytes = 256;
-  for (auto it = free_.begin(); it != free_.end(); ++it) {
-    if (it->second >= bytes) {
-      uint64_t off = it->first, len = it->second;
-      free_.erase(it);
-      if (len > bytes) free_[off + bytes] = len - bytes;
-      used_ += bytes;
-      return static_cast<int64_t>(off);
-    }
-  }
-  return -1;
-}
-
-void ExtentAllocator::free(uint64_t off, uint64_t bytes) {
-  if (bytes == 0) bytes = 256;
-  used_ -= bytes;
-  auto next = free_.lower_bound(off);
-  if (next != free_.begin()) {
-    auto prev = std::prev(next);
-    if (prev->first + prev->second == off) {
-      off = prev->first;
-      bytes += prev->second;
-      free_.erase(prev);
-    }
-  }
-  next = free_.lower_bound(off);
-  if (next != free_.end() && off + bytes == next->first) {
-    bytes += next->second;
-    free_.erase(next);
-  }
-  free_[off] = bytes;
-}
-
-uint64_t ExtentAllocator::largest_free() const {
-  uint64_t m = 0;
-  for (auto& kv : free_) m = std::max(m, kv.second);
-  return m;
-}
 
 // ---------------------------------------------------------------- ChunkStore
 ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
@@ -588,6 +544,7 @@ void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, ui
 // are fdatasync'ed from the caller's host buffer before the block becomes visible.
 WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
                                    bool durable_now) {
+  TraceRange tr(durable_now ? "dfs.store.write" : "dfs.store.stage");
   HIP_OK(hipSetDevice(cfg_.device));
   WriteResult res;
   DevExtent ext = reserve(n);
@@ -670,6 +627,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
 }
 
 bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64_t n, std::string* err) {
+  TraceRange tr("dfs.store.persist");
   if (!gpu() || cfg_.durability == Durability::HbmAck) return true;
   std::shared_ptr<std::vector<uint8_t>> meta;
   const uint8_t* d = nullptr;
@@ -802,6 +760,7 @@ ReadResult ChunkStore::stat(const std::string& id, uint64_t offset, uint64_t len
 }
 
 ReadResult ChunkStore::read_into(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out) {
+  TraceRange tr("dfs.store.read");
   if (!gpu()) return read_host(id, offset, bytes, out);
   HIP_OK(hipSetDevice(cfg_.device));
   ReadResult r;
@@ -1368,6 +1327,7 @@ std::vector<uint32_t> ChunkStore::meta(const std::string& id) {
 // K1b: every resident block (pinned by the caller) verified against its HBM .meta image in
 // one kernel launch per 64K blocks, one sync, one small D2H of the per-block verdicts.
 std::vector<std::string> ChunkStore::scrub_resident(const std::vector<std::string>& ids) {
+  TraceRange tr("dfs.store.scrub");
   std::vector<std::string> bad;
   if (!gpu() || ids.empty()) return bad;
   HIP_OK(hipSetDevice(cfg_.device));
@@ -1550,6 +1510,7 @@ bool ChunkStore::debug_corrupt(const std::string& id, uint64_t offset) {
 
 bool ChunkStore::gf_matmul_gpu(const std::vector<std::vector<uint8_t>>& mat, const std::vector<const uint8_t*>& in,
                                const std::vector<uint8_t*>& out, uint64_t len) {
+  TraceRange tr("dfs.store.rs_matmul");
   if (!gpu()) return false;
   int k = static_cast<int>(in.size()), rows = static_cast<int>(out.size());
   if (k > kMaxShards || rows > kMaxShards || static_cast<int>(mat.size()) != rows) return false;

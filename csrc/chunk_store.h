@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "disk_gate.h"
+#include "extent_alloc.h"
 #include "gpu_kernels.h"
 
 namespace dfs {
@@ -80,21 +81,6 @@ struct StoreStats {
   uint64_t crc_mismatches = 0;
   uint64_t gpu_kernel_launches = 0;
   uint64_t disk_gate_waits = 0;  // durable writes that queued for a node-wide disk slot
-};
-
-// First-fit extent allocator over [0, capacity) with coalescing.
-class ExtentAllocator {
- public:
-  explicit ExtentAllocator(uint64_t capacity = 0);
-  int64_t alloc(uint64_t bytes);  // -1 when no fit
-  void free(uint64_t off, uint64_t bytes);
-  uint64_t used() const { return used_; }
-  uint64_t capacity() const { return cap_; }
-  uint64_t largest_free() const;
-
- private:
-  uint64_t cap_, used_ = 0;
-  std::map<uint64_t, uint64_t> free_;  // off -> len
 };
 
 // Group commit of data files: callers that finished writing share one syncfs() round.

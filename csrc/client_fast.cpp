@@ -1,4 +1,5 @@
 #include "client_fast.h"
+#include "trace.h"
 
 #include <fcntl.h>
 #include <openssl/evp.h>
@@ -301,6 +302,7 @@ bool FastClient::fp_call(uint8_t op, const std::string& body, uint8_t* status, u
 
 FastClient::Status FastClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
                                      std::string* msg, Times* t) {
+  TraceRange tr("dfs.client.write");
   if (!base_ || n > slot_bytes_) return NotHandled;
   std::string sock = master_socket(path);
   if (sock.empty()) return NotHandled;
@@ -418,6 +420,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
 
 FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg,
                                     Times* t) {
+  TraceRange tr("dfs.client.read");
   if (!base_) return NotHandled;
   std::string sock = master_socket(path);
   if (sock.empty()) return NotHandled;

@@ -1,4 +1,5 @@
 #include "rccl_engine.h"
+#include "trace.h"
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -260,6 +261,7 @@ void RcclEngine::abort_pair(int src, int dst) {
 }
 
 int64_t RcclEngine::send(int peer, const std::string& id, uint64_t* size, std::string* err) {
+  TraceRange tr("dfs.rccl.send");
   Pair* p = pair(rank_, peer);
   if (!p || p->broken) {
     *err = "no RCCL path to rank " + std::to_string(peer);
@@ -295,6 +297,7 @@ int64_t RcclEngine::send(int peer, const std::string& id, uint64_t* size, std::s
 }
 
 bool RcclEngine::wait_send(int peer, int64_t seq, std::string* err) {
+  TraceRange tr("dfs.rccl.wait_send");
   Pair* p = pair(rank_, peer);
   if (!p) return false;
   Pair::Pending pend;
@@ -320,6 +323,7 @@ bool RcclEngine::wait_send(int peer, int64_t seq, std::string* err) {
 
 WriteResult RcclEngine::recv(int src, int64_t seq, const std::string& id, uint64_t size, uint32_t expected_crc,
                              bool persist_now) {
+  TraceRange tr("dfs.rccl.recv");
   WriteResult res;
   Pair* p = pair(src, rank_);
   if (!p || p->broken) {

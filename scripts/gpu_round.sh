@@ -21,7 +21,7 @@ if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
 fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "micro" ]; then
   # native I/O + kernel microbenchmark (C45) under a kernel trace
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv \
      -d "$OLDPWD/gpurun_out/prof_io" -o io -- "$OLDPWD/build/native/io_bench" --iters 30) \
      > gpurun_out/io_bench.json 2> gpurun_out/io_bench.err || exit $?
 fi

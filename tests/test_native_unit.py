@@ -1,7 +1,8 @@
 """Runs the native C++ unit tests (csrc/bench/unit_tests.cpp, built by build_native.py into
 build/native/unit_tests): JSON, shard map, joint majority, extent allocator, CRC, RS codec,
 WAL torn tails, disk gate and in-memory Raft clusters with partitions. One pytest case per
-native test so a failure names it."""
+native test so a failure names it. The same tests also run whole under AddressSanitizer +
+UBSan and ThreadSanitizer (host code only), where any report fails the case."""
 import subprocess
 from pathlib import Path
 
@@ -34,3 +35,20 @@ def test_unit_test_binary_exists():
 def test_native(name):
     r = subprocess.run([str(EXE), name], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and f"ok {name}" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_native_under_sanitizer(kind, tmp_path):
+    exe = ROOT / "build" / "native" / f"unit_tests_{kind}"
+    if not exe.exists() or exe.stat().st_mtime < SRC.stat().st_mtime:
+        import sys
+        sys.path.insert(0, str(ROOT))
+        import build_native
+
+        build_native.build_sanitized([kind])
+    env = {"PATH": "/usr/bin:/bin", "TMPDIR": str(tmp_path),
+           "ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "TSAN_OPTIONS": "halt_on_error=0:exitcode=66"}
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600, env=env)
+    out = r.stdout + r.stderr
+    assert "Sanitizer" not in r.stderr, out[-4000:]
+    assert r.returncode == 0 and "FAIL" not in r.stdout, out[-4000:]
