@@ -32,6 +32,7 @@
 #include "extent_alloc.h"
 #include "gf256.h"
 #include "json.h"
+#include "master_core.h"
 #include "raft.h"
 #include "shard_map.h"
 #include "wal.h"
@@ -473,6 +474,121 @@ TEST(raft_leadership_transfer) {
   CHECK(c.nodes[l]->transfer_leadership(target + 1));
   CHECK(eventually([&] { return c.nodes[target]->is_leader(); }, 5));
   CHECK(c.propose(target, Json("after").dump()) == 0);
+}
+
+// ------------------------------------------------------------------------------- MasterCore
+// The native master state machine on a real single-node Raft, hammered by concurrent
+// clients through its hot handlers (the calls the native client makes), while the applier
+// and access-stats threads run: under TSan this is the master's race check.
+struct SmHost : raft::Host {
+  std::shared_ptr<raft::StateMachine> sm;
+  std::vector<std::string> apply(const std::vector<std::pair<uint64_t, std::string>>& c) override {
+    return sm->apply(c);
+  }
+  std::string snapshot() override { return sm->snapshot(); }
+  void restore(const std::string& s) override { sm->restore(s); }
+  bool send(const std::string&, const std::string&, const std::string&, std::string*) override { return false; }
+};
+
+TEST(master_core_concurrent_create_complete_read_delete) {
+  std::string d = tmpdir("mcore");
+  auto core = std::make_shared<MasterCore>();
+  auto host = std::make_shared<SmHost>();
+  host->sm = core;
+  raft::Options o;
+  o.id = 1;
+  o.members = {{1, "n1"}};
+  o.client_address = "n1";
+  o.dir = d;
+  o.election_lo = 0.05;
+  o.election_hi = 0.1;
+  o.heartbeat = 0.02;
+  o.sync = false;
+  o.snapshot_threshold = 200;  // compaction happens during the run
+  raft::Node node(o, host);
+  node.start();
+  CHECK(eventually([&] { return node.is_leader(); }, 3));
+  core->attach(&node);
+  core->set_access_stats(true, 20);
+  core->exit_safe_mode();
+  for (int i = 0; i < 4; ++i) {
+    ChunkServerStatus st;
+    st.address = "cs" + std::to_string(i) + ":1";
+    st.last_heartbeat = std::chrono::duration_cast<std::chrono::milliseconds>(
+                            std::chrono::system_clock::now().time_since_epoch()).count();
+    st.available_space = 1ull << 40;
+    st.rack_id = "r" + std::to_string(i % 2);
+    core->upsert_chunk_server(st);
+  }
+  const int threads = 6, per = 25;
+  std::atomic<int> failures{0};
+  std::vector<std::string> errs(threads);
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      auto fail = [&](const std::string& why) {
+        ++failures;
+        errs[t] = why;
+      };
+      for (int i = 0; i < per; ++i) {
+        std::string path = "/t" + std::to_string(t) + "/f" + std::to_string(i), out;
+        pb::CreateFileRequest c;
+        c.path = path;
+        c.allocate_block = true;
+        c.defer_create = true;
+        c.preferred_chunk_server = "cs" + std::to_string(t % 4) + ":1";
+        if (core->handle("CreateFile", c.str(), &out) != MasterCore::OK) return fail("create rpc: " + out);
+        pb::CreateFileResponse cr;
+        if (!cr.decode(out) || !cr.success || !cr.has_allocation) return fail("create: " + cr.error_message);
+        const auto& alloc = cr.allocation;
+        if (alloc.chunk_server_addresses.size() != 3) return fail("placement size");
+        pb::CompleteFileRequest done;
+        done.path = path;
+        done.size = 1 + i;
+        done.etag_md5 = "etag";
+        done.create = true;
+        done.blocks.push_back(alloc.block);
+        pb::BlockChecksumInfo sum;
+        sum.block_id = alloc.block.block_id;
+        sum.actual_size = 1 + i;
+        done.block_checksums.push_back(sum);
+        if (core->handle("CompleteFile", done.str(), &out) != MasterCore::OK) return fail("complete rpc: " + out);
+        pb::CompleteFileResponse dr;
+        if (!dr.decode(out) || !dr.success) return fail("complete: " + dr.error_message);
+        pb::GetFileInfoRequest g;
+        g.path = path;
+        if (core->handle("GetFileInfo", g.str(), &out) != MasterCore::OK) return fail("info rpc: " + out);
+        pb::GetFileInfoResponse gr;
+        if (!gr.decode(out) || !gr.found || gr.metadata.size != static_cast<uint64_t>(1 + i)) return fail("info");
+        if (i % 3 == 0) {
+          pb::DeleteFileRequest del;
+          del.path = path;
+          if (core->handle("DeleteFile", del.str(), &out) != MasterCore::OK) return fail("delete rpc: " + out);
+          pb::DeleteFileResponse dd;
+          if (!dd.decode(out) || !dd.success) return fail("delete: " + dd.error_message);
+        }
+      }
+      pb::ListFilesRequest l;
+      l.path = "/t" + std::to_string(t) + "/";
+      std::string out;
+      if (core->handle("ListFiles", l.str(), &out) != MasterCore::OK) return fail("list rpc: " + out);
+      pb::ListFilesResponse lr;
+      lr.decode(out);
+      if (lr.files.size() != static_cast<size_t>(per - (per + 2) / 3)) return fail("list size " + std::to_string(lr.files.size()));
+    });
+  for (auto& th : ts) th.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw Failure("worker: " + e);
+  CHECK(failures.load() == 0);
+  CHECK(core->file_count() == static_cast<size_t>(threads * (per - (per + 2) / 3)));
+  CHECK(core->take_gc().size() > 0);  // deleted files' blocks are queued for DELETE commands
+  // the snapshot of the live state restores to an identical state machine
+  MasterCore copy;
+  copy.restore(core->snapshot());
+  CHECK(copy.file_count() == core->file_count());
+  core->detach();
+  node.stop();
+  std::filesystem::remove_all(d);
 }
 
 }  // namespace
