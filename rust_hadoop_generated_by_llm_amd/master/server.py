@@ -147,6 +147,15 @@ class MasterProcess:
         app.router.add_get("/shard_map", shard_map)
         for k in ("vote", "append", "snapshot", "timeout_now"):
             app.router.add_post(f"/raft/{k}", raft_route(k))
+        if os.environ.get("DFS_DEBUG_ENDPOINTS") == "1":
+            # fault injection for process-level chaos tests (the reference uses Toxiproxy):
+            # {"block": [raft peer http addresses]} drops this node's traffic to them
+            async def partition(req):
+                body = await req.json()
+                self.transport.blocked = {HttpTransport._base(a) for a in body.get("block", [])}
+                return web.json_response({"blocked": sorted(self.transport.blocked)})
+
+            app.router.add_post("/debug/partition", partition)
         return app
 
     async def run(self, ready_file: str | None = None) -> None:

@@ -26,6 +26,18 @@ class HttpTransport:
         self.timeout = timeout
         self.ssl_ctx = ssl_ctx
         self._session = None
+        # peers this process may not reach (network-partition injection for process-level
+        # chaos tests; set through the master's /debug/partition when DFS_DEBUG_ENDPOINTS=1)
+        self.blocked: set[str] = set()
+
+    @staticmethod
+    def _base(addr: str) -> str:
+        a = addr.rstrip("/")
+        return a if a.startswith("http") else "http://" + a
+
+    def _check(self, addr: str) -> None:
+        if self.blocked and self._base(addr) in self.blocked:
+            raise TransportError(f"{addr}: partitioned")
 
     async def _sess(self):
         if self._session is None:
@@ -39,6 +51,7 @@ class HttpTransport:
         return self._session
 
     async def send(self, addr: str, kind: str, payload: dict) -> dict:
+        self._check(addr)
         tries, backoff = _RETRY.get(kind, (1, 0.0))
         sess = await self._sess()
         url = addr.rstrip("/") + f"/raft/{kind}"
@@ -60,6 +73,7 @@ class HttpTransport:
     async def send_raw(self, addr: str, kind: str, body: str) -> str:
         """Same as :meth:`send` with the JSON body already encoded (the native node builds
         AppendEntries text directly from its log)."""
+        self._check(addr)
         tries, backoff = _RETRY.get(kind, (1, 0.0))
         sess = await self._sess()
         url = addr.rstrip("/") + f"/raft/{kind}"

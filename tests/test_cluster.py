@@ -500,3 +500,75 @@ def test_idle_shard_merges_and_becomes_standby():
         assert json.load(urllib.request.urlopen(f"{http}/shard_map"))["shard_id"] == ""
         pool.close()
         c.close()
+
+
+def _partition(http_addr: str, block: list[str]) -> None:
+    req = urllib.request.Request(http_addr + "/debug/partition", data=json.dumps({"block": block}).encode(),
+                                 headers={"Content-Type": "application/json"}, method="POST")
+    urllib.request.urlopen(req, timeout=5).read()
+
+
+def test_network_partition_isolates_leader_then_heals():
+    """network_partition_test.sh / the linearizability 'network_partition' scenario, on real
+    processes: cut the metadata leader off from its two followers (both directions), the
+    majority elects a new leader and keeps accepting writes, the isolated old leader must not
+    answer a read with stale state, and after healing every master converges."""
+    with LocalCluster(n_chunkservers=3, masters_per_shard=3, fsync=False,
+                      env={"DFS_DEBUG_ENDPOINTS": "1"}) as cl:
+        c = cl.client(initial_backoff_ms=100, max_retries=30, rpc_timeout=3.0)
+        c.create_file_from_buffer(b"before", "/np/before")
+        pool = ChannelPool()
+
+        def roles():
+            out = {}
+            for m in cl.master_addrs:
+                try:
+                    out[m] = pool.call(m, "MasterService", "GetClusterInfo", pb.GetClusterInfoRequest(), timeout=3)
+                except grpc.RpcError:
+                    pass
+            return out
+
+        old = next(m for m, i in roles().items() if i.role == "Leader")
+        old_http = cl.master_http[old]
+        others = [cl.master_http[m] for m in cl.master_addrs if m != old]
+        _partition(old_http, others)
+        for h in others:
+            _partition(h, [old_http])
+
+        deadline = time.time() + 60
+        while True:  # the client finds the majority side's new leader
+            try:
+                c.create_file_from_buffer(b"during", "/np/during")
+                break
+            except (DfsError, grpc.RpcError):
+                if time.time() > deadline:
+                    raise
+                time.sleep(0.3)
+        new = [m for m, i in roles().items() if i.role == "Leader" and m != old]
+        assert new, "the majority side must have elected a leader"
+
+        # the isolated node may still believe it leads, but a read there must not return
+        # the pre-partition view (the file written on the majority side would be missing)
+        try:
+            r = pool.call(old, "MasterService", "GetFileInfo", pb.GetFileInfoRequest(path="/np/during"), timeout=4)
+            assert r.found, "stale read served by an isolated leader"
+        except grpc.RpcError as e:
+            assert e.code() in (grpc.StatusCode.UNAVAILABLE, grpc.StatusCode.DEADLINE_EXCEEDED,
+                                grpc.StatusCode.FAILED_PRECONDITION, grpc.StatusCode.OUT_OF_RANGE), e
+
+        for h in [old_http, *others]:
+            _partition(h, [])
+        deadline = time.time() + 60
+        while True:  # healed: one leader, and the old one has caught up
+            info = roles()
+            leaders = [m for m, i in info.items() if i.role == "Leader"]
+            if len(leaders) == 1 and old in info and info[old].commit_index >= info[leaders[0]].commit_index > 0:
+                break
+            assert time.time() < deadline, {m: (i.role, i.current_term, i.commit_index) for m, i in info.items()}
+            time.sleep(0.3)
+        assert c.get_file_content("/np/before") == b"before"
+        assert c.get_file_content("/np/during") == b"during"
+        c.create_file_from_buffer(b"after", "/np/after")
+        assert c.get_file_content("/np/after") == b"after"
+        pool.close()
+        c.close()
