@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--workdir", default=None)
     p.add_argument("--timeout", type=float, default=1500.0)
     p.add_argument("--keep", action="store_true")
+    p.add_argument("--cleanup", choices=["auto", "always", "never"], default="auto",
+                   help="delete the run's data at exit (auto: only when disk space runs low)")
     p.add_argument("--rehearse-rccl", action="store_true",
                    help="bring RCCL up even when ranks share a GPU (it must fail cleanly and every "
                         "rank must fall back together) - a 1-GPU rehearsal of the failure path")
@@ -401,8 +403,28 @@ def main():
                 dist.destroy_process_group()
             except Exception:  # noqa: BLE001
                 pass
-        if not a.keep and rank == 0:
+        if rank == 0 and _should_clean(a, base):
             shutil.rmtree(base, ignore_errors=True)
+
+
+def _should_clean(a, base: str) -> bool:
+    """Whether to delete this run's data directory at exit.
+
+    Like `dfs_cli benchmark` (which never deletes what it wrote), the written blocks stay
+    on disk by default while the volume keeps plenty of room: measured on the MI355X boxes
+    (profiles/r1_disk/keep_vs_delete.md), deleting a run's ~1 GB of fsynced 1 MiB files makes
+    the NEXT durable-write run on the same overlay volume 1.4-2.4x slower for minutes, which
+    would leak one run's cleanup into the next run's timed region. `--cleanup always` deletes
+    anyway; `auto` deletes only when free space would drop below max(20 GiB, 25 % of the disk)."""
+    if a.keep or a.cleanup == "never":
+        return False
+    if a.cleanup == "always":
+        return True
+    try:
+        du = shutil.disk_usage(base)
+    except OSError:
+        return True
+    return du.free < max(20 << 30, du.total // 4)
 
 
 if __name__ == "__main__":
