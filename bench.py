@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--timeout", type=float, default=1500.0)
     p.add_argument("--keep", action="store_true")
     p.add_argument("--cleanup", choices=["auto", "always", "never"], default="auto",
-                   help="delete the run's data at exit (auto: only when disk space runs low)")
+                   help="delete the run's data at exit (auto: only when the disk is nearly full)")
     p.add_argument("--rehearse-rccl", action="store_true",
                    help="bring RCCL up even when ranks share a GPU (it must fail cleanly and every "
                         "rank must fall back together) - a 1-GPU rehearsal of the failure path")
@@ -192,8 +192,13 @@ def main():
 
     threading.Thread(target=watchdog, daemon=True).start()
 
-    base = bcast(a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=os.environ.get("TMPDIR", "/tmp")))
+    if rank == 0 and not a.workdir:
+        _make_room(Path(os.environ.get("TMPDIR", "/tmp")), _bytes_needed(a, n))
+    base = bcast((a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=os.environ.get("TMPDIR", "/tmp")))
+                 if rank == 0 else None)
     base_p = Path(base)
+    if rank == 0:
+        (base_p / ".dfs_bench").touch()  # marks a directory _make_room may reclaim later
     (base_p / f"rank{rank}").mkdir(parents=True, exist_ok=True)
     env = dict(os.environ)
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
@@ -407,6 +412,30 @@ def main():
             shutil.rmtree(base, ignore_errors=True)
 
 
+def _bytes_needed(a, n: int) -> int:
+    """Block bytes this run leaves on the node's volume (every replica of every file)."""
+    rf = min(3, n)
+    return n * rf * (a.steps + a.warmup) * a.count * (a.size + a.size // 128 + 4096)
+
+
+def _make_room(parent: Path, need: int) -> None:
+    """Reclaim earlier runs' data (oldest first) only when this run would not fit otherwise."""
+    try:
+        free = shutil.disk_usage(parent).free
+    except OSError:
+        return
+    want = int(need * 1.15) + (2 << 30)
+    if free >= want:
+        return
+    olds = sorted((d for d in parent.glob("dfs_bench_*") if (d / ".dfs_bench").exists()),
+                  key=lambda d: d.stat().st_mtime)
+    for d in olds:
+        print(f"[bench] reclaiming {d} for {need >> 20} MiB of new data", file=sys.stderr, flush=True)
+        shutil.rmtree(d, ignore_errors=True)
+        if shutil.disk_usage(parent).free >= want:
+            return
+
+
 def _should_clean(a, base: str) -> bool:
     """Whether to delete this run's data directory at exit.
 
@@ -415,7 +444,8 @@ def _should_clean(a, base: str) -> bool:
     (profiles/r1_disk/keep_vs_delete.md), deleting a run's ~1 GB of fsynced 1 MiB files makes
     the NEXT durable-write run on the same overlay volume 1.4-2.4x slower for minutes, which
     would leak one run's cleanup into the next run's timed region. `--cleanup always` deletes
-    anyway; `auto` deletes only when free space would drop below max(20 GiB, 25 % of the disk)."""
+    anyway; `auto` deletes only when the disk is getting full (free < max(10 GiB, 10 %)), and
+    a later run reclaims kept data itself if it would not fit (`_make_room`)."""
     if a.keep or a.cleanup == "never":
         return False
     if a.cleanup == "always":
@@ -424,7 +454,7 @@ def _should_clean(a, base: str) -> bool:
         du = shutil.disk_usage(base)
     except OSError:
         return True
-    return du.free < max(20 << 30, du.total // 4)
+    return du.free < max(10 << 30, du.total // 10)
 
 
 if __name__ == "__main__":
