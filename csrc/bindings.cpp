@@ -12,6 +12,7 @@
 #include "fastpath.h"
 #include "gf256.h"
 #include "rccl_engine.h"
+#include "sigv4.h"
 #include "wal.h"
 
 namespace py = pybind11;
@@ -472,6 +473,29 @@ PYBIND11_MODULE(_dfs_native, m) {
     return crypto::rsa_sha256_verify(n, e, msg, sig);
   });
   m.def("random_bytes", [](size_t n) { return py::bytes(crypto::random_bytes(n)); });
+
+  // ---------------- SigV4 (sigv4.h)
+  m.def("sigv4_uri_encode", &sigv4::uri_encode, py::arg("s"), py::arg("encode_slash") = true);
+  m.def("sigv4_normalize_query", &sigv4::normalize_query);
+  m.def("sigv4_signing_key", [](const std::string& secret, const std::string& date, const std::string& region,
+                                const std::string& service) {
+    return py::bytes(sigv4::signing_key(secret, date, region, service));
+  });
+  m.def("sigv4_signature", [](py::bytes key, const std::string& sts) { return sigv4::signature(key, sts); });
+  m.def("sigv4_canonical_request", [](const std::string& method, const std::string& path, const std::string& query,
+                                      std::vector<std::pair<std::string, std::string>> headers,
+                                      const std::string& signed_headers, const std::string& payload_hash) {
+    return sigv4::canonical_request({method, path, query, std::move(headers), signed_headers, payload_hash});
+  });
+  m.def("sigv4_verify", [](const std::string& method, const std::string& path, const std::string& query,
+                           std::vector<std::pair<std::string, std::string>> headers, const std::string& signed_headers,
+                           const std::string& payload_hash, const std::string& timestamp, const std::string& scope,
+                           py::bytes key, const std::string& sig) {
+    std::string creq;
+    bool ok = sigv4::verify({method, path, query, std::move(headers), signed_headers, payload_hash}, timestamp, scope,
+                            key, sig, &creq);
+    return py::make_tuple(ok, creq);
+  });
 
   // ---------------- node-wide disk admission (disk_gate.h)
   py::class_<DiskGate::Slot>(m, "DiskSlot")

@@ -1,0 +1,35 @@
+// AWS Signature Version 4 on the server side (C08 signing, C10 URI encoding; reference
+// dfs/common/src/auth/{signing,encoding}.rs and s3_server auth_middleware.rs:676-716):
+// canonical request, string to sign, the HMAC-SHA256 key chain and a constant-time
+// signature check, on OpenSSL. The S3 gateway verifies every signed request through here.
+#pragma once
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace dfs::sigv4 {
+
+// Percent-encoding with uppercase hex; unreserved = A-Z a-z 0-9 - _ . ~
+std::string uri_encode(const std::string& s, bool encode_slash);
+// Sort key=value pairs of a raw query, dropping X-Amz-Signature (values stay as sent).
+std::string normalize_query(const std::string& raw);
+
+struct Request {
+  std::string method, path, query;                        // path/query already canonical
+  std::vector<std::pair<std::string, std::string>> headers;  // lower-case names, canonical values, sorted
+  std::string signed_headers;                               // "host;x-amz-date"
+  std::string payload_hash;
+};
+
+std::string canonical_request(const Request& r);
+std::string sha256_hex(const std::string& data);
+std::string string_to_sign(const std::string& timestamp, const std::string& scope, const std::string& creq);
+std::string signing_key(const std::string& secret, const std::string& date, const std::string& region,
+                        const std::string& service);  // 32 raw bytes
+std::string signature(const std::string& key, const std::string& sts);  // lower-case hex
+// Constant-time comparison of the expected signature with `sig`; *creq receives the
+// canonical request (for the SignatureDoesNotMatch diagnostics).
+bool verify(const Request& r, const std::string& timestamp, const std::string& scope, const std::string& key,
+            const std::string& sig, std::string* creq);
+
+}  // namespace dfs::sigv4

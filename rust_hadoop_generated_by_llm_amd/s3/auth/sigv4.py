@@ -13,8 +13,9 @@ Behavioural parity with the reference:
   (s3_server/src/handlers.rs:291-320);
 * presigned URL generation (auth/presign.rs:17-88).
 
-HMAC/SHA-256 come from OpenSSL through :mod:`hashlib`/:mod:`hmac` (C, GIL released for
-large inputs).
+URI encoding, query normalisation, the canonical request, the signing-key chain and the
+constant-time signature check run natively (csrc/sigv4.cpp on OpenSSL); the aws-chunked
+chain and the client-side helpers use :mod:`hashlib`/:mod:`hmac`.
 """
 from __future__ import annotations
 
@@ -27,6 +28,7 @@ from dataclasses import dataclass, field
 from datetime import datetime, timezone
 from urllib.parse import parse_qsl, unquote
 
+from ...native import lib as _native
 from .errors import AuthError
 
 ALGORITHM = "AWS4-HMAC-SHA256"
@@ -34,9 +36,6 @@ UNSIGNED_PAYLOAD = "UNSIGNED-PAYLOAD"
 EMPTY_SHA256 = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 MAX_PRESIGN_EXPIRES = 604_800
 MAX_SKEW_MINUTES = 15
-
-_UNRESERVED = frozenset(b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789_.-~")
-
 
 @dataclass
 class ParsedCredentials:
@@ -64,15 +63,7 @@ class SigningInput:
 
 
 def uri_encode(s: str, encode_slash: bool = True) -> str:
-    out = []
-    for b in s.encode("utf-8"):
-        if b in _UNRESERVED:
-            out.append(chr(b))
-        elif b == 0x2F and not encode_slash:
-            out.append("/")
-        else:
-            out.append(f"%{b:02X}")
-    return "".join(out)
+    return _native.sigv4_uri_encode(s, encode_slash)
 
 
 def _split_cred(cred: str) -> list[str]:
@@ -125,47 +116,35 @@ def parse_query(raw: str) -> dict[str, str]:
 
 
 def normalize_query_string(raw: str) -> str:
-    pairs = []
-    for p in raw.split("&"):
-        if not p or p == "X-Amz-Signature" or p.startswith("X-Amz-Signature="):
-            continue
-        k, _, v = p.partition("=")
-        pairs.append((k, v))
-    pairs.sort()
-    return "&".join(f"{k}={v}" for k, v in pairs)
+    return _native.sigv4_normalize_query(raw)
+
+
+def _canon_headers(inp: SigningInput) -> list[tuple[str, str]]:
+    return [(name, ",".join(values)) for name, values in inp.headers.items()]
 
 
 def canonical_request(inp: SigningInput) -> str:
-    lines = [inp.method, inp.path, inp.query_string]
-    for name, values in inp.headers.items():
-        lines.append(f"{name}:{','.join(values)}")
-    return "\n".join(lines) + "\n\n" + inp.signed_headers_list + "\n" + inp.payload_hash
+    return _native.sigv4_canonical_request(inp.method, inp.path, inp.query_string, _canon_headers(inp),
+                                           inp.signed_headers_list, inp.payload_hash)
 
 
 def string_to_sign(timestamp: str, scope: str, creq: str) -> str:
     return f"{ALGORITHM}\n{timestamp}\n{scope}\n{hashlib.sha256(creq.encode()).hexdigest()}"
 
 
-def _hmac(key: bytes, msg: str) -> bytes:
-    return hmac.new(key, msg.encode(), hashlib.sha256).digest()
-
-
 def derive_signing_key(secret: str, date: str, region: str, service: str) -> bytes:
-    k = _hmac(("AWS4" + secret).encode(), date)
-    k = _hmac(k, region)
-    k = _hmac(k, service)
-    return _hmac(k, "aws4_request")
+    return _native.sigv4_signing_key(secret, date, region, service)
 
 
 def calculate_signature(signing_key: bytes, sts: str) -> str:
-    return hmac.new(signing_key, sts.encode(), hashlib.sha256).hexdigest()
+    return _native.sigv4_signature(signing_key, sts)
 
 
 def verify_signature_with_key(inp: SigningInput, cred: ParsedCredentials, signing_key: bytes) -> None:
-    creq = canonical_request(inp)
-    sts = string_to_sign(cred.timestamp, cred.scope, creq)
-    expected = calculate_signature(signing_key, sts)
-    if not hmac.compare_digest(expected.encode(), cred.signature.encode()):
+    ok, creq = _native.sigv4_verify(inp.method, inp.path, inp.query_string, _canon_headers(inp),
+                                    inp.signed_headers_list, inp.payload_hash, cred.timestamp, cred.scope,
+                                    signing_key, cred.signature)
+    if not ok:
         raise AuthError("signature_mismatch", f"canonical request:\n{creq}")
 
 
