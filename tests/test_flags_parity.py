@@ -1,0 +1,51 @@
+"""Flag names and defaults of every binary match the reference (SURVEY §5.6 table:
+bin/master.rs:21-80, bin/config_server.rs:19-48, bin/chunkserver.rs:33-72,
+dfs_cli.rs:16-43,131-171), so the reference's scripts and compose command lines translate 1:1."""
+from rust_hadoop_generated_by_llm_amd.chunkserver.server import build_parser as cs_parser
+from rust_hadoop_generated_by_llm_amd.cli.dfs_cli import build_parser as cli_parser
+from rust_hadoop_generated_by_llm_amd.config_server.server import build_parser as config_parser
+from rust_hadoop_generated_by_llm_amd.master.server import build_parser as master_parser
+
+
+def test_master_flags_and_defaults():
+    a = master_parser().parse_args([])
+    assert a.addr == "127.0.0.1:50051" and a.id == 1 and a.http_port == 8080
+    assert a.storage_dir == "/tmp/raft-logs" and a.shard_id == "shard-0"
+    assert (a.split_threshold_rps, a.split_cooldown_secs, a.merge_threshold_rps) == (100.0, 30, 1.0)
+    assert a.backup_bucket == "dfs-backups"
+    a = master_parser().parse_args(["-a", "0.0.0.0:1", "--peers", "x,y", "--config-servers", "c", "--tls-cert", "t",
+                                    "--tls-key", "k", "--ca-cert", "ca", "--domain-name", "d",
+                                    "--backup-s3-endpoint", "http://s3", "--advertise-addr", "h:1",
+                                    "--shard-config", "f.json"])
+    assert a.addr == "0.0.0.0:1" and a.peers == "x,y" and a.domain_name == "d"
+
+
+def test_config_server_flags_and_defaults():
+    a = config_parser().parse_args([])
+    assert (a.addr, a.id, a.http_port, a.storage_dir) == ("127.0.0.1:50052", 1, 8081, "/tmp/config-raft-logs")
+    config_parser().parse_args(["--peers", "p", "--advertise-addr", "a", "--tls-cert", "c", "--tls-key", "k",
+                                "--ca-cert", "ca"])
+
+
+def test_chunkserver_flags_and_defaults():
+    a = cs_parser().parse_args([])
+    assert a.addr == "127.0.0.1:50052" and a.storage_dir == "/tmp/chunkserver_data" and a.http_port == 8082
+    assert a.rack_id == ""
+    a = cs_parser().parse_args(["--config-servers", "c", "--cold-storage-dir", "/c", "--advertise-addr", "h",
+                                "--tls-cert", "t", "--tls-key", "k", "--ca-cert", "ca", "--domain-name", "d",
+                                "--gpu", "3", "--hbm-capacity", "64G", "--durability", "hbm-ack",
+                                "--rccl-rank", "1", "--rccl-world", "8", "--replication-transport", "grpc"])
+    assert a.gpu == 3 and a.durability == "hbm-ack" and a.replication_transport == "grpc"
+
+
+def test_dfs_cli_flags_and_benchmark_defaults():
+    p = cli_parser()
+    a = p.parse_args(["ls"])
+    assert a.master == "http://127.0.0.1:50051" and a.max_retries == 5 and a.initial_backoff_ms == 500
+    a = p.parse_args(["benchmark", "write"])
+    assert (a.count, a.size, a.concurrency, a.prefix) == (100, 1048576, 10, "bench_write")
+    a = p.parse_args(["benchmark", "stress-write"])
+    assert (a.duration, a.prefix) == (30, "bench_stress")
+    a = p.parse_args(["--host-alias", "a=b", "--host-alias", "c=d", "--ca-cert", "x", "--domain-name", "y",
+                      "--config-servers", "c1", "ls"])
+    assert a.host_alias == ["a=b", "c=d"]
