@@ -59,6 +59,11 @@ def parse():
     p.add_argument("--rehearse-rccl", action="store_true",
                    help="bring RCCL up even when ranks share a GPU (it must fail cleanly and every "
                         "rank must fall back together) - a 1-GPU rehearsal of the failure path")
+    p.add_argument("--stress-seconds", type=float, default=0.0,
+                   help="after the timed write+read steps, also run `dfs_cli benchmark stress-write` "
+                        "for this long per rank (0 = skip); reported under stress_write")
+    p.add_argument("--stress-size", type=int, default=10240)
+    p.add_argument("--stress-concurrency", type=int, default=5)
     p.add_argument("--profile-dir", default=None,
                    help="run each ChunkServer under rocprofv3 --kernel-trace --stats, output here")
     return p.parse_args()
@@ -198,6 +203,7 @@ def main():
                  if rank == 0 else None)
     base_p = Path(base)
     if rank == 0:
+        base_p.mkdir(parents=True, exist_ok=True)
         (base_p / ".dfs_bench").touch()  # marks a directory _make_room may reclaim later
     (base_p / f"rank{rank}").mkdir(parents=True, exist_ok=True)
     env = dict(os.environ)
@@ -347,6 +353,17 @@ def main():
         cpu1 = cpu_snapshot()
         host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
 
+        stress = None
+        if a.stress_seconds > 0:
+            # the reference's only published throughput (stress-write 30 s, 10240 B,
+            # conc 5 -> 470 ops/s); run outside the timed region, same cluster, every rank at once
+            from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_stress_write
+
+            barrier()
+            ss = bench_stress_write(client, a.stress_seconds, a.stress_size, a.stress_concurrency,
+                                    prefix=prefix_of(rank) + "/stress")
+            stress = {"ops": ss.count, "seconds": ss.total_s, "errors": ss.errors, "lat": ss.latencies,
+                      "first_error": getattr(ss, "first_error", "")}
         stats = {}
         try:
             import urllib.request
@@ -355,7 +372,7 @@ def main():
         except Exception:  # noqa: BLE001
             pass
         allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
-                       "rt": rt, "cs": stats, "rccl": cs_info.get("rccl", False),
+                       "rt": rt, "cs": stats, "stress": stress, "rccl": cs_info.get("rccl", False),
                        "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                    for k, v in (client.phase_times or {}).items() if v}})
         if rank == 0:
@@ -395,6 +412,17 @@ def main():
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],
             }
+            if a.stress_seconds > 0:
+                slat = sorted(x for r in allr for x in r["stress"]["lat"])
+                ops = sum(r["stress"]["ops"] for r in allr) / max(r["stress"]["seconds"] for r in allr)
+                result["stress_write"] = {
+                    "seconds": a.stress_seconds, "size": a.stress_size, "concurrency_per_rank": a.stress_concurrency,
+                    "ops_per_s": round(ops, 1), "mb_per_s": round(ops * a.stress_size / (1 << 20), 2),
+                    "errors": sum(r["stress"]["errors"] for r in allr),
+                    "first_error": next((r["stress"]["first_error"] for r in allr if r["stress"]["first_error"]), ""),
+                    "avg_ms": round(1e3 * sum(slat) / max(1, len(slat)), 3), "p50_ms": round(pct(slat, 50), 3),
+                    "p95_ms": round(pct(slat, 95), 3), "p99_ms": round(pct(slat, 99), 3),
+                    "vs_published_470_ops_per_s": round(ops / 470.0, 1)}
             print(json.dumps(result), flush=True)
         barrier()
         tpool.shutdown(wait=False)

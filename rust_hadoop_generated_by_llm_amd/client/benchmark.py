@@ -141,6 +141,7 @@ def bench_stress_write(client, duration: float = 30, size: int = 1 << 20, concur
     errors = [0]
     lock = threading.Lock()
     counter = [0]
+    first_error: list[str] = []
 
     def worker(w: int):
         while time.perf_counter() < deadline:
@@ -152,9 +153,11 @@ def bench_stress_write(client, duration: float = 30, size: int = 1 << 20, concur
                 client.create_file_from_buffer(payloads[i % len(payloads)], f"{prefix}/{run_id}/stress_{w}_{i}")
                 with lock:
                     lat.append(time.perf_counter() - t0)
-            except Exception:  # noqa: BLE001
+            except Exception as e:  # noqa: BLE001
                 with lock:
                     errors[0] += 1
+                    if not first_error:
+                        first_error.append(f"{type(e).__name__}: {e}"[:300])
 
     t0 = time.perf_counter()
     threads = [threading.Thread(target=worker, args=(w,)) for w in range(concurrency)]
@@ -162,4 +165,6 @@ def bench_stress_write(client, duration: float = 30, size: int = 1 << 20, concur
         t.start()
     for t in threads:
         t.join()
-    return Stats("Stress Write", len(lat), size, time.perf_counter() - t0, lat, errors[0])
+    st = Stats("Stress Write", len(lat), size, time.perf_counter() - t0, lat, errors[0])
+    st.first_error = first_error[0] if first_error else ""
+    return st

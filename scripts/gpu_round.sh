@@ -90,4 +90,10 @@ if [ "$STEP" = "diag2" ]; then
   sleep 30 && \
   { TIMEFORMAT="later user=%U sys=%S wall=%R"; time timeout -k 10 200 build/native/io_bench --disk-sweep --dir ./iob --cases "$C" ; } >> $D 2>&1 || exit $?
 fi
+if [ "$STEP" = "stress" ]; then
+  # the reference's published config: stress-write 30 s, 10240 B, concurrency 5 (470 ops/s)
+  timeout -k 10 600 python bench.py --steps 1 --warmup 1 --stress-seconds 30 > gpurun_out/bench_stress_nvme.json 2> gpurun_out/bench_stress_nvme.err && \
+  timeout -k 10 600 python bench.py --steps 1 --warmup 1 --stress-seconds 30 --durability hbm-ack > gpurun_out/bench_stress_hbm.json 2> gpurun_out/bench_stress_hbm.err && \
+  timeout -k 10 600 python bench.py --steps 1 --warmup 1 --stress-seconds 60 --stress-size 1048576 --stress-concurrency 10 > gpurun_out/bench_stress_1m.json 2> gpurun_out/bench_stress_1m.err || exit $?
+fi
 echo "gpu_round done"
