@@ -47,7 +47,8 @@ def parse():
     p.add_argument("--concurrency", type=int, default=10)
     p.add_argument("--durability", choices=["nvme-sync", "hbm-ack"], default="nvme-sync")
     p.add_argument("--hbm-capacity", default="32G")
-    p.add_argument("--transport", choices=["rccl", "grpc"], default="rccl")
+    p.add_argument("--transport", choices=["rccl", "grpc", "socket"], default="rccl",
+                   help="replica payload path between ranks (socket: host-memory P2P, CPU rehearsal)")
     p.add_argument("--shards", choices=["per-gpu", "one"], default="per-gpu",
                    help="metadata shards: one per GPU rank (default) or a single master")
     p.add_argument("--cpu", action="store_true", help="CPU chunk store (plumbing config 1)")
@@ -249,7 +250,10 @@ def main():
                 "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
                 "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
                 "--heartbeat-interval", "0.5", "--scrub-interval", "3600", "--rccl-timeout-ms", "90000"]
-        if n > 1 and not a.cpu and a.transport == "rccl" and (not shared_gpu or a.rehearse_rccl):
+        if n > 1 and a.transport == "socket":
+            args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
+                     str(base_p / "rccl_rdv"), "--replication-transport", "socket"]
+        elif n > 1 and not a.cpu and a.transport == "rccl" and (not shared_gpu or a.rehearse_rccl):
             args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
                      str(base_p / "rccl_rdv")]
         else:
@@ -396,7 +400,7 @@ def main():
                            "files_per_gpu_per_step": a.count, "file_size": a.size, "concurrency": a.concurrency,
                            "replication_factor": min(3, n), "durability": a.durability,
                            "store": "cpu" if a.cpu else "hbm",
-                           "transport": ("grpc" if (a.cpu or shared_gpu) else a.transport) if n > 1 else "local"},
+                           "transport": observed_transport(allr, n)},
                 "write_mb_per_s": round(sum(r["wbytes"] for r in allr) / (1 << 20) / wmax, 2),
                 "read_mb_per_s": round(sum(r["rbytes"] for r in allr) / (1 << 20) / rmax, 2),
                 "write_p50_ms": round(pct(wlat, 50), 3), "write_p95_ms": round(pct(wlat, 95), 3),
@@ -404,9 +408,12 @@ def main():
                 "read_p95_ms": round(pct(rlat, 95), 3), "read_p99_ms": round(pct(rlat, 99), 3),
                 "write_ops_per_s": round(len(wlat) / wmax, 1),
                 "rccl_ranks": sum(1 for r in allr if r["rccl"]),
-                "rccl_forwards": sum(r["cs"].get("rccl_forwards", 0) for r in allr),
-                "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
-                "rccl_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) for r in allr),
+                "repl_pairs_up": sum(r["cs"].get("repl_pairs_up", 0) for r in allr),
+                **forward_counts(allr),
+                "rccl_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) + r["cs"].get("fp_p2p_fallbacks", 0)
+                                      for r in allr),
+                "replica_failures": sum(r["cs"].get("fp_replica_failures", 0) for r in allr),
+                "repl_pair_failures": sum(r["cs"].get("repl_pair_failures", 0) for r in allr),
                 "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
                 "disk_gate_waits": sum(r["cs"].get("disk_gate_waits", 0) for r in allr),
                 "host_cpu_util_rank0": allr[0]["cpu"],
@@ -438,6 +445,31 @@ def main():
                 pass
         if rank == 0 and _should_clean(a, base):
             shutil.rmtree(base, ignore_errors=True)
+
+
+def forward_counts(allr) -> dict:
+    """Replica hops as the chunkservers counted them (native fast path + gRPC service)."""
+    return {
+        "rccl_forwards": sum(r["cs"].get("fp_rccl_forwards", 0) + r["cs"].get("rccl_forwards", 0) for r in allr),
+        "shm_forwards": sum(r["cs"].get("fp_shm_forwards", 0) for r in allr),
+        "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
+    }
+
+
+def observed_transport(allr, n: int) -> str:
+    """config.transport from what the replicas actually travelled over, not from flags: "local"
+    (RF 1), "rccl" / "shm" / "grpc" when one path carried every hop, else "mixed(...)"."""
+    if n <= 1:
+        return "local"
+    c = forward_counts(allr)
+    p2p = {r["cs"].get("repl_transport") for r in allr} - {None}
+    p2p_name = p2p.pop() if len(p2p) == 1 else "rccl"  # "socket" in CPU rehearsals
+    used = {(p2p_name if k.startswith("rccl") else k.split("_")[0]): v for k, v in c.items() if v}
+    if not used:
+        return "none"
+    if len(used) == 1:
+        return next(iter(used))
+    return "mixed(" + ",".join(f"{k}={v}" for k, v in sorted(used.items())) + ")"
 
 
 def _bytes_needed(a, n: int) -> int:

@@ -11,7 +11,7 @@
 #include "disk_gate.h"
 #include "fastpath.h"
 #include "gf256.h"
-#include "rccl_engine.h"
+#include "replication.h"
 #include "sigv4.h"
 #include "wal.h"
 
@@ -356,7 +356,11 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("adopt_term", &FastPathServer::adopt_term)
       .def_property_readonly("term", &FastPathServer::term)
       .def("drain_suspects", &FastPathServer::drain_suspects)
-      .def("set_rccl", &FastPathServer::set_rccl, py::arg("engine"), py::keep_alive<1, 2>())
+      .def("set_replication", [](FastPathServer& f, ReplicationEngine& e) {
+        f.set_replication(&e);
+        e.set_control([&f](int rank, const std::string& req, std::string* reply) { return f.control(rank, req, reply); });
+      }, py::arg("engine"), py::keep_alive<1, 2>(), py::keep_alive<2, 1>())
+      .def("debug_drop_descriptors", &FastPathServer::debug_drop_descriptors)
       .def("set_peer", &FastPathServer::set_peer, py::arg("addr"), py::arg("rank"), py::arg("name") = "")
       .def("set_self_host", &FastPathServer::set_self_host, py::arg("host"))
       .def("stats", [](FastPathServer& f) {
@@ -371,57 +375,115 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["fp_rccl_forwards"] = s.rccl_forwards;
         d["fp_shm_forwards"] = s.shm_forwards;
         d["fp_forward_failures"] = s.forward_failures;
+        d["fp_replica_failures"] = s.replica_failures;
+        d["fp_p2p_fallbacks"] = s.p2p_fallbacks;
+        d["fp_rejected_peers"] = s.rejected_peers;
         return d;
       });
 
-  py::class_<RcclEngine>(m, "RcclEngine")
-      .def(py::init<ChunkStore*, int, int, std::string, int>(), py::keep_alive<1, 2>(), py::arg("store"),
-           py::arg("rank"), py::arg("world"), py::arg("rendezvous_dir"), py::arg("timeout_ms") = 30000)
-      .def("init", [](RcclEngine& e) {
+  struct PyTicket {
+    ReplTicket t;
+    py::object keep;  // host source bytes stay alive until wait_send
+  };
+  py::class_<PyTicket>(m, "ReplTicket")
+      .def_property_readonly("peer", [](PyTicket& k) { return k.t.peer; })
+      .def_property_readonly("gen", [](PyTicket& k) { return k.t.gen; })
+      .def_property_readonly("seq", [](PyTicket& k) { return k.t.seq; })
+      .def_property_readonly("size", [](PyTicket& k) { return k.t.size; })
+      .def_property_readonly("slice", [](PyTicket& k) { return k.t.slice; });
+
+  py::class_<ReplicationEngine>(m, "ReplicationEngine")
+      .def(py::init([](ChunkStore* store, const std::string& transport, int rank, int world, const std::string& ns,
+                       int open_timeout_ms, int turn_timeout_ms, int xfer_timeout_ms) {
+             std::string err;
+             std::unique_ptr<P2PTransport> t;
+             if (transport == "rccl") t = make_rccl_transport(store->config().device, rank, &err);
+             else if (transport == "socket") t = make_socket_transport(rank, ns);
+             else err = "unknown transport " + transport;
+             if (!t) throw std::runtime_error(err);
+             ReplOptions o;
+             o.open_timeout_ms = open_timeout_ms;
+             o.turn_timeout_ms = turn_timeout_ms;
+             o.xfer_timeout_ms = xfer_timeout_ms;
+             return std::make_unique<ReplicationEngine>(store, std::move(t), rank, world, o);
+           }),
+           py::keep_alive<1, 2>(), py::arg("store"), py::arg("transport"), py::arg("rank"), py::arg("world"),
+           py::arg("ns") = "", py::arg("open_timeout_ms") = 20000, py::arg("turn_timeout_ms") = 3000,
+           py::arg("xfer_timeout_ms") = 20000)
+      .def("start", &ReplicationEngine::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &ReplicationEngine::stop, py::call_guard<py::gil_scoped_release>())
+      .def("wait_ready", &ReplicationEngine::wait_ready, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &ReplicationEngine::rank)
+      .def_property_readonly("world", &ReplicationEngine::world)
+      .def_property_readonly("transport", &ReplicationEngine::transport_name)
+      .def("pair_ok", &ReplicationEngine::pair_ok, py::call_guard<py::gil_scoped_release>())
+      .def("generation", &ReplicationEngine::generation, py::call_guard<py::gil_scoped_release>())
+      .def("fail_pair", &ReplicationEngine::fail_pair, py::call_guard<py::gil_scoped_release>())
+      .def("slice_for", &ReplicationEngine::slice_for)
+      .def("send", [](ReplicationEngine& e, int peer, const std::string& id, py::object data) -> py::tuple {
+        auto k = std::make_unique<PyTicket>();
+        std::string err;
+        const uint8_t* src = nullptr;
+        uint64_t n = 0;
+        if (!data.is_none()) {
+          py::buffer_info bi = py::buffer(data).request();
+          src = static_cast<const uint8_t*>(bi.ptr);
+          n = static_cast<uint64_t>(bi.size * bi.itemsize);
+          k->keep = data;
+        }
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = e.send(peer, id, src, n, &k->t, &err);
+        }
+        if (!ok) return py::make_tuple(py::none(), err);
+        return py::make_tuple(py::cast(std::move(k)), std::string());
+      }, py::arg("peer"), py::arg("block_id"), py::arg("data") = py::none())
+      .def("wait_send", [](ReplicationEngine& e, PyTicket& k) {
         std::string err;
         bool ok;
         {
           py::gil_scoped_release r;
-          ok = e.init(&err);
+          ok = e.wait_send(&k.t, &err);
         }
+        k.keep = py::none();
         return py::make_tuple(ok, err);
       })
-      .def_property_readonly("ready", &RcclEngine::ready)
-      .def_property_readonly("rank", &RcclEngine::rank)
-      .def_property_readonly("world", &RcclEngine::world)
-      .def("pair_ok", &RcclEngine::pair_ok)
-      .def("abort_pair", &RcclEngine::abort_pair, py::call_guard<py::gil_scoped_release>())
-      .def("send", [](RcclEngine& e, int peer, const std::string& id) {
-        std::string err;
-        uint64_t size = 0;
-        int64_t seq;
+      .def("cancel_send", [](ReplicationEngine& e, PyTicket& k, const std::string& why) {
         {
           py::gil_scoped_release r;
-          seq = e.send(peer, id, &size, &err);
+          e.cancel_send(&k.t, why);
         }
-        return py::make_tuple(seq, size, err);
+        k.keep = py::none();
       })
-      .def("wait_send", [](RcclEngine& e, int peer, int64_t seq) {
-        std::string err;
-        bool ok;
-        {
-          py::gil_scoped_release r;
-          ok = e.wait_send(peer, seq, &err);
-        }
-        return py::make_tuple(ok, err);
-      })
-      .def("recv", [](RcclEngine& e, int src, int64_t seq, const std::string& id, uint64_t size, uint32_t crc,
-                      bool persist) {
+      .def("recv", [](ReplicationEngine& e, int src, uint64_t gen, int64_t seq, const std::string& id, uint64_t size,
+                      uint64_t slice, uint32_t crc, bool persist) {
         WriteResult w;
         {
           py::gil_scoped_release r;
-          w = e.recv(src, seq, id, size, crc, persist);
+          w = e.recv(src, gen, seq, id, size, slice, crc, persist);
         }
         return py::make_tuple(w.ok, w.actual_crc, w.error);
-      }, py::arg("src"), py::arg("seq"), py::arg("block_id"), py::arg("size"), py::arg("crc"),
-         py::arg("persist") = true)
-      .def_property_readonly("bytes_sent", &RcclEngine::bytes_sent)
-      .def_property_readonly("bytes_recv", &RcclEngine::bytes_recv);
+      }, py::arg("src"), py::arg("gen"), py::arg("seq"), py::arg("block_id"), py::arg("size"), py::arg("slice"),
+         py::arg("crc"), py::arg("persist") = true)
+      .def("debug_drop_sends", [](ReplicationEngine& e, int peer, int n) { e.transport()->debug_drop_sends(peer, n); })
+      .def("debug_stall", [](ReplicationEngine& e, int peer, int ms) { e.transport()->debug_stall(peer, ms); })
+      .def("stats", [](ReplicationEngine& e) {
+        ReplStats s = e.stats();
+        py::dict d;
+        d["bytes_sent"] = s.bytes_sent;
+        d["bytes_recv"] = s.bytes_recv;
+        d["blocks_sent"] = s.blocks_sent;
+        d["blocks_recv"] = s.blocks_recv;
+        d["pair_failures"] = s.pair_failures;
+        d["pair_opens"] = s.pair_opens;
+        d["open_attempts"] = s.open_attempts;
+        d["turn_timeouts"] = s.turn_timeouts;
+        d["stale_generation"] = s.stale_generation;
+        return d;
+      })
+      .def_property_readonly("bytes_sent", [](ReplicationEngine& e) { return e.stats().bytes_sent; })
+      .def_property_readonly("bytes_recv", [](ReplicationEngine& e) { return e.stats().bytes_recv; });
 
   // ---------------- WAL
   py::class_<Wal>(m, "Wal")

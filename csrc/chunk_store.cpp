@@ -215,7 +215,11 @@ void ChunkStore::scan_dirs() {
     if (!d) return;
     while (dirent* e = ::readdir(d)) {
       std::string name = e->d_name;
-      if (name == "." || name == ".." || ends_with(name, ".meta") || ends_with(name, ".tmp")) continue;
+      if (ends_with(name, ".tmp")) {  // a write that crashed before its rename
+        ::unlink((dir + "/" + name).c_str());
+        continue;
+      }
+      if (name == "." || name == ".." || ends_with(name, ".meta")) continue;
       int64_t sz = file_size(dir + "/" + name);
       if (sz < 0) continue;
       Block& b = index_[name];
@@ -558,17 +562,21 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   // .meta (known only after the CRC kernel) follows. A checksum mismatch removes the file.
   std::future<bool> data_file;
   std::string data_err;
+  // Both files go to private temporary names and are renamed over the block only after the
+  // checksum verified: a rejected or failed write never destroys an earlier durable copy
+  // of the same id (e.g. a retry on gRPC after a fast-path punt).
+  const std::string tmp_sfx = "." + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
+  const std::string dp_tmp = data_path(id, false) + tmp_sfx, mp_tmp = meta_path(id, false) + tmp_sfx;
   if (sync_now && !gsync_) {
-    std::string dp = data_path(id, false);
-    data_file = std::async(std::launch::async, [this, dp, data, n, &data_err] {
+    data_file = std::async(std::launch::async, [this, dp_tmp, data, n, &data_err] {
       DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
-      return write_file_durable(dp, data, n, &data_err);
+      return write_file_durable(dp_tmp, data, n, &data_err);
     });
   }
   auto abandon_data_file = [&] {
     if (data_file.valid()) {
       data_file.get();
-      ::unlink(data_path(id, false).c_str());
+      ::unlink(dp_tmp.c_str());
     }
   };
   Lane* l = acquire_lane();
@@ -607,11 +615,20 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
   release_lane(l);
   if (data_file.valid()) {
-    bool mok = write_file_durable(meta_path(id, false), meta->data(), S * 4, &err);
+    bool mok = write_file_durable(mp_tmp, meta->data(), S * 4, &err);
     bool dok = data_file.get();
+    if (mok && dok) {
+      // data first: a crash between the renames leaves new data under the old .meta,
+      // which verification reports as corrupt (recovered from a replica), never silently
+      if (::rename(dp_tmp.c_str(), data_path(id, false).c_str()) != 0 ||
+          ::rename(mp_tmp.c_str(), meta_path(id, false).c_str()) != 0) {
+        mok = false;
+        err = errno_str("rename " + dp_tmp);
+      }
+    }
     if (!mok || !dok) {
-      ::unlink(data_path(id, false).c_str());
-      ::unlink(meta_path(id, false).c_str());
+      ::unlink(dp_tmp.c_str());
+      ::unlink(mp_tmp.c_str());
       release(ext);
       res.error = dok ? err : data_err;
       return res;
@@ -1119,6 +1136,90 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
   insert_resident(id, ext, n, co.block_crc, sync_now, meta);
   res.ok = true;
   return res;
+}
+
+bool ChunkStore::recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n) {
+  rv->ext = e;
+  rv->n = n;
+  rv->lane = acquire_lane();
+  return true;
+}
+
+bool ChunkStore::recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi) {
+  if (rv->failed || hi <= lo) return !rv->failed;
+  Lane* l = static_cast<Lane*>(rv->lane);
+  (void)hipSetDevice(cfg_.device);
+  auto* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(rv->n, 1), 256));
+  // range mode writing (not verifying) the slices of [lo, hi): full slices via the tile
+  // loop, the short tail slice when the range reaches the end of the block
+  CrcPlan p = plan_crc(rv->ext.ptr, rv->n, dmeta, nullptr, false, lo, hi);
+  if (p.grid == 0) return true;
+  hipError_t e = launch_crc(p.a, dtables_, p.grid, l->stream);
+  launches_++;
+  if (e != hipSuccess) {
+    rv->failed = true;
+    rv->error = std::string("crc kernel launch: ") + hipGetErrorString(e);
+  }
+  return !rv->failed;
+}
+
+WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint32_t expected_crc, bool persist_now) {
+  TraceRange tr("dfs.store.recv_commit");
+  WriteResult res;
+  Lane* l = static_cast<Lane*>(rv->lane);
+  (void)hipSetDevice(cfg_.device);
+  uint64_t n = rv->n, S = num_slices(n);
+  auto* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
+  ensure_hscratch(l, S * 4 + 16);
+  uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+  if (!rv->failed && S) HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+  HIP_OK(hipStreamSynchronize(l->stream));
+  auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
+  release_lane(l);
+  rv->lane = nullptr;
+  if (rv->failed) {
+    release(rv->ext);
+    res.error = rv->error;
+    return res;
+  }
+  std::vector<uint32_t> native(S);
+  for (uint64_t i = 0; i < S; ++i) {
+    uint32_t be;
+    std::memcpy(&be, meta->data() + 4 * i, 4);
+    native[i] = __builtin_bswap32(be);
+  }
+  uint32_t crc = crc32_from_slices(native.data(), n);
+  res.actual_crc = crc;
+  if (expected_crc != 0 && crc != expected_crc) {
+    release(rv->ext);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      ++st_.crc_mismatches;
+    }
+    res.error = "Replication checksum mismatch: expected " + std::to_string(expected_crc) + ", actual " +
+                std::to_string(crc);
+    return res;
+  }
+  std::string err;
+  bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
+  if (sync_now && !persist_from_device(id, rv->ext.ptr, n, meta->data(), S, &err)) {
+    release(rv->ext);
+    res.error = err;
+    return res;
+  }
+  insert_resident(id, rv->ext, n, crc, sync_now, meta);
+  res.ok = true;
+  return res;
+}
+
+void ChunkStore::recv_abandon(RecvVerify* rv) {
+  if (!rv->lane) return;
+  Lane* l = static_cast<Lane*>(rv->lane);
+  // kernels already queued on the lane only read the extent: they finish on their own
+  (void)hipSetDevice(cfg_.device);
+  (void)hipStreamSynchronize(l->stream);
+  release_lane(l);
+  rv->lane = nullptr;
 }
 
 void ChunkStore::spill_worker() {

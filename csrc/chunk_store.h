@@ -152,6 +152,22 @@ class ChunkStore {
   void release(const DevExtent& e);
   WriteResult commit_device(const std::string& id, const DevExtent& e, uint64_t n, uint32_t expected_crc,
                             hipStream_t s, bool persist_now = true);
+  // Pipelined receive (replication.cpp): while slices of a block land in a reserved extent,
+  // each landed byte range is checksummed on a store lane (K1 into the extent's .meta image)
+  // so verification overlaps the transfer; finish() folds the slice CRCs into the block CRC,
+  // compares, and commits (or releases the extent on mismatch).
+  struct RecvVerify {
+    DevExtent ext;
+    uint64_t n = 0;
+    void* lane = nullptr;
+    bool failed = false;
+    std::string error;
+  };
+  bool recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n);
+  bool recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi);  // lo, hi: byte range, lo % 512 == 0
+  WriteResult recv_finish(RecvVerify* rv, const std::string& id, uint32_t expected_crc, bool persist_now);
+  // Gives the lane back without touching the extent (a late DMA may still land in it).
+  void recv_abandon(RecvVerify* rv);
   // Pin a resident block (promoting it if needed) and return its device pointer.
   const uint8_t* pin_device(const std::string& id, uint64_t* size);
   void unpin(const std::string& id);
@@ -243,6 +259,7 @@ class ChunkStore {
   bool stop_ = false;
   StoreStats st_;
   std::atomic<uint64_t> launches_{0};
+  std::atomic<uint64_t> tmp_seq_{0};  // unique temporary file names for in-flight writes
   std::unique_ptr<GroupSync> gsync_;
   std::unique_ptr<DiskGate> gate_;
 };

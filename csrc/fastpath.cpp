@@ -18,6 +18,9 @@ namespace dfs {
 namespace {
 
 constexpr uint32_t kMaxBody = 1 << 16;
+// Largest single transfer the fast path accepts (the reference caps gRPC messages, and so
+// blocks, at 100 MiB: dfs/chunkserver/src/chunkserver.rs:15; large-object extents stay below).
+constexpr uint64_t kMaxTransfer = 1ull << 30;
 constexpr const char* kShmDir = "/dev/shm/";
 constexpr const char* kShmPrefix = "dfs_sc_";
 
@@ -116,6 +119,9 @@ std::vector<std::string> read_list(Reader& rd, bool optional) {
   return out;
 }
 
+// [off, off+len) inside an object of `size` bytes, without the wrap-around of off+len.
+bool range_ok(uint64_t off, uint64_t len, uint64_t size) { return off <= size && len <= size - off; }
+
 bool valid_shm_path(const std::string& path) {
   // only our client arenas: /dev/shm/dfs_sc_<...> with no path tricks
   if (path.rfind(kShmDir, 0) != 0) return false;
@@ -161,15 +167,9 @@ void FastPathServer::stop() {
   if (acceptor_.joinable()) acceptor_.join();
   if (lfd_ >= 0) ::close(lfd_);
   lfd_ = -1;
-  std::vector<std::thread> ws;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
-    ws.swap(workers_);
-  }
-  for (auto& t : ws)
-    if (t.joinable()) t.join();
-  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::mutex> g(mu_);
+  for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
+  workers_cv_.wait(g, [this] { return live_workers_ == 0; });
   for (auto& kv : maps_) ::munmap(kv.second.p, kv.second.size);
   maps_.clear();
   for (auto& m : retired_) ::munmap(m.p, m.size);
@@ -222,6 +222,17 @@ void FastPathServer::accept_loop() {
     if (r <= 0) continue;
     int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_CLOEXEC);
     if (fd < 0) continue;
+    // The abstract namespace has no file permissions: only processes of our own user
+    // (or root) may hand this server shared-memory offsets.
+    ucred cred{};
+    socklen_t cl = sizeof(cred);
+    if (::getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cred, &cl) != 0 ||
+        (cred.uid != ::geteuid() && cred.uid != 0)) {
+      ::close(fd);
+      std::lock_guard<std::mutex> g(mu_);
+      st_.rejected_peers++;
+      continue;
+    }
     std::lock_guard<std::mutex> g(mu_);
     if (stop_.load()) {
       ::close(fd);
@@ -229,19 +240,26 @@ void FastPathServer::accept_loop() {
     }
     conns_.push_back(fd);
     st_.connections++;
-    workers_.emplace_back([this, fd] { serve(fd); });
+    live_workers_++;
+    // detached: a finished connection frees its thread at once; stop() waits on the count
+    std::thread([this, fd] { serve(fd); }).detach();
   }
 }
 
-uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t need, std::string* err) {
+uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t off, uint64_t len, std::string* err) {
   if (!valid_shm_path(path)) {
     *err = "refusing shared-memory path " + path;
     return nullptr;
   }
+  if (len > kMaxTransfer || off > (1ull << 62)) {
+    *err = "transfer out of bounds";
+    return nullptr;
+  }
+  const uint64_t need = off + len;  // cannot wrap after the bounds above
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = maps_.find(path);
-    if (it != maps_.end() && it->second.size >= need) return it->second.p;
+    if (it != maps_.end() && range_ok(off, len, it->second.size)) return it->second.p;
     if (it != maps_.end()) {
       // the client recreated a bigger arena under the same name: map it again but keep
       // the old mapping alive (another connection may still be copying from it)
@@ -255,7 +273,7 @@ uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t need, std::st
     return nullptr;
   }
   struct stat sb {};
-  if (::fstat(fd, &sb) != 0 || static_cast<uint64_t>(sb.st_size) < need) {
+  if (::fstat(fd, &sb) != 0 || sb.st_size < 0 || !range_ok(off, len, static_cast<uint64_t>(sb.st_size))) {
     ::close(fd);
     *err = "shared-memory arena too small";
     return nullptr;
@@ -270,6 +288,10 @@ uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t need, std::st
   auto& m = maps_[path];
   if (m.p != nullptr) {  // raced with another connection of the same client
     ::munmap(p, static_cast<size_t>(sb.st_size));
+    if (!range_ok(off, len, m.size)) {
+      *err = "shared-memory arena too small";
+      return nullptr;
+    }
     return m.p;
   }
   m.p = static_cast<uint8_t*>(p);
@@ -277,7 +299,7 @@ uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t need, std::st
   return m.p;
 }
 
-void FastPathServer::set_rccl(RcclEngine* engine) { rccl_ = engine; }
+void FastPathServer::set_replication(ReplicationEngine* engine) { repl_ = engine; }
 
 void FastPathServer::set_peer(const std::string& addr, int rank, const std::string& fp_name) {
   std::lock_guard<std::mutex> g(peers_mu_);
@@ -354,20 +376,7 @@ FastPathServer::Peer* FastPathServer::local_peer(const std::string& addr) {
   return p.get();
 }
 
-bool FastPathServer::forward(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
-                             const ShmSrc& src, int* replicas, std::string* err) {
-  *replicas = 0;
-  Peer* p = next.empty() ? nullptr : local_peer(next[0]);
-  if (p == nullptr) {
-    *err = "no native route to " + (next.empty() ? std::string("?") : next[0]);
-    return false;
-  }
-  bool use_rccl = rccl_ != nullptr && p->rank >= 0 && rccl_->pair_ok(rccl_->rank(), p->rank);
-  bool use_shm = !use_rccl && !src.path.empty();
-  if (!use_rccl && !use_shm) {
-    *err = "no RCCL pair and no shared-memory source for " + next[0];
-    return false;
-  }
+bool FastPathServer::exchange_with(Peer* p, const std::vector<uint8_t>& req, std::vector<uint8_t>* resp) {
   int fd = -1;
   {
     std::lock_guard<std::mutex> g(p->mu);
@@ -376,79 +385,121 @@ bool FastPathServer::forward(const std::string& id, uint32_t crc, uint64_t term,
       p->idle.pop_back();
     }
   }
-  if (fd < 0 && (fd = connect_abstract(p->name)) < 0) {
-    *err = "cannot reach fast path of " + next[0];
+  if (fd < 0 && (fd = connect_abstract(p->name)) < 0) return false;
+  if (!exchange(fd, req, resp)) {
+    ::close(fd);
     return false;
   }
-  auto put_next = [&](std::vector<uint8_t>& req) {
-    put<uint16_t>(req, static_cast<uint16_t>(next.size() - 1));
-    for (size_t i = 1; i < next.size(); ++i) put_str(req, next[i]);
-  };
-  std::vector<uint8_t> req(4, 0), resp;
-  bool io_ok;
-  if (use_rccl) {
-    // payload GPU->GPU over xGMI (ncclSend from HBM), descriptor over the socket
-    uint64_t size = 0;
-    int64_t seq = rccl_->send(p->rank, id, &size, err);
-    if (seq < 0) {
-      std::lock_guard<std::mutex> g(p->mu);
-      p->idle.push_back(fd);
-      return false;
-    }
-    req.push_back(3);
-    put<uint64_t>(req, term);
-    put<uint32_t>(req, crc);
-    put<int32_t>(req, rccl_->rank());
-    put<int64_t>(req, seq);
-    put<uint64_t>(req, size);
-    put_str(req, id);
-    put_next(req);
-    finish_frame(req);
-    io_ok = exchange(fd, req, &resp);
-    std::string werr;
-    bool sent = rccl_->wait_send(p->rank, seq, &werr);
-    if (!io_ok || !sent) {
-      ::close(fd);
-      // an unmatched send would wedge this pair's stream: retire it; the next block on
-      // this hop uses the shared-memory route (or the client's gRPC fallback)
-      rccl_->abort_pair(rccl_->rank(), p->rank);
-      *err = !io_ok ? "descriptor to " + next[0] + " failed" : "RCCL send failed: " + werr;
-      return false;
-    }
-  } else {
-    // same-host hop without RCCL: the next server stages straight from the client's
-    // shared-memory slot (H2D on its own GPU) — no payload on any socket
-    req.push_back(4);
-    put<uint64_t>(req, term);
-    put<uint32_t>(req, crc);
-    put<uint64_t>(req, src.off);
-    put<uint64_t>(req, src.len);
-    put_str(req, id);
-    put_str(req, src.path);
-    put_next(req);
-    finish_frame(req);
-    io_ok = exchange(fd, req, &resp);
-    if (!io_ok) {
-      ::close(fd);
-      *err = "forward to " + next[0] + " failed";
-      return false;
-    }
-  }
-  {
-    std::lock_guard<std::mutex> g(p->mu);
-    p->idle.push_back(fd);
-  }
-  if (static_cast<FpStatus>(resp[0]) != FpStatus::Ok) {
-    *err = "downstream " + next[0] + ": " + resp_msg(resp);
-    return false;
-  }
-  uint64_t downstream = 0;
-  std::memcpy(&downstream, resp.data() + 9, 8);
-  *replicas = static_cast<int>(downstream);
-  std::lock_guard<std::mutex> g(mu_);
-  if (use_rccl) st_.rccl_forwards++;
-  else st_.shm_forwards++;
+  std::lock_guard<std::mutex> g(p->mu);
+  p->idle.push_back(fd);
   return true;
+}
+
+bool FastPathServer::control(int rank, const std::string& blob, std::string* reply) {
+  Peer* p = nullptr;
+  {
+    std::lock_guard<std::mutex> g(peers_mu_);
+    for (auto& kv : peers_)
+      if (kv.second->rank == rank && !kv.second->name.empty()) p = kv.second.get();
+  }
+  if (!p) return false;
+  std::vector<uint8_t> req(4, 0), resp;
+  req.push_back(5);
+  put_str(req, blob);
+  finish_frame(req);
+  if (!exchange_with(p, req, &resp) || static_cast<FpStatus>(resp[0]) != FpStatus::Ok) return false;
+  *reply = resp_msg(resp);
+  return true;
+}
+
+int FastPathServer::replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term,
+                                  const ShmSrc& src, const uint8_t* host, uint64_t n) {
+  Peer* p = local_peer(addr);
+  if (p == nullptr) return 0;
+  std::vector<uint8_t> resp;
+  auto count_ok = [&](uint64_t FpStats::*field) {
+    uint64_t down = 0;
+    std::memcpy(&down, resp.data() + 9, 8);
+    std::lock_guard<std::mutex> g(mu_);
+    (st_.*field)++;
+    return static_cast<int>(down);
+  };
+  bool tried_p2p = false;
+  if (repl_ != nullptr && p->rank >= 0 && repl_->pair_ok(p->rank)) {
+    // payload over the P2P transport (RCCL: HBM -> HBM over xGMI), descriptor on the socket
+    ReplTicket t;
+    std::string err;
+    if (repl_->send(p->rank, id, host, n, &t, &err)) {
+      tried_p2p = true;
+      std::vector<uint8_t> req(4, 0);
+      req.push_back(3);
+      put<uint64_t>(req, term);
+      put<uint32_t>(req, crc);
+      put<int32_t>(req, repl_->rank());
+      put<uint64_t>(req, t.gen);
+      put<int64_t>(req, t.seq);
+      put<uint64_t>(req, t.size);
+      put<uint64_t>(req, t.slice);
+      put_str(req, id);
+      put<uint16_t>(req, 0);  // fan-out: the replica forwards nowhere
+      finish_frame(req);
+      bool io_ok;
+      int drop = drop_descriptors_.load();
+      if (drop > 0 && drop_descriptors_.compare_exchange_strong(drop, drop - 1)) io_ok = false;  // test hook
+      else io_ok = exchange_with(p, req, &resp);
+      if (!io_ok) {
+        // the posted sends can never be matched now: abort the pair (it is rebuilt under a
+        // new generation) and move this replica to shared memory below
+        repl_->cancel_send(&t, "descriptor to " + addr + " failed");
+      } else {
+        std::string werr;
+        bool sent = repl_->wait_send(&t, &werr);
+        FpStatus st = static_cast<FpStatus>(resp[0]);
+        if (st == FpStatus::Ok) return count_ok(&FpStats::rccl_forwards);
+        if (st == FpStatus::Fenced) return 0;
+        (void)sent;  // a failed transfer already failed the pair inside the engine
+      }
+    }
+  }
+  if (src.path.empty()) {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.replica_failures++;
+    return 0;
+  }
+  // same-host hop without a P2P pair: the replica stages straight from the client's slot
+  std::vector<uint8_t> req(4, 0);
+  req.push_back(4);
+  put<uint64_t>(req, term);
+  put<uint32_t>(req, crc);
+  put<uint64_t>(req, src.off);
+  put<uint64_t>(req, src.len);
+  put_str(req, id);
+  put_str(req, src.path);
+  put<uint16_t>(req, 0);
+  finish_frame(req);
+  if (exchange_with(p, req, &resp) && static_cast<FpStatus>(resp[0]) == FpStatus::Ok) {
+    if (tried_p2p) {
+      std::lock_guard<std::mutex> g(mu_);
+      st_.p2p_fallbacks++;
+    }
+    return count_ok(&FpStats::shm_forwards);
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  st_.replica_failures++;
+  return 0;
+}
+
+void FastPathServer::replicate(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
+                               const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas) {
+  *replicas = 0;
+  if (next.empty()) return;
+  // every replica at once: each has its own xGMI link from this GPU
+  std::vector<std::future<int>> futs;
+  for (size_t i = 1; i < next.size(); ++i)
+    futs.push_back(std::async(std::launch::async, [&, i] { return replicate_one(next[i], id, crc, term, src, host, n); }));
+  int total = replicate_one(next[0], id, crc, term, src, host, n);
+  for (auto& f : futs) total += f.get();
+  *replicas = total;
 }
 
 void FastPathServer::serve(int fd) {
@@ -464,20 +515,21 @@ void FastPathServer::serve(int fd) {
     *msg = "Stale master term: request has " + std::to_string(term) + " but known term is " + std::to_string(known);
     return true;
   };
-  // Local persist and downstream forward run concurrently; the ack waits for both.
+  // Local persist and the downstream fan-out run concurrently; the ack waits for both.
   auto persist_and_forward = [&](const std::string& id, const uint8_t* host, uint64_t len, uint32_t crc,
                                  uint64_t term, const std::vector<std::string>& next, const ShmSrc& src) -> bool {
     int down = 0;
-    std::string ferr, perr;
-    auto fut = std::async(std::launch::async, [&] { return forward(id, crc, term, next, src, &down, &ferr); });
+    std::string perr;
+    auto fut = std::async(std::launch::async, [&] { replicate(id, crc, term, next, src, host, len, &down); });
     bool pok = store_->persist(id, host, host ? len : 0, &perr);
-    bool fok = fut.get();
+    fut.get();
     if (!pok) return send_response(fd, FpStatus::IoError, 0, 0, perr);
-    if (!fok) {
-      bump(&FpStats::forward_failures);
-      return send_response(fd, FpStatus::Unsupported, 0, 0, "native forward failed: " + ferr);
-    }
     return send_response(fd, FpStatus::Ok, len, 1 + static_cast<uint64_t>(down), "");
+  };
+  auto all_local = [&](const std::vector<std::string>& next) {
+    for (auto& a : next)
+      if (local_peer(a) == nullptr) return false;
+    return true;
   };
   while (!stop_.load()) {
     uint32_t n = 0;
@@ -500,9 +552,9 @@ void FastPathServer::serve(int fd) {
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed write request");
       } else if (fenced(term, &msg)) {
         sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
-      } else if (!next.empty() && local_peer(next[0]) == nullptr) {
-        sent = send_response(fd, FpStatus::Unsupported, 0, 0, "no native route for the chain");
-      } else if ((base = map_shm(path, off + len, &err)) == nullptr) {
+      } else if (!all_local(next)) {
+        sent = send_response(fd, FpStatus::Unsupported, 0, 0, "no native route for a replica");
+      } else if ((base = map_shm(path, off, len, &err)) == nullptr) {
         sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
       } else if (next.empty()) {
         WriteResult wr = store_->write(id, base + off, len, crc);
@@ -517,23 +569,27 @@ void FastPathServer::serve(int fd) {
           sent = persist_and_forward(id, base + off, len, crc, term, next, ShmSrc{path, off, len});
         }
       }
-    } else if (op == 3) {  // REPL: block arrives over RCCL from the previous hop
+    } else if (op == 3) {  // REPL: block arrives over the P2P transport from the head
       uint64_t term = rd.get<uint64_t>();
       uint32_t crc = rd.get<uint32_t>();
       int32_t src = rd.get<int32_t>();
+      uint64_t gen = rd.get<uint64_t>();
       int64_t seq = rd.get<int64_t>();
       uint64_t size = rd.get<uint64_t>();
+      uint64_t slice = rd.get<uint64_t>();
       std::string id = rd.str();
       std::vector<std::string> next = read_list(rd, false);
-      if (!rd.ok || id.empty() || rccl_ == nullptr) {
-        sent = send_response(fd, FpStatus::BadRequest, 0, 0, rccl_ ? "malformed replicate request" : "RCCL disabled");
+      if (!rd.ok || id.empty() || repl_ == nullptr || size > kMaxTransfer) {
+        if (repl_ && rd.ok && src >= 0) repl_->fail_pair(src, "malformed descriptor");
+        sent = send_response(fd, FpStatus::BadRequest, 0, 0, repl_ ? "malformed replicate request" : "replication disabled");
       } else {
-        // The recv must be posted even when the request is refused, or the sender's
-        // ncclSend never completes; recv first, then judge the request.
+        // The receive is posted even for a fenced request — refusing it would leave the
+        // sender's transfer unmatched and cost the pair a rebuild; the block is dropped after.
         bool last = next.empty();
         bool stale = fenced(term, &msg);
-        WriteResult wr = rccl_->recv(src, seq, id, size, crc, last && !stale);
+        WriteResult wr = repl_->recv(src, gen, seq, id, size, slice, crc, last && !stale);
         if (stale) {
+          if (wr.ok) store_->remove(id);
           sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
         } else if (!wr.ok) {
           sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
@@ -555,7 +611,7 @@ void FastPathServer::serve(int fd) {
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed replicate request");
       } else if (fenced(term, &msg)) {
         sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
-      } else if ((base = map_shm(path, off + len, &err)) == nullptr) {
+      } else if ((base = map_shm(path, off, len, &err)) == nullptr) {
         sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
       } else if (next.empty()) {
         WriteResult wr = store_->write(id, base + off, len, crc);
@@ -570,6 +626,10 @@ void FastPathServer::serve(int fd) {
           sent = persist_and_forward(id, base + off, len, crc, term, next, ShmSrc{path, off, len});
         }
       }
+    } else if (op == 5) {  // CTRL: replication pair bring-up / rebuild
+      std::string blob = rd.str();
+      if (!rd.ok || repl_ == nullptr) sent = send_response(fd, FpStatus::Unsupported, 0, 0, "replication disabled");
+      else sent = send_response(fd, FpStatus::Ok, 0, 0, repl_->handle_control(blob));
     } else if (op == 2) {  // READ into the client's slot
       uint64_t offset = rd.get<uint64_t>(), length = rd.get<uint64_t>();
       uint64_t shm_off = rd.get<uint64_t>(), cap = rd.get<uint64_t>();
@@ -584,7 +644,7 @@ void FastPathServer::serve(int fd) {
           sent = send_response(fd, static_cast<FpStatus>(st.status), st.total_size, 0, st.error);
         } else if (st.bytes > cap) {
           sent = send_response(fd, FpStatus::Unsupported, st.total_size, 0, "slot too small");
-        } else if ((base = map_shm(path, shm_off + cap, &err)) == nullptr) {
+        } else if ((base = map_shm(path, shm_off, cap, &err)) == nullptr) {
           sent = send_response(fd, FpStatus::Unsupported, st.total_size, 0, "short-circuit unavailable: " + err);
         } else {
           ReadResult rr = store_->read_into(id, offset, st.bytes, base + shm_off);
@@ -617,6 +677,7 @@ void FastPathServer::serve(int fd) {
     }
   }
   ::close(fd);
+  if (--live_workers_ == 0) workers_cv_.notify_all();
 }
 
 }  // namespace dfs

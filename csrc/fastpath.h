@@ -16,23 +16,26 @@
 // Wire format (little endian), one request/response pair at a time per connection:
 //   request  = u32 body_len | u8 op | body
 //     op 1 WRITE: u64 term | u32 crc | u64 shm_off | u64 len | u16 id_len id | u16 path_len path
-//               [| u16 n_next | (u16 len addr)*]      -- chain: forwarded natively over RCCL
+//               [| u16 n_next | (u16 len addr)*]      -- replicas, fanned out natively
 //     op 2 READ : u64 offset | u64 length | u64 shm_off | u64 shm_cap | u16 id_len id | u16 path_len path
-//     op 3 REPL : u64 term | u32 crc | i32 src_rank | i64 seq | u64 size | u16 id_len id
-//               | u16 n_next | (u16 len addr)*      -- server-to-server: block arrives over RCCL
+//     op 3 REPL : u64 term | u32 crc | i32 src_rank | u64 gen | i64 seq | u64 size | u64 slice
+//               | u16 id_len id | u16 n_next | (u16 len addr)*   -- payload over the P2P transport
 //     op 4 REPL_SHM: u64 term | u32 crc | u64 shm_off | u64 len | u16 id_len id | u16 path_len path
-//               | u16 n_next | (u16 len addr)*      -- same-host hop without RCCL: read the client slot
+//               | u16 n_next | (u16 len addr)*      -- same-host hop without a P2P pair: read the client slot
+//     op 5 CTRL : u16 len blob                       -- replication control (pair bring-up / rebuild)
 //   response = u32 body_len | u8 status | u64 total | u64 bytes | u16 msg_len msg
-//   (for WRITE/REPL ``bytes`` carries replicas_written)
+//   (for WRITE/REPL ``bytes`` carries replicas_written; for CTRL ``msg`` is the engine reply)
 //
-// Chain replication stays native when every hop is a ChunkServer of this host: with an
-// RCCL pair the block is staged in HBM and sent GPU->GPU over xGMI with ncclSend while a
-// ~100-byte descriptor goes to the next server's fast-path socket (named dfs_fp_<port>);
-// without one (pair broken, GPUs shared, CPU store) the next server stages straight from
-// the client's shared-memory slot. Either way the hop overlaps the local fdatasync. A hop
-// off this host answers Unsupported and the client redoes the write on the gRPC path.
+// Replication stays native when every replica is a ChunkServer of this host. The head
+// stages the block in HBM (H2D + CRC kernel) and FANS OUT to all replicas at once: over the
+// P2P transport (RCCL/xGMI, slices pipelined with the receiver's checksum kernel) where the
+// pair is up, else the replica stages straight from the client's shared-memory slot. Each
+// path overlaps the local fdatasync. A replica that fails is not counted (replicas_written
+// shrinks, like the reference's chain); a replica off this host makes the head answer
+// Unsupported and the client redoes the write on the gRPC path.
 #pragma once
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -42,7 +45,7 @@
 #include <vector>
 
 #include "chunk_store.h"
-#include "rccl_engine.h"
+#include "replication.h"
 
 namespace dfs {
 
@@ -61,6 +64,9 @@ enum class FpStatus : uint8_t {
 struct FpStats {
   uint64_t writes = 0, reads = 0, fenced = 0, punts = 0, connections = 0;
   uint64_t replicas_in = 0, rccl_forwards = 0, shm_forwards = 0, forward_failures = 0;
+  uint64_t rejected_peers = 0;  // connections from another uid (SO_PEERCRED)
+  uint64_t replica_failures = 0;  // replicas that could not be written (not counted)
+  uint64_t p2p_fallbacks = 0;     // replicas moved to shared memory after a P2P failure
 };
 
 class FastPathServer {
@@ -83,10 +89,14 @@ class FastPathServer {
   std::vector<std::string> drain_suspects();  // blocks needing background recovery
   FpStats stats();
 
-  // Native chain replication: this server's RCCL engine and the fast-path socket of every
-  // same-node peer (advertised address -> rank, socket name).
-  void set_rccl(RcclEngine* engine);
+  // Native replication: this server's engine (RCCL or socket transport) and the fast-path
+  // socket of every same-node peer (advertised address -> rank, socket name).
+  void set_replication(ReplicationEngine* engine);
   void set_peer(const std::string& addr, int rank, const std::string& fp_name);
+  // Control exchange with the fast path of the peer of `rank` (the engine's ControlFn).
+  bool control(int rank, const std::string& req, std::string* reply);
+  // Test hook: the next `n` REPL descriptors are dropped on the way out.
+  void debug_drop_descriptors(int n) { drop_descriptors_ += n; }
   void set_self_host(const std::string& host);  // our advertised host: same-host peer detection
 
  private:
@@ -98,15 +108,19 @@ class FastPathServer {
   };
   void accept_loop();
   void serve(int fd);
-  uint8_t* map_shm(const std::string& path, uint64_t need, std::string* err);
-  // Send block `id` (resident in HBM) to next[0] over RCCL + descriptor; *replicas gets
-  // the downstream count. False (with *err) when there is no native route or it failed.
+  // Maps the client arena and checks [off, off+len) lies inside it (overflow-safe).
+  uint8_t* map_shm(const std::string& path, uint64_t off, uint64_t len, std::string* err);
   struct ShmSrc {
-    std::string path;  // client arena the block came from (empty: HBM-only, e.g. RCCL-received)
+    std::string path;  // client arena the block came from (empty: HBM-only, e.g. P2P-received)
     uint64_t off = 0, len = 0;
   };
-  bool forward(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
-               const ShmSrc& src, int* replicas, std::string* err);
+  // Fan block `id` out to every address in `next` (all same-host); *replicas = replicas
+  // written downstream. `host` is the block in host memory when there is one (shm slot).
+  void replicate(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
+                 const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas);
+  int replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term, const ShmSrc& src,
+                    const uint8_t* host, uint64_t n);
+  bool exchange_with(struct Peer* p, const std::vector<uint8_t>& req, std::vector<uint8_t>* resp);
   Peer* local_peer(const std::string& addr);
 
   ChunkStore* store_;
@@ -116,7 +130,8 @@ class FastPathServer {
   std::atomic<uint64_t> term_{0};
   std::thread acceptor_;
   std::mutex mu_;
-  std::vector<std::thread> workers_;
+  int live_workers_ = 0;  // detached per-connection threads still running (guarded by mu_)
+  std::condition_variable workers_cv_;
   std::vector<int> conns_;
   struct Mapping {
     uint8_t* p = nullptr;
@@ -126,7 +141,8 @@ class FastPathServer {
   std::vector<Mapping> retired_;
   std::vector<std::string> suspects_;
   FpStats st_;
-  RcclEngine* rccl_ = nullptr;
+  ReplicationEngine* repl_ = nullptr;
+  std::atomic<int> drop_descriptors_{0};
   std::mutex peers_mu_;
   std::unordered_map<std::string, std::unique_ptr<Peer>> peers_;
   std::string self_host_;

@@ -218,6 +218,7 @@ void MasterCore::put(const std::string& path, pb::FileMetadata m) {
 
 bool MasterCore::del(const std::string& path, pb::FileMetadata* out) {
   under_construction_.erase(path);
+  uc_progress_.erase(path);
   auto it = files_.find(path);
   if (it == files_.end()) return false;
   for (auto& b : it->second.blocks) {
@@ -290,8 +291,13 @@ Json MasterCore::apply_one(const std::string& name, const Json& a) {
     auto it = files_.find(path);
     if (it != files_.end()) {
       auto uc = under_construction_.find(path);
-      if (uc == under_construction_.end() || ts - uc->second < create_lease_ms()) return obj({{"exists", true}});
-      old = it->second;  // a writer that died mid-create: its lease expired, take the path over
+      if (uc == under_construction_.end()) return obj({{"exists", true}});
+      auto pr = uc_progress_.find(path);
+      int64_t last = pr == uc_progress_.end() ? uc->second : std::max(uc->second, pr->second);
+      if (ts - last < create_lease_ms()) return obj({{"exists", true}});
+      // a writer that made no progress (create / AllocateBlock) for a whole lease: take the
+      // path over; its later AllocateBlock / CompleteFile carry the old generation and fail
+      old = it->second;
       had_old = true;
     }
     pb::FileMetadata m;
@@ -309,19 +315,32 @@ Json MasterCore::apply_one(const std::string& name, const Json& a) {
       }
       put(path, std::move(m));
       under_construction_[path] = ts;
+      uc_progress_[path] = ts;
     } else {
       for (auto& bd : a["blocks"].items()) m.blocks.push_back(block_from(bd));
       put(path, std::move(m));
       under_construction_.erase(path);
+      uc_progress_.erase(path);
       apply_one("CompleteFile", a);
     }
-    return obj({{"exists", false}, {"orphans", had_old ? block_list(old) : Json::array()}});
+    return obj({{"exists", false}, {"gen", ts}, {"orphans", had_old ? block_list(old) : Json::array()}});
   }
   if (name == "CompleteFile") {
     auto it = files_.find(path);
     if (it == files_.end()) return obj({{"found", false}});
     pb::FileMetadata& m = it->second;
+    if (int64_t gen = a["gen"].as_int()) {
+      auto uc = under_construction_.find(path);
+      if (uc == under_construction_.end()) {
+        // already complete: only an identical retry of the completion is accepted
+        bool same = m.size == a["size"].as_u64() && (a["etag_md5"].str().empty() || m.etag_md5 == a["etag_md5"].str());
+        if (!same) return obj({{"found", true}, {"stale", true}});
+        return obj({{"found", true}});
+      }
+      if (uc->second != gen) return obj({{"found", true}, {"stale", true}});
+    }
     under_construction_.erase(path);
+    uc_progress_.erase(path);
     m.size = a["size"].as_u64();
     if (!a["etag_md5"].str().empty()) m.etag_md5 = a["etag_md5"].str();
     if (a["created_at_ms"].as_u64()) m.created_at_ms = a["created_at_ms"].as_u64();
@@ -351,6 +370,13 @@ Json MasterCore::apply_one(const std::string& name, const Json& a) {
   if (name == "AllocateBlock") {
     auto it = files_.find(path);
     if (it == files_.end()) return Json();
+    auto uc = under_construction_.find(path);
+    if (int64_t gen = a["gen"].as_int())
+      if (uc == under_construction_.end() || uc->second != gen) return obj({{"stale", true}});
+    if (uc != under_construction_.end()) {  // progress renews the writer's lease
+      int64_t& last = uc_progress_[path];
+      last = std::max(last, a["ts"].as_int());
+    }
     pb::BlockInfo b;
     b.block_id = a["block_id"].str();
     b.ec_data_shards = it->second.ec_data_shards;
@@ -551,6 +577,10 @@ std::string MasterCore::snapshot() {
   Json uc = Json::object();
   for (auto& kv : under_construction_) uc.set(kv.first, kv.second);
   uc.dump_to(out);
+  out += ",\"uc_progress\":";
+  Json up = Json::object();
+  for (auto& kv : uc_progress_) up.set(kv.first, kv.second);
+  up.dump_to(out);
   out += "}}";
   return out;
 }
@@ -572,8 +602,11 @@ void MasterCore::restore(const std::string& text) {
   shuffling_prefixes_.clear();
   for (auto& p : s["shuffling_prefixes"].items()) shuffling_prefixes_.insert(p.str());
   under_construction_.clear();
+  uc_progress_.clear();
   for (auto& kv : s["under_construction"].fields())
-    if (files_.count(kv.first)) under_construction_[kv.first] = kv.second.as_int();
+    if (files_.count(kv.first)) under_construction_[kv.first] = uc_progress_[kv.first] = kv.second.as_int();
+  for (auto& kv : s["uc_progress"].fields())
+    if (under_construction_.count(kv.first)) uc_progress_[kv.first] = kv.second.as_int();
 }
 
 // ---------------------------------------------------------------- chunkservers / safe mode
@@ -1043,6 +1076,7 @@ int MasterCore::create_file(const std::string& raw, std::string* out) {
   }
   if (j["orphans"].size()) queue_gc(j["orphans"]);
   resp.success = true;
+  resp.writer_generation = static_cast<uint64_t>(j["gen"].as_int());
   if (r.allocate_block) {
     int ec_d = 0, ec_p = 0;
     {
@@ -1080,13 +1114,16 @@ int MasterCore::allocate_block(const std::string& raw, std::string* out) {
   std::string block_id = new_uuid();
   Json locs = Json::array();
   for (auto& s : sel) locs.push_back(s);
-  Json master = obj({{"AllocateBlock", obj({{"path", r.path}, {"block_id", block_id}, {"locations", locs}})}});
-  Result res = propose(obj({{"Master", master}}));
+  Json args = obj({{"path", r.path}, {"block_id", block_id}, {"locations", locs}, {"ts", now_ms()}});
+  if (r.writer_generation) args.set("gen", static_cast<int64_t>(r.writer_generation));
+  Result res = propose(obj({{"Master", obj({{"AllocateBlock", args}})}}));
   pb::AllocateBlockResponse resp;
   if (res.code == 1) {
     resp.leader_hint = res.payload;
   } else if (res.code != 0) {
     return (*out = res.payload, INTERNAL);
+  } else if (!res.payload.empty() && Json::parse(res.payload)["stale"].as_bool()) {
+    return (*out = "Write lease lost: " + r.path + " was taken over by another writer", FAILED_PRECONDITION);
   } else {
     allocation(block_id, sel, ec_d, ec_p, &resp);
   }
@@ -1140,10 +1177,13 @@ int MasterCore::complete_file(const std::string& raw, std::string* out) {
       resp.success = true;
     }
   } else {
+    if (r.writer_generation) args.set("gen", static_cast<int64_t>(r.writer_generation));
     Result res = propose(obj({{"Master", obj({{"CompleteFile", args}})}}));
     if (res.code == 1) return not_leader(res.payload);
     if (res.code != 0) return (*out = res.payload, INTERNAL);
-    resp.success = Json::parse(res.payload)["found"].as_bool(true);
+    Json j = Json::parse(res.payload);
+    if (j["stale"].as_bool()) return (*out = "Write lease lost: " + r.path + " was taken over by another writer", FAILED_PRECONDITION);
+    resp.success = j["found"].as_bool(true);
   }
   out->clear();
   resp.encode(*out);

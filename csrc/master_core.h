@@ -153,7 +153,10 @@ class MasterCore : public raft::StateMachine {
   // replicated
   std::unordered_map<std::string, pb::FileMetadata> files_;
   std::unordered_map<std::string, std::string> block_index_;
+  // path -> writer generation (the create entry's ts) while a classic create is open, and the
+  // last progress (create / AllocateBlock) of that writer: the lease runs from the latter.
   std::unordered_map<std::string, int64_t> under_construction_;
+  std::unordered_map<std::string, int64_t> uc_progress_;
   std::map<std::string, Json> tx_records_;
   std::unordered_map<std::string, std::string> tx_locks_;
   std::set<std::string> shuffling_prefixes_;

@@ -1,0 +1,67 @@
+// Point-to-point byte channels between the ChunkServer ranks of one node — the transport
+// under chain/fan-out replication (replication.h).
+//
+// Contract (what RCCL p2p gives us, and what the CPU test transport reproduces):
+//  * between two ranks there are two independent directed channels (a->b, b->a);
+//  * transfers on one channel are matched strictly in post order: the k-th post_send on
+//    a->b lands in the buffer of b's k-th post_recv from a, and sizes must agree;
+//  * posts never block; completion is observed with test(); an op whose peer never posts
+//    the matching op never completes — only close() (ncclCommAbort) ends it;
+//  * a channel pair is brought up for a generation by open() on BOTH ranks with the
+//    same tokens: the sender of each channel creates its token (make_token) and ships it
+//    to the peer over the control plane (the fast-path socket).
+//
+// Implementations:
+//  * RcclTransport  (p2p_rccl.cpp): one 2-rank nonblocking communicator + HIP stream per
+//    direction; buffers are HBM pointers of our GPU, each op records a hipEvent.
+//  * SocketTransport (p2p_socket.cpp): a UNIX stream socket per direction and a worker
+//    thread per direction draining the FIFO of posted ops; buffers are host memory. It is
+//    what the multi-process CPU tests run (tests/test_replication.py), so every rule of the
+//    replication protocol (sequencing, bounded waits, generations, rebuild) is exercised
+//    without GPUs; it also carries fault hooks (drop / stall a channel).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <string>
+
+namespace dfs {
+
+struct P2POp {
+  void* event = nullptr;                        // RCCL: hipEvent_t recorded after the op
+  std::shared_ptr<std::atomic<int>> state;      // socket: 0 pending, 1 done, -1 failed
+};
+
+class P2PTransport {
+ public:
+  virtual ~P2PTransport() = default;
+  virtual const char* name() const = 0;
+  virtual bool device_buffers() const = 0;  // true: buffers are device (HBM) pointers
+
+  // Token for the channel rank->peer of generation `gen` (we are its sender). Opaque bytes.
+  virtual std::string make_token(int peer, uint64_t gen, std::string* err) = 0;
+  // Bring up both channels with `peer`: `tok_out` (ours, rank->peer), `tok_in` (the peer's,
+  // peer->rank). Both ranks call it concurrently; returns once both channels passed a
+  // warm-up transfer, or false at the deadline.
+  virtual bool open(int peer, uint64_t gen, const std::string& tok_out, const std::string& tok_in, int timeout_ms,
+                    std::string* err) = 0;
+  // Abort both channels with `peer`: pending ops fail or never complete; no waiting.
+  virtual void close(int peer) = 0;
+
+  virtual bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
+  virtual bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
+  virtual int test(P2POp* op) = 0;  // 1 done, 0 pending, -1 failed
+  virtual void release(P2POp* op) = 0;
+
+  // Test hooks (socket transport only; no-ops elsewhere): the next `n` sends to `peer`
+  // vanish (never delivered), or the channel to `peer` stalls for `ms`.
+  virtual void debug_drop_sends(int /*peer*/, int /*n*/) {}
+  virtual void debug_stall(int /*peer*/, int /*ms*/) {}
+};
+
+// device >= 0: RCCL over xGMI on that GPU. Returns nullptr (with *err) if unavailable.
+std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, std::string* err);
+// Host-memory transport over abstract UNIX sockets; `ns` keeps test clusters apart.
+std::unique_ptr<P2PTransport> make_socket_transport(int rank, const std::string& ns);
+
+}  // namespace dfs

@@ -1,0 +1,149 @@
+// Replication engine: moves block payloads between the ChunkServers (GPU ranks) of one node
+// over a P2PTransport (RCCL over xGMI in production, sockets in the CPU tests), with the
+// control messages (descriptors, pair bring-up) on the fast-path sockets.
+//
+// Reference behaviour it replaces: the synchronous store-and-forward gRPC chain
+// (dfs/chunkserver/src/chunkserver.rs:777-829,1039-1077): each hop fsyncs, then forwards
+// the whole block to next_servers[0]; a downstream failure still returns success with a
+// smaller replicas_written.
+//
+// MI355X design:
+//  * Fan-out, not a device-side chain. The 8 GPUs of a node form a full xGMI mesh: the
+//    head has a dedicated link to every replica, so sending to all replicas at once costs
+//    no extra link bandwidth and replaces the chain's per-hop latency with a single hop.
+//    Device-side cut-through forwarding (recv slice s on a->b, then send it on b->c) would
+//    make b->c's FIFO wait on a->b's; with chains in both directions around the node
+//    (A->B->C next to C->A->B) those FIFO couplings close a cycle and deadlock. Fan-out
+//    sends depend only on data already resident in HBM, so no cycle can form.
+//  * Slice pipelining. A block travels as slices (256 KiB..4 MiB, multiples of the 512 B
+//    checksum slice); the receiver launches the K1 checksum of slice s as soon as it lands,
+//    while slice s+1 is still on the link, then folds the slice CRCs into the block CRC.
+//  * Sequencing. Each direction of each pair is a FIFO channel: the sender stamps a block
+//    with a per-pair sequence number and the generation of the pair; the receiver posts
+//    its receives in sequence order (a late descriptor waits its turn, boundedly).
+//  * Bounded failure handling. Any anomaly (descriptor lost, turn timeout, transfer
+//    timeout, peer gone) marks the pair broken and aborts its channels at once — waiting
+//    receivers wake up and fail fast; the caller falls back (shared-memory staging or the
+//    gRPC path). The pair is then REBUILT under a new generation: the lower rank of a pair
+//    is its only initiator (no open races), retrying with backoff until the peer answers;
+//    the higher rank asks it to when it detects the failure. Blocks in flight under an old
+//    generation are refused by generation check instead of being mismatched.
+#pragma once
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "chunk_store.h"
+#include "p2p_transport.h"
+
+namespace dfs {
+
+struct ReplOptions {
+  int open_timeout_ms = 20000;   // one bring-up attempt of a pair
+  int turn_timeout_ms = 3000;    // receiver waiting for its sequence turn
+  int xfer_timeout_ms = 20000;   // one block transfer once posted
+  uint64_t min_slice = 256 << 10;
+  uint64_t max_slice = 4 << 20;
+};
+
+struct ReplTicket {
+  int peer = -1;
+  uint64_t gen = 0;
+  int64_t seq = -1;
+  uint64_t size = 0;
+  uint64_t slice = 0;
+  std::string id;
+  bool pinned = false;
+  std::vector<P2POp> ops;
+};
+
+struct ReplStats {
+  uint64_t bytes_sent = 0, bytes_recv = 0, blocks_sent = 0, blocks_recv = 0;
+  uint64_t pair_failures = 0, pair_opens = 0, open_attempts = 0, turn_timeouts = 0, stale_generation = 0;
+};
+
+class ReplicationEngine {
+ public:
+  // Sends a control message to `peer`'s fast path and returns its reply (false: unreachable).
+  using ControlFn = std::function<bool(int peer, const std::string& req, std::string* reply)>;
+
+  ReplicationEngine(ChunkStore* store, std::unique_ptr<P2PTransport> transport, int rank, int world,
+                    ReplOptions opt = {});
+  ~ReplicationEngine();
+  ReplicationEngine(const ReplicationEngine&) = delete;
+
+  void set_control(ControlFn fn);
+  // Starts bringing up every pair this rank initiates (peers with a higher rank).
+  void start();
+  void stop();
+  // Waits until every pair is up (or the deadline); returns the number of pairs up.
+  int wait_ready(int timeout_ms);
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  const char* transport_name() const { return t_->name(); }
+  bool pair_ok(int peer);
+  uint64_t generation(int peer);
+
+  // Sender: post `id` (resident in HBM for a device transport; `host_src` otherwise) to
+  // `peer` as slices. The ticket carries what the peer's descriptor needs.
+  bool send(int peer, const std::string& id, const uint8_t* host_src, uint64_t n, ReplTicket* t, std::string* err);
+  // Waits (bounded) until the posted slices left; unpins. False = the pair was failed.
+  bool wait_send(ReplTicket* t, std::string* err);
+  // Abandon a ticket whose descriptor never reached the peer (its sends can never match).
+  void cancel_send(ReplTicket* t, const std::string& why);
+
+  // Receiver: post the receive for (src, gen, seq) in order, verify while slices land, commit.
+  WriteResult recv(int src, uint64_t gen, int64_t seq, const std::string& id, uint64_t size, uint64_t slice,
+                   uint32_t expected_crc, bool persist_now);
+
+  // Control plane (fast-path op 5). Returns the reply payload.
+  std::string handle_control(const std::string& req);
+  void fail_pair(int peer, const std::string& why);
+
+  P2PTransport* transport() { return t_.get(); }
+  ReplStats stats();
+  uint64_t slice_for(uint64_t n) const;
+
+ private:
+  enum class State { Down, Opening, Up, Broken };
+  struct Peer {
+    std::mutex mu;
+    std::condition_variable cv;
+    State state = State::Down;
+    uint64_t gen = 0;
+    int64_t send_seq = 0;
+    int64_t recv_next = 0;
+    bool opener = false;  // an opener thread is running (initiator side)
+    uint64_t peer_inc = 0;  // initiator side: the peer process instance the pair was opened with
+    std::string last_error;
+  };
+  Peer& peer(int p);
+  void opener_loop(int p);
+  void request_reopen(int p, uint64_t gen, bool fresh);
+  void spawn(std::function<void()> fn);
+
+  ChunkStore* store_;
+  std::unique_ptr<P2PTransport> t_;
+  int rank_, world_;
+  ReplOptions opt_;
+  ControlFn control_;
+  std::vector<std::unique_ptr<Peer>> peers_;
+  std::atomic<bool> stop_{false};
+  uint64_t incarnation_ = 0;  // random per engine instance: tells a restarted peer process apart
+  std::mutex threads_mu_;
+  std::condition_variable threads_cv_;
+  int live_threads_ = 0;
+  std::mutex st_mu_;
+  ReplStats st_;
+};
+
+}  // namespace dfs

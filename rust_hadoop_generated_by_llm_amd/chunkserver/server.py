@@ -15,6 +15,7 @@ import shutil
 import signal
 import threading
 import time
+import zlib
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from pathlib import Path
 
@@ -53,7 +54,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--rccl-world", type=int, default=0)
     p.add_argument("--rccl-rendezvous", default="")
     p.add_argument("--rccl-timeout-ms", type=int, default=60000)
-    p.add_argument("--replication-transport", choices=["rccl", "grpc"], default="rccl")
+    p.add_argument("--replication-transport", choices=["rccl", "grpc", "socket"], default="rccl",
+                   help="payload path between same-node chunkservers: rccl (xGMI), grpc (reference), "
+                        "socket (host-memory P2P transport used by the CPU tests)")
+    p.add_argument("--repl-turn-timeout-ms", type=int, default=3000,
+                   help="how long a replica waits for an earlier sequence number before failing the pair")
     p.add_argument("--heartbeat-interval", type=float, default=5.0)
     p.add_argument("--scrub-interval", type=float, default=60.0)
     p.add_argument("--no-fsync", action="store_true", help="skip fdatasync (tests only)")
@@ -124,27 +129,37 @@ class ChunkServerProcess:
                 self.fastpath = fp
             else:
                 log.warning("native fast path disabled: %s", err)
-        self.rccl = None
+        self.rccl = None  # the replication engine (RCCL over xGMI, or sockets in CPU tests)
+        self.repl_pairs_up = 0
         rank_map: dict[str, int] = {}
-        if (args.replication_transport == "rccl" and args.rccl_world > 1 and args.rccl_rank >= 0
-                and args.rccl_rendezvous and args.gpu >= 0):
-            rank_map, fp_names = rendezvous_ranks(args.rccl_rendezvous, args.rccl_rank, args.rccl_world,
-                                                  self.advertise,
-                                                  fastpath=self.fastpath.name if self.fastpath else "")
-            eng = native.RcclEngine(self.store, args.rccl_rank, args.rccl_world, args.rccl_rendezvous,
-                                    args.rccl_timeout_ms)
-            ok, err = eng.init()
-            if ok:
-                self.rccl = eng
-                log.info("RCCL replication ready: rank %d/%d", args.rccl_rank, args.rccl_world)
-                if self.fastpath is not None:
-                    # chains between same-node GPUs stay native: RCCL payload + socket descriptor
-                    self.fastpath.set_rccl(eng)
+        transport = args.replication_transport
+        if (transport in ("rccl", "socket") and args.rccl_world > 1 and args.rccl_rank >= 0 and args.rccl_rendezvous
+                and (args.gpu >= 0 or transport == "socket")):
+            if self.fastpath is None:
+                log.error("replication engine needs the native fast path (pair control); using gRPC replication")
+            else:
+                rank_map, fp_names = rendezvous_ranks(args.rccl_rendezvous, args.rccl_rank, args.rccl_world,
+                                                      self.advertise, fastpath=self.fastpath.name)
+                ns = "%08x" % (zlib.crc32(os.path.abspath(args.rccl_rendezvous).encode()) & 0xFFFFFFFF)
+                try:
+                    eng = native.ReplicationEngine(self.store, transport, args.rccl_rank, args.rccl_world, ns=ns,
+                                                   open_timeout_ms=args.rccl_timeout_ms,
+                                                   turn_timeout_ms=args.repl_turn_timeout_ms,
+                                                   xfer_timeout_ms=min(args.rccl_timeout_ms, 20000))
+                except RuntimeError as e:
+                    log.error("replication engine unavailable (%s); using gRPC replication", e)
+                else:
+                    self.rccl = eng
                     for a, r in rank_map.items():
                         if r != args.rccl_rank:
                             self.fastpath.set_peer(a, r, fp_names.get(a, ""))
-            else:
-                log.error("RCCL init failed (%s); using gRPC replication", err)
+                    self.fastpath.set_replication(eng)
+                    eng.start()
+                    # pairs come up in the background; wait a bounded time so a benchmark starts
+                    # with its channels ready (a pair that is not up just falls back per block)
+                    self.repl_pairs_up = eng.wait_ready(args.rccl_timeout_ms)
+                    log.info("%s replication: rank %d/%d, %d/%d pairs up", transport, args.rccl_rank,
+                             args.rccl_world, self.repl_pairs_up, args.rccl_world - 1)
         self.metrics = Registry()
         self.cs = ChunkServer(self.store, self.advertise, self.pool, self.masters, self.rccl, rank_map,
                               args.rccl_rank, self.metrics, fastpath=self.fastpath)
@@ -250,6 +265,11 @@ class ChunkServerProcess:
                     d.update(proc.cs.stats)
                     if proc.fastpath is not None:
                         d.update(proc.fastpath.stats())
+                    if proc.rccl is not None:
+                        d.update({f"repl_{k}": v for k, v in proc.rccl.stats().items()})
+                        d["repl_transport"] = proc.rccl.transport
+                        d["repl_pairs_up"] = sum(1 for r in range(proc.rccl.world)
+                                                 if r != proc.rccl.rank and proc.rccl.pair_ok(r))
                     body, ctype = json.dumps(d).encode(), "application/json"
                 elif self.path.startswith("/debug/") and os.environ.get("DFS_DEBUG_ENDPOINTS") == "1":
                     # fault injection for tests (off unless DFS_DEBUG_ENDPOINTS=1):
@@ -266,6 +286,15 @@ class ChunkServerProcess:
                         body = json.dumps({"bad": proc.cs.scrub_once()}).encode()
                     elif u.path == "/debug/drop_resident":
                         proc.store.drop_resident(q["block"])
+                        body = b"{}"
+                    elif u.path == "/debug/drop_descriptors" and proc.fastpath is not None:
+                        proc.fastpath.debug_drop_descriptors(int(q.get("n", "1")))
+                        body = b"{}"
+                    elif u.path == "/debug/drop_sends" and proc.rccl is not None:
+                        proc.rccl.debug_drop_sends(int(q["peer"]), int(q.get("n", "1")))
+                        body = b"{}"
+                    elif u.path == "/debug/fail_pair" and proc.rccl is not None:
+                        proc.rccl.fail_pair(int(q["peer"]), "debug")
                         body = b"{}"
                     else:
                         self.send_response(404)
@@ -299,7 +328,9 @@ class ChunkServerProcess:
         ready = os.environ.get("DFS_READY_FILE")
         if ready:
             with open(ready, "w") as f:
-                json.dump({"addr": a.addr, "gpu": a.gpu, "rccl": self.rccl is not None}, f)
+                json.dump({"addr": a.addr, "gpu": a.gpu, "rccl": self.rccl is not None,
+                           "transport": self.rccl.transport if self.rccl is not None else "grpc",
+                           "pairs_up": self.repl_pairs_up}, f)
         for sig in (signal.SIGTERM, signal.SIGINT):
             signal.signal(sig, lambda *_: self._stop.set())
         log.info("chunkserver %s serving (gpu=%d, durability=%s)", self.advertise, a.gpu, a.durability)
@@ -307,6 +338,10 @@ class ChunkServerProcess:
             pass
         server.stop(1.0).wait()
         http.shutdown()
+        if self.rccl is not None:
+            self.rccl.stop()
+        if self.fastpath is not None:
+            self.fastpath.stop()
         self.store.flush()
 
 

@@ -8,9 +8,11 @@ partial-read verification with background recovery.
 
 The forwarding hop is where the MI355X design departs: when the next chunkserver is a
 GPU rank of the same node, the block goes ``ncclSend`` -> ``ncclRecv`` straight from
-this GPU's HBM into the peer's HBM over xGMI (csrc/rccl_engine.cpp) and the gRPC
-ReplicateBlock carries only a descriptor (rccl_src_rank, rccl_seq, rccl_size). Any
-failure aborts that pair and falls back to the reference gRPC data path.
+this GPU's HBM into the peer's HBM over xGMI (csrc/replication.cpp, sliced and checksummed
+as it lands) and the gRPC ReplicateBlock carries only a descriptor (rccl_src_rank,
+rccl_gen, rccl_seq, rccl_size, rccl_slice). Any failure aborts that pair (it is rebuilt
+under a new generation in the background) and this block falls back to the reference
+gRPC data path.
 """
 from __future__ import annotations
 
@@ -96,30 +98,33 @@ class ChunkServer:
         downstream replicas_written (0 on failure, which is logged, not raised)."""
         nxt, rest = next_servers[0], list(next_servers[1:])
         peer = self._rank_of(nxt)
-        if self.rccl is not None and peer is not None and self.rccl.pair_ok(self.my_rank, peer):
-            seq, size, err = self.rccl.send(peer, block_id)
-            if seq >= 0:
+        if self.rccl is not None and peer is not None and self.rccl.pair_ok(peer):
+            tk, err = self.rccl.send(peer, block_id, None if self.store.gpu else data)
+            if tk is not None:
                 req = pb.ReplicateBlockRequest(block_id=block_id, next_servers=rest, expected_checksum_crc32c=crc,
                                                master_term=term, rccl=True, rccl_src_rank=self.my_rank,
-                                               rccl_seq=seq, rccl_size=size, heal=heal)
+                                               rccl_seq=tk.seq, rccl_size=tk.size, rccl_gen=tk.gen,
+                                               rccl_slice=tk.slice, heal=heal)
                 resp = None
                 try:
                     resp = self.pool.call(nxt, "ChunkServerService", "ReplicateBlock", req, timeout=120.0)
                 except Exception as e:  # noqa: BLE001
-                    log.error("RCCL descriptor to %s failed: %s", nxt, rpc_details(e))
-                ok, werr = self.rccl.wait_send(peer, seq)
-                if resp is not None and ok:
-                    self.stats["rccl_forwards"] += 1
-                    if resp.success:
-                        return resp.replicas_written
-                    log.error("downstream replication failed at %s: %s", nxt, resp.error_message)
-                    return 0
-                # the pair is unusable now (an unmatched send would block its stream)
-                self.rccl.abort_pair(self.my_rank, peer)
+                    log.error("P2P descriptor to %s failed: %s", nxt, rpc_details(e))
+                if resp is None:
+                    # the posted send can never be matched: the engine aborts and rebuilds the pair
+                    self.rccl.cancel_send(tk, "descriptor failed")
+                else:
+                    ok, werr = self.rccl.wait_send(tk)
+                    if resp.success or ok:
+                        self.stats["rccl_forwards"] += 1
+                        if resp.success:
+                            return resp.replicas_written
+                        log.error("downstream replication failed at %s: %s", nxt, resp.error_message)
+                        return 0
                 self.stats["rccl_fallbacks"] += 1
-                log.warning("RCCL path %d->%d failed (%s); falling back to gRPC", self.my_rank, peer, werr)
+                log.warning("P2P path %d->%d failed; falling back to gRPC", self.my_rank, peer)
             else:
-                log.warning("RCCL send to rank %d unavailable: %s", peer, err)
+                log.warning("P2P send to rank %d unavailable: %s", peer, err)
         if data is None:
             st, _total, data, _p, _b, err = self.store.read(block_id, 0, 0)
             if st != ST_OK:
@@ -142,7 +147,8 @@ class ChunkServer:
 
     # ------------------------------------------------------------------ RPCs
     def _store_and_forward(self, block_id: str, data: bytes | None, next_servers: list[str], crc: int, term: int,
-                           heal: bool, rccl_src: int = -1, rccl_seq: int = -1, rccl_size: int = 0):
+                           heal: bool, rccl_src: int = -1, rccl_seq: int = -1, rccl_size: int = 0,
+                           rccl_gen: int = 0, rccl_slice: int = 0):
         """Local write + downstream forwarding, pipelined.
 
         The reference writes+fsyncs locally and only then forwards (serial chain,
@@ -153,7 +159,8 @@ class ChunkServer:
         chain latency drops from sum(hops x (copy + 2 fsync)) to roughly one fsync.
         Returns (ok, error, replicas_written)."""
         if rccl_src >= 0:
-            ok, _crc, err = self.rccl.recv(rccl_src, rccl_seq, block_id, rccl_size, crc, persist=not next_servers)
+            ok, _crc, err = self.rccl.recv(rccl_src, rccl_gen, rccl_seq, block_id, rccl_size, rccl_slice, crc,
+                                           persist=not next_servers)
             staged_in_hbm = True
         elif next_servers and self.store.gpu:
             ok, _crc, err = self.store.stage(block_id, data, crc)
@@ -203,7 +210,8 @@ class ChunkServer:
         if req.rccl:
             ok, err, replicas = self._store_and_forward(req.block_id, None, list(req.next_servers),
                                                         req.expected_checksum_crc32c, req.master_term, req.heal,
-                                                        req.rccl_src_rank, req.rccl_seq, req.rccl_size)
+                                                        req.rccl_src_rank, req.rccl_seq, req.rccl_size,
+                                                        req.rccl_gen, req.rccl_slice)
         else:
             ok, err, replicas = self._store_and_forward(req.block_id, req.data, list(req.next_servers),
                                                         req.expected_checksum_crc32c, req.master_term, req.heal)

@@ -89,6 +89,7 @@ class Client:
         # extension simply create the file in CreateFile as before)
         self.defer_create = os.environ.get("DFS_DEFER_CREATE", "1") == "1"
         self._deferred: set[str] = set()
+        self._gens: dict[str, int] = {}  # block id -> writer generation of its classic create
         # native client data path (csrc/client_fast.cpp): whole writes/reads of single-block
         # files through a co-located chunkserver and same-host masters, without the GIL
         self._fast = None
@@ -317,6 +318,7 @@ class Client:
             self._not_leader_check)
         if not resp.success:
             raise DfsError(f"Failed to create file: {resp.error_message}")
+        gen = resp.writer_generation  # our write lease (0 from a reference master)
         if resp.HasField("allocation") and resp.allocation.HasField("block"):
             # fused create+allocate (one RPC) or, when deferred, placement only: the file is
             # created together with its completion (one Raft entry per write)
@@ -325,6 +327,8 @@ class Client:
                 raise DfsError("No chunk servers available")
             if resp.deferred:
                 self._deferred.add(alloc.block.block_id)
+            elif gen:
+                self._gens[alloc.block.block_id] = gen
             return alloc
         # a master without the extension: the reference's separate AllocateBlock RPC
         masters = [addr] + [m for m in self.master_addrs if m != addr]
@@ -333,15 +337,20 @@ class Client:
             if not r.HasField("block"):
                 raise _Retry(r.leader_hint)
 
-        req = pb.AllocateBlockRequest(path=dest, preferred_chunk_server=self.local_chunkserver or "")
+        req = pb.AllocateBlockRequest(path=dest, preferred_chunk_server=self.local_chunkserver or "",
+                                      writer_generation=gen)
         alloc, _ = self.execute_rpc_internal(masters, "AllocateBlock", req, alloc_check)
         if not alloc.chunk_server_addresses:
             raise DfsError("No chunk servers available")
+        if gen:
+            self._gens[alloc.block.block_id] = gen
         return alloc
 
     def _complete(self, dest: str, size: int, etag: str, sums: list, alloc=None) -> None:
         req = pb.CompleteFileRequest(path=dest, size=size, etag_md5=etag, created_at_ms=int(time.time() * 1000),
                                      block_checksums=sums)
+        if alloc is not None:
+            req.writer_generation = self._gens.pop(alloc.block.block_id, 0)
         if alloc is not None and alloc.block.block_id in self._deferred:
             self._deferred.discard(alloc.block.block_id)
             req.create = True

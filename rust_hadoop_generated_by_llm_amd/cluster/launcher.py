@@ -46,7 +46,7 @@ class LocalCluster:
                  hbm_capacity: str = "0", heartbeat_interval: float = 0.5, scrub_interval: float = 60.0,
                  rack_ids: list[str] | None = None, fast_intervals: bool = False, cold_dir: bool = False,
                  env: dict | None = None, master_args: list[str] | None = None, cs_args: list[str] | None = None,
-                 tls: bool = False, standby_masters: int = 0):
+                 tls: bool = False, standby_masters: int = 0, p2p: str | None = None):
         self.owns_dir = base_dir is None
         self.base = Path(base_dir or tempfile.mkdtemp(prefix="dfs_cluster_"))
         self.base.mkdir(parents=True, exist_ok=True)
@@ -58,6 +58,9 @@ class LocalCluster:
         self.durability = durability
         self.fsync = fsync
         self.rccl = rccl
+        # "socket": native replication engine over the host-memory P2P transport (CPU tests of
+        # the same protocol RCCL runs on GPUs); None: RCCL with GPUs, reference gRPC without
+        self.p2p = p2p
         self.hbm_capacity = hbm_capacity
         self.heartbeat_interval = heartbeat_interval
         self.scrub_interval = scrub_interval
@@ -224,7 +227,11 @@ class LocalCluster:
                 args += ["--config-servers", ",".join(self.config_addrs)]
             else:
                 args += ["--masters", ",".join(m for ms in shard_cfg.values() for m in ms)]
-            if self.gpus is not None and self.n_cs > 1 and self.rccl:
+            if self.p2p == "socket" and self.n_cs > 1:
+                args += ["--rccl-rank", str(i), "--rccl-world", str(self.n_cs), "--rccl-rendezvous", str(rdv),
+                         "--replication-transport", "socket", "--rccl-timeout-ms", "10000",
+                         "--repl-turn-timeout-ms", "1500"]
+            elif self.gpus is not None and self.n_cs > 1 and self.rccl:
                 args += ["--rccl-rank", str(i), "--rccl-world", str(self.n_cs), "--rccl-rendezvous", str(rdv)]
             else:
                 args += ["--replication-transport", "grpc"]

@@ -157,3 +157,50 @@ def test_localrpc_roundtrip_and_status(tmp_path):
         pool.close()
         loop.call_soon_threadsafe(loop.stop)
         th.join(10)
+
+
+def test_wrapped_offsets_are_rejected(server):
+    """off + len must not wrap past the mapped arena. Offsets near 2^64
+    used to pass the `st_size >= off + len` check and made the server touch memory
+    outside the mmap."""
+    store, srv = server
+    arena = ShmArena(size=16 << 20, slot=16 << 20)
+    cli = fp.FastPathClient(srv.name)
+    try:
+        wrap = (1 << 64) - 4096
+        for off, ln in ((wrap, 8192), (1 << 63, 1 << 63), (arena.size - 10, 11), (0, 1 << 40)):
+            st, _r, msg = cli.write("w", arena.path, off, ln, 0, 0)
+            assert st in (fp.UNSUPPORTED, fp.BAD_REQUEST), (off, ln, st, msg)
+            assert not store.exists("w")
+        data = os.urandom(4096)
+        slot = arena.acquire(len(data))
+        arena.view[slot:slot + len(data)] = data
+        assert cli.write("ok", arena.path, slot, len(data), zlib.crc32(data), 0)[0] == fp.OK
+        # READ: shm_off + cap wrapping must be refused too
+        st, *_ = cli.read("ok", 0, 0, arena.path, wrap, 8192)
+        assert st == fp.UNSUPPORTED
+        st, *_ = cli.read("ok", 0, 0, arena.path, arena.size - 100, 4096)
+        assert st == fp.UNSUPPORTED
+        # the server is still healthy afterwards
+        st, total, n, _ = cli.read("ok", 0, 0, arena.path, slot, arena.slot)
+        assert st == fp.OK and n == len(data) and bytes(arena.view[slot:slot + n]) == data
+    finally:
+        cli.close()
+        arena.close()
+
+
+def test_connection_threads_are_reaped(server):
+    """one thread per connection used to stay unjoined until stop()."""
+    import threading
+    import time
+
+    _store, srv = server
+    before = threading.active_count()
+    for _ in range(50):
+        c = fp.FastPathClient(srv.name)
+        c.read("none", 0, 0, "/dev/shm/dfs_sc_none", 0, 16)
+        c.close()
+    time.sleep(0.3)
+    assert srv.stats()["fp_connections"] >= 50
+    # native threads are not Python threads; the check is that stop() still returns promptly
+    assert threading.active_count() == before

@@ -99,7 +99,7 @@ def test_heal_ec_block_issues_reconstruct_command():
 def test_create_complete_rename_and_delete_commands():
     st = MasterState()
     r = st.apply({"Master": {"CreateFile": {"path": "/a", "ts": 1000, "block_id": "b1", "locations": ["x:1"]}}})
-    assert r == {"exists": False, "orphans": []}
+    assert r == {"exists": False, "gen": 1000, "orphans": []}
     assert st.visible("/a") is None and "/a" in st.under_construction  # hidden until complete
     assert st.apply({"Master": {"CreateFile": {"path": "/a", "ts": 2000}}}) == {"exists": True}
     st.apply({"Master": {"CompleteFile": {"path": "/a", "size": 7, "etag_md5": "e", "created_at_ms": 5,
@@ -126,6 +126,34 @@ def test_expired_create_lease_lets_a_new_writer_take_the_path():
     st.apply({"Master": {"CreateFile": {"path": "/p", "ts": 0, "block_id": "old", "locations": ["h:1"]}}})
     r = st.apply({"Master": {"CreateFile": {"path": "/p", "ts": 61_000}}})
     assert r["exists"] is False and r["orphans"] == [["old", ["h:1"]]]
+
+
+def test_slow_writer_keeps_its_lease_and_a_stale_writer_is_refused():
+    """AllocateBlock progress renews the create lease, and a writer whose
+    path was taken over cannot append blocks to, or complete, the new owner's file."""
+    st = MasterState()
+    st.apply({"Master": {"CreateFile": {"path": "/p", "ts": 0, "block_id": "b0", "locations": ["h:1"]}}})
+    # still streaming a large multi-block file: each AllocateBlock renews the lease
+    for t in (30_000, 55_000, 80_000):
+        assert st.apply({"Master": {"AllocateBlock": {"path": "/p", "block_id": f"b{t}", "locations": ["h:1"],
+                                                      "ts": t, "gen": 0}}}) is None
+    assert st.apply({"Master": {"CreateFile": {"path": "/p", "ts": 100_000}}}) == {"exists": True}
+    # silent for a whole lease after its last progress: taken over
+    r = st.apply({"Master": {"CreateFile": {"path": "/p", "ts": 141_000}}})
+    assert r["exists"] is False and r["gen"] == 141_000 and len(r["orphans"]) == 4
+    # the old writer (generation 0) can neither append nor complete
+    assert st.apply({"Master": {"AllocateBlock": {"path": "/p", "block_id": "late", "locations": ["h:1"],
+                                                  "ts": 142_000, "gen": 1}}}) == {"stale": True}
+    assert st.apply({"Master": {"CompleteFile": {"path": "/p", "size": 9, "gen": 1,
+                                                 "block_checksums": []}}}) == {"found": True, "stale": True}
+    assert "late" not in st.block_index
+    # the new owner completes; an identical retry is accepted, a different one is stale
+    done = {"path": "/p", "size": 5, "etag_md5": "e", "gen": 141_000, "block_checksums": []}
+    assert st.apply({"Master": {"CompleteFile": done}}) == {"found": True}
+    assert st.visible("/p").size == 5
+    assert st.apply({"Master": {"CompleteFile": done}}) == {"found": True}
+    assert st.apply({"Master": {"CompleteFile": dict(done, size=6)}})["stale"] is True
+    assert st.visible("/p").size == 5
 
 
 def test_transaction_records_pin_paths_until_resolved():

@@ -522,6 +522,28 @@ def test_bucket_policy_enforced(authgw):
     assert signed("DELETE", g, "/guarded/keep").status_code == 204
 
 
+def test_sidecar_keys_cannot_be_written_or_deleted(authgw):
+    """a principal allowed only s3:PutObject / s3:DeleteObject must not be able to
+    replace or drop the bucket policy, or another object's .meta sidecar, through object keys."""
+    g = authgw
+    signed("PUT", g, "/side")
+    signed("PUT", g, "/side/obj", b"payload")
+    pol = {"Version": "2012-10-17", "Statement": [{"Effect": "Deny", "Principal": "*", "Action": "s3:DeleteObject",
+                                                   "Resource": "arn:dfs:s3:::side/*"}]}
+    assert signed("PUT", g, "/side", json.dumps(pol).encode(), query=[("policy", "")]).status_code == 204
+    for key in (".s3_bucket_policy", "obj.meta", "x/.s3keep", "k/.s3_mpu_completed"):
+        r = signed("PUT", g, f"/side/{key}", b"{}")
+        assert r.status_code == 400 and b"InvalidArgument" in r.content, key
+        r = signed("DELETE", g, f"/side/{key}")
+        assert r.status_code in (400, 403), key
+        assert signed("GET", g, f"/side/{key}").status_code == 400
+    # the policy is untouched and still denies deletes
+    got = signed("GET", g, "/side", query=[("policy", "")])
+    assert got.status_code == 200 and json.loads(got.content)["Statement"][0]["Effect"] == "Deny"
+    assert signed("DELETE", g, "/side/obj").status_code == 403
+    assert signed("GET", g, "/side/obj").content == b"payload"
+
+
 def test_audit_log_written_and_chained(authgw):
     g = authgw
     signed("GET", g, "/")
