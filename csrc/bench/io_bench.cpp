@@ -118,6 +118,7 @@ static void disk_case(const std::string& dir, int threads, int per, bool direct,
 int main(int argc, char** argv) {
   int device = 0, iters = 50;
   bool fsync = true;
+  bool zero_copy = true;
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--disk-sweep") {
       std::string dir = "/tmp/io_bench_disk";
@@ -160,13 +161,16 @@ int main(int argc, char** argv) {
     else if (a == "--dir" && i + 1 < argc) dir = argv[++i];
     else if (a == "--iters" && i + 1 < argc) iters = std::atoi(argv[++i]);
     else if (a == "--no-fsync") fsync = false;
+    else if (a == "--staged") zero_copy = false;
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) device = -1;
   std::filesystem::remove_all(dir);
 
-  std::printf("{\n  \"device\": %d, \"iters\": %d, \"fsync\": %s,\n  \"store\": {", device, iters,
-              fsync ? "true" : "false");
+  // zero_copy: the client buffers are registered with the store the way the fast path
+  // registers a client's shared-memory arena (one DMA per copy); --staged: pinned bounce
+  std::printf("{\n  \"device\": %d, \"iters\": %d, \"fsync\": %s, \"zero_copy\": %s,\n  \"store\": {", device,
+              iters, fsync ? "true" : "false", zero_copy ? "true" : "false");
   bool first = true;
   const size_t sizes[] = {4096, 65536, 1 << 20, 64u << 20};
   for (int mode = 0; mode < 2; ++mode) {
@@ -184,6 +188,7 @@ int main(int argc, char** argv) {
       uint32_t crc = crc32(data.data(), sz);
       Lat w, r, pr;
       std::vector<uint8_t> out(sz);
+      bool reg = zero_copy && store.register_host(data.data(), sz) && store.register_host(out.data(), sz);
       for (int i = 0; i < n; ++i) {
         std::string id = std::string("b") + std::to_string(mode) + "_" + std::to_string(sz) + "_" + std::to_string(i);
         auto t0 = Clock::now();
@@ -212,6 +217,10 @@ int main(int argc, char** argv) {
           }
           pr.add(secs(t0, t1));
         }
+      }
+      if (reg) {
+        store.unregister_host(data.data());
+        store.unregister_host(out.data());
       }
       emit_case(first, tag, sz, w);
       emit_case(first, mode == 0 ? "read_after_nvme_sync" : "read_after_hbm_ack", sz, r);

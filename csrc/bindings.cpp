@@ -295,6 +295,9 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["crc_mismatches"] = t.crc_mismatches;
         d["gpu_kernel_launches"] = t.gpu_kernel_launches;
         d["disk_gate_waits"] = t.disk_gate_waits;
+        d["direct_dma"] = t.direct_dma;
+        d["staged_dma"] = t.staged_dma;
+        d["host_registered_bytes"] = t.host_registered_bytes;
         return d;
       })
       .def("gpu_crc", [](ChunkStore& s, py::buffer data) {
@@ -399,6 +402,7 @@ PYBIND11_MODULE(_dfs_native, m) {
              std::unique_ptr<P2PTransport> t;
              if (transport == "rccl") t = make_rccl_transport(store->config().device, rank, &err);
              else if (transport == "socket") t = make_socket_transport(rank, ns);
+             else if (transport == "hiploop" && store->gpu()) t = make_hiploop_transport(store->config().device, rank, ns);
              else err = "unknown transport " + transport;
              if (!t) throw std::runtime_error(err);
              ReplOptions o;

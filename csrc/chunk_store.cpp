@@ -388,7 +388,45 @@ bool ChunkStore::run_crc(Lane* l, const uint8_t* dptr, uint64_t n, uint32_t* met
   return true;
 }
 
+bool ChunkStore::register_host(const void* p, uint64_t n) {
+  if (!gpu() || !p || !n) return false;
+  HIP_OK(hipSetDevice(cfg_.device));
+  if (hipHostRegister(const_cast<void*>(p), n, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  std::lock_guard<std::mutex> g(reg_mu_);
+  reg_.emplace_back(reinterpret_cast<uintptr_t>(p), n);
+  return true;
+}
+
+void ChunkStore::unregister_host(const void* p) {
+  if (!gpu()) return;
+  std::lock_guard<std::mutex> g(reg_mu_);
+  for (auto it = reg_.begin(); it != reg_.end(); ++it)
+    if (it->first == reinterpret_cast<uintptr_t>(p)) {
+      (void)hipSetDevice(cfg_.device);
+      (void)hipHostUnregister(const_cast<void*>(p));
+      reg_.erase(it);
+      return;
+    }
+}
+
+bool ChunkStore::host_registered(const void* p, uint64_t n) {
+  uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> g(reg_mu_);
+  for (auto& r : reg_)
+    if (a >= r.first && n <= r.second && a - r.first <= r.second - n) return true;
+  return false;
+}
+
 bool ChunkStore::h2d_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n) {
+  if (host_registered(src, n)) {  // one DMA straight from the client's pinned slot
+    HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, l->stream));
+    direct_dma_++;
+    return true;
+  }
+  staged_dma_++;
   int i = 0;
   for (uint64_t off = 0; off < n; off += kChunk, i ^= 1) {
     uint64_t len = std::min<uint64_t>(kChunk, n - off);
@@ -401,6 +439,12 @@ bool ChunkStore::h2d_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t
 }
 
 bool ChunkStore::d2h_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n) {
+  if (host_registered(dst, n)) {  // straight into the client's pinned slot; caller syncs
+    HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, l->stream));
+    direct_dma_++;
+    return true;
+  }
+  staged_dma_++;
   uint64_t nch = (n + kChunk - 1) / kChunk;
   auto issue = [&](uint64_t c) {
     uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
@@ -1550,6 +1594,12 @@ StoreStats ChunkStore::stats() {
   s.hbm_used = alloc_.used();
   s.spill_queue = spill_q_.size();
   s.gpu_kernel_launches = launches_.load();
+  s.direct_dma = direct_dma_.load();
+  s.staged_dma = staged_dma_.load();
+  {
+    std::lock_guard<std::mutex> rg(reg_mu_);
+    for (auto& r : reg_) s.host_registered_bytes += r.second;
+  }
   return s;
 }
 

@@ -81,6 +81,9 @@ struct StoreStats {
   uint64_t crc_mismatches = 0;
   uint64_t gpu_kernel_launches = 0;
   uint64_t disk_gate_waits = 0;  // durable writes that queued for a node-wide disk slot
+  uint64_t direct_dma = 0;       // host<->HBM copies done straight from registered memory
+  uint64_t staged_dma = 0;       // copies bounced through pinned staging buffers
+  uint64_t host_registered_bytes = 0;
 };
 
 // Group commit of data files: callers that finished writing share one syncfs() round.
@@ -152,6 +155,11 @@ class ChunkStore {
   void release(const DevExtent& e);
   WriteResult commit_device(const std::string& id, const DevExtent& e, uint64_t n, uint32_t expected_crc,
                             hipStream_t s, bool persist_now = true);
+  // Zero-copy host<->HBM: host memory registered here (the clients' shared-memory arenas,
+  // mapped by the fast path) is DMA'd directly by the copy engines; anything else bounces
+  // through the lanes' pinned staging buffers.
+  bool register_host(const void* p, uint64_t n);
+  void unregister_host(const void* p);
   // Pipelined receive (replication.cpp): while slices of a block land in a reserved extent,
   // each landed byte range is checksummed on a store lane (K1 into the extent's .meta image)
   // so verification overlaps the transfer; finish() folds the slice CRCs into the block CRC,
@@ -259,7 +267,11 @@ class ChunkStore {
   bool stop_ = false;
   StoreStats st_;
   std::atomic<uint64_t> launches_{0};
-  std::atomic<uint64_t> tmp_seq_{0};  // unique temporary file names for in-flight writes
+  std::atomic<uint64_t> tmp_seq_{0};
+  bool host_registered(const void* p, uint64_t n);
+  std::mutex reg_mu_;
+  std::vector<std::pair<uintptr_t, uint64_t>> reg_;  // registered host ranges
+  std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};  // unique temporary file names for in-flight writes
   std::unique_ptr<GroupSync> gsync_;
   std::unique_ptr<DiskGate> gate_;
 };

@@ -170,9 +170,15 @@ void FastPathServer::stop() {
   std::unique_lock<std::mutex> g(mu_);
   for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
   workers_cv_.wait(g, [this] { return live_workers_ == 0; });
-  for (auto& kv : maps_) ::munmap(kv.second.p, kv.second.size);
+  for (auto& kv : maps_) {
+    if (kv.second.registered) store_->unregister_host(kv.second.p);
+    ::munmap(kv.second.p, kv.second.size);
+  }
   maps_.clear();
-  for (auto& m : retired_) ::munmap(m.p, m.size);
+  for (auto& m : retired_) {
+    if (m.registered) store_->unregister_host(m.p);
+    ::munmap(m.p, m.size);
+  }
   retired_.clear();
   std::lock_guard<std::mutex> pg(peers_mu_);
   for (auto& kv : peers_)
@@ -296,6 +302,9 @@ uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t off, uint64_t
   }
   m.p = static_cast<uint8_t*>(p);
   m.size = static_cast<uint64_t>(sb.st_size);
+  // pin the client's arena for the GPU copy engines: blocks then move slot <-> HBM in one
+  // DMA, with no bounce through staging buffers and no CPU memcpy (falls back if refused)
+  m.registered = store_->gpu() && store_->register_host(m.p, m.size);
   return m.p;
 }
 

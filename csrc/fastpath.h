@@ -136,6 +136,7 @@ class FastPathServer {
   struct Mapping {
     uint8_t* p = nullptr;
     uint64_t size = 0;
+    bool registered = false;  // hipHostRegister'ed for direct DMA
   };
   std::unordered_map<std::string, Mapping> maps_;
   std::vector<Mapping> retired_;

@@ -63,5 +63,8 @@ class P2PTransport {
 std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, std::string* err);
 // Host-memory transport over abstract UNIX sockets; `ns` keeps test clusters apart.
 std::unique_ptr<P2PTransport> make_socket_transport(int rank, const std::string& ns);
+// Single-GPU test transport: engines in ONE process (stores on the same GPU) exchange device
+// buffers with the RCCL matching contract, each matched pair a D2D copy (p2p_hiploop.cpp).
+std::unique_ptr<P2PTransport> make_hiploop_transport(int device, int rank, const std::string& ns);
 
 }  // namespace dfs
