@@ -1,0 +1,170 @@
+// Kernel-only microbenchmark of the checksum kernels on device-resident data (no H2D):
+// K1+K2 (per-slice .meta + whole-block CRC) at several block sizes, and the K1b batched
+// scrub over 1 GiB of 1 MiB blocks — each with the matrix-core chunk CRC (MFMA) and with
+// the LDS slicing-by-16 tables, every result checked against the host CRC.
+//
+//   build/native/crc_bench [--iters N] [--mib TOTAL]     -> JSON on stdout
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "crc32.h"
+#include "gpu_kernels.h"
+
+using namespace dfs;
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(2);                                                                  \
+    }                                                                                \
+  } while (0)
+
+struct Run {
+  double us;
+  bool ok;
+};
+
+static Run bench_block(const uint8_t* d, uint64_t n, const DevCrcTables* t, uint32_t* dmeta, uint32_t* dpart,
+                       hipStream_t s, int iters, const std::vector<uint8_t>& host) {
+  CrcLaunch a{};
+  a.data = d;
+  a.n = n;
+  a.s_full = n / kSliceBytes;
+  a.slice_lo = 0;
+  a.slice_hi = a.s_full;
+  a.vfront = (kSlicesPerTile - a.s_full % kSlicesPerTile) % kSlicesPerTile;
+  a.ntiles = (a.s_full + a.vfront) / kSlicesPerTile;
+  a.full_init = crc_init_term(kSliceBytes);
+  a.meta_out = dmeta;
+  a.part_crc = dpart;
+  int grid = crc_grid_for(a.ntiles, 0);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  CK(launch_crc(a, t, grid, s));  // warm-up + correctness
+  std::vector<uint32_t> part(grid), meta(a.s_full);
+  CK(hipMemcpyAsync(part.data(), dpart, grid * 4, hipMemcpyDeviceToHost, s));
+  CK(hipMemcpyAsync(meta.data(), dmeta, a.s_full * 4, hipMemcpyDeviceToHost, s));
+  CK(hipStreamSynchronize(s));
+  uint32_t r = 0;
+  for (uint32_t v : part) r ^= v;
+  r ^= crc_init_term(n);
+  bool ok = r == crc32(host.data(), n);
+  std::vector<uint32_t> ref(a.s_full);
+  crc32_slices(host.data(), n, ref.data());
+  for (uint64_t i = 0; ok && i < a.s_full; ++i) ok = __builtin_bswap32(meta[i]) == ref[i];
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) CK(launch_crc(a, t, grid, s));
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return {1e3 * ms / iters, ok};
+}
+
+int main(int argc, char** argv) {
+  int iters = 50;
+  uint64_t total_mib = 1024;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a == "--iters" && i + 1 < argc) iters = std::atoi(argv[++i]);
+    else if (a == "--mib" && i + 1 < argc) total_mib = std::strtoull(argv[++i], nullptr, 10);
+  }
+  CK(hipSetDevice(0));
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const uint64_t total = total_mib << 20;
+  std::vector<uint8_t> host(total);
+  std::mt19937_64 rng(42);
+  for (uint64_t i = 0; i < total; i += 8) {
+    uint64_t v = rng();
+    std::memcpy(host.data() + i, &v, 8);
+  }
+  uint8_t* d = nullptr;
+  uint32_t *dmeta = nullptr, *dpart = nullptr;
+  CK(hipMalloc(&d, total));
+  CK(hipMalloc(&dmeta, (total / kSliceBytes + 64) * 4));
+  CK(hipMalloc(&dpart, kMaxGridCrc * 4));
+  CK(hipMemcpy(d, host.data(), total, hipMemcpyHostToDevice));
+  DevCrcTables* t = upload_crc_tables(s);
+  if (!t) return 3;
+  std::printf("{\"iters\": %d, \"k1k2\": [", iters);
+  bool first = true;
+  for (uint64_t n : std::vector<uint64_t>{4096, 65536, 1ull << 20, 8ull << 20, 64ull << 20, total}) {
+    if (n > total) continue;
+    for (int mf = 1; mf >= 0; --mf) {
+      set_crc_mfma(mf == 1);
+      Run r = bench_block(d, n, t, dmeta, dpart, s, n >= (256ull << 20) ? std::max(3, iters / 10) : iters, host);
+      std::printf("%s\n  {\"bytes\": %llu, \"impl\": \"%s\", \"us\": %.2f, \"GBps\": %.1f, \"ok\": %s}", first ? "" : ",",
+                  static_cast<unsigned long long>(n), mf ? "mfma" : "lds_tables", r.us, n / r.us / 1e3,
+                  r.ok ? "true" : "false");
+      first = false;
+    }
+  }
+  std::printf("\n], \"scrub\": [");
+  // K1b over total bytes as 1 MiB blocks (meta images from the K1 pass above)
+  const uint64_t bs = 1 << 20, nb = total / bs;
+  std::vector<uint32_t> metas(total / kSliceBytes);
+  crc32_slices(host.data(), total, metas.data());
+  for (auto& v : metas) v = __builtin_bswap32(v);
+  CK(hipMemcpy(dmeta, metas.data(), metas.size() * 4, hipMemcpyHostToDevice));
+  std::vector<ScrubBlock> blocks(nb);
+  for (uint64_t b = 0; b < nb; ++b) {
+    blocks[b].data = d + b * bs;
+    blocks[b].meta = dmeta + b * (bs / kSliceBytes);
+    blocks[b].s_full = bs / kSliceBytes;
+    blocks[b].tile_start = b * (bs / kSliceBytes / kSlicesPerTile);
+    blocks[b].tail_len = 0;
+    blocks[b].tail_init = 0;
+  }
+  ScrubBlock* dblocks = nullptr;
+  uint32_t* dbad = nullptr;
+  CK(hipMalloc(&dblocks, nb * sizeof(ScrubBlock)));
+  CK(hipMalloc(&dbad, nb * 4));
+  CK(hipMemcpy(dblocks, blocks.data(), nb * sizeof(ScrubBlock), hipMemcpyHostToDevice));
+  ScrubLaunch sl{};
+  sl.blocks = dblocks;
+  sl.nblocks = static_cast<uint32_t>(nb);
+  sl.ntiles = nb * (bs / kSliceBytes / kSlicesPerTile);
+  sl.full_init = crc_init_term(kSliceBytes);
+  sl.bad = dbad;
+  first = true;
+  for (int mf = 1; mf >= 0; --mf) {
+    set_crc_mfma(mf == 1);
+    CK(hipMemset(dbad, 0xFF, nb * 4));
+    CK(launch_scrub(sl, t, s));
+    CK(hipStreamSynchronize(s));
+    std::vector<uint32_t> bad(nb);
+    CK(hipMemcpy(bad.data(), dbad, nb * 4, hipMemcpyDeviceToHost));
+    bool ok = true;
+    for (uint32_t v : bad) ok = ok && v == 0xFFFFFFFFu;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    int it = std::max(3, iters / 10);
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < it; ++i) CK(launch_scrub(sl, t, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    double us = 1e3 * ms / it;
+    std::printf("%s\n  {\"bytes\": %llu, \"blocks\": %llu, \"impl\": \"%s\", \"us\": %.1f, \"GBps\": %.1f, \"ok\": %s}",
+                first ? "" : ",", static_cast<unsigned long long>(total), static_cast<unsigned long long>(nb),
+                mf ? "mfma" : "lds_tables", us, total / us / 1e3, ok ? "true" : "false");
+    first = false;
+  }
+  std::printf("\n]}\n");
+  return 0;
+}

@@ -5,11 +5,14 @@
 // an MI355X box (profiles/r1_native/disk_sweep_*.json) the volume peaks at 10-30 concurrent
 // 1 MiB durable writers (8.5-9.2 GB/s buffered) and collapses to 3-4 GB/s with p99 > 100 ms
 // once 60-240 writers pile up — exactly the N=8 replication load. DiskGate caps the number
-// of durable writes in flight per filesystem ACROSS processes: `slots` lock files in
-// /dev/shm keyed by the storage directory's st_dev, each held with flock() for the duration
-// of one block's write+flush. flock locks die with their process, so a crashed chunkserver
-// never leaks a slot. The reference (dfs/chunkserver/src/chunkserver.rs write_block_async)
-// has no equivalent: each spawn_blocking write goes straight to the disk.
+// of durable writes in flight per filesystem ACROSS processes, each slot held for one
+// block's write+flush. Admission is a FIFO ticket semaphore in a /dev/shm page keyed by the
+// storage directory's st_dev (futex wait/wake across processes): writers enter strictly in
+// arrival order, which is what keeps the RF=3 write tail flat under load (r1's per-slot
+// flock queues let late arrivals barge and left unlucky waiters behind long queues). A
+// holder that dies mid-write is detected by pid and its capacity reclaimed. The reference
+// (dfs/chunkserver/src/chunkserver.rs write_block_async) has no equivalent: each
+// spawn_blocking write goes straight to the disk.
 #pragma once
 #include <condition_variable>
 #include <cstdint>
@@ -25,8 +28,8 @@ class DiskGate {
   // `dir` selects the filesystem (its st_dev); slots <= 0 disables the gate.
   DiskGate(const std::string& dir, int slots);
   ~DiskGate();
-  bool enabled() const { return !fds_.empty(); }
-  int slots() const { return static_cast<int>(fds_.size()); }
+  bool enabled() const { return shm_ != nullptr; }
+  int slots() const { return shm_ ? slots_ : 0; }
 
   class Slot {
    public:
@@ -42,24 +45,21 @@ class DiskGate {
     DiskGate* g_ = nullptr;
     int i_ = -1;
   };
-  // Blocks until one of the node's slots is free (immediately when disabled).
+  // Blocks until this writer's turn (FIFO across every process of the node; immediately
+  // when disabled).
   Slot acquire();
   // One non-blocking pass; `*got` says whether a slot was taken.
   Slot try_acquire(bool* got);
   uint64_t waits() const { return waits_; }
 
  private:
-  bool take(int i, bool block, Slot* s);
+  int claim(uint64_t ticket);
   void unlock(int i);
-  std::vector<int> fds_;
-  struct Local {  // one holder per slot inside this process (released from any thread)
-    std::mutex m;
-    std::condition_variable cv;
-    bool busy = false;
-  };
-  std::unique_ptr<Local[]> local_;
-  std::string dir_;
-  uint64_t next_ = 0, waits_ = 0;
+  void reap();
+  bool admitted(uint64_t ticket) const;
+  void* shm_ = nullptr;  // Shared admission state (disk_gate.cpp), one per filesystem and cap
+  int slots_ = 0;
+  uint64_t waits_ = 0;
 };
 
 // DFS_DISK_INFLIGHT (default 12; 0 disables) — the per-filesystem cap used by ChunkStore.

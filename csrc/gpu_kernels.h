@@ -17,6 +17,7 @@ constexpr int kCrcWgThreads = 256;
 constexpr int kSlicesPerTile = 32;  // 4 waves x 8 slices x 512 B = 16 KiB per tile
 constexpr int kMaxGridCrc = 1024;
 constexpr int kMaxShards = 32;
+constexpr int kCrcBasisBytes = 16 * 64 * 16;  // MFMA basis (A fragments), stored after DevCrcTables
 
 struct DevCrcTables {
   uint32_t slice16[16][256];
@@ -75,7 +76,10 @@ struct GfLaunch {
   uint8_t mat[kMaxShards * kMaxShards];  // rows x k, row-major
 };
 
-// Upload tables once per device. Returns device pointer.
+// Upload tables once per device (LDS image followed by the MFMA basis). Returns device pointer.
+// K1/K2/K1b use the matrix-core chunk CRC unless DFS_CRC_MFMA=0 (the LDS slicing-by-16 path).
+bool crc_mfma_enabled();
+void set_crc_mfma(bool on);  // benchmarks / tests: pick the K1 implementation
 DevCrcTables* upload_crc_tables(hipStream_t s);
 int crc_grid_for(uint64_t ntiles, uint32_t has_tail);
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);

@@ -13,6 +13,9 @@
 //    L2) is paid once per workgroup, not per tile.
 #include "gpu_kernels.h"
 
+#include <atomic>
+#include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -82,6 +85,103 @@ __device__ __forceinline__ uint32_t slice_crc(const DevCrcTables& lt, const uint
   return combine(r, 4, lane, lt.sh256);
 }
 
+// ---------------------------------------------------------------------------------------
+// Matrix-core chunk CRC. The raw CRC of a 64-byte chunk is a GF(2)-linear map of its 512
+// bits: R(chunk) = XOR over set bits (byte b, bit p) of V[b][p], V[b][p] = R(e_{b,p}).
+// That is a 32 x 512 binary matrix times the chunk's bit vector — an integer GEMM whose
+// result only needs its parity. One v_mfma_i32_32x32x32_i8 multiplies A (32 CRC bits x 32
+// K-bits of the basis) by B (32 K-bits x 32 chunks); 16 of them cover the 512 bits of 32
+// chunks (2 KiB), two passes the wave's 4 KiB.
+//  * B (data): lane (n = l&31, h = l>>5) loads bytes [32h, 32h+32) of chunk n. K-step s
+//    uses dword s>>1 and bit planes 4(s&1)..4(s&1)+3: fragment dword q is the dword ANDed
+//    with 0x01010101 << p (one VALU op; the planes are not shifted down).
+//  * A (basis, in 64 VGPRs for the whole kernel): element (s, h, j) is 2^(7-p) where bit i
+//    of V[byte][p] is set, so every product of a set data bit is 2^7 (mod 2^8) and bit 7 of
+//    the int32 accumulator is the parity — the GF(2) sum — for any K order, as long as A
+//    and B agree on it (the host builds A in upload_crc_tables with the same mapping).
+//  * D: lane (n, h) holds CRC bits i = (r&3) + 8(r>>2) + 4h of chunk n in register r; the
+//    two half-waves OR their 16 bits together with one shuffle.
+// 64 LDS table lookups per lane per 64 B become 32 MFMAs per 4 KiB per wave.
+using i32x4 = __attribute__((ext_vector_type(4))) int;
+using i32x16 = __attribute__((ext_vector_type(16))) int;
+
+__device__ __forceinline__ void load_basis(const i32x4* __restrict__ basis, int lane, i32x4 (&A)[16]) {
+#pragma unroll
+  for (int s = 0; s < 16; ++s) A[s] = basis[s * 64 + lane];
+}
+
+// The 64 B this lane feeds to the two MFMA passes over the wave's 8 slices starting at slice
+// i0 (two halves of chunk n in pass 0 and pass 1); slices outside [lo, hi) read as zeros.
+struct WaveData {
+  uint4 v[4];
+};
+
+__device__ __forceinline__ WaveData load_wave(const uint8_t* __restrict__ data, int64_t i0, int64_t lo, int64_t hi,
+                                              int lane) {
+  const int n = lane & 31, h = lane >> 5;
+  WaveData d;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = it * 32 + n;
+    const int64_t i = i0 + (c >> 3);
+    d.v[2 * it] = d.v[2 * it + 1] = make_uint4(0, 0, 0, 0);
+    if (i >= lo && i < hi) {
+      // streamed once: non-temporal, so checksum passes do not evict hot lines from L2
+      using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+      const u32x4* p = reinterpret_cast<const u32x4*>(data + static_cast<uint64_t>(i) * 512 + (c & 7) * 64 + h * 32);
+      u32x4 x = __builtin_nontemporal_load(p), y = __builtin_nontemporal_load(p + 1);
+      d.v[2 * it] = make_uint4(x[0], x[1], x[2], x[3]);
+      d.v[2 * it + 1] = make_uint4(y[0], y[1], y[2], y[3]);
+    }
+  }
+  return d;
+}
+
+// Raw CRC of the 64-byte chunk `lane` of the wave's 4 KiB (wave-wide: all 64 lanes together).
+__device__ __forceinline__ uint32_t wave_chunk_crcs(const i32x4 (&A)[16], const WaveData& d, int lane) {
+  const int h = lane >> 5;
+  uint32_t mine = 0;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const uint4 w0 = d.v[2 * it], w1 = d.v[2 * it + 1];
+    const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    i32x16 acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const uint32_t x = w[s >> 1];
+      const uint32_t m = 0x01010101u << (4 * (s & 1));
+      i32x4 b;
+      b.x = static_cast<int>(x & m);
+      b.y = static_cast<int>(x & (m << 1));
+      b.z = static_cast<int>(x & (m << 2));
+      b.w = static_cast<int>(x & (m << 3));
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s], b, acc, 0, 0, 0);
+    }
+    uint32_t part = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) part |= ((static_cast<uint32_t>(acc[r]) >> 7) & 1u) << ((r & 3) + 8 * (r >> 2) + 4 * h);
+    part |= __shfl_xor(part, 32);
+    if (it == h) mine = part;  // lane L keeps chunk L: it comes out of pass L >> 5
+  }
+  return mine;
+}
+
+// Chunk CRCs -> slice CRC (lane sl == 0 of each 8-lane group), as slice_crc does.
+__device__ __forceinline__ uint32_t slice_from_chunks(const DevCrcTables& lt, uint32_t r, int lane) {
+  r = combine(r, 1, lane, lt.sh64);
+  r = combine(r, 2, lane, lt.sh128);
+  return combine(r, 4, lane, lt.sh256);
+}
+
+// LDS image without the slicing-by-16 tables (only the short tail slice still needs them).
+__device__ __forceinline__ void load_shift_tables(const DevCrcTables* __restrict__ gt, DevCrcTables* lt, bool with_slice16) {
+  const uint4* src = reinterpret_cast<const uint4*>(gt);
+  uint4* dst = reinterpret_cast<uint4*>(lt);
+  constexpr int n16 = sizeof(DevCrcTables) / 16;
+  const int from = with_slice16 ? 0 : static_cast<int>(offsetof(DevCrcTables, sh64) / 16);
+  for (int i = from + threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
+}
+
 // Short slice of `len` bytes, front-padded with zeros to 512 B (wave-wide call, lanes 0..7 work).
 __device__ __forceinline__ uint32_t tail_crc(const DevCrcTables& lt, const uint8_t* base, uint32_t len, int lane) {
   const int sw = lane >> 3, sl = lane & 7;
@@ -106,6 +206,7 @@ __device__ __forceinline__ uint32_t tail_crc(const DevCrcTables& lt, const uint8
   return combine(r, 4, lane, lt.sh256);
 }
 
+// LDS slicing-by-16 implementation (DFS_CRC_MFMA=0; the A/B baseline of crc_bench).
 __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
                                                                    const DevCrcTables* __restrict__ gt) {
   __shared__ DevCrcTables lt;
@@ -207,6 +308,142 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_kernel(ScrubLaunch a,
 }
 
 // ---------------------------------------------------------------------------------------
+// K1/K2/K3 on the matrix cores (default). Each workgroup owns a CONTIGUOUS run of 16 KiB
+// tiles; each wave owns one 4 KiB sub-tile per tile and runs its own Horner accumulator for
+// the whole-block CRC (consecutive sub-tiles of a wave are exactly one tile apart, so one
+// lane-parallel GF(2) shift per tile) — no barrier inside the tile loop. The next tile's
+// data is loaded while the current one is on the matrix cores, and the first tile's loads
+// are issued before the LDS table fill, so a 1 MiB block costs one memory round trip.
+__global__ __launch_bounds__(kCrcWgThreads) void crc_tile_mfma_kernel(CrcLaunch a,
+                                                                      const DevCrcTables* __restrict__ gt) {
+  __shared__ DevCrcTables lt;
+  __shared__ uint32_t wacc[4];
+  __shared__ uint32_t wg_bad;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
+  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
+  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  const int64_t lo = static_cast<int64_t>(a.slice_lo), hi = static_cast<int64_t>(a.slice_hi);
+  auto first_slice = [&](uint64_t t) {
+    return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8) - static_cast<int64_t>(a.vfront);
+  };
+  WaveData cur;
+  if (t_begin < t_end) cur = load_wave(a.data, first_slice(t_begin), lo, hi, lane);
+  i32x4 A[16];
+  load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
+  load_shift_tables(gt, &lt, a.has_tail && blockIdx.x == 0);
+  if (threadIdx.x == 0) wg_bad = 0xFFFFFFFFu;
+  __syncthreads();
+
+  uint32_t acc = 0;
+  uint32_t bad = 0xFFFFFFFFu;
+  for (uint64_t t = t_begin; t < t_end; ++t) {
+    WaveData nxt;
+    if (t + 1 < t_end) nxt = load_wave(a.data, first_slice(t + 1), lo, hi, lane);
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, cur, lane), lane);
+    const int64_t i = first_slice(t) + sw;
+    if (i >= lo && i < hi && sl == 0) {
+      uint32_t be = __builtin_bswap32(r ^ a.full_init);
+      if (a.meta_out) a.meta_out[i] = be;
+      if (a.meta_expect && a.meta_expect[i] != be) bad = min(bad, static_cast<uint32_t>(i));
+    }
+    if (a.part_crc) {
+      r = combine(r, 8, lane, lt.sh512);
+      r = combine(r, 16, lane, lt.sh1k);
+      r = combine(r, 32, lane, lt.sh2k);  // wave-uniform: the 4 KiB sub-tile's raw CRC
+      acc = mat_apply(lt.tile_pow2[0], acc, lane) ^ r;
+    }
+    if (t + 1 < t_end) cur = nxt;
+  }
+
+  if (a.has_tail && blockIdx.x == 0 && wave == 0) {
+    uint32_t r = tail_crc(lt, a.data + a.s_full * 512, a.tail_len, lane);
+    if (lane == 0) {
+      uint32_t be = __builtin_bswap32(r ^ a.tail_init);
+      if (a.meta_out) a.meta_out[a.s_full] = be;
+      if (a.meta_expect && a.meta_expect[a.s_full] != be) bad = min(bad, static_cast<uint32_t>(a.s_full));
+    }
+  }
+  if (a.part_crc) {
+    // place this wave's accumulator in the block: (3 - wave) sub-tiles of its last tile
+    // and (ntiles - t_end) whole tiles follow it
+    for (int k = wave; k < 3; ++k) acc = tab4(lt.sh4k, acc);
+    uint64_t e = t_begin < t_end ? a.ntiles - t_end : 0;
+    for (int b = 0; e; ++b, e >>= 1)
+      if (e & 1) acc = mat_apply(lt.tile_pow2[b], acc, lane);
+    if (lane == 0) wacc[wave] = acc;
+  }
+  if (a.part_bad && bad != 0xFFFFFFFFu) atomicMin(&wg_bad, bad);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.part_crc) a.part_crc[blockIdx.x] = wacc[0] ^ wacc[1] ^ wacc[2] ^ wacc[3];
+    if (a.part_bad) a.part_bad[blockIdx.x] = wg_bad;
+  }
+}
+
+// K1b on the matrix cores: contiguous tile runs per workgroup, so the tile -> block lookup is
+// one binary search per workgroup and then a forward walk, and the next tile's data (and its
+// block) are fetched while the current tile computes.
+__global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_mfma_kernel(ScrubLaunch a,
+                                                                       const DevCrcTables* __restrict__ gt) {
+  __shared__ DevCrcTables lt;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
+  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
+  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  uint32_t blk = 0;
+  if (t_begin < t_end) {
+    uint32_t l = 0, h = a.nblocks;
+    while (h - l > 1) {
+      uint32_t mid = (l + h) >> 1;
+      if (a.blocks[mid].tile_start <= t_begin) l = mid;
+      else h = mid;
+    }
+    blk = l;
+  }
+  auto advance = [&](uint64_t t, uint32_t b) {
+    while (b + 1 < a.nblocks && a.blocks[b + 1].tile_start <= t) ++b;
+    return b;
+  };
+  auto first_slice = [&](uint64_t t, uint32_t b) {
+    return static_cast<int64_t>((t - a.blocks[b].tile_start) * kSlicesPerTile + wave * 8);
+  };
+  WaveData cur;
+  if (t_begin < t_end)
+    cur = load_wave(a.blocks[blk].data, first_slice(t_begin, blk), 0, static_cast<int64_t>(a.blocks[blk].s_full), lane);
+  i32x4 A[16];
+  load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
+  load_tables(gt, &lt);  // the tail loop below may need the slicing tables in any workgroup
+  __syncthreads();
+  for (uint64_t t = t_begin; t < t_end; ++t) {
+    WaveData nxt;
+    uint32_t nb = blk;
+    if (t + 1 < t_end) {
+      nb = advance(t + 1, blk);
+      nxt = load_wave(a.blocks[nb].data, first_slice(t + 1, nb), 0, static_cast<int64_t>(a.blocks[nb].s_full), lane);
+    }
+    const ScrubBlock& b = a.blocks[blk];
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, cur, lane), lane);
+    const int64_t i = first_slice(t, blk) + sw;
+    if (sl == 0 && i < static_cast<int64_t>(b.s_full) && b.meta[i] != __builtin_bswap32(r ^ a.full_init))
+      atomicMin(&a.bad[blk], static_cast<uint32_t>(i));
+    if (t + 1 < t_end) {
+      cur = nxt;
+      blk = nb;
+    }
+  }
+  const int waves = kCrcWgThreads / 64;
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * waves + wave; k < a.nblocks;
+       k += static_cast<uint64_t>(gridDim.x) * waves) {
+    const ScrubBlock& b = a.blocks[k];
+    if (!b.tail_len) continue;
+    uint32_t r = tail_crc(lt, b.data + b.s_full * 512, b.tail_len, lane);
+    if (lane == 0 && b.meta[b.s_full] != __builtin_bswap32(r ^ b.tail_init))
+      atomicMin(&a.bad[k], static_cast<uint32_t>(b.s_full));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // GF(2^8) shard matrix multiply: out[r] = XOR_c mat[r][c] * in[c]. Each lane owns 16 B of
 // every shard; logs of the input bytes are looked up once and reused by every output row.
 constexpr int kGfRowBlock = 4;
@@ -258,6 +495,30 @@ __global__ __launch_bounds__(256) void gf256_matmul_kernel(GfLaunch a) {
 
 }  // namespace
 
+// Raw CRC (zero init, no xorout) of a 64-byte message whose only set bit is bit p of byte b.
+static uint32_t chunk_basis_crc(int b, int p) {
+  uint32_t r = 0;
+  for (int i = 0; i < 64; ++i) {
+    r ^= i == b ? (1u << p) : 0u;
+    for (int k = 0; k < 8; ++k) r = (r >> 1) ^ ((r & 1u) ? kCrcPoly : 0u);
+  }
+  return r;
+}
+
+static std::atomic<int> g_crc_mfma{-1};
+
+bool crc_mfma_enabled() {
+  int v = g_crc_mfma.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("DFS_CRC_MFMA");
+    v = (e && e[0] == '0') ? 0 : 1;
+    g_crc_mfma.store(v);
+  }
+  return v == 1;
+}
+
+void set_crc_mfma(bool on) { g_crc_mfma.store(on ? 1 : 0); }
+
 DevCrcTables* upload_crc_tables(hipStream_t s) {
   static_assert(sizeof(DevCrcTables) % 16 == 0, "table image must be uint4-copyable");
   std::vector<uint8_t> host(sizeof(DevCrcTables));
@@ -274,9 +535,23 @@ DevCrcTables* upload_crc_tables(hipStream_t s) {
     const Gf2Mat& m = shift_pow2_bytes(14 + b);  // 16 KiB * 2^b
     std::memcpy(t->tile_pow2[b], m.col, sizeof(m.col));
   }
+  // MFMA basis right behind the LDS image (never copied to LDS): fragment [s][lane] of A,
+  // element j = byte j of the 16 B: CRC bit i = lane & 31 of V[32h + 4(s>>1) + (j&3)][4(s&1) + (j>>2)],
+  // scaled by 2^(7-p) (see wave_chunk_crcs)
+  host.resize(sizeof(DevCrcTables) + kCrcBasisBytes);
+  int8_t* basis = reinterpret_cast<int8_t*>(host.data() + sizeof(DevCrcTables));
+  for (int st = 0; st < 16; ++st)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int j = 0; j < 16; ++j) {
+        const int h = lane >> 5, bit = lane & 31;
+        const int byte = 32 * h + 4 * (st >> 1) + (j & 3), p = 4 * (st & 1) + (j >> 2);
+        const uint32_t v = chunk_basis_crc(byte, p);
+        basis[(st * 64 + lane) * 16 + j] = ((v >> bit) & 1u) ? static_cast<int8_t>(static_cast<uint8_t>(1u << (7 - p))) : 0;
+      }
+  t = reinterpret_cast<DevCrcTables*>(host.data());
   DevCrcTables* d = nullptr;
-  if (hipMalloc(&d, sizeof(DevCrcTables)) != hipSuccess) return nullptr;
-  if (hipMemcpyAsync(d, host.data(), sizeof(DevCrcTables), hipMemcpyHostToDevice, s) != hipSuccess ||
+  if (hipMalloc(&d, host.size()) != hipSuccess) return nullptr;
+  if (hipMemcpyAsync(d, host.data(), host.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
       hipStreamSynchronize(s) != hipSuccess) {
     (void)hipFree(d);
     return nullptr;
@@ -307,7 +582,8 @@ int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
 
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
+  if (crc_mfma_enabled()) hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
+  else hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
   return hipGetLastError();
 }
 
@@ -317,7 +593,10 @@ hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t
   uint64_t tail_waves = (a.nblocks + 3) / 4;
   if (g < tail_waves) g = tail_waves < 2048 ? tail_waves : 2048;
   if (g == 0) g = 1;
-  hipLaunchKernelGGL(crc_scrub_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
+  if (crc_mfma_enabled())
+    hipLaunchKernelGGL(crc_scrub_mfma_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
+  else
+    hipLaunchKernelGGL(crc_scrub_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
   return hipGetLastError();
 }
 

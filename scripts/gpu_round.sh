@@ -97,3 +97,9 @@ if [ "$STEP" = "stress" ]; then
   timeout -k 10 600 python bench.py --steps 1 --warmup 1 --stress-seconds 60 --stress-size 1048576 --stress-concurrency 10 > gpurun_out/bench_stress_1m.json 2> gpurun_out/bench_stress_1m.err || exit $?
 fi
 echo "gpu_round done"
+if [ "$STEP" = "gate3" ]; then
+  # FIFO disk admission: N=4 ranks sharing the GPU and the volume (RF=3, shm fan-out), then N=1
+  timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+    --master-port 29551 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/g3_n4.json 2> gpurun_out/g3_n4.err && \
+  timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/g3_n1.json 2> gpurun_out/g3_n1.err || exit $?
+fi

@@ -71,3 +71,31 @@ def test_disabled_gate_never_blocks(tmp_path):
     assert not g.enabled
     s = g.acquire()
     assert not s.held
+
+
+def test_admission_is_fifo(tmp_path):
+    """Waiters are admitted strictly in arrival order (ticket semaphore): no late arrival
+    barges past a queued writer, which is what bounds the RF=3 write tail under load."""
+    import threading
+
+    g = native.DiskGate(str(tmp_path), 1)
+    hold = [g.acquire()]  # node saturated
+    order, threads = [], []
+
+    def writer(i):
+        s = g.acquire()
+        order.append(i)
+        time.sleep(0.01)
+        s.release()
+
+    for i in range(8):
+        t = threading.Thread(target=writer, args=(i,))
+        t.start()
+        threads.append(t)
+        time.sleep(0.05)  # arrival order = i
+    for s in hold:
+        s.release()
+    for t in threads:
+        t.join(10)
+    assert order == list(range(8))
+    assert g.waits >= 8
