@@ -359,6 +359,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("adopt_term", &FastPathServer::adopt_term)
       .def_property_readonly("term", &FastPathServer::term)
       .def("drain_suspects", &FastPathServer::drain_suspects)
+      .def("recent_request_ids", &FastPathServer::recent_request_ids)
       .def("set_replication", [](FastPathServer& f, ReplicationEngine& e) {
         f.set_replication(&e);
         e.set_control([&f](int rank, const std::string& req, std::string* reply) { return f.control(rank, req, reply); });

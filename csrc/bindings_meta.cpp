@@ -348,7 +348,7 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("writes", &FastClient::writes)
       .def_property_readonly("reads", &FastClient::reads)
       .def("set_routing", &FastClient::set_routing, py::call_guard<py::gil_scoped_release>())
-      .def("write", [](FastClient& c, const std::string& path, py::buffer data) {
+      .def("write", [](FastClient& c, const std::string& path, py::buffer data, const std::string& rid) {
         py::buffer_info bi = data.request();
         int replicas = 0;
         std::string msg;
@@ -357,12 +357,12 @@ void bind_meta(py::module_& m) {
         {
           py::gil_scoped_release r;
           st = c.write(path, static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize),
-                       &replicas, &msg, &t);
+                       &replicas, &msg, &t, rid);
         }
         return py::make_tuple(static_cast<int>(st), replicas, msg,
                               py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete));
-      })
-      .def("read", [](FastClient& c, const std::string& path) {
+      }, py::arg("path"), py::arg("data"), py::arg("request_id") = "")
+      .def("read", [](FastClient& c, const std::string& path, const std::string& rid) {
         int64_t slot = -1;
         uint64_t n = 0;
         std::string msg;
@@ -370,7 +370,7 @@ void bind_meta(py::module_& m) {
         FastClient::Status st;
         {
           py::gil_scoped_release r;
-          st = c.read(path, &slot, &n, &msg, &t);
+          st = c.read(path, &slot, &n, &msg, &t, rid);
         }
         py::object data = py::none();
         if (st == FastClient::Ok) {
@@ -385,5 +385,5 @@ void bind_meta(py::module_& m) {
           }
         }
         return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
-      });
+      }, py::arg("path"), py::arg("request_id") = "");
 }

@@ -21,6 +21,16 @@ namespace dfs {
 
 namespace {
 
+// 128 random bits as 32 hex digits, like the Python client's uuid4().hex
+std::string new_request_id() {
+  thread_local std::mt19937_64 rng{std::random_device{}() ^ (static_cast<uint64_t>(::getpid()) << 32)};
+  char buf[33];
+  std::snprintf(buf, sizeof buf, "%016llx%016llx", static_cast<unsigned long long>(rng()),
+                static_cast<unsigned long long>(rng()));
+  return buf;
+}
+
+
 using Clock = std::chrono::steady_clock;
 
 double since(Clock::time_point& t) {
@@ -245,15 +255,15 @@ void FastClient::give_conn(const std::string& name, int fd) {
   idle_[name].push_back(fd);
 }
 
-bool FastClient::call(const std::string& sock, const std::string& method_path, const std::string& req, int* code,
-                      std::string* resp) {
+bool FastClient::call(const std::string& sock, const std::string& method_path, const std::string& rid,
+                      const std::string& req, int* code, std::string* resp) {
   int fd = take_conn(sock);
   if (fd < 0) return false;
   std::string msg;
-  msg.reserve(8 + method_path.size() + req.size());
-  put<uint32_t>(msg, static_cast<uint32_t>(2 + method_path.size() + 2 + req.size()));
+  msg.reserve(8 + method_path.size() + rid.size() + req.size());
+  put<uint32_t>(msg, static_cast<uint32_t>(2 + method_path.size() + 2 + rid.size() + req.size()));
   put_str(msg, method_path);
-  put<uint16_t>(msg, 0);  // request id: none
+  put_str(msg, rid);  // x-request-id: the master's handlers and logs see the client's id
   msg += req;
   uint32_t n = 0;
   if (!send_all(fd, msg) || !recv_all(fd, &n, 4) || n == 0 || n > (1u << 30)) {
@@ -301,7 +311,9 @@ bool FastClient::fp_call(uint8_t op, const std::string& body, uint8_t* status, u
 }
 
 FastClient::Status FastClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
-                                     std::string* msg, Times* t) {
+                                     std::string* msg, Times* t, const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  RequestScope rs(rid);
   TraceRange tr("dfs.client.write");
   if (!base_ || n > slot_bytes_) return NotHandled;
   std::string sock = master_socket(path);
@@ -332,7 +344,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   creq.preferred_chunk_server = local_cs_;
   int code;
   std::string raw;
-  if (!call(sock, "/dfs.MasterService/CreateFile", creq.str(), &code, &raw)) return NotHandled;
+  if (!call(sock, "/dfs.MasterService/CreateFile", rid, creq.str(), &code, &raw)) return NotHandled;
   if (code == kOutOfRange || code == kFailedPrecondition || code == kUnavailable) return NotHandled;
   if (code != 0) {
     *msg = "Failed to create file: " + raw;
@@ -365,11 +377,10 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   put<uint64_t>(body, n);
   put_str(body, alloc.block.block_id);
   put_str(body, arena_path_);
-  if (alloc.chunk_server_addresses.size() > 1) {
-    put<uint16_t>(body, static_cast<uint16_t>(alloc.chunk_server_addresses.size() - 1));
-    for (size_t i = 1; i < alloc.chunk_server_addresses.size(); ++i)
-      put_str(body, strip_scheme(alloc.chunk_server_addresses[i]));
-  }
+  put<uint16_t>(body, static_cast<uint16_t>(alloc.chunk_server_addresses.size() - 1));
+  for (size_t i = 1; i < alloc.chunk_server_addresses.size(); ++i)
+    put_str(body, strip_scheme(alloc.chunk_server_addresses[i]));
+  put_str(body, rid);
   uint8_t st;
   uint64_t total, written;
   std::string fmsg;
@@ -399,7 +410,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   done.ec_data_shards = alloc.ec_data_shards;
   done.ec_parity_shards = alloc.ec_parity_shards;
   done.blocks.push_back(alloc.block);
-  if (!call(sock, "/dfs.MasterService/CompleteFile", done.str(), &code, &raw)) {
+  if (!call(sock, "/dfs.MasterService/CompleteFile", rid, done.str(), &code, &raw)) {
     *msg = "Failed to complete file: master connection lost";
     return Failed;
   }
@@ -419,7 +430,9 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
 }
 
 FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg,
-                                    Times* t) {
+                                    Times* t, const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  RequestScope rs(rid);
   TraceRange tr("dfs.client.read");
   if (!base_) return NotHandled;
   std::string sock = master_socket(path);
@@ -429,7 +442,7 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
   req.path = path;
   int code;
   std::string raw;
-  if (!call(sock, "/dfs.MasterService/GetFileInfo", req.str(), &code, &raw)) return NotHandled;
+  if (!call(sock, "/dfs.MasterService/GetFileInfo", rid, req.str(), &code, &raw)) return NotHandled;
   if (code != 0) return code == kNotFound ? (*msg = raw, Failed) : NotHandled;
   pb::GetFileInfoResponse info;
   if (!info.decode(raw)) return NotHandled;
@@ -458,6 +471,7 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
   put<uint64_t>(body, slot_bytes_);
   put_str(body, b.block_id);
   put_str(body, arena_path_);
+  put_str(body, rid);
   uint8_t st;
   uint64_t total, got;
   std::string fmsg;

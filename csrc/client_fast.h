@@ -44,10 +44,13 @@ class FastClient {
   // Routing: shard map (serde JSON, "" = none) and the fallback master list.
   void set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters);
 
-  Status write(const std::string& path, const uint8_t* data, size_t n, int* replicas, std::string* msg, Times* t);
+  // `rid`: the request id carried on every hop (minted here when empty).
+  Status write(const std::string& path, const uint8_t* data, size_t n, int* replicas, std::string* msg, Times* t,
+               const std::string& rid = "");
   // On Ok the block sits in slot `*slot` (`*n` bytes); the caller copies it out and calls
   // release(*slot).
-  Status read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg, Times* t);
+  Status read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg, Times* t,
+              const std::string& rid = "");
   const uint8_t* slot_ptr(int64_t slot) const { return base_ + slot; }
   void release(int64_t slot);
 
@@ -58,7 +61,8 @@ class FastClient {
   int64_t acquire(size_t n);
   std::string master_socket(const std::string& path);
   // one request/response on a pooled connection; false on a transport error
-  bool call(const std::string& sock, const std::string& method_path, const std::string& req, int* code,
+  bool call(const std::string& sock, const std::string& method_path, const std::string& rid, const std::string& req,
+            int* code,
             std::string* resp);
   bool fp_call(uint8_t op, const std::string& body, uint8_t* status, uint64_t* total, uint64_t* nbytes,
                std::string* msg);

@@ -1,5 +1,6 @@
 // Native local data path of a ChunkServer; see fastpath.h for protocol and scope.
 #include "fastpath.h"
+#include "trace.h"
 
 #include <fcntl.h>
 #include <poll.h>
@@ -213,6 +214,25 @@ std::vector<std::string> FastPathServer::drain_suspects() {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<std::string> out;
   out.swap(suspects_);
+  return out;
+}
+
+namespace {
+constexpr size_t kRecentRids = 64;
+}
+
+void FastPathServer::note_rid(const std::string& rid) {
+  if (rid.empty()) return;
+  std::lock_guard<std::mutex> g(mu_);
+  if (recent_rids_.size() < kRecentRids) recent_rids_.push_back(rid);
+  else recent_rids_[recent_pos_++ % kRecentRids] = rid;
+}
+
+std::vector<std::string> FastPathServer::recent_request_ids() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (recent_rids_.size() < kRecentRids) return recent_rids_;
+  std::vector<std::string> out;
+  for (size_t i = 0; i < kRecentRids; ++i) out.push_back(recent_rids_[(recent_pos_ + i) % kRecentRids]);
   return out;
 }
 
@@ -451,6 +471,7 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
       put<uint64_t>(req, t.slice);
       put_str(req, id);
       put<uint16_t>(req, 0);  // fan-out: the replica forwards nowhere
+      put_str(req, t_request_id);
       finish_frame(req);
       bool io_ok;
       int drop = drop_descriptors_.load();
@@ -485,6 +506,7 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
   put_str(req, id);
   put_str(req, src.path);
   put<uint16_t>(req, 0);
+  put_str(req, t_request_id);
   finish_frame(req);
   if (exchange_with(p, req, &resp) && static_cast<FpStatus>(resp[0]) == FpStatus::Ok) {
     if (tried_p2p) {
@@ -504,8 +526,12 @@ void FastPathServer::replicate(const std::string& id, uint32_t crc, uint64_t ter
   if (next.empty()) return;
   // every replica at once: each has its own xGMI link from this GPU
   std::vector<std::future<int>> futs;
+  const std::string rid = t_request_id;
   for (size_t i = 1; i < next.size(); ++i)
-    futs.push_back(std::async(std::launch::async, [&, i] { return replicate_one(next[i], id, crc, term, src, host, n); }));
+    futs.push_back(std::async(std::launch::async, [&, i] {
+      RequestScope rs(rid);
+      return replicate_one(next[i], id, crc, term, src, host, n);
+    }));
   int total = replicate_one(next[0], id, crc, term, src, host, n);
   for (auto& f : futs) total += f.get();
   *replicas = total;
@@ -529,7 +555,11 @@ void FastPathServer::serve(int fd) {
                                  uint64_t term, const std::vector<std::string>& next, const ShmSrc& src) -> bool {
     int down = 0;
     std::string perr;
-    auto fut = std::async(std::launch::async, [&] { replicate(id, crc, term, next, src, host, len, &down); });
+    const std::string rid = t_request_id;
+    auto fut = std::async(std::launch::async, [&] {
+      RequestScope rs(rid);
+      replicate(id, crc, term, next, src, host, len, &down);
+    });
     bool pok = store_->persist(id, host, host ? len : 0, &perr);
     fut.get();
     if (!pok) return send_response(fd, FpStatus::IoError, 0, 0, perr);
@@ -555,6 +585,10 @@ void FastPathServer::serve(int fd) {
       uint64_t off = rd.get<uint64_t>(), len = rd.get<uint64_t>();
       std::string id = rd.str(), path = rd.str();
       std::vector<std::string> next = read_list(rd, true);
+      std::string rid = rd.p < rd.end ? rd.str() : std::string();  // request id (after the list)
+      RequestScope rs(rid);
+      note_rid(rid);
+      TraceRange tr("dfs.fp.write");
       std::string err;
       uint8_t* base = nullptr;
       if (!rd.ok || id.empty()) {
@@ -588,6 +622,9 @@ void FastPathServer::serve(int fd) {
       uint64_t slice = rd.get<uint64_t>();
       std::string id = rd.str();
       std::vector<std::string> next = read_list(rd, false);
+      std::string rid = rd.p < rd.end ? rd.str() : std::string();
+      RequestScope rs(rid);
+      note_rid(rid);
       if (!rd.ok || id.empty() || repl_ == nullptr || size > kMaxTransfer) {
         if (repl_ && rd.ok && src >= 0) repl_->fail_pair(src, "malformed descriptor");
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, repl_ ? "malformed replicate request" : "replication disabled");
@@ -614,6 +651,10 @@ void FastPathServer::serve(int fd) {
       uint64_t off = rd.get<uint64_t>(), len = rd.get<uint64_t>();
       std::string id = rd.str(), path = rd.str();
       std::vector<std::string> next = read_list(rd, false);
+      std::string rid = rd.p < rd.end ? rd.str() : std::string();
+      RequestScope rs(rid);
+      note_rid(rid);
+      TraceRange tr("dfs.fp.replicate_shm");
       std::string err;
       uint8_t* base = nullptr;
       if (!rd.ok || id.empty()) {
@@ -643,6 +684,10 @@ void FastPathServer::serve(int fd) {
       uint64_t offset = rd.get<uint64_t>(), length = rd.get<uint64_t>();
       uint64_t shm_off = rd.get<uint64_t>(), cap = rd.get<uint64_t>();
       std::string id = rd.str(), path = rd.str();
+      std::string rid = rd.p < rd.end ? rd.str() : std::string();
+      RequestScope rs(rid);
+      note_rid(rid);
+      TraceRange tr("dfs.fp.read");
       if (!rd.ok || id.empty()) {
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed read request");
       } else {

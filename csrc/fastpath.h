@@ -87,6 +87,9 @@ class FastPathServer {
   uint64_t term() const { return term_.load(); }
 
   std::vector<std::string> drain_suspects();  // blocks needing background recovery
+  // The request ids of the last few data-path ops served here (newest last): lets tests and
+  // operators follow one client request across the head and every replica.
+  std::vector<std::string> recent_request_ids();
   FpStats stats();
 
   // Native replication: this server's engine (RCCL or socket transport) and the fast-path
@@ -141,6 +144,9 @@ class FastPathServer {
   std::unordered_map<std::string, Mapping> maps_;
   std::vector<Mapping> retired_;
   std::vector<std::string> suspects_;
+  std::vector<std::string> recent_rids_;  // ring of the last kRecentRids request ids (mu_)
+  size_t recent_pos_ = 0;
+  void note_rid(const std::string& rid);
   FpStats st_;
   ReplicationEngine* repl_ = nullptr;
   std::atomic<int> drop_descriptors_{0};

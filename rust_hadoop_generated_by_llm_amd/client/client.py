@@ -28,7 +28,7 @@ from ..models import proto as pb
 from ..ops import crc as crcops
 from ..ops import erasure
 from ..parallel.sharding import ShardMap
-from ..utils.rpc import ChannelPool, rpc_code, rpc_details, strip_scheme, with_scheme
+from ..utils.rpc import ChannelPool, current_request_id, rpc_code, rpc_details, strip_scheme, with_scheme
 from ..native import lib as _native
 from ..utils import fastpath as fpmod
 from ..utils.shm import ShmArena
@@ -370,7 +370,7 @@ class Client:
         replicas_written (reference mod.rs:225-494)."""
         fc = self._fast
         if fc is not None:
-            st, replicas, msg, times = fc.write(dest, data)
+            st, replicas, msg, times = fc.write(dest, data, current_request_id.get())
             if st == 0:
                 self.fp_ops += 1
                 if self.phase_times is not None:
@@ -577,7 +577,7 @@ class Client:
     def get_file_content(self, path: str) -> bytes:
         fc = self._fast
         if fc is not None:
-            st, data, msg, times = fc.read(path)
+            st, data, msg, times = fc.read(path, current_request_id.get())
             if st == 0:
                 self.fp_ops += 1
                 if self.phase_times is not None:

@@ -10,6 +10,7 @@ from __future__ import annotations
 import socket
 import struct
 import threading
+import uuid
 
 OK, NOT_FOUND, OUT_OF_RANGE, CORRUPT, IO_ERROR, FENCED, UNSUPPORTED, BAD_REQUEST, PARTIAL_CORRUPT = range(9)
 
@@ -80,18 +81,27 @@ class FastPathClient:
         return st, total, nbytes, msg
 
     def write(self, block_id: str, shm_path: str, shm_off: int, length: int, crc: int, term: int,
-              next_servers: list[str] | tuple = ()):
+              next_servers: list[str] | tuple = (), request_id: str | None = None):
         """Returns (status, replicas_written, message). With ``next_servers`` the server
-        forwards the block along the chain natively (RCCL) or answers UNSUPPORTED."""
+        fans the block out to those replicas natively (P2P / shm) or answers UNSUPPORTED.
+        The request id travels to every replica (defaults to the current one)."""
         body = _WRITE.pack(term, crc & 0xFFFFFFFF, shm_off, length) + _s(block_id.encode()) + _s(shm_path.encode())
-        if next_servers:
-            body += struct.pack("<H", len(next_servers)) + b"".join(_s(a.encode()) for a in next_servers)
+        body += struct.pack("<H", len(next_servers)) + b"".join(_s(a.encode()) for a in next_servers)
+        body += _s(self._rid(request_id))
         st, _total, replicas, msg = self._call(1, body)
         return st, replicas, msg
 
-    def read(self, block_id: str, offset: int, length: int, shm_path: str, shm_off: int, cap: int):
+    def read(self, block_id: str, offset: int, length: int, shm_path: str, shm_off: int, cap: int,
+             request_id: str | None = None):
         body = _READ.pack(offset, length, shm_off, cap) + _s(block_id.encode()) + _s(shm_path.encode())
+        body += _s(self._rid(request_id))
         return self._call(2, body)  # (status, total, bytes, msg)
+
+    @staticmethod
+    def _rid(request_id: str | None) -> bytes:
+        from .rpc import current_request_id
+
+        return (request_id or current_request_id.get() or uuid.uuid4().hex).encode()
 
     def close(self) -> None:
         self._drop()

@@ -255,6 +255,31 @@ def test_killed_peer_counts_fewer_replicas_then_rejoins(cluster):
     arena.close()
 
 
+def test_request_id_reaches_every_replica(cluster):
+    """x-request-id (reference dfs/common/src/lib.rs:8-50; replication propagates it,
+    chunkserver.rs:787,1045): the client's id is carried to the head and to each replica,
+    over the P2P path and over the shared-memory fallback alike."""
+    head, a, b, c = cluster
+    arena = ShmArena(size=4 << 20, slot=2 << 20)
+    data = os.urandom(300_000)
+    slot = put(arena, data)
+    cli = fp.FastPathClient(head.fp.name, timeout=30)
+    st, replicas, msg = cli.write("rid-blk", arena.path, slot, len(data), zlib.crc32(data), 1,
+                                  next_servers=[a.addr, b.addr], request_id="rid-p2p-42")
+    assert st == fp.OK and replicas == 3, msg
+    head.fp.debug_drop_descriptors(1)  # this one's replica goes over shared memory
+    st, replicas, msg = cli.write("rid-blk2", arena.path, slot, len(data), zlib.crc32(data), 1,
+                                  next_servers=[c.addr], request_id="rid-shm-43")
+    assert st == fp.OK and replicas == 2, msg
+    st, *_ = cli.read("rid-blk", 0, 0, arena.path, slot, arena.slot, request_id="rid-read-44")
+    assert st == fp.OK
+    cli.close()
+    assert {"rid-p2p-42", "rid-shm-43", "rid-read-44"} <= set(head.fp.recent_request_ids())
+    assert "rid-p2p-42" in a.fp.recent_request_ids() and "rid-p2p-42" in b.fp.recent_request_ids()
+    assert "rid-shm-43" in c.fp.recent_request_ids()
+    arena.close()
+
+
 def test_slice_sizes_are_checksum_aligned(native, tmp_path):
     store = native.ChunkStore(str(tmp_path / "s"), "", -1, 0, 0, 100, 2, 1, False)
     eng = native.ReplicationEngine(store, "socket", 0, 2, ns="slices")
