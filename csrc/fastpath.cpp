@@ -676,6 +676,39 @@ void FastPathServer::serve(int fd) {
           sent = persist_and_forward(id, base + off, len, crc, term, next, ShmSrc{path, off, len});
         }
       }
+    } else if (op == 6) {  // EC: GF(2^8) matrix x shards on this server's GPU, in the client's slot
+      uint16_t k = rd.get<uint16_t>(), rows = rd.get<uint16_t>();
+      uint64_t len = rd.get<uint64_t>(), in_off = rd.get<uint64_t>(), out_off = rd.get<uint64_t>();
+      std::string mat = rd.str(), path = rd.str();
+      std::string rid = rd.p < rd.end ? rd.str() : std::string();
+      RequestScope rs(rid);
+      note_rid(rid);
+      TraceRange tr("dfs.fp.ec");
+      const uint64_t stride = (len + 15) / 16 * 16;
+      std::string err;
+      uint8_t* base = nullptr;
+      if (!rd.ok || k == 0 || rows == 0 || k > kMaxShards || rows > kMaxShards || mat.size() != size_t(k) * rows ||
+          len > kMaxTransfer) {
+        sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed ec request");
+      } else if (!store_->gpu()) {
+        sent = send_response(fd, FpStatus::Unsupported, 0, 0, "no GPU on this chunkserver");
+      } else if ((base = map_shm(path, std::min(in_off, out_off),
+                                 std::max(in_off + stride * k, out_off + stride * rows) - std::min(in_off, out_off),
+                                 &err)) == nullptr) {
+        sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
+      } else {
+        std::vector<std::vector<uint8_t>> M(rows, std::vector<uint8_t>(k));
+        for (int r = 0; r < rows; ++r)
+          for (int c = 0; c < k; ++c) M[r][c] = static_cast<uint8_t>(mat[r * k + c]);
+        std::vector<const uint8_t*> in(k);
+        std::vector<uint8_t*> out(rows);
+        for (int c = 0; c < k; ++c) in[c] = base + in_off + c * stride;
+        for (int r = 0; r < rows; ++r) out[r] = base + out_off + r * stride;
+        bool ok = store_->gf_matmul_gpu(M, in, out, len);
+        if (ok) bump(&FpStats::ec_ops);
+        sent = ok ? send_response(fd, FpStatus::Ok, len, rows, "")
+                  : send_response(fd, FpStatus::Unsupported, 0, 0, "GPU erasure coding failed");
+      }
     } else if (op == 5) {  // CTRL: replication pair bring-up / rebuild
       std::string blob = rd.str();
       if (!rd.ok || repl_ == nullptr) sent = send_response(fd, FpStatus::Unsupported, 0, 0, "replication disabled");

@@ -23,6 +23,9 @@
 //     op 4 REPL_SHM: u64 term | u32 crc | u64 shm_off | u64 len | u16 id_len id | u16 path_len path
 //               | u16 n_next | (u16 len addr)*      -- same-host hop without a P2P pair: read the client slot
 //     op 5 CTRL : u16 len blob                       -- replication control (pair bring-up / rebuild)
+//     op 6 EC   : u16 k | u16 rows | u64 len | u64 in_off | u64 out_off | u16 rows*k matrix | u16 path
+//               [| u16 rid]  -- GF(2^8) matrix x shards (RS encode / reconstruct) on this GPU;
+//               shards sit in the client's slot at 16-byte-aligned strides, outputs land there
 //   response = u32 body_len | u8 status | u64 total | u64 bytes | u16 msg_len msg
 //   (for WRITE/REPL ``bytes`` carries replicas_written; for CTRL ``msg`` is the engine reply)
 //
@@ -67,6 +70,7 @@ struct FpStats {
   uint64_t rejected_peers = 0;  // connections from another uid (SO_PEERCRED)
   uint64_t replica_failures = 0;  // replicas that could not be written (not counted)
   uint64_t p2p_fallbacks = 0;     // replicas moved to shared memory after a P2P failure
+  uint64_t ec_ops = 0;            // erasure-coding matrix products run for clients
 };
 
 class FastPathServer {

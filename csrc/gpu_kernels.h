@@ -72,9 +72,11 @@ struct GfLaunch {
   uint64_t len;   // bytes per shard (buffers padded to 16 B)
   int k;          // inputs
   int rows;       // outputs
-  const uint8_t* gf_tables;  // device: log[256] then exp[512] (poly 0x11D, generator 2)
-  uint8_t mat[kMaxShards * kMaxShards];  // rows x k, row-major
+  const uint32_t* tables;  // device: [rows][k] x 8 dwords, split-nibble product tables (gf_nibble_tables)
 };
+// Host: split-nibble tables of a rows x k coefficient matrix (poly 0x11D): per (r, c) the
+// 16 products of the low nibble, then the 16 of the high nibble, 32 bytes.
+void gf_nibble_tables(const uint8_t* mat, int rows, int k, uint32_t* out);
 
 // Upload tables once per device (LDS image followed by the MFMA basis). Returns device pointer.
 // K1/K2/K1b use the matrix-core chunk CRC unless DFS_CRC_MFMA=0 (the LDS slicing-by-16 path).
@@ -85,6 +87,5 @@ int crc_grid_for(uint64_t ntiles, uint32_t has_tail);
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
 hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s);
 hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s);
-const uint8_t* upload_gf_tables(hipStream_t s);
 
 }  // namespace dfs

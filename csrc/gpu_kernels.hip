@@ -444,44 +444,53 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_mfma_kernel(ScrubLaun
 }
 
 // ---------------------------------------------------------------------------------------
-// GF(2^8) shard matrix multiply: out[r] = XOR_c mat[r][c] * in[c]. Each lane owns 16 B of
-// every shard; logs of the input bytes are looked up once and reused by every output row.
+// GF(2^8) shard matrix multiply (K4 encode / K5 reconstruct): out[r] = XOR_c mat[r][c] * in[c].
+// Branch-free split-nibble form (ISA-L style): c * x = T_lo[x & 15] ^ T_hi[x >> 4], with the
+// two 16-byte tables per coefficient looked up four bytes at a time by v_perm_b32 (a byte
+// shuffle over an 8-byte table pair; bit 3 of the nibble picks the half through v_bfi_b32).
+// Per input dword the nibble selectors are prepared once and reused for every output row;
+// the tables of one (row, input) pair are wave-uniform and sit in scalar registers. No LDS,
+// no data-dependent branches: ~8 VALU ops per input byte for RS(6,3), far under the VALU
+// rate needed to keep up with HBM.
+struct NibbleSel {
+  uint32_t lo7, lo_m, hi7, hi_m;
+};
+
+__device__ __forceinline__ NibbleSel nibble_sel(uint32_t x) {
+  NibbleSel n;
+  n.lo7 = x & 0x07070707u;
+  n.hi7 = (x >> 4) & 0x07070707u;
+  // bit 3 of each nibble -> 0x00 / 0xFF per byte (perm selector 12 = 0x00, 13 = 0xFF)
+  n.lo_m = __builtin_amdgcn_perm(0u, 0u, ((x >> 3) & 0x01010101u) | 0x0C0C0C0Cu);
+  n.hi_m = __builtin_amdgcn_perm(0u, 0u, ((x >> 7) & 0x01010101u) | 0x0C0C0C0Cu);
+  return n;
+}
+
+// t[0..3]: low-nibble table bytes 0..15, t[4..7]: high-nibble table.
+__device__ __forceinline__ uint32_t gf_mul4(const uint32_t* __restrict__ t, const NibbleSel& n) {
+  uint32_t a = __builtin_amdgcn_perm(t[1], t[0], n.lo7), b = __builtin_amdgcn_perm(t[3], t[2], n.lo7);
+  uint32_t c = __builtin_amdgcn_perm(t[5], t[4], n.hi7), d = __builtin_amdgcn_perm(t[7], t[6], n.hi7);
+  return ((a & ~n.lo_m) | (b & n.lo_m)) ^ ((c & ~n.hi_m) | (d & n.hi_m));
+}
+
 constexpr int kGfRowBlock = 4;
 
 __global__ __launch_bounds__(256) void gf256_matmul_kernel(GfLaunch a) {
-  __shared__ uint8_t s_log[256];
-  __shared__ uint8_t s_exp[512];
-  __shared__ uint8_t s_clog[kMaxShards * kMaxShards];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) s_log[i] = a.gf_tables[i];
-  for (int i = threadIdx.x; i < 512; i += blockDim.x) s_exp[i] = a.gf_tables[256 + i];
-  __syncthreads();
-  for (int i = threadIdx.x; i < a.rows * a.k; i += blockDim.x) s_clog[i] = s_log[a.mat[i]];
-  __syncthreads();
-
   const uint64_t nvec = (a.len + 15) / 16;
   for (uint64_t vi = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; vi < nvec;
        vi += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     for (int r0 = 0; r0 < a.rows; r0 += kGfRowBlock) {
       uint32_t acc[kGfRowBlock][4] = {};
       for (int c = 0; c < a.k; ++c) {
-        uint4 w = reinterpret_cast<const uint4*>(a.in[c])[vi];
-        uint32_t words[4] = {w.x, w.y, w.z, w.w};
+        const uint4 w = reinterpret_cast<const uint4*>(a.in[c])[vi];
+        const NibbleSel ns[4] = {nibble_sel(w.x), nibble_sel(w.y), nibble_sel(w.z), nibble_sel(w.w)};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int rr = 0; rr < kGfRowBlock; ++rr) {
+          const int r = r0 + rr;
+          if (r >= a.rows) break;
+          const uint32_t* t = a.tables + (r * a.k + c) * 8;  // uniform: scalar loads
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            uint32_t byte = (words[q] >> (8 * b)) & 0xff;
-            if (!byte) continue;
-            uint32_t lb = s_log[byte];
-#pragma unroll
-            for (int rr = 0; rr < kGfRowBlock; ++rr) {
-              int r = r0 + rr;
-              if (r >= a.rows) break;
-              uint8_t coef = a.mat[r * a.k + c];
-              if (!coef) continue;
-              acc[rr][q] ^= static_cast<uint32_t>(s_exp[lb + s_clog[r * a.k + c]]) << (8 * b);
-            }
-          }
+          for (int q = 0; q < 4; ++q) acc[rr][q] ^= gf_mul4(t, ns[q]);
         }
       }
       for (int rr = 0; rr < kGfRowBlock; ++rr) {
@@ -559,20 +568,6 @@ DevCrcTables* upload_crc_tables(hipStream_t s) {
   return d;
 }
 
-const uint8_t* upload_gf_tables(hipStream_t s) {
-  const auto& t = gf::tables();
-  std::vector<uint8_t> host(768);
-  std::memcpy(host.data(), t.log, 256);
-  std::memcpy(host.data() + 256, t.exp, 512);
-  uint8_t* d = nullptr;
-  if (hipMalloc(&d, host.size()) != hipSuccess) return nullptr;
-  if (hipMemcpyAsync(d, host.data(), host.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess) {
-    (void)hipFree(d);
-    return nullptr;
-  }
-  return d;
-}
 
 int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
   uint64_t g = ntiles < static_cast<uint64_t>(kMaxGridCrc) ? ntiles : kMaxGridCrc;
@@ -598,6 +593,21 @@ hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t
   else
     hipLaunchKernelGGL(crc_scrub_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
   return hipGetLastError();
+}
+
+void gf_nibble_tables(const uint8_t* mat, int rows, int k, uint32_t* out) {
+  for (int r = 0; r < rows; ++r)
+    for (int c = 0; c < k; ++c) {
+      uint8_t coef = mat[r * k + c];
+      uint8_t lo[16], hi[16];
+      for (int v = 0; v < 16; ++v) {
+        lo[v] = gf::mul(coef, static_cast<uint8_t>(v));
+        hi[v] = gf::mul(coef, static_cast<uint8_t>(v << 4));
+      }
+      uint32_t* t = out + (r * k + c) * 8;
+      std::memcpy(t, lo, 16);
+      std::memcpy(t + 4, hi, 16);
+    }
 }
 
 hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s) {

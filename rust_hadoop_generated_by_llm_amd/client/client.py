@@ -68,6 +68,7 @@ class Client:
         self.hedge_delay_ms = hedge_delay_ms
         self.local_chunkserver = strip_scheme(local_chunkserver) if local_chunkserver else None
         self.ec_store = ec_store
+        self.ec_on_gpu = os.environ.get("DFS_CLIENT_GPU_EC", "1") == "1"
         self.rpc_timeout = rpc_timeout
         self.data_timeout = data_timeout
         self.pool = ChannelPool(ca_cert, domain_name)
@@ -107,6 +108,18 @@ class Client:
         return t1
 
     # ------------------------------------------------------------------ short-circuit I/O
+    def _ec_provider(self):
+        """Where RS encode/decode runs: an explicit store, else the co-located chunkserver's
+        GPU through the fast path (shards staged in our shm slot), else the CPU codec."""
+        if self.ec_store is not None:
+            return self.ec_store
+        if self.fastpath is not None and self.ec_on_gpu:
+            prov = getattr(self, "_fp_ec", None)
+            if prov is None or prov.client is not self.fastpath:
+                prov = self._fp_ec = fpmod.FastPathEc(self.fastpath, self._shm)
+            return prov if prov.gpu else None
+        return None
+
     def _shm(self) -> ShmArena | None:
         if not self.short_circuit:
             return None
@@ -457,7 +470,7 @@ class Client:
             raise DfsError(f"Master returned non-EC policy (data={k}, parity={m}) for EC file")
         if len(servers) != k + m:
             raise DfsError(f"Expected {k + m} chunk servers for EC({k},{m}), got {len(servers)}")
-        shards = erasure.encode(data, k, m, self.ec_store)
+        shards = erasure.encode(data, k, m, self._ec_provider())
         bid = alloc.block.block_id
 
         def put(i):
@@ -567,7 +580,7 @@ class Client:
         orig = block.original_size or block.size
         if all(s is not None for s in shards[:k]):
             return b"".join(shards[:k])[:orig]  # fast path: data shards intact
-        return erasure.decode(shards, k, m, orig, self.ec_store)
+        return erasure.decode(shards, k, m, orig, self._ec_provider())
 
     def fetch_single_block(self, block) -> bytes:
         if block.ec_data_shards > 0:

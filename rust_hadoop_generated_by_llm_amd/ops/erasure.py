@@ -8,11 +8,27 @@ CDNA4 kernel ``gf256_matmul_kernel`` (K4/K5); otherwise the native CPU table cod
 """
 from __future__ import annotations
 
+import logging
+import threading
+
 from ..native import lib
+
+log = logging.getLogger("dfs.erasure")
 
 
 class ErasureError(ValueError):
     pass
+
+
+# Matrix products that were meant for a GPU but ran on the host CPU instead (no slot, no GPU
+# on the server, a failed launch): counted and logged, never silent.
+STATS = {"gpu": 0, "cpu": 0, "cpu_fallbacks": 0}
+_stats_lock = threading.Lock()
+
+
+def _count(key: str) -> None:
+    with _stats_lock:
+        STATS[key] += 1
 
 
 def shard_len(data_len: int, data_shards: int) -> int:
@@ -25,7 +41,13 @@ def _matmul(matrix, inputs, length, store=None):
     if store is not None and getattr(store, "gpu", False):
         out = store.gf_matmul(matrix, inputs, length)
         if out is not None:
+            _count("gpu")
             return out
+        _count("cpu_fallbacks")
+        log.warning("GPU erasure coding unavailable for a %dx%d x %d B product; using the CPU codec",
+                    len(matrix), len(inputs), length)
+    else:
+        _count("cpu")
     return lib.gf_matmul_cpu(matrix, inputs, length)
 
 

@@ -97,6 +97,19 @@ class FastPathClient:
         body += _s(self._rid(request_id))
         return self._call(2, body)  # (status, total, bytes, msg)
 
+    def ec_matmul(self, matrix, k: int, length: int, shm_path: str, in_off: int, out_off: int,
+                  request_id: str | None = None):
+        """GF(2^8) ``matrix`` (rows x k) times the k shards at ``in_off`` of the client's
+        arena (each ``length`` bytes at a 16-byte-aligned stride); the rows land at ``out_off``.
+        Runs on the chunkserver's GPU (csrc/fastpath.cpp op 6). Returns the status."""
+        rows = len(matrix)
+        mat = bytes(v for row in matrix for v in row)
+        body = struct.pack("<HHQQQ", k, rows, length, in_off, out_off) + _s(mat) + _s(shm_path.encode())
+        body += _s(self._rid(request_id))
+        st, _total, _n, msg = self._call(6, body)
+        self.last_ec_message = msg
+        return st
+
     @staticmethod
     def _rid(request_id: str | None) -> bytes:
         from .rpc import current_request_id
@@ -105,3 +118,44 @@ class FastPathClient:
 
     def close(self) -> None:
         self._drop()
+
+
+class FastPathEc:
+    """Erasure-coding provider for ``ops/erasure.py`` backed by the co-located chunkserver's
+    GPU: shards are staged in the client's shared-memory slot (registered for direct DMA on
+    the server side) and the RS matrix product runs there. ``gf_matmul`` returns None when
+    the job does not fit a slot or the server cannot run it (the caller then counts a CPU
+    fallback)."""
+
+    def __init__(self, client: FastPathClient, arena_fn):
+        self.client = client
+        self.arena_fn = arena_fn  # () -> ShmArena | None
+        self.gpu = True  # False once the server said it has no GPU (host-store chunkserver)
+
+    def gf_matmul(self, matrix, inputs, length: int):
+        arena = self.arena_fn()
+        if arena is None or not matrix:
+            return None
+        k, rows = len(inputs), len(matrix)
+        stride = -(-max(length, 1) // 16) * 16
+        need = stride * (k + rows)
+        slot = arena.acquire(need)
+        if slot is None:
+            return None
+        try:
+            view = arena.view
+            for c, shard in enumerate(inputs):
+                off = slot + c * stride
+                view[off:off + length] = shard
+            try:
+                st = self.client.ec_matmul(matrix, k, length, arena.path, slot, slot + k * stride)
+            except FastPathError:
+                return None
+            if st == UNSUPPORTED and "no GPU" in getattr(self.client, "last_ec_message", ""):
+                self.gpu = False
+            if st != OK:
+                return None
+            base = slot + k * stride
+            return [bytes(view[base + r * stride:base + r * stride + length]) for r in range(rows)]
+        finally:
+            arena.release(slot)

@@ -83,3 +83,21 @@ def test_shard_len_and_errors():
         E.encode(b"", 2, 2)
     with pytest.raises(E.ErasureError):
         E.encode(b"x", 0, 2)
+
+
+def test_gpu_provider_fallback_is_counted():
+    """a GPU erasure-coding provider that cannot run a product must not fall
+    back silently — the CPU result is still exact, and the fallback is counted."""
+    from rust_hadoop_generated_by_llm_amd.ops import erasure
+
+    class Refusing:
+        gpu = True
+
+        def gf_matmul(self, matrix, inputs, length):
+            return None
+
+    before = dict(erasure.STATS)
+    data = os.urandom(10_000)
+    assert erasure.encode(data, 4, 2, Refusing()) == erasure.encode(data, 4, 2, None)
+    assert erasure.STATS["cpu_fallbacks"] == before["cpu_fallbacks"] + 1
+    assert erasure.STATS["cpu"] == before["cpu"] + 1

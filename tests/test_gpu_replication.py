@@ -138,3 +138,33 @@ def test_device_dropped_descriptor_rebuilds(gcluster):
     st, replicas, _ = write(a, arena, data, "drop2", [b])
     assert st == fp.OK and replicas == 2
     arena.close()
+
+
+def test_client_erasure_coding_runs_on_the_local_gpu(native, tmp_path, has_gpu):
+    """the client's RS encode/decode (reference dfs/client/src/mod.rs:308-412,
+    1110-1165) runs on the co-located chunkserver's GPU through the fast path (shards staged in
+    the client's registered shm slot), bit-identical to the CPU codec, and counted."""
+    if not has_gpu:
+        pytest.skip("no GPU")
+    from rust_hadoop_generated_by_llm_amd.ops import erasure
+
+    store = native.ChunkStore(str(tmp_path / "ec"), "", 0, 1 << 30, 0, 100, 4, 1, False)
+    srv = native.FastPathServer(store, f"dfs_fp_ec_{os.getpid()}")
+    assert srv.start()[0]
+    arena = ShmArena(size=128 << 20, slot=64 << 20)
+    prov = fp.FastPathEc(fp.FastPathClient(srv.name), lambda: arena)
+    try:
+        before = dict(erasure.STATS)
+        for n, (k, m) in ((1, (2, 2)), (100_001, (4, 2)), (6 << 20, (6, 3)), ((6 << 20) + 5, (10, 4))):
+            data = os.urandom(n)
+            shards = erasure.encode(data, k, m, prov)
+            assert shards == erasure.encode(data, k, m, None)
+            lost = [None if i in (0, k) else s for i, s in enumerate(shards)]
+            assert erasure.decode(lost, k, m, n, prov) == data
+        assert erasure.STATS["gpu"] - before["gpu"] == 8
+        assert erasure.STATS["cpu_fallbacks"] == before["cpu_fallbacks"]
+        assert srv.stats()["fp_ec_ops"] == 8
+        assert store.stats()["direct_dma"] > 0  # the slot is pinned: no staging copies
+    finally:
+        arena.close()
+        srv.stop()
