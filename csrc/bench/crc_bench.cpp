@@ -172,6 +172,7 @@ int main(int argc, char** argv) {
   for (auto km : std::vector<std::pair<int, int>>{{6, 3}, {4, 2}, {10, 4}}) {
     const int k = km.first, m = km.second;
     const uint64_t shard = std::min<uint64_t>(16ull << 20, total / (k + m)) & ~uint64_t(255);
+    CK(hipMemcpy(d, host.data(), (k + m) * shard, hipMemcpyHostToDevice));  // earlier outputs overwrote inputs
     std::vector<uint8_t> mat(static_cast<size_t>(m) * k);
     for (int r = 0; r < m; ++r)
       for (int c = 0; c < k; ++c) mat[r * k + c] = static_cast<uint8_t>(1 + ((r * 7 + c * 13) % 255));
