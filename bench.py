@@ -65,6 +65,10 @@ def parse():
                         "for this long per rank (0 = skip); reported under stress_write")
     p.add_argument("--stress-size", type=int, default=10240)
     p.add_argument("--stress-concurrency", type=int, default=5)
+    p.add_argument("--remote-steps", type=int, default=2,
+                   help="after the timed steps, repeat write+read this many times with a REMOTE client "
+                        "(no shared memory, no local sockets: every master and chunkserver RPC over gRPC/TCP, "
+                        "as the reference's dfs_cli does); reported under remote_client (0 = skip)")
     p.add_argument("--profile-dir", default=None,
                    help="run each ChunkServer under rocprofv3 --kernel-trace --stats, output here")
     return p.parse_args()
@@ -368,6 +372,27 @@ def main():
                                     prefix=prefix_of(rank) + "/stress")
             stress = {"ops": ss.count, "seconds": ss.total_s, "errors": ss.errors, "lat": ss.latencies,
                       "first_error": getattr(ss, "first_error", "")}
+        remote = None
+        if a.remote_steps > 0:
+            # the reference's wire path (dfs/client/src/mod.rs:415-451,921-944): a client that
+            # is not co-located, so every WriteBlock/ReadBlock carries the payload over gRPC
+            rc = Client([my_master], local_chunkserver=None, local_rpc=False)
+            rc.set_shard_map(ShardMap.load_config_file(str(shard_file)))
+            barrier()
+            rwl, rrl, rwb, rrb, rwt, rrt = [], [], 0, 0, 0.0, 0.0
+            for s in range(a.remote_steps):
+                ws, names = bench_write(rc, a.count, a.size, a.concurrency, prefix=prefix_of(rank) + "/remote",
+                                        payloads=payloads, run_id=f"rem{s}", pool=tpool)
+                rs = bench_read(rc, files=names, pool=tpool,
+                                verify={nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if s == 0 else None)
+                rwl += ws.latencies
+                rrl += rs.latencies
+                rwb += ws.count * ws.avg_size
+                rrb += rs.count * rs.avg_size
+                rwt += ws.total_s
+                rrt += rs.total_s
+            rc.close()
+            remote = {"wl": rwl, "rl": rrl, "wbytes": rwb, "rbytes": rrb, "wt": rwt, "rt": rrt}
         stats = {}
         try:
             import urllib.request
@@ -376,7 +401,7 @@ def main():
         except Exception:  # noqa: BLE001
             pass
         allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
-                       "rt": rt, "cs": stats, "stress": stress, "rccl": cs_info.get("rccl", False),
+                       "rt": rt, "cs": stats, "stress": stress, "remote": remote, "rccl": cs_info.get("rccl", False),
                        "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                    for k, v in (client.phase_times or {}).items() if v}})
         if rank == 0:
@@ -419,6 +444,19 @@ def main():
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],
             }
+            if a.remote_steps > 0:
+                rwl = sorted(x for r in allr for x in r["remote"]["wl"])
+                rrl = sorted(x for r in allr for x in r["remote"]["rl"])
+                rw = sum(r["remote"]["wbytes"] for r in allr) / (1 << 20) / max(r["remote"]["wt"] for r in allr)
+                rr = sum(r["remote"]["rbytes"] for r in allr) / (1 << 20) / max(r["remote"]["rt"] for r in allr)
+                result["remote_client"] = {
+                    "steps": a.remote_steps, "path": "gRPC/TCP for every master and chunkserver RPC (no shm, "
+                                                      "no UNIX sockets), Python grpcio client",
+                    "write_mb_per_s": round(rw, 2), "read_mb_per_s": round(rr, 2),
+                    "mb_per_s": round((sum(r["remote"]["wbytes"] + r["remote"]["rbytes"] for r in allr) / (1 << 20))
+                                      / max(r["remote"]["wt"] + r["remote"]["rt"] for r in allr), 2),
+                    "write_p50_ms": round(pct(rwl, 50), 3), "write_p99_ms": round(pct(rwl, 99), 3),
+                    "read_p50_ms": round(pct(rrl, 50), 3), "read_p99_ms": round(pct(rrl, 99), 3)}
             if a.stress_seconds > 0:
                 slat = sorted(x for r in allr for x in r["stress"]["lat"])
                 ops = sum(r["stress"]["ops"] for r in allr) / max(r["stress"]["seconds"] for r in allr)

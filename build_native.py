@@ -25,6 +25,10 @@ PKG = ROOT / "rust_hadoop_generated_by_llm_amd"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.environ.get("HIPCC", f"{ROCM}/bin/hipcc")
+# nghttp2 (native gRPC server): headers ship with the image's conda tree, the runtime library
+# with the system; link the system soname so the extension loads without conda on the path
+NGHTTP2_INC = os.environ.get("NGHTTP2_INC", "/opt/conda/include")
+NGHTTP2_LIB = os.environ.get("NGHTTP2_LIB", "/usr/lib/x86_64-linux-gnu/libnghttp2.so.14")
 
 
 def ext_path() -> Path:
@@ -36,6 +40,19 @@ def _includes() -> list[str]:
 
     return [f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
             f"-I{ROCM}/include"]
+
+
+def _nghttp2_include() -> list[str]:
+    """Only nghttp2's own headers (a copy under build/): putting the whole conda include
+    directory on the path would shadow the system OpenSSL headers."""
+    import shutil
+
+    dst = BUILD / "nghttp2_include" / "nghttp2"
+    if not (dst / "nghttp2.h").exists():
+        dst.mkdir(parents=True, exist_ok=True)
+        for f in ("nghttp2.h", "nghttp2ver.h"):
+            shutil.copy2(Path(NGHTTP2_INC) / "nghttp2" / f, dst / f)
+    return [f"-I{dst.parent}"]
 
 
 def _newer(src: Path, obj: Path, headers: list[Path]) -> bool:
@@ -63,7 +80,8 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
         objs.append(obj)
         if clean or _newer(src, obj, headers):
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
-            jobs.append([HIPCC, *flags, *lang, "-c", str(src), "-o", str(obj)])
+            extra = _nghttp2_include() if src.name == "grpc_server.cpp" else []
+            jobs.append([HIPCC, *flags, *extra, *lang, "-c", str(src), "-o", str(obj)])
 
     def run(cmd):
         if verbose:
@@ -81,8 +99,8 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
     out = ext_path()
     if clean or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(out), *map(str, objs),
-                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto", "-lpthread",
-                f"-Wl,-rpath,{ROCM}/lib"]
+                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto", NGHTTP2_LIB,
+                "-lpthread", f"-Wl,-rpath,{ROCM}/lib"]
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
@@ -106,8 +124,8 @@ def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[P
                 raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
         if clean or not exe.exists() or any(o.stat().st_mtime > exe.stat().st_mtime for o in [obj, *runtime]):
             r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-o", str(exe), str(obj), *map(str, runtime),
-                                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto", "-lpthread",
-                                f"-Wl,-rpath,{ROCM}/lib"], capture_output=True, text=True)
+                                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto",
+                                NGHTTP2_LIB, "-lpthread", f"-Wl,-rpath,{ROCM}/lib"], capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"link failed: {exe}\n{r.stdout}\n{r.stderr}")
         outs.append(exe)

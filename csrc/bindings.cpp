@@ -12,6 +12,8 @@
 #include "fastpath.h"
 #include "gf256.h"
 #include "replication.h"
+#include "cs_grpc.h"
+#include "grpc_server.h"
 #include "sigv4.h"
 #include "wal.h"
 
@@ -490,6 +492,59 @@ PYBIND11_MODULE(_dfs_native, m) {
       })
       .def_property_readonly("bytes_sent", [](ReplicationEngine& e) { return e.stats().bytes_sent; })
       .def_property_readonly("bytes_recv", [](ReplicationEngine& e) { return e.stats().bytes_recv; });
+
+  // ---------------- native gRPC ChunkServerService (nghttp2)
+  struct NativeGrpc {
+    std::shared_ptr<py::object> fallback;
+    std::unique_ptr<NativeChunkService> svc;
+    std::unique_ptr<GrpcServer> srv;
+  };
+  py::class_<NativeGrpc>(m, "NativeGrpcChunkServer")
+      .def(py::init([](ChunkStore* store, FastPathServer* fp, const std::string& host, int port, py::object fallback,
+                       int workers) {
+             auto n = std::make_unique<NativeGrpc>();
+             // the Python fallback is released with the GIL held, whichever thread drops it
+             n->fallback = std::shared_ptr<py::object>(new py::object(std::move(fallback)), [](py::object* o) {
+               py::gil_scoped_acquire g;
+               delete o;
+             });
+             auto fb = n->fallback;
+             n->svc = std::make_unique<NativeChunkService>(store, fp, [fb](const GrpcCall& c) -> GrpcReply {
+               py::gil_scoped_acquire g;
+               try {
+                 py::tuple r = (*fb)(c.path, c.request_id, py::bytes(c.message));
+                 return GrpcReply{r[0].cast<int>(), r[1].cast<std::string>()};
+               } catch (py::error_already_set& e) {
+                 return GrpcReply{13, std::string("python handler failed: ") + e.what()};
+               }
+             });
+             NativeChunkService* svc = n->svc.get();
+             n->srv = std::make_unique<GrpcServer>(host, port, [svc](const GrpcCall& c) { return svc->handle(c); },
+                                                   workers);
+             return n;
+           }),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::arg("store"), py::arg("fastpath"), py::arg("host"),
+           py::arg("port"), py::arg("fallback"), py::arg("workers") = 32)
+      .def("start", [](NativeGrpc& n) {
+        std::string err;
+        bool ok = n.srv->start(&err);
+        return py::make_tuple(ok, err);
+      })
+      .def("stop", [](NativeGrpc& n) {
+        py::gil_scoped_release r;  // workers may be waiting for the GIL in the fallback
+        n.srv->stop();
+      })
+      .def_property_readonly("port", [](NativeGrpc& n) { return n.srv->port(); })
+      .def("stats", [](NativeGrpc& n) {
+        CsGrpcStats s = n.svc->stats();
+        py::dict d;
+        d["native_grpc_calls"] = n.srv->calls();
+        d["native_grpc_writes"] = s.native_writes;
+        d["native_grpc_reads"] = s.native_reads;
+        d["native_grpc_replicates"] = s.native_replicates;
+        d["native_grpc_fallbacks"] = s.fallbacks;
+        return d;
+      });
 
   // ---------------- WAL
   py::class_<Wal>(m, "Wal")

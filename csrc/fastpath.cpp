@@ -520,6 +520,40 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
   return 0;
 }
 
+bool FastPathServer::all_local(const std::vector<std::string>& next) {
+  for (auto& a : next)
+    if (local_peer(a) == nullptr) return false;
+  return true;
+}
+
+bool FastPathServer::p2p_ready(const std::vector<std::string>& next) {
+  for (auto& a : next) {
+    Peer* p = local_peer(a);
+    if (p == nullptr || repl_ == nullptr || p->rank < 0 || !repl_->pair_ok(p->rank)) return false;
+  }
+  return true;
+}
+
+void FastPathServer::add_suspect(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  suspects_.push_back(id);
+}
+
+bool FastPathServer::persist_and_replicate(const std::string& id, const uint8_t* host, uint64_t n, uint32_t crc,
+                                           uint64_t term, const std::vector<std::string>& next, int* downstream,
+                                           std::string* err) {
+  // no shared-memory source: replicas go over the P2P transport (the block is staged in HBM)
+  // or, without a pair, fail and are not counted — as a downstream failure in the reference
+  const std::string rid = t_request_id;
+  auto fut = std::async(std::launch::async, [&] {
+    RequestScope rs(rid);
+    replicate(id, crc, term, next, ShmSrc{}, host, n, downstream);
+  });
+  bool ok = store_->persist(id, host, n, err);
+  fut.get();
+  return ok;
+}
+
 void FastPathServer::replicate(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
                                const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas) {
   *replicas = 0;
@@ -564,11 +598,6 @@ void FastPathServer::serve(int fd) {
     fut.get();
     if (!pok) return send_response(fd, FpStatus::IoError, 0, 0, perr);
     return send_response(fd, FpStatus::Ok, len, 1 + static_cast<uint64_t>(down), "");
-  };
-  auto all_local = [&](const std::vector<std::string>& next) {
-    for (auto& a : next)
-      if (local_peer(a) == nullptr) return false;
-    return true;
   };
   while (!stop_.load()) {
     uint32_t n = 0;

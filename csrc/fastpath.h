@@ -102,6 +102,15 @@ class FastPathServer {
   void set_peer(const std::string& addr, int rank, const std::string& fp_name);
   // Control exchange with the fast path of the peer of `rank` (the engine's ControlFn).
   bool control(int rank, const std::string& req, std::string* reply);
+  // For the native gRPC service (cs_grpc.cpp): whether every address is a same-host peer
+  // this server can replicate to natively; persist a staged block while fanning it out to
+  // `next` (the replicas count written downstream); queue a block for background recovery.
+  bool all_local(const std::vector<std::string>& next);
+  bool p2p_ready(const std::vector<std::string>& next);  // every hop has a P2P pair up
+  bool persist_and_replicate(const std::string& id, const uint8_t* host, uint64_t n, uint32_t crc, uint64_t term,
+                             const std::vector<std::string>& next, int* downstream, std::string* err);
+  void add_suspect(const std::string& id);
+  void note_rid(const std::string& rid);  // record a served request id (recent_request_ids)
   // Test hook: the next `n` REPL descriptors are dropped on the way out.
   void debug_drop_descriptors(int n) { drop_descriptors_ += n; }
   void set_self_host(const std::string& host);  // our advertised host: same-host peer detection
@@ -150,7 +159,6 @@ class FastPathServer {
   std::vector<std::string> suspects_;
   std::vector<std::string> recent_rids_;  // ring of the last kRecentRids request ids (mu_)
   size_t recent_pos_ = 0;
-  void note_rid(const std::string& rid);
   FpStats st_;
   ReplicationEngine* repl_ = nullptr;
   std::atomic<int> drop_descriptors_{0};

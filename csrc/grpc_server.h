@@ -1,0 +1,72 @@
+// Minimal native gRPC server: unary RPCs over HTTP/2 (h2c, prior knowledge) on nghttp2.
+//
+// grpc++ is not in this toolchain, nghttp2 is. The wire is plain gRPC —
+// HEADERS (:path /dfs.<Service>/<Method>, content-type application/grpc, te: trailers), one
+// length-prefixed message in DATA, and grpc-status / grpc-message trailers — so reference
+// clients (tonic) and Python grpcio talk to it unchanged (tests/test_native_grpc.py).
+//
+// Threading: one thread per connection owns its nghttp2 session (the library is not
+// thread-safe); complete requests are handed to a worker pool, so the many concurrent streams
+// a pooled client channel multiplexes run in parallel; finished responses come back to the
+// connection thread through an eventfd. Flow-control windows are opened wide (64 MiB per
+// stream, 1 GiB per connection) so a 1-100 MiB block never waits on WINDOW_UPDATE round trips.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace dfs {
+
+struct GrpcCall {
+  std::string path;        // "/dfs.ChunkServerService/WriteBlock"
+  std::string request_id;  // x-request-id metadata ("" if absent)
+  std::string message;     // the serialized request
+};
+
+struct GrpcReply {
+  int status = 0;          // grpc status code
+  std::string message;     // serialized response (status 0) or grpc-message text
+};
+
+class GrpcServer {
+ public:
+  using Handler = std::function<GrpcReply(const GrpcCall&)>;
+  GrpcServer(std::string host, int port, Handler handler, int workers = 32);
+  ~GrpcServer();
+  GrpcServer(const GrpcServer&) = delete;
+  bool start(std::string* err);
+  void stop();
+  int port() const { return port_; }
+  uint64_t calls() const { return calls_.load(); }
+
+ private:
+  struct Conn;
+  void accept_loop();
+  void serve(int fd);
+  void worker_loop();
+
+  std::string host_;
+  int port_;
+  Handler handler_;
+  int nworkers_;
+  int lfd_ = -1;
+  std::atomic<bool> stop_{false};
+  std::thread acceptor_;
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> jobs_;
+  std::vector<int> conns_;
+  int live_conns_ = 0;
+  std::condition_variable conns_cv_;
+  std::atomic<uint64_t> calls_{0};
+};
+
+}  // namespace dfs

@@ -15,6 +15,7 @@ import shutil
 import signal
 import threading
 import time
+import uuid
 import zlib
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from pathlib import Path
@@ -25,7 +26,8 @@ from ..native import require_gpu
 from ..parallel.sharding import ShardMap
 from ..utils import log as logsetup
 from ..utils.metrics import Registry
-from ..utils.rpc import ChannelPool, make_sync_server, rpc_details, server_credentials, strip_scheme, with_scheme
+from ..utils.rpc import (ChannelPool, RpcStatus, current_request_id, make_sync_server, rpc_details,
+                         server_credentials, snake, strip_scheme, with_scheme)
 from .service import ChunkServer
 
 log = logging.getLogger("dfs.chunkserver")
@@ -64,6 +66,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-fsync", action="store_true", help="skip fdatasync (tests only)")
     p.add_argument("--workers", type=int, default=64)
     p.add_argument("--no-fastpath", action="store_true", help="disable the native local UNIX-socket data path")
+    p.add_argument("--grpc-impl", choices=["native", "grpcio"], default=os.environ.get("DFS_CS_GRPC", "native"),
+                   help="ChunkServerService transport: native HTTP/2 gRPC (nghttp2, C++ data RPCs, Python "
+                        "handlers for the rest) or Python grpcio for everything")
     return p
 
 
@@ -160,6 +165,7 @@ class ChunkServerProcess:
                     self.repl_pairs_up = eng.wait_ready(args.rccl_timeout_ms)
                     log.info("%s replication: rank %d/%d, %d/%d pairs up", transport, args.rccl_rank,
                              args.rccl_world, self.repl_pairs_up, args.rccl_world - 1)
+        self.native_grpc = None
         self.metrics = Registry()
         self.cs = ChunkServer(self.store, self.advertise, self.pool, self.masters, self.rccl, rank_map,
                               args.rccl_rank, self.metrics, fastpath=self.fastpath)
@@ -265,6 +271,8 @@ class ChunkServerProcess:
                     d.update(proc.cs.stats)
                     if proc.fastpath is not None:
                         d.update(proc.fastpath.stats())
+                    if proc.native_grpc is not None:
+                        d.update(proc.native_grpc.stats())
                     if proc.rccl is not None:
                         d.update({f"repl_{k}": v for k, v in proc.rccl.stats().items()})
                         d["repl_transport"] = proc.rccl.transport
@@ -316,11 +324,44 @@ class ChunkServerProcess:
         srv.daemon_threads = True
         return srv
 
+    def _grpc_fallback(self, path: str, rid: str, payload: bytes):
+        """Python side of the native gRPC server: the RPCs (or cases) it does not run in C++."""
+        method = path.rsplit("/", 1)[-1]
+        entry = self._py_methods.get(method)
+        if entry is None:
+            return 12, f"unknown method {path}"
+        fn, req_cls = entry
+        token = current_request_id.set(rid or uuid.uuid4().hex)
+        try:
+            return 0, fn(req_cls.FromString(payload), None).SerializeToString()
+        except RpcStatus as e:
+            return e.code.value[0], e.message
+        except Exception as e:  # noqa: BLE001 - reported as INTERNAL like grpcio would
+            log.exception("%s failed", method)
+            return 13, f"{type(e).__name__}: {e}"
+        finally:
+            current_request_id.reset(token)
+
+    def _start_grpc(self, a, creds):
+        host, port = strip_scheme(a.addr).rsplit(":", 1)
+        if a.grpc_impl == "native" and creds is None and self.fastpath is not None:
+            self._py_methods = {name: (getattr(self.cs, snake(name)), req)
+                                for name, req, _resp in pb.SERVICES["ChunkServerService"]}
+            srv = native.NativeGrpcChunkServer(self.store, self.fastpath, host, int(port), self._grpc_fallback,
+                                               workers=a.workers)
+            ok, err = srv.start()
+            if ok:
+                self.native_grpc = srv
+                return None
+            log.error("native gRPC server failed (%s); serving ChunkServerService on grpcio", err)
+        server = make_sync_server({"ChunkServerService": self.cs}, a.addr, workers=a.workers, creds=creds)
+        server.start()
+        return server
+
     def run(self) -> None:
         a = self.args
         creds = server_credentials(a.tls_cert, a.tls_key)
-        server = make_sync_server({"ChunkServerService": self.cs}, a.addr, workers=a.workers, creds=creds)
-        server.start()
+        server = self._start_grpc(a, creds)
         http = self._http()
         threading.Thread(target=http.serve_forever, daemon=True, name="cs-http").start()
         threading.Thread(target=self._heartbeat_loop, daemon=True, name="cs-heartbeat").start()
@@ -336,7 +377,10 @@ class ChunkServerProcess:
         log.info("chunkserver %s serving (gpu=%d, durability=%s)", self.advertise, a.gpu, a.durability)
         while not self._stop.wait(0.5):
             pass
-        server.stop(1.0).wait()
+        if server is not None:
+            server.stop(1.0).wait()
+        if self.native_grpc is not None:
+            self.native_grpc.stop()
         http.shutdown()
         if self.rccl is not None:
             self.rccl.stop()

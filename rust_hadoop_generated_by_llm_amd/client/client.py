@@ -56,7 +56,7 @@ class Client:
                  max_retries: int = MAX_RETRIES, initial_backoff_ms: int = INITIAL_BACKOFF_MS,
                  ca_cert: str | None = None, domain_name: str | None = None, hedge_delay_ms: int | None = None,
                  local_chunkserver: str | None = None, ec_store=None, rpc_timeout: float = 30.0,
-                 data_timeout: float = 120.0, short_circuit: bool = True):
+                 data_timeout: float = 120.0, short_circuit: bool = True, local_rpc: bool = True):
         self.tls = ca_cert is not None
         self.master_addrs = [with_scheme(a, self.tls) for a in master_addrs if a]
         self.config_server_addrs = [with_scheme(a, self.tls) for a in (config_server_addrs or []) if a]
@@ -71,7 +71,8 @@ class Client:
         self.ec_on_gpu = os.environ.get("DFS_CLIENT_GPU_EC", "1") == "1"
         self.rpc_timeout = rpc_timeout
         self.data_timeout = data_timeout
-        self.pool = ChannelPool(ca_cert, domain_name)
+        # local_rpc=False: every RPC over gRPC/TCP, as a client on another host would
+        self.pool = ChannelPool(ca_cert, domain_name, local=local_rpc)
         self._exec = ThreadPoolExecutor(max_workers=32, thread_name_prefix="dfs-client")
         self.short_circuit = short_circuit and self.local_chunkserver is not None
         self._arena: ShmArena | None = None

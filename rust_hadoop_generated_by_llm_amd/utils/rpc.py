@@ -165,7 +165,7 @@ LOCAL_SERVICES = frozenset({"MasterService", "ConfigService"})
 class ChannelPool:
     """Persistent channels keyed by (target, tls). Thread-safe; shared per process."""
 
-    def __init__(self, ca_cert: str | None = None, domain_name: str | None = None):
+    def __init__(self, ca_cert: str | None = None, domain_name: str | None = None, local: bool = True):
         self._lock = threading.Lock()
         self._chans: dict[str, grpc.Channel] = {}
         self._ca = None
@@ -176,7 +176,7 @@ class ChannelPool:
         self._callables: dict[tuple[str, str, str], Callable] = {}
         # same-host fast transport for metadata services (utils/localrpc.py)
         self._local = None
-        if os.environ.get("DFS_NO_LOCALRPC") != "1" and ca_cert is None:
+        if local and os.environ.get("DFS_NO_LOCALRPC") != "1" and ca_cert is None:
             from .localrpc import LocalRegistry
 
             self._local = LocalRegistry()
