@@ -420,7 +420,8 @@ PYBIND11_MODULE(_dfs_native, m) {
            py::arg("xfer_timeout_ms") = 20000)
       .def("start", &ReplicationEngine::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &ReplicationEngine::stop, py::call_guard<py::gil_scoped_release>())
-      .def("wait_ready", &ReplicationEngine::wait_ready, py::call_guard<py::gil_scoped_release>())
+      .def("wait_ready", &ReplicationEngine::wait_ready, py::call_guard<py::gil_scoped_release>(), py::arg("timeout_ms"),
+           py::arg("give_up_after") = 3)
       .def_property_readonly("rank", &ReplicationEngine::rank)
       .def_property_readonly("world", &ReplicationEngine::world)
       .def_property_readonly("transport", &ReplicationEngine::transport_name)

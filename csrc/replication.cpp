@@ -138,15 +138,17 @@ void ReplicationEngine::stop() {
     if (p != rank_) t_->close(p);
 }
 
-int ReplicationEngine::wait_ready(int timeout_ms) {
+int ReplicationEngine::wait_ready(int timeout_ms, int give_up_after) {
   auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
   int up = 0;
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
     Peer& P = peer(p);
     std::unique_lock<std::mutex> lk(P.mu);
-    if (P.cv.wait_until(lk, deadline, [&] { return stop_.load() || P.state == State::Up; }) && P.state == State::Up)
-      ++up;
+    P.cv.wait_until(lk, deadline, [&] {
+      return stop_.load() || P.state == State::Up || (give_up_after > 0 && P.failed_opens >= give_up_after);
+    });
+    if (P.state == State::Up) ++up;
   }
   return up;
 }
@@ -238,6 +240,7 @@ void ReplicationEngine::opener_loop(int p) {
         P.last_error = err;
       }
       if (ok) P.opener = false;
+      else P.failed_opens++;
       P.cv.notify_all();
     }
     if (ok) {
@@ -317,6 +320,7 @@ std::string ReplicationEngine::handle_control(const std::string& req) {
       Q.state = ok ? State::Up : State::Broken;
       Q.last_error = e;
     }
+    if (!ok) Q.failed_opens++;
     Q.cv.notify_all();
     if (ok) {
       std::lock_guard<std::mutex> sg(st_mu_);

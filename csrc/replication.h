@@ -84,8 +84,10 @@ class ReplicationEngine {
   // Starts bringing up every pair this rank initiates (peers with a higher rank).
   void start();
   void stop();
-  // Waits until every pair is up (or the deadline); returns the number of pairs up.
-  int wait_ready(int timeout_ms);
+  // Waits until every pair is up, or every pair that is not up has failed `give_up_after`
+  // bring-up attempts (a deterministic failure, e.g. two ranks sharing one GPU), or the
+  // deadline; returns the number of pairs up. Pairs keep retrying in the background.
+  int wait_ready(int timeout_ms, int give_up_after = 3);
 
   int rank() const { return rank_; }
   int world() const { return world_; }
@@ -124,6 +126,7 @@ class ReplicationEngine {
     int64_t recv_next = 0;
     bool opener = false;  // an opener thread is running (initiator side)
     uint64_t peer_inc = 0;  // initiator side: the peer process instance the pair was opened with
+    int failed_opens = 0;   // bring-up attempts of this pair that failed (both sides count)
     std::string last_error;
   };
   Peer& peer(int p);

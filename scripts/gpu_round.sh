@@ -103,3 +103,8 @@ if [ "$STEP" = "gate3" ]; then
     --master-port 29551 bench.py --gpus 4 --steps 3 --warmup 1 --hbm-capacity 16G > gpurun_out/g3_n4.json 2> gpurun_out/g3_n4.err && \
   timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/g3_n1.json 2> gpurun_out/g3_n1.err || exit $?
 fi
+if [ "$STEP" = "grpcab" ]; then
+  # remote-client phase with the ChunkServerService on the native nghttp2 server vs grpcio
+  DFS_CS_GRPC=grpcio timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_grpcio.json 2> gpurun_out/ab_grpcio.err && \
+  DFS_CS_GRPC=native timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_native.json 2> gpurun_out/ab_native.err || exit $?
+fi
