@@ -361,6 +361,16 @@ def main():
         cpu1 = cpu_snapshot()
         host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
 
+        def cs_stats() -> dict:
+            try:
+                import urllib.request
+
+                return json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
+            except Exception:  # noqa: BLE001
+                return {}
+
+        # counters of the timed phase only (the stress / remote phases below add their own hops)
+        stats = cs_stats()
         stress = None
         if a.stress_seconds > 0:
             # the reference's only published throughput (stress-write 30 s, 10240 B,
@@ -393,13 +403,6 @@ def main():
                 rrt += rs.total_s
             rc.close()
             remote = {"wl": rwl, "rl": rrl, "wbytes": rwb, "rbytes": rrb, "wt": rwt, "rt": rrt}
-        stats = {}
-        try:
-            import urllib.request
-
-            stats = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
-        except Exception:  # noqa: BLE001
-            pass
         allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
                        "rt": rt, "cs": stats, "stress": stress, "remote": remote, "rccl": cs_info.get("rccl", False),
                        "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)

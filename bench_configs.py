@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""Secondary BASELINE.json configurations (bench.py measures the headline, config 2/scaling).
+
+    python bench_configs.py config1            # CPU plumbing: 1 master + 1 CS, put/get + benchmark
+    python bench_configs.py config4 [--gpu 0]  # 2-shard Raft masters: stress-write + cross-shard Rename
+    python bench_configs.py config5 [--gpu 0]  # S3 gateway: PUT/GET/Range/MPU + Parquet over S3 (pyarrow)
+
+Each prints one JSON line. The reference publishes no number for these configurations except
+the stress-write throughput (470 ops/s, 10 KiB, conc 5: BASELINE.md); the harness follows the
+reference's own flows:
+  * config 4: `dfs_cli benchmark stress-write` (dfs/client/src/bin/dfs_cli.rs:697-807) against a
+    two-shard namespace, then cross-shard renames through the coordinator's 2PC
+    (dfs/metaserver/src/master.rs:2728-3021);
+  * config 5: test_scripts/spark-s3-test/run_spark_test.sh writes and reads Parquet through
+    S3A (path-style, SigV4). Spark is not in this image; pyarrow's S3 filesystem (AWS SDK,
+    SigV4, multipart upload, ranged GETs for footer + column chunks) drives the same gateway
+    calls, and the S3 object benchmarks use plain HTTP like s3_integration_test.py.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import tempfile
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from rust_hadoop_generated_by_llm_amd.client.benchmark import (bench_read, bench_stress_write,  # noqa: E402
+                                                               bench_write, make_payloads)
+from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster  # noqa: E402
+
+
+def pct(v, p):
+    v = sorted(v)
+    return round(1e3 * v[min(len(v) - 1, len(v) * p // 100)], 3) if v else 0.0
+
+
+def emit(d):
+    print(json.dumps(d), flush=True)
+
+
+# ----------------------------------------------------------------------------- config 1
+def config1(a):
+    """single master + 1 chunkserver on CPU: put/get 1 MiB round trip + the benchmark."""
+    with LocalCluster(n_chunkservers=1, gpus=None) as c:
+        cl = c.client()
+        data = os.urandom(1 << 20)
+        t0 = time.perf_counter()
+        cl.create_file_from_buffer(data, "/plumbing/one")
+        t1 = time.perf_counter()
+        got = cl.get_file_content("/plumbing/one")
+        t2 = time.perf_counter()
+        assert got == data
+        ws, names = bench_write(cl, a.count, a.size, a.concurrency, prefix="/bench_write",
+                                payloads=make_payloads(a.count, a.size))
+        rs = bench_read(cl, files=names, concurrency=a.concurrency)
+        emit({"config": 1, "topology": "1 master + 1 chunkserver, host store (no GPU), nvme-sync",
+              "put_1mib_ms": round(1e3 * (t1 - t0), 3), "get_1mib_ms": round(1e3 * (t2 - t1), 3),
+              "write_mb_per_s": round(ws.count * ws.avg_size / (1 << 20) / ws.total_s, 2),
+              "read_mb_per_s": round(rs.count * rs.avg_size / (1 << 20) / rs.total_s, 2),
+              "write_p50_ms": pct(ws.latencies, 50), "write_p99_ms": pct(ws.latencies, 99),
+              "read_p50_ms": pct(rs.latencies, 50), "read_p99_ms": pct(rs.latencies, 99),
+              "files": a.count, "size": a.size, "concurrency": a.concurrency})
+        cl.close()
+
+
+# ----------------------------------------------------------------------------- config 4
+def config4(a):
+    gpus = [a.gpu] if a.gpu >= 0 else None
+    with LocalCluster(shards=2, config_server=True, n_chunkservers=1, gpus=gpus,
+                      hbm_capacity="16G" if gpus else "0") as c:
+        cl = c.client()
+        # the two-shard range map: the second shard owns "< /m" (sharding.rs:99-106)
+        ss = bench_stress_write(cl, a.stress_seconds, a.stress_size, a.stress_concurrency, prefix="/a/stress")
+        ss2 = bench_stress_write(cl, a.stress_seconds, a.stress_size, a.stress_concurrency, prefix="/z/stress")
+        # cross-shard renames: /a/... (shard owning "< /m") -> /z/... (the other shard) via 2PC
+        n = a.renames
+        srcs = [f"/a/ren/src_{i:05d}" for i in range(n)]
+        payload = os.urandom(a.stress_size)
+        with ThreadPoolExecutor(a.stress_concurrency) as ex:
+            list(ex.map(lambda p: cl.create_file_from_buffer(payload, p), srcs))
+        lats, errors = [], 0
+        lock = threading.Lock()
+
+        def ren(i):
+            nonlocal errors
+            t0 = time.perf_counter()
+            try:
+                cl.rename_file(srcs[i], f"/z/ren/dst_{i:05d}")
+                with lock:
+                    lats.append(time.perf_counter() - t0)
+            except Exception:  # noqa: BLE001
+                with lock:
+                    errors += 1
+
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(a.stress_concurrency) as ex:
+            list(ex.map(ren, range(n)))
+        el = time.perf_counter() - t0
+        ok = all(cl.exists(f"/z/ren/dst_{i:05d}") and not cl.exists(srcs[i]) for i in range(0, n, max(1, n // 50)))
+        shards = {sid: len(ms) for sid, ms in c.shard_masters.items()}
+        emit({"config": 4, "topology": f"config server + {len(shards)} Raft shards + 1 chunkserver "
+                                      f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync",
+              "stress_write": [{"prefix": p, "seconds": s.total_s, "size": a.stress_size,
+                                "concurrency": a.stress_concurrency, "ops": s.count, "errors": s.errors,
+                                "ops_per_s": round(s.count / s.total_s, 1), "p50_ms": pct(s.latencies, 50),
+                                "p99_ms": pct(s.latencies, 99), "vs_published_470_ops_per_s":
+                                round(s.count / s.total_s / 470.0, 1)} for p, s in (("/a", ss), ("/z", ss2))],
+              "cross_shard_rename": {"ops": n, "errors": errors, "seconds": round(el, 3),
+                                     "ops_per_s": round(len(lats) / el, 1), "p50_ms": pct(lats, 50),
+                                     "p99_ms": pct(lats, 99), "verified": ok}})
+        cl.close()
+
+
+# ----------------------------------------------------------------------------- config 5
+def config5(a):
+    import requests
+
+    gpus = [a.gpu] if a.gpu >= 0 else None
+    with LocalCluster(n_chunkservers=1, gpus=gpus, hbm_capacity="16G" if gpus else "0") as c:
+        env = {"AUDIT_LOG_ENABLED": "false", "LOCAL_CHUNKSERVER": c.cs_addrs[0]}
+        url = c.start_s3(env)
+        out = {"config": 5, "topology": f"S3 gateway + 1 master + 1 chunkserver "
+                                        f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync"}
+        s = requests.Session()
+        assert s.put(f"{url}/bench").status_code == 200
+        n, size = a.count, a.size
+        objs = make_payloads(n, size)
+
+        def timed(fn, items, conc):
+            lats = []
+            lock = threading.Lock()
+
+            def one(x):
+                t0 = time.perf_counter()
+                fn(x)
+                with lock:
+                    lats.append(time.perf_counter() - t0)
+
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(conc) as ex:
+                list(ex.map(one, items))
+            return time.perf_counter() - t0, lats
+
+        sess = threading.local()
+
+        def http():
+            if not hasattr(sess, "s"):
+                sess.s = requests.Session()
+            return sess.s
+
+        def put(i):
+            r = http().put(f"{url}/bench/obj_{i:05d}", data=objs[i % len(objs)])
+            assert r.status_code == 200 and r.headers["ETag"] == f'"{hashlib.md5(objs[i % len(objs)]).hexdigest()}"'
+
+        def get(i):
+            r = http().get(f"{url}/bench/obj_{i:05d}")
+            assert r.status_code == 200 and len(r.content) == size
+
+        def rng(i):
+            off = (i * 7919 * 4096) % (size - 65536)
+            r = http().get(f"{url}/bench/obj_{i % n:05d}", headers={"Range": f"bytes={off}-{off + 65535}"})
+            assert r.status_code == 206 and len(r.content) == 65536
+
+        el, lat = timed(put, range(n), a.concurrency)
+        out["put"] = {"objects": n, "size": size, "mb_per_s": round(n * size / (1 << 20) / el, 1),
+                      "p50_ms": pct(lat, 50), "p99_ms": pct(lat, 99)}
+        el, lat = timed(get, range(n), a.concurrency)
+        out["get"] = {"objects": n, "size": size, "mb_per_s": round(n * size / (1 << 20) / el, 1),
+                      "p50_ms": pct(lat, 50), "p99_ms": pct(lat, 99)}
+        m = 4 * n
+        el, lat = timed(rng, range(m), a.concurrency)
+        out["range_get_64k"] = {"requests": m, "req_per_s": round(m / el, 1), "p50_ms": pct(lat, 50),
+                                "p99_ms": pct(lat, 99)}
+        # multipart upload of one large object, parts in parallel (S3 MPU emulation, handlers.rs:234-432)
+        import xml.etree.ElementTree as ET
+
+        part = 8 << 20
+        nparts = a.mpu_parts
+        blob = os.urandom(part * nparts)
+        t0 = time.perf_counter()
+        r = s.post(f"{url}/bench/big.bin?uploads")
+        upload_id = ET.fromstring(r.content).find("UploadId").text
+        etags = {}
+
+        def up(k):
+            rr = http().put(f"{url}/bench/big.bin?partNumber={k + 1}&uploadId={upload_id}",
+                            data=blob[k * part:(k + 1) * part])
+            assert rr.status_code == 200
+            etags[k + 1] = rr.headers["ETag"]
+
+        with ThreadPoolExecutor(min(8, nparts)) as ex:
+            list(ex.map(up, range(nparts)))
+        body = "<CompleteMultipartUpload>" + "".join(
+            f"<Part><PartNumber>{k}</PartNumber><ETag>{etags[k]}</ETag></Part>" for k in sorted(etags)) + \
+            "</CompleteMultipartUpload>"
+        r = s.post(f"{url}/bench/big.bin?uploadId={upload_id}", data=body)
+        assert r.status_code == 200, r.text
+        mpu_s = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        got = s.get(f"{url}/bench/big.bin").content
+        mpu_get_s = time.perf_counter() - t0
+        assert got == blob
+        out["multipart"] = {"parts": nparts, "part_size": part, "upload_mb_per_s": round(len(blob) / (1 << 20) / mpu_s, 1),
+                            "get_mb_per_s": round(len(blob) / (1 << 20) / mpu_get_s, 1)}
+        out["parquet_over_s3"] = parquet_phase(url, a)
+        emit(out)
+
+
+def parquet_phase(url: str, a) -> dict:
+    """The Spark S3A flow of run_spark_test.sh, driven by pyarrow's S3 filesystem: write a
+    Parquet table (multipart upload), read it back whole and column-projected (ranged GETs
+    of the footer and the column chunks), aggregate, compare with the source."""
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    import pyarrow.fs as pafs
+    import pyarrow.parquet as pq
+
+    rows = a.parquet_rows
+    rng = np.random.default_rng(7)
+    table = pa.table({"id": np.arange(rows, dtype=np.int64),
+                      "grp": rng.integers(0, 100, rows, dtype=np.int32),
+                      "value": rng.random(rows),
+                      "payload": rng.integers(0, 1 << 62, rows, dtype=np.int64)})
+    s3 = pafs.S3FileSystem(endpoint_override=url.split("://")[1], scheme="http", access_key="ak",
+                           secret_key="sk", region="us-east-1", allow_bucket_creation=True)
+    s3.create_dir("parquet")
+    t0 = time.perf_counter()
+    pq.write_table(table, "parquet/events.parquet", filesystem=s3, row_group_size=max(1, rows // 8))
+    w = time.perf_counter() - t0
+    size = s3.get_file_info("parquet/events.parquet").size
+    t0 = time.perf_counter()
+    back = pq.read_table("parquet/events.parquet", filesystem=s3)
+    r = time.perf_counter() - t0
+    assert back.equals(table)
+    t0 = time.perf_counter()
+    cols = pq.read_table("parquet/events.parquet", filesystem=s3, columns=["grp", "value"])
+    agg = pc.sum(cols["value"]).as_py()
+    rc = time.perf_counter() - t0
+    assert abs(agg - pc.sum(table["value"]).as_py()) < 1e-6 * rows
+    return {"rows": rows, "file_bytes": size, "write_mb_per_s": round(size / (1 << 20) / w, 1),
+            "read_mb_per_s": round(size / (1 << 20) / r, 1), "projected_read_sum_s": round(rc, 3),
+            "verified": True}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("config", choices=["config1", "config4", "config5"])
+    p.add_argument("--gpu", type=int, default=-1)
+    p.add_argument("--count", type=int, default=100)
+    p.add_argument("--size", type=int, default=1 << 20)
+    p.add_argument("--concurrency", type=int, default=10)
+    p.add_argument("--stress-seconds", type=float, default=30.0)
+    p.add_argument("--stress-size", type=int, default=10240)
+    p.add_argument("--stress-concurrency", type=int, default=10)
+    p.add_argument("--renames", type=int, default=500)
+    p.add_argument("--mpu-parts", type=int, default=8)
+    p.add_argument("--parquet-rows", type=int, default=4_000_000)
+    a = p.parse_args()
+    os.environ.setdefault("DFS_LOG", "warning")
+    {"config1": config1, "config4": config4, "config5": config5}[a.config](a)
+
+
+if __name__ == "__main__":
+    main()

@@ -108,3 +108,8 @@ if [ "$STEP" = "grpcab" ]; then
   DFS_CS_GRPC=grpcio timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_grpcio.json 2> gpurun_out/ab_grpcio.err && \
   DFS_CS_GRPC=native timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_native.json 2> gpurun_out/ab_native.err || exit $?
 fi
+if [ "$STEP" = "configs" ]; then
+  # BASELINE configs 4 (2-shard stress-write + cross-shard Rename) and 5 (S3 + Parquet) on the GPU
+  timeout -k 10 500 python bench_configs.py config4 --gpu 0 > gpurun_out/config4.json 2> gpurun_out/config4.err && \
+  timeout -k 10 500 python bench_configs.py config5 --gpu 0 > gpurun_out/config5.json 2> gpurun_out/config5.err || exit $?
+fi
