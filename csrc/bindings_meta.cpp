@@ -137,7 +137,8 @@ void bind_meta(py::module_& m) {
   py::class_<raft::Node, std::unique_ptr<raft::Node, NodeDeleter>>(m, "RaftNode")
       .def(py::init([](int id, std::map<int, std::string> members, std::string client_address, std::string dir,
                        py::object host, double elo, double ehi, double hb, bool sync, uint64_t snapshot_threshold,
-                       int max_batch, std::string backup_endpoint, std::string backup_bucket, py::object native_sm) {
+                       int max_batch, std::string backup_endpoint, std::string backup_bucket, py::object native_sm,
+                       bool pre_vote) {
              raft::Options o;
              o.id = id;
              o.members = std::move(members);
@@ -151,6 +152,7 @@ void bind_meta(py::module_& m) {
              o.max_append_batch = max_batch;
              o.backup_endpoint = std::move(backup_endpoint);
              o.backup_bucket = std::move(backup_bucket);
+             o.pre_vote = pre_vote;
              std::shared_ptr<raft::StateMachine> sm;
              if (!native_sm.is_none()) sm = native_sm.cast<std::shared_ptr<raft::StateMachine>>();
              auto h = std::make_shared<PyRaftHost>(std::move(host), sm);
@@ -160,7 +162,7 @@ void bind_meta(py::module_& m) {
            py::arg("election_lo") = 1.5, py::arg("election_hi") = 3.0, py::arg("heartbeat") = 0.1,
            py::arg("sync") = true, py::arg("snapshot_threshold") = 10000, py::arg("max_append_batch") = 512,
            py::arg("backup_endpoint") = "", py::arg("backup_bucket") = "dfs-backups",
-           py::arg("native_sm") = py::none())
+           py::arg("native_sm") = py::none(), py::arg("pre_vote") = true)
       .def("start", &raft::Node::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &raft::Node::stop, py::call_guard<py::gil_scoped_release>())
       .def("propose", [](raft::Node& n, std::string cmd, py::object cb) {
@@ -207,6 +209,30 @@ void bind_meta(py::module_& m) {
       .def("info_json", &raft::Node::info_json, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("wal_syncs", &raft::Node::wal_syncs)
       .def_property_readonly("wal_bytes", &raft::Node::wal_bytes);
+
+  // ---------------- native shard map (csrc/shard_map.cpp), for parity tests with parallel/sharding.py
+  py::class_<ShardMap>(m, "NativeShardMap")
+      .def_static("new_range", &ShardMap::new_range)
+      .def_static("new_consistent_hash", &ShardMap::new_consistent_hash, py::arg("virtual_nodes") = 100)
+      .def_static("from_json", [](const std::string& s) { return ShardMap::from_json(Json::parse(s)); })
+      .def("to_json", [](const ShardMap& sm) { return sm.to_json().dump(); })
+      .def("add_shard", &ShardMap::add_shard)
+      .def("remove_shard", &ShardMap::remove_shard)
+      .def("split_shard", &ShardMap::split_shard)
+      .def("merge_shards", &ShardMap::merge_shards)
+      .def("rebalance_boundary", &ShardMap::rebalance_boundary)
+      .def("get_shard", [](const ShardMap& sm, const std::string& key) -> py::object {
+        std::string s = sm.get_shard(key);
+        if (s.empty()) return py::none();
+        return py::str(s);
+      })
+      .def("get_shards", [](const ShardMap& sm, const std::vector<std::string>& keys) {
+        std::vector<std::string> out;
+        out.reserve(keys.size());
+        for (const auto& k : keys) out.push_back(sm.get_shard(k));
+        return out;
+      })
+      .def("shards", &ShardMap::shards);
 
   // ---------------- native config-server state machine (C36)
   py::class_<ConfigCore, raft::StateMachine, std::shared_ptr<ConfigCore>>(m, "ConfigCore")

@@ -270,20 +270,26 @@ void Node::reset_election_timer_locked() {
 void Node::ticker_loop() {
   auto hb = std::chrono::microseconds(static_cast<int64_t>(opt_.heartbeat * 1e6));
   while (running_) {
-    bool elect = false;
+    bool elect = false, transfer = false;
     {
       std::unique_lock<std::mutex> lk(mu_);
       tick_cv_.wait_for(lk, hb, [&] { return !running_ || tick_now_; });
       tick_now_ = false;
       if (!running_) break;
-      if (role_ == Role::Leader) broadcast_locked();
-      else if (Clock::now() >= election_deadline_ && config_.is_voter(opt_.id)) elect = true;
+      if (role_ == Role::Leader) {
+        broadcast_locked();
+      } else if (Clock::now() >= election_deadline_ && config_.is_voter(opt_.id)) {
+        elect = true;
+        transfer = transfer_election_;
+        transfer_election_ = false;
+      }
     }
-    if (elect) run_election();
+    if (elect && opt_.pre_vote && !transfer) run_pre_vote();
+    else if (elect) run_election(transfer);
   }
 }
 
-void Node::start_election_locked(std::string* hs, std::string* vote_args) {
+void Node::start_election_locked(bool transfer, std::string* hs, std::string* vote_args) {
   role_ = Role::Candidate;
   ++current_term_;
   voted_for_ = opt_.id;
@@ -296,10 +302,51 @@ void Node::start_election_locked(std::string* hs, std::string* vote_args) {
   a.set("candidate_id", opt_.id);
   a.set("last_log_index", last_index_locked());
   a.set("last_log_term", term_at(last_index_locked()));
+  if (transfer) a.set("transfer", true);
   *vote_args = a.dump();
 }
 
-void Node::run_election() {
+bool Node::leader_recent_locked() const {
+  if (role_ == Role::Leader) return true;
+  if (leader_id_ < 0) return false;
+  auto lease = std::chrono::microseconds(static_cast<int64_t>(opt_.election_lo * 1e6));
+  return Clock::now() < leader_contact_ + lease;
+}
+
+// Pre-vote round: ask the voters whether they WOULD vote for us at term+1, changing no
+// state anywhere. Only a majority of yes starts the real election (aux_loop), so a server
+// that cannot win never bumps the cluster's term and never unseats a working leader.
+void Node::run_pre_vote() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!running_ || role_ == Role::Leader) return;
+    reset_election_timer_locked();  // no majority of yes: try again after another timeout
+    uint64_t round = ++prevote_round_;
+    prevotes_ = {opt_.id};
+    if (!config_.has_joint_majority(prevotes_)) {
+      Json a = Json::object();
+      a.set("term", current_term_ + 1);
+      a.set("candidate_id", opt_.id);
+      a.set("last_log_index", last_index_locked());
+      a.set("last_log_term", term_at(last_index_locked()));
+      a.set("pre_vote", true);
+      std::string args = a.dump();
+      for (int p : peers_locked()) {
+        if (!config_.is_voter(p)) continue;
+        Peer* pp = peer(p);
+        pp->vote_body = args;
+        pp->vote_term = current_term_;
+        pp->vote_pre = true;
+        pp->vote_round = round;
+        pp->aux_cv.notify_one();
+      }
+      return;
+    }
+  }
+  run_election(false);  // sole voter
+}
+
+void Node::run_election(bool transfer) {
   std::string args;
   uint64_t term;
   {
@@ -308,7 +355,7 @@ void Node::run_election() {
     {
       std::lock_guard<std::mutex> g(mu_);
       if (!running_) return;
-      start_election_locked(&hs, &args);
+      start_election_locked(transfer, &hs, &args);
       term = current_term_;
     }
     persist({hs});
@@ -324,6 +371,7 @@ void Node::run_election() {
     Peer* pp = peer(p);
     pp->vote_body = args;
     pp->vote_term = term;
+    pp->vote_pre = false;
     pp->aux_cv.notify_one();
   }
 }
@@ -331,13 +379,16 @@ void Node::run_election() {
 void Node::aux_loop(Peer* p) {
   for (;;) {
     std::string body, addr;
-    uint64_t term;
+    uint64_t term, round;
+    bool pre;
     {
       std::unique_lock<std::mutex> lk(mu_);
       p->aux_cv.wait(lk, [&] { return !running_ || !p->vote_body.empty(); });
       if (!running_) return;
       body.swap(p->vote_body);
       term = p->vote_term;
+      pre = p->vote_pre;
+      round = p->vote_round;
       addr = addr_locked(p->id);
     }
     std::string reply;
@@ -351,6 +402,22 @@ void Node::aux_loop(Peer* p) {
     uint64_t rt = r["term"].as_u64();
     if (rt > term) {
       observe_term(rt, "", -1);
+      continue;
+    }
+    if (pre) {
+      bool start = false;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (role_ != Role::Leader && prevote_round_ == round && current_term_ == term &&
+            r["vote_granted"].as_bool()) {
+          prevotes_.insert(r.has("peer_id") ? static_cast<int>(r["peer_id"].as_int()) : p->id);
+          if (config_.has_joint_majority(prevotes_)) {
+            ++prevote_round_;  // late yes votes of this round start nothing more
+            start = true;
+          }
+        }
+      }
+      if (start) run_election(false);
       continue;
     }
     std::lock_guard<std::mutex> g(mu_);
@@ -897,14 +964,25 @@ std::string Node::on_vote(const Json& a) {
     {
       std::lock_guard<std::mutex> g(mu_);
       uint64_t t = a["term"].as_u64();
+      const bool pre = a["pre_vote"].as_bool();
+      const int cand = static_cast<int>(a["candidate_id"].as_int());
+      uint64_t my_last = last_index_locked();
+      int64_t my_term = term_at(my_last);
+      int64_t llt = a["last_log_term"].as_int();
+      const bool log_ok = llt > my_term || (llt == my_term && a["last_log_index"].as_u64() >= my_last);
+      // a live leader exists: neither a pre-vote nor a newer term from a candidate that is
+      // not a leadership transfer target (thesis 4.2.3 / 9.6)
+      const bool sticky = opt_.pre_vote && !a["transfer"].as_bool() && t > current_term_ && leader_recent_locked();
+      if (pre || sticky) {
+        out.set("term", current_term_);
+        out.set("vote_granted", pre && !sticky && t > current_term_ && log_ok);
+        out.set("peer_id", opt_.id);
+        return out.dump();  // no state changed, nothing to persist
+      }
       if (t > current_term_ && step_down_locked(t, "", -1, cbs)) recs.push_back(hs_record());
       bool granted = false;
-      int cand = static_cast<int>(a["candidate_id"].as_int());
       if (t == current_term_ && (voted_for_ == -1 || voted_for_ == cand)) {
-        uint64_t my_last = last_index_locked();
-        int64_t my_term = term_at(my_last);
-        int64_t llt = a["last_log_term"].as_int();
-        if (llt > my_term || (llt == my_term && a["last_log_index"].as_u64() >= my_last)) {
+        if (log_ok) {
           granted = true;
           voted_for_ = cand;
           recs.push_back(hs_record());
@@ -945,6 +1023,7 @@ std::string Node::on_append(const Json& a) {
         recs.push_back(hs_record());
       leader_id_ = lid;
       leader_address_ = a["leader_address"].str();
+      leader_contact_ = Clock::now();
       reset_election_timer_locked();
       uint64_t prev = a["prev_log_index"].as_u64();
       if (prev > last_index_locked()) {
@@ -1007,6 +1086,7 @@ std::string Node::on_snapshot(const Json& a) {
           recs.push_back(hs_record());
         leader_id_ = lid;
         leader_address_ = a["leader_address"].str();
+        leader_contact_ = Clock::now();
         reset_election_timer_locked();
         // a snapshot at or behind what we already applied would roll the state back
         install = lii > last_included_index_ && lii > last_applied_;
@@ -1053,6 +1133,7 @@ std::string Node::on_timeout_now(const Json& a) {
   bool ok = a["term"].as_u64() >= current_term_ && role_ != Role::Leader;
   if (ok) {
     election_deadline_ = Clock::now();  // the ticker starts the election right away
+    transfer_election_ = true;
     tick_now_ = true;
     tick_cv_.notify_all();
   }

@@ -103,6 +103,11 @@ struct Options {
   bool sync = true;
   uint64_t snapshot_threshold = 10000;
   int max_append_batch = 512;
+  // Pre-Vote + leader stickiness (Raft thesis 9.6): a server that cannot win (a joining node
+  // with an empty log, a removed or partitioned node) probes with a pre-vote first, and a
+  // server that heard from a live leader within election_lo refuses to adopt a newer term
+  // from a RequestVote. Leadership transfer (TimeoutNow) bypasses both.
+  bool pre_vote = true;
   std::string backup_endpoint, backup_bucket = "dfs-backups";
 };
 
@@ -167,6 +172,8 @@ class Node {
     bool want_append = false;
     std::string vote_body;  // pending RequestVote args (empty = none)
     uint64_t vote_term = 0;
+    bool vote_pre = false;    // vote_body is a pre-vote of round vote_round
+    uint64_t vote_round = 0;
   };
   using Callbacks = std::vector<std::function<void()>>;
   using Clock = std::chrono::steady_clock;
@@ -193,8 +200,10 @@ class Node {
   Peer* peer(int id);  // create on first use (mu_ held)
 
   // role changes (mu_ held)
-  void start_election_locked(std::string* hs, std::string* vote_args);
-  void run_election();
+  void start_election_locked(bool transfer, std::string* hs, std::string* vote_args);
+  void run_election(bool transfer = false);
+  void run_pre_vote();
+  bool leader_recent_locked() const;  // heard from (or are) a live leader within election_lo
   // a reply or request carried a newer term: step down and persist it
   void observe_term(uint64_t term, const std::string& leader_addr, int leader_id);
   void become_leader_locked();
@@ -255,6 +264,10 @@ class Node {
   std::vector<ReadWaiter> read_waiters_;
   uint64_t leader_noop_index_ = 0;
   Clock::time_point election_deadline_;
+  Clock::time_point leader_contact_{};  // last accepted AppendEntries / InstallSnapshot
+  uint64_t prevote_round_ = 0;
+  std::set<int> prevotes_;
+  bool transfer_election_ = false;  // next election was asked for by TimeoutNow
   bool tick_now_ = false;
   std::mt19937_64 rng_;
 

@@ -42,10 +42,12 @@ class NullHost:
         pass
 
 
-def mk(tmp_path, nid=1, members=None):
+def mk(tmp_path, nid=1, members=None, pre_vote=False):
+    # the plain RequestVote rules below are checked with leader stickiness off (a vote right
+    # after an append would be refused by it); test_pre_vote_and_leader_stickiness covers it
     host = NullHost()
     node = native.RaftNode(nid, members or {1: "a", 2: "b", 3: "c"}, "client-a", str(tmp_path / f"n{nid}"), host,
-                           sync=False)
+                           sync=False, pre_vote=pre_vote)
     return node, host
 
 
@@ -136,6 +138,35 @@ def test_install_snapshot_rules(tmp_path):
     del n
     n2, host2 = mk(tmp_path)
     assert n2.last_included_index == 5 and json.loads(host2.restored) == {"x": 1}
+
+
+def test_pre_vote_and_leader_stickiness(tmp_path):
+    """Raft thesis 9.6 on the native node: pre-votes change no state; a server that heard
+    from a live leader within election_lo refuses (pre-)votes for newer terms without
+    adopting them; a leadership-transfer candidate bypasses that."""
+    host = NullHost()
+    n = native.RaftNode(1, {1: "a", 2: "b", 3: "c"}, "client-a", str(tmp_path / "n1"), host, 0.3, 0.6, sync=False)
+    # no leader known: a pre-vote for an up-to-date log is granted, nothing is persisted
+    r = rpc(n, "vote", term=1, candidate_id=2, last_log_index=0, last_log_term=0, pre_vote=True)
+    assert r["vote_granted"] and n.term == 0
+    assert append(n, 3, 0, 0, [1, 1, 3])["success"]  # leader 2 at term 3
+    # inside the lease: refused, term not adopted (a disruptive joiner / removed server)
+    r = rpc(n, "vote", term=9, candidate_id=3, last_log_index=3, last_log_term=3)
+    assert not r["vote_granted"] and r["term"] == 3 and n.term == 3
+    assert not rpc(n, "vote", term=4, candidate_id=3, last_log_index=3, last_log_term=3, pre_vote=True)["vote_granted"]
+    time.sleep(0.35)  # lease (election_lo) over
+    # pre-vote: stale log refused, up-to-date granted; neither changes term or vote
+    assert not rpc(n, "vote", term=4, candidate_id=3, last_log_index=9, last_log_term=1, pre_vote=True)["vote_granted"]
+    assert rpc(n, "vote", term=4, candidate_id=3, last_log_index=3, last_log_term=3, pre_vote=True)["vote_granted"]
+    assert rpc(n, "vote", term=4, candidate_id=2, last_log_index=3, last_log_term=3, pre_vote=True)["vote_granted"]
+    assert n.term == 3
+    # the real vote after the lease works as before
+    assert rpc(n, "vote", term=4, candidate_id=3, last_log_index=3, last_log_term=3)["vote_granted"] and n.term == 4
+    # a fresh leader contact re-arms the lease; TimeoutNow-driven candidates still win it
+    assert append(n, 4, 3, 3, [])["success"]
+    assert not rpc(n, "vote", term=5, candidate_id=3, last_log_index=3, last_log_term=3)["vote_granted"]
+    r = rpc(n, "vote", term=5, candidate_id=3, last_log_index=3, last_log_term=3, transfer=True)
+    assert r["vote_granted"] and n.term == 5
 
 
 def test_timeout_now_only_for_current_or_newer_terms(tmp_path):
@@ -278,9 +309,11 @@ def test_isolated_node_rejoins_and_terms_converge(tmp_path):
         l1 = await c.leader()
         lone = next(n for n in c.nodes.values() if n is not l1)
         c.faults.isolate(f"node{lone.id}", list(c.registry))
-        t0 = lone.current_term
+        t0, lt0 = lone.current_term, l1.current_term
         await asyncio.sleep(1.0)
-        assert lone.current_term > t0 and lone.role != LEADER  # keeps campaigning, never wins alone
+        # pre-vote: the lone node keeps probing but never wins a pre-vote, so it never bumps
+        # its term (without pre-vote it would, and unseat the leader when it comes back)
+        assert lone.current_term == t0 and lone.role != LEADER
         await propose_any(c, {"set": ["k", 1]})
         c.faults.heal()
         for _ in range(100):
@@ -289,6 +322,7 @@ def test_isolated_node_rejoins_and_terms_converge(tmp_path):
                 break
             await asyncio.sleep(0.05)
         assert len({n.current_term for n in c.nodes.values()}) == 1 and lone.sm.d.get("k") == 1
+        assert l1.role == LEADER and l1.current_term == lt0  # the rejoin disrupted nothing
         await c.stop()
 
     run(go())
