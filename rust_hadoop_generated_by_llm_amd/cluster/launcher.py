@@ -37,6 +37,9 @@ class Proc:
     ready_file: str
     info: dict = field(default_factory=dict)
     log_path: str = ""
+    module: str = ""
+    args: list = field(default_factory=list)
+    extra_env: dict | None = None
 
 
 class LocalCluster:
@@ -100,7 +103,7 @@ class LocalCluster:
         p = subprocess.Popen([sys.executable, "-m", f"{PKG}.{module}", *args], env=env, stdout=logf,
                              stderr=subprocess.STDOUT, cwd=str(ROOT), start_new_session=True)
         logf.close()
-        proc = Proc(name, p, ready, log_path=log_path)
+        proc = Proc(name, p, ready, log_path=log_path, module=module, args=list(args), extra_env=extra_env)
         self.procs.append(proc)
         return proc
 
@@ -333,6 +336,19 @@ class LocalCluster:
                 except ProcessLookupError:
                     pass
                 pr.popen.wait(timeout=30)
+
+    def restart(self, name: str, sig: int = signal.SIGKILL, before_start=None) -> Proc:
+        """Kill process `name` (SIGKILL by default: a crash, nothing flushed) and start it again
+        with the same arguments and storage; returns once it signalled ready again.
+        `before_start` runs while it is down (e.g. to damage its files)."""
+        old = next(pr for pr in self.procs if pr.name == name)
+        self.kill(name, sig)
+        self.procs.remove(old)
+        if before_start is not None:
+            before_start()
+        pr = self._spawn(name, old.module, old.args, old.extra_env)
+        self._wait_ready([pr])
+        return pr
 
     def stop(self) -> None:
         for pr in reversed(self.procs):
