@@ -16,6 +16,13 @@ Storage is an append-only segment directory instead of RocksDB: one file per UTC
 query opens only the overlapping segments and retention is an ``unlink``. The record JSON
 uses the reference field order and compact separators, so hashes verify against the
 reference's ``compute_hmac`` definition.
+
+Secondary indexes (the reference's ``idx_user`` / ``idx_resource`` column families,
+audit.rs:16-17,63-69): next to each segment, ``seg-<h>.uidx`` and ``seg-<h>.ridx`` hold one
+``<user|bucket>\\t<offset>\\t<length>`` line per record, appended after the segment bytes
+they point at. A user or bucket query reads only the index lines and seeks to the matching
+records; segment bytes past the last indexed record (a crash between the two appends, or a
+segment written before indexes existed) are scanned directly, so nothing is ever missed.
 """
 from __future__ import annotations
 
@@ -82,16 +89,73 @@ class SegmentStore:
                     pass
         return sorted(out)
 
+    INDEXES = {"user": ".uidx", "resource": ".ridx"}
+
+    def seg_path(self, seg: int, ext: str = ".log") -> str:
+        return os.path.join(self.path, f"seg-{seg}{ext}")
+
     def append(self, keyed: list[tuple[int, dict]], sync: bool = False) -> None:
-        by_seg: dict[int, list[str]] = {}
+        by_seg: dict[int, list[tuple[bytes, dict]]] = {}
         for key_ts, rec in keyed:
-            by_seg.setdefault(key_ts // HOUR_MS * HOUR_MS, []).append(f"{key_ts}\t{canonical_json(rec)}\n")
-        for seg, lines in sorted(by_seg.items()):
-            with open(os.path.join(self.path, f"seg-{seg}.log"), "a", encoding="utf-8") as f:
-                f.write("".join(lines))
+            line = f"{key_ts}\t{canonical_json(rec)}\n".encode()
+            by_seg.setdefault(key_ts // HOUR_MS * HOUR_MS, []).append((line, rec))
+        for seg, items in sorted(by_seg.items()):
+            with open(self.seg_path(seg), "ab") as f:
+                base = f.seek(0, os.SEEK_END)
+                f.write(b"".join(line for line, _ in items))
                 f.flush()
                 if sync:
                     os.fsync(f.fileno())
+            # index lines only after the records they point at are written
+            uidx, ridx, off = [], [], base
+            for line, rec in items:
+                ref = f"\t{off}\t{len(line)}\n"
+                uidx.append(_idx_key(rec.get("user_id")) + ref)
+                ridx.append(_idx_key(extract_bucket_name(rec.get("resource") or "")) + ref)
+                off += len(line)
+            for ext, lines in ((".uidx", uidx), (".ridx", ridx)):
+                with open(self.seg_path(seg, ext), "a", encoding="utf-8") as f:
+                    f.write("".join(lines))
+                    f.flush()
+                    if sync:
+                        os.fsync(f.fileno())
+
+    def lookup(self, kind: str, value: str, start_ms: int | None = None, end_ms: int | None = None):
+        """Records whose user id (kind="user") or bucket (kind="resource") is `value`, in key
+        order, through the per-segment index files."""
+        ext, want = self.INDEXES[kind], _idx_key(value)
+        for seg, p in self.segments():
+            if end_ms is not None and seg > end_ms:
+                break
+            if start_ms is not None and seg + HOUR_MS <= start_ms:
+                continue
+            refs, covered = [], 0
+            try:
+                with open(self.seg_path(seg, ext), encoding="utf-8") as f:
+                    for line in f:
+                        parts = line.rstrip("\n").split("\t")
+                        if len(parts) != 3:
+                            continue  # a torn last line
+                        off, ln = int(parts[1]), int(parts[2])
+                        covered = max(covered, off + ln)
+                        if parts[0] == want:
+                            refs.append((off, ln))
+            except OSError:
+                pass
+            with open(p, "rb") as f:
+                for off, ln in refs:
+                    f.seek(off)
+                    r = _parse_line(f.read(ln))
+                    if r is not None and _in_range(r[0], start_ms, end_ms):
+                        yield r
+                f.seek(covered)
+                for raw in f:  # unindexed tail: filter by content
+                    r = _parse_line(raw)
+                    if r is None or not _in_range(r[0], start_ms, end_ms):
+                        continue
+                    field = r[1].get("user_id") if kind == "user" else extract_bucket_name(r[1].get("resource") or "")
+                    if _idx_key(field) == want:
+                        yield r
 
     def last(self) -> tuple[int, dict] | None:
         for _, p in reversed(self.segments()):
@@ -114,22 +178,11 @@ class SegmentStore:
                 break
             if start_ms is not None and seg + HOUR_MS <= start_ms:
                 continue
-            with open(p, encoding="utf-8") as f:
-                for line in f:
-                    line = line.rstrip("\n")
-                    if not line:
-                        continue
-                    try:
-                        ts_s, js = line.split("\t", 1)
-                        ts = int(ts_s)
-                        rec = json.loads(js)
-                    except ValueError:
-                        continue
-                    if start_ms is not None and ts < start_ms:
-                        continue
-                    if end_ms is not None and ts > end_ms:
-                        continue
-                    yield ts, rec
+            with open(p, "rb") as f:
+                for raw in f:
+                    r = _parse_line(raw)
+                    if r is not None and _in_range(r[0], start_ms, end_ms):
+                        yield r
 
     def cleanup(self, retention_days: int, now_ms: int | None = None) -> int:
         now_ms = int(time.time() * 1000) if now_ms is None else now_ms
@@ -138,8 +191,33 @@ class SegmentStore:
         for seg, p in self.segments():
             if seg + HOUR_MS <= cutoff:
                 os.unlink(p)
+                for ext in self.INDEXES.values():
+                    try:
+                        os.unlink(self.seg_path(seg, ext))
+                    except FileNotFoundError:
+                        pass
                 n += 1
         return n
+
+
+def _idx_key(v) -> str:
+    # index keys are single tab/newline-free tokens
+    return str(v or "").replace("\t", " ").replace("\n", " ")
+
+
+def _parse_line(raw: bytes):
+    line = raw.decode("utf-8", errors="replace").rstrip("\n")
+    if not line:
+        return None
+    try:
+        ts_s, js = line.split("\t", 1)
+        return int(ts_s), json.loads(js)
+    except ValueError:
+        return None
+
+
+def _in_range(ts: int, start_ms: int | None, end_ms: int | None) -> bool:
+    return (start_ms is None or ts >= start_ms) and (end_ms is None or ts <= end_ms)
 
 
 class AuditLogger:
@@ -297,7 +375,13 @@ def reader_main(argv: list[str] | None = None) -> int:
     count = 0
     if not a.json:
         print(f"{'TIMESTAMP':<32} {'USER':<20} {'ACTION':<22} {'STATUS':<6} RESOURCE")
-    for _, rec in store.scan(start, end):
+    if a.user:
+        source = store.lookup("user", a.user, start, end)
+    elif a.resource and ":" not in a.resource and "/" not in a.resource:
+        source = store.lookup("resource", a.resource, start, end)
+    else:
+        source = store.scan(start, end)
+    for _, rec in source:
         if a.user and rec.get("user_id") != a.user:
             continue
         if a.resource and extract_bucket_name(rec.get("resource", "")) != a.resource and \
