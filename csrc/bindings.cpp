@@ -282,6 +282,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("flush", &ChunkStore::flush, py::call_guard<py::gil_scoped_release>())
       .def("drop_resident", &ChunkStore::drop_resident, py::call_guard<py::gil_scoped_release>())
       .def("debug_corrupt", &ChunkStore::debug_corrupt, py::call_guard<py::gil_scoped_release>())
+      .def("debug_pause_spill", &ChunkStore::debug_pause_spill, py::call_guard<py::gil_scoped_release>())
       .def("stats", [](ChunkStore& s) {
         StoreStats t = s.stats();
         py::dict d;

@@ -1272,7 +1272,7 @@ void ChunkStore::spill_worker() {
     const uint8_t* d = nullptr;
     {
       std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || !spill_q_.empty(); });
+      cv_.wait(lk, [&] { return stop_ || (!spill_paused_ && !spill_q_.empty()); });
       if (stop_ && spill_q_.empty()) return;
       id = spill_q_.front();
       spill_q_.pop_front();
@@ -1288,8 +1288,11 @@ void ChunkStore::spill_worker() {
     ensure_hscratch(l, S * 4 + 16);
     uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
     bool ok = true;
-    std::string dp = data_path(id, false);
-    int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    // private temporary names, renamed into place once both are durable: a crash mid-spill
+    // leaves only .tmp files (removed by scan_dirs), never a torn block under its real name
+    const std::string tmp_sfx = "." + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
+    const std::string dp_tmp = data_path(id, false) + tmp_sfx, mp_tmp = meta_path(id, false) + tmp_sfx;
+    int fd = ::open(dp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
     ok = fd >= 0;
     uint64_t nch = (size + kChunk - 1) / kChunk;
     for (uint64_t c = 0; ok && c < nch; ++c) {
@@ -1308,14 +1311,22 @@ void ChunkStore::spill_worker() {
     }
     int mfd = -1;
     if (ok) {
-      std::string mp = meta_path(id, false);
-      mfd = ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      mfd = ::open(mp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
       ok = mfd >= 0 && write_all(mfd, hmeta, S * 4, 0);
     }
     if (ok) ok = make_durable(fd, mfd, false);
     if (ok && cfg_.sync_writes) drop_cached(fd);
     if (fd >= 0) ::close(fd);
     if (mfd >= 0) ::close(mfd);
+    // .meta first: a crash between the renames leaves a .meta with no data file, which
+    // scan_dirs ignores (the block reads as missing, never as torn data)
+    if (ok && (::rename(mp_tmp.c_str(), meta_path(id, false).c_str()) != 0 ||
+               ::rename(dp_tmp.c_str(), data_path(id, false).c_str()) != 0))
+      ok = false;
+    if (!ok) {
+      ::unlink(dp_tmp.c_str());
+      ::unlink(mp_tmp.c_str());
+    }
     release_lane(l);
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -1335,6 +1346,14 @@ void ChunkStore::spill_worker() {
 }
 
 // ---------------------------------------------------------------- misc ops
+void ChunkStore::debug_pause_spill(bool on) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    spill_paused_ = on;
+  }
+  cv_.notify_all();
+}
+
 bool ChunkStore::exists(const std::string& id) {
   std::lock_guard<std::mutex> g(mu_);
   return index_.count(id) > 0;

@@ -149,6 +149,7 @@ class ChunkStore {
   void flush();          // wait until no dirty blocks remain
   void drop_resident();  // evict every clean resident block (tests / memory pressure)
   bool debug_corrupt(const std::string& id, uint64_t offset);  // flip a byte everywhere
+  void debug_pause_spill(bool on);  // hbm-ack crash tests: hold dirty blocks in HBM only
 
   // ---- replication engine hooks (RCCL receive / send) ----
   DevExtent reserve(uint64_t n);
@@ -262,6 +263,7 @@ class ChunkStore {
   std::mutex lane_mu_;
   std::condition_variable lane_cv_;
   std::deque<std::string> spill_q_;
+  bool spill_paused_ = false;  // mu_
   std::vector<std::thread> spillers_;
   bool stop_ = false;
   StoreStats st_;

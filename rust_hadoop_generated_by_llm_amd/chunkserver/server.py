@@ -292,6 +292,9 @@ class ChunkServerProcess:
                         body = json.dumps({"corrupted": bool(ok)}).encode()
                     elif u.path == "/debug/scrub":
                         body = json.dumps({"bad": proc.cs.scrub_once()}).encode()
+                    elif u.path == "/debug/pause_spill":
+                        proc.store.debug_pause_spill(q.get("on", "1") == "1")
+                        body = b"{}"
                     elif u.path == "/debug/drop_resident":
                         proc.store.drop_resident(q["block"])
                         body = b"{}"

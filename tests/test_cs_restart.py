@@ -6,6 +6,7 @@ not served.
 CPU twin of the restart/rescan rules: tests/test_wal_store_cpu.py::test_restart_rescans_directories."""
 import json
 import os
+import time
 import urllib.request
 
 import pytest
@@ -84,3 +85,47 @@ def test_gpu_chunkserver_crash_restart_fsync():
 def test_host_chunkserver_crash_restart_fsync():
     with LocalCluster(n_chunkservers=1, fsync=True, durability="nvme-sync") as cl:
         crash_restart(cl, gpu=False)
+
+
+@pytest.mark.gpu
+def test_gpu_hbm_ack_crash_semantics():
+    """hbm-ack acknowledges once the block is checksummed in HBM and spills to NVMe behind
+    the ack (SURVEY §5.4). Pinned here: blocks whose spill finished survive a SIGKILL;
+    blocks acked but not yet spilled are gone after it — reported missing, never served
+    torn — and the spill leaves no partial file under a block's real name."""
+    from rust_hadoop_generated_by_llm_amd import native
+
+    if native.gpu_count() < 1:
+        pytest.fail("GPU test selected but no HIP device is visible")
+    with LocalCluster(gpus=[0], fsync=True, durability="hbm-ack", hbm_capacity="2G",
+                      env={"DFS_DEBUG_ENDPOINTS": "1"}) as cl:
+        c = cl.client(initial_backoff_ms=50, max_retries=2)
+        spilled = {f"/ack/s{i}": os.urandom((1 << 20) + 3 * i) for i in range(4)}
+        for p, d in spilled.items():
+            c.create_file_from_buffer(d, p)
+        deadline = time.time() + 30
+        while stats(cl)["dirty_blocks"] > 0:  # spill drained: these are durable now
+            assert time.time() < deadline, "spill never drained"
+            time.sleep(0.05)
+        urllib.request.urlopen(f"{cl.cs_http[0]}/debug/pause_spill?on=1").read()
+        held = {f"/ack/h{i}": os.urandom((1 << 20) + 5 * i) for i in range(4)}
+        for p, d in held.items():
+            c.create_file_from_buffer(d, p)  # acked from HBM
+            assert c.get_file_content(p) == d
+        assert stats(cl)["dirty_blocks"] >= len(held)
+        held_ids = [c.get_file_info(p).blocks[0].block_id for p in held]
+        c.close()
+
+        cl.restart("cs0")
+        cl.wait_registered()
+        names = {n for _, _, fs in os.walk(cl.base / "cs0") for n in fs}
+        assert not any(n.endswith(".tmp") for n in names)
+        assert not any(b in names for b in held_ids)
+        c = cl.client(initial_backoff_ms=50, max_retries=2)
+        for p, d in spilled.items():
+            assert c.get_file_content(p) == d
+        for p in held:
+            with pytest.raises(DfsError):
+                c.get_file_content(p)
+        assert stats(cl)["crc_mismatches"] == 0
+        c.close()
