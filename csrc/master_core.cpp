@@ -57,6 +57,18 @@ pb::BlockInfo block_from(const Json& d) {
   return b;
 }
 
+Json attrs_json(const std::map<std::string, std::string>& a) {
+  Json o = Json::object();
+  for (auto& kv : a) o.set(kv.first, kv.second);
+  return o;
+}
+
+void attrs_from(const Json& j, std::map<std::string, std::string>* out) {
+  if (!j.is_object()) return;
+  out->clear();
+  for (auto& kv : j.fields()) (*out)[kv.first] = kv.second.str();
+}
+
 Json file_json(const pb::FileMetadata& m) {
   Json d = Json::object();
   d.set("path", m.path);
@@ -71,6 +83,7 @@ Json file_json(const pb::FileMetadata& m) {
   Json bl = Json::array();
   for (auto& b : m.blocks) bl.push_back(block_json(b));
   d.set("blocks", bl);
+  if (!m.attributes.empty()) d.set("attributes", attrs_json(m.attributes));  // absent: reference layout
   return d;
 }
 
@@ -86,6 +99,7 @@ pb::FileMetadata file_from(const Json& d) {
   m.access_count = d["access_count"].as_u64();
   m.moved_to_cold_at_ms = d["moved_to_cold_at_ms"].as_u64();
   for (auto& b : d["blocks"].items()) m.blocks.push_back(block_from(b));
+  attrs_from(d["attributes"], &m.attributes);
   return m;
 }
 
@@ -344,6 +358,7 @@ Json MasterCore::apply_one(const std::string& name, const Json& a) {
     m.size = a["size"].as_u64();
     if (!a["etag_md5"].str().empty()) m.etag_md5 = a["etag_md5"].str();
     if (a["created_at_ms"].as_u64()) m.created_at_ms = a["created_at_ms"].as_u64();
+    attrs_from(a["attributes"], &m.attributes);
     const Json& sums = a["block_checksums"];
     if (sums.size()) {
       for (auto& s : sums.items())
@@ -1145,6 +1160,7 @@ int MasterCore::complete_file(const std::string& raw, std::string* out) {
                    {"etag_md5", r.etag_md5.empty() ? Json() : Json(r.etag_md5)},
                    {"created_at_ms", r.created_at_ms ? Json(r.created_at_ms) : Json()},
                    {"block_checksums", sums}});
+  if (!r.attributes.empty()) args.set("attributes", attrs_json(r.attributes));
   pb::CompleteFileResponse resp;
   auto not_leader = [&](const std::string& hint) {
     // CompleteFileResponse has no leader_hint: the read-path status makes clients follow it

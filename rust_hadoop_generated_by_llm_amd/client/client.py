@@ -360,9 +360,10 @@ class Client:
             self._gens[alloc.block.block_id] = gen
         return alloc
 
-    def _complete(self, dest: str, size: int, etag: str, sums: list, alloc=None) -> None:
+    def _complete(self, dest: str, size: int, etag: str, sums: list, alloc=None,
+                  attributes: dict | None = None) -> None:
         req = pb.CompleteFileRequest(path=dest, size=size, etag_md5=etag, created_at_ms=int(time.time() * 1000),
-                                     block_checksums=sums)
+                                     block_checksums=sums, attributes=attributes or {})
         if alloc is not None:
             req.writer_generation = self._gens.pop(alloc.block.block_id, 0)
         if alloc is not None and alloc.block.block_id in self._deferred:
@@ -379,10 +380,13 @@ class Client:
     def _cs(self, addr: str) -> str:
         return self.resolve_url(with_scheme(addr, self.tls))
 
-    def create_file_from_buffer(self, data: bytes, dest: str) -> int:
+    def create_file_from_buffer(self, data: bytes, dest: str, attributes: dict | None = None,
+                                etag: str | None = None) -> int:
         """CreateFile -> AllocateBlock -> WriteBlock(chain) -> CompleteFile. Returns
-        replicas_written (reference mod.rs:225-494)."""
-        fc = self._fast
+        replicas_written (reference mod.rs:225-494). Extensions: `attributes` are stored in
+        FileMetadata.attributes by the same CompleteFile; `etag` is the caller's MD5 hex of
+        `data` (skips recomputing it)."""
+        fc = self._fast if not attributes else None
         if fc is not None:
             st, replicas, msg, times = fc.write(dest, data, current_request_id.get())
             if st == 0:
@@ -398,7 +402,7 @@ class Client:
         # MD5 is a strictly sequential chain (~1.5 ms per MiB on one core) and only needed
         # by CompleteFile: start it first so it overlaps the create RPC, the CRC and the
         # block transfer (hashlib and the native CRC both release the GIL).
-        md5_fut = self._exec.submit(lambda: hashlib.md5(data).hexdigest())
+        md5_fut = self._exec.submit(lambda: etag or hashlib.md5(data).hexdigest())
         crc = crcops.crc32(data)  # PCLMUL, ~50 us/MiB: cheaper inline than a pool hand-off
         t = self._phase("crc", t)
         alloc = self._create_and_allocate(dest)
@@ -450,14 +454,14 @@ class Client:
             except grpc.RpcError as e:
                 raise DfsError(f"Failed to write block: {rpc_details(e)}") from e
         t = self._phase("write", t)
-        etag = md5_fut.result()
+        md5 = md5_fut.result()
         t = self._phase("md5_wait", t)
         if not resp.success:
             raise DfsError(f"Failed to write block: {resp.error_message}")
         if resp.replicas_written < len(servers):
             log.warning("block written to %d/%d replicas", resp.replicas_written, len(servers))
-        self._complete(dest, len(data), etag, [pb.BlockChecksumInfo(block_id=block.block_id, checksum_crc32c=crc,
-                                                                    actual_size=len(data))], alloc)
+        self._complete(dest, len(data), md5, [pb.BlockChecksumInfo(block_id=block.block_id, checksum_crc32c=crc,
+                                                                    actual_size=len(data))], alloc, attributes)
         self._phase("complete", t)
         return resp.replicas_written
 
@@ -588,8 +592,10 @@ class Client:
             return self.read_ec_block(block)
         return self.read_block_range(block.locations, block.block_id, size_hint=block.size or None)
 
-    def get_file_content(self, path: str) -> bytes:
-        fc = self._fast
+    def get_file_content(self, path: str, info=None) -> bytes:
+        """`info`: the file's FileMetadata when the caller already fetched it (no second
+        GetFileInfo)."""
+        fc = self._fast if info is None else None
         if fc is not None:
             st, data, msg, times = fc.read(path, current_request_id.get())
             if st == 0:
@@ -601,7 +607,7 @@ class Client:
             if st == 2:
                 raise DfsError(msg)
         t = time.perf_counter()
-        meta = self.get_file_info(path)
+        meta = info if info is not None else self.get_file_info(path)
         t = self._phase("getinfo", t)
         if meta is None:
             raise DfsError("File not found")
@@ -623,8 +629,8 @@ class Client:
 
     get_file_concurrent = get_file
 
-    def read_file_range(self, path: str, offset: int, length: int) -> bytes:
-        meta = self.get_file_info(path)
+    def read_file_range(self, path: str, offset: int, length: int, info=None) -> bytes:
+        meta = info if info is not None else self.get_file_info(path)
         if meta is None:
             raise DfsError("File not found")
         if offset >= meta.size:

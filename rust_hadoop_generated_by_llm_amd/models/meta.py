@@ -29,6 +29,8 @@ def block_from_dict(d: dict):
 def file_to_dict(m) -> dict:
     d = {f: getattr(m, f) for f in _FILE_FIELDS}
     d["blocks"] = [block_to_dict(b) for b in m.blocks]
+    if m.attributes:  # extension; absent keeps the reference layout
+        d["attributes"] = dict(m.attributes)
     return d
 
 
@@ -36,6 +38,7 @@ def file_from_dict(d: dict):
     m = pb.FileMetadata(**{f: d[f] for f in _FILE_FIELDS if f in d and d[f] is not None})
     for b in d.get("blocks", []):
         m.blocks.append(block_from_dict(b))
+    m.attributes.update(d.get("attributes") or {})
     return m
 
 

@@ -5,12 +5,17 @@ state.rs}. Path-style addressing only (``/{bucket}/{key}``) and the same on-DFS 
 data written through either implementation is readable by the other:
 
 * bucket = marker file ``/{bucket}/.s3keep``; bucket policy = ``/{bucket}/.s3_bucket_policy``;
-* object = DFS file ``/{bucket}/{key}`` + sidecar ``/{bucket}/{key}.meta`` holding
-  ``{"headers": {"ETag": ..., "x-amz-meta-*": ..., "x-amz-sse-encrypted-dek": ...}}``;
-* multipart upload = ``/.s3_mpu/{uploadId}/{n}`` + ``{n}.etag``; completion renames
-  parts to ``/{bucket}/{key}/{n}`` (cross-shard renames go through the masters' 2PC),
-  writes ``/{bucket}/{key}/.s3_mpu_completed`` and the sidecar with ETag
-  ``md5(concat(part md5s))-N``.
+* object = DFS file ``/{bucket}/{key}``; its headers (``ETag``, ``Content-Type``,
+  ``x-amz-meta-*``, ``x-amz-sse-encrypted-dek``) travel in the same CompleteFile as
+  ``FileMetadata.attributes`` (extension field), so a PUT is one DFS file write and a GET
+  one GetFileInfo + one read. The reference keeps them in a sidecar file
+  ``/{bucket}/{key}.meta`` (``{"headers": {...}}``): sidecars are still READ when an object
+  has no attributes (data written by the reference), and ``S3_METADATA_SIDECAR=true`` also
+  WRITES them, for a bucket the reference gateway must read back;
+* multipart upload = ``/.s3_mpu/{uploadId}/{n}`` (part ETag = the part file's etag_md5);
+  completion renames parts to ``/{bucket}/{key}/{n}`` (cross-shard renames go through the
+  masters' 2PC) and writes ``/{bucket}/{key}/.s3_mpu_completed`` carrying the object
+  attributes, ETag ``md5(concat(part md5s))-N``.
 
 Deliberate fixes over the reference (each noted at its site): Range GETs learn the size
 from ``GetFileInfo`` instead of downloading the whole object; suffix ranges
@@ -31,7 +36,12 @@ import hashlib
 import json
 import logging
 import os
+import shutil
+import signal
+import socket
 import ssl
+import tempfile
+import threading
 import time
 import uuid
 from concurrent.futures import ThreadPoolExecutor
@@ -132,6 +142,7 @@ class S3Config:
         self.tls_cert = env.get("TLS_CERT")
         self.tls_key = env.get("TLS_KEY")
         self.local_chunkserver = env.get("LOCAL_CHUNKSERVER")
+        self.metadata_sidecar = env.get("S3_METADATA_SIDECAR", "") == "true"
 
 
 class _AuthOk:
@@ -599,14 +610,21 @@ class S3Gateway:
         return self.empty(204)
 
     # ------------------------------------------------------------------ objects
-    def _put_replace(self, data: bytes, path: str) -> None:
+    def _put_replace(self, data: bytes, path: str, attributes: dict | None = None, md5: str | None = None) -> None:
         try:
-            self.client.create_file_from_buffer(data, path)
+            self.client.create_file_from_buffer(data, path, attributes, md5)
         except DfsError as e:
             if "already exists" not in str(e):
                 raise
             self.client.delete_file(path)
-            self.client.create_file_from_buffer(data, path)
+            self.client.create_file_from_buffer(data, path, attributes, md5)
+
+    def _put_object_file(self, data: bytes, path: str, headers: dict, md5: str | None = None) -> None:
+        """The object file with its headers as attributes (+ the reference's sidecar when
+        S3_METADATA_SIDECAR=true)."""
+        self._put_replace(data, path, headers, md5)
+        if self.cfg.metadata_sidecar:
+            self._write_meta(path, headers)
 
     def _write_meta(self, path: str, headers: dict) -> None:
         meta = json.dumps({"headers": headers}, separators=(",", ":")).encode()
@@ -615,6 +633,16 @@ class S3Gateway:
             self.client.create_file_from_buffer(meta, path + ".meta")
         except DfsError as e:
             log.warning("failed to write object metadata for %s: %s", path, e)
+
+    def _meta_of(self, path: str, info) -> dict:
+        """Object headers: the file's attributes, else the reference's sidecar."""
+        if info is not None and info.attributes:
+            return dict(info.attributes)
+        return self._read_meta(path)
+
+    def _mpu_marker_meta(self, path: str) -> dict:
+        info = self.client.get_file_info(path + "/.s3_mpu_completed")
+        return self._meta_of(path, info) if info is not None else {}
 
     def _read_meta(self, path: str) -> dict:
         try:
@@ -626,13 +654,12 @@ class S3Gateway:
 
     async def put_object(self, bucket: str, key: str, body: bytes, headers) -> web.Response:
         path = f"/{bucket}/{key}"
-        etag_fut = self.run(lambda: f'"{hashlib.md5(body).hexdigest()}"')
+        md5 = await self.run(lambda: hashlib.md5(body).hexdigest())  # GIL released while hashing
+        etag = f'"{md5}"'
         dek = None
         data = body
         if self.sse is not None:
             data, dek = await self.run(self.sse.encrypt_object, body)
-        await self.run(self._put_replace, data, path)
-        etag = await etag_fut
         meta = {"ETag": etag}
         for k, v in headers.items():
             lk = k.lower()
@@ -642,7 +669,8 @@ class S3Gateway:
             meta["Content-Type"] = headers["Content-Type"]
         if dek is not None:
             meta["x-amz-sse-encrypted-dek"] = dek
-        await self.run(self._write_meta, path, meta)
+        # the stored bytes' MD5 is the client's etag_md5: ours when they are the plaintext
+        await self.run(self._put_object_file, data, path, meta, None if dek is not None else md5)
         out = {"ETag": etag}
         if dek is not None:
             out["x-amz-server-side-encryption"] = "AES256"
@@ -696,10 +724,9 @@ class S3Gateway:
     async def get_object(self, bucket: str, key: str, req_headers) -> web.Response:
         path = f"/{bucket}/{key}"
         info = await self.run(self.client.get_file_info, path)
-        meta_fut = asyncio.ensure_future(self.run(self._read_meta, path))
         if info is None:
             parts = await self.run(self._mpu_parts, path)
-            meta = await meta_fut
+            meta = await self.run(self._mpu_marker_meta, path) if parts is not None else {}
             if parts is None:
                 return self.xml(404, X.error("NoSuchKey", "The specified key does not exist.", path))
             headers, dek = self._object_headers(meta, None)
@@ -713,22 +740,23 @@ class S3Gateway:
         size = int(info.size)
         rng_hdr = req_headers.get("Range")
         rng = parse_range(rng_hdr, size)
-        # Speculatively start the (range) read while the sidecar loads; an SSE object
-        # needs the whole ciphertext, which is fetched below once the DEK is known.
+        # Start the (range) read at once (with the metadata just fetched, no second
+        # GetFileInfo); an SSE object needs the whole ciphertext, fetched below once the
+        # DEK is known. Objects without attributes load the reference's sidecar meanwhile.
         if isinstance(rng, tuple):
             s, e = rng
-            data_fut = asyncio.ensure_future(self.run(self.client.read_file_range, path, s, e - s + 1))
+            data_fut = asyncio.ensure_future(self.run(self.client.read_file_range, path, s, e - s + 1, info))
         elif rng is None and size > 0:
-            data_fut = asyncio.ensure_future(self.run(self.client.get_file_content, path))
+            data_fut = asyncio.ensure_future(self.run(self.client.get_file_content, path, info))
         else:
             data_fut = None
-        meta = await meta_fut
+        meta = dict(info.attributes) if info.attributes else await self.run(self._read_meta, path)
         headers, dek = self._object_headers(meta, info)
         if dek is not None and self.sse is not None:
             if data_fut is not None:
                 data_fut.cancel()
             try:
-                raw = await self.run(self.client.get_file_content, path)
+                raw = await self.run(self.client.get_file_content, path, info)
                 plain = await self.run(self._decrypt, raw, dek)
             except AuthError:
                 return self.s3_error(500, "InternalError", "SSE decryption failed")
@@ -744,12 +772,11 @@ class S3Gateway:
 
     async def head_object(self, bucket: str, key: str) -> web.Response:
         path = f"/{bucket}/{key}"
-        info_fut = self.run(self.client.get_file_info, path)
-        meta_fut = self.run(self._read_meta, path)
-        info, meta = await asyncio.gather(info_fut, meta_fut)
+        info = await self.run(self.client.get_file_info, path)
         if info is None:
             parts = await self.run(self._mpu_parts, path)
             if parts is not None:
+                meta = await self.run(self._mpu_marker_meta, path)
                 headers, _ = self._object_headers(meta, None)
                 headers["Last-Modified"] = formatdate(usegmt=True)
                 headers["Content-Length"] = str(meta.get("x-dfs-mpu-size", 0))
@@ -757,6 +784,7 @@ class S3Gateway:
             if path.endswith("/") and await self.run(self.client.list_all_files, path):
                 return self.empty(200, {"Content-Length": "0"})
             return self.empty(404)
+        meta = await self.run(self._meta_of, path, info)
         headers, _ = self._object_headers(meta, info)
         headers["Content-Length"] = str(info.size)
         return self.empty(200, headers)
@@ -805,13 +833,15 @@ class S3Gateway:
 
         def load_source():
             info = self.client.get_file_info(src_path)
-            meta = self._read_meta(src_path)
-            dek = meta.get("x-amz-sse-encrypted-dek")
             if info is not None:
-                return self._decrypt(self.client.get_file_content(src_path), dek), meta
+                meta = self._meta_of(src_path, info)
+                dek = meta.get("x-amz-sse-encrypted-dek")
+                return self._decrypt(self.client.get_file_content(src_path, info), dek), meta
             parts = self._mpu_parts(src_path)
             if parts is None:
-                return None, meta
+                return None, {}
+            meta = self._mpu_marker_meta(src_path)
+            dek = meta.get("x-amz-sse-encrypted-dek")
             return b"".join(self._decrypt(self.client.get_file_content(p), dek) for _, p in parts), meta
         try:
             data, src_meta = await self.run(load_source)
@@ -819,12 +849,12 @@ class S3Gateway:
             return self.s3_error(500, "InternalError", "SSE decryption failed")
         if data is None:
             return self.xml(404, X.error("NoSuchKey", "The specified key does not exist.", src_path))
-        etag = f'"{hashlib.md5(data).hexdigest()}"'
+        md5 = await self.run(lambda: hashlib.md5(data).hexdigest())
+        etag = f'"{md5}"'
         dek = None
         payload = data
         if self.sse is not None:
             payload, dek = await self.run(self.sse.encrypt_object, data)
-        await self.run(self._put_replace, payload, dest)
         meta = {"ETag": etag}
         if req_headers.get("x-amz-metadata-directive", "COPY").upper() == "REPLACE":
             meta.update({k.lower(): v for k, v in req_headers.items() if k.lower().startswith("x-amz-meta-")})
@@ -832,7 +862,7 @@ class S3Gateway:
             meta.update({k: v for k, v in src_meta.items() if k.startswith("x-amz-meta-") or k == "Content-Type"})
         if dek is not None:
             meta["x-amz-sse-encrypted-dek"] = dek
-        await self.run(self._write_meta, dest, meta)
+        await self.run(self._put_object_file, payload, dest, meta, None if dek is not None else md5)
         return self.xml(200, X.copy_object(datetime.now(timezone.utc).isoformat(), etag))
 
     # ------------------------------------------------------------------ listings
@@ -891,7 +921,7 @@ class S3Gateway:
         def describe(k: str) -> dict:
             p = entries[k]
             if p is None:
-                meta = self._read_meta(bp + k)
+                meta = self._mpu_marker_meta(bp + k)
                 return {"key": k, "last_modified": DEFAULT_DATE, "etag": meta.get("ETag", '"000-MPU"'),
                         "size": int(meta.get("x-dfs-mpu-size", 0))}
             info = self.client.get_file_info(p)
@@ -902,7 +932,9 @@ class S3Gateway:
                 if info.etag_md5:
                     etag = f'"{info.etag_md5}"'
                 lm = _iso_ms(info.created_at_ms)
-            if p + ".meta" in fileset:
+            if info is not None and info.attributes:
+                etag = info.attributes.get("ETag", etag)
+            elif p + ".meta" in fileset:
                 meta = self._read_meta(p)
                 etag = meta.get("ETag", etag)
             return {"key": k, "last_modified": lm, "etag": etag, "size": size}
@@ -924,13 +956,9 @@ class S3Gateway:
         if not await self.run(self.client.exists, f"{MPU_ROOT}/{upload_id}/.s3keep"):
             return self.xml(404, X.error("NoSuchUpload", "The specified upload does not exist.", upload_id))
         part = f"{MPU_ROOT}/{upload_id}/{n}"
-        etag = f'"{hashlib.md5(body).hexdigest()}"'
-
-        def work():
-            self._put_replace(body, part)
-            self._put_replace(etag.encode(), part + ".etag")
-        await self.run(work)
-        return self.empty(200, {"ETag": etag})
+        md5 = await self.run(lambda: hashlib.md5(body).hexdigest())
+        await self.run(self._put_replace, body, part, None, md5)  # part ETag = its etag_md5
+        return self.empty(200, {"ETag": f'"{md5}"'})
 
     async def complete_mpu(self, bucket: str, key: str, upload_id: str, body: bytes) -> web.Response:
         mpu_dir = f"{MPU_ROOT}/{upload_id}"
@@ -945,10 +973,12 @@ class S3Gateway:
             if mpu_dir + "/.s3keep" not in files:
                 return "nosuchupload"
             have: dict[int, str] = {}
-            for f in files:
-                name = f[len(mpu_dir) + 1:]
-                if name.endswith(".etag") and name[:-5].isdigit():
-                    have[int(name[:-5])] = self.client.get_file_content(f).decode().strip()
+            sizes: dict[int, int] = {}
+            part_files = [f for f in files if f[len(mpu_dir) + 1:].isdigit()]
+            for f, info in zip(part_files, self.client._exec.map(self.client.get_file_info, part_files)):
+                if info is not None:
+                    n = int(f[len(mpu_dir) + 1:])
+                    have[n], sizes[n] = f'"{info.etag_md5}"', int(info.size)
             if requested:
                 nums = []
                 for num, et in requested:
@@ -961,22 +991,21 @@ class S3Gateway:
                 nums = sorted(have)
             md5s = b"".join(bytes.fromhex(have[n].strip('"')) for n in nums)
             final_etag = f'"{hashlib.md5(md5s).hexdigest()}-{len(nums)}"'
-            total = 0
-            for n in nums:
-                info = self.client.get_file_info(f"{mpu_dir}/{n}")
-                total += int(info.size) if info is not None else 0
+            total = sum(sizes[n] for n in nums)
+            meta = {"ETag": final_etag, "x-dfs-mpu-size": str(total)}
             # replace whatever object was at the destination (plain file or older MPU)
             self._delete_quiet(dest)
             for f in self.client.list_all_files(dest + "/"):
                 self._delete_quiet(f)
-            self.client.create_file_from_buffer(b"", dest + "/.s3_mpu_completed")
+            self.client.create_file_from_buffer(b"", dest + "/.s3_mpu_completed", meta)
             for n in nums:
                 self.client.rename_file(f"{mpu_dir}/{n}", f"{dest}/{n}")
             for f in files:
                 if f.endswith(".etag") or f == mpu_dir + "/.s3keep" or \
                         (f[len(mpu_dir) + 1:].isdigit() and int(f[len(mpu_dir) + 1:]) not in nums):
                     self._delete_quiet(f)
-            self._write_meta(dest, {"ETag": final_etag, "x-dfs-mpu-size": str(total)})
+            if self.cfg.metadata_sidecar:
+                self._write_meta(dest, meta)
             return final_etag
         res = await self.run(work)
         if res == "nosuchupload":
@@ -996,7 +1025,44 @@ class S3Gateway:
 
 
 # ---------------------------------------------------------------------------- main
-def build_gateway(cfg: S3Config, client: Client | None = None) -> S3Gateway:
+class ForwardingAudit:
+    """Audit sink of gateway worker processes 1..N-1: records go as datagrams over a UNIX
+    socket to worker 0, whose AuditLogger owns the store, so one hash chain covers every
+    worker. Like AuditLogger.log it never blocks: a full socket counts a drop."""
+
+    def __init__(self, path: str, registry: Registry):
+        self.path = path
+        self.sock = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
+        self.sock.setblocking(False)
+        self.m_dropped = registry.counter("audit_log_dropped_total",
+                                          "Total number of audit logs dropped due to full buffer")
+
+    def log(self, rec: dict) -> None:
+        try:
+            self.sock.sendto(json.dumps(rec, separators=(",", ":")).encode(), self.path)
+        except OSError:
+            self.m_dropped.inc()
+
+    def flush(self, timeout: float = 10.0) -> bool:
+        return True
+
+    def close(self) -> None:
+        self.sock.close()
+
+
+def _audit_ingest(sock: socket.socket, audit: AuditLogger) -> None:
+    while True:
+        try:
+            data = sock.recv(1 << 16)
+        except OSError:
+            return
+        try:
+            audit.log(json.loads(data))
+        except ValueError:
+            log.warning("malformed audit datagram dropped")
+
+
+def build_gateway(cfg: S3Config, client: Client | None = None, audit_sink=None) -> S3Gateway:
     if client is None:
         client = Client([cfg.master_addr], cfg.config_servers, ca_cert=cfg.ca_cert, domain_name=cfg.domain_name,
                         local_chunkserver=cfg.local_chunkserver)
@@ -1013,7 +1079,9 @@ def build_gateway(cfg: S3Config, client: Client | None = None) -> S3Gateway:
         except (OSError, ValueError, KeyError) as e:
             log.error("failed to load IAM config %s: %s", cfg.iam_config_path, e)
     audit = None
-    if cfg.audit_enabled:
+    if cfg.audit_enabled and audit_sink is not None:
+        audit = audit_sink(registry)
+    elif cfg.audit_enabled:
         if cfg.audit_hmac_secret and len(cfg.audit_hmac_secret) >= 16:
             audit = AuditLogger(cfg.audit_dir, cfg.audit_retention_days, cfg.audit_batch_size,
                                 cfg.audit_hmac_secret, registry=registry)
@@ -1028,32 +1096,90 @@ def build_gateway(cfg: S3Config, client: Client | None = None) -> S3Gateway:
     return S3Gateway(client, cfg, registry=registry, oidc=oidc, sts=sts, iam=iam, audit=audit, sse=sse)
 
 
+def _die_with_parent() -> None:
+    try:
+        import ctypes
+
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+
+
 def main(argv: list[str] | None = None) -> int:
+    """One listening socket shared by S3_WORKERS processes (default 4), forked before any
+    gRPC channel or thread exists; each runs its own event loop and DFS client, so request
+    handling scales past one interpreter lock. Worker 0 owns the audit store."""
     ap = argparse.ArgumentParser(prog="s3_server", description="S3-compatible gateway over the DFS")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--workers", type=int, default=None)
     a = ap.parse_args(argv)
     logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO"),
                         format="%(asctime)s %(levelname)s %(name)s %(message)s")
     cfg = S3Config()
     if a.port is not None:
         cfg.port = a.port
-    gw = build_gateway(cfg)
+    workers = max(1, a.workers if a.workers is not None else int(os.environ.get("S3_WORKERS", "4") or 4))
+    lsock = socket.socket(socket.AF_INET6 if ":" in a.host else socket.AF_INET, socket.SOCK_STREAM)
+    lsock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    lsock.bind((a.host, cfg.port))
+    lsock.listen(1024)
+    ingest_path = ingest = None
+    if workers > 1 and cfg.audit_enabled:
+        ingest_path = os.path.join(tempfile.mkdtemp(prefix="s3audit-"), "ingest.sock")
+        ingest = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
+        ingest.bind(ingest_path)
+        ingest.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    children = []
+    worker_id = 0
+    for i in range(1, workers):
+        pid = os.fork()
+        if pid == 0:
+            worker_id = i
+            children = []
+            _die_with_parent()
+            if ingest is not None:
+                ingest.close()
+            break
+        children.append(pid)
+    sink = None
+    if worker_id > 0 and ingest_path:
+        sink = lambda reg: ForwardingAudit(ingest_path, reg)  # noqa: E731
+    gw = build_gateway(cfg, audit_sink=sink)
+    if worker_id == 0 and ingest is not None and gw.audit is not None:
+        threading.Thread(target=_audit_ingest, args=(ingest, gw.audit), name="audit-ingest", daemon=True).start()
     ssl_ctx = None
     if cfg.tls_cert and cfg.tls_key:
         ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
         ssl_ctx.load_cert_chain(cfg.tls_cert, cfg.tls_key)
-    log.info("S3 gateway on %s:%d (auth=%s, sse=%s, audit=%s)", a.host, cfg.port, cfg.auth_enabled,
-             gw.sse is not None, gw.audit is not None)
-    ready = os.environ.get("DFS_READY_FILE")
+    if worker_id == 0:
+        log.info("S3 gateway on %s:%d (workers=%d, auth=%s, sse=%s, audit=%s)", a.host, cfg.port, workers,
+                 cfg.auth_enabled, gw.sse is not None, gw.audit is not None)
+    ready = os.environ.get("DFS_READY_FILE") if worker_id == 0 else None
 
     async def on_start(_app):
         if ready:
             with open(ready, "w") as f:
-                json.dump({"port": cfg.port}, f)
+                json.dump({"port": cfg.port, "workers": workers}, f)
     app = gw.app()
     app.on_startup.append(on_start)
-    web.run_app(app, host=a.host, port=cfg.port, ssl_context=ssl_ctx, print=None, access_log=None)
+    try:
+        web.run_app(app, sock=lsock, ssl_context=ssl_ctx, print=None, access_log=None)
+    finally:
+        for pid in children:
+            try:
+                os.kill(pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        for pid in children:
+            try:
+                os.waitpid(pid, 0)
+            except ChildProcessError:
+                pass
+        if ingest_path:
+            shutil.rmtree(os.path.dirname(ingest_path), ignore_errors=True)
+    if worker_id > 0:
+        os._exit(0)
     return 0
 
 

@@ -73,10 +73,20 @@ def test_native_codec_roundtrip(name):
         out = native.pb_roundtrip(name, wire)
         assert out is not None, f"native decode of {name} failed"
         assert cls.FromString(out) == m
-        has_map = any(f.message_type is not None and f.message_type.GetOptions().map_entry
-                      for f in m.DESCRIPTOR.fields)
-        if not has_map:  # canonical encoding: identical bytes
+        if not _has_map(m.DESCRIPTOR):  # canonical encoding: identical bytes (map order is free)
             assert out == wire
+
+
+def _has_map(desc, seen=None) -> bool:
+    seen = set() if seen is None else seen
+    if desc.full_name in seen:
+        return False
+    seen.add(desc.full_name)
+    for f in desc.fields:
+        if f.message_type is not None:
+            if f.message_type.GetOptions().map_entry or _has_map(f.message_type, seen):
+                return True
+    return False
 
 
 def test_native_codec_rejects_truncated_input():

@@ -12,6 +12,7 @@ import asyncio
 import hashlib
 import json
 import os
+import signal
 import threading
 import time
 from datetime import datetime, timedelta, timezone
@@ -126,6 +127,44 @@ def test_object_put_get_head_metadata(gw):
     assert r.status_code == 200 and r.content == b"" and r.headers["ETag"] == md5q(b"")
     assert requests.get(f"{u}/objs/missing").status_code == 404
     assert requests.head(f"{u}/objs/missing").status_code == 404
+
+
+def test_object_headers_live_in_file_attributes(gw, cluster):
+    """Headers ride in FileMetadata.attributes (one DFS write per PUT, no sidecar file);
+    objects the reference gateway wrote (sidecar only) still read back with their headers;
+    S3_METADATA_SIDECAR=true writes the reference layout too."""
+    u = gw.url
+    c = cluster.client()
+    try:
+        requests.put(f"{u}/attrs")
+        body = os.urandom(70_000)
+        r = requests.put(f"{u}/attrs/o", data=body, headers={"x-amz-meta-k": "v", "Content-Type": "text/x"})
+        assert r.status_code == 200
+        info = c.get_file_info("/attrs/o")
+        assert dict(info.attributes) == {"ETag": md5q(body), "x-amz-meta-k": "v", "Content-Type": "text/x"}
+        assert info.etag_md5 == hashlib.md5(body).hexdigest()
+        assert not c.exists("/attrs/o.meta")
+        # a reference-written object: plain file + sidecar
+        c.create_file_from_buffer(b"legacy", "/attrs/legacy")
+        c.create_file_from_buffer(json.dumps({"headers": {"ETag": '"abc"', "x-amz-meta-old": "1"}}).encode(),
+                                  "/attrs/legacy.meta")
+        r = requests.get(f"{u}/attrs/legacy")
+        assert r.content == b"legacy" and r.headers["ETag"] == '"abc"' and r.headers["x-amz-meta-old"] == "1"
+        assert requests.head(f"{u}/attrs/legacy").headers["x-amz-meta-old"] == "1"
+        keys = {e.find("Key").text: e.find("ETag").text
+                for e in X.parse(requests.get(f"{u}/attrs?list-type=2").content).findall("Contents")}
+        assert keys == {"o": md5q(body), "legacy": '"abc"'}
+    finally:
+        c.close()
+    g2 = make_gw(cluster, {"AUDIT_LOG_ENABLED": "false", "S3_METADATA_SIDECAR": "true"})
+    try:
+        requests.put(f"{g2.url}/attrs/compat", data=b"z", headers={"x-amz-meta-a": "b"})
+        c = cluster.client()
+        side = json.loads(c.get_file_content("/attrs/compat.meta"))
+        assert side["headers"]["x-amz-meta-a"] == "b" and c.get_file_info("/attrs/compat").attributes["ETag"]
+        c.close()
+    finally:
+        g2.stop()
 
 
 def test_range_requests(gw):
@@ -606,3 +645,43 @@ def test_gateway_subprocess(cluster):
     assert requests.put(url + "/subproc").status_code == 200
     assert requests.put(url + "/subproc/o", data=b"via process").status_code == 200
     assert requests.get(url + "/subproc/o").content == b"via process"
+
+
+def test_gateway_workers_share_one_audit_chain(cluster, tmp_path):
+    """S3_WORKERS=3: three processes accept on one socket; every worker's audit records
+    reach worker 0's logger, so the store holds ONE verifiable hash chain with all of them."""
+    audit_dir = tmp_path / "audit"
+    url = cluster.start_s3({"S3_WORKERS": "3", "S3_AUTH_ENABLED": "true", "S3_ACCESS_KEY": "admin",
+                            "S3_SECRET_KEY": "admin-secret", "AUDIT_LOG_DIR": str(audit_dir),
+                            "AUDIT_HMAC_SECRET": AUDIT_SECRET, "AUDIT_LOG_BATCH_SIZE": "1"}, name="s3w")
+    pr = next(p for p in cluster.procs if p.name == "s3w")
+    assert pr.info.get("workers") == 3
+    import psutil
+
+    assert len(psutil.Process(pr.popen.pid).children()) == 2
+
+    class G:
+        pass
+
+    g = G()
+    g.url = url
+    assert signed("PUT", g, "/wk").status_code == 200
+    n = 60
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(i):
+        # a fresh connection per request spreads them over the workers
+        return signed("PUT", g, f"/wk/o{i}", body=b"x" * i).status_code
+
+    with ThreadPoolExecutor(6) as ex:
+        assert set(ex.map(one, range(n))) == {200}
+    deadline = time.time() + 20
+    while True:
+        recs = [r for _, r in SegmentStore(str(audit_dir)).scan()]
+        if len(recs) >= n + 1 or time.time() > deadline:
+            break
+        time.sleep(0.2)
+    assert len(recs) == n + 1
+    assert verify_chain(SegmentStore(str(audit_dir)), AUDIT_SECRET) == (n + 1, [])
+    cluster.kill("s3w", signal.SIGTERM)
+    assert not psutil.pid_exists(pr.popen.pid)
