@@ -120,6 +120,38 @@ def config4(a):
 
 
 # ----------------------------------------------------------------------------- config 5
+def _s3_payload(i: int, size: int) -> bytes:
+    import random
+
+    return random.Random(i).randbytes(size)
+
+
+def _s3_load(job):
+    """One load-generator process (a GIL of its own, like one S3 client host): runs its share
+    of the requests back to back over one keep-alive session; returns (start, end, latencies)."""
+    import requests
+
+    op, url, idxs, size, nobj = job
+    s = requests.Session()
+    bodies = {i: _s3_payload(i % nobj, size) for i in idxs} if op == "put" else {}
+    lats = []
+    t_start = time.time()
+    for i in idxs:
+        t0 = time.perf_counter()
+        if op == "put":
+            r = s.put(f"{url}/bench/obj_{i:05d}", data=bodies[i])
+            assert r.status_code == 200 and r.headers["ETag"] == f'"{hashlib.md5(bodies[i]).hexdigest()}"'
+        elif op == "get":
+            r = s.get(f"{url}/bench/obj_{i:05d}")
+            assert r.status_code == 200 and len(r.content) == size
+        else:
+            off = (i * 7919 * 4096) % (size - 65536)
+            r = s.get(f"{url}/bench/obj_{i % nobj:05d}", headers={"Range": f"bytes={off}-{off + 65535}"})
+            assert r.status_code == 206 and len(r.content) == 65536
+        lats.append(time.perf_counter() - t0)
+    return t_start, time.time(), lats
+
+
 def config5(a):
     import requests
 
@@ -132,51 +164,26 @@ def config5(a):
         s = requests.Session()
         assert s.put(f"{url}/bench").status_code == 200
         n, size = a.count, a.size
-        objs = make_payloads(n, size)
+        # concurrency = load-generator PROCESSES (Python threads in one process measured the
+        # client's interpreter lock, not the gateway), spawned before anything is timed
+        import multiprocessing as mp
 
-        def timed(fn, items, conc):
-            lats = []
-            lock = threading.Lock()
+        lg = mp.get_context("spawn").Pool(a.concurrency)
 
-            def one(x):
-                t0 = time.perf_counter()
-                fn(x)
-                with lock:
-                    lats.append(time.perf_counter() - t0)
+        def timed(op, count):
+            jobs = [(op, url, list(range(k, count, a.concurrency)), size, n) for k in range(a.concurrency)]
+            res = lg.map(_s3_load, jobs)
+            return max(r[1] for r in res) - min(r[0] for r in res), [x for r in res for x in r[2]]
 
-            t0 = time.perf_counter()
-            with ThreadPoolExecutor(conc) as ex:
-                list(ex.map(one, items))
-            return time.perf_counter() - t0, lats
-
-        sess = threading.local()
-
-        def http():
-            if not hasattr(sess, "s"):
-                sess.s = requests.Session()
-            return sess.s
-
-        def put(i):
-            r = http().put(f"{url}/bench/obj_{i:05d}", data=objs[i % len(objs)])
-            assert r.status_code == 200 and r.headers["ETag"] == f'"{hashlib.md5(objs[i % len(objs)]).hexdigest()}"'
-
-        def get(i):
-            r = http().get(f"{url}/bench/obj_{i:05d}")
-            assert r.status_code == 200 and len(r.content) == size
-
-        def rng(i):
-            off = (i * 7919 * 4096) % (size - 65536)
-            r = http().get(f"{url}/bench/obj_{i % n:05d}", headers={"Range": f"bytes={off}-{off + 65535}"})
-            assert r.status_code == 206 and len(r.content) == 65536
-
-        el, lat = timed(put, range(n), a.concurrency)
+        lg.starmap(_s3_payload, [(0, 16)] * a.concurrency, chunksize=1)  # workers up before timing
+        el, lat = timed("put", n)
         out["put"] = {"objects": n, "size": size, "mb_per_s": round(n * size / (1 << 20) / el, 1),
                       "p50_ms": pct(lat, 50), "p99_ms": pct(lat, 99)}
-        el, lat = timed(get, range(n), a.concurrency)
+        el, lat = timed("get", n)
         out["get"] = {"objects": n, "size": size, "mb_per_s": round(n * size / (1 << 20) / el, 1),
                       "p50_ms": pct(lat, 50), "p99_ms": pct(lat, 99)}
         m = 4 * n
-        el, lat = timed(rng, range(m), a.concurrency)
+        el, lat = timed("range", m)
         out["range_get_64k"] = {"requests": m, "req_per_s": round(m / el, 1), "p50_ms": pct(lat, 50),
                                 "p99_ms": pct(lat, 99)}
         # multipart upload of one large object, parts in parallel (S3 MPU emulation, handlers.rs:234-432)
@@ -191,7 +198,7 @@ def config5(a):
         etags = {}
 
         def up(k):
-            rr = http().put(f"{url}/bench/big.bin?partNumber={k + 1}&uploadId={upload_id}",
+            rr = requests.put(f"{url}/bench/big.bin?partNumber={k + 1}&uploadId={upload_id}",
                             data=blob[k * part:(k + 1) * part])
             assert rr.status_code == 200
             etags[k + 1] = rr.headers["ETag"]
@@ -210,7 +217,10 @@ def config5(a):
         assert got == blob
         out["multipart"] = {"parts": nparts, "part_size": part, "upload_mb_per_s": round(len(blob) / (1 << 20) / mpu_s, 1),
                             "get_mb_per_s": round(len(blob) / (1 << 20) / mpu_get_s, 1)}
+        lg.close()
         out["parquet_over_s3"] = parquet_phase(url, a)
+        out["load_generator"] = f"{a.concurrency} client processes (requests, keep-alive)"
+        out["gateway_workers"] = int(os.environ.get("S3_WORKERS", "4"))
         emit(out)
 
 

@@ -730,13 +730,15 @@ class S3Gateway:
             if parts is None:
                 return self.xml(404, X.error("NoSuchKey", "The specified key does not exist.", path))
             headers, dek = self._object_headers(meta, None)
-            try:
-                chunks = await asyncio.gather(*[self.run(self.client.get_file_content, p) for _, p in parts])
-                data = b"".join([await self.run(self._decrypt, c, dek) for c in chunks])
-            except AuthError:
-                return self.s3_error(500, "InternalError", "SSE decryption failed")
-            return self._range_response(lambda o, n: data[o:o + n], len(data),
-                                        parse_range(req_headers.get("Range"), len(data)), headers)
+            if dek is not None:
+                try:
+                    chunks = await asyncio.gather(*[self.run(self.client.get_file_content, p) for _, p in parts])
+                    data = b"".join([await self.run(self._decrypt, c, dek) for c in chunks])
+                except AuthError:
+                    return self.s3_error(500, "InternalError", "SSE decryption failed")
+                return self._range_response(lambda o, n: data[o:o + n], len(data),
+                                            parse_range(req_headers.get("Range"), len(data)), headers)
+            return await self._mpu_range(parts, meta, req_headers.get("Range"), headers)
         size = int(info.size)
         rng_hdr = req_headers.get("Range")
         rng = parse_range(rng_hdr, size)
@@ -767,6 +769,31 @@ class S3Gateway:
         body = await data_fut if data_fut is not None else b""
         if isinstance(rng, tuple):
             headers["Content-Range"] = f"bytes {rng[0]}-{rng[1]}/{size}"
+            return web.Response(status=206, body=body, headers=headers)
+        return web.Response(status=200, body=body, headers=headers)
+
+    async def _mpu_range(self, parts, meta: dict, rng_hdr, headers: dict) -> web.Response:
+        """GET (or Range GET) of a multipart object: only the parts overlapping the range are
+        read, each with a ranged read, in parallel (a Parquet footer or column-chunk request
+        touches one part, not the whole object)."""
+        sizes = _mpu_layout(meta, [n for n, _ in parts])
+        if sizes is None:  # completed before the layout attribute existed: ask the master
+            infos = await asyncio.gather(*[self.run(self.client.get_file_info, p) for _, p in parts])
+            sizes = [int(i.size) if i is not None else 0 for i in infos]
+        total = sum(sizes)
+        rng = parse_range(rng_hdr, total)
+        if rng == "unsatisfiable":
+            return self._range_response(None, total, rng, headers)
+        s, e = rng if isinstance(rng, tuple) else (0, total - 1)
+        reads, pos = [], 0
+        for (_, p), sz in zip(parts, sizes):
+            lo, hi = max(s, pos), min(e + 1, pos + sz)
+            if lo < hi:
+                reads.append(self.run(self.client.read_file_range, p, lo - pos, hi - lo))
+            pos += sz
+        body = b"".join(await asyncio.gather(*reads)) if reads else b""
+        if isinstance(rng, tuple):
+            headers["Content-Range"] = f"bytes {s}-{e}/{total}"
             return web.Response(status=206, body=body, headers=headers)
         return web.Response(status=200, body=body, headers=headers)
 
@@ -992,7 +1019,8 @@ class S3Gateway:
             md5s = b"".join(bytes.fromhex(have[n].strip('"')) for n in nums)
             final_etag = f'"{hashlib.md5(md5s).hexdigest()}-{len(nums)}"'
             total = sum(sizes[n] for n in nums)
-            meta = {"ETag": final_etag, "x-dfs-mpu-size": str(total)}
+            meta = {"ETag": final_etag, "x-dfs-mpu-size": str(total),
+                    "x-dfs-mpu-layout": ",".join(f"{n}:{sizes[n]}" for n in nums)}
             # replace whatever object was at the destination (plain file or older MPU)
             self._delete_quiet(dest)
             for f in self.client.list_all_files(dest + "/"):
@@ -1025,6 +1053,18 @@ class S3Gateway:
 
 
 # ---------------------------------------------------------------------------- main
+def _mpu_layout(meta: dict, nums: list[int]) -> list[int] | None:
+    """Part sizes from the completion marker's x-dfs-mpu-layout ("n:size,..."), if it
+    describes exactly these parts."""
+    try:
+        pairs = [tuple(int(x) for x in kv.split(":")) for kv in meta["x-dfs-mpu-layout"].split(",") if kv]
+    except (KeyError, ValueError):
+        return None
+    if [n for n, _ in pairs] != list(nums):
+        return None
+    return [sz for _, sz in pairs]
+
+
 class ForwardingAudit:
     """Audit sink of gateway worker processes 1..N-1: records go as datagrams over a UNIX
     socket to worker 0, whose AuditLogger owns the store, so one hash chain covers every
