@@ -170,7 +170,7 @@ void FastPathServer::stop() {
   lfd_ = -1;
   std::unique_lock<std::mutex> g(mu_);
   for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
-  workers_cv_.wait(g, [this] { return live_workers_ == 0; });
+  workers_cv_.wait(g, [this] { return live_workers_ == 0 && pending_regs_ == 0; });
   for (auto& kv : maps_) {
     if (kv.second.registered) store_->unregister_host(kv.second.p);
     ::munmap(kv.second.p, kv.second.size);
@@ -323,8 +323,24 @@ uint8_t* FastPathServer::map_shm(const std::string& path, uint64_t off, uint64_t
   m.p = static_cast<uint8_t*>(p);
   m.size = static_cast<uint64_t>(sb.st_size);
   // pin the client's arena for the GPU copy engines: blocks then move slot <-> HBM in one
-  // DMA, with no bounce through staging buffers and no CPU memcpy (falls back if refused)
-  m.registered = store_->gpu() && store_->register_host(m.p, m.size);
+  // DMA, with no bounce through staging buffers and no CPU memcpy. Pinning a 256 MiB arena
+  // takes tens of ms, so it runs on its own thread, off mu_: until it lands, this client's
+  // ops take the staged path (store_->host_registered says which) and nobody else waits.
+  if (store_->gpu()) {
+    ++pending_regs_;
+    uint8_t* base = m.p;
+    const uint64_t size = m.size;
+    std::thread([this, base, size] {
+      bool ok = store_->register_host(base, size);
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto& kv : maps_)
+        if (kv.second.p == base) kv.second.registered = ok;
+      for (auto& r : retired_)
+        if (r.p == base) r.registered = ok;
+      --pending_regs_;
+      workers_cv_.notify_all();
+    }).detach();
+  }
   return m.p;
 }
 

@@ -155,6 +155,7 @@ class FastPathServer {
     bool registered = false;  // hipHostRegister'ed for direct DMA
   };
   std::unordered_map<std::string, Mapping> maps_;
+  int pending_regs_ = 0;  // arena registrations in flight (mu_); stop() waits for them
   std::vector<Mapping> retired_;
   std::vector<std::string> suspects_;
   std::vector<std::string> recent_rids_;  // ring of the last kRecentRids request ids (mu_)

@@ -108,6 +108,13 @@ if [ "$STEP" = "grpcab" ]; then
   DFS_CS_GRPC=grpcio timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_grpcio.json 2> gpurun_out/ab_grpcio.err && \
   DFS_CS_GRPC=native timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_native.json 2> gpurun_out/ab_native.err || exit $?
 fi
+if [ "$STEP" = "s3" ]; then
+  # config 5 with the single-process gateway vs the multi-process one (A/B of S3_WORKERS)
+  S3_WORKERS=1 timeout -k 10 400 python bench_configs.py config5 --gpu 0 > gpurun_out/config5_w1.json 2> gpurun_out/config5_w1.err && \
+  S3_WORKERS=8 timeout -k 10 400 python bench_configs.py config5 --gpu 0 > gpurun_out/config5_w8.json 2> gpurun_out/config5_w8.err && \
+  timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/bench_n1.json 2> gpurun_out/bench_n1.err || exit $?
+fi
+
 if [ "$STEP" = "configs" ]; then
   # BASELINE configs 4 (2-shard stress-write + cross-shard Rename) and 5 (S3 + Parquet) on the GPU
   timeout -k 10 500 python bench_configs.py config4 --gpu 0 > gpurun_out/config4.json 2> gpurun_out/config4.err && \
