@@ -131,7 +131,8 @@ def _s3_load(job):
     of the requests back to back over one keep-alive session; returns (start, end, latencies)."""
     import requests
 
-    op, url, idxs, size, nobj = job
+    op, url, idxs, size, nobj = job[:5]
+    pfx = job[5] if len(job) > 5 else "obj"
     s = requests.Session()
     bodies = {i: _s3_payload(i % nobj, size) for i in idxs} if op == "put" else {}
     lats = []
@@ -139,10 +140,10 @@ def _s3_load(job):
     for i in idxs:
         t0 = time.perf_counter()
         if op == "put":
-            r = s.put(f"{url}/bench/obj_{i:05d}", data=bodies[i])
+            r = s.put(f"{url}/bench/{pfx}_{i:05d}", data=bodies[i])
             assert r.status_code == 200 and r.headers["ETag"] == f'"{hashlib.md5(bodies[i]).hexdigest()}"'
         elif op == "get":
-            r = s.get(f"{url}/bench/obj_{i:05d}")
+            r = s.get(f"{url}/bench/{pfx}_{i:05d}")
             assert r.status_code == 200 and len(r.content) == size
         else:
             off = (i * 7919 * 4096) % (size - 65536)
@@ -170,12 +171,16 @@ def config5(a):
 
         lg = mp.get_context("spawn").Pool(a.concurrency)
 
-        def timed(op, count):
-            jobs = [(op, url, list(range(k, count, a.concurrency)), size, n) for k in range(a.concurrency)]
+        def timed(op, count, pfx="obj"):
+            jobs = [(op, url, list(range(k, count, a.concurrency)), size, n, pfx) for k in range(a.concurrency)]
             res = lg.map(_s3_load, jobs)
             return max(r[1] for r in res) - min(r[0] for r in res), [x for r in res for x in r[2]]
 
         lg.starmap(_s3_payload, [(0, 16)] * a.concurrency, chunksize=1)  # workers up before timing
+        # untimed warm-up round (as bench.py's warmup steps): every gateway process and its
+        # DFS client have served requests before the clock starts
+        timed("put", n, "warm")
+        timed("get", n, "warm")
         el, lat = timed("put", n)
         out["put"] = {"objects": n, "size": size, "mb_per_s": round(n * size / (1 << 20) / el, 1),
                       "p50_ms": pct(lat, 50), "p99_ms": pct(lat, 99)}

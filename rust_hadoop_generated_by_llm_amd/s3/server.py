@@ -191,6 +191,7 @@ class S3Gateway:
         app.router.add_get("/metrics", self.h_metrics)
         app.router.add_route("*", "/{tail:.*}", self.dispatch)
         app.on_cleanup.append(self._cleanup)
+        app.on_startup.append(self._warm)
         if self.oidc is not None:
             app.on_startup.append(self._start_jwks_refresh)
         return app
@@ -201,6 +202,22 @@ class S3Gateway:
         if self.audit is not None:
             await self.run(self.audit.close)
         self.pool.shutdown(wait=False)
+
+    async def _warm(self, _app) -> None:
+        """Before serving: one tiny write + delete through the DFS client, so its channels,
+        its shared-memory arena and the co-located chunkserver's mapping (and GPU pinning) of
+        that arena exist before the first request instead of stalling it."""
+        if not self.client.local_chunkserver:
+            return
+
+        def work():
+            p = f"{MPU_ROOT}/.warm-{os.getpid()}-{uuid.uuid4().hex[:8]}"
+            try:
+                self.client.create_file_from_buffer(b"w", p)
+                self.client.delete_file(p)
+            except DfsError as e:
+                log.info("client warm-up skipped: %s", e)
+        await self.run(work)
 
     async def _start_jwks_refresh(self, _app) -> None:
         async def loop():
