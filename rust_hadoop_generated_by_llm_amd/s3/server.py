@@ -805,7 +805,9 @@ class S3Gateway:
         reads, pos = [], 0
         for (_, p), sz in zip(parts, sizes):
             lo, hi = max(s, pos), min(e + 1, pos + sz)
-            if lo < hi:
+            if lo == pos and hi == pos + sz:  # whole part: the client's native fast read
+                reads.append(self.run(self.client.get_file_content, p))
+            elif lo < hi:
                 reads.append(self.run(self.client.read_file_range, p, lo - pos, hi - lo))
             pos += sz
         body = b"".join(await asyncio.gather(*reads)) if reads else b""
