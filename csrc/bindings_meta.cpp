@@ -321,6 +321,20 @@ void bind_meta(py::module_& m) {
       .def("shuffling_prefixes", &MasterCore::shuffling_prefixes)
       .def("take_request_counts", &MasterCore::take_request_counts)
       .def("take_gc", &MasterCore::take_gc)
+      .def("heal_scan", [](const MasterCore& c, int rf, const std::vector<std::string>& live,
+                           const std::map<std::string, std::vector<std::string>>& bad,
+                           const std::set<std::pair<std::string, std::string>>& queued) {
+        std::vector<MasterCore::HealAction> acts;
+        {
+          py::gil_scoped_release r;
+          acts = c.heal_scan(rf, live, bad, queued);
+        }
+        py::list out;
+        for (auto& a : acts)
+          out.append(py::make_tuple(a.reconstruct, a.queue_on, a.block_id, a.target, a.shard_index, a.ec_data,
+                                    a.ec_parity, a.sources, a.original_size));
+        return out;
+      })
       .def("snapshot", &MasterCore::snapshot, py::call_guard<py::gil_scoped_release>())
       .def("restore", &MasterCore::restore, py::call_guard<py::gil_scoped_release>())
       .def("apply", [](MasterCore& c, uint64_t idx, const std::string& cmd) {

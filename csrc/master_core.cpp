@@ -790,6 +790,70 @@ std::map<std::string, uint64_t> MasterCore::take_request_counts() {
   return out;
 }
 
+std::vector<MasterCore::HealAction> MasterCore::heal_scan(
+    int rf, const std::vector<std::string>& live, const std::map<std::string, std::vector<std::string>>& bad,
+    const std::set<std::pair<std::string, std::string>>& queued) const {
+  std::vector<HealAction> out;
+  if (live.empty()) return out;
+  const std::set<std::string> live_set(live.begin(), live.end());
+  const size_t want = std::min<size_t>(static_cast<size_t>(std::max(rf, 0)), live.size());
+  auto holds = [](const pb::BlockInfo& b, const std::string& s) {
+    return std::find(b.locations.begin(), b.locations.end(), s) != b.locations.end();
+  };
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& kv : files_) {
+    for (const pb::BlockInfo& b : kv.second.blocks) {
+      if (b.ec_data_shards > 0) {
+        const size_t total = static_cast<size_t>(b.ec_data_shards + b.ec_parity_shards);
+        if (b.locations.size() != total) continue;
+        size_t alive = 0;
+        for (auto& l : b.locations) alive += live_set.count(l);
+        for (size_t idx = 0; idx < b.locations.size(); ++idx) {
+          if (live_set.count(b.locations[idx])) continue;
+          if (alive < static_cast<size_t>(b.ec_data_shards)) break;  // not reconstructible
+          auto t = std::find_if(live.begin(), live.end(), [&](const std::string& s) { return !holds(b, s); });
+          if (t == live.end()) continue;
+          HealAction a;
+          a.reconstruct = true;
+          a.queue_on = a.target = *t;
+          a.block_id = b.block_id;
+          a.shard_index = static_cast<int>(idx);
+          a.ec_data = b.ec_data_shards;
+          a.ec_parity = b.ec_parity_shards;
+          for (auto& l : b.locations) a.sources.push_back(live_set.count(l) ? l : std::string());
+          a.original_size = b.original_size;
+          out.push_back(std::move(a));
+        }
+        continue;
+      }
+      auto bi = bad.find(b.block_id);
+      std::vector<const std::string*> healthy;
+      for (auto& l : b.locations)
+        if (live_set.count(l) && (bi == bad.end() || std::find(bi->second.begin(), bi->second.end(), l) ==
+                                                         bi->second.end()))
+          healthy.push_back(&l);
+      // copies already queued (not yet reported) count toward the target: a pass that runs
+      // before the last one's replications land does not over-replicate
+      size_t inflight = 0;
+      for (auto q = queued.lower_bound({b.block_id, std::string()}); q != queued.end() && q->first == b.block_id; ++q)
+        inflight += !holds(b, q->second);
+      if (healthy.empty() || healthy.size() + inflight >= want) continue;
+      size_t needed = want - healthy.size() - inflight;
+      for (const std::string& s : live) {
+        if (!needed) break;
+        if (holds(b, s) || queued.count({b.block_id, s})) continue;
+        HealAction a;
+        a.queue_on = *healthy[0];
+        a.block_id = b.block_id;
+        a.target = s;
+        out.push_back(std::move(a));
+        --needed;
+      }
+    }
+  }
+  return out;
+}
+
 std::vector<std::pair<std::string, std::vector<std::string>>> MasterCore::take_gc() {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<std::pair<std::string, std::vector<std::string>>> out;

@@ -110,6 +110,23 @@ class MasterCore : public raft::StateMachine {
   std::map<std::string, uint64_t> take_request_counts();
   std::vector<std::pair<std::string, std::vector<std::string>>> take_gc();
 
+  // Healer scan (C29, reference master.rs:436-602) over the whole namespace in one pass under
+  // the lock: REPLICATE for replicated blocks short of min(rf, live) healthy copies (queued on
+  // the first healthy holder), RECONSTRUCT_EC_SHARD for EC shards on dead servers (queued on
+  // the target) while >= k shards survive. `live` sorted; `bad` = block -> servers whose copy
+  // failed verification; `queued` = (block, target) already pending anywhere (counted as
+  // copies on their way, and never queued twice).
+  struct HealAction {
+    bool reconstruct = false;
+    std::string queue_on, block_id, target;
+    int shard_index = -1, ec_data = 0, ec_parity = 0;
+    std::vector<std::string> sources;  // reconstruct: per shard index, "" where dead
+    uint64_t original_size = 0;
+  };
+  std::vector<HealAction> heal_scan(int rf, const std::vector<std::string>& live,
+                                    const std::map<std::string, std::vector<std::string>>& bad,
+                                    const std::set<std::pair<std::string, std::string>>& queued) const;
+
   void set_access_stats(bool on, int flush_ms);
   uint64_t requests() const { return requests_.load(); }
 

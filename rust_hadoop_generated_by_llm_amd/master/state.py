@@ -286,50 +286,27 @@ class MasterState:
 
     # ------------------------------------------------------------------ healer (C29)
     def heal_under_replicated_blocks(self, rf: int = REPLICATION_FACTOR) -> int:
-        """Queue REPLICATE / RECONSTRUCT_EC_SHARD commands (reference master.rs:436-602)."""
-        live_set = set(self.chunk_servers)
-        live = sorted(live_set)
+        """Queue REPLICATE / RECONSTRUCT_EC_SHARD commands (reference master.rs:436-602). The
+        namespace scan runs natively over MasterCore's file table (MasterCore::heal_scan), so
+        a pass costs no protobuf decode per file; (block, target) pairs already queued are
+        not queued again."""
+        live = sorted(self.chunk_servers)
         if not live:
             return 0
-        issued = 0
+        queued = {(c.block_id, c.target_chunk_server_address) for cmds in self.pending_commands.values()
+                  for c in cmds if c.target_chunk_server_address}
+        bad = {bid: sorted(locs) for bid, locs in self.bad_block_locations.items()}
         T = pb.ChunkServerCommand
-        for f in self.files.values():
-            for b in f.blocks:
-                if b.ec_data_shards > 0:
-                    k = b.ec_data_shards
-                    total = b.ec_data_shards + b.ec_parity_shards
-                    if len(b.locations) != total:
-                        continue
-                    live_count = sum(1 for loc in b.locations if loc in live_set)
-                    for idx, loc in enumerate(b.locations):
-                        if loc in live_set:
-                            continue
-                        if live_count < k:
-                            break
-                        target = next((s for s in live if s not in b.locations), None)
-                        if target is None:
-                            continue
-                        srcs = [l if l in live_set else "" for l in b.locations]
-                        self.pending_commands.setdefault(target, []).append(T(
-                            type=T.RECONSTRUCT_EC_SHARD, block_id=b.block_id, target_chunk_server_address=target,
-                            shard_index=idx, ec_data_shards=b.ec_data_shards, ec_parity_shards=b.ec_parity_shards,
-                            ec_shard_sources=srcs, original_block_size=b.original_size))
-                        issued += 1
-                else:
-                    bad_on = self.bad_block_locations.get(b.block_id, set())
-                    live_locs = [l for l in b.locations if l in live_set and l not in bad_on]
-                    needed = max(0, min(rf, len(live)) - len(live_locs))
-                    if needed == 0 or not live_locs:
-                        continue
-                    src = live_locs[0]
-                    queued = {c.target_chunk_server_address for c in self.pending_commands.get(src, [])
-                              if c.block_id == b.block_id}
-                    targets = [s for s in live if s not in b.locations and s not in queued][:needed]
-                    for t in targets:
-                        self.pending_commands.setdefault(src, []).append(T(
-                            type=T.REPLICATE, block_id=b.block_id, target_chunk_server_address=t, shard_index=-1))
-                        issued += 1
-        return issued
+        acts = self.core.heal_scan(rf, live, bad, queued)
+        for reconstruct, queue_on, bid, target, idx, k, m, srcs, orig in acts:
+            if reconstruct:
+                cmd = T(type=T.RECONSTRUCT_EC_SHARD, block_id=bid, target_chunk_server_address=target,
+                        shard_index=idx, ec_data_shards=k, ec_parity_shards=m, ec_shard_sources=srcs,
+                        original_block_size=orig)
+            else:
+                cmd = T(type=T.REPLICATE, block_id=bid, target_chunk_server_address=target, shard_index=-1)
+            self.pending_commands.setdefault(queue_on, []).append(cmd)
+        return len(acts)
 
     def drain_gc(self) -> None:
         """DELETE commands for blocks the native handlers found unreferenced."""
