@@ -10,10 +10,12 @@
 
 #include "client_fast.h"
 #include "dfs_pb.h"
+#include "grpc_server.h"
 #include "localrpc.h"
 #include "config_core.h"
 #include "master_core.h"
 #include "raft.h"
+#include "trace.h"
 
 namespace py = pybind11;
 using namespace dfs;
@@ -377,6 +379,63 @@ void bind_meta(py::module_& m) {
       })
       .def("stop", &LocalRpcServer::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("requests", &LocalRpcServer::requests);
+
+  // MasterService over native HTTP/2 gRPC (grpc_server.cpp): the methods MasterCore serves
+  // natively (CreateFile, AllocateBlock, CompleteFile, GetFileInfo, ...) never touch Python;
+  // the rest run the grpcio handlers through the same fallback as the local listener.
+  struct NativeGrpcMaster {
+    std::shared_ptr<PyRef> fallback;
+    std::unique_ptr<GrpcServer> srv;
+    std::atomic<uint64_t> native_calls{0}, fallback_calls{0};
+  };
+  py::class_<NativeGrpcMaster>(m, "NativeGrpcMasterServer")
+      .def(py::init([](std::shared_ptr<MasterCore> core, const std::string& host, int port, py::object fallback,
+                       int workers) {
+             auto n = std::make_unique<NativeGrpcMaster>();
+             n->fallback = std::make_shared<PyRef>(std::move(fallback));
+             auto fb = n->fallback;
+             NativeGrpcMaster* self = n.get();
+             static const std::string kPrefix = "/dfs.MasterService/";
+             n->srv = std::make_unique<GrpcServer>(host, port, [core, fb, self](const GrpcCall& c) -> GrpcReply {
+               if (c.path.compare(0, kPrefix.size(), kPrefix) == 0) {
+                 std::string method = c.path.substr(kPrefix.size());
+                 if (core->native_method(method)) {
+                   RequestScope scope(c.request_id);
+                   GrpcReply r;
+                   r.status = core->handle(method, c.message, &r.message);
+                   self->native_calls++;
+                   return r;
+                 }
+               }
+               self->fallback_calls++;
+               py::gil_scoped_acquire g;
+               try {
+                 py::tuple r = fb->obj(c.path, c.request_id, py::bytes(c.message));
+                 return GrpcReply{r[0].cast<int>(), r[1].cast<std::string>()};
+               } catch (py::error_already_set& e) {
+                 return GrpcReply{13, std::string("python handler failed: ") + e.what()};
+               }
+             }, workers);
+             return n;
+           }),
+           py::arg("core"), py::arg("host"), py::arg("port"), py::arg("fallback"), py::arg("workers") = 64)
+      .def("start", [](NativeGrpcMaster& n) {
+        std::string err;
+        bool ok = n.srv->start(&err);
+        return py::make_tuple(ok, err);
+      })
+      .def("stop", [](NativeGrpcMaster& n) {
+        py::gil_scoped_release r;
+        n.srv->stop();
+      })
+      .def_property_readonly("port", [](NativeGrpcMaster& n) { return n.srv->port(); })
+      .def("stats", [](NativeGrpcMaster& n) {
+        py::dict d;
+        d["native_grpc_calls"] = n.srv->calls();
+        d["native_grpc_native"] = n.native_calls.load();
+        d["native_grpc_fallback"] = n.fallback_calls.load();
+        return d;
+      });
 
   // ---------------- native client data path (co-located writers/readers)
   py::class_<FastClient>(m, "FastClient")

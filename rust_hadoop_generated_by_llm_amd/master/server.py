@@ -115,6 +115,11 @@ class MasterProcess:
         self.metrics.gauge("dfs_master_chunkservers", "live chunkservers", fn=lambda: len(self.state.chunk_servers))
         self.metrics.gauge("dfs_master_native_requests", "requests served by the native handlers",
                            fn=lambda: self.state.core.requests)
+        self._native_grpc = None
+        for key, help_ in (("native_grpc_calls", "gRPC calls served by the native HTTP/2 server"),
+                           ("native_grpc_fallback", "native gRPC calls handed to the Python handlers")):
+            self.metrics.gauge(f"dfs_master_{key}", help_,
+                               fn=lambda k=key: self._native_grpc.stats()[k] if self._native_grpc else 0)
 
     def http_app(self) -> web.Application:
         app = web.Application(client_max_size=1 << 30)
@@ -166,17 +171,31 @@ class MasterProcess:
                            reuse_address=True)
         await site.start()
         creds = server_credentials(a.tls_cert, a.tls_key)
-        server = make_aio_server({"MasterService": self.svc}, a.addr if ":" in a.addr else f"0.0.0.0:{a.addr}", creds)
-        await server.start()
+        bind = a.addr if ":" in a.addr else f"0.0.0.0:{a.addr}"
+        loop = asyncio.get_running_loop()
+        dispatch = build_dispatch({"MasterService": self.svc})
+
+        def fallback(path, rid, payload):
+            return asyncio.run_coroutine_threadsafe(dispatch(path, rid, bytes(payload)), loop).result(120)
+
+        server = self._native_grpc = None
+        if creds is None and os.environ.get("DFS_MASTER_GRPC", "native") == "native":
+            # MasterService on the native HTTP/2 server: MasterCore's methods (the whole
+            # write/read metadata path) are answered in C++, the rest by the handlers below
+            host, port = bind.rsplit(":", 1)
+            srv = native.NativeGrpcMasterServer(self.state.core, host, int(port), fallback)
+            ok, err = srv.start()
+            if ok:
+                self._native_grpc = srv
+            else:
+                log.warning("native gRPC server unavailable (%s); serving with grpcio", err)
+        if self._native_grpc is None:
+            server = make_aio_server({"MasterService": self.svc}, bind, creds)
+            await server.start()
         self._local_srv = None
         if creds is None and os.environ.get("DFS_NO_LOCALRPC") != "1":
             # same-host clients skip HTTP/2: a native listener serves the hot methods from
             # MasterCore and hands the rest to the Python handlers on this loop
-            loop = asyncio.get_running_loop()
-            dispatch = build_dispatch({"MasterService": self.svc})
-
-            def fallback(path, rid, payload):
-                return asyncio.run_coroutine_threadsafe(dispatch(path, rid, bytes(payload)), loop).result(120)
 
             srv = native.MasterLocalServer(socket_name(a.addr.rsplit(":", 1)[-1]), self.state.core, fallback)
             ok, err = srv.start()
@@ -203,7 +222,10 @@ class MasterProcess:
         await self.bg.stop()
         if self._local_srv is not None:
             await asyncio.get_running_loop().run_in_executor(None, self._local_srv.stop)
-        await server.stop(0.5)
+        if server is not None:
+            await server.stop(0.5)
+        if self._native_grpc is not None:
+            await asyncio.get_running_loop().run_in_executor(None, self._native_grpc.stop)
         await self.raft.stop()
         self.state.core.detach()
         await self.transport.close()

@@ -115,3 +115,35 @@ def test_large_messages_and_concurrent_streams(server):
     with ThreadPoolExecutor(16) as ex:  # one channel: 16 streams multiplexed on one connection
         assert all(ex.map(one, blobs.items()))
     assert srv.stats()["native_grpc_calls"] >= 130
+
+
+@pytest.mark.slow
+def test_master_service_on_native_grpc():
+    """MasterService served by the native HTTP/2 server (NativeGrpcMasterServer): a client
+    on "another host" (every RPC over gRPC/TCP) writes, lists, renames, reads and deletes;
+    the metadata hot path is answered in C++ and the rest falls back to the Python handlers,
+    both visible in the master's metrics."""
+    import urllib.request
+
+    from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster
+
+    with LocalCluster(n_chunkservers=1, fsync=False) as cl:
+        c = cl.client(local_rpc=False, short_circuit=False)
+        try:
+            blobs = {f"/ng/m{i}": os.urandom(10_000 * (i + 1)) for i in range(5)}
+            for p, d in blobs.items():
+                c.create_file_from_buffer(d, p)
+            assert sorted(c.list_files("/ng")) == sorted(blobs)
+            c.rename_file("/ng/m0", "/ng/renamed")
+            assert c.get_file_content("/ng/renamed") == blobs["/ng/m0"]
+            c.delete_file("/ng/m1")
+            assert not c.exists("/ng/m1")
+            with pytest.raises(Exception):
+                c.get_file_content("/ng/missing")
+        finally:
+            c.close()
+        http = cl.master_http[cl.master_addrs[0]]
+        text = urllib.request.urlopen(f"{http}/metrics").read().decode()
+        vals = {ln.split()[0]: float(ln.split()[1]) for ln in text.splitlines() if ln and not ln.startswith("#")}
+        assert vals["dfs_master_native_grpc_calls"] >= 15
+        assert 0 < vals["dfs_master_native_grpc_fallback"] < vals["dfs_master_native_grpc_calls"]
