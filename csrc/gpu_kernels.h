@@ -15,7 +15,7 @@ namespace dfs {
 
 constexpr int kCrcWgThreads = 256;
 constexpr int kSlicesPerTile = 32;  // 4 waves x 8 slices x 512 B = 16 KiB per tile
-constexpr int kMaxGridCrc = 1024;
+constexpr int kMaxGridCrc = 768;  // 3 resident workgroups x 256 CUs (see crc_tile_mfma_kernel)
 constexpr int kMaxShards = 32;
 constexpr int kCrcBasisBytes = 16 * 64 * 16;  // MFMA basis (A fragments), stored after DevCrcTables
 

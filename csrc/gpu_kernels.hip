@@ -167,19 +167,60 @@ __device__ __forceinline__ uint32_t wave_chunk_crcs(const i32x4 (&A)[16], const 
 }
 
 // Chunk CRCs -> slice CRC (lane sl == 0 of each 8-lane group), as slice_crc does.
-__device__ __forceinline__ uint32_t slice_from_chunks(const DevCrcTables& lt, uint32_t r, int lane) {
+template <class L>
+__device__ __forceinline__ uint32_t slice_from_chunks(const L& lt, uint32_t r, int lane) {
   r = combine(r, 1, lane, lt.sh64);
   r = combine(r, 2, lane, lt.sh128);
   return combine(r, 4, lane, lt.sh256);
 }
 
-// LDS image without the slicing-by-16 tables (only the short tail slice still needs them).
-__device__ __forceinline__ void load_shift_tables(const DevCrcTables* __restrict__ gt, DevCrcTables* lt, bool with_slice16) {
-  const uint4* src = reinterpret_cast<const uint4*>(gt);
+// LDS images of the matrix-core kernels: only the GF(2) shift tables they look up (the
+// slicing-by-16 tables of the table kernels are not needed: short tail slices go through
+// the MFMA path front-padded with zeros). A prefix of DevCrcTables from sh64 on.
+struct MfmaSliceLds {  // K1b: chunk -> slice combine (12 KiB)
+  uint32_t sh64[4][256], sh128[4][256], sh256[4][256];
+};
+struct MfmaTileLds {  // K1/K2/K3: + slice -> sub-tile combine and the tile shifts (32 KiB)
+  uint32_t sh64[4][256], sh128[4][256], sh256[4][256];
+  uint32_t sh512[4][256], sh1k[4][256], sh2k[4][256];
+  uint32_t sh4k[4][256];
+  uint32_t tile_pow2[32][32];
+};
+static_assert(sizeof(MfmaTileLds) == sizeof(DevCrcTables) - offsetof(DevCrcTables, sh64), "LDS image layout");
+
+template <class L>
+__device__ __forceinline__ void load_lds_image(const DevCrcTables* __restrict__ gt, L* lt) {
+  const uint4* src = reinterpret_cast<const uint4*>(&gt->sh64);
   uint4* dst = reinterpret_cast<uint4*>(lt);
-  constexpr int n16 = sizeof(DevCrcTables) / 16;
-  const int from = with_slice16 ? 0 : static_cast<int>(offsetof(DevCrcTables, sh64) / 16);
-  for (int i = from + threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
+  constexpr int n16 = sizeof(L) / 16;
+#pragma unroll 4
+  for (int i = threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
+}
+
+// The short tail slice (len < 512 bytes at `base`) as slice 0 of a wave's 4 KiB, front-padded
+// with zeros to 512 B (the raw CRC ignores leading zeros); every other slice reads as zeros.
+// Byte loads: it runs once per block.
+__device__ __forceinline__ WaveData load_tail_wave(const uint8_t* __restrict__ base, uint32_t len, int lane) {
+  const int n = lane & 31, h = lane >> 5;
+  WaveData d;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d.v[k] = make_uint4(0, 0, 0, 0);
+  if (n < 8) {
+    const int pad = 512 - static_cast<int>(len);
+    uint32_t w[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint32_t v = 0;
+      for (int b = 0; b < 4; ++b) {
+        const int pos = n * 64 + h * 32 + q * 4 + b;
+        v |= (pos >= pad ? static_cast<uint32_t>(base[pos - pad]) : 0u) << (8 * b);
+      }
+      w[q] = v;
+    }
+    d.v[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d.v[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  }
+  return d;
 }
 
 // Short slice of `len` bytes, front-padded with zeros to 512 B (wave-wide call, lanes 0..7 work).
@@ -314,9 +355,12 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_kernel(ScrubLaunch a,
 // lane-parallel GF(2) shift per tile) — no barrier inside the tile loop. The next tile's
 // data is loaded while the current one is on the matrix cores, and the first tile's loads
 // are issued before the LDS table fill, so a 1 MiB block costs one memory round trip.
-__global__ __launch_bounds__(kCrcWgThreads) void crc_tile_mfma_kernel(CrcLaunch a,
+// 3 waves/SIMD (168 VGPRs: the 64-VGPR basis + double-buffered data, no spills) x 4 SIMDs =
+// 3 workgroups per CU, which their 32 KiB LDS images allow; the grid is sized to exactly one
+// resident round (kMaxGridCrc = 3 x 256 CUs), so no second, partly empty round.
+__global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void crc_tile_mfma_kernel(CrcLaunch a,
                                                                       const DevCrcTables* __restrict__ gt) {
-  __shared__ DevCrcTables lt;
+  __shared__ MfmaTileLds lt;
   __shared__ uint32_t wacc[4];
   __shared__ uint32_t wg_bad;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
@@ -331,7 +375,7 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_tile_mfma_kernel(CrcLaunch 
   if (t_begin < t_end) cur = load_wave(a.data, first_slice(t_begin), lo, hi, lane);
   i32x4 A[16];
   load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
-  load_shift_tables(gt, &lt, a.has_tail && blockIdx.x == 0);
+  load_lds_image(gt, &lt);
   if (threadIdx.x == 0) wg_bad = 0xFFFFFFFFu;
   __syncthreads();
 
@@ -357,7 +401,8 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_tile_mfma_kernel(CrcLaunch 
   }
 
   if (a.has_tail && blockIdx.x == 0 && wave == 0) {
-    uint32_t r = tail_crc(lt, a.data + a.s_full * 512, a.tail_len, lane);
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(a.data + a.s_full * 512, a.tail_len, lane),
+                                                       lane), lane);
     if (lane == 0) {
       uint32_t be = __builtin_bswap32(r ^ a.tail_init);
       if (a.meta_out) a.meta_out[a.s_full] = be;
@@ -384,9 +429,9 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_tile_mfma_kernel(CrcLaunch 
 // K1b on the matrix cores: contiguous tile runs per workgroup, so the tile -> block lookup is
 // one binary search per workgroup and then a forward walk, and the next tile's data (and its
 // block) are fetched while the current tile computes.
-__global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_mfma_kernel(ScrubLaunch a,
+__global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void crc_scrub_mfma_kernel(ScrubLaunch a,
                                                                        const DevCrcTables* __restrict__ gt) {
-  __shared__ DevCrcTables lt;
+  __shared__ MfmaSliceLds lt;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
   const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
   const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
@@ -413,7 +458,7 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_mfma_kernel(ScrubLaun
     cur = load_wave(a.blocks[blk].data, first_slice(t_begin, blk), 0, static_cast<int64_t>(a.blocks[blk].s_full), lane);
   i32x4 A[16];
   load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
-  load_tables(gt, &lt);  // the tail loop below may need the slicing tables in any workgroup
+  load_lds_image(gt, &lt);
   __syncthreads();
   for (uint64_t t = t_begin; t < t_end; ++t) {
     WaveData nxt;
@@ -437,7 +482,8 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_scrub_mfma_kernel(ScrubLaun
        k += static_cast<uint64_t>(gridDim.x) * waves) {
     const ScrubBlock& b = a.blocks[k];
     if (!b.tail_len) continue;
-    uint32_t r = tail_crc(lt, b.data + b.s_full * 512, b.tail_len, lane);
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(b.data + b.s_full * 512, b.tail_len, lane),
+                                                       lane), lane);
     if (lane == 0 && b.meta[b.s_full] != __builtin_bswap32(r ^ b.tail_init))
       atomicMin(&a.bad[k], static_cast<uint32_t>(b.s_full));
   }
@@ -570,7 +616,15 @@ DevCrcTables* upload_crc_tables(hipStream_t s) {
 
 
 int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
-  uint64_t g = ntiles < static_cast<uint64_t>(kMaxGridCrc) ? ntiles : kMaxGridCrc;
+  // small blocks: at least `per` tiles per workgroup, so the per-workgroup fixed cost (the
+  // 16 KiB basis per wave and the LDS image, both from L2) is amortised over more data
+  static const uint64_t per = [] {
+    const char* e = std::getenv("DFS_CRC_MIN_TILES_PER_WG");
+    long v = e ? std::atol(e) : 1;
+    return static_cast<uint64_t>(v > 0 ? v : 1);
+  }();
+  uint64_t g = (ntiles + per - 1) / per;
+  g = g < static_cast<uint64_t>(kMaxGridCrc) ? g : kMaxGridCrc;
   if (g == 0 && has_tail) g = 1;
   return static_cast<int>(g);
 }
@@ -584,9 +638,10 @@ hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipSt
 
 hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s) {
   if (a.nblocks == 0) return hipSuccess;
-  uint64_t g = a.ntiles < 2048 ? a.ntiles : 2048;
+  const uint64_t cap = crc_mfma_enabled() ? kMaxGridCrc : 2048;
+  uint64_t g = a.ntiles < cap ? a.ntiles : cap;
   uint64_t tail_waves = (a.nblocks + 3) / 4;
-  if (g < tail_waves) g = tail_waves < 2048 ? tail_waves : 2048;
+  if (g < tail_waves) g = tail_waves < cap ? tail_waves : cap;
   if (g == 0) g = 1;
   if (crc_mfma_enabled())
     hipLaunchKernelGGL(crc_scrub_mfma_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
