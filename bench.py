@@ -401,8 +401,9 @@ def main():
                 rrb += rs.count * rs.avg_size
                 rwt += ws.total_s
                 rrt += rs.total_s
+            remote = {"wl": rwl, "rl": rrl, "wbytes": rwb, "rbytes": rrb, "wt": rwt, "rt": rrt,
+                      "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count}
             rc.close()
-            remote = {"wl": rwl, "rl": rrl, "wbytes": rwb, "rbytes": rrb, "wt": rwt, "rt": rrt}
         allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
                        "rt": rt, "cs": stats, "stress": stress, "remote": remote, "rccl": cs_info.get("rccl", False),
                        "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
@@ -453,8 +454,13 @@ def main():
                 rw = sum(r["remote"]["wbytes"] for r in allr) / (1 << 20) / max(r["remote"]["wt"] for r in allr)
                 rr = sum(r["remote"]["rbytes"] for r in allr) / (1 << 20) / max(r["remote"]["rt"] for r in allr)
                 result["remote_client"] = {
-                    "steps": a.remote_steps, "path": "gRPC/TCP for every master and chunkserver RPC (no shm, "
-                                                      "no UNIX sockets), Python grpcio client",
+                    "steps": a.remote_steps,
+                    "path": "gRPC/TCP for every master and chunkserver RPC (no shm, no UNIX sockets), " + (
+                        "native C++ client (HTTP/2 on nghttp2)" if all(
+                            r["remote"]["native_ops"] == r["remote"]["ops"] for r in allr) else
+                        "Python grpcio client" if all(r["remote"]["native_ops"] == 0 for r in allr) else
+                        "native C++ client with Python fallbacks"),
+                    "native_client_ops": sum(r["remote"]["native_ops"] for r in allr),
                     "write_mb_per_s": round(rw, 2), "read_mb_per_s": round(rr, 2),
                     "mb_per_s": round((sum(r["remote"]["wbytes"] + r["remote"]["rbytes"] for r in allr) / (1 << 20))
                                       / max(r["remote"]["wt"] + r["remote"]["rt"] for r in allr), 2),

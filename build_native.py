@@ -80,7 +80,7 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
         objs.append(obj)
         if clean or _newer(src, obj, headers):
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
-            extra = _nghttp2_include() if src.name == "grpc_server.cpp" else []
+            extra = _nghttp2_include() if src.name in ("grpc_server.cpp", "grpc_client.cpp") else []
             jobs.append([HIPCC, *flags, *extra, *lang, "-c", str(src), "-o", str(obj)])
 
     def run(cmd):

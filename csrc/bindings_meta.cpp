@@ -9,6 +9,8 @@
 #include <cstring>
 
 #include "client_fast.h"
+#include "client_remote.h"
+#include "grpc_client.h"
 #include "dfs_pb.h"
 #include "grpc_server.h"
 #include "localrpc.h"
@@ -485,4 +487,50 @@ void bind_meta(py::module_& m) {
         }
         return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
       }, py::arg("path"), py::arg("request_id") = "");
+
+  // ---------------- native remote client (every RPC over gRPC/TCP, client_remote.h)
+  py::class_<RemoteClient>(m, "RemoteClient")
+      .def(py::init<int, int>(), py::arg("hash_threads") = 4, py::arg("timeout_ms") = 120000)
+      .def_property_readonly("writes", &RemoteClient::writes)
+      .def_property_readonly("reads", &RemoteClient::reads)
+      .def_property_readonly("connects", &RemoteClient::connects)
+      .def("set_routing", &RemoteClient::set_routing, py::call_guard<py::gil_scoped_release>())
+      .def("write", [](RemoteClient& c, const std::string& path, py::buffer data, const std::string& rid) {
+        py::buffer_info bi = data.request();
+        int replicas = 0;
+        std::string msg;
+        FastClient::Times t;
+        FastClient::Status st;
+        {
+          py::gil_scoped_release r;
+          st = c.write(path, static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize),
+                       &replicas, &msg, &t, rid);
+        }
+        return py::make_tuple(static_cast<int>(st), replicas, msg,
+                              py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete));
+      }, py::arg("path"), py::arg("data"), py::arg("request_id") = "")
+      .def("read", [](RemoteClient& c, const std::string& path, const std::string& rid) {
+        std::string out, msg;
+        FastClient::Times t;
+        FastClient::Status st;
+        {
+          py::gil_scoped_release r;
+          st = c.read(path, &out, &msg, &t, rid);
+        }
+        py::object data = st == FastClient::Ok ? py::object(py::bytes(out)) : py::object(py::none());
+        return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
+      }, py::arg("path"), py::arg("request_id") = "");
+
+  // raw native gRPC unary call (interop tests)
+  m.def("grpc_call", [](const std::string& target, const std::string& path, py::bytes req, const std::string& rid,
+                        int timeout_ms) {
+    static GrpcChannelPool pool;
+    std::string in = req;
+    GrpcResult r;
+    {
+      py::gil_scoped_release g;
+      r = pool.call(target, path, in, rid, timeout_ms);
+    }
+    return py::make_tuple(r.transport_ok, r.status, py::bytes(r.message));
+  }, py::arg("target"), py::arg("path"), py::arg("request"), py::arg("request_id") = "", py::arg("timeout_ms") = 10000);
 }

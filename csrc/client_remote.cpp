@@ -1,0 +1,301 @@
+// Native remote client; design notes in client_remote.h.
+#include "client_remote.h"
+
+#include <openssl/evp.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <future>
+#include <random>
+
+#include "crc32.h"
+#include "dfs_pb.h"
+#include "json.h"
+#include "trace.h"
+
+namespace dfs {
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+constexpr int kNotFound = 5, kFailedPrecondition = 9, kOutOfRange = 11;
+
+std::string request_id() {
+  thread_local std::mt19937_64 rng{std::random_device{}()};
+  char buf[33];
+  std::snprintf(buf, sizeof buf, "%016llx%016llx", static_cast<unsigned long long>(rng()),
+                static_cast<unsigned long long>(rng()));
+  return buf;
+}
+
+double since(Clock::time_point& t) {
+  auto now = Clock::now();
+  double d = std::chrono::duration<double>(now - t).count();
+  t = now;
+  return d;
+}
+
+int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+std::string md5_hex(const uint8_t* p, size_t n) {
+  unsigned char d[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  EVP_Digest(p, n, d, &len, EVP_md5(), nullptr);
+  static const char* hx = "0123456789abcdef";
+  std::string out;
+  for (unsigned i = 0; i < len; ++i) {
+    out.push_back(hx[d[i] >> 4]);
+    out.push_back(hx[d[i] & 15]);
+  }
+  return out;
+}
+
+// "Not Leader" / "Not Leader|<hint>" in a status message or a response's error field
+bool not_leader(const std::string& m, std::string* hint) {
+  if (m.compare(0, 10, "Not Leader") != 0) return false;
+  auto bar = m.find('|');
+  *hint = bar == std::string::npos ? std::string() : m.substr(bar + 1);
+  return true;
+}
+
+}  // namespace
+
+RemoteClient::RemoteClient(int hash_threads, int timeout_ms) : pool_(timeout_ms) {
+  for (int i = 0; i < std::max(1, hash_threads); ++i) hashers_.emplace_back([this] { hash_loop(); });
+}
+
+RemoteClient::~RemoteClient() {
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    stop_ = true;
+  }
+  q_cv_.notify_all();
+  for (auto& t : hashers_) t.join();
+}
+
+void RemoteClient::hash_loop() {
+  for (;;) {
+    std::function<void()> job;
+    {
+      std::unique_lock<std::mutex> lk(q_mu_);
+      q_cv_.wait(lk, [this] { return stop_ || !queue_.empty(); });
+      if (queue_.empty()) return;
+      job = std::move(queue_.front());
+      queue_.pop_front();
+    }
+    job();
+  }
+}
+
+void RemoteClient::set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters) {
+  ShardMap m = shard_map_json.empty() ? ShardMap::new_range() : ShardMap::from_json(Json::parse(shard_map_json));
+  std::lock_guard<std::mutex> g(route_mu_);
+  map_ = std::move(m);
+  have_map_ = !shard_map_json.empty();
+  masters_ = masters;
+}
+
+std::vector<std::string> RemoteClient::masters_for(const std::string& path, std::string* shard) {
+  std::lock_guard<std::mutex> g(route_mu_);
+  std::vector<std::string> out;
+  shard->clear();
+  if (have_map_) {
+    *shard = map_.get_shard(path);
+    const auto* peers = shard->empty() ? nullptr : map_.peers(*shard);
+    if (peers) out = *peers;
+  }
+  if (out.empty()) out = masters_;
+  auto it = leader_.find(*shard);
+  if (it != leader_.end()) {
+    auto pos = std::find(out.begin(), out.end(), it->second);
+    if (pos != out.end()) std::rotate(out.begin(), pos, pos + 1);
+  }
+  return out;
+}
+
+bool RemoteClient::master_call(const std::string& path, const std::string& method, const std::string& req,
+                               const std::string& rid, int* code, std::string* resp) {
+  std::string shard;
+  std::vector<std::string> cands = masters_for(path, &shard);
+  const std::string full = "/dfs.MasterService/" + method;
+  *code = -1;
+  for (size_t i = 0; i < cands.size() && i < 8; ++i) {
+    GrpcResult r = pool_.call(cands[i], full, req, rid);
+    if (!r.transport_ok) continue;
+    std::string hint;
+    if (r.status == kFailedPrecondition && not_leader(r.message, &hint)) {
+      if (!hint.empty() && std::find(cands.begin() + static_cast<long>(i) + 1, cands.end(), hint) == cands.end())
+        cands.insert(cands.begin() + static_cast<long>(i) + 1, hint);
+      continue;
+    }
+    {
+      std::lock_guard<std::mutex> g(route_mu_);
+      leader_[shard] = cands[i];
+    }
+    *code = r.status;
+    *resp = std::move(r.message);
+    return true;
+  }
+  return false;
+}
+
+FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
+                                       std::string* msg, Times* t, const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? request_id() : rid_in;
+  RequestScope rs(rid);
+  TraceRange tr("dfs.remote.write");
+  auto clk = Clock::now();
+  auto md5_task = std::make_shared<std::packaged_task<std::string()>>([data, n] { return md5_hex(data, n); });
+  std::future<std::string> md5 = md5_task->get_future();
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    queue_.emplace_back([md5_task] { (*md5_task)(); });
+  }
+  q_cv_.notify_one();
+  struct Join {  // never return while the worker still reads the caller's buffer
+    std::future<std::string>& f;
+    ~Join() {
+      if (f.valid()) f.wait();
+    }
+  } join{md5};
+  const uint32_t crc = crc32(data, n);
+  t->crc = since(clk);
+
+  pb::CreateFileRequest creq;
+  creq.path = path;
+  creq.allocate_block = true;
+  creq.defer_create = true;
+  int code;
+  std::string raw;
+  if (!master_call(path, "CreateFile", creq.str(), rid, &code, &raw)) return FastClient::NotHandled;
+  if (code == kOutOfRange || code == kFailedPrecondition || code == 14) return FastClient::NotHandled;
+  if (code != 0) {
+    *msg = "Failed to create file: " + raw;
+    return FastClient::Failed;
+  }
+  pb::CreateFileResponse cresp;
+  if (!cresp.decode(raw)) return FastClient::NotHandled;
+  if (!cresp.success) {
+    if (cresp.error_message == "Not Leader") return FastClient::NotHandled;
+    *msg = "Failed to create file: " + cresp.error_message;
+    return FastClient::Failed;
+  }
+  if (!cresp.has_allocation || !cresp.allocation.has_block || !cresp.deferred) return FastClient::NotHandled;
+  const pb::AllocateBlockResponse& alloc = cresp.allocation;
+  if (alloc.chunk_server_addresses.empty()) {
+    *msg = "No chunk servers available";
+    return FastClient::Failed;
+  }
+  t->create = since(clk);
+
+  pb::WriteBlockRequest w;
+  w.block_id = alloc.block.block_id;
+  w.data.assign(reinterpret_cast<const char*>(data), n);
+  for (size_t i = 1; i < alloc.chunk_server_addresses.size(); ++i) w.next_servers.push_back(alloc.chunk_server_addresses[i]);
+  w.expected_checksum_crc32c = crc;
+  w.shard_index = -1;
+  w.master_term = alloc.master_term;
+  std::string wire = w.str();
+  std::string().swap(w.data);
+  GrpcResult wr = pool_.call(alloc.chunk_server_addresses[0], "/dfs.ChunkServerService/WriteBlock", wire, rid);
+  std::string().swap(wire);
+  if (!wr.transport_ok) {
+    *msg = "Failed to write block: " + wr.message;
+    return FastClient::Failed;
+  }
+  if (wr.status != 0) {
+    *msg = "Failed to write block: " + wr.message;
+    return FastClient::Failed;
+  }
+  pb::WriteBlockResponse wresp;
+  if (!wresp.decode(wr.message) || !wresp.success) {
+    *msg = "Failed to write block: " + wresp.error_message;
+    return FastClient::Failed;
+  }
+  *replicas = wresp.replicas_written;
+  t->write = since(clk);
+
+  pb::CompleteFileRequest done;
+  done.path = path;
+  done.size = n;
+  done.etag_md5 = md5.get();
+  t->md5_wait = since(clk);
+  done.created_at_ms = static_cast<uint64_t>(now_ms());
+  pb::BlockChecksumInfo sum;
+  sum.block_id = alloc.block.block_id;
+  sum.checksum_crc32c = crc;
+  sum.actual_size = n;
+  done.block_checksums.push_back(sum);
+  done.create = true;
+  done.ec_data_shards = alloc.ec_data_shards;
+  done.ec_parity_shards = alloc.ec_parity_shards;
+  done.blocks.push_back(alloc.block);
+  if (!master_call(path, "CompleteFile", done.str(), rid, &code, &raw)) {
+    *msg = "Failed to complete file: master unreachable";
+    return FastClient::Failed;
+  }
+  if (code != 0) {
+    *msg = "Failed to complete file: " + raw;
+    return FastClient::Failed;
+  }
+  pb::CompleteFileResponse dresp;
+  dresp.decode(raw);
+  if (!dresp.success) {
+    *msg = dresp.error_message.empty() ? "Failed to complete file" : "Failed to create file: " + dresp.error_message;
+    return FastClient::Failed;
+  }
+  t->complete = since(clk);
+  writes_++;
+  return FastClient::Ok;
+}
+
+FastClient::Status RemoteClient::read(const std::string& path, std::string* out, std::string* msg, Times* t,
+                                      const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? request_id() : rid_in;
+  RequestScope rs(rid);
+  TraceRange tr("dfs.remote.read");
+  auto clk = Clock::now();
+  pb::GetFileInfoRequest req;
+  req.path = path;
+  int code;
+  std::string raw;
+  if (!master_call(path, "GetFileInfo", req.str(), rid, &code, &raw)) return FastClient::NotHandled;
+  if (code != 0) return code == kNotFound ? (*msg = raw, FastClient::Failed) : FastClient::NotHandled;
+  pb::GetFileInfoResponse info;
+  if (!info.decode(raw)) return FastClient::NotHandled;
+  if (!info.found) {
+    *msg = "File not found";
+    return FastClient::Failed;
+  }
+  t->getinfo = since(clk);
+  const pb::FileMetadata& m = info.metadata;
+  if (m.size == 0) {
+    out->clear();
+    reads_++;
+    return FastClient::Ok;
+  }
+  if (m.blocks.size() != 1 || m.blocks[0].ec_data_shards > 0) return FastClient::NotHandled;
+  const pb::BlockInfo& b = m.blocks[0];
+  pb::ReadBlockRequest rreq;
+  rreq.block_id = b.block_id;
+  rreq.offset = 0;
+  rreq.length = b.size ? b.size : m.size;
+  const std::string wire = rreq.str();
+  for (const std::string& loc : b.locations) {
+    GrpcResult r = pool_.call(loc, "/dfs.ChunkServerService/ReadBlock", wire, rid);
+    if (!r.transport_ok || r.status != 0) continue;  // corrupt / missing / down: next replica
+    pb::ReadBlockResponse resp;
+    if (!resp.decode(r.message) || resp.data.size() != rreq.length) continue;
+    *out = std::move(resp.data);
+    t->read = since(clk);
+    reads_++;
+    return FastClient::Ok;
+  }
+  return FastClient::NotHandled;  // no replica answered cleanly: the Python path recovers / reports
+}
+
+}  // namespace dfs

@@ -1,0 +1,75 @@
+// Native remote client: the reference client's write / read of a single-block file
+// (dfs/client/src/mod.rs:225-494 write, 856-944 read) for a client on ANOTHER host — every
+// RPC over gRPC/TCP (grpc_client.h), nothing through shared memory or local sockets:
+//
+//   write: CRC-32 (PCLMUL) + MD5 on a worker, overlapped with CreateFile{allocate, deferred}
+//          -> WriteBlock(data, next_servers) to the chain head -> CompleteFile{create}
+//   read:  GetFileInfo -> ReadBlock from the first location that answers
+//
+// Leader changes are followed (Not Leader hints, then the shard's other peers). Anything
+// else it does not own — shard redirects, EC or multi-block files, TLS — returns NotHandled
+// and the Python client takes over, so semantics never change. It is what makes the
+// "remote client" numbers of bench.py a native client against native servers, like the
+// reference's Rust dfs_cli against its Rust servers.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "client_fast.h"
+#include "grpc_client.h"
+#include "shard_map.h"
+
+namespace dfs {
+
+class RemoteClient {
+ public:
+  using Status = FastClient::Status;
+  using Times = FastClient::Times;
+
+  explicit RemoteClient(int hash_threads = 4, int timeout_ms = 120000);
+  ~RemoteClient();
+  RemoteClient(const RemoteClient&) = delete;
+
+  // Routing: shard map (serde JSON, "" = none) and the fallback master list (gRPC URLs).
+  void set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters);
+
+  Status write(const std::string& path, const uint8_t* data, size_t n, int* replicas, std::string* msg, Times* t,
+               const std::string& rid = "");
+  Status read(const std::string& path, std::string* out, std::string* msg, Times* t, const std::string& rid = "");
+
+  uint64_t writes() const { return writes_.load(); }
+  uint64_t reads() const { return reads_.load(); }
+  uint64_t connects() const { return pool_.connects(); }
+
+ private:
+  // A MasterService call on the path's shard, following Not Leader hints; `*code` = -1 on
+  // transport failure everywhere.
+  bool master_call(const std::string& path, const std::string& method, const std::string& req,
+                   const std::string& rid, int* code, std::string* resp);
+  std::vector<std::string> masters_for(const std::string& path, std::string* shard);
+  void hash_loop();
+
+  GrpcChannelPool pool_;
+  std::mutex route_mu_;
+  ShardMap map_;
+  bool have_map_ = false;
+  std::vector<std::string> masters_;
+  std::map<std::string, std::string> leader_;  // shard ("" = no map) -> last known leader
+
+  std::mutex q_mu_;
+  std::condition_variable q_cv_;
+  std::deque<std::function<void()>> queue_;
+  std::vector<std::thread> hashers_;
+  bool stop_ = false;
+
+  std::atomic<uint64_t> writes_{0}, reads_{0};
+};
+
+}  // namespace dfs

@@ -1,0 +1,322 @@
+// Native gRPC client on nghttp2; design notes in grpc_client.h.
+#include "grpc_client.h"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <nghttp2/nghttp2.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+namespace dfs {
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+int hexval(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+std::string percent_decode(const uint8_t* p, size_t n) {
+  std::string o;
+  o.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    int hi, lo;
+    if (p[i] == '%' && i + 2 < n && (hi = hexval(static_cast<char>(p[i + 1]))) >= 0 &&
+        (lo = hexval(static_cast<char>(p[i + 2]))) >= 0) {
+      o.push_back(static_cast<char>(hi * 16 + lo));
+      i += 2;
+    } else {
+      o.push_back(static_cast<char>(p[i]));
+    }
+  }
+  return o;
+}
+
+std::string strip_scheme(const std::string& t) {
+  for (const char* s : {"http://", "https://"})
+    if (t.compare(0, std::strlen(s), s) == 0) return t.substr(std::strlen(s));
+  return t;
+}
+
+nghttp2_nv nv(const std::string& name, const std::string& value) {
+  return {reinterpret_cast<uint8_t*>(const_cast<char*>(name.data())),
+          reinterpret_cast<uint8_t*>(const_cast<char*>(value.data())), name.size(), value.size(),
+          NGHTTP2_NV_FLAG_NO_COPY_NAME | NGHTTP2_NV_FLAG_NO_COPY_VALUE};
+}
+
+int connect_to(const std::string& hostport, int timeout_ms, std::string* err) {
+  size_t colon = hostport.rfind(':');
+  if (colon == std::string::npos) {
+    *err = "bad target " + hostport;
+    return -1;
+  }
+  std::string host = hostport.substr(0, colon), port = hostport.substr(colon + 1);
+  if (host.size() > 1 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_socktype = SOCK_STREAM;
+  hints.ai_family = AF_UNSPEC;
+  if (int rc = ::getaddrinfo(host.c_str(), port.c_str(), &hints, &res); rc != 0) {
+    *err = std::string("resolve ") + hostport + ": " + gai_strerror(rc);
+    return -1;
+  }
+  int fd = -1;
+  for (addrinfo* ai = res; ai; ai = ai->ai_next) {
+    fd = ::socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC | SOCK_NONBLOCK, ai->ai_protocol);
+    if (fd < 0) continue;
+    int rc = ::connect(fd, ai->ai_addr, ai->ai_addrlen);
+    if (rc != 0 && errno == EINPROGRESS) {
+      pollfd p{fd, POLLOUT, 0};
+      int soerr = 0;
+      socklen_t sl = sizeof soerr;
+      if (::poll(&p, 1, timeout_ms) == 1 && ::getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl) == 0 && soerr == 0)
+        rc = 0;
+      else
+        errno = soerr ? soerr : ETIMEDOUT;
+    }
+    if (rc == 0) break;
+    *err = "connect " + hostport + ": " + std::strerror(errno);
+    ::close(fd);
+    fd = -1;
+  }
+  ::freeaddrinfo(res);
+  if (fd < 0) return -1;
+  int one = 1;
+  ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  int buf = 4 << 20;
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+  return fd;
+}
+
+}  // namespace
+
+struct GrpcChannelPool::Conn {
+  int fd = -1;
+  nghttp2_session* s = nullptr;
+  std::string authority;
+  // the call in flight
+  int32_t sid = -1;
+  std::string out;  // 5-byte prefix + request message
+  size_t off = 0;
+  std::string in;   // response DATA (5-byte prefix + message)
+  bool closed = false, reset = false;
+  int grpc_status = -1;
+  std::string grpc_message;
+  Clock::time_point deadline;
+
+  ~Conn() {
+    if (s) nghttp2_session_del(s);
+    if (fd >= 0) ::close(fd);
+  }
+
+  static ssize_t on_send(nghttp2_session*, const uint8_t* data, size_t len, int, void* user) {
+    auto* c = static_cast<Conn*>(user);
+    // the socket is non-blocking: wait for room until the call's deadline
+    size_t done = 0;
+    while (done < len) {
+      ssize_t r = ::send(c->fd, data + done, len - done, MSG_NOSIGNAL);
+      if (r > 0) {
+        done += static_cast<size_t>(r);
+      } else if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        int ms = static_cast<int>(
+            std::chrono::duration_cast<std::chrono::milliseconds>(c->deadline - Clock::now()).count());
+        pollfd p{c->fd, POLLOUT, 0};
+        if (ms <= 0 || ::poll(&p, 1, ms) <= 0) return NGHTTP2_ERR_CALLBACK_FAILURE;
+      } else if (r < 0 && errno == EINTR) {
+        continue;
+      } else {
+        return NGHTTP2_ERR_CALLBACK_FAILURE;
+      }
+    }
+    return static_cast<ssize_t>(len);
+  }
+
+  static int on_header(nghttp2_session*, const nghttp2_frame* f, const uint8_t* name, size_t namelen,
+                       const uint8_t* value, size_t valuelen, uint8_t, void* user) {
+    auto* c = static_cast<Conn*>(user);
+    if (f->hd.stream_id != c->sid) return 0;
+    std::string n(reinterpret_cast<const char*>(name), namelen);
+    if (n == "grpc-status") c->grpc_status = std::atoi(std::string(reinterpret_cast<const char*>(value), valuelen).c_str());
+    else if (n == "grpc-message") c->grpc_message = percent_decode(value, valuelen);
+    return 0;
+  }
+
+  static int on_data(nghttp2_session*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* user) {
+    auto* c = static_cast<Conn*>(user);
+    if (sid == c->sid) c->in.append(reinterpret_cast<const char*>(data), len);
+    return 0;
+  }
+
+  static int on_close(nghttp2_session*, int32_t sid, uint32_t error_code, void* user) {
+    auto* c = static_cast<Conn*>(user);
+    if (sid == c->sid) {
+      c->closed = true;
+      c->reset = error_code != NGHTTP2_NO_ERROR;
+    }
+    return 0;
+  }
+
+  static ssize_t read_body(nghttp2_session*, int32_t, uint8_t* buf, size_t len, uint32_t* flags, nghttp2_data_source*,
+                           void* user) {
+    auto* c = static_cast<Conn*>(user);
+    size_t n = std::min(len, c->out.size() - c->off);
+    std::memcpy(buf, c->out.data() + c->off, n);
+    c->off += n;
+    if (c->off == c->out.size()) *flags |= NGHTTP2_DATA_FLAG_EOF;
+    return static_cast<ssize_t>(n);
+  }
+
+  bool init(std::string* err) {
+    nghttp2_session_callbacks* cb;
+    nghttp2_session_callbacks_new(&cb);
+    nghttp2_session_callbacks_set_send_callback(cb, &Conn::on_send);
+    nghttp2_session_callbacks_set_on_header_callback(cb, &Conn::on_header);
+    nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cb, &Conn::on_data);
+    nghttp2_session_callbacks_set_on_stream_close_callback(cb, &Conn::on_close);
+    int rc = nghttp2_session_client_new(&s, cb, this);
+    nghttp2_session_callbacks_del(cb);
+    if (rc != 0) {
+      *err = "nghttp2 session";
+      return false;
+    }
+    nghttp2_settings_entry iv[] = {{NGHTTP2_SETTINGS_ENABLE_PUSH, 0},
+                                   {NGHTTP2_SETTINGS_INITIAL_WINDOW_SIZE, 64u << 20},
+                                   {NGHTTP2_SETTINGS_MAX_FRAME_SIZE, 1u << 20}};
+    if (nghttp2_submit_settings(s, NGHTTP2_FLAG_NONE, iv, 3) != 0 ||
+        nghttp2_session_set_local_window_size(s, NGHTTP2_FLAG_NONE, 0, 1 << 30) != 0) {
+      *err = "nghttp2 settings";
+      return false;
+    }
+    return true;
+  }
+
+  // Drive the session until our stream closes; false on transport failure / timeout.
+  bool pump() {
+    std::vector<uint8_t> buf(1 << 18);
+    for (;;) {
+      if (nghttp2_session_send(s) != 0) return false;
+      if (closed) return true;
+      int ms = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count());
+      if (ms <= 0) return false;
+      pollfd p{fd, POLLIN, 0};
+      int pr = ::poll(&p, 1, ms);
+      if (pr < 0 && errno == EINTR) continue;
+      if (pr <= 0) return false;
+      ssize_t n = ::recv(fd, buf.data(), buf.size(), 0);
+      if (n < 0 && (errno == EINTR || errno == EAGAIN)) continue;
+      if (n <= 0) return false;
+      if (nghttp2_session_mem_recv(s, buf.data(), static_cast<size_t>(n)) < 0) return false;
+    }
+  }
+};
+
+GrpcChannelPool::GrpcChannelPool(int timeout_ms) : timeout_ms_(timeout_ms) {}
+GrpcChannelPool::~GrpcChannelPool() = default;
+
+uint64_t GrpcChannelPool::connects() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return connects_;
+}
+
+std::unique_ptr<GrpcChannelPool::Conn> GrpcChannelPool::take(const std::string& target, int timeout_ms,
+                                                             std::string* err) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& v = idle_[target];
+    if (!v.empty()) {
+      auto c = std::move(v.back());
+      v.pop_back();
+      return c;
+    }
+    ++connects_;
+  }
+  auto c = std::make_unique<Conn>();
+  c->authority = strip_scheme(target);
+  c->fd = connect_to(c->authority, timeout_ms, err);
+  if (c->fd < 0 || !c->init(err)) return nullptr;
+  return c;
+}
+
+void GrpcChannelPool::give(const std::string& target, std::unique_ptr<Conn> c) {
+  std::lock_guard<std::mutex> g(mu_);
+  idle_[target].push_back(std::move(c));
+}
+
+GrpcResult GrpcChannelPool::call(const std::string& target, const std::string& path, const std::string& request,
+                                 const std::string& request_id, int timeout_ms) {
+  GrpcResult res;
+  if (timeout_ms < 0) timeout_ms = timeout_ms_;
+  std::string err;
+  std::unique_ptr<Conn> c = take(target, timeout_ms, &err);
+  if (!c) {
+    res.message = err;
+    return res;
+  }
+  c->deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
+  c->out.resize(5 + request.size());
+  c->out[0] = 0;
+  uint32_t be = htonl(static_cast<uint32_t>(request.size()));
+  std::memcpy(&c->out[1], &be, 4);
+  std::memcpy(&c->out[5], request.data(), request.size());
+  c->off = 0;
+  c->in.clear();
+  c->closed = c->reset = false;
+  c->grpc_status = -1;
+  c->grpc_message.clear();
+  static const std::string k_m = ":method", v_m = "POST", k_s = ":scheme", v_s = "http", k_p = ":path",
+                           k_a = ":authority", k_ct = "content-type", v_ct = "application/grpc", k_te = "te",
+                           v_te = "trailers", k_ua = "user-agent", v_ua = "dfs-native-client/1",
+                           k_rid = "x-request-id";
+  std::vector<nghttp2_nv> h = {nv(k_m, v_m), nv(k_s, v_s), nv(k_p, path), nv(k_a, c->authority),
+                               nv(k_ct, v_ct), nv(k_te, v_te), nv(k_ua, v_ua)};
+  if (!request_id.empty()) h.push_back(nv(k_rid, request_id));
+  nghttp2_data_provider dp;
+  dp.source.ptr = nullptr;
+  dp.read_callback = &Conn::read_body;
+  c->sid = nghttp2_submit_request(c->s, nullptr, h.data(), h.size(), &dp, nullptr);
+  if (c->sid < 0 || !c->pump()) {
+    res.message = "transport failure calling " + path + " on " + target;
+    return res;  // the connection is dropped
+  }
+  res.transport_ok = true;
+  if (c->grpc_status < 0) {
+    res.status = c->reset ? 14 : 13;  // UNAVAILABLE on a reset stream, else INTERNAL
+    res.message = c->reset ? "stream reset" : "response without grpc-status";
+  } else if (c->grpc_status != 0) {
+    res.status = c->grpc_status;
+    res.message = std::move(c->grpc_message);
+  } else if (c->in.size() < 5) {
+    res.status = 13;
+    res.message = "empty response";
+  } else {
+    uint32_t n;
+    std::memcpy(&n, &c->in[1], 4);
+    n = ntohl(n);
+    if (c->in[0] != 0 || c->in.size() < 5 + static_cast<size_t>(n)) {
+      res.status = 13;
+      res.message = "malformed or compressed response";
+    } else {
+      res.status = 0;
+      res.message = c->in.substr(5, n);
+    }
+  }
+  c->in.clear();
+  c->in.shrink_to_fit();
+  std::string().swap(c->out);
+  if (!c->reset && nghttp2_session_want_read(c->s)) give(target, std::move(c));
+  return res;
+}
+
+}  // namespace dfs

@@ -1113,9 +1113,11 @@ int MasterCore::create_file(const std::string& raw, std::string* out) {
     std::string err;
     if (!place(r.ec_data_shards, r.ec_parity_shards, r.preferred_chunk_server, &sel, &err))
       return (*out = err, UNAVAILABLE);
-    if (!node || !node->is_leader()) {
+    // no Raft entry here, so leadership must be known fresh: a leader cut off from its
+    // majority (possibly already replaced) would hand out a stale master term
+    if (!node || !node->is_leader() || !node->has_lease()) {
       resp.error_message = "Not Leader";
-      resp.leader_hint = node ? node->leader_address() : "";
+      resp.leader_hint = node && !node->is_leader() ? node->leader_address() : "";
       return reply();
     }
     resp.success = true;

@@ -306,6 +306,18 @@ void Node::start_election_locked(bool transfer, std::string* hs, std::string* vo
   *vote_args = a.dump();
 }
 
+bool Node::has_lease() const {
+  std::lock_guard<std::mutex> g(mu_);
+  if (role_ != Role::Leader) return false;
+  // a majority answered us within election_lo: with pre-vote and leader stickiness none of
+  // them votes for anyone else before election_lo passes, so no newer leader exists yet
+  const auto horizon = Clock::now() - std::chrono::microseconds(static_cast<int64_t>(opt_.election_lo * 1e6));
+  std::set<int> fresh = {opt_.id};
+  for (auto& kv : ack_at_)
+    if (kv.second >= horizon) fresh.insert(kv.first);
+  return config_.has_joint_majority(fresh);
+}
+
 bool Node::leader_recent_locked() const {
   if (role_ == Role::Leader) return true;
   if (leader_id_ < 0) return false;
@@ -435,6 +447,7 @@ void Node::become_leader_locked() {
   uint64_t nxt = last_index_locked() + 1;
   next_index_.clear();
   match_index_.clear();
+  ack_at_.clear();
   for (int p : peers_locked()) {
     next_index_[p] = nxt;
     match_index_[p] = 0;
@@ -614,6 +627,7 @@ bool Node::replicate_once(Peer* p) {
     return false;
   }
   std::string reply;
+  const Clock::time_point sent_at = Clock::now();
   if (!host_->send(addr, "append", body, &reply)) return false;
   Json r;
   try {
@@ -631,6 +645,9 @@ bool Node::replicate_once(Peer* p) {
   {
     std::lock_guard<std::mutex> g(mu_);
     if (role_ != Role::Leader || current_term_ != term) return false;
+    // any same-term answer means this follower still takes us as leader (as of sent_at)
+    Clock::time_point& ack = ack_at_[p->id];
+    ack = std::max(ack, sent_at);
     if (r["success"].as_bool()) {
       uint64_t m = r.has("match_index") ? r["match_index"].as_u64() : prev + count;
       uint64_t& mi = match_index_[p->id];

@@ -137,6 +137,9 @@ class Node {
   // Introspection (thread-safe snapshots of volatile state).
   Role role() const;
   bool is_leader() const { return role() == Role::Leader; }
+  // Leader whose leadership a majority confirmed within election_lo (leader lease): safe to
+  // answer without a Raft round trip (deferred block placement, see MasterCore::create_file).
+  bool has_lease() const;
   uint64_t term() const;
   int leader_id() const;
   std::string leader_address() const;
@@ -261,6 +264,7 @@ class Node {
   uint64_t unsynced_from_ = 0, durable_index_ = 0;
   uint64_t hb_round_ = 0;
   std::map<int, uint64_t> acked_round_;
+  std::map<int, Clock::time_point> ack_at_;  // leader: send time of each follower's latest same-term answer
   std::vector<ReadWaiter> read_waiters_;
   uint64_t leader_noop_index_ = 0;
   Clock::time_point election_deadline_;

@@ -100,7 +100,14 @@ class Client:
             fc = _native.FastClient(self.fastpath.name, self.local_chunkserver)
             if fc.ok:
                 self._fast = fc
-                self._sync_fast()
+        # native remote client (csrc/client_remote.cpp): the same single-block writes/reads for
+        # a client that is not co-located — every RPC over gRPC/TCP on the native HTTP/2 client
+        self._remote = None
+        if (self._fast is None and self.defer_create and not self.tls
+                and os.environ.get("DFS_NATIVE_REMOTE", "1") == "1"):
+            self._remote = _native.RemoteClient(4, int(data_timeout * 1000))
+        self.remote_ops = 0
+        self._sync_fast()
 
     def _phase(self, name: str, t0: float) -> float:
         t1 = time.perf_counter()
@@ -167,14 +174,15 @@ class Client:
         self._sync_fast()
 
     def _sync_fast(self) -> None:
-        if self._fast is not None:
-            with self._map_lock:
-                js = json.dumps(self.shard_map.to_json()) if self.shard_map.shards else ""
-            self._fast.set_routing(js, [self.resolve_url(a) for a in self.master_addrs])
+        for nc in (self._fast, getattr(self, "_remote", None)):
+            if nc is not None:
+                with self._map_lock:
+                    js = json.dumps(self.shard_map.to_json()) if self.shard_map.shards else ""
+                nc.set_routing(js, [self.resolve_url(a) for a in self.master_addrs])
 
     def add_host_alias(self, alias: str, real: str) -> None:
         self.host_aliases[alias] = real
-        self._fast = None  # aliases rewrite addresses: keep every call on the Python path
+        self._fast = self._remote = None  # aliases rewrite addresses: keep every call on the Python path
 
     def resolve_url(self, url: str) -> str:
         for alias, real in self.host_aliases.items():
@@ -184,6 +192,7 @@ class Client:
 
     def close(self) -> None:
         self._fast = None  # unmaps and unlinks the native client's shared-memory arena
+        self._remote = None
         self.pool.close()
         self._exec.shutdown(wait=False)
         if self._arena is not None:
@@ -387,10 +396,15 @@ class Client:
         FileMetadata.attributes by the same CompleteFile; `etag` is the caller's MD5 hex of
         `data` (skips recomputing it)."""
         fc = self._fast if not attributes else None
+        if fc is None and not attributes:
+            fc = self._remote
         if fc is not None:
             st, replicas, msg, times = fc.write(dest, data, current_request_id.get())
             if st == 0:
-                self.fp_ops += 1
+                if fc is self._remote:
+                    self.remote_ops += 1
+                else:
+                    self.fp_ops += 1
                 if self.phase_times is not None:
                     for name, v in zip(("crc", "create", "write", "md5_wait", "complete"), times):
                         self.phase_times.setdefault(name, []).append(v)
@@ -596,10 +610,15 @@ class Client:
         """`info`: the file's FileMetadata when the caller already fetched it (no second
         GetFileInfo)."""
         fc = self._fast if info is None else None
+        if fc is None and info is None and not self.hedge_delay_ms:
+            fc = self._remote
         if fc is not None:
             st, data, msg, times = fc.read(path, current_request_id.get())
             if st == 0:
-                self.fp_ops += 1
+                if fc is self._remote:
+                    self.remote_ops += 1
+                else:
+                    self.fp_ops += 1
                 if self.phase_times is not None:
                     for name, v in zip(("getinfo", "read"), times):
                         self.phase_times.setdefault(name, []).append(v)

@@ -108,6 +108,16 @@ if [ "$STEP" = "grpcab" ]; then
   DFS_CS_GRPC=grpcio timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_grpcio.json 2> gpurun_out/ab_grpcio.err && \
   DFS_CS_GRPC=native timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 3 > gpurun_out/ab_native.json 2> gpurun_out/ab_native.err || exit $?
 fi
+if [ "$STEP" = "mgrpcab" ]; then
+  # remote-client phase: MasterService on grpcio vs the native server (chunkserver native in both)
+  DFS_MASTER_GRPC=grpcio timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 4 > gpurun_out/mab_grpcio.json 2> gpurun_out/mab_grpcio.err && \
+  DFS_MASTER_GRPC=native timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 4 > gpurun_out/mab_native.json 2> gpurun_out/mab_native.err || exit $?
+fi
+if [ "$STEP" = "remoteab" ]; then
+  # remote-client phase: Python grpcio client vs the native C++ client (servers native in both)
+  DFS_NATIVE_REMOTE=0 timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 4 > gpurun_out/rab_python.json 2> gpurun_out/rab_python.err && \
+  DFS_NATIVE_REMOTE=1 timeout -k 10 600 python bench.py --steps 2 --warmup 1 --remote-steps 4 > gpurun_out/rab_native.json 2> gpurun_out/rab_native.err || exit $?
+fi
 if [ "$STEP" = "s3" ]; then
   # config 5 with the single-process gateway vs the multi-process one (A/B of S3_WORKERS)
   S3_WORKERS=1 timeout -k 10 400 python bench_configs.py config5 --gpu 0 > gpurun_out/config5_w1.json 2> gpurun_out/config5_w1.err && \
