@@ -449,7 +449,8 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("writes", &FastClient::writes)
       .def_property_readonly("reads", &FastClient::reads)
       .def("set_routing", &FastClient::set_routing, py::call_guard<py::gil_scoped_release>())
-      .def("write", [](FastClient& c, const std::string& path, py::buffer data, const std::string& rid) {
+      .def("write", [](FastClient& c, const std::string& path, py::buffer data, const std::string& rid,
+                         const std::map<std::string, std::string>& attrs) {
         py::buffer_info bi = data.request();
         int replicas = 0;
         std::string msg;
@@ -458,12 +459,14 @@ void bind_meta(py::module_& m) {
         {
           py::gil_scoped_release r;
           st = c.write(path, static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize),
-                       &replicas, &msg, &t, rid);
+                       &replicas, &msg, &t, rid, attrs.empty() ? nullptr : &attrs);
         }
         return py::make_tuple(static_cast<int>(st), replicas, msg,
                               py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete));
-      }, py::arg("path"), py::arg("data"), py::arg("request_id") = "")
-      .def("read", [](FastClient& c, const std::string& path, const std::string& rid) {
+      }, py::arg("path"), py::arg("data"), py::arg("request_id") = "",
+         py::arg("attributes") = std::map<std::string, std::string>())
+      .def("read", [](FastClient& c, const std::string& path, const std::string& rid, uint64_t offset,
+                        uint64_t length) {
         int64_t slot = -1;
         uint64_t n = 0;
         std::string msg;
@@ -471,7 +474,7 @@ void bind_meta(py::module_& m) {
         FastClient::Status st;
         {
           py::gil_scoped_release r;
-          st = c.read(path, &slot, &n, &msg, &t, rid);
+          st = c.read(path, &slot, &n, &msg, &t, rid, offset, length);
         }
         py::object data = py::none();
         if (st == FastClient::Ok) {
@@ -486,7 +489,7 @@ void bind_meta(py::module_& m) {
           }
         }
         return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
-      }, py::arg("path"), py::arg("request_id") = "");
+      }, py::arg("path"), py::arg("request_id") = "", py::arg("offset") = 0, py::arg("length") = 0);
 
   // ---------------- native remote client (every RPC over gRPC/TCP, client_remote.h)
   py::class_<RemoteClient>(m, "RemoteClient")
@@ -495,7 +498,8 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("reads", &RemoteClient::reads)
       .def_property_readonly("connects", &RemoteClient::connects)
       .def("set_routing", &RemoteClient::set_routing, py::call_guard<py::gil_scoped_release>())
-      .def("write", [](RemoteClient& c, const std::string& path, py::buffer data, const std::string& rid) {
+      .def("write", [](RemoteClient& c, const std::string& path, py::buffer data, const std::string& rid,
+                         const std::map<std::string, std::string>& attrs) {
         py::buffer_info bi = data.request();
         int replicas = 0;
         std::string msg;
@@ -504,22 +508,24 @@ void bind_meta(py::module_& m) {
         {
           py::gil_scoped_release r;
           st = c.write(path, static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize),
-                       &replicas, &msg, &t, rid);
+                       &replicas, &msg, &t, rid, attrs.empty() ? nullptr : &attrs);
         }
         return py::make_tuple(static_cast<int>(st), replicas, msg,
                               py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete));
-      }, py::arg("path"), py::arg("data"), py::arg("request_id") = "")
-      .def("read", [](RemoteClient& c, const std::string& path, const std::string& rid) {
+      }, py::arg("path"), py::arg("data"), py::arg("request_id") = "",
+         py::arg("attributes") = std::map<std::string, std::string>())
+      .def("read", [](RemoteClient& c, const std::string& path, const std::string& rid, uint64_t offset,
+                          uint64_t length) {
         std::string out, msg;
         FastClient::Times t;
         FastClient::Status st;
         {
           py::gil_scoped_release r;
-          st = c.read(path, &out, &msg, &t, rid);
+          st = c.read(path, &out, &msg, &t, rid, offset, length);
         }
         py::object data = st == FastClient::Ok ? py::object(py::bytes(out)) : py::object(py::none());
         return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
-      }, py::arg("path"), py::arg("request_id") = "");
+      }, py::arg("path"), py::arg("request_id") = "", py::arg("offset") = 0, py::arg("length") = 0);
 
   // raw native gRPC unary call (interop tests)
   m.def("grpc_call", [](const std::string& target, const std::string& path, py::bytes req, const std::string& rid,

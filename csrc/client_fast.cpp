@@ -311,7 +311,8 @@ bool FastClient::fp_call(uint8_t op, const std::string& body, uint8_t* status, u
 }
 
 FastClient::Status FastClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
-                                     std::string* msg, Times* t, const std::string& rid_in) {
+                                     std::string* msg, Times* t, const std::string& rid_in,
+                                     const std::map<std::string, std::string>* attrs) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.client.write");
@@ -410,6 +411,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   done.ec_data_shards = alloc.ec_data_shards;
   done.ec_parity_shards = alloc.ec_parity_shards;
   done.blocks.push_back(alloc.block);
+  if (attrs) done.attributes = *attrs;
   if (!call(sock, "/dfs.MasterService/CompleteFile", rid, done.str(), &code, &raw)) {
     *msg = "Failed to complete file: master connection lost";
     return Failed;
@@ -430,7 +432,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
 }
 
 FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg,
-                                    Times* t, const std::string& rid_in) {
+                                    Times* t, const std::string& rid_in, uint64_t offset, uint64_t length) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.client.read");
@@ -457,7 +459,15 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
     *n = 0;
     return Ok;
   }
-  if (m.blocks.size() != 1 || m.blocks[0].ec_data_shards > 0 || m.size > slot_bytes_) return NotHandled;
+  if (m.blocks.size() != 1 || m.blocks[0].ec_data_shards > 0) return NotHandled;
+  if (length > 0) {
+    if (offset >= m.size) return NotHandled;  // the Python path reports the range error
+    length = std::min<uint64_t>(length, m.size - offset);
+  } else {
+    offset = 0;
+  }
+  const uint64_t want = length > 0 ? length : m.size;
+  if (want > slot_bytes_) return NotHandled;
   const pb::BlockInfo& b = m.blocks[0];
   bool local = false;
   for (auto& l : b.locations) local |= strip_scheme(l) == local_cs_;
@@ -465,8 +475,8 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
   int64_t s = acquire(slot_bytes_);
   if (s < 0) return NotHandled;
   std::string body;
-  put<uint64_t>(body, 0);  // offset
-  put<uint64_t>(body, 0);  // length 0 = the whole block
+  put<uint64_t>(body, offset);
+  put<uint64_t>(body, length);  // 0 = the whole block
   put<uint64_t>(body, static_cast<uint64_t>(s));
   put<uint64_t>(body, slot_bytes_);
   put_str(body, b.block_id);

@@ -45,12 +45,14 @@ class FastClient {
   void set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters);
 
   // `rid`: the request id carried on every hop (minted here when empty).
+  // `attrs`: FileMetadata.attributes set by the same CompleteFile (nullptr = none).
   Status write(const std::string& path, const uint8_t* data, size_t n, int* replicas, std::string* msg, Times* t,
-               const std::string& rid = "");
+               const std::string& rid = "", const std::map<std::string, std::string>* attrs = nullptr);
   // On Ok the block sits in slot `*slot` (`*n` bytes); the caller copies it out and calls
   // release(*slot).
+  // `length` > 0: only [offset, offset + length) (clipped to the file), the K3 range read.
   Status read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg, Times* t,
-              const std::string& rid = "");
+              const std::string& rid = "", uint64_t offset = 0, uint64_t length = 0);
   const uint8_t* slot_ptr(int64_t slot) const { return base_ + slot; }
   void release(int64_t slot);
 

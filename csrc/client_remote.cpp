@@ -144,7 +144,8 @@ bool RemoteClient::master_call(const std::string& path, const std::string& metho
 }
 
 FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
-                                       std::string* msg, Times* t, const std::string& rid_in) {
+                                       std::string* msg, Times* t, const std::string& rid_in,
+                                       const std::map<std::string, std::string>* attrs) {
   const std::string rid = rid_in.empty() ? request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.remote.write");
@@ -234,6 +235,7 @@ FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* d
   done.ec_data_shards = alloc.ec_data_shards;
   done.ec_parity_shards = alloc.ec_parity_shards;
   done.blocks.push_back(alloc.block);
+  if (attrs) done.attributes = *attrs;
   if (!master_call(path, "CompleteFile", done.str(), rid, &code, &raw)) {
     *msg = "Failed to complete file: master unreachable";
     return FastClient::Failed;
@@ -254,7 +256,7 @@ FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* d
 }
 
 FastClient::Status RemoteClient::read(const std::string& path, std::string* out, std::string* msg, Times* t,
-                                      const std::string& rid_in) {
+                                      const std::string& rid_in, uint64_t offset, uint64_t length) {
   const std::string rid = rid_in.empty() ? request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.remote.read");
@@ -279,11 +281,18 @@ FastClient::Status RemoteClient::read(const std::string& path, std::string* out,
     return FastClient::Ok;
   }
   if (m.blocks.size() != 1 || m.blocks[0].ec_data_shards > 0) return FastClient::NotHandled;
+  if (length > 0) {
+    if (offset >= m.size) return FastClient::NotHandled;  // the Python path reports the range error
+    length = std::min<uint64_t>(length, m.size - offset);
+  } else {
+    offset = 0;
+    length = m.size;
+  }
   const pb::BlockInfo& b = m.blocks[0];
   pb::ReadBlockRequest rreq;
   rreq.block_id = b.block_id;
-  rreq.offset = 0;
-  rreq.length = b.size ? b.size : m.size;
+  rreq.offset = offset;
+  rreq.length = length;
   const std::string wire = rreq.str();
   for (const std::string& loc : b.locations) {
     GrpcResult r = pool_.call(loc, "/dfs.ChunkServerService/ReadBlock", wire, rid);

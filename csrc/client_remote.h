@@ -41,8 +41,9 @@ class RemoteClient {
   void set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters);
 
   Status write(const std::string& path, const uint8_t* data, size_t n, int* replicas, std::string* msg, Times* t,
-               const std::string& rid = "");
-  Status read(const std::string& path, std::string* out, std::string* msg, Times* t, const std::string& rid = "");
+               const std::string& rid = "", const std::map<std::string, std::string>* attrs = nullptr);
+  Status read(const std::string& path, std::string* out, std::string* msg, Times* t, const std::string& rid = "",
+              uint64_t offset = 0, uint64_t length = 0);
 
   uint64_t writes() const { return writes_.load(); }
   uint64_t reads() const { return reads_.load(); }

@@ -395,11 +395,9 @@ class Client:
         replicas_written (reference mod.rs:225-494). Extensions: `attributes` are stored in
         FileMetadata.attributes by the same CompleteFile; `etag` is the caller's MD5 hex of
         `data` (skips recomputing it)."""
-        fc = self._fast if not attributes else None
-        if fc is None and not attributes:
-            fc = self._remote
+        fc = self._fast if self._fast is not None else self._remote
         if fc is not None:
-            st, replicas, msg, times = fc.write(dest, data, current_request_id.get())
+            st, replicas, msg, times = fc.write(dest, data, current_request_id.get(), attributes or {})
             if st == 0:
                 if fc is self._remote:
                     self.remote_ops += 1
@@ -609,9 +607,7 @@ class Client:
     def get_file_content(self, path: str, info=None) -> bytes:
         """`info`: the file's FileMetadata when the caller already fetched it (no second
         GetFileInfo)."""
-        fc = self._fast if info is None else None
-        if fc is None and info is None and not self.hedge_delay_ms:
-            fc = self._remote
+        fc = self._native_reader()
         if fc is not None:
             st, data, msg, times = fc.read(path, current_request_id.get())
             if st == 0:
@@ -648,7 +644,24 @@ class Client:
 
     get_file_concurrent = get_file
 
+    def _native_reader(self):
+        """The native client for reads, if any (hedged reads stay on the Python path)."""
+        if self._fast is not None:
+            return self._fast
+        return self._remote if not self.hedge_delay_ms else None
+
     def read_file_range(self, path: str, offset: int, length: int, info=None) -> bytes:
+        fc = self._native_reader()
+        if fc is not None and length > 0:
+            st, data, msg, _times = fc.read(path, current_request_id.get(), offset, length)
+            if st == 0:
+                if fc is self._remote:
+                    self.remote_ops += 1
+                else:
+                    self.fp_ops += 1
+                return data
+            if st == 2:
+                raise DfsError(msg)
         meta = info if info is not None else self.get_file_info(path)
         if meta is None:
             raise DfsError("File not found")

@@ -171,6 +171,15 @@ def test_native_remote_client_interop(native, server_impl):
             for p, d in blobs.items():
                 assert c.get_file_content(p) == d
             assert c.remote_ops == 2 * len(blobs)
+            # ranged reads and attributes ride the native client too
+            big = blobs[f"/nr/{server_impl}/f4"]
+            assert c.read_file_range(f"/nr/{server_impl}/f4", 1_000_003, 70_001) == big[1_000_003:1_070_004]
+            assert c.read_file_range(f"/nr/{server_impl}/f4", len(big) - 5, 100) == big[-5:]
+            c.create_file_from_buffer(b"attr", f"/nr/{server_impl}/a", attributes={"ETag": '"x"', "k": "v"})
+            assert dict(c.get_file_info(f"/nr/{server_impl}/a").attributes) == {"ETag": '"x"', "k": "v"}
+            assert c.remote_ops == 2 * len(blobs) + 3
+            with pytest.raises(DfsError, match="exceeds"):
+                c.read_file_range(f"/nr/{server_impl}/f4", len(big) + 1, 10)
             info = c.get_file_info(f"/nr/{server_impl}/f3")
             assert len(info.blocks[0].locations) == 3 and info.etag_md5  # chained to all replicas, MD5 etag
             with pytest.raises(DfsError, match="not found"):
