@@ -270,7 +270,7 @@ void Node::reset_election_timer_locked() {
 void Node::ticker_loop() {
   auto hb = std::chrono::microseconds(static_cast<int64_t>(opt_.heartbeat * 1e6));
   while (running_) {
-    bool elect = false, transfer = false;
+    bool elect = false;
     {
       std::unique_lock<std::mutex> lk(mu_);
       tick_cv_.wait_for(lk, hb, [&] { return !running_ || tick_now_; });
@@ -280,12 +280,10 @@ void Node::ticker_loop() {
         broadcast_locked();
       } else if (Clock::now() >= election_deadline_ && config_.is_voter(opt_.id)) {
         elect = true;
-        transfer = transfer_election_;
-        transfer_election_ = false;
       }
     }
-    if (elect && opt_.pre_vote && !transfer) run_pre_vote();
-    else if (elect) run_election(transfer);
+    if (elect && opt_.pre_vote) run_pre_vote();
+    else if (elect) run_election(false);
   }
 }
 
@@ -1145,17 +1143,17 @@ std::string Node::on_snapshot(const Json& a) {
 }
 
 std::string Node::on_timeout_now(const Json& a) {
-  std::lock_guard<std::mutex> g(mu_);
   Json out = Json::object();
-  bool ok = a["term"].as_u64() >= current_term_ && role_ != Role::Leader;
-  if (ok) {
-    election_deadline_ = Clock::now();  // the ticker starts the election right away
-    transfer_election_ = true;
-    tick_now_ = true;
-    tick_cv_.notify_all();
+  bool ok;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ok = a["term"].as_u64() >= current_term_ && role_ != Role::Leader && config_.is_voter(opt_.id);
+    out.set("term", current_term_);
+    out.set("success", ok);
   }
-  out.set("term", current_term_);
-  out.set("success", ok);
+  // start the (transfer) election here and now: handing it to the ticker raced with the old
+  // leader's next heartbeat, which re-arms the election timer before the ticker looks
+  if (ok) run_election(true);
   return out.dump();
 }
 

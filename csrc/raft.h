@@ -271,7 +271,6 @@ class Node {
   Clock::time_point leader_contact_{};  // last accepted AppendEntries / InstallSnapshot
   uint64_t prevote_round_ = 0;
   std::set<int> prevotes_;
-  bool transfer_election_ = false;  // next election was asked for by TimeoutNow
   bool tick_now_ = false;
   std::mt19937_64 rng_;
 
