@@ -7,6 +7,8 @@
 #include <pybind11/stl.h>
 
 #include <cstring>
+#include <map>
+#include <set>
 
 #include "client_fast.h"
 #include "client_remote.h"
@@ -74,6 +76,21 @@ class PyRaftHost : public raft::Host {
     }
   }
   bool send(const std::string& addr, const std::string& kind, const std::string& body, std::string* reply) override {
+    std::string ep;
+    {
+      std::lock_guard<std::mutex> lk(peers_mu_);
+      if (blocked_.count(addr)) return false;
+      auto it = endpoints_.find(addr);
+      if (it != endpoints_.end()) ep = it->second;
+    }
+    if (!ep.empty()) {
+      // native peer path: the peer's native gRPC server hands the JSON straight to its node
+      // (reference timeouts: 1.5 s per RPC, snapshots get longer)
+      GrpcResult r = peers_.call(ep, "/dfs.RaftPeer/" + kind, body, "", kind == "snapshot" ? 30000 : 1500);
+      if (!r.transport_ok || r.status != 0) return false;
+      *reply = std::move(r.message);
+      return true;
+    }
     py::gil_scoped_acquire g;
     try {
       py::object r = host_->obj.attr("send")(addr, kind, py::str(body));
@@ -83,6 +100,15 @@ class PyRaftHost : public raft::Host {
     } catch (py::error_already_set& e) {
       return false;
     }
+  }
+  void set_peer_endpoint(const std::string& addr, const std::string& endpoint) override {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    if (endpoint.empty()) endpoints_.erase(addr);
+    else endpoints_[addr] = endpoint;
+  }
+  void set_blocked(const std::vector<std::string>& addrs) override {
+    std::lock_guard<std::mutex> lk(peers_mu_);
+    blocked_ = std::set<std::string>(addrs.begin(), addrs.end());
   }
   void backup(const std::string& url, const std::string& data) override {
     py::gil_scoped_acquire g;
@@ -95,6 +121,10 @@ class PyRaftHost : public raft::Host {
  private:
   std::shared_ptr<PyRef> host_;
   std::shared_ptr<raft::StateMachine> sm_;
+  std::mutex peers_mu_;
+  std::map<std::string, std::string> endpoints_;  // member address -> native gRPC endpoint
+  std::set<std::string> blocked_;
+  GrpcChannelPool peers_{1500};
 };
 
 // Read a node property with the GIL released (the getter may wait on the node mutex).
@@ -211,6 +241,10 @@ void bind_meta(py::module_& m) {
         return s;
       })
       .def("info_json", &raft::Node::info_json, py::call_guard<py::gil_scoped_release>())
+      .def("set_peer_endpoint", [](raft::Node& n, const std::string& addr, const std::string& ep) {
+        n.host().set_peer_endpoint(addr, ep);
+      })
+      .def("set_blocked", [](raft::Node& n, const std::vector<std::string>& addrs) { n.host().set_blocked(addrs); })
       .def_property_readonly("wal_syncs", &raft::Node::wal_syncs)
       .def_property_readonly("wal_bytes", &raft::Node::wal_bytes);
 
@@ -388,7 +422,7 @@ void bind_meta(py::module_& m) {
   struct NativeGrpcMaster {
     std::shared_ptr<PyRef> fallback;
     std::unique_ptr<GrpcServer> srv;
-    std::atomic<uint64_t> native_calls{0}, fallback_calls{0};
+    std::atomic<uint64_t> native_calls{0}, fallback_calls{0}, raft_calls{0};
   };
   py::class_<NativeGrpcMaster>(m, "NativeGrpcMasterServer")
       .def(py::init([](std::shared_ptr<MasterCore> core, const std::string& host, int port, py::object fallback,
@@ -398,7 +432,14 @@ void bind_meta(py::module_& m) {
              auto fb = n->fallback;
              NativeGrpcMaster* self = n.get();
              static const std::string kPrefix = "/dfs.MasterService/";
+             static const std::string kRaft = "/dfs.RaftPeer/";
              n->srv = std::make_unique<GrpcServer>(host, port, [core, fb, self](const GrpcCall& c) -> GrpcReply {
+               if (c.path.compare(0, kRaft.size(), kRaft) == 0) {  // Raft peer RPC: no Python at all
+                 GrpcReply r;
+                 r.status = core->raft_rpc(c.path.substr(kRaft.size()), c.message, &r.message);
+                 self->raft_calls++;
+                 return r;
+               }
                if (c.path.compare(0, kPrefix.size(), kPrefix) == 0) {
                  std::string method = c.path.substr(kPrefix.size());
                  if (core->native_method(method)) {
@@ -436,6 +477,7 @@ void bind_meta(py::module_& m) {
         d["native_grpc_calls"] = n.srv->calls();
         d["native_grpc_native"] = n.native_calls.load();
         d["native_grpc_fallback"] = n.fallback_calls.load();
+        d["native_raft_rpcs"] = n.raft_calls.load();
         return d;
       });
 

@@ -790,6 +790,18 @@ std::map<std::string, uint64_t> MasterCore::take_request_counts() {
   return out;
 }
 
+int MasterCore::raft_rpc(const std::string& kind, const std::string& body, std::string* out) {
+  raft::Node* node = node_.load();
+  if (!node) return (*out = "raft node not attached", UNAVAILABLE);
+  try {
+    *out = node->handle(kind, body);
+    return OK;
+  } catch (const std::exception& e) {
+    *out = e.what();
+    return INTERNAL;
+  }
+}
+
 std::vector<MasterCore::HealAction> MasterCore::heal_scan(
     int rf, const std::vector<std::string>& live, const std::map<std::string, std::vector<std::string>>& bad,
     const std::set<std::pair<std::string, std::string>>& queued) const {

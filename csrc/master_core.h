@@ -127,6 +127,10 @@ class MasterCore : public raft::StateMachine {
                                     const std::map<std::string, std::vector<std::string>>& bad,
                                     const std::set<std::pair<std::string, std::string>>& queued) const;
 
+  // Raft peer RPC (vote / append / snapshot / timeout_now, JSON) for the attached node, as
+  // served by the native gRPC server on /dfs.RaftPeer/<kind>.
+  int raft_rpc(const std::string& kind, const std::string& body, std::string* out);
+
   void set_access_stats(bool on, int flush_ms);
   uint64_t requests() const { return requests_.load(); }
 

@@ -92,6 +92,14 @@ class Host {
     (void)url;
     (void)data;
   }
+  // Optional native peer path: RPCs to `addr` (a member address) go straight to the peer's
+  // native endpoint `endpoint` ("" = back to the default transport); `blocked` addresses
+  // are unreachable (partition injection for chaos tests).
+  virtual void set_peer_endpoint(const std::string& addr, const std::string& endpoint) {
+    (void)addr;
+    (void)endpoint;
+  }
+  virtual void set_blocked(const std::vector<std::string>& addrs) { (void)addrs; }
 };
 
 struct Options {
@@ -153,6 +161,7 @@ class Node {
   uint64_t wal_syncs() const { return wal_ ? wal_->syncs() : 0; }
   uint64_t wal_bytes() const { return wal_ ? wal_->size_bytes() : 0; }
   int id() const { return opt_.id; }
+  Host& host() const { return *host_; }
 
  private:
   struct Entry {

@@ -117,7 +117,8 @@ class MasterProcess:
                            fn=lambda: self.state.core.requests)
         self._native_grpc = None
         for key, help_ in (("native_grpc_calls", "gRPC calls served by the native HTTP/2 server"),
-                           ("native_grpc_fallback", "native gRPC calls handed to the Python handlers")):
+                           ("native_grpc_fallback", "native gRPC calls handed to the Python handlers"),
+                           ("native_raft_rpcs", "Raft peer RPCs received over the native server")):
             self.metrics.gauge(f"dfs_master_{key}", help_,
                                fn=lambda k=key: self._native_grpc.stats()[k] if self._native_grpc else 0)
 
@@ -143,9 +144,14 @@ class MasterProcess:
 
             return h
 
+        async def raft_endpoint(_):
+            # where this node takes Raft peer RPCs natively (/dfs.RaftPeer/* on its gRPC port)
+            return web.json_response({"grpc": self.client_addr if self._native_grpc is not None else ""})
+
         app.router.add_get("/health", health)
         app.router.add_get("/metrics", metrics)
         app.router.add_get("/raft/state", raft_state)
+        app.router.add_get("/raft/endpoint", raft_endpoint)
 
         async def shard_map(_):
             return web.json_response({"shard_id": self.svc.shard_id, "map": self.svc.shard_map.to_json()})
@@ -158,10 +164,35 @@ class MasterProcess:
             async def partition(req):
                 body = await req.json()
                 self.transport.blocked = {HttpTransport._base(a) for a in body.get("block", [])}
+                self.raft._core.set_blocked(sorted(self.transport.blocked))
                 return web.json_response({"blocked": sorted(self.transport.blocked)})
 
             app.router.add_post("/debug/partition", partition)
         return app
+
+    async def _resolve_native_peers(self) -> None:
+        """Learn each Raft peer's native endpoint (GET /raft/endpoint) and hand it to the
+        native node: from then on AppendEntries / RequestVote travel node-to-node over the
+        native HTTP/2 servers without touching Python on either side. Peers without one
+        (TLS, grpcio, older builds) stay on the HTTP/JSON transport."""
+        import aiohttp
+
+        known: dict[str, str] = {}
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=2)) as sess:
+            while True:
+                members = dict(self.raft.config.all_members())
+                for mid, addr in members.items():
+                    if mid == self.raft.id or addr in known:
+                        continue
+                    try:
+                        async with sess.get(addr.rstrip("/") + "/raft/endpoint") as r:
+                            ep = (await r.json(content_type=None)).get("grpc", "") if r.status == 200 else ""
+                    except Exception:  # noqa: BLE001 - peer not up yet: ask again later
+                        continue
+                    known[addr] = ep
+                    if ep:
+                        self.raft._core.set_peer_endpoint(addr, ep)
+                await asyncio.sleep(1.0)  # only members not resolved yet are asked
 
     async def run(self, ready_file: str | None = None) -> None:
         a = self.args
@@ -204,6 +235,9 @@ class MasterProcess:
             else:
                 log.warning("local RPC listener unavailable: %s", err)
         await self.raft.start()
+        resolver = None
+        if self._native_grpc is not None:
+            resolver = asyncio.get_running_loop().create_task(self._resolve_native_peers())
         if self.config_servers:
             await self.bg.register()
             await self.bg.refresh_shard_map()
@@ -219,6 +253,8 @@ class MasterProcess:
             with open(ready_file, "w") as f:
                 json.dump({"addr": a.addr, "http": self.self_http}, f)
         await stop.wait()
+        if resolver is not None:
+            resolver.cancel()
         await self.bg.stop()
         if self._local_srv is not None:
             await asyncio.get_running_loop().run_in_executor(None, self._local_srv.stop)

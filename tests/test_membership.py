@@ -7,6 +7,7 @@ the quorum (two originals are removed, so every later commit needs its ack), the
 and the last voter refuses its own removal. The removed processes keep running: pre-vote and
 leader stickiness (csrc/raft.cpp on_vote / run_pre_vote) keep them from bumping the term."""
 import time
+import urllib.request
 
 import pytest
 
@@ -113,6 +114,10 @@ def test_add_and_remove_master_via_cli(capsys):
             wait_for(lambda: len(info(pool, leader).members) == 1, what="single-member config")
             rc, out = cli(capsys, "-m", leader, "cluster", "remove-server", str(originals.index(leader) + 1))
             assert rc == 1 and "would leave cluster empty" in out
+            # Raft peer RPCs reached node 4 natively (/dfs.RaftPeer/* on its gRPC port)
+            text = urllib.request.urlopen(f"{http4}/metrics").read().decode()
+            vals = {ln.split()[0]: float(ln.split()[1]) for ln in text.splitlines() if ln and not ln.startswith("#")}
+            assert vals["dfs_master_native_raft_rpcs"] > 0
             c.create_file_from_buffer(b"solo", "/m/solo")
             assert c.get_file_content("/m/solo") == b"solo"
         finally:
