@@ -295,6 +295,8 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["spill_queue"] = t.spill_queue;
         d["evictions"] = t.evictions;
         d["promotions"] = t.promotions;
+        d["mirror_hits"] = t.mirror_hits;
+        d["mirror_bytes"] = t.mirror_bytes;
         d["crc_mismatches"] = t.crc_mismatches;
         d["gpu_kernel_launches"] = t.gpu_kernel_launches;
         d["disk_gate_waits"] = t.disk_gate_waits;

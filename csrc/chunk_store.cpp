@@ -564,6 +564,7 @@ void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, ui
       cv_.wait(lk, [&] { return it->second.pins == 0; });
       free_extent_locked(it->second);
       lru_remove_locked(it->second);
+      drop_mirror_locked(it->second);
       if (it->second.cold) {  // the new version lives in the hot dir
         ::unlink(data_path(id, true).c_str());
         ::unlink(meta_path(id, true).c_str());
@@ -681,8 +682,76 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
     return res;
   }
   insert_resident(id, ext, n, co.block_crc, sync_now, meta);
+  if (n <= kMirrorMax) set_mirror(id, data, n, *meta);
   res.ok = true;
   return res;
+}
+
+void ChunkStore::drop_mirror_locked(Block& b) {
+  if (!b.mirror) return;
+  mirror_bytes_ -= std::min<uint64_t>(mirror_bytes_, b.mirror->size());
+  b.mirror.reset();
+  b.mirror_meta.reset();
+}
+
+void ChunkStore::set_mirror(const std::string& id, const uint8_t* data, uint64_t n, const std::vector<uint8_t>& meta_be) {
+  auto bytes = std::make_shared<std::vector<uint8_t>>(data, data + n);
+  auto sums = std::make_shared<std::vector<uint32_t>>(meta_be.size() / 4);
+  for (size_t i = 0; i < sums->size(); ++i) {
+    uint32_t be;
+    std::memcpy(&be, meta_be.data() + 4 * i, 4);
+    (*sums)[i] = __builtin_bswap32(be);
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = index_.find(id);
+  if (it == index_.end() || it->second.size != n) return;
+  drop_mirror_locked(it->second);
+  it->second.mirror = std::move(bytes);
+  it->second.mirror_meta = std::move(sums);
+  mirror_bytes_ += n;
+  mirror_fifo_.push_back(id);
+  while (mirror_bytes_ > mirror_budget_ && !mirror_fifo_.empty()) {
+    auto v = index_.find(mirror_fifo_.front());
+    mirror_fifo_.pop_front();
+    if (v != index_.end()) drop_mirror_locked(v->second);
+  }
+}
+
+// Served from the small-block mirror: every 512 B slice the range touches is re-checked
+// against its CRC on the CPU (PCLMUL) before a byte is returned; a mismatch drops the mirror
+// and the caller takes the device path (which verifies and reports corruption as usual).
+bool ChunkStore::read_mirror(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out, ReadResult* r) {
+  std::shared_ptr<std::vector<uint8_t>> m;
+  std::shared_ptr<std::vector<uint32_t>> sums;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end() || !it->second.mirror) return false;
+    m = it->second.mirror;
+    sums = it->second.mirror_meta;
+  }
+  const uint64_t size = m->size();
+  if (offset >= size || offset + bytes > size) return false;  // the device path reports it
+  if (bytes) {
+    for (uint64_t s = offset / kSliceBytes, last = (offset + bytes - 1) / kSliceBytes; s <= last; ++s) {
+      uint64_t so = s * kSliceBytes, sl = std::min<uint64_t>(kSliceBytes, size - so);
+      if (s >= sums->size() || crc32(m->data() + so, sl) != (*sums)[s]) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = index_.find(id);
+        if (it != index_.end() && it->second.mirror == m) drop_mirror_locked(it->second);
+        return false;
+      }
+    }
+    std::memcpy(out, m->data() + offset, bytes);
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ++mirror_hits_;
+  }
+  r->status = ReadStatus::Ok;
+  r->total_size = size;
+  r->bytes = bytes;
+  return true;
 }
 
 bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64_t n, std::string* err) {
@@ -821,8 +890,9 @@ ReadResult ChunkStore::stat(const std::string& id, uint64_t offset, uint64_t len
 ReadResult ChunkStore::read_into(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out) {
   TraceRange tr("dfs.store.read");
   if (!gpu()) return read_host(id, offset, bytes, out);
-  HIP_OK(hipSetDevice(cfg_.device));
   ReadResult r;
+  if (read_mirror(id, offset, bytes, out, &r)) return r;
+  HIP_OK(hipSetDevice(cfg_.device));
   uint64_t size = 0;
   const uint8_t* d = pin_device(id, &size);
   if (!d) {
@@ -1399,6 +1469,7 @@ bool ChunkStore::remove(const std::string& id) {
     cold = it->second.cold;
     free_extent_locked(it->second);
     lru_remove_locked(it->second);
+    drop_mirror_locked(it->second);
     index_.erase(it);
   }
   cv_.notify_all();
@@ -1613,6 +1684,8 @@ StoreStats ChunkStore::stats() {
   s.gpu_kernel_launches = launches_.load();
   s.direct_dma = direct_dma_.load();
   s.staged_dma = staged_dma_.load();
+  s.mirror_hits = mirror_hits_;
+  s.mirror_bytes = mirror_bytes_;
   {
     std::lock_guard<std::mutex> rg(reg_mu_);
     for (auto& r : reg_) s.host_registered_bytes += r.second;
@@ -1654,6 +1727,7 @@ bool ChunkStore::debug_corrupt(const std::string& id, uint64_t offset) {
     off = it->second.dev_off;
     size = it->second.size;
     if (it->second.host) (*it->second.host)[offset] ^= 0xFF;
+    if (it->second.mirror) (*it->second.mirror)[offset] ^= 0xFF;
   }
   (void)size;
   std::string dp = data_path(id, cold);

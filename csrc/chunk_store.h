@@ -84,6 +84,8 @@ struct StoreStats {
   uint64_t direct_dma = 0;       // host<->HBM copies done straight from registered memory
   uint64_t staged_dma = 0;       // copies bounced through pinned staging buffers
   uint64_t host_registered_bytes = 0;
+  uint64_t mirror_hits = 0;      // small-block reads served from the verified host mirror
+  uint64_t mirror_bytes = 0;
 };
 
 // Group commit of data files: callers that finished writing share one syncfs() round.
@@ -203,6 +205,10 @@ class ChunkStore {
     bool in_lru = false;
     std::shared_ptr<std::vector<uint8_t>> host;  // host-mode cache
     std::shared_ptr<std::vector<uint8_t>> staged_meta;  // BE .meta image awaiting persist()
+    // small blocks (<= kMirrorMax): host copy of the bytes + slice CRCs, so a 4 KiB read is a
+    // verified memcpy instead of a GPU round trip (kernel launch + DMA + sync, ~30 us)
+    std::shared_ptr<std::vector<uint8_t>> mirror;
+    std::shared_ptr<std::vector<uint32_t>> mirror_meta;
   };
   struct Lane {
     hipStream_t stream = nullptr;
@@ -263,6 +269,13 @@ class ChunkStore {
   std::mutex lane_mu_;
   std::condition_variable lane_cv_;
   std::deque<std::string> spill_q_;
+  static constexpr uint64_t kMirrorMax = 64ull << 10;
+  uint64_t mirror_budget_ = 256ull << 20, mirror_bytes_ = 0;  // mu_
+  std::deque<std::string> mirror_fifo_;                       // mu_: eviction order
+  uint64_t mirror_hits_ = 0;                                  // mu_
+  void set_mirror(const std::string& id, const uint8_t* data, uint64_t n, const std::vector<uint8_t>& meta_be);
+  void drop_mirror_locked(Block& b);
+  bool read_mirror(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out, ReadResult* r);
   bool spill_paused_ = false;  // mu_
   std::vector<std::thread> spillers_;
   bool stop_ = false;

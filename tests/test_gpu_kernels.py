@@ -131,3 +131,23 @@ def test_gpu_reed_solomon(gstore):
         shards = [None if i in lost else s for i, s in enumerate(g)]
         assert erasure.decode(shards, k, m, n, gstore) == d
     assert gstore.stats()["gpu_kernel_launches"] > 0
+
+
+def test_gpu_small_block_mirror(gstore):
+    """Blocks <= 64 KiB keep a host copy: reads are a CPU-verified memcpy (no GPU round trip);
+    a corrupted slice is still caught (the mirror is dropped and the device path reports it)."""
+    d = os.urandom(40_000)
+    assert gstore.write("mir", d, zlib.crc32(d))[0]
+    h0 = gstore.stats()["mirror_hits"]
+    st, total, out, partial, bad, err = gstore.read("mir", 0, 0)
+    assert st == 0 and out == d and total == len(d)
+    st, total, out, partial, bad, err = gstore.read("mir", 1234, 4096)
+    assert st == 0 and out == d[1234:1234 + 4096] and not partial
+    assert gstore.stats()["mirror_hits"] == h0 + 2
+    assert gstore.debug_corrupt("mir", 30_000)
+    st, *_rest, err = gstore.read("mir", 0, 0)
+    assert st == 3 and "chunk 58" in err  # 30000 // 512
+    st, total, out, partial, bad, err = gstore.read("mir", 29_900, 200)
+    assert st == 0 and partial and bad == 58
+    assert gstore.stats()["mirror_hits"] == h0 + 2  # the damaged mirror served nothing
+    gstore.remove("mir")
