@@ -630,10 +630,22 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   std::string err;
   h2d_chunked(l, ext.ptr, data, n);
   CrcOut co;
-  bool ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err);
-  if (ok && S) {
-    HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+  bool ok = true;
+  if (n <= kMirrorMax) {
+    // a few slices: PCLMUL on the host bytes beats a kernel launch plus the .meta readback;
+    // the image goes up with the data in the same stream round trip
+    std::vector<uint32_t> sums(S);
+    crc32_slices(data, n, sums.data());
+    for (uint64_t i = 0; i < S; ++i) reinterpret_cast<uint32_t*>(hmeta)[i] = __builtin_bswap32(sums[i]);
+    co.block_crc = crc32_from_slices(sums.data(), n);
+    if (S) HIP_OK(hipMemcpyAsync(dmeta, hmeta, S * 4, hipMemcpyHostToDevice, l->stream));
     HIP_OK(hipStreamSynchronize(l->stream));
+  } else {
+    ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err);
+    if (ok && S) {
+      HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+      HIP_OK(hipStreamSynchronize(l->stream));
+    }
   }
   if (!ok) {
     release_lane(l);
