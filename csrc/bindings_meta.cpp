@@ -216,6 +216,7 @@ void bind_meta(py::module_& m) {
       .def("add_non_voter", &raft::Node::add_non_voter, py::call_guard<py::gil_scoped_release>())
       .def("drop_non_voter", &raft::Node::drop_non_voter, py::call_guard<py::gil_scoped_release>())
       .def("caught_up", &raft::Node::caught_up, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("has_lease", [](raft::Node& n) { return unlocked([&] { return n.has_lease(); }); })
       .def_property_readonly("role", [](raft::Node& n) {
         raft::Role r;
         {

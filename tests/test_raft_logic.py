@@ -302,6 +302,38 @@ def test_three_way_partition_blocks_progress_until_healed(tmp_path):
     run(go())
 
 
+def test_leader_lease_expires_when_cut_off(tmp_path):
+    """The leader lease gating placement without a Raft entry (MasterCore deferred create):
+    held while a majority answers within election_lo, lost once the leader is cut off even
+    though it still believes it leads (no check-quorum step-down), back after the heal."""
+    async def go():
+        c = Cluster(tmp_path, n=3)
+        await c.start()
+        l1 = await c.leader()
+        await l1.propose({"set": ["a", 1]})
+        for _ in range(50):
+            if l1._core.has_lease:
+                break
+            await asyncio.sleep(0.02)
+        assert l1._core.has_lease
+        followers = [n for n in c.nodes.values() if n is not l1]
+        assert not any(n._core.has_lease for n in followers)
+        c.faults.isolate(f"node{l1.id}", list(c.registry))
+        await asyncio.sleep(0.4)  # > election_lo (0.15 s in this harness)
+        assert not l1._core.has_lease
+        l2 = await c.leader(exclude=(l1.id,))
+        assert l2 is not l1
+        c.faults.heal()
+        for _ in range(100):
+            if l2._core.has_lease and not l1._core.has_lease:
+                break
+            await asyncio.sleep(0.05)
+        assert l2._core.has_lease and not l1._core.has_lease
+        await c.stop()
+
+    run(go())
+
+
 def test_isolated_node_rejoins_and_terms_converge(tmp_path):
     async def go():
         c = Cluster(tmp_path, n=3)
