@@ -100,16 +100,36 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d, host.data(), total, hipMemcpyHostToDevice));
   DevCrcTables* t = upload_crc_tables(s);
   if (!t) return 3;
-  std::printf("{\"iters\": %d, \"k1k2\": [", iters);
+  // roofline probe: a plain streaming read of the whole buffer on this box
+  double stream_gbps = 0;
+  {
+    uint32_t* dout = nullptr;
+    CK(hipMalloc(&dout, 4 * kStreamReadGrid * 4));
+    CK(launch_stream_read(d, total, dout, s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int it = std::max(3, iters / 10);
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < it; ++i) CK(launch_stream_read(d, total, dout, s));
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    stream_gbps = total / (1e3 * ms / it) / 1e3;
+    (void)hipFree(dout);
+  }
+  std::printf("{\"iters\": %d, \"scrub_ring_buffers\": %d, \"tile_ring_buffers\": %d, \"stream_read_GBps\": %.1f, "
+              "\"k1k2\": [", iters, crc_ring_buffers(), crc_tile_ring_buffers(), stream_gbps);
   bool first = true;
   for (uint64_t n : std::vector<uint64_t>{4096, 65536, 1ull << 20, 8ull << 20, 64ull << 20, total}) {
     if (n > total) continue;
     for (int mf = 1; mf >= 0; --mf) {
       set_crc_mfma(mf == 1);
       Run r = bench_block(d, n, t, dmeta, dpart, s, n >= (256ull << 20) ? std::max(3, iters / 10) : iters, host);
-      std::printf("%s\n  {\"bytes\": %llu, \"impl\": \"%s\", \"us\": %.2f, \"GBps\": %.1f, \"ok\": %s}", first ? "" : ",",
-                  static_cast<unsigned long long>(n), mf ? "mfma" : "lds_tables", r.us, n / r.us / 1e3,
-                  r.ok ? "true" : "false");
+      std::printf("%s\n  {\"bytes\": %llu, \"impl\": \"%s\", \"us\": %.2f, \"GBps\": %.1f, \"of_stream\": %.3f, \"ok\": %s}",
+                  first ? "" : ",", static_cast<unsigned long long>(n), mf ? "mfma" : "lds_tables", r.us,
+                  n / r.us / 1e3, n / r.us / 1e3 / stream_gbps, r.ok ? "true" : "false");
       first = false;
     }
   }
@@ -161,9 +181,10 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     double us = 1e3 * ms / it;
-    std::printf("%s\n  {\"bytes\": %llu, \"blocks\": %llu, \"impl\": \"%s\", \"us\": %.1f, \"GBps\": %.1f, \"ok\": %s}",
+    std::printf("%s\n  {\"bytes\": %llu, \"blocks\": %llu, \"impl\": \"%s\", \"us\": %.1f, \"GBps\": %.1f, "
+                "\"of_stream\": %.3f, \"ok\": %s}",
                 first ? "" : ",", static_cast<unsigned long long>(total), static_cast<unsigned long long>(nb),
-                mf ? "mfma" : "lds_tables", us, total / us / 1e3, ok ? "true" : "false");
+                mf ? "mfma" : "lds_tables", us, total / us / 1e3, total / us / 1e3 / stream_gbps, ok ? "true" : "false");
     first = false;
   }
   std::printf("\n], \"rs\": [");

@@ -11,6 +11,7 @@
 #include "disk_gate.h"
 #include "fastpath.h"
 #include "gf256.h"
+#include "gpu_kernels.h"
 #include "replication.h"
 #include "cs_grpc.h"
 #include "grpc_server.h"
@@ -132,6 +133,12 @@ PYBIND11_MODULE(_dfs_native, m) {
   });
   m.def("cpu_has_pclmul", &cpu_has_pclmul);
   m.def("device_count", &device_count);
+  // checksum-kernel selection (tests / A-B runs): (mfma, scrub ring buffers, K1/K2/K3 ring buffers)
+  m.def("crc_kernels", [] { return py::make_tuple(crc_mfma_enabled(), crc_ring_buffers(), crc_tile_ring_buffers()); });
+  m.def("set_crc_kernels", [](bool mfma, int scrub_ring, int tile_ring) {
+    set_crc_mfma(mfma);
+    set_crc_ring(scrub_ring, tile_ring);
+  });
 
   // ---------------- GF(2^8) / Reed-Solomon
   m.def("rs_matrix", [](int k, int mm) { return from_matrix(gf::rs_matrix(k, mm)); });

@@ -84,6 +84,24 @@ bool crc_mfma_enabled();
 void set_crc_mfma(bool on);  // benchmarks / tests: pick the K1 implementation
 DevCrcTables* upload_crc_tables(hipStream_t s);
 int crc_grid_for(uint64_t ntiles, uint32_t has_tail);
+// Tile buffers per wave in the MFMA kernels' register ring (2..4; 2 = the 3-waves/SIMD
+// kernels, 3..4 = the deep-ring kernels at 2 waves/SIMD). Measured (profiles/r2_crc3): the
+// K1b scrub gains ~19 % from 3 buffers; K1/K2 does not (its per-tile combine work, not load
+// latency, is what the third wave hides), so it keeps 2. DFS_CRC_RING / DFS_CRC_TILE_RING
+// override, set_crc_ring is the benches' A/B switch; K1/K2/K3 launches below
+// kCrcRingMinTiles tiles (32 MiB) always use 2. Grid caps follow, never above kMaxGridCrc.
+constexpr int kCrcRingDefault = 3;
+constexpr int kCrcTileRingDefault = 2;
+int crc_ring_buffers();       // K1b scrub
+int crc_tile_ring_buffers();  // K1/K2/K3
+void set_crc_ring(int scrub_buffers, int tile_buffers);
+constexpr uint64_t kCrcRingMinTiles = 2048;
+
+// Benches: streaming read of n bytes (n % 16 == 0) on kStreamReadGrid x 256 threads; `out`
+// holds 4 x kStreamReadGrid words.
+constexpr int kStreamReadGrid = 2048;
+hipError_t launch_stream_read(const uint8_t* d, uint64_t n, uint32_t* out, hipStream_t s);
+
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
 hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s);
 hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s);

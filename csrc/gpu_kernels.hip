@@ -137,6 +137,30 @@ __device__ __forceinline__ WaveData load_wave(const uint8_t* __restrict__ data, 
   return d;
 }
 
+// Ring form of load_wave for the pipelined kernels: the loads are unconditional (slices
+// outside [lo, hi) read slice lo instead; requires lo < hi) and the consumer zeroes the
+// CHUNK CRCs of those slices (one select per lane instead of 16 on the data; the raw CRC of
+// zeros is zero, so it is the same as zeroed data). A conditional load into a zeroed
+// register is a VALU write to a register the ring may still have a load pending on, and the
+// compiler resolves that with a vmcnt(0) that drains the whole ring.
+__device__ __forceinline__ WaveData load_wave_ring(const uint8_t* __restrict__ data, int64_t i0, int64_t lo,
+                                                   int64_t hi, int lane) {
+  const int n = lane & 31, h = lane >> 5;
+  WaveData d;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = it * 32 + n;
+    int64_t i = i0 + (c >> 3);
+    i = (i >= lo && i < hi) ? i : lo;
+    using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+    const u32x4* p = reinterpret_cast<const u32x4*>(data + static_cast<uint64_t>(i) * 512 + (c & 7) * 64 + h * 32);
+    u32x4 x = __builtin_nontemporal_load(p), y = __builtin_nontemporal_load(p + 1);
+    d.v[2 * it] = make_uint4(x[0], x[1], x[2], x[3]);
+    d.v[2 * it + 1] = make_uint4(y[0], y[1], y[2], y[3]);
+  }
+  return d;
+}
+
 // Raw CRC of the 64-byte chunk `lane` of the wave's 4 KiB (wave-wide: all 64 lanes together).
 __device__ __forceinline__ uint32_t wave_chunk_crcs(const i32x4 (&A)[16], const WaveData& d, int lane) {
   const int h = lane >> 5;
@@ -489,6 +513,224 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
   }
 }
 
+
+
+// ---------------------------------------------------------------------------------------
+// Deep-ring variants of the two MFMA kernels (R = 3..4 buffers: crc_ring_buffers() for the
+// scrub, crc_tile_ring_buffers() for K1/K2/K3, see gpu_kernels.h for the defaults; deeper
+// rings spill at the 256-VGPR budget of 2 waves/SIMD).
+// The kernels stream every byte once, so what bounds them is the data in flight per CU, not
+// the matrix cores (32 MFMAs per 4 KiB per wave ≈ 9.8 TB/s at full rate): the kernels above
+// keep one tile in flight per wave at 3 waves/SIMD. Here each wave keeps R-1 tiles in flight
+// in a register ring (16 VGPRs per buffer) at 2 waves/SIMD (grid 512 = one resident round).
+// For the compiler to wait with a counted vmcnt(N) instead of draining the ring:
+//  * the ring loads are unconditional (tiles past the run re-read its last tile, slices
+//    outside the block read slice lo and their chunk CRCs are zeroed), and the loop
+//    runs whole groups of R tiles with the remainder (already loaded) after it;
+//  * nothing else in the loop is a global load whose result is used: the expected .meta word
+//    of a lane's slice is loaded with its data, and the scrub's block table is read through
+//    the constant address space (scalar loads; the table is read-only for the launch, and
+//    the atomics on `bad` would otherwise make the compiler treat it as clobbered).
+template <int R>
+struct Ring {
+  WaveData b[R];
+  uint32_t expect[R];
+};
+
+template <int R>
+__global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void crc_tile_ring_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
+  __shared__ MfmaTileLds lt;
+  __shared__ uint32_t wacc[4];
+  __shared__ uint32_t wg_bad;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
+  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
+  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  const int64_t lo = static_cast<int64_t>(a.slice_lo), hi = static_cast<int64_t>(a.slice_hi);
+  auto first_slice = [&](uint64_t t) {
+    return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8) - static_cast<int64_t>(a.vfront);
+  };
+  Ring<R> ring;
+  auto load = [&](int slot, uint64_t t) {
+    t = t < t_end ? t : t_end - 1;
+    const int64_t i0 = first_slice(t), i = i0 + sw;
+    ring.b[slot] = load_wave_ring(a.data, i0, lo, hi, lane);
+    ring.expect[slot] = a.meta_expect ? a.meta_expect[(i >= lo && i < hi) ? i : lo] : 0u;
+  };
+  const bool work = t_begin < t_end;  // workgroup-uniform
+  if (work) {
+#pragma unroll
+    for (int k = 0; k < R - 1; ++k) load(k, t_begin + k);
+  }
+  i32x4 A[16];
+  load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
+  load_lds_image(gt, &lt);
+  if (threadIdx.x == 0) wg_bad = 0xFFFFFFFFu;
+  __syncthreads();
+
+  uint32_t acc = 0;
+  uint32_t bad = 0xFFFFFFFFu;
+  auto step = [&](int slot, uint64_t t) {
+    const int64_t i = first_slice(t) + sw;
+    const bool valid = i >= lo && i < hi;
+    const uint32_t c = wave_chunk_crcs(A, ring.b[slot], lane);
+    uint32_t r = slice_from_chunks(lt, valid ? c : 0u, lane);
+    if (valid && sl == 0) {
+      uint32_t be = __builtin_bswap32(r ^ a.full_init);
+      if (a.meta_out) a.meta_out[i] = be;
+      if (a.meta_expect && ring.expect[slot] != be) bad = min(bad, static_cast<uint32_t>(i));
+    }
+    if (a.part_crc) {
+      r = combine(r, 8, lane, lt.sh512);
+      r = combine(r, 16, lane, lt.sh1k);
+      r = combine(r, 32, lane, lt.sh2k);  // wave-uniform: the 4 KiB sub-tile's raw CRC
+      acc = mat_apply(lt.tile_pow2[0], acc, lane) ^ r;
+    }
+  };
+  uint64_t t0 = t_begin;
+  if (work) {
+    for (; t0 + R <= t_end; t0 += R) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        load((k + R - 1) % R, t0 + k + R - 1);
+        step(k, t0 + k);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < R - 1; ++k)
+      if (t0 + k < t_end) step(k, t0 + k);  // loaded by the last group (or the prologue)
+  }
+
+  if (a.has_tail && blockIdx.x == 0 && wave == 0) {
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(a.data + a.s_full * 512, a.tail_len, lane),
+                                                       lane), lane);
+    if (lane == 0) {
+      uint32_t be = __builtin_bswap32(r ^ a.tail_init);
+      if (a.meta_out) a.meta_out[a.s_full] = be;
+      if (a.meta_expect && a.meta_expect[a.s_full] != be) bad = min(bad, static_cast<uint32_t>(a.s_full));
+    }
+  }
+  if (a.part_crc) {
+    for (int k = wave; k < 3; ++k) acc = tab4(lt.sh4k, acc);
+    uint64_t e = work ? a.ntiles - t_end : 0;
+    for (int b = 0; e; ++b, e >>= 1)
+      if (e & 1) acc = mat_apply(lt.tile_pow2[b], acc, lane);
+    if (lane == 0) wacc[wave] = acc;
+  }
+  if (a.part_bad && bad != 0xFFFFFFFFu) atomicMin(&wg_bad, bad);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (a.part_crc) a.part_crc[blockIdx.x] = wacc[0] ^ wacc[1] ^ wacc[2] ^ wacc[3];
+    if (a.part_bad) a.part_bad[blockIdx.x] = wg_bad;
+  }
+}
+
+using ConstScrubBlock = const __attribute__((address_space(4))) ScrubBlock;
+
+template <int R>
+__global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void crc_scrub_ring_kernel(ScrubLaunch a, const DevCrcTables* __restrict__ gt) {
+  __shared__ MfmaSliceLds lt;
+  ConstScrubBlock* blocks = (ConstScrubBlock*)a.blocks;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
+  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
+  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  const bool work = t_begin < t_end;  // workgroup-uniform
+  uint32_t blk = 0;
+  if (work) {
+    uint32_t l = 0, h = a.nblocks;
+    while (h - l > 1) {
+      uint32_t mid = (l + h) >> 1;
+      if (blocks[mid].tile_start <= t_begin) l = mid;
+      else h = mid;
+    }
+    blk = l;
+  }
+  auto advance = [&](uint64_t t, uint32_t b) {
+    while (b + 1 < a.nblocks && blocks[b + 1].tile_start <= t) ++b;
+    return b;
+  };
+  Ring<R> ring;
+  uint32_t lblk = blk;  // block of the next tile to load (non-decreasing: clamped tiles are too)
+  auto load = [&](int slot, uint64_t t) {
+    t = t < t_end ? t : t_end - 1;
+    lblk = advance(t, lblk);
+    const uint8_t* data = blocks[lblk].data;
+    const uint32_t* meta = blocks[lblk].meta;
+    const int64_t i0 = static_cast<int64_t>((t - blocks[lblk].tile_start) * kSlicesPerTile + wave * 8);
+    const int64_t hi = static_cast<int64_t>(blocks[lblk].s_full);
+    ring.b[slot] = load_wave_ring(data, i0, 0, hi, lane);
+    ring.expect[slot] = meta[i0 + sw < hi ? i0 + sw : 0];
+  };
+  if (work) {
+#pragma unroll
+    for (int k = 0; k < R - 1; ++k) load(k, t_begin + k);
+  }
+  i32x4 A[16];
+  load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
+  load_lds_image(gt, &lt);
+  __syncthreads();
+  auto step = [&](int slot, uint64_t t) {
+    blk = advance(t, blk);
+    const int64_t i0 = static_cast<int64_t>((t - blocks[blk].tile_start) * kSlicesPerTile + wave * 8);
+    const int64_t hi = static_cast<int64_t>(blocks[blk].s_full);
+    // slices past the block end are never compared, so their (re-read) data needs no masking
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, ring.b[slot], lane), lane);
+    const int64_t i = i0 + sw;
+    if (sl == 0 && i < hi && ring.expect[slot] != __builtin_bswap32(r ^ a.full_init))
+      atomicMin(&a.bad[blk], static_cast<uint32_t>(i));
+  };
+  if (work) {
+    uint64_t t0 = t_begin;
+    for (; t0 + R <= t_end; t0 += R) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        load((k + R - 1) % R, t0 + k + R - 1);
+        step(k, t0 + k);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < R - 1; ++k)
+      if (t0 + k < t_end) step(k, t0 + k);
+  }
+  const int waves = kCrcWgThreads / 64;
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * waves + wave; k < a.nblocks;
+       k += static_cast<uint64_t>(gridDim.x) * waves) {
+    ConstScrubBlock& b = blocks[k];
+    if (!b.tail_len) continue;
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(b.data + b.s_full * 512, b.tail_len, lane),
+                                                       lane), lane);
+    if (lane == 0 && b.meta[b.s_full] != __builtin_bswap32(r ^ b.tail_init))
+      atomicMin(&a.bad[k], static_cast<uint32_t>(b.s_full));
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Roofline probe for the benches: a plain streaming read of n bytes (16 B per lane, four
+// loads in flight per lane, non-temporal like the CRC kernels) XOR-folded into one word per
+// workgroup. Its TB/s on the same box is what "fraction of achievable HBM" divides by.
+__global__ __launch_bounds__(256) void stream_read_kernel(const uint4* __restrict__ p, uint64_t nvec, uint32_t* out) {
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  uint32_t x = 0;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x;
+  for (; i + 3 * stride < nvec; i += 4 * stride) {
+    u32x4 a = __builtin_nontemporal_load(q + i), b = __builtin_nontemporal_load(q + i + stride);
+    u32x4 c = __builtin_nontemporal_load(q + i + 2 * stride), d = __builtin_nontemporal_load(q + i + 3 * stride);
+    a ^= b ^ c ^ d;
+    x ^= a[0] ^ a[1] ^ a[2] ^ a[3];
+  }
+  for (; i < nvec; i += stride) {
+    u32x4 a = __builtin_nontemporal_load(q + i);
+    x ^= a[0] ^ a[1] ^ a[2] ^ a[3];
+  }
+  for (int m = 32; m; m >>= 1) x ^= __shfl_xor(x, m);
+  if ((threadIdx.x & 63) == 0) out[blockIdx.x * 4 + (threadIdx.x >> 6)] = x;
+}
+
 // ---------------------------------------------------------------------------------------
 // GF(2^8) shard matrix multiply (K4 encode / K5 reconstruct): out[r] = XOR_c mat[r][c] * in[c].
 // Branch-free split-nibble form (ISA-L style): c * x = T_lo[x & 15] ^ T_hi[x >> 4], with the
@@ -574,6 +816,42 @@ bool crc_mfma_enabled() {
 
 void set_crc_mfma(bool on) { g_crc_mfma.store(on ? 1 : 0); }
 
+static std::atomic<int> g_crc_ring{0}, g_crc_tile_ring{0};
+
+static int ring_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  int v = e ? std::atoi(e) : dflt;
+  return v < 2 ? 2 : (v > 4 ? 4 : v);
+}
+
+int crc_ring_buffers() {
+  int v = g_crc_ring.load(std::memory_order_relaxed);
+  if (v == 0) g_crc_ring.store(v = ring_env("DFS_CRC_RING", kCrcRingDefault));
+  return v;
+}
+
+int crc_tile_ring_buffers() {
+  int v = g_crc_tile_ring.load(std::memory_order_relaxed);
+  if (v == 0) g_crc_tile_ring.store(v = ring_env("DFS_CRC_TILE_RING", kCrcTileRingDefault));
+  return v;
+}
+
+void set_crc_ring(int scrub_buffers, int tile_buffers) {
+  g_crc_ring.store(scrub_buffers < 2 ? 2 : (scrub_buffers > 4 ? 4 : scrub_buffers));
+  g_crc_tile_ring.store(tile_buffers < 2 ? 2 : (tile_buffers > 4 ? 4 : tile_buffers));
+}
+
+// Ring depth of a K1/K2/K3 launch over `ntiles` tiles: a deep ring only pays once workgroups
+// have several tiles each (below kCrcRingMinTiles its longer prologue costs ~0.3 us per
+// launch, e.g. on 1 MiB blocks).
+static int ring_for(uint64_t ntiles) {
+  if (!crc_mfma_enabled()) return 0;
+  return ntiles >= kCrcRingMinTiles ? crc_tile_ring_buffers() : 2;
+}
+
+// One resident round: 3 workgroups per CU at 3 waves/SIMD (R = 2), 2 at 2 waves/SIMD.
+static uint64_t crc_grid_cap(int ring) { return ring > 2 ? 2 * 256 : kMaxGridCrc; }
+
 DevCrcTables* upload_crc_tables(hipStream_t s) {
   static_assert(sizeof(DevCrcTables) % 16 == 0, "table image must be uint4-copyable");
   std::vector<uint8_t> host(sizeof(DevCrcTables));
@@ -624,29 +902,44 @@ int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
     return static_cast<uint64_t>(v > 0 ? v : 1);
   }();
   uint64_t g = (ntiles + per - 1) / per;
-  g = g < static_cast<uint64_t>(kMaxGridCrc) ? g : kMaxGridCrc;
+  const uint64_t cap = crc_grid_cap(ring_for(ntiles));
+  g = g < cap ? g : cap;
   if (g == 0 && has_tail) g = 1;
   return static_cast<int>(g);
 }
 
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
-  if (crc_mfma_enabled()) hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
-  else hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
+  switch (ring_for(a.ntiles)) {
+    case 0: hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
+    case 2: hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
+    case 3: hipLaunchKernelGGL(crc_tile_ring_kernel<3>, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
+    default: hipLaunchKernelGGL(crc_tile_ring_kernel<4>, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s) {
   if (a.nblocks == 0) return hipSuccess;
-  const uint64_t cap = crc_mfma_enabled() ? kMaxGridCrc : 2048;
+  const int ring = crc_mfma_enabled() ? crc_ring_buffers() : 0;
+  const uint64_t cap = ring ? crc_grid_cap(ring) : 2048;
   uint64_t g = a.ntiles < cap ? a.ntiles : cap;
   uint64_t tail_waves = (a.nblocks + 3) / 4;
   if (g < tail_waves) g = tail_waves < cap ? tail_waves : cap;
   if (g == 0) g = 1;
-  if (crc_mfma_enabled())
-    hipLaunchKernelGGL(crc_scrub_mfma_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
-  else
-    hipLaunchKernelGGL(crc_scrub_kernel, dim3(static_cast<unsigned>(g)), dim3(kCrcWgThreads), 0, s, a, t);
+  const dim3 grid(static_cast<unsigned>(g));
+  switch (ring) {
+    case 0: hipLaunchKernelGGL(crc_scrub_kernel, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
+    case 2: hipLaunchKernelGGL(crc_scrub_mfma_kernel, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
+    case 3: hipLaunchKernelGGL(crc_scrub_ring_kernel<3>, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
+    default: hipLaunchKernelGGL(crc_scrub_ring_kernel<4>, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_read(const uint8_t* d, uint64_t n, uint32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(stream_read_kernel, dim3(kStreamReadGrid), dim3(256), 0, s, reinterpret_cast<const uint4*>(d), n / 16,
+                     out);
   return hipGetLastError();
 }
 

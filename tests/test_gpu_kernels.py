@@ -54,6 +54,34 @@ def test_gpu_write_read_verify(gstore, n):
         assert st == 0 and out == exp and not partial
 
 
+@pytest.mark.parametrize("rings", [(2, 2), (3, 3), (4, 4)])
+def test_gpu_ring_depths(gstore, native, rings):
+    """The register-ring variants of the MFMA kernels (scrub, and K1/K2/K3 on blocks of at
+    least kCrcRingMinTiles tiles = 32 MiB) against zlib, including the verify path and a
+    corruption the scrub must find."""
+    saved = native.crc_kernels()
+    native.set_crc_kernels(True, *rings)
+    try:
+        n = (40 << 20) + 512 * 5 + 77
+        d = os.urandom(n)
+        crc, meta = gstore.gpu_crc(d)
+        assert crc == zlib.crc32(d) and meta == ref_meta(d)
+        ok, crc, err = gstore.write("ring", d, zlib.crc32(d))
+        assert ok, err
+        st, total, out, partial, bad, err = gstore.read("ring", 0, 0)
+        assert (st, total, partial) == (0, n, False) and out == d
+        st, total, out, partial, bad, err = gstore.read("ring", 5 << 20, 33 << 20)
+        assert st == 0 and out == d[5 << 20:38 << 20] and not partial
+        assert gstore.scrub_resident(["ring"]) == []
+        assert gstore.debug_corrupt("ring", (33 << 20) + 100)
+        assert gstore.scrub_resident(["ring"]) == ["ring"]
+        st, *_rest, err = gstore.read("ring", 0, 0)
+        assert st == 3 and f"chunk {((33 << 20) + 100) // 512}" in err
+    finally:
+        native.set_crc_kernels(*saved)
+        gstore.remove("ring")
+
+
 def test_gpu_write_rejects_bad_crc(gstore):
     d = os.urandom(5000)
     ok, crc, err = gstore.write("badcrc", d, zlib.crc32(d) ^ 1)
