@@ -7,7 +7,7 @@
 // batched scrub, and Reed-Solomon RS(6,3) encode (GPU vs CPU). Run under
 // `rocprofv3 --kernel-trace --stats` to get per-kernel device time.
 //
-//   io_bench [--device N] [--dir PATH] [--iters N] [--no-fsync]   -> one JSON object on stdout
+//   io_bench [--device N] [--dir PATH] [--iters N] [--no-fsync] [--staged] [--rs-only]   -> one JSON object
 //   io_bench --disk-sweep [--dir PATH]   -> aggregate 1 MiB write+fdatasync bandwidth of the
 //            storage directory at 1..240 concurrent writers, buffered and O_DIRECT (what bounds
 //            nvme-sync replication when every GPU of a node writes RF replicas to one volume)
@@ -119,6 +119,7 @@ int main(int argc, char** argv) {
   int device = 0, iters = 50;
   bool fsync = true;
   bool zero_copy = true;
+  bool rs_only = false;  // only the RS(6,3) end-to-end case (pipeline tuning sweeps)
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--disk-sweep") {
       std::string dir = "/tmp/io_bench_disk";
@@ -162,6 +163,7 @@ int main(int argc, char** argv) {
     else if (a == "--iters" && i + 1 < argc) iters = std::atoi(argv[++i]);
     else if (a == "--no-fsync") fsync = false;
     else if (a == "--staged") zero_copy = false;
+    else if (a == "--rs-only") rs_only = true;
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) device = -1;
@@ -169,6 +171,8 @@ int main(int argc, char** argv) {
 
   // zero_copy: the client buffers are registered with the store the way the fast path
   // registers a client's shared-memory arena (one DMA per copy); --staged: pinned bounce
+  if (rs_only) std::printf("{\n  \"device\": %d, \"rs_only\": true,\n", device);
+  if (!rs_only) {
   std::printf("{\n  \"device\": %d, \"iters\": %d, \"fsync\": %s, \"zero_copy\": %s,\n  \"store\": {", device,
               iters, fsync ? "true" : "false", zero_copy ? "true" : "false");
   bool first = true;
@@ -292,6 +296,8 @@ int main(int argc, char** argv) {
     std::printf("  \"crc32_256MiB\": {\"cpu_GBps\": %.2f, \"gpu_incl_h2d_GBps\": %.2f, \"match\": %s},\n",
                 n / cpu_s / 1e9, gpu_s > 0 ? n / gpu_s / 1e9 : 0.0, cpu == gpu ? "true" : "false");
   }
+
+  }  // !rs_only
 
   // ---- RS(6,3) encode of 6 x 16 MiB shards: GPU vs CPU
   {

@@ -1796,7 +1796,14 @@ bool ChunkStore::gf_matmul_gpu(const std::vector<std::vector<uint8_t>>& mat, con
   gf_nibble_tables(flat.data(), rows, k, htab);
   HIP_OK(hipMemcpyAsync(dtab, htab, tbytes, hipMemcpyHostToDevice, lanes[0]->stream));
   HIP_OK(hipStreamSynchronize(lanes[0]->stream));
-  const uint64_t chunk = std::max<uint64_t>(4ull << 20, align_up(len / 8, 4096));  // per shard per step
+  // per shard per step: small enough that the pipeline's fill (first H2D) and drain (last
+  // D2H) are short, large enough that each copy runs at full DMA rate (DFS_RS_CHUNK_KIB)
+  static const uint64_t min_chunk = [] {
+    const char* e = std::getenv("DFS_RS_CHUNK_KIB");
+    long v = e ? std::atol(e) : 4096;
+    return static_cast<uint64_t>(v > 64 ? v : 64) << 10;
+  }();
+  const uint64_t chunk = std::max<uint64_t>(min_chunk, align_up(len / 64, 4096));
   bool ok = true;
   for (uint64_t off = 0, j = 0; off < len && ok; off += chunk, ++j) {
     Lane* l = lanes[j & 1];
