@@ -108,9 +108,14 @@ struct GrpcChannelPool::Conn {
   std::string authority;
   // the call in flight
   int32_t sid = -1;
-  std::string out;  // 5-byte prefix + request message
-  size_t off = 0;
-  std::string in;   // response DATA (5-byte prefix + message)
+  // request: 5-byte gRPC prefix + the caller's message (not copied; valid during the call)
+  char prefix[5];
+  const std::string* req = nullptr;
+  size_t off = 0;  // bytes of prefix + *req handed to nghttp2
+  // response: its prefix kept apart, so the message is moved out, not copied
+  char head[5];
+  size_t head_len = 0;
+  std::string in;
   bool closed = false, reset = false;
   int grpc_status = -1;
   std::string grpc_message;
@@ -155,7 +160,20 @@ struct GrpcChannelPool::Conn {
 
   static int on_data(nghttp2_session*, uint8_t, int32_t sid, const uint8_t* data, size_t len, void* user) {
     auto* c = static_cast<Conn*>(user);
-    if (sid == c->sid) c->in.append(reinterpret_cast<const char*>(data), len);
+    if (sid != c->sid) return 0;
+    if (c->head_len < 5) {
+      const size_t k = std::min<size_t>(5 - c->head_len, len);
+      std::memcpy(c->head + c->head_len, data, k);
+      c->head_len += k;
+      data += k;
+      len -= k;
+      if (c->head_len == 5) {
+        uint32_t n;
+        std::memcpy(&n, c->head + 1, 4);
+        c->in.reserve(std::min<uint32_t>(ntohl(n), 1u << 30));
+      }
+    }
+    c->in.append(reinterpret_cast<const char*>(data), len);
     return 0;
   }
 
@@ -171,10 +189,24 @@ struct GrpcChannelPool::Conn {
   static ssize_t read_body(nghttp2_session*, int32_t, uint8_t* buf, size_t len, uint32_t* flags, nghttp2_data_source*,
                            void* user) {
     auto* c = static_cast<Conn*>(user);
-    size_t n = std::min(len, c->out.size() - c->off);
-    std::memcpy(buf, c->out.data() + c->off, n);
-    c->off += n;
-    if (c->off == c->out.size()) *flags |= NGHTTP2_DATA_FLAG_EOF;
+    if (!c->req) {  // a stream of an earlier call (never expected: calls end with their stream)
+      *flags |= NGHTTP2_DATA_FLAG_EOF;
+      return 0;
+    }
+    const size_t total = 5 + c->req->size();
+    size_t n = 0;
+    if (c->off < 5) {
+      n = std::min(len, 5 - c->off);
+      std::memcpy(buf, c->prefix + c->off, n);
+      c->off += n;
+    }
+    if (n < len && c->off >= 5) {
+      size_t m = std::min(len - n, total - c->off);
+      std::memcpy(buf + n, c->req->data() + (c->off - 5), m);
+      c->off += m;
+      n += m;
+    }
+    if (c->off == total) *flags |= NGHTTP2_DATA_FLAG_EOF;
     return static_cast<ssize_t>(n);
   }
 
@@ -265,12 +297,12 @@ GrpcResult GrpcChannelPool::call(const std::string& target, const std::string& p
     return res;
   }
   c->deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
-  c->out.resize(5 + request.size());
-  c->out[0] = 0;
+  c->prefix[0] = 0;
   uint32_t be = htonl(static_cast<uint32_t>(request.size()));
-  std::memcpy(&c->out[1], &be, 4);
-  std::memcpy(&c->out[5], request.data(), request.size());
+  std::memcpy(c->prefix + 1, &be, 4);
+  c->req = &request;
   c->off = 0;
+  c->head_len = 0;
   c->in.clear();
   c->closed = c->reset = false;
   c->grpc_status = -1;
@@ -297,24 +329,24 @@ GrpcResult GrpcChannelPool::call(const std::string& target, const std::string& p
   } else if (c->grpc_status != 0) {
     res.status = c->grpc_status;
     res.message = std::move(c->grpc_message);
-  } else if (c->in.size() < 5) {
+  } else if (c->head_len < 5) {
     res.status = 13;
     res.message = "empty response";
   } else {
     uint32_t n;
-    std::memcpy(&n, &c->in[1], 4);
+    std::memcpy(&n, c->head + 1, 4);
     n = ntohl(n);
-    if (c->in[0] != 0 || c->in.size() < 5 + static_cast<size_t>(n)) {
+    if (c->head[0] != 0 || c->in.size() < static_cast<size_t>(n)) {
       res.status = 13;
       res.message = "malformed or compressed response";
     } else {
+      c->in.resize(n);
       res.status = 0;
-      res.message = c->in.substr(5, n);
+      res.message = std::move(c->in);
     }
   }
-  c->in.clear();
-  c->in.shrink_to_fit();
-  std::string().swap(c->out);
+  std::string().swap(c->in);
+  c->req = nullptr;
   if (!c->reset && nghttp2_session_want_read(c->s)) give(target, std::move(c));
   return res;
 }

@@ -61,9 +61,16 @@ nghttp2_nv nv(const std::string& name, const std::string& value) {
 
 struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
   struct Stream {
-    std::string path, rid, body;
-    std::string out;  // 5-byte prefix + response message
-    size_t off = 0;
+    std::string path, rid;
+    // request: the 5-byte gRPC prefix kept apart from the message, so the message moves to
+    // the handler without a copy
+    char head[5];
+    size_t head_len = 0;
+    std::string body;
+    // response: prefix + message, served by read_body without concatenating them
+    char prefix[5];
+    std::string out;
+    size_t off = 0;  // bytes of prefix + out already handed to nghttp2
     std::string status_str = "0";
     bool dispatched = false;
   };
@@ -95,10 +102,20 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     auto it = c->streams.find(sid);
     if (it == c->streams.end()) return NGHTTP2_ERR_TEMPORAL_CALLBACK_FAILURE;
     Stream& st = it->second;
-    size_t n = std::min(len, st.out.size() - st.off);
-    std::memcpy(buf, st.out.data() + st.off, n);
-    st.off += n;
-    if (st.off == st.out.size()) {
+    const size_t total = 5 + st.out.size();
+    size_t n = 0;
+    if (st.off < 5) {
+      n = std::min(len, 5 - st.off);
+      std::memcpy(buf, st.prefix + st.off, n);
+      st.off += n;
+    }
+    if (n < len && st.off >= 5) {
+      size_t m = std::min(len - n, total - st.off);
+      std::memcpy(buf + n, st.out.data() + (st.off - 5), m);
+      st.off += m;
+      n += m;
+    }
+    if (st.off == total) {
       *flags |= NGHTTP2_DATA_FLAG_EOF | NGHTTP2_DATA_FLAG_NO_END_STREAM;
       static const std::string k_status = "grpc-status";
       nghttp2_nv tr[] = {nv(k_status, st.status_str)};
@@ -114,11 +131,10 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     static const std::string k_status = ":status", v200 = "200", k_ct = "content-type", v_ct = "application/grpc",
                              k_gs = "grpc-status", k_gm = "grpc-message";
     if (r.status == 0) {
-      st.out.resize(5 + r.message.size());
-      st.out[0] = 0;
+      st.prefix[0] = 0;
       uint32_t n = htonl(static_cast<uint32_t>(r.message.size()));
-      std::memcpy(&st.out[1], &n, 4);
-      std::memcpy(&st.out[5], r.message.data(), r.message.size());
+      std::memcpy(st.prefix + 1, &n, 4);
+      st.out = std::move(r.message);
       st.off = 0;
       nghttp2_nv h[] = {nv(k_status, v200), nv(k_ct, v_ct)};
       nghttp2_data_provider dp;
@@ -139,14 +155,14 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     Stream& st = it->second;
     st.dispatched = true;
     GrpcReply bad;
-    if (st.body.size() < 5) {
+    if (st.head_len < 5) {
       bad = {13, "missing gRPC message"};
-    } else if (st.body[0] != 0) {
+    } else if (st.head[0] != 0) {
       bad = {12, "compressed messages are not supported"};
     } else {
       uint32_t n;
-      std::memcpy(&n, st.body.data() + 1, 4);
-      if (ntohl(n) != st.body.size() - 5) bad = {13, "gRPC message length mismatch"};
+      std::memcpy(&n, st.head + 1, 4);
+      if (ntohl(n) != st.body.size()) bad = {13, "gRPC message length mismatch"};
     }
     if (bad.status) {
       respond(sid, bad);
@@ -155,9 +171,8 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     auto call = std::make_shared<GrpcCall>();
     call->path = std::move(st.path);
     call->request_id = std::move(st.rid);
-    call->message.assign(st.body, 5, std::string::npos);
-    st.body.clear();
-    st.body.shrink_to_fit();
+    call->message = std::move(st.body);
+    st.body = std::string();
     auto self = shared_from_this();
     std::lock_guard<std::mutex> g(srv->mu_);
     srv->jobs_.emplace_back([self, sid, call] {
@@ -193,13 +208,21 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     auto* c = static_cast<Conn*>(user);
     auto it = c->streams.find(sid);
     if (it != c->streams.end()) {
-      if (it->second.body.empty() && len >= 5) {
-        // size the buffer once from the gRPC length prefix (1-100 MiB blocks)
-        uint32_t n;
-        std::memcpy(&n, data + 1, 4);
-        it->second.body.reserve(5 + std::min<uint32_t>(ntohl(n), 1u << 30));
+      Stream& st = it->second;
+      if (st.head_len < 5) {
+        const size_t k = std::min<size_t>(5 - st.head_len, len);
+        std::memcpy(st.head + st.head_len, data, k);
+        st.head_len += k;
+        data += k;
+        len -= k;
+        if (st.head_len == 5) {
+          // size the buffer once from the gRPC length prefix (1-100 MiB blocks)
+          uint32_t n;
+          std::memcpy(&n, st.head + 1, 4);
+          st.body.reserve(std::min<uint32_t>(ntohl(n), 1u << 30));
+        }
       }
-      it->second.body.append(reinterpret_cast<const char*>(data), len);
+      st.body.append(reinterpret_cast<const char*>(data), len);
     }
     return 0;
   }
