@@ -1,0 +1,67 @@
+"""The driver's bench.py contract, rehearsed on the CPU.
+
+The round-end driver runs `bench.py` at N=1 directly and at N=2/4/8 under
+`torch.distributed.run` (one rank per GPU, MAX over ranks, ONE JSON line from rank 0).
+Here the same multi-process path runs with the host chunk store (`--cpu`) and the
+host-memory socket replication transport, which speaks the same pair/sequence/descriptor
+protocol as the RCCL transport (`csrc/replication.cpp`), so the rendezvous, the fan-out to
+RF-1 replicas, the observed-transport label and the JSON shape are all exercised without
+a GPU. Reference workload: `dfs/client/src/bin/dfs_cli.rs:594-628` (write then read).
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(cmd, tmp_path, timeout=300):
+    env = dict(os.environ, TMPDIR=str(tmp_path), MASTER_ADDR="127.0.0.1")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout  # exactly one JSON line on rank 0's stdout
+    return json.loads(lines[0])
+
+
+def _check_common(d, n, steps, warmup):
+    assert REQUIRED <= set(d)
+    base = json.loads((ROOT / "BASELINE.json").read_text())
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == warmup
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["config"]["replication_factor"] == min(3, n)
+    assert d["config"]["store"] == "cpu"
+
+
+def test_bench_single_rank_cpu(tmp_path):
+    d = _run([sys.executable, "bench.py", "--cpu", "--steps", "1", "--warmup", "1", "--count", "10",
+              "--remote-steps", "1"], tmp_path)
+    _check_common(d, 1, 1, 1)
+    assert d["config"]["transport"] == "local"
+    assert d["remote_client"]["native_client_ops"] == d["remote_client"]["steps"] * 2 * 10
+
+
+@pytest.mark.parametrize("n", [4])
+def test_bench_multi_rank_socket_transport(tmp_path, n):
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+              "--master-addr", "127.0.0.1", "--master-port", "29671", "bench.py", "--gpus", str(n),
+              "--steps", "1", "--warmup", "1", "--cpu", "--count", "10", "--transport", "socket",
+              "--remote-steps", "0"], tmp_path)
+    _check_common(d, n, 1, 1)
+    assert d["config"]["global_batch"] == 10 * n
+    # every rank's engine came up, every directed pair is up, and every write reached
+    # RF-1 replicas over the peer transport (nothing fell back, nothing failed)
+    assert d["rccl_ranks"] == n
+    assert d["repl_pairs_up"] == n * (n - 1)
+    writes = (1 + 1) * 10 * n  # warmup + timed step
+    assert d["rccl_forwards"] == writes * (min(3, n) - 1)
+    assert d["rccl_fallbacks"] == 0 and d["replica_failures"] == 0 and d["repl_pair_failures"] == 0
+    assert d["config"]["transport"] == "socket"
