@@ -6,9 +6,14 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
+#include <thread>
 
 #include "client_fast.h"
 #include "client_remote.h"
@@ -153,6 +158,148 @@ struct NodeDeleter {
     delete n;
   }
 };
+
+// ---------------- native `dfs_cli benchmark` workers
+// The reference's benchmark runs its `concurrency` workers as tokio tasks inside the Rust
+// CLI (dfs/client/src/bin/dfs_cli.rs:594-628 write, :633-690 read), each timing one
+// client call. These are the same workers as native threads over the native clients, so
+// the measured latency is the client call and not Python's thread pool and GIL hand-offs.
+// Every op still moves the whole file: a write hashes (CRC + MD5) and ships the caller's
+// buffer; a read copies the block out of the transfer slot into a worker-owned buffer
+// (like `get_file_content`'s Vec) and, when an expected payload is given, compares it.
+struct BenchOut {
+  std::vector<int> status;  // FastClient::Status per op
+  std::vector<double> lat;  // seconds per op
+  std::vector<FastClient::Times> times;
+  std::vector<uint64_t> bytes;
+  std::string first_error;
+  uint64_t mismatches = 0;
+  double total_s = 0;
+};
+
+template <class Op>
+void bench_run(size_t count, int concurrency, BenchOut* out, Op op) {
+  out->status.assign(count, 0);
+  out->lat.assign(count, 0.0);
+  out->times.assign(count, FastClient::Times{});
+  out->bytes.assign(count, 0);
+  std::atomic<size_t> next{0};
+  std::mutex err_mu;
+  auto worker = [&] {
+    std::vector<uint8_t> buf;  // this worker's read buffer
+    for (size_t i; (i = next.fetch_add(1)) < count;) {
+      std::string msg;
+      auto t0 = std::chrono::steady_clock::now();
+      int st = op(i, &out->times[i], &out->bytes[i], &buf, &msg);
+      out->lat[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      out->status[i] = st;
+      if (st == FastClient::Failed) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (out->first_error.empty()) out->first_error = msg;
+      }
+    }
+  };
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> ws;
+  for (int k = 0; k < std::max(1, concurrency); ++k) ws.emplace_back(worker);
+  for (auto& w : ws) w.join();
+  out->total_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+py::tuple bench_result(const BenchOut& o, bool reads) {
+  py::list times;
+  for (const auto& t : o.times) {
+    if (reads) times.append(py::make_tuple(t.getinfo, t.read));
+    else times.append(py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete));
+  }
+  return py::make_tuple(o.status, o.lat, o.total_s, times, o.bytes, o.first_error, o.mismatches);
+}
+
+struct BufView {
+  const uint8_t* p = nullptr;
+  size_t n = 0;
+};
+
+std::vector<BufView> buf_views(const py::list& bufs) {
+  std::vector<BufView> v;
+  for (auto h : bufs) {
+    if (h.is_none()) {
+      v.push_back({});
+      continue;
+    }
+    py::buffer_info bi = py::reinterpret_borrow<py::buffer>(h).request();
+    v.push_back({static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize)});
+  }
+  return v;
+}
+
+// writes: paths[i] <- payloads[i % len(payloads)]; the caller keeps `payloads` alive
+template <class C>
+py::tuple bench_writes(C& c, const std::vector<std::string>& paths, const py::list& payloads, int concurrency) {
+  std::vector<BufView> pv = buf_views(payloads);
+  if (pv.empty()) throw std::invalid_argument("no payloads");
+  BenchOut o;
+  {
+    py::gil_scoped_release r;
+    bench_run(paths.size(), concurrency, &o,
+              [&](size_t i, FastClient::Times* t, uint64_t* nb, std::vector<uint8_t>*, std::string* msg) {
+                const BufView& b = pv[i % pv.size()];
+                int replicas = 0;
+                *nb = b.n;
+                return static_cast<int>(c.write(paths[i], b.p, b.n, &replicas, msg, t));
+              });
+  }
+  return bench_result(o, false);
+}
+
+// reads: expected[i] (or None) is compared with what paths[i] returned
+py::tuple bench_reads_fast(FastClient& c, const std::vector<std::string>& paths, const py::list& expected,
+                           int concurrency) {
+  std::vector<BufView> ev = buf_views(expected);
+  BenchOut o;
+  std::atomic<uint64_t> bad{0};
+  {
+    py::gil_scoped_release r;
+    bench_run(paths.size(), concurrency, &o,
+              [&](size_t i, FastClient::Times* t, uint64_t* nb, std::vector<uint8_t>* buf, std::string* msg) {
+                int64_t slot = -1;
+                uint64_t n = 0;
+                FastClient::Status st = c.read(paths[i], &slot, &n, msg, t);
+                if (st != FastClient::Ok) return static_cast<int>(st);
+                if (buf->size() < n) buf->resize(n);
+                if (n) std::memcpy(buf->data(), c.slot_ptr(slot), n);
+                if (slot >= 0) c.release(slot);
+                *nb = n;
+                if (i < ev.size() && ev[i].p && (ev[i].n != n || std::memcmp(ev[i].p, buf->data(), n) != 0)) bad++;
+                return static_cast<int>(st);
+              });
+  }
+  o.mismatches = bad.load();
+  return bench_result(o, true);
+}
+
+py::tuple bench_reads_remote(RemoteClient& c, const std::vector<std::string>& paths, const py::list& expected,
+                             int concurrency) {
+  std::vector<BufView> ev = buf_views(expected);
+  BenchOut o;
+  std::atomic<uint64_t> bad{0};
+  {
+    py::gil_scoped_release r;
+    bench_run(paths.size(), concurrency, &o,
+              [&](size_t i, FastClient::Times* t, uint64_t* nb, std::vector<uint8_t>*, std::string* msg) {
+                std::string data;  // the reply's payload, owned by this op
+                FastClient::Status st = c.read(paths[i], &data, msg, t);
+                if (st != FastClient::Ok) return static_cast<int>(st);
+                *nb = data.size();
+                if (i < ev.size() && ev[i].p &&
+                    (ev[i].n != data.size() || std::memcmp(ev[i].p, data.data(), data.size()) != 0))
+                  bad++;
+                return static_cast<int>(st);
+              });
+  }
+  o.mismatches = bad.load();
+  return bench_result(o, true);
+}
 
 }  // namespace
 
@@ -532,7 +679,9 @@ void bind_meta(py::module_& m) {
           }
         }
         return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
-      }, py::arg("path"), py::arg("request_id") = "", py::arg("offset") = 0, py::arg("length") = 0);
+      }, py::arg("path"), py::arg("request_id") = "", py::arg("offset") = 0, py::arg("length") = 0)
+      .def("bench_writes", &bench_writes<FastClient>, py::arg("paths"), py::arg("payloads"), py::arg("concurrency"))
+      .def("bench_reads", &bench_reads_fast, py::arg("paths"), py::arg("expected"), py::arg("concurrency"));
 
   // ---------------- native remote client (every RPC over gRPC/TCP, client_remote.h)
   py::class_<RemoteClient>(m, "RemoteClient")
@@ -568,7 +717,9 @@ void bind_meta(py::module_& m) {
         }
         py::object data = st == FastClient::Ok ? py::object(py::bytes(out)) : py::object(py::none());
         return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
-      }, py::arg("path"), py::arg("request_id") = "", py::arg("offset") = 0, py::arg("length") = 0);
+      }, py::arg("path"), py::arg("request_id") = "", py::arg("offset") = 0, py::arg("length") = 0)
+      .def("bench_writes", &bench_writes<RemoteClient>, py::arg("paths"), py::arg("payloads"), py::arg("concurrency"))
+      .def("bench_reads", &bench_reads_remote, py::arg("paths"), py::arg("expected"), py::arg("concurrency"));
 
   // raw native gRPC unary call (interop tests)
   m.def("grpc_call", [](const std::string& target, const std::string& path, py::bytes req, const std::string& rid,

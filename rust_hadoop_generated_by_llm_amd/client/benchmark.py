@@ -9,6 +9,8 @@ import time
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 
+from .client import DfsError
+
 
 @dataclass
 class Stats:
@@ -69,12 +71,67 @@ def make_payloads(n: int, size: int) -> list[bytes]:
     return [os.urandom(size) for _ in range(n)]
 
 
+_PHASES = {"write": ("crc", "create", "write", "md5_wait", "complete"), "read": ("getinfo", "read")}
+
+
+def _native_run(client, kind: str, names: list[str], bufs: list, concurrency: int) -> Stats | None:
+    """The benchmark workers as native threads over the client's native data path
+    (`bench_writes` / `bench_reads` in csrc/bindings_meta.cpp), like the reference CLI's
+    tokio tasks (dfs_cli.rs:594-690). None when the client has no native path (TLS, hedged
+    reads, no co-located chunkserver and no remote client) or DFS_BENCH_NATIVE=0. Ops the
+    native client does not own come back as NotHandled and are redone on the Python path,
+    so every name ends up written / read exactly as `create_file_from_buffer` /
+    `get_file_content` would do it."""
+    if os.environ.get("DFS_BENCH_NATIVE", "1") == "0":
+        return None
+    fc = (client._fast if client._fast is not None else client._remote) if kind == "write" else client._native_reader()
+    if fc is None or not hasattr(fc, "bench_writes"):
+        return None
+    t0 = time.perf_counter()
+    if kind == "write":
+        status, lat, _, times, nbytes, err, _ = fc.bench_writes(names, bufs, concurrency)
+    else:
+        status, lat, _, times, nbytes, err, bad = fc.bench_reads(names, bufs, concurrency)
+    lat = list(lat)
+    for i, st in enumerate(status):
+        if st == 2:
+            raise DfsError(err or f"{kind} of {names[i]} failed")
+        if st == 1:  # not handled natively: the Python client's path, timed the same way
+            t = time.perf_counter()
+            if kind == "write":
+                client.create_file_from_buffer(bufs[i % len(bufs)], names[i])
+            else:
+                data = client.get_file_content(names[i])
+                nbytes[i] = len(data)
+                if bufs and bufs[i] is not None and bufs[i] != data:
+                    raise RuntimeError(f"content mismatch reading {names[i]}")
+            lat[i] = time.perf_counter() - t
+    total = time.perf_counter() - t0
+    if kind == "read" and bad:
+        raise RuntimeError(f"content mismatch on {bad} native reads")
+    done = sum(1 for st in status if st == 0)
+    if fc is getattr(client, "_remote", None):
+        client.remote_ops += done
+    else:
+        client.fp_ops += done
+    if client.phase_times is not None:
+        for st, tv in zip(status, times):
+            if st == 0:
+                for name, v in zip(_PHASES[kind], tv):
+                    client.phase_times.setdefault(name, []).append(v)
+    n = len(names)
+    return Stats("Write" if kind == "write" else "Read", n, sum(nbytes) // max(1, n), total, lat)
+
+
 def bench_write(client, count: int = 100, size: int = 1 << 20, concurrency: int = 10, prefix: str = "bench_write",
                 payloads: list[bytes] | None = None, run_id: str | None = None,
                 pool: ThreadPoolExecutor | None = None) -> tuple[Stats, list[str]]:
     payloads = payloads or make_payloads(min(count, 64), size)
     run_id = run_id or str(int(time.time()))
     names = [f"{prefix}/{run_id}/bench_{i:010d}" for i in range(count)]
+    nat = _native_run(client, "write", names, payloads, concurrency)
+    if nat is not None:
+        return nat, names
     lat: list[float] = []
     lock = threading.Lock()
 
@@ -105,6 +162,9 @@ def bench_read(client, prefix: str = "bench_write", concurrency: int = 10, files
         files = [f for f in client.list_all_files() if f.startswith(prefix)]
     if not files:
         return Stats("Read", 0, 0, 0.0)
+    nat = _native_run(client, "read", files, [verify.get(f) for f in files] if verify else [], concurrency)
+    if nat is not None:
+        return nat
     lat: list[float] = []
     total_bytes = [0]
     lock = threading.Lock()

@@ -95,9 +95,13 @@ class Client:
         # native client data path (csrc/client_fast.cpp): whole writes/reads of single-block
         # files through a co-located chunkserver and same-host masters, without the GIL
         self._fast = None
+        # MD5 workers of the native clients: the ETag hash (~1 ms per MiB, one core, strictly
+        # sequential) is the longest CPU step of a write, so keep one worker per in-flight
+        # write of a concurrency-10 benchmark plus headroom; idle workers cost nothing
+        hash_threads = int(os.environ.get("DFS_HASH_THREADS", "16"))
         if (self.fastpath is not None and self.defer_create and not self.tls
                 and os.environ.get("DFS_NATIVE_CLIENT", "1") == "1"):
-            fc = _native.FastClient(self.fastpath.name, self.local_chunkserver)
+            fc = _native.FastClient(self.fastpath.name, self.local_chunkserver, hash_threads=hash_threads)
             if fc.ok:
                 self._fast = fc
         # native remote client (csrc/client_remote.cpp): the same single-block writes/reads for
@@ -105,7 +109,7 @@ class Client:
         self._remote = None
         if (self._fast is None and self.defer_create and not self.tls
                 and os.environ.get("DFS_NATIVE_REMOTE", "1") == "1"):
-            self._remote = _native.RemoteClient(4, int(data_timeout * 1000))
+            self._remote = _native.RemoteClient(hash_threads, int(data_timeout * 1000))
         self.remote_ops = 0
         self._sync_fast()
 

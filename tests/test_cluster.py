@@ -268,6 +268,37 @@ def test_local_short_circuit_and_fast_path():
         c.close()
 
 
+def test_native_benchmark_workers():
+    """`dfs_cli benchmark` workers as native threads (bench_writes / bench_reads): every
+    file written and read back byte-exact, a wrong expected payload is reported, and ops
+    the native client does not own (a stale fast-path socket) are redone in Python."""
+    from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_read, bench_write, make_payloads
+    from rust_hadoop_generated_by_llm_amd.native import lib as native
+
+    with LocalCluster(n_chunkservers=1, fsync=False) as cl:
+        c = cl.client(local_chunkserver=cl.cs_addrs[0])
+        c.phase_times = {}
+        payloads = make_payloads(3, 70_000)
+        ws, names = bench_write(c, 9, 70_000, 4, prefix="/nb", payloads=payloads, run_id="a")
+        assert ws.count == 9 and len(ws.latencies) == 9 and c._fast.writes == 9
+        assert set(c.phase_times) >= {"crc", "create", "write", "md5_wait", "complete"}
+        verify = {nm: payloads[i % 3] for i, nm in enumerate(names)}
+        rs = bench_read(c, files=names, concurrency=4, verify=verify)
+        assert rs.count == 9 and rs.avg_size == 70_000 and c._fast.reads == 9
+        for nm in names:
+            assert c.get_file_content(nm) == verify[nm]
+        with pytest.raises(RuntimeError, match="mismatch"):
+            bench_read(c, files=names, concurrency=4, verify={nm: b"x" * 70_000 for nm in names})
+        # NotHandled from the native client: the Python path writes and reads those names
+        c._fast = native.FastClient("dfs_fp_nonexistent", cl.cs_addrs[0])
+        c._sync_fast()
+        ws, names2 = bench_write(c, 4, 70_000, 2, prefix="/nb", payloads=payloads, run_id="b")
+        assert ws.count == 4 and c._fast.writes == 0
+        rs = bench_read(c, files=names2, concurrency=2, verify={nm: payloads[i % 3] for i, nm in enumerate(names2)})
+        assert rs.count == 4 and rs.avg_size == 70_000
+        c.close()
+
+
 def test_tls_cluster():
     """gRPC over TLS end to end (reference C06 TLS helper): masters and chunkservers serve
     with a CA-signed certificate, clients verify it; a plaintext client cannot talk to them."""
