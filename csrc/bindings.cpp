@@ -268,6 +268,18 @@ PYBIND11_MODULE(_dfs_native, m) {
         return py::make_tuple(static_cast<int>(rr.status), rr.total_size, rr.bytes, rr.partial_corrupt,
                               rr.bad_slice, rr.error);
       }, py::arg("block_id"), py::arg("offset"), py::arg("length"), py::arg("out"))
+      // pin a caller buffer for device DMA / kernel stores, as the fast path pins a client's
+      // shared-memory arena (tests and benches of the zero-copy and fused read paths)
+      .def("register_host", [](ChunkStore& s, py::buffer b) {
+        py::buffer_info bi = b.request(true);
+        py::gil_scoped_release r;
+        return s.register_host(bi.ptr, static_cast<uint64_t>(bi.size * bi.itemsize));
+      }, py::arg("buffer"))
+      .def("unregister_host", [](ChunkStore& s, py::buffer b) {
+        py::buffer_info bi = b.request(true);
+        py::gil_scoped_release r;
+        s.unregister_host(bi.ptr);
+      }, py::arg("buffer"))
       .def("exists", &ChunkStore::exists)
       .def("size", &ChunkStore::block_size)
       .def("crc", &ChunkStore::block_crc, py::call_guard<py::gil_scoped_release>())
@@ -308,6 +320,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["gpu_kernel_launches"] = t.gpu_kernel_launches;
         d["disk_gate_waits"] = t.disk_gate_waits;
         d["direct_dma"] = t.direct_dma;
+        d["fused_reads"] = t.fused_reads;
         d["staged_dma"] = t.staged_dma;
         d["host_registered_bytes"] = t.host_registered_bytes;
         return d;

@@ -393,9 +393,26 @@ bool ChunkStore::register_host(const void* p, uint64_t n) {
     (void)hipGetLastError();
     return false;
   }
+  void* dp = nullptr;
+  if (hipHostGetDevicePointer(&dp, const_cast<void*>(p), 0) != hipSuccess) {
+    (void)hipGetLastError();
+    dp = nullptr;
+  }
   std::lock_guard<std::mutex> g(reg_mu_);
   reg_.emplace_back(reinterpret_cast<uintptr_t>(p), n);
+  reg_dev_.push_back(reinterpret_cast<uintptr_t>(dp));
   return true;
+}
+
+uint8_t* ChunkStore::device_view(const void* p, uint64_t n) {
+  uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> g(reg_mu_);
+  for (size_t k = 0; k < reg_.size(); ++k) {
+    const auto& r = reg_[k];
+    if (a >= r.first && n <= r.second && a - r.first <= r.second - n)
+      return reg_dev_[k] ? reinterpret_cast<uint8_t*>(reg_dev_[k] + (a - r.first)) : nullptr;
+  }
+  return nullptr;
 }
 
 void ChunkStore::unregister_host(const void* p) {
@@ -405,6 +422,7 @@ void ChunkStore::unregister_host(const void* p) {
     if (it->first == reinterpret_cast<uintptr_t>(p)) {
       (void)hipSetDevice(cfg_.device);
       (void)hipHostUnregister(const_cast<void*>(p));
+      reg_dev_.erase(reg_dev_.begin() + (it - reg_.begin()));
       reg_.erase(it);
       return;
     }
@@ -924,15 +942,38 @@ ReadResult ChunkStore::read_into(const std::string& id, uint64_t offset, uint64_
   std::string err;
   CrcOut co;
   CrcPlan p = plan_crc(d, size, nullptr, dmeta, false, offset, offset + bytes);
-  if (p.grid > 0) {
-    p.a.part_bad = l->dscratch + kMaxGridCrc;
-    hipError_t e = launch_crc(p.a, dtables_, p.grid, l->stream);
+  static const bool fused_ok = [] {
+    const char* e = std::getenv("DFS_FUSED_READ");
+    return !(e && e[0] == '0');
+  }();
+  uint8_t* dout = fused_ok && crc_mfma_enabled() ? device_view(out, bytes) : nullptr;
+  void* dbad = nullptr;
+  if (dout && (reinterpret_cast<uintptr_t>(dout) - offset) % 16 == 0 && p.grid > 0 && p.grid <= kMaxGridCrc &&
+      hipHostGetDevicePointer(&dbad, l->hscratch, 0) == hipSuccess && dbad) {
+    // K3 fused: one kernel verifies the touched slices and stores the range into the
+    // reader's registered slot; its verdicts land in the lane's pinned scratch
+    ReadCopyLaunch rc;
+    rc.c = p.a;
+    rc.out = dout;
+    rc.off = offset;
+    rc.len = bytes;
+    rc.part_bad = static_cast<uint32_t*>(dbad);
+    hipError_t e = launch_read_copy(rc, dtables_, p.grid, l->stream);
     launches_++;
     if (e != hipSuccess) err = hipGetErrorString(e);
-    HIP_OK(hipMemcpyAsync(l->hscratch, l->dscratch + kMaxGridCrc, p.grid * 4, hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+    fused_reads_++;
+  } else {
+    if (p.grid > 0) {
+      p.a.part_bad = l->dscratch + kMaxGridCrc;
+      hipError_t e = launch_crc(p.a, dtables_, p.grid, l->stream);
+      launches_++;
+      if (e != hipSuccess) err = hipGetErrorString(e);
+      HIP_OK(hipMemcpyAsync(l->hscratch, l->dscratch + kMaxGridCrc, p.grid * 4, hipMemcpyDeviceToHost, l->stream));
+    }
+    d2h_chunked(l, out, d + offset, bytes);  // overlaps with verification on the same stream order
+    HIP_OK(hipStreamSynchronize(l->stream));
   }
-  d2h_chunked(l, out, d + offset, bytes);  // overlaps with verification on the same stream order
-  HIP_OK(hipStreamSynchronize(l->stream));
   uint32_t bad = 0xFFFFFFFFu;
   for (int g = 0; g < p.grid; ++g) bad = std::min(bad, reinterpret_cast<uint32_t*>(l->hscratch)[g]);
   release_lane(l);
@@ -1695,6 +1736,7 @@ StoreStats ChunkStore::stats() {
   s.spill_queue = spill_q_.size();
   s.gpu_kernel_launches = launches_.load();
   s.direct_dma = direct_dma_.load();
+  s.fused_reads = fused_reads_.load();
   s.staged_dma = staged_dma_.load();
   s.mirror_hits = mirror_hits_;
   s.mirror_bytes = mirror_bytes_;

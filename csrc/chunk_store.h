@@ -82,6 +82,7 @@ struct StoreStats {
   uint64_t gpu_kernel_launches = 0;
   uint64_t disk_gate_waits = 0;  // durable writes that queued for a node-wide disk slot
   uint64_t direct_dma = 0;       // host<->HBM copies done straight from registered memory
+  uint64_t fused_reads = 0;      // reads delivered by the K3 verify+copy kernel (no SDMA copy)
   uint64_t staged_dma = 0;       // copies bounced through pinned staging buffers
   uint64_t host_registered_bytes = 0;
   uint64_t mirror_hits = 0;      // small-block reads served from the verified host mirror
@@ -285,6 +286,10 @@ class ChunkStore {
   bool host_registered(const void* p, uint64_t n);
   std::mutex reg_mu_;
   std::vector<std::pair<uintptr_t, uint64_t>> reg_;  // registered host ranges
+  std::vector<uintptr_t> reg_dev_;  // device-visible address of each reg_ range (0 = none)
+  // device-visible alias of registered host memory [p, p + n), nullptr if not registered
+  uint8_t* device_view(const void* p, uint64_t n);
+  std::atomic<uint64_t> fused_reads_{0};  // K3 fused verify+copy reads
   std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};  // unique temporary file names for in-flight writes
   std::unique_ptr<GroupSync> gsync_;
   std::unique_ptr<DiskGate> gate_;

@@ -103,6 +103,18 @@ constexpr int kStreamReadGrid = 2048;
 hipError_t launch_stream_read(const uint8_t* d, uint64_t n, uint32_t* out, hipStream_t s);
 
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
+
+// K3 fused verify + copy of a range read (crc_read_copy_kernel): `c` is the range plan
+// (meta_expect set, part_* unused), `out` a device-visible pointer (registered host memory)
+// that receives [off, off + len) with (out - off) % 16 == 0, `part_bad` [grid] device-visible
+// words (min mismatching slice per workgroup, 0xFFFFFFFF = none). grid <= kMaxGridCrc.
+struct ReadCopyLaunch {
+  CrcLaunch c;
+  uint8_t* out;
+  uint64_t off, len;
+  uint32_t* part_bad;
+};
+hipError_t launch_read_copy(const ReadCopyLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
 hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s);
 hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s);
 

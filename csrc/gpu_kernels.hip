@@ -450,6 +450,96 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
   }
 }
 
+// K3 fused: verify AND deliver a read in one pass over HBM. The data the MFMA chunk CRC
+// already holds in registers is stored straight to the reader's buffer — host memory that
+// the store registered (the client's shared-memory slot), so the stores cross PCIe from the
+// CUs — instead of a verify kernel followed by an SDMA copy that reads the same bytes from
+// HBM again, plus a second small copy for the verdict. Only bytes inside [off, off + len)
+// are stored; the verdict per workgroup goes to host-visible memory too, so one kernel and
+// one stream sync make the whole read. The host guarantees (out - off) % 16 == 0.
+// Bytes of lane segment `q` (0..7, dwords of the lane's 32 B) of iteration `it`.
+__device__ __forceinline__ uint32_t seg_dword(const WaveData& d, int it, int q) {
+  const uint4 v = d.v[2 * it + (q >> 2)];
+  const int k = q & 3;
+  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+}
+
+__device__ __forceinline__ void store_wave(const ReadCopyLaunch& a, int64_t i0, const WaveData& d, int lane) {
+  const int n = lane & 31, h = lane >> 5;
+  const int64_t lo = static_cast<int64_t>(a.c.slice_lo), hi = static_cast<int64_t>(a.c.slice_hi);
+  const uint64_t end = a.off + a.len;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = it * 32 + n;
+    const int64_t i = i0 + (c >> 3);
+    if (i < lo || i >= hi) continue;
+    const uint64_t pos = static_cast<uint64_t>(i) * 512 + (c & 7) * 64 + h * 32;
+    if (pos >= a.off && pos + 32 <= end) {
+      uint4* dst = reinterpret_cast<uint4*>(a.out + (pos - a.off));
+      dst[0] = d.v[2 * it];
+      dst[1] = d.v[2 * it + 1];
+    } else if (pos + 32 > a.off && pos < end) {  // the range's first / last 32 B
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint32_t w = seg_dword(d, it, q);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint64_t p = pos + 4 * q + b;
+          if (p >= a.off && p < end) a.out[p - a.off] = static_cast<uint8_t>(w >> (8 * b));
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void crc_read_copy_kernel(
+    ReadCopyLaunch a, const DevCrcTables* __restrict__ gt) {
+  __shared__ MfmaSliceLds lt;
+  __shared__ uint32_t wg_bad;
+  const CrcLaunch& c = a.c;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
+  const uint64_t per = (c.ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
+  const uint64_t t_end = t_begin + per < c.ntiles ? t_begin + per : c.ntiles;
+  const int64_t lo = static_cast<int64_t>(c.slice_lo), hi = static_cast<int64_t>(c.slice_hi);
+  auto first_slice = [&](uint64_t t) { return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8); };
+  WaveData cur;
+  if (t_begin < t_end) cur = load_wave(c.data, first_slice(t_begin), lo, hi, lane);
+  i32x4 A[16];
+  load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
+  load_lds_image(gt, &lt);
+  if (threadIdx.x == 0) wg_bad = 0xFFFFFFFFu;
+  __syncthreads();
+
+  uint32_t bad = 0xFFFFFFFFu;
+  for (uint64_t t = t_begin; t < t_end; ++t) {
+    WaveData nxt;
+    if (t + 1 < t_end) nxt = load_wave(c.data, first_slice(t + 1), lo, hi, lane);
+    const int64_t i0 = first_slice(t);
+    store_wave(a, i0, cur, lane);
+    const uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, cur, lane), lane);
+    const int64_t i = i0 + sw;
+    if (i >= lo && i < hi && sl == 0 && c.meta_expect[i] != __builtin_bswap32(r ^ c.full_init))
+      bad = min(bad, static_cast<uint32_t>(i));
+    if (t + 1 < t_end) cur = nxt;
+  }
+
+  if (c.has_tail && blockIdx.x == 0 && wave == 0) {
+    const uint8_t* base = c.data + c.s_full * 512;
+    const uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(base, c.tail_len, lane), lane), lane);
+    if (lane == 0 && c.meta_expect[c.s_full] != __builtin_bswap32(r ^ c.tail_init))
+      bad = min(bad, static_cast<uint32_t>(c.s_full));
+    const uint64_t p0 = c.s_full * 512, end = a.off + a.len;
+    for (uint32_t k = lane; k < c.tail_len; k += 64) {
+      const uint64_t p = p0 + k;
+      if (p >= a.off && p < end) a.out[p - a.off] = base[k];
+    }
+  }
+  if (bad != 0xFFFFFFFFu) atomicMin(&wg_bad, bad);
+  __syncthreads();
+  if (threadIdx.x == 0) a.part_bad[blockIdx.x] = wg_bad;
+}
+
 // K1b on the matrix cores: contiguous tile runs per workgroup, so the tile -> block lookup is
 // one binary search per workgroup and then a forward walk, and the next tile's data (and its
 // block) are fetched while the current tile computes.
@@ -916,6 +1006,13 @@ hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipSt
     case 3: hipLaunchKernelGGL(crc_tile_ring_kernel<3>, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
     default: hipLaunchKernelGGL(crc_tile_ring_kernel<4>, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_read_copy(const ReadCopyLaunch& a, const DevCrcTables* t, int grid, hipStream_t s) {
+  if (grid <= 0) return hipSuccess;
+  if (grid > kMaxGridCrc) return hipErrorInvalidValue;  // part_bad holds kMaxGridCrc words
+  hipLaunchKernelGGL(crc_read_copy_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
   return hipGetLastError();
 }
 

@@ -179,3 +179,50 @@ def test_gpu_small_block_mirror(gstore):
     assert st == 0 and partial and bad == 58
     assert gstore.stats()["mirror_hits"] == h0 + 2  # the damaged mirror served nothing
     gstore.remove("mir")
+
+
+def test_gpu_fused_read_copy(gstore):
+    """K3 fused verify + copy (crc_read_copy_kernel): reads into a registered buffer are one
+    kernel that checks every touched slice and stores the range straight into host memory.
+    Whole blocks, slice-unaligned ranges (byte-wise edges), tails, and a corruption that
+    must still be reported; bytes outside the range are never written."""
+    import numpy as np
+
+    buf = np.zeros((40 << 20) + 4096, dtype=np.uint8)
+    assert gstore.register_host(buf)
+    try:
+        sizes = [(1 << 20), (1 << 20) + 777, 300000, 3 * (1 << 20) + 1, (33 << 20) + 512 * 3 + 5]
+        datas = {}
+        for i, n in enumerate(sizes):
+            d = os.urandom(n)
+            assert gstore.write(f"fz{i}", d, zlib.crc32(d))[0]
+            datas[f"fz{i}"] = d
+        f0 = gstore.stats()["fused_reads"]
+        expect_fused = 0
+        cases = [(0, 0), (0, 4096), (512 * 7, 512 * 9), (100, 70001), (1000, 1), (511, 2)]
+        for bid, d in datas.items():
+            n = len(d)
+            for off, ln in cases + [(n - 600, 600), (n - 1, 1), (n // 2 + 3, n // 2 - 3)]:
+                ln = n if ln == 0 else ln
+                if off + ln > n:
+                    continue
+                k = off % 16  # (out - off) % 16 == 0 keeps the 16 B stores aligned
+                buf[:] = 0xA5
+                st, total, got, partial, bad, err = gstore.read_into(bid, off, ln, buf[k:])
+                assert st == 0 and not partial, (bid, off, ln, err)
+                assert got == ln and buf[k:k + ln].tobytes() == d[off:off + ln], (bid, off, ln)
+                assert (buf[:k] == 0xA5).all() and (buf[k + ln:k + ln + 4096] == 0xA5).all(), (bid, off, ln)
+                expect_fused += 1
+        assert gstore.stats()["fused_reads"] - f0 == expect_fused  # every read took the fused kernel
+        # corruption: the whole-block read fails, a range around it reports the slice
+        assert gstore.debug_corrupt("fz1", 700000)
+        st, *_rest, err = gstore.read_into("fz1", 0, len(datas["fz1"]), buf)
+        assert st == 3 and f"chunk {700000 // 512}" in err
+        st, total, got, partial, bad, err = gstore.read_into("fz1", 699000, 4000, buf[699000 % 16:])
+        assert st == 0 and partial and bad == 700000 // 512
+        st, total, got, partial, bad, err = gstore.read_into("fz1", 0, 65536, buf)
+        assert st == 0 and not partial and buf[:65536].tobytes() == datas["fz1"][:65536]
+    finally:
+        gstore.unregister_host(buf)
+        for i in range(5):
+            gstore.remove(f"fz{i}")
