@@ -18,6 +18,7 @@ constexpr int kSlicesPerTile = 32;  // 4 waves x 8 slices x 512 B = 16 KiB per t
 constexpr int kMaxGridCrc = 768;  // 3 resident workgroups x 256 CUs (see crc_tile_mfma_kernel)
 constexpr int kMaxShards = 32;
 constexpr int kCrcBasisBytes = 16 * 64 * 16;  // MFMA basis (A fragments), stored after DevCrcTables
+constexpr int kCrcChunkShiftBytes = 7 * 4 * 256 * 4;  // chunk -> slice shift tables, stored after the basis
 
 struct DevCrcTables {
   uint32_t slice16[16][256];

@@ -190,35 +190,53 @@ __device__ __forceinline__ uint32_t wave_chunk_crcs(const i32x4 (&A)[16], const 
   return mine;
 }
 
-// Chunk CRCs -> slice CRC (lane sl == 0 of each 8-lane group), as slice_crc does.
+// Chunk CRCs -> slice CRC in one lookup round: lane sl of a slice's 8-lane group moves its
+// chunk CRC past the 64 * (7 - sl) bytes that follow the chunk in the slice (one tab4 into
+// its own shift table; sl == 7 needs none) and three xor-shuffles fold the group, since the
+// raw CRC of a concatenation is the XOR of the shifted parts. Every lane of the group ends
+// with the slice CRC. (The butterfly it replaces did three dependent tab4 rounds — 12 LDS
+// lookups per lane, the kernels' only bank conflicts — for the same result.)
 template <class L>
 __device__ __forceinline__ uint32_t slice_from_chunks(const L& lt, uint32_t r, int lane) {
-  r = combine(r, 1, lane, lt.sh64);
-  r = combine(r, 2, lane, lt.sh128);
-  return combine(r, 4, lane, lt.sh256);
+  const int sl = lane & 7;
+  uint32_t v = sl < 7 ? tab4(lt.cs[sl], r) : r;
+  v ^= __shfl_xor(v, 1);
+  v ^= __shfl_xor(v, 2);
+  return v ^ __shfl_xor(v, 4);
 }
 
 // LDS images of the matrix-core kernels: only the GF(2) shift tables they look up (the
 // slicing-by-16 tables of the table kernels are not needed: short tail slices go through
-// the MFMA path front-padded with zeros). A prefix of DevCrcTables from sh64 on.
-struct MfmaSliceLds {  // K1b: chunk -> slice combine (12 KiB)
-  uint32_t sh64[4][256], sh128[4][256], sh256[4][256];
+// the MFMA path front-padded with zeros). `cs` comes from the chunk-shift tables stored
+// behind the MFMA basis, the tile part is the suffix of DevCrcTables from sh512 on.
+struct MfmaSliceLds {  // K1b, fused K3: chunk -> slice combine (28 KiB)
+  uint32_t cs[7][4][256];
 };
-struct MfmaTileLds {  // K1/K2/K3: + slice -> sub-tile combine and the tile shifts (32 KiB)
-  uint32_t sh64[4][256], sh128[4][256], sh256[4][256];
+struct MfmaTileLds {  // K1/K2/K3: + slice -> sub-tile combine and the tile shifts (48 KiB)
+  uint32_t cs[7][4][256];
   uint32_t sh512[4][256], sh1k[4][256], sh2k[4][256];
   uint32_t sh4k[4][256];
   uint32_t tile_pow2[32][32];
 };
-static_assert(sizeof(MfmaTileLds) == sizeof(DevCrcTables) - offsetof(DevCrcTables, sh64), "LDS image layout");
+static_assert(sizeof(MfmaSliceLds) == kCrcChunkShiftBytes, "chunk-shift image");
+static_assert(sizeof(MfmaTileLds) - sizeof(MfmaSliceLds) == sizeof(DevCrcTables) - offsetof(DevCrcTables, sh512),
+              "LDS image layout");
+
+__device__ __forceinline__ void copy16(const void* __restrict__ from, void* to, int bytes) {
+  const uint4* src = reinterpret_cast<const uint4*>(from);
+  uint4* dst = reinterpret_cast<uint4*>(to);
+  const int n16 = bytes / 16;
+#pragma unroll 4
+  for (int i = threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
+}
 
 template <class L>
 __device__ __forceinline__ void load_lds_image(const DevCrcTables* __restrict__ gt, L* lt) {
-  const uint4* src = reinterpret_cast<const uint4*>(&gt->sh64);
-  uint4* dst = reinterpret_cast<uint4*>(lt);
-  constexpr int n16 = sizeof(L) / 16;
-#pragma unroll 4
-  for (int i = threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
+  const uint8_t* cs = reinterpret_cast<const uint8_t*>(gt + 1) + kCrcBasisBytes;
+  copy16(cs, lt, kCrcChunkShiftBytes);
+  if constexpr (sizeof(L) > kCrcChunkShiftBytes)
+    copy16(&gt->sh512, reinterpret_cast<uint8_t*>(lt) + kCrcChunkShiftBytes,
+           static_cast<int>(sizeof(L)) - kCrcChunkShiftBytes);
 }
 
 // The short tail slice (len < 512 bytes at `base`) as slice 0 of a wave's 4 KiB, front-padded
@@ -961,7 +979,10 @@ DevCrcTables* upload_crc_tables(hipStream_t s) {
   // MFMA basis right behind the LDS image (never copied to LDS): fragment [s][lane] of A,
   // element j = byte j of the 16 B: CRC bit i = lane & 31 of V[32h + 4(s>>1) + (j&3)][4(s&1) + (j>>2)],
   // scaled by 2^(7-p) (see wave_chunk_crcs)
-  host.resize(sizeof(DevCrcTables) + kCrcBasisBytes);
+  host.resize(sizeof(DevCrcTables) + kCrcBasisBytes + kCrcChunkShiftBytes);
+  // chunk-shift tables behind the basis: cs[sl] moves a 64 B chunk's CRC past 64 * (7 - sl) bytes
+  auto* cs = reinterpret_cast<uint32_t(*)[4][256]>(host.data() + sizeof(DevCrcTables) + kCrcBasisBytes);
+  for (int sl = 0; sl < 7; ++sl) shift_table(64 * (7 - sl), cs[sl]);
   int8_t* basis = reinterpret_cast<int8_t*>(host.data() + sizeof(DevCrcTables));
   for (int st = 0; st < 16; ++st)
     for (int lane = 0; lane < 64; ++lane)
