@@ -302,6 +302,10 @@ void ChunkStore::ensure_hscratch(Lane* l, uint64_t bytes) {
   if (l->hscratch) HIP_OK(hipHostFree(l->hscratch));
   HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&l->hscratch), bytes, hipHostMallocDefault));
   l->hscratch_cap = bytes;
+  if (hipHostGetDevicePointer(&l->hscratch_dev, l->hscratch, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    l->hscratch_dev = nullptr;
+  }
 }
 
 // Enqueue the CRC kernel on the lane stream and the D2H of its partials into hscratch
@@ -947,9 +951,8 @@ ReadResult ChunkStore::read_into(const std::string& id, uint64_t offset, uint64_
     return !(e && e[0] == '0');
   }();
   uint8_t* dout = fused_ok && crc_mfma_enabled() ? device_view(out, bytes) : nullptr;
-  void* dbad = nullptr;
-  if (dout && (reinterpret_cast<uintptr_t>(dout) - offset) % 16 == 0 && p.grid > 0 && p.grid <= kMaxGridCrc &&
-      hipHostGetDevicePointer(&dbad, l->hscratch, 0) == hipSuccess && dbad) {
+  void* dbad = l->hscratch_dev;
+  if (dout && dbad && (reinterpret_cast<uintptr_t>(dout) - offset) % 16 == 0 && p.grid > 0 && p.grid <= kMaxGridCrc) {
     // K3 fused: one kernel verifies the touched slices and stores the range into the
     // reader's registered slot; its verdicts land in the lane's pinned scratch
     ReadCopyLaunch rc;

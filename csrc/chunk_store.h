@@ -218,6 +218,7 @@ class ChunkStore {
     uint32_t* dscratch = nullptr;  // device: part_crc[kMaxGridCrc], part_bad[kMaxGridCrc]
     uint8_t* hscratch = nullptr;   // pinned: meta image + partials
     uint64_t hscratch_cap = 0;
+    void* hscratch_dev = nullptr;  // device-visible alias of hscratch (fused-read verdicts)
   };
   static constexpr uint64_t kChunk = 4ull << 20;
 

@@ -1,5 +1,10 @@
 #include "cs_grpc.h"
 
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
 #include "dfs_pb.h"
 #include "trace.h"
 
@@ -15,10 +20,70 @@ void put_varint(std::string& o, uint64_t v) {
   }
   o.push_back(static_cast<char>(v));
 }
+
+size_t put_varint(uint8_t* o, uint64_t v) {
+  size_t n = 0;
+  while (v >= 0x80) {
+    o[n++] = static_cast<uint8_t>((v & 0x7F) | 0x80);
+    v >>= 7;
+  }
+  o[n++] = static_cast<uint8_t>(v);
+  return n;
+}
 }  // namespace
 
+// Registered reply buffers for ReadBlock. A read that lands in memory the store has pinned
+// is one fused verify+copy kernel straight into the reply (K3, crc_read_copy_kernel) —
+// instead of a zero-filled std::string plus the staged bounce copy an unregistered
+// destination needs. Buffers are made on demand (at most kMax, one per in-flight read),
+// registered once, recycled when nghttp2 has sent the last byte, and live as long as the
+// process (the chunkserver's store outlives every reply).
+class ReplyPool : public std::enable_shared_from_this<ReplyPool> {
+ public:
+  static constexpr size_t kBytes = (4u << 20) + 4096;  // reads up to 4 MiB
+  static constexpr size_t kMax = 64;
+  static constexpr size_t kHead = 64;  // data starts at kHead + offset % 16 (fused-read alignment)
+  explicit ReplyPool(ChunkStore* s) : store_(s) {}
+
+  std::shared_ptr<uint8_t> take() {
+    uint8_t* b = nullptr;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!free_.empty()) {
+        b = free_.back();
+        free_.pop_back();
+      } else if (made_ < kMax) {
+        ++made_;
+      } else {
+        return nullptr;
+      }
+    }
+    if (!b) {
+      void* p = nullptr;
+      if (::posix_memalign(&p, 4096, kBytes) != 0) {
+        std::lock_guard<std::mutex> g(mu_);
+        --made_;
+        return nullptr;
+      }
+      b = static_cast<uint8_t*>(p);
+      (void)store_->register_host(b, kBytes);  // CPU store: plain memory, still no zero fill
+    }
+    // the deleter keeps the pool alive until the last reply using it is sent
+    return std::shared_ptr<uint8_t>(b, [self = shared_from_this()](uint8_t* x) {
+      std::lock_guard<std::mutex> g(self->mu_);
+      self->free_.push_back(x);
+    });
+  }
+
+ private:
+  ChunkStore* store_;
+  std::mutex mu_;
+  std::vector<uint8_t*> free_;
+  size_t made_ = 0;
+};
+
 NativeChunkService::NativeChunkService(ChunkStore* store, FastPathServer* fp, Fallback fallback)
-    : store_(store), fp_(fp), fallback_(std::move(fallback)) {}
+    : store_(store), fp_(fp), fallback_(std::move(fallback)), replies_(std::make_shared<ReplyPool>(store)) {}
 
 CsGrpcStats NativeChunkService::stats() const {
   return {writes_.load(), reads_.load(), replicates_.load(), fallbacks_.load()};
@@ -103,6 +168,39 @@ GrpcReply NativeChunkService::read_block(const GrpcCall& call, bool* handled) {
   if (st.status != ReadStatus::Ok) return {};
   // ReadBlockResponse encoded by hand so the verified range lands in the reply buffer
   // directly: field 1 (data) header, the bytes, then bytes_read and total_size
+  static const bool pool_on = [] {
+    const char* e = std::getenv("DFS_GRPC_REPLY_POOL");
+    return !(e && e[0] == '0');
+  }();
+  std::shared_ptr<uint8_t> buf =
+      pool_on && st.bytes + ReplyPool::kHead + 16 + 32 <= ReplyPool::kBytes ? replies_->take() : nullptr;
+  if (buf) {
+    uint8_t hdr[16];
+    size_t hl = 0;
+    hdr[hl++] = 0x0A;
+    hl += put_varint(hdr + hl, st.bytes);
+    uint8_t* data = buf.get() + ReplyPool::kHead + req.offset % 16;
+    std::memcpy(data - hl, hdr, hl);
+    ReadResult rr = store_->read_into(req.block_id, req.offset, st.bytes, data);
+    if (rr.status != ReadStatus::Ok) return {};  // corrupt / vanished: the Python service recovers
+    if (rr.partial_corrupt) fp_->add_suspect(req.block_id);
+    *handled = true;
+    uint8_t* end = data + st.bytes;
+    if (rr.bytes) {
+      *end++ = 0x10;
+      end += put_varint(end, rr.bytes);
+    }
+    if (rr.total_size) {
+      *end++ = 0x18;
+      end += put_varint(end, rr.total_size);
+    }
+    reads_++;
+    GrpcReply r;
+    r.ext = data - hl;
+    r.ext_len = static_cast<size_t>(end - (data - hl));
+    r.keep = std::move(buf);
+    return r;
+  }
   std::string out;
   out.reserve(st.bytes + 32);
   out.push_back(0x0A);

@@ -10,6 +10,7 @@
 #pragma once
 #include <atomic>
 #include <functional>
+#include <memory>
 #include <string>
 
 #include "chunk_store.h"
@@ -38,6 +39,7 @@ class NativeChunkService {
   ChunkStore* store_;
   FastPathServer* fp_;
   Fallback fallback_;
+  std::shared_ptr<class ReplyPool> replies_;
   std::atomic<uint64_t> writes_{0}, reads_{0}, replicates_{0}, fallbacks_{0};
 };
 

@@ -70,7 +70,10 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     // response: prefix + message, served by read_body without concatenating them
     char prefix[5];
     std::string out;
-    size_t off = 0;  // bytes of prefix + out already handed to nghttp2
+    std::shared_ptr<const void> keep;  // owner of body_p when the reply is external
+    const uint8_t* body_p = nullptr;
+    size_t body_n = 0;
+    size_t off = 0;  // bytes of prefix + body already handed to nghttp2
     std::string status_str = "0";
     bool dispatched = false;
   };
@@ -102,7 +105,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     auto it = c->streams.find(sid);
     if (it == c->streams.end()) return NGHTTP2_ERR_TEMPORAL_CALLBACK_FAILURE;
     Stream& st = it->second;
-    const size_t total = 5 + st.out.size();
+    const size_t total = 5 + st.body_n;
     size_t n = 0;
     if (st.off < 5) {
       n = std::min(len, 5 - st.off);
@@ -111,7 +114,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     }
     if (n < len && st.off >= 5) {
       size_t m = std::min(len - n, total - st.off);
-      std::memcpy(buf + n, st.out.data() + (st.off - 5), m);
+      std::memcpy(buf + n, st.body_p + (st.off - 5), m);
       st.off += m;
       n += m;
     }
@@ -132,9 +135,17 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
                              k_gs = "grpc-status", k_gm = "grpc-message";
     if (r.status == 0) {
       st.prefix[0] = 0;
-      uint32_t n = htonl(static_cast<uint32_t>(r.message.size()));
+      if (r.ext) {
+        st.keep = std::move(r.keep);
+        st.body_p = r.ext;
+        st.body_n = r.ext_len;
+      } else {
+        st.out = std::move(r.message);
+        st.body_p = reinterpret_cast<const uint8_t*>(st.out.data());
+        st.body_n = st.out.size();
+      }
+      uint32_t n = htonl(static_cast<uint32_t>(st.body_n));
       std::memcpy(st.prefix + 1, &n, 4);
-      st.out = std::move(r.message);
       st.off = 0;
       nghttp2_nv h[] = {nv(k_status, v200), nv(k_ct, v_ct)};
       nghttp2_data_provider dp;

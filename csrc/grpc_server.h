@@ -33,6 +33,12 @@ struct GrpcCall {
 struct GrpcReply {
   int status = 0;          // grpc status code
   std::string message;     // serialized response (status 0) or grpc-message text
+  // status 0 alternative to `message`: the serialized response lives in a buffer the
+  // handler owns (e.g. registered memory a GPU read landed in); `keep` holds it until the
+  // last byte is handed to nghttp2
+  std::shared_ptr<const void> keep;
+  const uint8_t* ext = nullptr;
+  size_t ext_len = 0;
 };
 
 class GrpcServer {

@@ -21,7 +21,7 @@ def gpu_cluster():
 
     if native.gpu_count() < 1:
         pytest.fail("GPU test selected but no HIP device is visible")
-    with LocalCluster(gpus=[0], fsync=False, hbm_capacity="4G", env={"DFS_DEBUG_ENDPOINTS": "1"}) as c:
+    with LocalCluster(gpus=[0], fsync=True, hbm_capacity="4G", env={"DFS_DEBUG_ENDPOINTS": "1"}) as c:
         yield c
 
 
@@ -43,6 +43,31 @@ def test_gpu_put_get_range_and_scrub(gpu_cluster):
     assert r["corrupted"]
     bad = json.load(urllib.request.urlopen(f"{gpu_cluster.cs_http[0]}/debug/scrub"))["bad"]
     assert bad == [blk.block_id]
+    c.close()
+
+
+def test_gpu_fused_reads_local_and_remote(gpu_cluster):
+    """Reads land through the fused K3 verify+copy kernel: into the co-located client's
+    registered shm slot, and into the native gRPC server's registered reply buffers for a
+    client that is not co-located (every RPC over gRPC/TCP)."""
+    data = os.urandom((2 << 20) + 333)
+    c = gpu_cluster.client(local_chunkserver=gpu_cluster.cs_addrs[0])
+    c.create_file_from_buffer(data, "/gpu/fz")
+    f0 = stats(gpu_cluster)["fused_reads"]
+    assert c.get_file_content("/gpu/fz") == data
+    assert c.read_file_range("/gpu/fz", 4096 + 48, 100_000) == data[4144:104_144]
+    f1 = stats(gpu_cluster)["fused_reads"]
+    assert f1 - f0 >= 2
+    # a range the slot cannot hold 16 B-congruent (the fast path lands ranges at the slot
+    # start) takes the verify kernel + DMA path, with the same bytes
+    assert c.read_file_range("/gpu/fz", 777, 100_000) == data[777:100_777]
+    f1 = stats(gpu_cluster)["fused_reads"]
+    rc = gpu_cluster.client(local_chunkserver=None, local_rpc=False)
+    for _ in range(3):
+        assert rc.get_file_content("/gpu/fz") == data
+    assert rc.read_file_range("/gpu/fz", 1_048_577, 5) == data[1_048_577:1_048_582]
+    assert stats(gpu_cluster)["fused_reads"] - f1 >= 3
+    rc.close()
     c.close()
 
 
