@@ -230,6 +230,7 @@ int64_t FastClient::acquire(size_t n) {
 }
 
 void FastClient::release(int64_t slot) {
+  slot -= slot % static_cast<int64_t>(slot_bytes_);  // a range read hands out slot + shift
   {
     std::lock_guard<std::mutex> g(slot_mu_);
     free_slots_.push_back(slot);
@@ -467,7 +468,10 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
     offset = 0;
   }
   const uint64_t want = length > 0 ? length : m.size;
-  if (want > slot_bytes_) return NotHandled;
+  // a range lands at slot + offset % 16, so the chunkserver's fused verify+copy kernel can
+  // store it with aligned 16 B writes (whole blocks start at offset 0 anyway)
+  const uint64_t shift = length > 0 ? offset % 16 : 0;
+  if (want + shift > slot_bytes_) return NotHandled;
   const pb::BlockInfo& b = m.blocks[0];
   bool local = false;
   for (auto& l : b.locations) local |= strip_scheme(l) == local_cs_;
@@ -477,8 +481,8 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
   std::string body;
   put<uint64_t>(body, offset);
   put<uint64_t>(body, length);  // 0 = the whole block
-  put<uint64_t>(body, static_cast<uint64_t>(s));
-  put<uint64_t>(body, slot_bytes_);
+  put<uint64_t>(body, static_cast<uint64_t>(s) + shift);
+  put<uint64_t>(body, slot_bytes_ - shift);
   put_str(body, b.block_id);
   put_str(body, arena_path_);
   put_str(body, rid);
@@ -490,7 +494,7 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
     return NotHandled;  // corrupt / missing here: the Python path recovers from a replica
   }
   t->read = since(clk);
-  *slot = s;
+  *slot = s + static_cast<int64_t>(shift);
   *n = got;
   reads_++;
   return Ok;

@@ -55,13 +55,12 @@ def test_gpu_fused_reads_local_and_remote(gpu_cluster):
     c.create_file_from_buffer(data, "/gpu/fz")
     f0 = stats(gpu_cluster)["fused_reads"]
     assert c.get_file_content("/gpu/fz") == data
+    # ranges land at slot + offset % 16 (client_fast.cpp), so unaligned ones are fused too
     assert c.read_file_range("/gpu/fz", 4096 + 48, 100_000) == data[4144:104_144]
-    f1 = stats(gpu_cluster)["fused_reads"]
-    assert f1 - f0 >= 2
-    # a range the slot cannot hold 16 B-congruent (the fast path lands ranges at the slot
-    # start) takes the verify kernel + DMA path, with the same bytes
     assert c.read_file_range("/gpu/fz", 777, 100_000) == data[777:100_777]
+    assert c.read_file_range("/gpu/fz", (2 << 20) + 300, 1000) == data[(2 << 20) + 300:]
     f1 = stats(gpu_cluster)["fused_reads"]
+    assert f1 - f0 >= 4
     rc = gpu_cluster.client(local_chunkserver=None, local_rpc=False)
     for _ in range(3):
         assert rc.get_file_content("/gpu/fz") == data
