@@ -4,6 +4,7 @@ the S3 gateway. CPU-only twins of these paths live in test_cluster.py / test_s3_
 """
 import json
 import os
+import time
 import urllib.request
 
 import pytest
@@ -53,7 +54,17 @@ def test_gpu_fused_reads_local_and_remote(gpu_cluster):
     data = os.urandom((2 << 20) + 333)
     c = gpu_cluster.client(local_chunkserver=gpu_cluster.cs_addrs[0])
     c.create_file_from_buffer(data, "/gpu/fz")
+    # the fast path pins a client's shm arena on a background thread (no lock held on the
+    # data path); until that lands, reads take the staged verify + DMA path
+    f_init = stats(gpu_cluster)["fused_reads"]
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        assert c.get_file_content("/gpu/fz") == data
+        if stats(gpu_cluster)["fused_reads"] > f_init:
+            break  # this client's arena is pinned: every read from now on is fused
+        time.sleep(0.05)
     f0 = stats(gpu_cluster)["fused_reads"]
+    assert f0 > f_init
     assert c.get_file_content("/gpu/fz") == data
     # ranges land at slot + offset % 16 (client_fast.cpp), so unaligned ones are fused too
     assert c.read_file_range("/gpu/fz", 4096 + 48, 100_000) == data[4144:104_144]
