@@ -316,6 +316,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["promotions"] = t.promotions;
         d["mirror_hits"] = t.mirror_hits;
         d["mirror_bytes"] = t.mirror_bytes;
+        d["io_threads_spawned"] = t.io_threads_spawned;
         d["crc_mismatches"] = t.crc_mismatches;
         d["gpu_kernel_launches"] = t.gpu_kernel_launches;
         d["disk_gate_waits"] = t.disk_gate_waits;
@@ -512,6 +513,8 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["open_attempts"] = s.open_attempts;
         d["turn_timeouts"] = s.turn_timeouts;
         d["stale_generation"] = s.stale_generation;
+        d["parked_extents"] = s.parked_extents;
+        d["reaped_extents"] = s.reaped_extents;
         return d;
       })
       .def_property_readonly("bytes_sent", [](ReplicationEngine& e) { return e.stats().bytes_sent; })

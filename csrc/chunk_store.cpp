@@ -30,7 +30,9 @@ static void drop_cached(int fd) {
 #endif
 }
 
-GroupSync::GroupSync(const std::string& dir) { fd_ = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC); }
+GroupSync::GroupSync(const std::string& dir, Mode mode) : mode_(mode) {
+  fd_ = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
+}
 
 GroupSync::~GroupSync() {
   if (fd_ >= 0) ::close(fd_);
@@ -49,7 +51,7 @@ bool GroupSync::sync() {
     running_ = true;
     uint64_t covers = issued_;
     lk.unlock();
-    bool ok = ::syncfs(fd_) == 0;
+    bool ok = (mode_ == Mode::FileSystem ? ::syncfs(fd_) : ::fsync(fd_)) == 0;
     lk.lock();
     running_ = false;
     if (!ok) failed_.emplace_back(done_ + 1, covers);
@@ -139,6 +141,13 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
   // than our two files, so the per-file fdatasync pair stays the default.
   const char* gs = std::getenv("DFS_GROUP_SYNC");
   if (cfg_.sync_writes && gs && std::string(gs) == "1") gsync_ = std::make_unique<GroupSync>(cfg_.storage_dir);
+  if (cfg_.sync_writes) {
+    // renames into place are durable only once the directory is flushed (the reference
+    // writes final names directly and sync_all()s the file, chunkserver.rs:192-209)
+    dsync_hot_ = std::make_unique<GroupSync>(cfg_.storage_dir, GroupSync::Mode::Directory);
+    if (!cfg_.cold_dir.empty())
+      dsync_cold_ = std::make_unique<GroupSync>(cfg_.cold_dir, GroupSync::Mode::Directory);
+  }
   if (cfg_.sync_writes)
     gate_ = std::make_unique<DiskGate>(cfg_.storage_dir,
                                        cfg_.disk_inflight < 0 ? disk_inflight_default() : cfg_.disk_inflight);
@@ -523,9 +532,14 @@ bool ChunkStore::make_durable(int data_fd, int meta_fd, bool cold) {
   if (gsync_ && !cold) return gsync_->sync();
   // The two flushes are independent: issue them concurrently (NVMe queues them side by
   // side) instead of paying two device round trips back to back.
-  auto meta = std::async(std::launch::async, [meta_fd] { return ::fdatasync(meta_fd) == 0; });
+  auto meta = io_.submit([meta_fd] { return ::fdatasync(meta_fd) == 0; });
   bool ok = ::fdatasync(data_fd) == 0;
   return meta.get() && ok;
+}
+
+bool ChunkStore::sync_dir(bool cold) {
+  GroupSync* g = cold ? dsync_cold_.get() : dsync_hot_.get();
+  return g == nullptr || g->sync();
 }
 
 bool ChunkStore::write_file_durable(const std::string& path, const uint8_t* p, uint64_t n, std::string* err) {
@@ -633,7 +647,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   const std::string tmp_sfx = "." + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
   const std::string dp_tmp = data_path(id, false) + tmp_sfx, mp_tmp = meta_path(id, false) + tmp_sfx;
   if (sync_now && !gsync_) {
-    data_file = std::async(std::launch::async, [this, dp_tmp, data, n, &data_err] {
+    data_file = io_.submit([this, dp_tmp, data, n, &data_err] {
       DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
       return write_file_durable(dp_tmp, data, n, &data_err);
     });
@@ -701,6 +715,9 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
           ::rename(mp_tmp.c_str(), meta_path(id, false).c_str()) != 0) {
         mok = false;
         err = errno_str("rename " + dp_tmp);
+      } else if (!sync_dir(false)) {  // the ack promises the names, not just the bytes
+        mok = false;
+        err = errno_str("fsync " + cfg_.storage_dir);
       }
     }
     if (!mok || !dok) {
@@ -1449,6 +1466,7 @@ void ChunkStore::spill_worker() {
     if (ok && (::rename(mp_tmp.c_str(), meta_path(id, false).c_str()) != 0 ||
                ::rename(dp_tmp.c_str(), data_path(id, false).c_str()) != 0))
       ok = false;
+    if (ok) ok = sync_dir(false);  // the block stays dirty (and retried) until its names are durable
     if (!ok) {
       ::unlink(dp_tmp.c_str());
       ::unlink(mp_tmp.c_str());
@@ -1548,6 +1566,10 @@ bool ChunkStore::move_to_cold(const std::string& id) {
   }
   if (::rename(data_path(id, false).c_str(), data_path(id, true).c_str()) != 0) return false;
   if (::rename(meta_path(id, false).c_str(), meta_path(id, true).c_str()) != 0) return false;
+  // both directory entries changed: flush the new one before the old (a crash in between
+  // leaves the block reachable under at least one tier)
+  (void)sync_dir(true);
+  (void)sync_dir(false);
   it->second.cold = true;
   // cold blocks leave the fast tier
   if (it->second.pins == 0) {
@@ -1743,6 +1765,7 @@ StoreStats ChunkStore::stats() {
   s.staged_dma = staged_dma_.load();
   s.mirror_hits = mirror_hits_;
   s.mirror_bytes = mirror_bytes_;
+  s.io_threads_spawned = io_.spawned();
   {
     std::lock_guard<std::mutex> rg(reg_mu_);
     for (auto& r : reg_) s.host_registered_bytes += r.second;

@@ -32,6 +32,7 @@
 #include "disk_gate.h"
 #include "extent_alloc.h"
 #include "gpu_kernels.h"
+#include "io_pool.h"
 
 namespace dfs {
 
@@ -87,18 +88,24 @@ struct StoreStats {
   uint64_t host_registered_bytes = 0;
   uint64_t mirror_hits = 0;      // small-block reads served from the verified host mirror
   uint64_t mirror_bytes = 0;
+  uint64_t io_threads_spawned = 0;  // helper threads ever started (steady state: none per write)
 };
 
-// Group commit of data files: callers that finished writing share one syncfs() round.
+// Group commit: callers that finished writing share one flush round — syncfs() of the
+// filesystem (data files, opt-in DFS_GROUP_SYNC) or fsync() of the directory itself (makes
+// the renames of every block that finished before the round durable, one journal commit
+// for a whole burst of writers instead of one per block).
 class GroupSync {
  public:
-  explicit GroupSync(const std::string& dir);
+  enum class Mode { FileSystem, Directory };
+  explicit GroupSync(const std::string& dir, Mode mode = Mode::FileSystem);
   ~GroupSync();
   bool sync();  // returns once a flush that started after this call has completed
   uint64_t rounds() const { return rounds_; }
 
  private:
   int fd_ = -1;
+  Mode mode_;
   std::mutex mu_;
   std::condition_variable cv_;
   uint64_t issued_ = 0, done_ = 0, rounds_ = 0;
@@ -293,6 +300,9 @@ class ChunkStore {
   std::atomic<uint64_t> fused_reads_{0};  // K3 fused verify+copy reads
   std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};  // unique temporary file names for in-flight writes
   std::unique_ptr<GroupSync> gsync_;
+  IoPool io_{8};  // data-file writes and .meta flushes beside the GPU staging (no per-write threads)
+  std::unique_ptr<GroupSync> dsync_hot_, dsync_cold_;  // directory fsync after renames
+  bool sync_dir(bool cold);
   std::unique_ptr<DiskGate> gate_;
 };
 

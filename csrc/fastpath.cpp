@@ -561,7 +561,7 @@ bool FastPathServer::persist_and_replicate(const std::string& id, const uint8_t*
   // no shared-memory source: replicas go over the P2P transport (the block is staged in HBM)
   // or, without a pair, fail and are not counted — as a downstream failure in the reference
   const std::string rid = t_request_id;
-  auto fut = std::async(std::launch::async, [&] {
+  auto fut = pool_.submit([&] {
     RequestScope rs(rid);
     replicate(id, crc, term, next, ShmSrc{}, host, n, downstream);
   });
@@ -578,7 +578,7 @@ void FastPathServer::replicate(const std::string& id, uint32_t crc, uint64_t ter
   std::vector<std::future<int>> futs;
   const std::string rid = t_request_id;
   for (size_t i = 1; i < next.size(); ++i)
-    futs.push_back(std::async(std::launch::async, [&, i] {
+    futs.push_back(pool_.submit([&, i] {
       RequestScope rs(rid);
       return replicate_one(next[i], id, crc, term, src, host, n);
     }));
@@ -606,7 +606,7 @@ void FastPathServer::serve(int fd) {
     int down = 0;
     std::string perr;
     const std::string rid = t_request_id;
-    auto fut = std::async(std::launch::async, [&] {
+    auto fut = pool_.submit([&] {
       RequestScope rs(rid);
       replicate(id, crc, term, next, src, host, len, &down);
     });
@@ -671,7 +671,7 @@ void FastPathServer::serve(int fd) {
       RequestScope rs(rid);
       note_rid(rid);
       if (!rd.ok || id.empty() || repl_ == nullptr || size > kMaxTransfer) {
-        if (repl_ && rd.ok && src >= 0) repl_->fail_pair(src, "malformed descriptor");
+        if (repl_ && rd.ok && src >= 0) repl_->fail_pair_gen(src, gen, "malformed descriptor");
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, repl_ ? "malformed replicate request" : "replication disabled");
       } else {
         // The receive is posted even for a fenced request — refusing it would leave the
@@ -732,14 +732,19 @@ void FastPathServer::serve(int fd) {
       const uint64_t stride = (len + 15) / 16 * 16;
       std::string err;
       uint8_t* base = nullptr;
+      // Each region is bounded on its own before any pointer is formed: offsets near 2^64
+      // must not wrap into a small span (len <= kMaxTransfer and k, rows <= kMaxShards keep
+      // stride * k far below 2^62, so only the offsets need checking).
+      const uint64_t in_len = stride * k, out_len = stride * rows;
+      const bool regions_ok = in_off <= (1ull << 62) && out_off <= (1ull << 62);
       if (!rd.ok || k == 0 || rows == 0 || k > kMaxShards || rows > kMaxShards || mat.size() != size_t(k) * rows ||
-          len > kMaxTransfer) {
+          len > kMaxTransfer || !regions_ok) {
         sent = send_response(fd, FpStatus::BadRequest, 0, 0, "malformed ec request");
       } else if (!store_->gpu()) {
         sent = send_response(fd, FpStatus::Unsupported, 0, 0, "no GPU on this chunkserver");
-      } else if ((base = map_shm(path, std::min(in_off, out_off),
-                                 std::max(in_off + stride * k, out_off + stride * rows) - std::min(in_off, out_off),
-                                 &err)) == nullptr) {
+      } else if ((base = map_shm(path, in_off, in_len, &err)) == nullptr ||
+                 map_shm(path, out_off, out_len, &err) != base) {
+        if (base != nullptr && err.empty()) err = "ec regions outside the arena";
         sent = send_response(fd, FpStatus::Unsupported, 0, 0, "short-circuit unavailable: " + err);
       } else {
         std::vector<std::vector<uint8_t>> M(rows, std::vector<uint8_t>(k));

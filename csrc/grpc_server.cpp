@@ -76,10 +76,15 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     size_t off = 0;  // bytes of prefix + body already handed to nghttp2
     std::string status_str = "0";
     bool dispatched = false;
+    bool too_big = false;   // over kMaxMessage (or the connection's budget): refused
+    uint32_t declared = 0;  // message length from the gRPC prefix
   };
+  static constexpr uint32_t kMaxMessage = 100u << 20;       // MAX_GRPC_MESSAGE_SIZE of the reference
+  static constexpr size_t kMaxConnBuffered = 1ull << 30;    // request bytes held per connection
   GrpcServer* srv = nullptr;
   int fd = -1;
   int efd = -1;
+  size_t buffered = 0;  // request bytes buffered across this connection's streams
   nghttp2_session* session = nullptr;
   std::map<int32_t, Stream> streams;
   std::mutex mu;
@@ -165,8 +170,11 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     if (it == streams.end() || it->second.dispatched) return;
     Stream& st = it->second;
     st.dispatched = true;
+    buffered -= std::min(buffered, st.body.size());
     GrpcReply bad;
-    if (st.head_len < 5) {
+    if (st.too_big) {
+      bad = {8, "message larger than the " + std::to_string(kMaxMessage) + " byte limit"};
+    } else if (st.head_len < 5) {
       bad = {13, "missing gRPC message"};
     } else if (st.head[0] != 0) {
       bad = {12, "compressed messages are not supported"};
@@ -220,6 +228,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     auto it = c->streams.find(sid);
     if (it != c->streams.end()) {
       Stream& st = it->second;
+      if (st.too_big) return 0;  // already refused: drop the rest of the upload
       if (st.head_len < 5) {
         const size_t k = std::min<size_t>(5 - st.head_len, len);
         std::memcpy(st.head + st.head_len, data, k);
@@ -227,15 +236,33 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
         data += k;
         len -= k;
         if (st.head_len == 5) {
-          // size the buffer once from the gRPC length prefix (1-100 MiB blocks)
           uint32_t n;
           std::memcpy(&n, st.head + 1, 4);
-          st.body.reserve(std::min<uint32_t>(ntohl(n), 1u << 30));
+          n = ntohl(n);
+          // the reference's tonic servers cap messages at 100 MiB (RESOURCE_EXHAUSTED); the
+          // buffer is sized from the prefix only once the prefix passed that check, and the
+          // connection's buffered bytes stay under kMaxConnBuffered whatever the stream count
+          if (n > kMaxMessage || c->buffered + n > kMaxConnBuffered) {
+            c->refuse(st);
+            return 0;
+          }
+          st.body.reserve(n);
+          st.declared = n;
         }
       }
+      if (len && (st.head_len < 5 || st.body.size() + len > st.declared)) {
+        c->refuse(st);  // more bytes than the prefix announced
+        return 0;
+      }
       st.body.append(reinterpret_cast<const char*>(data), len);
+      c->buffered += len;
     }
     return 0;
+  }
+  void refuse(Stream& st) {
+    st.too_big = true;
+    buffered -= std::min(buffered, st.body.size());
+    st.body = std::string();
   }
   static int on_frame(nghttp2_session*, const nghttp2_frame* f, void* user) {
     if ((f->hd.type == NGHTTP2_DATA || f->hd.type == NGHTTP2_HEADERS) && (f->hd.flags & NGHTTP2_FLAG_END_STREAM))
@@ -243,7 +270,11 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     return 0;
   }
   static int on_close(nghttp2_session*, int32_t sid, uint32_t, void* user) {
-    static_cast<Conn*>(user)->streams.erase(sid);
+    auto* c = static_cast<Conn*>(user);
+    auto it = c->streams.find(sid);
+    if (it == c->streams.end()) return 0;
+    if (!it->second.dispatched) c->buffered -= std::min(c->buffered, it->second.body.size());
+    c->streams.erase(it);
     return 0;
   }
 };

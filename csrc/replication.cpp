@@ -134,8 +134,52 @@ void ReplicationEngine::stop() {
   std::unique_lock<std::mutex> lk(threads_mu_);
   threads_cv_.wait(lk, [this] { return live_threads_ == 0; });
   lk.unlock();
-  for (int p = 0; p < world_; ++p)
-    if (p != rank_) t_->close(p);
+  for (int p = 0; p < world_; ++p) {
+    if (p == rank_) continue;
+    t_->close(p);
+    // shutting down: nothing of ours will receive again, the store outlives the engine
+    std::vector<std::pair<uint64_t, DevExtent>> left;
+    {
+      std::lock_guard<std::mutex> g(peer(p).mu);
+      left.swap(peer(p).parked);
+    }
+    for (auto& pe : left) store_->release(pe.second);
+  }
+}
+
+void ReplicationEngine::park(int p, uint64_t gen, const DevExtent& e) {
+  Peer& P = peer(p);
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.parked.emplace_back(gen, e);
+  }
+  {
+    std::lock_guard<std::mutex> lk(st_mu_);
+    st_.parked_extents++;
+  }
+  reap(p);  // the pair may already be up again on a newer generation
+}
+
+void ReplicationEngine::reap(int p) {
+  Peer& P = peer(p);
+  std::vector<DevExtent> free_now;
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (P.state != State::Up) return;
+    for (size_t i = 0; i < P.parked.size();) {
+      if (P.parked[i].first < P.gen) {
+        free_now.push_back(P.parked[i].second);
+        P.parked[i] = P.parked.back();
+        P.parked.pop_back();
+      } else {
+        ++i;
+      }
+    }
+  }
+  if (free_now.empty()) return;
+  for (auto& e : free_now) store_->release(e);
+  std::lock_guard<std::mutex> lk(st_mu_);
+  st_.reaped_extents += free_now.size();
 }
 
 int ReplicationEngine::wait_ready(int timeout_ms, int give_up_after) {
@@ -244,8 +288,11 @@ void ReplicationEngine::opener_loop(int p) {
       P.cv.notify_all();
     }
     if (ok) {
-      std::lock_guard<std::mutex> lk(st_mu_);
-      st_.pair_opens++;
+      {
+        std::lock_guard<std::mutex> lk(st_mu_);
+        st_.pair_opens++;
+      }
+      reap(p);
       return;
     }
     t_->close(p);
@@ -315,7 +362,7 @@ std::string ReplicationEngine::handle_control(const std::string& req) {
     std::string e;
     bool ok = t_->open(from, g, mine, tok, opt_.open_timeout_ms, &e);
     Peer& Q = peer(from);
-    std::lock_guard<std::mutex> lk(Q.mu);
+    std::unique_lock<std::mutex> lk(Q.mu);
     if (Q.gen == g) {
       Q.state = ok ? State::Up : State::Broken;
       Q.last_error = e;
@@ -326,6 +373,8 @@ std::string ReplicationEngine::handle_control(const std::string& req) {
       std::lock_guard<std::mutex> sg(st_mu_);
       st_.pair_opens++;
     }
+    lk.unlock();
+    if (ok) reap(from);
   });
   std::string r = reply(kOk, g, mine);
   put<uint64_t>(r, incarnation_);
@@ -334,12 +383,23 @@ std::string ReplicationEngine::handle_control(const std::string& req) {
 
 void ReplicationEngine::fail_pair(int p, const std::string& why) {
   if (p < 0 || p >= world_ || p == rank_) return;
+  uint64_t g;
+  {
+    std::lock_guard<std::mutex> lk(peer(p).mu);
+    g = peer(p).gen;
+  }
+  fail_pair_gen(p, g, why);
+}
+
+void ReplicationEngine::fail_pair_gen(int p, uint64_t gen, const std::string& why) {
+  if (p < 0 || p >= world_ || p == rank_) return;
   Peer& P = peer(p);
   uint64_t g;
   bool start = false;
   {
     std::lock_guard<std::mutex> lk(P.mu);
-    if (P.state != State::Up) return;  // already failed / being rebuilt
+    // already failed / being rebuilt, or the failure belongs to an older generation
+    if (P.state != State::Up || P.gen != gen) return;
     P.state = State::Broken;
     P.last_error = why;
     g = P.gen;
@@ -407,7 +467,7 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
   }
   for (auto& op : t->ops) t_->release(&op);
   t->ops.clear();
-  if (failed) fail_pair(p, "post_send failed: " + *err);
+  if (failed) fail_pair_gen(p, t->gen, "post_send failed: " + *err);
   if (t->pinned) store_->unpin(id);
   t->pinned = false;
   return false;
@@ -446,7 +506,7 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
     }
     if (!ok) break;
   }
-  if (!ok) fail_pair(t->peer, *err);  // abort before unpinning: no DMA reads a freed extent
+  if (!ok) fail_pair_gen(t->peer, t->gen, *err);  // abort before unpinning: no DMA reads a freed extent
   for (auto& op : t->ops) t_->release(&op);
   t->ops.clear();
   if (t->pinned) store_->unpin(t->id);
@@ -460,7 +520,7 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
 }
 
 void ReplicationEngine::cancel_send(ReplTicket* t, const std::string& why) {
-  fail_pair(t->peer, why);
+  fail_pair_gen(t->peer, t->gen, why);
   for (auto& op : t->ops) t_->release(&op);
   t->ops.clear();
   if (t->pinned) store_->unpin(t->id);
@@ -477,7 +537,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
   }
   if (size && (slice == 0 || slice % kSliceBytes != 0)) {
     res.error = "bad slice size";
-    fail_pair(src, res.error);
+    fail_pair_gen(src, gen, res.error);
     return res;
   }
   const bool dev = t_->device_buffers();
@@ -489,7 +549,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
     ext = store_->reserve(size);
     if (ext.off < 0) {
       res.error = "HBM arena full";
-      fail_pair(src, res.error);  // the matching send can never be consumed now
+      fail_pair_gen(src, gen, res.error);  // the matching send can never be consumed now
       return res;
     }
   } else {
@@ -540,9 +600,10 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
     if (!why.empty()) {
       lk.unlock();
       for (auto& op : ops) t_->release(&op);
-      if (fail) fail_pair(src, why);
-      // an extent that a posted receive may still write into is leaked, not reused
+      if (fail) fail_pair_gen(src, gen, why);
+      // an extent that a posted receive may still write into waits for the pair's rebuild
       if (dev && ops.empty()) store_->release(ext);
+      else if (dev) park(src, gen, ext);
       res.error = why;
       return res;
     }
@@ -580,7 +641,8 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
   for (auto& op : ops) t_->release(&op);
   if (!why.empty()) {
     if (dev) store_->recv_abandon(&rv);
-    fail_pair(src, why);
+    fail_pair_gen(src, gen, why);
+    if (dev) park(src, gen, ext);
     res.error = why;
     return res;
   }

@@ -68,6 +68,7 @@ struct ReplTicket {
 struct ReplStats {
   uint64_t bytes_sent = 0, bytes_recv = 0, blocks_sent = 0, blocks_recv = 0;
   uint64_t pair_failures = 0, pair_opens = 0, open_attempts = 0, turn_timeouts = 0, stale_generation = 0;
+  uint64_t parked_extents = 0, reaped_extents = 0;  // failed-receive extents held / freed after close
 };
 
 class ReplicationEngine {
@@ -109,7 +110,11 @@ class ReplicationEngine {
 
   // Control plane (fast-path op 5). Returns the reply payload.
   std::string handle_control(const std::string& req);
+  // Fails the pair's CURRENT generation (operator / test hook).
   void fail_pair(int peer, const std::string& why);
+  // Fails generation `gen` only: a waiter left over from an aborted generation must not
+  // tear down the pair that was rebuilt meanwhile (it just fails its own op).
+  void fail_pair_gen(int peer, uint64_t gen, const std::string& why);
 
   P2PTransport* transport() { return t_.get(); }
   ReplStats stats();
@@ -128,8 +133,19 @@ class ReplicationEngine {
     uint64_t peer_inc = 0;  // initiator side: the peer process instance the pair was opened with
     int failed_opens = 0;   // bring-up attempts of this pair that failed (both sides count)
     std::string last_error;
+    // Receive extents of failed transfers: a DMA of that generation may still land in them,
+    // so they are freed only after the next transport close() of this pair has returned
+    // (close() aborts the channels and, for device transports, drains inbound copies).
+    std::vector<std::pair<uint64_t, DevExtent>> parked;  // (generation, extent)
   };
   Peer& peer(int p);
+  // Park the receive extent of a failed generation-`gen` transfer. It is freed once a LATER
+  // generation of the pair is up: both ranks close() their channels before every open, and
+  // the open completes only when both did, so no copy of generation `gen` can land any more
+  // (RCCL: both communicators aborted; hipipc: both copy streams drained).
+  void park(int p, uint64_t gen, const DevExtent& e);
+  // Frees the parked extents of generations older than the pair's current, Up generation.
+  void reap(int p);
   void opener_loop(int p);
   void request_reopen(int p, uint64_t gen, bool fresh);
   void spawn(std::function<void()> fn);

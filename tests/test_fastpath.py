@@ -189,6 +189,24 @@ def test_wrapped_offsets_are_rejected(server):
         arena.close()
 
 
+def test_ec_wrapped_offsets_are_rejected(server):
+    """op 6 (GPU erasure coding) bounded only the union of its two
+    regions; in_off = 2^64-16 with out_off = 0 passed and pointed before the mapping. Each
+    region is now checked on its own, and a wrapping offset is refused before the GPU is
+    consulted (so this runs on a host-mode store too)."""
+    _store, srv = server
+    arena = ShmArena(size=4 << 20, slot=4 << 20)
+    cli = fp.FastPathClient(srv.name)
+    try:
+        mat = [[1, 0], [0, 1]]
+        for in_off, out_off in (((1 << 64) - 16, 0), (0, (1 << 64) - 16), (1 << 63, 0)):
+            st = cli.ec_matmul(mat, 2, 16, arena.path, in_off, out_off)
+            assert st == fp.BAD_REQUEST, (in_off, out_off, st, cli.last_ec_message)
+    finally:
+        cli.close()
+        arena.close()
+
+
 def test_connection_threads_are_reaped(server):
     """one thread per connection used to stay unjoined until stop()."""
     import threading

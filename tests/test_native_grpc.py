@@ -117,6 +117,28 @@ def test_large_messages_and_concurrent_streams(server):
     assert srv.stats()["native_grpc_calls"] >= 130
 
 
+def test_oversized_message_is_refused(server):
+    """the native server buffered any length prefix (up to 1 GiB each, 1024
+    streams). Like the reference's tonic servers (100 MiB MAX_GRPC_MESSAGE_SIZE) it now answers
+    RESOURCE_EXHAUSTED without holding the body, and keeps serving the connection."""
+    store, fp, srv, pool, addr, calls = server
+    ch = grpc.insecure_channel(addr.split("//")[1], options=[("grpc.max_send_message_length", 256 << 20),
+                                                             ("grpc.max_receive_message_length", 256 << 20)])
+    try:
+        stub = ch.unary_unary("/dfs.ChunkServerService/WriteBlock",
+                              request_serializer=pb.WriteBlockRequest.SerializeToString,
+                              response_deserializer=pb.WriteBlockResponse.FromString)
+        with pytest.raises(grpc.RpcError) as ei:
+            stub(pb.WriteBlockRequest(block_id="huge", data=bytes(101 << 20)), timeout=60)
+        assert ei.value.code() == grpc.StatusCode.RESOURCE_EXHAUSTED
+        assert not store.exists("huge")
+        ok = stub(pb.WriteBlockRequest(block_id="small", data=b"abc", expected_checksum_crc32c=zlib.crc32(b"abc")),
+                  timeout=60)
+        assert ok.success
+    finally:
+        ch.close()
+
+
 @pytest.mark.slow
 def test_master_service_on_native_grpc():
     """MasterService served by the native HTTP/2 server (NativeGrpcMasterServer): a client
