@@ -47,8 +47,10 @@ def parse():
     p.add_argument("--concurrency", type=int, default=10)
     p.add_argument("--durability", choices=["nvme-sync", "hbm-ack"], default="nvme-sync")
     p.add_argument("--hbm-capacity", default="32G")
-    p.add_argument("--transport", choices=["rccl", "grpc", "socket"], default="rccl",
-                   help="replica payload path between ranks (socket: host-memory P2P, CPU rehearsal)")
+    p.add_argument("--transport", choices=["hipipc", "hipipc-spin", "rccl", "grpc", "socket"], default="hipipc",
+                   help="replica payload path between ranks: hipipc (HBM->HBM one-sided copies over xGMI, also "
+                        "between ranks sharing one GPU), hipipc-spin (RCCL-like spinning p2p kernels), rccl, "
+                        "grpc (reference), socket (host-memory P2P, CPU rehearsal)")
     p.add_argument("--shards", choices=["per-gpu", "one"], default="per-gpu",
                    help="metadata shards: one per GPU rank (default) or a single master")
     p.add_argument("--cpu", action="store_true", help="CPU chunk store (plumbing config 1)")
@@ -254,12 +256,14 @@ def main():
                 "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
                 "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
                 "--heartbeat-interval", "0.5", "--scrub-interval", "3600", "--rccl-timeout-ms", "90000"]
-        if n > 1 and a.transport == "socket":
+        if n > 1 and (a.transport == "socket" or (not a.cpu and a.transport in ("hipipc", "hipipc-spin"))):
+            # hipipc works between processes that share a GPU too: a 1-GPU N-rank rehearsal
+            # forwards replicas HBM -> HBM through the same code as the 8-GPU node
             args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
-                     str(base_p / "rccl_rdv"), "--replication-transport", "socket"]
+                     str(base_p / "rccl_rdv"), "--replication-transport", a.transport]
         elif n > 1 and not a.cpu and a.transport == "rccl" and (not shared_gpu or a.rehearse_rccl):
             args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
-                     str(base_p / "rccl_rdv")]
+                     str(base_p / "rccl_rdv"), "--replication-transport", "rccl"]
         else:
             args += ["--replication-transport", "grpc"]
         cs_env = dict(env, DFS_READY_FILE=ready, SHARD_CONFIG=str(shard_file))

@@ -3,6 +3,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "chunk_store.h"
@@ -423,6 +424,25 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def_property_readonly("size", [](PyTicket& k) { return k.t.size; })
       .def_property_readonly("slice", [](PyTicket& k) { return k.t.slice; });
 
+  m.def("rccl_loopback_probe", [](int device, uint64_t bytes, uint64_t abort_bytes, int timeout_ms) {
+    RcclProbe p;
+    {
+      py::gil_scoped_release r;
+      p = rccl_loopback_probe(device, bytes, abort_bytes, timeout_ms);
+    }
+    py::dict d;
+    d["ok"] = p.ok;
+    d["bytes_ok"] = p.bytes_ok;
+    d["drained_after_abort"] = p.drained_after_abort;
+    d["reinit_ok"] = p.reinit_ok;
+    d["version"] = p.version;
+    d["xfer_ms"] = p.xfer_ms;
+    d["abort_ms"] = p.abort_ms;
+    d["init_ms"] = p.init_ms;
+    d["error"] = p.error;
+    return d;
+  }, py::arg("device"), py::arg("bytes"), py::arg("abort_bytes") = 0, py::arg("timeout_ms") = 20000);
+
   py::class_<ReplicationEngine>(m, "ReplicationEngine")
       .def(py::init([](ChunkStore* store, const std::string& transport, int rank, int world, const std::string& ns,
                        int open_timeout_ms, int turn_timeout_ms, int xfer_timeout_ms) {
@@ -431,6 +451,12 @@ PYBIND11_MODULE(_dfs_native, m) {
              if (transport == "rccl") t = make_rccl_transport(store->config().device, rank, &err);
              else if (transport == "socket") t = make_socket_transport(rank, ns);
              else if (transport == "hiploop" && store->gpu()) t = make_hiploop_transport(store->config().device, rank, ns);
+             else if (transport == "hipipc" || transport == "hipipc-spin") {
+               const char* sp = std::getenv("DFS_IPC_SPIN");
+               bool spin = transport == "hipipc-spin" || (sp && std::string(sp) == "1");
+               t = make_ipc_transport(store->config().device, rank, ns, store->arena_base(), store->arena_bytes(), spin,
+                                      &err);
+             }
              else err = "unknown transport " + transport;
              if (!t) throw std::runtime_error(err);
              ReplOptions o;
@@ -451,7 +477,8 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def_property_readonly("transport", &ReplicationEngine::transport_name)
       .def("pair_ok", &ReplicationEngine::pair_ok, py::call_guard<py::gil_scoped_release>())
       .def("generation", &ReplicationEngine::generation, py::call_guard<py::gil_scoped_release>())
-      .def("fail_pair", &ReplicationEngine::fail_pair, py::call_guard<py::gil_scoped_release>())
+      .def("fail_pair", &ReplicationEngine::fail_pair, py::call_guard<py::gil_scoped_release>(), py::arg("peer"),
+           py::arg("why") = "debug")
       .def("slice_for", &ReplicationEngine::slice_for)
       .def("send", [](ReplicationEngine& e, int peer, const std::string& id, py::object data) -> py::tuple {
         auto k = std::make_unique<PyTicket>();

@@ -130,6 +130,10 @@ class ChunkStore {
 
   bool gpu() const { return cfg_.device >= 0; }
   const StoreConfig& config() const { return cfg_; }
+  // The HBM arena (one hipMalloc): device transports export it to same-node peers, which
+  // then DMA replica slices straight into the extents this store reserves.
+  uint8_t* arena_base() const { return arena_; }
+  uint64_t arena_bytes() const { return st_.hbm_capacity; }
 
   WriteResult write(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
   // Two-phase write used by pipelined chain replication: stage() lands the block in HBM

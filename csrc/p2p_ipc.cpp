@@ -1,0 +1,635 @@
+// HIP-IPC implementation of P2PTransport ("hipipc"): the device transport between the
+// ChunkServer PROCESSES of one node (contract in p2p_transport.h).
+//
+// Why not RCCL p2p for this traffic. RCCL's ncclSend/ncclRecv run as kernels that wait on
+// the device for their peer. The replication engine keeps many blocks in flight in both
+// directions of every pair, on 2*(N-1) channel streams plus the store's lanes, and HIP
+// multiplexes those streams onto GPU_MAX_HW_QUEUES (4) hardware queues in order. A receive
+// kernel parked at the head of a queue then holds everything queued behind it — including
+// the send its own peer is waiting for — and with crossing traffic those waits can close a
+// cycle across processes. The channel-level proof in replication.h cannot see that coupling.
+//
+// This transport keeps every wait on the host, so no kernel ever waits for a peer:
+//  * Each rank exports its HBM arena (one hipMalloc) with hipIpcGetMemHandle; the peer maps
+//    it once per pair generation (xGMI peer mapping between GPUs, plain HBM when the ranks
+//    share one GPU).
+//  * Each directed channel has a ring in /dev/shm created by the RECEIVER: post_recv writes
+//    (offset in its arena, length) into slot k and bumps `posted` — the credit.
+//  * The SENDER's channel worker matches its k-th posted send with slot k, checks the length
+//    (RCCL fails a mismatched pair, so do we), and queues one copy-engine hipMemcpyAsync of
+//    the slice straight into the receiver's extent on the channel stream. When the copy's
+//    event completes it publishes `landed` = k + 1. A copy never waits for anything, so a
+//    hardware queue can hold it only for the copy's own duration.
+//  * The receiver's op k completes when `landed` > k (the engine then checksums the slice on
+//    a store lane while later slices are still in flight, exactly as with RCCL).
+//  * close() raises `abort` on both rings, stops the worker and drains the channel stream
+//    (copies always finish), so when it returns no copy of that generation can still land.
+//
+// Spin mode (make_ipc_transport(..., spin=true); DFS_IPC_SPIN=1) is the RCCL emulation used
+// to test the engine against the hazard above: post_send launches a kernel that parks on the
+// send stream until the credit appears and then copies with the whole grid; post_recv
+// launches a kernel that parks on the receive stream until the bytes landed
+// (p2p_kernels.hip). Every such wait is bounded by the device wall clock (DFS_IPC_SPIN_MS)
+// and by the abort word, so a kernel whose peer never comes still exits.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <climits>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "p2p_kernels.h"
+#include "p2p_transport.h"
+
+namespace dfs {
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+constexpr uint64_t kRingMagic = 0x474e495243504944ull;  // "DIPCRING"
+constexpr char kTokMagic[8] = {'D', 'F', 'S', 'I', 'P', 'C', '1', '\0'};
+constexpr int kMaxRanks = 64;
+constexpr size_t kProbeBytes = 2 * kMaxRanks * 64;  // [0,4096) mailbox per sender; [4096,8192) our patterns
+
+struct TokenWire {
+  char magic[8];
+  int32_t rank, device, pid;
+  uint32_t spin;
+  uint64_t gen;
+  hipIpcMemHandle_t arena;
+  uint64_t arena_bytes;
+  hipIpcMemHandle_t probe;
+  char ring[96];  // shm name of the creator's INBOUND ring (the creator receives on it)
+};
+
+long futex(uint32_t* addr, int op, uint32_t val, const timespec* ts) {
+  return ::syscall(SYS_futex, addr, op, val, ts, nullptr, 0);
+}
+
+template <class T>
+T ld(const T* p) {
+  return __atomic_load_n(p, __ATOMIC_ACQUIRE);
+}
+template <class T>
+void st(T* p, T v) {
+  __atomic_store_n(p, v, __ATOMIC_RELEASE);
+}
+
+void ring_wake(IpcRing* r) {
+  __atomic_fetch_add(&r->doorbell, 1u, __ATOMIC_SEQ_CST);
+  futex(&r->doorbell, FUTEX_WAKE, INT_MAX, nullptr);
+}
+
+// One process's mapping of a channel ring, registered for device access (spin kernels).
+struct RingMap {
+  IpcRing* r = nullptr;
+  IpcRing* dev = nullptr;
+  size_t bytes = 0;
+  std::string name;
+  bool owner = false;
+  ~RingMap() {
+    if (dev) (void)hipHostUnregister(r);
+    if (r) ::munmap(r, bytes);
+    if (owner && !name.empty()) ::shm_unlink(name.c_str());
+  }
+};
+
+std::shared_ptr<RingMap> map_ring(const std::string& name, bool create, uint64_t gen, std::string* err) {
+  const size_t bytes = (sizeof(IpcRing) + 4095) / 4096 * 4096;
+  if (create) ::shm_unlink(name.c_str());
+  int fd = ::shm_open(name.c_str(), create ? (O_RDWR | O_CREAT | O_EXCL) : O_RDWR, 0600);
+  if (fd < 0) {
+    *err = "shm_open " + name + ": " + std::strerror(errno);
+    return nullptr;
+  }
+  if (create && ::ftruncate(fd, static_cast<off_t>(bytes)) != 0) {
+    *err = "ftruncate " + name + ": " + std::strerror(errno);
+    ::close(fd);
+    ::shm_unlink(name.c_str());
+    return nullptr;
+  }
+  struct stat sb {};
+  if (::fstat(fd, &sb) != 0 || static_cast<size_t>(sb.st_size) < bytes) {
+    *err = "ring " + name + " too small";
+    ::close(fd);
+    return nullptr;
+  }
+  void* p = ::mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  ::close(fd);
+  if (p == MAP_FAILED) {
+    *err = std::string("mmap ring: ") + std::strerror(errno);
+    if (create) ::shm_unlink(name.c_str());
+    return nullptr;
+  }
+  auto m = std::make_shared<RingMap>();
+  m->r = static_cast<IpcRing*>(p);
+  m->bytes = bytes;
+  m->name = name;
+  m->owner = create;
+  if (create) {
+    std::memset(p, 0, bytes);
+    m->r->gen = gen;
+    m->r->receiver_pid = ::getpid();
+    st(&m->r->magic, kRingMagic);
+  } else if (ld(&m->r->magic) != kRingMagic || m->r->gen != gen) {
+    *err = "ring " + name + " is not generation " + std::to_string(gen);
+    return nullptr;
+  }
+  void* dev = nullptr;
+  if (hipHostRegister(p, bytes, hipHostRegisterMapped) == hipSuccess &&
+      hipHostGetDevicePointer(&dev, p, 0) == hipSuccess) {
+    m->dev = static_cast<IpcRing*>(dev);
+  } else {
+    (void)hipGetLastError();
+    *err = "hipHostRegister of ring " + name + " failed";
+    return nullptr;
+  }
+  return m;
+}
+
+struct SendItem {
+  const uint8_t* src = nullptr;
+  uint64_t n = 0;
+  uint64_t seq = 0;
+  std::shared_ptr<std::atomic<int>> st;
+  hipEvent_t ev = nullptr;
+};
+
+class IpcTransport final : public P2PTransport {
+ public:
+  IpcTransport(int device, int rank, std::string ns, uint8_t* arena, uint64_t arena_bytes, bool spin)
+      : device_(device), rank_(rank), ns_(std::move(ns)), arena_(arena), arena_bytes_(arena_bytes), spin_(spin) {
+    const char* ms = std::getenv("DFS_IPC_SPIN_MS");
+    spin_ticks_ = wall_ticks_per_ms(device) * static_cast<uint64_t>(ms ? std::max(1, std::atoi(ms)) : 5000);
+  }
+
+  bool init(std::string* err) {
+    if (rank_ < 0 || rank_ >= kMaxRanks) {
+      *err = "hipipc supports ranks 0.." + std::to_string(kMaxRanks - 1);
+      return false;
+    }
+    (void)hipSetDevice(device_);
+    if (hipIpcGetMemHandle(&arena_h_, arena_) != hipSuccess) {
+      *err = std::string("hipIpcGetMemHandle(arena): ") + hipGetErrorString(hipGetLastError());
+      return false;
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&probe_), kProbeBytes) != hipSuccess ||
+        hipMemset(probe_, 0, kProbeBytes) != hipSuccess || hipIpcGetMemHandle(&probe_h_, probe_) != hipSuccess) {
+      *err = "probe buffer / IPC handle failed";
+      return false;
+    }
+    return true;
+  }
+
+  ~IpcTransport() override {
+    std::vector<int> peers;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& kv : links_) peers.push_back(kv.first);
+    }
+    for (int p : peers) close(p);
+    (void)hipSetDevice(device_);
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : links_) {
+      Link& l = *kv.second;
+      for (hipStream_t s : {l.send_stream, l.recv_stream})
+        if (s) (void)hipStreamDestroy(s);
+      if (l.done_ctr) (void)hipFree(l.done_ctr);
+    }
+    for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
+    if (probe_) (void)hipFree(probe_);
+  }
+
+  const char* name() const override { return spin_ ? "hipipc-spin" : "hipipc"; }
+  bool device_buffers() const override { return true; }
+
+  std::string make_token(int peer, uint64_t gen, std::string* err) override {
+    if (peer < 0 || peer >= kMaxRanks) {
+      *err = "peer rank out of range";
+      return {};
+    }
+    const std::string name = "/dfs_ipc_" + ns_ + "_" + std::to_string(rank_) + "_" + std::to_string(peer) + "_" +
+                             std::to_string(gen) + "_" + std::to_string(::getpid());
+    auto ring = map_ring(name, true, gen, err);
+    if (!ring) return {};
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      made_[peer] = {gen, ring};
+    }
+    TokenWire t{};
+    std::memcpy(t.magic, kTokMagic, sizeof t.magic);
+    t.rank = rank_;
+    t.device = device_;
+    t.pid = ::getpid();
+    t.spin = spin_ ? 1 : 0;
+    t.gen = gen;
+    t.arena = arena_h_;
+    t.arena_bytes = arena_bytes_;
+    t.probe = probe_h_;
+    std::snprintf(t.ring, sizeof t.ring, "%s", name.c_str());
+    return std::string(reinterpret_cast<const char*>(&t), sizeof t);
+  }
+
+  bool open(int peer, uint64_t gen, const std::string& /*tok_out*/, const std::string& tok_in, int timeout_ms,
+            std::string* err) override {
+    if (tok_in.size() != sizeof(TokenWire)) {
+      *err = "malformed hipipc token";
+      return false;
+    }
+    TokenWire tw;
+    std::memcpy(&tw, tok_in.data(), sizeof tw);
+    if (std::memcmp(tw.magic, kTokMagic, sizeof tw.magic) != 0 || tw.gen != gen || tw.rank != peer) {
+      *err = "hipipc token does not match the pair";
+      return false;
+    }
+    if ((tw.spin != 0) != spin_) {
+      *err = "hipipc peers disagree on spin mode";
+      return false;
+    }
+    (void)hipSetDevice(device_);
+    Link& l = link(peer);
+    std::lock_guard<std::mutex> g(l.mu);
+    teardown_locked(l);
+    {
+      std::lock_guard<std::mutex> mg(mu_);
+      auto it = made_.find(peer);
+      if (it == made_.end() || it->second.first != gen) {
+        *err = "no inbound ring for generation " + std::to_string(gen);
+        return false;
+      }
+      l.in = it->second.second;
+      made_.erase(it);
+    }
+    tw.ring[sizeof tw.ring - 1] = '\0';
+    l.out = map_ring(tw.ring, false, gen, err);
+    if (!l.out) return fail_open(l, err);
+    void* pa = nullptr;
+    if (hipIpcOpenMemHandle(&pa, tw.arena, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      *err = std::string("hipIpcOpenMemHandle(peer arena): ") + hipGetErrorString(hipGetLastError());
+      return fail_open(l, err);
+    }
+    l.peer_arena = static_cast<uint8_t*>(pa);
+    l.peer_arena_bytes = tw.arena_bytes;
+    void* pp = nullptr;
+    if (hipIpcOpenMemHandle(&pp, tw.probe, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      *err = std::string("hipIpcOpenMemHandle(peer probe): ") + hipGetErrorString(hipGetLastError());
+      return fail_open(l, err);
+    }
+    l.peer_probe = static_cast<uint8_t*>(pp);
+    for (hipStream_t* s : {&l.send_stream, &l.recv_stream})
+      if (!*s && hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
+        *err = "hipStreamCreate failed";
+        return fail_open(l, err);
+      }
+    if (!l.done_ctr && hipMalloc(reinterpret_cast<void**>(&l.done_ctr), sizeof(uint32_t)) != hipSuccess) {
+      *err = "hipMalloc failed";
+      return fail_open(l, err);
+    }
+    (void)hipMemsetAsync(l.done_ctr, 0, sizeof(uint32_t), l.send_stream);
+    l.gen = gen;
+    l.send_seq = l.recv_seq = 0;
+    st(&l.in->r->receiver_ready, 1u);
+    st(&l.out->r->sender_attached, 1u);
+    // warm-up: 64 bytes each way through the peer's exported probe, proving the IPC mapping
+    // and the copy path end to end before the pair is declared up
+    uint64_t pat[8] = {kRingMagic, gen, static_cast<uint64_t>(rank_), static_cast<uint64_t>(peer), 0, 0, 0, 0};
+    uint8_t* mine = probe_ + kMaxRanks * 64 + peer * 64;
+    if (hipMemcpyAsync(mine, pat, sizeof pat, hipMemcpyHostToDevice, l.send_stream) != hipSuccess ||
+        hipMemcpyAsync(l.peer_probe + rank_ * 64, mine, sizeof pat, hipMemcpyDeviceToDevice, l.send_stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(l.send_stream) != hipSuccess) {
+      *err = "warm-up copy failed";
+      return fail_open(l, err);
+    }
+    st(&l.out->r->warm, gen);
+    ring_wake(l.out->r);
+    auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
+    while (ld(&l.in->r->warm) != gen) {
+      if (Clock::now() > deadline || ld(&l.in->r->abort)) {
+        *err = "peer never delivered its warm-up copy";
+        return fail_open(l, err);
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    uint64_t got[8] = {};
+    if (hipMemcpy(got, probe_ + peer * 64, sizeof got, hipMemcpyDeviceToHost) != hipSuccess || got[0] != kRingMagic ||
+        got[1] != gen || got[2] != static_cast<uint64_t>(peer) || got[3] != static_cast<uint64_t>(rank_)) {
+      *err = "warm-up bytes did not arrive intact";
+      return fail_open(l, err);
+    }
+    // both sides attached: the ring's name can go (the mappings stay)
+    ::shm_unlink(l.in->name.c_str());
+    l.in->owner = false;
+    if (!spin_) {
+      l.stop.store(false);
+      l.worker = std::thread([this, &l, out = l.out] { worker(&l, out); });
+    }
+    l.up = true;
+    return true;
+  }
+
+  void close(int peer) override {
+    Link& l = link(peer);
+    std::lock_guard<std::mutex> g(l.mu);
+    teardown_locked(l);
+  }
+
+  bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    Link& l = link(peer);
+    std::lock_guard<std::mutex> g(l.mu);
+    if (!l.up) {
+      *err = "hipipc channel down";
+      return false;
+    }
+    const uint64_t seq = l.send_seq++;
+    op->ctx = l.out;
+    op->seq = seq;
+    if (spin_) {
+      (void)hipSetDevice(device_);
+      IpcSendArgs a{&l.out->dev->posted, &l.out->dev->landed, &l.out->dev->abort, l.out->dev->slots, seq,
+                    static_cast<const uint8_t*>(buf), l.peer_arena, l.peer_arena_bytes, n, l.done_ctr, spin_ticks_};
+      hipEvent_t ev = event();
+      if (!ev || launch_ipc_send(a, send_grid(n), l.send_stream) != hipSuccess ||
+          hipEventRecord(ev, l.send_stream) != hipSuccess) {
+        if (ev) release_event(ev);
+        *err = "spin send launch failed";
+        return false;
+      }
+      op->event = ev;
+      return true;
+    }
+    op->state = std::make_shared<std::atomic<int>>(0);
+    {
+      std::lock_guard<std::mutex> q(l.qmu);
+      l.pending.push_back(SendItem{static_cast<const uint8_t*>(buf), n, seq, op->state, nullptr});
+    }
+    ring_wake(l.out->r);
+    return true;
+  }
+
+  bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    Link& l = link(peer);
+    std::lock_guard<std::mutex> g(l.mu);
+    if (!l.up) {
+      *err = "hipipc channel down";
+      return false;
+    }
+    auto* p = static_cast<uint8_t*>(buf);
+    if (p < arena_ || static_cast<uint64_t>(p - arena_) > arena_bytes_ || n > arena_bytes_ - (p - arena_)) {
+      *err = "receive buffer outside the exported arena";
+      return false;
+    }
+    IpcRing* r = l.in->r;
+    const uint64_t seq = l.recv_seq;
+    if (seq - ld(&r->landed) >= kIpcRing) {
+      *err = "hipipc ring full";
+      return false;
+    }
+    l.recv_seq++;
+    IpcSlot& s = r->slots[seq % kIpcRing];
+    __atomic_store_n(&s.off, static_cast<uint64_t>(p - arena_), __ATOMIC_RELAXED);
+    __atomic_store_n(&s.n, n, __ATOMIC_RELAXED);
+    st(&r->posted, seq + 1);  // the credit: the slot is visible before the count
+    ring_wake(r);
+    op->ctx = l.in;
+    op->seq = seq;
+    if (spin_) {
+      (void)hipSetDevice(device_);
+      hipEvent_t ev = event();
+      if (!ev || launch_ipc_wait(&l.in->dev->landed, seq + 1, &l.in->dev->abort, spin_ticks_, l.recv_stream) !=
+                     hipSuccess ||
+          hipEventRecord(ev, l.recv_stream) != hipSuccess) {
+        if (ev) release_event(ev);
+        st(&r->abort, 1u);  // the credit is out but its waiter is not: the channel is unusable
+        *err = "spin wait launch failed";
+        return false;
+      }
+      op->event = ev;
+    }
+    return true;
+  }
+
+  int test(P2POp* op) override {
+    if (op->state && !spin_) return op->state->load(std::memory_order_acquire);
+    auto* rm = static_cast<RingMap*>(op->ctx.get());
+    if (!rm) return -1;
+    if (op->event) {
+      hipError_t q = hipEventQuery(static_cast<hipEvent_t>(op->event));
+      if (q == hipErrorNotReady) return 0;
+      if (q != hipSuccess) return -1;
+      return ld(&rm->r->landed) > op->seq ? 1 : -1;  // the kernel ended: landed, or gave up
+    }
+    if (ld(&rm->r->landed) > op->seq) return 1;
+    return ld(&rm->r->abort) ? -1 : 0;
+  }
+
+  void release(P2POp* op) override {
+    if (op->event) release_event(static_cast<hipEvent_t>(op->event));
+    op->event = nullptr;
+    op->ctx.reset();
+    op->state.reset();
+  }
+
+ private:
+  struct Link {
+    std::mutex mu;  // open / close / post
+    bool up = false;
+    uint64_t gen = 0;
+    std::shared_ptr<RingMap> in, out;  // in: we receive (our ring); out: we send (the peer's ring)
+    uint8_t* peer_arena = nullptr;
+    uint64_t peer_arena_bytes = 0;
+    uint8_t* peer_probe = nullptr;
+    hipStream_t send_stream = nullptr, recv_stream = nullptr;
+    uint32_t* done_ctr = nullptr;
+    uint64_t send_seq = 0, recv_seq = 0;
+    std::mutex qmu;
+    std::deque<SendItem> pending;
+    std::thread worker;
+    std::atomic<bool> stop{false};
+  };
+
+  Link& link(int peer) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& l = links_[peer];
+    if (!l) l = std::make_unique<Link>();
+    return *l;
+  }
+
+  static int send_grid(uint64_t n) {
+    uint64_t g = n / (256 * 16 * 4);
+    return static_cast<int>(std::min<uint64_t>(64, std::max<uint64_t>(1, g)));
+  }
+
+  bool fail_open(Link& l, std::string* /*err*/) {
+    teardown_locked(l);
+    return false;
+  }
+
+  // Abort both rings, stop the worker, drain both streams (copies finish; spin kernels see
+  // the abort), unmap the peer. When this returns nothing of the old generation can land.
+  void teardown_locked(Link& l) {
+    (void)hipSetDevice(device_);
+    for (auto* m : {l.in.get(), l.out.get()})
+      if (m) {
+        st(&m->r->abort, 1u);
+        ring_wake(m->r);
+      }
+    if (l.worker.joinable()) {
+      l.stop.store(true);
+      if (l.out) ring_wake(l.out->r);
+      l.worker.join();
+    }
+    {
+      std::lock_guard<std::mutex> q(l.qmu);
+      for (auto& it : l.pending) it.st->store(-1);
+      l.pending.clear();
+    }
+    for (hipStream_t s : {l.send_stream, l.recv_stream})
+      if (s) (void)hipStreamSynchronize(s);
+    if (l.peer_arena) (void)hipIpcCloseMemHandle(l.peer_arena);
+    if (l.peer_probe) (void)hipIpcCloseMemHandle(l.peer_probe);
+    l.peer_arena = l.peer_probe = nullptr;
+    l.in.reset();
+    l.out.reset();
+    l.up = false;
+  }
+
+  // Host-driven sender of one channel: match posted sends with the receiver's credits in
+  // order, queue the copies, publish `landed` as their events complete (in order: one stream).
+  void worker(Link* l, std::shared_ptr<RingMap> out) {
+    (void)hipSetDevice(device_);
+    IpcRing* r = out->r;
+    std::deque<SendItem> inflight;
+    int idle = 0;
+    bool dead = false;
+    while (!l->stop.load() && !dead) {
+      bool progress = false;
+      for (;;) {
+        SendItem it;
+        {
+          std::lock_guard<std::mutex> q(l->qmu);
+          if (l->pending.empty() || ld(&r->posted) <= l->pending.front().seq) break;
+          it = l->pending.front();
+          l->pending.pop_front();
+        }
+        const IpcSlot& s = r->slots[it.seq % kIpcRing];
+        const uint64_t off = __atomic_load_n(&s.off, __ATOMIC_RELAXED), n = __atomic_load_n(&s.n, __ATOMIC_RELAXED);
+        hipEvent_t ev = nullptr;
+        if (n != it.n || off > l->peer_arena_bytes || n > l->peer_arena_bytes - off || ld(&r->abort) ||
+            (n && hipMemcpyAsync(l->peer_arena + off, it.src, n, hipMemcpyDeviceToDevice, l->send_stream) !=
+                      hipSuccess) ||
+            !(ev = event()) || hipEventRecord(ev, l->send_stream) != hipSuccess) {
+          if (ev) release_event(ev);
+          it.st->store(-1);
+          st(&r->abort, 1u);  // mismatched sizes or a failed copy end the channel (as RCCL would)
+          ring_wake(r);
+          dead = true;
+          break;
+        }
+        __atomic_fetch_add(&r->enqueued, 1ull, __ATOMIC_RELAXED);
+        it.ev = ev;
+        inflight.push_back(it);
+        progress = true;
+      }
+      while (!inflight.empty()) {
+        hipError_t q = hipEventQuery(inflight.front().ev);
+        if (q == hipErrorNotReady) break;
+        SendItem& it = inflight.front();
+        if (q == hipSuccess) {
+          st(&r->landed, it.seq + 1);
+          it.st->store(1, std::memory_order_release);
+        } else {
+          it.st->store(-1);
+          st(&r->abort, 1u);
+          dead = true;
+        }
+        release_event(it.ev);
+        inflight.pop_front();
+        progress = true;
+      }
+      if (ld(&r->abort)) break;
+      if (progress) {
+        idle = 0;
+        continue;
+      }
+      if (!inflight.empty()) {  // a copy is on the link: poll its event
+        if (++idle < 64) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(10));
+        continue;
+      }
+      // nothing to do: sleep until a send is posted here or a credit arrives from the peer
+      const uint32_t bell = __atomic_load_n(&r->doorbell, __ATOMIC_ACQUIRE);
+      {
+        std::lock_guard<std::mutex> q(l->qmu);
+        if (!l->pending.empty() && ld(&r->posted) > l->pending.front().seq) continue;
+      }
+      timespec ts{0, 2'000'000};
+      futex(&r->doorbell, FUTEX_WAIT, bell, &ts);
+    }
+    // stopping: the queued copies still finish (nothing can cancel a DMA); their ops fail
+    for (auto& it : inflight) {
+      (void)hipEventSynchronize(it.ev);
+      it.st->store(-1);
+      release_event(it.ev);
+    }
+  }
+
+  hipEvent_t event() {
+    {
+      std::lock_guard<std::mutex> g(ev_mu_);
+      if (!free_events_.empty()) {
+        hipEvent_t e = free_events_.back();
+        free_events_.pop_back();
+        return e;
+      }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return e;
+  }
+  void release_event(hipEvent_t e) {
+    std::lock_guard<std::mutex> g(ev_mu_);
+    free_events_.push_back(e);
+  }
+
+  int device_, rank_;
+  std::string ns_;
+  uint8_t* arena_;
+  uint64_t arena_bytes_;
+  bool spin_;
+  uint64_t spin_ticks_ = 0;
+  hipIpcMemHandle_t arena_h_{}, probe_h_{};
+  uint8_t* probe_ = nullptr;
+  std::mutex mu_;
+  std::map<int, std::unique_ptr<Link>> links_;
+  std::map<int, std::pair<uint64_t, std::shared_ptr<RingMap>>> made_;  // inbound rings awaiting open()
+  std::mutex ev_mu_;
+  std::vector<hipEvent_t> free_events_;
+};
+
+}  // namespace
+
+std::unique_ptr<P2PTransport> make_ipc_transport(int device, int rank, const std::string& ns, uint8_t* arena,
+                                                 uint64_t arena_bytes, bool spin, std::string* err) {
+  if (device < 0 || arena == nullptr || arena_bytes == 0) {
+    *err = "hipipc transport requires a GPU chunk store";
+    return nullptr;
+  }
+  auto t = std::make_unique<IpcTransport>(device, rank, ns, arena, arena_bytes, spin);
+  if (!t->init(err)) return nullptr;
+  return t;
+}
+
+}  // namespace dfs

@@ -23,6 +23,7 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+#include <algorithm>
 
 #include "p2p_transport.h"
 
@@ -253,6 +254,105 @@ class RcclTransport final : public P2PTransport {
 };
 
 }  // namespace
+
+// One-GPU hardware check of the pieces RcclTransport is built from: a NONBLOCKING
+// communicator brought up through settle(), a grouped ncclSend/ncclRecv (a 1-rank
+// communicator sends to itself; RCCL refuses two ranks on one GPU, so this is the only
+// RCCL p2p a 1-GPU box can run), completion observed through a hipEvent as test() does, the
+// bytes compared, then ncclCommAbort while a large transfer is still running (close()'s
+// path) and a fresh communicator on the same device afterwards (a pair rebuild).
+RcclProbe rccl_loopback_probe(int device, uint64_t bytes, uint64_t abort_bytes, int timeout_ms) {
+  RcclProbe out;
+  auto fail = [&](const std::string& e) {
+    out.error = e;
+    return out;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice");
+  int ver = 0;
+  ncclGetVersion(&ver);
+  out.version = ver;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return fail("hipStreamCreate");
+  const uint64_t cap = std::max(bytes, abort_bytes);
+  uint8_t *src = nullptr, *dst = nullptr;
+  if (hipMalloc(reinterpret_cast<void**>(&src), cap) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&dst), cap) != hipSuccess)
+    return fail("hipMalloc");
+  std::vector<uint8_t> pat(bytes);
+  for (uint64_t i = 0; i < bytes; ++i) pat[i] = static_cast<uint8_t>((i * 2654435761u) >> 13);
+  (void)hipMemcpy(src, pat.data(), bytes, hipMemcpyHostToDevice);
+  (void)hipMemset(dst, 0, cap);
+  hipEvent_t ev = nullptr;
+  (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  auto comm_up = [&](ncclComm_t* c, const std::string& what) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) {
+      out.error = "ncclGetUniqueId";
+      return false;
+    }
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    auto t0 = Clock::now();
+    ncclResult_t r = ncclCommInitRankConfig(c, 1, id, 0, &cfg);
+    bool ok = *c != nullptr && settle(*c, r, t0 + std::chrono::milliseconds(timeout_ms), &out.error, what);
+    out.init_ms.push_back(std::chrono::duration<double, std::milli>(Clock::now() - t0).count());
+    return ok;
+  };
+  auto self_xfer = [&](ncclComm_t c, uint64_t n, const std::string& what) {
+    ncclGroupStart();
+    ncclSend(src, n, ncclUint8, 0, c, s);
+    ncclRecv(dst, n, ncclUint8, 0, c, s);
+    ncclResult_t r = ncclGroupEnd();
+    return settle(c, r, Clock::now() + std::chrono::milliseconds(timeout_ms), &out.error, what) &&
+           hipEventRecord(ev, s) == hipSuccess;
+  };
+  auto wait_event = [&](int ms) {
+    auto deadline = Clock::now() + std::chrono::milliseconds(ms);
+    for (;;) {
+      hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) return true;
+      if (q != hipErrorNotReady || Clock::now() > deadline) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  };
+  ncclComm_t comm = nullptr;
+  if (!comm_up(&comm, "init")) return out;
+  auto t0 = Clock::now();
+  if (!self_xfer(comm, bytes, "grouped self send/recv") || !wait_event(timeout_ms)) {
+    if (out.error.empty()) out.error = "self transfer did not complete";
+    ncclCommAbort(comm);
+    return out;
+  }
+  out.xfer_ms = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+  std::vector<uint8_t> got(bytes);
+  (void)hipMemcpy(got.data(), dst, bytes, hipMemcpyDeviceToHost);
+  out.bytes_ok = got == pat;
+  if (abort_bytes) {
+    // abort with a large transfer in flight: close()'s path; the stream must drain, bounded
+    if (!self_xfer(comm, abort_bytes, "large self send/recv")) return out;
+    auto ta = Clock::now();
+    ncclCommAbort(comm);
+    comm = nullptr;
+    out.abort_ms = std::chrono::duration<double, std::milli>(Clock::now() - ta).count();
+    out.drained_after_abort = wait_event(timeout_ms);
+    // a rebuild: a new communicator on the same device carries bytes again
+    ncclComm_t again = nullptr;
+    (void)hipMemset(dst, 0, bytes);
+    if (comm_up(&again, "re-init") && self_xfer(again, bytes, "self send/recv after abort") && wait_event(timeout_ms)) {
+      (void)hipMemcpy(got.data(), dst, bytes, hipMemcpyDeviceToHost);
+      out.reinit_ok = got == pat;
+    }
+    if (again) ncclCommDestroy(again);
+  } else {
+    ncclCommDestroy(comm);
+  }
+  (void)hipEventDestroy(ev);
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  (void)hipStreamDestroy(s);
+  out.ok = out.bytes_ok && (abort_bytes == 0 || (out.drained_after_abort && out.reinit_ok));
+  return out;
+}
 
 std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, std::string* err) {
   if (device < 0) {

@@ -14,6 +14,10 @@
 // Implementations:
 //  * RcclTransport  (p2p_rccl.cpp): one 2-rank nonblocking communicator + HIP stream per
 //    direction; buffers are HBM pointers of our GPU, each op records a hipEvent.
+//  * IpcTransport   (p2p_ipc.cpp): HIP IPC between processes of one node; the receiver
+//    publishes each posted buffer (an offset in its exported arena) on a shared-memory ring,
+//    the sender's copy engine writes the slice there and bumps the ring's landed count. No
+//    kernel ever waits on a peer, so no hardware queue can be held by a peer (see p2p_ipc.cpp).
 //  * SocketTransport (p2p_socket.cpp): a UNIX stream socket per direction and a worker
 //    thread per direction draining the FIFO of posted ops; buffers are host memory. It is
 //    what the multi-process CPU tests run (tests/test_replication.py), so every rule of the
@@ -24,12 +28,15 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace dfs {
 
 struct P2POp {
   void* event = nullptr;                        // RCCL: hipEvent_t recorded after the op
   std::shared_ptr<std::atomic<int>> state;      // socket: 0 pending, 1 done, -1 failed
+  std::shared_ptr<void> ctx;                    // hipipc: the channel ring the op completes on
+  uint64_t seq = 0;                             // hipipc: position of the op on its channel
 };
 
 class P2PTransport {
@@ -59,6 +66,16 @@ class P2PTransport {
   virtual void debug_stall(int /*peer*/, int /*ms*/) {}
 };
 
+struct RcclProbe {
+  bool ok = false, bytes_ok = false, drained_after_abort = false, reinit_ok = false;
+  int version = 0;
+  double xfer_ms = 0, abort_ms = 0;
+  std::vector<double> init_ms;
+  std::string error;
+};
+// 1-GPU hardware check of RcclTransport's building blocks (p2p_rccl.cpp).
+RcclProbe rccl_loopback_probe(int device, uint64_t bytes, uint64_t abort_bytes, int timeout_ms);
+
 // device >= 0: RCCL over xGMI on that GPU. Returns nullptr (with *err) if unavailable.
 std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, std::string* err);
 // Host-memory transport over abstract UNIX sockets; `ns` keeps test clusters apart.
@@ -66,5 +83,11 @@ std::unique_ptr<P2PTransport> make_socket_transport(int rank, const std::string&
 // Single-GPU test transport: engines in ONE process (stores on the same GPU) exchange device
 // buffers with the RCCL matching contract, each matched pair a D2D copy (p2p_hiploop.cpp).
 std::unique_ptr<P2PTransport> make_hiploop_transport(int device, int rank, const std::string& ns);
+// Same-node device transport between PROCESSES (p2p_ipc.cpp): every rank exports its HBM
+// arena over HIP IPC; a matched send is a one-sided copy into the receiver's posted extent
+// (xGMI between GPUs, an in-HBM copy when ranks share one GPU). `spin` = RCCL emulation:
+// spinning send/wait kernels on the channel streams instead of host-driven copies.
+std::unique_ptr<P2PTransport> make_ipc_transport(int device, int rank, const std::string& ns, uint8_t* arena,
+                                                 uint64_t arena_bytes, bool spin, std::string* err);
 
 }  // namespace dfs

@@ -56,9 +56,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--rccl-world", type=int, default=0)
     p.add_argument("--rccl-rendezvous", default="")
     p.add_argument("--rccl-timeout-ms", type=int, default=60000)
-    p.add_argument("--replication-transport", choices=["rccl", "grpc", "socket"], default="rccl",
-                   help="payload path between same-node chunkservers: rccl (xGMI), grpc (reference), "
-                        "socket (host-memory P2P transport used by the CPU tests)")
+    p.add_argument("--replication-transport", choices=["hipipc", "hipipc-spin", "rccl", "grpc", "socket"],
+                   default="hipipc",
+                   help="payload path between same-node chunkservers: hipipc (HIP IPC one-sided copies into the "
+                        "peer's HBM over xGMI; no kernel ever waits on a peer), hipipc-spin (the same with RCCL-like "
+                        "spinning p2p kernels, for tests), rccl (ncclSend/ncclRecv), grpc (reference), socket "
+                        "(host-memory P2P transport used by the CPU tests)")
     p.add_argument("--repl-turn-timeout-ms", type=int, default=3000,
                    help="how long a replica waits for an earlier sequence number before failing the pair")
     p.add_argument("--heartbeat-interval", type=float, default=5.0)
@@ -138,8 +141,8 @@ class ChunkServerProcess:
         self.repl_pairs_up = 0
         rank_map: dict[str, int] = {}
         transport = args.replication_transport
-        if (transport in ("rccl", "socket") and args.rccl_world > 1 and args.rccl_rank >= 0 and args.rccl_rendezvous
-                and (args.gpu >= 0 or transport == "socket")):
+        if (transport in ("hipipc", "hipipc-spin", "rccl", "socket") and args.rccl_world > 1 and args.rccl_rank >= 0
+                and args.rccl_rendezvous and (args.gpu >= 0 or transport == "socket")):
             if self.fastpath is None:
                 log.error("replication engine needs the native fast path (pair control); using gRPC replication")
             else:

@@ -62,7 +62,9 @@ class LocalCluster:
         self.fsync = fsync
         self.rccl = rccl
         # "socket": native replication engine over the host-memory P2P transport (CPU tests of
-        # the same protocol RCCL runs on GPUs); None: RCCL with GPUs, reference gRPC without
+        # the same protocol the device transports run); "hipipc" / "hipipc-spin": the device
+        # transport between chunkserver processes (works with several of them on one GPU);
+        # None: RCCL with GPUs, reference gRPC without
         self.p2p = p2p
         self.hbm_capacity = hbm_capacity
         self.heartbeat_interval = heartbeat_interval
@@ -230,12 +232,13 @@ class LocalCluster:
                 args += ["--config-servers", ",".join(self.config_addrs)]
             else:
                 args += ["--masters", ",".join(m for ms in shard_cfg.values() for m in ms)]
-            if self.p2p == "socket" and self.n_cs > 1:
+            if self.p2p in ("socket", "hipipc", "hipipc-spin") and self.n_cs > 1:
                 args += ["--rccl-rank", str(i), "--rccl-world", str(self.n_cs), "--rccl-rendezvous", str(rdv),
-                         "--replication-transport", "socket", "--rccl-timeout-ms", "10000",
+                         "--replication-transport", self.p2p, "--rccl-timeout-ms", "10000",
                          "--repl-turn-timeout-ms", "1500"]
             elif self.gpus is not None and self.n_cs > 1 and self.rccl:
-                args += ["--rccl-rank", str(i), "--rccl-world", str(self.n_cs), "--rccl-rendezvous", str(rdv)]
+                args += ["--rccl-rank", str(i), "--rccl-world", str(self.n_cs), "--rccl-rendezvous", str(rdv),
+                         "--replication-transport", "rccl"]
             else:
                 args += ["--replication-transport", "grpc"]
             cprocs.append(self._spawn(f"cs{i}", "chunkserver.server", args))

@@ -49,10 +49,10 @@ def test_bench_single_rank_cpu(tmp_path):
     assert d["remote_client"]["native_client_ops"] == d["remote_client"]["steps"] * 2 * 10
 
 
-@pytest.mark.parametrize("n", [4])
+@pytest.mark.parametrize("n", [4, 8])
 def test_bench_multi_rank_socket_transport(tmp_path, n):
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-              "--master-addr", "127.0.0.1", "--master-port", "29671", "bench.py", "--gpus", str(n),
+              "--master-addr", "127.0.0.1", "--master-port", str(29671 + n), "bench.py", "--gpus", str(n),
               "--steps", "1", "--warmup", "1", "--cpu", "--count", "10", "--transport", "socket",
               "--remote-steps", "0"], tmp_path)
     _check_common(d, n, 1, 1)
