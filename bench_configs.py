@@ -226,6 +226,13 @@ def config5(a):
         out["parquet_over_s3"] = parquet_phase(url, a)
         out["load_generator"] = f"{a.concurrency} client processes (requests, keep-alive)"
         out["gateway_workers"] = int(os.environ.get("S3_WORKERS", "4"))
+        # what the native front end served itself vs handed to the Python workers
+        nat = {}
+        for ln in s.get(f"{url}/metrics").text.splitlines():
+            if ln.startswith(("s3_native_requests_total", "s3_native_handoffs_total", "s3_native_bytes")):
+                k, v = ln.rsplit(" ", 1)
+                nat[k] = int(float(v))
+        out["native_front"] = nat
         emit(out)
 
 

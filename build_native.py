@@ -99,7 +99,7 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
     out = ext_path()
     if clean or not out.exists() or any(o.stat().st_mtime > out.stat().st_mtime for o in objs):
         link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(out), *map(str, objs),
-                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto", NGHTTP2_LIB,
+                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lssl", "-lcrypto", NGHTTP2_LIB,
                 "-lpthread", f"-Wl,-rpath,{ROCM}/lib"]
         r = subprocess.run(link, capture_output=True, text=True)
         if r.returncode != 0:
@@ -124,7 +124,7 @@ def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[P
                 raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
         if clean or not exe.exists() or any(o.stat().st_mtime > exe.stat().st_mtime for o in [obj, *runtime]):
             r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-o", str(exe), str(obj), *map(str, runtime),
-                                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lcrypto",
+                                f"-L{ROCM}/lib", "-lamdhip64", "-lrccl", "-lrocprofiler-sdk-roctx", "-lssl", "-lcrypto",
                                 NGHTTP2_LIB, "-lpthread", f"-Wl,-rpath,{ROCM}/lib"], capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"link failed: {exe}\n{r.stdout}\n{r.stderr}")

@@ -17,6 +17,7 @@
 #include "cs_grpc.h"
 #include "grpc_server.h"
 #include "sigv4.h"
+#include "tls.h"
 #include "wal.h"
 
 namespace py = pybind11;
@@ -555,7 +556,7 @@ PYBIND11_MODULE(_dfs_native, m) {
   };
   py::class_<NativeGrpc>(m, "NativeGrpcChunkServer")
       .def(py::init([](ChunkStore* store, FastPathServer* fp, const std::string& host, int port, py::object fallback,
-                       int workers) {
+                       int workers, const std::string& tls_cert, const std::string& tls_key) {
              auto n = std::make_unique<NativeGrpc>();
              // the Python fallback is released with the GIL held, whichever thread drops it
              n->fallback = std::shared_ptr<py::object>(new py::object(std::move(fallback)), [](py::object* o) {
@@ -575,10 +576,17 @@ PYBIND11_MODULE(_dfs_native, m) {
              NativeChunkService* svc = n->svc.get();
              n->srv = std::make_unique<GrpcServer>(host, port, [svc](const GrpcCall& c) { return svc->handle(c); },
                                                    workers);
+             if (!tls_cert.empty()) {
+               std::string err;
+               auto t = TlsContext::server(tls_cert, tls_key, &err);
+               if (!t) throw std::runtime_error(err);
+               n->srv->set_tls(std::move(t));
+             }
              return n;
            }),
            py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::arg("store"), py::arg("fastpath"), py::arg("host"),
-           py::arg("port"), py::arg("fallback"), py::arg("workers") = 32)
+           py::arg("port"), py::arg("fallback"), py::arg("workers") = 32, py::arg("tls_cert") = "",
+           py::arg("tls_key") = "")
       .def("start", [](NativeGrpc& n) {
         std::string err;
         bool ok = n.srv->start(&err);

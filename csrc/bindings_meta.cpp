@@ -24,6 +24,8 @@
 #include "config_core.h"
 #include "master_core.h"
 #include "raft.h"
+#include "s3_front.h"
+#include "tls.h"
 #include "trace.h"
 
 namespace py = pybind11;
@@ -91,7 +93,7 @@ class PyRaftHost : public raft::Host {
     if (!ep.empty()) {
       // native peer path: the peer's native gRPC server hands the JSON straight to its node
       // (reference timeouts: 1.5 s per RPC, snapshots get longer)
-      GrpcResult r = peers_.call(ep, "/dfs.RaftPeer/" + kind, body, "", kind == "snapshot" ? 30000 : 1500);
+      GrpcResult r = peers_->call(ep, "/dfs.RaftPeer/" + kind, body, "", kind == "snapshot" ? 30000 : 1500);
       if (!r.transport_ok || r.status != 0) return false;
       *reply = std::move(r.message);
       return true;
@@ -129,7 +131,11 @@ class PyRaftHost : public raft::Host {
   std::mutex peers_mu_;
   std::map<std::string, std::string> endpoints_;  // member address -> native gRPC endpoint
   std::set<std::string> blocked_;
-  GrpcChannelPool peers_{1500};
+  std::unique_ptr<GrpcChannelPool> peers_ = std::make_unique<GrpcChannelPool>(1500);
+
+ public:
+  // https peers: the native Raft peer RPC runs over TLS (set before the node starts)
+  void set_peer_tls(std::shared_ptr<TlsContext> tls) { peers_ = std::make_unique<GrpcChannelPool>(1500, std::move(tls)); }
 };
 
 // Read a node property with the GIL released (the getter may wait on the node mutex).
@@ -319,7 +325,7 @@ void bind_meta(py::module_& m) {
       .def(py::init([](int id, std::map<int, std::string> members, std::string client_address, std::string dir,
                        py::object host, double elo, double ehi, double hb, bool sync, uint64_t snapshot_threshold,
                        int max_batch, std::string backup_endpoint, std::string backup_bucket, py::object native_sm,
-                       bool pre_vote) {
+                       bool pre_vote, bool peer_tls, std::string peer_ca, std::string peer_domain) {
              raft::Options o;
              o.id = id;
              o.members = std::move(members);
@@ -337,13 +343,20 @@ void bind_meta(py::module_& m) {
              std::shared_ptr<raft::StateMachine> sm;
              if (!native_sm.is_none()) sm = native_sm.cast<std::shared_ptr<raft::StateMachine>>();
              auto h = std::make_shared<PyRaftHost>(std::move(host), sm);
+             if (peer_tls) {
+               std::string err;
+               auto t = TlsContext::client(peer_ca, peer_domain, &err);
+               if (!t) throw std::runtime_error(err);
+               h->set_peer_tls(std::move(t));
+             }
              return std::unique_ptr<raft::Node, NodeDeleter>(new raft::Node(std::move(o), h));
            }),
            py::arg("id"), py::arg("members"), py::arg("client_address"), py::arg("dir"), py::arg("host"),
            py::arg("election_lo") = 1.5, py::arg("election_hi") = 3.0, py::arg("heartbeat") = 0.1,
            py::arg("sync") = true, py::arg("snapshot_threshold") = 10000, py::arg("max_append_batch") = 512,
            py::arg("backup_endpoint") = "", py::arg("backup_bucket") = "dfs-backups",
-           py::arg("native_sm") = py::none(), py::arg("pre_vote") = true)
+           py::arg("native_sm") = py::none(), py::arg("pre_vote") = true, py::arg("peer_tls") = false,
+           py::arg("peer_ca") = "", py::arg("peer_domain") = "")
       .def("start", &raft::Node::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &raft::Node::stop, py::call_guard<py::gil_scoped_release>())
       .def("propose", [](raft::Node& n, std::string cmd, py::object cb) {
@@ -574,7 +587,7 @@ void bind_meta(py::module_& m) {
   };
   py::class_<NativeGrpcMaster>(m, "NativeGrpcMasterServer")
       .def(py::init([](std::shared_ptr<MasterCore> core, const std::string& host, int port, py::object fallback,
-                       int workers) {
+                       int workers, const std::string& tls_cert, const std::string& tls_key) {
              auto n = std::make_unique<NativeGrpcMaster>();
              n->fallback = std::make_shared<PyRef>(std::move(fallback));
              auto fb = n->fallback;
@@ -607,9 +620,16 @@ void bind_meta(py::module_& m) {
                  return GrpcReply{13, std::string("python handler failed: ") + e.what()};
                }
              }, workers);
+             if (!tls_cert.empty()) {
+               std::string err;
+               auto t = TlsContext::server(tls_cert, tls_key, &err);
+               if (!t) throw std::runtime_error(err);
+               n->srv->set_tls(std::move(t));
+             }
              return n;
            }),
-           py::arg("core"), py::arg("host"), py::arg("port"), py::arg("fallback"), py::arg("workers") = 64)
+           py::arg("core"), py::arg("host"), py::arg("port"), py::arg("fallback"), py::arg("workers") = 64,
+           py::arg("tls_cert") = "", py::arg("tls_key") = "")
       .def("start", [](NativeGrpcMaster& n) {
         std::string err;
         bool ok = n.srv->start(&err);
@@ -626,6 +646,65 @@ void bind_meta(py::module_& m) {
         d["native_grpc_native"] = n.native_calls.load();
         d["native_grpc_fallback"] = n.fallback_calls.load();
         d["native_raft_rpcs"] = n.raft_calls.load();
+        return d;
+      });
+
+  // ---------------- native S3 front end (csrc/s3_front.cpp)
+  py::class_<S3Front>(m, "S3Front")
+      .def(py::init([](FastClient* fc, const std::string& host, int port, const std::string& backend, int workers,
+                       bool auth_enabled, const std::string& region, const std::string& access_key,
+                       const std::string& secret_key, bool allow_unsigned, const std::string& audit_socket,
+                       bool sse_enabled, bool metadata_sidecar) {
+             S3FrontConfig c;
+             c.host = host;
+             c.port = port;
+             c.backend = backend;
+             c.workers = workers;
+             c.auth_enabled = auth_enabled;
+             c.region = region;
+             c.access_key = access_key;
+             c.secret_key = secret_key;
+             c.allow_unsigned_payload = allow_unsigned;
+             c.audit_socket = audit_socket;
+             c.sse_enabled = sse_enabled;
+             c.metadata_sidecar = metadata_sidecar;
+             return std::make_unique<S3Front>(c, fc);
+           }),
+           py::arg("fast_client"), py::arg("host"), py::arg("port"), py::arg("backend"), py::arg("workers") = 32,
+           py::arg("auth_enabled") = false, py::arg("region") = "us-east-1", py::arg("access_key") = "",
+           py::arg("secret_key") = "", py::arg("allow_unsigned_payload") = true, py::arg("audit_socket") = "",
+           py::arg("sse_enabled") = false, py::arg("metadata_sidecar") = false, py::keep_alive<1, 2>())
+      .def("start", [](S3Front& f) {
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release r;
+          ok = f.start(&err);
+        }
+        return py::make_tuple(ok, err);
+      })
+      .def("stop", &S3Front::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("port", &S3Front::port)
+      .def("stats", [](S3Front& f) {
+        S3FrontStats s = f.stats();
+        py::dict d;
+        d["connections"] = s.connections;
+        d["requests"] = s.requests;
+        d["native"] = s.native;
+        d["proxied"] = s.proxied;
+        d["puts"] = s.puts;
+        d["parts"] = s.parts;
+        d["gets"] = s.gets;
+        d["range_gets"] = s.range_gets;
+        d["heads"] = s.heads;
+        d["mpu_gets"] = s.mpu_gets;
+        d["bytes_in"] = s.bytes_in;
+        d["bytes_out"] = s.bytes_out;
+        d["auth_native"] = s.auth_native;
+        d["audit_sent"] = s.audit_sent;
+        d["audit_dropped"] = s.audit_dropped;
+        d["by_status"] = s.by_status;
+        d["proxy_reasons"] = s.proxy_reasons;
         return d;
       });
 
@@ -685,7 +764,17 @@ void bind_meta(py::module_& m) {
 
   // ---------------- native remote client (every RPC over gRPC/TCP, client_remote.h)
   py::class_<RemoteClient>(m, "RemoteClient")
-      .def(py::init<int, int>(), py::arg("hash_threads") = 4, py::arg("timeout_ms") = 120000)
+      .def(py::init([](int hash_threads, int timeout_ms, bool tls, const std::string& ca, const std::string& domain) {
+             std::shared_ptr<TlsContext> t;
+             if (tls) {
+               std::string err;
+               t = TlsContext::client(ca, domain, &err);
+               if (!t) throw std::runtime_error(err);
+             }
+             return std::make_unique<RemoteClient>(hash_threads, timeout_ms, std::move(t));
+           }),
+           py::arg("hash_threads") = 4, py::arg("timeout_ms") = 120000, py::arg("tls") = false, py::arg("ca_cert") = "",
+           py::arg("domain_name") = "")
       .def_property_readonly("writes", &RemoteClient::writes)
       .def_property_readonly("reads", &RemoteClient::reads)
       .def_property_readonly("connects", &RemoteClient::connects)

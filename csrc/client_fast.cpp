@@ -314,12 +314,29 @@ bool FastClient::fp_call(uint8_t op, const std::string& body, uint8_t* status, u
 FastClient::Status FastClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
                                      std::string* msg, Times* t, const std::string& rid_in,
                                      const std::map<std::string, std::string>* attrs) {
+  if (!base_ || n > slot_bytes_) return NotHandled;
+  int64_t slot = acquire(n);
+  if (slot < 0) return NotHandled;
+  std::memcpy(base_ + slot, data, n);
+  std::string md5;
+  Status st = write_slot(path, slot, n, replicas, msg, t, rid_in, attrs, nullptr, &md5);
+  release(slot);
+  return st;
+}
+
+int64_t FastClient::acquire_slot(size_t n) { return acquire(n); }
+
+FastClient::Status FastClient::write_slot(const std::string& path, int64_t slot, size_t n, int* replicas,
+                                          std::string* msg, Times* t, const std::string& rid_in,
+                                          const std::map<std::string, std::string>* attrs, const char* etag_attr,
+                                          std::string* md5_out) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.client.write");
-  if (!base_ || n > slot_bytes_) return NotHandled;
+  if (!base_ || n > slot_bytes_ || slot < 0) return NotHandled;
   std::string sock = master_socket(path);
   if (sock.empty()) return NotHandled;
+  const uint8_t* data = base_ + slot;
   auto clk = Clock::now();
   // MD5 (the ETag) is a sequential chain and only CompleteFile needs it: hash on a worker
   // while the create RPC, the CRC and the block transfer run here
@@ -369,9 +386,6 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
     return NotHandled;  // nothing was recorded yet: the Python path redoes it
   t->create = since(clk);
 
-  int64_t slot = acquire(n);
-  if (slot < 0) return NotHandled;
-  std::memcpy(base_ + slot, data, n);
   std::string body;
   put<uint64_t>(body, alloc.master_term);
   put<uint32_t>(body, crc);
@@ -387,7 +401,6 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   uint64_t total, written;
   std::string fmsg;
   bool sent = fp_call(1, body, &st, &total, &written, &fmsg);
-  release(slot);
   if (!sent) return NotHandled;
   if (st == 5 || st == 4) {  // fenced / I/O error: what the gRPC path would report
     *msg = "Failed to write block: " + fmsg;
@@ -401,6 +414,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   done.path = path;
   done.size = n;
   done.etag_md5 = md5.get();
+  *md5_out = done.etag_md5;
   t->md5_wait = since(clk);
   done.created_at_ms = static_cast<uint64_t>(now_ms());
   pb::BlockChecksumInfo sum;
@@ -413,6 +427,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   done.ec_parity_shards = alloc.ec_parity_shards;
   done.blocks.push_back(alloc.block);
   if (attrs) done.attributes = *attrs;
+  if (etag_attr) done.attributes[etag_attr] = "\"" + done.etag_md5 + "\"";
   if (!call(sock, "/dfs.MasterService/CompleteFile", rid, done.str(), &code, &raw)) {
     *msg = "Failed to complete file: master connection lost";
     return Failed;
@@ -432,29 +447,81 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   return Ok;
 }
 
+FastClient::Status FastClient::stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg,
+                                    const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  std::string sock = master_socket(path);
+  if (sock.empty()) return NotHandled;
+  pb::GetFileInfoRequest req;
+  req.path = path;
+  int code;
+  std::string raw;
+  if (!call(sock, "/dfs.MasterService/GetFileInfo", rid, req.str(), &code, &raw)) return NotHandled;
+  if (code == kNotFound) {
+    *found = false;
+    return Ok;
+  }
+  if (code != 0) {
+    *msg = raw;
+    return NotHandled;  // redirect / not leader / unavailable: the Python path follows it
+  }
+  pb::GetFileInfoResponse info;
+  if (!info.decode(raw)) return NotHandled;
+  *found = info.found;
+  if (info.found) *meta_pb = info.metadata.str();
+  return Ok;
+}
+
+FastClient::Status FastClient::remove(const std::string& path, std::string* msg, const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  std::string sock = master_socket(path);
+  if (sock.empty()) return NotHandled;
+  pb::DeleteFileRequest req;
+  req.path = path;
+  int code;
+  std::string raw;
+  if (!call(sock, "/dfs.MasterService/DeleteFile", rid, req.str(), &code, &raw)) return NotHandled;
+  if (code != 0) {
+    *msg = raw;
+    return code == kNotFound ? Failed : NotHandled;
+  }
+  pb::DeleteFileResponse r;
+  if (!r.decode(raw)) return NotHandled;
+  if (!r.success) {
+    if (r.error_message == "Not Leader") return NotHandled;
+    *msg = r.error_message;
+    return Failed;
+  }
+  return Ok;
+}
+
 FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg,
                                     Times* t, const std::string& rid_in, uint64_t offset, uint64_t length) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.client.read");
   if (!base_) return NotHandled;
-  std::string sock = master_socket(path);
-  if (sock.empty()) return NotHandled;
   auto clk = Clock::now();
-  pb::GetFileInfoRequest req;
-  req.path = path;
-  int code;
-  std::string raw;
-  if (!call(sock, "/dfs.MasterService/GetFileInfo", rid, req.str(), &code, &raw)) return NotHandled;
-  if (code != 0) return code == kNotFound ? (*msg = raw, Failed) : NotHandled;
-  pb::GetFileInfoResponse info;
-  if (!info.decode(raw)) return NotHandled;
-  if (!info.found) {
+  bool found = false;
+  std::string meta;
+  Status st = stat(path, &found, &meta, msg, rid);
+  if (st != Ok) return st;
+  if (!found) {
     *msg = "File not found";
     return Failed;
   }
   t->getinfo = since(clk);
-  const pb::FileMetadata& m = info.metadata;
+  return read_known(meta, slot, n, msg, t, rid, offset, length);
+}
+
+FastClient::Status FastClient::read_known(const std::string& meta_pb, int64_t* slot, uint64_t* n, std::string* msg,
+                                          Times* t, const std::string& rid_in, uint64_t offset, uint64_t length) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  RequestScope rs(rid);
+  if (!base_) return NotHandled;
+  auto clk = Clock::now();
+  pb::FileMetadata m;
+  if (!m.decode(meta_pb)) return NotHandled;
   if (m.size == 0) {
     *slot = -1;
     *n = 0;
@@ -493,7 +560,7 @@ FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint
     release(s);
     return NotHandled;  // corrupt / missing here: the Python path recovers from a replica
   }
-  t->read = since(clk);
+  t->read += since(clk);
   *slot = s + static_cast<int64_t>(shift);
   *n = got;
   reads_++;

@@ -54,7 +54,25 @@ class FastClient {
   Status read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg, Times* t,
               const std::string& rid = "", uint64_t offset = 0, uint64_t length = 0);
   const uint8_t* slot_ptr(int64_t slot) const { return base_ + slot; }
+  uint8_t* slot_mut(int64_t slot) { return base_ + slot; }
+  size_t slot_bytes() const { return slot_bytes_; }
   void release(int64_t slot);
+
+  // ---- gateway entry points (csrc/s3_front.cpp): the payload is produced / consumed in
+  // place in a slot, so an HTTP body moves socket -> slot -> HBM with no staging copy.
+  int64_t acquire_slot(size_t n);  // -1: none free within 5 s, or n > slot_bytes()
+  // write() of bytes already in `slot`. When `etag_attr` is set, attrs[etag_attr] is
+  // replaced by the quoted MD5 before CompleteFile (the S3 ETag). *md5_out = the MD5.
+  // The caller keeps (and releases) the slot.
+  Status write_slot(const std::string& path, int64_t slot, size_t n, int* replicas, std::string* msg, Times* t,
+                    const std::string& rid, const std::map<std::string, std::string>* attrs, const char* etag_attr,
+                    std::string* md5_out);
+  // GetFileInfo on the path's shard: Ok with *found, or NotHandled (remote/non-leader master).
+  Status stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg, const std::string& rid);
+  // read() of a file whose metadata (serialized FileMetadata) the caller already holds.
+  Status read_known(const std::string& meta_pb, int64_t* slot, uint64_t* n, std::string* msg, Times* t,
+                    const std::string& rid, uint64_t offset, uint64_t length);
+  Status remove(const std::string& path, std::string* msg, const std::string& rid);
 
   uint64_t writes() const { return writes_.load(); }
   uint64_t reads() const { return reads_.load(); }

@@ -64,7 +64,8 @@ bool not_leader(const std::string& m, std::string* hint) {
 
 }  // namespace
 
-RemoteClient::RemoteClient(int hash_threads, int timeout_ms) : pool_(timeout_ms) {
+RemoteClient::RemoteClient(int hash_threads, int timeout_ms, std::shared_ptr<TlsContext> tls)
+    : pool_(timeout_ms, std::move(tls)) {
   for (int i = 0; i < std::max(1, hash_threads); ++i) hashers_.emplace_back([this] { hash_loop(); });
 }
 

@@ -7,7 +7,7 @@
 //   read:  GetFileInfo -> ReadBlock from the first location that answers
 //
 // Leader changes are followed (Not Leader hints, then the shard's other peers). Anything
-// else it does not own — shard redirects, EC or multi-block files, TLS — returns NotHandled
+// else it does not own — shard redirects, EC or multi-block files — returns NotHandled
 // and the Python client takes over, so semantics never change. It is what makes the
 // "remote client" numbers of bench.py a native client against native servers, like the
 // reference's Rust dfs_cli against its Rust servers.
@@ -24,6 +24,7 @@
 
 #include "client_fast.h"
 #include "grpc_client.h"
+#include "tls.h"
 #include "shard_map.h"
 
 namespace dfs {
@@ -33,7 +34,8 @@ class RemoteClient {
   using Status = FastClient::Status;
   using Times = FastClient::Times;
 
-  explicit RemoteClient(int hash_threads = 4, int timeout_ms = 120000);
+  // `tls`: TLS client context for https endpoints (nullptr = h2c).
+  explicit RemoteClient(int hash_threads = 4, int timeout_ms = 120000, std::shared_ptr<TlsContext> tls = nullptr);
   ~RemoteClient();
   RemoteClient(const RemoteClient&) = delete;
 

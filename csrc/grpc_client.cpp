@@ -15,6 +15,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "tls.h"
+
 namespace dfs {
 
 namespace {
@@ -104,6 +106,7 @@ int connect_to(const std::string& hostport, int timeout_ms, std::string* err) {
 
 struct GrpcChannelPool::Conn {
   int fd = -1;
+  std::unique_ptr<TlsConn> tls;  // TLS session on fd (https targets)
   nghttp2_session* s = nullptr;
   std::string authority;
   // the call in flight
@@ -123,11 +126,13 @@ struct GrpcChannelPool::Conn {
 
   ~Conn() {
     if (s) nghttp2_session_del(s);
+    tls.reset();
     if (fd >= 0) ::close(fd);
   }
 
   static ssize_t on_send(nghttp2_session*, const uint8_t* data, size_t len, int, void* user) {
     auto* c = static_cast<Conn*>(user);
+    if (c->tls) return c->tls->write_all(data, len, c->deadline) ? static_cast<ssize_t>(len) : NGHTTP2_ERR_CALLBACK_FAILURE;
     // the socket is non-blocking: wait for room until the call's deadline
     size_t done = 0;
     while (done < len) {
@@ -242,19 +247,28 @@ struct GrpcChannelPool::Conn {
       if (closed) return true;
       int ms = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count());
       if (ms <= 0) return false;
-      pollfd p{fd, POLLIN, 0};
-      int pr = ::poll(&p, 1, ms);
-      if (pr < 0 && errno == EINTR) continue;
-      if (pr <= 0) return false;
-      ssize_t n = ::recv(fd, buf.data(), buf.size(), 0);
-      if (n < 0 && (errno == EINTR || errno == EAGAIN)) continue;
+      if (!(tls && tls->pending())) {  // decrypted bytes already buffered need no poll
+        pollfd p{fd, POLLIN, 0};
+        int pr = ::poll(&p, 1, ms);
+        if (pr < 0 && errno == EINTR) continue;
+        if (pr <= 0) return false;
+      }
+      ssize_t n;
+      if (tls) {
+        n = static_cast<ssize_t>(tls->read(buf.data(), buf.size()));
+        if (n == 0) continue;  // the record is not complete yet
+      } else {
+        n = ::recv(fd, buf.data(), buf.size(), 0);
+        if (n < 0 && (errno == EINTR || errno == EAGAIN)) continue;
+      }
       if (n <= 0) return false;
       if (nghttp2_session_mem_recv(s, buf.data(), static_cast<size_t>(n)) < 0) return false;
     }
   }
 };
 
-GrpcChannelPool::GrpcChannelPool(int timeout_ms) : timeout_ms_(timeout_ms) {}
+GrpcChannelPool::GrpcChannelPool(int timeout_ms, std::shared_ptr<TlsContext> tls)
+    : timeout_ms_(timeout_ms), tls_(std::move(tls)) {}
 GrpcChannelPool::~GrpcChannelPool() = default;
 
 uint64_t GrpcChannelPool::connects() const {
@@ -277,7 +291,14 @@ std::unique_ptr<GrpcChannelPool::Conn> GrpcChannelPool::take(const std::string& 
   auto c = std::make_unique<Conn>();
   c->authority = strip_scheme(target);
   c->fd = connect_to(c->authority, timeout_ms, err);
-  if (c->fd < 0 || !c->init(err)) return nullptr;
+  if (c->fd < 0) return nullptr;
+  if (tls_) {
+    c->tls = std::make_unique<TlsConn>(tls_, c->fd);
+    std::string host = c->authority.substr(0, c->authority.rfind(':'));
+    if (host.size() > 1 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
+    if (!c->tls->handshake(host, Clock::now() + std::chrono::milliseconds(timeout_ms), err)) return nullptr;
+  }
+  if (!c->init(err)) return nullptr;
   return c;
 }
 
@@ -311,7 +332,8 @@ GrpcResult GrpcChannelPool::call(const std::string& target, const std::string& p
                            k_a = ":authority", k_ct = "content-type", v_ct = "application/grpc", k_te = "te",
                            v_te = "trailers", k_ua = "user-agent", v_ua = "dfs-native-client/1",
                            k_rid = "x-request-id";
-  std::vector<nghttp2_nv> h = {nv(k_m, v_m), nv(k_s, v_s), nv(k_p, path), nv(k_a, c->authority),
+  static const std::string v_https = "https";
+  std::vector<nghttp2_nv> h = {nv(k_m, v_m), nv(k_s, tls_ ? v_https : v_s), nv(k_p, path), nv(k_a, c->authority),
                                nv(k_ct, v_ct), nv(k_te, v_te), nv(k_ua, v_ua)};
   if (!request_id.empty()) h.push_back(nv(k_rid, request_id));
   nghttp2_data_provider dp;

@@ -1,4 +1,4 @@
-// Minimal native gRPC client: unary calls over HTTP/2 (h2c, prior knowledge) on nghttp2 —
+// Minimal native gRPC client: unary calls over HTTP/2 (h2c, or TLS + ALPN h2) on nghttp2 —
 // the client half of grpc_server.h, used by the native remote client (client_remote.h).
 //
 // One call owns one connection for its duration (connections are pooled per target and
@@ -16,6 +16,8 @@
 
 namespace dfs {
 
+class TlsContext;
+
 struct GrpcResult {
   bool transport_ok = false;  // false: connect / protocol / timeout failure (no status)
   int status = -1;            // grpc status code
@@ -24,7 +26,8 @@ struct GrpcResult {
 
 class GrpcChannelPool {
  public:
-  explicit GrpcChannelPool(int timeout_ms = 120000);
+  // `tls`: client TLS context (https targets, ALPN h2); nullptr = h2c.
+  explicit GrpcChannelPool(int timeout_ms = 120000, std::shared_ptr<TlsContext> tls = nullptr);
   ~GrpcChannelPool();
   GrpcChannelPool(const GrpcChannelPool&) = delete;
   GrpcChannelPool& operator=(const GrpcChannelPool&) = delete;
@@ -40,6 +43,7 @@ class GrpcChannelPool {
   void give(const std::string& target, std::unique_ptr<Conn> c);
 
   int timeout_ms_;
+  std::shared_ptr<TlsContext> tls_;
   mutable std::mutex mu_;
   std::map<std::string, std::vector<std::unique_ptr<Conn>>> idle_;
   uint64_t connects_ = 0;

@@ -11,9 +11,11 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cstring>
 #include <map>
 
+#include "tls.h"
 #include "trace.h"
 
 namespace dfs {
@@ -368,6 +370,31 @@ void GrpcServer::accept_loop() {
 }
 
 void GrpcServer::serve(int fd) {
+  std::unique_ptr<TlsConn> tc;
+  if (tls_) {
+    // bounded handshake on the blocking socket (a silent client must not pin this thread)
+    timeval tv{10, 0};
+    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    tc = std::make_unique<TlsConn>(tls_, fd);
+    std::string err;
+    if (!tc->handshake("", std::chrono::steady_clock::now() + std::chrono::seconds(10), &err)) {
+      tc.reset();
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto it = conns_.begin(); it != conns_.end(); ++it)
+        if (*it == fd) {
+          conns_.erase(it);
+          break;
+        }
+      ::close(fd);
+      if (--live_conns_ == 0) conns_cv_.notify_all();
+      return;
+    }
+    timeval none{0, 0};
+    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof none);
+    ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &none, sizeof none);
+  }
+  auto far = [] { return std::chrono::steady_clock::now() + std::chrono::hours(24); };
   auto c = std::make_shared<Conn>();
   c->srv = this;
   c->fd = fd;
@@ -398,15 +425,18 @@ void GrpcServer::serve(int fd) {
       ssize_t n = nghttp2_session_mem_send(c->session, &data);
       if (n < 0) return false;
       if (n == 0) return true;
-      if (!write_full(fd, data, static_cast<size_t>(n))) return false;
+      if (tc ? !tc->write_all(data, static_cast<size_t>(n), far()) : !write_full(fd, data, static_cast<size_t>(n)))
+        return false;
     }
   };
   ok = flush();
   while (ok && !stop_.load() && (nghttp2_session_want_read(c->session) || nghttp2_session_want_write(c->session))) {
     pollfd p[2] = {{fd, POLLIN, 0}, {c->efd, POLLIN, 0}};
-    if (::poll(p, 2, 500) < 0 && errno != EINTR) break;
-    if (p[0].revents & (POLLIN | POLLHUP | POLLERR)) {
-      ssize_t n = ::recv(fd, buf.data(), buf.size(), 0);
+    const bool buffered = tc && tc->pending();  // TLS records already decrypted: no poll
+    if (::poll(p, 2, buffered ? 0 : 500) < 0 && errno != EINTR) break;
+    if (buffered || (p[0].revents & (POLLIN | POLLHUP | POLLERR))) {
+      ssize_t n = tc ? static_cast<ssize_t>(tc->read(buf.data(), buf.size())) : ::recv(fd, buf.data(), buf.size(), 0);
+      if (tc && n == 0) continue;  // a record is still incomplete
       if (n <= 0) break;
       if (nghttp2_session_mem_recv(c->session, buf.data(), static_cast<size_t>(n)) < 0) break;
     }
@@ -422,6 +452,7 @@ void GrpcServer::serve(int fd) {
     }
     ok = flush();
   }
+  tc.reset();  // close_notify before the socket goes
   std::lock_guard<std::mutex> g(mu_);
   for (auto it = conns_.begin(); it != conns_.end(); ++it)
     if (*it == fd) {

@@ -1,4 +1,5 @@
-// Minimal native gRPC server: unary RPCs over HTTP/2 (h2c, prior knowledge) on nghttp2.
+// Minimal native gRPC server: unary RPCs over HTTP/2 on nghttp2 — h2c (prior knowledge), or
+// TLS with ALPN h2 when set_tls() is given the server's certificate (tls.h).
 //
 // grpc++ is not in this toolchain, nghttp2 is. The wire is plain gRPC —
 // HEADERS (:path /dfs.<Service>/<Method>, content-type application/grpc, te: trailers), one
@@ -24,6 +25,8 @@
 
 namespace dfs {
 
+class TlsContext;
+
 struct GrpcCall {
   std::string path;        // "/dfs.ChunkServerService/WriteBlock"
   std::string request_id;  // x-request-id metadata ("" if absent)
@@ -47,9 +50,12 @@ class GrpcServer {
   GrpcServer(std::string host, int port, Handler handler, int workers = 32);
   ~GrpcServer();
   GrpcServer(const GrpcServer&) = delete;
+  // Serve TLS (ALPN h2) instead of h2c; call before start().
+  void set_tls(std::shared_ptr<TlsContext> tls) { tls_ = std::move(tls); }
   bool start(std::string* err);
   void stop();
   int port() const { return port_; }
+  bool tls() const { return tls_ != nullptr; }
   uint64_t calls() const { return calls_.load(); }
 
  private:
@@ -73,6 +79,7 @@ class GrpcServer {
   int live_conns_ = 0;
   std::condition_variable conns_cv_;
   std::atomic<uint64_t> calls_{0};
+  std::shared_ptr<TlsContext> tls_;
 };
 
 }  // namespace dfs

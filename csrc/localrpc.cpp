@@ -95,6 +95,15 @@ void LocalRpcServer::accept_loop() {
       if (!running_) return;
       continue;
     }
+    // The abstract namespace has no file permissions: only processes of our own user (or
+    // root) may skip the network listener — which is what keeps a TLS deployment's metadata
+    // traffic off plaintext sockets for anyone else on the host.
+    ucred cred{};
+    socklen_t cl = sizeof(cred);
+    if (::getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cred, &cl) != 0 || (cred.uid != ::geteuid() && cred.uid != 0)) {
+      ::close(fd);
+      continue;
+    }
     std::lock_guard<std::mutex> g(mu_);
     if (!running_) {
       ::close(fd);

@@ -1,0 +1,1227 @@
+// Native S3 front end; design notes in s3_front.h.
+#include "s3_front.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cctype>
+#include <chrono>
+#include <cstring>
+#include <ctime>
+#include <future>
+#include <random>
+
+#include "dfs_pb.h"
+#include "sigv4.h"
+#include "trace.h"
+
+namespace dfs {
+
+namespace {
+
+constexpr size_t kMaxHead = 64 << 10;
+constexpr size_t kRelayChunk = 256 << 10;
+const char* kEmptyEtag = "\"d41d8cd98f00b204e9800998ecf8427e\"";
+const char* kUnsigned = "UNSIGNED-PAYLOAD";
+const char* kHidden[] = {".s3keep", ".s3_mpu_completed", ".meta", ".s3_bucket_policy"};
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+std::string lower(std::string s) {
+  for (auto& ch : s) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  return s;
+}
+
+std::string trim(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && std::isspace(static_cast<unsigned char>(s[a]))) ++a;
+  while (b > a && std::isspace(static_cast<unsigned char>(s[b - 1]))) --b;
+  return s.substr(a, b - a);
+}
+
+// " ".join(v.split()): the SigV4 canonical header value
+std::string collapse_ws(const std::string& v) {
+  std::string o;
+  bool sp = false;
+  for (char ch : v) {
+    if (std::isspace(static_cast<unsigned char>(ch))) {
+      sp = !o.empty();
+    } else {
+      if (sp) o.push_back(' ');
+      sp = false;
+      o.push_back(ch);
+    }
+  }
+  return o;
+}
+
+bool ends_with(const std::string& s, const char* suf) {
+  size_t n = std::strlen(suf);
+  return s.size() >= n && s.compare(s.size() - n, n, suf) == 0;
+}
+
+bool reserved_key(const std::string& key) {
+  for (const char* h : kHidden)
+    if (ends_with(key, h)) return true;
+  return false;
+}
+
+bool send_all(int fd, const void* p, size_t n) {
+  const auto* b = static_cast<const uint8_t*>(p);
+  while (n) {
+    ssize_t w = ::send(fd, b, n, MSG_NOSIGNAL);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return false;
+    b += w;
+    n -= static_cast<size_t>(w);
+  }
+  return true;
+}
+
+bool send_head_body(int fd, const std::string& head, const uint8_t* body, size_t n) {
+  if (n == 0 || n + head.size() <= (16 << 10)) {
+    if (n == 0) return send_all(fd, head.data(), head.size());
+    std::string all = head;
+    all.append(reinterpret_cast<const char*>(body), n);
+    return send_all(fd, all.data(), all.size());
+  }
+  iovec iv[2] = {{const_cast<char*>(head.data()), head.size()}, {const_cast<uint8_t*>(body), n}};
+  msghdr mh{};
+  mh.msg_iov = iv;
+  mh.msg_iovlen = 2;
+  ssize_t w;
+  do {
+    w = ::sendmsg(fd, &mh, MSG_NOSIGNAL);
+  } while (w < 0 && errno == EINTR);
+  if (w < 0) return false;
+  size_t done = static_cast<size_t>(w);
+  if (done < head.size()) {
+    if (!send_all(fd, head.data() + done, head.size() - done)) return false;
+    done = head.size();
+  }
+  size_t bo = done - head.size();
+  return send_all(fd, body + bo, n - bo);
+}
+
+std::string http_date(uint64_t ms) {
+  if (ms == 0) return "Wed, 01 Jan 2025 00:00:00 GMT";
+  time_t t = static_cast<time_t>(ms / 1000);
+  tm g{};
+  gmtime_r(&t, &g);
+  char b[64];
+  std::strftime(b, sizeof b, "%a, %d %b %Y %H:%M:%S GMT", &g);
+  return b;
+}
+
+std::string iso_now(double t, int64_t* ms_out) {
+  time_t s = static_cast<time_t>(t);
+  long us = static_cast<long>((t - static_cast<double>(s)) * 1e6);
+  tm g{};
+  gmtime_r(&s, &g);
+  char b[64];
+  std::strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%S", &g);
+  std::string o = b;
+  if (us) {
+    char u[16];
+    std::snprintf(u, sizeof u, ".%06ld", us);
+    o += u;
+  }
+  *ms_out = static_cast<int64_t>(t * 1000);
+  return o + "+00:00";
+}
+
+std::string json_str(const std::string& s) {
+  std::string o = "\"";
+  for (unsigned char ch : s) {
+    switch (ch) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (ch < 0x20) {
+          char u[8];
+          std::snprintf(u, sizeof u, "\\u%04x", ch);
+          o += u;
+        } else {
+          o.push_back(static_cast<char>(ch));
+        }
+    }
+  }
+  return o + "\"";
+}
+
+std::string uuid4() {
+  static thread_local std::mt19937_64 rng{std::random_device{}()};
+  uint64_t a = rng(), b = rng();
+  a = (a & 0xffffffffffff0fffull) | 0x4000ull;
+  b = (b & 0x3fffffffffffffffull) | 0x8000000000000000ull;
+  char s[40];
+  std::snprintf(s, sizeof s, "%08x-%04x-%04x-%04x-%012llx", static_cast<unsigned>(a >> 32),
+                static_cast<unsigned>((a >> 16) & 0xffff), static_cast<unsigned>(a & 0xffff),
+                static_cast<unsigned>(b >> 48), static_cast<unsigned long long>(b & 0xffffffffffffull));
+  return s;
+}
+
+bool all_digits(const std::string& s) {
+  if (s.empty() || s.size() > 18) return false;
+  for (char ch : s)
+    if (ch < '0' || ch > '9') return false;
+  return true;
+}
+
+// parse_range of s3/server.py: 0 = no (or ignored) range, 1 = [*s, *e], 2 = unsatisfiable,
+// 3 = a form this path does not decide (handed to Python)
+int parse_range(const std::string* v, uint64_t size, uint64_t* s, uint64_t* e) {
+  if (!v || v->compare(0, 6, "bytes=") != 0) return 0;
+  std::string spec = trim(v->substr(6));
+  if (spec.find(',') != std::string::npos || spec.find('-') == std::string::npos) return 0;
+  std::string a = spec.substr(0, spec.find('-')), b = spec.substr(spec.find('-') + 1);
+  if (a.empty()) {
+    if (!all_digits(b)) return 3;
+    uint64_t n = std::stoull(b);
+    if (n == 0 || size == 0) return 2;
+    *s = size > n ? size - n : 0;
+    *e = size - 1;
+    return 1;
+  }
+  if (!all_digits(a) || (!b.empty() && !all_digits(b))) return 3;
+  uint64_t start = std::stoull(a);
+  uint64_t end = b.empty() ? (size ? size - 1 : 0) : std::stoull(b);
+  if (start >= size) return 2;
+  end = std::min(end, size - 1);
+  if (end < start) return 0;
+  *s = start;
+  *e = end;
+  return 1;
+}
+
+// parse_qsl(keep_blank_values=True) for the keys this path looks at (no '%' or '+' handled:
+// such queries go to Python)
+bool simple_query(const std::string& q, std::map<std::string, std::string>* out) {
+  size_t i = 0;
+  while (i <= q.size() && !q.empty()) {
+    size_t amp = q.find('&', i);
+    std::string kv = q.substr(i, amp == std::string::npos ? std::string::npos : amp - i);
+    if (kv.find('%') != std::string::npos || kv.find('+') != std::string::npos) return false;
+    if (!kv.empty()) {
+      size_t eq = kv.find('=');
+      (*out)[kv.substr(0, eq)] = eq == std::string::npos ? "" : kv.substr(eq + 1);
+    }
+    if (amp == std::string::npos) break;
+    i = amp + 1;
+  }
+  return true;
+}
+
+}  // namespace
+
+struct S3Front::Conn {
+  int fd = -1;
+  std::string ip;
+  std::string buf;
+  size_t pos = 0;
+};
+
+struct S3Front::Req {
+  std::string method, target, raw_path, raw_query, version;
+  std::vector<std::pair<std::string, std::string>> headers;  // (lower-case name, value)
+  std::vector<std::string> names;                            // names as sent
+  bool keep_alive = true, chunked = false, expect_continue = false;
+  int64_t content_length = 0;
+  double started = 0;
+  std::string rid;
+  int status = 0;
+  const std::string* get(const char* lname) const {
+    for (auto& h : headers)
+      if (h.first == lname) return &h.second;
+    return nullptr;
+  }
+};
+
+S3Front::S3Front(S3FrontConfig cfg, FastClient* fc) : cfg_(std::move(cfg)), fc_(fc) {}
+
+S3Front::~S3Front() { stop(); }
+
+bool S3Front::start(std::string* err) {
+  lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+  int one = 1;
+  ::setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(cfg_.port));
+  if (cfg_.host.empty() || cfg_.host == "0.0.0.0") a.sin_addr.s_addr = INADDR_ANY;
+  else if (::inet_pton(AF_INET, cfg_.host == "localhost" ? "127.0.0.1" : cfg_.host.c_str(), &a.sin_addr) != 1) {
+    *err = "bad bind address " + cfg_.host;
+    return false;
+  }
+  if (::bind(lfd_, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0 || ::listen(lfd_, 1024) != 0) {
+    *err = std::string("bind/listen: ") + std::strerror(errno);
+    ::close(lfd_);
+    lfd_ = -1;
+    return false;
+  }
+  socklen_t al = sizeof a;
+  ::getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &al);
+  cfg_.port = ntohs(a.sin_port);
+  if (!cfg_.audit_socket.empty()) audit_fd_ = ::socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+  epfd_ = ::epoll_create1(EPOLL_CLOEXEC);
+  evfd_ = ::eventfd(0, EFD_CLOEXEC | EFD_NONBLOCK);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.u64 = 0;  // the listener
+  ::epoll_ctl(epfd_, EPOLL_CTL_ADD, lfd_, &ev);
+  ev.data.u64 = 1;  // stop
+  ::epoll_ctl(epfd_, EPOLL_CTL_ADD, evfd_, &ev);
+  for (int i = 0; i < std::max(1, cfg_.workers); ++i) workers_.emplace_back([this] { worker_loop(); });
+  epoller_ = std::thread([this] { epoll_loop(); });
+  return true;
+}
+
+void S3Front::stop() {
+  if (stop_.exchange(true)) return;
+  if (evfd_ >= 0) {
+    uint64_t one = 1;
+    (void)!::write(evfd_, &one, sizeof one);
+  }
+  if (epoller_.joinable()) epoller_.join();
+  {
+    std::lock_guard<std::mutex> g(conns_mu_);
+    for (auto& kv : conns_) ::shutdown(kv.first, SHUT_RDWR);
+  }
+  q_cv_.notify_all();
+  for (auto& t : workers_)
+    if (t.joinable()) t.join();
+  workers_.clear();
+  {
+    std::lock_guard<std::mutex> g(conns_mu_);
+    for (auto& kv : conns_) {
+      ::close(kv.first);
+      delete kv.second;
+    }
+    conns_.clear();
+  }
+  ready_.clear();  // the connections themselves were owned (and freed) through conns_
+  {
+    std::lock_guard<std::mutex> g(be_mu_);
+    for (int fd : be_idle_) ::close(fd);
+    be_idle_.clear();
+  }
+  for (int* fd : {&lfd_, &epfd_, &evfd_, &audit_fd_})
+    if (*fd >= 0) {
+      ::close(*fd);
+      *fd = -1;
+    }
+}
+
+S3FrontStats S3Front::stats() {
+  std::lock_guard<std::mutex> g(st_mu_);
+  return st_;
+}
+
+void S3Front::epoll_loop() {
+  epoll_event evs[64];
+  while (!stop_.load()) {
+    int n = ::epoll_wait(epfd_, evs, 64, 500);
+    for (int i = 0; i < n; ++i) {
+      if (evs[i].data.u64 == 1) return;
+      if (evs[i].data.u64 == 0) {
+        for (;;) {
+          sockaddr_in pa{};
+          socklen_t pl = sizeof pa;
+          int fd = ::accept4(lfd_, reinterpret_cast<sockaddr*>(&pa), &pl, SOCK_CLOEXEC);
+          if (fd < 0) break;
+          int one = 1;
+          ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          timeval tv{300, 0};
+          ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+          ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+          auto* c = new Conn();
+          c->fd = fd;
+          char ip[INET_ADDRSTRLEN] = "unknown";
+          ::inet_ntop(AF_INET, &pa.sin_addr, ip, sizeof ip);
+          c->ip = ip;
+          {
+            std::lock_guard<std::mutex> g(conns_mu_);
+            conns_[fd] = c;
+          }
+          {
+            std::lock_guard<std::mutex> g(st_mu_);
+            st_.connections++;
+          }
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP | EPOLLONESHOT;
+          ev.data.ptr = c;
+          ::epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
+        }
+        continue;
+      }
+      {
+        std::lock_guard<std::mutex> g(q_mu_);
+        ready_.push_back(static_cast<Conn*>(evs[i].data.ptr));
+      }
+      q_cv_.notify_one();
+    }
+  }
+}
+
+void S3Front::worker_loop() {
+  for (;;) {
+    Conn* c;
+    {
+      std::unique_lock<std::mutex> lk(q_mu_);
+      q_cv_.wait(lk, [this] { return stop_.load() || !ready_.empty(); });
+      if (stop_.load()) return;
+      c = ready_.front();
+      ready_.pop_front();
+    }
+    serve(c);
+  }
+}
+
+// ---------------------------------------------------------------- request loop
+void S3Front::serve(Conn* c) {
+  auto close_conn = [&] {
+    ::epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
+    std::lock_guard<std::mutex> g(conns_mu_);
+    conns_.erase(c->fd);
+    ::close(c->fd);
+    delete c;
+  };
+  char tmp[64 << 10];
+  for (;;) {
+    if (c->pos == c->buf.size()) {
+      c->buf.clear();
+      c->pos = 0;
+      ssize_t n = ::recv(c->fd, tmp, sizeof tmp, MSG_DONTWAIT);
+      if (n == 0 || (n < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)) return close_conn();
+      if (n < 0) {  // idle: back to the epoll thread
+        epoll_event ev{};
+        ev.events = EPOLLIN | EPOLLRDHUP | EPOLLONESHOT;
+        ev.data.ptr = c;
+        if (stop_.load() || ::epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev) != 0) return close_conn();
+        return;
+      }
+      c->buf.append(tmp, static_cast<size_t>(n));
+    }
+    size_t end;
+    while ((end = c->buf.find("\r\n\r\n", c->pos)) == std::string::npos) {
+      if (c->buf.size() - c->pos > kMaxHead) return close_conn();
+      ssize_t n = ::recv(c->fd, tmp, sizeof tmp, 0);
+      if (n <= 0) return close_conn();
+      c->buf.append(tmp, static_cast<size_t>(n));
+    }
+    Req r;
+    r.started = now_s();
+    const std::string head = c->buf.substr(c->pos, end - c->pos);
+    c->pos = end + 4;
+    size_t le = head.find("\r\n");
+    std::string line = head.substr(0, le);
+    size_t s1 = line.find(' '), s2 = line.rfind(' ');
+    if (s1 == std::string::npos || s2 == s1) return close_conn();
+    r.method = line.substr(0, s1);
+    r.target = line.substr(s1 + 1, s2 - s1 - 1);
+    r.version = line.substr(s2 + 1);
+    size_t q = r.target.find('?');
+    r.raw_path = r.target.substr(0, q);
+    r.raw_query = q == std::string::npos ? "" : r.target.substr(q + 1);
+    size_t p = le == std::string::npos ? head.size() : le + 2;
+    while (p < head.size()) {
+      size_t e = head.find("\r\n", p);
+      if (e == std::string::npos) e = head.size();
+      std::string h = head.substr(p, e - p);
+      size_t colon = h.find(':');
+      if (colon != std::string::npos) {
+        r.names.push_back(h.substr(0, colon));
+        r.headers.emplace_back(lower(h.substr(0, colon)), trim(h.substr(colon + 1)));
+      }
+      p = e + 2;
+    }
+    const std::string* conn = r.get("connection");
+    std::string cl = conn ? lower(*conn) : "";
+    r.keep_alive = r.version == "HTTP/1.1" ? cl.find("close") == std::string::npos
+                                             : cl.find("keep-alive") != std::string::npos;
+    if (const std::string* te = r.get("transfer-encoding")) r.chunked = lower(*te).find("chunked") != std::string::npos;
+    if (const std::string* len = r.get("content-length")) {
+      if (!all_digits(*len)) return close_conn();
+      r.content_length = static_cast<int64_t>(std::stoull(*len));
+    }
+    if (const std::string* ex = r.get("expect")) r.expect_continue = lower(*ex) == "100-continue";
+    const std::string* rid = r.get("x-request-id");
+    r.rid = rid ? *rid : std::string();
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.requests++;
+    }
+    if (!handle(c, r) || !r.keep_alive) return close_conn();
+  }
+}
+
+// Reads the request body (content_length bytes) into dst: buffered bytes first, then the
+// socket straight into the destination (a FastClient slot for PUTs).
+static bool read_body(S3Front::Conn* c, uint8_t* dst, uint64_t n);
+
+bool S3Front::handle(Conn* c, Req& r) {
+  // only plain paths are served here: a percent-escaped key goes to Python, whose URL
+  // decoding is the reference behaviour for it
+  const bool plain_path = r.raw_path.size() > 1 && r.raw_path[0] == '/' &&
+                          r.raw_path.find('%') == std::string::npos;
+  std::map<std::string, std::string> q;
+  if (!fc_ || !plain_path || !simple_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
+  std::string p = r.raw_path.substr(1);
+  size_t slash = p.find('/');
+  if (slash == std::string::npos || slash == 0 || slash + 1 >= p.size()) return proxy(c, r, nullptr, 0, "route");
+  const std::string bucket = p.substr(0, slash), key = p.substr(slash + 1);
+  if (reserved_key(key)) return proxy(c, r, nullptr, 0, "route");
+  q.erase("x-id");  // SDK operation tag, no meaning to S3 itself
+  const bool part = q.size() == 2 && q.count("partNumber") && q.count("uploadId");
+  if (!q.empty() && !part) return proxy(c, r, nullptr, 0, "query");
+  const bool is_put = r.method == "PUT", is_get = r.method == "GET", is_head = r.method == "HEAD";
+  if (!(is_put || ((is_get || is_head) && !part))) return proxy(c, r, nullptr, 0, "method");
+  if (cfg_.sse_enabled) return proxy(c, r, nullptr, 0, "sse");
+  if (is_put) {
+    if (r.chunked || r.get("x-amz-copy-source") || cfg_.metadata_sidecar) return proxy(c, r, nullptr, 0, "put-form");
+    const std::string* sha = r.get("x-amz-content-sha256");
+    const std::string* enc = r.get("content-encoding");
+    if ((sha && sha->compare(0, 10, "STREAMING-") == 0) || (enc && enc->find("aws-chunked") != std::string::npos))
+      return proxy(c, r, nullptr, 0, "aws-chunked");
+    if (static_cast<uint64_t>(r.content_length) > fc_->slot_bytes()) return proxy(c, r, nullptr, 0, "large");
+  } else if (r.content_length > 0 || r.chunked) {
+    return proxy(c, r, nullptr, 0, "body");
+  }
+  std::string user = "anonymous";
+  if (cfg_.auth_enabled) {
+    if (!verify_auth(r, &user)) return proxy(c, r, nullptr, 0, "auth");
+    if (bucket_has_policy(bucket)) return proxy(c, r, nullptr, 0, "bucket-policy");
+  }
+  std::string path = "/" + bucket + "/" + key;
+  bool ok;
+  if (is_put && part) {
+    const std::string& uid = q["uploadId"];
+    const std::string& pn = q["partNumber"];
+    if (uid.empty() || uid.find('/') != std::string::npos || uid == "." || uid == ".." || !all_digits(pn) ||
+        std::stoull(pn) < 1 || std::stoull(pn) > 10000)
+      return proxy(c, r, nullptr, 0, "part-args");
+    path = "/.s3_mpu/" + uid + "/" + std::to_string(std::stoull(pn));
+    ok = native_put(c, r, path, true);
+  } else if (is_put) {
+    ok = native_put(c, r, path, false);
+  } else {
+    ok = native_get(c, r, path, is_head);
+  }
+  if (r.status > 0 && cfg_.auth_enabled) audit(c, r, user, r.status);
+  return ok;
+}
+
+// ---------------------------------------------------------------- auth (static SigV4)
+int S3Front::verify_auth(Req& r, std::string* user) {
+  const std::string* auth = r.get("authorization");
+  if (!auth || auth->compare(0, 16, "AWS4-HMAC-SHA256") != 0) return 0;
+  if (r.get("x-amz-security-token")) return 0;  // STS sessions: IAM policy evaluation in Python
+  std::vector<std::string> parts;
+  size_t i = 0;
+  while (i <= auth->size()) {
+    size_t cm = auth->find(',', i);
+    parts.push_back(trim(auth->substr(i, cm == std::string::npos ? std::string::npos : cm - i)));
+    if (cm == std::string::npos) break;
+    i = cm + 1;
+  }
+  if (parts.size() < 3) return 0;
+  std::string cred;
+  {
+    size_t k = parts[0].find("Credential=");
+    if (k == std::string::npos) return 0;
+    cred = parts[0].substr(k + 11);
+    size_t sp = cred.find_first_of(" \t");
+    if (sp != std::string::npos) cred = cred.substr(0, sp);
+  }
+  std::vector<std::string> cp;
+  for (size_t a = 0;;) {
+    size_t b = cred.find('/', a);
+    cp.push_back(cred.substr(a, b == std::string::npos ? std::string::npos : b - a));
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  if (cp.size() < 5 || cp[4] != "aws4_request") return 0;
+  auto after_eq = [](const std::string& s) {
+    size_t e = s.find('=');
+    return e == std::string::npos ? std::string() : trim(s.substr(e + 1));
+  };
+  const std::string sh = after_eq(parts[1]), sig = after_eq(parts[2]);
+  const std::string* ts = r.get("x-amz-date");
+  if (!ts) ts = r.get("date");
+  if (!ts || sh.empty() || sig.empty()) return 0;
+  // %Y%m%dT%H%M%SZ within 15 minutes of now
+  tm t{};
+  if (ts->size() != 16 || !strptime(ts->c_str(), "%Y%m%dT%H%M%SZ", &t)) return 0;
+  double skew = std::abs(static_cast<double>(timegm(&t)) - now_s());
+  if (skew / 60.0 > 15.0) return 0;
+  const std::string &ak = cp[0], &date = cp[1], &region = cp[2], &service = cp[3];
+  if (region != cfg_.region || service != "s3") return 0;
+  if (cfg_.access_key.empty() || ak != cfg_.access_key) return 0;
+  std::string skey;
+  {
+    std::lock_guard<std::mutex> g(key_mu_);
+    auto it = key_cache_.find(date);
+    if (it != key_cache_.end()) skey = it->second;
+  }
+  if (skey.empty()) {
+    skey = sigv4::signing_key(cfg_.secret_key, date, region, service);
+    std::lock_guard<std::mutex> g(key_mu_);
+    if (key_cache_.size() > 8) key_cache_.clear();
+    key_cache_[date] = skey;
+  }
+  sigv4::Request sr;
+  sr.method = r.method;
+  sr.path = r.raw_path;
+  sr.query = sigv4::normalize_query(r.raw_query);
+  std::vector<std::string> names;
+  for (size_t a = 0;;) {
+    size_t b = sh.find(';', a);
+    std::string n = lower(trim(sh.substr(a, b == std::string::npos ? std::string::npos : b - a)));
+    if (!n.empty()) names.push_back(n);
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  std::sort(names.begin(), names.end());
+  names.erase(std::unique(names.begin(), names.end()), names.end());
+  std::string joined;
+  for (auto& n : names) {
+    std::string v;
+    bool first = true;
+    for (auto& h : r.headers)
+      if (h.first == n) {
+        if (!first) v += ",";
+        v += collapse_ws(h.second);
+        first = false;
+      }
+    sr.headers.emplace_back(n, v);
+    joined += (joined.empty() ? "" : ";") + n;
+  }
+  sr.signed_headers = joined;
+  const std::string* ph = r.get("x-amz-content-sha256");
+  sr.payload_hash = ph && !ph->empty() ? *ph : kUnsigned;
+  if (sr.payload_hash == kUnsigned && !cfg_.allow_unsigned_payload) return 0;
+  const std::string scope = date + "/" + region + "/" + service + "/aws4_request";
+  std::string creq;
+  if (!sigv4::verify(sr, *ts, scope, skey, sig, &creq)) return 0;
+  *user = ak;
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.auth_native++;
+  return 1;
+}
+
+bool S3Front::bucket_has_policy(const std::string& bucket) {
+  const double now = now_s();
+  {
+    std::lock_guard<std::mutex> g(pol_mu_);
+    auto it = policy_cache_.find(bucket);
+    if (it != policy_cache_.end() && it->second.first > now) return it->second.second;
+  }
+  bool found = true;  // unknown: treat as "has a policy" (Python decides)
+  std::string meta, msg;
+  if (fc_->stat("/" + bucket + "/.s3_bucket_policy", &found, &meta, &msg, "") != FastClient::Ok) found = true;
+  std::lock_guard<std::mutex> g(pol_mu_);
+  policy_cache_[bucket] = {now + 1.0, found};  // the gateway's 1 s policy cache
+  return found;
+}
+
+void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int status) {
+  if (audit_fd_ < 0) return;
+  std::string path = r.raw_path;
+  std::vector<std::string> segs;
+  for (size_t a = 0; a < path.size();) {
+    size_t b = path.find('/', a);
+    std::string s = path.substr(a, b == std::string::npos ? std::string::npos : b - a);
+    if (!s.empty()) segs.push_back(s);
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  std::string resource = "arn:dfs:s3:::";
+  for (size_t i = 0; i < segs.size(); ++i) resource += (i ? "/" : "") + segs[i];
+  std::string action = r.method == "GET" ? "s3:GetObject" : r.method == "HEAD" ? "s3:HeadObject" : "s3:PutObject";
+  const double t = now_s();
+  int64_t ms;
+  std::string ts = iso_now(t, &ms);
+  const std::string* ua = r.get("user-agent");
+  std::string rec = "{\"timestamp\":" + json_str(ts) + ",\"timestamp_ms\":" + std::to_string(ms) +
+                    ",\"request_id\":" + json_str(r.rid.empty() ? uuid4() : r.rid) +
+                    ",\"remote_ip\":" + json_str(c->ip) + ",\"user_id\":" + json_str(user) +
+                    ",\"role_arn\":null,\"action\":" + json_str(action) + ",\"resource\":" + json_str(resource) +
+                    ",\"status_code\":" + std::to_string(status) + ",\"error_code\":null,\"user_agent\":" +
+                    (ua ? json_str(*ua) : std::string("null")) +
+                    ",\"duration_ms\":" + std::to_string(static_cast<int64_t>((t - r.started) * 1000)) +
+                    ",\"previous_hash\":null,\"record_hash\":null}";
+  sockaddr_un sa{};
+  sa.sun_family = AF_UNIX;
+  std::snprintf(sa.sun_path, sizeof sa.sun_path, "%s", cfg_.audit_socket.c_str());
+  bool ok = ::sendto(audit_fd_, rec.data(), rec.size(), 0, reinterpret_cast<sockaddr*>(&sa), sizeof sa) ==
+            static_cast<ssize_t>(rec.size());
+  std::lock_guard<std::mutex> g(st_mu_);
+  (ok ? st_.audit_sent : st_.audit_dropped)++;
+}
+
+void S3Front::count(const Req& r, int status) {
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.native++;
+  st_.by_status[r.method + " " + std::to_string(status)]++;
+}
+
+void S3Front::note_proxy(const std::string& why) {
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.proxied++;
+  st_.proxy_reasons[why]++;
+}
+
+// ---------------------------------------------------------------- native object ops
+static bool read_body(S3Front::Conn* c, uint8_t* dst, uint64_t n) {
+  uint64_t have = std::min<uint64_t>(n, c->buf.size() - c->pos);
+  if (have) std::memcpy(dst, c->buf.data() + c->pos, have);
+  c->pos += have;
+  uint64_t got = have;
+  while (got < n) {
+    ssize_t k = ::recv(c->fd, dst + got, n - got, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    got += static_cast<uint64_t>(k);
+  }
+  return true;
+}
+
+bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
+  TraceRange tr(part ? "dfs.s3.upload_part" : "dfs.s3.put");
+  if (part) {  // the upload must exist before its body is accepted (NoSuchUpload from Python)
+    const std::string marker = path.substr(0, path.rfind('/')) + "/.s3keep";
+    bool found = false;
+    std::string meta, msg;
+    if (fc_->stat(marker, &found, &meta, &msg, r.rid) != FastClient::Ok || !found)
+      return proxy(c, r, nullptr, 0, "no-upload");
+  }
+  const uint64_t n = static_cast<uint64_t>(r.content_length);
+  int64_t slot = fc_->acquire_slot(std::max<uint64_t>(n, 1));
+  if (slot < 0) return proxy(c, r, nullptr, 0, "no-slot");
+  struct Release {
+    FastClient* fc;
+    int64_t s;
+    ~Release() { fc->release(s); }
+  } rel{fc_, slot};
+  if (r.expect_continue && !send_all(c->fd, "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+  uint8_t* dst = fc_->slot_mut(slot);
+  if (!read_body(c, dst, n)) return false;
+  std::map<std::string, std::string> attrs;
+  if (!part) {
+    // put_object: ETag, x-amz-meta-* (lower-cased) and Content-Type become the attributes
+    for (auto& h : r.headers)
+      if (h.first.compare(0, 11, "x-amz-meta-") == 0) attrs[h.first] = h.second;
+    if (const std::string* ct = r.get("content-type")) attrs["Content-Type"] = *ct;
+    attrs["ETag"] = "";
+  }
+  FastClient::Times t;
+  std::string msg, md5;
+  int reps = 0;
+  auto st = fc_->write_slot(path, slot, n, &reps, &msg, &t, r.rid, part ? nullptr : &attrs, part ? nullptr : "ETag",
+                            &md5);
+  if (st == FastClient::Failed && msg.find("already exists") != std::string::npos) {
+    // _put_replace: an existing key is replaced (delete, then create again)
+    std::string dmsg;
+    if (fc_->remove(path, &dmsg, r.rid) != FastClient::NotHandled)
+      st = fc_->write_slot(path, slot, n, &reps, &msg, &t, r.rid, part ? nullptr : &attrs, part ? nullptr : "ETag",
+                           &md5);
+  }
+  if (st != FastClient::Ok) return proxy(c, r, dst, n, "put-fallback");
+  std::string head = "HTTP/1.1 200 OK\r\nETag: \"" + md5 + "\"\r\nContent-Length: 0\r\n";
+  head += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
+  r.status = 200;
+  count(r, 200);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    (part ? st_.parts : st_.puts)++;
+    st_.bytes_in += n;
+  }
+  return send_all(c->fd, head.data(), head.size());
+}
+
+namespace {
+
+// _object_headers of s3/server.py; false: a case Python owns (SSE, sidecar metadata)
+bool object_headers(const pb::FileMetadata* m, const std::map<std::string, std::string>& attrs, std::string* out) {
+  std::string etag = m && !m->etag_md5.empty() ? "\"" + m->etag_md5 + "\"" : kEmptyEtag;
+  std::string h = "Last-Modified: " + http_date(m ? m->created_at_ms : 0) + "\r\nAccept-Ranges: bytes\r\n";
+  bool ctype = false;
+  for (auto& kv : attrs) {
+    if (kv.first == "ETag") {
+      etag = kv.second;
+    } else if (kv.first == "x-amz-sse-encrypted-dek") {
+      return false;
+    } else if (kv.first.compare(0, 11, "x-amz-meta-") == 0 || kv.first == "Content-Type") {
+      if (kv.second.find_first_of("\r\n") != std::string::npos) return false;
+      h += kv.first + ": " + kv.second + "\r\n";
+      ctype |= kv.first == "Content-Type";
+    }
+  }
+  h += "ETag: " + etag + "\r\n";
+  if (!ctype) h += "Content-Type: application/octet-stream\r\n";
+  *out = h;
+  return true;
+}
+
+}  // namespace
+
+bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
+  TraceRange tr(head ? "dfs.s3.head" : "dfs.s3.get");
+  bool found = false;
+  std::string meta, msg;
+  if (fc_->stat(path, &found, &meta, &msg, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "stat");
+  if (!found) {
+    if (head) return proxy(c, r, nullptr, 0, "head-missing");
+    std::string mm;
+    if (fc_->stat(path + "/.s3_mpu_completed", &found, &mm, &msg, r.rid) != FastClient::Ok || !found)
+      return proxy(c, r, nullptr, 0, "missing");
+    return native_mpu_get(c, r, path, mm);
+  }
+  pb::FileMetadata m;
+  if (!m.decode(meta)) return proxy(c, r, nullptr, 0, "decode");
+  std::string hdrs;
+  if (m.attributes.empty() || !object_headers(&m, m.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
+  const std::string ka = r.keep_alive ? "Connection: keep-alive\r\n" : "Connection: close\r\n";
+  if (head) {
+    std::string h = "HTTP/1.1 200 OK\r\n" + hdrs + "Content-Length: " + std::to_string(m.size) + "\r\n" + ka + "\r\n";
+    r.status = 200;
+    count(r, 200);
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.heads++;
+    }
+    return send_all(c->fd, h.data(), h.size());
+  }
+  uint64_t s = 0, e = 0;
+  int rng = parse_range(r.get("range"), m.size, &s, &e);
+  if (rng >= 2) return proxy(c, r, nullptr, 0, "range");
+  int64_t slot = -1;
+  uint64_t got = 0;
+  FastClient::Times t;
+  if (m.size > 0) {
+    auto st = fc_->read_known(meta, &slot, &got, &msg, &t, r.rid, rng == 1 ? s : 0, rng == 1 ? e - s + 1 : 0);
+    if (st != FastClient::Ok) return proxy(c, r, nullptr, 0, "read");
+  }
+  struct Release {
+    FastClient* fc;
+    int64_t s;
+    ~Release() {
+      if (s >= 0) fc->release(s);
+    }
+  } rel{fc_, slot};
+  const uint64_t want = rng == 1 ? e - s + 1 : m.size;
+  if (got != want) return proxy(c, r, nullptr, 0, "short-read");
+  std::string h;
+  if (rng == 1) {
+    h = "HTTP/1.1 206 Partial Content\r\n" + hdrs + "Content-Range: bytes " + std::to_string(s) + "-" +
+        std::to_string(e) + "/" + std::to_string(m.size) + "\r\n";
+    r.status = 206;
+  } else {
+    h = "HTTP/1.1 200 OK\r\n" + hdrs;
+    r.status = 200;
+  }
+  h += "Content-Length: " + std::to_string(got) + "\r\n" + ka + "\r\n";
+  count(r, r.status);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    (rng == 1 ? st_.range_gets : st_.gets)++;
+    st_.bytes_out += got;
+  }
+  return send_head_body(c->fd, h, got ? fc_->slot_ptr(slot) : nullptr, got);
+}
+
+// GET of a completed multipart object: the parts' sizes come from the layout the completion
+// recorded (x-dfs-mpu-layout), every part overlapping the range is checked first (so a
+// missing part still turns into Python's answer), then the parts stream out in order while
+// the next one is already being read.
+bool S3Front::native_mpu_get(Conn* c, Req& r, const std::string& path, const std::string& marker_meta) {
+  TraceRange tr("dfs.s3.mpu_get");
+  pb::FileMetadata mk;
+  if (!mk.decode(marker_meta)) return proxy(c, r, nullptr, 0, "decode");
+  auto lay = mk.attributes.find("x-dfs-mpu-layout");
+  if (lay == mk.attributes.end()) return proxy(c, r, nullptr, 0, "mpu-layout");
+  std::vector<std::pair<uint64_t, uint64_t>> parts;  // (number, size)
+  for (size_t a = 0; a < lay->second.size();) {
+    size_t b = lay->second.find(',', a);
+    std::string kv = lay->second.substr(a, b == std::string::npos ? std::string::npos : b - a);
+    size_t colon = kv.find(':');
+    if (colon == std::string::npos || !all_digits(kv.substr(0, colon)) || !all_digits(kv.substr(colon + 1)))
+      return proxy(c, r, nullptr, 0, "mpu-layout");
+    parts.emplace_back(std::stoull(kv.substr(0, colon)), std::stoull(kv.substr(colon + 1)));
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  std::string hdrs;
+  if (!object_headers(nullptr, mk.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
+  uint64_t total = 0;
+  for (auto& p : parts) total += p.second;
+  uint64_t s = 0, e = total ? total - 1 : 0;
+  int rng = parse_range(r.get("range"), total, &s, &e);
+  if (rng >= 2 || total == 0) return proxy(c, r, nullptr, 0, "mpu-range");
+  if (rng == 0) {
+    s = 0;
+    e = total - 1;
+  }
+  struct Piece {
+    std::string meta;
+    uint64_t off, len;
+    bool whole;
+  };
+  std::vector<Piece> pieces;
+  uint64_t pos = 0;
+  for (auto& p : parts) {
+    uint64_t lo = std::max(s, pos), hi = std::min(e + 1, pos + p.second);
+    if (lo < hi) {
+      bool found = false;
+      std::string pm, msg;
+      if (fc_->stat(path + "/" + std::to_string(p.first), &found, &pm, &msg, r.rid) != FastClient::Ok || !found)
+        return proxy(c, r, nullptr, 0, "mpu-part");
+      pb::FileMetadata m;
+      if (!m.decode(pm) || m.size != p.second) return proxy(c, r, nullptr, 0, "mpu-part");
+      pieces.push_back({pm, lo - pos, hi - lo, lo == pos && hi == pos + p.second});
+    }
+    pos += p.second;
+  }
+  const std::string ka = r.keep_alive ? "Connection: keep-alive\r\n" : "Connection: close\r\n";
+  std::string h;
+  const uint64_t len = e - s + 1;
+  if (rng == 1) {
+    h = "HTTP/1.1 206 Partial Content\r\n" + hdrs + "Content-Range: bytes " + std::to_string(s) + "-" +
+        std::to_string(e) + "/" + std::to_string(total) + "\r\n";
+    r.status = 206;
+  } else {
+    h = "HTTP/1.1 200 OK\r\n" + hdrs;
+    r.status = 200;
+  }
+  h += "Content-Length: " + std::to_string(len) + "\r\n" + ka + "\r\n";
+  struct Got {
+    int64_t slot = -1;
+    uint64_t n = 0;
+    bool ok = false;
+  };
+  auto fetch = [this, &r](const Piece& pc) {
+    Got g;
+    std::string msg;
+    FastClient::Times t;
+    g.ok = fc_->read_known(pc.meta, &g.slot, &g.n, &msg, &t, r.rid, pc.whole ? 0 : pc.off, pc.whole ? 0 : pc.len) ==
+               FastClient::Ok &&
+           g.n == pc.len;
+    return g;
+  };
+  // the first part is read before the head goes out, so an unreadable object is still
+  // answered by Python; later failures can only cut the connection
+  std::deque<std::future<Got>> inflight;
+  size_t next = 0;
+  const size_t window = 3;
+  while (next < pieces.size() && inflight.size() < window) {
+    const Piece* pc = &pieces[next++];
+    inflight.push_back(pool_.submit([fetch, pc] { return fetch(*pc); }));
+  }
+  bool sent_head = false, ok = true;
+  while (!inflight.empty()) {
+    Got g = inflight.front().get();
+    inflight.pop_front();
+    if (ok && next < pieces.size()) {
+      const Piece* pc = &pieces[next++];
+      inflight.push_back(pool_.submit([fetch, pc] { return fetch(*pc); }));
+    }
+    if (!g.ok || !ok) {
+      if (g.slot >= 0) fc_->release(g.slot);
+      if (!sent_head && ok) {
+        ok = false;
+        for (auto& f : inflight) {  // drain before handing the request over
+          Got x = f.get();
+          if (x.slot >= 0) fc_->release(x.slot);
+        }
+        inflight.clear();
+        return proxy(c, r, nullptr, 0, "mpu-read");
+      }
+      ok = false;
+      continue;
+    }
+    bool w = sent_head ? send_all(c->fd, fc_->slot_ptr(g.slot), g.n)
+                       : send_head_body(c->fd, h, fc_->slot_ptr(g.slot), g.n);
+    sent_head = true;
+    fc_->release(g.slot);
+    if (!w) ok = false;
+  }
+  if (!ok) return false;
+  count(r, r.status);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.mpu_gets++;
+    st_.bytes_out += len;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- hand-off to Python
+int S3Front::backend_conn() {
+  {
+    std::lock_guard<std::mutex> g(be_mu_);
+    if (!be_idle_.empty()) {
+      int fd = be_idle_.back();
+      be_idle_.pop_back();
+      return fd;
+    }
+  }
+  int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd < 0) return -1;
+  sockaddr_un sa{};
+  sa.sun_family = AF_UNIX;
+  std::snprintf(sa.sun_path, sizeof sa.sun_path, "%s", cfg_.backend.c_str());
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
+    ::close(fd);
+    return -1;
+  }
+  timeval tv{300, 0};
+  ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+  return fd;
+}
+
+void S3Front::backend_done(int fd, bool reuse) {
+  if (!reuse) {
+    ::close(fd);
+    return;
+  }
+  std::lock_guard<std::mutex> g(be_mu_);
+  be_idle_.push_back(fd);
+}
+
+namespace {
+
+// Copies one HTTP/1.1 chunked body from `src` (with `buf` holding bytes already read past
+// `*pos`) to `dst`, raw. Returns false on any I/O or framing error.
+bool relay_chunked(int src, std::string& buf, size_t* pos, int dst) {
+  auto need = [&](size_t k) {
+    char tmp[kRelayChunk];
+    while (buf.size() - *pos < k) {
+      ssize_t n = ::recv(src, tmp, sizeof tmp, 0);
+      if (n <= 0) return false;
+      buf.append(tmp, static_cast<size_t>(n));
+    }
+    return true;
+  };
+  auto line = [&](std::string* out) {
+    size_t e;
+    while ((e = buf.find("\r\n", *pos)) == std::string::npos) {
+      if (buf.size() - *pos > 8192 || !need(buf.size() - *pos + 1)) return false;
+    }
+    *out = buf.substr(*pos, e - *pos);
+    if (!send_all(dst, buf.data() + *pos, e + 2 - *pos)) return false;
+    *pos = e + 2;
+    return true;
+  };
+  for (;;) {
+    std::string l;
+    if (!line(&l)) return false;
+    size_t semi = l.find(';');
+    std::string hex = trim(l.substr(0, semi));
+    if (hex.empty() || hex.size() > 15) return false;
+    uint64_t n = std::stoull(hex, nullptr, 16);
+    if (n == 0) {
+      for (;;) {  // trailers, then the empty line
+        std::string t;
+        if (!line(&t)) return false;
+        if (t.empty()) return true;
+      }
+    }
+    uint64_t left = n + 2;
+    while (left) {
+      if (*pos == buf.size()) {
+        buf.clear();
+        *pos = 0;
+        if (!need(1)) return false;
+      }
+      size_t k = std::min<uint64_t>(left, buf.size() - *pos);
+      if (!send_all(dst, buf.data() + *pos, k)) return false;
+      *pos += k;
+      left -= k;
+    }
+  }
+}
+
+bool relay_n(int src, std::string& buf, size_t* pos, int dst, uint64_t n) {
+  uint64_t have = std::min<uint64_t>(n, buf.size() - *pos);
+  if (have && !send_all(dst, buf.data() + *pos, have)) return false;
+  *pos += have;
+  n -= have;
+  std::vector<char> tmp(kRelayChunk);
+  while (n) {
+    ssize_t k = ::recv(src, tmp.data(), std::min<uint64_t>(n, tmp.size()), 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0 || !send_all(dst, tmp.data(), static_cast<size_t>(k))) return false;
+    n -= static_cast<uint64_t>(k);
+  }
+  return true;
+}
+
+}  // namespace
+
+static bool read_body_fd(int fd, char* dst, uint64_t n) {
+  uint64_t got = 0;
+  while (got < n) {
+    ssize_t k = ::recv(fd, dst + got, n - got, 0);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return false;
+    got += static_cast<uint64_t>(k);
+  }
+  return true;
+}
+
+std::string S3Front::native_metrics() {
+  S3FrontStats s = stats();
+  std::string o = "# HELP s3_native_requests_total S3 requests served by the native front end\n"
+                  "# TYPE s3_native_requests_total counter\n";
+  for (auto& kv : s.by_status) {
+    size_t sp = kv.first.find(' ');
+    o += "s3_native_requests_total{method=\"" + kv.first.substr(0, sp) + "\",status=\"" + kv.first.substr(sp + 1) +
+         "\"} " + std::to_string(kv.second) + "\n";
+  }
+  o += "# HELP s3_native_handoffs_total S3 requests handed to the Python gateway, by reason\n"
+       "# TYPE s3_native_handoffs_total counter\n";
+  for (auto& kv : s.proxy_reasons)
+    o += "s3_native_handoffs_total{reason=\"" + kv.first + "\"} " + std::to_string(kv.second) + "\n";
+  o += "# TYPE s3_native_bytes_in_total counter\ns3_native_bytes_in_total " + std::to_string(s.bytes_in) + "\n";
+  o += "# TYPE s3_native_bytes_out_total counter\ns3_native_bytes_out_total " + std::to_string(s.bytes_out) + "\n";
+  return o;
+}
+
+bool S3Front::proxy(Conn* c, Req& r, const uint8_t* body, uint64_t body_len, const std::string& why) {
+  note_proxy(why);
+  int be = backend_conn();
+  auto bad_gateway = [&] {
+    const char* m = "HTTP/1.1 502 Bad Gateway\r\nContent-Length: 0\r\nConnection: close\r\n\r\n";
+    send_all(c->fd, m, std::strlen(m));
+    return false;
+  };
+  if (be < 0) return bad_gateway();
+  std::string head = r.method + " " + r.target + " HTTP/1.1\r\n";
+  for (size_t i = 0; i < r.headers.size(); ++i) {
+    const std::string& n = r.headers[i].first;
+    if (n == "connection" || n == "keep-alive" || n == "expect" || n == "proxy-connection" || n == "x-real-ip" ||
+        n == "x-forwarded-for")
+      continue;
+    head += r.names[i] + ": " + r.headers[i].second + "\r\n";
+  }
+  head += "X-Real-IP: " + c->ip + "\r\nX-Forwarded-For: " + c->ip + "\r\nConnection: keep-alive\r\n\r\n";
+  if (!body && r.expect_continue && (r.content_length > 0 || r.chunked) &&
+      !send_all(c->fd, "HTTP/1.1 100 Continue\r\n\r\n", 25)) {
+    backend_done(be, false);
+    return false;
+  }
+  bool ok = send_all(be, head.data(), head.size());
+  if (ok && body) ok = send_all(be, body, body_len);
+  else if (ok && r.chunked) ok = relay_chunked(c->fd, c->buf, &c->pos, be);
+  else if (ok && r.content_length > 0) ok = relay_n(c->fd, c->buf, &c->pos, be, static_cast<uint64_t>(r.content_length));
+  if (!ok) {
+    backend_done(be, false);
+    return false;
+  }
+  // the response head
+  std::string rb;
+  size_t rp = 0, end;
+  char tmp[16 << 10];
+  while ((end = rb.find("\r\n\r\n")) == std::string::npos) {
+    if (rb.size() > kMaxHead) {
+      backend_done(be, false);
+      return bad_gateway();
+    }
+    ssize_t n = ::recv(be, tmp, sizeof tmp, 0);
+    if (n <= 0) {
+      backend_done(be, false);
+      return bad_gateway();
+    }
+    rb.append(tmp, static_cast<size_t>(n));
+  }
+  std::string rh = rb.substr(0, end);
+  rp = end + 4;
+  size_t le = rh.find("\r\n");
+  std::string status_line = rh.substr(0, le);
+  int status = 0;
+  {
+    size_t sp = status_line.find(' ');
+    if (sp != std::string::npos) status = std::atoi(status_line.c_str() + sp + 1);
+  }
+  std::string out = status_line + "\r\n";
+  int64_t clen = -1;
+  bool chunked = false, be_close = false;
+  for (size_t p = le == std::string::npos ? rh.size() : le + 2; p < rh.size();) {
+    size_t e = rh.find("\r\n", p);
+    if (e == std::string::npos) e = rh.size();
+    std::string h = rh.substr(p, e - p);
+    p = e + 2;
+    size_t colon = h.find(':');
+    if (colon == std::string::npos) continue;
+    std::string n = lower(h.substr(0, colon)), v = trim(h.substr(colon + 1));
+    if (n == "connection") {
+      be_close = lower(v).find("close") != std::string::npos;
+      continue;
+    }
+    if (n == "keep-alive") continue;
+    if (n == "content-length" && all_digits(v)) clen = static_cast<int64_t>(std::stoull(v));
+    if (n == "transfer-encoding" && lower(v).find("chunked") != std::string::npos) chunked = true;
+    out += h + "\r\n";
+  }
+  const bool no_body = r.method == "HEAD" || status == 204 || status == 304 || (status >= 100 && status < 200);
+  if (r.method == "GET" && r.raw_path == "/metrics" && status == 200 && !chunked && clen >= 0) {
+    // the Python workers render their registry; the front appends its own counters
+    std::string text(static_cast<size_t>(clen), '\0');
+    uint64_t have = std::min<uint64_t>(clen, rb.size() - rp);
+    std::memcpy(text.data(), rb.data() + rp, have);
+    rp += have;
+    if (have < static_cast<uint64_t>(clen) && !read_body_fd(be, text.data() + have, clen - have)) {
+      backend_done(be, false);
+      return bad_gateway();
+    }
+    text += native_metrics();
+    std::string o2;
+    for (size_t p = 0; p < out.size();) {  // drop the old Content-Length
+      size_t e = out.find("\r\n", p);
+      std::string h = out.substr(p, e - p);
+      if (lower(h).compare(0, 15, "content-length:") != 0) o2 += h + "\r\n";
+      p = e + 2;
+    }
+    o2 += "Content-Length: " + std::to_string(text.size()) + "\r\n";
+    o2 += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
+    r.status = status;
+    backend_done(be, !be_close && rp == rb.size());
+    return send_head_body(c->fd, o2, reinterpret_cast<const uint8_t*>(text.data()), text.size());
+  }
+  const bool until_close = !no_body && !chunked && clen < 0;
+  if (until_close) r.keep_alive = false;
+  out += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
+  r.status = status;
+  ok = send_all(c->fd, out.data(), out.size());
+  if (ok && !no_body) {
+    if (chunked) {
+      ok = relay_chunked(be, rb, &rp, c->fd);
+    } else if (clen > 0) {
+      ok = relay_n(be, rb, &rp, c->fd, static_cast<uint64_t>(clen));
+    } else if (until_close) {
+      if (rp < rb.size()) ok = send_all(c->fd, rb.data() + rp, rb.size() - rp);
+      ssize_t n;
+      while (ok && (n = ::recv(be, tmp, sizeof tmp, 0)) > 0) ok = send_all(c->fd, tmp, static_cast<size_t>(n));
+      be_close = true;
+    }
+  }
+  backend_done(be, ok && !be_close && rp == rb.size());
+  return ok;
+}
+
+}  // namespace dfs

@@ -1,0 +1,119 @@
+// Native S3 front end: the HTTP/1.1 listener of the S3 gateway (C52-C54 data path; reference
+// dfs/s3_server/src/main.rs:243-256 router, handlers.rs:918-1365 object handlers,
+// auth_middleware.rs:19-365 SigV4).
+//
+// The hot object operations run here in C++, with no interpreter on the path:
+//   PUT object, UploadPart  -> body read from the socket straight into a FastClient slot
+//                              (the /dev/shm arena the co-located chunkserver has pinned for
+//                              its copy engines), CRC + MD5 in C++, then the native write
+//                              (CreateFile -> fast path -> HBM -> CompleteFile with the
+//                              object headers as attributes);
+//   GET / HEAD / Range GET  -> GetFileInfo, then the chunkserver's fused verify+copy kernel
+//                              lands the (range of the) block in a slot that is written to
+//                              the socket as is; multipart objects are streamed part by
+//                              part from the layout recorded at completion.
+// Everything else — buckets, listings, policies, STS, copy, multi-delete, MPU initiate /
+// complete / abort, SSE-encrypted objects, presigned or STS-signed requests, buckets with a
+// policy, any case this path does not own — is handed, unchanged, to the Python gateway
+// (aiohttp on a private UNIX socket, s3/server.py), which keeps the reference semantics.
+// Signed requests are verified here with csrc/sigv4.cpp (static credentials); anything
+// that does not verify is handed over too, so Python produces the exact error and audit
+// record. Native requests of an authenticated gateway send their audit record to the
+// gateway's audit store over the same datagram socket the Python workers use, so one hash
+// chain covers both.
+//
+// Concurrency: one epoll thread accepts and watches idle keep-alive connections
+// (EPOLLONESHOT); a ready connection is handed to a worker thread, which serves its
+// requests with blocking I/O (the DFS calls block) and re-arms it when it goes idle.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "client_fast.h"
+#include "io_pool.h"
+
+namespace dfs {
+
+struct S3FrontConfig {
+  std::string host = "0.0.0.0";
+  int port = 9000;
+  std::string backend;  // UNIX socket path of the Python gateway
+  int workers = 32;
+  bool auth_enabled = false;
+  std::string region = "us-east-1";
+  std::string access_key, secret_key;  // EnvCredentialProvider (S3_ACCESS_KEY / S3_SECRET_KEY)
+  bool allow_unsigned_payload = true;
+  std::string audit_socket;  // datagram socket of the audit store ("" = no audit)
+  bool sse_enabled = false;  // objects are encrypted: their data stays on the Python path
+  bool metadata_sidecar = false;
+};
+
+struct S3FrontStats {
+  uint64_t connections = 0, requests = 0, native = 0, proxied = 0;
+  uint64_t puts = 0, parts = 0, gets = 0, range_gets = 0, heads = 0, mpu_gets = 0;
+  uint64_t bytes_in = 0, bytes_out = 0, auth_native = 0, audit_sent = 0, audit_dropped = 0;
+  std::map<std::string, uint64_t> by_status;  // "METHOD status" -> count (native requests)
+  std::map<std::string, uint64_t> proxy_reasons;
+};
+
+class S3Front {
+ public:
+  S3Front(S3FrontConfig cfg, FastClient* fc);
+  ~S3Front();
+  S3Front(const S3Front&) = delete;
+  bool start(std::string* err);
+  void stop();
+  int port() const { return cfg_.port; }
+  S3FrontStats stats();
+
+  struct Conn;
+  struct Req;
+
+ private:
+  void epoll_loop();
+  void worker_loop();
+  void serve(Conn* c);  // all requests until the connection goes idle or closes
+  bool handle(Conn* c, Req& r);
+  bool proxy(Conn* c, Req& r, const uint8_t* body, uint64_t body_len, const std::string& why);
+  bool native_put(Conn* c, Req& r, const std::string& path, bool part);
+  bool native_get(Conn* c, Req& r, const std::string& path, bool head);
+  bool native_mpu_get(Conn* c, Req& r, const std::string& path, const std::string& marker_meta);
+  int verify_auth(Req& r, std::string* user);  // 1 ok, 0 hand over
+  bool bucket_has_policy(const std::string& bucket);
+  void audit(const Conn* c, const Req& r, const std::string& user, int status);
+  void count(const Req& r, int status);
+  int backend_conn();
+  void backend_done(int fd, bool reuse);
+  void note_proxy(const std::string& why);
+  std::string native_metrics();
+
+  S3FrontConfig cfg_;
+  FastClient* fc_;
+  int lfd_ = -1, epfd_ = -1, evfd_ = -1, audit_fd_ = -1;
+  std::atomic<bool> stop_{false};
+  std::thread epoller_;
+  std::vector<std::thread> workers_;
+  std::mutex q_mu_;
+  std::condition_variable q_cv_;
+  std::deque<Conn*> ready_;
+  std::mutex conns_mu_;
+  std::map<int, Conn*> conns_;
+  std::mutex be_mu_;
+  std::vector<int> be_idle_;
+  std::mutex pol_mu_;
+  std::map<std::string, std::pair<double, bool>> policy_cache_;  // bucket -> (expiry, has policy)
+  std::mutex key_mu_;
+  std::map<std::string, std::string> key_cache_;  // date -> signing key (the single static key)
+  IoPool pool_{4};
+  std::mutex st_mu_;
+  S3FrontStats st_;
+};
+
+}  // namespace dfs

@@ -350,11 +350,13 @@ class ChunkServerProcess:
 
     def _start_grpc(self, a, creds):
         host, port = strip_scheme(a.addr).rsplit(":", 1)
-        if a.grpc_impl == "native" and creds is None and self.fastpath is not None:
+        if a.grpc_impl == "native" and self.fastpath is not None:
             self._py_methods = {name: (getattr(self.cs, snake(name)), req)
                                 for name, req, _resp in pb.SERVICES["ChunkServerService"]}
+            # TLS (--tls-cert/--tls-key) is served natively: OpenSSL + ALPN h2 (csrc/tls.cpp)
             srv = native.NativeGrpcChunkServer(self.store, self.fastpath, host, int(port), self._grpc_fallback,
-                                               workers=a.workers)
+                                               workers=a.workers, tls_cert=a.tls_cert or "" if creds else "",
+                                               tls_key=a.tls_key or "" if creds else "")
             ok, err = srv.start()
             if ok:
                 self.native_grpc = srv

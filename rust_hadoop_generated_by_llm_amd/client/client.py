@@ -99,7 +99,9 @@ class Client:
         # sequential) is the longest CPU step of a write, so keep one worker per in-flight
         # write of a concurrency-10 benchmark plus headroom; idle workers cost nothing
         hash_threads = int(os.environ.get("DFS_HASH_THREADS", "16"))
-        if (self.fastpath is not None and self.defer_create and not self.tls
+        # (with TLS too: the fast path and the masters' local RPC are same-host UNIX sockets
+        # restricted to our uid, never the network)
+        if (self.fastpath is not None and self.defer_create
                 and os.environ.get("DFS_NATIVE_CLIENT", "1") == "1"):
             fc = _native.FastClient(self.fastpath.name, self.local_chunkserver, hash_threads=hash_threads)
             if fc.ok:
@@ -107,9 +109,11 @@ class Client:
         # native remote client (csrc/client_remote.cpp): the same single-block writes/reads for
         # a client that is not co-located — every RPC over gRPC/TCP on the native HTTP/2 client
         self._remote = None
-        if (self._fast is None and self.defer_create and not self.tls
+        if (self._fast is None and self.defer_create
                 and os.environ.get("DFS_NATIVE_REMOTE", "1") == "1"):
-            self._remote = _native.RemoteClient(hash_threads, int(data_timeout * 1000))
+            # TLS clients speak TLS + ALPN h2 natively (csrc/tls.cpp), trusting ca_cert
+            self._remote = _native.RemoteClient(hash_threads, int(data_timeout * 1000), tls=self.tls,
+                                                ca_cert=ca_cert or "", domain_name=domain_name or "")
         self.remote_ops = 0
         self._sync_fast()
 

@@ -79,7 +79,8 @@ class MasterProcess:
         self.raft = RaftNode(args.id, members, self.client_addr, os.path.join(args.storage_dir, f"raft_node_{args.id}"),
                              self.state, self.transport, snapshot_threshold=args.snapshot_threshold,
                              sync=not args.no_fsync, backup_s3_endpoint=args.backup_s3_endpoint,
-                             backup_bucket=args.backup_bucket, native_sm=self.state.core)
+                             backup_bucket=args.backup_bucket, native_sm=self.state.core,
+                             peer_tls=(args.ca_cert or "", args.domain_name or "") if args.tls_cert else None)
         self.state.core.attach(self.raft._core)
         self.state.enter_safe_mode()
         self.config_servers = [with_scheme(c) for c in args.config_servers.split(",") if c.strip()]
@@ -210,11 +211,13 @@ class MasterProcess:
             return asyncio.run_coroutine_threadsafe(dispatch(path, rid, bytes(payload)), loop).result(120)
 
         server = self._native_grpc = None
-        if creds is None and os.environ.get("DFS_MASTER_GRPC", "native") == "native":
+        if os.environ.get("DFS_MASTER_GRPC", "native") == "native":
             # MasterService on the native HTTP/2 server: MasterCore's methods (the whole
             # write/read metadata path) are answered in C++, the rest by the handlers below
             host, port = bind.rsplit(":", 1)
-            srv = native.NativeGrpcMasterServer(self.state.core, host, int(port), fallback)
+            srv = native.NativeGrpcMasterServer(self.state.core, host, int(port), fallback,
+                                                tls_cert=a.tls_cert or "" if creds else "",
+                                                tls_key=a.tls_key or "" if creds else "")
             ok, err = srv.start()
             if ok:
                 self._native_grpc = srv
@@ -224,7 +227,7 @@ class MasterProcess:
             server = make_aio_server({"MasterService": self.svc}, bind, creds)
             await server.start()
         self._local_srv = None
-        if creds is None and os.environ.get("DFS_NO_LOCALRPC") != "1":
+        if os.environ.get("DFS_NO_LOCALRPC") != "1":
             # same-host clients skip HTTP/2: a native listener serves the hot methods from
             # MasterCore and hands the rest to the Python handlers on this loop
 

@@ -159,7 +159,7 @@ class RaftNode:
                  state_machine: StateMachine, transport, *, snapshot_threshold: int = 10000,
                  election_timeout: tuple[float, float] = (1.5, 3.0), heartbeat_interval: float = 0.1,
                  sync: bool = True, backup_s3_endpoint: str | None = None, backup_bucket: str = "dfs-backups",
-                 max_append_batch: int = 512, native_sm=None):
+                 max_append_batch: int = 512, native_sm=None, peer_tls: tuple[str, str] | None = None):
         self.id = node_id
         self.client_address = client_address
         self.dir = storage_dir
@@ -175,7 +175,8 @@ class RaftNode:
         self._core = native.RaftNode(
             node_id, {int(k): v for k, v in members.items()}, client_address, storage_dir, self._host,
             election_timeout[0], election_timeout[1], heartbeat_interval, sync, snapshot_threshold,
-            max_append_batch, backup_s3_endpoint or "", backup_bucket, native_sm)
+            max_append_batch, backup_s3_endpoint or "", backup_bucket, native_sm,
+            peer_tls=peer_tls is not None, peer_ca=(peer_tls or ("", ""))[0], peer_domain=(peer_tls or ("", ""))[1])
         self.wal = _Wal(self._core)
         self._rpc = ThreadPoolExecutor(max_workers=4, thread_name_prefix=f"raft-rpc-{node_id}")
         self._running = False

@@ -1164,10 +1164,52 @@ def _die_with_parent() -> None:
         pass
 
 
+def native_front_wanted(cfg: S3Config) -> bool:
+    """The native front end (csrc/s3_front.cpp) serves the object data path when the gateway
+    is co-located with a chunkserver (its native client moves bodies through that server's
+    pinned shared memory) and TLS is not terminated here (the front speaks plain HTTP)."""
+    if cfg.env.get("S3_NATIVE_FRONT", "true") != "true" or not cfg.local_chunkserver:
+        return False
+    if cfg.tls_cert and cfg.tls_key:
+        return False
+    try:
+        from ..native import lib  # noqa: F401
+    except Exception:  # noqa: BLE001 - no extension: the Python gateway serves everything
+        return False
+    return True
+
+
+def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_socket: str):
+    """Worker 0 runs the native front on the public port; it hands what it does not serve to
+    the aiohttp workers on `backend` and sends its audit records to `audit_socket`."""
+    from ..native import lib
+
+    cfg = gw.cfg
+    creds = gw.creds
+    front = lib.S3Front(gw.client._fast, host, port, backend,
+                        workers=int(cfg.env.get("S3_FRONT_THREADS", "32") or 32),
+                        auth_enabled=cfg.auth_enabled, region=cfg.region,
+                        access_key=getattr(creds, "access_key", None) or "",
+                        secret_key=getattr(creds, "secret_key", None) or "",
+                        allow_unsigned_payload=cfg.allow_unsigned_payload,
+                        audit_socket=audit_socket if (cfg.auth_enabled and gw.audit is not None) else "",
+                        sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar)
+    ok, err = front.start()
+    if not ok:
+        raise RuntimeError(f"native S3 front end failed to start: {err}")
+    if gw.client._fast is None:
+        log.warning("native front end without a co-located native client: every request goes to Python")
+    return front
+
+
 def main(argv: list[str] | None = None) -> int:
     """One listening socket shared by S3_WORKERS processes (default 4), forked before any
     gRPC channel or thread exists; each runs its own event loop and DFS client, so request
-    handling scales past one interpreter lock. Worker 0 owns the audit store."""
+    handling scales past one interpreter lock. Worker 0 owns the audit store.
+
+    Co-located with a chunkserver (LOCAL_CHUNKSERVER), worker 0 also runs the native front
+    end on the public port and the workers' shared socket becomes a private UNIX socket that
+    only the front hands requests to (S3_NATIVE_FRONT=false keeps the Python-only layout)."""
     ap = argparse.ArgumentParser(prog="s3_server", description="S3-compatible gateway over the DFS")
     ap.add_argument("--port", type=int, default=None)
     ap.add_argument("--host", default="0.0.0.0")
@@ -1179,13 +1221,20 @@ def main(argv: list[str] | None = None) -> int:
     if a.port is not None:
         cfg.port = a.port
     workers = max(1, a.workers if a.workers is not None else int(os.environ.get("S3_WORKERS", "4") or 4))
-    lsock = socket.socket(socket.AF_INET6 if ":" in a.host else socket.AF_INET, socket.SOCK_STREAM)
-    lsock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-    lsock.bind((a.host, cfg.port))
+    native = native_front_wanted(cfg)
+    private_dir = tempfile.mkdtemp(prefix="s3gw-")
+    backend_path = os.path.join(private_dir, "backend.sock")
+    if native:
+        lsock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        lsock.bind(backend_path)
+    else:
+        lsock = socket.socket(socket.AF_INET6 if ":" in a.host else socket.AF_INET, socket.SOCK_STREAM)
+        lsock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        lsock.bind((a.host, cfg.port))
     lsock.listen(1024)
     ingest_path = ingest = None
-    if workers > 1 and cfg.audit_enabled:
-        ingest_path = os.path.join(tempfile.mkdtemp(prefix="s3audit-"), "ingest.sock")
+    if (workers > 1 or native) and cfg.audit_enabled:
+        ingest_path = os.path.join(private_dir, "ingest.sock")
         ingest = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
         ingest.bind(ingest_path)
         ingest.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
@@ -1211,20 +1260,25 @@ def main(argv: list[str] | None = None) -> int:
     if cfg.tls_cert and cfg.tls_key:
         ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
         ssl_ctx.load_cert_chain(cfg.tls_cert, cfg.tls_key)
+    front = None
+    if worker_id == 0 and native:
+        front = start_native_front(gw, a.host, cfg.port, backend_path, ingest_path or "")
     if worker_id == 0:
-        log.info("S3 gateway on %s:%d (workers=%d, auth=%s, sse=%s, audit=%s)", a.host, cfg.port, workers,
-                 cfg.auth_enabled, gw.sse is not None, gw.audit is not None)
+        log.info("S3 gateway on %s:%d (workers=%d, auth=%s, sse=%s, audit=%s, native front=%s)", a.host, cfg.port,
+                 workers, cfg.auth_enabled, gw.sse is not None, gw.audit is not None, front is not None)
     ready = os.environ.get("DFS_READY_FILE") if worker_id == 0 else None
 
     async def on_start(_app):
         if ready:
             with open(ready, "w") as f:
-                json.dump({"port": cfg.port, "workers": workers}, f)
+                json.dump({"port": cfg.port, "workers": workers, "native_front": front is not None}, f)
     app = gw.app()
     app.on_startup.append(on_start)
     try:
         web.run_app(app, sock=lsock, ssl_context=ssl_ctx, print=None, access_log=None)
     finally:
+        if front is not None:
+            front.stop()
         for pid in children:
             try:
                 os.kill(pid, signal.SIGTERM)
@@ -1235,8 +1289,8 @@ def main(argv: list[str] | None = None) -> int:
                 os.waitpid(pid, 0)
             except ChildProcessError:
                 pass
-        if ingest_path:
-            shutil.rmtree(os.path.dirname(ingest_path), ignore_errors=True)
+        if worker_id == 0:
+            shutil.rmtree(private_dir, ignore_errors=True)
     if worker_id > 0:
         os._exit(0)
     return 0

@@ -308,12 +308,55 @@ def test_tls_cluster():
         c.create_file_from_buffer(data, "/tls/f")
         assert c.get_file_content("/tls/f") == data
         assert len(c.get_file_info("/tls/f").blocks[0].locations) == 2
+        # TLS no longer drops anything to grpcio / the Python client — the
+        # native remote client (TLS + ALPN h2, csrc/tls.cpp) did the write and the read against
+        # the native HTTP/2 servers, which now terminate TLS themselves
+        assert c._remote is not None and c.remote_ops == 2
+        served = sum(json.load(urllib.request.urlopen(f"{u}/stats"))["native_grpc_calls"] for u in cl.cs_http)
+        assert served >= 2
+        # a grpcio TLS client interoperates with the native servers
+        pool = ChannelPool(cl.ca_cert)
+        st = pool.call(cl.master_addrs[0], "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(),
+                       timeout=5)
+        assert st.chunk_server_count == 2
+        r = pool.call(f"https://{cl.cs_addrs[0]}", "ChunkServerService", "ReadBlock",
+                      pb.ReadBlockRequest(block_id=c.get_file_info("/tls/f").blocks[0].block_id), timeout=10)
+        assert r.data == data
+        pool.close()
         c.close()
-        plain = ChannelPool()
+        # a co-located client keeps its same-host native paths under TLS
+        lc = cl.client(local_chunkserver=cl.cs_addrs[0])
+        lc.create_file_from_buffer(data, "/tls/local")
+        assert lc.get_file_content("/tls/local") == data and lc._fast is not None
+        lc.close()
+        plain = ChannelPool(local=False)  # over the network (same-uid UNIX sockets stay allowed)
         with pytest.raises(grpc.RpcError):
             plain.call(cl.master_addrs[0].replace("https://", "http://"), "MasterService", "GetSafeModeStatus",
                        pb.GetSafeModeStatusRequest(), timeout=3)
         plain.close()
+
+
+def test_tls_raft_group_native_peers():
+    """A 3-master shard under TLS: Raft AppendEntries / RequestVote travel node to node over
+    the native HTTP/2 servers, TLS on both ends (csrc/tls.cpp), not the HTTP/JSON fallback."""
+    with LocalCluster(n_chunkservers=1, masters_per_shard=3, fsync=False, tls=True) as cl:
+        c = cl.client()
+        c.create_file_from_buffer(b"replicated metadata", "/tlsraft/f")
+        assert c.get_file_content("/tlsraft/f") == b"replicated metadata"
+        c.close()
+        deadline = time.time() + 20
+        total = 0
+        while time.time() < deadline:
+            total = 0
+            for http in cl.master_http.values():
+                text = urllib.request.urlopen(f"{http}/metrics").read().decode()
+                vals = {ln.split()[0]: float(ln.split()[1]) for ln in text.splitlines()
+                        if ln and not ln.startswith("#")}
+                total += vals.get("dfs_master_native_raft_rpcs", 0)
+            if total > 10:
+                break
+            time.sleep(0.5)
+        assert total > 10
 
 
 def test_tiering_moves_cold_and_converts_to_ec():

@@ -12,6 +12,9 @@ import asyncio
 import hashlib
 import json
 import os
+import shutil
+import socket
+import tempfile
 import signal
 import threading
 import time
@@ -34,47 +37,87 @@ pytestmark = pytest.mark.slow
 
 
 class GatewayThread:
-    def __init__(self, gw):
+    """The gateway in this process. `native`: the production layout of s3/server.py with the
+    native front end (csrc/s3_front.cpp) on the TCP port, handing what it does not serve to
+    the aiohttp app on a private UNIX socket; audit records of native requests reach the
+    app's AuditLogger through the same datagram ingest socket the server's workers use."""
+
+    def __init__(self, gw, native: bool = False):
         self.gw = gw
+        self.native = native
         self.port = free_port()
         self.loop = asyncio.new_event_loop()
         self._ready = threading.Event()
         self._runner = None
+        self.front = None
+        self._dir = tempfile.mkdtemp(prefix="s3gw-test-")
+        self.backend = os.path.join(self._dir, "backend.sock")
         self.t = threading.Thread(target=self._run, daemon=True)
         self.t.start()
         assert self._ready.wait(30)
+        if native:
+            from rust_hadoop_generated_by_llm_amd.native import lib
+            from rust_hadoop_generated_by_llm_amd.s3.server import _audit_ingest
+
+            assert gw.client._fast is not None, "native front needs the co-located native client"
+            ingest = ""
+            if gw.audit is not None:
+                ingest = os.path.join(self._dir, "ingest.sock")
+                self._isock = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
+                self._isock.bind(ingest)
+                threading.Thread(target=_audit_ingest, args=(self._isock, gw.audit), daemon=True).start()
+            cfg = gw.cfg
+            self.front = lib.S3Front(gw.client._fast, "127.0.0.1", self.port, self.backend, workers=8,
+                                     auth_enabled=cfg.auth_enabled, region=cfg.region,
+                                     access_key=gw.creds.access_key or "", secret_key=gw.creds.secret_key or "",
+                                     allow_unsigned_payload=cfg.allow_unsigned_payload,
+                                     audit_socket=ingest if cfg.auth_enabled else "",
+                                     sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar)
+            ok, err = self.front.start()
+            assert ok, err
         self.url = f"http://127.0.0.1:{self.port}"
 
     def _run(self):
         asyncio.set_event_loop(self.loop)
         self._runner = web.AppRunner(self.gw.app(), access_log=None)
         self.loop.run_until_complete(self._runner.setup())
-        self.loop.run_until_complete(web.TCPSite(self._runner, "127.0.0.1", self.port).start())
+        site = web.UnixSite(self._runner, self.backend) if self.native else \
+            web.TCPSite(self._runner, "127.0.0.1", self.port)
+        self.loop.run_until_complete(site.start())
         self._ready.set()
         self.loop.run_forever()
         self.loop.run_until_complete(self._runner.cleanup())
         self.loop.close()
 
     def stop(self):
+        if self.front is not None:
+            self.front.stop()
         self.loop.call_soon_threadsafe(self.loop.stop)
         self.t.join(30)
+        shutil.rmtree(self._dir, ignore_errors=True)
+
+
+@pytest.fixture(scope="module", params=["python", "native"])
+def front(request):
+    return request.param
 
 
 @pytest.fixture(scope="module")
-def cluster():
+def cluster(front):
+    # one cluster per front end: the tests reuse object names
     with LocalCluster(n_chunkservers=3, fsync=False) as c:
         yield c
 
 
-def make_gw(cluster, env):
+def make_gw(cluster, env, front="python"):
     cfg = S3Config(env)
-    client = cluster.client()
-    return GatewayThread(build_gateway(cfg, client))
+    client = cluster.client(local_chunkserver=cluster.cs_addrs[0]) if front == "native" else cluster.client()
+    return GatewayThread(build_gateway(cfg, client), native=front == "native")
 
 
 @pytest.fixture(scope="module")
-def gw(cluster):
-    g = make_gw(cluster, {"AUDIT_LOG_ENABLED": "false"})
+def gw(cluster, front):
+    g = make_gw(cluster, {"AUDIT_LOG_ENABLED": "false"}, front)
     yield g
     g.stop()
 
@@ -373,7 +416,7 @@ def oidc_issuer():
 
 
 @pytest.fixture(scope="module")
-def authgw(cluster, oidc_issuer, tmp_path_factory):
+def authgw(cluster, oidc_issuer, tmp_path_factory, front):
     d = tmp_path_factory.mktemp("authgw")
     iam = d / "iam.json"
     iam.write_text(json.dumps(IAM_CONFIG))
@@ -381,7 +424,7 @@ def authgw(cluster, oidc_issuer, tmp_path_factory):
            "OIDC_ISSUER_URL": oidc_issuer["url"], "OIDC_CLIENT_ID": "dfs-client",
            "STS_SIGNING_KEY": "sts-signing-key-0123456789abcdef", "IAM_CONFIG_PATH": str(iam),
            "AUDIT_LOG_DIR": str(d / "audit"), "AUDIT_HMAC_SECRET": AUDIT_SECRET, "AUDIT_LOG_BATCH_SIZE": "5"}
-    g = make_gw(cluster, env)
+    g = make_gw(cluster, env, front)
     g.audit_dir = str(d / "audit")
     yield g
     g.stop()
@@ -601,10 +644,10 @@ def test_audit_log_written_and_chained(authgw):
                for r in recs)
 
 
-def test_unsigned_payload_policy_and_tls(cluster):
+def test_unsigned_payload_policy_and_tls(cluster, front):
     g = make_gw(cluster, {"S3_AUTH_ENABLED": "true", "S3_ACCESS_KEY": "ak", "S3_SECRET_KEY": "sk",
                           "S3_ALLOW_UNSIGNED_PAYLOAD": "false", "S3_REQUIRE_TLS": "true",
-                          "AUDIT_LOG_ENABLED": "false"})
+                          "AUDIT_LOG_ENABLED": "false"}, front)
     try:
         host = g.url.split("://")[1]
         h = sigv4.sign_headers("GET", "/", [], host, None, "ak", "sk", unsigned_payload=True)
@@ -617,8 +660,8 @@ def test_unsigned_payload_policy_and_tls(cluster):
         g.stop()
 
 
-def test_sse_at_rest(cluster):
-    g = make_gw(cluster, {"SSE_MASTER_KEY": "ab" * 32, "AUDIT_LOG_ENABLED": "false"})
+def test_sse_at_rest(cluster, front):
+    g = make_gw(cluster, {"SSE_MASTER_KEY": "ab" * 32, "AUDIT_LOG_ENABLED": "false"}, front)
     try:
         u = g.url
         requests.put(f"{u}/sse")
@@ -640,22 +683,28 @@ def test_sse_at_rest(cluster):
         g.stop()
 
 
-def test_gateway_subprocess(cluster):
+def _front_env(cluster, front):
+    # the s3.server process runs its native front end when co-located with a chunkserver
+    return {"LOCAL_CHUNKSERVER": cluster.cs_addrs[0]} if front == "native" else {"S3_NATIVE_FRONT": "false"}
+
+
+def test_gateway_subprocess(cluster, front):
     """The s3.server entry point runs as its own process (reference s3-server binary)."""
-    url = cluster.start_s3({"AUDIT_LOG_ENABLED": "false"})
+    url = cluster.start_s3({"AUDIT_LOG_ENABLED": "false", **_front_env(cluster, front)})
     assert requests.get(url + "/health").text == "OK"
     assert requests.put(url + "/subproc").status_code == 200
     assert requests.put(url + "/subproc/o", data=b"via process").status_code == 200
     assert requests.get(url + "/subproc/o").content == b"via process"
 
 
-def test_gateway_workers_share_one_audit_chain(cluster, tmp_path):
+def test_gateway_workers_share_one_audit_chain(cluster, tmp_path, front):
     """S3_WORKERS=3: three processes accept on one socket; every worker's audit records
     reach worker 0's logger, so the store holds ONE verifiable hash chain with all of them."""
     audit_dir = tmp_path / "audit"
     url = cluster.start_s3({"S3_WORKERS": "3", "S3_AUTH_ENABLED": "true", "S3_ACCESS_KEY": "admin",
                             "S3_SECRET_KEY": "admin-secret", "AUDIT_LOG_DIR": str(audit_dir),
-                            "AUDIT_HMAC_SECRET": AUDIT_SECRET, "AUDIT_LOG_BATCH_SIZE": "1"}, name="s3w")
+                            "AUDIT_HMAC_SECRET": AUDIT_SECRET, "AUDIT_LOG_BATCH_SIZE": "1",
+                            **_front_env(cluster, front)}, name="s3w")
     pr = next(p for p in cluster.procs if p.name == "s3w")
     assert pr.info.get("workers") == 3
     import psutil
@@ -687,3 +736,93 @@ def test_gateway_workers_share_one_audit_chain(cluster, tmp_path):
     assert verify_chain(SegmentStore(str(audit_dir)), AUDIT_SECRET) == (n + 1, [])
     cluster.kill("s3w", signal.SIGTERM)
     assert not psutil.pid_exists(pr.popen.pid)
+
+
+def test_native_front_serves_object_data(gw, front):
+    """PUT / GET / HEAD / Range GET / UploadPart / multipart GET are served
+    by the native front end (csrc/s3_front.cpp), bodies moving socket <-> shared-memory slot
+    <-> chunkserver without the interpreter; bucket and MPU control calls go to Python."""
+    if front != "native":
+        pytest.skip("native front end only")
+    u = gw.url
+    s0 = gw.front.stats()
+    assert requests.put(f"{u}/nat").status_code == 200
+    body = os.urandom((3 << 20) + 11)
+    r = requests.put(f"{u}/nat/k1", data=body, headers={"x-amz-meta-owner": "me", "Content-Type": "image/x"})
+    assert r.status_code == 200 and r.headers["ETag"] == md5q(body)
+    r = requests.get(f"{u}/nat/k1")
+    assert r.status_code == 200 and r.content == body and r.headers["ETag"] == md5q(body)
+    assert r.headers["x-amz-meta-owner"] == "me" and r.headers["Content-Type"] == "image/x"
+    r = requests.get(f"{u}/nat/k1", headers={"Range": "bytes=1000-66535"})
+    assert r.status_code == 206 and r.content == body[1000:66536]
+    assert r.headers["Content-Range"] == f"bytes 1000-66535/{len(body)}"
+    r = requests.get(f"{u}/nat/k1", headers={"Range": "bytes=-100"})
+    assert r.status_code == 206 and r.content == body[-100:]
+    h = requests.head(f"{u}/nat/k1")
+    assert h.status_code == 200 and int(h.headers["Content-Length"]) == len(body)
+    # overwrite: the key is replaced (delete + create), new ETag
+    body2 = os.urandom(1000)
+    assert requests.put(f"{u}/nat/k1", data=body2).headers["ETag"] == md5q(body2)
+    assert requests.get(f"{u}/nat/k1").content == body2
+    # multipart: initiate / complete in Python, parts and the GET native
+    import xml.etree.ElementTree as ET
+
+    up = ET.fromstring(requests.post(f"{u}/nat/big?uploads").content).find("UploadId").text
+    parts = [os.urandom((1 << 20) + i) for i in range(3)]
+    etags = []
+    for i, p in enumerate(parts):
+        r = requests.put(f"{u}/nat/big?partNumber={i + 1}&uploadId={up}", data=p)
+        assert r.status_code == 200 and r.headers["ETag"] == md5q(p)
+        etags.append(r.headers["ETag"])
+    done = "<CompleteMultipartUpload>" + "".join(
+        f"<Part><PartNumber>{i + 1}</PartNumber><ETag>{e}</ETag></Part>" for i, e in enumerate(etags)) + \
+        "</CompleteMultipartUpload>"
+    assert requests.post(f"{u}/nat/big?uploadId={up}", data=done).status_code == 200
+    whole = b"".join(parts)
+    assert requests.get(f"{u}/nat/big").content == whole
+    lo, hi = (1 << 20) - 5, (2 << 20) + 7
+    r = requests.get(f"{u}/nat/big", headers={"Range": f"bytes={lo}-{hi}"})
+    assert r.status_code == 206 and r.content == whole[lo:hi + 1]
+    # an upload that does not exist: Python's NoSuchUpload
+    r = requests.put(f"{u}/nat/x?partNumber=1&uploadId=nope", data=b"z")
+    assert r.status_code == 404 and b"NoSuchUpload" in r.content
+    s1 = gw.front.stats()
+    assert s1["puts"] - s0["puts"] >= 2 and s1["parts"] - s0["parts"] == 3
+    assert s1["gets"] - s0["gets"] >= 2 and s1["range_gets"] - s0["range_gets"] >= 2
+    assert s1["heads"] - s0["heads"] >= 1 and s1["mpu_gets"] - s0["mpu_gets"] == 2
+    assert s1["proxied"] > s0["proxied"]  # bucket / MPU control went to Python
+    m = requests.get(f"{u}/metrics").text
+    assert "s3_native_requests_total" in m and "s3_requests_total" in m
+
+
+def test_native_front_auth_and_audit(authgw, front):
+    """Signed requests with the static key are verified in C++ (csrc/sigv4.cpp) and audited
+    into the same hash chain; a bad signature is handed to Python, which answers 403."""
+    if front != "native":
+        pytest.skip("native front end only")
+    g = authgw
+    s0 = g.front.stats()
+    assert signed("PUT", g, "/natauth").status_code == 200
+    data = os.urandom(50_000)
+    assert signed("PUT", g, "/natauth/o", data).status_code == 200
+    assert signed("GET", g, "/natauth/o").content == data
+    r = signed("GET", g, "/natauth/o", sk="wrong-secret")
+    assert r.status_code == 403 and b"SignatureDoesNotMatch" in r.content
+    assert requests.get(g.url + "/natauth/o").status_code == 403  # anonymous
+    s1 = g.front.stats()
+    assert s1["auth_native"] - s0["auth_native"] >= 2 and s1["audit_sent"] - s0["audit_sent"] >= 2
+    assert g.gw.audit.flush(15)
+    deadline = time.time() + 10
+    while True:
+        recs = [r for _, r in SegmentStore(g.audit_dir).scan()]
+        if any(r["resource"] == "arn:dfs:s3:::natauth/o" and r["action"] == "s3:GetObject" and
+               r["status_code"] == 200 and r["user_id"] == "admin" for r in recs) or time.time() > deadline:
+            break
+        time.sleep(0.1)
+        g.gw.audit.flush(5)
+    assert any(r["resource"] == "arn:dfs:s3:::natauth/o" and r["action"] == "s3:PutObject" and r["user_id"] == "admin"
+               for r in recs)
+    assert any(r["resource"] == "arn:dfs:s3:::natauth/o" and r["action"] == "s3:GetObject" and r["status_code"] == 200
+               for r in recs)
+    n, errs = verify_chain(SegmentStore(g.audit_dir), AUDIT_SECRET)
+    assert errs == []
