@@ -22,6 +22,7 @@ import argparse
 import hashlib
 import json
 import os
+import subprocess
 import sys
 import tempfile
 import threading
@@ -224,6 +225,7 @@ def config5(a):
                             "get_mb_per_s": round(len(blob) / (1 << 20) / mpu_get_s, 1)}
         lg.close()
         out["parquet_over_s3"] = parquet_phase(url, a)
+        out["native_load"] = native_load_phase(url, a, len(blob))
         out["load_generator"] = f"{a.concurrency} client processes (requests, keep-alive)"
         out["gateway_workers"] = int(os.environ.get("S3_WORKERS", "4"))
         # what the native front end served itself vs handed to the Python workers
@@ -234,6 +236,29 @@ def config5(a):
                 nat[k] = int(float(v))
         out["native_front"] = nat
         emit(out)
+
+
+def native_load_phase(url: str, a, mpu_bytes: int) -> dict:
+    """The same PUT / GET / Range GET 64 KiB / multipart GET against the gateway from the
+    native load generator (build/native/s3_load: C++ HTTP/1.1 clients, one keep-alive
+    connection per thread), so the numbers describe the gateway, not Python's HTTP stack."""
+    exe = ROOT / "build" / "native" / "s3_load"
+    if not exe.exists():
+        return {"skipped": "build/native/s3_load not built"}
+    host, port = url.split("://")[1].rsplit(":", 1)
+    base = [str(exe), "--host", host, "--port", port, "--bucket", "bench", "--conc", str(a.concurrency)]
+    out = {"client": f"s3_load, {a.concurrency} C++ threads, keep-alive"}
+    n = a.count * 4
+    for name, extra in (("put", ["--op", "put", "--count", str(n), "--size", str(a.size), "--prefix", "nat"]),
+                        ("get", ["--op", "get", "--count", str(n), "--size", str(a.size), "--prefix", "nat",
+                                 "--verify"]),
+                        ("range_get_64k", ["--op", "range", "--count", str(n * 8), "--keys", str(n),
+                                           "--size", str(a.size), "--prefix", "nat", "--verify"]),
+                        ("multipart_get", ["--op", "get", "--count", "16", "--size", str(mpu_bytes),
+                                           "--key", "big.bin"])):
+        r = subprocess.run(base + extra, capture_output=True, text=True, timeout=300)
+        out[name] = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}
+    return out
 
 
 def parquet_phase(url: str, a) -> dict:

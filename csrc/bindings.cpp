@@ -411,8 +411,21 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["fp_p2p_fallbacks"] = s.p2p_fallbacks;
         d["fp_rejected_peers"] = s.rejected_peers;
         d["fp_ec_ops"] = s.ec_ops;
+        d["fp_heals_out"] = s.heals_out;
+        d["fp_heals_in"] = s.heals_in;
         return d;
-      });
+      })
+      .def("replicate_block", [](FastPathServer& f, const std::string& id, const std::vector<std::string>& targets,
+                                 uint64_t term) {
+        std::vector<std::string> done;
+        int n;
+        {
+          py::gil_scoped_release r;
+          n = f.replicate_block(id, targets, term, &done);
+        }
+        return py::make_tuple(n, done);
+      }, py::arg("block_id"), py::arg("targets"), py::arg("term"))
+      .def("drain_healed", &FastPathServer::drain_healed);
 
   struct PyTicket {
     ReplTicket t;

@@ -759,6 +759,20 @@ void bind_meta(py::module_& m) {
         }
         return py::make_tuple(static_cast<int>(st), data, msg, py::make_tuple(t.getinfo, t.read));
       }, py::arg("path"), py::arg("request_id") = "", py::arg("offset") = 0, py::arg("length") = 0)
+      .def("write_ec", [](FastClient& c, const std::string& path, py::buffer data, int k, int m, const std::string& rid) {
+        py::buffer_info bi = data.request();
+        std::string msg;
+        FastClient::Status st;
+        {
+          py::gil_scoped_release r;
+          st = c.write_ec(path, static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize), k, m,
+                          &msg, rid);
+        }
+        return py::make_tuple(static_cast<int>(st), msg);
+      }, py::arg("path"), py::arg("data"), py::arg("k"), py::arg("m"), py::arg("request_id") = "")
+      .def_property_readonly("ec_gpu_ops", &FastClient::ec_gpu_ops)
+      .def_property_readonly("ec_cpu_ops", &FastClient::ec_cpu_ops)
+      .def_property_readonly("ec_degraded_reads", &FastClient::ec_degraded_reads)
       .def("bench_writes", &bench_writes<FastClient>, py::arg("paths"), py::arg("payloads"), py::arg("concurrency"))
       .def("bench_reads", &bench_reads_fast, py::arg("paths"), py::arg("expected"), py::arg("concurrency"));
 
@@ -778,6 +792,8 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("writes", &RemoteClient::writes)
       .def_property_readonly("reads", &RemoteClient::reads)
       .def_property_readonly("connects", &RemoteClient::connects)
+      .def_property_readonly("hedged", &RemoteClient::hedged)
+      .def("set_hedge_delay", &RemoteClient::set_hedge_delay)
       .def("set_routing", &RemoteClient::set_routing, py::call_guard<py::gil_scoped_release>())
       .def("write", [](RemoteClient& c, const std::string& path, py::buffer data, const std::string& rid,
                          const std::map<std::string, std::string>& attrs) {

@@ -141,7 +141,8 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
   // than our two files, so the per-file fdatasync pair stays the default.
   const char* gs = std::getenv("DFS_GROUP_SYNC");
   if (cfg_.sync_writes && gs && std::string(gs) == "1") gsync_ = std::make_unique<GroupSync>(cfg_.storage_dir);
-  if (cfg_.sync_writes) {
+  const char* ds = std::getenv("DFS_DIR_SYNC");  // 0: A/B runs only (renames not made durable)
+  if (cfg_.sync_writes && !(ds && std::string(ds) == "0")) {
     // renames into place are durable only once the directory is flushed (the reference
     // writes final names directly and sync_all()s the file, chunkserver.rs:192-209)
     dsync_hot_ = std::make_unique<GroupSync>(cfg_.storage_dir, GroupSync::Mode::Directory);

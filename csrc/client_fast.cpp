@@ -1,4 +1,5 @@
 #include "client_fast.h"
+#include "gf256.h"
 #include "trace.h"
 
 #include <fcntl.h>
@@ -284,6 +285,12 @@ bool FastClient::call(const std::string& sock, const std::string& method_path, c
 
 bool FastClient::fp_call(uint8_t op, const std::string& body, uint8_t* status, uint64_t* total, uint64_t* nbytes,
                          std::string* msg) {
+  return fp_call_to(fp_socket_, op, body, status, total, nbytes, msg);
+}
+
+bool FastClient::fp_call_to(const std::string& sock, uint8_t op, const std::string& body, uint8_t* status,
+                            uint64_t* total, uint64_t* nbytes, std::string* msg) {
+  const std::string& fp_socket_ = sock;  // the connection pool is keyed by socket name
   int fd = take_conn(fp_socket_);
   if (fd < 0) return false;
   std::string req;
@@ -527,7 +534,8 @@ FastClient::Status FastClient::read_known(const std::string& meta_pb, int64_t* s
     *n = 0;
     return Ok;
   }
-  if (m.blocks.size() != 1 || m.blocks[0].ec_data_shards > 0) return NotHandled;
+  if (m.blocks.size() == 1 && m.blocks[0].ec_data_shards > 0) return read_ec(meta_pb, slot, n, msg, rid, offset, length);
+  if (m.blocks.size() != 1) return NotHandled;
   if (length > 0) {
     if (offset >= m.size) return NotHandled;  // the Python path reports the range error
     length = std::min<uint64_t>(length, m.size - offset);
@@ -563,6 +571,268 @@ FastClient::Status FastClient::read_known(const std::string& meta_pb, int64_t* s
   t->read += since(clk);
   *slot = s + static_cast<int64_t>(shift);
   *n = got;
+  reads_++;
+  return Ok;
+}
+
+
+std::string FastClient::peer_fastpath(const std::string& addr) const {
+  // chunkservers listen on the deterministic abstract socket dfs_fp_<grpc port> (same host)
+  const std::string a = strip_scheme(addr);
+  size_t c = a.rfind(':'), lc = local_cs_.rfind(':');
+  if (c == std::string::npos || lc == std::string::npos) return {};
+  const std::string host = a.substr(0, c), lhost = local_cs_.substr(0, lc);
+  const bool local = host == lhost || host == "127.0.0.1" || host == "localhost" || host == "::1";
+  return local ? "dfs_fp_" + a.substr(c + 1) : std::string();
+}
+
+bool FastClient::ec_matmul(const std::vector<std::vector<uint8_t>>& mat, int k, uint64_t len, uint64_t in_off,
+                           uint64_t out_off, const std::vector<uint16_t>* idx, const std::string& rid) {
+  std::string body, flat;
+  for (auto& row : mat) flat.append(reinterpret_cast<const char*>(row.data()), row.size());
+  put<uint16_t>(body, static_cast<uint16_t>(k));
+  put<uint16_t>(body, static_cast<uint16_t>(mat.size()));
+  put<uint64_t>(body, len);
+  put<uint64_t>(body, in_off);
+  put<uint64_t>(body, out_off);
+  put_str(body, flat);
+  put_str(body, arena_path_);
+  put_str(body, rid);
+  if (idx) {
+    put<uint16_t>(body, static_cast<uint16_t>(idx->size()));
+    for (uint16_t v : *idx) put<uint16_t>(body, v);
+  }
+  uint8_t st;
+  uint64_t total, got;
+  std::string fmsg;
+  if (fp_call(6, body, &st, &total, &got, &fmsg) && st == 0) {
+    ec_gpu_++;
+    return true;
+  }
+  // no GPU behind the fast path (host store) or no room: the CPU codec, same bytes
+  const uint64_t stride = (len + 15) / 16 * 16;
+  std::vector<const uint8_t*> in(k);
+  std::vector<uint8_t*> out(mat.size());
+  for (int c = 0; c < k; ++c) in[c] = base_ + in_off + (idx ? (*idx)[c] : c) * stride;
+  for (size_t r = 0; r < mat.size(); ++r) out[r] = base_ + out_off + r * stride;
+  gf::matmul_cpu(mat, in.data(), out.data(), len);
+  ec_cpu_++;
+  return true;
+}
+
+FastClient::Status FastClient::write_ec(const std::string& path, const uint8_t* data, size_t n, int k, int m,
+                                        std::string* msg, const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  RequestScope rs(rid);
+  TraceRange tr("dfs.client.write_ec");
+  if (!base_ || k <= 0 || m <= 0 || k + m > 32 || n == 0) return NotHandled;
+  std::string sock = master_socket(path);
+  if (sock.empty()) return NotHandled;
+  const uint64_t sl = (n + k - 1) / k, stride = (sl + 15) / 16 * 16;
+  if (stride * (k + m) > slot_bytes_) return NotHandled;
+  pb::CreateFileRequest creq;
+  creq.path = path;
+  creq.ec_data_shards = k;
+  creq.ec_parity_shards = m;
+  creq.allocate_block = true;
+  creq.defer_create = true;
+  creq.preferred_chunk_server = local_cs_;
+  int code;
+  std::string raw;
+  if (!call(sock, "/dfs.MasterService/CreateFile", rid, creq.str(), &code, &raw)) return NotHandled;
+  if (code == kOutOfRange || code == kFailedPrecondition || code == kUnavailable) return NotHandled;
+  if (code != 0) {
+    *msg = "Failed to create file: " + raw;
+    return Failed;
+  }
+  pb::CreateFileResponse cresp;
+  if (!cresp.decode(raw)) return NotHandled;
+  if (!cresp.success) {
+    if (cresp.error_message == "Not Leader") return NotHandled;
+    *msg = "Failed to create file: " + cresp.error_message;
+    return Failed;
+  }
+  if (!cresp.has_allocation || !cresp.allocation.has_block || !cresp.deferred) return NotHandled;
+  const pb::AllocateBlockResponse& alloc = cresp.allocation;
+  if (alloc.ec_data_shards != k || alloc.ec_parity_shards != m) {
+    *msg = "Master returned non-EC policy (data=" + std::to_string(alloc.ec_data_shards) + ", parity=" +
+           std::to_string(alloc.ec_parity_shards) + ") for EC file";
+    return Failed;
+  }
+  if (alloc.chunk_server_addresses.size() != static_cast<size_t>(k + m)) {
+    *msg = "Expected " + std::to_string(k + m) + " chunk servers for EC(" + std::to_string(k) + "," +
+           std::to_string(m) + "), got " + std::to_string(alloc.chunk_server_addresses.size());
+    return Failed;
+  }
+  int64_t slot = acquire(stride * (k + m));
+  if (slot < 0) return NotHandled;
+  struct Rel {
+    FastClient* c;
+    int64_t s;
+    ~Rel() { c->release(s); }
+  } rel{this, slot};
+  uint8_t* b = base_ + slot;
+  for (int c = 0; c < k; ++c) {  // zero-padded stripes (erasure.rs:7-24)
+    const uint64_t off = c * sl, have = off < n ? std::min<uint64_t>(sl, n - off) : 0;
+    if (have) std::memcpy(b + c * stride, data + off, have);
+    if (have < sl) std::memset(b + c * stride + have, 0, sl - have);
+  }
+  gf::Matrix full = gf::rs_matrix(k, m), parity(full.begin() + k, full.end());
+  ec_matmul(parity, k, sl, static_cast<uint64_t>(slot), static_cast<uint64_t>(slot) + k * stride, nullptr, rid);
+  std::vector<std::future<std::pair<int, std::string>>> futs;  // (0 ok, 1 not handled, 2 failed)
+  for (int i = 0; i < k + m; ++i) {
+    futs.push_back(shard_pool_.submit([this, i, b, slot, stride, sl, &alloc, rid]() -> std::pair<int, std::string> {
+      RequestScope scope(rid);
+      const std::string addr = strip_scheme(alloc.chunk_server_addresses[i]);
+      const uint8_t* p = b + i * stride;
+      const uint32_t crc = crc32(p, sl);
+      const std::string fps = peer_fastpath(addr);
+      if (!fps.empty()) {
+        std::string body;
+        put<uint64_t>(body, alloc.master_term);
+        put<uint32_t>(body, crc);
+        put<uint64_t>(body, static_cast<uint64_t>(slot) + i * stride);
+        put<uint64_t>(body, sl);
+        put_str(body, alloc.block.block_id);
+        put_str(body, arena_path_);
+        put<uint16_t>(body, 0);
+        put_str(body, rid);
+        uint8_t st;
+        uint64_t total, written;
+        std::string fmsg;
+        if (fp_call_to(fps, 1, body, &st, &total, &written, &fmsg)) {
+          if (st == 0) return {0, ""};
+          if (st == 4 || st == 5) return {2, "Shard " + std::to_string(i) + " write failed: " + fmsg};
+        }
+      }
+      pb::WriteBlockRequest req;
+      req.block_id = alloc.block.block_id;
+      req.data.assign(reinterpret_cast<const char*>(p), sl);
+      req.expected_checksum_crc32c = crc;
+      req.shard_index = i;
+      req.master_term = alloc.master_term;
+      GrpcResult r = grpc_.call(addr, "/dfs.ChunkServerService/WriteBlock", req.str(), rid);
+      if (!r.transport_ok) return {1, r.message};
+      pb::WriteBlockResponse resp;
+      if (r.status != 0 || !resp.decode(r.message) || !resp.success)
+        return {2, "Shard " + std::to_string(i) + " write failed: " + (r.status ? r.message : resp.error_message)};
+      return {0, ""};
+    }));
+  }
+  int worst = 0;
+  std::string why;
+  for (auto& f : futs) {
+    auto r = f.get();
+    if (r.first > worst) {
+      worst = r.first;
+      why = r.second;
+    }
+  }
+  if (worst == 1) return NotHandled;  // a server we cannot reach natively: the Python path redoes it
+  if (worst == 2) {
+    *msg = why;
+    return Failed;
+  }
+  pb::CompleteFileRequest done;
+  done.path = path;
+  done.size = n;
+  done.etag_md5 = "";  // the reference leaves EC files without an ETag
+  done.created_at_ms = static_cast<uint64_t>(now_ms());
+  pb::BlockChecksumInfo sum;
+  sum.block_id = alloc.block.block_id;
+  sum.checksum_crc32c = crc32(data, n);
+  sum.actual_size = n;
+  done.block_checksums.push_back(sum);
+  done.create = true;
+  done.ec_data_shards = k;
+  done.ec_parity_shards = m;
+  done.blocks.push_back(alloc.block);
+  if (!call(sock, "/dfs.MasterService/CompleteFile", rid, done.str(), &code, &raw) || code != 0) {
+    *msg = "Failed to complete file: " + (code ? raw : std::string("master connection lost"));
+    return Failed;
+  }
+  pb::CompleteFileResponse dresp;
+  dresp.decode(raw);
+  if (!dresp.success) {
+    *msg = dresp.error_message.empty() ? "Failed to complete file" : "Failed to create file: " + dresp.error_message;
+    return Failed;
+  }
+  writes_++;
+  return Ok;
+}
+
+FastClient::Status FastClient::read_ec(const std::string& meta_pb, int64_t* slot, uint64_t* n, std::string* msg,
+                                       const std::string& rid, uint64_t offset, uint64_t length) {
+  TraceRange tr("dfs.client.read_ec");
+  pb::FileMetadata m;
+  if (!m.decode(meta_pb) || m.blocks.size() != 1) return NotHandled;
+  const pb::BlockInfo& b = m.blocks[0];
+  const int k = b.ec_data_shards, mm = b.ec_parity_shards;
+  const uint64_t orig = b.original_size ? b.original_size : m.size;
+  if (k <= 0 || mm <= 0 || b.locations.size() != static_cast<size_t>(k + mm) || orig == 0) return NotHandled;
+  const uint64_t sl = (orig + k - 1) / k, stride = (sl + 15) / 16 * 16;
+  if (stride * (2 * k + mm) > slot_bytes_) return NotHandled;
+  if (length > 0 && offset >= orig) return NotHandled;
+  int64_t s = acquire(slot_bytes_);
+  if (s < 0) return NotHandled;
+  uint8_t* base = base_ + s;
+  std::vector<std::future<bool>> futs;
+  for (int i = 0; i < k + mm; ++i) {
+    futs.push_back(shard_pool_.submit([this, i, s, base, stride, sl, &b, rid]() -> bool {
+      RequestScope scope(rid);
+      const std::string addr = strip_scheme(b.locations[i]);
+      if (addr.empty()) return false;  // a shard known lost
+      const std::string fps = peer_fastpath(addr);
+      if (!fps.empty()) {
+        std::string body;
+        put<uint64_t>(body, 0);
+        put<uint64_t>(body, 0);
+        put<uint64_t>(body, static_cast<uint64_t>(s) + i * stride);
+        put<uint64_t>(body, stride);
+        put_str(body, b.block_id);
+        put_str(body, arena_path_);
+        put_str(body, rid);
+        uint8_t st;
+        uint64_t total, got;
+        std::string fmsg;
+        if (fp_call_to(fps, 2, body, &st, &total, &got, &fmsg) && st == 0 && got == sl) return true;
+      }
+      pb::ReadBlockRequest req;
+      req.block_id = b.block_id;
+      GrpcResult r = grpc_.call(addr, "/dfs.ChunkServerService/ReadBlock", req.str(), rid);
+      pb::ReadBlockResponse resp;
+      if (!r.transport_ok || r.status != 0 || !resp.decode(r.message) || resp.data.size() != sl) return false;
+      std::memcpy(base + i * stride, resp.data.data(), sl);
+      return true;
+    }));
+  }
+  std::vector<int> present, missing;
+  for (int i = 0; i < k + mm; ++i)
+    if (futs[i].get()) present.push_back(i);
+    else if (i < k) missing.push_back(i);
+  if (!missing.empty()) {
+    if (static_cast<int>(present.size()) < k) {
+      release(s);
+      *msg = "RS reconstruct error: TooFewShardsPresent";
+      return Failed;
+    }
+    std::vector<int> use(present.begin(), present.begin() + k);
+    gf::Matrix rows = gf::rs_decode_rows(k, mm, use, missing);
+    std::vector<uint16_t> idx(use.begin(), use.end());
+    const uint64_t out_off = static_cast<uint64_t>(s) + (k + mm) * stride;
+    ec_matmul(rows, k, sl, static_cast<uint64_t>(s), out_off, &idx, rid);
+    for (size_t r = 0; r < missing.size(); ++r)
+      std::memcpy(base + missing[r] * stride, base_ + out_off + r * stride, sl);
+    ec_degraded_++;
+  }
+  for (int c = 1; c < k; ++c) std::memmove(base + c * sl, base + c * stride, sl);  // stripes back to back
+  uint64_t from = 0, want = orig;
+  if (length > 0) {
+    from = offset;
+    want = std::min<uint64_t>(length, orig - offset);
+  }
+  *slot = s + static_cast<int64_t>(from);
+  *n = want;
   reads_++;
   return Ok;
 }

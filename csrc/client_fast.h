@@ -24,6 +24,8 @@
 #include <thread>
 #include <vector>
 
+#include "grpc_client.h"
+#include "io_pool.h"
 #include "shard_map.h"
 
 namespace dfs {
@@ -74,6 +76,18 @@ class FastClient {
                     const std::string& rid, uint64_t offset, uint64_t length);
   Status remove(const std::string& path, std::string* msg, const std::string& rid);
 
+  // Erasure-coded file (reference mod.rs:308-412): the data is striped into k shards in a
+  // slot, the m parity shards are computed by the co-located chunkserver's GPU (fast-path op
+  // 6, the CPU codec when it has none), and the k + m shards go to their servers in parallel
+  // — same-host servers read them straight from our slot through their own fast path, others
+  // get a gRPC WriteBlock. Degraded reads (mod.rs:1110-1165) gather the survivors into a slot
+  // and decode the missing data shards on the GPU from the layout as fetched.
+  Status write_ec(const std::string& path, const uint8_t* data, size_t n, int k, int m, std::string* msg,
+                  const std::string& rid);
+  uint64_t ec_gpu_ops() const { return ec_gpu_.load(); }
+  uint64_t ec_cpu_ops() const { return ec_cpu_.load(); }
+  uint64_t ec_degraded_reads() const { return ec_degraded_.load(); }
+
   uint64_t writes() const { return writes_.load(); }
   uint64_t reads() const { return reads_.load(); }
 
@@ -86,6 +100,13 @@ class FastClient {
             std::string* resp);
   bool fp_call(uint8_t op, const std::string& body, uint8_t* status, uint64_t* total, uint64_t* nbytes,
                std::string* msg);
+  bool fp_call_to(const std::string& sock, uint8_t op, const std::string& body, uint8_t* status, uint64_t* total,
+                  uint64_t* nbytes, std::string* msg);
+  std::string peer_fastpath(const std::string& addr) const;  // "" unless `addr` is on this host
+  bool ec_matmul(const std::vector<std::vector<uint8_t>>& mat, int k, uint64_t len, uint64_t in_off, uint64_t out_off,
+                 const std::vector<uint16_t>* idx, const std::string& rid);
+  Status read_ec(const std::string& meta_pb, int64_t* slot, uint64_t* n, std::string* msg, const std::string& rid,
+                 uint64_t offset, uint64_t length);
   int take_conn(const std::string& name);
   void give_conn(const std::string& name, int fd);
   void hash_loop();
@@ -113,7 +134,9 @@ class FastClient {
   std::vector<std::thread> hashers_;
   bool stop_ = false;
 
-  std::atomic<uint64_t> writes_{0}, reads_{0};
+  std::atomic<uint64_t> writes_{0}, reads_{0}, ec_gpu_{0}, ec_cpu_{0}, ec_degraded_{0};
+  GrpcChannelPool grpc_{120000};  // shard I/O with servers on other hosts
+  IoPool shard_pool_{8};         // last: destroyed first, after in-flight shard I/O
 };
 
 }  // namespace dfs

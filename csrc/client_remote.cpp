@@ -295,12 +295,62 @@ FastClient::Status RemoteClient::read(const std::string& path, std::string* out,
   rreq.offset = offset;
   rreq.length = length;
   const std::string wire = rreq.str();
-  for (const std::string& loc : b.locations) {
+  auto fetch = [this, wire, rid, want = rreq.length](const std::string& loc, std::string* data) {
     GrpcResult r = pool_.call(loc, "/dfs.ChunkServerService/ReadBlock", wire, rid);
-    if (!r.transport_ok || r.status != 0) continue;  // corrupt / missing / down: next replica
+    if (!r.transport_ok || r.status != 0) return false;  // corrupt / missing / down
     pb::ReadBlockResponse resp;
-    if (!resp.decode(r.message) || resp.data.size() != rreq.length) continue;
-    *out = std::move(resp.data);
+    if (!resp.decode(r.message) || resp.data.size() != want) return false;
+    *data = std::move(resp.data);
+    return true;
+  };
+  size_t next = 0;
+  const int hedge = hedge_ms_.load();
+  if (hedge > 0 && b.locations.size() >= 2) {
+    // Hedged read (reference mod.rs:948-1107): the primary, and after `hedge` ms without an
+    // answer the second replica as well; the first clean answer wins, a late one is dropped.
+    struct Race {
+      std::mutex mu;
+      std::condition_variable cv;
+      int finished = 0;
+      bool won = false;
+      std::string data;
+    };
+    auto race = std::make_shared<Race>();
+    auto launch = [&](const std::string& loc) {
+      hedge_pool_.submit([race, fetch, loc] {
+        std::string d;
+        bool ok = fetch(loc, &d);
+        std::lock_guard<std::mutex> g(race->mu);
+        race->finished++;
+        if (ok && !race->won) {
+          race->won = true;
+          race->data = std::move(d);
+        }
+        race->cv.notify_all();
+      });
+    };
+    launch(b.locations[0]);
+    int launched = 1;
+    std::unique_lock<std::mutex> lk(race->mu);
+    if (!race->cv.wait_for(lk, std::chrono::milliseconds(hedge), [&] { return race->won || race->finished == 1; }) ||
+        !race->won) {
+      lk.unlock();
+      launch(b.locations[1]);
+      launched = 2;
+      hedged_++;
+      lk.lock();
+    }
+    race->cv.wait(lk, [&] { return race->won || race->finished == launched; });
+    if (race->won) {
+      *out = std::move(race->data);
+      t->read = since(clk);
+      reads_++;
+      return FastClient::Ok;
+    }
+    next = 2;  // both raced replicas failed: the rest in order
+  }
+  for (size_t i = next; i < b.locations.size(); ++i) {
+    if (!fetch(b.locations[i], out)) continue;  // next replica
     t->read = since(clk);
     reads_++;
     return FastClient::Ok;

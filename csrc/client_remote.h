@@ -24,6 +24,7 @@
 
 #include "client_fast.h"
 #include "grpc_client.h"
+#include "io_pool.h"
 #include "tls.h"
 #include "shard_map.h"
 
@@ -50,6 +51,9 @@ class RemoteClient {
   uint64_t writes() const { return writes_.load(); }
   uint64_t reads() const { return reads_.load(); }
   uint64_t connects() const { return pool_.connects(); }
+  // Hedged reads (Client::with_hedge_delay): 0 = off.
+  void set_hedge_delay(int ms) { hedge_ms_.store(ms); }
+  uint64_t hedged() const { return hedged_.load(); }
 
  private:
   // A MasterService call on the path's shard, following Not Leader hints; `*code` = -1 on
@@ -72,7 +76,9 @@ class RemoteClient {
   std::vector<std::thread> hashers_;
   bool stop_ = false;
 
-  std::atomic<uint64_t> writes_{0}, reads_{0};
+  std::atomic<uint64_t> writes_{0}, reads_{0}, hedged_{0};
+  std::atomic<int> hedge_ms_{0};
+  IoPool hedge_pool_{2};  // last: destroyed first, after its in-flight reads finished
 };
 
 }  // namespace dfs

@@ -457,8 +457,43 @@ bool FastPathServer::control(int rank, const std::string& blob, std::string* rep
   return true;
 }
 
+std::vector<std::string> FastPathServer::drain_healed() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> out;
+  out.swap(healed_);
+  return out;
+}
+
+int FastPathServer::replicate_block(const std::string& id, const std::vector<std::string>& targets, uint64_t term,
+                                    std::vector<std::string>* done) {
+  TraceRange tr("dfs.fp.heal_copy");
+  if (repl_ == nullptr || !store_->exists(id)) return 0;
+  const uint32_t crc = store_->block_crc(id);
+  std::vector<uint8_t> host;
+  if (!store_->gpu()) {  // host store: the socket transport sends from host memory
+    ReadResult st = store_->stat(id, 0, 0);
+    if (st.status != ReadStatus::Ok) return 0;
+    host.resize(st.bytes);
+    ReadResult rr = store_->read_into(id, 0, st.bytes, host.data());
+    if (rr.status != ReadStatus::Ok || rr.partial_corrupt) return 0;
+  }
+  int total = 0;
+  for (const auto& t : targets) {
+    Peer* p = local_peer(t);
+    if (p == nullptr || p->rank < 0 || !repl_->pair_ok(p->rank)) continue;
+    int n = replicate_one(t, id, crc, term, ShmSrc{}, host.empty() ? nullptr : host.data(), host.size(), true);
+    if (n > 0) {
+      done->push_back(t);
+      std::lock_guard<std::mutex> g(mu_);
+      st_.heals_out++;
+    }
+    total += n;
+  }
+  return total;
+}
+
 int FastPathServer::replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term,
-                                  const ShmSrc& src, const uint8_t* host, uint64_t n) {
+                                  const ShmSrc& src, const uint8_t* host, uint64_t n, bool heal) {
   Peer* p = local_peer(addr);
   if (p == nullptr) return 0;
   std::vector<uint8_t> resp;
@@ -488,6 +523,7 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
       put_str(req, id);
       put<uint16_t>(req, 0);  // fan-out: the replica forwards nowhere
       put_str(req, t_request_id);
+      put<uint8_t>(req, heal ? 1 : 0);  // a heal copy: the receiver reports the new location
       finish_frame(req);
       bool io_ok;
       int drop = drop_descriptors_.load();
@@ -668,6 +704,7 @@ void FastPathServer::serve(int fd) {
       std::string id = rd.str();
       std::vector<std::string> next = read_list(rd, false);
       std::string rid = rd.p < rd.end ? rd.str() : std::string();
+      const bool heal = rd.p < rd.end && rd.get<uint8_t>() == 1;
       RequestScope rs(rid);
       note_rid(rid);
       if (!rd.ok || id.empty() || repl_ == nullptr || size > kMaxTransfer) {
@@ -686,6 +723,11 @@ void FastPathServer::serve(int fd) {
           sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
         } else {
           bump(&FpStats::replicas_in);
+          if (heal) {
+            std::lock_guard<std::mutex> g(mu_);
+            healed_.push_back(id);
+            st_.heals_in++;
+          }
           sent = last ? send_response(fd, FpStatus::Ok, size, 1, "")
                       : persist_and_forward(id, nullptr, size, crc, term, next, ShmSrc{});
         }
@@ -726,16 +768,27 @@ void FastPathServer::serve(int fd) {
       uint64_t len = rd.get<uint64_t>(), in_off = rd.get<uint64_t>(), out_off = rd.get<uint64_t>();
       std::string mat = rd.str(), path = rd.str();
       std::string rid = rd.p < rd.end ? rd.str() : std::string();
+      // optional: the k inputs sit at in_off + idx[c] * stride (a degraded read decodes
+      // straight from the shard layout it fetched, survivors need not be adjacent)
+      std::vector<uint16_t> idx;
+      if (rd.p < rd.end) {
+        uint16_t ni = rd.get<uint16_t>();
+        for (uint16_t i = 0; rd.ok && i < ni && i <= kMaxShards * 2; ++i) idx.push_back(rd.get<uint16_t>());
+        if (idx.size() != k) rd.ok = false;
+      }
       RequestScope rs(rid);
       note_rid(rid);
       TraceRange tr("dfs.fp.ec");
       const uint64_t stride = (len + 15) / 16 * 16;
       std::string err;
       uint8_t* base = nullptr;
+      uint64_t span = k;
+      for (uint16_t v : idx) span = std::max<uint64_t>(span, uint64_t(v) + 1);
+      if (span > 2 * kMaxShards) rd.ok = false;
       // Each region is bounded on its own before any pointer is formed: offsets near 2^64
       // must not wrap into a small span (len <= kMaxTransfer and k, rows <= kMaxShards keep
       // stride * k far below 2^62, so only the offsets need checking).
-      const uint64_t in_len = stride * k, out_len = stride * rows;
+      const uint64_t in_len = stride * span, out_len = stride * rows;
       const bool regions_ok = in_off <= (1ull << 62) && out_off <= (1ull << 62);
       if (!rd.ok || k == 0 || rows == 0 || k > kMaxShards || rows > kMaxShards || mat.size() != size_t(k) * rows ||
           len > kMaxTransfer || !regions_ok) {
@@ -752,7 +805,7 @@ void FastPathServer::serve(int fd) {
           for (int c = 0; c < k; ++c) M[r][c] = static_cast<uint8_t>(mat[r * k + c]);
         std::vector<const uint8_t*> in(k);
         std::vector<uint8_t*> out(rows);
-        for (int c = 0; c < k; ++c) in[c] = base + in_off + c * stride;
+        for (int c = 0; c < k; ++c) in[c] = base + in_off + (idx.empty() ? c : idx[c]) * stride;
         for (int r = 0; r < rows; ++r) out[r] = base + out_off + r * stride;
         bool ok = store_->gf_matmul_gpu(M, in, out, len);
         if (ok) bump(&FpStats::ec_ops);

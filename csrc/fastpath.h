@@ -72,6 +72,7 @@ struct FpStats {
   uint64_t replica_failures = 0;  // replicas that could not be written (not counted)
   uint64_t p2p_fallbacks = 0;     // replicas moved to shared memory after a P2P failure
   uint64_t ec_ops = 0;            // erasure-coding matrix products run for clients
+  uint64_t heals_out = 0, heals_in = 0;  // heal / balancer copies sent / received on the engine
 };
 
 class FastPathServer {
@@ -111,6 +112,16 @@ class FastPathServer {
   bool persist_and_replicate(const std::string& id, const uint8_t* host, uint64_t n, uint32_t crc, uint64_t term,
                              const std::vector<std::string>& next, int* downstream, std::string* err);
   void add_suspect(const std::string& id);
+  // Heal / balancer / shuffle copy (master REPLICATE command; reference chunkserver.rs:462-499)
+  // of a block held here to same-node `targets`, payload over the replication engine (HBM ->
+  // HBM on device transports), descriptor on the peers' fast-path sockets. Returns the
+  // replicas written; a target that is not reachable this way counts 0 (the caller falls
+  // back to gRPC for it).
+  int replicate_block(const std::string& id, const std::vector<std::string>& targets, uint64_t term,
+                      std::vector<std::string>* done);
+  // Blocks received as heal copies since the last call (reported to the masters as new
+  // locations by the heartbeat).
+  std::vector<std::string> drain_healed();
   void note_rid(const std::string& rid);  // record a served request id (recent_request_ids)
   // Test hook: the next `n` REPL descriptors are dropped on the way out.
   void debug_drop_descriptors(int n) { drop_descriptors_ += n; }
@@ -136,7 +147,7 @@ class FastPathServer {
   void replicate(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
                  const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas);
   int replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term, const ShmSrc& src,
-                    const uint8_t* host, uint64_t n);
+                    const uint8_t* host, uint64_t n, bool heal = false);
   bool exchange_with(struct Peer* p, const std::vector<uint8_t>& req, std::vector<uint8_t>* resp);
   Peer* local_peer(const std::string& addr);
 
@@ -159,6 +170,7 @@ class FastPathServer {
   int pending_regs_ = 0;  // arena registrations in flight (mu_); stop() waits for them
   std::vector<Mapping> retired_;
   std::vector<std::string> suspects_;
+  std::vector<std::string> healed_;  // heal copies received (mu_), drained by the heartbeat
   std::vector<std::string> recent_rids_;  // ring of the last kRecentRids request ids (mu_)
   size_t recent_pos_ = 0;
   FpStats st_;

@@ -321,6 +321,14 @@ class ChunkServer:
         if not self.store.exists(block_id):
             log.error("REPLICATE: block %s not held here", block_id)
             return False
+        if self.fastpath is not None and self.rccl is not None:
+            # same-node target with a P2P pair: the copy runs on the replication engine (HBM ->
+            # HBM over xGMI on GPUs), the descriptor on the target's fast-path socket, no Python
+            # on the receiving side (VERDICT r2 item 6 / SURVEY M7)
+            n, _done = self.fastpath.replicate_block(block_id, [strip_scheme(target)], self.known_term)
+            if n > 0:
+                self.stats["rccl_forwards"] += 1
+                return True
         n = self.forward(block_id, None, [target], 0, self.known_term, heal=True)
         return n > 0
 
@@ -415,9 +423,10 @@ class ChunkServer:
     def drain_reports(self) -> tuple[list[str], list[str], list[str], list[str], list[str]]:
         """(bad blocks, new blocks, EC jobs finished, EC jobs failed, EC shards rebuilt) for
         the next heartbeat."""
+        healed = self.fastpath.drain_healed() if self.fastpath is not None else []
         with self._lists_lock:
             bad, self.pending_bad_blocks = self.pending_bad_blocks, []
-            new, self.new_blocks = self.new_blocks, []
+            new, self.new_blocks = self.new_blocks + healed, []
             enc, self.ec_encoded = self.ec_encoded, []
             fail, self.ec_failed = self.ec_failed, []
             rebuilt, self.ec_rebuilt = self.ec_rebuilt, []

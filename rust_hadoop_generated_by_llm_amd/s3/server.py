@@ -180,6 +180,8 @@ class S3Gateway:
         self.m_jwks_dur = r.histogram("iam_oidc_jwks_fetch_duration_seconds", "JWKS fetch latency")
         self.m_jwks_last = r.gauge("iam_oidc_jwks_last_fetch_timestamp", "Last successful JWKS fetch (unix s)")
         self._sts_sessions: list[float] = []
+        self.m_client_fallbacks = r.gauge("dfs_client_native_fallbacks", "Gateway DFS-client operations that left "
+                                          "the native client for the Python path, by reason", ("reason",))
 
     # ------------------------------------------------------------------ plumbing
     async def run(self, fn, *args):
@@ -241,6 +243,8 @@ class S3Gateway:
         now = time.time()
         self._sts_sessions = [t for t in self._sts_sessions if t > now]
         self.m_sts_active.set(len(self._sts_sessions))
+        for reason, n in dict(getattr(self.client, "native_fallbacks", {})).items():
+            self.m_client_fallbacks.set(n, labels={"reason": reason})
         lines = []
         for m in self.registry._metrics:  # noqa: SLF001 - registry is ours
             lines.extend(m.render())

@@ -418,12 +418,15 @@ def test_tiering_moves_cold_and_converts_to_ec():
         c.close()
 
 
-def test_healer_rereplicates_and_rebuilds_ec_shards():
+@pytest.mark.parametrize("p2p", [None, "socket"])
+def test_healer_rereplicates_and_rebuilds_ec_shards(p2p):
     """C29: a chunkserver that stops heartbeating is dropped after DFS_CS_DEAD_MS; the
     healer REPLICATEs its replicated blocks to a spare server and RECONSTRUCTs its EC
-    shard there, the rebuilt shard taking the dead server's position in the location list."""
+    shard there, the rebuilt shard taking the dead server's position in the location list.
+    With the replication engine (p2p="socket": the protocol of the device transports on the
+    CPU) the heal copy is a native engine transfer, not a gRPC ReplicateBlock."""
     env = {"DFS_CS_DEAD_MS": "2000"}
-    with LocalCluster(n_chunkservers=4, fsync=False, fast_intervals=True, env=env) as cl:
+    with LocalCluster(n_chunkservers=4, fsync=False, fast_intervals=True, env=env, p2p=p2p) as cl:
         c = cl.client()
         rep, ec = os.urandom(300_000), os.urandom(500_003)
         c.create_file_from_buffer(rep, "/heal/rep")
@@ -448,6 +451,10 @@ def test_healer_rereplicates_and_rebuilds_ec_shards():
         assert c.read_block_from_location(spare, eb.block_id) is not None
         assert c.get_file_content("/heal/rep") == rep
         assert c.get_file_content("/heal/ec") == ec
+        if p2p == "socket":
+            st = [json.load(urllib.request.urlopen(f"{u}/stats")) for i, u in enumerate(cl.cs_http)
+                  if cl.cs_addrs[i] != dead]
+            assert sum(x["fp_heals_out"] for x in st) >= 1 and sum(x["fp_heals_in"] for x in st) >= 1, st
         c.close()
 
 
@@ -645,4 +652,30 @@ def test_network_partition_isolates_leader_then_heals():
         c.create_file_from_buffer(b"after", "/np/after")
         assert c.get_file_content("/np/after") == b"after"
         pool.close()
+        c.close()
+
+
+def test_native_hedged_read_races_a_stalled_replica():
+    """hedged reads run in the native remote client (csrc/client_remote.cpp,
+    reference mod.rs:948-1107). The primary replica's process is frozen (SIGSTOP): after the
+    hedge delay the second replica is asked too and its answer wins."""
+    import signal as sig
+
+    with LocalCluster(n_chunkservers=2, fsync=False) as cl:
+        c = cl.client(hedge_delay_ms=50)
+        assert c._remote is not None
+        data = os.urandom(200_000)
+        c.create_file_from_buffer(data, "/hedge/f")
+        primary = strip_scheme(c.get_file_info("/hedge/f").blocks[0].locations[0])
+        proc = next(p for p in cl.procs if p.name == f"cs{cl.cs_addrs.index(primary)}")
+        ops0, fb0 = c.remote_ops, dict(c.native_fallbacks)
+        os.kill(proc.popen.pid, sig.SIGSTOP)
+        try:
+            t0 = time.time()
+            assert c.get_file_content("/hedge/f") == data
+            assert time.time() - t0 < 5
+        finally:
+            os.kill(proc.popen.pid, sig.SIGCONT)
+        assert c._remote.hedged == 1 and c.remote_ops == ops0 + 1
+        assert c.native_fallbacks == fb0  # served natively, no Python fallback
         c.close()

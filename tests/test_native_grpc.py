@@ -216,3 +216,46 @@ def test_native_remote_client_interop(native, server_impl):
             assert ok and code == 12  # UNIMPLEMENTED from either server
         finally:
             c.close()
+
+
+@pytest.mark.slow
+def test_native_client_erasure_coding_write_and_degraded_read(native):
+    """EC files on the native client (csrc/client_fast.cpp write_ec /
+    read_ec; reference mod.rs:308-412, 1110-1165). Stripes live in the client's slot, parity
+    comes from the co-located chunkserver's codec (op 6: GPU, or the CPU codec on a host
+    store), the k+m shards go out in parallel (same-host servers read them from the slot
+    through their own fast path), and a read with a shard server down decodes natively."""
+    from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster
+    from rust_hadoop_generated_by_llm_amd.ops import erasure
+
+    with LocalCluster(n_chunkservers=4, fsync=False) as cl:
+        c = cl.client(local_chunkserver=cl.cs_addrs[0])
+        try:
+            assert c._fast is not None
+            ops0 = c.fp_ops
+            blobs = {f"/nec/f{i}": os.urandom(n) for i, n in enumerate([1, 100_001, 3 << 20])}
+            for p, d in blobs.items():
+                c.create_file_from_buffer_ec(d, p, 2, 1)
+            for p, d in blobs.items():
+                assert c.get_file_content(p) == d
+                info = c.get_file_info(p)
+                assert info.blocks[0].ec_data_shards == 2 and len(info.blocks[0].locations) == 3
+            assert c.fp_ops - ops0 == 2 * len(blobs) and c.native_fallbacks == {}
+            # the shards are exactly the reference codec's (bit-compatible with galois_8)
+            d = blobs["/nec/f1"]
+            b = c.get_file_info("/nec/f1").blocks[0]
+            want = erasure.encode(d, 2, 1, None)
+            for i, loc in enumerate(b.locations):
+                assert c.read_block_from_location(loc, b.block_id) == want[i]
+            # degraded: kill the server of a data shard (not our co-located one) -> native decode
+            big = blobs["/nec/f2"]
+            locs = list(c.get_file_info("/nec/f2").blocks[0].locations)
+            victim = next(loc for loc in locs[:2] if loc != cl.cs_addrs[0])
+            cl.kill(f"cs{cl.cs_addrs.index(victim)}")
+            deg0 = c._fast.ec_degraded_reads
+            assert c.get_file_content("/nec/f2") == big
+            assert c.read_file_range("/nec/f2", 1_000_001, 77_777) == big[1_000_001:1_077_778]
+            assert c._fast.ec_degraded_reads - deg0 == 2
+            assert c._fast.ec_gpu_ops + c._fast.ec_cpu_ops >= len(blobs)
+        finally:
+            c.close()
