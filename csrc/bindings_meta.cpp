@@ -793,6 +793,18 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("reads", &RemoteClient::reads)
       .def_property_readonly("connects", &RemoteClient::connects)
       .def_property_readonly("hedged", &RemoteClient::hedged)
+      .def_property_readonly("ec_degraded_reads", &RemoteClient::ec_degraded_reads)
+      .def("write_ec", [](RemoteClient& c, const std::string& path, py::buffer data, int k, int m, const std::string& rid) {
+        py::buffer_info bi = data.request();
+        std::string msg;
+        FastClient::Status st;
+        {
+          py::gil_scoped_release r;
+          st = c.write_ec(path, static_cast<const uint8_t*>(bi.ptr), static_cast<size_t>(bi.size * bi.itemsize), k, m,
+                          &msg, rid);
+        }
+        return py::make_tuple(static_cast<int>(st), msg);
+      }, py::arg("path"), py::arg("data"), py::arg("k"), py::arg("m"), py::arg("request_id") = "")
       .def("set_hedge_delay", &RemoteClient::set_hedge_delay)
       .def("set_routing", &RemoteClient::set_routing, py::call_guard<py::gil_scoped_release>())
       .def("write", [](RemoteClient& c, const std::string& path, py::buffer data, const std::string& rid,

@@ -1,5 +1,6 @@
 // Native remote client; design notes in client_remote.h.
 #include "client_remote.h"
+#include "gf256.h"
 
 #include <openssl/evp.h>
 
@@ -281,7 +282,12 @@ FastClient::Status RemoteClient::read(const std::string& path, std::string* out,
     reads_++;
     return FastClient::Ok;
   }
-  if (m.blocks.size() != 1 || m.blocks[0].ec_data_shards > 0) return FastClient::NotHandled;
+  if (m.blocks.size() == 1 && m.blocks[0].ec_data_shards > 0) {
+    FastClient::Status st = read_ec(m, out, msg, rid, offset, length);
+    if (st == FastClient::Ok) t->read = since(clk);
+    return st;
+  }
+  if (m.blocks.size() != 1) return FastClient::NotHandled;
   if (length > 0) {
     if (offset >= m.size) return FastClient::NotHandled;  // the Python path reports the range error
     length = std::min<uint64_t>(length, m.size - offset);
@@ -356,6 +362,166 @@ FastClient::Status RemoteClient::read(const std::string& path, std::string* out,
     return FastClient::Ok;
   }
   return FastClient::NotHandled;  // no replica answered cleanly: the Python path recovers / reports
+}
+
+
+FastClient::Status RemoteClient::write_ec(const std::string& path, const uint8_t* data, size_t n, int k, int m,
+                                          std::string* msg, const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? request_id() : rid_in;
+  RequestScope rs(rid);
+  TraceRange tr("dfs.remote.write_ec");
+  if (k <= 0 || m <= 0 || k + m > 32 || n == 0) return FastClient::NotHandled;
+  pb::CreateFileRequest creq;
+  creq.path = path;
+  creq.ec_data_shards = k;
+  creq.ec_parity_shards = m;
+  creq.allocate_block = true;
+  creq.defer_create = true;
+  int code;
+  std::string raw;
+  if (!master_call(path, "CreateFile", creq.str(), rid, &code, &raw)) return FastClient::NotHandled;
+  if (code == kOutOfRange || code == kFailedPrecondition || code == 14) return FastClient::NotHandled;
+  if (code != 0) {
+    *msg = "Failed to create file: " + raw;
+    return FastClient::Failed;
+  }
+  pb::CreateFileResponse cresp;
+  if (!cresp.decode(raw)) return FastClient::NotHandled;
+  if (!cresp.success) {
+    if (cresp.error_message == "Not Leader") return FastClient::NotHandled;
+    *msg = "Failed to create file: " + cresp.error_message;
+    return FastClient::Failed;
+  }
+  if (!cresp.has_allocation || !cresp.allocation.has_block || !cresp.deferred) return FastClient::NotHandled;
+  const pb::AllocateBlockResponse& alloc = cresp.allocation;
+  if (alloc.ec_data_shards != k || alloc.ec_parity_shards != m ||
+      alloc.chunk_server_addresses.size() != static_cast<size_t>(k + m)) {
+    *msg = "Expected " + std::to_string(k + m) + " chunk servers for EC(" + std::to_string(k) + "," +
+           std::to_string(m) + "), got " + std::to_string(alloc.chunk_server_addresses.size());
+    return FastClient::Failed;
+  }
+  const uint64_t sl = (n + k - 1) / k;
+  std::vector<std::string> shards(k + m, std::string(sl, '\0'));
+  for (int c = 0; c < k; ++c) {
+    const uint64_t off = c * sl;
+    if (off < n) std::memcpy(&shards[c][0], data + off, std::min<uint64_t>(sl, n - off));
+  }
+  gf::Matrix full = gf::rs_matrix(k, m), parity(full.begin() + k, full.end());
+  std::vector<const uint8_t*> in(k);
+  std::vector<uint8_t*> outp(m);
+  for (int c = 0; c < k; ++c) in[c] = reinterpret_cast<const uint8_t*>(shards[c].data());
+  for (int r = 0; r < m; ++r) outp[r] = reinterpret_cast<uint8_t*>(&shards[k + r][0]);
+  gf::matmul_cpu(parity, in.data(), outp.data(), sl);
+  std::vector<std::future<std::pair<int, std::string>>> futs;
+  for (int i = 0; i < k + m; ++i)
+    futs.push_back(hedge_pool_.submit([this, i, &shards, &alloc, rid]() -> std::pair<int, std::string> {
+      pb::WriteBlockRequest req;
+      req.block_id = alloc.block.block_id;
+      req.data = shards[i];
+      req.expected_checksum_crc32c = crc32(reinterpret_cast<const uint8_t*>(shards[i].data()), shards[i].size());
+      req.shard_index = i;
+      req.master_term = alloc.master_term;
+      GrpcResult r = pool_.call(alloc.chunk_server_addresses[i], "/dfs.ChunkServerService/WriteBlock", req.str(), rid);
+      if (!r.transport_ok) return {1, r.message};
+      pb::WriteBlockResponse resp;
+      if (r.status != 0 || !resp.decode(r.message) || !resp.success)
+        return {2, "Shard " + std::to_string(i) + " write failed: " + (r.status ? r.message : resp.error_message)};
+      return {0, ""};
+    }));
+  int worst = 0;
+  std::string why;
+  for (auto& f : futs) {
+    auto r = f.get();
+    if (r.first > worst) {
+      worst = r.first;
+      why = r.second;
+    }
+  }
+  if (worst == 1) return FastClient::NotHandled;
+  if (worst == 2) {
+    *msg = why;
+    return FastClient::Failed;
+  }
+  pb::CompleteFileRequest done;
+  done.path = path;
+  done.size = n;
+  done.created_at_ms = static_cast<uint64_t>(now_ms());
+  pb::BlockChecksumInfo sum;
+  sum.block_id = alloc.block.block_id;
+  sum.checksum_crc32c = crc32(data, n);
+  sum.actual_size = n;
+  done.block_checksums.push_back(sum);
+  done.create = true;
+  done.ec_data_shards = k;
+  done.ec_parity_shards = m;
+  done.blocks.push_back(alloc.block);
+  if (!master_call(path, "CompleteFile", done.str(), rid, &code, &raw) || code != 0) {
+    *msg = "Failed to complete file: " + (code > 0 ? raw : std::string("master unreachable"));
+    return FastClient::Failed;
+  }
+  pb::CompleteFileResponse dresp;
+  dresp.decode(raw);
+  if (!dresp.success) {
+    *msg = dresp.error_message.empty() ? "Failed to complete file" : "Failed to create file: " + dresp.error_message;
+    return FastClient::Failed;
+  }
+  writes_++;
+  return FastClient::Ok;
+}
+
+FastClient::Status RemoteClient::read_ec(const pb::FileMetadata& m, std::string* out, std::string* msg,
+                                         const std::string& rid, uint64_t offset, uint64_t length) {
+  const pb::BlockInfo& b = m.blocks[0];
+  const int k = b.ec_data_shards, mm = b.ec_parity_shards;
+  const uint64_t orig = b.original_size ? b.original_size : m.size;
+  if (k <= 0 || mm <= 0 || b.locations.size() != static_cast<size_t>(k + mm) || orig == 0) return FastClient::NotHandled;
+  if (length > 0 && offset >= orig) return FastClient::NotHandled;
+  const uint64_t sl = (orig + k - 1) / k;
+  std::vector<std::string> shards(k + mm);
+  std::vector<std::future<bool>> futs;
+  pb::ReadBlockRequest req;
+  req.block_id = b.block_id;
+  const std::string wire = req.str();
+  for (int i = 0; i < k + mm; ++i)
+    futs.push_back(hedge_pool_.submit([this, i, &b, &shards, wire, rid, sl]() -> bool {
+      if (b.locations[i].empty()) return false;
+      GrpcResult r = pool_.call(b.locations[i], "/dfs.ChunkServerService/ReadBlock", wire, rid);
+      pb::ReadBlockResponse resp;
+      if (!r.transport_ok || r.status != 0 || !resp.decode(r.message) || resp.data.size() != sl) return false;
+      shards[i] = std::move(resp.data);
+      return true;
+    }));
+  std::vector<int> present, missing;
+  for (int i = 0; i < k + mm; ++i)
+    if (futs[i].get()) present.push_back(i);
+    else if (i < k) missing.push_back(i);
+  if (!missing.empty()) {
+    if (static_cast<int>(present.size()) < k) {
+      *msg = "RS reconstruct error: TooFewShardsPresent";
+      return FastClient::Failed;
+    }
+    std::vector<int> use(present.begin(), present.begin() + k);
+    gf::Matrix rows = gf::rs_decode_rows(k, mm, use, missing);
+    std::vector<const uint8_t*> in(k);
+    std::vector<uint8_t*> outp(missing.size());
+    for (int c = 0; c < k; ++c) in[c] = reinterpret_cast<const uint8_t*>(shards[use[c]].data());
+    for (size_t r = 0; r < missing.size(); ++r) {
+      shards[missing[r]].assign(sl, '\0');
+      outp[r] = reinterpret_cast<uint8_t*>(&shards[missing[r]][0]);
+    }
+    gf::matmul_cpu(rows, in.data(), outp.data(), sl);
+    ec_degraded_++;
+  }
+  const uint64_t from = length > 0 ? offset : 0, want = length > 0 ? std::min<uint64_t>(length, orig - offset) : orig;
+  out->clear();
+  out->reserve(want);
+  for (uint64_t pos = from; pos < from + want;) {
+    const uint64_t c = pos / sl, o = pos % sl, take = std::min<uint64_t>(sl - o, from + want - pos);
+    out->append(shards[c], o, take);
+    pos += take;
+  }
+  reads_++;
+  return FastClient::Ok;
 }
 
 }  // namespace dfs

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "client_fast.h"
+#include "dfs_pb.h"
 #include "grpc_client.h"
 #include "io_pool.h"
 #include "tls.h"
@@ -51,6 +52,13 @@ class RemoteClient {
   uint64_t writes() const { return writes_.load(); }
   uint64_t reads() const { return reads_.load(); }
   uint64_t connects() const { return pool_.connects(); }
+  // Erasure-coded file from a client on another host (reference mod.rs:308-412): RS encode on
+  // this host's CPU (gf256.cpp, bit-compatible with galois_8), k + m WriteBlock calls in
+  // parallel; EC reads (mod.rs:1110-1165) gather the shards in parallel and decode when a
+  // data shard is missing.
+  Status write_ec(const std::string& path, const uint8_t* data, size_t n, int k, int m, std::string* msg,
+                  const std::string& rid);
+  uint64_t ec_degraded_reads() const { return ec_degraded_.load(); }
   // Hedged reads (Client::with_hedge_delay): 0 = off.
   void set_hedge_delay(int ms) { hedge_ms_.store(ms); }
   uint64_t hedged() const { return hedged_.load(); }
@@ -76,7 +84,9 @@ class RemoteClient {
   std::vector<std::thread> hashers_;
   bool stop_ = false;
 
-  std::atomic<uint64_t> writes_{0}, reads_{0}, hedged_{0};
+  Status read_ec(const pb::FileMetadata& m, std::string* out, std::string* msg, const std::string& rid, uint64_t offset,
+                 uint64_t length);
+  std::atomic<uint64_t> writes_{0}, reads_{0}, hedged_{0}, ec_degraded_{0};
   std::atomic<int> hedge_ms_{0};
   IoPool hedge_pool_{2};  // last: destroyed first, after its in-flight reads finished
 };

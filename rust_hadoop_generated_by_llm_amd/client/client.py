@@ -502,12 +502,17 @@ class Client:
     def create_file_from_buffer_ec(self, data: bytes, dest: str, ec_data_shards: int, ec_parity_shards: int) -> None:
         """RS(k,m) encode, scatter shard i to chunk_servers[i] in parallel, CompleteFile with
         the whole-buffer CRC and an empty etag (reference mod.rs:496-677)."""
-        if self._fast is not None:
-            # native: stripes in our slot, parity on the co-located GPU (op 6), k+m shard
-            # writes in parallel (client_fast.cpp write_ec)
-            st, msg = self._fast.write_ec(dest, data, ec_data_shards, ec_parity_shards, current_request_id.get())
+        fc = self._fast if self._fast is not None else self._remote
+        if fc is not None:
+            # native: co-located, stripes in our slot and parity on the local GPU (op 6); remote,
+            # the CPU codec; either way k+m shard writes in parallel (client_fast.cpp /
+            # client_remote.cpp write_ec)
+            st, msg = fc.write_ec(dest, data, ec_data_shards, ec_parity_shards, current_request_id.get())
             if st == 0:
-                self.fp_ops += 1
+                if fc is self._remote:
+                    self.remote_ops += 1
+                else:
+                    self.fp_ops += 1
                 return None
             if st == 2:
                 raise DfsError(msg)

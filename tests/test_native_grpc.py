@@ -209,9 +209,11 @@ def test_native_remote_client_interop(native, server_impl):
             with pytest.raises(DfsError, match="already exists"):
                 c.create_file_from_buffer(b"x", f"/nr/{server_impl}/f2")
             ops = c.remote_ops
-            c.create_file_from_buffer_ec(os.urandom(300_000), f"/nr/{server_impl}/ec", 2, 1)
-            assert len(c.get_file_content(f"/nr/{server_impl}/ec")) == 300_000  # EC: Python path
-            assert c.remote_ops == ops
+            ec = os.urandom(300_000)
+            c.create_file_from_buffer_ec(ec, f"/nr/{server_impl}/ec", 2, 1)
+            assert c.get_file_content(f"/nr/{server_impl}/ec") == ec  # EC natively too (CPU codec)
+            assert c.read_file_range(f"/nr/{server_impl}/ec", 149_990, 20) == ec[149_990:150_010]
+            assert c.remote_ops == ops + 3
             ok, code, msg = native.grpc_call(cl.master_addrs[0], "/dfs.MasterService/NoSuchMethod", b"")
             assert ok and code == 12  # UNIMPLEMENTED from either server
         finally:
