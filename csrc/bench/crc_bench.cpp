@@ -124,14 +124,17 @@ int main(int argc, char** argv) {
   bool first = true;
   for (uint64_t n : std::vector<uint64_t>{4096, 65536, 1ull << 20, 8ull << 20, 64ull << 20, total}) {
     if (n > total) continue;
-    for (int mf = 1; mf >= 0; --mf) {
-      set_crc_mfma(mf == 1);
+    for (int mf = 2; mf >= 0; --mf) {  // 2: the production size-based dispatch
+      set_crc_mfma(mf >= 1);
+      set_crc_lds_max_mib(mf == 2 ? kCrcLdsMaxMibDefault : 0);
       Run r = bench_block(d, n, t, dmeta, dpart, s, n >= (256ull << 20) ? std::max(3, iters / 10) : iters, host);
       std::printf("%s\n  {\"bytes\": %llu, \"impl\": \"%s\", \"us\": %.2f, \"GBps\": %.1f, \"of_stream\": %.3f, \"ok\": %s}",
-                  first ? "" : ",", static_cast<unsigned long long>(n), mf ? "mfma" : "lds_tables", r.us,
-                  n / r.us / 1e3, n / r.us / 1e3 / stream_gbps, r.ok ? "true" : "false");
+                  first ? "" : ",", static_cast<unsigned long long>(n),
+                  mf == 2 ? "dispatch" : (mf ? "mfma" : "lds_tables"), r.us, n / r.us / 1e3,
+                  n / r.us / 1e3 / stream_gbps, r.ok ? "true" : "false");
       first = false;
     }
+    set_crc_lds_max_mib(kCrcLdsMaxMibDefault);
   }
   std::printf("\n], \"scrub\": [");
   // K1b over total bytes as 1 MiB blocks (meta images from the K1 pass above)

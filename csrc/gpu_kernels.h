@@ -83,6 +83,10 @@ void gf_nibble_tables(const uint8_t* mat, int rows, int k, uint32_t* out);
 // K1/K2/K1b use the matrix-core chunk CRC unless DFS_CRC_MFMA=0 (the LDS slicing-by-16 path).
 bool crc_mfma_enabled();
 void set_crc_mfma(bool on);  // benchmarks / tests: pick the K1 implementation
+// K1/K2 blocks below this many MiB run the LDS-table kernel even with the matrix-core path
+// enabled (size-based dispatch; DFS_CRC_LDS_MAX_MIB, 0 = always the matrix cores).
+constexpr int kCrcLdsMaxMibDefault = 16;
+void set_crc_lds_max_mib(int mib);
 DevCrcTables* upload_crc_tables(hipStream_t s);
 int crc_grid_for(uint64_t ntiles, uint32_t has_tail);
 // Tile buffers per wave in the MFMA kernels' register ring (2..4; 2 = the 3-waves/SIMD

@@ -952,8 +952,25 @@ void set_crc_ring(int scrub_buffers, int tile_buffers) {
 // Ring depth of a K1/K2/K3 launch over `ntiles` tiles: a deep ring only pays once workgroups
 // have several tiles each (below kCrcRingMinTiles its longer prologue costs ~0.3 us per
 // launch, e.g. on 1 MiB blocks).
+// Size-based K1/K2 dispatch: below DFS_CRC_LDS_MAX_MIB (default 16 MiB) the LDS-table kernel
+// wins (its per-workgroup setup is smaller: 1 MiB 6.02 vs 6.47 us, 8 MiB 7.39 vs 8.89 us in
+// profiles/r2_crc4/crc_default.json); from 64 MiB up the matrix-core kernel is 1.3-1.9x faster.
+static std::atomic<int64_t> g_lds_max_mib{-1};
+
+void set_crc_lds_max_mib(int mib) { g_lds_max_mib.store(mib < 0 ? 0 : mib); }
+
+static uint64_t lds_max_tiles() {
+  int64_t mib = g_lds_max_mib.load(std::memory_order_relaxed);
+  if (mib < 0) {
+    const char* e = std::getenv("DFS_CRC_LDS_MAX_MIB");
+    long v = e ? std::atol(e) : kCrcLdsMaxMibDefault;
+    g_lds_max_mib.store(mib = v > 0 ? v : 0);
+  }
+  return static_cast<uint64_t>(mib) * (1ull << 20) / (kSlicesPerTile * 512ull);
+}
+
 static int ring_for(uint64_t ntiles) {
-  if (!crc_mfma_enabled()) return 0;
+  if (!crc_mfma_enabled() || ntiles < lds_max_tiles()) return 0;
   return ntiles >= kCrcRingMinTiles ? crc_tile_ring_buffers() : 2;
 }
 

@@ -35,6 +35,19 @@ def test_gpu_crc_matches_zlib(gstore, n):
     assert meta == ref_meta(d)
 
 
+@pytest.mark.parametrize("n", [511, 4096, (1 << 20) + 13, 8 << 20])
+def test_gpu_crc_matrix_core_kernel_below_the_dispatch_threshold(gstore, native, n):
+    """Blocks under 16 MiB run the LDS-table kernel by default (size-based dispatch); the
+    matrix-core kernel stays correct there too when forced (DFS_CRC_LDS_MAX_MIB=0)."""
+    native.set_crc_lds_max_mib(0)
+    try:
+        d = os.urandom(n)
+        crc, meta = gstore.gpu_crc(d)
+        assert crc == zlib.crc32(d) and meta == ref_meta(d)
+    finally:
+        native.set_crc_lds_max_mib(16)
+
+
 def test_gpu_crc_zero_and_pattern(gstore):
     for d in (b"\0" * (1 << 20), bytes(range(256)) * 4099):
         crc, meta = gstore.gpu_crc(d)
