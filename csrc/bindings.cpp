@@ -320,6 +320,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["mirror_hits"] = t.mirror_hits;
         d["mirror_bytes"] = t.mirror_bytes;
         d["io_threads_spawned"] = t.io_threads_spawned;
+        d["final_name_writes"] = t.final_name_writes;
         d["crc_mismatches"] = t.crc_mismatches;
         d["gpu_kernel_launches"] = t.gpu_kernel_launches;
         d["disk_gate_waits"] = t.disk_gate_waits;

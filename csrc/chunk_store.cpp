@@ -543,6 +543,30 @@ bool ChunkStore::sync_dir(bool cold) {
   return g == nullptr || g->sync();
 }
 
+bool ChunkStore::write_fd_durable(int fd, const uint8_t* p, uint64_t n, const std::string& what, std::string* err) {
+  if (!write_all(fd, p, n, 0)) {
+    *err = errno_str(what);
+    return false;
+  }
+  if (cfg_.sync_writes && ::fdatasync(fd) != 0) {
+    *err = errno_str("sync: " + what);
+    return false;
+  }
+  return true;
+}
+
+bool ChunkStore::claim_fresh(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (index_.count(id) || writing_.count(id)) return false;
+  writing_.insert(id);
+  return true;
+}
+
+void ChunkStore::unclaim_fresh(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  writing_.erase(id);
+}
+
 bool ChunkStore::write_file_durable(const std::string& path, const uint8_t* p, uint64_t n, std::string* err) {
   int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
   if (fd < 0) {
@@ -640,23 +664,62 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   // nvme-sync: the data file (the slow part: page-cache write + device flush) is written
   // and fdatasync'ed on a helper thread WHILE the GPU stages and checksums the block; the
   // .meta (known only after the CRC kernel) follows. A checksum mismatch removes the file.
-  std::future<bool> data_file;
+  std::future<bool> data_file, dir_file;
   std::string data_err;
-  // Both files go to private temporary names and are renamed over the block only after the
+  // A re-written id goes to private temporary names, renamed over the block only after the
   // checksum verified: a rejected or failed write never destroys an earlier durable copy
-  // of the same id (e.g. a retry on gRPC after a fast-path punt).
-  const std::string tmp_sfx = "." + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
+  // (e.g. a retry on gRPC after a fast-path punt). A fresh id — the common case, block ids
+  // are unique per allocation — is written under its final names like the reference's
+  // write-then-sync_all (chunkserver.rs:192-209): both names exist before any flush, so
+  // the directory fsync that makes them durable runs BESIDE the data and .meta flushes
+  // instead of after a rename (one device round trip on the ack path instead of two).
+  const bool fresh = sync_now && !gsync_ && claim_fresh(id);
+  const std::string tmp_sfx = fresh ? "" : "." + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
   const std::string dp_tmp = data_path(id, false) + tmp_sfx, mp_tmp = meta_path(id, false) + tmp_sfx;
-  if (sync_now && !gsync_) {
+  int dfd = -1, mfd = -1;
+  if (fresh) {
+    dfd = ::open(dp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    mfd = dfd < 0 ? -1 : ::open(mp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (mfd < 0) {
+      res.error = errno_str("open " + (dfd < 0 ? dp_tmp : mp_tmp));
+      if (dfd >= 0) ::close(dfd);
+      ::unlink(dp_tmp.c_str());
+      unclaim_fresh(id);
+      release(ext);
+      return res;
+    }
+    dir_file = io_.submit([this] { return sync_dir(false); });
+    data_file = io_.submit([this, dfd, data, n, &data_err] {
+      DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
+      return write_fd_durable(dfd, data, n, "write " + std::to_string(n) + " bytes", &data_err);
+    });
+  } else if (sync_now && !gsync_) {
     data_file = io_.submit([this, dp_tmp, data, n, &data_err] {
       DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
       return write_file_durable(dp_tmp, data, n, &data_err);
     });
   }
+  // the page-cache drop and the closes are off the ack path
+  auto close_fresh = [&] {
+    if (dfd < 0) return;
+    const bool drop = cfg_.sync_writes && gpu();
+    io_.submit([dfd, mfd, drop] {
+      if (drop) drop_cached(dfd);
+      ::close(dfd);
+      ::close(mfd);
+    });
+    dfd = mfd = -1;
+  };
   auto abandon_data_file = [&] {
     if (data_file.valid()) {
       data_file.get();
       ::unlink(dp_tmp.c_str());
+    }
+    if (dir_file.valid()) dir_file.get();
+    if (fresh) {
+      close_fresh();
+      ::unlink(mp_tmp.c_str());
+      unclaim_fresh(id);
     }
   };
   Lane* l = acquire_lane();
@@ -706,7 +769,25 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   }
   auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
   release_lane(l);
-  if (data_file.valid()) {
+  if (fresh) {
+    bool mok = write_fd_durable(mfd, meta->data(), S * 4, "write " + mp_tmp, &err);
+    bool dok = data_file.get();
+    bool sok = dir_file.get();
+    if (!sok) err = errno_str("fsync " + cfg_.storage_dir);
+    close_fresh();
+    if (!mok || !dok || !sok) {
+      ::unlink(dp_tmp.c_str());
+      ::unlink(mp_tmp.c_str());
+      unclaim_fresh(id);
+      release(ext);
+      res.error = dok ? err : data_err;
+      return res;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      ++st_.final_name_writes;
+    }
+  } else if (data_file.valid()) {
     bool mok = write_file_durable(mp_tmp, meta->data(), S * 4, &err);
     bool dok = data_file.get();
     if (mok && dok) {
@@ -734,6 +815,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
     return res;
   }
   insert_resident(id, ext, n, co.block_crc, sync_now, meta);
+  if (fresh) unclaim_fresh(id);  // indexed now: a later write of the id takes the tmp path
   if (n <= kMirrorMax) set_mirror(id, data, n, *meta);
   res.ok = true;
   return res;

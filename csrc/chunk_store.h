@@ -27,6 +27,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "disk_gate.h"
@@ -89,6 +90,7 @@ struct StoreStats {
   uint64_t mirror_hits = 0;      // small-block reads served from the verified host mirror
   uint64_t mirror_bytes = 0;
   uint64_t io_threads_spawned = 0;  // helper threads ever started (steady state: none per write)
+  uint64_t final_name_writes = 0;   // durable writes of fresh ids straight to their final names
 };
 
 // Group commit: callers that finished writing share one flush round — syncfs() of the
@@ -265,6 +267,7 @@ class ChunkStore {
   void spill_worker();
   bool make_durable(int data_fd, int meta_fd, bool cold);
   bool write_file_durable(const std::string& path, const uint8_t* p, uint64_t n, std::string* err);
+  bool write_fd_durable(int fd, const uint8_t* p, uint64_t n, const std::string& what, std::string* err);
   WriteResult write_host(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc);
   ReadResult read_host(const std::string& id, uint64_t offset, uint64_t bytes, uint8_t* out);
   std::vector<uint32_t> load_meta_file(const std::string& id, bool cold, bool* ok);
@@ -294,7 +297,10 @@ class ChunkStore {
   bool stop_ = false;
   StoreStats st_;
   std::atomic<uint64_t> launches_{0};
-  std::atomic<uint64_t> tmp_seq_{0};
+  std::atomic<uint64_t> tmp_seq_{0};  // unique temporary file names for in-flight writes
+  std::unordered_set<std::string> writing_;  // mu_: fresh ids being written under their final names
+  bool claim_fresh(const std::string& id);
+  void unclaim_fresh(const std::string& id);
   bool host_registered(const void* p, uint64_t n);
   std::mutex reg_mu_;
   std::vector<std::pair<uintptr_t, uint64_t>> reg_;  // registered host ranges
@@ -302,7 +308,7 @@ class ChunkStore {
   // device-visible alias of registered host memory [p, p + n), nullptr if not registered
   uint8_t* device_view(const void* p, uint64_t n);
   std::atomic<uint64_t> fused_reads_{0};  // K3 fused verify+copy reads
-  std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};  // unique temporary file names for in-flight writes
+  std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};
   std::unique_ptr<GroupSync> gsync_;
   IoPool io_{8};  // data-file writes and .meta flushes beside the GPU staging (no per-write threads)
   std::unique_ptr<GroupSync> dsync_hot_, dsync_cold_;  // directory fsync after renames

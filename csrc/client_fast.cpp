@@ -707,11 +707,10 @@ FastClient::Status FastClient::write_ec(const std::string& path, const uint8_t* 
       }
       pb::WriteBlockRequest req;
       req.block_id = alloc.block.block_id;
-      req.data.assign(reinterpret_cast<const char*>(p), sl);
       req.expected_checksum_crc32c = crc;
       req.shard_index = i;
       req.master_term = alloc.master_term;
-      GrpcResult r = grpc_.call(addr, "/dfs.ChunkServerService/WriteBlock", req.str(), rid);
+      GrpcResult r = grpc_.call(addr, "/dfs.ChunkServerService/WriteBlock", encode_with_payload(req, p, sl), rid);
       if (!r.transport_ok) return {1, r.message};
       pb::WriteBlockResponse resp;
       if (r.status != 0 || !resp.decode(r.message) || !resp.success)

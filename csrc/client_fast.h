@@ -24,11 +24,25 @@
 #include <thread>
 #include <vector>
 
+#include "dfs_pb.h"
 #include "grpc_client.h"
 #include "io_pool.h"
 #include "shard_map.h"
 
 namespace dfs {
+
+// A WriteBlockRequest with `data` (field 2) appended straight from the caller's buffer:
+// one copy of the payload into the wire message instead of two (field order is free in
+// proto3, and the server decodes field 2 as a view — cs_grpc.cpp decode_viewing).
+inline std::string encode_with_payload(const pb::WriteBlockRequest& w, const uint8_t* data, size_t n) {
+  std::string wire;
+  wire.reserve(n + 256 + w.block_id.size());
+  w.encode(wire);
+  pb::wire::tag(wire, 2, 2);
+  pb::wire::varint(wire, n);
+  wire.append(reinterpret_cast<const char*>(data), n);
+  return wire;
+}
 
 class FastClient {
  public:

@@ -197,13 +197,11 @@ FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* d
 
   pb::WriteBlockRequest w;
   w.block_id = alloc.block.block_id;
-  w.data.assign(reinterpret_cast<const char*>(data), n);
   for (size_t i = 1; i < alloc.chunk_server_addresses.size(); ++i) w.next_servers.push_back(alloc.chunk_server_addresses[i]);
   w.expected_checksum_crc32c = crc;
   w.shard_index = -1;
   w.master_term = alloc.master_term;
-  std::string wire = w.str();
-  std::string().swap(w.data);
+  std::string wire = encode_with_payload(w, data, n);
   GrpcResult wr = pool_.call(alloc.chunk_server_addresses[0], "/dfs.ChunkServerService/WriteBlock", wire, rid);
   std::string().swap(wire);
   if (!wr.transport_ok) {
@@ -417,11 +415,12 @@ FastClient::Status RemoteClient::write_ec(const std::string& path, const uint8_t
     futs.push_back(hedge_pool_.submit([this, i, &shards, &alloc, rid]() -> std::pair<int, std::string> {
       pb::WriteBlockRequest req;
       req.block_id = alloc.block.block_id;
-      req.data = shards[i];
-      req.expected_checksum_crc32c = crc32(reinterpret_cast<const uint8_t*>(shards[i].data()), shards[i].size());
+      const auto* sp = reinterpret_cast<const uint8_t*>(shards[i].data());
+      req.expected_checksum_crc32c = crc32(sp, shards[i].size());
       req.shard_index = i;
       req.master_term = alloc.master_term;
-      GrpcResult r = pool_.call(alloc.chunk_server_addresses[i], "/dfs.ChunkServerService/WriteBlock", req.str(), rid);
+      GrpcResult r = pool_.call(alloc.chunk_server_addresses[i], "/dfs.ChunkServerService/WriteBlock",
+                                encode_with_payload(req, sp, shards[i].size()), rid);
       if (!r.transport_ok) return {1, r.message};
       pb::WriteBlockResponse resp;
       if (r.status != 0 || !resp.decode(r.message) || !resp.success)

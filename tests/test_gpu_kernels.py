@@ -102,6 +102,29 @@ def test_gpu_write_rejects_bad_crc(gstore):
     assert not gstore.exists("badcrc")
 
 
+def test_gpu_durable_write_names(native, tmp_path):
+    """nvme-sync writes of fresh ids go straight to their final names (directory flush beside
+    the data flushes); a rejected fresh write leaves no file; a re-write of a known id takes
+    the tmp+rename path and a rejected re-write keeps the durable copy."""
+    s = native.ChunkStore(str(tmp_path), "", 0, 64 << 20, 0, 100, 2, 1, True)
+    base = s.stats()["final_name_writes"]
+    d = os.urandom((1 << 20) + 5)
+    assert s.write("fresh", d, zlib.crc32(d))[0]
+    assert (tmp_path / "fresh").read_bytes() == d and (tmp_path / "fresh.meta").read_bytes() == ref_meta(d)
+    assert s.stats()["final_name_writes"] == base + 1
+    ok, _crc, err = s.write("fresh_bad", d, zlib.crc32(d) ^ 1)
+    assert not ok and err.startswith("Checksum mismatch")
+    assert not (tmp_path / "fresh_bad").exists() and not (tmp_path / "fresh_bad.meta").exists()
+    d2 = os.urandom(70000)
+    assert not s.write("fresh", d2, zlib.crc32(d2) ^ 1)[0]  # known id: the old copy survives
+    assert (tmp_path / "fresh").read_bytes() == d
+    assert s.write("fresh", d2, zlib.crc32(d2))[0]
+    assert (tmp_path / "fresh").read_bytes() == d2 and (tmp_path / "fresh.meta").read_bytes() == ref_meta(d2)
+    assert s.stats()["final_name_writes"] == base + 1
+    assert not [p for p in os.listdir(tmp_path) if p.endswith(".tmp")]
+    assert s.read("fresh", 0, 0)[2] == d2
+
+
 def test_gpu_corruption_detected_full_and_partial(gstore):
     d = os.urandom(300000)
     assert gstore.write("corrupt", d, 0)[0]
