@@ -326,6 +326,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["disk_gate_waits"] = t.disk_gate_waits;
         d["direct_dma"] = t.direct_dma;
         d["fused_reads"] = t.fused_reads;
+        d["fused_writes"] = t.fused_writes;
         d["staged_dma"] = t.staged_dma;
         d["host_registered_bytes"] = t.host_registered_bytes;
         return d;

@@ -400,6 +400,37 @@ bool ChunkStore::run_crc(Lane* l, const uint8_t* dptr, uint64_t n, uint32_t* met
   return true;
 }
 
+// The writer's bytes sit in registered host memory: one kernel copies them into the HBM
+// extent while it checksums them, and leaves the .meta image and the whole-block partials in
+// the lane's pinned scratch (crc_write_copy_kernel) — no SDMA copy, no readback copies.
+bool ChunkStore::write_copy(Lane* l, const uint8_t* src_dev, uint8_t* dst, uint64_t n, uint32_t* dmeta,
+                            uint8_t* hmeta, CrcOut* out, std::string* err) {
+  CrcPlan p = plan_crc(src_dev, n, dmeta, nullptr, true, 0, n);
+  auto* hp = reinterpret_cast<uint32_t*>(l->hscratch);
+  WriteCopyLaunch w;
+  w.c = p.a;
+  w.c.part_crc = static_cast<uint32_t*>(l->hscratch_dev);
+  w.dst = dst;
+  w.meta_host = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(l->hscratch_dev) + (hmeta - l->hscratch));
+  hipError_t e = launch_write_copy(w, dtables_, p.grid, l->stream);
+  launches_++;
+  if (e != hipSuccess) {
+    *err = std::string("write-copy kernel launch: ") + hipGetErrorString(e);
+    return false;
+  }
+  HIP_OK(hipStreamSynchronize(l->stream));
+  fused_writes_++;
+  uint32_t r = 0;
+  for (int g = 0; g < p.grid; ++g) r ^= hp[g];
+  if (p.a.has_tail) {
+    const uint32_t tail_crc = __builtin_bswap32(reinterpret_cast<const uint32_t*>(hmeta)[p.a.s_full]);
+    r = crc_shift(r, p.a.tail_len) ^ (tail_crc ^ p.a.tail_init);
+  }
+  out->block_crc = r ^ crc_init_term(n);
+  out->bad_slice = -1;
+  return true;
+}
+
 bool ChunkStore::register_host(const void* p, uint64_t n) {
   if (!gpu() || !p || !n) return false;
   HIP_OK(hipSetDevice(cfg_.device));
@@ -673,7 +704,11 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   // write-then-sync_all (chunkserver.rs:192-209): both names exist before any flush, so
   // the directory fsync that makes them durable runs BESIDE the data and .meta flushes
   // instead of after a rename (one device round trip on the ack path instead of two).
-  const bool fresh = sync_now && !gsync_ && claim_fresh(id);
+  static const bool final_names = [] {  // DFS_FINAL_NAMES=0: every write via tmp + rename (A/B)
+    const char* e = std::getenv("DFS_FINAL_NAMES");
+    return !(e && e[0] == '0');
+  }();
+  const bool fresh = final_names && sync_now && !gsync_ && claim_fresh(id);
   const std::string tmp_sfx = fresh ? "" : "." + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
   const std::string dp_tmp = data_path(id, false) + tmp_sfx, mp_tmp = meta_path(id, false) + tmp_sfx;
   int dfd = -1, mfd = -1;
@@ -728,10 +763,17 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   ensure_hscratch(l, S * 4 + 16);
   uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
   std::string err;
-  h2d_chunked(l, ext.ptr, data, n);
   CrcOut co;
   bool ok = true;
-  if (n <= kMirrorMax) {
+  static const bool fused_ok = [] {  // DFS_FUSED_WRITE=0: SDMA copy + checksum kernel (A/B)
+    const char* e = std::getenv("DFS_FUSED_WRITE");
+    return !(e && e[0] == '0');
+  }();
+  const uint8_t* src_dev =
+      fused_ok && n > kMirrorMax && crc_mfma_enabled() && l->hscratch_dev ? device_view(data, n) : nullptr;
+  if (src_dev && reinterpret_cast<uintptr_t>(src_dev) % 16 == 0) {
+    ok = write_copy(l, src_dev, ext.ptr, n, dmeta, hmeta, &co, &err);
+  } else if (h2d_chunked(l, ext.ptr, data, n) && n <= kMirrorMax) {
     // a few slices: PCLMUL on the host bytes beats a kernel launch plus the .meta readback;
     // the image goes up with the data in the same stream round trip
     std::vector<uint32_t> sums(S);
@@ -1845,6 +1887,7 @@ StoreStats ChunkStore::stats() {
   s.gpu_kernel_launches = launches_.load();
   s.direct_dma = direct_dma_.load();
   s.fused_reads = fused_reads_.load();
+  s.fused_writes = fused_writes_.load();
   s.staged_dma = staged_dma_.load();
   s.mirror_hits = mirror_hits_;
   s.mirror_bytes = mirror_bytes_;

@@ -85,6 +85,7 @@ struct StoreStats {
   uint64_t disk_gate_waits = 0;  // durable writes that queued for a node-wide disk slot
   uint64_t direct_dma = 0;       // host<->HBM copies done straight from registered memory
   uint64_t fused_reads = 0;      // reads delivered by the K3 verify+copy kernel (no SDMA copy)
+  uint64_t fused_writes = 0;     // writes staged by the K1/K2 copy+checksum kernel (no SDMA copy)
   uint64_t staged_dma = 0;       // copies bounced through pinned staging buffers
   uint64_t host_registered_bytes = 0;
   uint64_t mirror_hits = 0;      // small-block reads served from the verified host mirror
@@ -308,6 +309,9 @@ class ChunkStore {
   // device-visible alias of registered host memory [p, p + n), nullptr if not registered
   uint8_t* device_view(const void* p, uint64_t n);
   std::atomic<uint64_t> fused_reads_{0};  // K3 fused verify+copy reads
+  std::atomic<uint64_t> fused_writes_{0};  // K1/K2 fused copy+checksum writes
+  bool write_copy(Lane* l, const uint8_t* src_dev, uint8_t* dst, uint64_t n, uint32_t* dmeta, uint8_t* hmeta,
+                  CrcOut* out, std::string* err);
   std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};
   std::unique_ptr<GroupSync> gsync_;
   IoPool io_{8};  // data-file writes and .meta flushes beside the GPU staging (no per-write threads)

@@ -120,6 +120,18 @@ struct ReadCopyLaunch {
   uint32_t* part_bad;
 };
 hipError_t launch_read_copy(const ReadCopyLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
+
+// K1/K2 fused with a write's host-to-device copy (crc_write_copy_kernel): `c` is a whole-block
+// plan whose `data` is the device-visible view of registered host memory, `meta_out` the HBM
+// .meta image and `part_crc` [grid] device-visible host words (whole-block partials);
+// `dst` the HBM extent, `meta_host` a device-visible host copy of the .meta image. The data
+// and dst must be 16 B aligned. grid <= kMaxGridCrc.
+struct WriteCopyLaunch {
+  CrcLaunch c;
+  uint8_t* dst;
+  uint32_t* meta_host;
+};
+hipError_t launch_write_copy(const WriteCopyLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
 hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s);
 hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s);
 

@@ -558,6 +558,86 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
   if (threadIdx.x == 0) a.part_bad[blockIdx.x] = wg_bad;
 }
 
+// K1/K2 fused with the host-to-device copy of a write (the mirror of crc_read_copy_kernel):
+// the waves load the block straight from the writer's registered host slot over PCIe, store
+// it into the HBM extent, checksum the registers they already hold on the matrix cores, and
+// write the .meta image both next to the block in HBM and into host-visible memory together
+// with the whole-block partials — one kernel and one stream sync instead of an SDMA copy,
+// the checksum kernel and two device-to-host copies (the .meta image and the partials).
+__device__ __forceinline__ void store_wave_dst(uint8_t* __restrict__ dst, int64_t i0, int64_t lo, int64_t hi,
+                                               const WaveData& d, int lane) {
+  const int n = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = it * 32 + n;
+    const int64_t i = i0 + (c >> 3);
+    if (i < lo || i >= hi) continue;
+    uint4* p = reinterpret_cast<uint4*>(dst + static_cast<uint64_t>(i) * 512 + (c & 7) * 64 + h * 32);
+    p[0] = d.v[2 * it];
+    p[1] = d.v[2 * it + 1];
+  }
+}
+
+__global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3, 3))) void crc_write_copy_kernel(
+    WriteCopyLaunch a, const DevCrcTables* __restrict__ gt) {
+  __shared__ MfmaTileLds lt;
+  __shared__ uint32_t wacc[4];
+  const CrcLaunch& c = a.c;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
+  const uint64_t per = (c.ntiles + gridDim.x - 1) / gridDim.x;
+  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
+  const uint64_t t_end = t_begin + per < c.ntiles ? t_begin + per : c.ntiles;
+  const int64_t lo = static_cast<int64_t>(c.slice_lo), hi = static_cast<int64_t>(c.slice_hi);
+  auto first_slice = [&](uint64_t t) {
+    return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8) - static_cast<int64_t>(c.vfront);
+  };
+  WaveData cur;
+  if (t_begin < t_end) cur = load_wave(c.data, first_slice(t_begin), lo, hi, lane);  // PCIe latency first
+  i32x4 A[16];
+  load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
+  load_lds_image(gt, &lt);
+  __syncthreads();
+
+  uint32_t acc = 0;
+  for (uint64_t t = t_begin; t < t_end; ++t) {
+    WaveData nxt;
+    if (t + 1 < t_end) nxt = load_wave(c.data, first_slice(t + 1), lo, hi, lane);
+    const int64_t i0 = first_slice(t);
+    store_wave_dst(a.dst, i0, lo, hi, cur, lane);
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, cur, lane), lane);
+    const int64_t i = i0 + sw;
+    if (i >= lo && i < hi && sl == 0) {
+      const uint32_t be = __builtin_bswap32(r ^ c.full_init);
+      c.meta_out[i] = be;
+      a.meta_host[i] = be;
+    }
+    r = combine(r, 8, lane, lt.sh512);
+    r = combine(r, 16, lane, lt.sh1k);
+    r = combine(r, 32, lane, lt.sh2k);
+    acc = mat_apply(lt.tile_pow2[0], acc, lane) ^ r;
+    if (t + 1 < t_end) cur = nxt;
+  }
+
+  if (c.has_tail && blockIdx.x == 0 && wave == 0) {
+    const uint8_t* base = c.data + c.s_full * 512;
+    const uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(base, c.tail_len, lane), lane), lane);
+    if (lane == 0) {
+      const uint32_t be = __builtin_bswap32(r ^ c.tail_init);
+      c.meta_out[c.s_full] = be;
+      a.meta_host[c.s_full] = be;
+    }
+    uint8_t* out = a.dst + c.s_full * 512;
+    for (uint32_t k = lane; k < c.tail_len; k += 64) out[k] = base[k];
+  }
+  for (int k = wave; k < 3; ++k) acc = tab4(lt.sh4k, acc);
+  uint64_t e = t_begin < t_end ? c.ntiles - t_end : 0;
+  for (int b = 0; e; ++b, e >>= 1)
+    if (e & 1) acc = mat_apply(lt.tile_pow2[b], acc, lane);
+  if (lane == 0) wacc[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) c.part_crc[blockIdx.x] = wacc[0] ^ wacc[1] ^ wacc[2] ^ wacc[3];
+}
+
 // K1b on the matrix cores: contiguous tile runs per workgroup, so the tile -> block lookup is
 // one binary search per workgroup and then a forward walk, and the next tile's data (and its
 // block) are fetched while the current tile computes.
@@ -1051,6 +1131,16 @@ hipError_t launch_read_copy(const ReadCopyLaunch& a, const DevCrcTables* t, int 
   if (grid <= 0) return hipSuccess;
   if (grid > kMaxGridCrc) return hipErrorInvalidValue;  // part_bad holds kMaxGridCrc words
   hipLaunchKernelGGL(crc_read_copy_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_write_copy(const WriteCopyLaunch& a, const DevCrcTables* t, int grid, hipStream_t s) {
+  if (grid <= 0) return hipSuccess;
+  // part_crc holds kMaxGridCrc words; the plan must be a whole block (K1/K2, no verify)
+  if (grid > kMaxGridCrc || a.c.slice_lo != 0 || a.c.slice_hi != a.c.s_full || !a.c.meta_out || !a.meta_host ||
+      !a.c.part_crc || !a.dst || (reinterpret_cast<uintptr_t>(a.c.data) | reinterpret_cast<uintptr_t>(a.dst)) % 16)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(crc_write_copy_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
   return hipGetLastError();
 }
 

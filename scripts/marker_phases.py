@@ -14,6 +14,7 @@ def main(d: str) -> None:
                 name = r.get("Function") or r.get("Operation") or ""
                 if not name.startswith("dfs."):
                     continue
+                name = name.split(" [", 1)[0]  # ranges carry "[request id]"
                 try:
                     us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
                 except (KeyError, ValueError):

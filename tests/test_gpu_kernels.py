@@ -217,6 +217,44 @@ def test_gpu_small_block_mirror(gstore):
     gstore.remove("mir")
 
 
+def test_gpu_fused_write_copy(gstore):
+    """K1/K2 fused with the host-to-device copy (crc_write_copy_kernel): a write whose bytes sit
+    in registered host memory is one kernel that stores the block into HBM, checksums it and
+    leaves the .meta image in host memory — against zlib, with tails and a multi-tile block,
+    and a wrong expected CRC still rejected. Blocks <= 64 KiB keep the host-CRC path."""
+    import numpy as np
+
+    buf = np.zeros((40 << 20) + 4096, dtype=np.uint8)
+    assert gstore.register_host(buf)
+    try:
+        f0 = gstore.stats()["fused_writes"]
+        sizes = [65537, 300000, (1 << 20), (1 << 20) + 13, 3 * (1 << 20) + 1, (40 << 20) + 512 * 3 + 77]
+        for i, n in enumerate(sizes):
+            d = np.frombuffer(os.urandom(n), dtype=np.uint8)
+            buf[:n] = d
+            ok, crc, err = gstore.write(f"fw{i}", buf[:n], zlib.crc32(d.tobytes()))
+            assert ok and crc == zlib.crc32(d.tobytes()), (n, err)
+            buf[:n] = 0  # the store must hold its own copy
+            st, total, out, partial, bad, err = gstore.read(f"fw{i}", 0, 0)
+            assert (st, total, partial) == (0, n, False) and out == d.tobytes(), n
+            assert gstore.scrub_resident([f"fw{i}"]) == []  # the HBM .meta image matches too
+        assert gstore.stats()["fused_writes"] - f0 == len(sizes)
+        d = os.urandom(500000)
+        buf[:len(d)] = np.frombuffer(d, dtype=np.uint8)
+        ok, _crc, err = gstore.write("fw_bad", buf[:len(d)], zlib.crc32(d) ^ 1)
+        assert not ok and err.startswith("Checksum mismatch") and not gstore.exists("fw_bad")
+        small = os.urandom(4000)
+        buf[:4000] = np.frombuffer(small, dtype=np.uint8)
+        f1 = gstore.stats()["fused_writes"]
+        assert gstore.write("fw_small", buf[:4000], zlib.crc32(small))[0]
+        assert gstore.stats()["fused_writes"] == f1 and gstore.read("fw_small", 0, 0)[2] == small
+    finally:
+        gstore.unregister_host(buf)
+        for i in range(6):
+            gstore.remove(f"fw{i}")
+        gstore.remove("fw_small")
+
+
 def test_gpu_fused_read_copy(gstore):
     """K3 fused verify + copy (crc_read_copy_kernel): reads into a registered buffer are one
     kernel that checks every touched slice and stores the range straight into host memory.
