@@ -445,7 +445,100 @@ void bind_meta(py::module_& m) {
       .def("shard_map_json", &ConfigCore::shard_map_json)
       .def("masters_json", &ConfigCore::masters_json)
       .def_property_readonly("version", &ConfigCore::version)
-      .def("split_candidates", &ConfigCore::split_candidates, py::arg("n") = 3);
+      .def("split_candidates", &ConfigCore::split_candidates, py::arg("n") = 3)
+      .def("attach", [](ConfigCore& c, raft::Node& n) { c.attach(&n); }, py::keep_alive<1, 2>())
+      .def("detach", &ConfigCore::detach)
+      .def("handle", [](ConfigCore& c, const std::string& method, py::bytes req) {
+        std::string in = req, out;
+        int code;
+        {
+          py::gil_scoped_release r;
+          code = c.handle(method, in, &out);
+        }
+        return py::make_tuple(code, py::bytes(out));
+      })
+      .def_property_readonly("requests", &ConfigCore::requests);
+
+  // ConfigService over native HTTP/2 gRPC and the same-host socket: every method and the
+  // Raft peer RPC answered by ConfigCore, no Python on any request.
+  struct NativeGrpcConfig {
+    std::unique_ptr<GrpcServer> srv;
+    std::atomic<uint64_t> raft_calls{0};
+  };
+  py::class_<NativeGrpcConfig>(m, "NativeGrpcConfigServer")
+      .def(py::init([](std::shared_ptr<ConfigCore> core, const std::string& host, int port, int workers,
+                       const std::string& tls_cert, const std::string& tls_key) {
+             auto n = std::make_unique<NativeGrpcConfig>();
+             NativeGrpcConfig* self = n.get();
+             static const std::string kPrefix = "/dfs.ConfigService/";
+             static const std::string kRaft = "/dfs.RaftPeer/";
+             n->srv = std::make_unique<GrpcServer>(host, port, [core, self](const GrpcCall& c) -> GrpcReply {
+               GrpcReply r;
+               RequestScope scope(c.request_id);
+               if (c.path.compare(0, kRaft.size(), kRaft) == 0) {
+                 r.status = core->raft_rpc(c.path.substr(kRaft.size()), c.message, &r.message);
+                 self->raft_calls++;
+               } else if (c.path.compare(0, kPrefix.size(), kPrefix) == 0) {
+                 r.status = core->handle(c.path.substr(kPrefix.size()), c.message, &r.message);
+               } else {
+                 r.status = 12;
+                 r.message = "unknown service: " + c.path;
+               }
+               return r;
+             }, workers);
+             if (!tls_cert.empty()) {
+               std::string err;
+               auto t = TlsContext::server(tls_cert, tls_key, &err);
+               if (!t) throw std::runtime_error(err);
+               n->srv->set_tls(std::move(t));
+             }
+             return n;
+           }),
+           py::arg("core"), py::arg("host"), py::arg("port"), py::arg("workers") = 16, py::arg("tls_cert") = "",
+           py::arg("tls_key") = "")
+      .def("start", [](NativeGrpcConfig& n) {
+        std::string err;
+        bool ok = n.srv->start(&err);
+        return py::make_tuple(ok, err);
+      })
+      .def("stop", [](NativeGrpcConfig& n) {
+        py::gil_scoped_release r;
+        n.srv->stop();
+      })
+      .def_property_readonly("port", [](NativeGrpcConfig& n) { return n.srv->port(); })
+      .def("stats", [](NativeGrpcConfig& n) {
+        py::dict d;
+        d["native_grpc_calls"] = n.srv->calls();
+        d["native_raft_rpcs"] = n.raft_calls.load();
+        return d;
+      });
+
+  struct ConfigLocal {  // (LocalRpcServer itself is bound once, as MasterLocalServer)
+    std::unique_ptr<LocalRpcServer> srv;
+  };
+  py::class_<ConfigLocal>(m, "ConfigLocalServer")
+      .def(py::init([](const std::string& name, std::shared_ptr<ConfigCore> core) {
+             static const std::string kPrefix = "/dfs.ConfigService/";
+             LocalRpcServer::Handler h = [core](const std::string& path, const std::string& rid, const std::string& payload,
+                                                std::string* out) -> int {
+               RequestScope scope(rid);
+               if (path.compare(0, kPrefix.size(), kPrefix) != 0) return (*out = "unknown service: " + path, 12);
+               return core->handle(path.substr(kPrefix.size()), payload, out);
+             };
+             auto c = std::make_unique<ConfigLocal>();
+             c->srv = std::make_unique<LocalRpcServer>(name, std::move(h));
+             return c;
+           }))
+      .def("start", [](ConfigLocal& s) {
+        std::string err;
+        bool ok = s.srv->start(&err);
+        return py::make_tuple(ok, err);
+      })
+      .def("stop", [](ConfigLocal& s) {
+        py::gil_scoped_release r;
+        s.srv->stop();
+      })
+      .def_property_readonly("requests", [](ConfigLocal& s) { return s.srv->requests(); });
 
   // ---------------- native master core + same-host RPC listener
   py::class_<MasterCore, raft::StateMachine, std::shared_ptr<MasterCore>>(m, "MasterCore")

@@ -2,6 +2,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <future>
+#include <memory>
+
+#include "dfs_pb.h"
 
 namespace dfs {
 
@@ -165,6 +169,193 @@ std::vector<std::string> ConfigCore::split_candidates(size_t n) const {
   std::vector<std::string> out;
   for (size_t i = 0; i < pick.size() && i < n; ++i) out.push_back(pick[i].second);
   return out;
+}
+
+// ---------------------------------------------------------------- ConfigService
+// Semantics of the reference's config_server.rs handlers (and of the Python service this
+// replaces): mutations commit through Raft and answer success=false + "Not Leader" +
+// leader_hint on a follower; FetchShardMap is a ReadIndex read (FAILED_PRECONDITION
+// "Not Leader|<hint>" on a follower) returning shard -> peers plus the `ranges` extension;
+// ShardHeartbeat is fire-and-forget on the leader.
+namespace {
+constexpr int kOk = 0, kFailedPrecondition = 9, kInternal = 13, kUnavailable = 14, kUnimplemented = 12;
+Json jstrings(const std::vector<std::string>& v) {
+  Json a = Json::array();
+  for (auto& x : v) a.push_back(Json(x));
+  return a;
+}
+}  // namespace
+
+bool ConfigCore::native_method(const std::string& m) {
+  return m == "FetchShardMap" || m == "AddShard" || m == "RemoveShard" || m == "SplitShard" || m == "MergeShard" ||
+         m == "RebalanceShard" || m == "RegisterMaster" || m == "ShardHeartbeat";
+}
+
+ConfigCore::Result ConfigCore::propose(const std::string& name, const Json& args) {
+  raft::Node* node = node_.load();
+  if (!node) return {1, ""};
+  Json inner = Json::object();
+  inner.set(name, args);
+  Json cmd = Json::object();
+  cmd.set("Config", inner);
+  auto prom = std::make_shared<std::promise<Result>>();
+  auto fut = prom->get_future();
+  node->propose(cmd.dump(), [prom](int code, const std::string& payload) { prom->set_value(Result{code, payload}); });
+  if (fut.wait_for(std::chrono::seconds(30)) != std::future_status::ready) return {2, "proposal timed out"};
+  return fut.get();
+}
+
+int ConfigCore::raft_rpc(const std::string& kind, const std::string& body, std::string* out) {
+  raft::Node* node = node_.load();
+  if (!node) return (*out = "raft node not attached", kUnavailable);
+  try {
+    *out = node->handle(kind, body);
+    return kOk;
+  } catch (const std::exception& e) {
+    *out = e.what();
+    return kInternal;
+  }
+}
+
+int ConfigCore::handle(const std::string& method, const std::string& req, std::string* out) {
+  requests_++;
+  // a mutation's reply: success, or the follower's "Not Leader" + hint, or an INTERNAL status
+  auto simple = [&](auto resp, const Result& r) -> int {
+    if (r.code == 2) return (*out = r.payload, kInternal);
+    resp.success = r.code == 0;
+    if (r.code == 1) {
+      resp.error_message = "Not Leader";
+      resp.leader_hint = r.payload;
+    }
+    *out = resp.str();
+    return kOk;
+  };
+  if (method == "FetchShardMap") {
+    raft::Node* node = node_.load();
+    Result r{1, ""};
+    if (node) {
+      auto prom = std::make_shared<std::promise<Result>>();
+      auto fut = prom->get_future();
+      node->read_index([prom](int code, const std::string& payload) { prom->set_value(Result{code, payload}); });
+      if (fut.wait_for(std::chrono::seconds(10)) != std::future_status::ready) return (*out = "ReadIndex timed out", kUnavailable);
+      r = fut.get();
+    }
+    if (r.code == 1) return (*out = "Not Leader|" + r.payload, kFailedPrecondition);
+    if (r.code != 0) return (*out = r.payload, kInternal);
+    pb::FetchShardMapResponse resp;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& sid : map_.shards()) {
+        const auto* p = map_.peers(sid);
+        if (p) resp.shards[sid].peers = *p;
+        else resp.shards[sid];
+      }
+      if (map_.strategy() == ShardMap::Strategy::Range) resp.ranges = map_.ranges();
+    }
+    *out = resp.str();
+    return kOk;
+  }
+  if (method == "AddShard") {
+    pb::AddShardRequest q;
+    if (!q.decode(req)) return (*out = "malformed AddShardRequest", kInternal);
+    Json a = Json::object();
+    a.set("shard_id", q.shard_id);
+    a.set("peers", jstrings(q.peers));
+    return simple(pb::AddShardResponse{}, propose("AddShard", a));
+  }
+  if (method == "RemoveShard") {
+    pb::RemoveShardRequest q;
+    if (!q.decode(req)) return (*out = "malformed RemoveShardRequest", kInternal);
+    Json a = Json::object();
+    a.set("shard_id", q.shard_id);
+    return simple(pb::RemoveShardResponse{}, propose("RemoveShard", a));
+  }
+  if (method == "RebalanceShard") {
+    pb::RebalanceShardRequest q;
+    if (!q.decode(req)) return (*out = "malformed RebalanceShardRequest", kInternal);
+    Json a = Json::object();
+    a.set("old_key", q.old_key);
+    a.set("new_key", q.new_key);
+    return simple(pb::RebalanceShardResponse{}, propose("RebalanceShard", a));
+  }
+  if (method == "SplitShard") {
+    pb::SplitShardRequest q;
+    if (!q.decode(req)) return (*out = "malformed SplitShardRequest", kInternal);
+    pb::SplitShardResponse resp;
+    // without explicit peers: standby masters first, else the three most recently
+    // heartbeated masters (the reference's choice)
+    std::vector<std::string> peers = q.new_shard_peers.empty() ? split_candidates(3) : q.new_shard_peers;
+    if (peers.empty()) {
+      resp.error_message = "No available master nodes for new shard";
+      *out = resp.str();
+      return kOk;
+    }
+    Json a = Json::object();
+    a.set("shard_id", q.shard_id);
+    a.set("split_key", q.split_key);
+    a.set("new_shard_id", q.new_shard_id);
+    a.set("new_shard_peers", jstrings(peers));
+    Result r = propose("SplitShard", a);
+    if (r.code == 0 && r.payload != "true") {
+      resp.error_message = "split rejected by the shard map";
+      *out = resp.str();
+      return kOk;
+    }
+    if (r.code == 0) resp.new_shard_peers = peers;
+    return simple(resp, r);
+  }
+  if (method == "MergeShard") {
+    // the apply result decides: two idle neighbours may try to merge into each other
+    pb::MergeShardRequest q;
+    if (!q.decode(req)) return (*out = "malformed MergeShardRequest", kInternal);
+    Json a = Json::object();
+    a.set("victim_shard_id", q.victim_shard_id);
+    a.set("retained_shard_id", q.retained_shard_id);
+    Result r = propose("MergeShard", a);
+    if (r.code == 0 && r.payload != "true") {
+      pb::MergeShardResponse resp;
+      resp.error_message = "merge rejected: unknown shard";
+      *out = resp.str();
+      return kOk;
+    }
+    return simple(pb::MergeShardResponse{}, r);
+  }
+  if (method == "RegisterMaster") {
+    pb::RegisterMasterRequest q;
+    if (!q.decode(req)) return (*out = "malformed RegisterMasterRequest", kInternal);
+    Json a = Json::object();
+    a.set("address", q.address);
+    a.set("shard_id", q.shard_id);
+    Result r = propose("RegisterMaster", a);
+    if (r.code == 2) return (*out = r.payload, kInternal);
+    pb::RegisterMasterResponse resp;
+    resp.success = r.code == 0;
+    *out = resp.str();
+    return kOk;
+  }
+  if (method == "ShardHeartbeat") {
+    pb::ShardHeartbeatRequest q;
+    if (!q.decode(req)) return (*out = "malformed ShardHeartbeatRequest", kInternal);
+    pb::ShardHeartbeatResponse resp;
+    raft::Node* node = node_.load();
+    if (node && node->is_leader()) {
+      Json rps = Json::object();
+      for (const auto& kv : q.rps_per_prefix) rps.set(kv.first, Json(kv.second));
+      Json a = Json::object();
+      a.set("address", q.address);
+      a.set("rps_per_prefix", rps);
+      Json inner = Json::object();
+      inner.set("ShardHeartbeat", a);
+      Json cmd = Json::object();
+      cmd.set("Config", inner);
+      node->propose_nowait(cmd.dump());
+      resp.success = true;
+    }
+    *out = resp.str();
+    return kOk;
+  }
+  *out = "method not implemented: " + method;
+  return kUnimplemented;
 }
 
 }  // namespace dfs

@@ -1,8 +1,10 @@
 // Native config-server state machine (C36): the Raft-replicated shard map and master
 // registry of the reference's ConfigService (dfs/metaserver/src/config_server.rs,
 // simple_raft.rs ConfigCommand apply). Applied on the native Raft applier thread like
-// MasterCore; the Python ConfigService keeps the gRPC surface and reads the state through
-// version-stamped JSON views.
+// MasterCore. The ConfigService RPCs are answered here too (handle(): every method of the
+// reference's config_server.rs, served by the native HTTP/2 server and the local socket),
+// so a config server runs no Python on any request; Python keeps process setup and the
+// /metrics and /shards HTTP views.
 //
 // Commands (externally tagged JSON, {"Config": {"<Name>": {...}}}):
 //   AddShard{shard_id, peers}  RemoveShard{shard_id}
@@ -13,6 +15,7 @@
 //   ShardHeartbeat{address, rps_per_prefix}
 // Snapshot: {"Config": {"shard_map": <ShardMap serde>, "masters": {addr: MasterInfo}}}.
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -41,7 +44,22 @@ class ConfigCore : public raft::StateMachine {
   // by most recent heartbeat, else the three most recently heartbeated masters.
   std::vector<std::string> split_candidates(size_t n = 3) const;
 
+  // ConfigService: `method` is the bare method name; returns a gRPC status code with the
+  // serialized response (OK) or the status message in *out.
+  void attach(raft::Node* node) { node_ = node; }
+  void detach() { node_ = nullptr; }
+  static bool native_method(const std::string& method);
+  int handle(const std::string& method, const std::string& req, std::string* out);
+  // Raft peer RPC (vote / append / snapshot / timeout_now, JSON) for /dfs.RaftPeer/<kind>.
+  int raft_rpc(const std::string& kind, const std::string& body, std::string* out);
+  uint64_t requests() const { return requests_.load(); }
+
  private:
+  struct Result {  // of a proposal: 0 applied (payload = apply result), 1 not leader (hint), 2 error
+    int code;
+    std::string payload;
+  };
+  Result propose(const std::string& name, const Json& args);
   struct MasterInfo {
     std::string shard_id;
     int64_t last_heartbeat = 0;  // unix seconds
@@ -54,6 +72,8 @@ class ConfigCore : public raft::StateMachine {
   ShardMap map_;
   std::map<std::string, MasterInfo> masters_;
   uint64_t version_ = 0;
+  std::atomic<raft::Node*> node_{nullptr};
+  std::atomic<uint64_t> requests_{0};
 };
 
 }  // namespace dfs

@@ -170,6 +170,7 @@ class LocalCluster:
                 str(self.base / "config"), *fs])
             self._wait_ready([pr])
             self.config_addrs = [f"http://127.0.0.1:{port}"]
+            self.config_http = f"http://127.0.0.1:{http}"
         # masters
         shard_cfg: dict[str, list[str]] = {}
         plans = []

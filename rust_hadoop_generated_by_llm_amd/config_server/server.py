@@ -2,7 +2,10 @@
 dfs/metaserver/src/config_server.rs and bin/config_server.rs).
 
 State ``{"Config": {"shard_map": ShardMap(Range), "masters": {addr: MasterInfo}}}``, held and
-applied natively (csrc/config_core.cpp) on the native Raft node's applier thread.
+applied natively (csrc/config_core.cpp) on the native Raft node's applier thread, which also
+answers every ConfigService RPC and the Raft peer RPC (``NativeGrpcConfigServer`` over HTTP/2,
+``ConfigLocalServer`` on the same-host socket): no request runs Python. The grpcio service
+below stays as the ``DFS_CONFIG_GRPC=grpcio`` A/B and for tests.
 FetchShardMap is linearizable (ReadIndex) and, like the reference, returns only
 shard -> peers (no range boundaries). SplitShard without peers allocates standby masters (registered
 with an empty shard id) first, else the three most recently heartbeated masters; the
@@ -23,11 +26,11 @@ from ..models import proto as pb
 from ..native import lib as _native
 from ..parallel.sharding import ShardMap
 from ..raft.membership import initial_members
-from ..raft.node import NotLeader, RaftNode
+from ..raft.node import NotLeader, RaftNode, resolve_native_peers
 from ..raft.transport import HttpTransport
 from ..utils import log as logsetup
 from ..utils.metrics import Registry
-from ..utils.localrpc import serve_local
+from ..utils.localrpc import serve_local, socket_name
 from ..utils.rpc import RpcStatus, StatusCode, make_aio_server, server_credentials, with_scheme
 
 log = logging.getLogger("dfs.config_server")
@@ -174,11 +177,15 @@ async def run(args) -> None:
                     os.path.join(args.storage_dir, f"raft_node_{args.id}"), state, transport,
                     snapshot_threshold=args.snapshot_threshold, sync=not args.no_fsync,
                     native_sm=state.core)
+    state.core.attach(raft._core)
     svc = ConfigService(state, raft)
     metrics = Registry()
     metrics.gauge("raft_role", "0=follower 1=candidate 2=leader",
                   fn=lambda: {"Follower": 0, "Candidate": 1, "Leader": 2}[raft.role])
     metrics.gauge("config_shards", "shards in the map", fn=lambda: len(state.shard_map.shards))
+    metrics.gauge("config_native_requests", "ConfigService RPCs answered by the native core",
+                  fn=lambda: state.core.requests)
+    native_srv = None
     app = web.Application(client_max_size=1 << 30)
 
     def raft_route(kind):
@@ -206,23 +213,49 @@ async def run(args) -> None:
     async def raft_state(_):
         return web.json_response(raft.cluster_info())
 
+    async def raft_endpoint(_):
+        # where this node takes Raft peer RPCs natively (/dfs.RaftPeer/* on its gRPC port)
+        return web.json_response({"grpc": with_scheme(args.advertise_addr or args.addr) if native_srv else ""})
+
     app.router.add_get("/shards", shards)
     app.router.add_get("/health", health)
     app.router.add_get("/metrics", metrics_h)
     app.router.add_get("/raft/state", raft_state)
+    app.router.add_get("/raft/endpoint", raft_endpoint)
     runner = web.AppRunner(app, access_log=None)
     await runner.setup()
     await web.TCPSite(runner, host, args.http_port, reuse_address=True).start()
     creds = server_credentials(args.tls_cert, args.tls_key)
-    server = make_aio_server({"ConfigService": svc}, args.addr, creds)
-    await server.start()
-    local_srv = None
+    server = None
+    if os.environ.get("DFS_CONFIG_GRPC", "native") == "native":
+        bind = args.addr if ":" in args.addr else f"0.0.0.0:{args.addr}"
+        h, port = bind.rsplit(":", 1)
+        srv = _native.NativeGrpcConfigServer(state.core, h, int(port), tls_cert=args.tls_cert or "" if creds else "",
+                                             tls_key=args.tls_key or "" if creds else "")
+        ok, err = srv.start()
+        if ok:
+            native_srv = srv
+        else:
+            log.warning("native gRPC server unavailable (%s); serving with grpcio", err)
+    if native_srv is None:
+        server = make_aio_server({"ConfigService": svc}, args.addr, creds)
+        await server.start()
+    local_srv = native_local = None
     if creds is None and os.environ.get("DFS_NO_LOCALRPC") != "1":
-        try:
-            local_srv = await serve_local({"ConfigService": svc}, args.addr.rsplit(":", 1)[-1])
-        except OSError as e:
-            log.warning("local RPC listener unavailable: %s", e)
+        if native_srv is not None:
+            srv = _native.ConfigLocalServer(socket_name(args.addr.rsplit(":", 1)[-1]), state.core)
+            ok, err = srv.start()
+            if ok:
+                native_local = srv
+            else:
+                log.warning("local RPC listener unavailable: %s", err)
+        else:
+            try:
+                local_srv = await serve_local({"ConfigService": svc}, args.addr.rsplit(":", 1)[-1])
+            except OSError as e:
+                log.warning("local RPC listener unavailable: %s", e)
     await raft.start()
+    resolver = asyncio.get_running_loop().create_task(resolve_native_peers(raft)) if native_srv else None
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
     for sig in (signal.SIGTERM, signal.SIGINT):
@@ -235,8 +268,16 @@ async def run(args) -> None:
         with open(ready, "w") as f:
             json.dump({"addr": args.addr}, f)
     await stop.wait()
-    await server.stop(0.5)
+    if resolver is not None:
+        resolver.cancel()
+    if native_local is not None:
+        await loop.run_in_executor(None, native_local.stop)
+    if server is not None:
+        await server.stop(0.5)
+    if native_srv is not None:
+        await loop.run_in_executor(None, native_srv.stop)
     await raft.stop()
+    state.core.detach()
     await transport.close()
     await runner.cleanup()
 

@@ -16,7 +16,7 @@ from aiohttp import web
 
 from ..parallel.sharding import ShardMap
 from ..raft.membership import initial_members
-from ..raft.node import RaftNode
+from ..raft.node import RaftNode, resolve_native_peers
 from ..raft.transport import HttpTransport
 from ..utils import log as logsetup
 from ..utils.metrics import Registry
@@ -172,28 +172,7 @@ class MasterProcess:
         return app
 
     async def _resolve_native_peers(self) -> None:
-        """Learn each Raft peer's native endpoint (GET /raft/endpoint) and hand it to the
-        native node: from then on AppendEntries / RequestVote travel node-to-node over the
-        native HTTP/2 servers without touching Python on either side. Peers without one
-        (TLS, grpcio, older builds) stay on the HTTP/JSON transport."""
-        import aiohttp
-
-        known: dict[str, str] = {}
-        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=2)) as sess:
-            while True:
-                members = dict(self.raft.config.all_members())
-                for mid, addr in members.items():
-                    if mid == self.raft.id or addr in known:
-                        continue
-                    try:
-                        async with sess.get(addr.rstrip("/") + "/raft/endpoint") as r:
-                            ep = (await r.json(content_type=None)).get("grpc", "") if r.status == 200 else ""
-                    except Exception:  # noqa: BLE001 - peer not up yet: ask again later
-                        continue
-                    known[addr] = ep
-                    if ep:
-                        self.raft._core.set_peer_endpoint(addr, ep)
-                await asyncio.sleep(1.0)  # only members not resolved yet are asked
+        await resolve_native_peers(self.raft)
 
     async def run(self, ready_file: str | None = None) -> None:
         a = self.args

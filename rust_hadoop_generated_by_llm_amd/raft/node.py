@@ -313,3 +313,28 @@ class RaftNode:
 
     def cluster_info(self) -> dict:
         return json.loads(self._core.info_json())
+
+
+async def resolve_native_peers(raft: "RaftNode") -> None:
+    """Learn each Raft peer's native endpoint (GET /raft/endpoint) and hand it to the native
+    node: from then on AppendEntries / RequestVote travel node-to-node over the native HTTP/2
+    servers without touching Python on either side. Peers without one (grpcio, older builds)
+    stay on the HTTP/JSON transport. Runs until cancelled; only unresolved members are asked."""
+    import aiohttp
+
+    known: dict[str, str] = {}
+    async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=2)) as sess:
+        while True:
+            members = dict(raft.config.all_members())
+            for mid, addr in members.items():
+                if mid == raft.id or addr in known:
+                    continue
+                try:
+                    async with sess.get(addr.rstrip("/") + "/raft/endpoint") as r:
+                        ep = (await r.json(content_type=None)).get("grpc", "") if r.status == 200 else ""
+                except Exception:  # noqa: BLE001 - peer not up yet: ask again later
+                    continue
+                known[addr] = ep
+                if ep:
+                    raft._core.set_peer_endpoint(addr, ep)
+            await asyncio.sleep(1.0)

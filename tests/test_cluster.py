@@ -506,6 +506,9 @@ def test_dynamic_split_hands_range_to_standby_master():
         assert old_files == {"/hot/x", "/zz/y"} and new_files == {"/a/f1", "/b/f2", "/a/new"}
         pool.close()
         assert set(files) | {"/a/new"} <= set(c.list_all_files())
+        # the config server answered the registrations, heartbeats, split and fetches natively
+        m = urllib.request.urlopen(f"{cl.config_http}/metrics").read().decode()
+        assert int(float(next(x for x in m.splitlines() if x.startswith("config_native_requests")).split()[-1])) > 5
         c.close()
 
 

@@ -120,3 +120,81 @@ def test_unknown_command_is_an_apply_error():
     else:
         raise AssertionError("expected an error")
     assert s.apply("NoOp", 2) is None
+
+
+def test_native_config_service_over_grpc_and_local_socket(tmp_path):
+    """Every ConfigService method answered by ConfigCore on the native HTTP/2 server (a grpcio
+    client interoperates) and on the same-host socket; a core without a Raft node answers like
+    a follower (success=false + "Not Leader", FetchShardMap FAILED_PRECONDITION)."""
+    import asyncio
+    import socket
+
+    import grpc
+    import pytest
+
+    from rust_hadoop_generated_by_llm_amd.models import proto as pb
+    from rust_hadoop_generated_by_llm_amd.raft.node import RaftNode
+    from rust_hadoop_generated_by_llm_amd.raft.transport import LocalTransport
+    from rust_hadoop_generated_by_llm_amd.utils.localrpc import socket_name
+    from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
+
+    loop = asyncio.new_event_loop()
+    s = ConfigState()
+    node = RaftNode(1, {1: "solo"}, "http://127.0.0.1:1", str(tmp_path / "raft"), s, LocalTransport("solo", {}),
+                    sync=False, native_sm=s.core)
+    s.core.attach(node._core)
+    loop.run_until_complete(node.start())
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    srv = lib.NativeGrpcConfigServer(s.core, "127.0.0.1", port)
+    assert srv.start()[0]
+    local = lib.ConfigLocalServer(socket_name(port), s.core)
+    assert local.start()[0]
+    addr = f"http://127.0.0.1:{port}"
+    remote, near = ChannelPool(local=False), ChannelPool()
+    try:
+        deadline = time.time() + 10
+        while not node.is_leader() and time.time() < deadline:
+            time.sleep(0.05)
+        call = lambda m, r, p=remote: p.call(addr, "ConfigService", m, r)  # noqa: E731
+        assert call("RegisterMaster", pb.RegisterMasterRequest(address="m1:1", shard_id="shard-0")).success
+        assert call("RegisterMaster", pb.RegisterMasterRequest(address="m2:1", shard_id="")).success
+        assert call("AddShard", pb.AddShardRequest(shard_id="shard-9", peers=["m9:1"])).success
+        assert call("RemoveShard", pb.RemoveShardRequest(shard_id="shard-9")).success
+        sp = call("SplitShard", pb.SplitShardRequest(shard_id="shard-0", split_key="/m", new_shard_id="shard-1"))
+        assert sp.success and list(sp.new_shard_peers) == ["m2:1"]  # the standby master
+        bad = call("SplitShard", pb.SplitShardRequest(shard_id="shard-0", split_key="/m", new_shard_id="shard-1",
+                                                      new_shard_peers=["x:1"]))
+        assert not bad.success and bad.error_message == "split rejected by the shard map"
+        fm = call("FetchShardMap", pb.FetchShardMapRequest(), near)  # same-host socket
+        assert {k: list(v.peers) for k, v in fm.shards.items()} == {"shard-0": ["m1:1"], "shard-1": ["m2:1"]}
+        assert fm.ranges["/m"] == "shard-1" and "shard-0" in fm.ranges.values()
+        assert call("RebalanceShard", pb.RebalanceShardRequest(old_key="/m", new_key="/n")).success
+        assert call("ShardHeartbeat", pb.ShardHeartbeatRequest(address="m1:1", rps_per_prefix={"/a/": 2.5})).success
+        deadline = time.time() + 5
+        while s.masters["m1:1"]["rps_per_prefix"] != {"/a/": 2.5} and time.time() < deadline:
+            time.sleep(0.05)
+        assert s.masters["m1:1"]["rps_per_prefix"] == {"/a/": 2.5}
+        mg = call("MergeShard", pb.MergeShardRequest(victim_shard_id="shard-1", retained_shard_id="shard-0"))
+        assert mg.success and s.shard_map.get_all_shards() == ["shard-0"]
+        mg = call("MergeShard", pb.MergeShardRequest(victim_shard_id="shard-7", retained_shard_id="shard-0"))
+        assert not mg.success and mg.error_message == "merge rejected: unknown shard"
+        assert s.core.requests == 11 and srv.stats()["native_grpc_calls"] == 10 and local.requests == 1
+        # follower behaviour: no node attached
+        s.core.detach()
+        r = call("AddShard", pb.AddShardRequest(shard_id="s", peers=["p:1"]))
+        assert not r.success and r.error_message == "Not Leader"
+        assert not call("RegisterMaster", pb.RegisterMasterRequest(address="m3:1", shard_id="s")).success
+        assert not call("ShardHeartbeat", pb.ShardHeartbeatRequest(address="m1:1")).success
+        with pytest.raises(grpc.RpcError) as ei:
+            call("FetchShardMap", pb.FetchShardMapRequest())
+        assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION and "Not Leader" in ei.value.details()
+    finally:
+        remote.close()
+        near.close()
+        local.stop()
+        srv.stop()
+        loop.run_until_complete(node.stop())
+        s.core.detach()
+        loop.close()
