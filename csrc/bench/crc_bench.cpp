@@ -4,6 +4,9 @@
 // the LDS slicing-by-16 tables, every result checked against the host CRC.
 //
 //   build/native/crc_bench [--iters N] [--mib TOTAL]     -> JSON on stdout
+//   build/native/crc_bench --sweep                        -> K1/K2 grid x register-ring sweep at
+//                                                            8 / 64 / 256 MiB, plus the streaming
+//                                                            read at those sizes (JSON)
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -35,7 +38,7 @@ struct Run {
 };
 
 static Run bench_block(const uint8_t* d, uint64_t n, const DevCrcTables* t, uint32_t* dmeta, uint32_t* dpart,
-                       hipStream_t s, int iters, const std::vector<uint8_t>& host) {
+                       hipStream_t s, int iters, const std::vector<uint8_t>& host, int grid_override = 0) {
   CrcLaunch a{};
   a.data = d;
   a.n = n;
@@ -47,7 +50,7 @@ static Run bench_block(const uint8_t* d, uint64_t n, const DevCrcTables* t, uint
   a.full_init = crc_init_term(kSliceBytes);
   a.meta_out = dmeta;
   a.part_crc = dpart;
-  int grid = crc_grid_for(a.ntiles, 0);
+  int grid = grid_override > 0 ? grid_override : crc_grid_for(a.ntiles, 0);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -77,10 +80,12 @@ static Run bench_block(const uint8_t* d, uint64_t n, const DevCrcTables* t, uint
 int main(int argc, char** argv) {
   int iters = 50;
   uint64_t total_mib = 1024;
+  bool sweep = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "--iters" && i + 1 < argc) iters = std::atoi(argv[++i]);
     else if (a == "--mib" && i + 1 < argc) total_mib = std::strtoull(argv[++i], nullptr, 10);
+    else if (a == "--sweep") sweep = true;
   }
   CK(hipSetDevice(0));
   hipStream_t s;
@@ -118,6 +123,50 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     stream_gbps = total / (1e3 * ms / it) / 1e3;
     (void)hipFree(dout);
+  }
+  if (sweep) {
+    // where the 64 MiB K1/K2 time goes: per-workgroup fixed cost (grid) vs load latency (ring)
+    std::printf("{\"stream_read_1GiB_GBps\": %.1f, \"stream\": [", stream_gbps);
+    bool f = true;
+    for (uint64_t n : std::vector<uint64_t>{8ull << 20, 64ull << 20, 256ull << 20}) {
+      uint32_t* dout = nullptr;
+      CK(hipMalloc(&dout, 4 * kStreamReadGrid * 4));
+      hipEvent_t e0, e1;
+      CK(hipEventCreate(&e0));
+      CK(hipEventCreate(&e1));
+      CK(launch_stream_read(d, n, dout, s));
+      CK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; ++i) CK(launch_stream_read(d, n, dout, s));
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = 1e3 * ms / iters;
+      std::printf("%s{\"bytes\": %llu, \"us\": %.2f, \"GBps\": %.1f}", f ? "" : ", ",
+                  static_cast<unsigned long long>(n), us, n / us / 1e3);
+      f = false;
+      (void)hipFree(dout);
+    }
+    std::printf("], \"k1k2\": [");
+    f = true;
+    set_crc_mfma(true);
+    set_crc_lds_max_mib(0);
+    for (uint64_t n : std::vector<uint64_t>{8ull << 20, 64ull << 20, 256ull << 20}) {
+      for (int ring : {2, 3, 4}) {
+        set_crc_ring(crc_ring_buffers(), ring);
+        for (int grid : {128, 256, 384, 512, 640, 768}) {
+          if (ring > 2 && grid > 512) continue;
+          // the kernel choice follows ring_for(ntiles): below kCrcRingMinTiles it is the R = 2 kernel
+          Run r = bench_block(d, n, t, dmeta, dpart, s, iters, host, grid);
+          std::printf("%s\n  {\"bytes\": %llu, \"ring\": %d, \"grid\": %d, \"us\": %.2f, \"GBps\": %.1f, \"ok\": %s}",
+                      f ? "" : ",", static_cast<unsigned long long>(n), ring, grid, r.us, n / r.us / 1e3,
+                      r.ok ? "true" : "false");
+          f = false;
+        }
+      }
+    }
+    std::printf("\n]}\n");
+    return 0;
   }
   std::printf("{\"iters\": %d, \"scrub_ring_buffers\": %d, \"tile_ring_buffers\": %d, \"stream_read_GBps\": %.1f, "
               "\"k1k2\": [", iters, crc_ring_buffers(), crc_tile_ring_buffers(), stream_gbps);
