@@ -12,6 +12,7 @@ import json
 import os
 import shutil
 import signal
+import random
 import socket
 import subprocess
 import sys
@@ -24,7 +25,24 @@ PKG = "rust_hadoop_generated_by_llm_amd"
 ROOT = Path(__file__).resolve().parents[2]
 
 
+_handed_out: set[int] = set()
+
+
 def free_port() -> int:
+    """A port nothing listens on, below the kernel's ephemeral range (32768+) so that no
+    outgoing connection takes it before its server binds, and never the same one twice in a
+    process (a port closed here is otherwise free to come back on the next call)."""
+    for _ in range(200):
+        p = random.randint(15000, 32000)
+        if p in _handed_out:
+            continue
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+        _handed_out.add(p)
+        return p
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
