@@ -327,6 +327,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["direct_dma"] = t.direct_dma;
         d["fused_reads"] = t.fused_reads;
         d["fused_writes"] = t.fused_writes;
+        d["sliced_stages"] = t.sliced_stages;
         d["staged_dma"] = t.staged_dma;
         d["host_registered_bytes"] = t.host_registered_bytes;
         return d;
@@ -416,6 +417,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["fp_ec_ops"] = s.ec_ops;
         d["fp_heals_out"] = s.heals_out;
         d["fp_heals_in"] = s.heals_in;
+        d["fp_sliced_writes"] = s.sliced_writes;
         return d;
       })
       .def("replicate_block", [](FastPathServer& f, const std::string& id, const std::vector<std::string>& targets,

@@ -431,6 +431,119 @@ bool ChunkStore::write_copy(Lane* l, const uint8_t* src_dev, uint8_t* dst, uint6
   return true;
 }
 
+// hscratch layout of a sliced stage: [0, 16 + S*4) after the standard partial words holds
+// the host .meta image (as in stage_impl), then kMaxGridCrc partial words per slice.
+static uint64_t sliced_partials_off(uint64_t S) {
+  return (2 * kMaxGridCrc * sizeof(uint32_t) + 16 + S * 4 + 63) / 64 * 64;
+}
+
+bool ChunkStore::stage_slices_begin(const uint8_t* data, uint64_t n, uint64_t slice, SliceStage* ss,
+                                    std::string* err) {
+  if (!gpu() || n == 0 || slice == 0 || slice % kSliceBytes != 0 || !crc_mfma_enabled()) return false;
+  const uint8_t* src_dev = device_view(data, n);
+  if (!src_dev || reinterpret_cast<uintptr_t>(src_dev) % 16 != 0) return false;
+  HIP_OK(hipSetDevice(cfg_.device));
+  ss->ext = reserve(n);
+  if (ss->ext.off < 0) {
+    *err = "HBM arena full";
+    return false;
+  }
+  ss->n = n;
+  ss->slice = slice;
+  Lane* l = acquire_lane();
+  ss->lane = l;
+  const uint64_t S = num_slices(n), nsl = (n + slice - 1) / slice;
+  ensure_hscratch(l, sliced_partials_off(S) + nsl * kMaxGridCrc * sizeof(uint32_t));
+  if (!l->hscratch_dev) {
+    release_lane(l);
+    release(ss->ext);
+    ss->lane = nullptr;
+    return false;
+  }
+  auto* dmeta = reinterpret_cast<uint32_t*>(ss->ext.ptr + align_up(n, 256));
+  auto* hdev = static_cast<uint8_t*>(l->hscratch_dev);
+  auto* meta_host_dev = reinterpret_cast<uint32_t*>(hdev + 2 * kMaxGridCrc * sizeof(uint32_t) + 16);
+  auto* parts_dev = reinterpret_cast<uint32_t*>(hdev + sliced_partials_off(S));
+  for (uint64_t k = 0; k < nsl; ++k) {
+    const uint64_t off = k * slice, len = std::min(slice, n - off);
+    CrcPlan p = plan_crc(src_dev + off, len, dmeta + off / kSliceBytes, nullptr, true, 0, len);
+    WriteCopyLaunch w;
+    w.c = p.a;
+    w.c.part_crc = parts_dev + k * kMaxGridCrc;
+    w.dst = ss->ext.ptr + off;
+    w.meta_host = meta_host_dev + off / kSliceBytes;
+    hipEvent_t ev = nullptr;
+    hipError_t e = launch_write_copy(w, dtables_, p.grid, l->stream);
+    launches_++;
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, l->stream);
+    if (e != hipSuccess) {
+      if (ev) (void)hipEventDestroy(ev);
+      *err = std::string("sliced stage launch: ") + hipGetErrorString(e);
+      (void)hipStreamSynchronize(l->stream);
+      stage_slices_end(ss);
+      return false;
+    }
+    ss->done.push_back(ev);
+    ss->grids.push_back(p.grid);
+  }
+  sliced_stages_++;
+  return true;
+}
+
+WriteResult ChunkStore::stage_slices_finish(const std::string& id, SliceStage* ss, uint32_t expected_crc, int pins) {
+  TraceRange tr("dfs.store.stage_slices");
+  WriteResult res;
+  auto* l = static_cast<Lane*>(ss->lane);
+  HIP_OK(hipSetDevice(cfg_.device));
+  HIP_OK(hipStreamSynchronize(l->stream));
+  const uint64_t n = ss->n, S = num_slices(n);
+  const uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+  const auto* parts = reinterpret_cast<const uint32_t*>(l->hscratch + sliced_partials_off(S));
+  uint32_t raw = 0;
+  for (size_t k = 0; k < ss->grids.size(); ++k) {
+    const uint64_t off = k * ss->slice, len = std::min(ss->slice, n - off);
+    uint32_t r = 0;
+    for (int g = 0; g < ss->grids[k]; ++g) r ^= parts[k * kMaxGridCrc + g];
+    const uint64_t tail = len % kSliceBytes;
+    if (tail) {  // only the last slice: its short tail slice, from the host .meta image
+      const uint32_t tail_crc = __builtin_bswap32(reinterpret_cast<const uint32_t*>(hmeta)[(off + len) / kSliceBytes]);
+      r = crc_shift(r, tail) ^ (tail_crc ^ crc_init_term(tail));
+    }
+    raw = crc_shift(raw, len) ^ r;
+  }
+  const uint32_t crc = raw ^ crc_init_term(n);
+  res.actual_crc = crc;
+  if (expected_crc != 0 && crc != expected_crc) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      ++st_.crc_mismatches;
+    }
+    res.error = "Checksum mismatch: expected " + std::to_string(expected_crc) + ", actual " + std::to_string(crc);
+    return res;  // the extent stays reserved: end() once the sends drained
+  }
+  auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
+  release_lane(l);
+  ss->lane = nullptr;
+  insert_resident(id, ss->ext, n, crc, false, meta, pins);
+  ss->ext = DevExtent{};  // owned by the index now
+  res.ok = true;
+  return res;
+}
+
+void ChunkStore::stage_slices_end(SliceStage* ss) {
+  if (ss->lane) {
+    auto* l = static_cast<Lane*>(ss->lane);
+    (void)hipStreamSynchronize(l->stream);
+    release_lane(l);
+    ss->lane = nullptr;
+  }
+  for (hipEvent_t e : ss->done) (void)hipEventDestroy(e);
+  ss->done.clear();
+  release(ss->ext);
+  ss->ext = DevExtent{};
+}
+
 bool ChunkStore::register_host(const void* p, uint64_t n) {
   if (!gpu() || !p || !n) return false;
   HIP_OK(hipSetDevice(cfg_.device));
@@ -647,7 +760,7 @@ WriteResult ChunkStore::stage(const std::string& id, const uint8_t* data, uint64
 }
 
 void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t crc, bool on_disk,
-                                 std::shared_ptr<std::vector<uint8_t>> meta) {
+                                 std::shared_ptr<std::vector<uint8_t>> meta, int pins) {
   bool hbm_ack = cfg_.durability == Durability::HbmAck;
   {
     std::unique_lock<std::mutex> lk(mu_);
@@ -671,6 +784,7 @@ void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, ui
     b.dirty = !on_disk;
     b.dev_off = ext.off;
     b.dev_bytes = ext.bytes;
+    b.pins = pins;
     if (!on_disk && !hbm_ack) b.staged_meta = std::move(meta);
     touch_locked(id, b);
     if (!on_disk && hbm_ack) spill_q_.push_back(id);
@@ -1888,6 +2002,7 @@ StoreStats ChunkStore::stats() {
   s.direct_dma = direct_dma_.load();
   s.fused_reads = fused_reads_.load();
   s.fused_writes = fused_writes_.load();
+  s.sliced_stages = sliced_stages_.load();
   s.staged_dma = staged_dma_.load();
   s.mirror_hits = mirror_hits_;
   s.mirror_bytes = mirror_bytes_;

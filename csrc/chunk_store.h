@@ -86,6 +86,7 @@ struct StoreStats {
   uint64_t direct_dma = 0;       // host<->HBM copies done straight from registered memory
   uint64_t fused_reads = 0;      // reads delivered by the K3 verify+copy kernel (no SDMA copy)
   uint64_t fused_writes = 0;     // writes staged by the K1/K2 copy+checksum kernel (no SDMA copy)
+  uint64_t sliced_stages = 0;    // pipelined head writes (per-slice fused kernels, sends overlap)
   uint64_t staged_dma = 0;       // copies bounced through pinned staging buffers
   uint64_t host_registered_bytes = 0;
   uint64_t mirror_hits = 0;      // small-block reads served from the verified host mirror
@@ -194,6 +195,23 @@ class ChunkStore {
   WriteResult recv_finish(RecvVerify* rv, const std::string& id, uint32_t expected_crc, bool persist_now);
   // Gives the lane back without touching the extent (a late DMA may still land in it).
   void recv_abandon(RecvVerify* rv);
+  // Pipelined head write (fast path, large replicated blocks): slice k of a block in
+  // registered host memory is copied into HBM and checksummed by its own fused kernel
+  // (crc_write_copy_kernel) and signals done[k], so the replica sends of slice k start while
+  // slice k+1 is still crossing PCIe. finish() waits, folds the slice partials into the
+  // block CRC, verifies, and indexes the block resident (not yet durable) holding `pins`
+  // pins; on failure the extent stays reserved. end() — once no send can still wait on the
+  // slice events or read the extent — frees the events and, after a failure, the extent.
+  struct SliceStage {
+    DevExtent ext;
+    uint64_t n = 0, slice = 0;
+    void* lane = nullptr;
+    std::vector<hipEvent_t> done;
+    std::vector<int> grids;
+  };
+  bool stage_slices_begin(const uint8_t* data, uint64_t n, uint64_t slice, SliceStage* ss, std::string* err);
+  WriteResult stage_slices_finish(const std::string& id, SliceStage* ss, uint32_t expected_crc, int pins);
+  void stage_slices_end(SliceStage* ss);
   // Pin a resident block (promoting it if needed) and return its device pointer.
   const uint8_t* pin_device(const std::string& id, uint64_t* size);
   void unpin(const std::string& id);
@@ -260,7 +278,7 @@ class ChunkStore {
   WriteResult stage_impl(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
                          bool durable_now);
   void insert_resident(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t crc, bool on_disk,
-                       std::shared_ptr<std::vector<uint8_t>> meta);
+                       std::shared_ptr<std::vector<uint8_t>> meta, int pins = 0);
   bool persist_from_device(const std::string& id, const uint8_t* d, uint64_t n, const uint8_t* meta_be,
                            uint64_t nslices, std::string* err);
   bool persist(const std::string& id, bool cold, const uint8_t* data, uint64_t n, const uint8_t* meta_be,
@@ -310,6 +328,7 @@ class ChunkStore {
   uint8_t* device_view(const void* p, uint64_t n);
   std::atomic<uint64_t> fused_reads_{0};  // K3 fused verify+copy reads
   std::atomic<uint64_t> fused_writes_{0};  // K1/K2 fused copy+checksum writes
+  std::atomic<uint64_t> sliced_stages_{0};
   bool write_copy(Lane* l, const uint8_t* src_dev, uint8_t* dst, uint64_t n, uint32_t* dmeta, uint8_t* hmeta,
                   CrcOut* out, std::string* err);
   std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};

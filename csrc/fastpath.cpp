@@ -493,7 +493,8 @@ int FastPathServer::replicate_block(const std::string& id, const std::vector<std
 }
 
 int FastPathServer::replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term,
-                                  const ShmSrc& src, const uint8_t* host, uint64_t n, bool heal) {
+                                  const ShmSrc& src, const uint8_t* host, uint64_t n, bool heal,
+                                  const StagedSource* staged) {
   Peer* p = local_peer(addr);
   if (p == nullptr) return 0;
   std::vector<uint8_t> resp;
@@ -509,7 +510,7 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
     // payload over the P2P transport (RCCL: HBM -> HBM over xGMI), descriptor on the socket
     ReplTicket t;
     std::string err;
-    if (repl_->send(p->rank, id, host, n, &t, &err)) {
+    if (repl_->send(p->rank, id, host, n, &t, &err, staged)) {
       tried_p2p = true;
       std::vector<uint8_t> req(4, 0);
       req.push_back(3);
@@ -607,7 +608,8 @@ bool FastPathServer::persist_and_replicate(const std::string& id, const uint8_t*
 }
 
 void FastPathServer::replicate(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
-                               const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas) {
+                               const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas,
+                               const StagedSource* staged) {
   *replicas = 0;
   if (next.empty()) return;
   // every replica at once: each has its own xGMI link from this GPU
@@ -616,11 +618,55 @@ void FastPathServer::replicate(const std::string& id, uint32_t crc, uint64_t ter
   for (size_t i = 1; i < next.size(); ++i)
     futs.push_back(pool_.submit([&, i] {
       RequestScope rs(rid);
-      return replicate_one(next[i], id, crc, term, src, host, n);
+      return replicate_one(next[i], id, crc, term, src, host, n, false, staged);
     }));
-  int total = replicate_one(next[0], id, crc, term, src, host, n);
+  int total = replicate_one(next[0], id, crc, term, src, host, n, false, staged);
   for (auto& f : futs) total += f.get();
   *replicas = total;
+}
+
+// Pipelined head write: the store stages the block slice by slice
+// (one fused copy+checksum kernel per engine slice) and every replica send posts slice k
+// as soon as it is in HBM, so the links carry slice k while slice k+1 crosses PCIe; the
+// store verifies the whole block from the slice partials while the tail is still in flight.
+// The replicas verify what they receive against the client's CRC on their own, so a block
+// the head rejects is rejected downstream too.
+bool FastPathServer::write_sliced(int fd, const std::string& id, const uint8_t* host, uint64_t len, uint32_t crc,
+                                  uint64_t term, const std::vector<std::string>& next, const ShmSrc& src, bool* sent) {
+  static const uint64_t min_bytes = [] {  // DFS_SLICED_WRITE_MIN_MIB (0 = off)
+    const char* e = std::getenv("DFS_SLICED_WRITE_MIN_MIB");
+    return (e ? std::strtoull(e, nullptr, 10) : 16ull) << 20;
+  }();
+  if (min_bytes == 0 || len < min_bytes || repl_ == nullptr || !store_->gpu() || !repl_->transport()->device_buffers() ||
+      !p2p_ready(next))
+    return false;
+  const uint64_t slice = repl_->slice_for(len);
+  if (len <= slice) return false;  // a single slice: nothing to overlap
+  ChunkStore::SliceStage ss;
+  std::string err;
+  if (!store_->stage_slices_begin(host, len, slice, &ss, &err)) return false;
+  StagedSource staged{ss.ext.ptr, slice, &ss.done};
+  int down = 0;
+  const std::string rid = t_request_id;
+  auto fut = pool_.submit([&] {
+    RequestScope rs(rid);
+    replicate(id, crc, term, next, src, host, len, &down, &staged);
+  });
+  WriteResult wr = store_->stage_slices_finish(id, &ss, crc, 1);  // pinned while the sends read it
+  std::string perr;
+  const bool pok = wr.ok && store_->persist(id, host, len, &perr);
+  fut.get();
+  if (wr.ok) store_->unpin(id);
+  store_->stage_slices_end(&ss);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.sliced_writes++;
+    if (wr.ok) st_.writes++;
+  }
+  if (!wr.ok) *sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
+  else if (!pok) *sent = send_response(fd, FpStatus::IoError, 0, 0, perr);
+  else *sent = send_response(fd, FpStatus::Ok, len, 1 + static_cast<uint64_t>(down), "");
+  return true;
 }
 
 void FastPathServer::serve(int fd) {
@@ -684,7 +730,7 @@ void FastPathServer::serve(int fd) {
         WriteResult wr = store_->write(id, base + off, len, crc);
         if (wr.ok) bump(&FpStats::writes);
         sent = wr.ok ? send_response(fd, FpStatus::Ok, len, 1, "") : send_response(fd, FpStatus::IoError, 0, 0, wr.error);
-      } else {
+      } else if (!write_sliced(fd, id, base + off, len, crc, term, next, ShmSrc{path, off, len}, &sent)) {
         WriteResult wr = store_->stage(id, base + off, len, crc);  // HBM + CRC verify, not yet durable
         if (!wr.ok) {
           sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);

@@ -73,6 +73,7 @@ struct FpStats {
   uint64_t p2p_fallbacks = 0;     // replicas moved to shared memory after a P2P failure
   uint64_t ec_ops = 0;            // erasure-coding matrix products run for clients
   uint64_t heals_out = 0, heals_in = 0;  // heal / balancer copies sent / received on the engine
+  uint64_t sliced_writes = 0;  // head writes whose replica sends overlapped the staging
 };
 
 class FastPathServer {
@@ -145,9 +146,14 @@ class FastPathServer {
   // Fan block `id` out to every address in `next` (all same-host); *replicas = replicas
   // written downstream. `host` is the block in host memory when there is one (shm slot).
   void replicate(const std::string& id, uint32_t crc, uint64_t term, const std::vector<std::string>& next,
-                 const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas);
+                 const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas,
+                 const StagedSource* staged = nullptr);
   int replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term, const ShmSrc& src,
-                    const uint8_t* host, uint64_t n, bool heal = false);
+                    const uint8_t* host, uint64_t n, bool heal = false, const StagedSource* staged = nullptr);
+  // Pipelined head write of a large replicated block; false = not applicable (the caller
+  // takes the stage-then-forward path), true = answered on `fd` (*sent = write result).
+  bool write_sliced(int fd, const std::string& id, const uint8_t* host, uint64_t len, uint32_t crc, uint64_t term,
+                    const std::vector<std::string>& next, const ShmSrc& src, bool* sent);
   bool exchange_with(struct Peer* p, const std::vector<uint8_t>& req, std::vector<uint8_t>* resp);
   Peer* local_peer(const std::string& addr);
 

@@ -424,12 +424,20 @@ void ReplicationEngine::fail_pair_gen(int p, uint64_t gen, const std::string& wh
 
 // ------------------------------------------------------------------ data
 bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_src, uint64_t n, ReplTicket* t,
-                             std::string* err) {
+                             std::string* err, const StagedSource* staged) {
   TraceRange tr("dfs.repl.send");
   t->peer = p;
   t->id = id;
   const uint8_t* src = host_src;
-  if (t_->device_buffers()) {
+  if (staged && (!t_->device_buffers() || !staged->dev || !staged->done || staged->slice == 0 ||
+                 staged->done->size() != (n + staged->slice - 1) / staged->slice)) {
+    *err = "staged send needs a device transport and one event per slice";
+    return false;
+  }
+  if (staged) {
+    (void)hipSetDevice(store_->config().device);
+    src = staged->dev;  // not indexed yet: the caller holds the extent
+  } else if (t_->device_buffers()) {
     (void)hipSetDevice(store_->config().device);
     uint64_t size = 0;
     src = store_->pin_device(id, &size);
@@ -444,8 +452,20 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
     return false;
   }
   t->size = n;
-  t->slice = slice_for(n);
+  t->slice = staged ? staged->slice : slice_for(n);
   Peer& P = peer(p);
+  const auto deadline = Clock::now() + std::chrono::milliseconds(opt_.xfer_timeout_ms);
+  // slice k of a staged block: wait (bounded) until the head's copy of it reached HBM
+  auto landed = [&](uint64_t k) {
+    hipEvent_t ev = (*staged->done)[k];
+    for (int spins = 0;; ++spins) {
+      hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) return true;
+      if (q != hipErrorNotReady || Clock::now() > deadline) return false;
+      if (spins < 64) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
+  };
   bool failed = false;
   {
     std::lock_guard<std::mutex> lk(P.mu);
@@ -456,6 +476,11 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
       t->seq = P.send_seq++;
       for (uint64_t off = 0; off < n; off += t->slice) {
         P2POp op;
+        if (staged && !landed(off / t->slice)) {
+          *err = "staging of slice " + std::to_string(off / t->slice) + " did not complete";
+          failed = true;
+          break;
+        }
         if (!t_->post_send(p, src + off, std::min(t->slice, n - off), &op, err)) {
           failed = true;
           break;

@@ -65,6 +65,14 @@ struct ReplTicket {
   std::vector<P2POp> ops;
 };
 
+// A block the head is still staging into HBM (ChunkStore::SliceStage): slice k may be sent
+// once done[k] has completed. The caller keeps `dev` alive until wait_send / cancel_send.
+struct StagedSource {
+  const uint8_t* dev = nullptr;
+  uint64_t slice = 0;
+  const std::vector<hipEvent_t>* done = nullptr;
+};
+
 struct ReplStats {
   uint64_t bytes_sent = 0, bytes_recv = 0, blocks_sent = 0, blocks_recv = 0;
   uint64_t pair_failures = 0, pair_opens = 0, open_attempts = 0, turn_timeouts = 0, stale_generation = 0;
@@ -98,7 +106,10 @@ class ReplicationEngine {
 
   // Sender: post `id` (resident in HBM for a device transport; `host_src` otherwise) to
   // `peer` as slices. The ticket carries what the peer's descriptor needs.
-  bool send(int peer, const std::string& id, const uint8_t* host_src, uint64_t n, ReplTicket* t, std::string* err);
+  // With `staged` (device transports), slices are posted as the head's staging lands them:
+  // the send of slice k overlaps the host-to-device copy of slice k+1.
+  bool send(int peer, const std::string& id, const uint8_t* host_src, uint64_t n, ReplTicket* t, std::string* err,
+            const StagedSource* staged = nullptr);
   // Waits (bounded) until the posted slices left; unpins. False = the pair was failed.
   bool wait_send(ReplTicket* t, std::string* err);
   // Abandon a ticket whose descriptor never reached the peer (its sends can never match).

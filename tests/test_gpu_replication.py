@@ -82,7 +82,7 @@ def test_device_fanout_slices_checksummed_on_arrival(native, gcluster):
     # the head pins a new client arena on a background thread; its first blocks may go staged
     assert write(a, arena, b"warm", "warm", [b, c])[0] == fp.OK
     wait_registered(a.store, 160 << 20)
-    direct0 = a.store.stats()["direct_dma"]
+    direct0, fused0, sliced0 = (a.store.stats()[k] for k in ("direct_dma", "fused_writes", "sliced_stages"))
     launches0 = b.store.stats()["gpu_kernel_launches"]
     for i, size in enumerate([1, 511, 512, 4097, (1 << 20), 3 * (1 << 20) + 17, 64 << 20]):
         data = os.urandom(size)
@@ -95,9 +95,13 @@ def test_device_fanout_slices_checksummed_on_arrival(native, gcluster):
     # the 64 MiB block alone arrives as 16 x 4 MiB slices, each checksummed as it lands
     assert b.store.stats()["gpu_kernel_launches"] - launches0 >= 16
     assert a.fp.stats()["fp_rccl_forwards"] == 16
-    # the head staged every block straight from the client's registered shm slot
+    # the head staged every block straight from the client's registered shm slot: one DMA
+    # (<= 64 KiB), the fused copy+checksum kernel, or per slice (the 64 MiB block: its sends
+    # start while its later slices are still crossing PCIe)
     st = a.store.stats()
-    assert st["direct_dma"] - direct0 >= 7 and st["host_registered_bytes"] >= 160 << 20
+    assert st["sliced_stages"] - sliced0 >= 1, st
+    zero_copy = st["direct_dma"] - direct0 + st["fused_writes"] - fused0 + st["sliced_stages"] - sliced0
+    assert zero_copy >= 7 and st["host_registered_bytes"] >= 160 << 20, st
     assert b.eng.stats()["bytes_recv"] == c.eng.stats()["bytes_recv"] > 64 << 20
     arena.close()
 
