@@ -231,9 +231,10 @@ def config5(a):
         # what the native front end served itself vs handed to the Python workers
         nat = {}
         for ln in s.get(f"{url}/metrics").text.splitlines():
-            if ln.startswith(("s3_native_requests_total", "s3_native_handoffs_total", "s3_native_bytes")):
+            if ln.startswith(("s3_native_requests_total", "s3_native_handoffs_total", "s3_native_bytes",
+                              "s3_native_get_")):
                 k, v = ln.rsplit(" ", 1)
-                nat[k] = int(float(v))
+                nat[k] = round(float(v), 4) if "seconds" in k else int(float(v))
         out["native_front"] = nat
         emit(out)
 
@@ -249,12 +250,13 @@ def native_load_phase(url: str, a, mpu_bytes: int) -> dict:
     base = [str(exe), "--host", host, "--port", port, "--bucket", "bench", "--conc", str(a.concurrency)]
     out = {"client": f"s3_load, {a.concurrency} C++ threads, keep-alive"}
     n = a.count * 4
+    # timed windows of ~0.3-1 s: PUT n objects, then GET every object 5 times, 64 KiB ranges 20x
     for name, extra in (("put", ["--op", "put", "--count", str(n), "--size", str(a.size), "--prefix", "nat"]),
-                        ("get", ["--op", "get", "--count", str(n), "--size", str(a.size), "--prefix", "nat",
-                                 "--verify"]),
-                        ("range_get_64k", ["--op", "range", "--count", str(n * 8), "--keys", str(n),
+                        ("get", ["--op", "get", "--count", str(n * 5), "--keys", str(n), "--size", str(a.size),
+                                 "--prefix", "nat", "--verify"]),
+                        ("range_get_64k", ["--op", "range", "--count", str(n * 20), "--keys", str(n),
                                            "--size", str(a.size), "--prefix", "nat", "--verify"]),
-                        ("multipart_get", ["--op", "get", "--count", "16", "--size", str(mpu_bytes),
+                        ("multipart_get", ["--op", "get", "--count", "48", "--size", str(mpu_bytes),
                                            "--key", "big.bin"])):
         r = subprocess.run(base + extra, capture_output=True, text=True, timeout=300)
         out[name] = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}

@@ -783,7 +783,10 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   TraceRange tr(head ? "dfs.s3.head" : "dfs.s3.get");
   bool found = false;
   std::string meta, msg;
+  using SC = std::chrono::steady_clock;
+  const auto t0 = SC::now();
   if (fc_->stat(path, &found, &meta, &msg, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "stat");
+  const auto t1 = SC::now();
   if (!found) {
     if (head) return proxy(c, r, nullptr, 0, "head-missing");
     std::string mm;
@@ -825,6 +828,7 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   } rel{fc_, slot};
   const uint64_t want = rng == 1 ? e - s + 1 : m.size;
   if (got != want) return proxy(c, r, nullptr, 0, "short-read");
+  const auto t2 = SC::now();
   std::string h;
   if (rng == 1) {
     h = "HTTP/1.1 206 Partial Content\r\n" + hdrs + "Content-Range: bytes " + std::to_string(s) + "-" +
@@ -836,12 +840,19 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   }
   h += "Content-Length: " + std::to_string(got) + "\r\n" + ka + "\r\n";
   count(r, r.status);
+  const bool ok = send_head_body(c->fd, h, got ? fc_->slot_ptr(slot) : nullptr, got);
+  const auto t3 = SC::now();
+  auto us = [](SC::duration d) { return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::microseconds>(d).count()); };
   {
     std::lock_guard<std::mutex> g(st_mu_);
     (rng == 1 ? st_.range_gets : st_.gets)++;
     st_.bytes_out += got;
+    st_.get_stat_us += us(t1 - t0);
+    st_.get_read_us += us(t2 - t1);
+    st_.get_send_us += us(t3 - t2);
+    st_.get_timed++;
   }
-  return send_head_body(c->fd, h, got ? fc_->slot_ptr(slot) : nullptr, got);
+  return ok;
 }
 
 // GET of a completed multipart object: the parts' sizes come from the layout the completion
@@ -1099,6 +1110,13 @@ std::string S3Front::native_metrics() {
     o += "s3_native_handoffs_total{reason=\"" + kv.first + "\"} " + std::to_string(kv.second) + "\n";
   o += "# TYPE s3_native_bytes_in_total counter\ns3_native_bytes_in_total " + std::to_string(s.bytes_in) + "\n";
   o += "# TYPE s3_native_bytes_out_total counter\ns3_native_bytes_out_total " + std::to_string(s.bytes_out) + "\n";
+  o += "# HELP s3_native_get_phase_seconds_total native GET time by phase (stat, read, send)\n"
+       "# TYPE s3_native_get_phase_seconds_total counter\n";
+  for (auto& kv : {std::make_pair("stat", s.get_stat_us), std::make_pair("read", s.get_read_us),
+                   std::make_pair("send", s.get_send_us)})
+    o += std::string("s3_native_get_phase_seconds_total{phase=\"") + kv.first + "\"} " +
+         std::to_string(kv.second / 1e6) + "\n";
+  o += "# TYPE s3_native_get_timed_total counter\ns3_native_get_timed_total " + std::to_string(s.get_timed) + "\n";
   return o;
 }
 

@@ -61,6 +61,9 @@ struct S3FrontStats {
   uint64_t bytes_in = 0, bytes_out = 0, auth_native = 0, audit_sent = 0, audit_dropped = 0;
   std::map<std::string, uint64_t> by_status;  // "METHOD status" -> count (native requests)
   std::map<std::string, uint64_t> proxy_reasons;
+  // native GET/Range GET phases, summed microseconds: metadata stat, block read into the
+  // slot, response send (where a GET's latency goes)
+  uint64_t get_stat_us = 0, get_read_us = 0, get_send_us = 0, get_timed = 0;
 };
 
 class S3Front {

@@ -15,3 +15,4 @@ cat $out/sliced.log | grep -v "^W2\|^E2" | tail -8
 python3 scripts/sliced_timeline.py --summary $out/prof_sliced | tee $out/sliced_summary.txt
 timeout -k 10 300 build/native/crc_bench --sweep --mib 256 --iters 30 > $out/crc_sweep.json 2> $out/crc_sweep.err || exit $?
 cat $out/crc_sweep.json
+bash scripts/gpu_s3.sh
