@@ -1290,7 +1290,18 @@ int MasterCore::list_files(const std::string& raw, std::string* out) {
   int c;
   if ((c = read_index(out)) != OK) return c;
   pb::ListFilesResponse resp;
-  resp.files = paths(r.path, true);
+  if (!r.with_metadata) {
+    resp.files = paths(r.path, true);
+  } else {  // one consistent pass: paths and their metadata under the same lock
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : files_) {
+      if (kv.first.compare(0, r.path.size(), r.path) != 0 || under_construction_.count(kv.first)) continue;
+      resp.files.push_back(kv.first);
+    }
+    std::sort(resp.files.begin(), resp.files.end());
+    resp.metadata.reserve(resp.files.size());
+    for (auto& p : resp.files) resp.metadata.push_back(files_.at(p));
+  }
   out->clear();
   resp.encode(*out);
   return OK;

@@ -320,6 +320,30 @@ class Client:
             files.update(resp.files)
         return sorted(files)
 
+    def list_all_files_with_metadata(self, path: str = "/") -> dict:
+        """``{path: FileMetadata}`` over every shard in ONE ListFiles round per shard (the
+        ``with_metadata`` extension) instead of a GetFileInfo per file. A master without the
+        extension answers paths only; those files are looked up one by one."""
+        if self.config_server_addrs:
+            self.refresh_shard_map()
+        with self._map_lock:
+            shards = self.shard_map.get_all_shards()
+            peer_lists = [self.shard_map.get_shard_peers(s) or [] for s in shards]
+        if not peer_lists:
+            peer_lists = [self.master_addrs]
+        out: dict = {}
+        for peers in peer_lists:
+            resp, _ = self.execute_rpc_internal([with_scheme(p, self.tls) for p in peers], "ListFiles",
+                                                pb.ListFilesRequest(path=path, with_metadata=True))
+            if len(resp.metadata) == len(resp.files):
+                out.update(zip(resp.files, resp.metadata))
+            else:
+                for f in resp.files:
+                    info = self.get_file_info(f)
+                    if info is not None:
+                        out[f] = info
+        return dict(sorted(out.items()))
+
     def get_file_info(self, path: str):
         resp, _ = self.execute_rpc(path, "GetFileInfo", pb.GetFileInfoRequest(path=path))
         return resp.metadata if resp.found else None

@@ -925,7 +925,10 @@ class S3Gateway:
             return self.s3_error(400, "InvalidArgument", "max-keys must be an integer")
         marker = (q.get("continuation-token") or q.get("start-after") or "") if v2 else q.get("marker", "")
         bp = f"/{bucket}/"
-        files = await self.run(self.client.list_all_files, bp)
+        # one ListFiles round per shard with every file's metadata (the with_metadata
+        # extension) instead of a GetFileInfo per listed key
+        infos = await self.run(self.client.list_all_files_with_metadata, bp)
+        files = list(infos)
         if not files and not await self.run(self.client.exists, bp + ".s3keep"):
             return self.xml(404, X.error("NoSuchBucket", "The specified bucket does not exist", bucket))
         fileset = set(files)
@@ -971,10 +974,11 @@ class S3Gateway:
         def describe(k: str) -> dict:
             p = entries[k]
             if p is None:
-                meta = self._mpu_marker_meta(bp + k)
+                mk = infos.get(bp + k + "/.s3_mpu_completed")
+                meta = self._meta_of(bp + k, mk) if mk is not None else self._mpu_marker_meta(bp + k)
                 return {"key": k, "last_modified": DEFAULT_DATE, "etag": meta.get("ETag", '"000-MPU"'),
                         "size": int(meta.get("x-dfs-mpu-size", 0))}
-            info = self.client.get_file_info(p)
+            info = infos.get(p)
             etag = EMPTY_ETAG
             size, lm = 0, DEFAULT_DATE
             if info is not None:

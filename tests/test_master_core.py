@@ -369,3 +369,27 @@ def test_handlers_guards_redirect_safe_mode_and_ec_shortage(master):
     assert code == 14 and msg.startswith("Need 6 chunk servers for EC(4,2), only 3 available")
     code, msg = call("AllocateBlock", pb.AllocateBlockRequest(path="/nope"), pb.AllocateBlockResponse)
     assert code == 5 and msg == "File not found"
+
+
+def test_list_files_with_metadata_in_one_call(master):
+    """ListFiles{with_metadata} (extension 100): every visible file's metadata aligned with the
+    paths, so an S3 listing page is one RPC per shard instead of one GetFileInfo per key; a
+    file still under construction is listed in neither form."""
+    st, call = master
+    for p, size in (("/l/a", 3), ("/l/b", 5), ("/m/c", 7)):
+        code, r = call("CreateFile", pb.CreateFileRequest(path=p, allocate_block=True, defer_create=True),
+                       pb.CreateFileResponse)
+        blk = r.allocation.block
+        code, c = call("CompleteFile", pb.CompleteFileRequest(path=p, size=size, etag_md5=f"e{size}", create=True,
+                                                              blocks=[blk], attributes={"ETag": f'"e{size}"'}),
+                       pb.CompleteFileResponse)
+        assert code == 0 and c.success
+    call("CreateFile", pb.CreateFileRequest(path="/l/open"), pb.CreateFileResponse)  # classic create: open
+    code, plain = call("ListFiles", pb.ListFilesRequest(path="/l/"), pb.ListFilesResponse)
+    assert list(plain.files) == ["/l/a", "/l/b"] and len(plain.metadata) == 0
+    code, r = call("ListFiles", pb.ListFilesRequest(path="/l/", with_metadata=True), pb.ListFilesResponse)
+    assert code == 0 and list(r.files) == ["/l/a", "/l/b"]
+    assert [(m.path, m.size, m.etag_md5, m.attributes["ETag"]) for m in r.metadata] == [
+        ("/l/a", 3, "e3", '"e3"'), ("/l/b", 5, "e5", '"e5"')]
+    code, one = call("GetFileInfo", pb.GetFileInfoRequest(path="/l/b"), pb.GetFileInfoResponse)
+    assert one.metadata.blocks[0].block_id == r.metadata[1].blocks[0].block_id
