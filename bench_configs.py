@@ -249,12 +249,12 @@ def native_load_phase(url: str, a, mpu_bytes: int) -> dict:
     host, port = url.split("://")[1].rsplit(":", 1)
     base = [str(exe), "--host", host, "--port", port, "--bucket", "bench", "--conc", str(a.concurrency)]
     out = {"client": f"s3_load, {a.concurrency} C++ threads, keep-alive"}
-    n = a.count * 4
-    # timed windows of ~0.3-1 s: PUT n objects, then GET every object 5 times, 64 KiB ranges 20x
+    n = a.count * 10
+    # timed windows of ~0.25-0.5 s: PUT n objects, then GET every object 10 times, 64 KiB ranges 100x
     for name, extra in (("put", ["--op", "put", "--count", str(n), "--size", str(a.size), "--prefix", "nat"]),
-                        ("get", ["--op", "get", "--count", str(n * 5), "--keys", str(n), "--size", str(a.size),
+                        ("get", ["--op", "get", "--count", str(n * 10), "--keys", str(n), "--size", str(a.size),
                                  "--prefix", "nat", "--verify"]),
-                        ("range_get_64k", ["--op", "range", "--count", str(n * 20), "--keys", str(n),
+                        ("range_get_64k", ["--op", "range", "--count", str(n * 100), "--keys", str(n),
                                            "--size", str(a.size), "--prefix", "nat", "--verify"]),
                         ("multipart_get", ["--op", "get", "--count", "48", "--size", str(mpu_bytes),
                                            "--key", "big.bin"])):
