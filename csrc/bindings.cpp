@@ -14,6 +14,7 @@
 #include "gf256.h"
 #include "gpu_kernels.h"
 #include "replication.h"
+#include "cs_agent.h"
 #include "cs_grpc.h"
 #include "grpc_server.h"
 #include "sigv4.h"
@@ -367,6 +368,75 @@ PYBIND11_MODULE(_dfs_native, m) {
         }
         if (!ok) return py::none();
         return py::cast(outs);
+      });
+
+  // ---------------- native chunkserver control loop (csrc/cs_agent.cpp)
+  py::class_<CsAgent>(m, "CsAgent")
+      .def(py::init([](ChunkStore* store, FastPathServer* fp, const std::string& advertise, const std::string& rack_id,
+                       const std::string& storage_dir, int gpu_rank, std::vector<std::string> masters,
+                       std::vector<std::string> config_servers, double heartbeat_s, double scrub_s,
+                       const std::string& ca_cert, const std::string& domain_name, bool tls) {
+             CsAgentConfig c;
+             c.advertise = advertise;
+             c.rack_id = rack_id;
+             c.storage_dir = storage_dir;
+             c.gpu_rank = gpu_rank;
+             c.masters = std::move(masters);
+             c.config_servers = std::move(config_servers);
+             c.heartbeat_ms = std::max(10, static_cast<int>(heartbeat_s * 1000));
+             c.scrub_ms = std::max(10, static_cast<int>(scrub_s * 1000));
+             c.tls = tls;
+             std::shared_ptr<TlsContext> ctx;
+             if (tls) {
+               std::string err;
+               ctx = TlsContext::client(ca_cert, domain_name, &err);
+               if (!ctx) throw std::runtime_error(err);
+             }
+             return std::make_unique<CsAgent>(c, store, fp, ctx);
+           }),
+           py::arg("store"), py::arg("fastpath"), py::arg("advertise"), py::arg("rack_id") = "",
+           py::arg("storage_dir") = "/tmp", py::arg("gpu_rank") = -1, py::arg("masters") = std::vector<std::string>{},
+           py::arg("config_servers") = std::vector<std::string>{}, py::arg("heartbeat_interval") = 5.0,
+           py::arg("scrub_interval") = 60.0, py::arg("ca_cert") = "", py::arg("domain_name") = "",
+           py::arg("tls") = false, py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("start", &CsAgent::start)
+      .def("stop", &CsAgent::stop, py::call_guard<py::gil_scoped_release>())
+      .def("heartbeat_once", &CsAgent::heartbeat_once, py::call_guard<py::gil_scoped_release>())
+      .def("scrub_once", &CsAgent::scrub_once, py::call_guard<py::gil_scoped_release>())
+      .def("recover", &CsAgent::recover, py::call_guard<py::gil_scoped_release>())
+      .def("queue_recovery", &CsAgent::queue_recovery)
+      .def("submit_command", [](CsAgent& a, py::bytes cmd) {
+        std::string c = cmd;
+        py::gil_scoped_release r;
+        a.submit_command(c);
+      })
+      .def("report_new_block", &CsAgent::report_new_block)
+      .def("report_bad_block", &CsAgent::report_bad_block)
+      .def("masters", &CsAgent::masters)
+      .def_property_readonly("known_term", &CsAgent::known_term)
+      .def("stats", [](CsAgent& a) {
+        CsAgentStats s = a.stats();
+        py::dict d;
+        d["agent_heartbeats"] = s.heartbeats;
+        d["agent_heartbeat_failures"] = s.heartbeat_failures;
+        d["agent_commands"] = s.commands;
+        d["agent_map_refreshes"] = s.map_refreshes;
+        d["agent_replicate_engine"] = s.replicate_engine;
+        d["agent_replicate_grpc"] = s.replicate_grpc;
+        d["agent_replicate_failed"] = s.replicate_failed;
+        d["agent_reconstructs"] = s.reconstructs;
+        d["agent_reconstruct_failed"] = s.reconstruct_failed;
+        d["agent_encodes"] = s.encodes;
+        d["agent_encode_failed"] = s.encode_failed;
+        d["agent_recoveries"] = s.recoveries;
+        d["agent_recovery_failed"] = s.recovery_failed;
+        d["agent_deletes"] = s.deletes;
+        d["agent_moves"] = s.moves;
+        d["agent_scrubs"] = s.scrubs;
+        d["agent_scrub_bad"] = s.scrub_bad;
+        d["agent_ec_gpu"] = s.ec_gpu;
+        d["agent_ec_cpu"] = s.ec_cpu;
+        return d;
       });
 
   // ---------------- RCCL replication

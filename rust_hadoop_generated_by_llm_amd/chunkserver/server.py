@@ -172,11 +172,26 @@ class ChunkServerProcess:
         self.metrics = Registry()
         self.cs = ChunkServer(self.store, self.advertise, self.pool, self.masters, self.rccl, rank_map,
                               args.rccl_rank, self.metrics, fastpath=self.fastpath)
+        self.agent = None
+        if self.fastpath is not None and os.environ.get("DFS_CS_AGENT", "native") == "native":
+            # heartbeat, the masters' commands, recovery and the scrubber run natively
+            # (csrc/cs_agent.cpp); the Python loops below stay as the DFS_CS_AGENT=python A/B
+            self.agent = native.CsAgent(
+                self.store, self.fastpath, self.advertise, rack_id=args.rack_id, storage_dir=args.storage_dir,
+                gpu_rank=args.rccl_rank, masters=[strip_scheme(m) for m in self.masters()],
+                config_servers=[strip_scheme(c) for c in self.config_servers],
+                heartbeat_interval=args.heartbeat_interval, scrub_interval=args.scrub_interval,
+                ca_cert=args.ca_cert or "", domain_name=args.domain_name or "", tls=bool(args.tls_cert))
+            self.cs.agent = self.agent
         self._setup_metrics()
         self._stop = threading.Event()
 
     # ------------------------------------------------------------------ helpers
     def masters(self) -> list[str]:
+        if getattr(self, "agent", None) is not None:  # the native loop keeps the shard map fresh
+            ms = self.agent.masters()
+            if ms:
+                return [with_scheme(m) for m in ms]
         ms = self.shard_map.get_all_masters()
         return [with_scheme(m) for m in ms] if ms else self.static_masters
 
@@ -276,6 +291,8 @@ class ChunkServerProcess:
                         d.update(proc.fastpath.stats())
                     if proc.native_grpc is not None:
                         d.update(proc.native_grpc.stats())
+                    if proc.agent is not None:
+                        d.update(proc.agent.stats())
                     if proc.rccl is not None:
                         d.update({f"repl_{k}": v for k, v in proc.rccl.stats().items()})
                         d["repl_transport"] = proc.rccl.transport
@@ -372,8 +389,11 @@ class ChunkServerProcess:
         server = self._start_grpc(a, creds)
         http = self._http()
         threading.Thread(target=http.serve_forever, daemon=True, name="cs-http").start()
-        threading.Thread(target=self._heartbeat_loop, daemon=True, name="cs-heartbeat").start()
-        threading.Thread(target=self._scrub_loop, daemon=True, name="cs-scrub").start()
+        if self.agent is not None:
+            self.agent.start()
+        else:
+            threading.Thread(target=self._heartbeat_loop, daemon=True, name="cs-heartbeat").start()
+            threading.Thread(target=self._scrub_loop, daemon=True, name="cs-scrub").start()
         ready = os.environ.get("DFS_READY_FILE")
         if ready:
             with open(ready, "w") as f:
@@ -385,6 +405,8 @@ class ChunkServerProcess:
         log.info("chunkserver %s serving (gpu=%d, durability=%s)", self.advertise, a.gpu, a.durability)
         while not self._stop.wait(0.5):
             pass
+        if self.agent is not None:
+            self.agent.stop()
         if server is not None:
             server.stop(1.0).wait()
         if self.native_grpc is not None:

@@ -58,6 +58,9 @@ class ChunkServer:
         self.stats = {"writes": 0, "reads": 0, "replicas_in": 0, "rccl_forwards": 0, "grpc_forwards": 0,
                       "rccl_fallbacks": 0, "recoveries": 0, "shm_writes": 0, "shm_reads": 0}
         self.shm = ShmMapper()
+        # native control loop (csrc/cs_agent.cpp): when set, it owns the heartbeat, the master's
+        # commands, recovery and the scrubber; the paths below delegate to it
+        self.agent = None
 
     # ------------------------------------------------------------------ fencing
     def fence(self, term: int) -> None:
@@ -86,6 +89,9 @@ class ChunkServer:
                 self.known_term = term
 
     def queue_recovery(self, block_id: str) -> None:
+        if self.agent is not None:
+            self.agent.queue_recovery(block_id)
+            return
         self._bg.submit(self.recover_block, block_id)
 
     # ------------------------------------------------------------------ forwarding
@@ -221,8 +227,11 @@ class ChunkServer:
             return pb.ReplicateBlockResponse(success=False, error_message=err)
         self.stats["replicas_in"] += 1
         if req.heal:
-            with self._lists_lock:
-                self.new_blocks.append(req.block_id)
+            if self.agent is not None:
+                self.agent.report_new_block(req.block_id)
+            else:
+                with self._lists_lock:
+                    self.new_blocks.append(req.block_id)
         return pb.ReplicateBlockResponse(success=True, replicas_written=replicas)
 
     def _read_shm(self, req):
@@ -294,6 +303,9 @@ class ChunkServer:
         (reference recover_block, chunkserver.rs:353-460; the self-skip uses the
         advertise address instead of the CHUNK_SERVER_ADDR env quirk)."""
         self.stats["recoveries"] += 1
+        if self.agent is not None:
+            err = self.agent.recover(block_id)
+            return err or None
         locs = self.block_locations(block_id)
         if not locs:
             return "No replica locations found for block"
@@ -406,6 +418,9 @@ class ChunkServer:
         return ok
 
     def handle_command(self, cmd) -> None:
+        if self.agent is not None:
+            self.agent.submit_command(cmd.SerializeToString())
+            return
         T = pb.ChunkServerCommand
         if cmd.master_term:
             self.adopt_term(cmd.master_term)
@@ -435,6 +450,8 @@ class ChunkServer:
     def scrub_once(self) -> list[str]:
         """K1b batched scrub: verify every block; queue bad ones for the next heartbeat
         and try to recover them (reference run_background_scrubber, chunkserver.rs:642-718)."""
+        if self.agent is not None:
+            return self.agent.scrub_once()
         bad = self.store.scrub()
         if bad:
             with self._lists_lock:

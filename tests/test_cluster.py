@@ -129,6 +129,7 @@ def test_corruption_detected_and_recovered(cluster3):
     assert got == data
     stats = json.load(urllib.request.urlopen(f"{http}/stats"))
     assert stats["recoveries"] >= 1
+    assert stats["agent_recoveries"] >= 1  # the fetch-verify-rewrite ran in the native agent
     # and the on-disk copy is good again: a scrub finds nothing
     assert json.load(urllib.request.urlopen(f"{http}/debug/scrub"))["bad"] == []
     # a partial read that touches only a corrupted slice still returns data and heals
@@ -413,6 +414,8 @@ def test_tiering_moves_cold_and_converts_to_ec():
                 break
             time.sleep(0.3)
         assert left == 0
+        st = [json.load(urllib.request.urlopen(f"{u}/stats")) for u in cl.cs_http]
+        assert sum(x["agent_encodes"] for x in st) >= 1 and sum(x["agent_deletes"] for x in st) >= 1, st
         cl.kill(f"cs{cs_index(cl, b.locations[0])}")
         assert c.get_file_content("/tier/f") == data  # degraded decode
         c.close()
@@ -451,10 +454,15 @@ def test_healer_rereplicates_and_rebuilds_ec_shards(p2p):
         assert c.read_block_from_location(spare, eb.block_id) is not None
         assert c.get_file_content("/heal/rep") == rep
         assert c.get_file_content("/heal/ec") == ec
+        st = [json.load(urllib.request.urlopen(f"{u}/stats")) for i, u in enumerate(cl.cs_http)
+              if cl.cs_addrs[i] != dead]
+        # heartbeats, the REPLICATE and RECONSTRUCT_EC_SHARD commands ran in the native agents
+        assert sum(x["agent_reconstructs"] for x in st) >= 1 and all(x["agent_heartbeats"] > 0 for x in st), st
         if p2p == "socket":
-            st = [json.load(urllib.request.urlopen(f"{u}/stats")) for i, u in enumerate(cl.cs_http)
-                  if cl.cs_addrs[i] != dead]
             assert sum(x["fp_heals_out"] for x in st) >= 1 and sum(x["fp_heals_in"] for x in st) >= 1, st
+            assert sum(x["agent_replicate_engine"] for x in st) >= 1, st
+        else:
+            assert sum(x["agent_replicate_grpc"] for x in st) >= 1, st
         c.close()
 
 
