@@ -510,26 +510,71 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
     // payload over the P2P transport (RCCL: HBM -> HBM over xGMI), descriptor on the socket
     ReplTicket t;
     std::string err;
-    if (repl_->send(p->rank, id, host, n, &t, &err, staged)) {
-      tried_p2p = true;
+    auto descriptor = [&](const ReplTicket& tk) {
       std::vector<uint8_t> req(4, 0);
       req.push_back(3);
       put<uint64_t>(req, term);
       put<uint32_t>(req, crc);
       put<int32_t>(req, repl_->rank());
-      put<uint64_t>(req, t.gen);
-      put<int64_t>(req, t.seq);
-      put<uint64_t>(req, t.size);
-      put<uint64_t>(req, t.slice);
+      put<uint64_t>(req, tk.gen);
+      put<int64_t>(req, tk.seq);
+      put<uint64_t>(req, tk.size);
+      put<uint64_t>(req, tk.slice);
       put_str(req, id);
       put<uint16_t>(req, 0);  // fan-out: the replica forwards nowhere
       put_str(req, t_request_id);
       put<uint8_t>(req, heal ? 1 : 0);  // a heal copy: the receiver reports the new location
       finish_frame(req);
+      return req;
+    };
+    // A staged (still landing) block announces itself before its first slice is posted, so
+    // the replica posts its receives while the head's later slices still cross PCIe; the
+    // reply is read after the posts. Otherwise: post, then one descriptor round trip.
+    int early_fd = -1;
+    auto announce = [&](const ReplTicket& tk) {
+      std::vector<uint8_t> req = descriptor(tk);
+      {
+        std::lock_guard<std::mutex> g(p->mu);
+        if (!p->idle.empty()) {
+          early_fd = p->idle.back();
+          p->idle.pop_back();
+        }
+      }
+      if (early_fd < 0) early_fd = connect_abstract(p->name);
+      if (early_fd >= 0 && write_full(early_fd, req.data(), req.size())) return true;
+      if (early_fd >= 0) ::close(early_fd);
+      early_fd = -1;
+      return false;
+    };
+    std::function<bool(const ReplTicket&)> ann;
+    if (staged) ann = announce;
+    const bool posted = repl_->send(p->rank, id, host, n, &t, &err, staged, ann);
+    if (!posted && early_fd >= 0) {  // announced, then failed: the pair is failed, the peer gives up
+      ::close(early_fd);
+      early_fd = -1;
+    }
+    if (posted) {
+      tried_p2p = true;
       bool io_ok;
       int drop = drop_descriptors_.load();
-      if (drop > 0 && drop_descriptors_.compare_exchange_strong(drop, drop - 1)) io_ok = false;  // test hook
-      else io_ok = exchange_with(p, req, &resp);
+      if (staged) {
+        uint32_t rn = 0;
+        io_ok = read_full(early_fd, &rn, 4) && rn >= 19 && rn <= kMaxBody;
+        if (io_ok) {
+          resp.resize(rn);
+          io_ok = read_full(early_fd, resp.data(), rn);
+        }
+        if (io_ok) {
+          std::lock_guard<std::mutex> g(p->mu);
+          p->idle.push_back(early_fd);
+        } else {
+          ::close(early_fd);
+        }
+      } else if (drop > 0 && drop_descriptors_.compare_exchange_strong(drop, drop - 1)) {
+        io_ok = false;  // test hook
+      } else {
+        io_ok = exchange_with(p, descriptor(t), &resp);
+      }
       if (!io_ok) {
         // the posted sends can never be matched now: abort the pair (it is rebuilt under a
         // new generation) and move this replica to shared memory below

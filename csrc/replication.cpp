@@ -424,7 +424,8 @@ void ReplicationEngine::fail_pair_gen(int p, uint64_t gen, const std::string& wh
 
 // ------------------------------------------------------------------ data
 bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_src, uint64_t n, ReplTicket* t,
-                             std::string* err, const StagedSource* staged) {
+                             std::string* err, const StagedSource* staged,
+                             const std::function<bool(const ReplTicket&)>& announce) {
   TraceRange tr("dfs.repl.send");
   t->peer = p;
   t->id = id;
@@ -474,7 +475,11 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
     } else {
       t->gen = P.gen;
       t->seq = P.send_seq++;
-      for (uint64_t off = 0; off < n; off += t->slice) {
+      if (announce && !announce(*t)) {
+        *err = "descriptor to rank " + std::to_string(p) + " failed";
+        failed = true;  // the sequence number is spent: the pair cannot stay in step
+      }
+      for (uint64_t off = 0; !failed && off < n; off += t->slice) {
         P2POp op;
         if (staged && !landed(off / t->slice)) {
           *err = "staging of slice " + std::to_string(off / t->slice) + " did not complete";

@@ -108,8 +108,11 @@ class ReplicationEngine {
   // `peer` as slices. The ticket carries what the peer's descriptor needs.
   // With `staged` (device transports), slices are posted as the head's staging lands them:
   // the send of slice k overlaps the host-to-device copy of slice k+1.
+  // `announce` (optional) runs once the ticket is stamped and BEFORE any slice is posted (the
+  // caller sends the peer its descriptor there, so the peer posts its receives while the
+  // staged slices are still landing); returning false fails the pair.
   bool send(int peer, const std::string& id, const uint8_t* host_src, uint64_t n, ReplTicket* t, std::string* err,
-            const StagedSource* staged = nullptr);
+            const StagedSource* staged = nullptr, const std::function<bool(const ReplTicket&)>& announce = nullptr);
   // Waits (bounded) until the posted slices left; unpins. False = the pair was failed.
   bool wait_send(ReplTicket* t, std::string* err);
   // Abandon a ticket whose descriptor never reached the peer (its sends can never match).
