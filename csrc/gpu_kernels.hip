@@ -289,6 +289,13 @@ __device__ __forceinline__ uint32_t tail_crc(const DevCrcTables& lt, const uint8
   return combine(r, 4, lane, lt.sh256);
 }
 
+// Contiguous, balanced tile runs: workgroup b owns [b*T/G, (b+1)*T/G), so every workgroup
+// gets floor or ceil of T/G tiles. (A ceil-sized split gave 64 MiB = 4096 tiles over 768
+// workgroups as 683 runs of 6 — some CUs 18 tiles, others 12 — and left 85 slots idle.)
+__device__ __forceinline__ uint64_t tile_run_begin(uint64_t ntiles, uint64_t b) {
+  return b * ntiles / gridDim.x;
+}
+
 // LDS slicing-by-16 implementation (DFS_CRC_MFMA=0; the A/B baseline of crc_bench).
 __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
                                                                    const DevCrcTables* __restrict__ gt) {
@@ -406,9 +413,7 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
   __shared__ uint32_t wacc[4];
   __shared__ uint32_t wg_bad;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
-  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
-  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
-  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  const uint64_t t_begin = tile_run_begin(a.ntiles, blockIdx.x), t_end = tile_run_begin(a.ntiles, blockIdx.x + 1);
   const int64_t lo = static_cast<int64_t>(a.slice_lo), hi = static_cast<int64_t>(a.slice_hi);
   auto first_slice = [&](uint64_t t) {
     return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8) - static_cast<int64_t>(a.vfront);
@@ -516,9 +521,7 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
   __shared__ uint32_t wg_bad;
   const CrcLaunch& c = a.c;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
-  const uint64_t per = (c.ntiles + gridDim.x - 1) / gridDim.x;
-  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
-  const uint64_t t_end = t_begin + per < c.ntiles ? t_begin + per : c.ntiles;
+  const uint64_t t_begin = tile_run_begin(c.ntiles, blockIdx.x), t_end = tile_run_begin(c.ntiles, blockIdx.x + 1);
   const int64_t lo = static_cast<int64_t>(c.slice_lo), hi = static_cast<int64_t>(c.slice_hi);
   auto first_slice = [&](uint64_t t) { return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8); };
   WaveData cur;
@@ -584,9 +587,7 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
   __shared__ uint32_t wacc[4];
   const CrcLaunch& c = a.c;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
-  const uint64_t per = (c.ntiles + gridDim.x - 1) / gridDim.x;
-  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
-  const uint64_t t_end = t_begin + per < c.ntiles ? t_begin + per : c.ntiles;
+  const uint64_t t_begin = tile_run_begin(c.ntiles, blockIdx.x), t_end = tile_run_begin(c.ntiles, blockIdx.x + 1);
   const int64_t lo = static_cast<int64_t>(c.slice_lo), hi = static_cast<int64_t>(c.slice_hi);
   auto first_slice = [&](uint64_t t) {
     return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8) - static_cast<int64_t>(c.vfront);
@@ -645,9 +646,7 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
                                                                        const DevCrcTables* __restrict__ gt) {
   __shared__ MfmaSliceLds lt;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
-  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
-  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
-  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  const uint64_t t_begin = tile_run_begin(a.ntiles, blockIdx.x), t_end = tile_run_begin(a.ntiles, blockIdx.x + 1);
   uint32_t blk = 0;
   if (t_begin < t_end) {
     uint32_t l = 0, h = a.nblocks;
@@ -732,9 +731,7 @@ void crc_tile_ring_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   __shared__ uint32_t wacc[4];
   __shared__ uint32_t wg_bad;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
-  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
-  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
-  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  const uint64_t t_begin = tile_run_begin(a.ntiles, blockIdx.x), t_end = tile_run_begin(a.ntiles, blockIdx.x + 1);
   const int64_t lo = static_cast<int64_t>(a.slice_lo), hi = static_cast<int64_t>(a.slice_hi);
   auto first_slice = [&](uint64_t t) {
     return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8) - static_cast<int64_t>(a.vfront);
@@ -822,9 +819,7 @@ void crc_scrub_ring_kernel(ScrubLaunch a, const DevCrcTables* __restrict__ gt) {
   __shared__ MfmaSliceLds lt;
   ConstScrubBlock* blocks = (ConstScrubBlock*)a.blocks;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, sw = lane >> 3, sl = lane & 7;
-  const uint64_t per = (a.ntiles + gridDim.x - 1) / gridDim.x;
-  const uint64_t t_begin = static_cast<uint64_t>(blockIdx.x) * per;
-  const uint64_t t_end = t_begin + per < a.ntiles ? t_begin + per : a.ntiles;
+  const uint64_t t_begin = tile_run_begin(a.ntiles, blockIdx.x), t_end = tile_run_begin(a.ntiles, blockIdx.x + 1);
   const bool work = t_begin < t_end;  // workgroup-uniform
   uint32_t blk = 0;
   if (work) {
