@@ -655,7 +655,8 @@ PYBIND11_MODULE(_dfs_native, m) {
              n->svc = std::make_unique<NativeChunkService>(store, fp, [fb](const GrpcCall& c) -> GrpcReply {
                py::gil_scoped_acquire g;
                try {
-                 py::tuple r = (*fb)(c.path, c.request_id, py::bytes(c.message));
+                 py::tuple r = (*fb)(c.path, c.request_id,
+                                     py::bytes(reinterpret_cast<const char*>(c.data()), c.size()));
                  return GrpcReply{r[0].cast<int>(), r[1].cast<std::string>()};
                } catch (py::error_already_set& e) {
                  return GrpcReply{13, std::string("python handler failed: ") + e.what()};
@@ -664,6 +665,8 @@ PYBIND11_MODULE(_dfs_native, m) {
              NativeChunkService* svc = n->svc.get();
              n->srv = std::make_unique<GrpcServer>(host, port, [svc](const GrpcCall& c) { return svc->handle(c); },
                                                    workers);
+             n->srv->set_body_allocator([svc](size_t len) { return svc->request_buffer(len); },
+                                        NativeChunkService::kRequestBufferMin);
              if (!tls_cert.empty()) {
                std::string err;
                auto t = TlsContext::server(tls_cert, tls_key, &err);

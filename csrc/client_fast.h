@@ -31,13 +31,24 @@
 
 namespace dfs {
 
-// A WriteBlockRequest with `data` (field 2) appended straight from the caller's buffer:
-// one copy of the payload into the wire message instead of two (field order is free in
-// proto3, and the server decodes field 2 as a view — cs_grpc.cpp decode_viewing).
+// A WriteBlockRequest with `data` (field 2) appended straight from the caller's buffer: one
+// copy of the payload into the wire message instead of two (field order is free in proto3,
+// and the server decodes field 2 as a view — cs_grpc.cpp decode_viewing). An
+// `alignment_pad` (field 110) in front makes the payload start at a multiple of 16 bytes of
+// the message, which the chunkserver receives into a page-aligned registered buffer: the
+// fused write kernel then loads the block straight from where the socket put it.
 inline std::string encode_with_payload(const pb::WriteBlockRequest& w, const uint8_t* data, size_t n) {
   std::string wire;
   wire.reserve(n + 256 + w.block_id.size());
   w.encode(wire);
+  size_t vl = 1;
+  for (uint64_t v = n; v >= 0x80; v >>= 7) ++vl;
+  // pad field: tag (2 bytes for field 110) + length (1 byte) + L bytes, then tag 2 + varint(n)
+  const size_t before = wire.size() + 3 + 1 + vl;
+  const size_t pad = (16 - before % 16) % 16;
+  pb::wire::tag(wire, 110, 2);
+  pb::wire::varint(wire, pad);
+  wire.append(pad, '\0');
   pb::wire::tag(wire, 2, 2);
   pb::wire::varint(wire, n);
   wire.append(reinterpret_cast<const char*>(data), n);

@@ -37,9 +37,8 @@ size_t put_varint(uint8_t* o, uint64_t v) {
 // frames and the store. The generated decoders only assign what they meet, so the
 // segments around the field decode one after another into the same message.
 template <class M>
-bool decode_viewing(M& m, const std::string& s, uint32_t field, const uint8_t** q, size_t* l) {
-  const auto* p = reinterpret_cast<const uint8_t*>(s.data());
-  const uint8_t* e = p + s.size();
+bool decode_viewing(M& m, const uint8_t* p, size_t size, uint32_t field, const uint8_t** q, size_t* l) {
+  const uint8_t* e = p + size;
   pb::wire::Reader r{p, e};
   const uint8_t* seg = p;
   *q = reinterpret_cast<const uint8_t*>("");
@@ -134,9 +133,25 @@ class ReplyPool : public std::enable_shared_from_this<ReplyPool> {
 };
 
 NativeChunkService::NativeChunkService(ChunkStore* store, FastPathServer* fp, Fallback fallback)
-    : store_(store), fp_(fp), fallback_(std::move(fallback)), replies_(std::make_shared<ReplyPool>(store)) {
+    : store_(store),
+      fp_(fp),
+      fallback_(std::move(fallback)),
+      replies_(std::make_shared<ReplyPool>(store)),
+      requests_(std::make_shared<ReplyPool>(store)) {
   const char* e = std::getenv("DFS_GRPC_REPLY_PREWARM");
-  if (store_->gpu()) replies_->prewarm(e ? static_cast<size_t>(std::atoi(e)) : 16);
+  if (store_->gpu()) {
+    replies_->prewarm(e ? static_cast<size_t>(std::atoi(e)) : 16);
+    requests_->prewarm(e ? static_cast<size_t>(std::atoi(e)) : 16);
+  }
+}
+
+// Registered buffers for large requests (WriteBlock payloads): the HTTP/2 DATA frames land
+// in memory the store can DMA from (or the fused write kernel can load over PCIe), and the
+// client's alignment_pad makes the payload 16-byte aligned in it. nullptr: the server keeps
+// its std::string body (CPU store, request larger than a pool buffer, pool exhausted).
+std::shared_ptr<uint8_t> NativeChunkService::request_buffer(size_t n) {
+  if (!store_->gpu() || n + 16 > ReplyPool::kBytes) return nullptr;
+  return requests_->take();
 }
 
 CsGrpcStats NativeChunkService::stats() const {
@@ -161,14 +176,14 @@ GrpcReply NativeChunkService::handle(const GrpcCall& call) {
   if (handled) return r;
   fallbacks_++;
   if (!fallback_) return {12, "method not implemented natively: " + call.path};
-  return fallback_(call);
+  return fallback_(call);  // the fallback reads call.data() / call.size()
 }
 
 GrpcReply NativeChunkService::write_block(const GrpcCall& call, bool* handled) {
   pb::WriteBlockRequest req;
   const uint8_t* data;
   size_t n;
-  if (!decode_viewing(req, call.message, 2, &data, &n)) {
+  if (!decode_viewing(req, call.data(), call.size(), 2, &data, &n)) {
     *handled = true;
     return {kInternal, "malformed WriteBlockRequest"};
   }
@@ -204,7 +219,7 @@ GrpcReply NativeChunkService::write_block(const GrpcCall& call, bool* handled) {
 
 GrpcReply NativeChunkService::read_block(const GrpcCall& call, bool* handled) {
   pb::ReadBlockRequest req;
-  if (!req.decode(call.message)) {
+  if (!req.decode(call.data(), call.size())) {
     *handled = true;
     return {kInternal, "malformed ReadBlockRequest"};
   }
@@ -281,7 +296,7 @@ GrpcReply NativeChunkService::replicate_block(const GrpcCall& call, bool* handle
   pb::ReplicateBlockRequest req;
   const uint8_t* data;
   size_t n;
-  if (!decode_viewing(req, call.message, 2, &data, &n)) {
+  if (!decode_viewing(req, call.data(), call.size(), 2, &data, &n)) {
     *handled = true;
     return {kInternal, "malformed ReplicateBlockRequest"};
   }

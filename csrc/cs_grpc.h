@@ -29,6 +29,9 @@ class NativeChunkService {
   NativeChunkService(ChunkStore* store, FastPathServer* fp, Fallback fallback);
   GrpcReply handle(const GrpcCall& call);
   CsGrpcStats stats() const;
+  // GrpcServer body allocator (registered request buffers); nullptr = default body.
+  std::shared_ptr<uint8_t> request_buffer(size_t n);
+  static constexpr size_t kRequestBufferMin = 64 << 10;
 
  private:
   GrpcReply write_block(const GrpcCall& call, bool* handled);
@@ -39,7 +42,7 @@ class NativeChunkService {
   ChunkStore* store_;
   FastPathServer* fp_;
   Fallback fallback_;
-  std::shared_ptr<class ReplyPool> replies_;
+  std::shared_ptr<class ReplyPool> replies_, requests_;
   std::atomic<uint64_t> writes_{0}, reads_{0}, replicates_{0}, fallbacks_{0};
 };
 

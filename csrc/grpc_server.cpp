@@ -69,6 +69,9 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     char head[5];
     size_t head_len = 0;
     std::string body;
+    std::shared_ptr<uint8_t> ext;  // body from the server's allocator (body stays empty)
+    size_t ext_len = 0;
+    size_t received() const { return ext ? ext_len : body.size(); }
     // response: prefix + message, served by read_body without concatenating them
     char prefix[5];
     std::string out;
@@ -172,7 +175,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     if (it == streams.end() || it->second.dispatched) return;
     Stream& st = it->second;
     st.dispatched = true;
-    buffered -= std::min(buffered, st.body.size());
+    buffered -= std::min(buffered, st.received());
     GrpcReply bad;
     if (st.too_big) {
       bad = {8, "message larger than the " + std::to_string(kMaxMessage) + " byte limit"};
@@ -183,7 +186,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     } else {
       uint32_t n;
       std::memcpy(&n, st.head + 1, 4);
-      if (ntohl(n) != st.body.size()) bad = {13, "gRPC message length mismatch"};
+      if (ntohl(n) != st.received()) bad = {13, "gRPC message length mismatch"};
     }
     if (bad.status) {
       respond(sid, bad);
@@ -192,8 +195,15 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     auto call = std::make_shared<GrpcCall>();
     call->path = std::move(st.path);
     call->request_id = std::move(st.rid);
-    call->message = std::move(st.body);
-    st.body = std::string();
+    if (st.ext) {
+      call->body = st.ext.get();
+      call->body_len = st.ext_len;
+      call->body_keep = std::move(st.ext);
+      st.ext_len = 0;
+    } else {
+      call->message = std::move(st.body);
+      st.body = std::string();
+    }
     auto self = shared_from_this();
     std::lock_guard<std::mutex> g(srv->mu_);
     srv->jobs_.emplace_back([self, sid, call] {
@@ -248,23 +258,31 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
             c->refuse(st);
             return 0;
           }
-          st.body.reserve(n);
           st.declared = n;
+          if (c->srv->body_alloc_ && n >= c->srv->body_min_) st.ext = c->srv->body_alloc_(n);
+          if (!st.ext) st.body.reserve(n);
         }
       }
-      if (len && (st.head_len < 5 || st.body.size() + len > st.declared)) {
+      if (len && (st.head_len < 5 || st.received() + len > st.declared)) {
         c->refuse(st);  // more bytes than the prefix announced
         return 0;
       }
-      st.body.append(reinterpret_cast<const char*>(data), len);
+      if (st.ext) {
+        std::memcpy(st.ext.get() + st.ext_len, data, len);
+        st.ext_len += len;
+      } else {
+        st.body.append(reinterpret_cast<const char*>(data), len);
+      }
       c->buffered += len;
     }
     return 0;
   }
   void refuse(Stream& st) {
     st.too_big = true;
-    buffered -= std::min(buffered, st.body.size());
+    buffered -= std::min(buffered, st.received());
     st.body = std::string();
+    st.ext.reset();
+    st.ext_len = 0;
   }
   static int on_frame(nghttp2_session*, const nghttp2_frame* f, void* user) {
     if ((f->hd.type == NGHTTP2_DATA || f->hd.type == NGHTTP2_HEADERS) && (f->hd.flags & NGHTTP2_FLAG_END_STREAM))
@@ -275,7 +293,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     auto* c = static_cast<Conn*>(user);
     auto it = c->streams.find(sid);
     if (it == c->streams.end()) return 0;
-    if (!it->second.dispatched) c->buffered -= std::min(c->buffered, it->second.body.size());
+    if (!it->second.dispatched) c->buffered -= std::min(c->buffered, it->second.received());
     c->streams.erase(it);
     return 0;
   }

@@ -30,7 +30,14 @@ class TlsContext;
 struct GrpcCall {
   std::string path;        // "/dfs.ChunkServerService/WriteBlock"
   std::string request_id;  // x-request-id metadata ("" if absent)
-  std::string message;     // the serialized request
+  std::string message;     // the serialized request (empty when `body` is set)
+  // A large request received into a buffer from the server's body allocator (registered
+  // host memory on a chunkserver) instead of `message`; `body_keep` owns it.
+  const uint8_t* body = nullptr;
+  size_t body_len = 0;
+  std::shared_ptr<const void> body_keep;
+  const uint8_t* data() const { return body ? body : reinterpret_cast<const uint8_t*>(message.data()); }
+  size_t size() const { return body ? body_len : message.size(); }
 };
 
 struct GrpcReply {
@@ -52,6 +59,15 @@ class GrpcServer {
   GrpcServer(const GrpcServer&) = delete;
   // Serve TLS (ALPN h2) instead of h2c; call before start().
   void set_tls(std::shared_ptr<TlsContext> tls) { tls_ = std::move(tls); }
+  // Requests of at least `min_bytes` are received into buffers from `alloc` (nullptr from it:
+  // the default std::string). A chunkserver hands out registered host memory here, so a
+  // WriteBlock payload is DMA'd (or copied by the fused write kernel) straight from where
+  // the socket put it. Call before start().
+  using BodyAlloc = std::function<std::shared_ptr<uint8_t>(size_t n)>;
+  void set_body_allocator(BodyAlloc alloc, size_t min_bytes) {
+    body_alloc_ = std::move(alloc);
+    body_min_ = min_bytes;
+  }
   bool start(std::string* err);
   void stop();
   int port() const { return port_; }
@@ -67,6 +83,8 @@ class GrpcServer {
   std::string host_;
   int port_;
   Handler handler_;
+  BodyAlloc body_alloc_;
+  size_t body_min_ = 0;
   int nworkers_;
   int lfd_ = -1;
   std::atomic<bool> stop_{false};

@@ -81,6 +81,22 @@ def test_gpu_fused_reads_local_and_remote(gpu_cluster):
     c.close()
 
 
+def test_gpu_remote_writes_land_in_registered_request_buffers(gpu_cluster):
+    """A client that is not co-located writes over gRPC/TCP: the native server receives the
+    WriteBlock into a registered, page-aligned request buffer and the client's alignment_pad
+    puts the payload on a 16-byte boundary, so the block is staged by the fused copy+checksum
+    kernel straight from where the socket put it (no bounce copy)."""
+    rc = gpu_cluster.client(local_chunkserver=None, local_rpc=False)
+    f0 = stats(gpu_cluster)["fused_writes"]
+    blobs = {f"/gpu/rw{i}": os.urandom(sz) for i, sz in enumerate([(1 << 20), 300_001, (3 << 20) + 5])}
+    for p, d in blobs.items():
+        rc.create_file_from_buffer(d, p)
+    for p, d in blobs.items():
+        assert rc.get_file_content(p) == d
+    assert stats(gpu_cluster)["fused_writes"] - f0 >= len(blobs)
+    rc.close()
+
+
 def test_gpu_cli_benchmark(gpu_cluster, capsys):
     m = ["-m", gpu_cluster.master_addrs[0]]
     assert dfs_cli.main([*m, "benchmark", "write", "-c", "20", "-s", "1048576", "-n", "10", "-p", "/gbw",
