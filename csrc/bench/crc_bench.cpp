@@ -4,6 +4,7 @@
 // the LDS slicing-by-16 tables, every result checked against the host CRC.
 //
 //   build/native/crc_bench [--iters N] [--mib TOTAL]     -> JSON on stdout
+//   build/native/crc_bench --single MIB [--iters N] -> the production K1/K2 dispatch at one size
 //   build/native/crc_bench --sweep                        -> K1/K2 grid x register-ring sweep at
 //                                                            8 / 64 / 256 MiB, plus the streaming
 //                                                            read at those sizes (JSON)
@@ -81,11 +82,13 @@ int main(int argc, char** argv) {
   int iters = 50;
   uint64_t total_mib = 1024;
   bool sweep = false;
+  uint64_t single_mib = 0;  // --single MIB: only the production K1/K2 dispatch at that size (PMC runs)
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "--iters" && i + 1 < argc) iters = std::atoi(argv[++i]);
     else if (a == "--mib" && i + 1 < argc) total_mib = std::strtoull(argv[++i], nullptr, 10);
     else if (a == "--sweep") sweep = true;
+    else if (a == "--single" && i + 1 < argc) single_mib = std::strtoull(argv[++i], nullptr, 10);
   }
   CK(hipSetDevice(0));
   hipStream_t s;
@@ -123,6 +126,13 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     stream_gbps = total / (1e3 * ms / it) / 1e3;
     (void)hipFree(dout);
+  }
+  if (single_mib) {
+    const uint64_t n = std::min<uint64_t>(single_mib << 20, total);
+    Run r = bench_block(d, n, t, dmeta, dpart, s, iters, host);
+    std::printf("{\"bytes\": %llu, \"us\": %.2f, \"GBps\": %.1f, \"ok\": %s}\n", static_cast<unsigned long long>(n), r.us,
+                n / r.us / 1e3, r.ok ? "true" : "false");
+    return r.ok ? 0 : 1;
   }
   if (sweep) {
     // where the 64 MiB K1/K2 time goes: per-workgroup fixed cost (grid) vs load latency (ring)
