@@ -392,6 +392,7 @@ def main():
             # is not co-located, so every WriteBlock/ReadBlock carries the payload over gRPC
             rc = Client([my_master], local_chunkserver=None, local_rpc=False)
             rc.set_shard_map(ShardMap.load_config_file(str(shard_file)))
+            rc.phase_times = {}
             barrier()
             rwl, rrl, rwb, rrb, rwt, rrt = [], [], 0, 0, 0.0, 0.0
             for s in range(a.remote_steps):
@@ -406,7 +407,8 @@ def main():
                 rwt += ws.total_s
                 rrt += rs.total_s
             remote = {"wl": rwl, "rl": rrl, "wbytes": rwb, "rbytes": rrb, "wt": rwt, "rt": rrt,
-                      "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count}
+                      "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count,
+                      "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in rc.phase_times.items() if v}}
             rc.close()
         allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
                        "rt": rt, "cs": stats, "stress": stress, "remote": remote, "rccl": cs_info.get("rccl", False),
@@ -470,7 +472,8 @@ def main():
                     "mb_per_s": round((sum(r["remote"]["wbytes"] + r["remote"]["rbytes"] for r in allr) / (1 << 20))
                                       / max(r["remote"]["wt"] + r["remote"]["rt"] for r in allr), 2),
                     "write_p50_ms": round(pct(rwl, 50), 3), "write_p99_ms": round(pct(rwl, 99), 3),
-                    "read_p50_ms": round(pct(rrl, 50), 3), "read_p99_ms": round(pct(rrl, 99), 3)}
+                    "read_p50_ms": round(pct(rrl, 50), 3), "read_p99_ms": round(pct(rrl, 99), 3),
+                    "client_phase_p50_ms_rank0": allr[0]["remote"].get("phases", {})}
             if a.stress_seconds > 0:
                 slat = sorted(x for r in allr for x in r["stress"]["lat"])
                 ops = sum(r["stress"]["ops"] for r in allr) / max(r["stress"]["seconds"] for r in allr)
