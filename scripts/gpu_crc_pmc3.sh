@@ -31,3 +31,5 @@ for d in sorted(glob.glob("gpurun_out/r3_pmc/p*_*")):
     for (k, c), v in sorted(agg.items()):
         print(f"  {k:40s} {c:28s} mean/dispatch {sum(v)/len(v):14.0f}  (n={len(v)})")
 PY
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --remote-steps 10 > $out/bench_remote.json 2> $out/bench_remote.err || exit $?
+python -c "import json; d=json.load(open('$out/bench_remote.json')); print(d['client_phase_p50_ms_rank0']); print(d['remote_client'])"
