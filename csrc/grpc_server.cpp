@@ -8,10 +8,12 @@
 #include <poll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <cerrno>
 #include <chrono>
+#include <algorithm>
 #include <cstring>
 #include <map>
 
@@ -21,6 +23,28 @@
 namespace dfs {
 
 namespace {
+
+bool writev_full(int fd, iovec* iv, int k) {
+  while (k > 0) {
+    msghdr mh{};
+    mh.msg_iov = iv;
+    mh.msg_iovlen = static_cast<size_t>(k);
+    ssize_t r = ::sendmsg(fd, &mh, MSG_NOSIGNAL);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    size_t done = static_cast<size_t>(r);
+    while (k > 0 && done >= iv[0].iov_len) {
+      done -= iv[0].iov_len;
+      ++iv;
+      --k;
+    }
+    if (k > 0) {
+      iv[0].iov_base = static_cast<uint8_t*>(iv[0].iov_base) + done;
+      iv[0].iov_len -= done;
+    }
+  }
+  return true;
+}
 
 bool write_full(int fd, const uint8_t* p, size_t n) {
   while (n > 0) {
@@ -78,7 +102,8 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     std::shared_ptr<const void> keep;  // owner of body_p when the reply is external
     const uint8_t* body_p = nullptr;
     size_t body_n = 0;
-    size_t off = 0;  // bytes of prefix + body already handed to nghttp2
+    size_t off = 0;       // bytes of prefix + body written to the socket
+    size_t read_off = 0;  // bytes of prefix + body scheduled into DATA frames
     std::string status_str = "0";
     bool dispatched = false;
     bool too_big = false;   // over kMaxMessage (or the connection's budget): refused
@@ -88,6 +113,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
   static constexpr size_t kMaxConnBuffered = 1ull << 30;    // request bytes held per connection
   GrpcServer* srv = nullptr;
   int fd = -1;
+  TlsConn* tc = nullptr;  // TLS session on fd (owned by serve())
   int efd = -1;
   size_t buffered = 0;  // request bytes buffered across this connection's streams
   nghttp2_session* session = nullptr;
@@ -109,32 +135,74 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
     (void)!::write(efd, &one, sizeof one);
   }
 
-  static ssize_t read_body(nghttp2_session* s, int32_t sid, uint8_t* buf, size_t len, uint32_t* flags,
+  // Response bodies go out without a copy into nghttp2's buffer (NGHTTP2_DATA_FLAG_NO_COPY):
+  // read_body sizes each DATA frame (up to the peer's max frame size via read_length), and
+  // send_data writes header + prefix + body bytes straight from the reply buffer with one
+  // sendmsg — a 1 MiB ReadBlock is one frame, not 64 frames of 16 KiB each copied twice.
+  static ssize_t read_body(nghttp2_session* s, int32_t sid, uint8_t*, size_t len, uint32_t* flags,
                            nghttp2_data_source*, void* user) {
     auto* c = static_cast<Conn*>(user);
     auto it = c->streams.find(sid);
     if (it == c->streams.end()) return NGHTTP2_ERR_TEMPORAL_CALLBACK_FAILURE;
     Stream& st = it->second;
     const size_t total = 5 + st.body_n;
-    size_t n = 0;
-    if (st.off < 5) {
-      n = std::min(len, 5 - st.off);
-      std::memcpy(buf, st.prefix + st.off, n);
-      st.off += n;
-    }
-    if (n < len && st.off >= 5) {
-      size_t m = std::min(len - n, total - st.off);
-      std::memcpy(buf + n, st.body_p + (st.off - 5), m);
-      st.off += m;
-      n += m;
-    }
-    if (st.off == total) {
+    const size_t n = std::min(len, total - st.read_off);
+    st.read_off += n;
+    *flags |= NGHTTP2_DATA_FLAG_NO_COPY;
+    if (st.read_off == total) {
       *flags |= NGHTTP2_DATA_FLAG_EOF | NGHTTP2_DATA_FLAG_NO_END_STREAM;
       static const std::string k_status = "grpc-status";
       nghttp2_nv tr[] = {nv(k_status, st.status_str)};
       if (nghttp2_submit_trailer(s, sid, tr, 1) != 0) return NGHTTP2_ERR_CALLBACK_FAILURE;
     }
     return static_cast<ssize_t>(n);
+  }
+
+  static ssize_t read_length(nghttp2_session*, uint8_t, int32_t, int32_t session_window, int32_t stream_window,
+                             uint32_t remote_max_frame, void*) {
+    int64_t n = std::min<int64_t>({session_window, stream_window, static_cast<int64_t>(remote_max_frame)});
+    return static_cast<ssize_t>(std::max<int64_t>(n, 1));
+  }
+
+  bool write_vec(iovec* iv, int k) {
+    if (tc) {
+      const auto far = std::chrono::steady_clock::now() + std::chrono::hours(24);
+      for (int i = 0; i < k; ++i)
+        if (iv[i].iov_len && !tc->write_all(static_cast<const uint8_t*>(iv[i].iov_base), iv[i].iov_len, far))
+          return false;
+      return true;
+    }
+    return writev_full(fd, iv, k);
+  }
+
+  static ssize_t on_send(nghttp2_session*, const uint8_t* data, size_t len, int, void* user) {
+    iovec iv{const_cast<uint8_t*>(data), len};
+    return static_cast<Conn*>(user)->write_vec(&iv, 1) ? static_cast<ssize_t>(len) : NGHTTP2_ERR_CALLBACK_FAILURE;
+  }
+
+  static int send_data(nghttp2_session*, nghttp2_frame* f, const uint8_t* framehd, size_t length,
+                       nghttp2_data_source*, void* user) {
+    auto* c = static_cast<Conn*>(user);
+    auto it = c->streams.find(f->hd.stream_id);
+    if (it == c->streams.end() || f->data.padlen > 0) return NGHTTP2_ERR_CALLBACK_FAILURE;
+    Stream& st = it->second;
+    iovec iv[3];
+    int k = 0;
+    iv[k++] = {const_cast<uint8_t*>(framehd), 9};
+    size_t off = st.off, rem = length;
+    if (off < 5 && rem) {
+      const size_t m = std::min(rem, 5 - off);
+      iv[k++] = {st.prefix + off, m};
+      off += m;
+      rem -= m;
+    }
+    if (rem) {
+      iv[k++] = {const_cast<uint8_t*>(st.body_p) + (off - 5), rem};
+      off += rem;
+    }
+    if (!c->write_vec(iv, k)) return NGHTTP2_ERR_CALLBACK_FAILURE;
+    st.off = off;
+    return 0;
   }
 
   void respond(int32_t sid, GrpcReply& r) {
@@ -157,6 +225,7 @@ struct GrpcServer::Conn : std::enable_shared_from_this<Conn> {
       uint32_t n = htonl(static_cast<uint32_t>(st.body_n));
       std::memcpy(st.prefix + 1, &n, 4);
       st.off = 0;
+      st.read_off = 0;
       nghttp2_nv h[] = {nv(k_status, v200), nv(k_ct, v_ct)};
       nghttp2_data_provider dp;
       dp.source.ptr = nullptr;
@@ -424,6 +493,9 @@ void GrpcServer::serve(int fd) {
   nghttp2_session_callbacks_set_on_data_chunk_recv_callback(cbs, &Conn::on_data);
   nghttp2_session_callbacks_set_on_frame_recv_callback(cbs, &Conn::on_frame);
   nghttp2_session_callbacks_set_on_stream_close_callback(cbs, &Conn::on_close);
+  nghttp2_session_callbacks_set_send_callback(cbs, &Conn::on_send);
+  nghttp2_session_callbacks_set_send_data_callback(cbs, &Conn::send_data);
+  nghttp2_session_callbacks_set_data_source_read_length_callback(cbs, &Conn::read_length);
   nghttp2_option* opt;
   nghttp2_option_new(&opt);
   nghttp2_option_set_no_http_messaging(opt, 0);
@@ -437,16 +509,9 @@ void GrpcServer::serve(int fd) {
   nghttp2_session_set_local_window_size(c->session, NGHTTP2_FLAG_NONE, 0, 1 << 30);
   std::vector<uint8_t> buf(1 << 20);
   bool ok = true;
-  auto flush = [&] {
-    for (;;) {
-      const uint8_t* data = nullptr;
-      ssize_t n = nghttp2_session_mem_send(c->session, &data);
-      if (n < 0) return false;
-      if (n == 0) return true;
-      if (tc ? !tc->write_all(data, static_cast<size_t>(n), far()) : !write_full(fd, data, static_cast<size_t>(n)))
-        return false;
-    }
-  };
+  c->tc = tc.get();
+  // frames go out through on_send / send_data, in order, straight to the socket
+  auto flush = [&] { return nghttp2_session_send(c->session) == 0; };
   ok = flush();
   while (ok && !stop_.load() && (nghttp2_session_want_read(c->session) || nghttp2_session_want_write(c->session))) {
     pollfd p[2] = {{fd, POLLIN, 0}, {c->efd, POLLIN, 0}};
@@ -470,6 +535,7 @@ void GrpcServer::serve(int fd) {
     }
     ok = flush();
   }
+  c->tc = nullptr;
   tc.reset();  // close_notify before the socket goes
   std::lock_guard<std::mutex> g(mu_);
   for (auto it = conns_.begin(); it != conns_.end(); ++it)
