@@ -810,6 +810,7 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("arena_path", &FastClient::arena_path)
       .def_property_readonly("writes", &FastClient::writes)
       .def_property_readonly("reads", &FastClient::reads)
+      .def("set_host_aliases", &FastClient::set_host_aliases)
       .def("set_routing", &FastClient::set_routing, py::call_guard<py::gil_scoped_release>())
       .def("write", [](FastClient& c, const std::string& path, py::buffer data, const std::string& rid,
                          const std::map<std::string, std::string>& attrs) {
@@ -899,6 +900,7 @@ void bind_meta(py::module_& m) {
         return py::make_tuple(static_cast<int>(st), msg);
       }, py::arg("path"), py::arg("data"), py::arg("k"), py::arg("m"), py::arg("request_id") = "")
       .def("set_hedge_delay", &RemoteClient::set_hedge_delay)
+      .def("set_host_aliases", &RemoteClient::set_host_aliases)
       .def("set_routing", &RemoteClient::set_routing, py::call_guard<py::gil_scoped_release>())
       .def("write", [](RemoteClient& c, const std::string& path, py::buffer data, const std::string& rid,
                          const std::map<std::string, std::string>& attrs) {

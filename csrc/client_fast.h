@@ -57,6 +57,8 @@ inline std::string encode_with_payload(const pb::WriteBlockRequest& w, const uin
 
 class FastClient {
  public:
+  // Host aliases for the gRPC hops to other hosts (EC shards): see GrpcChannelPool.
+  void set_host_aliases(std::vector<std::pair<std::string, std::string>> a) { grpc_.set_host_aliases(std::move(a)); }
   enum Status { Ok = 0, NotHandled = 1, Failed = 2 };
   struct Times {  // seconds, per phase (benchmark breakdown)
     double crc = 0, create = 0, write = 0, md5_wait = 0, complete = 0, getinfo = 0, read = 0;

@@ -61,6 +61,7 @@ class RemoteClient {
   uint64_t ec_degraded_reads() const { return ec_degraded_.load(); }
   // Hedged reads (Client::with_hedge_delay): 0 = off.
   void set_hedge_delay(int ms) { hedge_ms_.store(ms); }
+  void set_host_aliases(std::vector<std::pair<std::string, std::string>> a) { pool_.set_host_aliases(std::move(a)); }
   uint64_t hedged() const { return hedged_.load(); }
 
  private:

@@ -368,8 +368,23 @@ void GrpcChannelPool::give(const std::string& target, std::unique_ptr<Conn> c) {
   idle_[target].push_back(std::move(c));
 }
 
-GrpcResult GrpcChannelPool::call(const std::string& target, const std::string& path, const std::string& request,
+void GrpcChannelPool::set_host_aliases(std::vector<std::pair<std::string, std::string>> aliases) {
+  std::lock_guard<std::mutex> g(mu_);
+  aliases_ = std::move(aliases);
+}
+
+std::string GrpcChannelPool::resolve(const std::string& target) const {
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& a : aliases_) {
+    auto p = target.find(a.first);
+    if (!a.first.empty() && p != std::string::npos) return target.substr(0, p) + a.second + target.substr(p + a.first.size());
+  }
+  return target;
+}
+
+GrpcResult GrpcChannelPool::call(const std::string& target_in, const std::string& path, const std::string& request,
                                  const std::string& request_id, int timeout_ms) {
+  const std::string target = resolve(target_in);
   GrpcResult res;
   if (timeout_ms < 0) timeout_ms = timeout_ms_;
   std::string err;

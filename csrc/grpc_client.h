@@ -36,8 +36,12 @@ class GrpcChannelPool {
   GrpcResult call(const std::string& target, const std::string& path, const std::string& request,
                   const std::string& request_id, int timeout_ms = -1);
   uint64_t connects() const;
+  // Host aliases (the client library's add_host_alias): a target containing `alias` is
+  // dialled at `real` instead (first match, as client.py resolve_url).
+  void set_host_aliases(std::vector<std::pair<std::string, std::string>> aliases);
 
  private:
+  std::string resolve(const std::string& target) const;
   struct Conn;
   std::unique_ptr<Conn> take(const std::string& target, int timeout_ms, std::string* err);
   void give(const std::string& target, std::unique_ptr<Conn> c);
@@ -46,6 +50,7 @@ class GrpcChannelPool {
   std::shared_ptr<TlsContext> tls_;
   mutable std::mutex mu_;
   std::map<std::string, std::vector<std::unique_ptr<Conn>>> idle_;
+  std::vector<std::pair<std::string, std::string>> aliases_;  // mu_
   uint64_t connects_ = 0;
 };
 

@@ -200,8 +200,11 @@ class Client:
 
     def add_host_alias(self, alias: str, real: str) -> None:
         self.host_aliases[alias] = real
-        self._fast = self._remote = None  # aliases rewrite addresses: keep every call on the Python path
-        self._fallback("host_alias_disabled_native")
+        # the native clients dial through the same alias table (first match, like resolve_url)
+        for nc in (self._fast, self._remote):
+            if nc is not None:
+                nc.set_host_aliases(list(self.host_aliases.items()))
+        self._sync_fast()
 
     def resolve_url(self, url: str) -> str:
         for alias, real in self.host_aliases.items():

@@ -690,3 +690,20 @@ def test_native_hedged_read_races_a_stalled_replica():
         assert c._remote.hedged == 1 and c.remote_ops == ops0 + 1
         assert c.native_fallbacks == fb0  # served natively, no Python fallback
         c.close()
+
+
+def test_host_aliases_keep_the_native_clients(cluster3):
+    """`add_host_alias` (dfs_cli --host-alias) used to switch both native clients off; the
+    alias table now reaches their gRPC pools, so a remote client with an alias still writes and
+    reads natively (every address is dialled through the alias, first match)."""
+    import socket as _s
+
+    rc = cluster3.client(local_chunkserver=None, local_rpc=False)
+    rc.add_host_alias("127.0.0.1", "localhost")  # every master / chunkserver address goes through it
+    assert _s.gethostbyname("localhost") == "127.0.0.1"
+    n0 = rc.remote_ops
+    data = os.urandom(200_000)
+    rc.create_file_from_buffer(data, "/alias/f")
+    assert rc.get_file_content("/alias/f") == data
+    assert rc.remote_ops - n0 >= 2 and "host_alias_disabled_native" not in rc.native_fallbacks
+    rc.close()
