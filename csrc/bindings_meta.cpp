@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <optional>
 #include <set>
 #include <thread>
 
@@ -625,6 +626,31 @@ void bind_meta(py::module_& m) {
         for (auto& a : acts)
           out.append(py::make_tuple(a.reconstruct, a.queue_on, a.block_id, a.target, a.shard_index, a.ec_data,
                                     a.ec_parity, a.sources, a.original_size));
+        return out;
+      })
+      .def("pick_block", [](const MasterCore& c, const std::string& src, const std::string& dst,
+                            std::optional<std::string> prefix) {
+        py::gil_scoped_release r;
+        return c.pick_block(src, dst, prefix ? &*prefix : nullptr);
+      }, py::arg("src"), py::arg("dst"), py::arg("prefix") = py::none())
+      .def("tiering_scan", [](const MasterCore& c, uint64_t now_ms, uint64_t cold_ms) {
+        std::vector<MasterCore::ColdFile> v;
+        {
+          py::gil_scoped_release r;
+          v = c.tiering_scan(now_ms, cold_ms);
+        }
+        py::list out;
+        for (auto& f : v) out.append(py::make_tuple(f.path, f.blocks));
+        return out;
+      })
+      .def("ec_candidates", [](const MasterCore& c, uint64_t now_ms, uint64_t ec_ms) {
+        std::vector<std::string> v;
+        {
+          py::gil_scoped_release r;
+          v = c.ec_candidates(now_ms, ec_ms);
+        }
+        py::list out;
+        for (auto& s : v) out.append(py::bytes(s));
         return out;
       })
       .def("snapshot", &MasterCore::snapshot, py::call_guard<py::gil_scoped_release>())

@@ -866,6 +866,49 @@ std::vector<MasterCore::HealAction> MasterCore::heal_scan(
   return out;
 }
 
+std::string MasterCore::pick_block(const std::string& src, const std::string& dst, const std::string* prefix) const {
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& kv : files_) {
+    if (prefix && kv.first.compare(0, prefix->size(), *prefix) != 0) continue;
+    for (const pb::BlockInfo& b : kv.second.blocks) {
+      if (b.ec_data_shards != 0) continue;
+      const auto& l = b.locations;
+      if (std::find(l.begin(), l.end(), src) != l.end() && std::find(l.begin(), l.end(), dst) == l.end())
+        return b.block_id;
+    }
+  }
+  return std::string();
+}
+
+std::vector<MasterCore::ColdFile> MasterCore::tiering_scan(uint64_t now_ms, uint64_t cold_ms) const {
+  std::vector<ColdFile> out;
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& kv : files_) {
+    const pb::FileMetadata& f = kv.second;
+    if (f.moved_to_cold_at_ms != 0 || f.ec_data_shards != 0 || f.last_access_ms == 0 ||
+        now_ms <= f.last_access_ms || now_ms - f.last_access_ms <= cold_ms)
+      continue;
+    ColdFile c;
+    c.path = f.path;
+    for (const pb::BlockInfo& b : f.blocks) c.blocks.emplace_back(b.block_id, b.locations);
+    out.push_back(std::move(c));
+  }
+  return out;
+}
+
+std::vector<std::string> MasterCore::ec_candidates(uint64_t now_ms, uint64_t ec_ms) const {
+  std::vector<std::string> out;
+  std::lock_guard<std::mutex> g(mu_);
+  for (const auto& kv : files_) {
+    const pb::FileMetadata& f = kv.second;
+    if (f.moved_to_cold_at_ms == 0 || f.ec_data_shards != 0 || f.blocks.empty() || now_ms <= f.moved_to_cold_at_ms ||
+        now_ms - f.moved_to_cold_at_ms <= ec_ms)
+      continue;
+    out.push_back(f.str());
+  }
+  return out;
+}
+
 std::vector<std::pair<std::string, std::vector<std::string>>> MasterCore::take_gc() {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<std::pair<std::string, std::vector<std::string>>> out;

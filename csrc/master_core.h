@@ -127,6 +127,20 @@ class MasterCore : public raft::StateMachine {
                                     const std::map<std::string, std::vector<std::string>>& bad,
                                     const std::set<std::pair<std::string, std::string>>& queued) const;
 
+  // Balancer / shuffler pick (reference master.rs:1033-1120): a replicated block held by `src`
+  // and not by `dst`, under `prefix` when given; "" if none. One pass under the lock.
+  std::string pick_block(const std::string& src, const std::string& dst, const std::string* prefix) const;
+  // Tiering scan (C32, reference master.rs:1990-2060): files idle for longer than cold_ms that
+  // are neither cold nor EC yet, with each block's holders (MOVE_TO_COLD targets).
+  struct ColdFile {
+    std::string path;
+    std::vector<std::pair<std::string, std::vector<std::string>>> blocks;  // block id, locations
+  };
+  std::vector<ColdFile> tiering_scan(uint64_t now_ms, uint64_t cold_ms) const;
+  // EC conversion candidates: cold, replicated, non-empty files cold for longer than ec_ms
+  // (encoded FileMetadata, only those — the caller decodes a handful, not the namespace).
+  std::vector<std::string> ec_candidates(uint64_t now_ms, uint64_t ec_ms) const;
+
   // Raft peer RPC (vote / append / snapshot / timeout_now, JSON) for the attached node, as
   // served by the native gRPC server on /dfs.RaftPeer/<kind>.
   int raft_rpc(const std::string& kind, const std::string& body, std::string* out);

@@ -137,13 +137,8 @@ class MasterBackground:
 
     # ---------------------------------------------------------------- balancer / shuffler
     def _pick_block(self, src: str, dst: str, prefix: str | None = None) -> str | None:
-        for f in self.state.files.values():
-            if prefix is not None and not f.path.startswith(prefix):
-                continue
-            for b in f.blocks:
-                if b.ec_data_shards == 0 and src in b.locations and dst not in b.locations:
-                    return b.block_id
-        return None
+        # one native pass under the state lock (no per-file decode in Python)
+        return self.state.core.pick_block(src, dst, prefix) or None
 
     async def balance(self) -> None:
         servers = sorted(self.state.chunk_servers.items(), key=lambda kv: kv[1].available_space)
@@ -381,14 +376,12 @@ class MasterBackground:
             return
         now = now_ms()
         T = pb.ChunkServerCommand
-        for f in list(self.state.files.values()):
-            if (f.moved_to_cold_at_ms == 0 and f.ec_data_shards == 0 and f.last_access_ms > 0
-                    and now - f.last_access_ms > self.cold_threshold_ms):
-                for b in f.blocks:
-                    for loc in b.locations:
-                        self.state.pending_commands.setdefault(loc, []).append(
-                            T(type=T.MOVE_TO_COLD, block_id=b.block_id))
-                await self._propose("MoveToCold", {"path": f.path, "moved_at_ms": now})
+        # the namespace scan is native (MasterCore::tiering_scan): only idle files come back
+        for path, blocks in self.state.core.tiering_scan(now, self.cold_threshold_ms):
+            for bid, locs in blocks:
+                for loc in locs:
+                    self.state.pending_commands.setdefault(loc, []).append(T(type=T.MOVE_TO_COLD, block_id=bid))
+            await self._propose("MoveToCold", {"path": path, "moved_at_ms": now})
         if not self.ec_conversion:
             return
         await self._ec_convert(now)
@@ -407,10 +400,8 @@ class MasterBackground:
                 log.warning("EC job for %s timed out; will retry", bid)
                 jobs.pop(bid, None)
         live = {a for a, s in self.state.chunk_servers.items() if s.available_space > 0}
-        for f in list(self.state.files.values()):
-            if not (f.moved_to_cold_at_ms > 0 and f.ec_data_shards == 0 and f.blocks
-                    and now - f.moved_to_cold_at_ms > self.ec_threshold_ms):
-                continue
+        for raw in self.state.core.ec_candidates(now, self.ec_threshold_ms):
+            f = pb.FileMetadata.FromString(raw)
             if all(b.block_id in jobs and jobs[b.block_id]["done"] for b in f.blocks):
                 new_blocks = []
                 for b in f.blocks:

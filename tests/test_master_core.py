@@ -276,6 +276,50 @@ def test_tiering_access_stats_and_ec_conversion_commands():
     assert st.files["/f"].blocks[0].locations[3] == "new:1"
 
 
+def test_native_background_scans_match_a_python_model():
+    """Balancer/shuffler pick, tiering scan and EC-conversion candidates run natively over the
+    namespace (master/background.py calls them every few seconds); checked against a plain
+    Python filter over the decoded files."""
+    import random
+
+    rnd = random.Random(7)
+    st = MasterState()
+    servers = [f"h{i}:1" for i in range(5)]
+    files = []
+    for i in range(300):
+        ec = (2, 1) if i % 17 == 0 else (0, 0)
+        locs = servers[:3] if ec[0] else rnd.sample(servers, rnd.randint(1, 3))
+        f = file_with(f"/{'ab'[i % 2]}/{i:04d}", f"blk{i}", locs, ec)
+        files.append(f)
+    ingest(st, *files)
+    now = 1_000_000
+    for i, f in enumerate(files):
+        if i % 3 == 0:
+            st.apply({"Master": {"UpdateAccessStats": {"path": f.path, "accessed_at_ms": now - 100 * i}}})
+        if i % 5 == 0 and f.ec_data_shards == 0:
+            st.apply({"Master": {"MoveToCold": {"path": f.path, "moved_at_ms": now - 200 * i}}})
+    decoded = st.files.values()
+    for src in servers:
+        for dst in servers:
+            for prefix in (None, "/a/", "/b/1", "/zz"):
+                want = {b.block_id for f in decoded if prefix is None or f.path.startswith(prefix) for b in f.blocks
+                        if b.ec_data_shards == 0 and src in b.locations and dst not in b.locations}
+                got = st.core.pick_block(src, dst, prefix)
+                assert (got in want) if want else got == ""
+    cold_ms, ec_ms = 5_000, 10_000
+    want_cold = sorted(f.path for f in decoded if f.moved_to_cold_at_ms == 0 and f.ec_data_shards == 0
+                       and f.last_access_ms > 0 and now - f.last_access_ms > cold_ms)
+    got_cold = st.core.tiering_scan(now, cold_ms)
+    assert sorted(p for p, _ in got_cold) == want_cold and want_cold
+    by_path = {f.path: f for f in decoded}
+    for p, blocks in got_cold:
+        assert blocks == [(b.block_id, list(b.locations)) for b in by_path[p].blocks]
+    want_ec = sorted(f.path for f in decoded if f.moved_to_cold_at_ms > 0 and f.ec_data_shards == 0 and f.blocks
+                     and now - f.moved_to_cold_at_ms > ec_ms)
+    got_ec = sorted(pb.FileMetadata.FromString(r).path for r in st.core.ec_candidates(now, ec_ms))
+    assert got_ec == want_ec and want_ec
+
+
 def test_split_shard_drops_moved_files_and_snapshot_roundtrip():
     st = MasterState()
     ingest(st, file_with("/a/1", "x1", ["h:1"]), file_with("/m/2", "x2", ["h:1"]), file_with("/z/3", "x3", ["h:1"]))
