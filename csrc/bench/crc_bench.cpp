@@ -82,12 +82,14 @@ int main(int argc, char** argv) {
   int iters = 50;
   uint64_t total_mib = 1024;
   bool sweep = false;
+  bool wide_ab = false;  // --wide-ab: K1/K2 on the matrix cores, 3 x 4-wave vs 1 x 12-wave workgroups per CU
   uint64_t single_mib = 0;  // --single MIB: only the production K1/K2 dispatch at that size (PMC runs)
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "--iters" && i + 1 < argc) iters = std::atoi(argv[++i]);
     else if (a == "--mib" && i + 1 < argc) total_mib = std::strtoull(argv[++i], nullptr, 10);
     else if (a == "--sweep") sweep = true;
+    else if (a == "--wide-ab") wide_ab = true;
     else if (a == "--single" && i + 1 < argc) single_mib = std::strtoull(argv[++i], nullptr, 10);
   }
   CK(hipSetDevice(0));
@@ -133,6 +135,27 @@ int main(int argc, char** argv) {
     std::printf("{\"bytes\": %llu, \"us\": %.2f, \"GBps\": %.1f, \"ok\": %s}\n", static_cast<unsigned long long>(n), r.us,
                 n / r.us / 1e3, r.ok ? "true" : "false");
     return r.ok ? 0 : 1;
+  }
+  if (wide_ab) {
+    std::printf("{\"stream_read_GBps\": %.1f, \"k1k2\": [", stream_gbps);
+    set_crc_mfma(true);
+    set_crc_lds_max_mib(0);
+    bool f = true;
+    for (uint64_t mib : std::vector<uint64_t>{1, 8, 16, 32, 64, 128, 256, 1024}) {
+      const uint64_t n = mib << 20;
+      if (n > total) continue;
+      for (int rep = 0; rep < 2; ++rep)
+        for (int w : {0, 1}) {
+          set_crc_wide(w);
+          Run r = bench_block(d, n, t, dmeta, dpart, s, n >= (256ull << 20) ? std::max(3, iters / 10) : iters, host);
+          std::printf("%s\n  {\"bytes\": %llu, \"wide\": %d, \"rep\": %d, \"us\": %.2f, \"GBps\": %.1f, \"of_stream\": %.3f, "
+                      "\"ok\": %s}", f ? "" : ",", static_cast<unsigned long long>(n), w, rep, r.us, n / r.us / 1e3,
+                      n / r.us / 1e3 / stream_gbps, r.ok ? "true" : "false");
+          f = false;
+        }
+    }
+    std::printf("\n]}\n");
+    return 0;
   }
   if (sweep) {
     // where the 64 MiB K1/K2 time goes: per-workgroup fixed cost (grid) vs load latency (ring)

@@ -139,6 +139,8 @@ PYBIND11_MODULE(_dfs_native, m) {
   // checksum-kernel selection (tests / A-B runs): (mfma, scrub ring buffers, K1/K2/K3 ring buffers)
   m.def("crc_kernels", [] { return py::make_tuple(crc_mfma_enabled(), crc_ring_buffers(), crc_tile_ring_buffers()); });
   m.def("set_crc_lds_max_mib", &set_crc_lds_max_mib, "K1/K2 size-based dispatch threshold (0 = matrix cores only)");
+  m.def("crc_wide_mode", &crc_wide_mode);
+  m.def("set_crc_wide", &set_crc_wide, "K1/K2 one workgroup per CU: 0 off, 1 shared LDS image, 2 + LDS basis");
   m.def("set_crc_kernels", [](bool mfma, int scrub_ring, int tile_ring) {
     set_crc_mfma(mfma);
     set_crc_ring(scrub_ring, tile_ring);

@@ -19,6 +19,8 @@ constexpr int kMaxGridCrc = 768;  // 3 resident workgroups x 256 CUs (see crc_ti
 constexpr int kMaxShards = 32;
 constexpr int kCrcBasisBytes = 16 * 64 * 16;  // MFMA basis (A fragments), stored after DevCrcTables
 constexpr int kCrcChunkShiftBytes = 7 * 4 * 256 * 4;  // chunk -> slice shift tables, stored after the basis
+// behind those: slice -> 4 KiB sub-tile shift tables (7) and the 16 KiB tile shift (wide kernel)
+constexpr int kCrcWideExtraBytes = 8 * 4 * 256 * 4;
 
 struct DevCrcTables {
   uint32_t slice16[16][256];
@@ -101,6 +103,12 @@ int crc_ring_buffers();       // K1b scrub
 int crc_tile_ring_buffers();  // K1/K2/K3
 void set_crc_ring(int scrub_buffers, int tile_buffers);
 constexpr uint64_t kCrcRingMinTiles = 2048;
+// K1/K2 on matrix cores with one 12-wave workgroup per CU (shared LDS image + MFMA basis, and
+// a two-lookup combine per tile) from kCrcWideMinTiles tiles up; 0 = three 4-wave workgroups
+// per CU everywhere. DFS_CRC_WIDE overrides, set_crc_wide is the benches' A/B switch.
+constexpr int kCrcWideDefault = 1;
+int crc_wide_mode();
+void set_crc_wide(int mode);
 
 // Benches: streaming read of n bytes (n % 16 == 0) on kStreamReadGrid x 256 threads; `out`
 // holds 4 x kStreamReadGrid words.

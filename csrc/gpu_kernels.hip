@@ -39,25 +39,68 @@ __device__ __forceinline__ uint32_t chunk16(const uint32_t (*T)[256], uint32_t c
          T[3][w.w & 0xff] ^ T[2][(w.w >> 8) & 0xff] ^ T[1][(w.w >> 16) & 0xff] ^ T[0][w.w >> 24];
 }
 
+// Value of lane `lane ^ m` without LDS traffic: DPP for m <= 8 (xor 4 = half-row mirror of
+// the xor-3 quad permutation; xor 8 = rotate the 16-lane row by 8, either direction), the
+// CDNA4 permlane swaps for 16 and 32 (swapping v with itself leaves the even half-rows /
+// half-waves in r[0] and the odd ones in r[1]).
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t x) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), kCtrl, 0xF, 0xF, false));
+}
+
+template <int m>
+__device__ __forceinline__ uint32_t xchg(uint32_t v, int lane) {
+  if constexpr (m == 1) return dpp_mov<0xB1>(v);  // quad_perm [1,0,3,2]
+  else if constexpr (m == 2) return dpp_mov<0x4E>(v);  // quad_perm [2,3,0,1]
+  else if constexpr (m == 4) return dpp_mov<0x141>(dpp_mov<0x1B>(v));  // quad_perm [3,2,1,0], then half-row mirror
+  else if constexpr (m == 8) return dpp_mov<0x128>(v);  // row_ror:8
+  else if constexpr (m == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  } else {
+    static_assert(m == 32, "xchg: 1, 2, 4, 8, 16 or 32");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane & 32) ? r[0] : r[1];
+  }
+}
+
 // Butterfly step: lanes with (lane & m) == 0 hold the earlier bytes.
-__device__ __forceinline__ uint32_t combine(uint32_t r, int m, int lane, const uint32_t (*t)[256]) {
-  uint32_t p = __shfl_xor(r, m);
+template <int m>
+__device__ __forceinline__ uint32_t combine(uint32_t r, int lane, const uint32_t (*t)[256]) {
+  uint32_t p = xchg<m>(r, lane);
   bool right = lane & m;
   uint32_t left = right ? p : r;
   uint32_t rgt = right ? r : p;
   return tab4(t, left) ^ rgt;
 }
 
+// XOR all-reduce steps inside the wave without LDS traffic (ds_bpermute plus its address
+// arithmetic is what __shfl_xor compiles to). Applied smallest group first: xr4 / xr8 pair
+// lanes by mirroring a half-row / row (DPP), which equals the xor-4 / xor-8 partner's value
+// once the quads / 8-lane groups are already uniform; xr16 / xr32 use the CDNA4 permlane
+// swaps (a swap of v with itself leaves the two halves' values in the two results).
+template <int kCtrl>
+__device__ __forceinline__ uint32_t xr_dpp(uint32_t v) {
+  return v ^ static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), kCtrl, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint32_t xr1(uint32_t v) { return xr_dpp<0xB1>(v); }   // quad_perm [1,0,3,2]
+__device__ __forceinline__ uint32_t xr2(uint32_t v) { return xr_dpp<0x4E>(v); }   // quad_perm [2,3,0,1]
+__device__ __forceinline__ uint32_t xr4(uint32_t v) { return xr_dpp<0x141>(v); }  // row_half_mirror
+__device__ __forceinline__ uint32_t xr8(uint32_t v) { return xr_dpp<0x140>(v); }  // row_mirror
+__device__ __forceinline__ uint32_t xr16(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return r[0] ^ r[1];
+}
+__device__ __forceinline__ uint32_t xr32(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return r[0] ^ r[1];
+}
+
 // Lane-parallel GF(2) matrix apply: v uniform across the wave, lanes 0..31 own columns.
 __device__ __forceinline__ uint32_t mat_apply(const uint32_t* col, uint32_t v, int lane) {
   int i = lane & 31;
   uint32_t x = ((v >> i) & 1u) ? col[i] : 0u;
-  x ^= __shfl_xor(x, 16);
-  x ^= __shfl_xor(x, 8);
-  x ^= __shfl_xor(x, 4);
-  x ^= __shfl_xor(x, 2);
-  x ^= __shfl_xor(x, 1);
-  return x;
+  return xr16(xr8(xr4(xr2(xr1(x)))));
 }
 
 __device__ __forceinline__ void load_tables(const DevCrcTables* __restrict__ gt, DevCrcTables* lt) {
@@ -80,9 +123,9 @@ __device__ __forceinline__ uint32_t slice_crc(const DevCrcTables& lt, const uint
     r = chunk16(lt.slice16, r, c2);
     r = chunk16(lt.slice16, r, c3);
   }
-  r = combine(r, 1, lane, lt.sh64);
-  r = combine(r, 2, lane, lt.sh128);
-  return combine(r, 4, lane, lt.sh256);
+  r = combine<1>(r, lane, lt.sh64);
+  r = combine<2>(r, lane, lt.sh128);
+  return combine<4>(r, lane, lt.sh256);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -162,6 +205,12 @@ __device__ __forceinline__ WaveData load_wave_ring(const uint8_t* __restrict__ d
 }
 
 // Raw CRC of the 64-byte chunk `lane` of the wave's 4 KiB (wave-wide: all 64 lanes together).
+// Every product in the accumulators is 0 or +-2^7, so an accumulator's low byte is 0x80 or 0
+// (its parity, nothing below): three byte permutes gather the low bytes of four accumulators
+// into one dword (acc[4k + q] -> byte k), four such dwords shifted by q land in distinct bits,
+// and the half-waves interleave by 4. The basis rows are laid out so that this gather IS the
+// CRC bit order (row R of the MFMA carries CRC bit R ^ 7, see upload_crc_tables): 17 VALU
+// per pass instead of one extract-and-insert pair per accumulator.
 __device__ __forceinline__ uint32_t wave_chunk_crcs(const i32x4 (&A)[16], const WaveData& d, int lane) {
   const int h = lane >> 5;
   uint32_t mine = 0;
@@ -183,8 +232,14 @@ __device__ __forceinline__ uint32_t wave_chunk_crcs(const i32x4 (&A)[16], const 
     }
     uint32_t part = 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) part |= ((static_cast<uint32_t>(acc[r]) >> 7) & 1u) << ((r & 3) + 8 * (r >> 2) + 4 * h);
-    part |= __shfl_xor(part, 32);
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t lo = __builtin_amdgcn_perm(static_cast<uint32_t>(acc[4 + q]), static_cast<uint32_t>(acc[q]), 0x0c0c0400u);
+      const uint32_t hi = __builtin_amdgcn_perm(static_cast<uint32_t>(acc[12 + q]), static_cast<uint32_t>(acc[8 + q]),
+                                                0x0c0c0400u);
+      part |= __builtin_amdgcn_perm(hi, lo, 0x05040100u) >> q;  // bit 7 + 8k - q: acc[4k + q]
+    }
+    part >>= 4 * h;
+    part = xr32(part);  // the half-waves' bits are disjoint: XOR = OR
     if (it == h) mine = part;  // lane L keeps chunk L: it comes out of pass L >> 5
   }
   return mine;
@@ -200,9 +255,7 @@ template <class L>
 __device__ __forceinline__ uint32_t slice_from_chunks(const L& lt, uint32_t r, int lane) {
   const int sl = lane & 7;
   uint32_t v = sl < 7 ? tab4(lt.cs[sl], r) : r;
-  v ^= __shfl_xor(v, 1);
-  v ^= __shfl_xor(v, 2);
-  return v ^ __shfl_xor(v, 4);
+  return xr4(xr2(xr1(v)));
 }
 
 // LDS images of the matrix-core kernels: only the GF(2) shift tables they look up (the
@@ -222,21 +275,22 @@ static_assert(sizeof(MfmaSliceLds) == kCrcChunkShiftBytes, "chunk-shift image");
 static_assert(sizeof(MfmaTileLds) - sizeof(MfmaSliceLds) == sizeof(DevCrcTables) - offsetof(DevCrcTables, sh512),
               "LDS image layout");
 
+template <int kThreads = kCrcWgThreads>
 __device__ __forceinline__ void copy16(const void* __restrict__ from, void* to, int bytes) {
   const uint4* src = reinterpret_cast<const uint4*>(from);
   uint4* dst = reinterpret_cast<uint4*>(to);
   const int n16 = bytes / 16;
 #pragma unroll 4
-  for (int i = threadIdx.x; i < n16; i += kCrcWgThreads) dst[i] = src[i];
+  for (int i = threadIdx.x; i < n16; i += kThreads) dst[i] = src[i];
 }
 
-template <class L>
+template <class L, int kThreads = kCrcWgThreads>
 __device__ __forceinline__ void load_lds_image(const DevCrcTables* __restrict__ gt, L* lt) {
   const uint8_t* cs = reinterpret_cast<const uint8_t*>(gt + 1) + kCrcBasisBytes;
-  copy16(cs, lt, kCrcChunkShiftBytes);
+  copy16<kThreads>(cs, lt, kCrcChunkShiftBytes);
   if constexpr (sizeof(L) > kCrcChunkShiftBytes)
-    copy16(&gt->sh512, reinterpret_cast<uint8_t*>(lt) + kCrcChunkShiftBytes,
-           static_cast<int>(sizeof(L)) - kCrcChunkShiftBytes);
+    copy16<kThreads>(&gt->sh512, reinterpret_cast<uint8_t*>(lt) + kCrcChunkShiftBytes,
+                     static_cast<int>(sizeof(L)) - kCrcChunkShiftBytes);
 }
 
 // The short tail slice (len < 512 bytes at `base`) as slice 0 of a wave's 4 KiB, front-padded
@@ -284,9 +338,9 @@ __device__ __forceinline__ uint32_t tail_crc(const DevCrcTables& lt, const uint8
     for (int q = 0; q < 4; ++q)
       r = chunk16(lt.slice16, r, make_uint4(words[4 * q], words[4 * q + 1], words[4 * q + 2], words[4 * q + 3]));
   }
-  r = combine(r, 1, lane, lt.sh64);
-  r = combine(r, 2, lane, lt.sh128);
-  return combine(r, 4, lane, lt.sh256);
+  r = combine<1>(r, lane, lt.sh64);
+  r = combine<2>(r, lane, lt.sh128);
+  return combine<4>(r, lane, lt.sh256);
 }
 
 // Contiguous, balanced tile runs: workgroup b owns [b*T/G, (b+1)*T/G), so every workgroup
@@ -324,9 +378,9 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
       if (a.meta_expect && a.meta_expect[i] != be) bad = min(bad, static_cast<uint32_t>(i));
     }
     if (a.part_crc) {
-      r = combine(r, 8, lane, lt.sh512);
-      r = combine(r, 16, lane, lt.sh1k);
-      r = combine(r, 32, lane, lt.sh2k);
+      r = combine<8>(r, lane, lt.sh512);
+      r = combine<16>(r, lane, lt.sh1k);
+      r = combine<32>(r, lane, lt.sh2k);
       if (lane == 0) wsum[wave] = r;
       __syncthreads();
       if (wave == 0) {
@@ -439,9 +493,9 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
       if (a.meta_expect && a.meta_expect[i] != be) bad = min(bad, static_cast<uint32_t>(i));
     }
     if (a.part_crc) {
-      r = combine(r, 8, lane, lt.sh512);
-      r = combine(r, 16, lane, lt.sh1k);
-      r = combine(r, 32, lane, lt.sh2k);  // wave-uniform: the 4 KiB sub-tile's raw CRC
+      r = combine<8>(r, lane, lt.sh512);
+      r = combine<16>(r, lane, lt.sh1k);
+      r = combine<32>(r, lane, lt.sh2k);  // wave-uniform: the 4 KiB sub-tile's raw CRC
       acc = mat_apply(lt.tile_pow2[0], acc, lane) ^ r;
     }
     if (t + 1 < t_end) cur = nxt;
@@ -470,6 +524,113 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
   if (threadIdx.x == 0) {
     if (a.part_crc) a.part_crc[blockIdx.x] = wacc[0] ^ wacc[1] ^ wacc[2] ^ wacc[3];
     if (a.part_bad) a.part_bad[blockIdx.x] = wg_bad;
+  }
+}
+
+// K1/K2 with one workgroup per CU: kGroups groups of 4 waves share one LDS image and one
+// LDS copy of the MFMA basis. Each group is a "virtual workgroup" of the kernel above (its own
+// balanced tile run, partial word and verdict: part_crc/part_bad are indexed by
+// blockIdx.x * kGroups + group, so the host sees the same `grid` words). The per-tile combine
+// is two dependent table rounds instead of five: every lane of a slice group moves its slice
+// CRC to the end of the wave's 4 KiB with one lookup in its own shift table (ss[sw], the
+// slice-level twin of slice_from_chunks) and three xor-shuffles fold the sub-tile; the Horner
+// step is one lookup in the 16 KiB shift table (all lanes the same value: an LDS broadcast)
+// instead of a lane-parallel matrix apply with five shuffles. The image (68 KiB) only fits
+// one workgroup per CU, which is what this kernel is.
+struct MfmaWideLds {
+  uint32_t cs[7][4][256];  // chunk -> slice (64 B * (7 - sl))
+  uint32_t ss[7][4][256];  // slice -> sub-tile (512 B * (7 - sw))
+  uint32_t sh16k[4][256];  // one tile
+  uint32_t sh4k[4][256];   // one sub-tile (epilogue)
+  uint32_t tile_pow2[32][32];
+};
+static_assert(offsetof(MfmaWideLds, sh4k) == kCrcChunkShiftBytes + kCrcWideExtraBytes, "wide image: contiguous head");
+static_assert(sizeof(MfmaWideLds) - offsetof(MfmaWideLds, sh4k) == sizeof(DevCrcTables) - offsetof(DevCrcTables, sh4k),
+              "wide image: DevCrcTables tail");
+
+template <int kGroups>
+__global__ __launch_bounds__(kCrcWgThreads * kGroups) __attribute__((amdgpu_waves_per_eu(3, 3)))
+void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
+  constexpr int kThreads = kCrcWgThreads * kGroups;
+  __shared__ MfmaWideLds lt;
+  __shared__ i32x4 lbasis[16 * 64];
+  __shared__ uint32_t wacc[4 * kGroups];
+  __shared__ uint32_t wg_bad[kGroups];
+  const int lane = threadIdx.x & 63, gw = threadIdx.x >> 6, wave = gw & 3, grp = gw >> 2, sw = lane >> 3,
+            sl = lane & 7;
+  const uint64_t vb = static_cast<uint64_t>(blockIdx.x) * kGroups + grp, vg = static_cast<uint64_t>(gridDim.x) * kGroups;
+  const uint64_t t_begin = vb * a.ntiles / vg, t_end = (vb + 1) * a.ntiles / vg;
+  const int64_t lo = static_cast<int64_t>(a.slice_lo), hi = static_cast<int64_t>(a.slice_hi);
+  auto first_slice = [&](uint64_t t) {
+    return lo + static_cast<int64_t>(t * kSlicesPerTile + wave * 8) - static_cast<int64_t>(a.vfront);
+  };
+  // unconditional loads (load_wave_ring: out-of-block slices re-read slice lo, and their chunk
+  // CRCs are zeroed below), so no exec-masked branches around the loads in the loop
+  WaveData cur;
+  if (t_begin < t_end) cur = load_wave_ring(a.data, first_slice(t_begin), lo, hi, lane);
+  const uint8_t* img = reinterpret_cast<const uint8_t*>(gt + 1);
+  copy16<kThreads>(img, lbasis, kCrcBasisBytes);
+  copy16<kThreads>(img + kCrcBasisBytes, &lt, kCrcChunkShiftBytes + kCrcWideExtraBytes);
+  copy16<kThreads>(&gt->sh4k, &lt.sh4k, static_cast<int>(sizeof(DevCrcTables) - offsetof(DevCrcTables, sh4k)));
+  if (threadIdx.x < kGroups) wg_bad[threadIdx.x] = 0xFFFFFFFFu;
+  __syncthreads();
+  i32x4 A[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) A[s] = lbasis[s * 64 + lane];
+
+  uint32_t acc = 0;
+  uint32_t bad = 0xFFFFFFFFu;
+  // tile t's combine (table lookups and shuffles: a latency chain) is issued after tile t+1's
+  // matrix-core work, so each wave has independent MFMAs to issue while its lookups are out
+  auto finish = [&](uint32_t c, uint64_t t) {
+    const int64_t i = first_slice(t) + sw;
+    const bool valid = i >= lo && i < hi;
+    uint32_t r = slice_from_chunks(lt, valid ? c : 0u, lane);
+    if (valid && sl == 0) {
+      uint32_t be = __builtin_bswap32(r ^ a.full_init);
+      if (a.meta_out) a.meta_out[i] = be;
+      if (a.meta_expect && a.meta_expect[i] != be) bad = min(bad, static_cast<uint32_t>(i));
+    }
+    if (a.part_crc) {
+      uint32_t v = sw < 7 ? tab4(lt.ss[sw], r) : r;
+      v = xr32(xr16(xr8(v)));  // wave-uniform: the 4 KiB sub-tile's raw CRC
+      acc = tab4(lt.sh16k, acc) ^ v;
+    }
+  };
+  uint32_t cprev = 0;
+  for (uint64_t t = t_begin; t < t_end; ++t) {
+    WaveData nxt;
+    if (t + 1 < t_end) nxt = load_wave_ring(a.data, first_slice(t + 1), lo, hi, lane);
+    const uint32_t c = wave_chunk_crcs(A, cur, lane);
+    if (t > t_begin) finish(cprev, t - 1);
+    cprev = c;
+    if (t + 1 < t_end) cur = nxt;
+  }
+  if (t_begin < t_end) finish(cprev, t_end - 1);
+
+  if (a.has_tail && vb == 0 && wave == 0) {
+    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(a.data + a.s_full * 512, a.tail_len, lane),
+                                                       lane), lane);
+    if (lane == 0) {
+      uint32_t be = __builtin_bswap32(r ^ a.tail_init);
+      if (a.meta_out) a.meta_out[a.s_full] = be;
+      if (a.meta_expect && a.meta_expect[a.s_full] != be) bad = min(bad, static_cast<uint32_t>(a.s_full));
+    }
+  }
+  if (a.part_crc) {
+    for (int k = wave; k < 3; ++k) acc = tab4(lt.sh4k, acc);
+    uint64_t e = t_begin < t_end ? a.ntiles - t_end : 0;
+    for (int b = 0; e; ++b, e >>= 1)
+      if (e & 1) acc = mat_apply(lt.tile_pow2[b], acc, lane);
+    if (lane == 0) wacc[gw] = acc;
+  }
+  if (a.part_bad && bad != 0xFFFFFFFFu) atomicMin(&wg_bad[grp], bad);
+  __syncthreads();
+  if (threadIdx.x < kGroups) {
+    const int g = threadIdx.x;
+    const uint64_t v = static_cast<uint64_t>(blockIdx.x) * kGroups + g;
+    if (a.part_crc) a.part_crc[v] = wacc[4 * g] ^ wacc[4 * g + 1] ^ wacc[4 * g + 2] ^ wacc[4 * g + 3];
+    if (a.part_bad) a.part_bad[v] = wg_bad[g];
   }
 }
 
@@ -612,9 +773,9 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
       c.meta_out[i] = be;
       a.meta_host[i] = be;
     }
-    r = combine(r, 8, lane, lt.sh512);
-    r = combine(r, 16, lane, lt.sh1k);
-    r = combine(r, 32, lane, lt.sh2k);
+    r = combine<8>(r, lane, lt.sh512);
+    r = combine<16>(r, lane, lt.sh1k);
+    r = combine<32>(r, lane, lt.sh2k);
     acc = mat_apply(lt.tile_pow2[0], acc, lane) ^ r;
     if (t + 1 < t_end) cur = nxt;
   }
@@ -767,9 +928,9 @@ void crc_tile_ring_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
       if (a.meta_expect && ring.expect[slot] != be) bad = min(bad, static_cast<uint32_t>(i));
     }
     if (a.part_crc) {
-      r = combine(r, 8, lane, lt.sh512);
-      r = combine(r, 16, lane, lt.sh1k);
-      r = combine(r, 32, lane, lt.sh2k);  // wave-uniform: the 4 KiB sub-tile's raw CRC
+      r = combine<8>(r, lane, lt.sh512);
+      r = combine<16>(r, lane, lt.sh1k);
+      r = combine<32>(r, lane, lt.sh2k);  // wave-uniform: the 4 KiB sub-tile's raw CRC
       acc = mat_apply(lt.tile_pow2[0], acc, lane) ^ r;
     }
   };
@@ -1052,6 +1213,23 @@ static int ring_for(uint64_t ntiles) {
 // One resident round: 3 workgroups per CU at 3 waves/SIMD (R = 2), 2 at 2 waves/SIMD.
 static uint64_t crc_grid_cap(int ring) { return ring > 2 ? 2 * 256 : kMaxGridCrc; }
 
+// K1/K2 as crc_tile_wide_kernel (one workgroup of kCrcWideGroups x 4 waves per CU): 0 = off,
+// 1 = on. DFS_CRC_WIDE overrides the default.
+static std::atomic<int> g_crc_wide{-1};
+constexpr int kCrcWideGroups = kMaxGridCrc / 256;
+
+void set_crc_wide(int mode) { g_crc_wide.store(mode <= 0 ? 0 : 1); }
+
+int crc_wide_mode() {
+  int v = g_crc_wide.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("DFS_CRC_WIDE");
+    v = e ? std::atoi(e) : kCrcWideDefault;
+    g_crc_wide.store(v = v <= 0 ? 0 : 1);
+  }
+  return v;
+}
+
 DevCrcTables* upload_crc_tables(hipStream_t s) {
   static_assert(sizeof(DevCrcTables) % 16 == 0, "table image must be uint4-copyable");
   std::vector<uint8_t> host(sizeof(DevCrcTables));
@@ -1071,15 +1249,19 @@ DevCrcTables* upload_crc_tables(hipStream_t s) {
   // MFMA basis right behind the LDS image (never copied to LDS): fragment [s][lane] of A,
   // element j = byte j of the 16 B: CRC bit i = lane & 31 of V[32h + 4(s>>1) + (j&3)][4(s&1) + (j>>2)],
   // scaled by 2^(7-p) (see wave_chunk_crcs)
-  host.resize(sizeof(DevCrcTables) + kCrcBasisBytes + kCrcChunkShiftBytes);
-  // chunk-shift tables behind the basis: cs[sl] moves a 64 B chunk's CRC past 64 * (7 - sl) bytes
+  host.resize(sizeof(DevCrcTables) + kCrcBasisBytes + kCrcChunkShiftBytes + kCrcWideExtraBytes);
+  // chunk-shift tables behind the basis: cs[sl] moves a 64 B chunk's CRC past 64 * (7 - sl) bytes;
+  // then ss[sw] (a slice's CRC past 512 * (7 - sw) bytes) and the 16 KiB tile shift
   auto* cs = reinterpret_cast<uint32_t(*)[4][256]>(host.data() + sizeof(DevCrcTables) + kCrcBasisBytes);
   for (int sl = 0; sl < 7; ++sl) shift_table(64 * (7 - sl), cs[sl]);
+  for (int sw = 0; sw < 7; ++sw) shift_table(512 * (7 - sw), cs[7 + sw]);
+  shift_table(16384, cs[14]);
   int8_t* basis = reinterpret_cast<int8_t*>(host.data() + sizeof(DevCrcTables));
   for (int st = 0; st < 16; ++st)
     for (int lane = 0; lane < 64; ++lane)
       for (int j = 0; j < 16; ++j) {
-        const int h = lane >> 5, bit = lane & 31;
+        // row R = lane & 31 of A carries CRC bit R ^ 7 (the order wave_chunk_crcs gathers in)
+        const int h = lane >> 5, bit = (lane & 31) ^ 7;
         const int byte = 32 * h + 4 * (st >> 1) + (j & 3), p = 4 * (st & 1) + (j >> 2);
         const uint32_t v = chunk_basis_crc(byte, p);
         basis[(st * 64 + lane) * 16 + j] = ((v >> bit) & 1u) ? static_cast<int8_t>(static_cast<uint8_t>(1u << (7 - p))) : 0;
@@ -1105,8 +1287,12 @@ int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
     return static_cast<uint64_t>(v > 0 ? v : 1);
   }();
   uint64_t g = (ntiles + per - 1) / per;
-  const uint64_t cap = crc_grid_cap(ring_for(ntiles));
+  const int ring = ring_for(ntiles);
+  const uint64_t cap = crc_grid_cap(ring);
   g = g < cap ? g : cap;
+  // the wide kernel runs kCrcWideGroups virtual workgroups per launched one (empty runs
+  // leave a zero partial and no verdict)
+  if (ring == 2 && crc_wide_mode() && g) g = (g + kCrcWideGroups - 1) / kCrcWideGroups * kCrcWideGroups;
   if (g == 0 && has_tail) g = 1;
   return static_cast<int>(g);
 }
@@ -1115,7 +1301,14 @@ hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipSt
   if (grid <= 0) return hipSuccess;
   switch (ring_for(a.ntiles)) {
     case 0: hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
-    case 2: hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
+    case 2:
+      if (crc_wide_mode() && grid % kCrcWideGroups == 0) {
+        hipLaunchKernelGGL(crc_tile_wide_kernel<kCrcWideGroups>, dim3(grid / kCrcWideGroups),
+                           dim3(kCrcWgThreads * kCrcWideGroups), 0, s, a, t);
+      } else {
+        hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
+      }
+      break;
     case 3: hipLaunchKernelGGL(crc_tile_ring_kernel<3>, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
     default: hipLaunchKernelGGL(crc_tile_ring_kernel<4>, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
   }

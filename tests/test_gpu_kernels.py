@@ -48,6 +48,28 @@ def test_gpu_crc_matrix_core_kernel_below_the_dispatch_threshold(gstore, native,
         native.set_crc_lds_max_mib(16)
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("n", [511, (1 << 20) + 13, (8 << 20) - 4096 + 7, (64 << 20) + 513, 300 << 20])
+def test_gpu_crc_wide_workgroups(gstore, native, mode, n):
+    """K1/K2 with one workgroup per CU (three 4-wave groups sharing the LDS image and the MFMA
+    basis, two-lookup combine) against zlib: whole-block CRC and every slice word, with tails."""
+    saved = native.crc_wide_mode()
+    native.set_crc_lds_max_mib(0)
+    native.set_crc_wide(mode)
+    try:
+        d = os.urandom(n)
+        crc, meta = gstore.gpu_crc(d)
+        assert crc == zlib.crc32(d) and meta == ref_meta(d)
+        if n < (100 << 20):
+            ok, _, err = gstore.write(f"wide{mode}_{n}", d, zlib.crc32(d))
+            assert ok, err
+            st, total, out, partial, bad, err = gstore.read(f"wide{mode}_{n}", 0, 0)
+            assert (st, total, out) == (0, n, d)
+    finally:
+        native.set_crc_wide(saved)
+        native.set_crc_lds_max_mib(16)
+
+
 def test_gpu_crc_zero_and_pattern(gstore):
     for d in (b"\0" * (1 << 20), bytes(range(256)) * 4099):
         crc, meta = gstore.gpu_crc(d)
