@@ -548,7 +548,9 @@ static_assert(offsetof(MfmaWideLds, sh4k) == kCrcChunkShiftBytes + kCrcWideExtra
 static_assert(sizeof(MfmaWideLds) - offsetof(MfmaWideLds, sh4k) == sizeof(DevCrcTables) - offsetof(DevCrcTables, sh4k),
               "wide image: DevCrcTables tail");
 
-template <int kGroups>
+// kWrite: the K1/K2 write form (slice words out, whole-block partials, nothing to verify),
+// with those checks resolved at compile time so the loop body has no uniform branches.
+template <int kGroups, bool kWrite>
 __global__ __launch_bounds__(kCrcWgThreads * kGroups) __attribute__((amdgpu_waves_per_eu(3, 3)))
 void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   constexpr int kThreads = kCrcWgThreads * kGroups;
@@ -588,10 +590,10 @@ void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
     uint32_t r = slice_from_chunks(lt, valid ? c : 0u, lane);
     if (valid && sl == 0) {
       uint32_t be = __builtin_bswap32(r ^ a.full_init);
-      if (a.meta_out) a.meta_out[i] = be;
-      if (a.meta_expect && a.meta_expect[i] != be) bad = min(bad, static_cast<uint32_t>(i));
+      if (kWrite || a.meta_out) a.meta_out[i] = be;
+      if (!kWrite && a.meta_expect && a.meta_expect[i] != be) bad = min(bad, static_cast<uint32_t>(i));
     }
-    if (a.part_crc) {
+    if (kWrite || a.part_crc) {
       uint32_t v = sw < 7 ? tab4(lt.ss[sw], r) : r;
       v = xr32(xr16(xr8(v)));  // wave-uniform: the 4 KiB sub-tile's raw CRC
       acc = tab4(lt.sh16k, acc) ^ v;
@@ -1303,8 +1305,11 @@ hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipSt
     case 0: hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
     case 2:
       if (crc_wide_mode() && grid % kCrcWideGroups == 0) {
-        hipLaunchKernelGGL(crc_tile_wide_kernel<kCrcWideGroups>, dim3(grid / kCrcWideGroups),
-                           dim3(kCrcWgThreads * kCrcWideGroups), 0, s, a, t);
+        const dim3 g(grid / kCrcWideGroups), b(kCrcWgThreads * kCrcWideGroups);
+        if (a.meta_out && !a.meta_expect && a.part_crc)
+          hipLaunchKernelGGL((crc_tile_wide_kernel<kCrcWideGroups, true>), g, b, 0, s, a, t);
+        else
+          hipLaunchKernelGGL((crc_tile_wide_kernel<kCrcWideGroups, false>), g, b, 0, s, a, t);
       } else {
         hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
       }
