@@ -111,11 +111,12 @@ def build(clean: bool = False, verbose: bool = False) -> Path:
 
 
 def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[Path]) -> list[Path]:
-    """Native executables (csrc/bench/*.cpp) linked against the runtime objects, e.g. the
-    io_bench microbenchmark. Written to build/native/ (ships to the GPU box)."""
+    """Native executables linked against the runtime objects: the benchmarks and unit tests
+    (csrc/bench/*.cpp, e.g. io_bench) and the command-line tools (csrc/tools/*.cpp, dfs_cli).
+    Written to build/native/ (ships to the GPU box)."""
     runtime = [o for o in objs if not o.name.startswith("bindings")]
     outs = []
-    for src in sorted((CSRC / "bench").glob("*.cpp")):
+    for src in sorted((CSRC / "bench").glob("*.cpp")) + sorted((CSRC / "tools").glob("*.cpp")):
         obj = BUILD / ("bench_" + src.name + ".o")
         exe = BUILD / src.stem
         if clean or _newer(src, obj, headers):

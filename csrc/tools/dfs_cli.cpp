@@ -1,0 +1,719 @@
+// dfs_cli — the native command-line client (C51; reference dfs/client/src/bin/dfs_cli.rs).
+//
+// The reference CLI is a Rust binary over its Rust client library; this is the C++ one over
+// the native client (client_remote.cpp: every RPC over gRPC/TCP on nghttp2, TLS when the
+// endpoints are https). Same global flags and output as the Python CLI
+// (rust_hadoop_generated_by_llm_amd/cli/dfs_cli.py), which stays the implementation of the
+// tooling commands this binary hands over to it as a child process (workload, check-history,
+// presign, cluster up/add-server/remove-server, shuffle) and of the few data operations the
+// native client does not own (files over one block, paths another shard must serve):
+//
+//   dfs_cli [-m MASTER[,..]] [--config-servers A,B] [--max-retries N] [--initial-backoff-ms MS]
+//           [--host-alias a=b ...] [--ca-cert F] [--domain-name D] [--hedge-delay-ms MS]
+//     ls | put SRC DEST [--ec-data K --ec-parity M] | get SRC DEST | inspect PATH
+//     rename SRC DEST | delete PATH | safe-mode get|enter|leave | cluster info
+//     benchmark write [-c N -s BYTES -n CONC -p PREFIX --json] | benchmark read [-p -n --json]
+//     benchmark stress-write [-d SECS -s BYTES -n CONC -p PREFIX --json]
+//
+// Master RPCs follow the reference client's retry policy (mod.rs:1170-1290): Not Leader
+// hints (status text "Not Leader|addr" or a response's leader_hint), REDIRECT:<addr> from a
+// master that does not own the path (the shard map is refetched), exponential backoff.
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <random>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "client_remote.h"
+#include "dfs_pb.h"
+#include "grpc_client.h"
+#include "json.h"
+#include "shard_map.h"
+#include "tls.h"
+
+using namespace dfs;
+
+namespace {
+
+struct CliError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+std::vector<std::string> split(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (char c : s) {
+    if (c == sep) {
+      if (!cur.empty()) out.push_back(cur);
+      cur.clear();
+    } else if (c != ' ') {
+      cur.push_back(c);
+    }
+  }
+  if (!cur.empty()) out.push_back(cur);
+  return out;
+}
+
+bool starts_with(const std::string& s, const std::string& p) { return s.compare(0, p.size(), p) == 0; }
+
+struct Args {
+  std::vector<std::string> masters{"http://127.0.0.1:50051"};
+  std::vector<std::string> config_servers;
+  int max_retries = 5, backoff_ms = 500, hedge_ms = 0;
+  std::vector<std::pair<std::string, std::string>> aliases;
+  std::string ca_cert, domain;
+  std::vector<std::string> pos;                 // command and its positional arguments
+  std::map<std::string, std::string> opt;       // command options (--name or -x -> value)
+  std::set<std::string> flags;                  // valueless command options
+};
+
+// Options of the commands this binary runs (anything else goes to the Python CLI).
+const std::map<std::string, std::string> kShort = {{"-c", "--count"}, {"-s", "--size"}, {"-n", "--concurrency"},
+                                                   {"-p", "--prefix"}, {"-d", "--duration"}};
+const std::set<std::string> kValued = {"--count", "--size", "--concurrency", "--prefix", "--duration", "--ec-data",
+                                       "--ec-parity"};
+
+Args parse(int argc, char** argv) {
+  Args a;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) throw CliError("missing value for " + s);
+      return argv[++i];
+    };
+    if (a.pos.empty() && (s == "-m" || s == "--master")) a.masters = split(val(), ',');
+    else if (a.pos.empty() && s == "--config-servers") a.config_servers = split(val(), ',');
+    else if (a.pos.empty() && s == "--max-retries") a.max_retries = std::atoi(val().c_str());
+    else if (a.pos.empty() && s == "--initial-backoff-ms") a.backoff_ms = std::atoi(val().c_str());
+    else if (a.pos.empty() && s == "--hedge-delay-ms") a.hedge_ms = std::atoi(val().c_str());
+    else if (a.pos.empty() && s == "--ca-cert") a.ca_cert = val();
+    else if (a.pos.empty() && s == "--domain-name") a.domain = val();
+    else if (a.pos.empty() && s == "--host-alias") {
+      std::string p = val();
+      auto eq = p.find('=');
+      if (eq != std::string::npos) a.aliases.emplace_back(p.substr(0, eq), p.substr(eq + 1));
+    } else if (!a.pos.empty() && s.size() > 1 && s[0] == '-' && !std::isdigit(static_cast<unsigned char>(s[1]))) {
+      auto k = kShort.find(s);
+      const std::string name = k != kShort.end() ? k->second : s;
+      if (kValued.count(name) && i + 1 < argc) a.opt[name] = val();
+      else a.flags.insert(name);  // --json, or an option of a command the Python CLI runs
+    } else {
+      a.pos.push_back(s);
+    }
+  }
+  return a;
+}
+
+// The commands (and forms) run here; everything else is the Python CLI's.
+bool native_command(const Args& a) {
+  if (a.pos.empty()) return false;
+  const std::string& c = a.pos[0];
+  const std::string sub = a.pos.size() > 1 ? a.pos[1] : "";
+  if (c == "ls" || c == "get" || c == "inspect" || c == "rename" || c == "delete" || c == "put") return true;
+  if (c == "safe-mode") return sub == "get" || sub == "enter" || sub == "leave";
+  if (c == "cluster") return sub == "info";
+  if (c == "benchmark") return sub == "write" || sub == "read" || sub == "stress-write";
+  return false;
+}
+
+// The Python CLI as a child process (this process never touches the GPU), same argv.
+int run_python(int argc, char** argv) {
+  char self[4096];
+  ssize_t n = ::readlink("/proc/self/exe", self, sizeof self - 1);
+  std::string root = ".";
+  if (n > 0) {
+    self[n] = 0;
+    std::string p = self;  // <repo>/build/native/dfs_cli
+    for (int k = 0; k < 3 && p.find('/') != std::string::npos; ++k) p = p.substr(0, p.rfind('/'));
+    root = p;
+  }
+  std::fflush(stdout);
+  std::fflush(stderr);
+  pid_t pid = ::fork();
+  if (pid < 0) {
+    std::perror("fork");
+    return 1;
+  }
+  if (pid == 0) {
+    const char* old = std::getenv("PYTHONPATH");
+    std::string pp = root + (old && *old ? ":" + std::string(old) : "");
+    ::setenv("PYTHONPATH", pp.c_str(), 1);
+    std::vector<char*> av{const_cast<char*>("python3"), const_cast<char*>("-m"),
+                          const_cast<char*>("rust_hadoop_generated_by_llm_amd.cli.dfs_cli")};
+    for (int i = 1; i < argc; ++i) av.push_back(argv[i]);
+    av.push_back(nullptr);
+    ::execvp("python3", av.data());
+    std::perror("exec python3");
+    ::_exit(127);
+  }
+  int st = 0;
+  while (::waitpid(pid, &st, 0) < 0 && errno == EINTR) {
+  }
+  return WIFEXITED(st) ? WEXITSTATUS(st) : 1;
+}
+
+class Cli {
+ public:
+  explicit Cli(const Args& a) : a_(a) {
+    if (!a.ca_cert.empty()) {
+      std::string err;
+      tls_ = TlsContext::client(a.ca_cert, a.domain, &err);
+      if (!tls_) throw CliError("TLS: " + err);
+    }
+    pool_ = std::make_unique<GrpcChannelPool>(30000, tls_);
+    pool_->set_host_aliases(a.aliases);
+    for (auto& m : a.masters) masters_.push_back(scheme(m));
+    if (!a.config_servers.empty()) refresh_map(true);
+  }
+
+  std::string scheme(const std::string& addr) const {
+    if (addr.find("://") != std::string::npos) return addr;
+    return (tls_ ? "https://" : "http://") + addr;
+  }
+
+  // FetchShardMap from the first config server that answers (ShardMap.from_fetch: sorted
+  // shard ids on a Range map; the `ranges` extension gives the exact boundaries).
+  void refresh_map(bool warn) {
+    for (auto& c : a_.config_servers) {
+      GrpcResult r = pool_->call(scheme(c), "/dfs.ConfigService/FetchShardMap", std::string(), "", 5000);
+      if (!r.transport_ok || r.status != 0) continue;
+      pb::FetchShardMapResponse resp;
+      if (!resp.decode(r.message) || resp.shards.empty()) return;
+      ShardMap m = ShardMap::new_range();
+      for (auto& kv : resp.shards) m.add_shard(kv.first, kv.second.peers);
+      if (!resp.ranges.empty()) {
+        Json j = m.to_json();
+        Json ranges = Json::object();
+        for (auto& kv : resp.ranges)
+          if (resp.shards.count(kv.second)) ranges.set(kv.first, Json(kv.second));
+        Json range = Json::object();
+        range.set("ranges", ranges);
+        Json strat = Json::object();
+        strat.set("Range", range);
+        j.set("strategy", strat);
+        m = ShardMap::from_json(j);
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      map_ = m;
+      have_map_ = true;
+      return;
+    }
+    if (warn) std::fprintf(stderr, "warning: could not fetch shard map from the config servers\n");
+  }
+
+  std::string map_json() {
+    std::lock_guard<std::mutex> g(mu_);
+    return have_map_ ? map_.to_json().dump() : std::string();
+  }
+
+  std::vector<std::string> targets_for(const std::string& path) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (have_map_) {
+      const std::string s = map_.get_shard(path);
+      const auto* peers = s.empty() ? nullptr : map_.peers(s);
+      if (peers && !peers->empty()) {
+        std::vector<std::string> out;
+        for (auto& p : *peers) out.push_back(scheme(p));
+        return out;
+      }
+    }
+    return masters_;
+  }
+
+  std::vector<std::vector<std::string>> all_shards() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::vector<std::string>> out;
+    if (have_map_)
+      for (auto& s : map_.shards()) {
+        const auto* peers = map_.peers(s);
+        std::vector<std::string> v;
+        if (peers)
+          for (auto& p : *peers) v.push_back(scheme(p));
+        if (!v.empty()) out.push_back(v);
+      }
+    if (out.empty()) out.push_back(masters_);
+    return out;
+  }
+
+  // One MasterService call with the reference client's retry policy. `leader_hint` reads a
+  // response-level "Not Leader" (success = false + leader_hint); empty = no such field.
+  std::string call(std::vector<std::string> masters, const std::string& method, const std::string& req,
+                   const std::function<std::string(const std::string&)>& leader_hint = nullptr) {
+    int backoff = a_.backoff_ms;
+    std::string hint, last = "no masters configured";
+    int redirects = 0;
+    for (int attempt = 1; attempt <= std::max(1, a_.max_retries); ++attempt) {
+      std::vector<std::string> targets = masters;
+      if (!hint.empty()) targets.insert(targets.begin(), scheme(hint));
+      hint.clear();
+      for (auto& addr : targets) {
+        GrpcResult r = pool_->call(addr, "/dfs.MasterService/" + method, req, "");
+        if (!r.transport_ok) {
+          last = "unavailable: " + addr;
+          continue;
+        }
+        if (r.status == 0) {
+          if (leader_hint) {
+            std::string h = leader_hint(r.message);
+            if (h == "\x01") {  // Not Leader without a hint: next target
+              last = "Not Leader";
+              continue;
+            }
+            if (!h.empty()) {
+              last = "Not Leader";
+              hint = h;
+              break;
+            }
+          }
+          return r.message;
+        }
+        const std::string& msg = r.message;
+        last = std::to_string(r.status) + ": " + msg;
+        if (starts_with(msg, "REDIRECT:") && msg.size() > 9) {
+          hint = msg.substr(9);
+          ++redirects;
+          refresh_map(false);
+          if (redirects > 1) std::this_thread::sleep_for(std::chrono::milliseconds(std::min(50 * redirects, 1000)));
+          break;
+        }
+        if (starts_with(msg, "Not Leader|") && msg.size() > 11) {
+          hint = msg.substr(11);
+          break;
+        }
+        if (msg.find("Not Leader") != std::string::npos || r.status == 14 || r.status == 4) continue;
+        throw CliError(status_name(r.status) + ": " + msg);
+      }
+      if (attempt >= a_.max_retries) break;
+      if (hint.empty()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(backoff));
+        backoff = std::min(backoff * 2, 5000);
+      }
+    }
+    throw CliError("No available leader found after retries (" + last + ")");
+  }
+
+  static std::string status_name(int s) {
+    static const char* names[] = {"OK", "CANCELLED", "UNKNOWN", "INVALID_ARGUMENT", "DEADLINE_EXCEEDED", "NOT_FOUND",
+                                  "ALREADY_EXISTS", "PERMISSION_DENIED", "RESOURCE_EXHAUSTED", "FAILED_PRECONDITION",
+                                  "ABORTED", "OUT_OF_RANGE", "UNIMPLEMENTED", "INTERNAL", "UNAVAILABLE", "DATA_LOSS",
+                                  "UNAUTHENTICATED"};
+    return s >= 0 && s <= 16 ? names[s] : "ERROR";
+  }
+
+  // First --master only (safe-mode / cluster admin RPCs, like the reference CLI).
+  std::string admin(const std::string& method, const std::string& req) {
+    GrpcResult r = pool_->call(masters_.at(0), "/dfs.MasterService/" + method, req, "", 30000);
+    if (!r.transport_ok) throw CliError("unavailable: " + masters_.at(0));
+    if (r.status != 0) throw CliError(status_name(r.status) + ": " + r.message);
+    return r.message;
+  }
+
+  std::vector<std::string> list_all(const std::string& path = "/") {
+    if (!a_.config_servers.empty()) refresh_map(false);
+    std::set<std::string> files;
+    for (auto& peers : all_shards()) {
+      pb::ListFilesRequest q;
+      q.path = path;
+      pb::ListFilesResponse resp;
+      if (!resp.decode(call(peers, "ListFiles", q.str()))) throw CliError("bad ListFiles response");
+      files.insert(resp.files.begin(), resp.files.end());
+    }
+    return {files.begin(), files.end()};
+  }
+
+  RemoteClient& client() {
+    if (!rc_) {
+      rc_ = std::make_unique<RemoteClient>(4, 120000, tls_);
+      rc_->set_host_aliases(a_.aliases);
+      rc_->set_routing(map_json(), masters_);
+      if (a_.hedge_ms > 0) rc_->set_hedge_delay(a_.hedge_ms);
+    }
+    return *rc_;
+  }
+
+ private:
+  const Args& a_;
+  std::shared_ptr<TlsContext> tls_;
+  std::unique_ptr<GrpcChannelPool> pool_;
+  std::vector<std::string> masters_;
+  std::mutex mu_;
+  ShardMap map_ = ShardMap::new_range();
+  bool have_map_ = false;
+  std::unique_ptr<RemoteClient> rc_;
+};
+
+// "Not Leader" in a response body: hint, "\x01" (no hint), or "" (not that).
+template <class Resp>
+std::string body_not_leader(const std::string& raw) {
+  Resp r;
+  if (!r.decode(raw) || r.success || r.error_message != "Not Leader") return std::string();
+  return r.leader_hint.empty() ? std::string("\x01") : r.leader_hint;
+}
+
+std::string read_file(const std::string& p) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) throw CliError("cannot open " + p + ": " + std::strerror(errno));
+  return std::string(std::istreambuf_iterator<char>(f), {});
+}
+
+// ---------------------------------------------------------------- benchmark (dfs_cli.rs:581-882)
+struct Stats {
+  std::string name;
+  size_t count = 0;
+  uint64_t bytes = 0;
+  double seconds = 0;
+  std::vector<double> lat;  // seconds
+  size_t errors = 0;
+
+  double pct(int p) const {
+    if (lat.empty()) return 0;
+    return lat[std::min(lat.size() - 1, lat.size() * static_cast<size_t>(p) / 100)];
+  }
+  void print(bool as_json) {
+    std::sort(lat.begin(), lat.end());
+    const double avg_size = count ? static_cast<double>(bytes / count) : 0;
+    const double mbps = seconds > 0 ? count * avg_size / (1024.0 * 1024.0) / seconds : 0;
+    const double ops = seconds > 0 ? count / seconds : 0;
+    double sum = 0;
+    for (double v : lat) sum += v;
+    const double mn = lat.empty() ? 0 : lat.front(), mx = lat.empty() ? 0 : lat.back();
+    const double av = lat.empty() ? 0 : sum / lat.size();
+    if (as_json) {
+      std::printf("{\"name\": \"%s\", \"ops\": %zu, \"bytes\": %.0f, \"seconds\": %.6f, \"mb_per_s\": %.4f, "
+                  "\"ops_per_s\": %.4f, \"errors\": %zu, \"min_ms\": %.4f, \"avg_ms\": %.4f, \"p50_ms\": %.4f, "
+                  "\"p95_ms\": %.4f, \"p99_ms\": %.4f, \"max_ms\": %.4f}\n",
+                  name.c_str(), count, count * avg_size, seconds, mbps, ops, errors, 1e3 * mn, 1e3 * av,
+                  1e3 * pct(50), 1e3 * pct(95), 1e3 * pct(99), 1e3 * mx);
+      return;
+    }
+    std::printf("\n📊 %s Benchmark Results:\n----------------------------------------\n", name.c_str());
+    std::printf("Total Operations:  %zu\nTotal Time:        %.2fs\nThroughput:        %.2f MB/s\n"
+                "Throughput (OPS):  %.2f ops/s\n\nLatency Statistics:\n",
+                count, seconds, mbps, ops);
+    std::printf("  Min:  %.2fms\n  Avg:  %.2fms\n  P50:  %.2fms\n  P95:  %.2fms\n  P99:  %.2fms\n  Max:  %.2fms\n",
+                1e3 * mn, 1e3 * av, 1e3 * pct(50), 1e3 * pct(95), 1e3 * pct(99), 1e3 * mx);
+    std::printf("----------------------------------------\n");
+  }
+};
+
+using Clock = std::chrono::steady_clock;
+
+double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+std::vector<std::string> payloads(size_t n, size_t size) {
+  std::mt19937_64 rng(std::random_device{}());
+  std::vector<std::string> out(n, std::string(size, '\0'));
+  for (auto& p : out)
+    for (size_t i = 0; i < size; i += 8) {
+      uint64_t v = rng();
+      std::memcpy(&p[i], &v, std::min<size_t>(8, size - i));
+    }
+  return out;
+}
+
+// `conc` worker threads pull op indices until `next(i)` says stop; op(i) -> bytes or -1.
+void run_workers(int conc, const std::function<bool(size_t)>& more, const std::function<int64_t(size_t)>& op,
+                 Stats* st) {
+  std::atomic<size_t> idx{0};
+  std::mutex mu;
+  std::vector<std::thread> th;
+  std::string first_err;
+  for (int w = 0; w < std::max(1, conc); ++w)
+    th.emplace_back([&] {
+      for (;;) {
+        const size_t i = idx.fetch_add(1);
+        if (!more(i)) return;
+        auto t0 = Clock::now();
+        int64_t n = op(i);
+        const double dt = secs(t0, Clock::now());
+        std::lock_guard<std::mutex> g(mu);
+        if (n < 0) {
+          ++st->errors;
+        } else {
+          st->lat.push_back(dt);
+          st->bytes += static_cast<uint64_t>(n);
+          ++st->count;
+        }
+      }
+    });
+  for (auto& t : th) t.join();
+}
+
+int64_t write_one(RemoteClient& rc, const std::string& path, const std::string& data, std::string* err) {
+  int replicas = 0;
+  std::string msg;
+  RemoteClient::Times t;
+  auto s = rc.write(path, reinterpret_cast<const uint8_t*>(data.data()), data.size(), &replicas, &msg, &t);
+  if (s == FastClient::Ok) return static_cast<int64_t>(data.size());
+  *err = s == FastClient::NotHandled ? "not handled by the native client: " + path : msg;
+  return -1;
+}
+
+int cmd_benchmark(Cli& cli, const Args& a) {
+  const std::string action = a.pos.at(1);
+  const bool js = a.flags.count("--json") != 0;
+  auto opt = [&](const std::string& k, const std::string& d) {
+    auto it = a.opt.find(k);
+    return it == a.opt.end() ? d : it->second;
+  };
+  const int conc = std::atoi(opt("--concurrency", "10").c_str());
+  RemoteClient& rc = cli.client();
+  std::mutex emu;
+  std::string err;
+  auto note = [&](const std::string& e) {
+    std::lock_guard<std::mutex> g(emu);
+    if (err.empty()) err = e;
+  };
+  if (action == "write") {
+    const size_t count = std::strtoull(opt("--count", "100").c_str(), nullptr, 10);
+    const size_t size = std::strtoull(opt("--size", "1048576").c_str(), nullptr, 10);
+    const std::string prefix = opt("--prefix", "bench_write");
+    if (!js)
+      std::printf("🚀 Starting Write Benchmark: %zu files, %zu bytes each, concurrency=%d\n", count, size, conc);
+    auto bufs = payloads(std::min<size_t>(count, 64), size);
+    const std::string run = std::to_string(std::time(nullptr));
+    Stats st{"Write"};
+    auto t0 = Clock::now();
+    run_workers(conc, [&](size_t i) { return i < count; },
+                [&](size_t i) {
+                  char name[64];
+                  std::snprintf(name, sizeof name, "/bench_%010zu", i);
+                  std::string e;
+                  int64_t n = write_one(rc, prefix + "/" + run + name, bufs[i % bufs.size()], &e);
+                  if (n < 0) note(e);
+                  return n;
+                },
+                &st);
+    st.seconds = secs(t0, Clock::now());
+    if (st.errors) throw CliError(err);
+    st.print(js);
+    return 0;
+  }
+  if (action == "read") {
+    const std::string prefix = opt("--prefix", "bench_write");
+    if (!js) std::printf("🚀 Starting Read Benchmark: prefix=%s, concurrency=%d\n", prefix.c_str(), conc);
+    std::vector<std::string> files;
+    std::string bare = prefix;
+    while (!bare.empty() && bare[0] == '/') bare.erase(0, 1);
+    for (auto& f : cli.list_all()) {
+      std::string fb = f;
+      while (!fb.empty() && fb[0] == '/') fb.erase(0, 1);
+      if (starts_with(f, prefix) || starts_with(fb, bare)) files.push_back(f);
+    }
+    if (files.empty()) {
+      std::printf("No files found matching prefix: %s\n", prefix.c_str());
+      return 0;
+    }
+    if (!js) std::printf("Found %zu files to read\n", files.size());
+    Stats st{"Read"};
+    auto t0 = Clock::now();
+    run_workers(conc, [&](size_t i) { return i < files.size(); },
+                [&](size_t i) -> int64_t {
+                  std::string out, msg;
+                  RemoteClient::Times t;
+                  auto s = rc.read(files[i], &out, &msg, &t);
+                  if (s == FastClient::Ok) return static_cast<int64_t>(out.size());
+                  note(s == FastClient::NotHandled ? "not handled by the native client: " + files[i] : msg);
+                  return -1;
+                },
+                &st);
+    st.seconds = secs(t0, Clock::now());
+    if (st.errors) throw CliError(err);
+    st.print(js);
+    return 0;
+  }
+  // stress-write: as many writes as fit in the duration
+  const double duration = std::atof(opt("--duration", "30").c_str());
+  const size_t size = std::strtoull(opt("--size", "1048576").c_str(), nullptr, 10);
+  const std::string prefix = opt("--prefix", "bench_stress");
+  if (!js)
+    std::printf("🔥 Starting Write Stress Test: duration=%gs, size=%zu bytes, concurrency=%d\n", duration, size, conc);
+  auto bufs = payloads(16, size);
+  const std::string run = std::to_string(std::time(nullptr));
+  const auto t0 = Clock::now(), deadline = t0 + std::chrono::duration_cast<Clock::duration>(
+                                                    std::chrono::duration<double>(duration));
+  Stats st{"Stress Write"};
+  run_workers(conc, [&](size_t) { return Clock::now() < deadline; },
+              [&](size_t i) {
+                char name[64];
+                std::snprintf(name, sizeof name, "/stress_%010zu", i);
+                std::string e;
+                int64_t n = write_one(rc, prefix + "/" + run + name, bufs[i % bufs.size()], &e);
+                if (n < 0) note(e);
+                return n;
+              },
+              &st);
+  st.seconds = secs(t0, Clock::now());
+  st.print(js);
+  if (st.errors && !js) std::printf("Errors: %zu\n", st.errors);
+  return 0;
+}
+
+// ---------------------------------------------------------------- the other commands
+int run(Cli& cli, const Args& a, int argc, char** argv) {
+  const std::string& c = a.pos.at(0);
+  auto need = [&](size_t n) {
+    if (a.pos.size() < n + 1) throw CliError(c + ": missing arguments");
+  };
+  if (c == "safe-mode") {
+    const std::string act = a.pos.at(1);
+    if (act == "get") {
+      pb::GetSafeModeStatusResponse r;
+      r.decode(cli.admin("GetSafeModeStatus", std::string()));
+      std::printf("Safe Mode Status:\n  Active: %s\n  Manual: %s\n  ChunkServers: %u\n  Blocks: %u/%u\n"
+                  "  Threshold: %d%%\n",
+                  r.is_safe_mode ? "true" : "false", r.is_manual ? "true" : "false", r.chunk_server_count,
+                  r.reported_blocks, r.expected_blocks, static_cast<int>(r.threshold * 100));
+      return 0;
+    }
+    const bool enter = act == "enter";
+    pb::SetSafeModeRequest q;
+    q.enter = enter;
+    pb::SetSafeModeResponse r;
+    r.decode(cli.admin("SetSafeMode", q.str()));
+    if (r.success) {
+      std::printf(enter ? "Entered Safe Mode\n" : "Left Safe Mode\n");
+      return 0;
+    }
+    std::printf("Failed to %s Safe Mode: %s\n", enter ? "enter" : "leave", r.error_message.c_str());
+    return 1;
+  }
+  if (c == "cluster") {
+    pb::GetClusterInfoResponse r;
+    r.decode(cli.admin("GetClusterInfo", std::string()));
+    std::printf("Raft Cluster Info:\n  Node ID: %u\n  Role: %s\n  Term: %llu\n  Leader ID: %u\n  Leader Address: %s\n"
+                "  Commit Index: %llu\n  Last Applied: %llu\n  Members (%zu):\n",
+                r.node_id, r.role.c_str(), static_cast<unsigned long long>(r.current_term), r.leader_id,
+                r.leader_address.c_str(), static_cast<unsigned long long>(r.commit_index),
+                static_cast<unsigned long long>(r.last_applied), r.members.size());
+    for (auto& m : r.members)
+      std::printf("    - [%u] %s %s\n", m.server_id, m.address.c_str(), m.is_self ? "(self)" : "");
+    return 0;
+  }
+  if (c == "ls") {
+    for (auto& f : cli.list_all()) std::printf("%s\n", f.c_str());
+    return 0;
+  }
+  if (c == "inspect") {
+    need(1);
+    pb::GetFileInfoRequest q;
+    q.path = a.pos[1];
+    pb::GetFileInfoResponse r;
+    r.decode(cli.call(cli.targets_for(q.path), "GetFileInfo", q.str()));
+    if (!r.found) {
+      std::printf("File not found: %s\n", q.path.c_str());
+      return 0;
+    }
+    const pb::FileMetadata& m = r.metadata;
+    std::printf("File Metadata for: %s\n  Size: %llu bytes\n", m.path.c_str(), static_cast<unsigned long long>(m.size));
+    if (m.ec_data_shards > 0) std::printf("  Storage: EC RS(%d,%d)\n", m.ec_data_shards, m.ec_parity_shards);
+    else std::printf("  Storage: Replicated\n");
+    std::printf("  Blocks: %zu\n", m.blocks.size());
+    auto locs = [](const std::vector<std::string>& v) {
+      std::string s = "[";
+      for (size_t i = 0; i < v.size(); ++i) s += (i ? ", '" : "'") + v[i] + "'";
+      return s + "]";
+    };
+    for (size_t i = 0; i < m.blocks.size(); ++i) {
+      const auto& b = m.blocks[i];
+      if (b.ec_data_shards > 0)
+        std::printf("    Block %zu: ID=%s, Size=%llu, EC=RS(%d,%d), OriginalSize=%llu, Shards=%s\n", i,
+                    b.block_id.c_str(), static_cast<unsigned long long>(b.size), b.ec_data_shards, b.ec_parity_shards,
+                    static_cast<unsigned long long>(b.original_size), locs(b.locations).c_str());
+      else
+        std::printf("    Block %zu: ID=%s, Size=%llu, Locations=%s\n", i, b.block_id.c_str(),
+                    static_cast<unsigned long long>(b.size), locs(b.locations).c_str());
+    }
+    return 0;
+  }
+  if (c == "rename") {
+    need(2);
+    pb::RenameRequest q;
+    q.source_path = a.pos[1];
+    q.dest_path = a.pos[2];
+    pb::RenameResponse r;
+    r.decode(cli.call(cli.targets_for(q.source_path), "Rename", q.str(), body_not_leader<pb::RenameResponse>));
+    if (!r.success) throw CliError("Rename failed: " + r.error_message);
+    std::printf("File renamed successfully: %s -> %s\n", q.source_path.c_str(), q.dest_path.c_str());
+    return 0;
+  }
+  if (c == "delete") {
+    need(1);
+    pb::DeleteFileRequest q;
+    q.path = a.pos[1];
+    pb::DeleteFileResponse r;
+    r.decode(cli.call(cli.targets_for(q.path), "DeleteFile", q.str(), body_not_leader<pb::DeleteFileResponse>));
+    if (!r.success) throw CliError("Failed to delete file: " + r.error_message);
+    std::printf("File deleted: %s\n", q.path.c_str());
+    return 0;
+  }
+  if (c == "put") {
+    need(2);
+    const std::string data = read_file(a.pos[1]);
+    const int k = a.opt.count("--ec-data") ? std::atoi(a.opt.at("--ec-data").c_str()) : 0;
+    const int m = a.opt.count("--ec-parity") ? std::atoi(a.opt.at("--ec-parity").c_str()) : 0;
+    std::string msg;
+    FastClient::Status s;
+    if (k > 0 && m > 0) {
+      s = cli.client().write_ec(a.pos[2], reinterpret_cast<const uint8_t*>(data.data()), data.size(), k, m, &msg, "");
+    } else {
+      int replicas = 0;
+      RemoteClient::Times t;
+      s = cli.client().write(a.pos[2], reinterpret_cast<const uint8_t*>(data.data()), data.size(), &replicas, &msg, &t);
+    }
+    if (s == FastClient::NotHandled) return run_python(argc, argv);
+    if (s != FastClient::Ok) throw CliError(msg);
+    if (k > 0 && m > 0) std::printf("File uploaded successfully with EC RS(%d,%d)\n", k, m);
+    else std::printf("File uploaded successfully with replication\n");
+    return 0;
+  }
+  if (c == "get") {
+    need(2);
+    std::string out, msg;
+    RemoteClient::Times t;
+    auto s = cli.client().read(a.pos[1], &out, &msg, &t);
+    if (s == FastClient::NotHandled) return run_python(argc, argv);
+    if (s != FastClient::Ok) throw CliError(msg);
+    std::ofstream f(a.pos[2], std::ios::binary | std::ios::trunc);
+    if (!f || !f.write(out.data(), static_cast<std::streamsize>(out.size()))) throw CliError("cannot write " + a.pos[2]);
+    std::printf("File downloaded successfully\n");
+    return 0;
+  }
+  return cmd_benchmark(cli, a);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  try {
+    a = parse(argc, argv);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "Error: %s\n", e.what());
+    return 2;
+  }
+  if (!native_command(a) || std::getenv("DFS_CLI_PYTHON")) return run_python(argc, argv);
+  try {
+    Cli cli(a);
+    return run(cli, a, argc, argv);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "Error: %s\n", e.what());
+    return 1;
+  }
+}
