@@ -346,6 +346,11 @@ def verify_chain(store: SegmentStore, secret: str) -> tuple[int, list[str]]:
     return n, errors
 
 
+def _txt(rec: dict, k: str) -> str:
+    v = rec.get(k)
+    return "" if v is None else str(v)
+
+
 def _parse_time(s: str) -> int:
     return int(datetime.fromisoformat(s.replace("Z", "+00:00")).timestamp() * 1000)
 
@@ -394,8 +399,8 @@ def reader_main(argv: list[str] | None = None) -> int:
         if a.json:
             print(json.dumps(rec, separators=(",", ":")))
         else:
-            print(f"{rec.get('timestamp', ''):<32} {rec.get('user_id', ''):<20} {rec.get('action', ''):<22} "
-                  f"{rec.get('status_code', ''):<6} {rec.get('resource', '')}")
+            print(f"{_txt(rec, 'timestamp'):<32} {_txt(rec, 'user_id'):<20} {_txt(rec, 'action'):<22} "
+                  f"{_txt(rec, 'status_code'):<6} {_txt(rec, 'resource')}")
         count += 1
         if count >= a.limit:
             break
