@@ -26,6 +26,7 @@
 #include "master_core.h"
 #include "raft.h"
 #include "s3_front.h"
+#include "s3_policy.h"
 #include "tls.h"
 #include "trace.h"
 
@@ -820,12 +821,46 @@ void bind_meta(py::module_& m) {
         d["bytes_in"] = s.bytes_in;
         d["bytes_out"] = s.bytes_out;
         d["auth_native"] = s.auth_native;
+        d["policy_native"] = s.policy_native;
         d["audit_sent"] = s.audit_sent;
         d["audit_dropped"] = s.audit_dropped;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;
         return d;
       });
+
+  // ---------------- IAM / bucket policy engine (csrc/s3_policy.cpp; parity tests)
+  m.def("s3_wildcard", &s3policy::matches_wildcard);
+  m.def("s3_bucket_policy_eval", [](const std::string& doc, std::optional<std::string> principal, const std::string& action,
+                                    const std::string& resource) {
+    s3policy::BucketPolicy p;
+    try {
+      p = s3policy::BucketPolicy::parse(doc);
+    } catch (const std::exception& e) {
+      throw py::value_error(e.what());
+    }
+    switch (p.evaluate(principal ? &*principal : nullptr, action, resource)) {
+      case s3policy::PolicyResult::Allow: return std::string("Allow");
+      case s3policy::PolicyResult::ExplicitDeny: return std::string("ExplicitDeny");
+      default: return std::string("NotApplicable");
+    }
+  });
+  m.def("s3_iam_eval", [](const std::string& doc, const std::string& action, const std::string& resource,
+                          const std::string& role_arn, const std::string& principal_id, std::vector<std::string> groups,
+                          std::map<std::string, std::string> claims) {
+    s3policy::IamPolicy p;
+    try {
+      p = s3policy::IamPolicy::parse(doc);
+    } catch (const std::exception& e) {
+      throw py::value_error(e.what());
+    }
+    s3policy::Context ctx{principal_id, std::move(groups), std::move(claims)};
+    return py::make_tuple(p.evaluate(action, resource, role_arn, ctx), p.can_assume_role(role_arn, ctx));
+  });
+  m.def("s3_resolve_action", [](const std::string& method, const std::string& path, std::vector<std::string> keys) {
+    auto r = s3policy::resolve_action_and_resource(method, path, keys);
+    return py::make_tuple(r.first, r.second);
+  });
 
   // ---------------- native client data path (co-located writers/readers)
   py::class_<FastClient>(m, "FastClient")

@@ -504,7 +504,21 @@ bool S3Front::handle(Conn* c, Req& r) {
   std::string user = "anonymous";
   if (cfg_.auth_enabled) {
     if (!verify_auth(r, &user)) return proxy(c, r, nullptr, 0, "auth");
-    if (bucket_has_policy(bucket)) return proxy(c, r, nullptr, 0, "bucket-policy");
+    // bucket policy (reference auth_middleware.rs + bucket_policy.rs): a static-key caller has
+    // no role ARN, so only a Principal "*" Deny can apply; a denial is handed to the gateway,
+    // which answers it (403 + audit) exactly as for any other denied request
+    bool known = false;
+    auto pol = bucket_policy(bucket, &known);
+    if (!known) return proxy(c, r, nullptr, 0, "bucket-policy");
+    if (pol) {
+      std::vector<std::string> keys;
+      for (auto& kv : q) keys.push_back(kv.first);
+      auto ar = s3policy::resolve_action_and_resource(r.method, r.raw_path, keys);
+      if (pol->evaluate(nullptr, ar.first, ar.second) == s3policy::PolicyResult::ExplicitDeny)
+        return proxy(c, r, nullptr, 0, "bucket-policy-deny");
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.policy_native++;
+    }
   }
   std::string path = "/" + bucket + "/" + key;
   bool ok;
@@ -623,19 +637,39 @@ int S3Front::verify_auth(Req& r, std::string* user) {
   return 1;
 }
 
-bool S3Front::bucket_has_policy(const std::string& bucket) {
+std::shared_ptr<const s3policy::BucketPolicy> S3Front::bucket_policy(const std::string& bucket, bool* known) {
   const double now = now_s();
   {
     std::lock_guard<std::mutex> g(pol_mu_);
     auto it = policy_cache_.find(bucket);
-    if (it != policy_cache_.end() && it->second.first > now) return it->second.second;
+    if (it != policy_cache_.end() && it->second.first > now) {
+      *known = true;
+      return it->second.second;
+    }
   }
-  bool found = true;  // unknown: treat as "has a policy" (Python decides)
+  *known = false;
+  const std::string path = "/" + bucket + "/.s3_bucket_policy";
+  bool found = false;
   std::string meta, msg;
-  if (fc_->stat("/" + bucket + "/.s3_bucket_policy", &found, &meta, &msg, "") != FastClient::Ok) found = true;
+  if (fc_->stat(path, &found, &meta, &msg, "") != FastClient::Ok) return nullptr;
+  std::shared_ptr<const s3policy::BucketPolicy> pol;
+  if (found) {
+    int64_t slot = -1;
+    uint64_t n = 0;
+    FastClient::Times t;
+    if (fc_->read_known(meta, &slot, &n, &msg, &t, "", 0, 0) != FastClient::Ok) return nullptr;
+    std::string doc(reinterpret_cast<const char*>(fc_->slot_ptr(slot)), n);
+    fc_->release(slot);
+    try {
+      pol = std::make_shared<const s3policy::BucketPolicy>(s3policy::BucketPolicy::parse(doc));
+    } catch (const std::exception&) {
+      pol = nullptr;  // the gateway ignores an unparsable policy as well
+    }
+  }
+  *known = true;
   std::lock_guard<std::mutex> g(pol_mu_);
-  policy_cache_[bucket] = {now + 1.0, found};  // the gateway's 1 s policy cache
-  return found;
+  policy_cache_[bucket] = {now + 1.0, pol};  // the gateway's 1 s policy cache
+  return pol;
 }
 
 void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int status) {

@@ -31,12 +31,14 @@
 #include <cstdint>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "client_fast.h"
+#include "s3_policy.h"
 #include "io_pool.h"
 
 namespace dfs {
@@ -59,6 +61,7 @@ struct S3FrontStats {
   uint64_t connections = 0, requests = 0, native = 0, proxied = 0;
   uint64_t puts = 0, parts = 0, gets = 0, range_gets = 0, heads = 0, mpu_gets = 0;
   uint64_t bytes_in = 0, bytes_out = 0, auth_native = 0, audit_sent = 0, audit_dropped = 0;
+  uint64_t policy_native = 0;  // requests on a bucket with a policy, evaluated here and served natively
   std::map<std::string, uint64_t> by_status;  // "METHOD status" -> count (native requests)
   std::map<std::string, uint64_t> proxy_reasons;
   // native GET/Range GET phases, summed microseconds: metadata stat, block read into the
@@ -89,7 +92,10 @@ class S3Front {
   bool native_get(Conn* c, Req& r, const std::string& path, bool head);
   bool native_mpu_get(Conn* c, Req& r, const std::string& path, const std::string& marker_meta);
   int verify_auth(Req& r, std::string* user);  // 1 ok, 0 hand over
-  bool bucket_has_policy(const std::string& bucket);
+  // The bucket's policy: *known = false when it could not be read (the request is handed
+  // over); a null pointer when the bucket has none (or an unparsable one, which the gateway
+  // ignores too).
+  std::shared_ptr<const s3policy::BucketPolicy> bucket_policy(const std::string& bucket, bool* known);
   void audit(const Conn* c, const Req& r, const std::string& user, int status);
   void count(const Req& r, int status);
   int backend_conn();
@@ -111,7 +117,8 @@ class S3Front {
   std::mutex be_mu_;
   std::vector<int> be_idle_;
   std::mutex pol_mu_;
-  std::map<std::string, std::pair<double, bool>> policy_cache_;  // bucket -> (expiry, has policy)
+  // bucket -> (expiry, policy or null); the gateway's 1 s policy cache
+  std::map<std::string, std::pair<double, std::shared_ptr<const s3policy::BucketPolicy>>> policy_cache_;
   std::mutex key_mu_;
   std::map<std::string, std::string> key_cache_;  // date -> signing key (the single static key)
   IoPool pool_{4};

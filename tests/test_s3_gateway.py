@@ -795,6 +795,32 @@ def test_native_front_serves_object_data(gw, front):
     assert "s3_native_requests_total" in m and "s3_requests_total" in m
 
 
+def test_native_front_evaluates_bucket_policies(authgw, front):
+    """A bucket with a policy stays on the native path: the front evaluates the policy itself
+    (csrc/s3_policy.cpp) and hands over only the requests it denies, which the gateway answers
+    with 403 AccessDenied as before."""
+    if front != "native":
+        pytest.skip("native front end only")
+    g = authgw
+    assert signed("PUT", g, "/polnat").status_code == 200
+    for k in ("public", "secret-1"):
+        assert signed("PUT", g, f"/polnat/{k}", b"v-" + k.encode()).status_code == 200
+    pol = {"Version": "2012-10-17", "Statement": [
+        {"Effect": "Deny", "Principal": "*", "Action": "s3:GetObject", "Resource": "arn:dfs:s3:::polnat/secret*"},
+        {"Effect": "Allow", "Principal": {"AWS": ["arn:dfs:iam:::role/*"]}, "Action": "s3:*"}]}
+    assert signed("PUT", g, "/polnat", json.dumps(pol).encode(), query=[("policy", "")]).status_code == 204
+    time.sleep(1.1)  # the front's 1 s policy cache
+    s0 = g.front.stats()
+    assert signed("GET", g, "/polnat/public").content == b"v-public"
+    assert signed("PUT", g, "/polnat/public", b"v2").status_code == 200
+    r = signed("GET", g, "/polnat/secret-1")
+    assert r.status_code == 403 and b"AccessDenied" in r.content
+    s1 = g.front.stats()
+    assert s1["policy_native"] - s0["policy_native"] >= 2
+    assert s1["proxy_reasons"].get("bucket-policy-deny", 0) - s0["proxy_reasons"].get("bucket-policy-deny", 0) == 1
+    assert signed("DELETE", g, "/polnat", query=[("policy", "")]).status_code == 204
+
+
 def test_native_front_auth_and_audit(authgw, front):
     """Signed requests with the static key are verified in C++ (csrc/sigv4.cpp) and audited
     into the same hash chain; a bad signature is handed to Python, which answers 403."""
