@@ -673,7 +673,11 @@ void bind_meta(py::module_& m) {
                                                     const std::string& payload, std::string* out) -> int {
                if (path.compare(0, kPrefix.size(), kPrefix) == 0) {
                  std::string method = path.substr(kPrefix.size());
-                 if (core->native_method(method)) return core->handle(method, payload, out);
+                 if (core->native_method(method)) {
+                   int code = core->handle(method, payload, out);
+                   if (code != MasterCore::kDecline) return code;
+                   out->clear();
+                 }
                }
                // everything else runs the Python service handler on its event loop
                py::gil_scoped_acquire g;
@@ -727,8 +731,10 @@ void bind_meta(py::module_& m) {
                    RequestScope scope(c.request_id);
                    GrpcReply r;
                    r.status = core->handle(method, c.message, &r.message);
-                   self->native_calls++;
-                   return r;
+                   if (r.status != MasterCore::kDecline) {
+                     self->native_calls++;
+                     return r;
+                   }
                  }
                }
                self->fallback_calls++;

@@ -1093,7 +1093,7 @@ std::string MasterCore::new_uuid() {
 // ---------------------------------------------------------------- handlers
 bool MasterCore::native_method(const std::string& m) const {
   return m == "GetFileInfo" || m == "CreateFile" || m == "AllocateBlock" || m == "CompleteFile" ||
-         m == "ListFiles" || m == "DeleteFile" || m == "GetBlockLocations";
+         m == "ListFiles" || m == "DeleteFile" || m == "GetBlockLocations" || m == "Rename";
 }
 
 int MasterCore::handle(const std::string& method, const std::string& req, std::string* out) {
@@ -1104,6 +1104,7 @@ int MasterCore::handle(const std::string& method, const std::string& req, std::s
     if (method == "AllocateBlock") return allocate_block(req, out);
     if (method == "ListFiles") return list_files(req, out);
     if (method == "DeleteFile") return delete_file(req, out);
+    if (method == "Rename") return rename(req, out);
     if (method == "GetBlockLocations") return get_block_locations(req, out);
   } catch (const std::exception& e) {
     *out = e.what();
@@ -1384,6 +1385,51 @@ int MasterCore::delete_file(const std::string& raw, std::string* out) {
         queue_gc(j["blocks"]);
         resp.success = true;
       }
+    }
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+// Same-shard Rename (reference master.rs rename, the local case): one Raft entry whose apply
+// decides in log order; a rename whose destination another shard owns is declined to the
+// Python coordinator (2PC with presumed abort, master/service.py).
+int MasterCore::rename(const std::string& raw, std::string* out) {
+  pb::RenameRequest r;
+  if (!r.decode(raw)) return (*out = "malformed RenameRequest", INTERNAL);
+  record_request(r.source_path);
+  int c;
+  if ((c = check_ownership(r.source_path, out)) != OK) return c;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (safe_mode_) return (*out = kSafeModeMsg, UNAVAILABLE);
+    if (have_map_) {
+      std::string s = shard_map_.get_shard(r.source_path), d = shard_map_.get_shard(r.dest_path);
+      if ((s.empty() ? shard_id_ : s) != (d.empty() ? shard_id_ : d)) return kDecline;
+    }
+  }
+  if (!wait_unlocked(r.source_path, 5000, out) || !wait_unlocked(r.dest_path, 5000, out)) return UNAVAILABLE;
+  pb::RenameResponse resp;
+  bool exists;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    exists = visible(r.source_path) != nullptr;
+  }
+  if (!exists) {
+    resp.error_message = "Source file not found: " + r.source_path;
+  } else {
+    Result res = propose_unlocked("RenameFile", obj({{"source_path", r.source_path}, {"dest_path", r.dest_path}}));
+    if (res.code == 1) {
+      resp.error_message = "Not Leader";
+      resp.leader_hint = res.payload;
+    } else if (res.code != 0) {
+      return (*out = res.payload, res.code == 3 ? UNAVAILABLE : INTERNAL);
+    } else {
+      Json j = Json::parse(res.payload);
+      const Json& e = j["error"];
+      if (e.is_string() && !e.as_string().empty()) resp.error_message = e.as_string();
+      else resp.success = true;
     }
   }
   out->clear();

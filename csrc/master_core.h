@@ -71,7 +71,10 @@ class MasterCore : public raft::StateMachine {
   void restore(const std::string& state) override;
 
   // Hot RPCs: `method` is the bare MasterService method name. Returns a gRPC status code;
-  // *out holds the serialized response (OK) or the status message.
+  // *out holds the serialized response (OK) or the status message, or kDecline: the request
+  // is one this core does not serve (a cross-shard Rename, which is the Python
+  // coordinator's 2PC) and goes to the fallback handler unchanged.
+  static constexpr int kDecline = -100;
   bool native_method(const std::string& method) const;
   int handle(const std::string& method, const std::string& req, std::string* out);
 
@@ -173,6 +176,7 @@ class MasterCore : public raft::StateMachine {
   int complete_file(const std::string& req, std::string* out);
   int list_files(const std::string& req, std::string* out);
   int delete_file(const std::string& req, std::string* out);
+  int rename(const std::string& req, std::string* out);
   int get_block_locations(const std::string& req, std::string* out);
 
   // state machine helpers (mu_ held)

@@ -415,6 +415,29 @@ def test_handlers_guards_redirect_safe_mode_and_ec_shortage(master):
     assert code == 5 and msg == "File not found"
 
 
+def test_native_same_shard_rename_and_cross_shard_decline(master):
+    """Rename on the native handlers: a rename inside this shard is one Raft entry decided in
+    log order (missing source, taken destination); a destination another shard owns is
+    declined (kDecline = -100) so the request reaches the Python 2PC coordinator unchanged."""
+    st, call = master
+    ingest(st, file_with("/x/a", "ba", ["cs0:1"]), file_with("/x/taken", "bt", ["cs0:1"]))
+    code, r = call("Rename", pb.RenameRequest(source_path="/x/a", dest_path="/x/b"), pb.RenameResponse)
+    assert code == 0 and r.success
+    assert "/x/b" in st.files and "/x/a" not in st.files and st.files["/x/b"].blocks[0].block_id == "ba"
+    code, r = call("Rename", pb.RenameRequest(source_path="/x/a", dest_path="/x/c"), pb.RenameResponse)
+    assert code == 0 and not r.success and r.error_message == "Source file not found: /x/a"
+    code, r = call("Rename", pb.RenameRequest(source_path="/x/b", dest_path="/x/taken"), pb.RenameResponse)
+    assert code == 0 and not r.success and r.error_message == "Destination file already exists: /x/taken"
+    m = ShardMap.from_config({"s0": ["http://m0:1"], "s1": ["http://m1:1"]}, {"/m": "s1", "\U0010FFFF": "s0"})
+    st.core.set_shard_map(json.dumps(m.to_json()), "s0")
+    code, out = st.core.handle("Rename", pb.RenameRequest(source_path="/x/b", dest_path="/a/b").SerializeToString())
+    assert code == -100 and "/x/b" in st.files  # cross-shard: the coordinator's
+    code, msg = call("Rename", pb.RenameRequest(source_path="/a/q", dest_path="/x/q"), pb.RenameResponse)
+    assert code == 11 and msg == "REDIRECT:http://m1:1"  # the source's shard owns the request
+    code, r = call("Rename", pb.RenameRequest(source_path="/x/b", dest_path="/y/b"), pb.RenameResponse)
+    assert code == 0 and r.success and "/y/b" in st.files
+
+
 def test_list_files_with_metadata_in_one_call(master):
     """ListFiles{with_metadata} (extension 100): every visible file's metadata aligned with the
     paths, so an S3 listing page is one RPC per shard instead of one GetFileInfo per key; a
