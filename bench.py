@@ -281,6 +281,13 @@ def main():
             cp = procs.spawn(args, str(base_p / f"cs{rank}.log"), cs_env)
         cs_info = wait_file(ready, cp, 900, procs)
         my_cs = f"127.0.0.1:{cport}"
+        t_start = time.time()
+
+        def note(msg: str) -> None:
+            # progress on stderr outside the timed region (the JSON line stays alone on stdout)
+            print(f"[bench r{rank} +{time.time() - t_start:.1f}s] {msg}", file=sys.stderr, flush=True)
+
+        note("chunkserver up")
 
         from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_read, bench_write, make_payloads
         from rust_hadoop_generated_by_llm_amd.client.client import Client
@@ -303,6 +310,7 @@ def main():
                 raise TimeoutError("master never registered all chunkservers")
             time.sleep(0.1)
         pool.close()
+        note("master has every chunkserver")
         barrier()
 
         client = Client([my_master], local_chunkserver=my_cs)
@@ -320,7 +328,8 @@ def main():
             return ws, rs
 
         for w in range(a.warmup):
-            step(f"w{w}")
+            ws, rs = step(f"w{w}")
+            note(f"warm-up step {w}: write p50 {1e3 * ws._pct(50):.2f} ms, read p50 {1e3 * rs._pct(50):.2f} ms")
         use_cuda = torch.cuda.is_available() and not a.cpu
         if use_cuda:
             torch.cuda.set_device(gpu)
@@ -362,6 +371,7 @@ def main():
         if use_cuda:
             torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        note(f"{a.steps} timed steps in {elapsed:.3f} s")
         cpu1 = cpu_snapshot()
         host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
 
