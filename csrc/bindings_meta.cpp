@@ -659,6 +659,20 @@ void bind_meta(py::module_& m) {
       .def("apply", [](MasterCore& c, uint64_t idx, const std::string& cmd) {
         return c.apply({{idx, cmd}}).front();  // tests: apply one command outside Raft
       })
+      .def("enable_native_2pc", [](MasterCore& c, bool tls, const std::string& ca, const std::string& domain) {
+             std::shared_ptr<TlsContext> t;
+             if (tls) {
+               std::string err;
+               t = TlsContext::client(ca, domain, &err);
+               if (!t) throw std::runtime_error(err);
+             }
+             auto pool = std::make_shared<GrpcChannelPool>(5000, std::move(t));
+             c.enable_native_2pc([pool](const std::string& target, const std::string& path, const std::string& req,
+                                        int timeout_ms) {
+               return pool->call(target, path, req, t_request_id, timeout_ms);
+             });
+           }, py::arg("tls") = false, py::arg("ca") = "", py::arg("domain") = "")
+      .def("txn_stats", [](const MasterCore& c) { return c.txn_stats().dump(); })
       .def_property_readonly("requests", &MasterCore::requests);
 
   m.def("select_servers_rack_aware", [](MasterCore& c, size_t n, const std::string& preferred) {

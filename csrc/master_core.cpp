@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
 #include <future>
 #include <memory>
 
@@ -1093,7 +1094,9 @@ std::string MasterCore::new_uuid() {
 // ---------------------------------------------------------------- handlers
 bool MasterCore::native_method(const std::string& m) const {
   return m == "GetFileInfo" || m == "CreateFile" || m == "AllocateBlock" || m == "CompleteFile" ||
-         m == "ListFiles" || m == "DeleteFile" || m == "GetBlockLocations" || m == "Rename";
+         m == "ListFiles" || m == "DeleteFile" || m == "GetBlockLocations" || m == "Rename" ||
+         m == "PrepareTransaction" || m == "CommitTransaction" || m == "AbortTransaction" ||
+         m == "InquireTransaction";
 }
 
 int MasterCore::handle(const std::string& method, const std::string& req, std::string* out) {
@@ -1106,6 +1109,10 @@ int MasterCore::handle(const std::string& method, const std::string& req, std::s
     if (method == "DeleteFile") return delete_file(req, out);
     if (method == "Rename") return rename(req, out);
     if (method == "GetBlockLocations") return get_block_locations(req, out);
+    if (method == "PrepareTransaction") return prepare_transaction(req, out);
+    if (method == "CommitTransaction") return commit_transaction(req, out);
+    if (method == "AbortTransaction") return abort_transaction(req, out);
+    if (method == "InquireTransaction") return inquire_transaction(req, out);
   } catch (const std::exception& e) {
     *out = e.what();
     return INTERNAL;
@@ -1393,22 +1400,39 @@ int MasterCore::delete_file(const std::string& raw, std::string* out) {
 }
 
 // Same-shard Rename (reference master.rs rename, the local case): one Raft entry whose apply
-// decides in log order; a rename whose destination another shard owns is declined to the
-// Python coordinator (2PC with presumed abort, master/service.py).
+// decides in log order. A rename whose destination another shard owns runs the 2PC below
+// when a peer caller is configured (else it is declined to the Python coordinator,
+// master/service.py, which is also where more than kMaxCoordinators concurrent ones go).
 int MasterCore::rename(const std::string& raw, std::string* out) {
   pb::RenameRequest r;
   if (!r.decode(raw)) return (*out = "malformed RenameRequest", INTERNAL);
-  record_request(r.source_path);
   int c;
-  if ((c = check_ownership(r.source_path, out)) != OK) return c;
+  if ((c = check_ownership(r.source_path, out)) != OK) {
+    record_request(r.source_path);
+    return c;
+  }
+  std::string src_shard, dst_shard;
   {
     std::lock_guard<std::mutex> g(mu_);
     if (safe_mode_) return (*out = kSafeModeMsg, UNAVAILABLE);
     if (have_map_) {
       std::string s = shard_map_.get_shard(r.source_path), d = shard_map_.get_shard(r.dest_path);
-      if ((s.empty() ? shard_id_ : s) != (d.empty() ? shard_id_ : d)) return kDecline;
+      src_shard = s.empty() ? shard_id_ : s;
+      dst_shard = d.empty() ? shard_id_ : d;
     }
   }
+  if (src_shard != dst_shard) {
+    if (!peer_call_ || coordinators_.fetch_add(1) >= kMaxCoordinators) {
+      if (peer_call_) coordinators_--;
+      tx_declined_++;
+      return kDecline;  // the Python handler records the request
+    }
+    record_request(r.source_path);
+    int rc = rename_2pc(r, src_shard, dst_shard, out);
+    coordinators_--;
+    return rc;
+  }
+  record_request(r.source_path);
   if (!wait_unlocked(r.source_path, 5000, out) || !wait_unlocked(r.dest_path, 5000, out)) return UNAVAILABLE;
   pb::RenameResponse resp;
   bool exists;
@@ -1448,6 +1472,330 @@ int MasterCore::get_block_locations(const std::string& raw, std::string* out) {
     if (pb::BlockInfo* b = find_block_locked(r.block_id, nullptr)) {
       resp.locations = b->locations;
       resp.found = true;
+    }
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+// ---------------------------------------------------------------- cross-shard Rename (2PC)
+// Coordinator (the source shard's leader) and participant (the destination shard's leader)
+// of the reference's presumed-abort 2PC (master.rs:2562-2683, :2724-2900), same records and
+// the same recovery contract as the Python coordinator (master/service.py, tx_recovery in
+// master/background.py): Pending -> Prepared on the coordinator, PrepareTransaction pins the
+// destination on the participant, CommitTransaction creates it, the coordinator deletes the
+// source and marks the record Committed + acked. Differences: proposals whose outcomes do
+// not gate each other are queued back to back and ride one WAL group commit (record +
+// Prepared; source delete + Committed + acked; the participant's create + Committed), so a
+// rename costs 3 sequential Raft commits instead of 7.
+void MasterCore::enable_native_2pc(PeerCall call) { peer_call_ = std::move(call); }
+
+Json MasterCore::txn_stats() const {
+  return obj({{"native_started", tx_started_.load()},
+              {"native_committed", tx_committed_.load()},
+              {"native_aborted", tx_aborted_.load()},
+              {"native_pending", tx_pending_.load()},
+              {"declined", tx_declined_.load()},
+              {"enabled", static_cast<bool>(peer_call_)}});
+}
+
+namespace {
+
+Json master_cmd(const char* name, Json args) {
+  Json m = Json::object();
+  m.set(name, std::move(args));
+  return obj({{"Master", m}});
+}
+
+Json state_cmd(const std::string& tx, const char* st) {
+  return master_cmd("UpdateTransactionState", obj({{"tx_id", tx}, {"new_state", st}}));
+}
+
+Json op_json(const std::string& shard, const char* kind, Json body) {
+  Json op = Json::object();
+  op.set(kind, std::move(body));
+  return obj({{"shard_id", shard}, {"op_type", op}});
+}
+
+Json strings(const std::vector<std::string>& v) {
+  Json a = Json::array();
+  for (auto& x : v) a.push_back(x);
+  return a;
+}
+
+}  // namespace
+
+template <class Resp>
+bool MasterCore::call_peers(const std::vector<std::string>& peers, const std::string& method, const std::string& req) {
+  std::set<std::string> tried;
+  std::deque<std::string> queue(peers.begin(), peers.end());
+  while (!queue.empty()) {
+    std::string addr = queue.front();
+    queue.pop_front();
+    if (addr.empty() || !tried.insert(addr).second) continue;
+    GrpcResult g = peer_call_(addr, "/dfs.MasterService/" + method, req, 5000);
+    if (!g.transport_ok || g.status != 0) continue;  // unreachable, REDIRECT, ...: next peer
+    Resp resp;
+    if (!resp.decode(g.message)) continue;
+    if (resp.success) return true;
+    if (!resp.leader_hint.empty() && !tried.count(resp.leader_hint)) {
+      queue.push_front(resp.leader_hint);
+    } else if (!resp.error_message.empty() && resp.error_message != "Not Leader") {
+      return false;  // a decided refusal (destination exists / locked): no other peer helps
+    }
+  }
+  return false;
+}
+
+std::vector<MasterCore::Result> MasterCore::propose_all(const std::vector<Json>& cmds) {
+  std::vector<Result> out(cmds.size(), Result{1, ""});
+  raft::Node* node = node_.load();
+  if (!node) return out;
+  std::vector<std::future<Result>> futs;
+  for (auto& c : cmds) {
+    auto prom = std::make_shared<std::promise<Result>>();
+    futs.push_back(prom->get_future());
+    node->propose(c.dump(), [prom](int code, const std::string& payload) { prom->set_value(Result{code, payload}); });
+  }
+  auto deadline = Clock::now() + std::chrono::seconds(30);
+  for (size_t i = 0; i < futs.size(); ++i)
+    out[i] = futs[i].wait_until(deadline) == std::future_status::ready ? futs[i].get()
+                                                                       : Result{2, "proposal timed out"};
+  return out;
+}
+
+int MasterCore::rename_2pc(const pb::RenameRequest& r, const std::string& src_shard, const std::string& dst_shard,
+                           std::string* out) {
+  pb::RenameResponse resp;
+  auto reply = [&]() {
+    out->clear();
+    resp.encode(*out);
+    return static_cast<int>(OK);
+  };
+  const std::string& src = r.source_path;
+  const std::string& dst = r.dest_path;
+  if (!wait_unlocked(src, 5000, out)) return UNAVAILABLE;
+  pb::FileMetadata dmeta;
+  std::vector<std::string> dst_peers, my_peers;
+  std::string my_shard;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    const pb::FileMetadata* m = visible(src);
+    if (!m) {
+      resp.error_message = "Source file not found: " + src;
+      return reply();
+    }
+    dmeta = *m;
+    if (const auto* p = shard_map_.peers(dst_shard)) dst_peers = *p;
+    if (const auto* p = shard_map_.peers(shard_id_)) my_peers = *p;
+    my_shard = shard_id_;
+  }
+  dmeta.path = dst;
+  const std::string tx = new_uuid();
+  tx_started_++;
+  Json ops = Json::array();
+  ops.push_back(op_json(src_shard, "Delete", obj({{"path", src}})));
+  ops.push_back(op_json(dst_shard, "Create", obj({{"path", dst}, {"metadata", file_json(dmeta)}})));
+  Json rec = obj({{"tx_id", tx},
+                  {"tx_type", obj({{"Rename", obj({{"source_path", src}, {"dest_path", dst}})}})},
+                  {"state", "Pending"},
+                  {"timestamp", now_ms()},
+                  {"participants", strings({src_shard, dst_shard})},
+                  {"operations", ops},
+                  {"coordinator_shard", src_shard},
+                  {"participant_acked", false},
+                  {"inquiry_count", 0}});
+  auto abort_all = [&]() {
+    pb::AbortTransactionRequest a;
+    a.tx_id = tx;
+    call_peers<pb::AbortTransactionResponse>(dst_peers, "AbortTransaction", a.str());
+    propose(state_cmd(tx, "Aborted"));
+    tx_aborted_++;
+  };
+  // record (Pending) and Prepared back to back: a rejected record makes the update a no-op
+  std::vector<Result> rs = propose_all({master_cmd("CreateTransactionRecord", obj({{"record", rec}})),
+                                        state_cmd(tx, "Prepared")});
+  if (rs[0].code == 1) {
+    resp.error_message = "Not Leader";
+    resp.leader_hint = rs[0].payload;
+    return reply();
+  }
+  if (rs[0].code != 0) return (*out = rs[0].payload, INTERNAL);
+  const Json parsed = Json::parse(rs[0].payload);
+  const Json& conflict = parsed["conflict"];
+  if (conflict.is_string() && !conflict.as_string().empty()) {
+    resp.error_message = conflict.as_string();
+    return reply();
+  }
+  if (rs[1].code != 0) {
+    abort_all();
+    resp.error_message = "Internal error: Raft commit failed";
+    return reply();
+  }
+  pb::PrepareTransactionRequest prep;
+  prep.tx_id = tx;
+  prep.operation_type = "CREATE";
+  prep.path = dst;
+  prep.metadata = dmeta;
+  prep.has_metadata = true;
+  prep.coordinator_shard = my_shard;
+  prep.coordinator_peers = my_peers;
+  if (!call_peers<pb::PrepareTransactionResponse>(dst_peers, "PrepareTransaction", prep.str())) {
+    abort_all();
+    resp.error_message = "Cross-shard prepare failed";
+    return reply();
+  }
+  const char* drop = std::getenv("DFS_DEBUG_2PC_DROP_COMMIT");
+  pb::CommitTransactionRequest com;
+  com.tx_id = tx;
+  if ((drop && std::string(drop) == "1") ||
+      !call_peers<pb::CommitTransactionResponse>(dst_peers, "CommitTransaction", com.str())) {
+    // the record stays Prepared: tx_recovery (background) re-drives the commit
+    tx_pending_++;
+    resp.error_message = "Cross-shard commit pending, will be retried";
+    return reply();
+  }
+  rs = propose_all({master_cmd("ApplyTransactionOperation",
+                               obj({{"tx_id", tx}, {"operation", op_json(src_shard, "Delete", obj({{"path", src}}))}})),
+                    state_cmd(tx, "Committed"), master_cmd("SetParticipantAcked", obj({{"tx_id", tx}}))});
+  for (auto& x : rs)
+    if (x.code != 0) std::fprintf(stderr, "dfs master: tx %s: coordinator finish failed: %s\n", tx.c_str(),
+                                  x.payload.c_str());
+  tx_committed_++;
+  resp.success = true;
+  return reply();
+}
+
+int MasterCore::prepare_transaction(const std::string& raw, std::string* out) {
+  pb::PrepareTransactionRequest r;
+  if (!r.decode(raw)) return (*out = "malformed PrepareTransactionRequest", INTERNAL);
+  pb::PrepareTransactionResponse resp;
+  auto reply = [&]() {
+    out->clear();
+    resp.encode(*out);
+    return static_cast<int>(OK);
+  };
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (tx_records_.count(r.tx_id)) {  // a retried prepare
+      resp.success = true;
+      return reply();
+    }
+  }
+  int c;
+  if ((c = check_ownership(r.path, out)) != OK) return c;
+  std::string err;
+  if (!wait_unlocked(r.path, 1000, &err)) {
+    resp.error_message = "Destination is locked by another transaction: " + r.path;
+    return reply();
+  }
+  std::string me;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (files_.count(r.path)) {
+      resp.error_message = "Destination file already exists: " + r.path;
+      return reply();
+    }
+    me = shard_id_;
+  }
+  Json ops = Json::array();
+  ops.push_back(op_json(me, "Create", obj({{"path", r.path}, {"metadata", file_json(r.metadata)}})));
+  Json rec = obj({{"tx_id", r.tx_id},
+                  {"tx_type", obj({{"Rename", obj({{"source_path", ""}, {"dest_path", r.path}})}})},
+                  {"state", "Prepared"},
+                  {"timestamp", now_ms()},
+                  {"participants", strings({r.coordinator_shard, me})},
+                  {"operations", ops},
+                  {"coordinator_shard", r.coordinator_shard},
+                  {"participant_acked", false},
+                  {"inquiry_count", 0},
+                  {"coordinator_peers", strings(r.coordinator_peers)}});
+  Result res = propose(master_cmd("CreateTransactionRecord", obj({{"record", rec}})));
+  if (res.code == 1) {
+    resp.error_message = "Not Leader";
+    resp.leader_hint = res.payload;
+    return reply();
+  }
+  if (res.code != 0) return (*out = res.payload, INTERNAL);
+  const Json parsed = Json::parse(res.payload);
+  const Json& conflict = parsed["conflict"];
+  if (conflict.is_string() && !conflict.as_string().empty()) {
+    resp.error_message = conflict.as_string();
+    return reply();
+  }
+  resp.success = true;
+  return reply();
+}
+
+int MasterCore::commit_transaction(const std::string& raw, std::string* out) {
+  pb::CommitTransactionRequest r;
+  if (!r.decode(raw)) return (*out = "malformed CommitTransactionRequest", INTERNAL);
+  pb::CommitTransactionResponse resp;
+  auto reply = [&]() {
+    out->clear();
+    resp.encode(*out);
+    return static_cast<int>(OK);
+  };
+  Json op;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = tx_records_.find(r.tx_id);
+    if (it != tx_records_.end() && it->second["state"].str() == "Committed") {
+      resp.success = true;
+      return reply();
+    }
+    if (it == tx_records_.end() || !it->second["operations"].size()) {
+      resp.error_message = "Transaction not found: " + r.tx_id;
+      return reply();
+    }
+    op = it->second["operations"][0];
+  }
+  std::vector<Result> rs =
+      propose_all({master_cmd("ApplyTransactionOperation", obj({{"tx_id", r.tx_id}, {"operation", op}})),
+                   state_cmd(r.tx_id, "Committed")});
+  if (rs[0].code == 1) {
+    resp.error_message = "Not Leader";
+    resp.leader_hint = rs[0].payload;
+    return reply();
+  }
+  if (rs[0].code != 0) return (*out = rs[0].payload, INTERNAL);
+  resp.success = true;
+  return reply();
+}
+
+int MasterCore::abort_transaction(const std::string& raw, std::string* out) {
+  pb::AbortTransactionRequest r;
+  if (!r.decode(raw)) return (*out = "malformed AbortTransactionRequest", INTERNAL);
+  pb::AbortTransactionResponse resp;
+  Result res = propose(state_cmd(r.tx_id, "Aborted"));
+  if (res.code == 1) {
+    resp.error_message = "Not Leader";
+    resp.leader_hint = res.payload;
+  } else if (res.code != 0) {
+    return (*out = res.payload, INTERNAL);
+  } else {
+    resp.success = true;
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::inquire_transaction(const std::string& raw, std::string* out) {
+  pb::InquireTransactionRequest r;
+  if (!r.decode(raw)) return (*out = "malformed InquireTransactionRequest", INTERNAL);
+  int c;
+  if ((c = read_index(out)) != OK) return c;
+  pb::InquireTransactionResponse resp;
+  resp.status = "UNKNOWN";
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = tx_records_.find(r.tx_id);
+    if (it != tx_records_.end()) {
+      const std::string& st = it->second["state"].str();
+      if (st == "Committed") resp.status = "COMMITTED";
+      else if (st == "Aborted") resp.status = "ABORTED";
     }
   }
   out->clear();

@@ -23,6 +23,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <random>
@@ -33,6 +34,7 @@
 #include <vector>
 
 #include "dfs_pb.h"
+#include "grpc_client.h"
 #include "json.h"
 #include "raft.h"
 #include "shard_map.h"
@@ -144,6 +146,15 @@ class MasterCore : public raft::StateMachine {
   // (encoded FileMetadata, only those — the caller decodes a handful, not the namespace).
   std::vector<std::string> ec_candidates(uint64_t now_ms, uint64_t ec_ms) const;
 
+  // Cross-shard Rename as a native 2PC coordinator (reference master.rs:2562-2683 rename,
+  // :2724-2900 participant handlers). `call` is a unary gRPC call to a peer master (the
+  // bindings pass a GrpcChannelPool, tests wire two cores together); without it a
+  // cross-shard Rename is declined to the Python coordinator.
+  using PeerCall = std::function<GrpcResult(const std::string& target, const std::string& path,
+                                            const std::string& req, int timeout_ms)>;
+  void enable_native_2pc(PeerCall call);
+  Json txn_stats() const;
+
   // Raft peer RPC (vote / append / snapshot / timeout_now, JSON) for the attached node, as
   // served by the native gRPC server on /dfs.RaftPeer/<kind>.
   int raft_rpc(const std::string& kind, const std::string& body, std::string* out);
@@ -158,6 +169,7 @@ class MasterCore : public raft::StateMachine {
   };
   Result propose(const Json& cmd);
   Result propose_unlocked(const std::string& name, const Json& args);  // waits out tx pins
+  std::vector<Result> propose_all(const std::vector<Json>& cmds);       // queued back to back
   int read_index(std::string* err);
   bool wait_unlocked(const std::string& path, int timeout_ms, std::string* err);
   int check_ownership(const std::string& path, std::string* err) const;
@@ -178,6 +190,16 @@ class MasterCore : public raft::StateMachine {
   int delete_file(const std::string& req, std::string* out);
   int rename(const std::string& req, std::string* out);
   int get_block_locations(const std::string& req, std::string* out);
+  int rename_2pc(const pb::RenameRequest& r, const std::string& src_shard, const std::string& dst_shard,
+                 std::string* out);
+  int prepare_transaction(const std::string& req, std::string* out);
+  int commit_transaction(const std::string& req, std::string* out);
+  int abort_transaction(const std::string& req, std::string* out);
+  int inquire_transaction(const std::string& req, std::string* out);
+  // Unary call to the leader of a peer shard: each address in turn, following leader hints;
+  // true when a reply says success. `decode` parses (success, error_message, leader_hint).
+  template <class Resp>
+  bool call_peers(const std::vector<std::string>& peers, const std::string& method, const std::string& req);
 
   // state machine helpers (mu_ held)
   Json apply_one(const std::string& name, const Json& a);
@@ -214,6 +236,13 @@ class MasterCore : public raft::StateMachine {
   bool access_stats_ = true;
   int access_flush_ms_ = 1000;
   std::mt19937_64 rng_;
+
+  // native 2PC coordinator (enable_native_2pc); at most kMaxCoordinators renames hold an
+  // RPC worker while they wait on the peer shard, the rest go to the async Python coordinator
+  static constexpr int kMaxCoordinators = 8;
+  PeerCall peer_call_;  // set once before serving
+  std::atomic<int> coordinators_{0};
+  std::atomic<uint64_t> tx_started_{0}, tx_committed_{0}, tx_aborted_{0}, tx_pending_{0}, tx_declined_{0};
 
   std::atomic<raft::Node*> node_{nullptr};
   std::atomic<uint64_t> requests_{0};

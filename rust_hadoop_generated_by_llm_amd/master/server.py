@@ -82,6 +82,11 @@ class MasterProcess:
                              backup_bucket=args.backup_bucket, native_sm=self.state.core,
                              peer_tls=(args.ca_cert or "", args.domain_name or "") if args.tls_cert else None)
         self.state.core.attach(self.raft._core)
+        if os.environ.get("DFS_NATIVE_2PC", "1") == "1":
+            # cross-shard Rename coordinated in C++ (MasterCore::rename_2pc) over the native
+            # gRPC client; DFS_NATIVE_2PC=0 keeps the Python coordinator (master/service.py)
+            self.state.core.enable_native_2pc(bool(args.ca_cert), args.ca_cert or "",
+                                              args.domain_name or "")
         self.state.enter_safe_mode()
         self.config_servers = [with_scheme(c) for c in args.config_servers.split(",") if c.strip()]
         if self.config_servers:
@@ -116,6 +121,13 @@ class MasterProcess:
         self.metrics.gauge("dfs_master_chunkservers", "live chunkservers", fn=lambda: len(self.state.chunk_servers))
         self.metrics.gauge("dfs_master_native_requests", "requests served by the native handlers",
                            fn=lambda: self.state.core.requests)
+        for key, help_ in (("native_started", "cross-shard renames coordinated natively"),
+                           ("native_committed", "native 2PC renames committed"),
+                           ("native_aborted", "native 2PC renames aborted"),
+                           ("native_pending", "native 2PC renames left to tx recovery"),
+                           ("declined", "cross-shard renames handed to the Python coordinator")):
+            self.metrics.gauge(f"dfs_master_tx_{key}", help_,
+                               fn=lambda k=key: json.loads(self.state.core.txn_stats())[k])
         self._native_grpc = None
         for key, help_ in (("native_grpc_calls", "gRPC calls served by the native HTTP/2 server"),
                            ("native_grpc_fallback", "native gRPC calls handed to the Python handlers"),

@@ -40,7 +40,17 @@ def _ensure_built() -> None:
             try:
                 import build_native  # noqa: PLC0415
 
-                build_native.build()
+                # the extension and tools only: the sanitizer builds are the native unit
+                # tests' business (tests/test_native_unit.py builds them on demand)
+                saved = os.environ.get("DFS_BUILD_SANITIZERS")
+                os.environ["DFS_BUILD_SANITIZERS"] = "0"
+                try:
+                    build_native.build()
+                finally:
+                    if saved is None:
+                        os.environ.pop("DFS_BUILD_SANITIZERS", None)
+                    else:
+                        os.environ["DFS_BUILD_SANITIZERS"] = saved
             finally:
                 sys.path.pop(0)
 

@@ -183,6 +183,18 @@ def test_replica_failover_and_ec_degraded_read():
         c.close()
 
 
+def _master_metric_sum(cl, name: str) -> float:
+    total = 0.0
+    for http in cl.master_http.values():
+        try:
+            text = urllib.request.urlopen(f"{http}/metrics", timeout=5).read().decode()
+        except OSError:  # a master the test killed
+            continue
+        total += sum(float(ln.split()[1]) for ln in text.splitlines()
+                     if ln and not ln.startswith("#") and ln.split()[0] == name)
+    return total
+
+
 def test_cross_shard_rename_and_listing():
     with LocalCluster(n_chunkservers=3, shards=2, fsync=False) as cl:
         c = cl.client()
@@ -201,6 +213,9 @@ def test_cross_shard_rename_and_listing():
         run_workload(c, hist, ops=20, clients=3, key_space=4, rename_ratio=0.4, seed=7)
         assert checker.check_file(hist) == []
         c.close()
+        # the 2PC ran in C++ (MasterCore::rename_2pc), not in the Python coordinator
+        assert _master_metric_sum(cl, "dfs_master_tx_native_committed") >= 1
+        assert _master_metric_sum(cl, "dfs_master_tx_declined") == 0
 
 
 def test_master_raft_failover():
@@ -540,6 +555,7 @@ def test_2pc_abort_when_destination_shard_is_down():
         c.rename_file("/a/src", "/a/src2")  # not pinned by a leftover transaction lock
         assert c.get_file_content("/a/src2") == b"stay"
         c.close()
+        assert _master_metric_sum(cl, "dfs_master_tx_native_aborted") >= 1
 
 
 def test_2pc_recovery_finishes_commit_after_coordinator_loss():
@@ -561,6 +577,20 @@ def test_2pc_recovery_finishes_commit_after_coordinator_loss():
         assert c.get_file_content("/z/tx") == b"moving"
         assert not c.exists("/a/tx")
         c.close()
+        assert _master_metric_sum(cl, "dfs_master_tx_native_pending") >= 1
+
+
+def test_2pc_python_coordinator_still_serves():
+    """DFS_NATIVE_2PC=0 keeps the Python coordinator (master/service.py) as the A/B path;
+    both coordinators write the same records, so its renames still commit."""
+    with LocalCluster(n_chunkservers=2, shards=2, fsync=False, env={"DFS_NATIVE_2PC": "0"}) as cl:
+        c = cl.client()
+        c.create_file_from_buffer(b"py", "/a/py")
+        c.rename_file("/a/py", "/z/py")
+        assert c.get_file_content("/z/py") == b"py" and not c.exists("/a/py")
+        c.close()
+        assert _master_metric_sum(cl, "dfs_master_tx_declined") >= 1
+        assert _master_metric_sum(cl, "dfs_master_tx_native_started") == 0
 
 
 def test_idle_shard_merges_and_becomes_standby():
