@@ -249,7 +249,10 @@ def main():
         # ---------------- chunkserver for this rank's GPU
         cport, chttp = free_port(), free_port()
         ready = str(base_p / f"cs{rank}.ready")
-        ndev = torch.cuda.device_count() if not a.cpu else 0  # does not initialise HIP
+        # torch.cuda.device_count() goes through amdsmi, which keeps the DRM render nodes open:
+        # asked on every rank, every rank would count as a GPU process (a 1-GPU box allows 16,
+        # and an 8-rank rehearsal has 8 chunkservers already). One node: rank 0 asks for all.
+        ndev = bcast(torch.cuda.device_count() if rank == 0 and not a.cpu else None) or 0
         gpu = -1 if a.cpu else local_rank % max(1, ndev)
         shared_gpu = (not a.cpu) and ndev < n  # rehearsal mode: several ranks on one GPU
         args = [f"{PKG}.chunkserver.server", "--addr", f"127.0.0.1:{cport}",
@@ -330,7 +333,10 @@ def main():
         for w in range(a.warmup):
             ws, rs = step(f"w{w}")
             note(f"warm-up step {w}: write p50 {1e3 * ws._pct(50):.2f} ms, read p50 {1e3 * rs._pct(50):.2f} ms")
-        use_cuda = torch.cuda.is_available() and not a.cpu
+        # ranks that share one GPU (1-GPU rehearsals) leave the device to their chunkservers:
+        # only local rank 0 brackets the timed region with a device sync there, so an 8-rank
+        # rehearsal keeps 9 GPU processes on the card, not 16
+        use_cuda = not a.cpu and ndev > 0 and (not shared_gpu or local_rank == 0) and torch.cuda.is_available()
         if use_cuda:
             torch.cuda.set_device(gpu)
             torch.cuda.synchronize()

@@ -16,6 +16,7 @@
 #include <set>
 #include <thread>
 
+#include "audit_log.h"
 #include "client_fast.h"
 #include "client_remote.h"
 #include "grpc_client.h"
@@ -790,6 +791,28 @@ void bind_meta(py::module_& m) {
       });
 
   // ---------------- native S3 front end (csrc/s3_front.cpp)
+  // S3 audit log writer (C56): records from the gateway and, through the ingest socket, from
+  // the gateway's other workers and the native front, in one HMAC chain
+  py::class_<AuditLog>(m, "AuditLog")
+      .def(py::init<std::string, int, int, std::string, size_t, int, bool>(), py::arg("path"),
+           py::arg("retention_days") = 30, py::arg("batch_size") = 100, py::arg("hmac_secret") = "",
+           py::arg("capacity") = 10000, py::arg("flush_interval_ms") = 5000, py::arg("sync") = false)
+      .def("log", &AuditLog::log, py::call_guard<py::gil_scoped_release>())
+      .def("start_ingest", &AuditLog::start_ingest)
+      .def("flush", &AuditLog::flush, py::arg("timeout_ms") = 10000, py::call_guard<py::gil_scoped_release>())
+      .def("close", &AuditLog::close, py::call_guard<py::gil_scoped_release>())
+      .def("cleanup", &AuditLog::cleanup, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("head", &AuditLog::head)
+      .def("stats", [](const AuditLog& a) {
+        py::dict d;
+        d["total"] = a.total();
+        d["dropped"] = a.dropped();
+        d["flush_errors"] = a.flush_errors();
+        d["committed"] = a.committed();
+        d["ingested"] = a.ingested();
+        return d;
+      });
+
   py::class_<S3Front>(m, "S3Front")
       .def(py::init([](FastClient* fc, const std::string& host, int port, const std::string& backend, int workers,
                        bool auth_enabled, const std::string& region, const std::string& access_key,

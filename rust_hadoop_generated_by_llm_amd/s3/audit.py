@@ -38,7 +38,7 @@ import threading
 import time
 from datetime import datetime, timezone
 
-from ..utils.metrics import Registry
+from ..utils.metrics import Counter, Registry
 
 log = logging.getLogger("dfs.s3.audit")
 
@@ -220,7 +220,9 @@ def _in_range(ts: int, start_ms: int | None, end_ms: int | None) -> bool:
     return (start_ms is None or ts >= start_ms) and (end_ms is None or ts <= end_ms)
 
 
-class AuditLogger:
+class PyAuditLogger:
+    """The Python writer (DFS_AUDIT_NATIVE=0); AuditLogger is the native one by default."""
+
     def __init__(self, path: str, retention_days: int = 30, batch_size: int = 100, hmac_secret: str = "",
                  *, registry: Registry | None = None, flush_interval: float = 5.0, capacity: int = 10_000,
                  sync: bool = False):
@@ -239,6 +241,7 @@ class AuditLogger:
         self.committed_hash = last[1].get("record_hash") if last else None
         self.last_ts = last[0] if last else 0
         self._stop = threading.Event()
+        self._flush_req = threading.Event()  # flush(): commit what is queued now
         self._flushed = threading.Condition()
         self._pending = 0
         self._worker = threading.Thread(target=self._run, name="audit-logger", daemon=True)
@@ -296,9 +299,13 @@ class AuditLogger:
             except queue.Empty:
                 pass
             now = time.monotonic()
-            if len(batch) >= self.batch_size or (batch and now >= next_flush) or (batch and self._stop.is_set()):
+            forced = self._flush_req.is_set() and self.q.empty()
+            if len(batch) >= self.batch_size or (batch and (now >= next_flush or forced)) or \
+                    (batch and self._stop.is_set()):
                 self._commit(batch)
                 batch = []
+            if forced:
+                self._flush_req.clear()
             if now >= next_flush:
                 next_flush = now + self.flush_interval
             if now >= next_cleanup:
@@ -313,22 +320,90 @@ class AuditLogger:
     def flush(self, timeout: float = 10.0) -> bool:
         """Wait until every logged record is committed (tests, shutdown)."""
         deadline = time.monotonic() + timeout
-        saved = self.flush_interval
-        self.flush_interval = 0.0
-        try:
-            with self._flushed:
-                while self._pending > 0:
-                    left = deadline - time.monotonic()
-                    if left <= 0:
-                        return False
-                    self._flushed.wait(min(left, 0.1))
-            return True
-        finally:
-            self.flush_interval = saved
+        self._flush_req.set()
+        with self._flushed:
+            while self._pending > 0:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    return False
+                self._flushed.wait(min(left, 0.1))
+        return True
 
     def close(self) -> None:
         self._stop.set()
         self._worker.join(timeout=30)
+
+
+class _NativeCounter(Counter):
+    """A counter whose value lives in the native logger."""
+
+    def __init__(self, name: str, help_: str, fn):
+        super().__init__(name, help_)
+        self._fn = fn
+
+    def get(self, labels: dict | None = None) -> float:
+        return float(self._fn())
+
+    def render(self) -> list[str]:
+        with self._lock:
+            self._values[()] = float(self._fn())
+        return super().render()
+
+
+class NativeAuditLogger:
+    """Same contract as PyAuditLogger, written by ``csrc/audit_log.cpp``: the batching, the
+    HMAC chain, the segment/index appends and the datagram ingest of the other gateway workers
+    and the native S3 front all run in C++ threads (no interpreter lock on the record path)."""
+
+    def __init__(self, path: str, retention_days: int = 30, batch_size: int = 100, hmac_secret: str = "",
+                 *, registry: Registry | None = None, flush_interval: float = 5.0, capacity: int = 10_000,
+                 sync: bool = False):
+        from ..native import lib
+
+        self.store = SegmentStore(path)
+        self._n = lib.AuditLog(path, retention_days, batch_size, hmac_secret, capacity,
+                               max(1, int(flush_interval * 1000)), sync)
+        reg = registry or Registry()
+        stat = self._n.stats
+        self.m_total = reg.add(_NativeCounter("audit_log_total", "Total number of audit logs sent to the logger",
+                                              lambda: stat()["total"]))
+        self.m_dropped = reg.add(_NativeCounter("audit_log_dropped_total",
+                                                "Total number of audit logs dropped due to full buffer",
+                                                lambda: stat()["dropped"]))
+        self.m_flush_err = reg.add(_NativeCounter("audit_log_flush_errors_total",
+                                                  "Total number of audit log flush failures",
+                                                  lambda: stat()["flush_errors"]))
+
+    @property
+    def committed_hash(self) -> str | None:
+        return self._n.head or None
+
+    def log(self, rec: dict) -> None:
+        self._n.log(json.dumps(rec, separators=(",", ":"), ensure_ascii=False))
+
+    def start_ingest(self, sock) -> None:
+        """Records arriving as datagrams on `sock` (a bound SOCK_DGRAM socket) are logged by a
+        native thread."""
+        self._n.start_ingest(sock.fileno())
+
+    def stats(self) -> dict:
+        return self._n.stats()
+
+    def flush(self, timeout: float = 10.0) -> bool:
+        return self._n.flush(int(timeout * 1000))
+
+    def close(self) -> None:
+        self._n.close()
+
+
+def AuditLogger(*args, **kwargs):  # noqa: N802 - the reference's type name
+    """The audit writer: native (csrc/audit_log.cpp) unless DFS_AUDIT_NATIVE=0."""
+    if os.environ.get("DFS_AUDIT_NATIVE", "1") != "0":
+        try:
+            return NativeAuditLogger(*args, **kwargs)
+        except ImportError:  # no extension at all: the Python writer keeps the log
+            log.warning("native audit writer unavailable; using the Python one")
+    return PyAuditLogger(*args, **kwargs)
 
 
 # ---------------------------------------------------------------------------- reader

@@ -1263,7 +1263,11 @@ def main(argv: list[str] | None = None) -> int:
         sink = lambda reg: ForwardingAudit(ingest_path, reg)  # noqa: E731
     gw = build_gateway(cfg, audit_sink=sink)
     if worker_id == 0 and ingest is not None and gw.audit is not None:
-        threading.Thread(target=_audit_ingest, args=(ingest, gw.audit), name="audit-ingest", daemon=True).start()
+        if hasattr(gw.audit, "start_ingest"):  # native writer: a C++ thread receives the datagrams
+            gw.audit.start_ingest(ingest)
+        else:
+            threading.Thread(target=_audit_ingest, args=(ingest, gw.audit), name="audit-ingest",
+                             daemon=True).start()
     ssl_ctx = None
     if cfg.tls_cert and cfg.tls_key:
         ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)

@@ -65,7 +65,10 @@ class GatewayThread:
                 ingest = os.path.join(self._dir, "ingest.sock")
                 self._isock = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
                 self._isock.bind(ingest)
-                threading.Thread(target=_audit_ingest, args=(self._isock, gw.audit), daemon=True).start()
+                if hasattr(gw.audit, "start_ingest"):  # as s3/server.py main(): native ingest thread
+                    gw.audit.start_ingest(self._isock)
+                else:
+                    threading.Thread(target=_audit_ingest, args=(self._isock, gw.audit), daemon=True).start()
             cfg = gw.cfg
             self.front = lib.S3Front(gw.client._fast, "127.0.0.1", self.port, self.backend, workers=8,
                                      auth_enabled=cfg.auth_enabled, region=cfg.region,
