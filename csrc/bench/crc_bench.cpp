@@ -145,7 +145,7 @@ int main(int argc, char** argv) {
       const uint64_t n = mib << 20;
       if (n > total) continue;
       for (int rep = 0; rep < 2; ++rep)
-        for (int w : {0, 1}) {
+        for (int w : {0, 1, 2}) {
           set_crc_wide(w);
           Run r = bench_block(d, n, t, dmeta, dpart, s, n >= (256ull << 20) ? std::max(3, iters / 10) : iters, host);
           std::printf("%s\n  {\"bytes\": %llu, \"wide\": %d, \"rep\": %d, \"us\": %.2f, \"GBps\": %.1f, \"of_stream\": %.3f, "

@@ -551,7 +551,7 @@ static_assert(sizeof(MfmaWideLds) - offsetof(MfmaWideLds, sh4k) == sizeof(DevCrc
 // kWrite: the K1/K2 write form (slice words out, whole-block partials, nothing to verify),
 // with those checks resolved at compile time so the loop body has no uniform branches.
 template <int kGroups, bool kWrite>
-__global__ __launch_bounds__(kCrcWgThreads * kGroups) __attribute__((amdgpu_waves_per_eu(3, 3)))
+__global__ __launch_bounds__(kCrcWgThreads * kGroups) __attribute__((amdgpu_waves_per_eu(kGroups, kGroups)))
 void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   constexpr int kThreads = kCrcWgThreads * kGroups;
   __shared__ MfmaWideLds lt;
@@ -1215,22 +1215,28 @@ static int ring_for(uint64_t ntiles) {
 // One resident round: 3 workgroups per CU at 3 waves/SIMD (R = 2), 2 at 2 waves/SIMD.
 static uint64_t crc_grid_cap(int ring) { return ring > 2 ? 2 * 256 : kMaxGridCrc; }
 
-// K1/K2 as crc_tile_wide_kernel (one workgroup of kCrcWideGroups x 4 waves per CU): 0 = off,
-// 1 = on. DFS_CRC_WIDE overrides the default.
+// K1/K2 as crc_tile_wide_kernel (one workgroup of G x 4 waves per CU): 0 = off, 1 = G = 3
+// (3 waves/SIMD), 2 = G = 2 (2 waves/SIMD). DFS_CRC_WIDE overrides the default.
+// Why G = 2 can win although it halves the waves: the loop is matrix-pipe + VALU bound, so a
+// tile-iteration of a group costs ~G units on a CU, and a block of T tiles takes
+// ceil(T / (256 G)) iterations: 64 MiB = 4096 tiles is 6 x 3 = 18 units at G = 3 (runs of 5 or
+// 6: the CUs with 6 set the time) but 8 x 2 = 16 at G = 2 (every run exactly 8); every
+// power-of-two size divides evenly at G = 2.
 static std::atomic<int> g_crc_wide{-1};
-constexpr int kCrcWideGroups = kMaxGridCrc / 256;
 
-void set_crc_wide(int mode) { g_crc_wide.store(mode <= 0 ? 0 : 1); }
+void set_crc_wide(int mode) { g_crc_wide.store(mode <= 0 ? 0 : (mode >= 2 ? 2 : 1)); }
 
 int crc_wide_mode() {
   int v = g_crc_wide.load(std::memory_order_relaxed);
   if (v < 0) {
     const char* e = std::getenv("DFS_CRC_WIDE");
     v = e ? std::atoi(e) : kCrcWideDefault;
-    g_crc_wide.store(v = v <= 0 ? 0 : 1);
+    g_crc_wide.store(v = v <= 0 ? 0 : (v >= 2 ? 2 : 1));
   }
   return v;
 }
+
+static int crc_wide_groups() { return crc_wide_mode() == 2 ? 2 : kMaxGridCrc / 256; }
 
 DevCrcTables* upload_crc_tables(hipStream_t s) {
   static_assert(sizeof(DevCrcTables) % 16 == 0, "table image must be uint4-copyable");
@@ -1290,11 +1296,13 @@ int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
   }();
   uint64_t g = (ntiles + per - 1) / per;
   const int ring = ring_for(ntiles);
-  const uint64_t cap = crc_grid_cap(ring);
+  uint64_t cap = crc_grid_cap(ring);
+  const uint64_t G = crc_wide_groups();
+  if (ring == 2 && crc_wide_mode()) cap = 256 * G;  // one resident round of the wide kernel
   g = g < cap ? g : cap;
-  // the wide kernel runs kCrcWideGroups virtual workgroups per launched one (empty runs
-  // leave a zero partial and no verdict)
-  if (ring == 2 && crc_wide_mode() && g) g = (g + kCrcWideGroups - 1) / kCrcWideGroups * kCrcWideGroups;
+  // the wide kernel runs G virtual workgroups per launched one (empty runs leave a zero
+  // partial and no verdict)
+  if (ring == 2 && crc_wide_mode() && g) g = (g + G - 1) / G * G;
   if (g == 0 && has_tail) g = 1;
   return static_cast<int>(g);
 }
@@ -1304,12 +1312,17 @@ hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipSt
   switch (ring_for(a.ntiles)) {
     case 0: hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
     case 2:
-      if (crc_wide_mode() && grid % kCrcWideGroups == 0) {
-        const dim3 g(grid / kCrcWideGroups), b(kCrcWgThreads * kCrcWideGroups);
-        if (a.meta_out && !a.meta_expect && a.part_crc)
-          hipLaunchKernelGGL((crc_tile_wide_kernel<kCrcWideGroups, true>), g, b, 0, s, a, t);
-        else
-          hipLaunchKernelGGL((crc_tile_wide_kernel<kCrcWideGroups, false>), g, b, 0, s, a, t);
+      if (crc_wide_mode() && grid % crc_wide_groups() == 0) {
+        const int G = crc_wide_groups();
+        const dim3 g(grid / G), b(kCrcWgThreads * G);
+        const bool w = a.meta_out && !a.meta_expect && a.part_crc;
+        if (G == 2) {
+          if (w) hipLaunchKernelGGL((crc_tile_wide_kernel<2, true>), g, b, 0, s, a, t);
+          else hipLaunchKernelGGL((crc_tile_wide_kernel<2, false>), g, b, 0, s, a, t);
+        } else {
+          if (w) hipLaunchKernelGGL((crc_tile_wide_kernel<kMaxGridCrc / 256, true>), g, b, 0, s, a, t);
+          else hipLaunchKernelGGL((crc_tile_wide_kernel<kMaxGridCrc / 256, false>), g, b, 0, s, a, t);
+        }
       } else {
         hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
       }

@@ -48,11 +48,12 @@ def test_gpu_crc_matrix_core_kernel_below_the_dispatch_threshold(gstore, native,
         native.set_crc_lds_max_mib(16)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("n", [511, (1 << 20) + 13, (8 << 20) - 4096 + 7, (64 << 20) + 513, 300 << 20])
 def test_gpu_crc_wide_workgroups(gstore, native, mode, n):
-    """K1/K2 with one workgroup per CU (three 4-wave groups sharing the LDS image and the MFMA
-    basis, two-lookup combine) against zlib: whole-block CRC and every slice word, with tails."""
+    """K1/K2 with one workgroup per CU (three (mode 1) or two (mode 2) 4-wave groups sharing
+    the LDS image and the MFMA basis, two-lookup combine) against zlib: whole-block CRC and
+    every slice word, with tails."""
     saved = native.crc_wide_mode()
     native.set_crc_lds_max_mib(0)
     native.set_crc_wide(mode)
