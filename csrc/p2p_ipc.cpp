@@ -87,9 +87,23 @@ void st(T* p, T v) {
   __atomic_store_n(p, v, __ATOMIC_RELEASE);
 }
 
+// Receivers blocked in wait() sleep on landed_bell; the sender bumps it after publishing
+// `landed` (and every abort does), waking only when someone is registered as waiting.
+void landed_wake(IpcRing* r) {
+  __atomic_fetch_add(&r->landed_bell, 1u, __ATOMIC_SEQ_CST);
+  if (__atomic_load_n(&r->landed_waiters, __ATOMIC_SEQ_CST)) futex(&r->landed_bell, FUTEX_WAKE, INT_MAX, nullptr);
+}
+
 void ring_wake(IpcRing* r) {
   __atomic_fetch_add(&r->doorbell, 1u, __ATOMIC_SEQ_CST);
   futex(&r->doorbell, FUTEX_WAKE, INT_MAX, nullptr);
+  if (__atomic_load_n(&r->abort, __ATOMIC_SEQ_CST)) landed_wake(r);
+}
+
+// A send op's completion word (process-local): set, then wake a blocked wait().
+void finish_send(const std::shared_ptr<std::atomic<int>>& st, int v) {
+  st->store(v, std::memory_order_release);
+  ::syscall(SYS_futex, reinterpret_cast<uint32_t*>(st.get()), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
 }
 
 // One process's mapping of a channel ring, registered for device access (spin kernels).
@@ -435,6 +449,27 @@ class IpcTransport final : public P2PTransport {
     return ld(&rm->r->abort) ? -1 : 0;
   }
 
+  // Blocking completion for the host-driven mode: a send op sleeps on its completion word
+  // (the channel worker wakes it), a receive op on the ring's landed_bell (the peer's worker
+  // wakes it after publishing `landed`, or on abort). Spin-mode ops poll their event.
+  int wait(P2POp* op, int max_us) override {
+    int r = test(op);
+    if (r != 0 || spin_ || op->event) return r == 0 ? P2PTransport::wait(op, max_us) : r;
+    timespec ts{max_us / 1000000, static_cast<long>(max_us % 1000000) * 1000};
+    if (op->state) {
+      ::syscall(SYS_futex, reinterpret_cast<uint32_t*>(op->state.get()), FUTEX_WAIT_PRIVATE, 0u, &ts, nullptr, 0);
+      return test(op);
+    }
+    auto* rm = static_cast<RingMap*>(op->ctx.get());
+    if (!rm) return -1;
+    IpcRing* ring = rm->r;
+    __atomic_fetch_add(&ring->landed_waiters, 1u, __ATOMIC_SEQ_CST);
+    const uint32_t bell = __atomic_load_n(&ring->landed_bell, __ATOMIC_SEQ_CST);
+    if (test(op) == 0) futex(&ring->landed_bell, FUTEX_WAIT, bell, &ts);
+    __atomic_fetch_sub(&ring->landed_waiters, 1u, __ATOMIC_SEQ_CST);
+    return test(op);
+  }
+
   void release(P2POp* op) override {
     if (op->event) release_event(static_cast<hipEvent_t>(op->event));
     op->event = nullptr;
@@ -493,7 +528,7 @@ class IpcTransport final : public P2PTransport {
     }
     {
       std::lock_guard<std::mutex> q(l.qmu);
-      for (auto& it : l.pending) it.st->store(-1);
+      for (auto& it : l.pending) finish_send(it.st, -1);
       l.pending.clear();
     }
     for (hipStream_t s : {l.send_stream, l.recv_stream})
@@ -532,7 +567,7 @@ class IpcTransport final : public P2PTransport {
                       hipSuccess) ||
             !(ev = event()) || hipEventRecord(ev, l->send_stream) != hipSuccess) {
           if (ev) release_event(ev);
-          it.st->store(-1);
+          finish_send(it.st, -1);
           st(&r->abort, 1u);  // mismatched sizes or a failed copy end the channel (as RCCL would)
           ring_wake(r);
           dead = true;
@@ -549,10 +584,12 @@ class IpcTransport final : public P2PTransport {
         SendItem& it = inflight.front();
         if (q == hipSuccess) {
           st(&r->landed, it.seq + 1);
-          it.st->store(1, std::memory_order_release);
+          landed_wake(r);
+          finish_send(it.st, 1);
         } else {
-          it.st->store(-1);
+          finish_send(it.st, -1);
           st(&r->abort, 1u);
+          landed_wake(r);
           dead = true;
         }
         release_event(it.ev);
@@ -581,7 +618,7 @@ class IpcTransport final : public P2PTransport {
     // stopping: the queued copies still finish (nothing can cancel a DMA); their ops fail
     for (auto& it : inflight) {
       (void)hipEventSynchronize(it.ev);
-      it.st->store(-1);
+      finish_send(it.st, -1);
       release_event(it.ev);
     }
   }

@@ -30,6 +30,8 @@ struct alignas(64) IpcRing {
   alignas(64) uint64_t enqueued;   // copies the sender queued (count)
   alignas(64) uint32_t abort;      // either side: the channel is dead
   alignas(64) uint32_t doorbell;   // futex word: bumped on every post (both sides)
+  alignas(64) uint32_t landed_bell;     // futex word: bumped after `landed` advances or on abort
+  uint32_t landed_waiters;              // receivers blocked on landed_bell (wake only if > 0)
   alignas(64) uint32_t sender_attached;
   uint32_t receiver_ready;
   uint64_t warm;                   // generation whose warm-up copy the sender delivered

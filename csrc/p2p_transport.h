@@ -25,9 +25,11 @@
 //    without GPUs; it also carries fault hooks (drop / stall a channel).
 #pragma once
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace dfs {
@@ -58,6 +60,14 @@ class P2PTransport {
   virtual bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
   virtual bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
   virtual int test(P2POp* op) = 0;  // 1 done, 0 pending, -1 failed
+  // test(), but a pending op may block the caller for up to `max_us` first (a futex or event
+  // wait where the transport has one, so the engine's waiters sleep instead of polling).
+  virtual int wait(P2POp* op, int max_us) {
+    int r = test(op);
+    if (r != 0) return r;
+    std::this_thread::sleep_for(std::chrono::microseconds(max_us < 20 ? max_us : 20));
+    return test(op);
+  }
   virtual void release(P2POp* op) = 0;
 
   // Test hooks (socket transport only; no-ops elsewhere): the next `n` sends to `peer`

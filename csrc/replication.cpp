@@ -518,7 +518,7 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
         *err = "send failed";
         break;
       }
-      if ((++spins & 63) == 0) {
+      if ((++spins & 63) == 0 || spins > 64) {
         std::lock_guard<std::mutex> lk(P.mu);
         if (P.gen != t->gen || P.state != State::Up) {
           ok = false;
@@ -531,8 +531,9 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
         *err = "send timed out";
         break;
       }
-      if (spins < 256) std::this_thread::yield();
-      else std::this_thread::sleep_for(std::chrono::microseconds(20));
+      // a short spin for the common sub-100 us copy, then sleep in the transport (futex)
+      if (spins < 64) std::this_thread::yield();
+      else if (t_->wait(&op, 2000) != 0) continue;
     }
     if (!ok) break;
   }
@@ -651,7 +652,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
         why = "receive failed";
         break;
       }
-      if ((++spins & 63) == 0) {
+      if ((++spins & 63) == 0 || spins > 64) {
         std::lock_guard<std::mutex> lk(P.mu);
         if (P.gen != gen || P.state != State::Up) {
           why = "pair failed during receive";
@@ -662,8 +663,8 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
         why = "receive timed out";
         break;
       }
-      if (spins < 256) std::this_thread::yield();
-      else std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if (spins < 64) std::this_thread::yield();
+      else if (t_->wait(&ops[s], 2000) != 0) continue;
     }
     // slice s landed: checksum it on the lane while s+1.. are still on the link
     if (why.empty() && dev) store_->recv_slice(&rv, s * slice, std::min(size, (s + 1) * slice));
