@@ -467,6 +467,7 @@ def main():
                 "repl_pair_failures": sum(r["cs"].get("repl_pair_failures", 0) for r in allr),
                 "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
                 "fused_reads": sum(r["cs"].get("fused_reads", 0) for r in allr),
+                "direct_writes": sum(r["cs"].get("direct_writes", 0) for r in allr),
                 "disk_gate_waits": sum(r["cs"].get("disk_gate_waits", 0) for r in allr),
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],

@@ -324,6 +324,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["mirror_bytes"] = t.mirror_bytes;
         d["io_threads_spawned"] = t.io_threads_spawned;
         d["final_name_writes"] = t.final_name_writes;
+        d["direct_writes"] = t.direct_writes;
         d["crc_mismatches"] = t.crc_mismatches;
         d["gpu_kernel_launches"] = t.gpu_kernel_launches;
         d["disk_gate_waits"] = t.disk_gate_waits;

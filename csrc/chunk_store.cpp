@@ -92,6 +92,35 @@ bool write_all(int fd, const uint8_t* p, uint64_t n, uint64_t off) {
   return true;
 }
 
+// DFS_ODIRECT=1 (A/B, off by default): a fresh block's data file is written with O_DIRECT
+// straight from the caller's page-aligned buffer (the client's registered shm slot), so the
+// bytes skip the page cache (no 1 MiB memcpy into it, no eviction afterwards); the sub-4 KiB
+// tail, if any, is written buffered after clearing O_DIRECT on the descriptor.
+bool odirect_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DFS_ODIRECT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+// `off` and `p` 4 KiB aligned; a sub-4 KiB tail clears O_DIRECT (the last write of a file).
+// If the kernel refuses the direct write of these pages (EINVAL / EFAULT: memory it cannot
+// pin for DMA), the descriptor drops O_DIRECT and the range is written buffered.
+bool write_direct(int fd, const uint8_t* p, uint64_t n, uint64_t off = 0) {
+  auto buffered = [&](uint64_t from) {
+    const int fl = ::fcntl(fd, F_GETFL);
+    if (fl < 0 || ::fcntl(fd, F_SETFL, fl & ~O_DIRECT) != 0) return false;
+    return write_all(fd, p + from, n - from, off + from);
+  };
+  const uint64_t na = n & ~uint64_t(4095);
+  if (na && !write_all(fd, p, na, off)) {
+    if (errno != EINVAL && errno != EFAULT) return false;
+    return buffered(0);
+  }
+  return na == n || buffered(na);
+}
+
 bool read_all(int fd, uint8_t* p, uint64_t n, uint64_t off) {
   while (n) {
     ssize_t r = ::pread(fd, p, n, static_cast<off_t>(off));
@@ -826,8 +855,14 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   const std::string tmp_sfx = fresh ? "" : "." + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
   const std::string dp_tmp = data_path(id, false) + tmp_sfx, mp_tmp = meta_path(id, false) + tmp_sfx;
   int dfd = -1, mfd = -1;
+  bool direct = fresh && odirect_enabled() && cfg_.sync_writes && n >= 4096 &&
+                reinterpret_cast<uintptr_t>(data) % 4096 == 0;
   if (fresh) {
-    dfd = ::open(dp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    dfd = ::open(dp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC | (direct ? O_DIRECT : 0), 0644);
+    if (dfd < 0 && direct) {  // the filesystem refuses O_DIRECT: buffered
+      direct = false;
+      dfd = ::open(dp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    }
     mfd = dfd < 0 ? -1 : ::open(mp_tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
     if (mfd < 0) {
       res.error = errno_str("open " + (dfd < 0 ? dp_tmp : mp_tmp));
@@ -838,9 +873,16 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
       return res;
     }
     dir_file = io_.submit([this] { return sync_dir(false); });
-    data_file = io_.submit([this, dfd, data, n, &data_err] {
+    data_file = io_.submit([this, dfd, data, n, direct, &data_err] {
       DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
-      return write_fd_durable(dfd, data, n, "write " + std::to_string(n) + " bytes", &data_err);
+      if (!direct) return write_fd_durable(dfd, data, n, "write " + std::to_string(n) + " bytes", &data_err);
+      if (!write_direct(dfd, data, n) || ::fdatasync(dfd) != 0) {
+        data_err = errno_str("write (O_DIRECT) " + std::to_string(n) + " bytes");
+        return false;
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      ++st_.direct_writes;
+      return true;
     });
   } else if (sync_now && !gsync_) {
     data_file = io_.submit([this, dp_tmp, data, n, &data_err] {
@@ -1093,14 +1135,25 @@ bool ChunkStore::persist_from_device(const std::string& id, const uint8_t* d, ui
   DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
   Lane* l = acquire_lane();
   std::string dp = data_path(id, false);
-  int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  // replicas: the pinned bounce chunks are page aligned, so with DFS_ODIRECT=1 they go to the
+  // device without a page-cache copy (see odirect_enabled)
+  bool direct = odirect_enabled() && cfg_.sync_writes && n >= 4096;
+  int fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC | (direct ? O_DIRECT : 0), 0644);
+  if (fd < 0 && direct) {
+    direct = false;
+    fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  }
   bool ok = fd >= 0;
   uint64_t nch = (n + kChunk - 1) / kChunk;
   for (uint64_t c = 0; ok && c < nch; ++c) {
     uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
     HIP_OK(hipMemcpyAsync(l->pinned[c & 1], d + off, len, hipMemcpyDeviceToHost, l->stream));
     HIP_OK(hipStreamSynchronize(l->stream));
-    ok = write_all(fd, l->pinned[c & 1], len, off);
+    ok = direct ? write_direct(fd, l->pinned[c & 1], len, off) : write_all(fd, l->pinned[c & 1], len, off);
+  }
+  if (ok && direct) {
+    std::lock_guard<std::mutex> g(mu_);
+    ++st_.direct_writes;
   }
   release_lane(l);
   int mfd = -1;

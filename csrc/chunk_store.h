@@ -93,6 +93,7 @@ struct StoreStats {
   uint64_t mirror_bytes = 0;
   uint64_t io_threads_spawned = 0;  // helper threads ever started (steady state: none per write)
   uint64_t final_name_writes = 0;   // durable writes of fresh ids straight to their final names
+  uint64_t direct_writes = 0;       // of those, data files written with O_DIRECT (DFS_ODIRECT=1)
 };
 
 // Group commit: callers that finished writing share one flush round — syncfs() of the
