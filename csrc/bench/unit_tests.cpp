@@ -591,6 +591,140 @@ TEST(master_core_concurrent_create_complete_read_delete) {
   std::filesystem::remove_all(d);
 }
 
+// Cross-shard Rename through the native 2PC (MasterCore::rename_2pc + the participant
+// handlers): two shards, each a MasterCore on its own single-node Raft, wired together by a
+// PeerCall that invokes the other core's handlers in-process. Concurrent renames commit on
+// both sides; a taken destination and an unreachable participant abort with the source left
+// readable and unpinned. Under TSan this is the 2PC's race check.
+struct Shard {
+  std::string dir;
+  std::shared_ptr<MasterCore> core = std::make_shared<MasterCore>();
+  std::shared_ptr<SmHost> host = std::make_shared<SmHost>();
+  std::unique_ptr<raft::Node> node;
+  explicit Shard(const std::string& tag) {
+    dir = tmpdir(tag);
+    host->sm = core;
+    raft::Options o;
+    o.id = 1;
+    o.members = {{1, tag}};
+    o.client_address = tag;
+    o.dir = dir;
+    o.election_lo = 0.05;
+    o.election_hi = 0.1;
+    o.heartbeat = 0.02;
+    o.sync = false;
+    node = std::make_unique<raft::Node>(o, host);
+    node->start();
+  }
+  ~Shard() {
+    core->detach();
+    node->stop();
+    std::filesystem::remove_all(dir);
+  }
+  int call(const std::string& method, const std::string& req, std::string* out) { return core->handle(method, req, out); }
+  bool create(const std::string& path) {
+    std::string out;
+    pb::CreateFileRequest c;
+    c.path = path;
+    if (call("CreateFile", c.str(), &out) != MasterCore::OK) return false;
+    pb::CreateFileResponse cr;
+    if (!cr.decode(out) || !cr.success) return false;
+    pb::CompleteFileRequest d;
+    d.path = path;
+    d.size = 7;
+    d.etag_md5 = "e";
+    if (call("CompleteFile", d.str(), &out) != MasterCore::OK) return false;
+    pb::CompleteFileResponse dr;
+    return dr.decode(out) && dr.success;
+  }
+  bool visible(const std::string& path) {
+    std::string out;
+    pb::GetFileInfoRequest g;
+    g.path = path;
+    pb::GetFileInfoResponse gr;
+    return call("GetFileInfo", g.str(), &out) == MasterCore::OK && gr.decode(out) && gr.found;
+  }
+};
+
+pb::RenameResponse rename_on(Shard& s, const std::string& src, const std::string& dst, int* code) {
+  pb::RenameRequest r;
+  r.source_path = src;
+  r.dest_path = dst;
+  std::string out;
+  *code = s.call("Rename", r.str(), &out);
+  pb::RenameResponse resp;
+  if (*code == MasterCore::OK) resp.decode(out);
+  return resp;
+}
+
+TEST(master_core_native_2pc_rename) {
+  Shard a("sa"), b("sb");
+  CHECK(eventually([&] { return a.node->is_leader() && b.node->is_leader(); }, 3));
+  const std::string map =
+      R"({"strategy":{"Range":{"ranges":{"/m":"A","~~~~":"B"}}},"shards":["A","B"],"shard_peers":{"A":["a"],"B":["b"]}})";
+  std::atomic<bool> b_down{false};
+  auto wire = [&](const std::string& target, const std::string& path, const std::string& req, int) {
+    GrpcResult r;
+    Shard* s = target == "a" ? &a : (target == "b" && !b_down.load()) ? &b : nullptr;
+    if (!s) return r;  // unreachable: transport_ok = false
+    const std::string prefix = "/dfs.MasterService/";
+    r.transport_ok = true;
+    r.status = s->call(path.substr(prefix.size()), req, &r.message);
+    return r;
+  };
+  for (Shard* s : {&a, &b}) {
+    s->core->attach(s->node.get());
+    s->core->exit_safe_mode();
+    s->core->enable_native_2pc(wire);
+  }
+  a.core->set_shard_map(map, "A");
+  b.core->set_shard_map(map, "B");
+  const int threads = 4, per = 12;
+  for (int t = 0; t < threads; ++t)
+    for (int i = 0; i < per; ++i) CHECK(a.create("/a/s" + std::to_string(t) + "_" + std::to_string(i)));
+  std::atomic<int> bad{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      for (int i = 0; i < per; ++i) {
+        const std::string sfx = std::to_string(t) + "_" + std::to_string(i);
+        int code;
+        pb::RenameResponse r = rename_on(a, "/a/s" + sfx, "/z/d" + sfx, &code);
+        if (code != MasterCore::OK || !r.success) ++bad;
+      }
+    });
+  for (auto& th : ts) th.join();
+  CHECK(bad.load() == 0);
+  for (int t = 0; t < threads; ++t)
+    for (int i = 0; i < per; ++i) {
+      const std::string sfx = std::to_string(t) + "_" + std::to_string(i);
+      CHECK(b.visible("/z/d" + sfx));
+      CHECK(!a.visible("/a/s" + sfx));
+    }
+  Json stats = a.core->txn_stats();
+  CHECK(stats["native_committed"].as_int() == threads * per);
+  Json recs = Json::parse(a.core->tx_records());
+  for (auto& kv : recs.fields()) {
+    CHECK(kv.second["state"].str() == "Committed");
+    CHECK(kv.second["participant_acked"].as_bool());
+  }
+  // a taken destination: the participant refuses, the coordinator aborts, nothing stays pinned
+  CHECK(a.create("/a/keep"));
+  CHECK(b.create("/z/taken"));
+  int code;
+  pb::RenameResponse r = rename_on(a, "/a/keep", "/z/taken", &code);
+  CHECK(code == MasterCore::OK && !r.success);
+  CHECK(a.visible("/a/keep") && a.core->tx_lock("/a/keep").empty());
+  // the participant shard unreachable: prepare fails, abort, the source stays usable
+  b_down = true;
+  r = rename_on(a, "/a/keep", "/z/new", &code);
+  CHECK(code == MasterCore::OK && !r.success && r.error_message == "Cross-shard prepare failed");
+  CHECK(a.visible("/a/keep") && a.core->tx_lock("/a/keep").empty());
+  r = rename_on(a, "/a/keep", "/a/kept", &code);  // same shard: no 2PC, not blocked
+  CHECK(code == MasterCore::OK && r.success && a.visible("/a/kept"));
+  CHECK(a.core->txn_stats()["native_aborted"].as_int() == 2);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {

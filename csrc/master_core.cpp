@@ -566,36 +566,36 @@ Json MasterCore::apply_one(const std::string& name, const Json& a) {
   return Json();
 }
 
+// The replicated state is copied under the lock and serialized outside it, so a compaction
+// of a large namespace holds the handlers up for the copy, not for the JSON text.
 std::string MasterCore::snapshot() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::pair<std::string, pb::FileMetadata>> files;
+  Json tx = Json::object(), sp = Json::array(), uc = Json::object(), up = Json::object();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    files.assign(files_.begin(), files_.end());
+    for (auto& kv : tx_records_) tx.set(kv.first, kv.second);
+    for (auto& p : shuffling_prefixes_) sp.push_back(p);
+    for (auto& kv : under_construction_) uc.set(kv.first, kv.second);
+    for (auto& kv : uc_progress_) up.set(kv.first, kv.second);
+  }
+  std::sort(files.begin(), files.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   std::string out = "{\"Master\":{\"files\":{";
   bool first = true;
-  std::vector<const std::string*> keys;
-  keys.reserve(files_.size());
-  for (auto& kv : files_) keys.push_back(&kv.first);
-  std::sort(keys.begin(), keys.end(), [](auto* a, auto* b) { return *a < *b; });
-  for (auto* k : keys) {
+  for (auto& kv : files) {
     if (!first) out += ",";
     first = false;
-    json_escape(*k, out);
+    json_escape(kv.first, out);
     out += ":";
-    file_json(files_.at(*k)).dump_to(out);
+    file_json(kv.second).dump_to(out);
   }
   out += "},\"transaction_records\":";
-  Json tx = Json::object();
-  for (auto& kv : tx_records_) tx.set(kv.first, kv.second);
   tx.dump_to(out);
   out += ",\"shuffling_prefixes\":";
-  Json sp = Json::array();
-  for (auto& p : shuffling_prefixes_) sp.push_back(p);
   sp.dump_to(out);
   out += ",\"under_construction\":";
-  Json uc = Json::object();
-  for (auto& kv : under_construction_) uc.set(kv.first, kv.second);
   uc.dump_to(out);
   out += ",\"uc_progress\":";
-  Json up = Json::object();
-  for (auto& kv : uc_progress_) up.set(kv.first, kv.second);
   up.dump_to(out);
   out += "}}";
   return out;

@@ -238,8 +238,9 @@ class MasterCore : public raft::StateMachine {
   std::mt19937_64 rng_;
 
   // native 2PC coordinator (enable_native_2pc); at most kMaxCoordinators renames hold an
-  // RPC worker while they wait on the peer shard, the rest go to the async Python coordinator
-  static constexpr int kMaxCoordinators = 8;
+  // RPC worker while they wait on the peer shard (a quarter of the master's 64 native gRPC
+  // workers, so participant calls always find one), the rest go to the Python coordinator
+  static constexpr int kMaxCoordinators = 16;
   PeerCall peer_call_;  // set once before serving
   std::atomic<int> coordinators_{0};
   std::atomic<uint64_t> tx_started_{0}, tx_committed_{0}, tx_aborted_{0}, tx_pending_{0}, tx_declined_{0};

@@ -191,6 +191,7 @@ void Node::start() {
   ticker_ = std::thread([this] { ticker_loop(); });
   flusher_ = std::thread([this] { flusher_loop(); });
   applier_ = std::thread([this] { applier_loop(); });
+  snapshotter_ = std::thread([this] { snapshot_loop(); });
   bool solo;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -207,12 +208,13 @@ void Node::stop() {
     tick_cv_.notify_all();
     flush_cv_.notify_all();
     apply_cv_.notify_all();
+    snap_cv_.notify_all();
     for (auto& kv : peers_) {
       kv.second->cv.notify_all();
       kv.second->aux_cv.notify_all();
     }
   }
-  for (std::thread* t : {&ticker_, &flusher_, &applier_})
+  for (std::thread* t : {&ticker_, &flusher_, &applier_, &snapshotter_})
     if (t->joinable()) t->join();
   std::map<int, std::unique_ptr<Peer>> peers;
   {
@@ -838,10 +840,13 @@ void Node::applier_loop() {
       last_applied_ = std::max(last_applied_, batch.back().idx);
       check_reads_locked(cbs);
       snap_due = last_applied_ - last_included_index_ > opt_.snapshot_threshold;
+      if (snap_due && !snap_req_) {
+        snap_req_ = true;
+        snap_cv_.notify_one();
+      }
     }
     al.unlock();
     for (auto& cb : cbs) cb();
-    if (snap_due) take_snapshot();
   }
 }
 
@@ -871,20 +876,40 @@ std::string Node::apply_membership_locked(const Json& m, Callbacks& cbs) {
   return config_.to_json().dump();
 }
 
-void Node::take_snapshot() {
-  std::unique_lock<std::mutex> al(apply_mu_);
-  uint64_t idx, term;
-  std::string cfg;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    idx = last_applied_;
-    if (idx == 0 || idx <= last_included_index_) return;
-    term = static_cast<uint64_t>(std::max<int64_t>(0, term_at(idx)));
-    cfg = config_.to_json().dump();
+void Node::snapshot_loop() {
+  std::unique_lock<std::mutex> g(mu_);
+  for (;;) {
+    snap_cv_.wait(g, [&] { return snap_req_ || !running_; });
+    if (!running_) return;
+    g.unlock();
+    take_snapshot();
+    g.lock();
+    snap_req_ = false;  // entries applied meanwhile re-request it on a later batch if still due
   }
-  std::string state = host_->snapshot();
+}
+
+// Compaction: the state is captured under apply_mu_ (applies wait only for the capture), then
+// the snapshot file is written and the WAL rewritten without it; entries applied meanwhile
+// stay in the log (idx is the captured index). snap_mu_ keeps an InstallSnapshot from
+// interleaving with the file write.
+void Node::take_snapshot() {
+  std::lock_guard<std::mutex> sl(snap_mu_);
+  uint64_t idx, term;
+  std::string cfg, state;
+  {
+    std::lock_guard<std::mutex> al(apply_mu_);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      idx = last_applied_;
+      if (idx == 0 || idx <= last_included_index_) return;
+      term = static_cast<uint64_t>(std::max<int64_t>(0, term_at(idx)));
+      cfg = config_.to_json().dump();
+    }
+    state = host_->snapshot();
+  }
   std::string data = "{\"meta\":[" + std::to_string(idx) + "," + std::to_string(term) + "],\"state\":" + state +
                      ",\"config\":" + cfg + "}";
+  state.clear();
   atomic_write_file(snap_path(), data, opt_.sync);
   bool leader;
   {
@@ -905,7 +930,6 @@ void Node::take_snapshot() {
     }
     wal_->reset(recs);
   }
-  al.unlock();
   if (leader && !opt_.backup_endpoint.empty()) {
     std::string ep = opt_.backup_endpoint;
     while (!ep.empty() && ep.back() == '/') ep.pop_back();
@@ -1082,6 +1106,7 @@ std::string Node::on_append(const Json& a) {
 
 std::string Node::on_snapshot(const Json& a) {
   std::lock_guard<std::mutex> am(append_mu_);
+  std::lock_guard<std::mutex> sl(snap_mu_);  // not while a compaction writes the snapshot file
   std::unique_lock<std::mutex> al(apply_mu_);
   Callbacks cbs;
   Json out = Json::object();

@@ -251,7 +251,8 @@ class Node {
   mutable std::mutex mu_;
   std::mutex wal_order_mu_;  // WAL writes happen in the order their records were built
   std::mutex append_mu_;     // serialises AppendEntries / InstallSnapshot handlers
-  std::mutex apply_mu_;      // held while the state machine applies / snapshots / restores
+  std::mutex apply_mu_;      // held while the state machine applies / captures a snapshot / restores
+  std::mutex snap_mu_;       // one snapshot file writer at a time (compaction vs InstallSnapshot)
   std::condition_variable flush_cv_, apply_cv_, tick_cv_;
 
   // persistent state
@@ -284,7 +285,12 @@ class Node {
   std::mt19937_64 rng_;
 
   std::map<int, std::unique_ptr<Peer>> peers_;
-  std::thread ticker_, flusher_, applier_;
+  std::thread ticker_, flusher_, applier_, snapshotter_;
+  // compaction runs on its own thread: the applier only requests it (snap_req_, under mu_),
+  // so applies stall for the state capture, not for the snapshot file write and WAL rewrite
+  std::condition_variable snap_cv_;
+  bool snap_req_ = false;
+  void snapshot_loop();
   std::atomic<bool> running_{false};
   bool started_ = false;
 };
