@@ -674,7 +674,29 @@ void bind_meta(py::module_& m) {
              });
            }, py::arg("tls") = false, py::arg("ca") = "", py::arg("domain") = "")
       .def("txn_stats", [](const MasterCore& c) { return c.txn_stats().dump(); })
-      .def_property_readonly("requests", &MasterCore::requests);
+      .def("queue_command", [](MasterCore& c, const std::string& addr, py::bytes cmd) {
+        c.queue_command(addr, std::string(cmd));
+      })
+      .def("take_commands", [](MasterCore& c, const std::string& addr) {
+        py::list out;
+        for (auto& s : c.take_commands(addr)) out.append(py::bytes(s));
+        return out;
+      })
+      .def("peek_commands", [](const MasterCore& c) {
+        py::dict out;
+        for (auto& kv : c.peek_commands()) {
+          py::list l;
+          for (auto& s : kv.second) l.append(py::bytes(s));
+          out[py::str(kv.first)] = l;
+        }
+        return out;
+      })
+      .def("bad_blocks", &MasterCore::bad_blocks)
+      .def("add_bad_block", &MasterCore::add_bad_block)
+      .def("take_ec_reports", &MasterCore::take_ec_reports)
+      .def("take_heal_request", &MasterCore::take_heal_request)
+      .def_property_readonly("requests", &MasterCore::requests)
+      .def_property_readonly("heartbeats", &MasterCore::heartbeats);
 
   m.def("select_servers_rack_aware", [](MasterCore& c, size_t n, const std::string& preferred) {
     return select_servers_rack_aware(c.chunk_servers(), n, preferred);

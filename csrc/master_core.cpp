@@ -1096,7 +1096,7 @@ bool MasterCore::native_method(const std::string& m) const {
   return m == "GetFileInfo" || m == "CreateFile" || m == "AllocateBlock" || m == "CompleteFile" ||
          m == "ListFiles" || m == "DeleteFile" || m == "GetBlockLocations" || m == "Rename" ||
          m == "PrepareTransaction" || m == "CommitTransaction" || m == "AbortTransaction" ||
-         m == "InquireTransaction";
+         m == "InquireTransaction" || m == "Heartbeat";
 }
 
 int MasterCore::handle(const std::string& method, const std::string& req, std::string* out) {
@@ -1113,6 +1113,7 @@ int MasterCore::handle(const std::string& method, const std::string& req, std::s
     if (method == "CommitTransaction") return commit_transaction(req, out);
     if (method == "AbortTransaction") return abort_transaction(req, out);
     if (method == "InquireTransaction") return inquire_transaction(req, out);
+    if (method == "Heartbeat") return heartbeat(req, out);
   } catch (const std::exception& e) {
     *out = e.what();
     return INTERNAL;
@@ -1456,6 +1457,139 @@ int MasterCore::rename(const std::string& raw, std::string* out) {
       else resp.success = true;
     }
   }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+namespace {
+Json master_cmd(const char* name, Json args);  // below, with the 2PC helpers
+}  // namespace
+
+// ---------------------------------------------------------------- heartbeat (C33/C34)
+void MasterCore::queue_command(const std::string& addr, const std::string& cmd) {
+  std::lock_guard<std::mutex> g(mu_);
+  cmd_q_[addr].push_back(cmd);
+}
+
+std::vector<std::string> MasterCore::take_commands(const std::string& addr) {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> out;
+  auto it = cmd_q_.find(addr);
+  if (it != cmd_q_.end()) {
+    out.swap(it->second);
+    cmd_q_.erase(it);
+  }
+  return out;
+}
+
+std::map<std::string, std::vector<std::string>> MasterCore::peek_commands() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return cmd_q_;
+}
+
+std::map<std::string, std::vector<std::string>> MasterCore::bad_blocks() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::map<std::string, std::vector<std::string>> out;
+  for (auto& kv : bad_blocks_) out[kv.first].assign(kv.second.begin(), kv.second.end());
+  return out;
+}
+
+void MasterCore::add_bad_block(const std::string& block_id, const std::string& addr) {
+  std::lock_guard<std::mutex> g(mu_);
+  bad_blocks_[block_id].insert(addr);
+  heal_req_ = true;
+}
+
+std::pair<std::vector<std::string>, std::vector<std::string>> MasterCore::take_ec_reports() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::pair<std::vector<std::string>, std::vector<std::string>> out;
+  out.first.swap(ec_encoded_);
+  out.second.swap(ec_failed_);
+  return out;
+}
+
+bool MasterCore::take_heal_request() {
+  std::lock_guard<std::mutex> g(mu_);
+  bool r = heal_req_;
+  heal_req_ = false;
+  return r;
+}
+
+// Heartbeat (reference master.rs heartbeat handler): refresh the registry entry, record the
+// replicas / rebuilt EC shards the server reports (AddBlockLocation, fire-and-forget Raft
+// entries), safe-mode block accounting, bad-block reports (a heal pass is requested from the
+// background healer), unreferenced blocks as DELETE commands, and the queued commands for
+// this server with the current master term.
+int MasterCore::heartbeat(const std::string& raw, std::string* out) {
+  pb::HeartbeatRequest r;
+  if (!r.decode(raw)) return (*out = "malformed HeartbeatRequest", INTERNAL);
+  heartbeats_++;
+  const std::string& addr = r.chunk_server_address;
+  raft::Node* node = node_.load();
+  bool is_new, safe;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = chunk_servers_.find(addr);
+    is_new = it == chunk_servers_.end();
+    ChunkServerStatus st;
+    st.address = addr;
+    st.last_heartbeat = now_ms();
+    st.used_space = r.used_space;
+    st.available_space = r.available_space;
+    st.chunk_count = r.chunk_count;
+    st.rack_id = !r.rack_id.empty() ? r.rack_id : (is_new ? std::string() : it->second.rack_id);
+    st.gpu_rank = r.gpu_rank;
+    st.hbm_capacity = r.hbm_capacity;
+    st.hbm_used = r.hbm_used;
+    chunk_servers_[addr] = st;
+    for (auto& b : r.ec_encoded) ec_encoded_.push_back(b);
+    for (auto& b : r.ec_failed) ec_failed_.push_back(b);
+    for (auto& b : r.bad_blocks) bad_blocks_[b].insert(addr);
+    if (!r.bad_blocks.empty()) heal_req_ = true;
+    safe = safe_mode_;
+  }
+  if (node) {
+    for (auto& bid : r.new_blocks)  // replicas created by REPLICATE / reconstruction
+      node->propose_nowait(master_cmd("AddBlockLocation", obj({{"block_id", bid}, {"address", addr}})).dump());
+    for (auto& ent : r.ec_rebuilt) {  // "<block>/<shard index>": the rebuilt shard's position
+      size_t slash = ent.rfind('/');
+      if (slash == std::string::npos || slash == 0 || slash + 1 >= ent.size()) continue;
+      const std::string idx = ent.substr(slash + 1);
+      if (idx.find_first_not_of("0123456789") != std::string::npos) continue;
+      node->propose_nowait(master_cmd("AddBlockLocation", obj({{"block_id", ent.substr(0, slash)},
+                                                               {"address", addr},
+                                                               {"shard_index", static_cast<int64_t>(std::stoll(idx))}}))
+                               .dump());
+    }
+  }
+  if (safe && is_new) report_blocks(r.chunk_count);  // exits safe mode when due
+  if (safe && should_exit_safe_mode()) exit_safe_mode();
+  if (!r.bad_blocks.empty())
+    std::fprintf(stderr, "dfs master: heartbeat: %zu bad block(s) reported by %s\n", r.bad_blocks.size(), addr.c_str());
+  pb::HeartbeatResponse resp;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    // blocks no file references any more: DELETE on every holder (Python's drain_gc)
+    for (auto& e : gc_)
+      for (auto& loc : e.second) {
+        pb::ChunkServerCommand c;
+        c.type = pb::ChunkServerCommand::DELETE;
+        c.block_id = e.first;
+        cmd_q_[loc].push_back(c.str());
+      }
+    gc_.clear();
+    auto it = cmd_q_.find(addr);
+    if (it != cmd_q_.end()) {
+      for (auto& c : it->second) {
+        pb::ChunkServerCommand cmd;
+        if (cmd.decode(c)) resp.commands.push_back(std::move(cmd));
+      }
+      cmd_q_.erase(it);
+    }
+  }
+  resp.success = true;
+  resp.master_term = node ? node->term() : 0;
   out->clear();
   resp.encode(*out);
   return OK;

@@ -95,6 +95,19 @@ class MasterCore : public raft::StateMachine {
   void report_blocks(uint64_t n);  // + reported blocks, auto-exit when due
   Json safe_mode_status() const;
 
+  // Chunkserver commands (local, not replicated): queued by the healer / balancer / tiering
+  // (Python, serialized ChunkServerCommand) and by GC, handed out by the native Heartbeat.
+  void queue_command(const std::string& addr, const std::string& cmd);
+  std::vector<std::string> take_commands(const std::string& addr);
+  std::map<std::string, std::vector<std::string>> peek_commands() const;
+  // What heartbeats reported for the Python background tasks: blocks that failed
+  // verification (block -> servers), EC conversions done / failed, and whether a heal pass
+  // is due (a bad block arrived since the last call).
+  std::map<std::string, std::vector<std::string>> bad_blocks() const;
+  void add_bad_block(const std::string& block_id, const std::string& addr);
+  std::pair<std::vector<std::string>, std::vector<std::string>> take_ec_reports();
+  bool take_heal_request();
+
   // Queries for the Python services (serialized FileMetadata / JSON).
   bool get_file(const std::string& path, bool visible_only, std::string* pb) const;
   bool contains(const std::string& path) const;
@@ -161,6 +174,7 @@ class MasterCore : public raft::StateMachine {
 
   void set_access_stats(bool on, int flush_ms);
   uint64_t requests() const { return requests_.load(); }
+  uint64_t heartbeats() const { return heartbeats_.load(); }
 
  private:
   struct Result {  // of a proposal
@@ -190,6 +204,7 @@ class MasterCore : public raft::StateMachine {
   int delete_file(const std::string& req, std::string* out);
   int rename(const std::string& req, std::string* out);
   int get_block_locations(const std::string& req, std::string* out);
+  int heartbeat(const std::string& req, std::string* out);
   int rename_2pc(const pb::RenameRequest& r, const std::string& src_shard, const std::string& dst_shard,
                  std::string* out);
   int prepare_transaction(const std::string& req, std::string* out);
@@ -231,6 +246,10 @@ class MasterCore : public raft::StateMachine {
   std::string shard_id_;
   bool have_map_ = false;
   std::map<std::string, uint64_t> request_counts_;
+  std::map<std::string, std::vector<std::string>> cmd_q_;        // addr -> serialized commands
+  std::map<std::string, std::set<std::string>> bad_blocks_;      // block -> reporting servers
+  std::vector<std::string> ec_encoded_, ec_failed_;
+  bool heal_req_ = false;
   std::vector<std::pair<std::string, std::vector<std::string>>> gc_;
   std::map<std::string, uint64_t> access_buf_;
   bool access_stats_ = true;
@@ -246,7 +265,7 @@ class MasterCore : public raft::StateMachine {
   std::atomic<uint64_t> tx_started_{0}, tx_committed_{0}, tx_aborted_{0}, tx_pending_{0}, tx_declined_{0};
 
   std::atomic<raft::Node*> node_{nullptr};
-  std::atomic<uint64_t> requests_{0};
+  std::atomic<uint64_t> requests_{0}, heartbeats_{0};
   std::atomic<bool> running_{true};
   std::condition_variable access_cv_;
   std::thread access_thread_;

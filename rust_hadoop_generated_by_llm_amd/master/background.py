@@ -88,6 +88,7 @@ class MasterBackground:
             (self.iv.shard_refresh, self.refresh_shard_map, self.iv.shard_refresh),
             (self.iv.split, self.split_detector, self.iv.split),
             (self.iv.tiering, self.tiering, self.iv.tiering),
+            (0.25, self.heartbeat_reports, 0.25),
         ]
         for first, fn, every in jobs:
             self._tasks.append(loop.create_task(self._every(first, fn, every)))
@@ -129,6 +130,16 @@ class MasterBackground:
             self.state.pending_commands.pop(a, None)
         if dead:
             self.state.heal_under_replicated_blocks()
+
+    async def heartbeat_reports(self) -> None:
+        """What the native Heartbeat handler recorded: a bad block report triggers a heal pass
+        right away (as the reference's heartbeat handler does), EC conversion results update
+        tiering's jobs."""
+        self.svc.drain_heartbeat_reports()
+        if self.state.core.take_heal_request():
+            n = self.state.heal_under_replicated_blocks()
+            if n:
+                log.info("healer queued %d commands after a bad-block report", n)
 
     async def periodic_heal(self) -> None:
         n = self.state.heal_under_replicated_blocks()

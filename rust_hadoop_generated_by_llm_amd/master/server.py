@@ -121,6 +121,8 @@ class MasterProcess:
         self.metrics.gauge("dfs_master_chunkservers", "live chunkservers", fn=lambda: len(self.state.chunk_servers))
         self.metrics.gauge("dfs_master_native_requests", "requests served by the native handlers",
                            fn=lambda: self.state.core.requests)
+        self.metrics.gauge("dfs_master_native_heartbeats", "chunkserver heartbeats served by the native handler",
+                           fn=lambda: self.state.core.heartbeats)
         for key, help_ in (("native_started", "cross-shard renames coordinated natively"),
                            ("native_committed", "native 2PC renames committed"),
                            ("native_aborted", "native 2PC renames aborted"),

@@ -182,40 +182,20 @@ class MasterService:
         return pb.RegisterChunkServerResponse(success=True)
 
     async def heartbeat(self, req, ctx):
-        st = self.state
-        addr = req.chunk_server_address
-        is_new = addr not in st.chunk_servers
-        rack = req.rack_id or (st.chunk_servers[addr].rack_id if addr in st.chunk_servers else "")
-        st.chunk_servers[addr] = ChunkServerStatus(
-            last_heartbeat=now_ms(), used_space=req.used_space, available_space=req.available_space,
-            chunk_count=req.chunk_count, rack_id=rack, gpu_rank=req.gpu_rank,
-            hbm_capacity=req.hbm_capacity, hbm_used=req.hbm_used)
-        for bid in req.new_blocks:  # ext: replicas created by REPLICATE / reconstruction
-            self.raft.propose_nowait({"Master": {"AddBlockLocation": {"block_id": bid, "address": addr}}})
-        for ent in req.ec_rebuilt:  # ext: EC shard rebuilt here -> location at its shard index
-            bid, _, idx = ent.rpartition("/")
-            if bid and idx.isdigit():
-                self.raft.propose_nowait({"Master": {"AddBlockLocation": {"block_id": bid, "address": addr,
-                                                                          "shard_index": int(idx)}}})
-        for bid in req.ec_encoded:
+        """Served natively (MasterCore::heartbeat) on the native gRPC server and the local
+        socket; this is the grpcio path (no native server), the same native handler."""
+        return await self._native("Heartbeat", req, pb.HeartbeatResponse)
+
+    def drain_heartbeat_reports(self) -> None:
+        """EC conversion reports the native Heartbeat recorded (tiering's jobs live here)."""
+        encoded, failed = self.core.take_ec_reports()
+        for bid in encoded:
             job = self.ec_jobs.get(bid)
             if job is not None:
                 job["done"] = True
-        for bid in req.ec_failed:
+        for bid in failed:
             if self.ec_jobs.pop(bid, None) is not None:
-                log.warning("EC conversion of block %s failed at %s; will retry", bid, addr)
-        if st.safe_mode and is_new:
-            st.update_reported_blocks(req.chunk_count)
-        if st.safe_mode and st.should_exit_safe_mode():
-            st.exit_safe_mode()
-        if req.bad_blocks:
-            log.warning("heartbeat: %d bad block(s) reported by %s", len(req.bad_blocks), addr)
-            for bid in req.bad_blocks:
-                st.bad_block_locations.setdefault(bid, set()).add(addr)
-            st.heal_under_replicated_blocks()
-        st.drain_gc()
-        cmds = st.pending_commands.pop(addr, [])
-        return pb.HeartbeatResponse(success=True, commands=cmds, master_term=self.raft.current_term)
+                log.warning("EC conversion of block %s failed; will retry", bid)
 
     # ------------------------------------------------------------------ rename / 2PC
     async def rename(self, req, ctx):

@@ -9,8 +9,9 @@ had (reference: dfs/metaserver/src/master.rs:195-602):
 * ``state.files`` / ``block_index`` / ``under_construction`` / ``tx_locks`` /
   ``transaction_records`` are read-only mappings decoded on demand from the core;
 * ``state.chunk_servers`` is a mutable mapping backed by the core's registry;
-* ``pending_commands`` and ``bad_block_locations`` stay Python dicts — only heartbeats and
-  the healer touch them;
+* ``pending_commands`` and ``bad_block_locations`` are views of the core's command queue and
+  bad-block reports: the native Heartbeat handler hands the commands out and records the
+  reports, the Python background tasks queue commands and read the reports;
 * the healer (``heal_under_replicated_blocks``) runs here over those views.
 """
 from __future__ import annotations
@@ -184,6 +185,98 @@ class _ChunkServers(MutableMapping):
         return [v for _, v in self.items()]
 
 
+class _CmdList:
+    """`pending_commands.setdefault(addr, []).append(cmd)` queues into the native core."""
+
+    def __init__(self, core, addr):
+        self._core, self._addr = core, addr
+
+    def append(self, cmd) -> None:
+        self._core.queue_command(self._addr, cmd.SerializeToString())
+
+
+class _PendingCommands:
+    """addr -> queued ChunkServerCommand, held by MasterCore (the native Heartbeat pops them)."""
+
+    def __init__(self, core):
+        self._core = core
+
+    def setdefault(self, addr, default=None):
+        return _CmdList(self._core, addr)
+
+    def pop(self, addr, default=None):
+        raws = self._core.take_commands(addr)
+        return [pb.ChunkServerCommand.FromString(r) for r in raws] if raws else default
+
+    def values(self):
+        return [[pb.ChunkServerCommand.FromString(r) for r in v] for v in self._core.peek_commands().values()]
+
+    def items(self):
+        return [(k, [pb.ChunkServerCommand.FromString(r) for r in v])
+                for k, v in self._core.peek_commands().items()]
+
+    def get(self, addr, default=None):
+        v = self._core.peek_commands().get(addr)
+        return [pb.ChunkServerCommand.FromString(r) for r in v] if v else default
+
+    def __contains__(self, addr):
+        return addr in self._core.peek_commands()
+
+    def __getitem__(self, addr):
+        v = self.get(addr)
+        if v is None:
+            raise KeyError(addr)
+        return v
+
+    def __len__(self):
+        return len(self._core.peek_commands())
+
+
+class _BadSet:
+    def __init__(self, core, bid):
+        self._core, self._bid = core, bid
+
+    def add(self, addr) -> None:
+        self._core.add_bad_block(self._bid, addr)
+
+
+class _BadBlocks:
+    """block -> servers whose copy failed verification (reported by heartbeats, native)."""
+
+    def __init__(self, core):
+        self._core = core
+
+    def setdefault(self, bid, default=None):
+        return _BadSet(self._core, bid)
+
+    def items(self):
+        return [(k, set(v)) for k, v in self._core.bad_blocks().items()]
+
+    def get(self, bid, default=None):
+        v = self._core.bad_blocks().get(bid)
+        return set(v) if v is not None else default
+
+    def __contains__(self, bid):
+        return bid in self._core.bad_blocks()
+
+    def __setitem__(self, bid, addrs):
+        for a in addrs:
+            self._core.add_bad_block(bid, a)
+
+    def update(self, other) -> None:
+        for bid, addrs in dict(other).items():
+            self[bid] = addrs
+
+    def __getitem__(self, bid):
+        v = self.get(bid)
+        if v is None:
+            raise KeyError(bid)
+        return v
+
+    def __len__(self):
+        return len(self._core.bad_blocks())
+
+
 class MasterState:
     def __init__(self, core=None):
         self.core = core if core is not None else native.MasterCore()
@@ -194,9 +287,9 @@ class MasterState:
         self.tx_locks = _Pred(lambda p: bool(c.tx_lock(p)), c.tx_lock)
         self.transaction_records = _TxRecords(c)
         self.chunk_servers = _ChunkServers(c)
-        # local (not replicated), touched by heartbeats and the healer only
-        self.pending_commands: dict[str, list] = {}
-        self.bad_block_locations: dict[str, set[str]] = {}
+        # local (not replicated): the native Heartbeat hands commands out and records reports
+        self.pending_commands = _PendingCommands(c)
+        self.bad_block_locations = _BadBlocks(c)
 
     # ------------------------------------------------------------------ namespace
     @property

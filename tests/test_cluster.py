@@ -215,6 +215,8 @@ def test_cross_shard_rename_and_listing():
         c.close()
         # the 2PC ran in C++ (MasterCore::rename_2pc), not in the Python coordinator
         assert _master_metric_sum(cl, "dfs_master_tx_native_committed") >= 1
+        # and the chunkservers' heartbeats were answered by MasterCore::heartbeat
+        assert _master_metric_sum(cl, "dfs_master_native_heartbeats") >= 1
         assert _master_metric_sum(cl, "dfs_master_tx_declined") == 0
 
 

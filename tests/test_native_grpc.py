@@ -164,11 +164,23 @@ def test_master_service_on_native_grpc():
                 c.get_file_content("/ng/missing")
         finally:
             c.close()
+        # a method the Python handlers own (safe-mode status) goes through the fallback
+        from rust_hadoop_generated_by_llm_amd.models import proto as pb
+        from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
+
+        pool = ChannelPool(local=False)  # over HTTP/2, not the same-host socket
+        try:
+            st = pool.call(cl.master_addrs[0], "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(),
+                           timeout=10)
+            assert st.chunk_server_count == 1
+        finally:
+            pool.close()
         http = cl.master_http[cl.master_addrs[0]]
         text = urllib.request.urlopen(f"{http}/metrics").read().decode()
         vals = {ln.split()[0]: float(ln.split()[1]) for ln in text.splitlines() if ln and not ln.startswith("#")}
         assert vals["dfs_master_native_grpc_calls"] >= 15
         assert 0 < vals["dfs_master_native_grpc_fallback"] < vals["dfs_master_native_grpc_calls"]
+        assert vals["dfs_master_native_heartbeats"] >= 1
 
 
 @pytest.mark.slow
