@@ -1096,7 +1096,8 @@ bool MasterCore::native_method(const std::string& m) const {
   return m == "GetFileInfo" || m == "CreateFile" || m == "AllocateBlock" || m == "CompleteFile" ||
          m == "ListFiles" || m == "DeleteFile" || m == "GetBlockLocations" || m == "Rename" ||
          m == "PrepareTransaction" || m == "CommitTransaction" || m == "AbortTransaction" ||
-         m == "InquireTransaction" || m == "Heartbeat";
+         m == "InquireTransaction" || m == "Heartbeat" || m == "RegisterChunkServer" || m == "GetSafeModeStatus" ||
+         m == "SetSafeMode";
 }
 
 int MasterCore::handle(const std::string& method, const std::string& req, std::string* out) {
@@ -1114,6 +1115,9 @@ int MasterCore::handle(const std::string& method, const std::string& req, std::s
     if (method == "AbortTransaction") return abort_transaction(req, out);
     if (method == "InquireTransaction") return inquire_transaction(req, out);
     if (method == "Heartbeat") return heartbeat(req, out);
+    if (method == "RegisterChunkServer") return register_chunk_server(req, out);
+    if (method == "GetSafeModeStatus") return get_safe_mode_status(req, out);
+    if (method == "SetSafeMode") return set_safe_mode(req, out);
   } catch (const std::exception& e) {
     *out = e.what();
     return INTERNAL;
@@ -1590,6 +1594,62 @@ int MasterCore::heartbeat(const std::string& raw, std::string* out) {
   }
   resp.success = true;
   resp.master_term = node ? node->term() : 0;
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+// RegisterChunkServer / GetSafeModeStatus / SetSafeMode (reference master.rs:258-367 and the
+// handlers of the same names): the registry entry, the linearizable safe-mode view, manual
+// enter / leave.
+int MasterCore::register_chunk_server(const std::string& raw, std::string* out) {
+  pb::RegisterChunkServerRequest r;
+  if (!r.decode(raw)) return (*out = "malformed RegisterChunkServerRequest", INTERNAL);
+  ChunkServerStatus st;
+  st.address = r.address;
+  st.last_heartbeat = now_ms();
+  st.available_space = r.capacity;
+  st.rack_id = r.rack_id;
+  upsert_chunk_server(st);
+  pb::RegisterChunkServerResponse resp;
+  resp.success = true;
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::get_safe_mode_status(const std::string& raw, std::string* out) {
+  pb::GetSafeModeStatusRequest r;
+  if (!r.decode(raw)) return (*out = "malformed GetSafeModeStatusRequest", INTERNAL);
+  int c;
+  if ((c = read_index(out)) != OK) return c;
+  pb::GetSafeModeStatusResponse resp;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    resp.is_safe_mode = safe_mode_;
+    resp.is_manual = safe_mode_manual_;
+    resp.chunk_server_count = static_cast<uint32_t>(chunk_servers_.size());
+    resp.expected_blocks = static_cast<uint32_t>(expected_blocks_);
+    resp.reported_blocks = static_cast<uint32_t>(reported_blocks_);
+    resp.threshold = safe_mode_threshold_;
+    resp.entered_at = static_cast<uint64_t>(safe_mode_entered_at_);
+  }
+  out->clear();
+  resp.encode(*out);
+  return OK;
+}
+
+int MasterCore::set_safe_mode(const std::string& raw, std::string* out) {
+  pb::SetSafeModeRequest r;
+  if (!r.decode(raw)) return (*out = "malformed SetSafeModeRequest", INTERNAL);
+  if (r.enter) enter_safe_mode(true);
+  else exit_safe_mode();
+  pb::SetSafeModeResponse resp;
+  resp.success = true;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    resp.is_safe_mode = safe_mode_;
+  }
   out->clear();
   resp.encode(*out);
   return OK;

@@ -205,6 +205,9 @@ class MasterCore : public raft::StateMachine {
   int rename(const std::string& req, std::string* out);
   int get_block_locations(const std::string& req, std::string* out);
   int heartbeat(const std::string& req, std::string* out);
+  int register_chunk_server(const std::string& req, std::string* out);
+  int get_safe_mode_status(const std::string& req, std::string* out);
+  int set_safe_mode(const std::string& req, std::string* out);
   int rename_2pc(const pb::RenameRequest& r, const std::string& src_shard, const std::string& dst_shard,
                  std::string* out);
   int prepare_transaction(const std::string& req, std::string* out);

@@ -164,15 +164,18 @@ def test_master_service_on_native_grpc():
                 c.get_file_content("/ng/missing")
         finally:
             c.close()
-        # a method the Python handlers own (safe-mode status) goes through the fallback
+        # a method the Python handlers own (cluster info) goes through the fallback
         from rust_hadoop_generated_by_llm_amd.models import proto as pb
         from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
 
         pool = ChannelPool(local=False)  # over HTTP/2, not the same-host socket
         try:
+            info = pool.call(cl.master_addrs[0], "MasterService", "GetClusterInfo", pb.GetClusterInfoRequest(),
+                             timeout=10)
+            assert info is not None
             st = pool.call(cl.master_addrs[0], "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(),
-                           timeout=10)
-            assert st.chunk_server_count == 1
+                           timeout=10)  # native
+            assert st.chunk_server_count == 1 and not st.is_safe_mode
         finally:
             pool.close()
         http = cl.master_http[cl.master_addrs[0]]
