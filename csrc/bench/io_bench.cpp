@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -115,11 +117,97 @@ static void disk_case(const std::string& dir, int threads, int per, bool direct,
   std::filesystem::remove_all(dir);
 }
 
+// Journal variant of disk_case: T threads append 1 MiB records (+ a 4 KiB header/.meta
+// frame) to ONE preallocated, already-written segment at reserved offsets; a record is
+// durable once a group fdatasync that started after its pwrite completed. mode 0: buffered
+// appends, 1: O_DIRECT appends, 2: O_DIRECT|O_DSYNC per append (no group commit).
+static void journal_case(const std::string& dir, int threads, int per, int mode, bool first) {
+  std::filesystem::create_directories(dir);
+  const size_t n = 1 << 20, hdr = 4096, rec = n + hdr;
+  const uint64_t total = uint64_t(threads) * per * rec;
+  std::string f = dir + "/journal.seg";
+  int fd = ::open(f.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0644);
+  {  // preallocate by writing: later appends overwrite written extents (no metadata change)
+    std::vector<uint8_t> z(8 << 20, 0);
+    for (uint64_t off = 0; off < total; off += z.size())
+      if (::pwrite(fd, z.data(), std::min<uint64_t>(z.size(), total - off), off) < 0) break;
+    ::fsync(fd);
+    ::close(fd);
+  }
+  int flags = O_RDWR | (mode >= 1 ? O_DIRECT : 0) | (mode == 2 ? O_DSYNC : 0);
+  fd = ::open(f.c_str(), flags);
+  std::atomic<uint64_t> tail{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  uint64_t issued = 0, done = 0, rounds = 0;
+  bool running = false;
+  auto group_sync = [&]() {
+    std::unique_lock<std::mutex> lk(mu);
+    uint64_t ticket = ++issued;
+    while (done < ticket) {
+      if (running) { cv.wait(lk); continue; }
+      running = true;
+      uint64_t covers = issued;
+      lk.unlock();
+      ::fdatasync(fd);
+      lk.lock();
+      running = false;
+      done = covers;
+      ++rounds;
+      cv.notify_all();
+    }
+  };
+  std::vector<Lat> lat(threads);
+  std::vector<std::thread> ts;
+  std::atomic<int> errors{0};
+  auto t0 = Clock::now();
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      void* buf = nullptr;
+      if (posix_memalign(&buf, 4096, rec) != 0) { ++errors; return; }
+      std::memset(buf, t + 1, rec);
+      for (int i = 0; i < per; ++i) {
+        auto a = Clock::now();
+        uint64_t off = tail.fetch_add(rec);
+        if (::pwrite(fd, buf, rec, off) != static_cast<ssize_t>(rec)) ++errors;
+        if (mode != 2) group_sync();
+        lat[t].add(secs(a, Clock::now()));
+      }
+      std::free(buf);
+    });
+  for (auto& th : ts) th.join();
+  double el = secs(t0, Clock::now());
+  ::close(fd);
+  Lat all;
+  for (auto& l : lat) all.v.insert(all.v.end(), l.v.begin(), l.v.end());
+  static const char* names[] = {"buffered", "direct", "direct_dsync"};
+  std::printf("%s\n    {\"journal\": \"%s\", \"threads\": %d, \"records\": %d, \"GBps\": %.2f, \"p50_ms\": %.3f, \"p99_ms\": %.3f, \"sync_rounds\": %llu, \"errors\": %d}",
+              first ? "" : ",", names[mode], threads, threads * per, double(threads) * per * n / el / 1e9,
+              all.pct(0.5) * 1e3, all.pct(0.99) * 1e3, static_cast<unsigned long long>(rounds), errors.load());
+  std::fflush(stdout);
+  std::filesystem::remove_all(dir);
+}
+
 int main(int argc, char** argv) {
   int device = 0, iters = 50;
   bool fsync = true;
   bool zero_copy = true;
   bool rs_only = false;  // only the RS(6,3) end-to-end case (pipeline tuning sweeps)
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--journal-sweep") {
+      std::string dir = "/tmp/io_bench_journal";
+      for (int j = 1; j + 1 < argc; ++j)
+        if (std::string(argv[j]) == "--dir") dir = argv[j + 1];
+      std::printf("{\"journal_sweep\": [");
+      bool first = true;
+      for (int t : {1, 10, 30, 70}) {
+        disk_case(dir + "_files", t, std::max(8, 2400 / t / 4), false, 0, first);
+        first = false;
+        for (int mode = 0; mode < 3; ++mode) journal_case(dir, t, std::max(8, 2400 / t / 4), mode, false);
+      }
+      std::printf("\n]}\n");
+      return 0;
+    }
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--disk-sweep") {
       std::string dir = "/tmp/io_bench_disk";

@@ -178,8 +178,10 @@ PYBIND11_MODULE(_dfs_native, m) {
   // ---------------- chunk store
   py::class_<ChunkStore>(m, "ChunkStore")
       .def(py::init([](std::string storage_dir, std::string cold_dir, int device, uint64_t hbm_capacity,
-                       int durability, int cache_blocks, int lanes, int spill_threads, bool sync_writes) {
+                       int durability, int cache_blocks, int lanes, int spill_threads, bool sync_writes,
+                       int journal) {
              StoreConfig c;
+             c.journal = journal;
              c.storage_dir = storage_dir;
              c.cold_dir = cold_dir;
              c.device = device;
@@ -194,7 +196,7 @@ PYBIND11_MODULE(_dfs_native, m) {
            }),
            py::arg("storage_dir"), py::arg("cold_dir") = "", py::arg("device") = -1, py::arg("hbm_capacity") = 0,
            py::arg("durability") = 0, py::arg("cache_blocks") = 100, py::arg("lanes") = 8,
-           py::arg("spill_threads") = 4, py::arg("sync_writes") = true)
+           py::arg("spill_threads") = 4, py::arg("sync_writes") = true, py::arg("journal") = -1)
       .def_property_readonly("gpu", &ChunkStore::gpu)
       .def_property_readonly("device", [](ChunkStore& s) { return s.config().device; })
       .def("write", [](ChunkStore& s, const std::string& id, py::buffer data, uint32_t expected) {
@@ -308,6 +310,11 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("drop_resident", &ChunkStore::drop_resident, py::call_guard<py::gil_scoped_release>())
       .def("debug_corrupt", &ChunkStore::debug_corrupt, py::call_guard<py::gil_scoped_release>())
       .def("debug_pause_spill", &ChunkStore::debug_pause_spill, py::call_guard<py::gil_scoped_release>())
+      .def("materialize", &ChunkStore::materialize_all, py::call_guard<py::gil_scoped_release>(),
+           "write every journal record out as <id> + <id>.meta now and wait")
+      .def("debug_pause_materializer", &ChunkStore::debug_pause_materializer,
+           py::call_guard<py::gil_scoped_release>())
+      .def("journaled", &ChunkStore::journaled)
       .def("stats", [](ChunkStore& s) {
         StoreStats t = s.stats();
         py::dict d;
@@ -334,6 +341,24 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["sliced_stages"] = t.sliced_stages;
         d["staged_dma"] = t.staged_dma;
         d["host_registered_bytes"] = t.host_registered_bytes;
+        d["journal"] = t.journal;
+        d["journal_records"] = t.journal_records;
+        d["journal_bytes"] = t.journal_bytes;
+        d["journal_commits"] = t.journal_commits;
+        d["journal_sync_rounds"] = t.journal_sync_rounds;
+        d["journal_tombstones"] = t.journal_tombstones;
+        d["journal_full_waits"] = t.journal_full_waits;
+        d["journal_segs"] = t.journal_segs;
+        d["journal_segs_free"] = t.journal_segs_free;
+        d["journal_segs_retired"] = t.journal_segs_retired;
+        d["journal_replayed"] = t.journal_replayed;
+        d["journal_replay_skipped"] = t.journal_replay_skipped;
+        d["journal_failed"] = t.journal_failed;
+        d["materialized_blocks"] = t.materialized_blocks;
+        d["materialized_bytes"] = t.materialized_bytes;
+        d["materialize_pending"] = t.materialize_pending;
+        d["materialize_batches"] = t.materialize_batches;
+        d["materialize_errors"] = t.materialize_errors;
         return d;
       })
       .def("gpu_crc", [](ChunkStore& s, py::buffer data) {

@@ -14,6 +14,7 @@
 #include <cstring>
 #include <future>
 #include <stdexcept>
+#include <unordered_map>
 
 #include "crc32.h"
 #include "gf256.h"
@@ -147,6 +148,11 @@ int64_t file_size(const std::string& p) {
   return st.st_size;
 }
 
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::atoi(e) : dflt;
+}
+
 bool ends_with(const std::string& s, const std::string& suf) {
   return s.size() >= suf.size() && s.compare(s.size() - suf.size(), suf.size(), suf) == 0;
 }
@@ -211,10 +217,40 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     if (cfg_.durability == Durability::HbmAck)
       for (int i = 0; i < std::max(1, cfg_.spill_threads); ++i) spillers_.emplace_back([this] { spill_worker(); });
   }
+  int jmode = cfg_.journal;
+  if (jmode < 0) jmode = env_int("DFS_JOURNAL", 1);
+  if (jmode > 0 && cfg_.sync_writes && cfg_.durability == Durability::NvmeSync) {
+    JournalConfig jc;
+    jc.dir = cfg_.storage_dir + "/.journal";
+    jc.seg_bytes = static_cast<uint64_t>(env_int("DFS_JOURNAL_SEG_MB", 256)) << 20;
+    jc.max_segs = env_int("DFS_JOURNAL_SEGS", 16);
+    jc.direct = env_int("DFS_JOURNAL_DIRECT", 0) != 0;
+    jc.sync = cfg_.sync_writes;
+    mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 50) / 100.0;
+    mat_idle_ns_ = static_cast<uint64_t>(env_int("DFS_JOURNAL_IDLE_MS", 100)) * 1000000ull;
+    journal_ = std::make_unique<BlockJournal>(jc);
+    replay_journal();
+  }
   scan_dirs();
+  if (journal_) materializer_ = std::thread([this] { materializer_loop(); });
 }
 
 ChunkStore::~ChunkStore() {
+  if (materializer_.joinable()) {
+    {  // a clean stop writes every journal record out, so nothing is left to replay
+      std::lock_guard<std::mutex> g(mu_);
+      mat_stop_ = true;
+      mat_paused_ = false;
+    }
+    mat_cv_.notify_all();
+    materializer_.join();
+    bool drained;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      drained = mat_q_.empty() && mat_errors_ == 0;
+    }
+    if (drained && !journal_->stats().failed) journal_->retire_all();
+  }
   {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;
@@ -256,9 +292,18 @@ void ChunkStore::scan_dirs() {
         ::unlink((dir + "/" + name).c_str());
         continue;
       }
-      if (name == "." || name == ".." || ends_with(name, ".meta")) continue;
+      // dot names: the journal directory, quarantined files (block ids never start with '.')
+      if (name.empty() || name[0] == '.' || ends_with(name, ".meta")) continue;
       int64_t sz = file_size(dir + "/" + name);
       if (sz < 0) continue;
+      // a data file is a block only with its complete .meta beside it: anything else is a
+      // write torn by a crash, set aside instead of being reported as a present block
+      int64_t msz = file_size(dir + "/" + name + ".meta");
+      if (msz != static_cast<int64_t>(num_slices(static_cast<uint64_t>(sz)) * 4)) {
+        ::rename((dir + "/" + name).c_str(), (dir + "/.quarantine-" + name).c_str());
+        if (msz >= 0) ::rename((dir + "/" + name + ".meta").c_str(), (dir + "/.quarantine-" + name + ".meta").c_str());
+        continue;
+      }
       Block& b = index_[name];
       b.size = static_cast<uint64_t>(sz);
       b.on_disk = true;
@@ -304,7 +349,7 @@ int64_t ChunkStore::alloc_locked(std::unique_lock<std::mutex>& lk, uint64_t byte
     for (auto it = lru_.rbegin(); it != lru_.rend(); ++it) {
       Block& b = index_[*it];
       if (b.dirty) any_dirty = true;
-      if (b.pins == 0 && !b.dirty && b.on_disk && b.dev_off >= 0) {
+      if (b.pins == 0 && !b.dirty && (b.on_disk || b.jrec.seg) && b.dev_off >= 0) {
         free_extent_locked(b);
         lru_remove_locked(b);
         ++st_.evictions;
@@ -789,7 +834,7 @@ WriteResult ChunkStore::stage(const std::string& id, const uint8_t* data, uint64
 }
 
 void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t crc, bool on_disk,
-                                 std::shared_ptr<std::vector<uint8_t>> meta, int pins) {
+                                 std::shared_ptr<std::vector<uint8_t>> meta, int pins, const JournalRec* jr) {
   bool hbm_ack = cfg_.durability == Durability::HbmAck;
   {
     std::unique_lock<std::mutex> lk(mu_);
@@ -814,11 +859,57 @@ void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, ui
     b.dev_off = ext.off;
     b.dev_bytes = ext.bytes;
     b.pins = pins;
-    if (!on_disk && !hbm_ack) b.staged_meta = std::move(meta);
+    if (jr) {  // durable in the journal: clean, and queued for its own files
+      b.dirty = false;
+      b.jrec = *jr;
+      b.jmeta = std::move(meta);
+      enqueue_materialize_locked(id, b);
+    } else if (!on_disk && !hbm_ack) {
+      b.staged_meta = std::move(meta);
+    }
     touch_locked(id, b);
-    if (!on_disk && hbm_ack) spill_q_.push_back(id);
+    if (!on_disk && !jr && hbm_ack) spill_q_.push_back(id);
   }
   cv_.notify_all();
+}
+
+// H2D + checksum of a host buffer into `ext` on one lane; the BE .meta image comes back in
+// *meta_be and the whole-block CRC in co->block_crc.
+bool ChunkStore::device_stage(const uint8_t* data, uint64_t n, const DevExtent& ext, std::vector<uint8_t>* meta_be,
+                              CrcOut* co, std::string* err) {
+  Lane* l = acquire_lane();
+  uint64_t S = num_slices(n);
+  auto* dmeta = reinterpret_cast<uint32_t*>(ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
+  ensure_hscratch(l, S * 4 + 16);
+  uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+  bool ok = true;
+  static const bool fused_ok = [] {  // DFS_FUSED_WRITE=0: SDMA copy + checksum kernel (A/B)
+    const char* e = std::getenv("DFS_FUSED_WRITE");
+    return !(e && e[0] == '0');
+  }();
+  const uint8_t* src_dev =
+      fused_ok && n > kMirrorMax && crc_mfma_enabled() && l->hscratch_dev ? device_view(data, n) : nullptr;
+  if (src_dev && reinterpret_cast<uintptr_t>(src_dev) % 16 == 0) {
+    ok = write_copy(l, src_dev, ext.ptr, n, dmeta, hmeta, co, err);
+  } else if (h2d_chunked(l, ext.ptr, data, n) && n <= kMirrorMax) {
+    // a few slices: PCLMUL on the host bytes beats a kernel launch plus the .meta readback;
+    // the image goes up with the data in the same stream round trip
+    std::vector<uint32_t> sums(S);
+    crc32_slices(data, n, sums.data());
+    for (uint64_t i = 0; i < S; ++i) reinterpret_cast<uint32_t*>(hmeta)[i] = __builtin_bswap32(sums[i]);
+    co->block_crc = crc32_from_slices(sums.data(), n);
+    if (S) HIP_OK(hipMemcpyAsync(dmeta, hmeta, S * 4, hipMemcpyHostToDevice, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+  } else {
+    ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, co, err);
+    if (ok && S) {
+      HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+      HIP_OK(hipStreamSynchronize(l->stream));
+    }
+  }
+  if (ok) meta_be->assign(hmeta, hmeta + S * 4);
+  release_lane(l);
+  return ok;
 }
 
 // H2D (double-buffered pinned chunks) + fused K1/K2 kernel + D2H of the .meta image, then
@@ -835,6 +926,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
     return res;
   }
   bool sync_now = durable_now && cfg_.durability == Durability::NvmeSync;
+  if (sync_now && journal_ && journal_->fits(n, num_slices(n))) return stage_journal(id, data, n, expected_crc, ext);
   // nvme-sync: the data file (the slow part: page-cache write + device flush) is written
   // and fdatasync'ed on a helper thread WHILE the GPU stages and checksums the block; the
   // .meta (known only after the CRC kernel) follows. A checksum mismatch removes the file.
@@ -913,40 +1005,12 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
       unclaim_fresh(id);
     }
   };
-  Lane* l = acquire_lane();
   uint64_t S = num_slices(n);
-  auto* dmeta = reinterpret_cast<uint32_t*>(ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
-  ensure_hscratch(l, S * 4 + 16);
-  uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
   std::string err;
   CrcOut co;
-  bool ok = true;
-  static const bool fused_ok = [] {  // DFS_FUSED_WRITE=0: SDMA copy + checksum kernel (A/B)
-    const char* e = std::getenv("DFS_FUSED_WRITE");
-    return !(e && e[0] == '0');
-  }();
-  const uint8_t* src_dev =
-      fused_ok && n > kMirrorMax && crc_mfma_enabled() && l->hscratch_dev ? device_view(data, n) : nullptr;
-  if (src_dev && reinterpret_cast<uintptr_t>(src_dev) % 16 == 0) {
-    ok = write_copy(l, src_dev, ext.ptr, n, dmeta, hmeta, &co, &err);
-  } else if (h2d_chunked(l, ext.ptr, data, n) && n <= kMirrorMax) {
-    // a few slices: PCLMUL on the host bytes beats a kernel launch plus the .meta readback;
-    // the image goes up with the data in the same stream round trip
-    std::vector<uint32_t> sums(S);
-    crc32_slices(data, n, sums.data());
-    for (uint64_t i = 0; i < S; ++i) reinterpret_cast<uint32_t*>(hmeta)[i] = __builtin_bswap32(sums[i]);
-    co.block_crc = crc32_from_slices(sums.data(), n);
-    if (S) HIP_OK(hipMemcpyAsync(dmeta, hmeta, S * 4, hipMemcpyHostToDevice, l->stream));
-    HIP_OK(hipStreamSynchronize(l->stream));
-  } else {
-    ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err);
-    if (ok && S) {
-      HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
-      HIP_OK(hipStreamSynchronize(l->stream));
-    }
-  }
+  auto meta = std::make_shared<std::vector<uint8_t>>();
+  bool ok = device_stage(data, n, ext, meta.get(), &co, &err);
   if (!ok) {
-    release_lane(l);
     release(ext);
     abandon_data_file();
     res.error = err;
@@ -954,7 +1018,6 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   }
   res.actual_crc = co.block_crc;
   if (expected_crc != 0 && co.block_crc != expected_crc) {
-    release_lane(l);
     release(ext);
     abandon_data_file();
     {
@@ -965,8 +1028,6 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
                 std::to_string(co.block_crc);
     return res;
   }
-  auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
-  release_lane(l);
   if (fresh) {
     bool mok = write_fd_durable(mfd, meta->data(), S * 4, "write " + mp_tmp, &err);
     bool dok = data_file.get();
@@ -1092,6 +1153,7 @@ bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64
   std::shared_ptr<std::vector<uint8_t>> meta;
   const uint8_t* d = nullptr;
   uint64_t size = 0;
+  uint32_t crc = 0;
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = index_.find(id);
@@ -1107,24 +1169,41 @@ bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64
     }
     meta = b.staged_meta;
     size = b.size;
+    crc = b.crc;
     d = arena_ + b.dev_off;
     b.pins++;
   }
-  bool ok;
-  if (host_data && n == size) ok = persist(id, false, host_data, size, meta->data(), meta->size() / 4, err);
-  else ok = persist_from_device(id, d, size, meta->data(), meta->size() / 4, err);
+  bool ok, jok = false;
+  JournalRec jr;
+  const bool from_host = host_data && n == size;
+  if (journal_ && journal_->fits(size, meta->size() / 4)) {
+    ok = jok = journal_block(id, from_host ? host_data : nullptr, from_host ? nullptr : d, size, crc, *meta, &jr, err);
+  } else if (from_host) {
+    ok = persist(id, false, host_data, size, meta->data(), meta->size() / 4, err);
+  } else {
+    ok = persist_from_device(id, d, size, meta->data(), meta->size() / 4, err);
+  }
+  bool obsolete = jok;
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = index_.find(id);
     if (it != index_.end()) {
       it->second.pins--;
       if (ok && it->second.staged_meta == meta) {
-        it->second.on_disk = true;
         it->second.dirty = false;
         it->second.staged_meta.reset();
+        if (jok) {
+          it->second.jrec = jr;
+          it->second.jmeta = meta;
+          enqueue_materialize_locked(id, it->second);
+          obsolete = false;
+        } else {
+          it->second.on_disk = true;
+        }
       }
     }
   }
+  if (obsolete) journal_->materialized(jr.seg, 1);  // the block changed meanwhile: record unused
   cv_.notify_all();
   return ok;
 }
@@ -1186,13 +1265,24 @@ WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, u
   crc32_slices(data, n, sl.data());
   for (auto& v : sl) v = __builtin_bswap32(v);
   std::string err;
-  if (!persist(id, false, data, n, reinterpret_cast<const uint8_t*>(sl.data()), S, &err)) {
+  JournalRec jr;
+  std::shared_ptr<std::vector<uint8_t>> jmeta;
+  const bool jok = journal_ && journal_->fits(n, S);
+  if (jok) {
+    jmeta = std::make_shared<std::vector<uint8_t>>(reinterpret_cast<const uint8_t*>(sl.data()),
+                                                   reinterpret_cast<const uint8_t*>(sl.data()) + S * 4);
+    if (!journal_block(id, data, nullptr, n, actual, *jmeta, &jr, &err)) {
+      res.error = err;
+      return res;
+    }
+  } else if (!persist(id, false, data, n, reinterpret_cast<const uint8_t*>(sl.data()), S, &err)) {
     res.error = err;
     return res;
   }
   {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> lk(mu_);
     auto it = index_.find(id);
+    if (it != index_.end()) cv_.wait(lk, [&] { return it->second.pins == 0; });  // materializer / readers
     if (it != index_.end() && it->second.cold) {
       ::unlink(data_path(id, true).c_str());
       ::unlink(meta_path(id, true).c_str());
@@ -1203,8 +1293,14 @@ WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, u
     b.size = n;
     b.crc = actual;
     b.crc_known = true;
-    b.on_disk = true;
+    b.on_disk = !jok;
+    if (jok) {
+      b.jrec = jr;
+      b.jmeta = std::move(jmeta);
+      enqueue_materialize_locked(id, b);
+    }
   }
+  cv_.notify_all();
   res.ok = true;
   return res;
 }
@@ -1330,6 +1426,8 @@ ReadResult ChunkStore::read_host(const std::string& id, uint64_t offset, uint64_
   bool cold = false;
   uint64_t size = 0;
   bool full = false;
+  JournalRec jrec;
+  std::shared_ptr<std::vector<uint8_t>> jmeta;
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = index_.find(id);
@@ -1354,26 +1452,29 @@ ReadResult ChunkStore::read_host(const std::string& id, uint64_t offset, uint64_
       r.bytes = bytes;
       return r;
     }
+    jrec = b.jrec;
+    jmeta = b.jmeta;
+    if (jrec.seg) jrec.seg->readers++;  // released by DurableSrc
   }
-  std::string dp = data_path(id, cold);
-  int fd = ::open(dp.c_str(), O_RDONLY | O_CLOEXEC);
-  if (fd < 0) {
+  DurableSrc src;
+  const bool opened = open_durable(id, cold, jrec, jmeta, &src);
+  if (src.fd < 0) {
     r.status = errno == ENOENT ? ReadStatus::NotFound : ReadStatus::IoError;
     r.error = errno == ENOENT ? "Block not found" : errno_str("Failed to read block");
     return r;
   }
-  bool ok = read_all(fd, out, bytes, offset);
+  const int fd = src.fd;
+  const uint64_t base = src.base;
+  bool ok = read_all(fd, out, bytes, base + offset);
   if (!ok) {
-    ::close(fd);
     r.status = ReadStatus::IoError;
     r.error = errno_str("Failed to read block");
     return r;
   }
   r.bytes = bytes;
-  bool mok = false;
-  std::vector<uint32_t> meta = load_meta_file(id, cold, &mok);
+  bool mok = opened && src.meta_ok;
+  std::vector<uint32_t>& meta = src.meta;
   if (!mok) {
-    ::close(fd);
     r.error = "Checksum file missing";
     if (full) r.status = ReadStatus::Corrupt;
     else r.partial_corrupt = true;
@@ -1416,7 +1517,7 @@ ReadResult ChunkStore::read_host(const std::string& id, uint64_t offset, uint64_
     std::vector<uint8_t> buf(kSliceBytes);
     for (uint64_t s = first; s <= last && s < meta.size(); ++s) {
       uint64_t so = s * kSliceBytes, sl = std::min<uint64_t>(kSliceBytes, size - so);
-      if (!read_all(fd, buf.data(), sl, so)) break;
+      if (!read_all(fd, buf.data(), sl, base + so)) break;
       if (crc32(buf.data(), sl) != meta[s]) {
         r.partial_corrupt = true;
         r.bad_slice = static_cast<int64_t>(s);
@@ -1427,7 +1528,6 @@ ReadResult ChunkStore::read_host(const std::string& id, uint64_t offset, uint64_
       }
     }
   }
-  ::close(fd);
   return r;
 }
 
@@ -1457,6 +1557,8 @@ void ChunkStore::release(const DevExtent& e) {
 bool ChunkStore::promote(const std::string& id, std::string* err) {
   uint64_t size = 0;
   bool cold = false;
+  JournalRec jrec;
+  std::shared_ptr<std::vector<uint8_t>> jmeta;
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = index_.find(id);
@@ -1465,19 +1567,22 @@ bool ChunkStore::promote(const std::string& id, std::string* err) {
       return false;
     }
     if (it->second.dev_off >= 0) return true;
-    if (!it->second.on_disk) {
+    if (!it->second.on_disk && !it->second.jrec.seg) {
       *err = "block neither resident nor on disk";
       return false;
     }
     size = it->second.size;
     cold = it->second.cold;
+    jrec = it->second.jrec;
+    jmeta = it->second.jmeta;
+    if (jrec.seg) jrec.seg->readers++;  // released by DurableSrc
   }
-  bool mok = false;
-  std::vector<uint32_t> meta = load_meta_file(id, cold, &mok);
-  if (!mok) {
-    *err = "Checksum file missing";
+  DurableSrc src;
+  if (!open_durable(id, cold, jrec, jmeta, &src)) {
+    *err = src.meta_ok ? "Block not found" : "Checksum file missing";
     return false;
   }
+  std::vector<uint32_t>& meta = src.meta;
   uint64_t S = num_slices(size);
   if (meta.size() != S) {
     *err = "Checksum count mismatch";
@@ -1488,27 +1593,19 @@ bool ChunkStore::promote(const std::string& id, std::string* err) {
     *err = "HBM arena full";
     return false;
   }
-  std::string dp = data_path(id, cold);
-  int fd = ::open(dp.c_str(), O_RDONLY | O_CLOEXEC);
-  if (fd < 0) {
-    release(ext);
-    *err = "Block not found";
-    return false;
-  }
   Lane* l = acquire_lane();
   bool ok = true;
   int i = 0;
   for (uint64_t off = 0; off < size; off += kChunk, i ^= 1) {
     uint64_t len = std::min<uint64_t>(kChunk, size - off);
     HIP_OK(hipEventSynchronize(l->ev[i]));
-    if (!read_all(fd, l->pinned[i], len, off)) {
+    if (!read_all(src.fd, l->pinned[i], len, src.base + off)) {
       ok = false;
       break;
     }
     HIP_OK(hipMemcpyAsync(ext.ptr + off, l->pinned[i], len, hipMemcpyHostToDevice, l->stream));
     HIP_OK(hipEventRecord(l->ev[i], l->stream));
   }
-  ::close(fd);
   ensure_hscratch(l, S * 4 + 16);
   uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
   for (uint64_t s = 0; s < S; ++s) reinterpret_cast<uint32_t*>(hmeta)[s] = __builtin_bswap32(meta[s]);
@@ -1605,12 +1702,15 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
     return res;
   }
   bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
-  if (sync_now && !persist_from_device(id, ext.ptr, n, meta->data(), S, &err)) {
+  JournalRec jr;
+  const bool jok = sync_now && journal_ && journal_->fits(n, S);
+  if (jok ? !journal_block(id, nullptr, ext.ptr, n, co.block_crc, *meta, &jr, &err)
+          : sync_now && !persist_from_device(id, ext.ptr, n, meta->data(), S, &err)) {
     release(ext);
     res.error = err;
     return res;
   }
-  insert_resident(id, ext, n, co.block_crc, sync_now, meta);
+  insert_resident(id, ext, n, co.block_crc, sync_now && !jok, meta, 0, jok ? &jr : nullptr);
   res.ok = true;
   return res;
 }
@@ -1679,12 +1779,15 @@ WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint3
   }
   std::string err;
   bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
-  if (sync_now && !persist_from_device(id, rv->ext.ptr, n, meta->data(), S, &err)) {
+  JournalRec jr;
+  const bool jok = sync_now && journal_ && journal_->fits(n, S);
+  if (jok ? !journal_block(id, nullptr, rv->ext.ptr, n, crc, *meta, &jr, &err)
+          : sync_now && !persist_from_device(id, rv->ext.ptr, n, meta->data(), S, &err)) {
     release(rv->ext);
     res.error = err;
     return res;
   }
-  insert_resident(id, rv->ext, n, crc, sync_now, meta);
+  insert_resident(id, rv->ext, n, crc, sync_now && !jok, meta, 0, jok ? &jr : nullptr);
   res.ok = true;
   return res;
 }
@@ -1839,6 +1942,8 @@ bool ChunkStore::remove(const std::string& id) {
     index_.erase(it);
   }
   cv_.notify_all();
+  // an unretired journal record of the block would bring it back on replay
+  if (journal_) journal_->tombstone(id);
   ::unlink(data_path(id, cold).c_str());
   ::unlink(meta_path(id, cold).c_str());
   return true;
@@ -1849,6 +1954,13 @@ bool ChunkStore::move_to_cold(const std::string& id) {
   std::unique_lock<std::mutex> lk(mu_);
   auto it = index_.find(id);
   if (it == index_.end() || it->second.cold) return false;
+  if (it->second.jrec.seg) {  // its own files first
+    lk.unlock();
+    materialize_all();
+    lk.lock();
+    it = index_.find(id);
+    if (it == index_.end() || it->second.jrec.seg) return false;
+  }
   if (it->second.dirty) {
     lk.unlock();
     flush();
@@ -1874,23 +1986,32 @@ bool ChunkStore::move_to_cold(const std::string& id) {
 
 std::string ChunkStore::verify_on_disk(const std::string& id) {
   bool cold = false;
+  JournalRec jrec;
+  std::shared_ptr<std::vector<uint8_t>> jmeta;
+  int64_t sz = -1;
   {
     std::lock_guard<std::mutex> g(mu_);
     auto it = index_.find(id);
-    if (it != index_.end()) cold = it->second.cold;
-    else if (!cfg_.cold_dir.empty() && file_exists(data_path(id, true))) cold = true;
+    if (it != index_.end()) {
+      cold = it->second.cold;
+      jrec = it->second.jrec;
+      jmeta = it->second.jmeta;
+      if (jrec.seg) jrec.seg->readers++;  // released by DurableSrc
+      if (jrec.seg) sz = static_cast<int64_t>(it->second.size);
+    } else if (!cfg_.cold_dir.empty() && file_exists(data_path(id, true))) {
+      cold = true;
+    }
   }
-  bool mok = false;
-  auto meta = load_meta_file(id, cold, &mok);
-  if (!mok) return "Checksum file missing";
-  std::string dp = data_path(id, cold);
-  int64_t sz = file_size(dp);
-  if (sz < 0) return "Block not found";
+  DurableSrc src;
+  if (!open_durable(id, cold, jrec, jmeta, &src)) return src.fd < 0 ? "Block not found" : "Checksum file missing";
+  auto& meta = src.meta;
+  if (!jrec.seg) {
+    struct stat stt;
+    if (::fstat(src.fd, &stt) != 0) return "Block not found";
+    sz = stt.st_size;
+  }
   std::vector<uint8_t> data(static_cast<size_t>(sz));
-  int fd = ::open(dp.c_str(), O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return "Block not found";
-  bool ok = read_all(fd, data.data(), data.size(), 0);
-  ::close(fd);
+  bool ok = read_all(src.fd, data.data(), data.size(), src.base);
   if (!ok && sz > 0) return "read failed";
   std::vector<uint32_t> act(num_slices(data.size()));
   crc32_slices(data.data(), data.size(), act.data());
@@ -1922,6 +2043,19 @@ std::vector<uint32_t> ChunkStore::meta(const std::string& id) {
     for (auto& v : m) v = __builtin_bswap32(v);
     unpin(id);
     return m;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end() && it->second.jmeta) {
+      std::vector<uint32_t> m(it->second.jmeta->size() / 4);
+      for (size_t i = 0; i < m.size(); ++i) {
+        uint32_t be;
+        std::memcpy(&be, it->second.jmeta->data() + 4 * i, 4);
+        m[i] = __builtin_bswap32(be);
+      }
+      return m;
+    }
   }
   bool ok = false;
   return load_meta_file(id, cold, &ok);
@@ -2000,7 +2134,7 @@ std::vector<std::string> ChunkStore::scrub() {
       if (gpu() && kv.second.dev_off >= 0) {
         kv.second.pins++;
         resident.push_back(kv.first);
-      } else if (kv.second.on_disk) {
+      } else if (kv.second.on_disk || kv.second.jrec.seg) {
         disk.push_back(kv.first);
       }
     }
@@ -2018,7 +2152,7 @@ std::vector<std::string> ChunkStore::scrub() {
       {
         std::lock_guard<std::mutex> g(mu_);
         auto it = index_.find(id);
-        on_disk = it != index_.end() && it->second.on_disk && !it->second.dirty;
+        on_disk = it != index_.end() && (it->second.on_disk || it->second.jrec.seg) && !it->second.dirty;
       }
       if (on_disk && std::find(bad.begin(), bad.end(), id) == bad.end() && !verify_on_disk(id).empty())
         bad.push_back(id);
@@ -2060,6 +2194,27 @@ StoreStats ChunkStore::stats() {
   s.mirror_hits = mirror_hits_;
   s.mirror_bytes = mirror_bytes_;
   s.io_threads_spawned = io_.spawned();
+  if (journal_) {
+    JournalStats j = journal_->stats();
+    s.journal = true;
+    s.journal_records = j.records;
+    s.journal_bytes = j.bytes;
+    s.journal_commits = j.commits;
+    s.journal_sync_rounds = j.sync_rounds;
+    s.journal_tombstones = j.tombstones;
+    s.journal_full_waits = j.full_waits;
+    s.journal_segs = j.segs_total;
+    s.journal_segs_free = j.segs_free;
+    s.journal_segs_retired = j.segs_retired;
+    s.journal_replayed = j.replayed;
+    s.journal_replay_skipped = j.replay_skipped;
+    s.journal_failed = j.failed;
+    s.materialized_blocks = materialized_blocks_;
+    s.materialized_bytes = materialized_bytes_;
+    s.materialize_pending = mat_q_.size();
+    s.materialize_batches = mat_batches_;
+    s.materialize_errors = mat_errors_;
+  }
   {
     std::lock_guard<std::mutex> rg(reg_mu_);
     for (auto& r : reg_) s.host_registered_bytes += r.second;
@@ -2081,7 +2236,7 @@ void ChunkStore::drop_resident() {
   std::lock_guard<std::mutex> g(mu_);
   for (auto& kv : index_) {
     Block& b = kv.second;
-    if (b.pins == 0 && !b.dirty && b.on_disk) {
+    if (b.pins == 0 && !b.dirty && (b.on_disk || b.jrec.seg)) {
       free_extent_locked(b);
       lru_remove_locked(b);
       b.host.reset();
@@ -2102,6 +2257,15 @@ bool ChunkStore::debug_corrupt(const std::string& id, uint64_t offset) {
     size = it->second.size;
     if (it->second.host) (*it->second.host)[offset] ^= 0xFF;
     if (it->second.mirror) (*it->second.mirror)[offset] ^= 0xFF;
+    if (it->second.jrec.seg) {
+      uint8_t c = 0;
+      const int jfd = it->second.jrec.seg->fd;
+      const uint64_t at = it->second.jrec.data_off() + offset;
+      if (read_all(jfd, &c, 1, at)) {
+        c ^= 0xFF;
+        write_all(jfd, &c, 1, at);
+      }
+    }
   }
   (void)size;
   std::string dp = data_path(id, cold);
@@ -2213,6 +2377,381 @@ uint32_t ChunkStore::gpu_crc(const uint8_t* data, uint64_t n, std::vector<uint32
   release(ext);
   if (!ok) throw std::runtime_error(err);
   return co.block_crc;
+}
+
+
+// ---------------------------------------------------------------- block journal
+ChunkStore::DurableSrc::~DurableSrc() {
+  if (own_fd && fd >= 0) ::close(fd);
+  if (seg) seg->readers--;
+}
+
+// `jrec.seg`, when set, was captured under mu_ with its reader count raised (the segment
+// cannot retire until this DurableSrc lets go of it).
+bool ChunkStore::open_durable(const std::string& id, bool cold, const JournalRec& jrec,
+                              const std::shared_ptr<std::vector<uint8_t>>& jmeta, DurableSrc* s) {
+  if (jrec.seg) {
+    s->seg = jrec.seg;
+    s->fd = jrec.seg->fd;
+    s->base = jrec.data_off();
+    s->meta_ok = jmeta != nullptr;
+    if (jmeta) {
+      s->meta.resize(jmeta->size() / 4);
+      for (size_t i = 0; i < s->meta.size(); ++i) {
+        uint32_t be;
+        std::memcpy(&be, jmeta->data() + 4 * i, 4);
+        s->meta[i] = __builtin_bswap32(be);
+      }
+    }
+    return s->meta_ok;
+  }
+  s->fd = ::open(data_path(id, cold).c_str(), O_RDONLY | O_CLOEXEC);
+  if (s->fd < 0) return false;
+  s->own_fd = true;
+  s->meta = load_meta_file(id, cold, &s->meta_ok);
+  return s->meta_ok;
+}
+
+bool ChunkStore::journal_block(const std::string& id, const uint8_t* host, const uint8_t* dev, uint64_t n,
+                               uint32_t crc, const std::vector<uint8_t>& meta_be, JournalRec* out, std::string* err) {
+  TraceRange tr("dfs.store.journal");
+  const uint64_t S = meta_be.size() / 4;
+  JournalRec jr;
+  bool ok = true;
+  if (dev) {
+    // out of HBM through the lane's two pinned chunks: the D2H of chunk c+1 overlaps the
+    // append of chunk c. The lane is taken before the record so a writer never holds a
+    // reserved record while it waits for a lane (commit() waits on earlier records).
+    HIP_OK(hipSetDevice(cfg_.device));
+    Lane* l = acquire_lane();
+    if (!journal_->reserve(n, S, &jr, err)) {
+      release_lane(l);
+      return false;
+    }
+    const uint64_t nch = (n + kChunk - 1) / kChunk;
+    auto issue = [&](uint64_t c) {
+      const uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
+      HIP_OK(hipMemcpyAsync(l->pinned[c & 1], dev + off, len, hipMemcpyDeviceToHost, l->stream));
+      HIP_OK(hipEventRecord(l->ev[c & 1], l->stream));
+    };
+    if (nch) issue(0);
+    for (uint64_t c = 0; c < nch; ++c) {
+      if (c + 1 < nch) issue(c + 1);
+      HIP_OK(hipEventSynchronize(l->ev[c & 1]));
+      const uint64_t off = c * kChunk, len = std::min<uint64_t>(kChunk, n - off);
+      if (ok) ok = journal_->write(jr, off, l->pinned[c & 1], len);
+    }
+    release_lane(l);
+  } else {
+    if (!journal_->reserve(n, S, &jr, err)) return false;
+    ok = journal_->write(jr, 0, host, n);
+  }
+  if (!ok) {
+    *err = errno_str("journal append");
+    journal_->abandon(jr);
+    return false;
+  }
+  if (!journal_->finish(jr, id, n, crc, meta_be.data(), S) || !journal_->commit(jr)) {
+    *err = "journal commit failed";
+    journal_->materialized(jr.seg, 1);  // never indexed
+    return false;
+  }
+  *out = jr;
+  return true;
+}
+
+// The nvme-sync head write with the journal: the block bytes are appended to the reserved
+// record (from the caller's buffer, on an I/O thread) while the GPU stages and checksums
+// them; the header + .meta image follow once the kernel has produced them, and one group
+// commit makes the record durable. The block is acked resident in HBM and durable in the
+// journal; its `<id>` + `<id>.meta` files are written later by the materializer.
+WriteResult ChunkStore::stage_journal(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
+                                      const DevExtent& ext) {
+  WriteResult res;
+  const uint64_t S = num_slices(n);
+  JournalRec jr;
+  std::string err;
+  if (!journal_->reserve(n, S, &jr, &err)) {
+    release(ext);
+    res.error = err;
+    return res;
+  }
+  std::future<bool> wf;
+  bool wok = true;
+  if (n <= kMirrorMax) wok = journal_->write(jr, 0, data, n);  // a thread hand-off costs more
+  else wf = io_.submit([this, &jr, data, n] { return journal_->write(jr, 0, data, n); });
+  CrcOut co;
+  auto meta = std::make_shared<std::vector<uint8_t>>();
+  bool ok = device_stage(data, n, ext, meta.get(), &co, &err);
+  if (wf.valid()) wok = wf.get();
+  res.actual_crc = co.block_crc;
+  const bool mismatch = ok && expected_crc != 0 && co.block_crc != expected_crc;
+  if (!ok || mismatch || !wok) {
+    journal_->abandon(jr);
+    release(ext);
+    if (mismatch) {
+      std::lock_guard<std::mutex> g(mu_);
+      ++st_.crc_mismatches;
+      res.error = "Checksum mismatch: expected " + std::to_string(expected_crc) + ", actual " +
+                  std::to_string(co.block_crc);
+    } else {
+      res.error = ok ? errno_str("journal append") : err;
+    }
+    return res;
+  }
+  if (!journal_->finish(jr, id, n, co.block_crc, meta->data(), S) || !journal_->commit(jr)) {
+    journal_->materialized(jr.seg, 1);
+    release(ext);
+    res.error = "journal commit failed";
+    return res;
+  }
+  insert_resident(id, ext, n, co.block_crc, false, meta, 0, &jr);
+  if (n <= kMirrorMax) set_mirror(id, data, n, *meta);
+  res.ok = true;
+  return res;
+}
+
+void ChunkStore::enqueue_materialize_locked(const std::string& id, const Block& b) {
+  mat_q_.push_back(MatItem{id, b.jrec, b.size, b.jmeta});
+  mat_cv_.notify_all();
+}
+
+// Materialization competes with the acked writes for the volume, so it runs when the
+// journal fills up (pressure) or when the writers pause (idle), not on every append.
+bool ChunkStore::materialize_due() {
+  if (mat_idle_ns_ == 0) return true;
+  if (journal_->pressure() >= mat_pressure_) return true;
+  const uint64_t now = static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                                 std::chrono::steady_clock::now().time_since_epoch())
+                                                 .count());
+  return now - journal_->last_append_ns() >= mat_idle_ns_;
+}
+
+namespace {
+// The record's bytes into a fresh file: copy_file_range keeps them in the kernel (page
+// cache to page cache, or a reflink where the filesystem shares extents).
+bool copy_range(int in_fd, uint64_t in_off, int out_fd, uint64_t n) {
+  loff_t io = static_cast<loff_t>(in_off), oo = 0;
+  uint64_t left = n;
+  while (left) {
+    ssize_t r = ::copy_file_range(in_fd, &io, out_fd, &oo, left, 0);
+    if (r > 0) {
+      left -= static_cast<uint64_t>(r);
+      continue;
+    }
+    if (r < 0 && errno == EINTR) continue;
+    break;  // unsupported here (EXDEV / ENOSYS / EINVAL): plain reads and writes
+  }
+  if (!left) return true;
+  std::vector<uint8_t> buf(std::min<uint64_t>(left, 4ull << 20));
+  while (left) {
+    const uint64_t len = std::min<uint64_t>(left, buf.size());
+    if (!read_all(in_fd, buf.data(), len, static_cast<uint64_t>(io)) ||
+        !write_all(out_fd, buf.data(), len, static_cast<uint64_t>(oo)))
+      return false;
+    io += len;
+    oo += len;
+    left -= len;
+  }
+  return true;
+}
+}  // namespace
+
+void ChunkStore::materializer_loop() {
+  struct Job {
+    MatItem m;
+    bool current = false, ok = false;
+    int fd = -1, mfd = -1;
+  };
+  std::vector<Job> batch;
+  for (;;) {
+    batch.clear();
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      for (;;) {
+        if (mat_q_.empty()) {
+          mat_cv_.notify_all();  // materialize_all() waiters
+          if (mat_stop_) return;
+          mat_cv_.wait_for(lk, std::chrono::milliseconds(200));
+          if (mat_q_.empty()) {
+            lk.unlock();
+            journal_->retire_ready();  // segments whose readers have finished since
+            lk.lock();
+          }
+          continue;
+        }
+        if (!mat_paused_ && (mat_stop_ || mat_force_ > 0 || materialize_due())) break;
+        mat_cv_.wait_for(lk, std::chrono::milliseconds(mat_paused_ ? 50 : 5));
+      }
+      uint64_t bytes = 0;
+      while (!mat_q_.empty() && batch.size() < 1024 && bytes < (256ull << 20)) {
+        Job j;
+        j.m = std::move(mat_q_.front());
+        mat_q_.pop_front();
+        bytes += j.m.n;
+        auto it = index_.find(j.m.id);
+        // pinned while its files are written: a rewrite or remove() of the id waits for it
+        j.current = it != index_.end() && it->second.jrec.seg == j.m.rec.seg && it->second.jrec.off == j.m.rec.off;
+        if (j.current) it->second.pins++;
+        batch.push_back(std::move(j));
+      }
+      mat_busy_ = true;
+    }
+    TraceRange tr("dfs.store.materialize");
+    for (auto& j : batch) {
+      if (!j.current) continue;
+      const std::string dp = data_path(j.m.id, false), mp = meta_path(j.m.id, false);
+      j.fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      j.mfd = j.fd < 0 ? -1 : ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+      j.ok = j.mfd >= 0 && copy_range(j.m.rec.seg->fd, j.m.rec.data_off(), j.fd, j.m.n) &&
+             write_all(j.mfd, j.m.meta->data(), j.m.meta->size(), 0);
+    }
+    // one flush pass for the whole batch: the file flushes in parallel, then the directory
+    const size_t nthreads = std::min<size_t>(8, std::max<size_t>(1, batch.size() / 4));
+    std::vector<std::future<void>> fl;
+    for (size_t t = 0; t < nthreads; ++t)
+      fl.push_back(io_.submit([&batch, t, nthreads] {
+        for (size_t i = t; i < batch.size(); i += nthreads) {
+          Job& j = batch[i];
+          if (!j.ok) continue;
+          j.ok = ::fdatasync(j.fd) == 0 && ::fdatasync(j.mfd) == 0;
+        }
+      }));
+    for (auto& f : fl) f.get();
+    bool any = false;
+    for (auto& j : batch) any = any || j.ok;
+    const bool dir_ok = !any || sync_dir(false);
+    const bool drop = gpu();
+    for (auto& j : batch) {
+      if (j.fd >= 0) {
+        if (drop) drop_cached(j.fd);
+        ::close(j.fd);
+      }
+      if (j.mfd >= 0) ::close(j.mfd);
+      if (!dir_ok) j.ok = false;
+    }
+    std::vector<Job*> retry;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& j : batch) {
+        if (!j.current) continue;
+        auto it = index_.find(j.m.id);
+        if (it != index_.end()) {
+          it->second.pins--;
+          if (j.ok) {
+            it->second.on_disk = true;
+            it->second.jrec = JournalRec{};
+            it->second.jmeta.reset();
+            ++materialized_blocks_;
+            materialized_bytes_ += j.m.n;
+          }
+        }
+        if (!j.ok) {
+          ++mat_errors_;
+          retry.push_back(&j);
+        }
+      }
+      for (auto* j : retry) mat_q_.push_back(j->m);  // the record stays live until its files are durable
+      ++mat_batches_;
+      mat_busy_ = false;
+    }
+    cv_.notify_all();
+    mat_cv_.notify_all();
+    for (auto& j : batch)
+      if (!j.current || j.ok) journal_->materialized(j.m.rec.seg, 1);
+    if (!retry.empty()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  }
+}
+
+void ChunkStore::materialize_all() {
+  if (!journal_) return;
+  std::unique_lock<std::mutex> lk(mu_);
+  if (mat_paused_) return;
+  ++mat_force_;
+  mat_cv_.notify_all();
+  mat_cv_.wait(lk, [&] { return (mat_q_.empty() && !mat_busy_) || mat_paused_ || mat_stop_; });
+  --mat_force_;
+}
+
+void ChunkStore::debug_pause_materializer(bool on) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    mat_paused_ = on;
+  }
+  mat_cv_.notify_all();
+}
+
+bool ChunkStore::journaled(const std::string& id) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = index_.find(id);
+  return it != index_.end() && it->second.jrec.seg != nullptr;
+}
+
+// Restart: the records of unretired segments, latest state per block id, are verified
+// (slice CRCs of the data against the record's .meta image and the whole-block CRC; on the
+// GPU by the K1/K2 kernels) and written out as `<id>` + `<id>.meta`; tombstoned ids lose
+// their files. Then every segment is retired and scan_dirs() indexes the result.
+void ChunkStore::replay_journal() {
+  std::vector<ReplayRecord> recs = journal_->recover();
+  std::unordered_map<std::string, long> last;  // id -> index of its final record (-1: deleted)
+  for (size_t i = 0; i < recs.size(); ++i)
+    last[recs[i].id] = recs[i].type == kJrBlock ? static_cast<long>(i) : -1;
+  uint64_t replayed = 0, skipped = 0;
+  bool cold_touched = false;
+  std::vector<uint8_t> buf;
+  std::string err;
+  for (auto& kv : last) {
+    const std::string& id = kv.first;
+    if (!valid_block_id(id)) {
+      ++skipped;
+      continue;
+    }
+    if (!cfg_.cold_dir.empty() && file_exists(data_path(id, true))) {
+      // the journal holds the latest write of the id: it replaces a cold copy
+      ::unlink(data_path(id, true).c_str());
+      ::unlink(meta_path(id, true).c_str());
+      cold_touched = true;
+    }
+    if (kv.second < 0) {
+      ::unlink(data_path(id, false).c_str());
+      ::unlink(meta_path(id, false).c_str());
+      continue;
+    }
+    const ReplayRecord& r = recs[static_cast<size_t>(kv.second)];
+    buf.resize(r.n);
+    if (!read_all(r.seg->fd, buf.data(), r.n, r.data_off) && r.n) {
+      ++skipped;
+      continue;
+    }
+    std::vector<uint32_t> sl;
+    uint32_t whole;
+    if (gpu() && r.n > kMirrorMax) {
+      whole = gpu_crc(buf.data(), r.n, &sl);
+    } else {
+      sl.resize(num_slices(r.n));
+      crc32_slices(buf.data(), r.n, sl.data());
+      whole = crc32_from_slices(sl.data(), r.n);
+    }
+    bool good = whole == r.crc && sl.size() * 4 == r.meta_be.size();
+    for (size_t i = 0; good && i < sl.size(); ++i) {
+      uint32_t be;
+      std::memcpy(&be, r.meta_be.data() + 4 * i, 4);
+      good = __builtin_bswap32(be) == sl[i];
+    }
+    if (!good) {  // torn: never acknowledged (prefix order), so dropping it loses nothing
+      ++skipped;
+      continue;
+    }
+    if (!write_file_durable(data_path(id, false), buf.data(), r.n, &err) ||
+        !write_file_durable(meta_path(id, false), r.meta_be.data(), r.meta_be.size(), &err)) {
+      throw std::runtime_error("journal replay: " + err);
+    }
+    ++replayed;
+  }
+  if (!sync_dir(false) || (cold_touched && !sync_dir(true))) throw std::runtime_error("journal replay: directory sync");
+  journal_->note_replay(replayed, skipped);
+  recs.clear();
+  journal_->retire_all();
 }
 
 }  // namespace dfs

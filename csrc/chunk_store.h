@@ -34,6 +34,7 @@
 #include "extent_alloc.h"
 #include "gpu_kernels.h"
 #include "io_pool.h"
+#include "journal.h"
 
 namespace dfs {
 
@@ -49,6 +50,8 @@ struct StoreConfig {
   int lanes = 8;                 // concurrent GPU stream contexts
   int spill_threads = 4;
   bool sync_writes = true;       // fdatasync data + .meta
+  int journal = -1;              // group-committed block journal for nvme-sync writes (journal.h):
+                                 // -1: DFS_JOURNAL (default on), 0: per-file fdatasync, 1: on
   int disk_inflight = -1;        // node-wide cap on durable writes per filesystem (disk_gate.h);
                                  // -1: DFS_DISK_INFLIGHT (default 12), 0: ungated
 };
@@ -94,6 +97,14 @@ struct StoreStats {
   uint64_t io_threads_spawned = 0;  // helper threads ever started (steady state: none per write)
   uint64_t final_name_writes = 0;   // durable writes of fresh ids straight to their final names
   uint64_t direct_writes = 0;       // of those, data files written with O_DIRECT (DFS_ODIRECT=1)
+  // block journal (journal.h): group-committed durable writes + background materializer
+  bool journal = false;
+  uint64_t journal_records = 0, journal_bytes = 0, journal_commits = 0, journal_sync_rounds = 0;
+  uint64_t journal_tombstones = 0, journal_full_waits = 0, journal_segs = 0, journal_segs_free = 0;
+  uint64_t journal_segs_retired = 0, journal_replayed = 0, journal_replay_skipped = 0;
+  uint64_t materialized_blocks = 0, materialized_bytes = 0, materialize_pending = 0, materialize_batches = 0;
+  uint64_t materialize_errors = 0;
+  bool journal_failed = false;
 };
 
 // Group commit: callers that finished writing share one flush round — syncfs() of the
@@ -169,6 +180,11 @@ class ChunkStore {
   void drop_resident();  // evict every clean resident block (tests / memory pressure)
   bool debug_corrupt(const std::string& id, uint64_t offset);  // flip a byte everywhere
   void debug_pause_spill(bool on);  // hbm-ack crash tests: hold dirty blocks in HBM only
+  // Journal: write every queued record out as `<id>` + `<id>.meta` now and wait for it
+  // (tests, tiering, shutdown); pause holds the materializer (crash tests).
+  void materialize_all();
+  void debug_pause_materializer(bool on);
+  bool journaled(const std::string& id);  // durable in the journal, not yet in its own files
 
   // ---- replication engine hooks (RCCL receive / send) ----
   DevExtent reserve(uint64_t n);
@@ -243,6 +259,9 @@ class ChunkStore {
     // verified memcpy instead of a GPU round trip (kernel launch + DMA + sync, ~30 us)
     std::shared_ptr<std::vector<uint8_t>> mirror;
     std::shared_ptr<std::vector<uint32_t>> mirror_meta;
+    // durable in the block journal, not yet materialized into <id> + <id>.meta
+    JournalRec jrec;
+    std::shared_ptr<std::vector<uint8_t>> jmeta;  // BE .meta image of the journal record
   };
   struct Lane {
     hipStream_t stream = nullptr;
@@ -279,7 +298,33 @@ class ChunkStore {
   WriteResult stage_impl(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
                          bool durable_now);
   void insert_resident(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t crc, bool on_disk,
-                       std::shared_ptr<std::vector<uint8_t>> meta, int pins = 0);
+                       std::shared_ptr<std::vector<uint8_t>> meta, int pins = 0, const JournalRec* jr = nullptr);
+  // GPU staging of a host buffer into `ext`: fused copy+checksum kernel (registered memory),
+  // PCLMUL for small blocks, or SDMA copy + checksum kernel. Fills the BE .meta image.
+  bool device_stage(const uint8_t* data, uint64_t n, const DevExtent& ext, std::vector<uint8_t>* meta_be,
+                    CrcOut* co, std::string* err);
+  WriteResult stage_journal(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
+                            const DevExtent& ext);
+  // Appends a verified block (from host memory, or streamed out of HBM when dev != nullptr)
+  // to the journal and waits for its group commit.
+  bool journal_block(const std::string& id, const uint8_t* host, const uint8_t* dev, uint64_t n, uint32_t crc,
+                     const std::vector<uint8_t>& meta_be, JournalRec* out, std::string* err);
+  void enqueue_materialize_locked(const std::string& id, const Block& b);
+  void materializer_loop();
+  bool materialize_due();
+  void replay_journal();
+  // Where a block's durable bytes are read from: its own file or its journal record.
+  struct DurableSrc {
+    int fd = -1;
+    bool own_fd = false;
+    uint64_t base = 0;
+    SegRef seg;  // keeps a journal segment open while it is read
+    std::vector<uint32_t> meta;
+    bool meta_ok = false;
+    ~DurableSrc();
+  };
+  bool open_durable(const std::string& id, bool cold, const JournalRec& jrec,
+                    const std::shared_ptr<std::vector<uint8_t>>& jmeta, DurableSrc* s);
   bool persist_from_device(const std::string& id, const uint8_t* d, uint64_t n, const uint8_t* meta_be,
                            uint64_t nslices, std::string* err);
   bool persist(const std::string& id, bool cold, const uint8_t* data, uint64_t n, const uint8_t* meta_be,
@@ -338,6 +383,24 @@ class ChunkStore {
   std::unique_ptr<GroupSync> dsync_hot_, dsync_cold_;  // directory fsync after renames
   bool sync_dir(bool cold);
   std::unique_ptr<DiskGate> gate_;
+  // ---- block journal
+  struct MatItem {
+    std::string id;
+    JournalRec rec;
+    uint64_t n = 0;
+    std::shared_ptr<std::vector<uint8_t>> meta;
+  };
+  std::unique_ptr<BlockJournal> journal_;
+  std::deque<MatItem> mat_q_;         // mu_, append order
+  std::condition_variable mat_cv_;    // materializer wake-up / completion
+  int mat_force_ = 0;                 // mu_: materialize_all() callers waiting
+  bool mat_busy_ = false;             // mu_: a batch is being written
+  bool mat_paused_ = false;           // mu_
+  bool mat_stop_ = false;             // mu_
+  double mat_pressure_ = 0.5;         // materialize when this share of the journal is in use
+  uint64_t mat_idle_ns_ = 100000000;  // ... or after this long without an append
+  std::thread materializer_;
+  uint64_t materialized_blocks_ = 0, materialized_bytes_ = 0, mat_batches_ = 0, mat_errors_ = 0;  // mu_
 };
 
 }  // namespace dfs

@@ -129,7 +129,7 @@ def test_gpu_durable_write_names(native, tmp_path):
     """nvme-sync writes of fresh ids go straight to their final names (directory flush beside
     the data flushes); a rejected fresh write leaves no file; a re-write of a known id takes
     the tmp+rename path and a rejected re-write keeps the durable copy."""
-    s = native.ChunkStore(str(tmp_path), "", 0, 64 << 20, 0, 100, 2, 1, True)
+    s = native.ChunkStore(str(tmp_path), "", 0, 64 << 20, 0, 100, 2, 1, True, journal=0)
     base = s.stats()["final_name_writes"]
     d = os.urandom((1 << 20) + 5)
     assert s.write("fresh", d, zlib.crc32(d))[0]
@@ -146,6 +146,64 @@ def test_gpu_durable_write_names(native, tmp_path):
     assert s.stats()["final_name_writes"] == base + 1
     assert not [p for p in os.listdir(tmp_path) if p.endswith(".tmp")]
     assert s.read("fresh", 0, 0)[2] == d2
+
+
+def test_gpu_journal_write_evict_promote_materialize(native, tmp_path):
+    """nvme-sync through the block journal on the GPU store: the fused staging kernel runs
+    while the bytes are appended, one group commit acks; blocks evicted from a small arena
+    are promoted back from their journal records (checksummed), then materialized into the
+    reference files."""
+    s = native.ChunkStore(str(tmp_path), "", 0, 8 << 20, 0, 100, 2, 1, True, journal=1)
+    s.debug_pause_materializer(True)
+    blobs = {f"j{i}": os.urandom((1 << 20) + 977 * i) for i in range(12)}
+    blobs["small"] = os.urandom(4000)
+    for k, v in blobs.items():
+        ok, crc, err = s.write(k, v, zlib.crc32(v))
+        assert ok and crc == zlib.crc32(v), err
+    st = s.stats()
+    assert st["journal_records"] == 13 and st["evictions"] > 0 and not (tmp_path / "j0").exists()
+    for k, v in blobs.items():
+        assert s.read(k, 0, 0)[2] == v
+        assert s.read(k, 1000, 3000)[2] == v[1000:4000]
+    assert s.stats()["promotions"] > 0
+    assert s.scrub() == []
+    s.debug_pause_materializer(False)
+    s.materialize()
+    for k, v in blobs.items():
+        assert (tmp_path / k).read_bytes() == v and (tmp_path / f"{k}.meta").read_bytes() == ref_meta(v)
+    bad = os.urandom(70000)
+    assert not s.write("rej", bad, zlib.crc32(bad) ^ 1)[0] and not s.exists("rej")
+    assert s.stats()["journal_failed"] is False
+
+
+def test_gpu_journal_crash_replay_verifies_on_device(native, tmp_path):
+    import subprocess
+    import sys
+    import textwrap
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = textwrap.dedent(f"""
+        import os, zlib
+        from rust_hadoop_generated_by_llm_amd import native
+        s = native.lib.ChunkStore({str(tmp_path)!r}, "", 0, 64 << 20, 0, 100, 2, 1, True, journal=1)
+        s.debug_pause_materializer(True)
+        for i in range(6):
+            v = bytes([i + 1]) * ((2 << 20) + i)
+            assert s.write(f"r{{i}}", v, zlib.crc32(v))[0]
+        s.remove("r2")
+        os._exit(0)
+    """)
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, PYTHONPATH=root), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    s = native.ChunkStore(str(tmp_path), "", 0, 64 << 20, 0, 100, 2, 1, True, journal=1)
+    st = s.stats()
+    assert st["journal_replayed"] == 5 and st["journal_replay_skipped"] == 0
+    assert st["gpu_kernel_launches"] >= 5  # K1/K2 verified every replayed record
+    assert not s.exists("r2")
+    for i in (0, 1, 3, 4, 5):
+        v = bytes([i + 1]) * ((2 << 20) + i)
+        assert s.read(f"r{i}", 0, 0)[2] == v
 
 
 def test_gpu_corruption_detected_full_and_partial(gstore):

@@ -41,15 +41,20 @@ def test_atomic_write(native, tmp_path):
     assert open(p, "rb").read() == b'{"a":1}'
 
 
-@pytest.fixture()
-def store(native, tmp_path):
-    return native.ChunkStore(str(tmp_path / "hot"), str(tmp_path / "cold"), -1, 0, 0, 100, 1, 1, True)
+@pytest.fixture(params=[1, 0], ids=["journal", "per-file"])
+def store(native, tmp_path, request):
+    # journal=1: durable writes go through the group-committed block journal and the files
+    # appear once materialized; journal=0: the per-file fdatasync path
+    return native.ChunkStore(str(tmp_path / "hot"), str(tmp_path / "cold"), -1, 0, 0, 100, 1, 1, True,
+                             journal=request.param)
 
 
 def test_write_creates_data_and_meta(store, tmp_path):
     d = os.urandom(2000)
     ok, crc, err = store.write("blk", d, zlib.crc32(d))
     assert ok and crc == zlib.crc32(d)
+    store.materialize()
+    assert not store.journaled("blk")
     assert (tmp_path / "hot" / "blk").read_bytes() == d
     meta = (tmp_path / "hot" / "blk.meta").read_bytes()
     assert meta == b"".join(struct.pack(">I", zlib.crc32(d[i:i + 512])) for i in range(0, 2000, 512))
@@ -80,6 +85,7 @@ def test_full_and_partial_reads(store):
 def test_corruption_detection(store, tmp_path):
     d = os.urandom(4096)
     store.write("c", d, 0)
+    store.materialize()
     p = tmp_path / "hot" / "c"
     raw = bytearray(p.read_bytes())
     raw[0] ^= 0xFF
@@ -121,6 +127,7 @@ def test_restart_rescans_directories(native, tmp_path):
 
 def test_remove(store, tmp_path):
     store.write("z", b"abc", 0)
+    store.materialize()
     assert store.remove("z")
     assert not (tmp_path / "hot" / "z").exists() and not store.exists("z")
 
