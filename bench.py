@@ -249,10 +249,10 @@ def main():
         # ---------------- chunkserver for this rank's GPU
         cport, chttp = free_port(), free_port()
         ready = str(base_p / f"cs{rank}.ready")
-        # torch.cuda.device_count() goes through amdsmi, which keeps the DRM render nodes open:
-        # asked on every rank, every rank would count as a GPU process (a 1-GPU box allows 16,
-        # and an 8-rank rehearsal has 8 chunkservers already). One node: rank 0 asks for all.
-        ndev = bcast(torch.cuda.device_count() if rank == 0 and not a.cpu else None) or 0
+        # the benchmark ranks never open the GPU (no HIP / torch.cuda call in this process): the
+        # chunkservers are the only GPU processes, so N ranks keep N processes on the cards.
+        # The count comes from the KFD topology in sysfs, which opens no device.
+        ndev = 0 if a.cpu else visible_gpus()
         gpu = -1 if a.cpu else local_rank % max(1, ndev)
         shared_gpu = (not a.cpu) and ndev < n  # rehearsal mode: several ranks on one GPU
         args = [f"{PKG}.chunkserver.server", "--addr", f"127.0.0.1:{cport}",
@@ -333,16 +333,21 @@ def main():
         for w in range(a.warmup):
             ws, rs = step(f"w{w}")
             note(f"warm-up step {w}: write p50 {1e3 * ws._pct(50):.2f} ms, read p50 {1e3 * rs._pct(50):.2f} ms")
-        # ranks that share one GPU (1-GPU rehearsals) leave the device to their chunkservers:
-        # only local rank 0 brackets the timed region with a device sync there, so an 8-rank
-        # rehearsal keeps 9 GPU processes on the card, not 16
-        use_cuda = not a.cpu and ndev > 0 and (not shared_gpu or local_rank == 0) and torch.cuda.is_available()
-        if use_cuda:
-            torch.cuda.set_device(gpu)
-            torch.cuda.synchronize()
+        # the timed region is bracketed by barrier + device synchronize on both sides; the
+        # synchronize runs in the process that owns the GPU and queued all of its work (the
+        # chunkserver's /sync: hipDeviceSynchronize), not in this client process
+        def device_sync():
+            if a.cpu:
+                return
+            import urllib.request
+
+            r = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/sync", timeout=60).read())
+            if not r.get("synchronized"):
+                raise RuntimeError(f"chunkserver device sync failed: {r}")
+
+        device_sync()
         barrier()
-        if use_cuda:
-            torch.cuda.synchronize()
+        device_sync()
         import psutil
 
         def cpu_snapshot():
@@ -371,11 +376,9 @@ def main():
             rbytes += rs.count * rs.avg_size
             wt += ws.total_s
             rt += rs.total_s
-        if use_cuda:
-            torch.cuda.synchronize()
+        device_sync()
         barrier()
-        if use_cuda:
-            torch.cuda.synchronize()
+        device_sync()
         elapsed = time.perf_counter() - t0
         note(f"{a.steps} timed steps in {elapsed:.3f} s")
         cpu1 = cpu_snapshot()
@@ -427,7 +430,8 @@ def main():
                       "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in rc.phase_times.items() if v}}
             rc.close()
         allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
-                       "rt": rt, "cs": stats, "stress": stress, "remote": remote, "rccl": cs_info.get("rccl", False),
+                       "rt": rt, "cs": stats, "stress": stress, "remote": remote,
+                       "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
                        "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                    for k, v in (client.phase_times or {}).items() if v}})
         if rank == 0:
@@ -458,17 +462,26 @@ def main():
                 "write_p99_ms": round(pct(wlat, 99), 3), "read_p50_ms": round(pct(rlat, 50), 3),
                 "read_p95_ms": round(pct(rlat, 95), 3), "read_p99_ms": round(pct(rlat, 99), 3),
                 "write_ops_per_s": round(len(wlat) / wmax, 1),
-                "rccl_ranks": sum(1 for r in allr if r["rccl"]),
+                # replica hops between same-node chunkservers: which device transport carried
+                # them (hipipc / rccl / socket), on how many ranks, and how often it fell back
+                "p2p_transport": ",".join(sorted({r["p2p_transport"] for r in allr if r["p2p"]})) or "none",
+                "p2p_ranks": sum(1 for r in allr if r["p2p"]),
                 "repl_pairs_up": sum(r["cs"].get("repl_pairs_up", 0) for r in allr),
                 **forward_counts(allr),
-                "rccl_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) + r["cs"].get("fp_p2p_fallbacks", 0)
-                                      for r in allr),
+                "p2p_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) + r["cs"].get("fp_p2p_fallbacks", 0)
+                                     for r in allr),
                 "replica_failures": sum(r["cs"].get("fp_replica_failures", 0) for r in allr),
                 "repl_pair_failures": sum(r["cs"].get("repl_pair_failures", 0) for r in allr),
                 "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
                 "fused_reads": sum(r["cs"].get("fused_reads", 0) for r in allr),
                 "direct_writes": sum(r["cs"].get("direct_writes", 0) for r in allr),
                 "disk_gate_waits": sum(r["cs"].get("disk_gate_waits", 0) for r in allr),
+                # block journal (group commit): records appended, flush rounds that covered them,
+                # and blocks already written out as <id> + <id>.meta by the materializer
+                "journal": {k: sum(r["cs"].get(f, 0) for r in allr) for k, f in (
+                    ("records", "journal_records"), ("sync_rounds", "journal_sync_rounds"),
+                    ("materialized_blocks", "materialized_blocks"), ("materialize_pending", "materialize_pending"),
+                    ("full_waits", "journal_full_waits"))} if any(r["cs"].get("journal") for r in allr) else None,
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],
             }
@@ -520,12 +533,39 @@ def main():
 
 
 def forward_counts(allr) -> dict:
-    """Replica hops as the chunkservers counted them (native fast path + gRPC service)."""
+    """Replica hops as the chunkservers counted them (native fast path + gRPC service).
+    p2p_forwards: hops over the replication engine, whatever its transport; rccl_forwards:
+    the subset carried by RCCL itself (0 unless the engine's transport is rccl)."""
+    def p2p(r):
+        return r["cs"].get("fp_rccl_forwards", 0) + r["cs"].get("rccl_forwards", 0)
+
     return {
-        "rccl_forwards": sum(r["cs"].get("fp_rccl_forwards", 0) + r["cs"].get("rccl_forwards", 0) for r in allr),
+        "p2p_forwards": sum(p2p(r) for r in allr),
+        "rccl_forwards": sum(p2p(r) for r in allr if r["p2p"] and r["p2p_transport"] == "rccl"),
         "shm_forwards": sum(r["cs"].get("fp_shm_forwards", 0) for r in allr),
         "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
     }
+
+
+def visible_gpus() -> int:
+    """GPUs this node exposes, from the KFD topology (sysfs; opens no device) narrowed by the
+    usual visibility variables."""
+    nodes = Path("/sys/class/kfd/kfd/topology/nodes")
+    n = 0
+    try:
+        for d in nodes.iterdir():
+            try:
+                if int((d / "gpu_id").read_text().strip() or "0") != 0:
+                    n += 1
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def observed_transport(allr, n: int) -> str:
@@ -534,9 +574,10 @@ def observed_transport(allr, n: int) -> str:
     if n <= 1:
         return "local"
     c = forward_counts(allr)
+    c.pop("rccl_forwards")  # a subset of p2p_forwards
     p2p = {r["cs"].get("repl_transport") for r in allr} - {None}
-    p2p_name = p2p.pop() if len(p2p) == 1 else "rccl"  # "socket" in CPU rehearsals
-    used = {(p2p_name if k.startswith("rccl") else k.split("_")[0]): v for k, v in c.items() if v}
+    p2p_name = p2p.pop() if len(p2p) == 1 else "p2p"  # "socket" in CPU rehearsals
+    used = {(p2p_name if k.startswith("p2p") else k.split("_")[0]): v for k, v in c.items() if v}
     if not used:
         return "none"
     if len(used) == 1:

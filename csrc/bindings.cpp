@@ -136,6 +136,13 @@ PYBIND11_MODULE(_dfs_native, m) {
   });
   m.def("cpu_has_pclmul", &cpu_has_pclmul);
   m.def("device_count", &device_count);
+  // hipDeviceSynchronize on `device` in the calling process (the chunkserver owns its GPU:
+  // the benchmark brackets its timed region with this, through the server's /sync endpoint)
+  m.def("device_synchronize", [](int device) {
+    py::gil_scoped_release r;
+    if (device < 0) return true;
+    return hipSetDevice(device) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+  });
   // checksum-kernel selection (tests / A-B runs): (mfma, scrub ring buffers, K1/K2/K3 ring buffers)
   m.def("crc_kernels", [] { return py::make_tuple(crc_mfma_enabled(), crc_ring_buffers(), crc_tile_ring_buffers()); });
   m.def("set_crc_lds_max_mib", &set_crc_lds_max_mib, "K1/K2 size-based dispatch threshold (0 = matrix cores only)");

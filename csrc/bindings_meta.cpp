@@ -839,8 +839,9 @@ void bind_meta(py::module_& m) {
       .def(py::init([](FastClient* fc, const std::string& host, int port, const std::string& backend, int workers,
                        bool auth_enabled, const std::string& region, const std::string& access_key,
                        const std::string& secret_key, bool allow_unsigned, const std::string& audit_socket,
-                       bool sse_enabled, bool metadata_sidecar) {
+                       bool sse_enabled, bool metadata_sidecar, const std::string& policy_epoch) {
              S3FrontConfig c;
+             c.policy_epoch_path = policy_epoch;
              c.host = host;
              c.port = port;
              c.backend = backend;
@@ -858,7 +859,9 @@ void bind_meta(py::module_& m) {
            py::arg("fast_client"), py::arg("host"), py::arg("port"), py::arg("backend"), py::arg("workers") = 32,
            py::arg("auth_enabled") = false, py::arg("region") = "us-east-1", py::arg("access_key") = "",
            py::arg("secret_key") = "", py::arg("allow_unsigned_payload") = true, py::arg("audit_socket") = "",
-           py::arg("sse_enabled") = false, py::arg("metadata_sidecar") = false, py::keep_alive<1, 2>())
+           py::arg("sse_enabled") = false, py::arg("metadata_sidecar") = false, py::arg("policy_epoch") = "",
+           py::keep_alive<1, 2>())
+      .def("drop_policies", &S3Front::drop_policies, py::call_guard<py::gil_scoped_release>())
       .def("start", [](S3Front& f) {
         std::string err;
         bool ok;

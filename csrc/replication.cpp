@@ -234,7 +234,7 @@ void ReplicationEngine::opener_loop(int p) {
       g = P.gen + 1;
       P.gen = g;
       P.state = State::Opening;
-      P.send_seq = P.recv_next = 0;
+      P.send_seq = P.post_next = P.recv_next = 0;
       P.cv.notify_all();
     }
     t_->close(p);
@@ -346,7 +346,7 @@ std::string ReplicationEngine::handle_control(const std::string& req) {
     if (g <= P.gen) return reply(kStale, P.gen);
     P.gen = g;
     P.state = State::Opening;
-    P.send_seq = P.recv_next = 0;
+    P.send_seq = P.post_next = P.recv_next = 0;
     P.cv.notify_all();  // receivers waiting under the old generation fail now
   }
   t_->close(from);
@@ -467,33 +467,56 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
       else std::this_thread::sleep_for(std::chrono::microseconds(5));
     }
   };
-  bool failed = false;
+  bool failed = false, up = false;
   {
+    // only the sequence number is taken under the pair lock; the descriptor write and the
+    // slice posts (which may wait for the head's staging) run outside it, so a slow peer
+    // socket or a slow PCIe copy never blocks fail_pair_gen / reap / handle_control or the
+    // generation checks of other transfers
     std::lock_guard<std::mutex> lk(P.mu);
     if (P.state != State::Up) {
       *err = "pair " + std::to_string(rank_) + "->" + std::to_string(p) + " is not up";
     } else {
+      up = true;
       t->gen = P.gen;
       t->seq = P.send_seq++;
-      if (announce && !announce(*t)) {
-        *err = "descriptor to rank " + std::to_string(p) + " failed";
+    }
+  }
+  if (up) {
+    // the channels are FIFO: transfers post in sequence order (a ticket per peer)
+    {
+      std::unique_lock<std::mutex> lk(P.mu);
+      const bool turn = P.cv.wait_until(lk, deadline, [&] {
+        return P.gen != t->gen || P.state != State::Up || P.post_next == t->seq;
+      });
+      if (!turn || P.gen != t->gen || P.state != State::Up) {
+        *err = "pair " + std::to_string(rank_) + "->" + std::to_string(p) + " changed before the send was posted";
         failed = true;  // the sequence number is spent: the pair cannot stay in step
       }
-      for (uint64_t off = 0; !failed && off < n; off += t->slice) {
-        P2POp op;
-        if (staged && !landed(off / t->slice)) {
-          *err = "staging of slice " + std::to_string(off / t->slice) + " did not complete";
-          failed = true;
-          break;
-        }
-        if (!t_->post_send(p, src + off, std::min(t->slice, n - off), &op, err)) {
-          failed = true;
-          break;
-        }
-        t->ops.push_back(op);
-      }
-      if (!failed) return true;  // the pin is held until wait_send / cancel_send
     }
+    if (!failed && announce && !announce(*t)) {
+      *err = "descriptor to rank " + std::to_string(p) + " failed";
+      failed = true;
+    }
+    for (uint64_t off = 0; !failed && off < n; off += t->slice) {
+      P2POp op;
+      if (staged && !landed(off / t->slice)) {
+        *err = "staging of slice " + std::to_string(off / t->slice) + " did not complete";
+        failed = true;
+        break;
+      }
+      if (!t_->post_send(p, src + off, std::min(t->slice, n - off), &op, err)) {
+        failed = true;
+        break;
+      }
+      t->ops.push_back(op);
+    }
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      if (P.gen == t->gen && P.post_next == t->seq) P.post_next++;
+      P.cv.notify_all();
+    }
+    if (!failed) return true;  // the pin is held until wait_send / cancel_send
   }
   for (auto& op : t->ops) t_->release(&op);
   t->ops.clear();

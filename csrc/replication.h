@@ -142,6 +142,7 @@ class ReplicationEngine {
     State state = State::Down;
     uint64_t gen = 0;
     int64_t send_seq = 0;
+    int64_t post_next = 0;  // the sequence number whose slices may be posted next (FIFO channels)
     int64_t recv_next = 0;
     bool opener = false;  // an opener thread is running (initiator side)
     uint64_t peer_inc = 0;  // initiator side: the peer process instance the pair was opened with

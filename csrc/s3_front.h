@@ -55,6 +55,9 @@ struct S3FrontConfig {
   std::string audit_socket;  // datagram socket of the audit store ("" = no audit)
   bool sse_enabled = false;  // objects are encrypted: their data stays on the Python path
   bool metadata_sidecar = false;
+  // 8-byte shared counter the gateway's workers bump on every PutBucketPolicy /
+  // DeleteBucketPolicy ("" = none): a change empties the front's policy cache at once
+  std::string policy_epoch_path;
 };
 
 struct S3FrontStats {
@@ -119,6 +122,15 @@ class S3Front {
   std::mutex pol_mu_;
   // bucket -> (expiry, policy or null); the gateway's 1 s policy cache
   std::map<std::string, std::pair<double, std::shared_ptr<const s3policy::BucketPolicy>>> policy_cache_;
+  static constexpr size_t kPolicyCacheMax = 4096;  // entries; the cache is emptied beyond this
+  uint64_t cache_epoch_ = 0;                        // pol_mu_: epoch the cached entries belong to
+  const uint64_t* epoch_map_ = nullptr;             // mmap of cfg_.policy_epoch_path
+  uint64_t policy_epoch() const { return epoch_map_ ? __atomic_load_n(epoch_map_, __ATOMIC_ACQUIRE) : 0; }
+
+ public:
+  void drop_policies();  // the in-process form of an epoch bump
+
+ private:
   std::mutex key_mu_;
   std::map<std::string, std::string> key_cache_;  // date -> signing key (the single static key)
   IoPool pool_{4};

@@ -284,6 +284,11 @@ class ChunkServerProcess:
                     body, ctype = b"OK", "text/plain"
                 elif self.path == "/metrics":
                     body, ctype = proc.metrics.render().encode(), "text/plain"
+                elif self.path == "/sync":
+                    # device-side completion of everything this process queued on its GPU
+                    ok = native.device_synchronize(proc.args.gpu)
+                    body, ctype = json.dumps({"synchronized": bool(ok), "gpu": proc.args.gpu}).encode(), \
+                        "application/json"
                 elif self.path == "/stats":
                     d = dict(proc.store.stats())
                     d.update(proc.cs.stats)

@@ -40,6 +40,7 @@ import shutil
 import signal
 import socket
 import ssl
+import struct
 import tempfile
 import threading
 import time
@@ -152,6 +153,43 @@ class _AuthOk:
         self.user_id, self.role_arn, self.ctx, self.chunk_verifier = user_id, role_arn, ctx, chunk_verifier
 
 
+class PolicyEpoch:
+    """Bucket-policy change counter shared by every process of one gateway (the forked
+    aiohttp workers and the native front): a worker that stores or deletes a bucket policy
+    bumps it, and every cache that saw an older value drops its entries at once instead of
+    serving the old policy for up to its TTL. File-backed (an 8-byte counter in a page that
+    each process maps shared); without a file it is a process-local counter."""
+
+    def __init__(self, path: str | None = None):
+        import mmap
+
+        self.path = path
+        self._local = 0
+        self._mm = None
+        if path:
+            if not os.path.exists(path):
+                with open(path, "wb") as f:
+                    f.write(b"\0" * 4096)
+            fd = os.open(path, os.O_RDWR)
+            try:
+                self._mm = mmap.mmap(fd, 4096, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+            finally:
+                os.close(fd)
+
+    def get(self) -> int:
+        if self._mm is None:
+            return self._local
+        return struct.unpack_from("<Q", self._mm, 0)[0]
+
+    def bump(self) -> None:
+        # strictly increasing across processes: the system-wide monotonic clock, at least +1
+        nxt = max(self.get() + 1, time.monotonic_ns())
+        if self._mm is None:
+            self._local = nxt
+        else:
+            struct.pack_into("<Q", self._mm, 0, nxt)
+
+
 class S3Gateway:
     def __init__(self, client: Client, cfg: S3Config | None = None, *, registry: Registry | None = None,
                  credential_provider=None, oidc: OidcValidator | None = None, sts: StsTokenManager | None = None,
@@ -166,6 +204,9 @@ class S3Gateway:
         self.pool = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="s3-dfs")
         self._policy_cache: dict[str, tuple[float, BucketPolicy | None]] = {}
         self.policy_ttl = 1.0
+        self.policy_epoch = PolicyEpoch()
+        self._policy_epoch_seen = self.policy_epoch.get()
+        self.front = None  # the native front when it runs in this process (drop_policies on change)
         r = self.registry
         self.m_requests = r.counter("s3_requests_total", "Total number of S3 requests", ("method", "path", "status"))
         self.m_auth = r.counter("iam_auth_requests_total", "Total authentication attempts", ("result", "error_type"))
@@ -485,7 +526,17 @@ class S3Gateway:
         verifier = sigv4.ChunkVerifier(skey, cred.timestamp, cred.scope, cred.signature)
         return _AuthOk(user, role_arn, ctx, verifier)
 
+    def _policy_changed(self, bucket: str) -> None:
+        self._policy_cache.pop(bucket, None)
+        self.policy_epoch.bump()
+        if self.front is not None:
+            self.front.drop_policies()
+
     async def _bucket_policy(self, bucket: str) -> BucketPolicy | None:
+        ep = self.policy_epoch.get()
+        if ep != self._policy_epoch_seen:  # another worker changed a policy
+            self._policy_cache.clear()
+            self._policy_epoch_seen = ep
         ent = self._policy_cache.get(bucket)
         now = time.monotonic()
         if ent is not None and ent[0] > now:
@@ -498,7 +549,10 @@ class S3Gateway:
             except (DfsError, ValueError, json.JSONDecodeError):
                 return None
         pol = await self.run(load)
-        self._policy_cache[bucket] = (now + self.policy_ttl, pol)
+        if self.policy_epoch.get() == ep:  # not cached when a change raced the fetch
+            if len(self._policy_cache) >= 4096:
+                self._policy_cache.clear()
+            self._policy_cache[bucket] = (now + self.policy_ttl, pol)
         return pol
 
     # ------------------------------------------------------------------ STS (C55)
@@ -585,7 +639,7 @@ class S3Gateway:
             return self.xml(404, X.error("NoSuchBucket", "The specified bucket does not exist", bucket))
         for f in files:
             await self.run(self._delete_quiet, f)
-        self._policy_cache.pop(bucket, None)
+        self._policy_changed(bucket)
         return self.empty(204)
 
     async def head_bucket(self, bucket: str) -> web.Response:
@@ -622,12 +676,12 @@ class S3Gateway:
         except DfsError:
             return self.xml(500, "<Error><Code>InternalError</Code><Message>Failed to store bucket policy"
                                  "</Message></Error>")
-        self._policy_cache.pop(bucket, None)
+        self._policy_changed(bucket)
         return self.empty(204)
 
     async def delete_bucket_policy(self, bucket: str) -> web.Response:
         await self.run(self._delete_quiet, f"/{bucket}/.s3_bucket_policy")
-        self._policy_cache.pop(bucket, None)
+        self._policy_changed(bucket)
         return self.empty(204)
 
     # ------------------------------------------------------------------ objects
@@ -1187,7 +1241,8 @@ def native_front_wanted(cfg: S3Config) -> bool:
     return True
 
 
-def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_socket: str):
+def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_socket: str,
+                       policy_epoch: str = ""):
     """Worker 0 runs the native front on the public port; it hands what it does not serve to
     the aiohttp workers on `backend` and sends its audit records to `audit_socket`."""
     from ..native import lib
@@ -1201,10 +1256,12 @@ def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_
                         secret_key=getattr(creds, "secret_key", None) or "",
                         allow_unsigned_payload=cfg.allow_unsigned_payload,
                         audit_socket=audit_socket if (cfg.auth_enabled and gw.audit is not None) else "",
-                        sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar)
+                        sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar,
+                        policy_epoch=policy_epoch or (gw.policy_epoch.path or ""))
     ok, err = front.start()
     if not ok:
         raise RuntimeError(f"native S3 front end failed to start: {err}")
+    gw.front = front
     if gw.client._fast is None:
         log.warning("native front end without a co-located native client: every request goes to Python")
     return front
@@ -1246,6 +1303,8 @@ def main(argv: list[str] | None = None) -> int:
         ingest = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
         ingest.bind(ingest_path)
         ingest.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    epoch_path = os.path.join(private_dir, "policy_epoch")
+    PolicyEpoch(epoch_path)  # created before the fork: every worker maps the same page
     children = []
     worker_id = 0
     for i in range(1, workers):
@@ -1262,6 +1321,8 @@ def main(argv: list[str] | None = None) -> int:
     if worker_id > 0 and ingest_path:
         sink = lambda reg: ForwardingAudit(ingest_path, reg)  # noqa: E731
     gw = build_gateway(cfg, audit_sink=sink)
+    gw.policy_epoch = PolicyEpoch(epoch_path)
+    gw._policy_epoch_seen = gw.policy_epoch.get()
     if worker_id == 0 and ingest is not None and gw.audit is not None:
         if hasattr(gw.audit, "start_ingest"):  # native writer: a C++ thread receives the datagrams
             gw.audit.start_ingest(ingest)
@@ -1274,7 +1335,7 @@ def main(argv: list[str] | None = None) -> int:
         ssl_ctx.load_cert_chain(cfg.tls_cert, cfg.tls_key)
     front = None
     if worker_id == 0 and native:
-        front = start_native_front(gw, a.host, cfg.port, backend_path, ingest_path or "")
+        front = start_native_front(gw, a.host, cfg.port, backend_path, ingest_path or "", epoch_path)
     if worker_id == 0:
         log.info("S3 gateway on %s:%d (workers=%d, auth=%s, sse=%s, audit=%s, native front=%s)", a.host, cfg.port,
                  workers, cfg.auth_enabled, gw.sse is not None, gw.audit is not None, front is not None)

@@ -59,9 +59,20 @@ def test_bench_multi_rank_socket_transport(tmp_path, n):
     assert d["config"]["global_batch"] == 10 * n
     # every rank's engine came up, every directed pair is up, and every write reached
     # RF-1 replicas over the peer transport (nothing fell back, nothing failed)
-    assert d["rccl_ranks"] == n
+    assert d["p2p_ranks"] == n and d["p2p_transport"] == "socket"
     assert d["repl_pairs_up"] == n * (n - 1)
     writes = (1 + 1) * 10 * n  # warmup + timed step
-    assert d["rccl_forwards"] == writes * (min(3, n) - 1)
-    assert d["rccl_fallbacks"] == 0 and d["replica_failures"] == 0 and d["repl_pair_failures"] == 0
+    assert d["p2p_forwards"] == writes * (min(3, n) - 1)
+    assert d["rccl_forwards"] == 0  # the socket transport carried them, not RCCL
+    assert d["p2p_fallbacks"] == 0 and d["replica_failures"] == 0 and d["repl_pair_failures"] == 0
     assert d["config"]["transport"] == "socket"
+
+
+def test_bench_never_opens_the_gpu():
+    """The ranks leave the device to their chunkservers: no torch.cuda / HIP call in bench.py
+    (an N-rank node then has N GPU processes, not 2N), and the timed region is bracketed by
+    the chunkservers' device synchronize."""
+    src = (ROOT / "bench.py").read_text()
+    assert "torch.cuda" not in src.replace("(no HIP / torch.cuda call", "")
+    assert "native" not in src.split("def main")[1].split("client.benchmark")[0]
+    assert src.count("device_sync()") >= 4

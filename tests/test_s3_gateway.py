@@ -70,12 +70,19 @@ class GatewayThread:
                 else:
                     threading.Thread(target=_audit_ingest, args=(self._isock, gw.audit), daemon=True).start()
             cfg = gw.cfg
+            # as s3/server.py main(): the workers and the front share the policy epoch page
+            from rust_hadoop_generated_by_llm_amd.s3.server import PolicyEpoch
+
+            epoch = os.path.join(self._dir, "policy_epoch")
+            gw.policy_epoch = PolicyEpoch(epoch)
+            gw._policy_epoch_seen = gw.policy_epoch.get()
             self.front = lib.S3Front(gw.client._fast, "127.0.0.1", self.port, self.backend, workers=8,
                                      auth_enabled=cfg.auth_enabled, region=cfg.region,
                                      access_key=gw.creds.access_key or "", secret_key=gw.creds.secret_key or "",
                                      allow_unsigned_payload=cfg.allow_unsigned_payload,
                                      audit_socket=ingest if cfg.auth_enabled else "",
-                                     sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar)
+                                     sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar,
+                                     policy_epoch=epoch)
             ok, err = self.front.start()
             assert ok, err
         self.url = f"http://127.0.0.1:{self.port}"
@@ -811,8 +818,9 @@ def test_native_front_evaluates_bucket_policies(authgw, front):
     pol = {"Version": "2012-10-17", "Statement": [
         {"Effect": "Deny", "Principal": "*", "Action": "s3:GetObject", "Resource": "arn:dfs:s3:::polnat/secret*"},
         {"Effect": "Allow", "Principal": {"AWS": ["arn:dfs:iam:::role/*"]}, "Action": "s3:*"}]}
+    # no allow-all window: the front's policy cache is dropped by the gateway's epoch bump
+    assert signed("GET", g, "/polnat/secret-1").status_code == 200  # cached: "no policy"
     assert signed("PUT", g, "/polnat", json.dumps(pol).encode(), query=[("policy", "")]).status_code == 204
-    time.sleep(1.1)  # the front's 1 s policy cache
     s0 = g.front.stats()
     assert signed("GET", g, "/polnat/public").content == b"v-public"
     assert signed("PUT", g, "/polnat/public", b"v2").status_code == 200
@@ -821,7 +829,13 @@ def test_native_front_evaluates_bucket_policies(authgw, front):
     s1 = g.front.stats()
     assert s1["policy_native"] - s0["policy_native"] >= 2
     assert s1["proxy_reasons"].get("bucket-policy-deny", 0) - s0["proxy_reasons"].get("bucket-policy-deny", 0) == 1
+    # a new Deny is enforced by the very next request, and its removal likewise
+    deny_all = {"Version": "2012-10-17", "Statement": [
+        {"Effect": "Deny", "Principal": "*", "Action": "s3:GetObject", "Resource": "arn:dfs:s3:::polnat/*"}]}
+    assert signed("PUT", g, "/polnat", json.dumps(deny_all).encode(), query=[("policy", "")]).status_code == 204
+    assert signed("GET", g, "/polnat/public").status_code == 403
     assert signed("DELETE", g, "/polnat", query=[("policy", "")]).status_code == 204
+    assert signed("GET", g, "/polnat/public").content == b"v2"
 
 
 def test_native_front_auth_and_audit(authgw, front):
