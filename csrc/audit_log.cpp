@@ -315,12 +315,32 @@ bool AuditLog::append(const std::vector<std::pair<int64_t, Json>>& keyed) {
     std::string line = std::to_string(kv.first) + "\t" + audit::canonical_json(kv.second, false) + "\n";
     by_seg[kv.first / kHourMs * kHourMs].emplace_back(std::move(line), &kv.second);
   }
+  // A failed attempt is rolled back before the caller retries: every file this batch touches
+  // is cut back to its size before the attempt (or removed if the attempt created it), so a
+  // retry never writes a record twice and a batch that fails for good leaves no trace of
+  // records the chain head does not cover.
+  std::vector<std::pair<std::string, off_t>> before;  // path, size (-1: did not exist)
+  for (auto& sv : by_seg)
+    for (const char* ext : {".log", ".uidx", ".ridx"}) {
+      const std::string path = dir_ + "/seg-" + std::to_string(sv.first) + ext;
+      struct stat st;
+      before.emplace_back(path, ::stat(path.c_str(), &st) == 0 ? st.st_size : -1);
+    }
+  auto rollback = [&] {
+    const int saved = errno;
+    for (auto& b : before) {
+      if (b.second < 0) ::unlink(b.first.c_str());
+      else (void)::truncate(b.first.c_str(), b.second);
+    }
+    errno = saved;
+    return false;
+  };
   for (auto& sv : by_seg) {
     const std::string base_path = dir_ + "/seg-" + std::to_string(sv.first);
     std::string bytes;
     for (auto& it : sv.second) bytes += it.first;
     off_t base = 0;
-    if (!append_file(base_path + ".log", bytes, sync_, &base)) return false;
+    if (!append_file(base_path + ".log", bytes, sync_, &base)) return rollback();
     // index lines only after the records they point at are written
     std::string uidx, ridx;
     uint64_t off = static_cast<uint64_t>(base);
@@ -332,7 +352,7 @@ bool AuditLog::append(const std::vector<std::pair<int64_t, Json>>& keyed) {
     }
     if (!append_file(base_path + ".uidx", uidx, sync_, nullptr) ||
         !append_file(base_path + ".ridx", ridx, sync_, nullptr))
-      return false;
+      return rollback();
   }
   return true;
 }

@@ -559,6 +559,8 @@ void bind_meta(py::module_& m) {
         return py::make_tuple(code, py::bytes(out));
       })
       .def("set_shard_map", &MasterCore::set_shard_map, py::call_guard<py::gil_scoped_release>())
+      .def("note_shard_map_fresh", &MasterCore::note_shard_map_fresh, py::call_guard<py::gil_scoped_release>())
+      .def("set_shard_map_max_age", &MasterCore::set_shard_map_max_age, py::call_guard<py::gil_scoped_release>())
       .def("set_access_stats", &MasterCore::set_access_stats)
       .def("upsert_chunk_server", [](MasterCore& c, const std::string& addr, int64_t last_heartbeat, uint64_t used,
                                      uint64_t avail, uint64_t chunks, const std::string& rack, int32_t gpu_rank,

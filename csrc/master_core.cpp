@@ -219,6 +219,21 @@ void MasterCore::set_shard_map(const std::string& json, const std::string& shard
   have_map_ = !json.empty();
 }
 
+static int64_t steady_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void MasterCore::note_shard_map_fresh() {
+  std::lock_guard<std::mutex> g(mu_);
+  map_fresh_ms_ = steady_ms();
+}
+
+void MasterCore::set_shard_map_max_age(int64_t ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  map_max_age_ms_ = ms;
+}
+
 // ---------------------------------------------------------------- state machine
 void MasterCore::put(const std::string& path, pb::FileMetadata m) {
   auto it = files_.find(path);
@@ -1420,6 +1435,12 @@ int MasterCore::rename(const std::string& raw, std::string* out) {
   {
     std::lock_guard<std::mutex> g(mu_);
     if (safe_mode_) return (*out = kSafeModeMsg, UNAVAILABLE);
+    if (have_map_ && map_max_age_ms_ > 0 && steady_ms() - map_fresh_ms_ > map_max_age_ms_) {
+      // right after a split or merge the destination may have moved: a stale map could
+      // commit locally a rename that belongs to another shard
+      stale_map_declines_++;
+      return kDecline;
+    }
     if (have_map_) {
       std::string s = shard_map_.get_shard(r.source_path), d = shard_map_.get_shard(r.dest_path);
       src_shard = s.empty() ? shard_id_ : s;
@@ -1691,6 +1712,7 @@ Json MasterCore::txn_stats() const {
               {"native_aborted", tx_aborted_.load()},
               {"native_pending", tx_pending_.load()},
               {"declined", tx_declined_.load()},
+              {"stale_map_declines", stale_map_declines_.load()},
               {"enabled", static_cast<bool>(peer_call_)}});
 }
 

@@ -82,6 +82,11 @@ class MasterCore : public raft::StateMachine {
 
   // Routing: the shard map (JSON, ShardMap serde layout) and this master's shard id.
   void set_shard_map(const std::string& json, const std::string& shard_id);
+  // The map was just fetched from the config servers. With a max age set (> 0), a Rename
+  // decides same-shard vs 2PC natively only while the map is younger than that; otherwise it
+  // is declined to the Python handler, which refreshes the map first (master/service.py).
+  void note_shard_map_fresh();
+  void set_shard_map_max_age(int64_t ms);
 
   // Chunkserver registry (local, rebuilt from heartbeats).
   void upsert_chunk_server(const ChunkServerStatus& st);
@@ -248,6 +253,9 @@ class MasterCore : public raft::StateMachine {
   ShardMap shard_map_;
   std::string shard_id_;
   bool have_map_ = false;
+  int64_t map_fresh_ms_ = 0;    // mu_: steady-clock ms of the last note_shard_map_fresh()
+  int64_t map_max_age_ms_ = 0;  // mu_: 0 = no freshness requirement (no config servers)
+  std::atomic<uint64_t> stale_map_declines_{0};
   std::map<std::string, uint64_t> request_counts_;
   std::map<std::string, std::vector<std::string>> cmd_q_;        // addr -> serialized commands
   std::map<std::string, std::set<std::string>> bad_blocks_;      // block -> reporting servers

@@ -74,6 +74,8 @@ class MasterBackground:
         self._tasks: list[asyncio.Task] = []
         if config_servers:
             svc.shard_map_refresher = self.refresh_shard_map
+            # the native Rename trusts the map only while it is this young (else: Python refreshes)
+            svc.core.set_shard_map_max_age(svc.shard_map_max_age_ms)
 
     def start(self) -> None:
         loop = asyncio.get_running_loop()
@@ -281,6 +283,7 @@ class MasterBackground:
             new.shard_peers
         m._dirty()
         self.svc.sync_routing()
+        self.svc.core.note_shard_map_fresh()
         if not self.svc.shard_id:  # standby master: a SplitShard allocated us a shard
             me = self.svc.advertise_addr
             for sid in m.get_all_shards():

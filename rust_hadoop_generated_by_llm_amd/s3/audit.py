@@ -99,6 +99,27 @@ class SegmentStore:
         for key_ts, rec in keyed:
             line = f"{key_ts}\t{canonical_json(rec)}\n".encode()
             by_seg.setdefault(key_ts // HOUR_MS * HOUR_MS, []).append((line, rec))
+        # a failed attempt is rolled back (every touched file cut back to its size before it)
+        # so the caller's retry never writes a record twice (same as csrc/audit_log.cpp)
+        before = {}
+        for seg in by_seg:
+            for ext in (".log", ".uidx", ".ridx"):
+                p = self.seg_path(seg, ext)
+                before[p] = os.path.getsize(p) if os.path.exists(p) else -1
+        try:
+            self._append(by_seg, sync)
+        except OSError:
+            for p, size in before.items():
+                try:
+                    if size < 0:
+                        os.unlink(p)
+                    else:
+                        os.truncate(p, size)
+                except OSError:
+                    pass
+            raise
+
+    def _append(self, by_seg: dict, sync: bool) -> None:
         for seg, items in sorted(by_seg.items()):
             with open(self.seg_path(seg), "ab") as f:
                 base = f.seek(0, os.SEEK_END)

@@ -436,6 +436,15 @@ def test_native_same_shard_rename_and_cross_shard_decline(master):
     assert code == 11 and msg == "REDIRECT:http://m1:1"  # the source's shard owns the request
     code, r = call("Rename", pb.RenameRequest(source_path="/x/b", dest_path="/y/b"), pb.RenameResponse)
     assert code == 0 and r.success and "/y/b" in st.files
+    # with config servers the map must be young: a stale one sends the rename to Python, which
+    # refreshes the map before deciding same-shard vs 2PC (a split may have moved /y)
+    st.core.set_shard_map_max_age(1000)
+    code, out = st.core.handle("Rename", pb.RenameRequest(source_path="/y/b", dest_path="/y/c").SerializeToString())
+    assert code == -100 and "/y/b" in st.files
+    st.core.note_shard_map_fresh()
+    code, r = call("Rename", pb.RenameRequest(source_path="/y/b", dest_path="/y/c"), pb.RenameResponse)
+    assert code == 0 and r.success and "/y/c" in st.files
+    st.core.set_shard_map_max_age(0)
 
 
 def test_list_files_with_metadata_in_one_call(master):
