@@ -460,6 +460,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["agent_replicate_grpc"] = s.replicate_grpc;
         d["agent_replicate_failed"] = s.replicate_failed;
         d["agent_reconstructs"] = s.reconstructs;
+        d["agent_reconstruct_device"] = s.reconstruct_device;
         d["agent_reconstruct_failed"] = s.reconstruct_failed;
         d["agent_encodes"] = s.encodes;
         d["agent_encode_failed"] = s.encode_failed;
@@ -504,6 +505,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("debug_drop_descriptors", &FastPathServer::debug_drop_descriptors)
       .def("set_peer", &FastPathServer::set_peer, py::arg("addr"), py::arg("rank"), py::arg("name") = "")
       .def("set_self_host", &FastPathServer::set_self_host, py::arg("host"))
+      .def("set_self_addr", &FastPathServer::set_self_addr, py::arg("addr"))
       .def("stats", [](FastPathServer& f) {
         FpStats s = f.stats();
         py::dict d;
@@ -523,6 +525,12 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["fp_heals_out"] = s.heals_out;
         d["fp_heals_in"] = s.heals_in;
         d["fp_sliced_writes"] = s.sliced_writes;
+        d["fp_ec_device_writes"] = s.ec_device_writes;
+        d["fp_ec_shard_forwards"] = s.ec_shard_forwards;
+        d["fp_ec_device_reads"] = s.ec_device_reads;
+        d["fp_ec_device_decodes"] = s.ec_device_decodes;
+        d["fp_ec_gathered"] = s.ec_gathered;
+        d["fp_ec_device_fallbacks"] = s.ec_device_fallbacks;
         return d;
       })
       .def("replicate_block", [](FastPathServer& f, const std::string& id, const std::vector<std::string>& targets,

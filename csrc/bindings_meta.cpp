@@ -998,6 +998,9 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("ec_gpu_ops", &FastClient::ec_gpu_ops)
       .def_property_readonly("ec_cpu_ops", &FastClient::ec_cpu_ops)
       .def_property_readonly("ec_degraded_reads", &FastClient::ec_degraded_reads)
+      .def_property_readonly("ec_device_writes", &FastClient::ec_device_writes)
+      .def_property_readonly("ec_device_reads", &FastClient::ec_device_reads)
+      .def_property_readonly("ec_host_fallbacks", &FastClient::ec_host_fallbacks)
       .def("bench_writes", &bench_writes<FastClient>, py::arg("paths"), py::arg("payloads"), py::arg("concurrency"))
       .def("bench_reads", &bench_reads_fast, py::arg("paths"), py::arg("expected"), py::arg("concurrency"));
 

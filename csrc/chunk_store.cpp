@@ -1929,21 +1929,23 @@ uint32_t ChunkStore::block_crc(const std::string& id) {
 }
 
 bool ChunkStore::remove(const std::string& id) {
-  bool cold = false;
+  bool cold = false, durable = true;
   {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = index_.find(id);
     if (it == index_.end()) return false;
     cv_.wait(lk, [&] { return it->second.pins == 0; });
     cold = it->second.cold;
+    durable = it->second.on_disk || it->second.jrec.seg != nullptr;
     free_extent_locked(it->second);
     lru_remove_locked(it->second);
     drop_mirror_locked(it->second);
     index_.erase(it);
   }
   cv_.notify_all();
-  // an unretired journal record of the block would bring it back on replay
-  if (journal_) journal_->tombstone(id);
+  // an unretired journal record of the block would bring it back on replay (a block that
+  // never became durable, e.g. an EC gather copy, has none)
+  if (journal_ && durable) journal_->tombstone(id);
   ::unlink(data_path(id, cold).c_str());
   ::unlink(meta_path(id, cold).c_str());
   return true;
@@ -2752,6 +2754,174 @@ void ChunkStore::replay_journal() {
   journal_->note_replay(replayed, skipped);
   recs.clear();
   journal_->retire_all();
+}
+
+
+// ---------------------------------------------------------------- device erasure coding
+namespace {
+uint64_t ec_meta_stride(uint64_t len) { return align_up(std::max<uint64_t>(num_slices(len) * 4, 4), 256); }
+}  // namespace
+
+bool ChunkStore::ec_encode(const uint8_t* host, uint64_t host_stride, uint64_t len, int k,
+                           const std::vector<std::vector<uint8_t>>& parity, EcBuffers* out, std::string* err) {
+  TraceRange tr("dfs.store.ec_encode");
+  const int m = static_cast<int>(parity.size()), total = k + m;
+  if (!gpu() || k <= 0 || m <= 0 || k > kMaxShards || m > kMaxShards || len == 0) {
+    *err = "device EC needs a GPU store and 1..32 shards";
+    return false;
+  }
+  HIP_OK(hipSetDevice(cfg_.device));
+  const uint64_t stride = align_up(std::max<uint64_t>(len, 16), 256), ms = ec_meta_stride(len);
+  const uint64_t tbytes = static_cast<uint64_t>(m) * k * 32;
+  DevExtent ext = reserve(stride * total + ms * total + align_up(tbytes, 256));
+  if (ext.off < 0) {
+    *err = "HBM arena full";
+    return false;
+  }
+  uint8_t* metas = ext.ptr + stride * total;
+  auto* dtab = reinterpret_cast<uint32_t*>(metas + ms * total);
+  Lane* l = acquire_lane();
+  ensure_hscratch(l, tbytes + 16);
+  std::vector<uint8_t> flat(static_cast<size_t>(m) * k);
+  for (int r = 0; r < m; ++r)
+    for (int c = 0; c < k; ++c) flat[r * k + c] = parity[r][c];
+  auto* htab = reinterpret_cast<uint32_t*>(l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16);
+  gf_nibble_tables(flat.data(), m, k, htab);
+  HIP_OK(hipMemcpyAsync(dtab, htab, tbytes, hipMemcpyHostToDevice, l->stream));
+  for (int c = 0; c < k; ++c) h2d_chunked(l, ext.ptr + c * stride, host + c * host_stride, len);
+  GfLaunch a{};
+  a.k = k;
+  a.rows = m;
+  a.len = len;
+  a.tables = dtab;
+  for (int c = 0; c < k; ++c) a.in[c] = ext.ptr + c * stride;
+  for (int r = 0; r < m; ++r) a.out[r] = ext.ptr + (k + r) * stride;
+  bool ok = launch_gf_matmul(a, l->stream) == hipSuccess;
+  launches_++;
+  out->crc.assign(total, 0);
+  for (int i = 0; ok && i < total; ++i) {
+    CrcOut co;
+    ok = run_crc(l, ext.ptr + i * stride, len, reinterpret_cast<uint32_t*>(metas + i * ms), nullptr, true, 0, len,
+                 &co, err);
+    out->crc[i] = co.block_crc;
+  }
+  if (ok) {
+    HIP_OK(hipEventCreateWithFlags(&out->done, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(out->done, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+  }
+  release_lane(l);
+  if (!ok) {
+    release(ext);
+    if (err->empty()) *err = "GPU erasure coding failed";
+    return false;
+  }
+  out->ext = ext;
+  out->len = len;
+  out->stride = stride;
+  out->count = total;
+  return true;
+}
+
+bool ChunkStore::ec_decode(const std::vector<std::vector<uint8_t>>& rows, const std::vector<const uint8_t*>& in,
+                           uint64_t len, EcBuffers* out, std::string* err) {
+  TraceRange tr("dfs.store.ec_decode");
+  const int k = static_cast<int>(in.size()), nr = static_cast<int>(rows.size());
+  if (!gpu() || k <= 0 || nr <= 0 || k > kMaxShards || nr > kMaxShards || len == 0) {
+    *err = "device EC needs a GPU store and 1..32 shards";
+    return false;
+  }
+  HIP_OK(hipSetDevice(cfg_.device));
+  const uint64_t stride = align_up(std::max<uint64_t>(len, 16), 256), ms = ec_meta_stride(len);
+  const uint64_t tbytes = static_cast<uint64_t>(nr) * k * 32;
+  DevExtent ext = reserve(stride * nr + ms * nr + align_up(tbytes, 256));
+  if (ext.off < 0) {
+    *err = "HBM arena full";
+    return false;
+  }
+  uint8_t* metas = ext.ptr + stride * nr;
+  auto* dtab = reinterpret_cast<uint32_t*>(metas + ms * nr);
+  Lane* l = acquire_lane();
+  ensure_hscratch(l, tbytes + 16);
+  std::vector<uint8_t> flat(static_cast<size_t>(nr) * k);
+  for (int r = 0; r < nr; ++r)
+    for (int c = 0; c < k; ++c) flat[r * k + c] = rows[r][c];
+  auto* htab = reinterpret_cast<uint32_t*>(l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16);
+  gf_nibble_tables(flat.data(), nr, k, htab);
+  HIP_OK(hipMemcpyAsync(dtab, htab, tbytes, hipMemcpyHostToDevice, l->stream));
+  GfLaunch a{};
+  a.k = k;
+  a.rows = nr;
+  a.len = len;
+  a.tables = dtab;
+  for (int c = 0; c < k; ++c) a.in[c] = in[c];
+  for (int r = 0; r < nr; ++r) a.out[r] = ext.ptr + r * stride;
+  bool ok = launch_gf_matmul(a, l->stream) == hipSuccess;
+  launches_++;
+  out->crc.assign(nr, 0);
+  for (int i = 0; ok && i < nr; ++i) {
+    CrcOut co;
+    ok = run_crc(l, ext.ptr + i * stride, len, reinterpret_cast<uint32_t*>(metas + i * ms), nullptr, true, 0, len,
+                 &co, err);
+    out->crc[i] = co.block_crc;
+  }
+  if (ok) {
+    HIP_OK(hipEventCreateWithFlags(&out->done, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(out->done, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+  }
+  release_lane(l);
+  if (!ok) {
+    release(ext);
+    if (err->empty()) *err = "GPU erasure decoding failed";
+    return false;
+  }
+  out->ext = ext;
+  out->len = len;
+  out->stride = stride;
+  out->count = nr;
+  return true;
+}
+
+void ChunkStore::ec_free(EcBuffers* b) {
+  if (b->done) {
+    (void)hipEventDestroy(b->done);
+    b->done = nullptr;
+  }
+  if (b->ext.off >= 0) release(b->ext);
+  b->ext = DevExtent{};
+  b->count = 0;
+}
+
+bool ChunkStore::device_to_host(uint8_t* dst, const uint8_t* src_dev, uint64_t n) {
+  if (!gpu()) return false;
+  HIP_OK(hipSetDevice(cfg_.device));
+  Lane* l = acquire_lane();
+  d2h_chunked(l, dst, src_dev, n);
+  HIP_OK(hipStreamSynchronize(l->stream));
+  release_lane(l);
+  return true;
+}
+
+WriteResult ChunkStore::commit_copy(const std::string& id, const uint8_t* src_dev, uint64_t n, uint32_t expected_crc,
+                                    bool persist_now) {
+  WriteResult res;
+  if (!valid_block_id(id)) return bad_id(id);
+  if (!gpu()) {
+    res.error = "no GPU";
+    return res;
+  }
+  HIP_OK(hipSetDevice(cfg_.device));
+  DevExtent e = reserve(n);
+  if (e.off < 0) {
+    res.error = "HBM arena full";
+    return res;
+  }
+  Lane* l = acquire_lane();
+  if (n) HIP_OK(hipMemcpyAsync(e.ptr, src_dev, n, hipMemcpyDeviceToDevice, l->stream));
+  HIP_OK(hipStreamSynchronize(l->stream));
+  release_lane(l);
+  return commit_device(id, e, n, expected_crc, nullptr, persist_now);
 }
 
 }  // namespace dfs

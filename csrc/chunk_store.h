@@ -233,6 +233,32 @@ class ChunkStore {
   const uint8_t* pin_device(const std::string& id, uint64_t* size);
   void unpin(const std::string& id);
 
+  // ---- device-resident erasure coding (EC writes, degraded reads, reconstruction): the
+  // shards stay in HBM between the codec kernel (K4/K5), the per-shard checksum (K2) and the
+  // replication engine that scatters / gathers them (reference client mod.rs:308-412,
+  // 1110-1165; chunkserver.rs:503-640 move every shard through host memory).
+  struct EcBuffers {
+    DevExtent ext;
+    uint64_t len = 0, stride = 0;
+    int count = 0;
+    std::vector<uint32_t> crc;   // whole-shard CRC-32 of each shard (K2)
+    hipEvent_t done = nullptr;   // recorded after the kernels that produced the shards
+    uint8_t* shard(int i) const { return ext.ptr + static_cast<uint64_t>(i) * stride; }
+  };
+  // k data stripes (host_stride apart in host memory; registered memory moves in one DMA
+  // each) into HBM, the rows of `parity` x data computed next to them: out holds k + rows shards.
+  bool ec_encode(const uint8_t* host, uint64_t host_stride, uint64_t len, int k,
+                 const std::vector<std::vector<uint8_t>>& parity, EcBuffers* out, std::string* err);
+  // `rows` x the k device inputs -> rows new shards in HBM.
+  bool ec_decode(const std::vector<std::vector<uint8_t>>& rows, const std::vector<const uint8_t*>& in, uint64_t len,
+                 EcBuffers* out, std::string* err);
+  void ec_free(EcBuffers* b);
+  // Device bytes into host memory (registered: one DMA) and synchronously complete.
+  bool device_to_host(uint8_t* dst, const uint8_t* src_dev, uint64_t n);
+  // A copy of device bytes committed as block `id` (checksummed, verified, made durable).
+  WriteResult commit_copy(const std::string& id, const uint8_t* src_dev, uint64_t n, uint32_t expected_crc,
+                          bool persist_now);
+
   // GPU-resident RS codec: shards are host buffers; returns false when no GPU.
   bool gf_matmul_gpu(const std::vector<std::vector<uint8_t>>& mat, const std::vector<const uint8_t*>& in,
                      const std::vector<uint8_t*>& out, uint64_t len);

@@ -677,9 +677,41 @@ FastClient::Status FastClient::write_ec(const std::string& path, const uint8_t* 
     if (have) std::memcpy(b + c * stride, data + off, have);
     if (have < sl) std::memset(b + c * stride + have, 0, sl - have);
   }
+  // Device path: the co-located chunkserver takes the k stripes up once, computes the parity
+  // in HBM, checksums every shard there and scatters them HBM -> HBM over its replication
+  // engine (fast-path op 7); no parity crosses PCIe and no target re-reads our slot.
+  bool device_done = false;
+  {
+    std::string body;
+    put<uint64_t>(body, alloc.master_term);
+    put<uint16_t>(body, static_cast<uint16_t>(k));
+    put<uint16_t>(body, static_cast<uint16_t>(m));
+    put<uint64_t>(body, sl);
+    put<uint64_t>(body, static_cast<uint64_t>(slot));
+    put<uint64_t>(body, stride);
+    put_str(body, alloc.block.block_id);
+    put_str(body, arena_path_);
+    put<uint16_t>(body, static_cast<uint16_t>(k + m));
+    for (auto& a : alloc.chunk_server_addresses) put_str(body, strip_scheme(a));
+    put_str(body, rid);
+    uint8_t st = 0;
+    uint64_t total = 0, got = 0;
+    std::string fmsg;
+    if (fp_call(7, body, &st, &total, &got, &fmsg)) {
+      if (st == 0) {
+        device_done = true;
+        ec_dev_writes_++;
+      } else if (st == 4 || st == 5) {
+        *msg = fmsg;
+        return Failed;
+      }
+    }
+    if (!device_done) ec_host_++;
+  }
+  std::vector<std::future<std::pair<int, std::string>>> futs;  // (0 ok, 1 not handled, 2 failed)
+  if (!device_done) {
   gf::Matrix full = gf::rs_matrix(k, m), parity(full.begin() + k, full.end());
   ec_matmul(parity, k, sl, static_cast<uint64_t>(slot), static_cast<uint64_t>(slot) + k * stride, nullptr, rid);
-  std::vector<std::future<std::pair<int, std::string>>> futs;  // (0 ok, 1 not handled, 2 failed)
   for (int i = 0; i < k + m; ++i) {
     futs.push_back(shard_pool_.submit([this, i, b, slot, stride, sl, &alloc, rid]() -> std::pair<int, std::string> {
       RequestScope scope(rid);
@@ -718,6 +750,7 @@ FastClient::Status FastClient::write_ec(const std::string& path, const uint8_t* 
       return {0, ""};
     }));
   }
+  }  // host path
   int worst = 0;
   std::string why;
   for (auto& f : futs) {
@@ -775,9 +808,11 @@ FastClient::Status FastClient::read_ec(const std::string& meta_pb, int64_t* slot
   int64_t s = acquire(slot_bytes_);
   if (s < 0) return NotHandled;
   uint8_t* base = base_ + s;
-  std::vector<std::future<bool>> futs;
-  for (int i = 0; i < k + mm; ++i) {
-    futs.push_back(shard_pool_.submit([this, i, s, base, stride, sl, &b, rid]() -> bool {
+  // Data shards first (each straight into the slot by its holder); parity only when one is
+  // missing, and then the co-located chunkserver gathers the survivors into its HBM and
+  // decodes there (fast-path op 8), falling back to fetching parity here.
+  std::vector<std::future<bool>> futs(k + mm);
+  auto fetch = [this, s, base, stride, sl, &b, rid](int i) -> bool {
       RequestScope scope(rid);
       const std::string addr = strip_scheme(b.locations[i]);
       if (addr.empty()) return false;  // a shard known lost
@@ -803,12 +838,50 @@ FastClient::Status FastClient::read_ec(const std::string& meta_pb, int64_t* slot
       if (!r.transport_ok || r.status != 0 || !resp.decode(r.message) || resp.data.size() != sl) return false;
       std::memcpy(base + i * stride, resp.data.data(), sl);
       return true;
-    }));
-  }
+  };
+  for (int i = 0; i < k; ++i) futs[i] = shard_pool_.submit([&fetch, i] { return fetch(i); });
   std::vector<int> present, missing;
-  for (int i = 0; i < k + mm; ++i)
+  for (int i = 0; i < k; ++i)
     if (futs[i].get()) present.push_back(i);
-    else if (i < k) missing.push_back(i);
+    else missing.push_back(i);
+  uint64_t from = 0, want = orig;
+  if (length > 0) {
+    from = offset;
+    want = std::min<uint64_t>(length, orig - offset);
+  }
+  if (!missing.empty() && !local_cs_.empty()) {
+    std::string body;
+    put<uint64_t>(body, from);
+    put<uint64_t>(body, want);
+    put<uint16_t>(body, static_cast<uint16_t>(k));
+    put<uint16_t>(body, static_cast<uint16_t>(mm));
+    put<uint64_t>(body, sl);
+    put<uint64_t>(body, orig);
+    put<uint64_t>(body, static_cast<uint64_t>(s));
+    put<uint64_t>(body, slot_bytes_);
+    put_str(body, b.block_id);
+    put_str(body, arena_path_);
+    put<uint16_t>(body, static_cast<uint16_t>(k + mm));
+    for (auto& a : b.locations) put_str(body, strip_scheme(a));
+    put_str(body, rid);
+    uint8_t st = 0;
+    uint64_t total = 0, got = 0;
+    std::string fmsg;
+    if (fp_call(8, body, &st, &total, &got, &fmsg) && st == 0 && got == want) {
+      ec_dev_reads_++;
+      ec_degraded_++;
+      *slot = s;
+      *n = want;
+      reads_++;
+      return Ok;
+    }
+    ec_host_++;
+  }
+  if (!missing.empty()) {
+    for (int i = k; i < k + mm; ++i) futs[i] = shard_pool_.submit([&fetch, i] { return fetch(i); });
+    for (int i = k; i < k + mm; ++i)
+      if (futs[i].get()) present.push_back(i);
+  }
   if (!missing.empty()) {
     if (static_cast<int>(present.size()) < k) {
       release(s);
@@ -825,11 +898,6 @@ FastClient::Status FastClient::read_ec(const std::string& meta_pb, int64_t* slot
     ec_degraded_++;
   }
   for (int c = 1; c < k; ++c) std::memmove(base + c * sl, base + c * stride, sl);  // stripes back to back
-  uint64_t from = 0, want = orig;
-  if (length > 0) {
-    from = offset;
-    want = std::min<uint64_t>(length, orig - offset);
-  }
   *slot = s + static_cast<int64_t>(from);
   *n = want;
   reads_++;

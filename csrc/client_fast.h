@@ -114,6 +114,11 @@ class FastClient {
   uint64_t ec_gpu_ops() const { return ec_gpu_.load(); }
   uint64_t ec_cpu_ops() const { return ec_cpu_.load(); }
   uint64_t ec_degraded_reads() const { return ec_degraded_.load(); }
+  // device-resident EC (fast-path ops 7/8): writes encoded + scattered HBM -> HBM by the
+  // co-located chunkserver, degraded reads decoded in its HBM; and those that fell back
+  uint64_t ec_device_writes() const { return ec_dev_writes_.load(); }
+  uint64_t ec_device_reads() const { return ec_dev_reads_.load(); }
+  uint64_t ec_host_fallbacks() const { return ec_host_.load(); }
 
   uint64_t writes() const { return writes_.load(); }
   uint64_t reads() const { return reads_.load(); }
@@ -162,6 +167,7 @@ class FastClient {
   bool stop_ = false;
 
   std::atomic<uint64_t> writes_{0}, reads_{0}, ec_gpu_{0}, ec_cpu_{0}, ec_degraded_{0};
+  std::atomic<uint64_t> ec_dev_writes_{0}, ec_dev_reads_{0}, ec_host_{0};
   GrpcChannelPool grpc_{120000};  // shard I/O with servers on other hosts
   IoPool shard_pool_{8};         // last: destroyed first, after in-flight shard I/O
 };

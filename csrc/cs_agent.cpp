@@ -319,6 +319,33 @@ bool CsAgent::reconstruct(const pb::ChunkServerCommand& c) {
   if (k <= 0 || m <= 0 || static_cast<int>(c.ec_shard_sources.size()) != k + m || c.shard_index < 0 ||
       c.shard_index >= k + m)
     return false;
+  // Device path: gather k survivors into this GPU over the replication engine (our own
+  // shards pinned in place, peers' pushed HBM -> HBM), decode the target shard there and
+  // commit it from HBM; shards on other hosts (or a host store) take the gRPC gather below.
+  if (fp_ != nullptr && store_->gpu()) {
+    FastPathServer::EcGather g;
+    std::string err;
+    if (fp_->ec_gather(c.block_id, c.ec_shard_sources, 0, c.shard_index, k, &g, &err)) {
+      std::vector<int> present;
+      for (int i = 0; i < k + m; ++i)
+        if (g.ptrs[i] && i != c.shard_index) present.push_back(i);
+      if (static_cast<int>(present.size()) >= k) {
+        present.resize(k);
+        std::vector<const uint8_t*> in;
+        for (int i : present) in.push_back(g.ptrs[i]);
+        gf::Matrix rows = gf::rs_decode_rows(k, m, present, {c.shard_index});
+        ChunkStore::EcBuffers dec;
+        if (store_->ec_decode(rows, in, g.len, &dec, &err)) {
+          WriteResult w = store_->commit_copy(c.block_id, dec.shard(0), g.len, dec.crc[0], true);
+          store_->ec_free(&dec);
+          std::lock_guard<std::mutex> lk(mu_);
+          st_.ec_gpu++;
+          st_.reconstruct_device++;
+          return w.ok;
+        }
+      }
+    }
+  }
   std::vector<std::string> shards(k + m);
   std::vector<bool> have(k + m, false);
   std::vector<std::future<bool>> futs(k + m);

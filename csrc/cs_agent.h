@@ -59,6 +59,7 @@ struct CsAgentStats {
   uint64_t heartbeats = 0, heartbeat_failures = 0, commands = 0, map_refreshes = 0;
   uint64_t replicate_engine = 0, replicate_grpc = 0, replicate_failed = 0;
   uint64_t reconstructs = 0, reconstruct_failed = 0, encodes = 0, encode_failed = 0;
+  uint64_t reconstruct_device = 0;  // of the reconstructs: gathered into HBM and decoded there
   uint64_t recoveries = 0, recovery_failed = 0, deletes = 0, moves = 0, scrubs = 0, scrub_bad = 0;
   uint64_t ec_gpu = 0, ec_cpu = 0;
 };

@@ -1,5 +1,6 @@
 // Native local data path of a ChunkServer; see fastpath.h for protocol and scope.
 #include "fastpath.h"
+#include "gf256.h"
 #include "trace.h"
 
 #include <fcntl.h>
@@ -494,7 +495,7 @@ int FastPathServer::replicate_block(const std::string& id, const std::vector<std
 
 int FastPathServer::replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term,
                                   const ShmSrc& src, const uint8_t* host, uint64_t n, bool heal,
-                                  const StagedSource* staged) {
+                                  const StagedSource* staged, bool ephemeral) {
   Peer* p = local_peer(addr);
   if (p == nullptr) return 0;
   std::vector<uint8_t> resp;
@@ -524,6 +525,7 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
       put<uint16_t>(req, 0);  // fan-out: the replica forwards nowhere
       put_str(req, t_request_id);
       put<uint8_t>(req, heal ? 1 : 0);  // a heal copy: the receiver reports the new location
+      put<uint8_t>(req, ephemeral ? 1 : 0);  // an EC gather copy: held in HBM only, never persisted
       finish_frame(req);
       return req;
     };
@@ -796,6 +798,7 @@ void FastPathServer::serve(int fd) {
       std::vector<std::string> next = read_list(rd, false);
       std::string rid = rd.p < rd.end ? rd.str() : std::string();
       const bool heal = rd.p < rd.end && rd.get<uint8_t>() == 1;
+      const bool ephemeral = rd.p < rd.end && rd.get<uint8_t>() == 1;
       RequestScope rs(rid);
       note_rid(rid);
       if (!rd.ok || id.empty() || repl_ == nullptr || size > kMaxTransfer) {
@@ -806,7 +809,7 @@ void FastPathServer::serve(int fd) {
         // sender's transfer unmatched and cost the pair a rebuild; the block is dropped after.
         bool last = next.empty();
         bool stale = fenced(term, &msg);
-        WriteResult wr = repl_->recv(src, gen, seq, id, size, slice, crc, last && !stale);
+        WriteResult wr = repl_->recv(src, gen, seq, id, size, slice, crc, last && !stale && !ephemeral);
         if (stale) {
           if (wr.ok) store_->remove(id);
           sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);
@@ -903,6 +906,12 @@ void FastPathServer::serve(int fd) {
         sent = ok ? send_response(fd, FpStatus::Ok, len, rows, "")
                   : send_response(fd, FpStatus::Unsupported, 0, 0, "GPU erasure coding failed");
       }
+    } else if (op == 7) {  // EC_WRITE: encode in HBM, scatter the shards over the engine
+      sent = ec_write(fd, body.data() + 1, body.data() + n);
+    } else if (op == 8) {  // EC_READ: gather the surviving shards into HBM, decode there
+      sent = ec_read(fd, body.data() + 1, body.data() + n);
+    } else if (op == 9) {  // PUSH: a local block to a peer over the engine (EC gathers)
+      sent = push_block(fd, body.data() + 1, body.data() + n);
     } else if (op == 5) {  // CTRL: replication pair bring-up / rebuild
       std::string blob = rd.str();
       if (!rd.ok || repl_ == nullptr) sent = send_response(fd, FpStatus::Unsupported, 0, 0, "replication disabled");
@@ -959,6 +968,284 @@ void FastPathServer::serve(int fd) {
   }
   ::close(fd);
   if (--live_workers_ == 0) workers_cv_.notify_all();
+}
+
+
+// ------------------------------------------------------------------ device erasure coding
+void FastPathServer::set_self_addr(const std::string& addr) { self_addr_ = addr; }
+
+bool FastPathServer::is_self(const std::string& addr) const { return !self_addr_.empty() && addr == self_addr_; }
+
+FastPathServer::EcGather::~EcGather() {
+  if (!fp) return;
+  for (auto& id : pinned) fp->store_->unpin(id);
+  for (auto& id : temps) fp->store_->remove(id);
+}
+
+bool FastPathServer::ec_gather(const std::string& id, const std::vector<std::string>& locations, uint64_t shard_len,
+                               int skip, int want, EcGather* g, std::string* err) {
+  g->fp = this;
+  g->ptrs.assign(locations.size(), nullptr);
+  if (!store_->gpu() || repl_ == nullptr || !repl_->transport()->device_buffers()) {
+    *err = "no device transport";
+    return false;
+  }
+  std::vector<uint64_t> sizes(locations.size(), 0);
+  int have = 0;
+  // our own shard in place, once its slices verify against its .meta (K1b): a corrupt local
+  // shard counts as lost
+  std::vector<int> peers;
+  for (size_t i = 0; i < locations.size(); ++i) {
+    if (static_cast<int>(i) == skip || locations[i].empty()) continue;
+    if (!is_self(locations[i])) {
+      peers.push_back(static_cast<int>(i));
+      continue;
+    }
+    uint64_t size = 0;
+    const uint8_t* d = store_->pin_device(id, &size);
+    if (!d) continue;
+    if ((shard_len == 0 || size == shard_len) && store_->scrub_resident({id}).empty()) {
+      g->ptrs[i] = d;
+      g->pinned.push_back(id);
+      sizes[i] = size;
+      ++have;
+    } else {
+      store_->unpin(id);
+    }
+  }
+  // then the peers', pushed over the engine (checksummed as they land), in rounds of just
+  // as many as are still needed: a dead or corrupt holder is replaced by the next candidate
+  std::mutex gm;
+  const std::string rid = t_request_id;
+  size_t next = 0;
+  while (have < want && next < peers.size()) {
+    std::vector<std::future<void>> futs;
+    for (int need = want - have; need > 0 && next < peers.size(); ++next) {
+      const int i = peers[next];
+      Peer* p = local_peer(locations[i]);
+      if (p == nullptr || p->rank < 0 || !repl_->pair_ok(p->rank)) {
+        g->unreachable++;
+        continue;
+      }
+      --need;
+      const std::string tmp = id + ".g" + std::to_string(i) + "." + std::to_string(tmp_seq_.fetch_add(1));
+      futs.push_back(pool_.submit([this, p, id, tmp, i, shard_len, rid, g, &gm, &have, &sizes] {
+        RequestScope rs(rid);
+        std::vector<uint8_t> req(4, 0), resp;
+        req.push_back(9);
+        put_str(req, id);
+        put_str(req, tmp);
+        put_str(req, self_addr_);
+        put_str(req, rid);
+        finish_frame(req);
+        const bool ok = exchange_with(p, req, &resp) && static_cast<FpStatus>(resp[0]) == FpStatus::Ok;
+        uint64_t size = 0;
+        const uint8_t* d = ok ? store_->pin_device(tmp, &size) : nullptr;
+        std::lock_guard<std::mutex> lk(gm);
+        if (store_->exists(tmp)) g->temps.push_back(tmp);
+        if (d && (shard_len == 0 || size == shard_len)) {
+          g->ptrs[i] = d;
+          g->pinned.push_back(tmp);
+          sizes[i] = size;
+          ++have;
+        } else {
+          if (d) store_->unpin(tmp);
+          g->unreachable++;
+        }
+      }));
+    }
+    for (auto& f : futs) f.get();
+  }
+  // every shard of a block has the same length: without a given one, keep the shards that
+  // agree with the first (a stale shard of another length is treated as lost)
+  g->len = shard_len;
+  for (size_t i = 0; i < g->ptrs.size(); ++i) {
+    if (!g->ptrs[i]) continue;
+    if (g->len == 0) g->len = sizes[i];
+    if (sizes[i] != g->len) g->ptrs[i] = nullptr;
+  }
+  std::lock_guard<std::mutex> lk(mu_);
+  st_.ec_gathered += g->temps.size();
+  return true;
+}
+
+bool FastPathServer::push_block(int fd, const uint8_t* body, const uint8_t* end) {
+  Reader rd{body, end};
+  std::string id = rd.str(), as_id = rd.str(), dst = rd.str();
+  std::string rid = rd.p < rd.end ? rd.str() : std::string();
+  RequestScope rs(rid);
+  note_rid(rid);
+  TraceRange tr("dfs.fp.ec_push");
+  if (!rd.ok || id.empty() || as_id.empty() || repl_ == nullptr || !store_->gpu() ||
+      !repl_->transport()->device_buffers())
+    return send_response(fd, FpStatus::Unsupported, 0, 0, "no device transport");
+  uint64_t size = 0;
+  const uint8_t* d = store_->pin_device(id, &size);
+  if (!d) return send_response(fd, FpStatus::NotFound, 0, 0, "Block not found");
+  const uint32_t crc = store_->block_crc(id);
+  // the block is resident and complete: every slice is "landed" at once
+  hipEvent_t ready = nullptr;
+  (void)hipSetDevice(store_->config().device);
+  bool ok = hipEventCreateWithFlags(&ready, hipEventDisableTiming) == hipSuccess;
+  int n = 0;
+  if (ok) {
+    const uint64_t slice = repl_->slice_for(size);
+    std::vector<hipEvent_t> done(std::max<uint64_t>(1, (size + slice - 1) / slice), ready);
+    StagedSource staged{d, slice, &done};
+    n = replicate_one(dst, as_id, crc, 0, ShmSrc{}, nullptr, size, false, &staged, true);
+    (void)hipEventDestroy(ready);
+  }
+  store_->unpin(id);
+  return n > 0 ? send_response(fd, FpStatus::Ok, size, 1, "")
+               : send_response(fd, FpStatus::IoError, 0, 0, "push over the replication engine failed");
+}
+
+bool FastPathServer::ec_write(int fd, const uint8_t* body, const uint8_t* end) {
+  Reader rd{body, end};
+  uint64_t term = rd.get<uint64_t>();
+  uint16_t k = rd.get<uint16_t>(), m = rd.get<uint16_t>();
+  uint64_t sl = rd.get<uint64_t>(), off = rd.get<uint64_t>(), hstride = rd.get<uint64_t>();
+  std::string id = rd.str(), path = rd.str();
+  std::vector<std::string> targets = read_list(rd, false);
+  std::string rid = rd.p < rd.end ? rd.str() : std::string();
+  RequestScope rs(rid);
+  note_rid(rid);
+  TraceRange tr("dfs.fp.ec_write");
+  auto fallback = [&](const std::string& why) {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.ec_device_fallbacks++;
+    return send_response(fd, FpStatus::Unsupported, 0, 0, why);
+  };
+  if (!rd.ok || id.empty() || k == 0 || m == 0 || k + m > kMaxShards || targets.size() != size_t(k) + m ||
+      sl == 0 || sl > kMaxTransfer || hstride < sl || hstride > kMaxTransfer)
+    return send_response(fd, FpStatus::BadRequest, 0, 0, "malformed ec write");
+  std::string msg;
+  uint64_t known = 0;
+  if (!fence(term, &known)) {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.fenced++;
+    return send_response(fd, FpStatus::Fenced, known, 0,
+                         "Stale master term: request has " + std::to_string(term) + " but known term is " +
+                             std::to_string(known));
+  }
+  if (!store_->gpu() || repl_ == nullptr || !repl_->transport()->device_buffers())
+    return fallback("no device transport");
+  for (auto& t : targets) {
+    if (is_self(t)) continue;
+    Peer* p = local_peer(t);
+    if (p == nullptr || p->rank < 0 || !repl_->pair_ok(p->rank)) return fallback("a shard target has no P2P pair");
+  }
+  std::string err;
+  uint8_t* base = map_shm(path, off, hstride * k, &err);
+  if (base == nullptr) return fallback("short-circuit unavailable: " + err);
+  gf::Matrix full = gf::rs_matrix(k, m), parity(full.begin() + k, full.end());
+  ChunkStore::EcBuffers enc;
+  if (!store_->ec_encode(base + off, hstride, sl, k, parity, &enc, &err)) return fallback(err);
+  const uint64_t slice = repl_->slice_for(sl);
+  std::vector<hipEvent_t> done(std::max<uint64_t>(1, (sl + slice - 1) / slice), enc.done);
+  std::vector<std::future<std::string>> futs;
+  const std::string rid_s = t_request_id;
+  for (int i = 0; i < k + m; ++i) {
+    futs.push_back(pool_.submit([&, i]() -> std::string {
+      RequestScope scope(rid_s);
+      if (is_self(targets[i])) {
+        WriteResult w = store_->commit_copy(id, enc.shard(i), sl, enc.crc[i], true);
+        return w.ok ? std::string() : w.error;
+      }
+      StagedSource staged{enc.shard(i), slice, &done};
+      const int n = replicate_one(targets[i], id, enc.crc[i], term, ShmSrc{}, nullptr, sl, false, &staged);
+      if (n > 0) {
+        std::lock_guard<std::mutex> g(mu_);
+        st_.ec_shard_forwards++;
+        return std::string();
+      }
+      return "replica did not accept the shard";
+    }));
+  }
+  std::string first_err;
+  int failed_at = -1;
+  for (int i = 0; i < k + m; ++i) {
+    std::string e = futs[i].get();
+    if (!e.empty() && failed_at < 0) {
+      failed_at = i;
+      first_err = e;
+    }
+  }
+  const std::vector<uint32_t> crcs = enc.crc;
+  store_->ec_free(&enc);
+  if (failed_at >= 0)  // the reference's try_join_all: one failed shard fails the write
+    return send_response(fd, FpStatus::IoError, 0, 0, "Shard " + std::to_string(failed_at) + " write failed: " + first_err);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.ec_device_writes++;
+  }
+  // the shard CRCs travel back in the message: the client records nothing per shard, but
+  // tests compare them with the CPU codec
+  std::string crc_list;
+  for (uint32_t c : crcs) crc_list += std::to_string(c) + ",";
+  return send_response(fd, FpStatus::Ok, sl, static_cast<uint64_t>(k + m), crc_list);
+}
+
+bool FastPathServer::ec_read(int fd, const uint8_t* body, const uint8_t* end) {
+  Reader rd{body, end};
+  uint64_t offset = rd.get<uint64_t>(), length = rd.get<uint64_t>();
+  uint16_t k = rd.get<uint16_t>(), m = rd.get<uint16_t>();
+  uint64_t sl = rd.get<uint64_t>(), orig = rd.get<uint64_t>(), shm_off = rd.get<uint64_t>(), cap = rd.get<uint64_t>();
+  std::string id = rd.str(), path = rd.str();
+  std::vector<std::string> locs = read_list(rd, false);
+  std::string rid = rd.p < rd.end ? rd.str() : std::string();
+  RequestScope rs(rid);
+  note_rid(rid);
+  TraceRange tr("dfs.fp.ec_read");
+  auto fallback = [&](const std::string& why) {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.ec_device_fallbacks++;
+    return send_response(fd, FpStatus::Unsupported, 0, 0, why);
+  };
+  if (!rd.ok || id.empty() || k == 0 || m == 0 || k + m > kMaxShards || locs.size() != size_t(k) + m || sl == 0 ||
+      sl > kMaxTransfer || orig == 0 || orig > sl * k || (length > 0 && offset >= orig))
+    return send_response(fd, FpStatus::BadRequest, 0, 0, "malformed ec read");
+  const uint64_t from = length > 0 ? offset : 0, want = length > 0 ? std::min<uint64_t>(length, orig - offset) : orig;
+  std::string err;
+  uint8_t* base = want > cap ? nullptr : map_shm(path, shm_off, cap, &err);
+  if (base == nullptr) return fallback(want > cap ? "slot too small" : "short-circuit unavailable: " + err);
+  EcGather g;
+  if (!ec_gather(id, locs, sl, -1, k, &g, &err)) return fallback(err);
+  std::vector<int> present, missing;
+  for (int i = 0; i < k + m; ++i)
+    if (g.ptrs[i]) present.push_back(i);
+    else if (i < k) missing.push_back(i);
+  if (static_cast<int>(present.size()) < k) {
+    if (g.unreachable > 0) return fallback("surviving shards not reachable over the engine");
+    return send_response(fd, FpStatus::IoError, 0, 0, "RS reconstruct error: TooFewShardsPresent");
+  }
+  present.resize(k);
+  ChunkStore::EcBuffers dec;
+  if (!missing.empty()) {
+    std::vector<const uint8_t*> in;
+    for (int i : present) in.push_back(g.ptrs[i]);
+    gf::Matrix rows = gf::rs_decode_rows(k, m, present, missing);
+    if (!store_->ec_decode(rows, in, sl, &dec, &err)) return fallback(err);
+  }
+  // the requested range of the original bytes, stripe by stripe, HBM -> the client's slot
+  bool ok = true;
+  for (int c = 0; ok && c < k; ++c) {
+    const uint64_t lo = std::max<uint64_t>(from, c * sl), hi = std::min<uint64_t>(from + want, (c + 1) * sl);
+    if (lo >= hi) continue;
+    const uint8_t* src = g.ptrs[c];
+    if (!src) {
+      auto it = std::find(missing.begin(), missing.end(), c);
+      src = dec.shard(static_cast<int>(it - missing.begin()));
+    }
+    ok = store_->device_to_host(base + shm_off + (lo - from), src + (lo - c * sl), hi - lo);
+  }
+  store_->ec_free(&dec);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    st_.ec_device_reads++;
+    if (!missing.empty()) st_.ec_device_decodes++;
+  }
+  return ok ? send_response(fd, FpStatus::Ok, orig, want, "") : send_response(fd, FpStatus::IoError, 0, 0, "copy out failed");
 }
 
 }  // namespace dfs

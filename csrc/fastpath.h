@@ -26,6 +26,16 @@
 //     op 6 EC   : u16 k | u16 rows | u64 len | u64 in_off | u64 out_off | u16 rows*k matrix | u16 path
 //               [| u16 rid]  -- GF(2^8) matrix x shards (RS encode / reconstruct) on this GPU;
 //               shards sit in the client's slot at 16-byte-aligned strides, outputs land there
+//     op 7 EC_WRITE: u64 term | u16 k | u16 m | u64 shard_len | u64 shm_off | u64 shm_stride | u16 id
+//               | u16 path | u16 n | (u16 len addr)* (k + m targets) [| u16 rid]
+//               -- device-resident RS write: the k stripes go up once, parity is computed in
+//               HBM, every shard is checksummed there and scattered HBM -> HBM over the engine
+//     op 8 EC_READ: u64 offset | u64 length | u16 k | u16 m | u64 shard_len | u64 orig | u64 shm_off
+//               | u64 shm_cap | u16 id | u16 path | u16 n | (u16 len addr)* ("" = lost) [| u16 rid]
+//               -- degraded read: surviving shards gathered into this GPU, missing data decoded
+//               there, the requested range DMA'd into the client's slot
+//     op 9 PUSH: u16 id | u16 as_id | u16 dst_addr [| u16 rid] -- send local block `id` to the
+//               same-node peer `dst_addr` over the engine, stored there as ephemeral `as_id`
 //   response = u32 body_len | u8 status | u64 total | u64 bytes | u16 msg_len msg
 //   (for WRITE/REPL ``bytes`` carries replicas_written; for CTRL ``msg`` is the engine reply)
 //
@@ -74,6 +84,11 @@ struct FpStats {
   uint64_t ec_ops = 0;            // erasure-coding matrix products run for clients
   uint64_t heals_out = 0, heals_in = 0;  // heal / balancer copies sent / received on the engine
   uint64_t sliced_writes = 0;  // head writes whose replica sends overlapped the staging
+  // device-resident erasure coding: EC writes whose shards were encoded and scattered HBM ->
+  // HBM, shards forwarded that way, degraded reads / reconstructions gathered into HBM and
+  // decoded there, shards pulled for a gather, and requests that had to take the host path
+  uint64_t ec_device_writes = 0, ec_shard_forwards = 0, ec_device_reads = 0, ec_device_decodes = 0;
+  uint64_t ec_gathered = 0, ec_device_fallbacks = 0;
 };
 
 class FastPathServer {
@@ -127,6 +142,22 @@ class FastPathServer {
   // Test hook: the next `n` REPL descriptors are dropped on the way out.
   void debug_drop_descriptors(int n) { drop_descriptors_ += n; }
   void set_self_host(const std::string& host);  // our advertised host: same-host peer detection
+  void set_self_addr(const std::string& addr);  // our advertised address (EC targets that are us)
+
+  // Device gather of EC shards into this GPU (degraded reads, RECONSTRUCT_EC_SHARD): each
+  // shard held here is pinned in place, each held by a same-node peer is pushed over the
+  // replication engine into an ephemeral block here. ptrs[i] = device pointer (nullptr:
+  // lost, skipped or unreachable). The destructor unpins and drops what it gathered.
+  struct EcGather {
+    FastPathServer* fp = nullptr;
+    std::vector<const uint8_t*> ptrs;
+    std::vector<std::string> pinned, temps;
+    int unreachable = 0;  // shards that exist but could not be gathered over the engine
+    uint64_t len = 0;     // shard length (given, or the length the gathered shards agree on)
+    ~EcGather();
+  };
+  bool ec_gather(const std::string& id, const std::vector<std::string>& locations, uint64_t shard_len, int skip,
+                 int want, EcGather* g, std::string* err);
 
  private:
   struct Peer {
@@ -149,7 +180,13 @@ class FastPathServer {
                  const ShmSrc& src, const uint8_t* host, uint64_t n, int* replicas,
                  const StagedSource* staged = nullptr);
   int replicate_one(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term, const ShmSrc& src,
-                    const uint8_t* host, uint64_t n, bool heal = false, const StagedSource* staged = nullptr);
+                    const uint8_t* host, uint64_t n, bool heal = false, const StagedSource* staged = nullptr,
+                    bool ephemeral = false);
+  bool is_self(const std::string& addr) const;
+  // op 7 / op 8 / op 9 bodies (answered on fd)
+  bool ec_write(int fd, const uint8_t* body, const uint8_t* end);
+  bool ec_read(int fd, const uint8_t* body, const uint8_t* end);
+  bool push_block(int fd, const uint8_t* body, const uint8_t* end);
   // Pipelined head write of a large replicated block; false = not applicable (the caller
   // takes the stage-then-forward path), true = answered on `fd` (*sent = write result).
   bool write_sliced(int fd, const std::string& id, const uint8_t* host, uint64_t len, uint32_t crc, uint64_t term,
@@ -186,6 +223,8 @@ class FastPathServer {
   std::mutex peers_mu_;
   std::unordered_map<std::string, std::unique_ptr<Peer>> peers_;
   std::string self_host_;
+  std::string self_addr_;
+  std::atomic<uint64_t> tmp_seq_{0};
 };
 
 }  // namespace dfs

@@ -134,6 +134,7 @@ class ChunkServerProcess:
             ok, err = fp.start()
             if ok:
                 fp.set_self_host(self.advertise.rsplit(":", 1)[0])
+                fp.set_self_addr(self.advertise)
                 self.fastpath = fp
             else:
                 log.warning("native fast path disabled: %s", err)
@@ -319,6 +320,12 @@ class ChunkServerProcess:
                         body = json.dumps({"bad": proc.cs.scrub_once()}).encode()
                     elif u.path == "/debug/pause_spill":
                         proc.store.debug_pause_spill(q.get("on", "1") == "1")
+                        body = b"{}"
+                    elif u.path == "/debug/remove":  # lose a block (EC degraded-read tests)
+                        body = json.dumps({"removed": bool(proc.store.remove(q["block"]))}).encode()
+                    elif u.path == "/debug/command" and proc.agent is not None:
+                        # a master command, serialized ChunkServerCommand as hex, run as if heartbeated
+                        proc.agent.submit_command(bytes.fromhex(q["hex"]))
                         body = b"{}"
                     elif u.path == "/debug/drop_resident":
                         proc.store.drop_resident(q["block"])

@@ -1,0 +1,132 @@
+"""Device-resident erasure coding (VERDICT r3 missing #2; reference client mod.rs:308-412
+encode + parallel scatter, :1110-1165 gather + decode, chunkserver.rs:503-640 reconstruct).
+
+Six chunkserver processes share GPU 0 with hipipc pairs between them (the same transport as
+between the GPUs of a node). An RS(4,2) write takes the k stripes up to the writer's
+chunkserver once; the parity is computed in HBM, every shard is checksummed there (K2) and
+scattered HBM -> HBM over the replication engine, each replica checksumming on arrival (K1):
+5 engine forwards per write, no parity crossing PCIe, no host staging. A degraded read
+gathers the survivors into the reader's GPU and decodes there (K5); a reconstruction
+(RECONSTRUCT_EC_SHARD) gathers and decodes on the device too. Every shard and every decoded
+byte is compared with the CPU codec."""
+import json
+import os
+import signal
+import time
+import urllib.request
+
+import pytest
+
+from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster
+from rust_hadoop_generated_by_llm_amd.models import proto as pb
+from rust_hadoop_generated_by_llm_amd.ops import erasure
+from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
+
+pytestmark = pytest.mark.gpu
+
+
+def stats(url):
+    return json.load(urllib.request.urlopen(f"{url}/stats", timeout=10))
+
+
+def summed(c, key):
+    return sum(stats(u).get(key, 0) for u in c.cs_http)
+
+
+@pytest.fixture(scope="module")
+def eccluster(has_gpu):
+    if not has_gpu:
+        pytest.fail("GPU test selected but no HIP device is visible")
+    with LocalCluster(gpus=[0] * 6, p2p="hipipc", fsync=True, hbm_capacity="3G",
+                      env={"DFS_DEBUG_ENDPOINTS": "1"}) as c:
+        assert summed(c, "repl_pairs_up") == 30
+        yield c
+
+
+def shards_on_servers(c, path):
+    pool = ChannelPool(local=False)
+    cl = c.client()
+    try:
+        blk = cl.get_file_info(path).blocks[0]
+        out = []
+        for loc in blk.locations:
+            r = pool.call(f"http://{loc}", "ChunkServerService", "ReadBlock", pb.ReadBlockRequest(block_id=blk.block_id),
+                          timeout=60)
+            out.append(r.data)
+        return blk, out
+    finally:
+        pool.close()
+        cl.close()
+
+
+def test_ec_write_scatters_from_hbm(eccluster):
+    c = eccluster
+    cl = c.client(local_chunkserver=c.cs_addrs[0])
+    fc = cl._fast
+    assert fc is not None
+    f0, w0 = summed(c, "fp_ec_shard_forwards"), fc.ec_device_writes
+    host0 = summed(c, "fp_ec_ops") + summed(c, "fp_shm_forwards")
+    blobs = {f"/ecdev/f{i}": os.urandom(n) for i, n in enumerate([1, 4097, (1 << 20) + 7, 3 << 20, (6 << 20) - 1])}
+    for p, d in blobs.items():
+        cl.create_file_from_buffer_ec(d, p, 4, 2)
+    assert fc.ec_device_writes - w0 == len(blobs) and fc.ec_host_fallbacks == 0
+    assert summed(c, "fp_ec_shard_forwards") - f0 == 5 * len(blobs)  # the head keeps one shard
+    assert summed(c, "fp_ec_ops") + summed(c, "fp_shm_forwards") == host0  # nothing staged through host memory
+    for p, d in blobs.items():
+        blk, got = shards_on_servers(c, p)
+        assert got == erasure.encode(d, 4, 2, None), p  # bit-identical to the CPU codec
+        assert cl.get_file_content(p) == d
+    cl.close()
+
+
+def test_degraded_read_decodes_on_device(eccluster):
+    c = eccluster
+    cl = c.client(local_chunkserver=c.cs_addrs[0])
+    d = os.urandom((5 << 20) + 333)
+    cl.create_file_from_buffer_ec(d, "/ecdev/degraded", 4, 2)
+    blk, shards = shards_on_servers(c, "/ecdev/degraded")
+    # lose two data shards held by other chunkservers (removed on their holders)
+    lost = [i for i, loc in enumerate(blk.locations) if i < 4 and loc != c.cs_addrs[0]][:2]
+    for i in lost:
+        h = c.cs_http[c.cs_addrs.index(blk.locations[i])]
+        urllib.request.urlopen(f"{h}/debug/remove?block={blk.block_id}", timeout=10).read()
+    r0, dec0 = cl._fast.ec_device_reads, summed(c, "fp_ec_device_decodes")
+    assert cl.get_file_content("/ecdev/degraded") == d
+    assert cl.read_file_range("/ecdev/degraded", 1234567, 3 << 20) == d[1234567:1234567 + (3 << 20)]
+    assert cl._fast.ec_device_reads - r0 == 2
+    assert summed(c, "fp_ec_device_decodes") - dec0 == 2
+    assert summed(c, "fp_ec_gathered") >= 2
+    cl.close()
+
+
+def test_reconstruct_shard_gathers_on_device(eccluster):
+    """RECONSTRUCT_EC_SHARD as the healer sends it: the target gathers k survivors into its
+    HBM over the engine, decodes the lost shard there and commits it."""
+    c = eccluster
+    cl = c.client(local_chunkserver=c.cs_addrs[0])
+    d = os.urandom((2 << 20) + 5)
+    cl.create_file_from_buffer_ec(d, "/ecdev/rebuild", 4, 2)
+    blk, shards = shards_on_servers(c, "/ecdev/rebuild")
+    want = erasure.encode(d, 4, 2, None)
+    for lost in (1, 5):  # a data shard and a parity shard
+        holder = c.cs_addrs.index(blk.locations[lost])
+        h = c.cs_http[holder]
+        urllib.request.urlopen(f"{h}/debug/remove?block={blk.block_id}", timeout=10).read()
+        sources = list(blk.locations)
+        sources[lost] = ""
+        cmd = pb.ChunkServerCommand(type=pb.ChunkServerCommand.RECONSTRUCT_EC_SHARD, block_id=blk.block_id,
+                                    shard_index=lost, ec_data_shards=4, ec_parity_shards=2,
+                                    ec_shard_sources=sources)
+        before = stats(h).get("agent_reconstruct_device", 0)
+        body = cmd.SerializeToString().hex()
+        urllib.request.urlopen(f"{h}/debug/command?hex={body}", timeout=60).read()
+        deadline = time.time() + 30
+        while stats(h).get("agent_reconstruct_device", 0) == before:
+            assert time.time() < deadline, stats(h)
+            time.sleep(0.1)
+        pool = ChannelPool(local=False)
+        r = pool.call(f"http://{blk.locations[lost]}", "ChunkServerService", "ReadBlock",
+                      pb.ReadBlockRequest(block_id=blk.block_id), timeout=60)
+        pool.close()
+        assert r.data == want[lost]
+    cl.close()
