@@ -121,13 +121,17 @@ static void disk_case(const std::string& dir, int threads, int per, bool direct,
 // frame) to ONE preallocated, already-written segment at reserved offsets; a record is
 // durable once a group fdatasync that started after its pwrite completed. mode 0: buffered
 // appends, 1: O_DIRECT appends, 2: O_DIRECT|O_DSYNC per append (no group commit).
-static void journal_case(const std::string& dir, int threads, int per, int mode, bool first) {
+static void journal_case(const std::string& dir, int threads, int per, int mode, bool first, bool falloc = false) {
   std::filesystem::create_directories(dir);
   const size_t n = 1 << 20, hdr = 4096, rec = n + hdr;
   const uint64_t total = uint64_t(threads) * per * rec;
   std::string f = dir + "/journal.seg";
   int fd = ::open(f.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0644);
-  {  // preallocate by writing: later appends overwrite written extents (no metadata change)
+  if (falloc) {  // unwritten extents: every first write converts them (a metadata change per flush)
+    (void)::fallocate(fd, 0, 0, static_cast<off_t>(total));
+    ::fsync(fd);
+    ::close(fd);
+  } else {  // preallocate by writing: later appends overwrite written extents (no metadata change)
     std::vector<uint8_t> z(8 << 20, 0);
     for (uint64_t off = 0; off < total; off += z.size())
       if (::pwrite(fd, z.data(), std::min<uint64_t>(z.size(), total - off), off) < 0) break;
@@ -181,8 +185,8 @@ static void journal_case(const std::string& dir, int threads, int per, int mode,
   Lat all;
   for (auto& l : lat) all.v.insert(all.v.end(), l.v.begin(), l.v.end());
   static const char* names[] = {"buffered", "direct", "direct_dsync"};
-  std::printf("%s\n    {\"journal\": \"%s\", \"threads\": %d, \"records\": %d, \"GBps\": %.2f, \"p50_ms\": %.3f, \"p99_ms\": %.3f, \"sync_rounds\": %llu, \"errors\": %d}",
-              first ? "" : ",", names[mode], threads, threads * per, double(threads) * per * n / el / 1e9,
+  std::printf("%s\n    {\"journal\": \"%s%s\", \"threads\": %d, \"records\": %d, \"GBps\": %.2f, \"p50_ms\": %.3f, \"p99_ms\": %.3f, \"sync_rounds\": %llu, \"errors\": %d}",
+              first ? "" : ",", names[mode], falloc ? "_fallocated" : "", threads, threads * per, double(threads) * per * n / el / 1e9,
               all.pct(0.5) * 1e3, all.pct(0.99) * 1e3, static_cast<unsigned long long>(rounds), errors.load());
   std::fflush(stdout);
   std::filesystem::remove_all(dir);
@@ -204,6 +208,7 @@ int main(int argc, char** argv) {
         disk_case(dir + "_files", t, std::max(8, 2400 / t / 4), false, 0, first);
         first = false;
         for (int mode = 0; mode < 3; ++mode) journal_case(dir, t, std::max(8, 2400 / t / 4), mode, false);
+        journal_case(dir, t, std::max(8, 2400 / t / 4), 0, false, true);
       }
       std::printf("\n]}\n");
       return 0;

@@ -112,7 +112,55 @@ BlockJournal::BlockJournal(JournalConfig cfg) : cfg_(std::move(cfg)) {
   if (::mkdir(cfg_.dir.c_str(), 0755) == 0) fsync_dir(parent_of(cfg_.dir));
 }
 
-BlockJournal::~BlockJournal() = default;
+BlockJournal::~BlockJournal() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    prep_stop_ = true;
+  }
+  cv_.notify_all();
+  if (preparer_.joinable()) preparer_.join();
+}
+
+// Creates segment files up to the cap, zero-filled so appends overwrite written extents,
+// keeping `spares` of them ready for the writers (recycled segments count as ready).
+void BlockJournal::prepare_loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait(lk, [&] {
+      return prep_stop_ || (static_cast<int>(free_.size()) + preparing_ < std::max(1, cfg_.spares) &&
+                            static_cast<int>(segs_.size()) + preparing_ < cfg_.max_segs);
+    });
+    if (prep_stop_) return;
+    ++preparing_;
+    const std::string path = cfg_.dir + "/seg-" + std::to_string(next_file_++) + ".log";
+    lk.unlock();
+    SegRef s = open_seg(path, true);
+    bool ok = s != nullptr;
+    if (ok) {
+      if (cfg_.zero_fill) {
+        static const std::vector<uint8_t> zeros(8 << 20, 0);
+        for (uint64_t off = 0; ok && off < s->cap; off += zeros.size())
+          ok = pwrite_all(s->fd, zeros.data(), std::min<uint64_t>(zeros.size(), s->cap - off), off);
+      }
+      ok = ok && (!cfg_.sync || ::fdatasync(s->fd) == 0);
+      (void)::posix_fadvise(s->fd, 0, 0, POSIX_FADV_DONTNEED);
+      fsync_dir(cfg_.dir);  // the name survives a crash before its first record is acked
+    }
+    lk.lock();
+    --preparing_;
+    if (ok) {
+      segs_.push_back(s);
+      free_.push_back(s);
+      st_.prepared++;
+    } else {
+      ::unlink(path.c_str());
+      // no room for another segment: run with the ones there are (a writer waits for the
+      // materializer to recycle one instead of failing)
+      cfg_.max_segs = std::max<int>(2, static_cast<int>(segs_.size()));
+    }
+    cv_.notify_all();
+  }
+}
 
 uint64_t BlockJournal::hdr_bytes_for(uint64_t nslices) { return align_up(kHdr + 4 * nslices, kPage); }
 
@@ -221,6 +269,7 @@ std::vector<ReplayRecord> BlockJournal::recover() {
     order_.push_back(s);
   }
   st_.segs_total = segs_.size();
+  preparer_ = std::thread([this] { prepare_loop(); });  // spares get ready while the caller replays
   return out;
 }
 
@@ -262,20 +311,12 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
       *err = "journal failed";
       return nullptr;
     }
+    if (!preparer_.joinable()) preparer_ = std::thread([this] { prepare_loop(); });
     SegRef s;
     if (!free_.empty()) {
       s = free_.back();
       free_.pop_back();
-    } else if (static_cast<int>(segs_.size()) < cfg_.max_segs) {
-      std::string path = cfg_.dir + "/seg-" + std::to_string(next_file_++) + ".log";
-      s = open_seg(path, true);
-      if (!s) {
-        *err = std::string("journal segment ") + path + ": " + std::strerror(errno);
-        return nullptr;
-      }
-      fsync_dir(cfg_.dir);  // the new name must survive a crash before its first record is acked
-      segs_.push_back(s);
-      st_.segs_total = segs_.size();
+      cv_.notify_all();  // the preparer tops the spares up again
     }
     if (s) {
       const uint64_t seq = next_seq_++;
@@ -293,7 +334,7 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
       order_.push_back(s);
       return s;
     }
-    ++st_.full_waits;
+    if (static_cast<int>(segs_.size()) + preparing_ >= cfg_.max_segs) ++st_.full_waits;  // not just filling
     if (cv_.wait_until(lk, deadline) == std::cv_status::timeout) {
       *err = "journal full (materializer behind)";
       return nullptr;
@@ -418,6 +459,7 @@ bool BlockJournal::commit(const JournalRec& r) {
       if (s->done_upto > s->durable_upto) targets.emplace_back(s, s->done_upto);
     lk.unlock();
     bool ok = true;
+    if (cfg_.sync_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.sync_delay_us));
     if (cfg_.sync)
       for (auto& t : targets) ok = ::fdatasync(t.first->fd) == 0 && ok;
     lk.lock();

@@ -30,6 +30,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace dfs {
@@ -40,6 +41,12 @@ struct JournalConfig {
   int max_segs = 16;                // journal capacity = max_segs x seg_bytes
   bool direct = false;              // O_DIRECT appends (aligned sources only; else buffered)
   bool sync = true;                 // fdatasync on commit (false: tests / --no-fsync)
+  // Segments are zero-filled ahead of use by a background thread (written extents: an
+  // append is then a pure overwrite, and its flush carries no allocation metadata); this
+  // many stand ready beyond the active one (recycled segments need no fill).
+  int spares = 2;
+  bool zero_fill = true;   // false: fallocate only (unwritten extents, converted on first use)
+  int sync_delay_us = 0;   // tests: the commit leader waits this long first (makes rounds shared)
 };
 
 enum JournalRecType : uint32_t { kJrBlock = 1, kJrPad = 2, kJrTomb = 3 };
@@ -83,7 +90,7 @@ struct ReplayRecord {
 struct JournalStats {
   uint64_t records = 0, bytes = 0, commits = 0, sync_rounds = 0, tombstones = 0, pads = 0;
   uint64_t segs_total = 0, segs_free = 0, segs_retired = 0, full_waits = 0;
-  uint64_t replayed = 0, replay_skipped = 0;
+  uint64_t replayed = 0, replay_skipped = 0, prepared = 0;
   bool failed = false;
 };
 
@@ -129,8 +136,11 @@ class BlockJournal {
   SegRef activate_locked(std::unique_lock<std::mutex>& lk, std::string* err);
   bool write_seg_header(JournalSeg* s, uint64_t seq);
   void complete_locked(JournalSeg* s, uint64_t off, uint64_t end);
-  void retire_locked();
   SegRef open_seg(const std::string& path, bool create);
+  void prepare_loop();
+  std::thread preparer_;
+  bool prep_stop_ = false;
+  int preparing_ = 0;  // segment files being created and filled (mu_)
 
   JournalConfig cfg_;
   std::mutex mu_;

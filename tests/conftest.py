@@ -7,6 +7,11 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# block journal at test scale: 32 MiB segments, not zero-filled (every store and chunkserver
+# the tests start would otherwise write 512 MiB of spare segments); larger blocks take the
+# per-file path, which the tests exercise as well
+os.environ.setdefault("DFS_JOURNAL_SEG_MB", "32")
+os.environ.setdefault("DFS_JOURNAL_ZERO_FILL", "0")
 
 
 def pytest_configure(config):

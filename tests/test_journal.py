@@ -109,7 +109,9 @@ def test_torn_record_is_dropped_on_replay(native, tmp_path):
         os._exit(0)
     """)
     assert r.returncode == 0, r.stderr
-    seg = next((tmp_path / "hot" / ".journal").glob("seg-*.log"))
+    # the segment holding the records (spare segments are zero-filled)
+    seg = next(p for p in (tmp_path / "hot" / ".journal").glob("seg-*.log")
+               if bytes([67]) * 10000 in p.read_bytes()[: 1 << 20])
     raw = bytearray(seg.read_bytes()[: 1 << 20])
     # the last record's data: flip a byte as a torn write would leave it
     pos = raw.rfind(bytes([67]) * 10000)
@@ -160,9 +162,11 @@ def test_small_journal_recycles_segments_under_pressure(native, tmp_path, monkey
     assert s.stats()["journal_replayed"] == 0 and sorted(s.list_blocks()) == sorted(vals)
 
 
-def test_concurrent_writers_share_group_commits(native, tmp_path):
+def test_concurrent_writers_share_group_commits(native, tmp_path, monkeypatch):
     from concurrent.futures import ThreadPoolExecutor
 
+    # a slow flush (as on a real device) lets the writers that arrive meanwhile join the round
+    monkeypatch.setenv("DFS_JOURNAL_SYNC_DELAY_US", "3000")
     s = open_store(native, tmp_path)
     vals = {f"g{i}": os.urandom(200_000 + i) for i in range(64)}
     with ThreadPoolExecutor(16) as ex:
