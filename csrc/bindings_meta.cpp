@@ -841,9 +841,13 @@ void bind_meta(py::module_& m) {
       .def(py::init([](FastClient* fc, const std::string& host, int port, const std::string& backend, int workers,
                        bool auth_enabled, const std::string& region, const std::string& access_key,
                        const std::string& secret_key, bool allow_unsigned, const std::string& audit_socket,
-                       bool sse_enabled, bool metadata_sidecar, const std::string& policy_epoch) {
+                       bool sse_enabled, bool metadata_sidecar, const std::string& policy_epoch,
+                       const std::string& tls_cert, const std::string& tls_key, py::bytes sse_kek) {
              S3FrontConfig c;
+             c.sse_kek = std::string(sse_kek);
              c.policy_epoch_path = policy_epoch;
+             c.tls_cert = tls_cert;
+             c.tls_key = tls_key;
              c.host = host;
              c.port = port;
              c.backend = backend;
@@ -862,6 +866,7 @@ void bind_meta(py::module_& m) {
            py::arg("auth_enabled") = false, py::arg("region") = "us-east-1", py::arg("access_key") = "",
            py::arg("secret_key") = "", py::arg("allow_unsigned_payload") = true, py::arg("audit_socket") = "",
            py::arg("sse_enabled") = false, py::arg("metadata_sidecar") = false, py::arg("policy_epoch") = "",
+           py::arg("tls_cert") = "", py::arg("tls_key") = "", py::arg("sse_kek") = py::bytes(),
            py::keep_alive<1, 2>())
       .def("drop_policies", &S3Front::drop_policies, py::call_guard<py::gil_scoped_release>())
       .def("start", [](S3Front& f) {
@@ -894,6 +899,10 @@ void bind_meta(py::module_& m) {
         d["policy_native"] = s.policy_native;
         d["audit_sent"] = s.audit_sent;
         d["audit_dropped"] = s.audit_dropped;
+        d["tls_handshakes"] = s.tls_handshakes;
+        d["tls_failures"] = s.tls_failures;
+        d["sse_puts"] = s.sse_puts;
+        d["sse_gets"] = s.sse_gets;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;
         return d;

@@ -6,6 +6,9 @@
 #include <openssl/param_build.h>
 #include <openssl/rand.h>
 
+#include <algorithm>
+#include <cctype>
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 
@@ -73,6 +76,76 @@ std::string aes256gcm_decrypt(const std::string& key, const std::string& nonce, 
     throw std::runtime_error("aead::Error: authentication failed");
   out.resize(static_cast<size_t>(total + len));
   return out;
+}
+
+void aes256gcm_encrypt_inplace(const uint8_t* key, const uint8_t* nonce, uint8_t* p, size_t n, uint8_t* tag) {
+  CipherCtx ctx(EVP_CIPHER_CTX_new());
+  int len = 0;
+  if (!EVP_EncryptInit_ex(ctx.get(), EVP_aes_256_gcm(), nullptr, nullptr, nullptr) ||
+      !EVP_CIPHER_CTX_ctrl(ctx.get(), EVP_CTRL_GCM_SET_IVLEN, 12, nullptr) ||
+      !EVP_EncryptInit_ex(ctx.get(), nullptr, nullptr, key, nonce))
+    throw std::runtime_error("aes-gcm init failed");
+  for (size_t off = 0; off < n;) {  // GCM is a stream mode: in place is allowed
+    const int k = static_cast<int>(std::min<size_t>(n - off, 1u << 30));
+    if (!EVP_EncryptUpdate(ctx.get(), p + off, &len, p + off, k)) throw std::runtime_error("aes-gcm update failed");
+    off += static_cast<size_t>(k);
+  }
+  if (!EVP_EncryptFinal_ex(ctx.get(), p + n, &len) || len != 0) throw std::runtime_error("aes-gcm final failed");
+  if (!EVP_CIPHER_CTX_ctrl(ctx.get(), EVP_CTRL_GCM_GET_TAG, 16, tag)) throw std::runtime_error("aes-gcm tag failed");
+}
+
+bool aes256gcm_decrypt_inplace(const uint8_t* key, const uint8_t* nonce, uint8_t* p, size_t n, const uint8_t* tag) {
+  CipherCtx ctx(EVP_CIPHER_CTX_new());
+  int len = 0;
+  if (!EVP_DecryptInit_ex(ctx.get(), EVP_aes_256_gcm(), nullptr, nullptr, nullptr) ||
+      !EVP_CIPHER_CTX_ctrl(ctx.get(), EVP_CTRL_GCM_SET_IVLEN, 12, nullptr) ||
+      !EVP_DecryptInit_ex(ctx.get(), nullptr, nullptr, key, nonce))
+    return false;
+  for (size_t off = 0; off < n;) {
+    const int k = static_cast<int>(std::min<size_t>(n - off, 1u << 30));
+    if (!EVP_DecryptUpdate(ctx.get(), p + off, &len, p + off, k)) return false;
+    off += static_cast<size_t>(k);
+  }
+  uint8_t t[16];
+  std::memcpy(t, tag, 16);
+  if (!EVP_CIPHER_CTX_ctrl(ctx.get(), EVP_CTRL_GCM_SET_TAG, 16, t)) return false;
+  uint8_t fin[16];
+  return EVP_DecryptFinal_ex(ctx.get(), fin, &len) > 0;
+}
+
+std::string md5_hex(const uint8_t* p, size_t n) {
+  unsigned char d[EVP_MAX_MD_SIZE];
+  unsigned int len = 0;
+  EVP_Digest(p, n, d, &len, EVP_md5(), nullptr);
+  static const char* hx = "0123456789abcdef";
+  std::string out;
+  for (unsigned i = 0; i < len; ++i) {
+    out.push_back(hx[d[i] >> 4]);
+    out.push_back(hx[d[i] & 15]);
+  }
+  return out;
+}
+
+std::string base64_encode(const std::string& raw) {
+  std::string out(4 * ((raw.size() + 2) / 3) + 1, '\0');
+  const int n = EVP_EncodeBlock(reinterpret_cast<unsigned char*>(&out[0]), u(raw), static_cast<int>(raw.size()));
+  out.resize(static_cast<size_t>(n));
+  return out;
+}
+
+bool base64_decode(const std::string& b64, std::string* raw) {
+  if (b64.size() % 4) return false;
+  for (char ch : b64)
+    if (!(std::isalnum(static_cast<unsigned char>(ch)) || ch == '+' || ch == '/' || ch == '=')) return false;
+  std::string out(b64.size() / 4 * 3 + 1, '\0');
+  const int n = EVP_DecodeBlock(reinterpret_cast<unsigned char*>(&out[0]), u(b64), static_cast<int>(b64.size()));
+  if (n < 0) return false;
+  size_t pad = 0;  // EVP_DecodeBlock keeps the padding's zero bytes
+  if (!b64.empty() && b64.back() == '=') ++pad;
+  if (b64.size() > 1 && b64[b64.size() - 2] == '=') ++pad;
+  out.resize(static_cast<size_t>(n) - pad);
+  *raw = std::move(out);
+  return true;
 }
 
 bool rsa_sha256_verify(const std::string& n, const std::string& e, const std::string& msg, const std::string& sig) {

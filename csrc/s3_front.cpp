@@ -1,10 +1,12 @@
 // Native S3 front end; design notes in s3_front.h.
 #include "s3_front.h"
+#include "crypto.h"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/epoll.h>
 #include <sys/mman.h>
 #include <sys/eventfd.h>
@@ -113,6 +115,37 @@ bool send_head_body(int fd, const std::string& head, const uint8_t* body, size_t
   }
   size_t bo = done - head.size();
   return send_all(fd, body + bo, n - bo);
+}
+
+// One end of a relay or response: a plain socket, or a TLS session on it (the front's
+// client connections when the gateway terminates TLS; the backend socket is always plain).
+struct Io {
+  int fd = -1;
+  TlsConn* tls = nullptr;
+};
+
+long io_recv(Io io, void* p, size_t n) {
+  if (io.tls) return io.tls->read(p, n);  // blocking socket: >0 bytes, -1 closed / error
+  for (;;) {
+    ssize_t k = ::recv(io.fd, p, n, 0);
+    if (k < 0 && errno == EINTR) continue;
+    return k;
+  }
+}
+
+bool send_all(Io io, const void* p, size_t n) {
+  if (!io.tls) return send_all(io.fd, p, n);
+  return io.tls->write_all(p, n, std::chrono::steady_clock::now() + std::chrono::seconds(300));
+}
+
+bool send_head_body(Io io, const std::string& head, const uint8_t* body, size_t n) {
+  if (!io.tls) return send_head_body(io.fd, head, body, n);
+  if (n + head.size() <= (16 << 10)) {  // one TLS record for a small response
+    std::string all = head;
+    if (n) all.append(reinterpret_cast<const char*>(body), n);
+    return send_all(io, all.data(), all.size());
+  }
+  return send_all(io, head.data(), head.size()) && send_all(io, body, n);
 }
 
 std::string http_date(uint64_t ms) {
@@ -234,6 +267,8 @@ struct S3Front::Conn {
   std::string ip;
   std::string buf;
   size_t pos = 0;
+  std::unique_ptr<TlsConn> tls;  // TLS terminated here (cfg_.tls_cert)
+  Io io() const { return Io{fd, tls.get()}; }
 };
 
 struct S3Front::Req {
@@ -280,6 +315,14 @@ bool S3Front::start(std::string* err) {
   socklen_t al = sizeof a;
   ::getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &al);
   cfg_.port = ntohs(a.sin_port);
+  if (!cfg_.tls_cert.empty()) {
+    tls_ = TlsContext::server_http1(cfg_.tls_cert, cfg_.tls_key, err);
+    if (!tls_) {
+      ::close(lfd_);
+      lfd_ = -1;
+      return false;
+    }
+  }
   if (!cfg_.audit_socket.empty()) audit_fd_ = ::socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
   if (!cfg_.policy_epoch_path.empty()) {
     int efd = ::open(cfg_.policy_epoch_path.c_str(), O_RDONLY | O_CLOEXEC);
@@ -418,11 +461,35 @@ void S3Front::serve(Conn* c) {
     delete c;
   };
   char tmp[64 << 10];
+  if (tls_ && !c->tls) {  // first time this connection is served: the TLS handshake
+    c->tls = std::make_unique<TlsConn>(tls_, c->fd);
+    std::string err;
+    if (!c->tls->handshake("", std::chrono::steady_clock::now() + std::chrono::seconds(10), &err)) {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.tls_failures++;
+      return close_conn();
+    }
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.tls_handshakes++;
+  }
   for (;;) {
     if (c->pos == c->buf.size()) {
       c->buf.clear();
       c->pos = 0;
-      ssize_t n = ::recv(c->fd, tmp, sizeof tmp, MSG_DONTWAIT);
+      ssize_t n;
+      if (c->tls) {
+        // decrypted bytes may already sit in the session; otherwise poll the socket once
+        pollfd pf{c->fd, POLLIN, 0};
+        if (!c->tls->pending() && ::poll(&pf, 1, 0) <= 0) {
+          n = -1;
+          errno = EAGAIN;
+        } else {
+          n = c->tls->read(tmp, sizeof tmp);
+          if (n < 0) n = 0;  // closed
+        }
+      } else {
+        n = ::recv(c->fd, tmp, sizeof tmp, MSG_DONTWAIT);
+      }
       if (n == 0 || (n < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)) return close_conn();
       if (n < 0) {  // idle: back to the epoll thread
         epoll_event ev{};
@@ -436,7 +503,7 @@ void S3Front::serve(Conn* c) {
     size_t end;
     while ((end = c->buf.find("\r\n\r\n", c->pos)) == std::string::npos) {
       if (c->buf.size() - c->pos > kMaxHead) return close_conn();
-      ssize_t n = ::recv(c->fd, tmp, sizeof tmp, 0);
+      long n = io_recv(c->io(), tmp, sizeof tmp);
       if (n <= 0) return close_conn();
       c->buf.append(tmp, static_cast<size_t>(n));
     }
@@ -507,14 +574,17 @@ bool S3Front::handle(Conn* c, Req& r) {
   if (!q.empty() && !part) return proxy(c, r, nullptr, 0, "query");
   const bool is_put = r.method == "PUT", is_get = r.method == "GET", is_head = r.method == "HEAD";
   if (!(is_put || ((is_get || is_head) && !part))) return proxy(c, r, nullptr, 0, "method");
-  if (cfg_.sse_enabled) return proxy(c, r, nullptr, 0, "sse");
+  // SSE-S3: whole objects are encrypted / decrypted here (AES-256-GCM, the gateway's DEK
+  // envelope); multipart parts of an SSE gateway stay on the Python path
+  if (cfg_.sse_enabled && (cfg_.sse_kek.size() != 32 || part)) return proxy(c, r, nullptr, 0, "sse");
   if (is_put) {
     if (r.chunked || r.get("x-amz-copy-source") || cfg_.metadata_sidecar) return proxy(c, r, nullptr, 0, "put-form");
     const std::string* sha = r.get("x-amz-content-sha256");
     const std::string* enc = r.get("content-encoding");
     if ((sha && sha->compare(0, 10, "STREAMING-") == 0) || (enc && enc->find("aws-chunked") != std::string::npos))
       return proxy(c, r, nullptr, 0, "aws-chunked");
-    if (static_cast<uint64_t>(r.content_length) > fc_->slot_bytes()) return proxy(c, r, nullptr, 0, "large");
+    if (static_cast<uint64_t>(r.content_length) + (cfg_.sse_enabled ? 28 : 0) > fc_->slot_bytes())
+      return proxy(c, r, nullptr, 0, "large");
   } else if (r.content_length > 0 || r.chunked) {
     return proxy(c, r, nullptr, 0, "body");
   }
@@ -761,8 +831,7 @@ static bool read_body(S3Front::Conn* c, uint8_t* dst, uint64_t n) {
   c->pos += have;
   uint64_t got = have;
   while (got < n) {
-    ssize_t k = ::recv(c->fd, dst + got, n - got, 0);
-    if (k < 0 && errno == EINTR) continue;
+    long k = io_recv(c->io(), dst + got, n - got);
     if (k <= 0) return false;
     got += static_cast<uint64_t>(k);
   }
@@ -779,38 +848,65 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
       return proxy(c, r, nullptr, 0, "no-upload");
   }
   const uint64_t n = static_cast<uint64_t>(r.content_length);
-  int64_t slot = fc_->acquire_slot(std::max<uint64_t>(n, 1));
+  const bool sse = cfg_.sse_enabled && !part;  // handle() sent SSE parts to Python
+  const uint64_t stored = sse ? n + 28 : n;    // [nonce 12][ciphertext n][tag 16]
+  int64_t slot = fc_->acquire_slot(std::max<uint64_t>(stored, 1));
   if (slot < 0) return proxy(c, r, nullptr, 0, "no-slot");
   struct Release {
     FastClient* fc;
     int64_t s;
     ~Release() { fc->release(s); }
   } rel{fc_, slot};
-  if (r.expect_continue && !send_all(c->fd, "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+  if (r.expect_continue && !send_all(c->io(), "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
   uint8_t* dst = fc_->slot_mut(slot);
-  if (!read_body(c, dst, n)) return false;
+  if (!read_body(c, sse ? dst + 12 : dst, n)) return false;
   std::map<std::string, std::string> attrs;
+  std::string plain_md5, dk;
+  if (sse) {
+    // SseManager.encrypt_object (reference auth/sse.rs:10-62): a fresh DEK encrypts the
+    // object in place, the KEK wraps the DEK; the ETag stays the plaintext's MD5
+    plain_md5 = crypto::md5_hex(dst + 12, n);
+    dk = crypto::random_bytes(32);
+    const std::string n1 = crypto::random_bytes(12), n2 = crypto::random_bytes(12);
+    std::memcpy(dst, n1.data(), 12);
+    crypto::aes256gcm_encrypt_inplace(reinterpret_cast<const uint8_t*>(dk.data()), dst, dst + 12, n, dst + 12 + n);
+    const std::string wrapped = n2 + crypto::aes256gcm_encrypt(cfg_.sse_kek, n2, dk, "");
+    attrs["x-amz-sse-encrypted-dek"] = crypto::base64_encode(wrapped);
+  }
   if (!part) {
     // put_object: ETag, x-amz-meta-* (lower-cased) and Content-Type become the attributes
     for (auto& h : r.headers)
       if (h.first.compare(0, 11, "x-amz-meta-") == 0) attrs[h.first] = h.second;
     if (const std::string* ct = r.get("content-type")) attrs["Content-Type"] = *ct;
-    attrs["ETag"] = "";
+    attrs["ETag"] = sse ? "\"" + plain_md5 + "\"" : "";
   }
   FastClient::Times t;
   std::string msg, md5;
   int reps = 0;
-  auto st = fc_->write_slot(path, slot, n, &reps, &msg, &t, r.rid, part ? nullptr : &attrs, part ? nullptr : "ETag",
-                            &md5);
+  // without SSE the ETag attribute is the MD5 the write computes of the stored bytes
+  const char* etag_attr = part || sse ? nullptr : "ETag";
+  auto st = fc_->write_slot(path, slot, stored, &reps, &msg, &t, r.rid, part ? nullptr : &attrs, etag_attr, &md5);
   if (st == FastClient::Failed && msg.find("already exists") != std::string::npos) {
     // _put_replace: an existing key is replaced (delete, then create again)
     std::string dmsg;
     if (fc_->remove(path, &dmsg, r.rid) != FastClient::NotHandled)
-      st = fc_->write_slot(path, slot, n, &reps, &msg, &t, r.rid, part ? nullptr : &attrs, part ? nullptr : "ETag",
-                           &md5);
+      st = fc_->write_slot(path, slot, stored, &reps, &msg, &t, r.rid, part ? nullptr : &attrs, etag_attr, &md5);
   }
-  if (st != FastClient::Ok) return proxy(c, r, dst, n, "put-fallback");
-  std::string head = "HTTP/1.1 200 OK\r\nETag: \"" + md5 + "\"\r\nContent-Length: 0\r\n";
+  if (st != FastClient::Ok) {
+    if (!sse) return proxy(c, r, dst, n, "put-fallback");
+    // the slot holds ciphertext: decrypt it back so Python gets the body it would have read
+    if (!crypto::aes256gcm_decrypt_inplace(reinterpret_cast<const uint8_t*>(dk.data()), dst, dst + 12, n,
+                                           dst + 12 + n))
+      return false;
+    return proxy(c, r, dst + 12, n, "put-fallback");
+  }
+  if (sse) {
+    md5 = plain_md5;
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.sse_puts++;
+  }
+  std::string head = "HTTP/1.1 200 OK\r\nETag: \"" + md5 + "\"\r\n" +
+                     (sse ? "x-amz-server-side-encryption: AES256\r\n" : "") + "Content-Length: 0\r\n";
   head += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
   r.status = 200;
   count(r, 200);
@@ -819,13 +915,14 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
     (part ? st_.parts : st_.puts)++;
     st_.bytes_in += n;
   }
-  return send_all(c->fd, head.data(), head.size());
+  return send_all(c->io(), head.data(), head.size());
 }
 
 namespace {
 
 // _object_headers of s3/server.py; false: a case Python owns (SSE, sidecar metadata)
-bool object_headers(const pb::FileMetadata* m, const std::map<std::string, std::string>& attrs, std::string* out) {
+bool object_headers(const pb::FileMetadata* m, const std::map<std::string, std::string>& attrs, std::string* out,
+                    std::string* dek = nullptr) {
   std::string etag = m && !m->etag_md5.empty() ? "\"" + m->etag_md5 + "\"" : kEmptyEtag;
   std::string h = "Last-Modified: " + http_date(m ? m->created_at_ms : 0) + "\r\nAccept-Ranges: bytes\r\n";
   bool ctype = false;
@@ -833,7 +930,9 @@ bool object_headers(const pb::FileMetadata* m, const std::map<std::string, std::
     if (kv.first == "ETag") {
       etag = kv.second;
     } else if (kv.first == "x-amz-sse-encrypted-dek") {
-      return false;
+      if (!dek) return false;  // a caller that cannot decrypt
+      *dek = kv.second;
+      h += "x-amz-server-side-encryption: AES256\r\n";
     } else if (kv.first.compare(0, 11, "x-amz-meta-") == 0 || kv.first == "Content-Type") {
       if (kv.second.find_first_of("\r\n") != std::string::npos) return false;
       h += kv.first + ": " + kv.second + "\r\n";
@@ -865,9 +964,11 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   }
   pb::FileMetadata m;
   if (!m.decode(meta)) return proxy(c, r, nullptr, 0, "decode");
-  std::string hdrs;
-  if (m.attributes.empty() || !object_headers(&m, m.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
+  std::string hdrs, dek;
+  if (m.attributes.empty() || !object_headers(&m, m.attributes, &hdrs, &dek)) return proxy(c, r, nullptr, 0, "attrs");
+  if (!dek.empty() && cfg_.sse_kek.size() != 32) return proxy(c, r, nullptr, 0, "sse");
   const std::string ka = r.keep_alive ? "Connection: keep-alive\r\n" : "Connection: close\r\n";
+  if (!dek.empty() && !head) return sse_get(c, r, meta, m.size, hdrs, dek);
   if (head) {
     std::string h = "HTTP/1.1 200 OK\r\n" + hdrs + "Content-Length: " + std::to_string(m.size) + "\r\n" + ka + "\r\n";
     r.status = 200;
@@ -876,7 +977,7 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
       std::lock_guard<std::mutex> g(st_mu_);
       st_.heads++;
     }
-    return send_all(c->fd, h.data(), h.size());
+    return send_all(c->io(), h.data(), h.size());
   }
   uint64_t s = 0, e = 0;
   int rng = parse_range(r.get("range"), m.size, &s, &e);
@@ -909,7 +1010,7 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   }
   h += "Content-Length: " + std::to_string(got) + "\r\n" + ka + "\r\n";
   count(r, r.status);
-  const bool ok = send_head_body(c->fd, h, got ? fc_->slot_ptr(slot) : nullptr, got);
+  const bool ok = send_head_body(c->io(), h, got ? fc_->slot_ptr(slot) : nullptr, got);
   const auto t3 = SC::now();
   auto us = [](SC::duration d) { return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::microseconds>(d).count()); };
   {
@@ -922,6 +1023,63 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
     st_.get_timed++;
   }
   return ok;
+}
+
+// GET of an SSE object (SseManager.decrypt_object, reference auth/sse.rs:64-110): the whole
+// ciphertext is read into a slot, the DEK unwrapped with the KEK, the object decrypted in
+// place (the GCM tag authenticates it) and the (range of the) plaintext sent from there.
+bool S3Front::sse_get(Conn* c, Req& r, const std::string& meta, uint64_t size, const std::string& hdrs,
+                      const std::string& dek_b64) {
+  TraceRange tr("dfs.s3.get_sse");
+  std::string wrapped, dk;
+  if (size < 28 || size > fc_->slot_bytes() || !crypto::base64_decode(dek_b64, &wrapped) || wrapped.size() < 60)
+    return proxy(c, r, nullptr, 0, "sse");
+  try {
+    dk = crypto::aes256gcm_decrypt(cfg_.sse_kek, wrapped.substr(0, 12), wrapped.substr(12), "");
+  } catch (const std::exception&) {
+    return proxy(c, r, nullptr, 0, "sse");  // Python answers 500 InternalError
+  }
+  if (dk.size() != 32) return proxy(c, r, nullptr, 0, "sse");
+  int64_t slot = -1;
+  uint64_t got = 0;
+  std::string msg;
+  FastClient::Times t;
+  if (fc_->read_known(meta, &slot, &got, &msg, &t, r.rid, 0, 0) != FastClient::Ok) return proxy(c, r, nullptr, 0, "read");
+  struct Release {
+    FastClient* fc;
+    int64_t s;
+    ~Release() {
+      if (s >= 0) fc->release(s);
+    }
+  } rel{fc_, slot};
+  if (got != size) return proxy(c, r, nullptr, 0, "short-read");
+  uint8_t* b = fc_->slot_mut(slot);
+  const uint64_t plen = size - 28;
+  if (!crypto::aes256gcm_decrypt_inplace(reinterpret_cast<const uint8_t*>(dk.data()), b, b + 12, plen, b + 12 + plen))
+    return proxy(c, r, nullptr, 0, "sse");
+  uint64_t s = 0, e = 0;
+  int rng = parse_range(r.get("range"), plen, &s, &e);
+  if (rng >= 2) return proxy(c, r, nullptr, 0, "range");
+  const uint64_t from = rng == 1 ? s : 0, want = rng == 1 ? e - s + 1 : plen;
+  const std::string ka = r.keep_alive ? "Connection: keep-alive\r\n" : "Connection: close\r\n";
+  std::string h;
+  if (rng == 1) {
+    h = "HTTP/1.1 206 Partial Content\r\n" + hdrs + "Content-Range: bytes " + std::to_string(s) + "-" +
+        std::to_string(e) + "/" + std::to_string(plen) + "\r\n";
+    r.status = 206;
+  } else {
+    h = "HTTP/1.1 200 OK\r\n" + hdrs;
+    r.status = 200;
+  }
+  h += "Content-Length: " + std::to_string(want) + "\r\n" + ka + "\r\n";
+  count(r, r.status);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    (rng == 1 ? st_.range_gets : st_.gets)++;
+    st_.sse_gets++;
+    st_.bytes_out += want;
+  }
+  return send_head_body(c->io(), h, b + 12 + from, want);
 }
 
 // GET of a completed multipart object: the parts' sizes come from the layout the completion
@@ -1033,8 +1191,8 @@ bool S3Front::native_mpu_get(Conn* c, Req& r, const std::string& path, const std
       ok = false;
       continue;
     }
-    bool w = sent_head ? send_all(c->fd, fc_->slot_ptr(g.slot), g.n)
-                       : send_head_body(c->fd, h, fc_->slot_ptr(g.slot), g.n);
+    bool w = sent_head ? send_all(c->io(), fc_->slot_ptr(g.slot), g.n)
+                       : send_head_body(c->io(), h, fc_->slot_ptr(g.slot), g.n);
     sent_head = true;
     fc_->release(g.slot);
     if (!w) ok = false;
@@ -1087,11 +1245,11 @@ namespace {
 
 // Copies one HTTP/1.1 chunked body from `src` (with `buf` holding bytes already read past
 // `*pos`) to `dst`, raw. Returns false on any I/O or framing error.
-bool relay_chunked(int src, std::string& buf, size_t* pos, int dst) {
+bool relay_chunked(Io src, std::string& buf, size_t* pos, Io dst) {
   auto need = [&](size_t k) {
     char tmp[kRelayChunk];
     while (buf.size() - *pos < k) {
-      ssize_t n = ::recv(src, tmp, sizeof tmp, 0);
+      long n = io_recv(src, tmp, sizeof tmp);
       if (n <= 0) return false;
       buf.append(tmp, static_cast<size_t>(n));
     }
@@ -1136,15 +1294,14 @@ bool relay_chunked(int src, std::string& buf, size_t* pos, int dst) {
   }
 }
 
-bool relay_n(int src, std::string& buf, size_t* pos, int dst, uint64_t n) {
+bool relay_n(Io src, std::string& buf, size_t* pos, Io dst, uint64_t n) {
   uint64_t have = std::min<uint64_t>(n, buf.size() - *pos);
   if (have && !send_all(dst, buf.data() + *pos, have)) return false;
   *pos += have;
   n -= have;
   std::vector<char> tmp(kRelayChunk);
   while (n) {
-    ssize_t k = ::recv(src, tmp.data(), std::min<uint64_t>(n, tmp.size()), 0);
-    if (k < 0 && errno == EINTR) continue;
+    long k = io_recv(src, tmp.data(), std::min<uint64_t>(n, tmp.size()));
     if (k <= 0 || !send_all(dst, tmp.data(), static_cast<size_t>(k))) return false;
     n -= static_cast<uint64_t>(k);
   }
@@ -1194,7 +1351,7 @@ bool S3Front::proxy(Conn* c, Req& r, const uint8_t* body, uint64_t body_len, con
   int be = backend_conn();
   auto bad_gateway = [&] {
     const char* m = "HTTP/1.1 502 Bad Gateway\r\nContent-Length: 0\r\nConnection: close\r\n\r\n";
-    send_all(c->fd, m, std::strlen(m));
+    send_all(c->io(), m, std::strlen(m));
     return false;
   };
   if (be < 0) return bad_gateway();
@@ -1202,20 +1359,22 @@ bool S3Front::proxy(Conn* c, Req& r, const uint8_t* body, uint64_t body_len, con
   for (size_t i = 0; i < r.headers.size(); ++i) {
     const std::string& n = r.headers[i].first;
     if (n == "connection" || n == "keep-alive" || n == "expect" || n == "proxy-connection" || n == "x-real-ip" ||
-        n == "x-forwarded-for")
+        n == "x-forwarded-for" || n == "x-forwarded-proto")
       continue;
     head += r.names[i] + ": " + r.headers[i].second + "\r\n";
   }
-  head += "X-Real-IP: " + c->ip + "\r\nX-Forwarded-For: " + c->ip + "\r\nConnection: keep-alive\r\n\r\n";
+  // the gateway's TLS requirement sees how the request really arrived (never the client's say)
+  head += "X-Real-IP: " + c->ip + "\r\nX-Forwarded-For: " + c->ip + "\r\nX-Forwarded-Proto: " +
+          (c->tls ? "https" : "http") + "\r\nConnection: keep-alive\r\n\r\n";
   if (!body && r.expect_continue && (r.content_length > 0 || r.chunked) &&
-      !send_all(c->fd, "HTTP/1.1 100 Continue\r\n\r\n", 25)) {
+      !send_all(c->io(), "HTTP/1.1 100 Continue\r\n\r\n", 25)) {
     backend_done(be, false);
     return false;
   }
   bool ok = send_all(be, head.data(), head.size());
   if (ok && body) ok = send_all(be, body, body_len);
-  else if (ok && r.chunked) ok = relay_chunked(c->fd, c->buf, &c->pos, be);
-  else if (ok && r.content_length > 0) ok = relay_n(c->fd, c->buf, &c->pos, be, static_cast<uint64_t>(r.content_length));
+  else if (ok && r.chunked) ok = relay_chunked(c->io(), c->buf, &c->pos, Io{be});
+  else if (ok && r.content_length > 0) ok = relay_n(c->io(), c->buf, &c->pos, Io{be}, static_cast<uint64_t>(r.content_length));
   if (!ok) {
     backend_done(be, false);
     return false;
@@ -1288,22 +1447,22 @@ bool S3Front::proxy(Conn* c, Req& r, const uint8_t* body, uint64_t body_len, con
     o2 += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
     r.status = status;
     backend_done(be, !be_close && rp == rb.size());
-    return send_head_body(c->fd, o2, reinterpret_cast<const uint8_t*>(text.data()), text.size());
+    return send_head_body(c->io(), o2, reinterpret_cast<const uint8_t*>(text.data()), text.size());
   }
   const bool until_close = !no_body && !chunked && clen < 0;
   if (until_close) r.keep_alive = false;
   out += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
   r.status = status;
-  ok = send_all(c->fd, out.data(), out.size());
+  ok = send_all(c->io(), out.data(), out.size());
   if (ok && !no_body) {
     if (chunked) {
-      ok = relay_chunked(be, rb, &rp, c->fd);
+      ok = relay_chunked(Io{be}, rb, &rp, c->io());
     } else if (clen > 0) {
-      ok = relay_n(be, rb, &rp, c->fd, static_cast<uint64_t>(clen));
+      ok = relay_n(Io{be}, rb, &rp, c->io(), static_cast<uint64_t>(clen));
     } else if (until_close) {
-      if (rp < rb.size()) ok = send_all(c->fd, rb.data() + rp, rb.size() - rp);
+      if (rp < rb.size()) ok = send_all(c->io(), rb.data() + rp, rb.size() - rp);
       ssize_t n;
-      while (ok && (n = ::recv(be, tmp, sizeof tmp, 0)) > 0) ok = send_all(c->fd, tmp, static_cast<size_t>(n));
+      while (ok && (n = ::recv(be, tmp, sizeof tmp, 0)) > 0) ok = send_all(c->io(), tmp, static_cast<size_t>(n));
       be_close = true;
     }
   }

@@ -39,6 +39,7 @@
 
 #include "client_fast.h"
 #include "s3_policy.h"
+#include "tls.h"
 #include "io_pool.h"
 
 namespace dfs {
@@ -53,11 +54,14 @@ struct S3FrontConfig {
   std::string access_key, secret_key;  // EnvCredentialProvider (S3_ACCESS_KEY / S3_SECRET_KEY)
   bool allow_unsigned_payload = true;
   std::string audit_socket;  // datagram socket of the audit store ("" = no audit)
-  bool sse_enabled = false;  // objects are encrypted: their data stays on the Python path
+  bool sse_enabled = false;  // SSE-S3: objects are stored encrypted
+  std::string sse_kek;       // the 32-byte KEK (SSE_MASTER_KEY): encryption here; empty: Python does it
   bool metadata_sidecar = false;
   // 8-byte shared counter the gateway's workers bump on every PutBucketPolicy /
   // DeleteBucketPolicy ("" = none): a change empties the front's policy cache at once
   std::string policy_epoch_path;
+  // TLS terminated by the front itself (reference main.rs:263-274 binds rustls): PEM files
+  std::string tls_cert, tls_key;
 };
 
 struct S3FrontStats {
@@ -70,6 +74,7 @@ struct S3FrontStats {
   // native GET/Range GET phases, summed microseconds: metadata stat, block read into the
   // slot, response send (where a GET's latency goes)
   uint64_t get_stat_us = 0, get_read_us = 0, get_send_us = 0, get_timed = 0;
+  uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0;
 };
 
 class S3Front {
@@ -94,6 +99,8 @@ class S3Front {
   bool native_put(Conn* c, Req& r, const std::string& path, bool part);
   bool native_get(Conn* c, Req& r, const std::string& path, bool head);
   bool native_mpu_get(Conn* c, Req& r, const std::string& path, const std::string& marker_meta);
+  bool sse_get(Conn* c, Req& r, const std::string& meta, uint64_t size, const std::string& hdrs,
+               const std::string& dek_b64);
   int verify_auth(Req& r, std::string* user);  // 1 ok, 0 hand over
   // The bucket's policy: *known = false when it could not be read (the request is handed
   // over); a null pointer when the bucket has none (or an unparsable one, which the gateway
@@ -108,6 +115,7 @@ class S3Front {
 
   S3FrontConfig cfg_;
   FastClient* fc_;
+  std::shared_ptr<TlsContext> tls_;
   int lfd_ = -1, epfd_ = -1, evfd_ = -1, audit_fd_ = -1;
   std::atomic<bool> stop_{false};
   std::thread epoller_;

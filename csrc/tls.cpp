@@ -39,7 +39,27 @@ int select_h2(SSL*, const unsigned char** out, unsigned char* outlen, const unsi
   return SSL_TLSEXT_ERR_OK;
 }
 
+const unsigned char kAlpnHttp1[] = {8, 'h', 't', 't', 'p', '/', '1', '.', '1'};
+
+int select_http1(SSL*, const unsigned char** out, unsigned char* outlen, const unsigned char* in,
+                 unsigned int inlen, void*) {
+  unsigned char* o = nullptr;
+  if (SSL_select_next_proto(&o, outlen, kAlpnHttp1, sizeof kAlpnHttp1, in, inlen) != OPENSSL_NPN_NEGOTIATED)
+    return SSL_TLSEXT_ERR_NOACK;  // proceed without ALPN
+  *out = o;
+  return SSL_TLSEXT_ERR_OK;
+}
+
 }  // namespace
+
+std::shared_ptr<TlsContext> TlsContext::server_http1(const std::string& cert, const std::string& key,
+                                                     std::string* err) {
+  auto t = server(cert, key, err);
+  if (!t) return t;
+  t->http1_ = true;
+  SSL_CTX_set_alpn_select_cb(t->ctx_, &select_http1, nullptr);
+  return t;
+}
 
 TlsContext::~TlsContext() {
   if (ctx_) SSL_CTX_free(ctx_);
@@ -137,6 +157,7 @@ bool TlsConn::handshake(const std::string& host, Deadline deadline, std::string*
   const unsigned char* proto = nullptr;
   unsigned int plen = 0;
   SSL_get0_alpn_selected(ssl_, &proto, &plen);
+  if (ctx_->http1()) return true;
   if (plen != 2 || std::memcmp(proto, "h2", 2) != 0) {
     *err = "TLS peer did not negotiate h2 (ALPN)";
     return false;

@@ -23,6 +23,10 @@ class TlsContext {
   ~TlsContext();
   // Server side: certificate chain + private key (PEM files), ALPN h2.
   static std::shared_ptr<TlsContext> server(const std::string& cert, const std::string& key, std::string* err);
+  // Server side for HTTP/1.1 (the S3 front): ALPN "http/1.1" when the client offers it,
+  // none otherwise (S3 clients mostly send no ALPN at all).
+  static std::shared_ptr<TlsContext> server_http1(const std::string& cert, const std::string& key, std::string* err);
+  bool http1() const { return http1_; }
   // Client side: trust `ca` (PEM; empty = system roots), verify the peer's name against
   // `domain` (empty = the host of each target), offer ALPN h2.
   static std::shared_ptr<TlsContext> client(const std::string& ca, const std::string& domain, std::string* err);
@@ -33,6 +37,7 @@ class TlsContext {
  private:
   SSL_CTX* ctx_ = nullptr;
   bool server_ = false;
+  bool http1_ = false;
   std::string domain_;
 };
 

@@ -1229,10 +1229,10 @@ def _die_with_parent() -> None:
 def native_front_wanted(cfg: S3Config) -> bool:
     """The native front end (csrc/s3_front.cpp) serves the object data path when the gateway
     is co-located with a chunkserver (its native client moves bodies through that server's
-    pinned shared memory) and TLS is not terminated here (the front speaks plain HTTP)."""
+    pinned shared memory). It terminates TLS itself (TLS_CERT / TLS_KEY, OpenSSL), like the
+    reference binds rustls directly (main.rs:263-274); the aiohttp workers behind it then
+    listen on a private UNIX socket in plain HTTP."""
     if cfg.env.get("S3_NATIVE_FRONT", "true") != "true" or not cfg.local_chunkserver:
-        return False
-    if cfg.tls_cert and cfg.tls_key:
         return False
     try:
         from ..native import lib  # noqa: F401
@@ -1257,7 +1257,10 @@ def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_
                         allow_unsigned_payload=cfg.allow_unsigned_payload,
                         audit_socket=audit_socket if (cfg.auth_enabled and gw.audit is not None) else "",
                         sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar,
-                        policy_epoch=policy_epoch or (gw.policy_epoch.path or ""))
+                        policy_epoch=policy_epoch or (gw.policy_epoch.path or ""),
+                        tls_cert=cfg.tls_cert or "" if (cfg.tls_cert and cfg.tls_key) else "",
+                        tls_key=cfg.tls_key or "" if (cfg.tls_cert and cfg.tls_key) else "",
+                        sse_kek=gw.sse.kek if gw.sse is not None else b"")
     ok, err = front.start()
     if not ok:
         raise RuntimeError(f"native S3 front end failed to start: {err}")
@@ -1330,7 +1333,7 @@ def main(argv: list[str] | None = None) -> int:
             threading.Thread(target=_audit_ingest, args=(ingest, gw.audit), name="audit-ingest",
                              daemon=True).start()
     ssl_ctx = None
-    if cfg.tls_cert and cfg.tls_key:
+    if cfg.tls_cert and cfg.tls_key and not native:  # with the front, TLS ends there
         ssl_ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
         ssl_ctx.load_cert_chain(cfg.tls_cert, cfg.tls_key)
     front = None
