@@ -24,6 +24,7 @@
 #include <random>
 
 #include "dfs_pb.h"
+#include "json.h"
 #include "sigv4.h"
 #include "trace.h"
 
@@ -315,6 +316,21 @@ bool S3Front::start(std::string* err) {
   socklen_t al = sizeof a;
   ::getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &al);
   cfg_.port = ntohs(a.sin_port);
+  for (auto& kv : cfg_.sts_keys) {
+    std::string k = kv.second;
+    k.resize(32, '\0');  // _key32: zero-padded / truncated to 32 bytes
+    sts_keys_[kv.first] = k;
+  }
+  if (!cfg_.iam_config.empty()) {
+    try {
+      iam_ = std::make_unique<s3policy::IamPolicy>(s3policy::IamPolicy::parse(cfg_.iam_config));
+    } catch (const std::exception& e) {
+      *err = std::string("IAM config: ") + e.what();
+      ::close(lfd_);
+      lfd_ = -1;
+      return false;
+    }
+  }
   if (!cfg_.tls_cert.empty()) {
     tls_ = TlsContext::server_http1(cfg_.tls_cert, cfg_.tls_key, err);
     if (!tls_) {
@@ -589,19 +605,27 @@ bool S3Front::handle(Conn* c, Req& r) {
     return proxy(c, r, nullptr, 0, "body");
   }
   std::string user = "anonymous";
+  Session sess;
   if (cfg_.auth_enabled) {
-    if (!verify_auth(r, &user)) return proxy(c, r, nullptr, 0, "auth");
+    if (!verify_auth(r, &user, &sess)) return proxy(c, r, nullptr, 0, "auth");
+    std::vector<std::string> keys;
+    for (auto& kv : q) keys.push_back(kv.first);
+    auto ar = s3policy::resolve_action_and_resource(r.method, r.raw_path, keys);
+    // an STS session's role policy (reference auth_middleware.rs: IAM evaluation for
+    // sessions only); a denial goes to the gateway, which answers 403 + audit
+    if (!sess.role_arn.empty() && iam_) {
+      if (!iam_->evaluate(ar.first, ar.second, sess.role_arn, sess.ctx)) return proxy(c, r, nullptr, 0, "iam-deny");
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.iam_native++;
+    }
     // bucket policy (reference auth_middleware.rs + bucket_policy.rs): a static-key caller has
-    // no role ARN, so only a Principal "*" Deny can apply; a denial is handed to the gateway,
-    // which answers it (403 + audit) exactly as for any other denied request
+    // no role ARN, so only a Principal "*" Deny can apply to it; a session is matched by its role
     bool known = false;
     auto pol = bucket_policy(bucket, &known);
     if (!known) return proxy(c, r, nullptr, 0, "bucket-policy");
     if (pol) {
-      std::vector<std::string> keys;
-      for (auto& kv : q) keys.push_back(kv.first);
-      auto ar = s3policy::resolve_action_and_resource(r.method, r.raw_path, keys);
-      if (pol->evaluate(nullptr, ar.first, ar.second) == s3policy::PolicyResult::ExplicitDeny)
+      if (pol->evaluate(sess.role_arn.empty() ? nullptr : &sess.role_arn, ar.first, ar.second) ==
+          s3policy::PolicyResult::ExplicitDeny)
         return proxy(c, r, nullptr, 0, "bucket-policy-deny");
       std::lock_guard<std::mutex> g(st_mu_);
       st_.policy_native++;
@@ -622,15 +646,44 @@ bool S3Front::handle(Conn* c, Req& r) {
   } else {
     ok = native_get(c, r, path, is_head);
   }
-  if (r.status > 0 && cfg_.auth_enabled) audit(c, r, user, r.status);
+  if (r.status > 0 && cfg_.auth_enabled) audit(c, r, user, r.status, sess.role_arn);
   return ok;
 }
 
 // ---------------------------------------------------------------- auth (static SigV4)
-int S3Front::verify_auth(Req& r, std::string* user) {
+// An STS session token (StsTokenManager, reference auth/sts.rs:60-98):
+// base64([kid u32 BE][nonce 12][AES-256-GCM(JSON StsSessionData)]). False when it does not
+// open, has expired or is malformed: the request goes to Python for the exact error.
+bool S3Front::open_session(const std::string& token, Session* out) {
+  std::string raw;
+  if (sts_keys_.empty() || !crypto::base64_decode(token, &raw) || raw.size() < 32) return false;
+  const uint32_t kid = (uint32_t(uint8_t(raw[0])) << 24) | (uint32_t(uint8_t(raw[1])) << 16) |
+                       (uint32_t(uint8_t(raw[2])) << 8) | uint32_t(uint8_t(raw[3]));
+  auto k = sts_keys_.find(kid);
+  if (k == sts_keys_.end()) return false;
+  try {
+    Json j = Json::parse(crypto::aes256gcm_decrypt(k->second, raw.substr(4, 12), raw.substr(16), ""));
+    out->role_arn = j["role_arn"].str();
+    out->secret = j["temp_secret_key"].str();
+    if (j["expiration"].as_int() < static_cast<int64_t>(now_s()) || out->role_arn.empty() || out->secret.empty())
+      return false;
+    const Json& cl = j["claims"];  // Claims.to_policy_context()
+    out->ctx.principal_id = cl["sub"].str();
+    out->ctx.groups.clear();
+    if (cl["groups"].is_array())
+      for (auto& g : cl["groups"].items()) out->ctx.groups.push_back(g.str());
+    out->ctx.claims = {{"sub", cl["sub"].str()}, {"iss", cl["iss"].str()}};
+    return true;
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
   const std::string* auth = r.get("authorization");
   if (!auth || auth->compare(0, 16, "AWS4-HMAC-SHA256") != 0) return 0;
-  if (r.get("x-amz-security-token")) return 0;  // STS sessions: IAM policy evaluation in Python
+  const std::string* token = r.get("x-amz-security-token");
+  if (token && !open_session(*token, sess)) return 0;
   std::vector<std::string> parts;
   size_t i = 0;
   while (i <= auth->size()) {
@@ -671,18 +724,23 @@ int S3Front::verify_auth(Req& r, std::string* user) {
   if (skew / 60.0 > 15.0) return 0;
   const std::string &ak = cp[0], &date = cp[1], &region = cp[2], &service = cp[3];
   if (region != cfg_.region || service != "s3") return 0;
-  if (cfg_.access_key.empty() || ak != cfg_.access_key) return 0;
   std::string skey;
-  {
-    std::lock_guard<std::mutex> g(key_mu_);
-    auto it = key_cache_.find(date);
-    if (it != key_cache_.end()) skey = it->second;
-  }
-  if (skey.empty()) {
-    skey = sigv4::signing_key(cfg_.secret_key, date, region, service);
-    std::lock_guard<std::mutex> g(key_mu_);
-    if (key_cache_.size() > 8) key_cache_.clear();
-    key_cache_[date] = skey;
+  if (token) {
+    // a session's own secret: its signing key is never shared with the static key's slot
+    skey = sigv4::signing_key(sess->secret, date, region, service);
+  } else {
+    if (cfg_.access_key.empty() || ak != cfg_.access_key) return 0;
+    {
+      std::lock_guard<std::mutex> g(key_mu_);
+      auto it = key_cache_.find(date);
+      if (it != key_cache_.end()) skey = it->second;
+    }
+    if (skey.empty()) {
+      skey = sigv4::signing_key(cfg_.secret_key, date, region, service);
+      std::lock_guard<std::mutex> g(key_mu_);
+      if (key_cache_.size() > 8) key_cache_.clear();
+      key_cache_[date] = skey;
+    }
   }
   sigv4::Request sr;
   sr.method = r.method;
@@ -777,7 +835,7 @@ std::shared_ptr<const s3policy::BucketPolicy> S3Front::bucket_policy(const std::
   return pol;
 }
 
-void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int status) {
+void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int status, const std::string& role_arn) {
   if (audit_fd_ < 0) return;
   std::string path = r.raw_path;
   std::vector<std::string> segs;
@@ -798,7 +856,8 @@ void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int st
   std::string rec = "{\"timestamp\":" + json_str(ts) + ",\"timestamp_ms\":" + std::to_string(ms) +
                     ",\"request_id\":" + json_str(r.rid.empty() ? uuid4() : r.rid) +
                     ",\"remote_ip\":" + json_str(c->ip) + ",\"user_id\":" + json_str(user) +
-                    ",\"role_arn\":null,\"action\":" + json_str(action) + ",\"resource\":" + json_str(resource) +
+                    ",\"role_arn\":" + (role_arn.empty() ? std::string("null") : json_str(role_arn)) +
+                    ",\"action\":" + json_str(action) + ",\"resource\":" + json_str(resource) +
                     ",\"status_code\":" + std::to_string(status) + ",\"error_code\":null,\"user_agent\":" +
                     (ua ? json_str(*ua) : std::string("null")) +
                     ",\"duration_ms\":" + std::to_string(static_cast<int64_t>((t - r.started) * 1000)) +

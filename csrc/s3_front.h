@@ -62,6 +62,10 @@ struct S3FrontConfig {
   std::string policy_epoch_path;
   // TLS terminated by the front itself (reference main.rs:263-274 binds rustls): PEM files
   std::string tls_cert, tls_key;
+  // STS sessions verified here: the token keys by KID (StsTokenManager) and the IAM role
+  // configuration (IAM_CONFIG_PATH document) that decides what a session may do
+  std::map<uint32_t, std::string> sts_keys;
+  std::string iam_config;
 };
 
 struct S3FrontStats {
@@ -74,7 +78,7 @@ struct S3FrontStats {
   // native GET/Range GET phases, summed microseconds: metadata stat, block read into the
   // slot, response send (where a GET's latency goes)
   uint64_t get_stat_us = 0, get_read_us = 0, get_send_us = 0, get_timed = 0;
-  uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0;
+  uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0, iam_native = 0;
 };
 
 class S3Front {
@@ -101,12 +105,17 @@ class S3Front {
   bool native_mpu_get(Conn* c, Req& r, const std::string& path, const std::string& marker_meta);
   bool sse_get(Conn* c, Req& r, const std::string& meta, uint64_t size, const std::string& hdrs,
                const std::string& dek_b64);
-  int verify_auth(Req& r, std::string* user);  // 1 ok, 0 hand over
+  struct Session {  // an authenticated STS session (empty role_arn: the static key)
+    std::string role_arn, secret;
+    s3policy::Context ctx;
+  };
+  bool open_session(const std::string& token, Session* out);
+  int verify_auth(Req& r, std::string* user, Session* sess);  // 1 ok, 0 hand over
   // The bucket's policy: *known = false when it could not be read (the request is handed
   // over); a null pointer when the bucket has none (or an unparsable one, which the gateway
   // ignores too).
   std::shared_ptr<const s3policy::BucketPolicy> bucket_policy(const std::string& bucket, bool* known);
-  void audit(const Conn* c, const Req& r, const std::string& user, int status);
+  void audit(const Conn* c, const Req& r, const std::string& user, int status, const std::string& role_arn = "");
   void count(const Req& r, int status);
   int backend_conn();
   void backend_done(int fd, bool reuse);
@@ -116,6 +125,8 @@ class S3Front {
   S3FrontConfig cfg_;
   FastClient* fc_;
   std::shared_ptr<TlsContext> tls_;
+  std::map<uint32_t, std::string> sts_keys_;
+  std::unique_ptr<s3policy::IamPolicy> iam_;
   int lfd_ = -1, epfd_ = -1, evfd_ = -1, audit_fd_ = -1;
   std::atomic<bool> stop_{false};
   std::thread epoller_;

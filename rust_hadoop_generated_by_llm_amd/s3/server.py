@@ -1241,6 +1241,16 @@ def native_front_wanted(cfg: S3Config) -> bool:
     return True
 
 
+def native_front_auth(gw: S3Gateway) -> dict:
+    """What the native front needs to verify STS-session requests itself: the token keys by
+    KID and the IAM role document (only when the gateway loaded it)."""
+    out: dict = {"sts_keys": dict(gw.sts.keys) if gw.sts is not None else {}, "iam_config": ""}
+    if gw.iam is not None and gw.cfg.iam_config_path:
+        with open(gw.cfg.iam_config_path) as f:
+            out["iam_config"] = f.read()
+    return out
+
+
 def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_socket: str,
                        policy_epoch: str = ""):
     """Worker 0 runs the native front on the public port; it hands what it does not serve to
@@ -1260,7 +1270,8 @@ def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_
                         policy_epoch=policy_epoch or (gw.policy_epoch.path or ""),
                         tls_cert=cfg.tls_cert or "" if (cfg.tls_cert and cfg.tls_key) else "",
                         tls_key=cfg.tls_key or "" if (cfg.tls_cert and cfg.tls_key) else "",
-                        sse_kek=gw.sse.kek if gw.sse is not None else b"")
+                        sse_kek=gw.sse.kek if gw.sse is not None else b"",
+                        **native_front_auth(gw))
     ok, err = front.start()
     if not ok:
         raise RuntimeError(f"native S3 front end failed to start: {err}")
