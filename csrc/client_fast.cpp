@@ -454,6 +454,42 @@ FastClient::Status FastClient::write_slot(const std::string& path, int64_t slot,
   return Ok;
 }
 
+FastClient::Status FastClient::list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
+                                    const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  RequestScope rs(rid);
+  TraceRange tr("dfs.client.list");
+  std::vector<std::string> socks;
+  {
+    std::lock_guard<std::mutex> g(route_mu_);
+    if (have_map_) {
+      for (const auto& shard : map_.shards()) {
+        const auto* peers = map_.peers(shard);
+        if (!peers || peers->empty()) return NotHandled;
+        socks.push_back(local_rpc_name(peers->front()));
+      }
+    } else if (!masters_.empty()) {
+      socks.push_back(local_rpc_name(masters_.front()));
+    }
+  }
+  if (socks.empty()) return NotHandled;
+  pb::ListFilesRequest req;
+  req.path = prefix;
+  req.with_metadata = true;
+  const std::string body = req.str();
+  out->clear();
+  for (const auto& sock : socks) {
+    int code = 0;
+    std::string raw;
+    if (!call(sock, "/dfs.MasterService/ListFiles", rid, body, &code, &raw) || code != 0) return NotHandled;
+    pb::ListFilesResponse resp;
+    if (!resp.decode(raw) || resp.metadata.size() != resp.files.size()) return NotHandled;
+    for (size_t i = 0; i < resp.files.size(); ++i) out->emplace_back(resp.files[i], std::move(resp.metadata[i]));
+  }
+  std::sort(out->begin(), out->end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  return Ok;
+}
+
 FastClient::Status FastClient::stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg,
                                     const std::string& rid_in) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;

@@ -102,6 +102,11 @@ class FastClient {
   Status read_known(const std::string& meta_pb, int64_t* slot, uint64_t* n, std::string* msg, Times* t,
                     const std::string& rid, uint64_t offset, uint64_t length);
   Status remove(const std::string& path, std::string* msg, const std::string& rid);
+  // ListFiles{with_metadata} under `prefix` on every shard (one call per shard, its master's
+  // same-host socket), merged: (path, serialized FileMetadata). NotHandled if a shard's master
+  // is not local or does not return metadata.
+  Status list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
+              const std::string& rid);
 
   // Erasure-coded file (reference mod.rs:308-412): the data is striped into k shards in a
   // slot, the m parity shards are computed by the co-located chunkserver's GPU (fast-path op

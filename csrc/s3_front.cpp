@@ -1,5 +1,8 @@
 // Native S3 front end; design notes in s3_front.h.
 #include "s3_front.h"
+#include <unordered_set>
+#include <unordered_map>
+#include <set>
 #include "crypto.h"
 
 #include <arpa/inet.h>
@@ -261,6 +264,84 @@ bool simple_query(const std::string& q, std::map<std::string, std::string>* out)
   return true;
 }
 
+int hexval(char ch) {
+  if (ch >= '0' && ch <= '9') return ch - '0';
+  if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+  if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+  return -1;
+}
+
+// parse_qsl(raw, keep_blank_values=True) of the Python gateway: '+' is a space, %XX a byte,
+// a malformed escape stays as written. False on bytes that are not UTF-8 (Python would
+// substitute U+FFFD; the request goes there).
+bool decode_query(const std::string& q, std::map<std::string, std::string>* out) {
+  auto dec = [](const std::string& v, std::string* o) {
+    o->clear();
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (v[i] == '+') {
+        o->push_back(' ');
+      } else if (v[i] == '%' && i + 2 < v.size() && hexval(v[i + 1]) >= 0 && hexval(v[i + 2]) >= 0) {
+        o->push_back(static_cast<char>(hexval(v[i + 1]) * 16 + hexval(v[i + 2])));
+        i += 2;
+      } else {
+        o->push_back(v[i]);
+      }
+    }
+    // strict UTF-8
+    for (size_t i = 0; i < o->size();) {
+      unsigned char c0 = static_cast<unsigned char>((*o)[i]);
+      int n = c0 < 0x80 ? 1 : (c0 >> 5) == 6 ? 2 : (c0 >> 4) == 14 ? 3 : (c0 >> 3) == 30 ? 4 : 0;
+      if (!n || i + n > o->size()) return false;
+      for (int k = 1; k < n; ++k)
+        if ((static_cast<unsigned char>((*o)[i + k]) >> 6) != 2) return false;
+      i += static_cast<size_t>(n);
+    }
+    return true;
+  };
+  size_t i = 0;
+  while (!q.empty() && i <= q.size()) {
+    size_t amp = q.find('&', i);
+    std::string kv = q.substr(i, amp == std::string::npos ? std::string::npos : amp - i);
+    if (!kv.empty()) {
+      size_t eq = kv.find('=');
+      std::string k, v;
+      if (!dec(kv.substr(0, eq), &k) || !dec(eq == std::string::npos ? "" : kv.substr(eq + 1), &v)) return false;
+      (*out)[k] = v;
+    }
+    if (amp == std::string::npos) break;
+    i = amp + 1;
+  }
+  return true;
+}
+
+// xml.sax.saxutils.escape
+std::string xml_escape(const std::string& v) {
+  std::string o;
+  o.reserve(v.size());
+  for (char ch : v) {
+    if (ch == '&') o += "&amp;";
+    else if (ch == '<') o += "&lt;";
+    else if (ch == '>') o += "&gt;";
+    else o.push_back(ch);
+  }
+  return o;
+}
+
+std::string xel(const char* tag, const std::string& v) {
+  return std::string("<") + tag + ">" + xml_escape(v) + "</" + tag + ">";
+}
+
+// _iso_ms: seconds precision, ".000Z"
+std::string iso_ms(uint64_t ms) {
+  if (!ms) return "2025-01-01T00:00:00.000Z";
+  time_t t = static_cast<time_t>(ms / 1000);
+  tm g{};
+  gmtime_r(&t, &g);
+  char b[40];
+  std::strftime(b, sizeof b, "%Y-%m-%dT%H:%M:%S.000Z", &g);
+  return b;
+}
+
 }  // namespace
 
 struct S3Front::Conn {
@@ -280,6 +361,7 @@ struct S3Front::Req {
   int64_t content_length = 0;
   double started = 0;
   std::string rid;
+  std::string action;  // s3:<Action> once resolved for authorization (audit records)
   int status = 0;
   const std::string* get(const char* lname) const {
     for (auto& h : headers)
@@ -579,9 +661,18 @@ bool S3Front::handle(Conn* c, Req& r) {
   const bool plain_path = r.raw_path.size() > 1 && r.raw_path[0] == '/' &&
                           r.raw_path.find('%') == std::string::npos;
   std::map<std::string, std::string> q;
-  if (!fc_ || !plain_path || !simple_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
+  if (!fc_ || !plain_path) return proxy(c, r, nullptr, 0, "route");
   std::string p = r.raw_path.substr(1);
   size_t slash = p.find('/');
+  if (r.method == "GET" && slash != 0 && (slash == std::string::npos || slash + 1 == p.size())) {
+    // GET /bucket[/]: ListObjects (v1, or v2 with list-type=2) unless it is a sub-resource
+    const std::string bucket = p.substr(0, slash);
+    if (bucket.empty() || !decode_query(r.raw_query, &q) || q.count("location") || q.count("policy") ||
+        r.content_length > 0 || r.chunked)
+      return proxy(c, r, nullptr, 0, "route");
+    return native_list(c, r, bucket, q);
+  }
+  if (!simple_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
   if (slash == std::string::npos || slash == 0 || slash + 1 >= p.size()) return proxy(c, r, nullptr, 0, "route");
   const std::string bucket = p.substr(0, slash), key = p.substr(slash + 1);
   if (reserved_key(key)) return proxy(c, r, nullptr, 0, "route");
@@ -604,33 +695,9 @@ bool S3Front::handle(Conn* c, Req& r) {
   } else if (r.content_length > 0 || r.chunked) {
     return proxy(c, r, nullptr, 0, "body");
   }
-  std::string user = "anonymous";
+  std::string user = "anonymous", why;
   Session sess;
-  if (cfg_.auth_enabled) {
-    if (!verify_auth(r, &user, &sess)) return proxy(c, r, nullptr, 0, "auth");
-    std::vector<std::string> keys;
-    for (auto& kv : q) keys.push_back(kv.first);
-    auto ar = s3policy::resolve_action_and_resource(r.method, r.raw_path, keys);
-    // an STS session's role policy (reference auth_middleware.rs: IAM evaluation for
-    // sessions only); a denial goes to the gateway, which answers 403 + audit
-    if (!sess.role_arn.empty() && iam_) {
-      if (!iam_->evaluate(ar.first, ar.second, sess.role_arn, sess.ctx)) return proxy(c, r, nullptr, 0, "iam-deny");
-      std::lock_guard<std::mutex> g(st_mu_);
-      st_.iam_native++;
-    }
-    // bucket policy (reference auth_middleware.rs + bucket_policy.rs): a static-key caller has
-    // no role ARN, so only a Principal "*" Deny can apply to it; a session is matched by its role
-    bool known = false;
-    auto pol = bucket_policy(bucket, &known);
-    if (!known) return proxy(c, r, nullptr, 0, "bucket-policy");
-    if (pol) {
-      if (pol->evaluate(sess.role_arn.empty() ? nullptr : &sess.role_arn, ar.first, ar.second) ==
-          s3policy::PolicyResult::ExplicitDeny)
-        return proxy(c, r, nullptr, 0, "bucket-policy-deny");
-      std::lock_guard<std::mutex> g(st_mu_);
-      st_.policy_native++;
-    }
-  }
+  if (!authorize(r, bucket, q, &user, &sess, &why)) return proxy(c, r, nullptr, 0, why);
   std::string path = "/" + bucket + "/" + key;
   bool ok;
   if (is_put && part) {
@@ -647,6 +714,177 @@ bool S3Front::handle(Conn* c, Req& r) {
     ok = native_get(c, r, path, is_head);
   }
   if (r.status > 0 && cfg_.auth_enabled) audit(c, r, user, r.status, sess.role_arn);
+  return ok;
+}
+
+// Signature, session role policy and bucket policy of an authenticated gateway; false with
+// the hand-over reason when Python must answer (a denial, or anything not verified here).
+bool S3Front::authorize(Req& r, const std::string& bucket, const std::map<std::string, std::string>& q,
+                        std::string* user, Session* sess_out, std::string* why) {
+  Session& sess = *sess_out;
+  if (cfg_.auth_enabled) {
+    if (!verify_auth(r, user, &sess)) return (*why = "auth", false);
+    std::vector<std::string> keys;
+    for (auto& kv : q) keys.push_back(kv.first);
+    auto ar = s3policy::resolve_action_and_resource(r.method, r.raw_path, keys);
+    r.action = ar.first;
+    // an STS session's role policy (reference auth_middleware.rs: IAM evaluation for
+    // sessions only); a denial goes to the gateway, which answers 403 + audit
+    if (!sess.role_arn.empty() && iam_) {
+      if (!iam_->evaluate(ar.first, ar.second, sess.role_arn, sess.ctx)) return (*why = "iam-deny", false);
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.iam_native++;
+    }
+    // bucket policy (reference auth_middleware.rs + bucket_policy.rs): a static-key caller has
+    // no role ARN, so only a Principal "*" Deny can apply to it; a session is matched by its role
+    bool known = false;
+    auto pol = bucket_policy(bucket, &known);
+    if (!known) return (*why = "bucket-policy", false);
+    if (pol) {
+      if (pol->evaluate(sess.role_arn.empty() ? nullptr : &sess.role_arn, ar.first, ar.second) ==
+          s3policy::PolicyResult::ExplicitDeny)
+        return (*why = "bucket-policy-deny", false);
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.policy_native++;
+    }
+  }
+  return true;
+}
+
+// ListObjects / ListObjectsV2 (reference handlers.rs:1536-1697, s3/server.py list_objects):
+// one ListFiles{with_metadata} per shard over the masters' local sockets, the keys sorted
+// and paged (prefix, delimiter, marker / continuation-token / start-after, max-keys) and
+// the reference XML written here. Buckets that are missing or empty, and objects whose
+// headers live in a sidecar file, are Python's.
+bool S3Front::native_list(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q) {
+  TraceRange tr("dfs.s3.list");
+  const bool v2 = q.count("list-type") && q["list-type"] == "2";
+  const std::string prefix = q.count("prefix") ? q["prefix"] : "";
+  const std::string delim = q.count("delimiter") ? q["delimiter"] : "";
+  int64_t max_keys = 1000;
+  if (q.count("max-keys")) {
+    const std::string& mk = q["max-keys"];
+    if (mk.empty() || mk.size() > 9 || !all_digits(mk)) return proxy(c, r, nullptr, 0, "list-args");
+    max_keys = std::min<int64_t>(std::stoll(mk), 1000);
+  }
+  auto opt = [&](const char* k) { return q.count(k) ? q[k] : std::string(); };
+  const std::string marker = v2 ? (!opt("continuation-token").empty() ? opt("continuation-token") : opt("start-after"))
+                                : opt("marker");
+  std::string user = "anonymous", why;
+  Session sess;
+  if (!authorize(r, bucket, q, &user, &sess, &why)) return proxy(c, r, nullptr, 0, why);
+  const std::string bp = "/" + bucket + "/";
+  std::vector<std::pair<std::string, pb::FileMetadata>> files;
+  if (fc_->list(bp, &files, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "list");
+  if (files.empty()) return proxy(c, r, nullptr, 0, "list-empty");  // NoSuchBucket, or none at all
+  static const char* kHiddenSfx[] = {".s3keep", ".s3_mpu_completed", ".meta", ".s3_bucket_policy"};
+  auto hidden = [](const std::string& f) {
+    for (const char* h : kHiddenSfx)
+      if (ends_with(f, h)) return true;
+    return false;
+  };
+  std::unordered_set<std::string> fileset;
+  std::unordered_map<std::string, const pb::FileMetadata*> by_path;
+  std::set<std::string> mpu_dirs;
+  for (auto& f : files) {
+    fileset.insert(f.first);
+    by_path[f.first] = &f.second;
+    if (ends_with(f.first, "/.s3_mpu_completed")) mpu_dirs.insert(f.first.substr(0, f.first.size() - 18));
+  }
+  std::map<std::string, const pb::FileMetadata*> entries;  // key -> metadata (nullptr: MPU object)
+  for (auto& f : files) {
+    if (f.first.compare(0, bp.size(), bp) != 0 || hidden(f.first)) continue;
+    if (mpu_dirs.count(f.first.substr(0, f.first.rfind('/')))) continue;
+    entries[f.first.substr(bp.size())] = &f.second;
+  }
+  for (auto& d : mpu_dirs)
+    if (d.compare(0, bp.size(), bp) == 0) entries[d.substr(bp.size())] = nullptr;
+  std::vector<std::string> objects, cps;
+  std::set<std::string> seen;
+  bool truncated = false;
+  std::string next_marker;
+  int64_t nkeys = 0;
+  for (auto it = entries.upper_bound(marker); it != entries.end(); ++it) {
+    const std::string& k = it->first;
+    if (k.compare(0, prefix.size(), prefix) != 0) continue;
+    if (!delim.empty()) {
+      size_t i = k.find(delim, prefix.size());
+      if (i != std::string::npos) {
+        std::string cp = k.substr(0, i + delim.size());
+        if (seen.count(cp)) continue;
+        if (nkeys >= max_keys) {
+          truncated = true;
+          break;
+        }
+        seen.insert(cp);
+        cps.push_back(cp);
+        ++nkeys;
+        next_marker = cp;
+        continue;
+      }
+    }
+    if (nkeys >= max_keys) {
+      truncated = true;
+      break;
+    }
+    objects.push_back(k);
+    ++nkeys;
+    next_marker = k;
+  }
+  std::string contents;
+  for (auto& k : objects) {
+    const pb::FileMetadata* info = entries[k];
+    std::string etag = "\"d41d8cd98f00b204e9800998ecf8427e\"", lm = "2025-01-01T00:00:00.000Z";
+    uint64_t size = 0;
+    if (info == nullptr) {  // a completed multipart object: its marker's recorded headers
+      auto mk = by_path.find(bp + k + "/.s3_mpu_completed");
+      if (mk == by_path.end() || mk->second->attributes.empty()) return proxy(c, r, nullptr, 0, "list-sidecar");
+      const auto& at = mk->second->attributes;
+      auto e = at.find("ETag");
+      etag = e != at.end() ? e->second : "\"000-MPU\"";
+      auto sz = at.find("x-dfs-mpu-size");
+      if (sz != at.end() && !sz->second.empty() && all_digits(sz->second)) size = std::stoull(sz->second);
+    } else {
+      size = info->size;
+      if (!info->etag_md5.empty()) etag = "\"" + info->etag_md5 + "\"";
+      lm = iso_ms(info->created_at_ms);
+      if (!info->attributes.empty()) {
+        auto e = info->attributes.find("ETag");
+        if (e != info->attributes.end()) etag = e->second;
+      } else if (fileset.count(bp + k + ".meta")) {
+        return proxy(c, r, nullptr, 0, "list-sidecar");
+      }
+    }
+    contents += "<Contents>" + xel("Key", k) + xel("LastModified", lm) + xel("ETag", etag) +
+                xel("Size", std::to_string(size)) + xel("StorageClass", "STANDARD") +
+                "<Owner><ID>dfs</ID><DisplayName>dfs</DisplayName></Owner></Contents>";
+  }
+  std::string prefixes;
+  for (auto& cp : cps) prefixes += "<CommonPrefixes>" + xel("Prefix", cp) + "</CommonPrefixes>";
+  const std::string trunc = truncated ? "true" : "false";
+  std::string x = "<ListBucketResult>" + xel("Name", bucket) + xel("Prefix", prefix);
+  if (v2) {
+    x += xel("MaxKeys", std::to_string(max_keys)) + xel("IsTruncated", trunc) + contents + prefixes +
+         xel("KeyCount", std::to_string(nkeys));
+    if (q.count("continuation-token")) x += xel("ContinuationToken", q["continuation-token"]);
+    if (truncated) x += xel("NextContinuationToken", next_marker);
+    if (q.count("start-after")) x += xel("StartAfter", q["start-after"]);
+  } else {
+    x += xel("Marker", opt("marker"));
+    if (truncated && !delim.empty()) x += xel("NextMarker", next_marker);
+    x += xel("MaxKeys", std::to_string(max_keys)) + xel("IsTruncated", trunc) + contents + prefixes;
+  }
+  x += "</ListBucketResult>";
+  std::string h = "HTTP/1.1 200 OK\r\nContent-Type: application/xml\r\nContent-Length: " + std::to_string(x.size()) +
+                  "\r\n" + (r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+  r.status = 200;
+  count(r, 200);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.lists++;
+  }
+  const bool ok = send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(x.data()), x.size());
+  if (cfg_.auth_enabled) audit(c, r, user, 200, sess.role_arn);
   return ok;
 }
 
@@ -848,7 +1086,8 @@ void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int st
   }
   std::string resource = "arn:dfs:s3:::";
   for (size_t i = 0; i < segs.size(); ++i) resource += (i ? "/" : "") + segs[i];
-  std::string action = r.method == "GET" ? "s3:GetObject" : r.method == "HEAD" ? "s3:HeadObject" : "s3:PutObject";
+  std::string action = !r.action.empty() ? r.action
+                       : r.method == "GET" ? "s3:GetObject" : r.method == "HEAD" ? "s3:HeadObject" : "s3:PutObject";
   const double t = now_s();
   int64_t ms;
   std::string ts = iso_now(t, &ms);

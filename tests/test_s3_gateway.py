@@ -320,6 +320,32 @@ def test_list_objects_v2_pagination_and_v1(gw):
     root = X.parse(requests.get(f"{u}/lst?list-type=2&start-after=key-23&prefix=key-").content)
     assert [c.find("Key").text for c in root.findall("Contents")] == ["key-24"]
     assert requests.get(f"{u}/nosuchbkt?list-type=2").status_code == 404
+    if gw.front is not None:
+        # the native listing is byte-for-byte the Python gateway's (asked directly on its socket)
+        l0 = gw.front.stats()["lists"]
+        requests.put(f"{u}/lst/a&b<c>", data=b"esc")
+        for q in ("list-type=2&max-keys=10&prefix=key-", "list-type=2&delimiter=%2F", "prefix=dir%2F&delimiter=/",
+                  "list-type=2&max-keys=3&delimiter=/&prefix=", "marker=key-20", "max-keys=0",
+                  "list-type=2&continuation-token=key-05&max-keys=4", "list-type=2&start-after=dir&fetch-owner=true",
+                  "prefix=a%26b"):
+            native = requests.get(f"{u}/lst?{q}")
+            assert native.status_code == 200, q
+            assert native.content == backend_get(gw, f"/lst?{q}"), q
+        assert gw.front.stats()["lists"] - l0 == 9
+
+
+def backend_get(g, target: str) -> bytes:
+    """GET straight from the Python gateway behind the native front (its private socket)."""
+    sk = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    sk.connect(g.backend)
+    sk.sendall(f"GET {target} HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n".encode())
+    data = b""
+    while chunk := sk.recv(65536):
+        data += chunk
+    sk.close()
+    head, _, body = data.partition(b"\r\n\r\n")
+    assert head.startswith(b"HTTP/1.1 200"), head
+    return body
 
 
 def test_copy_and_multi_delete(gw):
