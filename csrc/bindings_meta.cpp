@@ -908,6 +908,7 @@ void bind_meta(py::module_& m) {
         d["sse_gets"] = s.sse_gets;
         d["iam_native"] = s.iam_native;
         d["lists"] = s.lists;
+        d["mpu_completes"] = s.mpu_completes;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;
         return d;

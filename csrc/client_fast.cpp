@@ -538,6 +538,31 @@ FastClient::Status FastClient::remove(const std::string& path, std::string* msg,
   return Ok;
 }
 
+FastClient::Status FastClient::rename(const std::string& src, const std::string& dst, std::string* msg,
+                                      const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  std::string sock = master_socket(src);
+  if (sock.empty()) return NotHandled;
+  pb::RenameRequest req;
+  req.source_path = src;
+  req.dest_path = dst;
+  int code;
+  std::string raw;
+  if (!call(sock, "/dfs.MasterService/Rename", rid, req.str(), &code, &raw)) return NotHandled;
+  if (code != 0) {
+    *msg = raw;
+    return NotHandled;  // redirect / not leader / safe mode: the caller's slower path retries
+  }
+  pb::RenameResponse r;
+  if (!r.decode(raw)) return NotHandled;
+  if (!r.success) {
+    if (r.error_message == "Not Leader") return NotHandled;
+    *msg = r.error_message;
+    return Failed;
+  }
+  return Ok;
+}
+
 FastClient::Status FastClient::read(const std::string& path, int64_t* slot, uint64_t* n, std::string* msg,
                                     Times* t, const std::string& rid_in, uint64_t offset, uint64_t length) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;

@@ -102,6 +102,8 @@ class FastClient {
   Status read_known(const std::string& meta_pb, int64_t* slot, uint64_t* n, std::string* msg, Times* t,
                     const std::string& rid, uint64_t offset, uint64_t length);
   Status remove(const std::string& path, std::string* msg, const std::string& rid);
+  // Rename on the source's shard (a cross-shard destination runs the master's 2PC).
+  Status rename(const std::string& src, const std::string& dst, std::string* msg, const std::string& rid);
   // ListFiles{with_metadata} under `prefix` on every shard (one call per shard, its master's
   // same-host socket), merged: (path, serialized FileMetadata). NotHandled if a shard's master
   // is not local or does not return metadata.

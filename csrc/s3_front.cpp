@@ -677,6 +677,11 @@ bool S3Front::handle(Conn* c, Req& r) {
   const std::string bucket = p.substr(0, slash), key = p.substr(slash + 1);
   if (reserved_key(key)) return proxy(c, r, nullptr, 0, "route");
   q.erase("x-id");  // SDK operation tag, no meaning to S3 itself
+  if (r.method == "POST" && q.size() == 1 && q.count("uploadId") && !r.chunked && r.content_length <= (1 << 20) &&
+      !cfg_.metadata_sidecar) {
+    const std::string* sha = r.get("x-amz-content-sha256");
+    if (!(sha && sha->compare(0, 10, "STREAMING-") == 0)) return native_complete(c, r, bucket, key, q);
+  }
   const bool part = q.size() == 2 && q.count("partNumber") && q.count("uploadId");
   if (!q.empty() && !part) return proxy(c, r, nullptr, 0, "query");
   const bool is_put = r.method == "PUT", is_get = r.method == "GET", is_head = r.method == "HEAD";
@@ -1320,6 +1325,250 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
     st_.get_send_us += us(t3 - t2);
     st_.get_timed++;
   }
+  return ok;
+}
+
+namespace {
+
+// ET.fromstring + _children/_text of s3/xml.py for a CompleteMultipartUpload body, namespace
+// agnostic: the (PartNumber, ETag) of every <Part> child of the root. False for anything
+// this small scanner does not model (DTDs, CDATA, malformed XML): Python parses those.
+bool parse_complete_body(const std::string& b, std::vector<std::pair<int64_t, std::string>>* parts) {
+  parts->clear();
+  size_t i = 0;
+  auto local = [](const std::string& t) {
+    size_t c = t.find(':');
+    return c == std::string::npos ? t : t.substr(c + 1);
+  };
+  auto unescape = [](const std::string& v, std::string* o) {
+    o->clear();
+    for (size_t k = 0; k < v.size(); ++k) {
+      if (v[k] != '&') {
+        o->push_back(v[k]);
+        continue;
+      }
+      size_t e = v.find(';', k);
+      if (e == std::string::npos) return false;
+      const std::string ent = v.substr(k + 1, e - k - 1);
+      if (ent == "quot") o->push_back('"');
+      else if (ent == "amp") o->push_back('&');
+      else if (ent == "lt") o->push_back('<');
+      else if (ent == "gt") o->push_back('>');
+      else if (ent == "apos") o->push_back('\'');
+      else return false;
+      k = e;
+    }
+    return true;
+  };
+  std::vector<std::string> stack;
+  std::string text, pn, et;
+  bool have_pn = false, have_et = false, in_part = false, root_done = false;
+  while (i < b.size()) {
+    if (b[i] != '<') {
+      text.push_back(b[i++]);
+      continue;
+    }
+    size_t e = b.find('>', i);
+    if (e == std::string::npos) return false;
+    std::string tag = b.substr(i + 1, e - i - 1);
+    i = e + 1;
+    if (tag.empty() || tag[0] == '!') return false;     // comments, CDATA, DTD
+    if (tag[0] == '?') {
+      if (!stack.empty()) return false;
+      continue;
+    }
+    const bool closing = tag[0] == '/';
+    const bool empty_el = !closing && tag.back() == '/';
+    std::string name = closing ? tag.substr(1) : (empty_el ? tag.substr(0, tag.size() - 1) : tag);
+    name = name.substr(0, name.find_first_of(" \t\r\n"));
+    if (name.empty()) return false;
+    if (closing) {
+      if (stack.empty() || stack.back() != name) return false;
+      const std::string ln = local(name);
+      if (stack.size() == 3 && in_part) {
+        std::string v;
+        if (!unescape(text, &v)) return false;
+        if (ln == "PartNumber" && !have_pn) pn = v, have_pn = true;
+        if (ln == "ETag" && !have_et) et = v, have_et = true;
+      }
+      if (stack.size() == 2 && in_part) {
+        // int(_text(p, "PartNumber", "0")), _text(p, "ETag", "").strip()
+        std::string num = have_pn ? pn : "0";
+        auto trimws = [](std::string v) {
+          size_t a = v.find_first_not_of(" \t\r\n"), z = v.find_last_not_of(" \t\r\n");
+          return a == std::string::npos ? std::string() : v.substr(a, z - a + 1);
+        };
+        num = trimws(num);
+        size_t d = num.size() && (num[0] == '+' || num[0] == '-') ? 1 : 0;
+        if (num.size() == d || num.size() > 12 || num.find_first_not_of("0123456789", d) != std::string::npos)
+          return false;
+        parts->emplace_back(std::stoll(num), trimws(have_et ? et : ""));
+        in_part = false;
+      }
+      stack.pop_back();
+      if (stack.empty()) root_done = true;
+      text.clear();
+      continue;
+    }
+    if (root_done) return false;  // a second root element
+    stack.push_back(name);
+    text.clear();
+    if (stack.size() == 2 && local(name) == "Part") {
+      in_part = true;
+      have_pn = have_et = false;
+    }
+    if (empty_el) {
+      if (stack.size() == 3 && in_part) {
+        const std::string ln = local(name);
+        if (ln == "PartNumber" && !have_pn) pn.clear(), have_pn = true;
+        if (ln == "ETag" && !have_et) et.clear(), have_et = true;
+      }
+      if (stack.size() == 2 && in_part) {
+        parts->emplace_back(0, "");  // <Part/>: PartNumber "0" -> rejected below as invalid part
+        in_part = false;
+      }
+      stack.pop_back();
+      if (stack.empty()) root_done = true;
+    }
+  }
+  return stack.empty() && root_done;
+}
+
+}  // namespace
+
+// CompleteMultipartUpload (reference handlers.rs:322-432, s3/server.py complete_mpu): the
+// parts listed with their metadata in one ListFiles, validated against the request, the
+// object's ETag md5(concat(md5s))-N, the completion marker written with the layout, and the
+// parts renamed under the object in parallel (each rename one Raft entry, or the master's
+// 2PC when the object's shard differs). Errors before anything changed are Python's.
+bool S3Front::native_complete(Conn* c, Req& r, const std::string& bucket, const std::string& key,
+                              std::map<std::string, std::string>& q) {
+  TraceRange tr("dfs.s3.mpu_complete");
+  const std::string upload_id = q["uploadId"];
+  std::string body(static_cast<size_t>(r.content_length), '\0');
+  if (r.expect_continue && !send_all(c->io(), "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+  if (!read_body(c, reinterpret_cast<uint8_t*>(&body[0]), body.size())) return false;
+  r.expect_continue = false;  // the body is read: a hand-over sends it along
+  auto hand_over = [&](const std::string& why) {
+    return proxy(c, r, reinterpret_cast<const uint8_t*>(body.data()), body.size(), why);
+  };
+  if (upload_id.empty() || upload_id.find('/') != std::string::npos || upload_id == "." || upload_id == "..")
+    return hand_over("mpu-args");
+  std::string user = "anonymous", why;
+  Session sess;
+  if (!authorize(r, bucket, q, &user, &sess, &why)) return hand_over(why);
+  std::vector<std::pair<int64_t, std::string>> requested;
+  bool blank = body.find_first_not_of(" \t\r\n") == std::string::npos;
+  if (!blank && !parse_complete_body(body, &requested)) return hand_over("mpu-xml");
+  const std::string mpu_dir = "/.s3_mpu/" + upload_id, dest = "/" + bucket + "/" + key;
+  std::vector<std::pair<std::string, pb::FileMetadata>> files;
+  if (fc_->list(mpu_dir + "/", &files, r.rid) != FastClient::Ok) return hand_over("mpu-list");
+  bool has_marker = false;
+  std::map<int64_t, std::pair<std::string, uint64_t>> have;  // part -> (etag hex, size)
+  for (auto& f : files) {
+    if (f.first == mpu_dir + "/.s3keep") has_marker = true;
+    const std::string tail = f.first.substr(std::min(f.first.size(), mpu_dir.size() + 1));
+    if (f.first.compare(0, mpu_dir.size() + 1, mpu_dir + "/") == 0 && !tail.empty() && tail.size() <= 9 &&
+        all_digits(tail))
+      have[std::stoll(tail)] = {f.second.etag_md5, f.second.size};
+  }
+  if (!has_marker) return hand_over("mpu-missing");  // NoSuchUpload
+  std::vector<int64_t> nums;
+  if (!requested.empty()) {
+    auto unq = [](std::string v) {
+      while (!v.empty() && v.front() == '"') v.erase(v.begin());
+      while (!v.empty() && v.back() == '"') v.pop_back();
+      return v;
+    };
+    for (auto& rq : requested) {
+      auto h = have.find(rq.first);
+      if (h == have.end() || (!rq.second.empty() && unq(rq.second) != h->second.first)) return hand_over("mpu-part");
+      nums.push_back(rq.first);
+    }
+    for (size_t i = 1; i < nums.size(); ++i)
+      if (nums[i] <= nums[i - 1]) return hand_over("mpu-order");
+  } else {
+    for (auto& h : have) nums.push_back(h.first);
+  }
+  std::string md5s;
+  uint64_t total = 0;
+  std::string layout;
+  for (int64_t n : nums) {
+    const std::string& hx = have[n].first;
+    if (hx.size() != 32) return hand_over("mpu-etag");
+    for (size_t k = 0; k < 32; k += 2) md5s.push_back(static_cast<char>(hexval(hx[k]) * 16 + hexval(hx[k + 1])));
+    total += have[n].second;
+    layout += (layout.empty() ? "" : ",") + std::to_string(n) + ":" + std::to_string(have[n].second);
+  }
+  const std::string final_etag = "\"" + crypto::md5_hex(reinterpret_cast<const uint8_t*>(md5s.data()), md5s.size()) +
+                                 "-" + std::to_string(nums.size()) + "\"";
+  // from here on the namespace changes; a failure is answered 500 like the gateway's DfsError
+  auto internal = [&](const std::string& msg) {
+    const std::string x = "<Error>" + xel("Code", "InternalError") + xel("Message", msg) + xel("Resource", dest) +
+                          "<RequestId></RequestId></Error>";
+    std::string h = "HTTP/1.1 500 Internal Server Error\r\nContent-Type: application/xml\r\nContent-Length: " +
+                    std::to_string(x.size()) + "\r\nConnection: close\r\n\r\n";
+    r.status = 500;
+    r.keep_alive = false;
+    count(r, 500);
+    if (cfg_.auth_enabled) audit(c, r, user, 500, sess.role_arn);
+    send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(x.data()), x.size());
+    return false;
+  };
+  std::string msg;
+  // replace whatever object was at the destination (plain file or an older multipart one)
+  (void)fc_->remove(dest, &msg, r.rid);
+  std::vector<std::pair<std::string, pb::FileMetadata>> old;
+  if (fc_->list(dest + "/", &old, r.rid) != FastClient::Ok) return internal("listing the destination failed");
+  for (auto& f : old) (void)fc_->remove(f.first, &msg, r.rid);
+  {
+    std::map<std::string, std::string> attrs{{"ETag", final_etag}, {"x-dfs-mpu-size", std::to_string(total)},
+                                             {"x-dfs-mpu-layout", layout}};
+    int64_t slot = fc_->acquire_slot(1);
+    if (slot < 0) return internal("no buffer");
+    FastClient::Times t;
+    std::string md5;
+    int reps = 0;
+    auto st = fc_->write_slot(dest + "/.s3_mpu_completed", slot, 0, &reps, &msg, &t, r.rid, &attrs, nullptr, &md5);
+    fc_->release(slot);
+    if (st != FastClient::Ok) return internal("Failed to create completion marker: " + msg);
+  }
+  // the parts move under the object concurrently (independent files, independent Raft entries)
+  std::vector<std::future<std::string>> futs;
+  for (int64_t n : nums)
+    futs.push_back(pool_.submit([this, n, &mpu_dir, &dest, &r] {
+      std::string m;
+      const std::string num = std::to_string(n);
+      auto st = fc_->rename(mpu_dir + "/" + num, dest + "/" + num, &m, r.rid);
+      return st == FastClient::Ok ? std::string() : (m.empty() ? "rename of part " + num + " failed" : m);
+    }));
+  std::string first_err;
+  for (auto& f : futs) {
+    std::string e = f.get();
+    if (!e.empty() && first_err.empty()) first_err = e;
+  }
+  if (!first_err.empty()) return internal(first_err);
+  std::set<int64_t> used(nums.begin(), nums.end());
+  for (auto& f : files) {
+    const std::string tail = f.first.substr(std::min(f.first.size(), mpu_dir.size() + 1));
+    const bool part = !tail.empty() && tail.size() <= 9 && all_digits(tail);
+    if (ends_with(f.first, ".etag") || f.first == mpu_dir + "/.s3keep" || (part && !used.count(std::stoll(tail))))
+      (void)fc_->remove(f.first, &msg, r.rid);
+  }
+  const std::string x = "<CompleteMultipartUploadResult>" +
+                        xel("Location", "http://localhost:" + std::to_string(cfg_.port) + "/" + bucket + "/" + key) +
+                        xel("Bucket", bucket) + xel("Key", key) + xel("ETag", final_etag) +
+                        "</CompleteMultipartUploadResult>";
+  std::string h = "HTTP/1.1 200 OK\r\nContent-Type: application/xml\r\nContent-Length: " + std::to_string(x.size()) +
+                  "\r\n" + (r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+  r.status = 200;
+  count(r, 200);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.mpu_completes++;
+  }
+  const bool ok = send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(x.data()), x.size());
+  if (cfg_.auth_enabled) audit(c, r, user, 200, sess.role_arn);
   return ok;
 }
 

@@ -865,7 +865,11 @@ def test_native_front_serves_object_data(gw, front):
     done = "<CompleteMultipartUpload>" + "".join(
         f"<Part><PartNumber>{i + 1}</PartNumber><ETag>{e}</ETag></Part>" for i, e in enumerate(etags)) + \
         "</CompleteMultipartUpload>"
-    assert requests.post(f"{u}/nat/big?uploadId={up}", data=done).status_code == 200
+    r = requests.post(f"{u}/nat/big?uploadId={up}", data=done)
+    assert r.status_code == 200
+    want_etag = '"' + hashlib.md5(b"".join(hashlib.md5(p).digest() for p in parts)).hexdigest() + '-3"'
+    assert X.find_text(X.parse(r.content), ["ETag"]) == want_etag
+    assert gw.front.stats()["mpu_completes"] >= 1  # completed natively, parts renamed in parallel
     whole = b"".join(parts)
     assert requests.get(f"{u}/nat/big").content == whole
     lo, hi = (1 << 20) - 5, (2 << 20) + 7
