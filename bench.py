@@ -67,10 +67,11 @@ def parse():
                         "for this long per rank (0 = skip); reported under stress_write")
     p.add_argument("--stress-size", type=int, default=10240)
     p.add_argument("--stress-concurrency", type=int, default=5)
-    p.add_argument("--remote-steps", type=int, default=2,
+    p.add_argument("--remote-steps", type=int, default=None,
                    help="after the timed steps, repeat write+read this many times with a REMOTE client "
                         "(no shared memory, no local sockets: every master and chunkserver RPC over gRPC/TCP, "
-                        "as the reference's dfs_cli does); reported under remote_client (0 = skip)")
+                        "as the reference's dfs_cli does); reported under remote_client (0 = skip; "
+                        "default 2 on one GPU, 0 with several: their replicas would only add volume usage)")
     p.add_argument("--profile-dir", default=None,
                    help="run each ChunkServer under rocprofv3 --kernel-trace --stats, output here")
     return p.parse_args()
@@ -204,10 +205,14 @@ def main():
 
     threading.Thread(target=watchdog, daemon=True).start()
 
+    if a.remote_steps is None:
+        a.remote_steps = 2 if n == 1 else 0
+    tmp_parent = Path(os.environ.get("TMPDIR", "/tmp"))
     if rank == 0 and not a.workdir:
-        _make_room(Path(os.environ.get("TMPDIR", "/tmp")), _bytes_needed(a, n))
-    base = bcast((a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=os.environ.get("TMPDIR", "/tmp")))
-                 if rank == 0 else None)
+        _make_room(tmp_parent, _bytes_needed(a, n))
+    base, journal_segs = bcast(((a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=str(tmp_parent))),
+                                _journal_segments(Path(a.workdir) if a.workdir else tmp_parent, _bytes_needed(a, n), n))
+                               if rank == 0 else None)
     base_p = Path(base)
     if rank == 0:
         base_p.mkdir(parents=True, exist_ok=True)
@@ -217,6 +222,8 @@ def main():
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     env.setdefault("DFS_LOG", "warning")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if journal_segs:
+        env.setdefault("DFS_JOURNAL_SEGS", str(journal_segs))
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE",
               "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
@@ -481,7 +488,9 @@ def main():
                 "journal": {k: sum(r["cs"].get(f, 0) for r in allr) for k, f in (
                     ("records", "journal_records"), ("sync_rounds", "journal_sync_rounds"),
                     ("materialized_blocks", "materialized_blocks"), ("materialize_pending", "materialize_pending"),
-                    ("full_waits", "journal_full_waits"))} if any(r["cs"].get("journal") for r in allr) else None,
+                    ("full_waits", "journal_full_waits"), ("segments", "journal_segs"),
+                    ("segments_retired", "journal_segs_retired"), ("prepare_errors", "journal_prepare_errors"),
+                    ("materialize_errors", "materialize_errors"))} if any(r["cs"].get("journal") for r in allr) else None,
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],
             }
@@ -588,7 +597,26 @@ def observed_transport(allr, n: int) -> str:
 def _bytes_needed(a, n: int) -> int:
     """Block bytes this run leaves on the node's volume (every replica of every file)."""
     rf = min(3, n)
-    return n * rf * (a.steps + a.warmup) * a.count * (a.size + a.size // 128 + 4096)
+    steps = a.steps + a.warmup + (a.remote_steps or 0)
+    return n * rf * steps * a.count * (a.size + a.size // 128 + 4096)
+
+
+JOURNAL_SEG_BYTES = 256 << 20
+
+
+def _journal_segments(parent: Path, need: int, n: int) -> int:
+    """Segments per chunkserver for the block journal, so that the N journals plus every
+    materialized replica of this run fit the volume together (the journal's segments are
+    recycled, not freed: at N=8 x RF 3 the run's blocks alone approach a 79 GB volume).
+    0 = leave the chunkservers' default (16 x 256 MiB)."""
+    if os.environ.get("DFS_JOURNAL_SEGS") or os.environ.get("DFS_JOURNAL") == "0":
+        return 0
+    try:
+        free = shutil.disk_usage(parent).free
+    except OSError:
+        return 0
+    budget = (free - int(need * 1.15) - (2 << 30)) // max(1, n)
+    return int(max(3, min(16, budget // JOURNAL_SEG_BYTES)))
 
 
 def _make_room(parent: Path, need: int) -> None:

@@ -192,7 +192,106 @@ static void journal_case(const std::string& dir, int threads, int per, int mode,
   std::filesystem::remove_all(dir);
 }
 
+// PCIe roofline of the bench path: `threads` concurrent 1 MiB transfers
+// host <-> HBM, (a) plain hipMemcpyAsync from pinned memory on one stream per thread (the
+// copy engines' rate) and (b) the store's fused kernels (crc_write_copy_kernel: load over
+// PCIe + checksum + store into HBM; crc_read_copy_kernel: verify + store over PCIe) from
+// registered host memory, as the fast path drives them for co-located clients.
+static void pcie_roofline(int device, int threads, int per, size_t n) {
+  (void)hipSetDevice(device);
+  std::vector<uint8_t*> host(threads), dev(threads);
+  std::vector<hipStream_t> st(threads);
+  for (int t = 0; t < threads; ++t) {
+    (void)hipHostMalloc(reinterpret_cast<void**>(&host[t]), n, hipHostMallocDefault);
+    std::memset(host[t], t + 1, n);
+    (void)hipMalloc(reinterpret_cast<void**>(&dev[t]), n);
+    (void)hipStreamCreateWithFlags(&st[t], hipStreamNonBlocking);
+  }
+  auto run = [&](auto&& body) {
+    std::vector<std::thread> ts;
+    auto t0 = Clock::now();
+    for (int t = 0; t < threads; ++t)
+      ts.emplace_back([&, t] {
+        for (int i = 0; i < per; ++i) body(t);
+      });
+    for (auto& th : ts) th.join();
+    return double(threads) * per * n / secs(t0, Clock::now()) / 1e9;
+  };
+  // warm-up
+  run([&](int t) {
+    (void)hipMemcpyAsync(dev[t], host[t], n, hipMemcpyHostToDevice, st[t]);
+    (void)hipStreamSynchronize(st[t]);
+  });
+  double h2d = run([&](int t) {
+    (void)hipMemcpyAsync(dev[t], host[t], n, hipMemcpyHostToDevice, st[t]);
+    (void)hipStreamSynchronize(st[t]);
+  });
+  double d2h = run([&](int t) {
+    (void)hipMemcpyAsync(host[t], dev[t], n, hipMemcpyDeviceToHost, st[t]);
+    (void)hipStreamSynchronize(st[t]);
+  });
+  StoreConfig cfg;
+  cfg.storage_dir = "/tmp/io_bench_roofline";
+  cfg.device = device;
+  cfg.hbm_capacity = 4ull << 30;
+  cfg.durability = Durability::HbmAck;
+  cfg.sync_writes = false;
+  cfg.lanes = std::max(8, threads);
+  double wr = 0, rd = 0;
+  uint64_t fused_w = 0, fused_r = 0;
+  {
+    ChunkStore store(cfg);
+    store.debug_pause_spill(true);  // store only: no NVMe spill competing for the host
+    for (int t = 0; t < threads; ++t) store.register_host(host[t], n);
+    const uint32_t crc = crc32(host[0], n);
+    std::vector<uint32_t> crcs(threads);
+    for (int t = 0; t < threads; ++t) crcs[t] = crc32(host[t], n);
+    (void)crc;
+    std::atomic<int> seq{0};
+    auto write_one = [&](int t) {
+      std::string id = "r" + std::to_string(seq.fetch_add(1));
+      if (!store.write(id, host[t], n, crcs[t]).ok) std::fprintf(stderr, "roofline write failed\n");
+    };
+    run(write_one);  // warm-up + ids for the reads
+    wr = run(write_one);
+    std::atomic<int> rs{0};
+    rd = run([&](int t) {
+      std::string id = "r" + std::to_string(rs.fetch_add(1) % (threads * per));
+      ReadResult r = store.read_into(id, 0, n, host[t]);
+      if (r.status != ReadStatus::Ok) std::fprintf(stderr, "roofline read failed\n");
+    });
+    StoreStats ss = store.stats();
+    fused_w = ss.fused_writes;
+    fused_r = ss.fused_reads;
+    for (int t = 0; t < threads; ++t) store.unregister_host(host[t]);
+    store.debug_pause_spill(false);
+  }
+  std::filesystem::remove_all("/tmp/io_bench_roofline");
+  for (int t = 0; t < threads; ++t) {
+    (void)hipHostFree(host[t]);
+    (void)hipFree(dev[t]);
+    (void)hipStreamDestroy(st[t]);
+  }
+  std::printf("{\"pcie_roofline\": {\"threads\": %d, \"bytes\": %zu, \"per_thread\": %d, \"memcpy_h2d_GBps\": %.2f, "
+              "\"memcpy_d2h_GBps\": %.2f, \"store_write_fused_GBps\": %.2f, \"store_read_fused_GBps\": %.2f, "
+              "\"write_vs_h2d\": %.3f, \"read_vs_d2h\": %.3f, \"fused_writes\": %llu, \"fused_reads\": %llu}}\n",
+              threads, n, per, h2d, d2h, wr, rd, h2d > 0 ? wr / h2d : 0.0, d2h > 0 ? rd / d2h : 0.0,
+              static_cast<unsigned long long>(fused_w), static_cast<unsigned long long>(fused_r));
+}
+
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--pcie-roofline") {
+      int threads = 10, per = 200;
+      size_t n = 1 << 20;
+      for (int j = 1; j + 1 < argc; ++j) {
+        if (std::string(argv[j]) == "--threads") threads = std::atoi(argv[j + 1]);
+        if (std::string(argv[j]) == "--per") per = std::atoi(argv[j + 1]);
+        if (std::string(argv[j]) == "--bytes") n = std::strtoull(argv[j + 1], nullptr, 10);
+      }
+      pcie_roofline(0, threads, per, n);
+      return 0;
+    }
   int device = 0, iters = 50;
   bool fsync = true;
   bool zero_copy = true;

@@ -366,6 +366,9 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["materialize_pending"] = t.materialize_pending;
         d["materialize_batches"] = t.materialize_batches;
         d["materialize_errors"] = t.materialize_errors;
+        d["materialize_last_error"] = t.materialize_last_error;
+        d["journal_prepare_errors"] = t.journal_prepare_errors;
+        d["journal_last_error"] = t.journal_last_error;
         return d;
       })
       .def("gpu_crc", [](ChunkStore& s, py::buffer data) {

@@ -226,7 +226,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.max_segs = env_int("DFS_JOURNAL_SEGS", 16);
     jc.direct = env_int("DFS_JOURNAL_DIRECT", 0) != 0;
     jc.spares = env_int("DFS_JOURNAL_SPARES", 2);
-    jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 1) != 0;
+    jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 0) != 0;
     jc.sync_delay_us = env_int("DFS_JOURNAL_SYNC_DELAY_US", 0);
     jc.sync = cfg_.sync_writes;
     mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 50) / 100.0;
@@ -2219,6 +2219,9 @@ StoreStats ChunkStore::stats() {
     s.materialize_pending = mat_q_.size();
     s.materialize_batches = mat_batches_;
     s.materialize_errors = mat_errors_;
+    s.materialize_last_error = mat_last_error_;
+    s.journal_prepare_errors = j.prepare_errors;
+    s.journal_last_error = j.last_error;
   }
   {
     std::lock_guard<std::mutex> rg(reg_mu_);
@@ -2567,6 +2570,7 @@ void ChunkStore::materializer_loop() {
     MatItem m;
     bool current = false, ok = false;
     int fd = -1, mfd = -1;
+    std::string err;
   };
   std::vector<Job> batch;
   for (;;) {
@@ -2610,6 +2614,7 @@ void ChunkStore::materializer_loop() {
       j.mfd = j.fd < 0 ? -1 : ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
       j.ok = j.mfd >= 0 && copy_range(j.m.rec.seg->fd, j.m.rec.data_off(), j.fd, j.m.n) &&
              write_all(j.mfd, j.m.meta->data(), j.m.meta->size(), 0);
+      if (!j.ok) j.err = errno_str(dp.c_str());
     }
     // one flush for the whole batch: syncfs() of the storage filesystem covers every file
     // written above and the directory entries (instead of two fdatasyncs per block)
@@ -2619,6 +2624,9 @@ void ChunkStore::materializer_loop() {
     if (any && cfg_.sync_writes) {
       int dfd = ::open(cfg_.storage_dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
       dir_ok = dfd >= 0 && ::syncfs(dfd) == 0;
+      if (!dir_ok)
+        for (auto& j : batch)
+          if (j.ok) j.err = errno_str("syncfs");
       if (dfd >= 0) ::close(dfd);
     }
     const bool drop = gpu();
@@ -2648,6 +2656,7 @@ void ChunkStore::materializer_loop() {
         }
         if (!j.ok) {
           ++mat_errors_;
+          mat_last_error_ = j.err;
           retry.push_back(&j);
         }
       }
@@ -2659,7 +2668,11 @@ void ChunkStore::materializer_loop() {
     mat_cv_.notify_all();
     for (auto& j : batch)
       if (!j.current || j.ok) journal_->materialized(j.m.rec.seg, 1);
-    if (!retry.empty()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    if (!retry.empty()) {
+      std::fprintf(stderr, "[store] materializing %zu block(s) failed, retrying: %s\n", retry.size(),
+                   retry.front()->err.c_str());
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
   }
 }
 

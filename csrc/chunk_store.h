@@ -103,8 +103,9 @@ struct StoreStats {
   uint64_t journal_tombstones = 0, journal_full_waits = 0, journal_segs = 0, journal_segs_free = 0;
   uint64_t journal_segs_retired = 0, journal_replayed = 0, journal_replay_skipped = 0;
   uint64_t materialized_blocks = 0, materialized_bytes = 0, materialize_pending = 0, materialize_batches = 0;
-  uint64_t materialize_errors = 0;
+  uint64_t materialize_errors = 0, journal_prepare_errors = 0;
   bool journal_failed = false;
+  std::string journal_last_error, materialize_last_error;
 };
 
 // Group commit: callers that finished writing share one flush round — syncfs() of the
@@ -427,6 +428,7 @@ class ChunkStore {
   uint64_t mat_idle_ns_ = 100000000;  // ... or after this long without an append
   std::thread materializer_;
   uint64_t materialized_blocks_ = 0, materialized_bytes_ = 0, mat_batches_ = 0, mat_errors_ = 0;  // mu_
+  std::string mat_last_error_;  // mu_
 };
 
 }  // namespace dfs

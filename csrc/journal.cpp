@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
 #include <chrono>
 #include <cstring>
 
@@ -134,6 +135,7 @@ void BlockJournal::prepare_loop() {
     ++preparing_;
     const std::string path = cfg_.dir + "/seg-" + std::to_string(next_file_++) + ".log";
     lk.unlock();
+    errno = 0;
     SegRef s = open_seg(path, true);
     bool ok = s != nullptr;
     if (ok) {
@@ -146,6 +148,11 @@ void BlockJournal::prepare_loop() {
       (void)::posix_fadvise(s->fd, 0, 0, POSIX_FADV_DONTNEED);
       fsync_dir(cfg_.dir);  // the name survives a crash before its first record is acked
     }
+    const int e = errno;
+    if (!ok) {
+      s.reset();
+      ::unlink(path.c_str());
+    }
     lk.lock();
     --preparing_;
     if (ok) {
@@ -153,13 +160,36 @@ void BlockJournal::prepare_loop() {
       free_.push_back(s);
       st_.prepared++;
     } else {
-      ::unlink(path.c_str());
-      // no room for another segment: run with the ones there are (a writer waits for the
-      // materializer to recycle one instead of failing)
-      cfg_.max_segs = std::max<int>(2, static_cast<int>(segs_.size()));
+      st_.prepare_errors++;
+      st_.last_error = "segment " + path + ": " + std::strerror(e ? e : EIO);
+      std::fprintf(stderr, "[journal] preparing %s failed: %s (%s)\n", path.c_str(), std::strerror(e ? e : EIO),
+                   describe_locked().c_str());
+      if ((e == ENOSPC || e == EDQUOT) && !segs_.empty()) {
+        // no room for another segment: run with the ones there are (a writer waits for the
+        // materializer to recycle one instead of failing)
+        cfg_.max_segs = std::max<int>(2, static_cast<int>(segs_.size()));
+      } else {
+        // transient (or nothing to fall back on): try again shortly
+        cv_.wait_for(lk, std::chrono::milliseconds(500), [&] { return prep_stop_; });
+      }
     }
     cv_.notify_all();
   }
+}
+
+std::string BlockJournal::describe_locked() const {
+  char buf[512];
+  int n = std::snprintf(buf, sizeof(buf), "segments %zu of max %d, in use %zu, free %zu, preparing %d",
+                        segs_.size(), cfg_.max_segs, order_.size(), free_.size(), preparing_);
+  if (!order_.empty() && n > 0 && n < static_cast<int>(sizeof(buf))) {
+    const JournalSeg* f = order_.front().get();
+    std::snprintf(buf + n, sizeof(buf) - n,
+                  "; oldest seq %llu: live %llu, sealed %d, completed %llu of %llu, readers %d",
+                  static_cast<unsigned long long>(f->seq), static_cast<unsigned long long>(f->live),
+                  f->sealed ? 1 : 0, static_cast<unsigned long long>(f->done_upto),
+                  static_cast<unsigned long long>(f->tail), f->readers.load());
+  }
+  return buf;
 }
 
 uint64_t BlockJournal::hdr_bytes_for(uint64_t nslices) { return align_up(kHdr + 4 * nslices, kPage); }
@@ -306,6 +336,7 @@ void BlockJournal::retire_all() {
 // the cap) and makes it the active one. Waits for the materializer when all are in use.
 SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::string* err) {
   auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+  auto next_report = std::chrono::steady_clock::now() + std::chrono::seconds(5);
   for (;;) {
     if (failed_) {
       *err = "journal failed";
@@ -334,9 +365,16 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
       order_.push_back(s);
       return s;
     }
-    if (static_cast<int>(segs_.size()) + preparing_ >= cfg_.max_segs) ++st_.full_waits;  // not just filling
-    if (cv_.wait_until(lk, deadline) == std::cv_status::timeout) {
-      *err = "journal full (materializer behind)";
+    const bool full = static_cast<int>(segs_.size()) + preparing_ >= cfg_.max_segs;
+    if (full) ++st_.full_waits;  // not just waiting for the preparer
+    if (std::chrono::steady_clock::now() >= next_report) {
+      std::fprintf(stderr, "[journal] writer waiting for a free segment (%s)\n", describe_locked().c_str());
+      next_report += std::chrono::seconds(10);
+    }
+    if (cv_.wait_until(lk, std::min(deadline, next_report)) == std::cv_status::timeout &&
+        std::chrono::steady_clock::now() >= deadline) {
+      *err = std::string(full ? "journal full (materializer behind): " : "no journal segment ready: ") +
+             describe_locked() + (st_.last_error.empty() ? "" : "; last error: " + st_.last_error);
       return nullptr;
     }
   }

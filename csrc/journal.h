@@ -41,11 +41,14 @@ struct JournalConfig {
   int max_segs = 16;                // journal capacity = max_segs x seg_bytes
   bool direct = false;              // O_DIRECT appends (aligned sources only; else buffered)
   bool sync = true;                 // fdatasync on commit (false: tests / --no-fsync)
-  // Segments are zero-filled ahead of use by a background thread (written extents: an
-  // append is then a pure overwrite, and its flush carries no allocation metadata); this
-  // many stand ready beyond the active one (recycled segments need no fill).
+  // Segments are created ahead of use by a background thread; this many stand ready beyond
+  // the active one. zero_fill writes them out once (written extents: a first-cycle append is
+  // a pure overwrite). Measured on the MI355X box's overlay volume the fill's own writes
+  // cost the concurrent appends more than unwritten-extent conversion does
+  // (profiles/r4_journal), so the default is fallocate only; recycled segments are written
+  // extents either way.
   int spares = 2;
-  bool zero_fill = true;   // false: fallocate only (unwritten extents, converted on first use)
+  bool zero_fill = false;
   int sync_delay_us = 0;   // tests: the commit leader waits this long first (makes rounds shared)
 };
 
@@ -90,8 +93,9 @@ struct ReplayRecord {
 struct JournalStats {
   uint64_t records = 0, bytes = 0, commits = 0, sync_rounds = 0, tombstones = 0, pads = 0;
   uint64_t segs_total = 0, segs_free = 0, segs_retired = 0, full_waits = 0;
-  uint64_t replayed = 0, replay_skipped = 0, prepared = 0;
+  uint64_t replayed = 0, replay_skipped = 0, prepared = 0, prepare_errors = 0;
   bool failed = false;
+  std::string last_error;  // the last segment preparation / header error, for /stats
 };
 
 class BlockJournal {
@@ -134,6 +138,7 @@ class BlockJournal {
 
  private:
   SegRef activate_locked(std::unique_lock<std::mutex>& lk, std::string* err);
+  std::string describe_locked() const;  // segment accounting, for errors and stall reports
   bool write_seg_header(JournalSeg* s, uint64_t seq);
   void complete_locked(JournalSeg* s, uint64_t off, uint64_t end);
   SegRef open_seg(const std::string& path, bool create);
