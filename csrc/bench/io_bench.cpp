@@ -199,60 +199,60 @@ static void journal_case(const std::string& dir, int threads, int per, int mode,
 // registered host memory, as the fast path drives them for co-located clients.
 static void pcie_roofline(int device, int threads, int per, size_t n) {
   (void)hipSetDevice(device);
-  std::vector<uint8_t*> host(threads), dev(threads);
-  std::vector<hipStream_t> st(threads);
-  for (int t = 0; t < threads; ++t) {
-    (void)hipHostMalloc(reinterpret_cast<void**>(&host[t]), n, hipHostMallocDefault);
-    std::memset(host[t], t + 1, n);
-    (void)hipMalloc(reinterpret_cast<void**>(&dev[t]), n);
-    (void)hipStreamCreateWithFlags(&st[t], hipStreamNonBlocking);
-  }
-  auto run = [&](auto&& body) {
-    std::vector<std::thread> ts;
-    auto t0 = Clock::now();
-    for (int t = 0; t < threads; ++t)
-      ts.emplace_back([&, t] {
-        for (int i = 0; i < per; ++i) body(t);
-      });
-    for (auto& th : ts) th.join();
-    return double(threads) * per * n / secs(t0, Clock::now()) / 1e9;
-  };
-  // warm-up
-  run([&](int t) {
-    (void)hipMemcpyAsync(dev[t], host[t], n, hipMemcpyHostToDevice, st[t]);
-    (void)hipStreamSynchronize(st[t]);
-  });
-  double h2d = run([&](int t) {
-    (void)hipMemcpyAsync(dev[t], host[t], n, hipMemcpyHostToDevice, st[t]);
-    (void)hipStreamSynchronize(st[t]);
-  });
-  double d2h = run([&](int t) {
-    (void)hipMemcpyAsync(host[t], dev[t], n, hipMemcpyDeviceToHost, st[t]);
-    (void)hipStreamSynchronize(st[t]);
-  });
   StoreConfig cfg;
   cfg.storage_dir = "/tmp/io_bench_roofline";
   cfg.device = device;
-  cfg.hbm_capacity = 4ull << 30;
+  cfg.hbm_capacity = 16ull << 30;
   cfg.durability = Durability::HbmAck;
   cfg.sync_writes = false;
   cfg.lanes = std::max(8, threads);
-  double wr = 0, rd = 0;
+  double h2d = 0, d2h = 0, wr = 0, rd = 0;
   uint64_t fused_w = 0, fused_r = 0;
   {
     ChunkStore store(cfg);
     store.debug_pause_spill(true);  // store only: no NVMe spill competing for the host
-    for (int t = 0; t < threads; ++t) store.register_host(host[t], n);
-    const uint32_t crc = crc32(host[0], n);
+    // the writers' buffers as the fast path has them: ordinary pages, registered with the
+    // store (hipHostRegister) so the fused kernels reach them over PCIe
+    std::vector<uint8_t*> host(threads), dev(threads);
+    std::vector<hipStream_t> st(threads);
+    for (int t = 0; t < threads; ++t) {
+      host[t] = static_cast<uint8_t*>(std::aligned_alloc(4096, (n + 4095) & ~size_t(4095)));
+      for (size_t i = 0; i < n; ++i) host[t][i] = static_cast<uint8_t>(i * 131 + t);
+      store.register_host(host[t], n);
+      (void)hipMalloc(reinterpret_cast<void**>(&dev[t]), n);
+      (void)hipStreamCreateWithFlags(&st[t], hipStreamNonBlocking);
+    }
+    auto run = [&](auto&& body) {
+      std::vector<std::thread> ts;
+      auto t0 = Clock::now();
+      for (int t = 0; t < threads; ++t)
+        ts.emplace_back([&, t] {
+          for (int i = 0; i < per; ++i) body(t);
+        });
+      for (auto& th : ts) th.join();
+      return double(threads) * per * n / secs(t0, Clock::now()) / 1e9;
+    };
+    auto h2d_one = [&](int t) {
+      (void)hipMemcpyAsync(dev[t], host[t], n, hipMemcpyHostToDevice, st[t]);
+      (void)hipStreamSynchronize(st[t]);
+    };
+    auto d2h_one = [&](int t) {
+      (void)hipMemcpyAsync(host[t], dev[t], n, hipMemcpyDeviceToHost, st[t]);
+      (void)hipStreamSynchronize(st[t]);
+    };
+    run(h2d_one);  // warm-up
+    h2d = run(h2d_one);
+    d2h = run(d2h_one);
+    for (int t = 0; t < threads; ++t)  // d2h overwrote them with the device's (random) bytes
+      for (size_t i = 0; i < n; ++i) host[t][i] = static_cast<uint8_t>(i * 131 + t);
     std::vector<uint32_t> crcs(threads);
     for (int t = 0; t < threads; ++t) crcs[t] = crc32(host[t], n);
-    (void)crc;
     std::atomic<int> seq{0};
     auto write_one = [&](int t) {
       std::string id = "r" + std::to_string(seq.fetch_add(1));
       if (!store.write(id, host[t], n, crcs[t]).ok) std::fprintf(stderr, "roofline write failed\n");
     };
-    run(write_one);  // warm-up + ids for the reads
+    run(write_one);  // warm-up, and the blocks the reads use
     wr = run(write_one);
     std::atomic<int> rs{0};
     rd = run([&](int t) {
@@ -263,15 +263,15 @@ static void pcie_roofline(int device, int threads, int per, size_t n) {
     StoreStats ss = store.stats();
     fused_w = ss.fused_writes;
     fused_r = ss.fused_reads;
-    for (int t = 0; t < threads; ++t) store.unregister_host(host[t]);
+    for (int t = 0; t < threads; ++t) {
+      store.unregister_host(host[t]);
+      std::free(host[t]);
+      (void)hipFree(dev[t]);
+      (void)hipStreamDestroy(st[t]);
+    }
     store.debug_pause_spill(false);
   }
   std::filesystem::remove_all("/tmp/io_bench_roofline");
-  for (int t = 0; t < threads; ++t) {
-    (void)hipHostFree(host[t]);
-    (void)hipFree(dev[t]);
-    (void)hipStreamDestroy(st[t]);
-  }
   std::printf("{\"pcie_roofline\": {\"threads\": %d, \"bytes\": %zu, \"per_thread\": %d, \"memcpy_h2d_GBps\": %.2f, "
               "\"memcpy_d2h_GBps\": %.2f, \"store_write_fused_GBps\": %.2f, \"store_read_fused_GBps\": %.2f, "
               "\"write_vs_h2d\": %.3f, \"read_vs_d2h\": %.3f, \"fused_writes\": %llu, \"fused_reads\": %llu}}\n",

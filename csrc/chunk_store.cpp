@@ -227,6 +227,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.direct = env_int("DFS_JOURNAL_DIRECT", 0) != 0;
     jc.spares = env_int("DFS_JOURNAL_SPARES", 2);
     jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 0) != 0;
+    jc.full_timeout_s = env_int("DFS_JOURNAL_FULL_TIMEOUT_S", 120);
     jc.sync_delay_us = env_int("DFS_JOURNAL_SYNC_DELAY_US", 0);
     jc.sync = cfg_.sync_writes;
     mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 50) / 100.0;

@@ -335,7 +335,7 @@ void BlockJournal::retire_all() {
 // Caller holds the lock. Seals nothing; takes a free segment (or creates one while under
 // the cap) and makes it the active one. Waits for the materializer when all are in use.
 SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::string* err) {
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(cfg_.full_timeout_s);
   auto next_report = std::chrono::steady_clock::now() + std::chrono::seconds(5);
   for (;;) {
     if (failed_) {
@@ -343,6 +343,10 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
       return nullptr;
     }
     if (!preparer_.joinable()) preparer_ = std::thread([this] { prepare_loop(); });
+    // another writer activated a segment while this one waited: append there instead (two
+    // activations would leave the first one unsealed behind the second, and retirement,
+    // which goes oldest first, would stop at it for good)
+    if (!order_.empty() && !order_.back()->sealed) return order_.back();
     SegRef s;
     if (!free_.empty()) {
       s = free_.back();
@@ -391,14 +395,16 @@ bool BlockJournal::reserve(uint64_t n, uint64_t nslices, JournalRec* r, std::str
     *err = "journal failed";
     return false;
   }
-  SegRef s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
-  if (!s || s->tail + len > s->cap) {
+  SegRef s;
+  for (;;) {
+    s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
+    if (s && s->tail + len <= s->cap) break;
     if (s) {
       s->sealed = true;
       cv_.notify_all();
     }
-    s = activate_locked(lk, err);
-    if (!s) return false;
+    // activate_locked may wait (and drop the lock): whatever it returns is checked again
+    if (!activate_locked(lk, err)) return false;
   }
   r->seg = s;
   r->off = s->tail;
@@ -517,11 +523,15 @@ void BlockJournal::tombstone(const std::string& id) {
   {
     std::unique_lock<std::mutex> lk(mu_);
     if (failed_) return;
-    SegRef s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
-    if (!s || s->tail + kPage > s->cap) {
-      if (s) s->sealed = true;
-      s = activate_locked(lk, &err);
-      if (!s) return;
+    SegRef s;
+    for (;;) {
+      s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
+      if (s && s->tail + kPage <= s->cap) break;
+      if (s) {
+        s->sealed = true;
+        cv_.notify_all();
+      }
+      if (!activate_locked(lk, &err)) return;
     }
     r.seg = s;
     r.off = s->tail;
@@ -562,6 +572,7 @@ void BlockJournal::retire_ready() {
     // is still reading from waits for the next call
     while (!order_.empty()) {
       SegRef f = order_.front();
+      if (!f->sealed && f != order_.back()) f->sealed = true;  // only the newest segment takes appends
       if (!f->sealed || f->live || f->done_upto < f->tail || f->readers.load() > 0) break;
       retire.push_back(f);
       order_.erase(order_.begin());

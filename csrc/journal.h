@@ -50,6 +50,7 @@ struct JournalConfig {
   int spares = 2;
   bool zero_fill = false;
   int sync_delay_us = 0;   // tests: the commit leader waits this long first (makes rounds shared)
+  int full_timeout_s = 120;  // a writer waiting this long for a free segment fails
 };
 
 enum JournalRecType : uint32_t { kJrBlock = 1, kJrPad = 2, kJrTomb = 3 };

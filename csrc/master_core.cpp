@@ -138,6 +138,9 @@ std::string locked_path(const Json& rec) {
 
 }  // namespace
 
+Json file_meta_json(const pb::FileMetadata& m) { return file_json(m); }
+Json block_info_json(const pb::BlockInfo& b) { return block_json(b); }
+
 // ---------------------------------------------------------------- placement
 std::vector<std::string> select_servers_rack_aware(const std::vector<ChunkServerStatus>& servers, size_t n,
                                                    const std::string& preferred) {

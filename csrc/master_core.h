@@ -56,6 +56,11 @@ struct ChunkServerStatus {
 std::vector<std::string> select_servers_rack_aware(const std::vector<ChunkServerStatus>& servers, size_t n,
                                                    const std::string& preferred);
 
+// The serde layout of FileMetadata / BlockInfo that Raft commands carry (IngestBatch,
+// ConvertToEc, transaction records; models/meta.py file_to_dict / block_to_dict).
+Json file_meta_json(const pb::FileMetadata& m);
+Json block_info_json(const pb::BlockInfo& b);
+
 class MasterCore : public raft::StateMachine {
  public:
   enum Code { OK = 0, NOT_FOUND = 5, FAILED_PRECONDITION = 9, INTERNAL = 13, UNAVAILABLE = 14, OUT_OF_RANGE = 11,

@@ -162,6 +162,29 @@ def test_small_journal_recycles_segments_under_pressure(native, tmp_path, monkey
     assert s.stats()["journal_replayed"] == 0 and sorted(s.list_blocks()) == sorted(vals)
 
 
+def test_concurrent_writers_recycle_a_small_journal(native, tmp_path, monkeypatch):
+    """Many writers at once on a journal of 3 small segments: whenever the active segment
+    fills, several writers wait for a free one at the same time. Exactly one activation may
+    win (the others append to it), or a segment left unsealed behind a newer one would block
+    retirement for good and every writer would end on 'journal full'."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    monkeypatch.setenv("DFS_JOURNAL_SEG_MB", "4")
+    monkeypatch.setenv("DFS_JOURNAL_SEGS", "3")
+    monkeypatch.setenv("DFS_JOURNAL_SPARES", "2")
+    monkeypatch.setenv("DFS_JOURNAL_FULL_TIMEOUT_S", "20")
+    s = open_store(native, tmp_path)
+    vals = {f"c{i}": os.urandom((1 << 20) - 4096 * (i % 7)) for i in range(120)}
+    with ThreadPoolExecutor(12) as ex:
+        res = list(ex.map(lambda kv: s.write(kv[0], kv[1], zlib.crc32(kv[1])), vals.items()))
+    assert all(r[0] for r in res), next(r for r in res if not r[0])
+    s.materialize()
+    st = s.stats()
+    assert st["journal_segs"] <= 3 and st["journal_segs_retired"] >= 20 and st["materialized_blocks"] == 120
+    for k, v in vals.items():
+        assert s.read(k, 0, 0)[2] == v
+
+
 def test_concurrent_writers_share_group_commits(native, tmp_path, monkeypatch):
     from concurrent.futures import ThreadPoolExecutor
 
