@@ -246,10 +246,14 @@ def main():
         barrier()
         if runs_master:
             ready = str(base_p / f"master{rank}.ready")
-            mp = procs.spawn([f"{PKG}.master.server", "--addr", f"127.0.0.1:{gport}", "--http-port", str(hport),
-                              "--storage-dir", str(base_p / f"rank{rank}" / "master"),
-                              "--shard-id", f"shard-{rank:03d}", "--shard-config", str(shard_file)],
-                             str(base_p / f"master{rank}.log"), dict(env, DFS_READY_FILE=ready))
+            from rust_hadoop_generated_by_llm_amd.cluster.launcher import role_command
+
+            # the native dfs_master executable (Python shell only with DFS_NATIVE_CONTROL=0)
+            mp = procs.spawn_raw(role_command("master.server", [
+                "--addr", f"127.0.0.1:{gport}", "--http-port", str(hport),
+                "--storage-dir", str(base_p / f"rank{rank}" / "master"),
+                "--shard-id", f"shard-{rank:03d}", "--shard-config", str(shard_file)], env),
+                str(base_p / f"master{rank}.log"), dict(env, DFS_READY_FILE=ready))
             wait_file(ready, mp, 300, procs)
         barrier()
         my_master = f"http://127.0.0.1:{ports[rank if per_gpu else 0]}"

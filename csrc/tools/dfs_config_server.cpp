@@ -26,7 +26,18 @@
 using namespace dfs;
 using namespace dfs::shell;
 
+static const char* kUsage =
+    "usage: dfs_config_server [--addr ADDR] [--id ID] [--peers PEERS] [--http-port HTTP_PORT]\n"
+    "                         [--advertise-addr ADVERTISE_ADDR] [--storage-dir STORAGE_DIR] [--tls-cert TLS_CERT]\n"
+    "                         [--tls-key TLS_KEY] [--ca-cert CA_CERT] [--no-fsync]\n"
+    "                         [--snapshot-threshold SNAPSHOT_THRESHOLD]\n";
+
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--help" || std::string(argv[i]) == "-h") {
+      std::fputs(kUsage, stdout);
+      return 0;
+    }
   block_stop_signals();
   Args a(argc, argv, {"no-fsync"});
   if (!a.error().empty()) {

@@ -982,7 +982,8 @@ HttpResponse Master::http(const HttpRequest& req) {
   if (req.path == "/debug/partition" && req.method == "POST" && env("DFS_DEBUG_ENDPOINTS") == "1") {
     std::set<std::string> blocked;
     try {
-      for (auto& b : Json::parse(req.body)["block"].items()) {
+      const Json body = Json::parse(req.body);  // (the loop below must not range over a temporary's member)
+      for (auto& b : body["block"].items()) {
         std::string x = b.str();
         while (!x.empty() && x.back() == '/') x.pop_back();
         blocked.insert(with_scheme(x));
@@ -1176,7 +1177,22 @@ int Master::run() {
 
 }  // namespace
 
+const char* kUsage =
+    "usage: dfs_master [-a ADDR | --addr ADDR] [--id ID] [--peers PEERS] [--http-port HTTP_PORT]\n"
+    "                  [--advertise-addr ADVERTISE_ADDR] [--storage-dir STORAGE_DIR] [--shard-id SHARD_ID]\n"
+    "                  [--standby] [--shard-config SHARD_CONFIG] [--config-servers CONFIG_SERVERS]\n"
+    "                  [--split-threshold-rps SPLIT_THRESHOLD_RPS] [--split-cooldown-secs SPLIT_COOLDOWN_SECS]\n"
+    "                  [--merge-threshold-rps MERGE_THRESHOLD_RPS] [--tls-cert TLS_CERT] [--tls-key TLS_KEY]\n"
+    "                  [--ca-cert CA_CERT] [--domain-name DOMAIN_NAME] [--backup-s3-endpoint BACKUP_S3_ENDPOINT]\n"
+    "                  [--backup-bucket BACKUP_BUCKET] [--snapshot-threshold SNAPSHOT_THRESHOLD] [--no-fsync]\n"
+    "                  [--fast-intervals] [--http-host HTTP_HOST]\n";
+
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--help" || std::string(argv[i]) == "-h") {
+      std::fputs(kUsage, stdout);
+      return 0;
+    }
   block_stop_signals();
   Args a(argc, argv, {"standby", "no-fsync", "fast-intervals"}, {{"a", "addr"}});
   if (!a.error().empty()) {

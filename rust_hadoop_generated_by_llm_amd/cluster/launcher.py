@@ -27,6 +27,22 @@ ROOT = Path(__file__).resolve().parents[2]
 
 _handed_out: set[int] = set()
 
+# Control-plane roles with a native executable (csrc/tools/dfs_master.cpp,
+# dfs_config_server.cpp): with DFS_NATIVE_CONTROL unset or 1 they run as those binaries, so
+# no Python interpreter lives in a master or config-server process; DFS_NATIVE_CONTROL=0
+# keeps the Python shells (the A/B launcher).
+NATIVE_BINARIES = {"master.server": "dfs_master", "config_server.server": "dfs_config_server"}
+
+
+def role_command(module: str, args: list[str], environ: dict | None = None) -> list[str]:
+    """argv for a role: its native executable when there is one (and it is enabled), else
+    ``python -m <package>.<module>``."""
+    env = os.environ if environ is None else environ
+    exe = ROOT / "build" / "native" / NATIVE_BINARIES.get(module, "-")
+    if module in NATIVE_BINARIES and env.get("DFS_NATIVE_CONTROL", "1") != "0" and exe.exists():
+        return [str(exe), *args]
+    return [sys.executable, "-m", f"{PKG}.{module}", *args]
+
 
 def free_port() -> int:
     """A port nothing listens on, below the kernel's ephemeral range (32768+) so that no
@@ -120,7 +136,7 @@ class LocalCluster:
             env.update(extra_env)
         log_path = str(self.base / f"{name}.log")
         logf = open(log_path, "ab")
-        p = subprocess.Popen([sys.executable, "-m", f"{PKG}.{module}", *args], env=env, stdout=logf,
+        p = subprocess.Popen(role_command(module, args, env), env=env, stdout=logf,
                              stderr=subprocess.STDOUT, cwd=str(ROOT), start_new_session=True)
         logf.close()
         proc = Proc(name, p, ready, log_path=log_path, module=module, args=list(args), extra_env=extra_env)

@@ -49,3 +49,21 @@ def test_dfs_cli_flags_and_benchmark_defaults():
     a = p.parse_args(["--host-alias", "a=b", "--host-alias", "c=d", "--ca-cert", "x", "--domain-name", "y",
                       "--config-servers", "c1", "ls"])
     assert a.host_alias == ["a=b", "c=d"]
+
+
+def _native_flags(exe: str) -> set[str]:
+    import re
+    import subprocess
+    from pathlib import Path
+
+    path = Path(__file__).resolve().parents[1] / "build" / "native" / exe
+    out = subprocess.run([str(path), "--help"], capture_output=True, text=True, timeout=30).stdout
+    return set(re.findall(r"--[a-z0-9-]+", out))
+
+
+def test_native_control_plane_binaries_take_the_same_flags():
+    """dfs_master / dfs_config_server (C++) accept every flag of the Python shells, which
+    in turn carry the reference's: the launcher starts either with the same command line."""
+    for exe, parser in (("dfs_master", master_parser), ("dfs_config_server", config_parser)):
+        py = {s for a in parser()._actions for s in a.option_strings if s.startswith("--") and s != "--help"}
+        assert _native_flags(exe) == py, exe
