@@ -248,7 +248,7 @@ def main():
             ready = str(base_p / f"master{rank}.ready")
             from rust_hadoop_generated_by_llm_amd.cluster.launcher import role_command
 
-            # the native dfs_master executable (Python shell only with DFS_NATIVE_CONTROL=0)
+            # the C++ dfs_master executable (the Python shell only with DFS_NATIVE_CONTROL=0)
             mp = procs.spawn_raw(role_command("master.server", [
                 "--addr", f"127.0.0.1:{gport}", "--http-port", str(hport),
                 "--storage-dir", str(base_p / f"rank{rank}" / "master"),
