@@ -493,7 +493,8 @@ def main():
                     ("records", "journal_records"), ("sync_rounds", "journal_sync_rounds"),
                     ("materialized_blocks", "materialized_blocks"), ("materialize_pending", "materialize_pending"),
                     ("full_waits", "journal_full_waits"), ("segments", "journal_segs"),
-                    ("segments_retired", "journal_segs_retired"), ("prepare_errors", "journal_prepare_errors"),
+                    ("segments_retired", "journal_segs_retired"), ("segments_filled", "journal_segs_filled"),
+                    ("prepare_errors", "journal_prepare_errors"),
                     ("materialize_errors", "materialize_errors"))} if any(r["cs"].get("journal") for r in allr) else None,
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],

@@ -368,6 +368,8 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["materialize_errors"] = t.materialize_errors;
         d["materialize_last_error"] = t.materialize_last_error;
         d["journal_prepare_errors"] = t.journal_prepare_errors;
+        d["journal_segs_filled"] = t.journal_segs_filled;
+        d["journal_fill_bytes"] = t.journal_fill_bytes;
         d["journal_last_error"] = t.journal_last_error;
         return d;
       })

@@ -226,7 +226,9 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.max_segs = env_int("DFS_JOURNAL_SEGS", 16);
     jc.direct = env_int("DFS_JOURNAL_DIRECT", 0) != 0;
     jc.spares = env_int("DFS_JOURNAL_SPARES", 2);
-    jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 0) != 0;
+    jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 1) != 0;
+    jc.idle_fill_ms = env_int("DFS_JOURNAL_IDLE_FILL_MS", 20);
+    jc.syncers = env_int("DFS_JOURNAL_SYNCERS", 1);
     jc.full_timeout_s = env_int("DFS_JOURNAL_FULL_TIMEOUT_S", 120);
     jc.sync_delay_us = env_int("DFS_JOURNAL_SYNC_DELAY_US", 0);
     jc.sync = cfg_.sync_writes;
@@ -2222,6 +2224,8 @@ StoreStats ChunkStore::stats() {
     s.materialize_errors = mat_errors_;
     s.materialize_last_error = mat_last_error_;
     s.journal_prepare_errors = j.prepare_errors;
+    s.journal_segs_filled = j.filled;
+    s.journal_fill_bytes = j.fill_bytes;
     s.journal_last_error = j.last_error;
   }
   {

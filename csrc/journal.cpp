@@ -122,56 +122,90 @@ BlockJournal::~BlockJournal() {
   if (preparer_.joinable()) preparer_.join();
 }
 
-// Creates segment files up to the cap, zero-filled so appends overwrite written extents,
-// keeping `spares` of them ready for the writers (recycled segments count as ready).
+// Creates every segment file up to the cap (fallocate: metadata only), then, with zero_fill,
+// writes the free ones out while the writers are idle (8 MiB at a time, re-checking between
+// chunks), so first-cycle appends are overwrites of written extents.
 void BlockJournal::prepare_loop() {
+  static const std::vector<uint8_t> zeros(8 << 20, 0);
   std::unique_lock<std::mutex> lk(mu_);
   for (;;) {
-    cv_.wait(lk, [&] {
-      return prep_stop_ || (static_cast<int>(free_.size()) + preparing_ < std::max(1, cfg_.spares) &&
-                            static_cast<int>(segs_.size()) + preparing_ < cfg_.max_segs);
-    });
     if (prep_stop_) return;
-    ++preparing_;
-    const std::string path = cfg_.dir + "/seg-" + std::to_string(next_file_++) + ".log";
-    lk.unlock();
-    errno = 0;
-    SegRef s = open_seg(path, true);
-    bool ok = s != nullptr;
-    if (ok) {
-      if (cfg_.zero_fill) {
-        static const std::vector<uint8_t> zeros(8 << 20, 0);
-        for (uint64_t off = 0; ok && off < s->cap; off += zeros.size())
-          ok = pwrite_all(s->fd, zeros.data(), std::min<uint64_t>(zeros.size(), s->cap - off), off);
+    if (static_cast<int>(segs_.size()) + preparing_ < cfg_.max_segs) {
+      ++preparing_;
+      const std::string path = cfg_.dir + "/seg-" + std::to_string(next_file_++) + ".log";
+      lk.unlock();
+      errno = 0;
+      SegRef s = open_seg(path, true);
+      bool ok = s != nullptr;
+      if (ok) {
+        ok = !cfg_.sync || ::fdatasync(s->fd) == 0;
+        fsync_dir(cfg_.dir);  // the name survives a crash before its first record is acked
       }
-      ok = ok && (!cfg_.sync || ::fdatasync(s->fd) == 0);
-      (void)::posix_fadvise(s->fd, 0, 0, POSIX_FADV_DONTNEED);
-      fsync_dir(cfg_.dir);  // the name survives a crash before its first record is acked
+      const int e = errno;
+      if (!ok) {
+        s.reset();
+        ::unlink(path.c_str());
+      }
+      lk.lock();
+      --preparing_;
+      if (ok) {
+        segs_.push_back(s);
+        free_.push_back(s);
+        st_.prepared++;
+      } else {
+        st_.prepare_errors++;
+        st_.last_error = "segment " + path + ": " + std::strerror(e ? e : EIO);
+        std::fprintf(stderr, "[journal] preparing %s failed: %s (%s)\n", path.c_str(), std::strerror(e ? e : EIO),
+                     describe_locked().c_str());
+        if ((e == ENOSPC || e == EDQUOT) && !segs_.empty()) {
+          // no room for another segment: run with the ones there are (a writer waits for the
+          // materializer to recycle one instead of failing)
+          cfg_.max_segs = std::max<int>(2, static_cast<int>(segs_.size()));
+        } else {
+          // transient (or nothing to fall back on): try again shortly
+          cv_.wait_for(lk, std::chrono::milliseconds(500), [&] { return prep_stop_; });
+        }
+      }
+      cv_.notify_all();
+      continue;
     }
-    const int e = errno;
-    if (!ok) {
-      s.reset();
-      ::unlink(path.c_str());
+    SegRef t;
+    if (cfg_.zero_fill)
+      for (auto& f : free_)
+        if (!f->filled) {
+          t = f;
+          break;
+        }
+    if (!t) {
+      cv_.wait_for(lk, std::chrono::milliseconds(200));
+      continue;
+    }
+    const uint64_t idle_ns = static_cast<uint64_t>(std::max(1, cfg_.idle_fill_ms)) * 1000000ull;
+    const uint64_t since = now_ns() - last_append_ns_;
+    if (last_append_ns_ && since < idle_ns) {  // writers active: wait until they pause
+      cv_.wait_for(lk, std::chrono::nanoseconds(idle_ns - since + 1000000));
+      continue;
+    }
+    t->filling = true;
+    const uint64_t off = t->fill_off, len = std::min<uint64_t>(zeros.size(), t->cap - off);
+    lk.unlock();
+    bool ok = pwrite_all(t->fd, zeros.data(), len, off);
+    const bool last = ok && off + len >= t->cap;
+    if (last) {
+      ok = !cfg_.sync || ::fdatasync(t->fd) == 0;
+      (void)::posix_fadvise(t->fd, 0, 0, POSIX_FADV_DONTNEED);
     }
     lk.lock();
-    --preparing_;
+    t->filling = false;
     if (ok) {
-      segs_.push_back(s);
-      free_.push_back(s);
-      st_.prepared++;
-    } else {
-      st_.prepare_errors++;
-      st_.last_error = "segment " + path + ": " + std::strerror(e ? e : EIO);
-      std::fprintf(stderr, "[journal] preparing %s failed: %s (%s)\n", path.c_str(), std::strerror(e ? e : EIO),
-                   describe_locked().c_str());
-      if ((e == ENOSPC || e == EDQUOT) && !segs_.empty()) {
-        // no room for another segment: run with the ones there are (a writer waits for the
-        // materializer to recycle one instead of failing)
-        cfg_.max_segs = std::max<int>(2, static_cast<int>(segs_.size()));
-      } else {
-        // transient (or nothing to fall back on): try again shortly
-        cv_.wait_for(lk, std::chrono::milliseconds(500), [&] { return prep_stop_; });
+      t->fill_off = off + len;
+      st_.fill_bytes += len;
+      if (last) {
+        t->filled = true;
+        st_.filled++;
       }
+    } else {
+      t->filled = true;  // give up on this one (appends still work on unwritten extents)
     }
     cv_.notify_all();
   }
@@ -323,7 +357,7 @@ void BlockJournal::retire_all() {
   std::lock_guard<std::mutex> g(mu_);
   for (auto& s : segs) {
     s->seq = 0;
-    s->tail = s->done_upto = s->durable_upto = s->live = 0;
+    s->tail = s->done_upto = s->durable_upto = s->syncing_upto = s->live = 0;
     s->done_out.clear();
     s->sealed = false;
     free_.push_back(s);
@@ -348,10 +382,18 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
     // which goes oldest first, would stop at it for good)
     if (!order_.empty() && !order_.back()->sealed) return order_.back();
     SegRef s;
-    if (!free_.empty()) {
-      s = free_.back();
-      free_.pop_back();
-      cv_.notify_all();  // the preparer tops the spares up again
+    {
+      // a written-out segment first; never one the preparer is writing zeros into right now
+      int pick = -1;
+      for (int i = static_cast<int>(free_.size()) - 1; i >= 0; --i) {
+        if (free_[i]->filling) continue;
+        if (pick < 0 || (free_[i]->filled && !free_[pick]->filled)) pick = i;
+      }
+      if (pick >= 0) {
+        s = free_[pick];
+        free_.erase(free_.begin() + pick);
+        cv_.notify_all();  // the preparer may create / fill another
+      }
     }
     if (s) {
       const uint64_t seq = next_seq_++;
@@ -362,14 +404,15 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
         return nullptr;
       }
       s->seq = seq;
-      s->tail = s->done_upto = s->durable_upto = kPage;
+      s->tail = s->done_upto = s->durable_upto = s->syncing_upto = kPage;
       s->done_out.clear();
       s->live = 0;
       s->sealed = false;
       order_.push_back(s);
       return s;
     }
-    const bool full = static_cast<int>(segs_.size()) + preparing_ >= cfg_.max_segs;
+    const bool full = static_cast<int>(segs_.size()) + preparing_ >= cfg_.max_segs &&
+                      std::none_of(free_.begin(), free_.end(), [](const SegRef& f) { return f->filling; });
     if (full) ++st_.full_waits;  // not just waiting for the preparer
     if (std::chrono::steady_clock::now() >= next_report) {
       std::fprintf(stderr, "[journal] writer waiting for a free segment (%s)\n", describe_locked().c_str());
@@ -490,25 +533,33 @@ bool BlockJournal::commit(const JournalRec& r) {
   std::unique_lock<std::mutex> lk(mu_);
   st_.commits++;
   JournalSeg* seg = r.seg.get();
+  const int max_syncers = std::max(1, cfg_.syncers);
   for (;;) {
     if (failed_) return false;
     if (seg->durable_upto >= r.end) return true;
-    if (seg->done_upto < r.end || committing_) {  // an earlier record is in flight / a round runs
+    // wait while an earlier record of the segment is still being written, while a running
+    // round already covers this record, or while every flush slot is busy
+    if (seg->done_upto < r.end || seg->syncing_upto >= r.end || syncers_ >= max_syncers) {
       cv_.wait(lk);
       continue;
     }
-    committing_ = true;
+    ++syncers_;
     std::vector<std::pair<SegRef, uint64_t>> targets;
     for (auto& s : order_)
-      if (s->done_upto > s->durable_upto) targets.emplace_back(s, s->done_upto);
+      if (s->done_upto > std::max(s->durable_upto, s->syncing_upto)) {
+        targets.emplace_back(s, s->done_upto);
+        s->syncing_upto = s->done_upto;
+      }
     lk.unlock();
     bool ok = true;
     if (cfg_.sync_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.sync_delay_us));
     if (cfg_.sync)
       for (auto& t : targets) ok = ::fdatasync(t.first->fd) == 0 && ok;
     lk.lock();
-    committing_ = false;
+    --syncers_;
     st_.sync_rounds++;
+    // a round that finishes flushed everything dirty when it started, i.e. every record
+    // completed before its snapshot, whatever rounds started earlier still run
     if (ok)
       for (auto& t : targets) t.first->durable_upto = std::max(t.first->durable_upto, t.second);
     else
@@ -588,8 +639,9 @@ void BlockJournal::retire_ready() {
   }
   std::lock_guard<std::mutex> g(mu_);
   for (auto& f : retire) {
+    if (f->tail + (8ull << 20) >= f->cap) f->filled = true;  // appends wrote (almost) all of it
     f->seq = 0;
-    f->tail = f->done_upto = f->durable_upto = 0;
+    f->tail = f->done_upto = f->durable_upto = f->syncing_upto = 0;
     f->done_out.clear();
     f->sealed = false;
     free_.push_back(f);
