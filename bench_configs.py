@@ -239,28 +239,181 @@ def config5(a):
         emit(out)
 
 
-def native_load_phase(url: str, a, mpu_bytes: int) -> dict:
-    """The same PUT / GET / Range GET 64 KiB / multipart GET against the gateway from the
-    native load generator (build/native/s3_load: C++ HTTP/1.1 clients, one keep-alive
-    connection per thread), so the numbers describe the gateway, not Python's HTTP stack."""
+def _front_counters(url: str) -> dict:
+    """The native front's request / hand-off counters from the gateway's /metrics: totals
+    plus the hand-offs by reason."""
+    import requests
+
+    out = {"requests": 0, "handoffs": 0, "reasons": {}}
+    try:
+        text = requests.get(f"{url}/metrics", verify=False, timeout=10).text
+    except Exception:  # noqa: BLE001
+        return out
+    for ln in text.splitlines():
+        if ln.startswith("s3_native_requests_total{"):
+            out["requests"] += int(float(ln.rsplit(" ", 1)[1]))
+        elif ln.startswith("s3_native_handoffs_total{"):
+            reason = ln.split('reason="', 1)[1].split('"', 1)[0]
+            v = int(float(ln.rsplit(" ", 1)[1]))
+            out["handoffs"] += v
+            out["reasons"][reason] = v
+    return out
+
+
+def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mpu_key: str = "big.bin") -> dict:
+    """PUT / GET / Range GET 64 KiB / ListObjectsV2 / multipart upload / multipart GET against
+    the gateway from the native load generator (build/native/s3_load: C++ HTTP/1.1 clients,
+    one keep-alive connection per thread), so the numbers describe the gateway, not Python's
+    HTTP stack. Every phase runs for --phase-seconds (>= 10 s windows). With
+    `creds` (secure mode) every request is HTTPS and SigV4-signed with an STS session, PUTs
+    ask for SSE-S3; each phase reports the front's hand-offs to Python during it."""
     exe = ROOT / "build" / "native" / "s3_load"
     if not exe.exists():
         return {"skipped": "build/native/s3_load not built"}
     host, port = url.split("://")[1].rsplit(":", 1)
-    base = [str(exe), "--host", host, "--port", port, "--bucket", "bench", "--conc", str(a.concurrency)]
-    out = {"client": f"s3_load, {a.concurrency} C++ threads, keep-alive"}
+    base = [str(exe), "--host", host, "--port", port, "--bucket", "bench", "--conc", str(a.concurrency),
+            "--seconds", str(a.phase_seconds)]
+    sec = []
+    if creds:
+        sec = ["--tls", "--ak", creds["ak"], "--sk", creds["sk"], "--token", creds["token"]]
+    out = {"client": f"s3_load, {a.concurrency} C++ threads, keep-alive, {a.phase_seconds:g} s per phase"
+                     + (", HTTPS + SigV4 with an STS session token" if creds else "")}
     n = a.count * 10
-    # timed windows of ~0.25-0.5 s: PUT n objects, then GET every object 10 times, 64 KiB ranges 100x
-    for name, extra in (("put", ["--op", "put", "--count", str(n), "--size", str(a.size), "--prefix", "nat"]),
-                        ("get", ["--op", "get", "--count", str(n * 10), "--keys", str(n), "--size", str(a.size),
-                                 "--prefix", "nat", "--verify"]),
-                        ("range_get_64k", ["--op", "range", "--count", str(n * 100), "--keys", str(n),
-                                           "--size", str(a.size), "--prefix", "nat", "--verify"]),
-                        ("multipart_get", ["--op", "get", "--count", "48", "--size", str(mpu_bytes),
-                                           "--key", "big.bin"])):
-        r = subprocess.run(base + extra, capture_output=True, text=True, timeout=300)
-        out[name] = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}
+    phases = (("put", ["--op", "put", "--keys", str(n), "--size", str(a.size), "--prefix", "nat"]
+               + (["--sse"] if creds else [])),
+              ("get", ["--op", "get", "--keys", str(n), "--size", str(a.size), "--prefix", "nat", "--verify"]),
+              ("range_get_64k", ["--op", "range", "--keys", str(n), "--size", str(a.size), "--prefix", "nat",
+                                 "--verify"]),
+              ("list_v2", ["--op", "list", "--prefix", "nat_00"]),
+              ("multipart_upload", ["--op", "mpu", "--size", str(a.mpu_object_mb << 20), "--parts", str(a.mpu_parts),
+                                    "--prefix", "natmpu", "--keys", "1"]),
+              ("multipart_get", ["--op", "get", "--size", str(mpu_bytes), "--key", mpu_key, "--keys", "1"]))
+    for name, extra in phases:
+        before = _front_counters(url)
+        r = subprocess.run(base + sec + extra, capture_output=True, text=True, timeout=a.phase_seconds * 4 + 300)
+        res = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}
+        after = _front_counters(url)
+        res["front_requests"] = after["requests"] - before["requests"]
+        # the closing /metrics scrape is itself a hand-off (unsigned, answered by Python): not counted
+        scrape = 1 if after["reasons"].get("auth", 0) > before["reasons"].get("auth", 0) else 0
+        res["front_handoffs"] = after["handoffs"] - before["handoffs"] - scrape
+        reasons = {k: v - before["reasons"].get(k, 0) for k, v in after["reasons"].items()}
+        reasons["auth"] = reasons.get("auth", 0) - scrape
+        res["front_handoff_reasons"] = {k: v for k, v in reasons.items() if v}
+        out[name] = res
     return out
+
+
+def _sts_session(url: str, role_arn: str) -> dict:
+    """A mock OIDC identity provider (RS256 JWKS, as tests/test_s3_gateway.py's) and one
+    AssumeRoleWithWebIdentity round trip: the STS session the secure load runs under."""
+    import requests
+    import xml.etree.ElementTree as ET
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _rsa  # noqa: E402 - the tests' RSA / JWT helpers (no third-party JWT library here)
+
+    st = _IDP
+    claims = {"sub": "bench", "aud": "dfs-client", "iss": st["url"], "exp": int(time.time()) + 3600,
+              "iat": int(time.time()), "groups": ["bench"]}
+    tok = _rsa.jwt_rs256(claims, st["n"], st["d"], "kid-1")
+    r = requests.get(url + "/", params={"Action": "AssumeRoleWithWebIdentity", "WebIdentityToken": tok,
+                                        "RoleArn": role_arn, "DurationSeconds": "3600"}, verify=False, timeout=30)
+    assert r.status_code == 200, r.text
+    root = ET.fromstring(r.content)
+    ns = {"s": root.tag.split("}")[0].strip("{")} if root.tag.startswith("{") else {}
+
+    def text(tag):
+        el = root.find(f".//s:{tag}", ns) if ns else root.find(f".//{tag}")
+        return el.text
+
+    return {"ak": text("AccessKeyId"), "sk": text("SecretAccessKey"), "token": text("SessionToken")}
+
+
+_IDP: dict = {}
+
+
+def _start_idp() -> None:
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    import _rsa  # noqa: E402
+
+    from rust_hadoop_generated_by_llm_amd.cluster.launcher import free_port
+
+    n, e, d = _rsa.generate(2048, seed=7)
+    port = free_port()
+    _IDP.update(url=f"http://127.0.0.1:{port}", jwk=_rsa.jwk(n, e, "kid-1"), n=n, d=d)
+
+    class H(BaseHTTPRequestHandler):
+        def do_GET(self):  # noqa: N802
+            if self.path == "/.well-known/openid-configuration":
+                body = json.dumps({"issuer": _IDP["url"], "jwks_uri": _IDP["url"] + "/jwks"})
+            elif self.path == "/jwks":
+                body = json.dumps({"keys": [_IDP["jwk"]]})
+            else:
+                self.send_response(404)
+                self.end_headers()
+                return
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.end_headers()
+            self.wfile.write(body.encode())
+
+        def log_message(self, *args):
+            pass
+
+    srv = ThreadingHTTPServer(("127.0.0.1", port), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+
+
+def config5_secure(a):
+    """Config 5 at the reference's production settings (main.rs:263-274 TLS, auth_middleware
+    SigV4 + STS sessions + IAM role policy, sse.rs SSE-S3): the gateway terminates TLS in its
+    native front, every request is signed with an STS session credential whose role policy
+    the front evaluates, every PUT is SSE-S3 encrypted. Reports each phase's hand-offs to Python."""
+    import requests
+    import urllib3
+
+    from rust_hadoop_generated_by_llm_amd.s3.auth import sigv4
+
+    urllib3.disable_warnings()
+    gpus = [a.gpu] if a.gpu >= 0 else None
+    _start_idp()
+    with LocalCluster(n_chunkservers=1, gpus=gpus, hbm_capacity="16G" if gpus else "0") as c:
+        ca, crt, key = c.make_certs()
+        iam = c.base / "iam.json"
+        role = "arn:dfs:iam:::role/bench-role"
+        iam.write_text(json.dumps({"Roles": [{
+            "RoleName": "bench-role", "Arn": role,
+            "AssumeRolePolicyDocument": {"Statement": [{
+                "Effect": "Allow", "Action": "sts:AssumeRoleWithWebIdentity",
+                "Condition": {"ForAnyValue:StringEquals": {"OIDC_ISSUER:groups": ["bench"]}}}]},
+            "Policies": [{"PolicyName": "bench", "PolicyDocument": {"Statement": [
+                {"Effect": "Allow", "Action": ["s3:GetObject", "s3:PutObject", "s3:ListBucket", "s3:HeadObject"],
+                 "Resource": ["arn:dfs:s3:::bench", "arn:dfs:s3:::bench/*"]}]}}]}]}))
+        env = {"LOCAL_CHUNKSERVER": c.cs_addrs[0], "TLS_CERT": crt, "TLS_KEY": key, "S3_REQUIRE_TLS": "true",
+               "S3_AUTH_ENABLED": "true", "S3_ACCESS_KEY": "admin", "S3_SECRET_KEY": "admin-secret",
+               "OIDC_ISSUER_URL": _IDP["url"], "OIDC_CLIENT_ID": "dfs-client",
+               "STS_SIGNING_KEY": "sts-signing-key-0123456789abcdef", "IAM_CONFIG_PATH": str(iam),
+               "SSE_MASTER_KEY": "cd" * 32, "AUDIT_LOG_ENABLED": "true"}
+        url = c.start_s3(env).replace("http://", "https://")
+        host = url.split("://")[1]
+        h = sigv4.sign_headers("PUT", "/bench", [], host, b"", "admin", "admin-secret")
+        assert requests.put(url + "/bench", headers=h, verify=False).status_code == 200
+        creds = _sts_session(url, role)
+        out = {"config": "5-secure", "topology": f"S3 gateway (native front: TLS + SigV4 + STS session + IAM role + "
+                                                 f"SSE-S3 + audit) + 1 master + 1 chunkserver "
+                                                 f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync"}
+        # the multipart object the multipart_get phase reads (uploaded by the same session)
+        exe = ROOT / "build" / "native" / "s3_load"
+        hostn, port = host.rsplit(":", 1)
+        subprocess.run([str(exe), "--host", hostn, "--port", port, "--bucket", "bench", "--conc", "1", "--op", "mpu",
+                        "--count", "1", "--size", str(a.mpu_parts * (8 << 20)), "--parts", str(a.mpu_parts),
+                        "--prefix", "seed", "--keys", "1", "--tls", "--ak", creds["ak"], "--sk", creds["sk"],
+                        "--token", creds["token"]], check=True, capture_output=True, timeout=300)
+        out["native_load"] = native_load_phase(url, a, a.mpu_parts * (8 << 20), creds, mpu_key="seed_mpu_0_0")
+        emit(out)
 
 
 def parquet_phase(url: str, a) -> dict:
@@ -313,9 +466,16 @@ def main():
     p.add_argument("--renames", type=int, default=500)
     p.add_argument("--mpu-parts", type=int, default=8)
     p.add_argument("--parquet-rows", type=int, default=4_000_000)
+    p.add_argument("--phase-seconds", type=float, default=10.0,
+                   help="length of each native load phase (PUT / GET / Range / List / MPU upload / MPU GET)")
+    p.add_argument("--mpu-object-mb", type=int, default=64, help="object size of the multipart-upload phase")
+    p.add_argument("--secure", action="store_true",
+                   help="config5 with TLS + SigV4/STS session + IAM role + SSE-S3 (the reference's production settings)")
     a = p.parse_args()
+    if a.config == "config5" and a.secure:
+        a.config = "config5_secure"
     os.environ.setdefault("DFS_LOG", "warning")
-    {"config1": config1, "config4": config4, "config5": config5}[a.config](a)
+    {"config1": config1, "config4": config4, "config5": config5, "config5_secure": config5_secure}[a.config](a)
 
 
 if __name__ == "__main__":

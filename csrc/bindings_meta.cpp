@@ -909,6 +909,7 @@ void bind_meta(py::module_& m) {
         d["iam_native"] = s.iam_native;
         d["lists"] = s.lists;
         d["mpu_completes"] = s.mpu_completes;
+        d["mpu_initiates"] = s.mpu_initiates;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;
         return d;

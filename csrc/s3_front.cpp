@@ -682,13 +682,17 @@ bool S3Front::handle(Conn* c, Req& r) {
     const std::string* sha = r.get("x-amz-content-sha256");
     if (!(sha && sha->compare(0, 10, "STREAMING-") == 0)) return native_complete(c, r, bucket, key, q);
   }
+  if (r.method == "POST" && q.size() == 1 && q.count("uploads") && q["uploads"].empty() && !r.chunked &&
+      r.content_length <= 0 && !cfg_.metadata_sidecar)
+    return native_initiate(c, r, bucket, key, q);
   const bool part = q.size() == 2 && q.count("partNumber") && q.count("uploadId");
   if (!q.empty() && !part) return proxy(c, r, nullptr, 0, "query");
   const bool is_put = r.method == "PUT", is_get = r.method == "GET", is_head = r.method == "HEAD";
   if (!(is_put || ((is_get || is_head) && !part))) return proxy(c, r, nullptr, 0, "method");
   // SSE-S3: whole objects are encrypted / decrypted here (AES-256-GCM, the gateway's DEK
-  // envelope); multipart parts of an SSE gateway stay on the Python path
-  if (cfg_.sse_enabled && (cfg_.sse_kek.size() != 32 || part)) return proxy(c, r, nullptr, 0, "sse");
+  // envelope). Multipart parts are stored as sent, as the reference's UploadPart does
+  // (handlers.rs encrypts in PutObject and CopyObject only), so they stay native too.
+  if (cfg_.sse_enabled && cfg_.sse_kek.size() != 32) return proxy(c, r, nullptr, 0, "sse");
   if (is_put) {
     if (r.chunked || r.get("x-amz-copy-source") || cfg_.metadata_sidecar) return proxy(c, r, nullptr, 0, "put-form");
     const std::string* sha = r.get("x-amz-content-sha256");
@@ -1441,6 +1445,40 @@ bool parse_complete_body(const std::string& b, std::vector<std::pair<int64_t, st
 // object's ETag md5(concat(md5s))-N, the completion marker written with the layout, and the
 // parts renamed under the object in parallel (each rename one Raft entry, or the master's
 // 2PC when the object's shard differs). Errors before anything changed are Python's.
+// InitiateMultipartUpload (reference handlers.rs:234-262): a fresh upload id and its marker
+// file /.s3_mpu/<id>/.s3keep (the Python gateway's initiate_mpu, same layout).
+bool S3Front::native_initiate(Conn* c, Req& r, const std::string& bucket, const std::string& key,
+                              std::map<std::string, std::string>& q) {
+  TraceRange tr("dfs.s3.mpu_initiate");
+  std::string user = "anonymous", why;
+  Session sess;
+  if (!authorize(r, bucket, q, &user, &sess, &why)) return proxy(c, r, nullptr, 0, why);
+  const std::string uid = uuid4();
+  {
+    int64_t slot = fc_->acquire_slot(1);
+    if (slot < 0) return proxy(c, r, nullptr, 0, "mpu-init");
+    FastClient::Times t;
+    std::string md5, msg;
+    int reps = 0;
+    auto st = fc_->write_slot("/.s3_mpu/" + uid + "/.s3keep", slot, 0, &reps, &msg, &t, r.rid, nullptr, nullptr, &md5);
+    fc_->release(slot);
+    if (st != FastClient::Ok) return proxy(c, r, nullptr, 0, "mpu-init");
+  }
+  const std::string x = "<InitiateMultipartUploadResult>" + xel("Bucket", bucket) + xel("Key", key) +
+                        xel("UploadId", uid) + "</InitiateMultipartUploadResult>";
+  std::string h = "HTTP/1.1 200 OK\r\nContent-Type: application/xml\r\nContent-Length: " + std::to_string(x.size()) +
+                  "\r\n" + (r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+  r.status = 200;
+  count(r, 200);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.mpu_initiates++;
+  }
+  const bool ok = send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(x.data()), x.size());
+  if (cfg_.auth_enabled) audit(c, r, user, 200, sess.role_arn);
+  return ok;
+}
+
 bool S3Front::native_complete(Conn* c, Req& r, const std::string& bucket, const std::string& key,
                               std::map<std::string, std::string>& q) {
   TraceRange tr("dfs.s3.mpu_complete");

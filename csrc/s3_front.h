@@ -78,7 +78,7 @@ struct S3FrontStats {
   // native GET/Range GET phases, summed microseconds: metadata stat, block read into the
   // slot, response send (where a GET's latency goes)
   uint64_t get_stat_us = 0, get_read_us = 0, get_send_us = 0, get_timed = 0;
-  uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0, iam_native = 0, lists = 0, mpu_completes = 0;
+  uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0, iam_native = 0, lists = 0, mpu_completes = 0, mpu_initiates = 0;
 };
 
 class S3Front {
@@ -113,6 +113,9 @@ class S3Front {
   bool authorize(Req& r, const std::string& bucket, const std::map<std::string, std::string>& q, std::string* user,
                  Session* sess, std::string* why);
   bool native_list(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q);
+  // InitiateMultipartUpload: the upload's marker file and the UploadId, no Python.
+  bool native_initiate(Conn* c, Req& r, const std::string& bucket, const std::string& key,
+                       std::map<std::string, std::string>& q);
   bool native_complete(Conn* c, Req& r, const std::string& bucket, const std::string& key,
                        std::map<std::string, std::string>& q);
   int verify_auth(Req& r, std::string* user, Session* sess);  // 1 ok, 0 hand over
