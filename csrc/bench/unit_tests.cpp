@@ -31,6 +31,7 @@
 #include "disk_gate.h"
 #include "extent_alloc.h"
 #include "gf256.h"
+#include "http_lite.h"
 #include "json.h"
 #include "master_core.h"
 #include "raft.h"
@@ -723,6 +724,40 @@ TEST(master_core_native_2pc_rename) {
   r = rename_on(a, "/a/keep", "/a/kept", &code);  // same shard: no 2PC, not blocked
   CHECK(code == MasterCore::OK && r.success && a.visible("/a/kept"));
   CHECK(a.core->txn_stats()["native_aborted"].as_int() == 2);
+}
+
+// ------------------------------------------------------------------------------- HTTP side channel
+// of the native control-plane processes (http_lite.h): keep-alive requests on one server,
+// bodies both ways, 404s, and a client that gives up on a dead port.
+TEST(http_lite_server_and_client_round_trip) {
+  std::atomic<int> calls{0};
+  HttpLiteServer srv("127.0.0.1", 0, [&](const HttpRequest& r) -> HttpResponse {
+    calls++;
+    if (r.path == "/echo" && r.method == "POST") return HttpResponse{200, "application/json", r.body + "!" + r.query};
+    if (r.path == "/health") return HttpResponse{200, "text/plain", "OK"};
+    return HttpResponse{404, "text/plain", "Not Found"};
+  });
+  std::string err;
+  CHECK(srv.start(&err));
+  const std::string base = "http://127.0.0.1:" + std::to_string(srv.port());
+  std::string reply;
+  CHECK(http_request("GET", base + "/health", "", "", 2000, &reply) == 200 && reply == "OK");
+  std::string big(3 << 20, 'x');
+  CHECK(http_request("POST", base + "/echo?q=1", big, "application/json", 5000, &reply) == 200);
+  CHECK(reply.size() == big.size() + 4 && reply.compare(reply.size() - 4, 4, "!q=1") == 0);
+  CHECK(http_request("GET", base + "/nope", "", "", 2000, &reply) == 404);
+  std::vector<std::thread> ts;
+  std::atomic<int> ok{0};
+  for (int t = 0; t < 8; ++t)
+    ts.emplace_back([&] {
+      std::string r;
+      for (int i = 0; i < 20; ++i) ok += http_request("POST", base + "/echo", "p", "text/plain", 2000, &r) == 200 && r == "p!";
+    });
+  for (auto& t : ts) t.join();
+  CHECK(ok == 160 && calls >= 163);
+  srv.stop();
+  std::string e2;
+  CHECK(http_request("GET", base + "/health", "", "", 500, &reply, &e2) == 0 && !e2.empty());
 }
 
 }  // namespace
