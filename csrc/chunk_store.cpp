@@ -893,8 +893,23 @@ bool ChunkStore::device_stage(const uint8_t* data, uint64_t n, const DevExtent& 
     const char* e = std::getenv("DFS_FUSED_WRITE");
     return !(e && e[0] == '0');
   }();
+  // The fused kernel loads the block over PCIe with the waves' own reads: lowest latency for
+  // one write (1 MiB: 39 vs 57 us, profiles/r3_fused_write), but GPU-initiated host reads top
+  // out well below the copy engines once several writes overlap (10 x 1 MiB: 29 vs 46 GB/s,
+  // profiles/r4_roofline). Past this many stagings in flight the SDMA engines take the copy.
+  static const int fused_max = [] {
+    const char* e = std::getenv("DFS_FUSED_WRITE_MAX_INFLIGHT");
+    return e ? std::atoi(e) : 2;
+  }();
+  struct Inflight {
+    std::atomic<int>& c;
+    int v;
+    explicit Inflight(std::atomic<int>& x) : c(x), v(x.fetch_add(1) + 1) {}
+    ~Inflight() { c.fetch_sub(1); }
+  } inflight(staging_);
+  const bool fused_now = fused_ok && (fused_max <= 0 || inflight.v <= fused_max);
   const uint8_t* src_dev =
-      fused_ok && n > kMirrorMax && crc_mfma_enabled() && l->hscratch_dev ? device_view(data, n) : nullptr;
+      fused_now && n > kMirrorMax && crc_mfma_enabled() && l->hscratch_dev ? device_view(data, n) : nullptr;
   if (src_dev && reinterpret_cast<uintptr_t>(src_dev) % 16 == 0) {
     ok = write_copy(l, src_dev, ext.ptr, n, dmeta, hmeta, co, err);
   } else if (h2d_chunked(l, ext.ptr, data, n) && n <= kMirrorMax) {

@@ -401,6 +401,7 @@ class ChunkStore {
   uint8_t* device_view(const void* p, uint64_t n);
   std::atomic<uint64_t> fused_reads_{0};  // K3 fused verify+copy reads
   std::atomic<uint64_t> fused_writes_{0};  // K1/K2 fused copy+checksum writes
+  std::atomic<int> staging_{0};            // device stagings in flight (fused vs SDMA choice)
   std::atomic<uint64_t> sliced_stages_{0};
   bool write_copy(Lane* l, const uint8_t* src_dev, uint8_t* dst, uint64_t n, uint32_t* dmeta, uint8_t* hmeta,
                   CrcOut* out, std::string* err);

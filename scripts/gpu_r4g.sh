@@ -16,4 +16,8 @@ timeout -k 10 500 python bench_configs.py config5 --gpu 0 --phase-seconds 10 --p
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29551 bench.py --gpus 2 --steps 5 --warmup 1 --transport hipipc > $O/bench_n2_hipipc.json 2> $O/bench_n2_hipipc.err && \
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29553 bench.py --gpus 2 --steps 5 --warmup 1 --transport hipipc-spin > $O/bench_n2_spin.json 2> $O/bench_n2_spin.err
+  --master-port 29553 bench.py --gpus 2 --steps 5 --warmup 1 --transport hipipc-spin > $O/bench_n2_spin.json 2> $O/bench_n2_spin.err && \
+timeout -k 10 120 build/native/io_bench --pcie-roofline > $O/pcie_roofline_hybrid.json 2> $O/pcie_roofline_hybrid.err && \
+timeout -k 10 120 build/native/io_bench --pcie-roofline --threads 1 --per 400 > $O/pcie_roofline_hybrid_t1.json 2> $O/pcie_roofline_hybrid_t1.err && \
+DFS_FUSED_WRITE_MAX_INFLIGHT=0 timeout -k 10 120 build/native/io_bench --pcie-roofline --threads 1 --per 400 > $O/pcie_roofline_fused_t1.json 2> $O/pcie_roofline_fused_t1.err && \
+DFS_FUSED_WRITE=0 timeout -k 10 120 build/native/io_bench --pcie-roofline --threads 1 --per 400 > $O/pcie_roofline_sdma_t1.json 2> $O/pcie_roofline_sdma_t1.err
