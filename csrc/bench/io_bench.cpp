@@ -196,6 +196,99 @@ static void journal_case(const std::string& dir, int threads, int per, int mode,
   std::filesystem::remove_all(dir);
 }
 
+// K journals on one volume (K chunkservers of a node), `per_journal` writers each appending
+// 1 MiB records to their journal's pre-written segment. Flush policy:
+//   0 per-journal group commit (each journal's leader fdatasyncs its own file),
+//   1 node-wide combining, fdatasync: one leader at a time flushes every journal with
+//     completed-but-unflushed records (one round covers all K),
+//   2 node-wide combining, syncfs: one leader syncfs()es the filesystem per round.
+// Threads stand in for processes: flush costs are the kernel's and the device's either way.
+static void multi_journal_case(const std::string& dir, int K, int per_journal, int per, int mode, bool first) {
+  std::filesystem::create_directories(dir);
+  const size_t n = 1 << 20, hdr = 4096, rec = n + hdr;
+  const uint64_t total = uint64_t(per_journal) * per * rec;
+  std::vector<int> fds(K);
+  for (int k = 0; k < K; ++k) {
+    std::string f = dir + "/j" + std::to_string(k) + ".seg";
+    int fd = ::open(f.c_str(), O_CREAT | O_RDWR | O_TRUNC, 0644);
+    std::vector<uint8_t> z(8 << 20, 0);
+    for (uint64_t off = 0; off < total; off += z.size())
+      if (::pwrite(fd, z.data(), std::min<uint64_t>(z.size(), total - off), off) < 0) break;
+    ::fsync(fd);
+    fds[k] = fd;
+  }
+  std::vector<std::atomic<uint64_t>> tails(K);
+  for (auto& t : tails) t = 0;
+  // per-journal state (mode 0) or one node-wide state (modes 1, 2): ticket counters
+  struct G {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t issued = 0, done = 0;
+    bool running = false;
+  };
+  std::vector<G> gs(mode == 0 ? K : 1);
+  std::vector<std::atomic<bool>> dirty(K);
+  for (auto& d : dirty) d = false;
+  std::atomic<uint64_t> rounds{0};
+  auto sync_for = [&](int k) {
+    G& g = gs[mode == 0 ? k : 0];
+    std::unique_lock<std::mutex> lk(g.mu);
+    uint64_t ticket = ++g.issued;
+    while (g.done < ticket) {
+      if (g.running) {
+        g.cv.wait(lk);
+        continue;
+      }
+      g.running = true;
+      uint64_t covers = g.issued;
+      lk.unlock();
+      if (mode == 0) {
+        ::fdatasync(fds[k]);
+      } else if (mode == 1) {
+        for (int j = 0; j < K; ++j)
+          if (dirty[j].exchange(false)) ::fdatasync(fds[j]);
+      } else {
+        ::syncfs(fds[0]);
+      }
+      lk.lock();
+      g.running = false;
+      g.done = covers;
+      rounds++;
+      g.cv.notify_all();
+    }
+  };
+  std::vector<Lat> lat(K * per_journal);
+  std::vector<std::thread> ts;
+  std::atomic<int> errors{0};
+  auto t0 = Clock::now();
+  for (int k = 0; k < K; ++k)
+    for (int w = 0; w < per_journal; ++w)
+      ts.emplace_back([&, k, w] {
+        std::vector<uint8_t> buf(rec, static_cast<uint8_t>(k * 16 + w + 1));
+        for (int i = 0; i < per; ++i) {
+          auto a = Clock::now();
+          uint64_t off = tails[k].fetch_add(rec);
+          if (::pwrite(fds[k], buf.data(), rec, off) != static_cast<ssize_t>(rec)) ++errors;
+          dirty[k] = true;
+          sync_for(k);
+          lat[k * per_journal + w].add(secs(a, Clock::now()));
+        }
+      });
+  for (auto& th : ts) th.join();
+  double el = secs(t0, Clock::now());
+  for (int fd : fds) ::close(fd);
+  Lat all;
+  for (auto& l : lat) all.v.insert(all.v.end(), l.v.begin(), l.v.end());
+  static const char* names[] = {"per_journal_fdatasync", "node_wide_fdatasync", "node_wide_syncfs"};
+  std::printf("%s\n    {\"journals\": %d, \"writers_per_journal\": %d, \"flush\": \"%s\", \"records\": %d, \"GBps\": %.2f, "
+              "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"flush_rounds\": %llu, \"errors\": %d}",
+              first ? "" : ",", K, per_journal, names[mode], K * per_journal * per,
+              double(K) * per_journal * per * n / el / 1e9, all.pct(0.5) * 1e3, all.pct(0.99) * 1e3,
+              static_cast<unsigned long long>(rounds.load()), errors.load());
+  std::fflush(stdout);
+  std::filesystem::remove_all(dir);
+}
+
 // PCIe roofline of the bench path: `threads` concurrent 1 MiB transfers
 // host <-> HBM, (a) plain hipMemcpyAsync from pinned memory on one stream per thread (the
 // copy engines' rate) and (b) the store's fused kernels (crc_write_copy_kernel: load over
@@ -284,6 +377,22 @@ static void pcie_roofline(int device, int threads, int per, size_t n) {
 }
 
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--multi-journal") {
+      std::string dir = "/tmp/io_bench_mj";
+      for (int j = 1; j + 1 < argc; ++j)
+        if (std::string(argv[j]) == "--dir") dir = argv[j + 1];
+      std::printf("{\"multi_journal\": [");
+      bool first = true;
+      for (int K : {1, 3, 7})
+        for (int mode = 0; mode < 3; ++mode) {
+          if (K == 1 && mode == 1) continue;  // same as per-journal
+          multi_journal_case(dir, K, K == 1 ? 21 : 3, K == 1 ? 12 : (K == 3 ? 28 : 12), mode, first);
+          first = false;
+        }
+      std::printf("\n]}\n");
+      return 0;
+    }
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--pcie-roofline") {
       int threads = 10, per = 200;

@@ -2241,6 +2241,8 @@ StoreStats ChunkStore::stats() {
     s.journal_prepare_errors = j.prepare_errors;
     s.journal_segs_filled = j.filled;
     s.journal_fill_bytes = j.fill_bytes;
+    s.journal_sync_ns = j.sync_ns;
+    s.journal_commit_ns = j.commit_ns;
     s.journal_last_error = j.last_error;
   }
   {

@@ -530,8 +530,14 @@ void BlockJournal::complete_locked(JournalSeg* s, uint64_t off, uint64_t end) {
 }
 
 bool BlockJournal::commit(const JournalRec& r) {
+  const uint64_t t_in = now_ns();
   std::unique_lock<std::mutex> lk(mu_);
   st_.commits++;
+  struct Acc {  // the caller's wait, whichever way it returns (lock held at every return)
+    JournalStats& st;
+    uint64_t t0;
+    ~Acc() { st.commit_ns += now_ns() - t0; }
+  } acc{st_, t_in};
   JournalSeg* seg = r.seg.get();
   const int max_syncers = std::max(1, cfg_.syncers);
   for (;;) {
@@ -553,11 +559,14 @@ bool BlockJournal::commit(const JournalRec& r) {
     lk.unlock();
     bool ok = true;
     if (cfg_.sync_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.sync_delay_us));
+    const uint64_t t_sync = now_ns();
     if (cfg_.sync)
       for (auto& t : targets) ok = ::fdatasync(t.first->fd) == 0 && ok;
+    const uint64_t d_sync = now_ns() - t_sync;
     lk.lock();
     --syncers_;
     st_.sync_rounds++;
+    st_.sync_ns += d_sync;
     // a round that finishes flushed everything dirty when it started, i.e. every record
     // completed before its snapshot, whatever rounds started earlier still run
     if (ok)

@@ -104,6 +104,7 @@ struct JournalStats {
   uint64_t records = 0, bytes = 0, commits = 0, sync_rounds = 0, tombstones = 0, pads = 0;
   uint64_t segs_total = 0, segs_free = 0, segs_retired = 0, full_waits = 0;
   uint64_t replayed = 0, replay_skipped = 0, prepared = 0, prepare_errors = 0, filled = 0, fill_bytes = 0;
+  uint64_t sync_ns = 0, commit_ns = 0;  // time in fdatasync rounds; time writers spent in commit()
   bool failed = false;
   std::string last_error;  // the last segment preparation / header error, for /stats
 };
