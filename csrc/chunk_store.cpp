@@ -229,6 +229,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 1) != 0;
     jc.idle_fill_ms = env_int("DFS_JOURNAL_IDLE_FILL_MS", 20);
     jc.syncers = env_int("DFS_JOURNAL_SYNCERS", 1);
+    jc.parts = env_int("DFS_JOURNAL_PARTS", 4);
     jc.full_timeout_s = env_int("DFS_JOURNAL_FULL_TIMEOUT_S", 120);
     jc.sync_delay_us = env_int("DFS_JOURNAL_SYNC_DELAY_US", 0);
     jc.sync = cfg_.sync_writes;
@@ -2289,7 +2290,7 @@ bool ChunkStore::debug_corrupt(const std::string& id, uint64_t offset) {
     if (it->second.mirror) (*it->second.mirror)[offset] ^= 0xFF;
     if (it->second.jrec.seg) {
       uint8_t c = 0;
-      const int jfd = it->second.jrec.seg->fd;
+      const int jfd = it->second.jrec.fd();
       const uint64_t at = it->second.jrec.data_off() + offset;
       if (read_all(jfd, &c, 1, at)) {
         c ^= 0xFF;
@@ -2422,7 +2423,7 @@ bool ChunkStore::open_durable(const std::string& id, bool cold, const JournalRec
                               const std::shared_ptr<std::vector<uint8_t>>& jmeta, DurableSrc* s) {
   if (jrec.seg) {
     s->seg = jrec.seg;
-    s->fd = jrec.seg->fd;
+    s->fd = jrec.fd();
     s->base = jrec.data_off();
     s->meta_ok = jmeta != nullptr;
     if (jmeta) {
@@ -2622,7 +2623,7 @@ void ChunkStore::materializer_loop() {
         bytes += j.m.n;
         auto it = index_.find(j.m.id);
         // pinned while its files are written: a rewrite or remove() of the id waits for it
-        j.current = it != index_.end() && it->second.jrec.seg == j.m.rec.seg && it->second.jrec.off == j.m.rec.off;
+        j.current = it != index_.end() && it->second.jrec.seg == j.m.rec.seg && it->second.jrec.part == j.m.rec.part && it->second.jrec.off == j.m.rec.off;
         if (j.current) it->second.pins++;
         batch.push_back(std::move(j));
       }
@@ -2634,7 +2635,7 @@ void ChunkStore::materializer_loop() {
       const std::string dp = data_path(j.m.id, false), mp = meta_path(j.m.id, false);
       j.fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
       j.mfd = j.fd < 0 ? -1 : ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-      j.ok = j.mfd >= 0 && copy_range(j.m.rec.seg->fd, j.m.rec.data_off(), j.fd, j.m.n) &&
+      j.ok = j.mfd >= 0 && copy_range(j.m.rec.fd(), j.m.rec.data_off(), j.fd, j.m.n) &&
              write_all(j.mfd, j.m.meta->data(), j.m.meta->size(), 0);
       if (!j.ok) j.err = errno_str(dp.c_str());
     }
@@ -2754,7 +2755,7 @@ void ChunkStore::replay_journal() {
     }
     const ReplayRecord& r = recs[static_cast<size_t>(kv.second)];
     buf.resize(r.n);
-    if (!read_all(r.seg->fd, buf.data(), r.n, r.data_off) && r.n) {
+    if (!read_all(r.fd(), buf.data(), r.n, r.data_off) && r.n) {
       ++skipped;
       continue;
     }

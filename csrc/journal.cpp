@@ -18,16 +18,18 @@ namespace dfs {
 
 namespace {
 
-constexpr uint32_t kSegMagic = 0x314a5344u;  // "DSJ1"
+constexpr uint32_t kSegMagic = 0x324a5344u;  // "DSJ2" (striped segments)
 constexpr uint32_t kRecMagic = 0x524a5344u;  // "DSJR"
 constexpr uint64_t kPage = 4096;
 constexpr uint64_t kHdr = 512;
 
-struct SegHdr {
+struct PartHdr {
   uint32_t magic;
   uint32_t version;
   uint64_t seq;
   uint64_t cap;
+  uint32_t part;
+  uint32_t nparts;
   uint32_t hdr_crc;
   uint32_t pad;
 };
@@ -35,8 +37,8 @@ struct SegHdr {
 struct RecHdr {
   uint32_t magic;
   uint32_t type;
-  uint64_t seq;
-  uint64_t off;
+  uint64_t seq;   // segment sequence number
+  uint64_t off;   // record offset in its part
   uint64_t rec_len;
   uint64_t hdr_bytes;
   uint64_t n;
@@ -45,7 +47,10 @@ struct RecHdr {
   uint32_t meta_crc;
   uint32_t id_len;
   char id[256];
-  uint8_t pad[kHdr - 320 - 4];
+  uint64_t lsn;   // journal-wide order (replay order across parts)
+  uint32_t part;
+  uint32_t pad0;
+  uint8_t pad[kHdr - 336 - 4];
   uint32_t hdr_crc;
 };
 static_assert(sizeof(RecHdr) == kHdr, "record header is 512 bytes");
@@ -102,13 +107,33 @@ std::string parent_of(const std::string& p) {
 
 }  // namespace
 
-JournalSeg::~JournalSeg() {
+JournalPart::~JournalPart() {
   if (fd >= 0) ::close(fd);
   if (dfd >= 0) ::close(dfd);
 }
 
+bool JournalSeg::complete() const {
+  for (auto& p : parts)
+    if (p->done_upto < p->tail) return false;
+  return true;
+}
+
+bool JournalSeg::filled() const {
+  for (auto& p : parts)
+    if (!p->filled) return false;
+  return true;
+}
+
+bool JournalSeg::filling() const {
+  for (auto& p : parts)
+    if (p->filling) return true;
+  return false;
+}
+
 BlockJournal::BlockJournal(JournalConfig cfg) : cfg_(std::move(cfg)) {
+  cfg_.parts = std::max(1, std::min(cfg_.parts, 64));
   cfg_.seg_bytes = std::max<uint64_t>(align_up(cfg_.seg_bytes, kPage), 4 << 20);
+  part_bytes_ = std::max<uint64_t>(cfg_.seg_bytes / cfg_.parts / kPage * kPage, 1 << 20);
   cfg_.max_segs = std::max(2, cfg_.max_segs);
   if (::mkdir(cfg_.dir.c_str(), 0755) == 0) fsync_dir(parent_of(cfg_.dir));
 }
@@ -122,9 +147,9 @@ BlockJournal::~BlockJournal() {
   if (preparer_.joinable()) preparer_.join();
 }
 
-// Creates every segment file up to the cap (fallocate: metadata only), then, with zero_fill,
-// writes the free ones out while the writers are idle (8 MiB at a time, re-checking between
-// chunks), so first-cycle appends are overwrites of written extents.
+// Creates every segment up to the cap (fallocate: metadata only), then, with zero_fill,
+// writes the parts of the free ones out while the writers are idle (8 MiB at a time,
+// re-checking between chunks), so first-cycle appends are overwrites of written extents.
 void BlockJournal::prepare_loop() {
   static const std::vector<uint8_t> zeros(8 << 20, 0);
   std::unique_lock<std::mutex> lk(mu_);
@@ -132,19 +157,19 @@ void BlockJournal::prepare_loop() {
     if (prep_stop_) return;
     if (static_cast<int>(segs_.size()) + preparing_ < cfg_.max_segs) {
       ++preparing_;
-      const std::string path = cfg_.dir + "/seg-" + std::to_string(next_file_++) + ".log";
+      const int index = next_file_++;
       lk.unlock();
       errno = 0;
-      SegRef s = open_seg(path, true);
+      SegRef s = open_seg(index, true);
       bool ok = s != nullptr;
       if (ok) {
-        ok = !cfg_.sync || ::fdatasync(s->fd) == 0;
-        fsync_dir(cfg_.dir);  // the name survives a crash before its first record is acked
+        for (auto& p : s->parts) ok = ok && (!cfg_.sync || ::fdatasync(p->fd) == 0);
+        fsync_dir(cfg_.dir);  // the names survive a crash before the first record is acked
       }
       const int e = errno;
-      if (!ok) {
+      if (!ok && s) {
+        for (auto& p : s->parts) ::unlink(p->path.c_str());
         s.reset();
-        ::unlink(path.c_str());
       }
       lk.lock();
       --preparing_;
@@ -154,8 +179,8 @@ void BlockJournal::prepare_loop() {
         st_.prepared++;
       } else {
         st_.prepare_errors++;
-        st_.last_error = "segment " + path + ": " + std::strerror(e ? e : EIO);
-        std::fprintf(stderr, "[journal] preparing %s failed: %s (%s)\n", path.c_str(), std::strerror(e ? e : EIO),
+        st_.last_error = "segment " + std::to_string(index) + ": " + std::strerror(e ? e : EIO);
+        std::fprintf(stderr, "[journal] preparing segment %d failed: %s (%s)\n", index, std::strerror(e ? e : EIO),
                      describe_locked().c_str());
         if ((e == ENOSPC || e == EDQUOT) && !segs_.empty()) {
           // no room for another segment: run with the ones there are (a writer waits for the
@@ -169,13 +194,16 @@ void BlockJournal::prepare_loop() {
       cv_.notify_all();
       continue;
     }
-    SegRef t;
+    JournalPart* t = nullptr;
     if (cfg_.zero_fill)
-      for (auto& f : free_)
-        if (!f->filled) {
-          t = f;
-          break;
-        }
+      for (auto& f : free_) {
+        for (auto& p : f->parts)
+          if (!p->filled) {
+            t = p.get();
+            break;
+          }
+        if (t) break;
+      }
     if (!t) {
       cv_.wait_for(lk, std::chrono::milliseconds(200));
       continue;
@@ -213,15 +241,13 @@ void BlockJournal::prepare_loop() {
 
 std::string BlockJournal::describe_locked() const {
   char buf[512];
-  int n = std::snprintf(buf, sizeof(buf), "segments %zu of max %d, in use %zu, free %zu, preparing %d",
-                        segs_.size(), cfg_.max_segs, order_.size(), free_.size(), preparing_);
+  int n = std::snprintf(buf, sizeof(buf), "segments %zu of max %d (%d parts), in use %zu, free %zu, preparing %d",
+                        segs_.size(), cfg_.max_segs, cfg_.parts, order_.size(), free_.size(), preparing_);
   if (!order_.empty() && n > 0 && n < static_cast<int>(sizeof(buf))) {
     const JournalSeg* f = order_.front().get();
-    std::snprintf(buf + n, sizeof(buf) - n,
-                  "; oldest seq %llu: live %llu, sealed %d, completed %llu of %llu, readers %d",
+    std::snprintf(buf + n, sizeof(buf) - n, "; oldest seq %llu: live %llu, sealed %d, complete %d, readers %d",
                   static_cast<unsigned long long>(f->seq), static_cast<unsigned long long>(f->live),
-                  f->sealed ? 1 : 0, static_cast<unsigned long long>(f->done_upto),
-                  static_cast<unsigned long long>(f->tail), f->readers.load());
+                  f->sealed ? 1 : 0, f->complete() ? 1 : 0, f->readers.load());
   }
   return buf;
 }
@@ -233,105 +259,129 @@ uint64_t BlockJournal::rec_bytes_for(uint64_t n, uint64_t nslices) {
 }
 
 bool BlockJournal::fits(uint64_t n, uint64_t nslices) const {
-  return rec_bytes_for(n, nslices) + kPage <= cfg_.seg_bytes;
+  return rec_bytes_for(n, nslices) + kPage <= part_bytes_;
 }
 
-SegRef BlockJournal::open_seg(const std::string& path, bool create) {
+SegRef BlockJournal::open_seg(int index, bool create) {
   auto s = std::make_shared<JournalSeg>();
-  s->path = path;
-  s->fd = ::open(path.c_str(), O_RDWR | O_CLOEXEC | (create ? O_CREAT : 0), 0644);
-  if (s->fd < 0) return nullptr;
-  struct stat st;
-  if (::fstat(s->fd, &st) != 0) return nullptr;
-  if (create || static_cast<uint64_t>(st.st_size) < cfg_.seg_bytes) {
-    // reserve the extent once; later appends are overwrites inside the file
-    if (::fallocate(s->fd, 0, 0, static_cast<off_t>(cfg_.seg_bytes)) != 0 &&
-        ::ftruncate(s->fd, static_cast<off_t>(cfg_.seg_bytes)) != 0)
-      return nullptr;
-    s->cap = cfg_.seg_bytes;
-  } else {
-    s->cap = static_cast<uint64_t>(st.st_size);
+  s->index = index;
+  for (int k = 0; k < cfg_.parts; ++k) {
+    auto p = std::make_unique<JournalPart>();
+    p->path = cfg_.dir + "/seg-" + std::to_string(index) + "." + std::to_string(k) + ".log";
+    p->fd = ::open(p->path.c_str(), O_RDWR | O_CLOEXEC | (create ? O_CREAT : 0), 0644);
+    if (p->fd < 0) return nullptr;
+    struct stat st;
+    if (::fstat(p->fd, &st) != 0) return nullptr;
+    if (create || static_cast<uint64_t>(st.st_size) < part_bytes_) {
+      // reserve the extent once; later appends are overwrites inside the file
+      if (::fallocate(p->fd, 0, 0, static_cast<off_t>(part_bytes_)) != 0 &&
+          ::ftruncate(p->fd, static_cast<off_t>(part_bytes_)) != 0)
+        return nullptr;
+    }
+    p->cap = std::max<uint64_t>(part_bytes_, static_cast<uint64_t>(st.st_size));
+    if (cfg_.direct) p->dfd = ::open(p->path.c_str(), O_RDWR | O_CLOEXEC | O_DIRECT);
+    s->parts.push_back(std::move(p));
   }
-  if (cfg_.direct) s->dfd = ::open(path.c_str(), O_RDWR | O_CLOEXEC | O_DIRECT);
   return s;
 }
 
-bool BlockJournal::write_seg_header(JournalSeg* s, uint64_t seq) {
+bool BlockJournal::write_part_header(JournalPart* p, uint64_t seq, int part, int nparts) {
   alignas(4096) static thread_local uint8_t page[kPage];
   std::memset(page, 0, kPage);
   if (seq) {
-    SegHdr h{};
+    PartHdr h{};
     h.magic = kSegMagic;
-    h.version = 1;
+    h.version = 2;
     h.seq = seq;
-    h.cap = s->cap;
-    h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(SegHdr, hdr_crc));
+    h.cap = p->cap;
+    h.part = static_cast<uint32_t>(part);
+    h.nparts = static_cast<uint32_t>(nparts);
+    h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(PartHdr, hdr_crc));
     std::memcpy(page, &h, sizeof(h));
   }
-  return pwrite_all(s->fd, page, kPage, 0);
+  return pwrite_all(p->fd, page, kPage, 0);
 }
 
 std::vector<ReplayRecord> BlockJournal::recover() {
   std::vector<ReplayRecord> out;
-  std::vector<std::pair<std::string, int>> files;
+  std::map<int, int> indices;  // segment index -> part files seen
   if (DIR* d = ::opendir(cfg_.dir.c_str())) {
     while (dirent* e = ::readdir(d)) {
-      int idx = -1;
-      if (std::sscanf(e->d_name, "seg-%d.log", &idx) == 1 && idx >= 0) files.emplace_back(e->d_name, idx);
+      int idx = -1, k = -1;
+      if (std::sscanf(e->d_name, "seg-%d.%d.log", &idx, &k) == 2 && idx >= 0 && k >= 0) indices[idx]++;
     }
     ::closedir(d);
   }
   std::vector<SegRef> live;
-  for (auto& f : files) {
-    SegRef s = open_seg(cfg_.dir + "/" + f.first, false);
+  for (auto& kv : indices) {
+    next_file_ = std::max(next_file_, kv.first + 1);
+    SegRef s = open_seg(kv.first, false);  // (a segment short of parts gets them created)
     if (!s) continue;
-    next_file_ = std::max(next_file_, f.second + 1);
     segs_.push_back(s);
-    SegHdr h{};
-    if (pread_all(s->fd, reinterpret_cast<uint8_t*>(&h), sizeof(h), 0) && h.magic == kSegMagic && h.seq > 0 &&
-        h.hdr_crc == crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(SegHdr, hdr_crc))) {
-      s->seq = h.seq;
-      next_seq_ = std::max(next_seq_, h.seq + 1);
-      live.push_back(s);
-    } else {
-      free_.push_back(s);
+    // the segment is live if any part holds a valid header; parts whose header does not match
+    // it (never flushed before a crash) hold no acknowledged record
+    uint64_t seq = 0;
+    std::vector<bool> valid(s->parts.size(), false);
+    for (size_t k = 0; k < s->parts.size(); ++k) {
+      PartHdr h{};
+      if (pread_all(s->parts[k]->fd, reinterpret_cast<uint8_t*>(&h), sizeof(h), 0) && h.magic == kSegMagic &&
+          h.seq > 0 && h.part == k && h.nparts == s->parts.size() &&
+          h.hdr_crc == crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(PartHdr, hdr_crc))) {
+        if (seq == 0 || h.seq > seq) {
+          seq = h.seq;
+          std::fill(valid.begin(), valid.end(), false);
+        }
+        if (h.seq == seq) valid[k] = true;
+      }
     }
+    if (seq == 0) {
+      free_.push_back(s);
+      continue;
+    }
+    s->seq = seq;
+    next_seq_ = std::max(next_seq_, seq + 1);
+    for (size_t k = 0; k < s->parts.size(); ++k) {
+      JournalPart* p = s->parts[k].get();
+      uint64_t off = kPage;
+      while (valid[k] && off + kPage <= p->cap) {
+        RecHdr h;
+        if (!pread_all(p->fd, reinterpret_cast<uint8_t*>(&h), kHdr, off)) break;
+        if (h.magic != kRecMagic || h.hdr_crc != crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc)))
+          break;
+        if (h.seq != seq || h.part != k || h.off != off || h.rec_len < kPage || h.rec_len % kPage ||
+            off + h.rec_len > p->cap)
+          break;
+        if (h.type == kJrBlock || h.type == kJrTomb) {
+          ReplayRecord r;
+          r.type = h.type;
+          r.id.assign(h.id, std::min<uint32_t>(h.id_len, sizeof(h.id)));
+          r.lsn = h.lsn;
+          r.seg = s;
+          r.part = static_cast<int>(k);
+          if (h.type == kJrBlock) {
+            if (h.hdr_bytes != hdr_bytes_for(h.nslices) || h.nslices != num_slices(h.n) ||
+                h.hdr_bytes + align_up(h.n, kPage) != h.rec_len)
+              break;
+            r.meta_be.resize(4 * h.nslices);
+            if (h.nslices && !pread_all(p->fd, r.meta_be.data(), r.meta_be.size(), off + kHdr)) break;
+            if (crc32(r.meta_be.data(), r.meta_be.size()) != h.meta_crc) break;
+            r.n = h.n;
+            r.crc = h.crc;
+            r.data_off = off + h.hdr_bytes;
+          }
+          next_lsn_ = std::max(next_lsn_, h.lsn + 1);
+          out.push_back(std::move(r));
+        }
+        off += h.rec_len;
+      }
+      p->tail = p->done_upto = p->durable_upto = p->syncing_upto = off;
+    }
+    s->sealed = true;
+    live.push_back(s);
   }
   std::sort(live.begin(), live.end(), [](const SegRef& a, const SegRef& b) { return a->seq < b->seq; });
-  std::vector<uint8_t> hdr_area;
-  for (auto& s : live) {
-    uint64_t off = kPage;
-    while (off + kPage <= s->cap) {
-      RecHdr h;
-      if (!pread_all(s->fd, reinterpret_cast<uint8_t*>(&h), kHdr, off)) break;
-      if (h.magic != kRecMagic || h.hdr_crc != crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc)))
-        break;
-      if (h.seq != s->seq || h.off != off || h.rec_len < kPage || h.rec_len % kPage || off + h.rec_len > s->cap)
-        break;
-      if (h.type == kJrBlock || h.type == kJrTomb) {
-        ReplayRecord r;
-        r.type = h.type;
-        r.id.assign(h.id, std::min<uint32_t>(h.id_len, sizeof(h.id)));
-        r.seg = s;
-        if (h.type == kJrBlock) {
-          if (h.hdr_bytes != hdr_bytes_for(h.nslices) || h.nslices != num_slices(h.n) ||
-              h.hdr_bytes + align_up(h.n, kPage) != h.rec_len)
-            break;
-          r.meta_be.resize(4 * h.nslices);
-          if (h.nslices && !pread_all(s->fd, r.meta_be.data(), r.meta_be.size(), off + kHdr)) break;
-          if (crc32(r.meta_be.data(), r.meta_be.size()) != h.meta_crc) break;
-          r.n = h.n;
-          r.crc = h.crc;
-          r.data_off = off + h.hdr_bytes;
-        }
-        out.push_back(std::move(r));
-      }
-      off += h.rec_len;
-    }
-    s->tail = s->done_upto = s->durable_upto = off;
-    s->sealed = true;
-    order_.push_back(s);
-  }
+  for (auto& s : live) order_.push_back(s);
+  std::stable_sort(out.begin(), out.end(), [](const ReplayRecord& a, const ReplayRecord& b) { return a.lsn < b.lsn; });
   st_.segs_total = segs_.size();
   preparer_ = std::thread([this] { prepare_loop(); });  // spares get ready while the caller replays
   return out;
@@ -343,31 +393,40 @@ void BlockJournal::note_replay(uint64_t replayed, uint64_t skipped) {
   st_.replay_skipped += skipped;
 }
 
+void BlockJournal::reset_seg_locked(JournalSeg* s) {
+  s->seq = 0;
+  s->live = 0;
+  s->sealed = false;
+  for (auto& p : s->parts) {
+    p->tail = p->done_upto = p->durable_upto = p->syncing_upto = 0;
+    p->done_out.clear();
+  }
+}
+
 void BlockJournal::retire_all() {
   std::vector<SegRef> segs;
   {
     std::lock_guard<std::mutex> g(mu_);
     segs.swap(order_);
   }
-  for (auto& s : segs) {
-    (void)write_seg_header(s.get(), 0);
-    if (cfg_.sync) (void)::fdatasync(s->fd);
-    (void)::posix_fadvise(s->fd, 0, 0, POSIX_FADV_DONTNEED);
-  }
+  for (auto& s : segs)
+    for (size_t k = 0; k < s->parts.size(); ++k) {
+      JournalPart* p = s->parts[k].get();
+      (void)write_part_header(p, 0, static_cast<int>(k), static_cast<int>(s->parts.size()));
+      if (cfg_.sync) (void)::fdatasync(p->fd);
+      (void)::posix_fadvise(p->fd, 0, 0, POSIX_FADV_DONTNEED);
+    }
   std::lock_guard<std::mutex> g(mu_);
   for (auto& s : segs) {
-    s->seq = 0;
-    s->tail = s->done_upto = s->durable_upto = s->syncing_upto = s->live = 0;
-    s->done_out.clear();
-    s->sealed = false;
+    reset_seg_locked(s.get());
     free_.push_back(s);
     ++st_.segs_retired;
   }
   cv_.notify_all();
 }
 
-// Caller holds the lock. Seals nothing; takes a free segment (or creates one while under
-// the cap) and makes it the active one. Waits for the materializer when all are in use.
+// Caller holds the lock. Seals nothing; takes a free segment (or waits for the preparer /
+// the materializer) and makes it the active one.
 SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::string* err) {
   auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(cfg_.full_timeout_s);
   auto next_report = std::chrono::steady_clock::now() + std::chrono::seconds(5);
@@ -386,8 +445,8 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
       // a written-out segment first; never one the preparer is writing zeros into right now
       int pick = -1;
       for (int i = static_cast<int>(free_.size()) - 1; i >= 0; --i) {
-        if (free_[i]->filling) continue;
-        if (pick < 0 || (free_[i]->filled && !free_[pick]->filled)) pick = i;
+        if (free_[i]->filling()) continue;
+        if (pick < 0 || (free_[i]->filled() && !free_[pick]->filled())) pick = i;
       }
       if (pick >= 0) {
         s = free_[pick];
@@ -397,22 +456,25 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
     }
     if (s) {
       const uint64_t seq = next_seq_++;
-      // no flush of its own: the first commit's fdatasync of this segment covers the header
-      if (!write_seg_header(s.get(), seq)) {
-        *err = std::string("journal header: ") + std::strerror(errno);
-        free_.push_back(s);
-        return nullptr;
-      }
+      // no flush of their own: the first commit's fdatasync of each part covers its header
+      for (size_t k = 0; k < s->parts.size(); ++k)
+        if (!write_part_header(s->parts[k].get(), seq, static_cast<int>(k), static_cast<int>(s->parts.size()))) {
+          *err = std::string("journal header: ") + std::strerror(errno);
+          free_.push_back(s);
+          return nullptr;
+        }
       s->seq = seq;
-      s->tail = s->done_upto = s->durable_upto = s->syncing_upto = kPage;
-      s->done_out.clear();
+      for (auto& p : s->parts) {
+        p->tail = p->done_upto = p->durable_upto = p->syncing_upto = kPage;
+        p->done_out.clear();
+      }
       s->live = 0;
       s->sealed = false;
       order_.push_back(s);
       return s;
     }
     const bool full = static_cast<int>(segs_.size()) + preparing_ >= cfg_.max_segs &&
-                      std::none_of(free_.begin(), free_.end(), [](const SegRef& f) { return f->filling; });
+                      std::none_of(free_.begin(), free_.end(), [](const SegRef& f) { return f->filling(); });
     if (full) ++st_.full_waits;  // not just waiting for the preparer
     if (std::chrono::steady_clock::now() >= next_report) {
       std::fprintf(stderr, "[journal] writer waiting for a free segment (%s)\n", describe_locked().c_str());
@@ -427,10 +489,36 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
   }
 }
 
+bool BlockJournal::place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, JournalRec* r, std::string* err) {
+  for (;;) {
+    SegRef s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
+    if (s) {
+      // round robin over the parts, so concurrent appends land in different files
+      const size_t np = s->parts.size();
+      for (size_t i = 0; i < np; ++i) {
+        const size_t k = (rr_ + i) % np;
+        JournalPart* p = s->parts[k].get();
+        if (p->tail + len > p->cap) continue;
+        rr_ = k + 1;
+        r->seg = s;
+        r->part = static_cast<int>(k);
+        r->off = p->tail;
+        r->end = p->tail + len;
+        p->tail += len;
+        return true;
+      }
+      s->sealed = true;  // no part has room
+      cv_.notify_all();
+    }
+    // activate_locked may wait (and drop the lock): whatever it returns is checked again
+    if (!activate_locked(lk, err)) return false;
+  }
+}
+
 bool BlockJournal::reserve(uint64_t n, uint64_t nslices, JournalRec* r, std::string* err) {
   const uint64_t len = rec_bytes_for(n, nslices);
-  if (len + kPage > cfg_.seg_bytes) {
-    *err = "block larger than a journal segment";
+  if (len + kPage > part_bytes_) {
+    *err = "block larger than a journal segment part";
     return false;
   }
   std::unique_lock<std::mutex> lk(mu_);
@@ -438,36 +526,22 @@ bool BlockJournal::reserve(uint64_t n, uint64_t nslices, JournalRec* r, std::str
     *err = "journal failed";
     return false;
   }
-  SegRef s;
-  for (;;) {
-    s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
-    if (s && s->tail + len <= s->cap) break;
-    if (s) {
-      s->sealed = true;
-      cv_.notify_all();
-    }
-    // activate_locked may wait (and drop the lock): whatever it returns is checked again
-    if (!activate_locked(lk, err)) return false;
-  }
-  r->seg = s;
-  r->off = s->tail;
+  if (!place_locked(lk, len, r, err)) return false;
   r->hdr_bytes = hdr_bytes_for(nslices);
-  r->end = s->tail + len;
-  s->tail += len;
-  s->live++;
+  r->seg->live++;
   last_append_ns_ = now_ns();
   return true;
 }
 
 bool BlockJournal::write(const JournalRec& r, uint64_t at, const uint8_t* p, uint64_t len) {
   const uint64_t off = r.data_off() + at;
-  const JournalSeg* s = r.seg.get();
-  if (s->dfd >= 0 && off % kPage == 0 && reinterpret_cast<uintptr_t>(p) % kPage == 0) {
+  const JournalPart* part = r.seg->parts[r.part].get();
+  if (part->dfd >= 0 && off % kPage == 0 && reinterpret_cast<uintptr_t>(p) % kPage == 0) {
     const uint64_t full = len & ~(kPage - 1);
-    if (full && !pwrite_all(s->dfd, p, full, off)) return false;
-    return full == len || pwrite_all(s->fd, p + full, len - full, off + full);
+    if (full && !pwrite_all(part->dfd, p, full, off)) return false;
+    return full == len || pwrite_all(part->fd, p + full, len - full, off + full);
   }
-  return pwrite_all(s->fd, p, len, off);
+  return pwrite_all(part->fd, p, len, off);
 }
 
 bool BlockJournal::finish(const JournalRec& r, const std::string& id, uint64_t n, uint32_t crc,
@@ -486,13 +560,20 @@ bool BlockJournal::finish(const JournalRec& r, const std::string& id, uint64_t n
   h.meta_crc = crc32(meta_be, 4 * nslices);
   h.id_len = static_cast<uint32_t>(std::min<size_t>(id.size(), sizeof(h.id)));
   std::memcpy(h.id, id.data(), h.id_len);
+  h.part = static_cast<uint32_t>(r.part);
+  {
+    // the LSN is taken when the record is finished, after its bytes are written: a later
+    // write of the same id (which can only start after this one returned) gets a larger one
+    std::lock_guard<std::mutex> g(mu_);
+    h.lsn = next_lsn_++;
+  }
   h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc));
   std::memcpy(area.data(), &h, kHdr);
   if (nslices) std::memcpy(area.data() + kHdr, meta_be, 4 * nslices);
-  bool ok = pwrite_all(r.seg->fd, area.data(), area.size(), r.off);
+  bool ok = pwrite_all(r.fd(), area.data(), area.size(), r.off);
   std::lock_guard<std::mutex> g(mu_);
   if (!ok) failed_ = true;  // the prefix cannot advance past a record that is not on disk
-  complete_locked(r.seg.get(), r.off, r.end);
+  complete_locked(r.seg->parts[r.part].get(), r.off, r.end);
   st_.records++;
   st_.bytes += n;
   cv_.notify_all();
@@ -506,29 +587,33 @@ void BlockJournal::abandon(const JournalRec& r) {
   h.seq = r.seg->seq;
   h.off = r.off;
   h.rec_len = r.end - r.off;
+  h.part = static_cast<uint32_t>(r.part);
   h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc));
-  bool ok = pwrite_all(r.seg->fd, reinterpret_cast<const uint8_t*>(&h), kHdr, r.off);
+  bool ok = pwrite_all(r.fd(), reinterpret_cast<const uint8_t*>(&h), kHdr, r.off);
   {
     std::lock_guard<std::mutex> g(mu_);
     if (!ok) failed_ = true;
-    complete_locked(r.seg.get(), r.off, r.end);
+    complete_locked(r.seg->parts[r.part].get(), r.off, r.end);
     st_.pads++;
   }
   materialized(r.seg, 1);
 }
 
-void BlockJournal::complete_locked(JournalSeg* s, uint64_t off, uint64_t end) {
-  if (off != s->done_upto) {
-    s->done_out[off] = end;
+void BlockJournal::complete_locked(JournalPart* p, uint64_t off, uint64_t end) {
+  if (off != p->done_upto) {
+    p->done_out[off] = end;
     return;
   }
-  s->done_upto = end;
-  for (auto it = s->done_out.begin(); it != s->done_out.end() && it->first == s->done_upto;) {
-    s->done_upto = it->second;
-    it = s->done_out.erase(it);
+  p->done_upto = end;
+  for (auto it = p->done_out.begin(); it != p->done_out.end() && it->first == p->done_upto;) {
+    p->done_upto = it->second;
+    it = p->done_out.erase(it);
   }
 }
 
+// Group commit per part: the first writer that finds its record complete but not durable
+// (and no running round covering it) flushes the part for everyone whose record completed
+// before; the others wait for that round. Parts commit independently, side by side.
 bool BlockJournal::commit(const JournalRec& r) {
   const uint64_t t_in = now_ns();
   std::unique_lock<std::mutex> lk(mu_);
@@ -538,41 +623,34 @@ bool BlockJournal::commit(const JournalRec& r) {
     uint64_t t0;
     ~Acc() { st.commit_ns += now_ns() - t0; }
   } acc{st_, t_in};
-  JournalSeg* seg = r.seg.get();
+  JournalPart* part = r.seg->parts[r.part].get();
   const int max_syncers = std::max(1, cfg_.syncers);
   for (;;) {
     if (failed_) return false;
-    if (seg->durable_upto >= r.end) return true;
-    // wait while an earlier record of the segment is still being written, while a running
-    // round already covers this record, or while every flush slot is busy
-    if (seg->done_upto < r.end || seg->syncing_upto >= r.end || syncers_ >= max_syncers) {
+    if (part->durable_upto >= r.end) return true;
+    // wait while an earlier record of the part is still being written, while a running
+    // round already covers this record, or while the part's flush slots are busy
+    if (part->done_upto < r.end || part->syncing_upto >= r.end || part->syncers >= max_syncers) {
       cv_.wait(lk);
       continue;
     }
-    ++syncers_;
-    std::vector<std::pair<SegRef, uint64_t>> targets;
-    for (auto& s : order_)
-      if (s->done_upto > std::max(s->durable_upto, s->syncing_upto)) {
-        targets.emplace_back(s, s->done_upto);
-        s->syncing_upto = s->done_upto;
-      }
+    ++part->syncers;
+    const uint64_t snap = part->done_upto;
+    part->syncing_upto = snap;
     lk.unlock();
     bool ok = true;
     if (cfg_.sync_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(cfg_.sync_delay_us));
     const uint64_t t_sync = now_ns();
-    if (cfg_.sync)
-      for (auto& t : targets) ok = ::fdatasync(t.first->fd) == 0 && ok;
+    if (cfg_.sync) ok = ::fdatasync(part->fd) == 0;
     const uint64_t d_sync = now_ns() - t_sync;
     lk.lock();
-    --syncers_;
+    --part->syncers;
     st_.sync_rounds++;
     st_.sync_ns += d_sync;
     // a round that finishes flushed everything dirty when it started, i.e. every record
     // completed before its snapshot, whatever rounds started earlier still run
-    if (ok)
-      for (auto& t : targets) t.first->durable_upto = std::max(t.first->durable_upto, t.second);
-    else
-      failed_ = true;  // after a failed flush the page state is unknown: refuse further acks
+    if (ok) part->durable_upto = std::max(part->durable_upto, snap);
+    else failed_ = true;  // after a failed flush the page state is unknown: refuse further acks
     cv_.notify_all();
   }
 }
@@ -583,20 +661,7 @@ void BlockJournal::tombstone(const std::string& id) {
   {
     std::unique_lock<std::mutex> lk(mu_);
     if (failed_) return;
-    SegRef s;
-    for (;;) {
-      s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
-      if (s && s->tail + kPage <= s->cap) break;
-      if (s) {
-        s->sealed = true;
-        cv_.notify_all();
-      }
-      if (!activate_locked(lk, &err)) return;
-    }
-    r.seg = s;
-    r.off = s->tail;
-    r.end = s->tail + kPage;
-    s->tail += kPage;
+    if (!place_locked(lk, kPage, &r, &err)) return;
   }
   RecHdr h{};
   h.magic = kRecMagic;
@@ -606,11 +671,16 @@ void BlockJournal::tombstone(const std::string& id) {
   h.rec_len = kPage;
   h.id_len = static_cast<uint32_t>(std::min<size_t>(id.size(), sizeof(h.id)));
   std::memcpy(h.id, id.data(), h.id_len);
+  h.part = static_cast<uint32_t>(r.part);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    h.lsn = next_lsn_++;
+  }
   h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc));
-  bool ok = pwrite_all(r.seg->fd, reinterpret_cast<const uint8_t*>(&h), kHdr, r.off);
+  bool ok = pwrite_all(r.fd(), reinterpret_cast<const uint8_t*>(&h), kHdr, r.off);
   std::lock_guard<std::mutex> g(mu_);
   if (!ok) failed_ = true;
-  complete_locked(r.seg.get(), r.off, r.end);
+  complete_locked(r.seg->parts[r.part].get(), r.off, r.end);
   st_.tombstones++;
   cv_.notify_all();
 }
@@ -633,26 +703,26 @@ void BlockJournal::retire_ready() {
     while (!order_.empty()) {
       SegRef f = order_.front();
       if (!f->sealed && f != order_.back()) f->sealed = true;  // only the newest segment takes appends
-      if (!f->sealed || f->live || f->done_upto < f->tail || f->readers.load() > 0) break;
+      if (!f->sealed || f->live || !f->complete() || f->readers.load() > 0) break;
       retire.push_back(f);
       order_.erase(order_.begin());
     }
   }
   if (retire.empty()) return;
-  // the invalidated header must be durable before the segment is reused: otherwise a crash
+  // the invalidated headers must be durable before the segment is reused: otherwise a crash
   // could replay its old records over newer materialized versions
-  for (auto& f : retire) {
-    (void)write_seg_header(f.get(), 0);
-    if (cfg_.sync) (void)::fdatasync(f->fd);
-    (void)::posix_fadvise(f->fd, 0, 0, POSIX_FADV_DONTNEED);
-  }
+  for (auto& f : retire)
+    for (size_t k = 0; k < f->parts.size(); ++k) {
+      JournalPart* p = f->parts[k].get();
+      (void)write_part_header(p, 0, static_cast<int>(k), static_cast<int>(f->parts.size()));
+      if (cfg_.sync) (void)::fdatasync(p->fd);
+      (void)::posix_fadvise(p->fd, 0, 0, POSIX_FADV_DONTNEED);
+    }
   std::lock_guard<std::mutex> g(mu_);
   for (auto& f : retire) {
-    if (f->tail + (8ull << 20) >= f->cap) f->filled = true;  // appends wrote (almost) all of it
-    f->seq = 0;
-    f->tail = f->done_upto = f->durable_upto = f->syncing_upto = 0;
-    f->done_out.clear();
-    f->sealed = false;
+    for (auto& p : f->parts)
+      if (p->tail + (8ull << 20) >= p->cap) p->filled = true;  // appends wrote (almost) all of it
+    reset_seg_locked(f.get());
     free_.push_back(f);
     ++st_.segs_retired;
   }

@@ -7,20 +7,28 @@
 // with many writers on one volume those flush storms are what bounds the node (VERDICT
 // r3: N=7 on one volume reached 25 % of N=1). Here every durable write of the hot tier
 // appends ONE record — header + big-endian .meta image + the block bytes — to a
-// preallocated segment file, and one fdatasync of the segment covers every record that
-// completed before it started (group commit). A background materializer (chunk_store.cpp)
-// later writes the reference's `<id>` + `<id>.meta` files from the record, makes them
-// durable in batches and retires the segment; on restart, unretired segments are replayed
-// (each record verified against its checksums before it is materialized).
+// preallocated segment, and one fdatasync covers every record that completed before it
+// started (group commit). A background materializer (chunk_store.cpp) later writes the
+// reference's `<id>` + `<id>.meta` files from the record, makes them durable in batches and
+// retires the segment; on restart, unretired segments are replayed (each record verified
+// against its checksums before it is materialized).
 //
-// On-disk layout, `<storage_dir>/.journal/seg-<n>.log`, each `seg_bytes` long:
-//   [segment header, 4 KiB][record][record]...            records never span segments
+// A segment is striped over `parts` files. Buffered writes to one file serialize on its
+// inode lock, so concurrent 1 MiB appends to a single file queue behind each other
+// (measured on the MI355X box's volume: 21 writers on one file p50 2.3 ms, the same load
+// over 3 files p50 0.7 ms, profiles/r4_journal); records go to the parts round robin and
+// each part has its own group commit, so the flushes of different parts run side by side.
+//
+// On-disk layout, `<storage_dir>/.journal/seg-<n>.<k>.log` (part k of segment n), each
+// seg_bytes / parts long:
+//   [part header, 4 KiB][record][record]...            records never span parts
 //   record = [RecHdr 512 B][.meta image, S x u32 BE][pad to 4 KiB][data n B][pad to 4 KiB]
-// A record is valid when its header checksum, segment sequence number and offset match
+// Every record carries a journal-wide sequence number (LSN) that orders replay across parts.
+// A record is valid when its header checksum, segment sequence number, part and offset match
 // and (block records) the data's slice CRCs equal the .meta image. Acknowledgement is
-// prefix-ordered per segment: a record is acked only after every record before it in the
-// segment is complete and flushed, so replay may stop at the first invalid record of a
-// segment without losing anything that was acknowledged.
+// prefix-ordered per part: a record is acked only after every record before it in its part
+// is complete and flushed, so replay may stop at the first invalid record of a part without
+// losing anything that was acknowledged. Segments retire oldest first, whole.
 #pragma once
 
 #include <atomic>
@@ -39,6 +47,7 @@ struct JournalConfig {
   std::string dir;                  // usually <storage_dir>/.journal
   uint64_t seg_bytes = 256ull << 20;
   int max_segs = 16;                // journal capacity = max_segs x seg_bytes
+  int parts = 4;                    // files a segment is striped over
   bool direct = false;              // O_DIRECT appends (aligned sources only; else buffered)
   bool sync = true;                 // fdatasync on commit (false: tests / --no-fsync)
   // Segment files are created (fallocate) ahead of use by a background thread, all of them up
@@ -50,9 +59,9 @@ struct JournalConfig {
   int spares = 2;          // kept ready when segments must be created on demand
   bool zero_fill = true;
   int idle_fill_ms = 20;   // the writers count as idle after this long without an append
-  // Flush rounds that may run at once. 1 = classic group commit (one leader, the others wait
-  // for the next round); more = pipelined: a writer whose record came after a running round's
-  // snapshot starts its own round instead of waiting for that one to finish.
+  // Flush rounds that may run at once per part. 1 = classic group commit (one leader, the
+  // others wait for the next round); more = pipelined: a writer whose record came after a
+  // running round's snapshot starts its own round instead of waiting for that one to finish.
   int syncers = 1;
   int sync_delay_us = 0;   // tests: the commit leader waits this long first (makes rounds shared)
   int full_timeout_s = 120;  // a writer waiting this long for a free segment fails
@@ -60,10 +69,9 @@ struct JournalConfig {
 
 enum JournalRecType : uint32_t { kJrBlock = 1, kJrPad = 2, kJrTomb = 3 };
 
-struct JournalSeg {
-  uint64_t seq = 0;       // 0 = free (header invalidated)
+struct JournalPart {
   int fd = -1;
-  int dfd = -1;           // O_DIRECT descriptor of the same file (-1: none)
+  int dfd = -1;  // O_DIRECT descriptor of the same file (-1: none)
   std::string path;
   uint64_t cap = 0;
   // append state (BlockJournal::mu_)
@@ -72,22 +80,34 @@ struct JournalSeg {
   std::map<uint64_t, uint64_t> done_out;  // completed [off, end) past the prefix
   uint64_t durable_upto = 0;
   uint64_t syncing_upto = 0;              // covered by a flush round in progress
+  int syncers = 0;                        // flush rounds in progress on this part
+  bool filled = false;   // every extent written once (zero fill done, or a full cycle of appends)
+  bool filling = false;  // the preparer is writing zeros into it right now
+  uint64_t fill_off = 0;
+  ~JournalPart();
+};
+
+struct JournalSeg {
+  uint64_t seq = 0;  // 0 = free (headers invalidated)
+  int index = 0;     // n of seg-<n>.<k>.log
+  std::vector<std::unique_ptr<JournalPart>> parts;
   uint64_t live = 0;                      // block records not yet materialized (or dropped)
   bool sealed = false;
-  bool filled = false;   // every extent written once (zero fill done, or a full cycle of appends)
-  bool filling = false;  // the preparer is writing zeros into it right now (not to be activated)
-  uint64_t fill_off = 0;
   std::atomic<int> readers{0};            // reads in progress from this segment (defer retirement)
-  ~JournalSeg();
+  bool complete() const;                  // every part's records are complete
+  bool filled() const;
+  bool filling() const;
 };
 using SegRef = std::shared_ptr<JournalSeg>;
 
 struct JournalRec {
   SegRef seg;
-  uint64_t off = 0;        // record start in the segment
+  int part = 0;
+  uint64_t off = 0;        // record start in the part
   uint64_t hdr_bytes = 0;  // header + .meta area (4 KiB multiple)
   uint64_t end = 0;
   uint64_t data_off() const { return off + hdr_bytes; }
+  int fd() const { return seg->parts[part]->fd; }
 };
 
 struct ReplayRecord {
@@ -95,9 +115,12 @@ struct ReplayRecord {
   std::string id;
   uint64_t n = 0;
   uint32_t crc = 0;
+  uint64_t lsn = 0;
   SegRef seg;
+  int part = 0;
   uint64_t data_off = 0;
   std::vector<uint8_t> meta_be;
+  int fd() const { return seg->parts[part]->fd; }
 };
 
 struct JournalStats {
@@ -115,10 +138,10 @@ class BlockJournal {
   ~BlockJournal();
   BlockJournal(const BlockJournal&) = delete;
 
-  // Recovery: every record of the unretired segments in append order (segments by
-  // sequence number, each up to its first invalid record). Block records carry their
-  // segment so the caller can read and verify the data. Call once, before any append;
-  // then retire_all() once the caller has materialized what it needed.
+  // Recovery: every record of the unretired segments in LSN order (each part up to its
+  // first invalid record). Block records carry their segment and part so the caller can
+  // read and verify the data. Call once, before any append; then retire_all() once the
+  // caller has materialized what it needed.
   std::vector<ReplayRecord> recover();
   void retire_all();
   void note_replay(uint64_t replayed, uint64_t skipped);
@@ -148,25 +171,30 @@ class BlockJournal {
   JournalStats stats();
 
  private:
+  // reserves `len` bytes in a part of the active segment (activating one if needed); lock held
+  bool place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, JournalRec* r, std::string* err);
   SegRef activate_locked(std::unique_lock<std::mutex>& lk, std::string* err);
   std::string describe_locked() const;  // segment accounting, for errors and stall reports
-  bool write_seg_header(JournalSeg* s, uint64_t seq);
-  void complete_locked(JournalSeg* s, uint64_t off, uint64_t end);
-  SegRef open_seg(const std::string& path, bool create);
+  bool write_part_header(JournalPart* p, uint64_t seq, int part, int nparts);
+  void complete_locked(JournalPart* p, uint64_t off, uint64_t end);
+  SegRef open_seg(int index, bool create);
+  void reset_seg_locked(JournalSeg* s);
   void prepare_loop();
   std::thread preparer_;
   bool prep_stop_ = false;
-  int preparing_ = 0;  // segment files being created and filled (mu_)
+  int preparing_ = 0;  // segment files being created (mu_)
 
   JournalConfig cfg_;
+  uint64_t part_bytes_ = 0;
   std::mutex mu_;
   std::condition_variable cv_;
-  std::vector<SegRef> segs_;   // every segment file
+  std::vector<SegRef> segs_;   // every segment
   std::vector<SegRef> order_;  // in use, oldest first (the last one is active)
   std::vector<SegRef> free_;
   uint64_t next_seq_ = 1;
+  uint64_t next_lsn_ = 1;
+  uint64_t rr_ = 0;  // round robin over the active segment's parts
   int next_file_ = 0;
-  int syncers_ = 0;  // flush rounds in progress
   bool failed_ = false;
   uint64_t last_append_ns_ = 0;
   JournalStats st_;
