@@ -387,10 +387,12 @@ def main():
             rbytes += rs.count * rs.avg_size
             wt += ws.total_s
             rt += rs.total_s
+        t_loop = time.perf_counter() - t0
         device_sync()
         barrier()
         device_sync()
         elapsed = time.perf_counter() - t0
+        end_sync_s = elapsed - t_loop
         note(f"{a.steps} timed steps in {elapsed:.3f} s")
         cpu1 = cpu_snapshot()
         host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
@@ -440,7 +442,8 @@ def main():
                       "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count,
                       "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in rc.phase_times.items() if v}}
             rc.close()
-        allr = gather({"elapsed": elapsed, "wl": wl, "rl": rl, "wbytes": wbytes, "rbytes": rbytes, "wt": wt,
+        allr = gather({"elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "wl": wl, "rl": rl, "wbytes": wbytes,
+                       "rbytes": rbytes, "wt": wt,
                        "rt": rt, "cs": stats, "stress": stress, "remote": remote,
                        "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
                        "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
@@ -473,6 +476,10 @@ def main():
                 "write_p99_ms": round(pct(wlat, 99), 3), "read_p50_ms": round(pct(rlat, 50), 3),
                 "read_p95_ms": round(pct(rlat, 95), 3), "read_p99_ms": round(pct(rlat, 99), 3),
                 "write_ops_per_s": round(len(wlat) / wmax, 1),
+                # where the timed region went besides the write and read phases (rank 0): the
+                # closing barrier + device synchronize, and the loop's own bookkeeping
+                "closing_sync_ms_rank0": round(1e3 * allr[0]["end_sync"], 3),
+                "between_phases_ms_per_step_rank0": round(1e3 * (allr[0]["loop"] - allr[0]["wt"] - allr[0]["rt"]) / a.steps, 3),
                 # replica hops between same-node chunkservers: which device transport carried
                 # them (hipipc / rccl / socket), on how many ranks, and how often it fell back
                 "p2p_transport": ",".join(sorted({r["p2p_transport"] for r in allr if r["p2p"]})) or "none",
