@@ -222,8 +222,10 @@ def main():
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     env.setdefault("DFS_LOG", "warning")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if journal_segs:
+    if journal_segs > 0:
         env.setdefault("DFS_JOURNAL_SEGS", str(journal_segs))
+    elif journal_segs < 0:
+        env["DFS_JOURNAL"] = "0"
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE",
               "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID"):
         env.pop(k, None)
@@ -469,6 +471,7 @@ def main():
                            "files_per_gpu_per_step": a.count, "file_size": a.size, "concurrency": a.concurrency,
                            "replication_factor": min(3, n), "durability": a.durability,
                            "store": "cpu" if a.cpu else "hbm",
+                           "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else "journal",
                            "transport": observed_transport(allr, n)},
                 "write_mb_per_s": round(sum(r["wbytes"] for r in allr) / (1 << 20) / wmax, 2),
                 "read_mb_per_s": round(sum(r["rbytes"] for r in allr) / (1 << 20) / rmax, 2),
@@ -621,15 +624,23 @@ def _journal_segments(parent: Path, need: int, n: int) -> int:
     """Segments per chunkserver for the block journal, so that the N journals plus every
     materialized replica of this run fit the volume together (the journal's segments are
     recycled, not freed: at N=8 x RF 3 the run's blocks alone approach a 79 GB volume).
-    0 = leave the chunkservers' default (16 x 256 MiB)."""
-    if os.environ.get("DFS_JOURNAL_SEGS") or os.environ.get("DFS_JOURNAL") == "0":
+    0 = leave the chunkservers' default (16 x 256 MiB); -1 = the journal cannot hold this
+    run's blocks on this volume, so every block would be written twice inside the timed
+    region (journal, then materialized): use the per-file path instead."""
+    if os.environ.get("DFS_JOURNAL_SEGS") or os.environ.get("DFS_JOURNAL"):
         return 0
     try:
         free = shutil.disk_usage(parent).free
     except OSError:
         return 0
     budget = (free - int(need * 1.15) - (2 << 30)) // max(1, n)
-    return int(max(3, min(16, budget // JOURNAL_SEG_BYTES)))
+    per_cs = need // max(1, n)
+    # enough segments to hold the run below the materializer's 70 % mark, two spare
+    want = -(-int(per_cs / 0.7) // JOURNAL_SEG_BYTES) + 2
+    segs = int(max(3, min(64, want, budget // JOURNAL_SEG_BYTES)))
+    if segs * JOURNAL_SEG_BYTES * 0.7 < per_cs:
+        return -1
+    return segs
 
 
 def _make_room(parent: Path, need: int) -> None:

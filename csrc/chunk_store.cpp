@@ -233,7 +233,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.full_timeout_s = env_int("DFS_JOURNAL_FULL_TIMEOUT_S", 120);
     jc.sync_delay_us = env_int("DFS_JOURNAL_SYNC_DELAY_US", 0);
     jc.sync = cfg_.sync_writes;
-    mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 50) / 100.0;
+    mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 70) / 100.0;
     mat_idle_ns_ = static_cast<uint64_t>(env_int("DFS_JOURNAL_IDLE_MS", 100)) * 1000000ull;
     journal_ = std::make_unique<BlockJournal>(jc);
     replay_journal();
