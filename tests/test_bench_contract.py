@@ -76,3 +76,26 @@ def test_bench_never_opens_the_gpu():
     assert "torch.cuda" not in src.replace("(no HIP / torch.cuda call", "")
     assert "native" not in src.split("def main")[1].split("client.benchmark")[0]
     assert src.count("device_sync()") >= 4
+
+
+def test_bench_sizes_the_journal_to_the_volume(monkeypatch):
+    """bench.py gives each chunkserver a journal that holds the run's blocks below the
+    materializer's mark, and falls back to the per-file path where the volume cannot hold
+    such a journal next to the materialized replicas (N=4/8 x RF 3 on a 79 GB volume)."""
+    import shutil
+    import types
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    a = types.SimpleNamespace(steps=20, warmup=5, remote_steps=0, count=100, size=1 << 20)
+    monkeypatch.delenv("DFS_JOURNAL", raising=False)
+    monkeypatch.delenv("DFS_JOURNAL_SEGS", raising=False)
+    monkeypatch.setattr(shutil, "disk_usage", lambda p: types.SimpleNamespace(free=79 << 30))
+    got = {n: bench._journal_segments(Path("/tmp"), bench._bytes_needed(a, n), n) for n in (1, 2, 4, 8)}
+    assert got[1] >= 3 and got[2] >= 3 and got[4] == -1 and got[8] == -1, got
+    for n in (1, 2):
+        per_cs = bench._bytes_needed(a, n) // n
+        assert got[n] * bench.JOURNAL_SEG_BYTES * 0.7 >= per_cs
+    monkeypatch.setenv("DFS_JOURNAL", "0")  # an explicit choice is left alone
+    assert bench._journal_segments(Path("/tmp"), bench._bytes_needed(a, 8), 8) == 0
