@@ -349,14 +349,18 @@ def main():
         # the timed region is bracketed by barrier + device synchronize on both sides; the
         # synchronize runs in the process that owns the GPU and queued all of its work (the
         # chunkserver's /sync: hipDeviceSynchronize), not in this client process
+        sync_log: list = []  # (request ms, hipDeviceSynchronize ms) of each device sync
+
         def device_sync():
             if a.cpu:
                 return
             import urllib.request
 
+            t_req = time.perf_counter()
             r = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/sync", timeout=60).read())
             if not r.get("synchronized"):
                 raise RuntimeError(f"chunkserver device sync failed: {r}")
+            sync_log.append((round(1e3 * (time.perf_counter() - t_req), 3), r.get("sync_ms")))
 
         device_sync()
         barrier()
@@ -444,7 +448,7 @@ def main():
                       "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count,
                       "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in rc.phase_times.items() if v}}
             rc.close()
-        allr = gather({"elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "wl": wl, "rl": rl, "wbytes": wbytes,
+        allr = gather({"elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
                        "rbytes": rbytes, "wt": wt,
                        "rt": rt, "cs": stats, "stress": stress, "remote": remote,
                        "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
@@ -482,6 +486,7 @@ def main():
                 # where the timed region went besides the write and read phases (rank 0): the
                 # closing barrier + device synchronize, and the loop's own bookkeeping
                 "closing_sync_ms_rank0": round(1e3 * allr[0]["end_sync"], 3),
+                "device_syncs_rank0": allr[0]["syncs"],
                 "between_phases_ms_per_step_rank0": round(1e3 * (allr[0]["loop"] - allr[0]["wt"] - allr[0]["rt"]) / a.steps, 3),
                 # replica hops between same-node chunkservers: which device transport carried
                 # them (hipipc / rccl / socket), on how many ranks, and how often it fell back

@@ -287,8 +287,10 @@ class ChunkServerProcess:
                     body, ctype = proc.metrics.render().encode(), "text/plain"
                 elif self.path == "/sync":
                     # device-side completion of everything this process queued on its GPU
+                    t_sync = time.perf_counter()
                     ok = native.device_synchronize(proc.args.gpu)
-                    body, ctype = json.dumps({"synchronized": bool(ok), "gpu": proc.args.gpu}).encode(), \
+                    body, ctype = json.dumps({"synchronized": bool(ok), "gpu": proc.args.gpu,
+                                              "sync_ms": round(1e3 * (time.perf_counter() - t_sync), 3)}).encode(), \
                         "application/json"
                 elif self.path == "/stats":
                     d = dict(proc.store.stats())
