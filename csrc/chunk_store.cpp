@@ -229,7 +229,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 1) != 0;
     jc.idle_fill_ms = env_int("DFS_JOURNAL_IDLE_FILL_MS", 20);
     jc.syncers = env_int("DFS_JOURNAL_SYNCERS", 1);
-    jc.parts = env_int("DFS_JOURNAL_PARTS", 4);
+    jc.parts = env_int("DFS_JOURNAL_PARTS", 8);
     jc.full_timeout_s = env_int("DFS_JOURNAL_FULL_TIMEOUT_S", 120);
     jc.sync_delay_us = env_int("DFS_JOURNAL_SYNC_DELAY_US", 0);
     jc.sync = cfg_.sync_writes;

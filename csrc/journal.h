@@ -47,7 +47,7 @@ struct JournalConfig {
   std::string dir;                  // usually <storage_dir>/.journal
   uint64_t seg_bytes = 256ull << 20;
   int max_segs = 16;                // journal capacity = max_segs x seg_bytes
-  int parts = 4;                    // files a segment is striped over
+  int parts = 8;                    // files a segment is striped over
   bool direct = false;              // O_DIRECT appends (aligned sources only; else buffered)
   bool sync = true;                 // fdatasync on commit (false: tests / --no-fsync)
   // Segment files are created (fallocate) ahead of use by a background thread, all of them up

@@ -12,6 +12,7 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 # per-file path, which the tests exercise as well
 os.environ.setdefault("DFS_JOURNAL_SEG_MB", "32")
 os.environ.setdefault("DFS_JOURNAL_ZERO_FILL", "0")
+os.environ.setdefault("DFS_JOURNAL_PARTS", "4")  # 8 MiB part files at test scale
 
 
 def pytest_configure(config):
