@@ -357,7 +357,8 @@ def main():
             import urllib.request
 
             t_req = time.perf_counter()
-            r = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/sync", timeout=60).read())
+            port = cs_info.get("sync_port") or chttp  # the chunkserver's native /sync listener
+            r = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{port}/sync", timeout=60).read())
             if not r.get("synchronized"):
                 raise RuntimeError(f"chunkserver device sync failed: {r}")
             sync_log.append((round(1e3 * (time.perf_counter() - t_req), 3), r.get("sync_ms")))

@@ -6,6 +6,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <chrono>
+
 #include "chunk_store.h"
 #include "crc32.h"
 #include "crypto.h"
@@ -17,6 +19,7 @@
 #include "cs_agent.h"
 #include "cs_grpc.h"
 #include "grpc_server.h"
+#include "http_lite.h"
 #include "sigv4.h"
 #include "tls.h"
 #include "wal.h"
@@ -138,6 +141,38 @@ PYBIND11_MODULE(_dfs_native, m) {
   m.def("device_count", &device_count);
   // hipDeviceSynchronize on `device` in the calling process (the chunkserver owns its GPU:
   // the benchmark brackets its timed region with this, through the server's /sync endpoint)
+  // The same device synchronize on a native HTTP listener of its own (GET /sync): the
+  // benchmark's timed region is bracketed by it, and no Python thread (GIL, thread start)
+  // sits between the request and hipDeviceSynchronize.
+  struct SyncServer {
+    std::unique_ptr<HttpLiteServer> srv;
+  };
+  py::class_<SyncServer>(m, "DeviceSyncServer")
+      .def(py::init([](const std::string& host, int port, int device) {
+             auto s = std::make_unique<SyncServer>();
+             s->srv = std::make_unique<HttpLiteServer>(host, port, [device](const HttpRequest& r) -> HttpResponse {
+               if (r.path != "/sync") return HttpResponse{404, "text/plain", "Not Found"};
+               const auto t0 = std::chrono::steady_clock::now();
+               bool ok = device < 0 || (hipSetDevice(device) == hipSuccess && hipDeviceSynchronize() == hipSuccess);
+               const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+               char body[160];
+               std::snprintf(body, sizeof(body), "{\"synchronized\": %s, \"gpu\": %d, \"sync_ms\": %.3f, \"native\": true}",
+                             ok ? "true" : "false", device, ms);
+               return HttpResponse{200, "application/json", body};
+             });
+             return s;
+           }),
+           py::arg("host"), py::arg("port"), py::arg("device"))
+      .def("start", [](SyncServer& s) {
+        std::string err;
+        bool ok = s.srv->start(&err);
+        return py::make_tuple(ok, err);
+      })
+      .def_property_readonly("port", [](SyncServer& s) { return s.srv->port(); })
+      .def("stop", [](SyncServer& s) {
+        py::gil_scoped_release r;
+        s.srv->stop();
+      });
   m.def("device_synchronize", [](int device) {
     py::gil_scoped_release r;
     if (device < 0) return true;

@@ -403,6 +403,13 @@ class ChunkServerProcess:
         server = self._start_grpc(a, creds)
         http = self._http()
         threading.Thread(target=http.serve_forever, daemon=True, name="cs-http").start()
+        sync_port = 0
+        try:  # GET /sync served natively (the benchmark's device-sync bracket, no Python on the path)
+            self._sync_srv = native.DeviceSyncServer("127.0.0.1", 0, a.gpu)
+            ok, _err = self._sync_srv.start()
+            sync_port = self._sync_srv.port if ok else 0
+        except AttributeError:
+            self._sync_srv = None
         if self.agent is not None:
             self.agent.start()
         else:
@@ -413,7 +420,7 @@ class ChunkServerProcess:
             with open(ready, "w") as f:
                 json.dump({"addr": a.addr, "gpu": a.gpu, "rccl": self.rccl is not None,
                            "transport": self.rccl.transport if self.rccl is not None else "grpc",
-                           "pairs_up": self.repl_pairs_up}, f)
+                           "pairs_up": self.repl_pairs_up, "sync_port": sync_port}, f)
         for sig in (signal.SIGTERM, signal.SIGINT):
             signal.signal(sig, lambda *_: self._stop.set())
         log.info("chunkserver %s serving (gpu=%d, durability=%s)", self.advertise, a.gpu, a.durability)
@@ -426,6 +433,8 @@ class ChunkServerProcess:
         if self.native_grpc is not None:
             self.native_grpc.stop()
         http.shutdown()
+        if getattr(self, "_sync_srv", None) is not None:
+            self._sync_srv.stop()
         if self.rccl is not None:
             self.rccl.stop()
         if self.fastpath is not None:
