@@ -294,11 +294,14 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
         res = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}
         after = _front_counters(url)
         res["front_requests"] = after["requests"] - before["requests"]
-        # the closing /metrics scrape is itself a hand-off (unsigned, answered by Python): not counted
-        scrape = 1 if after["reasons"].get("auth", 0) > before["reasons"].get("auth", 0) else 0
-        res["front_handoffs"] = after["handoffs"] - before["handoffs"] - scrape
+        # the closing /metrics scrape is itself one hand-off (answered by Python; its reason is
+        # "auth" on an authenticating gateway, "list-empty" on an open one): not counted
         reasons = {k: v - before["reasons"].get(k, 0) for k, v in after["reasons"].items()}
-        reasons["auth"] = reasons.get("auth", 0) - scrape
+        for why in ("auth", "list-empty"):
+            if reasons.get(why, 0) > 0:
+                reasons[why] -= 1
+                break
+        res["front_handoffs"] = sum(reasons.values())
         res["front_handoff_reasons"] = {k: v for k, v in reasons.items() if v}
         out[name] = res
     return out
