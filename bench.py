@@ -512,7 +512,7 @@ def main():
                     ("segments_retired", "journal_segs_retired"), ("segments_filled", "journal_segs_filled"),
                     ("prepare_errors", "journal_prepare_errors"),
                     ("materialize_errors", "materialize_errors"), ("sync_ns", "journal_sync_ns"),
-                    ("commit_ns", "journal_commit_ns"))} if any(r["cs"].get("journal") for r in allr) else None,
+                    ("commit_ns", "journal_commit_ns"), ("bypassed", "journal_bypassed"))} if any(r["cs"].get("journal") for r in allr) else None,
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],
             }

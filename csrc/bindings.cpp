@@ -406,6 +406,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["journal_segs_filled"] = t.journal_segs_filled;
         d["journal_fill_bytes"] = t.journal_fill_bytes;
         d["journal_sync_ns"] = t.journal_sync_ns;
+        d["journal_bypassed"] = t.journal_bypassed;
         d["journal_commit_ns"] = t.journal_commit_ns;
         d["journal_last_error"] = t.journal_last_error;
         return d;

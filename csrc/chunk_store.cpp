@@ -234,6 +234,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.sync_delay_us = env_int("DFS_JOURNAL_SYNC_DELAY_US", 0);
     jc.sync = cfg_.sync_writes;
     mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 70) / 100.0;
+    journal_bypass_ = env_int("DFS_JOURNAL_BYPASS", 1) != 0;  // 0: writers wait for the materializer
     mat_idle_ns_ = static_cast<uint64_t>(env_int("DFS_JOURNAL_IDLE_MS", 100)) * 1000000ull;
     journal_ = std::make_unique<BlockJournal>(jc);
     replay_journal();
@@ -948,7 +949,7 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
     return res;
   }
   bool sync_now = durable_now && cfg_.durability == Durability::NvmeSync;
-  if (sync_now && journal_ && journal_->fits(n, num_slices(n))) return stage_journal(id, data, n, expected_crc, ext);
+  if (sync_now && journal_takes(n, num_slices(n))) return stage_journal(id, data, n, expected_crc, ext);
   // nvme-sync: the data file (the slow part: page-cache write + device flush) is written
   // and fdatasync'ed on a helper thread WHILE the GPU stages and checksums the block; the
   // .meta (known only after the CRC kernel) follows. A checksum mismatch removes the file.
@@ -1198,7 +1199,7 @@ bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64
   bool ok, jok = false;
   JournalRec jr;
   const bool from_host = host_data && n == size;
-  if (journal_ && journal_->fits(size, meta->size() / 4)) {
+  if (journal_takes(size, meta->size() / 4)) {
     ok = jok = journal_block(id, from_host ? host_data : nullptr, from_host ? nullptr : d, size, crc, *meta, &jr, err);
   } else if (from_host) {
     ok = persist(id, false, host_data, size, meta->data(), meta->size() / 4, err);
@@ -1289,7 +1290,7 @@ WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, u
   std::string err;
   JournalRec jr;
   std::shared_ptr<std::vector<uint8_t>> jmeta;
-  const bool jok = journal_ && journal_->fits(n, S);
+  const bool jok = journal_takes(n, S);
   if (jok) {
     jmeta = std::make_shared<std::vector<uint8_t>>(reinterpret_cast<const uint8_t*>(sl.data()),
                                                    reinterpret_cast<const uint8_t*>(sl.data()) + S * 4);
@@ -1725,7 +1726,7 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
   }
   bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
   JournalRec jr;
-  const bool jok = sync_now && journal_ && journal_->fits(n, S);
+  const bool jok = sync_now && journal_takes(n, S);
   if (jok ? !journal_block(id, nullptr, ext.ptr, n, co.block_crc, *meta, &jr, &err)
           : sync_now && !persist_from_device(id, ext.ptr, n, meta->data(), S, &err)) {
     release(ext);
@@ -1802,7 +1803,7 @@ WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint3
   std::string err;
   bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
   JournalRec jr;
-  const bool jok = sync_now && journal_ && journal_->fits(n, S);
+  const bool jok = sync_now && journal_takes(n, S);
   if (jok ? !journal_block(id, nullptr, rv->ext.ptr, n, crc, *meta, &jr, &err)
           : sync_now && !persist_from_device(id, rv->ext.ptr, n, meta->data(), S, &err)) {
     release(rv->ext);
@@ -2243,6 +2244,7 @@ StoreStats ChunkStore::stats() {
     s.journal_segs_filled = j.filled;
     s.journal_fill_bytes = j.fill_bytes;
     s.journal_sync_ns = j.sync_ns;
+    s.journal_bypassed = bypassed_.load();
     s.journal_commit_ns = j.commit_ns;
     s.journal_last_error = j.last_error;
   }
@@ -2540,6 +2542,17 @@ WriteResult ChunkStore::stage_journal(const std::string& id, const uint8_t* data
   if (n <= kMirrorMax) set_mirror(id, data, n, *meta);
   res.ok = true;
   return res;
+}
+
+// A durable write goes to the journal while the journal has room below the materializer's
+// mark. Past it the materializer is already writing every journaled block a second time, so a
+// write through the journal would cost the volume twice; it takes the per-file path instead
+// (written once), and the journal takes writes again once the materializer has caught up.
+bool ChunkStore::journal_takes(uint64_t n, uint64_t nslices) {
+  if (!journal_ || !journal_->fits(n, nslices)) return false;
+  if (!journal_bypass_ || journal_->pressure() < mat_pressure_) return true;
+  bypassed_++;
+  return false;
 }
 
 void ChunkStore::enqueue_materialize_locked(const std::string& id, const Block& b) {

@@ -104,7 +104,7 @@ struct StoreStats {
   uint64_t journal_segs_retired = 0, journal_replayed = 0, journal_replay_skipped = 0;
   uint64_t materialized_blocks = 0, materialized_bytes = 0, materialize_pending = 0, materialize_batches = 0;
   uint64_t materialize_errors = 0, journal_prepare_errors = 0, journal_segs_filled = 0, journal_fill_bytes = 0;
-  uint64_t journal_sync_ns = 0, journal_commit_ns = 0;
+  uint64_t journal_sync_ns = 0, journal_commit_ns = 0, journal_bypassed = 0;
   bool journal_failed = false;
   std::string journal_last_error, materialize_last_error;
 };
@@ -338,6 +338,9 @@ class ChunkStore {
   bool journal_block(const std::string& id, const uint8_t* host, const uint8_t* dev, uint64_t n, uint32_t crc,
                      const std::vector<uint8_t>& meta_be, JournalRec* out, std::string* err);
   void enqueue_materialize_locked(const std::string& id, const Block& b);
+  bool journal_takes(uint64_t n, uint64_t nslices);
+  std::atomic<uint64_t> bypassed_{0};  // durable writes sent past a journal at its materialize mark
+  bool journal_bypass_ = true;
   void materializer_loop();
   bool materialize_due();
   void replay_journal();

@@ -147,6 +147,7 @@ def test_small_journal_recycles_segments_under_pressure(native, tmp_path, monkey
     monkeypatch.setenv("DFS_JOURNAL_SEG_MB", "8")
     monkeypatch.setenv("DFS_JOURNAL_PARTS", "2")
     monkeypatch.setenv("DFS_JOURNAL_SEGS", "3")
+    monkeypatch.setenv("DFS_JOURNAL_BYPASS", "0")  # writers wait for recycled segments
     s = open_store(native, tmp_path)
     vals = {}
     for i in range(30):
@@ -176,6 +177,7 @@ def test_concurrent_writers_recycle_a_small_journal(native, tmp_path, monkeypatc
     monkeypatch.setenv("DFS_JOURNAL_SEGS", "3")
     monkeypatch.setenv("DFS_JOURNAL_SPARES", "2")
     monkeypatch.setenv("DFS_JOURNAL_FULL_TIMEOUT_S", "20")
+    monkeypatch.setenv("DFS_JOURNAL_BYPASS", "0")
     s = open_store(native, tmp_path)
     vals = {f"c{i}": os.urandom((1 << 20) - 4096 * (i % 7)) for i in range(120)}
     with ThreadPoolExecutor(12) as ex:
@@ -186,6 +188,38 @@ def test_concurrent_writers_recycle_a_small_journal(native, tmp_path, monkeypatc
     assert st["journal_segs"] <= 3 and st["journal_segs_retired"] >= 15 and st["materialized_blocks"] == 120
     for k, v in vals.items():
         assert s.read(k, 0, 0)[2] == v
+
+
+def test_writes_past_the_materialize_mark_take_the_per_file_path(native, tmp_path):
+    """Once the journal is at the materializer's mark, every journaled block will be written a
+    second time; new durable writes then go straight to `<id>` + `<id>.meta` (written once)
+    until the materializer has caught up."""
+    import subprocess as sp
+
+    code = f"""
+import os, zlib
+from rust_hadoop_generated_by_llm_amd import native
+s = native.lib.ChunkStore({str(tmp_path / 'hot')!r}, "", -1, 0, 0, 100, 1, 1, True, journal=1)
+s.debug_pause_materializer(True)
+vals = {{f"b{{i}}": os.urandom((1 << 20) - 512 * i) for i in range(24)}}
+for k, v in vals.items():
+    assert s.write(k, v, zlib.crc32(v))[0]
+st = s.stats()
+assert st["journal_bypassed"] > 0, st
+assert st["journal_records"] + st["journal_bypassed"] == 24, st
+# bypassed writes are files already; journaled ones are not until materialized
+on_disk = [k for k in vals if os.path.exists({str(tmp_path / 'hot')!r} + "/" + k)]
+assert len(on_disk) == st["journal_bypassed"], (on_disk, st)
+for k, v in vals.items():
+    assert s.read(k, 0, 0)[2] == v
+s.debug_pause_materializer(False)
+s.materialize()
+assert all(os.path.exists({str(tmp_path / 'hot')!r} + "/" + k) for k in vals)
+print("ok")
+"""
+    env = dict(os.environ, PYTHONPATH=str(ROOT), DFS_JOURNAL_SEG_MB="8", DFS_JOURNAL_PARTS="2", DFS_JOURNAL_SEGS="4")
+    r = sp.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
 def test_concurrent_writers_share_group_commits(native, tmp_path, monkeypatch):
