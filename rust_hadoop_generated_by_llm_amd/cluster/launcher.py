@@ -281,8 +281,32 @@ class LocalCluster:
             self.cs_http.append(f"http://127.0.0.1:{http}")
         self._wait_ready(cprocs)
         self.wait_registered()
+        if self.n_cs > 1 and (self.p2p in ("socket", "hipipc", "hipipc-spin") or (self.gpus is not None and self.rccl)):
+            self.wait_replication_mesh()
         if self.shards > 1:
             self.wait_shard_maps()
+
+    def wait_replication_mesh(self, timeout: float = 60.0) -> None:
+        """Block until every chunkserver reports every peer pair up. A chunkserver writes its
+        ready file once ITS side of each pair is connected; the peer's side of the last pair can
+        still be finishing then, so /stats may briefly show one pair short."""
+        import urllib.request
+
+        want = self.n_cs - 1
+        deadline = time.time() + timeout
+        seen: list = []
+        while time.time() < deadline:
+            seen = []
+            for http in self.cs_http:
+                try:
+                    with urllib.request.urlopen(http + "/stats", timeout=2.0) as r:
+                        seen.append(json.loads(r.read()).get("repl_pairs_up"))
+                except OSError:
+                    seen.append(None)
+            if all(v == want for v in seen):
+                return
+            time.sleep(0.2)
+        raise TimeoutError(f"replication mesh not up after {timeout}s: pairs per chunkserver {seen}")
 
     def wait_shard_maps(self, timeout: float = 30.0) -> None:
         """Block until every master's shard map lists every shard (maps propagate from the

@@ -39,7 +39,10 @@ def eccluster(has_gpu):
         pytest.fail("GPU test selected but no HIP device is visible")
     with LocalCluster(gpus=[0] * 6, p2p="hipipc", fsync=True, hbm_capacity="3G",
                       env={"DFS_DEBUG_ENDPOINTS": "1"}) as c:
-        assert summed(c, "repl_pairs_up") == 30
+        deadline = time.time() + 60  # the 30 pairs come up in the background after start
+        while summed(c, "repl_pairs_up") != 30:
+            assert time.time() < deadline, [stats(u).get("repl_pairs_up") for u in c.cs_http]
+            time.sleep(0.2)
         yield c
 
 
