@@ -383,6 +383,7 @@ def main():
 
         client.phase_times = {}
         cpu0 = cpu_snapshot()
+        cg0 = cgroup_cpu()
         t0 = time.perf_counter()
         wl, rl, wbytes, rbytes = [], [], 0, 0
         wt = rt = 0.0
@@ -403,6 +404,7 @@ def main():
         note(f"{a.steps} timed steps in {elapsed:.3f} s")
         cpu1 = cpu_snapshot()
         host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
+        job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), elapsed)
 
         def cs_stats() -> dict:
             try:
@@ -453,7 +455,7 @@ def main():
                        "rbytes": rbytes, "wt": wt,
                        "rt": rt, "cs": stats, "stress": stress, "remote": remote,
                        "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
-                       "cpu": host_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
+                       "cpu": host_cpu, "job_cpu": job_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                    for k, v in (client.phase_times or {}).items() if v}})
         if rank == 0:
             tmax = max(r["elapsed"] for r in allr)
@@ -514,6 +516,9 @@ def main():
                     ("materialize_errors", "materialize_errors"), ("sync_ns", "journal_sync_ns"),
                     ("commit_ns", "journal_commit_ns"), ("bypassed", "journal_bypassed"))} if any(r["cs"].get("journal") for r in allr) else None,
                 "host_cpu_util_rank0": allr[0]["cpu"],
+                # the whole job's CPU over the timed region, from the cgroup every rank shares
+                # (cores used, the quota, and time the quota throttled it); null without cgroup
+                "host_cpu_job": allr[0]["job_cpu"],
                 "client_phase_p50_ms_rank0": allr[0]["phases"],
             }
             if a.remote_steps > 0:
@@ -597,6 +602,49 @@ def visible_gpus() -> int:
         if v is not None:
             n = min(n, len([x for x in v.split(",") if x.strip()]))
     return n
+
+
+def cgroup_cpu() -> dict | None:
+    """CPU counters of this process's cgroup (v2 `cpu.stat` / `cpu.max`, else v1 cpuacct + cpu):
+    usage and throttling cover every process of the job, chunkservers and masters included."""
+    snap = {"t": time.perf_counter(), "cpus": len(os.sched_getaffinity(0))}
+
+    def read(path):
+        with open(path) as f:
+            return f.read()
+
+    try:  # cgroup v2
+        rel = next((ln.split(":", 2)[2].strip() for ln in read("/proc/self/cgroup").splitlines()
+                    if ln.startswith("0::")), "/")
+        for base in ("/sys/fs/cgroup" + rel.rstrip("/"), "/sys/fs/cgroup"):
+            if os.path.exists(base + "/cpu.stat") and os.path.exists(base + "/cpu.max"):
+                st = dict(ln.split() for ln in read(base + "/cpu.stat").splitlines() if len(ln.split()) == 2)
+                q, per = read(base + "/cpu.max").split()
+                snap.update(usage_s=int(st["usage_usec"]) / 1e6, throttled_s=int(st.get("throttled_usec", 0)) / 1e6,
+                            nr_throttled=int(st.get("nr_throttled", 0)),
+                            quota_cores=None if q == "max" else round(int(q) / int(per), 2))
+                return snap
+        # cgroup v1: cpuacct usage (ns), cpu.stat throttled_time (ns), cfs quota
+        snap["usage_s"] = int(read("/sys/fs/cgroup/cpuacct/cpuacct.usage")) / 1e9
+        st = dict(ln.split() for ln in read("/sys/fs/cgroup/cpu/cpu.stat").splitlines() if len(ln.split()) == 2)
+        snap.update(throttled_s=int(st.get("throttled_time", 0)) / 1e9, nr_throttled=int(st.get("nr_throttled", 0)))
+        q = int(read("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"))
+        snap["quota_cores"] = None if q < 0 else round(q / int(read("/sys/fs/cgroup/cpu/cpu.cfs_period_us")), 2)
+        return snap
+    except (OSError, ValueError, KeyError):
+        return snap if "usage_s" in snap else None
+
+
+def cgroup_cpu_delta(c0: dict | None, c1: dict | None, elapsed: float) -> dict | None:
+    if not c0 or not c1 or "usage_s" not in c0:
+        return None
+    out = {"cores_used": round((c1["usage_s"] - c0["usage_s"]) / elapsed, 2), "cpus_visible": c1["cpus"]}
+    if "quota_cores" in c1:
+        out["quota_cores"] = c1["quota_cores"]
+    if "throttled_s" in c1:
+        out["throttled_ms"] = round(1e3 * (c1["throttled_s"] - c0["throttled_s"]), 1)
+        out["nr_throttled"] = c1["nr_throttled"] - c0["nr_throttled"]
+    return out
 
 
 def observed_transport(allr, n: int) -> str:
