@@ -327,6 +327,26 @@ def main():
             time.sleep(0.1)
         pool.close()
         note("master has every chunkserver")
+        # the journal creates its segment files, and writes each out once, in the background
+        # after start (journal.h); let that finish first, so the first-cycle zero fill and its
+        # flushes do not share the volume with the timed writes (a startup transient, not the
+        # steady state); bounded, and reported
+        import urllib.request
+
+        t_fill = time.perf_counter()
+        fill_deadline = time.time() + 180
+        unready = None
+        while time.time() < fill_deadline:
+            try:
+                st = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
+            except OSError:
+                st = {}
+            unready = st.get("journal_parts_unready", 0) if st.get("journal") else 0
+            if unready == 0:
+                break
+            time.sleep(0.2)
+        journal_settle_s = round(time.perf_counter() - t_fill, 2)
+        note(f"journal settled in {journal_settle_s} s ({unready} parts still unready)")
         barrier()
 
         client = Client([my_master], local_chunkserver=my_cs)
@@ -363,6 +383,14 @@ def main():
                 raise RuntimeError(f"chunkserver device sync failed: {r}")
             sync_log.append((round(1e3 * (time.perf_counter() - t_req), 3), r.get("sync_ms")))
 
+        # no cyclic-GC pass inside the timed region: a full collection over this process's
+        # imports (torch, grpc, numpy) is tens of ms, and one landing in the closing bracket
+        # showed up as a 100 ms device sync whose server side took 0.02 ms (profiles/r4_journal)
+        import gc
+
+        gc.collect()
+        gc.freeze()
+        gc.disable()
         device_sync()
         barrier()
         device_sync()
@@ -401,6 +429,7 @@ def main():
         device_sync()
         elapsed = time.perf_counter() - t0
         end_sync_s = elapsed - t_loop
+        gc.enable()
         note(f"{a.steps} timed steps in {elapsed:.3f} s")
         cpu1 = cpu_snapshot()
         host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
@@ -455,7 +484,7 @@ def main():
                        "rbytes": rbytes, "wt": wt,
                        "rt": rt, "cs": stats, "stress": stress, "remote": remote,
                        "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
-                       "cpu": host_cpu, "job_cpu": job_cpu, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
+                       "cpu": host_cpu, "job_cpu": job_cpu, "settle": journal_settle_s, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                    for k, v in (client.phase_times or {}).items() if v}})
         if rank == 0:
             tmax = max(r["elapsed"] for r in allr)
@@ -511,10 +540,12 @@ def main():
                     ("records", "journal_records"), ("sync_rounds", "journal_sync_rounds"),
                     ("materialized_blocks", "materialized_blocks"), ("materialize_pending", "materialize_pending"),
                     ("full_waits", "journal_full_waits"), ("segments", "journal_segs"),
-                    ("segments_retired", "journal_segs_retired"), ("segments_filled", "journal_segs_filled"),
+                    ("segments_retired", "journal_segs_retired"), ("parts_filled", "journal_segs_filled"),
                     ("prepare_errors", "journal_prepare_errors"),
                     ("materialize_errors", "materialize_errors"), ("sync_ns", "journal_sync_ns"),
-                    ("commit_ns", "journal_commit_ns"), ("bypassed", "journal_bypassed"))} if any(r["cs"].get("journal") for r in allr) else None,
+                    ("commit_ns", "journal_commit_ns"), ("bypassed", "journal_bypassed"),
+                    ("parts_unready", "journal_parts_unready"))} | {
+                    "settle_s_before_warmup": max(r["settle"] for r in allr)} if any(r["cs"].get("journal") for r in allr) else None,
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 # the whole job's CPU over the timed region, from the cgroup every rank shares
                 # (cores used, the quota, and time the quota throttled it); null without cgroup

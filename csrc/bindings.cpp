@@ -405,6 +405,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["journal_prepare_errors"] = t.journal_prepare_errors;
         d["journal_segs_filled"] = t.journal_segs_filled;
         d["journal_fill_bytes"] = t.journal_fill_bytes;
+        d["journal_parts_unready"] = t.journal_parts_unready;
         d["journal_sync_ns"] = t.journal_sync_ns;
         d["journal_bypassed"] = t.journal_bypassed;
         d["journal_commit_ns"] = t.journal_commit_ns;

@@ -2243,6 +2243,7 @@ StoreStats ChunkStore::stats() {
     s.journal_prepare_errors = j.prepare_errors;
     s.journal_segs_filled = j.filled;
     s.journal_fill_bytes = j.fill_bytes;
+    s.journal_parts_unready = j.parts_unready;
     s.journal_sync_ns = j.sync_ns;
     s.journal_bypassed = bypassed_.load();
     s.journal_commit_ns = j.commit_ns;

@@ -103,7 +103,8 @@ struct StoreStats {
   uint64_t journal_tombstones = 0, journal_full_waits = 0, journal_segs = 0, journal_segs_free = 0;
   uint64_t journal_segs_retired = 0, journal_replayed = 0, journal_replay_skipped = 0;
   uint64_t materialized_blocks = 0, materialized_bytes = 0, materialize_pending = 0, materialize_batches = 0;
-  uint64_t materialize_errors = 0, journal_prepare_errors = 0, journal_segs_filled = 0, journal_fill_bytes = 0;
+  uint64_t materialize_errors = 0, journal_prepare_errors = 0, journal_segs_filled = 0, journal_fill_bytes = 0,
+           journal_parts_unready = 0;
   uint64_t journal_sync_ns = 0, journal_commit_ns = 0, journal_bypassed = 0;
   bool journal_failed = false;
   std::string journal_last_error, materialize_last_error;

@@ -746,6 +746,11 @@ JournalStats BlockJournal::stats() {
   s.segs_total = segs_.size();
   s.segs_free = free_.size();
   s.failed = failed_;
+  const uint64_t missing = cfg_.max_segs > static_cast<int>(segs_.size()) ? cfg_.max_segs - segs_.size() : 0;
+  s.parts_unready = missing * static_cast<uint64_t>(cfg_.parts);
+  if (cfg_.zero_fill)
+    for (auto& seg : segs_)
+      for (auto& p : seg->parts) s.parts_unready += p->filled ? 0 : 1;
   return s;
 }
 

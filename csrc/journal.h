@@ -128,6 +128,7 @@ struct JournalStats {
   uint64_t segs_total = 0, segs_free = 0, segs_retired = 0, full_waits = 0;
   uint64_t replayed = 0, replay_skipped = 0, prepared = 0, prepare_errors = 0, filled = 0, fill_bytes = 0;
   uint64_t sync_ns = 0, commit_ns = 0;  // time in fdatasync rounds; time writers spent in commit()
+  uint64_t parts_unready = 0;  // part files not yet created, or (zero_fill) not yet written out once
   bool failed = false;
   std::string last_error;  // the last segment preparation / header error, for /stats
 };
