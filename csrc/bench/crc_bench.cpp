@@ -83,6 +83,7 @@ int main(int argc, char** argv) {
   uint64_t total_mib = 1024;
   bool sweep = false;
   bool wide_ab = false;  // --wide-ab: K1/K2 on the matrix cores, 3 x 4-wave vs 1 x 12-wave workgroups per CU
+  bool fp4_ab = false;   // --fp4-ab: the wide kernel's chunk CRCs on i8 vs FP4 matrix cores, 3 and 2 groups
   uint64_t single_mib = 0;  // --single MIB: only the production K1/K2 dispatch at that size (PMC runs)
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -90,6 +91,7 @@ int main(int argc, char** argv) {
     else if (a == "--mib" && i + 1 < argc) total_mib = std::strtoull(argv[++i], nullptr, 10);
     else if (a == "--sweep") sweep = true;
     else if (a == "--wide-ab") wide_ab = true;
+    else if (a == "--fp4-ab") fp4_ab = true;
     else if (a == "--single" && i + 1 < argc) single_mib = std::strtoull(argv[++i], nullptr, 10);
   }
   CK(hipSetDevice(0));
@@ -135,6 +137,45 @@ int main(int argc, char** argv) {
     std::printf("{\"bytes\": %llu, \"us\": %.2f, \"GBps\": %.1f, \"ok\": %s}\n", static_cast<unsigned long long>(n), r.us,
                 n / r.us / 1e3, r.ok ? "true" : "false");
     return r.ok ? 0 : 1;
+  }
+  if (fp4_ab) {
+    // plus a streaming read of the same bytes, so each size has its own like-for-like roofline
+    std::printf("{\"stream_read_GBps\": %.1f, \"k1k2\": [", stream_gbps);
+    set_crc_mfma(true);
+    set_crc_lds_max_mib(0);
+    uint32_t* dout = nullptr;
+    CK(hipMalloc(&dout, 4 * kStreamReadGrid * 4));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    bool f = true;
+    for (uint64_t mib : std::vector<uint64_t>{1, 8, 16, 32, 64, 128, 256, 1024}) {
+      const uint64_t n = mib << 20;
+      if (n > total) continue;
+      const int it = n >= (256ull << 20) ? std::max(3, iters / 10) : iters;
+      CK(hipEventRecord(e0, s));
+      for (int i = 0; i < it; ++i) CK(launch_stream_read(d, n, dout, s));
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double stream_us = 1e3 * ms / it;
+      for (int rep = 0; rep < 2; ++rep)
+        for (int w : {1, 2})
+          for (int fp4 : {0, 1}) {
+            set_crc_wide(w);
+            set_crc_fp4(fp4 != 0);
+            Run r = bench_block(d, n, t, dmeta, dpart, s, it, host);
+            std::printf("%s\n  {\"bytes\": %llu, \"wide\": %d, \"fp4\": %d, \"rep\": %d, \"us\": %.2f, \"GBps\": %.1f, "
+                        "\"of_stream\": %.3f, \"stream_same_size_us\": %.2f, \"of_stream_same_size\": %.3f, \"ok\": %s}",
+                        f ? "" : ",", static_cast<unsigned long long>(n), w, fp4, rep, r.us, n / r.us / 1e3,
+                        n / r.us / 1e3 / stream_gbps, stream_us, stream_us / r.us, r.ok ? "true" : "false");
+            f = false;
+          }
+    }
+    std::printf("\n]}\n");
+    (void)hipFree(dout);
+    return 0;
   }
   if (wide_ab) {
     std::printf("{\"stream_read_GBps\": %.1f, \"k1k2\": [", stream_gbps);

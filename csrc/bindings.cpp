@@ -182,6 +182,8 @@ PYBIND11_MODULE(_dfs_native, m) {
   m.def("crc_kernels", [] { return py::make_tuple(crc_mfma_enabled(), crc_ring_buffers(), crc_tile_ring_buffers()); });
   m.def("set_crc_lds_max_mib", &set_crc_lds_max_mib, "K1/K2 size-based dispatch threshold (0 = matrix cores only)");
   m.def("crc_wide_mode", &crc_wide_mode);
+  m.def("crc_fp4_enabled", &crc_fp4_enabled);
+  m.def("set_crc_fp4", &set_crc_fp4, "wide K1/K2: chunk CRCs on the FP4 matrix cores (else i8)");
   m.def("set_crc_wide", &set_crc_wide, "K1/K2 one workgroup per CU: 0 off, 1 shared LDS image, 2 + LDS basis");
   m.def("set_crc_kernels", [](bool mfma, int scrub_ring, int tile_ring) {
     set_crc_mfma(mfma);

@@ -21,6 +21,9 @@ constexpr int kCrcBasisBytes = 16 * 64 * 16;  // MFMA basis (A fragments), store
 constexpr int kCrcChunkShiftBytes = 7 * 4 * 256 * 4;  // chunk -> slice shift tables, stored after the basis
 // behind those: slice -> 4 KiB sub-tile shift tables (7) and the 16 KiB tile shift (wide kernel)
 constexpr int kCrcWideExtraBytes = 8 * 4 * 256 * 4;
+// behind those: the basis of the FP4 matrix-core form (8 A fragments of 16 B per lane)
+constexpr int kCrcBasisFp4Bytes = 8 * 64 * 16;
+constexpr int kCrcBasisFp4Offset = kCrcBasisBytes + kCrcChunkShiftBytes + kCrcWideExtraBytes;  // after DevCrcTables
 
 struct DevCrcTables {
   uint32_t slice16[16][256];
@@ -109,6 +112,12 @@ constexpr uint64_t kCrcRingMinTiles = 2048;
 constexpr int kCrcWideDefault = 1;
 int crc_wide_mode();
 void set_crc_wide(int mode);
+// The wide K1/K2 kernel's chunk CRC on the FP4 matrix cores (v_mfma_scale_f32_32x32x64_f8f6f4:
+// 64 input bits per row per instruction at the cycles of the i8 form's 32) instead of i8.
+// DFS_CRC_FP4 overrides, set_crc_fp4 is the benches' A/B switch.
+constexpr int kCrcFp4Default = 0;
+bool crc_fp4_enabled();
+void set_crc_fp4(bool on);
 
 // Benches: streaming read of n bytes (n % 16 == 0) on kStreamReadGrid x 256 threads; `out`
 // holds 4 x kStreamReadGrid words.

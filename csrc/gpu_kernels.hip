@@ -245,6 +245,52 @@ __device__ __forceinline__ uint32_t wave_chunk_crcs(const i32x4 (&A)[16], const 
   return mine;
 }
 
+// The same chunk CRCs on the FP4 matrix cores. v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1
+// operands (unit block scales) takes 64 K per instruction at the cycles of the i8 32x32x32, so a
+// 64 B chunk is 8 instructions instead of 16 and the basis 32 VGPRs instead of 64:
+//  * B: one data dword x gives the whole 32-element fragment: x & 0x11111111 (each nibble 0 or
+//    0b0001 = 0.5), x & 0x22222222 (0 or 1.0), x & 0x44444444 (0 or 2.0) and
+//    (x >> 1) & 0x44444444 (bit 3 of each nibble; 0 or 2.0; bit 3 itself is the sign).
+//  * A: 2.0 / 1.0 / 0.5 / 0.5 where the basis bit is set, so every product of two set bits is
+//    exactly 1.0 and the f32 accumulator counts them (at most 512 per pass: exact).
+//  * The accumulators start at 65536 = 2^16: in [2^16, 2^17) one ulp is 2^-7, so the count's
+//    bit 0 — the parity — is bit 7 of the float's encoding and bits 0..6 are 0. The low byte is
+//    0x80 or 0, exactly what the i8 form's gather expects.
+using i32x8 = __attribute__((ext_vector_type(8))) int;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+__device__ __forceinline__ uint32_t wave_chunk_crcs_fp4(const i32x4 (&A)[8], const WaveData& d, int lane) {
+  const int h = lane >> 5;
+  uint32_t mine = 0;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const uint4 w0 = d.v[2 * it], w1 = d.v[2 * it + 1];
+    const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 65536.0f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const uint32_t x = w[s];
+      const i32x8 b = {static_cast<int>(x & 0x11111111u), static_cast<int>(x & 0x22222222u),
+                       static_cast<int>(x & 0x44444444u), static_cast<int>((x >> 1) & 0x44444444u), 0, 0, 0, 0};
+      const i32x8 a = {A[s].x, A[s].y, A[s].z, A[s].w, 0, 0, 0, 0};
+      acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc, 4, 4, 0, 127, 0, 127);
+    }
+    uint32_t part = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(acc[4 + q]), __float_as_uint(acc[q]), 0x0c0c0400u);
+      const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(acc[12 + q]), __float_as_uint(acc[8 + q]), 0x0c0c0400u);
+      part |= __builtin_amdgcn_perm(hi, lo, 0x05040100u) >> q;
+    }
+    part >>= 4 * h;
+    part = xr32(part);
+    if (it == h) mine = part;
+  }
+  return mine;
+}
+
 // Chunk CRCs -> slice CRC in one lookup round: lane sl of a slice's 8-lane group moves its
 // chunk CRC past the 64 * (7 - sl) bytes that follow the chunk in the slice (one tab4 into
 // its own shift table; sl == 7 needs none) and three xor-shuffles fold the group, since the
@@ -550,12 +596,14 @@ static_assert(sizeof(MfmaWideLds) - offsetof(MfmaWideLds, sh4k) == sizeof(DevCrc
 
 // kWrite: the K1/K2 write form (slice words out, whole-block partials, nothing to verify),
 // with those checks resolved at compile time so the loop body has no uniform branches.
-template <int kGroups, bool kWrite>
+// kFp4: the chunk CRCs on the FP4 matrix cores (wave_chunk_crcs_fp4), else i8.
+template <int kGroups, bool kWrite, bool kFp4 = false>
 __global__ __launch_bounds__(kCrcWgThreads * kGroups) __attribute__((amdgpu_waves_per_eu(kGroups, kGroups)))
 void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   constexpr int kThreads = kCrcWgThreads * kGroups;
+  constexpr int kFrags = kFp4 ? 8 : 16;  // A fragments per lane
   __shared__ MfmaWideLds lt;
-  __shared__ i32x4 lbasis[16 * 64];
+  __shared__ i32x4 lbasis[kFrags * 64];
   __shared__ uint32_t wacc[4 * kGroups];
   __shared__ uint32_t wg_bad[kGroups];
   const int lane = threadIdx.x & 63, gw = threadIdx.x >> 6, wave = gw & 3, grp = gw >> 2, sw = lane >> 3,
@@ -571,14 +619,19 @@ void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   WaveData cur;
   if (t_begin < t_end) cur = load_wave_ring(a.data, first_slice(t_begin), lo, hi, lane);
   const uint8_t* img = reinterpret_cast<const uint8_t*>(gt + 1);
-  copy16<kThreads>(img, lbasis, kCrcBasisBytes);
+  if constexpr (kFp4) copy16<kThreads>(img + kCrcBasisFp4Offset, lbasis, kCrcBasisFp4Bytes);
+  else copy16<kThreads>(img, lbasis, kCrcBasisBytes);
   copy16<kThreads>(img + kCrcBasisBytes, &lt, kCrcChunkShiftBytes + kCrcWideExtraBytes);
   copy16<kThreads>(&gt->sh4k, &lt.sh4k, static_cast<int>(sizeof(DevCrcTables) - offsetof(DevCrcTables, sh4k)));
   if (threadIdx.x < kGroups) wg_bad[threadIdx.x] = 0xFFFFFFFFu;
   __syncthreads();
-  i32x4 A[16];
+  i32x4 A[kFrags];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) A[s] = lbasis[s * 64 + lane];
+  for (int s = 0; s < kFrags; ++s) A[s] = lbasis[s * 64 + lane];
+  auto chunk_crcs = [&](const WaveData& d) {
+    if constexpr (kFp4) return wave_chunk_crcs_fp4(A, d, lane);
+    else return wave_chunk_crcs(A, d, lane);
+  };
 
   uint32_t acc = 0;
   uint32_t bad = 0xFFFFFFFFu;
@@ -603,7 +656,7 @@ void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   for (uint64_t t = t_begin; t < t_end; ++t) {
     WaveData nxt;
     if (t + 1 < t_end) nxt = load_wave_ring(a.data, first_slice(t + 1), lo, hi, lane);
-    const uint32_t c = wave_chunk_crcs(A, cur, lane);
+    const uint32_t c = chunk_crcs(cur);
     if (t > t_begin) finish(cprev, t - 1);
     cprev = c;
     if (t + 1 < t_end) cur = nxt;
@@ -611,8 +664,7 @@ void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   if (t_begin < t_end) finish(cprev, t_end - 1);
 
   if (a.has_tail && vb == 0 && wave == 0) {
-    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(a.data + a.s_full * 512, a.tail_len, lane),
-                                                       lane), lane);
+    uint32_t r = slice_from_chunks(lt, chunk_crcs(load_tail_wave(a.data + a.s_full * 512, a.tail_len, lane)), lane);
     if (lane == 0) {
       uint32_t be = __builtin_bswap32(r ^ a.tail_init);
       if (a.meta_out) a.meta_out[a.s_full] = be;
@@ -1238,6 +1290,19 @@ int crc_wide_mode() {
 
 static int crc_wide_groups() { return crc_wide_mode() == 2 ? 2 : kMaxGridCrc / 256; }
 
+static std::atomic<int> g_crc_fp4{-1};
+
+void set_crc_fp4(bool on) { g_crc_fp4.store(on ? 1 : 0); }
+
+bool crc_fp4_enabled() {
+  int v = g_crc_fp4.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = std::getenv("DFS_CRC_FP4");
+    g_crc_fp4.store(v = (e ? std::atoi(e) : kCrcFp4Default) ? 1 : 0);
+  }
+  return v != 0;
+}
+
 DevCrcTables* upload_crc_tables(hipStream_t s) {
   static_assert(sizeof(DevCrcTables) % 16 == 0, "table image must be uint4-copyable");
   std::vector<uint8_t> host(sizeof(DevCrcTables));
@@ -1257,7 +1322,8 @@ DevCrcTables* upload_crc_tables(hipStream_t s) {
   // MFMA basis right behind the LDS image (never copied to LDS): fragment [s][lane] of A,
   // element j = byte j of the 16 B: CRC bit i = lane & 31 of V[32h + 4(s>>1) + (j&3)][4(s&1) + (j>>2)],
   // scaled by 2^(7-p) (see wave_chunk_crcs)
-  host.resize(sizeof(DevCrcTables) + kCrcBasisBytes + kCrcChunkShiftBytes + kCrcWideExtraBytes);
+  host.resize(sizeof(DevCrcTables) + kCrcBasisFp4Offset + kCrcBasisFp4Bytes);
+  static_assert(kCrcBasisFp4Offset == kCrcBasisBytes + kCrcChunkShiftBytes + kCrcWideExtraBytes, "image order");
   // chunk-shift tables behind the basis: cs[sl] moves a 64 B chunk's CRC past 64 * (7 - sl) bytes;
   // then ss[sw] (a slice's CRC past 512 * (7 - sw) bytes) and the 16 KiB tile shift
   auto* cs = reinterpret_cast<uint32_t(*)[4][256]>(host.data() + sizeof(DevCrcTables) + kCrcBasisBytes);
@@ -1274,6 +1340,21 @@ DevCrcTables* upload_crc_tables(hipStream_t s) {
         const uint32_t v = chunk_basis_crc(byte, p);
         basis[(st * 64 + lane) * 16 + j] = ((v >> bit) & 1u) ? static_cast<int8_t>(static_cast<uint8_t>(1u << (7 - p))) : 0;
       }
+  // FP4 basis (wave_chunk_crcs_fp4): fragment [s][lane], dword r, nibble q is the element that
+  // B takes from bit 4(q & 1) + r of byte (q >> 1) of data dword s of the lane's 32 B half;
+  // value 2.0 / 1.0 / 0.5 / 0.5 (e2m1 0b0100 / 0b0010 / 0b0001) for planes r = 0..3 where
+  // the basis bit is set, so the product with B's 0.5 / 1.0 / 2.0 / 2.0 is 1.0
+  uint8_t* b4 = host.data() + sizeof(DevCrcTables) + kCrcBasisFp4Offset;
+  std::memset(b4, 0, kCrcBasisFp4Bytes);
+  static const uint8_t kFp4Code[4] = {0x4, 0x2, 0x1, 0x1};
+  for (int st = 0; st < 8; ++st)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int r = 0; r < 4; ++r)
+        for (int q = 0; q < 8; ++q) {
+          const int h = lane >> 5, bit = (lane & 31) ^ 7;
+          const uint32_t v = chunk_basis_crc(32 * h + 4 * st + (q >> 1), 4 * (q & 1) + r);
+          if ((v >> bit) & 1u) b4[(st * 64 + lane) * 16 + 4 * r + (q >> 1)] |= kFp4Code[r] << (4 * (q & 1));
+        }
   t = reinterpret_cast<DevCrcTables*>(host.data());
   DevCrcTables* d = nullptr;
   if (hipMalloc(&d, host.size()) != hipSuccess) return nullptr;
@@ -1316,12 +1397,17 @@ hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipSt
         const int G = crc_wide_groups();
         const dim3 g(grid / G), b(kCrcWgThreads * G);
         const bool w = a.meta_out && !a.meta_expect && a.part_crc;
-        if (G == 2) {
-          if (w) hipLaunchKernelGGL((crc_tile_wide_kernel<2, true>), g, b, 0, s, a, t);
-          else hipLaunchKernelGGL((crc_tile_wide_kernel<2, false>), g, b, 0, s, a, t);
-        } else {
-          if (w) hipLaunchKernelGGL((crc_tile_wide_kernel<kMaxGridCrc / 256, true>), g, b, 0, s, a, t);
-          else hipLaunchKernelGGL((crc_tile_wide_kernel<kMaxGridCrc / 256, false>), g, b, 0, s, a, t);
+        constexpr int G3 = kMaxGridCrc / 256;
+        const int v = (G == 2 ? 0 : 4) | (w ? 2 : 0) | (crc_fp4_enabled() ? 1 : 0);
+        switch (v) {
+          case 0: hipLaunchKernelGGL((crc_tile_wide_kernel<2, false, false>), g, b, 0, s, a, t); break;
+          case 1: hipLaunchKernelGGL((crc_tile_wide_kernel<2, false, true>), g, b, 0, s, a, t); break;
+          case 2: hipLaunchKernelGGL((crc_tile_wide_kernel<2, true, false>), g, b, 0, s, a, t); break;
+          case 3: hipLaunchKernelGGL((crc_tile_wide_kernel<2, true, true>), g, b, 0, s, a, t); break;
+          case 4: hipLaunchKernelGGL((crc_tile_wide_kernel<G3, false, false>), g, b, 0, s, a, t); break;
+          case 5: hipLaunchKernelGGL((crc_tile_wide_kernel<G3, false, true>), g, b, 0, s, a, t); break;
+          case 6: hipLaunchKernelGGL((crc_tile_wide_kernel<G3, true, false>), g, b, 0, s, a, t); break;
+          default: hipLaunchKernelGGL((crc_tile_wide_kernel<G3, true, true>), g, b, 0, s, a, t); break;
         }
       } else {
         hipLaunchKernelGGL(crc_tile_mfma_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);

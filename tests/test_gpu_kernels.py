@@ -71,6 +71,32 @@ def test_gpu_crc_wide_workgroups(gstore, native, mode, n):
         native.set_crc_lds_max_mib(16)
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("n", [511, 4096 + 5, (1 << 20) + 13, (8 << 20) - 4096 + 7, (64 << 20) + 513, 300 << 20])
+def test_gpu_crc_wide_fp4_matrix_cores(gstore, native, mode, n):
+    """The wide K1/K2 kernel with its chunk CRCs on the FP4 matrix cores
+    (v_mfma_scale_f32_32x32x64_f8f6f4, e2m1 operands, parity in bit 7 of an f32 biased by 2^16)
+    against zlib: whole-block CRC, every slice word, tails; plus a patterned block whose bytes
+    set every nibble bit (0xFF) and the sign bit of every nibble (0x88)."""
+    saved_w, saved_f = native.crc_wide_mode(), native.crc_fp4_enabled()
+    native.set_crc_lds_max_mib(0)
+    native.set_crc_wide(mode)
+    native.set_crc_fp4(True)
+    try:
+        for d in (os.urandom(n), (b"\xff\x88\x00\x11" * (n // 4 + 1))[:n]):
+            crc, meta = gstore.gpu_crc(d)
+            assert crc == zlib.crc32(d) and meta == ref_meta(d)
+        if n < (100 << 20):
+            ok, _, err = gstore.write(f"fp4_{mode}_{n}", d, zlib.crc32(d))
+            assert ok, err
+            st, total, out, partial, bad, err = gstore.read(f"fp4_{mode}_{n}", 0, 0)
+            assert (st, total, out) == (0, n, d)
+    finally:
+        native.set_crc_fp4(saved_f)
+        native.set_crc_wide(saved_w)
+        native.set_crc_lds_max_mib(16)
+
+
 def test_gpu_crc_zero_and_pattern(gstore):
     for d in (b"\0" * (1 << 20), bytes(range(256)) * 4099):
         crc, meta = gstore.gpu_crc(d)
