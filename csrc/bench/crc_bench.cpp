@@ -287,8 +287,10 @@ int main(int argc, char** argv) {
   sl.full_init = crc_init_term(kSliceBytes);
   sl.bad = dbad;
   first = true;
-  for (int mf = 1; mf >= 0; --mf) {
-    set_crc_mfma(mf == 1);
+  const bool fp4_saved = crc_fp4_enabled();
+  for (int mf = 2; mf >= 0; --mf) {  // 2: matrix cores, FP4 form; 1: i8 form; 0: LDS tables
+    set_crc_mfma(mf >= 1);
+    set_crc_fp4(mf == 2);
     CK(hipMemset(dbad, 0xFF, nb * 4));
     CK(launch_scrub(sl, t, s));
     CK(hipStreamSynchronize(s));
@@ -310,9 +312,11 @@ int main(int argc, char** argv) {
     std::printf("%s\n  {\"bytes\": %llu, \"blocks\": %llu, \"impl\": \"%s\", \"us\": %.1f, \"GBps\": %.1f, "
                 "\"of_stream\": %.3f, \"ok\": %s}",
                 first ? "" : ",", static_cast<unsigned long long>(total), static_cast<unsigned long long>(nb),
-                mf ? "mfma" : "lds_tables", us, total / us / 1e3, total / us / 1e3 / stream_gbps, ok ? "true" : "false");
+                mf == 2 ? "mfma_fp4" : (mf ? "mfma" : "lds_tables"), us, total / us / 1e3, total / us / 1e3 / stream_gbps,
+                ok ? "true" : "false");
     first = false;
   }
+  set_crc_fp4(fp4_saved);
   std::printf("\n], \"rs\": [");
   // K4: RS(k,m) parity of k shards of `shard` bytes, device-resident (kernel only)
   first = true;

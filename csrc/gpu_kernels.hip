@@ -291,6 +291,23 @@ __device__ __forceinline__ uint32_t wave_chunk_crcs_fp4(const i32x4 (&A)[8], con
   return mine;
 }
 
+// The basis of either form in VGPRs, loaded from the uploaded image (kernels that keep no LDS copy).
+template <bool kFp4>
+struct ChunkBasis {
+  static constexpr int kFrags = kFp4 ? 8 : 16;
+  i32x4 A[kFrags];
+  __device__ __forceinline__ void load(const DevCrcTables* __restrict__ gt, int lane) {
+    const i32x4* p = reinterpret_cast<const i32x4*>(reinterpret_cast<const uint8_t*>(gt + 1) +
+                                                    (kFp4 ? kCrcBasisFp4Offset : 0));
+#pragma unroll
+    for (int s = 0; s < kFrags; ++s) A[s] = p[s * 64 + lane];
+  }
+  __device__ __forceinline__ uint32_t crcs(const WaveData& d, int lane) const {
+    if constexpr (kFp4) return wave_chunk_crcs_fp4(A, d, lane);
+    else return wave_chunk_crcs(A, d, lane);
+  }
+};
+
 // Chunk CRCs -> slice CRC in one lookup round: lane sl of a slice's 8-lane group moves its
 // chunk CRC past the 64 * (7 - sl) bytes that follow the chunk in the slice (one tab4 into
 // its own shift table; sl == 7 needs none) and three xor-shuffles fold the group, since the
@@ -1028,7 +1045,7 @@ void crc_tile_ring_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
 
 using ConstScrubBlock = const __attribute__((address_space(4))) ScrubBlock;
 
-template <int R>
+template <int R, bool kFp4 = false>
 __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void crc_scrub_ring_kernel(ScrubLaunch a, const DevCrcTables* __restrict__ gt) {
   __shared__ MfmaSliceLds lt;
@@ -1066,8 +1083,8 @@ void crc_scrub_ring_kernel(ScrubLaunch a, const DevCrcTables* __restrict__ gt) {
 #pragma unroll
     for (int k = 0; k < R - 1; ++k) load(k, t_begin + k);
   }
-  i32x4 A[16];
-  load_basis(reinterpret_cast<const i32x4*>(gt + 1), lane, A);
+  ChunkBasis<kFp4> basis;
+  basis.load(gt, lane);
   load_lds_image(gt, &lt);
   __syncthreads();
   auto step = [&](int slot, uint64_t t) {
@@ -1075,7 +1092,7 @@ void crc_scrub_ring_kernel(ScrubLaunch a, const DevCrcTables* __restrict__ gt) {
     const int64_t i0 = static_cast<int64_t>((t - blocks[blk].tile_start) * kSlicesPerTile + wave * 8);
     const int64_t hi = static_cast<int64_t>(blocks[blk].s_full);
     // slices past the block end are never compared, so their (re-read) data needs no masking
-    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, ring.b[slot], lane), lane);
+    uint32_t r = slice_from_chunks(lt, basis.crcs(ring.b[slot], lane), lane);
     const int64_t i = i0 + sw;
     if (sl == 0 && i < hi && ring.expect[slot] != __builtin_bswap32(r ^ a.full_init))
       atomicMin(&a.bad[blk], static_cast<uint32_t>(i));
@@ -1098,8 +1115,7 @@ void crc_scrub_ring_kernel(ScrubLaunch a, const DevCrcTables* __restrict__ gt) {
        k += static_cast<uint64_t>(gridDim.x) * waves) {
     ConstScrubBlock& b = blocks[k];
     if (!b.tail_len) continue;
-    uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, load_tail_wave(b.data + b.s_full * 512, b.tail_len, lane),
-                                                       lane), lane);
+    uint32_t r = slice_from_chunks(lt, basis.crcs(load_tail_wave(b.data + b.s_full * 512, b.tail_len, lane), lane), lane);
     if (lane == 0 && b.meta[b.s_full] != __builtin_bswap32(r ^ b.tail_init))
       atomicMin(&a.bad[k], static_cast<uint32_t>(b.s_full));
   }
@@ -1448,8 +1464,14 @@ hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t
   switch (ring) {
     case 0: hipLaunchKernelGGL(crc_scrub_kernel, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
     case 2: hipLaunchKernelGGL(crc_scrub_mfma_kernel, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
-    case 3: hipLaunchKernelGGL(crc_scrub_ring_kernel<3>, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
-    default: hipLaunchKernelGGL(crc_scrub_ring_kernel<4>, grid, dim3(kCrcWgThreads), 0, s, a, t); break;
+    case 3:
+      if (crc_fp4_enabled()) hipLaunchKernelGGL((crc_scrub_ring_kernel<3, true>), grid, dim3(kCrcWgThreads), 0, s, a, t);
+      else hipLaunchKernelGGL((crc_scrub_ring_kernel<3, false>), grid, dim3(kCrcWgThreads), 0, s, a, t);
+      break;
+    default:
+      if (crc_fp4_enabled()) hipLaunchKernelGGL((crc_scrub_ring_kernel<4, true>), grid, dim3(kCrcWgThreads), 0, s, a, t);
+      else hipLaunchKernelGGL((crc_scrub_ring_kernel<4, false>), grid, dim3(kCrcWgThreads), 0, s, a, t);
+      break;
   }
   return hipGetLastError();
 }

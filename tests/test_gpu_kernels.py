@@ -246,9 +246,20 @@ def test_gpu_corruption_detected_full_and_partial(gstore):
     gstore.remove("corrupt")
 
 
-def test_gpu_batched_scrub_finds_exactly_the_corrupt_blocks(gstore):
+@pytest.mark.parametrize("fp4", [False, True])
+def test_gpu_batched_scrub_finds_exactly_the_corrupt_blocks(gstore, native, fp4):
     # K1b: one launch over blocks of every shape (tiny, exact slices, tails, multi-tile);
-    # corrupt a middle slice, a last full slice and a tail byte in different blocks
+    # corrupt a middle slice, a last full slice and a tail byte in different blocks; with the
+    # chunk CRCs on the i8 and on the FP4 matrix cores
+    saved = native.crc_fp4_enabled()
+    native.set_crc_fp4(fp4)
+    try:
+        _batched_scrub(gstore)
+    finally:
+        native.set_crc_fp4(saved)
+
+
+def _batched_scrub(gstore):
     sizes = [1, 100, 511, 512, 513, 4096, 16384 + 1, 65536, (1 << 20), (1 << 20) + 300, 3 * (1 << 20) + 7]
     ids = []
     for i, n in enumerate(sizes * 3):
