@@ -347,6 +347,22 @@ __device__ __forceinline__ void copy16(const void* __restrict__ from, void* to, 
   for (int i = threadIdx.x; i < n16; i += kThreads) dst[i] = src[i];
 }
 
+// The same copy by LDS-DMA (global_load_lds_dwordx4: each wave instruction moves 1 KiB straight
+// into LDS, no VGPRs, no wait before the next one), so a kernel's whole LDS image is in flight at
+// once instead of one register round trip per pass. The destination of one instruction is
+// wave-uniform base + 16 x lane, which a linear copy is. bytes % 16 == 0; completes at the next
+// __syncthreads() (its vmcnt(0)).
+template <int kThreads>
+__device__ __forceinline__ void dma16(const void* __restrict__ from, void* to, int bytes) {
+  using LdsPtr = __attribute__((address_space(3))) void*;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(from);
+  uint8_t* dst = reinterpret_cast<uint8_t*>(to);
+  for (int base = wave * 1024; base < bytes; base += kThreads * 16)
+    if (base + lane * 16 < bytes)
+      __builtin_amdgcn_global_load_lds(src + base + lane * 16, (LdsPtr)(dst + base), 16, 0, 0);
+}
+
 template <class L, int kThreads = kCrcWgThreads>
 __device__ __forceinline__ void load_lds_image(const DevCrcTables* __restrict__ gt, L* lt) {
   const uint8_t* cs = reinterpret_cast<const uint8_t*>(gt + 1) + kCrcBasisBytes;
@@ -619,7 +635,7 @@ __global__ __launch_bounds__(kCrcWgThreads * kGroups) __attribute__((amdgpu_wave
 void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   constexpr int kThreads = kCrcWgThreads * kGroups;
   constexpr int kFrags = kFp4 ? 8 : 16;  // A fragments per lane
-  __shared__ MfmaWideLds lt;
+  __shared__ __attribute__((aligned(16))) MfmaWideLds lt;
   __shared__ i32x4 lbasis[kFrags * 64];
   __shared__ uint32_t wacc[4 * kGroups];
   __shared__ uint32_t wg_bad[kGroups];
@@ -634,12 +650,19 @@ void crc_tile_wide_kernel(CrcLaunch a, const DevCrcTables* __restrict__ gt) {
   // unconditional loads (load_wave_ring: out-of-block slices re-read slice lo, and their chunk
   // CRCs are zeroed below), so no exec-masked branches around the loads in the loop
   WaveData cur;
-  if (t_begin < t_end) cur = load_wave_ring(a.data, first_slice(t_begin), lo, hi, lane);
   const uint8_t* img = reinterpret_cast<const uint8_t*>(gt + 1);
-  if constexpr (kFp4) copy16<kThreads>(img + kCrcBasisFp4Offset, lbasis, kCrcBasisFp4Bytes);
-  else copy16<kThreads>(img, lbasis, kCrcBasisBytes);
-  copy16<kThreads>(img + kCrcBasisBytes, &lt, kCrcChunkShiftBytes + kCrcWideExtraBytes);
-  copy16<kThreads>(&gt->sh4k, &lt.sh4k, static_cast<int>(sizeof(DevCrcTables) - offsetof(DevCrcTables, sh4k)));
+  if constexpr (kFp4) {
+    // the LDS image and basis by LDS-DMA, all in flight together with the first tile's loads
+    dma16<kThreads>(img + kCrcBasisFp4Offset, lbasis, kCrcBasisFp4Bytes);
+    dma16<kThreads>(img + kCrcBasisBytes, &lt, kCrcChunkShiftBytes + kCrcWideExtraBytes);
+    dma16<kThreads>(&gt->sh4k, &lt.sh4k, static_cast<int>(sizeof(DevCrcTables) - offsetof(DevCrcTables, sh4k)));
+    if (t_begin < t_end) cur = load_wave_ring(a.data, first_slice(t_begin), lo, hi, lane);
+  } else {
+    if (t_begin < t_end) cur = load_wave_ring(a.data, first_slice(t_begin), lo, hi, lane);
+    copy16<kThreads>(img, lbasis, kCrcBasisBytes);
+    copy16<kThreads>(img + kCrcBasisBytes, &lt, kCrcChunkShiftBytes + kCrcWideExtraBytes);
+    copy16<kThreads>(&gt->sh4k, &lt.sh4k, static_cast<int>(sizeof(DevCrcTables) - offsetof(DevCrcTables, sh4k)));
+  }
   if (threadIdx.x < kGroups) wg_bad[threadIdx.x] = 0xFFFFFFFFu;
   __syncthreads();
   i32x4 A[kFrags];
