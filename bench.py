@@ -371,14 +371,19 @@ def main():
         # chunkserver's /sync: hipDeviceSynchronize), not in this client process
         sync_log: list = []  # (request ms, hipDeviceSynchronize ms) of each device sync
 
+        # one keep-alive connection to the chunkserver's native /sync listener, opened here, so
+        # a sync inside the bracket is one request on an established connection (no connect,
+        # accept or server thread start in the timed region)
+        import http.client
+
+        sync_conn = http.client.HTTPConnection("127.0.0.1", cs_info.get("sync_port") or chttp, timeout=60)
+
         def device_sync():
             if a.cpu:
                 return
-            import urllib.request
-
             t_req = time.perf_counter()
-            port = cs_info.get("sync_port") or chttp  # the chunkserver's native /sync listener
-            r = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{port}/sync", timeout=60).read())
+            sync_conn.request("GET", "/sync")
+            r = json.loads(sync_conn.getresponse().read())
             if not r.get("synchronized"):
                 raise RuntimeError(f"chunkserver device sync failed: {r}")
             sync_log.append((round(1e3 * (time.perf_counter() - t_req), 3), r.get("sync_ms")))

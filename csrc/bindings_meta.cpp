@@ -837,8 +837,32 @@ void bind_meta(py::module_& m) {
         return d;
       });
 
+  // the file-system side of a gateway on another host (front_store.h): private slots, gRPC to
+  // the masters and chunkservers
+  py::class_<RemoteFrontStore>(m, "RemoteFrontStore")
+      .def(py::init([](const std::string& shard_map_json, std::vector<std::string> masters, size_t slots,
+                       size_t slot_bytes, const std::string& ca_cert, const std::string& domain_name, bool tls) {
+             std::shared_ptr<TlsContext> ctx;
+             if (tls) {
+               std::string err;
+               ctx = TlsContext::client(ca_cert, domain_name, &err);
+               if (!ctx) throw std::runtime_error(err);
+             }
+             return std::make_unique<RemoteFrontStore>(shard_map_json, masters, slots, slot_bytes, 120000, ctx);
+           }),
+           py::arg("shard_map_json"), py::arg("masters"), py::arg("slots") = 32, py::arg("slot_bytes") = 16u << 20,
+           py::arg("ca_cert") = "", py::arg("domain_name") = "", py::arg("tls") = false)
+      .def("set_routing", &RemoteFrontStore::set_routing)
+      .def("stats", [](RemoteFrontStore& s) {
+        py::dict d;
+        d["writes"] = s.client().writes();
+        d["reads"] = s.client().reads();
+        d["connects"] = s.client().connects();
+        return d;
+      });
+
   py::class_<S3Front>(m, "S3Front")
-      .def(py::init([](FastClient* fc, const std::string& host, int port, const std::string& backend, int workers,
+      .def(py::init([](py::object client, const std::string& host, int port, const std::string& backend, int workers,
                        bool auth_enabled, const std::string& region, const std::string& access_key,
                        const std::string& secret_key, bool allow_unsigned, const std::string& audit_socket,
                        bool sse_enabled, bool metadata_sidecar, const std::string& policy_epoch,
@@ -863,7 +887,9 @@ void bind_meta(py::module_& m) {
              c.audit_socket = audit_socket;
              c.sse_enabled = sse_enabled;
              c.metadata_sidecar = metadata_sidecar;
-             return std::make_unique<S3Front>(c, fc);
+             if (py::isinstance<RemoteFrontStore>(client))
+               return std::make_unique<S3Front>(c, static_cast<FrontStore*>(client.cast<RemoteFrontStore*>()));
+             return std::make_unique<S3Front>(c, client.cast<FastClient*>());
            }),
            py::arg("fast_client"), py::arg("host"), py::arg("port"), py::arg("backend"), py::arg("workers") = 32,
            py::arg("auth_enabled") = false, py::arg("region") = "us-east-1", py::arg("access_key") = "",

@@ -123,6 +123,11 @@ bool RemoteClient::master_call(const std::string& path, const std::string& metho
                                const std::string& rid, int* code, std::string* resp) {
   std::string shard;
   std::vector<std::string> cands = masters_for(path, &shard);
+  return call_candidates(std::move(cands), shard, method, req, rid, code, resp);
+}
+
+bool RemoteClient::call_candidates(std::vector<std::string> cands, const std::string& shard, const std::string& method,
+                                   const std::string& req, const std::string& rid, int* code, std::string* resp) {
   const std::string full = "/dfs.MasterService/" + method;
   *code = -1;
   for (size_t i = 0; i < cands.size() && i < 8; ++i) {
@@ -148,6 +153,14 @@ bool RemoteClient::master_call(const std::string& path, const std::string& metho
 FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* data, size_t n, int* replicas,
                                        std::string* msg, Times* t, const std::string& rid_in,
                                        const std::map<std::string, std::string>* attrs) {
+  std::string md5;
+  return write_etag(path, data, n, replicas, msg, t, rid_in, attrs, nullptr, &md5);
+}
+
+FastClient::Status RemoteClient::write_etag(const std::string& path, const uint8_t* data, size_t n, int* replicas,
+                                            std::string* msg, Times* t, const std::string& rid_in,
+                                            const std::map<std::string, std::string>* attrs, const char* etag_attr,
+                                            std::string* md5_out) {
   const std::string rid = rid_in.empty() ? request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.remote.write");
@@ -224,6 +237,7 @@ FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* d
   done.path = path;
   done.size = n;
   done.etag_md5 = md5.get();
+  *md5_out = done.etag_md5;
   t->md5_wait = since(clk);
   done.created_at_ms = static_cast<uint64_t>(now_ms());
   pb::BlockChecksumInfo sum;
@@ -236,6 +250,7 @@ FastClient::Status RemoteClient::write(const std::string& path, const uint8_t* d
   done.ec_parity_shards = alloc.ec_parity_shards;
   done.blocks.push_back(alloc.block);
   if (attrs) done.attributes = *attrs;
+  if (etag_attr) done.attributes[etag_attr] = "\"" + done.etag_md5 + "\"";
   if (!master_call(path, "CompleteFile", done.str(), rid, &code, &raw)) {
     *msg = "Failed to complete file: master unreachable";
     return FastClient::Failed;
@@ -274,7 +289,13 @@ FastClient::Status RemoteClient::read(const std::string& path, std::string* out,
     return FastClient::Failed;
   }
   t->getinfo = since(clk);
-  const pb::FileMetadata& m = info.metadata;
+  return read_meta(info.metadata, out, msg, t, rid, offset, length);
+}
+
+FastClient::Status RemoteClient::read_meta(const pb::FileMetadata& m, std::string* out, std::string* msg, Times* t,
+                                           const std::string& rid, uint64_t offset, uint64_t length) {
+  RequestScope rs(rid);
+  auto clk = Clock::now();
   if (m.size == 0) {
     out->clear();
     reads_++;
@@ -362,6 +383,122 @@ FastClient::Status RemoteClient::read(const std::string& path, std::string* out,
   return FastClient::NotHandled;  // no replica answered cleanly: the Python path recovers / reports
 }
 
+
+FastClient::Status RemoteClient::stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg,
+                                      const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? request_id() : rid_in;
+  pb::GetFileInfoRequest req;
+  req.path = path;
+  int code;
+  std::string raw;
+  if (!master_call(path, "GetFileInfo", req.str(), rid, &code, &raw)) return FastClient::NotHandled;
+  if (code == kNotFound) {
+    *found = false;
+    return FastClient::Ok;
+  }
+  if (code != 0) {
+    *msg = raw;
+    return FastClient::NotHandled;
+  }
+  pb::GetFileInfoResponse info;
+  if (!info.decode(raw)) return FastClient::NotHandled;
+  *found = info.found;
+  if (info.found) *meta_pb = info.metadata.str();
+  return FastClient::Ok;
+}
+
+FastClient::Status RemoteClient::remove(const std::string& path, std::string* msg, const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? request_id() : rid_in;
+  pb::DeleteFileRequest req;
+  req.path = path;
+  int code;
+  std::string raw;
+  if (!master_call(path, "DeleteFile", req.str(), rid, &code, &raw)) return FastClient::NotHandled;
+  if (code != 0) {
+    *msg = raw;
+    return code == kNotFound ? FastClient::Failed : FastClient::NotHandled;
+  }
+  pb::DeleteFileResponse r;
+  if (!r.decode(raw)) return FastClient::NotHandled;
+  if (!r.success) {
+    if (r.error_message == "Not Leader") return FastClient::NotHandled;
+    *msg = r.error_message;
+    return FastClient::Failed;
+  }
+  return FastClient::Ok;
+}
+
+FastClient::Status RemoteClient::rename(const std::string& src, const std::string& dst, std::string* msg,
+                                        const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? request_id() : rid_in;
+  pb::RenameRequest req;
+  req.source_path = src;
+  req.dest_path = dst;
+  int code;
+  std::string raw;
+  if (!master_call(src, "Rename", req.str(), rid, &code, &raw)) return FastClient::NotHandled;
+  if (code != 0) {
+    *msg = raw;
+    return FastClient::NotHandled;
+  }
+  pb::RenameResponse r;
+  if (!r.decode(raw)) return FastClient::NotHandled;
+  if (!r.success) {
+    if (r.error_message == "Not Leader") return FastClient::NotHandled;
+    *msg = r.error_message;
+    return FastClient::Failed;
+  }
+  return FastClient::Ok;
+}
+
+FastClient::Status RemoteClient::list(const std::string& prefix,
+                                      std::vector<std::pair<std::string, pb::FileMetadata>>* out,
+                                      const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? request_id() : rid_in;
+  RequestScope rs(rid);
+  std::vector<std::pair<std::string, std::vector<std::string>>> shards;  // shard -> candidates
+  {
+    std::lock_guard<std::mutex> g(route_mu_);
+    if (have_map_) {
+      for (const auto& shard : map_.shards()) {
+        const auto* peers = map_.peers(shard);
+        if (!peers || peers->empty()) return FastClient::NotHandled;
+        std::vector<std::string> c = *peers;
+        auto it = leader_.find(shard);
+        if (it != leader_.end()) {
+          auto pos = std::find(c.begin(), c.end(), it->second);
+          if (pos != c.end()) std::rotate(c.begin(), pos, pos + 1);
+        }
+        shards.emplace_back(shard, std::move(c));
+      }
+    } else if (!masters_.empty()) {
+      std::vector<std::string> c = masters_;
+      auto it = leader_.find("");
+      if (it != leader_.end()) {
+        auto pos = std::find(c.begin(), c.end(), it->second);
+        if (pos != c.end()) std::rotate(c.begin(), pos, pos + 1);
+      }
+      shards.emplace_back("", std::move(c));
+    }
+  }
+  if (shards.empty()) return FastClient::NotHandled;
+  pb::ListFilesRequest req;
+  req.path = prefix;
+  req.with_metadata = true;
+  const std::string body = req.str();
+  out->clear();
+  for (auto& sh : shards) {
+    int code = 0;
+    std::string raw;
+    if (!call_candidates(sh.second, sh.first, "ListFiles", body, rid, &code, &raw) || code != 0)
+      return FastClient::NotHandled;
+    pb::ListFilesResponse resp;
+    if (!resp.decode(raw) || resp.metadata.size() != resp.files.size()) return FastClient::NotHandled;
+    for (size_t i = 0; i < resp.files.size(); ++i) out->emplace_back(resp.files[i], std::move(resp.metadata[i]));
+  }
+  std::sort(out->begin(), out->end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  return FastClient::Ok;
+}
 
 FastClient::Status RemoteClient::write_ec(const std::string& path, const uint8_t* data, size_t n, int k, int m,
                                           std::string* msg, const std::string& rid_in) {

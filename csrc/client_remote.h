@@ -64,11 +64,31 @@ class RemoteClient {
   void set_host_aliases(std::vector<std::pair<std::string, std::string>> a) { pool_.set_host_aliases(std::move(a)); }
   uint64_t hedged() const { return hedged_.load(); }
 
+  // ---- the S3 front's entry points for a gateway on another host (front_store.h), the
+  // remote twins of FastClient's: same statuses, same NotHandled cases (the gateway's Python
+  // path follows redirects and reports range errors).
+  // write() that also sets attrs[etag_attr] to the quoted MD5 (the S3 ETag); *md5_out = the MD5.
+  Status write_etag(const std::string& path, const uint8_t* data, size_t n, int* replicas, std::string* msg, Times* t,
+                    const std::string& rid, const std::map<std::string, std::string>* attrs, const char* etag_attr,
+                    std::string* md5_out);
+  Status stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg, const std::string& rid);
+  // read() of a file whose metadata the caller already holds
+  Status read_meta(const pb::FileMetadata& m, std::string* out, std::string* msg, Times* t, const std::string& rid,
+                   uint64_t offset, uint64_t length);
+  Status remove(const std::string& path, std::string* msg, const std::string& rid);
+  Status rename(const std::string& src, const std::string& dst, std::string* msg, const std::string& rid);
+  // ListFiles{with_metadata} under `prefix` on every shard (one call per shard), merged by path
+  Status list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
+              const std::string& rid);
+
  private:
   // A MasterService call on the path's shard, following Not Leader hints; `*code` = -1 on
   // transport failure everywhere.
   bool master_call(const std::string& path, const std::string& method, const std::string& req,
                    const std::string& rid, int* code, std::string* resp);
+  // the same over an explicit candidate list (the shard's peers, its last known leader first)
+  bool call_candidates(std::vector<std::string> cands, const std::string& shard, const std::string& method,
+                       const std::string& req, const std::string& rid, int* code, std::string* resp);
   std::vector<std::string> masters_for(const std::string& path, std::string* shard);
   void hash_loop();
 

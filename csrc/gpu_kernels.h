@@ -115,7 +115,7 @@ void set_crc_wide(int mode);
 // The wide K1/K2 kernel's chunk CRC on the FP4 matrix cores (v_mfma_scale_f32_32x32x64_f8f6f4:
 // 64 input bits per row per instruction at the cycles of the i8 form's 32) instead of i8.
 // DFS_CRC_FP4 overrides, set_crc_fp4 is the benches' A/B switch.
-constexpr int kCrcFp4Default = 0;
+constexpr int kCrcFp4Default = 1;
 bool crc_fp4_enabled();
 void set_crc_fp4(bool on);
 

@@ -1,6 +1,7 @@
 // Shared shell of the native control-plane executables (see node_shell.h).
 #include "node_shell.h"
 
+#include <execinfo.h>
 #include <pthread.h>
 #include <signal.h>
 #include <sys/time.h>
@@ -265,7 +266,29 @@ std::string Gauges::render() const {
   return out;
 }
 
+namespace {
+// A fatal signal's backtrace on stderr (async-signal-safe: backtrace + backtrace_symbols_fd
+// write straight to the fd), then the default action, so the exit status still says which.
+void on_fatal(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  char head[96];
+  const int len = std::snprintf(head, sizeof(head), "FATAL signal %d (%s); backtrace:\n", sig, strsignal(sig));
+  if (len > 0) (void)!::write(2, head, static_cast<size_t>(len));
+  backtrace_symbols_fd(frames, n, 2);
+  ::signal(sig, SIG_DFL);
+  ::raise(sig);
+}
+}  // namespace
+
+void install_crash_handler() {
+  void* warm[1];
+  (void)backtrace(warm, 1);  // loads libgcc's unwinder now, not inside the handler
+  for (int sig : {SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGABRT}) ::signal(sig, on_fatal);
+}
+
 void block_stop_signals() {
+  install_crash_handler();
   sigset_t s;
   sigemptyset(&s);
   sigaddset(&s, SIGTERM);

@@ -94,7 +94,9 @@ class Gauges {
 
 // SIGTERM / SIGINT are blocked in every thread from here on (call first in main); wait_for_stop
 // returns when one arrives.
-void block_stop_signals();
+void block_stop_signals();  // also installs install_crash_handler()
+// SIGSEGV / SIGBUS / SIGFPE / SIGILL / SIGABRT print a backtrace to stderr before the default action
+void install_crash_handler();
 void wait_for_stop();
 void write_ready_file(const std::string& json);  // $DFS_READY_FILE, if set
 

@@ -370,7 +370,10 @@ struct S3Front::Req {
   }
 };
 
-S3Front::S3Front(S3FrontConfig cfg, FastClient* fc) : cfg_(std::move(cfg)), fc_(fc) {}
+S3Front::S3Front(S3FrontConfig cfg, FastClient* fc)
+    : cfg_(std::move(cfg)), own_store_(std::make_unique<FastFrontStore>(fc)), fc_(own_store_.get()) {}
+
+S3Front::S3Front(S3FrontConfig cfg, FrontStore* store) : cfg_(std::move(cfg)), fc_(store) {}
 
 S3Front::~S3Front() {
   stop();
@@ -1160,7 +1163,7 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
   int64_t slot = fc_->acquire_slot(std::max<uint64_t>(stored, 1));
   if (slot < 0) return proxy(c, r, nullptr, 0, "no-slot");
   struct Release {
-    FastClient* fc;
+    FrontStore* fc;
     int64_t s;
     ~Release() { fc->release(s); }
   } rel{fc_, slot};
@@ -1297,7 +1300,7 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
     if (st != FastClient::Ok) return proxy(c, r, nullptr, 0, "read");
   }
   struct Release {
-    FastClient* fc;
+    FrontStore* fc;
     int64_t s;
     ~Release() {
       if (s >= 0) fc->release(s);
@@ -1631,7 +1634,7 @@ bool S3Front::sse_get(Conn* c, Req& r, const std::string& meta, uint64_t size, c
   FastClient::Times t;
   if (fc_->read_known(meta, &slot, &got, &msg, &t, r.rid, 0, 0) != FastClient::Ok) return proxy(c, r, nullptr, 0, "read");
   struct Release {
-    FastClient* fc;
+    FrontStore* fc;
     int64_t s;
     ~Release() {
       if (s >= 0) fc->release(s);

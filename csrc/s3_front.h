@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "client_fast.h"
+#include "front_store.h"
 #include "s3_policy.h"
 #include "tls.h"
 #include "io_pool.h"
@@ -83,7 +84,8 @@ struct S3FrontStats {
 
 class S3Front {
  public:
-  S3Front(S3FrontConfig cfg, FastClient* fc);
+  S3Front(S3FrontConfig cfg, FastClient* fc);     // co-located gateway
+  S3Front(S3FrontConfig cfg, FrontStore* store);  // any store (not owned), e.g. RemoteFrontStore
   ~S3Front();
   S3Front(const S3Front&) = delete;
   bool start(std::string* err);
@@ -131,7 +133,8 @@ class S3Front {
   std::string native_metrics();
 
   S3FrontConfig cfg_;
-  FastClient* fc_;
+  std::unique_ptr<FrontStore> own_store_;  // the FastClient adapter
+  FrontStore* fc_;
   std::shared_ptr<TlsContext> tls_;
   std::map<uint32_t, std::string> sts_keys_;
   std::unique_ptr<s3policy::IamPolicy> iam_;

@@ -117,6 +117,9 @@ class Client:
             if hedge_delay_ms:
                 self._remote.set_hedge_delay(int(hedge_delay_ms))
         self.remote_ops = 0
+        # other native objects that route by this client's shard map and masters (the S3
+        # front's RemoteFrontStore); kept in step by _sync_fast
+        self._routed_extra: list = []
         # ops that left the native clients for the Python path, by reason (VERDICT r2 weak #9:
         # fallbacks used to be silent); exported by the S3 gateway's /metrics
         self.native_fallbacks: dict[str, int] = {}
@@ -191,8 +194,13 @@ class Client:
             self.shard_map = m
         self._sync_fast()
 
+    def add_native_routing(self, nc) -> None:
+        """Keep `nc.set_routing(shard_map_json, masters)` in step with this client's routing."""
+        self._routed_extra.append(nc)
+        self._sync_fast()
+
     def _sync_fast(self) -> None:
-        for nc in (self._fast, getattr(self, "_remote", None)):
+        for nc in (self._fast, getattr(self, "_remote", None), *getattr(self, "_routed_extra", [])):
             if nc is not None:
                 with self._map_lock:
                     js = json.dumps(self.shard_map.to_json()) if self.shard_map.shards else ""

@@ -413,6 +413,10 @@ class LocalCluster:
         return pr
 
     def stop(self) -> None:
+        # DFS_KEEP_LOGS=<dir>: every process's log (and the exit status of any that died before
+        # the stop) survives the cluster's scratch directory, for post-mortems of benchmark runs
+        keep = os.environ.get("DFS_KEEP_LOGS")
+        died = {pr.name: pr.popen.returncode for pr in self.procs if pr.popen.poll() is not None}
         for pr in reversed(self.procs):
             if pr.popen.poll() is None:
                 try:
@@ -429,6 +433,13 @@ class LocalCluster:
                 except ProcessLookupError:
                     pass
                 pr.popen.wait(timeout=10)
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            for pr in self.procs:
+                if pr.log_path and os.path.exists(pr.log_path):
+                    shutil.copy(pr.log_path, os.path.join(keep, os.path.basename(pr.log_path)))
+            with open(os.path.join(keep, "exited_before_stop.json"), "w") as f:
+                json.dump(died, f)
         self.procs = []
         if self.owns_dir:
             shutil.rmtree(self.base, ignore_errors=True)

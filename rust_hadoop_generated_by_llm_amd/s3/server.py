@@ -207,6 +207,7 @@ class S3Gateway:
         self.policy_epoch = PolicyEpoch()
         self._policy_epoch_seen = self.policy_epoch.get()
         self.front = None  # the native front when it runs in this process (drop_policies on change)
+        self.front_store = None  # its RemoteFrontStore when no chunkserver is co-located
         r = self.registry
         self.m_requests = r.counter("s3_requests_total", "Total number of S3 requests", ("method", "path", "status"))
         self.m_auth = r.counter("iam_auth_requests_total", "Total authentication attempts", ("result", "error_type"))
@@ -1227,12 +1228,13 @@ def _die_with_parent() -> None:
 
 
 def native_front_wanted(cfg: S3Config) -> bool:
-    """The native front end (csrc/s3_front.cpp) serves the object data path when the gateway
-    is co-located with a chunkserver (its native client moves bodies through that server's
-    pinned shared memory). It terminates TLS itself (TLS_CERT / TLS_KEY, OpenSSL), like the
-    reference binds rustls directly (main.rs:263-274); the aiohttp workers behind it then
-    listen on a private UNIX socket in plain HTTP."""
-    if cfg.env.get("S3_NATIVE_FRONT", "true") != "true" or not cfg.local_chunkserver:
+    """The native front end (csrc/s3_front.cpp) serves the object data path. Co-located with a
+    chunkserver its native client moves bodies through that server's pinned shared memory; a
+    gateway on another host (no LOCAL_CHUNKSERVER) gives it a RemoteFrontStore, which speaks
+    gRPC to the masters and chunkservers (csrc/front_store.h). It terminates TLS itself
+    (TLS_CERT / TLS_KEY, OpenSSL), like the reference binds rustls directly (main.rs:263-274);
+    the aiohttp workers behind it then listen on a private UNIX socket in plain HTTP."""
+    if cfg.env.get("S3_NATIVE_FRONT", "true") != "true":
         return False
     try:
         from ..native import lib  # noqa: F401
@@ -1259,7 +1261,17 @@ def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_
 
     cfg = gw.cfg
     creds = gw.creds
-    front = lib.S3Front(gw.client._fast, host, port, backend,
+    store = gw.client._fast
+    if store is None:
+        # not co-located: private slots, every master / chunkserver call over gRPC (TLS when
+        # the gateway's client uses it), routed by the gateway client's shard map
+        store = lib.RemoteFrontStore("", [], slots=int(cfg.env.get("S3_FRONT_SLOTS", "32") or 32),
+                                     slot_bytes=int(cfg.env.get("S3_FRONT_SLOT_MB", "16") or 16) << 20,
+                                     ca_cert=cfg.ca_cert or "", domain_name=cfg.domain_name or "",
+                                     tls=bool(gw.client.tls))
+        gw.client.add_native_routing(store)
+        gw.front_store = store
+    front = lib.S3Front(store, host, port, backend,
                         workers=int(cfg.env.get("S3_FRONT_THREADS", "32") or 32),
                         auth_enabled=cfg.auth_enabled, region=cfg.region,
                         access_key=getattr(creds, "access_key", None) or "",
@@ -1277,7 +1289,7 @@ def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_
         raise RuntimeError(f"native S3 front end failed to start: {err}")
     gw.front = front
     if gw.client._fast is None:
-        log.warning("native front end without a co-located native client: every request goes to Python")
+        log.info("native front end for a gateway without a co-located chunkserver: gRPC to masters and chunkservers")
     return front
 
 

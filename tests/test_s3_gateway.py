@@ -59,7 +59,11 @@ class GatewayThread:
             from rust_hadoop_generated_by_llm_amd.native import lib
             from rust_hadoop_generated_by_llm_amd.s3.server import _audit_ingest
 
-            assert gw.client._fast is not None, "native front needs the co-located native client"
+            store = gw.client._fast
+            if store is None:  # a gateway on another host: as s3/server.py start_native_front
+                store = lib.RemoteFrontStore("", [], slots=16, slot_bytes=16 << 20)
+                gw.client.add_native_routing(store)
+                gw.front_store = store
             ingest = ""
             if gw.audit is not None:
                 ingest = os.path.join(self._dir, "ingest.sock")
@@ -76,7 +80,7 @@ class GatewayThread:
             epoch = os.path.join(self._dir, "policy_epoch")
             gw.policy_epoch = PolicyEpoch(epoch)
             gw._policy_epoch_seen = gw.policy_epoch.get()
-            self.front = lib.S3Front(gw.client._fast, "127.0.0.1", self.port, self.backend, workers=8,
+            self.front = lib.S3Front(store, "127.0.0.1", self.port, self.backend, workers=8,
                                      auth_enabled=cfg.auth_enabled, region=cfg.region,
                                      access_key=gw.creds.access_key or "", secret_key=gw.creds.secret_key or "",
                                      allow_unsigned_payload=cfg.allow_unsigned_payload,
@@ -108,8 +112,10 @@ class GatewayThread:
         shutil.rmtree(self._dir, ignore_errors=True)
 
 
-@pytest.fixture(scope="module", params=["python", "native"])
+@pytest.fixture(scope="module", params=["python", "native", "remote"])
 def front(request):
+    """python: aiohttp only; native: the native front co-located with a chunkserver (FastClient);
+    remote: the native front of a gateway on another host (RemoteFrontStore, gRPC only)."""
     return request.param
 
 
@@ -123,7 +129,7 @@ def cluster(front):
 def make_gw(cluster, env, front="python"):
     cfg = S3Config(env)
     client = cluster.client(local_chunkserver=cluster.cs_addrs[0]) if front == "native" else cluster.client()
-    return GatewayThread(build_gateway(cfg, client), native=front == "native")
+    return GatewayThread(build_gateway(cfg, client), native=front != "python")
 
 
 @pytest.fixture(scope="module")
@@ -709,7 +715,7 @@ def test_native_front_terminates_tls(cluster, front):
     """TLS_CERT/TLS_KEY with the native front (reference main.rs:263-274 binds rustls): the
     front does the handshake (OpenSSL) and serves objects natively over it; requests it hands
     to Python arrive there marked https, so S3_REQUIRE_TLS accepts them."""
-    if front != "native":
+    if front == "python":
         pytest.skip("native front end only")
     ca, crt, key = cluster.make_certs()
     url = cluster.start_s3({"AUDIT_LOG_ENABLED": "false", "TLS_CERT": crt, "TLS_KEY": key, "S3_REQUIRE_TLS": "true",
@@ -759,7 +765,7 @@ def test_sse_at_rest(cluster, front):
         assert g.gw.client.get_file_content("/sse/copy") != raw  # fresh DEK
         h = requests.head(f"{u}/sse/obj")
         assert h.headers["x-amz-server-side-encryption"] == "AES256" and int(h.headers["Content-Length"]) == len(raw)
-        if front == "native":  # encrypted and decrypted in the front, not handed to Python
+        if front != "python":  # encrypted and decrypted in the front, not handed to Python
             st = g.front.stats()
             assert st["sse_puts"] >= 1 and st["sse_gets"] >= 3, st
             assert st["proxy_reasons"].get("sse", 0) == 0, st
@@ -797,7 +803,7 @@ def test_sse_gateway_multipart(cluster, front):
         assert requests.get(f"{u}/ssempu/big").content == blob
         r = requests.get(f"{u}/ssempu/big", headers={"Range": "bytes=5242000-5243999"})
         assert r.status_code == 206 and r.content == blob[5242000:5244000]
-        if front == "native":
+        if front != "python":
             st = g.front.stats()
             assert st["proxy_reasons"].get("sse", 0) == 0 and st["mpu_completes"] >= 1, st
             assert st["mpu_initiates"] >= 1 and st["proxy_reasons"].get("query", 0) == 0, st
@@ -807,6 +813,8 @@ def test_sse_gateway_multipart(cluster, front):
 
 def _front_env(cluster, front):
     # the s3.server process runs its native front end when co-located with a chunkserver
+    if front == "remote":
+        return {}  # no chunkserver on this "host": the front speaks gRPC (RemoteFrontStore)
     return {"LOCAL_CHUNKSERVER": cluster.cs_addrs[0]} if front == "native" else {"S3_NATIVE_FRONT": "false"}
 
 
@@ -864,7 +872,7 @@ def test_native_front_serves_object_data(gw, front):
     """PUT / GET / HEAD / Range GET / UploadPart / multipart GET are served
     by the native front end (csrc/s3_front.cpp), bodies moving socket <-> shared-memory slot
     <-> chunkserver without the interpreter; bucket and MPU control calls go to Python."""
-    if front != "native":
+    if front == "python":
         pytest.skip("native front end only")
     u = gw.url
     s0 = gw.front.stats()
@@ -925,7 +933,7 @@ def test_native_front_evaluates_bucket_policies(authgw, front):
     """A bucket with a policy stays on the native path: the front evaluates the policy itself
     (csrc/s3_policy.cpp) and hands over only the requests it denies, which the gateway answers
     with 403 AccessDenied as before."""
-    if front != "native":
+    if front == "python":
         pytest.skip("native front end only")
     g = authgw
     assert signed("PUT", g, "/polnat").status_code == 200
@@ -957,7 +965,7 @@ def test_native_front_evaluates_bucket_policies(authgw, front):
 def test_native_front_auth_and_audit(authgw, front):
     """Signed requests with the static key are verified in C++ (csrc/sigv4.cpp) and audited
     into the same hash chain; a bad signature is handed to Python, which answers 403."""
-    if front != "native":
+    if front == "python":
         pytest.skip("native front end only")
     g = authgw
     s0 = g.front.stats()
