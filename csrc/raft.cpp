@@ -839,7 +839,11 @@ void Node::applier_loop() {
       }
       last_applied_ = std::max(last_applied_, batch.back().idx);
       check_reads_locked(cbs);
-      snap_due = last_applied_ - last_included_index_ > opt_.snapshot_threshold;
+      for (auto& e : batch) applied_bytes_since_snap_ += e.cmd.size();
+      // (a snapshot every 10,000 entries of a 450k-file namespace rewrote ~the whole state about
+      // once a second and held applies during each capture: rename p99 37 ms on the box)
+      snap_due = last_applied_ - last_included_index_ > opt_.snapshot_threshold &&
+                 2 * applied_bytes_since_snap_ >= last_snap_bytes_;
       if (snap_due && !snap_req_) {
         snap_req_ = true;
         snap_cv_.notify_one();
@@ -904,12 +908,17 @@ void Node::take_snapshot() {
       if (idx == 0 || idx <= last_included_index_) return;
       term = static_cast<uint64_t>(std::max<int64_t>(0, term_at(idx)));
       cfg = config_.to_json().dump();
+      applied_bytes_since_snap_ = 0;
     }
     state = host_->snapshot();
   }
   std::string data = "{\"meta\":[" + std::to_string(idx) + "," + std::to_string(term) + "],\"state\":" + state +
                      ",\"config\":" + cfg + "}";
   state.clear();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    last_snap_bytes_ = data.size();
+  }
   atomic_write_file(snap_path(), data, opt_.sync);
   bool leader;
   {

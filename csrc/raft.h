@@ -290,6 +290,11 @@ class Node {
   // so applies stall for the state capture, not for the snapshot file write and WAL rewrite
   std::condition_variable snap_cv_;
   bool snap_req_ = false;
+  // compaction pacing (mu_): command bytes applied since the last snapshot's capture, and that
+  // snapshot's size; a snapshot is due once the log holds both snapshot_threshold entries and
+  // half a snapshot's worth of bytes, so rewriting the state stays proportional to the log's
+  // growth however large the namespace is
+  uint64_t applied_bytes_since_snap_ = 0, last_snap_bytes_ = 0;
   void snapshot_loop();
   std::atomic<bool> running_{false};
   bool started_ = false;
