@@ -166,10 +166,14 @@ def config5(a):
 
     gpus = [a.gpu] if a.gpu >= 0 else None
     with LocalCluster(n_chunkservers=1, gpus=gpus, hbm_capacity="16G" if gpus else "0") as c:
-        env = {"AUDIT_LOG_ENABLED": "false", "LOCAL_CHUNKSERVER": c.cs_addrs[0]}
+        # --remote-gateway: the gateway as if on another host (no co-located chunkserver): its
+        # native front moves every body over gRPC (RemoteFrontStore) instead of shared memory
+        env = {"AUDIT_LOG_ENABLED": "false"} if a.remote_gateway else \
+            {"AUDIT_LOG_ENABLED": "false", "LOCAL_CHUNKSERVER": c.cs_addrs[0]}
         url = c.start_s3(env)
         out = {"config": 5, "topology": f"S3 gateway + 1 master + 1 chunkserver "
-                                        f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync"}
+                                        f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync",
+               "gateway": "remote: native front over gRPC" if a.remote_gateway else "co-located: native front over shm"}
         s = requests.Session()
         assert s.put(f"{url}/bench").status_code == 200
         n, size = a.count, a.size
@@ -479,6 +483,8 @@ def main():
     p.add_argument("--phase-seconds", type=float, default=10.0,
                    help="length of each native load phase (PUT / GET / Range / List / MPU upload / MPU GET)")
     p.add_argument("--mpu-object-mb", type=int, default=64, help="object size of the multipart-upload phase")
+    p.add_argument("--remote-gateway", action="store_true",
+                   help="config5: no LOCAL_CHUNKSERVER, the native front reaches the DFS over gRPC only")
     p.add_argument("--secure", action="store_true",
                    help="config5 with TLS + SigV4/STS session + IAM role + SSE-S3 (the reference's production settings)")
     a = p.parse_args()
