@@ -341,6 +341,7 @@ class ChunkStore {
   void enqueue_materialize_locked(const std::string& id, const Block& b);
   bool journal_takes(uint64_t n, uint64_t nslices);
   std::atomic<uint64_t> bypassed_{0};  // durable writes sent past a journal at its materialize mark
+  std::atomic<uint64_t> last_durable_write_ns_{0};  // any durable write, journaled or bypassed
   bool journal_bypass_ = true;
   void materializer_loop();
   bool materialize_due();
