@@ -299,10 +299,17 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
               ("multipart_upload", ["--op", "mpu", "--size", str(a.mpu_object_mb << 20), "--parts", str(a.mpu_parts),
                                     "--prefix", "natmpu", "--keys", "1"]),
               ("multipart_get", ["--op", "get", "--size", str(mpu_bytes), "--key", mpu_key, "--keys", "1"]))
+    from bench import cgroup_cpu, cgroup_cpu_delta
+
     for name, extra in phases:
         before = _front_counters(url)
+        cg0, t0 = cgroup_cpu(), time.perf_counter()
         r = subprocess.run(base + sec + extra, capture_output=True, text=True, timeout=a.phase_seconds * 4 + 300)
+        # the whole job's CPU during the phase (gateway, load generator, master, chunkserver
+        # share the box's quota): cores used, quota, throttled time
+        job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), time.perf_counter() - t0)
         res = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}
+        res["job_cpu"] = job_cpu
         after = _front_counters(url)
         res["front_requests"] = after["requests"] - before["requests"]
         # the closing /metrics scrape is itself one hand-off (answered by Python; its reason is
