@@ -236,7 +236,7 @@ def config5(a):
                             "get_mb_per_s": round(len(blob) / (1 << 20) / mpu_get_s, 1)}
         lg.close()
         out["parquet_over_s3"] = parquet_phase(url, a)
-        out["native_load"] = native_load_phase(url, a, len(blob))
+        out["native_load"] = native_load_phase(url, a, len(blob), cluster=c)
         out["load_generator"] = f"{a.concurrency} client processes (requests, keep-alive)"
         out["gateway_workers"] = int(os.environ.get("S3_WORKERS", "4"))
         # what the native front end served itself vs handed to the Python workers
@@ -271,7 +271,28 @@ def _front_counters(url: str) -> dict:
     return out
 
 
-def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mpu_key: str = "big.bin") -> dict:
+def _proc_cpu(cluster) -> dict:
+    """CPU seconds (user + system) of every cluster process and its children, by name, plus
+    this process's finished children (the load generator)."""
+    import resource
+
+    import psutil
+
+    out = {}
+    for pr in (cluster.procs if cluster is not None else []):
+        try:
+            ps = psutil.Process(pr.popen.pid)
+            kids = [ps] + ps.children(recursive=True)
+            out[pr.name] = sum(sum(k.cpu_times()[:2]) for k in kids)
+        except psutil.Error:
+            pass
+    ru = resource.getrusage(resource.RUSAGE_CHILDREN)
+    out["load_generator"] = ru.ru_utime + ru.ru_stime
+    return out
+
+
+def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mpu_key: str = "big.bin",
+                      cluster=None) -> dict:
     """PUT / GET / Range GET 64 KiB / ListObjectsV2 / multipart upload / multipart GET against
     the gateway from the native load generator (build/native/s3_load: C++ HTTP/1.1 clients,
     one keep-alive connection per thread), so the numbers describe the gateway, not Python's
@@ -303,13 +324,16 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
 
     for name, extra in phases:
         before = _front_counters(url)
-        cg0, t0 = cgroup_cpu(), time.perf_counter()
+        cg0, pc0, t0 = cgroup_cpu(), _proc_cpu(cluster), time.perf_counter()
         r = subprocess.run(base + sec + extra, capture_output=True, text=True, timeout=a.phase_seconds * 4 + 300)
         # the whole job's CPU during the phase (gateway, load generator, master, chunkserver
-        # share the box's quota): cores used, quota, throttled time
-        job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), time.perf_counter() - t0)
+        # share the box's quota): cores used, quota, throttled time; and cores per process
+        el = time.perf_counter() - t0
+        job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), el)
+        pc1 = _proc_cpu(cluster)
         res = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}
         res["job_cpu"] = job_cpu
+        res["cores_by_process"] = {k: round((v - pc0.get(k, 0.0)) / el, 2) for k, v in pc1.items()}
         after = _front_counters(url)
         res["front_requests"] = after["requests"] - before["requests"]
         # the closing /metrics scrape is itself one hand-off (answered by Python; its reason is
@@ -433,7 +457,8 @@ def config5_secure(a):
                         "--count", "1", "--size", str(a.mpu_parts * (8 << 20)), "--parts", str(a.mpu_parts),
                         "--prefix", "seed", "--keys", "1", "--tls", "--ak", creds["ak"], "--sk", creds["sk"],
                         "--token", creds["token"]], check=True, capture_output=True, timeout=300)
-        out["native_load"] = native_load_phase(url, a, a.mpu_parts * (8 << 20), creds, mpu_key="seed_mpu_0_0")
+        out["native_load"] = native_load_phase(url, a, a.mpu_parts * (8 << 20), creds, mpu_key="seed_mpu_0_0",
+                                               cluster=c)
         emit(out)
 
 
