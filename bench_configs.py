@@ -291,6 +291,23 @@ def _proc_cpu(cluster) -> dict:
     return out
 
 
+_CS_KEYS = ("journal_records", "journal_bypassed", "materialized_blocks", "materialize_batches",
+            "journal_sync_rounds", "journal_full_waits", "direct_writes", "writes", "disk_gate_waits")
+
+
+def _cs_counters(cluster) -> dict:
+    """Durable-path counters of the first chunkserver (its /stats), for per-phase deltas."""
+    if cluster is None or not cluster.cs_http:
+        return {}
+    try:
+        import urllib.request
+
+        st = json.loads(urllib.request.urlopen(cluster.cs_http[0] + "/stats", timeout=5).read())
+    except (OSError, ValueError):
+        return {}
+    return {k: st.get(k, 0) for k in _CS_KEYS if isinstance(st.get(k, 0), (int, float))}
+
+
 def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mpu_key: str = "big.bin",
                       cluster=None) -> dict:
     """PUT / GET / Range GET 64 KiB / ListObjectsV2 / multipart upload / multipart GET against
@@ -324,7 +341,7 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
 
     for name, extra in phases:
         before = _front_counters(url)
-        cg0, pc0, t0 = cgroup_cpu(), _proc_cpu(cluster), time.perf_counter()
+        cg0, pc0, cs0, t0 = cgroup_cpu(), _proc_cpu(cluster), _cs_counters(cluster), time.perf_counter()
         r = subprocess.run(base + sec + extra, capture_output=True, text=True, timeout=a.phase_seconds * 4 + 300)
         # the whole job's CPU during the phase (gateway, load generator, master, chunkserver
         # share the box's quota): cores used, quota, throttled time; and cores per process
@@ -334,6 +351,7 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
         res = json.loads(r.stdout) if r.stdout.strip() else {"error": r.stderr[-500:]}
         res["job_cpu"] = job_cpu
         res["cores_by_process"] = {k: round((v - pc0.get(k, 0.0)) / el, 2) for k, v in pc1.items()}
+        res["chunkserver"] = {k: v - cs0.get(k, 0) for k, v in _cs_counters(cluster).items()}
         after = _front_counters(url)
         res["front_requests"] = after["requests"] - before["requests"]
         # the closing /metrics scrape is itself one hand-off (answered by Python; its reason is
