@@ -283,7 +283,9 @@ def _proc_cpu(cluster) -> dict:
         try:
             ps = psutil.Process(pr.popen.pid)
             kids = [ps] + ps.children(recursive=True)
-            out[pr.name] = sum(sum(k.cpu_times()[:2]) for k in kids)
+            times = [k.cpu_times() for k in kids]
+            out[pr.name] = sum(t.user + t.system for t in times)
+            out[pr.name + "_sys"] = sum(t.system for t in times)  # kernel time (page cache, fs, flushes)
         except psutil.Error:
             pass
     ru = resource.getrusage(resource.RUSAGE_CHILDREN)

@@ -189,6 +189,18 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
                                        cfg_.disk_inflight < 0 ? disk_inflight_default() : cfg_.disk_inflight);
   if (gpu()) {
     HIP_OK(hipSetDevice(cfg_.device));
+    // how host threads wait for the device (every staging / read waits on an event):
+    // DFS_HIP_SYNC=spin (busy-wait), yield, block (sleep until the completion interrupt);
+    // unset = the runtime's default. Must precede the device's first use in the process.
+    if (const char* hs = std::getenv("DFS_HIP_SYNC")) {
+      const std::string m = hs;
+      const unsigned f = m == "spin" ? hipDeviceScheduleSpin : m == "yield" ? hipDeviceScheduleYield
+                         : m == "block" ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+      if (hipSetDeviceFlags(f) != hipSuccess) {
+        (void)hipGetLastError();
+        std::fprintf(stderr, "[store] DFS_HIP_SYNC=%s ignored: the device was already in use\n", hs);
+      }
+    }
     uint64_t cap = cfg_.hbm_capacity;
     if (cap == 0) {
       size_t fr = 0, tot = 0;
