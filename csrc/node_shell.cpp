@@ -272,9 +272,15 @@ namespace {
 void on_fatal(int sig) {
   void* frames[64];
   const int n = backtrace(frames, 64);
-  char head[96];
-  const int len = std::snprintf(head, sizeof(head), "FATAL signal %d (%s); backtrace:\n", sig, strsignal(sig));
-  if (len > 0) (void)!::write(2, head, static_cast<size_t>(len));
+  // no snprintf / strsignal here (not async-signal-safe): the number, written by hand
+  char head[48] = "FATAL signal ";
+  size_t len = std::strlen(head);
+  if (sig >= 10) head[len++] = static_cast<char>('0' + sig / 10);
+  head[len++] = static_cast<char>('0' + sig % 10);
+  const char tail[] = "; backtrace:\n";
+  std::memcpy(head + len, tail, sizeof(tail) - 1);
+  len += sizeof(tail) - 1;
+  (void)!::write(2, head, len);
   backtrace_symbols_fd(frames, n, 2);
   ::signal(sig, SIG_DFL);
   ::raise(sig);
