@@ -247,7 +247,10 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.sync = cfg_.sync_writes;
     mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 70) / 100.0;
     journal_bypass_ = env_int("DFS_JOURNAL_BYPASS", 1) != 0;  // 0: writers wait for the materializer
-    mat_idle_ns_ = static_cast<uint64_t>(env_int("DFS_JOURNAL_IDLE_MS", 100)) * 1000000ull;
+    // 500 ms: the pauses of a running benchmark (barriers, device syncs, a warm-up's end) are
+    // shorter, so a batch and its syncfs do not land on the first timed writes (with 100 ms,
+    // 256 blocks were materialized there and the driver's run lost 15-25 %: r4o, r4y)
+    mat_idle_ns_ = static_cast<uint64_t>(env_int("DFS_JOURNAL_IDLE_MS", 500)) * 1000000ull;
     journal_ = std::make_unique<BlockJournal>(jc);
     replay_journal();
   }
@@ -2653,7 +2656,13 @@ void ChunkStore::materializer_loop() {
         mat_cv_.wait_for(lk, std::chrono::milliseconds(mat_paused_ ? 50 : 5));
       }
       uint64_t bytes = 0;
-      while (!mat_q_.empty() && batch.size() < 1024 && bytes < (256ull << 20)) {
+      // a drain in a pause goes in small batches (one syncfs each) and re-checks for writers
+      // between them, so writers that resume wait for at most one small batch; under pressure,
+      // or when asked to drain, the batches are large
+      const bool urgent = mat_stop_ || mat_force_ > 0 || mat_idle_ns_ == 0 ||
+                          journal_->pressure() >= (journal_bypass_ ? 0.97 : mat_pressure_);
+      const uint64_t cap_bytes = urgent ? (256ull << 20) : (32ull << 20);
+      while (!mat_q_.empty() && batch.size() < 1024 && (bytes < cap_bytes || batch.empty())) {
         Job j;
         j.m = std::move(mat_q_.front());
         mat_q_.pop_front();
