@@ -147,13 +147,32 @@ def prefix_of(rank: int) -> str:
     return f"/bench_r{rank:03d}"
 
 
+def launch_ranks(gpus: int) -> int:
+    """`bench.py --gpus N` started without a launcher: run the N ranks under
+    torch.distributed.run as a CHILD process (this process has not touched the GPU and never
+    will; it is not replaced by exec) and return its exit code. The JSON line comes from the
+    children's rank 0, on this process's stdout."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    print(f"[bench] --gpus {gpus} without a launcher: starting {gpus} ranks under torch.distributed.run",
+          file=sys.stderr, flush=True)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env, cwd=str(ROOT))
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world != a.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {a.gpus}", file=sys.stderr)
+    if world != a.gpus:
+        # the reported n_gpus must be what ran: refuse rather than mislabel the run
+        print(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}; start N ranks (or omit the launcher)",
+              file=sys.stderr)
+        sys.exit(2)
     n = max(world, 1)
 
     import torch
@@ -222,7 +241,12 @@ def main():
     env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
     env.setdefault("DFS_LOG", "warning")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if journal_segs > 0:
+    if _journal_store_mode():
+        # the journal is the store of record and grows on demand: prepare (create and write
+        # out once) as many segments as this run's replicas need up front, within the volume
+        if journal_segs > 0:
+            env.setdefault("DFS_JOURNAL_SPARES", str(journal_segs))
+    elif journal_segs > 0:
         env.setdefault("DFS_JOURNAL_SEGS", str(journal_segs))
     elif journal_segs < 0:
         env["DFS_JOURNAL"] = "0"
@@ -450,6 +474,12 @@ def main():
 
         # counters of the timed phase only (the stress / remote phases below add their own hops)
         stats = cs_stats()
+        vol = {"rank_dir_bytes": _allocated_bytes(base_p / f"rank{rank}"),
+               "journal_used_bytes": stats.get("journal_used_bytes", 0),
+               "journal_live_bytes": stats.get("journal_live_bytes", 0),
+               "exported_blocks": stats.get("materialized_blocks", 0),
+               "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else (
+                   stats.get("journal_mode", "journal") if stats.get("journal") else "per-file")}
         stress = None
         if a.stress_seconds > 0:
             # the reference's only published throughput (stress-write 30 s, 10240 B,
@@ -487,7 +517,7 @@ def main():
             rc.close()
         allr = gather({"elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
                        "rbytes": rbytes, "wt": wt,
-                       "rt": rt, "cs": stats, "stress": stress, "remote": remote,
+                       "rt": rt, "cs": stats, "stress": stress, "remote": remote, "vol": vol,
                        "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
                        "cpu": host_cpu, "job_cpu": job_cpu, "settle": journal_settle_s, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                    for k, v in (client.phase_times or {}).items() if v}})
@@ -512,7 +542,8 @@ def main():
                            "files_per_gpu_per_step": a.count, "file_size": a.size, "concurrency": a.concurrency,
                            "replication_factor": min(3, n), "durability": a.durability,
                            "store": "cpu" if a.cpu else "hbm",
-                           "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else "journal",
+                           "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else (
+                               "journal (store of record)" if _journal_store_mode() else "journal (round-4 ring)"),
                            "transport": observed_transport(allr, n)},
                 "write_mb_per_s": round(sum(r["wbytes"] for r in allr) / (1 << 20) / wmax, 2),
                 "read_mb_per_s": round(sum(r["rbytes"] for r in allr) / (1 << 20) / rmax, 2),
@@ -549,8 +580,14 @@ def main():
                     ("prepare_errors", "journal_prepare_errors"),
                     ("materialize_errors", "materialize_errors"), ("sync_ns", "journal_sync_ns"),
                     ("commit_ns", "journal_commit_ns"), ("bypassed", "journal_bypassed"),
-                    ("parts_unready", "journal_parts_unready"))} | {
+                    ("parts_unready", "journal_parts_unready"), ("live_records", "journal_live_records"),
+                    ("segments_in_use", "journal_segs_in_use"), ("segments_marked", "journal_segs_marked"),
+                    ("relocated_blocks", "relocated_blocks"), ("supersedes", "journal_supersedes"),
+                    ("export_deferred_headroom", "export_deferred_headroom"))} | {
+                    "mode": ",".join(sorted({r["cs"].get("journal_mode", "?") for r in allr})),
                     "settle_s_before_warmup": max(r["settle"] for r in allr)} if any(r["cs"].get("journal") for r in allr) else None,
+                # where each rank's replicas live and how much of the volume they take
+                "volume": {"per_rank": [r["vol"] for r in allr], "free_bytes_after": _free_bytes(base_p)},
                 "host_cpu_util_rank0": allr[0]["cpu"],
                 # the whole job's CPU over the timed region, from the cgroup every rank shares
                 # (cores used, the quota, and time the quota throttled it); null without cgroup
@@ -708,29 +745,63 @@ def _bytes_needed(a, n: int) -> int:
 
 
 JOURNAL_SEG_BYTES = 256 << 20
+# a 256 MiB segment = 8 parts of 32 MiB; a 1 MiB block's record is 1 MiB + 12 KiB (header and
+# .meta page), 31 to a part: 96.8 % of a segment is block bytes
+JOURNAL_SEG_DATA = int(JOURNAL_SEG_BYTES * 0.96)
+
+
+def _journal_store_mode() -> bool:
+    return os.environ.get("DFS_JOURNAL_EXPORT", "store") != "idle"
 
 
 def _journal_segments(parent: Path, need: int, n: int) -> int:
-    """Segments per chunkserver for the block journal, so that the N journals plus every
-    materialized replica of this run fit the volume together (the journal's segments are
-    recycled, not freed: at N=8 x RF 3 the run's blocks alone approach a 79 GB volume).
-    0 = leave the chunkservers' default (16 x 256 MiB); -1 = the journal cannot hold this
-    run's blocks on this volume, so every block would be written twice inside the timed
-    region (journal, then materialized): use the per-file path instead."""
-    if os.environ.get("DFS_JOURNAL_SEGS") or os.environ.get("DFS_JOURNAL"):
+    """Journal segments per chunkserver for this run.
+
+    Store of record (default): the journal holds the run's replicas in about one copy's
+    space and grows on demand; the returned count is how many segments each chunkserver
+    prepares (creates and writes out once) before the timed region, so the timed appends
+    overwrite written extents. Bounded by the volume (what does not fit is created on
+    demand, never a per-file fallback). 0 = the chunkservers' default.
+
+    Round-4 mode (DFS_JOURNAL_EXPORT=idle): a ring of segments recycled by the materializer,
+    sized to hold the run below the 70 % mark; -1 = the ring cannot hold this run on this
+    volume: the per-file path instead."""
+    if os.environ.get("DFS_JOURNAL_SEGS") or os.environ.get("DFS_JOURNAL") or os.environ.get("DFS_JOURNAL_SPARES"):
         return 0
     try:
         free = shutil.disk_usage(parent).free
     except OSError:
         return 0
-    budget = (free - int(need * 1.15) - (2 << 30)) // max(1, n)
     per_cs = need // max(1, n)
+    if _journal_store_mode():
+        want = -(-per_cs // JOURNAL_SEG_DATA) + 1
+        budget = (free - (4 << 30)) // max(1, n) // JOURNAL_SEG_BYTES
+        return int(max(4, min(want, budget)))
+    budget = (free - int(need * 1.15) - (2 << 30)) // max(1, n)
     # enough segments to hold the run below the materializer's 70 % mark, two spare
     want = -(-int(per_cs / 0.7) // JOURNAL_SEG_BYTES) + 2
     segs = int(max(3, min(64, want, budget // JOURNAL_SEG_BYTES)))
     if segs * JOURNAL_SEG_BYTES * 0.7 < per_cs:
         return -1
     return segs
+
+
+def _allocated_bytes(d: Path) -> int:
+    tot = 0
+    for root, _dirs, files in os.walk(d):
+        for f in files:
+            try:
+                tot += os.lstat(os.path.join(root, f)).st_blocks * 512
+            except OSError:
+                pass
+    return tot
+
+
+def _free_bytes(d: Path) -> int:
+    try:
+        return shutil.disk_usage(d).free
+    except OSError:
+        return -1
 
 
 def _make_room(parent: Path, need: int) -> None:

@@ -359,6 +359,8 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("debug_pause_materializer", &ChunkStore::debug_pause_materializer,
            py::call_guard<py::gil_scoped_release>())
       .def("journaled", &ChunkStore::journaled)
+      .def("compact", &ChunkStore::compact, py::call_guard<py::gil_scoped_release>(), py::arg("max_live") = 1.0,
+           "relocate the live records of the oldest journal segment(s) holding at most max_live of their capacity")
       .def("stats", [](ChunkStore& s) {
         StoreStats t = s.stats();
         py::dict d;
@@ -390,7 +392,21 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["journal_bytes"] = t.journal_bytes;
         d["journal_commits"] = t.journal_commits;
         d["journal_sync_rounds"] = t.journal_sync_rounds;
+        d["journal_mode"] = t.journal_mode;
         d["journal_tombstones"] = t.journal_tombstones;
+        d["journal_supersedes"] = t.journal_supersedes;
+        d["journal_segs_in_use"] = t.journal_segs_in_use;
+        d["journal_segs_marked"] = t.journal_segs_marked;
+        d["journal_replay_verified"] = t.journal_replay_verified;
+        d["journal_live_records"] = t.journal_live_records;
+        d["journal_live_bytes"] = t.journal_live_bytes;
+        d["journal_used_bytes"] = t.journal_used_bytes;
+        d["journal_grow_blocked"] = t.journal_grow_blocked;
+        d["relocated_blocks"] = t.relocated_blocks;
+        d["relocated_bytes"] = t.relocated_bytes;
+        d["compactions"] = t.compactions;
+        d["export_deferred_headroom"] = t.export_deferred_headroom;
+        d["scrub_device_blocks"] = t.scrub_device_blocks;
         d["journal_full_waits"] = t.journal_full_waits;
         d["journal_segs"] = t.journal_segs;
         d["journal_segs_free"] = t.journal_segs_free;
@@ -599,6 +615,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def_property_readonly("peer", [](PyTicket& k) { return k.t.peer; })
       .def_property_readonly("gen", [](PyTicket& k) { return k.t.gen; })
       .def_property_readonly("seq", [](PyTicket& k) { return k.t.seq; })
+      .def_property_readonly("ch", [](PyTicket& k) { return k.t.ch; })
       .def_property_readonly("size", [](PyTicket& k) { return k.t.size; })
       .def_property_readonly("slice", [](PyTicket& k) { return k.t.slice; });
 
@@ -623,17 +640,24 @@ PYBIND11_MODULE(_dfs_native, m) {
 
   py::class_<ReplicationEngine>(m, "ReplicationEngine")
       .def(py::init([](ChunkStore* store, const std::string& transport, int rank, int world, const std::string& ns,
-                       int open_timeout_ms, int turn_timeout_ms, int xfer_timeout_ms) {
+                       int open_timeout_ms, int turn_timeout_ms, int xfer_timeout_ms, int channels) {
              std::string err;
              std::unique_ptr<P2PTransport> t;
-             if (transport == "rccl") t = make_rccl_transport(store->config().device, rank, &err);
-             else if (transport == "socket") t = make_socket_transport(rank, ns);
-             else if (transport == "hiploop" && store->gpu()) t = make_hiploop_transport(store->config().device, rank, ns);
+             if (channels <= 0) {
+               // DFS_REPL_CHANNELS (default 4); RCCL: DFS_REPL_CHANNELS_RCCL (default 1: every
+               // channel costs two communicators per pair)
+               const char* e = std::getenv(transport == "rccl" ? "DFS_REPL_CHANNELS_RCCL" : "DFS_REPL_CHANNELS");
+               channels = e && *e ? std::atoi(e) : (transport == "rccl" ? 1 : 4);
+             }
+             if (transport == "rccl") t = make_rccl_transport(store->config().device, rank, channels, &err);
+             else if (transport == "socket") t = make_socket_transport(rank, ns, channels);
+             else if (transport == "hiploop" && store->gpu())
+               t = make_hiploop_transport(store->config().device, rank, ns, channels);
              else if (transport == "hipipc" || transport == "hipipc-spin") {
                const char* sp = std::getenv("DFS_IPC_SPIN");
                bool spin = transport == "hipipc-spin" || (sp && std::string(sp) == "1");
                t = make_ipc_transport(store->config().device, rank, ns, store->arena_base(), store->arena_bytes(), spin,
-                                      &err);
+                                      channels, &err);
              }
              else err = "unknown transport " + transport;
              if (!t) throw std::runtime_error(err);
@@ -641,11 +665,13 @@ PYBIND11_MODULE(_dfs_native, m) {
              o.open_timeout_ms = open_timeout_ms;
              o.turn_timeout_ms = turn_timeout_ms;
              o.xfer_timeout_ms = xfer_timeout_ms;
+             o.channels = t->channels();
              return std::make_unique<ReplicationEngine>(store, std::move(t), rank, world, o);
            }),
            py::keep_alive<1, 2>(), py::arg("store"), py::arg("transport"), py::arg("rank"), py::arg("world"),
            py::arg("ns") = "", py::arg("open_timeout_ms") = 20000, py::arg("turn_timeout_ms") = 3000,
-           py::arg("xfer_timeout_ms") = 20000)
+           py::arg("xfer_timeout_ms") = 20000, py::arg("channels") = 0)
+      .def_property_readonly("channels", &ReplicationEngine::channels)
       .def("start", &ReplicationEngine::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &ReplicationEngine::stop, py::call_guard<py::gil_scoped_release>())
       .def("wait_ready", &ReplicationEngine::wait_ready, py::call_guard<py::gil_scoped_release>(), py::arg("timeout_ms"),
@@ -695,15 +721,15 @@ PYBIND11_MODULE(_dfs_native, m) {
         k.keep = py::none();
       })
       .def("recv", [](ReplicationEngine& e, int src, uint64_t gen, int64_t seq, const std::string& id, uint64_t size,
-                      uint64_t slice, uint32_t crc, bool persist) {
+                      uint64_t slice, uint32_t crc, bool persist, int ch) {
         WriteResult w;
         {
           py::gil_scoped_release r;
-          w = e.recv(src, gen, seq, id, size, slice, crc, persist);
+          w = e.recv(src, gen, ch, seq, id, size, slice, crc, persist);
         }
         return py::make_tuple(w.ok, w.actual_crc, w.error);
       }, py::arg("src"), py::arg("gen"), py::arg("seq"), py::arg("block_id"), py::arg("size"), py::arg("slice"),
-         py::arg("crc"), py::arg("persist") = true)
+         py::arg("crc"), py::arg("persist") = true, py::arg("ch") = 0)
       .def("debug_drop_sends", [](ReplicationEngine& e, int peer, int n) { e.transport()->debug_drop_sends(peer, n); })
       .def("debug_stall", [](ReplicationEngine& e, int peer, int ms) { e.transport()->debug_stall(peer, ms); })
       .def("stats", [](ReplicationEngine& e) {
@@ -718,6 +744,8 @@ PYBIND11_MODULE(_dfs_native, m) {
         d["open_attempts"] = s.open_attempts;
         d["turn_timeouts"] = s.turn_timeouts;
         d["stale_generation"] = s.stale_generation;
+        d["channel_waits"] = s.channel_waits;
+        d["channels"] = e.channels();
         d["parked_extents"] = s.parked_extents;
         d["reaped_extents"] = s.reaped_extents;
         return d;

@@ -5,6 +5,8 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/statvfs.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -232,12 +234,33 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
   int jmode = cfg_.journal;
   if (jmode < 0) jmode = env_int("DFS_JOURNAL", 1);
   if (jmode > 0 && cfg_.sync_writes && cfg_.durability == Durability::NvmeSync) {
+    // DFS_JOURNAL_EXPORT: store (default: the journal is the block's home; reference-format
+    // files are exported at a bounded rate while the volume has headroom), never (no export
+    // except on request), idle (round 4: everything materialized once the writers pause)
+    const char* em = std::getenv("DFS_JOURNAL_EXPORT");
+    const std::string emode = em && *em ? em : "store";
+    store_mode_ = emode != "idle";
+    export_ = emode != "never";
+    export_bps_ = env_int("DFS_EXPORT_MBPS", 256) * 1e6;
+    compact_live_ = env_int("DFS_COMPACT_LIVE_PCT", 50) / 100.0;
+    uint64_t vol_total = 0;
+    {
+      struct statvfs sv;
+      if (::statvfs(cfg_.storage_dir.c_str(), &sv) == 0) vol_total = static_cast<uint64_t>(sv.f_blocks) * sv.f_frsize;
+    }
+    // export doubles a block's footprint until its segment recycles: only while the volume
+    // keeps this much free (default 25 % of it, at least 8 GiB)
+    export_headroom_ = static_cast<uint64_t>(env_int("DFS_EXPORT_HEADROOM_MB", 0)) << 20;
+    if (export_headroom_ == 0) export_headroom_ = std::max<uint64_t>(8ull << 30, vol_total / 4);
     JournalConfig jc;
     jc.dir = cfg_.storage_dir + "/.journal";
     jc.seg_bytes = static_cast<uint64_t>(env_int("DFS_JOURNAL_SEG_MB", 256)) << 20;
-    jc.max_segs = env_int("DFS_JOURNAL_SEGS", 16);
+    jc.grow = store_mode_;
+    jc.max_segs = env_int("DFS_JOURNAL_SEGS", store_mode_ ? 0 : 16);
+    jc.reserve_bytes = static_cast<uint64_t>(env_int("DFS_JOURNAL_RESERVE_MB", 0)) << 20;
+    if (jc.reserve_bytes == 0) jc.reserve_bytes = std::max<uint64_t>(2ull << 30, vol_total / 50);
     jc.direct = env_int("DFS_JOURNAL_DIRECT", 0) != 0;
-    jc.spares = env_int("DFS_JOURNAL_SPARES", 2);
+    jc.spares = env_int("DFS_JOURNAL_SPARES", store_mode_ ? 4 : 2);
     jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 1) != 0;
     jc.idle_fill_ms = env_int("DFS_JOURNAL_IDLE_FILL_MS", 20);
     jc.syncers = env_int("DFS_JOURNAL_SYNCERS", 1);
@@ -260,7 +283,9 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
 
 ChunkStore::~ChunkStore() {
   if (materializer_.joinable()) {
-    {  // a clean stop writes every journal record out, so nothing is left to replay
+    {  // round-4 mode: a clean stop writes every journal record out (one pass; what fails
+       // stays in the journal and is replayed); store mode: the journal is the home, the
+       // exporter just stops
       std::lock_guard<std::mutex> g(mu_);
       mat_stop_ = true;
       mat_paused_ = false;
@@ -272,7 +297,11 @@ ChunkStore::~ChunkStore() {
       std::lock_guard<std::mutex> g(mu_);
       drained = mat_q_.empty() && mat_errors_ == 0;
     }
-    if (drained && !journal_->stats().failed) journal_->retire_all();
+    if (store_mode_) {
+      journal_->mark_sealed_now();  // the next start trusts these records
+      journal_->retire_ready();     // and finds no dead segment (the active one is sealed now)
+    }
+    else if (drained && !journal_->stats().failed) journal_->retire_all();
   }
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -317,6 +346,7 @@ void ChunkStore::scan_dirs() {
       }
       // dot names: the journal directory, quarantined files (block ids never start with '.')
       if (name.empty() || name[0] == '.' || ends_with(name, ".meta")) continue;
+      if (index_.count(name)) continue;  // replayed from the journal, its home
       int64_t sz = file_size(dir + "/" + name);
       if (sz < 0) continue;
       // a data file is a block only with its complete .meta beside it: anything else is a
@@ -859,6 +889,7 @@ WriteResult ChunkStore::stage(const std::string& id, const uint8_t* data, uint64
 void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, uint64_t n, uint32_t crc, bool on_disk,
                                  std::shared_ptr<std::vector<uint8_t>> meta, int pins, const JournalRec* jr) {
   bool hbm_ack = cfg_.durability == Durability::HbmAck;
+  JournalRec old;  // the replaced version's journal record, if any: no longer referenced
   {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = index_.find(id);
@@ -867,6 +898,7 @@ void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, ui
       free_extent_locked(it->second);
       lru_remove_locked(it->second);
       drop_mirror_locked(it->second);
+      old = it->second.jrec;
       if (it->second.cold) {  // the new version lives in the hot dir
         ::unlink(data_path(id, true).c_str());
         ::unlink(meta_path(id, true).c_str());
@@ -894,6 +926,7 @@ void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, ui
     if (!on_disk && !jr && hbm_ack) spill_q_.push_back(id);
   }
   cv_.notify_all();
+  if (old.seg) journal_->release(old);
 }
 
 // H2D + checksum of a host buffer into `ext` on one lane; the BE .meta image comes back in
@@ -965,6 +998,8 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
   }
   bool sync_now = durable_now && cfg_.durability == Durability::NvmeSync;
   if (sync_now && journal_takes(n, num_slices(n))) return stage_journal(id, data, n, expected_crc, ext);
+  std::unique_ptr<FileClaim> claim;  // the exporter keeps off the id's files until indexed
+  if (sync_now && journal_) claim = std::make_unique<FileClaim>(this, id);
   // nvme-sync: the data file (the slow part: page-cache write + device flush) is written
   // and fdatasync'ed on a helper thread WHILE the GPU stages and checksums the block; the
   // .meta (known only after the CRC kernel) follows. A checksum mismatch removes the file.
@@ -1111,6 +1146,12 @@ WriteResult ChunkStore::stage_impl(const std::string& id, const uint8_t* data, u
     res.error = err;
     return res;
   }
+  if (sync_now && !supersede_file(id, &err)) {
+    if (fresh) unclaim_fresh(id);
+    release(ext);
+    res.error = err;
+    return res;
+  }
   insert_resident(id, ext, n, co.block_crc, sync_now, meta);
   if (fresh) unclaim_fresh(id);  // indexed now: a later write of the id takes the tmp path
   if (n <= kMirrorMax) set_mirror(id, data, n, *meta);
@@ -1214,12 +1255,14 @@ bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64
   bool ok, jok = false;
   JournalRec jr;
   const bool from_host = host_data && n == size;
+  std::unique_ptr<FileClaim> claim;
   if (journal_takes(size, meta->size() / 4)) {
     ok = jok = journal_block(id, from_host ? host_data : nullptr, from_host ? nullptr : d, size, crc, *meta, &jr, err);
-  } else if (from_host) {
-    ok = persist(id, false, host_data, size, meta->data(), meta->size() / 4, err);
   } else {
-    ok = persist_from_device(id, d, size, meta->data(), meta->size() / 4, err);
+    if (journal_) claim = std::make_unique<FileClaim>(this, id);
+    ok = from_host ? persist(id, false, host_data, size, meta->data(), meta->size() / 4, err)
+                   : persist_from_device(id, d, size, meta->data(), meta->size() / 4, err);
+    ok = ok && supersede_file(id, err);
   }
   bool obsolete = jok;
   {
@@ -1241,7 +1284,7 @@ bool ChunkStore::persist(const std::string& id, const uint8_t* host_data, uint64
       }
     }
   }
-  if (obsolete) journal_->materialized(jr.seg, 1);  // the block changed meanwhile: record unused
+  if (obsolete) journal_->release(jr);  // the block changed meanwhile: record unused
   cv_.notify_all();
   return ok;
 }
@@ -1303,8 +1346,9 @@ WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, u
   crc32_slices(data, n, sl.data());
   for (auto& v : sl) v = __builtin_bswap32(v);
   std::string err;
-  JournalRec jr;
+  JournalRec jr, old;
   std::shared_ptr<std::vector<uint8_t>> jmeta;
+  std::unique_ptr<FileClaim> claim;
   const bool jok = journal_takes(n, S);
   if (jok) {
     jmeta = std::make_shared<std::vector<uint8_t>>(reinterpret_cast<const uint8_t*>(sl.data()),
@@ -1313,14 +1357,19 @@ WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, u
       res.error = err;
       return res;
     }
-  } else if (!persist(id, false, data, n, reinterpret_cast<const uint8_t*>(sl.data()), S, &err)) {
-    res.error = err;
-    return res;
+  } else {
+    if (journal_) claim = std::make_unique<FileClaim>(this, id);
+    if (!persist(id, false, data, n, reinterpret_cast<const uint8_t*>(sl.data()), S, &err) ||
+        !supersede_file(id, &err)) {
+      res.error = err;
+      return res;
+    }
   }
   {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = index_.find(id);
-    if (it != index_.end()) cv_.wait(lk, [&] { return it->second.pins == 0; });  // materializer / readers
+    if (it != index_.end()) cv_.wait(lk, [&] { return it->second.pins == 0; });  // exporter / readers
+    if (it != index_.end()) old = it->second.jrec;
     if (it != index_.end() && it->second.cold) {
       ::unlink(data_path(id, true).c_str());
       ::unlink(meta_path(id, true).c_str());
@@ -1339,6 +1388,7 @@ WriteResult ChunkStore::write_host(const std::string& id, const uint8_t* data, u
     }
   }
   cv_.notify_all();
+  if (old.seg) journal_->release(old);
   res.ok = true;
   return res;
 }
@@ -1742,8 +1792,10 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
   bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
   JournalRec jr;
   const bool jok = sync_now && journal_takes(n, S);
+  std::unique_ptr<FileClaim> claim;
+  if (sync_now && !jok && journal_) claim = std::make_unique<FileClaim>(this, id);
   if (jok ? !journal_block(id, nullptr, ext.ptr, n, co.block_crc, *meta, &jr, &err)
-          : sync_now && !persist_from_device(id, ext.ptr, n, meta->data(), S, &err)) {
+          : sync_now && (!persist_from_device(id, ext.ptr, n, meta->data(), S, &err) || !supersede_file(id, &err))) {
     release(ext);
     res.error = err;
     return res;
@@ -1819,8 +1871,11 @@ WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint3
   bool sync_now = persist_now && cfg_.durability == Durability::NvmeSync;
   JournalRec jr;
   const bool jok = sync_now && journal_takes(n, S);
+  std::unique_ptr<FileClaim> claim;
+  if (sync_now && !jok && journal_) claim = std::make_unique<FileClaim>(this, id);
   if (jok ? !journal_block(id, nullptr, rv->ext.ptr, n, crc, *meta, &jr, &err)
-          : sync_now && !persist_from_device(id, rv->ext.ptr, n, meta->data(), S, &err)) {
+          : sync_now && (!persist_from_device(id, rv->ext.ptr, n, meta->data(), S, &err) ||
+                         !supersede_file(id, &err))) {
     release(rv->ext);
     res.error = err;
     return res;
@@ -1968,6 +2023,7 @@ uint32_t ChunkStore::block_crc(const std::string& id) {
 
 bool ChunkStore::remove(const std::string& id) {
   bool cold = false, durable = true;
+  JournalRec old;
   {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = index_.find(id);
@@ -1975,6 +2031,7 @@ bool ChunkStore::remove(const std::string& id) {
     cv_.wait(lk, [&] { return it->second.pins == 0; });
     cold = it->second.cold;
     durable = it->second.on_disk || it->second.jrec.seg != nullptr;
+    old = it->second.jrec;
     free_extent_locked(it->second);
     lru_remove_locked(it->second);
     drop_mirror_locked(it->second);
@@ -1982,10 +2039,15 @@ bool ChunkStore::remove(const std::string& id) {
   }
   cv_.notify_all();
   // an unretired journal record of the block would bring it back on replay (a block that
-  // never became durable, e.g. an EC gather copy, has none)
-  if (journal_ && durable) journal_->tombstone(id);
+  // never became durable, e.g. an EC gather copy, has none): the tombstone is committed
+  // before the delete returns
+  if (journal_ && durable) {
+    std::string err;
+    if (!journal_->marker(kJrTomb, id, &err)) std::fprintf(stderr, "[store] tombstone %s: %s\n", id.c_str(), err.c_str());
+  }
   ::unlink(data_path(id, cold).c_str());
   ::unlink(meta_path(id, cold).c_str());
+  if (old.seg) journal_->release(old);
   return true;
 }
 
@@ -2183,20 +2245,26 @@ std::vector<std::string> ChunkStore::scrub() {
     for (auto& id : scrub_resident(resident)) bad.push_back(id);
     for (auto& id : resident) unpin(id);
   }
-  for (auto& id : disk)
-    if (!verify_on_disk(id).empty()) bad.push_back(id);
-  // resident blocks are also checked against their NVMe copy when one exists
-  if (gpu())
+  // durable copies (journal records, files): the non-resident blocks, and the resident
+  // blocks' copies, verified by the same K1b kernel in staged batches (the CPU takes what
+  // does not fit a batch)
+  std::vector<std::string> cpu;
+  if (gpu()) {
+    std::vector<std::string> copies = disk;
     for (auto& id : resident) {
-      bool on_disk;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        auto it = index_.find(id);
-        on_disk = it != index_.end() && (it->second.on_disk || it->second.jrec.seg) && !it->second.dirty;
-      }
-      if (on_disk && std::find(bad.begin(), bad.end(), id) == bad.end() && !verify_on_disk(id).empty())
-        bad.push_back(id);
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = index_.find(id);
+      if (it != index_.end() && (it->second.on_disk || it->second.jrec.seg) && !it->second.dirty &&
+          std::find(bad.begin(), bad.end(), id) == bad.end())
+        copies.push_back(id);
     }
+    for (auto& id : scrub_durable_gpu(copies, &cpu))
+      if (std::find(bad.begin(), bad.end(), id) == bad.end()) bad.push_back(id);
+  } else {
+    cpu = disk;
+  }
+  for (auto& id : cpu)
+    if (!verify_on_disk(id).empty() && std::find(bad.begin(), bad.end(), id) == bad.end()) bad.push_back(id);
   std::lock_guard<std::mutex> g(mu_);
   st_.crc_mismatches += bad.size();
   return bad;
@@ -2234,6 +2302,7 @@ StoreStats ChunkStore::stats() {
   s.mirror_hits = mirror_hits_;
   s.mirror_bytes = mirror_bytes_;
   s.io_threads_spawned = io_.spawned();
+  s.scrub_device_blocks = scrub_dev_blocks_.load();
   if (journal_) {
     JournalStats j = journal_->stats();
     s.journal = true;
@@ -2241,14 +2310,27 @@ StoreStats ChunkStore::stats() {
     s.journal_bytes = j.bytes;
     s.journal_commits = j.commits;
     s.journal_sync_rounds = j.sync_rounds;
+    s.journal_mode = !store_mode_ ? "idle" : export_ ? "store" : "store-noexport";
     s.journal_tombstones = j.tombstones;
+    s.journal_supersedes = j.supersedes;
     s.journal_full_waits = j.full_waits;
     s.journal_segs = j.segs_total;
     s.journal_segs_free = j.segs_free;
+    s.journal_segs_in_use = j.segs_in_use;
+    s.journal_segs_marked = j.segs_marked;
     s.journal_segs_retired = j.segs_retired;
     s.journal_replayed = j.replayed;
     s.journal_replay_skipped = j.replay_skipped;
+    s.journal_replay_verified = j.replay_verified;
+    s.journal_live_records = j.live_records;
+    s.journal_live_bytes = j.live_bytes;
+    s.journal_used_bytes = j.used_bytes;
     s.journal_failed = j.failed;
+    s.journal_grow_blocked = j.grow_blocked;
+    s.relocated_blocks = relocated_blocks_;
+    s.relocated_bytes = relocated_bytes_;
+    s.compactions = compactions_;
+    s.export_deferred_headroom = export_deferred_;
     s.materialized_blocks = materialized_blocks_;
     s.materialized_bytes = materialized_bytes_;
     s.materialize_pending = mat_q_.size();
@@ -2461,6 +2543,22 @@ bool ChunkStore::open_durable(const std::string& id, bool cold, const JournalRec
   return s->meta_ok;
 }
 
+ChunkStore::FileClaim::FileClaim(ChunkStore* st, const std::string& i) : s(st), id(i) {
+  std::lock_guard<std::mutex> g(s->mu_);
+  s->file_writers_[id]++;
+}
+
+ChunkStore::FileClaim::~FileClaim() {
+  std::lock_guard<std::mutex> g(s->mu_);
+  auto it = s->file_writers_.find(id);
+  if (it != s->file_writers_.end() && --it->second <= 0) s->file_writers_.erase(it);
+}
+
+bool ChunkStore::supersede_file(const std::string& id, std::string* err) {
+  if (!journal_) return true;
+  return journal_->marker(kJrFile, id, err);
+}
+
 bool ChunkStore::journal_block(const std::string& id, const uint8_t* host, const uint8_t* dev, uint64_t n,
                                uint32_t crc, const std::vector<uint8_t>& meta_be, JournalRec* out, std::string* err) {
   TraceRange tr("dfs.store.journal");
@@ -2500,9 +2598,9 @@ bool ChunkStore::journal_block(const std::string& id, const uint8_t* host, const
     journal_->abandon(jr);
     return false;
   }
-  if (!journal_->finish(jr, id, n, crc, meta_be.data(), S) || !journal_->commit(jr)) {
+  if (!journal_->finish(&jr, id, n, crc, meta_be.data(), S) || !journal_->commit(jr)) {
     *err = "journal commit failed";
-    journal_->materialized(jr.seg, 1);  // never indexed
+    journal_->release(jr);  // never indexed
     return false;
   }
   *out = jr;
@@ -2513,7 +2611,7 @@ bool ChunkStore::journal_block(const std::string& id, const uint8_t* host, const
 // record (from the caller's buffer, on an I/O thread) while the GPU stages and checksums
 // them; the header + .meta image follow once the kernel has produced them, and one group
 // commit makes the record durable. The block is acked resident in HBM and durable in the
-// journal; its `<id>` + `<id>.meta` files are written later by the materializer.
+// journal, which stays its durable home until the exporter writes `<id>` + `<id>.meta`.
 WriteResult ChunkStore::stage_journal(const std::string& id, const uint8_t* data, uint64_t n, uint32_t expected_crc,
                                       const DevExtent& ext) {
   WriteResult res;
@@ -2548,8 +2646,8 @@ WriteResult ChunkStore::stage_journal(const std::string& id, const uint8_t* data
     }
     return res;
   }
-  if (!journal_->finish(jr, id, n, co.block_crc, meta->data(), S) || !journal_->commit(jr)) {
-    journal_->materialized(jr.seg, 1);
+  if (!journal_->finish(&jr, id, n, co.block_crc, meta->data(), S) || !journal_->commit(jr)) {
+    journal_->release(jr);
     release(ext);
     res.error = "journal commit failed";
     return res;
@@ -2560,17 +2658,17 @@ WriteResult ChunkStore::stage_journal(const std::string& id, const uint8_t* data
   return res;
 }
 
-// A durable write goes to the journal while the journal has room below the materializer's
-// mark. Past it the materializer is already writing every journaled block a second time, so a
-// write through the journal would cost the volume twice; it takes the per-file path instead
-// (written once), and the journal takes writes again once the materializer has caught up.
+// Store of record: every durable write that fits a segment part goes to the journal. Round-4
+// mode: while the journal has room below the materializer's mark; past it the materializer
+// is already writing every journaled block a second time, so a write through the journal
+// would cost the volume twice; it takes the per-file path instead (written once).
 bool ChunkStore::journal_takes(uint64_t n, uint64_t nslices) {
   if (!journal_ || !journal_->fits(n, nslices)) return false;
   last_durable_write_ns_.store(static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                                          std::chrono::steady_clock::now().time_since_epoch())
                                                          .count()),
                                std::memory_order_relaxed);
-  if (!journal_bypass_ || journal_->pressure() < mat_pressure_) return true;
+  if (store_mode_ || !journal_bypass_ || journal_->pressure() < mat_pressure_) return true;
   bypassed_++;
   return false;
 }
@@ -2580,13 +2678,11 @@ void ChunkStore::enqueue_materialize_locked(const std::string& id, const Block& 
   mat_cv_.notify_all();
 }
 
-// Materialization competes with the acked writes for the volume, so it runs when the
-// writers pause (idle: no durable write, journaled or not, for DFS_JOURNAL_IDLE_MS), not on
-// every append. Without the bypass it also runs once the journal is at its mark (the writers
-// would block on a full journal otherwise). With the bypass, writes past the mark already go
-// to their own files, written once; draining the journal during that burst would add a second
-// write of every journaled block (and its syncfs) to the same volume, so it waits for a pause
-// (config 5's 10 s PUT phase: 2.2 GB/s at p99 67 ms with both running).
+// Round-4 mode: materialization competes with the acked writes for the volume, so it runs
+// when the writers pause (idle: no durable write, journaled or not, for DFS_JOURNAL_IDLE_MS),
+// not on every append. Without the bypass it also runs once the journal is at its mark (the
+// writers would block on a full journal otherwise). With the bypass, writes past the mark
+// already go to their own files, written once.
 bool ChunkStore::materialize_due() {
   if (mat_idle_ns_ == 0) return true;
   const double p = journal_->pressure();
@@ -2596,6 +2692,15 @@ bool ChunkStore::materialize_due() {
                                                  .count());
   const uint64_t last = std::max<uint64_t>(journal_->last_append_ns(), last_durable_write_ns_.load());
   return now - last >= mat_idle_ns_;
+}
+
+// Export doubles a block's footprint until its journal segment recycles; it runs only while
+// the volume keeps export_headroom_ free besides the batch (a full node keeps its blocks in
+// the journal, which holds them in about one copy's space).
+bool ChunkStore::export_headroom(uint64_t bytes) {
+  struct statvfs sv;
+  if (::statvfs(cfg_.storage_dir.c_str(), &sv) != 0) return false;
+  return static_cast<uint64_t>(sv.f_bavail) * sv.f_frsize >= export_headroom_ + bytes;
 }
 
 namespace {
@@ -2628,120 +2733,320 @@ bool copy_range(int in_fd, uint64_t in_off, int out_fd, uint64_t n) {
 }
 }  // namespace
 
-void ChunkStore::materializer_loop() {
+// Writes each pinned job as `<id>` + `<id>.meta` under private temporary names, starts the
+// writeback of all of them at once (sync_file_range) and then flushes each file
+// (fdatasync: per file, not the whole filesystem), renames each into place only while its
+// record is still the block's current version and no per-file writer holds the id (checked
+// and renamed under mu_, so an export never lands over a newer per-file version), and
+// flushes the directory once. A block whose names are durable leaves the journal: its index
+// entry points at the files and its record is released.
+uint64_t ChunkStore::export_batch(std::vector<MatItem>& batch, bool retry) {
+  TraceRange tr("dfs.store.export");
   struct Job {
-    MatItem m;
-    bool current = false, ok = false;
     int fd = -1, mfd = -1;
-    std::string err;
+    bool ok = false, renamed = false, claimed = false;
+    std::string dtmp, mtmp, err;
   };
-  std::vector<Job> batch;
+  std::vector<Job> jobs(batch.size());
+  for (size_t i = 0; i < batch.size(); ++i) {
+    Job& j = jobs[i];
+    const MatItem& m = batch[i];
+    const std::string sfx = ".x" + std::to_string(tmp_seq_.fetch_add(1)) + ".tmp";
+    j.dtmp = data_path(m.id, false) + sfx;
+    j.mtmp = meta_path(m.id, false) + sfx;
+    j.fd = ::open(j.dtmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    j.mfd = j.fd < 0 ? -1 : ::open(j.mtmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    j.ok = j.mfd >= 0 && copy_range(m.rec.fd(), m.rec.data_off(), j.fd, m.n) &&
+           write_all(j.mfd, m.meta->data(), m.meta->size(), 0);
+    if (!j.ok) j.err = errno_str(j.dtmp.c_str());
+  }
+  if (cfg_.sync_writes) {
+    for (auto& j : jobs)
+      if (j.ok) {
+        (void)::sync_file_range(j.fd, 0, 0, SYNC_FILE_RANGE_WRITE);
+        (void)::sync_file_range(j.mfd, 0, 0, SYNC_FILE_RANGE_WRITE);
+      }
+    for (auto& j : jobs)
+      if (j.ok && (::fdatasync(j.fd) != 0 || ::fdatasync(j.mfd) != 0)) {
+        j.ok = false;
+        j.err = errno_str("fdatasync " + j.dtmp);
+      }
+  }
+  const bool drop = gpu();
+  for (auto& j : jobs) {
+    if (j.fd >= 0) {
+      if (drop) drop_cached(j.fd);
+      ::close(j.fd);
+    }
+    if (j.mfd >= 0) ::close(j.mfd);
+  }
+  bool any = false;
+  for (size_t i = 0; i < batch.size(); ++i) {
+    Job& j = jobs[i];
+    if (j.ok) {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = index_.find(batch[i].id);
+      const bool current = it != index_.end() && it->second.jrec.same(batch[i].rec);
+      j.claimed = file_writers_.count(batch[i].id) > 0;
+      if (current && !j.claimed) {
+        // .meta first: a crash between the renames leaves a .meta with no data file (ignored)
+        if (::rename(j.mtmp.c_str(), meta_path(batch[i].id, false).c_str()) == 0 &&
+            ::rename(j.dtmp.c_str(), data_path(batch[i].id, false).c_str()) == 0) {
+          j.renamed = any = true;
+        } else {
+          j.ok = false;
+          j.err = errno_str("rename " + j.dtmp);
+        }
+      }
+    }
+    if (!j.renamed) {
+      ::unlink(j.dtmp.c_str());
+      ::unlink(j.mtmp.c_str());
+    }
+  }
+  // the names are durable once the directory is: only then does the index leave the journal
+  const bool dir_ok = !any || !cfg_.sync_writes || sync_dir(false);
+  std::vector<JournalRec> released;
+  uint64_t exported = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < batch.size(); ++i) {
+      Job& j = jobs[i];
+      MatItem& m = batch[i];
+      auto it = index_.find(m.id);
+      if (it == index_.end()) continue;
+      it->second.pins--;
+      if (!it->second.jrec.same(m.rec)) continue;  // rewritten meanwhile: that version counts
+      if (j.renamed && dir_ok) {
+        it->second.on_disk = true;
+        it->second.jrec = JournalRec{};
+        it->second.jmeta.reset();
+        released.push_back(m.rec);
+        ++materialized_blocks_;
+        materialized_bytes_ += m.n;
+        ++exported;
+        continue;
+      }
+      if (!j.ok || !dir_ok) {
+        ++mat_errors_;
+        mat_last_error_ = j.ok ? errno_str("fsync " + cfg_.storage_dir) : j.err;
+      }
+      // still journal-resident: the record stays its durable copy; try again later (a
+      // per-file writer that fails leaves the record current)
+      if (retry) mat_q_.push_back(std::move(m));
+    }
+    ++mat_batches_;
+  }
+  cv_.notify_all();
+  for (auto& r : released) journal_->release(r);
+  return exported;
+}
+
+// Moves one journal-resident block's record to the head of the journal, keeping its LSN
+// (a rewrite committed meanwhile has a larger one, so replay still prefers it). The block is
+// pinned while it moves: writers of the id and remove() wait, so a tombstone is never
+// appended before the copy it must cancel. A copy that lost the race with a rewrite is made
+// durable padding before the old record is given up.
+bool ChunkStore::relocate_one(const std::string& id, const JournalRec& old) {
+  std::shared_ptr<std::vector<uint8_t>> meta;
+  uint64_t n = 0;
+  uint32_t crc = 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end() || !it->second.jrec.same(old) || !it->second.jmeta) return false;
+    it->second.pins++;
+    meta = it->second.jmeta;
+    n = it->second.size;
+    crc = it->second.crc;
+  }
+  const uint64_t S = meta->size() / 4;
+  std::vector<uint8_t> buf(n);
+  bool ok = n == 0 || read_all(old.fd(), buf.data(), n, old.data_off());
+  JournalRec nr;
+  std::string err;
+  bool appended = false;
+  if (ok && journal_->reserve(n, S, &nr, &err)) {
+    if (!journal_->write(nr, 0, buf.data(), n)) {
+      journal_->abandon(nr);
+    } else {
+      appended = journal_->finish(&nr, id, n, crc, meta->data(), S, old.lsn) && journal_->commit(nr);
+      if (!appended) journal_->release(nr);
+    }
+  }
+  bool swapped = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(id);
+    if (it != index_.end()) {
+      it->second.pins--;
+      if (appended && it->second.jrec.same(old)) {
+        it->second.jrec = nr;
+        swapped = true;
+        ++relocated_blocks_;
+        relocated_bytes_ += n;
+        enqueue_materialize_locked(id, it->second);  // the queued item names the old record
+      }
+    }
+  }
+  cv_.notify_all();
+  if (swapped) {
+    journal_->release(old);
+  } else if (appended) {
+    journal_->pad_durable(nr);
+    journal_->release(nr);
+  }
+  return swapped;
+}
+
+uint64_t ChunkStore::relocate_segment(const SegRef& seg, uint64_t budget_bytes) {
+  std::lock_guard<std::mutex> cg(compact_mu_);
+  std::vector<std::pair<std::string, JournalRec>> todo;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : index_)
+      if (kv.second.jrec.seg == seg) todo.emplace_back(kv.first, kv.second.jrec);
+  }
+  // in record order: the copies land in the head in the order they were written
+  std::sort(todo.begin(), todo.end(), [](const auto& a, const auto& b) {
+    return a.second.part != b.second.part ? a.second.part < b.second.part : a.second.off < b.second.off;
+  });
+  uint64_t moved = 0, bytes = 0;
+  for (auto& t : todo) {
+    if (bytes >= budget_bytes) break;
+    if (relocate_one(t.first, t.second)) {
+      ++moved;
+      bytes += t.second.bytes();
+    }
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (bytes < budget_bytes) ++compactions_;  // the segment is empty now (unless it raced)
+  }
+  journal_->retire_ready();
+  return bytes;
+}
+
+uint64_t ChunkStore::compact(double max_live) {
+  if (!journal_ || !store_mode_) return 0;
+  uint64_t before;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    before = relocated_blocks_;
+  }
+  for (;;) {
+    SegRef seg = journal_->compaction_candidate(max_live);
+    if (!seg) break;
+    relocate_segment(seg, UINT64_MAX);
+    if (journal_->compaction_candidate(max_live) == seg) break;  // pinned by readers / raced
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  return relocated_blocks_ - before;
+}
+
+// The exporter / compaction thread. Store mode: journal-resident blocks are exported as
+// reference-format files through a token bucket (DFS_EXPORT_MBPS) at idle I/O priority,
+// while the volume has headroom; without headroom (or with export off) the oldest segment is
+// compacted once enough of the journal is dead. Round-4 mode: everything is materialized
+// when the writers pause (materialize_due). Either way materialize_all() forces a full
+// export, and a stop ends after at most one failed pass (what failed stays in the journal).
+void ChunkStore::materializer_loop() {
+  if (store_mode_) {
+    // idle I/O class for this thread (honoured by the BFQ / CFQ schedulers; the token bucket
+    // is what bounds it everywhere)
+    constexpr long kWhoProcess = 1, kClassIdle = 3, kClassShift = 13;
+    (void)::syscall(SYS_ioprio_set, kWhoProcess, 0L, kClassIdle << kClassShift);
+  }
+  const double burst = 64.0 * (1 << 20);
+  double tokens = burst;
+  auto t_prev = std::chrono::steady_clock::now();
+  bool headroom = false, stop_failed = false;
+  auto headroom_at = t_prev;
+  std::vector<MatItem> batch;
   for (;;) {
     batch.clear();
+    uint64_t bytes = 0;
+    bool compact_now = false, forced = false;
     {
       std::unique_lock<std::mutex> lk(mu_);
       for (;;) {
-        if (mat_q_.empty()) {
-          mat_cv_.notify_all();  // materialize_all() waiters
-          if (mat_stop_) return;
-          mat_cv_.wait_for(lk, std::chrono::milliseconds(200));
-          if (mat_q_.empty()) {
-            lk.unlock();
-            journal_->retire_ready();  // segments whose readers have finished since
-            lk.lock();
-          }
+        const auto t = std::chrono::steady_clock::now();
+        tokens = std::min(burst, tokens + export_bps_ * std::chrono::duration<double>(t - t_prev).count());
+        t_prev = t;
+        if (mat_q_.empty() && !mat_busy_) mat_cv_.notify_all();  // materialize_all() waiters
+        if (mat_stop_ && (store_mode_ || mat_q_.empty() || stop_failed)) return;
+        if (mat_paused_) {
+          mat_cv_.wait_for(lk, std::chrono::milliseconds(50));
           continue;
         }
-        if (!mat_paused_ && (mat_stop_ || mat_force_ > 0 || materialize_due())) break;
-        mat_cv_.wait_for(lk, std::chrono::milliseconds(mat_paused_ ? 50 : 5));
-      }
-      uint64_t bytes = 0;
-      // a drain in a pause goes in small batches (one syncfs each) and re-checks for writers
-      // between them, so writers that resume wait for at most one small batch; under pressure,
-      // or when asked to drain, the batches are large
-      const bool urgent = mat_stop_ || mat_force_ > 0 || mat_idle_ns_ == 0 ||
-                          journal_->pressure() >= (journal_bypass_ ? 0.97 : mat_pressure_);
-      const uint64_t cap_bytes = urgent ? (256ull << 20) : (32ull << 20);
-      while (!mat_q_.empty() && batch.size() < 1024 && (bytes < cap_bytes || batch.empty())) {
-        Job j;
-        j.m = std::move(mat_q_.front());
-        mat_q_.pop_front();
-        bytes += j.m.n;
-        auto it = index_.find(j.m.id);
-        // pinned while its files are written: a rewrite or remove() of the id waits for it
-        j.current = it != index_.end() && it->second.jrec.seg == j.m.rec.seg && it->second.jrec.part == j.m.rec.part && it->second.jrec.off == j.m.rec.off;
-        if (j.current) it->second.pins++;
-        batch.push_back(std::move(j));
-      }
-      mat_busy_ = true;
-    }
-    TraceRange tr("dfs.store.materialize");
-    for (auto& j : batch) {
-      if (!j.current) continue;
-      const std::string dp = data_path(j.m.id, false), mp = meta_path(j.m.id, false);
-      j.fd = ::open(dp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-      j.mfd = j.fd < 0 ? -1 : ::open(mp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-      j.ok = j.mfd >= 0 && copy_range(j.m.rec.fd(), j.m.rec.data_off(), j.fd, j.m.n) &&
-             write_all(j.mfd, j.m.meta->data(), j.m.meta->size(), 0);
-      if (!j.ok) j.err = errno_str(dp.c_str());
-    }
-    // one flush for the whole batch: syncfs() of the storage filesystem covers every file
-    // written above and the directory entries (instead of two fdatasyncs per block)
-    bool any = false;
-    for (auto& j : batch) any = any || j.ok;
-    bool dir_ok = true;
-    if (any && cfg_.sync_writes) {
-      int dfd = ::open(cfg_.storage_dir.c_str(), O_RDONLY | O_DIRECTORY | O_CLOEXEC);
-      dir_ok = dfd >= 0 && ::syncfs(dfd) == 0;
-      if (!dir_ok)
-        for (auto& j : batch)
-          if (j.ok) j.err = errno_str("syncfs");
-      if (dfd >= 0) ::close(dfd);
-    }
-    const bool drop = gpu();
-    for (auto& j : batch) {
-      if (j.fd >= 0) {
-        if (drop) drop_cached(j.fd);
-        ::close(j.fd);
-      }
-      if (j.mfd >= 0) ::close(j.mfd);
-      if (!dir_ok) j.ok = false;
-    }
-    std::vector<Job*> retry;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      for (auto& j : batch) {
-        if (!j.current) continue;
-        auto it = index_.find(j.m.id);
-        if (it != index_.end()) {
-          it->second.pins--;
-          if (j.ok) {
-            it->second.on_disk = true;
-            it->second.jrec = JournalRec{};
-            it->second.jmeta.reset();
-            ++materialized_blocks_;
-            materialized_bytes_ += j.m.n;
+        forced = mat_force_ > 0 || mat_stop_;
+        if (!mat_q_.empty()) {
+          if (forced) break;
+          if (!store_mode_) {
+            if (materialize_due()) break;
+          } else if (export_ && tokens >= std::min<double>(burst, static_cast<double>(mat_q_.front().n))) {
+            if (t >= headroom_at) {
+              lk.unlock();
+              headroom = export_headroom(64ull << 20);
+              lk.lock();
+              headroom_at = t + std::chrono::milliseconds(500);
+              if (!headroom) ++export_deferred_;
+            }
+            if (headroom) break;
           }
         }
-        if (!j.ok) {
-          ++mat_errors_;
-          mat_last_error_ = j.err;
-          retry.push_back(&j);
+        if (store_mode_ && tokens >= burst / 2) {
+          lk.unlock();
+          const JournalStats j = journal_->stats();
+          compact_now = (j.grow_blocked || (j.used_bytes && j.used_bytes - j.live_bytes > j.used_bytes / 4)) &&
+                        journal_->compaction_candidate(compact_live_) != nullptr;
+          lk.lock();
+          if (compact_now && !mat_paused_ && !mat_stop_) break;
+          compact_now = false;
         }
+        if (!store_mode_ && mat_q_.empty()) {
+          lk.unlock();
+          journal_->retire_ready();  // segments whose readers have finished since
+          lk.lock();
+        }
+        mat_cv_.wait_for(lk, std::chrono::milliseconds(store_mode_ ? 50 : mat_q_.empty() ? 200 : 5));
       }
-      for (auto* j : retry) mat_q_.push_back(j->m);  // the record stays live until its files are durable
-      ++mat_batches_;
+      if (!compact_now) {
+        // a drain in a pause goes in small batches and re-checks for writers between them;
+        // under pressure, or when asked to drain, the batches are large; the store mode's
+        // batches are what the token bucket allows
+        const bool urgent = forced || (!store_mode_ && (mat_idle_ns_ == 0 ||
+                                                         journal_->pressure() >= (journal_bypass_ ? 0.97 : mat_pressure_)));
+        const uint64_t cap = urgent ? (256ull << 20) : store_mode_ ? static_cast<uint64_t>(std::max(tokens, 1.0))
+                                                                   : (32ull << 20);
+        while (!mat_q_.empty() && batch.size() < 1024 && (bytes < cap || batch.empty())) {
+          MatItem m = std::move(mat_q_.front());
+          mat_q_.pop_front();
+          auto it = index_.find(m.id);
+          if (it == index_.end() || !it->second.jrec.same(m.rec)) continue;  // superseded: nothing to do
+          it->second.pins++;  // a rewrite or remove() of the id waits for the export
+          bytes += m.n;
+          batch.push_back(std::move(m));
+        }
+        mat_busy_ = !batch.empty();
+      }
+    }
+    if (compact_now) {
+      SegRef seg = journal_->compaction_candidate(compact_live_);
+      if (seg) tokens -= static_cast<double>(relocate_segment(seg, static_cast<uint64_t>(std::max(tokens, 1.0))));
+      continue;
+    }
+    if (batch.empty()) continue;
+    const size_t want = batch.size();
+    const uint64_t done = export_batch(batch, !mat_stop_);
+    tokens -= static_cast<double>(bytes);
+    {
+      std::lock_guard<std::mutex> g(mu_);
       mat_busy_ = false;
+      if (done < want && mat_stop_) stop_failed = true;
     }
-    cv_.notify_all();
     mat_cv_.notify_all();
-    for (auto& j : batch)
-      if (!j.current || j.ok) journal_->materialized(j.m.rec.seg, 1);
-    if (!retry.empty()) {
-      std::fprintf(stderr, "[store] materializing %zu block(s) failed, retrying: %s\n", retry.size(),
-                   retry.front()->err.c_str());
-      std::this_thread::sleep_for(std::chrono::milliseconds(100));
-    }
+    if (done < want && !mat_stop_ && !forced) std::this_thread::sleep_for(std::chrono::milliseconds(100));
   }
 }
 
@@ -2751,7 +3056,9 @@ void ChunkStore::materialize_all() {
   if (mat_paused_) return;
   ++mat_force_;
   mat_cv_.notify_all();
-  mat_cv_.wait(lk, [&] { return (mat_q_.empty() && !mat_busy_) || mat_paused_ || mat_stop_; });
+  // failures are requeued: give up once a pass made no progress for a while
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(60);
+  mat_cv_.wait_until(lk, deadline, [&] { return (mat_q_.empty() && !mat_busy_) || mat_paused_ || mat_stop_; });
   --mat_force_;
 }
 
@@ -2769,42 +3076,13 @@ bool ChunkStore::journaled(const std::string& id) {
   return it != index_.end() && it->second.jrec.seg != nullptr;
 }
 
-// Restart: the records of unretired segments, latest state per block id, are verified
-// (slice CRCs of the data against the record's .meta image and the whole-block CRC; on the
-// GPU by the K1/K2 kernels) and written out as `<id>` + `<id>.meta`; tombstoned ids lose
-// their files. Then every segment is retired and scan_dirs() indexes the result.
 void ChunkStore::replay_journal() {
   std::vector<ReplayRecord> recs = journal_->recover();
-  std::unordered_map<std::string, long> last;  // id -> index of its final record (-1: deleted)
-  for (size_t i = 0; i < recs.size(); ++i)
-    last[recs[i].id] = recs[i].type == kJrBlock ? static_cast<long>(i) : -1;
-  uint64_t replayed = 0, skipped = 0;
-  bool cold_touched = false;
-  std::vector<uint8_t> buf;
-  std::string err;
-  for (auto& kv : last) {
-    const std::string& id = kv.first;
-    if (!valid_block_id(id)) {
-      ++skipped;
-      continue;
-    }
-    if (!cfg_.cold_dir.empty() && file_exists(data_path(id, true))) {
-      // the journal holds the latest write of the id: it replaces a cold copy
-      ::unlink(data_path(id, true).c_str());
-      ::unlink(meta_path(id, true).c_str());
-      cold_touched = true;
-    }
-    if (kv.second < 0) {
-      ::unlink(data_path(id, false).c_str());
-      ::unlink(meta_path(id, false).c_str());
-      continue;
-    }
-    const ReplayRecord& r = recs[static_cast<size_t>(kv.second)];
+  // a replayed block record's data against its .meta image and whole-block CRC (K1/K2 on
+  // the GPU for blocks past the host-mirror size)
+  auto verify = [&](const ReplayRecord& r, std::vector<uint8_t>& buf) {
     buf.resize(r.n);
-    if (!read_all(r.fd(), buf.data(), r.n, r.data_off) && r.n) {
-      ++skipped;
-      continue;
-    }
+    if (r.n && !read_all(r.fd(), buf.data(), r.n, r.data_off())) return false;
     std::vector<uint32_t> sl;
     uint32_t whole;
     if (gpu() && r.n > kMirrorMax) {
@@ -2820,9 +3098,130 @@ void ChunkStore::replay_journal() {
       std::memcpy(&be, r.meta_be.data() + 4 * i, 4);
       good = __builtin_bswap32(be) == sl[i];
     }
-    if (!good) {  // torn: never acknowledged (prefix order), so dropping it loses nothing
+    return good;
+  };
+  uint64_t replayed = 0, skipped = 0, verified = 0;
+  bool cold_touched = false, hot_touched = false;
+  std::vector<uint8_t> buf;
+  auto drop_files = [&](const std::string& id) {
+    if (!cfg_.cold_dir.empty() && file_exists(data_path(id, true))) {
+      ::unlink(data_path(id, true).c_str());
+      ::unlink(meta_path(id, true).c_str());
+      cold_touched = true;
+    }
+    if (file_exists(data_path(id, false)) || file_exists(meta_path(id, false))) {
+      ::unlink(data_path(id, false).c_str());
+      ::unlink(meta_path(id, false).c_str());
+      hot_touched = true;
+    }
+  };
+  if (store_mode_) {
+    // Store of record: per id, from its newest record back, the first tombstone, supersede
+    // marker or intact block record decides. A block record is indexed where it lies (the
+    // journal stays its home; the exporter may write its files later). Records of segments
+    // sealed durable are trusted; the others' data is re-checked (a torn record was never
+    // acknowledged: the id falls back to its previous version).
+    std::unordered_map<std::string, std::vector<size_t>> by_id;
+    for (size_t i = 0; i < recs.size(); ++i) by_id[recs[i].id].push_back(i);
+    std::vector<char> keep(recs.size(), 0);
+    std::vector<size_t> chosen_recs;  // indexed below, under the lock (verification takes it)
+    for (auto& kv : by_id) {
+      const std::string& id = kv.first;
+      if (!valid_block_id(id)) {
+        ++skipped;
+        continue;
+      }
+      long chosen = -1;
+      uint32_t decided = 0;
+      for (auto it = kv.second.rbegin(); it != kv.second.rend(); ++it) {
+        const ReplayRecord& r = recs[*it];
+        if (r.type != kJrBlock) {
+          decided = r.type;
+          break;
+        }
+        if (!r.trusted) {
+          ++verified;
+          if (!verify(r, buf)) {
+            ++skipped;
+            continue;
+          }
+        }
+        chosen = static_cast<long>(*it);
+        decided = kJrBlock;
+        break;
+      }
+      if (decided == kJrTomb) drop_files(id);
+      if (decided != kJrBlock) continue;  // kJrFile: its files are the home (scan_dirs indexes them)
+      const ReplayRecord& r = recs[static_cast<size_t>(chosen)];
+      if (file_size(data_path(id, false)) == static_cast<int64_t>(r.n) &&
+          file_size(meta_path(id, false)) == static_cast<int64_t>(r.meta_be.size())) {
+        // an export of this very record that was durable before the crash (same size, same
+        // .meta image): the files are the home, the record is released (scan_dirs indexes them)
+        std::vector<uint8_t> m(r.meta_be.size());
+        int fd = ::open(meta_path(id, false).c_str(), O_RDONLY | O_CLOEXEC);
+        const bool same = fd >= 0 && (m.empty() || read_all(fd, m.data(), m.size(), 0)) && m == r.meta_be;
+        if (fd >= 0) ::close(fd);
+        if (same) continue;
+      }
+      keep[static_cast<size_t>(chosen)] = 1;
+      drop_files(id);  // an older per-file version: the record is the latest, and the home
+      chosen_recs.push_back(static_cast<size_t>(chosen));
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t i : chosen_recs) {
+        const ReplayRecord& r = recs[i];
+        Block& b = index_[r.id];
+        b = Block{};
+        b.size = r.n;
+        b.crc = r.crc;
+        b.crc_known = true;
+        b.jrec = r.rec;
+        b.jmeta = std::make_shared<std::vector<uint8_t>>(r.meta_be);
+        enqueue_materialize_locked(r.id, b);
+        ++replayed;
+      }
+    }
+    if ((hot_touched && !sync_dir(false)) || (cold_touched && !sync_dir(true)))
+      throw std::runtime_error("journal replay: directory sync");
+    std::vector<JournalRec> dead;
+    for (size_t i = 0; i < recs.size(); ++i)
+      if (recs[i].type == kJrBlock && !keep[i]) dead.push_back(recs[i].rec);
+    recs.clear();
+    journal_->note_replay(replayed, skipped, verified);
+    // (release() takes only the journal's lock)
+    for (auto& r : dead) journal_->release(r);
+    return;
+  }
+  // Round-4 mode: the latest state per block id is verified and written out as `<id>` +
+  // `<id>.meta`; tombstoned ids lose their files. Then every segment is retired and
+  // scan_dirs() indexes the result.
+  std::unordered_map<std::string, long> last;  // id -> index of its final record (-1: deleted, -2: own files)
+  for (size_t i = 0; i < recs.size(); ++i)
+    last[recs[i].id] = recs[i].type == kJrBlock ? static_cast<long>(i) : recs[i].type == kJrTomb ? -1 : -2;
+  std::string err;
+  for (auto& kv : last) {
+    const std::string& id = kv.first;
+    if (!valid_block_id(id)) {
       ++skipped;
       continue;
+    }
+    if (kv.second == -2) continue;
+    if (kv.second < 0) {
+      drop_files(id);
+      continue;
+    }
+    const ReplayRecord& r = recs[static_cast<size_t>(kv.second)];
+    ++verified;
+    if (!verify(r, buf)) {  // torn: never acknowledged (prefix order), so dropping it loses nothing
+      ++skipped;
+      continue;
+    }
+    if (!cfg_.cold_dir.empty() && file_exists(data_path(id, true))) {
+      // the journal holds the latest write of the id: it replaces a cold copy
+      ::unlink(data_path(id, true).c_str());
+      ::unlink(meta_path(id, true).c_str());
+      cold_touched = true;
     }
     if (!write_file_durable(data_path(id, false), buf.data(), r.n, &err) ||
         !write_file_durable(meta_path(id, false), r.meta_be.data(), r.meta_be.size(), &err)) {
@@ -2831,9 +3230,129 @@ void ChunkStore::replay_journal() {
     ++replayed;
   }
   if (!sync_dir(false) || (cold_touched && !sync_dir(true))) throw std::runtime_error("journal replay: directory sync");
-  journal_->note_replay(replayed, skipped);
+  journal_->note_replay(replayed, skipped, verified);
   recs.clear();
   journal_->retire_all();
+}
+
+// K1b over durable copies: blocks that are not resident (or resident blocks' journal / file
+// copies) are read into a staging extent, batch by batch, laid out as in the arena (data,
+// then the BE .meta image), and one launch of the scrub kernel verifies the batch. Blocks
+// larger than a batch go to `rest` (CPU verify).
+std::vector<std::string> ChunkStore::scrub_durable_gpu(const std::vector<std::string>& ids,
+                                                       std::vector<std::string>* rest) {
+  std::vector<std::string> bad;
+  if (!gpu() || ids.empty()) {
+    rest->insert(rest->end(), ids.begin(), ids.end());
+    return bad;
+  }
+  HIP_OK(hipSetDevice(cfg_.device));
+  constexpr uint64_t kBatchBytes = 64ull << 20;
+  size_t i = 0;
+  std::vector<uint8_t> data;
+  while (i < ids.size()) {
+    struct Item {
+      std::string id;
+      uint64_t n = 0, off = 0;
+      std::vector<uint8_t> bytes, meta_be;
+    };
+    std::vector<Item> items;
+    uint64_t total = 0;
+    for (; i < ids.size() && total < kBatchBytes; ++i) {
+      const std::string& id = ids[i];
+      bool cold = false;
+      JournalRec jrec;
+      std::shared_ptr<std::vector<uint8_t>> jmeta;
+      uint64_t size = 0;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = index_.find(id);
+        if (it == index_.end()) continue;
+        cold = it->second.cold;
+        jrec = it->second.jrec;
+        jmeta = it->second.jmeta;
+        size = it->second.size;
+        if (jrec.seg) jrec.seg->readers++;  // released by DurableSrc
+      }
+      const uint64_t need = align_up(std::max<uint64_t>(size, 1), 256) + align_up(num_slices(size) * 4 + 4, 256);
+      if (size == 0 || need > kBatchBytes) {
+        if (jrec.seg) jrec.seg->readers--;
+        rest->push_back(id);
+        continue;
+      }
+      DurableSrc src;
+      if (!open_durable(id, cold, jrec, jmeta, &src) || src.meta.size() != num_slices(size)) {
+        bad.push_back(id);  // missing, or its checksums are
+        continue;
+      }
+      Item it;
+      it.id = id;
+      it.n = size;
+      it.bytes.resize(size);
+      if (!read_all(src.fd, it.bytes.data(), size, src.base)) {
+        bad.push_back(id);
+        continue;
+      }
+      it.meta_be.resize(src.meta.size() * 4);
+      for (size_t s = 0; s < src.meta.size(); ++s) {
+        const uint32_t be = __builtin_bswap32(src.meta[s]);
+        std::memcpy(it.meta_be.data() + 4 * s, &be, 4);
+      }
+      it.off = total;
+      total += need;
+      items.push_back(std::move(it));
+    }
+    if (items.empty()) continue;
+    DevExtent ext = reserve(total);
+    if (ext.off < 0) {  // no room in the arena: CPU
+      for (auto& it : items) rest->push_back(it.id);
+      continue;
+    }
+    Lane* l = acquire_lane();
+    std::vector<ScrubBlock> hb;
+    uint64_t tiles = 0;
+    for (auto& it : items) {
+      uint8_t* d = ext.ptr + it.off;
+      h2d_chunked(l, d, it.bytes.data(), it.n);
+      uint8_t* dm = d + align_up(it.n, 256);
+      HIP_OK(hipMemcpyAsync(dm, it.meta_be.data(), it.meta_be.size(), hipMemcpyHostToDevice, l->stream));
+      HIP_OK(hipStreamSynchronize(l->stream));  // the pageable sources must outlive the copies
+      ScrubBlock b{};
+      b.data = d;
+      b.meta = reinterpret_cast<const uint32_t*>(dm);
+      b.s_full = it.n / kSliceBytes;
+      b.tile_start = tiles;
+      b.tail_len = static_cast<uint32_t>(it.n % kSliceBytes);
+      b.tail_init = b.tail_len ? crc_init_term(b.tail_len) : 0;
+      tiles += (b.s_full + kSlicesPerTile - 1) / kSlicesPerTile;
+      hb.push_back(b);
+    }
+    ScrubBlock* dblocks = nullptr;
+    uint32_t* dbad = nullptr;
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&dblocks), hb.size() * sizeof(ScrubBlock)));
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&dbad), hb.size() * sizeof(uint32_t)));
+    HIP_OK(hipMemcpyAsync(dblocks, hb.data(), hb.size() * sizeof(ScrubBlock), hipMemcpyHostToDevice, l->stream));
+    HIP_OK(hipMemsetAsync(dbad, 0xFF, hb.size() * sizeof(uint32_t), l->stream));
+    ScrubLaunch a{};
+    a.blocks = dblocks;
+    a.nblocks = static_cast<uint32_t>(hb.size());
+    a.ntiles = tiles;
+    a.full_init = crc_init_term(kSliceBytes);
+    a.bad = dbad;
+    HIP_OK(launch_scrub(a, dtables_, l->stream));
+    launches_++;
+    std::vector<uint32_t> hbad(hb.size());
+    HIP_OK(hipMemcpyAsync(hbad.data(), dbad, hb.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+    release_lane(l);
+    (void)hipFree(dblocks);
+    (void)hipFree(dbad);
+    release(ext);
+    for (size_t j = 0; j < items.size(); ++j)
+      if (hbad[j] != 0xFFFFFFFFu) bad.push_back(items[j].id);
+    scrub_dev_blocks_ += items.size();
+  }
+  return bad;
 }
 
 

@@ -97,16 +97,22 @@ struct StoreStats {
   uint64_t io_threads_spawned = 0;  // helper threads ever started (steady state: none per write)
   uint64_t final_name_writes = 0;   // durable writes of fresh ids straight to their final names
   uint64_t direct_writes = 0;       // of those, data files written with O_DIRECT (DFS_ODIRECT=1)
-  // block journal (journal.h): group-committed durable writes + background materializer
+  // block journal (journal.h): group-committed durable writes; the store of record, with a
+  // rate-limited exporter of reference-format files and compaction (or the round-4 mode)
   bool journal = false;
+  std::string journal_mode;  // "store" (export with headroom), "store-noexport", "idle" (round 4)
   uint64_t journal_records = 0, journal_bytes = 0, journal_commits = 0, journal_sync_rounds = 0;
-  uint64_t journal_tombstones = 0, journal_full_waits = 0, journal_segs = 0, journal_segs_free = 0;
-  uint64_t journal_segs_retired = 0, journal_replayed = 0, journal_replay_skipped = 0;
+  uint64_t journal_tombstones = 0, journal_supersedes = 0, journal_full_waits = 0, journal_segs = 0,
+           journal_segs_free = 0, journal_segs_in_use = 0, journal_segs_marked = 0;
+  uint64_t journal_segs_retired = 0, journal_replayed = 0, journal_replay_skipped = 0, journal_replay_verified = 0;
+  uint64_t journal_live_records = 0, journal_live_bytes = 0, journal_used_bytes = 0;
   uint64_t materialized_blocks = 0, materialized_bytes = 0, materialize_pending = 0, materialize_batches = 0;
   uint64_t materialize_errors = 0, journal_prepare_errors = 0, journal_segs_filled = 0, journal_fill_bytes = 0,
            journal_parts_unready = 0;
   uint64_t journal_sync_ns = 0, journal_commit_ns = 0, journal_bypassed = 0;
-  bool journal_failed = false;
+  uint64_t relocated_blocks = 0, relocated_bytes = 0, compactions = 0, export_deferred_headroom = 0;
+  uint64_t scrub_device_blocks = 0;  // durable (journal / file) copies verified by the K1b kernel
+  bool journal_failed = false, journal_grow_blocked = false;
   std::string journal_last_error, materialize_last_error;
 };
 
@@ -183,11 +189,14 @@ class ChunkStore {
   void drop_resident();  // evict every clean resident block (tests / memory pressure)
   bool debug_corrupt(const std::string& id, uint64_t offset);  // flip a byte everywhere
   void debug_pause_spill(bool on);  // hbm-ack crash tests: hold dirty blocks in HBM only
-  // Journal: write every queued record out as `<id>` + `<id>.meta` now and wait for it
-  // (tests, tiering, shutdown); pause holds the materializer (crash tests).
+  // Journal: export every journal-resident block as `<id>` + `<id>.meta` now and wait for it
+  // (tests, tiering, `/export`); pause holds the exporter (crash tests).
   void materialize_all();
   void debug_pause_materializer(bool on);
-  bool journaled(const std::string& id);  // durable in the journal, not yet in its own files
+  bool journaled(const std::string& id);  // durable in the journal, not in its own files
+  // Relocates the live records of the oldest journal segment when at most `max_live` of it is
+  // still live (or unconditionally with max_live >= 1); returns blocks moved (tests, /compact).
+  uint64_t compact(double max_live);
 
   // ---- replication engine hooks (RCCL receive / send) ----
   DevExtent reserve(uint64_t n);
@@ -343,9 +352,38 @@ class ChunkStore {
   std::atomic<uint64_t> bypassed_{0};  // durable writes sent past a journal at its materialize mark
   std::atomic<uint64_t> last_durable_write_ns_{0};  // any durable write, journaled or bypassed
   bool journal_bypass_ = true;
+  // store of record (round 5): no bypass, no drain at stop, replay indexes records in place;
+  // export_ = rate-limited export of reference-format files while the volume has headroom
+  bool store_mode_ = false;
+  bool export_ = true;
+  double export_bps_ = 256e6;        // exporter token bucket (bytes / s)
+  uint64_t export_headroom_ = 0;     // export only while the volume keeps this much free
+  double compact_live_ = 0.5;        // compaction: oldest segment at most this share live
   void materializer_loop();
   bool materialize_due();
+  bool export_headroom(uint64_t bytes);
+  struct MatItem;
+  // Exports the jobs (pins held) as `<id>` + `<id>.meta`: tmp names, per-file flush, rename
+  // only while the record is still current and no per-file writer owns the id, one
+  // directory flush. Returns the number exported; failures are requeued (retry = true).
+  uint64_t export_batch(std::vector<MatItem>& batch, bool retry);
+  uint64_t relocate_segment(const SegRef& seg, uint64_t budget_bytes);
+  bool relocate_one(const std::string& id, const JournalRec& old);
   void replay_journal();
+  void replay_store(std::vector<ReplayRecord>& recs);
+  // After a durable per-file write of `id`: a supersede marker, so replay keeps the file
+  // instead of an older journal version (no-op without a journal).
+  bool supersede_file(const std::string& id, std::string* err);
+  // Per-file writers of an id hold a claim while they write and index; the exporter never
+  // renames over a claimed id (mu_).
+  std::unordered_map<std::string, int> file_writers_;
+  struct FileClaim {
+    ChunkStore* s = nullptr;
+    std::string id;
+    FileClaim(ChunkStore* st, const std::string& i);
+    ~FileClaim();
+  };
+  std::vector<std::string> scrub_durable_gpu(const std::vector<std::string>& ids, std::vector<std::string>* rest);
   // Where a block's durable bytes are read from: its own file or its journal record.
   struct DurableSrc {
     int fd = -1;
@@ -435,6 +473,9 @@ class ChunkStore {
   uint64_t mat_idle_ns_ = 100000000;  // ... or after this long without an append
   std::thread materializer_;
   uint64_t materialized_blocks_ = 0, materialized_bytes_ = 0, mat_batches_ = 0, mat_errors_ = 0;  // mu_
+  uint64_t relocated_blocks_ = 0, relocated_bytes_ = 0, compactions_ = 0, export_deferred_ = 0;   // mu_
+  std::atomic<uint64_t> scrub_dev_blocks_{0};
+  std::mutex compact_mu_;       // one compaction at a time (exporter thread, compact())
   std::string mat_last_error_;  // mu_
 };
 

@@ -526,6 +526,7 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
       put_str(req, t_request_id);
       put<uint8_t>(req, heal ? 1 : 0);  // a heal copy: the receiver reports the new location
       put<uint8_t>(req, ephemeral ? 1 : 0);  // an EC gather copy: held in HBM only, never persisted
+      put<uint8_t>(req, static_cast<uint8_t>(tk.ch));  // the pair's channel the transfer is sequenced on
       finish_frame(req);
       return req;
     };
@@ -799,6 +800,7 @@ void FastPathServer::serve(int fd) {
       std::string rid = rd.p < rd.end ? rd.str() : std::string();
       const bool heal = rd.p < rd.end && rd.get<uint8_t>() == 1;
       const bool ephemeral = rd.p < rd.end && rd.get<uint8_t>() == 1;
+      const int ch = rd.p < rd.end ? rd.get<uint8_t>() : 0;
       RequestScope rs(rid);
       note_rid(rid);
       if (!rd.ok || id.empty() || repl_ == nullptr || size > kMaxTransfer) {
@@ -809,7 +811,7 @@ void FastPathServer::serve(int fd) {
         // sender's transfer unmatched and cost the pair a rebuild; the block is dropped after.
         bool last = next.empty();
         bool stale = fenced(term, &msg);
-        WriteResult wr = repl_->recv(src, gen, seq, id, size, slice, crc, last && !stale && !ephemeral);
+        WriteResult wr = repl_->recv(src, gen, ch, seq, id, size, slice, crc, last && !stale && !ephemeral);
         if (stale) {
           if (wr.ok) store_->remove(id);
           sent = send_response(fd, FpStatus::Fenced, term_.load(), 0, msg);

@@ -4,12 +4,14 @@
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/stat.h>
+#include <sys/statvfs.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cerrno>
-#include <cstdio>
 #include <chrono>
+#include <cstddef>
+#include <cstdio>
 #include <cstring>
 
 #include "crc32.h"
@@ -22,8 +24,23 @@ constexpr uint32_t kSegMagic = 0x324a5344u;  // "DSJ2" (striped segments)
 constexpr uint32_t kRecMagic = 0x524a5344u;  // "DSJR"
 constexpr uint64_t kPage = 4096;
 constexpr uint64_t kHdr = 512;
+constexpr uint32_t kFlagSealed = 1, kFlagRetired = 2;
 
+// version 3; version 2 (round 4: no flags, no LSN mark, retirement zeroed the page) still reads
 struct PartHdr {
+  uint32_t magic;
+  uint32_t version;
+  uint64_t seq;
+  uint64_t cap;
+  uint32_t part;
+  uint32_t nparts;
+  uint32_t flags;
+  uint32_t pad0;
+  uint64_t lsn_hw;  // every LSN in the journal is below this when the header is written
+  uint32_t hdr_crc;
+  uint32_t pad;
+};
+struct PartHdrV2 {
   uint32_t magic;
   uint32_t version;
   uint64_t seq;
@@ -105,6 +122,41 @@ std::string parent_of(const std::string& p) {
   return s == std::string::npos || s == 0 ? std::string("/") : p.substr(0, s);
 }
 
+// A part header as read back: valid, its segment sequence number, flags and LSN mark.
+struct HdrView {
+  bool ok = false;
+  uint64_t seq = 0, lsn_hw = 0;
+  uint32_t flags = 0;
+};
+
+HdrView read_part_header(int fd, size_t k, size_t nparts) {
+  HdrView v;
+  uint8_t raw[sizeof(PartHdr)];
+  if (!pread_all(fd, raw, sizeof(raw), 0)) return v;
+  uint32_t magic, version;
+  std::memcpy(&magic, raw, 4);
+  std::memcpy(&version, raw + 4, 4);
+  if (magic != kSegMagic) return v;
+  if (version == 3) {
+    PartHdr h;
+    std::memcpy(&h, raw, sizeof(h));
+    if (h.hdr_crc != crc32(raw, offsetof(PartHdr, hdr_crc)) || h.part != k || h.nparts != nparts || h.seq == 0)
+      return v;
+    v.ok = true;
+    v.seq = h.seq;
+    v.flags = h.flags;
+    v.lsn_hw = h.lsn_hw;
+  } else if (version == 2) {
+    PartHdrV2 h;
+    std::memcpy(&h, raw, sizeof(h));
+    if (h.hdr_crc != crc32(raw, offsetof(PartHdrV2, hdr_crc)) || h.part != k || h.nparts != nparts || h.seq == 0)
+      return v;
+    v.ok = true;
+    v.seq = h.seq;
+  }
+  return v;
+}
+
 }  // namespace
 
 JournalPart::~JournalPart() {
@@ -130,11 +182,22 @@ bool JournalSeg::filling() const {
   return false;
 }
 
+uint64_t JournalSeg::capacity() const {
+  uint64_t c = 0;
+  for (auto& p : parts) c += p->cap;
+  return c;
+}
+
 BlockJournal::BlockJournal(JournalConfig cfg) : cfg_(std::move(cfg)) {
   cfg_.parts = std::max(1, std::min(cfg_.parts, 64));
   cfg_.seg_bytes = std::max<uint64_t>(align_up(cfg_.seg_bytes, kPage), 4 << 20);
   part_bytes_ = std::max<uint64_t>(cfg_.seg_bytes / cfg_.parts / kPage * kPage, 1 << 20);
-  cfg_.max_segs = std::max(2, cfg_.max_segs);
+  if (cfg_.grow) {
+    if (cfg_.max_segs > 0) cfg_.max_segs = std::max(2, cfg_.max_segs);
+    cfg_.spares = std::max(1, cfg_.spares);
+  } else {
+    cfg_.max_segs = std::max(2, cfg_.max_segs);
+  }
   if (::mkdir(cfg_.dir.c_str(), 0755) == 0) fsync_dir(parent_of(cfg_.dir));
 }
 
@@ -147,15 +210,80 @@ BlockJournal::~BlockJournal() {
   if (preparer_.joinable()) preparer_.join();
 }
 
-// Creates every segment up to the cap (fallocate: metadata only), then, with zero_fill,
-// writes the parts of the free ones out while the writers are idle (8 MiB at a time,
-// re-checking between chunks), so first-cycle appends are overwrites of written extents.
+bool BlockJournal::room_for_segment() {
+  struct statvfs sv;
+  if (::statvfs(cfg_.dir.c_str(), &sv) != 0) return true;  // unknown: let the create itself fail
+  const uint64_t avail = static_cast<uint64_t>(sv.f_bavail) * sv.f_frsize;
+  return avail >= capacity_bytes() + cfg_.reserve_bytes;
+}
+
+// Marks the oldest sealed, complete, unmarked segment: its part headers get the `sealed` flag
+// and each part is flushed (which also flushes any record bytes a writer has not committed,
+// e.g. padding). Called with the lock held; drops it around the I/O.
+bool BlockJournal::mark_one(std::unique_lock<std::mutex>& lk) {
+  SegRef s;
+  for (auto& f : order_)
+    if (f->sealed && !f->marked && !f->marking && f->complete()) {
+      s = f;
+      break;
+    }
+  if (!s) return false;
+  s->marking = true;
+  const uint64_t seq = s->seq, lsn = next_lsn_;
+  lk.unlock();
+  bool ok = true;
+  for (size_t k = 0; k < s->parts.size(); ++k) {
+    JournalPart* p = s->parts[k].get();
+    ok = ok && write_part_header(p, seq, static_cast<int>(k), static_cast<int>(s->parts.size()), kFlagSealed, lsn);
+    ok = ok && (!cfg_.sync || ::fdatasync(p->fd) == 0);
+  }
+  lk.lock();
+  s->marking = false;
+  if (ok) {
+    s->marked = true;
+    st_.segs_marked++;
+  }
+  cv_.notify_all();
+  return ok;
+}
+
+void BlockJournal::mark_sealed_now() {
+  std::unique_lock<std::mutex> lk(mu_);
+  if (!order_.empty() && !order_.back()->sealed && order_.back()->complete()) order_.back()->sealed = true;
+  while (mark_one(lk)) {
+  }
+}
+
+// Creates segments (fallocate: metadata only) — all up to max_segs, or in grow mode enough
+// to keep `spares` free ones ready while the volume has room — and, in the writers' idle
+// windows, flushes the `sealed` headers of finished segments and (zero_fill) writes the free
+// parts out once (8 MiB at a time, re-checking between chunks), so first-cycle appends are
+// overwrites of written extents.
 void BlockJournal::prepare_loop() {
   static const std::vector<uint8_t> zeros(8 << 20, 0);
   std::unique_lock<std::mutex> lk(mu_);
+  auto grow_check_ns = 0ull;
   for (;;) {
     if (prep_stop_) return;
-    if (static_cast<int>(segs_.size()) + preparing_ < cfg_.max_segs) {
+    const int have = static_cast<int>(segs_.size()) + preparing_;
+    bool want = cfg_.grow ? static_cast<int>(free_.size()) + preparing_ < cfg_.spares &&
+                                (cfg_.max_segs <= 0 || have < cfg_.max_segs)
+                          : have < cfg_.max_segs;
+    if (want && cfg_.grow) {
+      const uint64_t t = now_ns();
+      if (grow_blocked_ && t < grow_check_ns) {
+        want = false;
+      } else {
+        lk.unlock();
+        const bool room = room_for_segment();
+        lk.lock();
+        grow_blocked_ = !room;
+        grow_check_ns = t + 1000000000ull;
+        want = room;
+        if (!room) cv_.notify_all();  // writers waiting for a segment learn the journal is full
+      }
+    }
+    if (want) {
       ++preparing_;
       const int index = next_file_++;
       lk.unlock();
@@ -184,8 +312,13 @@ void BlockJournal::prepare_loop() {
                      describe_locked().c_str());
         if ((e == ENOSPC || e == EDQUOT) && !segs_.empty()) {
           // no room for another segment: run with the ones there are (a writer waits for the
-          // materializer to recycle one instead of failing)
-          cfg_.max_segs = std::max<int>(2, static_cast<int>(segs_.size()));
+          // exporter / compaction to free one instead of failing)
+          if (cfg_.grow) {
+            grow_blocked_ = true;
+            grow_check_ns = now_ns() + 1000000000ull;
+          } else {
+            cfg_.max_segs = std::max<int>(2, static_cast<int>(segs_.size()));
+          }
         } else {
           // transient (or nothing to fall back on): try again shortly
           cv_.wait_for(lk, std::chrono::milliseconds(500), [&] { return prep_stop_; });
@@ -194,6 +327,10 @@ void BlockJournal::prepare_loop() {
       cv_.notify_all();
       continue;
     }
+    const uint64_t idle_ns = static_cast<uint64_t>(std::max(1, cfg_.idle_fill_ms)) * 1000000ull;
+    const uint64_t since = now_ns() - last_append_ns_;
+    const bool idle = !last_append_ns_ || since >= idle_ns;
+    if (idle && mark_one(lk)) continue;
     JournalPart* t = nullptr;
     if (cfg_.zero_fill)
       for (auto& f : free_) {
@@ -204,14 +341,19 @@ void BlockJournal::prepare_loop() {
           }
         if (t) break;
       }
-    if (!t) {
+    const bool sealed_pending = std::any_of(order_.begin(), order_.end(), [](const SegRef& f) {
+      return f->sealed && !f->marked && !f->marking && f->complete();
+    });
+    if (!t && !sealed_pending) {
       cv_.wait_for(lk, std::chrono::milliseconds(200));
       continue;
     }
-    const uint64_t idle_ns = static_cast<uint64_t>(std::max(1, cfg_.idle_fill_ms)) * 1000000ull;
-    const uint64_t since = now_ns() - last_append_ns_;
-    if (last_append_ns_ && since < idle_ns) {  // writers active: wait until they pause
+    if (!idle) {  // writers active: wait until they pause
       cv_.wait_for(lk, std::chrono::nanoseconds(idle_ns - since + 1000000));
+      continue;
+    }
+    if (!t) {
+      cv_.wait_for(lk, std::chrono::milliseconds(50));
       continue;
     }
     t->filling = true;
@@ -241,8 +383,10 @@ void BlockJournal::prepare_loop() {
 
 std::string BlockJournal::describe_locked() const {
   char buf[512];
-  int n = std::snprintf(buf, sizeof(buf), "segments %zu of max %d (%d parts), in use %zu, free %zu, preparing %d",
-                        segs_.size(), cfg_.max_segs, cfg_.parts, order_.size(), free_.size(), preparing_);
+  int n = std::snprintf(buf, sizeof(buf), "segments %zu of max %d%s (%d parts), in use %zu, free %zu, preparing %d",
+                        segs_.size(), cfg_.max_segs, cfg_.grow ? (grow_blocked_ ? " grow, volume at reserve" : " grow")
+                                                                : "",
+                        cfg_.parts, order_.size(), free_.size(), preparing_);
   if (!order_.empty() && n > 0 && n < static_cast<int>(sizeof(buf))) {
     const JournalSeg* f = order_.front().get();
     std::snprintf(buf + n, sizeof(buf) - n, "; oldest seq %llu: live %llu, sealed %d, complete %d, readers %d",
@@ -285,20 +429,21 @@ SegRef BlockJournal::open_seg(int index, bool create) {
   return s;
 }
 
-bool BlockJournal::write_part_header(JournalPart* p, uint64_t seq, int part, int nparts) {
+bool BlockJournal::write_part_header(JournalPart* p, uint64_t seq, int part, int nparts, uint32_t flags,
+                                     uint64_t lsn_hw) {
   alignas(4096) static thread_local uint8_t page[kPage];
   std::memset(page, 0, kPage);
-  if (seq) {
-    PartHdr h{};
-    h.magic = kSegMagic;
-    h.version = 2;
-    h.seq = seq;
-    h.cap = p->cap;
-    h.part = static_cast<uint32_t>(part);
-    h.nparts = static_cast<uint32_t>(nparts);
-    h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(PartHdr, hdr_crc));
-    std::memcpy(page, &h, sizeof(h));
-  }
+  PartHdr h{};
+  h.magic = kSegMagic;
+  h.version = 3;
+  h.seq = seq;
+  h.cap = p->cap;
+  h.part = static_cast<uint32_t>(part);
+  h.nparts = static_cast<uint32_t>(nparts);
+  h.flags = flags;
+  h.lsn_hw = lsn_hw;
+  h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(PartHdr, hdr_crc));
+  std::memcpy(page, &h, sizeof(h));
   return pwrite_all(p->fd, page, kPage, 0);
 }
 
@@ -318,28 +463,38 @@ std::vector<ReplayRecord> BlockJournal::recover() {
     SegRef s = open_seg(kv.first, false);  // (a segment short of parts gets them created)
     if (!s) continue;
     segs_.push_back(s);
-    // the segment is live if any part holds a valid header; parts whose header does not match
-    // it (never flushed before a crash) hold no acknowledged record
+    // the segment's sequence number is the largest valid header's; parts whose header does
+    // not carry it (never flushed before a crash) hold no acknowledged record. Every header,
+    // retired ones included, raises the sequence / LSN floors of this run.
     uint64_t seq = 0;
+    bool retired = false, sealed = true, any_hdr = false;
     std::vector<bool> valid(s->parts.size(), false);
+    std::vector<HdrView> hv(s->parts.size());
     for (size_t k = 0; k < s->parts.size(); ++k) {
-      PartHdr h{};
-      if (pread_all(s->parts[k]->fd, reinterpret_cast<uint8_t*>(&h), sizeof(h), 0) && h.magic == kSegMagic &&
-          h.seq > 0 && h.part == k && h.nparts == s->parts.size() &&
-          h.hdr_crc == crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(PartHdr, hdr_crc))) {
-        if (seq == 0 || h.seq > seq) {
-          seq = h.seq;
-          std::fill(valid.begin(), valid.end(), false);
-        }
-        if (h.seq == seq) valid[k] = true;
+      hv[k] = read_part_header(s->parts[k]->fd, k, s->parts.size());
+      if (!hv[k].ok) continue;
+      any_hdr = true;
+      next_seq_ = std::max(next_seq_, hv[k].seq + 1);
+      next_lsn_ = std::max(next_lsn_, hv[k].lsn_hw);
+      seq = std::max(seq, hv[k].seq);
+    }
+    for (size_t k = 0; k < s->parts.size(); ++k) {
+      if (hv[k].ok && hv[k].seq == seq) {
+        valid[k] = true;
+        retired = retired || (hv[k].flags & kFlagRetired);
+        sealed = sealed && (hv[k].flags & kFlagSealed);
+      } else {
+        sealed = false;
       }
     }
-    if (seq == 0) {
+    if (seq == 0 || retired) {
+      // free (a retirement that reached any part decided that every record is dead)
+      if (any_hdr)
+        for (auto& p : s->parts) p->filled = true;  // used before: written extents
       free_.push_back(s);
       continue;
     }
     s->seq = seq;
-    next_seq_ = std::max(next_seq_, seq + 1);
     for (size_t k = 0; k < s->parts.size(); ++k) {
       JournalPart* p = s->parts[k].get();
       uint64_t off = kPage;
@@ -351,13 +506,17 @@ std::vector<ReplayRecord> BlockJournal::recover() {
         if (h.seq != seq || h.part != k || h.off != off || h.rec_len < kPage || h.rec_len % kPage ||
             off + h.rec_len > p->cap)
           break;
-        if (h.type == kJrBlock || h.type == kJrTomb) {
+        if (h.type == kJrBlock || h.type == kJrTomb || h.type == kJrFile) {
           ReplayRecord r;
           r.type = h.type;
           r.id.assign(h.id, std::min<uint32_t>(h.id_len, sizeof(h.id)));
           r.lsn = h.lsn;
-          r.seg = s;
-          r.part = static_cast<int>(k);
+          r.trusted = sealed;
+          r.rec.seg = s;
+          r.rec.part = static_cast<int>(k);
+          r.rec.off = off;
+          r.rec.end = off + h.rec_len;
+          r.rec.lsn = h.lsn;
           if (h.type == kJrBlock) {
             if (h.hdr_bytes != hdr_bytes_for(h.nslices) || h.nslices != num_slices(h.n) ||
                 h.hdr_bytes + align_up(h.n, kPage) != h.rec_len)
@@ -367,7 +526,9 @@ std::vector<ReplayRecord> BlockJournal::recover() {
             if (crc32(r.meta_be.data(), r.meta_be.size()) != h.meta_crc) break;
             r.n = h.n;
             r.crc = h.crc;
-            r.data_off = off + h.hdr_bytes;
+            r.rec.hdr_bytes = h.hdr_bytes;
+            s->live++;
+            s->live_bytes += h.rec_len;
           }
           next_lsn_ = std::max(next_lsn_, h.lsn + 1);
           out.push_back(std::move(r));
@@ -375,8 +536,10 @@ std::vector<ReplayRecord> BlockJournal::recover() {
         off += h.rec_len;
       }
       p->tail = p->done_upto = p->durable_upto = p->syncing_upto = off;
+      p->filled = true;  // written once at least up to the tail; recycled later as written extents
     }
     s->sealed = true;
+    s->marked = sealed;
     live.push_back(s);
   }
   std::sort(live.begin(), live.end(), [](const SegRef& a, const SegRef& b) { return a->seq < b->seq; });
@@ -387,16 +550,19 @@ std::vector<ReplayRecord> BlockJournal::recover() {
   return out;
 }
 
-void BlockJournal::note_replay(uint64_t replayed, uint64_t skipped) {
+void BlockJournal::note_replay(uint64_t replayed, uint64_t skipped, uint64_t verified) {
   std::lock_guard<std::mutex> g(mu_);
   st_.replayed += replayed;
   st_.replay_skipped += skipped;
+  st_.replay_verified += verified;
 }
 
 void BlockJournal::reset_seg_locked(JournalSeg* s) {
   s->seq = 0;
   s->live = 0;
+  s->live_bytes = 0;
   s->sealed = false;
+  s->marked = false;
   for (auto& p : s->parts) {
     p->tail = p->done_upto = p->durable_upto = p->syncing_upto = 0;
     p->done_out.clear();
@@ -405,14 +571,16 @@ void BlockJournal::reset_seg_locked(JournalSeg* s) {
 
 void BlockJournal::retire_all() {
   std::vector<SegRef> segs;
+  uint64_t lsn;
   {
     std::lock_guard<std::mutex> g(mu_);
     segs.swap(order_);
+    lsn = next_lsn_;
   }
   for (auto& s : segs)
     for (size_t k = 0; k < s->parts.size(); ++k) {
       JournalPart* p = s->parts[k].get();
-      (void)write_part_header(p, 0, static_cast<int>(k), static_cast<int>(s->parts.size()));
+      (void)write_part_header(p, s->seq, static_cast<int>(k), static_cast<int>(s->parts.size()), kFlagRetired, lsn);
       if (cfg_.sync) (void)::fdatasync(p->fd);
       (void)::posix_fadvise(p->fd, 0, 0, POSIX_FADV_DONTNEED);
     }
@@ -426,7 +594,7 @@ void BlockJournal::retire_all() {
 }
 
 // Caller holds the lock. Seals nothing; takes a free segment (or waits for the preparer /
-// the materializer) and makes it the active one.
+// the exporter) and makes it the active one.
 SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::string* err) {
   auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(cfg_.full_timeout_s);
   auto next_report = std::chrono::steady_clock::now() + std::chrono::seconds(5);
@@ -458,7 +626,8 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
       const uint64_t seq = next_seq_++;
       // no flush of their own: the first commit's fdatasync of each part covers its header
       for (size_t k = 0; k < s->parts.size(); ++k)
-        if (!write_part_header(s->parts[k].get(), seq, static_cast<int>(k), static_cast<int>(s->parts.size()))) {
+        if (!write_part_header(s->parts[k].get(), seq, static_cast<int>(k), static_cast<int>(s->parts.size()), 0,
+                               next_lsn_)) {
           *err = std::string("journal header: ") + std::strerror(errno);
           free_.push_back(s);
           return nullptr;
@@ -469,12 +638,16 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
         p->done_out.clear();
       }
       s->live = 0;
+      s->live_bytes = 0;
       s->sealed = false;
+      s->marked = false;
       order_.push_back(s);
       return s;
     }
-    const bool full = static_cast<int>(segs_.size()) + preparing_ >= cfg_.max_segs &&
-                      std::none_of(free_.begin(), free_.end(), [](const SegRef& f) { return f->filling(); });
+    const int have = static_cast<int>(segs_.size()) + preparing_;
+    const bool capped = cfg_.grow ? grow_blocked_ || (cfg_.max_segs > 0 && have >= cfg_.max_segs)
+                                  : have >= cfg_.max_segs;
+    const bool full = capped && std::none_of(free_.begin(), free_.end(), [](const SegRef& f) { return f->filling(); });
     if (full) ++st_.full_waits;  // not just waiting for the preparer
     if (std::chrono::steady_clock::now() >= next_report) {
       std::fprintf(stderr, "[journal] writer waiting for a free segment (%s)\n", describe_locked().c_str());
@@ -482,7 +655,8 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
     }
     if (cv_.wait_until(lk, std::min(deadline, next_report)) == std::cv_status::timeout &&
         std::chrono::steady_clock::now() >= deadline) {
-      *err = std::string(full ? "journal full (materializer behind): " : "no journal segment ready: ") +
+      *err = std::string(full ? "journal full (no free segment and no room for another): "
+                              : "no journal segment ready: ") +
              describe_locked() + (st_.last_error.empty() ? "" : "; last error: " + st_.last_error);
       return nullptr;
     }
@@ -529,6 +703,7 @@ bool BlockJournal::reserve(uint64_t n, uint64_t nslices, JournalRec* r, std::str
   if (!place_locked(lk, len, r, err)) return false;
   r->hdr_bytes = hdr_bytes_for(nslices);
   r->seg->live++;
+  r->seg->live_bytes += len;
   last_append_ns_ = now_ns();
   return true;
 }
@@ -544,36 +719,39 @@ bool BlockJournal::write(const JournalRec& r, uint64_t at, const uint8_t* p, uin
   return pwrite_all(part->fd, p, len, off);
 }
 
-bool BlockJournal::finish(const JournalRec& r, const std::string& id, uint64_t n, uint32_t crc,
-                          const uint8_t* meta_be, uint64_t nslices) {
+bool BlockJournal::finish(JournalRec* r, const std::string& id, uint64_t n, uint32_t crc, const uint8_t* meta_be,
+                          uint64_t nslices, uint64_t keep_lsn) {
   std::vector<uint8_t> area(kHdr + 4 * nslices);
   RecHdr h{};
   h.magic = kRecMagic;
   h.type = kJrBlock;
-  h.seq = r.seg->seq;
-  h.off = r.off;
-  h.rec_len = r.end - r.off;
-  h.hdr_bytes = r.hdr_bytes;
+  h.seq = r->seg->seq;
+  h.off = r->off;
+  h.rec_len = r->end - r->off;
+  h.hdr_bytes = r->hdr_bytes;
   h.n = n;
   h.crc = crc;
   h.nslices = static_cast<uint32_t>(nslices);
   h.meta_crc = crc32(meta_be, 4 * nslices);
   h.id_len = static_cast<uint32_t>(std::min<size_t>(id.size(), sizeof(h.id)));
   std::memcpy(h.id, id.data(), h.id_len);
-  h.part = static_cast<uint32_t>(r.part);
-  {
+  h.part = static_cast<uint32_t>(r->part);
+  if (keep_lsn) {
+    h.lsn = keep_lsn;
+  } else {
     // the LSN is taken when the record is finished, after its bytes are written: a later
     // write of the same id (which can only start after this one returned) gets a larger one
     std::lock_guard<std::mutex> g(mu_);
     h.lsn = next_lsn_++;
   }
+  r->lsn = h.lsn;
   h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc));
   std::memcpy(area.data(), &h, kHdr);
   if (nslices) std::memcpy(area.data() + kHdr, meta_be, 4 * nslices);
-  bool ok = pwrite_all(r.fd(), area.data(), area.size(), r.off);
+  bool ok = pwrite_all(r->fd(), area.data(), area.size(), r->off);
   std::lock_guard<std::mutex> g(mu_);
   if (!ok) failed_ = true;  // the prefix cannot advance past a record that is not on disk
-  complete_locked(r.seg->parts[r.part].get(), r.off, r.end);
+  complete_locked(r->seg->parts[r->part].get(), r->off, r->end);
   st_.records++;
   st_.bytes += n;
   cv_.notify_all();
@@ -596,7 +774,23 @@ void BlockJournal::abandon(const JournalRec& r) {
     complete_locked(r.seg->parts[r.part].get(), r.off, r.end);
     st_.pads++;
   }
-  materialized(r.seg, 1);
+  release(r);
+}
+
+void BlockJournal::pad_durable(const JournalRec& r) {
+  RecHdr h{};
+  h.magic = kRecMagic;
+  h.type = kJrPad;
+  h.seq = r.seg->seq;
+  h.off = r.off;
+  h.rec_len = r.end - r.off;
+  h.part = static_cast<uint32_t>(r.part);
+  h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc));
+  bool ok = pwrite_all(r.fd(), reinterpret_cast<const uint8_t*>(&h), kHdr, r.off) &&
+            (!cfg_.sync || ::fdatasync(r.fd()) == 0);
+  std::lock_guard<std::mutex> g(mu_);
+  if (!ok) failed_ = true;
+  st_.pads++;
 }
 
 void BlockJournal::complete_locked(JournalPart* p, uint64_t off, uint64_t end) {
@@ -655,17 +849,20 @@ bool BlockJournal::commit(const JournalRec& r) {
   }
 }
 
-void BlockJournal::tombstone(const std::string& id) {
+bool BlockJournal::marker(uint32_t type, const std::string& id, std::string* err) {
   JournalRec r;
-  std::string err;
   {
     std::unique_lock<std::mutex> lk(mu_);
-    if (failed_) return;
-    if (!place_locked(lk, kPage, &r, &err)) return;
+    if (failed_) {
+      *err = "journal failed";
+      return false;
+    }
+    if (!place_locked(lk, kPage, &r, err)) return false;
+    last_append_ns_ = now_ns();
   }
   RecHdr h{};
   h.magic = kRecMagic;
-  h.type = kJrTomb;
+  h.type = type;
   h.seq = r.seg->seq;
   h.off = r.off;
   h.rec_len = kPage;
@@ -678,43 +875,55 @@ void BlockJournal::tombstone(const std::string& id) {
   }
   h.hdr_crc = crc32(reinterpret_cast<const uint8_t*>(&h), offsetof(RecHdr, hdr_crc));
   bool ok = pwrite_all(r.fd(), reinterpret_cast<const uint8_t*>(&h), kHdr, r.off);
-  std::lock_guard<std::mutex> g(mu_);
-  if (!ok) failed_ = true;
-  complete_locked(r.seg->parts[r.part].get(), r.off, r.end);
-  st_.tombstones++;
-  cv_.notify_all();
-}
-
-void BlockJournal::materialized(const SegRef& s, uint64_t count) {
   {
     std::lock_guard<std::mutex> g(mu_);
-    s->live -= std::min(s->live, count);
+    if (!ok) failed_ = true;
+    complete_locked(r.seg->parts[r.part].get(), r.off, r.end);
+    if (type == kJrTomb) st_.tombstones++;
+    else st_.supersedes++;
+    cv_.notify_all();
+  }
+  if (!ok || !commit(r)) {
+    *err = "journal marker append failed";
+    return false;
+  }
+  return true;
+}
+
+void BlockJournal::release(const JournalRec& r) {
+  if (!r.seg) return;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    r.seg->live -= std::min<uint64_t>(r.seg->live, 1);
+    r.seg->live_bytes -= std::min(r.seg->live_bytes, r.bytes());
   }
   retire_ready();
 }
 
 void BlockJournal::retire_ready() {
   std::vector<SegRef> retire;
+  uint64_t lsn;
   {
     std::lock_guard<std::mutex> g(mu_);
-    // oldest first: a segment retires only after every older one did, so a tombstone is
-    // never dropped while a record it cancels could still be replayed; a segment somebody
-    // is still reading from waits for the next call
+    // oldest first: a segment retires only after every older one did, so a tombstone or a
+    // newer version is never dropped while a record it cancels could still be replayed; a
+    // segment somebody is still reading from (or marking) waits for the next call
     while (!order_.empty()) {
       SegRef f = order_.front();
       if (!f->sealed && f != order_.back()) f->sealed = true;  // only the newest segment takes appends
-      if (!f->sealed || f->live || !f->complete() || f->readers.load() > 0) break;
+      if (!f->sealed || f->live || !f->complete() || f->readers.load() > 0 || f->marking) break;
       retire.push_back(f);
       order_.erase(order_.begin());
     }
+    lsn = next_lsn_;
   }
   if (retire.empty()) return;
-  // the invalidated headers must be durable before the segment is reused: otherwise a crash
-  // could replay its old records over newer materialized versions
+  // the retired headers must be durable before the segment is reused: otherwise a crash
+  // could replay its old records over newer versions
   for (auto& f : retire)
     for (size_t k = 0; k < f->parts.size(); ++k) {
       JournalPart* p = f->parts[k].get();
-      (void)write_part_header(p, 0, static_cast<int>(k), static_cast<int>(f->parts.size()));
+      (void)write_part_header(p, f->seq, static_cast<int>(k), static_cast<int>(f->parts.size()), kFlagRetired, lsn);
       if (cfg_.sync) (void)::fdatasync(p->fd);
       (void)::posix_fadvise(p->fd, 0, 0, POSIX_FADV_DONTNEED);
     }
@@ -729,9 +938,18 @@ void BlockJournal::retire_ready() {
   cv_.notify_all();
 }
 
+SegRef BlockJournal::compaction_candidate(double max_live) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (order_.size() < 2) return nullptr;
+  SegRef f = order_.front();
+  if (!f->sealed || !f->complete() || f->live == 0) return nullptr;
+  if (static_cast<double>(f->live_bytes) > max_live * static_cast<double>(f->capacity())) return nullptr;
+  return f;
+}
+
 double BlockJournal::pressure() {
   std::lock_guard<std::mutex> g(mu_);
-  const double cap = static_cast<double>(cfg_.max_segs);
+  const double cap = static_cast<double>(cfg_.max_segs > 0 ? cfg_.max_segs : std::max<size_t>(1, segs_.size()));
   return std::min(1.0, static_cast<double>(order_.size()) / cap);
 }
 
@@ -745,11 +963,25 @@ JournalStats BlockJournal::stats() {
   JournalStats s = st_;
   s.segs_total = segs_.size();
   s.segs_free = free_.size();
+  s.segs_in_use = order_.size();
   s.failed = failed_;
-  const uint64_t missing = cfg_.max_segs > static_cast<int>(segs_.size()) ? cfg_.max_segs - segs_.size() : 0;
+  s.grow_blocked = grow_blocked_;
+  for (auto& seg : order_) {
+    s.live_records += seg->live;
+    s.live_bytes += seg->live_bytes;
+    s.used_bytes += seg->capacity();
+  }
+  uint64_t missing = 0;
+  if (cfg_.grow) {
+    if (!grow_blocked_ && static_cast<int>(free_.size()) < cfg_.spares &&
+        (cfg_.max_segs <= 0 || static_cast<int>(segs_.size()) < cfg_.max_segs))
+      missing = static_cast<uint64_t>(cfg_.spares) - free_.size();
+  } else if (cfg_.max_segs > static_cast<int>(segs_.size())) {
+    missing = cfg_.max_segs - segs_.size();
+  }
   s.parts_unready = missing * static_cast<uint64_t>(cfg_.parts);
   if (cfg_.zero_fill)
-    for (auto& seg : segs_)
+    for (auto& seg : cfg_.grow ? free_ : segs_)
       for (auto& p : seg->parts) s.parts_unready += p->filled ? 0 : 1;
   return s;
 }

@@ -9,6 +9,7 @@
 // hipMemcpyAsync device-to-device copy on the channel's stream.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <deque>
 #include <map>
 #include <mutex>
@@ -35,23 +36,25 @@ struct Chan {
 };
 
 std::mutex g_mu;
-std::map<std::tuple<std::string, int, int>, std::shared_ptr<Chan>> g_chans;  // (ns, src, dst)
+std::map<std::tuple<std::string, int, int, int>, std::shared_ptr<Chan>> g_chans;  // (ns, src, dst, channel)
 
-std::shared_ptr<Chan> chan(const std::string& ns, int src, int dst) {
+std::shared_ptr<Chan> chan(const std::string& ns, int src, int dst, int ch) {
   std::lock_guard<std::mutex> g(g_mu);
-  auto& c = g_chans[{ns, src, dst}];
+  auto& c = g_chans[{ns, src, dst, ch}];
   if (!c) c = std::make_shared<Chan>();
   return c;
 }
 
 class HipLoopTransport final : public P2PTransport {
  public:
-  HipLoopTransport(int device, int rank, std::string ns) : device_(device), rank_(rank), ns_(std::move(ns)) {}
+  HipLoopTransport(int device, int rank, std::string ns, int channels)
+      : device_(device), rank_(rank), ns_(std::move(ns)), channels_(channels) {}
   ~HipLoopTransport() override {
     for (auto& kv : opened_) close(kv.first);
   }
   const char* name() const override { return "hiploop"; }
   bool device_buffers() const override { return true; }
+  int channels() const override { return channels_; }
 
   std::string make_token(int peer, uint64_t gen, std::string*) override {
     return ns_ + "/" + std::to_string(rank_) + "->" + std::to_string(peer) + "@" + std::to_string(gen);
@@ -59,31 +62,33 @@ class HipLoopTransport final : public P2PTransport {
 
   bool open(int peer, uint64_t, const std::string&, const std::string&, int, std::string*) override {
     (void)hipSetDevice(device_);
-    for (auto c : {chan(ns_, rank_, peer), chan(ns_, peer, rank_)}) {
-      std::lock_guard<std::mutex> g(c->mu);
-      if (!c->stream) (void)hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-      c->open = true;
-    }
+    for (int ch = 0; ch < channels_; ++ch)
+      for (auto c : {chan(ns_, rank_, peer, ch), chan(ns_, peer, rank_, ch)}) {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (!c->stream) (void)hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        c->open = true;
+      }
     opened_[peer] = true;
     return true;
   }
 
   void close(int peer) override {
-    for (auto c : {chan(ns_, rank_, peer), chan(ns_, peer, rank_)}) {
-      std::lock_guard<std::mutex> g(c->mu);
-      c->open = false;
-      for (auto* q : {&c->sends, &c->recvs}) {
-        for (auto& p : *q) p.st->store(-1);
-        q->clear();
+    for (int ch = 0; ch < channels_; ++ch)
+      for (auto c : {chan(ns_, rank_, peer, ch), chan(ns_, peer, rank_, ch)}) {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->open = false;
+        for (auto* q : {&c->sends, &c->recvs}) {
+          for (auto& p : *q) p.st->store(-1);
+          q->clear();
+        }
       }
-    }
   }
 
-  bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
-    return post(chan(ns_, rank_, peer), true, const_cast<void*>(buf), n, op, err);
+  bool post_send(int peer, int ch, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    return post(chan(ns_, rank_, peer, ch), true, const_cast<void*>(buf), n, op, err);
   }
-  bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) override {
-    return post(chan(ns_, peer, rank_), false, buf, n, op, err);
+  bool post_recv(int peer, int ch, void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    return post(chan(ns_, peer, rank_, ch), false, buf, n, op, err);
   }
 
   int test(P2POp* op) override {
@@ -140,13 +145,14 @@ class HipLoopTransport final : public P2PTransport {
 
   int device_, rank_;
   std::string ns_;
+  int channels_;
   std::map<int, bool> opened_;
 };
 
 }  // namespace
 
-std::unique_ptr<P2PTransport> make_hiploop_transport(int device, int rank, const std::string& ns) {
-  return std::make_unique<HipLoopTransport>(device, rank, ns);
+std::unique_ptr<P2PTransport> make_hiploop_transport(int device, int rank, const std::string& ns, int channels) {
+  return std::make_unique<HipLoopTransport>(device, rank, ns, std::max(1, std::min(channels, kMaxP2PChannels)));
 }
 
 }  // namespace dfs

@@ -13,7 +13,8 @@
 //  * Each rank exports its HBM arena (one hipMalloc) with hipIpcGetMemHandle; the peer maps
 //    it once per pair generation (xGMI peer mapping between GPUs, plain HBM when the ranks
 //    share one GPU).
-//  * Each directed channel has a ring in /dev/shm created by the RECEIVER: post_recv writes
+//  * Each directed channel (`channels` per direction of a pair, each with its own ring, copy
+//    stream, host worker and sequence space) has a ring in /dev/shm created by the RECEIVER: post_recv writes
 //    (offset in its arena, length) into slot k and bumps `posted` — the credit.
 //  * The SENDER's channel worker matches its k-th posted send with slot k, checks the length
 //    (RCCL fails a mismatched pair, so do we), and queues one copy-engine hipMemcpyAsync of
@@ -39,6 +40,7 @@
 #include <sys/syscall.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <climits>
 #include <cstdlib>
@@ -59,7 +61,7 @@ namespace {
 using Clock = std::chrono::steady_clock;
 
 constexpr uint64_t kRingMagic = 0x474e495243504944ull;  // "DIPCRING"
-constexpr char kTokMagic[8] = {'D', 'F', 'S', 'I', 'P', 'C', '1', '\0'};
+constexpr char kTokMagic[8] = {'D', 'F', 'S', 'I', 'P', 'C', '2', '\0'};
 constexpr int kMaxRanks = 64;
 constexpr size_t kProbeBytes = 2 * kMaxRanks * 64;  // [0,4096) mailbox per sender; [4096,8192) our patterns
 
@@ -71,7 +73,9 @@ struct TokenWire {
   hipIpcMemHandle_t arena;
   uint64_t arena_bytes;
   hipIpcMemHandle_t probe;
-  char ring[96];  // shm name of the creator's INBOUND ring (the creator receives on it)
+  uint32_t channels;
+  uint32_t pad;
+  char ring[96];  // shm name prefix of the creator's INBOUND rings (`<prefix>_c<k>`, one per channel)
 };
 
 long futex(uint32_t* addr, int op, uint32_t val, const timespec* ts) {
@@ -183,8 +187,9 @@ struct SendItem {
 
 class IpcTransport final : public P2PTransport {
  public:
-  IpcTransport(int device, int rank, std::string ns, uint8_t* arena, uint64_t arena_bytes, bool spin)
-      : device_(device), rank_(rank), ns_(std::move(ns)), arena_(arena), arena_bytes_(arena_bytes), spin_(spin) {
+  IpcTransport(int device, int rank, std::string ns, uint8_t* arena, uint64_t arena_bytes, bool spin, int channels)
+      : device_(device), rank_(rank), ns_(std::move(ns)), arena_(arena), arena_bytes_(arena_bytes), spin_(spin),
+        channels_(channels) {
     const char* ms = std::getenv("DFS_IPC_SPIN_MS");
     spin_ticks_ = wall_ticks_per_ms(device) * static_cast<uint64_t>(ms ? std::max(1, std::atoi(ms)) : 5000);
   }
@@ -216,31 +221,37 @@ class IpcTransport final : public P2PTransport {
     for (int p : peers) close(p);
     (void)hipSetDevice(device_);
     std::lock_guard<std::mutex> g(mu_);
-    for (auto& kv : links_) {
-      Link& l = *kv.second;
-      for (hipStream_t s : {l.send_stream, l.recv_stream})
-        if (s) (void)hipStreamDestroy(s);
-      if (l.done_ctr) (void)hipFree(l.done_ctr);
-    }
+    for (auto& kv : links_)
+      for (auto& c : kv.second->ch) {
+        for (hipStream_t s : {c->send_stream, c->recv_stream})
+          if (s) (void)hipStreamDestroy(s);
+        if (c->done_ctr) (void)hipFree(c->done_ctr);
+      }
     for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
     if (probe_) (void)hipFree(probe_);
   }
 
   const char* name() const override { return spin_ ? "hipipc-spin" : "hipipc"; }
   bool device_buffers() const override { return true; }
+  int channels() const override { return channels_; }
 
+  // our inbound rings for the pair, one per channel: the token carries their name prefix
   std::string make_token(int peer, uint64_t gen, std::string* err) override {
     if (peer < 0 || peer >= kMaxRanks) {
       *err = "peer rank out of range";
       return {};
     }
-    const std::string name = "/dfs_ipc_" + ns_ + "_" + std::to_string(rank_) + "_" + std::to_string(peer) + "_" +
-                             std::to_string(gen) + "_" + std::to_string(::getpid());
-    auto ring = map_ring(name, true, gen, err);
-    if (!ring) return {};
+    const std::string prefix = "/dfs_ipc_" + ns_ + "_" + std::to_string(rank_) + "_" + std::to_string(peer) + "_" +
+                               std::to_string(gen) + "_" + std::to_string(::getpid());
+    std::vector<std::shared_ptr<RingMap>> rings;
+    for (int c = 0; c < channels_; ++c) {
+      auto ring = map_ring(prefix + "_c" + std::to_string(c), true, gen, err);
+      if (!ring) return {};
+      rings.push_back(ring);
+    }
     {
       std::lock_guard<std::mutex> g(mu_);
-      made_[peer] = {gen, ring};
+      made_[peer] = {gen, std::move(rings)};
     }
     TokenWire t{};
     std::memcpy(t.magic, kTokMagic, sizeof t.magic);
@@ -252,7 +263,8 @@ class IpcTransport final : public P2PTransport {
     t.arena = arena_h_;
     t.arena_bytes = arena_bytes_;
     t.probe = probe_h_;
-    std::snprintf(t.ring, sizeof t.ring, "%s", name.c_str());
+    t.channels = static_cast<uint32_t>(channels_);
+    std::snprintf(t.ring, sizeof t.ring, "%s", prefix.c_str());
     return std::string(reinterpret_cast<const char*>(&t), sizeof t);
   }
 
@@ -272,10 +284,15 @@ class IpcTransport final : public P2PTransport {
       *err = "hipipc peers disagree on spin mode";
       return false;
     }
+    if (static_cast<int>(tw.channels) != channels_) {
+      *err = "hipipc peers disagree on the channel count";
+      return false;
+    }
     (void)hipSetDevice(device_);
     Link& l = link(peer);
     std::lock_guard<std::mutex> g(l.mu);
     teardown_locked(l);
+    std::vector<std::shared_ptr<RingMap>> ins;
     {
       std::lock_guard<std::mutex> mg(mu_);
       auto it = made_.find(peer);
@@ -283,12 +300,28 @@ class IpcTransport final : public P2PTransport {
         *err = "no inbound ring for generation " + std::to_string(gen);
         return false;
       }
-      l.in = it->second.second;
+      ins = std::move(it->second.second);
       made_.erase(it);
     }
     tw.ring[sizeof tw.ring - 1] = '\0';
-    l.out = map_ring(tw.ring, false, gen, err);
-    if (!l.out) return fail_open(l, err);
+    while (static_cast<int>(l.ch.size()) < channels_) l.ch.push_back(std::make_unique<Lane>());
+    for (int c = 0; c < channels_; ++c) {
+      Lane& ln = *l.ch[c];
+      ln.in = ins[c];
+      ln.out = map_ring(std::string(tw.ring) + "_c" + std::to_string(c), false, gen, err);
+      if (!ln.out) return fail_open(l, err);
+      for (hipStream_t* st : {&ln.send_stream, &ln.recv_stream})
+        if (!*st && hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
+          *err = "hipStreamCreate failed";
+          return fail_open(l, err);
+        }
+      if (!ln.done_ctr && hipMalloc(reinterpret_cast<void**>(&ln.done_ctr), sizeof(uint32_t)) != hipSuccess) {
+        *err = "hipMalloc failed";
+        return fail_open(l, err);
+      }
+      (void)hipMemsetAsync(ln.done_ctr, 0, sizeof(uint32_t), ln.send_stream);
+      ln.send_seq = ln.recv_seq = 0;
+    }
     void* pa = nullptr;
     if (hipIpcOpenMemHandle(&pa, tw.arena, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
       *err = std::string("hipIpcOpenMemHandle(peer arena): ") + hipGetErrorString(hipGetLastError());
@@ -302,36 +335,29 @@ class IpcTransport final : public P2PTransport {
       return fail_open(l, err);
     }
     l.peer_probe = static_cast<uint8_t*>(pp);
-    for (hipStream_t* s : {&l.send_stream, &l.recv_stream})
-      if (!*s && hipStreamCreateWithFlags(s, hipStreamNonBlocking) != hipSuccess) {
-        *err = "hipStreamCreate failed";
-        return fail_open(l, err);
-      }
-    if (!l.done_ctr && hipMalloc(reinterpret_cast<void**>(&l.done_ctr), sizeof(uint32_t)) != hipSuccess) {
-      *err = "hipMalloc failed";
-      return fail_open(l, err);
-    }
-    (void)hipMemsetAsync(l.done_ctr, 0, sizeof(uint32_t), l.send_stream);
     l.gen = gen;
-    l.send_seq = l.recv_seq = 0;
-    st(&l.in->r->receiver_ready, 1u);
-    st(&l.out->r->sender_attached, 1u);
+    for (auto& c : l.ch) {
+      st(&c->in->r->receiver_ready, 1u);
+      st(&c->out->r->sender_attached, 1u);
+    }
     // warm-up: 64 bytes each way through the peer's exported probe, proving the IPC mapping
-    // and the copy path end to end before the pair is declared up
+    // and the copy path end to end before the pair is declared up (channel 0's stream and
+    // ring; the other channels' rings were mapped above and checked for the generation)
+    Lane& c0 = *l.ch[0];
     uint64_t pat[8] = {kRingMagic, gen, static_cast<uint64_t>(rank_), static_cast<uint64_t>(peer), 0, 0, 0, 0};
     uint8_t* mine = probe_ + kMaxRanks * 64 + peer * 64;
-    if (hipMemcpyAsync(mine, pat, sizeof pat, hipMemcpyHostToDevice, l.send_stream) != hipSuccess ||
-        hipMemcpyAsync(l.peer_probe + rank_ * 64, mine, sizeof pat, hipMemcpyDeviceToDevice, l.send_stream) !=
+    if (hipMemcpyAsync(mine, pat, sizeof pat, hipMemcpyHostToDevice, c0.send_stream) != hipSuccess ||
+        hipMemcpyAsync(l.peer_probe + rank_ * 64, mine, sizeof pat, hipMemcpyDeviceToDevice, c0.send_stream) !=
             hipSuccess ||
-        hipStreamSynchronize(l.send_stream) != hipSuccess) {
+        hipStreamSynchronize(c0.send_stream) != hipSuccess) {
       *err = "warm-up copy failed";
       return fail_open(l, err);
     }
-    st(&l.out->r->warm, gen);
-    ring_wake(l.out->r);
+    st(&c0.out->r->warm, gen);
+    ring_wake(c0.out->r);
     auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
-    while (ld(&l.in->r->warm) != gen) {
-      if (Clock::now() > deadline || ld(&l.in->r->abort)) {
+    while (ld(&c0.in->r->warm) != gen) {
+      if (Clock::now() > deadline || ld(&c0.in->r->abort)) {
         *err = "peer never delivered its warm-up copy";
         return fail_open(l, err);
       }
@@ -343,12 +369,14 @@ class IpcTransport final : public P2PTransport {
       *err = "warm-up bytes did not arrive intact";
       return fail_open(l, err);
     }
-    // both sides attached: the ring's name can go (the mappings stay)
-    ::shm_unlink(l.in->name.c_str());
-    l.in->owner = false;
-    if (!spin_) {
-      l.stop.store(false);
-      l.worker = std::thread([this, &l, out = l.out] { worker(&l, out); });
+    for (auto& c : l.ch) {
+      // both sides attached: the ring's name can go (the mappings stay)
+      ::shm_unlink(c->in->name.c_str());
+      c->in->owner = false;
+      if (!spin_) {
+        c->stop.store(false);
+        c->worker = std::thread([this, lp = &l, cp = c.get(), out = c->out] { worker(lp, cp, out); });
+      }
     }
     l.up = true;
     return true;
@@ -360,23 +388,24 @@ class IpcTransport final : public P2PTransport {
     teardown_locked(l);
   }
 
-  bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
+  bool post_send(int peer, int ch, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
     Link& l = link(peer);
     std::lock_guard<std::mutex> g(l.mu);
-    if (!l.up) {
+    if (!l.up || ch < 0 || ch >= static_cast<int>(l.ch.size())) {
       *err = "hipipc channel down";
       return false;
     }
-    const uint64_t seq = l.send_seq++;
-    op->ctx = l.out;
+    Lane& c = *l.ch[ch];
+    const uint64_t seq = c.send_seq++;
+    op->ctx = c.out;
     op->seq = seq;
     if (spin_) {
       (void)hipSetDevice(device_);
-      IpcSendArgs a{&l.out->dev->posted, &l.out->dev->landed, &l.out->dev->abort, l.out->dev->slots, seq,
-                    static_cast<const uint8_t*>(buf), l.peer_arena, l.peer_arena_bytes, n, l.done_ctr, spin_ticks_};
+      IpcSendArgs a{&c.out->dev->posted, &c.out->dev->landed, &c.out->dev->abort, c.out->dev->slots, seq,
+                    static_cast<const uint8_t*>(buf), l.peer_arena, l.peer_arena_bytes, n, c.done_ctr, spin_ticks_};
       hipEvent_t ev = event();
-      if (!ev || launch_ipc_send(a, send_grid(n), l.send_stream) != hipSuccess ||
-          hipEventRecord(ev, l.send_stream) != hipSuccess) {
+      if (!ev || launch_ipc_send(a, send_grid(n), c.send_stream) != hipSuccess ||
+          hipEventRecord(ev, c.send_stream) != hipSuccess) {
         if (ev) release_event(ev);
         *err = "spin send launch failed";
         return false;
@@ -386,45 +415,46 @@ class IpcTransport final : public P2PTransport {
     }
     op->state = std::make_shared<std::atomic<int>>(0);
     {
-      std::lock_guard<std::mutex> q(l.qmu);
-      l.pending.push_back(SendItem{static_cast<const uint8_t*>(buf), n, seq, op->state, nullptr});
+      std::lock_guard<std::mutex> q(c.qmu);
+      c.pending.push_back(SendItem{static_cast<const uint8_t*>(buf), n, seq, op->state, nullptr});
     }
-    ring_wake(l.out->r);
+    ring_wake(c.out->r);
     return true;
   }
 
-  bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) override {
+  bool post_recv(int peer, int ch, void* buf, uint64_t n, P2POp* op, std::string* err) override {
     Link& l = link(peer);
     std::lock_guard<std::mutex> g(l.mu);
-    if (!l.up) {
+    if (!l.up || ch < 0 || ch >= static_cast<int>(l.ch.size())) {
       *err = "hipipc channel down";
       return false;
     }
+    Lane& c = *l.ch[ch];
     auto* p = static_cast<uint8_t*>(buf);
     if (p < arena_ || static_cast<uint64_t>(p - arena_) > arena_bytes_ || n > arena_bytes_ - (p - arena_)) {
       *err = "receive buffer outside the exported arena";
       return false;
     }
-    IpcRing* r = l.in->r;
-    const uint64_t seq = l.recv_seq;
+    IpcRing* r = c.in->r;
+    const uint64_t seq = c.recv_seq;
     if (seq - ld(&r->landed) >= kIpcRing) {
       *err = "hipipc ring full";
       return false;
     }
-    l.recv_seq++;
+    c.recv_seq++;
     IpcSlot& s = r->slots[seq % kIpcRing];
     __atomic_store_n(&s.off, static_cast<uint64_t>(p - arena_), __ATOMIC_RELAXED);
     __atomic_store_n(&s.n, n, __ATOMIC_RELAXED);
     st(&r->posted, seq + 1);  // the credit: the slot is visible before the count
     ring_wake(r);
-    op->ctx = l.in;
+    op->ctx = c.in;
     op->seq = seq;
     if (spin_) {
       (void)hipSetDevice(device_);
       hipEvent_t ev = event();
-      if (!ev || launch_ipc_wait(&l.in->dev->landed, seq + 1, &l.in->dev->abort, spin_ticks_, l.recv_stream) !=
+      if (!ev || launch_ipc_wait(&c.in->dev->landed, seq + 1, &c.in->dev->abort, spin_ticks_, c.recv_stream) !=
                      hipSuccess ||
-          hipEventRecord(ev, l.recv_stream) != hipSuccess) {
+          hipEventRecord(ev, c.recv_stream) != hipSuccess) {
         if (ev) release_event(ev);
         st(&r->abort, 1u);  // the credit is out but its waiter is not: the channel is unusable
         *err = "spin wait launch failed";
@@ -478,14 +508,10 @@ class IpcTransport final : public P2PTransport {
   }
 
  private:
-  struct Link {
-    std::mutex mu;  // open / close / post
-    bool up = false;
-    uint64_t gen = 0;
-    std::shared_ptr<RingMap> in, out;  // in: we receive (our ring); out: we send (the peer's ring)
-    uint8_t* peer_arena = nullptr;
-    uint64_t peer_arena_bytes = 0;
-    uint8_t* peer_probe = nullptr;
+  // One channel of a pair: its two rings (in: we receive, our ring; out: we send, the peer's
+  // ring), its copy stream and host worker, its own sequence space.
+  struct Lane {
+    std::shared_ptr<RingMap> in, out;
     hipStream_t send_stream = nullptr, recv_stream = nullptr;
     uint32_t* done_ctr = nullptr;
     uint64_t send_seq = 0, recv_seq = 0;
@@ -493,6 +519,15 @@ class IpcTransport final : public P2PTransport {
     std::deque<SendItem> pending;
     std::thread worker;
     std::atomic<bool> stop{false};
+  };
+  struct Link {
+    std::mutex mu;  // open / close / post
+    bool up = false;
+    uint64_t gen = 0;
+    uint8_t* peer_arena = nullptr;
+    uint64_t peer_arena_bytes = 0;
+    uint8_t* peer_probe = nullptr;
+    std::vector<std::unique_ptr<Lane>> ch;
   };
 
   Link& link(int peer) {
@@ -512,60 +547,65 @@ class IpcTransport final : public P2PTransport {
     return false;
   }
 
-  // Abort both rings, stop the worker, drain both streams (copies finish; spin kernels see
+  // Abort every ring, stop the workers, drain the streams (copies finish; spin kernels see
   // the abort), unmap the peer. When this returns nothing of the old generation can land.
   void teardown_locked(Link& l) {
     (void)hipSetDevice(device_);
-    for (auto* m : {l.in.get(), l.out.get()})
-      if (m) {
-        st(&m->r->abort, 1u);
-        ring_wake(m->r);
+    for (auto& c : l.ch)
+      for (auto* m : {c->in.get(), c->out.get()})
+        if (m) {
+          st(&m->r->abort, 1u);
+          ring_wake(m->r);
+        }
+    for (auto& c : l.ch) {
+      if (c->worker.joinable()) {
+        c->stop.store(true);
+        if (c->out) ring_wake(c->out->r);
+        c->worker.join();
       }
-    if (l.worker.joinable()) {
-      l.stop.store(true);
-      if (l.out) ring_wake(l.out->r);
-      l.worker.join();
+      {
+        std::lock_guard<std::mutex> q(c->qmu);
+        for (auto& it : c->pending) finish_send(it.st, -1);
+        c->pending.clear();
+      }
+      for (hipStream_t s : {c->send_stream, c->recv_stream})
+        if (s) (void)hipStreamSynchronize(s);
     }
-    {
-      std::lock_guard<std::mutex> q(l.qmu);
-      for (auto& it : l.pending) finish_send(it.st, -1);
-      l.pending.clear();
-    }
-    for (hipStream_t s : {l.send_stream, l.recv_stream})
-      if (s) (void)hipStreamSynchronize(s);
     if (l.peer_arena) (void)hipIpcCloseMemHandle(l.peer_arena);
     if (l.peer_probe) (void)hipIpcCloseMemHandle(l.peer_probe);
     l.peer_arena = l.peer_probe = nullptr;
-    l.in.reset();
-    l.out.reset();
+    for (auto& c : l.ch) {
+      c->in.reset();
+      c->out.reset();
+    }
     l.up = false;
   }
 
   // Host-driven sender of one channel: match posted sends with the receiver's credits in
   // order, queue the copies, publish `landed` as their events complete (in order: one stream).
-  void worker(Link* l, std::shared_ptr<RingMap> out) {
+  void worker(Link* l, Lane* c, std::shared_ptr<RingMap> out) {
     (void)hipSetDevice(device_);
     IpcRing* r = out->r;
     std::deque<SendItem> inflight;
     int idle = 0;
     bool dead = false;
-    while (!l->stop.load() && !dead) {
+    while (!c->stop.load() && !dead) {
       bool progress = false;
       for (;;) {
         SendItem it;
         {
-          std::lock_guard<std::mutex> q(l->qmu);
-          if (l->pending.empty() || ld(&r->posted) <= l->pending.front().seq) break;
-          it = l->pending.front();
-          l->pending.pop_front();
+          std::lock_guard<std::mutex> q(c->qmu);
+          if (c->pending.empty() || ld(&r->posted) <= c->pending.front().seq) break;
+          it = c->pending.front();
+          c->pending.pop_front();
         }
         const IpcSlot& s = r->slots[it.seq % kIpcRing];
         const uint64_t off = __atomic_load_n(&s.off, __ATOMIC_RELAXED), n = __atomic_load_n(&s.n, __ATOMIC_RELAXED);
         hipEvent_t ev = nullptr;
         if (n != it.n || off > l->peer_arena_bytes || n > l->peer_arena_bytes - off || ld(&r->abort) ||
-            (n && hipMemcpyAsync(l->peer_arena + off, it.src, n, hipMemcpyDeviceToDevice, l->send_stream) !=
+            (n && hipMemcpyAsync(l->peer_arena + off, it.src, n, hipMemcpyDeviceToDevice, c->send_stream) !=
                       hipSuccess) ||
-            !(ev = event()) || hipEventRecord(ev, l->send_stream) != hipSuccess) {
+            !(ev = event()) || hipEventRecord(ev, c->send_stream) != hipSuccess) {
           if (ev) release_event(ev);
           finish_send(it.st, -1);
           st(&r->abort, 1u);  // mismatched sizes or a failed copy end the channel (as RCCL would)
@@ -609,8 +649,8 @@ class IpcTransport final : public P2PTransport {
       // nothing to do: sleep until a send is posted here or a credit arrives from the peer
       const uint32_t bell = __atomic_load_n(&r->doorbell, __ATOMIC_ACQUIRE);
       {
-        std::lock_guard<std::mutex> q(l->qmu);
-        if (!l->pending.empty() && ld(&r->posted) > l->pending.front().seq) continue;
+        std::lock_guard<std::mutex> q(c->qmu);
+        if (!c->pending.empty() && ld(&r->posted) > c->pending.front().seq) continue;
       }
       timespec ts{0, 2'000'000};
       futex(&r->doorbell, FUTEX_WAIT, bell, &ts);
@@ -646,12 +686,14 @@ class IpcTransport final : public P2PTransport {
   uint8_t* arena_;
   uint64_t arena_bytes_;
   bool spin_;
+  int channels_;
   uint64_t spin_ticks_ = 0;
   hipIpcMemHandle_t arena_h_{}, probe_h_{};
   uint8_t* probe_ = nullptr;
   std::mutex mu_;
   std::map<int, std::unique_ptr<Link>> links_;
-  std::map<int, std::pair<uint64_t, std::shared_ptr<RingMap>>> made_;  // inbound rings awaiting open()
+  // inbound rings (one per channel) awaiting open()
+  std::map<int, std::pair<uint64_t, std::vector<std::shared_ptr<RingMap>>>> made_;
   std::mutex ev_mu_;
   std::vector<hipEvent_t> free_events_;
 };
@@ -659,12 +701,13 @@ class IpcTransport final : public P2PTransport {
 }  // namespace
 
 std::unique_ptr<P2PTransport> make_ipc_transport(int device, int rank, const std::string& ns, uint8_t* arena,
-                                                 uint64_t arena_bytes, bool spin, std::string* err) {
+                                                 uint64_t arena_bytes, bool spin, int channels, std::string* err) {
   if (device < 0 || arena == nullptr || arena_bytes == 0) {
     *err = "hipipc transport requires a GPU chunk store";
     return nullptr;
   }
-  auto t = std::make_unique<IpcTransport>(device, rank, ns, arena, arena_bytes, spin);
+  auto t = std::make_unique<IpcTransport>(device, rank, ns, arena, arena_bytes, spin,
+                                          std::max(1, std::min(channels, kMaxP2PChannels)));
   if (!t->init(err)) return nullptr;
   return t;
 }

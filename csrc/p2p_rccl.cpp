@@ -2,8 +2,9 @@
 //
 // One process per GPU = one ChunkServer = one RCCL rank, but replication needs
 // point-to-point traffic between arbitrary pairs with many blocks in flight, not
-// collectives over a world communicator. Each directed channel (a->b) is its own 2-rank
-// communicator (a = rank 0) with its own HIP stream: traffic on a communicator is then
+// collectives over a world communicator. Each directed channel (a->b, `channels` of them per
+// direction) is its own 2-rank communicator (a = rank 0) with its own HIP stream: traffic on
+// a communicator is then
 // unidirectional and strictly FIFO, which is exactly the matching rule the replication
 // protocol sequences against; two directions never share a communicator, so a send a->b
 // can never queue behind a receive a<-b. On the MI355X full xGMI mesh every such channel
@@ -51,7 +52,7 @@ bool settle(ncclComm_t comm, ncclResult_t r, Clock::time_point deadline, std::st
 
 class RcclTransport final : public P2PTransport {
  public:
-  RcclTransport(int device, int rank) : device_(device), rank_(rank) {}
+  RcclTransport(int device, int rank, int channels) : device_(device), rank_(rank), channels_(channels) {}
 
   ~RcclTransport() override {
     (void)hipSetDevice(device_);
@@ -59,41 +60,52 @@ class RcclTransport final : public P2PTransport {
     for (auto& kv : links_) {
       Link& l = *kv.second;
       abort_locked(l);
-      for (Chan* c : {&l.out, &l.in})
-        if (c->stream) (void)hipStreamDestroy(c->stream);
+      for (auto* v : {&l.out, &l.in})
+        for (auto& c : *v)
+          if (c.stream) (void)hipStreamDestroy(c.stream);
     }
     for (hipEvent_t e : free_events_) (void)hipEventDestroy(e);
   }
 
   const char* name() const override { return "rccl"; }
   bool device_buffers() const override { return true; }
+  int channels() const override { return channels_; }
 
+  // one unique id per channel of our direction, concatenated
   std::string make_token(int, uint64_t, std::string* err) override {
     (void)hipSetDevice(device_);
-    ncclUniqueId id;
-    ncclResult_t r = ncclGetUniqueId(&id);
-    if (r != ncclSuccess) {
-      *err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
-      return {};
+    std::string tok;
+    for (int c = 0; c < channels_; ++c) {
+      ncclUniqueId id;
+      ncclResult_t r = ncclGetUniqueId(&id);
+      if (r != ncclSuccess) {
+        *err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+        return {};
+      }
+      tok.append(id.internal, sizeof(id.internal));
     }
-    return std::string(id.internal, sizeof(id.internal));
+    return tok;
   }
 
   bool open(int peer, uint64_t gen, const std::string& tok_out, const std::string& tok_in, int timeout_ms,
             std::string* err) override {
-    if (tok_out.size() != sizeof(ncclUniqueId::internal) || tok_in.size() != sizeof(ncclUniqueId::internal)) {
-      *err = "malformed RCCL token";
+    const size_t idb = sizeof(ncclUniqueId::internal);
+    if (tok_out.size() != idb * channels_ || tok_in.size() != idb * channels_) {
+      *err = "malformed RCCL token (or the peers disagree on the channel count)";
       return false;
     }
     (void)hipSetDevice(device_);
     Link& l = link(peer);
     std::lock_guard<std::mutex> g(l.mu);
     abort_locked(l);
-    for (Chan* c : {&l.out, &l.in})
-      if (!c->stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        *err = "hipStreamCreate failed";
-        return false;
-      }
+    l.out.resize(channels_);
+    l.in.resize(channels_);
+    for (auto* v : {&l.out, &l.in})
+      for (auto& c : *v)
+        if (!c.stream && hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) {
+          *err = "hipStreamCreate failed";
+          return false;
+        }
     auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
     auto init = [&](Chan& c, const std::string& tok, int my, const std::string& what) {
       ncclUniqueId uid;
@@ -109,11 +121,16 @@ class RcclTransport final : public P2PTransport {
       }
       return settle(c.comm, r, deadline, err, what);
     };
-    const std::string tag = std::to_string(rank_) + "<->" + std::to_string(peer) + " gen " + std::to_string(gen);
-    // both ranks bring up the lo->hi communicator first, then hi->lo
-    bool ok = rank_ < peer ? init(l.out, tok_out, 0, "init out " + tag) && init(l.in, tok_in, 1, "init in " + tag)
-                           : init(l.in, tok_in, 1, "init in " + tag) && init(l.out, tok_out, 0, "init out " + tag);
-    if (ok) ok = warm_up(l, deadline, tag, err);
+    bool ok = true;
+    for (int c = 0; ok && c < channels_; ++c) {
+      const std::string tag =
+          std::to_string(rank_) + "<->" + std::to_string(peer) + " gen " + std::to_string(gen) + " ch " + std::to_string(c);
+      const std::string to = tok_out.substr(c * idb, idb), ti = tok_in.substr(c * idb, idb);
+      // both ranks bring up channel c's lo->hi communicator first, then hi->lo
+      ok = rank_ < peer ? init(l.out[c], to, 0, "init out " + tag) && init(l.in[c], ti, 1, "init in " + tag)
+                        : init(l.in[c], ti, 1, "init in " + tag) && init(l.out[c], to, 0, "init out " + tag);
+      if (ok) ok = warm_up(l.out[c], l.in[c], deadline, tag, err);
+    }
     if (!ok) {
       abort_locked(l);
       return false;
@@ -129,11 +146,11 @@ class RcclTransport final : public P2PTransport {
     abort_locked(l);
   }
 
-  bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
-    return post(peer, true, const_cast<void*>(buf), n, op, err);
+  bool post_send(int peer, int ch, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    return post(peer, ch, true, const_cast<void*>(buf), n, op, err);
   }
-  bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) override {
-    return post(peer, false, buf, n, op, err);
+  bool post_recv(int peer, int ch, void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    return post(peer, ch, false, buf, n, op, err);
   }
 
   int test(P2POp* op) override {
@@ -155,7 +172,7 @@ class RcclTransport final : public P2PTransport {
   };
   struct Link {
     std::mutex mu;  // ops on one communicator are issued by one thread at a time
-    Chan out, in;
+    std::vector<Chan> out, in;  // one per channel
     bool up = false;
   };
 
@@ -167,11 +184,12 @@ class RcclTransport final : public P2PTransport {
   }
 
   static void abort_locked(Link& l) {
-    for (Chan* c : {&l.out, &l.in})
-      if (c->comm) {
-        ncclCommAbort(c->comm);
-        c->comm = nullptr;
-      }
+    for (auto* v : {&l.out, &l.in})
+      for (auto& c : *v)
+        if (c.comm) {
+          ncclCommAbort(c.comm);
+          c.comm = nullptr;
+        }
     l.up = false;
   }
 
@@ -189,7 +207,7 @@ class RcclTransport final : public P2PTransport {
     return e;
   }
 
-  bool post(int peer, bool send, void* buf, uint64_t n, P2POp* op, std::string* err) {
+  bool post(int peer, int ch, bool send, void* buf, uint64_t n, P2POp* op, std::string* err) {
     Link& l = link(peer);
     hipEvent_t ev = event();
     if (!ev) {
@@ -197,8 +215,13 @@ class RcclTransport final : public P2PTransport {
       return false;
     }
     std::lock_guard<std::mutex> g(l.mu);
-    Chan& c = send ? l.out : l.in;
-    if (!l.up || !c.comm) {
+    if (!l.up || ch < 0 || ch >= static_cast<int>(l.out.size())) {
+      release_event(ev);
+      *err = "RCCL channel down";
+      return false;
+    }
+    Chan& c = send ? l.out[ch] : l.in[ch];
+    if (!c.comm) {
       release_event(ev);
       *err = "RCCL channel down";
       return false;
@@ -220,17 +243,17 @@ class RcclTransport final : public P2PTransport {
   }
 
   // One 4-byte transfer each way proves both lazily connected channels end to end.
-  bool warm_up(Link& l, Clock::time_point deadline, const std::string& tag, std::string* err) {
+  bool warm_up(Chan& out, Chan& in, Clock::time_point deadline, const std::string& tag, std::string* err) {
     int32_t* probe = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&probe), 2 * sizeof(int32_t)) != hipSuccess) {
       *err = "hipMalloc failed";
       return false;
     }
-    bool ok = settle(l.out.comm, ncclSend(probe, 1, ncclInt32, 1, l.out.comm, l.out.stream), deadline, err,
+    bool ok = settle(out.comm, ncclSend(probe, 1, ncclInt32, 1, out.comm, out.stream), deadline, err,
                      "warm-up send " + tag) &&
-              settle(l.in.comm, ncclRecv(probe + 1, 1, ncclInt32, 0, l.in.comm, l.in.stream), deadline, err,
+              settle(in.comm, ncclRecv(probe + 1, 1, ncclInt32, 0, in.comm, in.stream), deadline, err,
                      "warm-up recv " + tag);
-    for (Chan* c : {&l.out, &l.in}) {
+    for (Chan* c : {&out, &in}) {
       while (ok) {
         hipError_t q = hipStreamQuery(c->stream);
         if (q == hipSuccess) break;
@@ -247,7 +270,7 @@ class RcclTransport final : public P2PTransport {
     return ok;
   }
 
-  int device_, rank_;
+  int device_, rank_, channels_;
   std::mutex mu_;
   std::map<int, std::unique_ptr<Link>> links_;
   std::vector<hipEvent_t> free_events_;
@@ -354,7 +377,7 @@ RcclProbe rccl_loopback_probe(int device, uint64_t bytes, uint64_t abort_bytes, 
   return out;
 }
 
-std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, std::string* err) {
+std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, int channels, std::string* err) {
   if (device < 0) {
     *err = "RCCL transport requires a GPU";
     return nullptr;
@@ -364,7 +387,7 @@ std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, std::str
     *err = "no HIP device " + std::to_string(device);
     return nullptr;
   }
-  return std::make_unique<RcclTransport>(device, rank);
+  return std::make_unique<RcclTransport>(device, rank, std::max(1, std::min(channels, kMaxP2PChannels)));
 }
 
 }  // namespace dfs

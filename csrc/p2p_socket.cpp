@@ -1,6 +1,6 @@
 // Host-memory P2PTransport over abstract UNIX stream sockets (contract in p2p_transport.h).
 //
-// Each directed channel is one connected socket plus one worker thread that executes the
+// Each directed channel (`channels` per direction of a pair) is one connected socket plus one worker thread that executes the
 // channel's posted ops strictly in post order (send: write the bytes; recv: read exactly
 // the posted size) — the same FIFO matching rule as an RCCL p2p communicator. A "dropped"
 // send (debug hook) wedges the channel exactly like an RCCL send whose receive is never
@@ -10,6 +10,7 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
@@ -53,7 +54,7 @@ bool io_full(int fd, uint8_t* p, uint64_t n, bool send) {
 
 class SocketTransport final : public P2PTransport {
  public:
-  SocketTransport(int rank, std::string ns) : rank_(rank), ns_(std::move(ns)) {}
+  SocketTransport(int rank, std::string ns, int channels) : rank_(rank), ns_(std::move(ns)), channels_(channels) {}
   ~SocketTransport() override {
     std::vector<int> peers;
     {
@@ -62,35 +63,46 @@ class SocketTransport final : public P2PTransport {
     }
     for (int p : peers) close(p);
     std::lock_guard<std::mutex> g(mu_);
-    for (auto& kv : listeners_) ::close(kv.second);
+    for (auto& kv : listeners_)
+      for (int fd : kv.second) ::close(fd);
   }
 
   const char* name() const override { return "socket"; }
   bool device_buffers() const override { return false; }
+  int channels() const override { return channels_; }
 
+  // one listening socket per channel of our direction; the token is their names, one a line
   std::string make_token(int peer, uint64_t gen, std::string* err) override {
     static std::atomic<uint64_t> nonce{std::random_device{}()};
-    std::string name = "dfs_p2p_" + ns_ + "_" + std::to_string(rank_) + "_" + std::to_string(peer) + "_" +
-                       std::to_string(gen) + "_" + std::to_string(nonce.fetch_add(1));
-    int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
-    sockaddr_un a;
-    socklen_t len = abstract_addr(name, &a);
-    if (fd < 0 || ::bind(fd, reinterpret_cast<sockaddr*>(&a), len) != 0 || ::listen(fd, 4) != 0) {
-      *err = std::string("p2p listen: ") + std::strerror(errno);
-      if (fd >= 0) ::close(fd);
-      return {};
+    std::string tok;
+    std::vector<int> fds;
+    for (int ch = 0; ch < channels_; ++ch) {
+      std::string name = "dfs_p2p_" + ns_ + "_" + std::to_string(rank_) + "_" + std::to_string(peer) + "_" +
+                         std::to_string(gen) + "_" + std::to_string(ch) + "_" + std::to_string(nonce.fetch_add(1));
+      int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+      sockaddr_un a;
+      socklen_t len = abstract_addr(name, &a);
+      if (fd < 0 || ::bind(fd, reinterpret_cast<sockaddr*>(&a), len) != 0 || ::listen(fd, 4) != 0) {
+        *err = std::string("p2p listen: ") + std::strerror(errno);
+        if (fd >= 0) ::close(fd);
+        for (int f : fds) ::close(f);
+        return {};
+      }
+      fds.push_back(fd);
+      tok += (ch ? "\n" : "") + name;
     }
     std::lock_guard<std::mutex> g(mu_);
     auto it = listeners_.find(peer);
-    if (it != listeners_.end()) ::close(it->second);
-    listeners_[peer] = fd;
-    return name;
+    if (it != listeners_.end())
+      for (int fd : it->second) ::close(fd);
+    listeners_[peer] = std::move(fds);
+    return tok;
   }
 
   bool open(int peer, uint64_t, const std::string& tok_out, const std::string& tok_in, int timeout_ms,
             std::string* err) override {
     close(peer);
-    int lfd = -1;
+    std::vector<int> lfds;
     {
       std::lock_guard<std::mutex> g(mu_);
       auto it = listeners_.find(peer);
@@ -98,49 +110,68 @@ class SocketTransport final : public P2PTransport {
         *err = "no listener for our channel token " + tok_out;
         return false;
       }
-      lfd = it->second;
+      lfds = std::move(it->second);
       listeners_.erase(it);
     }
-    auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
-    // connect to the peer's listener first (a listening socket accepts the connection into
-    // its backlog before accept()), then accept ours: both ranks do the same, no wait cycle
-    int in_fd = -1;
-    while (in_fd < 0) {
-      int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
-      sockaddr_un a;
-      socklen_t len = abstract_addr(tok_in, &a);
-      if (fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr*>(&a), len) == 0) {
-        in_fd = fd;
-        break;
-      }
-      if (fd >= 0) ::close(fd);
-      if (Clock::now() > deadline) {
-        ::close(lfd);
-        *err = "p2p connect to " + tok_in + " timed out";
-        return false;
-      }
-      std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    std::vector<std::string> in_names;
+    for (size_t pos = 0;;) {
+      size_t nl = tok_in.find('\n', pos);
+      in_names.push_back(tok_in.substr(pos, nl == std::string::npos ? std::string::npos : nl - pos));
+      if (nl == std::string::npos) break;
+      pos = nl + 1;
     }
-    int out_fd = -1;
-    for (;;) {
+    auto fail = [&](const std::string& e, std::vector<int>& opened) {
+      for (int fd : lfds) ::close(fd);
+      for (int fd : opened) ::close(fd);
+      *err = e;
+      return false;
+    };
+    std::vector<int> in_fds, out_fds;
+    if (static_cast<int>(in_names.size()) != channels_ || static_cast<int>(lfds.size()) != channels_)
+      return fail("p2p peers disagree on the channel count", in_fds);
+    auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
+    // connect to every listener of the peer first (a listening socket accepts the connection
+    // into its backlog before accept()), then accept ours: both ranks do the same, no wait cycle
+    for (const auto& nm : in_names) {
+      int in_fd = -1;
+      while (in_fd < 0) {
+        int fd = ::socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+        sockaddr_un a;
+        socklen_t len = abstract_addr(nm, &a);
+        if (fd >= 0 && ::connect(fd, reinterpret_cast<sockaddr*>(&a), len) == 0) {
+          in_fd = fd;
+          break;
+        }
+        if (fd >= 0) ::close(fd);
+        if (Clock::now() > deadline) return fail("p2p connect to " + nm + " timed out", in_fds);
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      }
+      in_fds.push_back(in_fd);
+    }
+    for (int lfd : lfds) {
+      int out_fd = -1;
       int left = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count());
       pollfd p{lfd, POLLIN, 0};
-      if (left <= 0 || ::poll(&p, 1, left) <= 0) break;
-      out_fd = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
-      break;
+      if (left > 0 && ::poll(&p, 1, left) > 0) out_fd = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+      if (out_fd < 0) {
+        for (int fd : out_fds) ::close(fd);
+        return fail("p2p accept for " + tok_out + " timed out", in_fds);
+      }
+      out_fds.push_back(out_fd);
     }
-    ::close(lfd);
-    if (out_fd < 0) {
-      ::close(in_fd);
-      *err = "p2p accept for " + tok_out + " timed out";
-      return false;
-    }
+    for (int fd : lfds) ::close(fd);
     auto link = std::make_shared<Link>();
-    link->out.fd = out_fd;
-    link->in.fd = in_fd;
-    link->out.send = true;
-    link->out.worker = std::thread([c = &link->out] { run(c); });
-    link->in.worker = std::thread([c = &link->in] { run(c); });
+    for (int ch = 0; ch < channels_; ++ch) {
+      for (int dir = 0; dir < 2; ++dir) {
+        auto c = std::make_unique<Chan>();
+        c->fd = dir == 0 ? out_fds[ch] : in_fds[ch];
+        c->send = dir == 0;
+        c->link = link.get();
+        (dir == 0 ? link->out : link->in).push_back(std::move(c));
+      }
+    }
+    for (auto* v : {&link->out, &link->in})
+      for (auto& c : *v) c->worker = std::thread([cp = c.get()] { run(cp); });
     std::lock_guard<std::mutex> g(mu_);
     links_[peer] = std::move(link);
     return true;
@@ -155,42 +186,39 @@ class SocketTransport final : public P2PTransport {
       l = it->second;
       links_.erase(it);
     }
-    for (Chan* c : {&l->out, &l->in}) {
-      {
-        std::lock_guard<std::mutex> g(c->mu);
-        c->stop = true;
+    for (auto* v : {&l->out, &l->in})
+      for (auto& c : *v) {
+        {
+          std::lock_guard<std::mutex> g(c->mu);
+          c->stop = true;
+        }
+        ::shutdown(c->fd, SHUT_RDWR);
+        c->cv.notify_all();
       }
-      ::shutdown(c->fd, SHUT_RDWR);
-      c->cv.notify_all();
-    }
-    for (Chan* c : {&l->out, &l->in}) {
-      if (c->worker.joinable()) c->worker.join();
-      ::close(c->fd);
-      for (auto& op : c->q) op.st->store(-1);  // never executed
-      c->q.clear();
-    }
+    for (auto* v : {&l->out, &l->in})
+      for (auto& c : *v) {
+        if (c->worker.joinable()) c->worker.join();
+        ::close(c->fd);
+        for (auto& op : c->q) op.st->store(-1);  // never executed
+        c->q.clear();
+      }
   }
 
-  bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
-    return post(peer, true, const_cast<void*>(buf), n, op, err);
+  bool post_send(int peer, int ch, const void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    return post(peer, ch, true, const_cast<void*>(buf), n, op, err);
   }
-  bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) override {
-    return post(peer, false, buf, n, op, err);
+  bool post_recv(int peer, int ch, void* buf, uint64_t n, P2POp* op, std::string* err) override {
+    return post(peer, ch, false, buf, n, op, err);
   }
   int test(P2POp* op) override { return op->state ? op->state->load() : -1; }
   void release(P2POp* op) override { op->state.reset(); }
 
+  // the next `n` sends to the peer vanish, whichever channel carries them
   void debug_drop_sends(int peer, int n) override {
-    if (auto l = find(peer)) {
-      std::lock_guard<std::mutex> g(l->out.mu);
-      l->out.drop += n;
-    }
+    if (auto l = find(peer)) l->drop += n;
   }
   void debug_stall(int peer, int ms) override {
-    if (auto l = find(peer)) {
-      std::lock_guard<std::mutex> g(l->out.mu);
-      l->out.stall_ms = ms;
-    }
+    if (auto l = find(peer)) l->stall_ms = ms;
   }
 
  private:
@@ -199,19 +227,20 @@ class SocketTransport final : public P2PTransport {
     uint64_t n;
     std::shared_ptr<std::atomic<int>> st;
   };
+  struct Link;
   struct Chan {
     int fd = -1;
     bool send = false;
+    Link* link = nullptr;
     std::mutex mu;
     std::condition_variable cv;
     std::deque<Op> q;
     bool stop = false;
-    int drop = 0;
-    int stall_ms = 0;
     std::thread worker;
   };
   struct Link {
-    Chan out, in;
+    std::vector<std::unique_ptr<Chan>> out, in;  // one per channel
+    std::atomic<int> drop{0}, stall_ms{0};        // test hooks, shared by the out channels
   };
 
   std::shared_ptr<Link> find(int peer) {
@@ -220,13 +249,17 @@ class SocketTransport final : public P2PTransport {
     return it == links_.end() ? nullptr : it->second;
   }
 
-  bool post(int peer, bool send, void* buf, uint64_t n, P2POp* op, std::string* err) {
+  bool post(int peer, int ch, bool send, void* buf, uint64_t n, P2POp* op, std::string* err) {
     auto l = find(peer);
     if (!l) {
       *err = "p2p channel down";
       return false;
     }
-    Chan& c = send ? l->out : l->in;
+    if (ch < 0 || ch >= channels_) {
+      *err = "p2p channel out of range";
+      return false;
+    }
+    Chan& c = send ? *l->out[ch] : *l->in[ch];
     op->state = std::make_shared<std::atomic<int>>(0);
     std::lock_guard<std::mutex> g(c.mu);
     if (c.stop) {
@@ -247,16 +280,15 @@ class SocketTransport final : public P2PTransport {
         std::unique_lock<std::mutex> lk(c->mu);
         c->cv.wait(lk, [&] { return c->stop || (!wedged && !c->q.empty()); });
         if (c->stop) return;
-        if (c->send && c->drop > 0) {
+        int d = c->send ? c->link->drop.load() : 0;
+        if (d > 0 && c->link->drop.compare_exchange_strong(d, d - 1)) {
           // the send "vanishes": it and every later op of this channel stay pending
-          c->drop--;
           wedged = true;
           continue;
         }
         op = c->q.front();
         c->q.pop_front();
-        stall = c->stall_ms;
-        c->stall_ms = 0;
+        if (c->send) stall = c->link->stall_ms.exchange(0);
       }
       if (stall) std::this_thread::sleep_for(std::chrono::milliseconds(stall));
       bool ok = io_full(c->fd, op.buf, op.n, c->send);
@@ -273,15 +305,16 @@ class SocketTransport final : public P2PTransport {
 
   int rank_;
   std::string ns_;
+  int channels_;
   std::mutex mu_;
   std::map<int, std::shared_ptr<Link>> links_;
-  std::map<int, int> listeners_;  // peer -> listening fd of our pending out-channel token
+  std::map<int, std::vector<int>> listeners_;  // peer -> listening fds of our pending out-channel token
 };
 
 }  // namespace
 
-std::unique_ptr<P2PTransport> make_socket_transport(int rank, const std::string& ns) {
-  return std::make_unique<SocketTransport>(rank, ns);
+std::unique_ptr<P2PTransport> make_socket_transport(int rank, const std::string& ns, int channels) {
+  return std::make_unique<SocketTransport>(rank, ns, std::max(1, std::min(channels, kMaxP2PChannels)));
 }
 
 }  // namespace dfs

@@ -2,9 +2,12 @@
 // under chain/fan-out replication (replication.h).
 //
 // Contract (what RCCL p2p gives us, and what the CPU test transport reproduces):
-//  * between two ranks there are two independent directed channels (a->b, b->a);
+//  * between two ranks each direction (a->b, b->a) has `channels()` independent FIFO
+//    channels (round 5: several per direction, so one slow transfer — a slice still being
+//    staged, a large block — does not hold up the pair's other transfers);
 //  * transfers on one channel are matched strictly in post order: the k-th post_send on
-//    a->b lands in the buffer of b's k-th post_recv from a, and sizes must agree;
+//    channel c of a->b lands in the buffer of b's k-th post_recv on channel c from a, and
+//    sizes must agree; different channels never wait for each other;
 //  * posts never block; completion is observed with test(); an op whose peer never posts
 //    the matching op never completes — only close() (ncclCommAbort) ends it;
 //  * a channel pair is brought up for a generation by open() on BOTH ranks with the
@@ -13,7 +16,7 @@
 //
 // Implementations:
 //  * RcclTransport  (p2p_rccl.cpp): one 2-rank nonblocking communicator + HIP stream per
-//    direction; buffers are HBM pointers of our GPU, each op records a hipEvent.
+//    channel and direction; buffers are HBM pointers of our GPU, each op records a hipEvent.
 //  * IpcTransport   (p2p_ipc.cpp): HIP IPC between processes of one node; the receiver
 //    publishes each posted buffer (an offset in its exported arena) on a shared-memory ring,
 //    the sender's copy engine writes the slice there and bumps the ring's landed count. No
@@ -46,6 +49,7 @@ class P2PTransport {
   virtual ~P2PTransport() = default;
   virtual const char* name() const = 0;
   virtual bool device_buffers() const = 0;  // true: buffers are device (HBM) pointers
+  virtual int channels() const = 0;         // independent FIFO channels per direction of a pair
 
   // Token for the channel rank->peer of generation `gen` (we are its sender). Opaque bytes.
   virtual std::string make_token(int peer, uint64_t gen, std::string* err) = 0;
@@ -57,8 +61,9 @@ class P2PTransport {
   // Abort both channels with `peer`: pending ops fail or never complete; no waiting.
   virtual void close(int peer) = 0;
 
-  virtual bool post_send(int peer, const void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
-  virtual bool post_recv(int peer, void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
+  // `ch` in [0, channels()): the channel of the pair the op is matched on
+  virtual bool post_send(int peer, int ch, const void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
+  virtual bool post_recv(int peer, int ch, void* buf, uint64_t n, P2POp* op, std::string* err) = 0;
   virtual int test(P2POp* op) = 0;  // 1 done, 0 pending, -1 failed
   // test(), but a pending op may block the caller for up to `max_us` first (a futex or event
   // wait where the transport has one, so the engine's waiters sleep instead of polling).
@@ -86,18 +91,21 @@ struct RcclProbe {
 // 1-GPU hardware check of RcclTransport's building blocks (p2p_rccl.cpp).
 RcclProbe rccl_loopback_probe(int device, uint64_t bytes, uint64_t abort_bytes, int timeout_ms);
 
-// device >= 0: RCCL over xGMI on that GPU. Returns nullptr (with *err) if unavailable.
-std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, std::string* err);
+constexpr int kMaxP2PChannels = 16;
+
+// device >= 0: RCCL over xGMI on that GPU. Returns nullptr (with *err) if unavailable. Each
+// channel costs two 2-rank communicators per pair: at N=8 a process holds 14 x channels.
+std::unique_ptr<P2PTransport> make_rccl_transport(int device, int rank, int channels, std::string* err);
 // Host-memory transport over abstract UNIX sockets; `ns` keeps test clusters apart.
-std::unique_ptr<P2PTransport> make_socket_transport(int rank, const std::string& ns);
+std::unique_ptr<P2PTransport> make_socket_transport(int rank, const std::string& ns, int channels);
 // Single-GPU test transport: engines in ONE process (stores on the same GPU) exchange device
 // buffers with the RCCL matching contract, each matched pair a D2D copy (p2p_hiploop.cpp).
-std::unique_ptr<P2PTransport> make_hiploop_transport(int device, int rank, const std::string& ns);
+std::unique_ptr<P2PTransport> make_hiploop_transport(int device, int rank, const std::string& ns, int channels);
 // Same-node device transport between PROCESSES (p2p_ipc.cpp): every rank exports its HBM
 // arena over HIP IPC; a matched send is a one-sided copy into the receiver's posted extent
 // (xGMI between GPUs, an in-HBM copy when ranks share one GPU). `spin` = RCCL emulation:
 // spinning send/wait kernels on the channel streams instead of host-driven copies.
 std::unique_ptr<P2PTransport> make_ipc_transport(int device, int rank, const std::string& ns, uint8_t* arena,
-                                                 uint64_t arena_bytes, bool spin, std::string* err);
+                                                 uint64_t arena_bytes, bool spin, int channels, std::string* err);
 
 }  // namespace dfs

@@ -5,6 +5,7 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
 #include <random>
 
@@ -68,7 +69,11 @@ std::string reply(uint8_t status, uint64_t gen, const std::string& tok = {}) {
 ReplicationEngine::ReplicationEngine(ChunkStore* store, std::unique_ptr<P2PTransport> transport, int rank, int world,
                                      ReplOptions opt)
     : store_(store), t_(std::move(transport)), rank_(rank), world_(world), opt_(opt) {
-  for (int i = 0; i < world_; ++i) peers_.push_back(std::make_unique<Peer>());
+  channels_ = std::max(1, std::min(opt_.channels, t_->channels()));
+  for (int i = 0; i < world_; ++i) {
+    peers_.push_back(std::make_unique<Peer>());
+    reset_seqs_locked(*peers_.back());
+  }
   std::random_device rd;
   incarnation_ = (static_cast<uint64_t>(rd()) << 32) ^ rd() ^ static_cast<uint64_t>(::getpid());
 }
@@ -78,6 +83,22 @@ ReplicationEngine::~ReplicationEngine() { stop(); }
 void ReplicationEngine::set_control(ControlFn fn) { control_ = std::move(fn); }
 
 ReplicationEngine::Peer& ReplicationEngine::peer(int p) { return *peers_.at(static_cast<size_t>(p)); }
+
+void ReplicationEngine::reset_seqs_locked(Peer& P) {
+  P.send_seq.assign(channels_, 0);
+  P.post_next.assign(channels_, 0);
+  P.recv_next.assign(channels_, 0);
+  P.load.assign(channels_, 0);
+}
+
+void ReplicationEngine::unload(ReplTicket* t) {
+  if (!t->loaded) return;
+  Peer& P = peer(t->peer);
+  std::lock_guard<std::mutex> lk(P.mu);
+  // a rebuilt pair started its loads afresh: a ticket of an older generation counts nowhere
+  if (P.gen == t->gen && t->ch >= 0 && t->ch < static_cast<int>(P.load.size()) && P.load[t->ch] > 0) P.load[t->ch]--;
+  t->loaded = false;
+}
 
 void ReplicationEngine::spawn(std::function<void()> fn) {
   {
@@ -234,7 +255,7 @@ void ReplicationEngine::opener_loop(int p) {
       g = P.gen + 1;
       P.gen = g;
       P.state = State::Opening;
-      P.send_seq = P.post_next = P.recv_next = 0;
+      reset_seqs_locked(P);
       P.cv.notify_all();
     }
     t_->close(p);
@@ -346,7 +367,7 @@ std::string ReplicationEngine::handle_control(const std::string& req) {
     if (g <= P.gen) return reply(kStale, P.gen);
     P.gen = g;
     P.state = State::Opening;
-    P.send_seq = P.post_next = P.recv_next = 0;
+    reset_seqs_locked(P);
     P.cv.notify_all();  // receivers waiting under the old generation fail now
   }
   t_->close(from);
@@ -490,15 +511,30 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
     } else {
       up = true;
       t->gen = P.gen;
-      t->seq = P.send_seq++;
+      // the least-loaded channel (ties: round robin), so a transfer queues behind as few
+      // others as possible
+      int best = -1;
+      for (int i = 0; i < channels_; ++i) {
+        const int c = (P.rr + i) % channels_;
+        if (best < 0 || P.load[c] < P.load[best]) best = c;
+      }
+      P.rr = (best + 1) % channels_;
+      t->ch = best;
+      t->seq = P.send_seq[best]++;
+      P.load[best]++;
+      t->loaded = true;
     }
   }
   if (up) {
-    // the channels are FIFO: transfers post in sequence order (a ticket per peer)
+    // each channel is FIFO: transfers post in their channel's sequence order
     {
       std::unique_lock<std::mutex> lk(P.mu);
+      if (P.post_next[t->ch] != t->seq) {
+        std::lock_guard<std::mutex> sg(st_mu_);
+        st_.channel_waits++;
+      }
       const bool turn = P.cv.wait_until(lk, deadline, [&] {
-        return P.gen != t->gen || P.state != State::Up || P.post_next == t->seq;
+        return P.gen != t->gen || P.state != State::Up || P.post_next[t->ch] == t->seq;
       });
       if (!turn || P.gen != t->gen || P.state != State::Up) {
         *err = "pair " + std::to_string(rank_) + "->" + std::to_string(p) + " changed before the send was posted";
@@ -516,7 +552,7 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
         failed = true;
         break;
       }
-      if (!t_->post_send(p, src + off, std::min(t->slice, n - off), &op, err)) {
+      if (!t_->post_send(p, t->ch, src + off, std::min(t->slice, n - off), &op, err)) {
         failed = true;
         break;
       }
@@ -524,11 +560,12 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
     }
     {
       std::lock_guard<std::mutex> lk(P.mu);
-      if (P.gen == t->gen && P.post_next == t->seq) P.post_next++;
+      if (P.gen == t->gen && P.post_next[t->ch] == t->seq) P.post_next[t->ch]++;
       P.cv.notify_all();
     }
     if (!failed) return true;  // the pin is held until wait_send / cancel_send
   }
+  unload(t);
   for (auto& op : t->ops) t_->release(&op);
   t->ops.clear();
   if (failed) fail_pair_gen(p, t->gen, "post_send failed: " + *err);
@@ -572,6 +609,7 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
     if (!ok) break;
   }
   if (!ok) fail_pair_gen(t->peer, t->gen, *err);  // abort before unpinning: no DMA reads a freed extent
+  unload(t);
   for (auto& op : t->ops) t_->release(&op);
   t->ops.clear();
   if (t->pinned) store_->unpin(t->id);
@@ -586,18 +624,24 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
 
 void ReplicationEngine::cancel_send(ReplTicket* t, const std::string& why) {
   fail_pair_gen(t->peer, t->gen, why);
+  unload(t);
   for (auto& op : t->ops) t_->release(&op);
   t->ops.clear();
   if (t->pinned) store_->unpin(t->id);
   t->pinned = false;
 }
 
-WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const std::string& id, uint64_t size,
+WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, const std::string& id, uint64_t size,
                                     uint64_t slice, uint32_t expected_crc, bool persist_now) {
   TraceRange tr("dfs.repl.recv");
   WriteResult res;
   if (src < 0 || src >= world_ || src == rank_) {
     res.error = "bad source rank";
+    return res;
+  }
+  if (ch < 0 || ch >= channels_) {
+    res.error = "bad channel";
+    fail_pair_gen(src, gen, res.error);  // the peers disagree on the channel count
     return res;
   }
   if (size && (slice == 0 || slice % kSliceBytes != 0)) {
@@ -628,7 +672,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
     // an Opening pair of the same generation is waited for like a sequence turn
     bool turn = P.cv.wait_for(lk, std::chrono::milliseconds(opt_.turn_timeout_ms), [&] {
       return stop_.load() || P.gen != gen || P.state == State::Broken || P.state == State::Down ||
-             (P.state == State::Up && P.recv_next >= seq);
+             (P.state == State::Up && P.recv_next[ch] >= seq);
     });
     std::string why;
     bool fail = false;
@@ -639,18 +683,19 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
     } else if ((P.state != State::Up && P.state != State::Opening) || stop_.load()) {
       why = "pair down";
     } else if (!turn) {
-      why = "receive turn timeout at seq " + std::to_string(seq) + " (next " + std::to_string(P.recv_next) + ")";
+      why = "receive turn timeout at seq " + std::to_string(seq) + " of channel " + std::to_string(ch) + " (next " +
+            std::to_string(P.recv_next[ch]) + ")";
       fail = true;
       std::lock_guard<std::mutex> sg(st_mu_);
       st_.turn_timeouts++;
-    } else if (P.recv_next != seq) {
+    } else if (P.recv_next[ch] != seq) {
       why = "sequence " + std::to_string(seq) + " already consumed";
       fail = true;
     } else {
       std::string err;
       for (uint64_t off = 0; off < size; off += slice) {
         P2POp op;
-        if (!t_->post_recv(src, dst + off, std::min(slice, size - off), &op, &err)) {
+        if (!t_->post_recv(src, ch, dst + off, std::min(slice, size - off), &op, &err)) {
           why = "post_recv failed: " + err;
           fail = true;
           break;
@@ -658,7 +703,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int64_t seq, const st
         ops.push_back(op);
       }
       if (!fail) {
-        P.recv_next++;
+        P.recv_next[ch]++;
         P.cv.notify_all();
       }
     }

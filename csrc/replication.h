@@ -18,9 +18,12 @@
 //  * Slice pipelining. A block travels as slices (256 KiB..4 MiB, multiples of the 512 B
 //    checksum slice); the receiver launches the K1 checksum of slice s as soon as it lands,
 //    while slice s+1 is still on the link, then folds the slice CRCs into the block CRC.
-//  * Sequencing. Each direction of each pair is a FIFO channel: the sender stamps a block
-//    with a per-pair sequence number and the generation of the pair; the receiver posts
-//    its receives in sequence order (a late descriptor waits its turn, boundedly).
+//  * Sequencing. Each direction of each pair has K FIFO channels (round 5; K = channels,
+//    default 4): a transfer takes the least-loaded channel, the sender stamps it with the
+//    channel, a per-channel sequence number and the generation of the pair, and the receiver
+//    posts its receives in that channel's sequence order (a late descriptor waits its turn,
+//    boundedly). One transfer still waiting for its staging or for a late descriptor holds
+//    only its own channel; the pair's other transfers pass it on the others.
 //  * Bounded failure handling. Any anomaly (descriptor lost, turn timeout, transfer
 //    timeout, peer gone) marks the pair broken and aborts its channels at once — waiting
 //    receivers wake up and fail fast; the caller falls back (shared-memory staging or the
@@ -52,11 +55,14 @@ struct ReplOptions {
   int xfer_timeout_ms = 20000;   // one block transfer once posted
   uint64_t min_slice = 256 << 10;
   uint64_t max_slice = 4 << 20;
+  int channels = 4;  // FIFO channels per direction of a pair (capped by the transport's)
 };
 
 struct ReplTicket {
   int peer = -1;
   uint64_t gen = 0;
+  int ch = 0;         // the pair's channel the transfer is sequenced on
+  bool loaded = false;  // counted in the channel's in-flight load
   int64_t seq = -1;
   uint64_t size = 0;
   uint64_t slice = 0;
@@ -76,6 +82,7 @@ struct StagedSource {
 struct ReplStats {
   uint64_t bytes_sent = 0, bytes_recv = 0, blocks_sent = 0, blocks_recv = 0;
   uint64_t pair_failures = 0, pair_opens = 0, open_attempts = 0, turn_timeouts = 0, stale_generation = 0;
+  uint64_t channel_waits = 0;  // sends that found their channel's turn taken and waited for it
   uint64_t parked_extents = 0, reaped_extents = 0;  // failed-receive extents held / freed after close
 };
 
@@ -119,8 +126,9 @@ class ReplicationEngine {
   void cancel_send(ReplTicket* t, const std::string& why);
 
   // Receiver: post the receive for (src, gen, seq) in order, verify while slices land, commit.
-  WriteResult recv(int src, uint64_t gen, int64_t seq, const std::string& id, uint64_t size, uint64_t slice,
+  WriteResult recv(int src, uint64_t gen, int ch, int64_t seq, const std::string& id, uint64_t size, uint64_t slice,
                    uint32_t expected_crc, bool persist_now);
+  int channels() const { return channels_; }
 
   // Control plane (fast-path op 5). Returns the reply payload.
   std::string handle_control(const std::string& req);
@@ -141,9 +149,11 @@ class ReplicationEngine {
     std::condition_variable cv;
     State state = State::Down;
     uint64_t gen = 0;
-    int64_t send_seq = 0;
-    int64_t post_next = 0;  // the sequence number whose slices may be posted next (FIFO channels)
-    int64_t recv_next = 0;
+    // per channel: next sequence number to stamp, the one whose slices may be posted next,
+    // the one whose receives may be posted next, and transfers posted but not completed
+    std::vector<int64_t> send_seq, post_next, recv_next;
+    std::vector<int> load;
+    int rr = 0;  // round robin among equally loaded channels
     bool opener = false;  // an opener thread is running (initiator side)
     uint64_t peer_inc = 0;  // initiator side: the peer process instance the pair was opened with
     int failed_opens = 0;   // bring-up attempts of this pair that failed (both sides count)
@@ -154,6 +164,8 @@ class ReplicationEngine {
     std::vector<std::pair<uint64_t, DevExtent>> parked;  // (generation, extent)
   };
   Peer& peer(int p);
+  void reset_seqs_locked(Peer& P);
+  void unload(ReplTicket* t);
   // Park the receive extent of a failed generation-`gen` transfer. It is freed once a LATER
   // generation of the pair is up: both ranks close() their channels before every open, and
   // the open completes only when both did, so no copy of generation `gen` can land any more
@@ -169,6 +181,7 @@ class ReplicationEngine {
   std::unique_ptr<P2PTransport> t_;
   int rank_, world_;
   ReplOptions opt_;
+  int channels_ = 1;
   ControlFn control_;
   std::vector<std::unique_ptr<Peer>> peers_;
   std::atomic<bool> stop_{false};

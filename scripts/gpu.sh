@@ -1,0 +1,56 @@
+#!/bin/bash
+# One GPU-box session, parameterized: `scripts/gpu.sh <out-dir> <step> [<step> ...]`.
+# Every GPU step runs under its own `timeout -k`, and the steps are chained so the first
+# failure ends the session (no further GPU work after a fault, an abort or a time limit).
+#
+#   test      pytest -m gpu (one process) + smoke()
+#   bench     the driver's N=1 command (--steps 20 --warmup 5), twice
+#   sustain   1 MiB stress-write for 6 s after the timed steps (longer than 3x a round-4 journal)
+#   exportab  the driver's command with the exporter forced active (60 s windows at 256 MB/s),
+#             off (never) and the round-4 idle mode
+#   n2        2 ranks sharing the GPU (hipipc, RF 2)
+#   prof      rocprofv3 kernel trace of the chunkserver during a short bench
+#   configs   BASELINE configs 4 and 5
+set -o pipefail
+cd "$(dirname "$0")/.."
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out/${1:?out dir}
+shift
+mkdir -p "$O"
+run() {  # run <name> <seconds> <cmd...>: stdout -> $O/<name>.json, stderr -> $O/<name>.err
+  local name=$1 secs=$2
+  shift 2
+  echo "[gpu.sh] $name: $*" >&2
+  timeout -k 10 "$secs" "$@" > "$O/$name.json" 2> "$O/$name.err"
+  local rc=$?
+  [ $rc -eq 0 ] || { echo "[gpu.sh] $name failed rc=$rc" >&2; tail -20 "$O/$name.err" >&2; }
+  return $rc
+}
+for step in "$@"; do
+  case "$step" in
+    test)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        -p no:cacheprovider > "$O/pytest_gpu.log" 2>&1 || { tail -30 "$O/pytest_gpu.log"; exit 1; }
+      tail -3 "$O/pytest_gpu.log"
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1 ;;
+    bench)
+      run bench_a 600 python bench.py --steps 20 --warmup 5 && \
+      run bench_b 600 python bench.py --steps 20 --warmup 5 || exit 1 ;;
+    sustain)
+      run sustain 600 python bench.py --steps 5 --warmup 1 --remote-steps 0 --stress-seconds 6 \
+        --stress-size 1048576 --stress-concurrency 10 || exit 1 ;;
+    exportab)
+      DFS_EXPORT_MBPS=256 DFS_EXPORT_HEADROOM_MB=1 run export_active 600 python bench.py --steps 20 --warmup 5 && \
+      DFS_JOURNAL_EXPORT=never run export_never 600 python bench.py --steps 20 --warmup 5 && \
+      DFS_JOURNAL_EXPORT=idle run export_idle 600 python bench.py --steps 20 --warmup 5 || exit 1 ;;
+    n2)
+      run n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 || exit 1 ;;
+    prof)
+      run prof 600 python bench.py --steps 3 --warmup 1 --profile-dir "$O/prof" || exit 1 ;;
+    configs)
+      run config4 500 python bench_configs.py config4 --gpu 0 && \
+      run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
+echo "[gpu.sh] done" >&2

@@ -79,9 +79,10 @@ def test_bench_never_opens_the_gpu():
 
 
 def test_bench_sizes_the_journal_to_the_volume(monkeypatch):
-    """bench.py gives each chunkserver a journal that holds the run's blocks below the
-    materializer's mark, and falls back to the per-file path where the volume cannot hold
-    such a journal next to the materialized replicas (N=4/8 x RF 3 on a 79 GB volume)."""
+    """Store of record (default): every N keeps the journal (never the per-file fallback); each
+    chunkserver prepares the segments its replicas need, within the volume. Round-4 ring
+    (DFS_JOURNAL_EXPORT=idle): sized below the materializer's mark, per-file where the volume
+    cannot hold the ring next to the materialized replicas (N=4/8 x RF 3 on a 79 GB volume)."""
     import shutil
     import types
 
@@ -89,9 +90,16 @@ def test_bench_sizes_the_journal_to_the_volume(monkeypatch):
     import bench
 
     a = types.SimpleNamespace(steps=20, warmup=5, remote_steps=0, count=100, size=1 << 20)
-    monkeypatch.delenv("DFS_JOURNAL", raising=False)
-    monkeypatch.delenv("DFS_JOURNAL_SEGS", raising=False)
+    for k in ("DFS_JOURNAL", "DFS_JOURNAL_SEGS", "DFS_JOURNAL_SPARES", "DFS_JOURNAL_EXPORT"):
+        monkeypatch.delenv(k, raising=False)
     monkeypatch.setattr(shutil, "disk_usage", lambda p: types.SimpleNamespace(free=79 << 30))
+    got = {n: bench._journal_segments(Path("/tmp"), bench._bytes_needed(a, n), n) for n in (1, 2, 4, 8)}
+    assert all(v >= 4 for v in got.values()), got
+    for n in (1, 2, 4):
+        per_cs = bench._bytes_needed(a, n) // n
+        assert got[n] * bench.JOURNAL_SEG_DATA >= per_cs  # the run's replicas fit the prepared segments
+    assert got[8] * 8 * bench.JOURNAL_SEG_BYTES <= (79 << 30)  # within the volume (the rest on demand)
+    monkeypatch.setenv("DFS_JOURNAL_EXPORT", "idle")
     got = {n: bench._journal_segments(Path("/tmp"), bench._bytes_needed(a, n), n) for n in (1, 2, 4, 8)}
     assert got[1] >= 3 and got[2] >= 3 and got[4] == -1 and got[8] == -1, got
     for n in (1, 2):
@@ -99,3 +107,27 @@ def test_bench_sizes_the_journal_to_the_volume(monkeypatch):
         assert got[n] * bench.JOURNAL_SEG_BYTES * 0.7 >= per_cs
     monkeypatch.setenv("DFS_JOURNAL", "0")  # an explicit choice is left alone
     assert bench._journal_segments(Path("/tmp"), bench._bytes_needed(a, 8), 8) == 0
+
+
+def test_bench_gpus_without_a_launcher_runs_every_rank(tmp_path):
+    """`bench.py --gpus 4` with no WORLD_SIZE starts the 4 ranks itself (torch.distributed.run
+    as a child process) and reports n_gpus 4, never a silent 1-rank run."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(TMPDIR=str(tmp_path))
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--cpu", "--steps", "1", "--warmup", "1",
+                        "--count", "8", "--remote-steps", "0"], cwd=ROOT, env=env, capture_output=True, text=True,
+                       timeout=400)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    _check_common(d, 4, 1, 1)
+    assert d["config"]["global_batch"] == 8 * 4
+    assert len(d["volume"]["per_rank"]) == 4
+
+
+def test_bench_refuses_a_mismatched_world(tmp_path):
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", TMPDIR=str(tmp_path))
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu", "--steps", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and not p.stdout.strip()

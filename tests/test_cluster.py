@@ -614,9 +614,17 @@ def test_idle_shard_merges_and_becomes_standby():
                 break
             time.sleep(0.3)
         (survivor,) = c.shard_map.get_all_shards()
-        time.sleep(1.5)  # the victim's final Raft entry + re-registration
-        for p, d in files.items():
-            assert c.get_file_content(p) == d
+        # the victim's final Raft entry + re-registration, and the client's map refresh
+        deadline = time.time() + 15
+        while True:
+            try:
+                c.refresh_shard_map()
+                assert all(c.get_file_content(p) == d for p, d in files.items())
+                break
+            except Exception:  # noqa: BLE001
+                if time.time() > deadline:
+                    raise
+                time.sleep(0.3)
         pool = ChannelPool()
         (owner,) = c.shard_map.get_shard_peers(survivor)
         assert set(pool.call(owner, "MasterService", "ListFiles", pb.ListFilesRequest()).files) == set(files)

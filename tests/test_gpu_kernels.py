@@ -232,6 +232,27 @@ def test_gpu_journal_crash_replay_verifies_on_device(native, tmp_path):
         assert s.read(f"r{i}", 0, 0)[2] == v
 
 
+def test_gpu_scrub_runs_k1b_over_journal_resident_copies(native, tmp_path, monkeypatch):
+    """Store of record: blocks whose only durable copy is their journal record (evicted from
+    HBM) are scrubbed by the K1b kernel from staged batches; a flipped byte in one record is
+    found, and resident blocks' journal copies are checked the same way."""
+    monkeypatch.setenv("DFS_JOURNAL_EXPORT", "never")
+    s = native.ChunkStore(str(tmp_path), "", 0, 16 << 20, 0, 100, 2, 1, True, journal=1)
+    blobs = {f"k{i}": os.urandom((1 << 20) + 4099 * i) for i in range(24)}
+    for k, v in blobs.items():
+        assert s.write(k, v, zlib.crc32(v))[0]
+    assert all(s.journaled(k) for k in blobs) and not (tmp_path / "k0").exists()
+    s.drop_resident()
+    assert s.scrub() == []
+    st = s.stats()
+    assert st["scrub_device_blocks"] >= len(blobs) and st["journal_live_records"] == len(blobs)
+    assert s.debug_corrupt("k7", 5000)
+    assert s.scrub() == ["k7"]
+    for k, v in blobs.items():
+        if k != "k7":
+            assert s.read(k, 0, 0)[2] == v
+
+
 def test_gpu_corruption_detected_full_and_partial(gstore):
     d = os.urandom(300000)
     assert gstore.write("corrupt", d, 0)[0]

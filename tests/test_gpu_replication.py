@@ -130,7 +130,7 @@ def test_device_crossing_traffic_and_corruption_refused(native, gcluster):
     assert st == fp.OK
     tk, err = a.eng.send(b.rank, "good", None)
     assert tk is not None, err
-    ok, _crc, err = b.eng.recv(a.rank, tk.gen, tk.seq, "bad-copy", tk.size, tk.slice, zlib.crc32(data) ^ 1, True)
+    ok, _crc, err = b.eng.recv(a.rank, tk.gen, tk.seq, "bad-copy", tk.size, tk.slice, zlib.crc32(data) ^ 1, True, tk.ch)
     assert not ok and "mismatch" in err
     assert a.eng.wait_send(tk)[0]
     arena.close()

@@ -1,6 +1,11 @@
 """Block journal of the chunk store (csrc/journal.{h,cpp}): group-committed durable writes,
-background materialization into the reference's `<id>` + `<id>.meta` files
-(chunkserver.rs:192-209), crash replay with checksum verification, tombstones, segment reuse.
+crash replay with checksum verification, tombstones, segment reuse.
+
+Two modes. The default since round 5 is the store of record (tests/test_journal_store.py):
+records stay the blocks' durable home and the reference's `<id>` + `<id>.meta` files
+(chunkserver.rs:192-209) are exported at a bounded rate. The tests here pin the round-4
+mode (`DFS_JOURNAL_EXPORT=idle`: everything materialized once the writers pause, replay
+writes the files out and retires the journal), kept as the A/B.
 Host-mode store (CPU); the GPU tier runs the same protocol from HBM (test_gpu_kernels.py)."""
 import os
 import struct
@@ -15,6 +20,11 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 
 
+@pytest.fixture(autouse=True)
+def _idle_mode(monkeypatch):
+    monkeypatch.setenv("DFS_JOURNAL_EXPORT", "idle")
+
+
 def meta_of(d: bytes) -> bytes:
     return b"".join(struct.pack(">I", zlib.crc32(d[i:i + 512])) for i in range(0, len(d), 512))
 
@@ -25,7 +35,7 @@ def blob(i: int) -> bytes:
 
 def run_child(code: str, env: dict | None = None) -> subprocess.CompletedProcess:
     """Runs `code` in a fresh interpreter that ends with os._exit (no destructors: a crash)."""
-    e = dict(os.environ, PYTHONPATH=str(ROOT))
+    e = dict(os.environ, PYTHONPATH=str(ROOT), DFS_JOURNAL_EXPORT="idle")
     e.update(env or {})
     return subprocess.run([sys.executable, "-c", textwrap.dedent(code)], env=e, capture_output=True, text=True,
                           timeout=120)
@@ -83,6 +93,7 @@ def test_crash_replay_restores_acked_writes_and_deletes(native, tmp_path):
     s = open_store(native, tmp_path)
     st = s.stats()
     assert st["journal_replayed"] == 19 and st["journal_replay_skipped"] == 0
+    assert st["journal_mode"] == "idle"
     assert st["journal_segs_free"] >= 1 and st["journal_records"] == 0
     assert not s.exists("c4") and not (tmp_path / "hot" / "c4").exists()
     assert s.read("c5", 0, 0)[2] == b"second version" * 300
