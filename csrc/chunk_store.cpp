@@ -3247,7 +3247,9 @@ std::vector<std::string> ChunkStore::scrub_durable_gpu(const std::vector<std::st
     return bad;
   }
   HIP_OK(hipSetDevice(cfg_.device));
-  constexpr uint64_t kBatchBytes = 64ull << 20;
+  // a batch is a staging extent of the arena (it may evict clean resident blocks): at most
+  // an eighth of it, at most 64 MiB
+  const uint64_t kBatchBytes = std::max<uint64_t>(1ull << 20, std::min<uint64_t>(64ull << 20, arena_bytes() / 8));
   size_t i = 0;
   std::vector<uint8_t> data;
   while (i < ids.size()) {
@@ -3279,6 +3281,10 @@ std::vector<std::string> ChunkStore::scrub_durable_gpu(const std::vector<std::st
         if (jrec.seg) jrec.seg->readers--;
         rest->push_back(id);
         continue;
+      }
+      if (!items.empty() && total + need > kBatchBytes) {  // the next batch takes it
+        if (jrec.seg) jrec.seg->readers--;
+        break;
       }
       DurableSrc src;
       if (!open_durable(id, cold, jrec, jmeta, &src) || src.meta.size() != num_slices(size)) {
