@@ -292,7 +292,7 @@ def main():
         ndev = 0 if a.cpu else visible_gpus()
         gpu = -1 if a.cpu else local_rank % max(1, ndev)
         shared_gpu = (not a.cpu) and ndev < n  # rehearsal mode: several ranks on one GPU
-        args = [f"{PKG}.chunkserver.server", "--addr", f"127.0.0.1:{cport}",
+        args = ["--addr", f"127.0.0.1:{cport}",
                 "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
                 "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
                 "--heartbeat-interval", "0.5", "--scrub-interval", "3600", "--rccl-timeout-ms", "90000"]
@@ -307,6 +307,10 @@ def main():
         else:
             args += ["--replication-transport", "grpc"]
         cs_env = dict(env, DFS_READY_FILE=ready, SHARD_CONFIG=str(shard_file))
+        from rust_hadoop_generated_by_llm_amd.cluster.launcher import role_command
+
+        # the C++ dfs_chunkserver executable (the Python shell with DFS_NATIVE_CHUNKSERVER=0)
+        cs_cmd = role_command("chunkserver.server", args, cs_env)
         if a.profile_dir:
             # profile only the ChunkServer (where the kernels run); rocprofv3 is started
             # before anything in this process touches the GPU
@@ -314,11 +318,10 @@ def main():
             os.makedirs(pdir, exist_ok=True)
             cs_env["TMPDIR"] = "/tmp"
             cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "--output-format", "csv",
-                                  "-d", pdir,
-                                  "-o", "cs", "--", sys.executable, "-m", *args],
+                                  "-d", pdir, "-o", "cs", "--", *cs_cmd],
                                  str(base_p / f"cs{rank}.log"), cs_env)
         else:
-            cp = procs.spawn(args, str(base_p / f"cs{rank}.log"), cs_env)
+            cp = procs.spawn_raw(cs_cmd, str(base_p / f"cs{rank}.log"), cs_env)
         cs_info = wait_file(ready, cp, 900, procs)
         my_cs = f"127.0.0.1:{cport}"
         t_start = time.time()

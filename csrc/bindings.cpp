@@ -18,6 +18,7 @@
 #include "replication.h"
 #include "cs_agent.h"
 #include "cs_grpc.h"
+#include "cs_stats.h"
 #include "grpc_server.h"
 #include "http_lite.h"
 #include "sigv4.h"
@@ -81,6 +82,28 @@ int device_count() {
 }  // namespace
 
 void bind_meta(py::module_& m);  // bindings_meta.cpp
+
+// JSON (cs_stats.h) -> Python objects
+py::object json_to_py(const Json& j) {
+  switch (j.type()) {
+    case Json::Type::Null: return py::none();
+    case Json::Type::Bool: return py::bool_(j.as_bool());
+    case Json::Type::Int: return py::int_(j.as_int());
+    case Json::Type::Double: return py::float_(j.as_double());
+    case Json::Type::String: return py::str(j.as_string());
+    case Json::Type::Array: {
+      py::list l;
+      for (const auto& v : j.items()) l.append(json_to_py(v));
+      return l;
+    }
+    case Json::Type::Object: {
+      py::dict d;
+      for (const auto& kv : j.fields()) d[py::str(kv.first)] = json_to_py(kv.second);
+      return d;
+    }
+  }
+  return py::none();
+}
 
 PYBIND11_MODULE(_dfs_native, m) {
   m.doc() = "MI355X-native data plane: HBM chunk store, CDNA4 CRC/RS kernels, RCCL replication, WAL";
@@ -361,75 +384,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("journaled", &ChunkStore::journaled)
       .def("compact", &ChunkStore::compact, py::call_guard<py::gil_scoped_release>(), py::arg("max_live") = 1.0,
            "relocate the live records of the oldest journal segment(s) holding at most max_live of their capacity")
-      .def("stats", [](ChunkStore& s) {
-        StoreStats t = s.stats();
-        py::dict d;
-        d["blocks"] = t.blocks;
-        d["bytes"] = t.bytes;
-        d["hbm_capacity"] = t.hbm_capacity;
-        d["hbm_used"] = t.hbm_used;
-        d["hbm_resident_blocks"] = t.hbm_resident_blocks;
-        d["dirty_blocks"] = t.dirty_blocks;
-        d["spill_queue"] = t.spill_queue;
-        d["evictions"] = t.evictions;
-        d["promotions"] = t.promotions;
-        d["mirror_hits"] = t.mirror_hits;
-        d["mirror_bytes"] = t.mirror_bytes;
-        d["io_threads_spawned"] = t.io_threads_spawned;
-        d["final_name_writes"] = t.final_name_writes;
-        d["direct_writes"] = t.direct_writes;
-        d["crc_mismatches"] = t.crc_mismatches;
-        d["gpu_kernel_launches"] = t.gpu_kernel_launches;
-        d["disk_gate_waits"] = t.disk_gate_waits;
-        d["direct_dma"] = t.direct_dma;
-        d["fused_reads"] = t.fused_reads;
-        d["fused_writes"] = t.fused_writes;
-        d["sliced_stages"] = t.sliced_stages;
-        d["staged_dma"] = t.staged_dma;
-        d["host_registered_bytes"] = t.host_registered_bytes;
-        d["journal"] = t.journal;
-        d["journal_records"] = t.journal_records;
-        d["journal_bytes"] = t.journal_bytes;
-        d["journal_commits"] = t.journal_commits;
-        d["journal_sync_rounds"] = t.journal_sync_rounds;
-        d["journal_mode"] = t.journal_mode;
-        d["journal_tombstones"] = t.journal_tombstones;
-        d["journal_supersedes"] = t.journal_supersedes;
-        d["journal_segs_in_use"] = t.journal_segs_in_use;
-        d["journal_segs_marked"] = t.journal_segs_marked;
-        d["journal_replay_verified"] = t.journal_replay_verified;
-        d["journal_live_records"] = t.journal_live_records;
-        d["journal_live_bytes"] = t.journal_live_bytes;
-        d["journal_used_bytes"] = t.journal_used_bytes;
-        d["journal_grow_blocked"] = t.journal_grow_blocked;
-        d["relocated_blocks"] = t.relocated_blocks;
-        d["relocated_bytes"] = t.relocated_bytes;
-        d["compactions"] = t.compactions;
-        d["export_deferred_headroom"] = t.export_deferred_headroom;
-        d["scrub_device_blocks"] = t.scrub_device_blocks;
-        d["journal_full_waits"] = t.journal_full_waits;
-        d["journal_segs"] = t.journal_segs;
-        d["journal_segs_free"] = t.journal_segs_free;
-        d["journal_segs_retired"] = t.journal_segs_retired;
-        d["journal_replayed"] = t.journal_replayed;
-        d["journal_replay_skipped"] = t.journal_replay_skipped;
-        d["journal_failed"] = t.journal_failed;
-        d["materialized_blocks"] = t.materialized_blocks;
-        d["materialized_bytes"] = t.materialized_bytes;
-        d["materialize_pending"] = t.materialize_pending;
-        d["materialize_batches"] = t.materialize_batches;
-        d["materialize_errors"] = t.materialize_errors;
-        d["materialize_last_error"] = t.materialize_last_error;
-        d["journal_prepare_errors"] = t.journal_prepare_errors;
-        d["journal_segs_filled"] = t.journal_segs_filled;
-        d["journal_fill_bytes"] = t.journal_fill_bytes;
-        d["journal_parts_unready"] = t.journal_parts_unready;
-        d["journal_sync_ns"] = t.journal_sync_ns;
-        d["journal_bypassed"] = t.journal_bypassed;
-        d["journal_commit_ns"] = t.journal_commit_ns;
-        d["journal_last_error"] = t.journal_last_error;
-        return d;
-      })
+      .def("stats", [](ChunkStore& s) { return json_to_py(stats_json(s.stats())); })
       .def("gpu_crc", [](ChunkStore& s, py::buffer data) {
         py::buffer_info k;
         Buf v = view(data, k);
@@ -511,31 +466,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("report_bad_block", &CsAgent::report_bad_block)
       .def("masters", &CsAgent::masters)
       .def_property_readonly("known_term", &CsAgent::known_term)
-      .def("stats", [](CsAgent& a) {
-        CsAgentStats s = a.stats();
-        py::dict d;
-        d["agent_heartbeats"] = s.heartbeats;
-        d["agent_heartbeat_failures"] = s.heartbeat_failures;
-        d["agent_commands"] = s.commands;
-        d["agent_map_refreshes"] = s.map_refreshes;
-        d["agent_replicate_engine"] = s.replicate_engine;
-        d["agent_replicate_grpc"] = s.replicate_grpc;
-        d["agent_replicate_failed"] = s.replicate_failed;
-        d["agent_reconstructs"] = s.reconstructs;
-        d["agent_reconstruct_device"] = s.reconstruct_device;
-        d["agent_reconstruct_failed"] = s.reconstruct_failed;
-        d["agent_encodes"] = s.encodes;
-        d["agent_encode_failed"] = s.encode_failed;
-        d["agent_recoveries"] = s.recoveries;
-        d["agent_recovery_failed"] = s.recovery_failed;
-        d["agent_deletes"] = s.deletes;
-        d["agent_moves"] = s.moves;
-        d["agent_scrubs"] = s.scrubs;
-        d["agent_scrub_bad"] = s.scrub_bad;
-        d["agent_ec_gpu"] = s.ec_gpu;
-        d["agent_ec_cpu"] = s.ec_cpu;
-        return d;
-      });
+      .def("stats", [](CsAgent& a) { return json_to_py(stats_json(a.stats())); });
 
   // ---------------- RCCL replication
   py::class_<FastPathServer>(m, "FastPathServer")
@@ -568,33 +499,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("set_peer", &FastPathServer::set_peer, py::arg("addr"), py::arg("rank"), py::arg("name") = "")
       .def("set_self_host", &FastPathServer::set_self_host, py::arg("host"))
       .def("set_self_addr", &FastPathServer::set_self_addr, py::arg("addr"))
-      .def("stats", [](FastPathServer& f) {
-        FpStats s = f.stats();
-        py::dict d;
-        d["fp_writes"] = s.writes;
-        d["fp_reads"] = s.reads;
-        d["fp_fenced"] = s.fenced;
-        d["fp_punts"] = s.punts;
-        d["fp_connections"] = s.connections;
-        d["fp_replicas_in"] = s.replicas_in;
-        d["fp_rccl_forwards"] = s.rccl_forwards;
-        d["fp_shm_forwards"] = s.shm_forwards;
-        d["fp_forward_failures"] = s.forward_failures;
-        d["fp_replica_failures"] = s.replica_failures;
-        d["fp_p2p_fallbacks"] = s.p2p_fallbacks;
-        d["fp_rejected_peers"] = s.rejected_peers;
-        d["fp_ec_ops"] = s.ec_ops;
-        d["fp_heals_out"] = s.heals_out;
-        d["fp_heals_in"] = s.heals_in;
-        d["fp_sliced_writes"] = s.sliced_writes;
-        d["fp_ec_device_writes"] = s.ec_device_writes;
-        d["fp_ec_shard_forwards"] = s.ec_shard_forwards;
-        d["fp_ec_device_reads"] = s.ec_device_reads;
-        d["fp_ec_device_decodes"] = s.ec_device_decodes;
-        d["fp_ec_gathered"] = s.ec_gathered;
-        d["fp_ec_device_fallbacks"] = s.ec_device_fallbacks;
-        return d;
-      })
+      .def("stats", [](FastPathServer& f) { return json_to_py(stats_json(f.stats())); })
       .def("replicate_block", [](FastPathServer& f, const std::string& id, const std::vector<std::string>& targets,
                                  uint64_t term) {
         std::vector<std::string> done;
@@ -642,24 +547,7 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def(py::init([](ChunkStore* store, const std::string& transport, int rank, int world, const std::string& ns,
                        int open_timeout_ms, int turn_timeout_ms, int xfer_timeout_ms, int channels) {
              std::string err;
-             std::unique_ptr<P2PTransport> t;
-             if (channels <= 0) {
-               // DFS_REPL_CHANNELS (default 4); RCCL: DFS_REPL_CHANNELS_RCCL (default 1: every
-               // channel costs two communicators per pair)
-               const char* e = std::getenv(transport == "rccl" ? "DFS_REPL_CHANNELS_RCCL" : "DFS_REPL_CHANNELS");
-               channels = e && *e ? std::atoi(e) : (transport == "rccl" ? 1 : 4);
-             }
-             if (transport == "rccl") t = make_rccl_transport(store->config().device, rank, channels, &err);
-             else if (transport == "socket") t = make_socket_transport(rank, ns, channels);
-             else if (transport == "hiploop" && store->gpu())
-               t = make_hiploop_transport(store->config().device, rank, ns, channels);
-             else if (transport == "hipipc" || transport == "hipipc-spin") {
-               const char* sp = std::getenv("DFS_IPC_SPIN");
-               bool spin = transport == "hipipc-spin" || (sp && std::string(sp) == "1");
-               t = make_ipc_transport(store->config().device, rank, ns, store->arena_base(), store->arena_bytes(), spin,
-                                      channels, &err);
-             }
-             else err = "unknown transport " + transport;
+             std::unique_ptr<P2PTransport> t = make_transport(transport, store, rank, ns, channels, &err);
              if (!t) throw std::runtime_error(err);
              ReplOptions o;
              o.open_timeout_ms = open_timeout_ms;
@@ -733,22 +621,9 @@ PYBIND11_MODULE(_dfs_native, m) {
       .def("debug_drop_sends", [](ReplicationEngine& e, int peer, int n) { e.transport()->debug_drop_sends(peer, n); })
       .def("debug_stall", [](ReplicationEngine& e, int peer, int ms) { e.transport()->debug_stall(peer, ms); })
       .def("stats", [](ReplicationEngine& e) {
-        ReplStats s = e.stats();
-        py::dict d;
-        d["bytes_sent"] = s.bytes_sent;
-        d["bytes_recv"] = s.bytes_recv;
-        d["blocks_sent"] = s.blocks_sent;
-        d["blocks_recv"] = s.blocks_recv;
-        d["pair_failures"] = s.pair_failures;
-        d["pair_opens"] = s.pair_opens;
-        d["open_attempts"] = s.open_attempts;
-        d["turn_timeouts"] = s.turn_timeouts;
-        d["stale_generation"] = s.stale_generation;
-        d["channel_waits"] = s.channel_waits;
-        d["channels"] = e.channels();
-        d["parked_extents"] = s.parked_extents;
-        d["reaped_extents"] = s.reaped_extents;
-        return d;
+        Json d = stats_json(e.stats());
+        d.set("channels", e.channels());
+        return json_to_py(d);
       })
       .def_property_readonly("bytes_sent", [](ReplicationEngine& e) { return e.stats().bytes_sent; })
       .def_property_readonly("bytes_recv", [](ReplicationEngine& e) { return e.stats().bytes_recv; });
@@ -805,16 +680,7 @@ PYBIND11_MODULE(_dfs_native, m) {
         n.srv->stop();
       })
       .def_property_readonly("port", [](NativeGrpc& n) { return n.srv->port(); })
-      .def("stats", [](NativeGrpc& n) {
-        CsGrpcStats s = n.svc->stats();
-        py::dict d;
-        d["native_grpc_calls"] = n.srv->calls();
-        d["native_grpc_writes"] = s.native_writes;
-        d["native_grpc_reads"] = s.native_reads;
-        d["native_grpc_replicates"] = s.native_replicates;
-        d["native_grpc_fallbacks"] = s.fallbacks;
-        return d;
-      });
+      .def("stats", [](NativeGrpc& n) { return json_to_py(stats_json(n.svc->stats(), n.srv->calls())); });
 
   // ---------------- WAL
   py::class_<Wal>(m, "Wal")

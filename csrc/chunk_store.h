@@ -100,7 +100,7 @@ struct StoreStats {
   // block journal (journal.h): group-committed durable writes; the store of record, with a
   // rate-limited exporter of reference-format files and compaction (or the round-4 mode)
   bool journal = false;
-  std::string journal_mode;  // "store" (export with headroom), "store-noexport", "idle" (round 4)
+  std::string journal_mode = "none";  // "none" without fsync; "store" (export with headroom), "store-noexport", "idle" (round 4)
   uint64_t journal_records = 0, journal_bytes = 0, journal_commits = 0, journal_sync_rounds = 0;
   uint64_t journal_tombstones = 0, journal_supersedes = 0, journal_full_waits = 0, journal_segs = 0,
            journal_segs_free = 0, journal_segs_in_use = 0, journal_segs_marked = 0;

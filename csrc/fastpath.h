@@ -128,6 +128,17 @@ class FastPathServer {
   bool persist_and_replicate(const std::string& id, const uint8_t* host, uint64_t n, uint32_t crc, uint64_t term,
                              const std::vector<std::string>& next, int* downstream, std::string* err);
   void add_suspect(const std::string& id);
+  // For the native gRPC chain (dfs_chunkserver): a client's shared-memory slot
+  // [off, off+len) (nullptr + *err when it is not mappable here), the replication engine,
+  // and one replica pushed to a same-node `addr` over it (replicas written, 0 = failed).
+  uint8_t* map_client_shm(const std::string& path, uint64_t off, uint64_t len, std::string* err) {
+    return map_shm(path, off, len, err);
+  }
+  ReplicationEngine* replication() const { return repl_; }
+  int replicate_to(const std::string& addr, const std::string& id, uint32_t crc, uint64_t term, const uint8_t* host,
+                   uint64_t n, bool heal) {
+    return replicate_one(addr, id, crc, term, ShmSrc{}, host, n, heal);
+  }
   // Heal / balancer / shuffle copy (master REPLICATE command; reference chunkserver.rs:462-499)
   // of a block held here to same-node `targets`, payload over the replication engine (HBM ->
   // HBM on device transports), descriptor on the peers' fast-path sockets. Returns the

@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 
@@ -65,6 +66,25 @@ std::string reply(uint8_t status, uint64_t gen, const std::string& tok = {}) {
 }
 
 }  // namespace
+
+std::unique_ptr<P2PTransport> make_transport(const std::string& name, ChunkStore* store, int rank,
+                                             const std::string& ns, int channels, std::string* err) {
+  if (channels <= 0) {
+    const char* e = std::getenv(name == "rccl" ? "DFS_REPL_CHANNELS_RCCL" : "DFS_REPL_CHANNELS");
+    channels = e && *e ? std::atoi(e) : (name == "rccl" ? 1 : 4);
+  }
+  if (name == "rccl") return make_rccl_transport(store->config().device, rank, channels, err);
+  if (name == "socket") return make_socket_transport(rank, ns, channels);
+  if (name == "hiploop" && store->gpu()) return make_hiploop_transport(store->config().device, rank, ns, channels);
+  if (name == "hipipc" || name == "hipipc-spin") {
+    const char* sp = std::getenv("DFS_IPC_SPIN");
+    const bool spin = name == "hipipc-spin" || (sp && std::string(sp) == "1");
+    return make_ipc_transport(store->config().device, rank, ns, store->arena_base(), store->arena_bytes(), spin,
+                              channels, err);
+  }
+  *err = "unknown transport " + name;
+  return nullptr;
+}
 
 ReplicationEngine::ReplicationEngine(ChunkStore* store, std::unique_ptr<P2PTransport> transport, int rank, int world,
                                      ReplOptions opt)

@@ -79,6 +79,13 @@ struct StagedSource {
   const std::vector<hipEvent_t>* done = nullptr;
 };
 
+// The transport a chunkserver names on its command line: "hipipc" / "hipipc-spin" (HIP IPC
+// one-sided copies), "rccl", "socket" (host memory, CPU tests), "hiploop" (one process, tests).
+// channels <= 0: DFS_REPL_CHANNELS (default 4), or for RCCL DFS_REPL_CHANNELS_RCCL (default 1:
+// each channel costs two communicators per pair). nullptr + *err when unavailable.
+std::unique_ptr<P2PTransport> make_transport(const std::string& name, ChunkStore* store, int rank,
+                                             const std::string& ns, int channels, std::string* err);
+
 struct ReplStats {
   uint64_t bytes_sent = 0, bytes_recv = 0, blocks_sent = 0, blocks_recv = 0;
   uint64_t pair_failures = 0, pair_opens = 0, open_attempts = 0, turn_timeouts = 0, stale_generation = 0;

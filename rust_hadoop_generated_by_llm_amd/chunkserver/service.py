@@ -110,7 +110,7 @@ class ChunkServer:
                 req = pb.ReplicateBlockRequest(block_id=block_id, next_servers=rest, expected_checksum_crc32c=crc,
                                                master_term=term, rccl=True, rccl_src_rank=self.my_rank,
                                                rccl_seq=tk.seq, rccl_size=tk.size, rccl_gen=tk.gen,
-                                               rccl_slice=tk.slice, heal=heal)
+                                               rccl_slice=tk.slice, rccl_channel=tk.ch, heal=heal)
                 resp = None
                 try:
                     resp = self.pool.call(nxt, "ChunkServerService", "ReplicateBlock", req, timeout=120.0)
@@ -154,7 +154,7 @@ class ChunkServer:
     # ------------------------------------------------------------------ RPCs
     def _store_and_forward(self, block_id: str, data: bytes | None, next_servers: list[str], crc: int, term: int,
                            heal: bool, rccl_src: int = -1, rccl_seq: int = -1, rccl_size: int = 0,
-                           rccl_gen: int = 0, rccl_slice: int = 0):
+                           rccl_gen: int = 0, rccl_slice: int = 0, rccl_channel: int = 0):
         """Local write + downstream forwarding, pipelined.
 
         The reference writes+fsyncs locally and only then forwards (serial chain,
@@ -166,7 +166,7 @@ class ChunkServer:
         Returns (ok, error, replicas_written)."""
         if rccl_src >= 0:
             ok, _crc, err = self.rccl.recv(rccl_src, rccl_gen, rccl_seq, block_id, rccl_size, rccl_slice, crc,
-                                           persist=not next_servers)
+                                           persist=not next_servers, ch=rccl_channel)
             staged_in_hbm = True
         elif next_servers and self.store.gpu:
             ok, _crc, err = self.store.stage(block_id, data, crc)
@@ -217,7 +217,7 @@ class ChunkServer:
             ok, err, replicas = self._store_and_forward(req.block_id, None, list(req.next_servers),
                                                         req.expected_checksum_crc32c, req.master_term, req.heal,
                                                         req.rccl_src_rank, req.rccl_seq, req.rccl_size,
-                                                        req.rccl_gen, req.rccl_slice)
+                                                        req.rccl_gen, req.rccl_slice, req.rccl_channel)
         else:
             ok, err, replicas = self._store_and_forward(req.block_id, req.data, list(req.next_servers),
                                                         req.expected_checksum_crc32c, req.master_term, req.heal)

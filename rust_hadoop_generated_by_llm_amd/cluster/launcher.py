@@ -27,11 +27,20 @@ ROOT = Path(__file__).resolve().parents[2]
 
 _handed_out: set[int] = set()
 
-# Control-plane roles with a native executable (csrc/tools/dfs_master.cpp,
-# dfs_config_server.cpp): with DFS_NATIVE_CONTROL unset or 1 they run as those binaries, so
-# no Python interpreter lives in a master or config-server process; DFS_NATIVE_CONTROL=0
-# keeps the Python shells (the A/B launcher).
-NATIVE_BINARIES = {"master.server": "dfs_master", "config_server.server": "dfs_config_server"}
+# Roles with a native executable (csrc/tools/dfs_master.cpp, dfs_config_server.cpp,
+# dfs_chunkserver.cpp): with DFS_NATIVE_CONTROL unset or 1 they run as those binaries, so no
+# Python interpreter lives in a master, config-server or chunkserver process;
+# DFS_NATIVE_CONTROL=0 (or DFS_NATIVE_CHUNKSERVER=0 for the chunkservers alone) keeps the
+# Python shells (the A/B launcher).
+NATIVE_BINARIES = {"master.server": "dfs_master", "config_server.server": "dfs_config_server",
+                   "chunkserver.server": "dfs_chunkserver"}
+
+
+def _python_chunkserver(args: list[str], env) -> bool:
+    """The chunkserver configurations only the Python shell serves (its A/B knobs)."""
+    return (env.get("DFS_NATIVE_CHUNKSERVER", "1") == "0" or env.get("DFS_CS_GRPC", "native") != "native"
+            or env.get("DFS_CS_AGENT", "native") != "native" or "--no-fastpath" in args
+            or any(a.startswith("--grpc-impl") and (a.endswith("grpcio") or a == "--grpc-impl") for a in args))
 
 
 def role_command(module: str, args: list[str], environ: dict | None = None) -> list[str]:
@@ -39,6 +48,8 @@ def role_command(module: str, args: list[str], environ: dict | None = None) -> l
     ``python -m <package>.<module>``."""
     env = os.environ if environ is None else environ
     exe = ROOT / "build" / "native" / NATIVE_BINARIES.get(module, "-")
+    if module == "chunkserver.server" and _python_chunkserver(args, env):
+        return [sys.executable, "-m", f"{PKG}.{module}", *args]
     if module in NATIVE_BINARIES and env.get("DFS_NATIVE_CONTROL", "1") != "0" and exe.exists():
         return [str(exe), *args]
     return [sys.executable, "-m", f"{PKG}.{module}", *args]

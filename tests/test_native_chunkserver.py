@@ -1,0 +1,88 @@
+"""The native `dfs_chunkserver` executable (csrc/tools/dfs_chunkserver.cpp; reference
+dfs/chunkserver/src/bin/chunkserver.rs:74-375): no Python interpreter in a chunkserver
+process, and the reference's gRPC data path served natively — the store-and-forward chain
+WriteBlock -> ReplicateBlock{next_servers[1..]} for hops without a P2P pair
+(chunkserver.rs:777-829,1039-1077), and a corrupt full read recovered from another replica
+before it is answered (chunkserver.rs:913-949). The native gRPC service must not hand a single
+call to a fallback (there is none in this process)."""
+import json
+import os
+import urllib.request
+
+import psutil
+
+from rust_hadoop_generated_by_llm_amd.client.client import Client
+from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster
+from rust_hadoop_generated_by_llm_amd.models import proto as pb
+from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
+
+
+def cs_stats(cl, i):
+    return json.loads(urllib.request.urlopen(cl.cs_http[i] + "/stats", timeout=10).read())
+
+
+def test_chunkservers_run_as_native_executables():
+    with LocalCluster(n_chunkservers=2, fsync=False) as cl:
+        for p in cl.procs:
+            if p.name.startswith("cs"):
+                proc = psutil.Process(p.popen.pid)
+                assert os.path.basename(proc.cmdline()[0]) == "dfs_chunkserver", p.name
+                assert not any("python" in m.path for m in proc.memory_maps()), p.name
+        c = cl.client()
+        c.create_file_from_buffer(b"native chunkserver" * 100, "/ncs/a")
+        assert c.get_file_content("/ncs/a") == b"native chunkserver" * 100
+        c.close()
+        for i in range(2):
+            st = cs_stats(cl, i)
+            assert st["native_chunkserver"] is True and st["native_grpc_fallbacks"] == 0
+            assert st["journal_mode"] == "none"  # fsync=False: no journal
+        assert urllib.request.urlopen(cl.cs_http[0] + "/health", timeout=5).read() == b"OK"
+        assert b"dfs_chunkserver_total_chunks" in urllib.request.urlopen(cl.cs_http[0] + "/metrics", timeout=5).read()
+
+
+def test_remote_rf3_chain_over_grpc_is_native():
+    """RF 3 with --replication-transport grpc and a remote client (every byte over gRPC/TCP):
+    the head writes and forwards ReplicateBlock with the rest of the chain, the middle
+    forwards again, the tail writes; replicas_written counts all three; no fallbacks."""
+    with LocalCluster(n_chunkservers=3, fsync=True, env={"DFS_JOURNAL_EXPORT": "never"}) as cl:
+        c = Client(cl.master_addrs, local_chunkserver=None, local_rpc=False)
+        files = {f"/chain/f{i}": os.urandom(200_000 + 37 * i) for i in range(12)}
+        for p, d in files.items():
+            c.create_file_from_buffer(d, p)
+        for p, d in files.items():
+            assert c.get_file_content(p) == d
+        pool = ChannelPool()
+        for p, d in files.items():
+            info = c.get_file_info(p)
+            blk = info.blocks[0]
+            assert len(blk.locations) == 3
+            for loc in blk.locations:  # every replica holds the verified bytes
+                r = pool.call(loc, "ChunkServerService", "ReadBlock", pb.ReadBlockRequest(block_id=blk.block_id))
+                assert r.data == d
+        pool.close()
+        c.close()
+        st = [cs_stats(cl, i) for i in range(3)]
+        assert sum(s["native_grpc_fallbacks"] for s in st) == 0
+        # each write: head -> middle and middle -> tail over gRPC
+        assert sum(s["native_grpc_forwards"] for s in st) >= 2 * len(files)
+        assert sum(s["native_grpc_replicates"] for s in st) >= 2 * len(files)
+
+
+def test_corrupt_full_read_is_recovered_natively():
+    with LocalCluster(n_chunkservers=2, fsync=False, env={"DFS_DEBUG_ENDPOINTS": "1"}) as cl:
+        c = Client(cl.master_addrs, local_chunkserver=None, local_rpc=False)
+        data = os.urandom(300_000)
+        c.create_file_from_buffer(data, "/rec/x")
+        blk = c.get_file_info("/rec/x").blocks[0]
+        assert len(blk.locations) == 2
+        victim = blk.locations[0]
+        vi = cl.cs_addrs.index(victim.replace("http://", ""))
+        urllib.request.urlopen(f"{cl.cs_http[vi]}/debug/corrupt?block={blk.block_id}&offset=70000", timeout=10).read()
+        pool = ChannelPool()
+        r = pool.call(victim, "ChunkServerService", "ReadBlock", pb.ReadBlockRequest(block_id=blk.block_id),
+                      timeout=60)
+        assert r.data == data  # recovered from the other replica before it was served
+        pool.close()
+        c.close()
+        st = cs_stats(cl, vi)
+        assert st["native_grpc_recoveries"] >= 1 and st["native_grpc_fallbacks"] == 0
