@@ -936,6 +936,16 @@ void bind_meta(py::module_& m) {
         d["lists"] = s.lists;
         d["mpu_completes"] = s.mpu_completes;
         d["mpu_initiates"] = s.mpu_initiates;
+        d["deletes"] = s.deletes;
+        d["multi_deletes"] = s.multi_deletes;
+        d["deleted_keys"] = s.deleted_keys;
+        d["mpu_aborts"] = s.mpu_aborts;
+        d["copies"] = s.copies;
+        d["copy_bytes"] = s.copy_bytes;
+        d["chunked_puts"] = s.chunked_puts;
+        d["chunk_sigs"] = s.chunk_sigs;
+        d["chunk_sig_failures"] = s.chunk_sig_failures;
+        d["presigned"] = s.presigned;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;
         return d;

@@ -363,12 +363,228 @@ struct S3Front::Req {
   std::string rid;
   std::string action;  // s3:<Action> once resolved for authorization (audit records)
   int status = 0;
+  std::map<std::string, std::string> presign;  // X-Amz-* query authentication (presigned URL)
+  sigv4::ChunkChain chain;                      // set by a verified signature: aws-chunked bodies
+  bool chain_set = false;
   const std::string* get(const char* lname) const {
     for (auto& h : headers)
       if (h.first == lname) return &h.second;
     return nullptr;
   }
 };
+
+namespace {
+
+// an aws-chunked body (x-amz-content-sha256: STREAMING-..., or Content-Encoding: aws-chunked)
+bool aws_chunked(const S3Front::Req& r) {
+  const std::string* sha = r.get("x-amz-content-sha256");
+  const std::string* enc = r.get("content-encoding");
+  return (sha && sha->compare(0, 10, "STREAMING-") == 0) || (enc && enc->find("aws-chunked") != std::string::npos);
+}
+
+// repr() of a Python str, for the messages the gateway formats with {key!r}
+std::string py_repr(const std::string& v) {
+  const char q = v.find('\'') != std::string::npos && v.find('"') == std::string::npos ? '"' : '\'';
+  std::string o(1, q);
+  for (unsigned char ch : v) {
+    if (ch == '\\') o += "\\\\";
+    else if (ch == static_cast<unsigned char>(q)) o += std::string("\\") + q;
+    else if (ch == '\n') o += "\\n";
+    else if (ch == '\r') o += "\\r";
+    else if (ch == '\t') o += "\\t";
+    else if (ch < 0x20 || ch == 0x7f) {
+      char u[8];
+      std::snprintf(u, sizeof u, "\\x%02x", ch);
+      o += u;
+    } else {
+      o.push_back(static_cast<char>(ch));
+    }
+  }
+  return o + q;
+}
+
+// urllib.parse.unquote for the copy source: %XX decoded, '+' kept; false when the result is
+// not UTF-8 (Python would substitute U+FFFD: the request goes there)
+bool unquote(const std::string& v, std::string* o) {
+  std::map<std::string, std::string> m;
+  std::string enc;
+  for (char ch : v) enc += ch == '+' ? std::string("%2B") : ch == '&' ? std::string("%26") : ch == '=' ? std::string("%3D") : std::string(1, ch);
+  if (!decode_query("k=" + enc, &m)) return false;
+  *o = m["k"];
+  return true;
+}
+
+// "n:size,..." of a completion marker (x-dfs-mpu-layout)
+bool parse_layout(const std::string& lay, std::vector<std::pair<uint64_t, uint64_t>>* parts) {
+  parts->clear();
+  for (size_t a = 0; a < lay.size();) {
+    size_t b = lay.find(',', a);
+    std::string kv = lay.substr(a, b == std::string::npos ? std::string::npos : b - a);
+    size_t colon = kv.find(':');
+    if (colon == std::string::npos || !all_digits(kv.substr(0, colon)) || !all_digits(kv.substr(colon + 1)))
+      return false;
+    parts->emplace_back(std::stoull(kv.substr(0, colon)), std::stoull(kv.substr(colon + 1)));
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  return true;
+}
+
+// A small XML reader for request bodies (DeleteObjects): elements by local name (namespace
+// prefix dropped, as s3/xml.py's _local does), each with ElementTree's .text (character data
+// before the first child). False for anything outside this subset — comments, CDATA, DTDs,
+// unknown entities, mismatched tags: Python's ElementTree decides those.
+struct XNode {
+  std::string qname, name, text;
+  std::vector<XNode> kids;
+  const XNode* child(const char* n) const {
+    for (auto& k : kids)
+      if (k.name == n) return &k;
+    return nullptr;
+  }
+};
+
+bool xml_unescape(const std::string& raw, std::string* o) {
+  o->clear();
+  for (size_t k = 0; k < raw.size(); ++k) {
+    char ch = raw[k];
+    if (ch == '\r') {  // XML end-of-line handling: \r\n and lone \r become \n
+      if (k + 1 < raw.size() && raw[k + 1] == '\n') ++k;
+      o->push_back('\n');
+      continue;
+    }
+    if (ch != '&') {
+      o->push_back(ch);
+      continue;
+    }
+    size_t e = raw.find(';', k);
+    if (e == std::string::npos || e - k > 12) return false;
+    const std::string ent = raw.substr(k + 1, e - k - 1);
+    k = e;
+    if (ent == "amp") o->push_back('&');
+    else if (ent == "lt") o->push_back('<');
+    else if (ent == "gt") o->push_back('>');
+    else if (ent == "quot") o->push_back('"');
+    else if (ent == "apos") o->push_back('\'');
+    else if (ent.size() > 1 && ent[0] == '#') {
+      const bool hx = ent[1] == 'x';
+      const std::string num = ent.substr(hx ? 2 : 1);
+      if (num.empty() || num.find_first_not_of(hx ? "0123456789abcdefABCDEF" : "0123456789") != std::string::npos)
+        return false;
+      unsigned long cp = std::stoul(num, nullptr, hx ? 16 : 10);
+      if (cp == 0 || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return false;
+      if (cp < 0x80) {
+        o->push_back(static_cast<char>(cp));
+      } else if (cp < 0x800) {
+        o->push_back(static_cast<char>(0xC0 | (cp >> 6)));
+        o->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+      } else if (cp < 0x10000) {
+        o->push_back(static_cast<char>(0xE0 | (cp >> 12)));
+        o->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+        o->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+      } else {
+        o->push_back(static_cast<char>(0xF0 | (cp >> 18)));
+        o->push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+        o->push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+        o->push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+      }
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+bool parse_xml(const std::string& b, XNode* root) {
+  std::vector<XNode*> stack;
+  bool have_root = false, closed = false;
+  std::string text;
+  auto flush = [&]() {
+    if (stack.empty() || !stack.back()->kids.empty()) {  // outside the root, or a tail
+      bool ws = text.find_first_not_of(" \t\r\n") == std::string::npos;
+      text.clear();
+      return ws || !stack.empty();
+    }
+    std::string v;
+    if (!xml_unescape(text, &v)) return false;
+    stack.back()->text += v;
+    text.clear();
+    return true;
+  };
+  size_t i = 0;
+  while (i < b.size()) {
+    if (b[i] != '<') {
+      text.push_back(b[i++]);
+      continue;
+    }
+    if (!flush()) return false;
+    size_t j = i + 1;
+    char quote = 0;
+    for (; j < b.size(); ++j) {
+      if (quote) {
+        if (b[j] == quote) quote = 0;
+      } else if (b[j] == '"' || b[j] == '\'') {
+        quote = b[j];
+      } else if (b[j] == '>') {
+        break;
+      }
+    }
+    if (j >= b.size()) return false;
+    std::string tag = b.substr(i + 1, j - i - 1);
+    i = j + 1;
+    if (tag.empty() || tag[0] == '!') return false;
+    if (tag[0] == '?') {
+      if (have_root) return false;
+      continue;
+    }
+    const bool closing = tag[0] == '/', empty_el = !closing && tag.back() == '/';
+    std::string qn = closing ? tag.substr(1) : empty_el ? tag.substr(0, tag.size() - 1) : tag;
+    qn = qn.substr(0, qn.find_first_of(" \t\r\n"));
+    if (qn.empty()) return false;
+    if (closing) {
+      if (stack.empty() || stack.back()->qname != qn) return false;
+      stack.pop_back();
+      if (stack.empty()) closed = true;
+      continue;
+    }
+    if (closed || (stack.empty() && have_root)) return false;
+    XNode* node;
+    if (stack.empty()) {
+      *root = XNode{};
+      node = root;
+      have_root = true;
+    } else {
+      stack.back()->kids.emplace_back();
+      node = &stack.back()->kids.back();
+    }
+    node->qname = qn;
+    size_t colon = qn.find(':');
+    node->name = colon == std::string::npos ? qn : qn.substr(colon + 1);
+    if (!empty_el) stack.push_back(node);
+    else if (stack.empty()) closed = true;
+  }
+  if (!text.empty() && text.find_first_not_of(" \t\r\n") != std::string::npos) return false;
+  return have_root && closed && stack.empty();
+}
+
+// Runs fn(i) for i in [0, n) on up to `width` pool threads (the pool grows per task, so a
+// bulk request must not submit one task per item).
+template <class F>
+void parallel_for(IoPool& pool, size_t n, size_t width, F fn) {
+  if (n <= 1) {
+    if (n) fn(0);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::future<void>> fs;
+  for (size_t w = 0; w < std::min(n, width); ++w)
+    fs.push_back(pool.submit([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) fn(i);
+    }));
+  for (auto& f : fs) f.get();
+}
+
+}  // namespace
 
 S3Front::S3Front(S3FrontConfig cfg, FastClient* fc)
     : cfg_(std::move(cfg)), own_store_(std::make_unique<FastFrontStore>(fc)), fc_(own_store_.get()) {}
@@ -664,46 +880,61 @@ bool S3Front::handle(Conn* c, Req& r) {
   const bool plain_path = r.raw_path.size() > 1 && r.raw_path[0] == '/' &&
                           r.raw_path.find('%') == std::string::npos;
   std::map<std::string, std::string> q;
-  if (!fc_ || !plain_path) return proxy(c, r, nullptr, 0, "route");
+  if (!fc_ || !plain_path || !decode_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
+  // a presigned URL's authentication parameters are not part of the operation
+  for (auto it = q.begin(); it != q.end();) {
+    if (it->first.compare(0, 6, "X-Amz-") == 0) {
+      r.presign.insert(*it);
+      it = q.erase(it);
+    } else {
+      ++it;
+    }
+  }
   std::string p = r.raw_path.substr(1);
   size_t slash = p.find('/');
-  if (r.method == "GET" && slash != 0 && (slash == std::string::npos || slash + 1 == p.size())) {
-    // GET /bucket[/]: ListObjects (v1, or v2 with list-type=2) unless it is a sub-resource
+  if (slash != 0 && (slash == std::string::npos || slash + 1 == p.size())) {
     const std::string bucket = p.substr(0, slash);
-    if (bucket.empty() || !decode_query(r.raw_query, &q) || q.count("location") || q.count("policy") ||
-        r.content_length > 0 || r.chunked)
-      return proxy(c, r, nullptr, 0, "route");
-    return native_list(c, r, bucket, q);
+    if (bucket.empty()) return proxy(c, r, nullptr, 0, "route");
+    if (r.method == "GET") {
+      // ListObjects (v1, or v2 with list-type=2) unless it is a sub-resource
+      if (q.count("location") || q.count("policy") || r.content_length > 0 || r.chunked)
+        return proxy(c, r, nullptr, 0, "route");
+      return native_list(c, r, bucket, q);
+    }
+    if (r.method == "POST" && q.size() == 1 && q.count("delete")) return native_delete_objects(c, r, bucket, q);
+    return proxy(c, r, nullptr, 0, "route");
   }
-  if (!simple_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
   if (slash == std::string::npos || slash == 0 || slash + 1 >= p.size()) return proxy(c, r, nullptr, 0, "route");
   const std::string bucket = p.substr(0, slash), key = p.substr(slash + 1);
   if (reserved_key(key)) return proxy(c, r, nullptr, 0, "route");
   q.erase("x-id");  // SDK operation tag, no meaning to S3 itself
   if (r.method == "POST" && q.size() == 1 && q.count("uploadId") && !r.chunked && r.content_length <= (1 << 20) &&
-      !cfg_.metadata_sidecar) {
-    const std::string* sha = r.get("x-amz-content-sha256");
-    if (!(sha && sha->compare(0, 10, "STREAMING-") == 0)) return native_complete(c, r, bucket, key, q);
-  }
+      !cfg_.metadata_sidecar && !aws_chunked(r))
+    return native_complete(c, r, bucket, key, q);
   if (r.method == "POST" && q.size() == 1 && q.count("uploads") && q["uploads"].empty() && !r.chunked &&
       r.content_length <= 0 && !cfg_.metadata_sidecar)
     return native_initiate(c, r, bucket, key, q);
+  if (r.method == "POST" && q.size() == 1 && q.count("delete")) return native_delete_objects(c, r, bucket, q);
   const bool part = q.size() == 2 && q.count("partNumber") && q.count("uploadId");
-  if (!q.empty() && !part) return proxy(c, r, nullptr, 0, "query");
-  const bool is_put = r.method == "PUT", is_get = r.method == "GET", is_head = r.method == "HEAD";
-  if (!(is_put || ((is_get || is_head) && !part))) return proxy(c, r, nullptr, 0, "method");
+  const bool is_put = r.method == "PUT", is_get = r.method == "GET", is_head = r.method == "HEAD",
+             is_delete = r.method == "DELETE";
+  const bool abort = is_delete && q.size() == 1 && q.count("uploadId");
+  if (!q.empty() && !part && !abort) return proxy(c, r, nullptr, 0, "query");
+  if (!(is_put || is_delete || ((is_get || is_head) && !part))) return proxy(c, r, nullptr, 0, "method");
   // SSE-S3: whole objects are encrypted / decrypted here (AES-256-GCM, the gateway's DEK
   // envelope). Multipart parts are stored as sent, as the reference's UploadPart does
   // (handlers.rs encrypts in PutObject and CopyObject only), so they stay native too.
   if (cfg_.sse_enabled && cfg_.sse_kek.size() != 32) return proxy(c, r, nullptr, 0, "sse");
+  const std::string* copy_src = is_put ? r.get("x-amz-copy-source") : nullptr;
   if (is_put) {
-    if (r.chunked || r.get("x-amz-copy-source") || cfg_.metadata_sidecar) return proxy(c, r, nullptr, 0, "put-form");
-    const std::string* sha = r.get("x-amz-content-sha256");
-    const std::string* enc = r.get("content-encoding");
-    if ((sha && sha->compare(0, 10, "STREAMING-") == 0) || (enc && enc->find("aws-chunked") != std::string::npos))
-      return proxy(c, r, nullptr, 0, "aws-chunked");
-    if (static_cast<uint64_t>(r.content_length) + (cfg_.sse_enabled ? 28 : 0) > fc_->slot_bytes())
-      return proxy(c, r, nullptr, 0, "large");
+    if (r.chunked || cfg_.metadata_sidecar || (copy_src && (part || r.content_length > 0)))
+      return proxy(c, r, nullptr, 0, "put-form");
+    uint64_t body = static_cast<uint64_t>(r.content_length);
+    if (aws_chunked(r)) {  // the decoded size, when the client says it (it always does)
+      const std::string* dl = r.get("x-amz-decoded-content-length");
+      if (dl && all_digits(*dl)) body = std::min<uint64_t>(body, std::stoull(*dl));
+    }
+    if (body + (cfg_.sse_enabled ? 28 : 0) > fc_->slot_bytes()) return proxy(c, r, nullptr, 0, "large");
   } else if (r.content_length > 0 || r.chunked) {
     return proxy(c, r, nullptr, 0, "body");
   }
@@ -720,8 +951,17 @@ bool S3Front::handle(Conn* c, Req& r) {
       return proxy(c, r, nullptr, 0, "part-args");
     path = "/.s3_mpu/" + uid + "/" + std::to_string(std::stoull(pn));
     ok = native_put(c, r, path, true);
+  } else if (copy_src) {
+    ok = native_copy(c, r, path);
   } else if (is_put) {
     ok = native_put(c, r, path, false);
+  } else if (abort) {
+    const std::string& uid = q["uploadId"];
+    if (uid.empty() || uid.find('/') != std::string::npos || uid == "." || uid == "..")
+      return proxy(c, r, nullptr, 0, "part-args");
+    ok = native_abort(c, r, uid);
+  } else if (is_delete) {
+    ok = native_delete(c, r, path);
   } else {
     ok = native_get(c, r, path, is_head);
   }
@@ -929,28 +1169,59 @@ bool S3Front::open_session(const std::string& token, Session* out) {
   }
 }
 
+// SigV4 of the Authorization header, or of a presigned URL's query (reference
+// auth_middleware.rs:19-365, presign.rs; s3/server.py authenticate): the same canonical
+// request either way — the query without X-Amz-Signature, the signed headers, the payload
+// hash header or UNSIGNED-PAYLOAD. A presigned URL is bounded by X-Amz-Expires (at most 7
+// days) instead of the 15-minute skew. Anything that does not verify is handed over, so
+// Python answers with the exact error and audit record.
 int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
   const std::string* auth = r.get("authorization");
-  if (!auth || auth->compare(0, 16, "AWS4-HMAC-SHA256") != 0) return 0;
-  const std::string* token = r.get("x-amz-security-token");
-  if (token && !open_session(*token, sess)) return 0;
-  std::vector<std::string> parts;
-  size_t i = 0;
-  while (i <= auth->size()) {
-    size_t cm = auth->find(',', i);
-    parts.push_back(trim(auth->substr(i, cm == std::string::npos ? std::string::npos : cm - i)));
-    if (cm == std::string::npos) break;
-    i = cm + 1;
-  }
-  if (parts.size() < 3) return 0;
-  std::string cred;
-  {
+  auto qp = [&r](const char* k) -> const std::string* {
+    auto it = r.presign.find(k);
+    return it == r.presign.end() ? nullptr : &it->second;
+  };
+  const bool presigned = !auth && qp("X-Amz-Algorithm") && qp("X-Amz-Expires");
+  std::string cred, sh, sig;
+  const std::string* ts = nullptr;
+  if (auth) {
+    if (auth->compare(0, 16, "AWS4-HMAC-SHA256") != 0) return 0;
+    std::vector<std::string> parts;
+    size_t i = 0;
+    while (i <= auth->size()) {
+      size_t cm = auth->find(',', i);
+      parts.push_back(trim(auth->substr(i, cm == std::string::npos ? std::string::npos : cm - i)));
+      if (cm == std::string::npos) break;
+      i = cm + 1;
+    }
+    if (parts.size() < 3) return 0;
     size_t k = parts[0].find("Credential=");
     if (k == std::string::npos) return 0;
     cred = parts[0].substr(k + 11);
     size_t sp = cred.find_first_of(" \t");
     if (sp != std::string::npos) cred = cred.substr(0, sp);
+    auto after_eq = [](const std::string& v) {
+      size_t e = v.find('=');
+      return e == std::string::npos ? std::string() : trim(v.substr(e + 1));
+    };
+    sh = after_eq(parts[1]);
+    sig = after_eq(parts[2]);
+    ts = r.get("x-amz-date");
+    if (!ts) ts = r.get("date");
+  } else if (presigned) {
+    if (*qp("X-Amz-Algorithm") != "AWS4-HMAC-SHA256" || !qp("X-Amz-Credential") || !qp("X-Amz-SignedHeaders") ||
+        !qp("X-Amz-Signature") || !qp("X-Amz-Date"))
+      return 0;
+    cred = *qp("X-Amz-Credential");
+    sh = *qp("X-Amz-SignedHeaders");
+    sig = *qp("X-Amz-Signature");
+    ts = qp("X-Amz-Date");
+  } else {
+    return 0;
   }
+  const std::string* token = r.get("x-amz-security-token");
+  if (!token) token = qp("X-Amz-Security-Token");
+  if (token && !open_session(*token, sess)) return 0;
   std::vector<std::string> cp;
   for (size_t a = 0;;) {
     size_t b = cred.find('/', a);
@@ -959,19 +1230,19 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
     a = b + 1;
   }
   if (cp.size() < 5 || cp[4] != "aws4_request") return 0;
-  auto after_eq = [](const std::string& s) {
-    size_t e = s.find('=');
-    return e == std::string::npos ? std::string() : trim(s.substr(e + 1));
-  };
-  const std::string sh = after_eq(parts[1]), sig = after_eq(parts[2]);
-  const std::string* ts = r.get("x-amz-date");
-  if (!ts) ts = r.get("date");
   if (!ts || sh.empty() || sig.empty()) return 0;
-  // %Y%m%dT%H%M%SZ within 15 minutes of now
   tm t{};
   if (ts->size() != 16 || !strptime(ts->c_str(), "%Y%m%dT%H%M%SZ", &t)) return 0;
-  double skew = std::abs(static_cast<double>(timegm(&t)) - now_s());
-  if (skew / 60.0 > 15.0) return 0;
+  const double age = now_s() - static_cast<double>(timegm(&t));
+  if (presigned) {
+    // 0 < X-Amz-Expires <= 604800 and not yet expired
+    const std::string& ex = *qp("X-Amz-Expires");
+    if (!all_digits(ex) || ex.size() > 9) return 0;
+    const double expires = static_cast<double>(std::stoull(ex));
+    if (expires <= 0 || expires > 604800 || age > expires) return 0;
+  } else if (std::abs(age) / 60.0 > 15.0) {  // %Y%m%dT%H%M%SZ within 15 minutes of now
+    return 0;
+  }
   const std::string &ak = cp[0], &date = cp[1], &region = cp[2], &service = cp[3];
   if (region != cfg_.region || service != "s3") return 0;
   std::string skey;
@@ -1022,13 +1293,17 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
   sr.signed_headers = joined;
   const std::string* ph = r.get("x-amz-content-sha256");
   sr.payload_hash = ph && !ph->empty() ? *ph : kUnsigned;
-  if (sr.payload_hash == kUnsigned && !cfg_.allow_unsigned_payload) return 0;
+  if (sr.payload_hash == kUnsigned && !cfg_.allow_unsigned_payload && !presigned) return 0;
   const std::string scope = date + "/" + region + "/" + service + "/aws4_request";
   std::string creq;
   if (!sigv4::verify(sr, *ts, scope, skey, sig, &creq)) return 0;
   *user = ak;
+  // an aws-chunked body continues this signature's chain (seed = the request signature)
+  r.chain = sigv4::ChunkChain{skey, *ts, scope, sig};
+  r.chain_set = true;
   std::lock_guard<std::mutex> g(st_mu_);
   st_.auth_native++;
+  if (presigned) st_.presigned++;
   return 1;
 }
 
@@ -1157,10 +1432,14 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
     if (fc_->stat(marker, &found, &meta, &msg, r.rid) != FastClient::Ok || !found)
       return proxy(c, r, nullptr, 0, "no-upload");
   }
-  const uint64_t n = static_cast<uint64_t>(r.content_length);
+  uint64_t n = static_cast<uint64_t>(r.content_length);
+  const bool aws = aws_chunked(r);
+  if (aws) {  // decoded into the slot below; its size bounded by what the client announced
+    const std::string* dl = r.get("x-amz-decoded-content-length");
+    if (dl && all_digits(*dl)) n = std::min<uint64_t>(n, std::stoull(*dl));
+  }
   const bool sse = cfg_.sse_enabled && !part;  // handle() sent SSE parts to Python
-  const uint64_t stored = sse ? n + 28 : n;    // [nonce 12][ciphertext n][tag 16]
-  int64_t slot = fc_->acquire_slot(std::max<uint64_t>(stored, 1));
+  int64_t slot = fc_->acquire_slot(std::max<uint64_t>(sse ? n + 28 : n, 1));  // [nonce 12][ciphertext n][tag 16]
   if (slot < 0) return proxy(c, r, nullptr, 0, "no-slot");
   struct Release {
     FrontStore* fc;
@@ -1169,7 +1448,18 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
   } rel{fc_, slot};
   if (r.expect_continue && !send_all(c->io(), "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
   uint8_t* dst = fc_->slot_mut(slot);
-  if (!read_body(c, sse ? dst + 12 : dst, n)) return false;
+  if (aws) {
+    const int rc = read_aws_chunked(c, r, sse ? dst + 12 : dst, n, &n);
+    if (rc == 0) return false;
+    if (rc < 0) {  // s3/server.py route(): the body does not decode or its chain is broken
+      r.keep_alive = false;
+      s3_error(c, r, 403, "SignatureDoesNotMatch", "aws-chunked signature chain is invalid");
+      return false;
+    }
+  } else if (!read_body(c, sse ? dst + 12 : dst, n)) {
+    return false;
+  }
+  const uint64_t stored = sse ? n + 28 : n;
   std::map<std::string, std::string> attrs;
   std::string plain_md5, dk;
   if (sse) {
@@ -1203,6 +1493,12 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
       st = fc_->write_slot(path, slot, stored, &reps, &msg, &t, r.rid, part ? nullptr : &attrs, etag_attr, &md5);
   }
   if (st != FastClient::Ok) {
+    // a decoded aws-chunked body cannot be handed over under its signed STREAMING headers
+    if (aws) {
+      r.keep_alive = false;
+      s3_error(c, r, 500, "InternalError", msg.empty() ? "write failed" : msg, path);
+      return false;
+    }
     if (!sse) return proxy(c, r, dst, n, "put-fallback");
     // the slot holds ciphertext: decrypt it back so Python gets the body it would have read
     if (!crypto::aes256gcm_decrypt_inplace(reinterpret_cast<const uint8_t*>(dk.data()), dst, dst + 12, n,
@@ -1224,6 +1520,7 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
     std::lock_guard<std::mutex> g(st_mu_);
     (part ? st_.parts : st_.puts)++;
     st_.bytes_in += n;
+    if (aws) st_.chunked_puts++;
   }
   return send_all(c->io(), head.data(), head.size());
 }
@@ -1681,16 +1978,7 @@ bool S3Front::native_mpu_get(Conn* c, Req& r, const std::string& path, const std
   auto lay = mk.attributes.find("x-dfs-mpu-layout");
   if (lay == mk.attributes.end()) return proxy(c, r, nullptr, 0, "mpu-layout");
   std::vector<std::pair<uint64_t, uint64_t>> parts;  // (number, size)
-  for (size_t a = 0; a < lay->second.size();) {
-    size_t b = lay->second.find(',', a);
-    std::string kv = lay->second.substr(a, b == std::string::npos ? std::string::npos : b - a);
-    size_t colon = kv.find(':');
-    if (colon == std::string::npos || !all_digits(kv.substr(0, colon)) || !all_digits(kv.substr(colon + 1)))
-      return proxy(c, r, nullptr, 0, "mpu-layout");
-    parts.emplace_back(std::stoull(kv.substr(0, colon)), std::stoull(kv.substr(colon + 1)));
-    if (b == std::string::npos) break;
-    a = b + 1;
-  }
+  if (!parse_layout(lay->second, &parts)) return proxy(c, r, nullptr, 0, "mpu-layout");
   std::string hdrs;
   if (!object_headers(nullptr, mk.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
   uint64_t total = 0;
@@ -1793,6 +2081,389 @@ bool S3Front::native_mpu_get(Conn* c, Req& r, const std::string& path, const std
     st_.bytes_out += len;
   }
   return true;
+}
+
+// ---------------------------------------------------------------- delete, copy, aws-chunked
+bool S3Front::respond(Conn* c, Req& r, int status, const std::string& xml, const std::string& extra) {
+  const char* reason = status == 200 ? "OK" : status == 204 ? "No Content" : status == 400 ? "Bad Request"
+                       : status == 403 ? "Forbidden" : status == 404 ? "Not Found" : "Internal Server Error";
+  std::string h = "HTTP/1.1 " + std::to_string(status) + " " + reason + "\r\n" + extra;
+  if (!xml.empty()) h += "Content-Type: application/xml\r\n";
+  if (status != 204) h += "Content-Length: " + std::to_string(xml.size()) + "\r\n";
+  h += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
+  r.status = status;
+  count(r, status);
+  return send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(xml.data()), xml.size());
+}
+
+// X.error of s3/xml.py
+bool S3Front::s3_error(Conn* c, Req& r, int status, const std::string& code, const std::string& msg,
+                       const std::string& resource) {
+  return respond(c, r, status,
+                 "<Error>" + xel("Code", code) + xel("Message", msg) + xel("Resource", resource) +
+                     "<RequestId></RequestId></Error>");
+}
+
+// aws-chunked framing, `<hex>[;chunk-signature=<sig>]\r\n<data>\r\n ... 0[;...]\r\n[trailers]`
+// (s3/auth/sigv4.py decode_chunked, reference auth_middleware.rs streaming payloads), read
+// straight from the connection: chunk headers through the connection buffer, chunk data into
+// the slot. With STREAMING-AWS4-HMAC-SHA256-PAYLOAD on an authenticated gateway every chunk,
+// the final empty one included, must continue the request signature's chain.
+int S3Front::read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint64_t* n_out) {
+  const uint64_t total = static_cast<uint64_t>(std::max<int64_t>(r.content_length, 0));
+  const std::string* sha = r.get("x-amz-content-sha256");
+  sigv4::ChunkChain* chain =
+      cfg_.auth_enabled && r.chain_set && sha && *sha == "STREAMING-AWS4-HMAC-SHA256-PAYLOAD" ? &r.chain : nullptr;
+  uint64_t used = 0, n = 0, sigs = 0;
+  char tmp[16 << 10];
+  auto line = [&](std::string* out) -> int {
+    for (;;) {
+      size_t e = c->buf.find("\r\n", c->pos);
+      if (e != std::string::npos) {
+        const uint64_t k = e + 2 - c->pos;
+        if (used + k > total) return -1;  // the line runs past the body
+        out->assign(c->buf, c->pos, e - c->pos);
+        c->pos = e + 2;
+        used += k;
+        return 1;
+      }
+      const uint64_t have = c->buf.size() - c->pos;
+      if (have > 4096 || used + have >= total) return -1;
+      c->buf.erase(0, c->pos);
+      c->pos = 0;
+      long k = io_recv(c->io(), tmp, sizeof tmp);
+      if (k <= 0) return 0;
+      c->buf.append(tmp, static_cast<size_t>(k));
+    }
+  };
+  auto fail = [&](int rc) {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.chunk_sigs += sigs;
+    if (rc < 0 && chain) st_.chunk_sig_failures++;
+    return rc;
+  };
+  bool final_chunk = false;
+  while (used < total) {
+    std::string h;
+    int rc = line(&h);
+    if (rc <= 0) return fail(rc);
+    const size_t semi = h.find(';');
+    const std::string hex = trim(h.substr(0, semi));
+    if (hex.size() > 15 || hex.find_first_not_of("0123456789abcdefABCDEF") != std::string::npos) return fail(-1);
+    const uint64_t size = hex.empty() ? 0 : std::stoull(hex, nullptr, 16);
+    if (size > total - used || n + size > cap) return fail(-1);
+    if (!read_body(c, dst + n, size)) return fail(0);
+    used += size;
+    if (chain) {
+      std::string sig;
+      if (semi != std::string::npos) {
+        size_t k = h.find("chunk-signature=", semi);
+        if (k != std::string::npos) sig = trim(h.substr(k + 16));
+      }
+      if (!chain->verify(dst + n, size, sig)) return fail(-1);
+      ++sigs;
+    }
+    if (size == 0) {
+      final_chunk = true;
+      break;
+    }
+    n += size;
+    std::string crlf;
+    rc = line(&crlf);
+    if (rc <= 0) return fail(rc);
+    if (!crlf.empty()) return fail(-1);
+  }
+  if (chain && !final_chunk) return fail(-1);  // a signed stream ends with its signed empty chunk
+  while (used < total) {  // trailers (x-amz-checksum-*) and the closing CRLF
+    uint64_t have = std::min<uint64_t>(total - used, c->buf.size() - c->pos);
+    if (have) {
+      c->pos += have;
+      used += have;
+      continue;
+    }
+    long k = io_recv(c->io(), tmp, std::min<uint64_t>(sizeof tmp, total - used));
+    if (k <= 0) return fail(0);
+    used += static_cast<uint64_t>(k);
+  }
+  *n_out = n;
+  return fail(1);
+}
+
+// DeleteObject (reference handlers.rs delete_object; s3/server.py delete_object): the object
+// file, every file of a multipart object under "<key>/", and the sidecar "<key>.meta"; 204
+// whether or not anything existed. The three lookups go out together; a master that cannot
+// be reached here hands the (idempotent) request to Python.
+bool S3Front::native_delete(Conn* c, Req& r, const std::string& path) {
+  TraceRange tr("dfs.s3.delete");
+  auto kids_f = pool_.submit([this, &path, &r] {
+    std::vector<std::pair<std::string, pb::FileMetadata>> kids;
+    const bool ok = fc_->list(path + "/", &kids, r.rid) == FastClient::Ok;
+    return std::make_pair(ok, std::move(kids));
+  });
+  auto meta_f = pool_.submit([this, &path, &r] {
+    std::string m;
+    return fc_->remove(path + ".meta", &m, r.rid);
+  });
+  std::string msg;
+  const bool main_ok = fc_->remove(path, &msg, r.rid) != FastClient::NotHandled;
+  auto kids = kids_f.get();
+  const bool meta_ok = meta_f.get() != FastClient::NotHandled;
+  if (!main_ok || !meta_ok || !kids.first) return proxy(c, r, nullptr, 0, "delete");
+  std::atomic<bool> handled{true};
+  parallel_for(pool_, kids.second.size(), 16, [&](size_t i) {
+    std::string m;
+    if (fc_->remove(kids.second[i].first, &m, r.rid) == FastClient::NotHandled) handled = false;
+  });
+  if (!handled) return proxy(c, r, nullptr, 0, "delete");
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.deletes++;
+  }
+  return respond(c, r, 204, "");
+}
+
+// AbortMultipartUpload (reference handlers.rs:450-470; s3/server.py abort_mpu): the upload's
+// directory /.s3_mpu/<id>/ emptied; 204 whether or not it existed.
+bool S3Front::native_abort(Conn* c, Req& r, const std::string& upload_id) {
+  TraceRange tr("dfs.s3.mpu_abort");
+  std::vector<std::pair<std::string, pb::FileMetadata>> files;
+  if (fc_->list("/.s3_mpu/" + upload_id + "/", &files, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "abort");
+  std::atomic<bool> handled{true};
+  parallel_for(pool_, files.size(), 16, [&](size_t i) {
+    std::string m;
+    if (fc_->remove(files[i].first, &m, r.rid) == FastClient::NotHandled) handled = false;
+  });
+  if (!handled) return proxy(c, r, nullptr, 0, "abort");
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.mpu_aborts++;
+  }
+  return respond(c, r, 204, "");
+}
+
+// DeleteObjects (reference handlers.rs:1102-1180; s3/server.py delete_objects): the
+// <Delete><Object><Key>..</Key></Object>..<Quiet/></Delete> body parsed here, the keys removed
+// 16 at a time, a missing key reported as deleted, the DeleteResult written here.
+bool S3Front::native_delete_objects(Conn* c, Req& r, const std::string& bucket,
+                                    std::map<std::string, std::string>& q) {
+  TraceRange tr("dfs.s3.delete_objects");
+  if (r.chunked || r.content_length <= 0 || r.content_length > (4 << 20) || aws_chunked(r))
+    return proxy(c, r, nullptr, 0, "delete-body");
+  std::string body(static_cast<size_t>(r.content_length), '\0');
+  if (r.expect_continue && !send_all(c->io(), "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+  if (!read_body(c, reinterpret_cast<uint8_t*>(&body[0]), body.size())) return false;
+  r.expect_continue = false;  // the body is read: a hand-over sends it along
+  auto hand_over = [&](const std::string& why) {
+    return proxy(c, r, reinterpret_cast<const uint8_t*>(body.data()), body.size(), why);
+  };
+  std::string user = "anonymous", why;
+  Session sess;
+  if (!authorize(r, bucket, q, &user, &sess, &why)) return hand_over(why);
+  XNode root;
+  if (!parse_xml(body, &root) || root.name != "Delete") return hand_over("delete-xml");  // MalformedXML there
+  std::vector<std::string> keys;
+  for (auto& o : root.kids)
+    if (o.name == "Object") {
+      const XNode* k = o.child("Key");
+      keys.push_back(k ? k->text : std::string());
+    }
+  bool quiet = false;
+  if (const XNode* qn = root.child("Quiet")) quiet = lower(trim(qn->text)) == "true";
+  struct Res {
+    int kind = 0;  // 0 deleted, 1 error, 2 not handled here
+    std::string code, msg;
+  };
+  std::vector<Res> res(keys.size());
+  parallel_for(pool_, keys.size(), 16, [&](size_t i) {
+    const std::string& k = keys[i];
+    Res& o = res[i];
+    if (reserved_key(k)) {
+      o = {1, "InvalidArgument", "object key " + py_repr(k) + " is reserved"};
+      return;
+    }
+    const std::string path = "/" + bucket + "/" + k;
+    std::string m;
+    auto st = fc_->remove(path, &m, r.rid);
+    if (st == FastClient::NotHandled) {
+      o.kind = 2;
+      return;
+    }
+    if (st == FastClient::Failed && lower(m).find("not found") == std::string::npos) {
+      o = {1, "InternalError", m};
+      return;
+    }
+    (void)fc_->remove(path + ".meta", &m, r.rid);
+  });
+  std::string deleted, errors;
+  uint64_t nd = 0;
+  for (size_t i = 0; i < keys.size(); ++i) {
+    if (res[i].kind == 2) return hand_over("delete");  // every key again, in Python
+    if (res[i].kind == 0) {
+      ++nd;
+      if (!quiet) deleted += "<Deleted>" + xel("Key", keys[i]) + "</Deleted>";
+    } else {
+      errors += "<Error>" + xel("Key", keys[i]) + xel("Code", res[i].code) + xel("Message", res[i].msg) + "</Error>";
+    }
+  }
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.multi_deletes++;
+    st_.deleted_keys += nd;
+  }
+  const bool ok = respond(c, r, 200, "<DeleteResult>" + deleted + errors + "</DeleteResult>");
+  if (cfg_.auth_enabled) audit(c, r, user, 200, sess.role_arn);
+  return ok;
+}
+
+// CopyObject (reference handlers.rs:1182-1290; s3/server.py copy_object): the source — a plain
+// object, or a completed multipart one whose parts are read into one slot in parallel — is
+// decrypted in place when SSE wrapped it, re-encrypted under a fresh DEK when the gateway is
+// SSE, and written to the destination from the same slot with the source's (COPY) or the
+// request's (REPLACE) x-amz-meta-* headers. A missing or sidecar-described source, and any
+// error this path does not model, is Python's.
+bool S3Front::native_copy(Conn* c, Req& r, const std::string& dest) {
+  TraceRange tr("dfs.s3.copy");
+  std::string src;
+  {
+    std::string raw = *r.get("x-amz-copy-source");
+    raw = raw.substr(0, raw.find('?'));
+    if (!unquote(raw, &src)) return proxy(c, r, nullptr, 0, "copy-args");
+    if (src.empty() || src[0] != '/') src = "/" + src;
+    if (reserved_key(src)) return proxy(c, r, nullptr, 0, "copy-args");
+  }
+  const bool sse = cfg_.sse_enabled;
+  const uint64_t room = sse ? 28 : 0;
+  bool found = false;
+  std::string meta, msg;
+  if (fc_->stat(src, &found, &meta, &msg, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "copy-stat");
+  int64_t slot = -1;
+  struct Release {
+    FrontStore* fc;
+    int64_t* s;
+    ~Release() {
+      if (*s >= 0) fc->release(*s);
+    }
+  } rel{fc_, &slot};
+  std::map<std::string, std::string> src_attrs;
+  uint64_t n = 0;
+  bool at12 = false;  // the plaintext sits after a 12-byte nonce (a decrypted SSE source)
+  if (found) {
+    pb::FileMetadata m;
+    if (!m.decode(meta) || m.attributes.empty()) return proxy(c, r, nullptr, 0, "copy-attrs");
+    src_attrs = m.attributes;
+    auto dk = src_attrs.find("x-amz-sse-encrypted-dek");
+    const bool enc = dk != src_attrs.end();
+    if (enc && !sse) return proxy(c, r, nullptr, 0, "sse");
+    if (m.size + (enc ? 0 : room) > fc_->slot_bytes()) return proxy(c, r, nullptr, 0, "large");
+    if (m.size > 0) {
+      uint64_t got = 0;
+      FastClient::Times t;
+      if (fc_->read_known(meta, &slot, &got, &msg, &t, r.rid, 0, 0) != FastClient::Ok)
+        return proxy(c, r, nullptr, 0, "copy-read");
+      if (got != m.size) return proxy(c, r, nullptr, 0, "short-read");
+    } else if ((slot = fc_->acquire_slot(std::max<uint64_t>(room, 1))) < 0) {
+      return proxy(c, r, nullptr, 0, "no-slot");
+    }
+    n = m.size;
+    if (enc) {
+      std::string wrapped, key;
+      if (m.size < 28 || !crypto::base64_decode(dk->second, &wrapped) || wrapped.size() < 60)
+        return proxy(c, r, nullptr, 0, "sse");
+      try {
+        key = crypto::aes256gcm_decrypt(cfg_.sse_kek, wrapped.substr(0, 12), wrapped.substr(12), "");
+      } catch (const std::exception&) {
+        return proxy(c, r, nullptr, 0, "sse");
+      }
+      uint8_t* b = fc_->slot_mut(slot);
+      n = m.size - 28;
+      if (key.size() != 32 ||
+          !crypto::aes256gcm_decrypt_inplace(reinterpret_cast<const uint8_t*>(key.data()), b, b + 12, n, b + 12 + n))
+        return proxy(c, r, nullptr, 0, "sse");
+      at12 = true;
+    }
+  } else {
+    std::string mm;
+    if (fc_->stat(src + "/.s3_mpu_completed", &found, &mm, &msg, r.rid) != FastClient::Ok || !found)
+      return proxy(c, r, nullptr, 0, "copy-missing");  // NoSuchKey
+    pb::FileMetadata mk;
+    if (!mk.decode(mm) || mk.attributes.empty()) return proxy(c, r, nullptr, 0, "copy-attrs");
+    src_attrs = mk.attributes;
+    auto lay = src_attrs.find("x-dfs-mpu-layout");
+    std::vector<std::pair<uint64_t, uint64_t>> parts;
+    if (src_attrs.count("x-amz-sse-encrypted-dek") || lay == src_attrs.end() || !parse_layout(lay->second, &parts))
+      return proxy(c, r, nullptr, 0, "copy-mpu");
+    std::vector<uint64_t> offs;
+    for (auto& p : parts) {
+      offs.push_back(n);
+      n += p.second;
+    }
+    if (n + room > fc_->slot_bytes()) return proxy(c, r, nullptr, 0, "large");
+    if ((slot = fc_->acquire_slot(std::max<uint64_t>(n + room, 1))) < 0) return proxy(c, r, nullptr, 0, "no-slot");
+    uint8_t* d = fc_->slot_mut(slot) + (sse ? 12 : 0);
+    at12 = sse;
+    std::atomic<bool> ok{true};
+    parallel_for(pool_, parts.size(), 4, [&](size_t i) {
+      if (!ok) return;
+      bool f = false;
+      std::string pm, e;
+      pb::FileMetadata m;
+      if (fc_->stat(src + "/" + std::to_string(parts[i].first), &f, &pm, &e, r.rid) != FastClient::Ok || !f ||
+          !m.decode(pm) || m.size != parts[i].second) {
+        ok = false;
+        return;
+      }
+      if (m.size == 0) return;
+      int64_t ps = -1;
+      uint64_t got = 0;
+      FastClient::Times t;
+      if (fc_->read_known(pm, &ps, &got, &e, &t, r.rid, 0, 0) != FastClient::Ok || got != m.size) ok = false;
+      else std::memcpy(d + offs[i], fc_->slot_ptr(ps), got);
+      if (ps >= 0) fc_->release(ps);
+    });
+    if (!ok) return proxy(c, r, nullptr, 0, "copy-read");
+  }
+  uint8_t* b = fc_->slot_mut(slot);
+  const std::string md5 = crypto::md5_hex(at12 ? b + 12 : b, n);
+  const std::string etag = "\"" + md5 + "\"";
+  std::map<std::string, std::string> attrs{{"ETag", etag}};
+  const std::string* dir = r.get("x-amz-metadata-directive");
+  std::string directive = dir ? *dir : "COPY";
+  for (auto& ch : directive) ch = static_cast<char>(std::toupper(static_cast<unsigned char>(ch)));
+  if (directive == "REPLACE") {
+    for (auto& h : r.headers)
+      if (h.first.compare(0, 11, "x-amz-meta-") == 0) attrs[h.first] = h.second;
+  } else {
+    for (auto& kv : src_attrs)
+      if (kv.first.compare(0, 11, "x-amz-meta-") == 0 || kv.first == "Content-Type") attrs[kv.first] = kv.second;
+  }
+  uint64_t stored = n;
+  if (sse) {  // SseManager.encrypt_object: a fresh DEK, wrapped by the KEK
+    if (!at12) std::memmove(b + 12, b, n);
+    const std::string dk = crypto::random_bytes(32), n1 = crypto::random_bytes(12), n2 = crypto::random_bytes(12);
+    std::memcpy(b, n1.data(), 12);
+    crypto::aes256gcm_encrypt_inplace(reinterpret_cast<const uint8_t*>(dk.data()), b, b + 12, n, b + 12 + n);
+    attrs["x-amz-sse-encrypted-dek"] = crypto::base64_encode(n2 + crypto::aes256gcm_encrypt(cfg_.sse_kek, n2, dk, ""));
+    stored = n + 28;
+  }
+  FastClient::Times t;
+  std::string md5w;
+  int reps = 0;
+  auto st = fc_->write_slot(dest, slot, stored, &reps, &msg, &t, r.rid, &attrs, nullptr, &md5w);
+  if (st == FastClient::Failed && msg.find("already exists") != std::string::npos) {
+    std::string dmsg;
+    if (fc_->remove(dest, &dmsg, r.rid) != FastClient::NotHandled)
+      st = fc_->write_slot(dest, slot, stored, &reps, &msg, &t, r.rid, &attrs, nullptr, &md5w);
+  }
+  if (st != FastClient::Ok) return proxy(c, r, nullptr, 0, "copy-fallback");  // the copy again, in Python
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.copies++;
+    st_.copy_bytes += n;
+  }
+  int64_t ms;
+  return respond(c, r, 200,
+                 "<CopyObjectResult>" + xel("LastModified", iso_now(now_s(), &ms)) + xel("ETag", etag) +
+                     "</CopyObjectResult>");
 }
 
 // ---------------------------------------------------------------- hand-off to Python

@@ -12,10 +12,16 @@
 //                              lands the (range of the) block in a slot that is written to
 //                              the socket as is; multipart objects are streamed part by
 //                              part from the layout recorded at completion.
-// Everything else — buckets, listings, policies, STS, copy, multi-delete, MPU initiate /
-// complete / abort, SSE-encrypted objects, presigned or STS-signed requests, buckets with a
-// policy, any case this path does not own — is handed, unchanged, to the Python gateway
-// (aiohttp on a private UNIX socket, s3/server.py), which keeps the reference semantics.
+//   DELETE, DeleteObjects,  -> the object file, its multipart children and sidecar removed
+//   AbortMultipartUpload       over the masters' sockets (a bulk delete's keys in parallel);
+//   CopyObject              -> the source read into a slot (decrypted / re-encrypted under
+//                              SSE, multipart sources concatenated there) and written back;
+//   aws-chunked PUT         -> the chunk framing decoded from the socket into the slot, each
+//                              chunk's signature checked against the seed-signature chain;
+//   presigned URLs          -> query-string SigV4 (X-Amz-Credential/-Signature/-Expires).
+// Everything else — bucket create/delete, policies, STS, errors this path does not model, any
+// case it does not own — is handed, unchanged, to the Python gateway (aiohttp on a private
+// UNIX socket, s3/server.py), which keeps the reference semantics.
 // Signed requests are verified here with csrc/sigv4.cpp (static credentials); anything
 // that does not verify is handed over too, so Python produces the exact error and audit
 // record. Native requests of an authenticated gateway send their audit record to the
@@ -80,6 +86,8 @@ struct S3FrontStats {
   // slot, response send (where a GET's latency goes)
   uint64_t get_stat_us = 0, get_read_us = 0, get_send_us = 0, get_timed = 0;
   uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0, iam_native = 0, lists = 0, mpu_completes = 0, mpu_initiates = 0;
+  uint64_t deletes = 0, multi_deletes = 0, deleted_keys = 0, mpu_aborts = 0, copies = 0, copy_bytes = 0;
+  uint64_t chunked_puts = 0, chunk_sigs = 0, chunk_sig_failures = 0, presigned = 0;
 };
 
 class S3Front {
@@ -120,6 +128,17 @@ class S3Front {
                        std::map<std::string, std::string>& q);
   bool native_complete(Conn* c, Req& r, const std::string& bucket, const std::string& key,
                        std::map<std::string, std::string>& q);
+  bool native_delete(Conn* c, Req& r, const std::string& path);
+  bool native_abort(Conn* c, Req& r, const std::string& upload_id);
+  bool native_delete_objects(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q);
+  bool native_copy(Conn* c, Req& r, const std::string& dest);
+  // Reads an aws-chunked body (Content-Length framed) into dst (cap bytes): 1 ok (*n = decoded
+  // bytes), 0 connection error, -1 bad framing or a chunk signature that does not chain.
+  int read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint64_t* n);
+  // A response with an S3 XML body (or none); counts it as a native request.
+  bool respond(Conn* c, Req& r, int status, const std::string& xml, const std::string& extra = "");
+  bool s3_error(Conn* c, Req& r, int status, const std::string& code, const std::string& msg,
+                const std::string& resource = "");
   int verify_auth(Req& r, std::string* user, Session* sess);  // 1 ok, 0 hand over
   // The bucket's policy: *known = false when it could not be read (the request is handed
   // over); a null pointer when the bucket has none (or an unparsable one, which the gateway

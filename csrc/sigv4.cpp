@@ -79,12 +79,14 @@ std::string canonical_request(const Request& r) {
   return o + "\n\n" + r.signed_headers + "\n" + r.payload_hash;
 }
 
-std::string sha256_hex(const std::string& data) {
+std::string sha256_hex(const void* data, size_t len) {
   unsigned char out[EVP_MAX_MD_SIZE];
   unsigned int n = 0;
-  EVP_Digest(data.data(), data.size(), out, &n, EVP_sha256(), nullptr);
+  EVP_Digest(data, len, out, &n, EVP_sha256(), nullptr);
   return hex(out, n);
 }
+
+std::string sha256_hex(const std::string& data) { return sha256_hex(data.data(), data.size()); }
 
 std::string string_to_sign(const std::string& timestamp, const std::string& scope, const std::string& creq) {
   return "AWS4-HMAC-SHA256\n" + timestamp + "\n" + scope + "\n" + sha256_hex(creq);
@@ -103,8 +105,21 @@ std::string signature(const std::string& key, const std::string& sts) {
 bool verify(const Request& r, const std::string& timestamp, const std::string& scope, const std::string& key,
             const std::string& sig, std::string* creq) {
   *creq = canonical_request(r);
-  std::string expected = signature(key, string_to_sign(timestamp, scope, *creq));
+  return same_signature(signature(key, string_to_sign(timestamp, scope, *creq)), sig);
+}
+
+bool same_signature(const std::string& expected, const std::string& sig) {
   return expected.size() == sig.size() && CRYPTO_memcmp(expected.data(), sig.data(), sig.size()) == 0;
+}
+
+bool ChunkChain::verify(const void* chunk, size_t n, const std::string& sig) {
+  static const char kEmpty[] = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855";
+  const std::string sts =
+      "AWS4-HMAC-SHA256-PAYLOAD\n" + timestamp + "\n" + scope + "\n" + prev + "\n" + kEmpty + "\n" + sha256_hex(chunk, n);
+  std::string expected = signature(key, sts);
+  if (!same_signature(expected, sig)) return false;
+  prev = std::move(expected);
+  return true;
 }
 
 }  // namespace dfs::sigv4

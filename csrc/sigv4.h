@@ -23,6 +23,7 @@ struct Request {
 
 std::string canonical_request(const Request& r);
 std::string sha256_hex(const std::string& data);
+std::string sha256_hex(const void* data, size_t n);
 std::string string_to_sign(const std::string& timestamp, const std::string& scope, const std::string& creq);
 std::string signing_key(const std::string& secret, const std::string& date, const std::string& region,
                         const std::string& service);  // 32 raw bytes
@@ -31,5 +32,16 @@ std::string signature(const std::string& key, const std::string& sts);  // lower
 // canonical request (for the SignatureDoesNotMatch diagnostics).
 bool verify(const Request& r, const std::string& timestamp, const std::string& scope, const std::string& key,
             const std::string& sig, std::string* creq);
+// Constant-time equality of two lower-case hex signatures.
+bool same_signature(const std::string& expected, const std::string& sig);
+
+// The per-chunk signature chain of a STREAMING-AWS4-HMAC-SHA256-PAYLOAD body (aws-chunked;
+// reference auth_middleware.rs streaming payloads): every chunk's signature signs the previous
+// one and the chunk's SHA-256, starting from the request's own (seed) signature.
+struct ChunkChain {
+  std::string key, timestamp, scope, prev;
+  // True (and the chain advanced) when `sig` is the expected signature of this chunk.
+  bool verify(const void* chunk, size_t n, const std::string& sig);
+};
 
 }  // namespace dfs::sigv4

@@ -250,6 +250,7 @@ def decode_chunked(body: bytes, verifier: ChunkVerifier | None = None) -> bytes:
     pos = 0
     n = len(body)
     mv = memoryview(body)
+    final = False
     while pos < n:
         eol = body.find(b"\r\n", pos)
         if eol < 0:
@@ -269,9 +270,12 @@ def decode_chunked(body: bytes, verifier: ChunkVerifier | None = None) -> bytes:
             if not verifier.verify_chunk(bytes(chunk), sig):
                 raise ChunkedDecodeError("chunk signature mismatch")
         if size == 0:
+            final = True
             break
         out += chunk
         pos += size + 2
+    if verifier is not None and not final:  # a signed stream ends with its signed empty chunk
+        raise ChunkedDecodeError("chunk signature chain ends early")
     return bytes(out)
 
 
