@@ -312,7 +312,8 @@ def _cs_counters(cluster) -> dict:
 
 def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mpu_key: str = "big.bin",
                       cluster=None) -> dict:
-    """PUT / GET / Range GET 64 KiB / ListObjectsV2 / multipart upload / multipart GET against
+    """PUT / GET / Range GET 64 KiB / ListObjectsV2 / the S3A operations (HEAD, CopyObject,
+    DeleteObjects, rename, aws-chunked PUT) / multipart upload / multipart GET against
     the gateway from the native load generator (build/native/s3_load: C++ HTTP/1.1 clients,
     one keep-alive connection per thread), so the numbers describe the gateway, not Python's
     HTTP stack. Every phase runs for --phase-seconds (>= 10 s windows). With
@@ -336,6 +337,15 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
               ("range_get_64k", ["--op", "range", "--keys", str(n), "--size", str(a.size), "--prefix", "nat",
                                  "--verify"]),
               ("list_v2", ["--op", "list", "--prefix", "nat_00"]),
+              # the S3A shape (Hadoop S3AFileSystem): getFileStatus HEADs, rename = CopyObject +
+              # DELETE, directory delete = DeleteObjects pages, SDK PUTs as aws-chunked bodies
+              ("head", ["--op", "head", "--keys", str(n), "--prefix", "nat"]),
+              ("copy", ["--op", "copy", "--keys", str(n), "--size", str(a.size), "--prefix", "nat",
+                        "--count", str(n), "--seconds", "0"]),
+              ("multi_delete_100", ["--op", "multidelete", "--keys", str(n), "--prefix", "nat", "--batch", "100",
+                                    "--count", str(max(1, n // 100)), "--seconds", "0"]),
+              ("rename", ["--op", "rename", "--keys", str(n), "--size", str(a.size), "--prefix", "nat"]),
+              ("chunked_put", ["--op", "chunked", "--keys", str(n), "--size", str(a.size), "--prefix", "natc"]),
               ("multipart_upload", ["--op", "mpu", "--size", str(a.mpu_object_mb << 20), "--parts", str(a.mpu_parts),
                                     "--prefix", "natmpu", "--keys", "1"]),
               ("multipart_get", ["--op", "get", "--size", str(mpu_bytes), "--key", mpu_key, "--keys", "1"]))
@@ -455,7 +465,8 @@ def config5_secure(a):
                 "Effect": "Allow", "Action": "sts:AssumeRoleWithWebIdentity",
                 "Condition": {"ForAnyValue:StringEquals": {"OIDC_ISSUER:groups": ["bench"]}}}]},
             "Policies": [{"PolicyName": "bench", "PolicyDocument": {"Statement": [
-                {"Effect": "Allow", "Action": ["s3:GetObject", "s3:PutObject", "s3:ListBucket", "s3:HeadObject"],
+                {"Effect": "Allow", "Action": ["s3:GetObject", "s3:PutObject", "s3:ListBucket", "s3:HeadObject",
+                                               "s3:DeleteObject"],
                  "Resource": ["arn:dfs:s3:::bench", "arn:dfs:s3:::bench/*"]}]}}]}]}))
         env = {"LOCAL_CHUNKSERVER": c.cs_addrs[0], "TLS_CERT": crt, "TLS_KEY": key, "S3_REQUIRE_TLS": "true",
                "S3_AUTH_ENABLED": "true", "S3_ACCESS_KEY": "admin", "S3_SECRET_KEY": "admin-secret",

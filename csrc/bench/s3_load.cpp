@@ -3,9 +3,10 @@
 // load generator in bench_configs.py, without an interpreter on the client side, so the
 // numbers describe the gateway rather than the client.
 //
-//   s3_load --host 127.0.0.1 --port 9000 --op put|get|range|list|mpu --bucket b --prefix p
+//   s3_load --host 127.0.0.1 --port 9000 --op put|get|range|list|mpu|head|copy|rename|delete|
+//                                              multidelete|chunked --bucket b --prefix p
 //           [--key k] [--count N | --seconds S] --size BYTES --conc C [--range-size 65536]
-//           [--verify] [--keys K] [--parts P]
+//           [--verify] [--keys K] [--parts P] [--batch 100] [--chunk 65536]
 //           [--tls] [--ak AK --sk SK [--token SESSION_TOKEN] [--region R]] [--sse]
 //
 // --seconds runs every thread for that long (keys cycle) instead of a fixed request count.
@@ -13,7 +14,14 @@
 // benchmark client). --ak/--sk sign every request with SigV4 (UNSIGNED-PAYLOAD, as the AWS
 // SDKs do over TLS), with the STS session token when given; --sse asks for SSE-S3 on PUT.
 // list: ListObjectsV2 of `--prefix` (req/s); mpu: initiate + P parts + complete per object
-// (MB/s of object bytes). Payload of object i: a xorshift stream seeded by i (`--verify`
+// (MB/s of object bytes). The S3A-shaped operations (Hadoop's S3AFileSystem over the gateway):
+// head: HEAD of key i (getFileStatus); copy: CopyObject key i -> key i.cp; rename: CopyObject
+// key i -> key i.mv then DELETE key i.mv (S3A's rename is copy + delete; the source stays so
+// the phase can cycle); delete: DELETE key i.cp; multidelete: DeleteObjects of --batch keys
+// i.cp (S3A's bulk delete of a directory; keys/s in "keys_per_s"); chunked: PUT with an
+// aws-chunked body of --chunk byte chunks (STREAMING-AWS4-HMAC-SHA256-PAYLOAD with a
+// chunk-signature chain when signing, STREAMING-UNSIGNED-PAYLOAD-TRAILER otherwise — what the
+// AWS SDKs send over plain HTTP). Payload of object i: a xorshift stream seeded by i (`--verify`
 // checks GET bodies against it). Prints one JSON object: ops, seconds, MB/s, req/s, p50/p99
 // latency, errors.
 #include <arpa/inet.h>
@@ -55,7 +63,7 @@ void fill(std::vector<char>& b, uint64_t seed) {
 struct Opts {
   std::string host = "127.0.0.1", op = "get", bucket = "bench", prefix = "nat", fixed_key;
   int port = 9000, conc = 10, parts = 4;
-  uint64_t count = 100, size = 1 << 20, rsize = 65536, keys = 0;
+  uint64_t count = 100, size = 1 << 20, rsize = 65536, keys = 0, batch = 100, chunk = 65536;
   double seconds = 0;
   bool verify = false, tls = false, sse = false;
   std::string ak, sk, token, region = "us-east-1";
@@ -116,7 +124,7 @@ struct Conn {
     return true;
   }
   // Reads one response; returns the status (-1 on error); body into *body (if non-null).
-  int response(std::string* body) {
+  int response(std::string* body, bool no_body = false) {
     size_t end;
     char tmp[1 << 16];
     while ((end = buf.find("\r\n\r\n")) == std::string::npos) {
@@ -138,6 +146,7 @@ struct Conn {
         etag.erase(0, etag.find_first_not_of(' '));
       }
     }
+    if (no_body || status == 204) clen = 0;  // HEAD, 204: no body follows the head
     std::string sink;
     std::string* out = body ? body : &sink;
     out->resize(clen);
@@ -160,11 +169,17 @@ struct Signer {
   std::string day, key;
   explicit Signer(const Opts& opts) : o(opts) {}
   std::string headers(const std::string& method, const std::string& path, const std::string& query,
-                      uint64_t content_length, bool sse_header) {
+                      uint64_t content_length, bool sse_header,
+                      const std::vector<std::pair<std::string, std::string>>& extra = {},
+                      const std::string& payload = "UNSIGNED-PAYLOAD", dfs::sigv4::ChunkChain* seed = nullptr) {
     std::string h = "Host: " + o.host + ":" + std::to_string(o.port) + "\r\n";
     if (sse_header) h += "x-amz-server-side-encryption: AES256\r\n";
     if (method == "PUT" || method == "POST") h += "Content-Length: " + std::to_string(content_length) + "\r\n";
-    if (o.ak.empty()) return h;
+    for (auto& kv : extra) h += kv.first + ": " + kv.second + "\r\n";
+    if (o.ak.empty()) {
+      if (payload != "UNSIGNED-PAYLOAD") h += "x-amz-content-sha256: " + payload + "\r\n";
+      return h;
+    }
     char amz[32], date[16];
     std::time_t now = std::time(nullptr);
     std::tm t;
@@ -184,18 +199,20 @@ struct Signer {
     r.method = method;
     r.path = path;
     r.query = query;
-    r.payload_hash = "UNSIGNED-PAYLOAD";
+    r.payload_hash = payload;
     r.headers.emplace_back("host", o.host + ":" + std::to_string(o.port));
-    r.headers.emplace_back("x-amz-content-sha256", "UNSIGNED-PAYLOAD");
+    r.headers.emplace_back("x-amz-content-sha256", payload);
     r.headers.emplace_back("x-amz-date", amz);
     if (!o.token.empty()) r.headers.emplace_back("x-amz-security-token", o.token);
     if (sse_header) r.headers.emplace_back("x-amz-server-side-encryption", "AES256");
+    for (auto& kv : extra) r.headers.emplace_back(kv.first, kv.second);
     std::sort(r.headers.begin(), r.headers.end());
     for (auto& kv : r.headers) r.signed_headers += (r.signed_headers.empty() ? "" : ";") + kv.first;
     const std::string scope = std::string(date) + "/" + o.region + "/s3/aws4_request";
     const std::string sig =
         dfs::sigv4::signature(k, dfs::sigv4::string_to_sign(amz, scope, dfs::sigv4::canonical_request(r)));
-    h += "x-amz-content-sha256: UNSIGNED-PAYLOAD\r\nx-amz-date: " + std::string(amz) + "\r\n";
+    if (seed) *seed = dfs::sigv4::ChunkChain{k, amz, scope, sig};  // what an aws-chunked body continues
+    h += "x-amz-content-sha256: " + payload + "\r\nx-amz-date: " + std::string(amz) + "\r\n";
     if (!o.token.empty()) h += "x-amz-security-token: " + o.token + "\r\n";
     h += "Authorization: AWS4-HMAC-SHA256 Credential=" + o.ak + "/" + scope + ", SignedHeaders=" + r.signed_headers +
          ", Signature=" + sig + "\r\n";
@@ -232,6 +249,8 @@ int main(int argc, char** argv) {
     else if (a == "--verify") o.verify = true;
     else if (a == "--keys") o.keys = std::strtoull(nxt().c_str(), nullptr, 10);  // request i -> key i % keys
     else if (a == "--parts") o.parts = std::max(1, std::atoi(nxt().c_str()));
+    else if (a == "--batch") o.batch = std::max<uint64_t>(1, std::strtoull(nxt().c_str(), nullptr, 10));
+    else if (a == "--chunk") o.chunk = std::max<uint64_t>(1, std::strtoull(nxt().c_str(), nullptr, 10));
     else if (a == "--tls") o.tls = true;
     else if (a == "--sse") o.sse = true;
     else if (a == "--ak") o.ak = nxt();
@@ -250,7 +269,7 @@ int main(int argc, char** argv) {
   // client ~0.5 ms, which would be measured as gateway latency. Falls back to per-request
   // generation when the key set is too large to hold.
   std::vector<std::vector<char>> cache;
-  const bool need = o.op == "put" || o.op == "mpu" || (o.verify && o.fixed_key.empty());
+  const bool need = o.op == "put" || o.op == "chunked" || o.op == "mpu" || (o.verify && o.fixed_key.empty());
   const uint64_t ncache = o.op == "mpu" ? 1 : o.keys;
   if (need && ncache * o.size <= (4ull << 30)) {
     cache.resize(ncache);
@@ -260,7 +279,7 @@ int main(int argc, char** argv) {
     }
   }
   std::vector<std::vector<double>> lat(o.conc);
-  std::atomic<uint64_t> errors{0}, bytes{0};
+  std::atomic<uint64_t> errors{0}, bytes{0}, keys_deleted{0};
   std::mutex err_mu;
   std::string first_error;
   auto note_error = [&](const std::string& e) {
@@ -297,6 +316,78 @@ int main(int argc, char** argv) {
           std::string req = "PUT " + path + " HTTP/1.1\r\n" + signer.headers("PUT", path, "", o.size, o.sse) + "\r\n";
           st = c.send_all(req.data(), req.size()) && c.send_all(src, o.size) ? c.response(&body) : -1;
           if (st == 200) bytes += o.size;
+        } else if (o.op == "chunked") {
+          // aws-chunked body: <hex>[;chunk-signature=<64 hex>]\r\n<data>\r\n ... 0[;sig]\r\n\r\n
+          const char* src = payload.data();
+          if (!cache.empty()) src = cache[i % o.keys].data();
+          else fill(payload, i % o.keys);
+          const bool sign = !o.ak.empty();
+          const size_t sig_len = sign ? 17 + 64 : 0;  // ";chunk-signature=" + signature
+          uint64_t enc = 1 + sig_len + 4;             // the final empty chunk and the closing CRLF
+          char hx[24];
+          for (uint64_t off = 0; off < o.size; off += o.chunk) {
+            const uint64_t len = std::min<uint64_t>(o.chunk, o.size - off);
+            enc += static_cast<uint64_t>(std::snprintf(hx, sizeof hx, "%llx", static_cast<unsigned long long>(len))) +
+                   sig_len + 2 + len + 2;
+          }
+          dfs::sigv4::ChunkChain chain;
+          std::string req = "PUT " + path + " HTTP/1.1\r\n" +
+                            signer.headers("PUT", path, "", enc, false,
+                                           {{"content-encoding", "aws-chunked"},
+                                            {"x-amz-decoded-content-length", std::to_string(o.size)}},
+                                           sign ? "STREAMING-AWS4-HMAC-SHA256-PAYLOAD" : "STREAMING-UNSIGNED-PAYLOAD-TRAILER",
+                                           &chain) +
+                            "\r\n";
+          std::string b;
+          b.reserve(enc);
+          auto piece = [&](const char* p, uint64_t len) {
+            std::snprintf(hx, sizeof hx, "%llx", static_cast<unsigned long long>(len));
+            b += hx;
+            if (sign) b += ";chunk-signature=" + chain.next(p, len);
+            b += "\r\n";
+            b.append(p, len);
+            b += "\r\n";
+          };
+          for (uint64_t off = 0; off < o.size; off += o.chunk) piece(src + off, std::min<uint64_t>(o.chunk, o.size - off));
+          piece(src, 0);
+          st = b.size() == enc && c.send_all(req.data(), req.size()) && c.send_all(b.data(), b.size()) ? c.response(&body) : -1;
+          if (st == 200) bytes += o.size;
+        } else if (o.op == "head") {
+          std::string req = "HEAD " + path + " HTTP/1.1\r\n" + signer.headers("HEAD", path, "", 0, false) + "\r\n";
+          st = c.send_all(req.data(), req.size()) ? c.response(&body, true) : -1;
+        } else if (o.op == "copy" || o.op == "rename") {
+          const std::string dst = path + (o.op == "copy" ? ".cp" : ".mv");
+          std::string req = "PUT " + dst + " HTTP/1.1\r\n" +
+                            signer.headers("PUT", dst, "", 0, false, {{"x-amz-copy-source", path}}) + "\r\n";
+          st = c.send_all(req.data(), req.size()) ? c.response(&body) : -1;
+          if (st == 200 && body.find("<CopyObjectResult") == std::string::npos) st = -5;
+          if (st == 200 && o.op == "rename") {  // S3A rename: the copy, then the delete
+            req = "DELETE " + dst + " HTTP/1.1\r\n" + signer.headers("DELETE", dst, "", 0, false) + "\r\n";
+            st = c.send_all(req.data(), req.size()) ? c.response(&body) : -1;
+            if (st == 204) st = 200;
+          }
+          if (st == 200) bytes += o.size;
+        } else if (o.op == "delete") {
+          const std::string dst = path + ".cp";
+          std::string req = "DELETE " + dst + " HTTP/1.1\r\n" + signer.headers("DELETE", dst, "", 0, false) + "\r\n";
+          st = c.send_all(req.data(), req.size()) ? c.response(&body) : -1;
+          if (st == 204) st = 200;
+        } else if (o.op == "multidelete") {
+          std::string xml = "<Delete><Quiet>true</Quiet>";
+          for (uint64_t j = 0; j < o.batch; ++j) {
+            char k2[96];
+            std::snprintf(k2, sizeof k2, "%s_%05llu.cp", o.prefix.c_str(),
+                          static_cast<unsigned long long>((i * o.batch + j) % o.keys));
+            xml += std::string("<Object><Key>") + k2 + "</Key></Object>";
+          }
+          xml += "</Delete>";
+          const std::string bp = "/" + o.bucket;
+          std::string req = "POST " + bp + "?delete= HTTP/1.1\r\n" +
+                            signer.headers("POST", bp, "delete=", xml.size(), false) + "\r\n";
+          st = c.send_all(req.data(), req.size()) && c.send_all(xml.data(), xml.size()) ? c.response(&body) : -1;
+          if (st == 200 && body.find("<DeleteResult") == std::string::npos) st = -6;
+          if (st == 200 && body.find("<Error>") != std::string::npos) st = -7;
+          if (st == 200) keys_deleted += o.batch;
         } else if (o.op == "list") {
           const std::string q = "list-type=2&max-keys=1000&prefix=" + dfs::sigv4::uri_encode(o.prefix, true);
           std::string req = "GET /" + o.bucket + "?" + q + " HTTP/1.1\r\n" + signer.headers("GET", "/" + o.bucket, q, 0, false) +
@@ -358,7 +449,7 @@ int main(int argc, char** argv) {
         }
         if (st != 200 && st != 206) note_error(o.op + " " + key + ": status " + std::to_string(st) + " " + body.substr(0, 200));
         lat[t].push_back(std::chrono::duration<double>(Clock::now() - s0).count());
-        if (st < 0 && st != -2 && st != -3 && st != -4) {  // connection state unknown: reconnect
+        if (st < 0 && (st > -2 || st < -7)) {  // connection state unknown: reconnect
           c.close();
           c.buf.clear();
           if (!c.open(o)) break;
@@ -375,9 +466,10 @@ int main(int argc, char** argv) {
   std::string fe;
   for (char ch : first_error) fe += (ch == '"' || ch == '\\') ? '\'' : (ch < 32 ? ' ' : ch);
   std::printf("{\"op\": \"%s\", \"ops\": %zu, \"seconds\": %.4f, \"mb_per_s\": %.1f, \"req_per_s\": %.1f, "
-              "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"errors\": %llu, \"concurrency\": %d, \"size\": %llu, "
+              "\"p50_ms\": %.3f, \"p99_ms\": %.3f, \"keys_per_s\": %.1f, \"errors\": %llu, \"concurrency\": %d, \"size\": %llu, "
               "\"tls\": %s, \"signed\": %s, \"session\": %s, \"sse\": %s, \"first_error\": \"%s\"}\n",
               o.op.c_str(), all.size(), secs, bytes.load() / 1048576.0 / secs, all.size() / secs, pct(0.5), pct(0.99),
+              keys_deleted.load() / secs,
               static_cast<unsigned long long>(errors.load()), o.conc, static_cast<unsigned long long>(o.size),
               o.tls ? "true" : "false", o.ak.empty() ? "false" : "true", o.token.empty() ? "false" : "true",
               o.sse ? "true" : "false", fe.c_str());

@@ -112,14 +112,24 @@ bool same_signature(const std::string& expected, const std::string& sig) {
   return expected.size() == sig.size() && CRYPTO_memcmp(expected.data(), sig.data(), sig.size()) == 0;
 }
 
-bool ChunkChain::verify(const void* chunk, size_t n, const std::string& sig) {
+namespace {
+std::string chunk_signature(const ChunkChain& c, const void* chunk, size_t n) {
   static const char kEmpty[] = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855";
-  const std::string sts =
-      "AWS4-HMAC-SHA256-PAYLOAD\n" + timestamp + "\n" + scope + "\n" + prev + "\n" + kEmpty + "\n" + sha256_hex(chunk, n);
-  std::string expected = signature(key, sts);
+  return signature(c.key, "AWS4-HMAC-SHA256-PAYLOAD\n" + c.timestamp + "\n" + c.scope + "\n" + c.prev + "\n" +
+                              kEmpty + "\n" + sha256_hex(chunk, n));
+}
+}  // namespace
+
+bool ChunkChain::verify(const void* chunk, size_t n, const std::string& sig) {
+  std::string expected = chunk_signature(*this, chunk, n);
   if (!same_signature(expected, sig)) return false;
   prev = std::move(expected);
   return true;
+}
+
+std::string ChunkChain::next(const void* chunk, size_t n) {
+  prev = chunk_signature(*this, chunk, n);
+  return prev;
 }
 
 }  // namespace dfs::sigv4

@@ -42,6 +42,8 @@ struct ChunkChain {
   std::string key, timestamp, scope, prev;
   // True (and the chain advanced) when `sig` is the expected signature of this chunk.
   bool verify(const void* chunk, size_t n, const std::string& sig);
+  // The client side: this chunk's signature (the chain advanced to it).
+  std::string next(const void* chunk, size_t n);
 };
 
 }  // namespace dfs::sigv4
