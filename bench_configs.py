@@ -235,7 +235,13 @@ def config5(a):
         out["multipart"] = {"parts": nparts, "part_size": part, "upload_mb_per_s": round(len(blob) / (1 << 20) / mpu_s, 1),
                             "get_mb_per_s": round(len(blob) / (1 << 20) / mpu_get_s, 1)}
         lg.close()
+        f0 = _front_counters(url)
         out["parquet_over_s3"] = parquet_phase(url, a)
+        f1 = _front_counters(url)
+        # what pyarrow's S3 client (the AWS C++ SDK, as S3A's) sent that the native front handed over
+        pr = {k: v - f0["reasons"].get(k, 0) for k, v in f1["reasons"].items() if k != "metrics"}
+        out["parquet_over_s3"]["front_requests"] = f1["requests"] - f0["requests"]
+        out["parquet_over_s3"]["front_handoff_reasons"] = {k: v for k, v in pr.items() if v}
         out["native_load"] = native_load_phase(url, a, len(blob), cluster=c)
         out["load_generator"] = f"{a.concurrency} client processes (requests, keep-alive)"
         out["gateway_workers"] = int(os.environ.get("S3_WORKERS", "4"))
@@ -366,13 +372,9 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
         res["chunkserver"] = {k: v - cs0.get(k, 0) for k, v in _cs_counters(cluster).items()}
         after = _front_counters(url)
         res["front_requests"] = after["requests"] - before["requests"]
-        # the closing /metrics scrape is itself one hand-off (answered by Python; its reason is
-        # "auth" on an authenticating gateway, "list-empty" on an open one): not counted
-        reasons = {k: v - before["reasons"].get(k, 0) for k, v in after["reasons"].items()}
-        for why in ("auth", "list-empty"):
-            if reasons.get(why, 0) > 0:
-                reasons[why] -= 1
-                break
+        # the /metrics scrapes around the phase are answered by the Python workers (their
+        # registry plus the front's counters): reason "metrics", not counted as a hand-off
+        reasons = {k: v - before["reasons"].get(k, 0) for k, v in after["reasons"].items() if k != "metrics"}
         res["front_handoffs"] = sum(reasons.values())
         res["front_handoff_reasons"] = {k: v for k, v in reasons.items() if v}
         out[name] = res

@@ -946,6 +946,7 @@ void bind_meta(py::module_& m) {
         d["chunk_sigs"] = s.chunk_sigs;
         d["chunk_sig_failures"] = s.chunk_sig_failures;
         d["presigned"] = s.presigned;
+        d["bucket_ops"] = s.bucket_ops;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;
         return d;

@@ -880,6 +880,7 @@ bool S3Front::handle(Conn* c, Req& r) {
   const bool plain_path = r.raw_path.size() > 1 && r.raw_path[0] == '/' &&
                           r.raw_path.find('%') == std::string::npos;
   std::map<std::string, std::string> q;
+  if (r.raw_path == "/metrics" || r.raw_path == "/health") return proxy(c, r, nullptr, 0, "metrics");
   if (!fc_ || !plain_path || !decode_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
   // a presigned URL's authentication parameters are not part of the operation
   for (auto it = q.begin(); it != q.end();) {
@@ -902,6 +903,8 @@ bool S3Front::handle(Conn* c, Req& r) {
       return native_list(c, r, bucket, q);
     }
     if (r.method == "POST" && q.size() == 1 && q.count("delete")) return native_delete_objects(c, r, bucket, q);
+    if ((r.method == "PUT" || r.method == "HEAD") && q.empty() && !r.chunked && r.content_length <= (64 << 10))
+      return native_bucket(c, r, bucket, q);
     return proxy(c, r, nullptr, 0, "route");
   }
   if (slash == std::string::npos || slash == 0 || slash + 1 >= p.size()) return proxy(c, r, nullptr, 0, "route");
@@ -927,13 +930,15 @@ bool S3Front::handle(Conn* c, Req& r) {
   if (cfg_.sse_enabled && cfg_.sse_kek.size() != 32) return proxy(c, r, nullptr, 0, "sse");
   const std::string* copy_src = is_put ? r.get("x-amz-copy-source") : nullptr;
   if (is_put) {
-    if (r.chunked || cfg_.metadata_sidecar || (copy_src && (part || r.content_length > 0)))
+    const bool aws = aws_chunked(r);
+    const std::string* dl = aws ? r.get("x-amz-decoded-content-length") : nullptr;
+    const bool sized = dl && all_digits(*dl);
+    // Transfer-Encoding: chunked is served for aws-chunked bodies of a stated size (the SDKs'
+    // streaming uploads); a plain chunked body of unknown size goes to Python
+    if ((r.chunked && !(aws && sized)) || cfg_.metadata_sidecar || (copy_src && (part || r.content_length > 0 || r.chunked)))
       return proxy(c, r, nullptr, 0, "put-form");
     uint64_t body = static_cast<uint64_t>(r.content_length);
-    if (aws_chunked(r)) {  // the decoded size, when the client says it (it always does)
-      const std::string* dl = r.get("x-amz-decoded-content-length");
-      if (dl && all_digits(*dl)) body = std::min<uint64_t>(body, std::stoull(*dl));
-    }
+    if (sized) body = r.chunked ? std::stoull(*dl) : std::min<uint64_t>(body, std::stoull(*dl));
     if (body + (cfg_.sse_enabled ? 28 : 0) > fc_->slot_bytes()) return proxy(c, r, nullptr, 0, "large");
   } else if (r.content_length > 0 || r.chunked) {
     return proxy(c, r, nullptr, 0, "body");
@@ -1432,11 +1437,11 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
     if (fc_->stat(marker, &found, &meta, &msg, r.rid) != FastClient::Ok || !found)
       return proxy(c, r, nullptr, 0, "no-upload");
   }
-  uint64_t n = static_cast<uint64_t>(r.content_length);
+  uint64_t n = static_cast<uint64_t>(std::max<int64_t>(r.content_length, 0));
   const bool aws = aws_chunked(r);
   if (aws) {  // decoded into the slot below; its size bounded by what the client announced
     const std::string* dl = r.get("x-amz-decoded-content-length");
-    if (dl && all_digits(*dl)) n = std::min<uint64_t>(n, std::stoull(*dl));
+    if (dl && all_digits(*dl)) n = r.chunked ? std::stoull(*dl) : std::min<uint64_t>(n, std::stoull(*dl));
   }
   const bool sse = cfg_.sse_enabled && !part;  // handle() sent SSE parts to Python
   int64_t slot = fc_->acquire_slot(std::max<uint64_t>(sse ? n + 28 : n, 1));  // [nonce 12][ciphertext n][tag 16]
@@ -1563,11 +1568,38 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   if (fc_->stat(path, &found, &meta, &msg, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "stat");
   const auto t1 = SC::now();
   if (!found) {
-    if (head) return proxy(c, r, nullptr, 0, "head-missing");
+    // a completed multipart object, a "directory" probe, or NoSuchKey (s3/server.py
+    // get_object / head_object)
     std::string mm;
-    if (fc_->stat(path + "/.s3_mpu_completed", &found, &mm, &msg, r.rid) != FastClient::Ok || !found)
-      return proxy(c, r, nullptr, 0, "missing");
-    return native_mpu_get(c, r, path, mm);
+    if (fc_->stat(path + "/.s3_mpu_completed", &found, &mm, &msg, r.rid) != FastClient::Ok)
+      return proxy(c, r, nullptr, 0, "stat");
+    if (found && !head) return native_mpu_get(c, r, path, mm);
+    if (found) {
+      pb::FileMetadata mk;
+      std::string hdrs;
+      if (!mk.decode(mm) || !object_headers(nullptr, mk.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
+      const size_t lm = hdrs.find("Last-Modified: ");
+      hdrs.replace(lm, hdrs.find("\r\n", lm) - lm,
+                   "Last-Modified: " + http_date(static_cast<uint64_t>(now_s() * 1000)));  // formatdate(): now
+      auto sz = mk.attributes.find("x-dfs-mpu-size");
+      const std::string size = sz != mk.attributes.end() && all_digits(sz->second) ? sz->second : "0";
+      std::string h = "HTTP/1.1 200 OK\r\n" + hdrs + "Content-Length: " + size + "\r\n" +
+                      (r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+      r.status = 200;
+      count(r, 200);
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.heads++;
+      }
+      return send_all(c->io(), h.data(), h.size());
+    }
+    if (!head) return s3_error(c, r, 404, "NoSuchKey", "The specified key does not exist.", path);
+    if (path.back() == '/') {  // a "directory" marker probe: 200 when anything lives under it
+      std::vector<std::pair<std::string, pb::FileMetadata>> under;
+      if (fc_->list(path, &under, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "list");
+      if (!under.empty()) return respond(c, r, 200, "", "Content-Length: 0\r\n");
+    }
+    return respond(c, r, 404, "", "Content-Length: 0\r\n");
   }
   pb::FileMetadata m;
   if (!m.decode(meta)) return proxy(c, r, nullptr, 0, "decode");
@@ -2086,10 +2118,12 @@ bool S3Front::native_mpu_get(Conn* c, Req& r, const std::string& path, const std
 // ---------------------------------------------------------------- delete, copy, aws-chunked
 bool S3Front::respond(Conn* c, Req& r, int status, const std::string& xml, const std::string& extra) {
   const char* reason = status == 200 ? "OK" : status == 204 ? "No Content" : status == 400 ? "Bad Request"
-                       : status == 403 ? "Forbidden" : status == 404 ? "Not Found" : "Internal Server Error";
+                       : status == 403 ? "Forbidden" : status == 404 ? "Not Found" : status == 409 ? "Conflict"
+                       : "Internal Server Error";
   std::string h = "HTTP/1.1 " + std::to_string(status) + " " + reason + "\r\n" + extra;
   if (!xml.empty()) h += "Content-Type: application/xml\r\n";
-  if (status != 204) h += "Content-Length: " + std::to_string(xml.size()) + "\r\n";
+  if (status != 204 && extra.find("Content-Length:") == std::string::npos)
+    h += "Content-Length: " + std::to_string(xml.size()) + "\r\n";
   h += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
   r.status = status;
   count(r, status);
@@ -2104,63 +2138,181 @@ bool S3Front::s3_error(Conn* c, Req& r, int status, const std::string& code, con
                      "<RequestId></RequestId></Error>");
 }
 
+namespace {
+
+// The request body as a byte stream: Content-Length framed, or in the HTTP/1.1 chunked transfer
+// coding — what the AWS SDKs send for streaming uploads (Transfer-Encoding: chunked around an
+// aws-chunked payload, x-amz-decoded-content-length giving the object size). Reads go through
+// the connection buffer, then straight from the socket into the destination.
+class BodyIn {
+ public:
+  BodyIn(S3Front::Conn* c, bool chunked, uint64_t content_length, Io io)
+      : c_(c), io_(io), chunked_(chunked), left_(chunked ? 0 : content_length) {}
+  // Exactly n bytes of the body into dst: 1 ok, 0 connection error, -1 the body ends first.
+  int read(uint8_t* dst, uint64_t n) {
+    while (n) {
+      uint64_t a;
+      int rc = avail(&a);
+      if (rc != 1) return rc == 2 ? -1 : rc;
+      uint64_t k = std::min(a, n), have = std::min<uint64_t>(k, buf_left());
+      if (have) {
+        std::memcpy(dst, c_->buf.data() + c_->pos, have);
+        c_->pos += have;
+      } else {
+        long g = io_recv(io_, dst, k);
+        if (g <= 0) return 0;
+        have = static_cast<uint64_t>(g);
+      }
+      dst += have;
+      n -= have;
+      left_ -= have;
+    }
+    return 1;
+  }
+  // One CRLF-terminated line of the body (at most `max` bytes), without the CRLF.
+  int line(std::string* out, size_t max) {
+    out->clear();
+    for (;;) {
+      uint64_t a;
+      int rc = avail(&a);
+      if (rc != 1) return rc == 2 ? -1 : rc;
+      if (!buf_left() && !fill()) return 0;
+      const size_t lim = static_cast<size_t>(std::min<uint64_t>(a, buf_left()));
+      const char* p = c_->buf.data() + c_->pos;
+      const char* nl = static_cast<const char*>(std::memchr(p, '\n', lim));
+      const size_t take = nl ? static_cast<size_t>(nl - p) + 1 : lim;
+      out->append(p, take);
+      c_->pos += take;
+      left_ -= take;
+      if (out->size() > max + 2) return -1;
+      if (nl) {
+        if (out->size() < 2 || (*out)[out->size() - 2] != '\r') return -1;
+        out->resize(out->size() - 2);
+        return 1;
+      }
+    }
+  }
+  // The rest of the body, discarded: 1 at its end, 0 connection error, -1 bad framing.
+  int drain() {
+    for (;;) {
+      uint64_t a;
+      int rc = avail(&a);
+      if (rc == 2) return 1;
+      if (rc != 1) return rc;
+      if (!buf_left() && !fill()) return 0;
+      const uint64_t k = std::min<uint64_t>(a, buf_left());
+      c_->pos += k;
+      left_ -= k;
+    }
+  }
+
+ private:
+  uint64_t buf_left() const { return c_->buf.size() - c_->pos; }
+  bool fill() {
+    char tmp[16 << 10];
+    c_->buf.erase(0, c_->pos);
+    c_->pos = 0;
+    long k = io_recv(io_, tmp, sizeof tmp);
+    if (k <= 0) return false;
+    c_->buf.append(tmp, static_cast<size_t>(k));
+    return true;
+  }
+  // A CRLF line of the HTTP framing itself (chunk sizes, trailers).
+  int raw_line(std::string* out, size_t max) {
+    for (;;) {
+      size_t e = c_->buf.find("\r\n", c_->pos);
+      if (e != std::string::npos) {
+        if (e - c_->pos > max) return -1;
+        out->assign(c_->buf, c_->pos, e - c_->pos);
+        c_->pos = e + 2;
+        return 1;
+      }
+      if (buf_left() > max + 1) return -1;
+      char tmp[4096];
+      long k = io_recv(io_, tmp, sizeof tmp);
+      if (k <= 0) return 0;
+      c_->buf.append(tmp, static_cast<size_t>(k));
+    }
+  }
+  // 1: *n > 0 body bytes are next; 2: the body has ended; 0 connection error; -1 bad framing.
+  int avail(uint64_t* n) {
+    if (!chunked_) {
+      if (!left_) return 2;
+      *n = left_;
+      return 1;
+    }
+    while (!left_) {
+      if (eof_) return 2;
+      std::string h;
+      int rc;
+      if (need_crlf_) {  // the CRLF after the previous chunk's data
+        if ((rc = raw_line(&h, 0)) != 1) return rc;
+        need_crlf_ = false;
+      }
+      if ((rc = raw_line(&h, 1024)) != 1) return rc;
+      const std::string hex = trim(h.substr(0, h.find(';')));
+      if (hex.empty() || hex.size() > 15 || hex.find_first_not_of("0123456789abcdefABCDEF") != std::string::npos)
+        return -1;
+      left_ = std::stoull(hex, nullptr, 16);
+      if (!left_) {  // the last chunk: trailers up to the empty line
+        for (;;) {
+          if ((rc = raw_line(&h, 8192)) != 1) return rc;
+          if (h.empty()) break;
+        }
+        eof_ = true;
+        return 2;
+      }
+      need_crlf_ = true;
+    }
+    *n = left_;
+    return 1;
+  }
+
+  S3Front::Conn* c_;
+  Io io_;
+  bool chunked_, eof_ = false, need_crlf_ = false;
+  uint64_t left_;
+};
+
+}  // namespace
+
 // aws-chunked framing, `<hex>[;chunk-signature=<sig>]\r\n<data>\r\n ... 0[;...]\r\n[trailers]`
 // (s3/auth/sigv4.py decode_chunked, reference auth_middleware.rs streaming payloads), read
-// straight from the connection: chunk headers through the connection buffer, chunk data into
+// straight from the connection — Content-Length framed, or inside HTTP chunked transfer
+// coding as the SDKs send it: chunk headers through the connection buffer, chunk data into
 // the slot. With STREAMING-AWS4-HMAC-SHA256-PAYLOAD on an authenticated gateway every chunk,
 // the final empty one included, must continue the request signature's chain.
 int S3Front::read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint64_t* n_out) {
-  const uint64_t total = static_cast<uint64_t>(std::max<int64_t>(r.content_length, 0));
   const std::string* sha = r.get("x-amz-content-sha256");
   sigv4::ChunkChain* chain =
       cfg_.auth_enabled && r.chain_set && sha && *sha == "STREAMING-AWS4-HMAC-SHA256-PAYLOAD" ? &r.chain : nullptr;
-  uint64_t used = 0, n = 0, sigs = 0;
-  char tmp[16 << 10];
-  auto line = [&](std::string* out) -> int {
-    for (;;) {
-      size_t e = c->buf.find("\r\n", c->pos);
-      if (e != std::string::npos) {
-        const uint64_t k = e + 2 - c->pos;
-        if (used + k > total) return -1;  // the line runs past the body
-        out->assign(c->buf, c->pos, e - c->pos);
-        c->pos = e + 2;
-        used += k;
-        return 1;
-      }
-      const uint64_t have = c->buf.size() - c->pos;
-      if (have > 4096 || used + have >= total) return -1;
-      c->buf.erase(0, c->pos);
-      c->pos = 0;
-      long k = io_recv(c->io(), tmp, sizeof tmp);
-      if (k <= 0) return 0;
-      c->buf.append(tmp, static_cast<size_t>(k));
-    }
-  };
-  auto fail = [&](int rc) {
+  BodyIn in(c, r.chunked, static_cast<uint64_t>(std::max<int64_t>(r.content_length, 0)), c->io());
+  uint64_t n = 0, sigs = 0;
+  auto done = [&](int rc) {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.chunk_sigs += sigs;
     if (rc < 0 && chain) st_.chunk_sig_failures++;
     return rc;
   };
   bool final_chunk = false;
-  while (used < total) {
+  for (;;) {
     std::string h;
-    int rc = line(&h);
-    if (rc <= 0) return fail(rc);
+    int rc = in.line(&h, 4096);
+    if (rc == -1 && !chain && n > 0) break;  // the body ended without its empty chunk (decode_chunked)
+    if (rc != 1) return done(rc);
     const size_t semi = h.find(';');
     const std::string hex = trim(h.substr(0, semi));
-    if (hex.size() > 15 || hex.find_first_not_of("0123456789abcdefABCDEF") != std::string::npos) return fail(-1);
+    if (hex.size() > 15 || hex.find_first_not_of("0123456789abcdefABCDEF") != std::string::npos) return done(-1);
     const uint64_t size = hex.empty() ? 0 : std::stoull(hex, nullptr, 16);
-    if (size > total - used || n + size > cap) return fail(-1);
-    if (!read_body(c, dst + n, size)) return fail(0);
-    used += size;
+    if (n + size > cap) return done(-1);
+    if ((rc = in.read(dst + n, size)) != 1) return done(rc);
     if (chain) {
       std::string sig;
       if (semi != std::string::npos) {
         size_t k = h.find("chunk-signature=", semi);
         if (k != std::string::npos) sig = trim(h.substr(k + 16));
       }
-      if (!chain->verify(dst + n, size, sig)) return fail(-1);
+      if (!chain->verify(dst + n, size, sig)) return done(-1);
       ++sigs;
     }
     if (size == 0) {
@@ -2169,24 +2321,65 @@ int S3Front::read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint6
     }
     n += size;
     std::string crlf;
-    rc = line(&crlf);
-    if (rc <= 0) return fail(rc);
-    if (!crlf.empty()) return fail(-1);
+    if ((rc = in.line(&crlf, 0)) != 1) return done(rc);
+    if (!crlf.empty()) return done(-1);
   }
-  if (chain && !final_chunk) return fail(-1);  // a signed stream ends with its signed empty chunk
-  while (used < total) {  // trailers (x-amz-checksum-*) and the closing CRLF
-    uint64_t have = std::min<uint64_t>(total - used, c->buf.size() - c->pos);
-    if (have) {
-      c->pos += have;
-      used += have;
-      continue;
-    }
-    long k = io_recv(c->io(), tmp, std::min<uint64_t>(sizeof tmp, total - used));
-    if (k <= 0) return fail(0);
-    used += static_cast<uint64_t>(k);
-  }
+  if (chain && !final_chunk) return done(-1);  // a signed stream ends with its signed empty chunk
+  const int rc = in.drain();  // trailers (x-amz-checksum-*) and the closing CRLF
+  if (rc != 1) return done(rc);
   *n_out = n;
-  return fail(1);
+  return done(1);
+}
+
+// CreateBucket / HeadBucket (reference handlers.rs:667-722; s3/server.py create_bucket,
+// head_bucket): the bucket is its marker file /<bucket>/.s3keep. A CreateBucketConfiguration
+// body is read and ignored, as the gateway does.
+bool S3Front::native_bucket(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q) {
+  TraceRange tr("dfs.s3.bucket");
+  std::string body;
+  if (r.content_length > 0) {
+    if (r.expect_continue && !send_all(c->io(), "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+    body.resize(static_cast<size_t>(r.content_length));
+    if (!read_body(c, reinterpret_cast<uint8_t*>(&body[0]), body.size())) return false;
+    r.expect_continue = false;
+  }
+  auto hand_over = [&](const std::string& why) {
+    return proxy(c, r, body.empty() ? nullptr : reinterpret_cast<const uint8_t*>(body.data()), body.size(), why);
+  };
+  std::string user = "anonymous", why;
+  Session sess;
+  if (!authorize(r, bucket, q, &user, &sess, &why)) return hand_over(why);
+  const std::string marker = "/" + bucket + "/.s3keep";
+  std::string msg;
+  bool ok;
+  if (r.method == "PUT") {
+    int64_t slot = fc_->acquire_slot(1);
+    if (slot < 0) return hand_over("bucket");
+    FastClient::Times t;
+    std::string md5;
+    int reps = 0;
+    auto st = fc_->write_slot(marker, slot, 0, &reps, &msg, &t, r.rid, nullptr, nullptr, &md5);
+    fc_->release(slot);
+    if (st == FastClient::Failed && msg.find("already exists") != std::string::npos) ok = respond(c, r, 409, "");
+    else if (st != FastClient::Ok) return hand_over("bucket");
+    else ok = respond(c, r, 200, "", "Location: /" + bucket + "\r\n");
+  } else {
+    bool found = false;
+    std::string meta;
+    if (fc_->stat(marker, &found, &meta, &msg, r.rid) != FastClient::Ok) return hand_over("bucket");
+    if (!found) {  // a bucket of objects written without the marker still exists
+      std::vector<std::pair<std::string, pb::FileMetadata>> files;
+      if (fc_->list("/" + bucket + "/", &files, r.rid) != FastClient::Ok) return hand_over("bucket");
+      found = !files.empty();
+    }
+    ok = respond(c, r, found ? 200 : 404, "", "Content-Length: 0\r\n");
+  }
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.bucket_ops++;
+  }
+  if (cfg_.auth_enabled) audit(c, r, user, r.status, sess.role_arn);
+  return ok;
 }
 
 // DeleteObject (reference handlers.rs delete_object; s3/server.py delete_object): the object

@@ -87,7 +87,7 @@ struct S3FrontStats {
   uint64_t get_stat_us = 0, get_read_us = 0, get_send_us = 0, get_timed = 0;
   uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0, iam_native = 0, lists = 0, mpu_completes = 0, mpu_initiates = 0;
   uint64_t deletes = 0, multi_deletes = 0, deleted_keys = 0, mpu_aborts = 0, copies = 0, copy_bytes = 0;
-  uint64_t chunked_puts = 0, chunk_sigs = 0, chunk_sig_failures = 0, presigned = 0;
+  uint64_t chunked_puts = 0, chunk_sigs = 0, chunk_sig_failures = 0, presigned = 0, bucket_ops = 0;
 };
 
 class S3Front {
@@ -132,6 +132,7 @@ class S3Front {
   bool native_abort(Conn* c, Req& r, const std::string& upload_id);
   bool native_delete_objects(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q);
   bool native_copy(Conn* c, Req& r, const std::string& dest);
+  bool native_bucket(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q);
   // Reads an aws-chunked body (Content-Length framed) into dst (cap bytes): 1 ok (*n = decoded
   // bytes), 0 connection error, -1 bad framing or a chunk signature that does not chain.
   int read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint64_t* n);
