@@ -51,6 +51,10 @@ def parse():
                    help="replica payload path between ranks: hipipc (HBM->HBM one-sided copies over xGMI, also "
                         "between ranks sharing one GPU), hipipc-spin (RCCL-like spinning p2p kernels), rccl, "
                         "grpc (reference), socket (host-memory P2P, CPU rehearsal)")
+    p.add_argument("--transport-ab", choices=["auto", "on", "off"], default="auto",
+                   help="after the run, a short second measurement with the other replica transport (hipipc <-> "
+                        "rccl; socket -> grpc on CPU), reported under transport_ab; auto: on when every rank has "
+                        "its own GPU")
     p.add_argument("--shards", choices=["per-gpu", "one"], default="per-gpu",
                    help="metadata shards: one per GPU rank (default) or a single master")
     p.add_argument("--cpu", action="store_true", help="CPU chunk store (plumbing config 1)")
@@ -212,436 +216,474 @@ def main():
         if world > 1:
             dist.barrier()
 
-    procs = Procs()
-    done = threading.Event()
-
-    def watchdog():
-        if not done.wait(a.timeout):
-            print(f"bench watchdog: exceeded {a.timeout}s, tearing down", file=sys.stderr, flush=True)
-            print(procs.tails(), file=sys.stderr, flush=True)
-            procs.stop()
-            os._exit(3)
-
-    threading.Thread(target=watchdog, daemon=True).start()
-
     if a.remote_steps is None:
         a.remote_steps = 2 if n == 1 else 0
-    tmp_parent = Path(os.environ.get("TMPDIR", "/tmp"))
-    if rank == 0 and not a.workdir:
-        _make_room(tmp_parent, _bytes_needed(a, n))
-    base, journal_segs = bcast(((a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=str(tmp_parent))),
-                                _journal_segments(Path(a.workdir) if a.workdir else tmp_parent, _bytes_needed(a, n), n))
-                               if rank == 0 else None)
-    base_p = Path(base)
-    if rank == 0:
-        base_p.mkdir(parents=True, exist_ok=True)
-        (base_p / ".dfs_bench").touch()  # marks a directory _make_room may reclaim later
-    (base_p / f"rank{rank}").mkdir(parents=True, exist_ok=True)
-    env = dict(os.environ)
-    env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
-    env.setdefault("DFS_LOG", "warning")
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if _journal_store_mode():
-        # the journal is the store of record and grows on demand: prepare (create and write
-        # out once) as many segments as this run's replicas need up front, within the volume
-        if journal_segs > 0:
-            env.setdefault("DFS_JOURNAL_SPARES", str(journal_segs))
-    elif journal_segs > 0:
-        env.setdefault("DFS_JOURNAL_SEGS", str(journal_segs))
-    elif journal_segs < 0:
-        env["DFS_JOURNAL"] = "0"
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE",
-              "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID"):
-        env.pop(k, None)
-    try:
-        # ---------------- metadata shards: shard r owns /bench_r<r>/...
-        per_gpu = a.shards == "per-gpu"
-        runs_master = per_gpu or rank == 0
-        gport, hport = (free_port(), free_port()) if runs_master else (0, 0)
-        ports = gather(gport)
-        if per_gpu:
-            shards = {f"shard-{r:03d}": [f"http://127.0.0.1:{ports[r]}"] for r in range(n)}
-            ranges = {prefix_of(r) + "/\U0010FFFF": f"shard-{r:03d}" for r in range(n - 1)}
-            ranges["\U0010FFFF"] = f"shard-{n - 1:03d}"
-        else:
-            shards = {"shard-000": [f"http://127.0.0.1:{ports[0]}"]}
-            ranges = {"\U0010FFFF": "shard-000"}
-        shard_file = base_p / "shard_config.json"
+    pending: dict = {}  # rank 0: the primary result while the transport A/B phase runs
+
+    def measure(a, transport: str, alt: bool = False):
+        """One cluster up, W warm-up + K timed steps, torn down; rank 0 returns the result.
+        `alt`: the transport A/B phase, whose watchdog reports the primary result and exits
+        cleanly instead of losing it."""
+        procs = Procs()
+        done = threading.Event()
+        limit = min(a.timeout, 420.0) if alt else a.timeout
+
+        def watchdog():
+            if not done.wait(limit):
+                print(f"bench watchdog: exceeded {limit}s ({'transport A/B' if alt else 'run'}), tearing down",
+                      file=sys.stderr, flush=True)
+                print(procs.tails(), file=sys.stderr, flush=True)
+                procs.stop()
+                if alt and rank == 0 and pending:
+                    pending["transport_ab"] = {transport: {"error": f"timed out after {limit:.0f} s"}}
+                    print(json.dumps(pending), flush=True)
+                    os._exit(0)
+                os._exit(3 if not alt else 0)
+
+        threading.Thread(target=watchdog, daemon=True).start()
+
+        tmp_parent = Path(os.environ.get("TMPDIR", "/tmp"))
+        if rank == 0 and not a.workdir:
+            _make_room(tmp_parent, _bytes_needed(a, n))
+        base, journal_segs = bcast(((a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=str(tmp_parent))),
+                                    _journal_segments(Path(a.workdir) if a.workdir else tmp_parent, _bytes_needed(a, n), n))
+                                   if rank == 0 else None)
+        base_p = Path(base)
         if rank == 0:
-            shard_file.write_text(json.dumps({"shards": shards, "ranges": ranges}))
-        barrier()
-        if runs_master:
-            ready = str(base_p / f"master{rank}.ready")
+            base_p.mkdir(parents=True, exist_ok=True)
+            (base_p / ".dfs_bench").touch()  # marks a directory _make_room may reclaim later
+        (base_p / f"rank{rank}").mkdir(parents=True, exist_ok=True)
+        env = dict(os.environ)
+        env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
+        env.setdefault("DFS_LOG", "warning")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if _journal_store_mode():
+            # the journal is the store of record and grows on demand: prepare (create and write
+            # out once) as many segments as this run's replicas need up front, within the volume
+            if journal_segs > 0:
+                env.setdefault("DFS_JOURNAL_SPARES", str(journal_segs))
+        elif journal_segs > 0:
+            env.setdefault("DFS_JOURNAL_SEGS", str(journal_segs))
+        elif journal_segs < 0:
+            env["DFS_JOURNAL"] = "0"
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE",
+                  "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID"):
+            env.pop(k, None)
+        try:
+            # ---------------- metadata shards: shard r owns /bench_r<r>/...
+            per_gpu = a.shards == "per-gpu"
+            runs_master = per_gpu or rank == 0
+            gport, hport = (free_port(), free_port()) if runs_master else (0, 0)
+            ports = gather(gport)
+            if per_gpu:
+                shards = {f"shard-{r:03d}": [f"http://127.0.0.1:{ports[r]}"] for r in range(n)}
+                ranges = {prefix_of(r) + "/\U0010FFFF": f"shard-{r:03d}" for r in range(n - 1)}
+                ranges["\U0010FFFF"] = f"shard-{n - 1:03d}"
+            else:
+                shards = {"shard-000": [f"http://127.0.0.1:{ports[0]}"]}
+                ranges = {"\U0010FFFF": "shard-000"}
+            shard_file = base_p / "shard_config.json"
+            if rank == 0:
+                shard_file.write_text(json.dumps({"shards": shards, "ranges": ranges}))
+            barrier()
+            if runs_master:
+                ready = str(base_p / f"master{rank}.ready")
+                from rust_hadoop_generated_by_llm_amd.cluster.launcher import role_command
+
+                # the C++ dfs_master executable
+                mp = procs.spawn_raw(role_command("master.server", [
+                    "--addr", f"127.0.0.1:{gport}", "--http-port", str(hport),
+                    "--storage-dir", str(base_p / f"rank{rank}" / "master"),
+                    "--shard-id", f"shard-{rank:03d}", "--shard-config", str(shard_file)], env),
+                    str(base_p / f"master{rank}.log"), dict(env, DFS_READY_FILE=ready))
+                wait_file(ready, mp, 300, procs)
+            barrier()
+            my_master = f"http://127.0.0.1:{ports[rank if per_gpu else 0]}"
+            # ---------------- chunkserver for this rank's GPU
+            cport, chttp = free_port(), free_port()
+            ready = str(base_p / f"cs{rank}.ready")
+            # the benchmark ranks never open the GPU (no HIP / torch.cuda call in this process): the
+            # chunkservers are the only GPU processes, so N ranks keep N processes on the cards.
+            # The count comes from the KFD topology in sysfs, which opens no device.
+            ndev = 0 if a.cpu else visible_gpus()
+            gpu = -1 if a.cpu else local_rank % max(1, ndev)
+            shared_gpu = (not a.cpu) and ndev < n  # rehearsal mode: several ranks on one GPU
+            args = ["--addr", f"127.0.0.1:{cport}",
+                    "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
+                    "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
+                    "--heartbeat-interval", "0.5", "--scrub-interval", "3600", "--rccl-timeout-ms", "90000"]
+            if n > 1 and (transport == "socket" or (not a.cpu and transport in ("hipipc", "hipipc-spin"))):
+                # hipipc works between processes that share a GPU too: a 1-GPU N-rank rehearsal
+                # forwards replicas HBM -> HBM through the same code as the 8-GPU node
+                args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
+                         str(base_p / "rccl_rdv"), "--replication-transport", transport]
+            elif n > 1 and not a.cpu and transport == "rccl" and (not shared_gpu or a.rehearse_rccl):
+                args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
+                         str(base_p / "rccl_rdv"), "--replication-transport", "rccl"]
+            else:
+                args += ["--replication-transport", "grpc"]
+            cs_env = dict(env, DFS_READY_FILE=ready, SHARD_CONFIG=str(shard_file))
             from rust_hadoop_generated_by_llm_amd.cluster.launcher import role_command
 
-            # the C++ dfs_master executable (the Python shell only with DFS_NATIVE_CONTROL=0)
-            mp = procs.spawn_raw(role_command("master.server", [
-                "--addr", f"127.0.0.1:{gport}", "--http-port", str(hport),
-                "--storage-dir", str(base_p / f"rank{rank}" / "master"),
-                "--shard-id", f"shard-{rank:03d}", "--shard-config", str(shard_file)], env),
-                str(base_p / f"master{rank}.log"), dict(env, DFS_READY_FILE=ready))
-            wait_file(ready, mp, 300, procs)
-        barrier()
-        my_master = f"http://127.0.0.1:{ports[rank if per_gpu else 0]}"
-        # ---------------- chunkserver for this rank's GPU
-        cport, chttp = free_port(), free_port()
-        ready = str(base_p / f"cs{rank}.ready")
-        # the benchmark ranks never open the GPU (no HIP / torch.cuda call in this process): the
-        # chunkservers are the only GPU processes, so N ranks keep N processes on the cards.
-        # The count comes from the KFD topology in sysfs, which opens no device.
-        ndev = 0 if a.cpu else visible_gpus()
-        gpu = -1 if a.cpu else local_rank % max(1, ndev)
-        shared_gpu = (not a.cpu) and ndev < n  # rehearsal mode: several ranks on one GPU
-        args = ["--addr", f"127.0.0.1:{cport}",
-                "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
-                "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
-                "--heartbeat-interval", "0.5", "--scrub-interval", "3600", "--rccl-timeout-ms", "90000"]
-        if n > 1 and (a.transport == "socket" or (not a.cpu and a.transport in ("hipipc", "hipipc-spin"))):
-            # hipipc works between processes that share a GPU too: a 1-GPU N-rank rehearsal
-            # forwards replicas HBM -> HBM through the same code as the 8-GPU node
-            args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
-                     str(base_p / "rccl_rdv"), "--replication-transport", a.transport]
-        elif n > 1 and not a.cpu and a.transport == "rccl" and (not shared_gpu or a.rehearse_rccl):
-            args += ["--rccl-rank", str(rank), "--rccl-world", str(n), "--rccl-rendezvous",
-                     str(base_p / "rccl_rdv"), "--replication-transport", "rccl"]
-        else:
-            args += ["--replication-transport", "grpc"]
-        cs_env = dict(env, DFS_READY_FILE=ready, SHARD_CONFIG=str(shard_file))
-        from rust_hadoop_generated_by_llm_amd.cluster.launcher import role_command
+            # the C++ dfs_chunkserver executable (the Python shell with DFS_NATIVE_CHUNKSERVER=0)
+            cs_cmd = role_command("chunkserver.server", args, cs_env)
+            if a.profile_dir:
+                # profile only the ChunkServer (where the kernels run); rocprofv3 is started
+                # before anything in this process touches the GPU
+                pdir = os.path.abspath(os.path.join(a.profile_dir, f"cs{rank}"))
+                os.makedirs(pdir, exist_ok=True)
+                cs_env["TMPDIR"] = "/tmp"
+                cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "--output-format", "csv",
+                                      "-d", pdir, "-o", "cs", "--", *cs_cmd],
+                                     str(base_p / f"cs{rank}.log"), cs_env)
+            else:
+                cp = procs.spawn_raw(cs_cmd, str(base_p / f"cs{rank}.log"), cs_env)
+            cs_info = wait_file(ready, cp, 900, procs)
+            my_cs = f"127.0.0.1:{cport}"
+            t_start = time.time()
 
-        # the C++ dfs_chunkserver executable (the Python shell with DFS_NATIVE_CHUNKSERVER=0)
-        cs_cmd = role_command("chunkserver.server", args, cs_env)
-        if a.profile_dir:
-            # profile only the ChunkServer (where the kernels run); rocprofv3 is started
-            # before anything in this process touches the GPU
-            pdir = os.path.abspath(os.path.join(a.profile_dir, f"cs{rank}"))
-            os.makedirs(pdir, exist_ok=True)
-            cs_env["TMPDIR"] = "/tmp"
-            cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "--output-format", "csv",
-                                  "-d", pdir, "-o", "cs", "--", *cs_cmd],
-                                 str(base_p / f"cs{rank}.log"), cs_env)
-        else:
-            cp = procs.spawn_raw(cs_cmd, str(base_p / f"cs{rank}.log"), cs_env)
-        cs_info = wait_file(ready, cp, 900, procs)
-        my_cs = f"127.0.0.1:{cport}"
-        t_start = time.time()
+            def note(msg: str) -> None:
+                # progress on stderr outside the timed region (the JSON line stays alone on stdout)
+                print(f"[bench r{rank} +{time.time() - t_start:.1f}s] {msg}", file=sys.stderr, flush=True)
 
-        def note(msg: str) -> None:
-            # progress on stderr outside the timed region (the JSON line stays alone on stdout)
-            print(f"[bench r{rank} +{time.time() - t_start:.1f}s] {msg}", file=sys.stderr, flush=True)
+            note("chunkserver up")
 
-        note("chunkserver up")
+            from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_read, bench_write, make_payloads
+            from rust_hadoop_generated_by_llm_amd.client.client import Client
+            from rust_hadoop_generated_by_llm_amd.models import proto as pb
+            from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
+            from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
 
-        from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_read, bench_write, make_payloads
-        from rust_hadoop_generated_by_llm_amd.client.client import Client
-        from rust_hadoop_generated_by_llm_amd.models import proto as pb
-        from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
-        from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
-
-        # wait until our shard's master has registered every chunkserver and left safe mode
-        pool = ChannelPool()
-        deadline = time.time() + 300
-        while True:
-            try:
-                st = pool.call(my_master, "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(),
-                               timeout=2)
-                if st.chunk_server_count >= n and not st.is_safe_mode:
-                    break
-            except Exception:  # noqa: BLE001
-                pass
-            if time.time() > deadline:
-                raise TimeoutError("master never registered all chunkservers")
-            time.sleep(0.1)
-        pool.close()
-        note("master has every chunkserver")
-        # the journal creates its segment files, and writes each out once, in the background
-        # after start (journal.h); let that finish first, so the first-cycle zero fill and its
-        # flushes do not share the volume with the timed writes (a startup transient, not the
-        # steady state); bounded, and reported
-        import urllib.request
-
-        t_fill = time.perf_counter()
-        fill_deadline = time.time() + 180
-        unready = None
-        while time.time() < fill_deadline:
-            try:
-                st = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
-            except OSError:
-                st = {}
-            unready = st.get("journal_parts_unready", 0) if st.get("journal") else 0
-            if unready == 0:
-                break
-            time.sleep(0.2)
-        journal_settle_s = round(time.perf_counter() - t_fill, 2)
-        note(f"journal settled in {journal_settle_s} s ({unready} parts still unready)")
-        barrier()
-
-        client = Client([my_master], local_chunkserver=my_cs)
-        client.set_shard_map(ShardMap.load_config_file(str(shard_file)))
-        payloads = make_payloads(a.count, a.size)
-        from concurrent.futures import ThreadPoolExecutor
-
-        tpool = ThreadPoolExecutor(max_workers=a.concurrency, thread_name_prefix="bench")
-
-        def step(tag: str):
-            ws, names = bench_write(client, a.count, a.size, a.concurrency, prefix=prefix_of(rank),
-                                    payloads=payloads, run_id=tag, pool=tpool)
-            verify = {nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if tag == "w0" else None
-            rs = bench_read(client, files=names, pool=tpool, verify=verify)
-            return ws, rs
-
-        for w in range(a.warmup):
-            ws, rs = step(f"w{w}")
-            note(f"warm-up step {w}: write p50 {1e3 * ws._pct(50):.2f} ms, read p50 {1e3 * rs._pct(50):.2f} ms")
-        # the timed region is bracketed by barrier + device synchronize on both sides; the
-        # synchronize runs in the process that owns the GPU and queued all of its work (the
-        # chunkserver's /sync: hipDeviceSynchronize), not in this client process
-        sync_log: list = []  # (request ms, hipDeviceSynchronize ms) of each device sync
-
-        # one keep-alive connection to the chunkserver's native /sync listener, opened here, so
-        # a sync inside the bracket is one request on an established connection (no connect,
-        # accept or server thread start in the timed region)
-        import http.client
-
-        sync_conn = http.client.HTTPConnection("127.0.0.1", cs_info.get("sync_port") or chttp, timeout=60)
-
-        def device_sync():
-            if a.cpu:
-                return
-            t_req = time.perf_counter()
-            sync_conn.request("GET", "/sync")
-            r = json.loads(sync_conn.getresponse().read())
-            if not r.get("synchronized"):
-                raise RuntimeError(f"chunkserver device sync failed: {r}")
-            sync_log.append((round(1e3 * (time.perf_counter() - t_req), 3), r.get("sync_ms")))
-
-        # no cyclic-GC pass inside the timed region: a full collection over this process's
-        # imports (torch, grpc, numpy) is tens of ms, and one landing in the closing bracket
-        # showed up as a 100 ms device sync whose server side took 0.02 ms (profiles/r4_journal)
-        import gc
-
-        gc.collect()
-        gc.freeze()
-        gc.disable()
-        device_sync()
-        barrier()
-        device_sync()
-        import psutil
-
-        def cpu_snapshot():
-            snap = {"client": sum(psutil.Process().cpu_times()[:2])}
-            for i, p in enumerate(procs.items):
+            # wait until our shard's master has registered every chunkserver and left safe mode
+            pool = ChannelPool()
+            deadline = time.time() + 300
+            while True:
                 try:
-                    kids = [psutil.Process(p.pid)] + psutil.Process(p.pid).children(recursive=True)
-                    name = os.path.basename(procs.logs[i]).split(".")[0]
-                    times = [k.cpu_times() for k in kids]
-                    snap[name] = sum(t.user + t.system for t in times)
-                    snap[name + "_sys"] = sum(t.system for t in times)  # page cache / reclaim / flush
-                except psutil.Error:
+                    st = pool.call(my_master, "MasterService", "GetSafeModeStatus", pb.GetSafeModeStatusRequest(),
+                                   timeout=2)
+                    if st.chunk_server_count >= n and not st.is_safe_mode:
+                        break
+                except Exception:  # noqa: BLE001
                     pass
-            return snap
+                if time.time() > deadline:
+                    raise TimeoutError("master never registered all chunkservers")
+                time.sleep(0.1)
+            pool.close()
+            note("master has every chunkserver")
+            # the journal creates its segment files, and writes each out once, in the background
+            # after start (journal.h); let that finish first, so the first-cycle zero fill and its
+            # flushes do not share the volume with the timed writes (a startup transient, not the
+            # steady state); bounded, and reported
+            import urllib.request
 
-        client.phase_times = {}
-        cpu0 = cpu_snapshot()
-        cg0 = cgroup_cpu()
-        t0 = time.perf_counter()
-        wl, rl, wbytes, rbytes = [], [], 0, 0
-        wt = rt = 0.0
-        for s in range(a.steps):
-            ws, rs = step(f"s{s}")
-            wl += ws.latencies
-            rl += rs.latencies
-            wbytes += ws.count * ws.avg_size
-            rbytes += rs.count * rs.avg_size
-            wt += ws.total_s
-            rt += rs.total_s
-        t_loop = time.perf_counter() - t0
-        device_sync()
-        barrier()
-        device_sync()
-        elapsed = time.perf_counter() - t0
-        end_sync_s = elapsed - t_loop
-        gc.enable()
-        note(f"{a.steps} timed steps in {elapsed:.3f} s")
-        cpu1 = cpu_snapshot()
-        host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
-        job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), elapsed)
-
-        def cs_stats() -> dict:
-            try:
-                import urllib.request
-
-                return json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
-            except Exception:  # noqa: BLE001
-                return {}
-
-        # counters of the timed phase only (the stress / remote phases below add their own hops)
-        stats = cs_stats()
-        vol = {"rank_dir_bytes": _allocated_bytes(base_p / f"rank{rank}"),
-               "journal_used_bytes": stats.get("journal_used_bytes", 0),
-               "journal_live_bytes": stats.get("journal_live_bytes", 0),
-               "exported_blocks": stats.get("materialized_blocks", 0),
-               "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else (
-                   stats.get("journal_mode", "journal") if stats.get("journal") else "per-file")}
-        stress = None
-        if a.stress_seconds > 0:
-            # the reference's only published throughput (stress-write 30 s, 10240 B,
-            # conc 5 -> 470 ops/s); run outside the timed region, same cluster, every rank at once
-            from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_stress_write
-
+            t_fill = time.perf_counter()
+            fill_deadline = time.time() + 180
+            unready = None
+            while time.time() < fill_deadline:
+                try:
+                    st = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
+                except OSError:
+                    st = {}
+                unready = st.get("journal_parts_unready", 0) if st.get("journal") else 0
+                if unready == 0:
+                    break
+                time.sleep(0.2)
+            journal_settle_s = round(time.perf_counter() - t_fill, 2)
+            note(f"journal settled in {journal_settle_s} s ({unready} parts still unready)")
             barrier()
-            ss = bench_stress_write(client, a.stress_seconds, a.stress_size, a.stress_concurrency,
-                                    prefix=prefix_of(rank) + "/stress")
-            stress = {"ops": ss.count, "seconds": ss.total_s, "errors": ss.errors, "lat": ss.latencies,
-                      "first_error": getattr(ss, "first_error", "")}
-        remote = None
-        if a.remote_steps > 0:
-            # the reference's wire path (dfs/client/src/mod.rs:415-451,921-944): a client that
-            # is not co-located, so every WriteBlock/ReadBlock carries the payload over gRPC
-            rc = Client([my_master], local_chunkserver=None, local_rpc=False)
-            rc.set_shard_map(ShardMap.load_config_file(str(shard_file)))
-            rc.phase_times = {}
+
+            client = Client([my_master], local_chunkserver=my_cs)
+            client.set_shard_map(ShardMap.load_config_file(str(shard_file)))
+            payloads = make_payloads(a.count, a.size)
+            from concurrent.futures import ThreadPoolExecutor
+
+            tpool = ThreadPoolExecutor(max_workers=a.concurrency, thread_name_prefix="bench")
+
+            def step(tag: str):
+                ws, names = bench_write(client, a.count, a.size, a.concurrency, prefix=prefix_of(rank),
+                                        payloads=payloads, run_id=tag, pool=tpool)
+                verify = {nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if tag == "w0" else None
+                rs = bench_read(client, files=names, pool=tpool, verify=verify)
+                return ws, rs
+
+            for w in range(a.warmup):
+                ws, rs = step(f"w{w}")
+                note(f"warm-up step {w}: write p50 {1e3 * ws._pct(50):.2f} ms, read p50 {1e3 * rs._pct(50):.2f} ms")
+            # the timed region is bracketed by barrier + device synchronize on both sides; the
+            # synchronize runs in the process that owns the GPU and queued all of its work (the
+            # chunkserver's /sync: hipDeviceSynchronize), not in this client process
+            sync_log: list = []  # (request ms, hipDeviceSynchronize ms) of each device sync
+
+            # one keep-alive connection to the chunkserver's native /sync listener, opened here, so
+            # a sync inside the bracket is one request on an established connection (no connect,
+            # accept or server thread start in the timed region)
+            import http.client
+
+            sync_conn = http.client.HTTPConnection("127.0.0.1", cs_info.get("sync_port") or chttp, timeout=60)
+
+            def device_sync():
+                if a.cpu:
+                    return
+                t_req = time.perf_counter()
+                sync_conn.request("GET", "/sync")
+                r = json.loads(sync_conn.getresponse().read())
+                if not r.get("synchronized"):
+                    raise RuntimeError(f"chunkserver device sync failed: {r}")
+                sync_log.append((round(1e3 * (time.perf_counter() - t_req), 3), r.get("sync_ms")))
+
+            # no cyclic-GC pass inside the timed region: a full collection over this process's
+            # imports (torch, grpc, numpy) is tens of ms, and one landing in the closing bracket
+            # showed up as a 100 ms device sync whose server side took 0.02 ms (profiles/r4_journal)
+            import gc
+
+            gc.collect()
+            gc.freeze()
+            gc.disable()
+            device_sync()
             barrier()
-            rwl, rrl, rwb, rrb, rwt, rrt = [], [], 0, 0, 0.0, 0.0
-            for s in range(a.remote_steps):
-                ws, names = bench_write(rc, a.count, a.size, a.concurrency, prefix=prefix_of(rank) + "/remote",
-                                        payloads=payloads, run_id=f"rem{s}", pool=tpool)
-                rs = bench_read(rc, files=names, pool=tpool,
-                                verify={nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if s == 0 else None)
-                rwl += ws.latencies
-                rrl += rs.latencies
-                rwb += ws.count * ws.avg_size
-                rrb += rs.count * rs.avg_size
-                rwt += ws.total_s
-                rrt += rs.total_s
-            remote = {"wl": rwl, "rl": rrl, "wbytes": rwb, "rbytes": rrb, "wt": rwt, "rt": rrt,
-                      "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count,
-                      "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in rc.phase_times.items() if v}}
-            rc.close()
-        allr = gather({"elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
-                       "rbytes": rbytes, "wt": wt,
-                       "rt": rt, "cs": stats, "stress": stress, "remote": remote, "vol": vol,
-                       "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
-                       "cpu": host_cpu, "job_cpu": job_cpu, "settle": journal_settle_s, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
-                                                   for k, v in (client.phase_times or {}).items() if v}})
-        if rank == 0:
-            tmax = max(r["elapsed"] for r in allr)
-            tot = sum(r["wbytes"] + r["rbytes"] for r in allr)
-            wlat = sorted(x for r in allr for x in r["wl"])
-            rlat = sorted(x for r in allr for x in r["rl"])
+            device_sync()
+            import psutil
 
-            def pct(v, p):
-                return 1e3 * v[min(len(v) - 1, len(v) * p // 100)] if v else 0.0
+            def cpu_snapshot():
+                snap = {"client": sum(psutil.Process().cpu_times()[:2])}
+                for i, p in enumerate(procs.items):
+                    try:
+                        kids = [psutil.Process(p.pid)] + psutil.Process(p.pid).children(recursive=True)
+                        name = os.path.basename(procs.logs[i]).split(".")[0]
+                        times = [k.cpu_times() for k in kids]
+                        snap[name] = sum(t.user + t.system for t in times)
+                        snap[name + "_sys"] = sum(t.system for t in times)  # page cache / reclaim / flush
+                    except psutil.Error:
+                        pass
+                return snap
 
-            wmax = max(r["wt"] for r in allr)
-            rmax = max(r["rt"] for r in allr)
-            result = {
-                "metric": METRIC, "value": round(tot / (1 << 20) / tmax, 2), "unit": "MB/s", "n_gpus": n,
-                "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * tmax / a.steps, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "uint8",
-                "data": "synthetic random bytes",
-                "config": {"model": "dfs_cli benchmark write+read (1 MiB files)", "global_batch": a.count * n,
-                           "seq_len": a.size, "parallelism": f"cs{n}-shards{n if per_gpu else 1}",
-                           "files_per_gpu_per_step": a.count, "file_size": a.size, "concurrency": a.concurrency,
-                           "replication_factor": min(3, n), "durability": a.durability,
-                           "store": "cpu" if a.cpu else "hbm",
-                           "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else (
-                               "journal (store of record)" if _journal_store_mode() else "journal (round-4 ring)"),
-                           "transport": observed_transport(allr, n)},
-                "write_mb_per_s": round(sum(r["wbytes"] for r in allr) / (1 << 20) / wmax, 2),
-                "read_mb_per_s": round(sum(r["rbytes"] for r in allr) / (1 << 20) / rmax, 2),
-                "write_p50_ms": round(pct(wlat, 50), 3), "write_p95_ms": round(pct(wlat, 95), 3),
-                "write_p99_ms": round(pct(wlat, 99), 3), "read_p50_ms": round(pct(rlat, 50), 3),
-                "read_p95_ms": round(pct(rlat, 95), 3), "read_p99_ms": round(pct(rlat, 99), 3),
-                "write_ops_per_s": round(len(wlat) / wmax, 1),
-                # where the timed region went besides the write and read phases (rank 0): the
-                # closing barrier + device synchronize, and the loop's own bookkeeping
-                "closing_sync_ms_rank0": round(1e3 * allr[0]["end_sync"], 3),
-                "device_syncs_rank0": allr[0]["syncs"],
-                "between_phases_ms_per_step_rank0": round(1e3 * (allr[0]["loop"] - allr[0]["wt"] - allr[0]["rt"]) / a.steps, 3),
-                # replica hops between same-node chunkservers: which device transport carried
-                # them (hipipc / rccl / socket), on how many ranks, and how often it fell back
-                "p2p_transport": ",".join(sorted({r["p2p_transport"] for r in allr if r["p2p"]})) or "none",
-                "p2p_ranks": sum(1 for r in allr if r["p2p"]),
-                "repl_pairs_up": sum(r["cs"].get("repl_pairs_up", 0) for r in allr),
-                **forward_counts(allr),
-                "p2p_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) + r["cs"].get("fp_p2p_fallbacks", 0)
-                                     for r in allr),
-                "replica_failures": sum(r["cs"].get("fp_replica_failures", 0) for r in allr),
-                "repl_pair_failures": sum(r["cs"].get("repl_pair_failures", 0) for r in allr),
-                "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
-                "fused_reads": sum(r["cs"].get("fused_reads", 0) for r in allr),
-                "direct_writes": sum(r["cs"].get("direct_writes", 0) for r in allr),
-                "disk_gate_waits": sum(r["cs"].get("disk_gate_waits", 0) for r in allr),
-                # block journal (group commit): records appended, flush rounds that covered them,
-                # and blocks already written out as <id> + <id>.meta by the materializer
-                "journal": {k: sum(r["cs"].get(f, 0) for r in allr) for k, f in (
-                    ("records", "journal_records"), ("sync_rounds", "journal_sync_rounds"),
-                    ("materialized_blocks", "materialized_blocks"), ("materialize_pending", "materialize_pending"),
-                    ("full_waits", "journal_full_waits"), ("segments", "journal_segs"),
-                    ("segments_retired", "journal_segs_retired"), ("parts_filled", "journal_segs_filled"),
-                    ("prepare_errors", "journal_prepare_errors"),
-                    ("materialize_errors", "materialize_errors"), ("sync_ns", "journal_sync_ns"),
-                    ("commit_ns", "journal_commit_ns"), ("bypassed", "journal_bypassed"),
-                    ("parts_unready", "journal_parts_unready"), ("live_records", "journal_live_records"),
-                    ("segments_in_use", "journal_segs_in_use"), ("segments_marked", "journal_segs_marked"),
-                    ("relocated_blocks", "relocated_blocks"), ("supersedes", "journal_supersedes"),
-                    ("export_deferred_headroom", "export_deferred_headroom"))} | {
-                    "mode": ",".join(sorted({r["cs"].get("journal_mode", "?") for r in allr})),
-                    "settle_s_before_warmup": max(r["settle"] for r in allr)} if any(r["cs"].get("journal") for r in allr) else None,
-                # where each rank's replicas live and how much of the volume they take
-                "volume": {"per_rank": [r["vol"] for r in allr], "free_bytes_after": _free_bytes(base_p)},
-                "host_cpu_util_rank0": allr[0]["cpu"],
-                # the whole job's CPU over the timed region, from the cgroup every rank shares
-                # (cores used, the quota, and time the quota throttled it); null without cgroup
-                "host_cpu_job": allr[0]["job_cpu"],
-                "client_phase_p50_ms_rank0": allr[0]["phases"],
-            }
-            if a.remote_steps > 0:
-                rwl = sorted(x for r in allr for x in r["remote"]["wl"])
-                rrl = sorted(x for r in allr for x in r["remote"]["rl"])
-                rw = sum(r["remote"]["wbytes"] for r in allr) / (1 << 20) / max(r["remote"]["wt"] for r in allr)
-                rr = sum(r["remote"]["rbytes"] for r in allr) / (1 << 20) / max(r["remote"]["rt"] for r in allr)
-                result["remote_client"] = {
-                    "steps": a.remote_steps,
-                    "path": "gRPC/TCP for every master and chunkserver RPC (no shm, no UNIX sockets), " + (
-                        "native C++ client (HTTP/2 on nghttp2)" if all(
-                            r["remote"]["native_ops"] == r["remote"]["ops"] for r in allr) else
-                        "Python grpcio client" if all(r["remote"]["native_ops"] == 0 for r in allr) else
-                        "native C++ client with Python fallbacks"),
-                    "native_client_ops": sum(r["remote"]["native_ops"] for r in allr),
-                    "write_mb_per_s": round(rw, 2), "read_mb_per_s": round(rr, 2),
-                    "mb_per_s": round((sum(r["remote"]["wbytes"] + r["remote"]["rbytes"] for r in allr) / (1 << 20))
-                                      / max(r["remote"]["wt"] + r["remote"]["rt"] for r in allr), 2),
-                    "write_p50_ms": round(pct(rwl, 50), 3), "write_p99_ms": round(pct(rwl, 99), 3),
-                    "read_p50_ms": round(pct(rrl, 50), 3), "read_p99_ms": round(pct(rrl, 99), 3),
-                    "client_phase_p50_ms_rank0": allr[0]["remote"].get("phases", {})}
+            client.phase_times = {}
+            cpu0 = cpu_snapshot()
+            cg0 = cgroup_cpu()
+            t0 = time.perf_counter()
+            wl, rl, wbytes, rbytes = [], [], 0, 0
+            wt = rt = 0.0
+            for s in range(a.steps):
+                ws, rs = step(f"s{s}")
+                wl += ws.latencies
+                rl += rs.latencies
+                wbytes += ws.count * ws.avg_size
+                rbytes += rs.count * rs.avg_size
+                wt += ws.total_s
+                rt += rs.total_s
+            t_loop = time.perf_counter() - t0
+            device_sync()
+            barrier()
+            device_sync()
+            elapsed = time.perf_counter() - t0
+            end_sync_s = elapsed - t_loop
+            gc.enable()
+            note(f"{a.steps} timed steps in {elapsed:.3f} s")
+            cpu1 = cpu_snapshot()
+            host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
+            job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), elapsed)
+
+            def cs_stats() -> dict:
+                try:
+                    import urllib.request
+
+                    return json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
+                except Exception:  # noqa: BLE001
+                    return {}
+
+            # counters of the timed phase only (the stress / remote phases below add their own hops)
+            stats = cs_stats()
+            vol = {"rank_dir_bytes": _allocated_bytes(base_p / f"rank{rank}"),
+                   "journal_used_bytes": stats.get("journal_used_bytes", 0),
+                   "journal_live_bytes": stats.get("journal_live_bytes", 0),
+                   "exported_blocks": stats.get("materialized_blocks", 0),
+                   "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else (
+                       stats.get("journal_mode", "journal") if stats.get("journal") else "per-file")}
+            stress = None
             if a.stress_seconds > 0:
-                slat = sorted(x for r in allr for x in r["stress"]["lat"])
-                ops = sum(r["stress"]["ops"] for r in allr) / max(r["stress"]["seconds"] for r in allr)
-                result["stress_write"] = {
-                    "seconds": a.stress_seconds, "size": a.stress_size, "concurrency_per_rank": a.stress_concurrency,
-                    "ops_per_s": round(ops, 1), "mb_per_s": round(ops * a.stress_size / (1 << 20), 2),
-                    "errors": sum(r["stress"]["errors"] for r in allr),
-                    "first_error": next((r["stress"]["first_error"] for r in allr if r["stress"]["first_error"]), ""),
-                    "avg_ms": round(1e3 * sum(slat) / max(1, len(slat)), 3), "p50_ms": round(pct(slat, 50), 3),
-                    "p95_ms": round(pct(slat, 95), 3), "p99_ms": round(pct(slat, 99), 3),
-                    "vs_published_470_ops_per_s": round(ops / 470.0, 1)}
-            print(json.dumps(result), flush=True)
-        barrier()
-        tpool.shutdown(wait=False)
-        client.close()
-    finally:
-        done.set()
-        procs.stop()
-        if world > 1:
-            try:
-                dist.barrier()
-                dist.destroy_process_group()
-            except Exception:  # noqa: BLE001
-                pass
-        if rank == 0 and _should_clean(a, base):
-            shutil.rmtree(base, ignore_errors=True)
+                # the reference's only published throughput (BASELINE.md: stress-write 30 s, 10240 B,
+                # conc 5 -> 470 ops/s); run outside the timed region, same cluster, every rank at once
+                from rust_hadoop_generated_by_llm_amd.client.benchmark import bench_stress_write
+
+                barrier()
+                ss = bench_stress_write(client, a.stress_seconds, a.stress_size, a.stress_concurrency,
+                                        prefix=prefix_of(rank) + "/stress")
+                stress = {"ops": ss.count, "seconds": ss.total_s, "errors": ss.errors, "lat": ss.latencies,
+                          "first_error": getattr(ss, "first_error", "")}
+            remote = None
+            if a.remote_steps > 0:
+                # the reference's wire path (dfs/client/src/mod.rs:415-451,921-944): a client that
+                # is not co-located, so every WriteBlock/ReadBlock carries the payload over gRPC
+                rc = Client([my_master], local_chunkserver=None, local_rpc=False)
+                rc.set_shard_map(ShardMap.load_config_file(str(shard_file)))
+                rc.phase_times = {}
+                barrier()
+                rwl, rrl, rwb, rrb, rwt, rrt = [], [], 0, 0, 0.0, 0.0
+                for s in range(a.remote_steps):
+                    ws, names = bench_write(rc, a.count, a.size, a.concurrency, prefix=prefix_of(rank) + "/remote",
+                                            payloads=payloads, run_id=f"rem{s}", pool=tpool)
+                    rs = bench_read(rc, files=names, pool=tpool,
+                                    verify={nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if s == 0 else None)
+                    rwl += ws.latencies
+                    rrl += rs.latencies
+                    rwb += ws.count * ws.avg_size
+                    rrb += rs.count * rs.avg_size
+                    rwt += ws.total_s
+                    rrt += rs.total_s
+                remote = {"wl": rwl, "rl": rrl, "wbytes": rwb, "rbytes": rrb, "wt": rwt, "rt": rrt,
+                          "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count,
+                          "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in rc.phase_times.items() if v}}
+                rc.close()
+            allr = gather({"elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
+                           "rbytes": rbytes, "wt": wt,
+                           "rt": rt, "cs": stats, "stress": stress, "remote": remote, "vol": vol,
+                           "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
+                           "cpu": host_cpu, "job_cpu": job_cpu, "settle": journal_settle_s, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
+                                                       for k, v in (client.phase_times or {}).items() if v}})
+            if rank == 0:
+                tmax = max(r["elapsed"] for r in allr)
+                tot = sum(r["wbytes"] + r["rbytes"] for r in allr)
+                wlat = sorted(x for r in allr for x in r["wl"])
+                rlat = sorted(x for r in allr for x in r["rl"])
+
+                def pct(v, p):
+                    return 1e3 * v[min(len(v) - 1, len(v) * p // 100)] if v else 0.0
+
+                wmax = max(r["wt"] for r in allr)
+                rmax = max(r["rt"] for r in allr)
+                result = {
+                    "metric": METRIC, "value": round(tot / (1 << 20) / tmax, 2), "unit": "MB/s", "n_gpus": n,
+                    "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * tmax / a.steps, 3),
+                    "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "uint8",
+                    "data": "synthetic random bytes",
+                    "config": {"model": "dfs_cli benchmark write+read (1 MiB files)", "global_batch": a.count * n,
+                               "seq_len": a.size, "parallelism": f"cs{n}-shards{n if per_gpu else 1}",
+                               "files_per_gpu_per_step": a.count, "file_size": a.size, "concurrency": a.concurrency,
+                               "replication_factor": min(3, n), "durability": a.durability,
+                               "store": "cpu" if a.cpu else "hbm",
+                               "durable_path": "per-file" if env.get("DFS_JOURNAL") == "0" else (
+                                   "journal (store of record)" if _journal_store_mode() else "journal (round-4 ring)"),
+                               "transport": observed_transport(allr, n)},
+                    "write_mb_per_s": round(sum(r["wbytes"] for r in allr) / (1 << 20) / wmax, 2),
+                    "read_mb_per_s": round(sum(r["rbytes"] for r in allr) / (1 << 20) / rmax, 2),
+                    "write_p50_ms": round(pct(wlat, 50), 3), "write_p95_ms": round(pct(wlat, 95), 3),
+                    "write_p99_ms": round(pct(wlat, 99), 3), "read_p50_ms": round(pct(rlat, 50), 3),
+                    "read_p95_ms": round(pct(rlat, 95), 3), "read_p99_ms": round(pct(rlat, 99), 3),
+                    "write_ops_per_s": round(len(wlat) / wmax, 1),
+                    # where the timed region went besides the write and read phases (rank 0): the
+                    # closing barrier + device synchronize, and the loop's own bookkeeping
+                    "closing_sync_ms_rank0": round(1e3 * allr[0]["end_sync"], 3),
+                    "device_syncs_rank0": allr[0]["syncs"],
+                    "between_phases_ms_per_step_rank0": round(1e3 * (allr[0]["loop"] - allr[0]["wt"] - allr[0]["rt"]) / a.steps, 3),
+                    # replica hops between same-node chunkservers: which device transport carried
+                    # them (hipipc / rccl / socket), on how many ranks, and how often it fell back
+                    "p2p_transport": ",".join(sorted({r["p2p_transport"] for r in allr if r["p2p"]})) or "none",
+                    "p2p_ranks": sum(1 for r in allr if r["p2p"]),
+                    "repl_pairs_up": sum(r["cs"].get("repl_pairs_up", 0) for r in allr),
+                    **forward_counts(allr),
+                    "p2p_fallbacks": sum(r["cs"].get("rccl_fallbacks", 0) + r["cs"].get("fp_p2p_fallbacks", 0)
+                                         for r in allr),
+                    "replica_failures": sum(r["cs"].get("fp_replica_failures", 0) for r in allr),
+                    "repl_pair_failures": sum(r["cs"].get("repl_pair_failures", 0) for r in allr),
+                    "gpu_kernel_launches": sum(r["cs"].get("gpu_kernel_launches", 0) for r in allr),
+                    "fused_reads": sum(r["cs"].get("fused_reads", 0) for r in allr),
+                    "direct_writes": sum(r["cs"].get("direct_writes", 0) for r in allr),
+                    "disk_gate_waits": sum(r["cs"].get("disk_gate_waits", 0) for r in allr),
+                    # block journal (group commit): records appended, flush rounds that covered them,
+                    # and blocks already written out as <id> + <id>.meta by the materializer
+                    "journal": {k: sum(r["cs"].get(f, 0) for r in allr) for k, f in (
+                        ("records", "journal_records"), ("sync_rounds", "journal_sync_rounds"),
+                        ("materialized_blocks", "materialized_blocks"), ("materialize_pending", "materialize_pending"),
+                        ("full_waits", "journal_full_waits"), ("segments", "journal_segs"),
+                        ("segments_retired", "journal_segs_retired"), ("parts_filled", "journal_segs_filled"),
+                        ("prepare_errors", "journal_prepare_errors"),
+                        ("materialize_errors", "materialize_errors"), ("sync_ns", "journal_sync_ns"),
+                        ("commit_ns", "journal_commit_ns"), ("bypassed", "journal_bypassed"),
+                        ("parts_unready", "journal_parts_unready"), ("live_records", "journal_live_records"),
+                        ("segments_in_use", "journal_segs_in_use"), ("segments_marked", "journal_segs_marked"),
+                        ("relocated_blocks", "relocated_blocks"), ("supersedes", "journal_supersedes"),
+                        ("export_deferred_headroom", "export_deferred_headroom"))} | {
+                        "mode": ",".join(sorted({r["cs"].get("journal_mode", "?") for r in allr})),
+                        "settle_s_before_warmup": max(r["settle"] for r in allr)} if any(r["cs"].get("journal") for r in allr) else None,
+                    # where each rank's replicas live and how much of the volume they take
+                    "volume": {"per_rank": [r["vol"] for r in allr], "free_bytes_after": _free_bytes(base_p)},
+                    "host_cpu_util_rank0": allr[0]["cpu"],
+                    # the whole job's CPU over the timed region, from the cgroup every rank shares
+                    # (cores used, the quota, and time the quota throttled it); null without cgroup
+                    "host_cpu_job": allr[0]["job_cpu"],
+                    "client_phase_p50_ms_rank0": allr[0]["phases"],
+                }
+                if a.remote_steps > 0:
+                    rwl = sorted(x for r in allr for x in r["remote"]["wl"])
+                    rrl = sorted(x for r in allr for x in r["remote"]["rl"])
+                    rw = sum(r["remote"]["wbytes"] for r in allr) / (1 << 20) / max(r["remote"]["wt"] for r in allr)
+                    rr = sum(r["remote"]["rbytes"] for r in allr) / (1 << 20) / max(r["remote"]["rt"] for r in allr)
+                    result["remote_client"] = {
+                        "steps": a.remote_steps,
+                        "path": "gRPC/TCP for every master and chunkserver RPC (no shm, no UNIX sockets), " + (
+                            "native C++ client (HTTP/2 on nghttp2)" if all(
+                                r["remote"]["native_ops"] == r["remote"]["ops"] for r in allr) else
+                            "Python grpcio client" if all(r["remote"]["native_ops"] == 0 for r in allr) else
+                            "native C++ client with Python fallbacks"),
+                        "native_client_ops": sum(r["remote"]["native_ops"] for r in allr),
+                        "write_mb_per_s": round(rw, 2), "read_mb_per_s": round(rr, 2),
+                        "mb_per_s": round((sum(r["remote"]["wbytes"] + r["remote"]["rbytes"] for r in allr) / (1 << 20))
+                                          / max(r["remote"]["wt"] + r["remote"]["rt"] for r in allr), 2),
+                        "write_p50_ms": round(pct(rwl, 50), 3), "write_p99_ms": round(pct(rwl, 99), 3),
+                        "read_p50_ms": round(pct(rrl, 50), 3), "read_p99_ms": round(pct(rrl, 99), 3),
+                        "client_phase_p50_ms_rank0": allr[0]["remote"].get("phases", {})}
+                if a.stress_seconds > 0:
+                    slat = sorted(x for r in allr for x in r["stress"]["lat"])
+                    ops = sum(r["stress"]["ops"] for r in allr) / max(r["stress"]["seconds"] for r in allr)
+                    result["stress_write"] = {
+                        "seconds": a.stress_seconds, "size": a.stress_size, "concurrency_per_rank": a.stress_concurrency,
+                        "ops_per_s": round(ops, 1), "mb_per_s": round(ops * a.stress_size / (1 << 20), 2),
+                        "errors": sum(r["stress"]["errors"] for r in allr),
+                        "first_error": next((r["stress"]["first_error"] for r in allr if r["stress"]["first_error"]), ""),
+                        "avg_ms": round(1e3 * sum(slat) / max(1, len(slat)), 3), "p50_ms": round(pct(slat, 50), 3),
+                        "p95_ms": round(pct(slat, 95), 3), "p99_ms": round(pct(slat, 99), 3),
+                        "vs_published_470_ops_per_s": round(ops / 470.0, 1)}
+            barrier()
+            tpool.shutdown(wait=False)
+            client.close()
+            return result if rank == 0 else None
+        finally:
+            done.set()
+            procs.stop()
+            if rank == 0 and _should_clean(a, base):
+                shutil.rmtree(base, ignore_errors=True)
+
+    result = measure(a, a.transport)
+    # transport A/B (VERDICT r4): on distinct GPUs, the other device transport runs a short
+    # second measurement in the same job, so one JSON carries hipipc and RCCL side by side
+    other = {"hipipc": "rccl", "rccl": "hipipc", "socket": "grpc"}.get(a.transport)
+    ab = a.transport_ab == "on" or (a.transport_ab == "auto" and n > 1 and not a.cpu and visible_gpus() >= n)
+    if ab and other:
+        import copy
+
+        b = copy.copy(a)
+        b.steps, b.warmup, b.remote_steps, b.stress_seconds = min(a.steps, 10), 1, 0, 0.0
+        b.profile_dir = None
+        if rank == 0:
+            pending.update(result)
+        try:
+            alt = measure(b, other, alt=True)
+            if rank == 0:
+                result["transport_ab"] = {other: {k: alt.get(k) for k in (
+                    "value", "steps", "ms_per_step", "write_mb_per_s", "read_mb_per_s", "write_p50_ms", "write_p99_ms",
+                    "read_p50_ms", "p2p_transport", "repl_pairs_up", "p2p_forwards", "rccl_forwards",
+                    "p2p_fallbacks", "replica_failures")} | {"transport": alt["config"]["transport"]}}
+        except Exception as e:  # noqa: BLE001 - the primary result stands either way
+            if rank == 0:
+                result["transport_ab"] = {other: {"error": f"{type(e).__name__}: {e}"[:500]}}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        try:
+            dist.barrier()
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 def forward_counts(allr) -> dict:
@@ -830,7 +872,7 @@ def _should_clean(a, base: str) -> bool:
 
     Like `dfs_cli benchmark` (which never deletes what it wrote), the written blocks stay
     on disk by default while the volume keeps plenty of room: measured on the MI355X boxes
-    (profiles/r1_disk/keep_vs_delete.md), deleting a run's ~1 GB of fsynced 1 MiB files makes
+    (profiles/archive/r1_disk/keep_vs_delete.md), deleting a run's ~1 GB of fsynced 1 MiB files makes
     the NEXT durable-write run on the same overlay volume 1.4-2.4x slower for minutes, which
     would leak one run's cleanup into the next run's timed region. `--cleanup always` deletes
     anyway; `auto` deletes only when the disk is getting full (free < max(10 GiB, 10 %)), and

@@ -1454,7 +1454,7 @@ int MasterCore::rename(const std::string& raw, std::string* out) {
     if (!peer_call_ || coordinators_.fetch_add(1) >= kMaxCoordinators) {
       if (peer_call_) coordinators_--;
       tx_declined_++;
-      return kDecline;  // the Python handler records the request
+      return kDecline;  // dfs_master waits for a slot and retries (rename_declined)
     }
     record_request(r.source_path);
     int rc = rename_2pc(r, src_shard, dst_shard, out);

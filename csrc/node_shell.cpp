@@ -23,7 +23,8 @@
 namespace dfs::shell {
 
 Args::Args(int argc, char** argv, const std::set<std::string>& bool_flags,
-           const std::map<std::string, std::string>& short_names) {
+           const std::map<std::string, std::string>& short_names, const std::map<std::string, std::string>& defaults)
+    : defaults_(defaults) {
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     std::string name, value;
@@ -59,17 +60,25 @@ Args::Args(int argc, char** argv, const std::set<std::string>& bool_flags,
 
 std::string Args::get(const std::string& name, const std::string& dflt) const {
   auto it = kv_.find(name);
-  return it == kv_.end() ? dflt : it->second;
+  if (it != kv_.end()) return it->second;
+  auto d = defaults_.find(name);
+  return d == defaults_.end() ? dflt : d->second;
 }
 
 int64_t Args::get_int(const std::string& name, int64_t dflt) const {
-  auto it = kv_.find(name);
-  return it == kv_.end() ? dflt : std::strtoll(it->second.c_str(), nullptr, 10);
+  const std::string v = get(name, "");
+  return v.empty() ? dflt : std::strtoll(v.c_str(), nullptr, 10);
 }
 
 double Args::get_double(const std::string& name, double dflt) const {
-  auto it = kv_.find(name);
-  return it == kv_.end() ? dflt : std::strtod(it->second.c_str(), nullptr);
+  const std::string v = get(name, "");
+  return v.empty() ? dflt : std::strtod(v.c_str(), nullptr);
+}
+
+std::string defaults_help(const std::map<std::string, std::string>& defaults) {
+  std::string o = "defaults:\n";
+  for (auto& kv : defaults) o += "  --" + kv.first + " " + kv.second + "\n";
+  return o;
 }
 
 std::string with_scheme(const std::string& addr, bool tls) {

@@ -23,8 +23,11 @@ namespace dfs::shell {
 // --name value / --name=value / -a value; boolean flags take no value.
 class Args {
  public:
+  // `defaults`: the value of a flag that is not given (the reference's clap defaults); a
+  // default passed to get() applies only to flags without one here.
   Args(int argc, char** argv, const std::set<std::string>& bool_flags,
-       const std::map<std::string, std::string>& short_names = {});
+       const std::map<std::string, std::string>& short_names = {},
+       const std::map<std::string, std::string>& defaults = {});
   std::string get(const std::string& name, const std::string& dflt = "") const;
   int64_t get_int(const std::string& name, int64_t dflt) const;
   double get_double(const std::string& name, double dflt) const;
@@ -33,11 +36,13 @@ class Args {
   const std::string& error() const { return err_; }
 
  private:
-  std::map<std::string, std::string> kv_;
+  std::map<std::string, std::string> kv_, defaults_;
   std::set<std::string> flags_;
   std::string err_;
 };
 
+// "  --name default" lines of a defaults table (the --help text's defaults section).
+std::string defaults_help(const std::map<std::string, std::string>& defaults);
 std::string with_scheme(const std::string& addr, bool tls = false);
 std::vector<std::string> split_csv(const std::string& s);
 // "3@http://h:p" -> (3, url); "...metaserver-N..." -> (N + 1, url); else (-1, url)

@@ -5,9 +5,9 @@
 // the native Raft node, the HTTP/2 gRPC server (ConfigService + /dfs.RaftPeer/*), the
 // same-host socket listener, and the HTTP side channel (/raft/{vote,append,snapshot,
 // timeout_now}, /raft/state, /raft/endpoint, /shards, /health, /metrics). No Python runs in
-// it; config_server/server.py stays as the A/B launcher (DFS_NATIVE_CONTROL=0).
+// it.
 //
-// Flags (same spelling as the Python shell and the reference): --addr, --id, --peers,
+// Flags (the reference's spelling and defaults, printed by --help): --addr, --id, --peers,
 // --http-port, --advertise-addr, --storage-dir, --tls-cert, --tls-key, --ca-cert,
 // --no-fsync, --snapshot-threshold.
 #include <cstdio>
@@ -32,14 +32,22 @@ static const char* kUsage =
     "                         [--tls-key TLS_KEY] [--ca-cert CA_CERT] [--no-fsync]\n"
     "                         [--snapshot-threshold SNAPSHOT_THRESHOLD]\n";
 
+// The reference's defaults (bin/config_server.rs:19-48), printed by --help.
+const std::map<std::string, std::string> kDefaults = {{"addr", "127.0.0.1:50052"},
+                                                      {"id", "1"},
+                                                      {"http-port", "8081"},
+                                                      {"storage-dir", "/tmp/config-raft-logs"},
+                                                      {"snapshot-threshold", "10000"}};
+
 int main(int argc, char** argv) {
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--help" || std::string(argv[i]) == "-h") {
       std::fputs(kUsage, stdout);
+      std::fputs(defaults_help(kDefaults).c_str(), stdout);
       return 0;
     }
   block_stop_signals();
-  Args a(argc, argv, {"no-fsync"});
+  Args a(argc, argv, {"no-fsync"}, {}, kDefaults);
   if (!a.error().empty()) {
     std::fprintf(stderr, "dfs_config_server: %s\n", a.error().c_str());
     return 2;

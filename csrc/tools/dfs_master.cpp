@@ -3,8 +3,8 @@
 //
 // One Raft member of a metadata shard. MasterCore (master_core.cpp) holds the replicated
 // namespace and answers the hot MasterService RPCs and the 2PC coordinator/participant
-// RPCs; this executable owns everything around it that the Python shell (master/server.py,
-// service.py, background.py) used to run, so no interpreter lives in a master process:
+// RPCs; this executable owns everything around it, so no interpreter lives in a master
+// process:
 //
 //   * the native Raft node with a native host (peer RPCs over the peers' HTTP/2 endpoints,
 //     HTTP/JSON to peers without one), snapshots backed up with a PUT when configured;
@@ -1187,14 +1187,23 @@ const char* kUsage =
     "                  [--backup-bucket BACKUP_BUCKET] [--snapshot-threshold SNAPSHOT_THRESHOLD] [--no-fsync]\n"
     "                  [--fast-intervals] [--http-host HTTP_HOST]\n";
 
+// The reference's defaults (bin/master.rs:21-80), printed by --help.
+const std::map<std::string, std::string> kDefaults = {
+    {"addr", "127.0.0.1:50051"},   {"id", "1"},
+    {"http-port", "8080"},         {"storage-dir", "/tmp/raft-logs"},
+    {"shard-id", "shard-0"},       {"split-threshold-rps", "100.0"},
+    {"split-cooldown-secs", "30"}, {"merge-threshold-rps", "1.0"},
+    {"backup-bucket", "dfs-backups"}, {"snapshot-threshold", "10000"}};
+
 int main(int argc, char** argv) {
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--help" || std::string(argv[i]) == "-h") {
       std::fputs(kUsage, stdout);
+      std::fputs(defaults_help(kDefaults).c_str(), stdout);
       return 0;
     }
   block_stop_signals();
-  Args a(argc, argv, {"standby", "no-fsync", "fast-intervals"}, {{"a", "addr"}});
+  Args a(argc, argv, {"standby", "no-fsync", "fast-intervals"}, {{"a", "addr"}}, kDefaults);
   if (!a.error().empty()) {
     std::fprintf(stderr, "dfs_master: %s\n", a.error().c_str());
     return 2;

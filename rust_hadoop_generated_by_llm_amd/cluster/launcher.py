@@ -27,11 +27,10 @@ ROOT = Path(__file__).resolve().parents[2]
 
 _handed_out: set[int] = set()
 
-# Roles with a native executable (csrc/tools/dfs_master.cpp, dfs_config_server.cpp,
-# dfs_chunkserver.cpp): with DFS_NATIVE_CONTROL unset or 1 they run as those binaries, so no
-# Python interpreter lives in a master, config-server or chunkserver process;
-# DFS_NATIVE_CONTROL=0 (or DFS_NATIVE_CHUNKSERVER=0 for the chunkservers alone) keeps the
-# Python shells (the A/B launcher).
+# Roles that run as native executables (csrc/tools/dfs_master.cpp, dfs_config_server.cpp,
+# dfs_chunkserver.cpp), so no Python interpreter lives in a master, config-server or chunkserver
+# process. Masters and config servers have no other form; DFS_NATIVE_CHUNKSERVER=0 (or a knob
+# only the Python shell serves) starts the chunkserver's Python shell as the A/B.
 NATIVE_BINARIES = {"master.server": "dfs_master", "config_server.server": "dfs_config_server",
                    "chunkserver.server": "dfs_chunkserver"}
 
@@ -50,7 +49,9 @@ def role_command(module: str, args: list[str], environ: dict | None = None) -> l
     exe = ROOT / "build" / "native" / NATIVE_BINARIES.get(module, "-")
     if module == "chunkserver.server" and _python_chunkserver(args, env):
         return [sys.executable, "-m", f"{PKG}.{module}", *args]
-    if module in NATIVE_BINARIES and env.get("DFS_NATIVE_CONTROL", "1") != "0" and exe.exists():
+    if module in NATIVE_BINARIES:
+        if not exe.exists():
+            raise FileNotFoundError(f"{exe} is not built (python build_native.py)")
         return [str(exe), *args]
     return [sys.executable, "-m", f"{PKG}.{module}", *args]
 

@@ -11,6 +11,9 @@
 #   n2        2 ranks sharing the GPU (hipipc, RF 2)
 #   prof      rocprofv3 kernel trace of the chunkserver during a short bench
 #   configs   BASELINE configs 4 and 5
+#   secure    config 5 at production settings (TLS + SigV4/STS + IAM + SSE-S3 + audit)
+#   crcpmc    two rocprofv3 PMC passes over crc_bench (LDS/VALU, then MFMA busy vs GPU-active)
+#   probe     the box's block devices and mounts (where per-rank journals could live)
 set -o pipefail
 cd "$(dirname "$0")/.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -50,6 +53,20 @@ for step in "$@"; do
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
+    secure)
+      run config5_secure 600 python bench_configs.py config5 --gpu 0 --secure || exit 1 ;;
+    crcpmc)
+      R=$PWD
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS \
+         SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU \
+         -d "$R/$O/pmc_crc" -o crc --output-format csv -- "$R/build/native/crc_bench" --iters 5 --mib 256 \
+         > "$R/$O/pmc_crc.log" 2>&1) && \
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES \
+         SQ_WAVES GRBM_GUI_ACTIVE -d "$R/$O/pmc_mfma" -o crc --output-format csv -- "$R/build/native/crc_bench" \
+         --iters 5 --mib 256 > "$R/$O/pmc_mfma.log" 2>&1) || exit 1 ;;
+    probe)
+      { lsblk -o NAME,SIZE,TYPE,MOUNTPOINT,ROTA,MODEL 2>&1; df -h 2>&1; cat /proc/mounts; nproc; free -g; } \
+        > "$O/probe.txt" 2>&1 || true ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done

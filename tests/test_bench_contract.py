@@ -131,3 +131,24 @@ def test_bench_refuses_a_mismatched_world(tmp_path):
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu", "--steps", "1"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and not p.stdout.strip()
+
+
+def test_bench_transport_ab_block(tmp_path):
+    """--transport-ab: after the primary run, a short second measurement over the other replica
+    transport in the same job; the one JSON line carries both (the first multi-GPU run records
+    hipipc and RCCL side by side). On CPU the pair is socket -> grpc."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(TMPDIR=str(tmp_path))
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu", "--steps", "2", "--warmup", "1",
+                        "--count", "8", "--remote-steps", "0", "--transport", "socket", "--transport-ab", "on"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    _check_common(d, 2, 2, 1)
+    assert d["config"]["transport"] == "socket" and d["p2p_forwards"] > 0
+    ab = d["transport_ab"]["grpc"]
+    assert "error" not in ab, ab
+    # without a P2P pair the next server stages from the writer's slot (same host): "shm"
+    assert ab["value"] > 0 and ab["transport"] in ("grpc", "shm") and ab["p2p_forwards"] == 0

@@ -582,21 +582,6 @@ def test_2pc_recovery_finishes_commit_after_coordinator_loss():
         assert _master_metric_sum(cl, "dfs_master_tx_native_pending") >= 1
 
 
-def test_2pc_python_coordinator_still_serves():
-    """DFS_NATIVE_2PC=0 keeps the Python coordinator (master/service.py) as the A/B path;
-    both coordinators write the same records, so its renames still commit."""
-    # the Python coordinator lives in the Python master shell (DFS_NATIVE_CONTROL=0)
-    with LocalCluster(n_chunkservers=2, shards=2, fsync=False,
-                      env={"DFS_NATIVE_2PC": "0", "DFS_NATIVE_CONTROL": "0"}) as cl:
-        c = cl.client()
-        c.create_file_from_buffer(b"py", "/a/py")
-        c.rename_file("/a/py", "/z/py")
-        assert c.get_file_content("/z/py") == b"py" and not c.exists("/a/py")
-        c.close()
-        assert _master_metric_sum(cl, "dfs_master_tx_declined") >= 1
-        assert _master_metric_sum(cl, "dfs_master_tx_native_started") == 0
-
-
 def test_idle_shard_merges_and_becomes_standby():
     """C31 merge: with total rps below --merge-threshold-rps an idle shard pushes its files
     to its neighbour, the config server drops its range, and the master re-registers as a

@@ -7,7 +7,7 @@ import time
 from hypothesis import given, settings
 from hypothesis import strategies as st
 
-from rust_hadoop_generated_by_llm_amd.config_server.server import ConfigState
+from .harness.config_state import ConfigState
 from rust_hadoop_generated_by_llm_amd.native import lib
 from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
 
@@ -133,8 +133,8 @@ def test_native_config_service_over_grpc_and_local_socket(tmp_path):
     import pytest
 
     from rust_hadoop_generated_by_llm_amd.models import proto as pb
-    from rust_hadoop_generated_by_llm_amd.raft.node import RaftNode
-    from rust_hadoop_generated_by_llm_amd.raft.transport import LocalTransport
+    from .harness.raft_node import RaftNode
+    from .harness.raft_transport import LocalTransport
     from rust_hadoop_generated_by_llm_amd.utils.localrpc import socket_name
     from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
 

@@ -8,12 +8,12 @@ import time
 
 import pytest
 
-from rust_hadoop_generated_by_llm_amd.master.state import ChunkServerStatus, MasterState, select_servers_rack_aware
+from .harness.master_state import ChunkServerStatus, MasterState, select_servers_rack_aware
 from rust_hadoop_generated_by_llm_amd.models import meta as M
 from rust_hadoop_generated_by_llm_amd.models import proto as pb
 from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
-from rust_hadoop_generated_by_llm_amd.raft.node import RaftNode
-from rust_hadoop_generated_by_llm_amd.raft.transport import LocalTransport
+from .harness.raft_node import RaftNode
+from .harness.raft_transport import LocalTransport
 
 FOREVER = 9_999_999_999_999
 T = pb.ChunkServerCommand

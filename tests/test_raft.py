@@ -5,9 +5,9 @@ import asyncio
 
 import pytest
 
-from rust_hadoop_generated_by_llm_amd.raft.membership import CatchUpProgress, ClusterConfiguration, initial_members
-from rust_hadoop_generated_by_llm_amd.raft.node import LEADER, NotLeader, RaftNode
-from rust_hadoop_generated_by_llm_amd.raft.transport import FaultInjector, LocalTransport
+from .harness.raft_membership import CatchUpProgress, ClusterConfiguration, initial_members
+from .harness.raft_node import LEADER, NotLeader, RaftNode
+from .harness.raft_transport import FaultInjector, LocalTransport
 
 
 class KV:

@@ -14,9 +14,9 @@ from hypothesis import strategies as st
 
 from rust_hadoop_generated_by_llm_amd.client.checker import check_linearizability, parse_history
 from rust_hadoop_generated_by_llm_amd.native import lib as native
-from rust_hadoop_generated_by_llm_amd.raft.membership import ClusterConfiguration
-from rust_hadoop_generated_by_llm_amd.raft.node import LEADER, NotLeader
-from rust_hadoop_generated_by_llm_amd.raft.transport import TransportError
+from .harness.raft_membership import ClusterConfiguration
+from .harness.raft_node import LEADER, NotLeader
+from .harness.raft_transport import TransportError
 
 from .test_raft import Cluster, run
 
