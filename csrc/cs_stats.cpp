@@ -146,6 +146,8 @@ Json stats_json(const ReplStats& t) {
   d.set("channel_waits", t.channel_waits);
   d.set("parked_extents", t.parked_extents);
   d.set("reaped_extents", t.reaped_extents);
+  for (auto& kv : t.sent_to) d.set("link_sent_to_" + std::to_string(kv.first), kv.second);
+  for (auto& kv : t.recv_from) d.set("link_recv_from_" + std::to_string(kv.first), kv.second);
   return d;
 }
 

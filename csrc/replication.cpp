@@ -638,6 +638,7 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
     std::lock_guard<std::mutex> lk(st_mu_);
     st_.bytes_sent += t->size;
     st_.blocks_sent++;
+    st_.sent_to[t->peer] += t->size;
   }
   return ok;
 }
@@ -781,6 +782,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
     std::lock_guard<std::mutex> lk(st_mu_);
     st_.bytes_recv += size;
     st_.blocks_recv++;
+    st_.recv_from[src] += size;
   }
   return res;
 }

@@ -91,6 +91,8 @@ struct ReplStats {
   uint64_t pair_failures = 0, pair_opens = 0, open_attempts = 0, turn_timeouts = 0, stale_generation = 0;
   uint64_t channel_waits = 0;  // sends that found their channel's turn taken and waited for it
   uint64_t parked_extents = 0, reaped_extents = 0;  // failed-receive extents held / freed after close
+  // bytes of completed transfers by peer rank: what each link carried (multi-GPU diagnosis)
+  std::map<int, uint64_t> sent_to, recv_from;
 };
 
 class ReplicationEngine {
