@@ -3,10 +3,9 @@
 // The reference CLI is a Rust binary over its Rust client library; this is the C++ one over
 // the native client (client_remote.cpp: every RPC over gRPC/TCP on nghttp2, TLS when the
 // endpoints are https). Same global flags and output as the Python CLI
-// (rust_hadoop_generated_by_llm_amd/cli/dfs_cli.py), which stays the implementation of the
-// tooling commands this binary hands over to it as a child process (workload, check-history,
-// presign, cluster up/add-server/remove-server, shuffle) and of the few data operations the
-// native client does not own (files over one block, paths another shard must serve):
+// (rust_hadoop_generated_by_llm_amd/cli/dfs_cli.py), to which this binary hands only
+// `cluster up` (the local multi-process launcher) and the few data operations the native
+// client does not own (files over one block), as a child process:
 //
 //   dfs_cli [-m MASTER[,..]] [--config-servers A,B] [--max-retries N] [--initial-backoff-ms MS]
 //           [--host-alias a=b ...] [--ca-cert F] [--domain-name D] [--hedge-delay-ms MS]
@@ -14,6 +13,10 @@
 //     rename SRC DEST | delete PATH | safe-mode get|enter|leave | cluster info
 //     benchmark write [-c N -s BYTES -n CONC -p PREFIX --json] | benchmark read [-p -n --json]
 //     benchmark stress-write [-d SECS -s BYTES -n CONC -p PREFIX --json]
+//     cluster add-server ID ADDR | cluster remove-server ID | shuffle PREFIX
+//     workload --history F [--ops N --clients N --key-space N --rename-ratio R]
+//     check-history [PATH] [--self-test]   (csrc/lin_checker.cpp: WGL per key component)
+//     presign s3://bucket/key [--method GET|PUT|DELETE] [--expires S] [--endpoint URL]
 //
 // Master RPCs follow the reference client's retry policy (mod.rs:1170-1290): Not Leader
 // hints (status text "Not Leader|addr" or a response's leader_hint), REDIRECT:<addr> from a
@@ -41,10 +44,13 @@
 #include <vector>
 
 #include "client_remote.h"
+#include "crypto.h"
 #include "dfs_pb.h"
 #include "grpc_client.h"
 #include "json.h"
+#include "lin_checker.h"
 #include "shard_map.h"
+#include "sigv4.h"
 #include "tls.h"
 
 using namespace dfs;
@@ -86,8 +92,9 @@ struct Args {
 // Options of the commands this binary runs (anything else goes to the Python CLI).
 const std::map<std::string, std::string> kShort = {{"-c", "--count"}, {"-s", "--size"}, {"-n", "--concurrency"},
                                                    {"-p", "--prefix"}, {"-d", "--duration"}};
-const std::set<std::string> kValued = {"--count", "--size", "--concurrency", "--prefix", "--duration", "--ec-data",
-                                       "--ec-parity"};
+const std::set<std::string> kValued = {"--count",   "--size",       "--concurrency", "--prefix",  "--duration",
+                                       "--ec-data", "--ec-parity",  "--method",      "--expires", "--endpoint",
+                                       "--ops",     "--clients",    "--key-space",   "--rename-ratio", "--history"};
 
 Args parse(int argc, char** argv) {
   Args a;
@@ -127,9 +134,9 @@ bool native_command(const Args& a) {
   const std::string sub = a.pos.size() > 1 ? a.pos[1] : "";
   if (c == "ls" || c == "get" || c == "inspect" || c == "rename" || c == "delete" || c == "put") return true;
   if (c == "safe-mode") return sub == "get" || sub == "enter" || sub == "leave";
-  if (c == "cluster") return sub == "info";
+  if (c == "cluster") return sub == "info" || sub == "add-server" || sub == "remove-server";
   if (c == "benchmark") return sub == "write" || sub == "read" || sub == "stress-write";
-  return false;
+  return c == "shuffle" || c == "workload" || c == "check-history" || c == "presign";
 }
 
 // The Python CLI as a child process (this process never touches the GPU), same argv.
@@ -565,6 +572,224 @@ int cmd_benchmark(Cli& cli, const Args& a) {
   return 0;
 }
 
+// ---------------------------------------------------------------- tooling commands
+std::string opt_or(const Args& a, const std::string& k, const std::string& d) {
+  auto it = a.opt.find(k);
+  return it == a.opt.end() ? d : it->second;
+}
+
+// presign (reference auth/presign.rs:17-88, dfs_cli.rs presign): query-string SigV4 over the
+// host header only, UNSIGNED-PAYLOAD, credentials from the AWS_* environment.
+int cmd_presign(const Args& a) {
+  const char* ak = std::getenv("AWS_ACCESS_KEY_ID");
+  const char* sk = std::getenv("AWS_SECRET_ACCESS_KEY");
+  if (!ak || !*ak) return std::fprintf(stderr, "AWS_ACCESS_KEY_ID environment variable not set\n"), 1;
+  if (!sk || !*sk) return std::fprintf(stderr, "AWS_SECRET_ACCESS_KEY environment variable not set\n"), 1;
+  const char* rg = std::getenv("AWS_REGION");
+  if (!rg || !*rg) rg = std::getenv("AWS_DEFAULT_REGION");
+  const std::string region = rg && *rg ? rg : "us-east-1";
+  const char* ep = std::getenv("S3_ENDPOINT");
+  std::string endpoint = opt_or(a, "--endpoint", ep && *ep ? ep : "http://localhost:9000");
+  if (a.pos.size() < 2) return std::fprintf(stderr, "presign: missing URL\n"), 1;
+  const std::string url = a.pos[1];
+  if (!starts_with(url, "s3://")) return std::fprintf(stderr, "URL must start with s3://\n"), 1;
+  const std::string rest = url.substr(5);
+  const size_t slash = rest.find('/');
+  if (slash == std::string::npos) return std::fprintf(stderr, "URL must contain a key (s3://bucket/key)\n"), 1;
+  const std::string bucket = rest.substr(0, slash), key = rest.substr(slash + 1);
+  if (bucket.empty() || key.empty()) return std::fprintf(stderr, "Bucket and key must not be empty\n"), 1;
+  std::string method = opt_or(a, "--method", "GET");
+  for (auto& ch : method) ch = static_cast<char>(std::toupper(static_cast<unsigned char>(ch)));
+  if (method != "GET" && method != "PUT" && method != "DELETE")
+    return std::fprintf(stderr, "Unsupported method '%s'. Supported methods: GET, PUT, DELETE\n",
+                        opt_or(a, "--method", "GET").c_str()), 1;
+  const long long expires = std::atoll(opt_or(a, "--expires", "3600").c_str());
+  if (expires < 1 || expires > 604800) return std::fprintf(stderr, "--expires must be between 1 and 604800 seconds\n"), 1;
+  char date[16], amz[32];
+  std::time_t now = std::time(nullptr);
+  std::tm t{};
+  gmtime_r(&now, &t);
+  std::strftime(date, sizeof date, "%Y%m%d", &t);
+  std::strftime(amz, sizeof amz, "%Y%m%dT%H%M%SZ", &t);
+  const std::string scope = std::string(date) + "/" + region + "/s3/aws4_request";
+  std::vector<std::pair<std::string, std::string>> params = {
+      {"X-Amz-Algorithm", "AWS4-HMAC-SHA256"}, {"X-Amz-Credential", std::string(ak) + "/" + scope},
+      {"X-Amz-Date", amz}, {"X-Amz-Expires", std::to_string(expires)}, {"X-Amz-SignedHeaders", "host"}};
+  for (auto& kv : params) kv = {sigv4::uri_encode(kv.first, true), sigv4::uri_encode(kv.second, true)};
+  std::sort(params.begin(), params.end());
+  std::string cq;
+  for (auto& kv : params) cq += (cq.empty() ? "" : "&") + kv.first + "=" + kv.second;
+  while (!endpoint.empty() && endpoint.back() == '/') endpoint.pop_back();
+  std::string host = endpoint.substr(endpoint.find("://") == std::string::npos ? 0 : endpoint.find("://") + 3);
+  std::string path = "/" + sigv4::uri_encode(bucket, true);
+  for (size_t p = 0; p <= key.size();) {
+    size_t q = key.find('/', p);
+    path += "/" + sigv4::uri_encode(key.substr(p, q == std::string::npos ? std::string::npos : q - p), true);
+    if (q == std::string::npos) break;
+    p = q + 1;
+  }
+  sigv4::Request r;
+  r.method = method;
+  r.path = path;
+  r.query = cq;
+  r.headers = {{"host", host}};
+  r.signed_headers = "host";
+  r.payload_hash = "UNSIGNED-PAYLOAD";
+  const std::string sig = sigv4::signature(sigv4::signing_key(sk, date, region, "s3"),
+                                           sigv4::string_to_sign(amz, scope, sigv4::canonical_request(r)));
+  std::printf("%s%s?%s&X-Amz-Signature=%s\n", endpoint.c_str(), path.c_str(), cq.c_str(), sig.c_str());
+  return 0;
+}
+
+int cmd_check_history(const Args& a) {
+  if (a.flags.count("--self-test")) {
+    auto f = lin::self_test();
+    if (!f.empty()) {
+      std::string all;
+      for (auto& x : f) all += (all.empty() ? "" : "; ") + x;
+      std::fprintf(stderr, "Checker self-test FAILED: %s\n", all.c_str());
+      return 1;
+    }
+    std::printf("All checker self-tests passed.\n");
+    return 0;
+  }
+  if (a.pos.size() < 2) return std::fprintf(stderr, "check-history needs a history file (or --self-test)\n"), 1;
+  std::ifstream in(a.pos[1]);
+  if (!in) return std::fprintf(stderr, "Cannot open %s: %s\n", a.pos[1].c_str(), std::strerror(errno)), 1;
+  std::vector<lin::Op> ops;
+  std::string err;
+  if (!lin::parse_history(in, &ops, &err)) return std::fprintf(stderr, "Parse error: %s\n", err.c_str()), 1;
+  std::printf("Parsed %zu operations\n", ops.size());
+  auto v = lin::check(ops);
+  if (!v.empty()) {
+    std::fprintf(stderr, "Linearizability FAILED:\n");
+    for (auto& x : v) std::fprintf(stderr, "  - %s\n", x.c_str());
+    return 1;
+  }
+  std::printf("Linearizability check PASSED\n");
+  return 0;
+}
+
+std::string json_esc(const std::string& v) {
+  std::string o;
+  for (char ch : v) {
+    if (ch == '"' || ch == '\\') o.push_back('\\');
+    o.push_back(ch);
+  }
+  return o;
+}
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+// workload (reference workload.rs; client/workload.py): `clients` threads x `ops` operations
+// over `key_space` paths (/a/lin_i for even i, /z/lin_i for odd i, so renames cross shards), a
+// `rename_ratio` share renames and the rest split over put/get/delete, every invoke and return
+// recorded as a JSONL history for check-history.
+int cmd_workload(Cli& cli, const Args& a) {
+  const std::string hist = opt_or(a, "--history", "");
+  if (hist.empty()) throw CliError("workload: --history is required");
+  const int ops = std::atoi(opt_or(a, "--ops", "50").c_str());
+  const int clients = std::atoi(opt_or(a, "--clients", "5").c_str());
+  const int keys = std::max(1, std::atoi(opt_or(a, "--key-space", "4").c_str()));
+  const double rename_ratio = std::atof(opt_or(a, "--rename-ratio", "0.3").c_str());
+  std::ofstream out(hist, std::ios::trunc);
+  if (!out) throw CliError("cannot open " + hist);
+  std::mutex mu;
+  std::atomic<int64_t> next_id{0};
+  auto rec = [&](const std::string& line) {
+    std::lock_guard<std::mutex> g(mu);
+    out << line << "\n";
+    out.flush();
+  };
+  auto key_path = [](int i) { return (i % 2 == 0 ? "/a/lin_" : "/z/lin_") + std::to_string(i); };
+  auto classify = [](const std::string& m) {
+    return m.find("not found") != std::string::npos || m.find("Not found") != std::string::npos ? "not_found"
+                                                                                                 : "error";
+  };
+  RemoteClient& rc = cli.client();
+  std::random_device rd;
+  const uint64_t seed0 = (static_cast<uint64_t>(rd()) << 32) ^ rd();
+  std::vector<std::thread> th;
+  for (int cidx = 0; cidx < clients; ++cidx)
+    th.emplace_back([&, cidx] {
+      std::mt19937_64 rng(seed0 + static_cast<uint64_t>(cidx) * 0x9E3779B97F4A7C15ull);
+      std::uniform_real_distribution<double> u(0, 1);
+      const std::string name = "client_" + std::to_string(cidx);
+      for (int k = 0; k < ops; ++k) {
+        const int64_t id = next_id++;
+        const std::string base = "{\"id\": " + std::to_string(id) + ", \"client\": \"" + name + "\"";
+        const double r = u(rng);
+        if (r < rename_ratio) {
+          int s = 0, d = 0;
+          if (keys > 1) {
+            s = static_cast<int>(rng() % keys);
+            do d = static_cast<int>(rng() % keys);
+            while (d == s);
+          }
+          const std::string src = key_path(s), dst = key_path(d);
+          rec(base + ", \"type\": \"invoke\", \"op\": \"rename\", \"src\": \"" + src + "\", \"dst\": \"" + dst +
+              "\", \"ts_ns\": " + std::to_string(now_ns()) + "}");
+          std::string res = "ok";
+          try {
+            pb::RenameRequest q;
+            q.source_path = src;
+            q.dest_path = dst;
+            pb::RenameResponse resp;
+            resp.decode(cli.call(cli.targets_for(src), "Rename", q.str(), body_not_leader<pb::RenameResponse>));
+            if (!resp.success) res = classify(resp.error_message);
+          } catch (const std::exception& e) {
+            res = classify(e.what());
+          }
+          rec(base + ", \"type\": \"return\", \"op\": \"rename\", \"result\": \"" + res + "\", \"ts_ns\": " +
+              std::to_string(now_ns()) + "}");
+          continue;
+        }
+        const int which = std::min(2, static_cast<int>((r - rename_ratio) / ((1 - rename_ratio) / 3)));
+        const std::string kind = which == 0 ? "put" : which == 1 ? "get" : "delete";
+        const std::string path = key_path(static_cast<int>(rng() % keys));
+        std::string res;
+        if (kind == "put") {
+          const std::string data = "data_" + std::to_string(id) + "_" + std::to_string(now_ns());
+          const std::string h = crypto::md5_hex(reinterpret_cast<const uint8_t*>(data.data()), data.size());
+          rec(base + ", \"type\": \"invoke\", \"op\": \"put\", \"path\": \"" + path + "\", \"data_hash\": \"" + h +
+              "\", \"ts_ns\": " + std::to_string(now_ns()) + "}");
+          std::string e;
+          res = write_one(rc, path, data, &e) >= 0 ? "put_ok:" + h : "error";
+        } else if (kind == "get") {
+          rec(base + ", \"type\": \"invoke\", \"op\": \"get\", \"path\": \"" + path + "\", \"ts_ns\": " +
+              std::to_string(now_ns()) + "}");
+          std::string data, msg;
+          RemoteClient::Times t;
+          auto st = rc.read(path, &data, &msg, &t);
+          res = st == FastClient::Ok
+                    ? "get_ok:" + crypto::md5_hex(reinterpret_cast<const uint8_t*>(data.data()), data.size())
+                    : classify(msg);
+        } else {
+          rec(base + ", \"type\": \"invoke\", \"op\": \"delete\", \"path\": \"" + path + "\", \"ts_ns\": " +
+              std::to_string(now_ns()) + "}");
+          res = "ok";
+          try {
+            pb::DeleteFileRequest q;
+            q.path = path;
+            pb::DeleteFileResponse resp;
+            resp.decode(cli.call(cli.targets_for(path), "DeleteFile", q.str(), body_not_leader<pb::DeleteFileResponse>));
+            if (!resp.success) res = classify(resp.error_message);
+          } catch (const std::exception& e) {
+            res = classify(e.what());
+          }
+        }
+        rec(base + ", \"type\": \"return\", \"op\": \"" + kind + "\", \"path\": \"" + json_esc(path) +
+            "\", \"result\": \"" + res + "\", \"ts_ns\": " + std::to_string(now_ns()) + "}");
+      }
+    });
+  for (auto& t : th) t.join();
+  std::printf("Workload completed.\n");
+  return 0;
+}
+
 // ---------------------------------------------------------------- the other commands
 int run(Cli& cli, const Args& a, int argc, char** argv) {
   const std::string& c = a.pos.at(0);
@@ -594,6 +819,51 @@ int run(Cli& cli, const Args& a, int argc, char** argv) {
     std::printf("Failed to %s Safe Mode: %s\n", enter ? "enter" : "leave", r.error_message.c_str());
     return 1;
   }
+  if (c == "cluster" && a.pos.at(1) != "info") {
+    const bool add = a.pos[1] == "add-server";
+    need(add ? 3 : 2);
+    std::string raw;
+    if (add) {
+      pb::AddRaftServerRequest q;
+      q.server_id = static_cast<uint32_t>(std::strtoul(a.pos[2].c_str(), nullptr, 10));
+      q.server_address = a.pos[3];
+      raw = cli.admin("AddRaftServer", q.str());
+    } else {
+      pb::RemoveRaftServerRequest q;
+      q.server_id = static_cast<uint32_t>(std::strtoul(a.pos[2].c_str(), nullptr, 10));
+      raw = cli.admin("RemoveRaftServer", q.str());
+    }
+    bool success;
+    std::string error_message, leader_hint;
+    if (add) {
+      pb::AddRaftServerResponse r;
+      r.decode(raw);
+      success = r.success, error_message = r.error_message, leader_hint = r.leader_hint;
+    } else {
+      pb::RemoveRaftServerResponse r;
+      r.decode(raw);
+      success = r.success, error_message = r.error_message, leader_hint = r.leader_hint;
+    }
+    if (success) {
+      if (add) std::printf("Added server %s (%s) to cluster\n", a.pos[2].c_str(), a.pos[3].c_str());
+      else std::printf("Removed server %s from cluster\n", a.pos[2].c_str());
+      return 0;
+    }
+    std::printf("Failed to %s server: %s\n", add ? "add" : "remove", error_message.c_str());
+    if (!leader_hint.empty()) std::printf("Leader hint: %s\n", leader_hint.c_str());
+    return 1;
+  }
+  if (c == "shuffle") {
+    need(1);
+    pb::InitiateShuffleRequest q;
+    q.prefix = a.pos[1];
+    pb::InitiateShuffleResponse r;
+    r.decode(cli.call(cli.targets_for(q.prefix), "InitiateShuffle", q.str(), body_not_leader<pb::InitiateShuffleResponse>));
+    if (!r.success) throw CliError("Shuffle failed: " + r.error_message);
+    std::printf("Triggered background shuffling for prefix: %s\n", q.prefix.c_str());
+    return 0;
+  }
+  if (c == "workload") return cmd_workload(cli, a);
   if (c == "cluster") {
     pb::GetClusterInfoResponse r;
     r.decode(cli.admin("GetClusterInfo", std::string()));
@@ -709,6 +979,9 @@ int main(int argc, char** argv) {
     return 2;
   }
   if (!native_command(a) || std::getenv("DFS_CLI_PYTHON")) return run_python(argc, argv);
+  // commands that need no cluster
+  if (a.pos[0] == "presign") return cmd_presign(a);
+  if (a.pos[0] == "check-history") return cmd_check_history(a);
   try {
     Cli cli(a);
     return run(cli, a, argc, argv);

@@ -11,7 +11,6 @@ import urllib.request
 
 import pytest
 
-from rust_hadoop_generated_by_llm_amd.cli import dfs_cli
 from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster, free_port
 from rust_hadoop_generated_by_llm_amd.models import proto as pb
 from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
@@ -20,9 +19,14 @@ pytestmark = pytest.mark.slow
 
 
 def cli(capsys, *args):
-    rc = dfs_cli.main(list(args))
-    out = capsys.readouterr()
-    return rc, out.out + out.err
+    """The native dfs_cli executable, as an operator runs it (cluster admin is native)."""
+    import subprocess
+    from pathlib import Path
+
+    exe = Path(__file__).resolve().parents[1] / "build" / "native" / "dfs_cli"
+    p = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=60,
+                       env={"PATH": "/nonexistent"})  # no python3 on PATH: nothing is handed over
+    return p.returncode, p.stdout + p.stderr
 
 
 def info(pool, addr):

@@ -2,7 +2,8 @@
 clusters: the same commands and output as the Python CLI's test (test_cluster.py::
 test_cli_commands, reference dfs/client/src/bin/dfs_cli.rs), run as a separate process over
 gRPC/TCP, plus a two-shard cluster reached through the config server (shard map fetch, routing,
-cross-shard rename) and the hand-over of tooling commands to the Python CLI."""
+cross-shard rename, a linearizability workload across both shards) and the tooling commands
+(shuffle, presign, workload, check-history, cluster add/remove-server in test_membership.py)."""
 import json
 import os
 import subprocess
@@ -84,14 +85,53 @@ def test_native_cli_commands(cluster3, tmp_path):
     assert rc == 0 and "No files found" in out
 
 
-def test_native_cli_hands_tooling_commands_to_python(cluster3, tmp_path):
+NO_PYTHON = {"PATH": "/nonexistent"}  # no python3 to hand anything to: the command ran natively
+
+
+def test_native_cli_tooling_commands(cluster3, tmp_path):
+    """shuffle, presign, check-history and workload run in the executable (reference
+    dfs_cli.rs:45-199,471-522), with no Python CLI to fall back to."""
+    from rust_hadoop_generated_by_llm_amd.s3.auth import sigv4
+
     m = ["-m", cluster3.master_addrs[0]]
-    rc, out, err = run(*m, "shuffle", "/ncli")
+    rc, out, err = run(*m, "shuffle", "/ncli", env=NO_PYTHON)
     assert rc == 0 and "Triggered background shuffling" in out, err
-    rc, out, err = run("check-history", "--self-test")
+    rc, out, err = run("check-history", "--self-test", env=NO_PYTHON)
     assert rc == 0 and "self-tests passed" in out, err
-    rc, out, err = run("presign", "s3://b/k", env={"AWS_ACCESS_KEY_ID": "AK", "AWS_SECRET_ACCESS_KEY": "SK"})
-    assert rc == 0 and "X-Amz-Signature=" in out, err
+    # presign: byte-identical to the Python generator at the same timestamp
+    env = dict(NO_PYTHON, AWS_ACCESS_KEY_ID="AK", AWS_SECRET_ACCESS_KEY="SK", AWS_REGION="us-east-1")
+    rc, out, err = run("presign", "s3://bucket/dir/obj.txt", "--method", "put", "--expires", "120",
+                       "--endpoint", "http://127.0.0.1:9000", env=env)
+    assert rc == 0, err
+    url = out.strip()
+    dt = url.split("X-Amz-Date=")[1].split("&")[0]
+    assert url == sigv4.generate_presigned_url("http://127.0.0.1:9000", "bucket", "dir/obj.txt", "PUT", "AK", "SK",
+                                               "us-east-1", 120, now=(dt[:8], dt))
+    assert run("presign", "s3://bucket/k", "--method", "POST", env=env)[0] == 1
+    assert run("presign", "s3://bucket/k", "--expires", "604801", env=env)[0] == 1
+    assert run("presign", "s3://b/k", env=NO_PYTHON)[0] == 1  # no credentials
+    # workload -> history -> checker, all native; the Python checker agrees
+    hist = tmp_path / "hist.jsonl"
+    rc, out, err = run(*m, "workload", "--ops", "15", "--clients", "3", "--key-space", "3", "--rename-ratio", "0.3",
+                       "--history", str(hist), env=NO_PYTHON)
+    assert rc == 0 and "Workload completed" in out, err
+    rc, out, err = run("check-history", str(hist), env=NO_PYTHON)
+    assert rc == 0 and "Parsed 45 operations" in out and "PASSED" in out, (out, err)
+    from rust_hadoop_generated_by_llm_amd.client import checker
+
+    with open(hist) as f:
+        assert checker.check_linearizability(checker.parse_history(f)) == []
+    # a history with a stale read fails, naming the operation
+    bad = tmp_path / "bad.jsonl"
+    bad.write_text("\n".join(json.dumps(r) for r in [
+        {"id": 1, "client": "c", "type": "invoke", "op": "put", "path": "/a", "data_hash": "h1", "ts_ns": 1},
+        {"id": 1, "client": "c", "type": "return", "result": "put_ok:h1", "ts_ns": 2},
+        {"id": 2, "client": "c", "type": "invoke", "op": "delete", "path": "/a", "ts_ns": 3},
+        {"id": 2, "client": "c", "type": "return", "result": "ok", "ts_ns": 4},
+        {"id": 3, "client": "c", "type": "invoke", "op": "get", "path": "/a", "ts_ns": 5},
+        {"id": 3, "client": "c", "type": "return", "result": "get_ok:h1", "ts_ns": 6}]) + "\n")
+    rc, out, err = run("check-history", str(bad), env=NO_PYTHON)
+    assert rc == 1 and "non-linearizable history over keys ['/a']" in err and "id=3 get" in err, err
     # DFS_CLI_PYTHON forces the Python implementation of a native command (same output)
     rc, out, _ = run(*m, "ls", env={"DFS_CLI_PYTHON": "1"})
     assert rc == 0
@@ -117,4 +157,11 @@ def test_native_cli_routes_through_the_config_server(tmp_path):
         assert run(*g, "get", "/z/dst", str(dst))[0] == 0 and dst.read_bytes() == b"moving"
         rc, _, err = run(*g, "rename", "/z/dst", "/z/taken")
         assert rc == 1 and "Rename failed" in err
+        # a workload whose renames cross the shards, checked natively
+        hist = tmp_path / "x.jsonl"
+        rc, out, err = run(*g, "workload", "--ops", "20", "--clients", "3", "--key-space", "4", "--rename-ratio", "0.4",
+                           "--history", str(hist), env=NO_PYTHON)
+        assert rc == 0, err
+        rc, out, err = run("check-history", str(hist), env=NO_PYTHON)
+        assert rc == 0 and "PASSED" in out, (out, err)
         c.close()
