@@ -226,6 +226,7 @@ def main():
         cleanly instead of losing it."""
         procs = Procs()
         done = threading.Event()
+        extra_dirs: list = []
         limit = min(a.timeout, 420.0) if alt else a.timeout
 
         def watchdog():
@@ -243,16 +244,28 @@ def main():
         threading.Thread(target=watchdog, daemon=True).start()
 
         tmp_parent = Path(os.environ.get("TMPDIR", "/tmp"))
+        # ranks spread over the node's local volumes when it has several (one NVMe drive per
+        # GPU is common on 8-GPU nodes): each rank's journal, blocks and master WAL live on
+        # volume rank % V, so replicas of different ranks do not share one device's queue
+        vols = bcast(_data_volumes(Path(a.workdir) if a.workdir else tmp_parent) if rank == 0 else None)
+        vols = vols if (n > 1 and not a.workdir) else vols[:1]
+        on_vol = [r for r in range(n) if r % len(vols) == rank % len(vols)]
         if rank == 0 and not a.workdir:
-            _make_room(tmp_parent, _bytes_needed(a, n))
-        base, journal_segs = bcast(((a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=str(tmp_parent))),
-                                    _journal_segments(Path(a.workdir) if a.workdir else tmp_parent, _bytes_needed(a, n), n))
-                                   if rank == 0 else None)
+            _make_room(tmp_parent, _bytes_needed(a, n) * len([r for r in range(n) if r % len(vols) == 0]) // max(1, n))
+        base = bcast((a.workdir or tempfile.mkdtemp(prefix="dfs_bench_", dir=str(tmp_parent))) if rank == 0 else None)
         base_p = Path(base)
         if rank == 0:
             base_p.mkdir(parents=True, exist_ok=True)
             (base_p / ".dfs_bench").touch()  # marks a directory _make_room may reclaim later
-        (base_p / f"rank{rank}").mkdir(parents=True, exist_ok=True)
+        my_vol = Path(vols[rank % len(vols)])
+        if rank % len(vols) == 0:
+            rank_dir = base_p / f"rank{rank}"
+        else:
+            rank_dir = my_vol / f"{base_p.name}_rank{rank}"
+            extra_dirs.append(rank_dir)
+        rank_dir.mkdir(parents=True, exist_ok=True)
+        journal_segs = _journal_segments(base_p if rank % len(vols) == 0 else my_vol,
+                                         _bytes_needed(a, n) * len(on_vol) // max(1, n), len(on_vol))
         env = dict(os.environ)
         env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
         env.setdefault("DFS_LOG", "warning")
@@ -293,7 +306,7 @@ def main():
                 # the C++ dfs_master executable
                 mp = procs.spawn_raw(role_command("master.server", [
                     "--addr", f"127.0.0.1:{gport}", "--http-port", str(hport),
-                    "--storage-dir", str(base_p / f"rank{rank}" / "master"),
+                    "--storage-dir", str(rank_dir / "master"),
                     "--shard-id", f"shard-{rank:03d}", "--shard-config", str(shard_file)], env),
                     str(base_p / f"master{rank}.log"), dict(env, DFS_READY_FILE=ready))
                 wait_file(ready, mp, 300, procs)
@@ -309,7 +322,7 @@ def main():
             gpu = -1 if a.cpu else local_rank % max(1, ndev)
             shared_gpu = (not a.cpu) and ndev < n  # rehearsal mode: several ranks on one GPU
             args = ["--addr", f"127.0.0.1:{cport}",
-                    "--http-port", str(chttp), "--storage-dir", str(base_p / f"rank{rank}" / "data"),
+                    "--http-port", str(chttp), "--storage-dir", str(rank_dir / "data"),
                     "--gpu", str(gpu), "--durability", a.durability, "--hbm-capacity", a.hbm_capacity,
                     "--heartbeat-interval", "0.5", "--scrub-interval", "3600", "--rccl-timeout-ms", "90000"]
             if n > 1 and (transport == "socket" or (not a.cpu and transport in ("hipipc", "hipipc-spin"))):
@@ -493,7 +506,7 @@ def main():
 
             # counters of the timed phase only (the stress / remote phases below add their own hops)
             stats = cs_stats()
-            vol = {"rank_dir_bytes": _allocated_bytes(base_p / f"rank{rank}"),
+            vol = {"rank_dir_bytes": _allocated_bytes(rank_dir), "volume": str(my_vol), "volumes_in_job": len(vols),
                    "journal_used_bytes": stats.get("journal_used_bytes", 0),
                    "journal_live_bytes": stats.get("journal_live_bytes", 0),
                    "exported_blocks": stats.get("materialized_blocks", 0),
@@ -652,6 +665,8 @@ def main():
             procs.stop()
             if rank == 0 and _should_clean(a, base):
                 shutil.rmtree(base, ignore_errors=True)
+            for d in extra_dirs:  # a rank's directory on another volume: always removed
+                shutil.rmtree(d, ignore_errors=True)
 
     result = measure(a, a.transport)
     # transport A/B: on distinct GPUs, the other device transport runs a short
@@ -829,6 +844,51 @@ def _journal_segments(parent: Path, need: int, n: int) -> int:
     if segs * JOURNAL_SEG_BYTES * 0.7 < per_cs:
         return -1
     return segs
+
+
+_LOCAL_FS = {"ext4", "ext3", "xfs", "btrfs", "f2fs"}
+
+
+def _data_volumes(default: Path) -> list[str]:
+    """Writable directories on distinct local block devices, `default` (TMPDIR) first.
+
+    DFS_BENCH_DIRS (comma-separated) names them explicitly; DFS_BENCH_SPREAD=0 keeps every rank
+    on `default`. Otherwise every mounted local filesystem on another device that this user can
+    write to (the mount point, or its tmp/ or $USER/ subdirectory) with at least 64 GiB free is
+    added, one directory per device."""
+    if os.environ.get("DFS_BENCH_DIRS"):
+        return [p.strip() for p in os.environ["DFS_BENCH_DIRS"].split(",") if p.strip()]
+    out = [str(default)]
+    if os.environ.get("DFS_BENCH_SPREAD", "1") == "0":
+        return out
+    try:
+        devs = {os.stat(default).st_dev}
+        mounts = Path("/proc/mounts").read_text().splitlines()
+    except OSError:
+        return out
+    skip = ("/proc", "/sys", "/dev", "/run", "/boot", "/etc", "/usr", "/snap", "/var/lib", "/root", "/home")
+    for ln in mounts:
+        f = ln.split()
+        if len(f) < 3 or f[2] not in _LOCAL_FS or not f[0].startswith("/dev/"):
+            continue
+        mnt = f[1].replace("\\040", " ")
+        if mnt == "/" or mnt.startswith(skip) or "sandbox" in mnt or "graft" in mnt:
+            continue
+        try:
+            st = os.stat(mnt)
+        except OSError:
+            continue
+        if st.st_dev in devs or not Path(mnt).is_dir():
+            continue
+        for c in (Path(mnt), Path(mnt) / "tmp", Path(mnt) / os.environ.get("USER", "-")):
+            try:
+                if c.is_dir() and os.access(c, os.W_OK | os.X_OK) and shutil.disk_usage(c).free >= (64 << 30):
+                    devs.add(st.st_dev)
+                    out.append(str(c))
+                    break
+            except OSError:
+                continue
+    return out
 
 
 def _allocated_bytes(d: Path) -> int:

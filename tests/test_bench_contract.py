@@ -152,3 +152,23 @@ def test_bench_transport_ab_block(tmp_path):
     assert "error" not in ab, ab
     # without a P2P pair the next server stages from the writer's slot (same host): "shm"
     assert ab["value"] > 0 and ab["transport"] in ("grpc", "shm") and ab["p2p_forwards"] == 0
+
+
+def test_bench_spreads_ranks_over_volumes(tmp_path):
+    """DFS_BENCH_DIRS: rank r keeps its journal, blocks and master WAL on volume r % V (the
+    8-GPU node's one-NVMe-per-GPU layout); each rank reports its volume, and a rank's
+    directory on another volume is removed at exit."""
+    v2 = tmp_path / "vol2"
+    v2.mkdir()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(TMPDIR=str(tmp_path), DFS_BENCH_DIRS=f"{tmp_path},{v2}")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu", "--steps", "1", "--warmup", "1",
+                        "--count", "8", "--remote-steps", "0", "--transport", "socket"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-4000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.strip()][0])
+    per = d["volume"]["per_rank"]
+    assert [r["volume"] for r in per] == [str(tmp_path), str(v2)] and per[1]["rank_dir_bytes"] > 0, per
+    assert all(r["volumes_in_job"] == 2 for r in per)
+    assert d["p2p_forwards"] > 0
+    assert list(v2.iterdir()) == []  # the second volume's rank directory is gone
