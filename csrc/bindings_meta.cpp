@@ -867,8 +867,9 @@ void bind_meta(py::module_& m) {
                        const std::string& secret_key, bool allow_unsigned, const std::string& audit_socket,
                        bool sse_enabled, bool metadata_sidecar, const std::string& policy_epoch,
                        const std::string& tls_cert, const std::string& tls_key, py::bytes sse_kek,
-                       std::map<uint32_t, py::bytes> sts_keys, const std::string& iam_config) {
+                       std::map<uint32_t, py::bytes> sts_keys, const std::string& iam_config, bool require_tls) {
              S3FrontConfig c;
+             c.require_tls = require_tls;
              for (auto& kv : sts_keys) c.sts_keys[kv.first] = std::string(kv.second);
              c.iam_config = iam_config;
              c.sse_kek = std::string(sse_kek);
@@ -896,7 +897,8 @@ void bind_meta(py::module_& m) {
            py::arg("secret_key") = "", py::arg("allow_unsigned_payload") = true, py::arg("audit_socket") = "",
            py::arg("sse_enabled") = false, py::arg("metadata_sidecar") = false, py::arg("policy_epoch") = "",
            py::arg("tls_cert") = "", py::arg("tls_key") = "", py::arg("sse_kek") = py::bytes(),
-           py::arg("sts_keys") = std::map<uint32_t, py::bytes>(), py::arg("iam_config") = "", py::keep_alive<1, 2>())
+           py::arg("sts_keys") = std::map<uint32_t, py::bytes>(), py::arg("iam_config") = "",
+           py::arg("require_tls") = false, py::keep_alive<1, 2>())
       .def("drop_policies", &S3Front::drop_policies, py::call_guard<py::gil_scoped_release>())
       .def("start", [](S3Front& f) {
         std::string err;

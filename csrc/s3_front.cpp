@@ -12,6 +12,7 @@
 #include <poll.h>
 #include <sys/epoll.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
@@ -358,6 +359,7 @@ struct S3Front::Req {
   std::vector<std::pair<std::string, std::string>> headers;  // (lower-case name, value)
   std::vector<std::string> names;                            // names as sent
   bool keep_alive = true, chunked = false, expect_continue = false;
+  bool secure = false;  // arrived over the front's own TLS
   int64_t content_length = 0;
   double started = 0;
   std::string rid;
@@ -593,7 +595,7 @@ S3Front::S3Front(S3FrontConfig cfg, FrontStore* store) : cfg_(std::move(cfg)), f
 
 S3Front::~S3Front() {
   stop();
-  if (epoch_map_) ::munmap(const_cast<uint64_t*>(epoch_map_), 4096);
+  if (epoch_map_) ::munmap(epoch_map_, 4096);
 }
 
 bool S3Front::start(std::string* err) {
@@ -642,8 +644,15 @@ bool S3Front::start(std::string* err) {
   }
   if (!cfg_.audit_socket.empty()) audit_fd_ = ::socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
   if (!cfg_.policy_epoch_path.empty()) {
-    int efd = ::open(cfg_.policy_epoch_path.c_str(), O_RDONLY | O_CLOEXEC);
-    void* m = efd < 0 ? MAP_FAILED : ::mmap(nullptr, 4096, PROT_READ, MAP_SHARED, efd, 0);
+    int efd = ::open(cfg_.policy_epoch_path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0600);
+    if (efd >= 0) {
+      struct stat sb {};
+      if (::fstat(efd, &sb) == 0 && sb.st_size < 4096 && ::ftruncate(efd, 4096) != 0) {
+        ::close(efd);
+        efd = -1;
+      }
+    }
+    void* m = efd < 0 ? MAP_FAILED : ::mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, efd, 0);
     if (efd >= 0) ::close(efd);
     if (m == MAP_FAILED) {
       *err = "policy epoch " + cfg_.policy_epoch_path + ": " + std::strerror(errno);
@@ -651,7 +660,7 @@ bool S3Front::start(std::string* err) {
       lfd_ = -1;
       return false;
     }
-    epoch_map_ = static_cast<const uint64_t*>(m);
+    epoch_map_ = static_cast<uint64_t*>(m);
     cache_epoch_ = policy_epoch();
   }
   epfd_ = ::epoll_create1(EPOLL_CLOEXEC);
@@ -826,6 +835,7 @@ void S3Front::serve(Conn* c) {
     }
     Req r;
     r.started = now_s();
+    r.secure = c->tls != nullptr;
     const std::string head = c->buf.substr(c->pos, end - c->pos);
     c->pos = end + 4;
     size_t le = head.find("\r\n");
@@ -881,6 +891,8 @@ bool S3Front::handle(Conn* c, Req& r) {
                           r.raw_path.find('%') == std::string::npos;
   std::map<std::string, std::string> q;
   if (r.raw_path == "/metrics" || r.raw_path == "/health") return proxy(c, r, nullptr, 0, "metrics");
+  if (fc_ && r.raw_path == "/" && r.method == "GET" && r.raw_query.empty() && r.content_length <= 0 && !r.chunked)
+    return native_list_buckets(c, r);  // (STS requests at the root carry a query or a form body)
   if (!fc_ || !plain_path || !decode_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
   // a presigned URL's authentication parameters are not part of the operation
   for (auto it = q.begin(); it != q.end();) {
@@ -896,6 +908,11 @@ bool S3Front::handle(Conn* c, Req& r) {
   if (slash != 0 && (slash == std::string::npos || slash + 1 == p.size())) {
     const std::string bucket = p.substr(0, slash);
     if (bucket.empty()) return proxy(c, r, nullptr, 0, "route");
+    const bool small_body = !r.chunked && r.content_length <= (1 << 20) && !aws_chunked(r);
+    const bool policy = q.size() == 1 && q.count("policy");
+    if (r.method == "GET" && q.size() == 1 && q.count("location") && small_body) return native_bucket(c, r, bucket, q);
+    if (policy && small_body && (r.method == "GET" || r.method == "PUT" || r.method == "DELETE"))
+      return native_bucket(c, r, bucket, q);
     if (r.method == "GET") {
       // ListObjects (v1, or v2 with list-type=2) unless it is a sub-resource
       if (q.count("location") || q.count("policy") || r.content_length > 0 || r.chunked)
@@ -903,7 +920,8 @@ bool S3Front::handle(Conn* c, Req& r) {
       return native_list(c, r, bucket, q);
     }
     if (r.method == "POST" && q.size() == 1 && q.count("delete")) return native_delete_objects(c, r, bucket, q);
-    if ((r.method == "PUT" || r.method == "HEAD") && q.empty() && !r.chunked && r.content_length <= (64 << 10))
+    if ((r.method == "PUT" || r.method == "HEAD" || r.method == "DELETE") && q.empty() && small_body &&
+        r.content_length <= (64 << 10))
       return native_bucket(c, r, bucket, q);
     return proxy(c, r, nullptr, 0, "route");
   }
@@ -980,6 +998,7 @@ bool S3Front::authorize(Req& r, const std::string& bucket, const std::map<std::s
                         std::string* user, Session* sess_out, std::string* why) {
   Session& sess = *sess_out;
   if (cfg_.auth_enabled) {
+    if (cfg_.require_tls && !r.secure) return (*why = "insecure", false);
     if (!verify_auth(r, user, &sess)) return (*why = "auth", false);
     std::vector<std::string> keys;
     for (auto& kv : q) keys.push_back(kv.first);
@@ -994,6 +1013,9 @@ bool S3Front::authorize(Req& r, const std::string& bucket, const std::map<std::s
     }
     // bucket policy (reference auth_middleware.rs + bucket_policy.rs): a static-key caller has
     // no role ARN, so only a Principal "*" Deny can apply to it; a session is matched by its role
+    // the gateway evaluates no bucket policy for the policy sub-resource itself (so a Deny
+    // cannot lock its owner out) and none at the root
+    if (q.count("policy") || bucket.empty()) return true;
     bool known = false;
     auto pol = bucket_policy(bucket, &known);
     if (!known) return (*why = "bucket-policy", false);
@@ -1318,6 +1340,21 @@ void S3Front::drop_policies() {
   ++cache_epoch_;  // an answer fetched before this call is not cached
 }
 
+// PolicyEpoch.bump of s3/server.py: strictly increasing across the gateway's processes (the
+// system-wide monotonic clock, at least +1).
+void S3Front::policy_changed() {
+  if (epoch_map_) {
+    timespec ts{};
+    ::clock_gettime(CLOCK_MONOTONIC, &ts);
+    const uint64_t mono = static_cast<uint64_t>(ts.tv_sec) * 1000000000ull + static_cast<uint64_t>(ts.tv_nsec);
+    uint64_t cur = __atomic_load_n(epoch_map_, __ATOMIC_ACQUIRE);
+    while (!__atomic_compare_exchange_n(epoch_map_, &cur, std::max(cur + 1, mono), false, __ATOMIC_ACQ_REL,
+                                        __ATOMIC_ACQUIRE)) {
+    }
+  }
+  drop_policies();
+}
+
 std::shared_ptr<const s3policy::BucketPolicy> S3Front::bucket_policy(const std::string& bucket, bool* known) {
   const double now = now_s();
   // the epoch is read BEFORE the policy file: a policy written before the bump is seen by
@@ -1620,6 +1657,11 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   }
   uint64_t s = 0, e = 0;
   int rng = parse_range(r.get("range"), m.size, &s, &e);
+  if (rng == 2)  // _range_response: 416 with the size
+    return respond(c, r, 416,
+                   "<Error>" + xel("Code", "InvalidRange") + xel("Message", "The requested range is not satisfiable") +
+                       "<Resource></Resource><RequestId></RequestId></Error>",
+                   "Content-Range: bytes */" + std::to_string(m.size) + "\r\n");
   if (rng >= 2) return proxy(c, r, nullptr, 0, "range");
   int64_t slot = -1;
   uint64_t got = 0;
@@ -2119,7 +2161,8 @@ bool S3Front::native_mpu_get(Conn* c, Req& r, const std::string& path, const std
 bool S3Front::respond(Conn* c, Req& r, int status, const std::string& xml, const std::string& extra) {
   const char* reason = status == 200 ? "OK" : status == 204 ? "No Content" : status == 400 ? "Bad Request"
                        : status == 403 ? "Forbidden" : status == 404 ? "Not Found" : status == 409 ? "Conflict"
-                       : "Internal Server Error";
+                       : status == 416 ? "Range Not Satisfiable" : status == 405 ? "Method Not Allowed"
+                       : status == 501 ? "Not Implemented" : "Internal Server Error";
   std::string h = "HTTP/1.1 " + std::to_string(status) + " " + reason + "\r\n" + extra;
   if (!xml.empty()) h += "Content-Type: application/xml\r\n";
   if (status != 204 && extra.find("Content-Length:") == std::string::npos)
@@ -2349,21 +2392,108 @@ bool S3Front::native_bucket(Conn* c, Req& r, const std::string& bucket, std::map
   std::string user = "anonymous", why;
   Session sess;
   if (!authorize(r, bucket, q, &user, &sess, &why)) return hand_over(why);
-  const std::string marker = "/" + bucket + "/.s3keep";
+  const std::string marker = "/" + bucket + "/.s3keep", polpath = "/" + bucket + "/.s3_bucket_policy";
   std::string msg;
   bool ok;
-  if (r.method == "PUT") {
-    int64_t slot = fc_->acquire_slot(1);
-    if (slot < 0) return hand_over("bucket");
+  auto write_small = [&](const std::string& path, const std::string& data, std::string* m) {
+    int64_t slot = fc_->acquire_slot(std::max<size_t>(data.size(), 1));
+    if (slot < 0) return FastClient::NotHandled;
+    if (!data.empty()) std::memcpy(fc_->slot_mut(slot), data.data(), data.size());
     FastClient::Times t;
     std::string md5;
     int reps = 0;
-    auto st = fc_->write_slot(marker, slot, 0, &reps, &msg, &t, r.rid, nullptr, nullptr, &md5);
+    auto st = fc_->write_slot(path, slot, data.size(), &reps, m, &t, r.rid, nullptr, nullptr, &md5);
     fc_->release(slot);
+    return st;
+  };
+  if (q.count("policy")) {
+    // Get/Put/DeleteBucketPolicy (reference handlers.rs bucket policy; s3/server.py)
+    if (r.method == "GET") {
+      bool found = false;
+      std::string meta, doc;
+      if (fc_->stat(polpath, &found, &meta, &msg, r.rid) != FastClient::Ok) return hand_over("policy");
+      bool valid = false;
+      if (found) {
+        int64_t slot = -1;
+        uint64_t n = 0;
+        FastClient::Times t;
+        if (fc_->read_known(meta, &slot, &n, &msg, &t, r.rid, 0, 0) != FastClient::Ok) return hand_over("policy");
+        doc.assign(reinterpret_cast<const char*>(fc_->slot_ptr(slot)), n);
+        fc_->release(slot);
+        try {
+          (void)Json::parse(doc);
+          valid = true;
+        } catch (const std::exception&) {
+        }
+      }
+      if (!valid) {
+        ok = respond(c, r, 404,
+                     "<Error>" + xel("Code", "NoSuchBucketPolicy") + xel("Message", "The bucket policy does not exist") +
+                         "<Resource></Resource><RequestId></RequestId>" + xel("BucketName", bucket) + "</Error>");
+      } else {
+        std::string h = "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: " +
+                        std::to_string(doc.size()) + "\r\n" +
+                        (r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+        r.status = 200;
+        count(r, 200);
+        ok = send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(doc.data()), doc.size());
+      }
+    } else if (r.method == "PUT") {
+      try {
+        (void)s3policy::BucketPolicy::parse(body);
+      } catch (const std::exception&) {
+        ok = respond(c, r, 400, "<Error><Code>MalformedPolicy</Code><Message>Bucket policy must be valid JSON"
+                                "</Message></Error>");
+        goto done;
+      }
+      auto st = write_small(polpath, body, &msg);
+      if (st == FastClient::Failed && msg.find("already exists") != std::string::npos) {
+        std::string dm;
+        if (fc_->remove(polpath, &dm, r.rid) == FastClient::NotHandled) return hand_over("policy");
+        st = write_small(polpath, body, &msg);
+      }
+      if (st == FastClient::NotHandled) return hand_over("policy");
+      if (st != FastClient::Ok) {
+        ok = respond(c, r, 500, "<Error><Code>InternalError</Code><Message>Failed to store bucket policy"
+                                "</Message></Error>");
+        goto done;
+      }
+      policy_changed();
+      ok = respond(c, r, 204, "");
+    } else if (r.method == "DELETE") {
+      if (fc_->remove(polpath, &msg, r.rid) == FastClient::NotHandled) return hand_over("policy");
+      policy_changed();
+      ok = respond(c, r, 204, "");
+    } else {
+      return hand_over("method");
+    }
+  } else if (q.count("location")) {
+    ok = respond(c, r, 200, "<LocationConstraint>" + xml_escape(cfg_.region) + "</LocationConstraint>");
+  } else if (r.method == "PUT") {
+    auto st = write_small(marker, std::string(), &msg);
     if (st == FastClient::Failed && msg.find("already exists") != std::string::npos) ok = respond(c, r, 409, "");
     else if (st != FastClient::Ok) return hand_over("bucket");
     else ok = respond(c, r, 200, "", "Location: /" + bucket + "\r\n");
-  } else {
+  } else if (r.method == "DELETE") {
+    // DeleteBucket: empty (only the marker and policy) -> both removed; objects -> 409
+    std::vector<std::pair<std::string, pb::FileMetadata>> files;
+    if (fc_->list("/" + bucket + "/", &files, r.rid) != FastClient::Ok) return hand_over("bucket");
+    bool objects = false;
+    for (auto& f : files)
+      if (!ends_with(f.first, ".s3keep") && !ends_with(f.first, ".s3_bucket_policy")) objects = true;
+    if (objects) {
+      ok = s3_error(c, r, 409, "BucketNotEmpty", "The bucket you tried to delete is not empty", bucket);
+    } else if (files.empty()) {
+      ok = s3_error(c, r, 404, "NoSuchBucket", "The specified bucket does not exist", bucket);
+    } else {
+      for (auto& f : files) {
+        std::string dm;
+        (void)fc_->remove(f.first, &dm, r.rid);
+      }
+      policy_changed();
+      ok = respond(c, r, 204, "");
+    }
+  } else {  // HEAD
     bool found = false;
     std::string meta;
     if (fc_->stat(marker, &found, &meta, &msg, r.rid) != FastClient::Ok) return hand_over("bucket");
@@ -2374,11 +2504,38 @@ bool S3Front::native_bucket(Conn* c, Req& r, const std::string& bucket, std::map
     }
     ok = respond(c, r, found ? 200 : 404, "", "Content-Length: 0\r\n");
   }
+done:
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.bucket_ops++;
   }
   if (cfg_.auth_enabled) audit(c, r, user, r.status, sess.role_arn);
+  return ok;
+}
+
+// ListBuckets (reference handlers.rs list_buckets; s3/server.py list_buckets): the first path
+// component of every file in the namespace, the multipart staging root left out.
+bool S3Front::native_list_buckets(Conn* c, Req& r) {
+  TraceRange tr("dfs.s3.list_buckets");
+  std::map<std::string, std::string> q;
+  std::string user = "anonymous", why;
+  Session sess;
+  if (!authorize(r, "", q, &user, &sess, &why)) return proxy(c, r, nullptr, 0, why);
+  std::vector<std::pair<std::string, pb::FileMetadata>> files;
+  if (fc_->list("/", &files, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "list");
+  std::set<std::string> names;
+  for (auto& f : files) {
+    size_t a = f.first.find_first_not_of('/');
+    if (a == std::string::npos) continue;
+    std::string n = f.first.substr(a, f.first.find('/', a) == std::string::npos ? std::string::npos
+                                                                                 : f.first.find('/', a) - a);
+    if (!n.empty() && n != ".s3_mpu") names.insert(n);
+  }
+  std::string inner;
+  for (auto& n : names) inner += "<Bucket>" + xel("Name", n) + xel("CreationDate", "2025-01-01T00:00:00.000Z") + "</Bucket>";
+  const bool ok = respond(c, r, 200, "<ListAllMyBucketsResult><Owner><ID>dfs</ID><DisplayName>dfs</DisplayName></Owner>"
+                                     "<Buckets>" + inner + "</Buckets></ListAllMyBucketsResult>");
+  if (cfg_.auth_enabled) audit(c, r, user, 200, sess.role_arn);
   return ok;
 }
 

@@ -60,6 +60,7 @@ struct S3FrontConfig {
   std::string region = "us-east-1";
   std::string access_key, secret_key;  // EnvCredentialProvider (S3_ACCESS_KEY / S3_SECRET_KEY)
   bool allow_unsigned_payload = true;
+  bool require_tls = false;  // S3_REQUIRE_TLS: an authenticated request over plain HTTP is refused
   std::string audit_socket;  // datagram socket of the audit store ("" = no audit)
   bool sse_enabled = false;  // SSE-S3: objects are stored encrypted
   std::string sse_kek;       // the 32-byte KEK (SSE_MASTER_KEY): encryption here; empty: Python does it
@@ -132,7 +133,10 @@ class S3Front {
   bool native_abort(Conn* c, Req& r, const std::string& upload_id);
   bool native_delete_objects(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q);
   bool native_copy(Conn* c, Req& r, const std::string& dest);
+  // Bucket-level requests: CreateBucket, HeadBucket, DeleteBucket, GetBucketLocation and
+  // Get/Put/DeleteBucketPolicy; ListBuckets at the root.
   bool native_bucket(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q);
+  bool native_list_buckets(Conn* c, Req& r);
   // Reads an aws-chunked body (Content-Length framed) into dst (cap bytes): 1 ok (*n = decoded
   // bytes), 0 connection error, -1 bad framing or a chunk signature that does not chain.
   int read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint64_t* n);
@@ -174,8 +178,11 @@ class S3Front {
   std::map<std::string, std::pair<double, std::shared_ptr<const s3policy::BucketPolicy>>> policy_cache_;
   static constexpr size_t kPolicyCacheMax = 4096;  // entries; the cache is emptied beyond this
   uint64_t cache_epoch_ = 0;                        // pol_mu_: epoch the cached entries belong to
-  const uint64_t* epoch_map_ = nullptr;             // mmap of cfg_.policy_epoch_path
+  uint64_t* epoch_map_ = nullptr;                   // mmap of cfg_.policy_epoch_path (shared, writable)
   uint64_t policy_epoch() const { return epoch_map_ ? __atomic_load_n(epoch_map_, __ATOMIC_ACQUIRE) : 0; }
+  // A bucket policy changed here: bump the shared epoch (every gateway process drops its
+  // cached policies) and this front's own cache.
+  void policy_changed();
 
  public:
   void drop_policies();  // the in-process form of an epoch bump

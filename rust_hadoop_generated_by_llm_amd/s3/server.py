@@ -1283,7 +1283,7 @@ def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_
                         tls_cert=cfg.tls_cert or "" if (cfg.tls_cert and cfg.tls_key) else "",
                         tls_key=cfg.tls_key or "" if (cfg.tls_cert and cfg.tls_key) else "",
                         sse_kek=gw.sse.kek if gw.sse is not None else b"",
-                        **native_front_auth(gw))
+                        require_tls=cfg.require_tls, **native_front_auth(gw))
     ok, err = front.start()
     if not ok:
         raise RuntimeError(f"native S3 front end failed to start: {err}")

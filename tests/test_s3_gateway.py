@@ -87,7 +87,7 @@ class GatewayThread:
                                      audit_socket=ingest if cfg.auth_enabled else "",
                                      sse_enabled=gw.sse is not None, metadata_sidecar=cfg.metadata_sidecar,
                                      policy_epoch=epoch, sse_kek=gw.sse.kek if gw.sse is not None else b"",
-                                     **native_front_auth(gw))
+                                     require_tls=cfg.require_tls, **native_front_auth(gw))
             ok, err = self.front.start()
             assert ok, err
         self.url = f"http://127.0.0.1:{self.port}"
