@@ -949,6 +949,9 @@ void bind_meta(py::module_& m) {
         d["chunk_sig_failures"] = s.chunk_sig_failures;
         d["presigned"] = s.presigned;
         d["bucket_ops"] = s.bucket_ops;
+        d["sts_issued"] = s.sts_issued;
+        d["standalone_answers"] = s.standalone_answers;
+        d["auth_results"] = s.auth_results;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;
         return d;

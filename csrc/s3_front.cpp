@@ -275,6 +275,30 @@ int hexval(char ch) {
 // parse_qsl(raw, keep_blank_values=True) of the Python gateway: '+' is a space, %XX a byte,
 // a malformed escape stays as written. False on bytes that are not UTF-8 (Python would
 // substitute U+FFFD; the request goes there).
+// The request path percent-decoded as the gateway routes it ('+' stays itself in a path);
+// false for a bad escape, a NUL or invalid UTF-8.
+bool decode_path(const std::string& raw, std::string* o) {
+  o->clear();
+  for (size_t i = 0; i < raw.size(); ++i) {
+    if (raw[i] != '%') {
+      o->push_back(raw[i]);
+      continue;
+    }
+    if (i + 2 >= raw.size() || hexval(raw[i + 1]) < 0 || hexval(raw[i + 2]) < 0) return false;
+    o->push_back(static_cast<char>(hexval(raw[i + 1]) * 16 + hexval(raw[i + 2])));
+    i += 2;
+  }
+  for (size_t i = 0; i < o->size();) {
+    unsigned char c0 = static_cast<unsigned char>((*o)[i]);
+    int n = c0 < 0x80 ? 1 : (c0 >> 5) == 6 ? 2 : (c0 >> 4) == 14 ? 3 : (c0 >> 3) == 30 ? 4 : 0;
+    if (!n || c0 == 0 || i + n > o->size()) return false;
+    for (int k = 1; k < n; ++k)
+      if ((static_cast<unsigned char>((*o)[i + k]) >> 6) != 2) return false;
+    i += static_cast<size_t>(n);
+  }
+  return true;
+}
+
 bool decode_query(const std::string& q, std::map<std::string, std::string>* out) {
   auto dec = [](const std::string& v, std::string* o) {
     o->clear();
@@ -356,6 +380,7 @@ struct S3Front::Conn {
 
 struct S3Front::Req {
   std::string method, target, raw_path, raw_query, version;
+  std::string path;  // raw_path percent-decoded (the signature covers raw_path)
   std::vector<std::pair<std::string, std::string>> headers;  // (lower-case name, value)
   std::vector<std::string> names;                            // names as sent
   bool keep_alive = true, chunked = false, expect_continue = false;
@@ -366,6 +391,9 @@ struct S3Front::Req {
   std::string action;  // s3:<Action> once resolved for authorization (audit records)
   int status = 0;
   std::map<std::string, std::string> presign;  // X-Amz-* query authentication (presigned URL)
+  // why authentication failed, as the gateway reports it (auth/errors.py kind, the audit
+  // record's error code when it differs, the access key / role that were presented)
+  std::string auth_kind, auth_audit, auth_user = "anonymous", auth_role;
   sigv4::ChunkChain chain;                      // set by a verified signature: aws-chunked bodies
   bool chain_set = false;
   const std::string* get(const char* lname) const {
@@ -634,6 +662,9 @@ bool S3Front::start(std::string* err) {
       return false;
     }
   }
+  if (!cfg_.oidc_issuer.empty() && !cfg_.oidc_client_id.empty())
+    oidc_ = std::make_unique<sts::OidcValidator>(cfg_.oidc_issuer, cfg_.oidc_client_id, cfg_.oidc_allow_hs256,
+                                                 cfg_.oidc_ca);
   if (!cfg_.tls_cert.empty()) {
     tls_ = TlsContext::server_http1(cfg_.tls_cert, cfg_.tls_key, err);
     if (!tls_) {
@@ -885,14 +916,21 @@ void S3Front::serve(Conn* c) {
 static bool read_body(S3Front::Conn* c, uint8_t* dst, uint64_t n);
 
 bool S3Front::handle(Conn* c, Req& r) {
-  // only plain paths are served here: a percent-escaped key goes to Python, whose URL
-  // decoding is the reference behaviour for it
-  const bool plain_path = r.raw_path.size() > 1 && r.raw_path[0] == '/' &&
-                          r.raw_path.find('%') == std::string::npos;
+  // keys are routed by their decoded path (as the reference's axum path extractor decodes
+  // them); the signature is checked over the path as sent
+  if (!decode_path(r.raw_path, &r.path)) return proxy(c, r, nullptr, 0, "uri");
+  const bool plain_path = r.path.size() > 1 && r.path[0] == '/';
   std::map<std::string, std::string> q;
   if (r.raw_path == "/metrics" || r.raw_path == "/health") return proxy(c, r, nullptr, 0, "metrics");
-  if (fc_ && r.raw_path == "/" && r.method == "GET" && r.raw_query.empty() && r.content_length <= 0 && !r.chunked)
-    return native_list_buckets(c, r);  // (STS requests at the root carry a query or a form body)
+  if (r.raw_path == "/" && cfg_.backend.empty()) {  // STS at the root (s3/server.py dispatch)
+    std::map<std::string, std::string> sq;
+    const std::string* ct = r.get("content-type");
+    const bool form = r.method == "POST" && ct && lower(*ct).compare(0, 33, "application/x-www-form-urlencoded") == 0;
+    if (decode_query(r.raw_query, &sq) && (sq["Action"] == "AssumeRoleWithWebIdentity" || form))
+      return native_sts(c, r, sq);
+  }
+  if (fc_ && r.raw_path == "/" && r.method == "GET" && r.content_length <= 0 && !r.chunked)
+    return native_list_buckets(c, r);  // ListBuckets takes no query parameters of its own (as the gateway)
   if (!fc_ || !plain_path || !decode_query(r.raw_query, &q)) return proxy(c, r, nullptr, 0, "route");
   // a presigned URL's authentication parameters are not part of the operation
   for (auto it = q.begin(); it != q.end();) {
@@ -903,7 +941,7 @@ bool S3Front::handle(Conn* c, Req& r) {
       ++it;
     }
   }
-  std::string p = r.raw_path.substr(1);
+  std::string p = r.path.substr(1);
   size_t slash = p.find('/');
   if (slash != 0 && (slash == std::string::npos || slash + 1 == p.size())) {
     const std::string bucket = p.substr(0, slash);
@@ -998,18 +1036,29 @@ bool S3Front::authorize(Req& r, const std::string& bucket, const std::map<std::s
                         std::string* user, Session* sess_out, std::string* why) {
   Session& sess = *sess_out;
   if (cfg_.auth_enabled) {
-    if (cfg_.require_tls && !r.secure) return (*why = "insecure", false);
+    if (cfg_.require_tls && !r.secure) {
+      r.auth_kind = "insecure_transport";
+      return (*why = "insecure", false);
+    }
     if (!verify_auth(r, user, &sess)) return (*why = "auth", false);
     std::vector<std::string> keys;
     for (auto& kv : q) keys.push_back(kv.first);
-    auto ar = s3policy::resolve_action_and_resource(r.method, r.raw_path, keys);
+    auto ar = s3policy::resolve_action_and_resource(r.method, r.path, keys);
     r.action = ar.first;
     // an STS session's role policy (reference auth_middleware.rs: IAM evaluation for
     // sessions only); a denial goes to the gateway, which answers 403 + audit
     if (!sess.role_arn.empty() && iam_) {
-      if (!iam_->evaluate(ar.first, ar.second, sess.role_arn, sess.ctx)) return (*why = "iam-deny", false);
-      std::lock_guard<std::mutex> g(st_mu_);
-      st_.iam_native++;
+      bool allowed = iam_->evaluate(ar.first, ar.second, sess.role_arn, sess.ctx);
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        st_.policy_results[(allowed ? "allow|" : "deny|") + ar.first]++;
+        if (allowed) st_.iam_native++;
+      }
+      if (!allowed) {
+        r.auth_kind = "missing_auth";
+        r.auth_audit = "AccessDenied";
+        return (*why = "iam-deny", false);
+      }
     }
     // bucket policy (reference auth_middleware.rs + bucket_policy.rs): a static-key caller has
     // no role ARN, so only a Principal "*" Deny can apply to it; a session is matched by its role
@@ -1021,8 +1070,15 @@ bool S3Front::authorize(Req& r, const std::string& bucket, const std::map<std::s
     if (!known) return (*why = "bucket-policy", false);
     if (pol) {
       if (pol->evaluate(sess.role_arn.empty() ? nullptr : &sess.role_arn, ar.first, ar.second) ==
-          s3policy::PolicyResult::ExplicitDeny)
+          s3policy::PolicyResult::ExplicitDeny) {
+        {
+          std::lock_guard<std::mutex> g(st_mu_);
+          st_.policy_results["deny|" + ar.first]++;
+        }
+        r.auth_kind = "missing_auth";
+        r.auth_audit = "AccessDenied";
         return (*why = "bucket-policy-deny", false);
+      }
       std::lock_guard<std::mutex> g(st_mu_);
       st_.policy_native++;
     }
@@ -1171,28 +1227,28 @@ bool S3Front::native_list(Conn* c, Req& r, const std::string& bucket, std::map<s
 // An STS session token (StsTokenManager, reference auth/sts.rs:60-98):
 // base64([kid u32 BE][nonce 12][AES-256-GCM(JSON StsSessionData)]). False when it does not
 // open, has expired or is malformed: the request goes to Python for the exact error.
-bool S3Front::open_session(const std::string& token, Session* out) {
+int S3Front::open_session(const std::string& token, Session* out) {
   std::string raw;
-  if (sts_keys_.empty() || !crypto::base64_decode(token, &raw) || raw.size() < 32) return false;
+  if (!crypto::base64_decode(token, &raw) || raw.size() < 32) return 0;
   const uint32_t kid = (uint32_t(uint8_t(raw[0])) << 24) | (uint32_t(uint8_t(raw[1])) << 16) |
                        (uint32_t(uint8_t(raw[2])) << 8) | uint32_t(uint8_t(raw[3]));
   auto k = sts_keys_.find(kid);
-  if (k == sts_keys_.end()) return false;
+  if (k == sts_keys_.end()) return 0;
   try {
     Json j = Json::parse(crypto::aes256gcm_decrypt(k->second, raw.substr(4, 12), raw.substr(16), ""));
     out->role_arn = j["role_arn"].str();
     out->secret = j["temp_secret_key"].str();
-    if (j["expiration"].as_int() < static_cast<int64_t>(now_s()) || out->role_arn.empty() || out->secret.empty())
-      return false;
+    if (out->role_arn.empty() || out->secret.empty()) return 0;
+    if (j["expiration"].as_int() < static_cast<int64_t>(now_s())) return -1;
     const Json& cl = j["claims"];  // Claims.to_policy_context()
     out->ctx.principal_id = cl["sub"].str();
     out->ctx.groups.clear();
     if (cl["groups"].is_array())
       for (auto& g : cl["groups"].items()) out->ctx.groups.push_back(g.str());
     out->ctx.claims = {{"sub", cl["sub"].str()}, {"iss", cl["iss"].str()}};
-    return true;
+    return 1;
   } catch (const std::exception&) {
-    return false;
+    return 0;
   }
 }
 
@@ -1203,6 +1259,11 @@ bool S3Front::open_session(const std::string& token, Session* out) {
 // days) instead of the 15-minute skew. Anything that does not verify is handed over, so
 // Python answers with the exact error and audit record.
 int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
+  auto fail = [&r](const char* kind, const char* audit_code = "") {
+    r.auth_kind = kind;
+    r.auth_audit = audit_code;
+    return 0;
+  };
   const std::string* auth = r.get("authorization");
   auto qp = [&r](const char* k) -> const std::string* {
     auto it = r.presign.find(k);
@@ -1212,7 +1273,7 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
   std::string cred, sh, sig;
   const std::string* ts = nullptr;
   if (auth) {
-    if (auth->compare(0, 16, "AWS4-HMAC-SHA256") != 0) return 0;
+    if (auth->compare(0, 16, "AWS4-HMAC-SHA256") != 0) return fail("missing_auth");
     std::vector<std::string> parts;
     size_t i = 0;
     while (i <= auth->size()) {
@@ -1221,9 +1282,9 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
       if (cm == std::string::npos) break;
       i = cm + 1;
     }
-    if (parts.size() < 3) return 0;
+    if (parts.size() < 3) return fail("missing_auth");
     size_t k = parts[0].find("Credential=");
-    if (k == std::string::npos) return 0;
+    if (k == std::string::npos) return fail("missing_auth");
     cred = parts[0].substr(k + 11);
     size_t sp = cred.find_first_of(" \t");
     if (sp != std::string::npos) cred = cred.substr(0, sp);
@@ -1238,17 +1299,14 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
   } else if (presigned) {
     if (*qp("X-Amz-Algorithm") != "AWS4-HMAC-SHA256" || !qp("X-Amz-Credential") || !qp("X-Amz-SignedHeaders") ||
         !qp("X-Amz-Signature") || !qp("X-Amz-Date"))
-      return 0;
+      return fail("missing_auth");
     cred = *qp("X-Amz-Credential");
     sh = *qp("X-Amz-SignedHeaders");
     sig = *qp("X-Amz-Signature");
     ts = qp("X-Amz-Date");
   } else {
-    return 0;
+    return fail("missing_auth");
   }
-  const std::string* token = r.get("x-amz-security-token");
-  if (!token) token = qp("X-Amz-Security-Token");
-  if (token && !open_session(*token, sess)) return 0;
   std::vector<std::string> cp;
   for (size_t a = 0;;) {
     size_t b = cred.find('/', a);
@@ -1256,28 +1314,41 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
     if (b == std::string::npos) break;
     a = b + 1;
   }
-  if (cp.size() < 5 || cp[4] != "aws4_request") return 0;
-  if (!ts || sh.empty() || sig.empty()) return 0;
+  if (cp.size() < 5 || cp[4] != "aws4_request") return fail("missing_auth");
+  r.auth_user = cp[0];
+  if (!ts || sh.empty() || sig.empty()) return fail("missing_auth");
   tm t{};
-  if (ts->size() != 16 || !strptime(ts->c_str(), "%Y%m%dT%H%M%SZ", &t)) return 0;
-  const double age = now_s() - static_cast<double>(timegm(&t));
+  const bool ts_ok = ts->size() == 16 && strptime(ts->c_str(), "%Y%m%dT%H%M%SZ", &t);
+  const double age = ts_ok ? now_s() - static_cast<double>(timegm(&t)) : 0;
   if (presigned) {
     // 0 < X-Amz-Expires <= 604800 and not yet expired
+    if (!ts_ok) return fail("missing_auth", "InvalidArgument");
     const std::string& ex = *qp("X-Amz-Expires");
-    if (!all_digits(ex) || ex.size() > 9) return 0;
+    if (!all_digits(ex) || ex.size() > 9 || std::stoull(ex) == 0) return fail("missing_auth", "InvalidArgument");
     const double expires = static_cast<double>(std::stoull(ex));
-    if (expires <= 0 || expires > 604800 || age > expires) return 0;
-  } else if (std::abs(age) / 60.0 > 15.0) {  // %Y%m%dT%H%M%SZ within 15 minutes of now
-    return 0;
+    if (expires > 604800) return fail("missing_auth", "AuthorizationQueryParametersError");
+    if (age > expires) return fail("expired_token");
+  } else if (ts_ok && std::abs(age) / 60.0 > 15.0) {  // %Y%m%dT%H%M%SZ within 15 minutes of now
+    return fail("clock_skew");
   }
   const std::string &ak = cp[0], &date = cp[1], &region = cp[2], &service = cp[3];
-  if (region != cfg_.region || service != "s3") return 0;
+  if (region != cfg_.region || service != "s3") return fail("invalid_scope");
+  const std::string* token = r.get("x-amz-security-token");
+  if (!token) token = qp("X-Amz-Security-Token");
   std::string skey;
   if (token) {
+    if (sts_keys_.empty()) return fail("internal");  // "STS is not enabled"
+    const int os = open_session(*token, sess);
+    if (os == 0) return fail("invalid_token");
+    if (os < 0) {
+      r.auth_role = sess->role_arn;
+      return fail("expired_token");
+    }
+    r.auth_role = sess->role_arn;
     // a session's own secret: its signing key is never shared with the static key's slot
     skey = sigv4::signing_key(sess->secret, date, region, service);
   } else {
-    if (cfg_.access_key.empty() || ak != cfg_.access_key) return 0;
+    if (cfg_.access_key.empty() || ak != cfg_.access_key) return fail("invalid_access_key");
     {
       std::lock_guard<std::mutex> g(key_mu_);
       auto it = key_cache_.find(date);
@@ -1320,11 +1391,15 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
   sr.signed_headers = joined;
   const std::string* ph = r.get("x-amz-content-sha256");
   sr.payload_hash = ph && !ph->empty() ? *ph : kUnsigned;
-  if (sr.payload_hash == kUnsigned && !cfg_.allow_unsigned_payload && !presigned) return 0;
+  if (sr.payload_hash == kUnsigned && !cfg_.allow_unsigned_payload && !presigned) return fail("missing_auth");
   const std::string scope = date + "/" + region + "/" + service + "/aws4_request";
   std::string creq;
-  if (!sigv4::verify(sr, *ts, scope, skey, sig, &creq)) return 0;
+  if (!ts || !sigv4::verify(sr, *ts, scope, skey, sig, &creq)) return fail("signature_mismatch");
   *user = ak;
+  if (cfg_.backend.empty()) {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.auth_results["success|none"]++;
+  }
   // an aws-chunked body continues this signature's chain (seed = the request signature)
   r.chain = sigv4::ChunkChain{skey, *ts, scope, sig};
   r.chain_set = true;
@@ -1402,9 +1477,10 @@ std::shared_ptr<const s3policy::BucketPolicy> S3Front::bucket_policy(const std::
   return pol;
 }
 
-void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int status, const std::string& role_arn) {
+void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int status, const std::string& role_arn,
+                    const std::string& error_code, const std::string& action_in, const std::string& resource_in) {
   if (audit_fd_ < 0) return;
-  std::string path = r.raw_path;
+  std::string path = r.path.empty() ? r.raw_path : r.path;
   std::vector<std::string> segs;
   for (size_t a = 0; a < path.size();) {
     size_t b = path.find('/', a);
@@ -1415,7 +1491,8 @@ void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int st
   }
   std::string resource = "arn:dfs:s3:::";
   for (size_t i = 0; i < segs.size(); ++i) resource += (i ? "/" : "") + segs[i];
-  std::string action = !r.action.empty() ? r.action
+  if (!resource_in.empty()) resource = resource_in;
+  std::string action = !action_in.empty() ? action_in : !r.action.empty() ? r.action
                        : r.method == "GET" ? "s3:GetObject" : r.method == "HEAD" ? "s3:HeadObject" : "s3:PutObject";
   const double t = now_s();
   int64_t ms;
@@ -1426,7 +1503,8 @@ void S3Front::audit(const Conn* c, const Req& r, const std::string& user, int st
                     ",\"remote_ip\":" + json_str(c->ip) + ",\"user_id\":" + json_str(user) +
                     ",\"role_arn\":" + (role_arn.empty() ? std::string("null") : json_str(role_arn)) +
                     ",\"action\":" + json_str(action) + ",\"resource\":" + json_str(resource) +
-                    ",\"status_code\":" + std::to_string(status) + ",\"error_code\":null,\"user_agent\":" +
+                    ",\"status_code\":" + std::to_string(status) + ",\"error_code\":" +
+                    (error_code.empty() ? std::string("null") : json_str(error_code)) + ",\"user_agent\":" +
                     (ua ? json_str(*ua) : std::string("null")) +
                     ",\"duration_ms\":" + std::to_string(static_cast<int64_t>((t - r.started) * 1000)) +
                     ",\"previous_hash\":null,\"record_hash\":null}";
@@ -2816,6 +2894,238 @@ bool S3Front::native_copy(Conn* c, Req& r, const std::string& dest) {
                      "</CopyObjectResult>");
 }
 
+// ---------------------------------------------------------------- a front without Python
+namespace {
+
+struct AuthKind {
+  const char *code, *message;
+  int status;
+  const char* error_type;
+};
+
+// auth/errors.py (reference common/src/auth/mod.rs:39-108)
+const std::map<std::string, AuthKind>& auth_kinds() {
+  static const std::map<std::string, AuthKind> k = {
+      {"missing_auth", {"AccessDenied", "Access Denied", 403, "missing_auth"}},
+      {"invalid_access_key",
+       {"InvalidAccessKeyId", "The AWS Access Key Id you provided does not exist in our records.", 403,
+        "invalid_access_key"}},
+      {"signature_mismatch",
+       {"SignatureDoesNotMatch", "The request signature we calculated does not match the signature you provided.",
+        403, "signature_mismatch"}},
+      {"clock_skew",
+       {"RequestTimeTooSkewed", "The difference between the request time and the current time is too large.", 403,
+        "clock_skew"}},
+      {"invalid_scope",
+       {"AuthorizationHeaderMalformed", "The authorization header is malformed; the region or service is wrong.", 400,
+        "invalid_credential_scope"}},
+      {"insecure_transport", {"AccessDenied", "Access Denied (Insecure Transport)", 403, "insecure_transport"}},
+      {"invalid_token", {"InvalidTokenId", "The security token included in the request is invalid.", 403, "invalid_token"}},
+      {"expired_token", {"ExpiredToken", "The provided token has expired.", 403, "expired_token"}},
+      {"internal", {"InternalError", "An internal error occurred during authentication.", 500, "internal_error"}},
+  };
+  return k;
+}
+
+}  // namespace
+
+bool S3Front::auth_error(Conn* c, Req& r) {
+  auto it = auth_kinds().find(r.auth_kind);
+  const AuthKind& k = it != auth_kinds().end() ? it->second : auth_kinds().at("missing_auth");
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.auth_results[std::string("failure|") + k.error_type]++;
+  }
+  const std::string x = std::string("<?xml version=\"1.0\" encoding=\"UTF-8\"?>\n<Error>\n  <Code>") + k.code +
+                        "</Code>\n  <Message>" + xml_escape(k.message) + "</Message>\n  <Resource>/</Resource>\n</Error>";
+  const bool ok = respond(c, r, k.status, x);
+  if (cfg_.auth_enabled) {
+    if (r.action.empty()) {
+      std::map<std::string, std::string> q;
+      std::vector<std::string> keys;
+      if (decode_query(r.raw_query, &q))
+        for (auto& kv : q) keys.push_back(kv.first);
+      r.action = s3policy::resolve_action_and_resource(r.method, r.path, keys).first;
+    }
+    audit(c, r, r.auth_user, k.status, r.auth_role, r.auth_audit.empty() ? k.code : r.auth_audit);
+  }
+  return ok;
+}
+
+bool S3Front::standalone(Conn* c, Req& r, const uint8_t* body, uint64_t n, const std::string& why) {
+  (void)n;
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.standalone_answers++;
+    st_.proxy_reasons["standalone:" + why]++;
+  }
+  // a body this path did not read cannot be skipped reliably: the connection ends after the answer
+  if (!body && (r.content_length > 0 || r.chunked)) r.keep_alive = false;
+  if (!r.auth_kind.empty()) return auth_error(c, r);
+  if (why == "metrics") {
+    if (r.raw_path == "/health") {
+      std::string h = "HTTP/1.1 200 OK\r\nContent-Type: text/plain; charset=utf-8\r\nContent-Length: 2\r\n" +
+                      std::string(r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+      r.status = 200;
+      return send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>("OK"), 2);
+    }
+    const std::string m = native_metrics();
+    std::string h = "HTTP/1.1 200 OK\r\nContent-Type: text/plain; charset=utf-8\r\nContent-Length: " +
+                    std::to_string(m.size()) + "\r\n" +
+                    (r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n");
+    r.status = 200;
+    return send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(m.data()), m.size());
+  }
+  std::string p = r.path.size() > 1 ? r.path.substr(1) : "";
+  const size_t slash = p.find('/');
+  const std::string bucket = p.substr(0, slash), key = slash == std::string::npos ? "" : p.substr(slash + 1);
+  std::map<std::string, std::string> q;
+  decode_query(r.raw_query, &q);
+  const std::string upload = q.count("uploadId") ? q["uploadId"] : "";
+  if (!key.empty() && reserved_key(key))
+    return s3_error(c, r, 400, "InvalidArgument", "object key " + py_repr(key) + " is reserved");
+  if (why == "list-empty") return s3_error(c, r, 404, "NoSuchBucket", "The specified bucket does not exist", bucket);
+  if (why == "missing" || why == "head-missing")
+    return s3_error(c, r, 404, "NoSuchKey", "The specified key does not exist.", "/" + bucket + "/" + key);
+  if (why == "copy-missing") {
+    std::string src;
+    const std::string* cs = r.get("x-amz-copy-source");
+    if (!cs || !unquote(cs->substr(0, cs->find('?')), &src)) src.clear();
+    if (src.empty() || src[0] != '/') src = "/" + src;
+    return s3_error(c, r, 404, "NoSuchKey", "The specified key does not exist.", src);
+  }
+  if (why == "copy-args") return s3_error(c, r, 400, "InvalidArgument", "copy source is reserved");
+  if (why == "no-upload" || why == "mpu-missing")
+    return s3_error(c, r, 404, "NoSuchUpload", "The specified upload does not exist.", upload);
+  if (why == "mpu-part" || why == "mpu-order")
+    return s3_error(c, r, 400, why == "mpu-part" ? "InvalidPart" : "InvalidPartOrder",
+                    "One or more of the specified parts could not be found or the specified entity tag might not "
+                    "have matched.",
+                    upload);
+  if (why == "mpu-xml" || why == "delete-xml")
+    return s3_error(c, r, 400, "MalformedXML", "The XML you provided was not well-formed");
+  if (why == "part-args") {
+    if (upload.empty() || upload.find('/') != std::string::npos || upload == "." || upload == "..")
+      return s3_error(c, r, 400, "InvalidArgument", "bad uploadId");
+    const std::string pn = q.count("partNumber") ? q["partNumber"] : "";
+    if (!all_digits(pn)) return s3_error(c, r, 400, "InvalidArgument", "bad partNumber");
+    return s3_error(c, r, 400, "InvalidArgument", "partNumber must be 1..10000");
+  }
+  if (why == "list-args") return s3_error(c, r, 400, "InvalidArgument", "max-keys must be an integer");
+  if (why == "large")
+    return s3_error(c, r, 400, "EntityTooLarge", "Your proposed upload exceeds the maximum allowed object size.");
+  if (why == "method") return respond(c, r, 405, "");
+  if (why == "uri") return s3_error(c, r, 400, "InvalidURI", "Couldn't parse the specified URI.");
+  if (why == "route" || why == "query" || why == "put-form" || why == "body")
+    return s3_error(c, r, 501, "NotImplemented", "A header or query you provided implies functionality that is not "
+                                                 "implemented.");
+  return s3_error(c, r, 500, "InternalError", "the gateway could not serve the request (" + why + ")",
+                  r.raw_path);
+}
+
+// AssumeRoleWithWebIdentity (reference sts_handler.rs:65-395; s3/server.py handle_sts): the
+// web identity token validated against the OIDC issuer's JWKS, the role's trust policy
+// evaluated on its claims, and a session token sealed with the STS key.
+bool S3Front::native_sts(Conn* c, Req& r, std::map<std::string, std::string>& q) {
+  TraceRange tr("dfs.s3.sts");
+  std::map<std::string, std::string> params = q;
+  const std::string* ct = r.get("content-type");
+  if (r.method == "POST" && ct && lower(*ct).compare(0, 33, "application/x-www-form-urlencoded") == 0) {
+    if (r.chunked || r.content_length > (1 << 20)) return standalone(c, r, nullptr, 0, "body");
+    std::string body(static_cast<size_t>(std::max<int64_t>(r.content_length, 0)), '\0');
+    if (r.expect_continue && !send_all(c->io(), "HTTP/1.1 100 Continue\r\n\r\n", 25)) return false;
+    if (!body.empty() && !read_body(c, reinterpret_cast<uint8_t*>(&body[0]), body.size())) return false;
+    std::map<std::string, std::string> form;
+    if (decode_query(body, &form))
+      for (auto& kv : form) params[kv.first] = kv.second;
+  }
+  const std::string action = params.count("Action") ? params["Action"] : "Unknown";
+  const std::string sts_res = "arn:dfs:sts:::*";
+  auto fail = [&](int status, const std::string& code, const std::string& msg, const std::string& user = "anonymous",
+                  const std::string& role = "") {
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.sts_results["failure|" + code]++;
+    }
+    const bool ok = respond(c, r, status,
+                            "<ErrorResponse><Error>" + xel("Code", code) + xel("Message", msg) +
+                                "</Error><RequestId></RequestId></ErrorResponse>");
+    audit(c, r, user, status, role, code, action, sts_res);
+    return ok;
+  };
+  if (action != "AssumeRoleWithWebIdentity") {
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      st_.sts_results["failure|InvalidAction"]++;
+    }
+    const bool ok = respond(c, r, 400, "", "Content-Length: 0\r\n");
+    audit(c, r, "anonymous", 400, "", "InvalidAction", action, sts_res);
+    return ok;
+  }
+  if (!oidc_) return fail(500, "OIDC_NOT_ENABLED", "OIDC validation is not enabled on this server.");
+  if (sts_keys_.empty()) return fail(500, "STS_NOT_ENABLED", "STS is not enabled on this server.");
+  if (!iam_) return fail(500, "IAM_NOT_ENABLED", "IAM policy evaluation is not enabled on this server.");
+  const std::string token = params.count("WebIdentityToken") ? params["WebIdentityToken"] : "";
+  if (token.empty()) return fail(400, "MissingToken", "WebIdentityToken is required");
+  const std::string role_arn = params.count("RoleArn") ? params["RoleArn"] : "";
+  if (role_arn.empty()) return fail(400, "MissingRole", "RoleArn is required");
+  sts::Claims claims;
+  std::string kind, detail;
+  const bool valid = oidc_->validate(token, &claims, &kind, &detail);
+  {
+    std::lock_guard<std::mutex> g(st_mu_);
+    st_.oidc_results[valid ? "success" : "failure"]++;
+  }
+  if (!valid) return fail(403, "InvalidIdentityToken", kind + (detail.empty() ? "" : ": " + detail), "anonymous", role_arn);
+  s3policy::Context ctx;
+  ctx.principal_id = claims.sub;
+  ctx.groups = claims.groups;
+  ctx.claims = {{"sub", claims.sub}, {"iss", claims.iss}};
+  if (!iam_->can_assume_role(role_arn, ctx))
+    return fail(403, "AccessDenied", "User is not authorized to assume this role.", claims.sub, role_arn);
+  int64_t duration = 3600;
+  if (params.count("DurationSeconds")) {
+    const std::string& d = params["DurationSeconds"];
+    const bool neg = !d.empty() && d[0] == '-';
+    if (!all_digits(neg ? d.substr(1) : d))
+      return fail(400, "ValidationError", "DurationSeconds must be an integer", claims.sub, role_arn);
+    duration = neg ? -1 : std::stoll(d);
+  }
+  if (duration < 1 || duration > 43200)
+    return fail(400, "ValidationError", "DurationSeconds must be in [1, 43200]", claims.sub, role_arn);
+  const int64_t exp = static_cast<int64_t>(now_s()) + duration;
+  auto k = sts_keys_.find(cfg_.sts_active_kid);
+  if (k == sts_keys_.end())
+    return fail(500, "InternalError", "internal: active KID " + std::to_string(cfg_.sts_active_kid) + " not found",
+                claims.sub, role_arn);
+  const std::string secret = sts::random_alnum(40);
+  std::string akid = "ASIA" + uuid4().substr(0, 8) + uuid4().substr(9, 4) + uuid4().substr(14, 4);
+  for (auto& ch : akid) ch = static_cast<char>(std::toupper(static_cast<unsigned char>(ch)));
+  const std::string tok = sts::make_token(k->second, cfg_.sts_active_kid, role_arn, secret, exp, claims);
+  std::string role_name = role_arn.substr(role_arn.rfind('/') == std::string::npos ? 0 : role_arn.rfind('/') + 1);
+  if (role_name.empty()) role_name = "role";
+  const std::string session = params.count("RoleSessionName") ? params["RoleSessionName"] : "session";
+  char expiration[32];
+  time_t et = static_cast<time_t>(exp);
+  tm g{};
+  gmtime_r(&et, &g);
+  std::strftime(expiration, sizeof expiration, "%Y-%m-%dT%H:%M:%SZ", &g);
+  {
+    std::lock_guard<std::mutex> lg(st_mu_);
+    st_.sts_results["success|none"]++;
+    st_.sts_issued++;
+  }
+  const std::string x = "<AssumeRoleWithWebIdentityResponse><AssumeRoleWithWebIdentityResult><Credentials>" +
+                        xel("AccessKeyId", akid) + xel("SecretAccessKey", secret) + xel("SessionToken", tok) +
+                        xel("Expiration", expiration) + "</Credentials>" + xel("SubjectFromWebIdentityToken", claims.sub) +
+                        "<AssumedRoleUser>" + xel("AssumedRoleId", role_name + ":" + session) +
+                        xel("Arn", "arn:dfs:sts:::assumed-role/" + role_name + "/" + session) +
+                        "</AssumedRoleUser></AssumeRoleWithWebIdentityResult></AssumeRoleWithWebIdentityResponse>";
+  const bool ok = respond(c, r, 200, x);
+  audit(c, r, claims.sub, 200, role_arn, "", action, sts_res);
+  return ok;
+}
+
 // ---------------------------------------------------------------- hand-off to Python
 int S3Front::backend_conn() {
   {
@@ -2952,10 +3262,43 @@ std::string S3Front::native_metrics() {
     o += std::string("s3_native_get_phase_seconds_total{phase=\"") + kv.first + "\"} " +
          std::to_string(kv.second / 1e6) + "\n";
   o += "# TYPE s3_native_get_timed_total counter\ns3_native_get_timed_total " + std::to_string(s.get_timed) + "\n";
+  if (cfg_.backend.empty()) {  // no Python workers: the IAM metrics they would export (s3/server.py)
+    auto split = [](const std::string& k) {
+      size_t b = k.find('|');
+      return std::make_pair(k.substr(0, b), b == std::string::npos ? std::string() : k.substr(b + 1));
+    };
+    o += "# HELP iam_auth_requests_total Total authentication attempts\n# TYPE iam_auth_requests_total counter\n";
+    for (auto& kv : s.auth_results) {
+      auto rt = split(kv.first);
+      o += "iam_auth_requests_total{result=\"" + rt.first + "\",error_type=\"" + rt.second + "\"} " +
+           std::to_string(kv.second) + "\n";
+    }
+    o += "# HELP iam_sts_requests_total STS requests\n# TYPE iam_sts_requests_total counter\n";
+    for (auto& kv : s.sts_results) {
+      auto rt = split(kv.first);
+      o += "iam_sts_requests_total{result=\"" + rt.first + "\",error_type=\"" + rt.second + "\"} " +
+           std::to_string(kv.second) + "\n";
+    }
+    o += "# HELP iam_policy_evaluations_total Policy evaluations\n# TYPE iam_policy_evaluations_total counter\n";
+    for (auto& kv : s.policy_results) {
+      auto rt = split(kv.first);
+      o += "iam_policy_evaluations_total{result=\"" + rt.first + "\",action=\"" + rt.second + "\"} " +
+           std::to_string(kv.second) + "\n";
+    }
+    o += "# HELP iam_oidc_validations_total Total OIDC token validations\n# TYPE iam_oidc_validations_total counter\n";
+    for (auto& kv : s.oidc_results)
+      o += "iam_oidc_validations_total{result=\"" + kv.first + "\"} " + std::to_string(kv.second) + "\n";
+    if (oidc_) {
+      o += "# TYPE iam_oidc_jwks_fetches_total counter\n";
+      o += "iam_oidc_jwks_fetches_total{result=\"success\"} " + std::to_string(oidc_->fetches_ok()) + "\n";
+      o += "iam_oidc_jwks_fetches_total{result=\"failure\"} " + std::to_string(oidc_->fetches_failed()) + "\n";
+    }
+  }
   return o;
 }
 
 bool S3Front::proxy(Conn* c, Req& r, const uint8_t* body, uint64_t body_len, const std::string& why) {
+  if (cfg_.backend.empty()) return standalone(c, r, body, body_len, why);
   note_proxy(why);
   int be = backend_conn();
   auto bad_gateway = [&] {

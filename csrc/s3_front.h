@@ -46,6 +46,7 @@
 #include "client_fast.h"
 #include "front_store.h"
 #include "s3_policy.h"
+#include "sts.h"
 #include "tls.h"
 #include "io_pool.h"
 
@@ -74,6 +75,12 @@ struct S3FrontConfig {
   // configuration (IAM_CONFIG_PATH document) that decides what a session may do
   std::map<uint32_t, std::string> sts_keys;
   std::string iam_config;
+  // STS issuance in the front (a gateway without the Python workers, backend == ""): the
+  // OIDC issuer and client id (OIDC_ISSUER_URL / OIDC_CLIENT_ID), HS256 test issuers, the CA
+  // for an https issuer, and the KID new session tokens are sealed with
+  std::string oidc_issuer, oidc_client_id, oidc_ca;
+  bool oidc_allow_hs256 = false;
+  uint32_t sts_active_kid = 1;
 };
 
 struct S3FrontStats {
@@ -89,6 +96,12 @@ struct S3FrontStats {
   uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0, iam_native = 0, lists = 0, mpu_completes = 0, mpu_initiates = 0;
   uint64_t deletes = 0, multi_deletes = 0, deleted_keys = 0, mpu_aborts = 0, copies = 0, copy_bytes = 0;
   uint64_t chunked_puts = 0, chunk_sigs = 0, chunk_sig_failures = 0, presigned = 0, bucket_ops = 0;
+  // a gateway without Python workers: the IAM metrics the workers would export
+  std::map<std::string, uint64_t> auth_results;  // "success|none", "failure|<error_type>"
+  std::map<std::string, uint64_t> sts_results;   // "success|none", "failure|<code>"
+  std::map<std::string, uint64_t> policy_results;  // "allow|s3:GetObject", "deny|s3:DeleteObject"
+  std::map<std::string, uint64_t> oidc_results;  // "success", "failure"
+  uint64_t sts_issued = 0, standalone_answers = 0;
 };
 
 class S3Front {
@@ -120,7 +133,7 @@ class S3Front {
     std::string role_arn, secret;
     s3policy::Context ctx;
   };
-  bool open_session(const std::string& token, Session* out);
+  int open_session(const std::string& token, Session* out);  // 1 open, 0 invalid, -1 expired
   bool authorize(Req& r, const std::string& bucket, const std::map<std::string, std::string>& q, std::string* user,
                  Session* sess, std::string* why);
   bool native_list(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q);
@@ -145,11 +158,17 @@ class S3Front {
   bool s3_error(Conn* c, Req& r, int status, const std::string& code, const std::string& msg,
                 const std::string& resource = "");
   int verify_auth(Req& r, std::string* user, Session* sess);  // 1 ok, 0 hand over
+  // A front without a Python backend answers what it would hand over: the auth error, the
+  // S3 error or the STS exchange, as s3/server.py does.
+  bool standalone(Conn* c, Req& r, const uint8_t* body, uint64_t n, const std::string& why);
+  bool auth_error(Conn* c, Req& r);
+  bool native_sts(Conn* c, Req& r, std::map<std::string, std::string>& q);
   // The bucket's policy: *known = false when it could not be read (the request is handed
   // over); a null pointer when the bucket has none (or an unparsable one, which the gateway
   // ignores too).
   std::shared_ptr<const s3policy::BucketPolicy> bucket_policy(const std::string& bucket, bool* known);
-  void audit(const Conn* c, const Req& r, const std::string& user, int status, const std::string& role_arn = "");
+  void audit(const Conn* c, const Req& r, const std::string& user, int status, const std::string& role_arn = "",
+             const std::string& error_code = "", const std::string& action = "", const std::string& resource = "");
   void count(const Req& r, int status);
   int backend_conn();
   void backend_done(int fd, bool reuse);
@@ -162,6 +181,7 @@ class S3Front {
   std::shared_ptr<TlsContext> tls_;
   std::map<uint32_t, std::string> sts_keys_;
   std::unique_ptr<s3policy::IamPolicy> iam_;
+  std::unique_ptr<sts::OidcValidator> oidc_;
   int lfd_ = -1, epfd_ = -1, evfd_ = -1, audit_fd_ = -1;
   std::atomic<bool> stop_{false};
   std::thread epoller_;

@@ -103,6 +103,24 @@ std::shared_ptr<TlsContext> TlsContext::client(const std::string& ca, const std:
   return t;
 }
 
+std::shared_ptr<TlsContext> TlsContext::client_http1(const std::string& ca, std::string* err) {
+  auto t = std::shared_ptr<TlsContext>(new TlsContext());
+  t->http1_ = true;
+  t->ctx_ = SSL_CTX_new(TLS_client_method());
+  if (!t->ctx_ || SSL_CTX_set_min_proto_version(t->ctx_, TLS1_2_VERSION) != 1) {
+    *err = "TLS client config: " + ssl_errors();
+    return nullptr;
+  }
+  if ((ca.empty() ? SSL_CTX_set_default_verify_paths(t->ctx_) : SSL_CTX_load_verify_locations(t->ctx_, ca.c_str(),
+                                                                                                nullptr)) != 1) {
+    *err = "TLS CA (" + ca + "): " + ssl_errors();
+    return nullptr;
+  }
+  SSL_CTX_set_verify(t->ctx_, SSL_VERIFY_PEER, nullptr);
+  SSL_CTX_set_mode(t->ctx_, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
+  return t;
+}
+
 TlsConn::TlsConn(std::shared_ptr<TlsContext> ctx, int fd) : ctx_(std::move(ctx)), fd_(fd) {
   ssl_ = SSL_new(ctx_->ctx());
   if (ssl_) SSL_set_fd(ssl_, fd);

@@ -30,6 +30,9 @@ class TlsContext {
   // Client side: trust `ca` (PEM; empty = system roots), verify the peer's name against
   // `domain` (empty = the host of each target), offer ALPN h2.
   static std::shared_ptr<TlsContext> client(const std::string& ca, const std::string& domain, std::string* err);
+  // Client side for HTTP/1.1 fetches (OIDC discovery / JWKS): the same trust and name
+  // checks, no ALPN requirement.
+  static std::shared_ptr<TlsContext> client_http1(const std::string& ca, std::string* err);
   bool is_server() const { return server_; }
   const std::string& domain() const { return domain_; }
   SSL_CTX* ctx() const { return ctx_; }

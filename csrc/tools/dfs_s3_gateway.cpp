@@ -1,0 +1,309 @@
+// dfs_s3_gateway — the S3 gateway as one native process (C52-C57; reference
+// dfs/s3_server/src/main.rs:243-274 for the process, handlers.rs for the object API,
+// auth_middleware.rs for SigV4, sts_handler.rs for STS).
+//
+// The S3 front (csrc/s3_front.cpp) with no Python backend: every request is answered in this
+// process. The object, multipart, bucket and policy API; SigV4 (header, presigned, aws-chunked
+// chunk chains), STS sessions with their IAM role policies and bucket policies; STS
+// AssumeRoleWithWebIdentity against the OIDC issuer (csrc/sts.cpp); SSE-S3; the error answers
+// of every request the data path does not serve (auth errors with the reference's codes,
+// NoSuchKey / NoSuchBucket / NoSuchUpload / MalformedXML ...); /health and /metrics. Audit
+// records go to the native hash-chained writer (csrc/audit_log.cpp) in this process.
+//
+// Configuration is the Python gateway's environment (s3/server.py S3Config): MASTER_ADDR,
+// CONFIG_SERVERS, SHARD_CONFIG, LOCAL_CHUNKSERVER, CA_CERT, DOMAIN_NAME, PORT, TLS_CERT /
+// TLS_KEY, S3_AUTH_ENABLED, S3_ACCESS_KEY / S3_SECRET_KEY, S3_REGION, S3_REQUIRE_TLS,
+// S3_ALLOW_UNSIGNED_PAYLOAD, OIDC_ISSUER_URL / OIDC_CLIENT_ID / OIDC_ALLOW_HS256,
+// STS_SIGNING_KEY, IAM_CONFIG_PATH, SSE_MASTER_KEY, AUDIT_LOG_* / AUDIT_HMAC_SECRET; plus
+// S3_FRONT_THREADS, S3_FRONT_SLOTS and S3_FRONT_SLOT_MB (the largest single PUT). Flags:
+// --port, --host (--workers is accepted and ignored: one process, S3_FRONT_THREADS threads).
+// S3_METADATA_SIDECAR=true (reference sidecar files) is served by the Python gateway only; the
+// launcher starts that one for it.
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "audit_log.h"
+#include "client_fast.h"
+#include "dfs_pb.h"
+#include "front_store.h"
+#include "grpc_client.h"
+#include "json.h"
+#include "node_shell.h"
+#include "s3_front.h"
+#include "shard_map.h"
+#include "tls.h"
+
+using namespace dfs;
+using dfs::shell::log;
+using dfs::shell::kError;
+using dfs::shell::kInfo;
+using dfs::shell::kWarning;
+
+namespace {
+
+const char* kLog = "dfs.s3";
+
+std::string env(const char* k, const std::string& d = "") {
+  const char* v = std::getenv(k);
+  return v ? std::string(v) : d;
+}
+
+std::string read_file(const std::string& p) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot read " + p);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+std::string with_scheme(const std::string& a, bool tls) {
+  if (a.find("://") != std::string::npos) return a;
+  return (tls ? "https://" : "http://") + a;
+}
+
+// The shard map of SHARD_CONFIG ({"shards": {id: [peers]}, "ranges": {...}}), as serde JSON.
+std::string shard_config_json(const std::string& path) {
+  Json cfg = Json::parse(read_file(path));
+  ShardMap m = ShardMap::new_range();
+  for (auto& kv : cfg["shards"].fields()) {
+    std::vector<std::string> peers;
+    for (auto& p : kv.second.items()) peers.push_back(p.str());
+    m.add_shard(kv.first, peers);
+  }
+  Json j = m.to_json();
+  if (cfg["ranges"].is_object()) {
+    Json r = Json::object();
+    for (auto& kv : cfg["ranges"].fields()) r.set(kv.first, kv.second.str());
+    j.set("strategy", Json(Json::Object{{"Range", Json(Json::Object{{"ranges", r}})}}));
+  }
+  return ShardMap::from_json(j).to_json().dump();
+}
+
+// FetchShardMap from the first config server that answers (ShardMap.from_fetch).
+std::string fetch_shard_map(GrpcChannelPool& pool, const std::vector<std::string>& servers, bool tls) {
+  for (auto& c : servers) {
+    GrpcResult r = pool.call(with_scheme(c, tls), "/dfs.ConfigService/FetchShardMap", std::string(), "", 5000);
+    if (!r.transport_ok || r.status != 0) continue;
+    pb::FetchShardMapResponse resp;
+    if (!resp.decode(r.message) || resp.shards.empty()) continue;
+    ShardMap m = ShardMap::new_range();
+    for (auto& kv : resp.shards) m.add_shard(kv.first, kv.second.peers);
+    Json j = m.to_json();
+    if (!resp.ranges.empty()) {
+      Json ranges = Json::object();
+      for (auto& kv : resp.ranges)
+        if (resp.shards.count(kv.second)) ranges.set(kv.first, Json(kv.second));
+      j.set("strategy", Json(Json::Object{{"Range", Json(Json::Object{{"ranges", ranges}})}}));
+    }
+    return ShardMap::from_json(j).to_json().dump();
+  }
+  return std::string();
+}
+
+bool parse_hex32(const std::string& hex, std::string* out) {
+  std::string h;
+  for (char ch : hex)
+    if (!std::isspace(static_cast<unsigned char>(ch))) h.push_back(ch);
+  if (h.size() != 64) return false;
+  out->clear();
+  for (size_t i = 0; i < 64; i += 2) {
+    char* end = nullptr;
+    const std::string b = h.substr(i, 2);
+    long v = std::strtol(b.c_str(), &end, 16);
+    if (!end || *end) return false;
+    out->push_back(static_cast<char>(v));
+  }
+  return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string host = "0.0.0.0";
+  int port = std::atoi(env("PORT", "9000").c_str());
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&]() { return i + 1 < argc ? std::string(argv[++i]) : std::string(); };
+    if (a == "--port") port = std::atoi(val().c_str());
+    else if (a == "--host") host = val();
+    else if (a == "--workers") (void)val();
+    else if (a == "-h" || a == "--help") {
+      std::printf("usage: dfs_s3_gateway [--port PORT] [--host HOST] [--workers N]\n"
+                  "configuration from the environment (see the header of csrc/tools/dfs_s3_gateway.cpp)\n");
+      return 0;
+    }
+  }
+  shell::block_stop_signals();
+  if (env("S3_METADATA_SIDECAR") == "true") {
+    log(kError, kLog, "S3_METADATA_SIDECAR=true is served by the Python gateway (s3/server.py)");
+    return 2;
+  }
+  S3FrontConfig cfg;
+  cfg.host = host;
+  cfg.port = port;
+  cfg.backend = "";  // no Python workers: every request is answered here
+  cfg.workers = std::atoi(env("S3_FRONT_THREADS", "32").c_str());
+  cfg.auth_enabled = env("S3_AUTH_ENABLED") == "true";
+  cfg.region = env("S3_REGION", "us-east-1");
+  cfg.access_key = env("S3_ACCESS_KEY");
+  cfg.secret_key = env("S3_SECRET_KEY");
+  cfg.allow_unsigned_payload = env("S3_ALLOW_UNSIGNED_PAYLOAD", "true") == "true";
+  cfg.require_tls = env("S3_REQUIRE_TLS") == "true";
+  const std::string tls_cert = env("TLS_CERT"), tls_key = env("TLS_KEY");
+  if (!tls_cert.empty() && !tls_key.empty()) {
+    cfg.tls_cert = tls_cert;
+    cfg.tls_key = tls_key;
+  }
+  if (!env("SSE_MASTER_KEY").empty()) {
+    std::string kek;
+    if (parse_hex32(env("SSE_MASTER_KEY"), &kek)) {
+      cfg.sse_enabled = true;
+      cfg.sse_kek = kek;
+    } else {
+      log(kError, kLog, "SSE disabled: SSE_MASTER_KEY must be 32 bytes (64 hex chars)");
+    }
+  }
+  if (!env("STS_SIGNING_KEY").empty()) cfg.sts_keys[1] = env("STS_SIGNING_KEY");
+  if (!env("IAM_CONFIG_PATH").empty()) {
+    try {
+      cfg.iam_config = read_file(env("IAM_CONFIG_PATH"));
+    } catch (const std::exception& e) {
+      log(kError, kLog, "failed to load IAM config %s: %s", env("IAM_CONFIG_PATH").c_str(), e.what());
+    }
+  }
+  cfg.oidc_issuer = env("OIDC_ISSUER_URL");
+  cfg.oidc_client_id = env("OIDC_CLIENT_ID");
+  cfg.oidc_allow_hs256 = env("OIDC_ALLOW_HS256") == "true";
+  cfg.oidc_ca = env("OIDC_CA_CERT");
+
+  // private directory: the policy epoch page and the audit ingest socket
+  char tmpl[] = "/tmp/s3gw-XXXXXX";
+  const std::string priv = ::mkdtemp(tmpl) ? tmpl : "/tmp";
+  cfg.policy_epoch_path = priv + "/policy_epoch";
+  std::unique_ptr<AuditLog> audit;
+  int ingest_fd = -1;
+  if (env("AUDIT_LOG_ENABLED", "true") == "true") {
+    const std::string secret = env("AUDIT_HMAC_SECRET");
+    if (secret.size() >= 16) {
+      audit = std::make_unique<AuditLog>(env("AUDIT_LOG_DIR", "/tmp/s3_audit_log"),
+                                         std::atoi(env("AUDIT_LOG_RETENTION_DAYS", "30").c_str()),
+                                         std::atoi(env("AUDIT_LOG_BATCH_SIZE", "100").c_str()), secret);
+      const std::string path = priv + "/ingest.sock";
+      ingest_fd = ::socket(AF_UNIX, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+      sockaddr_un sa{};
+      sa.sun_family = AF_UNIX;
+      std::snprintf(sa.sun_path, sizeof sa.sun_path, "%s", path.c_str());
+      int buf = 8 << 20;
+      ::setsockopt(ingest_fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+      if (::bind(ingest_fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) == 0) {
+        audit->start_ingest(ingest_fd);
+        if (cfg.auth_enabled) cfg.audit_socket = path;
+      } else {
+        log(kError, kLog, "audit ingest socket %s: %s", path.c_str(), std::strerror(errno));
+      }
+    } else {
+      log(kWarning, kLog, "audit logging disabled: AUDIT_HMAC_SECRET must be set and at least 16 characters");
+    }
+  }
+
+  // the DFS side: co-located (FastClient over the chunkserver's shared memory) or remote (gRPC)
+  const std::string ca = env("CA_CERT"), domain = env("DOMAIN_NAME");
+  std::shared_ptr<TlsContext> ctls;
+  if (!ca.empty()) {
+    std::string err;
+    ctls = TlsContext::client(ca, domain, &err);
+    if (!ctls) {
+      log(kError, kLog, "TLS client: %s", err.c_str());
+      return 1;
+    }
+  }
+  const bool tls = ctls != nullptr;
+  std::vector<std::string> masters;
+  for (auto& m : shell::split_csv(env("MASTER_ADDR", "http://127.0.0.1:8081"))) masters.push_back(with_scheme(m, tls));
+  const std::vector<std::string> cfg_servers = shell::split_csv(env("CONFIG_SERVERS"));
+  GrpcChannelPool pool(10000, ctls);
+  std::string map_json;
+  if (!env("SHARD_CONFIG").empty()) {
+    try {
+      map_json = shard_config_json(env("SHARD_CONFIG"));
+    } catch (const std::exception& e) {
+      log(kWarning, kLog, "SHARD_CONFIG: %s", e.what());
+    }
+  } else if (!cfg_servers.empty()) {
+    map_json = fetch_shard_map(pool, cfg_servers, tls);
+  }
+  const size_t slot_bytes = static_cast<size_t>(std::atol(env("S3_FRONT_SLOT_MB", "128").c_str())) << 20;
+  const size_t slots = static_cast<size_t>(std::max(1L, std::atol(env("S3_FRONT_SLOTS", "16").c_str())));
+  std::unique_ptr<FastClient> fast;
+  std::unique_ptr<RemoteFrontStore> remote;
+  std::unique_ptr<S3Front> front;
+  const std::string local = env("LOCAL_CHUNKSERVER");
+  if (!local.empty() && env("DFS_NATIVE_CLIENT", "1") == "1") {
+    const std::string fp = "dfs_fp_" + local.substr(local.rfind(':') + 1);
+    fast = std::make_unique<FastClient>(fp, local, slots * slot_bytes, slot_bytes,
+                                        std::atoi(env("DFS_HASH_THREADS", "16").c_str()));
+    if (!fast->ok()) {
+      log(kWarning, kLog, "no shared-memory arena with %s: using gRPC", local.c_str());
+      fast.reset();
+    }
+  }
+  if (fast) {
+    fast->set_routing(map_json, masters);
+    front = std::make_unique<S3Front>(cfg, fast.get());
+  } else {
+    remote = std::make_unique<RemoteFrontStore>(map_json, masters, slots, slot_bytes, 120000, ctls);
+    front = std::make_unique<S3Front>(cfg, static_cast<FrontStore*>(remote.get()));
+  }
+  std::string err;
+  if (!front->start(&err)) {
+    log(kError, kLog, "S3 front failed to start: %s", err.c_str());
+    return 1;
+  }
+  // the shard map follows the config servers (splits and merges move ranges)
+  std::atomic<bool> stop{false};
+  std::thread refresher;
+  if (!cfg_servers.empty() && env("SHARD_CONFIG").empty()) {
+    refresher = std::thread([&] {
+      while (!stop.load()) {
+        for (int i = 0; i < 50 && !stop.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        if (stop.load()) break;
+        std::string js = fetch_shard_map(pool, cfg_servers, tls);
+        if (js.empty() || js == map_json) continue;
+        map_json = js;
+        if (fast) fast->set_routing(js, masters);
+        if (remote) remote->set_routing(js, masters);
+      }
+    });
+  }
+  log(kInfo, kLog, "S3 gateway on %s:%d (native process, auth=%d, sse=%d, audit=%d, %s)", host.c_str(), front->port(),
+      cfg.auth_enabled, cfg.sse_enabled, audit != nullptr, fast ? "co-located: shared memory" : "remote: gRPC");
+  Json ready = Json::object();
+  ready.set("port", front->port());
+  ready.set("workers", 1);
+  ready.set("native_front", true);
+  ready.set("native_gateway", true);
+  ready.set("store", fast ? "shm" : "grpc");
+  shell::write_ready_file(ready.dump());
+  shell::wait_for_stop();
+  stop = true;
+  if (refresher.joinable()) refresher.join();
+  front->stop();
+  if (audit) audit->close();
+  if (ingest_fd >= 0) ::close(ingest_fd);
+  std::remove(cfg.policy_epoch_path.c_str());
+  std::remove((priv + "/ingest.sock").c_str());
+  ::rmdir(priv.c_str());
+  return 0;
+}

@@ -30,9 +30,18 @@ _handed_out: set[int] = set()
 # Roles that run as native executables (csrc/tools/dfs_master.cpp, dfs_config_server.cpp,
 # dfs_chunkserver.cpp), so no Python interpreter lives in a master, config-server or chunkserver
 # process. Masters and config servers have no other form; DFS_NATIVE_CHUNKSERVER=0 (or a knob
-# only the Python shell serves) starts the chunkserver's Python shell as the A/B.
+# only the Python shell serves) starts the chunkserver's Python shell as the A/B, and
+# S3_NATIVE_GATEWAY=0 (or S3_WORKERS > 1, S3_METADATA_SIDECAR=true) the Python S3 gateway.
 NATIVE_BINARIES = {"master.server": "dfs_master", "config_server.server": "dfs_config_server",
-                   "chunkserver.server": "dfs_chunkserver"}
+                   "chunkserver.server": "dfs_chunkserver", "s3.server": "dfs_s3_gateway"}
+
+
+def _python_gateway(env) -> bool:
+    """The S3 gateway configurations only the Python gateway serves (its A/B knobs): the
+    reference's sidecar metadata files, several worker processes sharing one audit chain, or
+    the Python-only layout."""
+    return (env.get("S3_NATIVE_GATEWAY", "1") == "0" or env.get("S3_NATIVE_FRONT", "true") != "true"
+            or env.get("S3_METADATA_SIDECAR", "") == "true" or int(env.get("S3_WORKERS", "1") or 1) > 1)
 
 
 def _python_chunkserver(args: list[str], env) -> bool:
@@ -48,6 +57,8 @@ def role_command(module: str, args: list[str], environ: dict | None = None) -> l
     env = os.environ if environ is None else environ
     exe = ROOT / "build" / "native" / NATIVE_BINARIES.get(module, "-")
     if module == "chunkserver.server" and _python_chunkserver(args, env):
+        return [sys.executable, "-m", f"{PKG}.{module}", *args]
+    if module == "s3.server" and _python_gateway(env):
         return [sys.executable, "-m", f"{PKG}.{module}", *args]
     if module in NATIVE_BINARIES:
         if not exe.exists():

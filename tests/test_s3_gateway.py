@@ -922,7 +922,7 @@ def _front_env(cluster, front):
     # the s3.server process runs its native front end when co-located with a chunkserver
     if front == "remote":
         return {}  # no chunkserver on this "host": the front speaks gRPC (RemoteFrontStore)
-    return {"LOCAL_CHUNKSERVER": cluster.cs_addrs[0]} if front == "native" else {"S3_NATIVE_FRONT": "false"}
+    return {"LOCAL_CHUNKSERVER": cluster.cs_addrs[0]} if front in ("native", "exe") else {"S3_NATIVE_FRONT": "false"}
 
 
 def test_gateway_subprocess(cluster, front):
