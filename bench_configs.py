@@ -244,16 +244,25 @@ def config5(a):
         out["parquet_over_s3"]["front_handoff_reasons"] = {k: v for k, v in pr.items() if v}
         out["native_load"] = native_load_phase(url, a, len(blob), cluster=c)
         out["load_generator"] = f"{a.concurrency} client processes (requests, keep-alive)"
-        out["gateway_workers"] = int(os.environ.get("S3_WORKERS", "4"))
-        # what the native front end served itself vs handed to the Python workers
+        out["gateway"] += _gateway_kind(c)
+        # what the native front end served itself vs handed to Python (none for the executable)
         nat = {}
         for ln in s.get(f"{url}/metrics").text.splitlines():
             if ln.startswith(("s3_native_requests_total", "s3_native_handoffs_total", "s3_native_bytes",
-                              "s3_native_get_")):
+                              "s3_native_get_", "s3_native_fallback_answers_total")):
                 k, v = ln.rsplit(" ", 1)
                 nat[k] = round(float(v), 4) if "seconds" in k else int(float(v))
         out["native_front"] = nat
         emit(out)
+
+
+def _gateway_kind(cluster, name: str = "s3") -> str:
+    """Which S3 gateway process the launcher started: the native executable, or the Python
+    gateway (S3_NATIVE_GATEWAY=0) with its worker count."""
+    pr = next((p for p in cluster.procs if p.name == name), None)
+    if pr is not None and pr.info.get("native_gateway"):
+        return "; process: dfs_s3_gateway (native executable, no Python)"
+    return f"; process: s3/server.py, {int(os.environ.get('S3_WORKERS', '4'))} workers"
 
 
 def _front_counters(url: str) -> dict:
@@ -482,7 +491,8 @@ def config5_secure(a):
         creds = _sts_session(url, role)
         out = {"config": "5-secure", "topology": f"S3 gateway (native front: TLS + SigV4 + STS session + IAM role + "
                                                  f"SSE-S3 + audit) + 1 master + 1 chunkserver "
-                                                 f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync"}
+                                                 f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync",
+               "gateway": _gateway_kind(c).lstrip("; ")}
         # the multipart object the multipart_get phase reads (uploaded by the same session)
         exe = ROOT / "build" / "native" / "s3_load"
         hostn, port = host.rsplit(":", 1)

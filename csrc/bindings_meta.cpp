@@ -951,6 +951,7 @@ void bind_meta(py::module_& m) {
         d["bucket_ops"] = s.bucket_ops;
         d["sts_issued"] = s.sts_issued;
         d["standalone_answers"] = s.standalone_answers;
+        d["standalone_reasons"] = s.standalone_reasons;
         d["auth_results"] = s.auth_results;
         d["by_status"] = s.by_status;
         d["proxy_reasons"] = s.proxy_reasons;

@@ -2957,7 +2957,7 @@ bool S3Front::standalone(Conn* c, Req& r, const uint8_t* body, uint64_t n, const
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.standalone_answers++;
-    st_.proxy_reasons["standalone:" + why]++;
+    st_.standalone_reasons[why]++;
   }
   // a body this path did not read cannot be skipped reliably: the connection ends after the answer
   if (!body && (r.content_length > 0 || r.chunked)) r.keep_alive = false;
@@ -3253,6 +3253,12 @@ std::string S3Front::native_metrics() {
        "# TYPE s3_native_handoffs_total counter\n";
   for (auto& kv : s.proxy_reasons)
     o += "s3_native_handoffs_total{reason=\"" + kv.first + "\"} " + std::to_string(kv.second) + "\n";
+  if (cfg_.backend.empty()) {
+    o += "# HELP s3_native_fallback_answers_total requests the executable gateway answered on its fallback path "
+         "(errors, health, metrics), by reason\n# TYPE s3_native_fallback_answers_total counter\n";
+    for (auto& kv : s.standalone_reasons)
+      o += "s3_native_fallback_answers_total{reason=\"" + kv.first + "\"} " + std::to_string(kv.second) + "\n";
+  }
   o += "# TYPE s3_native_bytes_in_total counter\ns3_native_bytes_in_total " + std::to_string(s.bytes_in) + "\n";
   o += "# TYPE s3_native_bytes_out_total counter\ns3_native_bytes_out_total " + std::to_string(s.bytes_out) + "\n";
   o += "# HELP s3_native_get_phase_seconds_total native GET time by phase (stat, read, send)\n"

@@ -102,6 +102,9 @@ struct S3FrontStats {
   std::map<std::string, uint64_t> policy_results;  // "allow|s3:GetObject", "deny|s3:DeleteObject"
   std::map<std::string, uint64_t> oidc_results;  // "success", "failure"
   uint64_t sts_issued = 0, standalone_answers = 0;
+  // answers of the executable gateway's own fallback path (errors, /health, /metrics) by the
+  // reason a hosted front would have handed the request over for; never a hand-off
+  std::map<std::string, uint64_t> standalone_reasons;
 };
 
 class S3Front {
