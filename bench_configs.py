@@ -47,6 +47,12 @@ def emit(d):
     print(json.dumps(d), flush=True)
 
 
+def progress(msg: str):
+    """One line per phase on stderr, so a long config run shows where it is (and a silent one
+    where it stopped)."""
+    print(f"[bench_configs {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 # ----------------------------------------------------------------------------- config 1
 def config1(a):
     """single master + 1 chunkserver on CPU: put/get 1 MiB round trip + the benchmark."""
@@ -191,8 +197,10 @@ def config5(a):
         lg.starmap(_s3_payload, [(0, 16)] * a.concurrency, chunksize=1)  # workers up before timing
         # untimed warm-up round (as bench.py's warmup steps): every gateway process and its
         # DFS client have served requests before the clock starts
+        progress("config5: warm-up")
         timed("put", n, "warm")
         timed("get", n, "warm")
+        progress("config5: put / get / range")
         el, lat = timed("put", n)
         out["put"] = {"objects": n, "size": size, "mb_per_s": round(n * size / (1 << 20) / el, 1),
                       "p50_ms": pct(lat, 50), "p99_ms": pct(lat, 99)}
@@ -206,6 +214,7 @@ def config5(a):
         # multipart upload of one large object, parts in parallel (S3 MPU emulation, handlers.rs:234-432)
         import xml.etree.ElementTree as ET
 
+        progress("config5: multipart")
         part = 8 << 20
         nparts = a.mpu_parts
         blob = os.urandom(part * nparts)
@@ -236,6 +245,7 @@ def config5(a):
                             "get_mb_per_s": round(len(blob) / (1 << 20) / mpu_get_s, 1)}
         lg.close()
         f0 = _front_counters(url)
+        progress("config5: parquet")
         out["parquet_over_s3"] = parquet_phase(url, a)
         f1 = _front_counters(url)
         # what pyarrow's S3 client (the AWS C++ SDK, as S3A's) sent that the native front handed over
@@ -367,6 +377,7 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
     from bench import cgroup_cpu, cgroup_cpu_delta
 
     for name, extra in phases:
+        progress(f"native load: {name}")
         before = _front_counters(url)
         cg0, pc0, cs0, t0 = cgroup_cpu(), _proc_cpu(cluster), _cs_counters(cluster), time.perf_counter()
         r = subprocess.run(base + sec + extra, capture_output=True, text=True, timeout=a.phase_seconds * 4 + 300)

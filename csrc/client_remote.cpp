@@ -134,7 +134,21 @@ bool RemoteClient::call_candidates(std::vector<std::string> cands, const std::st
     GrpcResult r = pool_.call(cands[i], full, req, rid);
     if (!r.transport_ok) continue;
     std::string hint;
-    if (r.status == kFailedPrecondition && not_leader(r.message, &hint)) {
+    bool follower = r.status == kFailedPrecondition && not_leader(r.message, &hint);
+    if (!follower && r.status == 0 && (method == "CreateFile" || method == "DeleteFile" || method == "Rename")) {
+      // these answer a follower's refusal in the response: fields 1 success, 2 error_message,
+      // 3 leader_hint, which DeleteFileResponse is exactly (the decoder skips the rest)
+      pb::DeleteFileResponse head;
+      if (head.decode(r.message) && !head.success && head.error_message == "Not Leader") {
+        follower = true;
+        hint = head.leader_hint;
+      }
+    }
+    if (follower) {
+      if (!hint.empty() && hint.find("://") == std::string::npos) {
+        const size_t sch = cands[i].find("://");
+        if (sch != std::string::npos) hint = cands[i].substr(0, sch + 3) + hint;
+      }
       if (!hint.empty() && std::find(cands.begin() + static_cast<long>(i) + 1, cands.end(), hint) == cands.end())
         cands.insert(cands.begin() + static_cast<long>(i) + 1, hint);
       continue;

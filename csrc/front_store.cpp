@@ -90,4 +90,85 @@ FrontStore::Status RemoteFrontStore::list(const std::string& prefix,
   return rc_.list(prefix, out, rid);
 }
 
+LocalFirstFrontStore::LocalFirstFrontStore(FastClient* fc, const std::string& shard_map_json,
+                                           const std::vector<std::string>& masters, int timeout_ms,
+                                           std::shared_ptr<TlsContext> tls)
+    : fc_(fc), rc_(4, timeout_ms, std::move(tls)) {
+  fc_->set_routing(shard_map_json, masters);
+  rc_.set_routing(shard_map_json, masters);
+}
+
+FrontStore::Status LocalFirstFrontStore::write_slot(const std::string& path, int64_t slot, size_t n, int* replicas,
+                                                    std::string* msg, Times* t, const std::string& rid,
+                                                    const std::map<std::string, std::string>* attrs,
+                                                    const char* etag_attr, std::string* md5_out) {
+  Status st = fc_->write_slot(path, slot, n, replicas, msg, t, rid, attrs, etag_attr, md5_out);
+  if (st != FastClient::NotHandled || slot < 0 || n > fc_->slot_bytes()) return st;
+  fallbacks_++;
+  msg->clear();
+  return rc_.write_etag(path, fc_->slot_ptr(slot), n, replicas, msg, t, rid, attrs, etag_attr, md5_out);
+}
+
+FrontStore::Status LocalFirstFrontStore::stat(const std::string& path, bool* found, std::string* meta_pb,
+                                              std::string* msg, const std::string& rid) {
+  Status st = fc_->stat(path, found, meta_pb, msg, rid);
+  if (st != FastClient::NotHandled) return st;
+  fallbacks_++;
+  msg->clear();
+  return rc_.stat(path, found, meta_pb, msg, rid);
+}
+
+FrontStore::Status LocalFirstFrontStore::read_known(const std::string& meta_pb, int64_t* slot, uint64_t* n,
+                                                    std::string* msg, Times* t, const std::string& rid,
+                                                    uint64_t offset, uint64_t length) {
+  Status st = fc_->read_known(meta_pb, slot, n, msg, t, rid, offset, length);
+  if (st != FastClient::NotHandled) return st;
+  pb::FileMetadata m;
+  if (!m.decode(meta_pb)) return st;
+  fallbacks_++;
+  msg->clear();
+  std::string data;
+  st = rc_.read_meta(m, &data, msg, t, rid, offset, length);
+  if (st != FastClient::Ok) return st;
+  if (data.empty()) {
+    *slot = -1;
+    *n = 0;
+    return FastClient::Ok;
+  }
+  if (data.size() > fc_->slot_bytes()) return FastClient::NotHandled;
+  const int64_t s = fc_->acquire_slot(data.size());
+  if (s < 0) return FastClient::NotHandled;
+  std::memcpy(fc_->slot_mut(s), data.data(), data.size());
+  *slot = s;
+  *n = data.size();
+  return FastClient::Ok;
+}
+
+FrontStore::Status LocalFirstFrontStore::remove(const std::string& path, std::string* msg, const std::string& rid) {
+  Status st = fc_->remove(path, msg, rid);
+  if (st != FastClient::NotHandled) return st;
+  fallbacks_++;
+  msg->clear();
+  return rc_.remove(path, msg, rid);
+}
+
+FrontStore::Status LocalFirstFrontStore::rename(const std::string& src, const std::string& dst, std::string* msg,
+                                                const std::string& rid) {
+  Status st = fc_->rename(src, dst, msg, rid);
+  if (st != FastClient::NotHandled) return st;
+  fallbacks_++;
+  msg->clear();
+  return rc_.rename(src, dst, msg, rid);
+}
+
+FrontStore::Status LocalFirstFrontStore::list(const std::string& prefix,
+                                              std::vector<std::pair<std::string, pb::FileMetadata>>* out,
+                                              const std::string& rid) {
+  Status st = fc_->list(prefix, out, rid);
+  if (st != FastClient::NotHandled) return st;
+  fallbacks_++;
+  out->clear();
+  return rc_.list(prefix, out, rid);
+}
+
 }  // namespace dfs

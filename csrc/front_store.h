@@ -10,10 +10,15 @@
 //    the gateway as its own service, talking gRPC to masters and chunkservers): private slots,
 //    and every master and chunkserver call over gRPC through RemoteClient (client_remote.h),
 //    with its leader following, hedged reads and EC decode.
+//  * LocalFirstFrontStore (below), the executable gateway co-located with a chunkserver: the
+//    FastClient for everything it serves, and a RemoteClient (leader following over gRPC) for
+//    the calls it declines (a shard leader that is not its first peer or on another host, a
+//    dead local master, a multi-block file), with the body still in the FastClient's slot.
 // Either way the front serves the same requests natively; NotHandled sends a request to the
-// gateway's Python path, as before.
+// gateway's Python path (a hosted front) or its own error answer (the executable).
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <map>
@@ -48,6 +53,8 @@ class FrontStore {
   virtual Status rename(const std::string& src, const std::string& dst, std::string* msg, const std::string& rid) = 0;
   virtual Status list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
                       const std::string& rid) = 0;
+  // calls a first-choice path declined and a second one served (LocalFirstFrontStore)
+  virtual uint64_t fallbacks() const { return 0; }
 };
 
 // The co-located form: every call goes to the FastClient (not owned).
@@ -124,6 +131,42 @@ class RemoteFrontStore final : public FrontStore {
   std::mutex mu_;
   std::condition_variable cv_;
   std::vector<int64_t> free_;  // slot offsets
+};
+
+// The executable gateway's co-located store: FastClient first, RemoteClient for what it
+// declines. Slots are the FastClient's (shared with the chunkserver), so a PUT body received
+// into one is written over gRPC from there when the fast path cannot take it.
+class LocalFirstFrontStore final : public FrontStore {
+ public:
+  LocalFirstFrontStore(FastClient* fc, const std::string& shard_map_json, const std::vector<std::string>& masters,
+                       int timeout_ms = 120000, std::shared_ptr<TlsContext> tls = nullptr);
+  void set_routing(const std::string& shard_map_json, const std::vector<std::string>& masters) {
+    fc_->set_routing(shard_map_json, masters);
+    rc_.set_routing(shard_map_json, masters);
+  }
+
+  size_t slot_bytes() const override { return fc_->slot_bytes(); }
+  int64_t acquire_slot(size_t n) override { return fc_->acquire_slot(n); }
+  const uint8_t* slot_ptr(int64_t slot) const override { return fc_->slot_ptr(slot); }
+  uint8_t* slot_mut(int64_t slot) override { return fc_->slot_mut(slot); }
+  void release(int64_t slot) override { fc_->release(slot); }
+  Status write_slot(const std::string& path, int64_t slot, size_t n, int* replicas, std::string* msg, Times* t,
+                    const std::string& rid, const std::map<std::string, std::string>* attrs, const char* etag_attr,
+                    std::string* md5_out) override;
+  Status stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg,
+              const std::string& rid) override;
+  Status read_known(const std::string& meta_pb, int64_t* slot, uint64_t* n, std::string* msg, Times* t,
+                    const std::string& rid, uint64_t offset, uint64_t length) override;
+  Status remove(const std::string& path, std::string* msg, const std::string& rid) override;
+  Status rename(const std::string& src, const std::string& dst, std::string* msg, const std::string& rid) override;
+  Status list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
+              const std::string& rid) override;
+  uint64_t fallbacks() const override { return fallbacks_.load(); }
+
+ private:
+  FastClient* fc_;
+  RemoteClient rc_;
+  std::atomic<uint64_t> fallbacks_{0};
 };
 
 }  // namespace dfs

@@ -3259,6 +3259,8 @@ std::string S3Front::native_metrics() {
     for (auto& kv : s.standalone_reasons)
       o += "s3_native_fallback_answers_total{reason=\"" + kv.first + "\"} " + std::to_string(kv.second) + "\n";
   }
+  o += "# TYPE s3_native_store_fallbacks_total counter\ns3_native_store_fallbacks_total " +
+       std::to_string(fc_->fallbacks()) + "\n";
   o += "# TYPE s3_native_bytes_in_total counter\ns3_native_bytes_in_total " + std::to_string(s.bytes_in) + "\n";
   o += "# TYPE s3_native_bytes_out_total counter\ns3_native_bytes_out_total " + std::to_string(s.bytes_out) + "\n";
   o += "# HELP s3_native_get_phase_seconds_total native GET time by phase (stat, read, send)\n"

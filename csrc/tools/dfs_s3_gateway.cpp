@@ -247,6 +247,7 @@ int main(int argc, char** argv) {
   const size_t slot_bytes = static_cast<size_t>(std::atol(env("S3_FRONT_SLOT_MB", "128").c_str())) << 20;
   const size_t slots = static_cast<size_t>(std::max(1L, std::atol(env("S3_FRONT_SLOTS", "16").c_str())));
   std::unique_ptr<FastClient> fast;
+  std::unique_ptr<LocalFirstFrontStore> local_first;
   std::unique_ptr<RemoteFrontStore> remote;
   std::unique_ptr<S3Front> front;
   const std::string local = env("LOCAL_CHUNKSERVER");
@@ -260,8 +261,10 @@ int main(int argc, char** argv) {
     }
   }
   if (fast) {
-    fast->set_routing(map_json, masters);
-    front = std::make_unique<S3Front>(cfg, fast.get());
+    // the shared-memory client first; what it declines (a leader elsewhere, a dead local
+    // master) over gRPC with leader following, the body still in the shared slot
+    local_first = std::make_unique<LocalFirstFrontStore>(fast.get(), map_json, masters, 120000, ctls);
+    front = std::make_unique<S3Front>(cfg, static_cast<FrontStore*>(local_first.get()));
   } else {
     remote = std::make_unique<RemoteFrontStore>(map_json, masters, slots, slot_bytes, 120000, ctls);
     front = std::make_unique<S3Front>(cfg, static_cast<FrontStore*>(remote.get()));
@@ -282,7 +285,7 @@ int main(int argc, char** argv) {
         std::string js = fetch_shard_map(pool, cfg_servers, tls);
         if (js.empty() || js == map_json) continue;
         map_json = js;
-        if (fast) fast->set_routing(js, masters);
+        if (local_first) local_first->set_routing(js, masters);
         if (remote) remote->set_routing(js, masters);
       }
     });

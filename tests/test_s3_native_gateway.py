@@ -281,3 +281,40 @@ def test_refuses_sidecar_layout(cluster, tmp_path):
                SHARD_CONFIG=str(cluster.base / "shard_config.json"), DFS_READY_FILE=str(tmp_path / "r"))
     p = subprocess.run([str(EXE)], env=env, capture_output=True, timeout=30)
     assert p.returncode == 2 and b"SIDECAR" in p.stderr.upper()
+
+
+def test_follows_master_leader_changes():
+    """A Raft group of three masters: the executable's shared-memory client reaches only its
+    shard's first peer, so calls it declines (that peer not leading, or dead) go over gRPC
+    with leader following, the body still in the shared slot; the gateway keeps serving
+    across a leader kill (reference: the client follows Not Leader hints, mod.rs)."""
+    from rust_hadoop_generated_by_llm_amd.models import proto as pb
+    from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool
+
+    with LocalCluster(n_chunkservers=3, masters_per_shard=3, fsync=False) as cl:
+        g = Exe(cl, {"AUDIT_LOG_ENABLED": "false", "LOCAL_CHUNKSERVER": cl.cs_addrs[0]}, "s3ha")
+        u = g.url
+        assert requests.put(f"{u}/ha").status_code == 200
+        before = os.urandom(200_000)
+        assert requests.put(f"{u}/ha/before", data=before).status_code == 200
+        pool = ChannelPool()
+        leader = None
+        for m in cl.master_addrs:
+            if pool.call(m, "MasterService", "GetClusterInfo", pb.GetClusterInfoRequest()).role == "Leader":
+                leader = m
+        assert leader is not None
+        cl.kill(f"master_shard-0_{cl.master_addrs.index(leader) + 1}")
+        after = os.urandom(300_000)
+        deadline = time.time() + 30
+        while requests.put(f"{u}/ha/after", data=after).status_code != 200:
+            assert time.time() < deadline, "no write accepted after the leader was killed"
+            time.sleep(0.3)
+        assert requests.get(f"{u}/ha/before").content == before
+        assert requests.get(f"{u}/ha/after").content == after
+        keys = requests.get(f"{u}/ha?list-type=2").content
+        assert b"<Key>before</Key>" in keys and b"<Key>after</Key>" in keys
+        assert requests.delete(f"{u}/ha/before").status_code == 204
+        m = g.metrics()
+        fb = int(float(next(ln for ln in m.splitlines() if ln.startswith("s3_native_store_fallbacks_total")).split()[-1]))
+        assert fb > 0
+        pool.close()
