@@ -9,6 +9,8 @@
 #   exportab  the driver's command with the exporter forced active (60 s windows at 256 MB/s),
 #             off (never) and the round-4 idle mode
 #   n2        2 ranks sharing the GPU (hipipc, RF 2)
+#   n2hbm     the same with hbm-ack durability (the shared volume out of the ack path)
+#   n4        the driver's N=4 command on 4 ranks sharing the GPU
 #   prof      rocprofv3 kernel trace of the chunkserver during a short bench
 #   configs   BASELINE configs 4 and 5
 #   secure    config 5 at production settings (TLS + SigV4/STS + IAM + SSE-S3 + audit)
@@ -48,6 +50,10 @@ for step in "$@"; do
       DFS_JOURNAL_EXPORT=idle run export_idle 600 python bench.py --steps 20 --warmup 5 || exit 1 ;;
     n2)
       run n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 || exit 1 ;;
+    n2hbm)  # the same 2 ranks with the volume out of the ack path: what the channels carry
+      run n2_hbm 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack || exit 1 ;;
+    n4)     # the driver's N=4 command, 4 ranks sharing the GPU
+      run n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 || exit 1 ;;
     prof)
       run prof 600 python bench.py --steps 3 --warmup 1 --profile-dir "$O/prof" || exit 1 ;;
     configs)
