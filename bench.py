@@ -346,8 +346,10 @@ def main():
                 pdir = os.path.abspath(os.path.join(a.profile_dir, f"cs{rank}"))
                 os.makedirs(pdir, exist_ok=True)
                 cs_env["TMPDIR"] = "/tmp"
-                cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--marker-trace", "--stats", "--output-format", "csv",
-                                      "-d", pdir, "-o", "cs", "--", *cs_cmd],
+                # DFS_PROF_EXTRA: more trace domains, e.g. "--memory-copy-trace" (never --pmc here)
+                extra = [x for x in os.environ.get("DFS_PROF_EXTRA", "").split() if not x.startswith("--pmc")]
+                cp = procs.spawn_raw(["rocprofv3", "--kernel-trace", "--marker-trace", *extra, "--stats", "--output-format",
+                                      "csv", "-d", pdir, "-o", "cs", "--", *cs_cmd],
                                      str(base_p / f"cs{rank}.log"), cs_env)
             else:
                 cp = procs.spawn_raw(cs_cmd, str(base_p / f"cs{rank}.log"), cs_env)
@@ -625,6 +627,7 @@ def main():
                     # (cores used, the quota, and time the quota throttled it); null without cgroup
                     "host_cpu_job": allr[0]["job_cpu"],
                     "client_phase_p50_ms_rank0": allr[0]["phases"],
+                    **repl_phases(allr),
                 }
                 if a.remote_steps > 0:
                     rwl = sorted(x for r in allr for x in r["remote"]["wl"])
@@ -699,6 +702,32 @@ def main():
             dist.destroy_process_group()
         except Exception:  # noqa: BLE001
             pass
+
+
+def repl_phases(allr) -> dict:
+    """Mean microseconds per replica hop by phase, over every rank's chunkserver (empty when no
+    hop went over the replication engine). Head: staging + checksum of a chained write, then
+    its persist + fan-out; per device forward the descriptor round trip. Engine send side:
+    channel turn, slice posts, the copies landing; receive side: turn + posts, landing (with
+    the per-slice checksums), verify + index/persist."""
+    def tot(k):
+        return sum(r["cs"].get(k, 0) for r in allr)
+
+    out = {}
+    if tot("fp_chain_writes"):
+        out["head_stage"] = tot("fp_chain_stage_ns") / tot("fp_chain_writes")
+        out["head_forward"] = tot("fp_chain_forward_ns") / tot("fp_chain_writes")
+    if tot("fp_desc_calls"):
+        out["descriptor_rtt"] = tot("fp_desc_ns") / tot("fp_desc_calls")
+    if tot("repl_send_calls"):
+        for k in ("send_stage", "send_turn", "send_post"):
+            out[k] = tot(f"repl_{k}_ns") / tot("repl_send_calls")
+    if tot("repl_blocks_sent"):
+        out["wait_send"] = tot("repl_wait_send_ns") / tot("repl_blocks_sent")
+    if tot("repl_recv_calls"):
+        for k in ("recv_turn", "recv_land", "recv_finish"):
+            out[k] = tot(f"repl_{k}_ns") / tot("repl_recv_calls")
+    return {"repl_phase_us": {k: round(v / 1e3, 1) for k, v in out.items()}} if out else {}
 
 
 def forward_counts(allr) -> dict:

@@ -487,28 +487,53 @@ CrcPlan plan_crc(const uint8_t* d, uint64_t n, uint32_t* meta_out, const uint32_
 }  // namespace
 
 bool ChunkStore::run_crc(Lane* l, const uint8_t* dptr, uint64_t n, uint32_t* meta_out, const uint32_t* meta_expect,
-                         bool want_block, uint64_t byte_lo, uint64_t byte_hi, CrcOut* out, std::string* err) {
+                         bool want_block, uint64_t byte_lo, uint64_t byte_hi, CrcOut* out, std::string* err,
+                         uint8_t* hmeta, bool* meta_done) {
   // Synchronous helper used by paths that do not need to overlap anything else.
+  if (meta_done) *meta_done = false;
   CrcPlan p = plan_crc(dptr, n, meta_out, meta_expect, want_block, byte_lo, byte_hi);
   if (p.grid == 0) {
     out->block_crc = 0;
     out->bad_slice = -1;
     return true;
   }
-  p.a.part_crc = want_block ? l->dscratch : nullptr;
-  p.a.part_bad = meta_expect ? l->dscratch + kMaxGridCrc : nullptr;
+  // With a device view of the lane's pinned scratch, the kernel writes its partials (and, on
+  // the LDS kernel, the .meta image) straight into host memory: no readback copies, each of
+  // which costs a copy-engine round trip of ~20-30 us whatever its size (profiles/r5_final).
+  const bool want_host_meta = meta_out && crc_meta_host_ok(p.a.ntiles) && (hmeta || (want_block && p.a.has_tail));
+  // no destination of the caller's: the image goes after the partials (only its tail word is
+  // read); sized before any pointer into the scratch is taken (a caller's hmeta already is)
+  if (want_host_meta && !hmeta) ensure_hscratch(l, (p.a.s_full + 1) * 4 + 16);
+  auto* hp = reinterpret_cast<uint32_t*>(l->hscratch);
+  auto* hdev = static_cast<uint8_t*>(l->hscratch_dev);
+  const bool direct = hdev != nullptr;
+  const bool host_meta = direct && want_host_meta;
+  uint32_t* tail_host = nullptr;  // where the tail slice's BE CRC lands on the host
+  if (host_meta) {
+    uint8_t* dst = hmeta ? hmeta : l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+    p.a.meta_host = reinterpret_cast<uint32_t*>(hdev + (dst - l->hscratch));
+    tail_host = reinterpret_cast<uint32_t*>(dst) + p.a.s_full;
+  }
+  if (direct) {
+    p.a.part_crc = want_block ? reinterpret_cast<uint32_t*>(hdev) : nullptr;
+    p.a.part_bad = meta_expect ? reinterpret_cast<uint32_t*>(hdev) + kMaxGridCrc : nullptr;
+  } else {
+    p.a.part_crc = want_block ? l->dscratch : nullptr;
+    p.a.part_bad = meta_expect ? l->dscratch + kMaxGridCrc : nullptr;
+  }
   hipError_t e = launch_crc(p.a, dtables_, p.grid, l->stream);
   launches_++;
   if (e != hipSuccess) {
     *err = std::string("crc kernel launch: ") + hipGetErrorString(e);
     return false;
   }
-  auto* hp = reinterpret_cast<uint32_t*>(l->hscratch);
   uint64_t tail_meta_off = 2 * kMaxGridCrc;
-  HIP_OK(hipMemcpyAsync(hp, l->dscratch, 2 * kMaxGridCrc * sizeof(uint32_t), hipMemcpyDeviceToHost, l->stream));
-  if (want_block && p.a.has_tail && meta_out)
+  if (!direct)
+    HIP_OK(hipMemcpyAsync(hp, l->dscratch, 2 * kMaxGridCrc * sizeof(uint32_t), hipMemcpyDeviceToHost, l->stream));
+  if (want_block && p.a.has_tail && meta_out && !host_meta)
     HIP_OK(hipMemcpyAsync(hp + tail_meta_off, meta_out + p.a.s_full, 4, hipMemcpyDeviceToHost, l->stream));
   HIP_OK(hipStreamSynchronize(l->stream));
+  if (host_meta && hmeta && meta_done) *meta_done = true;
   out->bad_slice = -1;
   if (meta_expect) {
     uint32_t bad = 0xFFFFFFFFu;
@@ -519,7 +544,7 @@ bool ChunkStore::run_crc(Lane* l, const uint8_t* dptr, uint64_t n, uint32_t* met
     uint32_t r = 0;
     for (int g = 0; g < p.grid; ++g) r ^= hp[g];
     if (p.a.has_tail) {
-      uint32_t tail_crc = __builtin_bswap32(hp[tail_meta_off]);
+      uint32_t tail_crc = __builtin_bswap32(host_meta ? *tail_host : hp[tail_meta_off]);
       r = crc_shift(r, p.a.tail_len) ^ (tail_crc ^ p.a.tail_init);
     }
     out->block_crc = r ^ crc_init_term(n);
@@ -972,8 +997,9 @@ bool ChunkStore::device_stage(const uint8_t* data, uint64_t n, const DevExtent& 
     if (S) HIP_OK(hipMemcpyAsync(dmeta, hmeta, S * 4, hipMemcpyHostToDevice, l->stream));
     HIP_OK(hipStreamSynchronize(l->stream));
   } else {
-    ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, co, err);
-    if (ok && S) {
+    bool md = false;
+    ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, co, err, hmeta, &md);
+    if (ok && S && !md) {
       HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
       HIP_OK(hipStreamSynchronize(l->stream));
     }
@@ -1770,8 +1796,9 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
   uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
   std::string err;
   CrcOut co;
-  bool ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err);
-  if (ok && S) {
+  bool md = false;
+  bool ok = run_crc(l, ext.ptr, n, dmeta, nullptr, true, 0, n, &co, &err, hmeta, &md);
+  if (ok && S && !md) {
     HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
     HIP_OK(hipStreamSynchronize(l->stream));
   }
@@ -1809,6 +1836,7 @@ bool ChunkStore::recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n) {
   rv->ext = e;
   rv->n = n;
   rv->lane = acquire_lane();
+  ensure_hscratch(static_cast<Lane*>(rv->lane), num_slices(n) * 4 + 16);
   return true;
 }
 
@@ -1821,6 +1849,12 @@ bool ChunkStore::recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi) {
   // loop, the short tail slice when the range reaches the end of the block
   CrcPlan p = plan_crc(rv->ext.ptr, rv->n, dmeta, nullptr, false, lo, hi);
   if (p.grid == 0) return true;
+  // the slice's .meta words also go straight into the lane's pinned scratch (LDS kernel), so
+  // recv_finish needs no readback copy
+  if (rv->host_meta && l->hscratch_dev && crc_meta_host_ok(p.a.ntiles))
+    p.a.meta_host = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(l->hscratch_dev) + 2 * kMaxGridCrc * sizeof(uint32_t) + 16);
+  else
+    rv->host_meta = false;
   hipError_t e = launch_crc(p.a, dtables_, p.grid, l->stream);
   launches_++;
   if (e != hipSuccess) {
@@ -1839,7 +1873,8 @@ WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint3
   auto* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
   ensure_hscratch(l, S * 4 + 16);
   uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
-  if (!rv->failed && S) HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+  if (!rv->failed && S && !rv->host_meta)
+    HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
   HIP_OK(hipStreamSynchronize(l->stream));
   auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
   release_lane(l);

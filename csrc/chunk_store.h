@@ -217,6 +217,7 @@ class ChunkStore {
     uint64_t n = 0;
     void* lane = nullptr;
     bool failed = false;
+    bool host_meta = true;  // every slice kernel mirrored its .meta words into the lane's scratch
     std::string error;
   };
   bool recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n);
@@ -328,8 +329,11 @@ class ChunkStore {
     uint32_t block_crc = 0;
     int64_t bad_slice = -1;
   };
+  // hmeta (nullable, inside the lane's hscratch): where the caller wants the .meta image on
+  // the host; *meta_done says whether the kernel wrote it there itself (no readback copy)
   bool run_crc(Lane* l, const uint8_t* dptr, uint64_t n, uint32_t* meta_out, const uint32_t* meta_expect,
-               bool want_block, uint64_t byte_lo, uint64_t byte_hi, CrcOut* out, std::string* err);
+               bool want_block, uint64_t byte_lo, uint64_t byte_hi, CrcOut* out, std::string* err,
+               uint8_t* hmeta = nullptr, bool* meta_done = nullptr);
   bool h2d_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n);
   bool d2h_chunked(Lane* l, uint8_t* dst, const uint8_t* src, uint64_t n);
   bool promote(const std::string& id, std::string* err);  // load from NVMe into HBM

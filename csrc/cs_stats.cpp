@@ -9,6 +9,8 @@
 #include "fastpath.h"
 #include "replication.h"
 
+#include <utility>
+
 namespace dfs {
 
 Json stats_json(const StoreStats& t) {
@@ -129,6 +131,11 @@ Json stats_json(const FpStats& t) {
   d.set("fp_ec_device_decodes", t.ec_device_decodes);
   d.set("fp_ec_gathered", t.ec_gathered);
   d.set("fp_ec_device_fallbacks", t.ec_device_fallbacks);
+  d.set("fp_chain_writes", t.chain_writes);
+  d.set("fp_chain_stage_ns", t.chain_stage_ns);
+  d.set("fp_chain_forward_ns", t.chain_forward_ns);
+  d.set("fp_desc_calls", t.desc_calls);
+  d.set("fp_desc_ns", t.desc_ns);
   return d;
 }
 
@@ -146,6 +153,11 @@ Json stats_json(const ReplStats& t) {
   d.set("channel_waits", t.channel_waits);
   d.set("parked_extents", t.parked_extents);
   d.set("reaped_extents", t.reaped_extents);
+  for (auto [k, v] : {std::pair<const char*, uint64_t>{"send_calls", t.send_calls}, {"send_stage_ns", t.send_stage_ns},
+                      {"send_turn_ns", t.send_turn_ns}, {"send_post_ns", t.send_post_ns}, {"wait_send_ns", t.wait_send_ns},
+                      {"recv_calls", t.recv_calls}, {"recv_turn_ns", t.recv_turn_ns}, {"recv_land_ns", t.recv_land_ns},
+                      {"recv_finish_ns", t.recv_finish_ns}})
+    d.set(k, v);
   for (auto& kv : t.sent_to) d.set("link_sent_to_" + std::to_string(kv.first), kv.second);
   for (auto& kv : t.recv_from) d.set("link_recv_from_" + std::to_string(kv.first), kv.second);
   return d;

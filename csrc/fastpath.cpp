@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
 #include <cstring>
 #include <future>
 
@@ -558,6 +559,7 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
     }
     if (posted) {
       tried_p2p = true;
+      const auto d0 = std::chrono::steady_clock::now();
       bool io_ok;
       int drop = drop_descriptors_.load();
       if (staged) {
@@ -583,6 +585,12 @@ int FastPathServer::replicate_one(const std::string& addr, const std::string& id
         // new generation) and move this replica to shared memory below
         repl_->cancel_send(&t, "descriptor to " + addr + " failed");
       } else {
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          st_.desc_calls++;
+          st_.desc_ns += static_cast<uint64_t>(
+              std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - d0).count());
+        }
         std::string werr;
         bool sent = repl_->wait_send(&t, &werr);
         FpStatus st = static_cast<FpStatus>(resp[0]);
@@ -779,12 +787,19 @@ void FastPathServer::serve(int fd) {
         if (wr.ok) bump(&FpStats::writes);
         sent = wr.ok ? send_response(fd, FpStatus::Ok, len, 1, "") : send_response(fd, FpStatus::IoError, 0, 0, wr.error);
       } else if (!write_sliced(fd, id, base + off, len, crc, term, next, ShmSrc{path, off, len}, &sent)) {
+        const auto c0 = std::chrono::steady_clock::now();
         WriteResult wr = store_->stage(id, base + off, len, crc);  // HBM + CRC verify, not yet durable
         if (!wr.ok) {
           sent = send_response(fd, FpStatus::IoError, 0, 0, wr.error);
         } else {
           bump(&FpStats::writes);
+          const auto c1 = std::chrono::steady_clock::now();
           sent = persist_and_forward(id, base + off, len, crc, term, next, ShmSrc{path, off, len});
+          const auto c2 = std::chrono::steady_clock::now();
+          std::lock_guard<std::mutex> g(mu_);
+          st_.chain_writes++;
+          st_.chain_stage_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(c1 - c0).count());
+          st_.chain_forward_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(c2 - c1).count());
         }
       }
     } else if (op == 3) {  // REPL: block arrives over the P2P transport from the head

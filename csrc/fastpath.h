@@ -89,6 +89,11 @@ struct FpStats {
   // decoded there, shards pulled for a gather, and requests that had to take the host path
   uint64_t ec_device_writes = 0, ec_shard_forwards = 0, ec_device_reads = 0, ec_device_decodes = 0;
   uint64_t ec_gathered = 0, ec_device_fallbacks = 0;
+  // chained head writes (below the sliced size): staging + checksum, then the local persist
+  // and replica fan-out together (ns summed); each device forward's descriptor round trip
+  // (from its sends being posted to the replica's reply)
+  uint64_t chain_writes = 0, chain_stage_ns = 0, chain_forward_ns = 0;
+  uint64_t desc_calls = 0, desc_ns = 0;
 };
 
 class FastPathServer {

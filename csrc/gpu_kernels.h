@@ -49,6 +49,9 @@ struct CrcLaunch {
   const uint32_t* meta_expect;    // BE CRC per slice to verify against (nullable)
   uint32_t* part_crc;             // [grid] raw shifted partials for whole-block CRC (nullable)
   uint32_t* part_bad;             // [grid] min mismatching slice index, 0xFFFFFFFF = none
+  // device view of host-visible memory that receives a copy of meta_out (nullable; honoured
+  // only by the LDS kernel, see crc_meta_host_ok): the .meta image needs no readback copy
+  uint32_t* meta_host;
 };
 
 // K1b: one launch verifies many resident blocks against their HBM .meta images. Blocks are
@@ -148,6 +151,9 @@ struct WriteCopyLaunch {
   uint8_t* dst;
   uint32_t* meta_host;
 };
+// True when launch_crc runs a block of `ntiles` tiles on the kernel that honours
+// CrcLaunch::meta_host (the LDS kernel, below the MFMA size threshold).
+bool crc_meta_host_ok(uint64_t ntiles);
 hipError_t launch_write_copy(const WriteCopyLaunch& a, const DevCrcTables* t, int grid, hipStream_t s);
 hipError_t launch_gf_matmul(const GfLaunch& a, hipStream_t s);
 hipError_t launch_scrub(const ScrubLaunch& a, const DevCrcTables* t, hipStream_t s);

@@ -454,6 +454,7 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
     if (valid && sl == 0) {
       uint32_t be = __builtin_bswap32(r ^ a.full_init);
       if (a.meta_out) a.meta_out[i] = be;
+      if (a.meta_host) a.meta_host[i] = be;
       if (a.meta_expect && a.meta_expect[i] != be) bad = min(bad, static_cast<uint32_t>(i));
     }
     if (a.part_crc) {
@@ -482,6 +483,7 @@ __global__ __launch_bounds__(kCrcWgThreads) void crc_slices_kernel(CrcLaunch a,
     if (lane == 0) {
       uint32_t be = __builtin_bswap32(r ^ a.tail_init);
       if (a.meta_out) a.meta_out[a.s_full] = be;
+      if (a.meta_host) a.meta_host[a.s_full] = be;
       if (a.meta_expect && a.meta_expect[a.s_full] != be) bad = min(bad, static_cast<uint32_t>(a.s_full));
     }
   }
@@ -1427,8 +1429,11 @@ int crc_grid_for(uint64_t ntiles, uint32_t has_tail) {
   return static_cast<int>(g);
 }
 
+bool crc_meta_host_ok(uint64_t ntiles) { return ring_for(ntiles) == 0; }
+
 hipError_t launch_crc(const CrcLaunch& a, const DevCrcTables* t, int grid, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
+  if (a.meta_host && ring_for(a.ntiles) != 0) return hipErrorInvalidValue;  // only the LDS kernel mirrors it
   switch (ring_for(a.ntiles)) {
     case 0: hipLaunchKernelGGL(crc_slices_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t); break;
     case 2:

@@ -603,8 +603,7 @@ class IpcTransport final : public P2PTransport {
         const uint64_t off = __atomic_load_n(&s.off, __ATOMIC_RELAXED), n = __atomic_load_n(&s.n, __ATOMIC_RELAXED);
         hipEvent_t ev = nullptr;
         if (n != it.n || off > l->peer_arena_bytes || n > l->peer_arena_bytes - off || ld(&r->abort) ||
-            (n && hipMemcpyAsync(l->peer_arena + off, it.src, n, hipMemcpyDeviceToDevice, c->send_stream) !=
-                      hipSuccess) ||
+            (n && copy(l->peer_arena + off, it.src, n, c->send_stream) != hipSuccess) ||
             !(ev = event()) || hipEventRecord(ev, c->send_stream) != hipSuccess) {
           if (ev) release_event(ev);
           finish_send(it.st, -1);
@@ -661,6 +660,19 @@ class IpcTransport final : public P2PTransport {
       finish_send(it.st, -1);
       release_event(it.ev);
     }
+  }
+
+  // One slice into the peer's extent: by kernel (default), or by the copy engines
+  // (DFS_IPC_COPY=sdma, the round-4 path), or by the engines when the pointers are not
+  // 16-byte aligned.
+  static hipError_t copy(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t s) {
+    static const bool sdma = [] {
+      const char* e = std::getenv("DFS_IPC_COPY");
+      return e && std::string(e) == "sdma";
+    }();
+    if (!sdma && (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 16 == 0)
+      return launch_ipc_copy(dst, src, n, s);
+    return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s);
   }
 
   hipEvent_t event() {

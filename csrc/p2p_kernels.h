@@ -57,6 +57,11 @@ hipError_t launch_ipc_send(const IpcSendArgs& a, int grid, hipStream_t s);
 // Spin until *landed >= target (or abort, or spin_ticks): the receive side's kernel.
 hipError_t launch_ipc_wait(const uint64_t* landed, uint64_t target, uint32_t* abort, uint64_t spin_ticks,
                            hipStream_t s);
+// Host-driven mode's copy: n bytes from this device's arena into the peer's (IPC-mapped,
+// over xGMI between GPUs) by the waves' own 16-byte loads and stores. Both pointers must be
+// 16-byte aligned. A copy-engine hipMemcpyAsync of a 256 KiB slice took ~31 us on average
+// (rocprofv3 memory-copy trace, profiles/r5_final); the kernel runs at HBM / link speed.
+hipError_t launch_ipc_copy(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t s);
 // Device wall-clock frequency in ticks per millisecond (hipDeviceAttributeWallClockRate).
 uint64_t wall_ticks_per_ms(int device);
 

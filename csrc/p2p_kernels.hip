@@ -8,6 +8,8 @@
 // by the peer's kernel), sleeping between polls; the wall clock bounds every wait.
 #include "p2p_kernels.h"
 
+#include <algorithm>
+
 namespace dfs {
 
 namespace {
@@ -87,7 +89,37 @@ __global__ __launch_bounds__(64) void ipc_wait_kernel(const uint64_t* landed, ui
   }
 }
 
+__global__ __launch_bounds__(256) void ipc_copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                       uint64_t n) {
+  const uint64_t nv = n / 16;
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4* d4 = reinterpret_cast<uint4*>(dst);
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  // four independent 16-byte loads in flight per lane before their stores
+  for (; i + 3 * stride < nv; i += 4 * stride) {
+    const uint4 a = s4[i], b = s4[i + stride], c = s4[i + 2 * stride], d = s4[i + 3 * stride];
+    d4[i] = a;
+    d4[i + stride] = b;
+    d4[i + 2 * stride] = c;
+    d4[i + 3 * stride] = d;
+  }
+  for (; i < nv; i += stride) d4[i] = s4[i];
+  if (blockIdx.x == 0)
+    for (uint64_t k = nv * 16 + threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
+}
+
 }  // namespace
+
+hipError_t launch_ipc_copy(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 16) return hipErrorInvalidValue;
+  // one 16-byte vector per lane up to 4 MiB (1 MiB: 256 workgroups, one per CU), then
+  // grid-stride with four loads in flight
+  const uint64_t g = std::min<uint64_t>(1024, std::max<uint64_t>(1, (n + 4095) / 4096));
+  hipLaunchKernelGGL(ipc_copy_kernel, dim3(static_cast<unsigned>(g)), dim3(256), 0, s, dst, src, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_ipc_send(const IpcSendArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL(ipc_send_kernel, dim3(grid), dim3(256), 0, s, a);

@@ -19,6 +19,10 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+uint64_t ns_since(Clock::time_point t0) {
+  return static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count());
+}
+
 enum : uint8_t { kOpen = 1, kReopen = 2 };
 enum : uint8_t { kOk = 0, kStale = 1, kNotReady = 2, kError = 3 };
 
@@ -90,6 +94,12 @@ ReplicationEngine::ReplicationEngine(ChunkStore* store, std::unique_ptr<P2PTrans
                                      ReplOptions opt)
     : store_(store), t_(std::move(transport)), rank_(rank), world_(world), opt_(opt) {
   channels_ = std::max(1, std::min(opt_.channels, t_->channels()));
+  // DFS_REPL_MIN_SLICE_KIB: smallest slice of a pipelined transfer (a block of up to 4x this
+  // size goes in one piece per 4 slices; A/B of slicing against per-slice overheads)
+  if (const char* e = std::getenv("DFS_REPL_MIN_SLICE_KIB")) {
+    const uint64_t kib = std::strtoull(e, nullptr, 10);
+    if (kib >= kSliceBytes / 1024) opt_.min_slice = std::min<uint64_t>(kib << 10, opt_.max_slice);
+  }
   for (int i = 0; i < world_; ++i) {
     peers_.push_back(std::make_unique<Peer>());
     reset_seqs_locked(*peers_.back());
@@ -509,6 +519,7 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
     }
   };
   bool failed = false, up = false;
+  const auto t0 = Clock::now();
   // a staged block's first slice must be in HBM before the block takes a place in the pair's
   // FIFO: the sequence number is reserved only then, so a transfer whose PCIe staging is still
   // queued (10 writers share the copy engines) does not hold up the transfers behind it. With
@@ -545,8 +556,11 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
       t->loaded = true;
     }
   }
+  const uint64_t stage_ns = ns_since(t0);
+  uint64_t turn_ns = 0;
   if (up) {
     // each channel is FIFO: transfers post in their channel's sequence order
+    const auto t1 = Clock::now();
     {
       std::unique_lock<std::mutex> lk(P.mu);
       if (P.post_next[t->ch] != t->seq) {
@@ -561,6 +575,7 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
         failed = true;  // the sequence number is spent: the pair cannot stay in step
       }
     }
+    turn_ns = ns_since(t1);
     if (!failed && announce && !announce(*t)) {
       *err = "descriptor to rank " + std::to_string(p) + " failed";
       failed = true;
@@ -583,6 +598,13 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
       if (P.gen == t->gen && P.post_next[t->ch] == t->seq) P.post_next[t->ch]++;
       P.cv.notify_all();
     }
+    {
+      std::lock_guard<std::mutex> sg(st_mu_);
+      st_.send_calls++;
+      st_.send_stage_ns += stage_ns;
+      st_.send_turn_ns += turn_ns;
+      st_.send_post_ns += ns_since(t0) - stage_ns - turn_ns;
+    }
     if (!failed) return true;  // the pin is held until wait_send / cancel_send
   }
   unload(t);
@@ -597,7 +619,8 @@ bool ReplicationEngine::send(int p, const std::string& id, const uint8_t* host_s
 bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
   TraceRange tr("dfs.repl.wait_send");
   Peer& P = peer(t->peer);
-  auto deadline = Clock::now() + std::chrono::milliseconds(opt_.xfer_timeout_ms);
+  const auto t0 = Clock::now();
+  auto deadline = t0 + std::chrono::milliseconds(opt_.xfer_timeout_ms);
   bool ok = true;
   int spins = 0;
   for (auto& op : t->ops) {
@@ -638,6 +661,7 @@ bool ReplicationEngine::wait_send(ReplTicket* t, std::string* err) {
     std::lock_guard<std::mutex> lk(st_mu_);
     st_.bytes_sent += t->size;
     st_.blocks_sent++;
+    st_.wait_send_ns += ns_since(t0);
     st_.sent_to[t->peer] += t->size;
   }
   return ok;
@@ -687,6 +711,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
   }
   uint8_t* dst = dev ? ext.ptr : host.data();
   std::vector<P2POp> ops;
+  const auto t0 = Clock::now();
   {
     std::unique_lock<std::mutex> lk(P.mu);
     // a descriptor may overtake our side of a bring-up (the sender saw the pair up first):
@@ -739,6 +764,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
       return res;
     }
   }
+  const auto t1 = Clock::now();
   ChunkStore::RecvVerify rv;
   if (dev) store_->recv_begin(&rv, ext, size);
   auto deadline = Clock::now() + std::chrono::milliseconds(opt_.xfer_timeout_ms);
@@ -777,9 +803,14 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
     res.error = why;
     return res;
   }
+  const auto t2 = Clock::now();
   res = dev ? store_->recv_finish(&rv, id, expected_crc, persist_now) : store_->write(id, host.data(), size, expected_crc);
   if (res.ok) {
     std::lock_guard<std::mutex> lk(st_mu_);
+    st_.recv_calls++;
+    st_.recv_turn_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count());
+    st_.recv_land_ns += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count());
+    st_.recv_finish_ns += ns_since(t2);
     st_.bytes_recv += size;
     st_.blocks_recv++;
     st_.recv_from[src] += size;

@@ -91,6 +91,12 @@ struct ReplStats {
   uint64_t pair_failures = 0, pair_opens = 0, open_attempts = 0, turn_timeouts = 0, stale_generation = 0;
   uint64_t channel_waits = 0;  // sends that found their channel's turn taken and waited for it
   uint64_t parked_extents = 0, reaped_extents = 0;  // failed-receive extents held / freed after close
+  // where a transfer's time goes (ns summed over transfers; divide by the call counts). Send
+  // side: waiting for the staged slice 0, for the channel's turn, posting the slices, and
+  // wait_send (the copies landing). Receive side: waiting for the turn and posting, the
+  // slices landing (with their per-slice checksums), and recv_finish (verify + index/persist).
+  uint64_t send_calls = 0, send_stage_ns = 0, send_turn_ns = 0, send_post_ns = 0, wait_send_ns = 0;
+  uint64_t recv_calls = 0, recv_turn_ns = 0, recv_land_ns = 0, recv_finish_ns = 0;
   // bytes of completed transfers by peer rank: what each link carried (multi-GPU diagnosis)
   std::map<int, uint64_t> sent_to, recv_from;
 };

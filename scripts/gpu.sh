@@ -52,6 +52,16 @@ for step in "$@"; do
       run n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 || exit 1 ;;
     n2hbm)  # the same 2 ranks with the volume out of the ack path: what the channels carry
       run n2_hbm 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack || exit 1 ;;
+    n2lat)  # what one forward costs without queueing (concurrency 1), and with host waits that sleep
+      run n2_hbm_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 && \
+      run n1_hbm_c1 600 python bench.py --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 && \
+      DFS_HIP_SYNC=block run n2_hbm_block 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack || exit 1 ;;
+    n2phase)  # replica hop phases (repl_phase_us) at concurrency 1 and 10, hbm-ack
+      run n2p_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 && \
+      run n2p_c10 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack || exit 1 ;;
+    n2prof)   # rocprofv3 kernel + marker + memory-copy traces of both chunkservers, 2 ranks, conc 1
+      DFS_PROF_EXTRA=--memory-copy-trace run n2prof 600 python bench.py --gpus 2 --steps 5 --warmup 1 \
+        --durability hbm-ack --concurrency 1 --remote-steps 0 --profile-dir "$O/n2prof" || exit 1 ;;
     n4)     # the driver's N=4 command, 4 ranks sharing the GPU
       run n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 || exit 1 ;;
     prof)
