@@ -472,6 +472,15 @@ def main():
                         pass
                 return snap
 
+            def cs_stats() -> dict:
+                try:
+                    import urllib.request
+
+                    return json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
+                except Exception:  # noqa: BLE001
+                    return {}
+
+            thr0 = cs_stats().get("thread_cpu_ms", {})  # per-thread CPU of the chunkserver, before
             client.phase_times = {}
             cpu0 = cpu_snapshot()
             cg0 = cgroup_cpu()
@@ -497,17 +506,13 @@ def main():
             cpu1 = cpu_snapshot()
             host_cpu = {k: round((cpu1[k] - cpu0.get(k, 0.0)) / elapsed, 2) for k in cpu1}
             job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), elapsed)
-
-            def cs_stats() -> dict:
-                try:
-                    import urllib.request
-
-                    return json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
-                except Exception:  # noqa: BLE001
-                    return {}
-
             # counters of the timed phase only (the stress / remote phases below add their own hops)
             stats = cs_stats()
+            thr1 = stats.get("thread_cpu_ms", {})
+            # cores each named chunkserver thread group used over the timed region (HIP runtime
+            # threads keep the executable's name)
+            thread_cores = {k: round((v - thr0.get(k, 0)) / 1e3 / elapsed, 2) for k, v in thr1.items()
+                            if (v - thr0.get(k, 0)) / 1e3 / elapsed >= 0.01}
             vol = {"rank_dir_bytes": _allocated_bytes(rank_dir), "volume": str(my_vol), "volumes_in_job": len(vols),
                    "journal_used_bytes": stats.get("journal_used_bytes", 0),
                    "journal_live_bytes": stats.get("journal_live_bytes", 0),
@@ -553,7 +558,7 @@ def main():
                            "rbytes": rbytes, "wt": wt,
                            "rt": rt, "cs": stats, "stress": stress, "remote": remote, "vol": vol,
                            "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
-                           "cpu": host_cpu, "job_cpu": job_cpu, "settle": journal_settle_s, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
+                           "cpu": host_cpu, "job_cpu": job_cpu, "thread_cores": thread_cores, "settle": journal_settle_s, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                        for k, v in (client.phase_times or {}).items() if v}})
             if rank == 0:
                 tmax = max(r["elapsed"] for r in allr)
@@ -626,6 +631,7 @@ def main():
                     # the whole job's CPU over the timed region, from the cgroup every rank shares
                     # (cores used, the quota, and time the quota throttled it); null without cgroup
                     "host_cpu_job": allr[0]["job_cpu"],
+                    "cs_thread_cores_rank0": dict(sorted(allr[0]["thread_cores"].items(), key=lambda kv: -kv[1])),
                     "client_phase_p50_ms_rank0": allr[0]["phases"],
                     **repl_phases(allr),
                 }

@@ -1,5 +1,6 @@
 // ChunkStore implementation. See chunk_store.h for the design.
 #include "chunk_store.h"
+#include "thread_name.h"
 #include "trace.h"
 
 #include <dirent.h>
@@ -278,7 +279,10 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     replay_journal();
   }
   scan_dirs();
-  if (journal_) materializer_ = std::thread([this] { materializer_loop(); });
+  if (journal_) materializer_ = std::thread([this] {
+    name_thread("jr-export");
+    materializer_loop();
+  });
 }
 
 ChunkStore::~ChunkStore() {

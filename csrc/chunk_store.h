@@ -455,7 +455,7 @@ class ChunkStore {
                   CrcOut* out, std::string* err);
   std::atomic<uint64_t> direct_dma_{0}, staged_dma_{0};
   std::unique_ptr<GroupSync> gsync_;
-  IoPool io_{8};  // data-file writes and .meta flushes beside the GPU staging (no per-write threads)
+  IoPool io_{8, 30000, "store-io"};  // data-file writes and .meta flushes beside the GPU staging (no per-write threads)
   std::unique_ptr<GroupSync> dsync_hot_, dsync_cold_;  // directory fsync after renames
   bool sync_dir(bool cold);
   std::unique_ptr<DiskGate> gate_;

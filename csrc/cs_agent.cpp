@@ -1,5 +1,6 @@
 // Native ChunkServer control loop; design notes in cs_agent.h.
 #include "cs_agent.h"
+#include "thread_name.h"
 
 #include <sys/statvfs.h>
 
@@ -45,8 +46,14 @@ CsAgent::CsAgent(CsAgentConfig cfg, ChunkStore* store, FastPathServer* fp, std::
 CsAgent::~CsAgent() { stop(); }
 
 void CsAgent::start() {
-  hb_ = std::thread([this] { heartbeat_loop(); });
-  scrub_ = std::thread([this] { scrub_loop(); });
+  hb_ = std::thread([this] {
+    name_thread("cs-heartbeat");
+    heartbeat_loop();
+  });
+  scrub_ = std::thread([this] {
+    name_thread("cs-scrub");
+    scrub_loop();
+  });
 }
 
 void CsAgent::stop() {

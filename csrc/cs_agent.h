@@ -121,7 +121,7 @@ class CsAgent {
   std::vector<std::string> recovering_;  // block ids with a recovery queued or running
   CsAgentStats st_;
   std::thread hb_, scrub_;
-  IoPool jobs_{8};  // last: destroyed first, after its jobs finished
+  IoPool jobs_{8, 30000, "cs-jobs"};  // last: destroyed first, after its jobs finished
 };
 
 }  // namespace dfs

@@ -2,6 +2,7 @@
 #include "fastpath.h"
 #include "gf256.h"
 #include "trace.h"
+#include "thread_name.h"
 
 #include <fcntl.h>
 #include <poll.h>
@@ -160,7 +161,10 @@ bool FastPathServer::start(std::string* err) {
     lfd_ = -1;
     return false;
   }
-  acceptor_ = std::thread([this] { accept_loop(); });
+  acceptor_ = std::thread([this] {
+    name_thread("fp-accept");
+    accept_loop();
+  });
   return true;
 }
 
@@ -270,7 +274,10 @@ void FastPathServer::accept_loop() {
     st_.connections++;
     live_workers_++;
     // detached: a finished connection frees its thread at once; stop() waits on the count
-    std::thread([this, fd] { serve(fd); }).detach();
+    std::thread([this, fd] {
+      name_thread("fp-serve");
+      serve(fd);
+    }).detach();
   }
 }
 

@@ -233,7 +233,7 @@ class FastPathServer {
   std::vector<std::string> recent_rids_;  // ring of the last kRecentRids request ids (mu_)
   size_t recent_pos_ = 0;
   FpStats st_;
-  IoPool pool_{16};  // replica fan-out helpers: reused threads, none created per write
+  IoPool pool_{16, 30000, "fp-fanout"};  // replica fan-out helpers: reused threads, none created per write
   ReplicationEngine* repl_ = nullptr;
   std::atomic<int> drop_descriptors_{0};
   std::mutex peers_mu_;

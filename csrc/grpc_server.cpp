@@ -1,5 +1,6 @@
 // Native gRPC server on nghttp2; design notes in grpc_server.h.
 #include "grpc_server.h"
+#include "thread_name.h"
 
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -401,7 +402,11 @@ bool GrpcServer::start(std::string* err) {
   socklen_t al = sizeof a;
   ::getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &al);
   port_ = ntohs(a.sin_port);
-  for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker_loop(); });
+  for (int i = 0; i < nworkers_; ++i)
+    workers_.emplace_back([this] {
+      name_thread("grpc-worker");
+      worker_loop();
+    });
   acceptor_ = std::thread([this] { accept_loop(); });
   return true;
 }
@@ -452,7 +457,10 @@ void GrpcServer::accept_loop() {
     }
     conns_.push_back(fd);
     live_conns_++;
-    std::thread([this, fd] { serve(fd); }).detach();
+    std::thread([this, fd] {
+      name_thread("grpc-conn");
+      serve(fd);
+    }).detach();
   }
 }
 

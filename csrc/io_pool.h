@@ -18,11 +18,14 @@
 #include <mutex>
 #include <thread>
 
+#include "thread_name.h"
+
 namespace dfs {
 
 class IoPool {
  public:
-  explicit IoPool(int keep = 8, int idle_ms = 30000) : s_(std::make_shared<State>()) {
+  explicit IoPool(int keep = 8, int idle_ms = 30000, const char* name = "io-pool") : s_(std::make_shared<State>()) {
+    s_->name = name;
     s_->keep = keep;
     s_->idle_ms = idle_ms;
   }
@@ -64,9 +67,11 @@ class IoPool {
     int threads = 0, idle = 0, keep = 8, idle_ms = 30000;
     uint64_t spawned = 0;
     bool stop = false;
+    const char* name = "io-pool";
   };
 
   static void loop(std::shared_ptr<State> s) {
+    name_thread(s->name);
     std::unique_lock<std::mutex> lk(s->mu);
     for (;;) {
       if (s->q.empty()) {

@@ -1,5 +1,6 @@
 // BlockJournal implementation. See journal.h for the format and the protocol.
 #include "journal.h"
+#include "thread_name.h"
 
 #include <dirent.h>
 #include <fcntl.h>
@@ -260,6 +261,7 @@ void BlockJournal::mark_sealed_now() {
 // parts out once (8 MiB at a time, re-checking between chunks), so first-cycle appends are
 // overwrites of written extents.
 void BlockJournal::prepare_loop() {
+  name_thread("jr-prepare");
   static const std::vector<uint8_t> zeros(8 << 20, 0);
   std::unique_lock<std::mutex> lk(mu_);
   auto grow_check_ns = 0ull;

@@ -53,6 +53,7 @@
 
 #include "p2p_kernels.h"
 #include "p2p_transport.h"
+#include "thread_name.h"
 
 namespace dfs {
 
@@ -375,7 +376,10 @@ class IpcTransport final : public P2PTransport {
       c->in->owner = false;
       if (!spin_) {
         c->stop.store(false);
-        c->worker = std::thread([this, lp = &l, cp = c.get(), out = c->out] { worker(lp, cp, out); });
+        c->worker = std::thread([this, lp = &l, cp = c.get(), out = c->out] {
+          name_thread("ipc-chan");
+          worker(lp, cp, out);
+        });
       }
     }
     l.up = true;

@@ -12,6 +12,7 @@
 
 #include "crc32.h"
 #include "trace.h"
+#include "thread_name.h"
 
 namespace dfs {
 
@@ -136,6 +137,7 @@ void ReplicationEngine::spawn(std::function<void()> fn) {
     live_threads_++;
   }
   std::thread([this, fn = std::move(fn)] {
+    name_thread("repl-ctl");
     fn();
     std::lock_guard<std::mutex> g(threads_mu_);
     if (--live_threads_ == 0) threads_cv_.notify_all();

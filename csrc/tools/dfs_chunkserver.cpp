@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "chunk_store.h"
+#include "thread_name.h"
 #include "crc32.h"
 #include "cs_agent.h"
 #include "cs_grpc.h"
@@ -355,6 +356,10 @@ int main(int argc, char** argv) {
       d.set("repl_pairs_up", up);
     }
     d.set("native_chunkserver", true);
+    // CPU milliseconds by thread name (live threads): what the process spends its cores on
+    Json tc = Json::object();
+    for (const auto& [name, ms] : thread_cpu_ms()) tc.set(name, static_cast<uint64_t>(ms));
+    d.set("thread_cpu_ms", tc);
     return d;
   };
   Gauges metrics;
