@@ -66,6 +66,9 @@ for step in "$@"; do
       run n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 || exit 1 ;;
     prof)
       run prof 600 python bench.py --steps 3 --warmup 1 --profile-dir "$O/prof" || exit 1 ;;
+    profcopy) # the N=1 profile with the memory-copy trace (which copies still use the copy engines)
+      DFS_PROF_EXTRA=--memory-copy-trace run profcopy 600 python bench.py --steps 3 --warmup 1 --remote-steps 0 \
+        --profile-dir "$O/profcopy" || exit 1 ;;
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
