@@ -342,14 +342,14 @@ class IpcTransport final : public P2PTransport {
       st(&c->out->r->sender_attached, 1u);
     }
     // warm-up: 64 bytes each way through the peer's exported probe, proving the IPC mapping
-    // and the copy path end to end before the pair is declared up (channel 0's stream and
+    // and the copy path (the same kernel or copy-engine copy the slices take) end to end
+    // before the pair is declared up (channel 0's stream and
     // ring; the other channels' rings were mapped above and checked for the generation)
     Lane& c0 = *l.ch[0];
     uint64_t pat[8] = {kRingMagic, gen, static_cast<uint64_t>(rank_), static_cast<uint64_t>(peer), 0, 0, 0, 0};
     uint8_t* mine = probe_ + kMaxRanks * 64 + peer * 64;
     if (hipMemcpyAsync(mine, pat, sizeof pat, hipMemcpyHostToDevice, c0.send_stream) != hipSuccess ||
-        hipMemcpyAsync(l.peer_probe + rank_ * 64, mine, sizeof pat, hipMemcpyDeviceToDevice, c0.send_stream) !=
-            hipSuccess ||
+        copy(l.peer_probe + rank_ * 64, mine, sizeof pat, c0.send_stream) != hipSuccess ||  // the data path's copy
         hipStreamSynchronize(c0.send_stream) != hipSuccess) {
       *err = "warm-up copy failed";
       return fail_open(l, err);

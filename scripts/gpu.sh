@@ -69,6 +69,12 @@ for step in "$@"; do
     profcopy) # the N=1 profile with the memory-copy trace (which copies still use the copy engines)
       DFS_PROF_EXTRA=--memory-copy-trace run profcopy 600 python bench.py --steps 3 --warmup 1 --remote-steps 0 \
         --profile-dir "$O/profcopy" || exit 1 ;;
+    syncab)   # how host threads wait for the GPU: runtime default, blocking (interrupt), yield
+      run sync_default 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
+      DFS_HIP_SYNC=block run sync_block 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
+      DFS_HIP_SYNC=yield run sync_yield 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
+      DFS_HIP_SYNC=block run sync_block_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 && \
+      run sync_default_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 || exit 1 ;;
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
