@@ -75,6 +75,12 @@ for step in "$@"; do
       DFS_HIP_SYNC=yield run sync_yield 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
       DFS_HIP_SYNC=block run sync_block_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 && \
       run sync_default_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 || exit 1 ;;
+    volab)    # 4 ranks on one volume: exporter off, O_DIRECT journal, and the N=1 command with O_DIRECT
+      run vol_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_EXPORT=never run vol_n4_noexport 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_DIRECT=1 run vol_n4_direct 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_DIRECT=1 run vol_n1_direct 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
+      run vol_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 || exit 1 ;;
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
