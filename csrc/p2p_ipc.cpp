@@ -337,6 +337,14 @@ class IpcTransport final : public P2PTransport {
     }
     l.peer_probe = static_cast<uint8_t*>(pp);
     l.gen = gen;
+    // slices are copied by kernel when this device reaches the peer's memory (the same
+    // device, or a peer the runtime reports accessible over xGMI); else by the copy engines
+    {
+      int can = 0;
+      l.kernel_copy = tw.device == device_ ||
+                      (hipDeviceCanAccessPeer(&can, device_, tw.device) == hipSuccess && can != 0);
+      (void)hipGetLastError();
+    }
     for (auto& c : l.ch) {
       st(&c->in->r->receiver_ready, 1u);
       st(&c->out->r->sender_attached, 1u);
@@ -349,7 +357,7 @@ class IpcTransport final : public P2PTransport {
     uint64_t pat[8] = {kRingMagic, gen, static_cast<uint64_t>(rank_), static_cast<uint64_t>(peer), 0, 0, 0, 0};
     uint8_t* mine = probe_ + kMaxRanks * 64 + peer * 64;
     if (hipMemcpyAsync(mine, pat, sizeof pat, hipMemcpyHostToDevice, c0.send_stream) != hipSuccess ||
-        copy(l.peer_probe + rank_ * 64, mine, sizeof pat, c0.send_stream) != hipSuccess ||  // the data path's copy
+        copy(l.peer_probe + rank_ * 64, mine, sizeof pat, c0.send_stream, l.kernel_copy) != hipSuccess ||
         hipStreamSynchronize(c0.send_stream) != hipSuccess) {
       *err = "warm-up copy failed";
       return fail_open(l, err);
@@ -531,6 +539,7 @@ class IpcTransport final : public P2PTransport {
     uint8_t* peer_arena = nullptr;
     uint64_t peer_arena_bytes = 0;
     uint8_t* peer_probe = nullptr;
+    bool kernel_copy = false;  // this device's waves may store into the peer's mapping
     std::vector<std::unique_ptr<Lane>> ch;
   };
 
@@ -607,7 +616,7 @@ class IpcTransport final : public P2PTransport {
         const uint64_t off = __atomic_load_n(&s.off, __ATOMIC_RELAXED), n = __atomic_load_n(&s.n, __ATOMIC_RELAXED);
         hipEvent_t ev = nullptr;
         if (n != it.n || off > l->peer_arena_bytes || n > l->peer_arena_bytes - off || ld(&r->abort) ||
-            (n && copy(l->peer_arena + off, it.src, n, c->send_stream) != hipSuccess) ||
+            (n && copy(l->peer_arena + off, it.src, n, c->send_stream, l->kernel_copy) != hipSuccess) ||
             !(ev = event()) || hipEventRecord(ev, c->send_stream) != hipSuccess) {
           if (ev) release_event(ev);
           finish_send(it.st, -1);
@@ -668,13 +677,13 @@ class IpcTransport final : public P2PTransport {
 
   // One slice into the peer's extent: by kernel (default), or by the copy engines
   // (DFS_IPC_COPY=sdma, the round-4 path), or by the engines when the pointers are not
-  // 16-byte aligned.
-  static hipError_t copy(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t s) {
+  // 16-byte aligned or the peer's memory is not reachable from this device's waves.
+  static hipError_t copy(uint8_t* dst, const uint8_t* src, uint64_t n, hipStream_t s, bool kernel_ok) {
     static const bool sdma = [] {
       const char* e = std::getenv("DFS_IPC_COPY");
       return e && std::string(e) == "sdma";
     }();
-    if (!sdma && (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 16 == 0)
+    if (!sdma && kernel_ok && (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 16 == 0)
       return launch_ipc_copy(dst, src, n, s);
     return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s);
   }

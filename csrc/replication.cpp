@@ -95,11 +95,11 @@ ReplicationEngine::ReplicationEngine(ChunkStore* store, std::unique_ptr<P2PTrans
                                      ReplOptions opt)
     : store_(store), t_(std::move(transport)), rank_(rank), world_(world), opt_(opt) {
   channels_ = std::max(1, std::min(opt_.channels, t_->channels()));
-  // DFS_REPL_MIN_SLICE_KIB: smallest slice of a pipelined transfer (a block of up to 4x this
-  // size goes in one piece per 4 slices; A/B of slicing against per-slice overheads)
+  // DFS_REPL_MIN_SLICE_KIB: smallest slice of a pipelined transfer, for every transport (A/B
+  // of slicing against per-slice overheads)
   if (const char* e = std::getenv("DFS_REPL_MIN_SLICE_KIB")) {
     const uint64_t kib = std::strtoull(e, nullptr, 10);
-    if (kib >= kSliceBytes / 1024) opt_.min_slice = std::min<uint64_t>(kib << 10, opt_.max_slice);
+    if (kib >= kSliceBytes / 1024) opt_.min_slice = opt_.device_min_slice = std::min<uint64_t>(kib << 10, opt_.max_slice);
   }
   for (int i = 0; i < world_; ++i) {
     peers_.push_back(std::make_unique<Peer>());
@@ -264,7 +264,8 @@ uint64_t ReplicationEngine::generation(int p) {
 }
 
 uint64_t ReplicationEngine::slice_for(uint64_t n) const {
-  uint64_t s = std::min(std::max(n / 4, opt_.min_slice), opt_.max_slice);
+  const uint64_t mn = t_->device_buffers() ? opt_.device_min_slice : opt_.min_slice;
+  uint64_t s = std::min(std::max(n / 4, mn), opt_.max_slice);
   s = (s + kSliceBytes - 1) / kSliceBytes * kSliceBytes;
   uint64_t whole = (n + kSliceBytes - 1) / kSliceBytes * kSliceBytes;
   return std::max<uint64_t>(kSliceBytes, std::min(s, whole));

@@ -15,8 +15,9 @@
 //    make b->c's FIFO wait on a->b's; with chains in both directions around the node
 //    (A->B->C next to C->A->B) those FIFO couplings close a cycle and deadlock. Fan-out
 //    sends depend only on data already resident in HBM, so no cycle can form.
-//  * Slice pipelining. A block travels as slices (256 KiB..4 MiB, multiples of the 512 B
-//    checksum slice); the receiver launches the K1 checksum of slice s as soon as it lands,
+//  * Slice pipelining. A block travels as slices (256 KiB..4 MiB on the socket transport,
+//    1..4 MiB on the device transports; multiples of the 512 B checksum slice); the
+//    receiver launches the K1 checksum of slice s as soon as it lands,
 //    while slice s+1 is still on the link, then folds the slice CRCs into the block CRC.
 //  * Sequencing. Each direction of each pair has K FIFO channels (round 5; K = channels,
 //    default 4): a transfer takes the least-loaded channel, the sender stamps it with the
@@ -53,7 +54,11 @@ struct ReplOptions {
   int open_timeout_ms = 20000;   // one bring-up attempt of a pair
   int turn_timeout_ms = 3000;    // receiver waiting for its sequence turn
   int xfer_timeout_ms = 20000;   // one block transfer once posted
-  uint64_t min_slice = 256 << 10;
+  uint64_t min_slice = 256 << 10;         // host transports (socket): pipelined from 1 MiB up
+  // device transports: a 1 MiB block goes in one slice (each slice costs a copy launch, an
+  // event and a wake-up on both sides: 4 x 256 KiB took 73 us to land, 1 x 1 MiB 43 us,
+  // profiles/r5_repl); pipelining starts at 4 MiB
+  uint64_t device_min_slice = 1 << 20;
   uint64_t max_slice = 4 << 20;
   int channels = 4;  // FIFO channels per direction of a pair (capped by the transport's)
 };

@@ -81,6 +81,12 @@ for step in "$@"; do
       DFS_JOURNAL_DIRECT=1 run vol_n4_direct 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
       DFS_JOURNAL_DIRECT=1 run vol_n1_direct 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
       run vol_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 || exit 1 ;;
+    sliceab)  # 1 MiB replica transfers in one slice instead of four (hbm-ack and nvme-sync)
+      DFS_REPL_MIN_SLICE_KIB=1024 run s1m_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 --remote-steps 0 && \
+      DFS_REPL_MIN_SLICE_KIB=1024 run s1m_c10 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --remote-steps 0 && \
+      run s256k_c10 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --remote-steps 0 && \
+      DFS_REPL_MIN_SLICE_KIB=1024 run s1m_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 && \
+      run s256k_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 || exit 1 ;;
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
