@@ -203,7 +203,10 @@ def test_compaction_relocates_live_records(native, tmp_path, never):
         st0 = s.stats()
         moved = s.compact(0.5)
         st = s.stats()
-        assert moved > 0 and st["relocated_blocks"] == moved, st
+        # the background compactor may already have relocated some (the deletes trigger it):
+        # the explicit pass moves what is left
+        assert moved >= 0 and st["relocated_blocks"] >= st0["relocated_blocks"] + moved, (st0, st)
+        assert st["relocated_blocks"] > 0, st
         assert st["journal_segs_retired"] > st0["journal_segs_retired"], (st0, st)
         assert st["journal_live_records"] == len(keep), st
         for k in keep:
