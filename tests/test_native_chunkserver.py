@@ -36,6 +36,8 @@ def test_chunkservers_run_as_native_executables():
             st = cs_stats(cl, i)
             assert st["native_chunkserver"] is True and st["native_grpc_fallbacks"] == 0
             assert st["journal_mode"] == "none"  # fsync=False: no journal
+            # per-thread CPU by thread name (bench.py's cs_thread_cores_rank0)
+            assert "fp-accept" in st["thread_cpu_ms"] and "dfs_chunkserver" in st["thread_cpu_ms"], st["thread_cpu_ms"]
         assert urllib.request.urlopen(cl.cs_http[0] + "/health", timeout=5).read() == b"OK"
         assert b"dfs_chunkserver_total_chunks" in urllib.request.urlopen(cl.cs_http[0] + "/metrics", timeout=5).read()
 

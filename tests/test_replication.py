@@ -144,6 +144,16 @@ def test_fanout_crossing_chains_no_deadlock(cluster):
     assert all(nd.eng.stats()["pair_failures"] == 0 for nd in nodes)
     sent = sum(nd.eng.stats()["bytes_sent"] for nd in nodes)
     assert sent == 2 * sum(len(j[2]) for j in jobs)
+    # the hop timers bench.py reports as repl_phase_us: one send and one receive per replica,
+    # every phase accounted, and the head's descriptor round trip covering the receive side
+    es = [nd.eng.stats() for nd in nodes]
+    fs = [nd.fp.stats() for nd in nodes]
+    assert sum(e["send_calls"] for e in es) == sum(e["recv_calls"] for e in es) == 2 * len(jobs)
+    for k in ("send_post_ns", "wait_send_ns", "recv_turn_ns", "recv_land_ns", "recv_finish_ns"):
+        assert sum(e[k] for e in es) > 0, k
+    assert sum(f["fp_desc_calls"] for f in fs) == 2 * len(jobs)
+    assert sum(f["fp_chain_writes"] for f in fs) == len(jobs)
+    assert sum(f["fp_desc_ns"] for f in fs) >= sum(e["recv_land_ns"] + e["recv_finish_ns"] for e in es)
     arena.close()
 
 
