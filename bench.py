@@ -609,6 +609,9 @@ def main():
                     "fused_reads": sum(r["cs"].get("fused_reads", 0) for r in allr),
                     "direct_writes": sum(r["cs"].get("direct_writes", 0) for r in allr),
                     "disk_gate_waits": sum(r["cs"].get("disk_gate_waits", 0) for r in allr),
+                    # store calls that found all of a chunkserver's GPU stream contexts busy
+                    "lane_waits": sum(r["cs"].get("lane_waits", 0) for r in allr),
+                    "lane_wait_ms": round(sum(r["cs"].get("lane_wait_ns", 0) for r in allr) / 1e6, 3),
                     # block journal (group commit): records appended, flush rounds that covered them,
                     # and blocks already written out as <id> + <id>.meta by the materializer
                     "journal": {k: sum(r["cs"].get(f, 0) for r in allr) for k, f in (

@@ -423,7 +423,13 @@ int64_t ChunkStore::alloc_locked(std::unique_lock<std::mutex>& lk, uint64_t byte
 
 ChunkStore::Lane* ChunkStore::acquire_lane() {
   std::unique_lock<std::mutex> lk(lane_mu_);
-  lane_cv_.wait(lk, [&] { return !free_lanes_.empty(); });
+  if (free_lanes_.empty()) {  // every stream context busy: count the wait (lane_waits / lane_wait_ns)
+    const auto t0 = std::chrono::steady_clock::now();
+    lane_cv_.wait(lk, [&] { return !free_lanes_.empty(); });
+    lane_waits_++;
+    lane_wait_ns_ += static_cast<uint64_t>(
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+  }
   Lane* l = free_lanes_.back();
   free_lanes_.pop_back();
   return l;
@@ -1839,14 +1845,29 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
 bool ChunkStore::recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n) {
   rv->ext = e;
   rv->n = n;
-  rv->lane = acquire_lane();
-  ensure_hscratch(static_cast<Lane*>(rv->lane), num_slices(n) * 4 + 16);
+  // no lane yet: a receive waits for its bytes without holding one of the store's streams
+  // (at 10 writers per rank the waiting receives held the lanes the heads' stagings needed);
+  // DFS_RECV_LANE_EAGER=1 takes it here, as before (A/B)
+  static const bool eager = [] {
+    const char* e = std::getenv("DFS_RECV_LANE_EAGER");
+    return e && e[0] == '1';
+  }();
+  rv->lane = nullptr;
+  if (eager) recv_lane(rv);
   return true;
+}
+
+void* ChunkStore::recv_lane(RecvVerify* rv) {
+  if (!rv->lane) {
+    rv->lane = acquire_lane();
+    ensure_hscratch(static_cast<Lane*>(rv->lane), num_slices(rv->n) * 4 + 16);
+  }
+  return rv->lane;
 }
 
 bool ChunkStore::recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi) {
   if (rv->failed || hi <= lo) return !rv->failed;
-  Lane* l = static_cast<Lane*>(rv->lane);
+  Lane* l = static_cast<Lane*>(recv_lane(rv));
   (void)hipSetDevice(cfg_.device);
   auto* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(rv->n, 1), 256));
   // range mode writing (not verifying) the slices of [lo, hi): full slices via the tile
@@ -1871,7 +1892,7 @@ bool ChunkStore::recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi) {
 WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint32_t expected_crc, bool persist_now) {
   TraceRange tr("dfs.store.recv_commit");
   WriteResult res;
-  Lane* l = static_cast<Lane*>(rv->lane);
+  Lane* l = static_cast<Lane*>(recv_lane(rv));
   (void)hipSetDevice(cfg_.device);
   uint64_t n = rv->n, S = num_slices(n);
   auto* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
@@ -2342,6 +2363,11 @@ StoreStats ChunkStore::stats() {
   s.mirror_bytes = mirror_bytes_;
   s.io_threads_spawned = io_.spawned();
   s.scrub_device_blocks = scrub_dev_blocks_.load();
+  {
+    std::lock_guard<std::mutex> lg(lane_mu_);
+    s.lane_waits = lane_waits_;
+    s.lane_wait_ns = lane_wait_ns_;
+  }
   if (journal_) {
     JournalStats j = journal_->stats();
     s.journal = true;

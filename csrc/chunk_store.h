@@ -112,6 +112,7 @@ struct StoreStats {
   uint64_t journal_sync_ns = 0, journal_commit_ns = 0, journal_bypassed = 0;
   uint64_t relocated_blocks = 0, relocated_bytes = 0, compactions = 0, export_deferred_headroom = 0;
   uint64_t scrub_device_blocks = 0;  // durable (journal / file) copies verified by the K1b kernel
+  uint64_t lane_waits = 0, lane_wait_ns = 0;  // callers that found every lane (stream context) busy
   bool journal_failed = false, journal_grow_blocked = false;
   std::string journal_last_error, materialize_last_error;
 };
@@ -221,6 +222,7 @@ class ChunkStore {
     std::string error;
   };
   bool recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n);
+  void* recv_lane(RecvVerify* rv);  // the receive's lane, taken at its first slice
   bool recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi);  // lo, hi: byte range, lo % 512 == 0
   WriteResult recv_finish(RecvVerify* rv, const std::string& id, uint32_t expected_crc, bool persist_now);
   // Gives the lane back without touching the extent (a late DMA may still land in it).
@@ -322,6 +324,7 @@ class ChunkStore {
   void touch_locked(const std::string& id, Block& b);
   void lru_remove_locked(Block& b);
   Lane* acquire_lane();
+  uint64_t lane_waits_ = 0, lane_wait_ns_ = 0;  // under lane_mu_
   void release_lane(Lane* l);
   void ensure_hscratch(Lane* l, uint64_t bytes);
   // Device pass: CRC (and meta write or verify) over [slice range] of a resident block.

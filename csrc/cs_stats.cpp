@@ -58,6 +58,8 @@ Json stats_json(const StoreStats& t) {
   d.set("compactions", t.compactions);
   d.set("export_deferred_headroom", t.export_deferred_headroom);
   d.set("scrub_device_blocks", t.scrub_device_blocks);
+  d.set("lane_waits", t.lane_waits);
+  d.set("lane_wait_ns", t.lane_wait_ns);
   d.set("journal_full_waits", t.journal_full_waits);
   d.set("journal_segs", t.journal_segs);
   d.set("journal_segs_free", t.journal_segs_free);

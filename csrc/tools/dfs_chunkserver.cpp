@@ -226,7 +226,12 @@ int main(int argc, char** argv) {
   sc.hbm_capacity = parse_size(a.get("hbm-capacity", "0"));
   sc.durability = a.get("durability", "nvme-sync") == "hbm-ack" ? Durability::HbmAck : Durability::NvmeSync;
   sc.cache_blocks = std::atoi(env("BLOCK_CACHE_SIZE", "100").c_str());
-  sc.lanes = static_cast<int>(a.get_int("lanes", 8));
+  sc.lanes = static_cast<int>(a.get_int("lanes", [] {  // DFS_CS_LANES: the default when --lanes is absent
+    const char* e = std::getenv("DFS_CS_LANES");
+    // 16: with 8, waiting stagings, receives, reads and spills queued for a stream context
+    // (4,050 waits, 0.87 s in one 2-rank run; 16 lanes: 15 waits, profiles/r5_repl/laneab)
+    return e && std::atoi(e) > 0 ? std::atoi(e) : 16;
+  }()));
   sc.spill_threads = 4;
   sc.sync_writes = !a.flag("no-fsync");
   std::unique_ptr<ChunkStore> store;

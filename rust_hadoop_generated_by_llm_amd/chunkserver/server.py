@@ -51,7 +51,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--gpu", type=int, default=-1, help="HIP device for the HBM store (-1 = CPU store)")
     p.add_argument("--hbm-capacity", default="0", help="arena bytes (suffix K/M/G ok); 0 = auto")
     p.add_argument("--durability", choices=["nvme-sync", "hbm-ack"], default="nvme-sync")
-    p.add_argument("--lanes", type=int, default=8)
+    p.add_argument("--lanes", type=int, default=16)
     p.add_argument("--rccl-rank", type=int, default=-1)
     p.add_argument("--rccl-world", type=int, default=0)
     p.add_argument("--rccl-rendezvous", default="")

@@ -87,6 +87,15 @@ for step in "$@"; do
       run s256k_c10 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --remote-steps 0 && \
       DFS_REPL_MIN_SLICE_KIB=1024 run s1m_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 && \
       run s256k_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 || exit 1 ;;
+    laneab)   # 8 vs 16 stream contexts per chunkserver, receives taking theirs eagerly or at landing
+      DFS_RECV_LANE_EAGER=1 run l8e 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --remote-steps 0 && \
+      run l8 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --remote-steps 0 && \
+      DFS_CS_LANES=16 run l16 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --remote-steps 0 && \
+      DFS_CS_LANES=16 DFS_RECV_LANE_EAGER=1 run l16e 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --remote-steps 0 && \
+      DFS_CS_LANES=16 run l16_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 && \
+      run l8_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 && \
+      DFS_CS_LANES=16 run l16_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
+      run l8_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 || exit 1 ;;
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
