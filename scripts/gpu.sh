@@ -96,6 +96,17 @@ for step in "$@"; do
       run l8_n2 600 python bench.py --gpus 2 --steps 10 --warmup 2 --remote-steps 0 && \
       DFS_CS_LANES=16 run l16_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
       run l8_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 || exit 1 ;;
+    partab)   # 4 ranks on one volume: fewer journal parts per chunkserver (more records per flush)
+      run p8_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_PARTS=2 run p2_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_PARTS=1 run p1_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_SYNC_DELAY_US=300 run d300_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 || exit 1 ;;
+    partab2)  # more journal parts: 16 / 32 at 4 ranks, 16 at N=1
+      DFS_JOURNAL_PARTS=16 run p16_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_PARTS=32 run p32_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      run p8_n4b 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_PARTS=16 run p16_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
+      run p8_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 || exit 1 ;;
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
