@@ -535,6 +535,18 @@ def parquet_phase(url: str, a) -> dict:
     s3 = pafs.S3FileSystem(endpoint_override=url.split("://")[1], scheme="http", access_key="ak",
                            secret_key="sk", region="us-east-1", allow_bucket_creation=True)
     s3.create_dir("parquet")
+    # where the write time goes: the same table encoded into memory (pyarrow's Parquet
+    # encoder on this CPU, no S3), then those bytes uploaded on their own (the SDK's
+    # multipart upload against the gateway), then the end-to-end write Spark would do
+    t0 = time.perf_counter()
+    buf = pa.BufferOutputStream()
+    pq.write_table(table, buf, row_group_size=max(1, rows // 8))
+    encoded = buf.getvalue()
+    enc = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    with s3.open_output_stream("parquet/encoded.parquet") as f:
+        f.write(encoded)
+    up = time.perf_counter() - t0
     t0 = time.perf_counter()
     pq.write_table(table, "parquet/events.parquet", filesystem=s3, row_group_size=max(1, rows // 8))
     w = time.perf_counter() - t0
@@ -549,6 +561,8 @@ def parquet_phase(url: str, a) -> dict:
     rc = time.perf_counter() - t0
     assert abs(agg - pc.sum(table["value"]).as_py()) < 1e-6 * rows
     return {"rows": rows, "file_bytes": size, "write_mb_per_s": round(size / (1 << 20) / w, 1),
+            "encode_only_s": round(enc, 3), "upload_only_mb_per_s": round(encoded.size / (1 << 20) / up, 1),
+            "write_s": round(w, 3),
             "read_mb_per_s": round(size / (1 << 20) / r, 1), "projected_read_sum_s": round(rc, 3),
             "verified": True}
 
