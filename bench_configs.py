@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import hashlib
 import json
+import shutil
 import os
 import subprocess
 import sys
@@ -335,6 +336,28 @@ def _cs_counters(cluster) -> dict:
     return {k: st.get(k, 0) for k in _CS_KEYS if isinstance(st.get(k, 0), (int, float))}
 
 
+def _cs_gauges(cluster) -> dict:
+    """Where the first chunkserver's journal stands after a phase: used / live bytes, blocks,
+    reclaim work so far, whether it may still grow, and the volume's free bytes."""
+    if cluster is None or not cluster.cs_http:
+        return {}
+    try:
+        import urllib.request
+
+        st = json.loads(urllib.request.urlopen(cluster.cs_http[0] + "/stats", timeout=5).read())
+    except (OSError, ValueError):
+        return {}
+    keys = ("blocks", "journal_used_bytes", "journal_live_bytes", "journal_live_records", "journal_segs",
+            "journal_grow_blocked", "compactions", "relocated_blocks", "journal_tombstones", "materialize_pending",
+            "agent_deletes", "deletes")
+    out = {k: st[k] for k in keys if k in st}
+    try:
+        out["volume_free_bytes"] = shutil.disk_usage(cluster.base if hasattr(cluster, "base") else "/tmp").free
+    except OSError:
+        pass
+    return out
+
+
 def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mpu_key: str = "big.bin",
                       cluster=None) -> dict:
     """PUT / GET / Range GET 64 KiB / ListObjectsV2 / the S3A operations (HEAD, CopyObject,
@@ -390,6 +413,7 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
         res["job_cpu"] = job_cpu
         res["cores_by_process"] = {k: round((v - pc0.get(k, 0.0)) / el, 2) for k, v in pc1.items()}
         res["chunkserver"] = {k: v - cs0.get(k, 0) for k, v in _cs_counters(cluster).items()}
+        res["chunkserver_after"] = _cs_gauges(cluster)
         after = _front_counters(url)
         res["front_requests"] = after["requests"] - before["requests"]
         # the /metrics scrapes around the phase are answered by the Python workers (their

@@ -271,6 +271,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.sync = cfg_.sync_writes;
     mat_pressure_ = env_int("DFS_JOURNAL_PRESSURE_PCT", 70) / 100.0;
     journal_bypass_ = env_int("DFS_JOURNAL_BYPASS", 1) != 0;  // 0: writers wait for the materializer
+    journal_gate_ = env_int("DFS_JOURNAL_GATE", 0) != 0;
     // 500 ms: the pauses of a running benchmark (barriers, device syncs, a warm-up's end) are
     // shorter, so a batch and its syncfs do not land on the first timed writes (with 100 ms,
     // 256 blocks were materialized there and the driver's run lost 15-25 %: r4o, r4y)
@@ -2630,6 +2631,9 @@ bool ChunkStore::journal_block(const std::string& id, const uint8_t* host, const
   const uint64_t S = meta_be.size() / 4;
   JournalRec jr;
   bool ok = true;
+  // DFS_JOURNAL_GATE=1: the append + commit holds a node-wide disk slot (taken before any
+  // lane, so no slot holder ever waits for a lane holder that waits for a slot)
+  DiskGate::Slot slot = journal_gate_ && gate_ ? gate_->acquire() : DiskGate::Slot{};
   if (dev) {
     // out of HBM through the lane's two pinned chunks: the D2H of chunk c+1 overlaps the
     // append of chunk c. The lane is taken before the record so a writer never holds a
@@ -2683,6 +2687,7 @@ WriteResult ChunkStore::stage_journal(const std::string& id, const uint8_t* data
   const uint64_t S = num_slices(n);
   JournalRec jr;
   std::string err;
+  DiskGate::Slot slot = journal_gate_ && gate_ ? gate_->acquire() : DiskGate::Slot{};  // see journal_block
   if (!journal_->reserve(n, S, &jr, &err)) {
     release(ext);
     res.error = err;
@@ -3026,7 +3031,8 @@ void ChunkStore::materializer_loop() {
   double tokens = burst;
   auto t_prev = std::chrono::steady_clock::now();
   bool headroom = false, stop_failed = false;
-  auto headroom_at = t_prev;
+  bool want_compact = false, compact_urgent = false;
+  auto headroom_at = t_prev, compact_check_at = t_prev;
   std::vector<MatItem> batch;
   for (;;) {
     batch.clear();
@@ -3045,11 +3051,34 @@ void ChunkStore::materializer_loop() {
           continue;
         }
         forced = mat_force_ > 0 || mat_stop_;
+        // Reclaim before export: while a quarter of the journal is dead and its oldest segment
+        // can be compacted, the tokens go to relocation, not to exports. Segments are reused
+        // oldest first, so one old segment holding a few live records keeps every dead one
+        // behind it; with the exports spending every token as it arrived, compaction never
+        // ran under sustained overwrites and the journal grew until the volume was full (config
+        // 5's 10 s phases: 5,780 writer waits, multipart uploads timing out at 120 s, r5w). A
+        // journal that can no longer grow compacts without waiting for tokens.
+        if (store_mode_ && !forced && t >= compact_check_at) {
+          compact_check_at = t + std::chrono::milliseconds(20);
+          lk.unlock();
+          const JournalStats j = journal_->stats();
+          const bool dead = j.grow_blocked || (j.used_bytes && j.used_bytes - j.live_bytes > j.used_bytes / 4);
+          want_compact = dead && journal_->compaction_candidate(compact_live_) != nullptr;
+          compact_urgent = j.grow_blocked;
+          lk.lock();
+        }
+        if (want_compact && (tokens >= burst / 2 || compact_urgent) && !mat_paused_ && !mat_stop_) {
+          compact_now = true;
+          want_compact = false;  // re-evaluated after this pass
+          compact_check_at = t;
+          break;
+        }
         if (!mat_q_.empty()) {
           if (forced) break;
           if (!store_mode_) {
             if (materialize_due()) break;
-          } else if (export_ && tokens >= std::min<double>(burst, static_cast<double>(mat_q_.front().n))) {
+          } else if (export_ && !want_compact &&
+                     tokens >= std::min<double>(burst, static_cast<double>(mat_q_.front().n))) {
             if (t >= headroom_at) {
               lk.unlock();
               headroom = export_headroom(64ull << 20);
@@ -3059,15 +3088,6 @@ void ChunkStore::materializer_loop() {
             }
             if (headroom) break;
           }
-        }
-        if (store_mode_ && tokens >= burst / 2) {
-          lk.unlock();
-          const JournalStats j = journal_->stats();
-          compact_now = (j.grow_blocked || (j.used_bytes && j.used_bytes - j.live_bytes > j.used_bytes / 4)) &&
-                        journal_->compaction_candidate(compact_live_) != nullptr;
-          lk.lock();
-          if (compact_now && !mat_paused_ && !mat_stop_) break;
-          compact_now = false;
         }
         if (!store_mode_ && mat_q_.empty()) {
           lk.unlock();
@@ -3098,7 +3118,10 @@ void ChunkStore::materializer_loop() {
     }
     if (compact_now) {
       SegRef seg = journal_->compaction_candidate(compact_live_);
-      if (seg) tokens -= static_cast<double>(relocate_segment(seg, static_cast<uint64_t>(std::max(tokens, 1.0))));
+      // urgent (the journal cannot grow): one whole segment's live records whatever the tokens
+      const double budget = compact_urgent ? static_cast<double>(journal_->seg_bytes()) : std::max(tokens, 1.0);
+      if (seg) tokens -= static_cast<double>(relocate_segment(seg, static_cast<uint64_t>(budget)));
+      tokens = std::max(tokens, -burst);  // an urgent pass's debt is bounded
       continue;
     }
     if (batch.empty()) continue;

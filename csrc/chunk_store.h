@@ -325,6 +325,7 @@ class ChunkStore {
   void lru_remove_locked(Block& b);
   Lane* acquire_lane();
   uint64_t lane_waits_ = 0, lane_wait_ns_ = 0;  // under lane_mu_
+  bool journal_gate_ = false;  // journal appends + commits take a DiskGate slot (DFS_JOURNAL_GATE)
   void release_lane(Lane* l);
   void ensure_hscratch(Lane* l, uint64_t bytes);
   // Device pass: CRC (and meta write or verify) over [slice range] of a resident block.

@@ -204,6 +204,7 @@ class BlockJournal {
   // The oldest in-use segment, when it is sealed, complete and at most `max_live` of its
   // capacity is still live (compaction copies its live records forward); else nullptr.
   SegRef compaction_candidate(double max_live);
+  uint64_t seg_bytes() const { return cfg_.seg_bytes; }
   // Used segments (holding live or unretired records) over the capacity, 0..1 (round-4 mode).
   double pressure();
   uint64_t last_append_ns();

@@ -107,8 +107,16 @@ for step in "$@"; do
       run p8_n4b 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
       DFS_JOURNAL_PARTS=16 run p16_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 && \
       run p8_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 || exit 1 ;;
+    gateab)   # journal appends under the node-wide disk gate (12 / 24 slots) at 4 ranks, and N=1
+      run g0_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_GATE=1 run g12_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_GATE=1 DFS_DISK_INFLIGHT=24 run g24_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_GATE=1 DFS_DISK_INFLIGHT=6 run g6_n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 --remote-steps 0 && \
+      DFS_JOURNAL_GATE=1 run g12_n1 600 python bench.py --steps 20 --warmup 5 --remote-steps 0 || exit 1 ;;
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
+      run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
+    config5)
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
     secure)
       run config5_secure 600 python bench_configs.py config5 --gpu 0 --secure || exit 1 ;;

@@ -163,6 +163,37 @@ def test_exporter_runs_at_its_rate_without_a_pause(native, tmp_path, monkeypatch
     assert exported <= (40e6 * 2.0 + (64 << 20)), st  # bucket: rate x time + one burst
 
 
+def test_overwrites_reclaim_the_journal_while_the_exporter_runs(native, tmp_path, monkeypatch):
+    """Sustained overwrites of a few keys with the exporter busy and the journal capped at
+    6 segments: the dead records of overwritten blocks, and the records of blocks already
+    exported, are reclaimed while the writers keep writing (exports and compaction share the
+    token bucket, compaction first), so no writer ever finds the journal full."""
+    import time
+
+    for k, v in SMALL.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("DFS_JOURNAL_EXPORT", "store")
+    monkeypatch.setenv("DFS_EXPORT_HEADROOM_MB", "1")
+    monkeypatch.setenv("DFS_EXPORT_MBPS", "40")
+    monkeypatch.setenv("DFS_JOURNAL_SEGS", "6")  # 6 x 8 MiB: no growth past 48 MiB
+    monkeypatch.setenv("DFS_JOURNAL_FULL_TIMEOUT_S", "10")
+    s = open_store(native, tmp_path)
+    keep = os.urandom(100_000)
+    assert s.write("keep", keep, zlib.crc32(keep))[0]
+    t0 = time.time()
+    n = 0
+    while time.time() - t0 < 2.0:  # ~4x the journal's capacity, well above the export rate
+        v = os.urandom(256 << 10)
+        ok, _crc, err = s.write(f"k{n % 16}", v, zlib.crc32(v))[:3]
+        assert ok, (n, err, s.stats())
+        n += 1
+    st = s.stats()
+    assert n * (256 << 10) > 2 * 6 * (8 << 20), (n, st)  # the journal wrapped at least twice
+    assert st["journal_full_waits"] == 0, st
+    assert st["materialized_blocks"] > 0, st  # the exporter kept running beside compaction
+    assert s.read("keep", 0, 0)[2] == keep
+
+
 def test_supersede_marker_keeps_a_per_file_rewrite(native, tmp_path, never):
     """A rewrite too large for a segment part goes to its own files; the committed supersede
     marker stops replay from bringing back the older journal version."""
