@@ -395,7 +395,10 @@ def native_load_phase(url: str, a, mpu_bytes: int, creds: dict | None = None, mp
               ("rename", ["--op", "rename", "--keys", str(n), "--size", str(a.size), "--prefix", "nat"]),
               ("chunked_put", ["--op", "chunked", "--keys", str(n), "--size", str(a.size), "--prefix", "natc"]),
               ("multipart_upload", ["--op", "mpu", "--size", str(a.mpu_object_mb << 20), "--parts", str(a.mpu_parts),
-                                    "--prefix", "natmpu", "--keys", "1"]),
+                                    # 4 objects per thread, replaced in turn: a 10 s window at
+                                    # 5 GB/s would otherwise keep ~50 GB of unique objects on a
+                                    # 79 GB volume (r5w: the journal filled, uploads timed out)
+                                    "--prefix", "natmpu", "--keys", "4"]),
               ("multipart_get", ["--op", "get", "--size", str(mpu_bytes), "--key", mpu_key, "--keys", "1"]))
     from bench import cgroup_cpu, cgroup_cpu_delta
 

@@ -395,9 +395,12 @@ int main(int argc, char** argv) {
           st = c.send_all(req.data(), req.size()) ? c.response(&body) : -1;
           if (st == 200 && body.find("<ListBucketResult") == std::string::npos) st = -3;
         } else if (o.op == "mpu") {
-          // one multipart object per iteration: initiate, P parts, complete
+          // one multipart object per iteration: initiate, P parts, complete; each thread cycles
+          // over --keys objects (a completion replaces the older object and frees its parts), so
+          // a long window's live data stays bounded by threads x keys x object size
           char mkey[96];
-          std::snprintf(mkey, sizeof mkey, "%s_mpu_%d_%llu", o.prefix.c_str(), t, static_cast<unsigned long long>(i));
+          const uint64_t mk = o.keys > 0 ? i % o.keys : i;
+          std::snprintf(mkey, sizeof mkey, "%s_mpu_%d_%llu", o.prefix.c_str(), t, static_cast<unsigned long long>(mk));
           const std::string mpath = "/" + o.bucket + "/" + mkey;
           std::string req = "POST " + mpath + "?uploads= HTTP/1.1\r\n" + signer.headers("POST", mpath, "uploads=", 0, o.sse) + "\r\n";
           st = c.send_all(req.data(), req.size()) ? c.response(&body) : -1;
