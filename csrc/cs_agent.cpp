@@ -236,14 +236,38 @@ void CsAgent::dispatch(const pb::ChunkServerCommand& c) {
   constexpr int kReplicate = T::REPLICATE, kDelete = T::DELETE, kReconstruct = T::RECONSTRUCT_EC_SHARD,
                 kMoveToCold = T::MOVE_TO_COLD, kEncodeEc = T::ENCODE_EC;
   const int type = c.type;
+  if (type == kDelete) {
+    // queued, and removed by a bounded set of drain jobs: concurrent removes still share
+    // the journal's group-committed tombstone flushes
+    std::lock_guard<std::mutex> g(mu_);
+    del_q_.push_back(c.block_id);
+    if (del_workers_ < kDeleteWorkers) {
+      del_workers_++;
+      jobs_.submit([this] {
+        RequestScope rs(rid());
+        for (;;) {
+          std::string id;
+          {
+            std::lock_guard<std::mutex> g2(mu_);
+            if (del_q_.empty()) {
+              del_workers_--;
+              return;
+            }
+            id = std::move(del_q_.front());
+            del_q_.pop_front();
+          }
+          store_->remove(id);
+          std::lock_guard<std::mutex> g2(mu_);
+          st_.deletes++;
+        }
+      });
+    }
+    return;
+  }
   jobs_.submit([this, c, type] {
     RequestScope rs(rid());
     if (type == kReplicate) {
       replicate_to(c.block_id, c.target_chunk_server_address);
-    } else if (type == kDelete) {
-      store_->remove(c.block_id);
-      std::lock_guard<std::mutex> g(mu_);
-      st_.deletes++;
     } else if (type == kMoveToCold) {
       store_->move_to_cold(c.block_id);
       std::lock_guard<std::mutex> g(mu_);

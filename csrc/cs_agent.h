@@ -27,6 +27,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <memory>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -119,6 +120,12 @@ class CsAgent {
   std::vector<std::string> masters_;  // from the shard map (or cfg_.masters)
   std::vector<std::string> bad_, new_, enc_, fail_, rebuilt_;
   std::vector<std::string> recovering_;  // block ids with a recovery queued or running
+  // the masters' DELETE commands, drained by at most kDeleteWorkers jobs (a heartbeat can
+  // carry thousands after an overwrite-heavy burst; one job each grew the pool to as many
+  // threads)
+  std::deque<std::string> del_q_;
+  int del_workers_ = 0;
+  static constexpr int kDeleteWorkers = 8;
   CsAgentStats st_;
   std::thread hb_, scrub_;
   IoPool jobs_{8, 30000, "cs-jobs"};  // last: destroyed first, after its jobs finished
