@@ -247,6 +247,7 @@ void MasterCore::put(const std::string& path, pb::FileMetadata m) {
     }
   for (auto& b : m.blocks) block_index_[b.block_id] = path;
   files_[path] = std::move(m);
+  ordered_.insert(path);
 }
 
 bool MasterCore::del(const std::string& path, pb::FileMetadata* out) {
@@ -260,6 +261,7 @@ bool MasterCore::del(const std::string& path, pb::FileMetadata* out) {
   }
   if (out) *out = std::move(it->second);
   files_.erase(it);
+  ordered_.erase(path);
   return true;
 }
 
@@ -625,6 +627,7 @@ void MasterCore::restore(const std::string& text) {
   const Json& s = st ? *st : j;  // a legacy raw MasterState is accepted too
   std::lock_guard<std::mutex> g(mu_);
   files_.clear();
+  ordered_.clear();
   block_index_.clear();
   for (auto& kv : s["files"].fields()) put(kv.first, file_from(kv.second));
   tx_records_.clear();
@@ -739,20 +742,16 @@ size_t MasterCore::file_count() const {
 std::vector<std::string> MasterCore::paths(const std::string& prefix, bool visible_only) const {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<std::string> out;
-  for (auto& kv : files_) {
-    if (kv.first.compare(0, prefix.size(), prefix) != 0) continue;
-    if (visible_only && under_construction_.count(kv.first)) continue;
-    out.push_back(kv.first);
-  }
-  std::sort(out.begin(), out.end());
+  for_prefix(prefix, [&](const std::string& p) {
+    if (!visible_only || !under_construction_.count(p)) out.push_back(p);
+  });
   return out;
 }
 
 std::vector<std::string> MasterCore::files_pb(const std::string& prefix) const {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<std::string> out;
-  for (auto& kv : files_)
-    if (kv.first.compare(0, prefix.size(), prefix) == 0) out.push_back(kv.second.str());
+  for_prefix(prefix, [&](const std::string& p) { out.push_back(files_.at(p).str()); });
   return out;
 }
 
@@ -1368,11 +1367,9 @@ int MasterCore::list_files(const std::string& raw, std::string* out) {
     resp.files = paths(r.path, true);
   } else {  // one consistent pass: paths and their metadata under the same lock
     std::lock_guard<std::mutex> g(mu_);
-    for (auto& kv : files_) {
-      if (kv.first.compare(0, r.path.size(), r.path) != 0 || under_construction_.count(kv.first)) continue;
-      resp.files.push_back(kv.first);
-    }
-    std::sort(resp.files.begin(), resp.files.end());
+    for_prefix(r.path, [&](const std::string& p) {
+      if (!under_construction_.count(p)) resp.files.push_back(p);
+    });
     resp.metadata.reserve(resp.files.size());
     for (auto& p : resp.files) resp.metadata.push_back(files_.at(p));
   }

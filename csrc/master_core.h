@@ -241,6 +241,15 @@ class MasterCore : public raft::StateMachine {
   std::condition_variable applied_cv_;
   // replicated
   std::unordered_map<std::string, pb::FileMetadata> files_;
+  // the same paths in order (kept by put / del / restore): prefix listings walk
+  // [lower_bound(prefix), first path without it) instead of scanning every file under mu_
+  std::set<std::string> ordered_;
+  template <class F>
+  void for_prefix(const std::string& prefix, F&& f) const {
+    for (auto it = ordered_.lower_bound(prefix); it != ordered_.end() && it->compare(0, prefix.size(), prefix) == 0;
+         ++it)
+      f(*it);
+  }
   std::unordered_map<std::string, std::string> block_index_;
   // path -> writer generation (the create entry's ts) while a classic create is open, and the
   // last progress (create / AllocateBlock) of that writer: the lease runs from the latter.
