@@ -76,6 +76,11 @@ def parse():
                         "(no shared memory, no local sockets: every master and chunkserver RPC over gRPC/TCP, "
                         "as the reference's dfs_cli does); reported under remote_client (0 = skip; "
                         "default 2 on one GPU, 0 with several: their replicas would only add volume usage)")
+    p.add_argument("--roofline-records", type=int, default=None,
+                   help="after the timed region, every rank at once appends this many 1 MiB journal records "
+                        "per writer thread to a fresh journal on its volume (io_bench --roofline): the "
+                        "volume's rate each rank gets, recorded as volume.roofline_mb_s (0 = skip; "
+                        "default 30, 4 with --cpu)")
     p.add_argument("--profile-dir", default=None,
                    help="run each ChunkServer under rocprofv3 --kernel-trace --stats, output here")
     return p.parse_args()
@@ -391,19 +396,25 @@ def main():
             # steady state); bounded, and reported
             import urllib.request
 
-            t_fill = time.perf_counter()
-            fill_deadline = time.time() + 180
-            unready = None
-            while time.time() < fill_deadline:
-                try:
-                    st = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
-                except OSError:
-                    st = {}
-                unready = st.get("journal_parts_unready", 0) if st.get("journal") else 0
-                if unready == 0:
-                    break
-                time.sleep(0.2)
-            journal_settle_s = round(time.perf_counter() - t_fill, 2)
+            def settle_journal(limit_s: float):
+                t_fill = time.perf_counter()
+                fill_deadline = time.time() + limit_s
+                unready = None
+                while time.time() < fill_deadline:
+                    try:
+                        st = json.loads(urllib.request.urlopen(f"http://127.0.0.1:{chttp}/stats", timeout=5).read())
+                    except OSError:
+                        st = {}
+                    # every spare this run's replicas need created and written out once (the journal
+                    # then neither creates nor fills a segment while the timed writes run)
+                    unready = (st.get("journal_parts_unready", 0) + st.get("journal_spares_missing", 0) * 8
+                               if st.get("journal") else 0)
+                    if unready == 0:
+                        break
+                    time.sleep(0.05)
+                return round(time.perf_counter() - t_fill, 2), unready
+
+            journal_settle_s, unready = settle_journal(180)
             note(f"journal settled in {journal_settle_s} s ({unready} parts still unready)")
             barrier()
 
@@ -424,6 +435,12 @@ def main():
             for w in range(a.warmup):
                 ws, rs = step(f"w{w}")
                 note(f"warm-up step {w}: write p50 {1e3 * ws._pct(50):.2f} ms, read p50 {1e3 * rs._pct(50):.2f} ms")
+            # the warm-up's pauses let the journal top its spares up; let those be written out too,
+            # so the timed region starts (and, with two spares to spare, ends) with none unready
+            resettle_s, unready = settle_journal(60) if os.environ.get("DFS_BENCH_RESETTLE", "1") != "0" else (0.0, 0)
+            journal_settle_s = round(journal_settle_s + resettle_s, 2)
+            if resettle_s > 0.05 or unready:
+                note(f"journal re-settled after the warm-up in {resettle_s} s ({unready} parts still unready)")
             # the timed region is bracketed by barrier + device synchronize on both sides; the
             # synchronize runs in the process that owns the GPU and queued all of its work (the
             # chunkserver's /sync: hipDeviceSynchronize), not in this client process
@@ -480,15 +497,22 @@ def main():
                 except Exception:  # noqa: BLE001
                     return {}
 
-            thr0 = cs_stats().get("thread_cpu_ms", {})  # per-thread CPU of the chunkserver, before
+            st0 = cs_stats()
+            thr0 = st0.get("thread_cpu_ms", {})  # per-thread CPU of the chunkserver, before
+            # journal readiness at the start of the timed region (reported with its end)
+            jr0 = {k: st0.get("journal_" + k, 0) for k in JOURNAL_READY_KEYS}
             client.phase_times = {}
             cpu0 = cpu_snapshot()
             cg0 = cgroup_cpu()
             t0 = time.perf_counter()
             wl, rl, wbytes, rbytes = [], [], 0, 0
             wt = rt = 0.0
+            slow: list = []  # the write tail: (ms, step, op, phase ms)
             for s in range(a.steps):
                 ws, rs = step(f"s{s}")
+                ph = getattr(ws, "op_phases", None) or []
+                slow += [(x, s, i, ph[i] if i < len(ph) else None) for i, x in enumerate(ws.latencies)]
+                slow = sorted(slow, key=lambda e: -e[0])[:20]
                 wl += ws.latencies
                 rl += rs.latencies
                 wbytes += ws.count * ws.avg_size
@@ -508,6 +532,7 @@ def main():
             job_cpu = cgroup_cpu_delta(cg0, cgroup_cpu(), elapsed)
             # counters of the timed phase only (the stress / remote phases below add their own hops)
             stats = cs_stats()
+            jr1 = {k: stats.get("journal_" + k, 0) for k in JOURNAL_READY_KEYS}
             thr1 = stats.get("thread_cpu_ms", {})
             # cores each named chunkserver thread group used over the timed region (HIP runtime
             # threads keep the executable's name)
@@ -554,11 +579,28 @@ def main():
                           "native_ops": rc.remote_ops, "ops": 2 * a.remote_steps * a.count,
                           "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3) for k, v in rc.phase_times.items() if v}}
                 rc.close()
-            allr = gather({"elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
+            roof = None
+            nroof = a.roofline_records if a.roofline_records is not None else (4 if a.cpu else 30)
+            if nroof > 0 and a.durability == "nvme-sync":
+                # the volume's journal write rate with every rank appending at once (outside the
+                # timed region, after it): the bound the nvme-sync write of this N is read against
+                barrier()
+                try:
+                    r = subprocess.run([str(ROOT / "build" / "native" / "io_bench"), "--roofline", "--dir",
+                                        str(rank_dir / "roofline"), "--threads", str(a.concurrency),
+                                        "--per", str(nroof)], capture_output=True, text=True, timeout=180)
+                    roof = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {"error": r.stderr[-300:]}
+                except (OSError, ValueError, IndexError, subprocess.TimeoutExpired) as e:
+                    roof = {"error": str(e)[:300]}
+            slow_w = [{"ms": round(1e3 * x, 3), "step": st, "op": i,
+                       **({k: round(1e3 * v, 3) for k, v in zip(("crc", "create", "write", "md5_wait", "complete"), ph)}
+                          if ph else {})} for x, st, i, ph in slow]
+            allr = gather({"slow_w": slow_w, "roof": roof, "elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
                            "rbytes": rbytes, "wt": wt,
                            "rt": rt, "cs": stats, "stress": stress, "remote": remote, "vol": vol,
                            "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
-                           "cpu": host_cpu, "job_cpu": job_cpu, "thread_cores": thread_cores, "settle": journal_settle_s, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
+                           "cpu": host_cpu, "job_cpu": job_cpu, "thread_cores": thread_cores, "settle": journal_settle_s,
+                           "jready": {"start": jr0, "end": jr1}, "phases": {k: round(1e3 * sorted(v)[len(v) // 2], 3)
                                                        for k, v in (client.phase_times or {}).items() if v}})
             if rank == 0:
                 tmax = max(r["elapsed"] for r in allr)
@@ -627,15 +669,33 @@ def main():
                         ("relocated_blocks", "relocated_blocks"), ("supersedes", "journal_supersedes"),
                         ("export_deferred_headroom", "export_deferred_headroom"))} | {
                         "mode": ",".join(sorted({r["cs"].get("journal_mode", "?") for r in allr})),
-                        "settle_s_before_warmup": max(r["settle"] for r in allr)} if any(r["cs"].get("journal") for r in allr) else None,
+                        "settle_s_before_warmup": max(r["settle"] for r in allr),
+                        # readiness at both ends of the timed region, summed over ranks: parts a
+                        # writer could be handed unwritten, spares owed (topped up when idle),
+                        # top-ups deferred so far, segments created so far
+                        "timed_region": {end: {k: sum(r["jready"][end][k] for r in allr) for k in JOURNAL_READY_KEYS}
+                                         for end in ("start", "end")}} if any(r["cs"].get("journal") for r in allr) else None,
                     # where each rank's replicas live and how much of the volume they take
-                    "volume": {"per_rank": [r["vol"] for r in allr], "free_bytes_after": _free_bytes(base_p)},
+                    "volume": {"per_rank": [r["vol"] for r in allr], "free_bytes_after": _free_bytes(base_p),
+                               # every rank appending 1 MiB journal records at once after the timed
+                               # region (io_bench --roofline, conc threads each): per-rank MB/s, sum
+                               "roofline_mb_s": [(r["roof"] or {}).get("roofline_mb_s") for r in allr],
+                               "roofline_total_mb_s": round(sum((r["roof"] or {}).get("roofline_mb_s") or 0
+                                                                for r in allr), 1),
+                               "roofline_p50_ms": [(r["roof"] or {}).get("p50_ms") for r in allr]},
                     "host_cpu_util_rank0": allr[0]["cpu"],
                     # the whole job's CPU over the timed region, from the cgroup every rank shares
                     # (cores used, the quota, and time the quota throttled it); null without cgroup
                     "host_cpu_job": allr[0]["job_cpu"],
+                    # host cores the whole job kept busy per GB/s of client writes (timed region,
+                    # reads included): what an 8-rank node's CPU quota is read against
+                    "cores_per_gb_written": (round(allr[0]["job_cpu"]["cores_used"] / (
+                        sum(r["wbytes"] for r in allr) / 1e9 / max(r["wt"] for r in allr)), 3)
+                        if allr[0]["job_cpu"] and allr[0]["job_cpu"].get("cores_used") else None),
                     "cs_thread_cores_rank0": dict(sorted(allr[0]["thread_cores"].items(), key=lambda kv: -kv[1])),
                     "client_phase_p50_ms_rank0": allr[0]["phases"],
+                    # rank 0's 20 slowest timed writes: step, op index and where the time went
+                    "write_tail_rank0": allr[0]["slow_w"],
                     **repl_phases(allr),
                 }
                 if a.remote_steps > 0:
@@ -843,6 +903,7 @@ def _bytes_needed(a, n: int) -> int:
 
 
 JOURNAL_SEG_BYTES = 256 << 20
+JOURNAL_READY_KEYS = ("parts_unready", "spares_missing", "grow_deferred", "segs", "segs_in_use", "full_waits")
 # a 256 MiB segment = 8 parts of 32 MiB; a 1 MiB block's record is 1 MiB + 12 KiB (header and
 # .meta page), 31 to a part: 96.8 % of a segment is block bytes
 JOURNAL_SEG_DATA = int(JOURNAL_SEG_BYTES * 0.96)
@@ -872,7 +933,9 @@ def _journal_segments(parent: Path, need: int, n: int) -> int:
         return 0
     per_cs = need // max(1, n)
     if _journal_store_mode():
-        want = -(-per_cs // JOURNAL_SEG_DATA) + 1
+        # + 2: the journal tops its spares up only in idle windows unless fewer than 2 are
+        # free (DFS_JOURNAL_SPARES_LOW), so with two to spare no segment is created mid-run
+        want = -(-per_cs // JOURNAL_SEG_DATA) + 2
         budget = (free - (4 << 30)) // max(1, n) // JOURNAL_SEG_BYTES
         return int(max(4, min(want, budget)))
     budget = (free - int(need * 1.15) - (2 << 30)) // max(1, n)

@@ -136,7 +136,8 @@ def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[P
 # Host-only runtime sources the native unit tests need (no HIP): they also build with the
 # host compiler under ASan/UBSan and TSan (SURVEY §5.2 — the reference has no sanitizer runs).
 SANITIZE_SOURCES = ["json.cpp", "json_dump.cpp", "shard_map.cpp", "raft.cpp", "wal.cpp", "crc32.cpp", "gf256.cpp",
-                    "disk_gate.cpp", "extent_alloc.cpp", "master_core.cpp", "http_lite.cpp"]
+                    "disk_gate.cpp", "extent_alloc.cpp", "master_core.cpp", "http_lite.cpp",
+                    "journal.cpp"]
 SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
               "tsan": ["-fsanitize=thread"]}
 

@@ -33,6 +33,7 @@
 #include "disk_gate.h"
 #include "crc32.h"
 #include "gf256.h"
+#include "journal.h"
 
 using namespace dfs;
 using Clock = std::chrono::steady_clock;
@@ -376,7 +377,68 @@ static void pcie_roofline(int device, int threads, int per, size_t n) {
               static_cast<unsigned long long>(fused_w), static_cast<unsigned long long>(fused_r));
 }
 
+// --roofline: what the volume gives a chunkserver's journal right now — T writers appending
+// 1 MiB block records (header + .meta image + data) to a BlockJournal like the store's
+// (8 parts, 256 MiB segments, written out once before the timed appends), each record
+// group-committed before the next. bench.py runs it on every rank at once after its timed
+// region, so each rank's share of the node's volume is recorded next to its throughput.
+static void roofline(const std::string& dir, int threads, int per) {
+  std::filesystem::remove_all(dir);
+  const uint64_t n = 1 << 20, S = num_slices(n);
+  double secs_total = 0, mbps = 0;
+  std::vector<double> lat;
+  {
+    JournalConfig c;
+    c.dir = dir;
+    c.max_segs = static_cast<int>((uint64_t(threads) * per * (n + 12288)) / (c.seg_bytes * 9 / 10)) + 2;
+    BlockJournal j(c);
+    (void)j.recover();
+    for (int i = 0; i < 6000 && j.stats().parts_unready; ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    std::vector<uint8_t> meta(4 * S, 0);
+    std::mutex mu;
+    auto t0 = Clock::now();
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t)
+      ts.emplace_back([&, t] {
+        std::vector<uint8_t> buf(n, static_cast<uint8_t>(t + 1));
+        std::vector<double> mine;
+        for (int i = 0; i < per; ++i) {
+          auto a = Clock::now();
+          JournalRec r;
+          std::string err;
+          if (!j.reserve(n, S, &r, &err) || !j.write(r, 0, buf.data(), n) ||
+              !j.finish(&r, "roof-" + std::to_string(t) + "-" + std::to_string(i), n, 0, meta.data(), S) ||
+              !j.commit(r))
+            break;
+          mine.push_back(secs(a, Clock::now()));
+        }
+        std::lock_guard<std::mutex> g(mu);
+        lat.insert(lat.end(), mine.begin(), mine.end());
+      });
+    for (auto& t : ts) t.join();
+    secs_total = secs(t0, Clock::now());
+    mbps = lat.size() * (n / 1048576.0) / std::max(1e-9, secs_total);
+  }
+  std::filesystem::remove_all(dir);
+  std::sort(lat.begin(), lat.end());
+  auto pct = [&](double p) { return lat.empty() ? 0.0 : 1e3 * lat[std::min(lat.size() - 1, size_t(lat.size() * p))]; };
+  std::printf("{\"roofline_mb_s\": %.1f, \"threads\": %d, \"records\": %zu, \"seconds\": %.3f, \"p50_ms\": %.3f, "
+              "\"p99_ms\": %.3f}\n", mbps, threads, lat.size(), secs_total, pct(0.5), pct(0.99));
+}
+
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--roofline") {
+      std::string dir = "/tmp/io_bench_roofline";
+      int threads = 10, per = 30;
+      for (int j = 1; j + 1 < argc; ++j) {
+        if (std::string(argv[j]) == "--dir") dir = argv[j + 1];
+        if (std::string(argv[j]) == "--threads") threads = std::atoi(argv[j + 1]);
+        if (std::string(argv[j]) == "--per") per = std::atoi(argv[j + 1]);
+      }
+      roofline(dir, std::max(1, threads), std::max(1, per));
+      return 0;
+    }
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--multi-journal") {
       std::string dir = "/tmp/io_bench_mj";

@@ -32,6 +32,7 @@
 #include "extent_alloc.h"
 #include "gf256.h"
 #include "http_lite.h"
+#include "journal.h"
 #include "json.h"
 #include "master_core.h"
 #include "raft.h"
@@ -788,6 +789,232 @@ TEST(http_lite_server_and_client_round_trip) {
   srv.stop();
   std::string e2;
   CHECK(http_request("GET", base + "/health", "", "", 500, &reply, &e2) == 0 && !e2.empty());
+}
+
+// ------------------------------------------------------------------------ block journal
+// (journal.h): the store of record's append / group-commit / retire protocol, replay after
+// a crash (the object is dropped without retire_all, as a killed process would leave it).
+namespace jt {
+
+std::vector<uint8_t> meta_be_of(const std::vector<uint8_t>& d) {
+  std::vector<uint32_t> c(num_slices(d.size()));
+  crc32_slices(d.data(), d.size(), c.data());
+  std::vector<uint8_t> be(4 * c.size());
+  for (size_t i = 0; i < c.size(); ++i) {
+    be[4 * i] = c[i] >> 24;
+    be[4 * i + 1] = (c[i] >> 16) & 0xff;
+    be[4 * i + 2] = (c[i] >> 8) & 0xff;
+    be[4 * i + 3] = c[i] & 0xff;
+  }
+  return be;
+}
+
+// reserve -> write (in two pieces, out of order) -> finish -> commit
+bool append(BlockJournal& j, const std::string& id, const std::vector<uint8_t>& d, JournalRec* r) {
+  std::string err;
+  const uint64_t ns = num_slices(d.size());
+  if (!j.reserve(d.size(), ns, r, &err)) return false;
+  const uint64_t half = d.size() / 2;
+  if (!j.write(*r, half, d.data() + half, d.size() - half) || !j.write(*r, 0, d.data(), half)) return false;
+  auto be = meta_be_of(d);
+  if (!j.finish(r, id, d.size(), crc32(d.data(), d.size()), be.data(), ns)) return false;
+  return j.commit(*r);
+}
+
+JournalConfig small(const std::string& dir, bool grow) {
+  JournalConfig c;
+  c.dir = dir;
+  c.seg_bytes = 4 << 20;  // 4 parts of 1 MiB
+  c.parts = 4;
+  c.grow = grow;
+  c.max_segs = grow ? 0 : 3;
+  c.spares = 2;
+  c.reserve_bytes = 0;
+  c.idle_fill_ms = 5;
+  c.full_timeout_s = 2;
+  return c;
+}
+
+}  // namespace jt
+
+// 8 writers append and commit concurrently while records are released (exported), segments
+// retire, compaction-style relocations keep their LSN and tombstones are committed; a thread
+// marks sealed segments meanwhile. After the "crash", replay returns every acknowledged,
+// unreleased record with its bytes intact, newest version last, and no deleted id survives.
+TEST(journal_concurrent_commit_retire_and_crash_replay) {
+  const std::string d = tmpdir("journal_cc");
+  std::mutex mu;
+  std::map<std::string, std::pair<uint32_t, uint64_t>> live;  // id -> (crc, size) of the acked live version
+  std::set<std::string> deleted;
+  {
+    BlockJournal j(jt::small(d + "/j", true));
+    CHECK(j.recover().empty());
+    std::atomic<bool> stop{false};
+    std::thread marker_thread([&] {
+      while (!stop) {
+        j.mark_sealed_now();
+        j.retire_ready();
+        std::this_thread::sleep_for(std::chrono::milliseconds(3));
+      }
+    });
+    std::vector<std::thread> ts;
+    std::atomic<int> failures{0};
+    for (int t = 0; t < 8; ++t)
+      ts.emplace_back([&, t] {
+        std::mt19937 rng(1234 + t);
+        std::vector<std::pair<std::string, JournalRec>> mine;
+        for (int i = 0; i < 40; ++i) {
+          std::vector<uint8_t> data(1 + rng() % (200 << 10));
+          for (auto& b : data) b = static_cast<uint8_t>(rng());
+          const std::string id = "blk-" + std::to_string(t) + "-" + std::to_string(i % 25);  // some rewritten
+          JournalRec r;
+          if (!jt::append(j, id, data, &r)) {
+            failures++;
+            continue;
+          }
+          {
+            std::lock_guard<std::mutex> g(mu);
+            live[id] = {crc32(data.data(), data.size()), data.size()};
+            deleted.erase(id);
+          }
+          for (auto it = mine.begin(); it != mine.end(); ++it)
+            if (it->first == id) {  // the older version is superseded
+              j.release(it->second);
+              mine.erase(it);
+              break;
+            }
+          mine.emplace_back(id, r);
+          if (i % 7 == 3 && !mine.empty()) {  // delete the oldest: tombstone first, then release
+            auto victim = mine.front();
+            std::string err;
+            if (!j.marker(kJrTomb, victim.first, &err)) {
+              failures++;
+              continue;
+            }
+            {
+              std::lock_guard<std::mutex> g(mu);
+              live.erase(victim.first);
+              deleted.insert(victim.first);
+            }
+            j.release(victim.second);
+            mine.erase(mine.begin());
+          }
+        }
+      });
+    for (auto& t : ts) t.join();
+    stop = true;
+    marker_thread.join();
+    CHECK(failures == 0);
+    JournalStats st = j.stats();
+    CHECK(st.records == 320 && st.tombstones > 0 && st.sync_rounds > 0);
+    CHECK(st.segs_retired > 0);  // releases let old segments retire while writers ran
+  }  // dropped without retire_all: what a killed chunkserver leaves
+  BlockJournal j2(jt::small(d + "/j", true));
+  auto recs = j2.recover();
+  std::map<std::string, const ReplayRecord*> last;  // replay is in LSN order: the last one wins
+  for (auto& r : recs) last[r.id] = &r;
+  for (auto& kv : live) {
+    auto it = last.find(kv.first);
+    CHECK(it != last.end());
+    const ReplayRecord& r = *it->second;
+    CHECK(r.type == kJrBlock && r.crc == kv.second.first && r.n == kv.second.second);
+    std::vector<uint8_t> back(r.n);
+    CHECK(::pread(r.fd(), back.data(), r.n, static_cast<off_t>(r.data_off())) == static_cast<ssize_t>(r.n));
+    CHECK(crc32(back.data(), back.size()) == r.crc);
+    CHECK(jt::meta_be_of(back) == r.meta_be);
+  }
+  for (auto& id : deleted) {
+    auto it = last.find(id);
+    CHECK(it == last.end() || it->second->type == kJrTomb);
+  }
+  std::filesystem::remove_all(d);
+}
+
+// a segment is marked sealed (replay trusts its records without re-reading the
+// data) only after its records are flushed: a finished record whose commit has not run yet is
+// flushed by the marking itself, before the sealed header.
+TEST(journal_marks_a_segment_only_after_flushing_pending_records) {
+  const std::string d = tmpdir("journal_mark");
+  BlockJournal j(jt::small(d + "/j", true));
+  CHECK(j.recover().empty());
+  std::vector<uint8_t> data(100 << 10, 0x5a);
+  JournalRec r;
+  std::string err;
+  const uint64_t ns = num_slices(data.size());
+  CHECK(j.reserve(data.size(), ns, &r, &err));
+  CHECK(j.write(r, 0, data.data(), data.size()));
+  auto be = jt::meta_be_of(data);
+  CHECK(j.finish(&r, "pending", data.size(), crc32(data.data(), data.size()), be.data(), ns));
+  // complete but not committed: marking must flush the part before writing the header
+  j.mark_sealed_now();
+  JournalStats st = j.stats();
+  CHECK(st.segs_marked == 1 && st.mark_preflushes >= 1);
+  CHECK(j.commit(r));  // already durable: no new flush round needed
+  CHECK(j.stats().sync_rounds == st.sync_rounds);
+  std::filesystem::remove_all(d);
+}
+
+// a full journal (ring of 3 segments, every record live) still takes tombstones —
+// they go into the markers' reserve at the tail of each part — while a block append times out.
+TEST(journal_full_still_commits_tombstones) {
+  const std::string d = tmpdir("journal_full");
+  BlockJournal j(jt::small(d + "/j", false));
+  CHECK(j.recover().empty());
+  std::vector<uint8_t> data(240 << 10, 0x11);
+  std::vector<JournalRec> held;
+  int n = 0;
+  for (;;) {
+    JournalRec r;
+    std::string err;
+    const uint64_t ns = num_slices(data.size());
+    if (!j.reserve(data.size(), ns, &r, &err)) {
+      CHECK(err.find("journal full") != std::string::npos || err.find("segment") != std::string::npos);
+      break;
+    }
+    CHECK(j.write(r, 0, data.data(), data.size()));
+    auto be = jt::meta_be_of(data);
+    CHECK(j.finish(&r, "b" + std::to_string(n++), data.size(), crc32(data.data(), data.size()), be.data(), ns));
+    CHECK(j.commit(r));
+    held.push_back(r);
+    CHECK(n < 1000);
+  }
+  CHECK(n >= 3 * 4 * 3);  // 3 segments x 4 parts x at least 3 records of 244 KiB per 1 MiB part
+  for (int i = 0; i < 8; ++i) {
+    std::string err;
+    CHECK(j.marker(kJrTomb, "b" + std::to_string(i), &err));
+  }
+  CHECK(j.stats().reserve_markers >= 8);
+  // the tombstones replay after the records they cancel
+  for (auto& r : held) j.release(r);
+  std::filesystem::remove_all(d);
+}
+
+// Grow mode keeps `spares` free segments, but while the writers are active a top-up waits for
+// their next idle window unless fewer than spares_low are free.
+TEST(journal_defers_spare_creation_while_writers_are_active) {
+  const std::string d = tmpdir("journal_grow");
+  JournalConfig c = jt::small(d + "/j", true);
+  c.spares = 4;
+  c.spares_low = 2;
+  c.idle_fill_ms = 50;
+  BlockJournal j(c);
+  CHECK(j.recover().empty());
+  CHECK(eventually([&] { auto s = j.stats(); return s.spares_missing == 0 && s.parts_unready == 0; }, 10));
+  const uint64_t segs0 = j.stats().segs_total;
+  std::vector<uint8_t> data(300 << 10, 0x22);
+  // ~1.5 segments of appends back to back: free drops 4 -> 2 (still >= spares_low)
+  auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < 18; ++i) {
+    JournalRec r;
+    CHECK(jt::append(j, "g" + std::to_string(i), data, &r));
+  }
+  const double active_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  JournalStats mid = j.stats();
+  if (active_s < 0.04) CHECK(mid.segs_total == segs0);  // nothing created while the writers ran
+  CHECK(mid.spares_missing > 0 && mid.parts_unready == 0);
+  CHECK(eventually([&] { return j.stats().spares_missing == 0; }, 10));  // topped up once idle
+  CHECK(j.stats().grow_deferred >= 1 || active_s >= 0.04);
+  std::filesystem::remove_all(d);
 }
 
 }  // namespace

@@ -71,6 +71,13 @@ bool GroupSync::sync() {
 
 namespace {
 
+// the journal's clock (steady_clock since its epoch, ns): compared with last_append_ns()
+uint64_t mono_ns() {
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+          .count());
+}
+
 inline uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
 
 std::string errno_str(const std::string& what) { return what + ": " + std::strerror(errno); }
@@ -243,6 +250,10 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     store_mode_ = emode != "idle";
     export_ = emode != "never";
     export_bps_ = env_int("DFS_EXPORT_MBPS", 256) * 1e6;
+    // while acked writes are arriving (an append in the last 50 ms) the exporter runs at this
+    // rate in batches of at most 8 MiB, so its per-file flushes and directory flush never
+    // land on the writers as a 64-file burst; at full rate again once they pause
+    export_busy_bps_ = env_int("DFS_EXPORT_BUSY_MBPS", 64) * 1e6;
     compact_live_ = env_int("DFS_COMPACT_LIVE_PCT", 50) / 100.0;
     uint64_t vol_total = 0;
     {
@@ -262,6 +273,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     if (jc.reserve_bytes == 0) jc.reserve_bytes = std::max<uint64_t>(2ull << 30, vol_total / 50);
     jc.direct = env_int("DFS_JOURNAL_DIRECT", 0) != 0;
     jc.spares = env_int("DFS_JOURNAL_SPARES", store_mode_ ? 4 : 2);
+    jc.spares_low = env_int("DFS_JOURNAL_SPARES_LOW", 2);
     jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 1) != 0;
     jc.idle_fill_ms = env_int("DFS_JOURNAL_IDLE_FILL_MS", 20);
     jc.syncers = env_int("DFS_JOURNAL_SYNCERS", 1);
@@ -2089,9 +2101,35 @@ bool ChunkStore::remove(const std::string& id) {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = index_.find(id);
     if (it == index_.end()) return false;
-    cv_.wait(lk, [&] { return it->second.pins == 0; });
-    cold = it->second.cold;
     durable = it->second.on_disk || it->second.jrec.seg != nullptr;
+    old = it->second.jrec;
+  }
+  // an unretired journal record of the block would bring it back on replay (a block that
+  // never became durable, e.g. an EC gather copy, has none): the tombstone is committed
+  // before the block leaves the index. If it cannot be (journal failed, or no room even in
+  // the markers' reserve), the block stays and the delete fails, so the master retries it
+  // instead of the block coming back at the next restart.
+  if (journal_ && durable) {
+    std::string err;
+    if (!journal_->marker(kJrTomb, id, &err)) {
+      std::fprintf(stderr, "[store] delete %s kept: tombstone not durable: %s\n", id.c_str(), err.c_str());
+      std::lock_guard<std::mutex> g(mu_);
+      ++tomb_failures_;
+      return false;
+    }
+  }
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = index_.find(id);
+    if (it == index_.end()) return true;  // a concurrent delete won
+    cv_.wait(lk, [&] {
+      it = index_.find(id);
+      return it == index_.end() || it->second.pins == 0;
+    });
+    if (it == index_.end()) return true;
+    // (a rewrite that landed while the tombstone committed took a smaller LSN only if it
+    // finished first; either way the id is gone after replay, as it is here)
+    cold = it->second.cold;
     old = it->second.jrec;
     free_extent_locked(it->second);
     lru_remove_locked(it->second);
@@ -2099,13 +2137,6 @@ bool ChunkStore::remove(const std::string& id) {
     index_.erase(it);
   }
   cv_.notify_all();
-  // an unretired journal record of the block would bring it back on replay (a block that
-  // never became durable, e.g. an EC gather copy, has none): the tombstone is committed
-  // before the delete returns
-  if (journal_ && durable) {
-    std::string err;
-    if (!journal_->marker(kJrTomb, id, &err)) std::fprintf(stderr, "[store] tombstone %s: %s\n", id.c_str(), err.c_str());
-  }
   ::unlink(data_path(id, cold).c_str());
   ::unlink(meta_path(id, cold).c_str());
   if (old.seg) journal_->release(old);
@@ -2407,6 +2438,12 @@ StoreStats ChunkStore::stats() {
     s.journal_segs_filled = j.filled;
     s.journal_fill_bytes = j.fill_bytes;
     s.journal_parts_unready = j.parts_unready;
+    s.journal_spares_missing = j.spares_missing;
+    s.journal_grow_deferred = j.grow_deferred;
+    s.journal_mark_preflushes = j.mark_preflushes;
+    s.journal_reserve_markers = j.reserve_markers;
+    s.delete_tomb_failures = tomb_failures_;
+    s.export_busy_polls = export_busy_polls_;
     s.journal_sync_ns = j.sync_ns;
     s.journal_bypassed = bypassed_.load();
     s.journal_commit_ns = j.commit_ns;
@@ -3027,7 +3064,7 @@ void ChunkStore::materializer_loop() {
     constexpr long kWhoProcess = 1, kClassIdle = 3, kClassShift = 13;
     (void)::syscall(SYS_ioprio_set, kWhoProcess, 0L, kClassIdle << kClassShift);
   }
-  const double burst = 64.0 * (1 << 20);
+  const double burst = 64.0 * (1 << 20), kBusyBurst = 8.0 * (1 << 20);
   double tokens = burst;
   auto t_prev = std::chrono::steady_clock::now();
   bool headroom = false, stop_failed = false;
@@ -3042,7 +3079,12 @@ void ChunkStore::materializer_loop() {
       std::unique_lock<std::mutex> lk(mu_);
       for (;;) {
         const auto t = std::chrono::steady_clock::now();
-        tokens = std::min(burst, tokens + export_bps_ * std::chrono::duration<double>(t - t_prev).count());
+        const uint64_t last_append = store_mode_ ? journal_->last_append_ns() : 0;
+        const bool busy = last_append && mono_ns() - last_append < 50000000ull;
+        const double cap = busy ? std::min(burst, kBusyBurst) : burst;
+        tokens = std::min(cap, tokens + (busy ? export_busy_bps_ : export_bps_) *
+                                            std::chrono::duration<double>(t - t_prev).count());
+        if (busy) ++export_busy_polls_;
         t_prev = t;
         if (mat_q_.empty() && !mat_busy_) mat_cv_.notify_all();  // materialize_all() waiters
         if (mat_stop_ && (store_mode_ || mat_q_.empty() || stop_failed)) return;

@@ -108,7 +108,10 @@ struct StoreStats {
   uint64_t journal_live_records = 0, journal_live_bytes = 0, journal_used_bytes = 0;
   uint64_t materialized_blocks = 0, materialized_bytes = 0, materialize_pending = 0, materialize_batches = 0;
   uint64_t materialize_errors = 0, journal_prepare_errors = 0, journal_segs_filled = 0, journal_fill_bytes = 0,
-           journal_parts_unready = 0;
+           journal_parts_unready = 0, journal_spares_missing = 0, journal_grow_deferred = 0,
+           journal_mark_preflushes = 0, journal_reserve_markers = 0;
+  uint64_t delete_tomb_failures = 0;  // deletes refused: tombstone not durable (block kept)
+  uint64_t export_busy_polls = 0;     // exporter wake-ups at the writers-active rate
   uint64_t journal_sync_ns = 0, journal_commit_ns = 0, journal_bypassed = 0;
   uint64_t relocated_blocks = 0, relocated_bytes = 0, compactions = 0, export_deferred_headroom = 0;
   uint64_t scrub_device_blocks = 0;  // durable (journal / file) copies verified by the K1b kernel
@@ -325,6 +328,7 @@ class ChunkStore {
   void lru_remove_locked(Block& b);
   Lane* acquire_lane();
   uint64_t lane_waits_ = 0, lane_wait_ns_ = 0;  // under lane_mu_
+  uint64_t tomb_failures_ = 0;  // deletes refused because their tombstone could not be committed (mu_)
   bool journal_gate_ = false;  // journal appends + commits take a DiskGate slot (DFS_JOURNAL_GATE)
   void release_lane(Lane* l);
   void ensure_hscratch(Lane* l, uint64_t bytes);
@@ -365,6 +369,8 @@ class ChunkStore {
   bool store_mode_ = false;
   bool export_ = true;
   double export_bps_ = 256e6;        // exporter token bucket (bytes / s)
+  double export_busy_bps_ = 64e6;    // ... while writers are active (DFS_EXPORT_BUSY_MBPS)
+  uint64_t export_busy_polls_ = 0;   // exporter wake-ups that found the writers active (mu_)
   uint64_t export_headroom_ = 0;     // export only while the volume keeps this much free
   double compact_live_ = 0.5;        // compaction: oldest segment at most this share live
   void materializer_loop();

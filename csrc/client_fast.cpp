@@ -324,11 +324,37 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   if (!base_ || n > slot_bytes_) return NotHandled;
   int64_t slot = acquire(n);
   if (slot < 0) return NotHandled;
+  // the MD5 and the CRC read the caller's buffer while it is copied into the slot, so neither
+  // waits for the copy (the MD5, ~1 ms per MiB, is the write's longest chain)
+  Hashes h;
+  struct Join {
+    Hashes& h;
+    ~Join() { h.wait(); }
+  } join{h};
+  start_hashes(data, n, true, &h);
   std::memcpy(base_ + slot, data, n);
   std::string md5;
-  Status st = write_slot(path, slot, n, replicas, msg, t, rid_in, attrs, nullptr, &md5);
+  Status st = write_slot_impl(path, slot, n, replicas, msg, t, rid_in, attrs, nullptr, &md5, &h);
+  h.wait();
   release(slot);
   return st;
+}
+
+void FastClient::start_hashes(const uint8_t* p, size_t n, bool with_crc, Hashes* h) {
+  auto md5_task = std::make_shared<std::packaged_task<std::string()>>([p, n] { return md5_hex(p, n); });
+  h->md5 = md5_task->get_future();
+  std::shared_ptr<std::packaged_task<uint32_t()>> crc_task;
+  if (with_crc) {
+    crc_task = std::make_shared<std::packaged_task<uint32_t()>>([p, n] { return crc32(p, n); });
+    h->crc = crc_task->get_future();
+  }
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    queue_.emplace_back([md5_task] { (*md5_task)(); });
+    if (crc_task) queue_.emplace_front([crc_task] { (*crc_task)(); });
+  }
+  if (crc_task) q_cv_.notify_all();
+  else q_cv_.notify_one();
 }
 
 int64_t FastClient::acquire_slot(size_t n) { return acquire(n); }
@@ -337,6 +363,13 @@ FastClient::Status FastClient::write_slot(const std::string& path, int64_t slot,
                                           std::string* msg, Times* t, const std::string& rid_in,
                                           const std::map<std::string, std::string>* attrs, const char* etag_attr,
                                           std::string* md5_out) {
+  return write_slot_impl(path, slot, n, replicas, msg, t, rid_in, attrs, etag_attr, md5_out, nullptr);
+}
+
+FastClient::Status FastClient::write_slot_impl(const std::string& path, int64_t slot, size_t n, int* replicas,
+                                               std::string* msg, Times* t, const std::string& rid_in,
+                                               const std::map<std::string, std::string>* attrs,
+                                               const char* etag_attr, std::string* md5_out, Hashes* pre) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
   RequestScope rs(rid);
   TraceRange tr("dfs.client.write");
@@ -346,21 +379,22 @@ FastClient::Status FastClient::write_slot(const std::string& path, int64_t slot,
   const uint8_t* data = base_ + slot;
   auto clk = Clock::now();
   // MD5 (the ETag) is a sequential chain and only CompleteFile needs it: hash on a worker
-  // while the create RPC, the CRC and the block transfer run here
-  auto md5_task = std::make_shared<std::packaged_task<std::string()>>([data, n] { return md5_hex(data, n); });
-  std::future<std::string> md5 = md5_task->get_future();
-  {
-    std::lock_guard<std::mutex> g(q_mu_);
-    queue_.emplace_back([md5_task] { (*md5_task)(); });
+  // while the create RPC, the CRC and the block transfer run here (write() started it, and
+  // the CRC, on its own buffer already)
+  Hashes own;
+  struct Join {  // never return while the worker still reads the buffer
+    Hashes& h;
+    ~Join() { h.wait(); }
+  } join{own};
+  Hashes& h = pre ? *pre : own;
+  if (!pre) start_hashes(data, n, false, &own);
+  std::future<std::string>& md5 = h.md5;
+  uint32_t crc = 0;
+  bool have_crc = false;
+  if (!h.crc.valid()) {
+    crc = crc32(data, n);
+    have_crc = true;
   }
-  q_cv_.notify_one();
-  struct Join {  // never return while the worker still reads the caller's buffer
-    std::future<std::string>& f;
-    ~Join() {
-      if (f.valid()) f.wait();
-    }
-  } join{md5};
-  uint32_t crc = crc32(data, n);
   t->crc = since(clk);
 
   pb::CreateFileRequest creq;
@@ -391,6 +425,7 @@ FastClient::Status FastClient::write_slot(const std::string& path, int64_t slot,
   }
   if (!cresp.deferred || strip_scheme(alloc.chunk_server_addresses[0]) != local_cs_)
     return NotHandled;  // nothing was recorded yet: the Python path redoes it
+  if (!have_crc) crc = h.crc.get();  // computed beside the copy and the create RPC
   t->create = since(clk);
 
   std::string body;

@@ -17,6 +17,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <future>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -166,6 +167,21 @@ class FastClient {
   std::mutex conn_mu_;
   std::map<std::string, std::vector<int>> idle_;
 
+  // Hashes of a write's payload, started on the hash workers: the MD5 (the etag, a strictly
+  // sequential chain) and optionally the whole-buffer CRC (jumps the queue: it gates the
+  // block transfer). write() starts both on the caller's buffer before copying it into the slot.
+  struct Hashes {
+    std::future<std::string> md5;
+    std::future<uint32_t> crc;
+    void wait() {  // never return while a worker still reads the buffer
+      if (md5.valid()) md5.wait();
+      if (crc.valid()) crc.wait();
+    }
+  };
+  void start_hashes(const uint8_t* p, size_t n, bool with_crc, Hashes* h);
+  Status write_slot_impl(const std::string& path, int64_t slot, size_t n, int* replicas, std::string* msg, Times* t,
+                         const std::string& rid, const std::map<std::string, std::string>* attrs,
+                         const char* etag_attr, std::string* md5_out, Hashes* pre);
   // MD5 workers (the etag is a strictly sequential hash: overlap it with the RPCs)
   std::mutex q_mu_;
   std::condition_variable q_cv_;

@@ -77,6 +77,12 @@ Json stats_json(const StoreStats& t) {
   d.set("journal_segs_filled", t.journal_segs_filled);
   d.set("journal_fill_bytes", t.journal_fill_bytes);
   d.set("journal_parts_unready", t.journal_parts_unready);
+  d.set("journal_spares_missing", t.journal_spares_missing);
+  d.set("journal_grow_deferred", t.journal_grow_deferred);
+  d.set("journal_mark_preflushes", t.journal_mark_preflushes);
+  d.set("journal_reserve_markers", t.journal_reserve_markers);
+  d.set("delete_tomb_failures", t.delete_tomb_failures);
+  d.set("export_busy_polls", t.export_busy_polls);
   d.set("journal_sync_ns", t.journal_sync_ns);
   d.set("journal_bypassed", t.journal_bypassed);
   d.set("journal_commit_ns", t.journal_commit_ns);

@@ -26,6 +26,10 @@ constexpr uint32_t kRecMagic = 0x524a5344u;  // "DSJR"
 constexpr uint64_t kPage = 4096;
 constexpr uint64_t kHdr = 512;
 constexpr uint32_t kFlagSealed = 1, kFlagRetired = 2;
+// the tail of every part that block records leave free: room for 16 tombstone / supersede
+// markers per part when no free segment is left (a delete must not wait for journal space
+// that only deletes can free)
+constexpr uint64_t kMarkerReserve = 16 * kPage;
 
 // version 3; version 2 (round 4: no flags, no LSN mark, retirement zeroed the page) still reads
 struct PartHdr {
@@ -231,15 +235,34 @@ bool BlockJournal::mark_one(std::unique_lock<std::mutex>& lk) {
   if (!s) return false;
   s->marking = true;
   const uint64_t seq = s->seq, lsn = next_lsn_;
+  // complete() only says every record's bytes were written, not that they were flushed: a
+  // record whose commit is still running (or that nobody commits, e.g. padding) may sit in
+  // the page cache, and writeback could persist the sealed header before it — replay would
+  // then trust a torn record. So the parts not yet durable up to their tail are flushed
+  // first, and only then is the sealed header written and flushed.
+  std::vector<uint64_t> flush_to(s->parts.size(), 0);
+  for (size_t k = 0; k < s->parts.size(); ++k) {
+    const JournalPart* p = s->parts[k].get();
+    if (p->durable_upto < p->tail || p->syncers > 0) flush_to[k] = p->tail;
+  }
   lk.unlock();
   bool ok = true;
-  for (size_t k = 0; k < s->parts.size(); ++k) {
+  for (size_t k = 0; k < s->parts.size(); ++k)
+    if (flush_to[k] && cfg_.sync) ok = ok && ::fdatasync(s->parts[k]->fd) == 0;
+  if (ok) {
+    lk.lock();
+    for (size_t k = 0; k < s->parts.size(); ++k)
+      if (flush_to[k]) s->parts[k]->durable_upto = std::max(s->parts[k]->durable_upto, flush_to[k]);
+    lk.unlock();
+  }
+  for (size_t k = 0; ok && k < s->parts.size(); ++k) {
     JournalPart* p = s->parts[k].get();
     ok = ok && write_part_header(p, seq, static_cast<int>(k), static_cast<int>(s->parts.size()), kFlagSealed, lsn);
     ok = ok && (!cfg_.sync || ::fdatasync(p->fd) == 0);
   }
   lk.lock();
   s->marking = false;
+  st_.mark_preflushes += std::count_if(flush_to.begin(), flush_to.end(), [](uint64_t v) { return v != 0; });
   if (ok) {
     s->marked = true;
     st_.segs_marked++;
@@ -265,12 +288,23 @@ void BlockJournal::prepare_loop() {
   static const std::vector<uint8_t> zeros(8 << 20, 0);
   std::unique_lock<std::mutex> lk(mu_);
   auto grow_check_ns = 0ull;
+  bool deferring = false;
+  const uint64_t idle_ns = static_cast<uint64_t>(std::max(1, cfg_.idle_fill_ms)) * 1000000ull;
   for (;;) {
     if (prep_stop_) return;
     const int have = static_cast<int>(segs_.size()) + preparing_;
-    bool want = cfg_.grow ? static_cast<int>(free_.size()) + preparing_ < cfg_.spares &&
-                                (cfg_.max_segs <= 0 || have < cfg_.max_segs)
+    const int ready = static_cast<int>(free_.size()) + preparing_;
+    bool want = cfg_.grow ? ready < cfg_.spares && (cfg_.max_segs <= 0 || have < cfg_.max_segs)
                           : have < cfg_.max_segs;
+    if (want && cfg_.grow && ready >= cfg_.spares_low && last_append_ns_ && now_ns() - last_append_ns_ < idle_ns) {
+      // enough spares for now and the writers are active: top up in their next idle window,
+      // so no segment creation (and its flushes) shares the volume with acked writes
+      if (!deferring) st_.grow_deferred++;
+      deferring = true;
+      want = false;
+    } else if (want) {
+      deferring = false;
+    }
     if (want && cfg_.grow) {
       const uint64_t t = now_ns();
       if (grow_blocked_ && t < grow_check_ns) {
@@ -329,7 +363,6 @@ void BlockJournal::prepare_loop() {
       cv_.notify_all();
       continue;
     }
-    const uint64_t idle_ns = static_cast<uint64_t>(std::max(1, cfg_.idle_fill_ms)) * 1000000ull;
     const uint64_t since = now_ns() - last_append_ns_;
     const bool idle = !last_append_ns_ || since >= idle_ns;
     if (idle && mark_one(lk)) continue;
@@ -347,7 +380,8 @@ void BlockJournal::prepare_loop() {
       return f->sealed && !f->marked && !f->marking && f->complete();
     });
     if (!t && !sealed_pending) {
-      cv_.wait_for(lk, std::chrono::milliseconds(200));
+      // (a deferred top-up is re-checked once the writers have been idle for idle_ns)
+      cv_.wait_for(lk, deferring ? std::chrono::nanoseconds(idle_ns + 1000000) : std::chrono::nanoseconds(200000000));
       continue;
     }
     if (!idle) {  // writers active: wait until they pause
@@ -405,7 +439,7 @@ uint64_t BlockJournal::rec_bytes_for(uint64_t n, uint64_t nslices) {
 }
 
 bool BlockJournal::fits(uint64_t n, uint64_t nslices) const {
-  return rec_bytes_for(n, nslices) + kPage <= part_bytes_;
+  return rec_bytes_for(n, nslices) + kPage + kMarkerReserve <= part_bytes_;
 }
 
 SegRef BlockJournal::open_seg(int index, bool create) {
@@ -665,16 +699,36 @@ SegRef BlockJournal::activate_locked(std::unique_lock<std::mutex>& lk, std::stri
   }
 }
 
-bool BlockJournal::place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, JournalRec* r, std::string* err) {
+bool BlockJournal::place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, JournalRec* r, std::string* err,
+                                bool marker) {
   for (;;) {
     SegRef s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
+    if (!s && marker && free_.empty() && !order_.empty() && !order_.back()->marking) {
+      // no active segment: a marker goes into the newest segment's reserve (it retires last,
+      // so the marker still outlives every record it cancels); the segment is re-marked later
+      SegRef b = order_.back();
+      for (size_t k = 0; k < b->parts.size(); ++k) {
+        JournalPart* p = b->parts[k].get();
+        if (p->tail + len > p->cap) continue;
+        r->seg = b;
+        r->part = static_cast<int>(k);
+        r->off = p->tail;
+        r->end = p->tail + len;
+        p->tail += len;
+        b->marked = false;
+        st_.reserve_markers++;
+        return true;
+      }
+    }
     if (s) {
-      // round robin over the parts, so concurrent appends land in different files
+      // round robin over the parts, so concurrent appends land in different files; block
+      // records leave each part's marker reserve free
+      const uint64_t limit = marker ? 0 : kMarkerReserve;
       const size_t np = s->parts.size();
       for (size_t i = 0; i < np; ++i) {
         const size_t k = (rr_ + i) % np;
         JournalPart* p = s->parts[k].get();
-        if (p->tail + len > p->cap) continue;
+        if (p->tail + len + limit > p->cap) continue;
         rr_ = k + 1;
         r->seg = s;
         r->part = static_cast<int>(k);
@@ -693,7 +747,7 @@ bool BlockJournal::place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, 
 
 bool BlockJournal::reserve(uint64_t n, uint64_t nslices, JournalRec* r, std::string* err) {
   const uint64_t len = rec_bytes_for(n, nslices);
-  if (len + kPage > part_bytes_) {
+  if (len + kPage + kMarkerReserve > part_bytes_) {
     *err = "block larger than a journal segment part";
     return false;
   }
@@ -859,7 +913,7 @@ bool BlockJournal::marker(uint32_t type, const std::string& id, std::string* err
       *err = "journal failed";
       return false;
     }
-    if (!place_locked(lk, kPage, &r, err)) return false;
+    if (!place_locked(lk, kPage, &r, err, true)) return false;
     last_append_ns_ = now_ns();
   }
   RecHdr h{};
@@ -973,11 +1027,15 @@ JournalStats BlockJournal::stats() {
     s.live_bytes += seg->live_bytes;
     s.used_bytes += seg->capacity();
   }
+  // parts_unready: what a writer activating a segment could be handed that is not ready (a
+  // free segment not written out yet, or none at all below spares_low); spares_missing: the
+  // grow-mode top-up still owed (done in idle windows)
   uint64_t missing = 0;
   if (cfg_.grow) {
-    if (!grow_blocked_ && static_cast<int>(free_.size()) < cfg_.spares &&
-        (cfg_.max_segs <= 0 || static_cast<int>(segs_.size()) < cfg_.max_segs))
-      missing = static_cast<uint64_t>(cfg_.spares) - free_.size();
+    const bool can_grow = !grow_blocked_ && (cfg_.max_segs <= 0 || static_cast<int>(segs_.size()) < cfg_.max_segs);
+    const int nfree = static_cast<int>(free_.size());
+    if (can_grow && nfree < cfg_.spares) s.spares_missing = static_cast<uint64_t>(cfg_.spares - nfree);
+    if (can_grow && nfree < cfg_.spares_low) missing = static_cast<uint64_t>(cfg_.spares_low - nfree);
   } else if (cfg_.max_segs > static_cast<int>(segs_.size())) {
     missing = cfg_.max_segs - segs_.size();
   }

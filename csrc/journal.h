@@ -75,6 +75,10 @@ struct JournalConfig {
   // volume, profiles/r4_journal); a fill never competes with acked writes. The same idle
   // windows flush the `sealed` headers.
   int spares = 2;
+  // grow: while the writers are active, a spare is created only when fewer than this many are
+  // free (creating one is a fallocate + one flush per part + a directory flush on the volume
+  // the acked writes use); the rest of the top-up waits for an idle window
+  int spares_low = 2;
   bool zero_fill = true;
   int idle_fill_ms = 20;   // the writers count as idle after this long without an append
   // Flush rounds that may run at once per part. 1 = classic group commit (one leader, the
@@ -157,7 +161,11 @@ struct JournalStats {
            fill_bytes = 0;
   uint64_t live_records = 0, live_bytes = 0, used_bytes = 0;  // used: in-use segments x capacity
   uint64_t sync_ns = 0, commit_ns = 0;  // time in fdatasync rounds; time writers spent in commit()
-  uint64_t parts_unready = 0;  // part files not yet created, or (zero_fill) not yet written out once
+  uint64_t parts_unready = 0;  // free segments' parts not yet written out once (zero_fill), or missing below spares_low
+  uint64_t spares_missing = 0; // grow: segments short of `spares` (topped up in idle windows)
+  uint64_t grow_deferred = 0;  // grow: spare creations put off while the writers were active
+  uint64_t mark_preflushes = 0;  // parts flushed before a sealed header (records not yet durable)
+  uint64_t reserve_markers = 0;  // markers placed in a sealed segment's reserve (no active segment)
   bool failed = false, grow_blocked = false;
   std::string last_error;  // the last segment preparation / header error, for /stats
 };
@@ -191,7 +199,8 @@ class BlockJournal {
   void abandon(const JournalRec& r);  // the record becomes padding (and is released)
   bool commit(const JournalRec& r);   // returns once the record is on stable storage
   // A durable tombstone (kJrTomb) or supersede marker (kJrFile) for `id`; returns after its
-  // group commit.
+  // group commit. Markers may use the last kMarkerReserve bytes of every part, which block
+  // records leave free, so a delete can still commit its tombstone when no segment is free.
   bool marker(uint32_t type, const std::string& id, std::string* err);
   // A committed record nobody references becomes durable padding (a relocated copy that lost
   // the race with a rewrite: replay must not see it).
@@ -213,7 +222,8 @@ class BlockJournal {
 
  private:
   // reserves `len` bytes in a part of the active segment (activating one if needed); lock held
-  bool place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, JournalRec* r, std::string* err);
+  bool place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, JournalRec* r, std::string* err,
+                    bool marker = false);
   SegRef activate_locked(std::unique_lock<std::mutex>& lk, std::string* err);
   std::string describe_locked() const;  // segment accounting, for errors and stall reports
   bool write_part_header(JournalPart* p, uint64_t seq, int part, int nparts, uint32_t flags, uint64_t lsn_hw);

@@ -120,7 +120,10 @@ def _native_run(client, kind: str, names: list[str], bufs: list, concurrency: in
                 for name, v in zip(_PHASES[kind], tv):
                     client.phase_times.setdefault(name, []).append(v)
     n = len(names)
-    return Stats("Write" if kind == "write" else "Read", n, sum(nbytes) // max(1, n), total, lat)
+    out = Stats("Write" if kind == "write" else "Read", n, sum(nbytes) // max(1, n), total, lat)
+    # per-op phase times (seconds, _PHASES order; None for ops redone on the Python path)
+    out.op_phases = [tuple(tv) if st == 0 else None for st, tv in zip(status, times)]
+    return out
 
 
 def bench_write(client, count: int = 100, size: int = 1 << 20, concurrency: int = 10, prefix: str = "bench_write",

@@ -93,6 +93,20 @@ def _audit_records(g, pred, timeout=15.0):
         time.sleep(0.1)
 
 
+def _quiesced_count(g, quiet_s=1.0, timeout=20.0):
+    """Record count once the audit log has taken no new record for `quiet_s`."""
+    deadline = time.time() + timeout
+    last, since = -1, time.time()
+    while time.time() < deadline:
+        n = len(list(SegmentStore(g.audit_dir).scan()))
+        if n != last:
+            last, since = n, time.time()
+        elif time.time() - since >= quiet_s:
+            break
+        time.sleep(0.1)
+    return last
+
+
 def test_process_is_native(gw):
     """The launcher starts the executable for s3.server: no interpreter in the process."""
     import psutil
@@ -230,8 +244,12 @@ def test_audit_chain_written_natively(authgw):
     assert done(recs), recs[-5:]
     assert any(r["resource"] == "arn:dfs:sts:::*" and r["role_arn"] == "arn:dfs:iam:::role/tenant-a-role"
                for r in recs)
+    # the logger writes asynchronously: compare the chain with a quiesced log (no new record
+    # for a second; every request above has returned), scanned again after the verification
+    quiet = _quiesced_count(g)
     n, errs = verify_chain(SegmentStore(g.audit_dir), AUDIT_SECRET)
-    assert n == len(recs) and errs == []
+    after = [r for _, r in SegmentStore(g.audit_dir).scan()]
+    assert errs == [] and n == len(after) == quiet >= len(recs)
 
 
 def test_sse_at_rest(cluster):
