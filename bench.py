@@ -499,6 +499,7 @@ def main():
 
             st0 = cs_stats()
             thr0 = st0.get("thread_cpu_ms", {})  # per-thread CPU of the chunkserver, before
+            vm0 = _vmstat()
             # journal readiness at the start of the timed region (reported with its end)
             jr0 = {k: st0.get("journal_" + k, 0) for k in JOURNAL_READY_KEYS}
             client.phase_times = {}
@@ -533,6 +534,8 @@ def main():
             # counters of the timed phase only (the stress / remote phases below add their own hops)
             stats = cs_stats()
             jr1 = {k: stats.get("journal_" + k, 0) for k in JOURNAL_READY_KEYS}
+            vm1 = _vmstat()
+            vm_delta = {k: vm1[k] - vm0.get(k, 0) for k in vm1 if vm1[k] - vm0.get(k, 0)}
             thr1 = stats.get("thread_cpu_ms", {})
             # cores each named chunkserver thread group used over the timed region (HIP runtime
             # threads keep the executable's name)
@@ -593,9 +596,9 @@ def main():
                 except (OSError, ValueError, IndexError, subprocess.TimeoutExpired) as e:
                     roof = {"error": str(e)[:300]}
             slow_w = [{"ms": round(1e3 * x, 3), "step": st, "op": i,
-                       **({k: round(1e3 * v, 3) for k, v in zip(("crc", "create", "write", "md5_wait", "complete"), ph)}
+                       **({k: round(1e3 * v, 3) for k, v in zip(("crc", "create", "write", "md5_wait", "complete", "copy", "acquire"), ph)}
                           if ph else {})} for x, st, i, ph in slow]
-            allr = gather({"slow_w": slow_w, "roof": roof, "elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
+            allr = gather({"vm": vm_delta, "slow_w": slow_w, "roof": roof, "elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
                            "rbytes": rbytes, "wt": wt,
                            "rt": rt, "cs": stats, "stress": stress, "remote": remote, "vol": vol,
                            "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
@@ -696,6 +699,9 @@ def main():
                     "client_phase_p50_ms_rank0": allr[0]["phases"],
                     # rank 0's 20 slowest timed writes: step, op index and where the time went
                     "write_tail_rank0": allr[0]["slow_w"],
+                    # node-wide /proc/vmstat deltas over rank 0's timed region (NUMA hinting faults /
+                    # migrations, THP and compaction stalls that show up as a stalled copy)
+                    "vmstat_timed_rank0": allr[0]["vm"],
                     **repl_phases(allr),
                 }
                 if a.remote_steps > 0:
@@ -900,6 +906,19 @@ def _bytes_needed(a, n: int) -> int:
     rf = min(3, n)
     steps = a.steps + a.warmup + (a.remote_steps or 0)
     return n * rf * steps * a.count * (a.size + a.size // 128 + 4096)
+
+
+_VMSTAT_KEYS = ("numa_hint_faults", "numa_hint_faults_local", "numa_pages_migrated", "pgmigrate_success",
+                "pgmigrate_fail", "thp_fault_alloc", "compact_stall", "pgmajfault", "pgfault", "allocstall_normal",
+                "pgscan_direct", "nr_dirty")
+
+
+def _vmstat() -> dict:
+    try:
+        with open("/proc/vmstat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f) if k in _VMSTAT_KEYS}
+    except (OSError, ValueError):
+        return {}
 
 
 JOURNAL_SEG_BYTES = 256 << 20

@@ -9,6 +9,7 @@
 // in-memory transport with a partition matrix.
 //
 //   unit_tests [filter]   -> "ok <name>" / "FAIL <name>: <why>" lines, exit 1 on any failure
+#include <fcntl.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -249,7 +250,10 @@ TEST(wal_replays_records_and_drops_a_torn_tail) {
     auto r = w.replay();
     CHECK(r.size() == 3 && r[0] == "one" && r[2].size() == 3000);
   }
-  std::filesystem::resize_file(p, std::filesystem::file_size(p) - 10);  // crash mid-record
+  // the file is written out with zeros past the last frame (appends flush no metadata)
+  const uint64_t end = (8 + 3) + (8 + 3) + (8 + 3000);
+  CHECK(std::filesystem::file_size(p) > end);
+  std::filesystem::resize_file(p, end - 10);  // crash mid-record
   {
     Wal w(p, false);
     auto r = w.replay();
@@ -259,6 +263,34 @@ TEST(wal_replays_records_and_drops_a_torn_tail) {
   Wal w(p, false);
   auto r = w.replay();
   CHECK(r.size() == 3 && r[2] == "three");
+  // a batch whose first frame is torn while later ones reached the disk: the later frames
+  // must never reappear behind a shorter append that lands on the torn one
+  {
+    Wal w2(p, false);
+    (void)w2.replay();
+    w2.append({std::string(100, 'a'), "late-1", "late-2"});
+  }
+  {
+    int fd = ::open(p.c_str(), O_RDWR);
+    const uint64_t torn = end - 10 + 0;  // (the valid prefix after the first cut: "one", "two")
+    (void)torn;
+    // flip a payload byte of the 100-byte frame (it starts after "one", "two", "three")
+    const off_t at = static_cast<off_t>((8 + 3) + (8 + 3) + (8 + 5) + 8 + 50);
+    char c = 0;
+    CHECK(::pread(fd, &c, 1, at) == 1);
+    c ^= 0x5a;
+    CHECK(::pwrite(fd, &c, 1, at) == 1);
+    ::close(fd);
+  }
+  {
+    Wal w3(p, false);
+    auto r3 = w3.replay();
+    CHECK(r3.size() == 3 && r3[2] == "three");
+    w3.append({std::string(100, 'b')});  // the same size as the torn frame
+  }
+  Wal w4(p, false);
+  auto r4 = w4.replay();
+  CHECK(r4.size() == 4 && r4[3] == std::string(100, 'b'));
   std::filesystem::remove_all(d);
 }
 

@@ -14,6 +14,8 @@
 #include <mutex>
 #include <optional>
 #include <set>
+#include <condition_variable>
+#include <functional>
 #include <thread>
 
 #include "audit_log.h"
@@ -186,6 +188,65 @@ struct BenchOut {
   double total_s = 0;
 };
 
+// The workers are a persistent pool, like the reference CLI's tokio runtime: created once,
+// each keeping its read buffer (pre-touched) across calls. Spawning `concurrency` threads per
+// phase and giving each a fresh 1 MiB buffer meant thread stacks and buffers mapped and
+// unmapped twice per step, and the page faults and TLB shootdowns of that stalled the other
+// workers' copies (measured as 2-8 ms copy stalls of ~10 concurrent writes, r6).
+class BenchPool {
+ public:
+  static BenchPool& get() {
+    static BenchPool* p = new BenchPool();  // never destroyed: workers park between calls
+    return *p;
+  }
+  // runs job(worker_buffer) on `n` workers and returns when all have finished
+  void run(int n, const std::function<void(std::vector<uint8_t>*)>& job) {
+    std::unique_lock<std::mutex> lk(mu_);
+    busy_cv_.wait(lk, [&] { return !active_; });  // one run at a time
+    while (static_cast<int>(threads_.size()) < n) {
+      const int id = static_cast<int>(threads_.size());
+      bufs_.push_back(std::make_unique<std::vector<uint8_t>>());
+      threads_.emplace_back([this, id] { loop(id); });
+      threads_.back().detach();
+    }
+    job_ = &job;
+    want_ = n;
+    running_ = n;
+    active_ = true;
+    ++gen_;
+    cv_.notify_all();
+    done_cv_.wait(lk, [&] { return running_ == 0; });
+    job_ = nullptr;
+    active_ = false;
+    busy_cv_.notify_one();
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return gen_ != seen; });
+      seen = gen_;
+      if (id >= want_) continue;
+      const auto* job = job_;
+      std::vector<uint8_t>* buf = bufs_[id].get();
+      lk.unlock();
+      (*job)(buf);
+      lk.lock();
+      if (--running_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_, busy_cv_;
+  std::vector<std::thread> threads_;
+  std::vector<std::unique_ptr<std::vector<uint8_t>>> bufs_;
+  const std::function<void(std::vector<uint8_t>*)>* job_ = nullptr;
+  int want_ = 0, running_ = 0;
+  bool active_ = false;
+  uint64_t gen_ = 0;
+};
+
 template <class Op>
 void bench_run(size_t count, int concurrency, BenchOut* out, Op op) {
   out->status.assign(count, 0);
@@ -194,12 +255,11 @@ void bench_run(size_t count, int concurrency, BenchOut* out, Op op) {
   out->bytes.assign(count, 0);
   std::atomic<size_t> next{0};
   std::mutex err_mu;
-  auto worker = [&] {
-    std::vector<uint8_t> buf;  // this worker's read buffer
+  std::function<void(std::vector<uint8_t>*)> worker = [&](std::vector<uint8_t>* buf) {
     for (size_t i; (i = next.fetch_add(1)) < count;) {
       std::string msg;
       auto t0 = std::chrono::steady_clock::now();
-      int st = op(i, &out->times[i], &out->bytes[i], &buf, &msg);
+      int st = op(i, &out->times[i], &out->bytes[i], buf, &msg);
       out->lat[i] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       out->status[i] = st;
       if (st == FastClient::Failed) {
@@ -209,9 +269,7 @@ void bench_run(size_t count, int concurrency, BenchOut* out, Op op) {
     }
   };
   auto t0 = std::chrono::steady_clock::now();
-  std::vector<std::thread> ws;
-  for (int k = 0; k < std::max(1, concurrency); ++k) ws.emplace_back(worker);
-  for (auto& w : ws) w.join();
+  BenchPool::get().run(std::max(1, concurrency), worker);
   out->total_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
@@ -219,7 +277,7 @@ py::tuple bench_result(const BenchOut& o, bool reads) {
   py::list times;
   for (const auto& t : o.times) {
     if (reads) times.append(py::make_tuple(t.getinfo, t.read));
-    else times.append(py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete));
+    else times.append(py::make_tuple(t.crc, t.create, t.write, t.md5_wait, t.complete, t.copy, t.acquire));
   }
   return py::make_tuple(o.status, o.lat, o.total_s, times, o.bytes, o.first_error, o.mismatches);
 }
@@ -275,7 +333,7 @@ py::tuple bench_reads_fast(FastClient& c, const std::vector<std::string>& paths,
                 uint64_t n = 0;
                 FastClient::Status st = c.read(paths[i], &slot, &n, msg, t);
                 if (st != FastClient::Ok) return static_cast<int>(st);
-                if (buf->size() < n) buf->resize(n);
+                if (buf->size() < n) buf->resize(n);  // kept by the pool's worker across calls
                 if (n) std::memcpy(buf->data(), c.slot_ptr(slot), n);
                 if (slot >= 0) c.release(slot);
                 *nb = n;

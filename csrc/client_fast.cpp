@@ -153,7 +153,9 @@ FastClient::FastClient(std::string fastpath_socket, std::string local_chunkserve
   int fd = ::open(name, O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0600);
   if (fd >= 0) {
     if (::ftruncate(fd, static_cast<off_t>(arena_bytes_)) == 0) {
-      void* p = ::mmap(nullptr, arena_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      // populated up front: a slot's first use in a timed loop must not take 256 page faults
+      // (each allocating and zeroing a shmem page) inside its copy
+      void* p = ::mmap(nullptr, arena_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
       if (p != MAP_FAILED) {
         base_ = static_cast<uint8_t*>(p);
         arena_path_ = name;
@@ -322,8 +324,10 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
                                      std::string* msg, Times* t, const std::string& rid_in,
                                      const std::map<std::string, std::string>* attrs) {
   if (!base_ || n > slot_bytes_) return NotHandled;
+  auto c0 = Clock::now();
   int64_t slot = acquire(n);
   if (slot < 0) return NotHandled;
+  t->acquire = std::chrono::duration<double>(Clock::now() - c0).count();
   // the MD5 and the CRC read the caller's buffer while it is copied into the slot, so neither
   // waits for the copy (the MD5, ~1 ms per MiB, is the write's longest chain)
   Hashes h;
@@ -333,6 +337,7 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
   } join{h};
   start_hashes(data, n, true, &h);
   std::memcpy(base_ + slot, data, n);
+  t->copy = since(c0);
   std::string md5;
   Status st = write_slot_impl(path, slot, n, replicas, msg, t, rid_in, attrs, nullptr, &md5, &h);
   h.wait();

@@ -63,6 +63,8 @@ class FastClient {
   enum Status { Ok = 0, NotHandled = 1, Failed = 2 };
   struct Times {  // seconds, per phase (benchmark breakdown)
     double crc = 0, create = 0, write = 0, md5_wait = 0, complete = 0, getinfo = 0, read = 0;
+    double copy = 0;  // write(): slot acquire + copy of the caller's buffer into it
+    double acquire = 0;  // ... of which waiting for a free slot
   };
 
   FastClient(std::string fastpath_socket, std::string local_chunkserver, size_t arena_bytes, size_t slot_bytes,

@@ -4,7 +4,10 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -50,29 +53,31 @@ void write_fully(int fd, const std::string& buf, uint64_t off, const std::string
 }
 }  // namespace
 
-Wal::Wal(std::string path, bool sync) : path_(std::move(path)), sync_(sync) {}
+Wal::Wal(std::string path, bool sync) : path_(std::move(path)), sync_(sync) {
+  const char* e = std::getenv("DFS_WAL_PREFILL_MB");
+  prefill_ = static_cast<uint64_t>(e && *e ? std::atoll(e) : 8) << 20;
+}
 
 Wal::~Wal() {
   if (fd_ >= 0) ::close(fd_);
 }
 
-void Wal::open_for_append() {
+// Opens the log, finds its valid end (the first torn / corrupt frame, or a zero length: the
+// written-out zeros past the end), cuts everything after it and writes zeros ahead of it.
+// Appends then overwrite written extents inside the file: their fdatasync flushes data only,
+// with no size or extent change for the filesystem's journal to commit with it (the master's
+// CompleteFile paid one such metadata commit per write).
+void Wal::open_for_append(std::vector<std::string>* out) {
   if (fd_ >= 0) return;
   fd_ = ::open(path_.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
   if (fd_ < 0) throw std::runtime_error("wal open " + path_ + ": " + std::strerror(errno));
   struct stat st;
   ::fstat(fd_, &st);
-  size_ = static_cast<uint64_t>(st.st_size);
-}
-
-std::vector<std::string> Wal::replay() {
-  std::lock_guard<std::mutex> g(mu_);
-  open_for_append();
-  std::vector<std::string> out;
-  std::string buf(size_, '\0');
+  const uint64_t fsize = static_cast<uint64_t>(st.st_size);
+  std::string buf(fsize, '\0');
   size_t got = 0;
-  while (got < size_) {
-    ssize_t r = ::pread(fd_, &buf[got], size_ - got, static_cast<off_t>(got));
+  while (got < fsize) {
+    ssize_t r = ::pread(fd_, &buf[got], fsize - got, static_cast<off_t>(got));
     if (r <= 0) break;
     got += static_cast<size_t>(r);
   }
@@ -81,25 +86,53 @@ std::vector<std::string> Wal::replay() {
     uint32_t len, crc;
     std::memcpy(&len, &buf[pos], 4);
     std::memcpy(&crc, &buf[pos + 4], 4);
-    if (pos + 8 + len > got) break;
+    if (len == 0 || pos + 8 + len > got) break;
     if (crc32(reinterpret_cast<const uint8_t*>(&buf[pos + 8]), len) != crc) break;
-    out.emplace_back(buf, pos + 8, len);
+    if (out) out->emplace_back(buf, pos + 8, len);
     pos += 8 + len;
   }
-  if (pos != size_) {  // torn tail: cut it off so new appends follow valid records
-    if (::ftruncate(fd_, static_cast<off_t>(pos)) == 0) {
-      size_ = pos;
-      if (sync_) ::fdatasync(fd_);
-    }
+  size_ = pos;
+  filled_ = pos;
+  if (pos < got && std::all_of(buf.begin() + static_cast<std::ptrdiff_t>(pos), buf.begin() + static_cast<std::ptrdiff_t>(got),
+                               [](char c) { return c == 0; })) {
+    filled_ = got;  // a clean end: the zeros written ahead of it are still there
+  } else if (pos != fsize && ::ftruncate(fd_, static_cast<off_t>(pos)) == 0 && sync_) {
+    ::fdatasync(fd_);  // a torn tail goes, so no stale frame can ever follow new appends
   }
+  extend_fill(pos);
+}
+
+void Wal::extend_fill(uint64_t need) {
+  if (prefill_ == 0 || filled_ >= need + prefill_ / 2) return;
+  const uint64_t to = need + prefill_;
+  static const std::string zeros(1 << 20, '\0');
+  for (uint64_t off = filled_; off < to; off += zeros.size()) {
+    const uint64_t n = std::min<uint64_t>(zeros.size(), to - off);
+    write_fully(fd_, n == zeros.size() ? zeros : zeros.substr(0, n), off, "wal prefill");
+  }
+  filled_ = to;
+  if (sync_) ::fdatasync(fd_);  // the size and extents once, ahead of the appends
+}
+
+std::vector<std::string> Wal::replay() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> out;
+  if (fd_ >= 0) {  // already open: rescan from the start
+    ::close(fd_);
+    fd_ = -1;
+  }
+  open_for_append(&out);
   return out;
 }
 
 void Wal::append(const std::vector<std::string>& records) {
   if (records.empty()) return;
+  for (auto& r : records)
+    if (r.empty()) throw std::runtime_error("wal append: empty record");  // a zero length ends the log
   std::string buf = frame(records);
   std::lock_guard<std::mutex> g(mu_);
   open_for_append();
+  extend_fill(size_ + buf.size());
   write_fully(fd_, buf, size_, "wal append");
   size_ += buf.size();
   if (sync_) {

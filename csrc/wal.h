@@ -4,8 +4,10 @@
 //
 // Frame: [u32 length LE][u32 crc32(payload) LE][payload]. A batch of records is written
 // with one pwrite and made durable with ONE fdatasync (leader batching / group commit,
-// simple_raft.rs:1689-1778). Replay stops at the first torn or corrupt frame and
-// truncates the tail, so a crash mid-append loses only the unacknowledged batch.
+// simple_raft.rs:1689-1778). Replay stops at the first torn or corrupt frame (or a zero
+// length) and truncates the tail, so a crash mid-append loses only the unacknowledged batch.
+// The file is kept written out with zeros a few MiB past the last frame, so an append's
+// fdatasync carries no file-size / extent metadata.
 #pragma once
 #include <cstdint>
 #include <mutex>
@@ -26,11 +28,14 @@ class Wal {
   uint64_t syncs() const { return syncs_; }
 
  private:
-  void open_for_append();
+  void open_for_append(std::vector<std::string>* out = nullptr);
+  void extend_fill(uint64_t need);  // zeros written (and flushed) at least prefill_/2 past `need`
   std::string path_;
   bool sync_;
   int fd_ = -1;
-  uint64_t size_ = 0;
+  uint64_t size_ = 0;    // end of the valid frames
+  uint64_t filled_ = 0;  // the file's written bytes (frames, then zeros)
+  uint64_t prefill_ = 8 << 20;  // DFS_WAL_PREFILL_MB (0: the file grows with every append)
   uint64_t syncs_ = 0;
   std::mutex mu_;
 };

@@ -71,7 +71,7 @@ def make_payloads(n: int, size: int) -> list[bytes]:
     return [os.urandom(size) for _ in range(n)]
 
 
-_PHASES = {"write": ("crc", "create", "write", "md5_wait", "complete"), "read": ("getinfo", "read")}
+_PHASES = {"write": ("crc", "create", "write", "md5_wait", "complete", "copy", "acquire"), "read": ("getinfo", "read")}
 
 
 def _native_run(client, kind: str, names: list[str], bufs: list, concurrency: int) -> Stats | None:
