@@ -33,6 +33,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+from rust_hadoop_generated_by_llm_amd.utils.gpu import visible_gpus  # noqa: E402
+
 METRIC = "dfs_cli benchmark write+read MB/s & p50 lat, 1MB\u00d7100 conc=10, 1/2/4/8 GPUs"
 PKG = "rust_hadoop_generated_by_llm_amd"
 
@@ -818,27 +820,6 @@ def forward_counts(allr) -> dict:
         "shm_forwards": sum(r["cs"].get("fp_shm_forwards", 0) for r in allr),
         "grpc_forwards": sum(r["cs"].get("grpc_forwards", 0) for r in allr),
     }
-
-
-def visible_gpus() -> int:
-    """GPUs this node exposes, from the KFD topology (sysfs; opens no device) narrowed by the
-    usual visibility variables."""
-    nodes = Path("/sys/class/kfd/kfd/topology/nodes")
-    n = 0
-    try:
-        for d in nodes.iterdir():
-            try:
-                if int((d / "gpu_id").read_text().strip() or "0") != 0:
-                    n += 1
-            except (OSError, ValueError):
-                pass
-    except OSError:
-        return 0
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        v = os.environ.get(var)
-        if v is not None:
-            n = min(n, len([x for x in v.split(",") if x.strip()]))
-    return n
 
 
 def cgroup_cpu() -> dict | None:

@@ -2,7 +2,9 @@
 """Secondary BASELINE.json configurations (bench.py measures the headline, config 2/scaling).
 
     python bench_configs.py config1            # CPU plumbing: 1 master + 1 CS, put/get + benchmark
-    python bench_configs.py config4 [--gpu 0]  # 2-shard Raft masters: stress-write + cross-shard Rename
+    python bench_configs.py config3 [--gpu 0]  # 3 chunkservers, RF 3: the benchmark, nvme-sync + hbm-ack
+    python bench_configs.py config4 [--gpu 0]  # 2-shard Raft masters + 4 chunkservers (RF 3): stress-write 60 s
+                                               # per shard prefix + cross-shard Rename
     python bench_configs.py config5 [--gpu 0]  # S3 gateway: PUT/GET/Range/MPU + Parquet over S3 (pyarrow)
 
 Each prints one JSON line. The reference publishes no number for these configurations except
@@ -79,19 +81,90 @@ def config1(a):
         cl.close()
 
 
+def _cs_gpus(a, n: int) -> tuple[list[int] | None, bool]:
+    """GPU of each of n chunkservers: distinct GPUs while the box has them (from --gpu on),
+    otherwise several chunkservers share one (a rehearsal of the multi-GPU topology: the
+    replicas still cross between chunkserver processes, HBM to HBM over hipipc). Returns
+    (gpus, shared)."""
+    if a.gpu < 0:
+        return None, False
+    from rust_hadoop_generated_by_llm_amd.utils.gpu import visible_gpus
+
+    ndev = max(1, visible_gpus())
+    gpus = [(a.gpu + i) % ndev for i in range(n)]
+    return gpus, len(set(gpus)) < n
+
+
+def _topology(c, gpus, shared: bool) -> str:
+    where = ("host store" if gpus is None else
+             f"MI355X HBM store, {len(set(gpus))} GPU(s)" + (" shared by the chunkservers" if shared else ""))
+    return f"{c.n_cs} chunkservers ({where}), RF {min(3, c.n_cs)}"
+
+
+# ----------------------------------------------------------------------------- config 3
+def config3(a):
+    """BASELINE config 3: 3 chunkservers, replication factor 3 (the pipeline over the device
+    transport), the benchmark's 1 MiB x 100 at concurrency 10 from one client, nvme-sync and
+    hbm-ack. On a 1-GPU box the 3 chunkservers share the GPU (labelled)."""
+    out = {"config": 3, "files": a.count, "size": a.size, "concurrency": a.concurrency, "steps": a.steps, "runs": []}
+    for durability in ("nvme-sync", "hbm-ack"):
+        gpus, shared = _cs_gpus(a, 3)
+        progress(f"config 3: 3 chunkservers, {durability}")
+        with LocalCluster(n_chunkservers=3, gpus=gpus, durability=durability,
+                          hbm_capacity="16G" if gpus else "0", p2p="hipipc" if gpus else "socket") as c:
+            cl = c.client()
+            payloads = make_payloads(a.count, a.size)
+            ws, names = bench_write(cl, a.count, a.size, a.concurrency, prefix="/bench_write/w", payloads=payloads)
+            bench_read(cl, files=names, concurrency=a.concurrency)  # warm-up step
+            wl, rl, wt, rt, wb, rb = [], [], 0.0, 0.0, 0, 0
+            for s in range(a.steps):
+                ws, names = bench_write(cl, a.count, a.size, a.concurrency, prefix=f"/bench_write/s{s}", payloads=payloads)
+                rs = bench_read(cl, files=names, concurrency=a.concurrency,
+                                verify={n: payloads[i % len(payloads)] for i, n in enumerate(names)} if s == 0 else None)
+                wl += ws.latencies
+                rl += rs.latencies
+                wt += ws.total_s
+                rt += rs.total_s
+                wb += ws.count * ws.avg_size
+                rb += rs.count * rs.avg_size
+            info = cl.get_file_info(names[0])
+            replicas = len(info.blocks[0].locations) if info and info.blocks else 0
+            out["runs"].append({"durability": durability, "topology": _topology(c, gpus, shared),
+                                "replicas_per_block": replicas,
+                                "mb_per_s": round((wb + rb) / (1 << 20) / (wt + rt), 1),
+                                "write_mb_per_s": round(wb / (1 << 20) / wt, 1), "read_mb_per_s": round(rb / (1 << 20) / rt, 1),
+                                "write_p50_ms": pct(wl, 50), "write_p99_ms": pct(wl, 99),
+                                "read_p50_ms": pct(rl, 50), "read_p99_ms": pct(rl, 99)})
+            cl.close()
+    emit(out)
+
+
 # ----------------------------------------------------------------------------- config 4
 def config4(a):
-    gpus = [a.gpu] if a.gpu >= 0 else None
+    # the reference's compose topology: 4 chunkservers shared by both shards, so a write is
+    # replicated 3 ways (docker-compose.yml:49,98,118,137; master.rs:2400-2402)
+    gpus, shared = _cs_gpus(a, a.chunkservers)
     # a fixed two-shard map: with the default thresholds the shard whose prefix went idle
     # (/a during the /z phase) merges into its neighbour after a few seconds below 1 rps, and
     # the "cross-shard" renames then cross nothing (split/merge have their own cluster tests)
-    with LocalCluster(shards=2, config_server=True, n_chunkservers=1, gpus=gpus,
-                      hbm_capacity="16G" if gpus else "0",
+    with LocalCluster(shards=2, config_server=True, n_chunkservers=a.chunkservers, gpus=gpus,
+                      hbm_capacity="16G" if gpus else "0", p2p=("hipipc" if gpus else "socket") if a.chunkservers > 1 else None,
                       master_args=["--split-threshold-rps", "1e12", "--merge-threshold-rps", "-1"]) as c:
         cl = c.client()
+        from bench import cgroup_cpu, cgroup_cpu_delta
+
         # the two-shard range map: the second shard owns "< /m" (sharding.rs:99-106)
-        ss = bench_stress_write(cl, a.stress_seconds, a.stress_size, a.stress_concurrency, prefix="/a/stress")
-        ss2 = bench_stress_write(cl, a.stress_seconds, a.stress_size, a.stress_concurrency, prefix="/z/stress")
+        cpu = []
+        for pre in ("/a/stress", "/z/stress"):
+            progress(f"config 4: stress-write {pre}, {a.stress_seconds:.0f} s")
+            cg0, t0 = cgroup_cpu(), time.perf_counter()
+            st = bench_stress_write(cl, a.stress_seconds, a.stress_size, a.stress_concurrency, prefix=pre)
+            # the whole job's CPU in the phase: every process shares the box's quota
+            cpu.append(cgroup_cpu_delta(cg0, cgroup_cpu(), time.perf_counter() - t0))
+            if pre == "/a/stress":
+                ss = st
+            else:
+                ss2 = st
         # cross-shard renames: /a/... (shard owning "< /m") -> /z/... (the other shard) via 2PC
         n = a.renames
         srcs = [f"/a/ren/src_{i:05d}" for i in range(n)]
@@ -119,15 +192,22 @@ def config4(a):
         el = time.perf_counter() - t0
         ok = all(cl.exists(f"/z/ren/dst_{i:05d}") and not cl.exists(srcs[i]) for i in range(0, n, max(1, n // 50)))
         shards = {sid: len(ms) for sid, ms in c.shard_masters.items()}
-        emit({"config": 4, "topology": f"config server + {len(shards)} Raft shards + 1 chunkserver "
-                                      f"({'MI355X HBM store' if gpus else 'host store'}), nvme-sync",
+        probe = cl.get_file_info(srcs[0].replace("/a/ren/src", "/z/ren/dst"))
+        replicas = len(probe.blocks[0].locations) if probe and probe.blocks else 0
+        emit({"config": 4, "topology": f"config server + {len(shards)} Raft shards + {_topology(c, gpus, shared)}, nvme-sync",
+              "replication_factor": min(3, c.n_cs), "replicas_per_block": replicas,
               "dynamic_sharding": "off (fixed two-shard map)",
               "durable_path": "per-file" if os.environ.get("DFS_JOURNAL") == "0" else "journal",
               "stress_write": [{"prefix": p, "seconds": s.total_s, "size": a.stress_size,
                                 "concurrency": a.stress_concurrency, "ops": s.count, "errors": s.errors,
                                 "ops_per_s": round(s.count / s.total_s, 1), "p50_ms": pct(s.latencies, 50),
-                                "p99_ms": pct(s.latencies, 99), "vs_published_470_ops_per_s":
-                                round(s.count / s.total_s / 470.0, 1)} for p, s in (("/a", ss), ("/z", ss2))],
+                                "p99_ms": pct(s.latencies, 99),
+                                # the published 470 ops/s ran at RF 3 (4 chunkservers): compare only
+                                # a run at the same replication factor
+                                "vs_published_470_ops_per_s": (round(s.count / s.total_s / 470.0, 1)
+                                                               if min(3, c.n_cs) == 3 else None),
+                                "host_cpu_job": cj}
+                               for (p, s), cj in zip((("/a", ss), ("/z", ss2)), cpu)],
               "cross_shard_rename": {"ops": n, "errors": errors, "seconds": round(el, 3),
                                      "ops_per_s": round(len(lats) / el, 1), "p50_ms": pct(lats, 50),
                                      "p99_ms": pct(lats, 99), "verified": ok, "first_error": first_error}})
@@ -596,12 +676,15 @@ def parquet_phase(url: str, a) -> dict:
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("config", choices=["config1", "config4", "config5"])
+    p.add_argument("config", choices=["config1", "config3", "config4", "config5"])
+    p.add_argument("--chunkservers", type=int, default=4,
+                   help="config4: chunkservers (the reference's compose topology has 4: RF 3)")
+    p.add_argument("--steps", type=int, default=10, help="config3: timed benchmark steps per durability mode")
     p.add_argument("--gpu", type=int, default=-1)
     p.add_argument("--count", type=int, default=100)
     p.add_argument("--size", type=int, default=1 << 20)
     p.add_argument("--concurrency", type=int, default=10)
-    p.add_argument("--stress-seconds", type=float, default=30.0)
+    p.add_argument("--stress-seconds", type=float, default=60.0, help="config4: per shard prefix (BASELINE: 60 s)")
     p.add_argument("--stress-size", type=int, default=10240)
     p.add_argument("--stress-concurrency", type=int, default=10)
     p.add_argument("--renames", type=int, default=500)
@@ -618,7 +701,7 @@ def main():
     if a.config == "config5" and a.secure:
         a.config = "config5_secure"
     os.environ.setdefault("DFS_LOG", "warning")
-    {"config1": config1, "config4": config4, "config5": config5, "config5_secure": config5_secure}[a.config](a)
+    {"config1": config1, "config3": config3, "config4": config4, "config5": config5, "config5_secure": config5_secure}[a.config](a)
 
 
 if __name__ == "__main__":

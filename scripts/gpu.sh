@@ -13,6 +13,7 @@
 #   n4        the driver's N=4 command on 4 ranks sharing the GPU
 #   prof      rocprofv3 kernel trace of the chunkserver during a short bench
 #   configs   BASELINE configs 4 and 5
+#   config3 / config4   one of them (config 4 at the reference's compose topology: 4 chunkservers, RF 3)
 #   secure    config 5 at production settings (TLS + SigV4/STS + IAM + SSE-S3 + audit)
 #   crcpmc    two rocprofv3 PMC passes over crc_bench (LDS/VALU, then MFMA busy vs GPU-active)
 #   probe     the box's block devices and mounts (where per-rank journals could live)
@@ -116,6 +117,10 @@ for step in "$@"; do
     configs)
       run config4 500 python bench_configs.py config4 --gpu 0 && \
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
+    config3)  # 3 chunkservers, RF 3 (sharing the GPU on a 1-GPU box), nvme-sync + hbm-ack
+      run config3 600 python bench_configs.py config3 --gpu 0 || exit 1 ;;
+    config4)  # 2 shards + 4 chunkservers (RF 3), 60 s stress-write per shard prefix
+      run config4 600 python bench_configs.py config4 --gpu 0 || exit 1 ;;
     config5)
       run config5 500 python bench_configs.py config5 --gpu 0 || exit 1 ;;
     secure)
