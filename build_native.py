@@ -137,7 +137,8 @@ def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[P
 # host compiler under ASan/UBSan and TSan (SURVEY §5.2 — the reference has no sanitizer runs).
 SANITIZE_SOURCES = ["json.cpp", "json_dump.cpp", "shard_map.cpp", "raft.cpp", "wal.cpp", "crc32.cpp", "gf256.cpp",
                     "disk_gate.cpp", "extent_alloc.cpp", "master_core.cpp", "http_lite.cpp",
-                    "journal.cpp"]
+                    "journal.cpp", "audit_log.cpp", "lin_checker.cpp", "sts.cpp", "crypto.cpp", "tls.cpp",
+                    "sigv4.cpp", "p2p_socket.cpp", "grpc_server.cpp", "grpc_client.cpp"]
 SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
               "tsan": ["-fsanitize=thread"]}
 
@@ -154,8 +155,11 @@ def build_sanitized(kinds=("asan", "tsan"), clean: bool = False) -> list[Path]:
         if clean or not exe.exists() or exe.stat().st_mtime < newest:
             # LLVM's runtime (not GCC 11's) intercepts pthread_cond_clockwait, which libstdc++
             # uses for condition_variable::wait_for; without it TSan misreads every timed wait
+            # host code only; roctx (trace.h), nghttp2 and OpenSSL are linked as shipped
             cmd = [f"{ROCM}/llvm/bin/clang++", "-std=c++17", "-O1", "-g", "-pthread", *SANITIZERS[kind],
-                   f"-I{CSRC}", "-o", str(exe), *map(str, srcs)]
+                   f"-I{CSRC}", f"-I{ROCM}/include", *_nghttp2_include(), "-o", str(exe), *map(str, srcs),
+                   f"-L{ROCM}/lib", "-lrocprofiler-sdk-roctx", "-lssl", "-lcrypto", NGHTTP2_LIB,
+                   f"-Wl,-rpath,{ROCM}/lib"]
             r = subprocess.run(cmd, capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError(f"sanitizer build failed ({kind}):\n{r.stdout}\n{r.stderr}")

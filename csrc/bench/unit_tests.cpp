@@ -28,16 +28,25 @@
 #include <thread>
 #include <vector>
 
+#include "audit_json.h"
+#include "audit_log.h"
+#include "aws_chunked.h"
 #include "crc32.h"
 #include "disk_gate.h"
 #include "extent_alloc.h"
 #include "gf256.h"
+#include "grpc_client.h"
+#include "grpc_server.h"
 #include "http_lite.h"
 #include "journal.h"
 #include "json.h"
+#include "lin_checker.h"
 #include "master_core.h"
+#include "p2p_transport.h"
 #include "raft.h"
 #include "shard_map.h"
+#include "sigv4.h"
+#include "sts.h"
 #include "wal.h"
 
 using namespace dfs;
@@ -992,6 +1001,8 @@ TEST(journal_full_still_commits_tombstones) {
   const std::string d = tmpdir("journal_full");
   BlockJournal j(jt::small(d + "/j", false));
   CHECK(j.recover().empty());
+  // the ring's 3 segments are created (and written out) by the preparer first
+  CHECK(eventually([&] { auto st = j.stats(); return st.segs_total == 3 && st.parts_unready == 0; }, 30));
   std::vector<uint8_t> data(240 << 10, 0x11);
   std::vector<JournalRec> held;
   int n = 0;
@@ -1047,6 +1058,353 @@ TEST(journal_defers_spare_creation_while_writers_are_active) {
   CHECK(eventually([&] { return j.stats().spares_missing == 0; }, 10));  // topped up once idle
   CHECK(j.stats().grow_deferred >= 1 || active_s >= 0.04);
   std::filesystem::remove_all(d);
+}
+
+// ------------------------------------------------------------------ aws-chunked decoding
+namespace ac {
+struct MemSrc {  // the decoder's source over a byte string (the front reads a socket)
+  std::string s;
+  size_t pos = 0;
+  int line(std::string* out, size_t max) {
+    size_t e = s.find("\r\n", pos);
+    if (e == std::string::npos) return -1;
+    if (max == 0 && e != pos) return -1;
+    if (max && e - pos > max) return -1;
+    out->assign(s, pos, e - pos);
+    pos = e + 2;
+    return 1;
+  }
+  int read(uint8_t* dst, uint64_t n) {
+    if (s.size() - pos < n) return -1;
+    std::memcpy(dst, s.data() + pos, n);
+    pos += n;
+    return 1;
+  }
+  int drain() { return 1; }
+};
+sigv4::ChunkChain seed_chain() {
+  sigv4::ChunkChain c;
+  c.key = std::string(32, 'k');
+  c.timestamp = "20260101T000000Z";
+  c.scope = "20260101/us-east-1/s3/aws4_request";
+  c.prev = std::string(64, 'a');
+  return c;
+}
+std::string encode(const std::vector<std::string>& chunks, bool sign) {
+  sigv4::ChunkChain c = seed_chain();
+  std::string out;
+  char hex[32];
+  for (auto& ch : chunks) {
+    std::snprintf(hex, sizeof hex, "%zx", ch.size());
+    out += hex;
+    if (sign) out += ";chunk-signature=" + c.next(ch.data(), ch.size());
+    out += "\r\n" + ch + "\r\n";
+  }
+  out += "0";
+  if (sign) out += ";chunk-signature=" + c.next("", 0);
+  out += "\r\n\r\n";
+  return out;
+}
+}  // namespace ac
+
+// The S3 front's aws-chunked decoder (csrc/aws_chunked.h): framing, the chunk-signature
+// chain, and a mutation fuzz — no mutated signed stream ever decodes, nothing overruns `cap`.
+TEST(aws_chunked_decode_signature_chain_and_fuzz) {
+  std::mt19937 rng(7);
+  std::vector<std::string> chunks;
+  std::string all;
+  for (int i = 0; i < 6; ++i) {
+    std::string c(1 + rng() % 3000, '\0');
+    for (auto& b : c) b = static_cast<char>(rng());
+    chunks.push_back(c);
+    all += c;
+  }
+  std::vector<uint8_t> dst(all.size());
+  for (bool sign : {false, true}) {
+    ac::MemSrc in{ac::encode(chunks, sign)};
+    sigv4::ChunkChain chain = ac::seed_chain();
+    auto r = decode_aws_chunked(in, sign ? &chain : nullptr, dst.data(), dst.size());
+    CHECK(r.rc == 1 && r.bytes == all.size() && std::memcmp(dst.data(), all.data(), all.size()) == 0);
+    CHECK(r.sigs == (sign ? chunks.size() + 1 : 0));
+  }
+  {  // one byte too small a destination
+    ac::MemSrc in{ac::encode(chunks, false)};
+    std::vector<uint8_t> small(all.size() - 1);
+    CHECK(decode_aws_chunked(in, nullptr, small.data(), small.size()).rc == -1);
+  }
+  {  // a signed stream without its final signed empty chunk
+    std::string e = ac::encode(chunks, true);
+    e = e.substr(0, e.rfind("0;chunk-signature="));
+    ac::MemSrc in{e};
+    sigv4::ChunkChain chain = ac::seed_chain();
+    CHECK(decode_aws_chunked(in, &chain, dst.data(), dst.size()).rc != 1);
+  }
+  {  // a huge declared size cannot wrap the bound check
+    ac::MemSrc in{std::string("fffffffffffffff\r\n")};
+    CHECK(decode_aws_chunked(in, nullptr, dst.data(), dst.size()).rc == -1);
+  }
+  const std::string good = ac::encode(chunks, true);
+  int accepted = 0;
+  for (int it = 0; it < 3000; ++it) {
+    std::string m = good;
+    const int edits = 1 + static_cast<int>(rng() % 3);
+    for (int e = 0; e < edits; ++e) {
+      const size_t at = rng() % m.size();
+      switch (rng() % 3) {
+        case 0: m[at] = static_cast<char>(m[at] ^ (1 + rng() % 255)); break;
+        case 1: m.erase(at, 1 + rng() % 8); break;
+        default: m.insert(at, 1, static_cast<char>(rng())); break;
+      }
+      if (m.empty()) m = "x";
+    }
+    ac::MemSrc in{m};
+    sigv4::ChunkChain chain = ac::seed_chain();
+    std::vector<uint8_t> out(all.size() + 64);
+    auto r = decode_aws_chunked(in, &chain, out.data(), out.size());
+    if (r.rc == 1) {
+      ++accepted;  // only possible when the edit left the signed content intact
+      CHECK(r.bytes == all.size() && std::memcmp(out.data(), all.data(), all.size()) == 0);
+    }
+  }
+  CHECK(accepted < 3000);
+}
+
+// ------------------------------------------------------------------ audit log (C56)
+// 8 threads log concurrently into small batches; every accepted record is committed exactly
+// once, in one HMAC chain, and a new writer on the same directory continues that chain.
+TEST(audit_log_concurrent_batches_form_one_chain) {
+  const std::string d = tmpdir("audit");
+  const std::string secret = "audit-secret";
+  auto rec = [](int t, int i) {
+    return std::string("{\"timestamp\":\"2026-10-18T00:00:00Z\",\"timestamp_ms\":") + std::to_string(1790000000000LL + i) +
+           ",\"request_id\":\"r-" + std::to_string(t) + "-" + std::to_string(i) +
+           "\",\"remote_ip\":\"127.0.0.1\",\"user_id\":\"u" + std::to_string(t) +
+           "\",\"role_arn\":null,\"action\":\"s3:PutObject\",\"resource\":\"arn:dfs:s3:::b/k\",\"status_code\":200,"
+           "\"error_code\":null,\"user_agent\":\"ut\",\"duration_ms\":1.5}";
+  };
+  {
+    AuditLog log(d, 30, 7, secret, 100000, 50, true);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 8; ++t)
+      ts.emplace_back([&, t] {
+        for (int i = 0; i < 60; ++i) CHECK(log.log(rec(t, i)));
+      });
+    for (auto& t : ts) t.join();
+    CHECK(log.flush(10000));
+    CHECK(log.committed() == 480 && log.dropped() == 0 && log.flush_errors() == 0);
+    log.close();
+  }
+  std::string head;
+  {
+    AuditLog log(d, 30, 5, secret, 1000, 50, true);
+    for (int i = 0; i < 10; ++i) CHECK(log.log(rec(9, 1000 + i)));
+    CHECK(log.flush(10000));
+    head = log.head();
+    log.close();
+  }
+  // walk the segments: keys increase, previous_hash links, record_hash = HMAC(canonical)
+  std::vector<std::string> segs;
+  for (auto& e : std::filesystem::directory_iterator(d))
+    if (e.path().extension() == ".log") segs.push_back(e.path().string());
+  std::sort(segs.begin(), segs.end());
+  std::string prev;
+  int64_t last_key = -1;
+  int n = 0;
+  for (auto& sp : segs) {
+    FILE* f = std::fopen(sp.c_str(), "r");
+    CHECK(f != nullptr);
+    char* line = nullptr;
+    size_t cap = 0;
+    ssize_t len;
+    while ((len = ::getline(&line, &cap, f)) > 0) {
+      std::string l(line, static_cast<size_t>(len));
+      while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+      if (l.empty()) continue;
+      const size_t tab = l.find('\t');
+      CHECK(tab != std::string::npos);
+      const int64_t key = std::stoll(l.substr(0, tab));
+      CHECK(key >= last_key);  // monotonic key timestamps (audit.rs)
+      last_key = key;
+      Json r = Json::parse(l.substr(tab + 1));
+      CHECK((prev.empty() ? r["previous_hash"].is_null() || r["previous_hash"].str().empty() : r["previous_hash"].str() == prev));
+      CHECK(r["record_hash"].str() == audit::hmac_hex(secret, audit::canonical_json(r, true)));
+      prev = r["record_hash"].str();
+      ++n;
+    }
+    std::free(line);
+    std::fclose(f);
+  }
+  CHECK(n == 490 && prev == head);
+  std::filesystem::remove_all(d);
+}
+
+// ------------------------------------------------------------- socket P2P transport
+// Two ranks, 4 channels per direction: concurrent transfers on every channel land in post
+// order with their bytes; then the receiver drops the pair mid-stream and every pending op on
+// the sender ends (failed or done) instead of hanging; the pair reopens for a new generation.
+int wait_op(P2PTransport& t, P2POp* op, double secs) {  // wait() naps 20 us at most: poll
+  auto end = std::chrono::steady_clock::now() + std::chrono::duration<double>(secs);
+  int r;
+  while ((r = t.wait(op, 1000)) == 0 && std::chrono::steady_clock::now() < end) {
+  }
+  return r;
+}
+
+TEST(socket_transport_four_channels_and_a_dropped_peer) {
+  const std::string ns = "ut" + std::to_string(::getpid());
+  auto a = make_socket_transport(0, ns, 4), b = make_socket_transport(1, ns, 4);
+  CHECK(a && b && a->channels() == 4);
+  auto open_pair = [&](uint64_t gen) {
+    std::string e1, e2;
+    const std::string ta = a->make_token(1, gen, &e1), tb = b->make_token(0, gen, &e2);
+    CHECK(!ta.empty() && !tb.empty());
+    bool ok_a = false, ok_b = false;
+    std::thread th([&] { ok_b = b->open(0, gen, tb, ta, 5000, &e2); });
+    ok_a = a->open(1, gen, ta, tb, 5000, &e1);
+    th.join();
+    CHECK(ok_a && ok_b);
+  };
+  open_pair(1);
+  std::mt19937 rng(3);
+  const int per = 40;
+  std::vector<std::vector<std::string>> sent(4), got(4);
+  std::vector<P2POp> sops, rops;
+  std::vector<std::vector<char>> rbufs;
+  sops.reserve(4 * per);
+  rops.reserve(4 * per);
+  rbufs.reserve(4 * per);
+  for (int i = 0; i < per; ++i)
+    for (int ch = 0; ch < 4; ++ch) {
+      std::string m(1 + rng() % 70000, '\0');
+      for (auto& c : m) c = static_cast<char>(rng());
+      sent[ch].push_back(m);
+    }
+  std::string err;
+  for (int ch = 0; ch < 4; ++ch)
+    for (int i = 0; i < per; ++i) {
+      rbufs.emplace_back(sent[ch][i].size());
+      rops.emplace_back();
+      CHECK(b->post_recv(0, ch, rbufs.back().data(), rbufs.back().size(), &rops.back(), &err));
+    }
+  for (int i = 0; i < per; ++i)
+    for (int ch = 0; ch < 4; ++ch) {
+      sops.emplace_back();
+      CHECK(a->post_send(1, ch, sent[ch][i].data(), sent[ch][i].size(), &sops.back(), &err));
+    }
+  for (auto& op : sops) CHECK(wait_op(*a, &op, 20) == 1);
+  for (auto& op : rops) CHECK(wait_op(*b, &op, 20) == 1);
+  for (int ch = 0; ch < 4; ++ch)
+    for (int i = 0; i < per; ++i) CHECK(std::string(rbufs[ch * per + i].begin(), rbufs[ch * per + i].end()) == sent[ch][i]);
+  for (auto& op : sops) a->release(&op);
+  for (auto& op : rops) b->release(&op);
+  // the peer goes away with sends posted that it never receives
+  std::vector<P2POp> pend(8);
+  std::string big(1 << 20, 'z');
+  for (int i = 0; i < 8; ++i) CHECK(a->post_send(1, i % 4, big.data(), big.size(), &pend[i], &err));
+  b->close(0);
+  for (auto& op : pend) {
+    int r = wait_op(*a, &op, 5);
+    if (r == 0) {  // still queued behind a dead socket: close() must end it
+      a->close(1);
+      r = a->test(&op);
+    }
+    CHECK(r != 0);
+    a->release(&op);
+  }
+  a->close(1);
+  open_pair(2);  // a new generation comes up on both sides
+  P2POp s1, r1;
+  char out[5] = "ping", in[5] = {0};
+  CHECK(b->post_recv(0, 3, in, 4, &r1, &err) && a->post_send(1, 3, out, 4, &s1, &err));
+  CHECK(wait_op(*a, &s1, 5) == 1 && wait_op(*b, &r1, 5) == 1 && std::string(in) == "ping");
+  a->release(&s1);
+  b->release(&r1);
+}
+
+// ------------------------------------------------------------------ checker (C49)
+TEST(linearizability_checker_self_test) {
+  auto fails = lin::self_test();
+  for (auto& f : fails) std::printf("  %s\n", f.c_str());
+  CHECK(fails.empty());
+}
+
+// --------------------------------------------------------------------- OIDC (C15)
+// tokens with unknown kids must not drive one outbound discovery + JWKS fetch each.
+TEST(oidc_unknown_kid_refetch_is_rate_limited) {
+  sts::OidcValidator v("http://127.0.0.1:1", "dfs-client", true);
+  auto tok = [](const std::string& kid) {
+    auto b64 = [](const std::string& s) {
+      static const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+      std::string o;
+      uint32_t val = 0;
+      int bits = -6;
+      for (unsigned char c : s) {
+        val = ((val << 8) | c) & 0xFFFFFFu;  // at most 24 live bits
+        bits += 8;
+        while (bits >= 0) {
+          o.push_back(a[(val >> bits) & 0x3F]);
+          bits -= 6;
+        }
+      }
+      if (bits > -6) o.push_back(a[((val << 8) >> (bits + 8)) & 0x3F]);
+      return o;
+    };
+    return b64("{\"alg\":\"HS256\",\"kid\":\"" + kid + "\"}") + "." + b64("{\"sub\":\"x\"}") + "." + b64("sig");
+  };
+  sts::Claims c;
+  std::string kind, detail;
+  std::vector<std::thread> ts;
+  for (int i = 0; i < 8; ++i)
+    ts.emplace_back([&, i] {
+      sts::Claims cc;
+      std::string k, dd;
+      CHECK(!v.validate(tok("kid-" + std::to_string(i)), &cc, &k, &dd));
+    });
+  for (auto& t : ts) t.join();
+  CHECK(!v.validate(tok("another"), &c, &kind, &detail));
+  CHECK(kind == "internal");  // no JWKS at all
+  CHECK(v.fetches_failed() == 1 && v.fetches_ok() == 0);  // one attempt for 9 unknown kids
+}
+
+// ------------------------------------------------------------------ native gRPC wire
+// The HTTP/2 gRPC server and client (nghttp2): 16 threads x 50 unary calls on pooled
+// connections, payloads up to 1 MiB each way, request ids carried, an error status passed
+// through, and calls to a stopped server failing at the transport instead of hanging.
+TEST(grpc_server_and_client_concurrent_unary_calls) {
+  GrpcServer srv("127.0.0.1", 0, [](const GrpcCall& c) {
+    GrpcReply r;
+    if (c.path == "/t.S/Fail") {
+      r.status = 9;
+      r.message = "Not Leader|x";
+      return r;
+    }
+    r.message.assign(reinterpret_cast<const char*>(c.data()), c.size());
+    r.message += "|" + c.request_id;
+    return r;
+  });
+  std::string err;
+  CHECK(srv.start(&err));
+  const std::string target = "127.0.0.1:" + std::to_string(srv.port());
+  GrpcChannelPool pool(10000);
+  std::atomic<int> ok{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 16; ++t)
+    ts.emplace_back([&, t] {
+      std::mt19937 rng(t);
+      for (int i = 0; i < 50; ++i) {
+        std::string req(rng() % (i % 10 == 0 ? (1 << 20) : 4096), static_cast<char>('a' + t));
+        const std::string rid = "rid-" + std::to_string(t) + "-" + std::to_string(i);
+        GrpcResult r = pool.call(target, "/t.S/Echo", req, rid);
+        ok += r.transport_ok && r.status == 0 && r.message == req + "|" + rid;
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK(ok == 800);
+  GrpcResult f = pool.call(target, "/t.S/Fail", "x", "rid");
+  CHECK(f.transport_ok && f.status == 9 && f.message == "Not Leader|x");
+  srv.stop();
+  GrpcResult dead = pool.call(target, "/t.S/Echo", "x", "rid", 2000);
+  CHECK(!dead.transport_ok || dead.status != 0);
 }
 
 }  // namespace

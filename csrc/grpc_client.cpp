@@ -228,7 +228,12 @@ struct GrpcChannelPool::Conn {
       return true;
     }
     while (k > 0) {
-      ssize_t r = ::writev(fd, iv, k);
+      // sendmsg, not writev: a peer that closed the connection must fail the call with EPIPE,
+      // not raise SIGPIPE in the calling process (the unit tests' dead-server case)
+      msghdr mh{};
+      mh.msg_iov = iv;
+      mh.msg_iovlen = static_cast<size_t>(k);
+      ssize_t r = ::sendmsg(fd, &mh, MSG_NOSIGNAL);
       if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
         int ms = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count());
         pollfd p{fd, POLLOUT, 0};

@@ -703,7 +703,11 @@ bool BlockJournal::place_locked(std::unique_lock<std::mutex>& lk, uint64_t len, 
                                 bool marker) {
   for (;;) {
     SegRef s = order_.empty() || order_.back()->sealed ? nullptr : order_.back();
-    if (!s && marker && free_.empty() && !order_.empty() && !order_.back()->marking) {
+    if (!s && marker && free_.empty() && !order_.empty() && order_.back()->marking) {
+      cv_.wait(lk);  // its sealed header is being flushed: the reserve is usable right after
+      continue;
+    }
+    if (!s && marker && free_.empty() && !order_.empty()) {
       // no active segment: a marker goes into the newest segment's reserve (it retires last,
       // so the marker still outlives every record it cancels); the segment is re-marked later
       SegRef b = order_.back();

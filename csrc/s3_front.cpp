@@ -1,5 +1,6 @@
 // Native S3 front end; design notes in s3_front.h.
 #include "s3_front.h"
+#include "aws_chunked.h"
 #include <unordered_set>
 #include <unordered_map>
 #include <set>
@@ -1328,6 +1329,9 @@ int S3Front::verify_auth(Req& r, std::string* user, Session* sess) {
     const double expires = static_cast<double>(std::stoull(ex));
     if (expires > 604800) return fail("missing_auth", "AuthorizationQueryParametersError");
     if (age > expires) return fail("expired_token");
+    // signed for the future (beyond the clock-skew window): not yet valid, and otherwise a way
+    // to mint URLs that outlive the 7-day cap
+    if (-age / 60.0 > 15.0) return fail("clock_skew");
   } else if (ts_ok && std::abs(age) / 60.0 > 15.0) {  // %Y%m%dT%H%M%SZ within 15 minutes of now
     return fail("clock_skew");
   }
@@ -2408,48 +2412,14 @@ int S3Front::read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint6
   sigv4::ChunkChain* chain =
       cfg_.auth_enabled && r.chain_set && sha && *sha == "STREAMING-AWS4-HMAC-SHA256-PAYLOAD" ? &r.chain : nullptr;
   BodyIn in(c, r.chunked, static_cast<uint64_t>(std::max<int64_t>(r.content_length, 0)), c->io());
-  uint64_t n = 0, sigs = 0;
-  auto done = [&](int rc) {
+  const AwsChunkedResult res = decode_aws_chunked(in, chain, dst, cap);
+  {
     std::lock_guard<std::mutex> g(st_mu_);
-    st_.chunk_sigs += sigs;
-    if (rc < 0 && chain) st_.chunk_sig_failures++;
-    return rc;
-  };
-  bool final_chunk = false;
-  for (;;) {
-    std::string h;
-    int rc = in.line(&h, 4096);
-    if (rc == -1 && !chain && n > 0) break;  // the body ended without its empty chunk (decode_chunked)
-    if (rc != 1) return done(rc);
-    const size_t semi = h.find(';');
-    const std::string hex = trim(h.substr(0, semi));
-    if (hex.size() > 15 || hex.find_first_not_of("0123456789abcdefABCDEF") != std::string::npos) return done(-1);
-    const uint64_t size = hex.empty() ? 0 : std::stoull(hex, nullptr, 16);
-    if (n + size > cap) return done(-1);
-    if ((rc = in.read(dst + n, size)) != 1) return done(rc);
-    if (chain) {
-      std::string sig;
-      if (semi != std::string::npos) {
-        size_t k = h.find("chunk-signature=", semi);
-        if (k != std::string::npos) sig = trim(h.substr(k + 16));
-      }
-      if (!chain->verify(dst + n, size, sig)) return done(-1);
-      ++sigs;
-    }
-    if (size == 0) {
-      final_chunk = true;
-      break;
-    }
-    n += size;
-    std::string crlf;
-    if ((rc = in.line(&crlf, 0)) != 1) return done(rc);
-    if (!crlf.empty()) return done(-1);
+    st_.chunk_sigs += res.sigs;
+    if (res.rc < 0 && chain) st_.chunk_sig_failures++;
   }
-  if (chain && !final_chunk) return done(-1);  // a signed stream ends with its signed empty chunk
-  const int rc = in.drain();  // trailers (x-amz-checksum-*) and the closing CRLF
-  if (rc != 1) return done(rc);
-  *n_out = n;
-  return done(1);
+  if (res.rc == 1) *n_out = res.bytes;
+  return res.rc;
 }
 
 // CreateBucket / HeadBucket (reference handlers.rs:667-722; s3/server.py create_bucket,

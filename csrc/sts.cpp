@@ -11,6 +11,8 @@
 #include <unistd.h>
 
 #include <chrono>
+
+#include <chrono>
 #include <cmath>
 #include <cstring>
 
@@ -155,6 +157,10 @@ OidcValidator::OidcValidator(std::string issuer, std::string client_id, bool all
     : issuer_(std::move(issuer)), client_id_(std::move(client_id)), ca_(std::move(ca)), allow_hs256_(allow_hs256) {}
 
 bool OidcValidator::fetch_jwks(std::string* err) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    last_try_ = now_s();
+  }
   std::string base = issuer_;
   while (!base.empty() && base.back() == '/') base.pop_back();
   std::string body;
@@ -214,8 +220,19 @@ bool OidcValidator::validate(const std::string& token, Claims* out, std::string*
       have = have_ && keys_.count(kid);
     }
     if (!have) {
-      std::string err;
-      (void)fetch_jwks(&err);  // a rotated key: refetch once
+      // a rotated key: refetch, but at most once per kRefetchGapS, and never two at a time
+      std::unique_lock<std::mutex> lk(mu_);
+      if (fetching_) {
+        fetch_cv_.wait_for(lk, std::chrono::seconds(12), [&] { return !fetching_; });
+      } else if (last_try_ == 0 || now_s() - last_try_ >= kRefetchGapS) {
+        fetching_ = true;
+        lk.unlock();
+        std::string err;
+        (void)fetch_jwks(&err);
+        lk.lock();
+        fetching_ = false;
+        fetch_cv_.notify_all();
+      }
     }
     std::lock_guard<std::mutex> g(mu_);
     if (!have_) return bad("internal", "JWKS is not available");

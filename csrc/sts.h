@@ -8,6 +8,7 @@
 //   * token = base64(kid u32 BE || nonce 12 || AES-256-GCM(JSON{role_arn, temp_secret_key,
 //     expiration, claims})).
 #pragma once
+#include <condition_variable>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -32,6 +33,10 @@ bool http_get(const std::string& url, int timeout_ms, const std::string& ca, std
 
 class OidcValidator {
  public:
+  // An unknown kid triggers at most one discovery + JWKS fetch per this many seconds
+  // (concurrent validations share the running one): unauthenticated callers cannot drive
+  // unbounded outbound fetches from the gateway's request threads.
+  static constexpr double kRefetchGapS = 10.0;
   OidcValidator(std::string issuer, std::string client_id, bool allow_hs256, std::string ca = "");
   // Discovery + JWKS; false with *err.
   bool fetch_jwks(std::string* err);
@@ -46,6 +51,9 @@ class OidcValidator {
   std::string issuer_, client_id_, ca_;
   bool allow_hs256_;
   std::mutex mu_;
+  std::condition_variable fetch_cv_;
+  bool fetching_ = false;   // a refetch is running: others wait for it instead of fetching too
+  double last_try_ = 0;     // last fetch attempt (unknown kids refetch at most every kRefetchGapS)
   bool have_ = false;
   std::map<std::string, Json> keys_;  // kid -> JWK
   uint64_t ok_ = 0, failed_ = 0;

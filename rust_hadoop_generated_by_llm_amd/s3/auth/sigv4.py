@@ -184,7 +184,10 @@ def presigned_is_expired(ts: str, expires_secs: int, now: datetime | None = None
     if t is None:
         return True
     now = now or datetime.now(timezone.utc)
-    return (now - t).total_seconds() > expires_secs
+    age = (now - t).total_seconds()
+    # a URL dated more than the 15-minute clock-skew window ahead is not valid yet (and would
+    # otherwise outlive the 7-day cap)
+    return age > expires_secs or -age > 15 * 60
 
 
 class SigningKeyCache:

@@ -111,6 +111,9 @@ def test_presigned_expiry():
     assert not s.presigned_is_expired((now - timedelta(seconds=30)).strftime("%Y%m%dT%H%M%SZ"), 3600, now)
     assert s.presigned_is_expired((now - timedelta(seconds=7200)).strftime("%Y%m%dT%H%M%SZ"), 3600, now)
     assert s.presigned_is_expired("garbage", 3600, now)
+    # dated in the future beyond the 15-minute skew window: not valid yet
+    assert s.presigned_is_expired((now + timedelta(days=2)).strftime("%Y%m%dT%H%M%SZ"), 604800, now)
+    assert not s.presigned_is_expired((now + timedelta(minutes=5)).strftime("%Y%m%dT%H%M%SZ"), 3600, now)
 
 
 def test_signing_key_cache_lru_and_ttl():

@@ -644,6 +644,11 @@ def test_auth_presigned_urls(authgw):
     url = sigv4.generate_presigned_url(g.url, "pre", "file.txt", "GET", "admin", "admin-secret",
                                        expires_secs=604_801)
     assert requests.get(url).status_code == 403
+    # dated beyond the clock-skew window ahead: not valid yet (it would outlive the 7-day cap)
+    fut = datetime.now(timezone.utc) + timedelta(days=30)
+    url = sigv4.generate_presigned_url(g.url, "pre", "file.txt", "GET", "admin", "admin-secret", expires_secs=604_800,
+                                       now=(fut.strftime("%Y%m%d"), fut.strftime("%Y%m%dT%H%M%SZ")))
+    assert requests.get(url).status_code == 403
     url = sigv4.generate_presigned_url(g.url, "pre", "up.txt", "PUT", "admin", "admin-secret", expires_secs=60)
     assert requests.put(url, data=b"uploaded via presign").status_code == 200
     assert signed("GET", g, "/pre/up.txt").content == b"uploaded via presign"
