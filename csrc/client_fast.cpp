@@ -530,6 +530,45 @@ FastClient::Status FastClient::list(const std::string& prefix, std::vector<std::
   return Ok;
 }
 
+FastClient::Status FastClient::list_components(const std::string& prefix, std::set<std::string>* out,
+                                               const std::string& rid_in) {
+  const std::string rid = rid_in.empty() ? new_request_id() : rid_in;
+  RequestScope rs(rid);
+  std::vector<std::string> socks;
+  {
+    std::lock_guard<std::mutex> g(route_mu_);
+    if (have_map_) {
+      for (const auto& shard : map_.shards()) {
+        const auto* peers = map_.peers(shard);
+        if (!peers || peers->empty()) return NotHandled;
+        socks.push_back(local_rpc_name(peers->front()));
+      }
+    } else if (!masters_.empty()) {
+      socks.push_back(local_rpc_name(masters_.front()));
+    }
+  }
+  if (socks.empty()) return NotHandled;
+  pb::ListFilesRequest req;
+  req.path = prefix;
+  req.delimiter = "/";
+  const std::string body = req.str();
+  auto component = [&](const std::string& p) {  // the next path component after `prefix`
+    if (p.compare(0, prefix.size(), prefix) != 0) return;
+    const size_t e = p.find('/', prefix.size());
+    if (e != std::string::npos && e > prefix.size()) out->insert(p.substr(prefix.size(), e - prefix.size()));
+  };
+  for (const auto& sock : socks) {
+    int code = 0;
+    std::string raw;
+    if (!call(sock, "/dfs.MasterService/ListFiles", rid, body, &code, &raw) || code != 0) return NotHandled;
+    pb::ListFilesResponse resp;
+    if (!resp.decode(raw)) return NotHandled;
+    for (const auto& cp : resp.common_prefixes) component(cp);
+    for (const auto& f : resp.files) component(f);  // (a master without the extension lists every path)
+  }
+  return Ok;
+}
+
 FastClient::Status FastClient::stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg,
                                     const std::string& rid_in) {
   const std::string rid = rid_in.empty() ? new_request_id() : rid_in;

@@ -21,6 +21,7 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -99,6 +100,9 @@ class FastClient {
   Status write_slot(const std::string& path, int64_t slot, size_t n, int* replicas, std::string* msg, Times* t,
                     const std::string& rid, const std::map<std::string, std::string>* attrs, const char* etag_attr,
                     std::string* md5_out);
+  // The distinct next path components below `prefix` on every shard (ListFiles with the
+  // delimiter extension: one entry per component from each master, not every path).
+  Status list_components(const std::string& prefix, std::set<std::string>* out, const std::string& rid);
   // GetFileInfo on the path's shard: Ok with *found, or NotHandled (remote/non-leader master).
   Status stat(const std::string& path, bool* found, std::string* meta_pb, std::string* msg, const std::string& rid);
   // read() of a file whose metadata (serialized FileMetadata) the caller already holds.

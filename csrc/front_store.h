@@ -24,6 +24,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -53,6 +54,19 @@ class FrontStore {
   virtual Status rename(const std::string& src, const std::string& dst, std::string* msg, const std::string& rid) = 0;
   virtual Status list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
                       const std::string& rid) = 0;
+  // The distinct next path components below `prefix` (ListBuckets). This default lists every
+  // path; the co-located stores ask the masters for one entry per component instead.
+  virtual Status list_components(const std::string& prefix, std::set<std::string>* out, const std::string& rid) {
+    std::vector<std::pair<std::string, pb::FileMetadata>> files;
+    Status st = list(prefix, &files, rid);
+    if (st != FastClient::Ok) return st;
+    for (auto& f : files) {
+      const size_t e = f.first.find('/', prefix.size());
+      if (f.first.compare(0, prefix.size(), prefix) == 0 && e != std::string::npos && e > prefix.size())
+        out->insert(f.first.substr(prefix.size(), e - prefix.size()));
+    }
+    return FastClient::Ok;
+  }
   // calls a first-choice path declined and a second one served (LocalFirstFrontStore)
   virtual uint64_t fallbacks() const { return 0; }
 };
@@ -88,6 +102,9 @@ class FastFrontStore final : public FrontStore {
   Status list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
               const std::string& rid) override {
     return fc_->list(prefix, out, rid);
+  }
+  Status list_components(const std::string& prefix, std::set<std::string>* out, const std::string& rid) override {
+    return fc_->list_components(prefix, out, rid);
   }
 
  private:
@@ -162,6 +179,12 @@ class LocalFirstFrontStore final : public FrontStore {
   Status list(const std::string& prefix, std::vector<std::pair<std::string, pb::FileMetadata>>* out,
               const std::string& rid) override;
   uint64_t fallbacks() const override { return fallbacks_.load(); }
+  Status list_components(const std::string& prefix, std::set<std::string>* out, const std::string& rid) override {
+    if (fc_->list_components(prefix, out, rid) == FastClient::Ok) return FastClient::Ok;
+    ++fallbacks_;
+    out->clear();
+    return FrontStore::list_components(prefix, out, rid);
+  }
 
  private:
   FastClient* fc_;

@@ -1363,7 +1363,35 @@ int MasterCore::list_files(const std::string& raw, std::string* out) {
   int c;
   if ((c = read_index(out)) != OK) return c;
   pb::ListFilesResponse resp;
-  if (!r.with_metadata) {
+  if (!r.delimiter.empty()) {
+    // one entry per distinct next component: after a prefix is seen, jump past every path
+    // under it (they are contiguous in the ordered index)
+    std::lock_guard<std::mutex> g(mu_);
+    const std::string& pre = r.path;
+    auto it = ordered_.lower_bound(pre);
+    while (it != ordered_.end() && it->compare(0, pre.size(), pre) == 0) {
+      const size_t d = it->find(r.delimiter, pre.size());
+      if (d == std::string::npos) {
+        if (!under_construction_.count(*it)) {
+          resp.files.push_back(*it);
+          if (r.with_metadata) resp.metadata.push_back(files_.at(*it));
+        }
+        ++it;
+        continue;
+      }
+      std::string cp = it->substr(0, d + r.delimiter.size());
+      std::string past = cp;
+      // the smallest string greater than every path that starts with cp
+      while (!past.empty() && static_cast<unsigned char>(past.back()) == 0xff) past.pop_back();
+      if (past.empty()) {
+        resp.common_prefixes.push_back(std::move(cp));
+        break;
+      }
+      past.back() = static_cast<char>(static_cast<unsigned char>(past.back()) + 1);
+      resp.common_prefixes.push_back(std::move(cp));
+      it = ordered_.lower_bound(past);
+    }
+  } else if (!r.with_metadata) {
     resp.files = paths(r.path, true);
   } else {  // one consistent pass: paths and their metadata under the same lock
     std::lock_guard<std::mutex> g(mu_);

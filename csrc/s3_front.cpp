@@ -2569,16 +2569,11 @@ bool S3Front::native_list_buckets(Conn* c, Req& r) {
   std::string user = "anonymous", why;
   Session sess;
   if (!authorize(r, "", q, &user, &sess, &why)) return proxy(c, r, nullptr, 0, why);
-  std::vector<std::pair<std::string, pb::FileMetadata>> files;
-  if (fc_->list("/", &files, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "list");
+  // one entry per bucket from each master (ListFiles with the "/" delimiter walks the ordered
+  // path index bucket to bucket), not every file of the namespace
   std::set<std::string> names;
-  for (auto& f : files) {
-    size_t a = f.first.find_first_not_of('/');
-    if (a == std::string::npos) continue;
-    std::string n = f.first.substr(a, f.first.find('/', a) == std::string::npos ? std::string::npos
-                                                                                 : f.first.find('/', a) - a);
-    if (!n.empty() && n != ".s3_mpu") names.insert(n);
-  }
+  if (fc_->list_components("/", &names, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "list");
+  names.erase(".s3_mpu");
   std::string inner;
   for (auto& n : names) inner += "<Bucket>" + xel("Name", n) + xel("CreationDate", "2025-01-01T00:00:00.000Z") + "</Bucket>";
   const bool ok = respond(c, r, 200, "<ListAllMyBucketsResult><Owner><ID>dfs</ID><DisplayName>dfs</DisplayName></Owner>"

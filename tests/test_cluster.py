@@ -144,6 +144,26 @@ def test_corruption_detected_and_recovered(cluster3):
     c.close()
 
 
+def test_list_files_delimiter_walks_components(cluster3):
+    """ListFiles' delimiter extension (proto field 101): one common prefix per component below
+    the path (what ListBuckets asks for), not every file."""
+    cl = cluster3.client()
+    for p in ("/lsd_b1/x/1", "/lsd_b1/x/2", "/lsd_b1/y", "/lsd_b2/z", "/lsd_top"):
+        cl.create_file_from_buffer(b"d", p)
+    pool = ChannelPool()
+    try:
+        m = cluster3.master_addrs[0]
+        r = pool.call(m, "MasterService", "ListFiles", pb.ListFilesRequest(path="/lsd_b1/", delimiter="/"))
+        assert list(r.common_prefixes) == ["/lsd_b1/x/"] and list(r.files) == ["/lsd_b1/y"]
+        r = pool.call(m, "MasterService", "ListFiles", pb.ListFilesRequest(path="/", delimiter="/"))
+        assert {"/lsd_b1/", "/lsd_b2/"} <= set(r.common_prefixes) and "/lsd_top" in r.files
+        assert not any(f.count("/") > 1 for f in r.files)
+        assert list(r.common_prefixes) == sorted(r.common_prefixes)
+    finally:
+        pool.close()
+        cl.close()
+
+
 def test_safe_mode_blocks_writes(cluster3):
     c = cluster3.client(max_retries=1, initial_backoff_ms=10)
     pool = ChannelPool()
