@@ -96,6 +96,17 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def _die_with_parent():
+    """In the child between fork and exec: SIGKILL when the spawning rank exits (Linux
+    PR_SET_PDEATHSIG; inherited across exec, cleared only by a setuid exec)."""
+    import ctypes
+
+    try:
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGKILL, 0, 0, 0)  # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+
+
 class Procs:
     def __init__(self):
         self.items: list[subprocess.Popen] = []
@@ -106,8 +117,11 @@ class Procs:
 
     def spawn_raw(self, cmd: list[str], log: str, env: dict) -> subprocess.Popen:
         f = open(log, "ab")
+        # own session (stop() signals the whole group), and killed with this rank if the rank
+        # itself dies before its stop() runs (a launcher or a timeout killing the ranks used to
+        # leave masters and chunkservers running on the node)
         p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, env=env, cwd=str(ROOT),
-                             start_new_session=True)
+                             start_new_session=True, preexec_fn=_die_with_parent)
         f.close()
         self.items.append(p)
         self.logs.append(log)
@@ -600,7 +614,7 @@ def main():
             slow_w = [{"ms": round(1e3 * x, 3), "step": st, "op": i,
                        **({k: round(1e3 * v, 3) for k, v in zip(("crc", "create", "write", "md5_wait", "complete", "copy", "acquire"), ph)}
                           if ph else {})} for x, st, i, ph in slow]
-            allr = gather({"vm": vm_delta, "slow_w": slow_w, "roof": roof, "elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
+            allr = gather({"md5": getattr(client._fast, "md5_mode", None), "vm": vm_delta, "slow_w": slow_w, "roof": roof, "elapsed": elapsed, "end_sync": end_sync_s, "loop": t_loop, "syncs": sync_log, "wl": wl, "rl": rl, "wbytes": wbytes,
                            "rbytes": rbytes, "wt": wt,
                            "rt": rt, "cs": stats, "stress": stress, "remote": remote, "vol": vol,
                            "p2p": bool(cs_info.get("rccl", False)), "p2p_transport": cs_info.get("transport", "grpc"),
@@ -694,6 +708,9 @@ def main():
                     "host_cpu_job": allr[0]["job_cpu"],
                     # host cores the whole job kept busy per GB/s of client writes (timed region,
                     # reads included): what an 8-rank node's CPU quota is read against
+                    # how each rank's client hashed its ETags: OpenSSL per message, or the AVX-512
+                    # multi-buffer engine when the rank's CPU budget is small (md5_mb.h)
+                    "etag_md5": sorted({str(r["md5"]) for r in allr}),
                     "cores_per_gb_written": (round(allr[0]["job_cpu"]["cores_used"] / (
                         sum(r["wbytes"] for r in allr) / 1e9 / max(r["wt"] for r in allr)), 3)
                         if allr[0]["job_cpu"] and allr[0]["job_cpu"].get("cores_used") else None),

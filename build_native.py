@@ -138,7 +138,7 @@ def build_tools(objs: list[Path], flags: list[str], clean: bool, headers: list[P
 SANITIZE_SOURCES = ["json.cpp", "json_dump.cpp", "shard_map.cpp", "raft.cpp", "wal.cpp", "crc32.cpp", "gf256.cpp",
                     "disk_gate.cpp", "extent_alloc.cpp", "master_core.cpp", "http_lite.cpp",
                     "journal.cpp", "audit_log.cpp", "lin_checker.cpp", "sts.cpp", "crypto.cpp", "tls.cpp",
-                    "sigv4.cpp", "p2p_socket.cpp", "grpc_server.cpp", "grpc_client.cpp"]
+                    "sigv4.cpp", "p2p_socket.cpp", "grpc_server.cpp", "grpc_client.cpp", "md5_mb.cpp"]
 SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
               "tsan": ["-fsanitize=thread"]}
 

@@ -34,6 +34,7 @@
 #include "crc32.h"
 #include "gf256.h"
 #include "journal.h"
+#include "md5_mb.h"
 
 using namespace dfs;
 using Clock = std::chrono::steady_clock;
@@ -377,6 +378,81 @@ static void pcie_roofline(int device, int threads, int per, size_t n) {
               static_cast<unsigned long long>(fused_w), static_cast<unsigned long long>(fused_r));
 }
 
+// --md5: the ETag hash of a 1 MiB write, OpenSSL on one core against the multi-buffer engine
+// (md5_mb.cpp): one message alone (latency), and `conc` messages in flight at once, each
+// submitter starting its next as soon as its last returns (the benchmark's 10 writers).
+static void md5_bench(int conc, int per) {
+  const size_t n = 1 << 20;
+  std::vector<std::vector<uint8_t>> bufs(conc, std::vector<uint8_t>(n));
+  std::mt19937 rng(5);
+  for (auto& b : bufs)
+    for (auto& x : b) x = static_cast<uint8_t>(rng());
+  auto timed = [&](auto&& fn) {
+    auto t0 = Clock::now();
+    fn();
+    return secs(t0, Clock::now());
+  };
+  // engine: nullptr = OpenSSL on each submitting thread
+  auto run = [&](Md5MultiBuffer* mb, double* one_ms, double* p50, double* cpu_cores) {
+    double best = 1e9;
+    for (int i = 0; i < 10; ++i)
+      best = std::min(best, timed([&] {
+        if (mb) (void)mb->submit(bufs[0].data(), n).get();
+        else (void)md5_hex_scalar(bufs[0].data(), n);
+      }));
+    *one_ms = 1e3 * best;
+    std::vector<double> lat;
+    std::mutex mu;
+    struct timespec c0, c1;
+    ::clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &c0);
+    const double wall = timed([&] {
+      std::vector<std::thread> ts;
+      for (int t = 0; t < conc; ++t)
+        ts.emplace_back([&, t] {
+          std::vector<double> mine;
+          for (int i = 0; i < per; ++i) {
+            auto a = Clock::now();
+            if (mb) (void)mb->submit(bufs[t].data(), n).get();
+            else (void)md5_hex_scalar(bufs[t].data(), n);
+            mine.push_back(secs(a, Clock::now()));
+          }
+          std::lock_guard<std::mutex> g(mu);
+          lat.insert(lat.end(), mine.begin(), mine.end());
+        });
+      for (auto& t : ts) t.join();
+    });
+    ::clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &c1);
+    std::sort(lat.begin(), lat.end());
+    *p50 = 1e3 * lat[lat.size() / 2];
+    *cpu_cores = ((c1.tv_sec - c0.tv_sec) + 1e-9 * (c1.tv_nsec - c0.tv_nsec)) / wall;
+    return conc * per * 1.0 / wall;  // MiB/s
+  };
+  std::printf("{\"md5\": {\"avx512\": %s, \"concurrent\": %d, \"engines\": [", Md5MultiBuffer::available() ? "true" : "false",
+              conc);
+  struct E {
+    const char* name;
+    Md5MultiBuffer::Kind kind;
+    int lanes;
+  };
+  bool first = true;
+  for (const E& e : {E{"openssl", Md5MultiBuffer::Kind::None, 0}, E{"scalar-x1", Md5MultiBuffer::Kind::Scalar, 1},
+                     E{"scalar-x2", Md5MultiBuffer::Kind::Scalar, 2}, E{"scalar-x3", Md5MultiBuffer::Kind::Scalar, 3},
+                     E{"avx512-x16", Md5MultiBuffer::Kind::Avx512, 16}}) {
+    if (e.kind == Md5MultiBuffer::Kind::Avx512 && !Md5MultiBuffer::available()) continue;
+    std::unique_ptr<Md5MultiBuffer> mb;
+    if (e.kind != Md5MultiBuffer::Kind::None) {
+      const int lanes = e.kind == Md5MultiBuffer::Kind::Avx512 ? Md5MultiBuffer::kLanes : e.lanes;
+      mb = std::make_unique<Md5MultiBuffer>((conc + lanes - 1) / lanes, e.kind, e.lanes);
+    }
+    double one = 0, p50 = 0, cores = 0;
+    const double rate = run(mb.get(), &one, &p50, &cores);
+    std::printf("%s\n  {\"engine\": \"%s\", \"one_mib_ms\": %.3f, \"mib_s\": %.0f, \"p50_ms\": %.3f, \"cpu_cores\": %.2f}",
+                first ? "" : ",", e.name, one, rate, p50, cores);
+    first = false;
+  }
+  std::printf("\n]}}\n");
+}
+
 // --roofline: what the volume gives a chunkserver's journal right now — T writers appending
 // 1 MiB block records (header + .meta image + data) to a BlockJournal like the store's
 // (8 parts, 256 MiB segments, written out once before the timed appends), each record
@@ -427,6 +503,16 @@ static void roofline(const std::string& dir, int threads, int per) {
 }
 
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--md5") {
+      int conc = 10, per = 20;
+      for (int j = 1; j + 1 < argc; ++j) {
+        if (std::string(argv[j]) == "--conc") conc = std::atoi(argv[j + 1]);
+        if (std::string(argv[j]) == "--per") per = std::atoi(argv[j + 1]);
+      }
+      md5_bench(std::max(1, conc), std::max(1, per));
+      return 0;
+    }
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--roofline") {
       std::string dir = "/tmp/io_bench_roofline";

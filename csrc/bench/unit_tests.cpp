@@ -42,6 +42,7 @@
 #include "json.h"
 #include "lin_checker.h"
 #include "master_core.h"
+#include "md5_mb.h"
 #include "p2p_transport.h"
 #include "raft.h"
 #include "shard_map.h"
@@ -1405,6 +1406,34 @@ TEST(grpc_server_and_client_concurrent_unary_calls) {
   srv.stop();
   GrpcResult dead = pool.call(target, "/t.S/Echo", "x", "rid", 2000);
   CHECK(!dead.transport_ok || dead.status != 0);
+}
+
+// ------------------------------------------------------------------ multi-buffer MD5
+// The ETag hash of md5_mb.cpp against OpenSSL: every length class (empty, < 56, 56..63 with a
+// second padding block, whole blocks, MiB), 40 messages from 8 submitting threads through 2
+// engines, so lanes join and finish at different rounds.
+TEST(md5_multibuffer_matches_openssl) {
+  std::mt19937 rng(11);
+  std::vector<std::vector<uint8_t>> msgs;
+  for (size_t n : {0, 1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 1000, 4096, 65535, 1 << 20, (1 << 20) + 17})
+    msgs.emplace_back(n);
+  while (msgs.size() < 40) msgs.emplace_back(rng() % 300000);
+  for (auto& m : msgs)
+    for (auto& b : m) b = static_cast<uint8_t>(rng());
+  for (auto kind : {Md5MultiBuffer::Kind::Avx512, Md5MultiBuffer::Kind::Scalar})
+    for (int lanes : {1, 2, 3}) {
+      if (kind == Md5MultiBuffer::Kind::Avx512 && (lanes > 1 || !Md5MultiBuffer::available())) continue;
+      Md5MultiBuffer mb(2, kind, lanes);
+      std::vector<std::future<std::string>> fs(msgs.size());
+      std::vector<std::thread> ts;
+      for (int t = 0; t < 8; ++t)
+        ts.emplace_back([&, t] {
+          for (size_t i = t; i < msgs.size(); i += 8) fs[i] = mb.submit(msgs[i].data(), msgs[i].size());
+        });
+      for (auto& t : ts) t.join();
+      for (size_t i = 0; i < msgs.size(); ++i) CHECK(fs[i].get() == md5_hex_scalar(msgs[i].data(), msgs[i].size()));
+      CHECK(mb.messages() == msgs.size());
+    }
 }
 
 }  // namespace

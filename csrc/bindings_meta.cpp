@@ -1056,6 +1056,7 @@ void bind_meta(py::module_& m) {
            py::arg("hash_threads") = 8)
       .def_property_readonly("ok", &FastClient::ok)
       .def_property_readonly("arena_path", &FastClient::arena_path)
+      .def_property_readonly("md5_mode", &FastClient::md5_mode)
       .def_property_readonly("writes", &FastClient::writes)
       .def_property_readonly("reads", &FastClient::reads)
       .def("set_host_aliases", &FastClient::set_host_aliases)

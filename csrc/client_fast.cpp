@@ -168,6 +168,17 @@ FastClient::FastClient(std::string fastpath_socket, std::string local_chunkserve
        off += static_cast<int64_t>(slot_bytes_))
     free_slots_.push_back(off);
   for (int i = 0; i < std::max(1, hash_threads); ++i) hashers_.emplace_back([this] { hash_loop(); });
+  {
+    // the ETag hashes: AVX-512 lanes under a small CPU budget, else 2 messages interleaved per
+    // scalar thread (DFS_MD5_LANES), enough engines for hash_threads messages in flight
+    const auto kind = Md5MultiBuffer::wanted();
+    const char* ln = std::getenv("DFS_MD5_LANES");
+    const int lanes = ln && *ln ? std::atoi(ln) : 2;
+    if (kind == Md5MultiBuffer::Kind::Avx512)
+      md5mb_ = std::make_unique<Md5MultiBuffer>(std::max(1, (hash_threads + 15) / 16), kind);
+    else if (kind == Md5MultiBuffer::Kind::Scalar)
+      md5mb_ = std::make_unique<Md5MultiBuffer>(std::max(1, (hash_threads + lanes - 1) / lanes), kind, lanes);
+  }
 }
 
 FastClient::~FastClient() {
@@ -346,19 +357,25 @@ FastClient::Status FastClient::write(const std::string& path, const uint8_t* dat
 }
 
 void FastClient::start_hashes(const uint8_t* p, size_t n, bool with_crc, Hashes* h) {
-  auto md5_task = std::make_shared<std::packaged_task<std::string()>>([p, n] { return md5_hex(p, n); });
-  h->md5 = md5_task->get_future();
+  std::shared_ptr<std::packaged_task<std::string()>> md5_task;
+  if (md5mb_) {
+    h->md5 = md5mb_->submit(p, n);  // a lane of the multi-buffer engine
+  } else {
+    md5_task = std::make_shared<std::packaged_task<std::string()>>([p, n] { return md5_hex(p, n); });
+    h->md5 = md5_task->get_future();
+  }
   std::shared_ptr<std::packaged_task<uint32_t()>> crc_task;
   if (with_crc) {
     crc_task = std::make_shared<std::packaged_task<uint32_t()>>([p, n] { return crc32(p, n); });
     h->crc = crc_task->get_future();
   }
+  if (!md5_task && !crc_task) return;
   {
     std::lock_guard<std::mutex> g(q_mu_);
-    queue_.emplace_back([md5_task] { (*md5_task)(); });
+    if (md5_task) queue_.emplace_back([md5_task] { (*md5_task)(); });
     if (crc_task) queue_.emplace_front([crc_task] { (*crc_task)(); });
   }
-  if (crc_task) q_cv_.notify_all();
+  if (md5_task && crc_task) q_cv_.notify_all();
   else q_cv_.notify_one();
 }
 

@@ -29,6 +29,7 @@
 #include "dfs_pb.h"
 #include "grpc_client.h"
 #include "io_pool.h"
+#include "md5_mb.h"
 #include "shard_map.h"
 
 namespace dfs {
@@ -194,6 +195,14 @@ class FastClient {
   std::deque<std::function<void()>> queue_;
   std::vector<std::thread> hashers_;
   bool stop_ = false;
+  // the ETag MD5s on AVX-512 lanes, up to 16 messages per engine thread (md5_mb.h); null:
+  // no AVX-512F (or DFS_MD5_MB=0): the hash workers run OpenSSL, one message each
+  std::unique_ptr<Md5MultiBuffer> md5mb_;
+
+ public:
+  const char* md5_mode() const {
+    return !md5mb_ ? "openssl" : md5mb_->kind() == Md5MultiBuffer::Kind::Avx512 ? "avx512-x16" : md5mb_->lanes() == 3 ? "scalar-x3" : md5mb_->lanes() == 2 ? "scalar-x2" : "scalar-x1";
+  }
 
   std::atomic<uint64_t> writes_{0}, reads_{0}, ec_gpu_{0}, ec_cpu_{0}, ec_degraded_{0};
   std::atomic<uint64_t> ec_dev_writes_{0}, ec_dev_reads_{0}, ec_host_{0};

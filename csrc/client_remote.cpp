@@ -68,6 +68,17 @@ bool not_leader(const std::string& m, std::string* hint) {
 RemoteClient::RemoteClient(int hash_threads, int timeout_ms, std::shared_ptr<TlsContext> tls)
     : pool_(timeout_ms, std::move(tls)) {
   for (int i = 0; i < std::max(1, hash_threads); ++i) hashers_.emplace_back([this] { hash_loop(); });
+  {
+    // the ETag hashes: AVX-512 lanes under a small CPU budget, else 2 messages interleaved per
+    // scalar thread (DFS_MD5_LANES), enough engines for hash_threads messages in flight
+    const auto kind = Md5MultiBuffer::wanted();
+    const char* ln = std::getenv("DFS_MD5_LANES");
+    const int lanes = ln && *ln ? std::atoi(ln) : 2;
+    if (kind == Md5MultiBuffer::Kind::Avx512)
+      md5mb_ = std::make_unique<Md5MultiBuffer>(std::max(1, (hash_threads + 15) / 16), kind);
+    else if (kind == Md5MultiBuffer::Kind::Scalar)
+      md5mb_ = std::make_unique<Md5MultiBuffer>(std::max(1, (hash_threads + lanes - 1) / lanes), kind, lanes);
+  }
 }
 
 RemoteClient::~RemoteClient() {
@@ -179,13 +190,18 @@ FastClient::Status RemoteClient::write_etag(const std::string& path, const uint8
   RequestScope rs(rid);
   TraceRange tr("dfs.remote.write");
   auto clk = Clock::now();
-  auto md5_task = std::make_shared<std::packaged_task<std::string()>>([data, n] { return md5_hex(data, n); });
-  std::future<std::string> md5 = md5_task->get_future();
-  {
-    std::lock_guard<std::mutex> g(q_mu_);
-    queue_.emplace_back([md5_task] { (*md5_task)(); });
+  std::future<std::string> md5;
+  if (md5mb_) {
+    md5 = md5mb_->submit(data, n);  // a lane of the multi-buffer engine (md5_mb.h)
+  } else {
+    auto md5_task = std::make_shared<std::packaged_task<std::string()>>([data, n] { return md5_hex(data, n); });
+    md5 = md5_task->get_future();
+    {
+      std::lock_guard<std::mutex> g(q_mu_);
+      queue_.emplace_back([md5_task] { (*md5_task)(); });
+    }
+    q_cv_.notify_one();
   }
-  q_cv_.notify_one();
   struct Join {  // never return while the worker still reads the caller's buffer
     std::future<std::string>& f;
     ~Join() {

@@ -25,6 +25,7 @@
 #include "client_fast.h"
 #include "dfs_pb.h"
 #include "grpc_client.h"
+#include "md5_mb.h"
 #include "io_pool.h"
 #include "tls.h"
 #include "shard_map.h"
@@ -103,6 +104,7 @@ class RemoteClient {
   std::condition_variable q_cv_;
   std::deque<std::function<void()>> queue_;
   std::vector<std::thread> hashers_;
+  std::unique_ptr<Md5MultiBuffer> md5mb_;  // the ETag MD5s on AVX-512 lanes (null: OpenSSL workers)
   bool stop_ = false;
 
   Status read_ec(const pb::FileMetadata& m, std::string* out, std::string* msg, const std::string& rid, uint64_t offset,
