@@ -348,12 +348,12 @@ def config5(a):
 
 
 def _gateway_kind(cluster, name: str = "s3") -> str:
-    """Which S3 gateway process the launcher started: the native executable, or the Python
-    gateway (S3_NATIVE_GATEWAY=0) with its worker count."""
+    """Which S3 gateway process the launcher started: the native executable, or (an A/B run
+    with S3_NATIVE_GATEWAY=0) the Python gateway model of tests/models with its worker count."""
     pr = next((p for p in cluster.procs if p.name == name), None)
     if pr is not None and pr.info.get("native_gateway"):
         return "; process: dfs_s3_gateway (native executable, no Python)"
-    return f"; process: s3/server.py, {int(os.environ.get('S3_WORKERS', '4'))} workers"
+    return f"; process: tests/models/s3_gateway.py (model), {int(os.environ.get('S3_WORKERS', '4'))} workers"
 
 
 def _front_counters(url: str) -> dict:

@@ -1,7 +1,7 @@
 // Native ChunkServer control loop (C41/C43; reference dfs/chunkserver/src/bin/chunkserver.rs
 // :144-355 for the heartbeat and command dispatch, chunkserver.rs:353-718 for recovery, EC
 // reconstruction and the scrubber). It replaces the Python heartbeat/command/recovery code
-// of chunkserver/server.py + service.py when the native fast path is up:
+// of tests/models/chunkserver_shell.py + chunkserver_service.py when the native fast path is up:
 //
 //   heartbeat thread  every `heartbeat_ms`: FetchShardMap from the config servers (masters =
 //                     every shard's peers, else the static list), then HeartbeatRequest

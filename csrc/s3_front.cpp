@@ -1,5 +1,6 @@
 // Native S3 front end; design notes in s3_front.h.
 #include "s3_front.h"
+#include "audit_json.h"
 #include "aws_chunked.h"
 #include <unordered_set>
 #include <unordered_map>
@@ -222,7 +223,7 @@ bool all_digits(const std::string& s) {
   return true;
 }
 
-// parse_range of s3/server.py: 0 = no (or ignored) range, 1 = [*s, *e], 2 = unsatisfiable,
+// parse_range of tests/models/s3_gateway.py: 0 = no (or ignored) range, 1 = [*s, *e], 2 = unsatisfiable,
 // 3 = a form this path does not decide (handed to Python)
 int parse_range(const std::string* v, uint64_t size, uint64_t* s, uint64_t* e) {
   if (!v || v->compare(0, 6, "bytes=") != 0) return 0;
@@ -631,6 +632,7 @@ bool S3Front::start(std::string* err) {
   lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
   int one = 1;
   ::setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+  if (cfg_.reuse_port) ::setsockopt(lfd_, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
   sockaddr_in a{};
   a.sin_family = AF_INET;
   a.sin_port = htons(static_cast<uint16_t>(cfg_.port));
@@ -923,7 +925,7 @@ bool S3Front::handle(Conn* c, Req& r) {
   const bool plain_path = r.path.size() > 1 && r.path[0] == '/';
   std::map<std::string, std::string> q;
   if (r.raw_path == "/metrics" || r.raw_path == "/health") return proxy(c, r, nullptr, 0, "metrics");
-  if (r.raw_path == "/" && cfg_.backend.empty()) {  // STS at the root (s3/server.py dispatch)
+  if (r.raw_path == "/" && cfg_.backend.empty()) {  // STS at the root (tests/models/s3_gateway.py dispatch)
     std::map<std::string, std::string> sq;
     const std::string* ct = r.get("content-type");
     const bool form = r.method == "POST" && ct && lower(*ct).compare(0, 33, "application/x-www-form-urlencoded") == 0;
@@ -969,10 +971,10 @@ bool S3Front::handle(Conn* c, Req& r) {
   if (reserved_key(key)) return proxy(c, r, nullptr, 0, "route");
   q.erase("x-id");  // SDK operation tag, no meaning to S3 itself
   if (r.method == "POST" && q.size() == 1 && q.count("uploadId") && !r.chunked && r.content_length <= (1 << 20) &&
-      !cfg_.metadata_sidecar && !aws_chunked(r))
+      !aws_chunked(r))
     return native_complete(c, r, bucket, key, q);
   if (r.method == "POST" && q.size() == 1 && q.count("uploads") && q["uploads"].empty() && !r.chunked &&
-      r.content_length <= 0 && !cfg_.metadata_sidecar)
+      r.content_length <= 0)
     return native_initiate(c, r, bucket, key, q);
   if (r.method == "POST" && q.size() == 1 && q.count("delete")) return native_delete_objects(c, r, bucket, q);
   const bool part = q.size() == 2 && q.count("partNumber") && q.count("uploadId");
@@ -992,7 +994,7 @@ bool S3Front::handle(Conn* c, Req& r) {
     const bool sized = dl && all_digits(*dl);
     // Transfer-Encoding: chunked is served for aws-chunked bodies of a stated size (the SDKs'
     // streaming uploads); a plain chunked body of unknown size goes to Python
-    if ((r.chunked && !(aws && sized)) || cfg_.metadata_sidecar || (copy_src && (part || r.content_length > 0 || r.chunked)))
+    if ((r.chunked && !(aws && sized)) || (copy_src && (part || r.content_length > 0 || r.chunked)))
       return proxy(c, r, nullptr, 0, "put-form");
     uint64_t body = static_cast<uint64_t>(r.content_length);
     if (sized) body = r.chunked ? std::stoull(*dl) : std::min<uint64_t>(body, std::stoull(*dl));
@@ -1087,7 +1089,7 @@ bool S3Front::authorize(Req& r, const std::string& bucket, const std::map<std::s
   return true;
 }
 
-// ListObjects / ListObjectsV2 (reference handlers.rs:1536-1697, s3/server.py list_objects):
+// ListObjects / ListObjectsV2 (reference handlers.rs:1536-1697, tests/models/s3_gateway.py list_objects):
 // one ListFiles{with_metadata} per shard over the masters' local sockets, the keys sorted
 // and paged (prefix, delimiter, marker / continuation-token / start-after, max-keys) and
 // the reference XML written here. Buckets that are missing or empty, and objects whose
@@ -1174,12 +1176,23 @@ bool S3Front::native_list(Conn* c, Req& r, const std::string& bucket, std::map<s
     uint64_t size = 0;
     if (info == nullptr) {  // a completed multipart object: its marker's recorded headers
       auto mk = by_path.find(bp + k + "/.s3_mpu_completed");
-      if (mk == by_path.end() || mk->second->attributes.empty()) return proxy(c, r, nullptr, 0, "list-sidecar");
-      const auto& at = mk->second->attributes;
+      if (mk == by_path.end()) return proxy(c, r, nullptr, 0, "list-mpu");
+      std::map<std::string, std::string> side;
+      if (mk->second->attributes.empty() && !read_sidecar(bp + k, r.rid, &side)) return proxy(c, r, nullptr, 0, "list-sidecar");
+      const auto& at = mk->second->attributes.empty() ? side : mk->second->attributes;
       auto e = at.find("ETag");
       etag = e != at.end() ? e->second : "\"000-MPU\"";
       auto sz = at.find("x-dfs-mpu-size");
-      if (sz != at.end() && !sz->second.empty() && all_digits(sz->second)) size = std::stoull(sz->second);
+      if (sz != at.end() && !sz->second.empty() && all_digits(sz->second)) {
+        size = std::stoull(sz->second);
+      } else {  // (a reference-completed object: the sum of its parts)
+        const std::string pre = bp + k + "/";
+        for (int part = 1; part <= 10000; ++part) {  // parts are numbered from 1 (S3)
+          auto it = by_path.find(pre + std::to_string(part));
+          if (it == by_path.end()) break;
+          size += it->second->size;
+        }
+      }
     } else {
       size = info->size;
       if (!info->etag_md5.empty()) etag = "\"" + info->etag_md5 + "\"";
@@ -1188,7 +1201,10 @@ bool S3Front::native_list(Conn* c, Req& r, const std::string& bucket, std::map<s
         auto e = info->attributes.find("ETag");
         if (e != info->attributes.end()) etag = e->second;
       } else if (fileset.count(bp + k + ".meta")) {
-        return proxy(c, r, nullptr, 0, "list-sidecar");
+        std::map<std::string, std::string> side;
+        if (!read_sidecar(bp + k, r.rid, &side)) return proxy(c, r, nullptr, 0, "list-sidecar");
+        auto e = side.find("ETag");
+        if (e != side.end()) etag = e->second;
       }
     }
     contents += "<Contents>" + xel("Key", k) + xel("LastModified", lm) + xel("ETag", etag) +
@@ -1254,7 +1270,7 @@ int S3Front::open_session(const std::string& token, Session* out) {
 }
 
 // SigV4 of the Authorization header, or of a presigned URL's query (reference
-// auth_middleware.rs:19-365, presign.rs; s3/server.py authenticate): the same canonical
+// auth_middleware.rs:19-365, presign.rs; tests/models/s3_gateway.py authenticate): the same canonical
 // request either way — the query without X-Amz-Signature, the signed headers, the payload
 // hash header or UNSIGNED-PAYLOAD. A presigned URL is bounded by X-Amz-Expires (at most 7
 // days) instead of the 15-minute skew. Anything that does not verify is handed over, so
@@ -1419,7 +1435,7 @@ void S3Front::drop_policies() {
   ++cache_epoch_;  // an answer fetched before this call is not cached
 }
 
-// PolicyEpoch.bump of s3/server.py: strictly increasing across the gateway's processes (the
+// PolicyEpoch.bump of tests/models/s3_gateway.py: strictly increasing across the gateway's processes (the
 // system-wide monotonic clock, at least +1).
 void S3Front::policy_changed() {
   if (epoch_map_) {
@@ -1575,7 +1591,7 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
   if (aws) {
     const int rc = read_aws_chunked(c, r, sse ? dst + 12 : dst, n, &n);
     if (rc == 0) return false;
-    if (rc < 0) {  // s3/server.py route(): the body does not decode or its chain is broken
+    if (rc < 0) {  // tests/models/s3_gateway.py route(): the body does not decode or its chain is broken
       r.keep_alive = false;
       s3_error(c, r, 403, "SignatureDoesNotMatch", "aws-chunked signature chain is invalid");
       return false;
@@ -1635,6 +1651,10 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.sse_puts++;
   }
+  if (!part && cfg_.metadata_sidecar) {
+    attrs["ETag"] = "\"" + md5 + "\"";
+    (void)write_sidecar(path, attrs, r.rid);
+  }
   std::string head = "HTTP/1.1 200 OK\r\nETag: \"" + md5 + "\"\r\n" +
                      (sse ? "x-amz-server-side-encryption: AES256\r\n" : "") + "Content-Length: 0\r\n";
   head += r.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
@@ -1651,7 +1671,7 @@ bool S3Front::native_put(Conn* c, Req& r, const std::string& path, bool part) {
 
 namespace {
 
-// _object_headers of s3/server.py; false: a case Python owns (SSE, sidecar metadata)
+// _object_headers of tests/models/s3_gateway.py; false: a case Python owns (SSE, sidecar metadata)
 bool object_headers(const pb::FileMetadata* m, const std::map<std::string, std::string>& attrs, std::string* out,
                     std::string* dek = nullptr) {
   std::string etag = m && !m->etag_md5.empty() ? "\"" + m->etag_md5 + "\"" : kEmptyEtag;
@@ -1678,6 +1698,81 @@ bool object_headers(const pb::FileMetadata* m, const std::map<std::string, std::
 
 }  // namespace
 
+// The reference gateway keeps an object's headers in a sidecar DFS file `<path>.meta` holding
+// {"headers": {...}} (handlers.rs:984-1006 writes it, :1058-1079 reads it). Objects written
+// here carry them as file attributes; a file without attributes (written by the reference's
+// layout) is described by its sidecar. false: the store could not be asked.
+bool S3Front::read_sidecar(const std::string& path, const std::string& rid, std::map<std::string, std::string>* out) {
+  out->clear();
+  bool found = false;
+  std::string meta, msg;
+  if (fc_->stat(path + ".meta", &found, &meta, &msg, rid) != FastClient::Ok) return false;
+  if (!found) return true;
+  pb::FileMetadata m;
+  if (!m.decode(meta)) return true;
+  std::string doc;
+  if (m.size > 0) {
+    int64_t slot = -1;
+    uint64_t n = 0;
+    FastClient::Times t;
+    if (fc_->read_known(meta, &slot, &n, &msg, &t, rid, 0, 0) != FastClient::Ok) return false;
+    doc.assign(reinterpret_cast<const char*>(fc_->slot_ptr(slot)), n);
+    fc_->release(slot);
+  }
+  try {
+    const Json j = Json::parse(doc);
+    const Json& h = j["headers"];
+    if (h.is_object())
+      for (auto& kv : h.fields())
+        if (kv.second.is_string()) (*out)[kv.first] = kv.second.str();
+  } catch (const std::exception&) {
+    out->clear();  // (an unreadable sidecar describes nothing, as in tests/models/s3_gateway.py _read_meta)
+  }
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.sidecar_reads++;
+  return true;
+}
+
+// S3_METADATA_SIDECAR=true: the object's headers are also written as the reference's sidecar,
+// so a bucket the reference gateway must read back carries them where it looks. The JSON is
+// the Python gateway's (json.dumps, compact, ASCII-escaped; ETag first, then x-amz-meta-*,
+// Content-Type and the wrapped DEK); the old sidecar is deleted first, as both gateways do.
+bool S3Front::write_sidecar(const std::string& path, const std::map<std::string, std::string>& attrs,
+                            const std::string& rid) {
+  if (!cfg_.metadata_sidecar) return true;
+  std::string doc = "{\"headers\":{";
+  bool first = true;
+  auto add = [&](const std::string& k, const std::string& v) {
+    if (!first) doc += ",";
+    first = false;
+    audit::put_string(doc, k, true);
+    doc += ":";
+    audit::put_string(doc, v, true);
+  };
+  auto et = attrs.find("ETag");
+  if (et != attrs.end()) add(et->first, et->second);
+  for (auto& kv : attrs)
+    if (kv.first.compare(0, 11, "x-amz-meta-") == 0) add(kv.first, kv.second);
+  for (const char* k : {"Content-Type", "x-amz-sse-encrypted-dek", "x-dfs-mpu-size", "x-dfs-mpu-layout"}) {
+    auto it = attrs.find(k);
+    if (it != attrs.end()) add(it->first, it->second);
+  }
+  doc += "}}";
+  std::string msg;
+  (void)fc_->remove(path + ".meta", &msg, rid);
+  int64_t slot = fc_->acquire_slot(std::max<size_t>(doc.size(), 1));
+  if (slot < 0) return false;
+  std::memcpy(fc_->slot_mut(slot), doc.data(), doc.size());
+  FastClient::Times t;
+  std::string md5;
+  int reps = 0;
+  auto st = fc_->write_slot(path + ".meta", slot, doc.size(), &reps, &msg, &t, rid, nullptr, nullptr, &md5);
+  fc_->release(slot);
+  std::lock_guard<std::mutex> g(st_mu_);
+  st_.sidecar_writes++;
+  return st == FastClient::Ok;
+}
+
 bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   TraceRange tr(head ? "dfs.s3.head" : "dfs.s3.get");
   bool found = false;
@@ -1687,7 +1782,7 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   if (fc_->stat(path, &found, &meta, &msg, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "stat");
   const auto t1 = SC::now();
   if (!found) {
-    // a completed multipart object, a "directory" probe, or NoSuchKey (s3/server.py
+    // a completed multipart object, a "directory" probe, or NoSuchKey (tests/models/s3_gateway.py
     // get_object / head_object)
     std::string mm;
     if (fc_->stat(path + "/.s3_mpu_completed", &found, &mm, &msg, r.rid) != FastClient::Ok)
@@ -1696,7 +1791,11 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
     if (found) {
       pb::FileMetadata mk;
       std::string hdrs;
-      if (!mk.decode(mm) || !object_headers(nullptr, mk.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
+      std::map<std::string, std::string> side;
+      if (!mk.decode(mm)) return proxy(c, r, nullptr, 0, "attrs");
+      if (mk.attributes.empty() && !read_sidecar(path, r.rid, &side)) return proxy(c, r, nullptr, 0, "sidecar");
+      if (!object_headers(nullptr, mk.attributes.empty() ? side : mk.attributes, &hdrs))
+        return proxy(c, r, nullptr, 0, "attrs");
       const size_t lm = hdrs.find("Last-Modified: ");
       hdrs.replace(lm, hdrs.find("\r\n", lm) - lm,
                    "Last-Modified: " + http_date(static_cast<uint64_t>(now_s() * 1000)));  // formatdate(): now
@@ -1723,7 +1822,9 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
   pb::FileMetadata m;
   if (!m.decode(meta)) return proxy(c, r, nullptr, 0, "decode");
   std::string hdrs, dek;
-  if (m.attributes.empty() || !object_headers(&m, m.attributes, &hdrs, &dek)) return proxy(c, r, nullptr, 0, "attrs");
+  std::map<std::string, std::string> side;
+  if (m.attributes.empty() && !read_sidecar(path, r.rid, &side)) return proxy(c, r, nullptr, 0, "sidecar");
+  if (!object_headers(&m, m.attributes.empty() ? side : m.attributes, &hdrs, &dek)) return proxy(c, r, nullptr, 0, "attrs");
   if (!dek.empty() && cfg_.sse_kek.size() != 32) return proxy(c, r, nullptr, 0, "sse");
   const std::string ka = r.keep_alive ? "Connection: keep-alive\r\n" : "Connection: close\r\n";
   if (!dek.empty() && !head) return sse_get(c, r, meta, m.size, hdrs, dek);
@@ -1896,7 +1997,7 @@ bool parse_complete_body(const std::string& b, std::vector<std::pair<int64_t, st
 
 }  // namespace
 
-// CompleteMultipartUpload (reference handlers.rs:322-432, s3/server.py complete_mpu): the
+// CompleteMultipartUpload (reference handlers.rs:322-432, tests/models/s3_gateway.py complete_mpu): the
 // parts listed with their metadata in one ListFiles, validated against the request, the
 // object's ETag md5(concat(md5s))-N, the completion marker written with the layout, and the
 // parts renamed under the object in parallel (each rename one Raft entry, or the master's
@@ -2026,6 +2127,7 @@ bool S3Front::native_complete(Conn* c, Req& r, const std::string& bucket, const 
     auto st = fc_->write_slot(dest + "/.s3_mpu_completed", slot, 0, &reps, &msg, &t, r.rid, &attrs, nullptr, &md5);
     fc_->release(slot);
     if (st != FastClient::Ok) return internal("Failed to create completion marker: " + msg);
+    (void)write_sidecar(dest, attrs, r.rid);
   }
   // the parts move under the object concurrently (independent files, independent Raft entries)
   std::vector<std::future<std::string>> futs;
@@ -2131,12 +2233,25 @@ bool S3Front::native_mpu_get(Conn* c, Req& r, const std::string& path, const std
   TraceRange tr("dfs.s3.mpu_get");
   pb::FileMetadata mk;
   if (!mk.decode(marker_meta)) return proxy(c, r, nullptr, 0, "decode");
-  auto lay = mk.attributes.find("x-dfs-mpu-layout");
-  if (lay == mk.attributes.end()) return proxy(c, r, nullptr, 0, "mpu-layout");
   std::vector<std::pair<uint64_t, uint64_t>> parts;  // (number, size)
-  if (!parse_layout(lay->second, &parts)) return proxy(c, r, nullptr, 0, "mpu-layout");
+  auto lay = mk.attributes.find("x-dfs-mpu-layout");
+  if (lay != mk.attributes.end()) {
+    if (!parse_layout(lay->second, &parts)) return proxy(c, r, nullptr, 0, "mpu-layout");
+  } else {
+    // completed by the reference's gateway (no recorded layout): the parts are the numbered
+    // files under the object, in number order (handlers.rs:1088-1176)
+    std::vector<std::pair<std::string, pb::FileMetadata>> files;
+    if (fc_->list(path + "/", &files, r.rid) != FastClient::Ok) return proxy(c, r, nullptr, 0, "mpu-layout");
+    for (auto& f : files) {
+      const std::string tail = f.first.substr(path.size() + 1);
+      if (!tail.empty() && tail.size() <= 9 && all_digits(tail)) parts.emplace_back(std::stoull(tail), f.second.size);
+    }
+    std::sort(parts.begin(), parts.end());
+  }
+  std::map<std::string, std::string> side;
+  if (mk.attributes.empty() && !read_sidecar(path, r.rid, &side)) return proxy(c, r, nullptr, 0, "sidecar");
   std::string hdrs;
-  if (!object_headers(nullptr, mk.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
+  if (!object_headers(nullptr, mk.attributes.empty() ? side : mk.attributes, &hdrs)) return proxy(c, r, nullptr, 0, "attrs");
   uint64_t total = 0;
   for (auto& p : parts) total += p.second;
   uint64_t s = 0, e = total ? total - 1 : 0;
@@ -2422,7 +2537,7 @@ int S3Front::read_aws_chunked(Conn* c, Req& r, uint8_t* dst, uint64_t cap, uint6
   return res.rc;
 }
 
-// CreateBucket / HeadBucket (reference handlers.rs:667-722; s3/server.py create_bucket,
+// CreateBucket / HeadBucket (reference handlers.rs:667-722; tests/models/s3_gateway.py create_bucket,
 // head_bucket): the bucket is its marker file /<bucket>/.s3keep. A CreateBucketConfiguration
 // body is read and ignored, as the gateway does.
 bool S3Front::native_bucket(Conn* c, Req& r, const std::string& bucket, std::map<std::string, std::string>& q) {
@@ -2455,7 +2570,7 @@ bool S3Front::native_bucket(Conn* c, Req& r, const std::string& bucket, std::map
     return st;
   };
   if (q.count("policy")) {
-    // Get/Put/DeleteBucketPolicy (reference handlers.rs bucket policy; s3/server.py)
+    // Get/Put/DeleteBucketPolicy (reference handlers.rs bucket policy; tests/models/s3_gateway.py)
     if (r.method == "GET") {
       bool found = false;
       std::string meta, doc;
@@ -2561,7 +2676,7 @@ done:
   return ok;
 }
 
-// ListBuckets (reference handlers.rs list_buckets; s3/server.py list_buckets): the first path
+// ListBuckets (reference handlers.rs list_buckets; tests/models/s3_gateway.py list_buckets): the first path
 // component of every file in the namespace, the multipart staging root left out.
 bool S3Front::native_list_buckets(Conn* c, Req& r) {
   TraceRange tr("dfs.s3.list_buckets");
@@ -2582,7 +2697,7 @@ bool S3Front::native_list_buckets(Conn* c, Req& r) {
   return ok;
 }
 
-// DeleteObject (reference handlers.rs delete_object; s3/server.py delete_object): the object
+// DeleteObject (reference handlers.rs delete_object; tests/models/s3_gateway.py delete_object): the object
 // file, every file of a multipart object under "<key>/", and the sidecar "<key>.meta"; 204
 // whether or not anything existed. The three lookups go out together; a master that cannot
 // be reached here hands the (idempotent) request to Python.
@@ -2615,7 +2730,7 @@ bool S3Front::native_delete(Conn* c, Req& r, const std::string& path) {
   return respond(c, r, 204, "");
 }
 
-// AbortMultipartUpload (reference handlers.rs:450-470; s3/server.py abort_mpu): the upload's
+// AbortMultipartUpload (reference handlers.rs:450-470; tests/models/s3_gateway.py abort_mpu): the upload's
 // directory /.s3_mpu/<id>/ emptied; 204 whether or not it existed.
 bool S3Front::native_abort(Conn* c, Req& r, const std::string& upload_id) {
   TraceRange tr("dfs.s3.mpu_abort");
@@ -2634,7 +2749,7 @@ bool S3Front::native_abort(Conn* c, Req& r, const std::string& upload_id) {
   return respond(c, r, 204, "");
 }
 
-// DeleteObjects (reference handlers.rs:1102-1180; s3/server.py delete_objects): the
+// DeleteObjects (reference handlers.rs:1102-1180; tests/models/s3_gateway.py delete_objects): the
 // <Delete><Object><Key>..</Key></Object>..<Quiet/></Delete> body parsed here, the keys removed
 // 16 at a time, a missing key reported as deleted, the DeleteResult written here.
 bool S3Front::native_delete_objects(Conn* c, Req& r, const std::string& bucket,
@@ -2708,7 +2823,7 @@ bool S3Front::native_delete_objects(Conn* c, Req& r, const std::string& bucket,
   return ok;
 }
 
-// CopyObject (reference handlers.rs:1182-1290; s3/server.py copy_object): the source — a plain
+// CopyObject (reference handlers.rs:1182-1290; tests/models/s3_gateway.py copy_object): the source — a plain
 // object, or a completed multipart one whose parts are read into one slot in parallel — is
 // decrypted in place when SSE wrapped it, re-encrypted under a fresh DEK when the gateway is
 // SSE, and written to the destination from the same slot with the source's (COPY) or the
@@ -2742,8 +2857,9 @@ bool S3Front::native_copy(Conn* c, Req& r, const std::string& dest) {
   bool at12 = false;  // the plaintext sits after a 12-byte nonce (a decrypted SSE source)
   if (found) {
     pb::FileMetadata m;
-    if (!m.decode(meta) || m.attributes.empty()) return proxy(c, r, nullptr, 0, "copy-attrs");
-    src_attrs = m.attributes;
+    if (!m.decode(meta)) return proxy(c, r, nullptr, 0, "copy-attrs");
+    if (m.attributes.empty() && !read_sidecar(src, r.rid, &src_attrs)) return proxy(c, r, nullptr, 0, "copy-attrs");
+    if (!m.attributes.empty()) src_attrs = m.attributes;
     auto dk = src_attrs.find("x-amz-sse-encrypted-dek");
     const bool enc = dk != src_attrs.end();
     if (enc && !sse) return proxy(c, r, nullptr, 0, "sse");
@@ -2779,8 +2895,9 @@ bool S3Front::native_copy(Conn* c, Req& r, const std::string& dest) {
     if (fc_->stat(src + "/.s3_mpu_completed", &found, &mm, &msg, r.rid) != FastClient::Ok || !found)
       return proxy(c, r, nullptr, 0, "copy-missing");  // NoSuchKey
     pb::FileMetadata mk;
-    if (!mk.decode(mm) || mk.attributes.empty()) return proxy(c, r, nullptr, 0, "copy-attrs");
-    src_attrs = mk.attributes;
+    if (!mk.decode(mm)) return proxy(c, r, nullptr, 0, "copy-attrs");
+    if (mk.attributes.empty() && !read_sidecar(src, r.rid, &src_attrs)) return proxy(c, r, nullptr, 0, "copy-attrs");
+    if (!mk.attributes.empty()) src_attrs = mk.attributes;
     auto lay = src_attrs.find("x-dfs-mpu-layout");
     std::vector<std::pair<uint64_t, uint64_t>> parts;
     if (src_attrs.count("x-amz-sse-encrypted-dek") || lay == src_attrs.end() || !parse_layout(lay->second, &parts))
@@ -2848,6 +2965,7 @@ bool S3Front::native_copy(Conn* c, Req& r, const std::string& dest) {
       st = fc_->write_slot(dest, slot, stored, &reps, &msg, &t, r.rid, &attrs, nullptr, &md5w);
   }
   if (st != FastClient::Ok) return proxy(c, r, nullptr, 0, "copy-fallback");  // the copy again, in Python
+  (void)write_sidecar(dest, attrs, r.rid);
   {
     std::lock_guard<std::mutex> g(st_mu_);
     st_.copies++;
@@ -2988,7 +3106,7 @@ bool S3Front::standalone(Conn* c, Req& r, const uint8_t* body, uint64_t n, const
                   r.raw_path);
 }
 
-// AssumeRoleWithWebIdentity (reference sts_handler.rs:65-395; s3/server.py handle_sts): the
+// AssumeRoleWithWebIdentity (reference sts_handler.rs:65-395; tests/models/s3_gateway.py handle_sts): the
 // web identity token validated against the OIDC issuer's JWKS, the role's trust policy
 // evaluated on its claims, and a session token sealed with the STS key.
 bool S3Front::native_sts(Conn* c, Req& r, std::map<std::string, std::string>& q) {
@@ -3235,7 +3353,7 @@ std::string S3Front::native_metrics() {
     o += std::string("s3_native_get_phase_seconds_total{phase=\"") + kv.first + "\"} " +
          std::to_string(kv.second / 1e6) + "\n";
   o += "# TYPE s3_native_get_timed_total counter\ns3_native_get_timed_total " + std::to_string(s.get_timed) + "\n";
-  if (cfg_.backend.empty()) {  // no Python workers: the IAM metrics they would export (s3/server.py)
+  if (cfg_.backend.empty()) {  // no Python workers: the IAM metrics they would export (tests/models/s3_gateway.py)
     auto split = [](const std::string& k) {
       size_t b = k.find('|');
       return std::make_pair(k.substr(0, b), b == std::string::npos ? std::string() : k.substr(b + 1));

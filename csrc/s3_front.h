@@ -21,7 +21,7 @@
 //   presigned URLs          -> query-string SigV4 (X-Amz-Credential/-Signature/-Expires).
 // Everything else — bucket create/delete, policies, STS, errors this path does not model, any
 // case it does not own — is handed, unchanged, to the Python gateway (aiohttp on a private
-// UNIX socket, s3/server.py), which keeps the reference semantics.
+// UNIX socket, tests/models/s3_gateway.py), which keeps the reference semantics.
 // Signed requests are verified here with csrc/sigv4.cpp (static credentials); anything
 // that does not verify is handed over too, so Python produces the exact error and audit
 // record. Native requests of an authenticated gateway send their audit record to the
@@ -66,6 +66,9 @@ struct S3FrontConfig {
   bool sse_enabled = false;  // SSE-S3: objects are stored encrypted
   std::string sse_kek;       // the 32-byte KEK (SSE_MASTER_KEY): encryption here; empty: Python does it
   bool metadata_sidecar = false;
+  // several gateway processes on one port (S3_WORKERS > 1): the listening socket is bound with
+  // SO_REUSEPORT and the kernel spreads the connections over the processes
+  bool reuse_port = false;
   // 8-byte shared counter the gateway's workers bump on every PutBucketPolicy /
   // DeleteBucketPolicy ("" = none): a change empties the front's policy cache at once
   std::string policy_epoch_path;
@@ -96,6 +99,7 @@ struct S3FrontStats {
   uint64_t tls_handshakes = 0, tls_failures = 0, sse_puts = 0, sse_gets = 0, iam_native = 0, lists = 0, mpu_completes = 0, mpu_initiates = 0;
   uint64_t deletes = 0, multi_deletes = 0, deleted_keys = 0, mpu_aborts = 0, copies = 0, copy_bytes = 0;
   uint64_t chunked_puts = 0, chunk_sigs = 0, chunk_sig_failures = 0, presigned = 0, bucket_ops = 0;
+  uint64_t sidecar_reads = 0, sidecar_writes = 0;  // the reference's <key>.meta files
   // a gateway without Python workers: the IAM metrics the workers would export
   std::map<std::string, uint64_t> auth_results;  // "success|none", "failure|<error_type>"
   std::map<std::string, uint64_t> sts_results;   // "success|none", "failure|<code>"
@@ -129,6 +133,10 @@ class S3Front {
   bool proxy(Conn* c, Req& r, const uint8_t* body, uint64_t body_len, const std::string& why);
   bool native_put(Conn* c, Req& r, const std::string& path, bool part);
   bool native_get(Conn* c, Req& r, const std::string& path, bool head);
+  // the reference's sidecar `<path>.meta` ({"headers": {...}}): read for objects without
+  // attributes; written too with S3_METADATA_SIDECAR=true (false: the store failed)
+  bool read_sidecar(const std::string& path, const std::string& rid, std::map<std::string, std::string>* out);
+  bool write_sidecar(const std::string& path, const std::map<std::string, std::string>& attrs, const std::string& rid);
   bool native_mpu_get(Conn* c, Req& r, const std::string& path, const std::string& marker_meta);
   bool sse_get(Conn* c, Req& r, const std::string& meta, uint64_t size, const std::string& hdrs,
                const std::string& dek_b64);
@@ -162,7 +170,7 @@ class S3Front {
                 const std::string& resource = "");
   int verify_auth(Req& r, std::string* user, Session* sess);  // 1 ok, 0 hand over
   // A front without a Python backend answers what it would hand over: the auth error, the
-  // S3 error or the STS exchange, as s3/server.py does.
+  // S3 error or the STS exchange, as tests/models/s3_gateway.py does.
   bool standalone(Conn* c, Req& r, const uint8_t* body, uint64_t n, const std::string& why);
   bool auth_error(Conn* c, Req& r);
   bool native_sts(Conn* c, Req& r, std::map<std::string, std::string>& q);

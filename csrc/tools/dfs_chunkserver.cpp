@@ -2,7 +2,7 @@
 // dfs/chunkserver/src/bin/chunkserver.rs:74-375 for the process, chunkserver.rs:721-1088 for
 // the service).
 //
-// Everything the Python shell (chunkserver/server.py + service.py) used to host runs here in
+// Everything the Python shell (tests/models/chunkserver_shell.py + chunkserver_service.py) used to host runs here in
 // C++, so no interpreter lives in a chunkserver process:
 //   * the HBM chunk store on GPU --gpu (the host store with --gpu -1), its block journal,
 //     exporter and scrubber (chunk_store.cpp);
@@ -19,7 +19,7 @@
 //     journal-resident block out as <id> + <id>.meta now), /compact, and /debug/* with
 //     DFS_DEBUG_ENDPOINTS=1.
 //
-// Flags are those of chunkserver/server.py (the reference's spelling plus the MI355X
+// Flags are those of tests/models/chunkserver_shell.py (the reference's spelling plus the MI355X
 // additions), so the launcher, bench.py, the helm chart and the tests start either process
 // with the same command line.
 #include <hip/hip_runtime.h>
@@ -108,7 +108,7 @@ std::string read_file(const std::string& path) {
 }
 
 // Publish our advertised address and fast-path socket for our rank, then wait for every
-// rank's (chunkserver/server.py rendezvous_ranks: the same files, so mixed shells still meet).
+// rank's (tests/models/chunkserver_shell.py rendezvous_ranks: the same files, so mixed shells still meet).
 bool rendezvous(const std::string& dir, int rank, int world, const std::string& addr, const std::string& fp_name,
                 double timeout_s, std::map<std::string, int>* ranks, std::map<std::string, std::string>* names) {
   ::mkdir(dir.c_str(), 0755);

@@ -10,17 +10,27 @@
 // NoSuchKey / NoSuchBucket / NoSuchUpload / MalformedXML ...); /health and /metrics. Audit
 // records go to the native hash-chained writer (csrc/audit_log.cpp) in this process.
 //
-// Configuration is the Python gateway's environment (s3/server.py S3Config): MASTER_ADDR,
+// Configuration is the Python gateway's environment (tests/models/s3_gateway.py S3Config): MASTER_ADDR,
 // CONFIG_SERVERS, SHARD_CONFIG, LOCAL_CHUNKSERVER, CA_CERT, DOMAIN_NAME, PORT, TLS_CERT /
 // TLS_KEY, S3_AUTH_ENABLED, S3_ACCESS_KEY / S3_SECRET_KEY, S3_REGION, S3_REQUIRE_TLS,
 // S3_ALLOW_UNSIGNED_PAYLOAD, OIDC_ISSUER_URL / OIDC_CLIENT_ID / OIDC_ALLOW_HS256,
 // STS_SIGNING_KEY, IAM_CONFIG_PATH, SSE_MASTER_KEY, AUDIT_LOG_* / AUDIT_HMAC_SECRET; plus
 // S3_FRONT_THREADS, S3_FRONT_SLOTS and S3_FRONT_SLOT_MB (the largest single PUT). Flags:
-// --port, --host (--workers is accepted and ignored: one process, S3_FRONT_THREADS threads).
-// S3_METADATA_SIDECAR=true (reference sidecar files) is served by the Python gateway only; the
-// launcher starts that one for it.
+// --port, --host, --workers (or S3_WORKERS). S3_METADATA_SIDECAR=true also writes the
+// reference's `<key>.meta` sidecar files (objects without attributes are always described by
+// theirs).
+//
+// S3_WORKERS=N > 1: this process (worker 0) owns the audit hash chain and the policy epoch page
+// and starts N-1 copies of itself on the same port (SO_REUSEPORT: the kernel spreads the
+// connections). The copies send their audit records to worker 0's ingest socket as datagrams,
+// so one writer keeps one chain, and share its epoch page, so a bucket-policy change made
+// through any worker reaches all of them. They exit with worker 0 (PR_SET_PDEATHSIG).
+#include <signal.h>
+#include <spawn.h>
+#include <sys/prctl.h>
 #include <sys/socket.h>
 #include <sys/un.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -44,6 +54,8 @@
 #include "s3_front.h"
 #include "shard_map.h"
 #include "tls.h"
+
+extern char** environ;
 
 using namespace dfs;
 using dfs::shell::log;
@@ -133,12 +145,16 @@ bool parse_hex32(const std::string& hex, std::string* out) {
 int main(int argc, char** argv) {
   std::string host = "0.0.0.0";
   int port = std::atoi(env("PORT", "9000").c_str());
+  int workers = std::max(1, std::atoi(env("S3_WORKERS", "1").c_str()));
+  // a copy started by worker 0: its private directory (audit ingest socket, policy epoch page)
+  const std::string parent_dir = env("DFS_S3_WORKER_OF");
+  if (!parent_dir.empty()) ::prctl(PR_SET_PDEATHSIG, SIGTERM);
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto val = [&]() { return i + 1 < argc ? std::string(argv[++i]) : std::string(); };
     if (a == "--port") port = std::atoi(val().c_str());
     else if (a == "--host") host = val();
-    else if (a == "--workers") (void)val();
+    else if (a == "--workers") workers = std::max(1, std::atoi(val().c_str()));
     else if (a == "-h" || a == "--help") {
       std::printf("usage: dfs_s3_gateway [--port PORT] [--host HOST] [--workers N]\n"
                   "configuration from the environment (see the header of csrc/tools/dfs_s3_gateway.cpp)\n");
@@ -146,11 +162,9 @@ int main(int argc, char** argv) {
     }
   }
   shell::block_stop_signals();
-  if (env("S3_METADATA_SIDECAR") == "true") {
-    log(kError, kLog, "S3_METADATA_SIDECAR=true is served by the Python gateway (s3/server.py)");
-    return 2;
-  }
   S3FrontConfig cfg;
+  cfg.metadata_sidecar = env("S3_METADATA_SIDECAR") == "true";
+  cfg.reuse_port = workers > 1 || !parent_dir.empty();
   cfg.host = host;
   cfg.port = port;
   cfg.backend = "";  // no Python workers: every request is answered here
@@ -188,13 +202,17 @@ int main(int argc, char** argv) {
   cfg.oidc_allow_hs256 = env("OIDC_ALLOW_HS256") == "true";
   cfg.oidc_ca = env("OIDC_CA_CERT");
 
-  // private directory: the policy epoch page and the audit ingest socket
+  // private directory: the policy epoch page and the audit ingest socket (worker 0's, shared
+  // by the copies it starts)
   char tmpl[] = "/tmp/s3gw-XXXXXX";
-  const std::string priv = ::mkdtemp(tmpl) ? tmpl : "/tmp";
+  const std::string priv = !parent_dir.empty() ? parent_dir : ::mkdtemp(tmpl) ? tmpl : "/tmp";
   cfg.policy_epoch_path = priv + "/policy_epoch";
   std::unique_ptr<AuditLog> audit;
   int ingest_fd = -1;
-  if (env("AUDIT_LOG_ENABLED", "true") == "true") {
+  if (!parent_dir.empty()) {
+    if (cfg.auth_enabled && env("AUDIT_LOG_ENABLED", "true") == "true" && env("AUDIT_HMAC_SECRET").size() >= 16)
+      cfg.audit_socket = priv + "/ingest.sock";
+  } else if (env("AUDIT_LOG_ENABLED", "true") == "true") {
     const std::string secret = env("AUDIT_HMAC_SECRET");
     if (secret.size() >= 16) {
       audit = std::make_unique<AuditLog>(env("AUDIT_LOG_DIR", "/tmp/s3_audit_log"),
@@ -292,15 +310,52 @@ int main(int argc, char** argv) {
   }
   log(kInfo, kLog, "S3 gateway on %s:%d (native process, auth=%d, sse=%d, audit=%d, %s)", host.c_str(), front->port(),
       cfg.auth_enabled, cfg.sse_enabled, audit != nullptr, fast ? "co-located: shared memory" : "remote: gRPC");
+  // worker 0 starts the others on the port it bound (an ephemeral --port 0 included)
+  std::vector<pid_t> kids;
+  if (parent_dir.empty() && workers > 1) {
+    char self[4096];
+    const ssize_t sl = ::readlink("/proc/self/exe", self, sizeof self - 1);
+    if (sl > 0) {
+      self[sl] = 0;
+      std::vector<std::string> envs;
+      for (char** e = environ; *e; ++e) {
+        const std::string kv = *e;
+        if (kv.compare(0, 15, "DFS_READY_FILE=") != 0 && kv.compare(0, 17, "DFS_S3_WORKER_OF=") != 0) envs.push_back(kv);
+      }
+      envs.push_back("DFS_S3_WORKER_OF=" + priv);
+      std::vector<char*> envp;
+      for (auto& kv : envs) envp.push_back(const_cast<char*>(kv.c_str()));
+      envp.push_back(nullptr);
+      const std::string ps = std::to_string(front->port());
+      for (int w = 1; w < workers; ++w) {
+        std::vector<std::string> args = {self, "--port", ps, "--host", host, "--workers", "1"};
+        std::vector<char*> argp;
+        for (auto& s : args) argp.push_back(const_cast<char*>(s.c_str()));
+        argp.push_back(nullptr);
+        pid_t pid = -1;
+        if (::posix_spawn(&pid, self, nullptr, nullptr, argp.data(), envp.data()) == 0) kids.push_back(pid);
+        else log(kError, kLog, "starting gateway worker %d: %s", w, std::strerror(errno));
+      }
+    }
+  }
+  if (!parent_dir.empty()) {  // a copy: serves until worker 0 stops it
+    shell::wait_for_stop();
+    stop = true;
+    if (refresher.joinable()) refresher.join();
+    front->stop();
+    return 0;
+  }
   Json ready = Json::object();
   ready.set("port", front->port());
-  ready.set("workers", 1);
+  ready.set("workers", static_cast<int>(1 + kids.size()));
   ready.set("native_front", true);
   ready.set("native_gateway", true);
   ready.set("store", fast ? "shm" : "grpc");
   shell::write_ready_file(ready.dump());
   shell::wait_for_stop();
   stop = true;
+  for (pid_t k : kids) ::kill(k, SIGTERM);
+  for (pid_t k : kids) ::waitpid(k, nullptr, 0);
   if (refresher.joinable()) refresher.join();
   front->stop();
   if (audit) audit->close();

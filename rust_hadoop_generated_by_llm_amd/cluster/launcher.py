@@ -28,38 +28,37 @@ ROOT = Path(__file__).resolve().parents[2]
 _handed_out: set[int] = set()
 
 # Roles that run as native executables (csrc/tools/dfs_master.cpp, dfs_config_server.cpp,
-# dfs_chunkserver.cpp), so no Python interpreter lives in a master, config-server or chunkserver
-# process. Masters and config servers have no other form; DFS_NATIVE_CHUNKSERVER=0 (or a knob
-# only the Python shell serves) starts the chunkserver's Python shell as the A/B, and
-# S3_NATIVE_GATEWAY=0 (or S3_WORKERS > 1, S3_METADATA_SIDECAR=true) the Python S3 gateway.
+# dfs_chunkserver.cpp, dfs_s3_gateway.cpp): no Python interpreter lives in a master,
+# config-server, chunkserver or gateway process. The Python chunkserver shell and S3 gateway
+# are test models under tests/models/ (the interop and A/B tests ask for them with the knobs
+# below); the product has no Python form of these roles.
 NATIVE_BINARIES = {"master.server": "dfs_master", "config_server.server": "dfs_config_server",
                    "chunkserver.server": "dfs_chunkserver", "s3.server": "dfs_s3_gateway"}
+TEST_MODELS = {"chunkserver.server": "tests.models.chunkserver_shell", "s3.server": "tests.models.s3_gateway"}
 
 
-def _python_gateway(env) -> bool:
-    """The S3 gateway configurations only the Python gateway serves (its A/B knobs): the
-    reference's sidecar metadata files, several worker processes sharing one audit chain, or
-    the Python-only layout."""
-    return (env.get("S3_NATIVE_GATEWAY", "1") == "0" or env.get("S3_NATIVE_FRONT", "true") != "true"
-            or env.get("S3_METADATA_SIDECAR", "") == "true" or int(env.get("S3_WORKERS", "1") or 1) > 1)
+def _model_gateway(env) -> bool:
+    """Tests asking for the Python gateway model (S3_NATIVE_GATEWAY=0)."""
+    return env.get("S3_NATIVE_GATEWAY", "1") == "0"
 
 
-def _python_chunkserver(args: list[str], env) -> bool:
-    """The chunkserver configurations only the Python shell serves (its A/B knobs)."""
+def _model_chunkserver(args: list[str], env) -> bool:
+    """Tests asking for the Python chunkserver model (its grpcio server stack, its own paths)."""
     return (env.get("DFS_NATIVE_CHUNKSERVER", "1") == "0" or env.get("DFS_CS_GRPC", "native") != "native"
             or env.get("DFS_CS_AGENT", "native") != "native" or "--no-fastpath" in args
             or any(a.startswith("--grpc-impl") and (a.endswith("grpcio") or a == "--grpc-impl") for a in args))
 
 
 def role_command(module: str, args: list[str], environ: dict | None = None) -> list[str]:
-    """argv for a role: its native executable when there is one (and it is enabled), else
-    ``python -m <package>.<module>``."""
+    """argv for a role: its native executable, or (tests only) the Python model under tests/models."""
     env = os.environ if environ is None else environ
     exe = ROOT / "build" / "native" / NATIVE_BINARIES.get(module, "-")
-    if module == "chunkserver.server" and _python_chunkserver(args, env):
-        return [sys.executable, "-m", f"{PKG}.{module}", *args]
-    if module == "s3.server" and _python_gateway(env):
-        return [sys.executable, "-m", f"{PKG}.{module}", *args]
+    model = (module == "chunkserver.server" and _model_chunkserver(args, env)) or \
+            (module == "s3.server" and _model_gateway(env))
+    if model:
+        if not (ROOT / "tests" / "models").is_dir():
+            raise RuntimeError(f"{module}: the Python model is a test fixture (tests/models), not installed")
+        return [sys.executable, "-m", TEST_MODELS[module], *args]
     if module in NATIVE_BINARIES:
         if not exe.exists():
             raise FileNotFoundError(f"{exe} is not built (python build_native.py)")

@@ -1,4 +1,8 @@
-"""``dfs_chunkserver --gpu <i>`` — one ChunkServer process per MI355X (C43; reference
+"""TEST MODEL (not part of the product): the Python chunkserver shell (grpcio server + Python
+control loop over the native store), kept for the interop tests against a grpcio server
+stack. The product's chunkserver process is dfs_chunkserver (csrc/tools/dfs_chunkserver.cpp).
+
+``dfs_chunkserver --gpu <i>`` — one ChunkServer process per MI355X (C43; reference
 dfs/chunkserver/src/bin/chunkserver.rs).
 
 Startup: HBM ChunkStore on GPU i (or the CPU store with ``--gpu -1``), optional RCCL
@@ -20,15 +24,15 @@ import zlib
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from pathlib import Path
 
-from ..models import proto as pb
-from ..native import lib as native
-from ..native import require_gpu
-from ..parallel.sharding import ShardMap
-from ..utils import log as logsetup
-from ..utils.metrics import Registry
-from ..utils.rpc import (ChannelPool, RpcStatus, current_request_id, make_sync_server, rpc_details,
+from rust_hadoop_generated_by_llm_amd.models import proto as pb
+from rust_hadoop_generated_by_llm_amd.native import lib as native
+from rust_hadoop_generated_by_llm_amd.native import require_gpu
+from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
+from rust_hadoop_generated_by_llm_amd.utils import log as logsetup
+from rust_hadoop_generated_by_llm_amd.utils.metrics import Registry
+from rust_hadoop_generated_by_llm_amd.utils.rpc import (ChannelPool, RpcStatus, current_request_id, make_sync_server, rpc_details,
                          server_credentials, snake, strip_scheme, with_scheme)
-from .service import ChunkServer
+from tests.models.chunkserver_service import ChunkServer
 
 log = logging.getLogger("dfs.chunkserver")
 

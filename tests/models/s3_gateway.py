@@ -1,4 +1,8 @@
-"""S3-compatible HTTP gateway over the DFS (C52-C57).
+"""TEST MODEL (not part of the product): the Python S3 gateway, kept as an executable model of
+the native gateway (csrc/s3_front.cpp, csrc/tools/dfs_s3_gateway.cpp) for the A/B tests.
+The product's gateway process is dfs_s3_gateway.
+
+S3-compatible HTTP gateway over the DFS (C52-C57).
 
 Reference: dfs/s3_server/src/{main.rs, handlers.rs, auth_middleware.rs, sts_handler.rs,
 state.rs}. Path-style addressing only (``/{bucket}/{key}``) and the same on-DFS layout, so
@@ -52,16 +56,16 @@ from urllib.parse import parse_qsl, unquote
 
 from aiohttp import web
 
-from ..client.client import Client, DfsError
-from ..parallel.sharding import ShardMap
-from ..utils.metrics import Registry
-from . import xml as X
-from .audit import AuditLogger, make_record
-from .auth import sigv4
-from .auth.errors import AuthError
-from .auth.identity import (EnvCredentialProvider, OidcValidator, SseManager, StsSessionData, StsTokenManager,
+from rust_hadoop_generated_by_llm_amd.client.client import Client, DfsError
+from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
+from rust_hadoop_generated_by_llm_amd.utils.metrics import Registry
+from rust_hadoop_generated_by_llm_amd.s3 import xml as X
+from rust_hadoop_generated_by_llm_amd.s3.audit import AuditLogger, make_record
+from rust_hadoop_generated_by_llm_amd.s3.auth import sigv4
+from rust_hadoop_generated_by_llm_amd.s3.auth.errors import AuthError
+from rust_hadoop_generated_by_llm_amd.s3.auth.identity import (EnvCredentialProvider, OidcValidator, SseManager, StsSessionData, StsTokenManager,
                             parse_sse_master_key, random_alnum)
-from .auth.policy import BucketPolicy, PolicyEvaluator, PolicyResult, resolve_action_and_resource
+from rust_hadoop_generated_by_llm_amd.s3.auth.policy import BucketPolicy, PolicyEvaluator, PolicyResult, resolve_action_and_resource
 
 log = logging.getLogger("dfs.s3")
 
@@ -1237,7 +1241,7 @@ def native_front_wanted(cfg: S3Config) -> bool:
     if cfg.env.get("S3_NATIVE_FRONT", "true") != "true":
         return False
     try:
-        from ..native import lib  # noqa: F401
+        from rust_hadoop_generated_by_llm_amd.native import lib  # noqa: F401
     except Exception:  # noqa: BLE001 - no extension: the Python gateway serves everything
         return False
     return True
@@ -1257,7 +1261,7 @@ def start_native_front(gw: S3Gateway, host: str, port: int, backend: str, audit_
                        policy_epoch: str = ""):
     """Worker 0 runs the native front on the public port; it hands what it does not serve to
     the aiohttp workers on `backend` and sends its audit records to `audit_socket`."""
-    from ..native import lib
+    from rust_hadoop_generated_by_llm_amd.native import lib
 
     cfg = gw.cfg
     creds = gw.creds

@@ -1,7 +1,7 @@
 """Flag names and defaults of every binary match the reference (SURVEY §5.6 table:
 bin/master.rs:21-80, bin/config_server.rs:19-48, bin/chunkserver.rs:33-72,
 dfs_cli.rs:16-43,131-171), so the reference's scripts and compose command lines translate 1:1."""
-from rust_hadoop_generated_by_llm_amd.chunkserver.server import build_parser as cs_parser
+from tests.models.chunkserver_shell import build_parser as cs_parser
 from rust_hadoop_generated_by_llm_amd.cli.dfs_cli import build_parser as cli_parser
 
 

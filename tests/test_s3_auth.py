@@ -25,7 +25,7 @@ from rust_hadoop_generated_by_llm_amd.s3.auth.identity import (Claims, EnvCreden
 from rust_hadoop_generated_by_llm_amd.s3.auth.policy import (BucketPolicy, EvaluationContext, PolicyEvaluator,
                                                             PolicyResult, matches_wildcard,
                                                             resolve_action_and_resource)
-from rust_hadoop_generated_by_llm_amd.s3.server import parse_range
+from tests.models.s3_gateway import parse_range
 
 from . import _rsa
 

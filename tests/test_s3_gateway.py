@@ -29,7 +29,7 @@ from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster, free
 from rust_hadoop_generated_by_llm_amd.s3 import xml as X
 from rust_hadoop_generated_by_llm_amd.s3.audit import SegmentStore, verify_chain
 from rust_hadoop_generated_by_llm_amd.s3.auth import sigv4
-from rust_hadoop_generated_by_llm_amd.s3.server import S3Config, build_gateway
+from tests.models.s3_gateway import S3Config, build_gateway
 
 from . import _rsa
 
@@ -37,7 +37,7 @@ pytestmark = pytest.mark.slow
 
 
 class GatewayThread:
-    """The gateway in this process. `native`: the production layout of s3/server.py with the
+    """The gateway in this process. `native`: the production layout of tests/models/s3_gateway.py with the
     native front end (csrc/s3_front.cpp) on the TCP port, handing what it does not serve to
     the aiohttp app on a private UNIX socket; audit records of native requests reach the
     app's AuditLogger through the same datagram ingest socket the server's workers use."""
@@ -57,10 +57,10 @@ class GatewayThread:
         assert self._ready.wait(30)
         if native:
             from rust_hadoop_generated_by_llm_amd.native import lib
-            from rust_hadoop_generated_by_llm_amd.s3.server import _audit_ingest
+            from tests.models.s3_gateway import _audit_ingest
 
             store = gw.client._fast
-            if store is None:  # a gateway on another host: as s3/server.py start_native_front
+            if store is None:  # a gateway on another host: as tests/models/s3_gateway.py start_native_front
                 store = lib.RemoteFrontStore("", [], slots=16, slot_bytes=16 << 20)
                 gw.client.add_native_routing(store)
                 gw.front_store = store
@@ -69,13 +69,13 @@ class GatewayThread:
                 ingest = os.path.join(self._dir, "ingest.sock")
                 self._isock = socket.socket(socket.AF_UNIX, socket.SOCK_DGRAM)
                 self._isock.bind(ingest)
-                if hasattr(gw.audit, "start_ingest"):  # as s3/server.py main(): native ingest thread
+                if hasattr(gw.audit, "start_ingest"):  # as tests/models/s3_gateway.py main(): native ingest thread
                     gw.audit.start_ingest(self._isock)
                 else:
                     threading.Thread(target=_audit_ingest, args=(self._isock, gw.audit), daemon=True).start()
             cfg = gw.cfg
-            # as s3/server.py main(): the workers and the front share the policy epoch page
-            from rust_hadoop_generated_by_llm_amd.s3.server import PolicyEpoch, native_front_auth
+            # as tests/models/s3_gateway.py main(): the workers and the front share the policy epoch page
+            from tests.models.s3_gateway import PolicyEpoch, native_front_auth
 
             epoch = os.path.join(self._dir, "policy_epoch")
             gw.policy_epoch = PolicyEpoch(epoch)
@@ -927,7 +927,8 @@ def _front_env(cluster, front):
     # the s3.server process runs its native front end when co-located with a chunkserver
     if front == "remote":
         return {}  # no chunkserver on this "host": the front speaks gRPC (RemoteFrontStore)
-    return {"LOCAL_CHUNKSERVER": cluster.cs_addrs[0]} if front in ("native", "exe") else {"S3_NATIVE_FRONT": "false"}
+    # (the "python" front: the Python gateway model of tests/models/s3_gateway.py)
+    return {"LOCAL_CHUNKSERVER": cluster.cs_addrs[0]} if front in ("native", "exe") else {"S3_NATIVE_GATEWAY": "0"}
 
 
 def test_gateway_subprocess(cluster, front):

@@ -292,13 +292,75 @@ def test_remote_store_gateway(cluster):
         g.stop()
 
 
-def test_refuses_sidecar_layout(cluster, tmp_path):
-    """S3_METADATA_SIDECAR=true (the reference's .meta files) is the Python gateway's A/B;
-    the executable refuses it rather than serving another layout."""
-    env = dict(cluster.env, PORT="0", MASTER_ADDR=cluster.master_addrs[0], S3_METADATA_SIDECAR="true",
-               SHARD_CONFIG=str(cluster.base / "shard_config.json"), DFS_READY_FILE=str(tmp_path / "r"))
-    p = subprocess.run([str(EXE)], env=env, capture_output=True, timeout=30)
-    assert p.returncode == 2 and b"SIDECAR" in p.stderr.upper()
+def test_reference_sidecar_layout_served_natively(cluster):
+    """The reference gateway's object layout (handlers.rs:984-1006,1058-1079): headers in a
+    sidecar DFS file `<key>.meta` = {"headers": {...}}. The executable reads it for objects
+    without attributes (GET, HEAD, listings, CopyObject, multipart objects the reference
+    completed: numbered parts, no recorded layout) and, with S3_METADATA_SIDECAR=true, writes
+    it for PUT, CopyObject and CompleteMultipartUpload — with no hand-off to any backend."""
+    import json
+    import xml.etree.ElementTree as ET
+
+    c = cluster.client()
+    g = Exe(cluster, {"AUDIT_LOG_ENABLED": "false", "S3_METADATA_SIDECAR": "true",
+                      "LOCAL_CHUNKSERVER": cluster.cs_addrs[0]}, "s3xside")
+    try:
+        u = g.url
+        assert requests.put(f"{u}/refside").status_code == 200
+        # objects the reference wrote: plain file + sidecar
+        c.create_file_from_buffer(b"legacy bytes", "/refside/legacy")
+        c.create_file_from_buffer(json.dumps({"headers": {"ETag": '"abc"', "x-amz-meta-old": "1",
+                                                          "Content-Type": "text/old"}}).encode(), "/refside/legacy.meta")
+        r = requests.get(f"{u}/refside/legacy")
+        assert r.content == b"legacy bytes" and r.headers["ETag"] == '"abc"'
+        assert r.headers["x-amz-meta-old"] == "1" and r.headers["Content-Type"] == "text/old"
+        assert requests.head(f"{u}/refside/legacy").headers["x-amz-meta-old"] == "1"
+        # a multipart object completed by the reference: numbered parts, a bare marker, a sidecar
+        p1, p2 = os.urandom(70_000), os.urandom(1234)
+        c.create_file_from_buffer(p1, "/refside/big/1")
+        c.create_file_from_buffer(p2, "/refside/big/2")
+        c.create_file_from_buffer(b"", "/refside/big/.s3_mpu_completed")
+        c.create_file_from_buffer(json.dumps({"headers": {"ETag": '"mpu-2"'}}).encode(), "/refside/big.meta")
+        r = requests.get(f"{u}/refside/big")
+        assert r.content == p1 + p2 and r.headers["ETag"] == '"mpu-2"'
+        r = requests.get(f"{u}/refside/big", headers={"Range": "bytes=69990-70009"})
+        assert r.status_code == 206 and r.content == (p1 + p2)[69990:70010]
+        lst = ET.fromstring(requests.get(f"{u}/refside?list-type=2").content)
+        ns = lst.tag.split("}")[0] + "}" if lst.tag.startswith("{") else ""
+        got = {e.find(ns + "Key").text: (e.find(ns + "ETag").text, int(e.find(ns + "Size").text))
+               for e in lst.findall(ns + "Contents")}
+        assert got["legacy"] == ('"abc"', 12) and got["big"] == ('"mpu-2"', len(p1) + len(p2))
+        # writes with S3_METADATA_SIDECAR=true also leave the reference's sidecar
+        body = os.urandom(5000)
+        r = requests.put(f"{u}/refside/new", data=body, headers={"x-amz-meta-a": "b", "Content-Type": "text/n"})
+        assert r.status_code == 200
+        side = json.loads(c.get_file_content("/refside/new.meta"))
+        assert side == {"headers": {"ETag": r.headers["ETag"], "x-amz-meta-a": "b", "Content-Type": "text/n"}}
+        assert c.get_file_info("/refside/new").attributes["ETag"] == r.headers["ETag"]
+        # CopyObject of a sidecar-described source keeps its headers (COPY directive)
+        r = requests.put(f"{u}/refside/copy", headers={"x-amz-copy-source": "/refside/legacy"})
+        assert r.status_code == 200
+        r = requests.get(f"{u}/refside/copy")
+        assert r.content == b"legacy bytes" and r.headers["x-amz-meta-old"] == "1"
+        assert json.loads(c.get_file_content("/refside/copy.meta"))["headers"]["x-amz-meta-old"] == "1"
+        # multipart completion writes the sidecar of the object too
+        up = ET.fromstring(requests.post(f"{u}/refside/mp?uploads").content)
+        uid = next(e.text for e in up.iter() if e.tag.endswith("UploadId"))
+        e1 = requests.put(f"{u}/refside/mp?partNumber=1&uploadId={uid}", data=b"q" * 6000).headers["ETag"]
+        done = ("<CompleteMultipartUpload><Part><PartNumber>1</PartNumber><ETag>" + e1 +
+                "</ETag></Part></CompleteMultipartUpload>")
+        r = requests.post(f"{u}/refside/mp?uploadId={uid}", data=done)
+        assert r.status_code == 200
+        assert json.loads(c.get_file_content("/refside/mp.meta"))["headers"]["ETag"].endswith('-1"')
+        # DELETE removes the sidecar with the object
+        assert requests.delete(f"{u}/refside/new").status_code == 204
+        assert not c.exists("/refside/new.meta")
+        handoffs = [ln for ln in g.metrics().splitlines()
+                    if ln.startswith("s3_native_handoffs_total") and not ln.rstrip().endswith(" 0")]
+        assert handoffs == [], handoffs
+    finally:
+        g.stop()
+        c.close()
 
 
 def test_follows_master_leader_changes():
