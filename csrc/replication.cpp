@@ -76,7 +76,9 @@ std::unique_ptr<P2PTransport> make_transport(const std::string& name, ChunkStore
                                              const std::string& ns, int channels, std::string* err) {
   if (channels <= 0) {
     const char* e = std::getenv(name == "rccl" ? "DFS_REPL_CHANNELS_RCCL" : "DFS_REPL_CHANNELS");
-    channels = e && *e ? std::atoi(e) : (name == "rccl" ? 1 : 4);
+    // RCCL: K 2-rank communicators per pair direction (each with its own proxy thread and
+    // staging buffers: 2*K*(N-1) per process, 28 at N=8 with K=2); hipipc: K rings
+    channels = e && *e ? std::atoi(e) : (name == "rccl" ? 2 : 4);
   }
   if (name == "rccl") return make_rccl_transport(store->config().device, rank, channels, err);
   if (name == "socket") return make_socket_transport(rank, ns, channels);

@@ -22,9 +22,11 @@ failures and the bytes each link carried, so a failure names the link instead of
 The CPU analogues at 8 ranks (socket transport) are tests/test_multi_rank_cpu.py.
 
 RCCL resource cost (csrc/p2p_rccl.cpp): a pair is K 2-rank communicators per direction
-(DFS_REPL_CHANNELS_RCCL, default K=1), so one process holds 2*K*(N-1) communicators: 14 at
-N=8. Each communicator brings its own proxy thread and per-peer staging buffers, so the
-channel count for RCCL stays at 1 unless a multi-GPU run shows the FIFO turn is the bound.
+(DFS_REPL_CHANNELS_RCCL, default K=2 since round 6, like hipipc's several rings: one slow
+transfer no longer holds the pair's other transfers behind a single FIFO turn), so one
+process holds 2*K*(N-1) communicators: 4 at N=2, 12 at N=4, 28 at N=8, each with its own
+proxy thread, bootstrap sockets and per-peer staging buffers. The RCCL tests below run at
+the default K.
 """
 import os
 import signal
