@@ -992,7 +992,7 @@ bool ChunkStore::device_stage(const uint8_t* data, uint64_t n, const DevExtent& 
     return !(e && e[0] == '0');
   }();
   // The fused kernel loads the block over PCIe with the waves' own reads: lowest latency for
-  // one write (1 MiB: 39 vs 57 us, profiles/r3_fused_write), but GPU-initiated host reads top
+  // one write (1 MiB: 39 vs 57 us, profiles/archive/r3_fused_write), but GPU-initiated host reads top
   // out well below the copy engines once several writes overlap (10 x 1 MiB: 29 vs 46 GB/s,
   // profiles/r4_roofline). Past this many stagings in flight the SDMA engines take the copy.
   static const int fused_max = [] {
@@ -3080,7 +3080,12 @@ void ChunkStore::materializer_loop() {
       for (;;) {
         const auto t = std::chrono::steady_clock::now();
         const uint64_t last_append = store_mode_ ? journal_->last_append_ns() : 0;
-        const bool busy = last_append && mono_ns() - last_append < 50000000ull;
+        // Writers active: exports trickle (DFS_EXPORT_BUSY_MBPS, small bursts) so they stay out
+        // of the acked writes' way. Not while segments wait for compaction: reclaim is what
+        // keeps the writers from finding the journal full, and at the trickle rate it never
+        // got the half burst it starts at (config 5's multipart phase: 6,371 writer waits,
+        // uploads timing out at 120 s, profiles/r6/config5.json first run).
+        const bool busy = last_append && mono_ns() - last_append < 50000000ull && !want_compact;
         const double cap = busy ? std::min(burst, kBusyBurst) : burst;
         tokens = std::min(cap, tokens + (busy ? export_busy_bps_ : export_bps_) *
                                             std::chrono::duration<double>(t - t_prev).count());

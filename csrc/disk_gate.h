@@ -2,7 +2,7 @@
 //
 // Every GPU of a node runs its own ChunkServer process, and with RF=3 each client write
 // becomes three write+fdatasync streams that usually land on the same volume. Measured on
-// an MI355X box (profiles/r1_native/disk_sweep_*.json) the volume peaks at 10-30 concurrent
+// an MI355X box (profiles/archive/r1_disk/disk_sweep_*.json) the volume peaks at 10-30 concurrent
 // 1 MiB durable writers (8.5-9.2 GB/s buffered) and collapses to 3-4 GB/s with p99 > 100 ms
 // once 60-240 writers pile up — exactly the N=8 replication load. DiskGate caps the number
 // of durable writes in flight per filesystem ACROSS processes, each slot held for one

@@ -98,7 +98,7 @@ void set_crc_lds_max_mib(int mib);
 DevCrcTables* upload_crc_tables(hipStream_t s);
 int crc_grid_for(uint64_t ntiles, uint32_t has_tail);
 // Tile buffers per wave in the MFMA kernels' register ring (2..4; 2 = the 3-waves/SIMD
-// kernels, 3..4 = the deep-ring kernels at 2 waves/SIMD). Measured (profiles/r2_crc3): the
+// kernels, 3..4 = the deep-ring kernels at 2 waves/SIMD). Measured (profiles/archive/r2_crc3): the
 // K1b scrub gains ~19 % from 3 buffers; K1/K2 does not (its per-tile combine work, not load
 // latency, is what the third wave hides), so it keeps 2. DFS_CRC_RING / DFS_CRC_TILE_RING
 // override, set_crc_ring is the benches' A/B switch; K1/K2/K3 launches below

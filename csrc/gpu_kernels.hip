@@ -1285,7 +1285,7 @@ void set_crc_ring(int scrub_buffers, int tile_buffers) {
 // launch, e.g. on 1 MiB blocks).
 // Size-based K1/K2 dispatch: below DFS_CRC_LDS_MAX_MIB (default 16 MiB) the LDS-table kernel
 // wins (its per-workgroup setup is smaller: 1 MiB 6.02 vs 6.47 us, 8 MiB 7.39 vs 8.89 us in
-// profiles/r2_crc4/crc_default.json); from 64 MiB up the matrix-core kernel is 1.3-1.9x faster.
+// profiles/archive/r2_crc4/crc_default.json); from 64 MiB up the matrix-core kernel is 1.3-1.9x faster.
 static std::atomic<int64_t> g_lds_max_mib{-1};
 
 void set_crc_lds_max_mib(int mib) { g_lds_max_mib.store(mib < 0 ? 0 : mib); }

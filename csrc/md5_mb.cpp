@@ -238,7 +238,7 @@ Md5MultiBuffer::Kind Md5MultiBuffer::wanted() {
     if (v == "0" || v == "openssl") return Kind::None;
     if (v == "scalar") return Kind::Scalar;
     if (v == "1" || v == "avx512") return available() ? Kind::Avx512 : Kind::Scalar;
-    // the cheapest engine that the rank's CPU budget calls for (profiles/r6_md5, Zen 5, 10
+    // the cheapest engine that the rank's CPU budget calls for (profiles/r6/md5, Zen 5, 10
     // writes in flight): OpenSSL per message 0.99 ms on ~10 cores; 2 interleaved per thread
     // 1.01 ms on 5; AVX-512 lanes 1.9 ms on 1
     const double c = cores_per_rank();

@@ -43,7 +43,7 @@ class Md5MultiBuffer {
   static bool available();  // the CPU has AVX-512F (and the DFS_MD5_MB switch is not 0)
   // Which engine a client should hash its ETags on. On the MI355X hosts (Zen 5) an AVX-512
   // lane's step chain is twice a scalar core's (2-cycle vector integer latency,
-  // profiles/r6_md5): ~1.9 ms per MiB against ~1.0 for a scalar hash. So the AVX-512 engine is
+  // profiles/r6/md5): ~1.9 ms per MiB against ~1.0 for a scalar hash. So the AVX-512 engine is
   // a CPU-budget choice made from the cores this process may use (the cgroup quota, else the
   // online CPUs, divided by the ranks sharing the node: LOCAL_WORLD_SIZE or DFS_RANKS_ON_NODE):
   // >= DFS_MD5_OPENSSL_MIN_CORES (12): OpenSSL per message (lowest latency, ~1 core per write

@@ -194,6 +194,42 @@ def test_overwrites_reclaim_the_journal_while_the_exporter_runs(native, tmp_path
     assert s.read("keep", 0, 0)[2] == keep
 
 
+def test_busy_writers_still_get_segments_compacted(native, tmp_path, monkeypatch):
+    """Writers that never pause, with a long-lived record landing in every segment: segments
+    only come back through compaction (no headroom for exports here). The exporter's slow
+    busy-writer rate must not starve compaction: with it gating compaction too, config 5's
+    multipart phase found the journal full and timed out (profiles/r6/config5.json, r6 first
+    run: 6,371 writer waits, 10 uploads failed)."""
+    import time
+
+    for k, v in SMALL.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("DFS_JOURNAL_EXPORT", "store")
+    monkeypatch.setenv("DFS_EXPORT_HEADROOM_MB", str(1 << 30))  # never headroom: no exports
+    monkeypatch.setenv("DFS_EXPORT_BUSY_MBPS", "1")
+    monkeypatch.setenv("DFS_JOURNAL_SEGS", "6")
+    monkeypatch.setenv("DFS_JOURNAL_FULL_TIMEOUT_S", "10")
+    s = open_store(native, tmp_path)
+    kept = {}
+    t0 = time.time()
+    n = 0
+    while time.time() - t0 < 3.0:  # ~100 MB/s: the journal wraps every ~0.5 s, never idle 50 ms
+        v = os.urandom(256 << 10)
+        key = f"live{n}" if n % 16 == 0 and len(kept) < 40 else f"k{n % 8}"
+        ok, _crc, err = s.write(key, v, zlib.crc32(v))[:3]
+        assert ok, (n, err, s.stats())
+        if key.startswith("live"):
+            kept[key] = v
+        n += 1
+        time.sleep(0.002)
+    st = s.stats()
+    assert n * (256 << 10) > 3 * 6 * (8 << 20), (n, st)  # wrapped the journal 3 times
+    assert st["journal_full_waits"] == 0, st
+    assert st["relocated_blocks"] > 0, st
+    for key, v in list(kept.items())[:8]:
+        assert s.read(key, 0, 0)[2] == v
+
+
 def test_supersede_marker_keeps_a_per_file_rewrite(native, tmp_path, never):
     """A rewrite too large for a segment part goes to its own files; the committed supersede
     marker stops replay from bringing back the older journal version."""
