@@ -1040,7 +1040,7 @@ TEST(journal_defers_spare_creation_while_writers_are_active) {
   JournalConfig c = jt::small(d + "/j", true);
   c.spares = 4;
   c.spares_low = 2;
-  c.idle_fill_ms = 50;
+  c.idle_fill_ms = 400;  // no gap between two appends counts as idle, even under a sanitizer on a loaded host
   BlockJournal j(c);
   CHECK(j.recover().empty());
   CHECK(eventually([&] { auto s = j.stats(); return s.spares_missing == 0 && s.parts_unready == 0; }, 10));
@@ -1054,10 +1054,12 @@ TEST(journal_defers_spare_creation_while_writers_are_active) {
   }
   const double active_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   JournalStats mid = j.stats();
-  if (active_s < 0.04) CHECK(mid.segs_total == segs0);  // nothing created while the writers ran
-  CHECK(mid.spares_missing > 0 && mid.parts_unready == 0);
+  if (active_s < 0.4) {  // the writers never paused for an idle window
+    CHECK(mid.segs_total == segs0);  // nothing created while they ran
+    CHECK(mid.spares_missing > 0 && mid.parts_unready == 0);
+  }
   CHECK(eventually([&] { return j.stats().spares_missing == 0; }, 10));  // topped up once idle
-  CHECK(j.stats().grow_deferred >= 1 || active_s >= 0.04);
+  CHECK(j.stats().grow_deferred >= 1 || active_s >= 0.4);
   std::filesystem::remove_all(d);
 }
 

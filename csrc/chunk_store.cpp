@@ -235,6 +235,11 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     }
     dtables_ = upload_crc_tables(lanes_[0]->stream);
     if (!dtables_) throw std::runtime_error("failed to upload GPU tables");
+    pull_pool_ = std::make_shared<PinnedPool>();
+    if (hipMalloc(reinterpret_cast<void**>(&pull_parts_dev_), kMaxGridCrc * sizeof(uint32_t)) != hipSuccess) {
+      (void)hipGetLastError();
+      pull_parts_dev_ = nullptr;  // no receiver pull: the transport's senders copy
+    }
     st_.hbm_capacity = cap;
     if (cfg_.durability == Durability::HbmAck)
       for (int i = 0; i < std::max(1, cfg_.spill_threads); ++i) spillers_.emplace_back([this] { spill_worker(); });
@@ -254,7 +259,6 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     // rate in batches of at most 8 MiB, so its per-file flushes and directory flush never
     // land on the writers as a 64-file burst; at full rate again once they pause
     export_busy_bps_ = env_int("DFS_EXPORT_BUSY_MBPS", 64) * 1e6;
-    compact_live_ = env_int("DFS_COMPACT_LIVE_PCT", 50) / 100.0;
     uint64_t vol_total = 0;
     {
       struct statvfs sv;
@@ -340,6 +344,7 @@ ChunkStore::~ChunkStore() {
     }
     if (arena_) (void)hipFree(arena_);
     if (dtables_) (void)hipFree(dtables_);
+    if (pull_parts_dev_) (void)hipFree(pull_parts_dev_);
   }
 }
 
@@ -1855,9 +1860,70 @@ WriteResult ChunkStore::commit_device(const std::string& id, const DevExtent& ex
   return res;
 }
 
-bool ChunkStore::recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n) {
+// Receiver-pull scratch: pinned host buffers (hipHostMalloc is ~ms) reused across receives.
+// Held through shared_ptr by every launch closure, so a buffer goes back to the pool only
+// when no kernel of an abandoned receive can still write it.
+struct ChunkStore::PinnedPool {
+  std::mutex mu;
+  std::vector<std::pair<uint8_t*, uint64_t>> free;
+  ~PinnedPool() {
+    for (auto& f : free) (void)hipHostFree(f.first);
+  }
+};
+struct ChunkStore::PullScratch {
+  std::shared_ptr<PinnedPool> pool;
+  uint8_t* host = nullptr;
+  uint8_t* dev = nullptr;
+  uint64_t cap = 0;
+  ~PullScratch() {
+    if (!host) return;
+    std::lock_guard<std::mutex> g(pool->mu);
+    pool->free.emplace_back(host, cap);
+  }
+};
+
+bool ChunkStore::can_pull() const { return gpu() && crc_mfma_enabled() && dtables_ && pull_parts_dev_; }
+
+bool ChunkStore::recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n, bool pull) {
   rv->ext = e;
   rv->n = n;
+  rv->pull.reset();
+  if (pull) {
+    if (!can_pull()) return false;
+    const uint64_t want = align_up(num_slices(n) * 4 + 16, 4096);
+    auto sc = std::make_shared<PullScratch>();
+    sc->pool = pull_pool_;
+    {
+      std::lock_guard<std::mutex> g(pull_pool_->mu);
+      auto& fr = pull_pool_->free;
+      for (size_t i = 0; i < fr.size(); ++i)
+        if (fr[i].second >= want) {
+          sc->host = fr[i].first;
+          sc->cap = fr[i].second;
+          fr[i] = fr.back();
+          fr.pop_back();
+          break;
+        }
+    }
+    if (!sc->host) {
+      (void)hipSetDevice(cfg_.device);
+      if (hipHostMalloc(reinterpret_cast<void**>(&sc->host), want, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        sc->host = nullptr;
+        return false;
+      }
+      sc->cap = want;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, sc->host, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;  // sc goes back to the pool
+    }
+    sc->dev = static_cast<uint8_t*>(d);
+    rv->pull = std::move(sc);
+    rv->lane = nullptr;
+    return true;
+  }
   // no lane yet: a receive waits for its bytes without holding one of the store's streams
   // (at 10 writers per rank the waiting receives held the lanes the heads' stagings needed);
   // DFS_RECV_LANE_EAGER=1 takes it here, as before (A/B)
@@ -1902,21 +1968,53 @@ bool ChunkStore::recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi) {
   return !rv->failed;
 }
 
+std::function<int(const uint8_t*, void*)> ChunkStore::recv_pull(RecvVerify* rv, uint64_t lo, uint64_t hi) {
+  const uint64_t len = hi > lo ? hi - lo : 0;
+  uint8_t* dst = rv->ext.ptr + lo;
+  uint32_t* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(rv->n, 1), 256)) +
+                    lo / kSliceBytes;
+  std::shared_ptr<PullScratch> sc = rv->pull;
+  uint32_t* mh = sc ? reinterpret_cast<uint32_t*>(sc->dev) + lo / kSliceBytes : nullptr;
+  const DevCrcTables* tables = dtables_;
+  uint32_t* parts = pull_parts_dev_;
+  return [=](const uint8_t* src, void* stream) -> int {
+    if (!sc || lo % kSliceBytes || ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16))
+      return -1;  // the kernel moves 16-byte vectors from slice-aligned offsets
+    if (len == 0) return 0;
+    CrcPlan p = plan_crc(src, len, dmeta, nullptr, true, 0, len);
+    WriteCopyLaunch w;
+    w.c = p.a;
+    w.c.part_crc = parts;  // partials of the slice: unread (recv_finish combines the .meta words)
+    w.dst = dst;
+    w.meta_host = mh;
+    return launch_write_copy(w, tables, p.grid, static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -1;
+  };
+}
+
 WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint32_t expected_crc, bool persist_now) {
   TraceRange tr("dfs.store.recv_commit");
   WriteResult res;
-  Lane* l = static_cast<Lane*>(recv_lane(rv));
-  (void)hipSetDevice(cfg_.device);
   uint64_t n = rv->n, S = num_slices(n);
-  auto* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
-  ensure_hscratch(l, S * 4 + 16);
-  uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
-  if (!rv->failed && S && !rv->host_meta)
-    HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
-  HIP_OK(hipStreamSynchronize(l->stream));
-  auto meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
-  release_lane(l);
-  rv->lane = nullptr;
+  std::shared_ptr<std::vector<uint8_t>> meta;
+  if (rv->pull) {
+    // every slice's kernel finished before the transport completed the receive: the .meta
+    // image is already in the pinned scratch
+    meta = std::make_shared<std::vector<uint8_t>>(rv->pull->host, rv->pull->host + S * 4);
+    rv->pull.reset();
+    pulled_recvs_++;
+  } else {
+    Lane* l = static_cast<Lane*>(recv_lane(rv));
+    (void)hipSetDevice(cfg_.device);
+    auto* dmeta = reinterpret_cast<uint32_t*>(rv->ext.ptr + align_up(std::max<uint64_t>(n, 1), 256));
+    ensure_hscratch(l, S * 4 + 16);
+    uint8_t* hmeta = l->hscratch + 2 * kMaxGridCrc * sizeof(uint32_t) + 16;
+    if (!rv->failed && S && !rv->host_meta)
+      HIP_OK(hipMemcpyAsync(hmeta, dmeta, S * 4, hipMemcpyDeviceToHost, l->stream));
+    HIP_OK(hipStreamSynchronize(l->stream));
+    meta = std::make_shared<std::vector<uint8_t>>(hmeta, hmeta + S * 4);
+    release_lane(l);
+    rv->lane = nullptr;
+  }
   if (rv->failed) {
     release(rv->ext);
     res.error = rv->error;
@@ -1959,6 +2057,7 @@ WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint3
 }
 
 void ChunkStore::recv_abandon(RecvVerify* rv) {
+  rv->pull.reset();  // launches still queued keep the scratch until they are dropped
   if (!rv->lane) return;
   Lane* l = static_cast<Lane*>(rv->lane);
   // kernels already queued on the lane only read the extent: they finish on their own
@@ -2389,6 +2488,7 @@ StoreStats ChunkStore::stats() {
   s.direct_dma = direct_dma_.load();
   s.fused_reads = fused_reads_.load();
   s.fused_writes = fused_writes_.load();
+  s.pulled_recvs = pulled_recvs_.load();
   s.sliced_stages = sliced_stages_.load();
   s.staged_dma = staged_dma_.load();
   s.mirror_hits = mirror_hits_;
@@ -3068,7 +3168,7 @@ void ChunkStore::materializer_loop() {
   double tokens = burst;
   auto t_prev = std::chrono::steady_clock::now();
   bool headroom = false, stop_failed = false;
-  bool want_compact = false, compact_urgent = false;
+  bool want_compact = false, compact_urgent = false, reclaim = false;
   auto headroom_at = t_prev, compact_check_at = t_prev;
   std::vector<MatItem> batch;
   for (;;) {
@@ -3085,7 +3185,7 @@ void ChunkStore::materializer_loop() {
         // keeps the writers from finding the journal full, and at the trickle rate it never
         // got the half burst it starts at (config 5's multipart phase: 6,371 writer waits,
         // uploads timing out at 120 s, profiles/r6/config5.json first run).
-        const bool busy = last_append && mono_ns() - last_append < 50000000ull && !want_compact;
+        const bool busy = last_append && mono_ns() - last_append < 50000000ull && !reclaim;
         const double cap = busy ? std::min(burst, kBusyBurst) : burst;
         tokens = std::min(cap, tokens + (busy ? export_busy_bps_ : export_bps_) *
                                             std::chrono::duration<double>(t - t_prev).count());
@@ -3109,8 +3209,15 @@ void ChunkStore::materializer_loop() {
           compact_check_at = t + std::chrono::milliseconds(20);
           lk.unlock();
           const JournalStats j = journal_->stats();
-          const bool dead = j.grow_blocked || (j.used_bytes && j.used_bytes - j.live_bytes > j.used_bytes / 4);
-          want_compact = dead && journal_->compaction_candidate(compact_live_) != nullptr;
+          // dead space in the segments behind the active one (the active one's unwritten
+          // tail is not dead): a quarter of them, and more than one segment's worth
+          const uint64_t dead = j.sealed_used_bytes - std::min(j.sealed_used_bytes, j.sealed_live_bytes);
+          reclaim = j.grow_blocked || (dead > j.sealed_used_bytes / 4 && dead > journal_->seg_bytes());
+          // Segments retire oldest first, so an oldest segment that stays mostly live (blocks
+          // nobody overwrites, exports behind) holds every dead segment behind it: under
+          // reclaim it is relocated whatever its live share (config 5's multipart phase: 80 GB
+          // of journal for 2.35 GB live, the volume full, writers waiting, r6c5).
+          want_compact = reclaim && journal_->compaction_candidate(1.0) != nullptr;
           compact_urgent = j.grow_blocked;
           lk.lock();
         }
@@ -3164,7 +3271,7 @@ void ChunkStore::materializer_loop() {
       }
     }
     if (compact_now) {
-      SegRef seg = journal_->compaction_candidate(compact_live_);
+      SegRef seg = journal_->compaction_candidate(1.0);
       // urgent (the journal cannot grow): one whole segment's live records whatever the tokens
       const double budget = compact_urgent ? static_cast<double>(journal_->seg_bytes()) : std::max(tokens, 1.0);
       if (seg) tokens -= static_cast<double>(relocate_segment(seg, static_cast<uint64_t>(budget)));

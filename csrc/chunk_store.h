@@ -20,6 +20,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <list>
 #include <map>
 #include <memory>
@@ -89,6 +90,7 @@ struct StoreStats {
   uint64_t direct_dma = 0;       // host<->HBM copies done straight from registered memory
   uint64_t fused_reads = 0;      // reads delivered by the K3 verify+copy kernel (no SDMA copy)
   uint64_t fused_writes = 0;     // writes staged by the K1/K2 copy+checksum kernel (no SDMA copy)
+  uint64_t pulled_recvs = 0;  // replica receives moved by the receiver's copy+checksum kernel
   uint64_t sliced_stages = 0;    // pipelined head writes (per-slice fused kernels, sends overlap)
   uint64_t staged_dma = 0;       // copies bounced through pinned staging buffers
   uint64_t host_registered_bytes = 0;
@@ -216,6 +218,7 @@ class ChunkStore {
   // each landed byte range is checksummed on a store lane (K1 into the extent's .meta image)
   // so verification overlaps the transfer; finish() folds the slice CRCs into the block CRC,
   // compares, and commits (or releases the extent on mismatch).
+  struct PullScratch;  // pinned host memory a pulled receive's kernels write its .meta image to
   struct RecvVerify {
     DevExtent ext;
     uint64_t n = 0;
@@ -223,8 +226,17 @@ class ChunkStore {
     bool failed = false;
     bool host_meta = true;  // every slice kernel mirrored its .meta words into the lane's scratch
     std::string error;
+    std::shared_ptr<PullScratch> pull;  // receiver pull (recv_begin(..., true))
   };
-  bool recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n);
+  // pull: the slices arrive through recv_pull's kernels (the transport launches them), not
+  // recv_slice; returns false if the store cannot (no matrix-core CRC path, no pinned memory)
+  bool recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n, bool pull = false);
+  // Receiver pull: the launch of bytes [lo, hi) of the receive (lo a multiple of 512): one
+  // crc_write_copy_kernel that reads the sender's bytes (a device pointer into its mapped
+  // arena), stores them into the extent and writes the slices' .meta words to HBM and to the
+  // receive's pinned scratch. The closure owns the scratch it writes to.
+  std::function<int(const uint8_t*, void*)> recv_pull(RecvVerify* rv, uint64_t lo, uint64_t hi);
+  bool can_pull() const;
   void* recv_lane(RecvVerify* rv);  // the receive's lane, taken at its first slice
   bool recv_slice(RecvVerify* rv, uint64_t lo, uint64_t hi);  // lo, hi: byte range, lo % 512 == 0
   WriteResult recv_finish(RecvVerify* rv, const std::string& id, uint32_t expected_crc, bool persist_now);
@@ -372,7 +384,6 @@ class ChunkStore {
   double export_busy_bps_ = 64e6;    // ... while writers are active (DFS_EXPORT_BUSY_MBPS)
   uint64_t export_busy_polls_ = 0;   // exporter wake-ups that found the writers active (mu_)
   uint64_t export_headroom_ = 0;     // export only while the volume keeps this much free
-  double compact_live_ = 0.5;        // compaction: oldest segment at most this share live
   void materializer_loop();
   bool materialize_due();
   bool export_headroom(uint64_t bytes);
@@ -459,6 +470,10 @@ class ChunkStore {
   uint8_t* device_view(const void* p, uint64_t n);
   std::atomic<uint64_t> fused_reads_{0};  // K3 fused verify+copy reads
   std::atomic<uint64_t> fused_writes_{0};  // K1/K2 fused copy+checksum writes
+  struct PinnedPool;
+  std::shared_ptr<PinnedPool> pull_pool_;  // receiver-pull .meta scratch (outlives closures)
+  uint32_t* pull_parts_dev_ = nullptr;    // the pull kernels' whole-block partials (unread)
+  std::atomic<uint64_t> pulled_recvs_{0};
   std::atomic<int> staging_{0};            // device stagings in flight (fused vs SDMA choice)
   std::atomic<uint64_t> sliced_stages_{0};
   bool write_copy(Lane* l, const uint8_t* src_dev, uint8_t* dst, uint64_t n, uint32_t* dmeta, uint8_t* hmeta,

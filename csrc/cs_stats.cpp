@@ -35,6 +35,7 @@ Json stats_json(const StoreStats& t) {
   d.set("direct_dma", t.direct_dma);
   d.set("fused_reads", t.fused_reads);
   d.set("fused_writes", t.fused_writes);
+  d.set("pulled_recvs", t.pulled_recvs);
   d.set("sliced_stages", t.sliced_stages);
   d.set("staged_dma", t.staged_dma);
   d.set("host_registered_bytes", t.host_registered_bytes);

@@ -1030,6 +1030,10 @@ JournalStats BlockJournal::stats() {
     s.live_records += seg->live;
     s.live_bytes += seg->live_bytes;
     s.used_bytes += seg->capacity();
+    if (seg != order_.back()) {
+      s.sealed_used_bytes += seg->capacity();
+      s.sealed_live_bytes += seg->live_bytes;
+    }
   }
   // parts_unready: what a writer activating a segment could be handed that is not ready (a
   // free segment not written out yet, or none at all below spares_low); spares_missing: the

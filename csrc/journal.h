@@ -160,6 +160,8 @@ struct JournalStats {
   uint64_t replayed = 0, replay_skipped = 0, replay_verified = 0, prepared = 0, prepare_errors = 0, filled = 0,
            fill_bytes = 0;
   uint64_t live_records = 0, live_bytes = 0, used_bytes = 0;  // used: in-use segments x capacity
+  // the in-use segments behind the active one: what retiring or compacting them could free
+  uint64_t sealed_used_bytes = 0, sealed_live_bytes = 0;
   uint64_t sync_ns = 0, commit_ns = 0;  // time in fdatasync rounds; time writers spent in commit()
   uint64_t parts_unready = 0;  // free segments' parts not yet written out once (zero_fill), or missing below spares_low
   uint64_t spares_missing = 0; // grow: segments short of `spares` (topped up in idle windows)

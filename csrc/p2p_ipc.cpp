@@ -26,6 +26,18 @@
 //  * close() raises `abort` on both rings, stops the worker and drains the channel stream
 //    (copies always finish), so when it returns no copy of that generation can still land.
 //
+// Pull mode (make_ipc_transport(..., pull=true): the replication engine asks for it when the
+// store runs the matrix-core CRC kernels; DFS_IPC_PULL=0 turns it off) inverts the copy: the
+// sender only OFFERS each slice (its offset in the sender's arena) on the ring, and the
+// receiver's worker launches one kernel that reads the slice from the peer's mapped arena
+// (over xGMI between GPUs), stores it into the posted extent, and writes the slice CRCs (the
+// .meta image) to HBM and to pinned host memory (crc_write_copy_kernel, the same kernel that
+// takes a client's write over PCIe). That replaces the sender's copy kernel plus the
+// receiver's separate checksum pass on arrival: one kernel per hop, no readback. When the
+// kernel's event completes the receiver publishes `landed`, which completes both sides' ops.
+// The receiver decides per direction (its waves must reach the peer's memory) and tells the
+// sender through its inbound ring's `pull` word before its warm-up is published.
+//
 // Spin mode (make_ipc_transport(..., spin=true); DFS_IPC_SPIN=1) is the RCCL emulation used
 // to test the engine against the hazard above: post_send launches a kernel that parks on the
 // send stream until the credit appears and then copies with the whole grid; post_recv
@@ -186,11 +198,20 @@ struct SendItem {
   hipEvent_t ev = nullptr;
 };
 
+// A receive in pull mode: matched with the sender's seq-th offer, then launched.
+struct PullItem {
+  uint64_t n = 0;
+  uint64_t seq = 0;
+  P2PTransport::PullLaunch launch;
+  hipEvent_t ev = nullptr;
+};
+
 class IpcTransport final : public P2PTransport {
  public:
-  IpcTransport(int device, int rank, std::string ns, uint8_t* arena, uint64_t arena_bytes, bool spin, int channels)
+  IpcTransport(int device, int rank, std::string ns, uint8_t* arena, uint64_t arena_bytes, bool spin, int channels,
+               bool pull)
       : device_(device), rank_(rank), ns_(std::move(ns)), arena_(arena), arena_bytes_(arena_bytes), spin_(spin),
-        channels_(channels) {
+        channels_(channels), pull_(pull && !spin) {
     const char* ms = std::getenv("DFS_IPC_SPIN_MS");
     spin_ticks_ = wall_ticks_per_ms(device) * static_cast<uint64_t>(ms ? std::max(1, std::atoi(ms)) : 5000);
   }
@@ -346,6 +367,10 @@ class IpcTransport final : public P2PTransport {
       (void)hipGetLastError();
     }
     for (auto& c : l.ch) {
+      // our receives from this peer are pulled by our kernels when our waves reach its
+      // memory; published before our warm-up, which the peer waits for before reading it
+      c->i_pull = pull_ && l.kernel_copy;
+      st(&c->in->r->pull, c->i_pull ? 1u : 0u);
       st(&c->in->r->receiver_ready, 1u);
       st(&c->out->r->sender_attached, 1u);
     }
@@ -382,12 +407,19 @@ class IpcTransport final : public P2PTransport {
       // both sides attached: the ring's name can go (the mappings stay)
       ::shm_unlink(c->in->name.c_str());
       c->in->owner = false;
+      c->peer_pulls = !spin_ && ld(&c->out->r->pull) != 0;  // the peer's warm-up came after it
       if (!spin_) {
         c->stop.store(false);
-        c->worker = std::thread([this, lp = &l, cp = c.get(), out = c->out] {
-          name_thread("ipc-chan");
-          worker(lp, cp, out);
-        });
+        if (!c->peer_pulls)
+          c->worker = std::thread([this, lp = &l, cp = c.get(), out = c->out] {
+            name_thread("ipc-chan");
+            worker(lp, cp, out);
+          });
+        if (c->i_pull)
+          c->rworker = std::thread([this, lp = &l, cp = c.get(), in = c->in] {
+            name_thread("ipc-pull");
+            pull_worker(lp, cp, in);
+          });
       }
     }
     l.up = true;
@@ -425,12 +457,67 @@ class IpcTransport final : public P2PTransport {
       op->event = ev;
       return true;
     }
+    if (c.peer_pulls) {
+      // offer the slice: the receiver's kernel reads it from our arena; the op completes
+      // when the receiver publishes `landed` past it
+      const auto* p = static_cast<const uint8_t*>(buf);
+      IpcRing* r = c.out->r;
+      if (p < arena_ || static_cast<uint64_t>(p - arena_) > arena_bytes_ || n > arena_bytes_ - (p - arena_)) {
+        *err = "send buffer outside the exported arena";
+        st(&r->abort, 1u);  // the sequence number is spent: the channel cannot stay in step
+        ring_wake(r);
+        return false;
+      }
+      if (seq - ld(&r->landed) >= kIpcRing) {
+        *err = "hipipc ring full";
+        st(&r->abort, 1u);
+        ring_wake(r);
+        return false;
+      }
+      IpcSlot& s = r->offers[seq % kIpcRing];
+      __atomic_store_n(&s.off, static_cast<uint64_t>(p - arena_), __ATOMIC_RELAXED);
+      __atomic_store_n(&s.n, n, __ATOMIC_RELAXED);
+      st(&r->offered, seq + 1);
+      ring_wake(r);
+      return true;
+    }
     op->state = std::make_shared<std::atomic<int>>(0);
     {
       std::lock_guard<std::mutex> q(c.qmu);
       c.pending.push_back(SendItem{static_cast<const uint8_t*>(buf), n, seq, op->state, nullptr});
     }
     ring_wake(c.out->r);
+    return true;
+  }
+
+  bool pulls_from(int peer) override {
+    Link& l = link(peer);
+    std::lock_guard<std::mutex> g(l.mu);
+    return l.up && !l.ch.empty() && l.ch[0]->i_pull;
+  }
+
+  bool post_recv_pull(int peer, int ch, uint64_t n, PullLaunch launch, P2POp* op, std::string* err) override {
+    Link& l = link(peer);
+    std::lock_guard<std::mutex> g(l.mu);
+    if (!l.up || ch < 0 || ch >= static_cast<int>(l.ch.size()) || !l.ch[ch]->i_pull) {
+      *err = "hipipc pull channel down";
+      return false;
+    }
+    Lane& c = *l.ch[ch];
+    IpcRing* r = c.in->r;
+    const uint64_t seq = c.recv_seq;
+    if (seq - ld(&r->landed) >= kIpcRing) {
+      *err = "hipipc ring full";
+      return false;
+    }
+    c.recv_seq++;
+    {
+      std::lock_guard<std::mutex> q(c.rqmu);
+      c.rpending.push_back(PullItem{n, seq, std::move(launch), nullptr});
+    }
+    op->ctx = c.in;
+    op->seq = seq;
+    ring_wake(r);
     return true;
   }
 
@@ -531,6 +618,11 @@ class IpcTransport final : public P2PTransport {
     std::deque<SendItem> pending;
     std::thread worker;
     std::atomic<bool> stop{false};
+    bool i_pull = false;      // our receives on this channel are pulled by our kernels
+    bool peer_pulls = false;  // the peer pulls our sends: post_send only offers
+    std::mutex rqmu;
+    std::deque<PullItem> rpending;  // pull receives not launched yet (rqmu)
+    std::thread rworker;
   };
   struct Link {
     std::mutex mu;  // open / close / post
@@ -576,10 +668,19 @@ class IpcTransport final : public P2PTransport {
         if (c->out) ring_wake(c->out->r);
         c->worker.join();
       }
+      if (c->rworker.joinable()) {
+        c->stop.store(true);
+        if (c->in) ring_wake(c->in->r);
+        c->rworker.join();
+      }
       {
         std::lock_guard<std::mutex> q(c->qmu);
         for (auto& it : c->pending) finish_send(it.st, -1);
         c->pending.clear();
+      }
+      {
+        std::lock_guard<std::mutex> q(c->rqmu);
+        c->rpending.clear();  // never launched: their ops fail on the abort
       }
       for (hipStream_t s : {c->send_stream, c->recv_stream})
         if (s) (void)hipStreamSynchronize(s);
@@ -590,6 +691,7 @@ class IpcTransport final : public P2PTransport {
     for (auto& c : l.ch) {
       c->in.reset();
       c->out.reset();
+      c->i_pull = c->peer_pulls = false;
     }
     l.up = false;
   }
@@ -675,6 +777,90 @@ class IpcTransport final : public P2PTransport {
     }
   }
 
+  // Receiver of one channel in pull mode: match posted receives with the sender's offers in
+  // order, launch each one's copy+checksum kernel on the channel's receive stream, and
+  // publish `landed` as their events complete (in order: one stream). A launch sees the
+  // peer's bytes only after the offer, and `landed` is published only while the channel is
+  // not aborted, checked after the kernel finished: a sender that gave up (abort, then
+  // unpinning its extent) cannot have a receive completed over bytes it no longer owned.
+  void pull_worker(Link* l, Lane* c, std::shared_ptr<RingMap> in) {
+    (void)hipSetDevice(device_);
+    IpcRing* r = in->r;
+    std::deque<PullItem> inflight;
+    int idle = 0;
+    bool dead = false;
+    auto kill = [&] {
+      st(&r->abort, 1u);
+      ring_wake(r);
+      landed_wake(r);
+      dead = true;
+    };
+    while (!c->stop.load() && !dead) {
+      bool progress = false;
+      for (;;) {
+        PullItem it;
+        {
+          std::lock_guard<std::mutex> q(c->rqmu);
+          if (c->rpending.empty() || ld(&r->offered) <= c->rpending.front().seq) break;
+          it = std::move(c->rpending.front());
+          c->rpending.pop_front();
+        }
+        const IpcSlot& s = r->offers[it.seq % kIpcRing];
+        const uint64_t off = __atomic_load_n(&s.off, __ATOMIC_RELAXED), n = __atomic_load_n(&s.n, __ATOMIC_RELAXED);
+        hipEvent_t ev = nullptr;
+        if (n != it.n || off > l->peer_arena_bytes || n > l->peer_arena_bytes - off || ld(&r->abort) ||
+            (n && it.launch(l->peer_arena + off, c->recv_stream) != 0) || !(ev = event()) ||
+            hipEventRecord(ev, c->recv_stream) != hipSuccess) {
+          if (ev) release_event(ev);
+          kill();  // mismatched sizes or a failed launch end the channel (as RCCL would)
+          inflight.push_back(std::move(it));  // a launch that did queue work drains below
+          break;
+        }
+        __atomic_fetch_add(&r->enqueued, 1ull, __ATOMIC_RELAXED);
+        it.ev = ev;
+        inflight.push_back(std::move(it));
+        progress = true;
+      }
+      while (!dead && !inflight.empty()) {
+        hipError_t q = hipEventQuery(inflight.front().ev);
+        if (q == hipErrorNotReady) break;
+        PullItem& it = inflight.front();
+        if (q == hipSuccess && !__atomic_load_n(&r->abort, __ATOMIC_SEQ_CST)) {
+          st(&r->landed, it.seq + 1);
+          landed_wake(r);
+        } else {
+          kill();
+          break;
+        }
+        release_event(it.ev);
+        inflight.pop_front();
+        progress = true;
+      }
+      if (dead || ld(&r->abort)) break;
+      if (progress) {
+        idle = 0;
+        continue;
+      }
+      if (!inflight.empty()) {
+        if (++idle < 64) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(10));
+        continue;
+      }
+      const uint32_t bell = __atomic_load_n(&r->doorbell, __ATOMIC_ACQUIRE);
+      {
+        std::lock_guard<std::mutex> q(c->rqmu);
+        if (!c->rpending.empty() && ld(&r->offered) > c->rpending.front().seq) continue;
+      }
+      timespec ts{0, 2'000'000};
+      futex(&r->doorbell, FUTEX_WAIT, bell, &ts);
+    }
+    // stopping: kernels already queued finish (they read the peer's mapping, which stays
+    // until teardown unmaps it after this); their receives fail on the abort
+    (void)hipStreamSynchronize(c->recv_stream);
+    for (auto& it : inflight)
+      if (it.ev) release_event(it.ev);
+  }
+
   // One slice into the peer's extent: by kernel (default), or by the copy engines
   // (DFS_IPC_COPY=sdma, the round-4 path), or by the engines when the pointers are not
   // 16-byte aligned or the peer's memory is not reachable from this device's waves.
@@ -712,6 +898,7 @@ class IpcTransport final : public P2PTransport {
   uint64_t arena_bytes_;
   bool spin_;
   int channels_;
+  bool pull_;
   uint64_t spin_ticks_ = 0;
   hipIpcMemHandle_t arena_h_{}, probe_h_{};
   uint8_t* probe_ = nullptr;
@@ -726,13 +913,14 @@ class IpcTransport final : public P2PTransport {
 }  // namespace
 
 std::unique_ptr<P2PTransport> make_ipc_transport(int device, int rank, const std::string& ns, uint8_t* arena,
-                                                 uint64_t arena_bytes, bool spin, int channels, std::string* err) {
+                                                 uint64_t arena_bytes, bool spin, int channels, std::string* err,
+                                                 bool pull) {
   if (device < 0 || arena == nullptr || arena_bytes == 0) {
     *err = "hipipc transport requires a GPU chunk store";
     return nullptr;
   }
   auto t = std::make_unique<IpcTransport>(device, rank, ns, arena, arena_bytes, spin,
-                                          std::max(1, std::min(channels, kMaxP2PChannels)));
+                                          std::max(1, std::min(channels, kMaxP2PChannels)), pull);
   if (!t->init(err)) return nullptr;
   return t;
 }

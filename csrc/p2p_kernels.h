@@ -35,7 +35,13 @@ struct alignas(64) IpcRing {
   alignas(64) uint32_t sender_attached;
   uint32_t receiver_ready;
   uint64_t warm;                   // generation whose warm-up copy the sender delivered
+  uint32_t pull;                   // receiver: 1 = I pull (set before my warm-up is published)
   alignas(64) IpcSlot slots[kIpcRing];
+  // receiver pull: the sender offers each slice (offset in ITS arena, length) and the
+  // receiver's kernel reads it over xGMI; `landed` then counts the slices the receiver's
+  // kernels finished, which is also what completes the sender's op
+  alignas(64) uint64_t offered;    // slices offered (count); sender writes
+  alignas(64) IpcSlot offers[kIpcRing];
 };
 
 struct IpcSendArgs {

@@ -19,7 +19,8 @@
 //    channel and direction; buffers are HBM pointers of our GPU, each op records a hipEvent.
 //  * IpcTransport   (p2p_ipc.cpp): HIP IPC between processes of one node; the receiver
 //    publishes each posted buffer (an offset in its exported arena) on a shared-memory ring,
-//    the sender's copy engine writes the slice there and bumps the ring's landed count. No
+//    the sender's copy kernel writes the slice there and bumps the ring's landed count; or,
+//    in pull mode, the sender offers the slice and the receiver's copy+checksum kernel reads it. No
 //    kernel ever waits on a peer, so no hardware queue can be held by a peer (see p2p_ipc.cpp).
 //  * SocketTransport (p2p_socket.cpp): a UNIX stream socket per direction and a worker
 //    thread per direction draining the FIFO of posted ops; buffers are host memory. It is
@@ -30,6 +31,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <thread>
@@ -75,6 +77,23 @@ class P2PTransport {
   }
   virtual void release(P2POp* op) = 0;
 
+  // Receiver pull (hipipc with DFS_IPC_PULL, the default where this device's waves reach the
+  // peer's memory): the receiver moves the bytes itself, with a kernel that also checksums
+  // what it moves, instead of the sender's copy plus a separate checksum pass on arrival.
+  // pulls_from(peer): the receives from `peer` must be posted with post_recv_pull. `launch`
+  // runs on the transport's receive worker once the matching send is offered, with the
+  // sender's bytes (a device pointer into the peer's mapped arena) and the channel's stream
+  // (a hipStream_t); the op completes once the work it queued there finished. The closure
+  // must own what it references: it can outlive the receive that posted it (an abandoned
+  // receive's launch may still run until close()).
+  using PullLaunch = std::function<int(const uint8_t* src, void* stream)>;  // 0 = queued
+  virtual bool pulls_from(int /*peer*/) { return false; }
+  virtual bool post_recv_pull(int /*peer*/, int /*ch*/, uint64_t /*n*/, PullLaunch /*launch*/, P2POp* /*op*/,
+                              std::string* err) {
+    *err = "transport has no receiver pull";
+    return false;
+  }
+
   // Test hooks (socket transport only; no-ops elsewhere): the next `n` sends to `peer`
   // vanish (never delivered), or the channel to `peer` stalls for `ms`.
   virtual void debug_drop_sends(int /*peer*/, int /*n*/) {}
@@ -105,7 +124,10 @@ std::unique_ptr<P2PTransport> make_hiploop_transport(int device, int rank, const
 // arena over HIP IPC; a matched send is a one-sided copy into the receiver's posted extent
 // (xGMI between GPUs, an in-HBM copy when ranks share one GPU). `spin` = RCCL emulation:
 // spinning send/wait kernels on the channel streams instead of host-driven copies.
+// `pull`: receive by receiver-side kernels (P2PTransport::post_recv_pull) where this device
+// reaches the peer's memory; the peer learns it at open() and offers instead of copying.
 std::unique_ptr<P2PTransport> make_ipc_transport(int device, int rank, const std::string& ns, uint8_t* arena,
-                                                 uint64_t arena_bytes, bool spin, int channels, std::string* err);
+                                                 uint64_t arena_bytes, bool spin, int channels, std::string* err,
+                                                 bool pull = false);
 
 }  // namespace dfs

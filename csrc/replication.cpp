@@ -86,8 +86,11 @@ std::unique_ptr<P2PTransport> make_transport(const std::string& name, ChunkStore
   if (name == "hipipc" || name == "hipipc-spin") {
     const char* sp = std::getenv("DFS_IPC_SPIN");
     const bool spin = name == "hipipc-spin" || (sp && std::string(sp) == "1");
+    // receiver pull (one copy+checksum kernel per hop, on the receiver) unless DFS_IPC_PULL=0
+    const char* pe = std::getenv("DFS_IPC_PULL");
+    const bool pull = !spin && store->can_pull() && !(pe && std::string(pe) == "0");
     return make_ipc_transport(store->config().device, rank, ns, store->arena_base(), store->arena_bytes(), spin,
-                              channels, err);
+                              channels, err, pull);
   }
   *err = "unknown transport " + name;
   return nullptr;
@@ -716,6 +719,16 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
   }
   uint8_t* dst = dev ? ext.ptr : host.data();
   std::vector<P2POp> ops;
+  // receiver pull: our kernels move and checksum the slices as the sender offers them, so
+  // the receive's .meta scratch exists before the first slice is posted
+  ChunkStore::RecvVerify rv;
+  const bool pull = dev && t_->pulls_from(src);
+  if (pull && !store_->recv_begin(&rv, ext, size, true)) {
+    res.error = "no pinned scratch for a pulled receive";
+    store_->release(ext);
+    fail_pair_gen(src, gen, res.error);  // the sender's offer can never be consumed now
+    return res;
+  }
   const auto t0 = Clock::now();
   {
     std::unique_lock<std::mutex> lk(P.mu);
@@ -746,7 +759,9 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
       std::string err;
       for (uint64_t off = 0; off < size; off += slice) {
         P2POp op;
-        if (!t_->post_recv(src, ch, dst + off, std::min(slice, size - off), &op, &err)) {
+        const uint64_t len = std::min(slice, size - off);
+        if (pull ? !t_->post_recv_pull(src, ch, len, store_->recv_pull(&rv, off, off + len), &op, &err)
+                 : !t_->post_recv(src, ch, dst + off, len, &op, &err)) {
           why = "post_recv failed: " + err;
           fail = true;
           break;
@@ -760,6 +775,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
     }
     if (!why.empty()) {
       lk.unlock();
+      if (pull) store_->recv_abandon(&rv);
       for (auto& op : ops) t_->release(&op);
       if (fail) fail_pair_gen(src, gen, why);
       // an extent that a posted receive may still write into waits for the pair's rebuild
@@ -770,8 +786,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
     }
   }
   const auto t1 = Clock::now();
-  ChunkStore::RecvVerify rv;
-  if (dev) store_->recv_begin(&rv, ext, size);
+  if (dev && !pull) store_->recv_begin(&rv, ext, size);
   auto deadline = Clock::now() + std::chrono::milliseconds(opt_.xfer_timeout_ms);
   std::string why;
   int spins = 0;
@@ -797,8 +812,9 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
       if (spins < 64) std::this_thread::yield();
       else if (t_->wait(&ops[s], 2000) != 0) continue;
     }
-    // slice s landed: checksum it on the lane while s+1.. are still on the link
-    if (why.empty() && dev) store_->recv_slice(&rv, s * slice, std::min(size, (s + 1) * slice));
+    // slice s landed: checksum it on the lane while s+1.. are still on the link (pulled
+    // slices were checksummed by the kernel that moved them)
+    if (why.empty() && dev && !pull) store_->recv_slice(&rv, s * slice, std::min(size, (s + 1) * slice));
   }
   for (auto& op : ops) t_->release(&op);
   if (!why.empty()) {

@@ -11,6 +11,8 @@
 #   n2        2 ranks sharing the GPU (hipipc, RF 2)
 #   n2hbm     the same with hbm-ack durability (the shared volume out of the ack path)
 #   n4        the driver's N=4 command on 4 ranks sharing the GPU
+#   ipctest   the device-replication GPU tests only
+#   pullab    replica hops, receiver pull vs push (hbm-ack, conc 10 and 1)
 #   prof      rocprofv3 kernel trace of the chunkserver during a short bench
 #   configs   BASELINE configs 4 and 5
 #   config3 / config4   one of them (config 4 at the reference's compose topology: 4 chunkservers, RF 3)
@@ -60,6 +62,17 @@ for step in "$@"; do
     n2phase)  # replica hop phases (repl_phase_us) at concurrency 1 and 10, hbm-ack
       run n2p_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 && \
       run n2p_c10 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack || exit 1 ;;
+    ipctest)  # the device-replication GPU tests only (hipipc pull / push / spin, multi-GPU)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_ipc.py tests/test_gpu_replication.py tests/test_gpu_multi.py \
+        -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > "$O/pytest_ipc.log" 2>&1 || \
+        { tail -30 "$O/pytest_ipc.log"; exit 1; }
+      tail -3 "$O/pytest_ipc.log" ;;
+    pullab)   # replica hops at hbm-ack: receiver pull (one kernel per hop) vs the round-5 push + checksum
+      run n2_pull 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack && \
+      DFS_IPC_PULL=0 run n2_push 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack && \
+      run n2_pull_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 && \
+      DFS_IPC_PULL=0 run n2_push_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack \
+        --concurrency 1 || exit 1 ;;
     n2prof)   # rocprofv3 kernel + marker + memory-copy traces of both chunkservers, 2 ranks, conc 1
       DFS_PROF_EXTRA=--memory-copy-trace run n2prof 600 python bench.py --gpus 2 --steps 5 --warmup 1 \
         --durability hbm-ack --concurrency 1 --remote-steps 0 --profile-dir "$O/n2prof" || exit 1 ;;

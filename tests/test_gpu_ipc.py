@@ -4,8 +4,10 @@ HIP IPC, and every replica slice is a one-sided copy into the receiver's posted 
 checksummed (K1) as it lands. Crossing RF=3 traffic from four co-located clients at
 concurrency 10, blocks up to 64 MiB.
 
-Run twice: the production mode (host-driven copies: no kernel ever waits on a peer) and
-spin mode, the RCCL emulation in which every send and receive is a kernel parked on its
+Run three ways: the production mode, receiver pull (the sender offers each slice, the
+receiver's crc_write_copy_kernel reads it from the sender's arena, stores it and writes the
+.meta words in one pass: one kernel per hop); the round-5 push mode (DFS_IPC_PULL=0: the
+sender's copy kernel, then a checksum kernel on arrival); and spin mode, the RCCL emulation in which every send and receive is a kernel parked on its
 channel stream until the peer shows up (p2p_kernels.hip) — the shape that can couple
 unrelated streams through GPU_MAX_HW_QUEUES hardware queues. Reference semantics:
 dfs/chunkserver/src/chunkserver.rs:777-829,1039-1077 (replicas_written)."""
@@ -69,7 +71,7 @@ def totals(c: LocalCluster):
     for u in c.cs_http:
         s = stats(u)
         for k in ("fp_rccl_forwards", "fp_p2p_fallbacks", "fp_replica_failures", "fp_shm_forwards",
-                  "repl_pair_failures", "repl_turn_timeouts", "repl_bytes_recv", "grpc_forwards"):
+                  "repl_pair_failures", "repl_turn_timeouts", "repl_bytes_recv", "grpc_forwards", "pulled_recvs"):
             agg[k] = agg.get(k, 0) + s.get(k, 0)
         agg.setdefault("transports", set()).add(s.get("repl_transport"))
         agg.setdefault("pairs_up", 0)
@@ -77,22 +79,29 @@ def totals(c: LocalCluster):
     return agg
 
 
-@pytest.mark.parametrize("mode", ["hipipc", "hipipc-spin"])
+@pytest.mark.parametrize("mode", ["hipipc", "hipipc-push", "hipipc-spin"])
 def test_four_processes_one_gpu_crossing_traffic(mode):
     from rust_hadoop_generated_by_llm_amd import native
 
     if native.gpu_count() < 1:
         pytest.fail("GPU test selected but no HIP device is visible")
     env = {"DFS_IPC_SPIN_MS": "4000"}
-    with LocalCluster(gpus=[0, 0, 0, 0], p2p=mode, fsync=False, hbm_capacity="6G", env=env) as c:
+    transport = "hipipc" if mode == "hipipc-push" else mode
+    if mode == "hipipc-push":
+        env["DFS_IPC_PULL"] = "0"
+    with LocalCluster(gpus=[0, 0, 0, 0], p2p=transport, fsync=False, hbm_capacity="6G", env=env) as c:
         base = totals(c)
-        assert base["transports"] == {mode} and base["pairs_up"] == 12, base
+        assert base["transports"] == {transport} and base["pairs_up"] == 12, base
+        # odd sizes: a short tail slice (700,000 and 3 MiB + 17 B), several slices (64 MiB)
         sizes = [700_000, 1 << 20, 3 * (1 << 20) + 17, 64 << 20]
-        elapsed = run_crossing(c, 48, sizes, seed=7 if mode == "hipipc" else 8)
+        elapsed = run_crossing(c, 48, sizes, seed={"hipipc": 7, "hipipc-push": 9}.get(mode, 8))
         t = totals(c)
         writes = 48
         print(f"\n{mode}: {writes} RF=3 writes in {elapsed:.2f}s; {t}")
         assert t["fp_rccl_forwards"] - base["fp_rccl_forwards"] == writes * 2, t
         assert t["fp_p2p_fallbacks"] == 0 and t["fp_replica_failures"] == 0 and t["fp_shm_forwards"] == 0, t
         assert t["repl_pair_failures"] == 0 and t["repl_turn_timeouts"] == 0, t
+        # every replica of the pull mode came through the receivers' copy+checksum kernels
+        pulled = t["pulled_recvs"] - base["pulled_recvs"]
+        assert pulled == (writes * 2 if mode == "hipipc" else 0), t
         assert elapsed < 120
