@@ -972,7 +972,9 @@ void ChunkStore::insert_resident(const std::string& id, const DevExtent& ext, ui
       b.jrec = *jr;
       b.jmeta = std::move(meta);
       enqueue_materialize_locked(id, b);
-    } else if (!on_disk && !hbm_ack) {
+    } else if (!on_disk) {
+      // nvme-sync: persist_staged's .meta image; hbm-ack: the spill's, which then needs no
+      // device-to-host copy of it
       b.staged_meta = std::move(meta);
     }
     touch_locked(id, b);
@@ -1872,9 +1874,10 @@ struct ChunkStore::PinnedPool {
 };
 struct ChunkStore::PullScratch {
   std::shared_ptr<PinnedPool> pool;
-  uint8_t* host = nullptr;
+  uint8_t* host = nullptr;  // [0, S*4): the .meta image; [data_off, data_off + n): the bytes
   uint8_t* dev = nullptr;
   uint64_t cap = 0;
+  uint64_t data_off = 0;  // 0: no host copy of the bytes
   ~PullScratch() {
     if (!host) return;
     std::lock_guard<std::mutex> g(pool->mu);
@@ -1884,27 +1887,37 @@ struct ChunkStore::PullScratch {
 
 bool ChunkStore::can_pull() const { return gpu() && crc_mfma_enabled() && dtables_ && pull_parts_dev_; }
 
-bool ChunkStore::recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n, bool pull) {
+bool ChunkStore::recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n, bool pull, bool persist_now) {
   rv->ext = e;
   rv->n = n;
   rv->pull.reset();
   if (pull) {
     if (!can_pull()) return false;
-    const uint64_t want = align_up(num_slices(n) * 4 + 16, 4096);
+    // DFS_PULL_HOST=1: the pull kernel also leaves an nvme-sync replica's bytes in pinned host
+    // memory and the journal appends from there, instead of from HBM through a lane's pinned
+    // chunks. Measured a wash at 2 ranks (landing +30 us, the append's copy -30 us, inside a
+    // ~2 ms fdatasync round: profiles/r6/pull/n2_pullhost*.json vs n2_pulldev.json), so off.
+    static const bool host_ok = env_int("DFS_PULL_HOST", 0) != 0;
+    const bool host_copy = host_ok && persist_now && cfg_.durability == Durability::NvmeSync && journal_ &&
+                           n <= (16ull << 20) && n > 0;
+    const uint64_t meta_bytes = align_up(num_slices(n) * 4 + 16, 4096);
+    const uint64_t want = meta_bytes + (host_copy ? align_up(n, 4096) : 0);
     auto sc = std::make_shared<PullScratch>();
     sc->pool = pull_pool_;
     {
       std::lock_guard<std::mutex> g(pull_pool_->mu);
       auto& fr = pull_pool_->free;
-      for (size_t i = 0; i < fr.size(); ++i)
-        if (fr[i].second >= want) {
-          sc->host = fr[i].first;
-          sc->cap = fr[i].second;
-          fr[i] = fr.back();
-          fr.pop_back();
-          break;
-        }
+      size_t best = fr.size();
+      for (size_t i = 0; i < fr.size(); ++i)  // best fit: meta-only and host-copy receives share the pool
+        if (fr[i].second >= want && (best == fr.size() || fr[i].second < fr[best].second)) best = i;
+      if (best < fr.size()) {
+        sc->host = fr[best].first;
+        sc->cap = fr[best].second;
+        fr[best] = fr.back();
+        fr.pop_back();
+      }
     }
+    if (host_copy) sc->data_off = meta_bytes;
     if (!sc->host) {
       (void)hipSetDevice(cfg_.device);
       if (hipHostMalloc(reinterpret_cast<void**>(&sc->host), want, hipHostMallocDefault) != hipSuccess) {
@@ -1975,6 +1988,7 @@ std::function<int(const uint8_t*, void*)> ChunkStore::recv_pull(RecvVerify* rv, 
                     lo / kSliceBytes;
   std::shared_ptr<PullScratch> sc = rv->pull;
   uint32_t* mh = sc ? reinterpret_cast<uint32_t*>(sc->dev) + lo / kSliceBytes : nullptr;
+  uint8_t* hdst = sc && sc->data_off ? sc->dev + sc->data_off + lo : nullptr;
   const DevCrcTables* tables = dtables_;
   uint32_t* parts = pull_parts_dev_;
   return [=](const uint8_t* src, void* stream) -> int {
@@ -1987,6 +2001,7 @@ std::function<int(const uint8_t*, void*)> ChunkStore::recv_pull(RecvVerify* rv, 
     w.c.part_crc = parts;  // partials of the slice: unread (recv_finish combines the .meta words)
     w.dst = dst;
     w.meta_host = mh;
+    w.dst_host = hdst;
     return launch_write_copy(w, tables, p.grid, static_cast<hipStream_t>(stream)) == hipSuccess ? 0 : -1;
   };
 }
@@ -1996,11 +2011,12 @@ WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint3
   WriteResult res;
   uint64_t n = rv->n, S = num_slices(n);
   std::shared_ptr<std::vector<uint8_t>> meta;
+  std::shared_ptr<PullScratch> pulled;  // holds the host copy of the bytes until the append
   if (rv->pull) {
     // every slice's kernel finished before the transport completed the receive: the .meta
-    // image is already in the pinned scratch
+    // image (and, for an nvme-sync replica, the bytes) are already in the pinned scratch
     meta = std::make_shared<std::vector<uint8_t>>(rv->pull->host, rv->pull->host + S * 4);
-    rv->pull.reset();
+    pulled = std::move(rv->pull);
     pulled_recvs_++;
   } else {
     Lane* l = static_cast<Lane*>(recv_lane(rv));
@@ -2044,7 +2060,9 @@ WriteResult ChunkStore::recv_finish(RecvVerify* rv, const std::string& id, uint3
   const bool jok = sync_now && journal_takes(n, S);
   std::unique_ptr<FileClaim> claim;
   if (sync_now && !jok && journal_) claim = std::make_unique<FileClaim>(this, id);
-  if (jok ? !journal_block(id, nullptr, rv->ext.ptr, n, crc, *meta, &jr, &err)
+  const uint8_t* host_bytes = pulled && pulled->data_off ? pulled->host + pulled->data_off : nullptr;
+  if (host_bytes) pulled_host_appends_++;
+  if (jok ? !journal_block(id, host_bytes, host_bytes ? nullptr : rv->ext.ptr, n, crc, *meta, &jr, &err)
           : sync_now && (!persist_from_device(id, rv->ext.ptr, n, meta->data(), S, &err) ||
                          !supersede_file(id, &err))) {
     release(rv->ext);
@@ -2073,6 +2091,7 @@ void ChunkStore::spill_worker() {
     std::string id;
     uint64_t size = 0;
     const uint8_t* d = nullptr;
+    std::shared_ptr<std::vector<uint8_t>> smeta;
     {
       std::unique_lock<std::mutex> lk(mu_);
       cv_.wait(lk, [&] { return stop_ || (!spill_paused_ && !spill_q_.empty()); });
@@ -2084,6 +2103,7 @@ void ChunkStore::spill_worker() {
       it->second.pins++;
       size = it->second.size;
       d = arena_ + it->second.dev_off;
+      smeta = it->second.staged_meta;
     }
     DiskGate::Slot slot = gate_ ? gate_->acquire() : DiskGate::Slot{};
     Lane* l = acquire_lane();
@@ -2107,7 +2127,9 @@ void ChunkStore::spill_worker() {
       }
       ok = write_all(fd, l->pinned[c & 1], len, off);
     }
-    if (ok && S) {
+    if (ok && S && smeta && smeta->size() == S * 4) {
+      std::memcpy(hmeta, smeta->data(), S * 4);  // kept from the write: no readback
+    } else if (ok && S) {
       ok = hipMemcpyAsync(hmeta, d + align_up(std::max<uint64_t>(size, 1), 256), S * 4, hipMemcpyDeviceToHost,
                           l->stream) == hipSuccess &&
            hipStreamSynchronize(l->stream) == hipSuccess;
@@ -2140,6 +2162,7 @@ void ChunkStore::spill_worker() {
         if (ok && it->second.size == size) {
           it->second.dirty = false;
           it->second.on_disk = true;
+          it->second.staged_meta.reset();
         } else if (!ok) {
           spill_q_.push_back(id);  // retry later
         }
@@ -2489,6 +2512,7 @@ StoreStats ChunkStore::stats() {
   s.fused_reads = fused_reads_.load();
   s.fused_writes = fused_writes_.load();
   s.pulled_recvs = pulled_recvs_.load();
+  s.pulled_host_appends = pulled_host_appends_.load();
   s.sliced_stages = sliced_stages_.load();
   s.staged_dma = staged_dma_.load();
   s.mirror_hits = mirror_hits_;

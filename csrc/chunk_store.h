@@ -91,6 +91,7 @@ struct StoreStats {
   uint64_t fused_reads = 0;      // reads delivered by the K3 verify+copy kernel (no SDMA copy)
   uint64_t fused_writes = 0;     // writes staged by the K1/K2 copy+checksum kernel (no SDMA copy)
   uint64_t pulled_recvs = 0;  // replica receives moved by the receiver's copy+checksum kernel
+  uint64_t pulled_host_appends = 0;  // ... whose journal append read the kernel's host copy
   uint64_t sliced_stages = 0;    // pipelined head writes (per-slice fused kernels, sends overlap)
   uint64_t staged_dma = 0;       // copies bounced through pinned staging buffers
   uint64_t host_registered_bytes = 0;
@@ -229,8 +230,10 @@ class ChunkStore {
     std::shared_ptr<PullScratch> pull;  // receiver pull (recv_begin(..., true))
   };
   // pull: the slices arrive through recv_pull's kernels (the transport launches them), not
-  // recv_slice; returns false if the store cannot (no matrix-core CRC path, no pinned memory)
-  bool recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n, bool pull = false);
+  // recv_slice; returns false if the store cannot (no matrix-core CRC path, no pinned memory).
+  // persist_now (pull only): an nvme-sync receive whose record the journal appends — the
+  // kernels also leave the bytes in pinned host memory, so no device-to-host copy follows
+  bool recv_begin(RecvVerify* rv, const DevExtent& e, uint64_t n, bool pull = false, bool persist_now = false);
   // Receiver pull: the launch of bytes [lo, hi) of the receive (lo a multiple of 512): one
   // crc_write_copy_kernel that reads the sender's bytes (a device pointer into its mapped
   // arena), stores them into the extent and writes the slices' .meta words to HBM and to the
@@ -474,6 +477,7 @@ class ChunkStore {
   std::shared_ptr<PinnedPool> pull_pool_;  // receiver-pull .meta scratch (outlives closures)
   uint32_t* pull_parts_dev_ = nullptr;    // the pull kernels' whole-block partials (unread)
   std::atomic<uint64_t> pulled_recvs_{0};
+  std::atomic<uint64_t> pulled_host_appends_{0};  // pulled replicas appended from their host copy
   std::atomic<int> staging_{0};            // device stagings in flight (fused vs SDMA choice)
   std::atomic<uint64_t> sliced_stages_{0};
   bool write_copy(Lane* l, const uint8_t* src_dev, uint8_t* dst, uint64_t n, uint32_t* dmeta, uint8_t* hmeta,

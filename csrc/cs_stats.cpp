@@ -36,6 +36,7 @@ Json stats_json(const StoreStats& t) {
   d.set("fused_reads", t.fused_reads);
   d.set("fused_writes", t.fused_writes);
   d.set("pulled_recvs", t.pulled_recvs);
+  d.set("pulled_host_appends", t.pulled_host_appends);
   d.set("sliced_stages", t.sliced_stages);
   d.set("staged_dma", t.staged_dma);
   d.set("host_registered_bytes", t.host_registered_bytes);

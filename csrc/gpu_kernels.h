@@ -150,6 +150,9 @@ struct WriteCopyLaunch {
   CrcLaunch c;
   uint8_t* dst;
   uint32_t* meta_host;
+  // optional second copy of the bytes into device-visible host memory (16 B aligned): a
+  // pulled replica that the journal appends from the host, with no device-to-host copy
+  uint8_t* dst_host = nullptr;
 };
 // True when launch_crc runs a block of `ntiles` tiles on the kernel that honours
 // CrcLaunch::meta_host (the LDS kernel, below the MFMA size threshold).

@@ -862,6 +862,7 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
     if (t + 1 < t_end) nxt = load_wave(c.data, first_slice(t + 1), lo, hi, lane);
     const int64_t i0 = first_slice(t);
     store_wave_dst(a.dst, i0, lo, hi, cur, lane);
+    if (a.dst_host) store_wave_dst(a.dst_host, i0, lo, hi, cur, lane);
     uint32_t r = slice_from_chunks(lt, wave_chunk_crcs(A, cur, lane), lane);
     const int64_t i = i0 + sw;
     if (i >= lo && i < hi && sl == 0) {
@@ -885,7 +886,11 @@ __global__ __launch_bounds__(kCrcWgThreads) __attribute__((amdgpu_waves_per_eu(3
       a.meta_host[c.s_full] = be;
     }
     uint8_t* out = a.dst + c.s_full * 512;
-    for (uint32_t k = lane; k < c.tail_len; k += 64) out[k] = base[k];
+    uint8_t* hout = a.dst_host ? a.dst_host + c.s_full * 512 : nullptr;
+    for (uint32_t k = lane; k < c.tail_len; k += 64) {
+      out[k] = base[k];
+      if (hout) hout[k] = base[k];
+    }
   }
   for (int k = wave; k < 3; ++k) acc = tab4(lt.sh4k, acc);
   uint64_t e = t_begin < t_end ? c.ntiles - t_end : 0;
@@ -1474,7 +1479,8 @@ hipError_t launch_write_copy(const WriteCopyLaunch& a, const DevCrcTables* t, in
   if (grid <= 0) return hipSuccess;
   // part_crc holds kMaxGridCrc words; the plan must be a whole block (K1/K2, no verify)
   if (grid > kMaxGridCrc || a.c.slice_lo != 0 || a.c.slice_hi != a.c.s_full || !a.c.meta_out || !a.meta_host ||
-      !a.c.part_crc || !a.dst || (reinterpret_cast<uintptr_t>(a.c.data) | reinterpret_cast<uintptr_t>(a.dst)) % 16)
+      !a.c.part_crc || !a.dst ||
+      (reinterpret_cast<uintptr_t>(a.c.data) | reinterpret_cast<uintptr_t>(a.dst) | reinterpret_cast<uintptr_t>(a.dst_host)) % 16)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(crc_write_copy_kernel, dim3(grid), dim3(kCrcWgThreads), 0, s, a, t);
   return hipGetLastError();

@@ -723,7 +723,7 @@ WriteResult ReplicationEngine::recv(int src, uint64_t gen, int ch, int64_t seq, 
   // the receive's .meta scratch exists before the first slice is posted
   ChunkStore::RecvVerify rv;
   const bool pull = dev && t_->pulls_from(src);
-  if (pull && !store_->recv_begin(&rv, ext, size, true)) {
+  if (pull && !store_->recv_begin(&rv, ext, size, true, persist_now)) {
     res.error = "no pinned scratch for a pulled receive";
     store_->release(ext);
     fail_pair_gen(src, gen, res.error);  // the sender's offer can never be consumed now

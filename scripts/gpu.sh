@@ -13,6 +13,7 @@
 #   n4        the driver's N=4 command on 4 ranks sharing the GPU
 #   ipctest   the device-replication GPU tests only
 #   pullab    replica hops, receiver pull vs push (hbm-ack, conc 10 and 1)
+#   pullhost  2 ranks nvme-sync: pulled replicas appended from the kernel's host copy vs HBM vs push
 #   prof      rocprofv3 kernel trace of the chunkserver during a short bench
 #   configs   BASELINE configs 4 and 5
 #   config3 / config4   one of them (config 4 at the reference's compose topology: 4 chunkservers, RF 3)
@@ -73,6 +74,11 @@ for step in "$@"; do
       run n2_pull_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 && \
       DFS_IPC_PULL=0 run n2_push_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack \
         --concurrency 1 || exit 1 ;;
+    pullhost) # 2 ranks nvme-sync: pulled replicas appended from the kernel's host copy / from HBM / push
+      DFS_PULL_HOST=1 run n2_pullhost 600 python bench.py --gpus 2 --steps 10 --warmup 2 && \
+      run n2_pulldev 600 python bench.py --gpus 2 --steps 10 --warmup 2 && \
+      DFS_IPC_PULL=0 run n2_pushnv 600 python bench.py --gpus 2 --steps 10 --warmup 2 && \
+      DFS_PULL_HOST=1 run n2_pullhost_b 600 python bench.py --gpus 2 --steps 10 --warmup 2 || exit 1 ;;
     n2prof)   # rocprofv3 kernel + marker + memory-copy traces of both chunkservers, 2 ranks, conc 1
       DFS_PROF_EXTRA=--memory-copy-trace run n2prof 600 python bench.py --gpus 2 --steps 5 --warmup 1 \
         --durability hbm-ack --concurrency 1 --remote-steps 0 --profile-dir "$O/n2prof" || exit 1 ;;
