@@ -287,6 +287,15 @@ def main():
         rank_dir.mkdir(parents=True, exist_ok=True)
         journal_segs = _journal_segments(base_p if rank % len(vols) == 0 else my_vol,
                                          _bytes_needed(a, n) * len(on_vol) // max(1, n), len(on_vol))
+        # A run whose replicas do not fit its volumes (N ranks x RF copies of every step on one
+        # shared device) deletes each step's files after reading them back, so the journals
+        # reclaim them as the run goes: extra work inside the timed region (the number is
+        # conservative, not inflated), reported as `reclaim_between_steps`. Without it the
+        # journals would grow until the volume is full and the writers stall.
+        my_room = _free_bytes(base_p if rank % len(vols) == 0 else my_vol) - (6 << 30)
+        my_need = _bytes_needed(a, n) * len(on_vol) // max(1, n)
+        reclaim_steps = os.environ.get("DFS_BENCH_RECLAIM", "auto") == "1" or (
+            os.environ.get("DFS_BENCH_RECLAIM", "auto") == "auto" and any(gather(my_need > my_room)))
         env = dict(os.environ)
         env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
         env.setdefault("DFS_LOG", "warning")
@@ -446,6 +455,8 @@ def main():
                                         payloads=payloads, run_id=tag, pool=tpool)
                 verify = {nm: payloads[i % len(payloads)] for i, nm in enumerate(names)} if tag == "w0" else None
                 rs = bench_read(client, files=names, pool=tpool, verify=verify)
+                if reclaim_steps:
+                    list(tpool.map(client.delete_file, names))
                 return ws, rs
 
             for w in range(a.warmup):
@@ -696,6 +707,7 @@ def main():
                                          for end in ("start", "end")}} if any(r["cs"].get("journal") for r in allr) else None,
                     # where each rank's replicas live and how much of the volume they take
                     "volume": {"per_rank": [r["vol"] for r in allr], "free_bytes_after": _free_bytes(base_p),
+                               "reclaim_between_steps": reclaim_steps,
                                # every rank appending 1 MiB journal records at once after the timed
                                # region (io_bench --roofline, conc threads each): per-rank MB/s, sum
                                "roofline_mb_s": [(r["roof"] or {}).get("roofline_mb_s") for r in allr],

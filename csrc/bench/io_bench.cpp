@@ -29,6 +29,7 @@
 #include <thread>
 #include <vector>
 
+#include "trace.h"
 #include "chunk_store.h"
 #include "disk_gate.h"
 #include "crc32.h"
@@ -503,6 +504,7 @@ static void roofline(const std::string& dir, int threads, int per) {
 }
 
 int main(int argc, char** argv) {
+  dfs::trace_init();  // before any thread: roctx's first range calls setenv (trace.h)
   for (int i = 1; i < argc; ++i)
     if (std::string(argv[i]) == "--md5") {
       int conc = 10, per = 20;

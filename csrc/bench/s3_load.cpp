@@ -44,6 +44,7 @@
 #include <thread>
 #include <vector>
 
+#include "trace.h"
 #include "sigv4.h"
 
 namespace {
@@ -231,6 +232,7 @@ std::string xml_text(const std::string& body, const std::string& tag) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  dfs::trace_init();  // before any thread: roctx's first range calls setenv (trace.h)
   Opts o;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];

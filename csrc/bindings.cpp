@@ -8,6 +8,7 @@
 
 #include <chrono>
 
+#include "trace.h"
 #include "chunk_store.h"
 #include "crc32.h"
 #include "crypto.h"
@@ -107,6 +108,7 @@ py::object json_to_py(const Json& j) {
 
 PYBIND11_MODULE(_dfs_native, m) {
   m.doc() = "MI355X-native data plane: HBM chunk store, CDNA4 CRC/RS kernels, RCCL replication, WAL";
+  dfs::trace_init();  // at import, before the module starts a thread (trace.h)
 
   // ---------------- checksums
   m.def("copy_into", [](py::buffer dst, uint64_t off, py::buffer src) {

@@ -1119,6 +1119,15 @@ void bind_meta(py::module_& m) {
       .def_property_readonly("ec_device_writes", &FastClient::ec_device_writes)
       .def_property_readonly("ec_device_reads", &FastClient::ec_device_reads)
       .def_property_readonly("ec_host_fallbacks", &FastClient::ec_host_fallbacks)
+      .def("remove", [](FastClient& c, const std::string& path, const std::string& rid) {
+        std::string msg;
+        FastClient::Status st;
+        {
+          py::gil_scoped_release r;
+          st = c.remove(path, &msg, rid);
+        }
+        return py::make_tuple(static_cast<int>(st), msg);  // NotHandled: the caller's gRPC path
+      }, py::arg("path"), py::arg("request_id") = "")
       .def("bench_writes", &bench_writes<FastClient>, py::arg("paths"), py::arg("payloads"), py::arg("concurrency"))
       .def("bench_reads", &bench_reads_fast, py::arg("paths"), py::arg("expected"), py::arg("concurrency"));
 

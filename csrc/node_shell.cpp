@@ -1,4 +1,5 @@
 // Shared shell of the native control-plane executables (see node_shell.h).
+#include "trace.h"
 #include "node_shell.h"
 
 #include <execinfo.h>
@@ -304,6 +305,7 @@ void install_crash_handler() {
 
 void block_stop_signals() {
   install_crash_handler();
+  trace_init();  // before any thread: roctx's first range calls setenv (trace.h)
   sigset_t s;
   sigemptyset(&s);
   sigaddset(&s, SIGTERM);

@@ -43,6 +43,7 @@
 #include <thread>
 #include <vector>
 
+#include "trace.h"
 #include "client_remote.h"
 #include "crypto.h"
 #include "dfs_pb.h"
@@ -971,6 +972,7 @@ int run(Cli& cli, const Args& a, int argc, char** argv) {
 }  // namespace
 
 int main(int argc, char** argv) {
+  dfs::trace_init();  // before any thread: roctx's first range calls setenv (trace.h)
   Args a;
   try {
     a = parse(argc, argv);

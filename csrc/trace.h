@@ -30,6 +30,16 @@ class RequestScope {
   std::string saved_;
 };
 
+// roctx (and rocprofiler-register under it) calls setenv() while it initializes, on the
+// first range. glibc's getenv() is not safe against a concurrent setenv(): a chunkserver's
+// first ranges come from its worker threads while main still reads its environment, and one
+// CPU test run died with SIGSEGV inside getenv at startup. Every process therefore starts
+// roctx from main before it starts a thread (shell::block_stop_signals, the Python module).
+inline void trace_init() {
+  roctxRangePushA("dfs.init");
+  roctxRangePop();
+}
+
 class TraceRange {
  public:
   explicit TraceRange(const char* name) {

@@ -363,6 +363,13 @@ class Client:
         return self.get_file_info(path) is not None
 
     def delete_file(self, path: str) -> None:
+        fc = self._fast
+        if fc is not None:  # the same-host master socket, in C++ (csrc/client_fast.cpp)
+            st, msg = fc.remove(path)
+            if st == 0:
+                return
+            if st == 2:
+                raise DfsError(f"Failed to delete file: {msg}")
         resp, _ = self.execute_rpc(path, "DeleteFile", pb.DeleteFileRequest(path=path), self._not_leader_check)
         if not resp.success:
             raise DfsError(f"Failed to delete file: {resp.error_message}")

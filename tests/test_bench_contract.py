@@ -68,6 +68,19 @@ def test_bench_multi_rank_socket_transport(tmp_path, n):
     assert d["config"]["transport"] == "socket"
 
 
+def test_bench_reclaims_steps_when_the_volume_is_short(tmp_path, monkeypatch):
+    """A run whose replicas would not fit the volume deletes each step's files after reading
+    them (inside the timed region, reported), so the journals reclaim them as it goes."""
+    monkeypatch.setenv("DFS_BENCH_RECLAIM", "1")
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr", "127.0.0.1", "--master-port", "29699", "bench.py", "--gpus", "2",
+              "--steps", "2", "--warmup", "1", "--cpu", "--count", "10", "--transport", "socket",
+              "--remote-steps", "0"], tmp_path)
+    _check_common(d, 2, 2, 1)
+    assert d["volume"]["reclaim_between_steps"] is True
+    assert d["p2p_fallbacks"] == 0 and d["replica_failures"] == 0
+
+
 def test_bench_never_opens_the_gpu():
     """The ranks leave the device to their chunkservers: no torch.cuda / HIP call in bench.py
     (an N-rank node then has N GPU processes, not 2N), and the timed region is bracketed by
