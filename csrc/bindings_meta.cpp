@@ -469,6 +469,11 @@ void bind_meta(py::module_& m) {
       .def("set_blocked", [](raft::Node& n, const std::vector<std::string>& addrs) { n.host().set_blocked(addrs); })
       .def_property_readonly("wal_syncs", &raft::Node::wal_syncs)
       .def_property_readonly("wal_bytes", &raft::Node::wal_bytes);
+  m.def("raft_restore_snapshot_dir", [](const std::string& dir, const std::string& payload) {
+    std::string err;
+    const bool ok = raft::restore_snapshot_dir(dir, payload, &err);
+    return py::make_tuple(ok, err);
+  });
 
   // ---------------- native shard map (csrc/shard_map.cpp), for parity tests with parallel/sharding.py
   py::class_<ShardMap>(m, "NativeShardMap")

@@ -1300,4 +1300,40 @@ std::string Node::info_json() const {
   return o.dump();
 }
 
+bool restore_snapshot_dir(const std::string& dir, const std::string& payload, std::string* err) {
+  mkdirs(dir);
+  struct stat sb {};
+  if (::stat((dir + "/snapshot.json").c_str(), &sb) == 0) {
+    *err = dir + " already holds a snapshot";
+    return false;
+  }
+  if (::stat((dir + "/raft.wal").c_str(), &sb) == 0) {
+    Wal existing(dir + "/raft.wal", false);
+    if (!existing.replay().empty()) {
+      *err = dir + " already holds a Raft log";
+      return false;
+    }
+  }
+  Json snap;
+  try {
+    snap = Json::parse(payload);
+  } catch (const std::exception& e) {
+    *err = std::string("not a snapshot backup (JSON): ") + e.what();
+    return false;
+  }
+  if (!snap.is_object() || !snap["meta"].is_array() || snap["meta"].size() != 2 || !snap["meta"][0].is_int() ||
+      !snap["meta"][1].is_int() || !snap["state"].is_object()) {
+    *err = "not a snapshot backup: want {\"meta\":[index,term],\"state\":{...}}";
+    return false;
+  }
+  const uint64_t idx = snap["meta"][0].as_u64(), term = snap["meta"][1].as_u64();
+  atomic_write_file(dir + "/snapshot.json",
+                    "{\"meta\":[" + std::to_string(idx) + "," + std::to_string(term) + "],\"state\":" +
+                        snap["state"].dump() + ",\"config\":null}",
+                    true);
+  Wal w(dir + "/raft.wal", true);
+  w.append({"{\"k\":\"H\",\"term\":" + std::to_string(term) + ",\"vote\":null}"});
+  return true;
+}
+
 }  // namespace dfs::raft

@@ -300,4 +300,13 @@ class Node {
   bool started_ = false;
 };
 
+// Disaster recovery from an off-box snapshot backup (the bytes a leader PUT to
+// `{endpoint}/{bucket}/master-snapshots/node-{id}/...`, Options::backup_endpoint; the reference
+// is upload-only). Seeds an EMPTY node directory with the snapshot: its
+// state and (index, term) as the node's snapshot, the current term raised to the snapshot's
+// (so entries appended after it keep non-decreasing terms), and no membership, so the
+// restored node starts with the members it is given (--peers), not the backed-up cluster's.
+// Refuses a directory that already holds a snapshot or Raft log records.
+bool restore_snapshot_dir(const std::string& dir, const std::string& payload, std::string* err);
+
 }  // namespace dfs::raft

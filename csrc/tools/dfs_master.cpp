@@ -25,6 +25,7 @@
 #include <condition_variable>
 #include <deque>
 #include <cstdio>
+#include <fstream>
 #include <functional>
 #include <future>
 #include <map>
@@ -32,6 +33,7 @@
 #include <mutex>
 #include <random>
 #include <set>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1042,6 +1044,34 @@ int Master::run() {
   o.snapshot_threshold = static_cast<uint64_t>(a_.get_int("snapshot-threshold", 10000));
   o.backup_endpoint = a_.get("backup-s3-endpoint");
   o.backup_bucket = a_.get("backup-bucket", "dfs-backups");
+  if (!a_.get("restore-snapshot").empty()) {
+    // seed an empty storage dir from an off-box snapshot backup (a file, or the object's
+    // http(s) URL), then start as usual with this command line's members
+    const std::string src = a_.get("restore-snapshot");
+    std::string payload;
+    if (src.rfind("http://", 0) == 0 || src.rfind("https://", 0) == 0) {
+      const int st = http_request("GET", src, "", "", 60000, &payload, &err);
+      if (st != 200) {
+        std::fprintf(stderr, "dfs_master: restore: GET %s: %s\n", src.c_str(),
+                     err.empty() ? std::to_string(st).c_str() : err.c_str());
+        return 2;
+      }
+    } else {
+      std::ifstream f(src, std::ios::binary);
+      if (!f) {
+        std::fprintf(stderr, "dfs_master: restore: cannot read %s\n", src.c_str());
+        return 2;
+      }
+      std::stringstream ss;
+      ss << f.rdbuf();
+      payload = ss.str();
+    }
+    if (!raft::restore_snapshot_dir(o.dir, payload, &err)) {
+      std::fprintf(stderr, "dfs_master: restore: %s\n", err.c_str());
+      return 2;
+    }
+    log(kWarning, "dfs.master", "restored %s into %s", src.c_str(), o.dir.c_str());
+  }
   raft_host_ = std::make_shared<NativeRaftHost>(core_, tls ? client_tls : nullptr);
   node_ = std::make_unique<raft::Node>(o, raft_host_);
   core_->attach(node_.get());
@@ -1185,7 +1215,7 @@ const char* kUsage =
     "                  [--merge-threshold-rps MERGE_THRESHOLD_RPS] [--tls-cert TLS_CERT] [--tls-key TLS_KEY]\n"
     "                  [--ca-cert CA_CERT] [--domain-name DOMAIN_NAME] [--backup-s3-endpoint BACKUP_S3_ENDPOINT]\n"
     "                  [--backup-bucket BACKUP_BUCKET] [--snapshot-threshold SNAPSHOT_THRESHOLD] [--no-fsync]\n"
-    "                  [--fast-intervals] [--http-host HTTP_HOST]\n";
+    "                  [--fast-intervals] [--http-host HTTP_HOST] [--restore-snapshot FILE_OR_URL]\n";
 
 // The reference's defaults (bin/master.rs:21-80), printed by --help.
 const std::map<std::string, std::string> kDefaults = {

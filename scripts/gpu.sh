@@ -11,6 +11,7 @@
 #   n2        2 ranks sharing the GPU (hipipc, RF 2)
 #   n2hbm     the same with hbm-ack durability (the shared volume out of the ack path)
 #   n4        the driver's N=4 command on 4 ranks sharing the GPU
+#   reclaim   4 ranks deleting each step's files after the read-back (bench's short-volume mode)
 #   ipctest   the device-replication GPU tests only
 #   pullab    replica hops, receiver pull vs push (hbm-ack, conc 10 and 1)
 #   pullhost  2 ranks nvme-sync: pulled replicas appended from the kernel's host copy vs HBM vs push
@@ -82,6 +83,8 @@ for step in "$@"; do
     n2prof)   # rocprofv3 kernel + marker + memory-copy traces of both chunkservers, 2 ranks, conc 1
       DFS_PROF_EXTRA=--memory-copy-trace run n2prof 600 python bench.py --gpus 2 --steps 5 --warmup 1 \
         --durability hbm-ack --concurrency 1 --remote-steps 0 --profile-dir "$O/n2prof" || exit 1 ;;
+    reclaim)  # 4 ranks with each step's files deleted after the read-back (what a short volume triggers)
+      DFS_BENCH_RECLAIM=1 run n4_reclaim 900 python bench.py --gpus 4 --steps 10 --warmup 2 || exit 1 ;;
     n4)     # the driver's N=4 command, 4 ranks sharing the GPU
       run n4 900 python bench.py --gpus 4 --steps 5 --warmup 2 || exit 1 ;;
     prof)
