@@ -3,11 +3,13 @@
 covered there by the shared-GPU process tests (test_gpu_ipc.py) and on the CPU by the
 socket transport (test_replication.py).
 
-* hipipc between DISTINCT devices: every replica slice is a one-sided copy from the sender's
-  HBM into the peer GPU's arena over xGMI (hipIpcOpenMemHandle of a peer device's export,
-  then ipc_copy_kernel: the sender's waves load its extent and store into the peer's, 16 bytes
-  per lane, csrc/p2p_ipc.cpp + csrc/p2p_kernels.hip), crossing RF=3 traffic at conc 10 with
-  blocks up to 64 MiB, checked byte for byte and .meta for .meta on every replica;
+* hipipc between DISTINCT devices: every replica slice crosses xGMI in one kernel on the
+  receiver (receiver pull, round 6: hipIpcOpenMemHandle of the sender's export, then the
+  receiver's crc_write_copy_kernel loads the sender's extent over xGMI, stores it into its
+  own arena and writes the slice CRCs; csrc/p2p_ipc.cpp + csrc/gpu_kernels.hip; with
+  DFS_IPC_PULL=0 the sender's ipc_copy_kernel stores into the peer instead), crossing RF=3
+  traffic at conc 10 with blocks up to 64 MiB, checked byte for byte and .meta for .meta on
+  every replica;
 * a replica killed mid-transfer: the write still succeeds with fewer replicas (reference
   chunkserver.rs:777-829,1039-1077: replicas_written, downstream failure = success), no hang;
 * RCCL between two GPUs: csrc/p2p_rccl.cpp's real open() of the per-pair 2-rank
