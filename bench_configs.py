@@ -101,17 +101,43 @@ def _topology(c, gpus, shared: bool) -> str:
     return f"{c.n_cs} chunkservers ({where}), RF {min(3, c.n_cs)}"
 
 
+def _settle_journals(c, limit_s: float = 120.0) -> float:
+    """Wait until no chunkserver's journal has a part a writer could be handed unwritten."""
+    import urllib.request
+
+    t0 = time.time()
+    while time.time() - t0 < limit_s:
+        unready = 0
+        for u in c.cs_http:
+            try:
+                st = json.load(urllib.request.urlopen(f"{u}/stats", timeout=10))
+            except OSError:
+                unready += 1
+                continue
+            unready += int(st.get("journal_parts_unready", 0)) + int(st.get("journal_spares_missing", 0))
+        if unready == 0:
+            break
+        time.sleep(0.2)
+    return time.time() - t0
+
+
 # ----------------------------------------------------------------------------- config 3
 def config3(a):
     """BASELINE config 3: 3 chunkservers, replication factor 3 (the pipeline over the device
     transport), the benchmark's 1 MiB x 100 at concurrency 10 from one client, nvme-sync and
     hbm-ack. On a 1-GPU box the 3 chunkservers share the GPU (labelled)."""
     out = {"config": 3, "files": a.count, "size": a.size, "concurrency": a.concurrency, "steps": a.steps, "runs": []}
+    # like bench.py: every chunkserver holds every block (RF 3 on 3), so each journal gets the
+    # run's spare segments created and written out before the timed steps, not on demand
+    # under the acked writes (which put 150 ms stalls into the write tail)
+    need = (a.steps + 1) * a.count * (a.size + a.size // 128 + 4096)
+    env = {"DFS_JOURNAL_SPARES": str(-(-need // int((256 << 20) * 0.96)) + 2)}
     for durability in ("nvme-sync", "hbm-ack"):
         gpus, shared = _cs_gpus(a, 3)
         progress(f"config 3: 3 chunkservers, {durability}")
-        with LocalCluster(n_chunkservers=3, gpus=gpus, durability=durability,
+        with LocalCluster(n_chunkservers=3, gpus=gpus, durability=durability, env=env,
                           hbm_capacity="16G" if gpus else "0", p2p="hipipc" if gpus else "socket") as c:
+            _settle_journals(c)
             cl = c.client()
             payloads = make_payloads(a.count, a.size)
             ws, names = bench_write(cl, a.count, a.size, a.concurrency, prefix="/bench_write/w", payloads=payloads)
