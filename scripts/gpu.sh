@@ -75,6 +75,14 @@ for step in "$@"; do
       run n2_pull_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack --concurrency 1 && \
       DFS_IPC_PULL=0 run n2_push_c1 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack \
         --concurrency 1 || exit 1 ;;
+    pullrep)  # receiver pull vs push at 2 ranks, interleaved, 3 reps each, nvme-sync then hbm-ack
+      for i in 1 2 3; do
+        run n2pull_nv_$i 600 python bench.py --gpus 2 --steps 10 --warmup 2 && \
+        DFS_IPC_PULL=0 run n2push_nv_$i 600 python bench.py --gpus 2 --steps 10 --warmup 2 && \
+        run n2pull_hbm_$i 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack && \
+        DFS_IPC_PULL=0 run n2push_hbm_$i 600 python bench.py --gpus 2 --steps 10 --warmup 2 --durability hbm-ack \
+          || exit 1
+      done ;;
     pullhost) # 2 ranks nvme-sync: pulled replicas appended from the kernel's host copy / from HBM / push
       DFS_PULL_HOST=1 run n2_pullhost 600 python bench.py --gpus 2 --steps 10 --warmup 2 && \
       run n2_pulldev 600 python bench.py --gpus 2 --steps 10 --warmup 2 && \
