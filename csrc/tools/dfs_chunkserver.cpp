@@ -359,10 +359,14 @@ int main(int argc, char** argv) {
       merge_into(&d, stats_json(engine->stats()), "repl_");
       d.set("repl_channels", engine->channels());
       d.set("repl_transport", engine->transport_name());
-      int up = 0;
+      int up = 0, pulls = 0;
       for (int r = 0; r < engine->world(); ++r)
-        if (r != engine->rank() && engine->pair_ok(r)) ++up;
+        if (r != engine->rank() && engine->pair_ok(r)) {
+          ++up;
+          if (engine->transport()->pulls_from(r)) ++pulls;  // hipipc receiver pull from that peer
+        }
       d.set("repl_pairs_up", up);
+      d.set("repl_pull_peers", pulls);
     }
     d.set("native_chunkserver", true);
     // CPU milliseconds by thread name (live threads): what the process spends its cores on

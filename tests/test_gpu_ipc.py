@@ -71,7 +71,8 @@ def totals(c: LocalCluster):
     for u in c.cs_http:
         s = stats(u)
         for k in ("fp_rccl_forwards", "fp_p2p_fallbacks", "fp_replica_failures", "fp_shm_forwards",
-                  "repl_pair_failures", "repl_turn_timeouts", "repl_bytes_recv", "grpc_forwards", "pulled_recvs"):
+                  "repl_pair_failures", "repl_turn_timeouts", "repl_bytes_recv", "grpc_forwards", "pulled_recvs",
+                  "repl_pull_peers"):
             agg[k] = agg.get(k, 0) + s.get(k, 0)
         agg.setdefault("transports", set()).add(s.get("repl_transport"))
         agg.setdefault("pairs_up", 0)
@@ -104,4 +105,5 @@ def test_four_processes_one_gpu_crossing_traffic(mode):
         # every replica of the pull mode came through the receivers' copy+checksum kernels
         pulled = t["pulled_recvs"] - base["pulled_recvs"]
         assert pulled == (writes * 2 if mode == "hipipc" else 0), t
+        assert t["repl_pull_peers"] == (12 if mode == "hipipc" else 0), t
         assert elapsed < 120

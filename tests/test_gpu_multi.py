@@ -104,6 +104,11 @@ def test_hipipc_distinct_devices_crossing_rf3():
         t = totals(c)
         assert t["fp_rccl_forwards"] - base["fp_rccl_forwards"] == 36 * 2, t
         assert t["fp_p2p_fallbacks"] == 0 and t["fp_replica_failures"] == 0 and t["fp_shm_forwards"] == 0, t
+        # where the devices reach each other's memory every receive was pulled over xGMI by the
+        # receiver's copy+checksum kernel (one kernel per hop)
+        if t["repl_pull_peers"] == 6:
+            assert t["pulled_recvs"] - base["pulled_recvs"] == 36 * 2, t
+        print(f"\ndistinct devices: pull peers {t['repl_pull_peers']} of 6, pulled {t['pulled_recvs']}")
         assert elapsed < 120
         # every replica's chunkserver (one per GPU) holds <id> + <id>.meta in the reference format
         cl = c.client(local_chunkserver=c.cs_addrs[0])
