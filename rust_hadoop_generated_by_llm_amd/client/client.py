@@ -25,7 +25,6 @@ from concurrent.futures import FIRST_COMPLETED, ThreadPoolExecutor, wait
 import grpc
 
 from ..models import proto as pb
-from ..ops import crc as crcops
 from ..ops import erasure
 from ..parallel.sharding import ShardMap
 from ..utils.rpc import ChannelPool, current_request_id, rpc_code, rpc_details, strip_scheme, with_scheme
@@ -479,7 +478,7 @@ class Client:
         # by CompleteFile: start it first so it overlaps the create RPC, the CRC and the
         # block transfer (hashlib and the native CRC both release the GIL).
         md5_fut = self._exec.submit(lambda: etag or hashlib.md5(data).hexdigest())
-        crc = crcops.crc32(data)  # PCLMUL, ~50 us/MiB: cheaper inline than a pool hand-off
+        crc = _native.crc32(data)  # PCLMUL, ~50 us/MiB: cheaper inline than a pool hand-off
         t = self._phase("crc", t)
         alloc = self._create_and_allocate(dest)
         t = self._phase("create", t)
@@ -570,7 +569,7 @@ class Client:
         bid = alloc.block.block_id
 
         def put(i):
-            req = pb.WriteBlockRequest(block_id=bid, data=shards[i], expected_checksum_crc32c=crcops.crc32(shards[i]),
+            req = pb.WriteBlockRequest(block_id=bid, data=shards[i], expected_checksum_crc32c=_native.crc32(shards[i]),
                                        shard_index=i, master_term=alloc.master_term)
             r = self.pool.call(self._cs(servers[i]), "ChunkServerService", "WriteBlock", req, timeout=self.data_timeout)
             if not r.success:
@@ -578,7 +577,7 @@ class Client:
 
         for f in [self._exec.submit(put, i) for i in range(k + m)]:
             f.result()
-        self._complete(dest, len(data), "", [pb.BlockChecksumInfo(block_id=bid, checksum_crc32c=crcops.crc32(data),
+        self._complete(dest, len(data), "", [pb.BlockChecksumInfo(block_id=bid, checksum_crc32c=_native.crc32(data),
                                                                   actual_size=len(data))], alloc)
 
     # ------------------------------------------------------------------ read path
