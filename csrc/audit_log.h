@@ -7,7 +7,7 @@
 // timestamps, previous_hash -> record_hash = HMAC-SHA256(secret, JSON with record_hash =
 // null), the chain head recovered from the newest stored record, 3 write attempts with
 // 0.5 s * n backoff, hourly retention). The store is the segment directory of
-// s3/audit.py (seg-<hour_ms>.log lines "<key_ts>\t<canonical json>", plus .uidx / .ridx
+// tests/models/s3_audit.py (seg-<hour_ms>.log lines "<key_ts>\t<canonical json>", plus .uidx / .ridx
 // index lines "<key>\t<offset>\t<length>" appended after the bytes they point at), so the
 // Python reader, the native audit_reader and this writer share it byte for byte.
 //

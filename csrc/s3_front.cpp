@@ -463,7 +463,7 @@ bool parse_layout(const std::string& lay, std::vector<std::pair<uint64_t, uint64
 }
 
 // A small XML reader for request bodies (DeleteObjects): elements by local name (namespace
-// prefix dropped, as s3/xml.py's _local does), each with ElementTree's .text (character data
+// prefix dropped, as tests/models/s3_xml.py's _local does), each with ElementTree's .text (character data
 // before the first child). False for anything outside this subset — comments, CDATA, DTDs,
 // unknown entities, mismatched tags: Python's ElementTree decides those.
 struct XNode {
@@ -1891,7 +1891,7 @@ bool S3Front::native_get(Conn* c, Req& r, const std::string& path, bool head) {
 
 namespace {
 
-// ET.fromstring + _children/_text of s3/xml.py for a CompleteMultipartUpload body, namespace
+// ET.fromstring + _children/_text of tests/models/s3_xml.py for a CompleteMultipartUpload body, namespace
 // agnostic: the (PartNumber, ETag) of every <Part> child of the root. False for anything
 // this small scanner does not model (DTDs, CDATA, malformed XML): Python parses those.
 bool parse_complete_body(const std::string& b, std::vector<std::pair<int64_t, std::string>>* parts) {
@@ -2370,7 +2370,7 @@ bool S3Front::respond(Conn* c, Req& r, int status, const std::string& xml, const
   return send_head_body(c->io(), h, reinterpret_cast<const uint8_t*>(xml.data()), xml.size());
 }
 
-// X.error of s3/xml.py
+// X.error of tests/models/s3_xml.py
 bool S3Front::s3_error(Conn* c, Req& r, int status, const std::string& code, const std::string& msg,
                        const std::string& resource) {
   return respond(c, r, status,

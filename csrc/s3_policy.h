@@ -1,5 +1,5 @@
 // IAM role policies and S3 bucket policies (C13-C14), native twin of
-// rust_hadoop_generated_by_llm_amd/s3/auth/policy.py. Reference: dfs/s3_server/src/auth/
+// tests/models/s3_policy.py. Reference: dfs/s3_server/src/auth/
 // policy.rs:64-200 (wildcards, IamConfig roles, statements with Condition) and
 // auth/bucket_policy.rs (Principal "*" | "<arn glob>" | {"AWS": str|[str]}; Allow /
 // ExplicitDeny / NotApplicable), and auth_middleware.rs:400-493 (method/path/query ->

@@ -1,6 +1,6 @@
 // STS AssumeRoleWithWebIdentity for the native S3 gateway (C15 OIDC, C16 STS tokens, C55 the
 // endpoint; reference dfs/s3_server/src/sts_handler.rs:65-395, common/src/auth/oidc.rs:33-120,
-// auth/sts.rs:60-98). The same token format and validation rules as s3/auth/identity.py, so a
+// auth/sts.rs:60-98). The same token format and validation rules as tests/models/s3_identity.py, so a
 // session issued by either gateway opens in the other:
 //   * OIDC: <issuer>/.well-known/openid-configuration -> jwks_uri -> JWKS (cached, refetched
 //     when a kid is unknown); RS256 (RSA JWKs) always, HS256 ("oct" JWKs) only when allowed;

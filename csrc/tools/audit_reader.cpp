@@ -1,6 +1,6 @@
 // audit_reader — read, filter and verify the S3 gateway's audit log (C59; reference
-// dfs/s3_server/src/bin/audit_reader.rs). Native twin of rust_hadoop_generated_by_llm_amd/s3/
-// audit.py::reader_main over the same segment store (seg-<hour_ms>.log with one
+// dfs/s3_server/src/bin/audit_reader.rs). Checked against the Python model tests/models/
+// s3_audit.py::reader_main over the same segment store (seg-<hour_ms>.log with one
 // "<key_ts>\t<canonical json>" line per record, seg-<h>.uidx / .ridx index lines
 // "<user|bucket>\t<offset>\t<length>"), with the same flags and output:
 //

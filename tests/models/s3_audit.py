@@ -38,7 +38,7 @@ import threading
 import time
 from datetime import datetime, timezone
 
-from ..utils.metrics import Counter, Registry
+from rust_hadoop_generated_by_llm_amd.utils.metrics import Counter, Registry
 
 log = logging.getLogger("dfs.s3.audit")
 
@@ -379,7 +379,7 @@ class NativeAuditLogger:
     def __init__(self, path: str, retention_days: int = 30, batch_size: int = 100, hmac_secret: str = "",
                  *, registry: Registry | None = None, flush_interval: float = 5.0, capacity: int = 10_000,
                  sync: bool = False):
-        from ..native import lib
+        from rust_hadoop_generated_by_llm_amd.native import lib
 
         self.store = SegmentStore(path)
         self._n = lib.AuditLog(path, retention_days, batch_size, hmac_secret, capacity,

@@ -59,13 +59,13 @@ from aiohttp import web
 from rust_hadoop_generated_by_llm_amd.client.client import Client, DfsError
 from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
 from rust_hadoop_generated_by_llm_amd.utils.metrics import Registry
-from rust_hadoop_generated_by_llm_amd.s3 import xml as X
-from rust_hadoop_generated_by_llm_amd.s3.audit import AuditLogger, make_record
+from tests.models import s3_xml as X
+from tests.models.s3_audit import AuditLogger, make_record
 from rust_hadoop_generated_by_llm_amd.s3.auth import sigv4
 from rust_hadoop_generated_by_llm_amd.s3.auth.errors import AuthError
-from rust_hadoop_generated_by_llm_amd.s3.auth.identity import (EnvCredentialProvider, OidcValidator, SseManager, StsSessionData, StsTokenManager,
+from tests.models.s3_identity import (EnvCredentialProvider, OidcValidator, SseManager, StsSessionData, StsTokenManager,
                             parse_sse_master_key, random_alnum)
-from rust_hadoop_generated_by_llm_amd.s3.auth.policy import BucketPolicy, PolicyEvaluator, PolicyResult, resolve_action_and_resource
+from tests.models.s3_policy import BucketPolicy, PolicyEvaluator, PolicyResult, resolve_action_and_resource
 
 log = logging.getLogger("dfs.s3")
 

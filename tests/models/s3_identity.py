@@ -27,9 +27,9 @@ import time
 import urllib.request
 from dataclasses import dataclass, field
 
-from ...native import lib
-from .errors import AuthError
-from .policy import EvaluationContext
+from rust_hadoop_generated_by_llm_amd.native import lib
+from rust_hadoop_generated_by_llm_amd.s3.auth.errors import AuthError
+from tests.models.s3_policy import EvaluationContext
 
 
 # ---------------------------------------------------------------------------- credentials

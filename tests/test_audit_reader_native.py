@@ -1,5 +1,5 @@
 """build/native/audit_reader (csrc/tools/audit_reader.cpp) against the Python reader
-(s3/audit.py::reader_main, reference dfs/s3_server/src/bin/audit_reader.rs) on the same
+(tests/models/s3_audit.py::reader_main, reference dfs/s3_server/src/bin/audit_reader.rs) on the same
 segment store: identical output for every filter combination, index lookups with a lagging
 index, chain verification with the right and a wrong secret, and tamper detection."""
 import json
@@ -9,7 +9,7 @@ from pathlib import Path
 
 import pytest
 
-from rust_hadoop_generated_by_llm_amd.s3.audit import AuditLogger, SegmentStore, make_record, reader_main
+from tests.models.s3_audit import AuditLogger, SegmentStore, make_record, reader_main
 
 ROOT = Path(__file__).resolve().parents[1]
 READER = ROOT / "build" / "native" / "audit_reader"
@@ -106,7 +106,7 @@ def test_native_writer_matches_python_writer(tmp_path):
     segments and index files for the same records and batch boundaries: same sort, same
     monotonic keys, same canonical JSON (non-ASCII, control characters, nulls), same HMAC
     chain, continued across a restart."""
-    from rust_hadoop_generated_by_llm_amd.s3.audit import NativeAuditLogger, PyAuditLogger, verify_chain
+    from tests.models.s3_audit import NativeAuditLogger, PyAuditLogger, verify_chain
 
     base = datetime(2026, 5, 2, 23, 58, tzinfo=timezone.utc)
     users = ["alice", "Zoë", None, "tab\tuser", "nl\nuser"]
@@ -147,7 +147,7 @@ def test_native_writer_ingest_and_drops(tmp_path):
     (never blocks) and counts it."""
     import socket
 
-    from rust_hadoop_generated_by_llm_amd.s3.audit import NativeAuditLogger
+    from tests.models.s3_audit import NativeAuditLogger
 
     lg = NativeAuditLogger(str(tmp_path / "a"), batch_size=1000, hmac_secret=SECRET, flush_interval=60,
                            capacity=8)

@@ -14,15 +14,15 @@ from datetime import datetime, timedelta, timezone
 
 import pytest
 
-from rust_hadoop_generated_by_llm_amd.s3 import xml as X
-from rust_hadoop_generated_by_llm_amd.s3.audit import (AuditLogger, SegmentStore, compute_hmac, make_record,
+from tests.models import s3_xml as X
+from tests.models.s3_audit import (AuditLogger, SegmentStore, compute_hmac, make_record,
                                                       reader_main, verify_chain)
 from rust_hadoop_generated_by_llm_amd.s3.auth import sigv4 as s
 from rust_hadoop_generated_by_llm_amd.s3.auth.errors import AuthError
-from rust_hadoop_generated_by_llm_amd.s3.auth.identity import (Claims, EnvCredentialProvider, OidcValidator,
+from tests.models.s3_identity import (Claims, EnvCredentialProvider, OidcValidator,
                                                               SseManager, StsSessionData, StsTokenManager,
                                                               make_hs256_jwt, parse_sse_master_key, random_alnum)
-from rust_hadoop_generated_by_llm_amd.s3.auth.policy import (BucketPolicy, EvaluationContext, PolicyEvaluator,
+from tests.models.s3_policy import (BucketPolicy, EvaluationContext, PolicyEvaluator,
                                                             PolicyResult, matches_wildcard,
                                                             resolve_action_and_resource)
 from tests.models.s3_gateway import parse_range

@@ -26,8 +26,8 @@ import requests
 from aiohttp import web
 
 from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster, free_port
-from rust_hadoop_generated_by_llm_amd.s3 import xml as X
-from rust_hadoop_generated_by_llm_amd.s3.audit import SegmentStore, verify_chain
+from tests.models import s3_xml as X
+from tests.models.s3_audit import SegmentStore, verify_chain
 from rust_hadoop_generated_by_llm_amd.s3.auth import sigv4
 from tests.models.s3_gateway import S3Config, build_gateway
 

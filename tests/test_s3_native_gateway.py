@@ -15,7 +15,7 @@ import pytest
 import requests
 
 from rust_hadoop_generated_by_llm_amd.cluster.launcher import ROOT, LocalCluster
-from rust_hadoop_generated_by_llm_amd.s3.audit import SegmentStore, verify_chain
+from tests.models.s3_audit import SegmentStore, verify_chain
 
 from .test_s3_gateway import (  # noqa: F401  (scenarios and fixtures re-collected here)
     AUDIT_SECRET, IAM_CONFIG, assume, creds_of, jwt, md5q, oidc_issuer, signed,

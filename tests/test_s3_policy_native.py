@@ -1,5 +1,5 @@
 """The native IAM / bucket policy engine (csrc/s3_policy.cpp, used by the native S3 front)
-against the Python engine (s3/auth/policy.py; reference auth/policy.rs, auth/bucket_policy.rs,
+against the Python engine (tests/models/s3_policy.py; reference auth/policy.rs, auth/bucket_policy.rs,
 auth_middleware.rs:400-493) on randomized documents, principals, actions and resources."""
 import json
 import random
@@ -7,7 +7,7 @@ import random
 import pytest
 
 from rust_hadoop_generated_by_llm_amd import native as N
-from rust_hadoop_generated_by_llm_amd.s3.auth.policy import (BucketPolicy, EvaluationContext, PolicyEvaluator,
+from tests.models.s3_policy import (BucketPolicy, EvaluationContext, PolicyEvaluator,
                                                              matches_wildcard, resolve_action_and_resource)
 
 lib = N.lib
