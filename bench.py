@@ -248,7 +248,7 @@ def main():
         procs = Procs()
         done = threading.Event()
         extra_dirs: list = []
-        limit = min(a.timeout, 420.0) if alt else a.timeout
+        limit = min(a.timeout, 240.0) if alt else a.timeout  # the A/B phase: 10 steps, never the driver's budget
 
         def watchdog():
             if not done.wait(limit):
