@@ -276,6 +276,7 @@ ChunkStore::ChunkStore(StoreConfig cfg) : cfg_(std::move(cfg)) {
     jc.reserve_bytes = static_cast<uint64_t>(env_int("DFS_JOURNAL_RESERVE_MB", 0)) << 20;
     if (jc.reserve_bytes == 0) jc.reserve_bytes = std::max<uint64_t>(2ull << 30, vol_total / 50);
     jc.direct = env_int("DFS_JOURNAL_DIRECT", 0) != 0;
+    jc.early_wb_bytes = static_cast<uint64_t>(env_int("DFS_JOURNAL_EARLY_WB_KB", 0)) << 10;
     jc.spares = env_int("DFS_JOURNAL_SPARES", store_mode_ ? 4 : 2);
     jc.spares_low = env_int("DFS_JOURNAL_SPARES_LOW", 2);
     jc.zero_fill = env_int("DFS_JOURNAL_ZERO_FILL", 1) != 0;

@@ -776,7 +776,19 @@ bool BlockJournal::write(const JournalRec& r, uint64_t at, const uint8_t* p, uin
     if (full && !pwrite_all(part->dfd, p, full, off)) return false;
     return full == len || pwrite_all(part->fd, p + full, len - full, off + full);
   }
-  return pwrite_all(part->fd, p, len, off);
+  if (!cfg_.sync || cfg_.early_wb_bytes == 0 || len <= cfg_.early_wb_bytes)
+    return pwrite_all(part->fd, p, len, off);
+  // pieces end on multiples of early_wb_bytes (page-aligned), so a page handed to writeback is
+  // never written again by the next piece
+  const uint64_t piece = align_up(cfg_.early_wb_bytes, kPage);
+  for (uint64_t o = off, e = off + len; o < e;) {
+    const uint64_t next = std::min(e, (o / piece + 1) * piece);
+    if (!pwrite_all(part->fd, p + (o - off), next - o, o)) return false;
+    // only starts the write-out (no wait); the commit's fdatasync still makes it durable
+    (void)::sync_file_range(part->fd, static_cast<off_t>(o), static_cast<off_t>(next - o), SYNC_FILE_RANGE_WRITE);
+    o = next;
+  }
+  return true;
 }
 
 bool BlockJournal::finish(JournalRec* r, const std::string& id, uint64_t n, uint32_t crc, const uint8_t* meta_be,

@@ -68,6 +68,12 @@ struct JournalConfig {
   int parts = 8;                    // files a segment is striped over
   bool direct = false;              // O_DIRECT appends (aligned sources only; else buffered)
   bool sync = true;                 // fdatasync on commit (false: tests / --no-fsync)
+  // Early writeback: a buffered append is written in pieces of this many bytes (page-aligned
+  // file offsets), each handed to writeback at once (sync_file_range WRITE), so the device
+  // is already writing the record's first pieces while the rest are copied and the header is
+  // formed; the commit's fdatasync then waits for less. 0 = off (one pwrite, writeback
+  // starts at the fdatasync).
+  uint64_t early_wb_bytes = 0;
   // Segment files are created (fallocate) ahead of use by a background thread. With zero_fill
   // that thread also writes the free ones out once while the writers are idle (no append for
   // a few ms), so an append overwrites written extents and its flush carries no
