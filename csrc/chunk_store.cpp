@@ -2444,6 +2444,7 @@ std::vector<std::string> ChunkStore::scrub_resident(const std::vector<std::strin
 
 std::vector<std::string> ChunkStore::scrub() {
   std::vector<std::string> bad;
+  size_t hbm_bad = 0;  // bad[0, hbm_bad): HBM copies; the rest: durable copies
   std::vector<std::string> resident, disk;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -2458,6 +2459,7 @@ std::vector<std::string> ChunkStore::scrub() {
   }
   if (!resident.empty()) {
     for (auto& id : scrub_resident(resident)) bad.push_back(id);
+    hbm_bad = bad.size();
     for (auto& id : resident) unpin(id);
   }
   // durable copies (journal records, files): the non-resident blocks, and the resident
@@ -2480,9 +2482,19 @@ std::vector<std::string> ChunkStore::scrub() {
   }
   for (auto& id : cpu)
     if (!verify_on_disk(id).empty() && std::find(bad.begin(), bad.end(), id) == bad.end()) bad.push_back(id);
+  // a durable copy can change under the scan (exported to its files, relocated, rewritten by
+  // a recovery): a durable-copy mismatch is reported only if the copy the index names now
+  // fails again, so a scan racing those moves does not queue recoveries of healthy blocks
+  std::vector<std::string> confirmed;
+  uint64_t transient = 0;
+  for (size_t i = 0; i < bad.size(); ++i) {
+    if (i < hbm_bad || !verify_on_disk(bad[i]).empty()) confirmed.push_back(bad[i]);
+    else ++transient;
+  }
   std::lock_guard<std::mutex> g(mu_);
-  st_.crc_mismatches += bad.size();
-  return bad;
+  st_.crc_mismatches += confirmed.size();
+  st_.scrub_transient += transient;
+  return confirmed;
 }
 
 std::vector<std::string> ChunkStore::list_blocks() {

@@ -85,6 +85,7 @@ struct StoreStats {
   uint64_t evictions = 0;
   uint64_t promotions = 0;
   uint64_t crc_mismatches = 0;
+  uint64_t scrub_transient = 0;  // durable-copy mismatches a re-check of the current copy did not confirm
   uint64_t gpu_kernel_launches = 0;
   uint64_t disk_gate_waits = 0;  // durable writes that queued for a node-wide disk slot
   uint64_t direct_dma = 0;       // host<->HBM copies done straight from registered memory

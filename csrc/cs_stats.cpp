@@ -30,6 +30,7 @@ Json stats_json(const StoreStats& t) {
   d.set("final_name_writes", t.final_name_writes);
   d.set("direct_writes", t.direct_writes);
   d.set("crc_mismatches", t.crc_mismatches);
+  d.set("scrub_transient", t.scrub_transient);
   d.set("gpu_kernel_launches", t.gpu_kernel_launches);
   d.set("disk_gate_waits", t.disk_gate_waits);
   d.set("direct_dma", t.direct_dma);

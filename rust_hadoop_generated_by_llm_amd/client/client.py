@@ -115,6 +115,15 @@ class Client:
                                                 ca_cert=ca_cert or "", domain_name=domain_name or "")
             if hedge_delay_ms:
                 self._remote.set_hedge_delay(int(hedge_delay_ms))
+        # a co-located client's second native path: what the shared-memory client declines (its
+        # shard's first master is a follower, the chain head is on another host) goes to the
+        # native gRPC client, which follows the masters' leader hints, before the Python path
+        self._remote_alt = None
+        if (self._fast is not None and os.environ.get("DFS_NATIVE_REMOTE", "1") == "1"):
+            self._remote_alt = _native.RemoteClient(2, int(data_timeout * 1000), tls=self.tls,
+                                                    ca_cert=ca_cert or "", domain_name=domain_name or "")
+            if hedge_delay_ms:
+                self._remote_alt.set_hedge_delay(int(hedge_delay_ms))
         self.remote_ops = 0
         # other native objects that route by this client's shard map and masters (the S3
         # front's RemoteFrontStore); kept in step by _sync_fast
@@ -184,8 +193,9 @@ class Client:
 
     def with_hedge_delay(self, delay_ms: int) -> "Client":
         self.hedge_delay_ms = delay_ms
-        if self._remote is not None:
-            self._remote.set_hedge_delay(int(delay_ms or 0))  # hedging runs in the native client too
+        for nc in (self._remote, self._remote_alt):
+            if nc is not None:
+                nc.set_hedge_delay(int(delay_ms or 0))  # hedging runs in the native client too
         return self
 
     def set_shard_map(self, m: ShardMap) -> None:
@@ -199,7 +209,8 @@ class Client:
         self._sync_fast()
 
     def _sync_fast(self) -> None:
-        for nc in (self._fast, getattr(self, "_remote", None), *getattr(self, "_routed_extra", [])):
+        for nc in (self._fast, getattr(self, "_remote", None), getattr(self, "_remote_alt", None),
+                   *getattr(self, "_routed_extra", [])):
             if nc is not None:
                 with self._map_lock:
                     js = json.dumps(self.shard_map.to_json()) if self.shard_map.shards else ""
@@ -208,7 +219,7 @@ class Client:
     def add_host_alias(self, alias: str, real: str) -> None:
         self.host_aliases[alias] = real
         # the native clients dial through the same alias table (first match, like resolve_url)
-        for nc in (self._fast, self._remote):
+        for nc in (self._fast, self._remote, self._remote_alt):
             if nc is not None:
                 nc.set_host_aliases(list(self.host_aliases.items()))
         self._sync_fast()
@@ -222,6 +233,7 @@ class Client:
     def close(self) -> None:
         self._fast = None  # unmaps and unlinks the native client's shared-memory arena
         self._remote = None
+        self._remote_alt = None
         self.pool.close()
         self._exec.shutdown(wait=False)
         if self._arena is not None:
@@ -469,7 +481,14 @@ class Client:
                 return replicas
             if st == 2:
                 raise DfsError(msg)
-            # not handled natively (remote master/head, redirect, not leader): Python path
+            if fc is self._fast and self._remote_alt is not None:
+                st, replicas, msg, times = self._remote_alt.write(dest, data, current_request_id.get(), attributes or {})
+                if st == 0:
+                    self.remote_ops += 1
+                    return replicas
+                if st == 2:
+                    raise DfsError(msg)
+            # not handled natively (shard redirect, no leader reachable): Python path
             self._fallback("write_not_handled")
         else:
             self._fallback("write_no_native_client")
@@ -699,6 +718,13 @@ class Client:
                 return data
             if st == 2:
                 raise DfsError(msg)
+            if fc is self._fast and self._remote_alt is not None:
+                st, data, msg, _times = self._remote_alt.read(path, current_request_id.get())
+                if st == 0:
+                    self.remote_ops += 1
+                    return data
+                if st == 2:
+                    raise DfsError(msg)
             self._fallback("read_not_handled")
         else:
             self._fallback("read_no_native_client")
@@ -744,6 +770,13 @@ class Client:
                 return data
             if st == 2:
                 raise DfsError(msg)
+            if fc is self._fast and self._remote_alt is not None:
+                st, data, msg, _times = self._remote_alt.read(path, current_request_id.get(), offset, length)
+                if st == 0:
+                    self.remote_ops += 1
+                    return data
+                if st == 2:
+                    raise DfsError(msg)
             self._fallback("range_not_handled")
         else:
             self._fallback("range_no_native_client")

@@ -19,10 +19,11 @@ import pytest
 
 from rust_hadoop_generated_by_llm_amd.cli import dfs_cli
 from rust_hadoop_generated_by_llm_amd.client import checker
-from rust_hadoop_generated_by_llm_amd.client.client import DfsError
+from rust_hadoop_generated_by_llm_amd.client.client import Client, DfsError
 from rust_hadoop_generated_by_llm_amd.client.workload import run_workload
 from rust_hadoop_generated_by_llm_amd.cluster.launcher import LocalCluster
 from rust_hadoop_generated_by_llm_amd.models import proto as pb
+from rust_hadoop_generated_by_llm_amd.parallel.sharding import ShardMap
 from rust_hadoop_generated_by_llm_amd.utils.rpc import ChannelPool, strip_scheme
 
 pytestmark = pytest.mark.slow
@@ -265,6 +266,39 @@ def test_master_raft_failover():
         assert c.get_file_content("/raft/before") == b"before"
         assert c.get_file_content("/raft/after") == b"after"
         pool.close()
+        c.close()
+
+
+def test_colocated_client_follows_the_leader_natively():
+    """The shared-memory client asks its shard's first master, which here is a follower: it
+    declines, and the co-located client's native gRPC client (csrc/client_remote.cpp) follows
+    the leader hint, so writes, reads and range reads stay native (no Python fallback)."""
+    with LocalCluster(n_chunkservers=1, masters_per_shard=3, fsync=False) as cl:
+        pool = ChannelPool()
+        leader = None
+        deadline = time.time() + 30
+        while leader is None and time.time() < deadline:
+            for m in cl.master_addrs:
+                try:
+                    if pool.call(m, "MasterService", "GetClusterInfo", pb.GetClusterInfoRequest()).role == "Leader":
+                        leader = m
+                except grpc.RpcError:
+                    pass
+            time.sleep(0.1)
+        pool.close()
+        assert leader is not None
+        followers = [m for m in cl.master_addrs if m != leader]
+        c = Client(followers + [leader], local_chunkserver=cl.cs_addrs[0])
+        c.set_shard_map(ShardMap.from_config({k: followers + [leader] for k in cl.shard_masters}))
+        assert c._fast is not None and c._remote_alt is not None
+        blobs = {f"/lead/f{i}": os.urandom(100_000 + i) for i in range(3)}
+        for p, d in blobs.items():
+            c.create_file_from_buffer(d, p)
+        for p, d in blobs.items():
+            assert c.get_file_content(p) == d
+        assert c.read_file_range("/lead/f1", 777, 4000) == blobs["/lead/f1"][777:4777]
+        assert c.native_fallbacks == {}, c.native_fallbacks
+        assert c.remote_ops == 7
         c.close()
 
 
