@@ -141,10 +141,27 @@ bool RemoteClient::call_candidates(std::vector<std::string> cands, const std::st
                                    const std::string& req, const std::string& rid, int* code, std::string* resp) {
   const std::string full = "/dfs.MasterService/" + method;
   *code = -1;
+  bool redirected = false;
   for (size_t i = 0; i < cands.size() && i < 8; ++i) {
     GrpcResult r = pool_.call(cands[i], full, req, rid);
     if (!r.transport_ok) continue;
     std::string hint;
+    // "REDIRECT:<addr>": this master's shard does not own the path (our shard map is stale,
+    // e.g. after a split); the owner's address is the next candidate. Its answer is not
+    // cached as this shard's leader.
+    static const std::string kRedirect = "REDIRECT:";
+    if (r.status == kOutOfRange && r.message.compare(0, kRedirect.size(), kRedirect) == 0 &&
+        r.message.size() > kRedirect.size()) {
+      hint = r.message.substr(kRedirect.size());
+      if (hint.find("://") == std::string::npos) {
+        const size_t sch = cands[i].find("://");
+        if (sch != std::string::npos) hint = cands[i].substr(0, sch + 3) + hint;
+      }
+      if (std::find(cands.begin() + static_cast<long>(i) + 1, cands.end(), hint) == cands.end())
+        cands.insert(cands.begin() + static_cast<long>(i) + 1, hint);
+      redirected = true;
+      continue;
+    }
     bool follower = r.status == kFailedPrecondition && not_leader(r.message, &hint);
     if (!follower && r.status == 0 && (method == "CreateFile" || method == "DeleteFile" || method == "Rename")) {
       // these answer a follower's refusal in the response: fields 1 success, 2 error_message,
@@ -164,7 +181,7 @@ bool RemoteClient::call_candidates(std::vector<std::string> cands, const std::st
         cands.insert(cands.begin() + static_cast<long>(i) + 1, hint);
       continue;
     }
-    {
+    if (!redirected) {
       std::lock_guard<std::mutex> g(route_mu_);
       leader_[shard] = cands[i];
     }

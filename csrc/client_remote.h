@@ -6,9 +6,9 @@
 //          -> WriteBlock(data, next_servers) to the chain head -> CompleteFile{create}
 //   read:  GetFileInfo -> ReadBlock from the first location that answers
 //
-// Leader changes are followed (Not Leader hints, then the shard's other peers). Anything
-// else it does not own — shard redirects, EC or multi-block files — returns NotHandled
-// and the Python client takes over, so semantics never change. It is what makes the
+// Leader changes are followed (Not Leader hints, then the shard's other peers), and so are
+// REDIRECT:<owner> answers to a stale shard map. Anything else it does not own (multi-block
+// files) returns NotHandled and the Python client takes over, so semantics never change. It is what makes the
 // "remote client" numbers of bench.py a native client against native servers, like the
 // reference's Rust dfs_cli against its Rust servers.
 #pragma once

@@ -44,9 +44,17 @@ def _ensure_built() -> None:
                 # tests' business (tests/test_native_unit.py builds them on demand)
                 saved = os.environ.get("DFS_BUILD_SANITIZERS")
                 os.environ["DFS_BUILD_SANITIZERS"] = "0"
+                # the build's output goes to stderr, whoever prints it (this process or the
+                # compilers it starts): stdout may be a contract, e.g. bench.py's one JSON line
+                sys.stdout.flush()
+                out_fd = os.dup(1)
+                os.dup2(2, 1)
                 try:
                     build_native.build()
                 finally:
+                    sys.stdout.flush()
+                    os.dup2(out_fd, 1)
+                    os.close(out_fd)
                     if saved is None:
                         os.environ.pop("DFS_BUILD_SANITIZERS", None)
                     else:

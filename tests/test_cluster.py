@@ -241,6 +241,30 @@ def test_cross_shard_rename_and_listing():
         assert _master_metric_sum(cl, "dfs_master_tx_declined") == 0
 
 
+def test_native_client_follows_shard_redirects():
+    """A client whose shard map is stale (every path routed to one shard): the other shard's
+    paths are answered REDIRECT:<owner> by that master, and the native gRPC client
+    (csrc/client_remote.cpp) follows the hint, so the ops stay native (no Python fallback)."""
+    with LocalCluster(n_chunkservers=1, shards=2, fsync=False) as cl:
+        good = cl.client()
+        owner = good.shard_map.get_shard("/z/x")
+        other = next(k for k in cl.shard_masters if k != owner)
+        good.close()
+        c = Client(cl.master_addrs)
+        c.set_shard_map(ShardMap.from_config({other: cl.shard_masters[other]}))
+        assert c._remote is not None and c._fast is None
+        assert c.shard_map.get_shard("/z/x") == other  # stale: the owner is another shard
+        blobs = {f"/z/redir{i}": os.urandom(50_000 + i) for i in range(3)}
+        for p, d in blobs.items():
+            c.create_file_from_buffer(d, p)
+        for p, d in blobs.items():
+            assert c.get_file_content(p) == d
+        assert c.read_file_range("/z/redir2", 100, 900) == blobs["/z/redir2"][100:1000]
+        assert c.native_fallbacks == {}, c.native_fallbacks
+        assert c.remote_ops == 7
+        c.close()
+
+
 def test_master_raft_failover():
     with LocalCluster(n_chunkservers=3, masters_per_shard=3, fsync=False) as cl:
         c = cl.client(initial_backoff_ms=100, max_retries=10)
