@@ -3,6 +3,7 @@
 #   head     this tree
 #   oldgrow  this tree with the journal topping up spares under load (round 5's behaviour)
 #   r4       the round-4 tree (git worktree at 435766d in ab_r4/, built in place)
+#   r5       the round-5 tree (git worktree at 6116051 in ab_r5/, built in place)
 #   name:VAR=v[,VAR2=w]  this tree with those environment variables
 # Every run is under its own time limit; the first failure ends the session.
 set -o pipefail
@@ -19,6 +20,8 @@ for i in $(seq 1 "$REPS"); do
       oldgrow) (DFS_JOURNAL_SPARES_LOW=1000 timeout -k 10 300 python bench.py --steps 20 --warmup 5 \
                   > "$O/${v}_$i.json" 2> "$O/${v}_$i.err") ;;
       r4)      (cd ab_r4 && timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "../$O/${v}_$i.json" \
+                  2> "../$O/${v}_$i.err") ;;
+      r5)      (cd ab_r5 && timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "../$O/${v}_$i.json" \
                   2> "../$O/${v}_$i.err") ;;
       *:*)     (name=${v%%:*}; envs=${v#*:}; env ${envs//,/ } timeout -k 10 300 python bench.py --steps 20 --warmup 5 \
                   > "$O/${v%%:*}_$i.json" 2> "$O/${v%%:*}_$i.err") ;;
